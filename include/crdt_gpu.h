@@ -1,0 +1,173 @@
+/*
+ * crdt_gpu.h — C ABI of the MI355X batched CvRDT merge engine (libcrdt_gpu.so).
+ *
+ * Drop-in boundary for the `crdts` 3.0.0 (rust-crdt) state-merge path.  The reference
+ * exposes one merge per pair of states:
+ *
+ *     CvRDT::merge(&mut self, other: Self)                      traits.rs:4-7
+ *     FunkyCvRDT::merge(&mut self, other) -> Result<(), Error>  traits.rs:49-55 (LWWReg)
+ *
+ * and users fold it over replicas (`acc.merge(r)` loops, test/orswot.rs:50-53,
+ * pncounter.rs:151-154).  This library adds the batched forms a `gpu` module of the
+ * crate binds through `extern "C"` (see INTEGRATION.md for the Rust / ctypes stubs):
+ *
+ *     *_lub_many    — G independent left folds, each over R replicas  (acc = T::new(); for r: acc.merge(r))
+ *     *_merge_batch — N independent pairwise merges, self[i].merge(other[i]), in place
+ *
+ * States are dense structure-of-arrays in device memory (HBM): actors/members are interned
+ * to dense indices by the caller, an absent actor is a 0 counter (exact: VClock::apply_dot
+ * never stores 0, vclock.rs:155-159).  All pointers are DEVICE pointers unless stated.
+ * Every stride is in 64-bit words.  Results are bit-exact against the reference fold.
+ *
+ * Conventions
+ *   - Return value: CRDT_OK (0) or a negative status; crdt_last_error() has the text.
+ *     No C++ exception crosses this ABI.  LWW marker conflicts are DATA, not a status.
+ *   - Calls are stream-ordered on the ctx's stream and asynchronous unless stated.
+ *     The caller owns every buffer; the library keeps no pointer past return.
+ *   - One ctx per host thread; a ctx is bound to one device.
+ */
+#ifndef CRDT_GPU_H
+#define CRDT_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ------------------------------------------------------------------ */
+#define CRDT_OK 0
+#define CRDT_EINVAL -1       /* bad argument (null pointer, zero dim, stride < width, ...) */
+#define CRDT_EHIP -2         /* a HIP runtime call failed                                   */
+#define CRDT_ENOMEM -3       /* device scratch allocation failed                            */
+#define CRDT_EUNSUPPORTED -4 /* shape the kernels do not handle                             */
+
+/* ---- flags for *_lub_many ---------------------------------------------------------- */
+/* out := out ⊔ fold(in) instead of out := fold(in): i.e. `self.merge(r)` for every r,
+ * starting from the caller's current state rather than from T::new(). */
+#define CRDT_ACCUMULATE 0x1u
+
+typedef struct crdt_ctx crdt_ctx;
+
+/* ---- context ------------------------------------------------------------------------- */
+/* Create a ctx bound to HIP device `device` (>= 0).  Scratch is owned by the ctx. */
+int crdt_ctx_create(int device, crdt_ctx **out);
+int crdt_ctx_destroy(crdt_ctx *ctx);
+/* Launch on `hip_stream` (a hipStream_t; NULL = the device's null stream). */
+int crdt_ctx_set_stream(crdt_ctx *ctx, void *hip_stream);
+/* Block until all work issued through ctx has finished. */
+int crdt_ctx_synchronize(crdt_ctx *ctx);
+/* Text of the last failure on this ctx (static storage owned by ctx). ctx may be NULL. */
+const char *crdt_last_error(const crdt_ctx *ctx);
+/* Library version, e.g. "0.1.0"; and the gfx target the code objects were built for. */
+const char *crdt_version(void);
+const char *crdt_build_target(void);
+
+/* Per-kernel timing with HIP events recorded on the ctx stream around the DOMINANT kernel of
+ * each call (the replica stream pass).  Enabling costs two event records per call. */
+int crdt_ctx_set_timing(crdt_ctx *ctx, int enable);
+/* Sum of elapsed ms and launch count for kernel class `name` ("lub_stream", "orswot_join",
+ * "lww_reduce", ...) since the last reset.  Synchronises the ctx stream. */
+int crdt_ctx_timing(crdt_ctx *ctx, const char *name, double *total_ms, uint64_t *launches);
+int crdt_ctx_timing_reset(crdt_ctx *ctx);
+
+/* ---- VClock / GCounter: elementwise-max lub ----------------------------------------------
+ * Replaces VClock::merge (vclock.rs:130-136, via apply_dot :155-159) and GCounter::merge
+ * (gcounter.rs:44-48) folded over replicas.
+ * Replica (g, r) row = in + g*group_stride + r*row_stride, A counters contiguous.
+ * Output row g = out + g*out_stride.                                                    */
+int crdt_vclock_lub_many(crdt_ctx *ctx, const uint64_t *in, size_t G, size_t R, size_t A,
+                         size_t row_stride, size_t group_stride, uint64_t *out,
+                         size_t out_stride, unsigned flags);
+/* self[i] := self[i] ⊔ other[i] for i < N (rows of A counters). */
+int crdt_vclock_merge_batch(crdt_ctx *ctx, uint64_t *self, const uint64_t *other, size_t N,
+                            size_t A, size_t self_stride, size_t other_stride);
+int crdt_gcounter_lub_many(crdt_ctx *ctx, const uint64_t *in, size_t G, size_t R, size_t A,
+                           size_t row_stride, size_t group_stride, uint64_t *out,
+                           size_t out_stride, unsigned flags);
+int crdt_gcounter_merge_batch(crdt_ctx *ctx, uint64_t *self, const uint64_t *other, size_t N,
+                              size_t A, size_t self_stride, size_t other_stride);
+
+/* ---- PNCounter: dual max ---------------------------------------------------------------
+ * Replaces PNCounter::merge (pncounter.rs:70-75).  A replica row holds 2*A words:
+ * P counters in [0, A), N counters in [A, 2A).  Strides as for VClock (row_stride >= 2A). */
+int crdt_pncounter_lub_many(crdt_ctx *ctx, const uint64_t *in, size_t G, size_t R, size_t A,
+                            size_t row_stride, size_t group_stride, uint64_t *out,
+                            size_t out_stride, unsigned flags);
+int crdt_pncounter_merge_batch(crdt_ctx *ctx, uint64_t *self, const uint64_t *other,
+                               size_t N, size_t A, size_t self_stride, size_t other_stride);
+
+/* ---- GSet: bitmap union ----------------------------------------------------------------
+ * Replaces GSet::merge (gset.rs:38-40 → insert :69-71).  Elements are interned to bit
+ * positions; a replica row is `words` u64 words (bit u of word u/64 = element u present). */
+int crdt_gset_lub_many(crdt_ctx *ctx, const uint64_t *in, size_t G, size_t R, size_t words,
+                       size_t row_stride, size_t group_stride, uint64_t *out,
+                       size_t out_stride, unsigned flags);
+int crdt_gset_merge_batch(crdt_ctx *ctx, uint64_t *self, const uint64_t *other, size_t N,
+                          size_t words, size_t self_stride, size_t other_stride);
+
+/* ---- LWWReg<u64 val, u64 marker> -------------------------------------------------------
+ * Replaces FunkyCvRDT::merge for LWWReg (lwwreg.rs:43-45 → update :84-98).
+ * lub_many folds group g as acc = replica[g][0]; for r in 1..R: acc.merge(replica[g][r]),
+ * where an erroring merge leaves acc unchanged (exactly what update does on Err).
+ * Outputs: out_marker[g], out_val[g] = the folded state (max marker, val of the FIRST
+ * replica holding it); first_conflict[g] = index r of the first merge that returns
+ * Err(ConflictingMarker) in that fold, or UINT64_MAX if none.  Any of the three outputs
+ * may be NULL.  Inputs: marker/val at [g*group_stride + r]. */
+int crdt_lwwreg_lub_many(crdt_ctx *ctx, const uint64_t *marker, const uint64_t *val, size_t G,
+                         size_t R, size_t group_stride, uint64_t *out_marker,
+                         uint64_t *out_val, uint64_t *first_conflict);
+/* self[i].merge(other[i]) for i < N; conflict[i] = 1 where it returns Err (state then
+ * unchanged), else 0.  conflict may be NULL. */
+int crdt_lwwreg_merge_batch(crdt_ctx *ctx, uint64_t *self_marker, uint64_t *self_val,
+                            const uint64_t *other_marker, const uint64_t *other_val,
+                            size_t N, uint8_t *conflict);
+
+/* ---- Orswot<member, actor> ---------------------------------------------------------------
+ * Replaces Orswot::merge (orswot.rs:81-149) incl. apply_rm (:230-250) and apply_deferred
+ * (:281-286).  Dense layout per replica (g, r):
+ *   clock   C[g][r][a]      at clock   + g*clock_gstride + r*clock_rstride + a
+ *   entries E[g][r][m][a]   at entries + g*entry_gstride + r*entry_rstride + m*entry_mstride + a
+ *                            (E = the member's dot clock; member absent <=> row all 0)
+ *   deferred removes, pooled per group (CSR): group g owns d in [def_off[g], def_off[g+1]);
+ *     rm clock  def_clock[d*A + a], member set bitmap def_members[d*Mw + w], Mw = ceil(M/64).
+ *     def_off is a HOST array of G+1 entries.
+ * Output per group g: out_clock[g*A + a], out_entries[g*M*A + m*A + a] (packed), and for the
+ * deferred pool: out_def_keep[d] = 1 iff d is the representative of a surviving deferred
+ * remove (¬(rm ≤ final clock), first of its group with that exact clock), and
+ * out_def_members[d*Mw + w] = union of the member sets of every surviving deferred of the
+ * group with the same clock (only meaningful where out_def_keep[d] = 1). */
+typedef struct crdt_orswot_batch {
+  size_t G, R, M, A;
+  const uint64_t *clock;
+  size_t clock_rstride, clock_gstride;
+  const uint64_t *entries;
+  size_t entry_mstride, entry_rstride, entry_gstride;
+  const size_t *def_off; /* host, G+1 entries; NULL or all-zero = no deferred removes */
+  const uint64_t *def_clock;
+  const uint64_t *def_members;
+} crdt_orswot_batch;
+
+typedef struct crdt_orswot_out {
+  uint64_t *clock;       /* [G][A]    */
+  uint64_t *entries;     /* [G][M][A] */
+  uint8_t *def_keep;     /* [D]       */
+  uint64_t *def_members; /* [D][Mw]   */
+} crdt_orswot_out;
+
+int crdt_orswot_lub_many(crdt_ctx *ctx, const crdt_orswot_batch *in, crdt_orswot_out *out);
+
+/* ---- synthetic inputs (bench / test data, generated in HBM) --------------------------------
+ * Counter-based and reproducible on the CPU (tests/golden/make_golden.py restates them).
+ * kind 0 = clock/counter cells, 1 = GSet bitmap words, 2 = LWW markers, 3 = LWW vals.
+ * Row r < rows of the output is row (first_row + r) of the global synthetic matrix: cell
+ * (first_row + r, i) gets synth(seed, (first_row + r)*width + i), stored at out[r*row_stride + i].
+ * (first_row lets every rank generate its own replica shard of one global input.) */
+int crdt_synth_fill(crdt_ctx *ctx, uint64_t *out, size_t rows, size_t width, size_t row_stride,
+                    size_t first_row, uint64_t seed, int kind);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CRDT_GPU_H */

@@ -1,0 +1,338 @@
+// ORACLE — test infrastructure only.  Not part of the product and never linked into it.
+//
+// A CPU restatement of the reference `crdts` 3.0.0 merge paths (rust-crdt; the Rust crate
+// cannot be built here: no cargo/rustc, see DESIGN.md "Oracle").  The containers mirror the
+// reference's: VClock = ordered map actor -> counter (BTreeMap, vclock.rs:56-60), Orswot
+// entries = hash map member -> VClock, deferred = map VClock -> member set (orswot.rs:20-25).
+// Every function follows the cited reference lines statement by statement.  It is pinned by
+// the reference's own known-answer tests (tests/golden/kat_*.json via oracle/oracle.py, whose
+// pure-Python twin is cross-checked against this file) and is used by tests/ as the parity
+// checker and by bench.py as the `cpu_baseline` (kind "port").
+//
+// Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg load this library.
+#include <chrono>
+#include <cstdint>
+#include <cstring>
+#include <map>
+#include <set>
+#include <unordered_map>
+#include <vector>
+
+namespace oracle {
+
+using Actor = uint32_t;
+using Member = uint32_t;
+using u64 = uint64_t;
+
+// ---- VClock (vclock.rs) ---------------------------------------------------------------
+struct VClock {
+  std::map<Actor, u64> dots;  // vclock.rs:59
+
+  u64 get(Actor a) const {  // vclock.rs:207-209
+    auto it = dots.find(a);
+    return it == dots.end() ? 0 : it->second;
+  }
+  void apply_dot(Actor a, u64 counter) {  // vclock.rs:155-159
+    if (get(a) < counter) dots[a] = counter;
+  }
+  void merge(VClock &&other) {  // vclock.rs:130-136 (consumes other)
+    for (auto &kv : other.dots) apply_dot(kv.first, kv.second);
+    other.dots.clear();
+  }
+  void forget(const VClock &other) {  // vclock.rs:95-105
+    for (auto &kv : other.dots)
+      if (kv.second >= get(kv.first)) dots.erase(kv.first);
+  }
+  bool empty() const { return dots.empty(); }
+  bool operator==(const VClock &o) const { return dots == o.dots; }
+  bool operator<(const VClock &o) const { return dots < o.dots; }  // map key only
+  // partial_cmp (vclock.rs:68-80): 0 Equal, 1 Greater, -1 Less, 2 None
+  int partial_cmp(const VClock &other) const {
+    if (*this == other) return 0;
+    bool ge = true;
+    for (auto &kv : other.dots)
+      if (!(get(kv.first) >= kv.second)) { ge = false; break; }
+    if (ge) return 1;
+    bool le = true;
+    for (auto &kv : dots)
+      if (!(other.get(kv.first) >= kv.second)) { le = false; break; }
+    if (le) return -1;
+    return 2;
+  }
+  // self >= other  <=>  partial_cmp(self, other) in {Greater, Equal}
+  bool geq(const VClock &other) const {
+    int c = partial_cmp(other);
+    return c == 0 || c == 1;
+  }
+  static VClock intersection(const VClock &left, const VClock &right) {  // vclock.rs:218-227
+    VClock out;
+    for (auto &kv : left.dots)
+      if (right.get(kv.first) == kv.second) out.dots.insert(kv);
+    return out;
+  }
+  VClock clone_without(const VClock &base) const {  // vclock.rs:148-152
+    VClock c = *this;
+    c.forget(base);
+    return c;
+  }
+};
+
+static VClock vclock_from_row(const u64 *row, size_t A) {
+  VClock v;
+  for (size_t a = 0; a < A; ++a)
+    if (row[a]) v.dots.emplace_hint(v.dots.end(), (Actor)a, row[a]);
+  return v;
+}
+static void vclock_to_row(const VClock &v, u64 *row, size_t A) {
+  std::memset(row, 0, A * 8);
+  for (auto &kv : v.dots) row[kv.first] = kv.second;
+}
+
+// ---- LWWReg (lwwreg.rs) --------------------------------------------------------------
+struct LWWReg {
+  u64 val, marker;
+  int update(u64 v, u64 m) {  // lwwreg.rs:84-98; returns 1 on Err(ConflictingMarker)
+    if (marker < m) {
+      val = v;
+      marker = m;
+      return 0;
+    } else if (marker == m && v != val) {
+      return 1;
+    }
+    return 0;
+  }
+};
+
+// ---- Orswot (orswot.rs) --------------------------------------------------------------
+struct Orswot {
+  VClock clock;                                   // orswot.rs:22
+  std::unordered_map<Member, VClock> entries;     // orswot.rs:23
+  std::map<VClock, std::set<Member>> deferred;    // orswot.rs:24 (keyed by whole clock)
+
+  void apply_rm(std::set<Member> members, VClock clock_rm) {  // orswot.rs:230-250
+    for (Member m : members) {
+      auto it = entries.find(m);
+      if (it != entries.end()) {
+        it->second.forget(clock_rm);
+        if (it->second.empty()) entries.erase(it);
+      }
+    }
+    int c = clock_rm.partial_cmp(clock);
+    if (c == 2 /*None*/ || c == 1 /*Greater*/) {
+      auto it = deferred.find(clock_rm);
+      if (it != deferred.end()) it->second.insert(members.begin(), members.end());
+      else deferred.emplace(std::move(clock_rm), std::move(members));
+    }
+  }
+  void apply_deferred() {  // orswot.rs:281-286
+    auto d = std::move(deferred);
+    deferred.clear();
+    for (auto &kv : d) apply_rm(kv.second, kv.first);
+  }
+  void merge(Orswot &&other) {  // orswot.rs:81-149
+    // :84-106 rebuild self.entries
+    std::unordered_map<Member, VClock> kept;
+    kept.reserve(entries.size());
+    for (auto &kv : entries) {
+      if (other.entries.find(kv.first) == other.entries.end()) {
+        if (other.clock.geq(kv.second)) {
+          // other has seen this entry and dropped it
+        } else {
+          VClock c = std::move(kv.second);
+          c.forget(other.clock);
+          kept.emplace(kv.first, std::move(c));
+        }
+      } else {
+        kept.emplace(kv.first, std::move(kv.second));
+      }
+    }
+    entries = std::move(kept);
+    // :108-138
+    for (auto &kv : other.entries) {
+      auto it = entries.find(kv.first);
+      if (it != entries.end()) {
+        VClock common = VClock::intersection(kv.second, it->second);
+        common.merge(kv.second.clone_without(clock));
+        common.merge(it->second.clone_without(other.clock));
+        if (common.empty()) entries.erase(it);
+        else it->second = std::move(common);
+      } else {
+        if (clock.geq(kv.second)) {
+          // we've seen this entry and dropped it
+        } else {
+          VClock c = std::move(kv.second);
+          c.forget(clock);
+          entries.emplace(kv.first, std::move(c));
+        }
+      }
+    }
+    // :141-143 merge deferred removals
+    for (auto &kv : other.deferred) apply_rm(kv.second, kv.first);
+    // :145
+    clock.merge(std::move(other.clock));
+    // :147
+    apply_deferred();
+  }
+};
+
+}  // namespace oracle
+
+using namespace oracle;
+
+static double now_s() {
+  using namespace std::chrono;
+  return duration<double>(steady_clock::now().time_since_epoch()).count();
+}
+
+extern "C" {
+
+// ---- VClock / GCounter / PNCounter ----------------------------------------------------
+// Left fold from VClock::new() over R dense rows (W counters each); returns fold seconds
+// (ingest into maps is outside the timed region, as the reference receives map states).
+double oracle_vclock_fold(const uint64_t *rows, size_t R, size_t W, size_t stride,
+                          uint64_t *out) {
+  std::vector<VClock> reps;
+  reps.reserve(R);
+  for (size_t r = 0; r < R; ++r) reps.push_back(vclock_from_row(rows + r * stride, W));
+  double t0 = now_s();
+  VClock acc;
+  for (auto &r : reps) acc.merge(std::move(r));  // GCounter::merge gcounter.rs:44-48
+  double t1 = now_s();
+  vclock_to_row(acc, out, W);
+  return t1 - t0;
+}
+
+// PNCounter rows hold P in [0,A) and N in [A,2A) (pncounter.rs:70-75 merges p then n).
+double oracle_pncounter_fold(const uint64_t *rows, size_t R, size_t A, size_t stride,
+                             uint64_t *out) {
+  std::vector<std::pair<VClock, VClock>> reps;
+  reps.reserve(R);
+  for (size_t r = 0; r < R; ++r)
+    reps.emplace_back(vclock_from_row(rows + r * stride, A), vclock_from_row(rows + r * stride + A, A));
+  double t0 = now_s();
+  VClock p, n;
+  for (auto &r : reps) {
+    p.merge(std::move(r.first));
+    n.merge(std::move(r.second));
+  }
+  double t1 = now_s();
+  vclock_to_row(p, out, A);
+  vclock_to_row(n, out + A, A);
+  return t1 - t0;
+}
+
+// Pairwise: self[i].merge(other[i]) on dense rows (A counters), in place.
+void oracle_vclock_merge_pairs(uint64_t *self, const uint64_t *other, size_t N, size_t A) {
+  for (size_t i = 0; i < N; ++i) {
+    VClock s = vclock_from_row(self + i * A, A);
+    s.merge(vclock_from_row(other + i * A, A));
+    vclock_to_row(s, self + i * A, A);
+  }
+}
+
+// VClock::forget (vclock.rs:95-105) and partial_cmp (vclock.rs:68-80) on dense rows.
+void oracle_vclock_forget(uint64_t *self, const uint64_t *other, size_t A) {
+  VClock s = vclock_from_row(self, A);
+  s.forget(vclock_from_row(other, A));
+  vclock_to_row(s, self, A);
+}
+int oracle_vclock_partial_cmp(const uint64_t *a, const uint64_t *b, size_t A) {
+  return vclock_from_row(a, A).partial_cmp(vclock_from_row(b, A));
+}
+
+// ---- GSet (gset.rs:38-40): union of ordered sets, dense bitmap in/out -------------------
+double oracle_gset_fold(const uint64_t *rows, size_t R, size_t words, size_t stride,
+                        uint64_t *out) {
+  std::vector<std::set<uint64_t>> reps(R);
+  for (size_t r = 0; r < R; ++r)
+    for (size_t w = 0; w < words; ++w) {
+      uint64_t x = rows[r * stride + w];
+      while (x) {
+        int b = __builtin_ctzll(x);
+        x &= x - 1;
+        reps[r].insert(w * 64 + b);
+      }
+    }
+  double t0 = now_s();
+  std::set<uint64_t> acc;
+  for (auto &s : reps)
+    for (uint64_t e : s) acc.insert(e);  // other.value.into_iter().for_each(insert)
+  double t1 = now_s();
+  std::memset(out, 0, words * 8);
+  for (uint64_t e : acc) out[e / 64] |= 1ull << (e % 64);
+  return t1 - t0;
+}
+
+// ---- LWWReg fold: acc = r[0]; acc.merge(r[i]) ignoring (but recording) Err ------------------
+double oracle_lwwreg_fold(const uint64_t *marker, const uint64_t *val, size_t R,
+                          uint64_t *out_marker, uint64_t *out_val, uint64_t *first_conflict) {
+  double t0 = now_s();
+  LWWReg acc{val[0], marker[0]};
+  uint64_t first = ~0ull;
+  for (size_t i = 1; i < R; ++i)
+    if (acc.update(val[i], marker[i]) && first == ~0ull) first = i;
+  double t1 = now_s();
+  *out_marker = acc.marker;
+  *out_val = acc.val;
+  *first_conflict = first;
+  return t1 - t0;
+}
+
+// ---- Orswot fold from Orswot::new() over R dense replicas ----------------------------------
+// Replica r: clock[r*A + a], entries[r*M*A + m*A + a]; deferred of replica r are
+// d in [def_off[r], def_off[r+1]) with rm clock def_clock[d*A..] and member bitmap
+// def_members[d*Mw..].  Output: out_clock[A], out_entries[M*A]; surviving deferred removes
+// are written as out_def_clock[k*A..], out_def_members[k*Mw..] for k < *out_ndef (caller
+// provides room for max_def).  Returns fold seconds (ingest excluded).
+double oracle_orswot_fold(const uint64_t *clock, const uint64_t *entries, size_t R, size_t M,
+                          size_t A, const uint64_t *def_off, const uint64_t *def_clock,
+                          const uint64_t *def_members, uint64_t *out_clock, uint64_t *out_entries,
+                          uint64_t *out_def_clock, uint64_t *out_def_members, size_t max_def,
+                          size_t *out_ndef) {
+  const size_t Mw = (M + 63) / 64;
+  std::vector<Orswot> reps(R);
+  for (size_t r = 0; r < R; ++r) {
+    Orswot &o = reps[r];
+    o.clock = vclock_from_row(clock + r * A, A);
+    for (size_t m = 0; m < M; ++m) {
+      VClock e = vclock_from_row(entries + (r * M + m) * A, A);
+      if (!e.empty()) o.entries.emplace((Member)m, std::move(e));
+    }
+    if (def_off)
+      for (uint64_t d = def_off[r]; d < def_off[r + 1]; ++d) {
+        VClock rm = vclock_from_row(def_clock + d * A, A);
+        std::set<Member> mem;
+        for (size_t w = 0; w < Mw; ++w) {
+          uint64_t x = def_members[d * Mw + w];
+          while (x) {
+            int b = __builtin_ctzll(x);
+            x &= x - 1;
+            mem.insert((Member)(w * 64 + b));
+          }
+        }
+        auto it = o.deferred.find(rm);
+        if (it != o.deferred.end()) it->second.insert(mem.begin(), mem.end());
+        else o.deferred.emplace(std::move(rm), std::move(mem));
+      }
+  }
+  double t0 = now_s();
+  Orswot acc;
+  for (auto &r : reps) acc.merge(std::move(r));
+  double t1 = now_s();
+  vclock_to_row(acc.clock, out_clock, A);
+  std::memset(out_entries, 0, M * A * 8);
+  for (auto &kv : acc.entries) vclock_to_row(kv.second, out_entries + (size_t)kv.first * A, A);
+  size_t k = 0;
+  for (auto &kv : acc.deferred) {
+    if (k < max_def) {
+      vclock_to_row(kv.first, out_def_clock + k * A, A);
+      std::memset(out_def_members + k * Mw, 0, Mw * 8);
+      for (Member m : kv.second) out_def_members[k * Mw + m / 64] |= 1ull << (m % 64);
+    }
+    ++k;
+  }
+  *out_ndef = k;
+  return t1 - t0;
+}
+
+}  // extern "C"

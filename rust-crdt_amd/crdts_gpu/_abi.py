@@ -1,0 +1,112 @@
+"""ctypes binding of libcrdt_gpu.so (include/crdt_gpu.h).
+
+This is the only way the package reaches the kernels.  There is no CPU fallback: if the
+library is missing or no HIP device is visible, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # rust-crdt_amd/
+LIB_PATH = os.environ.get("CRDT_GPU_LIB", os.path.join(PKG_ROOT, "libcrdt_gpu.so"))
+
+CRDT_OK = 0
+CRDT_EINVAL = -1
+CRDT_EHIP = -2
+CRDT_ENOMEM = -3
+CRDT_EUNSUPPORTED = -4
+CRDT_ACCUMULATE = 0x1
+
+# Every symbol declared in include/crdt_gpu.h (checked by tests/test_abi.py).
+EXPORTS = (
+    "crdt_ctx_create", "crdt_ctx_destroy", "crdt_ctx_set_stream", "crdt_ctx_synchronize",
+    "crdt_last_error", "crdt_version", "crdt_build_target", "crdt_ctx_set_timing",
+    "crdt_ctx_timing", "crdt_ctx_timing_reset",
+    "crdt_vclock_lub_many", "crdt_vclock_merge_batch",
+    "crdt_gcounter_lub_many", "crdt_gcounter_merge_batch",
+    "crdt_pncounter_lub_many", "crdt_pncounter_merge_batch",
+    "crdt_gset_lub_many", "crdt_gset_merge_batch",
+    "crdt_lwwreg_lub_many", "crdt_lwwreg_merge_batch",
+    "crdt_orswot_lub_many", "crdt_synth_fill",
+)
+
+
+class CrdtGpuError(RuntimeError):
+    """A libcrdt_gpu call returned a negative status."""
+
+    def __init__(self, fn: str, code: int, msg: str):
+        super().__init__(f"{fn} -> {code}: {msg}")
+        self.code = code
+
+
+class CrdtGpuUnavailable(RuntimeError):
+    """libcrdt_gpu.so is not built (or not loadable): there is no CPU fallback."""
+
+
+P = ctypes.c_void_p
+S = ctypes.c_size_t
+U64 = ctypes.c_uint64
+
+
+class OrswotBatch(ctypes.Structure):
+    _fields_ = [
+        ("G", S), ("R", S), ("M", S), ("A", S),
+        ("clock", P), ("clock_rstride", S), ("clock_gstride", S),
+        ("entries", P), ("entry_mstride", S), ("entry_rstride", S), ("entry_gstride", S),
+        ("def_off", ctypes.POINTER(S)), ("def_clock", P), ("def_members", P),
+    ]
+
+
+class OrswotOut(ctypes.Structure):
+    _fields_ = [("clock", P), ("entries", P), ("def_keep", P), ("def_members", P)]
+
+
+_SIGS = {
+    "crdt_ctx_create": ([ctypes.c_int, ctypes.POINTER(P)], ctypes.c_int),
+    "crdt_ctx_destroy": ([P], ctypes.c_int),
+    "crdt_ctx_set_stream": ([P, P], ctypes.c_int),
+    "crdt_ctx_synchronize": ([P], ctypes.c_int),
+    "crdt_last_error": ([P], ctypes.c_char_p),
+    "crdt_version": ([], ctypes.c_char_p),
+    "crdt_build_target": ([], ctypes.c_char_p),
+    "crdt_ctx_set_timing": ([P, ctypes.c_int], ctypes.c_int),
+    "crdt_ctx_timing": ([P, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(U64)], ctypes.c_int),
+    "crdt_ctx_timing_reset": ([P], ctypes.c_int),
+    "crdt_synth_fill": ([P, P, S, S, S, S, U64, ctypes.c_int], ctypes.c_int),
+    "crdt_lwwreg_lub_many": ([P, P, P, S, S, S, P, P, P], ctypes.c_int),
+    "crdt_lwwreg_merge_batch": ([P, P, P, P, P, S, P], ctypes.c_int),
+    "crdt_orswot_lub_many": ([P, ctypes.POINTER(OrswotBatch), ctypes.POINTER(OrswotOut)], ctypes.c_int),
+}
+for _t in ("vclock", "gcounter", "pncounter", "gset"):
+    _SIGS[f"crdt_{_t}_lub_many"] = ([P, P, S, S, S, S, S, P, S, ctypes.c_uint], ctypes.c_int)
+    _SIGS[f"crdt_{_t}_merge_batch"] = ([P, P, P, S, S, S, S], ctypes.c_int)
+
+_lib = None
+
+
+def load():
+    """Load libcrdt_gpu.so (raises CrdtGpuUnavailable if it was never built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise CrdtGpuUnavailable(
+            f"{LIB_PATH} not found: build it with `make -C rust-crdt_amd` (or "
+            "`python -c 'import __graft_entry__ as g; g.build()'`). There is no CPU fallback.")
+    try:
+        lib = ctypes.CDLL(LIB_PATH)
+    except OSError as e:  # pragma: no cover - depends on the ROCm runtime being present
+        raise CrdtGpuUnavailable(f"cannot load {LIB_PATH}: {e}") from e
+    for name, (argtypes, restype) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argtypes
+        fn.restype = restype
+    _lib = lib
+    return lib
+
+
+def check(ctx_ptr, fn: str, rc: int) -> None:
+    if rc != CRDT_OK:
+        msg = load().crdt_last_error(ctx_ptr)
+        raise CrdtGpuError(fn, rc, (msg or b"").decode(errors="replace"))

@@ -1,0 +1,30 @@
+"""Batched `GCounter` merge (reference: src/gcounter.rs:44-48 — VClock merge on `inner`).
+
+Dense layout: (R, A) or (G, R, A) u64 counters, actor interned to a column.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from . import _lattice
+from .context import Context
+
+
+def lub_many(states: torch.Tensor, out: Optional[torch.Tensor] = None, accumulate: bool = False,
+             ctx: Optional[Context] = None) -> torch.Tensor:
+    return _lattice.lub_many("gcounter", ctx, states, out=out, accumulate=accumulate)
+
+
+def merge_batch(self_states: torch.Tensor, other_states: torch.Tensor,
+                ctx: Optional[Context] = None) -> torch.Tensor:
+    return _lattice.merge_batch("gcounter", ctx, self_states, other_states)
+
+
+def read(states: torch.Tensor) -> list:
+    """GCounter::read (gcounter.rs:70-72): exact (unbounded) sum per row, on the host."""
+    import numpy as np
+    a = states.detach().cpu().numpy().view(np.uint64)
+    rows = a.reshape(-1, a.shape[-1])
+    return [sum(int(x) for x in row) for row in rows]

@@ -1,0 +1,94 @@
+// Internal shared definitions for libcrdt_gpu (not part of the ABI).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "crdt_gpu.h"
+
+namespace crdt {
+
+using u64 = unsigned long long;
+using u64x2 = unsigned long long __attribute__((ext_vector_type(2)));
+
+// One wave is 64 lanes on gfx950; every block size below is a multiple of it.
+constexpr int kWave = 64;
+constexpr int kBlock = 256;
+
+struct KernelTimer {
+  double total_ms = 0.0;
+  uint64_t launches = 0;
+};
+
+struct PendingTiming {
+  std::string name;
+  hipEvent_t start, stop;
+};
+
+}  // namespace crdt
+
+struct crdt_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int cu_count = 256;
+  bool timing = false;
+  std::string last_error;
+  // Device scratch (grown on demand, never shrunk; freed in destroy).
+  void *scratch = nullptr;
+  size_t scratch_bytes = 0;
+  std::map<std::string, crdt::KernelTimer> timers;
+  std::vector<crdt::PendingTiming> pending;
+  std::vector<hipEvent_t> free_events;
+};
+
+namespace crdt {
+
+int fail(crdt_ctx *ctx, int code, const char *fmt, ...);
+int hip_fail(crdt_ctx *ctx, hipError_t e, const char *what);
+// Ensure ctx->scratch holds at least `bytes`; returns CRDT_OK or CRDT_ENOMEM.
+int ensure_scratch(crdt_ctx *ctx, size_t bytes);
+// Bracket the dominant kernel of a call with events when timing is on.
+void timing_begin(crdt_ctx *ctx, const char *name);
+void timing_end(crdt_ctx *ctx);
+
+// Max / OR join on u64 lanes.
+enum class Op : int { Max = 0, Or = 1 };
+
+template <Op OP>
+__device__ __forceinline__ u64 join(u64 a, u64 b) {
+  if constexpr (OP == Op::Max) return a > b ? a : b;
+  else return a | b;
+}
+template <Op OP>
+__device__ __forceinline__ u64x2 join2(u64x2 a, u64x2 b) {
+  u64x2 r;
+  r.x = join<OP>(a.x, b.x);
+  r.y = join<OP>(a.y, b.y);
+  return r;
+}
+
+// Host entry for the lattice (max / or) lub used by vclock, gcounter, pncounter and gset.
+int lattice_lub_many(crdt_ctx *ctx, Op op, const u64 *in, size_t G, size_t R, size_t W,
+                     size_t row_stride, size_t group_stride, u64 *out, size_t out_stride,
+                     unsigned flags);
+int lattice_merge_batch(crdt_ctx *ctx, Op op, u64 *self, const u64 *other, size_t N, size_t W,
+                        size_t self_stride, size_t other_stride);
+
+}  // namespace crdt
+
+#define CRDT_CHECK_CTX(ctx)                   \
+  do {                                        \
+    if (!(ctx)) return CRDT_EINVAL;           \
+  } while (0)
+
+#define CRDT_HIP(ctx, expr)                            \
+  do {                                                 \
+    hipError_t _e = (expr);                            \
+    if (_e != hipSuccess) return crdt::hip_fail((ctx), _e, #expr); \
+  } while (0)

@@ -1,0 +1,172 @@
+// Context lifecycle, error reporting, scratch and event timing for libcrdt_gpu.
+#include <cstdarg>
+
+#include "common.hpp"
+
+namespace crdt {
+
+static thread_local std::string g_orphan_error;  // errors raised with ctx == NULL
+
+int fail(crdt_ctx *ctx, int code, const char *fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (ctx) ctx->last_error = buf;
+  else g_orphan_error = buf;
+  return code;
+}
+
+int hip_fail(crdt_ctx *ctx, hipError_t e, const char *what) {
+  return fail(ctx, CRDT_EHIP, "%s failed: %s (%d)", what, hipGetErrorString(e), (int)e);
+}
+
+int ensure_scratch(crdt_ctx *ctx, size_t bytes) {
+  if (bytes <= ctx->scratch_bytes) return CRDT_OK;
+  if (ctx->scratch) {
+    // The old scratch may still be read by queued kernels: drain the stream first.
+    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipFree(ctx->scratch);
+    ctx->scratch = nullptr;
+    ctx->scratch_bytes = 0;
+  }
+  size_t want = bytes < (1u << 20) ? (1u << 20) : bytes + bytes / 4;
+  hipError_t e = hipMalloc(&ctx->scratch, want);
+  if (e != hipSuccess) {
+    ctx->scratch = nullptr;
+    return fail(ctx, CRDT_ENOMEM, "scratch hipMalloc(%zu) failed: %s", want, hipGetErrorString(e));
+  }
+  ctx->scratch_bytes = want;
+  // Arrival counters live at the front of scratch and must start at zero (kernels that use
+  // them reset them to zero when they finish).
+  e = hipMemsetAsync(ctx->scratch, 0, want, ctx->stream);
+  if (e != hipSuccess) return hip_fail(ctx, e, "hipMemsetAsync(scratch)");
+  return CRDT_OK;
+}
+
+static hipEvent_t take_event(crdt_ctx *ctx) {
+  if (!ctx->free_events.empty()) {
+    hipEvent_t e = ctx->free_events.back();
+    ctx->free_events.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  (void)hipEventCreate(&e);
+  return e;
+}
+
+void timing_begin(crdt_ctx *ctx, const char *name) {
+  if (!ctx->timing) return;
+  PendingTiming p;
+  p.name = name;
+  p.start = take_event(ctx);
+  p.stop = take_event(ctx);
+  (void)hipEventRecord(p.start, ctx->stream);
+  ctx->pending.push_back(p);
+}
+
+void timing_end(crdt_ctx *ctx) {
+  if (!ctx->timing || ctx->pending.empty()) return;
+  (void)hipEventRecord(ctx->pending.back().stop, ctx->stream);
+}
+
+static void drain_timings(crdt_ctx *ctx) {
+  for (auto &p : ctx->pending) {
+    (void)hipEventSynchronize(p.stop);
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, p.start, p.stop) == hipSuccess) {
+      auto &t = ctx->timers[p.name];
+      t.total_ms += ms;
+      t.launches += 1;
+    }
+    ctx->free_events.push_back(p.start);
+    ctx->free_events.push_back(p.stop);
+  }
+  ctx->pending.clear();
+}
+
+}  // namespace crdt
+
+using namespace crdt;
+
+extern "C" {
+
+int crdt_ctx_create(int device, crdt_ctx **out) {
+  if (!out) return fail(nullptr, CRDT_EINVAL, "crdt_ctx_create: out is NULL");
+  *out = nullptr;
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n == 0)
+    return fail(nullptr, CRDT_EHIP, "crdt_ctx_create: no HIP device (%s)", hipGetErrorString(e));
+  if (device < 0 || device >= n)
+    return fail(nullptr, CRDT_EINVAL, "crdt_ctx_create: device %d out of range [0,%d)", device, n);
+  e = hipSetDevice(device);
+  if (e != hipSuccess) return hip_fail(nullptr, e, "hipSetDevice");
+  auto *ctx = new crdt_ctx();
+  ctx->device = device;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+    ctx->cu_count = prop.multiProcessorCount;
+  *out = ctx;
+  return CRDT_OK;
+}
+
+int crdt_ctx_destroy(crdt_ctx *ctx) {
+  if (!ctx) return CRDT_OK;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  for (auto &p : ctx->pending) {
+    (void)hipEventDestroy(p.start);
+    (void)hipEventDestroy(p.stop);
+  }
+  for (auto e : ctx->free_events) (void)hipEventDestroy(e);
+  if (ctx->scratch) (void)hipFree(ctx->scratch);
+  delete ctx;
+  return CRDT_OK;
+}
+
+int crdt_ctx_set_stream(crdt_ctx *ctx, void *hip_stream) {
+  CRDT_CHECK_CTX(ctx);
+  ctx->stream = reinterpret_cast<hipStream_t>(hip_stream);
+  return CRDT_OK;
+}
+
+int crdt_ctx_synchronize(crdt_ctx *ctx) {
+  CRDT_CHECK_CTX(ctx);
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  CRDT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return CRDT_OK;
+}
+
+const char *crdt_last_error(const crdt_ctx *ctx) {
+  return ctx ? ctx->last_error.c_str() : g_orphan_error.c_str();
+}
+
+const char *crdt_version(void) { return "0.1.0"; }
+const char *crdt_build_target(void) { return "gfx950"; }
+
+int crdt_ctx_set_timing(crdt_ctx *ctx, int enable) {
+  CRDT_CHECK_CTX(ctx);
+  ctx->timing = enable != 0;
+  return CRDT_OK;
+}
+
+int crdt_ctx_timing(crdt_ctx *ctx, const char *name, double *total_ms, uint64_t *launches) {
+  CRDT_CHECK_CTX(ctx);
+  if (!name) return fail(ctx, CRDT_EINVAL, "crdt_ctx_timing: name is NULL");
+  drain_timings(ctx);
+  auto it = ctx->timers.find(name);
+  if (total_ms) *total_ms = it == ctx->timers.end() ? 0.0 : it->second.total_ms;
+  if (launches) *launches = it == ctx->timers.end() ? 0 : it->second.launches;
+  return CRDT_OK;
+}
+
+int crdt_ctx_timing_reset(crdt_ctx *ctx) {
+  CRDT_CHECK_CTX(ctx);
+  drain_timings(ctx);
+  ctx->timers.clear();
+  return CRDT_OK;
+}
+
+}  // extern "C"

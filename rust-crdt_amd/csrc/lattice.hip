@@ -1,0 +1,399 @@
+// Lattice lub kernels: elementwise max (VClock, GCounter, PNCounter) and bitwise OR (GSet).
+//
+// Reference semantics (crdts 3.0.0):
+//   VClock::merge    vclock.rs:130-136 -> apply_dot :155-159  => out[a] = max(self[a], other[a])
+//   GCounter::merge  gcounter.rs:44-48  (VClock on `inner`)
+//   PNCounter::merge pncounter.rs:70-75 (P and N independently)  => max over a row of 2A words
+//   GSet::merge      gset.rs:38-40 -> insert :69-71             => union = OR of interned bitmaps
+// All four joins are associative, commutative and idempotent (README.md:37-47), so the fold
+// `acc = T::new(); for r: acc.merge(r)` equals any tree of joins: the kernels fold a slice
+// of replicas per thread in registers, combine the threads of a workgroup through LDS and
+// the workgroups of a group through a two-level last-arriver combine inside the same launch.
+//
+// HBM layout: replica (g, r) row = in + g*gstride + r*rstride, W words contiguous.
+// Loads are 16 B per lane (u64x2) and non-temporal: every input byte is read exactly once.
+#include "common.hpp"
+
+namespace crdt {
+
+template <int V>
+struct VecOf;
+template <>
+struct VecOf<1> {
+  using T = u64;
+};
+template <>
+struct VecOf<2> {
+  using T = u64x2;
+};
+
+template <Op OP>
+__device__ __forceinline__ u64 vjoin(u64 a, u64 b) {
+  return join<OP>(a, b);
+}
+template <Op OP>
+__device__ __forceinline__ u64x2 vjoin(u64x2 a, u64x2 b) {
+  return join2<OP>(a, b);
+}
+
+template <typename VT>
+__device__ __forceinline__ VT vzero() {
+  return VT(0);
+}
+
+// Fold n rows spaced `step` vectors apart, U loads in flight per thread.
+template <Op OP, typename VT, int U, bool NT>
+__device__ __forceinline__ VT fold_rows(const VT *__restrict__ p, size_t n, long long step) {
+  VT acc = vzero<VT>();
+  size_t i = 0;
+  for (; i + U <= n; i += U) {
+    VT v[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      if constexpr (NT) v[k] = __builtin_nontemporal_load(p + k * step);
+      else v[k] = p[k * step];
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) acc = vjoin<OP>(acc, v[k]);
+    p += U * step;
+  }
+  for (; i < n; ++i) {
+    VT v;
+    if constexpr (NT) v = __builtin_nontemporal_load(p);
+    else v = *p;
+    acc = vjoin<OP>(acc, v);
+    p += step;
+  }
+  return acc;
+}
+
+// Combine the TR row-lanes of a workgroup that share a column (lane l = rsub*PW + cl).
+// Result valid for rsub == 0.  Every thread of the block must call it.
+template <Op OP, typename VT>
+__device__ __forceinline__ VT block_rows_combine(VT acc, VT *red, int l, int PW, int TR) {
+  if (TR > 1) {
+    red[l] = acc;
+    __syncthreads();
+    if (l < PW) {
+      for (int j = 1; j < TR; ++j) acc = vjoin<OP>(acc, red[l + j * PW]);
+    }
+    __syncthreads();
+  }
+  return acc;
+}
+
+struct LubPlan {
+  const u64 *in;
+  u64 *out;
+  u64 *part;   // [units][S][PW] vectors
+  u64 *cpart;  // [units][ncl][PW] vectors
+  unsigned *cnt1;  // [units][ncl]
+  unsigned *cnt2;  // [units]
+  long long rstride, gstride, ostride;  // words
+  unsigned long long R, Rs;
+  int Wv, PW, TR, ncolblk, S, CL, ncl;
+  int accumulate;
+};
+
+template <Op OP, typename VT>
+__device__ __forceinline__ void store_out(const LubPlan &p, size_t g, int col, VT v) {
+  VT *o = reinterpret_cast<VT *>(p.out + g * p.ostride) + col;
+  if (p.accumulate) v = vjoin<OP>(v, *o);
+  *o = v;
+}
+
+// Agent-scope arrival on a counter after this block's stores (MI355X_MICROARCH.md
+// "Valid forms": waitcnt -> barrier -> lane-0 release fence -> waitcnt -> atomic).
+// Returns (block-uniformly) whether this block is the last of `expected` arrivals; the last
+// arriver resets the counter and performs the agent-scope acquire before returning.
+__device__ __forceinline__ bool arrive_last(unsigned *counter, unsigned expected, int *s_flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int last = (t == expected - 1);
+    if (last) {
+      __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    *s_flag = last;
+  }
+  __syncthreads();
+  return *s_flag != 0;
+}
+
+// One launch = the whole lub.  Block b -> (unit u = g*ncolblk + cb, slice s).
+template <Op OP, int V, int U>
+__global__ __launch_bounds__(kBlock) void lub_stream_kernel(LubPlan p) {
+  using VT = typename VecOf<V>::T;
+  __shared__ VT red[kBlock];
+  __shared__ int s_flag;
+  const int l = threadIdx.x;
+  const unsigned b = blockIdx.x;
+  const int s = b % p.S;
+  const unsigned u = b / p.S;
+  const int cb = u % p.ncolblk;
+  const size_t g = u / p.ncolblk;
+  const int cl = l % p.PW;
+  const int rsub = l / p.PW;
+  const int col = cb * kBlock + cl;
+  const bool active = rsub < p.TR && col < p.Wv;
+
+  VT acc = vzero<VT>();
+  if (active) {
+    const unsigned long long rbeg = (unsigned long long)s * p.Rs;
+    const unsigned long long rend = min(p.R, rbeg + p.Rs);
+    const unsigned long long r0 = rbeg + rsub;
+    if (r0 < rend) {
+      const size_t n = (rend - r0 + p.TR - 1) / p.TR;
+      const VT *src = reinterpret_cast<const VT *>(p.in + g * p.gstride + r0 * p.rstride) + col;
+      acc = fold_rows<OP, VT, U, true>(src, n, (long long)p.TR * p.rstride / V);
+    }
+  }
+  acc = block_rows_combine<OP>(acc, red, l, p.PW, p.TR);
+  const bool writer = (l < p.PW) && col < p.Wv;
+  if (p.S == 1) {
+    if (writer) store_out<OP>(p, g, col, acc);
+    return;
+  }
+
+  // Level 1: publish this slice's partial row; the last slice of the cluster combines it.
+  VT *part = reinterpret_cast<VT *>(p.part);
+  if (writer) part[((size_t)u * p.S + s) * p.PW + cl] = acc;
+  const int c = s / p.CL;
+  const int csize = min(p.CL, p.S - c * p.CL);
+  if (!arrive_last(p.cnt1 + (size_t)u * p.ncl + c, csize, &s_flag)) return;
+
+  acc = vzero<VT>();
+  {
+    const int TRc = p.TR;
+    if (rsub < TRc && col < p.Wv) {
+      const int r0 = rsub;
+      if (r0 < csize) {
+        const size_t n = (csize - r0 + TRc - 1) / TRc;
+        acc = fold_rows<OP, VT, 4, false>(part + ((size_t)u * p.S + c * p.CL + r0) * p.PW + cl, n,
+                                          (long long)TRc * p.PW);
+      }
+    }
+  }
+  acc = block_rows_combine<OP>(acc, red, l, p.PW, p.TR);
+  if (p.ncl == 1) {
+    if (writer) store_out<OP>(p, g, col, acc);
+    return;
+  }
+
+  // Level 2: publish the cluster partial; the last cluster combines all of them.
+  VT *cpart = reinterpret_cast<VT *>(p.cpart);
+  if (writer) cpart[((size_t)u * p.ncl + c) * p.PW + cl] = acc;
+  if (!arrive_last(p.cnt2 + u, p.ncl, &s_flag)) return;
+
+  acc = vzero<VT>();
+  if (rsub < p.TR && col < p.Wv && rsub < p.ncl) {
+    const size_t n = (p.ncl - rsub + p.TR - 1) / p.TR;
+    acc = fold_rows<OP, VT, 4, false>(cpart + ((size_t)u * p.ncl + rsub) * p.PW + cl, n,
+                                      (long long)p.TR * p.PW);
+  }
+  acc = block_rows_combine<OP>(acc, red, l, p.PW, p.TR);
+  if (writer) store_out<OP>(p, g, col, acc);
+}
+
+// self[i] := self[i] ⊔ other[i]: three streams (2 reads, 1 write), TR rows per block step.
+template <Op OP, int V>
+__global__ __launch_bounds__(kBlock) void merge_pairs_kernel(u64 *self, const u64 *other,
+                                                             unsigned long long N, int Wv, int PW,
+                                                             int TR, long long sstride,
+                                                             long long ostride,
+                                                             unsigned long long rows_per_block) {
+  using VT = typename VecOf<V>::T;
+  const int l = threadIdx.x;
+  const int cl = l % PW;
+  const int rsub = l / PW;
+  const int col = blockIdx.y * kBlock + cl;
+  if (rsub >= TR || col >= Wv) return;
+  const unsigned long long rbeg = (unsigned long long)blockIdx.x * rows_per_block;
+  const unsigned long long rend = min(N, rbeg + rows_per_block);
+  for (unsigned long long r = rbeg + rsub; r < rend; r += TR) {
+    VT *sp = reinterpret_cast<VT *>(self + r * sstride) + col;
+    const VT *op = reinterpret_cast<const VT *>(other + r * ostride) + col;
+    VT a = *sp;
+    VT bv = __builtin_nontemporal_load(op);
+    *sp = vjoin<OP>(a, bv);
+  }
+}
+
+static bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+int lattice_lub_many(crdt_ctx *ctx, Op op, const u64 *in, size_t G, size_t R, size_t W,
+                     size_t row_stride, size_t group_stride, u64 *out, size_t out_stride,
+                     unsigned flags) {
+  CRDT_CHECK_CTX(ctx);
+  if (G == 0 || W == 0) return CRDT_OK;
+  if (!out) return fail(ctx, CRDT_EINVAL, "lub_many: out is NULL");
+  if (G > 1 && out_stride < W)
+    return fail(ctx, CRDT_EINVAL, "lub_many: out_stride %zu < row width %zu", out_stride, W);
+  if (W > (size_t)1 << 30) return fail(ctx, CRDT_EUNSUPPORTED, "lub_many: row width %zu too large", W);
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  const bool accumulate = flags & CRDT_ACCUMULATE;
+  if (R == 0) {  // fold of nothing = T::new() (all zero); with ACCUMULATE: unchanged
+    if (!accumulate)
+      CRDT_HIP(ctx, hipMemset2DAsync(out, (G > 1 ? out_stride : W) * 8, 0, W * 8, G, ctx->stream));
+    return CRDT_OK;
+  }
+  if (!in) return fail(ctx, CRDT_EINVAL, "lub_many: in is NULL");
+  if (R > 1 && row_stride < W)
+    return fail(ctx, CRDT_EINVAL, "lub_many: row_stride %zu < row width %zu", row_stride, W);
+
+  const bool vec2 = (W % 2 == 0) && (R == 1 || row_stride % 2 == 0) &&
+                    (G == 1 || (group_stride % 2 == 0 && out_stride % 2 == 0)) && aligned16(in) &&
+                    aligned16(out);
+  const int V = vec2 ? 2 : 1;
+  LubPlan p{};
+  p.in = in;
+  p.out = out;
+  p.rstride = (long long)row_stride;
+  p.gstride = (long long)group_stride;
+  p.ostride = (long long)out_stride;
+  p.R = R;
+  p.Wv = (int)(W / V);
+  p.PW = p.Wv <= kBlock ? p.Wv : kBlock;
+  p.TR = kBlock / p.PW;
+  p.ncolblk = (p.Wv + kBlock - 1) / kBlock;
+  p.accumulate = accumulate ? 1 : 0;
+
+  // Slice replicas so the grid holds ~8 workgroups per CU, each thread folding >= 16 rows.
+  const size_t units = G * (size_t)p.ncolblk;
+  const size_t target = (size_t)ctx->cu_count * 8;
+  const size_t steps = (R + p.TR - 1) / p.TR;
+  size_t S = 1;
+  if (units < target) {
+    S = (target + units - 1) / units;
+    size_t max_s = steps / 16;
+    if (max_s < 1) max_s = 1;
+    if (S > max_s) S = max_s;
+  }
+  size_t Rs = (R + S - 1) / S;
+  Rs = (Rs + p.TR - 1) / p.TR * p.TR;  // whole block steps per slice
+  S = (R + Rs - 1) / Rs;
+  if ((size_t)units * S > 0x7fffffffULL)
+    return fail(ctx, CRDT_EUNSUPPORTED, "lub_many: grid too large (%zu units x %zu slices)", units, S);
+  p.S = (int)S;
+  p.Rs = Rs;
+  p.CL = 32;
+  p.ncl = (p.S + p.CL - 1) / p.CL;
+
+  if (p.S > 1) {
+    const size_t vecb = (size_t)V * 8;
+    const size_t part_b = units * S * p.PW * vecb;
+    const size_t cpart_b = units * p.ncl * p.PW * vecb;
+    const size_t cnt_b = (units * p.ncl + units) * sizeof(unsigned);
+    const size_t cnt_pad = (cnt_b + 255) / 256 * 256;
+    int rc = ensure_scratch(ctx, cnt_pad + part_b + cpart_b);
+    if (rc) return rc;
+    char *base = static_cast<char *>(ctx->scratch);
+    p.cnt1 = reinterpret_cast<unsigned *>(base);
+    p.cnt2 = p.cnt1 + units * p.ncl;
+    p.part = reinterpret_cast<u64 *>(base + cnt_pad);
+    p.cpart = reinterpret_cast<u64 *>(base + cnt_pad + part_b);
+  }
+
+  const dim3 grid((unsigned)(units * S));
+  timing_begin(ctx, "lub_stream");
+  if (op == Op::Max) {
+    if (V == 2) hipLaunchKernelGGL((lub_stream_kernel<Op::Max, 2, 8>), grid, dim3(kBlock), 0, ctx->stream, p);
+    else hipLaunchKernelGGL((lub_stream_kernel<Op::Max, 1, 8>), grid, dim3(kBlock), 0, ctx->stream, p);
+  } else {
+    if (V == 2) hipLaunchKernelGGL((lub_stream_kernel<Op::Or, 2, 8>), grid, dim3(kBlock), 0, ctx->stream, p);
+    else hipLaunchKernelGGL((lub_stream_kernel<Op::Or, 1, 8>), grid, dim3(kBlock), 0, ctx->stream, p);
+  }
+  timing_end(ctx);
+  CRDT_HIP(ctx, hipGetLastError());
+  return CRDT_OK;
+}
+
+int lattice_merge_batch(crdt_ctx *ctx, Op op, u64 *self, const u64 *other, size_t N, size_t W,
+                        size_t self_stride, size_t other_stride) {
+  CRDT_CHECK_CTX(ctx);
+  if (N == 0 || W == 0) return CRDT_OK;
+  if (!self || !other) return fail(ctx, CRDT_EINVAL, "merge_batch: NULL buffer");
+  if (N > 1 && (self_stride < W || other_stride < W))
+    return fail(ctx, CRDT_EINVAL, "merge_batch: stride < row width %zu", W);
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  const bool vec2 = W % 2 == 0 && (N == 1 || (self_stride % 2 == 0 && other_stride % 2 == 0)) &&
+                    aligned16(self) && aligned16(other);
+  const int V = vec2 ? 2 : 1;
+  const int Wv = (int)(W / V);
+  const int PW = Wv <= kBlock ? Wv : kBlock;
+  const int TR = kBlock / PW;
+  const int ncolblk = (Wv + kBlock - 1) / kBlock;
+  // ~16 row steps per block, capped at 8 blocks per CU worth of rows.
+  unsigned long long rpb = (unsigned long long)TR * 16;
+  unsigned long long nb = (N + rpb - 1) / rpb;
+  if (nb > 0x7fffffffULL) return fail(ctx, CRDT_EUNSUPPORTED, "merge_batch: N too large");
+  dim3 grid((unsigned)nb, (unsigned)ncolblk);
+  timing_begin(ctx, "merge_pairs");
+  if (op == Op::Max) {
+    if (V == 2) hipLaunchKernelGGL((merge_pairs_kernel<Op::Max, 2>), grid, dim3(kBlock), 0, ctx->stream, self, other, N, Wv, PW, TR, (long long)self_stride, (long long)other_stride, rpb);
+    else hipLaunchKernelGGL((merge_pairs_kernel<Op::Max, 1>), grid, dim3(kBlock), 0, ctx->stream, self, other, N, Wv, PW, TR, (long long)self_stride, (long long)other_stride, rpb);
+  } else {
+    if (V == 2) hipLaunchKernelGGL((merge_pairs_kernel<Op::Or, 2>), grid, dim3(kBlock), 0, ctx->stream, self, other, N, Wv, PW, TR, (long long)self_stride, (long long)other_stride, rpb);
+    else hipLaunchKernelGGL((merge_pairs_kernel<Op::Or, 1>), grid, dim3(kBlock), 0, ctx->stream, self, other, N, Wv, PW, TR, (long long)self_stride, (long long)other_stride, rpb);
+  }
+  timing_end(ctx);
+  CRDT_HIP(ctx, hipGetLastError());
+  return CRDT_OK;
+}
+
+}  // namespace crdt
+
+using crdt::Op;
+using crdt::u64;
+
+extern "C" {
+
+int crdt_vclock_lub_many(crdt_ctx *ctx, const uint64_t *in, size_t G, size_t R, size_t A,
+                         size_t row_stride, size_t group_stride, uint64_t *out,
+                         size_t out_stride, unsigned flags) {
+  return crdt::lattice_lub_many(ctx, Op::Max, (const u64 *)in, G, R, A, row_stride, group_stride,
+                                (u64 *)out, out_stride, flags);
+}
+int crdt_vclock_merge_batch(crdt_ctx *ctx, uint64_t *self, const uint64_t *other, size_t N,
+                            size_t A, size_t self_stride, size_t other_stride) {
+  return crdt::lattice_merge_batch(ctx, Op::Max, (u64 *)self, (const u64 *)other, N, A,
+                                   self_stride, other_stride);
+}
+int crdt_gcounter_lub_many(crdt_ctx *ctx, const uint64_t *in, size_t G, size_t R, size_t A,
+                           size_t row_stride, size_t group_stride, uint64_t *out,
+                           size_t out_stride, unsigned flags) {
+  return crdt_vclock_lub_many(ctx, in, G, R, A, row_stride, group_stride, out, out_stride, flags);
+}
+int crdt_gcounter_merge_batch(crdt_ctx *ctx, uint64_t *self, const uint64_t *other, size_t N,
+                              size_t A, size_t self_stride, size_t other_stride) {
+  return crdt_vclock_merge_batch(ctx, self, other, N, A, self_stride, other_stride);
+}
+int crdt_pncounter_lub_many(crdt_ctx *ctx, const uint64_t *in, size_t G, size_t R, size_t A,
+                            size_t row_stride, size_t group_stride, uint64_t *out,
+                            size_t out_stride, unsigned flags) {
+  return crdt::lattice_lub_many(ctx, Op::Max, (const u64 *)in, G, R, 2 * A, row_stride,
+                                group_stride, (u64 *)out, out_stride, flags);
+}
+int crdt_pncounter_merge_batch(crdt_ctx *ctx, uint64_t *self, const uint64_t *other,
+                               size_t N, size_t A, size_t self_stride, size_t other_stride) {
+  return crdt::lattice_merge_batch(ctx, Op::Max, (u64 *)self, (const u64 *)other, N, 2 * A,
+                                   self_stride, other_stride);
+}
+int crdt_gset_lub_many(crdt_ctx *ctx, const uint64_t *in, size_t G, size_t R, size_t words,
+                       size_t row_stride, size_t group_stride, uint64_t *out,
+                       size_t out_stride, unsigned flags) {
+  return crdt::lattice_lub_many(ctx, Op::Or, (const u64 *)in, G, R, words, row_stride,
+                                group_stride, (u64 *)out, out_stride, flags);
+}
+int crdt_gset_merge_batch(crdt_ctx *ctx, uint64_t *self, const uint64_t *other, size_t N,
+                          size_t words, size_t self_stride, size_t other_stride) {
+  return crdt::lattice_merge_batch(ctx, Op::Or, (u64 *)self, (const u64 *)other, N, words,
+                                   self_stride, other_stride);
+}
+
+}  // extern "C"

@@ -1,0 +1,390 @@
+// Orswot<member, actor> batched merge (lub of many replicas).
+//
+// Reference: Orswot::merge (orswot.rs:81-149), apply_rm (:230-250), apply_deferred (:281-286),
+// VClock::forget (vclock.rs:95-105), intersection (:218-227), clone_without (:148-152).
+//
+// Dense restatement per (member m, actor a), with e = entry dot counter (0 = no dot),
+// c = the replica clock's counter for a:
+//   join((e1,c1),(e2,c2)) = ( max( e1==e2 ? e1 : 0,       // intersection (:113)
+//                                  e1>c2  ? e1 : 0,       // our_clock.clone_without(other.clock) (:115)
+//                                  e2>c1  ? e2 : 0 ),     // clock.clone_without(self.clock) (:114)
+//                             max(c1, c2) )               // self.clock.merge (:145)
+// One-sided members reduce to the same formula (:86-101 drop-if-dominated + forget, :124-136),
+// and a member is present iff some e != 0 (empty common clock => removed, :116-118).
+// Under the reference's invariants (each dot unique, e <= c) the join is associative, so
+// replicas are folded per thread, then slice partials are joined by the last-arriving block.
+// Deferred removes (rm, S) of every replica are then applied after the join: for m in S,
+// e = e > rm[a] ? e : 0 (forget); a deferred survives iff !(rm <= final clock) (:240-249);
+// survivors with identical rm clocks merge their member sets (:242-246).
+#include "common.hpp"
+
+namespace crdt {
+
+constexpr int kOrMPT = 4;  // members per thread
+
+template <int V>
+struct OVec;
+template <>
+struct OVec<1> {
+  using T = u64;
+};
+template <>
+struct OVec<2> {
+  using T = u64x2;
+};
+
+__device__ __forceinline__ u64 umax(u64 a, u64 b) { return a > b ? a : b; }
+
+__device__ __forceinline__ u64 dot_join(u64 e1, u64 c1, u64 e2, u64 c2) {
+  const u64 t0 = e1 == e2 ? e1 : 0;
+  const u64 t1 = e1 > c2 ? e1 : 0;
+  const u64 t2 = e2 > c1 ? e2 : 0;
+  return umax(t0, umax(t1, t2));
+}
+__device__ __forceinline__ u64x2 dot_join(u64x2 e1, u64x2 c1, u64x2 e2, u64x2 c2) {
+  u64x2 r;
+  r.x = dot_join(e1.x, c1.x, e2.x, c2.x);
+  r.y = dot_join(e1.y, c1.y, e2.y, c2.y);
+  return r;
+}
+__device__ __forceinline__ u64x2 umax(u64x2 a, u64x2 b) {
+  u64x2 r;
+  r.x = umax(a.x, b.x);
+  r.y = umax(a.y, b.y);
+  return r;
+}
+
+struct OrPlan {
+  const u64 *clock;
+  const u64 *entries;
+  long long c_rstride, c_gstride, e_mstride, e_rstride, e_gstride;  // words
+  unsigned long long G, R, M, A, Rs;
+  int Wv, PW, MB, ncolblk, nmblk, S;
+  u64 *part;       // per unit: S slabs of (MB*MPT*PW E vectors + PW C vectors)
+  unsigned *cnt;   // [units]
+  u64 *out_clock;  // [G][A]
+  u64 *out_entries;  // [G][M][A]
+};
+
+template <int V>
+__global__ __launch_bounds__(kBlock) void orswot_join_kernel(OrPlan p) {
+  using VT = typename OVec<V>::T;
+  __shared__ int s_flag;
+  const int l = threadIdx.x;
+  const unsigned b = blockIdx.x;
+  const int s = b % p.S;
+  unsigned u = b / p.S;
+  const int cb = u % p.ncolblk;
+  const unsigned rest = u / p.ncolblk;
+  const int mb = rest % p.nmblk;
+  const size_t g = rest / p.nmblk;
+  const int cl = l % p.PW;
+  const int ml = l / p.PW;
+  const int col = cb * kBlock + cl;
+  const bool active = ml < p.MB && col < p.Wv;
+  const size_t mbase = (size_t)mb * p.MB * kOrMPT + ml;
+
+  VT e[kOrMPT], c;
+  c = VT(0);
+#pragma unroll
+  for (int j = 0; j < kOrMPT; ++j) e[j] = VT(0);
+  bool mok[kOrMPT];
+#pragma unroll
+  for (int j = 0; j < kOrMPT; ++j) mok[j] = active && (mbase + (size_t)j * p.MB) < p.M;
+
+  if (active) {
+    const unsigned long long rbeg = (unsigned long long)s * p.Rs;
+    const unsigned long long rend = min(p.R, rbeg + p.Rs);
+    const VT *cp = reinterpret_cast<const VT *>(p.clock + g * p.c_gstride + rbeg * p.c_rstride) + col;
+    const VT *ep = reinterpret_cast<const VT *>(p.entries + g * p.e_gstride + rbeg * p.e_rstride +
+                                                mbase * p.e_mstride) + col;
+    const long long cstep = p.c_rstride / V;
+    const long long estep = p.e_rstride / V;
+    const long long mstep = (long long)p.MB * p.e_mstride / V;
+    for (unsigned long long r = rbeg; r < rend; ++r) {
+      const VT c2 = *cp;
+      VT e2[kOrMPT];
+#pragma unroll
+      for (int j = 0; j < kOrMPT; ++j)
+        e2[j] = mok[j] ? __builtin_nontemporal_load(ep + j * mstep) : VT(0);
+#pragma unroll
+      for (int j = 0; j < kOrMPT; ++j) e[j] = dot_join(e[j], c, e2[j], c2);
+      c = umax(c, c2);
+      cp += cstep;
+      ep += estep;
+    }
+  }
+
+  const size_t slab = (size_t)p.MB * kOrMPT * p.PW + p.PW;  // vectors
+  auto store_final = [&](void) {
+    if (!active) return;
+    VT *oe = reinterpret_cast<VT *>(p.out_entries + g * p.M * p.A);
+#pragma unroll
+    for (int j = 0; j < kOrMPT; ++j)
+      if (mok[j]) oe[(mbase + (size_t)j * p.MB) * (p.A / V) + col] = e[j];
+    if (mb == 0 && ml == 0) reinterpret_cast<VT *>(p.out_clock + g * p.A)[col] = c;
+  };
+  if (p.S == 1) {
+    store_final();
+    return;
+  }
+  VT *part = reinterpret_cast<VT *>(p.part) + ((size_t)u * p.S + s) * slab;
+  if (active) {
+#pragma unroll
+    for (int j = 0; j < kOrMPT; ++j) part[(ml + j * p.MB) * p.PW + cl] = e[j];
+    if (ml == 0) part[(size_t)p.MB * kOrMPT * p.PW + cl] = c;
+  }
+  // Release this slab; the last slice of the unit joins all slabs (in slice order).
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (l == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned t = __hip_atomic_fetch_add(p.cnt + u, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int last = t == (unsigned)p.S - 1;
+    if (last) {
+      __hip_atomic_store(p.cnt + u, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    s_flag = last;
+  }
+  __syncthreads();
+  if (!s_flag) return;
+  if (active) {
+    c = VT(0);
+#pragma unroll
+    for (int j = 0; j < kOrMPT; ++j) e[j] = VT(0);
+    const VT *pp = reinterpret_cast<const VT *>(p.part) + (size_t)u * p.S * slab;
+    for (int k = 0; k < p.S; ++k, pp += slab) {
+      const VT c2 = pp[(size_t)p.MB * kOrMPT * p.PW + cl];
+#pragma unroll
+      for (int j = 0; j < kOrMPT; ++j) e[j] = dot_join(e[j], c, pp[(ml + j * p.MB) * p.PW + cl], c2);
+      c = umax(c, c2);
+    }
+  }
+  store_final();
+}
+
+struct DefPlan {
+  const size_t *def_off;  // device copy, G+1
+  unsigned long long G, D, M, A, Mw;
+  const u64 *def_clock, *def_members;
+  const u64 *out_clock;
+  u64 *out_entries;
+  u64 *hash;          // [D]
+  unsigned *surv;     // [D] compacted survivor list
+  unsigned *nsurv;    // counter
+  uint8_t *out_keep;
+  u64 *out_members;
+};
+
+__device__ __forceinline__ unsigned long long group_of(const size_t *off, unsigned long long G,
+                                                       unsigned long long d) {
+  unsigned long long lo = 0, hi = G;  // find g with off[g] <= d < off[g+1]
+  while (hi - lo > 1) {
+    const unsigned long long mid = (lo + hi) / 2;
+    if (off[mid] <= d) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// One workgroup per deferred remove: survival test, row hash, ceiling on the joined entries.
+__global__ __launch_bounds__(kBlock) void orswot_deferred_kernel(DefPlan p) {
+  __shared__ u64 s_hash[kBlock / kWave];
+  const unsigned long long d = blockIdx.x;
+  const unsigned long long g = group_of(p.def_off, p.G, d);
+  const u64 *rm = p.def_clock + d * p.A;
+  const u64 *cf = p.out_clock + g * p.A;
+  int greater = 0;
+  u64 h = 0;
+  for (unsigned long long a = threadIdx.x; a < p.A; a += kBlock) {
+    const u64 x = rm[a];
+    greater |= x > cf[a];
+    // Order-independent row hash (sum of per-cell mixes) to pre-filter identical clocks.
+    u64 z = x * 0x9E3779B97F4A7C15ULL + a;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    h += z ^ (z >> 31);
+  }
+  const int keep = __syncthreads_or(greater);
+  for (int off = kWave / 2; off > 0; off >>= 1) h += __shfl_down(h, off, kWave);
+  if ((threadIdx.x & (kWave - 1)) == 0) s_hash[threadIdx.x / kWave] = h;
+  // Ceiling: forget(rm) on every member of S (race-benign: only zeros are written and the
+  // test reads the joined value, which no other write can change except to zero).
+  const u64 *bits = p.def_members + d * p.Mw;
+  u64 *E = p.out_entries + g * p.M * p.A;
+  for (unsigned long long w = 0; w < p.Mw; ++w) {
+    u64 word = bits[w];
+    while (word) {
+      const int bit = __builtin_ctzll(word);
+      word &= word - 1;
+      const unsigned long long m = w * 64 + bit;
+      if (m >= p.M) break;
+      u64 *row = E + m * p.A;
+      for (unsigned long long a = threadIdx.x; a < p.A; a += kBlock) {
+        const u64 e = row[a];
+        if (e != 0 && e <= rm[a]) row[a] = 0;
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    u64 t = 0;
+    for (int w = 0; w < kBlock / kWave; ++w) t += s_hash[w];
+    p.hash[d] = t;
+    if (keep) p.surv[atomicAdd(p.nsurv, 1u)] = (unsigned)d;
+  }
+}
+
+// One thread per survivor: representative = smallest survivor index of the same group with
+// an identical rm clock; OR its member set into the representative's output row.
+__global__ __launch_bounds__(kBlock) void orswot_dedup_kernel(DefPlan p) {
+  const unsigned k = blockIdx.x * blockDim.x + threadIdx.x;
+  const unsigned n = *p.nsurv;
+  if (k >= n) return;
+  const unsigned d = p.surv[k];
+  const unsigned long long g = group_of(p.def_off, p.G, d);
+  const u64 h = p.hash[d];
+  const u64 *rm = p.def_clock + (size_t)d * p.A;
+  unsigned rep = d;
+  for (unsigned j = 0; j < n; ++j) {
+    const unsigned d2 = p.surv[j];
+    if (d2 >= rep || p.hash[d2] != h) continue;
+    if (d2 < p.def_off[g] || d2 >= p.def_off[g + 1]) continue;
+    const u64 *rm2 = p.def_clock + (size_t)d2 * p.A;
+    bool eq = true;
+    for (unsigned long long a = 0; a < p.A && eq; ++a) eq = rm[a] == rm2[a];
+    if (eq) rep = d2;
+  }
+  if (rep == d) p.out_keep[d] = 1;
+  const u64 *src = p.def_members + (size_t)d * p.Mw;
+  u64 *dst = p.out_members + (size_t)rep * p.Mw;
+  for (unsigned long long w = 0; w < p.Mw; ++w)
+    if (src[w]) atomicOr(dst + w, src[w]);
+}
+
+static bool al16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+}  // namespace crdt
+
+using namespace crdt;
+
+extern "C" int crdt_orswot_lub_many(crdt_ctx *ctx, const crdt_orswot_batch *in,
+                                    crdt_orswot_out *out) {
+  CRDT_CHECK_CTX(ctx);
+  if (!in || !out) return fail(ctx, CRDT_EINVAL, "orswot_lub_many: NULL batch/out");
+  const size_t G = in->G, R = in->R, M = in->M, A = in->A;
+  if (G == 0 || M == 0 || A == 0) return CRDT_OK;
+  if (!out->clock || !out->entries) return fail(ctx, CRDT_EINVAL, "orswot_lub_many: NULL output");
+  if (R > 0 && (!in->clock || !in->entries))
+    return fail(ctx, CRDT_EINVAL, "orswot_lub_many: NULL input");
+  if (in->entry_mstride < A && M > 1)
+    return fail(ctx, CRDT_EINVAL, "orswot_lub_many: entry_mstride < A");
+  if (A > (1u << 20) || M > (1ull << 32))
+    return fail(ctx, CRDT_EUNSUPPORTED, "orswot_lub_many: A or M too large");
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  const size_t D = (in->def_off && G > 0) ? in->def_off[G] - in->def_off[0] : 0;
+  if (in->def_off && in->def_off[0] != 0)
+    return fail(ctx, CRDT_EINVAL, "orswot_lub_many: def_off[0] must be 0");
+  if (D > 0 && (!in->def_clock || !in->def_members || !out->def_keep || !out->def_members))
+    return fail(ctx, CRDT_EINVAL, "orswot_lub_many: deferred buffers missing");
+  if (D > 0xffffffffULL) return fail(ctx, CRDT_EUNSUPPORTED, "orswot_lub_many: too many deferred");
+  const size_t Mw = (M + 63) / 64;
+
+  if (R == 0) {
+    CRDT_HIP(ctx, hipMemsetAsync(out->clock, 0, G * A * 8, ctx->stream));
+    CRDT_HIP(ctx, hipMemsetAsync(out->entries, 0, G * M * A * 8, ctx->stream));
+  } else {
+    const bool vec2 = A % 2 == 0 && in->clock_rstride % 2 == 0 && in->clock_gstride % 2 == 0 &&
+                      in->entry_mstride % 2 == 0 && in->entry_rstride % 2 == 0 &&
+                      in->entry_gstride % 2 == 0 && al16(in->clock) && al16(in->entries) &&
+                      al16(out->clock) && al16(out->entries);
+    const int V = vec2 ? 2 : 1;
+    OrPlan p{};
+    p.clock = (const u64 *)in->clock;
+    p.entries = (const u64 *)in->entries;
+    p.c_rstride = in->clock_rstride;
+    p.c_gstride = in->clock_gstride;
+    p.e_mstride = in->entry_mstride;
+    p.e_rstride = in->entry_rstride;
+    p.e_gstride = in->entry_gstride;
+    p.G = G;
+    p.R = R;
+    p.M = M;
+    p.A = A;
+    p.Wv = (int)(A / V);
+    p.PW = p.Wv <= kBlock ? p.Wv : kBlock;
+    p.MB = kBlock / p.PW;
+    p.ncolblk = (p.Wv + kBlock - 1) / kBlock;
+    const size_t mpb = (size_t)p.MB * kOrMPT;
+    p.nmblk = (int)((M + mpb - 1) / mpb);
+    p.out_clock = (u64 *)out->clock;
+    p.out_entries = (u64 *)out->entries;
+    const size_t units = G * (size_t)p.nmblk * p.ncolblk;
+    const size_t target = (size_t)ctx->cu_count * 8;
+    size_t S = 1;
+    if (units < target) {
+      S = (target + units - 1) / units;
+      size_t max_s = R / 8;
+      if (max_s < 1) max_s = 1;
+      if (S > max_s) S = max_s;
+      if (S > 64) S = 64;
+    }
+    size_t Rs = (R + S - 1) / S;
+    S = (R + Rs - 1) / Rs;
+    p.S = (int)S;
+    p.Rs = Rs;
+    if (units * S > 0x7fffffffULL) return fail(ctx, CRDT_EUNSUPPORTED, "orswot_lub_many: grid too large");
+    if (S > 1) {
+      const size_t slab_b = (mpb * p.PW + p.PW) * V * 8;
+      const size_t cnt_pad = (units * sizeof(unsigned) + 255) / 256 * 256;
+      int rc = ensure_scratch(ctx, cnt_pad + units * S * slab_b);
+      if (rc) return rc;
+      p.cnt = static_cast<unsigned *>(ctx->scratch);
+      p.part = reinterpret_cast<u64 *>(static_cast<char *>(ctx->scratch) + cnt_pad);
+    }
+    timing_begin(ctx, "orswot_join");
+    if (V == 2) hipLaunchKernelGGL((orswot_join_kernel<2>), dim3((unsigned)(units * S)), dim3(kBlock), 0, ctx->stream, p);
+    else hipLaunchKernelGGL((orswot_join_kernel<1>), dim3((unsigned)(units * S)), dim3(kBlock), 0, ctx->stream, p);
+    timing_end(ctx);
+    CRDT_HIP(ctx, hipGetLastError());
+  }
+
+  if (D == 0) return CRDT_OK;
+  // Deferred bookkeeping lives in a second scratch region after the join's (the join has been
+  // queued already; growing scratch here synchronises before freeing, so it stays valid).
+  const size_t off_b = (G + 1) * sizeof(size_t);
+  const size_t need = 256 + ((off_b + 255) / 256 * 256) + D * 8 + D * 4;
+  // Use a dedicated allocation so the join's scratch (possibly still in flight) is untouched.
+  void *dscratch = nullptr;
+  CRDT_HIP(ctx, hipMallocAsync(&dscratch, need, ctx->stream));
+  char *base = static_cast<char *>(dscratch);
+  DefPlan q{};
+  q.nsurv = reinterpret_cast<unsigned *>(base);
+  q.def_off = reinterpret_cast<const size_t *>(base + 256);
+  q.hash = reinterpret_cast<u64 *>(base + 256 + (off_b + 255) / 256 * 256);
+  q.surv = reinterpret_cast<unsigned *>(q.hash + D);
+  q.G = G;
+  q.D = D;
+  q.M = M;
+  q.A = A;
+  q.Mw = Mw;
+  q.def_clock = (const u64 *)in->def_clock;
+  q.def_members = (const u64 *)in->def_members;
+  q.out_clock = (const u64 *)out->clock;
+  q.out_entries = (u64 *)out->entries;
+  q.out_keep = out->def_keep;
+  q.out_members = (u64 *)out->def_members;
+  CRDT_HIP(ctx, hipMemsetAsync(q.nsurv, 0, 4, ctx->stream));
+  CRDT_HIP(ctx, hipMemcpyAsync((void *)q.def_off, in->def_off, off_b, hipMemcpyHostToDevice, ctx->stream));
+  CRDT_HIP(ctx, hipMemsetAsync(out->def_keep, 0, D, ctx->stream));
+  CRDT_HIP(ctx, hipMemsetAsync(out->def_members, 0, D * Mw * 8, ctx->stream));
+  hipLaunchKernelGGL(orswot_deferred_kernel, dim3((unsigned)D), dim3(kBlock), 0, ctx->stream, q);
+  hipLaunchKernelGGL(orswot_dedup_kernel, dim3((unsigned)((D + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                     ctx->stream, q);
+  CRDT_HIP(ctx, hipFreeAsync(dscratch, ctx->stream));
+  CRDT_HIP(ctx, hipGetLastError());
+  return CRDT_OK;
+}

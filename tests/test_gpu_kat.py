@@ -1,0 +1,123 @@
+"""Replay the reference's known-answer tests with every merge executed by libcrdt_gpu:
+reference-shaped states are interned to the dense layout, merged on the GPU as a 2-replica
+lub_many (acc = new(); acc.merge(self); acc.merge(other) == self.merge(other)), and egressed."""
+import numpy as np
+import pytest
+
+import kat_runner as K
+import oracle as O
+from gpu_util import to_dev, to_host
+
+pytestmark = pytest.mark.gpu
+
+import crdts_gpu as cg  # noqa: E402
+from crdts_gpu import intern  # noqa: E402
+
+
+def _vc_pair(a: O.VClock, b: O.VClock, idx):
+    rows = intern.clocks_to_dense([a.dots, b.dots], idx)
+    return rows
+
+
+def gpu_merge(dst, src, kind):
+    if kind in ("vclock", "gcounter"):
+        da = dst if kind == "vclock" else dst.inner
+        sa = src if kind == "vclock" else src.inner
+        idx = intern.Index()
+        rows = _vc_pair(da, sa, idx)
+        out = to_host(cg.vclock.lub_many(to_dev(rows)))
+        da.dots = intern.dense_to_clocks(out[None, :], idx)[0]
+        return dst
+    if kind == "pncounter":
+        idx = intern.Index()
+        p = intern.clocks_to_dense([dst.p.inner.dots, src.p.inner.dots], idx)
+        n = intern.clocks_to_dense([dst.n.inner.dots, src.n.inner.dots], idx, width=p.shape[1])
+        p = np.pad(p, ((0, 0), (0, n.shape[1] - p.shape[1])))
+        out = to_host(cg.pncounter.lub_many(to_dev(np.concatenate([p, n], axis=1))))
+        A = p.shape[1]
+        dst.p.inner.dots = intern.dense_to_clocks(out[None, :A], idx)[0]
+        dst.n.inner.dots = intern.dense_to_clocks(out[None, A:], idx)[0]
+        return dst
+    if kind == "gset":
+        idx = intern.Index()
+        bm = intern.sets_to_bitmap([dst.value, src.value], idx)
+        out = to_host(cg.gset.lub_many(to_dev(bm)))
+        dst.value = intern.bitmap_to_sets(out[None, :], idx)[0]
+        return dst
+    if kind == "lwwreg":
+        vals = intern.Index([dst.val, src.val])
+        m = to_dev(np.array([dst.marker, src.marker], dtype=np.uint64))
+        v = to_dev(np.array([vals.pos[dst.val], vals.pos[src.val]], dtype=np.uint64))
+        conflict = cg.lwwreg.merge_batch(m[:1].clone(), v[:1].clone(), m[1:], v[1:])
+        if int(conflict.cpu()[0]):
+            raise O.ConflictingMarker()
+        res = cg.lwwreg.lub_many(m, v)
+        dst.marker, dst.val = int(to_host(res.marker)), vals.ids[int(to_host(res.val))]
+        return dst
+    if kind == "orswot":
+        return gpu_orswot_merge(dst, src)
+    raise TypeError(kind)
+
+
+def gpu_orswot_merge(dst: O.Orswot, src: O.Orswot) -> O.Orswot:
+    actors, members = intern.Index(), intern.Index()
+    states = [dst, src]
+    for s in states:
+        for a in s.clock.dots:
+            actors.intern(a)
+        for m, c in s.entries.items():
+            members.intern(m)
+            for a in c.dots:
+                actors.intern(a)
+        for k, ms in s.deferred.items():
+            for a in k.dots:
+                actors.intern(a)
+            for m in ms:
+                members.intern(m)
+    A, M = max(1, len(actors)), max(1, len(members))
+    Mw = (M + 63) // 64
+    clock = np.zeros((2, A), dtype=np.uint64)
+    entries = np.zeros((2, M, A), dtype=np.uint64)
+    dcl, dmem = [], []
+    for r, s in enumerate(states):
+        for a, v in s.clock.dots.items():
+            clock[r, actors.pos[a]] = v
+        for m, c in s.entries.items():
+            for a, v in c.dots.items():
+                entries[r, members.pos[m], actors.pos[a]] = v
+        for k, ms in s.deferred.items():
+            row = np.zeros(A, dtype=np.uint64)
+            for a, v in k.dots.items():
+                row[actors.pos[a]] = v
+            bits = np.zeros(Mw, dtype=np.uint64)
+            for m in ms:
+                p = members.pos[m]
+                bits[p // 64] |= np.uint64(1) << np.uint64(p % 64)
+            dcl.append(row)
+            dmem.append(bits)
+    D = len(dcl)
+    kw = {}
+    if D:
+        kw = dict(def_off=[0, D], def_clock=to_dev(np.stack(dcl)), def_members=to_dev(np.stack(dmem)))
+    res = cg.orswot.lub_many(to_dev(clock), to_dev(entries), **kw)
+    c, e = to_host(res.clock), to_host(res.entries)
+    out = O.Orswot()
+    out.clock = O.VClock({actors.ids[a]: int(v) for a, v in enumerate(c) if v and a < len(actors)})
+    for m in range(len(members)):
+        row = e[m]
+        if row.any():
+            out.entries[members.ids[m]] = O.VClock({actors.ids[a]: int(v) for a, v in enumerate(row) if v})
+    if D:
+        for rm, ms in cg.orswot.deferred_set(kw["def_clock"], res.def_keep, res.def_members):
+            k = O.VClock({actors.ids[a]: v for a, v in enumerate(rm) if v})
+            out.deferred[k] = {members.ids[m] for m in ms}
+    return out
+
+
+CASES = [c for f in ("kat_vclock.json", "kat_counters.json", "kat_orswot.json")
+         for c in K.load_cases(f) if any(s[0] in ("merge", "merge_err") for s in c["steps"])]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
+def test_kat_gpu(gpu_ctx, case):
+    K.run_case(case, merge_hook=gpu_merge)

@@ -1,0 +1,83 @@
+"""GPU parity: Orswot lub_many vs the oracle fold (reference semantics incl. deferred removes)."""
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+from gpu_util import to_dev, to_host
+
+pytestmark = pytest.mark.gpu
+
+import crdts_gpu as cg  # noqa: E402
+
+
+def _run(gpu_ctx, clock, entries, off, dcl, dmem):
+    R, M, A = entries.shape
+    D = dcl.shape[0]
+    kw = {}
+    if D:
+        kw = dict(def_off=[0, D], def_clock=to_dev(dcl), def_members=to_dev(dmem))
+    res = cg.orswot.lub_many(to_dev(clock), to_dev(entries), ctx=gpu_ctx, **kw)
+    c, e = to_host(res.clock), to_host(res.entries)
+    d = cg.orswot.deferred_set(kw["def_clock"], res.def_keep, res.def_members) if D else set()
+    return c, e, d
+
+
+@pytest.mark.parametrize("seed,R,M,A", [(1, 1, 1, 1), (2, 2, 5, 3), (3, 9, 40, 6), (4, 33, 64, 8),
+                                        (5, 64, 200, 16), (6, 300, 128, 64), (7, 20, 70, 33),
+                                        (8, 1000, 16, 4)])
+def test_orswot_lub_many(gpu_ctx, seed, R, M, A):
+    clock, entries, off, dcl, dmem = O.gen_orswot(seed, R, M, A, kmax=16)
+    oc, oe, odef, _ = O.orswot_fold(clock, entries, off, dcl, dmem)
+    c, e, d = _run(gpu_ctx, clock, entries, off, dcl, dmem)
+    np.testing.assert_array_equal(c, oc)
+    np.testing.assert_array_equal(e, oe)
+    assert d == odef
+
+
+def test_orswot_groups(gpu_ctx):
+    G, R, M, A = 3, 12, 50, 8
+    parts = [O.gen_orswot(40 + g, R, M, A, kmax=10) for g in range(G)]
+    clock = np.stack([p[0] for p in parts])
+    entries = np.stack([p[1] for p in parts])
+    dcl = np.concatenate([p[3] for p in parts])
+    dmem = np.concatenate([p[4] for p in parts])
+    off = np.cumsum([0] + [p[3].shape[0] for p in parts])
+    res = cg.orswot.lub_many(to_dev(clock), to_dev(entries), def_off=off, def_clock=to_dev(dcl),
+                             def_members=to_dev(dmem), ctx=gpu_ctx)
+    gc, ge = to_host(res.clock), to_host(res.entries)
+    for g, p in enumerate(parts):
+        oc, oe, odef, _ = O.orswot_fold(*p)
+        np.testing.assert_array_equal(gc[g], oc)
+        np.testing.assert_array_equal(ge[g], oe)
+        got = cg.orswot.deferred_set(to_dev(dcl), res.def_keep, res.def_members, int(off[g]), int(off[g + 1]))
+        assert got == odef
+
+
+def test_orswot_duplicate_deferred_union(gpu_ctx):
+    """Two replicas holding the same future rm clock over different members: one survivor with
+    the union of the member sets (orswot.rs:242-246)."""
+    A, M = 4, 8
+    clock = np.array([[1, 0, 0, 0], [0, 2, 0, 0]], dtype=np.uint64)
+    entries = np.zeros((2, M, A), dtype=np.uint64)
+    entries[0, 1, 0] = 1
+    entries[1, 2, 1] = 2
+    rm = np.array([0, 0, 5, 0], dtype=np.uint64)
+    dcl = np.stack([rm, rm, np.array([1, 1, 0, 0], dtype=np.uint64)])
+    dmem = np.array([[1 << 3], [1 << 4], [1 << 1]], dtype=np.uint64)
+    off = np.array([0, 1, 3], dtype=np.uint64)
+    oc, oe, odef, _ = O.orswot_fold(clock, entries, off, dcl, dmem)
+    c, e, d = _run(gpu_ctx, clock, entries, off, dcl, dmem)
+    assert d == odef == {((0, 0, 5, 0), frozenset({3, 4}))}
+    np.testing.assert_array_equal(e, oe)
+
+
+def test_orswot_empty_and_idempotent(gpu_ctx):
+    clock, entries, off, dcl, dmem = O.gen_orswot(9, 10, 30, 6, kmax=8, p_def=0.0)
+    res = cg.orswot.lub_many(to_dev(clock), to_dev(entries), ctx=gpu_ctx)
+    # lub of the lub with itself (and with the inputs again) changes nothing
+    twice = cg.orswot.lub_many(torch.stack([res.clock, res.clock]), torch.stack([res.entries, res.entries]), ctx=gpu_ctx)
+    assert torch.equal(twice.clock, res.clock) and torch.equal(twice.entries, res.entries)
+    none = cg.orswot.lub_many(torch.empty((0, 6), dtype=torch.int64, device="cuda:0"),
+                              torch.empty((0, 30, 6), dtype=torch.int64, device="cuda:0"), ctx=gpu_ctx)
+    assert int(none.clock.abs().sum()) == 0 and int(none.entries.abs().sum()) == 0

@@ -1,0 +1,159 @@
+"""Cross-check the two oracle twins (pure Python vs C++ ref_fold.cpp) and the dense
+restatements of the merge against the reference-semantics fold (CPU only)."""
+import numpy as np
+import pytest
+
+import oracle as O
+
+
+def py_vclock_fold(rows):
+    acc = O.VClock()
+    for row in rows:
+        acc.merge(O.VClock({a: int(v) for a, v in enumerate(row) if v}))
+    out = np.zeros(rows.shape[1], dtype=np.uint64)
+    for a, v in acc.dots.items():
+        out[a] = v
+    return out
+
+
+@pytest.mark.parametrize("R,A,seed", [(1, 1, 1), (7, 5, 2), (64, 16, 3), (300, 64, 4)])
+def test_vclock_fold_twins(R, A, seed):
+    rows = O.synth_matrix(seed, R, A, 0)
+    got, _ = O.vclock_fold(rows)
+    np.testing.assert_array_equal(got, py_vclock_fold(rows))
+    np.testing.assert_array_equal(got, rows.max(axis=0))  # dense restatement a2
+
+
+def test_pncounter_fold_twins():
+    rows = O.synth_matrix(9, 50, 2 * 12, 0)
+    got, _ = O.pncounter_fold(rows)
+    exp = np.concatenate([py_vclock_fold(rows[:, :12]), py_vclock_fold(rows[:, 12:])])
+    np.testing.assert_array_equal(got, exp)
+
+
+def test_gset_fold_twins():
+    rows = O.synth_matrix(5, 40, 3, 1)
+    got, _ = O.gset_fold(rows)
+    acc = O.GSet()
+    for row in rows:
+        s = O.GSet(O.bitmap_members(row))
+        acc.merge(s)
+    np.testing.assert_array_equal(got, np.bitwise_or.reduce(rows, axis=0))
+    assert O.bitmap_members(got) == frozenset(acc.value)
+
+
+def test_lwwreg_fold_twins():
+    R = 500
+    m = O.synth_matrix(3, 1, R, 2)[0] % np.uint64(40)
+    v = O.synth_matrix(3, 1, R, 3)[0] % np.uint64(3)
+    om, ov, fc, _ = O.lwwreg_fold(m, v)
+    acc = O.LWWReg(int(v[0]), int(m[0]))
+    first = 2**64 - 1
+    for i in range(1, R):
+        try:
+            acc.merge(O.LWWReg(int(v[i]), int(m[i])))
+        except O.ConflictingMarker:
+            first = min(first, i)
+    assert (om, ov, fc) == (acc.marker, acc.val, first)
+
+
+def py_orswot_from_dense(clock, entries, dcl, dmem):
+    o = O.Orswot()
+    o.clock = O.VClock({a: int(v) for a, v in enumerate(clock) if v})
+    for m in range(entries.shape[0]):
+        e = O.VClock({a: int(v) for a, v in enumerate(entries[m]) if v})
+        if not e.is_empty():
+            o.entries[m] = e
+    for rm, bits in zip(dcl, dmem):
+        k = O.VClock({a: int(v) for a, v in enumerate(rm) if v})
+        o.deferred.setdefault(k, set()).update(O.bitmap_members(bits))
+    return o
+
+
+def dense_orswot_join_fold(clock, entries):
+    """e = max(e1==e2?e1:0, e1>c2?e1:0, e2>c1?e2:0), c = max — as a left fold."""
+    e = np.zeros(entries.shape[1:], dtype=np.uint64)
+    c = np.zeros(clock.shape[1], dtype=np.uint64)
+    for r in range(entries.shape[0]):
+        e2, c2 = entries[r], clock[r]
+        t0 = np.where(e == e2, e, 0)
+        t1 = np.where(e > c2, e, 0)
+        t2 = np.where(e2 > c, e2, 0)
+        e = np.maximum(t0, np.maximum(t1, t2)).astype(np.uint64)
+        c = np.maximum(c, c2)
+    return c, e
+
+
+def dense_orswot_lub(clock, entries, def_off, def_clock, def_members):
+    c, e = dense_orswot_join_fold(clock, entries)
+    M = e.shape[0]
+    surv = {}
+    for d in range(def_clock.shape[0]):
+        rm = def_clock[d]
+        ms = O.bitmap_members(def_members[d])
+        for m in ms:
+            e[m] = np.where(e[m] > rm, e[m], 0)
+        if np.any(rm > c):
+            surv.setdefault(tuple(int(x) for x in rm), set()).update(ms)
+    return c, e, {(k, frozenset(v)) for k, v in surv.items()}
+
+
+@pytest.mark.parametrize("seed,R,M,A", [(1, 2, 5, 3), (2, 5, 16, 4), (3, 9, 40, 6), (4, 24, 70, 8)])
+def test_orswot_fold_twins(seed, R, M, A):
+    clock, entries, off, dcl, dmem = O.gen_orswot(seed, R, M, A, kmax=12)
+    oc, oe, odef, _ = O.orswot_fold(clock, entries, off, dcl, dmem)
+    # pure-Python twin
+    acc = O.Orswot()
+    for r in range(R):
+        lo, hi = int(off[r]), int(off[r + 1])
+        acc.merge(py_orswot_from_dense(clock[r], entries[r], dcl[lo:hi], dmem[lo:hi]))
+    assert {m: c.dots for m, c in acc.entries.items()} == {
+        m: {a: int(v) for a, v in enumerate(oe[m]) if v} for m in range(M) if oe[m].any()}
+    assert acc.clock.dots == {a: int(v) for a, v in enumerate(oc) if v}
+    pyd = {(tuple(acc_k.get(a) for a in range(A)), frozenset(v)) for acc_k, v in acc.deferred.items()}
+    assert pyd == odef
+    # dense restatement used by the kernels (join fold + ceiling + survival + dedup)
+    dc, de, ddef = dense_orswot_lub(clock, entries, off, dcl, dmem)
+    np.testing.assert_array_equal(dc, oc)
+    np.testing.assert_array_equal(de, oe)
+    assert ddef == odef
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_orswot_tree_equals_left_fold(seed):
+    """The kernels reduce replicas as a tree; on well-formed inputs this must equal the fold."""
+    clock, entries, off, dcl, dmem = O.gen_orswot(100 + seed, 16, 24, 5, kmax=10)
+    c1, e1 = dense_orswot_join_fold(clock, entries)
+    # tree: fold two halves independently, then join the partial states
+    ca, ea = dense_orswot_join_fold(clock[:7], entries[:7])
+    cb, eb = dense_orswot_join_fold(clock[7:], entries[7:])
+    c2, e2 = dense_orswot_join_fold(np.stack([ca, cb]), np.stack([ea, eb]))
+    np.testing.assert_array_equal(c1, c2)
+    np.testing.assert_array_equal(e1, e2)
+
+
+def test_orswot_witness_convergence():
+    """prop_merge_converges (test/orswot.rs:33-68): ops routed by actor % i to i witnesses,
+    folded from new(), converge for every i in 2..11 — oracle check with a fixed op list."""
+    rng = np.random.default_rng(7)
+    ops = []
+    counters = {}
+    for _ in range(60):
+        actor = int(rng.integers(0, 11))
+        members = set(int(x) for x in rng.integers(0, 8, size=int(rng.integers(1, 3))))
+        if rng.random() < 0.6:
+            counters[actor] = counters.get(actor, 0) + 1
+            ops.append((actor, O.OrswotAdd(O.Dot(actor, counters[actor]), members)))
+        else:
+            ops.append((actor, O.OrswotRm(O.VClock({actor: int(rng.integers(1, 6))}), members)))
+    result = None
+    for i in range(2, 11):
+        w = [O.Orswot() for _ in range(i)]
+        for actor, op in ops:
+            w[actor % i].apply(op)
+        merged = O.Orswot()
+        for x in w:
+            merged.merge(x)
+        if result is None:
+            result = merged
+        assert merged == result
