@@ -558,7 +558,7 @@ def gen_orswot(seed: int, R: int, M: int, A: int, kmax: int = 24, p_def: float =
             # some removes carry a past (dominated) context on other actors
             back = (rng.random(A) < 0.3) & ~fut
             rm[back] = rm[back] // np.uint64(2)
-            ms = rng.choice(M, size=int(rng.integers(1, 4)), replace=False)
+            ms = rng.choice(M, size=min(M, int(rng.integers(1, 4))), replace=False)
             bits = np.zeros(Mw, dtype=np.uint64)
             for m in ms:
                 bits[m // 64] |= np.uint64(1) << np.uint64(m % 64)

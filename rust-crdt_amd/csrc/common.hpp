@@ -26,6 +26,16 @@ struct KernelTimer {
   uint64_t launches = 0;
 };
 
+// Launch-geometry knobs (defaults chosen by measurement).  Overridable for
+// tuning runs through the environment variable CRDT_TUNE="key=value,..." read at ctx create.
+struct Tune {
+  int lub_blocks_per_cu = 8;
+  int lub_min_steps = 16;
+  int lub_interleave = 1;
+  int lub_unroll = 8;
+  int lub_nt = 1;
+};
+
 struct PendingTiming {
   std::string name;
   hipEvent_t start, stop;
@@ -38,6 +48,7 @@ struct crdt_ctx {
   hipStream_t stream = nullptr;
   int cu_count = 256;
   bool timing = false;
+  crdt::Tune tune;
   std::string last_error;
   // Device scratch (grown on demand, never shrunk; freed in destroy).
   void *scratch = nullptr;

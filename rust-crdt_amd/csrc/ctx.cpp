@@ -1,5 +1,6 @@
 // Context lifecycle, error reporting, scratch and event timing for libcrdt_gpu.
 #include <cstdarg>
+#include <cstdlib>
 
 #include "common.hpp"
 
@@ -108,6 +109,26 @@ int crdt_ctx_create(int device, crdt_ctx **out) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     ctx->cu_count = prop.multiProcessorCount;
+  if (const char *t = getenv("CRDT_TUNE")) {
+    std::string spec(t);
+    size_t pos = 0;
+    while (pos < spec.size()) {
+      size_t end = spec.find(',', pos);
+      if (end == std::string::npos) end = spec.size();
+      std::string kv = spec.substr(pos, end - pos);
+      size_t eq = kv.find('=');
+      if (eq != std::string::npos) {
+        std::string k = kv.substr(0, eq);
+        int v = atoi(kv.c_str() + eq + 1);
+        if (k == "bpc" && v > 0) ctx->tune.lub_blocks_per_cu = v;
+        else if (k == "minsteps" && v > 0) ctx->tune.lub_min_steps = v;
+        else if (k == "interleave") ctx->tune.lub_interleave = v != 0;
+        else if (k == "unroll" && (v == 4 || v == 8 || v == 16)) ctx->tune.lub_unroll = v;
+        else if (k == "nt") ctx->tune.lub_nt = v != 0;
+      }
+      pos = end + 1;
+    }
+  }
   *out = ctx;
   return CRDT_OK;
 }

@@ -93,6 +93,7 @@ struct LubPlan {
   unsigned long long R, Rs;
   int Wv, PW, TR, ncolblk, S, CL, ncl;
   int accumulate;
+  int interleave;  // 1: slice s takes row-steps s, s+S, s+2S, ... (all slices sweep HBM together)
 };
 
 template <Op OP, typename VT>
@@ -126,7 +127,7 @@ __device__ __forceinline__ bool arrive_last(unsigned *counter, unsigned expected
 }
 
 // One launch = the whole lub.  Block b -> (unit u = g*ncolblk + cb, slice s).
-template <Op OP, int V, int U>
+template <Op OP, int V, int U, bool NT = true>
 __global__ __launch_bounds__(kBlock) void lub_stream_kernel(LubPlan p) {
   using VT = typename VecOf<V>::T;
   __shared__ VT red[kBlock];
@@ -144,13 +145,21 @@ __global__ __launch_bounds__(kBlock) void lub_stream_kernel(LubPlan p) {
 
   VT acc = vzero<VT>();
   if (active) {
-    const unsigned long long rbeg = (unsigned long long)s * p.Rs;
-    const unsigned long long rend = min(p.R, rbeg + p.Rs);
-    const unsigned long long r0 = rbeg + rsub;
+    unsigned long long r0, rend, rstep;
+    if (p.interleave) {
+      r0 = (unsigned long long)s * p.TR + rsub;
+      rend = p.R;
+      rstep = (unsigned long long)p.S * p.TR;
+    } else {
+      const unsigned long long rbeg = (unsigned long long)s * p.Rs;
+      rend = min(p.R, rbeg + p.Rs);
+      r0 = rbeg + rsub;
+      rstep = p.TR;
+    }
     if (r0 < rend) {
-      const size_t n = (rend - r0 + p.TR - 1) / p.TR;
+      const size_t n = (rend - r0 + rstep - 1) / rstep;
       const VT *src = reinterpret_cast<const VT *>(p.in + g * p.gstride + r0 * p.rstride) + col;
-      acc = fold_rows<OP, VT, U, true>(src, n, (long long)p.TR * p.rstride / V);
+      acc = fold_rows<OP, VT, U, NT>(src, n, (long long)rstep * p.rstride / V);
     }
   }
   acc = block_rows_combine<OP>(acc, red, l, p.PW, p.TR);
@@ -263,14 +272,14 @@ int lattice_lub_many(crdt_ctx *ctx, Op op, const u64 *in, size_t G, size_t R, si
   p.ncolblk = (p.Wv + kBlock - 1) / kBlock;
   p.accumulate = accumulate ? 1 : 0;
 
-  // Slice replicas so the grid holds ~8 workgroups per CU, each thread folding >= 16 rows.
+  // Slice replicas so the grid holds ~bpc workgroups per CU, each thread folding >= min_steps rows.
   const size_t units = G * (size_t)p.ncolblk;
-  const size_t target = (size_t)ctx->cu_count * 8;
+  const size_t target = (size_t)ctx->cu_count * ctx->tune.lub_blocks_per_cu;
   const size_t steps = (R + p.TR - 1) / p.TR;
   size_t S = 1;
   if (units < target) {
     S = (target + units - 1) / units;
-    size_t max_s = steps / 16;
+    size_t max_s = steps / ctx->tune.lub_min_steps;
     if (max_s < 1) max_s = 1;
     if (S > max_s) S = max_s;
   }
@@ -281,6 +290,7 @@ int lattice_lub_many(crdt_ctx *ctx, Op op, const u64 *in, size_t G, size_t R, si
     return fail(ctx, CRDT_EUNSUPPORTED, "lub_many: grid too large (%zu units x %zu slices)", units, S);
   p.S = (int)S;
   p.Rs = Rs;
+  p.interleave = ctx->tune.lub_interleave;
   p.CL = 32;
   p.ncl = (p.S + p.CL - 1) / p.CL;
 
@@ -301,13 +311,21 @@ int lattice_lub_many(crdt_ctx *ctx, Op op, const u64 *in, size_t G, size_t R, si
 
   const dim3 grid((unsigned)(units * S));
   timing_begin(ctx, "lub_stream");
+  const int U = ctx->tune.lub_unroll;
+#define CRDT_LAUNCH_LUB(OPV, VV, UV) \
+  hipLaunchKernelGGL((lub_stream_kernel<OPV, VV, UV>), grid, dim3(kBlock), 0, ctx->stream, p)
   if (op == Op::Max) {
-    if (V == 2) hipLaunchKernelGGL((lub_stream_kernel<Op::Max, 2, 8>), grid, dim3(kBlock), 0, ctx->stream, p);
-    else hipLaunchKernelGGL((lub_stream_kernel<Op::Max, 1, 8>), grid, dim3(kBlock), 0, ctx->stream, p);
+    if (V == 2) {
+      if (!ctx->tune.lub_nt) hipLaunchKernelGGL((lub_stream_kernel<Op::Max, 2, 8, false>), grid, dim3(kBlock), 0, ctx->stream, p);
+      else if (U == 4) CRDT_LAUNCH_LUB(Op::Max, 2, 4);
+      else if (U == 16) CRDT_LAUNCH_LUB(Op::Max, 2, 16);
+      else CRDT_LAUNCH_LUB(Op::Max, 2, 8);
+    } else CRDT_LAUNCH_LUB(Op::Max, 1, 8);
   } else {
-    if (V == 2) hipLaunchKernelGGL((lub_stream_kernel<Op::Or, 2, 8>), grid, dim3(kBlock), 0, ctx->stream, p);
-    else hipLaunchKernelGGL((lub_stream_kernel<Op::Or, 1, 8>), grid, dim3(kBlock), 0, ctx->stream, p);
+    if (V == 2) CRDT_LAUNCH_LUB(Op::Or, 2, 8);
+    else CRDT_LAUNCH_LUB(Op::Or, 1, 8);
   }
+#undef CRDT_LAUNCH_LUB
   timing_end(ctx);
   CRDT_HIP(ctx, hipGetLastError());
   return CRDT_OK;
