@@ -29,9 +29,10 @@ struct KernelTimer {
 // Launch-geometry knobs (defaults chosen by measurement).  Overridable for
 // tuning runs through the environment variable CRDT_TUNE="key=value,..." read at ctx create.
 struct Tune {
-  int lub_blocks_per_cu = 8;
+  int lub_blocks_per_cu = 1;
+  int lub_grid = 0;  // >0: total workgroups target (overrides lub_blocks_per_cu)
   int lub_min_steps = 16;
-  int lub_interleave = 1;
+  int lub_interleave = 0;
   int lub_unroll = 8;
   int lub_nt = 1;
 };
@@ -53,6 +54,10 @@ struct crdt_ctx {
   // Device scratch (grown on demand, never shrunk; freed in destroy).
   void *scratch = nullptr;
   size_t scratch_bytes = 0;
+  // Arrival counters of the last-arriver combines: a dedicated region that is zero between
+  // calls (kernels reset every counter they use), never shared with scratch.
+  unsigned *counters = nullptr;
+  size_t counters_n = 0;
   std::map<std::string, crdt::KernelTimer> timers;
   std::vector<crdt::PendingTiming> pending;
   std::vector<hipEvent_t> free_events;
@@ -64,6 +69,8 @@ int fail(crdt_ctx *ctx, int code, const char *fmt, ...);
 int hip_fail(crdt_ctx *ctx, hipError_t e, const char *what);
 // Ensure ctx->scratch holds at least `bytes`; returns CRDT_OK or CRDT_ENOMEM.
 int ensure_scratch(crdt_ctx *ctx, size_t bytes);
+// Ensure ctx->counters holds at least n zeroed counters.
+int ensure_counters(crdt_ctx *ctx, size_t n);
 // Bracket the dominant kernel of a call with events when timing is on.
 void timing_begin(crdt_ctx *ctx, const char *name);
 void timing_end(crdt_ctx *ctx);

@@ -39,10 +39,26 @@ int ensure_scratch(crdt_ctx *ctx, size_t bytes) {
     return fail(ctx, CRDT_ENOMEM, "scratch hipMalloc(%zu) failed: %s", want, hipGetErrorString(e));
   }
   ctx->scratch_bytes = want;
-  // Arrival counters live at the front of scratch and must start at zero (kernels that use
-  // them reset them to zero when they finish).
-  e = hipMemsetAsync(ctx->scratch, 0, want, ctx->stream);
-  if (e != hipSuccess) return hip_fail(ctx, e, "hipMemsetAsync(scratch)");
+  return CRDT_OK;
+}
+
+int ensure_counters(crdt_ctx *ctx, size_t n) {
+  if (n <= ctx->counters_n) return CRDT_OK;
+  if (ctx->counters) {
+    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipFree(ctx->counters);
+    ctx->counters = nullptr;
+    ctx->counters_n = 0;
+  }
+  size_t want = n < 16384 ? 16384 : n * 2;
+  hipError_t e = hipMalloc(&ctx->counters, want * sizeof(unsigned));
+  if (e != hipSuccess) {
+    ctx->counters = nullptr;
+    return fail(ctx, CRDT_ENOMEM, "counter hipMalloc failed: %s", hipGetErrorString(e));
+  }
+  e = hipMemsetAsync(ctx->counters, 0, want * sizeof(unsigned), ctx->stream);
+  if (e != hipSuccess) return hip_fail(ctx, e, "hipMemsetAsync(counters)");
+  ctx->counters_n = want;
   return CRDT_OK;
 }
 
@@ -123,8 +139,9 @@ int crdt_ctx_create(int device, crdt_ctx **out) {
         if (k == "bpc" && v > 0) ctx->tune.lub_blocks_per_cu = v;
         else if (k == "minsteps" && v > 0) ctx->tune.lub_min_steps = v;
         else if (k == "interleave") ctx->tune.lub_interleave = v != 0;
-        else if (k == "unroll" && (v == 4 || v == 8 || v == 16)) ctx->tune.lub_unroll = v;
+        else if (k == "unroll" && (v == 4 || v == 8 || v == 16 || v == 32)) ctx->tune.lub_unroll = v;
         else if (k == "nt") ctx->tune.lub_nt = v != 0;
+        else if (k == "grid" && v > 0) ctx->tune.lub_grid = v;
       }
       pos = end + 1;
     }
@@ -143,6 +160,7 @@ int crdt_ctx_destroy(crdt_ctx *ctx) {
   }
   for (auto e : ctx->free_events) (void)hipEventDestroy(e);
   if (ctx->scratch) (void)hipFree(ctx->scratch);
+  if (ctx->counters) (void)hipFree(ctx->counters);
   delete ctx;
   return CRDT_OK;
 }

@@ -274,7 +274,8 @@ int lattice_lub_many(crdt_ctx *ctx, Op op, const u64 *in, size_t G, size_t R, si
 
   // Slice replicas so the grid holds ~bpc workgroups per CU, each thread folding >= min_steps rows.
   const size_t units = G * (size_t)p.ncolblk;
-  const size_t target = (size_t)ctx->cu_count * ctx->tune.lub_blocks_per_cu;
+  const size_t target = ctx->tune.lub_grid > 0 ? (size_t)ctx->tune.lub_grid
+                                               : (size_t)ctx->cu_count * ctx->tune.lub_blocks_per_cu;
   const size_t steps = (R + p.TR - 1) / p.TR;
   size_t S = 1;
   if (units < target) {
@@ -298,15 +299,15 @@ int lattice_lub_many(crdt_ctx *ctx, Op op, const u64 *in, size_t G, size_t R, si
     const size_t vecb = (size_t)V * 8;
     const size_t part_b = units * S * p.PW * vecb;
     const size_t cpart_b = units * p.ncl * p.PW * vecb;
-    const size_t cnt_b = (units * p.ncl + units) * sizeof(unsigned);
-    const size_t cnt_pad = (cnt_b + 255) / 256 * 256;
-    int rc = ensure_scratch(ctx, cnt_pad + part_b + cpart_b);
+    int rc = ensure_scratch(ctx, part_b + cpart_b);
+    if (rc) return rc;
+    rc = ensure_counters(ctx, units * p.ncl + units);
     if (rc) return rc;
     char *base = static_cast<char *>(ctx->scratch);
-    p.cnt1 = reinterpret_cast<unsigned *>(base);
+    p.cnt1 = ctx->counters;
     p.cnt2 = p.cnt1 + units * p.ncl;
-    p.part = reinterpret_cast<u64 *>(base + cnt_pad);
-    p.cpart = reinterpret_cast<u64 *>(base + cnt_pad + part_b);
+    p.part = reinterpret_cast<u64 *>(base);
+    p.cpart = reinterpret_cast<u64 *>(base + part_b);
   }
 
   const dim3 grid((unsigned)(units * S));
@@ -319,6 +320,7 @@ int lattice_lub_many(crdt_ctx *ctx, Op op, const u64 *in, size_t G, size_t R, si
       if (!ctx->tune.lub_nt) hipLaunchKernelGGL((lub_stream_kernel<Op::Max, 2, 8, false>), grid, dim3(kBlock), 0, ctx->stream, p);
       else if (U == 4) CRDT_LAUNCH_LUB(Op::Max, 2, 4);
       else if (U == 16) CRDT_LAUNCH_LUB(Op::Max, 2, 16);
+      else if (U == 32) CRDT_LAUNCH_LUB(Op::Max, 2, 32);
       else CRDT_LAUNCH_LUB(Op::Max, 2, 8);
     } else CRDT_LAUNCH_LUB(Op::Max, 1, 8);
   } else {

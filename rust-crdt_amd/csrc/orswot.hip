@@ -339,11 +339,12 @@ extern "C" int crdt_orswot_lub_many(crdt_ctx *ctx, const crdt_orswot_batch *in,
     if (units * S > 0x7fffffffULL) return fail(ctx, CRDT_EUNSUPPORTED, "orswot_lub_many: grid too large");
     if (S > 1) {
       const size_t slab_b = (mpb * p.PW + p.PW) * V * 8;
-      const size_t cnt_pad = (units * sizeof(unsigned) + 255) / 256 * 256;
-      int rc = ensure_scratch(ctx, cnt_pad + units * S * slab_b);
+      int rc = ensure_scratch(ctx, units * S * slab_b);
       if (rc) return rc;
-      p.cnt = static_cast<unsigned *>(ctx->scratch);
-      p.part = reinterpret_cast<u64 *>(static_cast<char *>(ctx->scratch) + cnt_pad);
+      rc = ensure_counters(ctx, units);
+      if (rc) return rc;
+      p.cnt = ctx->counters;
+      p.part = reinterpret_cast<u64 *>(ctx->scratch);
     }
     timing_begin(ctx, "orswot_join");
     if (V == 2) hipLaunchKernelGGL((orswot_join_kernel<2>), dim3((unsigned)(units * S)), dim3(kBlock), 0, ctx->stream, p);
