@@ -167,6 +167,20 @@ int crdt_orswot_lub_many(crdt_ctx *ctx, const crdt_orswot_batch *in, crdt_orswot
 int crdt_synth_fill(crdt_ctx *ctx, uint64_t *out, size_t rows, size_t width, size_t row_stride,
                     size_t first_row, uint64_t seed, int kind);
 
+/* Well-formed synthetic Orswot replicas, packed clock[R][A] and entries[R][M][A] (replica r is
+ * global replica first_row + r).  clock[r][a] = synth(seed, r*A + a) % (kmax + 1); actor a's
+ * k-th add targets member (a*P + k) mod M (P = 0x9E3779B1 mod M), so a dot is unique and
+ * entries[r][m][a] = k <= clock[r][a] or 0; a quarter of the cells are observed removes (0).
+ * Requires kmax < M.  Restated on the CPU by oracle.synth_orswot. */
+int crdt_synth_orswot(crdt_ctx *ctx, uint64_t *clock, uint64_t *entries, size_t R, size_t M,
+                      size_t A, size_t first_row, uint64_t seed, uint64_t kmax);
+/* For each deferred remove d held by replica def_row[d] (rm clock def_clock[d*A..], member
+ * bitmap def_members[d*Mw..]): forget(rm) on those members of that replica's entries — the
+ * state apply_rm (orswot.rs:230-238) leaves behind.  Used to build consistent inputs. */
+int crdt_synth_orswot_rm(crdt_ctx *ctx, uint64_t *entries, size_t M, size_t A, size_t D,
+                         const uint32_t *def_row, const uint64_t *def_clock,
+                         const uint64_t *def_members);
+
 #ifdef __cplusplus
 }
 #endif

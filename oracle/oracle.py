@@ -398,6 +398,34 @@ def synth_matrix(seed: int, rows: int, width: int, kind: int, row0: int = 0) -> 
     return synth_values(seed, idx, kind).reshape(rows, width)
 
 
+def synth_orswot(seed: int, R: int, M: int, A: int, kmax: int, row0: int = 0):
+    """Restatement of crdt_synth_orswot for replicas [row0, row0+R): (clock (R,A), entries (R,M,A))."""
+    r = np.arange(row0, row0 + R, dtype=np.uint64)
+    a = np.arange(A, dtype=np.uint64)
+    m = np.arange(M, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        c = mix64(np.uint64(seed) + (r[:, None] * np.uint64(A) + a[None, :] + np.uint64(1)) * _GOLD)
+    c = c % np.uint64(kmax + 1)
+    pm = np.uint64(0x9E3779B1 % M)
+    k = (m[:, None] + np.uint64(M) - (a[None, :] * pm) % np.uint64(M)) % np.uint64(M)  # (M, A)
+    e = np.where((k[None] >= 1) & (k[None] <= c[:, None, :]), k[None], np.uint64(0))
+    cell = (r[:, None, None] * np.uint64(M * A) + m[None, :, None] * np.uint64(A) + a[None, None, :])
+    with np.errstate(over="ignore"):
+        obs = (mix64(np.uint64(0xD1B54A32D192ED03) + cell) & np.uint64(3)) == 0
+    e = np.where(obs, np.uint64(0), e).astype(np.uint64)
+    return c.astype(np.uint64), e
+
+
+def apply_rm_rows(entries: np.ndarray, rows, def_clock, def_members) -> np.ndarray:
+    """forget(rm) of each deferred on its own replica's listed members (apply_rm's entry part)."""
+    e = entries.copy()
+    for d, r in enumerate(rows):
+        for mm in bitmap_members(def_members[d]):
+            row = e[r, mm]
+            row[row <= def_clock[d]] = 0
+    return e
+
+
 # ---------------------------------------------------------------------------------------
 # ctypes access to the C++ twin
 # ---------------------------------------------------------------------------------------

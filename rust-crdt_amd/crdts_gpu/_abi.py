@@ -28,7 +28,7 @@ EXPORTS = (
     "crdt_pncounter_lub_many", "crdt_pncounter_merge_batch",
     "crdt_gset_lub_many", "crdt_gset_merge_batch",
     "crdt_lwwreg_lub_many", "crdt_lwwreg_merge_batch",
-    "crdt_orswot_lub_many", "crdt_synth_fill",
+    "crdt_orswot_lub_many", "crdt_synth_fill", "crdt_synth_orswot", "crdt_synth_orswot_rm",
 )
 
 
@@ -74,6 +74,8 @@ _SIGS = {
     "crdt_ctx_timing": ([P, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(U64)], ctypes.c_int),
     "crdt_ctx_timing_reset": ([P], ctypes.c_int),
     "crdt_synth_fill": ([P, P, S, S, S, S, U64, ctypes.c_int], ctypes.c_int),
+    "crdt_synth_orswot": ([P, P, P, S, S, S, S, U64, U64], ctypes.c_int),
+    "crdt_synth_orswot_rm": ([P, P, S, S, S, P, P, P], ctypes.c_int),
     "crdt_lwwreg_lub_many": ([P, P, P, S, S, S, P, P, P], ctypes.c_int),
     "crdt_lwwreg_merge_batch": ([P, P, P, P, P, S, P], ctypes.c_int),
     "crdt_orswot_lub_many": ([P, ctypes.POINTER(OrswotBatch), ctypes.POINTER(OrswotOut)], ctypes.c_int),

@@ -1,0 +1,91 @@
+"""Synthetic replica states for benchmarks and parity tests, generated in HBM.
+
+Counter-based (stateless hash) so the CPU can regenerate any sampled replica bit for bit
+(oracle.synth_* restates the formulas independently).  Formulas: include/crdt_gpu.h
+(crdt_synth_fill, crdt_synth_orswot).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import NamedTuple, Optional
+
+import numpy as np
+import torch
+
+from .context import Context, dptr, synth_fill  # noqa: F401
+
+_GOLD = np.uint64(0x9E3779B97F4A7C15)
+
+
+def _mix64(z):
+    z = np.asarray(z, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def orswot_clock_rows(seed: int, rows: np.ndarray, A: int, kmax: int) -> np.ndarray:
+    """clock[r][a] of crdt_synth_orswot for the given global replica indices (host)."""
+    rows = np.asarray(rows, dtype=np.uint64)
+    idx = rows[:, None] * np.uint64(A) + np.arange(A, dtype=np.uint64)[None, :]
+    with np.errstate(over="ignore"):
+        h = _mix64(np.uint64(seed) + (idx + np.uint64(1)) * _GOLD)
+    return h % np.uint64(kmax + 1)
+
+
+class OrswotInput(NamedTuple):
+    clock: torch.Tensor      # (R, A)
+    entries: torch.Tensor    # (R, M, A)
+    def_off: np.ndarray      # (R+1,) per replica CSR (host)
+    def_clock: torch.Tensor  # (D, A)
+    def_members: torch.Tensor  # (D, Mw)
+
+
+def orswot_deferred(seed: int, R: int, M: int, A: int, kmax: int, first_row: int = 0,
+                    p_def: float = 0.1, max_per_replica: int = 3):
+    """Host-side deferred removes for replicas [first_row, first_row+R): each replica holds one
+    to `max_per_replica` removes with probability p_def, each with a "future" context
+    (rm[a] = clock[a] + delta on ~10% of actors, at least one) over 1-3 members."""
+    rng = np.random.default_rng(seed ^ 0xDEF0 ^ (first_row * 0x9E37))
+    has = rng.random(R) < p_def
+    counts = np.where(has, rng.integers(1, max_per_replica + 1, size=R), 0)
+    off = np.concatenate([[0], np.cumsum(counts)]).astype(np.uint64)
+    D = int(off[-1])
+    Mw = (M + 63) // 64
+    rows = np.repeat(np.arange(R), counts)
+    base = orswot_clock_rows(seed, rows + first_row, A, kmax) if D else np.zeros((0, A), np.uint64)
+    fut = rng.random((D, A)) < 0.1
+    if D:
+        fut[np.arange(D), rng.integers(0, A, size=D)] = True
+    delta = rng.integers(1, 4, size=(D, A)).astype(np.uint64)
+    rm = np.where(fut, base + delta, base).astype(np.uint64)
+    members = np.zeros((D, Mw), dtype=np.uint64)
+    nm = rng.integers(1, 4, size=D)
+    for d in range(D):
+        for m in rng.choice(M, size=min(M, int(nm[d])), replace=False):
+            members[d, m // 64] |= np.uint64(1) << np.uint64(m % 64)
+    return off, rows.astype(np.uint32), rm, members
+
+
+def orswot_replicas(ctx: Optional[Context], R: int, M: int, A: int, seed: int, kmax: int = 48,
+                    first_row: int = 0, p_def: float = 0.1, device: Optional[torch.device] = None,
+                    entries: Optional[torch.Tensor] = None, clock: Optional[torch.Tensor] = None) -> OrswotInput:
+    """Generate R well-formed Orswot replicas in HBM, with deferred removes pre-applied."""
+    ctx = ctx or Context.default()
+    dev = device or torch.device("cuda", ctx.device)
+    if clock is None:
+        clock = torch.empty((R, A), dtype=torch.int64, device=dev)
+    if entries is None:
+        entries = torch.empty((R, M, A), dtype=torch.int64, device=dev)
+    ctx.call("crdt_synth_orswot", dptr(clock), dptr(entries), R, M, A, first_row,
+             ctypes.c_uint64(seed), ctypes.c_uint64(kmax))
+    off, rows, rm, members = orswot_deferred(seed, R, M, A, kmax, first_row, p_def)
+    D = rm.shape[0]
+    dcl = torch.from_numpy(rm.view(np.int64)).to(dev)
+    dmem = torch.from_numpy(members.view(np.int64)).to(dev)
+    if D:
+        drow = torch.from_numpy(rows.astype(np.int32)).to(dev)
+        ctx.call("crdt_synth_orswot_rm", dptr(entries), M, A, D, dptr(drow), dptr(dcl), dptr(dmem))
+        torch.cuda.current_stream(dev).synchronize()
+    return OrswotInput(clock, entries, off, dcl, dmem)

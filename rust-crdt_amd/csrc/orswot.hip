@@ -66,7 +66,7 @@ struct OrPlan {
   u64 *out_entries;  // [G][M][A]
 };
 
-template <int V>
+template <int V, int UR>
 __global__ __launch_bounds__(kBlock) void orswot_join_kernel(OrPlan p) {
   using VT = typename OVec<V>::T;
   __shared__ int s_flag;
@@ -101,7 +101,27 @@ __global__ __launch_bounds__(kBlock) void orswot_join_kernel(OrPlan p) {
     const long long cstep = p.c_rstride / V;
     const long long estep = p.e_rstride / V;
     const long long mstep = (long long)p.MB * p.e_mstride / V;
-    for (unsigned long long r = rbeg; r < rend; ++r) {
+    unsigned long long r = rbeg;
+    // UR replicas' loads in flight, then their joins in fold order.
+    for (; r + UR <= rend; r += UR) {
+      VT c2[UR], e2[UR][kOrMPT];
+#pragma unroll
+      for (int q = 0; q < UR; ++q) {
+        c2[q] = cp[q * cstep];
+#pragma unroll
+        for (int j = 0; j < kOrMPT; ++j)
+          e2[q][j] = mok[j] ? __builtin_nontemporal_load(ep + q * estep + j * mstep) : VT(0);
+      }
+#pragma unroll
+      for (int q = 0; q < UR; ++q) {
+#pragma unroll
+        for (int j = 0; j < kOrMPT; ++j) e[j] = dot_join(e[j], c, e2[q][j], c2[q]);
+        c = umax(c, c2[q]);
+      }
+      cp += UR * cstep;
+      ep += UR * estep;
+    }
+    for (; r < rend; ++r) {
       const VT c2 = *cp;
       VT e2[kOrMPT];
 #pragma unroll
@@ -323,7 +343,7 @@ extern "C" int crdt_orswot_lub_many(crdt_ctx *ctx, const crdt_orswot_batch *in,
     p.out_clock = (u64 *)out->clock;
     p.out_entries = (u64 *)out->entries;
     const size_t units = G * (size_t)p.nmblk * p.ncolblk;
-    const size_t target = (size_t)ctx->cu_count * 8;
+    const size_t target = (size_t)ctx->cu_count * ctx->tune.orswot_blocks_per_cu;
     size_t S = 1;
     if (units < target) {
       S = (target + units - 1) / units;
@@ -347,8 +367,15 @@ extern "C" int crdt_orswot_lub_many(crdt_ctx *ctx, const crdt_orswot_batch *in,
       p.part = reinterpret_cast<u64 *>(ctx->scratch);
     }
     timing_begin(ctx, "orswot_join");
-    if (V == 2) hipLaunchKernelGGL((orswot_join_kernel<2>), dim3((unsigned)(units * S)), dim3(kBlock), 0, ctx->stream, p);
-    else hipLaunchKernelGGL((orswot_join_kernel<1>), dim3((unsigned)(units * S)), dim3(kBlock), 0, ctx->stream, p);
+    const dim3 grid((unsigned)(units * S));
+    const int UR = ctx->tune.orswot_unroll;
+    if (V == 2) {
+      if (UR == 1) hipLaunchKernelGGL((orswot_join_kernel<2, 1>), grid, dim3(kBlock), 0, ctx->stream, p);
+      else if (UR == 4) hipLaunchKernelGGL((orswot_join_kernel<2, 4>), grid, dim3(kBlock), 0, ctx->stream, p);
+      else hipLaunchKernelGGL((orswot_join_kernel<2, 2>), grid, dim3(kBlock), 0, ctx->stream, p);
+    } else {
+      hipLaunchKernelGGL((orswot_join_kernel<1, 2>), grid, dim3(kBlock), 0, ctx->stream, p);
+    }
     timing_end(ctx);
     CRDT_HIP(ctx, hipGetLastError());
   }

@@ -73,3 +73,113 @@ extern "C" int crdt_synth_fill(crdt_ctx *ctx, uint64_t *out, size_t rows, size_t
   CRDT_HIP(ctx, hipGetLastError());
   return CRDT_OK;
 }
+
+// ---- Orswot replicas ----------------------------------------------------------------------
+// Well-formed by construction (the invariants the dot-store join relies on: every dot (a, k)
+// adds exactly one member, and every entry counter is <= the replica clock):
+//   clock[r][a]      = synth(seed, r*A + a) % (kmax + 1)
+//   actor a's k-th add targets member mem(a, k) = (a*P + k) mod M, so for member m the only
+//   candidate event is k(m, a) = (m - a*P) mod M (kmax < M keeps it unique);
+//   entries[r][m][a] = k(m, a) if 1 <= k(m, a) <= clock[r][a] and the cell's hash does not
+//                      mark an observed remove (1/4 of cells), else 0.
+namespace crdt {
+
+constexpr u64 kOrswotP = 0x9E3779B1ULL;
+constexpr u64 kObsSalt = 0xD1B54A32D192ED03ULL;
+
+__global__ __launch_bounds__(kBlock) void synth_orswot_kernel(u64 *clock, u64 *entries,
+                                                              unsigned long long R,
+                                                              unsigned long long M,
+                                                              unsigned long long A,
+                                                              unsigned long long first_row,
+                                                              u64 seed, u64 kmax, int which) {
+  const unsigned long long nthreads = (unsigned long long)gridDim.x * blockDim.x;
+  if (which == 0) {
+    const unsigned long long total = R * A;
+    for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += nthreads)
+      clock[i] = mix64(seed + (i + first_row * A + 1) * 0x9E3779B97F4A7C15ULL) % (kmax + 1);
+    return;
+  }
+  const unsigned long long total = R * M * A;
+  const u64 pm = kOrswotP % M;
+  for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += nthreads) {
+    const unsigned long long a = i % A;
+    const unsigned long long rm = i / A;
+    const unsigned long long m = rm % M;
+    const unsigned long long r = rm / M;
+    const unsigned long long gr = r + first_row;
+    const u64 c = mix64(seed + (gr * A + a + 1) * 0x9E3779B97F4A7C15ULL) % (kmax + 1);
+    const u64 k = (m + M - (a * pm) % M) % M;
+    u64 e = (k >= 1 && k <= c) ? k : 0;
+    if (e && (mix64(kObsSalt + (gr * M * A + m * A + a)) & 3) == 0) e = 0;
+    entries[i] = e;
+  }
+}
+
+// forget(rm) on the listed members of each replica's own entries: what apply_rm
+// (orswot.rs:230-238) leaves behind for a deferred remove the replica holds.
+__global__ __launch_bounds__(kBlock) void synth_orswot_rm_kernel(u64 *entries, unsigned long long M,
+                                                                 unsigned long long A,
+                                                                 const unsigned *def_row,
+                                                                 const u64 *def_clock,
+                                                                 const u64 *def_members,
+                                                                 unsigned long long Mw) {
+  const unsigned long long d = blockIdx.x;
+  const unsigned long long r = def_row[d];
+  const u64 *rm = def_clock + d * A;
+  const u64 *bits = def_members + d * Mw;
+  for (unsigned long long w = 0; w < Mw; ++w) {
+    u64 word = bits[w];
+    while (word) {
+      const int b = __builtin_ctzll(word);
+      word &= word - 1;
+      const unsigned long long m = w * 64 + b;
+      if (m >= M) break;
+      u64 *row = entries + (r * M + m) * A;
+      for (unsigned long long a = threadIdx.x; a < A; a += kBlock)
+        if (row[a] <= rm[a]) row[a] = 0;
+    }
+  }
+}
+
+}  // namespace crdt
+
+extern "C" int crdt_synth_orswot(crdt_ctx *ctx, uint64_t *clock, uint64_t *entries, size_t R,
+                                 size_t M, size_t A, size_t first_row, uint64_t seed,
+                                 uint64_t kmax) {
+  CRDT_CHECK_CTX(ctx);
+  if (R == 0 || M == 0 || A == 0) return CRDT_OK;
+  if (!clock || !entries) return crdt::fail(ctx, CRDT_EINVAL, "synth_orswot: NULL output");
+  if (kmax >= M) return crdt::fail(ctx, CRDT_EINVAL, "synth_orswot: kmax must be < M");
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  const unsigned blocks = (unsigned)ctx->cu_count * 16;
+  hipLaunchKernelGGL(crdt::synth_orswot_kernel, dim3(blocks), dim3(crdt::kBlock), 0, ctx->stream,
+                     (crdt::u64 *)clock, (crdt::u64 *)entries, (unsigned long long)R,
+                     (unsigned long long)M, (unsigned long long)A, (unsigned long long)first_row,
+                     (crdt::u64)seed, (crdt::u64)kmax, 0);
+  hipLaunchKernelGGL(crdt::synth_orswot_kernel, dim3(blocks), dim3(crdt::kBlock), 0, ctx->stream,
+                     (crdt::u64 *)clock, (crdt::u64 *)entries, (unsigned long long)R,
+                     (unsigned long long)M, (unsigned long long)A, (unsigned long long)first_row,
+                     (crdt::u64)seed, (crdt::u64)kmax, 1);
+  CRDT_HIP(ctx, hipGetLastError());
+  return CRDT_OK;
+}
+
+extern "C" int crdt_synth_orswot_rm(crdt_ctx *ctx, uint64_t *entries, size_t M, size_t A,
+                                    size_t D, const uint32_t *def_row, const uint64_t *def_clock,
+                                    const uint64_t *def_members) {
+  CRDT_CHECK_CTX(ctx);
+  if (D == 0) return CRDT_OK;
+  if (!entries || !def_row || !def_clock || !def_members)
+    return crdt::fail(ctx, CRDT_EINVAL, "synth_orswot_rm: NULL buffer");
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  hipLaunchKernelGGL(crdt::synth_orswot_rm_kernel, dim3((unsigned)D), dim3(crdt::kBlock), 0,
+                     ctx->stream, (crdt::u64 *)entries, (unsigned long long)M,
+                     (unsigned long long)A, (const unsigned *)def_row,
+                     (const crdt::u64 *)def_clock, (const crdt::u64 *)def_members,
+                     (unsigned long long)((M + 63) / 64));
+  CRDT_HIP(ctx, hipGetLastError());
+  return CRDT_OK;
+}

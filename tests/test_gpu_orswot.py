@@ -81,3 +81,28 @@ def test_orswot_empty_and_idempotent(gpu_ctx):
     none = cg.orswot.lub_many(torch.empty((0, 6), dtype=torch.int64, device="cuda:0"),
                               torch.empty((0, 30, 6), dtype=torch.int64, device="cuda:0"), ctx=gpu_ctx)
     assert int(none.clock.abs().sum()) == 0 and int(none.entries.abs().sum()) == 0
+
+
+def test_synth_orswot_matches_cpu(gpu_ctx):
+    from crdts_gpu import synth
+    R, M, A, kmax = 37, 130, 12, 40
+    inp = synth.orswot_replicas(gpu_ctx, R, M, A, seed=77, kmax=kmax, first_row=5, p_def=0.3)
+    c, e = O.synth_orswot(77, R, M, A, kmax, row0=5)
+    rows = np.repeat(np.arange(R), np.diff(inp.def_off.astype(np.int64)))
+    e = O.apply_rm_rows(e, rows, to_host(inp.def_clock), to_host(inp.def_members))
+    np.testing.assert_array_equal(to_host(inp.clock), c)
+    np.testing.assert_array_equal(to_host(inp.entries), e)
+
+
+@pytest.mark.parametrize("R,M,A", [(512, 300, 64), (2000, 64, 16), (129, 1000, 8)])
+def test_orswot_lub_many_synth(gpu_ctx, R, M, A):
+    from crdts_gpu import synth
+    inp = synth.orswot_replicas(gpu_ctx, R, M, A, seed=R + M, kmax=min(M - 1, 30), p_def=0.1)
+    D = inp.def_clock.shape[0]
+    res = cg.orswot.lub_many(inp.clock, inp.entries, def_off=[0, D], def_clock=inp.def_clock,
+                             def_members=inp.def_members, ctx=gpu_ctx)
+    oc, oe, odef, _ = O.orswot_fold(to_host(inp.clock), to_host(inp.entries), inp.def_off,
+                                    to_host(inp.def_clock), to_host(inp.def_members))
+    np.testing.assert_array_equal(to_host(res.clock), oc)
+    np.testing.assert_array_equal(to_host(res.entries), oe)
+    assert cg.orswot.deferred_set(inp.def_clock, res.def_keep, res.def_members) == odef
