@@ -35,7 +35,7 @@ struct Tune {
   int lub_interleave = 0;
   int lub_unroll = 8;
   int lub_nt = 1;
-  int orswot_blocks_per_cu = 8;
+  int orswot_blocks_per_cu = 2;
   int orswot_unroll = 2;
 };
 

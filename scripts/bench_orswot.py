@@ -30,11 +30,20 @@ ap.add_argument("--tune", nargs="*", default=[""])
 args = ap.parse_args()
 
 R, M, A = args.replicas, args.members, args.actors
+T0 = time.time()
+
+
+def log(msg):
+    print(f"[{time.time() - T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
+
+
 torch.cuda.set_device(0)
 ctx0 = cg.Context(0)
 t0 = time.time()
+log(f"generating {R}x{M}x{A} ({R * M * A * 8 / 2**30:.1f} GiB entries)")
 inp = synth.orswot_replicas(ctx0, R, M, A, seed=0x5EED0003, kmax=args.kmax, p_def=0.1)
 torch.cuda.synchronize()
+log("generated")
 gen_s = time.time() - t0
 D = inp.def_clock.shape[0]
 goff = [0, D]
@@ -44,6 +53,7 @@ res = None
 for tune in args.tune:
     os.environ["CRDT_TUNE"] = tune
     ctx = cg.Context(0)
+    log(f"tune {tune!r}: warmup")
     for _ in range(2):
         res = cg.orswot.lub_many(inp.clock, inp.entries, def_off=goff, def_clock=inp.def_clock,
                                  def_members=inp.def_members, ctx=ctx)
@@ -69,6 +79,7 @@ for tune in args.tune:
 # ---- parity on sampled members vs the oracle fold (reference semantics) ----------------------
 import oracle as O  # noqa: E402  (checker only)
 
+log("parity: copying sampled members")
 rng = np.random.default_rng(1)
 msub = np.sort(rng.choice(M, size=min(M, args.sample_members), replace=False))
 clock_h = inp.clock.cpu().numpy().view(np.uint64)
@@ -89,6 +100,7 @@ for r in rows:
     e_cpu = O.apply_rm_rows(e_cpu, [0] * len(dr), dcl_h[dr], dmem_h[dr])
     assert np.array_equal(c_cpu[0], clock_h[r]), "synth clock mismatch"
     assert np.array_equal(e_cpu[0][msub], ent_h[r]), "synth entries mismatch"
+log("parity: oracle fold")
 t2 = time.time()
 oc, oe, odef, fold_s = O.orswot_fold(clock_h, ent_h, inp.def_off, dcl_h, sub_mem)
 got_c = res.clock.cpu().numpy().view(np.uint64)
@@ -97,7 +109,7 @@ keep = res.def_keep.cpu().numpy()
 gmem = res.def_members.cpu().numpy().view(np.uint64)
 got_def = set()
 for d in np.nonzero(keep)[0]:
-    ms = frozenset(j for j, m in enumerate(msub) if (int(gmem[d, m // 64]) >> (m % 64)) & 1)
+    ms = frozenset(j for j, m in enumerate(msub.tolist()) if (int(gmem[d, m // 64]) >> (m % 64)) & 1)
     got_def.add((tuple(int(x) for x in dcl_h[d]), ms))
 ok = np.array_equal(oc, got_c) and np.array_equal(oe, got_e) and got_def == odef
 print(json.dumps({"parity": "ok" if ok else "MISMATCH", "sample_members": msub.tolist(),
