@@ -114,10 +114,12 @@ int crdt_gset_merge_batch(crdt_ctx *ctx, uint64_t *self, const uint64_t *other, 
  * Outputs: out_marker[g], out_val[g] = the folded state (max marker, val of the FIRST
  * replica holding it); first_conflict[g] = index r of the first merge that returns
  * Err(ConflictingMarker) in that fold, or UINT64_MAX if none.  Any of the three outputs
- * may be NULL.  Inputs: marker/val at [g*group_stride + r]. */
+ * may be NULL.  Inputs: marker/val at [g*group_stride + r].
+ * flags = CRDT_ACCUMULATE: acc starts at the caller's state (out_marker[g], out_val[g], both
+ * required) and every replica 0..R-1 is merged into it (R may then be 0). */
 int crdt_lwwreg_lub_many(crdt_ctx *ctx, const uint64_t *marker, const uint64_t *val, size_t G,
                          size_t R, size_t group_stride, uint64_t *out_marker,
-                         uint64_t *out_val, uint64_t *first_conflict);
+                         uint64_t *out_val, uint64_t *first_conflict, unsigned flags);
 /* self[i].merge(other[i]) for i < N; conflict[i] = 1 where it returns Err (state then
  * unchanged), else 0.  conflict may be NULL. */
 int crdt_lwwreg_merge_batch(crdt_ctx *ctx, uint64_t *self_marker, uint64_t *self_val,

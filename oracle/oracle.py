@@ -599,3 +599,36 @@ def gen_orswot(seed: int, R: int, M: int, A: int, kmax: int = 24, p_def: float =
     def_clock = np.array(dcl, dtype=np.uint64).reshape(D, A) if D else np.zeros((0, A), np.uint64)
     def_members = np.array(dmem, dtype=np.uint64).reshape(D, Mw) if D else np.zeros((0, Mw), np.uint64)
     return clock, entries, np.array(def_off, dtype=np.uint64), def_clock, def_members
+
+
+# ---------------------------------------------------------------------------------------
+# Dense restatement of the Orswot lub, checked against the map fold above
+# by tests/test_oracle_twins.py; used as the injected local fold in the CPU (gloo) tests.
+# ---------------------------------------------------------------------------------------
+def dense_orswot_join_fold(clock: np.ndarray, entries: np.ndarray):
+    """e = max(e1==e2?e1:0, e1>c2?e1:0, e2>c1?e2:0), c = max(c1,c2), as a left fold."""
+    e = np.zeros(entries.shape[1:], dtype=np.uint64)
+    c = np.zeros(clock.shape[1], dtype=np.uint64)
+    for r in range(entries.shape[0]):
+        e2, c2 = entries[r], clock[r]
+        t0 = np.where(e == e2, e, 0)
+        t1 = np.where(e > c2, e, 0)
+        t2 = np.where(e2 > c, e2, 0)
+        e = np.maximum(t0, np.maximum(t1, t2)).astype(np.uint64)
+        c = np.maximum(c, c2)
+    return c, e
+
+
+def dense_orswot_lub(clock, entries, def_clock, def_members):
+    """Join fold, then every deferred remove: forget ceiling on its members, survival
+    !(rm <= C), survivors with identical rm clocks merged.  Returns (c, e, deferred set)."""
+    c, e = dense_orswot_join_fold(clock, entries)
+    surv = {}
+    for d in range(def_clock.shape[0]):
+        rm = def_clock[d]
+        ms = bitmap_members(def_members[d])
+        for m in ms:
+            e[m] = np.where(e[m] > rm, e[m], 0)
+        if np.any(rm > c):
+            surv.setdefault(tuple(int(x) for x in rm), set()).update(ms)
+    return c, e, {(k, frozenset(v)) for k, v in surv.items()}

@@ -73,3 +73,93 @@ def shard_range(R: int, rank: int, world: int):
     base, extra = divmod(R, world)
     lo = rank * base + min(rank, extra)
     return lo, lo + base + (1 if rank < extra else 0)
+
+
+# ---- LWWReg ---------------------------------------------------------------------------------
+NO_CONFLICT = 2**63 - 1  # int64 stand-in for u64::MAX in the MIN all-reduce
+
+
+def lwwreg_lub_many_sharded(marker: torch.Tensor, val: torch.Tensor, base: int, group=None,
+                            local=None):
+    """Exact sharded LWW fold (state AND first conflicting merge) over replicas split in rank
+    order: rank k holds replicas [base, base + R_k) of every group ((R_k,) or (G, R_k)).
+
+    1. local fold of each shard; all-gather the (G,) marker/val states;
+    2. rank k folds the states of ranks < k (the prefix) and re-runs its shard continuing from
+       that prefix (CRDT_ACCUMULATE), which yields the conflict indices of the GLOBAL fold;
+    3. MIN all-reduce of base + local index; the final state is the fold of all rank states.
+    Returns (marker (G,), val (G,), first_conflict (G,) int64, -1 = none)."""
+    if local is None:
+        from . import lwwreg
+        local = lwwreg.lub_many
+    squeeze = marker.dim() == 1
+    m2 = marker.reshape(1, -1) if squeeze else marker
+    v2 = val.reshape(1, -1) if squeeze else val
+    G = m2.shape[0]
+    lm, lv, lf = local(m2, v2)
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    if world == 1:
+        fc = torch.where(lf == -1, lf, lf + base)
+        return (lm[0], lv[0], fc[0]) if squeeze else (lm, lv, fc)
+    states = allgather_rows(torch.stack([lm, lv]), group)  # (world, 2, G)
+    gm = states[:, 0, :].transpose(0, 1).contiguous()  # (G, world)
+    gv = states[:, 1, :].transpose(0, 1).contiguous()
+    if rank > 0:
+        pm, pv, _ = local(gm[:, :rank].contiguous(), gv[:, :rank].contiguous())
+        _, _, lf = local(m2, v2, init=(pm, pv))
+    fc = torch.where(lf == -1, torch.full_like(lf, NO_CONFLICT), lf + base)
+    dist.all_reduce(fc, op=dist.ReduceOp.MIN, group=group)
+    fc = torch.where(fc == NO_CONFLICT, torch.full_like(fc, -1), fc)
+    fm, fv, _ = local(gm, gv)
+    return (fm[0], fv[0], fc[0]) if squeeze else (fm, fv, fc)
+
+
+# ---- Orswot ---------------------------------------------------------------------------------
+def orswot_lub_many_sharded(clock: torch.Tensor, entries: torch.Tensor, def_clock: torch.Tensor,
+                            def_members: torch.Tensor, def_group: torch.Tensor, group=None,
+                            local=None):
+    """Sharded Orswot lub: rank k holds replicas of every group ((G, R_k, A) / (G, R_k, M, A))
+    plus its replicas' deferred removes, pooled as rows with their group ids `def_group` (D_k,).
+
+    The dot-store join is associative under the reference invariants, so each rank joins its
+    shard WITHOUT deferred removes, the partial (clock, entries) states are all-gathered, and
+    every rank re-merges the `world` partials together with ALL ranks' deferred removes (the
+    forget ceiling and the survival test need the global clock).  Returns an OrswotLub."""
+    if local is None:
+        from . import orswot
+        local = orswot.lub_many
+    G, _, A = clock.shape
+    M = entries.shape[2]
+    part = local(clock, entries)
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    if world == 1:
+        pc, pe = part.clock.unsqueeze(1), part.entries.unsqueeze(1)
+        dcl, dmem, dgrp = def_clock, def_members, def_group
+    else:
+        pc = allgather_rows(part.clock, group).transpose(0, 1).contiguous()    # (G, world, A)
+        pe = allgather_rows(part.entries, group).transpose(0, 1).contiguous()  # (G, world, M, A)
+        # deferred removes: sizes first, then padded rows
+        n = torch.tensor([def_clock.shape[0]], dtype=torch.int64, device=clock.device)
+        ns = allgather_rows(n, group).reshape(-1).tolist()
+        dmax = max(1, max(ns))
+        Mw = def_members.shape[1]
+        pad = torch.zeros((dmax, A + Mw + 1), dtype=torch.int64, device=clock.device)
+        k = def_clock.shape[0]
+        if k:
+            pad[:k, :A] = def_clock
+            pad[:k, A:A + Mw] = def_members
+            pad[:k, A + Mw] = def_group.to(torch.int64)
+        allp = allgather_rows(pad, group)  # (world, dmax, A+Mw+1)
+        rows = torch.cat([allp[r, :ns[r]] for r in range(world)]) if sum(ns) else pad[:0]
+        dcl, dmem, dgrp = rows[:, :A], rows[:, A:A + Mw], rows[:, A + Mw]
+    # pool the deferred removes by group (stable: rank order, then local order)
+    if dcl.shape[0]:
+        order = torch.argsort(dgrp, stable=True)
+        dcl, dmem = dcl[order].contiguous(), dmem[order].contiguous()
+        counts = torch.bincount(dgrp.to(torch.int64), minlength=G).tolist()
+        off = [0]
+        for c in counts:
+            off.append(off[-1] + c)
+        return local(pc, pe, def_off=off, def_clock=dcl, def_members=dmem)
+    return local(pc, pe)

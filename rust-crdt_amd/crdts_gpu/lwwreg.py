@@ -14,6 +14,7 @@ from typing import NamedTuple, Optional
 
 import torch
 
+from . import _abi
 from .context import Context, dptr
 
 NO_CONFLICT = -1  # u64::MAX bit pattern in an int64 tensor
@@ -25,7 +26,10 @@ class LwwLub(NamedTuple):
     first_conflict: torch.Tensor
 
 
-def lub_many(marker: torch.Tensor, val: torch.Tensor, ctx: Optional[Context] = None) -> LwwLub:
+def lub_many(marker: torch.Tensor, val: torch.Tensor, ctx: Optional[Context] = None,
+             init: Optional[tuple] = None) -> LwwLub:
+    """`init=(marker, val)` continues the fold from that state (CRDT_ACCUMULATE): every replica
+    is then merged into it and first_conflict indexes this call's replicas."""
     ctx = ctx or Context.default(marker.device.index)
     ctx.check_tensor(marker, "lwwreg.lub_many(marker)")
     ctx.check_tensor(val, "lwwreg.lub_many(val)")
@@ -37,11 +41,17 @@ def lub_many(marker: torch.Tensor, val: torch.Tensor, ctx: Optional[Context] = N
     if m2.stride(1) != 1 or v2.stride(1) != 1 or m2.stride(0) != v2.stride(0):
         raise ValueError("lwwreg.lub_many: rows must be contiguous with equal strides")
     G, R = m2.shape
-    om = torch.empty(G, dtype=marker.dtype, device=marker.device)
-    ov = torch.empty_like(om)
+    flags = 0
+    if init is not None:
+        om = init[0].reshape(G).to(marker.dtype).clone()
+        ov = init[1].reshape(G).to(marker.dtype).clone()
+        flags = _abi.CRDT_ACCUMULATE
+    else:
+        om = torch.empty(G, dtype=marker.dtype, device=marker.device)
+        ov = torch.empty_like(om)
     fc = torch.empty_like(om)
     ctx.call("crdt_lwwreg_lub_many", dptr(m2), dptr(v2), G, R, m2.stride(0) if G > 1 else R,
-             dptr(om), dptr(ov), dptr(fc))
+             dptr(om), dptr(ov), dptr(fc), flags)
     if squeeze:
         return LwwLub(om[0], ov[0], fc[0])
     return LwwLub(om, ov, fc)

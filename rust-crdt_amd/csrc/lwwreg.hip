@@ -19,6 +19,7 @@
 namespace crdt {
 
 constexpr u64 kNone = ~0ULL;
+constexpr u64 kPrior = ~0ULL - 1;  // index of the caller's state under CRDT_ACCUMULATE (before replica 0)
 constexpr int kLwwPer = 8;                      // replicas per thread
 constexpr int kLwwChunk = kBlock * kLwwPer;     // replicas per chunk (one workgroup)
 
@@ -84,7 +85,9 @@ struct LwwPlan {
   unsigned long long G, R, gstride, nch;
   MI *part;  // [G][nch]
   MI *pre;   // [G][nch] exclusive chunk prefixes
+  u64 *prior_val;  // [G] the caller's val under CRDT_ACCUMULATE
   u64 *out_marker, *out_val, *first_conflict;
+  int accumulate;
 };
 
 // Thread t of chunk c owns replicas c*CH + t*kLwwPer .. +kLwwPer (contiguous, fold order).
@@ -109,12 +112,16 @@ __global__ __launch_bounds__(kBlock) void lww_chunk_scan(LwwPlan p) {
   const unsigned long long g = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= p.G) return;
   MI run{0, kNone};
+  if (p.accumulate) {  // the caller's state precedes replica 0 (ties keep it: it is earlier)
+    run = MI{p.out_marker[g], kPrior};
+    p.prior_val[g] = p.out_val[g];
+  }
   for (unsigned long long c = 0; c < p.nch; ++c) {
     p.pre[g * p.nch + c] = run;
     run = mi_join(run, p.part[g * p.nch + c]);
   }
   if (p.out_marker) p.out_marker[g] = run.m;
-  if (p.out_val) p.out_val[g] = p.val[g * p.gstride + run.i];
+  if (p.out_val) p.out_val[g] = run.i == kPrior ? p.prior_val[g] : p.val[g * p.gstride + run.i];
 }
 
 __global__ __launch_bounds__(kBlock) void lww_conflict(LwwPlan p) {
@@ -141,7 +148,8 @@ __global__ __launch_bounds__(kBlock) void lww_conflict(LwwPlan p) {
     const unsigned long long r = r0 + k;
     if (r < p.R) {
       if (run.i != kNone && m[k] == run.m && first == kNone) {
-        if (vl[r] != vl[run.i]) first = r;
+        const u64 held = run.i == kPrior ? p.prior_val[g] : vl[run.i];
+        if (vl[r] != held) first = r;
       }
       run = mi_join(run, MI{m[k], r});
     }
@@ -175,9 +183,16 @@ extern "C" {
 
 int crdt_lwwreg_lub_many(crdt_ctx *ctx, const uint64_t *marker, const uint64_t *val, size_t G,
                          size_t R, size_t group_stride, uint64_t *out_marker,
-                         uint64_t *out_val, uint64_t *first_conflict) {
+                         uint64_t *out_val, uint64_t *first_conflict, unsigned flags) {
   CRDT_CHECK_CTX(ctx);
   if (G == 0) return CRDT_OK;
+  const bool accumulate = flags & CRDT_ACCUMULATE;
+  if (accumulate && (!out_marker || !out_val))
+    return fail(ctx, CRDT_EINVAL, "lwwreg_lub_many: CRDT_ACCUMULATE needs out_marker and out_val");
+  if (R == 0 && accumulate) {
+    if (first_conflict) CRDT_HIP(ctx, hipMemsetAsync(first_conflict, 0xFF, G * 8, ctx->stream));
+    return CRDT_OK;
+  }
   if (R == 0) return fail(ctx, CRDT_EINVAL, "lwwreg_lub_many: R == 0 (LWWReg has no identity; the fold starts at replica 0)");
   if (!marker || !val) return fail(ctx, CRDT_EINVAL, "lwwreg_lub_many: NULL input");
   if (G > 1 && group_stride < R)
@@ -195,10 +210,12 @@ int crdt_lwwreg_lub_many(crdt_ctx *ctx, const uint64_t *marker, const uint64_t *
   p.first_conflict = (u64 *)first_conflict;
   const size_t nparts = G * p.nch;
   if (G * p.nch > 0x7fffffffULL) return fail(ctx, CRDT_EUNSUPPORTED, "lwwreg_lub_many: grid too large");
-  int rc = ensure_scratch(ctx, 2 * nparts * sizeof(MI));
+  p.accumulate = accumulate ? 1 : 0;
+  int rc = ensure_scratch(ctx, 2 * nparts * sizeof(MI) + G * sizeof(u64));
   if (rc) return rc;
   p.part = static_cast<MI *>(ctx->scratch);
   p.pre = p.part + nparts;
+  p.prior_val = reinterpret_cast<u64 *>(p.pre + nparts);
   timing_begin(ctx, "lww_reduce");
   hipLaunchKernelGGL(lww_chunk_reduce, dim3((unsigned)nparts), dim3(kBlock), 0, ctx->stream, p);
   timing_end(ctx);

@@ -91,3 +91,144 @@ def test_sign_bias_preserves_unsigned_order():
     order_u = np.argsort(vals, kind="stable")
     order_s = np.argsort(b.numpy(), kind="stable")
     assert (order_u == order_s).all()
+
+
+# ---- LWWReg and Orswot sharded exchanges -----------------------------------------------------
+def _lww_local(m, v, init=None):
+    import oracle as O
+    mm, vv = m.numpy().view(np.uint64), v.numpy().view(np.uint64)
+    G = mm.shape[0]
+    om, ov, of = (np.zeros(G, dtype=np.uint64) for _ in range(3))
+    for g in range(G):
+        if init is None:
+            acc, start = O.LWWReg(int(vv[g, 0]), int(mm[g, 0])), 1
+        else:
+            acc, start = O.LWWReg(int(init[1].numpy().view(np.uint64)[g]), int(init[0].numpy().view(np.uint64)[g])), 0
+        first = 2**64 - 1
+        for r in range(start, mm.shape[1]):
+            try:
+                acc.merge(O.LWWReg(int(vv[g, r]), int(mm[g, r])))
+            except O.ConflictingMarker:
+                first = min(first, r)
+        om[g], ov[g], of[g] = acc.marker, acc.val, first
+    t = lambda a: torch.from_numpy(a.view(np.int64).copy())
+    return t(om), t(ov), t(of)
+
+
+def _lww_worker(rank, world, port, G, R, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (os.path.join(here, ".."), os.path.join(here, "..", "rust-crdt_amd"), os.path.join(here, "..", "oracle"), here):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import oracle as O
+    from crdts_gpu import dist as cdist
+    m = O.synth_matrix(41, G, R, 2) % np.uint64(6)
+    v = O.synth_matrix(41, G, R, 3) % np.uint64(2)
+    lo, hi = cdist.shard_range(R, rank, world)
+    tm = torch.from_numpy(m[:, lo:hi].view(np.int64).copy())
+    tv = torch.from_numpy(v[:, lo:hi].view(np.int64).copy())
+    fm, fv, fc = cdist.lwwreg_lub_many_sharded(tm, tv, lo, local=_lww_local)
+    if rank == 0:
+        q.put((fm.numpy().copy(), fv.numpy().copy(), fc.numpy().copy()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,G,R", [(2, 3, 40), (3, 2, 31)])
+def test_lww_sharded_exact_conflicts(world, G, R):
+    import oracle as O
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_lww_worker, args=(r, world, port, G, R, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    fm, fv, fc = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    m = O.synth_matrix(41, G, R, 2) % np.uint64(6)
+    v = O.synth_matrix(41, G, R, 3) % np.uint64(2)
+    for g in range(G):
+        om, ov, of, _ = O.lwwreg_fold(m[g], v[g])
+        got_fc = 2**64 - 1 if fc[g] == -1 else int(fc[g])
+        assert (int(fm[g]), int(fv[g]), got_fc) == (om, ov, of)
+
+
+def _orswot_local(clock, entries, def_off=None, def_clock=None, def_members=None):
+    import oracle as O
+    from crdts_gpu.orswot import OrswotLub
+    c3 = clock.numpy().view(np.uint64)
+    e4 = entries.numpy().view(np.uint64)
+    G, _, A = c3.shape
+    M = e4.shape[2]
+    Mw = (M + 63) // 64
+    oc = np.zeros((G, A), np.uint64)
+    oe = np.zeros((G, M, A), np.uint64)
+    D = 0 if def_off is None else int(def_off[-1])
+    keep = np.zeros(D, np.uint8)
+    mem = np.zeros((D, Mw), np.uint64)
+    dcl = def_clock.numpy().view(np.uint64) if D else None
+    dmm = def_members.numpy().view(np.uint64) if D else None
+    for g in range(G):
+        lo, hi = (int(def_off[g]), int(def_off[g + 1])) if D else (0, 0)
+        c, e, surv = O.dense_orswot_lub(c3[g], e4[g], dcl[lo:hi] if D else np.zeros((0, A), np.uint64),
+                                        dmm[lo:hi] if D else np.zeros((0, Mw), np.uint64))
+        oc[g], oe[g] = c, e
+        for d in range(lo, hi):  # representative = first survivor with that clock
+            key = tuple(int(x) for x in dcl[d])
+            for k, ms in surv:
+                if k == key and not any(tuple(int(x) for x in dcl[d2]) == key and keep[d2] for d2 in range(lo, d)):
+                    keep[d] = 1
+                    for mm in ms:
+                        mem[d, mm // 64] |= np.uint64(1) << np.uint64(mm % 64)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64).copy())
+    return OrswotLub(t(oc), t(oe), torch.from_numpy(keep), t(mem))
+
+
+def _orswot_worker(rank, world, port, R, M, A, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (os.path.join(here, ".."), os.path.join(here, "..", "rust-crdt_amd"), os.path.join(here, "..", "oracle"), here):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import oracle as O
+    from crdts_gpu import dist as cdist
+    clock, entries, off, dcl, dmem = O.gen_orswot(99, R, M, A, kmax=10)
+    lo, hi = cdist.shard_range(R, rank, world)
+    d0, d1 = int(off[lo]), int(off[hi])
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64).copy())
+    res = cdist.orswot_lub_many_sharded(t(clock[lo:hi][None]), t(entries[lo:hi][None]), t(dcl[d0:d1]),
+                                        t(dmem[d0:d1]), torch.zeros(d1 - d0, dtype=torch.int64),
+                                        local=_orswot_local)
+    if rank == 0:
+        from crdts_gpu.orswot import deferred_set
+        D = res.def_keep.shape[0] if res.def_keep is not None else 0
+        allcl = torch.cat([t(dcl)]) if D else None
+        # the re-merge pools deferred removes in rank order == original order here
+        dset = deferred_set(allcl, res.def_keep, res.def_members) if D else set()
+        q.put((res.clock.numpy().copy(), res.entries.numpy().copy(), dset))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_orswot_sharded_world(world):
+    import oracle as O
+    R, M, A = 13, 20, 5
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_orswot_worker, args=(r, world, port, R, M, A, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    c, e, dset = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    clock, entries, off, dcl, dmem = O.gen_orswot(99, R, M, A, kmax=10)
+    oc, oe, odef, _ = O.orswot_fold(clock, entries, off, dcl, dmem)
+    np.testing.assert_array_equal(c.view(np.uint64)[0], oc)
+    np.testing.assert_array_equal(e.view(np.uint64)[0], oe)
+    assert dset == odef

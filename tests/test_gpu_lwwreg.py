@@ -61,3 +61,30 @@ def test_lww_merge_batch(gpu_ctx, N):
         except O.ConflictingMarker:
             err = 1
         assert (int(gm[i]), int(gv[i]), int(gc[i])) == (reg.marker, reg.val, err)
+
+
+@pytest.mark.parametrize("G,R,split", [(1, 5000, 1234), (3, 700, 350), (2, 9000, 8999), (1, 10, 0)])
+def test_lww_accumulate_continues_the_fold(gpu_ctx, G, R, split):
+    """lub of the tail continued from the lub of the head == lub of everything, and the tail's
+    conflict index + split == the global first conflict when the head has none."""
+    m, v = _inputs(0x77 + R, G, R, 9, 2)
+    dm, dv = to_dev(m), to_dev(v)
+    full = cg.lwwreg.lub_many(dm, dv, ctx=gpu_ctx)
+    if split == 0:
+        init = (dm[:, 0].contiguous(), dv[:, 0].contiguous())
+        tail = cg.lwwreg.lub_many(dm[:, 1:].contiguous(), dv[:, 1:].contiguous(), ctx=gpu_ctx, init=init)
+        off = 1
+        head_fc = np.full(G, NONE)
+    else:
+        head = cg.lwwreg.lub_many(dm[:, :split].contiguous(), dv[:, :split].contiguous(), ctx=gpu_ctx)
+        tail = cg.lwwreg.lub_many(dm[:, split:].contiguous(), dv[:, split:].contiguous(), ctx=gpu_ctx,
+                                  init=(head.marker, head.val))
+        off = split
+        head_fc = to_host(head.first_conflict)
+    np.testing.assert_array_equal(to_host(tail.marker), to_host(full.marker))
+    np.testing.assert_array_equal(to_host(tail.val), to_host(full.val))
+    tfc = to_host(tail.first_conflict)
+    ffc = to_host(full.first_conflict)
+    for g in range(G):
+        exp = head_fc[g] if head_fc[g] != NONE else (NONE if tfc[g] == NONE else tfc[g] + np.uint64(off))
+        assert ffc[g] == exp

@@ -70,32 +70,11 @@ def py_orswot_from_dense(clock, entries, dcl, dmem):
     return o
 
 
-def dense_orswot_join_fold(clock, entries):
-    """e = max(e1==e2?e1:0, e1>c2?e1:0, e2>c1?e2:0), c = max — as a left fold."""
-    e = np.zeros(entries.shape[1:], dtype=np.uint64)
-    c = np.zeros(clock.shape[1], dtype=np.uint64)
-    for r in range(entries.shape[0]):
-        e2, c2 = entries[r], clock[r]
-        t0 = np.where(e == e2, e, 0)
-        t1 = np.where(e > c2, e, 0)
-        t2 = np.where(e2 > c, e2, 0)
-        e = np.maximum(t0, np.maximum(t1, t2)).astype(np.uint64)
-        c = np.maximum(c, c2)
-    return c, e
+dense_orswot_join_fold = O.dense_orswot_join_fold
 
 
 def dense_orswot_lub(clock, entries, def_off, def_clock, def_members):
-    c, e = dense_orswot_join_fold(clock, entries)
-    M = e.shape[0]
-    surv = {}
-    for d in range(def_clock.shape[0]):
-        rm = def_clock[d]
-        ms = O.bitmap_members(def_members[d])
-        for m in ms:
-            e[m] = np.where(e[m] > rm, e[m], 0)
-        if np.any(rm > c):
-            surv.setdefault(tuple(int(x) for x in rm), set()).update(ms)
-    return c, e, {(k, frozenset(v)) for k, v in surv.items()}
+    return O.dense_orswot_lub(clock, entries, def_clock, def_members)
 
 
 @pytest.mark.parametrize("seed,R,M,A", [(1, 2, 5, 3), (2, 5, 16, 4), (3, 9, 40, 6), (4, 24, 70, 8)])
