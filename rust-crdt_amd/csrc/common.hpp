@@ -37,6 +37,7 @@ struct Tune {
   int lub_nt = 1;
   int orswot_blocks_per_cu = 2;
   int orswot_unroll = 2;
+  int merge_blocks_per_cu = 2;
 };
 
 struct PendingTiming {

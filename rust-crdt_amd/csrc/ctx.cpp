@@ -142,6 +142,7 @@ int crdt_ctx_create(int device, crdt_ctx **out) {
         else if (k == "unroll" && (v == 4 || v == 8 || v == 16 || v == 32)) ctx->tune.lub_unroll = v;
         else if (k == "nt") ctx->tune.lub_nt = v != 0;
         else if (k == "grid" && v > 0) ctx->tune.lub_grid = v;
+        else if (k == "mbpc" && v > 0) ctx->tune.merge_blocks_per_cu = v;
         else if (k == "obpc" && v > 0) ctx->tune.orswot_blocks_per_cu = v;
         else if (k == "ounroll" && (v == 1 || v == 2 || v == 4)) ctx->tune.orswot_unroll = v;
       }

@@ -211,12 +211,14 @@ __global__ __launch_bounds__(kBlock) void lub_stream_kernel(LubPlan p) {
 
 // self[i] := self[i] ⊔ other[i]: three streams (2 reads, 1 write), TR rows per block step.
 template <Op OP, int V>
-__global__ __launch_bounds__(kBlock) void merge_pairs_kernel(u64 *self, const u64 *other,
+__global__ __launch_bounds__(kBlock) void merge_pairs_kernel(u64 *__restrict__ self,
+                                                             const u64 *__restrict__ other,
                                                              unsigned long long N, int Wv, int PW,
                                                              int TR, long long sstride,
                                                              long long ostride,
                                                              unsigned long long rows_per_block) {
   using VT = typename VecOf<V>::T;
+  constexpr int U = 4;  // row pairs in flight per lane
   const int l = threadIdx.x;
   const int cl = l % PW;
   const int rsub = l / PW;
@@ -224,12 +226,22 @@ __global__ __launch_bounds__(kBlock) void merge_pairs_kernel(u64 *self, const u6
   if (rsub >= TR || col >= Wv) return;
   const unsigned long long rbeg = (unsigned long long)blockIdx.x * rows_per_block;
   const unsigned long long rend = min(N, rbeg + rows_per_block);
-  for (unsigned long long r = rbeg + rsub; r < rend; r += TR) {
+  unsigned long long r = rbeg + rsub;
+  for (; r + (U - 1) * TR < rend; r += U * TR) {
+    VT a[U], bv[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      a[k] = reinterpret_cast<const VT *>(self + (r + k * TR) * sstride)[col];
+      bv[k] = __builtin_nontemporal_load(reinterpret_cast<const VT *>(other + (r + k * TR) * ostride) + col);
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k)
+      reinterpret_cast<VT *>(self + (r + k * TR) * sstride)[col] = vjoin<OP>(a[k], bv[k]);
+  }
+  for (; r < rend; r += TR) {
     VT *sp = reinterpret_cast<VT *>(self + r * sstride) + col;
     const VT *op = reinterpret_cast<const VT *>(other + r * ostride) + col;
-    VT a = *sp;
-    VT bv = __builtin_nontemporal_load(op);
-    *sp = vjoin<OP>(a, bv);
+    *sp = vjoin<OP>(*sp, __builtin_nontemporal_load(op));
   }
 }
 
@@ -348,8 +360,11 @@ int lattice_merge_batch(crdt_ctx *ctx, Op op, u64 *self, const u64 *other, size_
   const int PW = Wv <= kBlock ? Wv : kBlock;
   const int TR = kBlock / PW;
   const int ncolblk = (Wv + kBlock - 1) / kBlock;
-  // ~16 row steps per block, capped at 8 blocks per CU worth of rows.
-  unsigned long long rpb = (unsigned long long)TR * 16;
+  // Contiguous row ranges, ~mbpc workgroups per CU (each lane >= 16 row steps).
+  const unsigned long long want = (unsigned long long)ctx->cu_count * ctx->tune.merge_blocks_per_cu;
+  unsigned long long rpb = (N + want - 1) / want;
+  rpb = (rpb + TR - 1) / TR * TR;
+  if (rpb < (unsigned long long)TR * 16) rpb = (unsigned long long)TR * 16;
   unsigned long long nb = (N + rpb - 1) / rpb;
   if (nb > 0x7fffffffULL) return fail(ctx, CRDT_EUNSUPPORTED, "merge_batch: N too large");
   dim3 grid((unsigned)nb, (unsigned)ncolblk);

@@ -88,20 +88,43 @@ struct LwwPlan {
   u64 *prior_val;  // [G] the caller's val under CRDT_ACCUMULATE
   u64 *out_marker, *out_val, *first_conflict;
   int accumulate;
+  bool vec;  // 16-byte aligned group rows: coalesced u64x2 staging
 };
 
-// Thread t of chunk c owns replicas c*CH + t*kLwwPer .. +kLwwPer (contiguous, fold order).
+// Stage a chunk's markers in LDS with coalesced loads (16 B per lane when aligned); thread t
+// then owns replicas c*CH + t*kLwwPer .. +kLwwPer (contiguous, fold order) from LDS.
+__device__ __forceinline__ void stage_chunk(const u64 *__restrict__ mk, unsigned long long c0,
+                                            unsigned long long R, bool vec, u64 *sm) {
+  if (vec && c0 + kLwwChunk <= R) {
+    const u64x2 *src = reinterpret_cast<const u64x2 *>(mk + c0);
+#pragma unroll
+    for (int k = 0; k < kLwwPer / 2; ++k) {
+      const int j = k * kBlock + threadIdx.x;
+      reinterpret_cast<u64x2 *>(sm)[j] = __builtin_nontemporal_load(src + j);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < kLwwPer; ++k) {
+      const int j = k * kBlock + threadIdx.x;
+      sm[j] = c0 + j < R ? mk[c0 + j] : 0;
+    }
+  }
+  __syncthreads();
+}
+
 __global__ __launch_bounds__(kBlock) void lww_chunk_reduce(LwwPlan p) {
   __shared__ MI wt[kBlock / kWave];
+  __shared__ u64 sm[kLwwChunk];
   const unsigned long long c = blockIdx.x % p.nch;
   const unsigned long long g = blockIdx.x / p.nch;
-  const u64 *mk = p.marker + g * p.gstride;
-  const unsigned long long r0 = c * kLwwChunk + (unsigned long long)threadIdx.x * kLwwPer;
+  const unsigned long long c0 = c * kLwwChunk;
+  stage_chunk(p.marker + g * p.gstride, c0, p.R, p.vec, sm);
+  const unsigned long long r0 = c0 + (unsigned long long)threadIdx.x * kLwwPer;
   MI x{0, kNone};
 #pragma unroll
   for (int k = 0; k < kLwwPer; ++k) {
     const unsigned long long r = r0 + k;
-    if (r < p.R) x = mi_join(x, MI{mk[r], r});
+    if (r < p.R) x = mi_join(x, MI{sm[threadIdx.x * kLwwPer + k], r});
   }
   x = block_reduce(x, wt);
   if (threadIdx.x == 0) p.part[g * p.nch + c] = x;
@@ -124,24 +147,59 @@ __global__ __launch_bounds__(kBlock) void lww_chunk_scan(LwwPlan p) {
   if (p.out_val) p.out_val[g] = run.i == kPrior ? p.prior_val[g] : p.val[g * p.gstride + run.i];
 }
 
+// One workgroup per group (many chunks): the same exclusive scan, 256 chunk aggregates per step.
+__global__ __launch_bounds__(kBlock) void lww_chunk_scan_block(LwwPlan p) {
+  __shared__ MI wt[kBlock / kWave];
+  __shared__ MI s_carry;
+  const unsigned long long g = blockIdx.x;
+  if (threadIdx.x == 0) {
+    s_carry = MI{0, kNone};
+    if (p.accumulate) {
+      s_carry = MI{p.out_marker[g], kPrior};
+      p.prior_val[g] = p.out_val[g];
+    }
+  }
+  __syncthreads();
+  for (unsigned long long c0 = 0; c0 < p.nch; c0 += kBlock) {
+    const unsigned long long c = c0 + threadIdx.x;
+    const MI x = c < p.nch ? p.part[g * p.nch + c] : MI{0, kNone};
+    const MI carry = s_carry;
+    const MI excl = block_exclusive_scan(x, wt);
+    if (c < p.nch) p.pre[g * p.nch + c] = mi_join(carry, excl);
+    if (threadIdx.x == kBlock - 1) s_carry = mi_join(carry, mi_join(excl, x));
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const MI run = s_carry;
+    if (p.out_marker) p.out_marker[g] = run.m;
+    if (p.out_val) p.out_val[g] = run.i == kPrior ? p.prior_val[g] : p.val[g * p.gstride + run.i];
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void lww_conflict(LwwPlan p) {
   __shared__ MI wt[kBlock / kWave];
   __shared__ unsigned long long s_first;
+  __shared__ u64 sm[kLwwChunk];
   const unsigned long long c = blockIdx.x % p.nch;
   const unsigned long long g = blockIdx.x / p.nch;
-  const u64 *mk = p.marker + g * p.gstride;
+  const MI pre = p.pre[g * p.nch + c];
+  // A merge can only err on a marker equal to the running max; if every marker of the chunk is
+  // below the incoming prefix max, none can (block-uniform early exit, no loads).
+  if (pre.i != kNone && p.part[g * p.nch + c].m < pre.m) return;
   const u64 *vl = p.val + g * p.gstride;
-  const unsigned long long r0 = c * kLwwChunk + (unsigned long long)threadIdx.x * kLwwPer;
+  const unsigned long long c0 = c * kLwwChunk;
   if (threadIdx.x == 0) s_first = kNone;
+  stage_chunk(p.marker + g * p.gstride, c0, p.R, p.vec, sm);
+  const unsigned long long r0 = c0 + (unsigned long long)threadIdx.x * kLwwPer;
   u64 m[kLwwPer];
   MI agg{0, kNone};
 #pragma unroll
   for (int k = 0; k < kLwwPer; ++k) {
     const unsigned long long r = r0 + k;
-    m[k] = r < p.R ? mk[r] : 0;
+    m[k] = sm[threadIdx.x * kLwwPer + k];
     if (r < p.R) agg = mi_join(agg, MI{m[k], r});
   }
-  MI run = mi_join(p.pre[g * p.nch + c], block_exclusive_scan(agg, wt));
+  MI run = mi_join(pre, block_exclusive_scan(agg, wt));
   unsigned long long first = kNone;
 #pragma unroll
   for (int k = 0; k < kLwwPer; ++k) {
@@ -211,6 +269,7 @@ int crdt_lwwreg_lub_many(crdt_ctx *ctx, const uint64_t *marker, const uint64_t *
   const size_t nparts = G * p.nch;
   if (G * p.nch > 0x7fffffffULL) return fail(ctx, CRDT_EUNSUPPORTED, "lwwreg_lub_many: grid too large");
   p.accumulate = accumulate ? 1 : 0;
+  p.vec = (reinterpret_cast<uintptr_t>(marker) & 15) == 0 && (G == 1 || group_stride % 2 == 0);
   int rc = ensure_scratch(ctx, 2 * nparts * sizeof(MI) + G * sizeof(u64));
   if (rc) return rc;
   p.part = static_cast<MI *>(ctx->scratch);
@@ -219,8 +278,11 @@ int crdt_lwwreg_lub_many(crdt_ctx *ctx, const uint64_t *marker, const uint64_t *
   timing_begin(ctx, "lww_reduce");
   hipLaunchKernelGGL(lww_chunk_reduce, dim3((unsigned)nparts), dim3(kBlock), 0, ctx->stream, p);
   timing_end(ctx);
-  hipLaunchKernelGGL(lww_chunk_scan, dim3((unsigned)((G + kBlock - 1) / kBlock)), dim3(kBlock), 0,
-                     ctx->stream, p);
+  if (p.nch > 16)  // long groups: a workgroup scans each group's chunk aggregates
+    hipLaunchKernelGGL(lww_chunk_scan_block, dim3((unsigned)G), dim3(kBlock), 0, ctx->stream, p);
+  else
+    hipLaunchKernelGGL(lww_chunk_scan, dim3((unsigned)((G + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                       ctx->stream, p);
   if (first_conflict) {
     CRDT_HIP(ctx, hipMemsetAsync(first_conflict, 0xFF, G * sizeof(uint64_t), ctx->stream));
     hipLaunchKernelGGL(lww_conflict, dim3((unsigned)nparts), dim3(kBlock), 0, ctx->stream, p);
