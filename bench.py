@@ -40,6 +40,8 @@ def parse():
     ap.add_argument("--actors", type=int, default=A_ACTORS)
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="target fold seconds of the CPU baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL on ROCm) for real runs; gloo lets several ranks share one GPU in tests")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="PMC-derived HBM bytes per launch (written by profiles/collect.sh)")
     return ap.parse_args()
@@ -88,10 +90,14 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    torch.cuda.set_device(local)
+    dev = local % torch.cuda.device_count()
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    ctx = cg.Context.default(local)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(args.dist_backend)
+    ctx = cg.Context.default(dev)
 
     R, A = args.replicas, args.actors
     # Synthetic replicas, generated in HBM; rank k owns rows [k*R, (k+1)*R) of the global input.
@@ -136,7 +142,16 @@ def main():
 
     # Parity (outside the timed region): unsigned max with torch ops + sampled CPU rows.
     sign = torch.tensor(-(2**63), dtype=torch.int64, device="cuda")
-    ok = bool(torch.equal(g_out, (g_in ^ sign).amax(0) ^ sign)) and bool(torch.equal(p_out, (p_in ^ sign).amax(0) ^ sign))
+    ref_g, ref_p = (g_in ^ sign).amax(0) ^ sign, (p_in ^ sign).amax(0) ^ sign
+    if world > 1:  # the exchanged result must equal the max of every rank's torch reference
+        ref = torch.cat([ref_g, ref_p])
+        cdist.allreduce_umax_(ref)
+        ok = bool(torch.equal(both, ref))
+        t_ok = torch.tensor([1 if ok else 0], dtype=torch.int64, device="cuda")
+        dist.all_reduce(t_ok, op=dist.ReduceOp.MIN)
+        ok = bool(t_ok.item())
+    else:
+        ok = bool(torch.equal(g_out, ref_g)) and bool(torch.equal(p_out, ref_p))
 
     merges_per_step = 2 * R * world
     value = merges_per_step * args.steps / elapsed
