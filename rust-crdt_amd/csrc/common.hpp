@@ -57,10 +57,18 @@ struct crdt_ctx {
   // Device scratch (grown on demand, never shrunk; freed in destroy).
   void *scratch = nullptr;
   size_t scratch_bytes = 0;
+  // Second region for the Orswot deferred-remove bookkeeping (used after the join).
+  void *dscratch = nullptr;
+  size_t dscratch_bytes = 0;
   // Arrival counters of the last-arriver combines: a dedicated region that is zero between
   // calls (kernels reset every counter they use), never shared with scratch.
   unsigned *counters = nullptr;
   size_t counters_n = 0;
+  // Pinned host staging for small host->device copies of caller arrays (crdt_orswot_lub_many
+  // def_off): the caller's memory is not read after return.
+  void *pinned = nullptr;
+  size_t pinned_bytes = 0;
+  hipEvent_t pinned_done = nullptr;
   std::map<std::string, crdt::KernelTimer> timers;
   std::vector<crdt::PendingTiming> pending;
   std::vector<hipEvent_t> free_events;
@@ -72,8 +80,14 @@ int fail(crdt_ctx *ctx, int code, const char *fmt, ...);
 int hip_fail(crdt_ctx *ctx, hipError_t e, const char *what);
 // Ensure ctx->scratch holds at least `bytes`; returns CRDT_OK or CRDT_ENOMEM.
 int ensure_scratch(crdt_ctx *ctx, size_t bytes);
+int ensure_dscratch(crdt_ctx *ctx, size_t bytes);
 // Ensure ctx->counters holds at least n zeroed counters.
 int ensure_counters(crdt_ctx *ctx, size_t n);
+// Copy `bytes` of host memory to device memory `dst` on the ctx stream; `src` is read before
+// return (through a pinned staging buffer), so the caller may free it immediately.
+int stage_h2d(crdt_ctx *ctx, void *dst, const void *src, size_t bytes);
+// Fill `bytes` of device memory with `byte` by a kernel on the ctx stream.
+int device_fill(crdt_ctx *ctx, void *dst, size_t bytes, unsigned char byte);
 // Bracket the dominant kernel of a call with events when timing is on.
 void timing_begin(crdt_ctx *ctx, const char *name);
 void timing_end(crdt_ctx *ctx);

@@ -42,6 +42,24 @@ int ensure_scratch(crdt_ctx *ctx, size_t bytes) {
   return CRDT_OK;
 }
 
+int ensure_dscratch(crdt_ctx *ctx, size_t bytes) {
+  if (bytes <= ctx->dscratch_bytes) return CRDT_OK;
+  if (ctx->dscratch) {
+    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipFree(ctx->dscratch);
+    ctx->dscratch = nullptr;
+    ctx->dscratch_bytes = 0;
+  }
+  size_t want = bytes < (1u << 16) ? (1u << 16) : bytes + bytes / 4;
+  hipError_t e = hipMalloc(&ctx->dscratch, want);
+  if (e != hipSuccess) {
+    ctx->dscratch = nullptr;
+    return fail(ctx, CRDT_ENOMEM, "dscratch hipMalloc(%zu) failed: %s", want, hipGetErrorString(e));
+  }
+  ctx->dscratch_bytes = want;
+  return CRDT_OK;
+}
+
 int ensure_counters(crdt_ctx *ctx, size_t n) {
   if (n <= ctx->counters_n) return CRDT_OK;
   if (ctx->counters) {
@@ -56,10 +74,63 @@ int ensure_counters(crdt_ctx *ctx, size_t n) {
     ctx->counters = nullptr;
     return fail(ctx, CRDT_ENOMEM, "counter hipMalloc failed: %s", hipGetErrorString(e));
   }
-  e = hipMemsetAsync(ctx->counters, 0, want * sizeof(unsigned), ctx->stream);
-  if (e != hipSuccess) return hip_fail(ctx, e, "hipMemsetAsync(counters)");
   ctx->counters_n = want;
+  return device_fill(ctx, ctx->counters, want * sizeof(unsigned), 0);
+}
+
+int stage_h2d(crdt_ctx *ctx, void *dst, const void *src, size_t bytes) {
+  if (bytes == 0) return CRDT_OK;
+  if (ctx->pinned_done) {  // the previous staged copy must have left the buffer
+    hipError_t e = hipEventSynchronize(ctx->pinned_done);
+    if (e != hipSuccess) return hip_fail(ctx, e, "hipEventSynchronize(pinned)");
+  } else {
+    hipError_t e = hipEventCreateWithFlags(&ctx->pinned_done, hipEventDisableTiming);
+    if (e != hipSuccess) return hip_fail(ctx, e, "hipEventCreate(pinned)");
+  }
+  if (bytes > ctx->pinned_bytes) {
+    if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+    ctx->pinned = nullptr;
+    ctx->pinned_bytes = 0;
+    size_t want = bytes < 65536 ? 65536 : bytes * 2;
+    hipError_t e = hipHostMalloc(&ctx->pinned, want, hipHostMallocDefault);
+    if (e != hipSuccess) return fail(ctx, CRDT_ENOMEM, "hipHostMalloc(%zu) failed", want);
+    ctx->pinned_bytes = want;
+  }
+  std::memcpy(ctx->pinned, src, bytes);
+  hipError_t e = hipMemcpyAsync(dst, ctx->pinned, bytes, hipMemcpyHostToDevice, ctx->stream);
+  if (e != hipSuccess) return hip_fail(ctx, e, "hipMemcpyAsync(staged)");
+  e = hipEventRecord(ctx->pinned_done, ctx->stream);
+  if (e != hipSuccess) return hip_fail(ctx, e, "hipEventRecord(pinned)");
   return CRDT_OK;
+}
+
+// Kernel-based fill: ordered with the kernels around it on the ctx stream like any launch.
+// (Small hipMemsetAsync calls were observed to race with the kernels that consume their
+// result on the legacy null stream, so nothing a later kernel reads is zeroed by a memset.)
+__global__ void fill_u64_kernel(unsigned long long *p, size_t n, unsigned long long v) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    p[i] = v;
+}
+__global__ void fill_u8_kernel(unsigned char *p, size_t n, unsigned char v) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    p[i] = v;
+}
+
+int device_fill(crdt_ctx *ctx, void *dst, size_t bytes, unsigned char byte) {
+  if (bytes == 0) return CRDT_OK;
+  const bool wide = (reinterpret_cast<uintptr_t>(dst) % 8 == 0) && bytes % 8 == 0;
+  const size_t n = wide ? bytes / 8 : bytes;
+  size_t blocks = (n + kBlock - 1) / kBlock;
+  const size_t cap = (size_t)ctx->cu_count * 8;
+  if (blocks > cap) blocks = cap;
+  if (wide)
+    hipLaunchKernelGGL(fill_u64_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, ctx->stream,
+                       (unsigned long long *)dst, n, 0x0101010101010101ULL * byte);
+  else
+    hipLaunchKernelGGL(fill_u8_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, ctx->stream,
+                       (unsigned char *)dst, n, byte);
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? CRDT_OK : hip_fail(ctx, e, "device_fill");
 }
 
 static hipEvent_t take_event(crdt_ctx *ctx) {
@@ -164,6 +235,9 @@ int crdt_ctx_destroy(crdt_ctx *ctx) {
   for (auto e : ctx->free_events) (void)hipEventDestroy(e);
   if (ctx->scratch) (void)hipFree(ctx->scratch);
   if (ctx->counters) (void)hipFree(ctx->counters);
+  if (ctx->dscratch) (void)hipFree(ctx->dscratch);
+  if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+  if (ctx->pinned_done) (void)hipEventDestroy(ctx->pinned_done);
   delete ctx;
   return CRDT_OK;
 }

@@ -248,7 +248,8 @@ int crdt_lwwreg_lub_many(crdt_ctx *ctx, const uint64_t *marker, const uint64_t *
   if (accumulate && (!out_marker || !out_val))
     return fail(ctx, CRDT_EINVAL, "lwwreg_lub_many: CRDT_ACCUMULATE needs out_marker and out_val");
   if (R == 0 && accumulate) {
-    if (first_conflict) CRDT_HIP(ctx, hipMemsetAsync(first_conflict, 0xFF, G * 8, ctx->stream));
+    if (first_conflict)
+      if (int rc = device_fill(ctx, first_conflict, G * 8, 0xFF)) return rc;
     return CRDT_OK;
   }
   if (R == 0) return fail(ctx, CRDT_EINVAL, "lwwreg_lub_many: R == 0 (LWWReg has no identity; the fold starts at replica 0)");
@@ -284,7 +285,7 @@ int crdt_lwwreg_lub_many(crdt_ctx *ctx, const uint64_t *marker, const uint64_t *
     hipLaunchKernelGGL(lww_chunk_scan, dim3((unsigned)((G + kBlock - 1) / kBlock)), dim3(kBlock), 0,
                        ctx->stream, p);
   if (first_conflict) {
-    CRDT_HIP(ctx, hipMemsetAsync(first_conflict, 0xFF, G * sizeof(uint64_t), ctx->stream));
+    if (int rc = device_fill(ctx, first_conflict, G * sizeof(uint64_t), 0xFF)) return rc;
     hipLaunchKernelGGL(lww_conflict, dim3((unsigned)nparts), dim3(kBlock), 0, ctx->stream, p);
   }
   CRDT_HIP(ctx, hipGetLastError());

@@ -314,8 +314,9 @@ extern "C" int crdt_orswot_lub_many(crdt_ctx *ctx, const crdt_orswot_batch *in,
   const size_t Mw = (M + 63) / 64;
 
   if (R == 0) {
-    CRDT_HIP(ctx, hipMemsetAsync(out->clock, 0, G * A * 8, ctx->stream));
-    CRDT_HIP(ctx, hipMemsetAsync(out->entries, 0, G * M * A * 8, ctx->stream));
+    int rc = device_fill(ctx, out->clock, G * A * 8, 0);
+    if (!rc) rc = device_fill(ctx, out->entries, G * M * A * 8, 0);
+    if (rc) return rc;
   } else {
     const bool vec2 = A % 2 == 0 && in->clock_rstride % 2 == 0 && in->clock_gstride % 2 == 0 &&
                       in->entry_mstride % 2 == 0 && in->entry_rstride % 2 == 0 &&
@@ -381,14 +382,12 @@ extern "C" int crdt_orswot_lub_many(crdt_ctx *ctx, const crdt_orswot_batch *in,
   }
 
   if (D == 0) return CRDT_OK;
-  // Deferred bookkeeping lives in a second scratch region after the join's (the join has been
-  // queued already; growing scratch here synchronises before freeing, so it stays valid).
+  // Deferred bookkeeping lives in its own ctx-owned region (plain hipMalloc, like scratch), so
+  // the join's scratch, possibly still in flight, is untouched.
   const size_t off_b = (G + 1) * sizeof(size_t);
   const size_t need = 256 + ((off_b + 255) / 256 * 256) + D * 8 + D * 4;
-  // Use a dedicated allocation so the join's scratch (possibly still in flight) is untouched.
-  void *dscratch = nullptr;
-  CRDT_HIP(ctx, hipMallocAsync(&dscratch, need, ctx->stream));
-  char *base = static_cast<char *>(dscratch);
+  if (int rc = ensure_dscratch(ctx, need)) return rc;
+  char *base = static_cast<char *>(ctx->dscratch);
   DefPlan q{};
   q.nsurv = reinterpret_cast<unsigned *>(base);
   q.def_off = reinterpret_cast<const size_t *>(base + 256);
@@ -405,14 +404,16 @@ extern "C" int crdt_orswot_lub_many(crdt_ctx *ctx, const crdt_orswot_batch *in,
   q.out_entries = (u64 *)out->entries;
   q.out_keep = out->def_keep;
   q.out_members = (u64 *)out->def_members;
-  CRDT_HIP(ctx, hipMemsetAsync(q.nsurv, 0, 4, ctx->stream));
-  CRDT_HIP(ctx, hipMemcpyAsync((void *)q.def_off, in->def_off, off_b, hipMemcpyHostToDevice, ctx->stream));
-  CRDT_HIP(ctx, hipMemsetAsync(out->def_keep, 0, D, ctx->stream));
-  CRDT_HIP(ctx, hipMemsetAsync(out->def_members, 0, D * Mw * 8, ctx->stream));
+  if (int rc = device_fill(ctx, q.nsurv, 4, 0)) return rc;
+  {  // the caller's def_off may be freed on return: stage it through pinned ctx memory
+    int rc = stage_h2d(ctx, (void *)q.def_off, in->def_off, off_b);
+    if (rc) return rc;
+  }
+  if (int rc = device_fill(ctx, out->def_keep, D, 0)) return rc;
+  if (int rc = device_fill(ctx, out->def_members, D * Mw * 8, 0)) return rc;
   hipLaunchKernelGGL(orswot_deferred_kernel, dim3((unsigned)D), dim3(kBlock), 0, ctx->stream, q);
   hipLaunchKernelGGL(orswot_dedup_kernel, dim3((unsigned)((D + kBlock - 1) / kBlock)), dim3(kBlock), 0,
                      ctx->stream, q);
-  CRDT_HIP(ctx, hipFreeAsync(dscratch, ctx->stream));
   CRDT_HIP(ctx, hipGetLastError());
   return CRDT_OK;
 }

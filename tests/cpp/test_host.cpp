@@ -323,7 +323,31 @@ static void orswot_prop_merge_converges(Gpu &g) {  // test/orswot.rs:33-68
       for (auto &p : ops) w[p.first % i].apply(p.second);
       auto merged = lub_many(g, w);  // == Orswot::new() merged with every witness
       if (!result) result = merged;
-      else ok = ok && (merged == *result);
+      else if (!(merged == *result)) {
+        if (ok) {
+          std::fprintf(stderr, "seed %d i %d mismatch\n", seed, i);
+          for (auto *o : {&*result, &merged}) {
+            std::fprintf(stderr, "  clock:");
+            for (auto &kv : o->clock.dots) std::fprintf(stderr, " %d:%llu", kv.first, (unsigned long long)kv.second);
+            std::fprintf(stderr, "\n  entries:");
+            for (auto &e : o->entries) {
+              std::fprintf(stderr, " m%d{", e.first);
+              for (auto &kv : e.second.dots) std::fprintf(stderr, "%d:%llu ", kv.first, (unsigned long long)kv.second);
+              std::fprintf(stderr, "}");
+            }
+            std::fprintf(stderr, "\n  deferred:");
+            for (auto &d : o->deferred) {
+              std::fprintf(stderr, " {");
+              for (auto &kv : d.first.dots) std::fprintf(stderr, "%d:%llu ", kv.first, (unsigned long long)kv.second);
+              std::fprintf(stderr, "}->[");
+              for (auto m : d.second) std::fprintf(stderr, "%d ", m);
+              std::fprintf(stderr, "]");
+            }
+            std::fprintf(stderr, "\n");
+          }
+        }
+        ok = false;
+      }
     }
     CHECK(ok);
   }

@@ -106,3 +106,60 @@ def test_orswot_lub_many_synth(gpu_ctx, R, M, A):
     np.testing.assert_array_equal(to_host(res.clock), oc)
     np.testing.assert_array_equal(to_host(res.entries), oe)
     assert cg.orswot.deferred_set(inp.def_clock, res.def_keep, res.def_members) == odef
+
+
+def _witness_states(seed, i, n_ops=40):
+    """test/orswot.rs:33-68: random Add/Rm ops routed by actor % i to i witnesses."""
+    rng = np.random.default_rng(seed)
+    ops = []
+    for _ in range(n_ops):
+        actor = int(rng.integers(0, 11))
+        members = set(int(x) for x in rng.integers(0, 8, size=int(rng.integers(1, 4))))
+        counter = int(rng.integers(1, 9))
+        if rng.integers(0, 2) == 0:
+            ops.append((actor, O.OrswotAdd(O.Dot(actor, counter), members)))
+        else:
+            ops.append((actor, O.OrswotRm(O.VClock({actor: counter}), members)))
+    w = [O.Orswot() for _ in range(i)]
+    for a, op in ops:
+        w[a % i].apply(op)
+    return w
+
+
+def _dense(ws, A=11, M=8):
+    R = len(ws)
+    clock = np.zeros((R, A), np.uint64)
+    ent = np.zeros((R, M, A), np.uint64)
+    dcl, dm, off = [], [], [0]
+    for r, w in enumerate(ws):
+        for a, v in w.clock.dots.items():
+            clock[r, a] = v
+        for m, c in w.entries.items():
+            for a, v in c.dots.items():
+                ent[r, m, a] = v
+        for k, ms in w.deferred.items():
+            row = np.zeros(A, np.uint64)
+            for a, v in k.dots.items():
+                row[a] = v
+            bits = np.zeros(1, np.uint64)
+            for m in ms:
+                bits[0] |= np.uint64(1) << np.uint64(m)
+            dcl.append(row)
+            dm.append(bits)
+        off.append(len(dcl))
+    return clock, ent, np.array(off, np.uint64), np.array(dcl, np.uint64).reshape(-1, A), np.array(dm, np.uint64).reshape(-1, 1)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_orswot_witness_convergence_gpu(gpu_ctx, seed):
+    """prop_merge_converges on the GPU: for i in 2..11 witnesses the GPU lub equals the
+    reference fold (oracle) — and is identical when run twice (determinism)."""
+    for i in range(2, 11):
+        ws = _witness_states(seed, i)
+        clock, ent, off, dcl, dm = _dense(ws)
+        oc, oe, odef, _ = O.orswot_fold(clock, ent, off, dcl, dm)
+        for _rep in range(2):
+            c, e, d = _run(gpu_ctx, clock, ent, off, dcl, dm)
+            assert np.array_equal(c, oc), (seed, i, "clock")
+            assert np.array_equal(e, oe), (seed, i, "entries", np.argwhere(e != oe)[:4])
+            assert d == odef, (seed, i, d, odef)
