@@ -175,6 +175,128 @@ struct Orswot {
   }
 };
 
+// ---- MVReg<u64, A> (mvreg.rs) ------------------------------------------------------------
+struct MVReg {
+  std::vector<std::pair<VClock, u64>> vals;  // mvreg.rs:34 (ordered Vec)
+
+  static bool lt(const VClock &x, const VClock &y) { return x.partial_cmp(y) == -1; }
+  void forget(const VClock &clock) {  // mvreg.rs:88-104
+    std::vector<std::pair<VClock, u64>> out;
+    out.reserve(vals.size());
+    for (auto &cv : vals) {
+      VClock c = cv.first;  // .clone().into_iter()
+      c.forget(clock);
+      if (!c.empty()) out.emplace_back(std::move(c), cv.second);
+    }
+    vals = std::move(out);
+  }
+  void merge(MVReg &&other) {  // mvreg.rs:112-128
+    std::vector<std::pair<VClock, u64>> kept;
+    for (auto &cv : vals) {
+      size_t n = 0;
+      for (auto &o : other.vals) n += lt(cv.first, o.first);
+      if (n == 0) kept.push_back(std::move(cv));
+    }
+    vals = std::move(kept);
+    std::vector<std::pair<VClock, u64>> add;
+    for (auto &o : other.vals) {
+      size_t n = 0;
+      for (auto &s : vals) n += lt(o.first, s.first);
+      if (n != 0) continue;
+      bool all_ne = true;
+      for (auto &s : vals) all_ne &= !(o.first == s.first);
+      if (all_ne) add.push_back(std::move(o));
+    }
+    for (auto &x : add) vals.push_back(std::move(x));
+  }
+};
+
+// ---- Map<u32, MVReg<u64>, A> (map.rs) ---------------------------------------------------------
+struct MapEntry {
+  VClock clock;  // map.rs:42
+  MVReg val;     // map.rs:45
+};
+
+struct MapMV {
+  VClock clock;                                      // map.rs:35
+  std::map<uint32_t, MapEntry> entries;              // map.rs:36 (BTreeMap)
+  std::map<VClock, std::set<uint32_t>> deferred;     // map.rs:37 (keyed by whole clock)
+
+  void apply_keyset_rm(std::set<uint32_t> keyset, VClock clock_rm) {  // map.rs:318-348
+    for (uint32_t key : keyset) {
+      auto it = entries.find(key);
+      if (it != entries.end()) {
+        it->second.clock.forget(clock_rm);
+        if (it->second.clock.empty()) entries.erase(it);
+        else it->second.val.forget(clock_rm);
+      }
+    }
+    int c = clock.partial_cmp(clock_rm);
+    if (c == 2 /*None*/ || c == -1 /*Less*/) {
+      auto it = deferred.find(clock_rm);
+      if (it != deferred.end()) it->second.insert(keyset.begin(), keyset.end());
+      else deferred.emplace(std::move(clock_rm), std::move(keyset));
+    }
+  }
+  void apply_deferred() {  // map.rs:311-316
+    auto d = std::move(deferred);
+    deferred.clear();
+    for (auto &kv : d) apply_keyset_rm(kv.second, kv.first);
+  }
+  void merge(MapMV &&other) {  // map.rs:140-220
+    // :142-165 rebuild self.entries
+    for (auto it = entries.begin(); it != entries.end();) {
+      if (other.entries.find(it->first) == other.entries.end()) {
+        MapEntry &e = it->second;
+        if (other.clock.geq(e.clock)) {
+          it = entries.erase(it);  // other has seen this entry and dropped it
+          continue;
+        }
+        e.clock.forget(other.clock);
+        VClock removed_information = other.clock;
+        removed_information.forget(e.clock);
+        e.val.forget(removed_information);
+      }
+      ++it;
+    }
+    // :167-210
+    for (auto &kv : other.entries) {
+      MapEntry &entry = kv.second;
+      auto it = entries.find(kv.first);
+      if (it != entries.end()) {
+        MapEntry &our = it->second;
+        VClock common = VClock::intersection(entry.clock, our.clock);
+        common.merge(entry.clock.clone_without(clock));
+        common.merge(our.clock.clone_without(other.clock));
+        if (common.empty()) {
+          entries.erase(it);
+        } else {
+          our.val.merge(std::move(entry.val));
+          VClock deleted = entry.clock;
+          deleted.merge(VClock(our.clock));
+          deleted.forget(common);
+          our.val.forget(deleted);
+          our.clock = std::move(common);
+        }
+      } else {
+        if (clock.geq(entry.clock)) {
+          // we've seen this entry and dropped it
+        } else {
+          entry.clock.forget(clock);
+          VClock we_deleted = clock;
+          we_deleted.forget(entry.clock);
+          entry.val.forget(we_deleted);
+          entries.emplace(kv.first, std::move(entry));
+        }
+      }
+    }
+    // :213-215
+    for (auto &kv : other.deferred) apply_keyset_rm(kv.second, kv.first);
+    clock.merge(std::move(other.clock));  // :217
+    apply_deferred();                     // :219
+  }
+};
+
 }  // namespace oracle
 
 using namespace oracle;
@@ -328,6 +450,87 @@ double oracle_orswot_fold(const uint64_t *clock, const uint64_t *entries, size_t
       vclock_to_row(kv.first, out_def_clock + k * A, A);
       std::memset(out_def_members + k * Mw, 0, Mw * 8);
       for (Member m : kv.second) out_def_members[k * Mw + m / 64] |= 1ull << (m % 64);
+    }
+    ++k;
+  }
+  *out_ndef = k;
+  return t1 - t0;
+}
+
+// ---- Map<u32, MVReg<u64>> fold from Map::new() over R dense replicas ------------------------
+// Replica r: clock[r*A + a]; entry clock ec[(r*K + k)*A + a] (key absent <=> row all 0); val
+// slots s < V: clock vclk[((r*K + k)*V + s)*A + a] (slot empty <=> row all 0, used slots come
+// first, in Vec order) and value vval[(r*K + k)*V + s].  Deferred removes of replica r are
+// d in [def_off[r], def_off[r+1]): rm clock def_clock[d*A..], key bitmap def_keys[d*Kw..].
+// Output (dense, Vout slots per key): out_clock[A], out_ec[K*A], out_vclk[K*Vout*A],
+// out_vval[K*Vout], out_nval[K] (true number of vals; > Vout means the slots overflowed), and
+// the surviving deferred removes as in oracle_orswot_fold.  Returns fold seconds.
+double oracle_map_fold(const uint64_t *clock, const uint64_t *ec, const uint64_t *vclk,
+                       const uint64_t *vval, size_t R, size_t K, size_t A, size_t V,
+                       const uint64_t *def_off, const uint64_t *def_clock, const uint64_t *def_keys,
+                       size_t Vout, uint64_t *out_clock, uint64_t *out_ec, uint64_t *out_vclk,
+                       uint64_t *out_vval, uint64_t *out_nval, uint64_t *out_def_clock,
+                       uint64_t *out_def_keys, size_t max_def, size_t *out_ndef) {
+  const size_t Kw = (K + 63) / 64;
+  std::vector<MapMV> reps(R);
+  for (size_t r = 0; r < R; ++r) {
+    MapMV &m = reps[r];
+    m.clock = vclock_from_row(clock + r * A, A);
+    for (size_t k = 0; k < K; ++k) {
+      VClock e = vclock_from_row(ec + (r * K + k) * A, A);
+      if (e.empty()) continue;
+      MapEntry ent;
+      ent.clock = std::move(e);
+      for (size_t s = 0; s < V; ++s) {
+        VClock c = vclock_from_row(vclk + ((r * K + k) * V + s) * A, A);
+        if (!c.empty()) ent.val.vals.emplace_back(std::move(c), vval[(r * K + k) * V + s]);
+      }
+      m.entries.emplace((uint32_t)k, std::move(ent));
+    }
+    if (def_off)
+      for (uint64_t d = def_off[r]; d < def_off[r + 1]; ++d) {
+        VClock rm = vclock_from_row(def_clock + d * A, A);
+        std::set<uint32_t> keys;
+        for (size_t w = 0; w < Kw; ++w) {
+          uint64_t x = def_keys[d * Kw + w];
+          while (x) {
+            int b = __builtin_ctzll(x);
+            x &= x - 1;
+            keys.insert((uint32_t)(w * 64 + b));
+          }
+        }
+        auto it = m.deferred.find(rm);
+        if (it != m.deferred.end()) it->second.insert(keys.begin(), keys.end());
+        else m.deferred.emplace(std::move(rm), std::move(keys));
+      }
+  }
+  double t0 = now_s();
+  MapMV acc;
+  for (auto &r : reps) acc.merge(std::move(r));
+  double t1 = now_s();
+  vclock_to_row(acc.clock, out_clock, A);
+  std::memset(out_ec, 0, K * A * 8);
+  std::memset(out_vclk, 0, K * Vout * A * 8);
+  std::memset(out_vval, 0, K * Vout * 8);
+  std::memset(out_nval, 0, K * 8);
+  for (auto &kv : acc.entries) {
+    const size_t k = kv.first;
+    vclock_to_row(kv.second.clock, out_ec + k * A, A);
+    out_nval[k] = kv.second.val.vals.size();
+    size_t s = 0;
+    for (auto &cv : kv.second.val.vals) {
+      if (s >= Vout) break;
+      vclock_to_row(cv.first, out_vclk + (k * Vout + s) * A, A);
+      out_vval[k * Vout + s] = cv.second;
+      ++s;
+    }
+  }
+  size_t k = 0;
+  for (auto &kv : acc.deferred) {
+    if (k < max_def) {
+      vclock_to_row(kv.first, out_def_clock + k * A, A);
+      std::memset(out_def_keys + k * Kw, 0, Kw * 8);
+      for (uint32_t key : kv.second) out_def_keys[k * Kw + key / 64] |= 1ull << (key % 64);
     }
     ++k;
   }
