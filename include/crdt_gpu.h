@@ -160,6 +160,63 @@ typedef struct crdt_orswot_out {
 
 int crdt_orswot_lub_many(crdt_ctx *ctx, const crdt_orswot_batch *in, crdt_orswot_out *out);
 
+/* ---- Map<K, MVReg<u64, A>, A> --------------------------------------------------------------
+ * Replaces Map::merge (map.rs:140-220) with V = MVReg (MVReg::merge mvreg.rs:112-128,
+ * MVReg::forget :88-104), incl. apply_keyset_rm (map.rs:318-348) and apply_deferred (:311-316),
+ * folded as acc = Map::new(); for r in 0..R: acc.merge(replica[g][r]).  Exact for any input
+ * (no associativity is assumed: each key is folded in replica order).
+ * Dense layout per replica (g, r) — keys, actors and MVReg values interned by the caller:
+ *   clock C[a]            at clock + g*clock_gstride + r*clock_rstride + a
+ *   entry clocks EC[k][a] at ec    + g*ec_gstride    + r*ec_rstride    + k*A + a
+ *                          (key absent <=> row all 0)
+ *   value clocks VC[k][s][a] at vclk + g*vclk_gstride + r*vclk_rstride + (k*V + s)*A + a and
+ *   values VV[k][s]         at vval + g*vval_gstride + r*vval_rstride + k*V + s, for the
+ *                          s < V value slots of the key's MVReg in Vec order (slot empty <=>
+ *                          clock row all 0; empty slots are skipped)
+ *   deferred removes pooled per group (CSR): group g owns d in [def_off[g], def_off[g+1])
+ *     (def_off a HOST array of G+1 entries), held by replica def_row[d] of the group (device
+ *     u32, non-decreasing within the group, < R), rm clock def_clock[d*A + a], key bitmap
+ *     def_keys[d*Kw + w], Kw = ceil(K/64).
+ * Output per group g (packed): clock[g*A + a], ec[(g*K + k)*A + a], value slots s < Vout:
+ * vclk[((g*K + k)*Vout + s)*A + a], vval[(g*K + k)*Vout + s]; nval[g*K + k] = number of values
+ * (may be NULL); flags[g] (required): bit 0 = some key folded to more than Vout values (its
+ * slots are then incomplete: retry with a larger Vout), bit 1 = def_row not non-decreasing or
+ * >= R, bit 2 = the fold state of some key needed more values than it holds (results of the
+ * group incomplete: retry with Vstate = 8).  The state holds VO = 2*pow2(V') values, V' the
+ * smallest power of two with V' >= V and 2V' >= min(8, max(Vout, Vstate)); VO <= 8.
+ * Deferred output as for Orswot (def_keep / def_keys over keys).
+ * Limits: A <= 256, V <= 4, Vout <= 64. */
+typedef struct crdt_map_batch {
+  size_t G, R, K, A, V;
+  const uint64_t *clock;
+  size_t clock_rstride, clock_gstride;
+  const uint64_t *ec;
+  size_t ec_rstride, ec_gstride;
+  const uint64_t *vclk;
+  size_t vclk_rstride, vclk_gstride;
+  const uint64_t *vval;
+  size_t vval_rstride, vval_gstride;
+  const size_t *def_off; /* host, G+1 entries; NULL or all-zero = no deferred removes */
+  const uint32_t *def_row;
+  const uint64_t *def_clock;
+  const uint64_t *def_keys;
+} crdt_map_batch;
+
+typedef struct crdt_map_out {
+  size_t Vout;
+  size_t Vstate; /* value capacity hint for the fold state (0 = from Vout and V) */
+  uint64_t *clock; /* [G][A]          */
+  uint64_t *ec;    /* [G][K][A]       */
+  uint64_t *vclk;  /* [G][K][Vout][A] */
+  uint64_t *vval;  /* [G][K][Vout]    */
+  uint32_t *nval;  /* [G][K] or NULL  */
+  uint32_t *flags; /* [G]             */
+  uint8_t *def_keep; /* [D]     */
+  uint64_t *def_keys; /* [D][Kw] */
+} crdt_map_out;
+
+int crdt_map_lub_many(crdt_ctx *ctx, const crdt_map_batch *in, crdt_map_out *out);
+
 /* ---- synthetic inputs (bench / test data, generated in HBM) --------------------------------
  * Counter-based and reproducible on the CPU (tests/golden/make_golden.py restates them).
  * kind 0 = clock/counter cells, 1 = GSet bitmap words, 2 = LWW markers, 3 = LWW vals.

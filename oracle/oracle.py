@@ -731,7 +731,7 @@ def lib():
         L.oracle_orswot_fold.argtypes = [P, P, S, S, S, P, P, P, P, P, P, P, S, ctypes.POINTER(S)]
         L.oracle_orswot_fold.restype = ctypes.c_double
         L.oracle_map_fold.argtypes = [P, P, P, P, S, S, S, S, P, P, P, S, P, P, P, P, P, P, P, S,
-                                      ctypes.POINTER(S)]
+                                      ctypes.POINTER(S), P]
         L.oracle_map_fold.restype = ctypes.c_double
         _LIB = L
     return _LIB
@@ -1094,9 +1094,11 @@ def dense_map_fold(clock, ec, vclk, vval, def_row, def_clock, def_keys, Vout: in
     return P[R].copy(), o_ec, o_vc, o_vv, o_n, deferred
 
 
-def map_fold(clock, ec, vclk, vval, def_row=None, def_clock=None, def_keys=None, Vout: int = 4):
+def map_fold(clock, ec, vclk, vval, def_row=None, def_clock=None, def_keys=None, Vout: int = 4,
+             peak: Optional[np.ndarray] = None):
     """C++ twin (ref_fold.cpp oracle_map_fold): the reference fold over map-based states.
-    Returns (clock, ec, vclk, vval, nval, deferred set, fold seconds)."""
+    Returns (clock, ec, vclk, vval, nval, deferred set, fold seconds); `peak` (K,) u64, if
+    given, receives the most values each key held after any step's entry join."""
     clock, ec, vclk, vval = _c64(clock), _c64(ec), _c64(vclk), _c64(vval)
     R, K, A = ec.shape
     V = vclk.shape[2]
@@ -1123,7 +1125,8 @@ def map_fold(clock, ec, vclk, vval, def_row=None, def_clock=None, def_keys=None,
     nd = ctypes.c_size_t(0)
     t = lib().oracle_map_fold(_p(clock), _p(ec), _p(vclk), _p(vval), R, K, A, V, _p(def_off),
                               _p(def_clock), _p(def_keys), Vout, _p(oc), _p(oe), _p(ovc), _p(ovv),
-                              _p(on), _p(odc), _p(odk), maxd, ctypes.byref(nd))
+                              _p(on), _p(odc), _p(odk), maxd, ctypes.byref(nd),
+                              _p(peak) if peak is not None else None)
     n = nd.value
     assert n <= maxd
     deferred = {(tuple(int(x) for x in odc[k]), bitmap_members(odk[k])) for k in range(n)}

@@ -221,6 +221,7 @@ struct MapMV {
   VClock clock;                                      // map.rs:35
   std::map<uint32_t, MapEntry> entries;              // map.rs:36 (BTreeMap)
   std::map<VClock, std::set<uint32_t>> deferred;     // map.rs:37 (keyed by whole clock)
+  uint64_t *peak = nullptr;  // test instrumentation: max values per key after each entry join
 
   void apply_keyset_rm(std::set<uint32_t> keyset, VClock clock_rm) {  // map.rs:318-348
     for (uint32_t key : keyset) {
@@ -290,6 +291,9 @@ struct MapMV {
         }
       }
     }
+    if (peak)
+      for (auto &kv : entries)
+        if (kv.second.val.vals.size() > peak[kv.first]) peak[kv.first] = kv.second.val.vals.size();
     // :213-215
     for (auto &kv : other.deferred) apply_keyset_rm(kv.second, kv.first);
     clock.merge(std::move(other.clock));  // :217
@@ -464,13 +468,15 @@ double oracle_orswot_fold(const uint64_t *clock, const uint64_t *entries, size_t
 // d in [def_off[r], def_off[r+1]): rm clock def_clock[d*A..], key bitmap def_keys[d*Kw..].
 // Output (dense, Vout slots per key): out_clock[A], out_ec[K*A], out_vclk[K*Vout*A],
 // out_vval[K*Vout], out_nval[K] (true number of vals; > Vout means the slots overflowed), and
-// the surviving deferred removes as in oracle_orswot_fold.  Returns fold seconds.
+// the surviving deferred removes as in oracle_orswot_fold; out_peak[K] (may be NULL) = the most
+// values a key held after any step's entry join.  Returns fold seconds.
 double oracle_map_fold(const uint64_t *clock, const uint64_t *ec, const uint64_t *vclk,
                        const uint64_t *vval, size_t R, size_t K, size_t A, size_t V,
                        const uint64_t *def_off, const uint64_t *def_clock, const uint64_t *def_keys,
                        size_t Vout, uint64_t *out_clock, uint64_t *out_ec, uint64_t *out_vclk,
                        uint64_t *out_vval, uint64_t *out_nval, uint64_t *out_def_clock,
-                       uint64_t *out_def_keys, size_t max_def, size_t *out_ndef) {
+                       uint64_t *out_def_keys, size_t max_def, size_t *out_ndef,
+                       uint64_t *out_peak) {
   const size_t Kw = (K + 63) / 64;
   std::vector<MapMV> reps(R);
   for (size_t r = 0; r < R; ++r) {
@@ -504,8 +510,10 @@ double oracle_map_fold(const uint64_t *clock, const uint64_t *ec, const uint64_t
         else m.deferred.emplace(std::move(rm), std::move(keys));
       }
   }
+  if (out_peak) std::memset(out_peak, 0, K * 8);
   double t0 = now_s();
   MapMV acc;
+  acc.peak = out_peak;
   for (auto &r : reps) acc.merge(std::move(r));
   double t1 = now_s();
   vclock_to_row(acc.clock, out_clock, A);

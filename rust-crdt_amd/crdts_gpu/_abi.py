@@ -28,7 +28,8 @@ EXPORTS = (
     "crdt_pncounter_lub_many", "crdt_pncounter_merge_batch",
     "crdt_gset_lub_many", "crdt_gset_merge_batch",
     "crdt_lwwreg_lub_many", "crdt_lwwreg_merge_batch",
-    "crdt_orswot_lub_many", "crdt_synth_fill", "crdt_synth_orswot", "crdt_synth_orswot_rm",
+    "crdt_orswot_lub_many", "crdt_map_lub_many",
+    "crdt_synth_fill", "crdt_synth_orswot", "crdt_synth_orswot_rm",
 )
 
 
@@ -62,6 +63,22 @@ class OrswotOut(ctypes.Structure):
     _fields_ = [("clock", P), ("entries", P), ("def_keep", P), ("def_members", P)]
 
 
+class MapBatch(ctypes.Structure):  # crdt_map_batch
+    _fields_ = [
+        ("G", S), ("R", S), ("K", S), ("A", S), ("V", S),
+        ("clock", P), ("clock_rstride", S), ("clock_gstride", S),
+        ("ec", P), ("ec_rstride", S), ("ec_gstride", S),
+        ("vclk", P), ("vclk_rstride", S), ("vclk_gstride", S),
+        ("vval", P), ("vval_rstride", S), ("vval_gstride", S),
+        ("def_off", ctypes.POINTER(S)), ("def_row", P), ("def_clock", P), ("def_keys", P),
+    ]
+
+
+class MapOut(ctypes.Structure):  # crdt_map_out
+    _fields_ = [("Vout", S), ("Vstate", S), ("clock", P), ("ec", P), ("vclk", P), ("vval", P), ("nval", P),
+                ("flags", P), ("def_keep", P), ("def_keys", P)]
+
+
 _SIGS = {
     "crdt_ctx_create": ([ctypes.c_int, ctypes.POINTER(P)], ctypes.c_int),
     "crdt_ctx_destroy": ([P], ctypes.c_int),
@@ -79,6 +96,7 @@ _SIGS = {
     "crdt_lwwreg_lub_many": ([P, P, P, S, S, S, P, P, P, ctypes.c_uint], ctypes.c_int),
     "crdt_lwwreg_merge_batch": ([P, P, P, P, P, S, P], ctypes.c_int),
     "crdt_orswot_lub_many": ([P, ctypes.POINTER(OrswotBatch), ctypes.POINTER(OrswotOut)], ctypes.c_int),
+    "crdt_map_lub_many": ([P, ctypes.POINTER(MapBatch), ctypes.POINTER(MapOut)], ctypes.c_int),
 }
 for _t in ("vclock", "gcounter", "pncounter", "gset"):
     _SIGS[f"crdt_{_t}_lub_many"] = ([P, P, S, S, S, S, S, P, S, ctypes.c_uint], ctypes.c_int)

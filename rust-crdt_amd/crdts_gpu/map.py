@@ -1,0 +1,144 @@
+"""Batched `Map<K, MVReg<u64, A>, A>` merge (reference: src/map.rs:140-220, src/mvreg.rs:112-128).
+
+Dense layout (keys, actors and MVReg values interned to indices / u64 by the caller, see
+`intern`):
+    clock (R, A)        or (G, R, A)         replica map clocks
+    ec    (R, K, A)     or (G, R, K, A)      entry clocks; key absent <=> row all 0
+    vclk  (R, K, V, A)  or (G, R, K, V, A)   MVReg value clocks, slots in Vec order (empty <=> 0)
+    vval  (R, K, V)     or (G, R, K, V)      MVReg values
+    deferred removes pooled per group:
+        def_off   host sequence of G+1 offsets (group g owns [def_off[g], def_off[g+1]))
+        def_row   (D,) device int32: replica index within the group (non-decreasing per group)
+        def_clock (D, A) rm clocks; def_keys (D, ceil(K/64)) key bitmaps
+
+lub_many computes, per group, the exact left fold `acc = Map::new(); for r: acc.merge(r)`
+(test/map.rs:660-692 merges this way) and returns MapLub(clock (G,A), ec (G,K,A),
+vclk (G,K,Vout,A), vval (G,K,Vout), nval (G,K) int32, flags (G,) int32, def_keep, def_keys).
+With check=True (default) a flagged group raises: bit 0 = more than `vout` values on a key
+(retry with a larger vout), bit 1 = def_row not sorted / out of range; bit 2 (the fold state
+ran out of value slots mid-fold) first reruns the fold with the largest state (8 values).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import NamedTuple, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _abi
+from .context import Context
+
+
+class MapLub(NamedTuple):
+    clock: torch.Tensor
+    ec: torch.Tensor
+    vclk: torch.Tensor
+    vval: torch.Tensor
+    nval: torch.Tensor
+    flags: torch.Tensor
+    def_keep: Optional[torch.Tensor]
+    def_keys: Optional[torch.Tensor]
+
+
+class MapCapacityError(RuntimeError):
+    """A folded key holds more MVReg values than the output slots (flags bit 0)."""
+
+
+def lub_many(clock: torch.Tensor, ec: torch.Tensor, vclk: torch.Tensor, vval: torch.Tensor,
+             def_off: Optional[Sequence[int]] = None, def_row: Optional[torch.Tensor] = None,
+             def_clock: Optional[torch.Tensor] = None, def_keys: Optional[torch.Tensor] = None,
+             vout: int = 4, ctx: Optional[Context] = None, check: bool = True,
+             vstate: int = 0) -> MapLub:
+    ctx = ctx or Context.default(clock.device.index)
+    for t, nm in ((clock, "clock"), (ec, "ec"), (vclk, "vclk"), (vval, "vval")):
+        ctx.check_tensor(t, f"map.lub_many({nm})")
+    squeeze = clock.dim() == 2
+    c = clock.unsqueeze(0) if squeeze else clock
+    e = ec.unsqueeze(0) if squeeze else ec
+    vc = vclk.unsqueeze(0) if squeeze else vclk
+    vv = vval.unsqueeze(0) if squeeze else vval
+    if c.dim() != 3 or e.dim() != 4 or vc.dim() != 5 or vv.dim() != 4:
+        raise ValueError("map.lub_many: clock (G,R,A), ec (G,R,K,A), vclk (G,R,K,V,A), vval (G,R,K,V) expected")
+    G, R, A = c.shape
+    K, V = e.shape[2], vc.shape[3]
+    if (tuple(e.shape) != (G, R, K, A) or tuple(vc.shape) != (G, R, K, V, A)
+            or tuple(vv.shape) != (G, R, K, V)):
+        raise ValueError(f"map.lub_many: shapes clock {tuple(c.shape)} ec {tuple(e.shape)} "
+                         f"vclk {tuple(vc.shape)} vval {tuple(vv.shape)} do not agree")
+    # per-replica blocks must be packed (strides only on the replica and group axes)
+    for t, nm, inner in ((c, "clock", (1,)), (e, "ec", (A, 1)), (vc, "vclk", (V * A, A, 1)),
+                         (vv, "vval", (V, 1))):
+        if tuple(t.stride()[2:]) != inner:
+            raise ValueError(f"map.lub_many: {nm} must be packed within a replica")
+    Kw = (K + 63) // 64
+    dev = clock.device
+    out_clock = torch.empty((G, A), dtype=torch.int64, device=dev)
+    out_ec = torch.empty((G, K, A), dtype=torch.int64, device=dev)
+    out_vc = torch.empty((G, K, vout, A), dtype=torch.int64, device=dev)
+    out_vv = torch.empty((G, K, vout), dtype=torch.int64, device=dev)
+    nval = torch.empty((G, K), dtype=torch.int32, device=dev)
+    flags = torch.empty(G, dtype=torch.int32, device=dev)
+    b = _abi.MapBatch()
+    b.G, b.R, b.K, b.A, b.V = G, R, K, A, V
+    b.clock, b.clock_rstride, b.clock_gstride = c.data_ptr(), c.stride(1), c.stride(0)
+    b.ec, b.ec_rstride, b.ec_gstride = e.data_ptr(), e.stride(1), e.stride(0)
+    b.vclk, b.vclk_rstride, b.vclk_gstride = vc.data_ptr(), vc.stride(1), vc.stride(0)
+    b.vval, b.vval_rstride, b.vval_gstride = vv.data_ptr(), vv.stride(1), vv.stride(0)
+    o = _abi.MapOut()
+    o.Vout, o.Vstate = vout, vstate
+    o.clock, o.ec, o.vclk, o.vval = out_clock.data_ptr(), out_ec.data_ptr(), out_vc.data_ptr(), out_vv.data_ptr()
+    o.nval, o.flags = nval.data_ptr(), flags.data_ptr()
+    keep = keys_out = None
+    off_arr = None
+    if def_off is not None:
+        off = np.asarray(def_off, dtype=np.uint64)
+        if off.shape != (G + 1,):
+            raise ValueError(f"map.lub_many: def_off must have G+1 = {G + 1} entries")
+        D = int(off[-1])
+        if D > 0:
+            for t, nm in ((def_clock, "def_clock"), (def_keys, "def_keys")):
+                if t is None:
+                    raise ValueError(f"map.lub_many: {nm} required with deferred removes")
+                ctx.check_tensor(t, f"map.lub_many({nm})")
+                if not t.is_contiguous():
+                    raise ValueError(f"map.lub_many: {nm} must be contiguous")
+            if def_row is None or def_row.dtype not in (torch.int32, torch.uint32) or not def_row.is_contiguous():
+                raise ValueError("map.lub_many: def_row must be a contiguous int32 device tensor")
+            if tuple(def_clock.shape) != (D, A) or tuple(def_keys.shape) != (D, Kw) or tuple(def_row.shape) != (D,):
+                raise ValueError(f"map.lub_many: def_row {tuple(def_row.shape)} / def_clock "
+                                 f"{tuple(def_clock.shape)} / def_keys {tuple(def_keys.shape)}; expected "
+                                 f"({D},) / ({D},{A}) / ({D},{Kw})")
+            off_arr = (ctypes.c_size_t * (G + 1))(*[int(x) for x in off])
+            b.def_off = ctypes.cast(off_arr, ctypes.POINTER(ctypes.c_size_t))
+            b.def_row, b.def_clock, b.def_keys = def_row.data_ptr(), def_clock.data_ptr(), def_keys.data_ptr()
+            keep = torch.empty(D, dtype=torch.uint8, device=dev)
+            keys_out = torch.empty((D, Kw), dtype=torch.int64, device=dev)
+            o.def_keep, o.def_keys = keep.data_ptr(), keys_out.data_ptr()
+    ctx.call("crdt_map_lub_many", ctypes.byref(b), ctypes.byref(o))
+    if check:
+        f = 0
+        for x in flags.cpu().numpy().tolist():
+            f |= int(x)
+        if f & 2:
+            raise ValueError("map.lub_many: def_row must be non-decreasing within each group and < R")
+        if f & 4 and vstate < 8:  # the fold state overflowed: rerun with the largest state
+            return lub_many(clock, ec, vclk, vval, def_off, def_row, def_clock, def_keys, vout, ctx,
+                            check, vstate=8)
+        if f & 4:
+            raise MapCapacityError("map.lub_many: a key held more than 8 MVReg values during the "
+                                   "fold (the kernel's state capacity); results incomplete")
+        if f & 1:
+            raise MapCapacityError(f"map.lub_many: a key folds to more than vout={vout} values; "
+                                   "retry with a larger vout")
+    res = MapLub(out_clock, out_ec, out_vc, out_vv, nval, flags, keep, keys_out)
+    if squeeze:
+        res = MapLub(out_clock[0], out_ec[0], out_vc[0], out_vv[0], nval[0], flags, keep, keys_out)
+    return res
+
+
+def deferred_set(def_clock: torch.Tensor, def_keep: torch.Tensor, def_keys: torch.Tensor,
+                 lo: int = 0, hi: Optional[int] = None) -> set:
+    """Egress of the surviving deferred removes: {(rm clock tuple, frozenset of key indices)}."""
+    from .orswot import deferred_set as _ds
+    return _ds(def_clock, def_keep, def_keys, lo, hi)

@@ -92,6 +92,24 @@ int device_fill(crdt_ctx *ctx, void *dst, size_t bytes, unsigned char byte);
 void timing_begin(crdt_ctx *ctx, const char *name);
 void timing_end(crdt_ctx *ctx);
 
+// Pooled deferred-remove list of a batch (Orswot members / Map keys): survival !(rm <= final
+// clock), optional ceiling forget on the joined entries, representative + set union of
+// survivors with identical rm clocks (orswot.rs:240-249, map.rs:336-345).
+struct DefPlan {
+  const size_t *def_off;  // device copy, G+1 (set by launch_deferred)
+  unsigned long long G, D, M, A, Mw;
+  const u64 *def_clock, *def_members;
+  const u64 *out_clock;
+  u64 *out_entries;   // joined entries [G][M][A] (ceiling target when apply_ceiling)
+  int apply_ceiling;
+  u64 *hash;          // [D]
+  unsigned *surv;     // [D] compacted survivor list
+  unsigned *nsurv;    // counter
+  uint8_t *out_keep;
+  u64 *out_members;
+};
+int launch_deferred(crdt_ctx *ctx, const size_t *host_def_off, DefPlan q);
+
 // Max / OR join on u64 lanes.
 enum class Op : int { Max = 0, Or = 1 };
 

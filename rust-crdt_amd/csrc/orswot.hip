@@ -186,18 +186,6 @@ __global__ __launch_bounds__(kBlock) void orswot_join_kernel(OrPlan p) {
   store_final();
 }
 
-struct DefPlan {
-  const size_t *def_off;  // device copy, G+1
-  unsigned long long G, D, M, A, Mw;
-  const u64 *def_clock, *def_members;
-  const u64 *out_clock;
-  u64 *out_entries;
-  u64 *hash;          // [D]
-  unsigned *surv;     // [D] compacted survivor list
-  unsigned *nsurv;    // counter
-  uint8_t *out_keep;
-  u64 *out_members;
-};
 
 __device__ __forceinline__ unsigned long long group_of(const size_t *off, unsigned long long G,
                                                        unsigned long long d) {
@@ -235,7 +223,7 @@ __global__ __launch_bounds__(kBlock) void orswot_deferred_kernel(DefPlan p) {
   // test reads the joined value, which no other write can change except to zero).
   const u64 *bits = p.def_members + d * p.Mw;
   u64 *E = p.out_entries + g * p.M * p.A;
-  for (unsigned long long w = 0; w < p.Mw; ++w) {
+  for (unsigned long long w = 0; w < p.Mw && p.apply_ceiling; ++w) {
     u64 word = bits[w];
     while (word) {
       const int bit = __builtin_ctzll(word);
@@ -286,6 +274,34 @@ __global__ __launch_bounds__(kBlock) void orswot_dedup_kernel(DefPlan p) {
 }
 
 static bool al16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+// Survival, ceiling (optional) and dedup of a pooled deferred-remove list (shared by Orswot and
+// Map): stages the host def_off, fills the outputs, launches the two kernels.
+int launch_deferred(crdt_ctx *ctx, const size_t *host_def_off, DefPlan q) {
+  const size_t G = q.G, D = q.D;
+  // Deferred bookkeeping lives in its own ctx-owned region (plain hipMalloc, like scratch), so
+  // the join's scratch, possibly still in flight, is untouched.
+  const size_t off_b = (G + 1) * sizeof(size_t);
+  const size_t need = 256 + ((off_b + 255) / 256 * 256) + D * 8 + D * 4;
+  if (int rc = ensure_dscratch(ctx, need)) return rc;
+  char *base = static_cast<char *>(ctx->dscratch);
+  q.nsurv = reinterpret_cast<unsigned *>(base);
+  q.def_off = reinterpret_cast<const size_t *>(base + 256);
+  q.hash = reinterpret_cast<u64 *>(base + 256 + (off_b + 255) / 256 * 256);
+  q.surv = reinterpret_cast<unsigned *>(q.hash + D);
+  if (int rc = device_fill(ctx, q.nsurv, 4, 0)) return rc;
+  {  // the caller's def_off may be freed on return: stage it through pinned ctx memory
+    int rc = stage_h2d(ctx, (void *)q.def_off, host_def_off, off_b);
+    if (rc) return rc;
+  }
+  if (int rc = device_fill(ctx, q.out_keep, D, 0)) return rc;
+  if (int rc = device_fill(ctx, q.out_members, D * q.Mw * 8, 0)) return rc;
+  hipLaunchKernelGGL(orswot_deferred_kernel, dim3((unsigned)D), dim3(kBlock), 0, ctx->stream, q);
+  hipLaunchKernelGGL(orswot_dedup_kernel, dim3((unsigned)((D + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                     ctx->stream, q);
+  CRDT_HIP(ctx, hipGetLastError());
+  return CRDT_OK;
+}
 
 }  // namespace crdt
 
@@ -382,17 +398,7 @@ extern "C" int crdt_orswot_lub_many(crdt_ctx *ctx, const crdt_orswot_batch *in,
   }
 
   if (D == 0) return CRDT_OK;
-  // Deferred bookkeeping lives in its own ctx-owned region (plain hipMalloc, like scratch), so
-  // the join's scratch, possibly still in flight, is untouched.
-  const size_t off_b = (G + 1) * sizeof(size_t);
-  const size_t need = 256 + ((off_b + 255) / 256 * 256) + D * 8 + D * 4;
-  if (int rc = ensure_dscratch(ctx, need)) return rc;
-  char *base = static_cast<char *>(ctx->dscratch);
   DefPlan q{};
-  q.nsurv = reinterpret_cast<unsigned *>(base);
-  q.def_off = reinterpret_cast<const size_t *>(base + 256);
-  q.hash = reinterpret_cast<u64 *>(base + 256 + (off_b + 255) / 256 * 256);
-  q.surv = reinterpret_cast<unsigned *>(q.hash + D);
   q.G = G;
   q.D = D;
   q.M = M;
@@ -402,18 +408,8 @@ extern "C" int crdt_orswot_lub_many(crdt_ctx *ctx, const crdt_orswot_batch *in,
   q.def_members = (const u64 *)in->def_members;
   q.out_clock = (const u64 *)out->clock;
   q.out_entries = (u64 *)out->entries;
+  q.apply_ceiling = 1;
   q.out_keep = out->def_keep;
   q.out_members = (u64 *)out->def_members;
-  if (int rc = device_fill(ctx, q.nsurv, 4, 0)) return rc;
-  {  // the caller's def_off may be freed on return: stage it through pinned ctx memory
-    int rc = stage_h2d(ctx, (void *)q.def_off, in->def_off, off_b);
-    if (rc) return rc;
-  }
-  if (int rc = device_fill(ctx, out->def_keep, D, 0)) return rc;
-  if (int rc = device_fill(ctx, out->def_members, D * Mw * 8, 0)) return rc;
-  hipLaunchKernelGGL(orswot_deferred_kernel, dim3((unsigned)D), dim3(kBlock), 0, ctx->stream, q);
-  hipLaunchKernelGGL(orswot_dedup_kernel, dim3((unsigned)((D + kBlock - 1) / kBlock)), dim3(kBlock), 0,
-                     ctx->stream, q);
-  CRDT_HIP(ctx, hipGetLastError());
-  return CRDT_OK;
+  return launch_deferred(ctx, in->def_off, q);
 }

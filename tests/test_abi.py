@@ -21,6 +21,7 @@ def test_header_declares_expected_surface():
     for t in ("vclock", "gcounter", "pncounter", "gset"):
         assert f"crdt_{t}_lub_many" in names and f"crdt_{t}_merge_batch" in names
     assert "crdt_lwwreg_lub_many" in names and "crdt_orswot_lub_many" in names
+    assert "crdt_map_lub_many" in names
 
 
 def test_library_exports_every_declared_symbol():
@@ -55,3 +56,6 @@ def test_ctypes_struct_layout_matches_header():
     # 4 dims + ptr + 2 strides + ptr + 3 strides + 3 ptrs = 14 eight-byte fields
     assert ctypes.sizeof(abi.OrswotBatch) == 14 * 8
     assert ctypes.sizeof(abi.OrswotOut) == 4 * 8
+    # 5 dims + 4 x (ptr + 2 strides) + def_off + 3 ptrs = 21; out: Vout, Vstate + 8 ptrs = 10
+    assert ctypes.sizeof(abi.MapBatch) == 21 * 8
+    assert ctypes.sizeof(abi.MapOut) == 10 * 8

@@ -1,0 +1,161 @@
+"""GPU parity: Map<K, MVReg<u64>> lub_many vs the oracle's reference fold (C++ twin over
+map-based states, oracle/ref_fold.cpp; itself pinned by the reference's map/mvreg tests and
+cross-checked with the Python twin in tests/test_oracle_map_dense.py).  Bit-exact on entry
+clocks, value clocks, values (in Vec order), value counts and surviving deferred removes."""
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+from gpu_util import to_dev, to_host
+
+pytestmark = pytest.mark.gpu
+
+import crdts_gpu as cg  # noqa: E402
+
+
+def _gpu(gpu_ctx, d, vout, groups=None):
+    """d: dense dict of one group (or stacked when groups = list of per-group D counts)."""
+    D = d["def_clock"].shape[0]
+    kw = {}
+    if D:
+        G = 1 if groups is None else len(groups)
+        off = [0] + list(np.cumsum(groups if groups is not None else [D]))
+        kw = dict(def_off=off,
+                  def_row=torch.from_numpy(np.asarray(d["def_row"], np.int64).astype(np.int32)).cuda(),
+                  def_clock=to_dev(d["def_clock"]), def_keys=to_dev(d["def_keys"]))
+    res = cg.map.lub_many(to_dev(d["clock"]), to_dev(d["ec"]), to_dev(d["vclk"]), to_dev(d["vval"]),
+                          vout=vout, ctx=gpu_ctx, **kw)
+    return res, kw
+
+
+def _check(gpu_ctx, d, vout):
+    exp = O.map_fold(d["clock"], d["ec"], d["vclk"], d["vval"], d["def_row"], d["def_clock"],
+                     d["def_keys"], vout)
+    res, kw = _gpu(gpu_ctx, d, vout)
+    np.testing.assert_array_equal(to_host(res.clock), exp[0])
+    np.testing.assert_array_equal(to_host(res.ec), exp[1])
+    np.testing.assert_array_equal(to_host(res.vclk), exp[2])
+    np.testing.assert_array_equal(to_host(res.vval), exp[3])
+    np.testing.assert_array_equal(res.nval.cpu().numpy(), exp[4])
+    got = cg.map.deferred_set(kw["def_clock"], res.def_keep, res.def_keys) if kw else set()
+    assert got == exp[5]
+    return exp
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_map_lub_many_op_replay(gpu_ctx, seed):
+    rng = np.random.default_rng(seed)
+    K, A = int(rng.integers(1, 70)), int(rng.integers(1, 9))
+    R = int(rng.integers(1, 40))
+    p_rm = float(rng.choice([0.15, 0.3, 0.45]))
+    maps = O.gen_map_replicas(seed, R, K, A, steps=int(rng.integers(20, 300)), p_rm=p_rm, p_up=0.7 - p_rm)
+    V = O.max_vals(maps)
+    d = O.map_to_dense(maps, K, A, V)
+    vout = max(4, O.max_vals([O.map_fold_objects(maps)]))
+    _check(gpu_ctx, d, vout)
+
+
+def _random_dense(rng, R, K, A, V, cmax, D=None, keys_per_rm=None):
+    # replica clocks mostly below the entry clocks, so that entries survive the fold
+    clock = rng.integers(0, max(2, cmax // 2), size=(R, A)).astype(np.uint64)
+    ec = rng.integers(0, cmax, size=(R, K, A)).astype(np.uint64)
+    ec[rng.random((R, K)) < 0.3] = 0
+    vclk = rng.integers(0, cmax, size=(R, K, V, A)).astype(np.uint64)
+    vclk[rng.random((R, K, V, A)) < 0.4] = 0
+    nv = rng.integers(0, V + 1, size=(R, K))
+    for s in range(V):
+        vclk[:, :, s][nv <= s] = 0
+    vval = rng.integers(0, 7, size=(R, K, V)).astype(np.uint64)
+    D = int(rng.integers(0, R // 2 + 2)) if D is None else D
+    def_row = np.sort(rng.integers(0, R, size=D)).astype(np.uint64)
+    def_clock = rng.integers(0, cmax + 2, size=(D, A)).astype(np.uint64)
+    Kw = (K + 63) // 64
+    def_keys = np.zeros((D, Kw), np.uint64)
+    for d in range(D):
+        n = int(rng.integers(1, K + 1)) if keys_per_rm is None else min(K, keys_per_rm)
+        for k in rng.choice(K, size=n, replace=False):
+            def_keys[d, k // 64] |= np.uint64(1) << np.uint64(k % 64)
+    return dict(clock=clock, ec=ec, vclk=vclk, vval=vval, def_row=def_row, def_clock=def_clock,
+                def_keys=def_keys)
+
+
+@pytest.mark.parametrize("seed,R,K,A,V,cmax", [
+    (1, 1, 1, 1, 1, 4), (2, 7, 3, 2, 2, 5), (3, 40, 9, 4, 2, 6), (4, 25, 5, 33, 2, 3),
+    (5, 12, 4, 64, 1, 3), (6, 10, 6, 65, 1, 3), (7, 6, 3, 200, 1, 3), (8, 50, 130, 3, 3, 5),
+    (9, 30, 8, 8, 2, 4), (10, 33, 2, 5, 2, 1000), (11, 16, 5, 100, 2, 2), (12, 64, 3, 2, 4, 3),
+])
+def test_map_lub_many_arbitrary(gpu_ctx, seed, R, K, A, V, cmax):
+    """Arbitrary dense states: exactness of the left fold does not rest on any invariant."""
+    rng = np.random.default_rng(seed)
+    d = _random_dense(rng, R, K, A, V, cmax)
+    peak = np.zeros(K, np.uint64)
+    exp = O.map_fold(d["clock"], d["ec"], d["vclk"], d["vval"], d["def_row"], d["def_clock"],
+                     d["def_keys"], 64, peak=peak)
+    vout = max(1, int(exp[4].max()) if exp[4].size else 1)
+    if int(peak.max()) > 8:  # beyond the kernel's state capacity: must be reported, not wrong
+        with pytest.raises(cg.map.MapCapacityError):
+            _gpu(gpu_ctx, d, vout)
+        return
+    _check(gpu_ctx, d, vout)
+
+
+def test_map_many_concurrent_deferred(gpu_ctx):
+    """More than the 4 register-tracked removes active on one key: the rescan path."""
+    rng = np.random.default_rng(77)
+    R, K, A = 40, 3, 4
+    d = _random_dense(rng, R, K, A, 2, cmax=3, D=60, keys_per_rm=K)
+    d["def_clock"][:, 0] = 50  # never dominated: every remove stays active to the end
+    exp = O.map_fold(d["clock"], d["ec"], d["vclk"], d["vval"], d["def_row"], d["def_clock"],
+                     d["def_keys"], 64)
+    _check(gpu_ctx, d, max(1, int(exp[4].max())))
+
+
+def test_map_groups(gpu_ctx):
+    G, R, K, A = 3, 15, 10, 5
+    parts = []
+    for g in range(G):
+        maps = O.gen_map_replicas(500 + g, R, K, A, steps=150, p_rm=0.3, p_up=0.4)
+        parts.append(O.map_to_dense(maps, K, A, 3))
+    st = {k: np.stack([p[k] for p in parts]) for k in ("clock", "ec", "vclk", "vval")}
+    st["def_row"] = np.concatenate([p["def_row"] for p in parts])
+    st["def_clock"] = np.concatenate([p["def_clock"] for p in parts])
+    st["def_keys"] = np.concatenate([p["def_keys"] for p in parts])
+    counts = [p["def_row"].shape[0] for p in parts]
+    res, kw = _gpu(gpu_ctx, st, 6, groups=counts)
+    off = np.cumsum([0] + counts)
+    for g, p in enumerate(parts):
+        exp = O.map_fold(p["clock"], p["ec"], p["vclk"], p["vval"], p["def_row"], p["def_clock"],
+                         p["def_keys"], 6)
+        np.testing.assert_array_equal(to_host(res.clock[g]), exp[0])
+        np.testing.assert_array_equal(to_host(res.ec[g]), exp[1])
+        np.testing.assert_array_equal(to_host(res.vclk[g]), exp[2])
+        np.testing.assert_array_equal(to_host(res.vval[g]), exp[3])
+        got = cg.map.deferred_set(kw["def_clock"], res.def_keep, res.def_keys, int(off[g]), int(off[g + 1])) if kw else set()
+        assert got == exp[5]
+
+
+def test_map_empty_and_errors(gpu_ctx):
+    A, K = 3, 4
+    z = lambda *s: torch.zeros(s, dtype=torch.int64, device="cuda:0")  # noqa: E731
+    res = cg.map.lub_many(z(0, A), z(0, K, A), z(0, K, 2, A), z(0, K, 2), ctx=gpu_ctx)
+    assert not to_host(res.clock).any() and not to_host(res.ec).any() and not to_host(res.vclk).any()
+    # capacity: three concurrent values folded into vout=2 slots
+    rng = np.random.default_rng(3)
+    clock = np.zeros((3, A), np.uint64)
+    ec = np.zeros((3, K, A), np.uint64)
+    vclk = np.zeros((3, K, 1, A), np.uint64)
+    vval = np.zeros((3, K, 1), np.uint64)
+    for r in range(3):
+        clock[r, r] = ec[r, 0, r] = vclk[r, 0, 0, r] = 1
+        vval[r, 0, 0] = 10 + r
+    with pytest.raises(cg.map.MapCapacityError):
+        cg.map.lub_many(to_dev(clock), to_dev(ec), to_dev(vclk), to_dev(vval), vout=2, ctx=gpu_ctx)
+    res = cg.map.lub_many(to_dev(clock), to_dev(ec), to_dev(vclk), to_dev(vval), vout=3, ctx=gpu_ctx)
+    assert res.nval.cpu().tolist()[0] == 3
+    assert to_host(res.vval)[0].tolist() == [10, 11, 12]
+    # unsorted deferred rows are reported
+    d = _random_dense(rng, 6, K, A, 1, 4, D=3)
+    d["def_row"] = np.array([4, 1, 2], np.uint64)
+    with pytest.raises(ValueError):
+        _gpu(gpu_ctx, d, 8)
