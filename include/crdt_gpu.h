@@ -240,6 +240,16 @@ int crdt_synth_orswot_rm(crdt_ctx *ctx, uint64_t *entries, size_t M, size_t A, s
                          const uint32_t *def_row, const uint64_t *def_clock,
                          const uint64_t *def_members);
 
+/* Well-formed synthetic Map<K, MVReg<u64>> replicas (config 4), packed clock[R][A],
+ * ec[R][K][A], vclk[R][K][V][A], vval[R][K][V] for global replicas first_row + r; model in
+ * csrc/synth.hip, restated on the CPU by oracle.synth_map.  def_off (device, R+1 local
+ * offsets, may be NULL), def_clock[D][A], def_keys[D][Kw]: the replicas' own deferred removes,
+ * pre-applied (apply_keyset_rm, map.rs:318-333). */
+int crdt_synth_map(crdt_ctx *ctx, uint64_t *clock, uint64_t *ec, uint64_t *vclk, uint64_t *vval,
+                   size_t R, size_t K, size_t A, size_t V, size_t first_row, uint64_t seed,
+                   uint64_t kmax, const uint64_t *def_off, const uint64_t *def_clock,
+                   const uint64_t *def_keys);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1191,3 +1191,142 @@ def gen_map_replicas(seed: int, R: int, K: int, A: int, steps: int = 200, p_ooo:
 
 def max_vals(maps) -> int:
     return max([len(e.val.vals) for m in maps for e in m.entries.values()] + [1])
+
+
+# ---------------------------------------------------------------------------------------
+# Well-formed synthetic Map<K, MVReg<u64>> replicas (config 4): numpy restatement of
+# rust-crdt_amd/csrc/synth.hip crdt_synth_map (bit-exact), used for sampled-key parity.
+# ---------------------------------------------------------------------------------------
+_SALT_KIND = np.uint64(0xA5A5A5A55A5A5A5A)
+_SALT_VAL = np.uint64(0x5EED5EED0B57AC1E)
+_SALT_DEF = np.uint64(0xDEF0DEF0DEF0DEF0)
+
+
+def _key_count(K: int, A: int, res: int) -> int:
+    """#{k < K : k % A == res}."""
+    return (K - res + A - 1) // A if res < K else 0
+
+
+def map_keys_of(a: int, K: int, A: int) -> np.ndarray:
+    """The keys actor a writes, in its round-robin order: k % A == a, then k % A == a-1."""
+    if A == 1:
+        return np.arange(K, dtype=np.int64)
+    prim = np.arange(a, K, A, dtype=np.int64)
+    sec = np.arange((a - 1) % A, K, A, dtype=np.int64)
+    return np.concatenate([prim, sec])
+
+
+def synth_map_clock(seed: int, rows: int, A: int, kmax: int, row0: int = 0) -> np.ndarray:
+    r = np.arange(row0, row0 + rows, dtype=np.uint64)
+    a = np.arange(A, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        c = mix64(np.uint64(seed) + (r[:, None] * np.uint64(A) + a[None, :] + np.uint64(1)) * _GOLD)
+    return (c % np.uint64(kmax + 1)).astype(np.uint64)
+
+
+def _op_hash(seed: int, salt, a, n):
+    with np.errstate(over="ignore"):
+        return mix64((np.uint64(seed) ^ salt) + (np.asarray(a, np.uint64) << np.uint64(32)) + np.asarray(n, np.uint64))
+
+
+def synth_map_deferred(seed: int, rows: int, K: int, A: int, kmax: int, p_def: float = 0.1,
+                       row0: int = 0):
+    """Deferred removes with a future context, per replica (closed form in the replica index,
+    so every rank of a sharded run builds the same global list).  Returns (def_row local,
+    def_clock (D, A), def_keys (D, Kw))."""
+    c = synth_map_clock(seed, rows, A, kmax, row0)
+    Kw = (K + 63) // 64
+    rows_out, dcl, dk = [], [], []
+    thr = int(p_def * 1000)
+    for rl in range(rows):
+        with np.errstate(over="ignore"):
+            h = int(mix64((np.uint64(seed) ^ _SALT_DEF) + np.uint64(row0 + rl)))
+        nd = 1 + (h >> 32) % 2 if h % 1000 < thr else 0
+        for d in range(nd):
+            hd = int(mix64(np.uint64((h + 0x9E37 * (d + 1)) & (2**64 - 1))))
+            w = hd % A
+            rm = np.zeros(A, np.uint64)
+            rm[w] = c[rl, w] + np.uint64(1 + (hd >> 8) % 4)
+            if A > 1:
+                b = (w + 1 + (hd >> 16) % (A - 1)) % A
+                rm[b] = c[rl, b] // np.uint64(2)
+            keys = map_keys_of(w, K, A)
+            bits = np.zeros(Kw, np.uint64)
+            for i in range(1 + (hd >> 24) % 3):
+                j = int(mix64(np.uint64((hd + i + 1) & (2**64 - 1)))) % len(keys)
+                k = int(keys[j])
+                bits[k // 64] |= np.uint64(1) << np.uint64(k % 64)
+            rows_out.append(rl)
+            dcl.append(rm)
+            dk.append(bits)
+    D = len(rows_out)
+    return (np.array(rows_out, np.int64), np.array(dcl, np.uint64).reshape(D, A),
+            np.array(dk, np.uint64).reshape(D, Kw))
+
+
+def synth_map(seed: int, rows: int, K: int, A: int, V: int, kmax: int, row0: int = 0,
+              keys=None, deferred=None, clock_override=None):
+    """Dense replicas [row0, row0+rows) for the key subset `keys` (default all).
+
+    Model (every replica is a causally closed state of one op history): key k is written by
+    actors w0 = k % A and w1 = (k+1) % A; actor a's n-th op (n = 1, 2, ...) targets the
+    ((n-1) mod M_a)-th key of map_keys_of(a) and is a remove (1/8, mix of (a, n)) or an update
+    writing val mix(a, n) with MVReg clock {a: n} (derive_add_ctx of a state that has seen only
+    a's own ops, map.rs:272, ctx.rs:42-48).  Replica r has seen ops 1..c[r][a] of every actor.
+    So entry (r, k) holds, per writer w in (w0, w1) order, w's latest op on k if it is an
+    update: ec[w] = n, one MVReg value ({w: n}, mix(w, n)); a remove (rm clock = w's own entry
+    view, map.rs:291) leaves nothing of w.  Deferred removes (synth_map_deferred) of the replica
+    are pre-applied (apply_keyset_rm, map.rs:318-333): a writer's dot survives iff n > rm[w]."""
+    keys = np.arange(K, dtype=np.int64) if keys is None else np.asarray(keys, np.int64)
+    c = synth_map_clock(seed, rows, A, kmax, row0) if clock_override is None else np.asarray(clock_override, np.uint64)
+    nk = len(keys)
+    ec = np.zeros((rows, nk, A), np.uint64)
+    vclk = np.zeros((rows, nk, V, A), np.uint64)
+    vval = np.zeros((rows, nk, V), np.uint64)
+    ceil = np.zeros((rows, nk, A), np.uint64)
+    if deferred is not None:
+        drow, dcl, dk = deferred
+        pos = {int(k): i for i, k in enumerate(keys)}
+        for d in range(len(drow)):
+            for k in bitmap_members(dk[d]):
+                if k in pos:
+                    i = pos[k]
+                    ceil[drow[d], i] = np.maximum(ceil[drow[d], i], dcl[d])
+    writers = [0] if A == 1 else [0, 1]
+    slot = np.zeros((rows, nk), np.int64)
+    for wi in writers:
+        w = (keys + wi) % A
+        if A == 1:
+            M = np.full(nk, K, np.int64)
+            j = keys.copy()
+        else:
+            P = np.array([_key_count(K, A, int(x)) for x in w], np.int64)
+            S = np.array([_key_count(K, A, int((x - 1) % A)) for x in w], np.int64)
+            M = P + S
+            j = np.where(keys % A == w, keys // A, P + keys // A)
+        cw = c[:, w].astype(np.int64)  # (rows, nk)
+        n = np.where(cw >= j[None] + 1, j[None] + 1 + M[None] * ((cw - j[None] - 1) // M[None]), 0)
+        isrm = (_op_hash(seed, _SALT_KIND, w[None].astype(np.uint64), n.astype(np.uint64)) & np.uint64(7)) == 0
+        val = _op_hash(seed, _SALT_VAL, w[None].astype(np.uint64), n.astype(np.uint64))
+        cl = np.take_along_axis(ceil, np.broadcast_to(w[None, :, None], (rows, nk, 1)), axis=2)[..., 0]
+        live = (n > 0) & ~isrm & (n.astype(np.uint64) > cl)
+        rr, kk = np.nonzero(live)
+        ww = w[kk]
+        ec[rr, kk, ww] = n[rr, kk].astype(np.uint64)
+        s = slot[rr, kk]
+        ok = s < V
+        vclk[rr[ok], kk[ok], s[ok], ww[ok]] = n[rr, kk][ok].astype(np.uint64)
+        vval[rr[ok], kk[ok], s[ok]] = val[rr, kk][ok]
+        slot[rr, kk] += 1
+    return dict(clock=c, ec=ec, vclk=vclk, vval=vval)
+
+
+def restrict_deferred_keys(def_keys: np.ndarray, keys) -> np.ndarray:
+    """Re-index key bitmaps onto a key subset (keys[i] -> bit i); keys are independent in the
+    Map fold given the clocks, so folding a key subset restricts the full fold exactly."""
+    keys = np.asarray(keys, np.int64)
+    out = np.zeros((def_keys.shape[0], (len(keys) + 63) // 64), np.uint64)
+    for i, k in enumerate(keys.tolist()):
+        bit = (def_keys[:, k // 64] >> np.uint64(k % 64)) & np.uint64(1)
+        out[:, i // 64] |= bit << np.uint64(i % 64)
+    return out

@@ -29,7 +29,7 @@ EXPORTS = (
     "crdt_gset_lub_many", "crdt_gset_merge_batch",
     "crdt_lwwreg_lub_many", "crdt_lwwreg_merge_batch",
     "crdt_orswot_lub_many", "crdt_map_lub_many",
-    "crdt_synth_fill", "crdt_synth_orswot", "crdt_synth_orswot_rm",
+    "crdt_synth_fill", "crdt_synth_orswot", "crdt_synth_orswot_rm", "crdt_synth_map",
 )
 
 
@@ -93,6 +93,7 @@ _SIGS = {
     "crdt_synth_fill": ([P, P, S, S, S, S, U64, ctypes.c_int], ctypes.c_int),
     "crdt_synth_orswot": ([P, P, P, S, S, S, S, U64, U64], ctypes.c_int),
     "crdt_synth_orswot_rm": ([P, P, S, S, S, P, P, P], ctypes.c_int),
+    "crdt_synth_map": ([P, P, P, P, P, S, S, S, S, S, U64, U64, P, P, P], ctypes.c_int),
     "crdt_lwwreg_lub_many": ([P, P, P, S, S, S, P, P, P, ctypes.c_uint], ctypes.c_int),
     "crdt_lwwreg_merge_batch": ([P, P, P, P, P, S, P], ctypes.c_int),
     "crdt_orswot_lub_many": ([P, ctypes.POINTER(OrswotBatch), ctypes.POINTER(OrswotOut)], ctypes.c_int),

@@ -89,3 +89,85 @@ def orswot_replicas(ctx: Optional[Context], R: int, M: int, A: int, seed: int, k
         ctx.call("crdt_synth_orswot_rm", dptr(entries), M, A, D, dptr(drow), dptr(dcl), dptr(dmem))
         torch.cuda.current_stream(dev).synchronize()
     return OrswotInput(clock, entries, off, dcl, dmem)
+
+
+class MapInput(NamedTuple):
+    clock: torch.Tensor      # (R, A)
+    ec: torch.Tensor         # (R, K, A)
+    vclk: torch.Tensor       # (R, K, V, A)
+    vval: torch.Tensor       # (R, K, V)
+    def_off: list            # [0, D] (one group)
+    def_row: torch.Tensor    # (D,) int32
+    def_clock: torch.Tensor  # (D, A)
+    def_keys: torch.Tensor   # (D, Kw)
+
+
+def map_deferred(seed: int, R: int, K: int, A: int, kmax: int, p_def: float = 0.1, first_row: int = 0):
+    """Host-side deferred removes of crdt_synth_map's model (closed form in the replica index):
+    replica r holds 1-2 removes with probability p_def, each by a writer w with a future
+    context rm[w] = clock[r][w] + 1..4 (and a past one on a second actor) over 1-3 of w's keys.
+    Returns (def_row local (D,), def_clock (D, A), def_keys (D, Kw))."""
+    Kw = (K + 63) // 64
+    r = np.arange(first_row, first_row + R, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        h = _mix64((np.uint64(seed) ^ np.uint64(0xDEF0DEF0DEF0DEF0)) + r)
+    thr = int(p_def * 1000)
+    nd = np.where(h % np.uint64(1000) < np.uint64(thr), np.uint64(1) + (h >> np.uint64(32)) % np.uint64(2), np.uint64(0))
+    rows = np.repeat(np.arange(R), nd.astype(np.int64))
+    D = rows.shape[0]
+    di = np.concatenate([np.arange(int(n)) for n in nd]) if D else np.zeros(0, np.int64)
+    with np.errstate(over="ignore"):
+        hd = _mix64(h[rows] + np.uint64(0x9E37) * (di.astype(np.uint64) + np.uint64(1)))
+    Au = np.uint64(A)
+    w = (hd % Au).astype(np.int64)
+    clock = map_clock_rows(seed, rows + first_row, A, kmax) if D else np.zeros((0, A), np.uint64)
+    rm = np.zeros((D, A), np.uint64)
+    rm[np.arange(D), w] = clock[np.arange(D), w] + np.uint64(1) + (hd >> np.uint64(8)) % np.uint64(4)
+    if A > 1:
+        b = ((w.astype(np.uint64) + np.uint64(1) + (hd >> np.uint64(16)) % np.uint64(A - 1)) % Au).astype(np.int64)
+        rm[np.arange(D), b] = clock[np.arange(D), b] // np.uint64(2)
+    keys = np.zeros((D, Kw), np.uint64)
+    nk = (np.uint64(1) + (hd >> np.uint64(24)) % np.uint64(3)).astype(np.int64)
+    for d in range(D):
+        wk = _map_keys_of(int(w[d]), K, A)
+        for i in range(int(nk[d])):
+            with np.errstate(over="ignore"):
+                j = int(_mix64(hd[d] + np.uint64(i + 1))) % len(wk)
+            k = int(wk[j])
+            keys[d, k // 64] |= np.uint64(1) << np.uint64(k % 64)
+    return rows, rm, keys
+
+
+def _map_keys_of(a: int, K: int, A: int) -> np.ndarray:
+    if A == 1:
+        return np.arange(K, dtype=np.int64)
+    return np.concatenate([np.arange(a, K, A), np.arange((a - 1) % A, K, A)]).astype(np.int64)
+
+
+def map_clock_rows(seed: int, rows: np.ndarray, A: int, kmax: int) -> np.ndarray:
+    """clock[r][a] of crdt_synth_map for the given global replica indices (host)."""
+    return orswot_clock_rows(seed, rows, A, kmax)
+
+
+def map_replicas(ctx: Optional[Context], R: int, K: int, A: int, V: int, seed: int, kmax: int = 256,
+                 first_row: int = 0, p_def: float = 0.1) -> MapInput:
+    """Generate R well-formed Map<K, MVReg<u64>> replicas in HBM (crdt_synth_map), with their
+    deferred removes (host-built, then uploaded) pre-applied."""
+    ctx = ctx or Context.default()
+    dev = torch.device("cuda", ctx.device)
+    clock = torch.empty((R, A), dtype=torch.int64, device=dev)
+    ec = torch.empty((R, K, A), dtype=torch.int64, device=dev)
+    vclk = torch.empty((R, K, V, A), dtype=torch.int64, device=dev)
+    vval = torch.empty((R, K, V), dtype=torch.int64, device=dev)
+    rows, rm, keys = map_deferred(seed, R, K, A, kmax, p_def, first_row)
+    D = rm.shape[0]
+    off = np.searchsorted(rows, np.arange(R + 1), side="left").astype(np.int64)
+    d_off = torch.from_numpy(off).to(dev)
+    dcl = torch.from_numpy(np.ascontiguousarray(rm).view(np.int64)).to(dev)
+    dk = torch.from_numpy(np.ascontiguousarray(keys).view(np.int64)).to(dev)
+    ctx.call("crdt_synth_map", dptr(clock), dptr(ec), dptr(vclk), dptr(vval), R, K, A, V, first_row,
+             ctypes.c_uint64(seed), ctypes.c_uint64(kmax),
+             dptr(d_off) if D else None, dptr(dcl) if D else None, dptr(dk) if D else None)
+    torch.cuda.current_stream(dev).synchronize()
+    drow = torch.from_numpy(rows.astype(np.int32)).to(dev)
+    return MapInput(clock, ec, vclk, vval, [0, D], drow, dcl, dk)

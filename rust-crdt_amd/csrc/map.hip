@@ -19,7 +19,8 @@
 // Mapping: one wave per (group, key); lane l holds actors l, l+64, ... (APL per lane), so every
 // "for all actors" / "any actor" test is one vector compare + a wave vote (__all / __any), and
 // all control flow is wave-uniform.  The replica stream (entry clock, VI value clocks, VI values
-// and the replica clock) is software-pipelined PF replicas ahead in registers.
+// and the replica clock) is staged chunk by chunk through a per-wave LDS double buffer; the
+// MVReg lives in fixed register slots (MVState).
 //
 // Per step i with e = acc entry clock, e2 = replica entry clock, Co = replica clock:
 //   acc only      (:146-161): Co >= e ? drop : e = e>Co?e:0, vals.forget(Co>e?Co:0)
@@ -51,7 +52,8 @@ struct MapPlan {
   unsigned *o_flags;  // per group: bit0 > Vout values, bit1 bad def_row, bit2 state capacity
 };
 
-constexpr int kMapQ = 4;  // deferred removes tracked per key in registers before the slow path
+constexpr int kMapQ = 4;    // deferred removes tracked per key in registers before the slow path
+constexpr int kMapL = 256;  // removes naming one key listed in LDS (beyond: walk the group list)
 
 template <int APL, int VI>
 struct MapStep {
@@ -69,6 +71,13 @@ __device__ __forceinline__ bool all_ge(const u64 (&x)[APL], const u64 (&y)[APL])
   bool t = true;
 #pragma unroll
   for (int j = 0; j < APL; ++j) t &= x[j] >= y[j];
+  return wall(t);
+}
+template <int APL>
+__device__ __forceinline__ bool all_eq(const u64 (&x)[APL], const u64 (&y)[APL]) {
+  bool t = true;
+#pragma unroll
+  for (int j = 0; j < APL; ++j) t &= x[j] == y[j];
   return wall(t);
 }
 template <int APL>
@@ -104,47 +113,49 @@ __device__ __forceinline__ void vforget(u64 (&x)[APL], const u64 (&y)[APL]) {
   for (int j = 0; j < APL; ++j) x[j] = x[j] > y[j] ? x[j] : 0;
 }
 
-// The MVReg state of one key: n values, value clocks per lane, values wave-uniform.
+// The MVReg of one key: VO slots (clocks per lane, values / order keys wave-uniform), a valid
+// mask, and the next order key.  The Vec order (mvreg.rs:34) only decides the output order, so
+// values never move when others are dropped: an appended value takes a free slot and the next
+// order key, and egress writes the slots in key order.
 template <int APL, int VO>
 struct MVState {
   u64 c[VO][APL];
   u64 v[VO];
-  int n;
+  u64 seq[VO];
+  unsigned vm;
+  u64 next;
 };
 
-// Append (x, val) at position n (uniform); past VO the state overflows (flag, value dropped).
+// vals.forget(X) (mvreg.rs:88-104): forget every value clock, drop the emptied ones.
 template <int APL, int VO>
-__device__ __forceinline__ void mv_push(MVState<APL, VO> &s, const u64 (&x)[APL], u64 val, int &ovf) {
-  if (s.n >= VO) {
+__device__ __forceinline__ void mv_forget(MVState<APL, VO> &s, const u64 (&X)[APL]) {
+#pragma unroll
+  for (int q = 0; q < VO; ++q)
+    if (s.vm & (1u << q)) {
+      vforget(s.c[q], X);
+      if (!any_nz(s.c[q])) s.vm &= ~(1u << q);
+    }
+}
+
+// Append (x, val) at the end of the Vec order, in the first free slot.
+template <int APL, int VO>
+__device__ __forceinline__ void mv_append(MVState<APL, VO> &s, const u64 (&x)[APL], u64 val, int &ovf) {
+  const unsigned freem = ~s.vm & ((1u << VO) - 1u);
+  if (freem == 0) {
     ovf |= 4;  // the fold state itself ran out of value slots (results incomplete)
     return;
   }
+  const int q0 = __builtin_ctz(freem);
 #pragma unroll
   for (int q = 0; q < VO; ++q)
-    if (q == s.n) {
+    if (q == q0) {
 #pragma unroll
       for (int j = 0; j < APL; ++j) s.c[q][j] = x[j];
       s.v[q] = val;
+      s.seq[q] = s.next;
     }
-  s.n++;
-}
-
-// vals.forget(X) (mvreg.rs:88-104): forget every value clock, drop the emptied ones, keep order.
-template <int APL, int VO>
-__device__ __forceinline__ void mv_forget(MVState<APL, VO> &s, const u64 (&X)[APL], int &ovf) {
-  MVState<APL, VO> o;
-  o.n = 0;
-#pragma unroll
-  for (int q = 0; q < VO; ++q) {
-    if (q < s.n) {
-      u64 x[APL];
-#pragma unroll
-      for (int j = 0; j < APL; ++j) x[j] = s.c[q][j];
-      vforget(x, X);
-      if (any_nz(x)) mv_push(o, x, s.v[q], ovf);
-    }
-  }
-  s = o;
+  s.next++;
+  s.vm |= 1u << q0;
 }
 
 // Replica stream staging.  A chunk of C replicas is loaded into registers (every load in
@@ -233,6 +244,102 @@ __device__ __forceinline__ MapStep<APL, VI> map_step_read(const u64 *st, unsigne
   return in;
 }
 
+// Speculative no-op scan over the steps of a staged chunk (A <= 64).  Lane (s, g) = (lane / 4,
+// lane % 4) checks step s of the chunk on actors g, g+4, ... against the CURRENT fold state,
+// mirrored in LDS (me = entry clock, mc = value clocks, vm = valid slots); the four groups of a
+// step are combined bitwise on the ballot masks.  Bit 4s of the result is set iff step s
+// provably leaves (present, e, vals) unchanged:
+//   present, replica has the key:   e2 <= e, and e[a] == 0 | e[a] == e2[a] | e[a] > Co[a] for
+//                                   every a (so common == e and nothing is forgotten), and the
+//                                   MVReg merge keeps every value and appends none;
+//   present, replica lacks the key: e[a] == 0 | e[a] > Co[a] (e survives the forget) and no
+//                                   value clock changes under forget(Co > e ? Co : 0);
+//   absent, replica lacks the key:  always.
+// (Absent with the replica holding the key depends on Cs and is left to the exact step.)
+// Most steps of a fold change nothing, so their cost drops from a full exact step (~330 issued
+// instructions) to a share of this wave-wide scan.
+__device__ __forceinline__ u64 and4(u64 m) { return m & (m >> 1) & (m >> 2) & (m >> 3) & 0x1111111111111111ULL; }
+__device__ __forceinline__ u64 or4(u64 m) { return (m | (m >> 1) | (m >> 2) | (m >> 3)) & 0x1111111111111111ULL; }
+
+template <int VI, int VO>
+__device__ __forceinline__ u64 map_noop_steps(const u64 *buf, unsigned long long W, unsigned long long A,
+                                              const u64 *me, const u64 *mc, unsigned vm, bool present,
+                                              unsigned n, int lane) {
+  const unsigned st = (unsigned)lane >> 2;
+  const unsigned gq = (unsigned)lane & 3u;
+  const u64 *stp = buf + (st < n ? st : n - 1) * W;
+  u64 mP2 = 0, mA = ~0ull, mB = ~0ull, mB2 = ~0ull;
+  u64 mNZ[VI], mRI[VO], mLe1[VO][VI], mNe1[VO][VI], mLe2[VI][VO];
+#pragma unroll
+  for (int t = 0; t < VI; ++t) mNZ[t] = 0;
+#pragma unroll
+  for (int q = 0; q < VO; ++q) {
+    mRI[q] = ~0ull;
+#pragma unroll
+    for (int t = 0; t < VI; ++t) {
+      mLe1[q][t] = ~0ull;
+      mNe1[q][t] = 0;
+      mLe2[t][q] = ~0ull;
+    }
+  }
+  const unsigned iters = (unsigned)((A + 3) / 4);
+  for (unsigned m = 0; m < iters; ++m) {  // uniform trip count: absent actors read as zeros
+    const unsigned long long a = gq + 4ull * m;
+    const bool on = a < A;
+    const u64 e2 = on ? stp[a] : 0;
+    const u64 co = on ? stp[(1 + VI) * A + a] : 0;
+    const u64 ea = on ? me[a] : 0;
+    u64 c2[VI], sq[VO];
+#pragma unroll
+    for (int t = 0; t < VI; ++t) c2[t] = on ? stp[(1 + t) * A + a] : 0;
+#pragma unroll
+    for (int q = 0; q < VO; ++q) sq[q] = (on && (vm & (1u << q))) ? mc[q * A + a] : 0;
+    mP2 |= __ballot(e2 != 0);
+    mA &= __ballot(e2 <= ea);
+    mB &= __ballot(ea == 0 || ea == e2 || ea > co);
+    mB2 &= __ballot(ea == 0 || ea > co);
+    const u64 ri = co > ea ? co : 0;
+#pragma unroll
+    for (int t = 0; t < VI; ++t) mNZ[t] |= __ballot(c2[t] != 0);
+#pragma unroll
+    for (int q = 0; q < VO; ++q) {
+      if (vm & (1u << q)) {
+        mRI[q] &= __ballot(sq[q] == 0 || sq[q] > ri);
+#pragma unroll
+        for (int t = 0; t < VI; ++t) {
+          mLe1[q][t] &= __ballot(sq[q] <= c2[t]);
+          mNe1[q][t] |= __ballot(sq[q] != c2[t]);
+          mLe2[t][q] &= __ballot(c2[t] <= sq[q]);
+        }
+      }
+    }
+  }
+  const u64 P2 = or4(mP2);
+  u64 NZ[VI];
+#pragma unroll
+  for (int t = 0; t < VI; ++t) NZ[t] = or4(mNZ[t]);
+  u64 mvbad = 0, riok = 0x1111111111111111ULL;
+#pragma unroll
+  for (int q = 0; q < VO; ++q) {
+    if (vm & (1u << q)) {
+      riok &= and4(mRI[q]);
+#pragma unroll
+      for (int t = 0; t < VI; ++t) mvbad |= and4(mLe1[q][t]) & or4(mNe1[q][t]) & NZ[t];  // a value dropped
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < VI; ++t) {
+    u64 cov = 0;
+#pragma unroll
+    for (int q = 0; q < VO; ++q)
+      if (vm & (1u << q)) cov |= and4(mLe2[t][q]);
+    mvbad |= NZ[t] & ~cov;  // an incoming value appended
+  }
+  const u64 both = P2 & and4(mA) & and4(mB) & ~mvbad;
+  const u64 only_acc = ~P2 & and4(mB2) & riok;
+  return (present ? (both | only_acc) : ~P2) & 0x1111111111111111ULL;
+}
+
 template <int APL, int VI, int VO>
 __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan p) {
   const unsigned long long g = blockIdx.x / p.K;
@@ -245,10 +352,12 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan p) {
 #pragma unroll
   for (int j = 0; j < APL; ++j) e[j] = cs[j] = 0;
   MVState<APL, VO> mv;
-  mv.n = 0;
+  mv.vm = 0;
+  mv.next = 0;
 #pragma unroll
   for (int q = 0; q < VO; ++q) {
     mv.v[q] = 0;
+    mv.seq[q] = 0;
 #pragma unroll
     for (int j = 0; j < APL; ++j) mv.c[q][j] = 0;
   }
@@ -275,32 +384,95 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan p) {
   constexpr int C = MapChunk<APL, VI>::C;
   const unsigned long long A = p.A;
   const unsigned long long W = (2 + VI) * A + VI;
-  u64 *lbuf[2] = {map_lds, map_lds + C * W};
+  // (buffer addresses are always computed from map_lds: a pointer table would hide the LDS
+  // address space and turn every access into a flat op that waits on the prefetch loads)
+
+  // The removes naming this key, in replica order, gathered once into LDS (row, index), so the
+  // fold loop never waits on a global load for them (a vector load would drain the whole
+  // prefetched chunk: vmcnt is in order).  More than kMapL of them: walk the group list.
+  unsigned *lrow = reinterpret_cast<unsigned *>(map_lds + 2 * C * W);
+  unsigned *lidx = lrow + kMapL;
+  // fold-state mirror read by the speculative scan: entry clock, then VO value clocks
+  u64 *mirror = map_lds + 2 * C * W + kMapL;  // (kMapL u64 = the two u32 lists)
+  constexpr bool kSpec = APL == 1 && VO <= 4;
+  if (kSpec)
+    for (unsigned long long x = lane; x < (1 + VO) * A; x += 64) mirror[x] = 0;
+  unsigned long long nl = 0;
+  {
+    int badl = 0;
+    for (unsigned long long base = dbeg; base < dend; base += 64) {
+      const unsigned long long d = base + lane;
+      bool hit = false;
+      unsigned row = 0;
+      if (d < dend) {
+        row = p.def_row[d];
+        hit = (p.def_keys[d * p.Kw + kw] & kbit) != 0;
+        if (k == 0 && (row >= R || (d > dbeg && p.def_row[d - 1] > row))) badl = 1;
+      }
+      const u64 m = __ballot(hit);
+      if (hit) {
+        const unsigned long long pos = nl + __popcll(m & ((1ull << lane) - 1));
+        if (pos < kMapL) {
+          lrow[pos] = row;
+          lidx[pos] = (unsigned)d;
+        }
+      }
+      nl += __popcll(m);
+    }
+    if (__any(badl)) bad = 1;
+  }
+  const bool direct = nl > kMapL;
+  unsigned long long lp = 0;
+  unsigned next_row = (!direct && nl > 0) ? lrow[0] : 0xffffffffu;
   const unsigned long long nch = (R + C - 1) / C;
+  int cool = 0;
   MapChunk<APL, VI> regs;
   if (nch > 0) {
     map_chunk_load(regs, p, g, k, 0, lane);
-    map_chunk_store(regs, lbuf[0], A, W, R < (unsigned long long)C ? R : C, lane);
+    map_chunk_store(regs, map_lds, A, W, R < (unsigned long long)C ? R : C, lane);
     if (nch > 1) map_chunk_load(regs, p, g, k, C, lane);
   }
 
   for (unsigned long long ch = 0; ch < nch; ++ch) {
-    const u64 *buf = lbuf[ch & 1];
+    const u64 *buf = map_lds + ((ch & 1) ? C * W : 0);
     const unsigned long long i0 = ch * C;
     const unsigned long long n = R - i0 < (unsigned long long)C ? R - i0 : C;
-    MapStep<APL, VI> nxt = map_step_read<APL, VI>(buf, A, lane);
+    unsigned long long s = 0;
 #pragma unroll 1
-    for (unsigned long long s = 0; s < n; ++s) {
+    while (s < n) {
+      if (kSpec && cool == 0 && nq == 0 && !slow && !direct) {
+        // steps s.. that provably change nothing, up to the next remove naming this key
+        const unsigned long long lim0 = next_row < i0 + n ? next_row - i0 : n;
+        const unsigned long long lim = lim0 > s ? lim0 : s;
+        unsigned long long j = s;
+        if (lim > s) {
+          const u64 noop = map_noop_steps<VI, VO>(buf, W, A, mirror, mirror + A, mv.vm, present,
+                                                   (unsigned)n, lane);
+          const u64 from = (s >= 16) ? 0 : (~0ull << (4 * s));
+          const u64 upto = (lim >= 16) ? ~0ull : ((1ull << (4 * lim)) - 1);
+          const u64 stop = ~noop & 0x1111111111111111ULL & from & upto;
+          j = stop ? (unsigned long long)(__builtin_ctzll(stop) >> 2) : lim;
+          for (unsigned long long u = s; u < j; ++u) {  // acc.clock.merge of the skipped replicas
+            const unsigned long long a = lane;
+            const u64 co = a < A ? buf[u * W + (1 + VI) * A + a] : 0;
+            cs[0] = cs[0] > co ? cs[0] : co;
+          }
+          if (j == s) cool = 4;  // the scan found nothing to skip: run a few exact steps first
+        }
+        s = j;
+        if (s >= n) break;
+      }
+      if (cool > 0) --cool;
       const unsigned long long i = i0 + s;
-      const MapStep<APL, VI> in = nxt;
-      if (s + 1 < n) nxt = map_step_read<APL, VI>(buf + (s + 1) * W, A, lane);
+      const MapStep<APL, VI> in = map_step_read<APL, VI>(buf + s * W, A, lane);
+      ++s;
       {
       // ---- 1. entry join (map.rs:142-210) ----
       const bool p2 = any_nz(in.e);
       if (present && !p2) {
         if (all_ge(in.co, e)) {
           present = false;
-          mv.n = 0;
+          mv.vm = 0;
 #pragma unroll
           for (int j = 0; j < APL; ++j) e[j] = 0;
         } else {
@@ -310,7 +482,7 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan p) {
             e[j] = e[j] > in.co[j] ? e[j] : 0;
             ri[j] = in.co[j] > e[j] ? in.co[j] : 0;
           }
-          mv_forget(mv, ri, ovf);
+          if (any_nz(ri)) mv_forget(mv, ri);
         }
       } else if (!present && p2) {
         if (!all_ge(cs, in.e)) {
@@ -320,7 +492,8 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan p) {
             e[j] = in.e[j] > cs[j] ? in.e[j] : 0;
             ri[j] = cs[j] > e[j] ? cs[j] : 0;
           }
-          mv.n = 0;
+          mv.vm = 0;
+          mv.next = 0;
 #pragma unroll
           for (int t = 0; t < VI; ++t) {
             if (any_nz(in.c[t])) {
@@ -328,83 +501,79 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan p) {
 #pragma unroll
               for (int j = 0; j < APL; ++j) x[j] = in.c[t][j];
               vforget(x, ri);
-              if (any_nz(x)) mv_push(mv, x, in.v[t], ovf);
+              if (any_nz(x)) mv_append(mv, x, in.v[t], ovf);
             }
           }
           present = true;
         }
       } else if (present && p2) {
-        u64 common[APL], dl[APL];
+        u64 dl[APL];
+        bool dl_any = false;
 #pragma unroll
-        for (int j = 0; j < APL; ++j) {
-          const u64 t0 = e[j] == in.e[j] ? e[j] : 0;
-          const u64 t1 = in.e[j] > cs[j] ? in.e[j] : 0;
-          const u64 t2 = e[j] > in.co[j] ? e[j] : 0;
-          u64 c = t0 > t1 ? t0 : t1;
-          common[j] = c > t2 ? c : t2;
-          const u64 m = e[j] > in.e[j] ? e[j] : in.e[j];
-          dl[j] = m > common[j] ? m : 0;
-        }
-        if (!any_nz(common)) {
-          present = false;
-          mv.n = 0;
+        for (int j = 0; j < APL; ++j) dl[j] = 0;
+        if (!all_eq(e, in.e)) {  // (e == e2 everywhere: common = e, nothing forgotten)
+          u64 common[APL];
 #pragma unroll
-          for (int j = 0; j < APL; ++j) e[j] = 0;
-        } else {
-          // MVReg::merge then forget(deleted) (map.rs:183-188, mvreg.rs:112-128)
-          bool ne2[VI];
-#pragma unroll
-          for (int t = 0; t < VI; ++t) ne2[t] = any_nz(in.c[t]);
-          bool keep1[VO];
-#pragma unroll
-          for (int s = 0; s < VO; ++s) {
-            keep1[s] = s < mv.n;
-            if (keep1[s]) {
-#pragma unroll
-              for (int t = 0; t < VI; ++t)
-                if (ne2[t] && vlt(mv.c[s], in.c[t])) keep1[s] = false;
-            }
+          for (int j = 0; j < APL; ++j) {
+            const u64 t0 = e[j] == in.e[j] ? e[j] : 0;
+            const u64 t1 = in.e[j] > cs[j] ? in.e[j] : 0;
+            const u64 t2 = e[j] > in.co[j] ? e[j] : 0;
+            const u64 c = t0 > t1 ? t0 : t1;
+            common[j] = c > t2 ? c : t2;
+            const u64 m = e[j] > in.e[j] ? e[j] : in.e[j];
+            dl[j] = m > common[j] ? m : 0;
           }
-          bool keep2[VI];
-#pragma unroll
-          for (int t = 0; t < VI; ++t) {
-            keep2[t] = ne2[t];
-            if (keep2[t]) {
-#pragma unroll
-              for (int s = 0; s < VO; ++s)
-                if (keep1[s] && vle(in.c[t], mv.c[s])) keep2[t] = false;
-            }
+          if (!any_nz(common)) {
+            present = false;
+            mv.vm = 0;
+          } else {
+            dl_any = any_nz(dl);
           }
-          MVState<APL, VO> o;
-          o.n = 0;
-#pragma unroll
-          for (int s = 0; s < VO; ++s) {
-            if (keep1[s]) {
-              u64 x[APL];
-#pragma unroll
-              for (int j = 0; j < APL; ++j) x[j] = mv.c[s][j];
-              vforget(x, dl);
-              if (any_nz(x)) mv_push(o, x, mv.v[s], ovf);
-            }
-          }
-#pragma unroll
-          for (int t = 0; t < VI; ++t) {
-            if (keep2[t]) {
-              u64 x[APL];
-#pragma unroll
-              for (int j = 0; j < APL; ++j) x[j] = in.c[t][j];
-              vforget(x, dl);
-              if (any_nz(x)) mv_push(o, x, in.v[t], ovf);
-            }
-          }
-          mv = o;
 #pragma unroll
           for (int j = 0; j < APL; ++j) e[j] = common[j];
+        }
+        if (present) {
+          // MVReg::merge then forget(deleted) (map.rs:183-188, mvreg.rs:112-128)
+          unsigned v2m = 0;
+#pragma unroll
+          for (int t = 0; t < VI; ++t)
+            if (any_nz(in.c[t])) v2m |= 1u << t;
+          unsigned keep = mv.vm;
+#pragma unroll
+          for (int q = 0; q < VO; ++q) {
+            if (keep & (1u << q)) {
+#pragma unroll
+              for (int t = 0; t < VI; ++t)
+                if ((v2m & (1u << t)) && vlt(mv.c[q], in.c[t])) {
+                  keep &= ~(1u << q);
+                  break;
+                }
+            }
+          }
+          unsigned addm = 0;
+#pragma unroll
+          for (int t = 0; t < VI; ++t) {
+            if (v2m & (1u << t)) {
+              bool add = true;
+#pragma unroll
+              for (int q = 0; q < VO; ++q)
+                if ((keep & (1u << q)) && vle(in.c[t], mv.c[q])) {
+                  add = false;
+                  break;
+                }
+              if (add) addm |= 1u << t;
+            }
+          }
+          mv.vm = keep;
+#pragma unroll
+          for (int t = 0; t < VI; ++t)
+            if (addm & (1u << t)) mv_append(mv, in.c[t], in.v[t], ovf);
+          if (dl_any) mv_forget(mv, dl);
         }
       }
 
       // ---- 2. deferred removes active at step i (map.rs:213-219, :311-348) ----
-      if (dp < dend || nq > 0 || slow) {
+      if ((direct ? dp < dend : next_row <= i) || nq > 0 || slow) {
         if (!slow) {  // expire: dropped from acc.deferred once acc.clock (= Cs) dominates it
           int w = 0;
 #pragma unroll
@@ -420,26 +589,39 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan p) {
           }
           nq = w;
         }
-        while (dp < dend) {
-          const unsigned row = p.def_row[dp];
-          if (row > i) break;
-          if (row < i) bad = 1;  // rows must be non-decreasing within the group
-          if (p.def_keys[dp * p.Kw + kw] & kbit) {
-            if (!slow && nq < kMapQ) {
-#pragma unroll
-              for (int q = 0; q < kMapQ; ++q)
-                if (q == nq)
-#pragma unroll
-                  for (int j = 0; j < APL; ++j) {
-                    const unsigned long long a = lane + 64ull * j;
-                    rq[q][j] = a < p.A ? p.def_clock[dp * p.A + a] : 0;
-                  }
-              ++nq;
-            } else {
-              slow = true;
-            }
+        // activate the removes held by replica i that name this key
+        while (true) {
+          unsigned long long d;
+          if (!direct) {
+            if (next_row > i) break;
+            d = lidx[lp];
+            ++lp;
+            next_row = lp < nl ? lrow[lp] : 0xffffffffu;
+          } else {
+            if (dp >= dend) break;
+            const unsigned row = p.def_row[dp];
+            if (row > i) break;
+            d = dp++;
+            if (!(p.def_keys[d * p.Kw + kw] & kbit)) continue;
           }
-          ++dp;
+          if (!slow && nq < kMapQ) {
+#pragma unroll
+            for (int q = 0; q < kMapQ; ++q)
+              if (q == nq)
+#pragma unroll
+                for (int j = 0; j < APL; ++j) {
+                  const unsigned long long a = lane + 64ull * j;
+                  u64 x = a < p.A ? p.def_clock[d * p.A + a] : 0;
+                  // consume the load here (one wait per activation): a register still pending
+                  // at the loop back-edge would make every later step wait on vmcnt(0), i.e.
+                  // on the whole prefetched chunk
+                  asm volatile("; rm clock landed" : "+v"(x));
+                  rq[q][j] = x;
+                }
+            ++nq;
+          } else {
+            slow = true;
+          }
         }
         u64 ceil[APL];
         bool have = false;
@@ -454,8 +636,10 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan p) {
               for (int j = 0; j < APL; ++j) ceil[j] = ceil[j] > rq[q][j] ? ceil[j] : rq[q][j];
             }
         } else {  // more than kMapQ concurrent removes on this key: rescan every started one
-          for (unsigned long long d = dbeg; d < dp; ++d) {
-            if (!(p.def_keys[d * p.Kw + kw] & kbit)) continue;
+          const unsigned long long nscan = direct ? dp - dbeg : lp;
+          for (unsigned long long x = 0; x < nscan; ++x) {
+            const unsigned long long d = direct ? dbeg + x : lidx[x];
+            if (direct && !(p.def_keys[d * p.Kw + kw] & kbit)) continue;
             u64 rm[APL];
 #pragma unroll
             for (int j = 0; j < APL; ++j) {
@@ -473,9 +657,9 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan p) {
           vforget(e, ceil);
           if (!any_nz(e)) {
             present = false;
-            mv.n = 0;
+            mv.vm = 0;
           } else {
-            mv_forget(mv, ceil, ovf);
+            mv_forget(mv, ceil);
           }
         }
       }
@@ -484,17 +668,37 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan p) {
 #pragma unroll
       for (int j = 0; j < APL; ++j) cs[j] = cs[j] > in.co[j] ? cs[j] : in.co[j];
       }
+      if (kSpec) {  // refresh the state mirror for the next scan
+        if ((unsigned long long)lane < A) {
+          mirror[lane] = e[0];
+#pragma unroll
+          for (int q = 0; q < VO; ++q) mirror[(1 + q) * A + lane] = mv.c[q][0];
+        }
+      }
     }
     if (ch + 1 < nch) {  // stage the next chunk (its loads were issued a whole chunk ago)
       const unsigned long long nn = R - (ch + 1) * C < (unsigned long long)C ? R - (ch + 1) * C : C;
-      map_chunk_store(regs, lbuf[(ch + 1) & 1], A, W, nn, lane);
+      map_chunk_store(regs, map_lds + (((ch + 1) & 1) ? C * W : 0), A, W, nn, lane);
       if (ch + 2 < nch) map_chunk_load(regs, p, g, k, (ch + 2) * C, lane);
     }
   }
-  if (dp < dend) bad = 1;  // a row >= R was never reached
+  if (direct && dp < dend) bad = 1;  // a row >= R was never reached
 
-  // ---- egress ----
-  if (mv.n > (int)p.Vout) ovf |= 1;
+  // ---- egress: slots in Vec order (ascending order key) ----
+  const int nv = __builtin_popcount(mv.vm);
+  if (nv > (int)p.Vout) ovf |= 1;
+  int rank[VO];
+#pragma unroll
+  for (int q = 0; q < VO; ++q) {
+    rank[q] = -1;
+    if (mv.vm & (1u << q)) {
+      int r = 0;
+#pragma unroll
+      for (int q2 = 0; q2 < VO; ++q2)
+        if ((mv.vm & (1u << q2)) && mv.seq[q2] < mv.seq[q]) ++r;
+      rank[q] = r;
+    }
+  }
   const unsigned long long gk = g * p.K + k;
 #pragma unroll
   for (int j = 0; j < APL; ++j) {
@@ -502,23 +706,24 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan p) {
     if (a < p.A) {
       p.o_ec[gk * p.A + a] = present ? e[j] : 0;
       if (k == 0) p.o_clock[g * p.A + a] = cs[j];
+      for (unsigned long long o = 0; o < p.Vout; ++o) {
+        u64 x = 0;
 #pragma unroll
-      for (int q = 0; q < VO; ++q)
-        if ((unsigned long long)q < p.Vout) p.o_vclk[(gk * p.Vout + q) * p.A + a] = q < mv.n ? mv.c[q][j] : 0;
+        for (int q = 0; q < VO; ++q)
+          if (rank[q] == (int)o) x = mv.c[q][j];
+        p.o_vclk[(gk * p.Vout + o) * p.A + a] = x;
+      }
     }
   }
-  // slots beyond the template capacity (Vout > VO) are zero
-  for (unsigned long long q = VO; q < p.Vout; ++q)
-    for (unsigned long long a = lane; a < p.A; a += 64) p.o_vclk[(gk * p.Vout + q) * p.A + a] = 0;
   if (lane == 0) {
-    for (unsigned long long q = 0; q < p.Vout; ++q) {
+    for (unsigned long long o = 0; o < p.Vout; ++o) {
       u64 v = 0;
 #pragma unroll
-      for (int s = 0; s < VO; ++s)
-        if ((unsigned long long)s == q && s < mv.n) v = mv.v[s];
-      p.o_vval[gk * p.Vout + q] = v;
+      for (int q = 0; q < VO; ++q)
+        if (rank[q] == (int)o) v = mv.v[q];
+      p.o_vval[gk * p.Vout + o] = v;
     }
-    if (p.o_nval) p.o_nval[gk] = present ? (unsigned)mv.n : 0u;
+    if (p.o_nval) p.o_nval[gk] = present ? (unsigned)nv : 0u;
     const unsigned f = (unsigned)ovf | (bad ? 2u : 0u);
     if (f) atomicOr(p.o_flags + g, f);
   }
@@ -531,7 +736,8 @@ using namespace crdt;
 template <int APL, int VI, int VO>
 static hipError_t launch_map(const MapPlan &p, unsigned long long blocks, hipStream_t s) {
   const size_t W = (2 + VI) * p.A + VI;
-  const size_t lds = 2 * (size_t)MapChunk<APL, VI>::C * W * sizeof(u64);
+  const size_t lds = 2 * (size_t)MapChunk<APL, VI>::C * W * sizeof(u64) + kMapL * 2 * sizeof(unsigned) +
+                     (1 + VO) * p.A * sizeof(u64);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   if (lds > 64 * 1024) {  // beyond the default dynamic-LDS limit (gfx950 has 160 KB per CU)
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&map_fold_kernel<APL, VI, VO>),

@@ -183,3 +183,137 @@ extern "C" int crdt_synth_orswot_rm(crdt_ctx *ctx, uint64_t *entries, size_t M, 
   CRDT_HIP(ctx, hipGetLastError());
   return CRDT_OK;
 }
+
+// ---- Map<K, MVReg<u64>> replicas (BASELINE config 4) ----------------------------------------
+// Restated bit-for-bit by oracle.synth_map / synth_map_deferred (model in their docstrings):
+//   clock[r][a] = synth(seed, r*A + a) % (kmax + 1)  (ops 1..clock[r][a] of actor a seen)
+//   key k is written by w0 = k % A and w1 = (k + 1) % A; actor a's n-th op targets the
+//   ((n-1) mod M_a)-th of its keys (k % A == a in key order, then k % A == a-1), and is a
+//   remove iff mix(seed ^ KIND, a << 32 | n) % 8 == 0, else an update with MVReg clock {a: n}
+//   and value mix(seed ^ VAL, a << 32 | n).
+//   Entry (r, k): per writer w (w0 then w1), w's latest op n <= clock[r][w] on k, if an update
+//   whose dot survives the replica's own deferred removes naming k (n > max rm[w]):
+//   ec[w] = n and the next value slot = ({w: n}, value).
+namespace crdt {
+
+constexpr u64 kSaltKind = 0xA5A5A5A55A5A5A5AULL;
+constexpr u64 kSaltVal = 0x5EED5EED0B57AC1EULL;
+
+__device__ __forceinline__ u64 key_count(u64 K, u64 A, u64 res) {
+  return res < K ? (K - res + A - 1) / A : 0;
+}
+
+struct SynthMapPlan {
+  u64 *clock, *ec, *vclk, *vval;
+  unsigned long long R, K, A, V, first_row, kmax;
+  u64 seed;
+  const u64 *def_off;  // local replica CSR [R+1] or null
+  const u64 *def_clock, *def_keys;
+  unsigned long long Kw;
+};
+
+__device__ __forceinline__ u64 synth_map_c(const SynthMapPlan &p, u64 r, u64 a) {
+  return mix64(p.seed + ((p.first_row + r) * p.A + a + 1) * 0x9E3779B97F4A7C15ULL) % (p.kmax + 1);
+}
+
+// Latest op n <= c of writer w on key k (0 if none).
+__device__ __forceinline__ u64 synth_map_latest(const SynthMapPlan &p, u64 w, u64 k, u64 c) {
+  u64 M, j;
+  if (p.A == 1) {
+    M = p.K;
+    j = k;
+  } else {
+    const u64 P = key_count(p.K, p.A, w);
+    M = P + key_count(p.K, p.A, (w + p.A - 1) % p.A);
+    j = (k % p.A == w) ? k / p.A : P + k / p.A;
+  }
+  if (c < j + 1) return 0;
+  return j + 1 + M * ((c - j - 1) / M);
+}
+
+__global__ __launch_bounds__(kBlock) void synth_map_kernel(SynthMapPlan p) {
+  const unsigned long long total = p.R * p.K * p.A;
+  const unsigned long long nthreads = (unsigned long long)gridDim.x * blockDim.x;
+  for (unsigned long long idx = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += nthreads) {
+    const u64 a = idx % p.A;
+    const u64 rk = idx / p.A;
+    const u64 k = rk % p.K;
+    const u64 r = rk / p.K;
+    if (k == 0) p.clock[r * p.A + a] = synth_map_c(p, r, a);
+    const int nw = p.A == 1 ? 1 : 2;
+    u64 wv[2], nv[2];
+    bool live[2];
+    for (int i = 0; i < nw; ++i) {
+      const u64 w = (k + i) % p.A;
+      const u64 n = synth_map_latest(p, w, k, synth_map_c(p, r, w));
+      const bool upd = n > 0 && (mix64((p.seed ^ kSaltKind) + (w << 32) + n) & 7) != 0;
+      u64 ceil = 0;
+      if (p.def_off)
+        for (u64 d = p.def_off[r]; d < p.def_off[r + 1]; ++d)
+          if ((p.def_keys[d * p.Kw + k / 64] >> (k % 64)) & 1) {
+            const u64 x = p.def_clock[d * p.A + w];
+            ceil = x > ceil ? x : ceil;
+          }
+      wv[i] = w;
+      nv[i] = n;
+      live[i] = upd && n > ceil;
+    }
+    u64 e = 0;
+    int slot = 0;
+    u64 *vc = p.vclk + rk * p.V * p.A;
+    u64 *vv = p.vval + rk * p.V;
+    for (u64 s = 0; s < p.V; ++s) vc[s * p.A + a] = 0;
+    for (int i = 0; i < nw; ++i) {
+      if (!live[i]) continue;
+      if (wv[i] == a) e = nv[i];
+      if ((u64)slot < p.V) {
+        if (wv[i] == a) vc[slot * p.A + a] = nv[i];
+        if (a == 0) vv[slot] = mix64((p.seed ^ kSaltVal) + (wv[i] << 32) + nv[i]);
+      }
+      ++slot;
+    }
+    if (a == 0)
+      for (u64 s = slot; s < p.V; ++s) vv[s] = 0;
+    p.ec[rk * p.A + a] = e;
+  }
+}
+
+}  // namespace crdt
+
+extern "C" int crdt_synth_map(crdt_ctx *ctx, uint64_t *clock, uint64_t *ec, uint64_t *vclk,
+                              uint64_t *vval, size_t R, size_t K, size_t A, size_t V,
+                              size_t first_row, uint64_t seed, uint64_t kmax,
+                              const uint64_t *def_off, const uint64_t *def_clock,
+                              const uint64_t *def_keys) {
+  CRDT_CHECK_CTX(ctx);
+  if (R == 0 || K == 0 || A == 0) return CRDT_OK;
+  if (!clock || !ec || (V > 0 && (!vclk || !vval)))
+    return crdt::fail(ctx, CRDT_EINVAL, "synth_map: NULL output");
+  if (def_off && (!def_clock || !def_keys))
+    return crdt::fail(ctx, CRDT_EINVAL, "synth_map: deferred buffers missing");
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  crdt::SynthMapPlan p{};
+  p.clock = (crdt::u64 *)clock;
+  p.ec = (crdt::u64 *)ec;
+  p.vclk = (crdt::u64 *)vclk;
+  p.vval = (crdt::u64 *)vval;
+  p.R = R;
+  p.K = K;
+  p.A = A;
+  p.V = V;
+  p.first_row = first_row;
+  p.kmax = kmax;
+  p.seed = seed;
+  p.def_off = (const crdt::u64 *)def_off;
+  p.def_clock = (const crdt::u64 *)def_clock;
+  p.def_keys = (const crdt::u64 *)def_keys;
+  p.Kw = (K + 63) / 64;
+  const unsigned long long total = (unsigned long long)R * K * A;
+  unsigned long long blocks = (total + crdt::kBlock - 1) / crdt::kBlock;
+  const unsigned long long cap = (unsigned long long)ctx->cu_count * 16;
+  if (blocks > cap) blocks = cap;
+  hipLaunchKernelGGL(crdt::synth_map_kernel, dim3((unsigned)blocks), dim3(crdt::kBlock), 0, ctx->stream, p);
+  CRDT_HIP(ctx, hipGetLastError());
+  return CRDT_OK;
+}

@@ -1,0 +1,16 @@
+#!/bin/bash
+# PMC passes over the Map fold kernel: instruction mix and stall counters (one pass per group).
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
+mkdir -p gpurun_out/pmc_map
+export TMPDIR=/tmp
+i=0
+for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \
+           "SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INST_CYCLES_VMEM_RD SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_INSTS_BRANCH SQ_ACTIVE_INST_ANY"; do
+  i=$((i+1))
+  echo "== pass $i: $set"
+  timeout -s KILL 120 rocprofv3 --pmc $set --output-format csv -d gpurun_out/pmc_map/p$i -o run -- python3 scripts/prof_map.py "$@" > gpurun_out/pmc_map/p$i.log 2>&1
+  rc=$?
+  echo "rc=$rc"; tail -2 gpurun_out/pmc_map/p$i.log
+  [ $rc -ne 0 ] && exit $rc
+done
+echo "== all done"

@@ -159,3 +159,48 @@ def test_map_empty_and_errors(gpu_ctx):
     d["def_row"] = np.array([4, 1, 2], np.uint64)
     with pytest.raises(ValueError):
         _gpu(gpu_ctx, d, 8)
+
+
+def test_synth_map_matches_cpu(gpu_ctx):
+    from crdts_gpu import synth
+    seed, R, K, A, V, kmax = 11, 90, 70, 9, 3, 30
+    inp = synth.map_replicas(gpu_ctx, R, K, A, V, seed, kmax=kmax, p_def=0.3)
+    dfr = O.synth_map_deferred(seed, R, K, A, kmax, p_def=0.3)
+    exp = O.synth_map(seed, R, K, A, V, kmax, deferred=dfr)
+    for nm in ("clock", "ec", "vclk", "vval"):
+        np.testing.assert_array_equal(to_host(getattr(inp, nm)), exp[nm], err_msg=nm)
+    assert inp.def_clock.shape[0] == len(dfr[0]) > 0
+    np.testing.assert_array_equal(to_host(inp.def_clock), dfr[1])
+    np.testing.assert_array_equal(to_host(inp.def_keys), dfr[2])
+
+
+@pytest.mark.parametrize("R,K,A,kmax", [(4096, 256, 32, 64), (3000, 100, 7, 40)])
+def test_map_synth_sampled_keys(gpu_ctx, R, K, A, kmax):
+    """Synthetic replicas in HBM, folded on the GPU; the oracle folds a key sample over every
+    replica (keys are independent given the clocks) and must match bit for bit."""
+    from crdts_gpu import synth
+    seed = 0x5EED0004
+    inp = synth.map_replicas(gpu_ctx, R, K, A, 2, seed, kmax=kmax, p_def=0.1)
+    res = cg.map.lub_many(inp.clock, inp.ec, inp.vclk, inp.vval, def_off=inp.def_off,
+                          def_row=inp.def_row, def_clock=inp.def_clock, def_keys=inp.def_keys,
+                          vout=4, ctx=gpu_ctx)
+    keys = np.random.default_rng(R).choice(K, size=8, replace=False)
+    dfr = O.synth_map_deferred(seed, R, K, A, kmax, p_def=0.1)
+    d = O.synth_map(seed, R, K, A, 2, kmax, keys=keys, deferred=dfr)
+    sub_keys = O.restrict_deferred_keys(dfr[2], keys)
+    exp = O.map_fold(d["clock"], d["ec"], d["vclk"], d["vval"], dfr[0], dfr[1], sub_keys, 4)
+    np.testing.assert_array_equal(to_host(res.clock), exp[0])
+    np.testing.assert_array_equal(to_host(res.ec)[keys], exp[1])
+    np.testing.assert_array_equal(to_host(res.vclk)[keys], exp[2])
+    np.testing.assert_array_equal(to_host(res.vval)[keys], exp[3])
+    np.testing.assert_array_equal(res.nval.cpu().numpy()[keys], exp[4])
+    # surviving deferred removes restricted to the sample
+    got = cg.map.deferred_set(inp.def_clock, res.def_keep, res.def_keys)
+    pos = {int(k): i for i, k in enumerate(keys)}
+    got_sub = set()
+    for c, ks in got:
+        sub = frozenset(pos[k] for k in ks if k in pos)
+        if sub:
+            got_sub.add((c, sub))
+    exp_sub = {(c, ks) for c, ks in exp[5] if ks}
+    assert got_sub == exp_sub

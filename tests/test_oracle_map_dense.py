@@ -84,3 +84,40 @@ def test_dense_fold_arbitrary_states(seed):
     d = _random_dense(rng, R, K, A, V, cmax=int(rng.choice([3, 6, 1000])))
     py, cc = _fold_all(d, Vout=R * V + 1)
     _same(py, cc)
+
+
+def test_synth_map_deferred_twins():
+    """crdts_gpu.synth.map_deferred (vectorised, what the product-side generator uploads) and
+    oracle.synth_map_deferred (loop restatement) build the same deferred lists."""
+    import crdts_gpu.synth as S
+    for seed, R, K, A, kmax in [(1, 300, 64, 8, 40), (2, 100, 10, 1, 5), (3, 200, 33, 2, 9),
+                                (4, 500, 1024, 32, 256)]:
+        a = S.map_deferred(seed, R, K, A, kmax, p_def=0.2)
+        b = O.synth_map_deferred(seed, R, K, A, kmax, p_def=0.2)
+        for x, y in zip(a, b):
+            assert np.array_equal(np.asarray(x), np.asarray(y))
+
+
+@pytest.mark.parametrize("seed,R,K,A,kmax", [(5, 120, 64, 8, 40), (6, 80, 17, 3, 12), (7, 60, 9, 1, 20)])
+def test_synth_map_converges_to_max_prefix(seed, R, K, A, kmax):
+    """Without deferred removes every synthetic replica is a causally closed state of one op
+    history, so the reference fold equals the state at the max prefix (as MVReg sets)."""
+    d = O.synth_map(seed, R, K, A, 2, kmax)
+    exp = O.map_fold(d["clock"], d["ec"], d["vclk"], d["vval"], Vout=4)
+    cm = d["clock"].max(0)
+    top = O.synth_map(seed, 1, K, A, 2, kmax, clock_override=cm[None])
+    assert np.array_equal(exp[1], top["ec"][0])
+    for k in range(K):
+        a = {(tuple(exp[2][k, s]), int(exp[3][k, s])) for s in range(4) if exp[2][k, s].any()}
+        b = {(tuple(top["vclk"][0, k, s]), int(top["vval"][0, k, s])) for s in range(2) if top["vclk"][0, k, s].any()}
+        assert a == b
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_synth_map_with_deferred_dense_fold(seed):
+    R, K, A, kmax = 150, 40, 6, 30
+    dfr = O.synth_map_deferred(seed, R, K, A, kmax, p_def=0.3)
+    d = O.synth_map(seed, R, K, A, 2, kmax, deferred=dfr)
+    py = O.dense_map_fold(d["clock"], d["ec"], d["vclk"], d["vval"], dfr[0], dfr[1], dfr[2], 4)
+    cc = O.map_fold(d["clock"], d["ec"], d["vclk"], d["vval"], dfr[0], dfr[1], dfr[2], 4)
+    _same(py, cc)
