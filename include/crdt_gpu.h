@@ -71,6 +71,9 @@ int crdt_ctx_set_timing(crdt_ctx *ctx, int enable);
  * "lww_reduce", ...) since the last reset.  Synchronises the ctx stream. */
 int crdt_ctx_timing(crdt_ctx *ctx, const char *name, double *total_ms, uint64_t *launches);
 int crdt_ctx_timing_reset(crdt_ctx *ctx);
+/* Override launch-geometry knobs ("key=value,...", the CRDT_TUNE syntax read at create; see
+ * DESIGN.md §3).  Results never depend on them; tests use it to exercise every staging path. */
+int crdt_ctx_tune(crdt_ctx *ctx, const char *spec);
 
 /* ---- VClock / GCounter: elementwise-max lub ----------------------------------------------
  * Replaces VClock::merge (vclock.rs:130-136, via apply_dot :155-159) and GCounter::merge

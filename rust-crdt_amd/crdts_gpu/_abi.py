@@ -22,7 +22,7 @@ CRDT_ACCUMULATE = 0x1
 EXPORTS = (
     "crdt_ctx_create", "crdt_ctx_destroy", "crdt_ctx_set_stream", "crdt_ctx_synchronize",
     "crdt_last_error", "crdt_version", "crdt_build_target", "crdt_ctx_set_timing",
-    "crdt_ctx_timing", "crdt_ctx_timing_reset",
+    "crdt_ctx_timing", "crdt_ctx_timing_reset", "crdt_ctx_tune",
     "crdt_vclock_lub_many", "crdt_vclock_merge_batch",
     "crdt_gcounter_lub_many", "crdt_gcounter_merge_batch",
     "crdt_pncounter_lub_many", "crdt_pncounter_merge_batch",
@@ -90,6 +90,7 @@ _SIGS = {
     "crdt_ctx_set_timing": ([P, ctypes.c_int], ctypes.c_int),
     "crdt_ctx_timing": ([P, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(U64)], ctypes.c_int),
     "crdt_ctx_timing_reset": ([P], ctypes.c_int),
+    "crdt_ctx_tune": ([P, ctypes.c_char_p], ctypes.c_int),
     "crdt_synth_fill": ([P, P, S, S, S, S, U64, ctypes.c_int], ctypes.c_int),
     "crdt_synth_orswot": ([P, P, P, S, S, S, S, U64, U64], ctypes.c_int),
     "crdt_synth_orswot_rm": ([P, P, S, S, S, P, P, P], ctypes.c_int),

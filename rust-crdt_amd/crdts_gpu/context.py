@@ -77,6 +77,10 @@ class Context:
     def timing_reset(self) -> None:
         self.call("crdt_ctx_timing_reset")
 
+    def tune(self, spec: str) -> None:
+        """Override launch-geometry knobs ("key=value,...", CRDT_TUNE syntax); never changes results."""
+        self.call("crdt_ctx_tune", spec.encode())
+
     # -- tensor checks ----------------------------------------------------------------------
     def check_tensor(self, t: torch.Tensor, what: str) -> None:
         if not isinstance(t, torch.Tensor):

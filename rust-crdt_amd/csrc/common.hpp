@@ -38,6 +38,9 @@ struct Tune {
   int orswot_blocks_per_cu = 2;
   int orswot_unroll = 2;
   int merge_blocks_per_cu = 2;
+  int map_glds = 1;    // Map fold: LDS-DMA staging where the shape allows it
+  int map_chunk = 16;  // ... replicas per LDS chunk slot (8 or 16)
+  int map_ring = 2;    // ... chunk slots in the ring (2-4)
 };
 
 struct PendingTiming {

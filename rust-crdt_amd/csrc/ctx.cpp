@@ -180,6 +180,35 @@ using namespace crdt;
 
 extern "C" {
 
+// Launch-geometry knobs "key=value,..." (DESIGN.md §3); unknown keys / values are ignored.
+static void apply_tune(crdt_ctx *ctx, const char *t) {
+  std::string spec(t);
+  size_t pos = 0;
+  while (pos < spec.size()) {
+    size_t end = spec.find(',', pos);
+    if (end == std::string::npos) end = spec.size();
+    std::string kv = spec.substr(pos, end - pos);
+    size_t eq = kv.find('=');
+    if (eq != std::string::npos) {
+      std::string k = kv.substr(0, eq);
+      int v = atoi(kv.c_str() + eq + 1);
+      if (k == "bpc" && v > 0) ctx->tune.lub_blocks_per_cu = v;
+      else if (k == "minsteps" && v > 0) ctx->tune.lub_min_steps = v;
+      else if (k == "interleave") ctx->tune.lub_interleave = v != 0;
+      else if (k == "unroll" && (v == 4 || v == 8 || v == 16 || v == 32)) ctx->tune.lub_unroll = v;
+      else if (k == "nt") ctx->tune.lub_nt = v != 0;
+      else if (k == "grid" && v > 0) ctx->tune.lub_grid = v;
+      else if (k == "mbpc" && v > 0) ctx->tune.merge_blocks_per_cu = v;
+      else if (k == "obpc" && v > 0) ctx->tune.orswot_blocks_per_cu = v;
+      else if (k == "ounroll" && (v == 1 || v == 2 || v == 4)) ctx->tune.orswot_unroll = v;
+      else if (k == "mglds") ctx->tune.map_glds = v != 0;
+      else if (k == "mchunk" && (v == 8 || v == 16)) ctx->tune.map_chunk = v;
+      else if (k == "mring" && v >= 2 && v <= 4) ctx->tune.map_ring = v;
+    }
+    pos = end + 1;
+  }
+}
+
 int crdt_ctx_create(int device, crdt_ctx **out) {
   if (!out) return fail(nullptr, CRDT_EINVAL, "crdt_ctx_create: out is NULL");
   *out = nullptr;
@@ -196,30 +225,7 @@ int crdt_ctx_create(int device, crdt_ctx **out) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     ctx->cu_count = prop.multiProcessorCount;
-  if (const char *t = getenv("CRDT_TUNE")) {
-    std::string spec(t);
-    size_t pos = 0;
-    while (pos < spec.size()) {
-      size_t end = spec.find(',', pos);
-      if (end == std::string::npos) end = spec.size();
-      std::string kv = spec.substr(pos, end - pos);
-      size_t eq = kv.find('=');
-      if (eq != std::string::npos) {
-        std::string k = kv.substr(0, eq);
-        int v = atoi(kv.c_str() + eq + 1);
-        if (k == "bpc" && v > 0) ctx->tune.lub_blocks_per_cu = v;
-        else if (k == "minsteps" && v > 0) ctx->tune.lub_min_steps = v;
-        else if (k == "interleave") ctx->tune.lub_interleave = v != 0;
-        else if (k == "unroll" && (v == 4 || v == 8 || v == 16 || v == 32)) ctx->tune.lub_unroll = v;
-        else if (k == "nt") ctx->tune.lub_nt = v != 0;
-        else if (k == "grid" && v > 0) ctx->tune.lub_grid = v;
-        else if (k == "mbpc" && v > 0) ctx->tune.merge_blocks_per_cu = v;
-        else if (k == "obpc" && v > 0) ctx->tune.orswot_blocks_per_cu = v;
-        else if (k == "ounroll" && (v == 1 || v == 2 || v == 4)) ctx->tune.orswot_unroll = v;
-      }
-      pos = end + 1;
-    }
-  }
+  if (const char *t = getenv("CRDT_TUNE")) apply_tune(ctx, t);
   *out = ctx;
   return CRDT_OK;
 }
@@ -286,3 +292,10 @@ int crdt_ctx_timing_reset(crdt_ctx *ctx) {
 }
 
 }  // extern "C"
+
+int crdt_ctx_tune(crdt_ctx *ctx, const char *spec) {
+  CRDT_CHECK_CTX(ctx);
+  if (!spec) return fail(ctx, CRDT_EINVAL, "crdt_ctx_tune: spec is NULL");
+  apply_tune(ctx, spec);
+  return CRDT_OK;
+}

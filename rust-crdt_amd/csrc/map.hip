@@ -158,32 +158,39 @@ __device__ __forceinline__ void mv_append(MVState<APL, VO> &s, const u64 (&x)[AP
   s.vm |= 1u << q0;
 }
 
-// Replica stream staging.  A chunk of C replicas is loaded into registers (every load in
-// flight at once), written to one half of a per-wave LDS double buffer while the fold runs over
-// the other half, so each chunk's loads have a whole chunk of fold steps to land.  The fold
-// reads its step from LDS (dynamic index, no unrolled register ring).  LDS step image, W words:
+// Replica stream staging.  The fold reads its steps from a per-wave LDS ring of NB chunk slots
+// of C replicas (dynamic index, no unrolled register ring).  LDS step image, W = (2+VI)*A words:
 //   [0, A) entry clock | [(1+t)A, (2+t)A) value clock t < VI | [(1+VI)A, (2+VI)A) replica clock
-//   | [(2+VI)A, (2+VI)A + VI) values
-template <int APL, int VI>
+// and, in a separate per-slot array, the VI values of each step.
+// Two ways to fill a slot:
+//  * LDS-DMA (map_chunk_glds, A <= 64 even, VI = V, 16-byte aligned rows): global_load_lds
+//    writes each step image straight into its slot (no VGPRs held by loads in flight), NB-1
+//    chunks ahead; the fold waits for a chunk with a counted vmcnt.
+//  * register staging (map_chunk_load / map_chunk_store, any shape): a chunk is loaded into
+//    registers (every load in flight at once) and written to the other slot of a double buffer
+//    while the fold runs over the current one.
+template <int APL, int VI, int CM>
 struct MapChunk {
   static constexpr int words = (2 + VI) * APL + 1;  // u64 registers per staged replica per lane
   static constexpr int raw = (APL >= 4 ? 48 : 96) / words;
-  static constexpr int C = raw > 16 ? 16 : (raw < 2 ? 2 : raw);
+  static constexpr int C0 = raw > 16 ? 16 : (raw < 2 ? 2 : raw);
+  static constexpr int C = C0 > CM ? CM : C0;
   u64 e[C][APL];
   u64 c[C][VI][APL];
   u64 co[C][APL];
   u64 v[C];  // lane t < VI holds value slot t
 };
 
-template <int APL, int VI>
-__device__ __forceinline__ void map_chunk_load(MapChunk<APL, VI> &r, const MapPlan &p,
+template <int APL, int VI, int CM>
+__device__ __forceinline__ void map_chunk_load(MapChunk<APL, VI, CM> &r, const MapPlan &p,
                                                unsigned long long g, unsigned long long k,
-                                               unsigned long long i0, int lane) {
-  constexpr int C = MapChunk<APL, VI>::C;
+                                               unsigned long long i0, unsigned long long iend,
+                                               int lane) {
+  constexpr int C = MapChunk<APL, VI, CM>::C;
 #pragma unroll
   for (int s = 0; s < C; ++s) {
     const unsigned long long i = i0 + s;
-    if (i < p.R) {
+    if (i < iend) {
       const u64 *ec = p.ec + g * p.e_gs + i * p.e_rs + k * p.A;
       const u64 *vc = p.vclk + g * p.vc_gs + i * p.vc_rs + k * p.V * p.A;
       const u64 *cl = p.clock + g * p.c_gs + i * p.c_rs;
@@ -203,11 +210,11 @@ __device__ __forceinline__ void map_chunk_load(MapChunk<APL, VI> &r, const MapPl
   }
 }
 
-template <int APL, int VI>
-__device__ __forceinline__ void map_chunk_store(const MapChunk<APL, VI> &r, u64 *buf,
+template <int APL, int VI, int CM>
+__device__ __forceinline__ void map_chunk_store(const MapChunk<APL, VI, CM> &r, u64 *buf, u64 *vals,
                                                 unsigned long long A, unsigned long long W,
                                                 unsigned long long nsteps, int lane) {
-  constexpr int C = MapChunk<APL, VI>::C;
+  constexpr int C = MapChunk<APL, VI, CM>::C;
 #pragma unroll
   for (int s = 0; s < C; ++s) {
     if ((unsigned long long)s < nsteps) {
@@ -222,13 +229,61 @@ __device__ __forceinline__ void map_chunk_store(const MapChunk<APL, VI> &r, u64 
           st[(1 + VI) * A + a] = r.co[s][j];
         }
       }
-      if (lane < VI) st[(2 + VI) * A + lane] = r.v[s];
+      if (lane < VI) vals[s * VI + lane] = r.v[s];
     }
   }
 }
 
+__device__ __forceinline__ void glds16(const void *g, u64 *lds) {
+  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void *)lds, 16, 0, 0);
+}
+__device__ __forceinline__ void glds4(const void *g, u64 *lds) {
+  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void *)lds, 4, 0, 0);
+}
+
+// DMA one chunk (steps i0 .. i0+C-1, clamped to iend-1: past the end a slot holds copies that
+// are never read) into an LDS slot.  Exactly C*NI + 1 global_load_lds per call, each with at
+// least one active lane (NI = ceil(W / 128) 1-KiB pieces per step image; the values of all C
+// steps in one 4-byte-per-lane piece), so a fixed vmcnt count retires a chunk.
+template <int VI, int C, int NI>
+__device__ __forceinline__ void map_chunk_glds(const MapPlan &p, unsigned long long g, unsigned long long k,
+                                               unsigned long long i0, unsigned long long iend, u64 *img,
+                                               u64 *vals, int lane) {
+  const unsigned long long A = p.A, W = (2 + VI) * A;
+  const u64 *ecb = p.ec + g * p.e_gs + k * A;
+  const u64 *vcb = p.vclk + g * p.vc_gs + k * VI * A;
+  const u64 *clb = p.clock + g * p.c_gs;
+#pragma unroll
+  for (int s = 0; s < C; ++s) {
+    const unsigned long long i = i0 + s < iend ? i0 + s : iend - 1;
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const unsigned long long o = (unsigned long long)(j * 64 + lane) * 2;  // word offset in the image
+      if (o < W) {
+        const u64 *src = o < A ? ecb + i * p.e_rs + o
+                               : (o < (1 + VI) * A ? vcb + i * p.vc_rs + (o - A) : clb + i * p.c_rs + (o - (1 + VI) * A));
+        glds16(src, img + s * W + j * 128);
+      }
+    }
+  }
+  const int sv = lane / (2 * VI), dw = lane % (2 * VI);
+  if (sv < C) {
+    const unsigned long long i = i0 + sv < iend ? i0 + sv : iend - 1;
+    const unsigned *src = reinterpret_cast<const unsigned *>(p.vval + g * p.vv_gs + i * p.vv_rs + k * VI) + dw;
+    glds4(src, vals);
+  }
+}
+
+// Wait until at most N vector-memory ops are outstanding (counts above the 6-bit field clamp
+// to 63: waiting for more than needed is safe).
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N > 63 ? 63 : N) : "memory");
+}
+
 template <int APL, int VI>
-__device__ __forceinline__ MapStep<APL, VI> map_step_read(const u64 *st, unsigned long long A, int lane) {
+__device__ __forceinline__ MapStep<APL, VI> map_step_read(const u64 *st, const u64 *vals,
+                                                          unsigned long long A, int lane) {
   MapStep<APL, VI> in;
 #pragma unroll
   for (int j = 0; j < APL; ++j) {
@@ -240,41 +295,71 @@ __device__ __forceinline__ MapStep<APL, VI> map_step_read(const u64 *st, unsigne
     in.co[j] = on ? st[(1 + VI) * A + a] : 0;
   }
 #pragma unroll
-  for (int t = 0; t < VI; ++t) in.v[t] = st[(2 + VI) * A + t];
+  for (int t = 0; t < VI; ++t) in.v[t] = vals[t];
   return in;
 }
 
-// Speculative no-op scan over the steps of a staged chunk (A <= 64).  Lane (s, g) = (lane / 4,
-// lane % 4) checks step s of the chunk on actors g, g+4, ... against the CURRENT fold state,
-// mirrored in LDS (me = entry clock, mc = value clocks, vm = valid slots); the four groups of a
-// step are combined bitwise on the ballot masks.  Bit 4s of the result is set iff step s
-// provably leaves (present, e, vals) unchanged:
-//   present, replica has the key:   e2 <= e, and e[a] == 0 | e[a] == e2[a] | e[a] > Co[a] for
-//                                   every a (so common == e and nothing is forgotten), and the
-//                                   MVReg merge keeps every value and appends none;
-//   present, replica lacks the key: e[a] == 0 | e[a] > Co[a] (e survives the forget) and no
-//                                   value clock changes under forget(Co > e ? Co : 0);
-//   absent, replica lacks the key:  always.
-// (Absent with the replica holding the key depends on Cs and is left to the exact step.)
+// Speculative no-op scan over the steps of a staged chunk (A <= 64).  The wave checks NS steps
+// at once: lane (s, g) = (lane / LPS, lane % LPS), LPS = 64 / NS, checks step s on actors g,
+// g+LPS, ... against the CURRENT fold state, mirrored in LDS (me = entry clock, mc = value
+// clocks, vm = valid slots, mcs = acc clock Cs); the LPS lanes of a step are combined bitwise on
+// the ballot masks.  Bit LPS*s of the result is set only if step s provably leaves (present, e,
+// vals) unchanged.  With e = acc entry clock, e2 / c2[t] / Co = the replica's entry clock /
+// value clocks / clock, and Cs' >= Cs the acc clock at step s (so e2 <= Cs implies e2 <= Cs'):
+//   present, replica has the key (map.rs:170-192): common = max(e==e2?e:0, e2>Cs'?e2:0,
+//     e>Co?e:0) equals e if every actor has (e == 0 | e == e2 | e > Co) and (e2 <= e | e2 <= Cs);
+//     then deleted = (e2 > e ? e2 : 0), and the MVReg is unchanged if no own value is < an
+//     incoming one (mvreg.rs:114-118), no own value clock has an actor 0 < x <= deleted, and
+//     every incoming value is <= an own one (not appended, :120-126) or forgotten to empty by
+//     deleted (appended, then dropped by forget: only the Vec order key counter moves);
+//   present, replica lacks the key (:146-161): e[a] == 0 | e[a] > Co[a] (e survives the forget)
+//     and no value clock changes under forget(Co > e ? Co : 0);
+//   absent, replica has the key (:193-197): e2 <= Cs (seen and dropped);
+//   absent, replica lacks the key: always.
+// The deferred forget of such a step is the identity too: the state was forgotten by the max
+// of the active removes at the last exact step, the active set only shrinks until the next
+// activation (scans stop there), and forget(x) of a state already forgotten by y >= x is the
+// identity (vclock.rs:98-104).
 // Most steps of a fold change nothing, so their cost drops from a full exact step (~330 issued
 // instructions) to a share of this wave-wide scan.
-__device__ __forceinline__ u64 and4(u64 m) { return m & (m >> 1) & (m >> 2) & (m >> 3) & 0x1111111111111111ULL; }
-__device__ __forceinline__ u64 or4(u64 m) { return (m | (m >> 1) | (m >> 2) | (m >> 3)) & 0x1111111111111111ULL; }
-
-template <int VI, int VO>
-__device__ __forceinline__ u64 map_noop_steps(const u64 *buf, unsigned long long W, unsigned long long A,
-                                              const u64 *me, const u64 *mc, unsigned vm, bool present,
-                                              unsigned n, int lane) {
-  const unsigned st = (unsigned)lane >> 2;
-  const unsigned gq = (unsigned)lane & 3u;
-  const u64 *stp = buf + (st < n ? st : n - 1) * W;
-  u64 mP2 = 0, mA = ~0ull, mB = ~0ull, mB2 = ~0ull;
-  u64 mNZ[VI], mRI[VO], mLe1[VO][VI], mNe1[VO][VI], mLe2[VI][VO];
+template <int LPS>
+__device__ __forceinline__ u64 grp_mask() {
+  u64 m = 0;
 #pragma unroll
-  for (int t = 0; t < VI; ++t) mNZ[t] = 0;
+  for (int b = 0; b < 64; b += LPS) m |= 1ull << b;
+  return m;
+}
+template <int LPS>
+__device__ __forceinline__ u64 andN(u64 m) {  // bit LPS*s: AND of the LPS bits of step s
+#pragma unroll
+  for (int sh = 1; sh < LPS; sh <<= 1) m &= m >> sh;
+  return m & grp_mask<LPS>();
+}
+template <int LPS>
+__device__ __forceinline__ u64 orN(u64 m) {
+#pragma unroll
+  for (int sh = 1; sh < LPS; sh <<= 1) m |= m >> sh;
+  return m & grp_mask<LPS>();
+}
+
+template <int VI, int VO, int LPS>
+__device__ __forceinline__ u64 map_noop_steps(const u64 *buf, unsigned long long W, unsigned long long A,
+                                              const u64 *me, const u64 *mc, const u64 *mcs, unsigned vm,
+                                              bool present, unsigned n, int lane) {
+  const unsigned st = (unsigned)lane / LPS;
+  const unsigned gq = (unsigned)lane % LPS;
+  const u64 *stp = buf + (st < n ? st : n - 1) * W;
+  u64 mP2 = 0, mT = ~0ull, mB = ~0ull, mB2 = ~0ull, mCs = ~0ull;
+  u64 mNZ[VI], mVan[VI], mRI[VO], mDL[VO], mLe1[VO][VI], mNe1[VO][VI], mLe2[VI][VO];
+#pragma unroll
+  for (int t = 0; t < VI; ++t) {
+    mNZ[t] = 0;
+    mVan[t] = ~0ull;
+  }
 #pragma unroll
   for (int q = 0; q < VO; ++q) {
     mRI[q] = ~0ull;
+    mDL[q] = ~0ull;
 #pragma unroll
     for (int t = 0; t < VI; ++t) {
       mLe1[q][t] = ~0ull;
@@ -282,29 +367,36 @@ __device__ __forceinline__ u64 map_noop_steps(const u64 *buf, unsigned long long
       mLe2[t][q] = ~0ull;
     }
   }
-  const unsigned iters = (unsigned)((A + 3) / 4);
+  const unsigned iters = (unsigned)((A + LPS - 1) / LPS);
   for (unsigned m = 0; m < iters; ++m) {  // uniform trip count: absent actors read as zeros
-    const unsigned long long a = gq + 4ull * m;
+    const unsigned long long a = gq + (unsigned long long)LPS * m;
     const bool on = a < A;
     const u64 e2 = on ? stp[a] : 0;
     const u64 co = on ? stp[(1 + VI) * A + a] : 0;
     const u64 ea = on ? me[a] : 0;
+    const u64 ca = on ? mcs[a] : 0;
     u64 c2[VI], sq[VO];
 #pragma unroll
     for (int t = 0; t < VI; ++t) c2[t] = on ? stp[(1 + t) * A + a] : 0;
 #pragma unroll
     for (int q = 0; q < VO; ++q) sq[q] = (on && (vm & (1u << q))) ? mc[q * A + a] : 0;
     mP2 |= __ballot(e2 != 0);
-    mA &= __ballot(e2 <= ea);
+    mT &= __ballot(e2 <= ea || e2 <= ca);
     mB &= __ballot(ea == 0 || ea == e2 || ea > co);
     mB2 &= __ballot(ea == 0 || ea > co);
+    mCs &= __ballot(e2 <= ca);
     const u64 ri = co > ea ? co : 0;
+    const u64 dl = e2 > ea ? e2 : 0;
 #pragma unroll
-    for (int t = 0; t < VI; ++t) mNZ[t] |= __ballot(c2[t] != 0);
+    for (int t = 0; t < VI; ++t) {
+      mNZ[t] |= __ballot(c2[t] != 0);
+      mVan[t] &= __ballot(c2[t] <= dl);
+    }
 #pragma unroll
     for (int q = 0; q < VO; ++q) {
       if (vm & (1u << q)) {
         mRI[q] &= __ballot(sq[q] == 0 || sq[q] > ri);
+        mDL[q] &= __ballot(sq[q] == 0 || sq[q] > dl);
 #pragma unroll
         for (int t = 0; t < VI; ++t) {
           mLe1[q][t] &= __ballot(sq[q] <= c2[t]);
@@ -314,33 +406,35 @@ __device__ __forceinline__ u64 map_noop_steps(const u64 *buf, unsigned long long
       }
     }
   }
-  const u64 P2 = or4(mP2);
+  const u64 G1 = grp_mask<LPS>();
+  const u64 P2 = orN<LPS>(mP2);
   u64 NZ[VI];
 #pragma unroll
-  for (int t = 0; t < VI; ++t) NZ[t] = or4(mNZ[t]);
-  u64 mvbad = 0, riok = 0x1111111111111111ULL;
+  for (int t = 0; t < VI; ++t) NZ[t] = orN<LPS>(mNZ[t]);
+  u64 mvbad = 0, riok = G1;
 #pragma unroll
   for (int q = 0; q < VO; ++q) {
     if (vm & (1u << q)) {
-      riok &= and4(mRI[q]);
+      riok &= andN<LPS>(mRI[q]);
+      mvbad |= ~andN<LPS>(mDL[q]);  // an own value clock changed by forget(deleted)
 #pragma unroll
-      for (int t = 0; t < VI; ++t) mvbad |= and4(mLe1[q][t]) & or4(mNe1[q][t]) & NZ[t];  // a value dropped
+      for (int t = 0; t < VI; ++t) mvbad |= andN<LPS>(mLe1[q][t]) & orN<LPS>(mNe1[q][t]) & NZ[t];  // dropped
     }
   }
 #pragma unroll
   for (int t = 0; t < VI; ++t) {
-    u64 cov = 0;
+    u64 cov = andN<LPS>(mVan[t]);  // appended, then forgotten to empty
 #pragma unroll
     for (int q = 0; q < VO; ++q)
-      if (vm & (1u << q)) cov |= and4(mLe2[t][q]);
-    mvbad |= NZ[t] & ~cov;  // an incoming value appended
+      if (vm & (1u << q)) cov |= andN<LPS>(mLe2[t][q]);
+    mvbad |= NZ[t] & ~cov;  // an incoming value kept
   }
-  const u64 both = P2 & and4(mA) & and4(mB) & ~mvbad;
-  const u64 only_acc = ~P2 & and4(mB2) & riok;
-  return (present ? (both | only_acc) : ~P2) & 0x1111111111111111ULL;
+  const u64 both = P2 & andN<LPS>(mT) & andN<LPS>(mB) & ~mvbad;
+  const u64 only_acc = ~P2 & andN<LPS>(mB2) & riok;
+  return (present ? (both | only_acc) : (~P2 | andN<LPS>(mCs))) & G1;
 }
 
-template <int APL, int VI, int VO>
+template <int APL, int VI, int VO, int CM, int NB, bool GL>
 __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan p) {
   const unsigned long long g = blockIdx.x / p.K;
   const unsigned long long k = blockIdx.x % p.K;
@@ -381,22 +475,29 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan p) {
   const u64 kbit = 1ull << (k % 64);
 
   extern __shared__ u64 map_lds[];
-  constexpr int C = MapChunk<APL, VI>::C;
+  constexpr int C = GL ? CM : MapChunk<APL, VI, CM>::C;
+  static_assert(!GL || (APL == 1 && NB >= 2), "LDS-DMA staging: one actor per lane");
+  static_assert(GL || NB == 2, "register staging double-buffers");
+  // speculative scan geometry: NS >= C steps per scan, LPS lanes per step
+  constexpr int NS = C > 8 ? 16 : (C > 4 ? 8 : (C > 2 ? 4 : 2));
+  constexpr int LPS = 64 / NS;
   const unsigned long long A = p.A;
-  const unsigned long long W = (2 + VI) * A + VI;
-  // (buffer addresses are always computed from map_lds: a pointer table would hide the LDS
-  // address space and turn every access into a flat op that waits on the prefetch loads)
-
-  // The removes naming this key, in replica order, gathered once into LDS (row, index), so the
-  // fold loop never waits on a global load for them (a vector load would drain the whole
-  // prefetched chunk: vmcnt is in order).  More than kMapL of them: walk the group list.
-  unsigned *lrow = reinterpret_cast<unsigned *>(map_lds + 2 * C * W);
+  const unsigned long long W = (2 + VI) * A;
+  // LDS: NB image slots (C*W words each), NB value slots (C*VI), the per-key remove list, the
+  // fold-state mirror.  (Addresses are always computed from map_lds: a pointer table would hide
+  // the LDS address space and turn every access into a flat op.)
+  u64 *const vbase = map_lds + NB * C * W;
+  unsigned *lrow = reinterpret_cast<unsigned *>(vbase + NB * C * VI);
   unsigned *lidx = lrow + kMapL;
-  // fold-state mirror read by the speculative scan: entry clock, then VO value clocks
-  u64 *mirror = map_lds + 2 * C * W + kMapL;  // (kMapL u64 = the two u32 lists)
+  // fold-state mirror read by the speculative scan: entry clock, VO value clocks, acc clock
+  u64 *mirror = vbase + NB * C * VI + kMapL;  // (kMapL u64 = the two u32 lists)
   constexpr bool kSpec = APL == 1 && VO <= 4;
   if (kSpec)
-    for (unsigned long long x = lane; x < (1 + VO) * A; x += 64) mirror[x] = 0;
+    for (unsigned long long x = lane; x < (2 + VO) * A; x += 64) mirror[x] = 0;
+
+  // The removes naming this key, in replica order, gathered once into LDS (row, index), so the
+  // fold loop never waits on a global load for them (a vector load would drain the prefetched
+  // chunks: vmcnt is in order).  More than kMapL of them: walk the group list.
   unsigned long long nl = 0;
   {
     int badl = 0;
@@ -426,47 +527,92 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan p) {
   unsigned next_row = (!direct && nl > 0) ? lrow[0] : 0xffffffffu;
   const unsigned long long nch = (R + C - 1) / C;
   int cool = 0;
-  MapChunk<APL, VI> regs;
-  if (nch > 0) {
-    map_chunk_load(regs, p, g, k, 0, lane);
-    map_chunk_store(regs, map_lds, A, W, R < (unsigned long long)C ? R : C, lane);
-    if (nch > 1) map_chunk_load(regs, p, g, k, C, lane);
+#ifdef MAP_STATS
+  unsigned st_exact = 0, st_scan = 0, st_fail = 0, st_nq = 0, st_pres = 0;
+#endif
+  // chunk staging
+  MapChunk<APL, VI, (GL ? 2 : CM)> regs;
+  const int ni = GL ? (int)((W + 127) / 128) : 0;  // 1-KiB pieces per step image (GL: 1 or 2)
+  if constexpr (GL) {
+    for (unsigned long long c = 0; c + 1 < NB && c < nch; ++c) {
+      if (ni == 1) map_chunk_glds<VI, C, 1>(p, g, k, c * C, R, map_lds + c * C * W, vbase + c * C * VI, lane);
+      else map_chunk_glds<VI, C, 2>(p, g, k, c * C, R, map_lds + c * C * W, vbase + c * C * VI, lane);
+    }
+  } else {
+    if (nch > 0) {
+      map_chunk_load(regs, p, g, k, 0, R, lane);
+      map_chunk_store(regs, map_lds, vbase, A, W, R < (unsigned long long)C ? R : C, lane);
+      if (nch > 1) map_chunk_load(regs, p, g, k, C, R, lane);
+    }
   }
 
   for (unsigned long long ch = 0; ch < nch; ++ch) {
-    const u64 *buf = map_lds + ((ch & 1) ? C * W : 0);
+    const unsigned slot = (unsigned)(ch % NB);
+    const u64 *buf = map_lds + slot * C * W;
+    const u64 *vb = vbase + slot * C * VI;
+    if constexpr (GL) {
+      // issue chunk ch+NB-1 into the slot chunk ch-1 used, then wait for chunk ch
+      const unsigned long long nx = ch + NB - 1;
+      if (nx < nch) {
+        const unsigned ns = (unsigned)(nx % NB);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot's last LDS reads are done
+        if (ni == 1) map_chunk_glds<VI, C, 1>(p, g, k, nx * C, R, map_lds + ns * C * W, vbase + ns * C * VI, lane);
+        else map_chunk_glds<VI, C, 2>(p, g, k, nx * C, R, map_lds + ns * C * W, vbase + ns * C * VI, lane);
+      }
+      const unsigned long long after = (nch - 1 - ch) < (unsigned long long)(NB - 1) ? nch - 1 - ch : NB - 1;
+      if (ni == 1) {
+        constexpr int P1 = C + 1;
+        if (after == 0) wait_vmcnt<0>();
+        else if (after == 1) wait_vmcnt<P1>();
+        else if (NB > 2 && after == 2) wait_vmcnt<(NB > 2 ? 2 * P1 : 0)>();
+        else wait_vmcnt<(NB > 3 ? 3 * P1 : 0)>();
+      } else {
+        constexpr int P2 = 2 * C + 1;
+        if (after == 0) wait_vmcnt<0>();
+        else if (after == 1) wait_vmcnt<P2>();
+        else if (NB > 2 && after == 2) wait_vmcnt<(NB > 2 ? 2 * P2 : 0)>();
+        else wait_vmcnt<(NB > 3 ? 3 * P2 : 0)>();
+      }
+    }
     const unsigned long long i0 = ch * C;
     const unsigned long long n = R - i0 < (unsigned long long)C ? R - i0 : C;
     unsigned long long s = 0;
 #pragma unroll 1
     while (s < n) {
-      if (kSpec && cool == 0 && nq == 0 && !slow && !direct) {
+      if (kSpec && cool == 0 && !slow && !direct) {
         // steps s.. that provably change nothing, up to the next remove naming this key
         const unsigned long long lim0 = next_row < i0 + n ? next_row - i0 : n;
         const unsigned long long lim = lim0 > s ? lim0 : s;
         unsigned long long j = s;
         if (lim > s) {
-          const u64 noop = map_noop_steps<VI, VO>(buf, W, A, mirror, mirror + A, mv.vm, present,
-                                                   (unsigned)n, lane);
-          const u64 from = (s >= 16) ? 0 : (~0ull << (4 * s));
-          const u64 upto = (lim >= 16) ? ~0ull : ((1ull << (4 * lim)) - 1);
-          const u64 stop = ~noop & 0x1111111111111111ULL & from & upto;
-          j = stop ? (unsigned long long)(__builtin_ctzll(stop) >> 2) : lim;
+          const u64 noop = map_noop_steps<VI, VO, LPS>(buf, W, A, mirror, mirror + A,
+                                                        mirror + (1 + VO) * A, mv.vm, present,
+                                                        (unsigned)n, lane);
+          const u64 from = (s >= NS) ? 0 : (~0ull << (LPS * s));
+          const u64 upto = (lim >= NS) ? ~0ull : ((1ull << (LPS * lim)) - 1);
+          const u64 stop = ~noop & grp_mask<LPS>() & from & upto;
+          j = stop ? (unsigned long long)(__builtin_ctzll(stop) / LPS) : lim;
           for (unsigned long long u = s; u < j; ++u) {  // acc.clock.merge of the skipped replicas
             const unsigned long long a = lane;
             const u64 co = a < A ? buf[u * W + (1 + VI) * A + a] : 0;
             cs[0] = cs[0] > co ? cs[0] : co;
           }
+          if (j > s && (unsigned long long)lane < A) mirror[(1 + VO) * A + lane] = cs[0];
           if (j == s) cool = 4;  // the scan found nothing to skip: run a few exact steps first
+#ifdef MAP_STATS
+          ++st_scan; if (j == s) ++st_fail;
+#endif
         }
         s = j;
         if (s >= n) break;
       }
       if (cool > 0) --cool;
+#ifdef MAP_STATS
+      ++st_exact; if (nq) ++st_nq; if (present) ++st_pres;
+#endif
       const unsigned long long i = i0 + s;
-      const MapStep<APL, VI> in = map_step_read<APL, VI>(buf + s * W, A, lane);
+      const MapStep<APL, VI> in = map_step_read<APL, VI>(buf + s * W, vb + s * VI, A, lane);
       ++s;
-      {
       // ---- 1. entry join (map.rs:142-210) ----
       const bool p2 = any_nz(in.e);
       if (present && !p2) {
@@ -599,7 +745,7 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan p) {
             next_row = lp < nl ? lrow[lp] : 0xffffffffu;
           } else {
             if (dp >= dend) break;
-            const unsigned row = p.def_row[dp];
+            const unsigned long long row = p.def_row[dp];
             if (row > i) break;
             d = dp++;
             if (!(p.def_keys[d * p.Kw + kw] & kbit)) continue;
@@ -667,23 +813,30 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan p) {
       // ---- 3. acc.clock.merge(other.clock) (map.rs:217) ----
 #pragma unroll
       for (int j = 0; j < APL; ++j) cs[j] = cs[j] > in.co[j] ? cs[j] : in.co[j];
-      }
+
       if (kSpec) {  // refresh the state mirror for the next scan
         if ((unsigned long long)lane < A) {
           mirror[lane] = e[0];
+          mirror[(1 + VO) * A + lane] = cs[0];
 #pragma unroll
           for (int q = 0; q < VO; ++q) mirror[(1 + q) * A + lane] = mv.c[q][0];
         }
       }
     }
-    if (ch + 1 < nch) {  // stage the next chunk (its loads were issued a whole chunk ago)
-      const unsigned long long nn = R - (ch + 1) * C < (unsigned long long)C ? R - (ch + 1) * C : C;
-      map_chunk_store(regs, map_lds + (((ch + 1) & 1) ? C * W : 0), A, W, nn, lane);
-      if (ch + 2 < nch) map_chunk_load(regs, p, g, k, (ch + 2) * C, lane);
+    if constexpr (!GL) {
+      if (ch + 1 < nch) {  // stage the next chunk (its loads were issued a whole chunk ago)
+        const unsigned long long nn = R - (ch + 1) * C < (unsigned long long)C ? R - (ch + 1) * C : C;
+        const unsigned ns = (unsigned)((ch + 1) % NB);
+        map_chunk_store(regs, map_lds + ns * C * W, vbase + ns * C * VI, A, W, nn, lane);
+        if (ch + 2 < nch) map_chunk_load(regs, p, g, k, (ch + 2) * C, R, lane);
+      }
     }
   }
   if (direct && dp < dend) bad = 1;  // a row >= R was never reached
 
+#ifdef MAP_STATS
+  if (lane == 0 && (k % 97) == 0) printf("k=%llu exact=%u scan=%u fail=%u nq=%u pres=%u nl=%llu\n", k, st_exact, st_scan, st_fail, st_nq, st_pres, nl);
+#endif
   // ---- egress: slots in Vec order (ascending order key) ----
   const int nv = __builtin_popcount(mv.vm);
   if (nv > (int)p.Vout) ovf |= 1;
@@ -733,29 +886,49 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan p) {
 
 using namespace crdt;
 
-template <int APL, int VI, int VO>
+template <int APL, int VI, int VO, int CM, int NB, bool GL>
 static hipError_t launch_map(const MapPlan &p, unsigned long long blocks, hipStream_t s) {
-  const size_t W = (2 + VI) * p.A + VI;
-  const size_t lds = 2 * (size_t)MapChunk<APL, VI>::C * W * sizeof(u64) + kMapL * 2 * sizeof(unsigned) +
-                     (1 + VO) * p.A * sizeof(u64);
+  constexpr int C = GL ? CM : MapChunk<APL, VI, CM>::C;
+  const size_t W = (2 + VI) * p.A;
+  const size_t lds = (size_t)NB * C * (W + VI) * sizeof(u64) + kMapL * 2 * sizeof(unsigned) +
+                     (2 + VO) * p.A * sizeof(u64);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   if (lds > 64 * 1024) {  // beyond the default dynamic-LDS limit (gfx950 has 160 KB per CU)
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&map_fold_kernel<APL, VI, VO>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&map_fold_kernel<APL, VI, VO, CM, NB, GL>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL((map_fold_kernel<APL, VI, VO>), dim3((unsigned)blocks), dim3(64), lds, s, p);
+  hipLaunchKernelGGL((map_fold_kernel<APL, VI, VO, CM, NB, GL>), dim3((unsigned)blocks), dim3(64), lds, s, p);
   return hipGetLastError();
 }
 
+// Register-staged fold for VI input / 2*VI state value slots (any shape within the limits).
 template <int APL>
 static hipError_t launch_map_vi(const MapPlan &p, int VI, unsigned long long blocks, hipStream_t s) {
   switch (VI) {
-    case 1: return launch_map<APL, 1, 2>(p, blocks, s);
-    case 2: return launch_map<APL, 2, 4>(p, blocks, s);
-    default: return launch_map<APL, 4, 8>(p, blocks, s);
+    case 1: return launch_map<APL, 1, 2, 16, 2, false>(p, blocks, s);
+    case 2: return launch_map<APL, 2, 4, 16, 2, false>(p, blocks, s);
+    default: return launch_map<APL, 4, 8, 16, 2, false>(p, blocks, s);
   }
 }
+
+// LDS-DMA fold (A <= 64, even; VI = V <= 2; 4 state values): chunk C and ring depth NB.
+template <int VI>
+static hipError_t launch_map_glds(const MapPlan &p, int cm, int nb, unsigned long long blocks, hipStream_t s) {
+  if (cm == 8 && nb == 4) return launch_map<1, VI, 4, 8, 4, true>(p, blocks, s);
+  if (cm == 8 && nb == 3) return launch_map<1, VI, 4, 8, 3, true>(p, blocks, s);
+  if (cm == 16 && nb == 3) return launch_map<1, VI, 4, 16, 3, true>(p, blocks, s);
+  return launch_map<1, VI, 4, 16, 2, true>(p, blocks, s);
+}
+
+// Smallest VI (1, 2, 4) with VI >= V and 2*VI >= min(8, want): the fold state holds 2*VI values.
+static int map_vi(size_t V, size_t want) {
+  int VI = 1;
+  while ((size_t)VI < V || (size_t)(2 * VI) < (want < 8 ? want : 8)) VI *= 2;
+  return VI > 4 ? 4 : VI;
+}
+
+static bool aligned16(const void *x) { return (reinterpret_cast<uintptr_t>(x) & 15) == 0; }
 
 extern "C" int crdt_map_lub_many(crdt_ctx *ctx, const crdt_map_batch *in, crdt_map_out *out) {
   CRDT_CHECK_CTX(ctx);
@@ -779,6 +952,7 @@ extern "C" int crdt_map_lub_many(crdt_ctx *ctx, const crdt_map_batch *in, crdt_m
   if (D > 0xffffffffULL) return fail(ctx, CRDT_EUNSUPPORTED, "map_lub_many: too many deferred");
   CRDT_HIP(ctx, hipSetDevice(ctx->device));
   const size_t Kw = (K + 63) / 64;
+  const size_t want = out->Vstate > Vout ? out->Vstate : Vout;
 
   MapPlan p{};
   p.clock = (const u64 *)in->clock;
@@ -817,18 +991,23 @@ extern "C" int crdt_map_lub_many(crdt_ctx *ctx, const crdt_map_batch *in, crdt_m
     p.def_clock = (const u64 *)in->def_clock;
     p.def_keys = (const u64 *)in->def_keys;
   }
-  // value-slot templates: VI >= V input slots, VO = 2*VI state slots >= min(8, Vout, Vstate)
-  const size_t want = out->Vstate > Vout ? out->Vstate : Vout;
-  int VI = 1;
-  while ((size_t)VI < V || (size_t)(2 * VI) < (want < 8 ? want : 8)) VI *= 2;
-  if (VI > 4) VI = 4;
-  const int APL = A <= 64 ? 1 : (A <= 128 ? 2 : 4);
+  // LDS-DMA staging when every step image is whole 16-byte pieces (A even, 16-byte aligned
+  // rows and strides) and the state fits 4 values; register staging otherwise
+  const bool even = ((p.c_rs | p.c_gs | p.e_rs | p.e_gs | p.vc_rs | p.vc_gs) & 1) == 0;
+  const bool glds = ctx->tune.map_glds && R > 0 && A <= 64 && (A & 1) == 0 && (V == 1 || V == 2) &&
+                    want <= 4 && even && aligned16(p.clock) && aligned16(p.ec) && aligned16(p.vclk);
   const unsigned long long blocks = G * K;
   timing_begin(ctx, "map_fold");
   hipError_t he;
-  if (APL == 1) he = launch_map_vi<1>(p, VI, blocks, ctx->stream);
-  else if (APL == 2) he = launch_map_vi<2>(p, VI, blocks, ctx->stream);
-  else he = launch_map_vi<4>(p, VI, blocks, ctx->stream);
+  if (glds) {
+    he = V == 1 ? launch_map_glds<1>(p, ctx->tune.map_chunk, ctx->tune.map_ring, blocks, ctx->stream)
+                : launch_map_glds<2>(p, ctx->tune.map_chunk, ctx->tune.map_ring, blocks, ctx->stream);
+  } else {
+    const int VI = map_vi(V, want);
+    if (A <= 64) he = launch_map_vi<1>(p, VI, blocks, ctx->stream);
+    else if (A <= 128) he = launch_map_vi<2>(p, VI, blocks, ctx->stream);
+    else he = launch_map_vi<4>(p, VI, blocks, ctx->stream);
+  }
   timing_end(ctx);
   if (he != hipSuccess) return hip_fail(ctx, he, "map_fold_kernel launch");
 

@@ -79,7 +79,7 @@ ctx.set_timing(False)
 kern = ms / n / 1e3
 flags = res.flags.cpu().numpy()
 out = {"workload": f"map<u32,mvreg<u64>> lub {R}x{K}x{A} V={V}", "replicas": R, "keys": K,
-       "actors": A, "slots": V, "deferred": D, "wall_ms": wall * 1e3, "kernel_ms": kern * 1e3,
+       "actors": A, "slots": V, "deferred": D, "wall_ms": wall * 1e3, "kernel_ms": kern * 1e3, "tune": os.environ.get("CRDT_TUNE", ""),
        "algorithmic_bytes": alg_bytes, "kernel_GBs": alg_bytes / kern / 1e9,
        "frac_of_8TBs": alg_bytes / kern / 8e12, "replica_merges_per_s": R / wall,
        "flags": int(np.bitwise_or.reduce(flags)) if flags.size else 0}

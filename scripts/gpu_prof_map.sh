@@ -1,11 +1,13 @@
 #!/bin/bash
-# PMC passes over the Map fold kernel: instruction mix and stall counters (one pass per group).
+# PMC passes over the Map fold kernel: instruction mix, stall and memory counters (one pass per group).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 mkdir -p gpurun_out/pmc_map
 export TMPDIR=/tmp
 i=0
 for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \
-           "SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INST_CYCLES_VMEM_RD SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_INSTS_BRANCH SQ_ACTIVE_INST_ANY"; do
+           "SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INST_CYCLES_VMEM_RD SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_INSTS_BRANCH SQ_ACTIVE_INST_ANY" \
+           "SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SALU SQ_ACTIVE_INST_MISC SQ_ACTIVE_INST_FLAT SQ_INST_CYCLES_SALU SQ_INSTS_LDS" \
+           "TCC_HIT_sum TCC_MISS_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum"; do
   i=$((i+1))
   echo "== pass $i: $set"
   timeout -s KILL 120 rocprofv3 --pmc $set --output-format csv -d gpurun_out/pmc_map/p$i -o run -- python3 scripts/prof_map.py "$@" > gpurun_out/pmc_map/p$i.log 2>&1

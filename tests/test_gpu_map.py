@@ -13,6 +13,21 @@ pytestmark = pytest.mark.gpu
 
 import crdts_gpu as cg  # noqa: E402
 
+# Staging paths of the fold kernel (results must not depend on them): LDS-DMA ring with 16- and
+# 8-replica chunks and 2-4 slots (taken where A is even, V <= 2 and the state fits 4 values),
+# and register staging (every shape).
+MODES = ["mglds=1,mchunk=16,mring=2", "mglds=1,mchunk=8,mring=4", "mglds=1,mchunk=16,mring=3", "mglds=0"]
+
+
+@pytest.fixture(scope="module", params=MODES)
+def mctx(request):
+    import torch
+    assert torch.cuda.is_available()
+    torch.cuda.set_device(0)
+    ctx = cg.Context(0)
+    ctx.tune(request.param)
+    return ctx
+
 
 def _gpu(gpu_ctx, d, vout, groups=None):
     """d: dense dict of one group (or stacked when groups = list of per-group D counts)."""
@@ -44,7 +59,7 @@ def _check(gpu_ctx, d, vout):
 
 
 @pytest.mark.parametrize("seed", range(24))
-def test_map_lub_many_op_replay(gpu_ctx, seed):
+def test_map_lub_many_op_replay(mctx, seed):
     rng = np.random.default_rng(seed)
     K, A = int(rng.integers(1, 70)), int(rng.integers(1, 9))
     R = int(rng.integers(1, 40))
@@ -53,7 +68,7 @@ def test_map_lub_many_op_replay(gpu_ctx, seed):
     V = O.max_vals(maps)
     d = O.map_to_dense(maps, K, A, V)
     vout = max(4, O.max_vals([O.map_fold_objects(maps)]))
-    _check(gpu_ctx, d, vout)
+    _check(mctx, d, vout)
 
 
 def _random_dense(rng, R, K, A, V, cmax, D=None, keys_per_rm=None):
@@ -85,7 +100,7 @@ def _random_dense(rng, R, K, A, V, cmax, D=None, keys_per_rm=None):
     (5, 12, 4, 64, 1, 3), (6, 10, 6, 65, 1, 3), (7, 6, 3, 200, 1, 3), (8, 50, 130, 3, 3, 5),
     (9, 30, 8, 8, 2, 4), (10, 33, 2, 5, 2, 1000), (11, 16, 5, 100, 2, 2), (12, 64, 3, 2, 4, 3),
 ])
-def test_map_lub_many_arbitrary(gpu_ctx, seed, R, K, A, V, cmax):
+def test_map_lub_many_arbitrary(mctx, seed, R, K, A, V, cmax):
     """Arbitrary dense states: exactness of the left fold does not rest on any invariant."""
     rng = np.random.default_rng(seed)
     d = _random_dense(rng, R, K, A, V, cmax)
@@ -95,12 +110,12 @@ def test_map_lub_many_arbitrary(gpu_ctx, seed, R, K, A, V, cmax):
     vout = max(1, int(exp[4].max()) if exp[4].size else 1)
     if int(peak.max()) > 8:  # beyond the kernel's state capacity: must be reported, not wrong
         with pytest.raises(cg.map.MapCapacityError):
-            _gpu(gpu_ctx, d, vout)
+            _gpu(mctx, d, vout)
         return
-    _check(gpu_ctx, d, vout)
+    _check(mctx, d, vout)
 
 
-def test_map_many_concurrent_deferred(gpu_ctx):
+def test_map_many_concurrent_deferred(mctx):
     """More than the 4 register-tracked removes active on one key: the rescan path."""
     rng = np.random.default_rng(77)
     R, K, A = 40, 3, 4
@@ -108,10 +123,10 @@ def test_map_many_concurrent_deferred(gpu_ctx):
     d["def_clock"][:, 0] = 50  # never dominated: every remove stays active to the end
     exp = O.map_fold(d["clock"], d["ec"], d["vclk"], d["vval"], d["def_row"], d["def_clock"],
                      d["def_keys"], 64)
-    _check(gpu_ctx, d, max(1, int(exp[4].max())))
+    _check(mctx, d, max(1, int(exp[4].max())))
 
 
-def test_map_groups(gpu_ctx):
+def test_map_groups(mctx):
     G, R, K, A = 3, 15, 10, 5
     parts = []
     for g in range(G):
@@ -122,7 +137,7 @@ def test_map_groups(gpu_ctx):
     st["def_clock"] = np.concatenate([p["def_clock"] for p in parts])
     st["def_keys"] = np.concatenate([p["def_keys"] for p in parts])
     counts = [p["def_row"].shape[0] for p in parts]
-    res, kw = _gpu(gpu_ctx, st, 6, groups=counts)
+    res, kw = _gpu(mctx, st, 6, groups=counts)
     off = np.cumsum([0] + counts)
     for g, p in enumerate(parts):
         exp = O.map_fold(p["clock"], p["ec"], p["vclk"], p["vval"], p["def_row"], p["def_clock"],
@@ -174,16 +189,16 @@ def test_synth_map_matches_cpu(gpu_ctx):
     np.testing.assert_array_equal(to_host(inp.def_keys), dfr[2])
 
 
-@pytest.mark.parametrize("R,K,A,kmax", [(4096, 256, 32, 64), (3000, 100, 7, 40)])
-def test_map_synth_sampled_keys(gpu_ctx, R, K, A, kmax):
+@pytest.mark.parametrize("R,K,A,kmax", [(4096, 256, 32, 64), (3000, 100, 7, 40), (2000, 64, 64, 30), (1500, 40, 2, 9)])
+def test_map_synth_sampled_keys(mctx, R, K, A, kmax):
     """Synthetic replicas in HBM, folded on the GPU; the oracle folds a key sample over every
     replica (keys are independent given the clocks) and must match bit for bit."""
     from crdts_gpu import synth
     seed = 0x5EED0004
-    inp = synth.map_replicas(gpu_ctx, R, K, A, 2, seed, kmax=kmax, p_def=0.1)
+    inp = synth.map_replicas(mctx, R, K, A, 2, seed, kmax=kmax, p_def=0.1)
     res = cg.map.lub_many(inp.clock, inp.ec, inp.vclk, inp.vval, def_off=inp.def_off,
                           def_row=inp.def_row, def_clock=inp.def_clock, def_keys=inp.def_keys,
-                          vout=4, ctx=gpu_ctx)
+                          vout=4, ctx=mctx)
     keys = np.random.default_rng(R).choice(K, size=8, replace=False)
     dfr = O.synth_map_deferred(seed, R, K, A, kmax, p_def=0.1)
     d = O.synth_map(seed, R, K, A, 2, kmax, keys=keys, deferred=dfr)
@@ -204,3 +219,17 @@ def test_map_synth_sampled_keys(gpu_ctx, R, K, A, kmax):
             got_sub.add((c, sub))
     exp_sub = {(c, ks) for c, ks in exp[5] if ks}
     assert got_sub == exp_sub
+
+
+@pytest.mark.parametrize("seed,R,K,A,V", [(21, 37, 9, 2, 1), (22, 70, 5, 8, 2), (23, 19, 6, 64, 2),
+                                         (24, 50, 12, 32, 2), (25, 33, 3, 16, 1), (26, 1, 4, 4, 2)])
+def test_map_even_actor_shapes(mctx, seed, R, K, A, V):
+    """Shapes the LDS-DMA staging takes (A even, V <= 2, 4 output slots), incl. partial chunks."""
+    rng = np.random.default_rng(seed)
+    d = _random_dense(rng, R, K, A, V, cmax=4)
+    peak = np.zeros(K, np.uint64)
+    exp = O.map_fold(d["clock"], d["ec"], d["vclk"], d["vval"], d["def_row"], d["def_clock"],
+                     d["def_keys"], 64, peak=peak)
+    if int(peak.max()) > 8 or int(exp[4].max() if exp[4].size else 0) > 4:
+        pytest.skip("needs more than 4 output values")
+    _check(mctx, d, 4)
