@@ -308,10 +308,13 @@ __device__ __forceinline__ MapStep<APL, VI> map_step_read(const u64 *st, const u
 // value clocks / clock, and Cs' >= Cs the acc clock at step s (so e2 <= Cs implies e2 <= Cs'):
 //   present, replica has the key (map.rs:170-192): common = max(e==e2?e:0, e2>Cs'?e2:0,
 //     e>Co?e:0) equals e if every actor has (e == 0 | e == e2 | e > Co) and (e2 <= e | e2 <= Cs);
-//     then deleted = (e2 > e ? e2 : 0), and the MVReg is unchanged if no own value is < an
-//     incoming one (mvreg.rs:114-118), no own value clock has an actor 0 < x <= deleted, and
-//     every incoming value is <= an own one (not appended, :120-126) or forgotten to empty by
-//     deleted (appended, then dropped by forget: only the Vec order key counter moves);
+//     then deleted = (e2 > e ? e2 : 0).  The MVReg is unchanged if (a) the own values are an
+//     antichain (the caller only scans then), (b) forget(deleted) changes no own value clock
+//     (no actor with 0 < x <= deleted), and (c) every incoming value is <= an own one (not
+//     appended, mvreg.rs:120-126) or forgotten to empty by deleted (appended, then dropped:
+//     only the Vec order key counter moves).  No own value is dropped by the merge then
+//     (mvreg.rs:114-118): own < incoming t <= own' contradicts (a); own < t with t <= deleted
+//     means own <= deleted, which (b) excludes for a non-empty clock;
 //   present, replica lacks the key (:146-161): e[a] == 0 | e[a] > Co[a] (e survives the forget)
 //     and no value clock changes under forget(Co > e ? Co : 0);
 //   absent, replica has the key (:193-197): e2 <= Cs (seen and dropped);
@@ -320,8 +323,9 @@ __device__ __forceinline__ MapStep<APL, VI> map_step_read(const u64 *st, const u
 // of the active removes at the last exact step, the active set only shrinks until the next
 // activation (scans stop there), and forget(x) of a state already forgotten by y >= x is the
 // identity (vclock.rs:98-104).
-// Most steps of a fold change nothing, so their cost drops from a full exact step (~330 issued
-// instructions) to a share of this wave-wide scan.
+// Most steps of a fold change nothing, so their cost drops from a full exact step to a share
+// of this wave-wide scan: per actor and step one vector compare and one scalar mask op per
+// test, all LDS reads unpredicated (lanes past A read actor A-1 and are masked out).
 template <int LPS>
 __device__ __forceinline__ u64 grp_mask() {
   u64 m = 0;
@@ -343,82 +347,63 @@ __device__ __forceinline__ u64 orN(u64 m) {
 }
 
 template <int VI, int VO, int LPS>
-__device__ __forceinline__ u64 map_noop_steps(const u64 *buf, unsigned long long W, unsigned long long A,
-                                              const u64 *me, const u64 *mc, const u64 *mcs, unsigned vm,
-                                              bool present, unsigned n, int lane) {
+__device__ __forceinline__ u64 map_noop_steps(const u64 *buf, unsigned W, unsigned A, const u64 *me,
+                                              const u64 *mc, const u64 *mcs, unsigned vm, bool present,
+                                              unsigned n, int lane) {
   const unsigned st = (unsigned)lane / LPS;
   const unsigned gq = (unsigned)lane % LPS;
   const u64 *stp = buf + (st < n ? st : n - 1) * W;
-  u64 mP2 = 0, mT = ~0ull, mB = ~0ull, mB2 = ~0ull, mCs = ~0ull;
-  u64 mNZ[VI], mVan[VI], mRI[VO], mDL[VO], mLe1[VO][VI], mNe1[VO][VI], mLe2[VI][VO];
+  u64 mP2 = 0, mE = ~0ull, mO = ~0ull, mCs = ~0ull;
+  u64 mRI[VO], mDL[VO], mLe2[VI][VO], mVan[VI];
 #pragma unroll
-  for (int t = 0; t < VI; ++t) {
-    mNZ[t] = 0;
-    mVan[t] = ~0ull;
-  }
+  for (int t = 0; t < VI; ++t) mVan[t] = ~0ull;
 #pragma unroll
   for (int q = 0; q < VO; ++q) {
     mRI[q] = ~0ull;
     mDL[q] = ~0ull;
 #pragma unroll
-    for (int t = 0; t < VI; ++t) {
-      mLe1[q][t] = ~0ull;
-      mNe1[q][t] = 0;
-      mLe2[t][q] = ~0ull;
-    }
+    for (int t = 0; t < VI; ++t) mLe2[t][q] = ~0ull;
   }
-  const unsigned iters = (unsigned)((A + LPS - 1) / LPS);
-  for (unsigned m = 0; m < iters; ++m) {  // uniform trip count: absent actors read as zeros
-    const unsigned long long a = gq + (unsigned long long)LPS * m;
-    const bool on = a < A;
-    const u64 e2 = on ? stp[a] : 0;
-    const u64 co = on ? stp[(1 + VI) * A + a] : 0;
-    const u64 ea = on ? me[a] : 0;
-    const u64 ca = on ? mcs[a] : 0;
+  const unsigned iters = (A + LPS - 1) / LPS;
+  for (unsigned m = 0; m < iters; ++m) {  // uniform trip count
+    const unsigned a0 = gq + LPS * m;
+    const u64 off = __ballot(a0 >= A);  // lanes past the last actor: neutral in every test
+    const unsigned a = a0 < A ? a0 : A - 1;
+    const u64 e2 = stp[a];
+    const u64 co = stp[(1 + VI) * A + a];
+    const u64 ea = me[a];
+    const u64 ca = mcs[a];
     u64 c2[VI], sq[VO];
 #pragma unroll
-    for (int t = 0; t < VI; ++t) c2[t] = on ? stp[(1 + t) * A + a] : 0;
+    for (int t = 0; t < VI; ++t) c2[t] = stp[(1 + t) * A + a];
 #pragma unroll
-    for (int q = 0; q < VO; ++q) sq[q] = (on && (vm & (1u << q))) ? mc[q * A + a] : 0;
-    mP2 |= __ballot(e2 != 0);
-    mT &= __ballot(e2 <= ea || e2 <= ca);
-    mB &= __ballot(ea == 0 || ea == e2 || ea > co);
-    mB2 &= __ballot(ea == 0 || ea > co);
-    mCs &= __ballot(e2 <= ca);
+    for (int q = 0; q < VO; ++q) sq[q] = mc[q * A + a];
+    mP2 |= __ballot(e2 != 0) & ~off;
+    mE &= __ballot((e2 <= ea || e2 <= ca) && (ea == 0 || ea == e2 || ea > co)) | off;
+    mO &= __ballot(ea == 0 || ea > co) | off;
+    mCs &= __ballot(e2 <= ca) | off;
     const u64 ri = co > ea ? co : 0;
     const u64 dl = e2 > ea ? e2 : 0;
 #pragma unroll
-    for (int t = 0; t < VI; ++t) {
-      mNZ[t] |= __ballot(c2[t] != 0);
-      mVan[t] &= __ballot(c2[t] <= dl);
-    }
+    for (int t = 0; t < VI; ++t) mVan[t] &= __ballot(c2[t] <= dl) | off;
 #pragma unroll
     for (int q = 0; q < VO; ++q) {
       if (vm & (1u << q)) {
-        mRI[q] &= __ballot(sq[q] == 0 || sq[q] > ri);
-        mDL[q] &= __ballot(sq[q] == 0 || sq[q] > dl);
+        mRI[q] &= __ballot(sq[q] == 0 || sq[q] > ri) | off;
+        mDL[q] &= __ballot(sq[q] == 0 || sq[q] > dl) | off;
 #pragma unroll
-        for (int t = 0; t < VI; ++t) {
-          mLe1[q][t] &= __ballot(sq[q] <= c2[t]);
-          mNe1[q][t] |= __ballot(sq[q] != c2[t]);
-          mLe2[t][q] &= __ballot(c2[t] <= sq[q]);
-        }
+        for (int t = 0; t < VI; ++t) mLe2[t][q] &= __ballot(c2[t] <= sq[q]) | off;
       }
     }
   }
   const u64 G1 = grp_mask<LPS>();
   const u64 P2 = orN<LPS>(mP2);
-  u64 NZ[VI];
-#pragma unroll
-  for (int t = 0; t < VI; ++t) NZ[t] = orN<LPS>(mNZ[t]);
-  u64 mvbad = 0, riok = G1;
+  u64 both = P2 & andN<LPS>(mE), only = ~P2 & andN<LPS>(mO);
 #pragma unroll
   for (int q = 0; q < VO; ++q) {
     if (vm & (1u << q)) {
-      riok &= andN<LPS>(mRI[q]);
-      mvbad |= ~andN<LPS>(mDL[q]);  // an own value clock changed by forget(deleted)
-#pragma unroll
-      for (int t = 0; t < VI; ++t) mvbad |= andN<LPS>(mLe1[q][t]) & orN<LPS>(mNe1[q][t]) & NZ[t];  // dropped
+      only &= andN<LPS>(mRI[q]);
+      both &= andN<LPS>(mDL[q]);
     }
   }
 #pragma unroll
@@ -427,11 +412,21 @@ __device__ __forceinline__ u64 map_noop_steps(const u64 *buf, unsigned long long
 #pragma unroll
     for (int q = 0; q < VO; ++q)
       if (vm & (1u << q)) cov |= andN<LPS>(mLe2[t][q]);
-    mvbad |= NZ[t] & ~cov;  // an incoming value kept
+    both &= cov;
   }
-  const u64 both = P2 & andN<LPS>(mT) & andN<LPS>(mB) & ~mvbad;
-  const u64 only_acc = ~P2 & andN<LPS>(mB2) & riok;
-  return (present ? (both | only_acc) : (~P2 | andN<LPS>(mCs))) & G1;
+  return (present ? (both | only) : (~P2 | andN<LPS>(mCs))) & G1;
+}
+
+// Own values pairwise not strictly ordered (precondition (a) of the scan).
+template <int APL, int VO>
+__device__ __forceinline__ bool mv_antichain(const MVState<APL, VO> &s) {
+  bool ok = true;
+#pragma unroll
+  for (int q = 0; q < VO; ++q)
+#pragma unroll
+    for (int q2 = 0; q2 < VO; ++q2)
+      if (q != q2 && (s.vm & (1u << q)) && (s.vm & (1u << q2)) && vlt(s.c[q], s.c[q2])) ok = false;
+  return ok;
 }
 
 template <int APL, int VI, int VO, int CM, int NB, bool GL>
@@ -527,6 +522,7 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan p) {
   unsigned next_row = (!direct && nl > 0) ? lrow[0] : 0xffffffffu;
   const unsigned long long nch = (R + C - 1) / C;
   int cool = 0;
+  bool anti = true;  // own values an antichain (scan precondition), refreshed after exact steps
 #ifdef MAP_STATS
   unsigned st_exact = 0, st_scan = 0, st_fail = 0, st_nq = 0, st_pres = 0;
 #endif
@@ -579,13 +575,13 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan p) {
     unsigned long long s = 0;
 #pragma unroll 1
     while (s < n) {
-      if (kSpec && cool == 0 && !slow && !direct) {
+      if (kSpec && cool == 0 && anti && !slow && !direct) {
         // steps s.. that provably change nothing, up to the next remove naming this key
         const unsigned long long lim0 = next_row < i0 + n ? next_row - i0 : n;
         const unsigned long long lim = lim0 > s ? lim0 : s;
         unsigned long long j = s;
         if (lim > s) {
-          const u64 noop = map_noop_steps<VI, VO, LPS>(buf, W, A, mirror, mirror + A,
+          const u64 noop = map_noop_steps<VI, VO, LPS>(buf, (unsigned)W, (unsigned)A, mirror, mirror + A,
                                                         mirror + (1 + VO) * A, mv.vm, present,
                                                         (unsigned)n, lane);
           const u64 from = (s >= NS) ? 0 : (~0ull << (LPS * s));
@@ -815,6 +811,7 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan p) {
       for (int j = 0; j < APL; ++j) cs[j] = cs[j] > in.co[j] ? cs[j] : in.co[j];
 
       if (kSpec) {  // refresh the state mirror for the next scan
+        anti = mv_antichain(mv);
         if ((unsigned long long)lane < A) {
           mirror[lane] = e[0];
           mirror[(1 + VO) * A + lane] = cs[0];
