@@ -41,6 +41,7 @@ struct Tune {
   int map_glds = 1;    // Map fold: LDS-DMA staging where the shape allows it
   int map_chunk = 16;  // ... replicas per LDS chunk slot (8 or 16)
   int map_ring = 2;    // ... chunk slots in the ring (2-4)
+  int map_spec = 1;    // ... speculative no-op scan
 };
 
 struct PendingTiming {

@@ -204,6 +204,7 @@ static void apply_tune(crdt_ctx *ctx, const char *t) {
       else if (k == "mglds") ctx->tune.map_glds = v != 0;
       else if (k == "mchunk" && (v == 8 || v == 16)) ctx->tune.map_chunk = v;
       else if (k == "mring" && v >= 2 && v <= 4) ctx->tune.map_ring = v;
+      else if (k == "mspec") ctx->tune.map_spec = v != 0;
     }
     pos = end + 1;
   }

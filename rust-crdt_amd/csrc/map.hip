@@ -50,6 +50,7 @@ struct MapPlan {
   u64 *o_clock, *o_ec, *o_vclk, *o_vval;
   unsigned *o_nval;
   unsigned *o_flags;  // per group: bit0 > Vout values, bit1 bad def_row, bit2 state capacity
+  int spec;           // speculative no-op scan on (tuning / diagnosis knob; results are identical)
 };
 
 constexpr int kMapQ = 4;    // deferred removes tracked per key in registers before the slow path
@@ -234,6 +235,12 @@ __device__ __forceinline__ void map_chunk_store(const MapChunk<APL, VI, CM> &r, 
   }
 }
 
+// LDS stride of a staged step image: W words padded to 4 (mod 32), so the steps the scan reads
+// side by side start 8 banks apart instead of on the same bank.
+__host__ __device__ __forceinline__ unsigned long long map_ws(unsigned long long W) {
+  return W + (36 - W % 32) % 32;
+}
+
 __device__ __forceinline__ void glds16(const void *g, u64 *lds) {
   __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void *)lds, 16, 0, 0);
 }
@@ -241,30 +248,57 @@ __device__ __forceinline__ void glds4(const void *g, u64 *lds) {
   __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void *)lds, 4, 0, 0);
 }
 
+// Per-lane source of the LDS-DMA pieces: piece j of a step image covers image words
+// [j*128, j*128+128); lane l moves words o = j*128 + 2l, 2l+1 of replica i from
+// src0[j] + i * stride[j] bytes (entry clock, value clock or replica clock row).  Computed once.
+template <int NI>
+struct GldsLanes {
+  const char *src0[NI];
+  unsigned long long stride[NI];
+  bool on[NI];
+};
+
+template <int VI, int NI>
+__device__ __forceinline__ GldsLanes<NI> glds_lanes(const MapPlan &p, unsigned long long g, unsigned long long k,
+                                                    int lane) {
+  GldsLanes<NI> L;
+  const unsigned long long A = p.A, W = (2 + VI) * A;
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const unsigned long long o = (unsigned long long)(j * 64 + lane) * 2;
+    L.on[j] = o < W;
+    const u64 *b;
+    long long st;
+    if (o < A) {
+      b = p.ec + g * p.e_gs + k * A + o;
+      st = p.e_rs;
+    } else if (o < (1 + VI) * A) {
+      b = p.vclk + g * p.vc_gs + k * VI * A + (o - A);
+      st = p.vc_rs;
+    } else {
+      b = p.clock + g * p.c_gs + (o < W ? o - (1 + VI) * A : 0);
+      st = p.c_rs;
+    }
+    L.src0[j] = reinterpret_cast<const char *>(b);
+    L.stride[j] = (unsigned long long)st * 8;
+  }
+  return L;
+}
+
 // DMA one chunk (steps i0 .. i0+C-1, clamped to iend-1: past the end a slot holds copies that
 // are never read) into an LDS slot.  Exactly C*NI + 1 global_load_lds per call, each with at
 // least one active lane (NI = ceil(W / 128) 1-KiB pieces per step image; the values of all C
 // steps in one 4-byte-per-lane piece), so a fixed vmcnt count retires a chunk.
 template <int VI, int C, int NI>
-__device__ __forceinline__ void map_chunk_glds(const MapPlan &p, unsigned long long g, unsigned long long k,
-                                               unsigned long long i0, unsigned long long iend, u64 *img,
-                                               u64 *vals, int lane) {
-  const unsigned long long A = p.A, W = (2 + VI) * A;
-  const u64 *ecb = p.ec + g * p.e_gs + k * A;
-  const u64 *vcb = p.vclk + g * p.vc_gs + k * VI * A;
-  const u64 *clb = p.clock + g * p.c_gs;
+__device__ __forceinline__ void map_chunk_glds(const MapPlan &p, const GldsLanes<NI> &L, unsigned long long g,
+                                               unsigned long long k, unsigned long long i0, unsigned long long iend,
+                                               u64 *img, unsigned long long WS, u64 *vals, int lane) {
 #pragma unroll
   for (int s = 0; s < C; ++s) {
     const unsigned long long i = i0 + s < iend ? i0 + s : iend - 1;
 #pragma unroll
-    for (int j = 0; j < NI; ++j) {
-      const unsigned long long o = (unsigned long long)(j * 64 + lane) * 2;  // word offset in the image
-      if (o < W) {
-        const u64 *src = o < A ? ecb + i * p.e_rs + o
-                               : (o < (1 + VI) * A ? vcb + i * p.vc_rs + (o - A) : clb + i * p.c_rs + (o - (1 + VI) * A));
-        glds16(src, img + s * W + j * 128);
-      }
-    }
+    for (int j = 0; j < NI; ++j)
+      if (L.on[j]) glds16(L.src0[j] + i * L.stride[j], img + s * WS + j * 128);
   }
   const int sv = lane / (2 * VI), dw = lane % (2 * VI);
   if (sv < C) {
@@ -346,19 +380,19 @@ __device__ __forceinline__ u64 orN(u64 m) {
   return m & grp_mask<LPS>();
 }
 
-template <int VI, int VO, int LPS>
+template <int VI, int NQ, int LPS, bool RAGGED, bool PRESENT>
 __device__ __forceinline__ u64 map_noop_steps(const u64 *buf, unsigned W, unsigned A, const u64 *me,
-                                              const u64 *mc, const u64 *mcs, unsigned vm, bool present,
-                                              unsigned n, int lane) {
+                                              const u64 *mc, const u64 *mcs, unsigned n, int lane) {
+  // NQ = the number of own values, compacted into mirror slots 0..NQ-1 (PRESENT only)
   const unsigned st = (unsigned)lane / LPS;
   const unsigned gq = (unsigned)lane % LPS;
   const u64 *stp = buf + (st < n ? st : n - 1) * W;
   u64 mP2 = 0, mE = ~0ull, mO = ~0ull, mCs = ~0ull;
-  u64 mRI[VO], mDL[VO], mLe2[VI][VO], mVan[VI];
+  u64 mRI[NQ > 0 ? NQ : 1], mDL[NQ > 0 ? NQ : 1], mLe2[VI][NQ > 0 ? NQ : 1], mVan[VI];
 #pragma unroll
   for (int t = 0; t < VI; ++t) mVan[t] = ~0ull;
 #pragma unroll
-  for (int q = 0; q < VO; ++q) {
+  for (int q = 0; q < NQ; ++q) {
     mRI[q] = ~0ull;
     mDL[q] = ~0ull;
 #pragma unroll
@@ -367,30 +401,34 @@ __device__ __forceinline__ u64 map_noop_steps(const u64 *buf, unsigned W, unsign
   const unsigned iters = (A + LPS - 1) / LPS;
   for (unsigned m = 0; m < iters; ++m) {  // uniform trip count
     const unsigned a0 = gq + LPS * m;
-    const u64 off = __ballot(a0 >= A);  // lanes past the last actor: neutral in every test
-    const unsigned a = a0 < A ? a0 : A - 1;
+    // lanes past the last actor (only when LPS does not divide A): neutral in every test
+    const u64 off = RAGGED ? __ballot(a0 >= A) : 0;
+    const unsigned a = RAGGED ? (a0 < A ? a0 : A - 1) : a0;
     const u64 e2 = stp[a];
-    const u64 co = stp[(1 + VI) * A + a];
-    const u64 ea = me[a];
-    const u64 ca = mcs[a];
-    u64 c2[VI], sq[VO];
+    if constexpr (!PRESENT) {
+      const u64 ca = mcs[a];
+      mP2 |= __ballot(e2 != 0) & ~off;
+      mCs &= __ballot(e2 <= ca) | off;
+    } else {
+      const u64 co = stp[(1 + VI) * A + a];
+      const u64 ea = me[a];
+      const u64 ca = mcs[a];
+      u64 c2[VI], sq[NQ > 0 ? NQ : 1];
 #pragma unroll
-    for (int t = 0; t < VI; ++t) c2[t] = stp[(1 + t) * A + a];
+      for (int t = 0; t < VI; ++t) c2[t] = stp[(1 + t) * A + a];
 #pragma unroll
-    for (int q = 0; q < VO; ++q) sq[q] = mc[q * A + a];
-    mP2 |= __ballot(e2 != 0) & ~off;
-    mE &= __ballot((e2 <= ea || e2 <= ca) && (ea == 0 || ea == e2 || ea > co)) | off;
-    mO &= __ballot(ea == 0 || ea > co) | off;
-    mCs &= __ballot(e2 <= ca) | off;
-    const u64 ri = co > ea ? co : 0;
-    const u64 dl = e2 > ea ? e2 : 0;
+      for (int q = 0; q < NQ; ++q) sq[q] = mc[q * A + a];
+      mP2 |= __ballot(e2 != 0) & ~off;
+      mE &= __ballot(((e2 <= ea) | (e2 <= ca)) & ((ea == 0) | (ea == e2) | (ea > co))) | off;
+      mO &= __ballot((ea == 0) | (ea > co)) | off;
+      const u64 ri = co > ea ? co : 0;
+      const u64 dl = e2 > ea ? e2 : 0;
 #pragma unroll
-    for (int t = 0; t < VI; ++t) mVan[t] &= __ballot(c2[t] <= dl) | off;
+      for (int t = 0; t < VI; ++t) mVan[t] &= __ballot(c2[t] <= dl) | off;
 #pragma unroll
-    for (int q = 0; q < VO; ++q) {
-      if (vm & (1u << q)) {
-        mRI[q] &= __ballot(sq[q] == 0 || sq[q] > ri) | off;
-        mDL[q] &= __ballot(sq[q] == 0 || sq[q] > dl) | off;
+      for (int q = 0; q < NQ; ++q) {
+        mRI[q] &= __ballot(sq[q] - 1 >= ri) | off;  // sq == 0 | sq > ri (wrapping)
+        mDL[q] &= __ballot(sq[q] - 1 >= dl) | off;
 #pragma unroll
         for (int t = 0; t < VI; ++t) mLe2[t][q] &= __ballot(c2[t] <= sq[q]) | off;
       }
@@ -398,23 +436,37 @@ __device__ __forceinline__ u64 map_noop_steps(const u64 *buf, unsigned W, unsign
   }
   const u64 G1 = grp_mask<LPS>();
   const u64 P2 = orN<LPS>(mP2);
+  if constexpr (!PRESENT) return (~P2 | andN<LPS>(mCs)) & G1;
   u64 both = P2 & andN<LPS>(mE), only = ~P2 & andN<LPS>(mO);
 #pragma unroll
-  for (int q = 0; q < VO; ++q) {
-    if (vm & (1u << q)) {
-      only &= andN<LPS>(mRI[q]);
-      both &= andN<LPS>(mDL[q]);
-    }
+  for (int q = 0; q < NQ; ++q) {
+    only &= andN<LPS>(mRI[q]);
+    both &= andN<LPS>(mDL[q]);
   }
 #pragma unroll
   for (int t = 0; t < VI; ++t) {
     u64 cov = andN<LPS>(mVan[t]);  // appended, then forgotten to empty
 #pragma unroll
-    for (int q = 0; q < VO; ++q)
-      if (vm & (1u << q)) cov |= andN<LPS>(mLe2[t][q]);
+    for (int q = 0; q < NQ; ++q) cov |= andN<LPS>(mLe2[t][q]);
     both &= cov;
   }
-  return (present ? (both | only) : (~P2 | andN<LPS>(mCs))) & G1;
+  return (both | only) & G1;
+}
+
+// Dispatch on (present, number of own values, ragged actor tail); more than NQMAX own values:
+// no scan (returns 0 = no step provably a no-op).
+template <int VI, int LPS, bool RAGGED>
+__device__ __forceinline__ u64 map_noop_dispatch(const u64 *buf, unsigned W, unsigned A, const u64 *mirror,
+                                                 unsigned VO, bool present, int nv, unsigned n, int lane) {
+  const u64 *me = mirror, *mc = mirror + A, *mcs = mirror + (1 + VO) * A;
+  if (!present) return map_noop_steps<VI, 0, LPS, RAGGED, false>(buf, W, A, me, mc, mcs, n, lane);
+  switch (nv) {
+    case 0: return map_noop_steps<VI, 0, LPS, RAGGED, true>(buf, W, A, me, mc, mcs, n, lane);
+    case 1: return map_noop_steps<VI, 1, LPS, RAGGED, true>(buf, W, A, me, mc, mcs, n, lane);
+    case 2: return map_noop_steps<VI, 2, LPS, RAGGED, true>(buf, W, A, me, mc, mcs, n, lane);
+    case 3: return map_noop_steps<VI, 3, LPS, RAGGED, true>(buf, W, A, me, mc, mcs, n, lane);
+    default: return 0;
+  }
 }
 
 // Own values pairwise not strictly ordered (precondition (a) of the scan).
@@ -478,10 +530,11 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan p) {
   constexpr int LPS = 64 / NS;
   const unsigned long long A = p.A;
   const unsigned long long W = (2 + VI) * A;
-  // LDS: NB image slots (C*W words each), NB value slots (C*VI), the per-key remove list, the
+  const unsigned long long WS = map_ws(W);  // padded step stride in the ring
+  // LDS: NB image slots (C*WS words each), NB value slots (C*VI), the per-key remove list, the
   // fold-state mirror.  (Addresses are always computed from map_lds: a pointer table would hide
   // the LDS address space and turn every access into a flat op.)
-  u64 *const vbase = map_lds + NB * C * W;
+  u64 *const vbase = map_lds + NB * C * WS;
   unsigned *lrow = reinterpret_cast<unsigned *>(vbase + NB * C * VI);
   unsigned *lidx = lrow + kMapL;
   // fold-state mirror read by the speculative scan: entry clock, VO value clocks, acc clock
@@ -525,36 +578,49 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan p) {
   bool anti = true;  // own values an antichain (scan precondition), refreshed after exact steps
 #ifdef MAP_STATS
   unsigned st_exact = 0, st_scan = 0, st_fail = 0, st_nq = 0, st_pres = 0;
+  u64 cy_issue = 0, cy_wait = 0, cy_scan = 0, cy_skip = 0, cy_exact = 0, cy_t0 = 0, cy_all = __builtin_amdgcn_s_memtime();
+#define MAP_TICK() (cy_t0 = __builtin_amdgcn_s_memtime())
+#define MAP_TOCK(acc) (acc += __builtin_amdgcn_s_memtime() - cy_t0)
+#else
+#define MAP_TICK() ((void)0)
+#define MAP_TOCK(acc) ((void)0)
 #endif
   // chunk staging
   MapChunk<APL, VI, (GL ? 2 : CM)> regs;
   const int ni = GL ? (int)((W + 127) / 128) : 0;  // 1-KiB pieces per step image (GL: 1 or 2)
+  GldsLanes<1> gl1;
+  GldsLanes<2> gl2;
   if constexpr (GL) {
+    if (ni == 1) gl1 = glds_lanes<VI, 1>(p, g, k, lane);
+    else gl2 = glds_lanes<VI, 2>(p, g, k, lane);
     for (unsigned long long c = 0; c + 1 < NB && c < nch; ++c) {
-      if (ni == 1) map_chunk_glds<VI, C, 1>(p, g, k, c * C, R, map_lds + c * C * W, vbase + c * C * VI, lane);
-      else map_chunk_glds<VI, C, 2>(p, g, k, c * C, R, map_lds + c * C * W, vbase + c * C * VI, lane);
+      if (ni == 1) map_chunk_glds<VI, C, 1>(p, gl1, g, k, c * C, R, map_lds + c * C * WS, WS, vbase + c * C * VI, lane);
+      else map_chunk_glds<VI, C, 2>(p, gl2, g, k, c * C, R, map_lds + c * C * WS, WS, vbase + c * C * VI, lane);
     }
   } else {
     if (nch > 0) {
       map_chunk_load(regs, p, g, k, 0, R, lane);
-      map_chunk_store(regs, map_lds, vbase, A, W, R < (unsigned long long)C ? R : C, lane);
+      map_chunk_store(regs, map_lds, vbase, A, WS, R < (unsigned long long)C ? R : C, lane);
       if (nch > 1) map_chunk_load(regs, p, g, k, C, R, lane);
     }
   }
 
   for (unsigned long long ch = 0; ch < nch; ++ch) {
     const unsigned slot = (unsigned)(ch % NB);
-    const u64 *buf = map_lds + slot * C * W;
+    const u64 *buf = map_lds + slot * C * WS;
     const u64 *vb = vbase + slot * C * VI;
     if constexpr (GL) {
       // issue chunk ch+NB-1 into the slot chunk ch-1 used, then wait for chunk ch
       const unsigned long long nx = ch + NB - 1;
+      MAP_TICK();
       if (nx < nch) {
         const unsigned ns = (unsigned)(nx % NB);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot's last LDS reads are done
-        if (ni == 1) map_chunk_glds<VI, C, 1>(p, g, k, nx * C, R, map_lds + ns * C * W, vbase + ns * C * VI, lane);
-        else map_chunk_glds<VI, C, 2>(p, g, k, nx * C, R, map_lds + ns * C * W, vbase + ns * C * VI, lane);
+        if (ni == 1) map_chunk_glds<VI, C, 1>(p, gl1, g, k, nx * C, R, map_lds + ns * C * WS, WS, vbase + ns * C * VI, lane);
+        else map_chunk_glds<VI, C, 2>(p, gl2, g, k, nx * C, R, map_lds + ns * C * WS, WS, vbase + ns * C * VI, lane);
       }
+      MAP_TOCK(cy_issue);
+      MAP_TICK();
       const unsigned long long after = (nch - 1 - ch) < (unsigned long long)(NB - 1) ? nch - 1 - ch : NB - 1;
       if (ni == 1) {
         constexpr int P1 = C + 1;
@@ -569,31 +635,47 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan p) {
         else if (NB > 2 && after == 2) wait_vmcnt<(NB > 2 ? 2 * P2 : 0)>();
         else wait_vmcnt<(NB > 3 ? 3 * P2 : 0)>();
       }
+      MAP_TOCK(cy_wait);
     }
     const unsigned long long i0 = ch * C;
     const unsigned long long n = R - i0 < (unsigned long long)C ? R - i0 : C;
     unsigned long long s = 0;
 #pragma unroll 1
     while (s < n) {
-      if (kSpec && cool == 0 && anti && !slow && !direct) {
+      if (kSpec && p.spec && cool == 0 && anti && !slow && !direct) {
         // steps s.. that provably change nothing, up to the next remove naming this key
         const unsigned long long lim0 = next_row < i0 + n ? next_row - i0 : n;
         const unsigned long long lim = lim0 > s ? lim0 : s;
         unsigned long long j = s;
         if (lim > s) {
-          const u64 noop = map_noop_steps<VI, VO, LPS>(buf, (unsigned)W, (unsigned)A, mirror, mirror + A,
-                                                        mirror + (1 + VO) * A, mv.vm, present,
-                                                        (unsigned)n, lane);
+          MAP_TICK();
+          const int nv = __builtin_popcount(__builtin_amdgcn_readfirstlane(mv.vm));
+          const u64 noop =
+              A % LPS == 0
+                  ? map_noop_dispatch<VI, LPS, false>(buf, (unsigned)WS, (unsigned)A, mirror, VO, present, nv,
+                                                      (unsigned)n, lane)
+                  : map_noop_dispatch<VI, LPS, true>(buf, (unsigned)WS, (unsigned)A, mirror, VO, present, nv,
+                                                     (unsigned)n, lane);
           const u64 from = (s >= NS) ? 0 : (~0ull << (LPS * s));
           const u64 upto = (lim >= NS) ? ~0ull : ((1ull << (LPS * lim)) - 1);
           const u64 stop = ~noop & grp_mask<LPS>() & from & upto;
           j = stop ? (unsigned long long)(__builtin_ctzll(stop) / LPS) : lim;
-          for (unsigned long long u = s; u < j; ++u) {  // acc.clock.merge of the skipped replicas
-            const unsigned long long a = lane;
-            const u64 co = a < A ? buf[u * W + (1 + VI) * A + a] : 0;
-            cs[0] = cs[0] > co ? cs[0] : co;
+          MAP_TOCK(cy_scan);
+          MAP_TICK();
+          {  // acc.clock.merge of the skipped replicas: every read issued at once, range masked
+            const unsigned long long a = (unsigned long long)lane < A ? lane : A - 1;
+            u64 mx = cs[0];
+#pragma unroll
+            for (int u = 0; u < C; ++u) {
+              const u64 co = buf[u * WS + (1 + VI) * A + a];
+              const u64 take = ((unsigned long long)u >= s && (unsigned long long)u < j) ? ~0ull : 0ull;
+              const u64 x = co & take;
+              mx = mx > x ? mx : x;
+            }
+            if ((unsigned long long)lane < A) cs[0] = mx;
           }
           if (j > s && (unsigned long long)lane < A) mirror[(1 + VO) * A + lane] = cs[0];
+          MAP_TOCK(cy_skip);
           if (j == s) cool = 4;  // the scan found nothing to skip: run a few exact steps first
 #ifdef MAP_STATS
           ++st_scan; if (j == s) ++st_fail;
@@ -606,8 +688,9 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan p) {
 #ifdef MAP_STATS
       ++st_exact; if (nq) ++st_nq; if (present) ++st_pres;
 #endif
+      MAP_TICK();
       const unsigned long long i = i0 + s;
-      const MapStep<APL, VI> in = map_step_read<APL, VI>(buf + s * W, vb + s * VI, A, lane);
+      const MapStep<APL, VI> in = map_step_read<APL, VI>(buf + s * WS, vb + s * VI, A, lane);
       ++s;
       // ---- 1. entry join (map.rs:142-210) ----
       const bool p2 = any_nz(in.e);
@@ -815,16 +898,19 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan p) {
         if ((unsigned long long)lane < A) {
           mirror[lane] = e[0];
           mirror[(1 + VO) * A + lane] = cs[0];
+          int r = 0;  // own value clocks compacted into slots 0..nv-1 (any order)
 #pragma unroll
-          for (int q = 0; q < VO; ++q) mirror[(1 + q) * A + lane] = mv.c[q][0];
+          for (int q = 0; q < VO; ++q)
+            if (mv.vm & (1u << q)) mirror[(1 + r++) * A + lane] = mv.c[q][0];
         }
       }
+      MAP_TOCK(cy_exact);
     }
     if constexpr (!GL) {
       if (ch + 1 < nch) {  // stage the next chunk (its loads were issued a whole chunk ago)
         const unsigned long long nn = R - (ch + 1) * C < (unsigned long long)C ? R - (ch + 1) * C : C;
         const unsigned ns = (unsigned)((ch + 1) % NB);
-        map_chunk_store(regs, map_lds + ns * C * W, vbase + ns * C * VI, A, W, nn, lane);
+        map_chunk_store(regs, map_lds + ns * C * WS, vbase + ns * C * VI, A, WS, nn, lane);
         if (ch + 2 < nch) map_chunk_load(regs, p, g, k, (ch + 2) * C, R, lane);
       }
     }
@@ -832,7 +918,10 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan p) {
   if (direct && dp < dend) bad = 1;  // a row >= R was never reached
 
 #ifdef MAP_STATS
-  if (lane == 0 && (k % 97) == 0) printf("k=%llu exact=%u scan=%u fail=%u nq=%u pres=%u nl=%llu\n", k, st_exact, st_scan, st_fail, st_nq, st_pres, nl);
+  cy_all = __builtin_amdgcn_s_memtime() - cy_all;
+  if (lane == 0 && (k % 97) == 0)
+    printf("k=%llu exact=%u scan=%u fail=%u nq=%u pres=%u nl=%llu | cyc all=%llu issue=%llu wait=%llu scan=%llu skip=%llu exact=%llu\n",
+           k, st_exact, st_scan, st_fail, st_nq, st_pres, nl, cy_all, cy_issue, cy_wait, cy_scan, cy_skip, cy_exact);
 #endif
   // ---- egress: slots in Vec order (ascending order key) ----
   const int nv = __builtin_popcount(mv.vm);
@@ -887,7 +976,7 @@ template <int APL, int VI, int VO, int CM, int NB, bool GL>
 static hipError_t launch_map(const MapPlan &p, unsigned long long blocks, hipStream_t s) {
   constexpr int C = GL ? CM : MapChunk<APL, VI, CM>::C;
   const size_t W = (2 + VI) * p.A;
-  const size_t lds = (size_t)NB * C * (W + VI) * sizeof(u64) + kMapL * 2 * sizeof(unsigned) +
+  const size_t lds = (size_t)NB * C * (map_ws(W) + VI) * sizeof(u64) + kMapL * 2 * sizeof(unsigned) +
                      (2 + VO) * p.A * sizeof(u64);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   if (lds > 64 * 1024) {  // beyond the default dynamic-LDS limit (gfx950 has 160 KB per CU)
@@ -977,6 +1066,7 @@ extern "C" int crdt_map_lub_many(crdt_ctx *ctx, const crdt_map_batch *in, crdt_m
   p.o_vval = (u64 *)out->vval;
   p.o_nval = out->nval;
   p.o_flags = out->flags;
+  p.spec = ctx->tune.map_spec;
   if (int rc = device_fill(ctx, out->flags, G * sizeof(unsigned), 0)) return rc;
   if (D > 0) {
     // the kernel walks def_off on the device: stage it (the caller's array may be freed)
