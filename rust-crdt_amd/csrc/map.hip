@@ -64,8 +64,13 @@ struct MapStep {
   u64 v[VI];
 };
 
-__device__ __forceinline__ bool wall(bool x) { return __all(x); }
-__device__ __forceinline__ bool wany(bool x) { return __any(x); }
+// Wave votes as ballots: the results are provably uniform (scalar registers), so the control
+// flow built on them stays scalar — no EXEC-masked regions, no divergent loops whose live-outs
+// the compiler would have to move to vector registers.
+__device__ __forceinline__ bool wall(bool x) { return __ballot(!x) == 0; }
+// A wave-uniform condition the compiler cannot prove uniform: make it so.
+__device__ __forceinline__ bool uni(bool x) { return __builtin_amdgcn_readfirstlane((int)x) != 0; }
+__device__ __forceinline__ bool wany(bool x) { return __ballot(x) != 0; }
 
 template <int APL>
 __device__ __forceinline__ bool all_ge(const u64 (&x)[APL], const u64 (&y)[APL]) {
@@ -380,7 +385,7 @@ __device__ __forceinline__ u64 orN(u64 m) {
   return m & grp_mask<LPS>();
 }
 
-template <int VI, int NQ, int LPS, bool RAGGED, bool PRESENT>
+template <int VI, int NQ, int LPS, int IT, bool PRESENT>
 __device__ __forceinline__ u64 map_noop_steps(const u64 *buf, unsigned W, unsigned A, const u64 *me,
                                               const u64 *mc, const u64 *mcs, unsigned n, int lane) {
   // NQ = the number of own values, compacted into mirror slots 0..NQ-1 (PRESENT only)
@@ -398,13 +403,15 @@ __device__ __forceinline__ u64 map_noop_steps(const u64 *buf, unsigned W, unsign
 #pragma unroll
     for (int t = 0; t < VI; ++t) mLe2[t][q] = ~0ull;
   }
-  const unsigned iters = (A + LPS - 1) / LPS;
-  for (unsigned m = 0; m < iters; ++m) {  // uniform trip count
+  // IT >= ceil(A / LPS) iterations, fully unrolled: every LDS read of the scan can be in
+  // flight at once.  Lanes past the last actor read actor A-1 and are neutral in every test.
+#pragma unroll
+  for (unsigned m = 0; m < IT; ++m) {
     const unsigned a0 = gq + LPS * m;
-    // lanes past the last actor (only when LPS does not divide A): neutral in every test
-    const u64 off = RAGGED ? __ballot(a0 >= A) : 0;
-    const unsigned a = RAGGED ? (a0 < A ? a0 : A - 1) : a0;
+    const u64 off = __ballot(a0 >= A);
+    const unsigned a = a0 < A ? a0 : A - 1;
     const u64 e2 = stp[a];
+    // one vector compare per test, combined on the (scalar) ballot masks
     if constexpr (!PRESENT) {
       const u64 ca = mcs[a];
       mP2 |= __ballot(e2 != 0) & ~off;
@@ -413,22 +420,27 @@ __device__ __forceinline__ u64 map_noop_steps(const u64 *buf, unsigned W, unsign
       const u64 co = stp[(1 + VI) * A + a];
       const u64 ea = me[a];
       const u64 ca = mcs[a];
-      u64 c2[VI], sq[NQ > 0 ? NQ : 1];
+      u64 c2[VI], sq[NQ > 0 ? NQ : 1], sq1[NQ > 0 ? NQ : 1];
 #pragma unroll
       for (int t = 0; t < VI; ++t) c2[t] = stp[(1 + t) * A + a];
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) sq[q] = mc[q * A + a];
+      for (int q = 0; q < NQ; ++q) {
+        sq[q] = mc[q * A + a];
+        sq1[q] = sq[q] - 1;  // x - 1 >= y <=> x == 0 | x > y (wrapping)
+      }
+      const u64 eGtCo = __ballot(ea - 1 >= co);  // ea == 0 | ea > co
+      const u64 coGtE = __ballot(co > ea);       // ri = coGtE ? co : 0
+      const u64 e2GtE = __ballot(e2 > ea);       // deleted = e2GtE ? e2 : 0
       mP2 |= __ballot(e2 != 0) & ~off;
-      mE &= __ballot(((e2 <= ea) | (e2 <= ca)) & ((ea == 0) | (ea == e2) | (ea > co))) | off;
-      mO &= __ballot((ea == 0) | (ea > co)) | off;
-      const u64 ri = co > ea ? co : 0;
-      const u64 dl = e2 > ea ? e2 : 0;
+      mE &= ((__ballot(e2 <= ea) | __ballot(e2 <= ca)) & (eGtCo | __ballot(ea == e2))) | off;
+      mO &= eGtCo | off;
 #pragma unroll
-      for (int t = 0; t < VI; ++t) mVan[t] &= __ballot(c2[t] <= dl) | off;
+      for (int t = 0; t < VI; ++t)  // c2 <= deleted
+        mVan[t] &= (__ballot(c2[t] <= e2) & e2GtE) | (__ballot(c2[t] == 0) & ~e2GtE) | off;
 #pragma unroll
       for (int q = 0; q < NQ; ++q) {
-        mRI[q] &= __ballot(sq[q] - 1 >= ri) | off;  // sq == 0 | sq > ri (wrapping)
-        mDL[q] &= __ballot(sq[q] - 1 >= dl) | off;
+        mRI[q] &= ~coGtE | __ballot(sq1[q] >= co) | off;  // sq == 0 | sq > ri
+        mDL[q] &= ~e2GtE | __ballot(sq1[q] >= e2) | off;  // sq == 0 | sq > deleted
 #pragma unroll
         for (int t = 0; t < VI; ++t) mLe2[t][q] &= __ballot(c2[t] <= sq[q]) | off;
       }
@@ -453,20 +465,31 @@ __device__ __forceinline__ u64 map_noop_steps(const u64 *buf, unsigned W, unsign
   return (both | only) & G1;
 }
 
-// Dispatch on (present, number of own values, ragged actor tail); more than NQMAX own values:
-// no scan (returns 0 = no step provably a no-op).
-template <int VI, int LPS, bool RAGGED>
-__device__ __forceinline__ u64 map_noop_dispatch(const u64 *buf, unsigned W, unsigned A, const u64 *mirror,
-                                                 unsigned VO, bool present, int nv, unsigned n, int lane) {
+// Dispatch on (present, number of own values); more than 3 own values: no scan (returns 0 = no
+// step provably a no-op).
+template <int VI, int LPS, int IT>
+__device__ __forceinline__ u64 map_noop_nv(const u64 *buf, unsigned W, unsigned A, const u64 *mirror,
+                                           unsigned VO, bool present, int nv, unsigned n, int lane) {
   const u64 *me = mirror, *mc = mirror + A, *mcs = mirror + (1 + VO) * A;
-  if (!present) return map_noop_steps<VI, 0, LPS, RAGGED, false>(buf, W, A, me, mc, mcs, n, lane);
+  if (!present) return map_noop_steps<VI, 0, LPS, IT, false>(buf, W, A, me, mc, mcs, n, lane);
   switch (nv) {
-    case 0: return map_noop_steps<VI, 0, LPS, RAGGED, true>(buf, W, A, me, mc, mcs, n, lane);
-    case 1: return map_noop_steps<VI, 1, LPS, RAGGED, true>(buf, W, A, me, mc, mcs, n, lane);
-    case 2: return map_noop_steps<VI, 2, LPS, RAGGED, true>(buf, W, A, me, mc, mcs, n, lane);
-    case 3: return map_noop_steps<VI, 3, LPS, RAGGED, true>(buf, W, A, me, mc, mcs, n, lane);
+    case 0: return map_noop_steps<VI, 0, LPS, IT, true>(buf, W, A, me, mc, mcs, n, lane);
+    case 1: return map_noop_steps<VI, 1, LPS, IT, true>(buf, W, A, me, mc, mcs, n, lane);
+    case 2: return map_noop_steps<VI, 2, LPS, IT, true>(buf, W, A, me, mc, mcs, n, lane);
+    case 3: return map_noop_steps<VI, 3, LPS, IT, true>(buf, W, A, me, mc, mcs, n, lane);
     default: return 0;
   }
+}
+
+// ... and on the unrolled iteration count ceil(A / LPS) (A <= 64).
+template <int VI, int LPS>
+__device__ __forceinline__ u64 map_noop_dispatch(const u64 *buf, unsigned W, unsigned A, const u64 *mirror,
+                                                 unsigned VO, bool present, int nv, unsigned n, int lane) {
+  const unsigned it = (A + LPS - 1) / LPS;
+  if (it <= 2) return map_noop_nv<VI, LPS, 2>(buf, W, A, mirror, VO, present, nv, n, lane);
+  if (it <= 4) return map_noop_nv<VI, LPS, 4>(buf, W, A, mirror, VO, present, nv, n, lane);
+  if (LPS >= 8 || it <= 8) return map_noop_nv<VI, LPS, (LPS >= 8 ? 8 : 8)>(buf, W, A, mirror, VO, present, nv, n, lane);
+  return map_noop_nv<VI, LPS, (LPS >= 8 ? 8 : 16)>(buf, W, A, mirror, VO, present, nv, n, lane);
 }
 
 // Own values pairwise not strictly ordered (precondition (a) of the scan).
@@ -568,11 +591,13 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan p) {
       }
       nl += __popcll(m);
     }
-    if (__any(badl)) bad = 1;
+    if (wany(badl)) bad = 1;
   }
   const bool direct = nl > kMapL;
   unsigned long long lp = 0;
-  unsigned next_row = (!direct && nl > 0) ? lrow[0] : 0xffffffffu;
+  // (uniform values read through LDS / global memory go through readfirstlane, so that the fold's
+  // control flow stays scalar)
+  unsigned next_row = (!direct && nl > 0) ? __builtin_amdgcn_readfirstlane(lrow[0]) : 0xffffffffu;
   const unsigned long long nch = (R + C - 1) / C;
   int cool = 0;
   bool anti = true;  // own values an antichain (scan precondition), refreshed after exact steps
@@ -642,20 +667,16 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan p) {
     unsigned long long s = 0;
 #pragma unroll 1
     while (s < n) {
-      if (kSpec && p.spec && cool == 0 && anti && !slow && !direct) {
+      if (uni(kSpec && p.spec && cool == 0 && anti && !slow && !direct)) {
         // steps s.. that provably change nothing, up to the next remove naming this key
         const unsigned long long lim0 = next_row < i0 + n ? next_row - i0 : n;
         const unsigned long long lim = lim0 > s ? lim0 : s;
         unsigned long long j = s;
-        if (lim > s) {
+        if (uni(lim > s)) {
           MAP_TICK();
           const int nv = __builtin_popcount(__builtin_amdgcn_readfirstlane(mv.vm));
-          const u64 noop =
-              A % LPS == 0
-                  ? map_noop_dispatch<VI, LPS, false>(buf, (unsigned)WS, (unsigned)A, mirror, VO, present, nv,
-                                                      (unsigned)n, lane)
-                  : map_noop_dispatch<VI, LPS, true>(buf, (unsigned)WS, (unsigned)A, mirror, VO, present, nv,
-                                                     (unsigned)n, lane);
+          const u64 noop = map_noop_dispatch<VI, LPS>(buf, (unsigned)WS, (unsigned)A, mirror, VO, present, nv,
+                                                       (unsigned)n, lane);
           const u64 from = (s >= NS) ? 0 : (~0ull << (LPS * s));
           const u64 upto = (lim >= NS) ? ~0ull : ((1ull << (LPS * lim)) - 1);
           const u64 stop = ~noop & grp_mask<LPS>() & from & upto;
@@ -819,12 +840,12 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan p) {
           unsigned long long d;
           if (!direct) {
             if (next_row > i) break;
-            d = lidx[lp];
+            d = __builtin_amdgcn_readfirstlane(lidx[lp]);
             ++lp;
-            next_row = lp < nl ? lrow[lp] : 0xffffffffu;
+            next_row = lp < nl ? __builtin_amdgcn_readfirstlane(lrow[lp]) : 0xffffffffu;
           } else {
             if (dp >= dend) break;
-            const unsigned long long row = p.def_row[dp];
+            const unsigned long long row = __builtin_amdgcn_readfirstlane(p.def_row[dp]);
             if (row > i) break;
             d = dp++;
             if (!(p.def_keys[d * p.Kw + kw] & kbit)) continue;
@@ -863,7 +884,7 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan p) {
         } else {  // more than kMapQ concurrent removes on this key: rescan every started one
           const unsigned long long nscan = direct ? dp - dbeg : lp;
           for (unsigned long long x = 0; x < nscan; ++x) {
-            const unsigned long long d = direct ? dbeg + x : lidx[x];
+            const unsigned long long d = direct ? dbeg + x : __builtin_amdgcn_readfirstlane(lidx[x]);
             if (direct && !(p.def_keys[d * p.Kw + kw] & kbit)) continue;
             u64 rm[APL];
 #pragma unroll
@@ -871,7 +892,7 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan p) {
               const unsigned long long a = lane + 64ull * j;
               rm[j] = a < p.A ? p.def_clock[d * p.A + a] : 0;
             }
-            if (p.def_row[d] == i || !all_ge(cs, rm)) {
+            if (__builtin_amdgcn_readfirstlane(p.def_row[d]) == i || !all_ge(cs, rm)) {
               have = true;
 #pragma unroll
               for (int j = 0; j < APL; ++j) ceil[j] = ceil[j] > rm[j] ? ceil[j] : rm[j];
