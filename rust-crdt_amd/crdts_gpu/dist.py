@@ -163,3 +163,66 @@ def orswot_lub_many_sharded(clock: torch.Tensor, entries: torch.Tensor, def_cloc
             off.append(off[-1] + c)
         return local(pc, pe, def_off=off, def_clock=dcl, def_members=dmem)
     return local(pc, pe)
+
+
+# ---- Map<K, MVReg> ----------------------------------------------------------------------------
+def _key_bits(bitmaps: torch.Tensor) -> torch.Tensor:
+    """(D, Kw) int64 key bitmaps -> (D, Kw*64) 0/1 int64."""
+    sh = torch.arange(64, device=bitmaps.device, dtype=torch.int64)
+    return ((bitmaps.unsqueeze(-1) >> sh) & 1).reshape(bitmaps.shape[0], -1)
+
+
+def _pack_bits(bits: torch.Tensor) -> torch.Tensor:
+    """(D, n) 0/1 int64 -> (D, ceil(n/64)) int64 bitmaps (distinct bits: the sum is the OR)."""
+    D, n = bits.shape
+    Kw = (n + 63) // 64
+    pad = torch.zeros((D, Kw * 64), dtype=torch.int64, device=bits.device)
+    pad[:, :n] = bits
+    sh = torch.arange(64, device=bits.device, dtype=torch.int64)
+    return (pad.reshape(D, Kw, 64) << sh).sum(-1)
+
+
+def restrict_key_bitmaps(bitmaps: torch.Tensor, k0: int, Kk: int) -> torch.Tensor:
+    """Key bitmaps over all keys -> bitmaps over keys [k0, k0+Kk) re-indexed from 0."""
+    return _pack_bits(_key_bits(bitmaps)[:, k0:k0 + Kk])
+
+
+def expand_key_bitmaps(bitmaps: torch.Tensor, k0: int, K: int) -> torch.Tensor:
+    """Bitmaps over local keys [0, Kk) -> bitmaps over all K keys (local key i = key k0 + i)."""
+    loc = _key_bits(bitmaps)
+    full = torch.zeros((bitmaps.shape[0], K), dtype=torch.int64, device=bitmaps.device)
+    n = min(loc.shape[1], K - k0)
+    full[:, k0:k0 + n] = loc[:, :n]
+    return _pack_bits(full)
+
+
+def map_lub_many_sharded(clock: torch.Tensor, ec: torch.Tensor, vclk: torch.Tensor, vval: torch.Tensor,
+                         k0: int, K: int, def_off=None, def_row=None, def_clock=None, def_keys=None,
+                         vout: int = 4, group=None, local=None):
+    """Key-sharded Map<K, MVReg> lub: rank k owns keys [k0, k0 + Kk) of every replica
+    (ec (G, R, Kk, A), vclk (G, R, Kk, V, A), vval (G, R, Kk, V)) and holds every replica's map
+    clock (G, R, A) and the group's whole deferred list (key bitmaps over all K keys).
+
+    Keys are independent given the replica clocks and the deferred list (csrc/map.hip header), so
+    each rank's fold of its keys is the exact left fold with no data-path collective — unlike a
+    replica split, which would need the (non-associative) re-merge.  The one
+    exchange is the surviving-remove output: the clock and the survival flags are the same on
+    every rank; each rank's key sets cover its own keys only, so a SUM all-reduce of the
+    bitmaps is their union.  Returns a MapLub whose ec / vclk / vval / nval are the rank's keys
+    and whose def_keys are over all K keys."""
+    if local is None:
+        from . import map as cmap
+        local = cmap.lub_many
+    Kk = ec.shape[-2]
+    kw = {}
+    if def_off is not None and int(def_off[-1]) > 0:
+        kw = dict(def_off=def_off, def_row=def_row, def_clock=def_clock,
+                  def_keys=restrict_key_bitmaps(def_keys, k0, Kk).contiguous())
+    res = local(clock, ec, vclk, vval, vout=vout, **kw)
+    if res.def_keys is None:
+        return res
+    gk = expand_key_bitmaps(res.def_keys, k0, K)
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    if world > 1:
+        dist.all_reduce(gk, op=dist.ReduceOp.SUM, group=group)
+    return res._replace(def_keys=gk)

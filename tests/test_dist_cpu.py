@@ -232,3 +232,93 @@ def test_orswot_sharded_world(world):
     np.testing.assert_array_equal(c.view(np.uint64)[0], oc)
     np.testing.assert_array_equal(e.view(np.uint64)[0], oe)
     assert dset == odef
+
+
+def _map_local(clock, ec, vclk, vval, vout=4, def_off=None, def_row=None, def_clock=None, def_keys=None):
+    """Oracle stand-in for crdts_gpu.map.lub_many (one group), same deferred-output convention:
+    keep[d] = d is the first surviving remove with its rm clock (survival: !(rm <= final clock),
+    map.rs:336-345), def_keys[d] = the union of the key sets of the survivors with that clock."""
+    import oracle as O
+    from crdts_gpu.map import MapLub
+    c = clock.numpy().view(np.uint64)[0]
+    e, vc, vv = (x.numpy().view(np.uint64)[0] for x in (ec, vclk, vval))
+    K = e.shape[1]
+    Kw = (K + 63) // 64
+    D = 0 if def_off is None else int(def_off[-1])
+    rows = def_row.numpy().astype(np.int64) if D else None
+    dcl = def_clock.numpy().view(np.uint64) if D else None
+    dk = def_keys.numpy().view(np.uint64) if D else None
+    oc, oe, ovc, ovv, on, _, _ = O.map_fold(c, e, vc, vv, rows, dcl, dk, vout)
+    keep = np.zeros(D, np.uint8)
+    keys = np.zeros((D, Kw), np.uint64)
+    for d in range(D):
+        if np.all(dcl[d] <= oc):
+            continue
+        first = next(d2 for d2 in range(D) if np.array_equal(dcl[d2], dcl[d]))
+        keep[first] = 1
+        keys[first] |= dk[d]
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64).copy())  # noqa: E731
+    return MapLub(t(oc[None]), t(oe[None]), t(ovc[None]), t(ovv[None]), torch.from_numpy(on[None].astype(np.int32)),
+                  torch.zeros(1, dtype=torch.int32), torch.from_numpy(keep) if D else None, t(keys) if D else None)
+
+
+def _map_data(seed):
+    import oracle as O
+    maps = O.gen_map_replicas(seed, 30, 21, 5, steps=260, p_rm=0.3, p_up=0.4)
+    return O.map_to_dense(maps, 21, 5, O.max_vals(maps))
+
+
+def _map_worker(rank, world, port, seed, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (os.path.join(here, ".."), os.path.join(here, "..", "rust-crdt_amd"), os.path.join(here, "..", "oracle"), here):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from crdts_gpu import dist as cdist
+    d = _map_data(seed)
+    K = d["ec"].shape[1]
+    k0, k1 = cdist.shard_range(K, rank, world)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64).copy())  # noqa: E731
+    D = d["def_row"].shape[0]
+    kw = dict(def_off=[0, D], def_row=torch.from_numpy(d["def_row"].astype(np.int32)),
+              def_clock=t(d["def_clock"]), def_keys=t(d["def_keys"])) if D else {}
+    res = cdist.map_lub_many_sharded(t(d["clock"][None]), t(d["ec"][None, :, k0:k1]),
+                                     t(d["vclk"][None, :, k0:k1]), t(d["vval"][None, :, k0:k1]), k0, K,
+                                     vout=8, local=_map_local, **kw)
+    q.put((rank, k0, res.clock.numpy().copy(), res.ec.numpy().copy(), res.vclk.numpy().copy(),
+           res.vval.numpy().copy(), res.nval.numpy().copy(),
+           None if res.def_keep is None else res.def_keep.numpy().copy(),
+           None if res.def_keys is None else res.def_keys.numpy().copy()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,seed", [(2, 3), (3, 4)])
+def test_map_key_sharded_world(world, seed):
+    """Key-sharded Map fold: the ranks' key ranges assemble to the oracle's whole left fold, and
+    the exchanged surviving removes equal the oracle's deferred set."""
+    import oracle as O
+    from crdts_gpu.orswot import deferred_set
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_map_worker, args=(r, world, port, seed, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    d = _map_data(seed)
+    exp = O.map_fold(d["clock"], d["ec"], d["vclk"], d["vval"], d["def_row"], d["def_clock"], d["def_keys"], 8)
+    assert d["def_row"].shape[0] > 0
+    for rank, k0, c, e, vc, vv, nv, keep, keys in outs:
+        n = e.shape[1]
+        np.testing.assert_array_equal(c.view(np.uint64)[0], exp[0])
+        np.testing.assert_array_equal(e.view(np.uint64)[0], exp[1][k0:k0 + n])
+        np.testing.assert_array_equal(vc.view(np.uint64)[0], exp[2][k0:k0 + n])
+        np.testing.assert_array_equal(vv.view(np.uint64)[0], exp[3][k0:k0 + n])
+        np.testing.assert_array_equal(nv[0], exp[4][k0:k0 + n])
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64).copy())  # noqa: E731
+        got = deferred_set(t(d["def_clock"]), torch.from_numpy(keep), torch.from_numpy(keys))
+        assert got == exp[5]
