@@ -220,6 +220,40 @@ typedef struct crdt_map_out {
 
 int crdt_map_lub_many(crdt_ctx *ctx, const crdt_map_batch *in, crdt_map_out *out);
 
+/* ---- causal helpers on dense clock rows -----------------------------------
+ * Row-pair ops over N pairs (x_i, y_i) of A-word rows (VClock, GCounter inner, or a PNCounter
+ * P‖N row with A = 2·actors):
+ *   CRDT_PAIR_GLB     out_i = x_i.glb(y_i): pointwise min, a 0 drops the actor   vclock.rs:246-259
+ *   CRDT_PAIR_FORGET  out_i = x_i.forget(y_i): keep x[a] iff x[a] > y[a]         vclock.rs:95-105
+ *                     (GCounter::forget gcounter.rs:51-53, PNCounter::forget pncounter.rs:78-81
+ *                     are the same op on their rows)
+ * `out` may alias `x` (in place, like the reference's &mut self). */
+#define CRDT_PAIR_GLB 1
+#define CRDT_PAIR_FORGET 2
+int crdt_vclock_pair_op(crdt_ctx *ctx, int op, uint64_t *out, const uint64_t *x, const uint64_t *y,
+                        size_t N, size_t A, size_t out_stride, size_t x_stride, size_t y_stride);
+
+/* VClock::partial_cmp (vclock.rs:68-80) of N row pairs: out[i] = 0 Equal, 1 Greater (x ≥ y),
+ * -1 Less, 2 None (concurrent). */
+int crdt_vclock_partial_cmp(crdt_ctx *ctx, const uint64_t *x, const uint64_t *y, size_t N, size_t A,
+                            size_t x_stride, size_t y_stride, int8_t *out);
+
+/* All-pairs partial_cmp of N clocks (the dominance / concurrency matrix): out[i*N + j] =
+ * partial_cmp(x_i, x_j) coded as above.  N <= 4,194,240. */
+int crdt_vclock_cmp_matrix(crdt_ctx *ctx, const uint64_t *x, size_t N, size_t A, size_t x_stride,
+                           int8_t *out);
+
+/* read() of N counters, exact: out[2i] + 2^64·out[2i+1] is
+ *   GCounter::read  (gcounter.rs:70-72, BigUint sum of the A counters of row i), or
+ *   PNCounter::read (pncounter.rs:110-115, BigInt P − N of row i = P[0..A) ‖ N[A..2A)) as a
+ *                   two's-complement 128-bit integer.
+ * Exact for A < 2^62 (the reference's num-bigint is unbounded; no sum of u64 counters of one
+ * row reaches 2^126). */
+int crdt_gcounter_read(crdt_ctx *ctx, const uint64_t *in, size_t N, size_t A, size_t row_stride,
+                       uint64_t *out);
+int crdt_pncounter_read(crdt_ctx *ctx, const uint64_t *in, size_t N, size_t A, size_t row_stride,
+                        uint64_t *out);
+
 /* ---- synthetic inputs (bench / test data, generated in HBM) --------------------------------
  * Counter-based and reproducible on the CPU (tests/golden/make_golden.py restates them).
  * kind 0 = clock/counter cells, 1 = GSet bitmap words, 2 = LWW markers, 3 = LWW vals.

@@ -29,6 +29,8 @@ EXPORTS = (
     "crdt_gset_lub_many", "crdt_gset_merge_batch",
     "crdt_lwwreg_lub_many", "crdt_lwwreg_merge_batch",
     "crdt_orswot_lub_many", "crdt_map_lub_many",
+    "crdt_vclock_pair_op", "crdt_vclock_partial_cmp", "crdt_vclock_cmp_matrix", "crdt_gcounter_read",
+    "crdt_pncounter_read",
     "crdt_synth_fill", "crdt_synth_orswot", "crdt_synth_orswot_rm", "crdt_synth_map",
 )
 
@@ -99,6 +101,11 @@ _SIGS = {
     "crdt_lwwreg_merge_batch": ([P, P, P, P, P, S, P], ctypes.c_int),
     "crdt_orswot_lub_many": ([P, ctypes.POINTER(OrswotBatch), ctypes.POINTER(OrswotOut)], ctypes.c_int),
     "crdt_map_lub_many": ([P, ctypes.POINTER(MapBatch), ctypes.POINTER(MapOut)], ctypes.c_int),
+    "crdt_vclock_pair_op": ([P, ctypes.c_int, P, P, P, S, S, S, S, S], ctypes.c_int),
+    "crdt_vclock_partial_cmp": ([P, P, P, S, S, S, S, P], ctypes.c_int),
+    "crdt_vclock_cmp_matrix": ([P, P, S, S, S, P], ctypes.c_int),
+    "crdt_gcounter_read": ([P, P, S, S, S, P], ctypes.c_int),
+    "crdt_pncounter_read": ([P, P, S, S, S, P], ctypes.c_int),
 }
 for _t in ("vclock", "gcounter", "pncounter", "gset"):
     _SIGS[f"crdt_{_t}_lub_many"] = ([P, P, S, S, S, S, S, P, S, ctypes.c_uint], ctypes.c_int)

@@ -22,9 +22,9 @@ def merge_batch(self_states: torch.Tensor, other_states: torch.Tensor,
     return _lattice.merge_batch("gcounter", ctx, self_states, other_states)
 
 
-def read(states: torch.Tensor) -> list:
-    """GCounter::read (gcounter.rs:70-72): exact (unbounded) sum per row, on the host."""
-    import numpy as np
-    a = states.detach().cpu().numpy().view(np.uint64)
-    rows = a.reshape(-1, a.shape[-1])
-    return [sum(int(x) for x in row) for row in rows]
+def read(states: torch.Tensor, ctx: Optional[Context] = None) -> list:
+    """GCounter::read (gcounter.rs:70-72) of every row (N, A) or of one (A,) state: the exact sum,
+    as 128-bit words on the device (crdt_gcounter_read), returned as Python ints (BigUint)."""
+    from . import causal
+    vals = causal.words_to_ints(causal.read_sums("gcounter", states, ctx), signed=False)
+    return vals[0] if states.dim() == 1 else vals

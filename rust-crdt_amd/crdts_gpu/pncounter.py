@@ -28,10 +28,10 @@ def merge_batch(self_states: torch.Tensor, other_states: torch.Tensor,
     return _lattice.merge_batch("pncounter", ctx, self_states, other_states, width_div=2)
 
 
-def read(states: torch.Tensor) -> list:
-    """PNCounter::read (pncounter.rs:110-115): exact P - N per row, on the host."""
-    import numpy as np
-    a = states.detach().cpu().numpy().view(np.uint64)
-    rows = a.reshape(-1, a.shape[-1])
-    A = rows.shape[1] // 2
-    return [sum(int(x) for x in r[:A]) - sum(int(x) for x in r[A:]) for r in rows]
+def read(states: torch.Tensor, ctx: Optional[Context] = None) -> list:
+    """PNCounter::read (pncounter.rs:110-115) of every row (N, 2A) = P ‖ N or of one (2A,) state:
+    exact P - N as 128-bit two's complement on the device (crdt_pncounter_read), returned as
+    Python ints (BigInt)."""
+    from . import causal
+    vals = causal.words_to_ints(causal.read_sums("pncounter", states, ctx), signed=True)
+    return vals[0] if states.dim() == 1 else vals

@@ -1,0 +1,268 @@
+// Batched causal helpers on dense clock rows: VClock::glb,
+// Causal::forget, VClock::partial_cmp (pairwise and all-pairs) and the GCounter / PNCounter
+// read() sums.  All are HBM-bound elementwise / row-reduction passes (the all-pairs matrix is
+// an LDS-tiled compare kernel), no MFMA.
+//
+// Reference: vclock.rs:68-80 (partial_cmp), :95-105 (forget), :246-259 (glb);
+// gcounter.rs:51-53 (forget = inner.forget), :70-72 (read); pncounter.rs:78-81 (forget),
+// :110-115 (read).  Dense convention: actor absent <=> 0 (vclock.rs:155-159 never stores 0), so
+// glb's "drop zero minima" and forget's "remove the actor" are a 0 in the dense row.
+#include "common.hpp"
+
+namespace crdt {
+
+// One wave per row pair; lanes cover the row's words, 2 per lane (16-byte loads) when every
+// row starts 16-byte aligned and A is even, else 1.
+struct PairPlan {
+  u64 *out;
+  const u64 *x, *y;
+  unsigned long long N, A, os, xs, ys;
+  int op;  // CRDT_PAIR_GLB / CRDT_PAIR_FORGET
+  int vec2;
+};
+
+__device__ __forceinline__ u64 pair_apply(int op, u64 a, u64 b) {
+  // glb: min (vclock.rs:246-259); forget: keep a iff a > b (vclock.rs:98-104: counter >= own
+  // removes the actor)
+  return op == CRDT_PAIR_GLB ? (a < b ? a : b) : (a > b ? a : 0);
+}
+
+__global__ __launch_bounds__(kBlock) void pair_op_kernel(PairPlan p) {
+  const int lane = threadIdx.x % kWave;
+  const unsigned long long w0 = (blockIdx.x * (unsigned long long)kBlock + threadIdx.x) / kWave;
+  const unsigned long long nw = (unsigned long long)gridDim.x * (kBlock / kWave);
+  for (unsigned long long r = w0; r < p.N; r += nw) {
+    const u64 *xr = p.x + r * p.xs, *yr = p.y + r * p.ys;
+    u64 *orow = p.out + r * p.os;
+    if (p.vec2) {
+      for (unsigned long long c = 2ull * lane; c < p.A; c += 2ull * kWave) {
+        const u64x2 a = *reinterpret_cast<const u64x2 *>(xr + c);
+        const u64x2 b = *reinterpret_cast<const u64x2 *>(yr + c);
+        u64x2 o;
+        o.x = pair_apply(p.op, a.x, b.x);
+        o.y = pair_apply(p.op, a.y, b.y);
+        *reinterpret_cast<u64x2 *>(orow + c) = o;
+      }
+    } else {
+      for (unsigned long long c = lane; c < p.A; c += kWave) orow[c] = pair_apply(p.op, xr[c], yr[c]);
+    }
+  }
+}
+
+// partial_cmp of row pairs: Equal 0, Greater 1, Less -1, None 2 (vclock.rs:69-80: equal first,
+// then "every counter of other <= self's" = Greater, then the mirror = Less).
+__global__ __launch_bounds__(kBlock) void pair_cmp_kernel(PairPlan p, int8_t *res) {
+  const int lane = threadIdx.x % kWave;
+  const unsigned long long w0 = (blockIdx.x * (unsigned long long)kBlock + threadIdx.x) / kWave;
+  const unsigned long long nw = (unsigned long long)gridDim.x * (kBlock / kWave);
+  for (unsigned long long r = w0; r < p.N; r += nw) {
+    const u64 *xr = p.x + r * p.xs, *yr = p.y + r * p.ys;
+    bool ge = true, le = true;
+    if (p.vec2) {
+      for (unsigned long long c = 2ull * lane; c < p.A; c += 2ull * kWave) {
+        const u64x2 a = *reinterpret_cast<const u64x2 *>(xr + c);
+        const u64x2 b = *reinterpret_cast<const u64x2 *>(yr + c);
+        ge &= (a.x >= b.x) & (a.y >= b.y);
+        le &= (a.x <= b.x) & (a.y <= b.y);
+      }
+    } else {
+      for (unsigned long long c = lane; c < p.A; c += kWave) {
+        ge &= xr[c] >= yr[c];
+        le &= xr[c] <= yr[c];
+      }
+    }
+    const bool G = __ballot(!ge) == 0, L = __ballot(!le) == 0;
+    if (lane == 0) res[r] = (int8_t)(G && L ? 0 : (G ? 1 : (L ? -1 : 2)));
+  }
+}
+
+// All-pairs partial_cmp matrix of N clocks: res[i*N + j] = partial_cmp(x_i, x_j).  A 64x64 tile
+// of pairs per workgroup; both 64-clock blocks are staged through LDS 32 actors at a time
+// (actor-major, padded), each thread owns 16 pairs (one i, 16 j) and accumulates the
+// "all >=" / "all <=" bits over the actor chunks.
+constexpr int kCmpT = 64;   // clocks per tile side
+constexpr int kCmpK = 32;   // actors per LDS stage
+__global__ __launch_bounds__(kBlock) void cmp_matrix_kernel(const u64 *x, unsigned long long N,
+                                                            unsigned long long A, unsigned long long xs,
+                                                            int8_t *res) {
+  __shared__ u64 ti[kCmpK][kCmpT + 1];
+  __shared__ u64 tj[kCmpK][kCmpT + 1];
+  const unsigned long long i0 = (unsigned long long)blockIdx.y * kCmpT;
+  const unsigned long long j0 = (unsigned long long)blockIdx.x * kCmpT;
+  const int t = threadIdx.x;
+  const int ii = t % kCmpT;          // this thread's i within the tile
+  const int jb = (t / kCmpT) * 16;   // its 16 j's
+  unsigned ge = 0xffffu, le = 0xffffu;  // bit q: pair (ii, jb + q)
+  for (unsigned long long a0 = 0; a0 < A; a0 += kCmpK) {
+    // stage: 64 clocks x 32 actors per block, 8 words per thread per block
+    for (int e = t; e < kCmpT * kCmpK; e += kBlock) {
+      const int c = e / kCmpK, k = e % kCmpK;  // consecutive threads walk one clock's actors
+      const unsigned long long a = a0 + k;
+      const unsigned long long gi = i0 + c, gj = j0 + c;
+      ti[k][c] = (gi < N && a < A) ? x[gi * xs + a] : 0;
+      tj[k][c] = (gj < N && a < A) ? x[gj * xs + a] : 0;
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int k = 0; k < kCmpK; ++k) {
+      const u64 vi = ti[k][ii];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const u64 vj = tj[k][jb + q];
+        ge &= ~((unsigned)(vi < vj) << q);
+        le &= ~((unsigned)(vi > vj) << q);
+      }
+    }
+    __syncthreads();
+  }
+  const unsigned long long gi = i0 + ii;
+  if (gi >= N) return;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const unsigned long long gj = j0 + jb + q;
+    if (gj < N) {
+      const bool G = (ge >> q) & 1, L = (le >> q) & 1;
+      res[gi * N + gj] = (int8_t)(G && L ? 0 : (G ? 1 : (L ? -1 : 2)));
+    }
+  }
+}
+
+// 128-bit exact row sums (GCounter::read, BigUint sum of u64 counters; A < 2^64 terms fit in
+// 128 bits).  PNCounter: P - N of the row's two halves as a two's-complement 128-bit integer
+// (|sum| < 2^126 for A < 2^62).  One wave per row: per-lane (lo, hi) accumulators, then a
+// butterfly reduction with carries.
+struct ReadPlan {
+  const u64 *in;
+  unsigned long long N, A, rs;
+  int pn;  // 0: GCounter (A words), 1: PNCounter (P in [0, A), N in [A, 2A))
+  u64 *out;  // [N][2] (lo, hi)
+};
+
+__device__ __forceinline__ void add128(u64 &lo, u64 &hi, u64 blo, u64 bhi) {
+  const u64 l = lo + blo;
+  hi += bhi + (l < lo ? 1 : 0);
+  lo = l;
+}
+
+__device__ __forceinline__ void wave_sum128(u64 &lo, u64 &hi) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const u64 olo = __shfl_xor(lo, off, kWave);
+    const u64 ohi = __shfl_xor(hi, off, kWave);
+    add128(lo, hi, olo, ohi);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void read_sum_kernel(ReadPlan p) {
+  const int lane = threadIdx.x % kWave;
+  const unsigned long long w0 = (blockIdx.x * (unsigned long long)kBlock + threadIdx.x) / kWave;
+  const unsigned long long nw = (unsigned long long)gridDim.x * (kBlock / kWave);
+  for (unsigned long long r = w0; r < p.N; r += nw) {
+    const u64 *row = p.in + r * p.rs;
+    u64 plo = 0, phi = 0, nlo = 0, nhi = 0;
+    for (unsigned long long c = lane; c < p.A; c += kWave) {
+      add128(plo, phi, row[c], 0);
+      if (p.pn) add128(nlo, nhi, row[p.A + c], 0);
+    }
+    wave_sum128(plo, phi);
+    if (p.pn) {
+      wave_sum128(nlo, nhi);
+      // P - N = P + ~N + 1
+      add128(plo, phi, ~nlo, ~nhi);
+      add128(plo, phi, 1, 0);
+    }
+    if (lane == 0) {
+      p.out[2 * r] = plo;
+      p.out[2 * r + 1] = phi;
+    }
+  }
+}
+
+static unsigned rows_grid(const crdt_ctx *ctx, unsigned long long N) {
+  // one wave per row, 4 waves per workgroup; enough workgroups to fill the chip 8 deep
+  const unsigned long long want = (N + 3) / 4;
+  const unsigned long long cap = (unsigned long long)ctx->cu_count * 8;
+  return (unsigned)(want < cap ? (want ? want : 1) : cap);
+}
+
+static bool al16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+}  // namespace crdt
+
+using namespace crdt;
+
+extern "C" int crdt_vclock_pair_op(crdt_ctx *ctx, int op, uint64_t *out, const uint64_t *x, const uint64_t *y,
+                                   size_t N, size_t A, size_t out_stride, size_t x_stride, size_t y_stride) {
+  CRDT_CHECK_CTX(ctx);
+  if (op != CRDT_PAIR_GLB && op != CRDT_PAIR_FORGET) return fail(ctx, CRDT_EINVAL, "vclock_pair_op: op %d", op);
+  if (N == 0 || A == 0) return CRDT_OK;
+  if (!out || !x || !y) return fail(ctx, CRDT_EINVAL, "vclock_pair_op: NULL buffer");
+  if (out_stride < A || x_stride < A || y_stride < A) return fail(ctx, CRDT_EINVAL, "vclock_pair_op: stride < A");
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  PairPlan p{(u64 *)out, (const u64 *)x, (const u64 *)y, N, A, out_stride, x_stride, y_stride, op, 0};
+  p.vec2 = (A % 2 == 0) && ((out_stride | x_stride | y_stride) % 2 == 0) && al16(out) && al16(x) && al16(y);
+  timing_begin(ctx, "pair_op");
+  hipLaunchKernelGGL(pair_op_kernel, dim3(rows_grid(ctx, N)), dim3(kBlock), 0, ctx->stream, p);
+  timing_end(ctx);
+  CRDT_HIP(ctx, hipGetLastError());
+  return CRDT_OK;
+}
+
+extern "C" int crdt_vclock_partial_cmp(crdt_ctx *ctx, const uint64_t *x, const uint64_t *y, size_t N, size_t A,
+                                       size_t x_stride, size_t y_stride, int8_t *out) {
+  CRDT_CHECK_CTX(ctx);
+  if (N == 0) return CRDT_OK;
+  if (!out || (A > 0 && (!x || !y))) return fail(ctx, CRDT_EINVAL, "vclock_partial_cmp: NULL buffer");
+  if (A > 0 && (x_stride < A || y_stride < A)) return fail(ctx, CRDT_EINVAL, "vclock_partial_cmp: stride < A");
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  PairPlan p{nullptr, (const u64 *)x, (const u64 *)y, N, A, 0, x_stride, y_stride, 0, 0};
+  p.vec2 = (A % 2 == 0) && ((x_stride | y_stride) % 2 == 0) && al16(x) && al16(y);
+  timing_begin(ctx, "pair_cmp");
+  hipLaunchKernelGGL(pair_cmp_kernel, dim3(rows_grid(ctx, N)), dim3(kBlock), 0, ctx->stream, p, out);
+  timing_end(ctx);
+  CRDT_HIP(ctx, hipGetLastError());
+  return CRDT_OK;
+}
+
+extern "C" int crdt_vclock_cmp_matrix(crdt_ctx *ctx, const uint64_t *x, size_t N, size_t A, size_t x_stride,
+                                      int8_t *out) {
+  CRDT_CHECK_CTX(ctx);
+  if (N == 0) return CRDT_OK;
+  if (!out || (A > 0 && !x)) return fail(ctx, CRDT_EINVAL, "vclock_cmp_matrix: NULL buffer");
+  if (A > 0 && x_stride < A) return fail(ctx, CRDT_EINVAL, "vclock_cmp_matrix: stride < A");
+  const unsigned long long tiles = (N + kCmpT - 1) / kCmpT;
+  if (tiles > 65535) return fail(ctx, CRDT_EUNSUPPORTED, "vclock_cmp_matrix: N = %zu too large", N);
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  timing_begin(ctx, "cmp_matrix");
+  hipLaunchKernelGGL(cmp_matrix_kernel, dim3((unsigned)tiles, (unsigned)tiles), dim3(kBlock), 0, ctx->stream,
+                     (const u64 *)x, (unsigned long long)N, (unsigned long long)A, (unsigned long long)x_stride,
+                     out);
+  timing_end(ctx);
+  CRDT_HIP(ctx, hipGetLastError());
+  return CRDT_OK;
+}
+
+static int read_rows(crdt_ctx *ctx, int pn, const uint64_t *in, size_t N, size_t A, size_t stride, uint64_t *out) {
+  CRDT_CHECK_CTX(ctx);
+  if (N == 0) return CRDT_OK;
+  if (!out || (A > 0 && !in)) return fail(ctx, CRDT_EINVAL, "read: NULL buffer");
+  if (A > 0 && stride < (pn ? 2 : 1) * A) return fail(ctx, CRDT_EINVAL, "read: row stride too small");
+  if (A >= (1ull << 62)) return fail(ctx, CRDT_EUNSUPPORTED, "read: A too large for 128-bit sums");
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  ReadPlan p{(const u64 *)in, N, A, stride, pn, (u64 *)out};
+  timing_begin(ctx, "read_sum");
+  hipLaunchKernelGGL(read_sum_kernel, dim3(rows_grid(ctx, N)), dim3(kBlock), 0, ctx->stream, p);
+  timing_end(ctx);
+  CRDT_HIP(ctx, hipGetLastError());
+  return CRDT_OK;
+}
+
+extern "C" int crdt_gcounter_read(crdt_ctx *ctx, const uint64_t *in, size_t N, size_t A, size_t row_stride,
+                                  uint64_t *out) {
+  return read_rows(ctx, 0, in, N, A, row_stride, out);
+}
+
+extern "C" int crdt_pncounter_read(crdt_ctx *ctx, const uint64_t *in, size_t N, size_t A, size_t row_stride,
+                                   uint64_t *out) {
+  return read_rows(ctx, 1, in, N, A, row_stride, out);
+}

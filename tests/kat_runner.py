@@ -1,7 +1,9 @@
 """Replays the reference's known-answer tests (tests/golden/kat_*.json).
 
 `merge_hook(dst_obj, src_obj, kind) -> new_dst_obj` lets the GPU tests route every merge
-through libcrdt_gpu; by default the oracle's own merge runs.
+through libcrdt_gpu; by default the oracle's own merge runs.  `causal_hook` (optional) routes
+VClock forget / glb / partial_cmp and counter read() the same way: an object with methods
+forget(x, y) / glb(x, y) (mutate x), cmp(x, y) -> Ordering code or None, read(counter) -> int.
 """
 import json
 import os
@@ -77,7 +79,7 @@ def _cmp(x, op, y):
     raise ValueError(op)
 
 
-def run_case(case, merge_hook=default_merge):
+def run_case(case, merge_hook=default_merge, causal_hook=None):
     env = {}
     for st in case["steps"]:
         op, args = st[0], st[1:]
@@ -104,9 +106,15 @@ def run_case(case, merge_hook=default_merge):
             dst, src = env[args[0]], env[args[1]]
             env[args[0]] = merge_hook(dst, src, kind_of(dst))
         elif op == "forget":
-            env[args[0]].forget(env[args[1]])
+            if causal_hook is not None and isinstance(env[args[0]], O.VClock):
+                causal_hook.forget(env[args[0]], env[args[1]])
+            else:
+                env[args[0]].forget(env[args[1]])
         elif op == "glb":
-            env[args[0]].glb(env[args[1]])
+            if causal_hook is not None:
+                causal_hook.glb(env[args[0]], env[args[1]])
+            else:
+                env[args[0]].glb(env[args[1]])
         elif op == "update":
             reg, val, marker, expect_err = env[args[0]], args[1], args[2], args[3]
             try:
@@ -152,10 +160,14 @@ def run_case(case, merge_hook=default_merge):
             assert env[args[0]].get(args[1]) == args[2]
         elif op == "assert_cmp":
             assert _cmp(env[args[0]], args[1], env[args[2]]), st
+            if causal_hook is not None and isinstance(env[args[0]], O.VClock):
+                assert causal_hook.cmp(env[args[0]], env[args[2]]) == env[args[0]].partial_cmp(env[args[2]]), st
         elif op == "assert_read":
             v = env[args[0]]
             if isinstance(v, (O.GCounter, O.PNCounter)):
                 assert v.read() == args[1], (v.read(), args[1])
+                if causal_hook is not None:
+                    assert causal_hook.read(v) == args[1], (causal_hook.read(v), args[1])
             elif isinstance(v, O.GSet):
                 assert v.value == set(args[1])
             else:

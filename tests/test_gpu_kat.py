@@ -121,3 +121,49 @@ CASES = [c for f in ("kat_vclock.json", "kat_counters.json", "kat_orswot.json")
 @pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
 def test_kat_gpu(gpu_ctx, case):
     K.run_case(case, merge_hook=gpu_merge)
+
+
+class GpuCausal:
+    """Routes the KATs' VClock forget / glb / partial_cmp and counter read() through
+    libcrdt_gpu (crdt_vclock_pair_op, crdt_vclock_partial_cmp, crdt_*counter_read)."""
+
+    CODES = {0: O.EQUAL, 1: O.GREATER, -1: O.LESS, 2: O.NONE}
+
+    def _pair(self, x, y):
+        idx = intern.Index()
+        rows = intern.clocks_to_dense([x.dots, y.dots], idx)
+        return idx, to_dev(rows)
+
+    def forget(self, x, y):
+        idx, d = self._pair(x, y)
+        out = to_host(cg.causal.forget(d[0], d[1]))
+        x.dots = intern.dense_to_clocks(out[None, :], idx)[0]
+
+    def glb(self, x, y):
+        idx, d = self._pair(x, y)
+        out = to_host(cg.causal.glb(d[0], d[1]))
+        x.dots = intern.dense_to_clocks(out[None, :], idx)[0]
+
+    def cmp(self, x, y):
+        _, d = self._pair(x, y)
+        return self.CODES[int(cg.causal.partial_cmp(d[0], d[1]).cpu())]
+
+    def read(self, v):
+        idx = intern.Index()
+        if isinstance(v, O.GCounter):
+            rows = intern.clocks_to_dense([v.inner.dots], idx)
+            return cg.gcounter.read(to_dev(rows[0]))
+        p = intern.clocks_to_dense([v.p.inner.dots], idx)
+        n = intern.clocks_to_dense([v.n.inner.dots], idx, width=p.shape[1])
+        p = np.pad(p, ((0, 0), (0, n.shape[1] - p.shape[1])))
+        return cg.pncounter.read(to_dev(np.concatenate([p, n], axis=1)[0]))
+
+
+CAUSAL_CASES = [c for f in ("kat_vclock.json", "kat_counters.json") for c in K.load_cases(f)
+                if any(s[0] in ("forget", "glb", "assert_cmp", "assert_read") for s in c["steps"])]
+
+
+@pytest.mark.parametrize("case", CAUSAL_CASES, ids=[c["name"] for c in CAUSAL_CASES])
+def test_kat_gpu_causal(gpu_ctx, case):
+    """The reference's KATs with merges AND forget / glb / partial_cmp / read on the GPU."""
+    K.run_case(case, merge_hook=gpu_merge, causal_hook=GpuCausal())
