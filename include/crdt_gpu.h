@@ -254,6 +254,30 @@ int crdt_gcounter_read(crdt_ctx *ctx, const uint64_t *in, size_t N, size_t A, si
 int crdt_pncounter_read(crdt_ctx *ctx, const uint64_t *in, size_t N, size_t A, size_t row_stride,
                         uint64_t *out);
 
+/* ---- batched CmRDT::apply ---------------------------------------------------
+ * Apply n_ops ops to N dense states; op i targets state state_idx[i] (row at
+ * states + state_idx[i]*row_stride).  The ops of these types are per-cell joins, so they commute:
+ * the batch equals applying them one by one in any order, as the reference's apply does.
+ *   VClock::apply / apply_dot (vclock.rs:125-127, :155-159), GCounter::apply (gcounter.rs:39-41):
+ *       row[actor[i]] = max(row[actor[i]], counter[i])                       (A-word rows)
+ *   PNCounter::apply (pncounter.rs:62-67): dir[i] == 0 (Dir::Pos) -> P column actor[i],
+ *       1 (Dir::Neg) -> N column A + actor[i]                                 (2A-word rows P ‖ N)
+ *   GSet::apply / insert (gset.rs:46-48, :69-71): set bit element[i] of a ceil(U/64)-word bitmap
+ * state_idx / actor / element are device u32, counter device u64, dir device u8.  Ops with
+ * state_idx >= N or actor >= A (element >= U) are skipped and counted into *bad (device u32,
+ * added to; may be NULL). */
+int crdt_vclock_apply_batch(crdt_ctx *ctx, uint64_t *states, size_t N, size_t A, size_t row_stride,
+                            const uint32_t *state_idx, const uint32_t *actor, const uint64_t *counter,
+                            size_t n_ops, uint32_t *bad);
+int crdt_gcounter_apply_batch(crdt_ctx *ctx, uint64_t *states, size_t N, size_t A, size_t row_stride,
+                              const uint32_t *state_idx, const uint32_t *actor, const uint64_t *counter,
+                              size_t n_ops, uint32_t *bad);
+int crdt_pncounter_apply_batch(crdt_ctx *ctx, uint64_t *states, size_t N, size_t A, size_t row_stride,
+                               const uint32_t *state_idx, const uint32_t *actor, const uint64_t *counter,
+                               const uint8_t *dir, size_t n_ops, uint32_t *bad);
+int crdt_gset_apply_batch(crdt_ctx *ctx, uint64_t *states, size_t N, size_t U, size_t row_stride,
+                          const uint32_t *state_idx, const uint32_t *element, size_t n_ops, uint32_t *bad);
+
 /* ---- synthetic inputs (bench / test data, generated in HBM) --------------------------------
  * Counter-based and reproducible on the CPU (tests/golden/make_golden.py restates them).
  * kind 0 = clock/counter cells, 1 = GSet bitmap words, 2 = LWW markers, 3 = LWW vals.

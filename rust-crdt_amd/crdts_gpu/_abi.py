@@ -30,7 +30,8 @@ EXPORTS = (
     "crdt_lwwreg_lub_many", "crdt_lwwreg_merge_batch",
     "crdt_orswot_lub_many", "crdt_map_lub_many",
     "crdt_vclock_pair_op", "crdt_vclock_partial_cmp", "crdt_vclock_cmp_matrix", "crdt_gcounter_read",
-    "crdt_pncounter_read",
+    "crdt_pncounter_read", "crdt_vclock_apply_batch", "crdt_gcounter_apply_batch",
+    "crdt_pncounter_apply_batch", "crdt_gset_apply_batch",
     "crdt_synth_fill", "crdt_synth_orswot", "crdt_synth_orswot_rm", "crdt_synth_map",
 )
 
@@ -106,6 +107,10 @@ _SIGS = {
     "crdt_vclock_cmp_matrix": ([P, P, S, S, S, P], ctypes.c_int),
     "crdt_gcounter_read": ([P, P, S, S, S, P], ctypes.c_int),
     "crdt_pncounter_read": ([P, P, S, S, S, P], ctypes.c_int),
+    "crdt_vclock_apply_batch": ([P, P, S, S, S, P, P, P, S, P], ctypes.c_int),
+    "crdt_gcounter_apply_batch": ([P, P, S, S, S, P, P, P, S, P], ctypes.c_int),
+    "crdt_pncounter_apply_batch": ([P, P, S, S, S, P, P, P, P, S, P], ctypes.c_int),
+    "crdt_gset_apply_batch": ([P, P, S, S, S, P, P, S, P], ctypes.c_int),
 }
 for _t in ("vclock", "gcounter", "pncounter", "gset"):
     _SIGS[f"crdt_{_t}_lub_many"] = ([P, P, S, S, S, S, S, P, S, ctypes.c_uint], ctypes.c_int)

@@ -72,6 +72,19 @@ b = m_in[:64].cpu().numpy().view(np.uint64)
 ok = all(mm[i, j] == codes[vc(b[i]).partial_cmp(vc(b[j]))] for i in range(64) for j in range(64))
 res.append(dict(op="cmp_matrix", clocks=Nm, actors=Am, pairs=Nm * Nm, parity="ok" if ok else "MISMATCH",
                 kernel_us=r["kernel_us"], pair_compares_per_s=Nm * Nm / (r["kernel_us"] / 1e6)))
+# batched apply: 64M GCounter dots scattered over the 1M x 256 states (random cells)
+n_ops = 1 << 26
+g = torch.Generator(device="cuda")
+g.manual_seed(7)
+si = torch.randint(0, N, (n_ops,), device="cuda", dtype=torch.int32, generator=g)
+ac = torch.randint(0, A, (n_ops,), device="cuda", dtype=torch.int32, generator=g)
+ct = torch.randint(0, 1 << 40, (n_ops,), device="cuda", dtype=torch.int64, generator=g)
+before = x[si[:64].long(), ac[:64].long()].clone()
+r = timed("apply", lambda: cg.apply.apply_dots("gcounter", x, si, ac, ct, ctx=ctx), n_ops * 16)
+after = x[si[:64].long(), ac[:64].long()]
+ok = bool(((after.cpu().numpy().view(np.uint64) >= ct[:64].cpu().numpy().view(np.uint64)).all()))
+res.append(dict(op="gcounter_apply", states=N, actors=A, ops=n_ops, parity="ok" if ok else "MISMATCH",
+                kernel_us=r["kernel_us"], ops_per_s=n_ops / (r["kernel_us"] / 1e6)))
 for d in res:
     print(json.dumps(d), flush=True)
 sys.exit(0 if all(d["parity"] == "ok" for d in res) else 3)
