@@ -36,8 +36,8 @@ __global__ __launch_bounds__(kBlock) void pair_op_kernel(PairPlan p) {
     u64 *orow = p.out + r * p.os;
     if (p.vec2) {
       for (unsigned long long c = 2ull * lane; c < p.A; c += 2ull * kWave) {
-        const u64x2 a = *reinterpret_cast<const u64x2 *>(xr + c);
-        const u64x2 b = *reinterpret_cast<const u64x2 *>(yr + c);
+        const u64x2 a = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(xr + c));
+        const u64x2 b = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(yr + c));
         u64x2 o;
         o.x = pair_apply(p.op, a.x, b.x);
         o.y = pair_apply(p.op, a.y, b.y);
@@ -60,8 +60,8 @@ __global__ __launch_bounds__(kBlock) void pair_cmp_kernel(PairPlan p, int8_t *re
     bool ge = true, le = true;
     if (p.vec2) {
       for (unsigned long long c = 2ull * lane; c < p.A; c += 2ull * kWave) {
-        const u64x2 a = *reinterpret_cast<const u64x2 *>(xr + c);
-        const u64x2 b = *reinterpret_cast<const u64x2 *>(yr + c);
+        const u64x2 a = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(xr + c));
+        const u64x2 b = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(yr + c));
         ge &= (a.x >= b.x) & (a.y >= b.y);
         le &= (a.x <= b.x) & (a.y <= b.y);
       }
@@ -136,6 +136,7 @@ struct ReadPlan {
   unsigned long long N, A, rs;
   int pn;  // 0: GCounter (A words), 1: PNCounter (P in [0, A), N in [A, 2A))
   u64 *out;  // [N][2] (lo, hi)
+  int vec2;
 };
 
 __device__ __forceinline__ void add128(u64 &lo, u64 &hi, u64 blo, u64 bhi) {
@@ -160,9 +161,22 @@ __global__ __launch_bounds__(kBlock) void read_sum_kernel(ReadPlan p) {
   for (unsigned long long r = w0; r < p.N; r += nw) {
     const u64 *row = p.in + r * p.rs;
     u64 plo = 0, phi = 0, nlo = 0, nhi = 0;
-    for (unsigned long long c = lane; c < p.A; c += kWave) {
-      add128(plo, phi, row[c], 0);
-      if (p.pn) add128(nlo, nhi, row[p.A + c], 0);
+    if (p.vec2) {  // 16-byte loads
+      for (unsigned long long c = 2ull * lane; c < p.A; c += 2ull * kWave) {
+        const u64x2 v = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(row + c));
+        add128(plo, phi, v.x, 0);
+        add128(plo, phi, v.y, 0);
+        if (p.pn) {
+          const u64x2 w = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(row + p.A + c));
+          add128(nlo, nhi, w.x, 0);
+          add128(nlo, nhi, w.y, 0);
+        }
+      }
+    } else {
+      for (unsigned long long c = lane; c < p.A; c += kWave) {
+        add128(plo, phi, __builtin_nontemporal_load(row + c), 0);
+        if (p.pn) add128(nlo, nhi, __builtin_nontemporal_load(row + p.A + c), 0);
+      }
     }
     wave_sum128(plo, phi);
     if (p.pn) {
@@ -179,9 +193,10 @@ __global__ __launch_bounds__(kBlock) void read_sum_kernel(ReadPlan p) {
 }
 
 static unsigned rows_grid(const crdt_ctx *ctx, unsigned long long N) {
-  // one wave per row, 4 waves per workgroup; enough workgroups to fill the chip 8 deep
+  // one wave per row, 4 waves per workgroup; enough workgroups to fill the chip
+  // (tune rows_wpc: workgroups per CU, default 8)
   const unsigned long long want = (N + 3) / 4;
-  const unsigned long long cap = (unsigned long long)ctx->cu_count * 8;
+  const unsigned long long cap = (unsigned long long)ctx->cu_count * ctx->tune.rows_blocks_per_cu;
   return (unsigned)(want < cap ? (want ? want : 1) : cap);
 }
 
@@ -249,7 +264,8 @@ static int read_rows(crdt_ctx *ctx, int pn, const uint64_t *in, size_t N, size_t
   if (A > 0 && stride < (pn ? 2 : 1) * A) return fail(ctx, CRDT_EINVAL, "read: row stride too small");
   if (A >= (1ull << 62)) return fail(ctx, CRDT_EUNSUPPORTED, "read: A too large for 128-bit sums");
   CRDT_HIP(ctx, hipSetDevice(ctx->device));
-  ReadPlan p{(const u64 *)in, N, A, stride, pn, (u64 *)out};
+  ReadPlan p{(const u64 *)in, N, A, stride, pn, (u64 *)out, 0};
+  p.vec2 = (A % 2 == 0) && (stride % 2 == 0) && al16(in);
   timing_begin(ctx, "read_sum");
   hipLaunchKernelGGL(read_sum_kernel, dim3(rows_grid(ctx, N)), dim3(kBlock), 0, ctx->stream, p);
   timing_end(ctx);

@@ -205,6 +205,7 @@ static void apply_tune(crdt_ctx *ctx, const char *t) {
       else if (k == "mchunk" && (v == 8 || v == 16)) ctx->tune.map_chunk = v;
       else if (k == "mring" && v >= 2 && v <= 4) ctx->tune.map_ring = v;
       else if (k == "mspec") ctx->tune.map_spec = v != 0;
+      else if (k == "rbpc" && v > 0) ctx->tune.rows_blocks_per_cu = v;
     }
     pos = end + 1;
   }

@@ -86,5 +86,6 @@ ok = bool(((after.cpu().numpy().view(np.uint64) >= ct[:64].cpu().numpy().view(np
 res.append(dict(op="gcounter_apply", states=N, actors=A, ops=n_ops, parity="ok" if ok else "MISMATCH",
                 kernel_us=r["kernel_us"], ops_per_s=n_ops / (r["kernel_us"] / 1e6)))
 for d in res:
+    d["tune"] = os.environ.get("CRDT_TUNE", "")
     print(json.dumps(d), flush=True)
 sys.exit(0 if all(d["parity"] == "ok" for d in res) else 3)
