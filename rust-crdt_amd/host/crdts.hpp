@@ -237,6 +237,119 @@ void merge_batch(Gpu &gpu, std::vector<VClock<A>> &selves, const std::vector<VCl
   for (size_t i = 0; i < N; ++i) selves[i] = detail::read_row(ix, res.data() + i * W, W);
 }
 
+// ---- causal helpers on the GPU (crdt_vclock_pair_op / partial_cmp / cmp_matrix) ------------
+namespace detail {
+// Pairs -> two dense (N x W) row blocks over one interner.
+template <class A>
+size_t pair_rows(const std::vector<VClock<A>> &xs, const std::vector<VClock<A>> &ys, Interner<A> &ix,
+                 std::vector<uint64_t> &x, std::vector<uint64_t> &y) {
+  if (xs.size() != ys.size()) throw std::invalid_argument("pair op: size mismatch");
+  for (auto &r : xs) intern_clock(ix, r);
+  for (auto &r : ys) intern_clock(ix, r);
+  ix.freeze();
+  const size_t N = xs.size(), W = ix.size();
+  x.assign(N * W, 0);
+  y.assign(N * W, 0);
+  for (size_t i = 0; i < N; ++i) {
+    write_row(ix, xs[i], x.data() + i * W);
+    write_row(ix, ys[i], y.data() + i * W);
+  }
+  return W;
+}
+template <class A>
+void pair_op(Gpu &gpu, int op, std::vector<VClock<A>> &selves, const std::vector<VClock<A>> &others) {
+  Interner<A> ix;
+  std::vector<uint64_t> x, y;
+  const size_t W = pair_rows(selves, others, ix, x, y), N = selves.size();
+  if (N == 0 || W == 0) return;
+  DeviceBuf<uint64_t> dx(x), dy(y);
+  gpu.check(crdt_vclock_pair_op(gpu.ctx(), op, dx.get(), dx.get(), dy.get(), N, W, W, W, W), "crdt_vclock_pair_op");
+  gpu.sync();
+  auto res = dx.download();
+  for (size_t i = 0; i < N; ++i) selves[i] = read_row(ix, res.data() + i * W, W);
+}
+inline std::optional<Ordering> ordering_of(int8_t c) {
+  if (c == 0) return Ordering::Equal;
+  if (c == 1) return Ordering::Greater;
+  if (c == -1) return Ordering::Less;
+  return std::nullopt;
+}
+}  // namespace detail
+
+// for i: selves[i].glb(&others[i])      (vclock.rs:246-259)
+template <class A>
+void glb_batch(Gpu &gpu, std::vector<VClock<A>> &selves, const std::vector<VClock<A>> &others) {
+  detail::pair_op(gpu, CRDT_PAIR_GLB, selves, others);
+}
+// for i: selves[i].forget(&others[i])   (Causal::forget, vclock.rs:95-105)
+template <class A>
+void forget_batch(Gpu &gpu, std::vector<VClock<A>> &selves, const std::vector<VClock<A>> &others) {
+  detail::pair_op(gpu, CRDT_PAIR_FORGET, selves, others);
+}
+// xs[i].partial_cmp(&ys[i])               (vclock.rs:68-80; nullopt = concurrent)
+template <class A>
+std::vector<std::optional<Ordering>> partial_cmp_batch(Gpu &gpu, const std::vector<VClock<A>> &xs,
+                                                        const std::vector<VClock<A>> &ys) {
+  Interner<A> ix;
+  std::vector<uint64_t> x, y;
+  const size_t W = detail::pair_rows(xs, ys, ix, x, y), N = xs.size();
+  std::vector<std::optional<Ordering>> out;
+  if (N == 0) return out;
+  if (W == 0) return std::vector<std::optional<Ordering>>(N, Ordering::Equal);
+  DeviceBuf<uint64_t> dx(x), dy(y);
+  DeviceBuf<int8_t> dc(N);
+  gpu.check(crdt_vclock_partial_cmp(gpu.ctx(), dx.get(), dy.get(), N, W, W, W, dc.get()), "crdt_vclock_partial_cmp");
+  gpu.sync();
+  for (int8_t c : dc.download()) out.push_back(detail::ordering_of(c));
+  return out;
+}
+// every clocks[i].partial_cmp(&clocks[j]), row-major N x N
+template <class A>
+std::vector<std::optional<Ordering>> cmp_matrix(Gpu &gpu, const std::vector<VClock<A>> &clocks) {
+  Interner<A> ix;
+  for (auto &c : clocks) detail::intern_clock(ix, c);
+  ix.freeze();
+  const size_t N = clocks.size(), W = ix.size();
+  std::vector<std::optional<Ordering>> out;
+  if (N == 0) return out;
+  if (W == 0) return std::vector<std::optional<Ordering>>(N * N, Ordering::Equal);
+  std::vector<uint64_t> x(N * W, 0);
+  for (size_t i = 0; i < N; ++i) detail::write_row(ix, clocks[i], x.data() + i * W);
+  DeviceBuf<uint64_t> dx(x);
+  DeviceBuf<int8_t> dc(N * N);
+  gpu.check(crdt_vclock_cmp_matrix(gpu.ctx(), dx.get(), N, W, W, dc.get()), "crdt_vclock_cmp_matrix");
+  gpu.sync();
+  for (int8_t c : dc.download()) out.push_back(detail::ordering_of(c));
+  return out;
+}
+// for (i, dot) in ops { states[i].apply(dot) }   (CmRDT::apply, vclock.rs:125-127, 155-159)
+template <class A>
+void apply_batch(Gpu &gpu, std::vector<VClock<A>> &states, const std::vector<std::pair<size_t, Dot<A>>> &ops) {
+  Interner<A> ix;
+  for (auto &s : states) detail::intern_clock(ix, s);
+  for (auto &o : ops) ix.add(o.second.actor);
+  ix.freeze();
+  const size_t N = states.size(), W = ix.size();
+  if (N == 0 || W == 0 || ops.empty()) return;
+  std::vector<uint64_t> rows(N * W, 0), ctr;
+  std::vector<uint32_t> si, ac;
+  for (size_t i = 0; i < N; ++i) detail::write_row(ix, states[i], rows.data() + i * W);
+  for (auto &o : ops) {
+    if (o.first >= N) throw std::out_of_range("apply_batch: state index");
+    si.push_back((uint32_t)o.first);
+    ac.push_back(ix.at(o.second.actor));
+    ctr.push_back(o.second.counter);
+  }
+  DeviceBuf<uint64_t> drows(rows), dctr(ctr);
+  DeviceBuf<uint32_t> dsi(si), dac(ac), bad(std::vector<uint32_t>{0});
+  gpu.check(crdt_vclock_apply_batch(gpu.ctx(), drows.get(), N, W, W, dsi.get(), dac.get(), dctr.get(), ops.size(),
+                                    bad.get()),
+            "crdt_vclock_apply_batch");
+  gpu.sync();
+  auto res = drows.download();
+  for (size_t i = 0; i < N; ++i) states[i] = detail::read_row(ix, res.data() + i * W, W);
+}
+
 // ---- GCounter (gcounter.rs) / PNCounter (pncounter.rs) ------------------------------------
 template <class A>
 class GCounter {
@@ -268,6 +381,25 @@ GCounter<A> lub_many(Gpu &gpu, const std::vector<GCounter<A>> &replicas) {
   GCounter<A> g;
   g.inner = detail::read_row(ix, out.data(), W);
   return g;
+}
+
+// GCounter::read of many counters on the GPU (crdt_gcounter_read, exact 128-bit sums).
+template <class A>
+std::vector<unsigned __int128> read_batch(Gpu &gpu, const std::vector<GCounter<A>> &cs) {
+  Interner<A> ix;
+  for (auto &c : cs) detail::intern_clock(ix, c.inner);
+  ix.freeze();
+  const size_t N = cs.size(), W = ix.size();
+  std::vector<unsigned __int128> out(N, 0);
+  if (N == 0 || W == 0) return out;
+  std::vector<uint64_t> rows(N * W, 0);
+  for (size_t i = 0; i < N; ++i) detail::write_row(ix, cs[i].inner, rows.data() + i * W);
+  DeviceBuf<uint64_t> d(rows), w(2 * N);
+  gpu.check(crdt_gcounter_read(gpu.ctx(), d.get(), N, W, W, w.get()), "crdt_gcounter_read");
+  gpu.sync();
+  auto h = w.download();
+  for (size_t i = 0; i < N; ++i) out[i] = ((unsigned __int128)h[2 * i + 1] << 64) | h[2 * i];
+  return out;
 }
 
 enum class Dir { Pos, Neg };  // pncounter.rs:36-41

@@ -1,6 +1,7 @@
 // C++ host-mirror tests (rust-crdt_amd/host/crdts.hpp): the reference's own tests, restated
 // with every merge executed by libcrdt_gpu on the GPU.  Run by tests/test_gpu_host_cpp.py.
-//   test/vclock.rs:118-231, src/gcounter.rs:79-92, src/pncounter.rs:135-184,
+//   test/vclock.rs:104-231, src/vclock.rs:231-245 (glb doctest), src/gcounter.rs:79-92,
+//   src/pncounter.rs:135-184,
 //   src/gset.rs:29-37, src/lwwreg.rs:36-42,112-138, src/orswot.rs:294-394, test/orswot.rs:33-236
 #include <cstdio>
 #include <cstdlib>
@@ -100,6 +101,66 @@ static void test_vclock_lub_many_and_batch(Gpu &g) {
   }
   CHECK(ok);
   CHECK(lub_many(g, std::vector<VClock<uint32_t>>{}) == VClock<uint32_t>());
+}
+
+static void test_forget_gpu(Gpu &g) {  // test/vclock.rs:104-116, forget on the GPU
+  std::vector<VClock<uint8_t>> a{vc<uint8_t>({{1, 4}, {2, 3}, {5, 9}})};
+  std::vector<VClock<uint8_t>> b{vc<uint8_t>({{1, 5}, {2, 3}, {5, 8}})};
+  forget_batch(g, a, b);
+  CHECK(a[0] == vc<uint8_t>({{5, 9}}));
+}
+static void doctest_glb_gpu(Gpu &g) {  // src/vclock.rs:231-245, glb on the GPU
+  VClock<int> c;
+  c.apply({23, 6});
+  c.apply({89, 14});
+  auto c2 = c;
+  std::vector<VClock<int>> cs{c}, c2s{c2};
+  glb_batch(g, cs, c2s);  // no-op: glb { c, c } = c
+  CHECK(cs[0] == c2);
+  cs[0].apply({43, 1});
+  CHECK(cs[0].get(43) == 1);
+  glb_batch(g, cs, c2s);  // removes the 43 => 1 entry
+  CHECK(cs[0].get(43) == 0);
+}
+static void test_causal_batches_gpu(Gpu &g) {  // GPU vs host on random clocks
+  std::mt19937_64 rng(11);
+  std::vector<VClock<uint32_t>> xs(400), ys(400);
+  for (size_t i = 0; i < xs.size(); ++i) {
+    for (int k = 0; k < 12; ++k) xs[i].apply({uint32_t(rng() % 20), rng() % 5 + 1});
+    ys[i] = (i % 4 == 0) ? xs[i] : VClock<uint32_t>();  // equal, dominated, dominating, concurrent
+    if (i % 4 == 1)
+      for (auto &kv : xs[i].dots) ys[i].apply({kv.first, kv.second > 1 ? kv.second - 1 : 0});
+    if (i % 4 == 2) {
+      ys[i] = xs[i];
+      ys[i].apply({uint32_t(rng() % 20), 9});
+    }
+    if (i % 4 == 3)
+      for (int k = 0; k < 12; ++k) ys[i].apply({uint32_t(rng() % 20), rng() % 5 + 1});
+  }
+  auto cmp = partial_cmp_batch(g, xs, ys);
+  bool ok = cmp.size() == xs.size();
+  for (size_t i = 0; ok && i < xs.size(); ++i) ok = cmp[i] == xs[i].partial_cmp(ys[i]);
+  CHECK(ok);
+  auto m = cmp_matrix(g, xs);
+  ok = m.size() == xs.size() * xs.size();
+  for (size_t i = 0; ok && i < xs.size(); i += 7)
+    for (size_t j = 0; ok && j < xs.size(); j += 3) ok = m[i * xs.size() + j] == xs[i].partial_cmp(xs[j]);
+  CHECK(ok);
+  auto states = xs;
+  std::vector<std::pair<size_t, Dot<uint32_t>>> ops;
+  for (int k = 0; k < 5000; ++k) ops.push_back({rng() % states.size(), {uint32_t(rng() % 30), rng() % 9}});
+  apply_batch(g, states, ops);
+  auto host = xs;
+  for (auto &o : ops) host[o.first].apply(o.second);
+  CHECK(states == host);
+  std::vector<GCounter<uint32_t>> gcs(xs.size());
+  for (size_t i = 0; i < xs.size(); ++i) gcs[i].inner = xs[i];
+  gcs[0].inner.apply({99, ~0ull});  // sum beyond 2^64
+  gcs[0].inner.apply({98, ~0ull});
+  auto rd = read_batch(g, gcs);
+  ok = true;
+  for (size_t i = 0; i < gcs.size(); ++i) ok = ok && rd[i] == gcs[i].read();
+  CHECK(ok);
 }
 
 // ---- src/gcounter.rs / src/pncounter.rs -------------------------------------------------------
@@ -361,6 +422,9 @@ int main() {
   test_merge_same_id(g);
   test_vclock_ordering();
   test_vclock_lub_many_and_batch(g);
+  test_forget_gpu(g);
+  doctest_glb_gpu(g);
+  test_causal_batches_gpu(g);
   gcounter_test_basic(g);
   pncounter_test_basic();
   pncounter_prop_merge_converges(g);
