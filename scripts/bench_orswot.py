@@ -27,6 +27,8 @@ ap.add_argument("--kmax", type=int, default=48)
 ap.add_argument("--steps", type=int, default=5)
 ap.add_argument("--sample-members", type=int, default=6)
 ap.add_argument("--tune", nargs="*", default=[""])
+ap.add_argument("--map-oracle-max", type=int, default=8192,
+                help="largest R checked with the map-based oracle fold (slow: O(R x D))")
 args = ap.parse_args()
 
 R, M, A = args.replicas, args.members, args.actors
@@ -100,9 +102,21 @@ for r in rows:
     e_cpu = O.apply_rm_rows(e_cpu, [0] * len(dr), dcl_h[dr], dmem_h[dr])
     assert np.array_equal(c_cpu[0], clock_h[r]), "synth clock mismatch"
     assert np.array_equal(e_cpu[0][msub], ent_h[r]), "synth entries mismatch"
-log("parity: oracle fold")
 t2 = time.time()
-oc, oe, odef, fold_s = O.orswot_fold(clock_h, ent_h, inp.def_off, dcl_h, sub_mem)
+if R <= args.map_oracle_max:
+    log("parity: oracle fold (map-based reference restatement)")
+    oc, oe, odef, fold_s = O.orswot_fold(clock_h, ent_h, inp.def_off, dcl_h, sub_mem)
+    oracle_kind = "orswot_fold (std::unordered_map states, oracle/ref_fold.cpp)"
+else:
+    # The map-based restatement re-applies every surviving deferred remove on every merge, as
+    # the reference does (orswot.rs:141-147): O(R x D) — minutes at config-3 size.  Its dense
+    # equivalent (join fold, then each remove once), cross-checked against it in
+    # tests/test_oracle_twins.py, checks the full-size result.
+    log("parity: dense oracle fold (join fold + removes, equivalent to the map-based fold)")
+    t_f = time.time()
+    oc, oe, odef = O.dense_orswot_lub(clock_h, ent_h, dcl_h, sub_mem)
+    fold_s = time.time() - t_f
+    oracle_kind = "dense_orswot_lub (numpy, = orswot_fold on every tested input)"
 got_c = res.clock.cpu().numpy().view(np.uint64)
 got_e = res.entries[torch.from_numpy(msub).cuda()].cpu().numpy().view(np.uint64)
 keep = res.def_keep.cpu().numpy()
@@ -112,8 +126,7 @@ for d in np.nonzero(keep)[0]:
     ms = frozenset(j for j, m in enumerate(msub.tolist()) if (int(gmem[d, m // 64]) >> (m % 64)) & 1)
     got_def.add((tuple(int(x) for x in dcl_h[d]), ms))
 ok = np.array_equal(oc, got_c) and np.array_equal(oe, got_e) and got_def == odef
-print(json.dumps({"parity": "ok" if ok else "MISMATCH", "sample_members": msub.tolist(),
-                  "surviving_deferred": len(odef), "oracle_fold_s": fold_s,
-                  "oracle_replica_merges_per_s_sampled": R / fold_s, "gen_s": gen_s,
+print(json.dumps({"parity": "ok" if ok else "MISMATCH", "oracle": oracle_kind, "sample_members": msub.tolist(),
+                  "surviving_deferred": len(odef), "oracle_fold_s": fold_s, "gen_s": gen_s,
                   "check_s": time.time() - t2}), flush=True)
 sys.exit(0 if ok else 3)
