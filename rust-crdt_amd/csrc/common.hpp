@@ -36,7 +36,7 @@ struct Tune {
   int lub_unroll = 8;
   int lub_nt = 1;
   int orswot_blocks_per_cu = 2;
-  int orswot_unroll = 2;
+  int orswot_unroll = 1;
   int merge_blocks_per_cu = 2;
   int map_glds = 1;    // Map fold: LDS-DMA staging where the shape allows it
   int map_chunk = 16;  // ... replicas per LDS chunk slot (8 or 16)
