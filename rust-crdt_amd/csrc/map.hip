@@ -268,24 +268,22 @@ __device__ __forceinline__ GldsLanes<NI> glds_lanes(const MapPlan &p, unsigned l
                                                     int lane) {
   GldsLanes<NI> L;
   const unsigned long long A = p.A, W = (2 + VI) * A;
+  // the three row sources as values first: a per-lane choice between struct FIELDS would be
+  // lowered as a dynamic-offset load, which forces the whole plan into scratch memory
+  const unsigned long long be = (unsigned long long)(p.ec + g * p.e_gs + k * A);
+  const unsigned long long bv = (unsigned long long)(p.vclk + g * p.vc_gs + k * VI * A);
+  const unsigned long long bc = (unsigned long long)(p.clock + g * p.c_gs);
+  const unsigned long long se = (unsigned long long)p.e_rs * 8, sv = (unsigned long long)p.vc_rs * 8,
+                           sc = (unsigned long long)p.c_rs * 8;
 #pragma unroll
   for (int j = 0; j < NI; ++j) {
     const unsigned long long o = (unsigned long long)(j * 64 + lane) * 2;
     L.on[j] = o < W;
-    const u64 *b;
-    long long st;
-    if (o < A) {
-      b = p.ec + g * p.e_gs + k * A + o;
-      st = p.e_rs;
-    } else if (o < (1 + VI) * A) {
-      b = p.vclk + g * p.vc_gs + k * VI * A + (o - A);
-      st = p.vc_rs;
-    } else {
-      b = p.clock + g * p.c_gs + (o < W ? o - (1 + VI) * A : 0);
-      st = p.c_rs;
-    }
-    L.src0[j] = reinterpret_cast<const char *>(b);
-    L.stride[j] = (unsigned long long)st * 8;
+    const bool ie = o < A, iv = !ie && o < (1 + VI) * A;
+    const unsigned long long off = ie ? o : (iv ? o - A : (o < W ? o - (1 + VI) * A : 0));
+    const unsigned long long base = ie ? be : (iv ? bv : bc);
+    L.src0[j] = reinterpret_cast<const char *>(base + off * 8);
+    L.stride[j] = ie ? se : (iv ? sv : sc);
   }
   return L;
 }
@@ -481,17 +479,6 @@ __device__ __forceinline__ u64 map_noop_nv(const u64 *buf, unsigned W, unsigned 
   }
 }
 
-// ... and on the unrolled iteration count ceil(A / LPS) (A <= 64).
-template <int VI, int LPS>
-__device__ __forceinline__ u64 map_noop_dispatch(const u64 *buf, unsigned W, unsigned A, const u64 *mirror,
-                                                 unsigned VO, bool present, int nv, unsigned n, int lane) {
-  const unsigned it = (A + LPS - 1) / LPS;
-  if (it <= 2) return map_noop_nv<VI, LPS, 2>(buf, W, A, mirror, VO, present, nv, n, lane);
-  if (it <= 4) return map_noop_nv<VI, LPS, 4>(buf, W, A, mirror, VO, present, nv, n, lane);
-  if (LPS >= 8 || it <= 8) return map_noop_nv<VI, LPS, (LPS >= 8 ? 8 : 8)>(buf, W, A, mirror, VO, present, nv, n, lane);
-  return map_noop_nv<VI, LPS, (LPS >= 8 ? 8 : 16)>(buf, W, A, mirror, VO, present, nv, n, lane);
-}
-
 // Own values pairwise not strictly ordered (precondition (a) of the scan).
 template <int APL, int VO>
 __device__ __forceinline__ bool mv_antichain(const MVState<APL, VO> &s) {
@@ -504,8 +491,12 @@ __device__ __forceinline__ bool mv_antichain(const MVState<APL, VO> &s) {
   return ok;
 }
 
-template <int APL, int VI, int VO, int CM, int NB, bool GL>
-__global__ __launch_bounds__(64) void map_fold_kernel(MapPlan p) {
+// ITM: unrolled scan iterations ceil(A / LPS) rounded up to a power of two, fixed per launch so
+// each kernel's register allocation only covers its own scan shape.
+template <int APL, int VI, int VO, int CM, int NB, bool GL, int ITM>
+__global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
+  const MapPlan p = pk;  // a local copy the optimizer can split into registers (the by-value
+                         // kernel argument itself would be materialized in scratch memory)
   const unsigned long long g = blockIdx.x / p.K;
   const unsigned long long k = blockIdx.x % p.K;
   const int lane = threadIdx.x;
@@ -675,8 +666,8 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan p) {
         if (uni(lim > s)) {
           MAP_TICK();
           const int nv = __builtin_popcount(__builtin_amdgcn_readfirstlane(mv.vm));
-          const u64 noop = map_noop_dispatch<VI, LPS>(buf, (unsigned)WS, (unsigned)A, mirror, VO, present, nv,
-                                                       (unsigned)n, lane);
+          const u64 noop = map_noop_nv<VI, LPS, ITM>(buf, (unsigned)WS, (unsigned)A, mirror, VO, present, nv,
+                                                      (unsigned)n, lane);
           const u64 from = (s >= NS) ? 0 : (~0ull << (LPS * s));
           const u64 upto = (lim >= NS) ? ~0ull : ((1ull << (LPS * lim)) - 1);
           const u64 stop = ~noop & grp_mask<LPS>() & from & upto;
@@ -993,20 +984,42 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan p) {
 
 using namespace crdt;
 
-template <int APL, int VI, int VO, int CM, int NB, bool GL>
-static hipError_t launch_map(const MapPlan &p, unsigned long long blocks, hipStream_t s) {
+template <int APL, int VI, int VO, int CM, int NB, bool GL, int ITM>
+static hipError_t launch_map_it(const MapPlan &p, unsigned long long blocks, hipStream_t s) {
   constexpr int C = GL ? CM : MapChunk<APL, VI, CM>::C;
   const size_t W = (2 + VI) * p.A;
   const size_t lds = (size_t)NB * C * (map_ws(W) + VI) * sizeof(u64) + kMapL * 2 * sizeof(unsigned) +
                      (2 + VO) * p.A * sizeof(u64);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   if (lds > 64 * 1024) {  // beyond the default dynamic-LDS limit (gfx950 has 160 KB per CU)
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&map_fold_kernel<APL, VI, VO, CM, NB, GL>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&map_fold_kernel<APL, VI, VO, CM, NB, GL, ITM>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL((map_fold_kernel<APL, VI, VO, CM, NB, GL>), dim3((unsigned)blocks), dim3(64), lds, s, p);
+  hipLaunchKernelGGL((map_fold_kernel<APL, VI, VO, CM, NB, GL, ITM>), dim3((unsigned)blocks), dim3(64), lds, s, p);
   return hipGetLastError();
+}
+
+// Scan shape: NS steps per scan (C rounded up to a power of two, <= 16), LPS = 64 / NS lanes per
+// step, ceil(A / LPS) iterations rounded up to a power of two (A <= 64 when the scan runs).
+template <int APL, int VI, int VO, int CM, int NB, bool GL>
+static hipError_t launch_map(const MapPlan &p, unsigned long long blocks, hipStream_t s) {
+  if constexpr (APL != 1) {
+    return launch_map_it<APL, VI, VO, CM, NB, GL, 2>(p, blocks, s);  // no scan: A > 64
+  } else {
+    constexpr int C = GL ? CM : MapChunk<APL, VI, CM>::C;
+    constexpr int NS = C > 8 ? 16 : (C > 4 ? 8 : (C > 2 ? 4 : 2));
+    constexpr int LPS = 64 / NS;
+    const unsigned long long it = (p.A + LPS - 1) / LPS;
+    if (it <= 2) return launch_map_it<APL, VI, VO, CM, NB, GL, 2>(p, blocks, s);
+    if (it <= 4) return launch_map_it<APL, VI, VO, CM, NB, GL, 4>(p, blocks, s);
+    if constexpr (LPS >= 8) {
+      return launch_map_it<APL, VI, VO, CM, NB, GL, 8>(p, blocks, s);
+    } else {
+      if (it <= 8) return launch_map_it<APL, VI, VO, CM, NB, GL, 8>(p, blocks, s);
+      return launch_map_it<APL, VI, VO, CM, NB, GL, 16>(p, blocks, s);
+    }
+  }
 }
 
 // Register-staged fold for VI input / 2*VI state value slots (any shape within the limits).
@@ -1019,12 +1032,11 @@ static hipError_t launch_map_vi(const MapPlan &p, int VI, unsigned long long blo
   }
 }
 
-// LDS-DMA fold (A <= 64, even; VI = V <= 2; 4 state values): chunk C and ring depth NB.
+// LDS-DMA fold (A <= 64, even; VI = V <= 2; 4 state values): 16-replica chunks in 2 slots
+// (default) or 8-replica chunks in 4 slots.
 template <int VI>
 static hipError_t launch_map_glds(const MapPlan &p, int cm, int nb, unsigned long long blocks, hipStream_t s) {
   if (cm == 8 && nb == 4) return launch_map<1, VI, 4, 8, 4, true>(p, blocks, s);
-  if (cm == 8 && nb == 3) return launch_map<1, VI, 4, 8, 3, true>(p, blocks, s);
-  if (cm == 16 && nb == 3) return launch_map<1, VI, 4, 16, 3, true>(p, blocks, s);
   return launch_map<1, VI, 4, 16, 2, true>(p, blocks, s);
 }
 
