@@ -339,12 +339,12 @@ __device__ __forceinline__ MapStep<APL, VI> map_step_read(const u64 *st, const u
 // Speculative no-op scan over the steps of a staged chunk (A <= 64).  The wave checks NS steps
 // at once: lane (s, g) = (lane / LPS, lane % LPS), LPS = 64 / NS, checks step s on actors g,
 // g+LPS, ... against the CURRENT fold state, mirrored in LDS (me = entry clock, mc = value
-// clocks, vm = valid slots, mcs = acc clock Cs); the LPS lanes of a step are combined bitwise on
-// the ballot masks.  Bit LPS*s of the result is set only if step s provably leaves (present, e,
+// clocks, vm = valid slots, mmx = max(entry clock, acc clock Cs)); the LPS lanes of a step are
+// combined bitwise on the ballot masks.  Bit LPS*s of the result is set only if step s provably leaves (present, e,
 // vals) unchanged.  With e = acc entry clock, e2 / c2[t] / Co = the replica's entry clock /
 // value clocks / clock, and Cs' >= Cs the acc clock at step s (so e2 <= Cs implies e2 <= Cs'):
 //   present, replica has the key (map.rs:170-192): common = max(e==e2?e:0, e2>Cs'?e2:0,
-//     e>Co?e:0) equals e if every actor has (e == 0 | e == e2 | e > Co) and (e2 <= e | e2 <= Cs);
+//     e>Co?e:0) equals e if every actor has (e == 0 | e == e2 | e > Co) and e2 <= max(e, Cs);
 //     then deleted = (e2 > e ? e2 : 0).  The MVReg is unchanged if (a) the own values are an
 //     antichain (the caller only scans then), (b) forget(deleted) changes no own value clock
 //     (no actor with 0 < x <= deleted), and (c) every incoming value is <= an own one (not
@@ -362,7 +362,7 @@ __device__ __forceinline__ MapStep<APL, VI> map_step_read(const u64 *st, const u
 // identity (vclock.rs:98-104).
 // Most steps of a fold change nothing, so their cost drops from a full exact step to a share
 // of this wave-wide scan: per actor and step one vector compare and one scalar mask op per
-// test, all LDS reads unpredicated (lanes past A read actor A-1 and are masked out).
+// test, all LDS reads unpredicated.
 template <int LPS>
 __device__ __forceinline__ u64 grp_mask() {
   u64 m = 0;
@@ -385,39 +385,39 @@ __device__ __forceinline__ u64 orN(u64 m) {
 
 template <int VI, int NQ, int LPS, int IT, bool PRESENT>
 __device__ __forceinline__ u64 map_noop_steps(const u64 *buf, unsigned W, unsigned A, const u64 *me,
-                                              const u64 *mc, const u64 *mcs, unsigned n, int lane) {
+                                              const u64 *mc, const u64 *mmx, unsigned n, int lane) {
   // NQ = the number of own values, compacted into mirror slots 0..NQ-1 (PRESENT only)
   const unsigned st = (unsigned)lane / LPS;
   const unsigned gq = (unsigned)lane % LPS;
   const u64 *stp = buf + (st < n ? st : n - 1) * W;
-  u64 mP2 = 0, mE = ~0ull, mO = ~0ull, mCs = ~0ull;
-  u64 mRI[NQ > 0 ? NQ : 1], mDL[NQ > 0 ? NQ : 1], mLe2[VI][NQ > 0 ? NQ : 1], mVan[VI];
+  // Tests ANDed into the same verdict share one accumulator (andN(x) & andN(y) = andN(x & y)):
+  // mB for "replica has the key", mO for "replica lacks it"; the value-cover tests are ORed over
+  // own values after andN, so each keeps its own.
+  u64 mP2 = 0, mB = ~0ull, mO = ~0ull;
+  u64 mLe2[VI][NQ > 0 ? NQ : 1], mVan[VI];
 #pragma unroll
-  for (int t = 0; t < VI; ++t) mVan[t] = ~0ull;
+  for (int t = 0; t < VI; ++t) {
+    mVan[t] = ~0ull;
 #pragma unroll
-  for (int q = 0; q < NQ; ++q) {
-    mRI[q] = ~0ull;
-    mDL[q] = ~0ull;
-#pragma unroll
-    for (int t = 0; t < VI; ++t) mLe2[t][q] = ~0ull;
+    for (int q = 0; q < NQ; ++q) mLe2[t][q] = ~0ull;
   }
   // IT >= ceil(A / LPS) iterations, fully unrolled: every LDS read of the scan can be in
-  // flight at once.  Lanes past the last actor read actor A-1 and are neutral in every test.
+  // flight at once.  Lanes past the last actor re-read actor A-1 of their own step: every test
+  // bit is a function of (step, actor) alone and the masks are only ANDed / ORed, so a duplicate
+  // is neutral and no range mask is needed.
 #pragma unroll
   for (unsigned m = 0; m < IT; ++m) {
     const unsigned a0 = gq + LPS * m;
-    const u64 off = __ballot(a0 >= A);
     const unsigned a = a0 < A ? a0 : A - 1;
     const u64 e2 = stp[a];
+    const u64 mx = mmx[a];  // max(e, Cs); = Cs when absent (e == 0 then)
     // one vector compare per test, combined on the (scalar) ballot masks
     if constexpr (!PRESENT) {
-      const u64 ca = mcs[a];
-      mP2 |= __ballot(e2 != 0) & ~off;
-      mCs &= __ballot(e2 <= ca) | off;
+      mP2 |= __ballot(e2 != 0);
+      mB &= __ballot(e2 <= mx);
     } else {
       const u64 co = stp[(1 + VI) * A + a];
       const u64 ea = me[a];
-      const u64 ca = mcs[a];
       u64 c2[VI], sq[NQ > 0 ? NQ : 1], sq1[NQ > 0 ? NQ : 1];
 #pragma unroll
       for (int t = 0; t < VI; ++t) c2[t] = stp[(1 + t) * A + a];
@@ -427,32 +427,29 @@ __device__ __forceinline__ u64 map_noop_steps(const u64 *buf, unsigned W, unsign
         sq1[q] = sq[q] - 1;  // x - 1 >= y <=> x == 0 | x > y (wrapping)
       }
       const u64 eGtCo = __ballot(ea - 1 >= co);  // ea == 0 | ea > co
-      const u64 coGtE = __ballot(co > ea);       // ri = coGtE ? co : 0
-      const u64 e2GtE = __ballot(e2 > ea);       // deleted = e2GtE ? e2 : 0
-      mP2 |= __ballot(e2 != 0) & ~off;
-      mE &= ((__ballot(e2 <= ea) | __ballot(e2 <= ca)) & (eGtCo | __ballot(ea == e2))) | off;
-      mO &= eGtCo | off;
+      const u64 del = e2 > ea ? e2 : 0;          // deleted
+      mP2 |= __ballot(e2 != 0);
+      mB &= __ballot(e2 <= mx) & (eGtCo | __ballot(ea == e2));
+      mO &= eGtCo;
 #pragma unroll
-      for (int t = 0; t < VI; ++t)  // c2 <= deleted
-        mVan[t] &= (__ballot(c2[t] <= e2) & e2GtE) | (__ballot(c2[t] == 0) & ~e2GtE) | off;
+      for (int t = 0; t < VI; ++t) mVan[t] &= __ballot(c2[t] <= del);  // appended, forgotten to empty
+      if constexpr (NQ > 0) {
+        const u64 ri = co > ea ? co : 0;
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        mRI[q] &= ~coGtE | __ballot(sq1[q] >= co) | off;  // sq == 0 | sq > ri
-        mDL[q] &= ~e2GtE | __ballot(sq1[q] >= e2) | off;  // sq == 0 | sq > deleted
+        for (int q = 0; q < NQ; ++q) {
+          mO &= __ballot(sq1[q] >= ri);   // sq == 0 | sq > ri
+          mB &= __ballot(sq1[q] >= del);  // sq == 0 | sq > deleted
 #pragma unroll
-        for (int t = 0; t < VI; ++t) mLe2[t][q] &= __ballot(c2[t] <= sq[q]) | off;
+          for (int t = 0; t < VI; ++t) mLe2[t][q] &= __ballot(c2[t] <= sq[q]);
+        }
       }
     }
   }
   const u64 G1 = grp_mask<LPS>();
   const u64 P2 = orN<LPS>(mP2);
-  if constexpr (!PRESENT) return (~P2 | andN<LPS>(mCs)) & G1;
-  u64 both = P2 & andN<LPS>(mE), only = ~P2 & andN<LPS>(mO);
-#pragma unroll
-  for (int q = 0; q < NQ; ++q) {
-    only &= andN<LPS>(mRI[q]);
-    both &= andN<LPS>(mDL[q]);
-  }
+  if constexpr (!PRESENT) return (~P2 | andN<LPS>(mB)) & G1;
+  u64 both = P2 & andN<LPS>(mB);
+  const u64 only = ~P2 & andN<LPS>(mO);
 #pragma unroll
   for (int t = 0; t < VI; ++t) {
     u64 cov = andN<LPS>(mVan[t]);  // appended, then forgotten to empty
@@ -468,13 +465,13 @@ __device__ __forceinline__ u64 map_noop_steps(const u64 *buf, unsigned W, unsign
 template <int VI, int LPS, int IT>
 __device__ __forceinline__ u64 map_noop_nv(const u64 *buf, unsigned W, unsigned A, const u64 *mirror,
                                            unsigned VO, bool present, int nv, unsigned n, int lane) {
-  const u64 *me = mirror, *mc = mirror + A, *mcs = mirror + (1 + VO) * A;
-  if (!present) return map_noop_steps<VI, 0, LPS, IT, false>(buf, W, A, me, mc, mcs, n, lane);
+  const u64 *me = mirror, *mc = mirror + A, *mmx = mirror + (1 + VO) * A;
+  if (!present) return map_noop_steps<VI, 0, LPS, IT, false>(buf, W, A, me, mc, mmx, n, lane);
   switch (nv) {
-    case 0: return map_noop_steps<VI, 0, LPS, IT, true>(buf, W, A, me, mc, mcs, n, lane);
-    case 1: return map_noop_steps<VI, 1, LPS, IT, true>(buf, W, A, me, mc, mcs, n, lane);
-    case 2: return map_noop_steps<VI, 2, LPS, IT, true>(buf, W, A, me, mc, mcs, n, lane);
-    case 3: return map_noop_steps<VI, 3, LPS, IT, true>(buf, W, A, me, mc, mcs, n, lane);
+    case 0: return map_noop_steps<VI, 0, LPS, IT, true>(buf, W, A, me, mc, mmx, n, lane);
+    case 1: return map_noop_steps<VI, 1, LPS, IT, true>(buf, W, A, me, mc, mmx, n, lane);
+    case 2: return map_noop_steps<VI, 2, LPS, IT, true>(buf, W, A, me, mc, mmx, n, lane);
+    case 3: return map_noop_steps<VI, 3, LPS, IT, true>(buf, W, A, me, mc, mmx, n, lane);
     default: return 0;
   }
 }
@@ -686,7 +683,7 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
             }
             if ((unsigned long long)lane < A) cs[0] = mx;
           }
-          if (j > s && (unsigned long long)lane < A) mirror[(1 + VO) * A + lane] = cs[0];
+          if (j > s && (unsigned long long)lane < A) mirror[(1 + VO) * A + lane] = e[0] > cs[0] ? e[0] : cs[0];
           MAP_TOCK(cy_skip);
           if (j == s) cool = 4;  // the scan found nothing to skip: run a few exact steps first
 #ifdef MAP_STATS
@@ -909,7 +906,7 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
         anti = mv_antichain(mv);
         if ((unsigned long long)lane < A) {
           mirror[lane] = e[0];
-          mirror[(1 + VO) * A + lane] = cs[0];
+          mirror[(1 + VO) * A + lane] = e[0] > cs[0] ? e[0] : cs[0];
           int r = 0;  // own value clocks compacted into slots 0..nv-1 (any order)
 #pragma unroll
           for (int q = 0; q < VO; ++q)
