@@ -51,6 +51,11 @@ struct MapPlan {
   unsigned *o_nval;
   unsigned *o_flags;  // per group: bit0 > Vout values, bit1 bad def_row, bit2 state capacity
   int spec;           // speculative no-op scan on (tuning / diagnosis knob; results are identical)
+  // LDS-DMA path: per (group, chunk of C replicas) the max of the chunk's replica clocks,
+  // [G][nch][A] (map_chunk_max_kernel), staged with each chunk so a wholly skipped chunk merges
+  // its clocks with one compare (the acc clock only ever takes maxima of replica clocks, map.rs:217)
+  const u64 *cmax;
+  unsigned long long nch;
 };
 
 constexpr int kMapQ = 4;    // deferred removes tracked per key in registers before the slow path
@@ -289,19 +294,43 @@ __device__ __forceinline__ GldsLanes<NI> glds_lanes(const MapPlan &p, unsigned l
 }
 
 // DMA one chunk (steps i0 .. i0+C-1, clamped to iend-1: past the end a slot holds copies that
-// are never read) into an LDS slot.  Exactly C*NI + 1 global_load_lds per call, each with at
+// are never read) into an LDS slot.  Exactly C*NI + 2 global_load_lds per call, each with at
 // least one active lane (NI = ceil(W / 128) 1-KiB pieces per step image; the values of all C
-// steps in one 4-byte-per-lane piece), so a fixed vmcnt count retires a chunk.
+// steps in one 4-byte-per-lane piece; the chunk's clock max in one), so a fixed vmcnt count
+// retires a chunk.  Sources advance by their row stride (no per-step 64-bit multiply).
 template <int VI, int C, int NI>
 __device__ __forceinline__ void map_chunk_glds(const MapPlan &p, const GldsLanes<NI> &L, unsigned long long g,
                                                unsigned long long k, unsigned long long i0, unsigned long long iend,
-                                               u64 *img, unsigned long long WS, u64 *vals, int lane) {
+                                               u64 *img, unsigned long long WS, u64 *vals, u64 *cm, int lane) {
+  if (i0 + C <= iend) {  // a whole chunk (uniform)
+    const char *src[NI];
 #pragma unroll
-  for (int s = 0; s < C; ++s) {
-    const unsigned long long i = i0 + s < iend ? i0 + s : iend - 1;
+    for (int j = 0; j < NI; ++j) src[j] = L.src0[j] + i0 * L.stride[j];
+    if ((2 + VI) * p.A == NI * 128) {  // every lane moves a piece: no EXEC-masked regions
 #pragma unroll
-    for (int j = 0; j < NI; ++j)
-      if (L.on[j]) glds16(L.src0[j] + i * L.stride[j], img + s * WS + j * 128);
+      for (int s = 0; s < C; ++s)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          glds16(src[j], img + s * WS + j * 128);
+          src[j] += L.stride[j];
+        }
+    } else {
+#pragma unroll
+      for (int s = 0; s < C; ++s)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          if (L.on[j]) glds16(src[j], img + s * WS + j * 128);
+          src[j] += L.stride[j];
+        }
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < C; ++s) {
+      const unsigned long long i = i0 + s < iend ? i0 + s : iend - 1;
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+        if (L.on[j]) glds16(L.src0[j] + i * L.stride[j], img + s * WS + j * 128);
+    }
   }
   const int sv = lane / (2 * VI), dw = lane % (2 * VI);
   if (sv < C) {
@@ -309,6 +338,9 @@ __device__ __forceinline__ void map_chunk_glds(const MapPlan &p, const GldsLanes
     const unsigned *src = reinterpret_cast<const unsigned *>(p.vval + g * p.vv_gs + i * p.vv_rs + k * VI) + dw;
     glds4(src, vals);
   }
+  // the chunk's clock max: one more piece (lanes 0 .. A/2-1, A even)
+  if ((unsigned long long)(2 * lane) < p.A)
+    glds16(p.cmax + (g * p.nch + i0 / C) * p.A + 2 * lane, cm);
 }
 
 // Wait until at most N vector-memory ops are outstanding (counts above the 6-bit field clamp
@@ -551,6 +583,7 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
   // fold-state mirror read by the speculative scan: entry clock, VO value clocks, acc clock
   u64 *mirror = vbase + NB * C * VI + kMapL;  // (kMapL u64 = the two u32 lists)
   constexpr bool kSpec = APL == 1 && VO <= 4;
+  u64 *const cml = mirror + (2 + VO) * A;  // GL: NB staged chunk clock maxima (A words each)
   if (kSpec)
     for (unsigned long long x = lane; x < (2 + VO) * A; x += 64) mirror[x] = 0;
 
@@ -607,8 +640,8 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
     if (ni == 1) gl1 = glds_lanes<VI, 1>(p, g, k, lane);
     else gl2 = glds_lanes<VI, 2>(p, g, k, lane);
     for (unsigned long long c = 0; c + 1 < NB && c < nch; ++c) {
-      if (ni == 1) map_chunk_glds<VI, C, 1>(p, gl1, g, k, c * C, R, map_lds + c * C * WS, WS, vbase + c * C * VI, lane);
-      else map_chunk_glds<VI, C, 2>(p, gl2, g, k, c * C, R, map_lds + c * C * WS, WS, vbase + c * C * VI, lane);
+      if (ni == 1) map_chunk_glds<VI, C, 1>(p, gl1, g, k, c * C, R, map_lds + c * C * WS, WS, vbase + c * C * VI, cml + c * A, lane);
+      else map_chunk_glds<VI, C, 2>(p, gl2, g, k, c * C, R, map_lds + c * C * WS, WS, vbase + c * C * VI, cml + c * A, lane);
     }
   } else {
     if (nch > 0) {
@@ -629,20 +662,20 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
       if (nx < nch) {
         const unsigned ns = (unsigned)(nx % NB);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot's last LDS reads are done
-        if (ni == 1) map_chunk_glds<VI, C, 1>(p, gl1, g, k, nx * C, R, map_lds + ns * C * WS, WS, vbase + ns * C * VI, lane);
-        else map_chunk_glds<VI, C, 2>(p, gl2, g, k, nx * C, R, map_lds + ns * C * WS, WS, vbase + ns * C * VI, lane);
+        if (ni == 1) map_chunk_glds<VI, C, 1>(p, gl1, g, k, nx * C, R, map_lds + ns * C * WS, WS, vbase + ns * C * VI, cml + ns * A, lane);
+        else map_chunk_glds<VI, C, 2>(p, gl2, g, k, nx * C, R, map_lds + ns * C * WS, WS, vbase + ns * C * VI, cml + ns * A, lane);
       }
       MAP_TOCK(cy_issue);
       MAP_TICK();
       const unsigned long long after = (nch - 1 - ch) < (unsigned long long)(NB - 1) ? nch - 1 - ch : NB - 1;
       if (ni == 1) {
-        constexpr int P1 = C + 1;
+        constexpr int P1 = C + 2;
         if (after == 0) wait_vmcnt<0>();
         else if (after == 1) wait_vmcnt<P1>();
         else if (NB > 2 && after == 2) wait_vmcnt<(NB > 2 ? 2 * P1 : 0)>();
         else wait_vmcnt<(NB > 3 ? 3 * P1 : 0)>();
       } else {
-        constexpr int P2 = 2 * C + 1;
+        constexpr int P2 = 2 * C + 2;
         if (after == 0) wait_vmcnt<0>();
         else if (after == 1) wait_vmcnt<P2>();
         else if (NB > 2 && after == 2) wait_vmcnt<(NB > 2 ? 2 * P2 : 0)>();
@@ -671,7 +704,11 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
           j = stop ? (unsigned long long)(__builtin_ctzll(stop) / LPS) : lim;
           MAP_TOCK(cy_scan);
           MAP_TICK();
-          {  // acc.clock.merge of the skipped replicas: every read issued at once, range masked
+          if (GL && s == 0 && j == n) {  // the whole chunk: its staged clock max
+            const unsigned long long a = (unsigned long long)lane < A ? lane : A - 1;
+            const u64 x = cml[slot * A + a];
+            if ((unsigned long long)lane < A) cs[0] = cs[0] > x ? cs[0] : x;
+          } else {  // acc.clock.merge of the skipped replicas: every read issued at once, range masked
             const unsigned long long a = (unsigned long long)lane < A ? lane : A - 1;
             u64 mx = cs[0];
 #pragma unroll
@@ -981,12 +1018,29 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
 
 using namespace crdt;
 
+// Max of the replica clocks of each chunk of C replicas, [G][nch][A]: the clock merge of a
+// chunk the fold skips entirely (one block per (group, chunk), lane = actor).
+__global__ __launch_bounds__(64) void map_chunk_max_kernel(const u64 *clock, long long c_rs, long long c_gs,
+                                                           unsigned long long R, unsigned long long A,
+                                                           unsigned long long nch, unsigned C, u64 *out) {
+  const unsigned long long g = blockIdx.x / nch, ch = blockIdx.x % nch;
+  const unsigned long long i0 = ch * C, i1 = R < i0 + C ? R : i0 + C;
+  for (unsigned long long a = threadIdx.x; a < A; a += 64) {
+    u64 m = 0;
+    for (unsigned long long i = i0; i < i1; ++i) {
+      const u64 x = __builtin_nontemporal_load(clock + g * c_gs + i * c_rs + a);
+      m = m > x ? m : x;
+    }
+    out[(g * nch + ch) * A + a] = m;
+  }
+}
+
 template <int APL, int VI, int VO, int CM, int NB, bool GL, int ITM>
 static hipError_t launch_map_it(const MapPlan &p, unsigned long long blocks, hipStream_t s) {
   constexpr int C = GL ? CM : MapChunk<APL, VI, CM>::C;
   const size_t W = (2 + VI) * p.A;
   const size_t lds = (size_t)NB * C * (map_ws(W) + VI) * sizeof(u64) + kMapL * 2 * sizeof(unsigned) +
-                     (2 + VO) * p.A * sizeof(u64);
+                     (2 + VO) * p.A * sizeof(u64) + (GL ? NB * p.A * sizeof(u64) : 0);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   if (lds > 64 * 1024) {  // beyond the default dynamic-LDS limit (gfx950 has 160 KB per CU)
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&map_fold_kernel<APL, VI, VO, CM, NB, GL, ITM>),
@@ -1098,25 +1152,35 @@ extern "C" int crdt_map_lub_many(crdt_ctx *ctx, const crdt_map_batch *in, crdt_m
   p.o_flags = out->flags;
   p.spec = ctx->tune.map_spec;
   if (int rc = device_fill(ctx, out->flags, G * sizeof(unsigned), 0)) return rc;
+  // LDS-DMA staging when every step image is whole 16-byte pieces (A even, 16-byte aligned
+  // rows and strides) and the state fits 4 values; register staging otherwise
+  const bool even = ((p.c_rs | p.c_gs | p.e_rs | p.e_gs | p.vc_rs | p.vc_gs) & 1) == 0;
+  const bool glds = ctx->tune.map_glds && R > 0 && A <= 64 && (A & 1) == 0 && (V == 1 || V == 2) &&
+                    want <= 4 && even && aligned16(p.clock) && aligned16(p.ec) && aligned16(p.vclk) &&
+                    G * ((R + 7) / 8) < 0x7fffffffULL;
+  const unsigned gC = (ctx->tune.map_chunk == 8 && ctx->tune.map_ring == 4) ? 8 : 16;  // launch_map_glds
+  // scratch: [def_off copy | chunk clock maxima]
+  const size_t off_b = D > 0 ? ((G + 1) * sizeof(size_t) + 255) / 256 * 256 : 0;
+  if (glds) p.nch = (R + gC - 1) / gC;
+  const size_t cm_b = glds ? G * p.nch * A * sizeof(u64) : 0;
+  if (off_b + cm_b > 0)
+    if (int rc = ensure_scratch(ctx, off_b + cm_b)) return rc;
   if (D > 0) {
     // the kernel walks def_off on the device: stage it (the caller's array may be freed)
-    const size_t off_b = (G + 1) * sizeof(size_t);
-    if (int rc = ensure_scratch(ctx, off_b)) return rc;
-    if (int rc = stage_h2d(ctx, ctx->scratch, in->def_off, off_b)) return rc;
+    if (int rc = stage_h2d(ctx, ctx->scratch, in->def_off, (G + 1) * sizeof(size_t))) return rc;
     p.def_off = reinterpret_cast<const size_t *>(ctx->scratch);
     p.def_row = in->def_row;
     p.def_clock = (const u64 *)in->def_clock;
     p.def_keys = (const u64 *)in->def_keys;
   }
-  // LDS-DMA staging when every step image is whole 16-byte pieces (A even, 16-byte aligned
-  // rows and strides) and the state fits 4 values; register staging otherwise
-  const bool even = ((p.c_rs | p.c_gs | p.e_rs | p.e_gs | p.vc_rs | p.vc_gs) & 1) == 0;
-  const bool glds = ctx->tune.map_glds && R > 0 && A <= 64 && (A & 1) == 0 && (V == 1 || V == 2) &&
-                    want <= 4 && even && aligned16(p.clock) && aligned16(p.ec) && aligned16(p.vclk);
   const unsigned long long blocks = G * K;
   timing_begin(ctx, "map_fold");
   hipError_t he;
   if (glds) {
+    u64 *cm = reinterpret_cast<u64 *>(static_cast<char *>(ctx->scratch) + off_b);
+    p.cmax = cm;
+    hipLaunchKernelGGL(map_chunk_max_kernel, dim3((unsigned)(G * p.nch)), dim3(64), 0, ctx->stream, p.clock,
+                       p.c_rs, p.c_gs, (unsigned long long)R, (unsigned long long)A, p.nch, gC, cm);
     he = V == 1 ? launch_map_glds<1>(p, ctx->tune.map_chunk, ctx->tune.map_ring, blocks, ctx->stream)
                 : launch_map_glds<2>(p, ctx->tune.map_chunk, ctx->tune.map_ring, blocks, ctx->stream);
   } else {
