@@ -11,14 +11,17 @@
 
 namespace crdt {
 
-// One wave per row pair; lanes cover the row's words, 2 per lane (16-byte loads) when every
-// row starts 16-byte aligned and A is even, else 1.
+// Row groups: a wave covers 64 / LR rows at once, LR lanes per row (a power of two, chosen so
+// each lane moves ~8 pieces of its row: 16-byte pieces when every row starts 16-byte aligned
+// and A is even, else words).  All of a lane's loads are independent, so they are in flight
+// together; per-row reductions stay inside the LR-lane group (ballot bits / xor shuffles).
 struct PairPlan {
   u64 *out;
   const u64 *x, *y;
   unsigned long long N, A, os, xs, ys;
   int op;  // CRDT_PAIR_GLB / CRDT_PAIR_FORGET
   int vec2;
+  int lr_log;  // log2(LR)
 };
 
 __device__ __forceinline__ u64 pair_apply(int op, u64 a, u64 b) {
@@ -27,52 +30,75 @@ __device__ __forceinline__ u64 pair_apply(int op, u64 a, u64 b) {
   return op == CRDT_PAIR_GLB ? (a < b ? a : b) : (a > b ? a : 0);
 }
 
+// Wave-uniform row-group loop: every lane runs the same iterations (rows past N are masked),
+// so group-wide votes and shuffles see the whole wave.
+#define ROW_GROUP_LOOP(N, lr_log)                                                                  \
+  const int lane = threadIdx.x % kWave;                                                             \
+  const int LR = 1 << (lr_log);                                                                     \
+  const int gl = lane & (LR - 1);                                                                   \
+  const unsigned long long RW = kWave >> (lr_log);                                                  \
+  const unsigned long long w0 = (blockIdx.x * (unsigned long long)kBlock + threadIdx.x) / kWave;   \
+  const unsigned long long nw = (unsigned long long)gridDim.x * (kBlock / kWave);                   \
+  for (unsigned long long rb = w0 * RW; rb < (N); rb += nw * RW)
+
 __global__ __launch_bounds__(kBlock) void pair_op_kernel(PairPlan p) {
-  const int lane = threadIdx.x % kWave;
-  const unsigned long long w0 = (blockIdx.x * (unsigned long long)kBlock + threadIdx.x) / kWave;
-  const unsigned long long nw = (unsigned long long)gridDim.x * (kBlock / kWave);
-  for (unsigned long long r = w0; r < p.N; r += nw) {
+  ROW_GROUP_LOOP(p.N, p.lr_log) {
+    const unsigned long long r = rb + (lane >> p.lr_log);
+    if (r >= p.N) continue;
     const u64 *xr = p.x + r * p.xs, *yr = p.y + r * p.ys;
     u64 *orow = p.out + r * p.os;
     if (p.vec2) {
-      for (unsigned long long c = 2ull * lane; c < p.A; c += 2ull * kWave) {
+#pragma unroll 8
+      for (unsigned long long c = 2ull * gl; c < p.A; c += 2ull * LR) {
         const u64x2 a = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(xr + c));
         const u64x2 b = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(yr + c));
         u64x2 o;
         o.x = pair_apply(p.op, a.x, b.x);
         o.y = pair_apply(p.op, a.y, b.y);
-        *reinterpret_cast<u64x2 *>(orow + c) = o;
+        __builtin_nontemporal_store(o, reinterpret_cast<u64x2 *>(orow + c));
       }
     } else {
-      for (unsigned long long c = lane; c < p.A; c += kWave) orow[c] = pair_apply(p.op, xr[c], yr[c]);
+#pragma unroll 8
+      for (unsigned long long c = gl; c < p.A; c += LR) orow[c] = pair_apply(p.op, xr[c], yr[c]);
     }
   }
+}
+
+// Bits of the LR-lane groups of a wave: bit g*LR set iff every bit of group g is set in m.
+__device__ __forceinline__ u64 group_all(u64 m, int lr_log) {
+  for (int sh = 1; sh < (1 << lr_log); sh <<= 1) m &= m >> sh;
+  return m;
 }
 
 // partial_cmp of row pairs: Equal 0, Greater 1, Less -1, None 2 (vclock.rs:69-80: equal first,
 // then "every counter of other <= self's" = Greater, then the mirror = Less).
 __global__ __launch_bounds__(kBlock) void pair_cmp_kernel(PairPlan p, int8_t *res) {
-  const int lane = threadIdx.x % kWave;
-  const unsigned long long w0 = (blockIdx.x * (unsigned long long)kBlock + threadIdx.x) / kWave;
-  const unsigned long long nw = (unsigned long long)gridDim.x * (kBlock / kWave);
-  for (unsigned long long r = w0; r < p.N; r += nw) {
-    const u64 *xr = p.x + r * p.xs, *yr = p.y + r * p.ys;
+  ROW_GROUP_LOOP(p.N, p.lr_log) {
+    const unsigned long long r = rb + (lane >> p.lr_log);
+    const bool on = r < p.N;
+    const unsigned long long rr = on ? r : p.N - 1;
+    const u64 *xr = p.x + rr * p.xs, *yr = p.y + rr * p.ys;
     bool ge = true, le = true;
     if (p.vec2) {
-      for (unsigned long long c = 2ull * lane; c < p.A; c += 2ull * kWave) {
+#pragma unroll 8
+      for (unsigned long long c = 2ull * gl; c < p.A; c += 2ull * LR) {
         const u64x2 a = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(xr + c));
         const u64x2 b = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(yr + c));
         ge &= (a.x >= b.x) & (a.y >= b.y);
         le &= (a.x <= b.x) & (a.y <= b.y);
       }
     } else {
-      for (unsigned long long c = lane; c < p.A; c += kWave) {
+#pragma unroll 8
+      for (unsigned long long c = gl; c < p.A; c += LR) {
         ge &= xr[c] >= yr[c];
         le &= xr[c] <= yr[c];
       }
     }
-    const bool G = __ballot(!ge) == 0, L = __ballot(!le) == 0;
-    if (lane == 0) res[r] = (int8_t)(G && L ? 0 : (G ? 1 : (L ? -1 : 2)));
+    const u64 G = group_all(__ballot(ge), p.lr_log), L = group_all(__ballot(le), p.lr_log);
+    if (on && gl == 0) {
+      const bool g = (G >> lane) & 1, l = (L >> lane) & 1;
+      res[r] = (int8_t)(g && l ? 0 : (g ? 1 : (l ? -1 : 2)));
+    }
   }
 }
 
@@ -137,6 +163,7 @@ struct ReadPlan {
   int pn;  // 0: GCounter (A words), 1: PNCounter (P in [0, A), N in [A, 2A))
   u64 *out;  // [N][2] (lo, hi)
   int vec2;
+  int lr_log;
 };
 
 __device__ __forceinline__ void add128(u64 &lo, u64 &hi, u64 blo, u64 bhi) {
@@ -145,9 +172,9 @@ __device__ __forceinline__ void add128(u64 &lo, u64 &hi, u64 blo, u64 bhi) {
   lo = l;
 }
 
-__device__ __forceinline__ void wave_sum128(u64 &lo, u64 &hi) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
+// Sum over the aligned LR-lane group of each lane (xor offsets < LR stay inside the group).
+__device__ __forceinline__ void group_sum128(u64 &lo, u64 &hi, int LR) {
+  for (int off = LR >> 1; off >= 1; off >>= 1) {
     const u64 olo = __shfl_xor(lo, off, kWave);
     const u64 ohi = __shfl_xor(hi, off, kWave);
     add128(lo, hi, olo, ohi);
@@ -155,47 +182,59 @@ __device__ __forceinline__ void wave_sum128(u64 &lo, u64 &hi) {
 }
 
 __global__ __launch_bounds__(kBlock) void read_sum_kernel(ReadPlan p) {
-  const int lane = threadIdx.x % kWave;
-  const unsigned long long w0 = (blockIdx.x * (unsigned long long)kBlock + threadIdx.x) / kWave;
-  const unsigned long long nw = (unsigned long long)gridDim.x * (kBlock / kWave);
-  for (unsigned long long r = w0; r < p.N; r += nw) {
-    const u64 *row = p.in + r * p.rs;
+  ROW_GROUP_LOOP(p.N, p.lr_log) {
+    const unsigned long long r = rb + (lane >> p.lr_log);
+    const bool on = r < p.N;
+    const u64 *row = p.in + (on ? r : p.N - 1) * p.rs;
     u64 plo = 0, phi = 0, nlo = 0, nhi = 0;
     if (p.vec2) {  // 16-byte loads
-      for (unsigned long long c = 2ull * lane; c < p.A; c += 2ull * kWave) {
+#pragma unroll 8
+      for (unsigned long long c = 2ull * gl; c < p.A; c += 2ull * LR) {
         const u64x2 v = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(row + c));
         add128(plo, phi, v.x, 0);
         add128(plo, phi, v.y, 0);
-        if (p.pn) {
+      }
+      if (p.pn) {
+#pragma unroll 8
+        for (unsigned long long c = 2ull * gl; c < p.A; c += 2ull * LR) {
           const u64x2 w = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(row + p.A + c));
           add128(nlo, nhi, w.x, 0);
           add128(nlo, nhi, w.y, 0);
         }
       }
     } else {
-      for (unsigned long long c = lane; c < p.A; c += kWave) {
+#pragma unroll 8
+      for (unsigned long long c = gl; c < p.A; c += LR) {
         add128(plo, phi, __builtin_nontemporal_load(row + c), 0);
         if (p.pn) add128(nlo, nhi, __builtin_nontemporal_load(row + p.A + c), 0);
       }
     }
-    wave_sum128(plo, phi);
+    group_sum128(plo, phi, LR);
     if (p.pn) {
-      wave_sum128(nlo, nhi);
+      group_sum128(nlo, nhi, LR);
       // P - N = P + ~N + 1
       add128(plo, phi, ~nlo, ~nhi);
       add128(plo, phi, 1, 0);
     }
-    if (lane == 0) {
+    if (on && gl == 0) {
       p.out[2 * r] = plo;
       p.out[2 * r + 1] = phi;
     }
   }
 }
 
-static unsigned rows_grid(const crdt_ctx *ctx, unsigned long long N) {
-  // one wave per row, 4 waves per workgroup; enough workgroups to fill the chip
-  // (tune rows_wpc: workgroups per CU, default 8)
-  const unsigned long long want = (N + 3) / 4;
+// LR lanes per row (power of two, <= 64) so that each lane moves about 8 pieces of its row.
+static int row_lr_log(unsigned long long pieces) {
+  int lg = 0;
+  while (lg < 6 && (pieces + (1ull << lg) - 1) >> lg > 8) ++lg;
+  return lg;
+}
+
+static unsigned rows_grid(const crdt_ctx *ctx, unsigned long long N, int lr_log) {
+  // 64 / LR rows per wave, 4 waves per workgroup; enough workgroups to fill the chip
+  // (tune rows_wpc: workgroups per CU)
+  const unsigned long long rpb = 4ull * (kWave >> lr_log);
+  const unsigned long long want = (N + rpb - 1) / rpb;
   const unsigned long long cap = (unsigned long long)ctx->cu_count * ctx->tune.rows_blocks_per_cu;
   return (unsigned)(want < cap ? (want ? want : 1) : cap);
 }
@@ -216,8 +255,9 @@ extern "C" int crdt_vclock_pair_op(crdt_ctx *ctx, int op, uint64_t *out, const u
   CRDT_HIP(ctx, hipSetDevice(ctx->device));
   PairPlan p{(u64 *)out, (const u64 *)x, (const u64 *)y, N, A, out_stride, x_stride, y_stride, op, 0};
   p.vec2 = (A % 2 == 0) && ((out_stride | x_stride | y_stride) % 2 == 0) && al16(out) && al16(x) && al16(y);
+  p.lr_log = row_lr_log(p.vec2 ? A / 2 : A);
   timing_begin(ctx, "pair_op");
-  hipLaunchKernelGGL(pair_op_kernel, dim3(rows_grid(ctx, N)), dim3(kBlock), 0, ctx->stream, p);
+  hipLaunchKernelGGL(pair_op_kernel, dim3(rows_grid(ctx, N, p.lr_log)), dim3(kBlock), 0, ctx->stream, p);
   timing_end(ctx);
   CRDT_HIP(ctx, hipGetLastError());
   return CRDT_OK;
@@ -232,8 +272,9 @@ extern "C" int crdt_vclock_partial_cmp(crdt_ctx *ctx, const uint64_t *x, const u
   CRDT_HIP(ctx, hipSetDevice(ctx->device));
   PairPlan p{nullptr, (const u64 *)x, (const u64 *)y, N, A, 0, x_stride, y_stride, 0, 0};
   p.vec2 = (A % 2 == 0) && ((x_stride | y_stride) % 2 == 0) && al16(x) && al16(y);
+  p.lr_log = row_lr_log(p.vec2 ? A / 2 : A);
   timing_begin(ctx, "pair_cmp");
-  hipLaunchKernelGGL(pair_cmp_kernel, dim3(rows_grid(ctx, N)), dim3(kBlock), 0, ctx->stream, p, out);
+  hipLaunchKernelGGL(pair_cmp_kernel, dim3(rows_grid(ctx, N, p.lr_log)), dim3(kBlock), 0, ctx->stream, p, out);
   timing_end(ctx);
   CRDT_HIP(ctx, hipGetLastError());
   return CRDT_OK;
@@ -264,10 +305,11 @@ static int read_rows(crdt_ctx *ctx, int pn, const uint64_t *in, size_t N, size_t
   if (A > 0 && stride < (pn ? 2 : 1) * A) return fail(ctx, CRDT_EINVAL, "read: row stride too small");
   if (A >= (1ull << 62)) return fail(ctx, CRDT_EUNSUPPORTED, "read: A too large for 128-bit sums");
   CRDT_HIP(ctx, hipSetDevice(ctx->device));
-  ReadPlan p{(const u64 *)in, N, A, stride, pn, (u64 *)out, 0};
+  ReadPlan p{(const u64 *)in, N, A, stride, pn, (u64 *)out, 0, 0};
   p.vec2 = (A % 2 == 0) && (stride % 2 == 0) && al16(in);
+  p.lr_log = row_lr_log(p.vec2 ? A / 2 : A);
   timing_begin(ctx, "read_sum");
-  hipLaunchKernelGGL(read_sum_kernel, dim3(rows_grid(ctx, N)), dim3(kBlock), 0, ctx->stream, p);
+  hipLaunchKernelGGL(read_sum_kernel, dim3(rows_grid(ctx, N, p.lr_log)), dim3(kBlock), 0, ctx->stream, p);
   timing_end(ctx);
   CRDT_HIP(ctx, hipGetLastError());
   return CRDT_OK;
