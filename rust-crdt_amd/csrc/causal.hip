@@ -230,12 +230,17 @@ static int row_lr_log(unsigned long long pieces) {
   return lg;
 }
 
-static unsigned rows_grid(const crdt_ctx *ctx, unsigned long long N, int lr_log) {
+// Workgroups per CU measured on MI355X at 1M rows x 256 (scripts/bench_causal.py, CRDT_TUNE=rbpc):
+// two-read-one-write passes prefer few (2: 72% vs 16: 69%), partial_cmp 4 (84%), read many (32: 79%).
+constexpr int kRbpcPair = 2, kRbpcCmp = 4, kRbpcRead = 32;
+
+static unsigned rows_grid(const crdt_ctx *ctx, unsigned long long N, int lr_log, int bpc) {
   // 64 / LR rows per wave, 4 waves per workgroup; enough workgroups to fill the chip
   // (tune rows_wpc: workgroups per CU)
   const unsigned long long rpb = 4ull * (kWave >> lr_log);
   const unsigned long long want = (N + rpb - 1) / rpb;
-  const unsigned long long cap = (unsigned long long)ctx->cu_count * ctx->tune.rows_blocks_per_cu;
+  const unsigned long long cap =
+      (unsigned long long)ctx->cu_count * (ctx->tune.rows_blocks_per_cu > 0 ? ctx->tune.rows_blocks_per_cu : bpc);
   return (unsigned)(want < cap ? (want ? want : 1) : cap);
 }
 
@@ -257,7 +262,7 @@ extern "C" int crdt_vclock_pair_op(crdt_ctx *ctx, int op, uint64_t *out, const u
   p.vec2 = (A % 2 == 0) && ((out_stride | x_stride | y_stride) % 2 == 0) && al16(out) && al16(x) && al16(y);
   p.lr_log = row_lr_log(p.vec2 ? A / 2 : A);
   timing_begin(ctx, "pair_op");
-  hipLaunchKernelGGL(pair_op_kernel, dim3(rows_grid(ctx, N, p.lr_log)), dim3(kBlock), 0, ctx->stream, p);
+  hipLaunchKernelGGL(pair_op_kernel, dim3(rows_grid(ctx, N, p.lr_log, kRbpcPair)), dim3(kBlock), 0, ctx->stream, p);
   timing_end(ctx);
   CRDT_HIP(ctx, hipGetLastError());
   return CRDT_OK;
@@ -274,7 +279,7 @@ extern "C" int crdt_vclock_partial_cmp(crdt_ctx *ctx, const uint64_t *x, const u
   p.vec2 = (A % 2 == 0) && ((x_stride | y_stride) % 2 == 0) && al16(x) && al16(y);
   p.lr_log = row_lr_log(p.vec2 ? A / 2 : A);
   timing_begin(ctx, "pair_cmp");
-  hipLaunchKernelGGL(pair_cmp_kernel, dim3(rows_grid(ctx, N, p.lr_log)), dim3(kBlock), 0, ctx->stream, p, out);
+  hipLaunchKernelGGL(pair_cmp_kernel, dim3(rows_grid(ctx, N, p.lr_log, kRbpcCmp)), dim3(kBlock), 0, ctx->stream, p, out);
   timing_end(ctx);
   CRDT_HIP(ctx, hipGetLastError());
   return CRDT_OK;
@@ -309,7 +314,7 @@ static int read_rows(crdt_ctx *ctx, int pn, const uint64_t *in, size_t N, size_t
   p.vec2 = (A % 2 == 0) && (stride % 2 == 0) && al16(in);
   p.lr_log = row_lr_log(p.vec2 ? A / 2 : A);
   timing_begin(ctx, "read_sum");
-  hipLaunchKernelGGL(read_sum_kernel, dim3(rows_grid(ctx, N, p.lr_log)), dim3(kBlock), 0, ctx->stream, p);
+  hipLaunchKernelGGL(read_sum_kernel, dim3(rows_grid(ctx, N, p.lr_log, kRbpcRead)), dim3(kBlock), 0, ctx->stream, p);
   timing_end(ctx);
   CRDT_HIP(ctx, hipGetLastError());
   return CRDT_OK;

@@ -42,7 +42,7 @@ struct Tune {
   int map_chunk = 16;  // ... replicas per LDS chunk slot (8 or 16)
   int map_ring = 2;    // ... chunk slots in the ring (2-4)
   int map_spec = 1;    // ... speculative no-op scan
-  int rows_blocks_per_cu = 16;  // row-pair / row-reduction kernels (causal.hip)
+  int rows_blocks_per_cu = 0;  // row-pair / row-reduction kernels (causal.hip); 0 = per-kernel default
 };
 
 struct PendingTiming {
