@@ -30,17 +30,6 @@ __device__ __forceinline__ u64 pair_apply(int op, u64 a, u64 b) {
   return op == CRDT_PAIR_GLB ? (a < b ? a : b) : (a > b ? a : 0);
 }
 
-// Wave-uniform row-group loop: every lane runs the same iterations (rows past N are masked),
-// so group-wide votes and shuffles see the whole wave.
-#define ROW_GROUP_LOOP(N, lr_log)                                                                  \
-  const int lane = threadIdx.x % kWave;                                                             \
-  const int LR = 1 << (lr_log);                                                                     \
-  const int gl = lane & (LR - 1);                                                                   \
-  const unsigned long long RW = kWave >> (lr_log);                                                  \
-  const unsigned long long w0 = (blockIdx.x * (unsigned long long)kBlock + threadIdx.x) / kWave;   \
-  const unsigned long long nw = (unsigned long long)gridDim.x * (kBlock / kWave);                   \
-  for (unsigned long long rb = w0 * RW; rb < (N); rb += nw * RW)
-
 __global__ __launch_bounds__(kBlock) void pair_op_kernel(PairPlan p) {
   ROW_GROUP_LOOP(p.N, p.lr_log) {
     const unsigned long long r = rb + (lane >> p.lr_log);
@@ -223,13 +212,6 @@ __global__ __launch_bounds__(kBlock) void read_sum_kernel(ReadPlan p) {
   }
 }
 
-// LR lanes per row (power of two, <= 64) so that each lane moves about 8 pieces of its row.
-static int row_lr_log(unsigned long long pieces) {
-  int lg = 0;
-  while (lg < 6 && (pieces + (1ull << lg) - 1) >> lg > 8) ++lg;
-  return lg;
-}
-
 // Workgroups per CU measured on MI355X at 1M rows x 256 (scripts/bench_causal.py, CRDT_TUNE=rbpc):
 // two-read-one-write passes prefer few (2: 72% vs 16: 69%), partial_cmp 4 (84%), read many (32: 79%).
 constexpr int kRbpcPair = 2, kRbpcCmp = 4, kRbpcRead = 32;
@@ -256,7 +238,7 @@ extern "C" int crdt_vclock_pair_op(crdt_ctx *ctx, int op, uint64_t *out, const u
   if (op != CRDT_PAIR_GLB && op != CRDT_PAIR_FORGET) return fail(ctx, CRDT_EINVAL, "vclock_pair_op: op %d", op);
   if (N == 0 || A == 0) return CRDT_OK;
   if (!out || !x || !y) return fail(ctx, CRDT_EINVAL, "vclock_pair_op: NULL buffer");
-  if (out_stride < A || x_stride < A || y_stride < A) return fail(ctx, CRDT_EINVAL, "vclock_pair_op: stride < A");
+  if (N > 1 && (out_stride < A || x_stride < A || y_stride < A)) return fail(ctx, CRDT_EINVAL, "vclock_pair_op: stride < A");
   CRDT_HIP(ctx, hipSetDevice(ctx->device));
   PairPlan p{(u64 *)out, (const u64 *)x, (const u64 *)y, N, A, out_stride, x_stride, y_stride, op, 0};
   p.vec2 = (A % 2 == 0) && ((out_stride | x_stride | y_stride) % 2 == 0) && al16(out) && al16(x) && al16(y);
@@ -273,7 +255,7 @@ extern "C" int crdt_vclock_partial_cmp(crdt_ctx *ctx, const uint64_t *x, const u
   CRDT_CHECK_CTX(ctx);
   if (N == 0) return CRDT_OK;
   if (!out || (A > 0 && (!x || !y))) return fail(ctx, CRDT_EINVAL, "vclock_partial_cmp: NULL buffer");
-  if (A > 0 && (x_stride < A || y_stride < A)) return fail(ctx, CRDT_EINVAL, "vclock_partial_cmp: stride < A");
+  if (N > 1 && A > 0 && (x_stride < A || y_stride < A)) return fail(ctx, CRDT_EINVAL, "vclock_partial_cmp: stride < A");
   CRDT_HIP(ctx, hipSetDevice(ctx->device));
   PairPlan p{nullptr, (const u64 *)x, (const u64 *)y, N, A, 0, x_stride, y_stride, 0, 0};
   p.vec2 = (A % 2 == 0) && ((x_stride | y_stride) % 2 == 0) && al16(x) && al16(y);
@@ -307,7 +289,7 @@ static int read_rows(crdt_ctx *ctx, int pn, const uint64_t *in, size_t N, size_t
   CRDT_CHECK_CTX(ctx);
   if (N == 0) return CRDT_OK;
   if (!out || (A > 0 && !in)) return fail(ctx, CRDT_EINVAL, "read: NULL buffer");
-  if (A > 0 && stride < (pn ? 2 : 1) * A) return fail(ctx, CRDT_EINVAL, "read: row stride too small");
+  if (N > 1 && A > 0 && stride < (pn ? 2 : 1) * A) return fail(ctx, CRDT_EINVAL, "read: row stride too small");
   if (A >= (1ull << 62)) return fail(ctx, CRDT_EUNSUPPORTED, "read: A too large for 128-bit sums");
   CRDT_HIP(ctx, hipSetDevice(ctx->device));
   ReadPlan p{(const u64 *)in, N, A, stride, pn, (u64 *)out, 0, 0};

@@ -38,6 +38,7 @@ struct Tune {
   int orswot_blocks_per_cu = 2;
   int orswot_unroll = 1;
   int merge_blocks_per_cu = 2;
+  int merge_rows = 1;  // merge_batch of 16-byte rows by LR-lane row groups (0: merge_pairs_kernel)
   int map_glds = 1;    // Map fold: LDS-DMA staging where the shape allows it
   int map_chunk = 16;  // ... replicas per LDS chunk slot (8 or 16)
   int map_ring = 2;    // ... chunk slots in the ring (2-4)
@@ -137,6 +138,24 @@ int lattice_lub_many(crdt_ctx *ctx, Op op, const u64 *in, size_t G, size_t R, si
                      unsigned flags);
 int lattice_merge_batch(crdt_ctx *ctx, Op op, u64 *self, const u64 *other, size_t N, size_t W,
                         size_t self_stride, size_t other_stride);
+
+// Wave-uniform row-group loop: every lane runs the same iterations (rows past N are masked),
+// so group-wide votes and shuffles see the whole wave.
+#define ROW_GROUP_LOOP(N, lr_log)                                                                  \
+  const int lane = threadIdx.x % kWave;                                                             \
+  const int LR = 1 << (lr_log);                                                                     \
+  const int gl = lane & (LR - 1);                                                                   \
+  const unsigned long long RW = kWave >> (lr_log);                                                  \
+  const unsigned long long w0 = (blockIdx.x * (unsigned long long)kBlock + threadIdx.x) / kWave;   \
+  const unsigned long long nw = (unsigned long long)gridDim.x * (kBlock / kWave);                   \
+  for (unsigned long long rb = w0 * RW; rb < (N); rb += nw * RW)
+
+// LR lanes per row (power of two, <= 64) so that each lane moves about 8 pieces of its row.
+inline int row_lr_log(unsigned long long pieces) {
+  int lg = 0;
+  while (lg < 6 && (pieces + (1ull << lg) - 1) >> lg > 8) ++lg;
+  return lg;
+}
 
 }  // namespace crdt
 

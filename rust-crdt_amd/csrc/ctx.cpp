@@ -199,6 +199,7 @@ static void apply_tune(crdt_ctx *ctx, const char *t) {
       else if (k == "nt") ctx->tune.lub_nt = v != 0;
       else if (k == "grid" && v > 0) ctx->tune.lub_grid = v;
       else if (k == "mbpc" && v > 0) ctx->tune.merge_blocks_per_cu = v;
+      else if (k == "mrows" && (v == 0 || v == 1)) ctx->tune.merge_rows = v;
       else if (k == "obpc" && v > 0) ctx->tune.orswot_blocks_per_cu = v;
       else if (k == "ounroll" && (v == 1 || v == 2 || v == 4)) ctx->tune.orswot_unroll = v;
       else if (k == "mglds") ctx->tune.map_glds = v != 0;
