@@ -163,6 +163,50 @@ typedef struct crdt_orswot_out {
 
 int crdt_orswot_lub_many(crdt_ctx *ctx, const crdt_orswot_batch *in, crdt_orswot_out *out);
 
+/* Batched Orswot CmRDT::apply (orswot.rs:55-79 with apply_rm :230-250 and apply_deferred
+ * :281-286): state s < N applies its ops [op_off[s], op_off[s+1]) in order, in place.
+ * State layout (device): clock C[s][a] at clock + s*clock_stride + a; entries E[s][m][a] at
+ * entries + s*entry_sstride + m*entry_mstride + a (member absent <=> row all 0); the deferred
+ * list of state s has def_count[s] <= Dcap slots, slot d holding the rm clock
+ * def_clock[(s*Dcap + d)*A + a] and the member bitmap def_members[(s*Dcap + d)*Mw + w],
+ * Mw = ceil(M/64), clocks pairwise distinct (the reference's HashMap<VClock, HashSet<M>>).
+ * Ops (device): kind[o] 0 = Op::Add { dot: (actor[o], counter[o]), members },
+ * 1 = Op::Rm { clock: rm_clock[rm_row[o]*A ..], members }; members of op o are
+ * mem[mem_off[o] .. mem_off[o+1]) (u32 member indices, duplicates allowed).  op_off has N+1
+ * entries, mem_off n_ops+1.  actor/counter may be NULL if no op is an Add, rm_row/rm_clock if
+ * none is an Rm (n_rm_rows = rows of rm_clock).
+ * status[s] (device u32, written for every s): bit 0 = the deferred list needed more than Dcap
+ * slots (the state is incomplete: retry with a larger Dcap), bit 1 = an op named an actor,
+ * member or rm row out of range or a bad kind / member range (that op, or its bad members, were
+ * skipped), bit 2 = def_count[s] > Dcap on input, bit 3 = op_off[s..s+1] invalid (bits 2 and 3:
+ * state left untouched).  Limits: A <= 256, Dcap*(A + Mw)*8 <= 65536. */
+typedef struct crdt_orswot_states {
+  size_t N, M, A, Dcap;
+  uint64_t *clock;
+  size_t clock_stride;
+  uint64_t *entries;
+  size_t entry_mstride, entry_sstride;
+  uint64_t *def_clock;   /* [N][Dcap][A]  */
+  uint64_t *def_members; /* [N][Dcap][Mw] */
+  uint32_t *def_count;   /* [N]           */
+} crdt_orswot_states;
+
+typedef struct crdt_orswot_ops {
+  size_t n_ops;
+  const uint64_t *op_off; /* [N+1]     */
+  const uint8_t *kind;    /* [n_ops]   */
+  const uint32_t *actor;  /* [n_ops]   */
+  const uint64_t *counter; /* [n_ops]  */
+  const uint32_t *rm_row; /* [n_ops]   */
+  const uint64_t *rm_clock; /* [n_rm_rows][A] */
+  size_t n_rm_rows;
+  const uint64_t *mem_off; /* [n_ops+1] */
+  const uint32_t *mem;
+} crdt_orswot_ops;
+
+int crdt_orswot_apply_batch(crdt_ctx *ctx, const crdt_orswot_states *states, const crdt_orswot_ops *ops,
+                            uint32_t *status);
+
 /* ---- Map<K, MVReg<u64, A>, A> --------------------------------------------------------------
  * Replaces Map::merge (map.rs:140-220) with V = MVReg (MVReg::merge mvreg.rs:112-128,
  * MVReg::forget :88-104), incl. apply_keyset_rm (map.rs:318-348) and apply_deferred (:311-316),

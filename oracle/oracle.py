@@ -733,6 +733,8 @@ def lib():
         L.oracle_map_fold.argtypes = [P, P, P, P, S, S, S, S, P, P, P, S, P, P, P, P, P, P, P, S,
                                       ctypes.POINTER(S), P]
         L.oracle_map_fold.restype = ctypes.c_double
+        L.oracle_orswot_apply_streams.argtypes = [S, S, S, P, P, P, P, P, P, P, P, P, P, P]
+        L.oracle_orswot_apply_streams.restype = ctypes.c_double
         _LIB = L
     return _LIB
 
@@ -818,6 +820,21 @@ def orswot_fold(clock: np.ndarray, entries: np.ndarray, def_off=None, def_clock=
     return oc, oe, deferred, t
 
 
+def orswot_apply_streams(N: int, M: int, A: int, op_off, kind, actor, counter, rm_row, rm_clock, mem_off, mem):
+    """C++ twin: every state applies its op stream from Orswot::new() (orswot.rs:55-79) over
+    std containers.  Arrays in the crdt_orswot_ops layout (numpy).  Returns
+    (clock (N, A), entries (N, M, A), ndef (N,), apply seconds)."""
+    out_c = np.zeros((N, A), np.uint64)
+    out_e = np.zeros((N, M, A), np.uint64)
+    ndef = np.zeros(N, np.uint64)
+    arrs = [np.ascontiguousarray(op_off, np.uint64), np.ascontiguousarray(kind, np.uint8),
+            np.ascontiguousarray(actor, np.uint32), np.ascontiguousarray(counter, np.uint64),
+            np.ascontiguousarray(rm_row, np.uint32), np.ascontiguousarray(rm_clock, np.uint64),
+            np.ascontiguousarray(mem_off, np.uint64), np.ascontiguousarray(mem, np.uint32)]
+    t = lib().oracle_orswot_apply_streams(N, M, A, *[_p(a) for a in arrs], _p(out_c), _p(out_e), _p(ndef))
+    return out_c, out_e, ndef, t
+
+
 def bitmap_members(words: np.ndarray) -> frozenset:
     out = []
     for w, x in enumerate(np.asarray(words, dtype=np.uint64).tolist()):
@@ -895,6 +912,72 @@ def dense_orswot_join_fold(clock: np.ndarray, entries: np.ndarray):
         e = np.maximum(t0, np.maximum(t1, t2)).astype(np.uint64)
         c = np.maximum(c, c2)
     return c, e
+
+
+def dense_orswot_apply(clock, entries, dcl, dmb, cnt, ops):
+    """Dense restatement of one state's Orswot CmRDT::apply stream — the algorithm
+    crdt_orswot_apply_batch runs per wave (orswot.rs:55-79, apply_rm :230-250, apply_deferred
+    :281-286), checked against Orswot.apply by tests/test_oracle_orswot_apply.py.
+    clock (A,), entries (M, A), dcl (Dcap, A), dmb (Dcap, Mw) are updated in place; ops are
+    ("add", a, k, members) / ("rm", dense rm row, members).  Returns (deferred count, status)."""
+    A = clock.shape[0]
+    M = entries.shape[0]
+    Dcap = dcl.shape[0]
+    st = 0
+
+    def forget(m, rm):  # VClock::forget vclock.rs:95-105 on a dense row
+        row = entries[m]
+        row[(row != 0) & (row <= rm)] = 0
+
+    def members_of(bits):
+        return [m for m in bitmap_members(bits) if m < M]
+
+    for op in ops:
+        if op[0] == "add":
+            _, a, k, ms = op
+            if a >= A:
+                st |= 2
+                continue
+            if clock[a] >= np.uint64(k):  # :60-63
+                continue
+            for m in ms:  # :65-68
+                if m >= M:
+                    st |= 2
+                    continue
+                entries[m, a] = max(entries[m, a], np.uint64(k))
+            clock[a] = np.uint64(k)  # :70
+            nk = 0  # apply_deferred :281-286
+            for d in range(cnt):
+                rm = dcl[d].copy()
+                for m in members_of(dmb[d]):
+                    forget(m, rm)
+                if (rm > clock).any():
+                    dcl[nk], dmb[nk] = rm, dmb[d].copy()
+                    nk += 1
+            cnt = nk
+        else:
+            _, rm, ms = op
+            rm = np.asarray(rm, dtype=np.uint64)
+            for m in ms:  # :231-238
+                if m >= M:
+                    st |= 2
+                    continue
+                forget(m, rm)
+            if not (rm > clock).any():  # :239-249, rm <= clock: already seen
+                continue
+            slot = next((d for d in range(cnt) if np.array_equal(dcl[d], rm)), -1)
+            if slot < 0:
+                if cnt >= Dcap:
+                    st |= 1
+                    continue
+                slot = cnt
+                cnt += 1
+                dcl[slot] = rm
+                dmb[slot] = 0
+            for m in ms:
+                if m < M:
+                    dmb[slot, m // 64] |= np.uint64(1) << np.uint64(m % 64)
+    return cnt, st
 
 
 def dense_orswot_lub(clock, entries, def_clock, def_members):

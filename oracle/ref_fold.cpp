@@ -129,6 +129,12 @@ struct Orswot {
     deferred.clear();
     for (auto &kv : d) apply_rm(kv.second, kv.first);
   }
+  void apply_add(Actor a, u64 counter, const std::set<Member> &members) {  // orswot.rs:59-72
+    if (clock.get(a) >= counter) return;  // we've already seen this op
+    for (Member m : members) entries[m].apply_dot(a, counter);
+    clock.apply_dot(a, counter);
+    apply_deferred();
+  }
   void merge(Orswot &&other) {  // orswot.rs:81-149
     // :84-106 rebuild self.entries
     std::unordered_map<Member, VClock> kept;
@@ -458,6 +464,47 @@ double oracle_orswot_fold(const uint64_t *clock, const uint64_t *entries, size_t
     ++k;
   }
   *out_ndef = k;
+  return t1 - t0;
+}
+
+// ---- Orswot CmRDT::apply streams (orswot.rs:55-79) from Orswot::new() -----------------------
+// State s applies ops [op_off[s], op_off[s+1]): kind 0 = Op::Add { dot (actor, counter) },
+// 1 = Op::Rm { clock rm_clock[rm_row*A..] }, members mem[mem_off[o]..mem_off[o+1]) (the layout
+// of crdt_orswot_ops).  Output per state: clock[s*A..], entries[(s*M + m)*A..] and the number of
+// deferred removes ndef[s].  Returns apply seconds (op ingest into sets / maps excluded).
+double oracle_orswot_apply_streams(size_t N, size_t M, size_t A, const uint64_t *op_off, const uint8_t *kind,
+                                   const uint32_t *actor, const uint64_t *counter, const uint32_t *rm_row,
+                                   const uint64_t *rm_clock, const uint64_t *mem_off, const uint32_t *mem,
+                                   uint64_t *out_clock, uint64_t *out_entries, uint64_t *out_ndef) {
+  struct OpIn {
+    int kind;
+    Actor a;
+    u64 k;
+    VClock rm;
+    std::set<Member> ms;
+  };
+  std::vector<std::vector<OpIn>> streams(N);
+  for (size_t s = 0; s < N; ++s)
+    for (uint64_t o = op_off[s]; o < op_off[s + 1]; ++o) {
+      OpIn op{kind[o], actor ? actor[o] : 0, counter ? counter[o] : 0, {}, {}};
+      if (op.kind == 1) op.rm = vclock_from_row(rm_clock + (size_t)rm_row[o] * A, A);
+      for (uint64_t j = mem_off[o]; j < mem_off[o + 1]; ++j) op.ms.insert(mem[j]);
+      streams[s].push_back(std::move(op));
+    }
+  std::vector<Orswot> st(N);
+  double t0 = now_s();
+  for (size_t s = 0; s < N; ++s)
+    for (auto &op : streams[s]) {
+      if (op.kind == 0) st[s].apply_add(op.a, op.k, op.ms);
+      else st[s].apply_rm(std::move(op.ms), std::move(op.rm));  // orswot.rs:74-76
+    }
+  double t1 = now_s();
+  for (size_t s = 0; s < N; ++s) {
+    vclock_to_row(st[s].clock, out_clock + s * A, A);
+    std::memset(out_entries + s * M * A, 0, M * A * 8);
+    for (auto &kv : st[s].entries) vclock_to_row(kv.second, out_entries + (s * M + kv.first) * A, A);
+    out_ndef[s] = st[s].deferred.size();
+  }
   return t1 - t0;
 }
 

@@ -28,7 +28,7 @@ EXPORTS = (
     "crdt_pncounter_lub_many", "crdt_pncounter_merge_batch",
     "crdt_gset_lub_many", "crdt_gset_merge_batch",
     "crdt_lwwreg_lub_many", "crdt_lwwreg_merge_batch",
-    "crdt_orswot_lub_many", "crdt_map_lub_many",
+    "crdt_orswot_lub_many", "crdt_orswot_apply_batch", "crdt_map_lub_many",
     "crdt_vclock_pair_op", "crdt_vclock_partial_cmp", "crdt_vclock_cmp_matrix", "crdt_gcounter_read",
     "crdt_pncounter_read", "crdt_vclock_apply_batch", "crdt_gcounter_apply_batch",
     "crdt_pncounter_apply_batch", "crdt_gset_apply_batch",
@@ -66,6 +66,21 @@ class OrswotOut(ctypes.Structure):
     _fields_ = [("clock", P), ("entries", P), ("def_keep", P), ("def_members", P)]
 
 
+class OrswotStates(ctypes.Structure):  # crdt_orswot_states
+    _fields_ = [
+        ("N", S), ("M", S), ("A", S), ("Dcap", S),
+        ("clock", P), ("clock_stride", S), ("entries", P), ("entry_mstride", S), ("entry_sstride", S),
+        ("def_clock", P), ("def_members", P), ("def_count", P),
+    ]
+
+
+class OrswotOps(ctypes.Structure):  # crdt_orswot_ops
+    _fields_ = [
+        ("n_ops", S), ("op_off", P), ("kind", P), ("actor", P), ("counter", P), ("rm_row", P),
+        ("rm_clock", P), ("n_rm_rows", S), ("mem_off", P), ("mem", P),
+    ]
+
+
 class MapBatch(ctypes.Structure):  # crdt_map_batch
     _fields_ = [
         ("G", S), ("R", S), ("K", S), ("A", S), ("V", S),
@@ -101,6 +116,7 @@ _SIGS = {
     "crdt_lwwreg_lub_many": ([P, P, P, S, S, S, P, P, P, ctypes.c_uint], ctypes.c_int),
     "crdt_lwwreg_merge_batch": ([P, P, P, P, P, S, P], ctypes.c_int),
     "crdt_orswot_lub_many": ([P, ctypes.POINTER(OrswotBatch), ctypes.POINTER(OrswotOut)], ctypes.c_int),
+    "crdt_orswot_apply_batch": ([P, ctypes.POINTER(OrswotStates), ctypes.POINTER(OrswotOps), P], ctypes.c_int),
     "crdt_map_lub_many": ([P, ctypes.POINTER(MapBatch), ctypes.POINTER(MapOut)], ctypes.c_int),
     "crdt_vclock_pair_op": ([P, ctypes.c_int, P, P, P, S, S, S, S, S], ctypes.c_int),
     "crdt_vclock_partial_cmp": ([P, P, P, S, S, S, S, P], ctypes.c_int),

@@ -109,3 +109,131 @@ def deferred_set(def_clock: torch.Tensor, def_keep: torch.Tensor, def_members: t
                     x &= x - 1
             out.add((tuple(int(v) for v in clocks[d]), frozenset(ms)))
     return out
+
+
+# ---------------------------------------------------------------------------------------------
+# Batched CmRDT::apply (orswot.rs:55-79, apply_rm :230-250, apply_deferred :281-286)
+# ---------------------------------------------------------------------------------------------
+class OrswotOpBatch(NamedTuple):
+    """Device op streams (crdt_orswot_ops): state s applies ops [op_off[s], op_off[s+1]) in order."""
+    op_off: torch.Tensor   # (N+1,) int64
+    kind: torch.Tensor     # (n_ops,) uint8: 0 = Op::Add, 1 = Op::Rm
+    actor: torch.Tensor    # (n_ops,) int32  (Add: dot.actor)
+    counter: torch.Tensor  # (n_ops,) int64  (Add: dot.counter, u64 bits)
+    rm_row: torch.Tensor   # (n_ops,) int32  (Rm: row of rm_clock)
+    rm_clock: torch.Tensor  # (n_rm, A) int64
+    mem_off: torch.Tensor  # (n_ops+1,) int64
+    mem: torch.Tensor      # (n_mem,) int32 member indices
+
+
+def encode_ops(streams, A: int, device) -> OrswotOpBatch:
+    """Host ingest of per-state op streams (already interned to dense indices).
+
+    streams[s] is a sequence of ops, each ("add", actor, counter, members) for
+    Op::Add { dot: Dot { actor, counter }, members } or ("rm", clock, members) for
+    Op::Rm { clock, members }, with `clock` a mapping actor -> counter or a dense row of A
+    counters and `members` an iterable of member indices (orswot.rs:33-46)."""
+    op_off, kind, actor, counter, rm_row, mem_off, mem, rm_rows = [0], [], [], [], [], [0], [], []
+    for ops in streams:
+        for op in ops:
+            if op[0] == "add":
+                _, a, k, ms = op
+                kind.append(0)
+                actor.append(int(a))
+                counter.append(int(k))
+                rm_row.append(0)
+            elif op[0] == "rm":
+                _, clk, ms = op
+                row = np.zeros(A, dtype=np.uint64)
+                if hasattr(clk, "items"):
+                    for a, k in clk.items():
+                        row[int(a)] = np.uint64(k)
+                else:
+                    row[:] = np.asarray(clk, dtype=np.uint64)
+                kind.append(1)
+                actor.append(0)
+                counter.append(0)
+                rm_row.append(len(rm_rows))
+                rm_rows.append(row)
+            else:
+                raise ValueError(f"orswot.encode_ops: unknown op {op[0]!r}")
+            ms = [int(m) for m in ms]
+            mem.extend(ms)
+            mem_off.append(len(mem))
+        op_off.append(len(kind))
+
+    def t(x, dt):
+        return torch.from_numpy(np.asarray(x, dtype=dt)).to(device)
+
+    n_rm = len(rm_rows)
+    rm_rows.append(np.zeros(A, dtype=np.uint64))  # pads: never-empty device buffers (rm_clock, mem)
+    mem.append(0)
+    rc = np.array(rm_rows, dtype=np.uint64).reshape(n_rm + 1, A)
+    return OrswotOpBatch(
+        t(op_off, np.int64), t(kind, np.uint8), t(actor, np.int32),
+        t(np.array(counter, dtype=np.uint64).view(np.int64), np.int64), t(rm_row, np.int32),
+        torch.from_numpy(rc.view(np.int64)).to(device), t(mem_off, np.int64), t(mem, np.int32))
+
+
+def apply_batch(clock: torch.Tensor, entries: torch.Tensor, def_clock: torch.Tensor, def_members: torch.Tensor,
+                def_count: torch.Tensor, ops: OrswotOpBatch, ctx: Optional[Context] = None) -> torch.Tensor:
+    """Apply every state's op stream in place (clock (N, A), entries (N, M, A), deferred slots
+    def_clock (N, Dcap, A) / def_members (N, Dcap, ceil(M/64)) / def_count (N,) int32).
+    Returns the per-state status (N,) int32 tensor (include/crdt_gpu.h: bit 0 = deferred
+    capacity exceeded, bit 1 = out-of-range op skipped, bits 2-3 = invalid input, state untouched)."""
+    ctx = ctx or Context.default(clock.device.index)
+    for t, nm in ((clock, "clock"), (entries, "entries"), (def_clock, "def_clock"), (def_members, "def_members")):
+        ctx.check_tensor(t, f"orswot.apply_batch({nm})")
+    if clock.dim() != 2 or entries.dim() != 3 or def_clock.dim() != 3 or def_members.dim() != 3:
+        raise ValueError("orswot.apply_batch: clock (N,A), entries (N,M,A), def_clock (N,Dcap,A), "
+                         "def_members (N,Dcap,Mw) expected")
+    N, A = clock.shape
+    M = entries.shape[1]
+    Mw = (M + 63) // 64
+    Dcap = def_clock.shape[1]
+    if (entries.shape[0] != N or entries.shape[2] != A or clock.stride(1) != 1 or entries.stride(2) != 1
+            or entries.stride(0) < M * entries.stride(1)):
+        raise ValueError(f"orswot.apply_batch: entries {tuple(entries.shape)} / clock {tuple(clock.shape)} mismatch")
+    if (tuple(def_clock.shape) != (N, Dcap, A) or tuple(def_members.shape) != (N, Dcap, Mw)
+            or not def_clock.is_contiguous() or not def_members.is_contiguous()):
+        raise ValueError("orswot.apply_batch: def_clock / def_members must be contiguous (N, Dcap, A) / (N, Dcap, Mw)")
+    if def_count.dtype not in (torch.int32, torch.uint32) or tuple(def_count.shape) != (N,):
+        raise ValueError("orswot.apply_batch: def_count must be an (N,) int32 tensor")
+    if ops.op_off.shape[0] != N + 1:
+        raise ValueError(f"orswot.apply_batch: op_off has {ops.op_off.shape[0]} entries, expected {N + 1}")
+    want = {"op_off": (torch.int64, torch.uint64), "kind": (torch.uint8,), "actor": (torch.int32, torch.uint32),
+            "counter": (torch.int64, torch.uint64), "rm_row": (torch.int32, torch.uint32),
+            "rm_clock": (torch.int64, torch.uint64), "mem_off": (torch.int64, torch.uint64),
+            "mem": (torch.int32, torch.uint32)}
+    for nm, t in list(zip(ops._fields, ops)) + [("def_count", def_count)]:
+        dts = want.get(nm, (torch.int32, torch.uint32))
+        if t.device.type != "cuda" or t.device.index != ctx.device:
+            raise ValueError(f"orswot.apply_batch({nm}): expected a cuda:{ctx.device} tensor")
+        if t.dtype not in dts or not t.is_contiguous():
+            raise ValueError(f"orswot.apply_batch({nm}): expected a contiguous tensor of {dts}")
+    if ops.mem_off.shape[0] < ops.kind.shape[0] + 1 or ops.rm_clock.dim() != 2 or ops.rm_clock.shape[1] != A:
+        raise ValueError("orswot.apply_batch: mem_off needs n_ops+1 entries, rm_clock (n_rm, A)")
+    for nm in ("actor", "counter", "rm_row"):
+        if getattr(ops, nm).shape[0] != ops.kind.shape[0]:
+            raise ValueError(f"orswot.apply_batch: ops.{nm} must have n_ops entries")
+    st = _abi.OrswotStates()
+    st.N, st.M, st.A, st.Dcap = N, M, A, Dcap
+    st.clock, st.clock_stride = clock.data_ptr(), clock.stride(0)
+    st.entries, st.entry_mstride, st.entry_sstride = entries.data_ptr(), entries.stride(1), entries.stride(0)
+    st.def_clock, st.def_members, st.def_count = def_clock.data_ptr(), def_members.data_ptr(), def_count.data_ptr()
+    o = _abi.OrswotOps()
+    o.n_ops = ops.kind.shape[0]
+    o.op_off, o.kind, o.actor, o.counter = (ops.op_off.data_ptr(), ops.kind.data_ptr(), ops.actor.data_ptr(),
+                                            ops.counter.data_ptr())
+    o.rm_row, o.rm_clock, o.n_rm_rows = ops.rm_row.data_ptr(), ops.rm_clock.data_ptr(), ops.rm_clock.shape[0]
+    o.mem_off, o.mem = ops.mem_off.data_ptr(), ops.mem.data_ptr()
+    status = torch.empty(N, dtype=torch.int32, device=clock.device)
+    ctx.call("crdt_orswot_apply_batch", ctypes.byref(st), ctypes.byref(o), dptr(status))
+    return status
+
+
+def deferred_slots(def_clock: torch.Tensor, def_members: torch.Tensor, def_count: torch.Tensor, s: int) -> set:
+    """Egress of state s's deferred list to {(rm clock tuple, frozenset of members)}."""
+    n = int(def_count[s].item())
+    keep = torch.ones(n, dtype=torch.uint8)
+    return deferred_set(def_clock[s, :n], keep, def_members[s, :n])

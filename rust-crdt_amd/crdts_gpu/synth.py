@@ -171,3 +171,41 @@ def map_replicas(ctx: Optional[Context], R: int, K: int, A: int, V: int, seed: i
     torch.cuda.current_stream(dev).synchronize()
     drow = torch.from_numpy(rows.astype(np.int32)).to(dev)
     return MapInput(clock, ec, vclk, vval, [0, D], drow, dcl, dk)
+
+
+def orswot_op_streams(N: int, T: int, M: int, A: int, seed: int, p_rm: float = 0.2, p_future: float = 0.3,
+                      rm_actors: int = 4, device="cuda"):
+    """T ops per state for N states (an orswot.OrswotOpBatch, generated on `device` with torch's
+    RNG): Op::Add of one member with the next dot of a random actor (the per-state count of
+    that actor's adds so far, so every add is new), or w.p. p_rm an Op::Rm of one member whose
+    clock keeps ~rm_actors actors of the state's clock at that point, with w.p. p_future one
+    actor bumped past it (a remove from the future: deferred until that actor's next add)."""
+    from .orswot import OrswotOpBatch
+
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    n = N * T
+    kind = (torch.rand((N, T), generator=g, device=device) < p_rm).to(torch.uint8)
+    actor = torch.randint(0, A, (N, T), generator=g, device=device, dtype=torch.int64)
+    onehot = torch.zeros((N, T, A), dtype=torch.int64, device=device)
+    onehot.scatter_(2, actor.unsqueeze(2), (kind == 0).to(torch.int64).unsqueeze(2))
+    cum = onehot.cumsum(1)  # adds of each actor up to and including op t
+    del onehot
+    counter = torch.gather(cum, 2, actor.unsqueeze(2)).squeeze(2)
+    keep = torch.rand((N, T, A), generator=g, device=device) < (rm_actors / A)
+    rm = torch.where(keep, cum, torch.zeros((), dtype=torch.int64, device=device))
+    fut = (torch.rand((N, T), generator=g, device=device) < p_future).to(torch.int64)
+    bump = torch.randint(0, A, (N, T, 1), generator=g, device=device)
+    rm.scatter_add_(2, bump, fut.unsqueeze(2) * (1 + torch.gather(cum, 2, bump).squeeze(2) - torch.gather(
+        rm, 2, bump).squeeze(2)).unsqueeze(2))
+    del cum, keep
+    member = torch.randint(0, M, (n,), generator=g, device=device, dtype=torch.int32)
+    return OrswotOpBatch(
+        op_off=torch.arange(N + 1, device=device, dtype=torch.int64) * T,
+        kind=kind.reshape(n).contiguous(),
+        actor=actor.reshape(n).to(torch.int32),
+        counter=counter.reshape(n).contiguous(),
+        rm_row=torch.arange(n, device=device, dtype=torch.int32),
+        rm_clock=rm.reshape(n, A).contiguous(),
+        mem_off=torch.arange(n + 1, device=device, dtype=torch.int64),
+        mem=member)

@@ -1,0 +1,330 @@
+// Batched Orswot CmRDT::apply: N independent states, each with its own ordered op stream
+// (the order-dependent half of the kept trait surface).
+//
+// Reference (orswot.rs:55-79, 230-250, 281-286), restated on the dense layout
+// (clock C[a], entries E[m][a] with a 0 cell = actor absent, deferred list of (rm clock, member
+// set) with pairwise-distinct clocks):
+//   Op::Add { dot (a, k), members }:
+//       if C[a] >= k: seen, no-op                                          (:60-63)
+//       for m in members: E[m][a] = max(E[m][a], k)     (entry().or_default().apply(dot), :65-68)
+//       C[a] = k                                                           (:70)
+//       apply_deferred(): every deferred (rm, S) is re-applied: forget E[m] by rm for m in S,
+//           kept iff !(rm <= C); no two kept clocks are equal, so no sets merge   (:71, :281-286)
+//   Op::Rm { clock rm, members }:  apply_rm                                (:74-76, :230-250)
+//       for m in members: E[m][a] = E[m][a] > rm[a] ? E[m][a] : 0   (VClock::forget, vclock.rs:95-105;
+//                                                   an all-zero row is the removed entry)
+//       if !(rm <= C) (partial_cmp in {None, Greater}): defer (rm, members), OR-ing the set into
+//       an existing deferred with the identical clock (HashMap keyed by the whole VClock)
+// Ops of one state are sequential (apply is not commutative: the seen test and the deferred
+// removes depend on order), so the unit of parallelism is the state: one wave per state, lanes
+// over actors (clock rows in registers, A <= 256) or over the op's member list.  The op headers
+// of 64 ops are loaded at once (lane = op) and read out with readlane; the deferred list lives in
+// LDS for the whole stream.  Exact for ANY input state (apply_deferred re-forgets every deferred
+// member row, as the reference does, instead of assuming the invariant the reference's own
+// states keep).
+#include "common.hpp"
+
+namespace crdt {
+
+constexpr int kApplyMaxA = 256;
+constexpr int kCA = kApplyMaxA / kWave;  // clock words per lane
+
+struct OrswotApplyPlan {
+  u64 *clock;
+  unsigned long long clock_stride;
+  u64 *entries;
+  unsigned long long entry_mstride, entry_sstride;
+  u64 *def_clock, *def_members;
+  uint32_t *def_count;
+  unsigned long long N, M, A, Mw, Dcap;
+  const u64 *op_off;
+  const uint8_t *kind;
+  const uint32_t *actor;
+  const u64 *counter;
+  const uint32_t *rm_row;
+  const u64 *rm_clock;
+  unsigned long long n_rm_rows;
+  const u64 *mem_off;
+  const uint32_t *mem;
+  unsigned long long n_ops;
+  uint32_t *status;
+  int wpb;
+};
+
+__device__ __forceinline__ u64 rl64(u64 x, int l) {
+  const unsigned lo = __builtin_amdgcn_readlane((int)(unsigned)x, l);
+  const unsigned hi = __builtin_amdgcn_readlane((int)(unsigned)(x >> 32), l);
+  return ((u64)hi << 32) | lo;
+}
+__device__ __forceinline__ unsigned rl32(unsigned x, int l) {
+  return (unsigned)__builtin_amdgcn_readlane((int)x, l);
+}
+
+__device__ __forceinline__ void wave_fence() {
+  // Stores of this wave (global and LDS) are complete and visible to its later loads (all lanes of
+  // a workgroup share the CU's L1, so workgroup scope is enough).
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+}
+
+// forget one entry row by the clock held in registers: keep e[a] iff e[a] > rm[a]
+__device__ __forceinline__ void forget_row(u64 *row, const u64 (&r)[kCA], int lane, unsigned long long A) {
+#pragma unroll
+  for (int j = 0; j < kCA; ++j) {
+    const unsigned long long a = lane + j * kWave;
+    if (a < A) {
+      const u64 v = row[a];
+      if (v != 0 && v <= r[j]) row[a] = 0;
+    }
+  }
+}
+
+// forget every member row named in an LDS bitmap of Mw words
+__device__ __forceinline__ void forget_members(const OrswotApplyPlan &p, u64 *E, const u64 *bits,
+                                               const u64 (&r)[kCA], int lane) {
+  for (unsigned long long w0 = 0; w0 < p.Mw; w0 += kWave) {
+    const u64 word = (w0 + lane < p.Mw) ? bits[w0 + lane] : 0;
+    u64 nz = __ballot(word != 0);
+    while (nz) {
+      const int l = __builtin_ctzll(nz);
+      nz &= nz - 1;
+      u64 wv = rl64(word, l);
+      while (wv) {
+        const unsigned long long m = (w0 + l) * 64 + __builtin_ctzll(wv);
+        wv &= wv - 1;
+        if (m < p.M) forget_row(E + m * p.entry_mstride, r, lane, p.A);
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ bool any_greater(const u64 (&r)[kCA], const u64 (&c)[kCA], int lane,
+                                            unsigned long long A) {
+  bool g = false;
+#pragma unroll
+  for (int j = 0; j < kCA; ++j)
+    if (lane + j * kWave < (int)A && r[j] > c[j]) g = true;
+  return __ballot(g) != 0;
+}
+
+__global__ __launch_bounds__(kBlock) void orswot_apply_kernel(OrswotApplyPlan p) {
+  extern __shared__ u64 lds[];
+  const int lane = threadIdx.x % kWave;
+  const int wib = threadIdx.x / kWave;
+  const unsigned long long per_wave = p.Dcap * (p.A + p.Mw);
+  u64 *dcl = lds + wib * per_wave;  // [Dcap][A] rm clocks
+  u64 *dmb = dcl + p.Dcap * p.A;    // [Dcap][Mw] member bitmaps
+  const unsigned long long A = p.A;
+
+  for (unsigned long long s = (unsigned long long)blockIdx.x * p.wpb + wib; s < p.N;
+       s += (unsigned long long)gridDim.x * p.wpb) {
+    unsigned st = 0;
+    const unsigned long long ob = p.op_off[s], oe = p.op_off[s + 1];
+    unsigned dcnt = p.def_count[s];
+    if (dcnt > p.Dcap || oe < ob || oe > p.n_ops) {
+      if (lane == 0) p.status[s] = (dcnt > p.Dcap ? 4u : 0u) | (oe < ob || oe > p.n_ops ? 8u : 0u);
+      continue;  // state left untouched
+    }
+    u64 c[kCA];
+    u64 *C = p.clock + s * p.clock_stride;
+#pragma unroll
+    for (int j = 0; j < kCA; ++j) {
+      const unsigned long long a = lane + j * kWave;
+      c[j] = a < A ? C[a] : 0;
+    }
+    u64 *E = p.entries + s * p.entry_sstride;
+    const u64 *gdc = p.def_clock + s * p.Dcap * A;
+    const u64 *gdm = p.def_members + s * p.Dcap * p.Mw;
+    for (unsigned long long i = lane; i < dcnt * A; i += kWave) dcl[i] = gdc[i];
+    for (unsigned long long i = lane; i < dcnt * p.Mw; i += kWave) dmb[i] = gdm[i];
+    wave_fence();
+
+    for (unsigned long long base = ob; base < oe; base += kWave) {
+      // op headers, lane = op
+      const unsigned long long o = base + lane;
+      const bool ov = o < oe;
+      const unsigned h_kind = ov ? p.kind[o] : 0u;
+      const unsigned h_actor = ov && p.actor ? p.actor[o] : 0u;
+      const u64 h_counter = ov && p.counter ? p.counter[o] : 0ull;
+      const unsigned h_rm = ov && p.rm_row ? p.rm_row[o] : 0u;
+      const u64 h_mb = ov ? p.mem_off[o] : 0ull;
+      const u64 h_me = ov ? p.mem_off[o + 1] : 0ull;
+      const int nb = (int)((oe - base) < (unsigned long long)kWave ? (oe - base) : kWave);
+      for (int i = 0; i < nb; ++i) {
+        const unsigned kind = rl32(h_kind, i);
+        const u64 mb = rl64(h_mb, i), me = rl64(h_me, i);
+        if (me < mb || kind > 1) {
+          st |= 2u;
+          continue;
+        }
+        if (kind == 0) {  // ---- Op::Add
+          const unsigned long long a = rl32(h_actor, i);
+          const u64 k = rl64(h_counter, i);
+          if (a >= A) {
+            st |= 2u;
+            continue;
+          }
+          const int ja = (int)(a / kWave), la = (int)(a % kWave);
+          u64 cj = c[0];
+#pragma unroll
+          for (int j = 1; j < kCA; ++j)
+            if (j == ja) cj = c[j];
+          if (rl64(cj, la) >= k) continue;  // already seen (:60-63)
+          bool bad = false;
+          for (u64 jm = mb + lane; jm < me; jm += kWave) {
+            const unsigned long long m = p.mem[jm];
+            if (m >= p.M) {
+              bad = true;
+              continue;
+            }
+            u64 *cell = E + m * p.entry_mstride + a;
+            if (*cell < k) *cell = k;
+          }
+          if (__ballot(bad)) st |= 2u;
+#pragma unroll
+          for (int j = 0; j < kCA; ++j)
+            if (j == ja && lane == la) c[j] = k;
+          wave_fence();
+          // apply_deferred (:281-286)
+          unsigned nk = 0;
+          for (unsigned d = 0; d < dcnt; ++d) {
+            u64 r[kCA];
+#pragma unroll
+            for (int j = 0; j < kCA; ++j) {
+              const unsigned long long aa = lane + j * kWave;
+              r[j] = aa < A ? dcl[d * A + aa] : 0;
+            }
+            forget_members(p, E, dmb + d * p.Mw, r, lane);
+            if (any_greater(r, c, lane, A)) {
+              if (nk != d) {
+                for (unsigned long long t = lane; t < A; t += kWave) dcl[nk * A + t] = dcl[d * A + t];
+                for (unsigned long long t = lane; t < p.Mw; t += kWave) dmb[nk * p.Mw + t] = dmb[d * p.Mw + t];
+              }
+              ++nk;
+            }
+          }
+          dcnt = nk;
+          wave_fence();
+        } else {  // ---- Op::Rm -> apply_rm (:230-250)
+          const unsigned rr = rl32(h_rm, i);
+          if (rr >= p.n_rm_rows) {
+            st |= 2u;
+            continue;
+          }
+          u64 r[kCA];
+          const u64 *R = p.rm_clock + (unsigned long long)rr * A;
+#pragma unroll
+          for (int j = 0; j < kCA; ++j) {
+            const unsigned long long aa = lane + j * kWave;
+            r[j] = aa < A ? R[aa] : 0;
+          }
+          for (u64 jb = mb; jb < me; jb += kWave) {
+            const unsigned mm = jb + lane < me ? p.mem[jb + lane] : 0u;
+            const int n = (int)((me - jb) < (u64)kWave ? (me - jb) : kWave);
+            for (int t = 0; t < n; ++t) {
+              const unsigned long long m = rl32(mm, t);
+              if (m >= p.M) {
+                st |= 2u;
+                continue;
+              }
+              forget_row(E + m * p.entry_mstride, r, lane, A);
+            }
+          }
+          wave_fence();
+          if (!any_greater(r, c, lane, A)) continue;  // rm <= C: already seen (:239-249)
+          int slot = -1;
+          for (unsigned d = 0; d < dcnt; ++d) {
+            bool ne = false;
+#pragma unroll
+            for (int j = 0; j < kCA; ++j) {
+              const unsigned long long aa = lane + j * kWave;
+              if (aa < A && dcl[d * A + aa] != r[j]) ne = true;
+            }
+            if (__ballot(ne) == 0) {
+              slot = (int)d;
+              break;
+            }
+          }
+          if (slot < 0) {
+            if (dcnt >= p.Dcap) {
+              st |= 1u;  // deferred capacity exceeded: this state's result is incomplete
+              continue;
+            }
+            slot = (int)dcnt++;
+#pragma unroll
+            for (int j = 0; j < kCA; ++j) {
+              const unsigned long long aa = lane + j * kWave;
+              if (aa < A) dcl[slot * A + aa] = r[j];
+            }
+            for (unsigned long long t = lane; t < p.Mw; t += kWave) dmb[slot * p.Mw + t] = 0;
+            wave_fence();
+          }
+          u64 *bits = dmb + (unsigned long long)slot * p.Mw;
+          for (u64 jm = mb + lane; jm < me; jm += kWave) {
+            const unsigned long long m = p.mem[jm];
+            if (m < p.M) atomicOr(bits + m / 64, 1ull << (m % 64));
+          }
+          wave_fence();
+        }
+      }
+    }
+    // write the state back
+#pragma unroll
+    for (int j = 0; j < kCA; ++j) {
+      const unsigned long long a = lane + j * kWave;
+      if (a < A) C[a] = c[j];
+    }
+    u64 *wdc = p.def_clock + s * p.Dcap * A;
+    u64 *wdm = p.def_members + s * p.Dcap * p.Mw;
+    for (unsigned long long i = lane; i < dcnt * A; i += kWave) wdc[i] = dcl[i];
+    for (unsigned long long i = lane; i < dcnt * p.Mw; i += kWave) wdm[i] = dmb[i];
+    if (lane == 0) {
+      p.def_count[s] = dcnt;
+      p.status[s] = st;
+    }
+    wave_fence();
+  }
+}
+
+}  // namespace crdt
+
+using namespace crdt;
+
+extern "C" int crdt_orswot_apply_batch(crdt_ctx *ctx, const crdt_orswot_states *sv, const crdt_orswot_ops *ops,
+                                       uint32_t *status) {
+  CRDT_CHECK_CTX(ctx);
+  if (!sv || !ops || !status) return fail(ctx, CRDT_EINVAL, "orswot_apply_batch: NULL argument");
+  const crdt_orswot_states &s = *sv;
+  if (s.N == 0) return CRDT_OK;
+  if (s.A == 0 || s.A > (size_t)kApplyMaxA)
+    return fail(ctx, CRDT_EINVAL, "orswot_apply_batch: A = %zu outside 1..%d", s.A, kApplyMaxA);
+  if (!s.clock || !s.entries || !s.def_count || !ops->op_off || !ops->mem_off || !status)
+    return fail(ctx, CRDT_EINVAL, "orswot_apply_batch: NULL buffer");
+  if (s.Dcap && (!s.def_clock || !s.def_members))
+    return fail(ctx, CRDT_EINVAL, "orswot_apply_batch: deferred capacity without deferred buffers");
+  if (ops->n_ops && (!ops->kind || !ops->mem))
+    return fail(ctx, CRDT_EINVAL, "orswot_apply_batch: NULL op buffer");
+  if (s.clock_stride < s.A || s.entry_mstride < s.A || s.entry_sstride < s.M * s.entry_mstride)
+    return fail(ctx, CRDT_EINVAL, "orswot_apply_batch: strides smaller than the rows they hold");
+  const size_t Mw = (s.M + 63) / 64;
+  const size_t per_wave = s.Dcap * (s.A + Mw) * 8;
+  const size_t lds_cap = 64 * 1024;
+  if (per_wave > lds_cap)
+    return fail(ctx, CRDT_EINVAL, "orswot_apply_batch: Dcap * (A + ceil(M/64)) * 8 = %zu B exceeds %zu B of LDS",
+                per_wave, lds_cap);
+  int wpb = kBlock / kWave;
+  while (wpb > 1 && per_wave * wpb > lds_cap) --wpb;
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  OrswotApplyPlan p{(u64 *)s.clock, s.clock_stride, (u64 *)s.entries, s.entry_mstride, s.entry_sstride,
+                    (u64 *)s.def_clock, (u64 *)s.def_members, s.def_count, s.N, s.M, s.A, Mw, s.Dcap,
+                    (const u64 *)ops->op_off, ops->kind, ops->actor, (const u64 *)ops->counter, ops->rm_row,
+                    (const u64 *)ops->rm_clock, ops->rm_clock ? ops->n_rm_rows : 0, (const u64 *)ops->mem_off,
+                    ops->mem, ops->n_ops, status, wpb};
+  const unsigned long long want = (s.N + wpb - 1) / wpb;
+  const unsigned long long cap = (unsigned long long)ctx->cu_count * 64;
+  timing_begin(ctx, "orswot_apply");
+  hipLaunchKernelGGL(orswot_apply_kernel, dim3((unsigned)(want < cap ? want : cap)), dim3(wpb * kWave),
+                     per_wave * wpb, ctx->stream, p);
+  timing_end(ctx);
+  CRDT_HIP(ctx, hipGetLastError());
+  return CRDT_OK;
+}

@@ -4,6 +4,8 @@
 through libcrdt_gpu; by default the oracle's own merge runs.  `causal_hook` (optional) routes
 VClock forget / glb / partial_cmp and counter read() the same way: an object with methods
 forget(x, y) / glb(x, y) (mutate x), cmp(x, y) -> Ordering code or None, read(counter) -> int.
+`apply_hook(state, op)` applies an Orswot op built by the reference's ctx API (add / rm steps)
+to `state` in place (default: the oracle's own CmRDT::apply).
 """
 import json
 import os
@@ -79,7 +81,11 @@ def _cmp(x, op, y):
     raise ValueError(op)
 
 
-def run_case(case, merge_hook=default_merge, causal_hook=None):
+def default_apply(v, op):
+    v.apply(op)
+
+
+def run_case(case, merge_hook=default_merge, causal_hook=None, apply_hook=default_apply):
     env = {}
     for st in case["steps"]:
         op, args = st[0], st[1:]
@@ -133,23 +139,23 @@ def run_case(case, merge_hook=default_merge, causal_hook=None):
             assert err == expect_err
         elif op == "add":
             v = env[args[0]]
-            v.apply(v.add(args[1], v.read().derive_add_ctx(args[2])))
+            apply_hook(v, v.add(args[1], v.read().derive_add_ctx(args[2])))
         elif op == "rm":
             v = env[args[0]]
-            v.apply(v.rm(args[1], v.contains(args[1]).derive_rm_ctx()))
+            apply_hook(v, v.rm(args[1], v.contains(args[1]).derive_rm_ctx()))
         elif op == "rm_clock":
             v = env[args[0]]
-            v.apply(v.rm(args[1], O.RmCtx(_vc(args[2]))))
+            apply_hook(v, v.rm(args[1], O.RmCtx(_vc(args[2]))))
         elif op == "save_read":
             env[args[0]] = env[args[1]].read()
         elif op == "save_contains":
             env[args[0]] = env[args[1]].contains(args[2])
         elif op == "add_ctx":
             v, ctx = env[args[0]], env[args[2]]
-            v.apply(v.add(args[1], ctx.derive_add_ctx(args[3])))
+            apply_hook(v, v.add(args[1], ctx.derive_add_ctx(args[3])))
         elif op == "rm_ctx":
             v, ctx = env[args[0]], env[args[2]]
-            v.apply(v.rm(args[1], ctx.derive_rm_ctx()))
+            apply_hook(v, v.rm(args[1], ctx.derive_rm_ctx()))
         elif op == "assert_add_op":
             v = env[args[0]]
             opv = v.add(args[1], v.read().derive_add_ctx(args[2]))

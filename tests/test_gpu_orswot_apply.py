@@ -1,0 +1,135 @@
+"""Batched Orswot CmRDT::apply (crdt_orswot_apply_batch) vs the oracle's one-by-one apply
+(orswot.rs:55-79, apply_rm :230-250, apply_deferred :281-286).
+
+Inputs: the reference's own KAT scripts with every Orswot op routed through the kernel, op-replay
+streams built with the reference's ctx API (test/orswot.rs:15-31 style: one actor per origin,
+out-of-order delivery so removes defer), and arbitrary ops on arbitrary states (the kernel
+claims exactness for any input, not only for states the reference can reach)."""
+import numpy as np
+import pytest
+import torch
+
+import kat_runner as K
+import oracle as O
+from gpu_util import to_dev, to_host
+from orswot_apply_util import (arbitrary_case, dense_states, map_orswot, op_tuple, oracle_streams,
+                               replay_streams, to_object)
+
+pytestmark = pytest.mark.gpu
+
+import crdts_gpu as cg  # noqa: E402
+
+
+def gpu_apply_streams(ctx, states, streams, M, A, Dcap=None):
+    """Apply streams[s] to a copy of states[s] for every s in one batched call; returns the
+    resulting oracle objects and the status array."""
+    if Dcap is None:
+        Dcap = max(1, max(len(o.deferred) for o in states) + max(
+            sum(1 for op in ops if isinstance(op, O.OrswotRm)) for ops in streams))
+    clock, entries, dcl, dmb, cnt = dense_states(states, M, A, Dcap)
+    tc, te, tdc, tdm = to_dev(clock), to_dev(entries), to_dev(dcl), to_dev(dmb)
+    tcnt = torch.from_numpy(cnt).cuda()
+    ops = cg.orswot.encode_ops([[op_tuple(op) for op in ops] for ops in streams], A, "cuda:0")
+    status = cg.orswot.apply_batch(tc, te, tdc, tdm, tcnt, ops, ctx=ctx)
+    torch.cuda.synchronize()
+    c, e, d, dm = to_host(tc), to_host(te), to_host(tdc), to_host(tdm)
+    n = tcnt.cpu().numpy()
+    return [to_object(c, e, d, dm, n, s) for s in range(len(states))], status.cpu().numpy()
+
+
+# ---- the reference's KATs with Orswot apply on the GPU ------------------------------------------
+def gpu_apply_hook(ctx):
+    """Route one Orswot op through crdt_orswot_apply_batch: intern the state's and the op's
+    actors / members (KAT ids are strings and ints), apply, map the result back in place."""
+    def hook(v, op):
+        actors, members = cg.intern.Index(), cg.intern.Index()
+        iv = map_orswot(v, actors.intern, members.intern)
+        if isinstance(op, O.OrswotAdd):
+            iop = O.OrswotAdd(O.Dot(actors.intern(op.dot.actor), op.dot.counter), [members.intern(m) for m in op.members])
+        else:
+            iop = O.OrswotRm(O.VClock({actors.intern(a): c for a, c in op.clock.dots.items()}),
+                             [members.intern(m) for m in op.members])
+        (res,), status = gpu_apply_streams(ctx, [iv], [[iop]], max(1, len(members)), max(1, len(actors)))
+        assert status[0] == 0
+        back = map_orswot(res, lambda a: actors.ids[a], lambda m: members.ids[m])
+        v.clock, v.entries, v.deferred = back.clock, back.entries, back.deferred
+    return hook
+
+
+APPLY_CASES = [c for c in K.load_cases("kat_orswot.json")
+               if any(s[0] in ("add", "rm", "rm_clock", "add_ctx", "rm_ctx") for s in c["steps"])]
+
+
+@pytest.mark.parametrize("case", APPLY_CASES, ids=[c["name"] for c in APPLY_CASES])
+def test_kat_orswot_apply_gpu(gpu_ctx, case):
+    K.run_case(case, apply_hook=gpu_apply_hook(gpu_ctx))
+
+
+# ---- op replay (ctx API, one actor per origin, out-of-order delivery) ---------------------------
+@pytest.mark.parametrize("seed,n_states,n_origins,M,n_ops", [
+    (1, 64, 4, 12, 60), (2, 200, 8, 40, 150), (3, 16, 64, 200, 400), (4, 100, 3, 5, 100)])
+def test_orswot_apply_replay(gpu_ctx, seed, n_states, n_origins, M, n_ops):
+    streams = replay_streams(seed, n_states, n_origins, M, n_ops)
+    states = [O.Orswot() for _ in streams]
+    got, status = gpu_apply_streams(gpu_ctx, states, streams, M, n_origins)
+    exp = oracle_streams(states, streams)
+    assert (status == 0).all()
+    assert sum(len(o.deferred) for o in exp) > 0 or seed == 4  # the replay exercises deferral
+    for s, (g, e) in enumerate(zip(got, exp)):
+        assert g == e, f"state {s}: {g} != {e}"
+
+
+# ---- arbitrary states and ops ------------------------------------------------------------------
+@pytest.mark.parametrize("seed,N,M,A", [(5, 40, 16, 8), (6, 24, 70, 65), (7, 8, 130, 256), (8, 30, 3, 1)])
+def test_orswot_apply_arbitrary(gpu_ctx, seed, N, M, A):
+    states, streams = arbitrary_case(seed, N, M, A)
+    got, status = gpu_apply_streams(gpu_ctx, states, streams, M, A)
+    exp = oracle_streams(states, streams)
+    assert (status == 0).all()
+    for s, (g, e) in enumerate(zip(got, exp)):
+        assert g == e, f"state {s}"
+
+
+def test_orswot_apply_overflow_and_bad_ops(gpu_ctx):
+    A, M = 4, 8
+    st = [O.Orswot(), O.Orswot(), O.Orswot()]
+    fut1 = O.OrswotRm(O.VClock({0: 5}), [1])
+    fut2 = O.OrswotRm(O.VClock({1: 5}), [2])
+    add = O.OrswotAdd(O.Dot(2, 1), [3])
+    streams = [[fut1, fut2, add], [add, fut1, fut1], [add]]
+    got, status = gpu_apply_streams(gpu_ctx, st, streams, M, A, Dcap=1)
+    assert status[0] & 1 and status[1] == 0 and status[2] == 0  # state 0 needs 2 deferred slots
+    exp = oracle_streams(st, streams)
+    assert got[1] == exp[1] and got[2] == exp[2]
+    # an out-of-range member is skipped and flagged; the rest of the op still applies
+    bad = O.OrswotAdd(O.Dot(0, 1), [2, 99])
+    got, status = gpu_apply_streams(gpu_ctx, [O.Orswot()], [[bad]], M, A, Dcap=1)
+    assert status[0] == 2
+    assert set(got[0].entries) == {2} and got[0].clock.dots == {0: 1}
+
+
+def test_orswot_apply_empty(gpu_ctx):
+    st = [O.Orswot() for _ in range(5)]
+    got, status = gpu_apply_streams(gpu_ctx, st, [[] for _ in st], 4, 2, Dcap=1)
+    assert (status == 0).all() and all(g == O.Orswot() for g in got)
+
+
+@pytest.mark.parametrize("N,T,M,A", [(512, 64, 300, 64), (64, 200, 40, 256), (300, 32, 1000, 17)])
+def test_orswot_apply_synth_streams(gpu_ctx, N, T, M, A):
+    """The bench's device-generated streams vs the C++ twin (std containers), every state."""
+    ops = cg.synth.orswot_op_streams(N, T, M, A, seed=N + T, device="cuda:0")
+    Dcap = 16
+    clock = torch.zeros((N, A), dtype=torch.int64, device="cuda:0")
+    entries = torch.zeros((N, M, A), dtype=torch.int64, device="cuda:0")
+    dcl = torch.zeros((N, Dcap, A), dtype=torch.int64, device="cuda:0")
+    dmb = torch.zeros((N, Dcap, (M + 63) // 64), dtype=torch.int64, device="cuda:0")
+    cnt = torch.zeros(N, dtype=torch.int32, device="cuda:0")
+    status = cg.orswot.apply_batch(clock, entries, dcl, dmb, cnt, ops, ctx=gpu_ctx)
+    torch.cuda.synchronize()
+    arr = [t.cpu().numpy() for t in ops]
+    oc, oe, ond, _ = O.orswot_apply_streams(N, M, A, *arr)
+    assert (status.cpu().numpy() == 0).all()
+    np.testing.assert_array_equal(to_host(clock), oc)
+    np.testing.assert_array_equal(to_host(entries), oe)
+    np.testing.assert_array_equal(cnt.cpu().numpy(), ond.astype(np.int32))
+    assert ond.sum() > 0
