@@ -42,6 +42,7 @@ extern "C" {
 #define CRDT_EHIP -2         /* a HIP runtime call failed                                   */
 #define CRDT_ENOMEM -3       /* device scratch allocation failed                            */
 #define CRDT_EUNSUPPORTED -4 /* shape the kernels do not handle                             */
+#define CRDT_ECOMM -5        /* an RCCL call failed (sharded entry points)                  */
 
 /* ---- flags for *_lub_many ---------------------------------------------------------- */
 /* out := out ⊔ fold(in) instead of out := fold(in): i.e. `self.merge(r)` for every r,
@@ -206,6 +207,50 @@ typedef struct crdt_orswot_ops {
 
 int crdt_orswot_apply_batch(crdt_ctx *ctx, const crdt_orswot_states *states, const crdt_orswot_ops *ops,
                             uint32_t *status);
+
+/* ---- multi-GPU: replica-sharded lub over RCCL ----------------------------
+ * One process (one ctx) per GPU.  Rank 0 calls crdt_comm_unique_id and sends the 128 bytes to
+ * every rank over the caller's own channel; every rank then calls crdt_ctx_comm_init (collective:
+ * all ranks must call it).  The *_sharded calls are collective too: rank k passes its own replica
+ * shard (same G and row width on every rank, any R_k >= 0) and every rank receives the global
+ * lub, equal to lub_many over the concatenation of the shards.
+ *   vclock / gcounter / pncounter: local lub_many + one ncclAllReduce(ncclUint64, ncclMax) of the
+ *       packed G x W partials (W = A, 2A for PNCounter) — out is packed [G][W]
+ *   gset: local lub_many + ncclAllGather of the partial bitmaps + OR-fold of the world partials
+ *   orswot: local join without deferred removes, ncclAllGather of the partial (clock, entries),
+ *       all ranks' deferred removes gathered and pooled per group (rank order, then local order),
+ *       re-merge of the world partials with every deferred remove (orswot.rs:141-147).  Output:
+ *       clock [G][A], entries [G][M][A], and the surviving deferred removes compacted: *ndef (host)
+ *       = their number; the first min(*ndef, def_cap) are written as def_clock[d*A + a],
+ *       def_members[d*Mw + w] (union over the survivors with that exact clock in the group) and
+ *       def_group[d] (device u32), in group order.
+ * The replaced reference operation is the same CvRDT::merge fold (traits.rs:4-7), split over
+ * processes: a Rust caller would distribute the id over its own transport. */
+#define CRDT_UNIQUE_ID_BYTES 128
+int crdt_comm_unique_id(uint8_t *id /* [CRDT_UNIQUE_ID_BYTES] */);
+int crdt_ctx_comm_init(crdt_ctx *ctx, const uint8_t *id, int nranks, int rank);
+int crdt_ctx_comm_destroy(crdt_ctx *ctx);
+int crdt_ctx_comm_info(const crdt_ctx *ctx, int *nranks, int *rank);
+int crdt_vclock_lub_many_sharded(crdt_ctx *ctx, const uint64_t *in, size_t G, size_t R, size_t A,
+                                 size_t row_stride, size_t group_stride, uint64_t *out);
+int crdt_gcounter_lub_many_sharded(crdt_ctx *ctx, const uint64_t *in, size_t G, size_t R, size_t A,
+                                   size_t row_stride, size_t group_stride, uint64_t *out);
+int crdt_pncounter_lub_many_sharded(crdt_ctx *ctx, const uint64_t *in, size_t G, size_t R, size_t A,
+                                    size_t row_stride, size_t group_stride, uint64_t *out);
+int crdt_gset_lub_many_sharded(crdt_ctx *ctx, const uint64_t *in, size_t G, size_t R, size_t words,
+                               size_t row_stride, size_t group_stride, uint64_t *out);
+
+typedef struct crdt_orswot_sharded_out {
+  uint64_t *clock;       /* [G][A]      */
+  uint64_t *entries;     /* [G][M][A]   */
+  size_t def_cap;        /* rows available below */
+  uint64_t *def_clock;   /* [def_cap][A]  */
+  uint64_t *def_members; /* [def_cap][Mw] */
+  uint32_t *def_group;   /* [def_cap]     */
+  size_t *ndef;          /* host: number of surviving deferred removes */
+} crdt_orswot_sharded_out;
+
+int crdt_orswot_lub_many_sharded(crdt_ctx *ctx, const crdt_orswot_batch *in, crdt_orswot_sharded_out *out);
 
 /* ---- Map<K, MVReg<u64, A>, A> --------------------------------------------------------------
  * Replaces Map::merge (map.rs:140-220) with V = MVReg (MVReg::merge mvreg.rs:112-128,

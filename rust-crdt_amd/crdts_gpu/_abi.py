@@ -16,6 +16,8 @@ CRDT_EINVAL = -1
 CRDT_EHIP = -2
 CRDT_ENOMEM = -3
 CRDT_EUNSUPPORTED = -4
+CRDT_ECOMM = -5
+CRDT_UNIQUE_ID_BYTES = 128
 CRDT_ACCUMULATE = 0x1
 
 # Every symbol declared in include/crdt_gpu.h (checked by tests/test_abi.py).
@@ -33,6 +35,9 @@ EXPORTS = (
     "crdt_pncounter_read", "crdt_vclock_apply_batch", "crdt_gcounter_apply_batch",
     "crdt_pncounter_apply_batch", "crdt_gset_apply_batch",
     "crdt_synth_fill", "crdt_synth_orswot", "crdt_synth_orswot_rm", "crdt_synth_map",
+    "crdt_comm_unique_id", "crdt_ctx_comm_init", "crdt_ctx_comm_destroy", "crdt_ctx_comm_info",
+    "crdt_vclock_lub_many_sharded", "crdt_gcounter_lub_many_sharded", "crdt_pncounter_lub_many_sharded",
+    "crdt_gset_lub_many_sharded", "crdt_orswot_lub_many_sharded",
 )
 
 
@@ -79,6 +84,11 @@ class OrswotOps(ctypes.Structure):  # crdt_orswot_ops
         ("n_ops", S), ("op_off", P), ("kind", P), ("actor", P), ("counter", P), ("rm_row", P),
         ("rm_clock", P), ("n_rm_rows", S), ("mem_off", P), ("mem", P),
     ]
+
+
+class OrswotShardedOut(ctypes.Structure):  # crdt_orswot_sharded_out
+    _fields_ = [("clock", P), ("entries", P), ("def_cap", S), ("def_clock", P), ("def_members", P),
+                ("def_group", P), ("ndef", ctypes.POINTER(S))]
 
 
 class MapBatch(ctypes.Structure):  # crdt_map_batch
@@ -128,6 +138,16 @@ _SIGS = {
     "crdt_pncounter_apply_batch": ([P, P, S, S, S, P, P, P, P, S, P], ctypes.c_int),
     "crdt_gset_apply_batch": ([P, P, S, S, S, P, P, S, P], ctypes.c_int),
 }
+_SIGS.update({
+    "crdt_comm_unique_id": ([P], ctypes.c_int),
+    "crdt_ctx_comm_init": ([P, P, ctypes.c_int, ctypes.c_int], ctypes.c_int),
+    "crdt_ctx_comm_destroy": ([P], ctypes.c_int),
+    "crdt_ctx_comm_info": ([P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
+    "crdt_orswot_lub_many_sharded": ([P, ctypes.POINTER(OrswotBatch), ctypes.POINTER(OrswotShardedOut)],
+                                     ctypes.c_int),
+})
+for _t in ("vclock", "gcounter", "pncounter", "gset"):
+    _SIGS[f"crdt_{_t}_lub_many_sharded"] = ([P, P, S, S, S, S, S, P], ctypes.c_int)
 for _t in ("vclock", "gcounter", "pncounter", "gset"):
     _SIGS[f"crdt_{_t}_lub_many"] = ([P, P, S, S, S, S, S, P, S, ctypes.c_uint], ctypes.c_int)
     _SIGS[f"crdt_{_t}_merge_batch"] = ([P, P, P, S, S, S, S], ctypes.c_int)

@@ -1,0 +1,136 @@
+"""Replica-sharded lub through the C ABI's own RCCL communicator (include/crdt_gpu.h,
+"multi-GPU"): the path a Rust caller takes, with no torch.distributed in the exchange.
+
+    uid = unique_id()                       # rank 0; distribute the 128 bytes to every rank
+    comm_init(ctx, uid, nranks, rank)       # collective
+    lub_many_sharded("gcounter", shard)     # collective: every rank gets the global lub
+    orswot_lub_many_sharded(clock, entries, def_off, def_clock, def_members)
+
+`crdts_gpu.dist` is the torch.distributed twin of the same exchange (gloo-testable on CPU)."""
+from __future__ import annotations
+
+import ctypes
+from typing import NamedTuple, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _abi
+from ._lattice import _geometry
+from .context import Context, dptr
+
+
+def unique_id() -> bytes:
+    lib = _abi.load()
+    buf = (ctypes.c_uint8 * _abi.CRDT_UNIQUE_ID_BYTES)()
+    _abi.check(None, "crdt_comm_unique_id", lib.crdt_comm_unique_id(buf))
+    return bytes(buf)
+
+
+def comm_init(ctx: Context, uid: bytes, nranks: int, rank: int) -> None:
+    if len(uid) != _abi.CRDT_UNIQUE_ID_BYTES:
+        raise ValueError(f"comm_init: unique id must be {_abi.CRDT_UNIQUE_ID_BYTES} bytes")
+    buf = (ctypes.c_uint8 * _abi.CRDT_UNIQUE_ID_BYTES).from_buffer_copy(uid)
+    ctx.call("crdt_ctx_comm_init", buf, int(nranks), int(rank))
+
+
+def comm_destroy(ctx: Context) -> None:
+    ctx.call("crdt_ctx_comm_destroy")
+
+
+def comm_info(ctx: Context):
+    n, r = ctypes.c_int(), ctypes.c_int()
+    ctx.call("crdt_ctx_comm_info", ctypes.byref(n), ctypes.byref(r))
+    return n.value, r.value
+
+
+_WIDTH_DIV = {"vclock": 1, "gcounter": 1, "pncounter": 2, "gset": 1}
+
+
+def lub_many_sharded(kind: str, shard: torch.Tensor, ctx: Optional[Context] = None) -> torch.Tensor:
+    """Global lub of the replicas held across the ctx's ranks; `shard` is this rank's (R_k, W)
+    or (G, R_k, W) block.  Returns (W,) or (G, W), identical on every rank."""
+    if kind not in _WIDTH_DIV:
+        raise ValueError(f"lub_many_sharded: unknown kind {kind}")
+    ctx = ctx or Context.default(shard.device.index)
+    ctx.check_tensor(shard, f"{kind}.lub_many_sharded")
+    G, R, W, rstride, gstride = _geometry(shard, f"{kind}.lub_many_sharded")
+    if W % _WIDTH_DIV[kind]:
+        raise ValueError(f"{kind}.lub_many_sharded: row width {W} not a multiple of {_WIDTH_DIV[kind]}")
+    out = torch.empty((G, W), dtype=shard.dtype, device=shard.device)
+    ctx.call(f"crdt_{kind}_lub_many_sharded", dptr(shard), G, R, W // _WIDTH_DIV[kind], rstride, gstride, dptr(out))
+    return out[0] if shard.dim() == 2 else out
+
+
+class OrswotSharded(NamedTuple):
+    clock: torch.Tensor        # (G, A)
+    entries: torch.Tensor      # (G, M, A)
+    def_clock: torch.Tensor    # (ndef, A)   surviving deferred removes
+    def_members: torch.Tensor  # (ndef, Mw)  member union per surviving rm clock
+    def_group: torch.Tensor    # (ndef,) int32
+
+
+def orswot_lub_many_sharded(clock: torch.Tensor, entries: torch.Tensor, def_off: Optional[Sequence[int]] = None,
+                            def_clock: Optional[torch.Tensor] = None, def_members: Optional[torch.Tensor] = None,
+                            ctx: Optional[Context] = None, def_cap: Optional[int] = None) -> OrswotSharded:
+    """Rank k's shard: clock (G, R_k, A), entries (G, R_k, M, A) and its deferred removes pooled
+    per group (host def_off of G+1 entries, def_clock (D_k, A), def_members (D_k, Mw))."""
+    ctx = ctx or Context.default(clock.device.index)
+    ctx.check_tensor(clock, "orswot.lub_many_sharded(clock)")
+    ctx.check_tensor(entries, "orswot.lub_many_sharded(entries)")
+    if clock.dim() != 3 or entries.dim() != 4 or clock.stride(2) != 1 or entries.stride(3) != 1:
+        raise ValueError("orswot.lub_many_sharded: clock (G,R,A) / entries (G,R,M,A), actor axis contiguous")
+    G, R, A = clock.shape
+    M = entries.shape[2]
+    Mw = (M + 63) // 64
+    b = _abi.OrswotBatch()
+    b.G, b.R, b.M, b.A = G, R, M, A
+    b.clock, b.clock_rstride, b.clock_gstride = clock.data_ptr(), clock.stride(1), clock.stride(0)
+    b.entries = entries.data_ptr()
+    b.entry_mstride, b.entry_rstride, b.entry_gstride = entries.stride(2), entries.stride(1), entries.stride(0)
+    off_arr = None
+    D = 0
+    if def_off is not None:
+        off = [int(x) for x in def_off]
+        if len(off) != G + 1:
+            raise ValueError(f"orswot.lub_many_sharded: def_off must have G+1 = {G + 1} entries")
+        D = off[-1]
+        if D:
+            for t, nm, w in ((def_clock, "def_clock", A), (def_members, "def_members", Mw)):
+                if t is None or not t.is_contiguous() or tuple(t.shape) != (D, w):
+                    raise ValueError(f"orswot.lub_many_sharded: {nm} must be a contiguous ({D}, {w}) tensor")
+                ctx.check_tensor(t, f"orswot.lub_many_sharded({nm})")
+            b.def_clock, b.def_members = def_clock.data_ptr(), def_members.data_ptr()
+        off_arr = (ctypes.c_size_t * (G + 1))(*off)
+        b.def_off = ctypes.cast(off_arr, ctypes.POINTER(ctypes.c_size_t))
+    cap = def_cap if def_cap is not None else max(1, 4 * D + 64)
+    oc = torch.empty((G, A), dtype=clock.dtype, device=clock.device)
+    oe = torch.empty((G, M, A), dtype=clock.dtype, device=clock.device)
+    odc = torch.empty((cap, A), dtype=clock.dtype, device=clock.device)
+    odm = torch.empty((cap, Mw), dtype=clock.dtype, device=clock.device)
+    odg = torch.empty((cap,), dtype=torch.int32, device=clock.device)
+    nd = ctypes.c_size_t()
+    o = _abi.OrswotShardedOut()
+    o.clock, o.entries, o.def_cap = oc.data_ptr(), oe.data_ptr(), cap
+    o.def_clock, o.def_members, o.def_group = odc.data_ptr(), odm.data_ptr(), odg.data_ptr()
+    o.ndef = ctypes.pointer(nd)
+    ctx.call("crdt_orswot_lub_many_sharded", ctypes.byref(b), ctypes.byref(o))
+    n = nd.value
+    if n > cap:  # more survivors than room: run again with exactly enough
+        return orswot_lub_many_sharded(clock, entries, def_off, def_clock, def_members, ctx, def_cap=n)
+    return OrswotSharded(oc, oe, odc[:n], odm[:n], odg[:n])
+
+
+def deferred_groups(res: OrswotSharded, G: int):
+    """Egress: per group, {(rm clock tuple, frozenset of members)} of the surviving removes."""
+    out = [set() for _ in range(G)]
+    dc = res.def_clock.cpu().numpy().view(np.uint64)
+    dm = res.def_members.cpu().numpy().view(np.uint64)
+    for d, g in enumerate(res.def_group.cpu().numpy().tolist()):
+        ms = []
+        for w, x in enumerate(dm[d].tolist()):
+            while x:
+                ms.append(w * 64 + (x & -x).bit_length() - 1)
+                x &= x - 1
+        out[g].add((tuple(int(v) for v in dc[d]), frozenset(ms)))
+    return out

@@ -78,6 +78,13 @@ struct crdt_ctx {
   std::map<std::string, crdt::KernelTimer> timers;
   std::vector<crdt::PendingTiming> pending;
   std::vector<hipEvent_t> free_events;
+  // Multi-GPU (csrc/shard.hip): this rank's RCCL communicator and the buffers of the exchange
+  // (partials, gathered partials, deferred pools), owned by the ctx and reused.
+  void *comm = nullptr;
+  int nranks = 1, rank = 0;
+  void (*comm_destroy)(void *) = nullptr;
+  void *sbuf[8] = {};
+  size_t sbuf_bytes[8] = {};
 };
 
 namespace crdt {

@@ -247,6 +247,9 @@ int crdt_ctx_destroy(crdt_ctx *ctx) {
   if (ctx->dscratch) (void)hipFree(ctx->dscratch);
   if (ctx->pinned) (void)hipHostFree(ctx->pinned);
   if (ctx->pinned_done) (void)hipEventDestroy(ctx->pinned_done);
+  if (ctx->comm && ctx->comm_destroy) ctx->comm_destroy(ctx->comm);
+  for (void *b : ctx->sbuf)
+    if (b) (void)hipFree(b);
   delete ctx;
   return CRDT_OK;
 }
