@@ -208,6 +208,41 @@ typedef struct crdt_orswot_ops {
 int crdt_orswot_apply_batch(crdt_ctx *ctx, const crdt_orswot_states *states, const crdt_orswot_ops *ops,
                             uint32_t *status);
 
+/* ---- batched Causal::forget of whole states -----------------------------------
+ * State s forgets the clock y + s*y_stride (y_stride = 0: one clock for every state), in place.
+ * Orswot::forget (orswot.rs:150-183): clock, entry clocks (an emptied entry = all-zero row =
+ *     dropped) and deferred rm clocks.  Deferred removes are a pool of D rows: row d belongs to
+ *     state def_state[d] (device u32); def_keep[d] = 0 iff its rm clock emptied (dropped by the
+ *     reference, :168-180); member sets are untouched.  When two surviving rm clocks of one state
+ *     become equal the reference's HashMap collect keeps ONE of them with its own member set,
+ *     chosen by hash iteration order (unspecified); both rows are kept here.  Rows with
+ *     def_state[d] >= N are left untouched (def_keep[d] = 1).
+ * Map::forget (map.rs:85-114) with V = MVReg: entry clocks, every value clock (MVReg::forget
+ *     mvreg.rs:88-104: an emptied value is dropped: slot clock all 0, value 0), an entry whose own
+ *     clock empties is dropped with its values, deferred rm clocks as for Orswot, the map clock.
+ *     Layout (device, per state s): clock + s*clock_stride; ec + s*ec_stride + k*A;
+ *     vclk + s*vclk_stride + (k*V + j)*A; vval + s*vval_stride + k*V + j (the crdt_map_lub_many
+ *     slot convention: empty slot <=> all-zero clock row, skipped on egress). */
+int crdt_orswot_forget_batch(crdt_ctx *ctx, uint64_t *clock, size_t clock_stride, uint64_t *entries,
+                             size_t entry_mstride, size_t entry_sstride, size_t N, size_t M, size_t A,
+                             const uint64_t *y, size_t y_stride, uint64_t *def_clock,
+                             const uint32_t *def_state, size_t D, uint8_t *def_keep);
+
+typedef struct crdt_map_states {
+  size_t N, K, A, V;
+  uint64_t *clock;
+  size_t clock_stride;
+  uint64_t *ec;
+  size_t ec_stride;
+  uint64_t *vclk;
+  size_t vclk_stride;
+  uint64_t *vval;
+  size_t vval_stride;
+} crdt_map_states;
+
+int crdt_map_forget_batch(crdt_ctx *ctx, const crdt_map_states *states, const uint64_t *y, size_t y_stride,
+                          uint64_t *def_clock, const uint32_t *def_state, size_t D, uint8_t *def_keep);
+
 /* ---- multi-GPU: replica-sharded lub over RCCL ----------------------------
  * One process (one ctx) per GPU.  Rank 0 calls crdt_comm_unique_id and sends the 128 bytes to
  * every rank over the caller's own channel; every rank then calls crdt_ctx_comm_init (collective:

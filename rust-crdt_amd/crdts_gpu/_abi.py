@@ -38,6 +38,7 @@ EXPORTS = (
     "crdt_comm_unique_id", "crdt_ctx_comm_init", "crdt_ctx_comm_destroy", "crdt_ctx_comm_info",
     "crdt_vclock_lub_many_sharded", "crdt_gcounter_lub_many_sharded", "crdt_pncounter_lub_many_sharded",
     "crdt_gset_lub_many_sharded", "crdt_orswot_lub_many_sharded",
+    "crdt_orswot_forget_batch", "crdt_map_forget_batch",
 )
 
 
@@ -91,6 +92,11 @@ class OrswotShardedOut(ctypes.Structure):  # crdt_orswot_sharded_out
                 ("def_group", P), ("ndef", ctypes.POINTER(S))]
 
 
+class MapStates(ctypes.Structure):  # crdt_map_states
+    _fields_ = [("N", S), ("K", S), ("A", S), ("V", S), ("clock", P), ("clock_stride", S), ("ec", P),
+                ("ec_stride", S), ("vclk", P), ("vclk_stride", S), ("vval", P), ("vval_stride", S)]
+
+
 class MapBatch(ctypes.Structure):  # crdt_map_batch
     _fields_ = [
         ("G", S), ("R", S), ("K", S), ("A", S), ("V", S),
@@ -139,6 +145,8 @@ _SIGS = {
     "crdt_gset_apply_batch": ([P, P, S, S, S, P, P, S, P], ctypes.c_int),
 }
 _SIGS.update({
+    "crdt_orswot_forget_batch": ([P, P, S, P, S, S, S, S, S, P, S, P, P, S, P], ctypes.c_int),
+    "crdt_map_forget_batch": ([P, ctypes.POINTER(MapStates), P, S, P, P, S, P], ctypes.c_int),
     "crdt_comm_unique_id": ([P], ctypes.c_int),
     "crdt_ctx_comm_init": ([P, P, ctypes.c_int, ctypes.c_int], ctypes.c_int),
     "crdt_ctx_comm_destroy": ([P], ctypes.c_int),

@@ -142,3 +142,59 @@ def deferred_set(def_clock: torch.Tensor, def_keep: torch.Tensor, def_keys: torc
     """Egress of the surviving deferred removes: {(rm clock tuple, frozenset of key indices)}."""
     from .orswot import deferred_set as _ds
     return _ds(def_clock, def_keep, def_keys, lo, hi)
+
+
+def _forget_clock(ctx, y, N, A, what):
+    ctx.check_tensor(y, what)
+    if y.dim() == 1:
+        if y.shape[0] != A:
+            raise ValueError(f"{what}: y must be (A,) or (N, A)")
+        return y, 0
+    if tuple(y.shape) != (N, A) or y.stride(1) != 1:
+        raise ValueError(f"{what}: y must be (A,) or (N, A) with contiguous rows")
+    return y, y.stride(0)
+
+
+def _forget_deferred(ctx, def_clock, def_state, N, A, what):
+    """-> (ptr, state ptr, D, keep tensor or None)"""
+    if def_clock is None or def_clock.shape[0] == 0:
+        return None, None, 0, None
+    ctx.check_tensor(def_clock, what)
+    D = def_clock.shape[0]
+    if tuple(def_clock.shape) != (D, A) or not def_clock.is_contiguous():
+        raise ValueError(f"{what}: def_clock must be a contiguous (D, A) tensor")
+    if (def_state is None or def_state.dtype not in (torch.int32, torch.uint32) or tuple(def_state.shape) != (D,)
+            or def_state.device != def_clock.device or not def_state.is_contiguous()):
+        raise ValueError(f"{what}: def_state must be a contiguous (D,) int32 tensor on the same device")
+    keep = torch.empty(D, dtype=torch.uint8, device=def_clock.device)
+    return def_clock.data_ptr(), def_state.data_ptr(), D, keep
+
+
+def forget_batch(clock: torch.Tensor, ec: torch.Tensor, vclk: torch.Tensor, vval: torch.Tensor, y: torch.Tensor,
+                 def_clock: Optional[torch.Tensor] = None, def_state: Optional[torch.Tensor] = None,
+                 ctx: Optional[Context] = None) -> Optional[torch.Tensor]:
+    """Causal::forget of N Map<K, MVReg> states in place (map.rs:85-114, mvreg.rs:88-104):
+    clock (N, A), ec (N, K, A), vclk (N, K, V, A), vval (N, K, V), y (A,) or (N, A); deferred as
+    for orswot.forget_batch.  Returns def_keep or None."""
+    ctx = ctx or Context.default(clock.device.index)
+    for t, nm in ((clock, "clock"), (ec, "ec"), (vclk, "vclk"), (vval, "vval")):
+        ctx.check_tensor(t, f"map.forget_batch({nm})")
+    if clock.dim() != 2 or ec.dim() != 3 or vclk.dim() != 4 or vval.dim() != 3:
+        raise ValueError("map.forget_batch: clock (N,A), ec (N,K,A), vclk (N,K,V,A), vval (N,K,V) expected")
+    N, A = clock.shape
+    K, V = vclk.shape[1], vclk.shape[2]
+    if (tuple(ec.shape) != (N, K, A) or tuple(vclk.shape) != (N, K, V, A) or tuple(vval.shape) != (N, K, V)
+            or clock.stride(1) != 1 or ec.stride(2) != 1 or ec.stride(1) != A or vclk.stride(3) != 1
+            or vclk.stride(2) != A or vclk.stride(1) != V * A or vval.stride(2) != 1 or vval.stride(1) != V):
+        raise ValueError("map.forget_batch: per-state blocks must be packed (K, A) / (K, V, A) / (K, V)")
+    y, ys = _forget_clock(ctx, y, N, A, "map.forget_batch(y)")
+    dp, sp, D, keep = _forget_deferred(ctx, def_clock, def_state, N, A, "map.forget_batch(def_clock)")
+    st = _abi.MapStates()
+    st.N, st.K, st.A, st.V = N, K, A, V
+    st.clock, st.clock_stride = clock.data_ptr(), clock.stride(0)
+    st.ec, st.ec_stride = ec.data_ptr(), ec.stride(0)
+    st.vclk, st.vclk_stride = vclk.data_ptr(), vclk.stride(0)
+    st.vval, st.vval_stride = vval.data_ptr(), vval.stride(0)
+    ctx.call("crdt_map_forget_batch", ctypes.byref(st), y.data_ptr(), ys, dp, sp, D,
+             keep.data_ptr() if keep is not None else None)
+    return keep

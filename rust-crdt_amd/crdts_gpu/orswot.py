@@ -237,3 +237,50 @@ def deferred_slots(def_clock: torch.Tensor, def_members: torch.Tensor, def_count
     n = int(def_count[s].item())
     keep = torch.ones(n, dtype=torch.uint8)
     return deferred_set(def_clock[s, :n], keep, def_members[s, :n])
+
+
+def _forget_clock(ctx, y, N, A, what):
+    ctx.check_tensor(y, what)
+    if y.dim() == 1:
+        if y.shape[0] != A:
+            raise ValueError(f"{what}: y must be (A,) or (N, A)")
+        return y, 0
+    if tuple(y.shape) != (N, A) or y.stride(1) != 1:
+        raise ValueError(f"{what}: y must be (A,) or (N, A) with contiguous rows")
+    return y, y.stride(0)
+
+
+def _forget_deferred(ctx, def_clock, def_state, N, A, what):
+    """-> (ptr, state ptr, D, keep tensor or None)"""
+    if def_clock is None or def_clock.shape[0] == 0:
+        return None, None, 0, None
+    ctx.check_tensor(def_clock, what)
+    D = def_clock.shape[0]
+    if tuple(def_clock.shape) != (D, A) or not def_clock.is_contiguous():
+        raise ValueError(f"{what}: def_clock must be a contiguous (D, A) tensor")
+    if (def_state is None or def_state.dtype not in (torch.int32, torch.uint32) or tuple(def_state.shape) != (D,)
+            or def_state.device != def_clock.device or not def_state.is_contiguous()):
+        raise ValueError(f"{what}: def_state must be a contiguous (D,) int32 tensor on the same device")
+    keep = torch.empty(D, dtype=torch.uint8, device=def_clock.device)
+    return def_clock.data_ptr(), def_state.data_ptr(), D, keep
+
+
+def forget_batch(clock: torch.Tensor, entries: torch.Tensor, y: torch.Tensor, def_clock: Optional[torch.Tensor] = None,
+                 def_state: Optional[torch.Tensor] = None, ctx: Optional[Context] = None) -> Optional[torch.Tensor]:
+    """Causal::forget of N Orswot states in place (orswot.rs:150-183): clock (N, A), entries
+    (N, M, A), y (A,) shared or (N, A) per state, deferred rm clocks def_clock (D, A) of states
+    def_state (D,) int32.  Returns def_keep (D,) uint8 (0 = that remove was forgotten) or None."""
+    ctx = ctx or Context.default(clock.device.index)
+    ctx.check_tensor(clock, "orswot.forget_batch(clock)")
+    ctx.check_tensor(entries, "orswot.forget_batch(entries)")
+    if clock.dim() != 2 or entries.dim() != 3 or clock.stride(1) != 1 or entries.stride(2) != 1:
+        raise ValueError("orswot.forget_batch: clock (N, A), entries (N, M, A) with the actor axis contiguous")
+    N, A = clock.shape
+    M = entries.shape[1]
+    if entries.shape[0] != N or entries.shape[2] != A:
+        raise ValueError("orswot.forget_batch: entries do not match clock")
+    y, ys = _forget_clock(ctx, y, N, A, "orswot.forget_batch(y)")
+    dp, sp, D, keep = _forget_deferred(ctx, def_clock, def_state, N, A, "orswot.forget_batch(def_clock)")
+    ctx.call("crdt_orswot_forget_batch", clock.data_ptr(), clock.stride(0), entries.data_ptr(), entries.stride(1),
+             entries.stride(0), N, M, A, y.data_ptr(), ys, dp, sp, D, keep.data_ptr() if keep is not None else None)
+    return keep

@@ -1,0 +1,195 @@
+// Batched Causal::forget of whole Orswot and Map<K, MVReg> states: state s
+// forgets the clock y_s, in place.  Every piece is VClock::forget (vclock.rs:95-105: keep x[a]
+// iff x[a] > y[a]) on a dense row; what makes it a state op is the bookkeeping the reference
+// does around it:
+//   Orswot::forget (orswot.rs:150-183): clock, every entry clock (an emptied entry is dropped =
+//       an all-zero row), every deferred rm clock (an emptied one is dropped: keep[d] = 0).
+//   Map::forget (map.rs:85-114): every entry clock and its MVReg (MVReg::forget mvreg.rs:88-104
+//       drops a value whose clock empties); the entry is dropped iff its own clock empties (then
+//       its values go too), deferred rm clocks as for Orswot, then the map clock.
+// Rows are processed by LR-lane groups (causal.hip's row-group shape): HBM-bound streaming,
+// read + write of every row.
+#include "common.hpp"
+
+namespace crdt {
+
+struct ForgetPlan {
+  u64 *x;
+  const u64 *y;
+  unsigned long long nrows, per_state, sstride, rstride, ystride, A;
+  const uint32_t *ysel;  // row -> state (deferred pools); null: state = row / per_state
+  unsigned long long nstates;  // rows naming a state >= nstates are left untouched (keep = 1)
+  uint8_t *keep;         // row nonempty after forget (may be null)
+  int lr_log, vec2;
+};
+
+__device__ __forceinline__ u64 fgt(u64 x, u64 y) { return x > y ? x : 0ull; }
+
+// Bits g*LR of the LR-lane groups with any bit set in m.
+__device__ __forceinline__ u64 group_any(u64 m, int lr_log) {
+  for (int sh = 1; sh < (1 << lr_log); sh <<= 1) m |= m >> sh;
+  return m;
+}
+
+__global__ __launch_bounds__(kBlock) void forget_rows_kernel(ForgetPlan p) {
+  ROW_GROUP_LOOP(p.nrows, p.lr_log) {
+    const unsigned long long r = rb + (lane >> p.lr_log);
+    const unsigned long long rr = r < p.nrows ? r : p.nrows - 1;
+    const unsigned long long s = p.ysel ? p.ysel[rr] : rr / p.per_state;
+    const bool on = r < p.nrows && s < p.nstates;
+    u64 *xr = p.ysel ? p.x + rr * p.rstride : p.x + (rr / p.per_state) * p.sstride + (rr % p.per_state) * p.rstride;
+    const u64 *yr = p.y + (on ? s : 0) * p.ystride;
+    bool nz = false;
+    if (on) {
+      if (p.vec2) {
+#pragma unroll 4
+        for (unsigned long long c = 2ull * gl; c < p.A; c += 2ull * LR) {
+          u64x2 a = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(xr + c));
+          const u64x2 b = *reinterpret_cast<const u64x2 *>(yr + c);
+          a.x = fgt(a.x, b.x);
+          a.y = fgt(a.y, b.y);
+          nz |= (a.x | a.y) != 0;
+          __builtin_nontemporal_store(a, reinterpret_cast<u64x2 *>(xr + c));
+        }
+      } else {
+#pragma unroll 4
+        for (unsigned long long c = gl; c < p.A; c += LR) {
+          const u64 v = fgt(xr[c], yr[c]);
+          nz |= v != 0;
+          xr[c] = v;
+        }
+      }
+    }
+    if (p.keep) {
+      const u64 any = group_any(__ballot(nz), p.lr_log);
+      if (r < p.nrows && gl == 0) p.keep[r] = (uint8_t)(on ? (any >> lane) & 1 : 1);
+    }
+  }
+}
+
+struct MapForgetPlan {
+  u64 *ec, *vclk, *vval;
+  unsigned long long N, K, A, V, ec_s, vclk_s, vval_s;
+  const u64 *y;
+  unsigned long long ystride;
+  int lr_log;
+};
+
+// one (state, key) per LR-lane group: entry clock, then the key's V value slots
+__global__ __launch_bounds__(kBlock) void map_forget_kernel(MapForgetPlan p) {
+  const unsigned long long rows = p.N * p.K;
+  ROW_GROUP_LOOP(rows, p.lr_log) {
+    const unsigned long long r = rb + (lane >> p.lr_log);
+    const bool on = r < rows;
+    const unsigned long long rr = on ? r : rows - 1;
+    const unsigned long long s = rr / p.K, k = rr % p.K;
+    u64 *er = p.ec + s * p.ec_s + k * p.A;
+    const u64 *yr = p.y + s * p.ystride;
+    bool nz = false;
+    if (on)
+      for (unsigned long long c = gl; c < p.A; c += LR) {
+        const u64 v = fgt(er[c], yr[c]);
+        nz |= v != 0;
+        er[c] = v;
+      }
+    const bool alive = (group_any(__ballot(nz), p.lr_log) >> (lane & ~(LR - 1))) & 1;  // map.rs:93-98
+    for (unsigned long long j = 0; j < p.V; ++j) {
+      u64 *vr = p.vclk + s * p.vclk_s + (k * p.V + j) * p.A;
+      bool vz = false;
+      if (on)
+        for (unsigned long long c = gl; c < p.A; c += LR) {
+          const u64 v = alive ? fgt(vr[c], yr[c]) : 0ull;  // MVReg::forget mvreg.rs:88-104
+          vz |= v != 0;
+          vr[c] = v;
+        }
+      const bool keepv = (group_any(__ballot(vz), p.lr_log) >> (lane & ~(LR - 1))) & 1;
+      if (on && gl == 0 && !keepv) p.vval[s * p.vval_s + k * p.V + j] = 0;
+    }
+  }
+}
+
+static int lr_for(unsigned long long pieces) {
+  int lg = 0;
+  while (lg < 6 && (1ull << lg) < pieces) ++lg;
+  return lg;
+}
+
+static bool al16(const void *p) { return ((uintptr_t)p & 15) == 0; }
+
+static int launch_forget(crdt_ctx *ctx, ForgetPlan p) {
+  if (p.nrows == 0 || p.A == 0) return CRDT_OK;
+  p.vec2 = (p.A % 2 == 0) && (p.rstride % 2 == 0) && (p.sstride % 2 == 0 || p.ysel) && (p.ystride % 2 == 0) &&
+           al16(p.x) && al16(p.y);
+  p.lr_log = lr_for(p.vec2 ? (p.A + 1) / 2 : p.A);
+  const unsigned long long per_block = (kBlock >> p.lr_log) * 4;
+  const unsigned long long want = (p.nrows + per_block - 1) / per_block;
+  const unsigned long long cap = (unsigned long long)ctx->cu_count * 8;
+  hipLaunchKernelGGL(forget_rows_kernel, dim3((unsigned)(want < cap ? want : cap)), dim3(kBlock), 0, ctx->stream, p);
+  CRDT_HIP(ctx, hipGetLastError());
+  return CRDT_OK;
+}
+
+}  // namespace crdt
+
+using namespace crdt;
+
+extern "C" int crdt_orswot_forget_batch(crdt_ctx *ctx, uint64_t *clock, size_t clock_stride, uint64_t *entries,
+                                        size_t entry_mstride, size_t entry_sstride, size_t N, size_t M, size_t A,
+                                        const uint64_t *y, size_t y_stride, uint64_t *def_clock,
+                                        const uint32_t *def_state, size_t D, uint8_t *def_keep) {
+  CRDT_CHECK_CTX(ctx);
+  if (N == 0 || A == 0) return CRDT_OK;
+  if (!clock || !y || (M && !entries) || (D && (!def_clock || !def_state || !def_keep)))
+    return fail(ctx, CRDT_EINVAL, "orswot_forget_batch: NULL buffer");
+  if (clock_stride < A || (M && (entry_mstride < A || entry_sstride < M * entry_mstride)))
+    return fail(ctx, CRDT_EINVAL, "orswot_forget_batch: stride smaller than the rows it holds");
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  timing_begin(ctx, "forget_rows");
+  // entries of every state (orswot.rs:154-166), then the deferred rm clocks (:168-180)
+  if (M) {
+    int rc = launch_forget(ctx, ForgetPlan{(u64 *)entries, (const u64 *)y, N * M, M, entry_sstride, entry_mstride,
+                                           y_stride, A, nullptr, N, nullptr, 0, 0});
+    if (rc) return rc;
+  }
+  timing_end(ctx);
+  if (D) {
+    int rc = launch_forget(ctx, ForgetPlan{(u64 *)def_clock, (const u64 *)y, D, 1, A, A, y_stride, A, def_state,
+                                           N, def_keep, 0, 0});
+    if (rc) return rc;
+  }
+  // the clock last: y may alias a state's own clock row (forget by oneself empties the state)
+  return launch_forget(ctx, ForgetPlan{(u64 *)clock, (const u64 *)y, N, 1, clock_stride, clock_stride, y_stride, A,
+                                       nullptr, N, nullptr, 0, 0});
+}
+
+extern "C" int crdt_map_forget_batch(crdt_ctx *ctx, const crdt_map_states *m, const uint64_t *y, size_t y_stride,
+                                     uint64_t *def_clock, const uint32_t *def_state, size_t D, uint8_t *def_keep) {
+  CRDT_CHECK_CTX(ctx);
+  if (!m) return fail(ctx, CRDT_EINVAL, "map_forget_batch: NULL states");
+  const size_t N = m->N, K = m->K, A = m->A, V = m->V;
+  if (N == 0 || A == 0) return CRDT_OK;
+  if (!m->clock || !y || (K && (!m->ec || (V && (!m->vclk || !m->vval)))) ||
+      (D && (!def_clock || !def_state || !def_keep)))
+    return fail(ctx, CRDT_EINVAL, "map_forget_batch: NULL buffer");
+  if (m->clock_stride < A || (K && (m->ec_stride < K * A || (V && (m->vclk_stride < K * V * A || m->vval_stride < K * V)))))
+    return fail(ctx, CRDT_EINVAL, "map_forget_batch: stride smaller than the rows it holds");
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  if (K) {
+    MapForgetPlan p{(u64 *)m->ec, (u64 *)m->vclk, (u64 *)m->vval, N, K, A, V, m->ec_stride, m->vclk_stride, m->vval_stride,
+                    (const u64 *)y, y_stride, lr_for(A)};
+    const unsigned long long per_block = (kBlock >> p.lr_log) * 4;
+    const unsigned long long want = (N * K + per_block - 1) / per_block;
+    const unsigned long long cap = (unsigned long long)ctx->cu_count * 8;
+    timing_begin(ctx, "map_forget");
+    hipLaunchKernelGGL(map_forget_kernel, dim3((unsigned)(want < cap ? want : cap)), dim3(kBlock), 0, ctx->stream, p);
+    timing_end(ctx);
+    CRDT_HIP(ctx, hipGetLastError());
+  }
+  if (D) {
+    int rc = launch_forget(ctx, ForgetPlan{(u64 *)def_clock, (const u64 *)y, D, 1, A, A, y_stride, A, def_state,
+                                           N, def_keep, 0, 0});
+    if (rc) return rc;
+  }
+  return launch_forget(ctx, ForgetPlan{(u64 *)m->clock, (const u64 *)y, N, 1, m->clock_stride, m->clock_stride,
+                                       y_stride, A, nullptr, N, nullptr, 0, 0});
+}
