@@ -13,8 +13,9 @@ The JSON line also carries
   roofline      the dominant kernel (lub_stream_kernel, both launches of the step), its
                 average launch duration from HIP events on the launch stream vs the algorithmic
                 bytes per launch (DESIGN.md §Measurement), against 8 TB/s;
-  cpu_baseline  the oracle's restated reference fold (VClock::merge over ordered maps, one
-                core) on a bounded sample of the same workload (rank 0 at N=1 only).
+  cpu_baseline  the oracle's restated reference fold (VClock::merge over ordered maps) on a
+                bounded sample of the same workload, split over the host's threads (up to 16),
+                plus the one-thread figure (rank 0 at N=1 only).
 """
 import argparse
 import json
@@ -47,32 +48,53 @@ def parse():
     return ap.parse_args()
 
 
+def cpu_threads():
+    """Host threads for the CPU baseline: the CPUs this process may run on, at most 16 (the
+    GPU box's CPU share; os.cpu_count() there reports the whole machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
 def cpu_baseline(args):
     """Restated reference fold (oracle, 'port'): VClock::merge (vclock.rs:130-136) over ordered
-    maps for GCounter rows and P/N pairs for PNCounter rows, one thread, bounded sample."""
+    maps for GCounter rows and P/N pairs for PNCounter rows, on a bounded sample of the same
+    synthetic input — split over the host's threads (partials merged at the end, SURVEY §8d
+    CPU timing (2)), and on one thread for reference."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
 
-    sample = 16384
-    done_rows, fold_s, reps = 0, 0.0, 0
-    t_start = time.time()
-    while fold_s < args.cpu_seconds and time.time() - t_start < 4 * args.cpu_seconds:
-        row0 = reps * sample
-        g = O.synth_matrix(SEED_G, sample, args.actors, 0, row0=row0)
-        _, tg = O.vclock_fold(g)
-        p = O.synth_matrix(SEED_P, sample, 2 * args.actors, 0, row0=row0)
-        _, tp = O.pncounter_fold(p)
-        fold_s += tg + tp
-        done_rows += 2 * sample
-        reps += 1
+    T = cpu_threads()
+
+    def run(threads, per_thread, seconds):
+        done_rows, fold_s, reps = 0, 0.0, 0
+        t_start = time.time()
+        while fold_s < seconds and time.time() - t_start < 4 * seconds:
+            n = per_thread * threads
+            row0 = reps * n
+            g = O.synth_matrix(SEED_G, n, args.actors, 0, row0=row0)
+            _, tg = O.counter_fold_mt(g, False, threads)
+            p = O.synth_matrix(SEED_P, n, 2 * args.actors, 0, row0=row0)
+            _, tp = O.counter_fold_mt(p, True, threads)
+            fold_s += tg + tp
+            done_rows += 2 * n
+            reps += 1
+        return done_rows / fold_s, reps, fold_s
+
+    v1, reps1, s1 = run(1, 16384, args.cpu_seconds / 2)
+    vT, repsT, sT = run(T, 4096, args.cpu_seconds)
     return {
-        "value": done_rows / fold_s,
+        "value": vT,
         "unit": "replica-merges/s",
-        "cores": 1,
+        "cores": T,
         "kind": "port",
-        "sample": (f"{reps} x ({sample} GCounter x {args.actors} + {sample} PNCounter x 2x{args.actors}) "
-                   f"replicas of the same synthetic input, left fold of the restated VClock::merge over "
-                   f"std::map (oracle/ref_fold.cpp), 1 thread, map ingest excluded; {fold_s:.2f} s of fold"),
+        "sample": (f"{repsT} x ({T}x4096 GCounter x {args.actors} + {T}x4096 PNCounter x 2x{args.actors}) replicas "
+                   f"of the same synthetic input, left fold of the restated VClock::merge over std::map "
+                   f"(oracle/ref_fold.cpp) split over {T} threads + final merge of the partials, map ingest "
+                   f"excluded; {sT:.2f} s of fold"),
+        "single_core": {"value": v1, "cores": 1, "sample": f"{reps1} x (16384 + 16384) replicas, {s1:.2f} s of fold"},
     }
 
 

@@ -735,6 +735,8 @@ def lib():
         L.oracle_map_fold.restype = ctypes.c_double
         L.oracle_orswot_apply_streams.argtypes = [S, S, S, P, P, P, P, P, P, P, P, P, P, P]
         L.oracle_orswot_apply_streams.restype = ctypes.c_double
+        L.oracle_counter_fold_mt.argtypes = [P, S, S, S, ctypes.c_int, ctypes.c_int, P]
+        L.oracle_counter_fold_mt.restype = ctypes.c_double
         _LIB = L
     return _LIB
 
@@ -753,6 +755,16 @@ def vclock_fold(rows: np.ndarray) -> Tuple[np.ndarray, float]:
     R, A = rows.shape
     out = np.zeros(A, dtype=np.uint64)
     t = lib().oracle_vclock_fold(_p(rows), R, A, A, _p(out))
+    return out, t
+
+
+def counter_fold_mt(rows: np.ndarray, pn: bool, threads: int) -> Tuple[np.ndarray, float]:
+    """The restated GCounter (pn=False) / PNCounter (pn=True, rows P | N) left fold split over
+    `threads` host threads, partials merged at the end (oracle_counter_fold_mt)."""
+    rows = _c64(rows)
+    out = np.zeros(rows.shape[1], np.uint64)
+    t = lib().oracle_counter_fold_mt(_p(rows), rows.shape[0], rows.shape[1], rows.shape[1], int(pn), int(threads),
+                                     _p(out))
     return out, t
 
 

@@ -10,7 +10,9 @@
 // checker and by bench.py as the `cpu_baseline` (kind "port").
 //
 // Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg load this library.
+#include <atomic>
 #include <chrono>
+#include <thread>
 #include <cstdint>
 #include <cstring>
 #include <map>
@@ -350,6 +352,48 @@ double oracle_pncounter_fold(const uint64_t *rows, size_t R, size_t A, size_t st
   double t1 = now_s();
   vclock_to_row(p, out, A);
   vclock_to_row(n, out + A, A);
+  return t1 - t0;
+}
+
+// The same left fold split over `threads` host threads (SURVEY §8d CPU timing (2)): thread t
+// folds rows [t*R/T, (t+1)*R/T) from T::new(), then the T partials are merged in thread order
+// (merge is a join: any split gives the same result).  pn = 1: rows are PNCounter P | N halves
+// of W/2 counters each.  Ingest into maps runs before the clock starts; the timed region is
+// the parallel fold plus the final combine.  Returns seconds.
+double oracle_counter_fold_mt(const uint64_t *rows, size_t R, size_t W, size_t stride, int pn, int threads,
+                              uint64_t *out) {
+  const size_t T = threads < 1 ? 1 : (size_t)threads;
+  const size_t H = pn ? W / 2 : W;
+  std::vector<std::vector<VClock>> in_p(T), in_n(T);
+  std::vector<VClock> acc_p(T), acc_n(T);
+  std::atomic<int> ready{0}, go{0};
+  std::vector<std::thread> pool;
+  for (size_t t = 0; t < T; ++t)
+    pool.emplace_back([&, t] {
+      const size_t lo = t * R / T, hi = (t + 1) * R / T;
+      for (size_t r = lo; r < hi; ++r) {
+        in_p[t].push_back(vclock_from_row(rows + r * stride, H));
+        if (pn) in_n[t].push_back(vclock_from_row(rows + r * stride + H, H));
+      }
+      ready.fetch_add(1);
+      while (!go.load(std::memory_order_acquire)) std::this_thread::yield();
+      for (size_t i = 0; i < in_p[t].size(); ++i) {
+        acc_p[t].merge(std::move(in_p[t][i]));  // gcounter.rs:44-48 / vclock.rs:130-136
+        if (pn) acc_n[t].merge(std::move(in_n[t][i]));  // pncounter.rs:70-75
+      }
+    });
+  while (ready.load() < (int)T) std::this_thread::yield();
+  double t0 = now_s();
+  go.store(1, std::memory_order_release);
+  for (auto &th : pool) th.join();
+  VClock p, n;
+  for (size_t t = 0; t < T; ++t) {
+    p.merge(std::move(acc_p[t]));
+    if (pn) n.merge(std::move(acc_n[t]));
+  }
+  double t1 = now_s();
+  vclock_to_row(p, out, H);
+  if (pn) vclock_to_row(n, out + H, H);
   return t1 - t0;
 }
 
