@@ -31,33 +31,104 @@ __device__ __forceinline__ u64 group_any(u64 m, int lr_log) {
   return m;
 }
 
+// Row r -> its state and its row pointer.
+__device__ __forceinline__ u64 *forget_row_ptr(const ForgetPlan &p, unsigned long long r, unsigned long long &s) {
+  s = p.ysel ? p.ysel[r] : r / p.per_state;
+  return p.ysel ? p.x + r * p.rstride : p.x + (r / p.per_state) * p.sstride + (r % p.per_state) * p.rstride;
+}
+
+// Row width <= 64 pieces: LR = pow2 >= pieces lanes per row (one coalesced access per row), and
+// kU row groups per lane in flight at once (ILP across rows, not within a row).
+constexpr int kU = 4;
+
 __global__ __launch_bounds__(kBlock) void forget_rows_kernel(ForgetPlan p) {
+  const int lane = threadIdx.x % kWave;
+  const int LR = 1 << p.lr_log;
+  const int gl = lane & (LR - 1);
+  const unsigned long long RW = kWave >> p.lr_log;
+  const unsigned long long w0 = (blockIdx.x * (unsigned long long)kBlock + threadIdx.x) / kWave;
+  const unsigned long long nw = (unsigned long long)gridDim.x * (kBlock / kWave);
+  const unsigned long long W = p.vec2 ? (p.A + 1) / 2 : p.A;  // pieces per row
+  for (unsigned long long rb = w0 * RW * kU; rb < p.nrows; rb += nw * RW * kU) {
+    u64 *xr[kU];
+    const u64 *yr[kU];
+    bool on[kU];
+#pragma unroll
+    for (int j = 0; j < kU; ++j) {
+      const unsigned long long r = rb + j * RW + (lane >> p.lr_log);
+      unsigned long long s = 0;
+      xr[j] = forget_row_ptr(p, r < p.nrows ? r : p.nrows - 1, s);
+      on[j] = r < p.nrows && s < p.nstates && (unsigned long long)gl < W;
+      yr[j] = p.y + (on[j] ? s : 0) * p.ystride;
+    }
+    bool nz[kU];
+    if (p.vec2) {
+      u64x2 a[kU], b[kU];
+#pragma unroll
+      for (int j = 0; j < kU; ++j)
+        if (on[j]) {
+          a[j] = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(xr[j] + 2 * gl));
+          b[j] = *reinterpret_cast<const u64x2 *>(yr[j] + 2 * gl);
+        }
+#pragma unroll
+      for (int j = 0; j < kU; ++j) {
+        nz[j] = false;
+        if (on[j]) {
+          a[j].x = fgt(a[j].x, b[j].x);
+          a[j].y = fgt(a[j].y, b[j].y);
+          nz[j] = (a[j].x | a[j].y) != 0;
+          __builtin_nontemporal_store(a[j], reinterpret_cast<u64x2 *>(xr[j] + 2 * gl));
+        }
+      }
+    } else {
+      u64 a[kU], b[kU];
+#pragma unroll
+      for (int j = 0; j < kU; ++j)
+        if (on[j]) {
+          a[j] = xr[j][gl];
+          b[j] = yr[j][gl];
+        }
+#pragma unroll
+      for (int j = 0; j < kU; ++j) {
+        nz[j] = false;
+        if (on[j]) {
+          a[j] = fgt(a[j], b[j]);
+          nz[j] = a[j] != 0;
+          xr[j][gl] = a[j];
+        }
+      }
+    }
+    if (p.keep) {
+#pragma unroll
+      for (int j = 0; j < kU; ++j) {
+        const unsigned long long r = rb + j * RW + (lane >> p.lr_log);
+        const u64 any = group_any(__ballot(nz[j]), p.lr_log);
+        if (r < p.nrows && gl == 0) {
+          unsigned long long s = 0;
+          (void)forget_row_ptr(p, r, s);
+          p.keep[r] = (uint8_t)(s < p.nstates ? (any >> lane) & 1 : 1);
+        }
+      }
+    }
+  }
+}
+
+// Rows wider than 64 pieces: LR = 64 lanes walk the row.
+__global__ __launch_bounds__(kBlock) void forget_wide_rows_kernel(ForgetPlan p) {
   ROW_GROUP_LOOP(p.nrows, p.lr_log) {
     const unsigned long long r = rb + (lane >> p.lr_log);
     const unsigned long long rr = r < p.nrows ? r : p.nrows - 1;
-    const unsigned long long s = p.ysel ? p.ysel[rr] : rr / p.per_state;
+    unsigned long long s = 0;
+    u64 *xr = forget_row_ptr(p, rr, s);
     const bool on = r < p.nrows && s < p.nstates;
-    u64 *xr = p.ysel ? p.x + rr * p.rstride : p.x + (rr / p.per_state) * p.sstride + (rr % p.per_state) * p.rstride;
     const u64 *yr = p.y + (on ? s : 0) * p.ystride;
     bool nz = false;
     if (on) {
-      if (p.vec2) {
 #pragma unroll 4
-        for (unsigned long long c = 2ull * gl; c < p.A; c += 2ull * LR) {
-          u64x2 a = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(xr + c));
-          const u64x2 b = *reinterpret_cast<const u64x2 *>(yr + c);
-          a.x = fgt(a.x, b.x);
-          a.y = fgt(a.y, b.y);
-          nz |= (a.x | a.y) != 0;
-          __builtin_nontemporal_store(a, reinterpret_cast<u64x2 *>(xr + c));
-        }
-      } else {
-#pragma unroll 4
-        for (unsigned long long c = gl; c < p.A; c += LR) {
-          const u64 v = fgt(xr[c], yr[c]);
-          nz |= v != 0;
-          xr[c] = v;
-        }
+      for (unsigned long long c = gl; c < p.A; c += LR) {
+        const u64 v = fgt(xr[c], yr[c]);
+        nz |= v != 0;
+        xr[c] = v;
       }
     }
     if (p.keep) {
@@ -108,10 +179,59 @@ __global__ __launch_bounds__(kBlock) void map_forget_kernel(MapForgetPlan p) {
   }
 }
 
-static int lr_for(unsigned long long pieces) {
-  int lg = 0;
-  while (lg < 6 && (1ull << lg) < pieces) ++lg;
-  return lg;
+// grid: workgroups per CU (CRDT_TUNE rows_blocks_per_cu, else 4), never more than the rows need
+static unsigned forget_grid(crdt_ctx *ctx, unsigned long long rows, int lr_log) {
+  const unsigned long long per_block = kBlock >> lr_log;
+  const unsigned long long want = (rows + per_block - 1) / per_block;
+  const int bpc = ctx->tune.rows_blocks_per_cu > 0 ? ctx->tune.rows_blocks_per_cu : 4;
+  const unsigned long long cap = (unsigned long long)ctx->cu_count * bpc;
+  return (unsigned)(want < cap ? want : cap);
+}
+
+// A <= 64 and V <= 4: one word per lane, kU (state, key) rows per lane group in flight at once
+// (entry clock, value clocks and y of all of them loaded before any vote).
+__global__ __launch_bounds__(kBlock) void map_forget_narrow_kernel(MapForgetPlan p) {
+  const unsigned long long rows = p.N * p.K;
+  const int lane = threadIdx.x % kWave;
+  const int LR = 1 << p.lr_log;
+  const int gl = lane & (LR - 1);
+  const unsigned long long RW = kWave >> p.lr_log;
+  const unsigned long long w0 = (blockIdx.x * (unsigned long long)kBlock + threadIdx.x) / kWave;
+  const unsigned long long nw = (unsigned long long)gridDim.x * (kBlock / kWave);
+  for (unsigned long long rb = w0 * RW * kU; rb < rows; rb += nw * RW * kU) {
+    u64 *er[kU], *vr[kU];
+    u64 ev[kU], yv[kU], vv[kU][4];
+    bool act[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const unsigned long long r = rb + u * RW + (lane >> p.lr_log);
+      const unsigned long long rr = r < rows ? r : rows - 1;
+      const unsigned long long s = rr / p.K, k = rr % p.K;
+      act[u] = r < rows && (unsigned long long)gl < p.A;
+      er[u] = p.ec + s * p.ec_s + k * p.A + gl;
+      vr[u] = p.vclk + s * p.vclk_s + k * p.V * p.A + gl;
+      yv[u] = act[u] ? p.y[s * p.ystride + gl] : 0ull;
+      ev[u] = act[u] ? *er[u] : 0ull;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) vv[u][j] = (act[u] && (unsigned long long)j < p.V) ? vr[u][j * p.A] : 0ull;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const unsigned long long r = rb + u * RW + (lane >> p.lr_log);
+      const unsigned long long rr = r < rows ? r : rows - 1;
+      const u64 e = fgt(ev[u], yv[u]);
+      const bool alive = (group_any(__ballot(e != 0), p.lr_log) >> (lane & ~(LR - 1))) & 1;  // map.rs:93-98
+      if (act[u]) *er[u] = e;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if ((unsigned long long)j >= p.V) break;
+        const u64 v = alive ? fgt(vv[u][j], yv[u]) : 0ull;  // MVReg::forget mvreg.rs:88-104
+        if (act[u]) vr[u][j * p.A] = v;
+        const bool keepv = (group_any(__ballot(v != 0), p.lr_log) >> (lane & ~(LR - 1))) & 1;
+        if (r < rows && gl == 0 && !keepv) p.vval[(rr / p.K) * p.vval_s + (rr % p.K) * p.V + j] = 0;
+      }
+    }
+  }
 }
 
 static bool al16(const void *p) { return ((uintptr_t)p & 15) == 0; }
@@ -120,11 +240,18 @@ static int launch_forget(crdt_ctx *ctx, ForgetPlan p) {
   if (p.nrows == 0 || p.A == 0) return CRDT_OK;
   p.vec2 = (p.A % 2 == 0) && (p.rstride % 2 == 0) && (p.sstride % 2 == 0 || p.ysel) && (p.ystride % 2 == 0) &&
            al16(p.x) && al16(p.y);
-  p.lr_log = lr_for(p.vec2 ? (p.A + 1) / 2 : p.A);
-  const unsigned long long per_block = (kBlock >> p.lr_log) * 4;
-  const unsigned long long want = (p.nrows + per_block - 1) / per_block;
-  const unsigned long long cap = (unsigned long long)ctx->cu_count * 8;
-  hipLaunchKernelGGL(forget_rows_kernel, dim3((unsigned)(want < cap ? want : cap)), dim3(kBlock), 0, ctx->stream, p);
+  const unsigned long long W = p.vec2 ? (p.A + 1) / 2 : p.A;
+  if (W <= (unsigned long long)kWave) {
+    p.lr_log = 0;
+    while ((1ull << p.lr_log) < W) ++p.lr_log;
+    hipLaunchKernelGGL(forget_rows_kernel, dim3(forget_grid(ctx, (p.nrows + kU - 1) / kU, p.lr_log)), dim3(kBlock), 0,
+                       ctx->stream, p);
+  } else {
+    p.vec2 = 0;
+    p.lr_log = 6;
+    hipLaunchKernelGGL(forget_wide_rows_kernel, dim3(forget_grid(ctx, p.nrows, p.lr_log)), dim3(kBlock), 0,
+                       ctx->stream, p);
+  }
   CRDT_HIP(ctx, hipGetLastError());
   return CRDT_OK;
 }
@@ -176,12 +303,14 @@ extern "C" int crdt_map_forget_batch(crdt_ctx *ctx, const crdt_map_states *m, co
   CRDT_HIP(ctx, hipSetDevice(ctx->device));
   if (K) {
     MapForgetPlan p{(u64 *)m->ec, (u64 *)m->vclk, (u64 *)m->vval, N, K, A, V, m->ec_stride, m->vclk_stride, m->vval_stride,
-                    (const u64 *)y, y_stride, lr_for(A)};
-    const unsigned long long per_block = (kBlock >> p.lr_log) * 4;
-    const unsigned long long want = (N * K + per_block - 1) / per_block;
-    const unsigned long long cap = (unsigned long long)ctx->cu_count * 8;
+                    (const u64 *)y, y_stride, 0};
+    while (p.lr_log < 6 && (1ull << p.lr_log) < A) ++p.lr_log;  // a key's rows: one access per row
     timing_begin(ctx, "map_forget");
-    hipLaunchKernelGGL(map_forget_kernel, dim3((unsigned)(want < cap ? want : cap)), dim3(kBlock), 0, ctx->stream, p);
+    if (A <= (size_t)kWave && V <= 4)
+      hipLaunchKernelGGL(map_forget_narrow_kernel, dim3(forget_grid(ctx, (N * K + kU - 1) / kU, p.lr_log)),
+                         dim3(kBlock), 0, ctx->stream, p);
+    else
+      hipLaunchKernelGGL(map_forget_kernel, dim3(forget_grid(ctx, N * K, p.lr_log)), dim3(kBlock), 0, ctx->stream, p);
     timing_end(ctx);
     CRDT_HIP(ctx, hipGetLastError());
   }
