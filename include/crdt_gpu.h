@@ -243,6 +243,37 @@ typedef struct crdt_map_states {
 int crdt_map_forget_batch(crdt_ctx *ctx, const crdt_map_states *states, const uint64_t *y, size_t y_stride,
                           uint64_t *def_clock, const uint32_t *def_state, size_t D, uint8_t *def_keep);
 
+/* Batched Map<K, MVReg<u64>> CmRDT::apply (map.rs:119-137, apply_keyset_rm :318-348,
+ * apply_deferred :311-316, MVReg::apply mvreg.rs:130-166): state s applies its ops
+ * [op_off[s], op_off[s+1]) in order, in place, on the crdt_map_states layout (value slots in Vec
+ * order, empty slot <=> all-zero clock; an append goes after the last used slot, compacting the
+ * slots when that one is the last).  Deferred removes: def_count[s] <= Dcap slots, rm clock
+ * def_clock[(s*Dcap + d)*A + a], key bitmap def_keys[(s*Dcap + d)*Kw + w], Kw = ceil(K/64).
+ * Ops: kind 0 = Op::Up { dot: (actor, counter), key, op: Put { clock: clk_pool[clk_row*A ..],
+ * val } }, kind 1 = Op::Rm { clock: clk_pool[clk_row*A ..], keyset: keys[key_off[o] ..
+ * key_off[o+1]) } (key_off: n_ops+1 entries, may be NULL when no op is an Rm).
+ * status[s]: bit 0 = deferred slots exhausted, bit 1 = an out-of-range op / key skipped,
+ * bits 2-3 = invalid input (state untouched), bit 4 = a register needed more than V values (the
+ * state is incomplete: retry with more slots).  Limits: A <= 256, 1 <= V <= 8,
+ * Dcap*(A + Kw)*8 <= 65536. */
+typedef struct crdt_map_ops {
+  size_t n_ops;
+  const uint64_t *op_off;   /* [N+1]       */
+  const uint8_t *kind;      /* [n_ops]     */
+  const uint32_t *actor;    /* [n_ops] Up  */
+  const uint64_t *counter;  /* [n_ops] Up  */
+  const uint32_t *key;      /* [n_ops] Up  */
+  const uint64_t *val;      /* [n_ops] Up  */
+  const uint32_t *clk_row;  /* [n_ops]     */
+  const uint64_t *clk_pool; /* [n_clk_rows][A] */
+  size_t n_clk_rows;
+  const uint64_t *key_off;  /* [n_ops+1] Rm */
+  const uint32_t *keys;
+} crdt_map_ops;
+
+int crdt_map_apply_batch(crdt_ctx *ctx, const crdt_map_states *states, uint64_t *def_clock, uint64_t *def_keys,
+                         uint32_t *def_count, size_t Dcap, const crdt_map_ops *ops, uint32_t *status);
+
 /* ---- multi-GPU: replica-sharded lub over RCCL ----------------------------
  * One process (one ctx) per GPU.  Rank 0 calls crdt_comm_unique_id and sends the 128 bytes to
  * every rank over the caller's own channel; every rank then calls crdt_ctx_comm_init (collective:

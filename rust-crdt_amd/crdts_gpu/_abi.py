@@ -38,7 +38,7 @@ EXPORTS = (
     "crdt_comm_unique_id", "crdt_ctx_comm_init", "crdt_ctx_comm_destroy", "crdt_ctx_comm_info",
     "crdt_vclock_lub_many_sharded", "crdt_gcounter_lub_many_sharded", "crdt_pncounter_lub_many_sharded",
     "crdt_gset_lub_many_sharded", "crdt_orswot_lub_many_sharded",
-    "crdt_orswot_forget_batch", "crdt_map_forget_batch",
+    "crdt_orswot_forget_batch", "crdt_map_forget_batch", "crdt_map_apply_batch",
 )
 
 
@@ -97,6 +97,11 @@ class MapStates(ctypes.Structure):  # crdt_map_states
                 ("ec_stride", S), ("vclk", P), ("vclk_stride", S), ("vval", P), ("vval_stride", S)]
 
 
+class MapOps(ctypes.Structure):  # crdt_map_ops
+    _fields_ = [("n_ops", S), ("op_off", P), ("kind", P), ("actor", P), ("counter", P), ("key", P), ("val", P),
+                ("clk_row", P), ("clk_pool", P), ("n_clk_rows", S), ("key_off", P), ("keys", P)]
+
+
 class MapBatch(ctypes.Structure):  # crdt_map_batch
     _fields_ = [
         ("G", S), ("R", S), ("K", S), ("A", S), ("V", S),
@@ -147,6 +152,7 @@ _SIGS = {
 _SIGS.update({
     "crdt_orswot_forget_batch": ([P, P, S, P, S, S, S, S, S, P, S, P, P, S, P], ctypes.c_int),
     "crdt_map_forget_batch": ([P, ctypes.POINTER(MapStates), P, S, P, P, S, P], ctypes.c_int),
+    "crdt_map_apply_batch": ([P, ctypes.POINTER(MapStates), P, P, P, S, ctypes.POINTER(MapOps), P], ctypes.c_int),
     "crdt_comm_unique_id": ([P], ctypes.c_int),
     "crdt_ctx_comm_init": ([P, P, ctypes.c_int, ctypes.c_int], ctypes.c_int),
     "crdt_ctx_comm_destroy": ([P], ctypes.c_int),

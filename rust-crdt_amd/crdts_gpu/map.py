@@ -198,3 +198,127 @@ def forget_batch(clock: torch.Tensor, ec: torch.Tensor, vclk: torch.Tensor, vval
     ctx.call("crdt_map_forget_batch", ctypes.byref(st), y.data_ptr(), ys, dp, sp, D,
              keep.data_ptr() if keep is not None else None)
     return keep
+
+
+# ---------------------------------------------------------------------------------------------
+# Batched CmRDT::apply (map.rs:119-137, apply_keyset_rm :318-348, MVReg::apply mvreg.rs:130-166)
+# ---------------------------------------------------------------------------------------------
+class MapOpBatch(NamedTuple):
+    """Device op streams (crdt_map_ops): state s applies ops [op_off[s], op_off[s+1]) in order."""
+    op_off: torch.Tensor    # (N+1,) int64
+    kind: torch.Tensor      # (n_ops,) uint8: 0 = Op::Up, 1 = Op::Rm
+    actor: torch.Tensor     # (n_ops,) int32   Up: dot.actor
+    counter: torch.Tensor   # (n_ops,) int64   Up: dot.counter
+    key: torch.Tensor       # (n_ops,) int32   Up: key
+    val: torch.Tensor       # (n_ops,) int64   Up: Put.val
+    clk_row: torch.Tensor   # (n_ops,) int32   row of clk_pool: Put.clock (Up) / rm clock (Rm)
+    clk_pool: torch.Tensor  # (n_clk, A) int64
+    key_off: torch.Tensor   # (n_ops+1,) int64 Rm keysets
+    keys: torch.Tensor      # (n_keys,) int32
+
+
+def encode_ops(streams, A: int, device) -> MapOpBatch:
+    """Host ingest of per-state op streams (interned to dense indices): ("up", actor, counter,
+    key, put_clock, val) for Op::Up { dot, key, op: MVReg Op::Put { clock, val } } or
+    ("rm", clock, keys) for Op::Rm { clock, keyset } (map.rs:51-66, mvreg.rs:38-47); clocks are
+    mappings actor -> counter or dense rows of A counters."""
+    def row(clk):
+        r = np.zeros(A, dtype=np.uint64)
+        if hasattr(clk, "items"):
+            for a, c in clk.items():
+                r[int(a)] = np.uint64(c)
+        else:
+            r[:] = np.asarray(clk, dtype=np.uint64)
+        return r
+
+    op_off, kind, actor, counter, key, val, clk_row, key_off, keys, pool = [0], [], [], [], [], [], [], [0], [], []
+    for ops in streams:
+        for op in ops:
+            if op[0] == "up":
+                _, a, k, kk, pc, v = op
+                kind.append(0)
+                actor.append(int(a))
+                counter.append(int(k))
+                key.append(int(kk))
+                val.append(int(v))
+                clk_row.append(len(pool))
+                pool.append(row(pc))
+            elif op[0] == "rm":
+                _, rc, ks = op
+                kind.append(1)
+                actor.append(0)
+                counter.append(0)
+                key.append(0)
+                val.append(0)
+                clk_row.append(len(pool))
+                pool.append(row(rc))
+                keys.extend(int(x) for x in ks)
+            else:
+                raise ValueError(f"map.encode_ops: unknown op {op[0]!r}")
+            key_off.append(len(keys))
+        op_off.append(len(kind))
+    pool.append(np.zeros(A, dtype=np.uint64))  # pads: never-empty device buffers
+    keys.append(0)
+
+    def t(x, dt):
+        return torch.from_numpy(np.asarray(x, dtype=dt)).to(device)
+
+    u64 = lambda x: t(np.array(x, dtype=np.uint64).view(np.int64), np.int64)  # noqa: E731
+    return MapOpBatch(t(op_off, np.int64), t(kind, np.uint8), t(actor, np.int32), u64(counter), t(key, np.int32),
+                      u64(val), t(clk_row, np.int32),
+                      torch.from_numpy(np.stack(pool).view(np.int64)).to(device), t(key_off, np.int64),
+                      t(keys, np.int32))
+
+
+def apply_batch(clock: torch.Tensor, ec: torch.Tensor, vclk: torch.Tensor, vval: torch.Tensor,
+                def_clock: torch.Tensor, def_keys: torch.Tensor, def_count: torch.Tensor, ops: MapOpBatch,
+                ctx: Optional[Context] = None) -> torch.Tensor:
+    """Apply every state's op stream in place: clock (N, A), ec (N, K, A), vclk (N, K, V, A),
+    vval (N, K, V), deferred slots def_clock (N, Dcap, A) / def_keys (N, Dcap, ceil(K/64)) /
+    def_count (N,) int32.  Returns the per-state status (N,) int32 (include/crdt_gpu.h)."""
+    ctx = ctx or Context.default(clock.device.index)
+    for t_, nm in ((clock, "clock"), (ec, "ec"), (vclk, "vclk"), (vval, "vval"), (def_clock, "def_clock"),
+                   (def_keys, "def_keys")):
+        ctx.check_tensor(t_, f"map.apply_batch({nm})")
+    N, A = clock.shape
+    K, V = vclk.shape[1], vclk.shape[2]
+    Kw = (K + 63) // 64
+    Dcap = def_clock.shape[1]
+    if (tuple(ec.shape) != (N, K, A) or tuple(vclk.shape) != (N, K, V, A) or tuple(vval.shape) != (N, K, V)
+            or clock.stride(1) != 1 or ec.stride(2) != 1 or ec.stride(1) != A or vclk.stride(3) != 1
+            or vclk.stride(2) != A or vclk.stride(1) != V * A or vval.stride(2) != 1 or vval.stride(1) != V):
+        raise ValueError("map.apply_batch: per-state blocks must be packed (K, A) / (K, V, A) / (K, V)")
+    if (tuple(def_clock.shape) != (N, Dcap, A) or tuple(def_keys.shape) != (N, Dcap, Kw)
+            or not def_clock.is_contiguous() or not def_keys.is_contiguous()):
+        raise ValueError("map.apply_batch: def_clock / def_keys must be contiguous (N, Dcap, A) / (N, Dcap, Kw)")
+    want = {"op_off": (torch.int64,), "kind": (torch.uint8,), "actor": (torch.int32,), "counter": (torch.int64,),
+            "key": (torch.int32,), "val": (torch.int64,), "clk_row": (torch.int32,), "clk_pool": (torch.int64,),
+            "key_off": (torch.int64,), "keys": (torch.int32,)}
+    for nm, t_ in list(zip(ops._fields, ops)) + [("def_count", def_count)]:
+        dts = want.get(nm, (torch.int32,))
+        if t_.device.type != "cuda" or t_.device.index != ctx.device or t_.dtype not in dts or not t_.is_contiguous():
+            raise ValueError(f"map.apply_batch({nm}): expected a contiguous cuda:{ctx.device} tensor of {dts}")
+    n = ops.kind.shape[0]
+    if (ops.op_off.shape[0] != N + 1 or ops.key_off.shape[0] != n + 1 or ops.clk_pool.dim() != 2
+            or ops.clk_pool.shape[1] != A or tuple(def_count.shape) != (N,)):
+        raise ValueError("map.apply_batch: op_off (N+1,), key_off (n_ops+1,), clk_pool (n, A), def_count (N,)")
+    for nm in ("actor", "counter", "key", "val", "clk_row"):
+        if getattr(ops, nm).shape[0] != n:
+            raise ValueError(f"map.apply_batch: ops.{nm} must have n_ops entries")
+    st = _abi.MapStates()
+    st.N, st.K, st.A, st.V = N, K, A, V
+    st.clock, st.clock_stride = clock.data_ptr(), clock.stride(0)
+    st.ec, st.ec_stride = ec.data_ptr(), ec.stride(0)
+    st.vclk, st.vclk_stride = vclk.data_ptr(), vclk.stride(0)
+    st.vval, st.vval_stride = vval.data_ptr(), vval.stride(0)
+    o = _abi.MapOps()
+    o.n_ops = n
+    o.op_off, o.kind, o.actor, o.counter = (ops.op_off.data_ptr(), ops.kind.data_ptr(), ops.actor.data_ptr(),
+                                            ops.counter.data_ptr())
+    o.key, o.val, o.clk_row, o.clk_pool = ops.key.data_ptr(), ops.val.data_ptr(), ops.clk_row.data_ptr(), \
+        ops.clk_pool.data_ptr()
+    o.n_clk_rows, o.key_off, o.keys = ops.clk_pool.shape[0], ops.key_off.data_ptr(), ops.keys.data_ptr()
+    status = torch.empty(N, dtype=torch.int32, device=clock.device)
+    ctx.call("crdt_map_apply_batch", ctypes.byref(st), def_clock.data_ptr(), def_keys.data_ptr(),
+             def_count.data_ptr(), Dcap, ctypes.byref(o), status.data_ptr())
+    return status

@@ -1,0 +1,391 @@
+// Batched Map<K, MVReg<u64>> CmRDT::apply: N independent states, each with its own ordered op
+// stream.  Reference (map.rs:119-137, apply_keyset_rm :318-348,
+// apply_deferred :311-316; MVReg::apply mvreg.rs:130-166, MVReg::forget :88-104), restated on
+// the dense layout of crdt_map_lub_many (entry clock EC[k][a], value slots VC[k][j][a] / VV[k][j]
+// in Vec order with empty slots skipped, deferred (rm clock, key set) slots):
+//   Op::Up { dot (a, k), key, op: Put { clock pc, val } }:
+//       if C[a] >= k: seen, no-op                                              (:123-126)
+//       EC[key][a] = max(EC[key][a], k)                      (entry().or_default(), clock.apply)
+//       MVReg::apply: if pc is empty: nothing; else drop every value whose clock is <= pc
+//           (partial_cmp not in {None, Greater}); append (pc, val) unless a remaining value's
+//           clock is > pc                                                 (mvreg.rs:130-166)
+//       C[a] = k; apply_deferred()                                              (:133-134)
+//   Op::Rm { clock rm, keyset }: apply_keyset_rm                                (:121, :318-348)
+//       for key in keyset: EC[key] = EC[key].forget(rm); if it empties the entry is dropped
+//           (values too), else every value clock forgets rm and an emptied value is dropped
+//       if !(rm <= C) (C.partial_cmp(rm) in {None, Less}): defer (rm, keyset), OR-ing the keys
+//           into an existing deferred with the identical clock
+// One wave per state (lanes = actors, A <= 256; the state's clock in registers, its deferred list
+// in LDS for the whole stream, entries and values in HBM), as orswot_apply.hip.
+#include "common.hpp"
+
+namespace crdt {
+
+constexpr int kMA = 4;  // clock words per lane (A <= 256)
+constexpr int kMaxV = 8;
+
+struct MapApplyPlan {
+  u64 *clock;
+  unsigned long long clock_s;
+  u64 *ec;
+  unsigned long long ec_s;
+  u64 *vclk;
+  unsigned long long vclk_s;
+  u64 *vval;
+  unsigned long long vval_s;
+  u64 *def_clock, *def_keys;
+  uint32_t *def_count;
+  unsigned long long N, K, A, V, Kw, Dcap;
+  const u64 *op_off;
+  const uint8_t *kind;
+  const uint32_t *actor;
+  const u64 *counter;
+  const uint32_t *key;
+  const u64 *val;
+  const uint32_t *clk_row;
+  const u64 *clk_pool;
+  unsigned long long n_clk_rows;
+  const u64 *key_off;
+  const uint32_t *keys;
+  unsigned long long n_ops;
+  uint32_t *status;
+  int wpb;
+};
+
+struct Row {
+  u64 w[kMA];
+};
+
+__device__ __forceinline__ Row load_row(const u64 *p, int lane, unsigned long long A) {
+  Row r;
+#pragma unroll
+  for (int j = 0; j < kMA; ++j) {
+    const unsigned long long a = lane + j * kWave;
+    r.w[j] = a < A ? p[a] : 0ull;
+  }
+  return r;
+}
+__device__ __forceinline__ void store_row(u64 *p, const Row &r, int lane, unsigned long long A) {
+#pragma unroll
+  for (int j = 0; j < kMA; ++j) {
+    const unsigned long long a = lane + j * kWave;
+    if (a < A) p[a] = r.w[j];
+  }
+}
+__device__ __forceinline__ bool any_nz(const Row &r) {
+  bool b = false;
+#pragma unroll
+  for (int j = 0; j < kMA; ++j) b |= r.w[j] != 0;
+  return __ballot(b) != 0;
+}
+// x <= y on every actor (padding lanes hold 0 on both sides)
+__device__ __forceinline__ bool all_le(const Row &x, const Row &y) {
+  bool b = false;
+#pragma unroll
+  for (int j = 0; j < kMA; ++j) b |= x.w[j] > y.w[j];
+  return __ballot(b) == 0;
+}
+__device__ __forceinline__ bool rows_eq(const Row &x, const Row &y) {
+  bool b = false;
+#pragma unroll
+  for (int j = 0; j < kMA; ++j) b |= x.w[j] != y.w[j];
+  return __ballot(b) == 0;
+}
+__device__ __forceinline__ Row forget_row(const Row &x, const Row &y) {  // vclock.rs:95-105
+  Row r;
+#pragma unroll
+  for (int j = 0; j < kMA; ++j) r.w[j] = x.w[j] > y.w[j] ? x.w[j] : 0ull;
+  return r;
+}
+__device__ __forceinline__ Row zero_row() {
+  Row r;
+#pragma unroll
+  for (int j = 0; j < kMA; ++j) r.w[j] = 0;
+  return r;
+}
+__device__ __forceinline__ unsigned rl32m(unsigned x, int l) { return (unsigned)__builtin_amdgcn_readlane((int)x, l); }
+__device__ __forceinline__ u64 rl64m(u64 x, int l) {
+  return ((u64)rl32m((unsigned)(x >> 32), l) << 32) | rl32m((unsigned)x, l);
+}
+__device__ __forceinline__ void wave_fence_m() { __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup"); }
+
+struct KeyRefs {
+  u64 *ec, *vc, *vv;
+};
+__device__ __forceinline__ KeyRefs key_refs(const MapApplyPlan &p, unsigned long long s, unsigned long long k) {
+  return KeyRefs{p.ec + s * p.ec_s + k * p.A, p.vclk + s * p.vclk_s + k * p.V * p.A, p.vval + s * p.vval_s + k * p.V};
+}
+
+// apply_keyset_rm's body for one key (map.rs:320-333)
+__device__ void key_rm(const MapApplyPlan &p, unsigned long long s, unsigned long long k, const Row &rm, int lane) {
+  const KeyRefs q = key_refs(p, s, k);
+  const Row e = load_row(q.ec, lane, p.A);
+  if (!any_nz(e)) return;  // no entry for this key
+  const Row e2 = forget_row(e, rm);
+  const bool alive = any_nz(e2);
+  store_row(q.ec, e2, lane, p.A);
+  for (unsigned long long j = 0; j < p.V; ++j) {
+    u64 *vr = q.vc + j * p.A;
+    const Row v = load_row(vr, lane, p.A);
+    if (!any_nz(v)) continue;
+    const Row v2 = alive ? forget_row(v, rm) : zero_row();  // MVReg::forget mvreg.rs:88-104
+    store_row(vr, v2, lane, p.A);
+    if (!any_nz(v2) && lane == 0) q.vv[j] = 0;
+  }
+}
+
+// forget every key of an LDS bitmap
+__device__ void keyset_rm(const MapApplyPlan &p, unsigned long long s, const u64 *bits, const Row &rm, int lane) {
+  for (unsigned long long w0 = 0; w0 < p.Kw; w0 += kWave) {
+    const u64 word = (w0 + lane < p.Kw) ? bits[w0 + lane] : 0ull;
+    u64 nz = __ballot(word != 0);
+    while (nz) {
+      const int l = __builtin_ctzll(nz);
+      nz &= nz - 1;
+      u64 wv = rl64m(word, l);
+      while (wv) {
+        const unsigned long long k = (w0 + l) * 64 + __builtin_ctzll(wv);
+        wv &= wv - 1;
+        if (k < p.K) key_rm(p, s, k, rm, lane);
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ bool any_gt(const Row &r, const Row &c) {  // !(r <= c)
+  return !all_le(r, c);
+}
+
+__global__ __launch_bounds__(kBlock) void map_apply_kernel(MapApplyPlan p) {
+  extern __shared__ u64 lds[];
+  const int lane = threadIdx.x % kWave;
+  const int wib = threadIdx.x / kWave;
+  const unsigned long long A = p.A;
+  const unsigned long long per_wave = p.Dcap * (A + p.Kw);
+  u64 *dcl = lds + wib * per_wave;  // [Dcap][A]
+  u64 *dkb = dcl + p.Dcap * A;      // [Dcap][Kw]
+
+  for (unsigned long long s = (unsigned long long)blockIdx.x * p.wpb + wib; s < p.N;
+       s += (unsigned long long)gridDim.x * p.wpb) {
+    unsigned st = 0;
+    const unsigned long long ob = p.op_off[s], oe = p.op_off[s + 1];
+    unsigned dcnt = p.def_count[s];
+    if (dcnt > p.Dcap || oe < ob || oe > p.n_ops) {
+      if (lane == 0) p.status[s] = (dcnt > p.Dcap ? 4u : 0u) | (oe < ob || oe > p.n_ops ? 8u : 0u);
+      continue;
+    }
+    u64 *Cg = p.clock + s * p.clock_s;
+    Row C = load_row(Cg, lane, A);
+    const u64 *gdc = p.def_clock + s * p.Dcap * A;
+    const u64 *gdk = p.def_keys + s * p.Dcap * p.Kw;
+    for (unsigned long long i = lane; i < dcnt * A; i += kWave) dcl[i] = gdc[i];
+    for (unsigned long long i = lane; i < dcnt * p.Kw; i += kWave) dkb[i] = gdk[i];
+    wave_fence_m();
+
+    for (unsigned long long base = ob; base < oe; base += kWave) {
+      const unsigned long long o = base + lane;
+      const bool ov = o < oe;
+      const unsigned h_kind = ov ? p.kind[o] : 0u;
+      const unsigned h_actor = ov && p.actor ? p.actor[o] : 0u;
+      const u64 h_counter = ov && p.counter ? p.counter[o] : 0ull;
+      const unsigned h_key = ov && p.key ? p.key[o] : 0u;
+      const u64 h_val = ov && p.val ? p.val[o] : 0ull;
+      const unsigned h_row = ov && p.clk_row ? p.clk_row[o] : 0u;
+      const u64 h_kb = ov && p.key_off ? p.key_off[o] : 0ull;
+      const u64 h_ke = ov && p.key_off ? p.key_off[o + 1] : 0ull;
+      const int nb = (int)((oe - base) < (unsigned long long)kWave ? (oe - base) : kWave);
+      for (int i = 0; i < nb; ++i) {
+        const unsigned kind = rl32m(h_kind, i);
+        const unsigned rr = rl32m(h_row, i);
+        if (kind > 1 || rr >= p.n_clk_rows) {
+          st |= 2u;
+          continue;
+        }
+        const Row oc = load_row(p.clk_pool + (unsigned long long)rr * A, lane, A);
+        if (kind == 0) {  // ---- Op::Up
+          const unsigned long long a = rl32m(h_actor, i), k = rl32m(h_key, i);
+          const u64 kc = rl64m(h_counter, i);
+          if (a >= A || k >= p.K) {
+            st |= 2u;
+            continue;
+          }
+          const int ja = (int)(a / kWave), la = (int)(a % kWave);
+          u64 cj = C.w[0];
+#pragma unroll
+          for (int j = 1; j < kMA; ++j)
+            if (j == ja) cj = C.w[j];
+          if (rl64m(cj, la) >= kc) continue;  // seen (:123-126)
+          const KeyRefs q = key_refs(p, s, k);
+          if (lane == la) {  // entry clock apply(dot) (:130)
+            u64 *cell = q.ec + a;
+            if (*cell < kc) *cell = kc;
+          }
+          if (any_nz(oc)) {  // MVReg::apply (mvreg.rs:130-166)
+            bool should_add = true;
+            int last = -1, used = 0;
+            for (unsigned long long j = 0; j < p.V; ++j) {
+              u64 *vr = q.vc + j * A;
+              const Row v = load_row(vr, lane, A);
+              if (!any_nz(v)) continue;
+              if (all_le(v, oc)) {  // partial_cmp in {Less, Equal}: dropped
+                store_row(vr, zero_row(), lane, A);
+                if (lane == 0) q.vv[j] = 0;
+                continue;
+              }
+              if (all_le(oc, v)) should_add = false;  // v > pc (Greater)
+              last = (int)j;
+              ++used;
+            }
+            if (should_add) {
+              int slot = last + 1;
+              if (slot >= (int)p.V) {
+                if (used >= (int)p.V) {
+                  st |= 16u;  // more values than slots: the state is incomplete
+                  slot = -1;
+                } else {  // compact the used slots in order, then append
+                  wave_fence_m();
+                  int w = 0;
+                  for (unsigned long long j = 0; j < p.V; ++j) {
+                    const Row v = load_row(q.vc + j * A, lane, A);
+                    if (!any_nz(v)) continue;
+                    if ((unsigned long long)w != j) {
+                      const u64 x = q.vv[j];
+                      wave_fence_m();
+                      store_row(q.vc + (unsigned long long)w * A, v, lane, A);
+                      store_row(q.vc + j * A, zero_row(), lane, A);
+                      if (lane == 0) {
+                        q.vv[w] = x;
+                        q.vv[j] = 0;
+                      }
+                      wave_fence_m();
+                    }
+                    ++w;
+                  }
+                  slot = w;
+                }
+              }
+              if (slot >= 0) {
+                store_row(q.vc + (unsigned long long)slot * A, oc, lane, A);
+                if (lane == 0) q.vv[slot] = rl64m(h_val, i);
+              }
+            }
+          }
+#pragma unroll
+          for (int j = 0; j < kMA; ++j)
+            if (j == ja && lane == la) C.w[j] = kc;  // self.clock.apply(dot) (:133)
+          wave_fence_m();
+          unsigned nk = 0;  // apply_deferred (:134, :311-316)
+          for (unsigned d = 0; d < dcnt; ++d) {
+            const Row rm = load_row(dcl + d * A, lane, A);
+            keyset_rm(p, s, dkb + d * p.Kw, rm, lane);
+            wave_fence_m();
+            if (any_gt(rm, C)) {
+              if (nk != d) {
+                for (unsigned long long t = lane; t < A; t += kWave) dcl[nk * A + t] = dcl[d * A + t];
+                for (unsigned long long t = lane; t < p.Kw; t += kWave) dkb[nk * p.Kw + t] = dkb[d * p.Kw + t];
+              }
+              ++nk;
+            }
+          }
+          dcnt = nk;
+          wave_fence_m();
+        } else {  // ---- Op::Rm -> apply_keyset_rm (:318-348)
+          const u64 kb = rl64m(h_kb, i), ke = rl64m(h_ke, i);
+          if (ke < kb) {
+            st |= 2u;
+            continue;
+          }
+          for (u64 jb = kb; jb < ke; jb += kWave) {
+            const unsigned kk = jb + lane < ke ? p.keys[jb + lane] : 0u;
+            const int n = (int)((ke - jb) < (u64)kWave ? (ke - jb) : kWave);
+            for (int t = 0; t < n; ++t) {
+              const unsigned long long k = rl32m(kk, t);
+              if (k >= p.K) {
+                st |= 2u;
+                continue;
+              }
+              key_rm(p, s, k, oc, lane);
+              wave_fence_m();
+            }
+          }
+          if (!any_gt(oc, C)) continue;  // rm <= clock: not deferred (:336-345)
+          int slot = -1;
+          for (unsigned d = 0; d < dcnt; ++d)
+            if (rows_eq(load_row(dcl + d * A, lane, A), oc)) {
+              slot = (int)d;
+              break;
+            }
+          if (slot < 0) {
+            if (dcnt >= p.Dcap) {
+              st |= 1u;
+              continue;
+            }
+            slot = (int)dcnt++;
+            store_row(dcl + (unsigned long long)slot * A, oc, lane, A);
+            for (unsigned long long t = lane; t < p.Kw; t += kWave) dkb[slot * p.Kw + t] = 0;
+            wave_fence_m();
+          }
+          u64 *bits = dkb + (unsigned long long)slot * p.Kw;
+          for (u64 jk = kb + lane; jk < ke; jk += kWave) {
+            const unsigned long long k = p.keys[jk];
+            if (k < p.K) atomicOr(bits + k / 64, 1ull << (k % 64));
+          }
+          wave_fence_m();
+        }
+      }
+    }
+    store_row(Cg, C, lane, A);
+    u64 *wdc = p.def_clock + s * p.Dcap * A;
+    u64 *wdk = p.def_keys + s * p.Dcap * p.Kw;
+    for (unsigned long long i = lane; i < dcnt * A; i += kWave) wdc[i] = dcl[i];
+    for (unsigned long long i = lane; i < dcnt * p.Kw; i += kWave) wdk[i] = dkb[i];
+    if (lane == 0) {
+      p.def_count[s] = dcnt;
+      p.status[s] = st;
+    }
+    wave_fence_m();
+  }
+}
+
+}  // namespace crdt
+
+using namespace crdt;
+
+extern "C" int crdt_map_apply_batch(crdt_ctx *ctx, const crdt_map_states *m, uint64_t *def_clock, uint64_t *def_keys,
+                                    uint32_t *def_count, size_t Dcap, const crdt_map_ops *ops, uint32_t *status) {
+  CRDT_CHECK_CTX(ctx);
+  if (!m || !ops || !status) return fail(ctx, CRDT_EINVAL, "map_apply_batch: NULL argument");
+  const size_t N = m->N, K = m->K, A = m->A, V = m->V;
+  if (N == 0) return CRDT_OK;
+  if (A == 0 || A > (size_t)(kMA * kWave) || V == 0 || V > (size_t)kMaxV || K == 0)
+    return fail(ctx, CRDT_EINVAL, "map_apply_batch: need 1 <= A <= %d, 1 <= V <= %d, K >= 1", kMA * kWave, kMaxV);
+  if (!m->clock || !m->ec || !m->vclk || !m->vval || !def_count || !ops->op_off)
+    return fail(ctx, CRDT_EINVAL, "map_apply_batch: NULL buffer");
+  if (Dcap && (!def_clock || !def_keys)) return fail(ctx, CRDT_EINVAL, "map_apply_batch: NULL deferred buffers");
+  if (ops->n_ops && (!ops->kind || !ops->clk_row || !ops->clk_pool))
+    return fail(ctx, CRDT_EINVAL, "map_apply_batch: NULL op buffer");
+  if (m->clock_stride < A || m->ec_stride < K * A || m->vclk_stride < K * V * A || m->vval_stride < K * V)
+    return fail(ctx, CRDT_EINVAL, "map_apply_batch: stride smaller than the rows it holds");
+  const size_t Kw = (K + 63) / 64;
+  const size_t per_wave = Dcap * (A + Kw) * 8;
+  const size_t lds_cap = 64 * 1024;
+  if (per_wave > lds_cap)
+    return fail(ctx, CRDT_EINVAL, "map_apply_batch: Dcap * (A + ceil(K/64)) * 8 = %zu B exceeds %zu B of LDS",
+                per_wave, lds_cap);
+  int wpb = kBlock / kWave;
+  while (wpb > 1 && per_wave * wpb > lds_cap) --wpb;
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  MapApplyPlan p{(u64 *)m->clock, m->clock_stride, (u64 *)m->ec, m->ec_stride, (u64 *)m->vclk, m->vclk_stride,
+                 (u64 *)m->vval, m->vval_stride, (u64 *)def_clock, (u64 *)def_keys, def_count, N, K, A, V, Kw, Dcap,
+                 (const u64 *)ops->op_off, ops->kind, ops->actor, (const u64 *)ops->counter, ops->key,
+                 (const u64 *)ops->val, ops->clk_row, (const u64 *)ops->clk_pool, ops->n_clk_rows,
+                 (const u64 *)ops->key_off, ops->keys, ops->n_ops, status, wpb};
+  const unsigned long long want = (N + wpb - 1) / wpb;
+  const unsigned long long cap = (unsigned long long)ctx->cu_count * 64;
+  timing_begin(ctx, "map_apply");
+  hipLaunchKernelGGL(map_apply_kernel, dim3((unsigned)(want < cap ? want : cap)), dim3(wpb * kWave), per_wave * wpb,
+                     ctx->stream, p);
+  timing_end(ctx);
+  CRDT_HIP(ctx, hipGetLastError());
+  return CRDT_OK;
+}

@@ -1,0 +1,114 @@
+"""GPU parity: batched Map<K, MVReg<u64>> CmRDT::apply (crdt_map_apply_batch) vs the oracle's
+one-by-one Map.apply (map.rs:119-137, apply_keyset_rm :318-348, MVReg::apply mvreg.rs:130-166).
+
+Op streams come from op replay with the reference's ctx API (writes with the ctx of get(key),
+removes with an rm ctx read here or at another replica, test/map.rs:71-146 style), delivered to
+each state as a random subset in perturbed causal order and cut at a random point, so removes
+defer and concurrent writes leave several values per register."""
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+from gpu_util import to_host
+
+pytestmark = pytest.mark.gpu
+
+import crdts_gpu as cg  # noqa: E402
+
+
+def replay_streams(seed, n_states, n_origins, K, n_ops):
+    rng = np.random.default_rng(seed)
+    origins = [O.Map(O.MVReg) for _ in range(n_origins)]
+    ops, val = [], 1
+    for _ in range(n_ops):
+        a = int(rng.integers(n_origins))
+        m = origins[a]
+        x = rng.random()
+        if x < 0.1:
+            m.merge(origins[int(rng.integers(n_origins))])
+            continue
+        k = int(rng.integers(K))
+        if x < 0.75:
+            op = m.update(k, m.get(k).derive_add_ctx(a), lambda r, c, v=val: r.write(v, c))
+            val += 1
+        else:
+            src = m if rng.random() < 0.5 else origins[int(rng.integers(n_origins))]
+            op = m.rm(k, src.get(k).derive_rm_ctx())
+        m.apply(op)
+        ops.append(op)
+    streams = []
+    for _ in range(n_states):
+        keep = np.flatnonzero(rng.random(len(ops)) < rng.uniform(0.4, 1.0))
+        idx = keep[np.argsort(keep + rng.normal(0, rng.uniform(0, 10), size=keep.shape[0]))]
+        idx = idx[:int(rng.integers(len(idx) // 2, len(idx) + 1))]
+        streams.append([ops[i] for i in idx])
+    return streams
+
+
+def op_tuple(op):
+    if isinstance(op, O.MapUp):
+        return ("up", op.dot.actor, op.dot.counter, op.key, dict(op.op.clock.dots), op.op.val)
+    return ("rm", dict(op.clock.dots), sorted(op.keyset))
+
+
+def oracle_apply(streams):
+    out, peak = [], 1
+    for ops in streams:
+        m = O.Map(O.MVReg)
+        for op in ops:
+            m.apply(op)
+            peak = max([peak] + [len(e.val.vals) for e in m.entries.values()])
+        out.append(m)
+    return out, peak
+
+
+def gpu_apply(ctx, streams, K, A, V, Dcap):
+    N = len(streams)
+    Kw = (K + 63) // 64
+    z = lambda *s: torch.zeros(s, dtype=torch.int64, device="cuda:0")  # noqa: E731
+    clock, ec, vclk, vval = z(N, A), z(N, K, A), z(N, K, V, A), z(N, K, V)
+    dcl, dks = z(N, Dcap, A), z(N, Dcap, Kw)
+    cnt = torch.zeros(N, dtype=torch.int32, device="cuda:0")
+    ops = cg.map.encode_ops([[op_tuple(o) for o in s] for s in streams], A, "cuda:0")
+    status = cg.map.apply_batch(clock, ec, vclk, vval, dcl, dks, cnt, ops, ctx=ctx)
+    torch.cuda.synchronize()
+    c, e, vc, vv = to_host(clock), to_host(ec), to_host(vclk), to_host(vval)
+    dc, dk, n = to_host(dcl), to_host(dks), cnt.cpu().numpy()
+    maps = []
+    for s in range(N):
+        deferred = [(dc[s, d], O.bitmap_members(dk[s, d])) for d in range(int(n[s]))]
+        maps.append((O.dense_to_map(c[s], e[s], vc[s], vv[s], deferred), vc[s], vv[s], e[s]))
+    return maps, status.cpu().numpy()
+
+
+@pytest.mark.parametrize("seed,n_states,n_origins,K,n_ops", [
+    (1, 48, 3, 6, 80), (2, 100, 5, 20, 150), (3, 16, 70, 40, 300), (4, 64, 2, 2, 120)])
+def test_map_apply_replay(gpu_ctx, seed, n_states, n_origins, K, n_ops):
+    streams = replay_streams(seed, n_states, n_origins, K, n_ops)
+    exp, peak = oracle_apply(streams)
+    Dcap = max(1, max(sum(1 for o in s if isinstance(o, O.MapRm)) for s in streams))
+    got, status = gpu_apply(gpu_ctx, streams, K, n_origins, min(peak, 8), min(Dcap, 24))
+    assert (status == 0).all(), status
+    assert sum(len(m.deferred) for m in exp) > 0 or seed in (1, 4)
+    for s, ((g, vc, vv, ec), e) in enumerate(zip(got, exp)):
+        assert g.clock == e.clock and g.entries == e.entries, s
+        assert g.deferred == e.deferred, s
+        # the value slots keep Vec order: the kernel's used slots in index order == oracle's vals
+        for k, ent in e.entries.items():
+            used = [j for j in range(vc.shape[1]) if vc[k, j].any()]
+            assert [int(vv[k, j]) for j in used] == [v for _, v in ent.val.vals], (s, k)
+        assert not vc[~ec.any(axis=1)].any()
+
+
+def test_map_apply_value_overflow(gpu_ctx):
+    # two concurrent writes to one key need 2 value slots
+    a, b = O.Map(O.MVReg), O.Map(O.MVReg)
+    op1 = a.update(0, a.get(0).derive_add_ctx(0), lambda r, c: r.write(11, c))
+    op2 = b.update(0, b.get(0).derive_add_ctx(1), lambda r, c: r.write(22, c))
+    got, status = gpu_apply(gpu_ctx, [[op1, op2], [op1]], 1, 2, 1, 1)
+    assert status[0] & 16 and status[1] == 0
+    exp, _ = oracle_apply([[op1, op2], [op1]])
+    assert got[1][0].entries == exp[1].entries
+    got, status = gpu_apply(gpu_ctx, [[op1, op2]], 1, 2, 2, 1)
+    assert status[0] == 0 and got[0][0].entries == oracle_apply([[op1, op2]])[0][0].entries
