@@ -209,3 +209,46 @@ def orswot_op_streams(N: int, T: int, M: int, A: int, seed: int, p_rm: float = 0
         rm_clock=rm.reshape(n, A).contiguous(),
         mem_off=torch.arange(n + 1, device=device, dtype=torch.int64),
         mem=member)
+
+
+def map_op_streams(N: int, T: int, K: int, A: int, seed: int, p_rm: float = 0.2, p_future: float = 0.3,
+                   p_stale: float = 0.2, rm_actors: int = 4, device="cuda"):
+    """T Map<K, MVReg> ops per state for N states (a map.MapOpBatch, generated on `device`):
+    an Op::Up of a random key with the next dot of a random actor whose Put clock is the state's
+    clock at that point plus the dot (a write with a fresh read ctx: it supersedes the key's
+    values) or, w.p. p_stale, the clock of 1-8 ops earlier plus the dot (a write from a stale
+    ctx: concurrent with what came since, so values accumulate); or w.p. p_rm an Op::Rm of one
+    key with ~rm_actors actors of the state's clock, w.p. p_future from the future (deferred).
+    Value = op index + 1."""
+    from .map import MapOpBatch
+
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    n = N * T
+    i64 = torch.int64
+    kind = (torch.rand((N, T), generator=g, device=device) < p_rm).to(torch.uint8)
+    actor = torch.randint(0, A, (N, T), generator=g, device=device, dtype=i64)
+    onehot = torch.zeros((N, T, A), dtype=i64, device=device)
+    onehot.scatter_(2, actor.unsqueeze(2), (kind == 0).to(i64).unsqueeze(2))
+    cum = onehot.cumsum(1)  # the state's clock after op t (ops applied in order)
+    del onehot
+    counter = torch.gather(cum, 2, actor.unsqueeze(2)).squeeze(2)
+    stale = torch.rand((N, T), generator=g, device=device) < p_stale
+    lag = torch.randint(1, 9, (N, T), generator=g, device=device) * stale
+    src = (torch.arange(T, device=device).unsqueeze(0) - lag).clamp(min=0)
+    put = torch.gather(cum, 1, src.unsqueeze(2).expand(N, T, A)).clone()
+    put.scatter_(2, actor.unsqueeze(2), counter.unsqueeze(2))  # the Put's clock holds its own dot
+    keep = torch.rand((N, T, A), generator=g, device=device) < (rm_actors / A)
+    rm = torch.where(keep, cum, torch.zeros((), dtype=i64, device=device))
+    fut = (torch.rand((N, T), generator=g, device=device) < p_future).to(i64)
+    bump = torch.randint(0, A, (N, T, 1), generator=g, device=device)
+    rm.scatter_(2, bump, torch.gather(rm, 2, bump) + fut.unsqueeze(2) * (
+        1 + torch.gather(cum, 2, bump) - torch.gather(rm, 2, bump)))
+    pool = torch.where((kind == 0).unsqueeze(2), put, rm).reshape(n, A).contiguous()
+    del cum, keep, put, rm
+    key = torch.randint(0, K, (n,), generator=g, device=device, dtype=torch.int32)
+    return MapOpBatch(op_off=torch.arange(N + 1, device=device, dtype=i64) * T, kind=kind.reshape(n).contiguous(),
+                      actor=actor.reshape(n).to(torch.int32), counter=counter.reshape(n).contiguous(), key=key,
+                      val=torch.arange(1, n + 1, device=device, dtype=i64),
+                      clk_row=torch.arange(n, device=device, dtype=torch.int32), clk_pool=pool,
+                      key_off=torch.arange(n + 1, device=device, dtype=i64), keys=key)

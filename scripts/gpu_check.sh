@@ -21,6 +21,7 @@ for s in $STEPS; do
     bench) run bench 300 python -u bench.py --steps 20 --warmup 3 ;;
     prof)  run prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
     apply) run bench_apply 300 python -u scripts/bench_orswot_apply.py ;;
+    mapapply) run bench_mapapply 300 python -u scripts/bench_map_apply.py ;;
     forget) run bench_forget 300 python -u scripts/bench_forget.py ;;
     causal) run bench_causal 300 python -u scripts/bench_causal.py ;;
   esac

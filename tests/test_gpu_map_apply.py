@@ -112,3 +112,27 @@ def test_map_apply_value_overflow(gpu_ctx):
     assert got[1][0].entries == exp[1].entries
     got, status = gpu_apply(gpu_ctx, [[op1, op2]], 1, 2, 2, 1)
     assert status[0] == 0 and got[0][0].entries == oracle_apply([[op1, op2]])[0][0].entries
+
+
+@pytest.mark.parametrize("N,T,K,A,V", [(256, 64, 16, 8, 4), (64, 100, 70, 33, 6)])
+def test_map_apply_synth_streams(gpu_ctx, N, T, K, A, V):
+    """The bench's device-generated streams (crdts_gpu.synth.map_op_streams) vs the oracle."""
+    b = cg.synth.map_op_streams(N, T, K, A, seed=N + K, device="cuda:0")
+    h = {f: getattr(b, f).cpu().numpy() for f in b._fields}
+    streams = []
+    for s in range(N):
+        ops = []
+        for o in range(int(h["op_off"][s]), int(h["op_off"][s + 1])):
+            row = h["clk_pool"][h["clk_row"][o]].view(np.uint64)
+            clk = O.VClock({a: int(v) for a, v in enumerate(row) if v})
+            k = int(h["keys"][h["key_off"][o]])
+            ops.append(O.MapUp(O.Dot(int(h["actor"][o]), int(h["counter"][o])), k, O.MVRegPut(clk, int(h["val"][o])))
+                       if h["kind"][o] == 0 else O.MapRm(clk, {k}))
+        streams.append(ops)
+    exp, peak = oracle_apply(streams)
+    assert peak <= V
+    got, status = gpu_apply(gpu_ctx, streams, K, A, V, 16)
+    assert (status == 0).all()
+    assert sum(len(m.deferred) for m in exp) > 0
+    for s, ((g, _, _, _), e) in enumerate(zip(got, exp)):
+        assert g == e, s
