@@ -44,6 +44,7 @@ struct Tune {
   int map_ring = 2;    // ... chunk slots in the ring (2-4)
   int map_spec = 1;    // ... speculative no-op scan
   int rows_blocks_per_cu = 0;  // row-pair / row-reduction kernels (causal.hip); 0 = per-kernel default
+  int apply_hot_slots = 8;     // Orswot apply: deferred slots kept in LDS per state (the rest in HBM)
 };
 
 struct PendingTiming {

@@ -36,7 +36,7 @@ struct OrswotApplyPlan {
   unsigned long long entry_mstride, entry_sstride;
   u64 *def_clock, *def_members;
   uint32_t *def_count;
-  unsigned long long N, M, A, Mw, Dcap;
+  unsigned long long N, M, A, Mw, Dcap, Dh;  // Dh: hot deferred slots kept in LDS (the rest in HBM)
   const u64 *op_off;
   const uint8_t *kind;
   const uint32_t *actor;
@@ -110,9 +110,9 @@ __global__ __launch_bounds__(kBlock) void orswot_apply_kernel(OrswotApplyPlan p)
   extern __shared__ u64 lds[];
   const int lane = threadIdx.x % kWave;
   const int wib = threadIdx.x / kWave;
-  const unsigned long long per_wave = p.Dcap * (p.A + p.Mw);
-  u64 *dcl = lds + wib * per_wave;  // [Dcap][A] rm clocks
-  u64 *dmb = dcl + p.Dcap * p.A;    // [Dcap][Mw] member bitmaps
+  const unsigned long long per_wave = p.Dh * (p.A + p.Mw);
+  u64 *lcl = lds + wib * per_wave;  // [Dh][A] rm clocks of the hot slots
+  u64 *lmb = lcl + p.Dh * p.A;      // [Dh][Mw] their member bitmaps
   const unsigned long long A = p.A;
 
   for (unsigned long long s = (unsigned long long)blockIdx.x * p.wpb + wib; s < p.N;
@@ -132,10 +132,15 @@ __global__ __launch_bounds__(kBlock) void orswot_apply_kernel(OrswotApplyPlan p)
       c[j] = a < A ? C[a] : 0;
     }
     u64 *E = p.entries + s * p.entry_sstride;
-    const u64 *gdc = p.def_clock + s * p.Dcap * A;
-    const u64 *gdm = p.def_members + s * p.Dcap * p.Mw;
-    for (unsigned long long i = lane; i < dcnt * A; i += kWave) dcl[i] = gdc[i];
-    for (unsigned long long i = lane; i < dcnt * p.Mw; i += kWave) dmb[i] = gdm[i];
+    // slot d lives in LDS for d < Dh, else in the state's own HBM slot (generic pointers: the
+    // same code reads either; most states never hold more than Dh deferred removes)
+    u64 *gdc = p.def_clock + s * p.Dcap * A;
+    u64 *gdm = p.def_members + s * p.Dcap * p.Mw;
+    auto SC = [&](unsigned long long d) -> u64 * { return d < p.Dh ? lcl + d * A : gdc + d * A; };
+    auto SM = [&](unsigned long long d) -> u64 * { return d < p.Dh ? lmb + d * p.Mw : gdm + d * p.Mw; };
+    const unsigned long long dhot = dcnt < p.Dh ? dcnt : p.Dh;
+    for (unsigned long long i = lane; i < dhot * A; i += kWave) lcl[i] = gdc[i];
+    for (unsigned long long i = lane; i < dhot * p.Mw; i += kWave) lmb[i] = gdm[i];
     wave_fence();
 
     for (unsigned long long base = ob; base < oe; base += kWave) {
@@ -191,13 +196,14 @@ __global__ __launch_bounds__(kBlock) void orswot_apply_kernel(OrswotApplyPlan p)
 #pragma unroll
             for (int j = 0; j < kCA; ++j) {
               const unsigned long long aa = lane + j * kWave;
-              r[j] = aa < A ? dcl[d * A + aa] : 0;
+              r[j] = aa < A ? SC(d)[aa] : 0;
             }
-            forget_members(p, E, dmb + d * p.Mw, r, lane);
+            forget_members(p, E, SM(d), r, lane);
             if (any_greater(r, c, lane, A)) {
               if (nk != d) {
-                for (unsigned long long t = lane; t < A; t += kWave) dcl[nk * A + t] = dcl[d * A + t];
-                for (unsigned long long t = lane; t < p.Mw; t += kWave) dmb[nk * p.Mw + t] = dmb[d * p.Mw + t];
+                u64 *dc = SC(nk), *sc = SC(d), *dm = SM(nk), *sm = SM(d);
+                for (unsigned long long t = lane; t < A; t += kWave) dc[t] = sc[t];
+                for (unsigned long long t = lane; t < p.Mw; t += kWave) dm[t] = sm[t];
               }
               ++nk;
             }
@@ -237,7 +243,7 @@ __global__ __launch_bounds__(kBlock) void orswot_apply_kernel(OrswotApplyPlan p)
 #pragma unroll
             for (int j = 0; j < kCA; ++j) {
               const unsigned long long aa = lane + j * kWave;
-              if (aa < A && dcl[d * A + aa] != r[j]) ne = true;
+              if (aa < A && SC(d)[aa] != r[j]) ne = true;
             }
             if (__ballot(ne) == 0) {
               slot = (int)d;
@@ -253,12 +259,12 @@ __global__ __launch_bounds__(kBlock) void orswot_apply_kernel(OrswotApplyPlan p)
 #pragma unroll
             for (int j = 0; j < kCA; ++j) {
               const unsigned long long aa = lane + j * kWave;
-              if (aa < A) dcl[slot * A + aa] = r[j];
+              if (aa < A) SC(slot)[aa] = r[j];
             }
-            for (unsigned long long t = lane; t < p.Mw; t += kWave) dmb[slot * p.Mw + t] = 0;
+            for (unsigned long long t = lane; t < p.Mw; t += kWave) SM(slot)[t] = 0;
             wave_fence();
           }
-          u64 *bits = dmb + (unsigned long long)slot * p.Mw;
+          u64 *bits = SM(slot);
           for (u64 jm = mb + lane; jm < me; jm += kWave) {
             const unsigned long long m = p.mem[jm];
             if (m < p.M) atomicOr(bits + m / 64, 1ull << (m % 64));
@@ -273,10 +279,9 @@ __global__ __launch_bounds__(kBlock) void orswot_apply_kernel(OrswotApplyPlan p)
       const unsigned long long a = lane + j * kWave;
       if (a < A) C[a] = c[j];
     }
-    u64 *wdc = p.def_clock + s * p.Dcap * A;
-    u64 *wdm = p.def_members + s * p.Dcap * p.Mw;
-    for (unsigned long long i = lane; i < dcnt * A; i += kWave) wdc[i] = dcl[i];
-    for (unsigned long long i = lane; i < dcnt * p.Mw; i += kWave) wdm[i] = dmb[i];
+    const unsigned long long dout = dcnt < p.Dh ? dcnt : p.Dh;  // slots >= Dh are already in HBM
+    for (unsigned long long i = lane; i < dout * A; i += kWave) gdc[i] = lcl[i];
+    for (unsigned long long i = lane; i < dout * p.Mw; i += kWave) gdm[i] = lmb[i];
     if (lane == 0) {
       p.def_count[s] = dcnt;
       p.status[s] = st;
@@ -306,16 +311,17 @@ extern "C" int crdt_orswot_apply_batch(crdt_ctx *ctx, const crdt_orswot_states *
   if (s.clock_stride < s.A || s.entry_mstride < s.A || s.entry_sstride < s.M * s.entry_mstride)
     return fail(ctx, CRDT_EINVAL, "orswot_apply_batch: strides smaller than the rows they hold");
   const size_t Mw = (s.M + 63) / 64;
-  const size_t per_wave = s.Dcap * (s.A + Mw) * 8;
+  const size_t Dh = s.Dcap < (size_t)ctx->tune.apply_hot_slots ? s.Dcap : (size_t)ctx->tune.apply_hot_slots;
+  const size_t per_wave = Dh * (s.A + Mw) * 8;
   const size_t lds_cap = 64 * 1024;
   if (per_wave > lds_cap)
-    return fail(ctx, CRDT_EINVAL, "orswot_apply_batch: Dcap * (A + ceil(M/64)) * 8 = %zu B exceeds %zu B of LDS",
+    return fail(ctx, CRDT_EINVAL, "orswot_apply_batch: hot slots * (A + ceil(M/64)) * 8 = %zu B exceeds %zu B of LDS",
                 per_wave, lds_cap);
   int wpb = kBlock / kWave;
   while (wpb > 1 && per_wave * wpb > lds_cap) --wpb;
   CRDT_HIP(ctx, hipSetDevice(ctx->device));
   OrswotApplyPlan p{(u64 *)s.clock, s.clock_stride, (u64 *)s.entries, s.entry_mstride, s.entry_sstride,
-                    (u64 *)s.def_clock, (u64 *)s.def_members, s.def_count, s.N, s.M, s.A, Mw, s.Dcap,
+                    (u64 *)s.def_clock, (u64 *)s.def_members, s.def_count, s.N, s.M, s.A, Mw, s.Dcap, Dh,
                     (const u64 *)ops->op_off, ops->kind, ops->actor, (const u64 *)ops->counter, ops->rm_row,
                     (const u64 *)ops->rm_clock, ops->rm_clock ? ops->n_rm_rows : 0, (const u64 *)ops->mem_off,
                     ops->mem, ops->n_ops, status, wpb};
