@@ -133,3 +133,21 @@ def test_orswot_apply_synth_streams(gpu_ctx, N, T, M, A):
     np.testing.assert_array_equal(to_host(entries), oe)
     np.testing.assert_array_equal(cnt.cpu().numpy(), ond.astype(np.int32))
     assert ond.sum() > 0
+
+
+@pytest.mark.parametrize("hot", [0, 1, 3])
+def test_orswot_apply_deferred_spill(hot):
+    """Deferred slots beyond the LDS-resident ones live in the state's HBM slots (CRDT_TUNE hot=N):
+    the same results with none, one or three slots in LDS."""
+    ctx = cg.Context(0)
+    ctx.tune(f"hot={hot}")
+    try:
+        states, streams = arbitrary_case(9 + hot, 24, 40, 16, max_ops=60)
+        got, status = gpu_apply_streams(ctx, states, streams, 40, 16)
+        exp = oracle_streams(states, streams)
+        assert (status == 0).all()
+        assert max(len(e.deferred) for e in exp) > hot  # some state really spills to HBM
+        for s, (g, e) in enumerate(zip(got, exp)):
+            assert g == e, s
+    finally:
+        ctx.close()
