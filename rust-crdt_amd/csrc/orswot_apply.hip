@@ -27,7 +27,7 @@
 namespace crdt {
 
 constexpr int kApplyMaxA = 256;
-constexpr int kCA = kApplyMaxA / kWave;  // clock words per lane
+constexpr int kCAMax = kApplyMaxA / kWave;  // clock words per lane at the widest A
 
 struct OrswotApplyPlan {
   u64 *clock;
@@ -67,6 +67,7 @@ __device__ __forceinline__ void wave_fence() {
 }
 
 // forget one entry row by the clock held in registers: keep e[a] iff e[a] > rm[a]
+template <int kCA>
 __device__ __forceinline__ void forget_row(u64 *row, const u64 (&r)[kCA], int lane, unsigned long long A) {
 #pragma unroll
   for (int j = 0; j < kCA; ++j) {
@@ -79,6 +80,7 @@ __device__ __forceinline__ void forget_row(u64 *row, const u64 (&r)[kCA], int la
 }
 
 // forget every member row named in an LDS bitmap of Mw words
+template <int kCA>
 __device__ __forceinline__ void forget_members(const OrswotApplyPlan &p, u64 *E, const u64 *bits,
                                                const u64 (&r)[kCA], int lane) {
   for (unsigned long long w0 = 0; w0 < p.Mw; w0 += kWave) {
@@ -97,6 +99,7 @@ __device__ __forceinline__ void forget_members(const OrswotApplyPlan &p, u64 *E,
   }
 }
 
+template <int kCA>
 __device__ __forceinline__ bool any_greater(const u64 (&r)[kCA], const u64 (&c)[kCA], int lane,
                                             unsigned long long A) {
   bool g = false;
@@ -106,6 +109,8 @@ __device__ __forceinline__ bool any_greater(const u64 (&r)[kCA], const u64 (&c)[
   return __ballot(g) != 0;
 }
 
+// kCA clock words per lane: 1 for A <= 64 (fewer VGPRs, more waves per SIMD), 4 up to A = 256
+template <int kCA>
 __global__ __launch_bounds__(kBlock) void orswot_apply_kernel(OrswotApplyPlan p) {
   extern __shared__ u64 lds[];
   const int lane = threadIdx.x % kWave;
@@ -328,8 +333,11 @@ extern "C" int crdt_orswot_apply_batch(crdt_ctx *ctx, const crdt_orswot_states *
   const unsigned long long want = (s.N + wpb - 1) / wpb;
   const unsigned long long cap = (unsigned long long)ctx->cu_count * 64;
   timing_begin(ctx, "orswot_apply");
-  hipLaunchKernelGGL(orswot_apply_kernel, dim3((unsigned)(want < cap ? want : cap)), dim3(wpb * kWave),
-                     per_wave * wpb, ctx->stream, p);
+  const dim3 grid((unsigned)(want < cap ? want : cap)), block(wpb * kWave);
+  if (s.A <= (size_t)kWave)
+    hipLaunchKernelGGL(orswot_apply_kernel<1>, grid, block, per_wave * wpb, ctx->stream, p);
+  else
+    hipLaunchKernelGGL(orswot_apply_kernel<kCAMax>, grid, block, per_wave * wpb, ctx->stream, p);
   timing_end(ctx);
   CRDT_HIP(ctx, hipGetLastError());
   return CRDT_OK;
