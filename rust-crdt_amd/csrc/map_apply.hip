@@ -52,55 +52,64 @@ struct MapApplyPlan {
   int wpb;
 };
 
-struct Row {
-  u64 w[kMA];
+// W clock words per lane: 1 for A <= 64 (fewer VGPRs, more waves per SIMD), 2 to A = 128, 4 to 256
+template <int W>
+struct RowT {
+  u64 w[W];
 };
 
-__device__ __forceinline__ Row load_row(const u64 *p, int lane, unsigned long long A) {
-  Row r;
+template <int W>
+__device__ __forceinline__ RowT<W> load_row(const u64 *p, int lane, unsigned long long A) {
+  RowT<W> r;
 #pragma unroll
-  for (int j = 0; j < kMA; ++j) {
+  for (int j = 0; j < W; ++j) {
     const unsigned long long a = lane + j * kWave;
     r.w[j] = a < A ? p[a] : 0ull;
   }
   return r;
 }
-__device__ __forceinline__ void store_row(u64 *p, const Row &r, int lane, unsigned long long A) {
+template <int W>
+__device__ __forceinline__ void store_row(u64 *p, const RowT<W> &r, int lane, unsigned long long A) {
 #pragma unroll
-  for (int j = 0; j < kMA; ++j) {
+  for (int j = 0; j < W; ++j) {
     const unsigned long long a = lane + j * kWave;
     if (a < A) p[a] = r.w[j];
   }
 }
-__device__ __forceinline__ bool any_nz(const Row &r) {
+template <int W>
+__device__ __forceinline__ bool any_nz(const RowT<W> &r) {
   bool b = false;
 #pragma unroll
-  for (int j = 0; j < kMA; ++j) b |= r.w[j] != 0;
+  for (int j = 0; j < W; ++j) b |= r.w[j] != 0;
   return __ballot(b) != 0;
 }
 // x <= y on every actor (padding lanes hold 0 on both sides)
-__device__ __forceinline__ bool all_le(const Row &x, const Row &y) {
+template <int W>
+__device__ __forceinline__ bool all_le(const RowT<W> &x, const RowT<W> &y) {
   bool b = false;
 #pragma unroll
-  for (int j = 0; j < kMA; ++j) b |= x.w[j] > y.w[j];
+  for (int j = 0; j < W; ++j) b |= x.w[j] > y.w[j];
   return __ballot(b) == 0;
 }
-__device__ __forceinline__ bool rows_eq(const Row &x, const Row &y) {
+template <int W>
+__device__ __forceinline__ bool rows_eq(const RowT<W> &x, const RowT<W> &y) {
   bool b = false;
 #pragma unroll
-  for (int j = 0; j < kMA; ++j) b |= x.w[j] != y.w[j];
+  for (int j = 0; j < W; ++j) b |= x.w[j] != y.w[j];
   return __ballot(b) == 0;
 }
-__device__ __forceinline__ Row forget_row(const Row &x, const Row &y) {  // vclock.rs:95-105
-  Row r;
+template <int W>
+__device__ __forceinline__ RowT<W> forget_row(const RowT<W> &x, const RowT<W> &y) {  // vclock.rs:95-105
+  RowT<W> r;
 #pragma unroll
-  for (int j = 0; j < kMA; ++j) r.w[j] = x.w[j] > y.w[j] ? x.w[j] : 0ull;
+  for (int j = 0; j < W; ++j) r.w[j] = x.w[j] > y.w[j] ? x.w[j] : 0ull;
   return r;
 }
-__device__ __forceinline__ Row zero_row() {
-  Row r;
+template <int W>
+__device__ __forceinline__ RowT<W> zero_row() {
+  RowT<W> r;
 #pragma unroll
-  for (int j = 0; j < kMA; ++j) r.w[j] = 0;
+  for (int j = 0; j < W; ++j) r.w[j] = 0;
   return r;
 }
 __device__ __forceinline__ unsigned rl32m(unsigned x, int l) { return (unsigned)__builtin_amdgcn_readlane((int)x, l); }
@@ -117,25 +126,27 @@ __device__ __forceinline__ KeyRefs key_refs(const MapApplyPlan &p, unsigned long
 }
 
 // apply_keyset_rm's body for one key (map.rs:320-333)
-__device__ void key_rm(const MapApplyPlan &p, unsigned long long s, unsigned long long k, const Row &rm, int lane) {
+template <int W>
+__device__ void key_rm(const MapApplyPlan &p, unsigned long long s, unsigned long long k, const RowT<W> &rm, int lane) {
   const KeyRefs q = key_refs(p, s, k);
-  const Row e = load_row(q.ec, lane, p.A);
+  const RowT<W> e = load_row<W>(q.ec, lane, p.A);
   if (!any_nz(e)) return;  // no entry for this key
-  const Row e2 = forget_row(e, rm);
+  const RowT<W> e2 = forget_row(e, rm);
   const bool alive = any_nz(e2);
   store_row(q.ec, e2, lane, p.A);
   for (unsigned long long j = 0; j < p.V; ++j) {
     u64 *vr = q.vc + j * p.A;
-    const Row v = load_row(vr, lane, p.A);
+    const RowT<W> v = load_row<W>(vr, lane, p.A);
     if (!any_nz(v)) continue;
-    const Row v2 = alive ? forget_row(v, rm) : zero_row();  // MVReg::forget mvreg.rs:88-104
+    const RowT<W> v2 = alive ? forget_row(v, rm) : zero_row<W>();  // MVReg::forget mvreg.rs:88-104
     store_row(vr, v2, lane, p.A);
     if (!any_nz(v2) && lane == 0) q.vv[j] = 0;
   }
 }
 
 // forget every key of an LDS bitmap
-__device__ void keyset_rm(const MapApplyPlan &p, unsigned long long s, const u64 *bits, const Row &rm, int lane) {
+template <int W>
+__device__ void keyset_rm(const MapApplyPlan &p, unsigned long long s, const u64 *bits, const RowT<W> &rm, int lane) {
   for (unsigned long long w0 = 0; w0 < p.Kw; w0 += kWave) {
     const u64 word = (w0 + lane < p.Kw) ? bits[w0 + lane] : 0ull;
     u64 nz = __ballot(word != 0);
@@ -152,10 +163,12 @@ __device__ void keyset_rm(const MapApplyPlan &p, unsigned long long s, const u64
   }
 }
 
-__device__ __forceinline__ bool any_gt(const Row &r, const Row &c) {  // !(r <= c)
+template <int W>
+__device__ __forceinline__ bool any_gt(const RowT<W> &r, const RowT<W> &c) {  // !(r <= c)
   return !all_le(r, c);
 }
 
+template <int W>
 __global__ __launch_bounds__(kBlock) void map_apply_kernel(MapApplyPlan p) {
   extern __shared__ u64 lds[];
   const int lane = threadIdx.x % kWave;
@@ -175,7 +188,7 @@ __global__ __launch_bounds__(kBlock) void map_apply_kernel(MapApplyPlan p) {
       continue;
     }
     u64 *Cg = p.clock + s * p.clock_s;
-    Row C = load_row(Cg, lane, A);
+    RowT<W> C = load_row<W>(Cg, lane, A);
     const u64 *gdc = p.def_clock + s * p.Dcap * A;
     const u64 *gdk = p.def_keys + s * p.Dcap * p.Kw;
     for (unsigned long long i = lane; i < dcnt * A; i += kWave) dcl[i] = gdc[i];
@@ -201,7 +214,7 @@ __global__ __launch_bounds__(kBlock) void map_apply_kernel(MapApplyPlan p) {
           st |= 2u;
           continue;
         }
-        const Row oc = load_row(p.clk_pool + (unsigned long long)rr * A, lane, A);
+        const RowT<W> oc = load_row<W>(p.clk_pool + (unsigned long long)rr * A, lane, A);
         if (kind == 0) {  // ---- Op::Up
           const unsigned long long a = rl32m(h_actor, i), k = rl32m(h_key, i);
           const u64 kc = rl64m(h_counter, i);
@@ -212,7 +225,7 @@ __global__ __launch_bounds__(kBlock) void map_apply_kernel(MapApplyPlan p) {
           const int ja = (int)(a / kWave), la = (int)(a % kWave);
           u64 cj = C.w[0];
 #pragma unroll
-          for (int j = 1; j < kMA; ++j)
+          for (int j = 1; j < W; ++j)
             if (j == ja) cj = C.w[j];
           if (rl64m(cj, la) >= kc) continue;  // seen (:123-126)
           const KeyRefs q = key_refs(p, s, k);
@@ -225,10 +238,10 @@ __global__ __launch_bounds__(kBlock) void map_apply_kernel(MapApplyPlan p) {
             int last = -1, used = 0;
             for (unsigned long long j = 0; j < p.V; ++j) {
               u64 *vr = q.vc + j * A;
-              const Row v = load_row(vr, lane, A);
+              const RowT<W> v = load_row<W>(vr, lane, A);
               if (!any_nz(v)) continue;
               if (all_le(v, oc)) {  // partial_cmp in {Less, Equal}: dropped
-                store_row(vr, zero_row(), lane, A);
+                store_row(vr, zero_row<W>(), lane, A);
                 if (lane == 0) q.vv[j] = 0;
                 continue;
               }
@@ -246,13 +259,13 @@ __global__ __launch_bounds__(kBlock) void map_apply_kernel(MapApplyPlan p) {
                   wave_fence_m();
                   int w = 0;
                   for (unsigned long long j = 0; j < p.V; ++j) {
-                    const Row v = load_row(q.vc + j * A, lane, A);
+                    const RowT<W> v = load_row<W>(q.vc + j * A, lane, A);
                     if (!any_nz(v)) continue;
                     if ((unsigned long long)w != j) {
                       const u64 x = q.vv[j];
                       wave_fence_m();
                       store_row(q.vc + (unsigned long long)w * A, v, lane, A);
-                      store_row(q.vc + j * A, zero_row(), lane, A);
+                      store_row(q.vc + j * A, zero_row<W>(), lane, A);
                       if (lane == 0) {
                         q.vv[w] = x;
                         q.vv[j] = 0;
@@ -271,12 +284,12 @@ __global__ __launch_bounds__(kBlock) void map_apply_kernel(MapApplyPlan p) {
             }
           }
 #pragma unroll
-          for (int j = 0; j < kMA; ++j)
+          for (int j = 0; j < W; ++j)
             if (j == ja && lane == la) C.w[j] = kc;  // self.clock.apply(dot) (:133)
           wave_fence_m();
           unsigned nk = 0;  // apply_deferred (:134, :311-316)
           for (unsigned d = 0; d < dcnt; ++d) {
-            const Row rm = load_row(dcl + d * A, lane, A);
+            const RowT<W> rm = load_row<W>(dcl + d * A, lane, A);
             keyset_rm(p, s, dkb + d * p.Kw, rm, lane);
             wave_fence_m();
             if (any_gt(rm, C)) {
@@ -311,7 +324,7 @@ __global__ __launch_bounds__(kBlock) void map_apply_kernel(MapApplyPlan p) {
           if (!any_gt(oc, C)) continue;  // rm <= clock: not deferred (:336-345)
           int slot = -1;
           for (unsigned d = 0; d < dcnt; ++d)
-            if (rows_eq(load_row(dcl + d * A, lane, A), oc)) {
+            if (rows_eq(load_row<W>(dcl + d * A, lane, A), oc)) {
               slot = (int)d;
               break;
             }
@@ -383,8 +396,13 @@ extern "C" int crdt_map_apply_batch(crdt_ctx *ctx, const crdt_map_states *m, uin
   const unsigned long long want = (N + wpb - 1) / wpb;
   const unsigned long long cap = (unsigned long long)ctx->cu_count * 64;
   timing_begin(ctx, "map_apply");
-  hipLaunchKernelGGL(map_apply_kernel, dim3((unsigned)(want < cap ? want : cap)), dim3(wpb * kWave), per_wave * wpb,
-                     ctx->stream, p);
+  const dim3 grid((unsigned)(want < cap ? want : cap)), block(wpb * kWave);
+  if (A <= (size_t)kWave)
+    hipLaunchKernelGGL(map_apply_kernel<1>, grid, block, per_wave * wpb, ctx->stream, p);
+  else if (A <= (size_t)(2 * kWave))
+    hipLaunchKernelGGL(map_apply_kernel<2>, grid, block, per_wave * wpb, ctx->stream, p);
+  else
+    hipLaunchKernelGGL(map_apply_kernel<kMA>, grid, block, per_wave * wpb, ctx->stream, p);
   timing_end(ctx);
   CRDT_HIP(ctx, hipGetLastError());
   return CRDT_OK;

@@ -114,7 +114,9 @@ def test_map_apply_value_overflow(gpu_ctx):
     assert status[0] == 0 and got[0][0].entries == oracle_apply([[op1, op2]])[0][0].entries
 
 
-@pytest.mark.parametrize("N,T,K,A,V", [(256, 64, 16, 8, 4), (64, 100, 70, 33, 6)])
+# A = 8 / 33 run the one-word-per-lane kernel, 100 the two-word one, 200 the four-word one
+@pytest.mark.parametrize("N,T,K,A,V", [(256, 64, 16, 8, 4), (64, 100, 70, 33, 6), (48, 80, 24, 100, 8),
+                                       (32, 80, 20, 200, 8)])
 def test_map_apply_synth_streams(gpu_ctx, N, T, K, A, V):
     """The bench's device-generated streams (crdts_gpu.synth.map_op_streams) vs the oracle."""
     b = cg.synth.map_op_streams(N, T, K, A, seed=N + K, device="cuda:0")
