@@ -45,6 +45,7 @@ struct Tune {
   int map_spec = 1;    // ... speculative no-op scan
   int rows_blocks_per_cu = 0;  // row-pair / row-reduction kernels (causal.hip); 0 = per-kernel default
   int apply_hot_slots = 8;     // Orswot apply: deferred slots kept in LDS per state (the rest in HBM)
+  int map_forget_vec2 = 1;     // Map forget: 16-byte pieces per lane where the shape allows it
 };
 
 struct PendingTiming {

@@ -236,6 +236,63 @@ __global__ __launch_bounds__(kBlock) void map_forget_narrow_kernel(MapForgetPlan
 
 static bool al16(const void *p) { return ((uintptr_t)p & 15) == 0; }
 
+// A <= 128 even, V <= 4, 16-byte aligned rows: the narrow kernel with two pieces per lane (one
+// 16-byte non-temporal access per lane, LR = pow2 >= A/2 lanes per row) and 32-bit (state, key)
+// index math (N*K < 2^32, checked on the host).
+__global__ __launch_bounds__(kBlock) void map_forget_vec2_kernel(MapForgetPlan p) {
+  const unsigned rows = (unsigned)(p.N * p.K), K = (unsigned)p.K;
+  const int lane = threadIdx.x % kWave;
+  const int LR = 1 << p.lr_log;
+  const unsigned gl = lane & (LR - 1);
+  const unsigned RW = kWave >> p.lr_log;
+  const unsigned W = (unsigned)(p.A / 2);
+  const unsigned w0 = (blockIdx.x * (unsigned)kBlock + threadIdx.x) / kWave;
+  const unsigned nw = gridDim.x * (unsigned)(kBlock / kWave);
+  for (unsigned rb = w0 * RW * kU; rb < rows; rb += nw * RW * kU) {
+    u64x2 *er[kU], *vr[kU];
+    u64x2 ev[kU], yv[kU], vv[kU][4];
+    bool act[kU];
+    unsigned sk[kU][2];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const unsigned r = rb + u * RW + (lane >> p.lr_log);
+      const unsigned rr = r < rows ? r : rows - 1;
+      const unsigned s = rr / K, k = rr - s * K;
+      sk[u][0] = s;
+      sk[u][1] = k;
+      act[u] = r < rows && gl < W;
+      er[u] = reinterpret_cast<u64x2 *>(p.ec + s * p.ec_s + (unsigned long long)k * p.A) + gl;
+      vr[u] = reinterpret_cast<u64x2 *>(p.vclk + s * p.vclk_s + (unsigned long long)k * p.V * p.A) + gl;
+      const u64x2 z = {0ull, 0ull};
+      yv[u] = act[u] ? reinterpret_cast<const u64x2 *>(p.y + s * p.ystride)[gl] : z;
+      ev[u] = act[u] ? __builtin_nontemporal_load(er[u]) : z;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        vv[u][j] = (act[u] && (unsigned long long)j < p.V) ? __builtin_nontemporal_load(vr[u] + j * W) : z;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const unsigned r = rb + u * RW + (lane >> p.lr_log);
+      u64x2 e;
+      e.x = fgt(ev[u].x, yv[u].x);
+      e.y = fgt(ev[u].y, yv[u].y);
+      const bool alive = (group_any(__ballot((e.x | e.y) != 0), p.lr_log) >> (lane & ~(LR - 1))) & 1;  // map.rs:93-98
+      if (act[u]) __builtin_nontemporal_store(e, er[u]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if ((unsigned long long)j >= p.V) break;
+        u64x2 v;  // MVReg::forget mvreg.rs:88-104
+        v.x = alive ? fgt(vv[u][j].x, yv[u].x) : 0ull;
+        v.y = alive ? fgt(vv[u][j].y, yv[u].y) : 0ull;
+        if (act[u]) __builtin_nontemporal_store(v, vr[u] + j * W);
+        const bool keepv = (group_any(__ballot((v.x | v.y) != 0), p.lr_log) >> (lane & ~(LR - 1))) & 1;
+        if (r < rows && gl == 0 && !keepv) p.vval[sk[u][0] * p.vval_s + (unsigned long long)sk[u][1] * p.V + j] = 0;
+      }
+    }
+  }
+}
+
+
 static int launch_forget(crdt_ctx *ctx, ForgetPlan p) {
   if (p.nrows == 0 || p.A == 0) return CRDT_OK;
   p.vec2 = (p.A % 2 == 0) && (p.rstride % 2 == 0) && (p.sstride % 2 == 0 || p.ysel) && (p.ystride % 2 == 0) &&
@@ -304,9 +361,16 @@ extern "C" int crdt_map_forget_batch(crdt_ctx *ctx, const crdt_map_states *m, co
   if (K) {
     MapForgetPlan p{(u64 *)m->ec, (u64 *)m->vclk, (u64 *)m->vval, N, K, A, V, m->ec_stride, m->vclk_stride, m->vval_stride,
                     (const u64 *)y, y_stride, 0};
-    while (p.lr_log < 6 && (1ull << p.lr_log) < A) ++p.lr_log;  // a key's rows: one access per row
+    const bool vec2 = A % 2 == 0 && A <= 2 * (size_t)kWave && V <= 4 && N * K < (1ull << 32) &&
+                      m->ec_stride % 2 == 0 && m->vclk_stride % 2 == 0 && y_stride % 2 == 0 && al16(m->ec) &&
+                      al16(m->vclk) && al16(y) && ctx->tune.map_forget_vec2 != 0;
+    const size_t W = vec2 ? A / 2 : A;  // pieces per row
+    while (p.lr_log < 6 && (1ull << p.lr_log) < W) ++p.lr_log;  // a key's rows: one access per row
     timing_begin(ctx, "map_forget");
-    if (A <= (size_t)kWave && V <= 4)
+    if (vec2)
+      hipLaunchKernelGGL(map_forget_vec2_kernel, dim3(forget_grid(ctx, (N * K + kU - 1) / kU, p.lr_log)),
+                         dim3(kBlock), 0, ctx->stream, p);
+    else if (A <= (size_t)kWave && V <= 4)
       hipLaunchKernelGGL(map_forget_narrow_kernel, dim3(forget_grid(ctx, (N * K + kU - 1) / kU, p.lr_log)),
                          dim3(kBlock), 0, ctx->stream, p);
     else

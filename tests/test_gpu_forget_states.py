@@ -73,8 +73,15 @@ def test_orswot_forget_batch(gpu_ctx, seed, N, M, A, shared):
         _check_deferred(rows, o.deferred, A)
 
 
-@pytest.mark.parametrize("seed,R,K,A,shared", [(5, 24, 16, 8, False), (6, 16, 40, 32, True), (7, 10, 8, 65, False)])
-def test_map_forget_batch(gpu_ctx, seed, R, K, A, shared):
+# even A <= 128 runs map_forget_vec2_kernel (16-byte pieces), odd A <= 64 the narrow kernel, A = 65
+# (odd, > 64) the wide one; mfv2=0 forces the narrow kernel for an even A
+@pytest.mark.parametrize("seed,R,K,A,shared,tune", [
+    (5, 24, 16, 8, False, ""), (6, 16, 40, 32, True, ""), (7, 10, 8, 65, False, ""), (8, 12, 20, 100, False, ""),
+    (9, 20, 12, 7, True, ""), (10, 16, 24, 32, False, "mfv2=0")])
+def test_map_forget_batch(gpu_ctx, seed, R, K, A, shared, tune):
+    if tune:
+        gpu_ctx = cg.Context(0)
+        gpu_ctx.tune(tune)
     maps = O.gen_map_replicas(seed, R, K, A, steps=150)
     V = max(1, O.max_vals(maps))
     d = O.map_to_dense(maps, K, A, V)
