@@ -19,6 +19,20 @@ using u64x2 = unsigned long long __attribute__((ext_vector_type(2)));
 
 // One wave is 64 lanes on gfx950; every block size below is a multiple of it.
 constexpr int kWave = 64;
+
+// Waves per SIMD asked of the one-wave-per-state apply kernels (0: the compiler's choice, 6 at
+// 77 VGPRs).  Forcing 7 (~60 B/lane of scratch spills) made both kernels 8% faster at A <= 64
+// (profiles/r01_apply_wpe.log) but the spilling A = 200 instantiation of map_apply_kernel then
+// returned wrong states (tests/test_gpu_map_apply.py), so the default stays 0 until the op
+// headers move out of VGPRs and no spill is needed.
+#ifndef CRDT_APPLY_WPE
+#define CRDT_APPLY_WPE 0
+#endif
+#if CRDT_APPLY_WPE
+#define CRDT_APPLY_ATTR __attribute__((amdgpu_waves_per_eu(CRDT_APPLY_WPE)))
+#else
+#define CRDT_APPLY_ATTR
+#endif
 constexpr int kBlock = 256;
 
 struct KernelTimer {

@@ -169,7 +169,7 @@ __device__ __forceinline__ bool any_gt(const RowT<W> &r, const RowT<W> &c) {  //
 }
 
 template <int W>
-__global__ __launch_bounds__(kBlock) void map_apply_kernel(MapApplyPlan p) {
+__global__ __launch_bounds__(kBlock) CRDT_APPLY_ATTR void map_apply_kernel(MapApplyPlan p) {
   extern __shared__ u64 lds[];
   const int lane = threadIdx.x % kWave;
   const int wib = threadIdx.x / kWave;

@@ -111,7 +111,7 @@ __device__ __forceinline__ bool any_greater(const u64 (&r)[kCA], const u64 (&c)[
 
 // kCA clock words per lane: 1 for A <= 64 (fewer VGPRs, more waves per SIMD), 4 up to A = 256
 template <int kCA>
-__global__ __launch_bounds__(kBlock) void orswot_apply_kernel(OrswotApplyPlan p) {
+__global__ __launch_bounds__(kBlock) CRDT_APPLY_ATTR void orswot_apply_kernel(OrswotApplyPlan p) {
   extern __shared__ u64 lds[];
   const int lane = threadIdx.x % kWave;
   const int wib = threadIdx.x / kWave;

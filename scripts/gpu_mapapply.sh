@@ -4,3 +4,5 @@ tail -12 gpurun_out/mapapply_tests.log
 [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python -u scripts/bench_map_apply.py > gpurun_out/bench_mapapply.log 2>&1 || exit $?
 grep '^{' gpurun_out/bench_mapapply.log
+timeout -k 10 300 python -u scripts/bench_orswot_apply.py > gpurun_out/bench_apply.log 2>&1 || exit $?
+grep "^{" gpurun_out/bench_apply.log
