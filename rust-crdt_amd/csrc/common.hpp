@@ -20,7 +20,7 @@ using u64x2 = unsigned long long __attribute__((ext_vector_type(2)));
 // One wave is 64 lanes on gfx950; every block size below is a multiple of it.
 constexpr int kWave = 64;
 
-// Waves per SIMD asked of the one-wave-per-state apply kernels (0: the compiler's choice, 6 at
+// Waves per SIMD asked of map_apply_kernel (0: the compiler's choice, 6 at
 // 77 VGPRs).  Forcing 7 (~60 B/lane of scratch spills) made both kernels 8% faster at A <= 64
 // (profiles/r01_apply_wpe.log) but the spilling A = 200 instantiation of map_apply_kernel then
 // returned wrong states (tests/test_gpu_map_apply.py), so the default stays 0 until the op

@@ -28,6 +28,7 @@ namespace crdt {
 
 constexpr int kApplyMaxA = 256;
 constexpr int kCAMax = kApplyMaxA / kWave;  // clock words per lane at the widest A
+constexpr unsigned kBadOp = 0xFFFFFFFFu, kRmOp = 0xFFFFFFFEu;  // packed op header tags
 
 struct OrswotApplyPlan {
   u64 *clock;
@@ -111,7 +112,7 @@ __device__ __forceinline__ bool any_greater(const u64 (&r)[kCA], const u64 (&c)[
 
 // kCA clock words per lane: 1 for A <= 64 (fewer VGPRs, more waves per SIMD), 4 up to A = 256
 template <int kCA>
-__global__ __launch_bounds__(kBlock) CRDT_APPLY_ATTR void orswot_apply_kernel(OrswotApplyPlan p) {
+__device__ __forceinline__ void orswot_apply_body(const OrswotApplyPlan &p) {
   extern __shared__ u64 lds[];
   const int lane = threadIdx.x % kWave;
   const int wib = threadIdx.x / kWave;
@@ -152,27 +153,38 @@ __global__ __launch_bounds__(kBlock) CRDT_APPLY_ATTR void orswot_apply_kernel(Or
       // op headers, lane = op
       const unsigned long long o = base + lane;
       const bool ov = o < oe;
-      const unsigned h_kind = ov ? p.kind[o] : 0u;
-      const unsigned h_actor = ov && p.actor ? p.actor[o] : 0u;
-      const u64 h_counter = ov && p.counter ? p.counter[o] : 0ull;
-      const unsigned h_rm = ov && p.rm_row ? p.rm_row[o] : 0u;
-      const u64 h_mb = ov ? p.mem_off[o] : 0ull;
-      const u64 h_me = ov ? p.mem_off[o + 1] : 0ull;
+      // packed to keep VGPRs down: h_ka = actor of a valid Add, kRmOp for a Rm, kBadOp for a
+      // malformed op (kind > 1, actor >= A or member range reversed); h_cr = counter of an Add,
+      // rm row of a Rm; member offsets as 32 bits (an op whose member range ends at or beyond
+      // 2^32 is reported malformed, status bit 2, never silently truncated)
+      unsigned h_ka = kBadOp, h_mb = 0, h_me = 0;
+      u64 h_cr = 0;
+      if (ov) {
+        const unsigned kind = p.kind[o];
+        const u64 mb = p.mem_off[o], me = p.mem_off[o + 1];
+        h_mb = (unsigned)mb;
+        h_me = (unsigned)me;
+        const bool range_ok = me >= mb && me <= 0xFFFFFFFFull;
+        if (range_ok && kind == 0) {
+          const unsigned a = p.actor ? p.actor[o] : 0u;
+          h_ka = a < A ? a : kBadOp;
+          h_cr = p.counter ? p.counter[o] : 0ull;
+        } else if (range_ok && kind == 1) {
+          h_ka = kRmOp;
+          h_cr = p.rm_row ? p.rm_row[o] : 0u;
+        }
+      }
       const int nb = (int)((oe - base) < (unsigned long long)kWave ? (oe - base) : kWave);
       for (int i = 0; i < nb; ++i) {
-        const unsigned kind = rl32(h_kind, i);
-        const u64 mb = rl64(h_mb, i), me = rl64(h_me, i);
-        if (me < mb || kind > 1) {
+        const unsigned ka = rl32(h_ka, i);
+        const u64 mb = rl32(h_mb, i), me = rl32(h_me, i);
+        if (ka == kBadOp) {
           st |= 2u;
           continue;
         }
-        if (kind == 0) {  // ---- Op::Add
-          const unsigned long long a = rl32(h_actor, i);
-          const u64 k = rl64(h_counter, i);
-          if (a >= A) {
-            st |= 2u;
-            continue;
-          }
+        if (ka != kRmOp) {  // ---- Op::Add
+          const unsigned long long a = ka;
+          const u64 k = rl64(h_cr, i);
           const int ja = (int)(a / kWave), la = (int)(a % kWave);
           u64 cj = c[0];
 #pragma unroll
@@ -216,7 +228,7 @@ __global__ __launch_bounds__(kBlock) CRDT_APPLY_ATTR void orswot_apply_kernel(Or
           dcnt = nk;
           wave_fence();
         } else {  // ---- Op::Rm -> apply_rm (:230-250)
-          const unsigned rr = rl32(h_rm, i);
+          const unsigned rr = (unsigned)rl64(h_cr, i);
           if (rr >= p.n_rm_rows) {
             st |= 2u;
             continue;
@@ -295,6 +307,17 @@ __global__ __launch_bounds__(kBlock) CRDT_APPLY_ATTR void orswot_apply_kernel(Or
   }
 }
 
+// A <= 64: 72 VGPRs, no scratch, and asking for 7 waves per SIMD (the scheduler's target, the
+// same register count) is 9% faster (1.99 -> 1.80 ms, profiles/r01_apply_wpe.log).  The A <= 256
+// instance would spill at 7 waves, so it keeps the compiler's choice.
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7))) void orswot_apply_kernel_a64(
+    OrswotApplyPlan p) {
+  orswot_apply_body<1>(p);
+}
+__global__ __launch_bounds__(kBlock) void orswot_apply_kernel_a256(OrswotApplyPlan p) {
+  orswot_apply_body<kCAMax>(p);
+}
+
 }  // namespace crdt
 
 using namespace crdt;
@@ -335,9 +358,9 @@ extern "C" int crdt_orswot_apply_batch(crdt_ctx *ctx, const crdt_orswot_states *
   timing_begin(ctx, "orswot_apply");
   const dim3 grid((unsigned)(want < cap ? want : cap)), block(wpb * kWave);
   if (s.A <= (size_t)kWave)
-    hipLaunchKernelGGL(orswot_apply_kernel<1>, grid, block, per_wave * wpb, ctx->stream, p);
+    hipLaunchKernelGGL(orswot_apply_kernel_a64, grid, block, per_wave * wpb, ctx->stream, p);
   else
-    hipLaunchKernelGGL(orswot_apply_kernel<kCAMax>, grid, block, per_wave * wpb, ctx->stream, p);
+    hipLaunchKernelGGL(orswot_apply_kernel_a256, grid, block, per_wave * wpb, ctx->stream, p);
   timing_end(ctx);
   CRDT_HIP(ctx, hipGetLastError());
   return CRDT_OK;
