@@ -108,6 +108,29 @@ def test_orswot_apply_overflow_and_bad_ops(gpu_ctx):
     assert set(got[0].entries) == {2} and got[0].clock.dots == {0: 1}
 
 
+def test_orswot_apply_malformed_headers(gpu_ctx):
+    """Ops with kind > 1, a reversed member range or a member range ending at or beyond 2^32 are
+    skipped and flagged (status bit 2) without touching memory; the rest of the stream applies."""
+    A, M, Dcap = 4, 8, 2
+    add1, add2 = O.OrswotAdd(O.Dot(0, 1), [2]), O.OrswotAdd(O.Dot(1, 1), [3])
+    rm = O.OrswotRm(O.VClock({0: 1}), [4])
+    streams = [[add1, add2], [add1, rm], [add1, add2]]
+    st = [O.Orswot() for _ in streams]
+    clock, entries, dcl, dmb, cnt = dense_states(st, M, A, Dcap)
+    tc, te, tdc, tdm = to_dev(clock), to_dev(entries), to_dev(dcl), to_dev(dmb)
+    tcnt = torch.from_numpy(cnt).cuda()
+    ops = cg.orswot.encode_ops([[op_tuple(op) for op in ops] for ops in streams], A, "cuda:0")
+    ops.mem_off[2] = 1 << 32           # state 0's last op (op 1): member range reaches 2^32
+    ops.kind[2] = 2                    # state 1's first op: no such kind
+    ops.mem_off[6] = ops.mem_off[5] - 1  # state 2's last op (op 5): reversed range
+    status = cg.orswot.apply_batch(tc, te, tdc, tdm, tcnt, ops, ctx=gpu_ctx).cpu().numpy()
+    torch.cuda.synchronize()
+    assert status.tolist() == [2, 2, 2]
+    got = [to_object(to_host(tc), to_host(te), to_host(tdc), to_host(tdm), tcnt.cpu().numpy(), s) for s in range(3)]
+    exp = oracle_streams(st, [[add1], [rm], [add1]])
+    assert got == exp
+
+
 def test_orswot_apply_empty(gpu_ctx):
     st = [O.Orswot() for _ in range(5)]
     got, status = gpu_apply_streams(gpu_ctx, st, [[] for _ in st], 4, 2, Dcap=1)
