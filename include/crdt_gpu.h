@@ -178,8 +178,8 @@ int crdt_orswot_lub_many(crdt_ctx *ctx, const crdt_orswot_batch *in, crdt_orswot
  * none is an Rm (n_rm_rows = rows of rm_clock).
  * status[s] (device u32, written for every s): bit 0 = the deferred list needed more than Dcap
  * slots (the state is incomplete: retry with a larger Dcap), bit 1 = an op named an actor,
- * member or rm row out of range or a bad kind / member range (that op, or its bad members, were
- * skipped), bit 2 = def_count[s] > Dcap on input, bit 3 = op_off[s..s+1] invalid (bits 2 and 3:
+ * member or rm row out of range or a bad kind / member range (reversed, or ending past n_mem)
+ * (that op, or its bad members, were skipped), bit 2 = def_count[s] > Dcap on input, bit 3 = op_off[s..s+1] invalid (bits 2 and 3:
  * state left untouched).  Limits: A <= 256, Dcap*(A + Mw)*8 <= 65536. */
 typedef struct crdt_orswot_states {
   size_t N, M, A, Dcap;
@@ -202,7 +202,8 @@ typedef struct crdt_orswot_ops {
   const uint64_t *rm_clock; /* [n_rm_rows][A] */
   size_t n_rm_rows;
   const uint64_t *mem_off; /* [n_ops+1] */
-  const uint32_t *mem;
+  const uint32_t *mem;      /* [n_mem]   */
+  size_t n_mem;             /* entries of mem: a member range ending past it is malformed */
 } crdt_orswot_ops;
 
 int crdt_orswot_apply_batch(crdt_ctx *ctx, const crdt_orswot_states *states, const crdt_orswot_ops *ops,
@@ -252,9 +253,11 @@ int crdt_map_forget_batch(crdt_ctx *ctx, const crdt_map_states *states, const ui
  * Ops: kind 0 = Op::Up { dot: (actor, counter), key, op: Put { clock: clk_pool[clk_row*A ..],
  * val } }, kind 1 = Op::Rm { clock: clk_pool[clk_row*A ..], keyset: keys[key_off[o] ..
  * key_off[o+1]) } (key_off: n_ops+1 entries, may be NULL when no op is an Rm).
- * status[s]: bit 0 = deferred slots exhausted, bit 1 = an out-of-range op / key skipped,
+ * status[s]: bit 0 = deferred slots exhausted, bit 1 = an out-of-range op / key skipped (incl. a
+ * key range reversed or ending past n_keys),
  * bits 2-3 = invalid input (state untouched), bit 4 = a register needed more than V values (the
- * state is incomplete: retry with more slots).  Limits: A <= 256, 1 <= V <= 8,
+ * state is incomplete: retry with more slots), bit 5 = internal slot invariant violated (never
+ * expected; the value was not written).  Limits: A <= 256, 1 <= V <= 8,
  * Dcap*(A + Kw)*8 <= 65536. */
 typedef struct crdt_map_ops {
   size_t n_ops;
@@ -268,7 +271,8 @@ typedef struct crdt_map_ops {
   const uint64_t *clk_pool; /* [n_clk_rows][A] */
   size_t n_clk_rows;
   const uint64_t *key_off;  /* [n_ops+1] Rm */
-  const uint32_t *keys;
+  const uint32_t *keys;     /* [n_keys]    */
+  size_t n_keys;            /* entries of keys: a key range ending past it is malformed */
 } crdt_map_ops;
 
 int crdt_map_apply_batch(crdt_ctx *ctx, const crdt_map_states *states, uint64_t *def_clock, uint64_t *def_keys,

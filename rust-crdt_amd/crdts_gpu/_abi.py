@@ -83,7 +83,7 @@ class OrswotStates(ctypes.Structure):  # crdt_orswot_states
 class OrswotOps(ctypes.Structure):  # crdt_orswot_ops
     _fields_ = [
         ("n_ops", S), ("op_off", P), ("kind", P), ("actor", P), ("counter", P), ("rm_row", P),
-        ("rm_clock", P), ("n_rm_rows", S), ("mem_off", P), ("mem", P),
+        ("rm_clock", P), ("n_rm_rows", S), ("mem_off", P), ("mem", P), ("n_mem", S),
     ]
 
 
@@ -99,7 +99,8 @@ class MapStates(ctypes.Structure):  # crdt_map_states
 
 class MapOps(ctypes.Structure):  # crdt_map_ops
     _fields_ = [("n_ops", S), ("op_off", P), ("kind", P), ("actor", P), ("counter", P), ("key", P), ("val", P),
-                ("clk_row", P), ("clk_pool", P), ("n_clk_rows", S), ("key_off", P), ("keys", P)]
+                ("clk_row", P), ("clk_pool", P), ("n_clk_rows", S), ("key_off", P), ("keys", P),
+                ("n_keys", S)]
 
 
 class MapBatch(ctypes.Structure):  # crdt_map_batch

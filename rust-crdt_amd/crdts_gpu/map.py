@@ -318,6 +318,7 @@ def apply_batch(clock: torch.Tensor, ec: torch.Tensor, vclk: torch.Tensor, vval:
     o.key, o.val, o.clk_row, o.clk_pool = ops.key.data_ptr(), ops.val.data_ptr(), ops.clk_row.data_ptr(), \
         ops.clk_pool.data_ptr()
     o.n_clk_rows, o.key_off, o.keys = ops.clk_pool.shape[0], ops.key_off.data_ptr(), ops.keys.data_ptr()
+    o.n_keys = ops.keys.shape[0]
     status = torch.empty(N, dtype=torch.int32, device=clock.device)
     ctx.call("crdt_map_apply_batch", ctypes.byref(st), def_clock.data_ptr(), def_keys.data_ptr(),
              def_count.data_ptr(), Dcap, ctypes.byref(o), status.data_ptr())

@@ -226,7 +226,7 @@ def apply_batch(clock: torch.Tensor, entries: torch.Tensor, def_clock: torch.Ten
     o.op_off, o.kind, o.actor, o.counter = (ops.op_off.data_ptr(), ops.kind.data_ptr(), ops.actor.data_ptr(),
                                             ops.counter.data_ptr())
     o.rm_row, o.rm_clock, o.n_rm_rows = ops.rm_row.data_ptr(), ops.rm_clock.data_ptr(), ops.rm_clock.shape[0]
-    o.mem_off, o.mem = ops.mem_off.data_ptr(), ops.mem.data_ptr()
+    o.mem_off, o.mem, o.n_mem = ops.mem_off.data_ptr(), ops.mem.data_ptr(), ops.mem.shape[0]
     status = torch.empty(N, dtype=torch.int32, device=clock.device)
     ctx.call("crdt_orswot_apply_batch", ctypes.byref(st), ctypes.byref(o), dptr(status))
     return status

@@ -361,15 +361,20 @@ extern "C" int crdt_map_forget_batch(crdt_ctx *ctx, const crdt_map_states *m, co
   if (K) {
     MapForgetPlan p{(u64 *)m->ec, (u64 *)m->vclk, (u64 *)m->vval, N, K, A, V, m->ec_stride, m->vclk_stride, m->vval_stride,
                     (const u64 *)y, y_stride, 0};
-    const bool vec2 = A % 2 == 0 && A <= 2 * (size_t)kWave && V <= 4 && N * K < (1ull << 32) &&
+    // the vec2 kernel walks rows with 32-bit indices: the last row plus one whole grid step must
+    // stay below 2^32 so `rb += step` can never wrap (a wrapped walk would never exit)
+    int lr2 = 0;
+    while (lr2 < 6 && (1ull << lr2) < A / 2) ++lr2;
+    const unsigned long long grid2 = forget_grid(ctx, (N * K + kU - 1) / kU, lr2);
+    const unsigned long long step2 = grid2 * (kBlock / kWave) * (kWave >> lr2) * kU;
+    const bool vec2 = A % 2 == 0 && A <= 2 * (size_t)kWave && V <= 4 && N * K + step2 <= (1ull << 32) &&
                       m->ec_stride % 2 == 0 && m->vclk_stride % 2 == 0 && y_stride % 2 == 0 && al16(m->ec) &&
                       al16(m->vclk) && al16(y) && ctx->tune.map_forget_vec2 != 0;
     const size_t W = vec2 ? A / 2 : A;  // pieces per row
     while (p.lr_log < 6 && (1ull << p.lr_log) < W) ++p.lr_log;  // a key's rows: one access per row
     timing_begin(ctx, "map_forget");
     if (vec2)
-      hipLaunchKernelGGL(map_forget_vec2_kernel, dim3(forget_grid(ctx, (N * K + kU - 1) / kU, p.lr_log)),
-                         dim3(kBlock), 0, ctx->stream, p);
+      hipLaunchKernelGGL(map_forget_vec2_kernel, dim3((unsigned)grid2), dim3(kBlock), 0, ctx->stream, p);
     else if (A <= (size_t)kWave && V <= 4)
       hipLaunchKernelGGL(map_forget_narrow_kernel, dim3(forget_grid(ctx, (N * K + kU - 1) / kU, p.lr_log)),
                          dim3(kBlock), 0, ctx->stream, p);

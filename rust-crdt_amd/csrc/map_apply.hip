@@ -47,6 +47,7 @@ struct MapApplyPlan {
   unsigned long long n_clk_rows;
   const u64 *key_off;
   const uint32_t *keys;
+  unsigned long long n_keys;
   unsigned long long n_ops;
   uint32_t *status;
   int wpb;
@@ -277,9 +278,16 @@ __global__ __launch_bounds__(kBlock) CRDT_APPLY_ATTR void map_apply_kernel(MapAp
                   slot = w;
                 }
               }
+              // readlane with every lane active: inside `if (lane == 0)` only lane 0 of a
+              // spilled h_val would be reloaded and lane i's copy would be stale
+              const u64 pv = rl64m(h_val, i);
+              if (slot >= (int)p.V) {  // unreachable by construction; reported, never written
+                st |= 32u;
+                slot = -1;
+              }
               if (slot >= 0) {
                 store_row(q.vc + (unsigned long long)slot * A, oc, lane, A);
-                if (lane == 0) q.vv[slot] = rl64m(h_val, i);
+                if (lane == 0) q.vv[slot] = pv;
               }
             }
           }
@@ -304,7 +312,7 @@ __global__ __launch_bounds__(kBlock) CRDT_APPLY_ATTR void map_apply_kernel(MapAp
           wave_fence_m();
         } else {  // ---- Op::Rm -> apply_keyset_rm (:318-348)
           const u64 kb = rl64m(h_kb, i), ke = rl64m(h_ke, i);
-          if (ke < kb) {
+          if (ke < kb || ke > p.n_keys) {  // reversed, or runs past the keys buffer
             st |= 2u;
             continue;
           }
@@ -392,7 +400,7 @@ extern "C" int crdt_map_apply_batch(crdt_ctx *ctx, const crdt_map_states *m, uin
                  (u64 *)m->vval, m->vval_stride, (u64 *)def_clock, (u64 *)def_keys, def_count, N, K, A, V, Kw, Dcap,
                  (const u64 *)ops->op_off, ops->kind, ops->actor, (const u64 *)ops->counter, ops->key,
                  (const u64 *)ops->val, ops->clk_row, (const u64 *)ops->clk_pool, ops->n_clk_rows,
-                 (const u64 *)ops->key_off, ops->keys, ops->n_ops, status, wpb};
+                 (const u64 *)ops->key_off, ops->keys, ops->keys ? ops->n_keys : 0, ops->n_ops, status, wpb};
   const unsigned long long want = (N + wpb - 1) / wpb;
   const unsigned long long cap = (unsigned long long)ctx->cu_count * 64;
   timing_begin(ctx, "map_apply");

@@ -47,6 +47,7 @@ struct OrswotApplyPlan {
   unsigned long long n_rm_rows;
   const u64 *mem_off;
   const uint32_t *mem;
+  unsigned long long n_mem;
   unsigned long long n_ops;
   uint32_t *status;
   int wpb;
@@ -156,7 +157,8 @@ __device__ __forceinline__ void orswot_apply_body(const OrswotApplyPlan &p) {
       // packed to keep VGPRs down: h_ka = actor of a valid Add, kRmOp for a Rm, kBadOp for a
       // malformed op (kind > 1, actor >= A or member range reversed); h_cr = counter of an Add,
       // rm row of a Rm; member offsets as 32 bits (an op whose member range ends at or beyond
-      // 2^32 is reported malformed, status bit 2, never silently truncated)
+      // 2^32 is reported malformed, status bit 1, never silently truncated; so is a range that
+      // runs past the n_mem entries of mem)
       unsigned h_ka = kBadOp, h_mb = 0, h_me = 0;
       u64 h_cr = 0;
       if (ov) {
@@ -164,7 +166,7 @@ __device__ __forceinline__ void orswot_apply_body(const OrswotApplyPlan &p) {
         const u64 mb = p.mem_off[o], me = p.mem_off[o + 1];
         h_mb = (unsigned)mb;
         h_me = (unsigned)me;
-        const bool range_ok = me >= mb && me <= 0xFFFFFFFFull;
+        const bool range_ok = me >= mb && me <= 0xFFFFFFFFull && me <= p.n_mem;
         if (range_ok && kind == 0) {
           const unsigned a = p.actor ? p.actor[o] : 0u;
           h_ka = a < A ? a : kBadOp;
@@ -352,7 +354,7 @@ extern "C" int crdt_orswot_apply_batch(crdt_ctx *ctx, const crdt_orswot_states *
                     (u64 *)s.def_clock, (u64 *)s.def_members, s.def_count, s.N, s.M, s.A, Mw, s.Dcap, Dh,
                     (const u64 *)ops->op_off, ops->kind, ops->actor, (const u64 *)ops->counter, ops->rm_row,
                     (const u64 *)ops->rm_clock, ops->rm_clock ? ops->n_rm_rows : 0, (const u64 *)ops->mem_off,
-                    ops->mem, ops->n_ops, status, wpb};
+                    ops->mem, ops->mem ? ops->n_mem : 0, ops->n_ops, status, wpb};
   const unsigned long long want = (s.N + wpb - 1) / wpb;
   const unsigned long long cap = (unsigned long long)ctx->cu_count * 64;
   timing_begin(ctx, "orswot_apply");

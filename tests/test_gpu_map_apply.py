@@ -114,6 +114,34 @@ def test_map_apply_value_overflow(gpu_ctx):
     assert status[0] == 0 and got[0][0].entries == oracle_apply([[op1, op2]])[0][0].entries
 
 
+def test_map_apply_key_range_past_buffer(gpu_ctx):
+    """An Rm whose key range runs past the n_keys entries of `keys` (or is reversed) is malformed
+    (status bit 1) and skipped without reading past the buffer; the rest of the stream applies."""
+    a = O.Map(O.MVReg)
+    up = a.update(1, a.get(1).derive_add_ctx(0), lambda r, c: r.write(7, c))
+    a.apply(up)
+    rm = a.rm(1, a.get(1).derive_rm_ctx())
+    up2 = a.update(2, a.get(2).derive_add_ctx(0), lambda r, c: r.write(8, c))
+    streams = [[up, rm, up2], [up, rm]]
+    K, A, V, Dcap = 4, 2, 2, 2
+    N, Kw = len(streams), 1
+    z = lambda *s: torch.zeros(s, dtype=torch.int64, device="cuda:0")  # noqa: E731
+    clock, ec, vclk, vval, dcl, dks = z(N, A), z(N, K, A), z(N, K, V, A), z(N, K, V), z(N, Dcap, A), z(N, Dcap, Kw)
+    cnt = torch.zeros(N, dtype=torch.int32, device="cuda:0")
+    ops = cg.map.encode_ops([[op_tuple(o) for o in s] for s in streams], A, "cuda:0")
+    n_keys = ops.keys.shape[0]
+    ops.key_off[2] = n_keys + 4096     # state 0's Rm (op 1): range far past keys
+    ops.key_off[5] = n_keys + 1        # state 1's Rm (op 4, the last op): one past the end
+    status = cg.map.apply_batch(clock, ec, vclk, vval, dcl, dks, cnt, ops, ctx=gpu_ctx).cpu().numpy()
+    torch.cuda.synchronize()
+    assert status.tolist() == [2, 2]
+    exp, _ = oracle_apply([[up, up2], [up]])
+    c, e, vc, vv = to_host(clock), to_host(ec), to_host(vclk), to_host(vval)
+    for s in range(N):
+        assert int(cnt[s]) == 0
+        assert O.dense_to_map(c[s], e[s], vc[s], vv[s], []) == exp[s], s
+
+
 # A = 8 / 33 run the one-word-per-lane kernel, 100 the two-word one, 200 the four-word one
 @pytest.mark.parametrize("N,T,K,A,V", [(256, 64, 16, 8, 4), (64, 100, 70, 33, 6), (48, 80, 24, 100, 8),
                                        (32, 80, 20, 200, 8)])

@@ -131,6 +131,28 @@ def test_orswot_apply_malformed_headers(gpu_ctx):
     assert got == exp
 
 
+def test_orswot_apply_member_range_past_buffer(gpu_ctx):
+    """A member range that runs past the n_mem entries of `mem` is malformed (status bit 1): the
+    op is skipped without reading past the buffer, the rest of the stream applies."""
+    A, M, Dcap = 4, 8, 2
+    add1, add2 = O.OrswotAdd(O.Dot(0, 1), [2]), O.OrswotAdd(O.Dot(1, 1), [3, 5])
+    rm = O.OrswotRm(O.VClock({0: 1}), [2])
+    streams = [[add1, rm], [add1, add2]]
+    st = [O.Orswot() for _ in streams]
+    clock, entries, dcl, dmb, cnt = dense_states(st, M, A, Dcap)
+    tc, te, tdc, tdm = to_dev(clock), to_dev(entries), to_dev(dcl), to_dev(dmb)
+    tcnt = torch.from_numpy(cnt).cuda()
+    ops = cg.orswot.encode_ops([[op_tuple(op) for op in ops] for ops in streams], A, "cuda:0")
+    n_mem = ops.mem.shape[0]
+    ops.mem_off[2] = n_mem + 1         # op 1 (state 0's Rm) ends one past mem; op 2 is then reversed
+    ops.mem_off[4] = n_mem + 4096      # op 3 (state 1's add2, the last op) ends far past mem
+    status = cg.orswot.apply_batch(tc, te, tdc, tdm, tcnt, ops, ctx=gpu_ctx).cpu().numpy()
+    torch.cuda.synchronize()
+    assert status.tolist() == [2, 2]
+    got = [to_object(to_host(tc), to_host(te), to_host(tdc), to_host(tdm), tcnt.cpu().numpy(), s) for s in range(2)]
+    assert got == oracle_streams(st, [[add1], []])
+
+
 def test_orswot_apply_empty(gpu_ctx):
     st = [O.Orswot() for _ in range(5)]
     got, status = gpu_apply_streams(gpu_ctx, st, [[] for _ in st], 4, 2, Dcap=1)
