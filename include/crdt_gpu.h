@@ -438,7 +438,8 @@ int crdt_gset_apply_batch(crdt_ctx *ctx, uint64_t *states, size_t N, size_t U, s
                           const uint32_t *state_idx, const uint32_t *element, size_t n_ops, uint32_t *bad);
 
 /* ---- synthetic inputs (bench / test data, generated in HBM) --------------------------------
- * Counter-based and reproducible on the CPU (tests/golden/make_golden.py restates them).
+ * Counter-based and reproducible on the CPU (oracle/oracle.py synth_* restates them; small
+ * fixtures of both are pinned by tests/golden/make_golden.py -> tests/golden/synth.json).
  * kind 0 = clock/counter cells, 1 = GSet bitmap words, 2 = LWW markers, 3 = LWW vals.
  * Row r < rows of the output is row (first_row + r) of the global synthetic matrix: cell
  * (first_row + r, i) gets synth(seed, (first_row + r)*width + i), stored at out[r*row_stride + i].
@@ -449,7 +450,8 @@ int crdt_synth_fill(crdt_ctx *ctx, uint64_t *out, size_t rows, size_t width, siz
 /* Well-formed synthetic Orswot replicas, packed clock[R][A] and entries[R][M][A] (replica r is
  * global replica first_row + r).  clock[r][a] = synth(seed, r*A + a) % (kmax + 1); actor a's
  * k-th add targets member (a*P + k) mod M (P = 0x9E3779B1 mod M), so a dot is unique and
- * entries[r][m][a] = k <= clock[r][a] or 0; a quarter of the cells are observed removes (0).
+ * entries[r][m][a] = k <= clock[r][a] or 0: a quarter of the dots are removed, and a replica has
+ * observed (zeroed) a removed dot once clock[r][a] >= k + 1 + delta(m, a), delta in 0..7.
  * Requires kmax < M.  Restated on the CPU by oracle.synth_orswot. */
 int crdt_synth_orswot(crdt_ctx *ctx, uint64_t *clock, uint64_t *entries, size_t R, size_t M,
                       size_t A, size_t first_row, uint64_t seed, uint64_t kmax);

@@ -684,9 +684,10 @@ def synth_orswot(seed: int, R: int, M: int, A: int, kmax: int, row0: int = 0):
     pm = np.uint64(0x9E3779B1 % M)
     k = (m[:, None] + np.uint64(M) - (a[None, :] * pm) % np.uint64(M)) % np.uint64(M)  # (M, A)
     e = np.where((k[None] >= 1) & (k[None] <= c[:, None, :]), k[None], np.uint64(0))
-    cell = (r[:, None, None] * np.uint64(M * A) + m[None, :, None] * np.uint64(A) + a[None, None, :])
-    with np.errstate(over="ignore"):
-        obs = (mix64(np.uint64(0xD1B54A32D192ED03) + cell) & np.uint64(3)) == 0
+    with np.errstate(over="ignore"):  # dot (m, a) removed w.p. 1/4, observed past k + 1 + delta
+        hd = mix64(np.uint64(0xD1B54A32D192ED03) + m[:, None] * np.uint64(A) + a[None, :])  # (M, A)
+    thr = k + np.uint64(1) + ((hd >> np.uint64(8)) & np.uint64(7))
+    obs = ((hd & np.uint64(3)) == 0)[None] & (c[:, None, :] >= thr[None])
     e = np.where(obs, np.uint64(0), e).astype(np.uint64)
     return c.astype(np.uint64), e
 
@@ -1005,6 +1006,18 @@ def dense_orswot_lub(clock, entries, def_clock, def_members):
         if np.any(rm > c):
             surv.setdefault(tuple(int(x) for x in rm), set()).update(ms)
     return c, e, {(k, frozenset(v)) for k, v in surv.items()}
+
+
+def dense_orswot_survivors(final_clock, def_clock, def_members):
+    """The deferred part of dense_orswot_lub on whole member bitmaps, given the folded clock:
+    a remove survives iff !(rm <= C) (orswot.rs:240-249), survivors with identical rm clocks
+    merge their member sets (the HashMap<VClock, HashSet<M>> of :242-246).  Returns the set of
+    (rm clock tuple, frozenset members)."""
+    c = np.asarray(final_clock, np.uint64)
+    surv = {}
+    for d in np.flatnonzero(np.any(np.asarray(def_clock, np.uint64) > c[None, :], axis=1)):
+        surv.setdefault(tuple(int(x) for x in def_clock[d]), set()).update(bitmap_members(def_members[d]))
+    return {(k, frozenset(v)) for k, v in surv.items()}
 
 
 # ---------------------------------------------------------------------------------------

@@ -25,12 +25,29 @@ def _bias(t: torch.Tensor) -> torch.Tensor:
     return t ^ torch.tensor(SIGN, dtype=t.dtype, device=t.device)
 
 
+def _gloo(group) -> bool:
+    return dist.get_backend(group) == "gloo"
+
+
+def all_reduce_(t: torch.Tensor, op, group=None) -> torch.Tensor:
+    """In-place all-reduce.  gloo has no device-memory collectives on ROCm, so a device tensor is
+    staged through host memory there (tests run two ranks on one GPU that way; RCCL refuses two
+    ranks per GPU).  RCCL ("nccl") reduces in place in HBM."""
+    if t.is_cuda and _gloo(group):
+        h = t.cpu()
+        dist.all_reduce(h, op=op, group=group)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, op=op, group=group)
+    return t
+
+
 def allreduce_umax_(partial: torch.Tensor, group=None) -> torch.Tensor:
     """In-place unsigned-64 max all-reduce of an int64 tensor holding u64 bits."""
     if partial.dtype != torch.int64:
         raise TypeError("allreduce_umax_: int64 tensor holding u64 bits expected")
     b = _bias(partial)
-    dist.all_reduce(b, op=dist.ReduceOp.MAX, group=group)
+    all_reduce_(b, dist.ReduceOp.MAX, group)
     partial.copy_(_bias(b))
     return partial
 
@@ -39,8 +56,10 @@ def allgather_rows(partial: torch.Tensor, group=None) -> torch.Tensor:
     """(…, W) partial -> (world, …, W) stacked in rank order."""
     world = dist.get_world_size(group)
     out = torch.empty((world,) + tuple(partial.shape), dtype=partial.dtype, device=partial.device)
-    if dist.get_backend(group) == "gloo":  # gloo has no all_gather_into_tensor
-        dist.all_gather(list(out.unbind(0)), partial.contiguous(), group=group)
+    if _gloo(group):  # gloo has no all_gather_into_tensor and no device-memory collectives here
+        host = torch.empty((world,) + tuple(partial.shape), dtype=partial.dtype)
+        dist.all_gather(list(host.unbind(0)), partial.contiguous().cpu(), group=group)
+        out.copy_(host)
     else:
         dist.all_gather_into_tensor(out, partial.contiguous(), group=group)
     return out
@@ -109,7 +128,7 @@ def lwwreg_lub_many_sharded(marker: torch.Tensor, val: torch.Tensor, base: int, 
         pm, pv, _ = local(gm[:, :rank].contiguous(), gv[:, :rank].contiguous())
         _, _, lf = local(m2, v2, init=(pm, pv))
     fc = torch.where(lf == -1, torch.full_like(lf, NO_CONFLICT), lf + base)
-    dist.all_reduce(fc, op=dist.ReduceOp.MIN, group=group)
+    all_reduce_(fc, dist.ReduceOp.MIN, group)
     fc = torch.where(fc == NO_CONFLICT, torch.full_like(fc, -1), fc)
     fm, fv, _ = local(gm, gv)
     return (fm[0], fv[0], fc[0]) if squeeze else (fm, fv, fc)
@@ -224,5 +243,5 @@ def map_lub_many_sharded(clock: torch.Tensor, ec: torch.Tensor, vclk: torch.Tens
     gk = expand_key_bitmaps(res.def_keys, k0, K)
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     if world > 1:
-        dist.all_reduce(gk, op=dist.ReduceOp.SUM, group=group)
+        all_reduce_(gk, dist.ReduceOp.SUM, group)
     return res._replace(def_keys=gk)

@@ -20,11 +20,11 @@ using u64x2 = unsigned long long __attribute__((ext_vector_type(2)));
 // One wave is 64 lanes on gfx950; every block size below is a multiple of it.
 constexpr int kWave = 64;
 
-// Waves per SIMD asked of map_apply_kernel (0: the compiler's choice, 6 at
-// 77 VGPRs).  Forcing 7 (~60 B/lane of scratch spills) made both kernels 8% faster at A <= 64
-// (profiles/r01_apply_wpe.log) but the spilling A = 200 instantiation of map_apply_kernel then
-// returned wrong states (tests/test_gpu_map_apply.py), so the default stays 0 until the op
-// headers move out of VGPRs and no spill is needed.
+// Waves per SIMD asked of the A > 64 map_apply_kernel instances (0: the compiler's choice).  The
+// A <= 64 instance asks for 7 (map_apply.hip).  Round 1 blamed a miscompute of a forced-7 build
+// on spilling; the cause was a readlane of a spilled VGPR inside a one-lane branch (only the
+// active lane's copy is reloaded), fixed in map_apply.hip, and the forced build now passes
+// tests/test_gpu_map_apply.py (profiles/r02_map_apply_wpe7_tests.log).
 #ifndef CRDT_APPLY_WPE
 #define CRDT_APPLY_WPE 0
 #endif

@@ -170,7 +170,7 @@ __device__ __forceinline__ bool any_gt(const RowT<W> &r, const RowT<W> &c) {  //
 }
 
 template <int W>
-__global__ __launch_bounds__(kBlock) CRDT_APPLY_ATTR void map_apply_kernel(MapApplyPlan p) {
+__device__ __forceinline__ void map_apply_body(const MapApplyPlan &p) {
   extern __shared__ u64 lds[];
   const int lane = threadIdx.x % kWave;
   const int wib = threadIdx.x / kWave;
@@ -368,6 +368,18 @@ __global__ __launch_bounds__(kBlock) CRDT_APPLY_ATTR void map_apply_kernel(MapAp
   }
 }
 
+// A <= 64: asking for 7 waves per SIMD (72 VGPRs, 28 B/lane of spills) is 7% faster than the
+// compiler's 6 (3.29 vs 3.53 ms, profiles/r02_map_apply_wpe7_ab.log).  Round 1's miscompute at
+// that occupancy was a readlane of a spilled VGPR inside `if (lane == 0)` (fixed above), not the
+// spilling itself; the wider instances keep the compiler's choice (they would spill 44-116 B/lane).
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7))) void map_apply_kernel_w1(MapApplyPlan p) {
+  map_apply_body<1>(p);
+}
+template <int W>
+__global__ __launch_bounds__(kBlock) CRDT_APPLY_ATTR void map_apply_kernel(MapApplyPlan p) {
+  map_apply_body<W>(p);
+}
+
 }  // namespace crdt
 
 using namespace crdt;
@@ -406,7 +418,7 @@ extern "C" int crdt_map_apply_batch(crdt_ctx *ctx, const crdt_map_states *m, uin
   timing_begin(ctx, "map_apply");
   const dim3 grid((unsigned)(want < cap ? want : cap)), block(wpb * kWave);
   if (A <= (size_t)kWave)
-    hipLaunchKernelGGL(map_apply_kernel<1>, grid, block, per_wave * wpb, ctx->stream, p);
+    hipLaunchKernelGGL(map_apply_kernel_w1, grid, block, per_wave * wpb, ctx->stream, p);
   else if (A <= (size_t)(2 * kWave))
     hipLaunchKernelGGL(map_apply_kernel<2>, grid, block, per_wave * wpb, ctx->stream, p);
   else

@@ -2,7 +2,7 @@
 //
 // Bench and parity inputs are far larger than what is worth shipping over PCIe (config 2 is
 // 6 GiB), so they are generated on device from a stateless hash that the CPU restates
-// bit-for-bit (tests/golden/make_golden.py, oracle/oracle.py: synth_*).
+// bit-for-bit (oracle/oracle.py: synth_*; tests/golden/make_golden.py writes small fixtures).
 //   h(seed, idx) = splitmix64 finaliser of (seed + (idx + 1) * 0x9E3779B97F4A7C15)
 //   kind 0, counters : (h & 3) == 0 -> 0 (actor absent, 1/4);  ((h >> 2) & 63) == 0 -> h
 //                      (full-range u64, 3/256);  else h >> 16 (48-bit)
@@ -80,8 +80,12 @@ extern "C" int crdt_synth_fill(crdt_ctx *ctx, uint64_t *out, size_t rows, size_t
 //   clock[r][a]      = synth(seed, r*A + a) % (kmax + 1)
 //   actor a's k-th add targets member mem(a, k) = (a*P + k) mod M, so for member m the only
 //   candidate event is k(m, a) = (m - a*P) mod M (kmax < M keeps it unique);
-//   entries[r][m][a] = k(m, a) if 1 <= k(m, a) <= clock[r][a] and the cell's hash does not
-//                      mark an observed remove (1/4 of cells), else 0.
+//   entries[r][m][a] = k(m, a) if 1 <= k(m, a) <= clock[r][a] and replica r has not observed a
+//                      remove of that dot, else 0.  A quarter of the dots are removed (the dot's
+//                      hash hd(m, a) & 3 == 0); the remove is observed by the replicas that have
+//                      seen actor a advance past it: clock[r][a] >= k + 1 + ((hd >> 8) & 7).
+//   So the fold keeps exactly the dots nobody has observed removed (a non-empty set), as a
+//   remove that propagates with the actor's history would leave it.
 namespace crdt {
 
 constexpr u64 kOrswotP = 0x9E3779B1ULL;
@@ -113,7 +117,8 @@ __global__ __launch_bounds__(kBlock) void synth_orswot_kernel(u64 *clock, u64 *e
     const u64 c = mix64(seed + (gr * A + a + 1) * 0x9E3779B97F4A7C15ULL) % (kmax + 1);
     const u64 k = (m + M - (a * pm) % M) % M;
     u64 e = (k >= 1 && k <= c) ? k : 0;
-    if (e && (mix64(kObsSalt + (gr * M * A + m * A + a)) & 3) == 0) e = 0;
+    const u64 hd = mix64(kObsSalt + (m * A + a));
+    if (e && (hd & 3) == 0 && c >= k + 1 + ((hd >> 8) & 7)) e = 0;
     entries[i] = e;
   }
 }
