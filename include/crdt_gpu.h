@@ -209,6 +209,20 @@ typedef struct crdt_orswot_ops {
 int crdt_orswot_apply_batch(crdt_ctx *ctx, const crdt_orswot_states *states, const crdt_orswot_ops *ops,
                             uint32_t *status);
 
+/* Pairwise in-place Orswot merge (the batched form of CvRDT::merge, traits.rs:4-7 ->
+ * Orswot::merge orswot.rs:81-149 with apply_rm :230-250 and apply_deferred :281-286):
+ * self[i].merge(other[i]) for i < N, exact for ANY pair of states.  Both sides use the
+ * crdt_orswot_states layout (the apply layout: per-state deferred slots, clocks pairwise distinct
+ * within a state); N, M and A must match, Dcap may differ.  self's clock, entries, deferred slots
+ * and def_count are rewritten; other is read only (its def_count may be NULL when its Dcap is 0).
+ * The surviving deferred removes (!(rm <= merged clock)) of both sides are compacted into self's
+ * slots (self's survivors first, in slot order, then other's; identical clocks merge their member
+ * sets, as the reference's HashMap<VClock, HashSet<M>> does).
+ * status[s] (device u32): bit 0 = more survivors than self's Dcap (state incomplete), bit 2 =
+ * def_count above Dcap on input (state untouched).  Limit: Dcap(self) + Dcap(other) <= 512. */
+int crdt_orswot_merge_batch(crdt_ctx *ctx, const crdt_orswot_states *self, const crdt_orswot_states *other,
+                            uint32_t *status);
+
 /* ---- batched Causal::forget of whole states -----------------------------------
  * State s forgets the clock y + s*y_stride (y_stride = 0: one clock for every state), in place.
  * Orswot::forget (orswot.rs:150-183): clock, entry clocks (an emptied entry = all-zero row =
@@ -277,6 +291,26 @@ typedef struct crdt_map_ops {
 
 int crdt_map_apply_batch(crdt_ctx *ctx, const crdt_map_states *states, uint64_t *def_clock, uint64_t *def_keys,
                          uint32_t *def_count, size_t Dcap, const crdt_map_ops *ops, uint32_t *status);
+
+/* Deferred-remove slots of N Map states (the crdt_map_apply_batch convention): state s holds
+ * count[s] <= Dcap removes, rm clock clock[(s*Dcap + d)*A + a], key bitmap keys[(s*Dcap + d)*Kw + w]. */
+typedef struct crdt_map_deferred {
+  uint64_t *clock;
+  uint64_t *keys;
+  uint32_t *count;
+  size_t Dcap;
+} crdt_map_deferred;
+
+/* Pairwise in-place Map<K, MVReg<u64>> merge: self[i].merge(other[i]) for i < N (Map::merge
+ * map.rs:140-220, MVReg::merge mvreg.rs:112-128, MVReg::forget :88-104, apply_keyset_rm
+ * map.rs:318-348), exact for ANY pair of states, on the crdt_map_states layout (N, K, A equal on
+ * both sides; V may differ; value slots in Vec order: self's kept values then other's added ones,
+ * written from slot 0, empty slots zeroed).  Deferred removes as crdt_orswot_merge_batch over key
+ * bitmaps.  status[s]: bit 0 = deferred slots exhausted, bit 2 = invalid def_count (untouched),
+ * bit 4 = some register needed more than self's V slots (that key is incomplete).
+ * Limits: A <= 256, 1 <= V <= 8 on each side, Dcap(self) + Dcap(other) <= 512. */
+int crdt_map_merge_batch(crdt_ctx *ctx, const crdt_map_states *self, const crdt_map_deferred *self_def,
+                         const crdt_map_states *other, const crdt_map_deferred *other_def, uint32_t *status);
 
 /* ---- multi-GPU: replica-sharded lub over RCCL ----------------------------
  * One process (one ctx) per GPU.  Rank 0 calls crdt_comm_unique_id and sends the 128 bytes to

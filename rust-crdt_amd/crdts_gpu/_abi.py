@@ -39,6 +39,7 @@ EXPORTS = (
     "crdt_vclock_lub_many_sharded", "crdt_gcounter_lub_many_sharded", "crdt_pncounter_lub_many_sharded",
     "crdt_gset_lub_many_sharded", "crdt_orswot_lub_many_sharded",
     "crdt_orswot_forget_batch", "crdt_map_forget_batch", "crdt_map_apply_batch",
+    "crdt_orswot_merge_batch", "crdt_map_merge_batch",
 )
 
 
@@ -103,6 +104,10 @@ class MapOps(ctypes.Structure):  # crdt_map_ops
                 ("n_keys", S)]
 
 
+class MapDeferred(ctypes.Structure):  # crdt_map_deferred
+    _fields_ = [("clock", P), ("keys", P), ("count", P), ("Dcap", S)]
+
+
 class MapBatch(ctypes.Structure):  # crdt_map_batch
     _fields_ = [
         ("G", S), ("R", S), ("K", S), ("A", S), ("V", S),
@@ -154,6 +159,9 @@ _SIGS.update({
     "crdt_orswot_forget_batch": ([P, P, S, P, S, S, S, S, S, P, S, P, P, S, P], ctypes.c_int),
     "crdt_map_forget_batch": ([P, ctypes.POINTER(MapStates), P, S, P, P, S, P], ctypes.c_int),
     "crdt_map_apply_batch": ([P, ctypes.POINTER(MapStates), P, P, P, S, ctypes.POINTER(MapOps), P], ctypes.c_int),
+    "crdt_orswot_merge_batch": ([P, ctypes.POINTER(OrswotStates), ctypes.POINTER(OrswotStates), P], ctypes.c_int),
+    "crdt_map_merge_batch": ([P, ctypes.POINTER(MapStates), ctypes.POINTER(MapDeferred), ctypes.POINTER(MapStates),
+                              ctypes.POINTER(MapDeferred), P], ctypes.c_int),
     "crdt_comm_unique_id": ([P], ctypes.c_int),
     "crdt_ctx_comm_init": ([P, P, ctypes.c_int, ctypes.c_int], ctypes.c_int),
     "crdt_ctx_comm_destroy": ([P], ctypes.c_int),

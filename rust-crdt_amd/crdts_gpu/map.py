@@ -323,3 +323,62 @@ def apply_batch(clock: torch.Tensor, ec: torch.Tensor, vclk: torch.Tensor, vval:
     ctx.call("crdt_map_apply_batch", ctypes.byref(st), def_clock.data_ptr(), def_keys.data_ptr(),
              def_count.data_ptr(), Dcap, ctypes.byref(o), status.data_ptr())
     return status
+
+
+# ---------------------------------------------------------------------------------------------
+# Pairwise in-place merge_batch: self[i].merge(other[i]) (map.rs:140-220)
+# ---------------------------------------------------------------------------------------------
+class MapStates(NamedTuple):
+    """N Map<K, MVReg<u64>> states: the apply_batch layout plus deferred slots."""
+    clock: torch.Tensor      # (N, A)
+    ec: torch.Tensor         # (N, K, A)
+    vclk: torch.Tensor       # (N, K, V, A)
+    vval: torch.Tensor       # (N, K, V)
+    def_clock: torch.Tensor  # (N, Dcap, A)
+    def_keys: torch.Tensor   # (N, Dcap, ceil(K/64))
+    def_count: torch.Tensor  # (N,) int32
+
+
+def _map_states_structs(ctx: Context, st: MapStates, what: str):
+    for t, nm in zip(st, st._fields):
+        if nm != "def_count":
+            ctx.check_tensor(t, f"{what}({nm})")
+    N, A = st.clock.shape
+    K, V = st.ec.shape[1], st.vclk.shape[2]
+    Kw = (K + 63) // 64
+    Dcap = st.def_clock.shape[1]
+    if (tuple(st.ec.shape) != (N, K, A) or tuple(st.vclk.shape) != (N, K, V, A) or tuple(st.vval.shape) != (N, K, V)
+            or st.clock.stride(1) != 1 or st.ec.stride(2) != 1 or st.ec.stride(1) != A or st.vclk.stride(3) != 1
+            or st.vclk.stride(2) != A or st.vclk.stride(1) != V * A or st.vval.stride(2) != 1 or st.vval.stride(1) != V):
+        raise ValueError(f"{what}: per-state blocks must be packed (K, A) / (K, V, A) / (K, V)")
+    if (tuple(st.def_clock.shape) != (N, Dcap, A) or tuple(st.def_keys.shape) != (N, Dcap, Kw)
+            or not st.def_clock.is_contiguous() or not st.def_keys.is_contiguous()):
+        raise ValueError(f"{what}: def_clock / def_keys must be contiguous (N, Dcap, A) / (N, Dcap, Kw)")
+    if (st.def_count.dtype not in (torch.int32, torch.uint32) or tuple(st.def_count.shape) != (N,)
+            or st.def_count.device != st.clock.device):
+        raise ValueError(f"{what}: def_count must be an (N,) int32 tensor on the states' device")
+    s = _abi.MapStates()
+    s.N, s.K, s.A, s.V = N, K, A, V
+    s.clock, s.clock_stride = st.clock.data_ptr(), st.clock.stride(0)
+    s.ec, s.ec_stride = st.ec.data_ptr(), st.ec.stride(0)
+    s.vclk, s.vclk_stride = st.vclk.data_ptr(), st.vclk.stride(0)
+    s.vval, s.vval_stride = st.vval.data_ptr(), st.vval.stride(0)
+    d = _abi.MapDeferred()
+    d.clock, d.keys, d.count, d.Dcap = st.def_clock.data_ptr(), st.def_keys.data_ptr(), st.def_count.data_ptr(), Dcap
+    return s, d
+
+
+def merge_batch(self_states: MapStates, other: MapStates, ctx: Optional[Context] = None) -> torch.Tensor:
+    """self[i].merge(other[i]) for every i, in place on `self_states` (Map::merge map.rs:140-220 with
+    MVReg::merge mvreg.rs:112-128), exact for any pair of states.  Returns status (N,) int32:
+    bit 0 = deferred slots exhausted, bit 2 = invalid def_count, bit 4 = a register needed more
+    than self's V value slots."""
+    ctx = ctx or Context.default(self_states.clock.device.index)
+    a, ad = _map_states_structs(ctx, self_states, "map.merge_batch(self)")
+    b, bd = _map_states_structs(ctx, other, "map.merge_batch(other)")
+    if (a.N, a.K, a.A) != (b.N, b.K, b.A):
+        raise ValueError("map.merge_batch: self and other differ in N, K or A")
+    status = torch.empty(a.N, dtype=torch.int32, device=self_states.clock.device)
+    ctx.call("crdt_map_merge_batch", ctypes.byref(a), ctypes.byref(ad), ctypes.byref(b), ctypes.byref(bd),
+             status.data_ptr())
+    return status

@@ -284,3 +284,55 @@ def forget_batch(clock: torch.Tensor, entries: torch.Tensor, y: torch.Tensor, de
     ctx.call("crdt_orswot_forget_batch", clock.data_ptr(), clock.stride(0), entries.data_ptr(), entries.stride(1),
              entries.stride(0), N, M, A, y.data_ptr(), ys, dp, sp, D, keep.data_ptr() if keep is not None else None)
     return keep
+
+
+# ---------------------------------------------------------------------------------------------
+# Pairwise in-place merge_batch: self[i].merge(other[i]) (orswot.rs:81-149)
+# ---------------------------------------------------------------------------------------------
+class OrswotStates(NamedTuple):
+    """N Orswot states in the per-state layout of apply_batch / merge_batch."""
+    clock: torch.Tensor        # (N, A)
+    entries: torch.Tensor      # (N, M, A)
+    def_clock: torch.Tensor    # (N, Dcap, A)
+    def_members: torch.Tensor  # (N, Dcap, ceil(M/64))
+    def_count: torch.Tensor    # (N,) int32
+
+
+def _states_struct(ctx: Context, st: OrswotStates, what: str) -> "_abi.OrswotStates":
+    for t, nm in ((st.clock, "clock"), (st.entries, "entries"), (st.def_clock, "def_clock"),
+                  (st.def_members, "def_members")):
+        ctx.check_tensor(t, f"{what}({nm})")
+    if st.clock.dim() != 2 or st.entries.dim() != 3 or st.def_clock.dim() != 3 or st.def_members.dim() != 3:
+        raise ValueError(f"{what}: clock (N,A), entries (N,M,A), def_clock (N,Dcap,A), def_members (N,Dcap,Mw)")
+    N, A = st.clock.shape
+    M = st.entries.shape[1]
+    Dcap = st.def_clock.shape[1]
+    if (st.entries.shape[0] != N or st.entries.shape[2] != A or st.clock.stride(1) != 1 or st.entries.stride(2) != 1
+            or st.entries.stride(0) < M * st.entries.stride(1)):
+        raise ValueError(f"{what}: entries {tuple(st.entries.shape)} / clock {tuple(st.clock.shape)} mismatch")
+    if (tuple(st.def_clock.shape) != (N, Dcap, A) or tuple(st.def_members.shape) != (N, Dcap, (M + 63) // 64)
+            or not st.def_clock.is_contiguous() or not st.def_members.is_contiguous()):
+        raise ValueError(f"{what}: def_clock / def_members must be contiguous (N, Dcap, A) / (N, Dcap, Mw)")
+    if (st.def_count.dtype not in (torch.int32, torch.uint32) or tuple(st.def_count.shape) != (N,)
+            or st.def_count.device != st.clock.device):
+        raise ValueError(f"{what}: def_count must be an (N,) int32 tensor on the states' device")
+    s = _abi.OrswotStates()
+    s.N, s.M, s.A, s.Dcap = N, M, A, Dcap
+    s.clock, s.clock_stride = st.clock.data_ptr(), st.clock.stride(0)
+    s.entries, s.entry_mstride, s.entry_sstride = st.entries.data_ptr(), st.entries.stride(1), st.entries.stride(0)
+    s.def_clock, s.def_members, s.def_count = st.def_clock.data_ptr(), st.def_members.data_ptr(), st.def_count.data_ptr()
+    return s
+
+
+def merge_batch(self_states: OrswotStates, other: OrswotStates, ctx: Optional[Context] = None) -> torch.Tensor:
+    """self[i].merge(other[i]) for every i, in place on `self_states` (CvRDT::merge, traits.rs:4-7 ->
+    Orswot::merge, orswot.rs:81-149), exact for any pair of states.  Returns status (N,) int32:
+    bit 0 = more surviving deferred removes than self's Dcap slots, bit 2 = invalid def_count."""
+    ctx = ctx or Context.default(self_states.clock.device.index)
+    a = _states_struct(ctx, self_states, "orswot.merge_batch(self)")
+    b = _states_struct(ctx, other, "orswot.merge_batch(other)")
+    if (a.N, a.M, a.A) != (b.N, b.M, b.A):
+        raise ValueError("orswot.merge_batch: self and other differ in N, M or A")
+    status = torch.empty(a.N, dtype=torch.int32, device=self_states.clock.device)
+    ctx.call("crdt_orswot_merge_batch", ctypes.byref(a), ctypes.byref(b), dptr(status))
+    return status

@@ -1,0 +1,585 @@
+// Pairwise in-place merge_batch for the causal types: N independent `self[i].merge(other[i])`
+// (CvRDT::merge, traits.rs:4-7) on the per-state layouts of the apply entry points
+// (crdt_orswot_states / crdt_map_states + deferred slots), exact for ANY pair of states.
+//
+// Orswot::merge (orswot.rs:81-149).  Per member m, actor a, with e1/e2 the entry cells and c1/c2
+// the clocks BEFORE the merge, the entry phase (:84-138) is the per-cell dot-store join
+//   e = max(e1 == e2 ? e1 : 0, e1 > c2 ? e1 : 0, e2 > c1 ? e2 : 0)
+// (intersection ∪ clone_without ∪ clone_without, and forget / drop-if-dominated for one-sided
+// members; an all-zero row is an absent member, so it is exact without any invariant).  Then
+// other.deferred is applied (apply_rm :141-143), the clocks merge (:145) and apply_deferred (:147)
+// re-applies self.deferred (its old removes plus other's that were deferred).  Successive forgets
+// of one entry compose to one forget by their max, and re-applying is idempotent, so the entry
+// result is: join, then forget by the ceiling Rc[m] = max of the rm clocks of EVERY deferred
+// remove of either side that names m.  A remove survives iff !(rm <= merged clock) (:240-249);
+// survivors with an identical clock merge their member sets (the HashMap<VClock, HashSet<M>>).
+//
+// Map<K, MVReg<u64>>::merge (map.rs:140-220) has the same skeleton per key (entry clock join with
+// the reset-remove value forgets of :146-208, MVReg::merge mvreg.rs:112-128 for keys on both
+// sides, then every deferred remove naming the key forgets the entry and its values,
+// apply_keyset_rm :318-348).  Keys are independent given the two clocks and the two deferred
+// lists: one wave per (pair, key), lane = actor.
+//
+// Kernels: *_pair_join (entries / keys, bandwidth-bound: read self, read other, write self),
+// then pair_deferred_kernel (one wave per pair: merged clock, surviving removes compacted into
+// self's slots).  The second launch runs after the first on the ctx stream, so the join reads
+// the pre-merge clock and deferred lists of self.
+#include "common.hpp"
+
+namespace crdt {
+
+__device__ __forceinline__ void pfence() { __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup"); }
+__device__ __forceinline__ bool pany(bool x) { return __ballot(x) != 0; }
+
+// ---- shared: surviving deferred removes of a pair ------------------------------------------------
+struct PairDefPlan {
+  unsigned long long N, A, BW;  // BW: bitmap words per remove (members / keys)
+  u64 *c1;                      // self clock rows (written: merged clock)
+  unsigned long long c1_s;
+  const u64 *c2;
+  unsigned long long c2_s;
+  u64 *d1c, *d1b;  // self slots [N][D1][A], [N][D1][BW]
+  uint32_t *d1n;
+  unsigned long long D1;
+  const u64 *d2c, *d2b;  // other slots
+  const uint32_t *d2n;
+  unsigned long long D2;
+  uint32_t *status;
+  unsigned status_or;  // bits the join kernel may already have set are OR-ed in (map: bit 4)
+};
+
+// One wave per pair: candidates are self's removes then other's (in slot order).  A candidate
+// survives iff some rm[a] > max(c1[a], c2[a]); a survivor equal to an already kept clock ORs its
+// bitmap into that slot, else it is compacted into self's next slot (never past one not yet read:
+// the write slot is always <= the candidate index).
+__global__ __launch_bounds__(kBlock) void pair_deferred_kernel(PairDefPlan p) {
+  const int lane = threadIdx.x % kWave;
+  const unsigned long long w0 = (blockIdx.x * (unsigned long long)kBlock + threadIdx.x) / kWave;
+  const unsigned long long nw = (unsigned long long)gridDim.x * (kBlock / kWave);
+  for (unsigned long long s = w0; s < p.N; s += nw) {
+    const unsigned n1 = p.d1n[s], n2 = p.d2n ? p.d2n[s] : 0u;
+    if (n1 > p.D1 || n2 > p.D2) {
+      if (lane == 0) p.status[s] = 4u;  // invalid counts: the state was left untouched
+      continue;
+    }
+    u64 *c1 = p.c1 + s * p.c1_s;
+    const u64 *c2 = p.c2 + s * p.c2_s;
+    u64 *sc = p.d1c + s * p.D1 * p.A, *sb = p.d1b + s * p.D1 * p.BW;
+    const u64 *oc = p.d2c ? p.d2c + s * p.D2 * p.A : nullptr, *ob = p.d2b ? p.d2b + s * p.D2 * p.BW : nullptr;
+    unsigned st = (p.status_or && p.status) ? (p.status[s] & p.status_or) : 0u;
+    unsigned nk = 0;
+    for (unsigned j = 0; j < n1 + n2; ++j) {
+      const u64 *rc = j < n1 ? sc + (unsigned long long)j * p.A : oc + (unsigned long long)(j - n1) * p.A;
+      const u64 *rb = j < n1 ? sb + (unsigned long long)j * p.BW : ob + (unsigned long long)(j - n1) * p.BW;
+      bool gt = false;
+      for (unsigned long long a = lane; a < p.A; a += kWave) {
+        const u64 x = c1[a], y = c2[a];
+        gt |= rc[a] > (x > y ? x : y);
+      }
+      if (!pany(gt)) continue;  // rm <= merged clock: seen, dropped
+      int slot = -1;
+      for (unsigned t = 0; t < nk; ++t) {
+        bool ne = false;
+        for (unsigned long long a = lane; a < p.A; a += kWave) ne |= sc[(unsigned long long)t * p.A + a] != rc[a];
+        if (!pany(ne)) {
+          slot = (int)t;
+          break;
+        }
+      }
+      if (slot >= 0) {  // identical clock: union of the member / key sets
+        for (unsigned long long w = lane; w < p.BW; w += kWave) sb[(unsigned long long)slot * p.BW + w] |= rb[w];
+        pfence();
+        continue;
+      }
+      if (nk >= p.D1) {
+        st |= 1u;  // more survivors than self's slots: the state is incomplete
+        continue;
+      }
+      if (!(j < n1 && j == nk)) {
+        for (unsigned long long a = lane; a < p.A; a += kWave) sc[(unsigned long long)nk * p.A + a] = rc[a];
+        for (unsigned long long w = lane; w < p.BW; w += kWave) sb[(unsigned long long)nk * p.BW + w] = rb[w];
+      }
+      pfence();
+      ++nk;
+    }
+    // merged clock (:145) last: the survival tests above read the pre-merge c1
+    for (unsigned long long a = lane; a < p.A; a += kWave) {
+      const u64 x = c1[a], y = c2[a];
+      c1[a] = x > y ? x : y;
+    }
+    if (lane == 0) {
+      p.d1n[s] = nk;
+      p.status[s] = st;
+    }
+    pfence();
+  }
+}
+
+// ---- Orswot entry join --------------------------------------------------------------------------
+constexpr int kPairGroups = 16;  // deferred removes per pair handled: 32 * kPairGroups
+constexpr int kPairRows = 64;    // member rows per workgroup
+
+struct OrswotPairPlan {
+  u64 *e1;
+  unsigned long long e1_m, e1_s;
+  const u64 *e2;
+  unsigned long long e2_m, e2_s;
+  const u64 *c1;
+  unsigned long long c1_s;
+  const u64 *c2;
+  unsigned long long c2_s;
+  const u64 *d1c, *d1b;
+  const uint32_t *d1n;
+  unsigned long long D1;
+  const u64 *d2c, *d2b;
+  const uint32_t *d2n;
+  unsigned long long D2;
+  unsigned long long N, M, A, Mw, mblocks;
+  int lp_log;  // log2 lanes per member row (pieces of V words)
+};
+
+__device__ __forceinline__ u64 cell_join(u64 e1, u64 e2, u64 c1, u64 c2) {  // orswot.rs:84-138
+  const u64 t0 = e1 == e2 ? e1 : 0ull;
+  const u64 t1 = e1 > c2 ? e1 : 0ull;
+  const u64 t2 = e2 > c1 ? e2 : 0ull;
+  const u64 t = t0 > t1 ? t0 : t1;
+  return t > t2 ? t : t2;
+}
+
+// Workgroup = (pair s, block of kPairRows member rows); 2^lp_log lanes cover a row in V-word
+// pieces (V = 2: 16-byte non-temporal accesses), 256 >> lp_log rows per pass.  Per block the
+// deferred removes of both sides are turned into hit masks in LDS (bit d of hit[g][row] = remove
+// 32g + d names that member); a cell with hits forgets by each hit remove's rm (global, L2).
+template <int V>
+__global__ __launch_bounds__(kBlock) void orswot_pair_join_kernel(OrswotPairPlan p) {
+  __shared__ unsigned hit[kPairGroups][kPairRows];
+  const unsigned long long s = blockIdx.x / p.mblocks;
+  const unsigned long long m0 = (blockIdx.x % p.mblocks) * kPairRows;
+  const unsigned n1 = p.d1n[s], n2 = p.d2n ? p.d2n[s] : 0u;
+  if (n1 > p.D1 || n2 > p.D2) return;  // reported by pair_deferred_kernel, state untouched
+  const unsigned nd = n1 + n2;
+  const unsigned ng = (nd + 31) / 32;
+  for (unsigned i = threadIdx.x; i < ng * kPairRows; i += kBlock) {
+    const unsigned g = i / kPairRows, r = i % kPairRows;
+    const unsigned long long m = m0 + r;
+    unsigned mask = 0;
+    if (m < p.M) {
+      for (unsigned d = g * 32; d < nd && d < g * 32 + 32; ++d) {
+        const u64 *b = d < n1 ? p.d1b + (s * p.D1 + d) * p.Mw : p.d2b + (s * p.D2 + (d - n1)) * p.Mw;
+        if ((b[m / 64] >> (m % 64)) & 1ull) mask |= 1u << (d - g * 32);
+      }
+    }
+    hit[g][r] = mask;
+  }
+  __syncthreads();
+  const int lpr = 1 << p.lp_log;
+  const int piece = threadIdx.x & (lpr - 1);
+  const int rows_per_pass = kBlock >> p.lp_log;
+  const unsigned long long W = (p.A + V - 1) / V;  // pieces per row
+  const u64 *c1 = p.c1 + s * p.c1_s, *c2 = p.c2 + s * p.c2_s;
+  for (unsigned long long pc = piece; pc < W; pc += lpr) {
+    const unsigned long long a0 = pc * V;
+    u64 k1[V], k2[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      k1[v] = a0 + v < p.A ? c1[a0 + v] : 0ull;
+      k2[v] = a0 + v < p.A ? c2[a0 + v] : 0ull;
+    }
+    for (int r = threadIdx.x >> p.lp_log; r < kPairRows; r += rows_per_pass) {
+      const unsigned long long m = m0 + r;
+      if (m >= p.M) break;
+      u64 *pe1 = p.e1 + s * p.e1_s + m * p.e1_m + a0;
+      const u64 *pe2 = p.e2 + s * p.e2_s + m * p.e2_m + a0;
+      u64 x[V], y[V];
+      if constexpr (V == 2) {
+        const u64x2 a = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(pe1));
+        const u64x2 b = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(pe2));
+        x[0] = a.x, x[1] = a.y, y[0] = b.x, y[1] = b.y;
+      } else {
+        x[0] = __builtin_nontemporal_load(pe1);
+        y[0] = __builtin_nontemporal_load(pe2);
+      }
+#pragma unroll
+      for (int v = 0; v < V; ++v) x[v] = cell_join(x[v], y[v], k1[v], k2[v]);
+      for (unsigned g = 0; g < ng; ++g) {
+        unsigned mask = hit[g][r];
+        while (mask) {
+          const unsigned d = g * 32 + __builtin_ctz(mask);
+          mask &= mask - 1;
+          const u64 *rm = d < n1 ? p.d1c + (s * p.D1 + d) * p.A : p.d2c + (s * p.D2 + (d - n1)) * p.A;
+#pragma unroll
+          for (int v = 0; v < V; ++v)
+            if (a0 + v < p.A && x[v] <= rm[a0 + v]) x[v] = 0;  // VClock::forget, vclock.rs:95-105
+        }
+      }
+      if constexpr (V == 2) {
+        u64x2 o;
+        o.x = x[0];
+        o.y = x[1];
+        __builtin_nontemporal_store(o, reinterpret_cast<u64x2 *>(pe1));
+      } else {
+        __builtin_nontemporal_store(x[0], pe1);
+      }
+    }
+  }
+}
+
+// ---- Map<K, MVReg> key merge --------------------------------------------------------------------
+constexpr int kMapPairMaxV = 8;
+
+struct MapPairPlan {
+  unsigned long long N, K, A, V1, V2, Kw;
+  const u64 *c1;
+  unsigned long long c1_s;
+  const u64 *c2;
+  unsigned long long c2_s;
+  u64 *ec1, *vc1, *vv1;
+  unsigned long long ec1_s, vc1_s, vv1_s;
+  const u64 *ec2, *vc2, *vv2;
+  unsigned long long ec2_s, vc2_s, vv2_s;
+  const u64 *d1c, *d1k;
+  const uint32_t *d1n;
+  unsigned long long D1;
+  const u64 *d2c, *d2k;
+  const uint32_t *d2n;
+  unsigned long long D2;
+  uint32_t *status;  // bit 4 = a register needed more than V1 slots (set with atomicOr)
+};
+
+template <int APL>
+struct PRow {
+  u64 w[APL];
+};
+template <int APL>
+__device__ __forceinline__ PRow<APL> prow(const u64 *p, int lane, unsigned long long A) {
+  PRow<APL> r;
+#pragma unroll
+  for (int j = 0; j < APL; ++j) {
+    const unsigned long long a = lane + j * kWave;
+    r.w[j] = a < A ? p[a] : 0ull;
+  }
+  return r;
+}
+template <int APL>
+__device__ __forceinline__ void pstore(u64 *p, const PRow<APL> &r, int lane, unsigned long long A) {
+#pragma unroll
+  for (int j = 0; j < APL; ++j) {
+    const unsigned long long a = lane + j * kWave;
+    if (a < A) p[a] = r.w[j];
+  }
+}
+template <int APL>
+__device__ __forceinline__ bool pnz(const PRow<APL> &r) {
+  bool b = false;
+#pragma unroll
+  for (int j = 0; j < APL; ++j) b |= r.w[j] != 0;
+  return pany(b);
+}
+template <int APL>
+__device__ __forceinline__ bool ple(const PRow<APL> &x, const PRow<APL> &y) {  // x <= y everywhere
+  bool b = false;
+#pragma unroll
+  for (int j = 0; j < APL; ++j) b |= x.w[j] > y.w[j];
+  return !pany(b);
+}
+template <int APL>
+__device__ __forceinline__ bool peq(const PRow<APL> &x, const PRow<APL> &y) {
+  bool b = false;
+#pragma unroll
+  for (int j = 0; j < APL; ++j) b |= x.w[j] != y.w[j];
+  return !pany(b);
+}
+// partial_cmp == Less (vclock.rs:68-80): x <= y and x != y
+template <int APL>
+__device__ __forceinline__ bool plt(const PRow<APL> &x, const PRow<APL> &y) {
+  return ple(x, y) && !peq(x, y);
+}
+template <int APL>
+__device__ __forceinline__ PRow<APL> pforget(const PRow<APL> &x, const PRow<APL> &y) {  // keep x iff x > y
+  PRow<APL> r;
+#pragma unroll
+  for (int j = 0; j < APL; ++j) r.w[j] = x.w[j] > y.w[j] ? x.w[j] : 0ull;
+  return r;
+}
+template <int APL>
+__device__ __forceinline__ PRow<APL> pmax(const PRow<APL> &x, const PRow<APL> &y) {
+  PRow<APL> r;
+#pragma unroll
+  for (int j = 0; j < APL; ++j) r.w[j] = x.w[j] > y.w[j] ? x.w[j] : y.w[j];
+  return r;
+}
+__device__ __forceinline__ u64 prl64(u64 x, int l) {
+  const unsigned lo = __builtin_amdgcn_readlane((int)(unsigned)x, l);
+  const unsigned hi = __builtin_amdgcn_readlane((int)(unsigned)(x >> 32), l);
+  return ((u64)hi << 32) | lo;
+}
+
+// One wave per (pair, key); APL clock words per lane (A <= 64 * APL).
+template <int APL>
+__global__ __launch_bounds__(kBlock) void map_pair_join_kernel(MapPairPlan p) {
+  const int lane = threadIdx.x % kWave;
+  const unsigned long long w0 = (blockIdx.x * (unsigned long long)kBlock + threadIdx.x) / kWave;
+  const unsigned long long nw = (unsigned long long)gridDim.x * (kBlock / kWave);
+  const unsigned long long A = p.A;
+  for (unsigned long long it = w0; it < p.N * p.K; it += nw) {
+    const unsigned long long s = it / p.K, k = it % p.K;
+    const unsigned n1 = p.d1n[s], n2 = p.d2n ? p.d2n[s] : 0u;
+    if (n1 > p.D1 || n2 > p.D2) continue;  // reported by pair_deferred_kernel
+    u64 *ec1 = p.ec1 + s * p.ec1_s + k * A;
+    u64 *vc1 = p.vc1 + s * p.vc1_s + k * p.V1 * A;
+    u64 *vv1 = p.vv1 + s * p.vv1_s + k * p.V1;
+    const u64 *ec2 = p.ec2 + s * p.ec2_s + k * A;
+    const u64 *vc2 = p.vc2 + s * p.vc2_s + k * p.V2 * A;
+    const u64 *vv2 = p.vv2 + s * p.vv2_s + k * p.V2;
+    const PRow<APL> e1 = prow<APL>(ec1, lane, A), e2 = prow<APL>(ec2, lane, A);
+    const bool p1 = pnz(e1), p2 = pnz(e2);
+    if (!p1 && !p2) continue;  // no entry on either side: nothing to merge
+    const PRow<APL> c1 = prow<APL>(p.c1 + s * p.c1_s, lane, A), c2 = prow<APL>(p.c2 + s * p.c2_s, lane, A);
+    // occupied value slots (Vec order = slot order, empty slot <=> zero clock)
+    unsigned m1 = 0, m2 = 0;
+    for (unsigned q = 0; q < p.V1; ++q)
+      if (pnz(prow<APL>(vc1 + q * A, lane, A))) m1 |= 1u << q;
+    for (unsigned q = 0; q < p.V2; ++q)
+      if (pnz(prow<APL>(vc2 + q * A, lane, A))) m2 |= 1u << q;
+    bool present = true;
+    PRow<APL> e, X;  // resulting entry clock, forget clock of the values
+    unsigned keep1 = 0, add2 = 0;
+    if (p1 && !p2) {  // :146-161
+      if (ple(e1, c2)) {
+        present = false;
+      } else {
+        e = pforget(e1, c2);
+        X = pforget(c2, e);  // removed_information = other.clock.forget(entry.clock)
+        keep1 = m1;
+      }
+    } else if (!p1 && p2) {  // :193-208
+      if (ple(e2, c1)) {
+        present = false;
+      } else {
+        e = pforget(e2, c1);
+        X = pforget(c1, e);  // information_we_deleted
+        add2 = m2;
+      }
+    } else {  // :170-192
+      PRow<APL> common;
+#pragma unroll
+      for (int j = 0; j < APL; ++j) {
+        const u64 a = e1.w[j], b = e2.w[j];
+        const u64 t0 = a == b ? a : 0ull, t1 = b > c1.w[j] ? b : 0ull, t2 = a > c2.w[j] ? a : 0ull;
+        const u64 t = t0 > t1 ? t0 : t1;
+        common.w[j] = t > t2 ? t : t2;
+      }
+      if (!pnz(common)) {
+        present = false;
+      } else {
+        // MVReg::merge (mvreg.rs:112-128): own values not strictly below one of other's, then
+        // other's not strictly below a kept own value and not equal to one
+        for (unsigned q = 0; q < p.V1; ++q) {
+          if (!((m1 >> q) & 1u)) continue;
+          const PRow<APL> x = prow<APL>(vc1 + q * A, lane, A);
+          bool dom = false;
+          for (unsigned r = 0; r < p.V2 && !dom; ++r)
+            if ((m2 >> r) & 1u) dom = plt(x, prow<APL>(vc2 + r * A, lane, A));
+          if (!dom) keep1 |= 1u << q;
+        }
+        for (unsigned r = 0; r < p.V2; ++r) {
+          if (!((m2 >> r) & 1u)) continue;
+          const PRow<APL> y = prow<APL>(vc2 + r * A, lane, A);
+          bool drop = false;
+          for (unsigned q = 0; q < p.V1 && !drop; ++q)
+            if ((keep1 >> q) & 1u) {
+              const PRow<APL> x = prow<APL>(vc1 + q * A, lane, A);
+              drop = plt(y, x) || peq(y, x);
+            }
+          if (!drop) add2 |= 1u << r;
+        }
+        X = pforget(pmax(e1, e2), common);  // information_that_was_deleted
+        e = common;
+      }
+    }
+    // every deferred remove of either side naming k (apply_keyset_rm :318-333, composed by max)
+    PRow<APL> Rk;
+#pragma unroll
+    for (int j = 0; j < APL; ++j) Rk.w[j] = 0;
+    bool hasR = false;
+    if (present) {
+      for (unsigned d = 0; d < n1 + n2; ++d) {
+        const u64 *kb = d < n1 ? p.d1k + (s * p.D1 + d) * p.Kw : p.d2k + (s * p.D2 + (d - n1)) * p.Kw;
+        if (!((kb[k / 64] >> (k % 64)) & 1ull)) continue;
+        const u64 *rc = d < n1 ? p.d1c + (s * p.D1 + d) * A : p.d2c + (s * p.D2 + (d - n1)) * A;
+        Rk = pmax(Rk, prow<APL>(rc, lane, A));
+        hasR = true;
+      }
+      if (hasR) {
+        e = pforget(e, Rk);
+        if (!pnz(e)) present = false;
+      }
+    }
+    // the values' u64 payloads, read before any slot is written (lane q holds slot q)
+    const u64 v1l = (unsigned long long)lane < p.V1 ? vv1[lane] : 0ull;
+    const u64 v2l = (unsigned long long)lane < p.V2 ? vv2[lane] : 0ull;
+    unsigned w = 0;
+    if (present) {
+      pstore(ec1, e, lane, A);
+      // own kept values first (slot order), then other's added ones: the Vec order of :113-127.
+      // Writing slot w never clobbers an unread own slot (w <= the slot being read).
+      for (unsigned q = 0; q < p.V1; ++q) {
+        if (!((keep1 >> q) & 1u)) continue;
+        PRow<APL> x = pforget(prow<APL>(vc1 + q * A, lane, A), X);  // MVReg::forget mvreg.rs:88-104
+        if (hasR) x = pforget(x, Rk);
+        if (!pnz(x)) continue;
+        const u64 val = prl64(v1l, (int)q);
+        if (w < p.V1) {
+          pstore(vc1 + (unsigned long long)w * A, x, lane, A);
+          if (lane == 0) vv1[w] = val;
+        }
+        ++w;
+      }
+      for (unsigned r = 0; r < p.V2; ++r) {
+        if (!((add2 >> r) & 1u)) continue;
+        PRow<APL> y = pforget(prow<APL>(vc2 + r * A, lane, A), X);
+        if (hasR) y = pforget(y, Rk);
+        if (!pnz(y)) continue;
+        const u64 val = prl64(v2l, (int)r);
+        if (w < p.V1) {
+          pstore(vc1 + (unsigned long long)w * A, y, lane, A);
+          if (lane == 0) vv1[w] = val;
+        }
+        ++w;
+      }
+      if (w > p.V1 && lane == 0) atomicOr(p.status + s, 16u);
+    } else {
+      PRow<APL> z;
+#pragma unroll
+      for (int j = 0; j < APL; ++j) z.w[j] = 0;
+      pstore(ec1, z, lane, A);
+    }
+    for (unsigned q = w; q < p.V1; ++q) {  // clear the slots past the last written value
+      PRow<APL> z;
+#pragma unroll
+      for (int j = 0; j < APL; ++j) z.w[j] = 0;
+      pstore(vc1 + (unsigned long long)q * A, z, lane, A);
+      if (lane == 0) vv1[q] = 0;
+    }
+  }
+}
+
+static unsigned pair_grid(crdt_ctx *ctx, unsigned long long waves, int per_cu) {
+  const unsigned long long want = (waves + (kBlock / kWave) - 1) / (kBlock / kWave);
+  const unsigned long long cap = (unsigned long long)ctx->cu_count * per_cu;
+  return (unsigned)(want < cap ? (want ? want : 1) : cap);
+}
+
+static bool al16p(const void *p) { return ((uintptr_t)p & 15) == 0; }
+
+static int launch_pair_deferred(crdt_ctx *ctx, PairDefPlan q) {
+  hipLaunchKernelGGL(pair_deferred_kernel, dim3(pair_grid(ctx, q.N, 8)), dim3(kBlock), 0, ctx->stream, q);
+  CRDT_HIP(ctx, hipGetLastError());
+  return CRDT_OK;
+}
+
+}  // namespace crdt
+
+using namespace crdt;
+
+extern "C" int crdt_orswot_merge_batch(crdt_ctx *ctx, const crdt_orswot_states *self, const crdt_orswot_states *other,
+                                       uint32_t *status) {
+  CRDT_CHECK_CTX(ctx);
+  if (!self || !other || !status) return fail(ctx, CRDT_EINVAL, "orswot_merge_batch: NULL argument");
+  const crdt_orswot_states &a = *self, &b = *other;
+  if (a.N != b.N || a.M != b.M || a.A != b.A)
+    return fail(ctx, CRDT_EINVAL, "orswot_merge_batch: self and other differ in N, M or A");
+  const size_t N = a.N, M = a.M, A = a.A;
+  if (N == 0) return CRDT_OK;
+  if (A == 0) return fail(ctx, CRDT_EINVAL, "orswot_merge_batch: A = 0");
+  if (!a.clock || !b.clock || !a.def_count || (M && (!a.entries || !b.entries)))
+    return fail(ctx, CRDT_EINVAL, "orswot_merge_batch: NULL buffer");
+  if ((a.Dcap && (!a.def_clock || !a.def_members)) || (b.Dcap && (!b.def_clock || !b.def_members || !b.def_count)))
+    return fail(ctx, CRDT_EINVAL, "orswot_merge_batch: deferred capacity without deferred buffers");
+  if (a.clock_stride < A || b.clock_stride < A ||
+      (M && (a.entry_mstride < A || b.entry_mstride < A || a.entry_sstride < M * a.entry_mstride ||
+             b.entry_sstride < M * b.entry_mstride)))
+    return fail(ctx, CRDT_EINVAL, "orswot_merge_batch: strides smaller than the rows they hold");
+  if (a.Dcap + b.Dcap > (size_t)(32 * kPairGroups))
+    return fail(ctx, CRDT_EUNSUPPORTED, "orswot_merge_batch: Dcap(self) + Dcap(other) = %zu > %d", a.Dcap + b.Dcap,
+                32 * kPairGroups);
+  const size_t Mw = (M + 63) / 64;
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  if (M) {
+    const bool v2 = A % 2 == 0 && a.entry_mstride % 2 == 0 && b.entry_mstride % 2 == 0 && a.entry_sstride % 2 == 0 &&
+                    b.entry_sstride % 2 == 0 && al16p(a.entries) && al16p(b.entries);
+    const unsigned long long W = v2 ? A / 2 : A;
+    int lp = 0;
+    while (lp < 6 && (1ull << lp) < W) ++lp;
+    const unsigned long long mblocks = (M + kPairRows - 1) / kPairRows;
+    if (N * mblocks > 0x7FFFFFFFull) return fail(ctx, CRDT_EUNSUPPORTED, "orswot_merge_batch: grid too large");
+    OrswotPairPlan p{(u64 *)a.entries, a.entry_mstride, a.entry_sstride, (const u64 *)b.entries, b.entry_mstride,
+                     b.entry_sstride, (const u64 *)a.clock, a.clock_stride, (const u64 *)b.clock, b.clock_stride,
+                     (const u64 *)a.def_clock, (const u64 *)a.def_members, a.def_count, a.Dcap,
+                     (const u64 *)b.def_clock, (const u64 *)b.def_members, b.Dcap ? b.def_count : nullptr, b.Dcap,
+                     N, M, A, Mw, mblocks, lp};
+    timing_begin(ctx, "orswot_pair_join");
+    if (v2)
+      hipLaunchKernelGGL(orswot_pair_join_kernel<2>, dim3((unsigned)(N * mblocks)), dim3(kBlock), 0, ctx->stream, p);
+    else
+      hipLaunchKernelGGL(orswot_pair_join_kernel<1>, dim3((unsigned)(N * mblocks)), dim3(kBlock), 0, ctx->stream, p);
+    timing_end(ctx);
+    CRDT_HIP(ctx, hipGetLastError());
+  }
+  return launch_pair_deferred(ctx, PairDefPlan{N, A, Mw, (u64 *)a.clock, a.clock_stride, (const u64 *)b.clock,
+                                               b.clock_stride, (u64 *)a.def_clock, (u64 *)a.def_members, a.def_count,
+                                               a.Dcap, (const u64 *)b.def_clock, (const u64 *)b.def_members,
+                                               b.Dcap ? b.def_count : nullptr, b.Dcap, status, 0u});
+}
+
+extern "C" int crdt_map_merge_batch(crdt_ctx *ctx, const crdt_map_states *self, const crdt_map_deferred *self_def,
+                                    const crdt_map_states *other, const crdt_map_deferred *other_def,
+                                    uint32_t *status) {
+  CRDT_CHECK_CTX(ctx);
+  if (!self || !other || !self_def || !other_def || !status)
+    return fail(ctx, CRDT_EINVAL, "map_merge_batch: NULL argument");
+  const crdt_map_states &a = *self, &b = *other;
+  if (a.N != b.N || a.K != b.K || a.A != b.A)
+    return fail(ctx, CRDT_EINVAL, "map_merge_batch: self and other differ in N, K or A");
+  const size_t N = a.N, K = a.K, A = a.A;
+  if (N == 0) return CRDT_OK;
+  if (A == 0 || A > 4 * (size_t)kWave || a.V == 0 || a.V > (size_t)kMapPairMaxV || b.V == 0 ||
+      b.V > (size_t)kMapPairMaxV)
+    return fail(ctx, CRDT_EINVAL, "map_merge_batch: need 1 <= A <= 256 and 1 <= V <= %d on both sides", kMapPairMaxV);
+  if (!a.clock || !b.clock || !self_def->count || (K && (!a.ec || !a.vclk || !a.vval || !b.ec || !b.vclk || !b.vval)))
+    return fail(ctx, CRDT_EINVAL, "map_merge_batch: NULL buffer");
+  if ((self_def->Dcap && (!self_def->clock || !self_def->keys)) ||
+      (other_def->Dcap && (!other_def->clock || !other_def->keys || !other_def->count)))
+    return fail(ctx, CRDT_EINVAL, "map_merge_batch: deferred capacity without deferred buffers");
+  if (a.clock_stride < A || b.clock_stride < A || a.ec_stride < K * A || b.ec_stride < K * A ||
+      a.vclk_stride < K * a.V * A || b.vclk_stride < K * b.V * A || a.vval_stride < K * a.V || b.vval_stride < K * b.V)
+    return fail(ctx, CRDT_EINVAL, "map_merge_batch: strides smaller than the rows they hold");
+  const size_t Kw = (K + 63) / 64;
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  // status is written whole by the deferred pass; the key pass only ORs bit 4 into it first
+  CRDT_HIP(ctx, hipMemsetAsync(status, 0, N * sizeof(uint32_t), ctx->stream));
+  if (K) {
+    MapPairPlan p{N, K, A, a.V, b.V, Kw, (const u64 *)a.clock, a.clock_stride, (const u64 *)b.clock, b.clock_stride,
+                  (u64 *)a.ec, (u64 *)a.vclk, (u64 *)a.vval, a.ec_stride, a.vclk_stride, a.vval_stride,
+                  (const u64 *)b.ec, (const u64 *)b.vclk, (const u64 *)b.vval, b.ec_stride, b.vclk_stride,
+                  b.vval_stride, (const u64 *)self_def->clock, (const u64 *)self_def->keys, self_def->count,
+                  self_def->Dcap, (const u64 *)other_def->clock, (const u64 *)other_def->keys,
+                  other_def->Dcap ? other_def->count : nullptr, other_def->Dcap, status};
+    const unsigned grid = pair_grid(ctx, (unsigned long long)N * K, 16);
+    timing_begin(ctx, "map_pair_join");
+    if (A <= (size_t)kWave)
+      hipLaunchKernelGGL(map_pair_join_kernel<1>, dim3(grid), dim3(kBlock), 0, ctx->stream, p);
+    else if (A <= 2 * (size_t)kWave)
+      hipLaunchKernelGGL(map_pair_join_kernel<2>, dim3(grid), dim3(kBlock), 0, ctx->stream, p);
+    else
+      hipLaunchKernelGGL(map_pair_join_kernel<4>, dim3(grid), dim3(kBlock), 0, ctx->stream, p);
+    timing_end(ctx);
+    CRDT_HIP(ctx, hipGetLastError());
+  }
+  return launch_pair_deferred(ctx, PairDefPlan{N, A, Kw, (u64 *)a.clock, a.clock_stride, (const u64 *)b.clock,
+                                               b.clock_stride, (u64 *)self_def->clock, (u64 *)self_def->keys,
+                                               self_def->count, self_def->Dcap, (const u64 *)other_def->clock,
+                                               (const u64 *)other_def->keys,
+                                               other_def->Dcap ? other_def->count : nullptr, other_def->Dcap, status,
+                                               16u});
+}

@@ -1,8 +1,10 @@
 """Replay the reference's known-answer tests with every merge executed by libcrdt_gpu:
-reference-shaped states are interned to the dense layout, merged on the GPU as a 2-replica
-lub_many (acc = new(); acc.merge(self); acc.merge(other) == self.merge(other)), and egressed."""
+reference-shaped states are interned to the dense layout, merged on the GPU and egressed.  Two
+routes per merge: a 2-replica lub_many (acc = new(); acc.merge(self); acc.merge(other)) and the
+in-place pairwise merge_batch (self.merge(other) itself, N = 1)."""
 import numpy as np
 import pytest
+import torch
 
 import kat_runner as K
 import oracle as O
@@ -19,13 +21,23 @@ def _vc_pair(a: O.VClock, b: O.VClock, idx):
     return rows
 
 
-def gpu_merge(dst, src, kind):
+def _pair_merge(mod, rows, mode):
+    """rows (2, W) -> merged row: lub_many of the 2 replicas, or merge_batch of self=row 0."""
+    d = to_dev(rows)
+    if mode == "lub2":
+        return to_host(mod.lub_many(d))
+    me = d[:1].clone()
+    mod.merge_batch(me, d[1:])
+    return to_host(me)[0]
+
+
+def gpu_merge(dst, src, kind, mode="lub2"):
     if kind in ("vclock", "gcounter"):
         da = dst if kind == "vclock" else dst.inner
         sa = src if kind == "vclock" else src.inner
         idx = intern.Index()
         rows = _vc_pair(da, sa, idx)
-        out = to_host(cg.vclock.lub_many(to_dev(rows)))
+        out = _pair_merge(cg.vclock if kind == "vclock" else cg.gcounter, rows, mode)
         da.dots = intern.dense_to_clocks(out[None, :], idx)[0]
         return dst
     if kind == "pncounter":
@@ -33,7 +45,7 @@ def gpu_merge(dst, src, kind):
         p = intern.clocks_to_dense([dst.p.inner.dots, src.p.inner.dots], idx)
         n = intern.clocks_to_dense([dst.n.inner.dots, src.n.inner.dots], idx, width=p.shape[1])
         p = np.pad(p, ((0, 0), (0, n.shape[1] - p.shape[1])))
-        out = to_host(cg.pncounter.lub_many(to_dev(np.concatenate([p, n], axis=1))))
+        out = _pair_merge(cg.pncounter, np.concatenate([p, n], axis=1), mode)
         A = p.shape[1]
         dst.p.inner.dots = intern.dense_to_clocks(out[None, :A], idx)[0]
         dst.n.inner.dots = intern.dense_to_clocks(out[None, A:], idx)[0]
@@ -41,7 +53,7 @@ def gpu_merge(dst, src, kind):
     if kind == "gset":
         idx = intern.Index()
         bm = intern.sets_to_bitmap([dst.value, src.value], idx)
-        out = to_host(cg.gset.lub_many(to_dev(bm)))
+        out = _pair_merge(cg.gset, bm, mode)
         dst.value = intern.bitmap_to_sets(out[None, :], idx)[0]
         return dst
     if kind == "lwwreg":
@@ -55,8 +67,41 @@ def gpu_merge(dst, src, kind):
         dst.marker, dst.val = int(to_host(res.marker)), vals.ids[int(to_host(res.val))]
         return dst
     if kind == "orswot":
-        return gpu_orswot_merge(dst, src)
+        return gpu_orswot_merge(dst, src) if mode == "lub2" else gpu_orswot_merge_batch(dst, src)
     raise TypeError(kind)
+
+
+def gpu_orswot_merge_batch(dst: O.Orswot, src: O.Orswot) -> O.Orswot:
+    """dst.merge(src) as crdt_orswot_merge_batch with N = 1 (in place on dst's dense state)."""
+    from orswot_apply_util import dense_states, to_object
+    actors, members = intern.Index(), intern.Index()
+    for s in (dst, src):
+        for a in s.clock.dots:
+            actors.intern(a)
+        for m, c in s.entries.items():
+            members.intern(m)
+            for a in c.dots:
+                actors.intern(a)
+        for k, ms in s.deferred.items():
+            for a in k.dots:
+                actors.intern(a)
+            for m in ms:
+                members.intern(m)
+    A, M = max(1, len(actors)), max(1, len(members))
+    fa, fm = (lambda a: actors.pos[a]), (lambda m: members.pos[m])
+    from orswot_apply_util import map_orswot
+    Dcap = max(1, len(dst.deferred) + len(src.deferred))
+    sides = []
+    for s in (dst, src):
+        c, e, dc, dm, n = dense_states([map_orswot(s, fa, fm)], M, A, Dcap)
+        sides.append(cg.orswot.OrswotStates(to_dev(c), to_dev(e), to_dev(dc), to_dev(dm),
+                                            torch.from_numpy(n.astype(np.int32)).cuda()))
+    status = cg.orswot.merge_batch(sides[0], sides[1]).cpu().numpy()
+    assert status[0] == 0, status
+    me = sides[0]
+    dense = to_object(to_host(me.clock), to_host(me.entries), to_host(me.def_clock), to_host(me.def_members),
+                      me.def_count.cpu().numpy(), 0)
+    return map_orswot(dense, lambda a: actors.ids[a], lambda m: members.ids[m])
 
 
 def gpu_orswot_merge(dst: O.Orswot, src: O.Orswot) -> O.Orswot:
@@ -118,9 +163,10 @@ CASES = [c for f in ("kat_vclock.json", "kat_counters.json", "kat_orswot.json")
          for c in K.load_cases(f) if any(s[0] in ("merge", "merge_err") for s in c["steps"])]
 
 
+@pytest.mark.parametrize("mode", ["lub2", "merge_batch"])
 @pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
-def test_kat_gpu(gpu_ctx, case):
-    K.run_case(case, merge_hook=gpu_merge)
+def test_kat_gpu(gpu_ctx, case, mode):
+    K.run_case(case, merge_hook=lambda d, s, k: gpu_merge(d, s, k, mode))
 
 
 class GpuCausal:
