@@ -1,13 +1,18 @@
 #!/usr/bin/env python3
-"""Benchmark: batched CvRDT lub (replica-merges/s) on MI355X — BASELINE.json config 2.
+"""Benchmark: batched CvRDT lub (replica-merges/s) on MI355X — BASELINE.json config 2 (default).
 
-One step = the two lubs of config 2 over HBM-resident synthetic replicas:
+--workload c2 (default): one step = the two lubs of config 2 over HBM-resident synthetic replicas:
     GCounter  lub_many of 1,048,576 replicas x 256 actors (u64)       2 GiB read
     PNCounter lub_many of 1,048,576 replicas x (2 x 256) actors (u64)  4 GiB read
-= 2,097,152 replica-merges per rank per step.  With --gpus N (torchrun, one process per GPU)
-every rank holds its own 1M-replica shard of one global input (weak scaling) and the step ends
-with the one real exchange of the path: an unsigned-max all-reduce of the 768-word partial
-lubs over RCCL.  value = replica-merges of all ranks / max-over-ranks wall time.
+= 2,097,152 replica-merges per rank per step.
+--workload c5: one step = one GPU's shard of config 5, VClock lub_many of 1,048,576 replicas x
+1,024 actors (8 GiB read; 8 ranks = the 8M-replica config-5 input).
+With --gpus N (torchrun, one process per GPU) every rank holds its own 1M-replica shard of one
+global input (weak scaling) and each lub of the step is the C ABI's own sharded entry point
+(crdt_{gcounter,pncounter,vclock}_lub_many_sharded: local lub + ONE ncclAllReduce(ncclUint64,
+ncclMax) over the ctx's RCCL communicator, the path a Rust caller without torch.distributed
+takes; torch.distributed only ships the 128-byte unique id and runs the barriers).
+value = replica-merges of all ranks / max-over-ranks wall time.
 
 The JSON line also carries
   roofline      the dominant kernel (lub_stream_kernel, both launches of the step), its
@@ -28,7 +33,7 @@ sys.path.insert(0, os.path.join(ROOT, "rust-crdt_amd"))
 
 R_REPLICAS = 1 << 20
 A_ACTORS = 256
-SEED_G, SEED_P = 0x5EED0002, 0x5EED0003
+SEED_G, SEED_P, SEED_V = 0x5EED0002, 0x5EED0003, 0x5EED0005
 HBM_PEAK_GBS = 8000.0
 
 
@@ -37,10 +42,15 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--replicas", type=int, default=R_REPLICAS, help="replicas per rank (config 2: 1M)")
-    ap.add_argument("--actors", type=int, default=A_ACTORS)
+    ap.add_argument("--workload", choices=("c2", "c5"), default=os.environ.get("CRDT_BENCH_WORKLOAD", "c2"),
+                    help="c2: GCounter+PNCounter 1M x 256 (BASELINE config 2); c5: VClock 1M x 1024 per GPU "
+                         "(one shard of config 5)")
+    ap.add_argument("--replicas", type=int, default=R_REPLICAS, help="replicas per rank (configs 2 and 5: 1M)")
+    ap.add_argument("--actors", type=int, default=None, help="default 256 (c2) / 1024 (c5)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="target fold seconds of the CPU baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--exchange", choices=("cabi", "torch"), default="cabi",
+                    help="N > 1: the C ABI's own RCCL communicator (crdt_*_lub_many_sharded) or torch.distributed")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL on ROCm) for real runs; gloo lets several ranks share one GPU in tests")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
@@ -83,18 +93,37 @@ def cpu_baseline(args):
             reps += 1
         return done_rows / fold_s, reps, fold_s
 
-    v1, reps1, s1 = run(1, 16384, args.cpu_seconds / 2)
-    vT, repsT, sT = run(T, 4096, args.cpu_seconds)
+    def run_c5(threads, per_thread, seconds):
+        done_rows, fold_s, reps = 0, 0.0, 0
+        t_start = time.time()
+        while fold_s < seconds and time.time() - t_start < 4 * seconds:
+            n = per_thread * threads
+            v = O.synth_matrix(SEED_V, n, args.actors, 0, row0=reps * n)
+            _, tv = O.counter_fold_mt(v, False, threads)
+            fold_s += tv
+            done_rows += n
+            reps += 1
+        return done_rows / fold_s, reps, fold_s
+
+    if args.workload == "c5":
+        v1, reps1, s1 = run_c5(1, 4096, args.cpu_seconds / 2)
+        vT, repsT, sT = run_c5(T, 2048, args.cpu_seconds)
+        what = f"{repsT} x {T}x2048 VClock x {args.actors} replicas"
+        one = f"{reps1} x 4096 replicas, {s1:.2f} s of fold"
+    else:
+        v1, reps1, s1 = run(1, 16384, args.cpu_seconds / 2)
+        vT, repsT, sT = run(T, 4096, args.cpu_seconds)
+        what = f"{repsT} x ({T}x4096 GCounter x {args.actors} + {T}x4096 PNCounter x 2x{args.actors}) replicas"
+        one = f"{reps1} x (16384 + 16384) replicas, {s1:.2f} s of fold"
     return {
         "value": vT,
         "unit": "replica-merges/s",
         "cores": T,
         "kind": "port",
-        "sample": (f"{repsT} x ({T}x4096 GCounter x {args.actors} + {T}x4096 PNCounter x 2x{args.actors}) replicas "
-                   f"of the same synthetic input, left fold of the restated VClock::merge over std::map "
-                   f"(oracle/ref_fold.cpp) split over {T} threads + final merge of the partials, map ingest "
-                   f"excluded; {sT:.2f} s of fold"),
-        "single_core": {"value": v1, "cores": 1, "sample": f"{reps1} x (16384 + 16384) replicas, {s1:.2f} s of fold"},
+        "sample": (f"{what} of the same synthetic input, left fold of the restated VClock::merge over std::map "
+                   f"(oracle/ref_fold.cpp) split over {T} threads (this job's CPU share of the GPU box) + final "
+                   f"merge of the partials, map ingest excluded; {sT:.2f} s of fold"),
+        "single_core": {"value": v1, "cores": 1, "sample": one},
     }
 
 
@@ -121,24 +150,34 @@ def main():
             dist.init_process_group(args.dist_backend)
     ctx = cg.Context.default(dev)
 
+    if args.actors is None:
+        args.actors = 1024 if args.workload == "c5" else A_ACTORS
     R, A = args.replicas, args.actors
+    cabi = world > 1 and args.exchange == "cabi"
+    if cabi:  # the C ABI's own communicator; torch.distributed only ships the 128-byte id
+        uid = [cg.shard.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        cg.shard.comm_init(ctx, uid[0], world, rank)
     # Synthetic replicas, generated in HBM; rank k owns rows [k*R, (k+1)*R) of the global input.
-    g_in = torch.empty((R, A), dtype=torch.int64, device="cuda")
-    p_in = torch.empty((R, 2 * A), dtype=torch.int64, device="cuda")
-    cg.synth_fill(ctx, g_in, SEED_G, 0, first_row=rank * R)
-    cg.synth_fill(ctx, p_in, SEED_P, 0, first_row=rank * R)
-    g_out = torch.empty((A,), dtype=torch.int64, device="cuda")
-    p_out = torch.empty((2 * A,), dtype=torch.int64, device="cuda")
-    both = torch.empty((3 * A,), dtype=torch.int64, device="cuda")
+    if args.workload == "c5":
+        lubs = [("vclock", torch.empty((R, A), dtype=torch.int64, device="cuda"), SEED_V)]
+    else:
+        lubs = [("gcounter", torch.empty((R, A), dtype=torch.int64, device="cuda"), SEED_G),
+                ("pncounter", torch.empty((R, 2 * A), dtype=torch.int64, device="cuda"), SEED_P)]
+    for _, x, seed in lubs:
+        cg.synth_fill(ctx, x, seed, 0, first_row=rank * R)
+    outs = [torch.empty((x.shape[1],), dtype=torch.int64, device="cuda") for _, x, _ in lubs]
+    mods = {"vclock": cg.vclock, "gcounter": cg.gcounter, "pncounter": cg.pncounter}
     torch.cuda.synchronize()
 
     def step():
-        cg.gcounter.lub_many(g_in, out=g_out, ctx=ctx)
-        cg.pncounter.lub_many(p_in, out=p_out, ctx=ctx)
-        if world > 1:
-            both[:A].copy_(g_out)
-            both[A:].copy_(p_out)
-            cdist.allreduce_umax_(both)
+        for (kind, x, _), o in zip(lubs, outs):
+            if cabi:  # local lub + one ncclAllReduce(ncclUint64, ncclMax), one C call
+                o.copy_(cg.shard.lub_many_sharded(kind, x, ctx=ctx))
+            else:
+                mods[kind].lub_many(x, out=o, ctx=ctx)
+                if world > 1:  # torch.distributed twin: sign-biased MAX all-reduce
+                    cdist.allreduce_umax_(o)
 
     for _ in range(args.warmup):
         step()
@@ -159,33 +198,35 @@ def main():
     kern_ms, launches = ctx.timing("lub_stream")
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        cdist.all_reduce_(t, dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # Parity (outside the timed region): unsigned max with torch ops + sampled CPU rows.
+    # Parity (outside the timed region): unsigned max with torch ops; for N > 1 the exchanged
+    # result must equal the max over every rank's torch reference (torch.distributed's own RCCL)
     sign = torch.tensor(-(2**63), dtype=torch.int64, device="cuda")
-    ref_g, ref_p = (g_in ^ sign).amax(0) ^ sign, (p_in ^ sign).amax(0) ^ sign
-    if world > 1:  # the exchanged result must equal the max of every rank's torch reference
-        ref = torch.cat([ref_g, ref_p])
+    refs = [(x ^ sign).amax(0) ^ sign for _, x, _ in lubs]
+    got, ref = torch.cat(outs), torch.cat(refs)
+    if world > 1:
         cdist.allreduce_umax_(ref)
-        ok = bool(torch.equal(both, ref))
-        t_ok = torch.tensor([1 if ok else 0], dtype=torch.int64, device="cuda")
-        dist.all_reduce(t_ok, op=dist.ReduceOp.MIN)
+        t_ok = torch.tensor([1 if bool(torch.equal(got, ref)) else 0], dtype=torch.int64, device="cuda")
+        cdist.all_reduce_(t_ok, dist.ReduceOp.MIN)
         ok = bool(t_ok.item())
     else:
-        ok = bool(torch.equal(g_out, ref_g)) and bool(torch.equal(p_out, ref_p))
+        ok = bool(torch.equal(got, ref))
 
-    merges_per_step = 2 * R * world
+    merges_per_step = len(lubs) * R * world
     value = merges_per_step * args.steps / elapsed
-    bytes_per_step = (R * A * 8 + A * 8) + (R * 2 * A * 8 + 2 * A * 8)
-    avg_launch_bytes = bytes_per_step / 2
+    bytes_per_step = sum(R * x.shape[1] * 8 + x.shape[1] * 8 for _, x, _ in lubs)
+    avg_launch_bytes = bytes_per_step / len(lubs)
     avg_launch_s = (kern_ms / 1e3) / launches if launches else float("nan")
     achieved = avg_launch_bytes / avg_launch_s / 1e9
+    workload = (f"vclock lub {R}x{A} (config 5 shard)" if args.workload == "c5"
+                else f"gcounter+pncounter lub {R}x{A}")
     traffic = None
     try:
         with open(args.traffic_json) as f:
             tj = json.load(f)
-        if tj.get("workload") == f"gcounter+pncounter lub {R}x{A}":
+        if tj.get("workload") == workload:
             traffic = tj.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
@@ -203,19 +244,22 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u64",
-            "data": "synthetic (counter-based splitmix64 replicas generated in HBM, seeds 0x5EED0002/3)",
+            "data": "synthetic (counter-based splitmix64 replicas generated in HBM, seeds 0x5EED0002/3/5)",
             "config": {
-                "workload": f"gcounter+pncounter lub {R}x{A}",
+                "workload": workload,
                 "replicas_per_gpu": R,
                 "actors": A,
-                "types": ["GCounter (A u64)", "PNCounter (2A u64)"],
+                "types": (["VClock (A u64)"] if args.workload == "c5" else ["GCounter (A u64)", "PNCounter (2A u64)"]),
                 "replica_merges_per_step": merges_per_step,
-                "exchange": "RCCL all-reduce MAX (sign-biased u64) of 3A words" if world > 1 else "none",
+                "exchange": ((f"C-ABI crdt_*_lub_many_sharded: ncclAllReduce(ncclUint64, ncclMax) of each partial "
+                              f"lub ({sum(x.shape[1] for _, x, _ in lubs)} words per step)") if cabi else
+                             "torch.distributed all-reduce MAX (sign-biased u64)") if world > 1 else "none",
                 "parallelism": f"replica-shard x{world}",
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "lub_stream_kernel<Max,2,8> (GCounter + PNCounter launches)",
+                "kernel": ("lub_stream_kernel<Max,2,8> (VClock launch)" if args.workload == "c5"
+                           else "lub_stream_kernel<Max,2,8> (GCounter + PNCounter launches)"),
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

@@ -356,6 +356,16 @@ typedef struct crdt_orswot_sharded_out {
 
 int crdt_orswot_lub_many_sharded(crdt_ctx *ctx, const crdt_orswot_batch *in, crdt_orswot_sharded_out *out);
 
+/* LWWReg (lwwreg.rs:43-45 -> update :84-98), replicas split in rank order: rank k holds replicas
+ * [base_k, base_k + R_k) of every group (marker / val at [g*group_stride + r], R_k may be 0) and
+ * passes its base_k.  Every rank receives the state of the GLOBAL left fold (out_marker[g],
+ * out_val[g]) and first_conflict[g] = the global index of its first erroring merge (UINT64_MAX if
+ * none; may be NULL): each rank continues the fold from the fold of the lower ranks' states, then a
+ * MIN all-reduce.  Exchange: ncclAllGather of (G markers, G vals, R_k) + ncclAllReduce(ncclMin). */
+int crdt_lwwreg_lub_many_sharded(crdt_ctx *ctx, const uint64_t *marker, const uint64_t *val, size_t G, size_t R,
+                                 size_t group_stride, uint64_t base, uint64_t *out_marker, uint64_t *out_val,
+                                 uint64_t *first_conflict);
+
 /* ---- Map<K, MVReg<u64, A>, A> --------------------------------------------------------------
  * Replaces Map::merge (map.rs:140-220) with V = MVReg (MVReg::merge mvreg.rs:112-128,
  * MVReg::forget :88-104), incl. apply_keyset_rm (map.rs:318-348) and apply_deferred (:311-316),
@@ -412,6 +422,15 @@ typedef struct crdt_map_out {
 } crdt_map_out;
 
 int crdt_map_lub_many(crdt_ctx *ctx, const crdt_map_batch *in, crdt_map_out *out);
+
+/* Map<K, MVReg> sharded by KEYS: rank k holds keys [k0, k0 + in->K) of every
+ * replica (the crdt_map_batch layout with K = its key count), every replica's clock and the group's
+ * whole deferred list with key bitmaps over all K keys (def_keys [D][ceil(K/64)]).  Keys are
+ * independent given the clocks and the deferred list, so each rank's fold of its keys is the exact
+ * left fold (no data-path collective); out holds the rank's keys, except out->def_keys
+ * [D][ceil(K/64)]: the surviving removes' key sets over ALL keys, assembled by one
+ * ncclAllReduce(ncclSum) (disjoint ranges: sum = union).  def_keep is the same on every rank. */
+int crdt_map_lub_many_sharded(crdt_ctx *ctx, const crdt_map_batch *in, size_t k0, size_t K, crdt_map_out *out);
 
 /* ---- causal helpers on dense clock rows -----------------------------------
  * Row-pair ops over N pairs (x_i, y_i) of A-word rows (VClock, GCounter inner, or a PNCounter

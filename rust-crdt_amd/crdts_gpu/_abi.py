@@ -38,6 +38,7 @@ EXPORTS = (
     "crdt_comm_unique_id", "crdt_ctx_comm_init", "crdt_ctx_comm_destroy", "crdt_ctx_comm_info",
     "crdt_vclock_lub_many_sharded", "crdt_gcounter_lub_many_sharded", "crdt_pncounter_lub_many_sharded",
     "crdt_gset_lub_many_sharded", "crdt_orswot_lub_many_sharded",
+    "crdt_lwwreg_lub_many_sharded", "crdt_map_lub_many_sharded",
     "crdt_orswot_forget_batch", "crdt_map_forget_batch", "crdt_map_apply_batch",
     "crdt_orswot_merge_batch", "crdt_map_merge_batch",
 )
@@ -162,6 +163,8 @@ _SIGS.update({
     "crdt_orswot_merge_batch": ([P, ctypes.POINTER(OrswotStates), ctypes.POINTER(OrswotStates), P], ctypes.c_int),
     "crdt_map_merge_batch": ([P, ctypes.POINTER(MapStates), ctypes.POINTER(MapDeferred), ctypes.POINTER(MapStates),
                               ctypes.POINTER(MapDeferred), P], ctypes.c_int),
+    "crdt_lwwreg_lub_many_sharded": ([P, P, P, S, S, S, U64, P, P, P], ctypes.c_int),
+    "crdt_map_lub_many_sharded": ([P, ctypes.POINTER(MapBatch), S, S, ctypes.POINTER(MapOut)], ctypes.c_int),
     "crdt_comm_unique_id": ([P], ctypes.c_int),
     "crdt_ctx_comm_init": ([P, P, ctypes.c_int, ctypes.c_int], ctypes.c_int),
     "crdt_ctx_comm_destroy": ([P], ctypes.c_int),

@@ -49,7 +49,10 @@ def lub_many(clock: torch.Tensor, ec: torch.Tensor, vclk: torch.Tensor, vval: to
              def_off: Optional[Sequence[int]] = None, def_row: Optional[torch.Tensor] = None,
              def_clock: Optional[torch.Tensor] = None, def_keys: Optional[torch.Tensor] = None,
              vout: int = 4, ctx: Optional[Context] = None, check: bool = True,
-             vstate: int = 0) -> MapLub:
+             vstate: int = 0, _key_shard: Optional[tuple] = None) -> MapLub:
+    """`_key_shard=(k0, K_total)`: this rank's keys [k0, k0 + K) of a key-sharded fold through the
+    C ABI's communicator (crdt_map_lub_many_sharded; use crdts_gpu.shard.map_lub_many_sharded):
+    def_keys / the returned def_keys are then over all K_total keys."""
     ctx = ctx or Context.default(clock.device.index)
     for t, nm in ((clock, "clock"), (ec, "ec"), (vclk, "vclk"), (vval, "vval")):
         ctx.check_tensor(t, f"map.lub_many({nm})")
@@ -71,7 +74,7 @@ def lub_many(clock: torch.Tensor, ec: torch.Tensor, vclk: torch.Tensor, vval: to
                          (vv, "vval", (V, 1))):
         if tuple(t.stride()[2:]) != inner:
             raise ValueError(f"map.lub_many: {nm} must be packed within a replica")
-    Kw = (K + 63) // 64
+    Kw = (K + 63) // 64 if _key_shard is None else (int(_key_shard[1]) + 63) // 64
     dev = clock.device
     out_clock = torch.empty((G, A), dtype=torch.int64, device=dev)
     out_ec = torch.empty((G, K, A), dtype=torch.int64, device=dev)
@@ -115,7 +118,11 @@ def lub_many(clock: torch.Tensor, ec: torch.Tensor, vclk: torch.Tensor, vval: to
             keep = torch.empty(D, dtype=torch.uint8, device=dev)
             keys_out = torch.empty((D, Kw), dtype=torch.int64, device=dev)
             o.def_keep, o.def_keys = keep.data_ptr(), keys_out.data_ptr()
-    ctx.call("crdt_map_lub_many", ctypes.byref(b), ctypes.byref(o))
+    if _key_shard is None:
+        ctx.call("crdt_map_lub_many", ctypes.byref(b), ctypes.byref(o))
+    else:
+        ctx.call("crdt_map_lub_many_sharded", ctypes.byref(b), int(_key_shard[0]), int(_key_shard[1]),
+                 ctypes.byref(o))
     if check:
         f = 0
         for x in flags.cpu().numpy().tolist():
@@ -124,7 +131,7 @@ def lub_many(clock: torch.Tensor, ec: torch.Tensor, vclk: torch.Tensor, vval: to
             raise ValueError("map.lub_many: def_row must be non-decreasing within each group and < R")
         if f & 4 and vstate < 8:  # the fold state overflowed: rerun with the largest state
             return lub_many(clock, ec, vclk, vval, def_off, def_row, def_clock, def_keys, vout, ctx,
-                            check, vstate=8)
+                            check, vstate=8, _key_shard=_key_shard)
         if f & 4:
             raise MapCapacityError("map.lub_many: a key held more than 8 MVReg values during the "
                                    "fold (the kernel's state capacity); results incomplete")

@@ -5,6 +5,8 @@
     comm_init(ctx, uid, nranks, rank)       # collective
     lub_many_sharded("gcounter", shard)     # collective: every rank gets the global lub
     orswot_lub_many_sharded(clock, entries, def_off, def_clock, def_members)
+    lwwreg_lub_many_sharded(marker, val, base)       # replicas [base, base + R_k) of the global order
+    map_lub_many_sharded(clock, ec, vclk, vval, k0, K, ...)   # KEY shards [k0, k0 + K_k)
 
 `crdts_gpu.dist` is the torch.distributed twin of the same exchange (gloo-testable on CPU)."""
 from __future__ import annotations
@@ -134,3 +136,36 @@ def deferred_groups(res: OrswotSharded, G: int):
                 x &= x - 1
         out[g].add((tuple(int(v) for v in dc[d]), frozenset(ms)))
     return out
+
+
+def lwwreg_lub_many_sharded(marker: torch.Tensor, val: torch.Tensor, base: int, ctx: Optional[Context] = None):
+    """LWWReg fold over replicas split in rank order (crdt_lwwreg_lub_many_sharded): rank k passes its
+    (R_k,) or (G, R_k) marker / val block and the global index `base` of its first replica.  Returns
+    (marker, val, first_conflict) of the GLOBAL left fold on every rank (first_conflict -1 = none)."""
+    ctx = ctx or Context.default(marker.device.index)
+    ctx.check_tensor(marker, "lwwreg.lub_many_sharded(marker)")
+    ctx.check_tensor(val, "lwwreg.lub_many_sharded(val)")
+    if marker.shape != val.shape or marker.dim() not in (1, 2):
+        raise ValueError("lwwreg.lub_many_sharded: marker and val must share a (R,) or (G, R) shape")
+    squeeze = marker.dim() == 1
+    m2 = marker.reshape(1, -1) if squeeze else marker
+    v2 = val.reshape(1, -1) if squeeze else val
+    G, R = m2.shape
+    if R and (m2.stride(1) != 1 or v2.stride(1) != 1 or m2.stride(0) != v2.stride(0)):
+        raise ValueError("lwwreg.lub_many_sharded: rows must be contiguous with equal strides")
+    om = torch.empty(G, dtype=torch.int64, device=marker.device)
+    ov, fc = torch.empty_like(om), torch.empty_like(om)
+    ctx.call("crdt_lwwreg_lub_many_sharded", dptr(m2) if R else None, dptr(v2) if R else None, G, R,
+             m2.stride(0) if G > 1 else max(R, 1), ctypes.c_uint64(int(base)), dptr(om), dptr(ov), dptr(fc))
+    return (om[0], ov[0], fc[0]) if squeeze else (om, ov, fc)
+
+
+def map_lub_many_sharded(clock: torch.Tensor, ec: torch.Tensor, vclk: torch.Tensor, vval: torch.Tensor, k0: int,
+                         K: int, def_off=None, def_row=None, def_clock=None, def_keys=None, vout: int = 4,
+                         ctx: Optional[Context] = None):
+    """Key-sharded Map<K, MVReg> fold (crdt_map_lub_many_sharded): this rank's keys [k0, k0 + K_k) of
+    every replica (ec (G, R, K_k, A), ...), every replica clock, the whole deferred list with key
+    bitmaps over all K keys.  Returns a map.MapLub of the rank's keys whose def_keys span all K."""
+    from . import map as cmap
+    return cmap.lub_many(clock, ec, vclk, vval, def_off=def_off, def_row=def_row, def_clock=def_clock,
+                         def_keys=def_keys, vout=vout, ctx=ctx, _key_shard=(int(k0), int(K)))

@@ -115,6 +115,56 @@ static int lattice_sharded(crdt_ctx *ctx, Op op, const u64 *in, size_t G, size_t
   return lattice_lub_many(ctx, op, (const u64 *)all, G, ctx->nranks, W, n, W, out, W, 0);
 }
 
+
+// LWWReg exchange: tm[g*n + j] / tv[g*n + j] <- marker / val of group g of rank ranks[j] in the
+// gathered [nranks][2G+1] buffer (so the world states of a group are one contiguous "replica" row)
+__global__ __launch_bounds__(kBlock) void lww_world_rows_kernel(u64 *tm, u64 *tv, const u64 *all,
+                                                                const uint32_t *ranks, unsigned long long n,
+                                                                unsigned long long G) {
+  for (unsigned long long i = blockIdx.x * (unsigned long long)kBlock + threadIdx.x; i < G * n;
+       i += (unsigned long long)gridDim.x * kBlock) {
+    const unsigned long long g = i / n, j = i % n;
+    const u64 *row = all + (unsigned long long)ranks[j] * (2 * G + 1);
+    tm[i] = row[g];
+    tv[i] = row[G + g];
+  }
+}
+
+// local first-conflict index -> global (UINT64_MAX stays "none")
+__global__ __launch_bounds__(kBlock) void lww_rebase_kernel(u64 *fc, unsigned long long G, u64 base) {
+  for (unsigned long long g = blockIdx.x * (unsigned long long)kBlock + threadIdx.x; g < G;
+       g += (unsigned long long)gridDim.x * kBlock)
+    if (fc[g] != ~0ull) fc[g] += base;
+}
+
+// Map key shards: 64 bits of a key bitmap starting at bit `pos` (may be negative or run past
+// `nbits`: those bits read as 0)
+__device__ __forceinline__ u64 bits64(const u64 *b, long long pos, long long nbits) {
+  u64 v = 0;
+  for (int t = 0; t < 64; t += 1) {
+    const long long q = pos + t;
+    if (q >= 0 && q < nbits && ((b[q >> 6] >> (q & 63)) & 1ull)) v |= 1ull << t;
+  }
+  return v;
+}
+// dst[d][w] (dw words) = bits [off + 64w, off + 64w + 64) of src[d] (sw words, nbits valid bits),
+// i.e. a key range re-indexed from `off` (off < 0: placing a local range at -off)
+__global__ __launch_bounds__(kBlock) void bitmap_shift_kernel(u64 *dst, const u64 *src, unsigned long long D,
+                                                              unsigned long long dw, unsigned long long sw,
+                                                              long long off, long long nbits) {
+  for (unsigned long long i = blockIdx.x * (unsigned long long)kBlock + threadIdx.x; i < D * dw;
+       i += (unsigned long long)gridDim.x * kBlock) {
+    const unsigned long long d = i / dw, w = i % dw;
+    dst[i] = bits64(src + d * sw, off + (long long)(w * 64), nbits);
+  }
+}
+
+static unsigned small_grid(crdt_ctx *ctx, unsigned long long n) {
+  const unsigned long long want = (n + kBlock - 1) / kBlock;
+  const unsigned long long cap = (unsigned long long)ctx->cu_count * 4;
+  return (unsigned)(want == 0 ? 1 : (want < cap ? want : cap));
+}
+
 }  // namespace crdt
 
 using namespace crdt;
@@ -325,6 +375,113 @@ int crdt_orswot_lub_many_sharded(crdt_ctx *ctx, const crdt_orswot_batch *in, crd
     }
   }
   *out->ndef = nkeep;
+  return CRDT_OK;
+}
+
+int crdt_lwwreg_lub_many_sharded(crdt_ctx *ctx, const uint64_t *marker, const uint64_t *val, size_t G, size_t R,
+                                 size_t group_stride, uint64_t base, uint64_t *out_marker, uint64_t *out_val,
+                                 uint64_t *first_conflict) {
+  CRDT_CHECK_CTX(ctx);
+  CRDT_TRY(need_comm(ctx));
+  if (G == 0) return CRDT_OK;
+  if (!out_marker || !out_val) return fail(ctx, CRDT_EINVAL, "lwwreg_lub_many_sharded: NULL output");
+  if (R && (!marker || !val)) return fail(ctx, CRDT_EINVAL, "lwwreg_lub_many_sharded: NULL input");
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  auto comm = (ncclComm_t)ctx->comm;
+  const size_t W = (size_t)ctx->nranks, row = 2 * G + 1;
+  void *send, *all, *tmv, *pst;
+  CRDT_TRY(sbuf(ctx, 0, row * 8, &send));
+  CRDT_TRY(sbuf(ctx, 1, W * row * 8, &all));
+  CRDT_TRY(sbuf(ctx, 2, 2 * G * W * 8, &tmv));
+  CRDT_TRY(sbuf(ctx, 3, 3 * G * 8 + W * 4 + 64, &pst));
+  uint64_t *lm = (uint64_t *)send, *lv = lm + G;
+  uint64_t *tm = (uint64_t *)tmv, *tv = tm + G * W;
+  uint64_t *pm = (uint64_t *)pst, *pv = pm + G, *fc = pv + G;
+  uint32_t *ranks = (uint32_t *)(fc + G);
+  // 1. local fold of the shard (acc = shard[0]; conflicts indexed locally); R_k travels along
+  if (R) CRDT_TRY(crdt_lwwreg_lub_many(ctx, marker, val, G, R, group_stride, lm, lv, fc, 0));
+  const uint64_t rk = R;
+  CRDT_TRY(stage_h2d(ctx, lm + 2 * G, &rk, 8));
+  // 2. all-gather the rank states
+  timing_begin(ctx, "shard_exchange");
+  CRDT_NCCL(ctx, ncclAllGather(send, all, row, ncclUint64, comm, ctx->stream));
+  timing_end(ctx);
+  std::vector<uint64_t> counts(W);
+  for (size_t r = 0; r < W; ++r)
+    CRDT_HIP(ctx, hipMemcpyAsync(&counts[r], (u64 *)all + r * row + 2 * G, 8, hipMemcpyDeviceToHost, ctx->stream));
+  CRDT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  std::vector<uint32_t> nz;
+  size_t before = 0;  // non-empty ranks before this one
+  for (size_t r = 0; r < W; ++r)
+    if (counts[r]) {
+      if ((int)r < ctx->rank) ++before;
+      nz.push_back((uint32_t)r);
+    }
+  const size_t n = nz.size();
+  if (n == 0) {  // no replica anywhere: the zero register, no conflict
+    CRDT_HIP(ctx, hipMemsetAsync(out_marker, 0, G * 8, ctx->stream));
+    CRDT_HIP(ctx, hipMemsetAsync(out_val, 0, G * 8, ctx->stream));
+    if (first_conflict) CRDT_HIP(ctx, hipMemsetAsync(first_conflict, 0xFF, G * 8, ctx->stream));
+    return CRDT_OK;
+  }
+  CRDT_TRY(stage_h2d(ctx, ranks, nz.data(), n * 4));
+  hipLaunchKernelGGL(lww_world_rows_kernel, dim3(small_grid(ctx, G * n)), dim3(kBlock), 0, ctx->stream, (u64 *)tm, (u64 *)tv,
+                     (const u64 *)all, (const uint32_t *)ranks, (unsigned long long)n, (unsigned long long)G);
+  CRDT_HIP(ctx, hipGetLastError());
+  // 3. the shard continues the GLOBAL fold from the fold of the lower ranks' states, so its
+  //    conflicts are those of the global left fold (lwwreg.rs:84-98 is order-dependent)
+  if (!R) {
+    CRDT_HIP(ctx, hipMemsetAsync(fc, 0xFF, G * 8, ctx->stream));
+  } else if (before > 0) {
+    CRDT_TRY(crdt_lwwreg_lub_many(ctx, tm, tv, G, before, n, pm, pv, nullptr, 0));
+    CRDT_TRY(crdt_lwwreg_lub_many(ctx, marker, val, G, R, group_stride, pm, pv, fc, CRDT_ACCUMULATE));
+  }
+  hipLaunchKernelGGL(lww_rebase_kernel, dim3(small_grid(ctx, G)), dim3(kBlock), 0, ctx->stream, (u64 *)fc,
+                     (unsigned long long)G, (u64)base);
+  CRDT_HIP(ctx, hipGetLastError());
+  CRDT_NCCL(ctx, ncclAllReduce(fc, first_conflict ? (void *)first_conflict : (void *)fc, G, ncclUint64, ncclMin, comm,
+                               ctx->stream));
+  // 4. the global state: the fold of the world's rank states
+  return crdt_lwwreg_lub_many(ctx, tm, tv, G, n, n, out_marker, out_val, nullptr, 0);
+}
+
+int crdt_map_lub_many_sharded(crdt_ctx *ctx, const crdt_map_batch *in, size_t k0, size_t K, crdt_map_out *out) {
+  CRDT_CHECK_CTX(ctx);
+  CRDT_TRY(need_comm(ctx));
+  if (!in || !out) return fail(ctx, CRDT_EINVAL, "map_lub_many_sharded: NULL argument");
+  const size_t G = in->G, Kk = in->K, A = in->A;
+  if (k0 + Kk > K) return fail(ctx, CRDT_EINVAL, "map_lub_many_sharded: key range [%zu, %zu) past K = %zu", k0, k0 + Kk, K);
+  const size_t D = (in->def_off && G > 0) ? in->def_off[G] - in->def_off[0] : 0;
+  const size_t Kw = (K + 63) / 64, Kwl = (Kk + 63) / 64;
+  if (D == 0 || Kk == 0 || A == 0) return crdt_map_lub_many(ctx, in, out);
+  if (!in->def_keys || !out->def_keys || !out->def_keep)
+    return fail(ctx, CRDT_EINVAL, "map_lub_many_sharded: deferred buffers missing");
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  auto comm = (ncclComm_t)ctx->comm;
+  // the key bitmaps restricted to this rank's keys [k0, k0 + Kk), re-indexed from 0
+  void *lk, *ok;
+  CRDT_TRY(sbuf(ctx, 0, D * Kwl * 8, &lk));
+  CRDT_TRY(sbuf(ctx, 1, D * Kwl * 8, &ok));
+  hipLaunchKernelGGL(bitmap_shift_kernel, dim3(small_grid(ctx, D * Kwl)), dim3(kBlock), 0, ctx->stream, (u64 *)lk,
+                     (const u64 *)in->def_keys, (unsigned long long)D, (unsigned long long)Kwl,
+                     (unsigned long long)Kw, (long long)k0, (long long)(k0 + Kk));
+  CRDT_HIP(ctx, hipGetLastError());
+  crdt_map_batch loc = *in;
+  loc.def_keys = (const uint64_t *)lk;
+  crdt_map_out lo = *out;
+  lo.def_keys = (uint64_t *)ok;
+  // keys are independent given the clocks and the deferred list: the exact left fold of the
+  // rank's keys, with no data-path collective
+  CRDT_TRY(crdt_map_lub_many(ctx, &loc, &lo));
+  // surviving removes' key sets over all K keys: this rank's bits placed at k0, then a SUM
+  // all-reduce (disjoint key ranges: the sum is the union)
+  hipLaunchKernelGGL(bitmap_shift_kernel, dim3(small_grid(ctx, D * Kw)), dim3(kBlock), 0, ctx->stream,
+                     (u64 *)out->def_keys, (const u64 *)ok, (unsigned long long)D, (unsigned long long)Kw,
+                     (unsigned long long)Kwl, -(long long)k0, (long long)Kk);
+  CRDT_HIP(ctx, hipGetLastError());
+  timing_begin(ctx, "shard_exchange");
+  CRDT_NCCL(ctx, ncclAllReduce(out->def_keys, out->def_keys, D * Kw, ncclUint64, ncclSum, comm, ctx->stream));
+  timing_end(ctx);
   return CRDT_OK;
 }
 

@@ -70,3 +70,45 @@ def test_orswot_sharded_world1(comm_ctx, seed, G, R, M, A):
     # a too-small def_cap is retried with exactly enough room
     small = cg.shard.orswot_lub_many_sharded(to_dev(clock), to_dev(entries), ctx=comm_ctx, def_cap=1, **kw)
     assert cg.shard.deferred_groups(small, G) == got_d
+
+
+@pytest.mark.parametrize("G,R,base", [(3, 201, 0), (2, 57, 1000), (1, 0, 7)])
+def test_lwwreg_sharded_world1(comm_ctx, G, R, base):
+    """crdt_lwwreg_lub_many_sharded at world 1: the global fold is the local one, conflicts are
+    reported at base + local index (lwwreg.rs:84-98)."""
+    m = O.synth_matrix(47, G, max(R, 1), 2)[:, :R] % np.uint64(7)
+    v = O.synth_matrix(47, G, max(R, 1), 3)[:, :R] % np.uint64(2)
+    fm, fv, fc = cg.shard.lwwreg_lub_many_sharded(to_dev(m), to_dev(v), base, ctx=comm_ctx)
+    fm, fv, fc = to_host(fm), to_host(fv), to_host(fc)
+    for g in range(G):
+        if R == 0:
+            assert int(fc[g]) == 2**64 - 1
+            continue
+        om, ov, of, _ = O.lwwreg_fold(m[g], v[g])
+        assert (int(fm[g]), int(fv[g])) == (om, ov)
+        assert int(fc[g]) == (of if of == 2**64 - 1 else of + base)
+    assert R == 0 or any(int(x) != 2**64 - 1 for x in fc)
+
+
+@pytest.mark.parametrize("k0,Kk", [(0, 29), (5, 15), (20, 9)])
+def test_map_sharded_world1(comm_ctx, k0, Kk):
+    """crdt_map_lub_many_sharded at world 1 over a key range: the rank's keys equal the oracle's
+    whole-map fold restricted to them, and the surviving removes' key sets (over ALL keys) hold
+    exactly this rank's keys of them (the bitmap restriction / placement around the exchange)."""
+    import dist_world2_data as D
+    d = D.map_input()
+    K = d["ec"].shape[1]
+    exp = O.map_fold(d["clock"], d["ec"], d["vclk"], d["vval"], d["def_row"], d["def_clock"], d["def_keys"], 8)
+    Dn = d["def_row"].shape[0]
+    t = lambda a: to_dev(np.ascontiguousarray(a))  # noqa: E731
+    res = cg.shard.map_lub_many_sharded(t(d["clock"]), t(d["ec"][:, k0:k0 + Kk]), t(d["vclk"][:, k0:k0 + Kk]),
+                                        t(d["vval"][:, k0:k0 + Kk]), k0, K, def_off=[0, Dn],
+                                        def_row=torch.from_numpy(d["def_row"].astype(np.int32)).cuda(),
+                                        def_clock=t(d["def_clock"]), def_keys=t(d["def_keys"]), vout=8, ctx=comm_ctx)
+    np.testing.assert_array_equal(to_host(res.clock), exp[0])
+    np.testing.assert_array_equal(to_host(res.ec), exp[1][k0:k0 + Kk])
+    np.testing.assert_array_equal(to_host(res.vclk), exp[2][k0:k0 + Kk])
+    np.testing.assert_array_equal(to_host(res.vval), exp[3][k0:k0 + Kk])
+    got = cg.map.deferred_set(t(d["def_clock"]), res.def_keep, res.def_keys)
+    want = {(c, frozenset(k for k in ks if k0 <= k < k0 + Kk)) for c, ks in exp[5]}
+    assert got == want and len(want) > 0
