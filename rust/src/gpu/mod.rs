@@ -1,0 +1,677 @@
+//! Batched state merges on an MI355X through `libcrdt_gpu` (hand-written gfx950 HIP kernels
+//! behind the C ABI of `include/crdt_gpu.h`).
+//!
+//! This is the `gpu` module a maintainer adds to the `crdts` crate (`src/gpu/`), together with
+//! `build.rs` (the hipcc step) and `pub mod gpu;` in `src/lib.rs` behind a `gpu` feature.  It keeps
+//! the crate's trait surface (`CvRDT::merge`, `traits.rs:4-7`; `FunkyCvRDT::merge` for `LWWReg`,
+//! `traits.rs:49-55`) and adds the batched forms:
+//!
+//! * [`BatchCvRDT::lub_many`]: `let mut acc = T::new(); for r in replicas { acc.merge(r) }`
+//!   (the fold of `test/orswot.rs:50-53`), computed on the GPU;
+//! * [`BatchCvRDT::merge_batch`]: `for (s, o) in selves.iter_mut().zip(others) { s.merge(o) }`.
+//!
+//! States are interned to the dense structure-of-arrays layout the kernels read (actors, members
+//! and set elements to dense indices; an absent actor is a 0 counter, exact because
+//! `VClock::apply_dot` never stores 0, `vclock.rs:155-159`), copied to HBM, merged, and rebuilt.
+//! Callers that keep replica states resident in HBM use [`ffi`] directly on device buffers.
+//!
+//! Field access: `VClock::dots`, the `Orswot` fields and the `LWWReg` fields are already visible
+//! to an in-crate module; the maintainer changes `GCounter::inner`, `PNCounter::{p, n}` and
+//! `GSet::value` from private to `pub(crate)` (visibility only, no behaviour change).
+//!
+//! Not built in the repository that ships it (its image has no Rust toolchain); the extern block
+//! in [`ffi`] is generated from the header and checked against it by `tests/test_rust_shim.py`.
+#![allow(unsafe_code)]
+
+pub mod ffi;
+mod hip;
+
+use std::collections::{BTreeMap, BTreeSet, HashMap, HashSet};
+use std::ffi::CStr;
+use std::hash::Hash;
+use std::os::raw::c_int;
+use std::ptr;
+
+use crate::error::Error as CrdtError;
+use crate::orswot::Member;
+use crate::traits::CvRDT;
+use crate::vclock::{Actor, VClock};
+use crate::{GCounter, GSet, LWWReg, Orswot, PNCounter};
+
+pub use hip::DeviceBuf;
+
+/// A failed library or HIP call (status code and the library's message).
+#[derive(Debug, Clone, PartialEq, Eq)]
+pub struct GpuError {
+    /// `CRDT_E*` status (negative) or the HIP error code of a staging copy.
+    pub code: i32,
+    /// `crdt_last_error` text, or a description of the failed staging step.
+    pub msg: String,
+}
+
+impl std::fmt::Display for GpuError {
+    fn fmt(&self, f: &mut std::fmt::Formatter<'_>) -> std::fmt::Result {
+        write!(f, "libcrdt_gpu error {}: {}", self.code, self.msg)
+    }
+}
+
+impl std::error::Error for GpuError {}
+
+/// A `crdt_ctx`: one per host thread, bound to one HIP device (scratch and stream owned here).
+pub struct GpuCtx {
+    raw: *mut ffi::crdt_ctx,
+}
+
+impl GpuCtx {
+    /// `crdt_ctx_create(device)`.
+    pub fn new(device: i32) -> Result<Self, GpuError> {
+        let mut raw = ptr::null_mut();
+        let rc = unsafe { ffi::crdt_ctx_create(device, &mut raw) };
+        if rc != ffi::CRDT_OK {
+            return Err(GpuError { code: rc, msg: last_error(ptr::null()) });
+        }
+        Ok(GpuCtx { raw })
+    }
+
+    /// The raw handle, for calls through [`ffi`] on caller-owned device buffers.
+    pub fn as_ptr(&self) -> *mut ffi::crdt_ctx {
+        self.raw
+    }
+
+    /// Map a status code to `Result` (the library never throws across the ABI).
+    pub fn check(&self, rc: c_int) -> Result<(), GpuError> {
+        if rc == ffi::CRDT_OK {
+            Ok(())
+        } else {
+            Err(GpuError { code: rc, msg: last_error(self.raw) })
+        }
+    }
+
+    /// Block until the work issued through this ctx has finished.
+    pub fn synchronize(&self) -> Result<(), GpuError> {
+        self.check(unsafe { ffi::crdt_ctx_synchronize(self.raw) })
+    }
+}
+
+impl Drop for GpuCtx {
+    fn drop(&mut self) {
+        unsafe {
+            ffi::crdt_ctx_destroy(self.raw);
+        }
+    }
+}
+
+fn last_error(ctx: *const ffi::crdt_ctx) -> String {
+    unsafe {
+        let p = ffi::crdt_last_error(ctx);
+        if p.is_null() {
+            String::new()
+        } else {
+            CStr::from_ptr(p).to_string_lossy().into_owned()
+        }
+    }
+}
+
+/// Batched extension of `CvRDT` (`traits.rs:4-7`); the single-pair `merge` is unchanged.
+pub trait BatchCvRDT: CvRDT + Sized {
+    /// `let mut acc = Self::new(); for r in replicas { acc.merge(r) }`, on the GPU.
+    fn lub_many(ctx: &GpuCtx, replicas: Vec<Self>) -> Result<Self, GpuError>;
+    /// `for (s, o) in selves.iter_mut().zip(others) { s.merge(o) }`, on the GPU, in place.
+    fn merge_batch(ctx: &GpuCtx, selves: &mut [Self], others: Vec<Self>) -> Result<(), GpuError>;
+}
+
+/// Dense indices for ids (actors, members, set elements): first-seen order.
+struct Index<T: Ord + Clone> {
+    pos: BTreeMap<T, usize>,
+    ids: Vec<T>,
+}
+
+impl<T: Ord + Clone> Index<T> {
+    fn new() -> Self {
+        Index { pos: BTreeMap::new(), ids: Vec::new() }
+    }
+    fn intern(&mut self, id: &T) -> usize {
+        if let Some(&i) = self.pos.get(id) {
+            return i;
+        }
+        let i = self.ids.len();
+        self.pos.insert(id.clone(), i);
+        self.ids.push(id.clone());
+        i
+    }
+    fn width(&self) -> usize {
+        self.ids.len().max(1)
+    }
+}
+
+/// Hash-keyed index for `Member: Clone + Hash + Eq` ids (no `Ord` bound in the crate).
+struct HIndex<T: Clone + Hash + Eq> {
+    pos: HashMap<T, usize>,
+    ids: Vec<T>,
+}
+
+impl<T: Clone + Hash + Eq> HIndex<T> {
+    fn new() -> Self {
+        HIndex { pos: HashMap::new(), ids: Vec::new() }
+    }
+    fn intern(&mut self, id: &T) -> usize {
+        if let Some(&i) = self.pos.get(id) {
+            return i;
+        }
+        let i = self.ids.len();
+        self.pos.insert(id.clone(), i);
+        self.ids.push(id.clone());
+        i
+    }
+    fn width(&self) -> usize {
+        self.ids.len().max(1)
+    }
+}
+
+fn clock_row<A: Actor>(c: &VClock<A>, idx: &Index<A>, row: &mut [u64]) {
+    for (a, n) in c.dots.iter() {
+        row[idx.pos[a]] = *n;
+    }
+}
+
+fn row_clock<A: Actor>(row: &[u64], idx: &Index<A>) -> VClock<A> {
+    let mut c = VClock::new();
+    for (i, &n) in row.iter().enumerate() {
+        if n != 0 && i < idx.ids.len() {
+            c.dots.insert(idx.ids[i].clone(), n);
+        }
+    }
+    c
+}
+
+/// Lattice lub / merge_batch of dense rows through one of the max / OR entry points.
+enum Lattice {
+    VClock,
+    GCounter,
+    PNCounter,
+    GSet,
+}
+
+fn lattice_lub(ctx: &GpuCtx, kind: Lattice, rows: &[u64], r: usize, w: usize) -> Result<Vec<u64>, GpuError> {
+    let input = DeviceBuf::from_host(rows)?;
+    let out = DeviceBuf::<u64>::zeroed(w)?;
+    let width = if let Lattice::PNCounter = kind { w / 2 } else { w };
+    let rc = unsafe {
+        let (i, o) = (input.as_ptr(), out.as_mut_ptr());
+        match kind {
+            Lattice::VClock => ffi::crdt_vclock_lub_many(ctx.raw, i, 1, r, width, w, r * w, o, w, 0),
+            Lattice::GCounter => ffi::crdt_gcounter_lub_many(ctx.raw, i, 1, r, width, w, r * w, o, w, 0),
+            Lattice::PNCounter => ffi::crdt_pncounter_lub_many(ctx.raw, i, 1, r, width, w, r * w, o, w, 0),
+            Lattice::GSet => ffi::crdt_gset_lub_many(ctx.raw, i, 1, r, width, w, r * w, o, w, 0),
+        }
+    };
+    ctx.check(rc)?;
+    out.to_host()
+}
+
+fn lattice_pairs(ctx: &GpuCtx, kind: Lattice, selves: &[u64], others: &[u64], n: usize, w: usize)
+                 -> Result<Vec<u64>, GpuError> {
+    let s = DeviceBuf::from_host(selves)?;
+    let o = DeviceBuf::from_host(others)?;
+    let width = if let Lattice::PNCounter = kind { w / 2 } else { w };
+    let rc = unsafe {
+        let (sp, op) = (s.as_mut_ptr(), o.as_ptr());
+        match kind {
+            Lattice::VClock => ffi::crdt_vclock_merge_batch(ctx.raw, sp, op, n, width, w, w),
+            Lattice::GCounter => ffi::crdt_gcounter_merge_batch(ctx.raw, sp, op, n, width, w, w),
+            Lattice::PNCounter => ffi::crdt_pncounter_merge_batch(ctx.raw, sp, op, n, width, w, w),
+            Lattice::GSet => ffi::crdt_gset_merge_batch(ctx.raw, sp, op, n, width, w, w),
+        }
+    };
+    ctx.check(rc)?;
+    s.to_host()
+}
+
+// ---- VClock / GCounter: elementwise max (vclock.rs:130-136, gcounter.rs:44-48) ----------------
+impl<A: Actor> BatchCvRDT for VClock<A> {
+    fn lub_many(ctx: &GpuCtx, replicas: Vec<Self>) -> Result<Self, GpuError> {
+        let mut idx = Index::new();
+        for r in &replicas {
+            for a in r.dots.keys() {
+                idx.intern(a);
+            }
+        }
+        let (r, w) = (replicas.len(), idx.width());
+        if r == 0 {
+            return Ok(VClock::new());
+        }
+        let mut rows = vec![0u64; r * w];
+        for (i, c) in replicas.iter().enumerate() {
+            clock_row(c, &idx, &mut rows[i * w..(i + 1) * w]);
+        }
+        let out = lattice_lub(ctx, Lattice::VClock, &rows, r, w)?;
+        Ok(row_clock(&out, &idx))
+    }
+
+    fn merge_batch(ctx: &GpuCtx, selves: &mut [Self], others: Vec<Self>) -> Result<(), GpuError> {
+        let n = selves.len().min(others.len());
+        if n == 0 {
+            return Ok(());
+        }
+        let mut idx = Index::new();
+        for c in selves.iter().chain(others.iter()) {
+            for a in c.dots.keys() {
+                idx.intern(a);
+            }
+        }
+        let w = idx.width();
+        let (mut s, mut o) = (vec![0u64; n * w], vec![0u64; n * w]);
+        for i in 0..n {
+            clock_row(&selves[i], &idx, &mut s[i * w..(i + 1) * w]);
+            clock_row(&others[i], &idx, &mut o[i * w..(i + 1) * w]);
+        }
+        let out = lattice_pairs(ctx, Lattice::VClock, &s, &o, n, w)?;
+        for i in 0..n {
+            selves[i] = row_clock(&out[i * w..(i + 1) * w], &idx);
+        }
+        Ok(())
+    }
+}
+
+impl<A: Actor> BatchCvRDT for GCounter<A> {
+    fn lub_many(ctx: &GpuCtx, replicas: Vec<Self>) -> Result<Self, GpuError> {
+        let inner = replicas.into_iter().map(|g| g.inner).collect();
+        let mut out = GCounter::new();
+        out.inner = <VClock<A> as BatchCvRDT>::lub_many(ctx, inner)?;
+        Ok(out)
+    }
+
+    fn merge_batch(ctx: &GpuCtx, selves: &mut [Self], others: Vec<Self>) -> Result<(), GpuError> {
+        let mut s: Vec<VClock<A>> = selves.iter().map(|g| g.inner.clone()).collect();
+        <VClock<A> as BatchCvRDT>::merge_batch(ctx, &mut s, others.into_iter().map(|g| g.inner).collect())?;
+        for (g, c) in selves.iter_mut().zip(s) {
+            g.inner = c;
+        }
+        Ok(())
+    }
+}
+
+// ---- PNCounter: P and N maxima over rows P | N (pncounter.rs:70-75) ------------------------------
+fn pn_rows<A: Actor>(states: &[&PNCounter<A>], idx: &Index<A>) -> Vec<u64> {
+    let w = idx.width();
+    let mut rows = vec![0u64; states.len() * 2 * w];
+    for (i, s) in states.iter().enumerate() {
+        let row = &mut rows[i * 2 * w..(i + 1) * 2 * w];
+        clock_row(&s.p.inner, idx, &mut row[..w]);
+        clock_row(&s.n.inner, idx, &mut row[w..]);
+    }
+    rows
+}
+
+fn pn_state<A: Actor>(row: &[u64], idx: &Index<A>) -> PNCounter<A> {
+    let w = idx.width();
+    let mut s = PNCounter::new();
+    s.p.inner = row_clock(&row[..w], idx);
+    s.n.inner = row_clock(&row[w..], idx);
+    s
+}
+
+impl<A: Actor> BatchCvRDT for PNCounter<A> {
+    fn lub_many(ctx: &GpuCtx, replicas: Vec<Self>) -> Result<Self, GpuError> {
+        if replicas.is_empty() {
+            return Ok(PNCounter::new());
+        }
+        let mut idx = Index::new();
+        for r in &replicas {
+            for a in r.p.inner.dots.keys().chain(r.n.inner.dots.keys()) {
+                idx.intern(a);
+            }
+        }
+        let refs: Vec<&Self> = replicas.iter().collect();
+        let rows = pn_rows(&refs, &idx);
+        let out = lattice_lub(ctx, Lattice::PNCounter, &rows, replicas.len(), 2 * idx.width())?;
+        Ok(pn_state(&out, &idx))
+    }
+
+    fn merge_batch(ctx: &GpuCtx, selves: &mut [Self], others: Vec<Self>) -> Result<(), GpuError> {
+        let n = selves.len().min(others.len());
+        if n == 0 {
+            return Ok(());
+        }
+        let mut idx = Index::new();
+        for r in selves.iter().chain(others.iter()) {
+            for a in r.p.inner.dots.keys().chain(r.n.inner.dots.keys()) {
+                idx.intern(a);
+            }
+        }
+        let w2 = 2 * idx.width();
+        let s = pn_rows(&selves[..n].iter().collect::<Vec<_>>(), &idx);
+        let o = pn_rows(&others[..n].iter().collect::<Vec<_>>(), &idx);
+        let out = lattice_pairs(ctx, Lattice::PNCounter, &s, &o, n, w2)?;
+        for i in 0..n {
+            selves[i] = pn_state(&out[i * w2..(i + 1) * w2], &idx);
+        }
+        Ok(())
+    }
+}
+
+// ---- GSet: bitmap union (gset.rs:38-40) ---------------------------------------------------------
+fn set_row<T: Ord + Clone>(s: &BTreeSet<T>, idx: &Index<T>, row: &mut [u64]) {
+    for x in s {
+        let b = idx.pos[x];
+        row[b / 64] |= 1u64 << (b % 64);
+    }
+}
+
+fn row_set<T: Ord + Clone>(row: &[u64], idx: &Index<T>) -> BTreeSet<T> {
+    let mut out = BTreeSet::new();
+    for (w, &word) in row.iter().enumerate() {
+        let mut x = word;
+        while x != 0 {
+            let b = w * 64 + x.trailing_zeros() as usize;
+            x &= x - 1;
+            if b < idx.ids.len() {
+                out.insert(idx.ids[b].clone());
+            }
+        }
+    }
+    out
+}
+
+impl<T: Ord + Clone> BatchCvRDT for GSet<T> {
+    fn lub_many(ctx: &GpuCtx, replicas: Vec<Self>) -> Result<Self, GpuError> {
+        if replicas.is_empty() {
+            return Ok(GSet::new());
+        }
+        let mut idx = Index::new();
+        for r in &replicas {
+            for x in &r.value {
+                idx.intern(x);
+            }
+        }
+        let w = (idx.width() + 63) / 64;
+        let mut rows = vec![0u64; replicas.len() * w];
+        for (i, r) in replicas.iter().enumerate() {
+            set_row(&r.value, &idx, &mut rows[i * w..(i + 1) * w]);
+        }
+        let out = lattice_lub(ctx, Lattice::GSet, &rows, replicas.len(), w)?;
+        let mut g = GSet::new();
+        g.value = row_set(&out, &idx);
+        Ok(g)
+    }
+
+    fn merge_batch(ctx: &GpuCtx, selves: &mut [Self], others: Vec<Self>) -> Result<(), GpuError> {
+        let n = selves.len().min(others.len());
+        if n == 0 {
+            return Ok(());
+        }
+        let mut idx = Index::new();
+        for r in selves.iter().chain(others.iter()) {
+            for x in &r.value {
+                idx.intern(x);
+            }
+        }
+        let w = (idx.width() + 63) / 64;
+        let (mut s, mut o) = (vec![0u64; n * w], vec![0u64; n * w]);
+        for i in 0..n {
+            set_row(&selves[i].value, &idx, &mut s[i * w..(i + 1) * w]);
+            set_row(&others[i].value, &idx, &mut o[i * w..(i + 1) * w]);
+        }
+        let out = lattice_pairs(ctx, Lattice::GSet, &s, &o, n, w)?;
+        for i in 0..n {
+            selves[i].value = row_set(&out[i * w..(i + 1) * w], &idx);
+        }
+        Ok(())
+    }
+}
+
+// ---- LWWReg<V, u64>: FunkyCvRDT (lwwreg.rs:43-45 -> update :84-98) --------------------------------
+/// Batched `FunkyCvRDT::merge` for `LWWReg<V, u64>` (values interned; equal values <=> equal ids).
+pub trait BatchFunkyLww: Sized {
+    /// The fold `acc = replicas[0]; for r in replicas[1..] { acc.merge(r) }` where an erroring
+    /// merge leaves `acc` unchanged (as `update` does); returns the state and the index of the
+    /// first merge that returned `Err(ConflictingMarker)`, if any.
+    fn lub_many(ctx: &GpuCtx, replicas: Vec<Self>) -> Result<(Self, Option<usize>), GpuError>;
+    /// `selves[i].merge(others[i])` for every i: `Err(ConflictingMarker)` where the markers are
+    /// equal and the values differ, that register then unchanged.
+    fn merge_batch(ctx: &GpuCtx, selves: &mut [Self], others: Vec<Self>)
+                   -> Result<Vec<Result<(), CrdtError>>, GpuError>;
+}
+
+impl<V: Ord + Clone + PartialEq> BatchFunkyLww for LWWReg<V, u64> {
+    fn lub_many(ctx: &GpuCtx, replicas: Vec<Self>) -> Result<(Self, Option<usize>), GpuError> {
+        let r = replicas.len();
+        if r == 0 {
+            return Err(GpuError { code: ffi::CRDT_EINVAL, msg: "LWWReg lub_many of no replica".into() });
+        }
+        let mut vals = Index::new();
+        let markers: Vec<u64> = replicas.iter().map(|x| x.marker).collect();
+        let ids: Vec<u64> = replicas.iter().map(|x| vals.intern(&x.val) as u64).collect();
+        let (m, v) = (DeviceBuf::from_host(&markers)?, DeviceBuf::from_host(&ids)?);
+        let (om, ov, of) = (DeviceBuf::<u64>::zeroed(1)?, DeviceBuf::<u64>::zeroed(1)?, DeviceBuf::<u64>::zeroed(1)?);
+        ctx.check(unsafe {
+            ffi::crdt_lwwreg_lub_many(ctx.raw, m.as_ptr(), v.as_ptr(), 1, r, r, om.as_mut_ptr(), ov.as_mut_ptr(),
+                                      of.as_mut_ptr(), 0)
+        })?;
+        let (mk, vi, fc) = (om.to_host()?[0], ov.to_host()?[0], of.to_host()?[0]);
+        let state = LWWReg { val: vals.ids[vi as usize].clone(), marker: mk };
+        Ok((state, if fc == u64::MAX { None } else { Some(fc as usize) }))
+    }
+
+    fn merge_batch(ctx: &GpuCtx, selves: &mut [Self], others: Vec<Self>)
+                   -> Result<Vec<Result<(), CrdtError>>, GpuError> {
+        let n = selves.len().min(others.len());
+        let mut vals = Index::new();
+        let sm: Vec<u64> = selves[..n].iter().map(|x| x.marker).collect();
+        let sv: Vec<u64> = selves[..n].iter().map(|x| vals.intern(&x.val) as u64).collect();
+        let om: Vec<u64> = others[..n].iter().map(|x| x.marker).collect();
+        let ov: Vec<u64> = others[..n].iter().map(|x| vals.intern(&x.val) as u64).collect();
+        if n == 0 {
+            return Ok(Vec::new());
+        }
+        let (dsm, dsv) = (DeviceBuf::from_host(&sm)?, DeviceBuf::from_host(&sv)?);
+        let (dom, dov) = (DeviceBuf::from_host(&om)?, DeviceBuf::from_host(&ov)?);
+        let conflict = DeviceBuf::<u8>::zeroed(n)?;
+        ctx.check(unsafe {
+            ffi::crdt_lwwreg_merge_batch(ctx.raw, dsm.as_mut_ptr(), dsv.as_mut_ptr(), dom.as_ptr(), dov.as_ptr(), n,
+                                         conflict.as_mut_ptr())
+        })?;
+        let (m2, v2, c) = (dsm.to_host()?, dsv.to_host()?, conflict.to_host()?);
+        let mut res = Vec::with_capacity(n);
+        for i in 0..n {
+            if c[i] != 0 {
+                res.push(Err(CrdtError::ConflictingMarker));
+            } else {
+                selves[i].marker = m2[i];
+                selves[i].val = vals.ids[v2[i] as usize].clone();
+                res.push(Ok(()));
+            }
+        }
+        Ok(res)
+    }
+}
+
+// ---- Orswot: dot-store join + deferred removes (orswot.rs:81-149, 230-250, 281-286) ---------------
+struct OrswotDense<M: Member, A: Actor> {
+    actors: Index<A>,
+    members: HIndex<M>,
+}
+
+impl<M: Member, A: Actor> OrswotDense<M, A> {
+    fn of<'a, I: Iterator<Item = &'a Orswot<M, A>>>(states: I) -> Self
+    where
+        M: 'a,
+        A: 'a,
+    {
+        let mut d = OrswotDense { actors: Index::new(), members: HIndex::new() };
+        for s in states {
+            for a in s.clock.dots.keys() {
+                d.actors.intern(a);
+            }
+            for (m, c) in s.entries.iter() {
+                d.members.intern(m);
+                for a in c.dots.keys() {
+                    d.actors.intern(a);
+                }
+            }
+            for (k, ms) in s.deferred.iter() {
+                for a in k.dots.keys() {
+                    d.actors.intern(a);
+                }
+                for m in ms {
+                    d.members.intern(m);
+                }
+            }
+        }
+        d
+    }
+
+    /// (clock [A], entries [M][A], deferred rm rows [D][A], member bitmaps [D][Mw])
+    fn ingest(&self, s: &Orswot<M, A>) -> (Vec<u64>, Vec<u64>, Vec<u64>, Vec<u64>) {
+        let (a, m) = (self.actors.width(), self.members.width());
+        let mw = (m + 63) / 64;
+        let mut clock = vec![0u64; a];
+        clock_row(&s.clock, &self.actors, &mut clock);
+        let mut entries = vec![0u64; m * a];
+        for (mem, c) in s.entries.iter() {
+            let i = self.members.pos[mem];
+            clock_row(c, &self.actors, &mut entries[i * a..(i + 1) * a]);
+        }
+        let (mut dcl, mut dmb) = (Vec::new(), Vec::new());
+        for (k, ms) in s.deferred.iter() {
+            let mut row = vec![0u64; a];
+            clock_row(k, &self.actors, &mut row);
+            let mut bits = vec![0u64; mw];
+            for mem in ms {
+                let b = self.members.pos[mem];
+                bits[b / 64] |= 1u64 << (b % 64);
+            }
+            dcl.extend(row);
+            dmb.extend(bits);
+        }
+        (clock, entries, dcl, dmb)
+    }
+
+    fn egress(&self, clock: &[u64], entries: &[u64], deferred: &[(Vec<u64>, Vec<u64>)]) -> Orswot<M, A> {
+        let a = self.actors.width();
+        let mut s = Orswot::new();
+        s.clock = row_clock(clock, &self.actors);
+        for (i, mem) in self.members.ids.iter().enumerate() {
+            let row = &entries[i * a..(i + 1) * a];
+            if row.iter().any(|&x| x != 0) {
+                s.entries.insert(mem.clone(), row_clock(row, &self.actors));
+            }
+        }
+        for (rm, bits) in deferred {
+            let mut ms = HashSet::new();
+            for (w, &word) in bits.iter().enumerate() {
+                let mut x = word;
+                while x != 0 {
+                    let b = w * 64 + x.trailing_zeros() as usize;
+                    x &= x - 1;
+                    if b < self.members.ids.len() {
+                        ms.insert(self.members.ids[b].clone());
+                    }
+                }
+            }
+            s.deferred.entry(row_clock(rm, &self.actors)).or_insert_with(HashSet::new).extend(ms);
+        }
+        s
+    }
+}
+
+impl<M: Member, A: Actor> BatchCvRDT for Orswot<M, A> {
+    fn lub_many(ctx: &GpuCtx, replicas: Vec<Self>) -> Result<Self, GpuError> {
+        if replicas.is_empty() {
+            return Ok(Orswot::new());
+        }
+        let d = OrswotDense::of(replicas.iter());
+        let (r, a, m) = (replicas.len(), d.actors.width(), d.members.width());
+        let mw = (m + 63) / 64;
+        let (mut clock, mut entries, mut dcl, mut dmb) = (Vec::new(), Vec::new(), Vec::new(), Vec::new());
+        for s in &replicas {
+            let (c, e, x, y) = d.ingest(s);
+            clock.extend(c);
+            entries.extend(e);
+            dcl.extend(x);
+            dmb.extend(y);
+        }
+        let nd = dcl.len() / a;
+        let def_off: [usize; 2] = [0, nd];
+        let (dc, de) = (DeviceBuf::from_host(&clock)?, DeviceBuf::from_host(&entries)?);
+        let (ddc, ddm) = (DeviceBuf::from_host(&dcl)?, DeviceBuf::from_host(&dmb)?);
+        let (oc, oe) = (DeviceBuf::<u64>::zeroed(a)?, DeviceBuf::<u64>::zeroed(m * a)?);
+        let (ok, om) = (DeviceBuf::<u8>::zeroed(nd)?, DeviceBuf::<u64>::zeroed(nd * mw)?);
+        let batch = ffi::crdt_orswot_batch {
+            G: 1, R: r, M: m, A: a,
+            clock: dc.as_ptr(), clock_rstride: a, clock_gstride: r * a,
+            entries: de.as_ptr(), entry_mstride: a, entry_rstride: m * a, entry_gstride: r * m * a,
+            def_off: def_off.as_ptr(), def_clock: ddc.as_ptr(), def_members: ddm.as_ptr(),
+        };
+        let mut out = ffi::crdt_orswot_out {
+            clock: oc.as_mut_ptr(), entries: oe.as_mut_ptr(), def_keep: ok.as_mut_ptr(), def_members: om.as_mut_ptr(),
+        };
+        ctx.check(unsafe { ffi::crdt_orswot_lub_many(ctx.raw, &batch, &mut out) })?;
+        let (c, e, keep, mem) = (oc.to_host()?, oe.to_host()?, ok.to_host()?, om.to_host()?);
+        let mut surv = Vec::new();
+        for i in 0..nd {
+            if keep[i] != 0 {
+                surv.push((dcl[i * a..(i + 1) * a].to_vec(), mem[i * mw..(i + 1) * mw].to_vec()));
+            }
+        }
+        Ok(d.egress(&c, &e, &surv))
+    }
+
+    fn merge_batch(ctx: &GpuCtx, selves: &mut [Self], others: Vec<Self>) -> Result<(), GpuError> {
+        let n = selves.len().min(others.len());
+        if n == 0 {
+            return Ok(());
+        }
+        let d = OrswotDense::of(selves[..n].iter().chain(others[..n].iter()));
+        let (a, m) = (d.actors.width(), d.members.width());
+        let mw = (m + 63) / 64;
+        let dcap_o = others[..n].iter().map(|s| s.deferred.len()).max().unwrap_or(0).max(1);
+        let dcap_s = selves[..n].iter().map(|s| s.deferred.len()).max().unwrap_or(0).max(1) + dcap_o;
+        // per-state deferred slots (the crdt_orswot_states layout)
+        let side = |states: &[Self], dcap: usize| {
+            let (mut c, mut e) = (Vec::with_capacity(n * a), Vec::with_capacity(n * m * a));
+            let (mut dc, mut dm, mut cnt) = (vec![0u64; n * dcap * a], vec![0u64; n * dcap * mw], vec![0u32; n]);
+            for (i, s) in states.iter().enumerate() {
+                let (x, y, rows, bits) = d.ingest(s);
+                c.extend(x);
+                e.extend(y);
+                let k = rows.len() / a;
+                dc[i * dcap * a..i * dcap * a + k * a].copy_from_slice(&rows);
+                dm[i * dcap * mw..i * dcap * mw + k * mw].copy_from_slice(&bits);
+                cnt[i] = k as u32;
+            }
+            (c, e, dc, dm, cnt)
+        };
+        let (sc, se, sdc, sdm, scnt) = side(&selves[..n], dcap_s);
+        let (oc, oe, odc, odm, ocnt) = side(&others[..n], dcap_o);
+        let bufs_s = (DeviceBuf::from_host(&sc)?, DeviceBuf::from_host(&se)?, DeviceBuf::from_host(&sdc)?,
+                      DeviceBuf::from_host(&sdm)?, DeviceBuf::from_host(&scnt)?);
+        let bufs_o = (DeviceBuf::from_host(&oc)?, DeviceBuf::from_host(&oe)?, DeviceBuf::from_host(&odc)?,
+                      DeviceBuf::from_host(&odm)?, DeviceBuf::from_host(&ocnt)?);
+        let st = |b: &(DeviceBuf<u64>, DeviceBuf<u64>, DeviceBuf<u64>, DeviceBuf<u64>, DeviceBuf<u32>), dcap: usize| {
+            ffi::crdt_orswot_states {
+                N: n, M: m, A: a, Dcap: dcap,
+                clock: b.0.as_mut_ptr(), clock_stride: a,
+                entries: b.1.as_mut_ptr(), entry_mstride: a, entry_sstride: m * a,
+                def_clock: b.2.as_mut_ptr(), def_members: b.3.as_mut_ptr(), def_count: b.4.as_mut_ptr(),
+            }
+        };
+        let (ss, os) = (st(&bufs_s, dcap_s), st(&bufs_o, dcap_o));
+        let status = DeviceBuf::<u32>::zeroed(n)?;
+        ctx.check(unsafe { ffi::crdt_orswot_merge_batch(ctx.raw, &ss, &os, status.as_mut_ptr()) })?;
+        let (c, e, dc, dm, cnt, stv) = (bufs_s.0.to_host()?, bufs_s.1.to_host()?, bufs_s.2.to_host()?,
+                                         bufs_s.3.to_host()?, bufs_s.4.to_host()?, status.to_host()?);
+        for i in 0..n {
+            if stv[i] != 0 {
+                return Err(GpuError { code: ffi::CRDT_EUNSUPPORTED, msg: format!("orswot merge_batch status {}", stv[i]) });
+            }
+            let mut defs = Vec::new();
+            for k in 0..cnt[i] as usize {
+                let base = i * dcap_s + k;
+                defs.push((dc[base * a..(base + 1) * a].to_vec(), dm[base * mw..(base + 1) * mw].to_vec()));
+            }
+            selves[i] = d.egress(&c[i * a..(i + 1) * a], &e[i * m * a..(i + 1) * m * a], &defs);
+        }
+        Ok(())
+    }
+}

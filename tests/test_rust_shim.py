@@ -1,0 +1,127 @@
+"""The committed Rust binding (rust/src/gpu/: the `gpu` module + build.rs the crate would add) must
+match include/crdt_gpu.h.  No Rust toolchain exists in this image, so this is the check that keeps
+the binding honest (the markdown stub had drifted, `crdt_lwwreg_lub_many` lost its
+`flags` argument):
+  * ffi.rs is exactly what scripts/gen_rust_ffi.py generates from the header;
+  * every header function is declared with the same arity and the mapped types, every struct with
+    the same fields in the same order;
+  * every `ffi::crdt_*(...)` call in the safe layer passes as many arguments as the declaration
+    takes, and every `ffi::<struct> { ... }` literal names every field of that struct."""
+import os
+import re
+import subprocess
+import sys
+
+import pytest
+
+import rust_ffi_map as F
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = open(os.path.join(ROOT, "include", "crdt_gpu.h")).read()
+FFI = open(os.path.join(ROOT, "rust", "src", "gpu", "ffi.rs")).read()
+MOD = open(os.path.join(ROOT, "rust", "src", "gpu", "mod.rs")).read()
+
+
+def test_ffi_is_generated_from_the_header(tmp_path):
+    import shutil
+    work = tmp_path / "repo"
+    for d in ("include", "scripts", "tests"):
+        shutil.copytree(os.path.join(ROOT, d), work / d, ignore=shutil.ignore_patterns("__pycache__", "golden"))
+    subprocess.run([sys.executable, str(work / "scripts" / "gen_rust_ffi.py")], check=True, capture_output=True)
+    assert (work / "rust" / "src" / "gpu" / "ffi.rs").read_text() == FFI, \
+        "rust/src/gpu/ffi.rs is stale: run python scripts/gen_rust_ffi.py"
+
+
+def test_every_function_and_struct_matches():
+    consts, structs, funcs = F.parse_header(HEADER)
+    rstructs, rfuncs = F.parse_rust_ffi(FFI)
+    assert {n for _, n, _ in funcs} == set(rfuncs)
+    for ret, name, params in funcs:
+        rparams, rret = rfuncs[name]
+        assert len(rparams) == len(params), name
+        assert rparams == [F.rust_type(t) for t, _ in params], name
+        assert rret == F.rust_type(ret), name
+    assert {n for n, _ in structs} | {"crdt_ctx"} == set(rstructs)
+    for sname, fields in structs:
+        assert [f for f, _ in rstructs[sname]] == [F.rust_field(n) for _, n in fields], sname
+        assert [t for _, t in rstructs[sname]] == [F.rust_type(t) for t, _ in fields], sname
+    # the ctypes binding and the Rust binding cover the same ABI
+    sys.path.insert(0, os.path.join(ROOT, "rust-crdt_amd"))
+    from crdts_gpu import _abi
+    assert set(_abi.EXPORTS) == set(rfuncs)
+
+
+def test_known_signatures():
+    _, rfuncs = F.parse_rust_ffi(FFI)
+    args, ret = rfuncs["crdt_lwwreg_lub_many"]
+    assert len(args) == 10 and args[-1] == "c_uint" and ret == "c_int"  # the `flags` argument
+    assert rfuncs["crdt_ctx_create"][0] == ["c_int", "*mut *mut crdt_ctx"]
+    assert rfuncs["crdt_last_error"] == (["*const crdt_ctx"], "*const c_char")
+
+
+def _call_args(text, start):
+    """Top-level argument count of the call whose '(' is at text[start]."""
+    depth, n, i, nonblank = 0, 0, start, False
+    while True:
+        ch = text[i]
+        if ch in "([{":
+            depth += 1
+            if depth > 1:
+                nonblank = True
+        elif ch in ")]}":
+            depth -= 1
+            if depth == 0:
+                return n + (1 if nonblank else 0)
+        elif ch == "," and depth == 1:
+            n += 1
+        elif not ch.isspace() and depth >= 1:
+            nonblank = True
+        i += 1
+
+
+def test_safe_layer_calls_match_the_declarations():
+    _, rfuncs = F.parse_rust_ffi(FFI)
+    calls = list(re.finditer(r"ffi::(crdt_\w+)\(", MOD))
+    assert len(calls) >= 15
+    for m in calls:
+        name = m.group(1)
+        assert name in rfuncs, name
+        assert _call_args(MOD, m.end() - 1) == len(rfuncs[name][0]), name
+
+
+def test_struct_literals_name_every_field():
+    rstructs, _ = F.parse_rust_ffi(FFI)
+    lits = list(re.finditer(r"ffi::(crdt_\w+) \{", MOD))
+    assert lits
+    for m in lits:
+        i, depth = m.end() - 1, 0
+        j = i
+        while True:
+            if MOD[j] == "{":
+                depth += 1
+            elif MOD[j] == "}":
+                depth -= 1
+                if depth == 0:
+                    break
+            j += 1
+        body = re.sub(r"\([^()]*\)", "", MOD[i + 1:j])  # drop call arguments before splitting
+        names = {p.split(":", 1)[0].strip() for p in body.split(",") if ":" in p}
+        assert names == {f for f, _ in rstructs[m.group(1)]}, m.group(1)
+
+
+@pytest.mark.parametrize("path", ["rust/build.rs", "rust/src/gpu/mod.rs", "rust/src/gpu/hip.rs"])
+def test_rust_sources_balanced(path):
+    """Cheap syntax sanity without rustc: balanced delimiters outside strings and comments."""
+    src = open(os.path.join(ROOT, path)).read()
+    src = re.sub(r"//[^\n]*", "", src)
+    src = re.sub(r'"(\\.|[^"\\])*"', '""', src)
+    src = re.sub(r"'(\\.|[^'\\])'", "''", src)
+    stack = []
+    pairs = {")": "(", "]": "[", "}": "{"}
+    for ch in src:
+        if ch in "([{":
+            stack.append(ch)
+        elif ch in ")]}":
+            assert stack and stack[-1] == pairs[ch], path
+            stack.pop()
+    assert not stack, path
