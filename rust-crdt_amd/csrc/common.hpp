@@ -51,6 +51,7 @@ struct Tune {
   int lub_nt = 1;
   int orswot_blocks_per_cu = 2;
   int orswot_unroll = 1;
+  int orswot_mpt = 4;  // member rows per thread of the join (4, 8, 16)
   int merge_blocks_per_cu = 2;
   int merge_rows = 1;  // merge_batch of 16-byte rows by LR-lane row groups (0: merge_pairs_kernel)
   int map_glds = 1;    // Map fold: LDS-DMA staging where the shape allows it
@@ -136,6 +137,9 @@ struct DefPlan {
   unsigned *nsurv;    // counter
   uint8_t *out_keep;
   u64 *out_members;
+  u64 *tkey;          // dedup table: keys (0 = empty) [tmask+1]
+  unsigned *trep;     // ... min survivor index per key
+  unsigned long long tmask;
 };
 int launch_deferred(crdt_ctx *ctx, const size_t *host_def_off, DefPlan q);
 

@@ -202,6 +202,7 @@ static void apply_tune(crdt_ctx *ctx, const char *t) {
       else if (k == "mrows" && (v == 0 || v == 1)) ctx->tune.merge_rows = v;
       else if (k == "obpc" && v > 0) ctx->tune.orswot_blocks_per_cu = v;
       else if (k == "ounroll" && (v == 1 || v == 2 || v == 4)) ctx->tune.orswot_unroll = v;
+      else if (k == "ompt" && (v == 4 || v == 8 || v == 16)) ctx->tune.orswot_mpt = v;
       else if (k == "mglds") ctx->tune.map_glds = v != 0;
       else if (k == "mchunk" && (v == 8 || v == 16)) ctx->tune.map_chunk = v;
       else if (k == "mring" && v >= 2 && v <= 4) ctx->tune.map_ring = v;

@@ -20,7 +20,6 @@
 
 namespace crdt {
 
-constexpr int kOrMPT = 4;  // members per thread
 
 template <int V>
 struct OVec;
@@ -66,8 +65,12 @@ struct OrPlan {
   u64 *out_entries;  // [G][M][A]
 };
 
-template <int V, int UR>
+// MPT member rows per thread (CRDT_TUNE ompt=4/8/16): a workgroup covers MB*MPT member rows of
+// PW actor vectors, so MPT sets the bytes in flight per thread and how many workgroups re-read
+// each replica clock row.
+template <int V, int UR, int MPT>
 __global__ __launch_bounds__(kBlock) void orswot_join_kernel(OrPlan p) {
+  constexpr int kOrMPT = MPT;
   using VT = typename OVec<V>::T;
   __shared__ int s_flag;
   const int l = threadIdx.x;
@@ -246,25 +249,60 @@ __global__ __launch_bounds__(kBlock) void orswot_deferred_kernel(DefPlan p) {
   }
 }
 
-// One thread per survivor: representative = smallest survivor index of the same group with
-// an identical rm clock; OR its member set into the representative's output row.
+// Survivors with identical rm clocks (and group) must find their representative, the smallest
+// such index.  Open-addressing table keyed by the row hash mixed with the group: pass 1 inserts
+// every survivor and keeps the minimum index per key (atomicMin), pass 2 looks its key up and
+// verifies the candidate's clock exactly; only a true 64-bit collision (two different clocks, same
+// key) falls back to a scan of the survivor list.  O(survivors), not O(survivors^2).
+__device__ __forceinline__ u64 dedup_key(u64 h, unsigned long long g) {
+  u64 z = h ^ ((g + 1) * 0x9E3779B97F4A7C15ULL);
+  z = (z ^ (z >> 31)) * 0xD6E8FEB86659FD93ULL;
+  z ^= z >> 32;
+  return z ? z : 1;  // 0 marks an empty slot
+}
+
+__device__ __forceinline__ unsigned long long dedup_slot(const DefPlan &p, u64 key, bool insert, unsigned d) {
+  unsigned long long t = key & p.tmask;
+  while (true) {
+    const u64 cur = insert ? atomicCAS(p.tkey + t, 0ull, key) : p.tkey[t];
+    if (cur == key || (insert && cur == 0)) return t;
+    if (!insert && cur == 0) return ~0ull;  // not found: cannot happen for an inserted key
+    t = (t + 1) & p.tmask;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void orswot_dedup_insert_kernel(DefPlan p) {
+  const unsigned k = blockIdx.x * blockDim.x + threadIdx.x;
+  const unsigned n = *p.nsurv;
+  if (k >= n) return;
+  const unsigned d = p.surv[k];
+  const u64 key = dedup_key(p.hash[d], group_of(p.def_off, p.G, d));
+  atomicMin(p.trep + dedup_slot(p, key, true, d), d);
+}
+
 __global__ __launch_bounds__(kBlock) void orswot_dedup_kernel(DefPlan p) {
   const unsigned k = blockIdx.x * blockDim.x + threadIdx.x;
   const unsigned n = *p.nsurv;
   if (k >= n) return;
   const unsigned d = p.surv[k];
   const unsigned long long g = group_of(p.def_off, p.G, d);
-  const u64 h = p.hash[d];
+  const u64 key = dedup_key(p.hash[d], g);
+  const unsigned long long t = dedup_slot(p, key, false, d);
   const u64 *rm = p.def_clock + (size_t)d * p.A;
-  unsigned rep = d;
-  for (unsigned j = 0; j < n; ++j) {
-    const unsigned d2 = p.surv[j];
-    if (d2 >= rep || p.hash[d2] != h) continue;
-    if (d2 < p.def_off[g] || d2 >= p.def_off[g + 1]) continue;
+  auto same = [&](unsigned d2) {
+    if (d2 < p.def_off[g] || d2 >= p.def_off[g + 1]) return false;
     const u64 *rm2 = p.def_clock + (size_t)d2 * p.A;
-    bool eq = true;
-    for (unsigned long long a = 0; a < p.A && eq; ++a) eq = rm[a] == rm2[a];
-    if (eq) rep = d2;
+    for (unsigned long long a = 0; a < p.A; ++a)
+      if (rm[a] != rm2[a]) return false;
+    return true;
+  };
+  unsigned rep = t == ~0ull ? d : p.trep[t];
+  if (rep != d && !same(rep)) {  // a true key collision: exact scan of the survivors
+    rep = d;
+    for (unsigned j = 0; j < n; ++j) {
+      const unsigned d2 = p.surv[j];
+      if (d2 < rep && p.hash[d2] == p.hash[d] && same(d2)) rep = d2;
+    }
   }
   if (rep == d) p.out_keep[d] = 1;
   const u64 *src = p.def_members + (size_t)d * p.Mw;
@@ -282,13 +320,21 @@ int launch_deferred(crdt_ctx *ctx, const size_t *host_def_off, DefPlan q) {
   // Deferred bookkeeping lives in its own ctx-owned region (plain hipMalloc, like scratch), so
   // the join's scratch, possibly still in flight, is untouched.
   const size_t off_b = (G + 1) * sizeof(size_t);
-  const size_t need = 256 + ((off_b + 255) / 256 * 256) + D * 8 + D * 4;
+  size_t T = 64;
+  while (T < 2 * D) T <<= 1;  // dedup table: load factor <= 1/2
+  const size_t off_pad = (off_b + 255) / 256 * 256;
+  const size_t need = 256 + off_pad + D * 8 + D * 4 + 64 + T * 12;
   if (int rc = ensure_dscratch(ctx, need)) return rc;
   char *base = static_cast<char *>(ctx->dscratch);
   q.nsurv = reinterpret_cast<unsigned *>(base);
   q.def_off = reinterpret_cast<const size_t *>(base + 256);
-  q.hash = reinterpret_cast<u64 *>(base + 256 + (off_b + 255) / 256 * 256);
+  q.hash = reinterpret_cast<u64 *>(base + 256 + off_pad);
   q.surv = reinterpret_cast<unsigned *>(q.hash + D);
+  q.tkey = reinterpret_cast<u64 *>(base + ((256 + off_pad + D * 12 + 63) / 64 * 64));
+  q.trep = reinterpret_cast<unsigned *>(q.tkey + T);
+  q.tmask = T - 1;
+  if (int rc = device_fill(ctx, q.tkey, T * 8, 0)) return rc;
+  if (int rc = device_fill(ctx, q.trep, T * 4, 0xFF)) return rc;
   if (int rc = device_fill(ctx, q.nsurv, 4, 0)) return rc;
   {  // the caller's def_off may be freed on return: stage it through pinned ctx memory
     int rc = stage_h2d(ctx, (void *)q.def_off, host_def_off, off_b);
@@ -297,6 +343,8 @@ int launch_deferred(crdt_ctx *ctx, const size_t *host_def_off, DefPlan q) {
   if (int rc = device_fill(ctx, q.out_keep, D, 0)) return rc;
   if (int rc = device_fill(ctx, q.out_members, D * q.Mw * 8, 0)) return rc;
   hipLaunchKernelGGL(orswot_deferred_kernel, dim3((unsigned)D), dim3(kBlock), 0, ctx->stream, q);
+  hipLaunchKernelGGL(orswot_dedup_insert_kernel, dim3((unsigned)((D + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                     ctx->stream, q);
   hipLaunchKernelGGL(orswot_dedup_kernel, dim3((unsigned)((D + kBlock - 1) / kBlock)), dim3(kBlock), 0,
                      ctx->stream, q);
   CRDT_HIP(ctx, hipGetLastError());
@@ -355,7 +403,8 @@ extern "C" int crdt_orswot_lub_many(crdt_ctx *ctx, const crdt_orswot_batch *in,
     p.PW = p.Wv <= kBlock ? p.Wv : kBlock;
     p.MB = kBlock / p.PW;
     p.ncolblk = (p.Wv + kBlock - 1) / kBlock;
-    const size_t mpb = (size_t)p.MB * kOrMPT;
+    const int MPT = ctx->tune.orswot_mpt == 8 ? 8 : (ctx->tune.orswot_mpt == 16 ? 16 : 4);
+    const size_t mpb = (size_t)p.MB * MPT;
     p.nmblk = (int)((M + mpb - 1) / mpb);
     p.out_clock = (u64 *)out->clock;
     p.out_entries = (u64 *)out->entries;
@@ -386,13 +435,22 @@ extern "C" int crdt_orswot_lub_many(crdt_ctx *ctx, const crdt_orswot_batch *in,
     timing_begin(ctx, "orswot_join");
     const dim3 grid((unsigned)(units * S));
     const int UR = ctx->tune.orswot_unroll;
+#define CRDT_ORJ(VV, UU, MM) hipLaunchKernelGGL((orswot_join_kernel<VV, UU, MM>), grid, dim3(kBlock), 0, ctx->stream, p)
     if (V == 2) {
-      if (UR == 1) hipLaunchKernelGGL((orswot_join_kernel<2, 1>), grid, dim3(kBlock), 0, ctx->stream, p);
-      else if (UR == 4) hipLaunchKernelGGL((orswot_join_kernel<2, 4>), grid, dim3(kBlock), 0, ctx->stream, p);
-      else hipLaunchKernelGGL((orswot_join_kernel<2, 2>), grid, dim3(kBlock), 0, ctx->stream, p);
+      if (MPT == 4) {
+        if (UR == 1) CRDT_ORJ(2, 1, 4);
+        else if (UR == 4) CRDT_ORJ(2, 4, 4);
+        else CRDT_ORJ(2, 2, 4);
+      } else if (MPT == 8) {
+        if (UR == 1) CRDT_ORJ(2, 1, 8);
+        else CRDT_ORJ(2, 2, 8);
+      } else {
+        CRDT_ORJ(2, 1, 16);
+      }
     } else {
-      hipLaunchKernelGGL((orswot_join_kernel<1, 2>), grid, dim3(kBlock), 0, ctx->stream, p);
+      CRDT_ORJ(1, 2, 4);
     }
+#undef CRDT_ORJ
     timing_end(ctx);
     CRDT_HIP(ctx, hipGetLastError());
   }
