@@ -490,6 +490,56 @@ int crdt_pncounter_apply_batch(crdt_ctx *ctx, uint64_t *states, size_t N, size_t
 int crdt_gset_apply_batch(crdt_ctx *ctx, uint64_t *states, size_t N, size_t U, size_t row_stride,
                           const uint32_t *state_idx, const uint32_t *element, size_t n_ops, uint32_t *bad);
 
+/* ---- serde wire format ingest / egress -------------------------------------
+ * Replicas ship whole states serialized through the serde derives of the reference types
+ * (vclock.rs:56, gcounter.rs:25, pncounter.rs:28, gset.rs:7, lwwreg.rs:13, orswot.rs:20).  These
+ * entry points read / write the bytes `bincode::serialize` (bincode 1.x default options) produces:
+ * little-endian fixed-width integers, a struct = its fields in order, a map / set / Vec = u64 length
+ * then its entries (key, value).  Instantiations: actors u32, members / set elements u64:
+ *   VClock<u32> = GCounter<u32>: u64 n, n x (u32 actor, u64 counter)        (actors ascending)
+ *   PNCounter<u32>: GCounter p then GCounter n
+ *   GSet<u64>: u64 n, n x u64 (ascending);  LWWReg<u64, u64>: u64 val, u64 marker
+ *   Orswot<u64, u32>: VClock clock; u64 n, n x (u64 member, VClock); u64 d, d x (VClock rm,
+ *       u64 k, k x u64 member)                     (HashMap / HashSet: any order on input)
+ * Frames (device): state s is bytes[frame_off[s] .. frame_off[s+1]), offsets 4-byte aligned.
+ * Dictionaries (device, ascending, unique): the dense column / bit / row of an id is its position.
+ * status[s] (device u32): bit 0 = malformed frame (truncated, trailing bytes, misaligned), bit 1 = an
+ * id missing from its dictionary (skipped), bit 2 = more deferred removes than def_cap.
+ * Egress writes the same format (maps in ascending dictionary order) and the frame offsets
+ * (device, N+1); it always returns the byte total in *total (host, synchronises) and writes the
+ * bytes only when `bytes` is non-NULL and cap >= *total (call once with NULL to size a buffer).
+ * Limits: A <= 4096 (VClock family), ceil(U/64) <= 4096, A + ceil(M/64) <= 4096 (Orswot). */
+int crdt_vclock_ingest(crdt_ctx *ctx, const uint8_t *bytes, const uint64_t *frame_off, size_t N,
+                       const uint32_t *actors, size_t A, uint64_t *out, size_t row_stride, uint32_t *status);
+int crdt_pncounter_ingest(crdt_ctx *ctx, const uint8_t *bytes, const uint64_t *frame_off, size_t N,
+                          const uint32_t *actors, size_t A, uint64_t *out, size_t row_stride, uint32_t *status);
+int crdt_gset_ingest(crdt_ctx *ctx, const uint8_t *bytes, const uint64_t *frame_off, size_t N,
+                     const uint64_t *elems, size_t U, uint64_t *out, size_t row_stride, uint32_t *status);
+int crdt_lwwreg_ingest(crdt_ctx *ctx, const uint8_t *bytes, const uint64_t *frame_off, size_t N,
+                       uint64_t *marker, uint64_t *val, uint32_t *status);
+/* Orswot: clock [N][A], entries [N][M][A] (zero-filled, then the present members' rows), the
+ * deferred removes pooled in state order: def_off [N+1] (device, written), rows d < def_cap of
+ * def_clock [D][A] / def_members [D][ceil(M/64)], *n_def = D (host). */
+int crdt_orswot_ingest(crdt_ctx *ctx, const uint8_t *bytes, const uint64_t *frame_off, size_t N,
+                       const uint32_t *actors, size_t A, const uint64_t *members, size_t M, uint64_t *clock,
+                       uint64_t *entries, uint64_t *def_off, uint64_t *def_clock, uint64_t *def_members,
+                       size_t def_cap, size_t *n_def, uint32_t *status);
+int crdt_vclock_egress(crdt_ctx *ctx, const uint64_t *rows, size_t N, size_t A, size_t row_stride,
+                       const uint32_t *actors, uint64_t *frame_off, uint8_t *bytes, size_t cap, size_t *total);
+int crdt_pncounter_egress(crdt_ctx *ctx, const uint64_t *rows, size_t N, size_t A, size_t row_stride,
+                          const uint32_t *actors, uint64_t *frame_off, uint8_t *bytes, size_t cap, size_t *total);
+int crdt_gset_egress(crdt_ctx *ctx, const uint64_t *rows, size_t N, size_t U, size_t row_stride,
+                     const uint64_t *elems, uint64_t *frame_off, uint8_t *bytes, size_t cap, size_t *total);
+/* 16 bytes per state at bytes + 16*s (val, marker). */
+int crdt_lwwreg_egress(crdt_ctx *ctx, const uint64_t *marker, const uint64_t *val, size_t N, uint8_t *bytes);
+/* Orswot states (clock [N][A], entries [N][M][A] packed) and their deferred removes pooled by state
+ * (def_off device [N+1] or NULL = none; def_keep [D] or NULL = all kept): the lub_many output
+ * shape with def_off as a device array. */
+int crdt_orswot_egress(crdt_ctx *ctx, const uint64_t *clock, const uint64_t *entries, size_t N, size_t M, size_t A,
+                       const uint32_t *actors, const uint64_t *members, const uint64_t *def_off,
+                       const uint64_t *def_clock, const uint64_t *def_members, const uint8_t *def_keep,
+                       uint64_t *frame_off, uint8_t *bytes, size_t cap, size_t *total);
+
 /* ---- synthetic inputs (bench / test data, generated in HBM) --------------------------------
  * Counter-based and reproducible on the CPU (oracle/oracle.py synth_* restates them; small
  * fixtures of both are pinned by tests/golden/make_golden.py -> tests/golden/synth.json).

@@ -1438,3 +1438,98 @@ def restrict_deferred_keys(def_keys: np.ndarray, keys) -> np.ndarray:
         bit = (def_keys[:, k // 64] >> np.uint64(k % 64)) & np.uint64(1)
         out[:, i // 64] |= bit << np.uint64(i % 64)
     return out
+
+
+# ---------------------------------------------------------------------------------------
+# bincode 1.x (default options) restatement of the serde derives, used by
+# tests/test_*wire*.py to build and check the frames crdt_*_ingest / _egress read and write.
+# Published encoding: little-endian fixed-width integers; a struct is its fields in order; a
+# map / set / Vec is a u64 length then its entries (key, value).  The reference types'
+# derives: VClock { dots: BTreeMap<A, u64> } (vclock.rs:56-60), GCounter { inner } (gcounter.rs:25-28),
+# PNCounter { p, n } (pncounter.rs:28-32), GSet { value: BTreeSet } (gset.rs:7-10),
+# LWWReg { val, marker } (lwwreg.rs:13-19), Orswot { clock, entries: HashMap<M, VClock>,
+# deferred: HashMap<VClock, HashSet<M>> } (orswot.rs:20-25).  Actors u32, members / elements u64.
+# Parity of the byte format itself is unpinned (the reference ships no serialized fixtures and
+# bincode is not among its dependencies); the semantic round trips are pinned by the KATs.
+# ---------------------------------------------------------------------------------------
+import struct as _st
+
+
+def bc_vclock(dots) -> bytes:
+    items = sorted((int(a), int(c)) for a, c in dict(dots).items() if c)
+    return _st.pack("<Q", len(items)) + b"".join(_st.pack("<IQ", a, c) for a, c in items)
+
+
+def bc_pncounter(p, n) -> bytes:
+    return bc_vclock(p) + bc_vclock(n)
+
+
+def bc_gset(values) -> bytes:
+    v = sorted(int(x) for x in values)
+    return _st.pack("<Q", len(v)) + b"".join(_st.pack("<Q", x) for x in v)
+
+
+def bc_lwwreg(val, marker) -> bytes:
+    return _st.pack("<QQ", int(val), int(marker))
+
+
+def bc_orswot(clock, entries, deferred, order=None) -> bytes:
+    """clock {a: c}; entries {m: {a: c}}; deferred [(rm {a: c}, members)].  `order` (optional)
+    permutes the entries (a HashMap serializes in any order)."""
+    ms = list(entries) if order is None else order
+    out = bc_vclock(clock) + _st.pack("<Q", len(ms))
+    for m in ms:
+        out += _st.pack("<Q", int(m)) + bc_vclock(entries[m])
+    out += _st.pack("<Q", len(deferred))
+    for rm, members in deferred:
+        mem = list(members)
+        out += bc_vclock(rm) + _st.pack("<Q", len(mem)) + b"".join(_st.pack("<Q", int(x)) for x in mem)
+    return out
+
+
+def unbc_vclock(b: bytes, pos: int = 0):
+    (n,) = _st.unpack_from("<Q", b, pos)
+    pos += 8
+    dots = {}
+    for _ in range(n):
+        a, c = _st.unpack_from("<IQ", b, pos)
+        dots[a] = c
+        pos += 12
+    return dots, pos
+
+
+def unbc_gset(b: bytes, pos: int = 0):
+    (n,) = _st.unpack_from("<Q", b, pos)
+    vals = [_st.unpack_from("<Q", b, pos + 8 + 8 * i)[0] for i in range(n)]
+    return set(vals), pos + 8 + 8 * n
+
+
+def unbc_orswot(b: bytes, pos: int = 0):
+    """-> (clock, entries {m: dots}, deferred {tuple(sorted rm items): set(members)}, pos); removes
+    with the same clock merge their sets, as the HashMap<VClock, HashSet<M>> does."""
+    clock, pos = unbc_vclock(b, pos)
+    (n,) = _st.unpack_from("<Q", b, pos)
+    pos += 8
+    entries = {}
+    for _ in range(n):
+        (m,) = _st.unpack_from("<Q", b, pos)
+        entries[m], pos = unbc_vclock(b, pos + 8)
+    (d,) = _st.unpack_from("<Q", b, pos)
+    pos += 8
+    deferred = {}
+    for _ in range(d):
+        rm, pos = unbc_vclock(b, pos)
+        (k,) = _st.unpack_from("<Q", b, pos)
+        mem = {_st.unpack_from("<Q", b, pos + 8 + 8 * i)[0] for i in range(k)}
+        pos += 8 + 8 * k
+        deferred.setdefault(tuple(sorted(rm.items())), set()).update(mem)
+    return clock, entries, deferred, pos
+
+
+def frames(blobs, align: int = 4):
+    """Concatenate frames (each padded to `align` bytes by construction) -> (bytes, offsets)."""
+    off = [0]
+    for x in blobs:
+        assert len(x) % align == 0
+        off.append(off[-1] + len(x))
+    return b"".join(blobs), off

@@ -39,6 +39,8 @@ EXPORTS = (
     "crdt_vclock_lub_many_sharded", "crdt_gcounter_lub_many_sharded", "crdt_pncounter_lub_many_sharded",
     "crdt_gset_lub_many_sharded", "crdt_orswot_lub_many_sharded",
     "crdt_lwwreg_lub_many_sharded", "crdt_map_lub_many_sharded",
+    "crdt_vclock_ingest", "crdt_pncounter_ingest", "crdt_gset_ingest", "crdt_lwwreg_ingest", "crdt_orswot_ingest",
+    "crdt_vclock_egress", "crdt_pncounter_egress", "crdt_gset_egress", "crdt_lwwreg_egress", "crdt_orswot_egress",
     "crdt_orswot_forget_batch", "crdt_map_forget_batch", "crdt_map_apply_batch",
     "crdt_orswot_merge_batch", "crdt_map_merge_batch",
 )
@@ -165,6 +167,16 @@ _SIGS.update({
                               ctypes.POINTER(MapDeferred), P], ctypes.c_int),
     "crdt_lwwreg_lub_many_sharded": ([P, P, P, S, S, S, U64, P, P, P], ctypes.c_int),
     "crdt_map_lub_many_sharded": ([P, ctypes.POINTER(MapBatch), S, S, ctypes.POINTER(MapOut)], ctypes.c_int),
+    "crdt_vclock_ingest": ([P, P, P, S, P, S, P, S, P], ctypes.c_int),
+    "crdt_pncounter_ingest": ([P, P, P, S, P, S, P, S, P], ctypes.c_int),
+    "crdt_gset_ingest": ([P, P, P, S, P, S, P, S, P], ctypes.c_int),
+    "crdt_lwwreg_ingest": ([P, P, P, S, P, P, P], ctypes.c_int),
+    "crdt_orswot_ingest": ([P, P, P, S, P, S, P, S, P, P, P, P, P, S, ctypes.POINTER(S), P], ctypes.c_int),
+    "crdt_vclock_egress": ([P, P, S, S, S, P, P, P, S, ctypes.POINTER(S)], ctypes.c_int),
+    "crdt_pncounter_egress": ([P, P, S, S, S, P, P, P, S, ctypes.POINTER(S)], ctypes.c_int),
+    "crdt_gset_egress": ([P, P, S, S, S, P, P, P, S, ctypes.POINTER(S)], ctypes.c_int),
+    "crdt_lwwreg_egress": ([P, P, P, S, P], ctypes.c_int),
+    "crdt_orswot_egress": ([P, P, P, S, S, S, P, P, P, P, P, P, P, P, S, ctypes.POINTER(S)], ctypes.c_int),
     "crdt_comm_unique_id": ([P], ctypes.c_int),
     "crdt_ctx_comm_init": ([P, P, ctypes.c_int, ctypes.c_int], ctypes.c_int),
     "crdt_ctx_comm_destroy": ([P], ctypes.c_int),

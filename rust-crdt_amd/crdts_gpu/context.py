@@ -82,10 +82,13 @@ class Context:
         self.call("crdt_ctx_tune", spec.encode())
 
     # -- tensor checks ----------------------------------------------------------------------
-    def check_tensor(self, t: torch.Tensor, what: str) -> None:
+    def check_tensor(self, t: torch.Tensor, what: str, dtypes=None) -> None:
         if not isinstance(t, torch.Tensor):
             raise TypeError(f"{what}: expected a torch.Tensor")
-        if t.dtype not in U64_DTYPES:
+        if dtypes is not None:
+            if t.dtype not in dtypes:
+                raise TypeError(f"{what}: dtype {t.dtype}; expected one of {dtypes}")
+        elif t.dtype not in U64_DTYPES:
             raise TypeError(f"{what}: dtype {t.dtype}; expected int64/uint64 holding u64 bits")
         if t.device.type != "cuda" or t.device.index != self.device:
             raise ValueError(f"{what}: tensor on {t.device}; expected cuda:{self.device}")

@@ -1,0 +1,195 @@
+"""Serde wire format ingest / egress on the device (include/crdt_gpu.h "serde wire format").
+
+Replicas ship whole serialized states; these calls turn a batch of received frames (the bytes
+`bincode::serialize` writes for VClock / GCounter / PNCounter<u32>, GSet<u64>, LWWReg<u64, u64>,
+Orswot<u64, u32>) into the dense layout the merge kernels read, and merged dense states back into
+frames.  Every tensor is a device tensor: bytes (uint8), frame offsets (int64, N+1, 4-byte
+aligned), dictionaries (sorted ascending: actors int32 holding u32 ids, members / elements int64
+holding u64 ids).  Nothing here runs on the host except the shape checks.
+
+    rows, status = vclock_ingest(bytes, frame_off, actors)          # (N, A), (N,) int32
+    frame_off, data = vclock_egress(rows, actors)                   # (N+1,), (total,) uint8
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import NamedTuple, Optional
+
+import torch
+
+from .context import Context, dptr
+
+BAD, MISSING, CAP = 1, 2, 4  # status bits
+
+
+def _ctx(t: torch.Tensor, ctx: Optional[Context]) -> Context:
+    return ctx or Context.default(t.device.index)
+
+
+def _frames(ctx, data, frame_off, what):
+    ctx.check_tensor(data, f"{what}(bytes)", (torch.uint8,))
+    ctx.check_tensor(frame_off, f"{what}(frame_off)")
+    if data.dtype != torch.uint8 or data.dim() != 1 or not data.is_contiguous():
+        raise ValueError(f"{what}: bytes must be a contiguous uint8 vector")
+    if frame_off.dtype != torch.int64 or frame_off.dim() != 1 or not frame_off.is_contiguous() or frame_off.shape[0] < 1:
+        raise ValueError(f"{what}: frame_off must be a contiguous int64 (N+1,) tensor")
+    return frame_off.shape[0] - 1
+
+
+def _dict(ctx, d, dt, what):
+    ctx.check_tensor(d, what, (dt,))
+    if d.dtype != dt or d.dim() != 1 or not d.is_contiguous() or d.shape[0] == 0:
+        raise ValueError(f"{what}: a non-empty contiguous {dt} dictionary is required")
+    return d.shape[0]
+
+
+def _status(N, dev):
+    return torch.zeros(N, dtype=torch.int32, device=dev)
+
+
+def _ptr_or_dummy(data):
+    return dptr(data) if data.numel() else None
+
+
+def vclock_ingest(data: torch.Tensor, frame_off: torch.Tensor, actors: torch.Tensor, out: Optional[torch.Tensor] = None,
+                  ctx: Optional[Context] = None, _fn: str = "crdt_vclock_ingest", _k: int = 1):
+    """VClock / GCounter frames -> (rows (N, A) int64, status (N,) int32)."""
+    ctx = _ctx(data, ctx)
+    N = _frames(ctx, data, frame_off, "wire.vclock_ingest")
+    A = _dict(ctx, actors, torch.int32, "wire.vclock_ingest(actors)")
+    if out is None:
+        out = torch.empty((N, _k * A), dtype=torch.int64, device=data.device)
+    if out.dim() != 2 or out.shape[0] != N or out.shape[1] < _k * A or out.stride(1) != 1:
+        raise ValueError(f"wire ingest: out must be ({N}, >= {_k * A}) with contiguous rows")
+    st = _status(N, data.device)
+    ctx.call(_fn, _ptr_or_dummy(data), dptr(frame_off), N, dptr(actors), A, dptr(out), out.stride(0), dptr(st))
+    return out, st
+
+
+def pncounter_ingest(data, frame_off, actors, out=None, ctx=None):
+    """PNCounter frames (p then n) -> (rows (N, 2A) = P | N, status)."""
+    return vclock_ingest(data, frame_off, actors, out, ctx, "crdt_pncounter_ingest", 2)
+
+
+def gset_ingest(data: torch.Tensor, frame_off: torch.Tensor, elems: torch.Tensor, out: Optional[torch.Tensor] = None,
+                ctx: Optional[Context] = None):
+    """GSet<u64> frames -> (bitmap rows (N, ceil(U/64)), status)."""
+    ctx = _ctx(data, ctx)
+    N = _frames(ctx, data, frame_off, "wire.gset_ingest")
+    U = _dict(ctx, elems, torch.int64, "wire.gset_ingest(elems)")
+    W = (U + 63) // 64
+    if out is None:
+        out = torch.empty((N, W), dtype=torch.int64, device=data.device)
+    st = _status(N, data.device)
+    ctx.call("crdt_gset_ingest", _ptr_or_dummy(data), dptr(frame_off), N, dptr(elems), U, dptr(out), out.stride(0),
+             dptr(st))
+    return out, st
+
+
+def lwwreg_ingest(data: torch.Tensor, frame_off: torch.Tensor, ctx: Optional[Context] = None):
+    """LWWReg<u64, u64> frames -> (marker (N,), val (N,), status)."""
+    ctx = _ctx(data, ctx)
+    N = _frames(ctx, data, frame_off, "wire.lwwreg_ingest")
+    m = torch.empty(N, dtype=torch.int64, device=data.device)
+    v = torch.empty_like(m)
+    st = _status(N, data.device)
+    ctx.call("crdt_lwwreg_ingest", _ptr_or_dummy(data), dptr(frame_off), N, dptr(m), dptr(v), dptr(st))
+    return m, v, st
+
+
+class OrswotFrames(NamedTuple):
+    clock: torch.Tensor        # (N, A)
+    entries: torch.Tensor      # (N, M, A)
+    def_off: torch.Tensor      # (N+1,) int64, device: state s owns removes [def_off[s], def_off[s+1])
+    def_clock: torch.Tensor    # (D, A)
+    def_members: torch.Tensor  # (D, ceil(M/64))
+    status: torch.Tensor       # (N,) int32
+
+
+def orswot_ingest(data: torch.Tensor, frame_off: torch.Tensor, actors: torch.Tensor, members: torch.Tensor,
+                  def_cap: Optional[int] = None, ctx: Optional[Context] = None) -> OrswotFrames:
+    """Orswot<u64, u32> frames -> dense states + the deferred removes pooled in state order."""
+    ctx = _ctx(data, ctx)
+    N = _frames(ctx, data, frame_off, "wire.orswot_ingest")
+    A = _dict(ctx, actors, torch.int32, "wire.orswot_ingest(actors)")
+    M = _dict(ctx, members, torch.int64, "wire.orswot_ingest(members)")
+    Mw = (M + 63) // 64
+    dev = data.device
+    clock = torch.empty((N, A), dtype=torch.int64, device=dev)
+    entries = torch.empty((N, M, A), dtype=torch.int64, device=dev)
+    def_off = torch.empty(N + 1, dtype=torch.int64, device=dev)
+    cap = def_cap if def_cap is not None else max(1, N)
+    dcl = torch.empty((cap, A), dtype=torch.int64, device=dev)
+    dmb = torch.empty((cap, Mw), dtype=torch.int64, device=dev)
+    st = _status(N, dev)
+    nd = ctypes.c_size_t()
+    ctx.call("crdt_orswot_ingest", _ptr_or_dummy(data), dptr(frame_off), N, dptr(actors), A, dptr(members), M,
+             dptr(clock), dptr(entries), dptr(def_off), dptr(dcl), dptr(dmb), cap, ctypes.byref(nd), dptr(st))
+    D = nd.value
+    if D > cap and def_cap is None:  # more removes than guessed: once more with exactly enough room
+        return orswot_ingest(data, frame_off, actors, members, def_cap=D, ctx=ctx)
+    return OrswotFrames(clock, entries, def_off, dcl[:min(D, cap)], dmb[:min(D, cap)], st)
+
+
+def _egress(ctx, fn, N, dev, *args):
+    frame_off = torch.empty(N + 1, dtype=torch.int64, device=dev)
+    total = ctypes.c_size_t()
+    ctx.call(fn, *args, dptr(frame_off), None, 0, ctypes.byref(total))
+    data = torch.empty(max(total.value, 1), dtype=torch.uint8, device=dev)
+    ctx.call(fn, *args, dptr(frame_off), dptr(data), data.numel(), ctypes.byref(total))
+    return frame_off, data[:total.value]
+
+
+def vclock_egress(rows: torch.Tensor, actors: torch.Tensor, ctx: Optional[Context] = None, _fn="crdt_vclock_egress",
+                  _k: int = 1):
+    """Dense rows (N, A) -> (frame_off (N+1,), bytes) of VClock / GCounter frames."""
+    ctx = _ctx(rows, ctx)
+    ctx.check_tensor(rows, "wire.vclock_egress(rows)")
+    A = _dict(ctx, actors, torch.int32, "wire.vclock_egress(actors)")
+    if rows.dim() != 2 or rows.shape[1] < _k * A or rows.stride(1) != 1:
+        raise ValueError(f"wire egress: rows must be (N, >= {_k * A}) with contiguous rows")
+    N = rows.shape[0]
+    return _egress(ctx, _fn, N, rows.device, dptr(rows), N, A, rows.stride(0), dptr(actors))
+
+
+def pncounter_egress(rows, actors, ctx=None):
+    return vclock_egress(rows, actors, ctx, "crdt_pncounter_egress", 2)
+
+
+def gset_egress(rows: torch.Tensor, elems: torch.Tensor, ctx: Optional[Context] = None):
+    ctx = _ctx(rows, ctx)
+    ctx.check_tensor(rows, "wire.gset_egress(rows)")
+    U = _dict(ctx, elems, torch.int64, "wire.gset_egress(elems)")
+    if rows.dim() != 2 or rows.shape[1] < (U + 63) // 64 or rows.stride(1) != 1:
+        raise ValueError("wire.gset_egress: rows must be (N, >= ceil(U/64))")
+    N = rows.shape[0]
+    return _egress(ctx, "crdt_gset_egress", N, rows.device, dptr(rows), N, U, rows.stride(0), dptr(elems))
+
+
+def lwwreg_egress(marker: torch.Tensor, val: torch.Tensor, ctx: Optional[Context] = None):
+    ctx = _ctx(marker, ctx)
+    N = marker.shape[0]
+    data = torch.empty(max(16 * N, 1), dtype=torch.uint8, device=marker.device)
+    ctx.call("crdt_lwwreg_egress", dptr(marker.contiguous()), dptr(val.contiguous()), N, dptr(data))
+    off = torch.arange(0, 16 * (N + 1), 16, dtype=torch.int64, device=marker.device)
+    return off, data[:16 * N]
+
+
+def orswot_egress(clock: torch.Tensor, entries: torch.Tensor, actors: torch.Tensor, members: torch.Tensor,
+                  def_off: Optional[torch.Tensor] = None, def_clock: Optional[torch.Tensor] = None,
+                  def_members: Optional[torch.Tensor] = None, def_keep: Optional[torch.Tensor] = None,
+                  ctx: Optional[Context] = None):
+    """Dense Orswot states (clock (N, A), entries (N, M, A)) + removes pooled by state (device
+    def_off (N+1,), def_clock, def_members, def_keep or None) -> (frame_off, bytes)."""
+    ctx = _ctx(clock, ctx)
+    A = _dict(ctx, actors, torch.int32, "wire.orswot_egress(actors)")
+    M = _dict(ctx, members, torch.int64, "wire.orswot_egress(members)")
+    N = clock.shape[0]
+    if tuple(clock.shape) != (N, A) or tuple(entries.shape) != (N, M, A) or not clock.is_contiguous() \
+            or not entries.is_contiguous():
+        raise ValueError("wire.orswot_egress: clock (N, A) and entries (N, M, A), contiguous")
+    dp = [None, None, None, None]
+    if def_off is not None:
+        dp = [dptr(def_off), dptr(def_clock), dptr(def_members), dptr(def_keep) if def_keep is not None else None]
+    return _egress(ctx, "crdt_orswot_egress", N, clock.device, dptr(clock), dptr(entries), N, M, A, dptr(actors),
+                   dptr(members), *dp)

@@ -557,7 +557,7 @@ extern "C" int crdt_map_merge_batch(crdt_ctx *ctx, const crdt_map_states *self, 
   const size_t Kw = (K + 63) / 64;
   CRDT_HIP(ctx, hipSetDevice(ctx->device));
   // status is written whole by the deferred pass; the key pass only ORs bit 4 into it first
-  CRDT_HIP(ctx, hipMemsetAsync(status, 0, N * sizeof(uint32_t), ctx->stream));
+  if (int rc = device_fill(ctx, status, N * sizeof(uint32_t), 0)) return rc;
   if (K) {
     MapPairPlan p{N, K, A, a.V, b.V, Kw, (const u64 *)a.clock, a.clock_stride, (const u64 *)b.clock, b.clock_stride,
                   (u64 *)a.ec, (u64 *)a.vclk, (u64 *)a.vval, a.ec_stride, a.vclk_stride, a.vval_stride,

@@ -419,9 +419,9 @@ int crdt_lwwreg_lub_many_sharded(crdt_ctx *ctx, const uint64_t *marker, const ui
     }
   const size_t n = nz.size();
   if (n == 0) {  // no replica anywhere: the zero register, no conflict
-    CRDT_HIP(ctx, hipMemsetAsync(out_marker, 0, G * 8, ctx->stream));
-    CRDT_HIP(ctx, hipMemsetAsync(out_val, 0, G * 8, ctx->stream));
-    if (first_conflict) CRDT_HIP(ctx, hipMemsetAsync(first_conflict, 0xFF, G * 8, ctx->stream));
+    CRDT_TRY(device_fill(ctx, out_marker, G * 8, 0));
+    CRDT_TRY(device_fill(ctx, out_val, G * 8, 0));
+    if (first_conflict) CRDT_TRY(device_fill(ctx, first_conflict, G * 8, 0xFF));
     return CRDT_OK;
   }
   CRDT_TRY(stage_h2d(ctx, ranks, nz.data(), n * 4));
@@ -431,7 +431,7 @@ int crdt_lwwreg_lub_many_sharded(crdt_ctx *ctx, const uint64_t *marker, const ui
   // 3. the shard continues the GLOBAL fold from the fold of the lower ranks' states, so its
   //    conflicts are those of the global left fold (lwwreg.rs:84-98 is order-dependent)
   if (!R) {
-    CRDT_HIP(ctx, hipMemsetAsync(fc, 0xFF, G * 8, ctx->stream));
+    CRDT_TRY(device_fill(ctx, fc, G * 8, 0xFF));
   } else if (before > 0) {
     CRDT_TRY(crdt_lwwreg_lub_many(ctx, tm, tv, G, before, n, pm, pv, nullptr, 0));
     CRDT_TRY(crdt_lwwreg_lub_many(ctx, marker, val, G, R, group_stride, pm, pv, fc, CRDT_ACCUMULATE));

@@ -1,0 +1,843 @@
+// Serde wire format <-> dense SoA, on the device (the step before the path).
+//
+// Replicas ship whole states (the crate is transport-agnostic, README.md:12-16), serialized with
+// the serde derives of the reference types (vclock.rs:56, gcounter.rs:25, pncounter.rs:28,
+// gset.rs:7, lwwreg.rs:13, orswot.rs:20).  The crate does not pick an encoding; this file reads and
+// writes the one `bincode::serialize` (bincode 1.x, default options) produces, restated here:
+//   integers little-endian at fixed width (u32 = 4 B, u64 = 8 B); a struct is its fields in
+//   declaration order; a map / set / Vec is a u64 length followed by its entries (key then value);
+//   no padding, no field names.
+// So, for the instantiations the kernels take (actors A = u32, members / elements M = u64):
+//   VClock<u32>      = u64 n, then n x (u32 actor, u64 counter), actors ascending (BTreeMap)
+//   GCounter<u32>    = VClock                               (struct { inner })
+//   PNCounter<u32>   = GCounter p, GCounter n               (struct { p, n })
+//   GSet<u64>        = u64 n, then n x u64, ascending       (BTreeSet)
+//   LWWReg<u64, u64> = u64 val, u64 marker                  (struct { val, marker })
+//   Orswot<u64, u32> = VClock clock; u64 n, n x (u64 member, VClock) (HashMap: any order);
+//                      u64 d, d x (VClock rm, u64 k, k x u64 member) (HashMap<VClock, HashSet>)
+// Every field is 4 or 8 bytes, so with 4-byte-aligned frame offsets every field is 4-aligned and
+// is read / written as 32-bit words (a u64 as two).
+//
+// Frames: state s = bytes[frame_off[s] .. frame_off[s+1]).  Ids are interned through sorted
+// dictionaries (device): the dense column of an actor / bit of an element / row of a member is its
+// position in the dictionary.  Ingest is one wave per state: the record loop runs across lanes
+// (lane i parses record i), rows are assembled in LDS and written out with coalesced stores.
+// Egress is count -> exclusive scan -> write.
+#include "common.hpp"
+
+namespace crdt {
+
+constexpr unsigned kWireBad = 1u, kWireMissing = 2u, kWireCap = 4u;
+constexpr int kWireRowLds = 4096;  // u64 words of the LDS row per wave (A or bitmap words)
+
+struct Frame {
+  const uint32_t *w;  // 4-aligned base
+  unsigned long long nw;  // words in the frame
+};
+
+__device__ __forceinline__ u64 rd64(const uint32_t *w, unsigned long long k) {
+  return (u64)w[k] | ((u64)w[k + 1] << 32);
+}
+
+__device__ __forceinline__ long long find_u32(const uint32_t *dict, unsigned long long n, uint32_t id,
+                                              unsigned long long hint) {
+  if (hint < n && dict[hint] == id) return (long long)hint;  // the dense, in-order case
+  unsigned long long lo = 0, hi = n;
+  while (lo < hi) {
+    const unsigned long long mid = (lo + hi) / 2;
+    if (dict[mid] < id) lo = mid + 1;
+    else hi = mid;
+  }
+  return (lo < n && dict[lo] == id) ? (long long)lo : -1;
+}
+__device__ __forceinline__ long long find_u64(const u64 *dict, unsigned long long n, u64 id, unsigned long long hint) {
+  if (hint < n && dict[hint] == id) return (long long)hint;
+  unsigned long long lo = 0, hi = n;
+  while (lo < hi) {
+    const unsigned long long mid = (lo + hi) / 2;
+    if (dict[mid] < id) lo = mid + 1;
+    else hi = mid;
+  }
+  return (lo < n && dict[lo] == id) ? (long long)lo : -1;
+}
+
+__device__ __forceinline__ void wfence() { __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup"); }
+
+// Parse the VClock at word k of frame f into the LDS row (A u64, zeroed here); returns the word
+// after it (or ~0 on a truncated clock).  st |= kWireMissing for an actor not in the dictionary.
+__device__ unsigned long long parse_vclock(const Frame &f, unsigned long long k, const uint32_t *actors,
+                                           unsigned long long A, u64 *row, int lane, unsigned &st) {
+  for (unsigned long long a = lane; a < A; a += kWave) row[a] = 0;
+  wfence();
+  if (k + 2 > f.nw) {
+    st |= kWireBad;
+    return ~0ull;
+  }
+  const u64 n = rd64(f.w, k);
+  if (n > (f.nw - k - 2) / 3) {
+    st |= kWireBad;
+    return ~0ull;
+  }
+  const uint32_t *rec = f.w + k + 2;
+  bool miss = false;
+  for (unsigned long long i = lane; i < n; i += kWave) {
+    const uint32_t id = rec[3 * i];
+    const u64 cnt = rd64(rec, 3 * i + 1);
+    const long long col = find_u32(actors, A, id, i);
+    if (col < 0) miss = true;
+    else row[col] = cnt;
+  }
+  if (__ballot(miss)) st |= kWireMissing;
+  wfence();
+  return k + 2 + 3 * n;
+}
+
+template <typename T>
+__device__ __forceinline__ void store_row(u64 *dst, const u64 *row, unsigned long long W, int lane) {
+  for (unsigned long long a = lane; a < W; a += kWave) dst[a] = row[a];
+}
+
+struct IngestPlan {
+  const uint8_t *bytes;
+  const u64 *frame_off;
+  unsigned long long N;
+  const uint32_t *actors;  // sorted dictionaries
+  unsigned long long A;
+  const u64 *elems;
+  unsigned long long U;
+  u64 *out;  // rows
+  unsigned long long row_stride;
+  int nclocks;  // VClocks per frame: 1 (VClock / GCounter) or 2 (PNCounter: p then n)
+  uint32_t *status;
+  // Orswot
+  const u64 *members;
+  unsigned long long M, Mw;
+  u64 *entries;  // [N][M][A]
+  u64 *dpos;     // [N] word index of the deferred section
+  u64 *dcount;   // [N]
+  u64 *def_off;  // [N+1] exclusive scan of dcount
+  u64 *def_clock, *def_members;
+  unsigned long long def_cap;
+};
+
+__device__ __forceinline__ bool frame_of(const IngestPlan &p, unsigned long long s, Frame &f) {
+  const u64 b = p.frame_off[s], e = p.frame_off[s + 1];
+  if ((b & 3) || (e & 3) || e < b) return false;
+  f.w = reinterpret_cast<const uint32_t *>(p.bytes + b);
+  f.nw = (e - b) / 4;
+  return true;
+}
+
+// VClock / GCounter / PNCounter frames -> rows of nclocks*A counters.
+__global__ __launch_bounds__(kBlock) void vclock_ingest_kernel(IngestPlan p) {
+  extern __shared__ u64 lds[];
+  const int lane = threadIdx.x % kWave, wib = threadIdx.x / kWave;
+  const int wpb = blockDim.x / kWave;
+  u64 *row = lds + (unsigned long long)wib * p.A;
+  for (unsigned long long s = (unsigned long long)blockIdx.x * wpb + wib; s < p.N;
+       s += (unsigned long long)gridDim.x * wpb) {
+    unsigned st = 0;
+    Frame f;
+    u64 *dst = p.out + s * p.row_stride;
+    if (!frame_of(p, s, f)) {
+      st = kWireBad;
+      for (unsigned long long a = lane; a < (unsigned long long)p.nclocks * p.A; a += kWave) dst[a] = 0;
+    } else {
+      unsigned long long k = 0;
+      for (int c = 0; c < p.nclocks; ++c) {
+        if (k != ~0ull) {
+          k = parse_vclock(f, k, p.actors, p.A, row, lane, st);
+        } else {  // after a truncated clock: the remaining clocks are empty
+          for (unsigned long long a = lane; a < p.A; a += kWave) row[a] = 0;
+          wfence();
+        }
+        store_row<u64>(dst + c * p.A, row, p.A, lane);
+        wfence();
+      }
+      if (k != f.nw) st |= kWireBad;  // trailing bytes or a truncated frame
+    }
+    if (lane == 0) p.status[s] = st;
+  }
+}
+
+// GSet<u64> frames -> bitmap rows of ceil(U/64) words.
+__global__ __launch_bounds__(kBlock) void gset_ingest_kernel(IngestPlan p) {
+  extern __shared__ u64 lds[];
+  const int lane = threadIdx.x % kWave, wib = threadIdx.x / kWave;
+  const int wpb = blockDim.x / kWave;
+  const unsigned long long W = (p.U + 63) / 64;
+  u64 *row = lds + (unsigned long long)wib * W;
+  for (unsigned long long s = (unsigned long long)blockIdx.x * wpb + wib; s < p.N;
+       s += (unsigned long long)gridDim.x * wpb) {
+    unsigned st = 0;
+    Frame f;
+    for (unsigned long long w = lane; w < W; w += kWave) row[w] = 0;
+    wfence();
+    if (!frame_of(p, s, f) || f.nw < 2) {
+      st = kWireBad;
+    } else {
+      const u64 n = rd64(f.w, 0);
+      if (2 + 2 * n != f.nw) st |= kWireBad;
+      const u64 nn = n < (f.nw - 2) / 2 ? n : (f.nw - 2) / 2;
+      bool miss = false;
+      for (unsigned long long i = lane; i < nn; i += kWave) {
+        const long long b = find_u64(p.elems, p.U, rd64(f.w, 2 + 2 * i), i);
+        if (b < 0) miss = true;
+        else atomicOr(row + b / 64, 1ull << (b % 64));
+      }
+      if (__ballot(miss)) st |= kWireMissing;
+    }
+    wfence();
+    store_row<u64>(p.out + s * p.row_stride, row, W, lane);
+    if (lane == 0) p.status[s] = st;
+    wfence();
+  }
+}
+
+// LWWReg<u64, u64> frames (16 B: val, marker) -> the two planes.
+__global__ __launch_bounds__(kBlock) void lwwreg_ingest_kernel(IngestPlan p, u64 *marker, u64 *val) {
+  for (unsigned long long s = blockIdx.x * (unsigned long long)kBlock + threadIdx.x; s < p.N;
+       s += (unsigned long long)gridDim.x * kBlock) {
+    Frame f;
+    unsigned st = 0;
+    if (!frame_of(p, s, f) || f.nw != 4) {
+      st = kWireBad;
+      marker[s] = 0;
+      val[s] = 0;
+    } else {
+      val[s] = rd64(f.w, 0);
+      marker[s] = rd64(f.w, 2);
+    }
+    p.status[s] = st;
+  }
+}
+
+// Orswot<u64, u32> pass 1: clock and entries (the entries were zero-filled before), the deferred
+// section's position and count.
+__global__ __launch_bounds__(kBlock) void orswot_ingest_kernel(IngestPlan p) {
+  extern __shared__ u64 lds[];
+  const int lane = threadIdx.x % kWave, wib = threadIdx.x / kWave;
+  const int wpb = blockDim.x / kWave;
+  u64 *row = lds + (unsigned long long)wib * p.A;
+  for (unsigned long long s = (unsigned long long)blockIdx.x * wpb + wib; s < p.N;
+       s += (unsigned long long)gridDim.x * wpb) {
+    unsigned st = 0;
+    Frame f;
+    u64 dpos = 0, dcnt = 0;
+    if (!frame_of(p, s, f)) {
+      st = kWireBad;
+      for (unsigned long long a = lane; a < p.A; a += kWave) p.out[s * p.row_stride + a] = 0;
+    } else {
+      unsigned long long k = parse_vclock(f, 0, p.actors, p.A, row, lane, st);
+      store_row<u64>(p.out + s * p.row_stride, row, p.A, lane);
+      wfence();
+      if (k != ~0ull && k + 2 <= f.nw) {
+        const u64 n = rd64(f.w, k);
+        k += 2;
+        for (u64 e = 0; e < n && k != ~0ull; ++e) {
+          if (k + 2 > f.nw) {
+            st |= kWireBad;
+            k = ~0ull;
+            break;
+          }
+          const long long mi = find_u64(p.members, p.M, rd64(f.w, k), p.M);
+          k = parse_vclock(f, k + 2, p.actors, p.A, row, lane, st);
+          if (mi < 0) {
+            st |= kWireMissing;
+          } else {
+            store_row<u64>(p.entries + (s * p.M + (unsigned long long)mi) * p.A, row, p.A, lane);
+          }
+          wfence();
+        }
+        if (k != ~0ull && k + 2 <= f.nw) {
+          dcnt = rd64(f.w, k);
+          dpos = k + 2;
+        } else {
+          st |= kWireBad;
+        }
+      } else {
+        st |= kWireBad;
+      }
+    }
+    if (lane == 0) {
+      p.status[s] = st;
+      p.dpos[s] = dpos;
+      p.dcount[s] = (st & kWireBad) ? 0 : dcnt;
+    }
+  }
+}
+
+// Orswot pass 3: deferred removes -> pooled rows at def_off[s] (rm clock row, member bitmap).
+__global__ __launch_bounds__(kBlock) void orswot_ingest_deferred_kernel(IngestPlan p) {
+  extern __shared__ u64 lds[];
+  const int lane = threadIdx.x % kWave, wib = threadIdx.x / kWave;
+  const int wpb = blockDim.x / kWave;
+  u64 *row = lds + (unsigned long long)wib * (p.A + p.Mw);
+  u64 *bits = row + p.A;
+  for (unsigned long long s = (unsigned long long)blockIdx.x * wpb + wib; s < p.N;
+       s += (unsigned long long)gridDim.x * wpb) {
+    const u64 n = p.dcount[s];
+    if (n == 0) continue;
+    unsigned st = p.status[s];
+    Frame f;
+    frame_of(p, s, f);
+    unsigned long long k = p.dpos[s];
+    const u64 d0 = p.def_off[s];
+    for (u64 j = 0; j < n && k != ~0ull; ++j) {
+      k = parse_vclock(f, k, p.actors, p.A, row, lane, st);
+      for (unsigned long long w = lane; w < p.Mw; w += kWave) bits[w] = 0;
+      wfence();
+      if (k == ~0ull || k + 2 > f.nw) {
+        st |= kWireBad;
+        break;
+      }
+      const u64 m = rd64(f.w, k);
+      k += 2;
+      if (m > (f.nw - k) / 2) {
+        st |= kWireBad;
+        break;
+      }
+      bool miss = false;
+      for (unsigned long long i = lane; i < m; i += kWave) {
+        const long long b = find_u64(p.members, p.M, rd64(f.w, k + 2 * i), p.M);
+        if (b < 0) miss = true;
+        else atomicOr(bits + b / 64, 1ull << (b % 64));
+      }
+      if (__ballot(miss)) st |= kWireMissing;
+      k += 2 * m;
+      wfence();
+      const u64 d = d0 + j;
+      if (d < p.def_cap) {
+        store_row<u64>(p.def_clock + d * p.A, row, p.A, lane);
+        store_row<u64>(p.def_members + d * p.Mw, bits, p.Mw, lane);
+      } else {
+        st |= kWireCap;
+      }
+      wfence();
+    }
+    if (k != f.nw) st |= kWireBad;
+    if (lane == 0) p.status[s] = st;
+  }
+}
+
+// ---- exclusive scan of u64 counts (frame sizes, deferred counts) ----------------------------------
+constexpr int kScanItems = 1024;
+
+__global__ __launch_bounds__(kBlock) void scan_block_kernel(const u64 *in, u64 *out, u64 *block_sums,
+                                                            unsigned long long n) {
+  __shared__ u64 sh[kScanItems];
+  const unsigned long long base = (unsigned long long)blockIdx.x * kScanItems;
+  for (int i = threadIdx.x; i < kScanItems; i += kBlock) sh[i] = base + i < n ? in[base + i] : 0;
+  __syncthreads();
+  if (threadIdx.x == 0) {  // 1024 adds: negligible next to the passes it serves
+    u64 run = 0;
+    for (int i = 0; i < kScanItems; ++i) {
+      const u64 v = sh[i];
+      sh[i] = run;
+      run += v;
+    }
+    block_sums[blockIdx.x] = run;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kScanItems; i += kBlock)
+    if (base + i < n) out[base + i] = sh[i];
+}
+
+__global__ void scan_sums_kernel(u64 *block_sums, unsigned long long nb, u64 *total) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    u64 run = 0;
+    for (unsigned long long i = 0; i < nb; ++i) {
+      const u64 v = block_sums[i];
+      block_sums[i] = run;
+      run += v;
+    }
+    *total = run;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void scan_add_kernel(u64 *out, const u64 *block_sums, unsigned long long n,
+                                                          const u64 *total) {
+  const unsigned long long i = blockIdx.x * (unsigned long long)kBlock + threadIdx.x;
+  if (i < n) out[i] += block_sums[i / kScanItems];
+  if (i == n) out[n] = *total;  // out has n+1 entries: the last is the sum
+}
+
+// out[0..n] = exclusive scan of in[0..n), out[n] = sum; *host_total = sum (synchronises).
+static int exclusive_scan(crdt_ctx *ctx, const u64 *in, u64 *out, unsigned long long n, u64 *scratch,
+                          unsigned long long *host_total) {
+  const unsigned long long nb = (n + kScanItems - 1) / kScanItems;
+  u64 *sums = scratch, *total = scratch + (nb ? nb : 1);
+  if (n) hipLaunchKernelGGL(scan_block_kernel, dim3((unsigned)nb), dim3(kBlock), 0, ctx->stream, in, out, sums, n);
+  hipLaunchKernelGGL(scan_sums_kernel, dim3(1), dim3(64), 0, ctx->stream, sums, nb, total);
+  hipLaunchKernelGGL(scan_add_kernel, dim3((unsigned)((n + 1 + kBlock - 1) / kBlock)), dim3(kBlock), 0, ctx->stream,
+                     out, sums, n, total);
+  CRDT_HIP(ctx, hipGetLastError());
+  if (host_total) {
+    u64 t = 0;
+    CRDT_HIP(ctx, hipMemcpyAsync(&t, total, 8, hipMemcpyDeviceToHost, ctx->stream));
+    CRDT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    *host_total = t;
+  }
+  return CRDT_OK;
+}
+
+// ---- egress ---------------------------------------------------------------------------------------
+struct EgressPlan {
+  const u64 *rows;
+  unsigned long long N, A, row_stride;
+  int nclocks;
+  const uint32_t *actors;
+  const u64 *elems;
+  unsigned long long U;
+  u64 *sizes;      // [N] bytes of each frame
+  const u64 *frame_off;
+  uint8_t *bytes;
+  // Orswot
+  const u64 *entries;  // [N][M][A]
+  unsigned long long M, Mw;
+  const u64 *members;
+  const u64 *def_off;  // [N+1] device: state s owns pooled removes [def_off[s], def_off[s+1])
+  const u64 *def_clock, *def_members;
+  const uint8_t *def_keep;  // may be NULL (all kept)
+};
+
+__device__ __forceinline__ u64 nnz_row(const u64 *r, unsigned long long A, int lane) {
+  unsigned long long c = 0;
+  for (unsigned long long a = lane; a < A; a += kWave) c += r[a] != 0;
+  for (int off = kWave / 2; off > 0; off >>= 1) c += __shfl_xor(c, off, kWave);
+  return c;
+}
+__device__ __forceinline__ u64 popc_row(const u64 *r, unsigned long long W, int lane) {
+  unsigned long long c = 0;
+  for (unsigned long long w = lane; w < W; w += kWave) c += __popcll(r[w]);
+  for (int off = kWave / 2; off > 0; off >>= 1) c += __shfl_xor(c, off, kWave);
+  return c;
+}
+__device__ __forceinline__ void wr64(uint32_t *w, unsigned long long k, u64 v) {
+  w[k] = (uint32_t)v;
+  w[k + 1] = (uint32_t)(v >> 32);
+}
+
+// Write a dense row as a VClock at word k (len, then (actor, counter) ascending); returns the
+// next word.  Lanes take columns; a wave prefix count gives every nonzero its record slot.
+__device__ unsigned long long write_vclock(uint32_t *w, unsigned long long k, const u64 *r, unsigned long long A,
+                                           const uint32_t *actors, int lane) {
+  const u64 n = nnz_row(r, A, lane);
+  if (lane == 0) wr64(w, k, n);
+  unsigned long long base = 0;
+  for (unsigned long long a0 = 0; a0 < A; a0 += kWave) {
+    const unsigned long long a = a0 + lane;
+    const u64 v = a < A ? r[a] : 0;
+    const u64 m = __ballot(v != 0);
+    if (v != 0) {
+      const unsigned long long i = base + __popcll(m & ((1ull << lane) - 1));
+      w[k + 2 + 3 * i] = actors[a];
+      wr64(w, k + 3 + 3 * i, v);
+    }
+    base += __popcll(m);
+  }
+  return k + 2 + 3 * n;
+}
+
+__global__ __launch_bounds__(kBlock) void vclock_egress_kernel(EgressPlan p, int write) {
+  const int lane = threadIdx.x % kWave;
+  const unsigned long long w0 = (blockIdx.x * (unsigned long long)kBlock + threadIdx.x) / kWave;
+  const unsigned long long nw = (unsigned long long)gridDim.x * (kBlock / kWave);
+  for (unsigned long long s = w0; s < p.N; s += nw) {
+    const u64 *r = p.rows + s * p.row_stride;
+    if (!write) {
+      u64 sz = 0;
+      for (int c = 0; c < p.nclocks; ++c) sz += 8 + 12 * nnz_row(r + c * p.A, p.A, lane);
+      if (lane == 0) p.sizes[s] = sz;
+      continue;
+    }
+    uint32_t *w = reinterpret_cast<uint32_t *>(p.bytes + p.frame_off[s]);
+    unsigned long long k = 0;
+    for (int c = 0; c < p.nclocks; ++c) k = write_vclock(w, k, r + c * p.A, p.A, p.actors, lane);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void gset_egress_kernel(EgressPlan p, int write) {
+  const int lane = threadIdx.x % kWave;
+  const unsigned long long w0 = (blockIdx.x * (unsigned long long)kBlock + threadIdx.x) / kWave;
+  const unsigned long long nw = (unsigned long long)gridDim.x * (kBlock / kWave);
+  const unsigned long long W = (p.U + 63) / 64;
+  for (unsigned long long s = w0; s < p.N; s += nw) {
+    const u64 *r = p.rows + s * p.row_stride;
+    const u64 n = popc_row(r, W, lane);
+    if (!write) {
+      if (lane == 0) p.sizes[s] = 8 + 8 * n;
+      continue;
+    }
+    uint32_t *w = reinterpret_cast<uint32_t *>(p.bytes + p.frame_off[s]);
+    if (lane == 0) wr64(w, 0, n);
+    unsigned long long base = 0;  // elements ascending = dictionary order = bit order
+    for (unsigned long long w0b = 0; w0b < W; w0b += kWave) {
+      const unsigned long long wi = w0b + lane;
+      u64 x = wi < W ? r[wi] : 0;
+      const unsigned c = __popcll(x);
+      unsigned long long pre = c;  // inclusive prefix of the lane counts
+      for (int off = 1; off < kWave; off <<= 1) {
+        const unsigned long long t = __shfl_up(pre, off, kWave);
+        if (lane >= off) pre += t;
+      }
+      unsigned long long i = base + pre - c;
+      while (x) {
+        const int b = __builtin_ctzll(x);
+        x &= x - 1;
+        wr64(w, 2 + 2 * i, p.elems[wi * 64 + b]);
+        ++i;
+      }
+      base += __shfl(pre, kWave - 1, kWave);
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void lwwreg_egress_kernel(const u64 *marker, const u64 *val, unsigned long long N,
+                                                               uint8_t *bytes) {
+  for (unsigned long long s = blockIdx.x * (unsigned long long)kBlock + threadIdx.x; s < N;
+       s += (unsigned long long)gridDim.x * kBlock) {
+    uint32_t *w = reinterpret_cast<uint32_t *>(bytes + 16 * s);
+    wr64(w, 0, val[s]);
+    wr64(w, 2, marker[s]);
+  }
+}
+
+// Orswot: clock; entries of every present member (index order); surviving removes.
+__global__ __launch_bounds__(kBlock) void orswot_egress_kernel(EgressPlan p, int write) {
+  const int lane = threadIdx.x % kWave;
+  const unsigned long long w0 = (blockIdx.x * (unsigned long long)kBlock + threadIdx.x) / kWave;
+  const unsigned long long nw = (unsigned long long)gridDim.x * (kBlock / kWave);
+  for (unsigned long long s = w0; s < p.N; s += nw) {
+    const u64 *c = p.rows + s * p.row_stride;
+    const u64 *E = p.entries + s * p.M * p.A;
+    const u64 d0 = p.def_off ? p.def_off[s] : 0, d1 = p.def_off ? p.def_off[s + 1] : 0;
+    uint32_t *w = write ? reinterpret_cast<uint32_t *>(p.bytes + p.frame_off[s]) : nullptr;
+    u64 sz = 8 + 12 * nnz_row(c, p.A, lane);
+    unsigned long long k = write ? write_vclock(w, 0, c, p.A, p.actors, lane) : 0;
+    u64 ne = 0;
+    for (unsigned long long m = 0; m < p.M; ++m) ne += nnz_row(E + m * p.A, p.A, lane) != 0;
+    sz += 8;
+    if (write) {
+      if (lane == 0) wr64(w, k, ne);
+      k += 2;
+    }
+    for (unsigned long long m = 0; m < p.M; ++m) {
+      const u64 n = nnz_row(E + m * p.A, p.A, lane);
+      if (n == 0) continue;
+      sz += 8 + 8 + 12 * n;
+      if (write) {
+        if (lane == 0) wr64(w, k, p.members[m]);
+        k = write_vclock(w, k + 2, E + m * p.A, p.A, p.actors, lane);
+      }
+    }
+    u64 nd = 0;
+    for (u64 d = d0; d < d1; ++d) nd += (!p.def_keep || p.def_keep[d]) ? 1 : 0;
+    sz += 8;
+    if (write) {
+      if (lane == 0) wr64(w, k, nd);
+      k += 2;
+    }
+    for (u64 d = d0; d < d1; ++d) {
+      if (p.def_keep && !p.def_keep[d]) continue;
+      const u64 *rm = p.def_clock + d * p.A, *mb = p.def_members + d * p.Mw;
+      const u64 nm = popc_row(mb, p.Mw, lane);
+      sz += 8 + 12 * nnz_row(rm, p.A, lane) + 8 + 8 * nm;
+      if (!write) continue;
+      k = write_vclock(w, k, rm, p.A, p.actors, lane);
+      if (lane == 0) {
+        wr64(w, k, nm);
+        unsigned long long i = 0;
+        for (unsigned long long x = 0; x < p.Mw; ++x) {
+          u64 word = mb[x];
+          while (word) {
+            const int b = __builtin_ctzll(word);
+            word &= word - 1;
+            wr64(w, k + 2 + 2 * i, p.members[x * 64 + b]);
+            ++i;
+          }
+        }
+      }
+      k += 2 + 2 * nm;
+    }
+    if (!write && lane == 0) p.sizes[s] = sz;
+  }
+}
+
+static unsigned wave_grid(crdt_ctx *ctx, unsigned long long waves, int wpb, int per_cu) {
+  const unsigned long long want = (waves + wpb - 1) / wpb;
+  const unsigned long long cap = (unsigned long long)ctx->cu_count * per_cu;
+  return (unsigned)(want == 0 ? 1 : (want < cap ? want : cap));
+}
+
+// frame sizes -> frame_off (device, N+1) -> *total; returns CRDT_OK
+static int egress_layout(crdt_ctx *ctx, u64 *sizes, u64 *frame_off, unsigned long long N, size_t *total) {
+  unsigned long long t = 0;
+  u64 *sc = sizes + N;
+  int rc = exclusive_scan(ctx, sizes, frame_off, N, sc, &t);
+  if (rc) return rc;
+  if (total) *total = t;
+  return CRDT_OK;
+}
+
+static int wire_scratch(crdt_ctx *ctx, unsigned long long N, u64 **sizes) {
+  const unsigned long long nb = (N + kScanItems - 1) / kScanItems + 2;
+  int rc = ensure_scratch(ctx, (N + nb + 8) * 8);
+  if (rc) return rc;
+  *sizes = reinterpret_cast<u64 *>(ctx->scratch);
+  return CRDT_OK;
+}
+
+static int check_frames(crdt_ctx *ctx, const void *bytes, const uint64_t *frame_off, size_t N, uint32_t *status) {
+  if (N && (!frame_off || !status)) return fail(ctx, CRDT_EINVAL, "ingest: NULL frame_off / status");
+  (void)bytes;
+  return CRDT_OK;
+}
+
+}  // namespace crdt
+
+using namespace crdt;
+
+extern "C" {
+
+static int vclock_ingest_common(crdt_ctx *ctx, const uint8_t *bytes, const uint64_t *frame_off, size_t N,
+                                const uint32_t *actors, size_t A, uint64_t *out, size_t row_stride, uint32_t *status,
+                                int nclocks, const char *what) {
+  CRDT_CHECK_CTX(ctx);
+  if (N == 0) return CRDT_OK;
+  if (int rc = check_frames(ctx, bytes, frame_off, N, status)) return rc;
+  if (A == 0 || !actors || !out) return fail(ctx, CRDT_EINVAL, "%s: need actors (A >= 1) and out", what);
+  if (A > (size_t)kWireRowLds) return fail(ctx, CRDT_EUNSUPPORTED, "%s: A = %zu > %d", what, A, kWireRowLds);
+  if (row_stride < (size_t)nclocks * A) return fail(ctx, CRDT_EINVAL, "%s: row_stride < %d*A", what, nclocks);
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  int wpb = 4;
+  while (wpb > 1 && (size_t)wpb * A * 8 > 64 * 1024) --wpb;
+  IngestPlan p{};
+  p.bytes = bytes;
+  p.frame_off = (const u64 *)frame_off;
+  p.N = N;
+  p.actors = actors;
+  p.A = A;
+  p.out = (u64 *)out;
+  p.row_stride = row_stride;
+  p.nclocks = nclocks;
+  p.status = status;
+  timing_begin(ctx, "wire_ingest");
+  hipLaunchKernelGGL(vclock_ingest_kernel, dim3(wave_grid(ctx, N, wpb, 32)), dim3(wpb * kWave), wpb * A * 8,
+                     ctx->stream, p);
+  timing_end(ctx);
+  CRDT_HIP(ctx, hipGetLastError());
+  return CRDT_OK;
+}
+
+int crdt_vclock_ingest(crdt_ctx *ctx, const uint8_t *bytes, const uint64_t *frame_off, size_t N, const uint32_t *actors,
+                       size_t A, uint64_t *out, size_t row_stride, uint32_t *status) {
+  return vclock_ingest_common(ctx, bytes, frame_off, N, actors, A, out, row_stride, status, 1, "vclock_ingest");
+}
+
+int crdt_pncounter_ingest(crdt_ctx *ctx, const uint8_t *bytes, const uint64_t *frame_off, size_t N,
+                          const uint32_t *actors, size_t A, uint64_t *out, size_t row_stride, uint32_t *status) {
+  return vclock_ingest_common(ctx, bytes, frame_off, N, actors, A, out, row_stride, status, 2, "pncounter_ingest");
+}
+
+int crdt_gset_ingest(crdt_ctx *ctx, const uint8_t *bytes, const uint64_t *frame_off, size_t N, const uint64_t *elems,
+                     size_t U, uint64_t *out, size_t row_stride, uint32_t *status) {
+  CRDT_CHECK_CTX(ctx);
+  if (N == 0) return CRDT_OK;
+  if (int rc = check_frames(ctx, bytes, frame_off, N, status)) return rc;
+  const size_t W = (U + 63) / 64;
+  if (U == 0 || !elems || !out) return fail(ctx, CRDT_EINVAL, "gset_ingest: need elems (U >= 1) and out");
+  if (W > (size_t)kWireRowLds) return fail(ctx, CRDT_EUNSUPPORTED, "gset_ingest: U = %zu too large", U);
+  if (row_stride < W) return fail(ctx, CRDT_EINVAL, "gset_ingest: row_stride < ceil(U/64)");
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  int wpb = 4;
+  while (wpb > 1 && (size_t)wpb * W * 8 > 64 * 1024) --wpb;
+  IngestPlan p{};
+  p.bytes = bytes;
+  p.frame_off = (const u64 *)frame_off;
+  p.N = N;
+  p.elems = (const u64 *)elems;
+  p.U = U;
+  p.out = (u64 *)out;
+  p.row_stride = row_stride;
+  p.status = status;
+  timing_begin(ctx, "wire_ingest");
+  hipLaunchKernelGGL(gset_ingest_kernel, dim3(wave_grid(ctx, N, wpb, 32)), dim3(wpb * kWave), wpb * W * 8, ctx->stream,
+                     p);
+  timing_end(ctx);
+  CRDT_HIP(ctx, hipGetLastError());
+  return CRDT_OK;
+}
+
+int crdt_lwwreg_ingest(crdt_ctx *ctx, const uint8_t *bytes, const uint64_t *frame_off, size_t N, uint64_t *marker,
+                       uint64_t *val, uint32_t *status) {
+  CRDT_CHECK_CTX(ctx);
+  if (N == 0) return CRDT_OK;
+  if (int rc = check_frames(ctx, bytes, frame_off, N, status)) return rc;
+  if (!marker || !val) return fail(ctx, CRDT_EINVAL, "lwwreg_ingest: NULL output");
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  IngestPlan p{};
+  p.bytes = bytes;
+  p.frame_off = (const u64 *)frame_off;
+  p.N = N;
+  p.status = status;
+  hipLaunchKernelGGL(lwwreg_ingest_kernel, dim3(wave_grid(ctx, N, 4, 16)), dim3(kBlock), 0, ctx->stream, p,
+                     (u64 *)marker, (u64 *)val);
+  CRDT_HIP(ctx, hipGetLastError());
+  return CRDT_OK;
+}
+
+int crdt_orswot_ingest(crdt_ctx *ctx, const uint8_t *bytes, const uint64_t *frame_off, size_t N, const uint32_t *actors,
+                       size_t A, const uint64_t *members, size_t M, uint64_t *clock, uint64_t *entries,
+                       uint64_t *def_off, uint64_t *def_clock, uint64_t *def_members, size_t def_cap, size_t *n_def,
+                       uint32_t *status) {
+  CRDT_CHECK_CTX(ctx);
+  if (n_def) *n_def = 0;
+  if (N == 0) return CRDT_OK;
+  if (int rc = check_frames(ctx, bytes, frame_off, N, status)) return rc;
+  if (A == 0 || M == 0 || !actors || !members || !clock || !entries || !def_off)
+    return fail(ctx, CRDT_EINVAL, "orswot_ingest: need actors, members, clock, entries, def_off");
+  if (def_cap && (!def_clock || !def_members)) return fail(ctx, CRDT_EINVAL, "orswot_ingest: NULL deferred output");
+  const size_t Mw = (M + 63) / 64;
+  if (A + Mw > (size_t)kWireRowLds) return fail(ctx, CRDT_EUNSUPPORTED, "orswot_ingest: A + M/64 too large");
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  // scratch: deferred positions + counts [2N], scan block sums
+  const unsigned long long nb = (N + kScanItems - 1) / kScanItems + 2;
+  if (int rc = ensure_scratch(ctx, (2 * N + nb + 8) * 8)) return rc;
+  u64 *dpos = reinterpret_cast<u64 *>(ctx->scratch), *dcount = dpos + N, *sc = dcount + N;
+  if (int rc = device_fill(ctx, entries, N * M * A * 8, 0)) return rc;
+  int wpb = 4;
+  while (wpb > 1 && (size_t)wpb * (A + Mw) * 8 > 64 * 1024) --wpb;
+  IngestPlan p{};
+  p.bytes = bytes;
+  p.frame_off = (const u64 *)frame_off;
+  p.N = N;
+  p.actors = actors;
+  p.A = A;
+  p.out = (u64 *)clock;
+  p.row_stride = A;
+  p.status = status;
+  p.members = (const u64 *)members;
+  p.M = M;
+  p.Mw = Mw;
+  p.entries = (u64 *)entries;
+  p.dpos = dpos;
+  p.dcount = dcount;
+  p.def_off = (u64 *)def_off;
+  p.def_clock = (u64 *)def_clock;
+  p.def_members = (u64 *)def_members;
+  p.def_cap = def_cap;
+  const unsigned grid = wave_grid(ctx, N, wpb, 32);
+  timing_begin(ctx, "wire_ingest");
+  hipLaunchKernelGGL(orswot_ingest_kernel, dim3(grid), dim3(wpb * kWave), wpb * A * 8, ctx->stream, p);
+  CRDT_HIP(ctx, hipGetLastError());
+  unsigned long long D = 0;
+  if (int rc = exclusive_scan(ctx, dcount, (u64 *)def_off, N, sc, &D)) return rc;
+  if (D)
+    hipLaunchKernelGGL(orswot_ingest_deferred_kernel, dim3(grid), dim3(wpb * kWave), wpb * (A + Mw) * 8, ctx->stream,
+                       p);
+  timing_end(ctx);
+  CRDT_HIP(ctx, hipGetLastError());
+  if (n_def) *n_def = D;
+  return CRDT_OK;
+}
+
+static int egress_common(crdt_ctx *ctx, EgressPlan p, size_t N, uint64_t *frame_off, uint8_t *bytes, size_t cap,
+                         size_t *total, void (*kern)(EgressPlan, int), const char *what) {
+  CRDT_CHECK_CTX(ctx);
+  if (total) *total = 0;
+  if (N == 0) return CRDT_OK;
+  if (!frame_off || !total) return fail(ctx, CRDT_EINVAL, "%s: need frame_off and total", what);
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  u64 *sizes = nullptr;
+  if (int rc = wire_scratch(ctx, N, &sizes)) return rc;
+  p.sizes = sizes;
+  const unsigned grid = wave_grid(ctx, N, 4, 32);
+  timing_begin(ctx, "wire_egress");
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, ctx->stream, p, 0);
+  CRDT_HIP(ctx, hipGetLastError());
+  if (int rc = egress_layout(ctx, sizes, (u64 *)frame_off, N, total)) return rc;
+  if (bytes && cap >= *total) {
+    p.frame_off = (const u64 *)frame_off;
+    p.bytes = bytes;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, ctx->stream, p, 1);
+    CRDT_HIP(ctx, hipGetLastError());
+  }
+  timing_end(ctx);
+  return CRDT_OK;
+}
+
+int crdt_vclock_egress(crdt_ctx *ctx, const uint64_t *rows, size_t N, size_t A, size_t row_stride,
+                       const uint32_t *actors, uint64_t *frame_off, uint8_t *bytes, size_t cap, size_t *total) {
+  if (ctx && N && (!rows || !actors || A == 0)) return fail(ctx, CRDT_EINVAL, "vclock_egress: NULL rows / actors");
+  EgressPlan p{};
+  p.rows = (const u64 *)rows;
+  p.N = N;
+  p.A = A;
+  p.row_stride = row_stride;
+  p.nclocks = 1;
+  p.actors = actors;
+  return egress_common(ctx, p, N, frame_off, bytes, cap, total, vclock_egress_kernel, "vclock_egress");
+}
+
+int crdt_pncounter_egress(crdt_ctx *ctx, const uint64_t *rows, size_t N, size_t A, size_t row_stride,
+                          const uint32_t *actors, uint64_t *frame_off, uint8_t *bytes, size_t cap, size_t *total) {
+  if (ctx && N && (!rows || !actors || A == 0)) return fail(ctx, CRDT_EINVAL, "pncounter_egress: NULL rows / actors");
+  EgressPlan p{};
+  p.rows = (const u64 *)rows;
+  p.N = N;
+  p.A = A;
+  p.row_stride = row_stride;
+  p.nclocks = 2;
+  p.actors = actors;
+  return egress_common(ctx, p, N, frame_off, bytes, cap, total, vclock_egress_kernel, "pncounter_egress");
+}
+
+int crdt_gset_egress(crdt_ctx *ctx, const uint64_t *rows, size_t N, size_t U, size_t row_stride, const uint64_t *elems,
+                     uint64_t *frame_off, uint8_t *bytes, size_t cap, size_t *total) {
+  if (ctx && N && (!rows || !elems || U == 0)) return fail(ctx, CRDT_EINVAL, "gset_egress: NULL rows / elems");
+  EgressPlan p{};
+  p.rows = (const u64 *)rows;
+  p.N = N;
+  p.U = U;
+  p.row_stride = row_stride;
+  p.elems = (const u64 *)elems;
+  return egress_common(ctx, p, N, frame_off, bytes, cap, total, gset_egress_kernel, "gset_egress");
+}
+
+int crdt_lwwreg_egress(crdt_ctx *ctx, const uint64_t *marker, const uint64_t *val, size_t N, uint8_t *bytes) {
+  CRDT_CHECK_CTX(ctx);
+  if (N == 0) return CRDT_OK;
+  if (!marker || !val || !bytes) return fail(ctx, CRDT_EINVAL, "lwwreg_egress: NULL buffer");
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  hipLaunchKernelGGL(lwwreg_egress_kernel, dim3(wave_grid(ctx, N, 4, 16)), dim3(kBlock), 0, ctx->stream,
+                     (const u64 *)marker, (const u64 *)val, (unsigned long long)N, bytes);
+  CRDT_HIP(ctx, hipGetLastError());
+  return CRDT_OK;
+}
+
+int crdt_orswot_egress(crdt_ctx *ctx, const uint64_t *clock, const uint64_t *entries, size_t N, size_t M, size_t A,
+                       const uint32_t *actors, const uint64_t *members, const uint64_t *def_off,
+                       const uint64_t *def_clock, const uint64_t *def_members, const uint8_t *def_keep,
+                       uint64_t *frame_off, uint8_t *bytes, size_t cap, size_t *total) {
+  if (ctx && N && (!clock || !entries || !actors || !members || A == 0 || M == 0))
+    return fail(ctx, CRDT_EINVAL, "orswot_egress: NULL state / dictionaries");
+  if (ctx && def_off && (!def_clock || !def_members)) return fail(ctx, CRDT_EINVAL, "orswot_egress: NULL deferred");
+  EgressPlan p{};
+  p.rows = (const u64 *)clock;
+  p.N = N;
+  p.A = A;
+  p.row_stride = A;
+  p.actors = actors;
+  p.entries = (const u64 *)entries;
+  p.M = M;
+  p.Mw = (M + 63) / 64;
+  p.members = (const u64 *)members;
+  p.def_off = (const u64 *)def_off;
+  p.def_clock = (const u64 *)def_clock;
+  p.def_members = (const u64 *)def_members;
+  p.def_keep = def_keep;
+  return egress_common(ctx, p, N, frame_off, bytes, cap, total, orswot_egress_kernel, "orswot_egress");
+}
+
+}  // extern "C"

@@ -1,0 +1,308 @@
+"""GPU parity: serde wire format (bincode 1.x) ingest / egress (crdt_*_ingest, crdt_*_egress;
+SURVEY §8f row 1) against the oracle's bincode restatement (oracle.bc_* / unbc_*):
+  * ingest of random frames equals the dense layout built on the host, byte-exact egress of
+    canonical frames, order-free Orswot maps;
+  * end to end: serialized replicas -> ingest -> lub_many -> egress -> decode == the oracle's
+    fold of the same replicas (VClock, PNCounter, GSet, LWWReg, Orswot with deferred removes);
+  * the reference's KATs with every merge routed through bytes (serialize both states, ingest,
+    merge on the GPU, egress, decode);
+  * malformed frames (truncated, trailing bytes, misaligned) and ids missing from a dictionary
+    are reported per state, never read past the frame."""
+import numpy as np
+import pytest
+import torch
+
+import kat_runner as K
+import oracle as O
+from gpu_util import to_dev, to_host
+
+pytestmark = pytest.mark.gpu
+
+import crdts_gpu as cg  # noqa: E402
+from crdts_gpu import wire  # noqa: E402
+
+
+def dev_bytes(blob: bytes):
+    return torch.from_numpy(np.frombuffer(blob, np.uint8).copy()).cuda() if blob else torch.zeros(4, dtype=torch.uint8,
+                                                                                                  device="cuda")
+
+
+def dev_off(off):
+    return torch.tensor(off, dtype=torch.int64, device="cuda")
+
+
+def host_frames(data: torch.Tensor, off: torch.Tensor):
+    b = bytes(data.cpu().numpy().tobytes())
+    o = off.cpu().numpy().tolist()
+    return [b[o[i]:o[i + 1]] for i in range(len(o) - 1)]
+
+
+def actor_dict(rng, A):
+    ids = np.sort(rng.choice(2**32 - 1, size=A, replace=False)).astype(np.uint32)
+    return ids, torch.from_numpy(ids.view(np.int32).copy()).cuda()
+
+
+def u64_dict(rng, M):
+    ids = np.sort(rng.choice(2**62, size=M, replace=False)).astype(np.uint64)
+    return ids, torch.from_numpy(ids.view(np.int64).copy()).cuda()
+
+
+def rand_rows(rng, N, A, p=0.6):
+    rows = rng.integers(1, 2**63, size=(N, A), dtype=np.uint64)
+    rows[rng.random((N, A)) > p] = 0
+    rows[rng.integers(0, N, size=max(1, N // 10))] = 0  # some empty clocks
+    return rows
+
+
+def row_dots(row, ids):
+    return {int(ids[a]): int(v) for a, v in enumerate(row) if v}
+
+
+@pytest.mark.parametrize("N,A", [(300, 70), (64, 1), (17, 1024), (1, 4096)])
+def test_vclock_ingest_egress(gpu_ctx, N, A):
+    rng = np.random.default_rng(N + A)
+    ids, dd = actor_dict(rng, A)
+    rows = rand_rows(rng, N, A)
+    blob, off = O.frames([O.bc_vclock(row_dots(r, ids)) for r in rows])
+    got, st = wire.vclock_ingest(dev_bytes(blob), dev_off(off), dd, ctx=gpu_ctx)
+    assert (st.cpu().numpy() == 0).all()
+    np.testing.assert_array_equal(to_host(got), rows)
+    eoff, edata = wire.vclock_egress(got, dd, ctx=gpu_ctx)
+    assert eoff.cpu().tolist() == off
+    assert bytes(edata.cpu().numpy().tobytes()) == blob  # canonical frames round-trip byte for byte
+
+
+def test_pncounter_gset_lwwreg_round_trip(gpu_ctx):
+    rng = np.random.default_rng(5)
+    N, A, U = 200, 33, 300
+    ids, dd = actor_dict(rng, A)
+    p, n = rand_rows(rng, N, A), rand_rows(rng, N, A, 0.3)
+    blob, off = O.frames([O.bc_pncounter(row_dots(p[i], ids), row_dots(n[i], ids)) for i in range(N)])
+    got, st = wire.pncounter_ingest(dev_bytes(blob), dev_off(off), dd, ctx=gpu_ctx)
+    assert (st.cpu().numpy() == 0).all()
+    np.testing.assert_array_equal(to_host(got), np.concatenate([p, n], axis=1))
+    eoff, edata = wire.pncounter_egress(got, dd, ctx=gpu_ctx)
+    assert bytes(edata.cpu().numpy().tobytes()) == blob
+    # GSet<u64>
+    eids, ed = u64_dict(rng, U)
+    sets = [set(int(x) for x in rng.choice(eids, size=int(rng.integers(0, 40)), replace=False)) for _ in range(N)]
+    blob, off = O.frames([O.bc_gset(s) for s in sets])
+    bm, st = wire.gset_ingest(dev_bytes(blob), dev_off(off), ed, ctx=gpu_ctx)
+    assert (st.cpu().numpy() == 0).all()
+    pos = {int(x): i for i, x in enumerate(eids)}
+    exp = np.zeros((N, (U + 63) // 64), np.uint64)
+    for i, s in enumerate(sets):
+        for x in s:
+            exp[i, pos[x] // 64] |= np.uint64(1) << np.uint64(pos[x] % 64)
+    np.testing.assert_array_equal(to_host(bm), exp)
+    eoff, edata = wire.gset_egress(bm, ed, ctx=gpu_ctx)
+    assert bytes(edata.cpu().numpy().tobytes()) == blob
+    # LWWReg<u64, u64>
+    vals, marks = rng.integers(0, 2**63, N).astype(np.uint64), rng.integers(0, 2**63, N).astype(np.uint64)
+    blob, off = O.frames([O.bc_lwwreg(v, m) for v, m in zip(vals, marks)])
+    m, v, st = wire.lwwreg_ingest(dev_bytes(blob), dev_off(off), ctx=gpu_ctx)
+    assert (st.cpu().numpy() == 0).all()
+    np.testing.assert_array_equal(to_host(m), marks)
+    np.testing.assert_array_equal(to_host(v), vals)
+    eoff, edata = wire.lwwreg_egress(m, v, ctx=gpu_ctx)
+    assert bytes(edata.cpu().numpy().tobytes()) == blob
+
+
+def orswot_objects(seed, R, M, A):
+    """gen_orswot replicas as (clock, entries, deferred) dicts over dense indices."""
+    clock, entries, off, dcl, dmem = O.gen_orswot(seed, R, M, A, kmax=12, p_def=0.5)
+    out = []
+    for r in range(R):
+        ent = {m: {a: int(v) for a, v in enumerate(entries[r, m]) if v} for m in range(M) if entries[r, m].any()}
+        de = {}
+        for d in range(int(off[r]), int(off[r + 1])):
+            key = tuple((a, int(v)) for a, v in enumerate(dcl[d]) if v)
+            de.setdefault(key, set()).update(O.bitmap_members(dmem[d]))
+        out.append(({a: int(v) for a, v in enumerate(clock[r]) if v}, ent, de))
+    return out, (clock, entries, off, dcl, dmem)
+
+
+def orswot_blob(states, aids, mids, rng):
+    blobs = []
+    for c, ent, de in states:
+        ent_ids = {int(mids[m]): {int(aids[a]): v for a, v in e.items()} for m, e in ent.items()}
+        order = list(ent_ids)
+        rng.shuffle(order)  # HashMap: any order
+        dlist = [({int(aids[a]): v for a, v in k}, [int(mids[m]) for m in ms]) for k, ms in de.items()]
+        blobs.append(O.bc_orswot({int(aids[a]): v for a, v in c.items()}, ent_ids, dlist, order=order))
+    return O.frames(blobs)
+
+
+def test_orswot_ingest_egress(gpu_ctx):
+    rng = np.random.default_rng(11)
+    R, M, A = 40, 90, 9
+    states, (clock, entries, off, dcl, dmem) = orswot_objects(3, R, M, A)
+    aids, ad = actor_dict(rng, A)
+    mids, md = u64_dict(rng, M)
+    blob, foff = orswot_blob(states, aids, mids, rng)
+    res = wire.orswot_ingest(dev_bytes(blob), dev_off(foff), ad, md, ctx=gpu_ctx)
+    assert (res.status.cpu().numpy() == 0).all()
+    np.testing.assert_array_equal(to_host(res.clock), clock)
+    np.testing.assert_array_equal(to_host(res.entries), entries)
+    # pooled removes in state order; within a state, frame order (= the object's dict order)
+    got_def = [set() for _ in range(R)]
+    doff = res.def_off.cpu().numpy()
+    gd, gm = to_host(res.def_clock), to_host(res.def_members)
+    for r in range(R):
+        for d in range(int(doff[r]), int(doff[r + 1])):
+            got_def[r].add((tuple((a, int(v)) for a, v in enumerate(gd[d]) if v), O.bitmap_members(gm[d])))
+    assert got_def == [{(k, frozenset(ms)) for k, ms in de.items()} for _, _, de in states]
+    assert int(doff[-1]) > 0
+    # egress of the ingested states decodes to the same objects
+    eoff, edata = wire.orswot_egress(res.clock, res.entries, ad, md, res.def_off, res.def_clock, res.def_members,
+                                     ctx=gpu_ctx)
+    for r, fr in enumerate(host_frames(edata, eoff)):
+        c, e, d, pos = O.unbc_orswot(fr)
+        assert pos == len(fr)
+        c0, e0, d0 = states[r]
+        assert c == {int(aids[a]): v for a, v in c0.items()}
+        assert e == {int(mids[m]): {int(aids[a]): v for a, v in x.items()} for m, x in e0.items()}
+        assert d == {tuple(sorted((int(aids[a]), v) for a, v in k)): {int(mids[m]) for m in ms} for k, ms in d0.items()}
+
+
+def test_end_to_end_orswot_fold_through_bytes(gpu_ctx):
+    """R serialized replicas -> ingest -> lub_many -> egress -> decode == the oracle fold."""
+    rng = np.random.default_rng(12)
+    R, M, A = 64, 120, 16
+    states, raw = orswot_objects(8, R, M, A)
+    aids, ad = actor_dict(rng, A)
+    mids, md = u64_dict(rng, M)
+    blob, foff = orswot_blob(states, aids, mids, rng)
+    res = wire.orswot_ingest(dev_bytes(blob), dev_off(foff), ad, md, ctx=gpu_ctx)
+    D = res.def_clock.shape[0]
+    lub = cg.orswot.lub_many(res.clock, res.entries, def_off=[0, D], def_clock=res.def_clock,
+                             def_members=res.def_members, ctx=gpu_ctx)
+    one = torch.tensor([0, D], dtype=torch.int64, device="cuda")
+    eoff, edata = wire.orswot_egress(lub.clock[None].contiguous(), lub.entries[None].contiguous(), ad, md, one,
+                                     res.def_clock, lub.def_members, lub.def_keep, ctx=gpu_ctx)
+    c, e, d, pos = O.unbc_orswot(host_frames(edata, eoff)[0])
+    oc, oe, odef, _ = O.orswot_fold(*raw)
+    assert c == {int(aids[a]): int(v) for a, v in enumerate(oc) if v}
+    assert e == {int(mids[m]): {int(aids[a]): int(v) for a, v in enumerate(oe[m]) if v} for m in range(M) if oe[m].any()}
+    assert d == {tuple(sorted((int(aids[a]), v) for a, v in enumerate(k) if v)): {int(mids[m]) for m in ms}
+                 for k, ms in odef}
+    assert odef
+
+
+def test_end_to_end_counters_through_bytes(gpu_ctx):
+    rng = np.random.default_rng(13)
+    R, A = 500, 64
+    ids, dd = actor_dict(rng, A)
+    rows = rand_rows(rng, R, 2 * A)
+    blob, off = O.frames([O.bc_pncounter(row_dots(r[:A], ids), row_dots(r[A:], ids)) for r in rows])
+    dense, st = wire.pncounter_ingest(dev_bytes(blob), dev_off(off), dd, ctx=gpu_ctx)
+    lub = cg.pncounter.lub_many(dense, ctx=gpu_ctx)
+    eoff, edata = wire.pncounter_egress(lub[None], dd, ctx=gpu_ctx)
+    fr = host_frames(edata, eoff)[0]
+    p, pos = O.unbc_vclock(fr)
+    n, pos = O.unbc_vclock(fr, pos)
+    exp, _ = O.pncounter_fold(rows)
+    assert p == row_dots(exp[:A], ids) and n == row_dots(exp[A:], ids) and pos == len(fr)
+
+
+def test_malformed_frames_and_missing_ids(gpu_ctx):
+    rng = np.random.default_rng(14)
+    A = 8
+    ids, dd = actor_dict(rng, A)
+    good = O.bc_vclock({int(ids[1]): 5, int(ids[3]): 7})
+    missing = O.bc_vclock({int(ids[1]): 5, int(ids[2]) + 1: 9})   # an actor outside the dictionary
+    truncated = good[:-4]
+    trailing = good + b"\x00\x00\x00\x00"
+    lying = b"\xff" + good[1:]                                      # a length far past the frame
+    parts = [good, missing, truncated, trailing, lying]
+    blob = b"".join(parts)
+    off = np.cumsum([0] + [len(x) for x in parts]).tolist()
+    rows, st = wire.vclock_ingest(dev_bytes(blob), dev_off(off), dd, ctx=gpu_ctx)
+    assert st.cpu().tolist() == [0, 2, 1, 1, 1]
+    r = to_host(rows)
+    assert r[0, 1] == 5 and r[0, 3] == 7 and r[1, 1] == 5 and r[1].sum() == 5
+    # a misaligned frame offset is malformed (frames are whole 4-byte words)
+    rows, st = wire.vclock_ingest(dev_bytes(good + good), dev_off([0, 2, len(good) * 2]), dd, ctx=gpu_ctx)
+    assert st.cpu().tolist() == [1, 1]
+
+
+# ---- the reference's KATs with every merge through bytes -------------------------------------
+def _ids(values):
+    """Deterministic u32 / u64 ids for the KATs' actors and members (strings or ints)."""
+    vs = sorted(set(values), key=lambda x: (str(type(x)), x))
+    return {v: i + 1 for i, v in enumerate(vs)}
+
+
+def wire_merge(dst, src, kind):
+    if kind in ("vclock", "gcounter", "pncounter"):
+        def parts(x):
+            if kind == "vclock":
+                return [x.dots]
+            if kind == "gcounter":
+                return [x.inner.dots]
+            return [x.p.inner.dots, x.n.inner.dots]
+        pa, pb = parts(dst), parts(src)
+        amap = _ids([a for d in pa + pb for a in d])
+        inv = {v: k for k, v in amap.items()}
+        aids = np.array(sorted(amap.values()) or [1], np.uint32)
+        dd = torch.from_numpy(aids.view(np.int32).copy()).cuda()
+        enc = (lambda ds: b"".join(O.bc_vclock({amap[a]: c for a, c in d.items()}) for d in ds))
+        blob, off = O.frames([enc(pa), enc(pb)])
+        ing = wire.pncounter_ingest if kind == "pncounter" else wire.vclock_ingest
+        egr = wire.pncounter_egress if kind == "pncounter" else wire.vclock_egress
+        rows, st = ing(dev_bytes(blob), dev_off(off), dd)
+        assert (st.cpu().numpy() == 0).all()
+        mod = {"vclock": cg.vclock, "gcounter": cg.gcounter, "pncounter": cg.pncounter}[kind]
+        eoff, edata = egr(mod.lub_many(rows)[None], dd)
+        fr = host_frames(edata, eoff)[0]
+        out, pos = O.unbc_vclock(fr)
+        dec = [out]
+        if kind == "pncounter":
+            dec.append(O.unbc_vclock(fr, pos)[0])
+        back = [{inv[a]: c for a, c in d.items()} for d in dec]
+        if kind == "vclock":
+            dst.dots = back[0]
+        elif kind == "gcounter":
+            dst.inner.dots = back[0]
+        else:
+            dst.p.inner.dots, dst.n.inner.dots = back
+        return dst
+    if kind == "orswot":
+        amap = _ids([a for s in (dst, src) for c in [s.clock] + list(s.entries.values()) + list(s.deferred)
+                     for a in c.dots])
+        mmap = _ids([m for s in (dst, src) for m in list(s.entries) + [x for ms in s.deferred.values() for x in ms]])
+        ainv, minv = {v: k for k, v in amap.items()}, {v: k for k, v in mmap.items()}
+        aids = np.array(sorted(amap.values()) or [1], np.uint32)
+        mids = np.array(sorted(mmap.values()) or [1], np.uint64)
+        ad = torch.from_numpy(aids.view(np.int32).copy()).cuda()
+        md = torch.from_numpy(mids.view(np.int64).copy()).cuda()
+        blobs = [O.bc_orswot({amap[a]: c for a, c in s.clock.dots.items()},
+                             {mmap[m]: {amap[a]: c for a, c in e.dots.items()} for m, e in s.entries.items()},
+                             [({amap[a]: c for a, c in k.dots.items()}, [mmap[m] for m in ms])
+                              for k, ms in s.deferred.items()]) for s in (dst, src)]
+        blob, off = O.frames(blobs)
+        res = wire.orswot_ingest(dev_bytes(blob), dev_off(off), ad, md)
+        assert (res.status.cpu().numpy() == 0).all()
+        D = res.def_clock.shape[0]
+        kw = dict(def_off=[0, D], def_clock=res.def_clock, def_members=res.def_members) if D else {}
+        lub = cg.orswot.lub_many(res.clock, res.entries, **kw)
+        one = torch.tensor([0, D], dtype=torch.int64, device="cuda")
+        eoff, edata = wire.orswot_egress(lub.clock[None].contiguous(), lub.entries[None].contiguous(), ad, md,
+                                         one if D else None, res.def_clock, lub.def_members, lub.def_keep)
+        c, e, d, _ = O.unbc_orswot(host_frames(edata, eoff)[0])
+        out = O.Orswot()
+        out.clock = O.VClock({ainv[a]: v for a, v in c.items()})
+        out.entries = {minv[m]: O.VClock({ainv[a]: v for a, v in x.items()}) for m, x in e.items()}
+        out.deferred = {O.VClock({ainv[a]: v for a, v in k}): {minv[m] for m in ms} for k, ms in d.items()}
+        return out
+    from test_gpu_kat import gpu_merge
+    return gpu_merge(dst, src, kind)
+
+
+CASES = [c for f in ("kat_vclock.json", "kat_counters.json", "kat_orswot.json")
+         for c in K.load_cases(f) if any(s[0] in ("merge", "merge_err") for s in c["steps"])]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
+def test_kat_merges_through_the_wire(gpu_ctx, case):
+    K.run_case(case, merge_hook=wire_merge)

@@ -1,0 +1,38 @@
+"""CPU: the oracle's bincode restatement (test infrastructure for the wire ingest / egress) —
+hand-computed byte layouts of small states and decode(encode(x)) == x."""
+import struct
+
+import numpy as np
+
+import oracle as O
+
+
+def test_vclock_bytes_by_hand():
+    # BTreeMap<u32, u64> {1: 5, 7: 2^40}: u64 len 2, then (1u32, 5u64), (7u32, 2^40 u64), ascending
+    b = O.bc_vclock({7: 2**40, 1: 5})
+    assert b == (b"\x02" + b"\x00" * 7 + b"\x01\x00\x00\x00" + b"\x05" + b"\x00" * 7
+                 + b"\x07\x00\x00\x00" + struct.pack("<Q", 2**40))
+    assert O.bc_vclock({}) == b"\x00" * 8
+    assert O.bc_vclock({3: 0}) == b"\x00" * 8  # an absent actor (0) is not stored (vclock.rs:156)
+
+
+def test_struct_layouts():
+    assert O.bc_lwwreg(9, 2) == struct.pack("<QQ", 9, 2)                     # val, marker
+    assert O.bc_pncounter({1: 1}, {2: 3}) == O.bc_vclock({1: 1}) + O.bc_vclock({2: 3})  # p then n
+    assert O.bc_gset({5, 1}) == struct.pack("<QQQ", 2, 1, 5)
+    b = O.bc_orswot({0: 2}, {10: {0: 2}}, [({1: 4}, [10, 11])])
+    assert b == (O.bc_vclock({0: 2}) + struct.pack("<QQ", 1, 10) + O.bc_vclock({0: 2}) + struct.pack("<Q", 1)
+                 + O.bc_vclock({1: 4}) + struct.pack("<QQQ", 2, 10, 11))
+
+
+def test_round_trips():
+    rng = np.random.default_rng(0)
+    for _ in range(50):
+        dots = {int(a): int(c) for a, c in zip(rng.integers(0, 2**32, 20), rng.integers(1, 2**63, 20))}
+        assert O.unbc_vclock(O.bc_vclock(dots))[0] == dots
+        s = set(int(x) for x in rng.integers(0, 2**63, 30))
+        assert O.unbc_gset(O.bc_gset(s))[0] == s
+        ent = {int(m): {int(a): int(rng.integers(1, 99))} for m, a in zip(rng.integers(0, 2**60, 5), range(5))}
+        de = [({9: 3}, [1, 2]), ({9: 3}, [4]), ({8: 1}, [])]
+        c, e, d, pos = O.unbc_orswot(O.bc_orswot({1: 1}, ent, de, order=list(ent)[::-1]))
+        assert c == {1: 1} and e == ent and d == {((9, 3),): {1, 2, 4}, ((8, 1),): set()}
