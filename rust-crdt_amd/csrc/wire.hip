@@ -118,7 +118,27 @@ struct IngestPlan {
   u64 *def_off;  // [N+1] exclusive scan of dcount
   u64 *def_clock, *def_members;
   unsigned long long def_cap;
+  unsigned long long dict_words;  // > 0: the dictionaries are staged in LDS (this many u64 words)
 };
+
+// Stage the block's dictionaries in LDS (dependent binary-search loads then hit LDS, not L2):
+// layout [actors u32 (A, padded to 8 B) | elems or members u64].  Returns the row area.
+__device__ __forceinline__ u64 *stage_dicts(const IngestPlan &p, u64 *lds, const uint32_t *&actors, const u64 *&elems,
+                                            const u64 *&members) {
+  if (!p.dict_words) return lds;
+  uint32_t *la = reinterpret_cast<uint32_t *>(lds);
+  const unsigned long long aw = p.actors ? (p.A + 1) / 2 : 0;
+  for (unsigned long long i = threadIdx.x; i < (p.actors ? p.A : 0); i += blockDim.x) la[i] = p.actors[i];
+  u64 *lu = lds + aw;
+  const u64 *src = p.members ? p.members : p.elems;
+  const unsigned long long nu = p.members ? p.M : (p.elems ? p.U : 0);
+  for (unsigned long long i = threadIdx.x; i < nu; i += blockDim.x) lu[i] = src[i];
+  __syncthreads();
+  if (p.actors) actors = la;
+  if (p.members) members = lu;
+  else if (p.elems) elems = lu;
+  return lds + p.dict_words;
+}
 
 __device__ __forceinline__ bool frame_of(const IngestPlan &p, unsigned long long s, Frame &f) {
   const u64 b = p.frame_off[s], e = p.frame_off[s + 1];
@@ -133,7 +153,9 @@ __global__ __launch_bounds__(kBlock) void vclock_ingest_kernel(IngestPlan p) {
   extern __shared__ u64 lds[];
   const int lane = threadIdx.x % kWave, wib = threadIdx.x / kWave;
   const int wpb = blockDim.x / kWave;
-  u64 *row = lds + (unsigned long long)wib * p.A;
+  const uint32_t *actors = p.actors;
+  const u64 *elems = p.elems, *members = p.members;
+  u64 *row = stage_dicts(p, lds, actors, elems, members) + (unsigned long long)wib * p.A;
   for (unsigned long long s = (unsigned long long)blockIdx.x * wpb + wib; s < p.N;
        s += (unsigned long long)gridDim.x * wpb) {
     unsigned st = 0;
@@ -146,7 +168,7 @@ __global__ __launch_bounds__(kBlock) void vclock_ingest_kernel(IngestPlan p) {
       unsigned long long k = 0;
       for (int c = 0; c < p.nclocks; ++c) {
         if (k != ~0ull) {
-          k = parse_vclock(f, k, p.actors, p.A, row, lane, st);
+          k = parse_vclock(f, k, actors, p.A, row, lane, st);
         } else {  // after a truncated clock: the remaining clocks are empty
           for (unsigned long long a = lane; a < p.A; a += kWave) row[a] = 0;
           wfence();
@@ -166,7 +188,9 @@ __global__ __launch_bounds__(kBlock) void gset_ingest_kernel(IngestPlan p) {
   const int lane = threadIdx.x % kWave, wib = threadIdx.x / kWave;
   const int wpb = blockDim.x / kWave;
   const unsigned long long W = (p.U + 63) / 64;
-  u64 *row = lds + (unsigned long long)wib * W;
+  const uint32_t *actors = p.actors;
+  const u64 *elems = p.elems, *members = p.members;
+  u64 *row = stage_dicts(p, lds, actors, elems, members) + (unsigned long long)wib * W;
   for (unsigned long long s = (unsigned long long)blockIdx.x * wpb + wib; s < p.N;
        s += (unsigned long long)gridDim.x * wpb) {
     unsigned st = 0;
@@ -181,7 +205,7 @@ __global__ __launch_bounds__(kBlock) void gset_ingest_kernel(IngestPlan p) {
       const u64 nn = n < (f.nw - 2) / 2 ? n : (f.nw - 2) / 2;
       bool miss = false;
       for (unsigned long long i = lane; i < nn; i += kWave) {
-        const long long b = find_u64(p.elems, p.U, rd64(f.w, 2 + 2 * i), i);
+        const long long b = find_u64(elems, p.U, rd64(f.w, 2 + 2 * i), i);
         if (b < 0) miss = true;
         else atomicOr(row + b / 64, 1ull << (b % 64));
       }
@@ -218,7 +242,9 @@ __global__ __launch_bounds__(kBlock) void orswot_ingest_kernel(IngestPlan p) {
   extern __shared__ u64 lds[];
   const int lane = threadIdx.x % kWave, wib = threadIdx.x / kWave;
   const int wpb = blockDim.x / kWave;
-  u64 *row = lds + (unsigned long long)wib * p.A;
+  const uint32_t *actors = p.actors;
+  const u64 *elems = p.elems, *members = p.members;
+  u64 *row = stage_dicts(p, lds, actors, elems, members) + (unsigned long long)wib * p.A;
   for (unsigned long long s = (unsigned long long)blockIdx.x * wpb + wib; s < p.N;
        s += (unsigned long long)gridDim.x * wpb) {
     unsigned st = 0;
@@ -228,7 +254,7 @@ __global__ __launch_bounds__(kBlock) void orswot_ingest_kernel(IngestPlan p) {
       st = kWireBad;
       for (unsigned long long a = lane; a < p.A; a += kWave) p.out[s * p.row_stride + a] = 0;
     } else {
-      unsigned long long k = parse_vclock(f, 0, p.actors, p.A, row, lane, st);
+      unsigned long long k = parse_vclock(f, 0, actors, p.A, row, lane, st);
       store_row<u64>(p.out + s * p.row_stride, row, p.A, lane);
       wfence();
       if (k != ~0ull && k + 2 <= f.nw) {
@@ -240,8 +266,8 @@ __global__ __launch_bounds__(kBlock) void orswot_ingest_kernel(IngestPlan p) {
             k = ~0ull;
             break;
           }
-          const long long mi = find_u64(p.members, p.M, rd64(f.w, k), p.M);
-          k = parse_vclock(f, k + 2, p.actors, p.A, row, lane, st);
+          const long long mi = find_u64(members, p.M, rd64(f.w, k), p.M);
+          k = parse_vclock(f, k + 2, actors, p.A, row, lane, st);
           if (mi < 0) {
             st |= kWireMissing;
           } else {
@@ -272,7 +298,9 @@ __global__ __launch_bounds__(kBlock) void orswot_ingest_deferred_kernel(IngestPl
   extern __shared__ u64 lds[];
   const int lane = threadIdx.x % kWave, wib = threadIdx.x / kWave;
   const int wpb = blockDim.x / kWave;
-  u64 *row = lds + (unsigned long long)wib * (p.A + p.Mw);
+  const uint32_t *actors = p.actors;
+  const u64 *elems = p.elems, *members = p.members;
+  u64 *row = stage_dicts(p, lds, actors, elems, members) + (unsigned long long)wib * (p.A + p.Mw);
   u64 *bits = row + p.A;
   for (unsigned long long s = (unsigned long long)blockIdx.x * wpb + wib; s < p.N;
        s += (unsigned long long)gridDim.x * wpb) {
@@ -284,7 +312,7 @@ __global__ __launch_bounds__(kBlock) void orswot_ingest_deferred_kernel(IngestPl
     unsigned long long k = p.dpos[s];
     const u64 d0 = p.def_off[s];
     for (u64 j = 0; j < n && k != ~0ull; ++j) {
-      k = parse_vclock(f, k, p.actors, p.A, row, lane, st);
+      k = parse_vclock(f, k, actors, p.A, row, lane, st);
       for (unsigned long long w = lane; w < p.Mw; w += kWave) bits[w] = 0;
       wfence();
       if (k == ~0ull || k + 2 > f.nw) {
@@ -299,7 +327,7 @@ __global__ __launch_bounds__(kBlock) void orswot_ingest_deferred_kernel(IngestPl
       }
       bool miss = false;
       for (unsigned long long i = lane; i < m; i += kWave) {
-        const long long b = find_u64(p.members, p.M, rd64(f.w, k + 2 * i), p.M);
+        const long long b = find_u64(members, p.M, rd64(f.w, k + 2 * i), p.M);
         if (b < 0) miss = true;
         else atomicOr(bits + b / 64, 1ull << (b % 64));
       }
@@ -622,9 +650,11 @@ static int vclock_ingest_common(crdt_ctx *ctx, const uint8_t *bytes, const uint6
   p.row_stride = row_stride;
   p.nclocks = nclocks;
   p.status = status;
+  const size_t dw = (A + 1) / 2;
+  if ((dw + wpb * A) * 8 <= 64 * 1024) p.dict_words = dw;
   timing_begin(ctx, "wire_ingest");
-  hipLaunchKernelGGL(vclock_ingest_kernel, dim3(wave_grid(ctx, N, wpb, 32)), dim3(wpb * kWave), wpb * A * 8,
-                     ctx->stream, p);
+  hipLaunchKernelGGL(vclock_ingest_kernel, dim3(wave_grid(ctx, N, wpb, 32)), dim3(wpb * kWave),
+                     (p.dict_words + wpb * A) * 8, ctx->stream, p);
   timing_end(ctx);
   CRDT_HIP(ctx, hipGetLastError());
   return CRDT_OK;
@@ -661,9 +691,10 @@ int crdt_gset_ingest(crdt_ctx *ctx, const uint8_t *bytes, const uint64_t *frame_
   p.out = (u64 *)out;
   p.row_stride = row_stride;
   p.status = status;
+  if ((U + wpb * W) * 8 <= 64 * 1024) p.dict_words = U;
   timing_begin(ctx, "wire_ingest");
-  hipLaunchKernelGGL(gset_ingest_kernel, dim3(wave_grid(ctx, N, wpb, 32)), dim3(wpb * kWave), wpb * W * 8, ctx->stream,
-                     p);
+  hipLaunchKernelGGL(gset_ingest_kernel, dim3(wave_grid(ctx, N, wpb, 32)), dim3(wpb * kWave),
+                     (p.dict_words + wpb * W) * 8, ctx->stream, p);
   timing_end(ctx);
   CRDT_HIP(ctx, hipGetLastError());
   return CRDT_OK;
@@ -727,15 +758,17 @@ int crdt_orswot_ingest(crdt_ctx *ctx, const uint8_t *bytes, const uint64_t *fram
   p.def_clock = (u64 *)def_clock;
   p.def_members = (u64 *)def_members;
   p.def_cap = def_cap;
+  const size_t dw = (A + 1) / 2 + M;
+  if ((dw + wpb * (A + Mw)) * 8 <= 64 * 1024) p.dict_words = dw;
   const unsigned grid = wave_grid(ctx, N, wpb, 32);
   timing_begin(ctx, "wire_ingest");
-  hipLaunchKernelGGL(orswot_ingest_kernel, dim3(grid), dim3(wpb * kWave), wpb * A * 8, ctx->stream, p);
+  hipLaunchKernelGGL(orswot_ingest_kernel, dim3(grid), dim3(wpb * kWave), (p.dict_words + wpb * A) * 8, ctx->stream, p);
   CRDT_HIP(ctx, hipGetLastError());
   unsigned long long D = 0;
   if (int rc = exclusive_scan(ctx, dcount, (u64 *)def_off, N, sc, &D)) return rc;
   if (D)
-    hipLaunchKernelGGL(orswot_ingest_deferred_kernel, dim3(grid), dim3(wpb * kWave), wpb * (A + Mw) * 8, ctx->stream,
-                       p);
+    hipLaunchKernelGGL(orswot_ingest_deferred_kernel, dim3(grid), dim3(wpb * kWave),
+                       (p.dict_words + wpb * (A + Mw)) * 8, ctx->stream, p);
   timing_end(ctx);
   CRDT_HIP(ctx, hipGetLastError());
   if (n_def) *n_def = D;
