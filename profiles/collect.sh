@@ -3,7 +3,7 @@
 #   1. kernel trace + stats of the bench command     -> gpurun_out/prof_<tag>/
 #   2. FETCH_SIZE pass, 3. WRITE_SIZE pass (separate: FETCH_SIZE takes 3 TCC slots, WRITE_SIZE 2)
 # then summarises them into profiles/<tag>_*.csv / .json (scripts/summarize_prof.py).
-tag=${1:-r01}
+tag=${1:-r02}
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 export TMPDIR=/tmp
 mkdir -p gpurun_out
