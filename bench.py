@@ -105,6 +105,20 @@ def cpu_baseline(args):
             reps += 1
         return done_rows / fold_s, reps, fold_s
 
+    def run_dense(threads, rows_per_rep, seconds):
+        """SURVEY §8d CPU timing (3): the same fold on the dense SoA rows (elementwise u64 max over
+        row ranges per thread, oracle_dense_max_mt) — the CPU's own bandwidth roofline."""
+        done_rows, fold_s, reps = 0, 0.0, 0
+        width = args.actors
+        m = O.synth_matrix(SEED_V if args.workload == "c5" else SEED_G, rows_per_rep, width, 0)
+        t_start = time.time()
+        while fold_s < seconds and time.time() - t_start < 4 * seconds:
+            _, t = O.dense_max_mt(m, threads)
+            fold_s += t
+            done_rows += rows_per_rep
+            reps += 1
+        return done_rows / fold_s, reps, fold_s, m.nbytes
+
     if args.workload == "c5":
         v1, reps1, s1 = run_c5(1, 4096, args.cpu_seconds / 2)
         vT, repsT, sT = run_c5(T, 2048, args.cpu_seconds)
@@ -115,6 +129,7 @@ def cpu_baseline(args):
         vT, repsT, sT = run(T, 4096, args.cpu_seconds)
         what = f"{repsT} x ({T}x4096 GCounter x {args.actors} + {T}x4096 PNCounter x 2x{args.actors}) replicas"
         one = f"{reps1} x (16384 + 16384) replicas, {s1:.2f} s of fold"
+    vd, repsd, sd, nb = run_dense(T, 1 << 18, max(1.0, args.cpu_seconds / 4))
     return {
         "value": vT,
         "unit": "replica-merges/s",
@@ -124,6 +139,10 @@ def cpu_baseline(args):
                    f"(oracle/ref_fold.cpp) split over {T} threads (this job's CPU share of the GPU box) + final "
                    f"merge of the partials, map ingest excluded; {sT:.2f} s of fold"),
         "single_core": {"value": v1, "cores": 1, "sample": one},
+        "dense_soa": {"value": vd, "cores": T, "GBs": vd * nb / (1 << 18) / 1e9,
+                      "sample": (f"{repsd} x elementwise max over {1 << 18} dense rows x {args.actors} u64 "
+                                 f"({nb / 2**20:.0f} MiB, {sd:.2f} s) split over {T} threads (oracle_dense_max_mt): "
+                                 "the CPU fold without the reference's map containers")},
     }
 
 

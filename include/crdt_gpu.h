@@ -16,7 +16,8 @@
  *
  * States are dense structure-of-arrays in device memory (HBM): actors/members are interned
  * to dense indices by the caller, an absent actor is a 0 counter (exact: VClock::apply_dot
- * never stores 0, vclock.rs:155-159).  All pointers are DEVICE pointers unless stated.
+ * never stores 0, vclock.rs:155-159).  All pointers are DEVICE pointers unless stated or the
+ * ctx is in CRDT_MEM_HOST mode (crdt_ctx_set_mem_kind below).
  * Every stride is in 64-bit words.  Results are bit-exact against the reference fold.
  *
  * Conventions
@@ -75,6 +76,27 @@ int crdt_ctx_timing_reset(crdt_ctx *ctx);
 /* Override launch-geometry knobs ("key=value,...", the CRDT_TUNE syntax read at create; see
  * DESIGN.md §3).  Results never depend on them; tests use it to exercise every staging path. */
 int crdt_ctx_tune(crdt_ctx *ctx, const char *spec);
+
+/* ---- memory kind (crdt_mem_kind) ---------------------------------------------------------
+ * CRDT_MEM_DEVICE (default): every buffer pointer is a device pointer and calls are
+ * asynchronous on the ctx stream.  CRDT_MEM_HOST: the buffers of
+ *     crdt_{vclock,gcounter,pncounter,gset}_lub_many / _merge_batch,
+ *     crdt_lwwreg_lub_many / _merge_batch
+ * are HOST pointers (pageable, or pinned by crdt_host_alloc for direct DMA); the library streams
+ * them through two ctx-owned device chunk buffers (tune key stage_kb, default 256 MiB each),
+ * overlapping the H2D copy of chunk k+1 with the fold of chunk k, and the call returns when the
+ * results are in host memory.  Results are identical to the device-pointer call.  In host mode
+ * crdt_lwwreg_lub_many needs out_marker and out_val; a device pointer is rejected (CRDT_EINVAL);
+ * every other entry point returns CRDT_EUNSUPPORTED. */
+#define CRDT_MEM_DEVICE 0
+#define CRDT_MEM_HOST 1
+int crdt_ctx_set_mem_kind(crdt_ctx *ctx, int kind);
+/* The ctx's current kind, or CRDT_EINVAL for a NULL ctx. */
+int crdt_ctx_mem_kind(const crdt_ctx *ctx);
+/* Page-locked host memory (hipHostMalloc): host-mode inputs in it are copied by DMA at the full
+ * link rate.  Free with crdt_host_free. */
+int crdt_host_alloc(size_t bytes, void **out);
+int crdt_host_free(void *p);
 
 /* ---- VClock / GCounter: elementwise-max lub ----------------------------------------------
  * Replaces VClock::merge (vclock.rs:130-136, via apply_dot :155-159) and GCounter::merge

@@ -738,6 +738,8 @@ def lib():
         L.oracle_orswot_apply_streams.restype = ctypes.c_double
         L.oracle_counter_fold_mt.argtypes = [P, S, S, S, ctypes.c_int, ctypes.c_int, P]
         L.oracle_counter_fold_mt.restype = ctypes.c_double
+        L.oracle_dense_max_mt.argtypes = [P, S, S, S, ctypes.c_int, P]
+        L.oracle_dense_max_mt.restype = ctypes.c_double
         _LIB = L
     return _LIB
 
@@ -766,6 +768,15 @@ def counter_fold_mt(rows: np.ndarray, pn: bool, threads: int) -> Tuple[np.ndarra
     out = np.zeros(rows.shape[1], np.uint64)
     t = lib().oracle_counter_fold_mt(_p(rows), rows.shape[0], rows.shape[1], rows.shape[1], int(pn), int(threads),
                                      _p(out))
+    return out, t
+
+
+def dense_max_mt(rows: np.ndarray, threads: int) -> Tuple[np.ndarray, float]:
+    """Elementwise max of dense u64 rows over `threads` host threads (oracle_dense_max_mt): the
+    dense-SoA CPU fold of SURVEY §8d CPU timing (3).  Returns (max row, seconds)."""
+    rows = _c64(rows)
+    out = np.zeros(rows.shape[1], np.uint64)
+    t = lib().oracle_dense_max_mt(_p(rows), rows.shape[0], rows.shape[1], rows.shape[1], int(threads), _p(out))
     return out, t
 
 

@@ -397,6 +397,36 @@ double oracle_counter_fold_mt(const uint64_t *rows, size_t R, size_t W, size_t s
   return t1 - t0;
 }
 
+// SURVEY §8d CPU timing (3), "the honest CPU roofline": the same fold on the DENSE SoA rows
+// (elementwise max of u64 rows, the restatement of vclock.rs:130-136 under the dense convention),
+// split over `threads` host threads by row ranges, partials maxed at the end.  Returns seconds.
+double oracle_dense_max_mt(const uint64_t *rows, size_t R, size_t W, size_t stride, int threads, uint64_t *out) {
+  const size_t T = threads < 1 ? 1 : (size_t)threads;
+  std::vector<std::vector<uint64_t>> part(T, std::vector<uint64_t>(W, 0));
+  std::atomic<int> ready{0}, go{0};
+  std::vector<std::thread> pool;
+  for (size_t t = 0; t < T; ++t)
+    pool.emplace_back([&, t] {
+      const size_t lo = t * R / T, hi = (t + 1) * R / T;
+      uint64_t *acc = part[t].data();
+      ready.fetch_add(1);
+      while (!go.load(std::memory_order_acquire)) std::this_thread::yield();
+      for (size_t r = lo; r < hi; ++r) {
+        const uint64_t *row = rows + r * stride;
+        for (size_t a = 0; a < W; ++a) acc[a] = row[a] > acc[a] ? row[a] : acc[a];
+      }
+    });
+  while (ready.load() < (int)T) std::this_thread::yield();
+  double t0 = now_s();
+  go.store(1, std::memory_order_release);
+  for (auto &th : pool) th.join();
+  for (size_t a = 0; a < W; ++a) out[a] = 0;
+  for (size_t t = 0; t < T; ++t)
+    for (size_t a = 0; a < W; ++a) out[a] = part[t][a] > out[a] ? part[t][a] : out[a];
+  double t1 = now_s();
+  return t1 - t0;
+}
+
 // Pairwise: self[i].merge(other[i]) on dense rows (A counters), in place.
 void oracle_vclock_merge_pairs(uint64_t *self, const uint64_t *other, size_t N, size_t A) {
   for (size_t i = 0; i < N; ++i) {

@@ -19,6 +19,8 @@ CRDT_EUNSUPPORTED = -4
 CRDT_ECOMM = -5
 CRDT_UNIQUE_ID_BYTES = 128
 CRDT_ACCUMULATE = 0x1
+CRDT_MEM_DEVICE = 0
+CRDT_MEM_HOST = 1
 
 # Every symbol declared in include/crdt_gpu.h (checked by tests/test_abi.py).
 EXPORTS = (
@@ -43,6 +45,7 @@ EXPORTS = (
     "crdt_vclock_egress", "crdt_pncounter_egress", "crdt_gset_egress", "crdt_lwwreg_egress", "crdt_orswot_egress",
     "crdt_orswot_forget_batch", "crdt_map_forget_batch", "crdt_map_apply_batch",
     "crdt_orswot_merge_batch", "crdt_map_merge_batch",
+    "crdt_ctx_set_mem_kind", "crdt_ctx_mem_kind", "crdt_host_alloc", "crdt_host_free",
 )
 
 
@@ -139,6 +142,10 @@ _SIGS = {
     "crdt_ctx_timing": ([P, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(U64)], ctypes.c_int),
     "crdt_ctx_timing_reset": ([P], ctypes.c_int),
     "crdt_ctx_tune": ([P, ctypes.c_char_p], ctypes.c_int),
+    "crdt_ctx_set_mem_kind": ([P, ctypes.c_int], ctypes.c_int),
+    "crdt_ctx_mem_kind": ([P], ctypes.c_int),
+    "crdt_host_alloc": ([S, ctypes.POINTER(P)], ctypes.c_int),
+    "crdt_host_free": ([P], ctypes.c_int),
     "crdt_synth_fill": ([P, P, S, S, S, S, U64, ctypes.c_int], ctypes.c_int),
     "crdt_synth_orswot": ([P, P, P, S, S, S, S, U64, U64], ctypes.c_int),
     "crdt_synth_orswot_rm": ([P, P, S, S, S, P, P, P], ctypes.c_int),

@@ -90,12 +90,14 @@ using namespace crdt;
 extern "C" int crdt_vclock_apply_batch(crdt_ctx *ctx, uint64_t *states, size_t N, size_t A, size_t row_stride,
                                        const uint32_t *state_idx, const uint32_t *actor, const uint64_t *counter,
                                        size_t n_ops, uint32_t *bad) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
   return apply_ops(ctx, 0, false, states, N, A, row_stride, state_idx, actor, counter, nullptr, n_ops, bad);
 }
 
 extern "C" int crdt_gcounter_apply_batch(crdt_ctx *ctx, uint64_t *states, size_t N, size_t A, size_t row_stride,
                                          const uint32_t *state_idx, const uint32_t *actor, const uint64_t *counter,
                                          size_t n_ops, uint32_t *bad) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
   return apply_ops(ctx, 0, false, states, N, A, row_stride, state_idx, actor, counter, nullptr, n_ops, bad);
 }
 
@@ -103,11 +105,13 @@ extern "C" int crdt_pncounter_apply_batch(crdt_ctx *ctx, uint64_t *states, size_
                                           const uint32_t *state_idx, const uint32_t *actor,
                                           const uint64_t *counter, const uint8_t *dir, size_t n_ops,
                                           uint32_t *bad) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
   return apply_ops(ctx, 0, true, states, N, A, row_stride, state_idx, actor, counter, dir, n_ops, bad);
 }
 
 extern "C" int crdt_gset_apply_batch(crdt_ctx *ctx, uint64_t *states, size_t N, size_t U, size_t row_stride,
                                      const uint32_t *state_idx, const uint32_t *element, size_t n_ops,
                                      uint32_t *bad) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
   return apply_ops(ctx, 1, false, states, N, U, row_stride, state_idx, element, nullptr, nullptr, n_ops, bad);
 }

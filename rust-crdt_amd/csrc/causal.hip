@@ -234,6 +234,7 @@ using namespace crdt;
 
 extern "C" int crdt_vclock_pair_op(crdt_ctx *ctx, int op, uint64_t *out, const uint64_t *x, const uint64_t *y,
                                    size_t N, size_t A, size_t out_stride, size_t x_stride, size_t y_stride) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
   CRDT_CHECK_CTX(ctx);
   if (op != CRDT_PAIR_GLB && op != CRDT_PAIR_FORGET) return fail(ctx, CRDT_EINVAL, "vclock_pair_op: op %d", op);
   if (N == 0 || A == 0) return CRDT_OK;
@@ -252,6 +253,7 @@ extern "C" int crdt_vclock_pair_op(crdt_ctx *ctx, int op, uint64_t *out, const u
 
 extern "C" int crdt_vclock_partial_cmp(crdt_ctx *ctx, const uint64_t *x, const uint64_t *y, size_t N, size_t A,
                                        size_t x_stride, size_t y_stride, int8_t *out) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
   CRDT_CHECK_CTX(ctx);
   if (N == 0) return CRDT_OK;
   if (!out || (A > 0 && (!x || !y))) return fail(ctx, CRDT_EINVAL, "vclock_partial_cmp: NULL buffer");
@@ -269,6 +271,7 @@ extern "C" int crdt_vclock_partial_cmp(crdt_ctx *ctx, const uint64_t *x, const u
 
 extern "C" int crdt_vclock_cmp_matrix(crdt_ctx *ctx, const uint64_t *x, size_t N, size_t A, size_t x_stride,
                                       int8_t *out) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
   CRDT_CHECK_CTX(ctx);
   if (N == 0) return CRDT_OK;
   if (!out || (A > 0 && !x)) return fail(ctx, CRDT_EINVAL, "vclock_cmp_matrix: NULL buffer");
@@ -304,10 +307,12 @@ static int read_rows(crdt_ctx *ctx, int pn, const uint64_t *in, size_t N, size_t
 
 extern "C" int crdt_gcounter_read(crdt_ctx *ctx, const uint64_t *in, size_t N, size_t A, size_t row_stride,
                                   uint64_t *out) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
   return read_rows(ctx, 0, in, N, A, row_stride, out);
 }
 
 extern "C" int crdt_pncounter_read(crdt_ctx *ctx, const uint64_t *in, size_t N, size_t A, size_t row_stride,
                                    uint64_t *out) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
   return read_rows(ctx, 1, in, N, A, row_stride, out);
 }

@@ -5,6 +5,7 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <map>
 #include <string>
@@ -61,6 +62,8 @@ struct Tune {
   int rows_blocks_per_cu = 0;  // row-pair / row-reduction kernels (causal.hip); 0 = per-kernel default
   int apply_hot_slots = 8;     // Orswot apply: deferred slots kept in LDS per state (the rest in HBM)
   int map_forget_vec2 = 1;     // Map forget: 16-byte pieces per lane where the shape allows it
+  int map_pair_reg = 1;        // Map merge_batch, V <= 4: 1 sub-wave register kernel, 2 whole-wave one, 0 generic
+  int stage_kb = 262144;       // CRDT_MEM_HOST: bytes per device chunk buffer (KiB; two buffers)
 };
 
 struct PendingTiming {
@@ -102,6 +105,15 @@ struct crdt_ctx {
   void (*comm_destroy)(void *) = nullptr;
   void *sbuf[8] = {};
   size_t sbuf_bytes[8] = {};
+  // Host-memory mode (csrc/host_stage.hip): CRDT_MEM_DEVICE / CRDT_MEM_HOST, the copy stream, two
+  // device chunk buffers with their copied / free events, and the device accumulator.
+  int mem_kind = CRDT_MEM_DEVICE;
+  hipStream_t hstream = nullptr;
+  void *hbuf[2] = {};
+  size_t hbuf_bytes = 0;
+  void *hacc = nullptr;
+  size_t hacc_bytes = 0;
+  hipEvent_t hcopied[2] = {}, hfree[2] = {};
 };
 
 namespace crdt {
@@ -166,6 +178,20 @@ int lattice_lub_many(crdt_ctx *ctx, Op op, const u64 *in, size_t G, size_t R, si
 int lattice_merge_batch(crdt_ctx *ctx, Op op, u64 *self, const u64 *other, size_t N, size_t W,
                         size_t self_stride, size_t other_stride);
 
+// Host-memory mode (host_stage.hip): the same entry points over host pointers, staged in chunks.
+int lattice_lub_many_host(crdt_ctx *ctx, Op op, const u64 *in, size_t G, size_t R, size_t W,
+                          size_t row_stride, size_t group_stride, u64 *out, size_t out_stride,
+                          unsigned flags);
+int lattice_merge_batch_host(crdt_ctx *ctx, Op op, u64 *self, const u64 *other, size_t N, size_t W,
+                             size_t self_stride, size_t other_stride);
+int lww_lub_many_dev(crdt_ctx *ctx, const u64 *marker, const u64 *val, size_t G, size_t R, size_t group_stride,
+                     u64 *out_marker, u64 *out_val, u64 *first_conflict, unsigned flags);
+int lww_merge_batch_dev(crdt_ctx *ctx, u64 *sm, u64 *sv, const u64 *om, const u64 *ov, size_t N, uint8_t *conflict);
+int lww_lub_many_host(crdt_ctx *ctx, const u64 *marker, const u64 *val, size_t G, size_t R, size_t group_stride,
+                      u64 *out_marker, u64 *out_val, u64 *first_conflict, unsigned flags);
+int lww_merge_batch_host(crdt_ctx *ctx, u64 *sm, u64 *sv, const u64 *om, const u64 *ov, size_t N, uint8_t *conflict);
+void free_stage(crdt_ctx *ctx);
+
 // Wave-uniform row-group loop: every lane runs the same iterations (rows past N are masked),
 // so group-wide votes and shuffles see the whole wave.
 #define ROW_GROUP_LOOP(N, lr_log)                                                                  \
@@ -195,4 +221,13 @@ inline int row_lr_log(unsigned long long pieces) {
   do {                                                 \
     hipError_t _e = (expr);                            \
     if (_e != hipSuccess) return crdt::hip_fail((ctx), _e, #expr); \
+  } while (0)
+
+// Entry points without a host-memory path: refuse CRDT_MEM_HOST instead of reading host
+// pointers as device memory (host_stage.hip lists the ones that have one).
+#define CRDT_DEVICE_MEM_ONLY(ctx)                                                              \
+  do {                                                                                         \
+    if ((ctx) && (ctx)->mem_kind != CRDT_MEM_DEVICE)                                            \
+      return crdt::fail((ctx), CRDT_EUNSUPPORTED, "%s: device pointers only (CRDT_MEM_HOST is " \
+                        "supported by the lattice and lwwreg lub_many / merge_batch)", __func__); \
   } while (0)

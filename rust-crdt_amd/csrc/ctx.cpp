@@ -210,6 +210,8 @@ static void apply_tune(crdt_ctx *ctx, const char *t) {
       else if (k == "rbpc" && v > 0) ctx->tune.rows_blocks_per_cu = v;
       else if (k == "hot" && v >= 0 && v <= 64) ctx->tune.apply_hot_slots = v;
       else if (k == "mfv2") ctx->tune.map_forget_vec2 = v != 0;
+      else if (k == "stage_kb" && v >= 4) ctx->tune.stage_kb = v;
+      else if (k == "mpreg" && v >= 0 && v <= 2) ctx->tune.map_pair_reg = v;
     }
     pos = end + 1;
   }
@@ -250,6 +252,7 @@ int crdt_ctx_destroy(crdt_ctx *ctx) {
   if (ctx->dscratch) (void)hipFree(ctx->dscratch);
   if (ctx->pinned) (void)hipHostFree(ctx->pinned);
   if (ctx->pinned_done) (void)hipEventDestroy(ctx->pinned_done);
+  free_stage(ctx);
   if (ctx->comm && ctx->comm_destroy) ctx->comm_destroy(ctx->comm);
   for (void *b : ctx->sbuf)
     if (b) (void)hipFree(b);

@@ -321,6 +321,7 @@ extern "C" int crdt_orswot_forget_batch(crdt_ctx *ctx, uint64_t *clock, size_t c
                                         size_t entry_mstride, size_t entry_sstride, size_t N, size_t M, size_t A,
                                         const uint64_t *y, size_t y_stride, uint64_t *def_clock,
                                         const uint32_t *def_state, size_t D, uint8_t *def_keep) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
   CRDT_CHECK_CTX(ctx);
   if (N == 0 || A == 0) return CRDT_OK;
   if (!clock || !y || (M && !entries) || (D && (!def_clock || !def_state || !def_keep)))
@@ -348,6 +349,7 @@ extern "C" int crdt_orswot_forget_batch(crdt_ctx *ctx, uint64_t *clock, size_t c
 
 extern "C" int crdt_map_forget_batch(crdt_ctx *ctx, const crdt_map_states *m, const uint64_t *y, size_t y_stride,
                                      uint64_t *def_clock, const uint32_t *def_state, size_t D, uint8_t *def_keep) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
   CRDT_CHECK_CTX(ctx);
   if (!m) return fail(ctx, CRDT_EINVAL, "map_forget_batch: NULL states");
   const size_t N = m->N, K = m->K, A = m->A, V = m->V;

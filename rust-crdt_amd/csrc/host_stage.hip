@@ -1,0 +1,365 @@
+// Host-memory mode (crdt_mem_kind, SURVEY §6 ABI row): with crdt_ctx_set_mem_kind(ctx,
+// CRDT_MEM_HOST) the lattice and LWWReg entry points take HOST pointers — the form a Rust
+// `lub_many(replicas: Vec<Self>)` / `merge_batch(&mut [Self], Vec<Self>)` starts from — and stage
+// them through two ctx-owned device chunk buffers:
+//
+//   copy stream:  H2D chunk k -> buf[k&1]          (waits until the fold of chunk k-2 left it)
+//   ctx stream:   fold / merge of chunk k with CRDT_ACCUMULATE into a device accumulator
+//                 (waits for the copy), then the D2H of results
+//
+// so PCIe transfers of chunk k+1 overlap the HBM pass over chunk k, and inputs larger than the
+// device's free memory stream through a bounded window.  A chunked lattice fold is the same fold
+// (max / or are associative and commutative, vclock.rs:130-136, gset.rs:38-40); the chunked LWW
+// fold continues the exact left fold with CRDT_ACCUMULATE (lwwreg.rs:43-45 -> update :84-98) and
+// keeps the FIRST conflicting merge over the whole group by offsetting each chunk's index.
+// Host-mode calls are synchronous: results are in the caller's host memory on return.
+// Pinned host memory (crdt_host_alloc) is DMA'd directly; pageable memory goes through the HIP
+// runtime's own staging.  Entry points without a host path fail with CRDT_EUNSUPPORTED in this
+// mode (CRDT_DEVICE_MEM_ONLY in each).
+#include "common.hpp"
+
+namespace crdt {
+
+__global__ void lww_fc_combine_kernel(u64 *glob, const u64 *chunk, u64 r0, unsigned long long n) {
+  const unsigned long long g = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n) return;
+  const u64 c = chunk[g];
+  if (glob[g] == ~0ull && c != ~0ull) glob[g] = c + r0;
+}
+
+static size_t stage_budget(crdt_ctx *ctx) { return (size_t)ctx->tune.stage_kb << 10; }
+
+// Two chunk buffers of >= bytes each, the copy stream and its events; plus `acc` bytes of
+// accumulator (ctx->hacc).
+static int ensure_stage(crdt_ctx *ctx, size_t bytes, size_t acc) {
+  if (!ctx->hstream) {
+    CRDT_HIP(ctx, hipStreamCreateWithFlags(&ctx->hstream, hipStreamNonBlocking));
+    for (int b = 0; b < 2; ++b) {
+      CRDT_HIP(ctx, hipEventCreateWithFlags(&ctx->hcopied[b], hipEventDisableTiming));
+      CRDT_HIP(ctx, hipEventCreateWithFlags(&ctx->hfree[b], hipEventDisableTiming));
+    }
+  }
+  if (bytes > ctx->hbuf_bytes) {
+    CRDT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    CRDT_HIP(ctx, hipStreamSynchronize(ctx->hstream));
+    for (auto &b : ctx->hbuf)
+      if (b) {
+        (void)hipFree(b);
+        b = nullptr;
+      }
+    ctx->hbuf_bytes = 0;
+    for (auto &b : ctx->hbuf)
+      if (hipMalloc(&b, bytes) != hipSuccess) {
+        b = nullptr;
+        return fail(ctx, CRDT_ENOMEM, "host staging: hipMalloc(%zu) failed", bytes);
+      }
+    ctx->hbuf_bytes = bytes;
+  }
+  if (acc > ctx->hacc_bytes) {
+    CRDT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (ctx->hacc) (void)hipFree(ctx->hacc);
+    ctx->hacc = nullptr;
+    ctx->hacc_bytes = 0;
+    if (hipMalloc(&ctx->hacc, acc) != hipSuccess) {
+      ctx->hacc = nullptr;
+      return fail(ctx, CRDT_ENOMEM, "host staging: accumulator hipMalloc(%zu) failed", acc);
+    }
+    ctx->hacc_bytes = acc;
+  }
+  return CRDT_OK;
+}
+
+// A device pointer passed in host mode is a caller error (the copies would read device memory
+// as if it were host memory): reject it.  Unregistered (pageable) and pinned host memory pass.
+static int check_host(crdt_ctx *ctx, const void *p, const char *what) {
+  if (!p) return CRDT_OK;
+  hipPointerAttribute_t a{};
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return CRDT_OK;
+  }
+  if (a.type == hipMemoryTypeDevice)
+    return fail(ctx, CRDT_EINVAL, "CRDT_MEM_HOST: %s is a device pointer", what);
+  return CRDT_OK;
+}
+
+// rows x width bytes from a pitched source to a pitched destination (pitch ignored for 1 row).
+static hipError_t copy_rows(void *dst, size_t dpitch, const void *src, size_t spitch, size_t width,
+                            size_t rows, hipMemcpyKind kind, hipStream_t s) {
+  if (rows == 0 || width == 0) return hipSuccess;
+  if (rows == 1 || (dpitch == width && spitch == width))
+    return hipMemcpyAsync(dst, src, width * rows, kind, s);
+  return hipMemcpy2DAsync(dst, dpitch, src, spitch, width, rows, kind, s);
+}
+
+#define STAGE_HIP(expr)                                      \
+  do {                                                       \
+    hipError_t _e = (expr);                                  \
+    if (_e != hipSuccess) return hip_fail(ctx, _e, #expr);   \
+  } while (0)
+
+// Chunk k may start copying once the kernel that read buffer k&1 two chunks ago has finished.
+static int begin_chunk(crdt_ctx *ctx, int b) {
+  STAGE_HIP(hipStreamWaitEvent(ctx->hstream, ctx->hfree[b], 0));
+  return CRDT_OK;
+}
+static int copied_chunk(crdt_ctx *ctx, int b) {
+  STAGE_HIP(hipEventRecord(ctx->hcopied[b], ctx->hstream));
+  STAGE_HIP(hipStreamWaitEvent(ctx->stream, ctx->hcopied[b], 0));
+  return CRDT_OK;
+}
+static int end_chunk(crdt_ctx *ctx, int b) {
+  STAGE_HIP(hipEventRecord(ctx->hfree[b], ctx->stream));
+  return CRDT_OK;
+}
+
+// Wait for both streams whatever happened, so no queued copy still reads caller memory.
+static int finish(crdt_ctx *ctx, int rc) {
+  const hipError_t a = hipStreamSynchronize(ctx->hstream);
+  const hipError_t b = hipStreamSynchronize(ctx->stream);
+  if (rc) return rc;
+  if (a != hipSuccess) return hip_fail(ctx, a, "hipStreamSynchronize(copy stream)");
+  if (b != hipSuccess) return hip_fail(ctx, b, "hipStreamSynchronize(ctx stream)");
+  return CRDT_OK;
+}
+
+static int lattice_lub_host_body(crdt_ctx *ctx, Op op, const u64 *in, size_t G, size_t R, size_t W,
+                                 size_t row_stride, size_t group_stride, u64 *out, size_t out_stride,
+                                 unsigned flags) {
+  const bool accumulate = flags & CRDT_ACCUMULATE;
+  const size_t rowb = W * 8, budget = stage_budget(ctx);
+  const size_t Gc = std::min(G, std::max<size_t>(1, budget / rowb));
+  const size_t Rc = R ? std::min(R, std::max<size_t>(1, budget / (Gc * rowb))) : 0;
+  if (int rc = ensure_stage(ctx, std::max<size_t>(1, Gc * Rc) * rowb, Gc * rowb)) return rc;
+  u64 *acc = static_cast<u64 *>(ctx->hacc);
+  const size_t ostride = G > 1 ? out_stride : W;
+  size_t k = 0;
+  for (size_t g0 = 0; g0 < G; g0 += Gc) {
+    const size_t gn = std::min(Gc, G - g0);
+    if (accumulate)
+      STAGE_HIP(copy_rows(acc, rowb, out + g0 * ostride, ostride * 8, rowb, gn, hipMemcpyHostToDevice, ctx->stream));
+    if (R == 0) {
+      if (int rc = lattice_lub_many(ctx, op, nullptr, gn, 0, W, W, 0, acc, W, flags)) return rc;
+    }
+    for (size_t r0 = 0; r0 < R; r0 += Rc, ++k) {
+      const size_t rn = std::min(Rc, R - r0);
+      const int b = (int)(k & 1);
+      u64 *buf = static_cast<u64 *>(ctx->hbuf[b]);
+      if (int rc = begin_chunk(ctx, b)) return rc;
+      const u64 *src = in + g0 * group_stride + r0 * row_stride;
+      if (row_stride == W || rn == 1) {  // each group's chunk is one contiguous run of rn rows
+        STAGE_HIP(copy_rows(buf, rn * rowb, src, group_stride * 8, rn * rowb, gn, hipMemcpyHostToDevice, ctx->hstream));
+      } else {
+        for (size_t g = 0; g < gn; ++g)
+          STAGE_HIP(copy_rows(buf + g * rn * W, rowb, src + g * group_stride, row_stride * 8, rowb, rn,
+                              hipMemcpyHostToDevice, ctx->hstream));
+      }
+      if (int rc = copied_chunk(ctx, b)) return rc;
+      const unsigned f = (r0 > 0 || accumulate) ? CRDT_ACCUMULATE : 0u;
+      if (int rc = lattice_lub_many(ctx, op, buf, gn, rn, W, W, rn * W, acc, W, f)) return rc;
+      if (int rc = end_chunk(ctx, b)) return rc;
+    }
+    STAGE_HIP(copy_rows(out + g0 * ostride, ostride * 8, acc, rowb, rowb, gn, hipMemcpyDeviceToHost, ctx->stream));
+  }
+  return CRDT_OK;
+}
+
+int lattice_lub_many_host(crdt_ctx *ctx, Op op, const u64 *in, size_t G, size_t R, size_t W,
+                          size_t row_stride, size_t group_stride, u64 *out, size_t out_stride,
+                          unsigned flags) {
+  if (G == 0 || W == 0) return CRDT_OK;
+  if (!out) return fail(ctx, CRDT_EINVAL, "lub_many: out is NULL");
+  if (G > 1 && out_stride < W)
+    return fail(ctx, CRDT_EINVAL, "lub_many: out_stride %zu < row width %zu", out_stride, W);
+  if (R > 0 && !in) return fail(ctx, CRDT_EINVAL, "lub_many: in is NULL");
+  if (R > 1 && row_stride < W)
+    return fail(ctx, CRDT_EINVAL, "lub_many: row_stride %zu < row width %zu", row_stride, W);
+  if (G > 1 && R > 0 && group_stride < (R - 1) * row_stride + W)
+    return fail(ctx, CRDT_EINVAL, "lub_many: group_stride %zu overlaps the previous group", group_stride);
+  if (int rc = check_host(ctx, in, "in")) return rc;
+  if (int rc = check_host(ctx, out, "out")) return rc;
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  return finish(ctx, lattice_lub_host_body(ctx, op, in, G, R, W, row_stride, group_stride, out, out_stride, flags));
+}
+
+static int lattice_merge_host_body(crdt_ctx *ctx, Op op, u64 *self, const u64 *other, size_t N, size_t W,
+                                   size_t self_stride, size_t other_stride) {
+  const size_t rowb = W * 8;
+  const size_t Nc = std::min(N, std::max<size_t>(1, stage_budget(ctx) / (2 * rowb)));
+  if (int rc = ensure_stage(ctx, 2 * Nc * rowb, 8)) return rc;
+  const size_t ss = N > 1 ? self_stride : W, os = N > 1 ? other_stride : W;
+  size_t k = 0;
+  for (size_t i0 = 0; i0 < N; i0 += Nc, ++k) {
+    const size_t n = std::min(Nc, N - i0);
+    const int b = (int)(k & 1);
+    u64 *ds = static_cast<u64 *>(ctx->hbuf[b]), *dO = ds + n * W;
+    if (int rc = begin_chunk(ctx, b)) return rc;
+    STAGE_HIP(copy_rows(ds, rowb, self + i0 * ss, ss * 8, rowb, n, hipMemcpyHostToDevice, ctx->hstream));
+    STAGE_HIP(copy_rows(dO, rowb, other + i0 * os, os * 8, rowb, n, hipMemcpyHostToDevice, ctx->hstream));
+    if (int rc = copied_chunk(ctx, b)) return rc;
+    if (int rc = lattice_merge_batch(ctx, op, ds, dO, n, W, W, W)) return rc;
+    STAGE_HIP(copy_rows(self + i0 * ss, ss * 8, ds, rowb, rowb, n, hipMemcpyDeviceToHost, ctx->stream));
+    if (int rc = end_chunk(ctx, b)) return rc;
+  }
+  return CRDT_OK;
+}
+
+int lattice_merge_batch_host(crdt_ctx *ctx, Op op, u64 *self, const u64 *other, size_t N, size_t W,
+                             size_t self_stride, size_t other_stride) {
+  if (N == 0 || W == 0) return CRDT_OK;
+  if (!self || !other) return fail(ctx, CRDT_EINVAL, "merge_batch: NULL buffer");
+  if (N > 1 && (self_stride < W || other_stride < W))
+    return fail(ctx, CRDT_EINVAL, "merge_batch: stride < row width %zu", W);
+  if (int rc = check_host(ctx, self, "self")) return rc;
+  if (int rc = check_host(ctx, other, "other")) return rc;
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  return finish(ctx, lattice_merge_host_body(ctx, op, self, other, N, W, self_stride, other_stride));
+}
+
+static int lww_lub_host_body(crdt_ctx *ctx, const u64 *marker, const u64 *val, size_t G, size_t R,
+                             size_t group_stride, u64 *out_marker, u64 *out_val, u64 *first_conflict,
+                             unsigned flags) {
+  const bool accumulate = flags & CRDT_ACCUMULATE;
+  const size_t budget = stage_budget(ctx);
+  const size_t Gc = std::min(G, std::max<size_t>(1, budget / 16));
+  const size_t Rc = std::min(R, std::max<size_t>(1, budget / (Gc * 16)));
+  if (int rc = ensure_stage(ctx, Gc * Rc * 16, Gc * 32)) return rc;
+  u64 *am = static_cast<u64 *>(ctx->hacc), *av = am + Gc, *fc = av + Gc, *fcc = fc + Gc;
+  const size_t gs = G > 1 ? group_stride : R;
+  size_t k = 0;
+  for (size_t g0 = 0; g0 < G; g0 += Gc) {
+    const size_t gn = std::min(Gc, G - g0);
+    if (accumulate) {
+      STAGE_HIP(hipMemcpyAsync(am, out_marker + g0, gn * 8, hipMemcpyHostToDevice, ctx->stream));
+      STAGE_HIP(hipMemcpyAsync(av, out_val + g0, gn * 8, hipMemcpyHostToDevice, ctx->stream));
+    }
+    for (size_t r0 = 0; r0 < R; r0 += Rc, ++k) {
+      const size_t rn = std::min(Rc, R - r0);
+      const int b = (int)(k & 1);
+      u64 *bm = static_cast<u64 *>(ctx->hbuf[b]), *bv = bm + gn * rn;
+      if (int rc = begin_chunk(ctx, b)) return rc;
+      STAGE_HIP(copy_rows(bm, rn * 8, marker + g0 * gs + r0, gs * 8, rn * 8, gn, hipMemcpyHostToDevice, ctx->hstream));
+      STAGE_HIP(copy_rows(bv, rn * 8, val + g0 * gs + r0, gs * 8, rn * 8, gn, hipMemcpyHostToDevice, ctx->hstream));
+      if (int rc = copied_chunk(ctx, b)) return rc;
+      const bool first = r0 == 0;
+      const unsigned f = (!first || accumulate) ? CRDT_ACCUMULATE : 0u;
+      if (int rc = lww_lub_many_dev(ctx, bm, bv, gn, rn, rn, am, av, first_conflict ? (first ? fc : fcc) : nullptr, f))
+        return rc;
+      if (first_conflict && !first) {
+        hipLaunchKernelGGL(lww_fc_combine_kernel, dim3((unsigned)((gn + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                           ctx->stream, fc, fcc, (u64)r0, (unsigned long long)gn);
+        STAGE_HIP(hipGetLastError());
+      }
+      if (int rc = end_chunk(ctx, b)) return rc;
+    }
+    STAGE_HIP(hipMemcpyAsync(out_marker + g0, am, gn * 8, hipMemcpyDeviceToHost, ctx->stream));
+    STAGE_HIP(hipMemcpyAsync(out_val + g0, av, gn * 8, hipMemcpyDeviceToHost, ctx->stream));
+    if (first_conflict)
+      STAGE_HIP(hipMemcpyAsync(first_conflict + g0, fc, gn * 8, hipMemcpyDeviceToHost, ctx->stream));
+  }
+  return CRDT_OK;
+}
+
+int lww_lub_many_host(crdt_ctx *ctx, const u64 *marker, const u64 *val, size_t G, size_t R, size_t group_stride,
+                      u64 *out_marker, u64 *out_val, u64 *first_conflict, unsigned flags) {
+  if (G == 0) return CRDT_OK;
+  const bool accumulate = flags & CRDT_ACCUMULATE;
+  if (accumulate && (!out_marker || !out_val))
+    return fail(ctx, CRDT_EINVAL, "lwwreg_lub_many: CRDT_ACCUMULATE needs out_marker and out_val");
+  if (R == 0 && accumulate) {  // nothing merged: state unchanged, no conflict
+    if (first_conflict) std::memset(first_conflict, 0xFF, G * 8);
+    return CRDT_OK;
+  }
+  if (R == 0) return fail(ctx, CRDT_EINVAL, "lwwreg_lub_many: R == 0 (LWWReg has no identity; the fold starts at replica 0)");
+  if (!marker || !val) return fail(ctx, CRDT_EINVAL, "lwwreg_lub_many: NULL input");
+  if (G > 1 && group_stride < R)
+    return fail(ctx, CRDT_EINVAL, "lwwreg_lub_many: group_stride %zu < R %zu", group_stride, R);
+  if (!out_marker || !out_val)  // host mode stages whole results: both state outputs are required
+    return fail(ctx, CRDT_EINVAL, "lwwreg_lub_many: CRDT_MEM_HOST needs out_marker and out_val");
+  for (auto [p, w] : {std::pair<const void *, const char *>{marker, "marker"}, {val, "val"}, {out_marker, "out_marker"},
+                      {out_val, "out_val"}, {first_conflict, "first_conflict"}})
+    if (int rc = check_host(ctx, p, w)) return rc;
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  return finish(ctx, lww_lub_host_body(ctx, marker, val, G, R, group_stride, out_marker, out_val, first_conflict, flags));
+}
+
+static int lww_merge_host_body(crdt_ctx *ctx, u64 *sm, u64 *sv, const u64 *om, const u64 *ov, size_t N,
+                               uint8_t *conflict) {
+  const size_t Nc = std::min(N, std::max<size_t>(1, stage_budget(ctx) / 40));
+  if (int rc = ensure_stage(ctx, Nc * 40, 8)) return rc;
+  size_t k = 0;
+  for (size_t i0 = 0; i0 < N; i0 += Nc, ++k) {
+    const size_t n = std::min(Nc, N - i0);
+    const int b = (int)(k & 1);
+    u64 *dsm = static_cast<u64 *>(ctx->hbuf[b]), *dsv = dsm + n, *dom = dsv + n, *dov = dom + n;
+    uint8_t *dc = reinterpret_cast<uint8_t *>(dov + n);
+    if (int rc = begin_chunk(ctx, b)) return rc;
+    STAGE_HIP(hipMemcpyAsync(dsm, sm + i0, n * 8, hipMemcpyHostToDevice, ctx->hstream));
+    STAGE_HIP(hipMemcpyAsync(dsv, sv + i0, n * 8, hipMemcpyHostToDevice, ctx->hstream));
+    STAGE_HIP(hipMemcpyAsync(dom, om + i0, n * 8, hipMemcpyHostToDevice, ctx->hstream));
+    STAGE_HIP(hipMemcpyAsync(dov, ov + i0, n * 8, hipMemcpyHostToDevice, ctx->hstream));
+    if (int rc = copied_chunk(ctx, b)) return rc;
+    if (int rc = lww_merge_batch_dev(ctx, dsm, dsv, dom, dov, n, conflict ? dc : nullptr)) return rc;
+    STAGE_HIP(hipMemcpyAsync(sm + i0, dsm, n * 8, hipMemcpyDeviceToHost, ctx->stream));
+    STAGE_HIP(hipMemcpyAsync(sv + i0, dsv, n * 8, hipMemcpyDeviceToHost, ctx->stream));
+    if (conflict) STAGE_HIP(hipMemcpyAsync(conflict + i0, dc, n, hipMemcpyDeviceToHost, ctx->stream));
+    if (int rc = end_chunk(ctx, b)) return rc;
+  }
+  return CRDT_OK;
+}
+
+int lww_merge_batch_host(crdt_ctx *ctx, u64 *sm, u64 *sv, const u64 *om, const u64 *ov, size_t N, uint8_t *conflict) {
+  if (N == 0) return CRDT_OK;
+  if (!sm || !sv || !om || !ov) return fail(ctx, CRDT_EINVAL, "lwwreg_merge_batch: NULL buffer");
+  for (auto [p, w] : {std::pair<const void *, const char *>{sm, "self_marker"}, {sv, "self_val"}, {om, "other_marker"},
+                      {ov, "other_val"}, {conflict, "conflict"}})
+    if (int rc = check_host(ctx, p, w)) return rc;
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  return finish(ctx, lww_merge_host_body(ctx, sm, sv, om, ov, N, conflict));
+}
+
+void free_stage(crdt_ctx *ctx) {
+  if (ctx->hstream) (void)hipStreamSynchronize(ctx->hstream);
+  for (auto &b : ctx->hbuf)
+    if (b) (void)hipFree(b);
+  if (ctx->hacc) (void)hipFree(ctx->hacc);
+  for (int b = 0; b < 2; ++b) {
+    if (ctx->hcopied[b]) (void)hipEventDestroy(ctx->hcopied[b]);
+    if (ctx->hfree[b]) (void)hipEventDestroy(ctx->hfree[b]);
+  }
+  if (ctx->hstream) (void)hipStreamDestroy(ctx->hstream);
+}
+
+}  // namespace crdt
+
+extern "C" {
+
+int crdt_ctx_set_mem_kind(crdt_ctx *ctx, int kind) {
+  CRDT_CHECK_CTX(ctx);
+  if (kind != CRDT_MEM_DEVICE && kind != CRDT_MEM_HOST)
+    return crdt::fail(ctx, CRDT_EINVAL, "crdt_ctx_set_mem_kind: unknown kind %d", kind);
+  ctx->mem_kind = kind;
+  return CRDT_OK;
+}
+
+int crdt_ctx_mem_kind(const crdt_ctx *ctx) { return ctx ? ctx->mem_kind : CRDT_EINVAL; }
+
+int crdt_host_alloc(size_t bytes, void **out) {
+  if (!out) return crdt::fail(nullptr, CRDT_EINVAL, "crdt_host_alloc: out is NULL");
+  *out = nullptr;
+  if (bytes == 0) return CRDT_OK;
+  hipError_t e = hipHostMalloc(out, bytes, hipHostMallocDefault);
+  if (e != hipSuccess) {
+    *out = nullptr;
+    return crdt::fail(nullptr, CRDT_ENOMEM, "crdt_host_alloc(%zu): %s", bytes, hipGetErrorString(e));
+  }
+  return CRDT_OK;
+}
+
+int crdt_host_free(void *p) {
+  if (!p) return CRDT_OK;
+  hipError_t e = hipHostFree(p);
+  return e == hipSuccess ? CRDT_OK : crdt::hip_fail(nullptr, e, "hipHostFree");
+}
+
+}  // extern "C"

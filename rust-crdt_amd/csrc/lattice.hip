@@ -424,17 +424,33 @@ int lattice_merge_batch(crdt_ctx *ctx, Op op, u64 *self, const u64 *other, size_
 using crdt::Op;
 using crdt::u64;
 
+// CRDT_MEM_HOST routes the public lattice entry points through the chunked host staging.
+static int lub_dispatch(crdt_ctx *ctx, Op op, const u64 *in, size_t G, size_t R, size_t W, size_t row_stride,
+                        size_t group_stride, u64 *out, size_t out_stride, unsigned flags) {
+  CRDT_CHECK_CTX(ctx);
+  if (ctx->mem_kind == CRDT_MEM_HOST)
+    return crdt::lattice_lub_many_host(ctx, op, in, G, R, W, row_stride, group_stride, out, out_stride, flags);
+  return crdt::lattice_lub_many(ctx, op, in, G, R, W, row_stride, group_stride, out, out_stride, flags);
+}
+static int merge_dispatch(crdt_ctx *ctx, Op op, u64 *self, const u64 *other, size_t N, size_t W, size_t self_stride,
+                          size_t other_stride) {
+  CRDT_CHECK_CTX(ctx);
+  if (ctx->mem_kind == CRDT_MEM_HOST)
+    return crdt::lattice_merge_batch_host(ctx, op, self, other, N, W, self_stride, other_stride);
+  return crdt::lattice_merge_batch(ctx, op, self, other, N, W, self_stride, other_stride);
+}
+
 extern "C" {
 
 int crdt_vclock_lub_many(crdt_ctx *ctx, const uint64_t *in, size_t G, size_t R, size_t A,
                          size_t row_stride, size_t group_stride, uint64_t *out,
                          size_t out_stride, unsigned flags) {
-  return crdt::lattice_lub_many(ctx, Op::Max, (const u64 *)in, G, R, A, row_stride, group_stride,
+  return lub_dispatch(ctx, Op::Max, (const u64 *)in, G, R, A, row_stride, group_stride,
                                 (u64 *)out, out_stride, flags);
 }
 int crdt_vclock_merge_batch(crdt_ctx *ctx, uint64_t *self, const uint64_t *other, size_t N,
                             size_t A, size_t self_stride, size_t other_stride) {
-  return crdt::lattice_merge_batch(ctx, Op::Max, (u64 *)self, (const u64 *)other, N, A,
+  return merge_dispatch(ctx, Op::Max, (u64 *)self, (const u64 *)other, N, A,
                                    self_stride, other_stride);
 }
 int crdt_gcounter_lub_many(crdt_ctx *ctx, const uint64_t *in, size_t G, size_t R, size_t A,
@@ -449,23 +465,23 @@ int crdt_gcounter_merge_batch(crdt_ctx *ctx, uint64_t *self, const uint64_t *oth
 int crdt_pncounter_lub_many(crdt_ctx *ctx, const uint64_t *in, size_t G, size_t R, size_t A,
                             size_t row_stride, size_t group_stride, uint64_t *out,
                             size_t out_stride, unsigned flags) {
-  return crdt::lattice_lub_many(ctx, Op::Max, (const u64 *)in, G, R, 2 * A, row_stride,
+  return lub_dispatch(ctx, Op::Max, (const u64 *)in, G, R, 2 * A, row_stride,
                                 group_stride, (u64 *)out, out_stride, flags);
 }
 int crdt_pncounter_merge_batch(crdt_ctx *ctx, uint64_t *self, const uint64_t *other,
                                size_t N, size_t A, size_t self_stride, size_t other_stride) {
-  return crdt::lattice_merge_batch(ctx, Op::Max, (u64 *)self, (const u64 *)other, N, 2 * A,
+  return merge_dispatch(ctx, Op::Max, (u64 *)self, (const u64 *)other, N, 2 * A,
                                    self_stride, other_stride);
 }
 int crdt_gset_lub_many(crdt_ctx *ctx, const uint64_t *in, size_t G, size_t R, size_t words,
                        size_t row_stride, size_t group_stride, uint64_t *out,
                        size_t out_stride, unsigned flags) {
-  return crdt::lattice_lub_many(ctx, Op::Or, (const u64 *)in, G, R, words, row_stride,
+  return lub_dispatch(ctx, Op::Or, (const u64 *)in, G, R, words, row_stride,
                                 group_stride, (u64 *)out, out_stride, flags);
 }
 int crdt_gset_merge_batch(crdt_ctx *ctx, uint64_t *self, const uint64_t *other, size_t N,
                           size_t words, size_t self_stride, size_t other_stride) {
-  return crdt::lattice_merge_batch(ctx, Op::Or, (u64 *)self, (const u64 *)other, N, words,
+  return merge_dispatch(ctx, Op::Or, (u64 *)self, (const u64 *)other, N, words,
                                    self_stride, other_stride);
 }
 

@@ -233,15 +233,8 @@ __global__ __launch_bounds__(kBlock) void lww_merge_pairs(u64 *sm, u64 *sv, cons
   if (conflict) conflict[i] = err;
 }
 
-}  // namespace crdt
-
-using namespace crdt;
-
-extern "C" {
-
-int crdt_lwwreg_lub_many(crdt_ctx *ctx, const uint64_t *marker, const uint64_t *val, size_t G,
-                         size_t R, size_t group_stride, uint64_t *out_marker,
-                         uint64_t *out_val, uint64_t *first_conflict, unsigned flags) {
+int lww_lub_many_dev(crdt_ctx *ctx, const u64 *marker, const u64 *val, size_t G, size_t R, size_t group_stride,
+                     u64 *out_marker, u64 *out_val, u64 *first_conflict, unsigned flags) {
   CRDT_CHECK_CTX(ctx);
   if (G == 0) return CRDT_OK;
   const bool accumulate = flags & CRDT_ACCUMULATE;
@@ -292,9 +285,8 @@ int crdt_lwwreg_lub_many(crdt_ctx *ctx, const uint64_t *marker, const uint64_t *
   return CRDT_OK;
 }
 
-int crdt_lwwreg_merge_batch(crdt_ctx *ctx, uint64_t *self_marker, uint64_t *self_val,
-                            const uint64_t *other_marker, const uint64_t *other_val,
-                            size_t N, uint8_t *conflict) {
+int lww_merge_batch_dev(crdt_ctx *ctx, u64 *self_marker, u64 *self_val, const u64 *other_marker,
+                        const u64 *other_val, size_t N, uint8_t *conflict) {
   CRDT_CHECK_CTX(ctx);
   if (N == 0) return CRDT_OK;
   if (!self_marker || !self_val || !other_marker || !other_val)
@@ -309,6 +301,34 @@ int crdt_lwwreg_merge_batch(crdt_ctx *ctx, uint64_t *self_marker, uint64_t *self
   timing_end(ctx);
   CRDT_HIP(ctx, hipGetLastError());
   return CRDT_OK;
+}
+
+}  // namespace crdt
+
+using namespace crdt;
+
+extern "C" {
+
+int crdt_lwwreg_lub_many(crdt_ctx *ctx, const uint64_t *marker, const uint64_t *val, size_t G,
+                         size_t R, size_t group_stride, uint64_t *out_marker,
+                         uint64_t *out_val, uint64_t *first_conflict, unsigned flags) {
+  CRDT_CHECK_CTX(ctx);
+  if (ctx->mem_kind == CRDT_MEM_HOST)
+    return lww_lub_many_host(ctx, (const u64 *)marker, (const u64 *)val, G, R, group_stride, (u64 *)out_marker,
+                             (u64 *)out_val, (u64 *)first_conflict, flags);
+  return lww_lub_many_dev(ctx, (const u64 *)marker, (const u64 *)val, G, R, group_stride, (u64 *)out_marker,
+                          (u64 *)out_val, (u64 *)first_conflict, flags);
+}
+
+int crdt_lwwreg_merge_batch(crdt_ctx *ctx, uint64_t *self_marker, uint64_t *self_val,
+                            const uint64_t *other_marker, const uint64_t *other_val,
+                            size_t N, uint8_t *conflict) {
+  CRDT_CHECK_CTX(ctx);
+  if (ctx->mem_kind == CRDT_MEM_HOST)
+    return lww_merge_batch_host(ctx, (u64 *)self_marker, (u64 *)self_val, (const u64 *)other_marker,
+                                (const u64 *)other_val, N, conflict);
+  return lww_merge_batch_dev(ctx, (u64 *)self_marker, (u64 *)self_val, (const u64 *)other_marker,
+                             (const u64 *)other_val, N, conflict);
 }
 
 }  // extern "C"

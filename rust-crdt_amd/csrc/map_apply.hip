@@ -386,6 +386,7 @@ using namespace crdt;
 
 extern "C" int crdt_map_apply_batch(crdt_ctx *ctx, const crdt_map_states *m, uint64_t *def_clock, uint64_t *def_keys,
                                     uint32_t *def_count, size_t Dcap, const crdt_map_ops *ops, uint32_t *status) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
   CRDT_CHECK_CTX(ctx);
   if (!m || !ops || !status) return fail(ctx, CRDT_EINVAL, "map_apply_batch: NULL argument");
   const size_t N = m->N, K = m->K, A = m->A, V = m->V;

@@ -464,6 +464,381 @@ __global__ __launch_bounds__(kBlock) void map_pair_join_kernel(MapPairPlan p) {
   }
 }
 
+// Register-resident form of map_pair_join_kernel for V1, V2 <= VM: every row of the key (both
+// entry clocks, both map clocks, all value clocks, the value payloads and the key's bit of every
+// deferred remove) is loaded in ONE batch of independent loads before any vote, so a key costs
+// one memory round trip (two when a remove names it) instead of a chain of dependent ones; the
+// MVReg compares then run on registers.  Same statement-by-statement semantics as the generic
+// kernel above (map.rs:142-210, mvreg.rs:112-128, apply_keyset_rm :318-333).
+template <int APL, int VM>
+__global__ __launch_bounds__(kBlock) void map_pair_join_reg_kernel(MapPairPlan p) {
+  const int lane = threadIdx.x % kWave;
+  const unsigned long long w0 = (blockIdx.x * (unsigned long long)kBlock + threadIdx.x) / kWave;
+  const unsigned long long nw = (unsigned long long)gridDim.x * (kBlock / kWave);
+  const unsigned long long A = p.A;
+  const unsigned V1 = (unsigned)p.V1, V2 = (unsigned)p.V2;
+  for (unsigned long long it = w0; it < p.N * p.K; it += nw) {
+    const unsigned long long s = it / p.K, k = it % p.K;
+    const unsigned n1 = p.d1n[s], n2 = p.d2n ? p.d2n[s] : 0u;
+    if (n1 > p.D1 || n2 > p.D2) continue;  // reported by pair_deferred_kernel
+    u64 *ec1 = p.ec1 + s * p.ec1_s + k * A;
+    u64 *vc1 = p.vc1 + s * p.vc1_s + k * p.V1 * A;
+    u64 *vv1 = p.vv1 + s * p.vv1_s + k * p.V1;
+    const u64 *ec2 = p.ec2 + s * p.ec2_s + k * A;
+    const u64 *vc2 = p.vc2 + s * p.vc2_s + k * p.V2 * A;
+    const u64 *vv2 = p.vv2 + s * p.vv2_s + k * p.V2;
+    // ---- one batch of loads
+    const PRow<APL> e1 = prow<APL>(ec1, lane, A), e2 = prow<APL>(ec2, lane, A);
+    const PRow<APL> c1 = prow<APL>(p.c1 + s * p.c1_s, lane, A), c2 = prow<APL>(p.c2 + s * p.c2_s, lane, A);
+    PRow<APL> x[VM], y[VM];
+#pragma unroll
+    for (int q = 0; q < VM; ++q) {
+#pragma unroll
+      for (int j = 0; j < APL; ++j) x[q].w[j] = y[q].w[j] = 0;
+      if ((unsigned)q < V1) x[q] = prow<APL>(vc1 + (unsigned long long)q * A, lane, A);
+      if ((unsigned)q < V2) y[q] = prow<APL>(vc2 + (unsigned long long)q * A, lane, A);
+    }
+    const u64 v1l = (unsigned)lane < V1 ? vv1[lane] : 0ull;
+    const u64 v2l = (unsigned)lane < V2 ? vv2[lane] : 0ull;
+    const unsigned nd = n1 + n2;
+    bool hitl = false;  // lane d: remove d (self's, then other's) names k
+    if ((unsigned)lane < nd) {
+      const u64 *kb = (unsigned)lane < n1 ? p.d1k + (s * p.D1 + lane) * p.Kw : p.d2k + (s * p.D2 + (lane - n1)) * p.Kw;
+      hitl = (kb[k / 64] >> (k % 64)) & 1ull;
+    }
+    // ---- compute on registers
+    const bool p1 = pnz(e1), p2 = pnz(e2);
+    if (!p1 && !p2) continue;  // no entry on either side: nothing to merge
+    unsigned m1 = 0, m2 = 0;
+#pragma unroll
+    for (int q = 0; q < VM; ++q) {
+      if (pnz(x[q])) m1 |= 1u << q;  // rows past V1 / V2 are zero
+      if (pnz(y[q])) m2 |= 1u << q;
+    }
+    bool present = true;
+    PRow<APL> e, X;
+    unsigned keep1 = 0, add2 = 0;
+    if (p1 && !p2) {  // :146-161
+      if (ple(e1, c2)) {
+        present = false;
+      } else {
+        e = pforget(e1, c2);
+        X = pforget(c2, e);
+        keep1 = m1;
+      }
+    } else if (!p1 && p2) {  // :193-208
+      if (ple(e2, c1)) {
+        present = false;
+      } else {
+        e = pforget(e2, c1);
+        X = pforget(c1, e);
+        add2 = m2;
+      }
+    } else {  // :170-192
+      PRow<APL> common;
+#pragma unroll
+      for (int j = 0; j < APL; ++j) {
+        const u64 a = e1.w[j], b = e2.w[j];
+        const u64 t0 = a == b ? a : 0ull, t1 = b > c1.w[j] ? b : 0ull, t2 = a > c2.w[j] ? a : 0ull;
+        const u64 t = t0 > t1 ? t0 : t1;
+        common.w[j] = t > t2 ? t : t2;
+      }
+      if (!pnz(common)) {
+        present = false;
+      } else {
+#pragma unroll
+        for (int q = 0; q < VM; ++q) {
+          if (!((m1 >> q) & 1u)) continue;
+          bool dom = false;
+#pragma unroll
+          for (int r = 0; r < VM; ++r)
+            if (((m2 >> r) & 1u) && !dom) dom = plt(x[q], y[r]);
+          if (!dom) keep1 |= 1u << q;
+        }
+#pragma unroll
+        for (int r = 0; r < VM; ++r) {
+          if (!((m2 >> r) & 1u)) continue;
+          bool drop = false;
+#pragma unroll
+          for (int q = 0; q < VM; ++q)
+            if (((keep1 >> q) & 1u) && !drop) drop = plt(y[r], x[q]) || peq(y[r], x[q]);
+          if (!drop) add2 |= 1u << r;
+        }
+        X = pforget(pmax(e1, e2), common);
+        e = common;
+      }
+    }
+    PRow<APL> Rk;
+#pragma unroll
+    for (int j = 0; j < APL; ++j) Rk.w[j] = 0;
+    bool hasR = false;
+    if (present) {
+      u64 hits = __ballot(hitl);
+      for (unsigned base = 64; base < nd; base += 64) {  // more than 64 removes on the pair
+        bool h = false;
+        const unsigned d = base + lane;
+        if (d < nd) {
+          const u64 *kb = d < n1 ? p.d1k + (s * p.D1 + d) * p.Kw : p.d2k + (s * p.D2 + (d - n1)) * p.Kw;
+          h = (kb[k / 64] >> (k % 64)) & 1ull;
+        }
+        const u64 hb = __ballot(h);
+        for (u64 m = hb; m; m &= m - 1) {
+          const unsigned dd = base + (unsigned)__builtin_ctzll(m);
+          const u64 *rc = dd < n1 ? p.d1c + (s * p.D1 + dd) * A : p.d2c + (s * p.D2 + (dd - n1)) * A;
+          Rk = pmax(Rk, prow<APL>(rc, lane, A));
+          hasR = true;
+        }
+      }
+      for (; hits; hits &= hits - 1) {
+        const unsigned d = (unsigned)__builtin_ctzll(hits);
+        const u64 *rc = d < n1 ? p.d1c + (s * p.D1 + d) * A : p.d2c + (s * p.D2 + (d - n1)) * A;
+        Rk = pmax(Rk, prow<APL>(rc, lane, A));
+        hasR = true;
+      }
+      if (hasR) {
+        e = pforget(e, Rk);
+        if (!pnz(e)) present = false;
+      }
+    }
+    unsigned w = 0;
+    if (present) {
+      pstore(ec1, e, lane, A);
+#pragma unroll
+      for (int q = 0; q < VM; ++q) {
+        if (!((keep1 >> q) & 1u)) continue;
+        PRow<APL> z = pforget(x[q], X);  // MVReg::forget mvreg.rs:88-104
+        if (hasR) z = pforget(z, Rk);
+        if (!pnz(z)) continue;
+        const u64 val = prl64(v1l, q);
+        if (w < V1) {
+          pstore(vc1 + (unsigned long long)w * A, z, lane, A);
+          if (lane == 0) vv1[w] = val;
+        }
+        ++w;
+      }
+#pragma unroll
+      for (int r = 0; r < VM; ++r) {
+        if (!((add2 >> r) & 1u)) continue;
+        PRow<APL> z = pforget(y[r], X);
+        if (hasR) z = pforget(z, Rk);
+        if (!pnz(z)) continue;
+        const u64 val = prl64(v2l, r);
+        if (w < V1) {
+          pstore(vc1 + (unsigned long long)w * A, z, lane, A);
+          if (lane == 0) vv1[w] = val;
+        }
+        ++w;
+      }
+      if (w > V1 && lane == 0) atomicOr(p.status + s, 16u);
+    } else {
+      PRow<APL> z;
+#pragma unroll
+      for (int j = 0; j < APL; ++j) z.w[j] = 0;
+      pstore(ec1, z, lane, A);
+    }
+    for (unsigned q = w; q < V1; ++q) {
+      PRow<APL> z;
+#pragma unroll
+      for (int j = 0; j < APL; ++j) z.w[j] = 0;
+      pstore(vc1 + (unsigned long long)q * A, z, lane, A);
+      if (lane == 0) vv1[q] = 0;
+    }
+  }
+}
+
+// Sub-wave form for A <= SEG < 64 (one actor per lane): a wave merges 64 / SEG keys at once, one
+// SEG-lane segment per key, so a narrow key (A = 32 at config 4) does not leave half the wave
+// idle and twice the rows are in flight per wave.  Votes are per segment (the segment's bits of
+// the ballot); the segments of a wave may branch differently (divergent, not wrong: every
+// segment's lanes only read and write their own key).  Otherwise map_pair_join_reg_kernel.
+template <int SEG>
+struct Seg {
+  int lane, sl, base;
+  u64 mask;
+  __device__ Seg(int l) : lane(l), sl(l & (SEG - 1)), base(l & ~(SEG - 1)),
+                          mask(SEG == 64 ? ~0ull : (((1ull << SEG) - 1) << (l & ~(SEG - 1)))) {}
+  __device__ bool any(bool x) const { return (__ballot(x) & mask) != 0; }
+  __device__ u64 bits(bool x) const { return (__ballot(x) & mask) >> base; }
+};
+
+template <int SEG, int VM>
+__global__ __launch_bounds__(kBlock) void map_pair_join_seg_kernel(MapPairPlan p) {
+  constexpr int KPW = kWave / SEG;  // keys per wave
+  const Seg<SEG> sg(threadIdx.x % kWave);
+  const int sl = sg.sl;
+  const unsigned long long w0 = (blockIdx.x * (unsigned long long)kBlock + threadIdx.x) / kWave;
+  const unsigned long long nw = (unsigned long long)gridDim.x * (kBlock / kWave);
+  const unsigned long long A = p.A, NK = p.N * p.K;
+  const unsigned V1 = (unsigned)p.V1, V2 = (unsigned)p.V2;
+  const bool act = (unsigned long long)sl < A;
+  for (unsigned long long it0 = w0 * KPW; it0 < NK; it0 += nw * KPW) {
+    const unsigned long long it = it0 + (unsigned long long)(sg.base / SEG);
+    if (it >= NK) continue;  // a segment past the end (last wave only)
+    const unsigned long long s = it / p.K, k = it % p.K;
+    const unsigned n1 = p.d1n[s], n2 = p.d2n ? p.d2n[s] : 0u;
+    if (n1 > p.D1 || n2 > p.D2) continue;  // reported by pair_deferred_kernel
+    u64 *ec1 = p.ec1 + s * p.ec1_s + k * A;
+    u64 *vc1 = p.vc1 + s * p.vc1_s + k * p.V1 * A;
+    u64 *vv1 = p.vv1 + s * p.vv1_s + k * p.V1;
+    const u64 *ec2 = p.ec2 + s * p.ec2_s + k * A;
+    const u64 *vc2 = p.vc2 + s * p.vc2_s + k * p.V2 * A;
+    const u64 *vv2 = p.vv2 + s * p.vv2_s + k * p.V2;
+    // ---- one batch of loads
+    u64 e1 = 0, e2 = 0, c1 = 0, c2 = 0, x[VM], y[VM];
+#pragma unroll
+    for (int q = 0; q < VM; ++q) x[q] = y[q] = 0;
+    if (act) {
+      e1 = ec1[sl];
+      e2 = ec2[sl];
+      c1 = p.c1[s * p.c1_s + sl];
+      c2 = p.c2[s * p.c2_s + sl];
+#pragma unroll
+      for (int q = 0; q < VM; ++q) {
+        if ((unsigned)q < V1) x[q] = vc1[(unsigned long long)q * A + sl];
+        if ((unsigned)q < V2) y[q] = vc2[(unsigned long long)q * A + sl];
+      }
+    }
+    const u64 v1l = (unsigned)sl < V1 ? vv1[sl] : 0ull;
+    const u64 v2l = (unsigned)sl < V2 ? vv2[sl] : 0ull;
+    // each segment's value payloads to all its lanes while the whole wave is still converged
+    u64 val1[VM], val2[VM];
+#pragma unroll
+    for (int q = 0; q < VM; ++q) {
+      val1[q] = __shfl(v1l, sg.base + q);
+      val2[q] = __shfl(v2l, sg.base + q);
+    }
+    const unsigned nd = n1 + n2;
+    bool hitl = false;  // segment lane d: remove d (self's, then other's) names k
+    if ((unsigned)sl < nd) {
+      const u64 *kb = (unsigned)sl < n1 ? p.d1k + (s * p.D1 + sl) * p.Kw : p.d2k + (s * p.D2 + (sl - n1)) * p.Kw;
+      hitl = (kb[k / 64] >> (k % 64)) & 1ull;
+    }
+    // ---- compute
+    const bool p1 = sg.any(e1 != 0), p2 = sg.any(e2 != 0);
+    if (!p1 && !p2) continue;
+    unsigned m1 = 0, m2 = 0;
+#pragma unroll
+    for (int q = 0; q < VM; ++q) {
+      if (sg.any(x[q] != 0)) m1 |= 1u << q;
+      if (sg.any(y[q] != 0)) m2 |= 1u << q;
+    }
+    auto le = [&](u64 a, u64 b) { return !sg.any(a > b); };           // a <= b everywhere
+    auto lt = [&](u64 a, u64 b) { return le(a, b) && sg.any(a != b); };  // partial_cmp == Less
+    bool present = true;
+    u64 e = 0, X = 0;
+    unsigned keep1 = 0, add2 = 0;
+    if (p1 && !p2) {  // :146-161
+      if (le(e1, c2)) {
+        present = false;
+      } else {
+        e = e1 > c2 ? e1 : 0;
+        X = c2 > e ? c2 : 0;
+        keep1 = m1;
+      }
+    } else if (!p1 && p2) {  // :193-208
+      if (le(e2, c1)) {
+        present = false;
+      } else {
+        e = e2 > c1 ? e2 : 0;
+        X = c1 > e ? c1 : 0;
+        add2 = m2;
+      }
+    } else {  // :170-192
+      const u64 t0 = e1 == e2 ? e1 : 0ull, t1 = e2 > c1 ? e2 : 0ull, t2 = e1 > c2 ? e1 : 0ull;
+      const u64 t = t0 > t1 ? t0 : t1;
+      const u64 common = t > t2 ? t : t2;
+      if (!sg.any(common != 0)) {
+        present = false;
+      } else {
+#pragma unroll
+        for (int q = 0; q < VM; ++q) {
+          if (!((m1 >> q) & 1u)) continue;
+          bool dom = false;
+#pragma unroll
+          for (int r = 0; r < VM; ++r)
+            if (((m2 >> r) & 1u) && !dom) dom = lt(x[q], y[r]);
+          if (!dom) keep1 |= 1u << q;
+        }
+#pragma unroll
+        for (int r = 0; r < VM; ++r) {
+          if (!((m2 >> r) & 1u)) continue;
+          bool drop = false;
+#pragma unroll
+          for (int q = 0; q < VM; ++q)
+            if (((keep1 >> q) & 1u) && !drop) drop = le(y[r], x[q]);  // y < x or y == x
+          if (!drop) add2 |= 1u << r;
+        }
+        const u64 mx = e1 > e2 ? e1 : e2;
+        X = mx > common ? mx : 0;
+        e = common;
+      }
+    }
+    u64 Rk = 0;
+    bool hasR = false;
+    if (present) {
+      for (unsigned b0 = 0; b0 < nd; b0 += SEG) {
+        bool h = hitl;
+        if (b0) {  // more than SEG removes on the pair
+          h = false;
+          const unsigned d = b0 + sl;
+          if (d < nd) {
+            const u64 *kb = d < n1 ? p.d1k + (s * p.D1 + d) * p.Kw : p.d2k + (s * p.D2 + (d - n1)) * p.Kw;
+            h = (kb[k / 64] >> (k % 64)) & 1ull;
+          }
+        }
+        for (u64 m = sg.bits(h); m; m &= m - 1) {
+          const unsigned d = b0 + (unsigned)__builtin_ctzll(m);
+          const u64 *rc = d < n1 ? p.d1c + (s * p.D1 + d) * A : p.d2c + (s * p.D2 + (d - n1)) * A;
+          const u64 r = act ? rc[sl] : 0ull;
+          Rk = Rk > r ? Rk : r;
+          hasR = true;
+        }
+      }
+      if (hasR) {
+        e = e > Rk ? e : 0;
+        if (!sg.any(e != 0)) present = false;
+      }
+    }
+    unsigned w = 0;
+    if (present) {
+      if (act) ec1[sl] = e;
+#pragma unroll
+      for (int q = 0; q < VM; ++q) {
+        if (!((keep1 >> q) & 1u)) continue;
+        u64 z = x[q] > X ? x[q] : 0;  // MVReg::forget mvreg.rs:88-104
+        if (hasR) z = z > Rk ? z : 0;
+        const u64 val = val1[q];
+        if (!sg.any(z != 0)) continue;
+        if (w < V1) {
+          if (act) vc1[(unsigned long long)w * A + sl] = z;
+          if (sl == 0) vv1[w] = val;
+        }
+        ++w;
+      }
+#pragma unroll
+      for (int r = 0; r < VM; ++r) {
+        if (!((add2 >> r) & 1u)) continue;
+        u64 z = y[r] > X ? y[r] : 0;
+        if (hasR) z = z > Rk ? z : 0;
+        const u64 val = val2[r];
+        if (!sg.any(z != 0)) continue;
+        if (w < V1) {
+          if (act) vc1[(unsigned long long)w * A + sl] = z;
+          if (sl == 0) vv1[w] = val;
+        }
+        ++w;
+      }
+      if (w > V1 && sl == 0) atomicOr(p.status + s, 16u);
+    } else if (act) {
+      ec1[sl] = 0;
+    }
+    for (unsigned q = w; q < V1; ++q) {
+      if (act) vc1[(unsigned long long)q * A + sl] = 0;
+      if (sl == 0) vv1[q] = 0;
+    }
+  }
+}
+
 static unsigned pair_grid(crdt_ctx *ctx, unsigned long long waves, int per_cu) {
   const unsigned long long want = (waves + (kBlock / kWave) - 1) / (kBlock / kWave);
   const unsigned long long cap = (unsigned long long)ctx->cu_count * per_cu;
@@ -484,6 +859,7 @@ using namespace crdt;
 
 extern "C" int crdt_orswot_merge_batch(crdt_ctx *ctx, const crdt_orswot_states *self, const crdt_orswot_states *other,
                                        uint32_t *status) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
   CRDT_CHECK_CTX(ctx);
   if (!self || !other || !status) return fail(ctx, CRDT_EINVAL, "orswot_merge_batch: NULL argument");
   const crdt_orswot_states &a = *self, &b = *other;
@@ -535,6 +911,7 @@ extern "C" int crdt_orswot_merge_batch(crdt_ctx *ctx, const crdt_orswot_states *
 extern "C" int crdt_map_merge_batch(crdt_ctx *ctx, const crdt_map_states *self, const crdt_map_deferred *self_def,
                                     const crdt_map_states *other, const crdt_map_deferred *other_def,
                                     uint32_t *status) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
   CRDT_CHECK_CTX(ctx);
   if (!self || !other || !self_def || !other_def || !status)
     return fail(ctx, CRDT_EINVAL, "map_merge_batch: NULL argument");
@@ -567,7 +944,20 @@ extern "C" int crdt_map_merge_batch(crdt_ctx *ctx, const crdt_map_states *self, 
                   other_def->Dcap ? other_def->count : nullptr, other_def->Dcap, status};
     const unsigned grid = pair_grid(ctx, (unsigned long long)N * K, 16);
     timing_begin(ctx, "map_pair_join");
-    if (A <= (size_t)kWave)
+    if (ctx->tune.map_pair_reg && a.V <= 4 && b.V <= 4) {  // register-resident rows (one load batch per key)
+      if (A <= 16 && ctx->tune.map_pair_reg == 1)
+        hipLaunchKernelGGL((map_pair_join_seg_kernel<16, 4>), dim3(grid), dim3(kBlock), 0, ctx->stream, p);
+      else if (A <= 32 && ctx->tune.map_pair_reg == 1)
+        hipLaunchKernelGGL((map_pair_join_seg_kernel<32, 4>), dim3(grid), dim3(kBlock), 0, ctx->stream, p);
+      else if (A <= (size_t)kWave && ctx->tune.map_pair_reg == 1)
+        hipLaunchKernelGGL((map_pair_join_seg_kernel<64, 4>), dim3(grid), dim3(kBlock), 0, ctx->stream, p);
+      else if (A <= (size_t)kWave)
+        hipLaunchKernelGGL((map_pair_join_reg_kernel<1, 4>), dim3(grid), dim3(kBlock), 0, ctx->stream, p);
+      else if (A <= 2 * (size_t)kWave)
+        hipLaunchKernelGGL((map_pair_join_reg_kernel<2, 4>), dim3(grid), dim3(kBlock), 0, ctx->stream, p);
+      else
+        hipLaunchKernelGGL((map_pair_join_reg_kernel<4, 4>), dim3(grid), dim3(kBlock), 0, ctx->stream, p);
+    } else if (A <= (size_t)kWave)
       hipLaunchKernelGGL(map_pair_join_kernel<1>, dim3(grid), dim3(kBlock), 0, ctx->stream, p);
     else if (A <= 2 * (size_t)kWave)
       hipLaunchKernelGGL(map_pair_join_kernel<2>, dim3(grid), dim3(kBlock), 0, ctx->stream, p);

@@ -326,6 +326,7 @@ using namespace crdt;
 
 extern "C" int crdt_orswot_apply_batch(crdt_ctx *ctx, const crdt_orswot_states *sv, const crdt_orswot_ops *ops,
                                        uint32_t *status) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
   CRDT_CHECK_CTX(ctx);
   if (!sv || !ops || !status) return fail(ctx, CRDT_EINVAL, "orswot_apply_batch: NULL argument");
   const crdt_orswot_states &s = *sv;

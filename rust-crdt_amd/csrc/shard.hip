@@ -217,22 +217,27 @@ int crdt_ctx_comm_info(const crdt_ctx *ctx, int *nranks, int *rank) {
 
 int crdt_vclock_lub_many_sharded(crdt_ctx *ctx, const uint64_t *in, size_t G, size_t R, size_t A, size_t row_stride,
                                  size_t group_stride, uint64_t *out) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
   return lattice_sharded(ctx, Op::Max, (const u64 *)in, G, R, A, row_stride, group_stride, (u64 *)out);
 }
 int crdt_gcounter_lub_many_sharded(crdt_ctx *ctx, const uint64_t *in, size_t G, size_t R, size_t A,
                                    size_t row_stride, size_t group_stride, uint64_t *out) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
   return lattice_sharded(ctx, Op::Max, (const u64 *)in, G, R, A, row_stride, group_stride, (u64 *)out);
 }
 int crdt_pncounter_lub_many_sharded(crdt_ctx *ctx, const uint64_t *in, size_t G, size_t R, size_t A,
                                     size_t row_stride, size_t group_stride, uint64_t *out) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
   return lattice_sharded(ctx, Op::Max, (const u64 *)in, G, R, 2 * A, row_stride, group_stride, (u64 *)out);
 }
 int crdt_gset_lub_many_sharded(crdt_ctx *ctx, const uint64_t *in, size_t G, size_t R, size_t words,
                                size_t row_stride, size_t group_stride, uint64_t *out) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
   return lattice_sharded(ctx, Op::Or, (const u64 *)in, G, R, words, row_stride, group_stride, (u64 *)out);
 }
 
 int crdt_orswot_lub_many_sharded(crdt_ctx *ctx, const crdt_orswot_batch *in, crdt_orswot_sharded_out *out) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
   CRDT_CHECK_CTX(ctx);
   CRDT_TRY(need_comm(ctx));
   if (!in || !out || !out->clock || !out->entries || !out->ndef)
@@ -381,6 +386,7 @@ int crdt_orswot_lub_many_sharded(crdt_ctx *ctx, const crdt_orswot_batch *in, crd
 int crdt_lwwreg_lub_many_sharded(crdt_ctx *ctx, const uint64_t *marker, const uint64_t *val, size_t G, size_t R,
                                  size_t group_stride, uint64_t base, uint64_t *out_marker, uint64_t *out_val,
                                  uint64_t *first_conflict) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
   CRDT_CHECK_CTX(ctx);
   CRDT_TRY(need_comm(ctx));
   if (G == 0) return CRDT_OK;
@@ -446,6 +452,7 @@ int crdt_lwwreg_lub_many_sharded(crdt_ctx *ctx, const uint64_t *marker, const ui
 }
 
 int crdt_map_lub_many_sharded(crdt_ctx *ctx, const crdt_map_batch *in, size_t k0, size_t K, crdt_map_out *out) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
   CRDT_CHECK_CTX(ctx);
   CRDT_TRY(need_comm(ctx));
   if (!in || !out) return fail(ctx, CRDT_EINVAL, "map_lub_many_sharded: NULL argument");

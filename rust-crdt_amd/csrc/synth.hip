@@ -54,6 +54,7 @@ __global__ __launch_bounds__(kBlock) void synth_fill_kernel(u64 *out, unsigned l
 
 extern "C" int crdt_synth_fill(crdt_ctx *ctx, uint64_t *out, size_t rows, size_t width,
                                size_t row_stride, size_t first_row, uint64_t seed, int kind) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
   CRDT_CHECK_CTX(ctx);
   if (rows == 0 || width == 0) return CRDT_OK;
   if (!out) return crdt::fail(ctx, CRDT_EINVAL, "synth_fill: out is NULL");
@@ -154,6 +155,7 @@ __global__ __launch_bounds__(kBlock) void synth_orswot_rm_kernel(u64 *entries, u
 extern "C" int crdt_synth_orswot(crdt_ctx *ctx, uint64_t *clock, uint64_t *entries, size_t R,
                                  size_t M, size_t A, size_t first_row, uint64_t seed,
                                  uint64_t kmax) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
   CRDT_CHECK_CTX(ctx);
   if (R == 0 || M == 0 || A == 0) return CRDT_OK;
   if (!clock || !entries) return crdt::fail(ctx, CRDT_EINVAL, "synth_orswot: NULL output");
@@ -175,6 +177,7 @@ extern "C" int crdt_synth_orswot(crdt_ctx *ctx, uint64_t *clock, uint64_t *entri
 extern "C" int crdt_synth_orswot_rm(crdt_ctx *ctx, uint64_t *entries, size_t M, size_t A,
                                     size_t D, const uint32_t *def_row, const uint64_t *def_clock,
                                     const uint64_t *def_members) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
   CRDT_CHECK_CTX(ctx);
   if (D == 0) return CRDT_OK;
   if (!entries || !def_row || !def_clock || !def_members)
@@ -291,6 +294,7 @@ extern "C" int crdt_synth_map(crdt_ctx *ctx, uint64_t *clock, uint64_t *ec, uint
                               size_t first_row, uint64_t seed, uint64_t kmax,
                               const uint64_t *def_off, const uint64_t *def_clock,
                               const uint64_t *def_keys) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
   CRDT_CHECK_CTX(ctx);
   if (R == 0 || K == 0 || A == 0) return CRDT_OK;
   if (!clock || !ec || (V > 0 && (!vclk || !vval)))

@@ -662,16 +662,19 @@ static int vclock_ingest_common(crdt_ctx *ctx, const uint8_t *bytes, const uint6
 
 int crdt_vclock_ingest(crdt_ctx *ctx, const uint8_t *bytes, const uint64_t *frame_off, size_t N, const uint32_t *actors,
                        size_t A, uint64_t *out, size_t row_stride, uint32_t *status) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
   return vclock_ingest_common(ctx, bytes, frame_off, N, actors, A, out, row_stride, status, 1, "vclock_ingest");
 }
 
 int crdt_pncounter_ingest(crdt_ctx *ctx, const uint8_t *bytes, const uint64_t *frame_off, size_t N,
                           const uint32_t *actors, size_t A, uint64_t *out, size_t row_stride, uint32_t *status) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
   return vclock_ingest_common(ctx, bytes, frame_off, N, actors, A, out, row_stride, status, 2, "pncounter_ingest");
 }
 
 int crdt_gset_ingest(crdt_ctx *ctx, const uint8_t *bytes, const uint64_t *frame_off, size_t N, const uint64_t *elems,
                      size_t U, uint64_t *out, size_t row_stride, uint32_t *status) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
   CRDT_CHECK_CTX(ctx);
   if (N == 0) return CRDT_OK;
   if (int rc = check_frames(ctx, bytes, frame_off, N, status)) return rc;
@@ -702,6 +705,7 @@ int crdt_gset_ingest(crdt_ctx *ctx, const uint8_t *bytes, const uint64_t *frame_
 
 int crdt_lwwreg_ingest(crdt_ctx *ctx, const uint8_t *bytes, const uint64_t *frame_off, size_t N, uint64_t *marker,
                        uint64_t *val, uint32_t *status) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
   CRDT_CHECK_CTX(ctx);
   if (N == 0) return CRDT_OK;
   if (int rc = check_frames(ctx, bytes, frame_off, N, status)) return rc;
@@ -722,6 +726,7 @@ int crdt_orswot_ingest(crdt_ctx *ctx, const uint8_t *bytes, const uint64_t *fram
                        size_t A, const uint64_t *members, size_t M, uint64_t *clock, uint64_t *entries,
                        uint64_t *def_off, uint64_t *def_clock, uint64_t *def_members, size_t def_cap, size_t *n_def,
                        uint32_t *status) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
   CRDT_CHECK_CTX(ctx);
   if (n_def) *n_def = 0;
   if (N == 0) return CRDT_OK;
@@ -802,6 +807,7 @@ static int egress_common(crdt_ctx *ctx, EgressPlan p, size_t N, uint64_t *frame_
 
 int crdt_vclock_egress(crdt_ctx *ctx, const uint64_t *rows, size_t N, size_t A, size_t row_stride,
                        const uint32_t *actors, uint64_t *frame_off, uint8_t *bytes, size_t cap, size_t *total) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
   if (ctx && N && (!rows || !actors || A == 0)) return fail(ctx, CRDT_EINVAL, "vclock_egress: NULL rows / actors");
   EgressPlan p{};
   p.rows = (const u64 *)rows;
@@ -815,6 +821,7 @@ int crdt_vclock_egress(crdt_ctx *ctx, const uint64_t *rows, size_t N, size_t A, 
 
 int crdt_pncounter_egress(crdt_ctx *ctx, const uint64_t *rows, size_t N, size_t A, size_t row_stride,
                           const uint32_t *actors, uint64_t *frame_off, uint8_t *bytes, size_t cap, size_t *total) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
   if (ctx && N && (!rows || !actors || A == 0)) return fail(ctx, CRDT_EINVAL, "pncounter_egress: NULL rows / actors");
   EgressPlan p{};
   p.rows = (const u64 *)rows;
@@ -828,6 +835,7 @@ int crdt_pncounter_egress(crdt_ctx *ctx, const uint64_t *rows, size_t N, size_t 
 
 int crdt_gset_egress(crdt_ctx *ctx, const uint64_t *rows, size_t N, size_t U, size_t row_stride, const uint64_t *elems,
                      uint64_t *frame_off, uint8_t *bytes, size_t cap, size_t *total) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
   if (ctx && N && (!rows || !elems || U == 0)) return fail(ctx, CRDT_EINVAL, "gset_egress: NULL rows / elems");
   EgressPlan p{};
   p.rows = (const u64 *)rows;
@@ -839,6 +847,7 @@ int crdt_gset_egress(crdt_ctx *ctx, const uint64_t *rows, size_t N, size_t U, si
 }
 
 int crdt_lwwreg_egress(crdt_ctx *ctx, const uint64_t *marker, const uint64_t *val, size_t N, uint8_t *bytes) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
   CRDT_CHECK_CTX(ctx);
   if (N == 0) return CRDT_OK;
   if (!marker || !val || !bytes) return fail(ctx, CRDT_EINVAL, "lwwreg_egress: NULL buffer");
@@ -853,6 +862,7 @@ int crdt_orswot_egress(crdt_ctx *ctx, const uint64_t *clock, const uint64_t *ent
                        const uint32_t *actors, const uint64_t *members, const uint64_t *def_off,
                        const uint64_t *def_clock, const uint64_t *def_members, const uint8_t *def_keep,
                        uint64_t *frame_off, uint8_t *bytes, size_t cap, size_t *total) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
   if (ctx && N && (!clock || !entries || !actors || !members || A == 0 || M == 0))
     return fail(ctx, CRDT_EINVAL, "orswot_egress: NULL state / dictionaries");
   if (ctx && def_off && (!def_clock || !def_members)) return fail(ctx, CRDT_EINVAL, "orswot_egress: NULL deferred");

@@ -12,8 +12,11 @@
 //!
 //! States are interned to the dense structure-of-arrays layout the kernels read (actors, members
 //! and set elements to dense indices; an absent actor is a 0 counter, exact because
-//! `VClock::apply_dot` never stores 0, `vclock.rs:155-159`), copied to HBM, merged, and rebuilt.
-//! Callers that keep replica states resident in HBM use [`ffi`] directly on device buffers.
+//! `VClock::apply_dot` never stores 0, `vclock.rs:155-159`), merged on the GPU, and rebuilt.
+//! The lattice types and `LWWReg` hand their host rows straight to the library through a second
+//! ctx in `CRDT_MEM_HOST` mode (it streams them through HBM in chunks, overlapping PCIe with the
+//! fold); `Orswot` stages its buffers with [`DeviceBuf`].  Callers that keep replica states
+//! resident in HBM use [`ffi`] directly on device buffers with [`GpuCtx::as_ptr`].
 //!
 //! Field access: `VClock::dots`, the `Orswot` fields and the `LWWReg` fields are already visible
 //! to an in-crate module; the maintainer changes `GCounter::inner`, `PNCounter::{p, n}` and
@@ -60,6 +63,8 @@ impl std::error::Error for GpuError {}
 /// A `crdt_ctx`: one per host thread, bound to one HIP device (scratch and stream owned here).
 pub struct GpuCtx {
     raw: *mut ffi::crdt_ctx,
+    /// Same device, `CRDT_MEM_HOST` mode: host pointers, staged by the library.
+    host: *mut ffi::crdt_ctx,
 }
 
 impl GpuCtx {
@@ -70,7 +75,24 @@ impl GpuCtx {
         if rc != ffi::CRDT_OK {
             return Err(GpuError { code: rc, msg: last_error(ptr::null()) });
         }
-        Ok(GpuCtx { raw })
+        let mut host = ptr::null_mut();
+        let rc = unsafe { ffi::crdt_ctx_create(device, &mut host) };
+        if rc != ffi::CRDT_OK {
+            unsafe { ffi::crdt_ctx_destroy(raw) };
+            return Err(GpuError { code: rc, msg: last_error(ptr::null()) });
+        }
+        let ctx = GpuCtx { raw, host };
+        ctx.check_host(unsafe { ffi::crdt_ctx_set_mem_kind(host, ffi::CRDT_MEM_HOST) })?;
+        Ok(ctx)
+    }
+
+    /// Status of a call issued on the host-memory ctx.
+    fn check_host(&self, rc: c_int) -> Result<(), GpuError> {
+        if rc == ffi::CRDT_OK {
+            Ok(())
+        } else {
+            Err(GpuError { code: rc, msg: last_error(self.host) })
+        }
     }
 
     /// The raw handle, for calls through [`ffi`] on caller-owned device buffers.
@@ -97,6 +119,7 @@ impl Drop for GpuCtx {
     fn drop(&mut self) {
         unsafe {
             ffi::crdt_ctx_destroy(self.raw);
+            ffi::crdt_ctx_destroy(self.host);
         }
     }
 }
@@ -192,39 +215,38 @@ enum Lattice {
     GSet,
 }
 
+// Host rows go to the CRDT_MEM_HOST ctx as they are: the library stages them (no DeviceBuf).
 fn lattice_lub(ctx: &GpuCtx, kind: Lattice, rows: &[u64], r: usize, w: usize) -> Result<Vec<u64>, GpuError> {
-    let input = DeviceBuf::from_host(rows)?;
-    let out = DeviceBuf::<u64>::zeroed(w)?;
+    let mut out = vec![0u64; w];
     let width = if let Lattice::PNCounter = kind { w / 2 } else { w };
     let rc = unsafe {
-        let (i, o) = (input.as_ptr(), out.as_mut_ptr());
+        let (i, o) = (rows.as_ptr(), out.as_mut_ptr());
         match kind {
-            Lattice::VClock => ffi::crdt_vclock_lub_many(ctx.raw, i, 1, r, width, w, r * w, o, w, 0),
-            Lattice::GCounter => ffi::crdt_gcounter_lub_many(ctx.raw, i, 1, r, width, w, r * w, o, w, 0),
-            Lattice::PNCounter => ffi::crdt_pncounter_lub_many(ctx.raw, i, 1, r, width, w, r * w, o, w, 0),
-            Lattice::GSet => ffi::crdt_gset_lub_many(ctx.raw, i, 1, r, width, w, r * w, o, w, 0),
+            Lattice::VClock => ffi::crdt_vclock_lub_many(ctx.host, i, 1, r, width, w, r * w, o, w, 0),
+            Lattice::GCounter => ffi::crdt_gcounter_lub_many(ctx.host, i, 1, r, width, w, r * w, o, w, 0),
+            Lattice::PNCounter => ffi::crdt_pncounter_lub_many(ctx.host, i, 1, r, width, w, r * w, o, w, 0),
+            Lattice::GSet => ffi::crdt_gset_lub_many(ctx.host, i, 1, r, width, w, r * w, o, w, 0),
         }
     };
-    ctx.check(rc)?;
-    out.to_host()
+    ctx.check_host(rc)?;
+    Ok(out)
 }
 
 fn lattice_pairs(ctx: &GpuCtx, kind: Lattice, selves: &[u64], others: &[u64], n: usize, w: usize)
                  -> Result<Vec<u64>, GpuError> {
-    let s = DeviceBuf::from_host(selves)?;
-    let o = DeviceBuf::from_host(others)?;
+    let mut s = selves.to_vec();
     let width = if let Lattice::PNCounter = kind { w / 2 } else { w };
     let rc = unsafe {
-        let (sp, op) = (s.as_mut_ptr(), o.as_ptr());
+        let (sp, op) = (s.as_mut_ptr(), others.as_ptr());
         match kind {
-            Lattice::VClock => ffi::crdt_vclock_merge_batch(ctx.raw, sp, op, n, width, w, w),
-            Lattice::GCounter => ffi::crdt_gcounter_merge_batch(ctx.raw, sp, op, n, width, w, w),
-            Lattice::PNCounter => ffi::crdt_pncounter_merge_batch(ctx.raw, sp, op, n, width, w, w),
-            Lattice::GSet => ffi::crdt_gset_merge_batch(ctx.raw, sp, op, n, width, w, w),
+            Lattice::VClock => ffi::crdt_vclock_merge_batch(ctx.host, sp, op, n, width, w, w),
+            Lattice::GCounter => ffi::crdt_gcounter_merge_batch(ctx.host, sp, op, n, width, w, w),
+            Lattice::PNCounter => ffi::crdt_pncounter_merge_batch(ctx.host, sp, op, n, width, w, w),
+            Lattice::GSet => ffi::crdt_gset_merge_batch(ctx.host, sp, op, n, width, w, w),
         }
     };
-    ctx.check(rc)?;
-    s.to_host()
+    ctx.check_host(rc)?;
+    Ok(s)
 }
 
 // ---- VClock / GCounter: elementwise max (vclock.rs:130-136, gcounter.rs:44-48) ----------------
@@ -442,13 +464,10 @@ impl<V: Ord + Clone + PartialEq> BatchFunkyLww for LWWReg<V, u64> {
         let mut vals = Index::new();
         let markers: Vec<u64> = replicas.iter().map(|x| x.marker).collect();
         let ids: Vec<u64> = replicas.iter().map(|x| vals.intern(&x.val) as u64).collect();
-        let (m, v) = (DeviceBuf::from_host(&markers)?, DeviceBuf::from_host(&ids)?);
-        let (om, ov, of) = (DeviceBuf::<u64>::zeroed(1)?, DeviceBuf::<u64>::zeroed(1)?, DeviceBuf::<u64>::zeroed(1)?);
-        ctx.check(unsafe {
-            ffi::crdt_lwwreg_lub_many(ctx.raw, m.as_ptr(), v.as_ptr(), 1, r, r, om.as_mut_ptr(), ov.as_mut_ptr(),
-                                      of.as_mut_ptr(), 0)
+        let (mut mk, mut vi, mut fc) = (0u64, 0u64, 0u64);
+        ctx.check_host(unsafe {
+            ffi::crdt_lwwreg_lub_many(ctx.host, markers.as_ptr(), ids.as_ptr(), 1, r, r, &mut mk, &mut vi, &mut fc, 0)
         })?;
-        let (mk, vi, fc) = (om.to_host()?[0], ov.to_host()?[0], of.to_host()?[0]);
         let state = LWWReg { val: vals.ids[vi as usize].clone(), marker: mk };
         Ok((state, if fc == u64::MAX { None } else { Some(fc as usize) }))
     }
@@ -464,14 +483,11 @@ impl<V: Ord + Clone + PartialEq> BatchFunkyLww for LWWReg<V, u64> {
         if n == 0 {
             return Ok(Vec::new());
         }
-        let (dsm, dsv) = (DeviceBuf::from_host(&sm)?, DeviceBuf::from_host(&sv)?);
-        let (dom, dov) = (DeviceBuf::from_host(&om)?, DeviceBuf::from_host(&ov)?);
-        let conflict = DeviceBuf::<u8>::zeroed(n)?;
-        ctx.check(unsafe {
-            ffi::crdt_lwwreg_merge_batch(ctx.raw, dsm.as_mut_ptr(), dsv.as_mut_ptr(), dom.as_ptr(), dov.as_ptr(), n,
-                                         conflict.as_mut_ptr())
+        let (mut m2, mut v2, mut c) = (sm, sv, vec![0u8; n]);
+        ctx.check_host(unsafe {
+            ffi::crdt_lwwreg_merge_batch(ctx.host, m2.as_mut_ptr(), v2.as_mut_ptr(), om.as_ptr(), ov.as_ptr(), n,
+                                         c.as_mut_ptr())
         })?;
-        let (m2, v2, c) = (dsm.to_host()?, dsv.to_host()?, conflict.to_host()?);
         let mut res = Vec::with_capacity(n);
         for i in 0..n {
             if c[i] != 0 {

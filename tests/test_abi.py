@@ -59,3 +59,30 @@ def test_ctypes_struct_layout_matches_header():
     # 5 dims + 4 x (ptr + 2 strides) + def_off + 3 ptrs = 21; out: Vout, Vstate + 8 ptrs = 10
     assert ctypes.sizeof(abi.MapBatch) == 21 * 8
     assert ctypes.sizeof(abi.MapOut) == 10 * 8
+
+
+HOST_CAPABLE = {f"crdt_{t}_{op}" for t in ("vclock", "gcounter", "pncounter", "gset", "lwwreg")
+                for op in ("lub_many", "merge_batch")}
+CTX_ONLY = {"crdt_ctx_destroy", "crdt_ctx_set_stream", "crdt_ctx_synchronize", "crdt_ctx_set_timing",
+            "crdt_ctx_timing", "crdt_ctx_timing_reset", "crdt_ctx_tune", "crdt_ctx_set_mem_kind",
+            "crdt_ctx_comm_init", "crdt_ctx_comm_destroy", "crdt_ctx_comm_info", "crdt_ctx_mem_kind"}
+
+
+def test_every_compute_entry_point_guards_host_mode():
+    """CRDT_MEM_HOST (include/crdt_gpu.h) is honoured by the lattice / lwwreg entry points only;
+    every other entry point taking a ctx must refuse it (CRDT_DEVICE_MEM_ONLY as its first
+    statement) rather than read host pointers as device memory."""
+    import glob
+    pat = re.compile(r'^(?:extern "C" )?int\s+(crdt_\w+)\(([^)]*)\)\s*\{\n(.*?)\n', re.M | re.S)
+    seen = set()
+    for f in glob.glob(os.path.join(ROOT, "rust-crdt_amd", "csrc", "*.*")):
+        for m in pat.finditer(open(f).read()):
+            name, args, first = m.group(1), m.group(2), m.group(3).strip()
+            if "crdt_ctx *ctx" not in args:
+                continue
+            seen.add(name)
+            if name in HOST_CAPABLE:
+                assert "CRDT_CHECK_CTX" in first or "_dispatch(ctx" in first or first.startswith("return crdt_"), name
+            elif name not in CTX_ONLY:
+                assert first.startswith("CRDT_DEVICE_MEM_ONLY(ctx);"), (f, name)
+    assert HOST_CAPABLE <= seen and len(seen) > 50

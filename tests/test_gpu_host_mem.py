@@ -1,0 +1,151 @@
+"""GPU parity of the host-memory mode (crdt_mem_kind = CRDT_MEM_HOST, csrc/host_stage.hip): the
+lattice and LWWReg entry points on HOST arrays, streamed through the device in chunks, against
+the oracle folds (vclock.rs:130-136, pncounter.rs:70-75, gset.rs:38-40, lwwreg.rs:43-45 / :84-98).
+Small chunk budgets (tune key stage_kb) force many chunks, group tiles and the chunk-boundary
+bookkeeping (accumulation, LWW first-conflict index offsets); pageable and pinned inputs, strided
+rows and the refusal paths are covered."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+import crdts_gpu as cg  # noqa: E402
+from crdts_gpu import host  # noqa: E402
+
+U64MAX = np.uint64(2**64 - 1)
+
+
+@pytest.fixture(scope="module")
+def hctx():
+    c = host.HostContext(0, tune="stage_kb=4")  # 4 KiB chunks: many chunks at test sizes
+    yield c
+    c.close()
+
+
+def rand_rows(rng, shape, hi=2**40):
+    return rng.integers(0, hi, size=shape, dtype=np.uint64)
+
+
+@pytest.mark.parametrize("kind", ["vclock", "gcounter", "pncounter", "gset"])
+@pytest.mark.parametrize("G,R,W", [(1, 1, 4), (1, 1000, 6), (3, 257, 64), (40, 9, 130), (700, 2, 8)])
+def test_lub_many_host(hctx, kind, G, R, W):
+    rng = np.random.default_rng(G * 1000 + R + W)
+    x = rand_rows(rng, (G, R, W))
+    exp = np.bitwise_or.reduce(x, axis=1) if kind == "gset" else x.max(axis=1)
+    for g in range(min(G, 3)):  # pin the numpy reduction on a few groups against the oracle
+        fold = O.gset_fold(x[g])[0] if kind == "gset" else O.vclock_fold(x[g])[0]
+        assert np.array_equal(fold, exp[g])
+    got = host.lub_many(kind, x, ctx=hctx)
+    assert np.array_equal(got, exp)
+    # pinned input, strided rows (a column slice of wider rows), strided output, accumulate
+    wide = host.pinned_empty((G, R, W + 3))
+    wide[...] = rand_rows(rng, (G, R, W + 3))
+    view = wide[:, :, 1:W + 1]
+    out_wide = np.zeros((G, W + 5), np.uint64)
+    out = out_wide[:, 2:W + 2]
+    out[...] = rand_rows(rng, (G, W))
+    start = out.copy()
+    host.lub_many(kind, view, out=out, accumulate=True, ctx=hctx)
+    red = np.bitwise_or.reduce(view, axis=1) if kind == "gset" else view.max(axis=1)
+    assert np.array_equal(out, (start | red) if kind == "gset" else np.maximum(start, red))
+    assert not out_wide[:, :2].any() and not out_wide[:, W + 2:].any()
+
+
+def test_lub_many_host_edges(hctx):
+    out = np.full((2, 4), 7, np.uint64)
+    host.lub_many("vclock", np.zeros((2, 0, 4), np.uint64), out=out, ctx=hctx)
+    assert not out.any()  # fold of nothing = VClock::new()
+    out[...] = 5
+    host.lub_many("vclock", np.zeros((2, 0, 4), np.uint64), out=out, accumulate=True, ctx=hctx)
+    assert (out == 5).all()
+    big = host.HostContext(0)  # default 256 MiB chunks: one chunk
+    x = rand_rows(np.random.default_rng(3), (5000, 256))
+    assert np.array_equal(host.lub_many("gcounter", x, ctx=big), x.max(axis=0))
+    big.close()
+
+
+@pytest.mark.parametrize("kind", ["vclock", "pncounter", "gset"])
+@pytest.mark.parametrize("N,W", [(1, 4), (1000, 6), (37, 300)])
+def test_merge_batch_host(hctx, kind, N, W):
+    rng = np.random.default_rng(N + W)
+    a, b = rand_rows(rng, (N, W)), rand_rows(rng, (N, W))
+    exp = (a | b) if kind == "gset" else np.maximum(a, b)
+    if kind == "vclock":
+        assert np.array_equal(O.vclock_merge_pairs(a, b), exp)
+    got = host.merge_batch(kind, a.copy(), b, ctx=hctx)
+    assert np.array_equal(got, exp)
+    # strided self / other rows
+    sw, ow = rand_rows(rng, (N, W + 2)), rand_rows(rng, (N, W + 1))
+    s0 = sw.copy()
+    host.merge_batch(kind, sw[:, 1:W + 1], ow[:, :W], ctx=hctx)
+    e2 = (s0[:, 1:W + 1] | ow[:, :W]) if kind == "gset" else np.maximum(s0[:, 1:W + 1], ow[:, :W])
+    assert np.array_equal(sw[:, 1:W + 1], e2)
+    assert np.array_equal(sw[:, 0], s0[:, 0]) and np.array_equal(sw[:, W + 1], s0[:, W + 1])
+
+
+def lww_case(rng, G, R, n_markers):
+    m = rng.integers(0, n_markers, size=(G, R), dtype=np.uint64)
+    v = rng.integers(0, 3, size=(G, R), dtype=np.uint64)
+    return m, v
+
+
+@pytest.mark.parametrize("G,R,nm", [(1, 5000, 50), (7, 1300, 4000), (300, 3, 2), (1, 1, 5), (2000, 17, 5)])
+def test_lwwreg_lub_many_host(hctx, G, R, nm):
+    rng = np.random.default_rng(G + R)
+    m, v = lww_case(rng, G, R, nm)
+    got = host.lwwreg_lub_many(m, v, ctx=hctx)
+    for g in range(G):
+        om, ov, fc, _ = O.lwwreg_fold(m[g], v[g])
+        assert (int(got.marker[g]), int(got.val[g]), int(got.first_conflict[g])) == (om, ov, fc), g
+
+
+def test_lwwreg_conflict_in_later_chunk(hctx):
+    """The first conflicting merge sits beyond the first chunk (4 KiB = 256 replicas per chunk
+    at G = 1): its index must be the global one."""
+    R = 2000
+    m = np.arange(1, R + 1, dtype=np.uint64)
+    v = np.zeros(R, np.uint64)
+    m[1500] = m[1499]
+    v[1500] = 9  # same marker, different value -> Err at replica 1500
+    m[1800] = m[1799] = 10**9
+    v[1800] = 1  # a later conflict too
+    got = host.lwwreg_lub_many(m, v, ctx=hctx)
+    om, ov, fc, _ = O.lwwreg_fold(m, v)
+    assert fc == 1500 and int(got.first_conflict[0]) == 1500
+    assert (int(got.marker[0]), int(got.val[0])) == (om, ov)
+
+
+def test_lwwreg_merge_batch_host(hctx):
+    rng = np.random.default_rng(5)
+    N = 3000
+    sm, sv = lww_case(rng, 1, N, 4)
+    om_, ov_ = lww_case(rng, 1, N, 4)
+    sm, sv, om_, ov_ = sm[0].copy(), sv[0].copy(), om_[0], ov_[0]
+    s0m, s0v = sm.copy(), sv.copy()
+    conflict = host.lwwreg_merge_batch(sm, sv, om_, ov_, ctx=hctx)
+    for i in range(N):
+        em, ev, fc, _ = O.lwwreg_fold(np.array([s0m[i], om_[i]]), np.array([s0v[i], ov_[i]]))
+        assert (int(sm[i]), int(sv[i]), int(conflict[i])) == (em, ev, int(fc == 1)), i
+
+
+def test_host_mode_refusals(hctx):
+    # a device pointer handed to host mode is rejected, not read
+    d = torch.zeros((4, 8), dtype=torch.int64, device="cuda")
+    out = np.zeros(8, np.uint64)
+    rc = hctx.raw("crdt_vclock_lub_many", ctypes.c_void_p(d.data_ptr()), 1, 4, 8, 8, 32, ctypes.c_void_p(out.ctypes.data), 8, 0)
+    assert rc == cg._abi.CRDT_EINVAL
+    # entry points without a host path refuse the mode
+    assert hctx.raw("crdt_vclock_apply_batch", None, 0, 0, 0, None, None, None, 0, None) == -4
+    assert hctx.raw("crdt_orswot_lub_many", None, None) == -4
+    assert hctx.raw("crdt_map_lub_many", None, None) == -4
+    assert hctx.raw("crdt_vclock_ingest", None, None, 0, None, 0, None, 0, None) == -4
+    assert hctx.raw("crdt_vclock_lub_many_sharded", None, 0, 0, 0, 0, 0, None) == -4
+    assert hctx.lib.crdt_ctx_mem_kind(hctx.ptr) == cg._abi.CRDT_MEM_HOST
+    # device mode is unaffected on another ctx
+    ctx = cg.Context(0)
+    assert ctx.lib.crdt_ctx_mem_kind(ctx.ptr) == cg._abi.CRDT_MEM_DEVICE

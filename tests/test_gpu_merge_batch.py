@@ -163,6 +163,57 @@ def test_map_merge_batch_replay(gpu_ctx, seed, N, n_origins, K, n_ops):
     assert sum(len(m.entries) for m in exp) > 0
 
 
+def arbitrary_maps(rng, n, K, A, V, cmax, max_def=3):
+    maps = []
+    for _ in range(n):
+        clock = rng.integers(0, cmax, size=A).astype(np.uint64)
+        ec = rng.integers(0, cmax + 1, size=(K, A)).astype(np.uint64)
+        ec[rng.random(K) < 0.3] = 0
+        vclk = rng.integers(0, cmax + 1, size=(K, V, A)).astype(np.uint64)
+        vclk[rng.random((K, V, A)) < 0.5] = 0
+        vval = rng.integers(0, 9, size=(K, V)).astype(np.uint64)
+        for k in range(K):  # one register never holds two equal clocks (mvreg.rs:72 sanity check)
+            for s in range(1, V):
+                if any(np.array_equal(vclk[k, s], vclk[k, t]) for t in range(s)):
+                    vclk[k, s] = 0
+        deferred = []
+        for _ in range(int(rng.integers(0, max_def))):
+            rm = rng.integers(0, cmax + 2, size=A).astype(np.uint64) * (rng.random(A) < 0.3)
+            if rm.any() and not any(np.array_equal(rm, r) for r, _ in deferred):
+                deferred.append((rm, set(int(x) for x in rng.choice(K, size=int(rng.integers(1, K + 1)), replace=False))))
+        maps.append(O.dense_to_map(clock, ec, vclk, vval, deferred))
+    return maps
+
+
+@pytest.mark.parametrize("reg", [1, 2, 0])
+@pytest.mark.parametrize("seed,N,K,A,V,cmax", [(21, 40, 5, 3, 2, 4), (22, 25, 9, 33, 2, 3), (23, 16, 4, 70, 1, 3),
+                                               (24, 30, 70, 8, 3, 6), (25, 12, 3, 200, 2, 2), (26, 20, 6, 5, 5, 3),
+                                               (27, 24, 7, 32, 2, 4), (28, 9, 5, 17, 4, 3)])
+def test_map_merge_batch_arbitrary_kernels(gpu_ctx, reg, seed, N, K, A, V, cmax):
+    """Arbitrary dense states through each Map key kernel: the sub-wave register kernel (mpreg=1:
+    16 / 32 / 64 lanes per key by A), the whole-wave register kernel (mpreg=2, and A > 64 under
+    1) and the generic one (mpreg=0, and self V = 5 under every setting): identical to the oracle."""
+    rng = np.random.default_rng(seed)
+    maps = arbitrary_maps(rng, N, K, A, V, cmax) + arbitrary_maps(rng, N, K, A, min(V, 2), cmax)
+    gpu_ctx.tune(f"mpreg={reg}")
+    try:
+        map_check(gpu_ctx, maps[:N], maps[N:], K, A)
+    finally:
+        gpu_ctx.tune("mpreg=1")
+
+
+def test_map_merge_batch_many_removes(gpu_ctx):
+    """More than 64 deferred removes on one pair (the register kernel's remove-bit batch spans
+    several waves' worth of lanes)."""
+    rng = np.random.default_rng(31)
+    maps = arbitrary_maps(rng, 4, 6, 4, 2, 40, max_def=1)
+    for m, nd in zip(maps, (40, 3, 35, 70)):
+        while len(m.deferred) < nd:
+            rm = O.VClock({int(a): int(rng.integers(41, 200)) for a in rng.choice(4, size=2, replace=False)})
+            m.deferred.setdefault(rm, set()).update(int(x) for x in rng.choice(6, size=2, replace=False))
+    map_check(gpu_ctx, maps[:2], maps[2:], 6, 4)
+
+
 @pytest.mark.parametrize("seed,N,K,A,V,cmax", [(21, 40, 5, 3, 2, 4), (22, 25, 9, 33, 2, 3), (23, 16, 4, 70, 1, 3),
                                                (24, 30, 70, 8, 3, 6), (25, 12, 3, 200, 2, 2)])
 def test_map_merge_batch_arbitrary(gpu_ctx, seed, N, K, A, V, cmax):

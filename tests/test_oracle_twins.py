@@ -24,6 +24,15 @@ def test_vclock_fold_twins(R, A, seed):
     np.testing.assert_array_equal(got, rows.max(axis=0))  # dense restatement a2
 
 
+@pytest.mark.parametrize("R,A,T", [(1, 3, 4), (1000, 256, 3), (77, 1024, 8)])
+def test_dense_max_mt_is_the_fold(R, A, T):
+    """The dense-SoA CPU fold of bench.py's cpu_baseline.dense_soa equals the map-based fold."""
+    rows = O.synth_matrix(R + A, R, A, 0)
+    got, _ = O.dense_max_mt(rows, T)
+    np.testing.assert_array_equal(got, O.counter_fold_mt(rows, False, T)[0])
+    np.testing.assert_array_equal(got, rows.max(axis=0))
+
+
 def test_pncounter_fold_twins():
     rows = O.synth_matrix(9, 50, 2 * 12, 0)
     got, _ = O.pncounter_fold(rows)
