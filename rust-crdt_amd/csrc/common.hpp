@@ -63,6 +63,7 @@ struct Tune {
   int apply_hot_slots = 8;     // Orswot apply: deferred slots kept in LDS per state (the rest in HBM)
   int map_forget_vec2 = 1;     // Map forget: 16-byte pieces per lane where the shape allows it
   int map_pair_reg = 1;        // Map merge_batch, V <= 4: 1 sub-wave register kernel, 2 whole-wave one, 0 generic
+  int pair_rows = 128;         // Orswot merge_batch: member rows per workgroup (64, 128, 256)
   int stage_kb = 262144;       // CRDT_MEM_HOST: bytes per device chunk buffer (KiB; two buffers)
 };
 

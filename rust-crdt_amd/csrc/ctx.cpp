@@ -212,6 +212,7 @@ static void apply_tune(crdt_ctx *ctx, const char *t) {
       else if (k == "mfv2") ctx->tune.map_forget_vec2 = v != 0;
       else if (k == "stage_kb" && v >= 4) ctx->tune.stage_kb = v;
       else if (k == "mpreg" && v >= 0 && v <= 2) ctx->tune.map_pair_reg = v;
+      else if (k == "prows" && (v == 64 || v == 128 || v == 256)) ctx->tune.pair_rows = v;
     }
     pos = end + 1;
   }

@@ -117,7 +117,7 @@ __global__ __launch_bounds__(kBlock) void pair_deferred_kernel(PairDefPlan p) {
 
 // ---- Orswot entry join --------------------------------------------------------------------------
 constexpr int kPairGroups = 16;  // deferred removes per pair handled: 32 * kPairGroups
-constexpr int kPairRows = 64;    // member rows per workgroup
+constexpr int kPairUR = 8;       // member rows per thread with loads in flight together
 
 struct OrswotPairPlan {
   u64 *e1;
@@ -150,7 +150,7 @@ __device__ __forceinline__ u64 cell_join(u64 e1, u64 e2, u64 c1, u64 c2) {  // o
 // pieces (V = 2: 16-byte non-temporal accesses), 256 >> lp_log rows per pass.  Per block the
 // deferred removes of both sides are turned into hit masks in LDS (bit d of hit[g][row] = remove
 // 32g + d names that member); a cell with hits forgets by each hit remove's rm (global, L2).
-template <int V>
+template <int V, int kPairRows>
 __global__ __launch_bounds__(kBlock) void orswot_pair_join_kernel(OrswotPairPlan p) {
   __shared__ unsigned hit[kPairGroups][kPairRows];
   const unsigned long long s = blockIdx.x / p.mblocks;
@@ -159,19 +159,21 @@ __global__ __launch_bounds__(kBlock) void orswot_pair_join_kernel(OrswotPairPlan
   if (n1 > p.D1 || n2 > p.D2) return;  // reported by pair_deferred_kernel, state untouched
   const unsigned nd = n1 + n2;
   const unsigned ng = (nd + 31) / 32;
-  for (unsigned i = threadIdx.x; i < ng * kPairRows; i += kBlock) {
-    const unsigned g = i / kPairRows, r = i % kPairRows;
-    const unsigned long long m = m0 + r;
-    unsigned mask = 0;
-    if (m < p.M) {
-      for (unsigned d = g * 32; d < nd && d < g * 32 + 32; ++d) {
-        const u64 *b = d < n1 ? p.d1b + (s * p.D1 + d) * p.Mw : p.d2b + (s * p.D2 + (d - n1)) * p.Mw;
-        if ((b[m / 64] >> (m % 64)) & 1ull) mask |= 1u << (d - g * 32);
+  if (ng) {  // workgroup-uniform: most pairs carry no removes and skip the masks and the barrier
+    for (unsigned i = threadIdx.x; i < ng * kPairRows; i += kBlock) {
+      const unsigned g = i / kPairRows, r = i % kPairRows;
+      const unsigned long long m = m0 + r;
+      unsigned mask = 0;
+      if (m < p.M) {
+        for (unsigned d = g * 32; d < nd && d < g * 32 + 32; ++d) {
+          const u64 *b = d < n1 ? p.d1b + (s * p.D1 + d) * p.Mw : p.d2b + (s * p.D2 + (d - n1)) * p.Mw;
+          if ((b[m / 64] >> (m % 64)) & 1ull) mask |= 1u << (d - g * 32);
+        }
       }
+      hit[g][r] = mask;
     }
-    hit[g][r] = mask;
+    __syncthreads();
   }
-  __syncthreads();
   const int lpr = 1 << p.lp_log;
   const int piece = threadIdx.x & (lpr - 1);
   const int rows_per_pass = kBlock >> p.lp_log;
@@ -185,40 +187,53 @@ __global__ __launch_bounds__(kBlock) void orswot_pair_join_kernel(OrswotPairPlan
       k1[v] = a0 + v < p.A ? c1[a0 + v] : 0ull;
       k2[v] = a0 + v < p.A ? c2[a0 + v] : 0ull;
     }
-    for (int r = threadIdx.x >> p.lp_log; r < kPairRows; r += rows_per_pass) {
-      const unsigned long long m = m0 + r;
-      if (m >= p.M) break;
-      u64 *pe1 = p.e1 + s * p.e1_s + m * p.e1_m + a0;
-      const u64 *pe2 = p.e2 + s * p.e2_s + m * p.e2_m + a0;
-      u64 x[V], y[V];
-      if constexpr (V == 2) {
-        const u64x2 a = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(pe1));
-        const u64x2 b = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(pe2));
-        x[0] = a.x, x[1] = a.y, y[0] = b.x, y[1] = b.y;
-      } else {
-        x[0] = __builtin_nontemporal_load(pe1);
-        y[0] = __builtin_nontemporal_load(pe2);
-      }
+    // UR rows per thread in flight: all their loads are issued before the first store (a store to
+    // self's row could otherwise alias the next row's loads and serialize the round trips)
+    for (int rb = threadIdx.x >> p.lp_log; rb < kPairRows; rb += rows_per_pass * kPairUR) {
+      u64 x[kPairUR][V], y[kPairUR][V];
 #pragma unroll
-      for (int v = 0; v < V; ++v) x[v] = cell_join(x[v], y[v], k1[v], k2[v]);
-      for (unsigned g = 0; g < ng; ++g) {
-        unsigned mask = hit[g][r];
-        while (mask) {
-          const unsigned d = g * 32 + __builtin_ctz(mask);
-          mask &= mask - 1;
-          const u64 *rm = d < n1 ? p.d1c + (s * p.D1 + d) * p.A : p.d2c + (s * p.D2 + (d - n1)) * p.A;
-#pragma unroll
-          for (int v = 0; v < V; ++v)
-            if (a0 + v < p.A && x[v] <= rm[a0 + v]) x[v] = 0;  // VClock::forget, vclock.rs:95-105
+      for (int u = 0; u < kPairUR; ++u) {
+        const int r = rb + u * rows_per_pass;
+        const unsigned long long m = m0 + r;
+        if (r >= kPairRows || m >= p.M) break;
+        const u64 *pe1 = p.e1 + s * p.e1_s + m * p.e1_m + a0;
+        const u64 *pe2 = p.e2 + s * p.e2_s + m * p.e2_m + a0;
+        if constexpr (V == 2) {
+          const u64x2 a = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(pe1));
+          const u64x2 b = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(pe2));
+          x[u][0] = a.x, x[u][1] = a.y, y[u][0] = b.x, y[u][1] = b.y;
+        } else {
+          x[u][0] = __builtin_nontemporal_load(pe1);
+          y[u][0] = __builtin_nontemporal_load(pe2);
         }
       }
-      if constexpr (V == 2) {
-        u64x2 o;
-        o.x = x[0];
-        o.y = x[1];
-        __builtin_nontemporal_store(o, reinterpret_cast<u64x2 *>(pe1));
-      } else {
-        __builtin_nontemporal_store(x[0], pe1);
+#pragma unroll
+      for (int u = 0; u < kPairUR; ++u) {
+        const int r = rb + u * rows_per_pass;
+        const unsigned long long m = m0 + r;
+        if (r >= kPairRows || m >= p.M) break;
+#pragma unroll
+        for (int v = 0; v < V; ++v) x[u][v] = cell_join(x[u][v], y[u][v], k1[v], k2[v]);
+        for (unsigned g = 0; g < ng; ++g) {
+          unsigned mask = hit[g][r];
+          while (mask) {
+            const unsigned d = g * 32 + __builtin_ctz(mask);
+            mask &= mask - 1;
+            const u64 *rm = d < n1 ? p.d1c + (s * p.D1 + d) * p.A : p.d2c + (s * p.D2 + (d - n1)) * p.A;
+#pragma unroll
+            for (int v = 0; v < V; ++v)
+              if (a0 + v < p.A && x[u][v] <= rm[a0 + v]) x[u][v] = 0;  // VClock::forget, vclock.rs:95-105
+          }
+        }
+        u64 *pe1 = p.e1 + s * p.e1_s + m * p.e1_m + a0;
+        if constexpr (V == 2) {
+          u64x2 o;
+          o.x = x[u][0];
+          o.y = x[u][1];
+          __builtin_nontemporal_store(o, reinterpret_cast<u64x2 *>(pe1));
+        } else {
+          __builtin_nontemporal_store(x[u][0], pe1);
+        }
       }
     }
   }
@@ -887,7 +902,8 @@ extern "C" int crdt_orswot_merge_batch(crdt_ctx *ctx, const crdt_orswot_states *
     const unsigned long long W = v2 ? A / 2 : A;
     int lp = 0;
     while (lp < 6 && (1ull << lp) < W) ++lp;
-    const unsigned long long mblocks = (M + kPairRows - 1) / kPairRows;
+    const int rows = ctx->tune.pair_rows;  // member rows per workgroup (64, 128, 256)
+    const unsigned long long mblocks = (M + rows - 1) / rows;
     if (N * mblocks > 0x7FFFFFFFull) return fail(ctx, CRDT_EUNSUPPORTED, "orswot_merge_batch: grid too large");
     OrswotPairPlan p{(u64 *)a.entries, a.entry_mstride, a.entry_sstride, (const u64 *)b.entries, b.entry_mstride,
                      b.entry_sstride, (const u64 *)a.clock, a.clock_stride, (const u64 *)b.clock, b.clock_stride,
@@ -895,10 +911,18 @@ extern "C" int crdt_orswot_merge_batch(crdt_ctx *ctx, const crdt_orswot_states *
                      (const u64 *)b.def_clock, (const u64 *)b.def_members, b.Dcap ? b.def_count : nullptr, b.Dcap,
                      N, M, A, Mw, mblocks, lp};
     timing_begin(ctx, "orswot_pair_join");
-    if (v2)
-      hipLaunchKernelGGL(orswot_pair_join_kernel<2>, dim3((unsigned)(N * mblocks)), dim3(kBlock), 0, ctx->stream, p);
-    else
-      hipLaunchKernelGGL(orswot_pair_join_kernel<1>, dim3((unsigned)(N * mblocks)), dim3(kBlock), 0, ctx->stream, p);
+    const dim3 grid((unsigned)(N * mblocks));
+#define CRDT_PAIR_JOIN(VV, RR) hipLaunchKernelGGL((orswot_pair_join_kernel<VV, RR>), grid, dim3(kBlock), 0, ctx->stream, p)
+    if (v2) {
+      if (rows == 64) CRDT_PAIR_JOIN(2, 64);
+      else if (rows == 256) CRDT_PAIR_JOIN(2, 256);
+      else CRDT_PAIR_JOIN(2, 128);
+    } else {
+      if (rows == 64) CRDT_PAIR_JOIN(1, 64);
+      else if (rows == 256) CRDT_PAIR_JOIN(1, 256);
+      else CRDT_PAIR_JOIN(1, 128);
+    }
+#undef CRDT_PAIR_JOIN
     timing_end(ctx);
     CRDT_HIP(ctx, hipGetLastError());
   }

@@ -34,9 +34,11 @@ def timed(name, fn, reset, reps=5):
     return ms / n / 1e3
 
 
+MAP_ONLY = os.environ.get("FORGET_MAP_ONLY") == "1"  # spread diagnosis: skip the Orswot part
 # ---- Orswot
 N, M, A = 16384, 4096, 64
-src = torch.empty((N, M, A), dtype=torch.int64, device="cuda")
+src = torch.empty((N if not MAP_ONLY else 1, M, A), dtype=torch.int64, device="cuda")
+N = src.shape[0]
 cg.synth_fill(ctx, src.view(N * M, A), 0x5EED0021, 0)
 src.remainder_(64)  # small counters so the forget clears a fair share
 ent = torch.empty_like(src)
@@ -95,6 +97,9 @@ ef = np.where(e0 > yy[:, None, :], e0, 0)
 alive = ef.any(axis=2)
 vf = np.where(v0 > yy[:, None, None, :], v0, 0) * alive[:, :, None, None]
 ok = bool(np.array_equal(e1, ef) and np.array_equal(v1, vf))
+base = min(ec0.data_ptr(), ec.data_ptr())
 print(json.dumps({"op": "map_forget_batch", "states": N, "keys": K, "actors": A, "vals": V, "kernel_us": t * 1e6,
+                  "offsets_gib": {k: (v.data_ptr() - base) / 2**30 for k, v in (("ec0", ec0), ("vc0", vc0), ("ec", ec),
+                                                                              ("vc", vc), ("vv", vv))},
                   "GBs": nbytes / t / 1e9, "frac_of_8TBs": nbytes / t / 8e12,
                   "parity": "ok" if ok else "MISMATCH"}), flush=True)

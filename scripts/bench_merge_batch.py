@@ -153,6 +153,24 @@ def mapb():
     return ok
 
 
+def calib():
+    """The same 2-read-1-write byte stream through the plain lattice merge_batch (VClock rows of
+    256 actors, crdt_vclock_merge_batch): the practical ceiling of a read-self / read-other /
+    write-self pass on this part, beside the 8 TB/s peak."""
+    rows = args.orswot_pairs * 4096 * 64 // 256
+    a = torch.empty((rows, 256), dtype=torch.int64, device=dev)
+    b = torch.empty_like(a)
+    cg.synth_fill(ctx, a, 0x5EED0031, 0)
+    cg.synth_fill(ctx, b, 0x5EED0032, 0)
+    ms = timed(lambda: cg.vclock.merge_batch(a, b, ctx=ctx), lambda: None)
+    alg = 3 * a.numel() * 8
+    print(json.dumps({"op": "calibration_vclock_merge_batch", "rows": rows, "actors": 256, "ms": ms,
+                      "algorithmic_bytes": alg, "GBs": alg / ms / 1e6, "frac_of_8TBs": alg / ms / 8e9}), flush=True)
+    del a, b
+    torch.cuda.empty_cache()
+
+
+calib()
 good = orswot()
 torch.cuda.empty_cache()
 good = mapb() and good
