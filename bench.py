@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--actors", type=int, default=None, help="default 256 (c2) / 1024 (c5)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="target fold seconds of the CPU baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--fused", action=argparse.BooleanOptionalAction, default=True,
+                    help="all lubs of a step in one launch (crdt_lub_many_multi); --no-fused: one launch per lub")
     ap.add_argument("--exchange", choices=("cabi", "torch"), default="cabi",
                     help="N > 1: the C ABI's own RCCL communicator (crdt_*_lub_many_sharded) or torch.distributed")
     ap.add_argument("--dist-backend", default="nccl",
@@ -189,7 +191,18 @@ def main():
     mods = {"vclock": cg.vclock, "gcounter": cg.gcounter, "pncounter": cg.pncounter}
     torch.cuda.synchronize()
 
+    items = [(kind, x, o) for (kind, x, _), o in zip(lubs, outs)]
+
     def step():
+        if args.fused:  # every lub of the step in ONE launch (crdt_lub_many_multi)
+            if cabi:  # + one grouped ncclAllReduce(ncclUint64, ncclMax) per step
+                cg.shard.lub_many_multi_sharded(items, ctx=ctx)
+            else:
+                cg.lub_many_multi(items, ctx=ctx)
+                if world > 1:
+                    for o in outs:
+                        cdist.allreduce_umax_(o)
+            return
         for (kind, x, _), o in zip(lubs, outs):
             if cabi:  # local lub + one ncclAllReduce(ncclUint64, ncclMax), one C call
                 o.copy_(cg.shard.lub_many_sharded(kind, x, ctx=ctx))
@@ -236,7 +249,8 @@ def main():
     merges_per_step = len(lubs) * R * world
     value = merges_per_step * args.steps / elapsed
     bytes_per_step = sum(R * x.shape[1] * 8 + x.shape[1] * 8 for _, x, _ in lubs)
-    avg_launch_bytes = bytes_per_step / len(lubs)
+    launches_per_step = launches / args.steps if launches else float(len(lubs))
+    avg_launch_bytes = bytes_per_step / launches_per_step
     avg_launch_s = (kern_ms / 1e3) / launches if launches else float("nan")
     achieved = avg_launch_bytes / avg_launch_s / 1e9
     workload = (f"vclock lub {R}x{A} (config 5 shard)" if args.workload == "c5"
@@ -245,7 +259,7 @@ def main():
     try:
         with open(args.traffic_json) as f:
             tj = json.load(f)
-        if tj.get("workload") == workload:
+        if tj.get("workload") == workload and tj.get("fused", False) == bool(args.fused):
             traffic = tj.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
@@ -274,11 +288,14 @@ def main():
                               f"lub ({sum(x.shape[1] for _, x, _ in lubs)} words per step)") if cabi else
                              "torch.distributed all-reduce MAX (sign-biased u64)") if world > 1 else "none",
                 "parallelism": f"replica-shard x{world}",
+                "launches_per_step": launches_per_step,
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": ("lub_stream_kernel<Max,2,8> (VClock launch)" if args.workload == "c5"
-                           else "lub_stream_kernel<Max,2,8> (GCounter + PNCounter launches)"),
+                "kernel": (("lub_multi_kernel<Max,2,8>" if args.fused else "lub_stream_kernel<Max,2,8>")
+                           + (" (VClock launch)" if args.workload == "c5" else
+                              (" (GCounter + PNCounter in one launch)" if args.fused
+                               else " (GCounter + PNCounter launches)"))),
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

@@ -133,6 +133,25 @@ int crdt_gset_lub_many(crdt_ctx *ctx, const uint64_t *in, size_t G, size_t R, si
 int crdt_gset_merge_batch(crdt_ctx *ctx, uint64_t *self, const uint64_t *other, size_t N,
                           size_t words, size_t self_stride, size_t other_stride);
 
+/* ---- several lattice lubs in one launch ------------------------------------------------------
+ * Each segment is one crdt_{vclock,gcounter,pncounter,gset}_lub_many call (same dims, strides,
+ * flags and result); segments of the same join (max: VClock / GCounter / PNCounter; or: GSet)
+ * run in ONE launch (up to 8 per launch), so a batch of CRDT states of several types pays one
+ * launch ramp and tail.  A = counters per replica (PNCounter: per half) or words (GSet). */
+#define CRDT_KIND_VCLOCK 1
+#define CRDT_KIND_GCOUNTER 2
+#define CRDT_KIND_PNCOUNTER 3
+#define CRDT_KIND_GSET 4
+typedef struct crdt_lub_segment {
+  int kind; /* CRDT_KIND_* */
+  const uint64_t *in;
+  size_t G, R, A, row_stride, group_stride;
+  uint64_t *out;
+  size_t out_stride;
+  unsigned flags;
+} crdt_lub_segment;
+int crdt_lub_many_multi(crdt_ctx *ctx, const crdt_lub_segment *segs, size_t nseg);
+
 /* ---- LWWReg<u64 val, u64 marker> -------------------------------------------------------
  * Replaces FunkyCvRDT::merge for LWWReg (lwwreg.rs:43-45 → update :84-98).
  * lub_many folds group g as acc = replica[g][0]; for r in 1..R: acc.merge(replica[g][r]),
@@ -377,6 +396,10 @@ typedef struct crdt_orswot_sharded_out {
 } crdt_orswot_sharded_out;
 
 int crdt_orswot_lub_many_sharded(crdt_ctx *ctx, const crdt_orswot_batch *in, crdt_orswot_sharded_out *out);
+/* crdt_lub_many_multi over replica shards: one fused local launch, then ONE grouped RCCL call
+ * (an in-place ncclMax all-reduce per max segment; GSet segments as crdt_gset_lub_many_sharded).
+ * Outputs must be contiguous (out_stride == row words, or G == 1). */
+int crdt_lub_many_multi_sharded(crdt_ctx *ctx, const crdt_lub_segment *segs, size_t nseg);
 
 /* LWWReg (lwwreg.rs:43-45 -> update :84-98), replicas split in rank order: rank k holds replicas
  * [base_k, base_k + R_k) of every group (marker / val at [g*group_stride + r], R_k may be 0) and

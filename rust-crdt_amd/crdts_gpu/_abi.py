@@ -21,6 +21,7 @@ CRDT_UNIQUE_ID_BYTES = 128
 CRDT_ACCUMULATE = 0x1
 CRDT_MEM_DEVICE = 0
 CRDT_MEM_HOST = 1
+CRDT_KIND = {"vclock": 1, "gcounter": 2, "pncounter": 3, "gset": 4}
 
 # Every symbol declared in include/crdt_gpu.h (checked by tests/test_abi.py).
 EXPORTS = (
@@ -46,6 +47,7 @@ EXPORTS = (
     "crdt_orswot_forget_batch", "crdt_map_forget_batch", "crdt_map_apply_batch",
     "crdt_orswot_merge_batch", "crdt_map_merge_batch",
     "crdt_ctx_set_mem_kind", "crdt_ctx_mem_kind", "crdt_host_alloc", "crdt_host_free",
+    "crdt_lub_many_multi", "crdt_lub_many_multi_sharded",
 )
 
 
@@ -114,6 +116,11 @@ class MapDeferred(ctypes.Structure):  # crdt_map_deferred
     _fields_ = [("clock", P), ("keys", P), ("count", P), ("Dcap", S)]
 
 
+class LubSegment(ctypes.Structure):  # crdt_lub_segment
+    _fields_ = [("kind", ctypes.c_int), ("in_", P), ("G", S), ("R", S), ("A", S), ("row_stride", S),
+                ("group_stride", S), ("out", P), ("out_stride", S), ("flags", ctypes.c_uint)]
+
+
 class MapBatch(ctypes.Structure):  # crdt_map_batch
     _fields_ = [
         ("G", S), ("R", S), ("K", S), ("A", S), ("V", S),
@@ -146,6 +153,8 @@ _SIGS = {
     "crdt_ctx_mem_kind": ([P], ctypes.c_int),
     "crdt_host_alloc": ([S, ctypes.POINTER(P)], ctypes.c_int),
     "crdt_host_free": ([P], ctypes.c_int),
+    "crdt_lub_many_multi": ([P, ctypes.POINTER(LubSegment), S], ctypes.c_int),
+    "crdt_lub_many_multi_sharded": ([P, ctypes.POINTER(LubSegment), S], ctypes.c_int),
     "crdt_synth_fill": ([P, P, S, S, S, S, U64, ctypes.c_int], ctypes.c_int),
     "crdt_synth_orswot": ([P, P, P, S, S, S, S, U64, U64], ctypes.c_int),
     "crdt_synth_orswot_rm": ([P, P, S, S, S, P, P, P], ctypes.c_int),

@@ -64,6 +64,18 @@ def lub_many_sharded(kind: str, shard: torch.Tensor, ctx: Optional[Context] = No
     return out[0] if shard.dim() == 2 else out
 
 
+def lub_many_multi_sharded(items, ctx: Optional[Context] = None):
+    """crdt_lub_many_multi_sharded: items (kind, shard, out) as _lattice.lub_many_multi, each out
+    the global lub over the ranks (one fused local launch + one grouped RCCL all-reduce)."""
+    from ._lattice import segments
+    if not items:
+        return []
+    ctx = ctx or Context.default(items[0][1].device.index)
+    arr = segments(items, ctx)
+    ctx.call("crdt_lub_many_multi_sharded", arr, len(items))
+    return [o for _, _, o in items]
+
+
 class OrswotSharded(NamedTuple):
     clock: torch.Tensor        # (G, A)
     entries: torch.Tensor      # (G, M, A)

@@ -59,6 +59,7 @@ struct Tune {
   int map_chunk = 16;  // ... replicas per LDS chunk slot (8 or 16)
   int map_ring = 2;    // ... chunk slots in the ring (2-4)
   int map_spec = 1;    // ... speculative no-op scan
+  int map_nt = 0;      // ... non-temporal policy on the LDS-DMA step images
   int rows_blocks_per_cu = 0;  // row-pair / row-reduction kernels (causal.hip); 0 = per-kernel default
   int apply_hot_slots = 8;     // Orswot apply: deferred slots kept in LDS per state (the rest in HBM)
   int map_forget_vec2 = 1;     // Map forget: 16-byte pieces per lane where the shape allows it
@@ -178,6 +179,17 @@ int lattice_lub_many(crdt_ctx *ctx, Op op, const u64 *in, size_t G, size_t R, si
                      unsigned flags);
 int lattice_merge_batch(crdt_ctx *ctx, Op op, u64 *self, const u64 *other, size_t N, size_t W,
                         size_t self_stride, size_t other_stride);
+// One lattice lub of a multi-segment call (crdt_lub_many_multi): W = words per replica row.
+struct LubReq {
+  Op op;
+  const u64 *in;
+  size_t G, R, W, row_stride, group_stride;
+  u64 *out;
+  size_t out_stride;
+  unsigned flags;
+};
+int lattice_lub_many_multi(crdt_ctx *ctx, const LubReq *reqs, size_t n);
+int lub_reqs_from_segments(crdt_ctx *ctx, const crdt_lub_segment *segs, size_t nseg, std::vector<LubReq> &reqs);
 
 // Host-memory mode (host_stage.hip): the same entry points over host pointers, staged in chunks.
 int lattice_lub_many_host(crdt_ctx *ctx, Op op, const u64 *in, size_t G, size_t R, size_t W,

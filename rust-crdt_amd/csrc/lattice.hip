@@ -127,13 +127,9 @@ __device__ __forceinline__ bool arrive_last(unsigned *counter, unsigned expected
 }
 
 // One launch = the whole lub.  Block b -> (unit u = g*ncolblk + cb, slice s).
-template <Op OP, int V, int U, bool NT = true>
-__global__ __launch_bounds__(kBlock) void lub_stream_kernel(LubPlan p) {
-  using VT = typename VecOf<V>::T;
-  __shared__ VT red[kBlock];
-  __shared__ int s_flag;
+template <Op OP, int V, int U, bool NT, typename VT>
+__device__ __forceinline__ void lub_stream_body(const LubPlan &p, unsigned b, VT *red, int &s_flag) {
   const int l = threadIdx.x;
-  const unsigned b = blockIdx.x;
   const int s = b % p.S;
   const unsigned u = b / p.S;
   const int cb = u % p.ncolblk;
@@ -209,6 +205,37 @@ __global__ __launch_bounds__(kBlock) void lub_stream_kernel(LubPlan p) {
   if (writer) store_out<OP>(p, g, col, acc);
 }
 
+template <Op OP, int V, int U, bool NT = true>
+__global__ __launch_bounds__(kBlock) void lub_stream_kernel(LubPlan p) {
+  using VT = typename VecOf<V>::T;
+  __shared__ VT red[kBlock];
+  __shared__ int s_flag;
+  lub_stream_body<OP, V, U, NT, VT>(p, blockIdx.x, red, s_flag);
+}
+
+// Several lubs of one join op in ONE launch (crdt_lub_many_multi): segment i owns blocks
+// [start[i], start[i+1]) and runs exactly the single-lub body on its own plan, so the launch pays
+// one ramp and one tail instead of one per lub.
+constexpr int kLubMultiMax = 8;
+struct LubMulti {
+  LubPlan p[kLubMultiMax];
+  unsigned start[kLubMultiMax + 1];
+  int n;
+};
+
+template <Op OP, int V, int U>
+__global__ __launch_bounds__(kBlock) void lub_multi_kernel(LubMulti m) {
+  using VT = typename VecOf<V>::T;
+  __shared__ VT red[kBlock];
+  __shared__ int s_flag;
+  const unsigned b = blockIdx.x;
+  int i = 0;
+#pragma unroll
+  for (int j = 1; j < kLubMultiMax; ++j)
+    if (j < m.n && b >= m.start[j]) i = j;
+  lub_stream_body<OP, V, U, true, VT>(m.p[i], b - m.start[i], red, s_flag);
+}
+
 // self[i] := self[i] ⊔ other[i]: three streams (2 reads, 1 write), TR rows per block step.
 template <Op OP, int V>
 __global__ __launch_bounds__(kBlock) void merge_pairs_kernel(u64 *__restrict__ self,
@@ -268,16 +295,23 @@ __global__ __launch_bounds__(kBlock) void merge_rows_kernel(u64 *self, const u64
 
 static bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
-int lattice_lub_many(crdt_ctx *ctx, Op op, const u64 *in, size_t G, size_t R, size_t W,
-                     size_t row_stride, size_t group_stride, u64 *out, size_t out_stride,
-                     unsigned flags) {
-  CRDT_CHECK_CTX(ctx);
+// Validation and launch geometry of one lub (no scratch yet).  launch = false: nothing to run
+// (an empty fold was already written, or G / W is 0).
+struct LubSetup {
+  LubPlan p;
+  int V = 1;
+  bool launch = false;
+  size_t blocks = 0, part_b = 0, cpart_b = 0, ncnt = 0;
+};
+
+static int lub_prepare(crdt_ctx *ctx, Op op, const u64 *in, size_t G, size_t R, size_t W, size_t row_stride,
+                       size_t group_stride, u64 *out, size_t out_stride, unsigned flags, LubSetup &su) {
+  su = LubSetup{};
   if (G == 0 || W == 0) return CRDT_OK;
   if (!out) return fail(ctx, CRDT_EINVAL, "lub_many: out is NULL");
   if (G > 1 && out_stride < W)
     return fail(ctx, CRDT_EINVAL, "lub_many: out_stride %zu < row width %zu", out_stride, W);
   if (W > (size_t)1 << 30) return fail(ctx, CRDT_EUNSUPPORTED, "lub_many: row width %zu too large", W);
-  CRDT_HIP(ctx, hipSetDevice(ctx->device));
   const bool accumulate = flags & CRDT_ACCUMULATE;
   if (R == 0) {  // fold of nothing = T::new() (all zero); with ACCUMULATE: unchanged
     if (!accumulate)
@@ -292,7 +326,7 @@ int lattice_lub_many(crdt_ctx *ctx, Op op, const u64 *in, size_t G, size_t R, si
                     (G == 1 || (group_stride % 2 == 0 && out_stride % 2 == 0)) && aligned16(in) &&
                     aligned16(out);
   const int V = vec2 ? 2 : 1;
-  LubPlan p{};
+  LubPlan &p = su.p;
   p.in = in;
   p.out = out;
   p.rstride = (long long)row_stride;
@@ -327,23 +361,44 @@ int lattice_lub_many(crdt_ctx *ctx, Op op, const u64 *in, size_t G, size_t R, si
   p.interleave = ctx->tune.lub_interleave;
   p.CL = 32;
   p.ncl = (p.S + p.CL - 1) / p.CL;
-
   if (p.S > 1) {
     const size_t vecb = (size_t)V * 8;
-    const size_t part_b = units * S * p.PW * vecb;
-    const size_t cpart_b = units * p.ncl * p.PW * vecb;
-    int rc = ensure_scratch(ctx, part_b + cpart_b);
-    if (rc) return rc;
-    rc = ensure_counters(ctx, units * p.ncl + units);
-    if (rc) return rc;
-    char *base = static_cast<char *>(ctx->scratch);
-    p.cnt1 = ctx->counters;
-    p.cnt2 = p.cnt1 + units * p.ncl;
-    p.part = reinterpret_cast<u64 *>(base);
-    p.cpart = reinterpret_cast<u64 *>(base + part_b);
+    su.part_b = units * S * p.PW * vecb;
+    su.cpart_b = units * p.ncl * p.PW * vecb;
+    su.ncnt = units * p.ncl + units;
   }
+  su.V = V;
+  su.blocks = units * S;
+  su.launch = true;
+  return CRDT_OK;
+}
 
-  const dim3 grid((unsigned)(units * S));
+// Scratch of a prepared lub at `base` (part, then cpart) and counters at `cnt`.
+static void lub_assign(LubSetup &su, char *base, unsigned *cnt) {
+  if (su.p.S <= 1) return;
+  const size_t units = su.blocks / su.p.S;
+  su.p.cnt1 = cnt;
+  su.p.cnt2 = cnt + units * su.p.ncl;
+  su.p.part = reinterpret_cast<u64 *>(base);
+  su.p.cpart = reinterpret_cast<u64 *>(base + su.part_b);
+}
+
+int lattice_lub_many(crdt_ctx *ctx, Op op, const u64 *in, size_t G, size_t R, size_t W,
+                     size_t row_stride, size_t group_stride, u64 *out, size_t out_stride,
+                     unsigned flags) {
+  CRDT_CHECK_CTX(ctx);
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  LubSetup su;
+  if (int rc = lub_prepare(ctx, op, in, G, R, W, row_stride, group_stride, out, out_stride, flags, su)) return rc;
+  if (!su.launch) return CRDT_OK;
+  if (su.p.S > 1) {
+    if (int rc = ensure_scratch(ctx, su.part_b + su.cpart_b)) return rc;
+    if (int rc = ensure_counters(ctx, su.ncnt)) return rc;
+    lub_assign(su, static_cast<char *>(ctx->scratch), ctx->counters);
+  }
+  const LubPlan &p = su.p;
+  const int V = su.V;
+  const dim3 grid((unsigned)su.blocks);
   timing_begin(ctx, "lub_stream");
   const int U = ctx->tune.lub_unroll;
 #define CRDT_LAUNCH_LUB(OPV, VV, UV) \
@@ -363,6 +418,73 @@ int lattice_lub_many(crdt_ctx *ctx, Op op, const u64 *in, size_t G, size_t R, si
 #undef CRDT_LAUNCH_LUB
   timing_end(ctx);
   CRDT_HIP(ctx, hipGetLastError());
+  return CRDT_OK;
+}
+
+// Several lattice lubs, one launch per (join op, vector width) class of up to kLubMultiMax
+// segments; results identical to one lattice_lub_many per segment (each segment's blocks run the
+// single-lub body on its own plan and scratch).
+int lattice_lub_many_multi(crdt_ctx *ctx, const LubReq *reqs, size_t n) {
+  CRDT_CHECK_CTX(ctx);
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  std::vector<LubSetup> su(n);
+  for (size_t i = 0; i < n; ++i) {
+    const LubReq &q = reqs[i];
+    if (int rc = lub_prepare(ctx, q.op, q.in, q.G, q.R, q.W, q.row_stride, q.group_stride, q.out, q.out_stride,
+                             q.flags, su[i]))
+      return rc;
+  }
+  // one scratch / counter region for every segment (a later launch of this call never reuses an
+  // earlier one's region, so launches need no ordering beyond the stream's)
+  size_t sb = 0, nc = 0;
+  for (auto &x : su)
+    if (x.launch) {
+      sb += (x.part_b + x.cpart_b + 255) / 256 * 256;
+      nc += x.ncnt;
+    }
+  if (sb) {
+    if (int rc = ensure_scratch(ctx, sb)) return rc;
+    if (int rc = ensure_counters(ctx, nc)) return rc;
+  }
+  {
+    char *base = static_cast<char *>(ctx->scratch);
+    unsigned *cnt = ctx->counters;
+    for (auto &x : su)
+      if (x.launch && x.p.S > 1) {
+        lub_assign(x, base, cnt);
+        base += (x.part_b + x.cpart_b + 255) / 256 * 256;
+        cnt += x.ncnt;
+      }
+  }
+  std::vector<bool> done(n, false);
+  for (size_t i = 0; i < n; ++i) {
+    if (!su[i].launch || done[i]) continue;
+    LubMulti m{};
+    m.n = 0;
+    size_t blocks = 0;
+    const Op op = reqs[i].op;
+    const int V = su[i].V;
+    for (size_t j = i; j < n && m.n < kLubMultiMax; ++j) {
+      if (!su[j].launch || done[j] || reqs[j].op != op || su[j].V != V) continue;
+      m.p[m.n] = su[j].p;
+      m.start[m.n] = (unsigned)blocks;
+      blocks += su[j].blocks;
+      ++m.n;
+      done[j] = true;
+    }
+    if (blocks > 0x7fffffffULL) return fail(ctx, CRDT_EUNSUPPORTED, "lub_many_multi: grid too large");
+    for (int k = m.n; k <= kLubMultiMax; ++k) m.start[k] = (unsigned)blocks;
+    timing_begin(ctx, "lub_stream");
+    if (op == Op::Max) {
+      if (V == 2) hipLaunchKernelGGL((lub_multi_kernel<Op::Max, 2, 8>), dim3((unsigned)blocks), dim3(kBlock), 0, ctx->stream, m);
+      else hipLaunchKernelGGL((lub_multi_kernel<Op::Max, 1, 8>), dim3((unsigned)blocks), dim3(kBlock), 0, ctx->stream, m);
+    } else {
+      if (V == 2) hipLaunchKernelGGL((lub_multi_kernel<Op::Or, 2, 8>), dim3((unsigned)blocks), dim3(kBlock), 0, ctx->stream, m);
+      else hipLaunchKernelGGL((lub_multi_kernel<Op::Or, 1, 8>), dim3((unsigned)blocks), dim3(kBlock), 0, ctx->stream, m);
+    }
+    timing_end(ctx);
+    CRDT_HIP(ctx, hipGetLastError());
+  }
   return CRDT_OK;
 }
 
@@ -440,6 +562,34 @@ static int merge_dispatch(crdt_ctx *ctx, Op op, u64 *self, const u64 *other, siz
   return crdt::lattice_merge_batch(ctx, op, self, other, N, W, self_stride, other_stride);
 }
 
+// crdt_lub_many_multi: the per-kind dims of each segment mapped to the lattice form
+// (PNCounter rows hold 2A words; GCounter is VClock).
+int crdt::lub_reqs_from_segments(crdt_ctx *ctx, const crdt_lub_segment *segs, size_t nseg,
+                                 std::vector<crdt::LubReq> &reqs) {
+  if (nseg && !segs) return crdt::fail(ctx, CRDT_EINVAL, "lub_many_multi: segs is NULL");
+  reqs.resize(nseg);
+  for (size_t i = 0; i < nseg; ++i) {
+    const crdt_lub_segment &sg = segs[i];
+    crdt::LubReq &q = reqs[i];
+    switch (sg.kind) {
+      case CRDT_KIND_VCLOCK:
+      case CRDT_KIND_GCOUNTER: q.op = Op::Max; q.W = sg.A; break;
+      case CRDT_KIND_PNCOUNTER: q.op = Op::Max; q.W = 2 * sg.A; break;
+      case CRDT_KIND_GSET: q.op = Op::Or; q.W = sg.A; break;
+      default: return crdt::fail(ctx, CRDT_EINVAL, "lub_many_multi: segment %zu has unknown kind %d", i, sg.kind);
+    }
+    q.in = (const u64 *)sg.in;
+    q.G = sg.G;
+    q.R = sg.R;
+    q.row_stride = sg.row_stride;
+    q.group_stride = sg.group_stride;
+    q.out = (u64 *)sg.out;
+    q.out_stride = sg.out_stride;
+    q.flags = sg.flags;
+  }
+  return CRDT_OK;
+}
+
 extern "C" {
 
 int crdt_vclock_lub_many(crdt_ctx *ctx, const uint64_t *in, size_t G, size_t R, size_t A,
@@ -483,6 +633,14 @@ int crdt_gset_merge_batch(crdt_ctx *ctx, uint64_t *self, const uint64_t *other, 
                           size_t words, size_t self_stride, size_t other_stride) {
   return merge_dispatch(ctx, Op::Or, (u64 *)self, (const u64 *)other, N, words,
                                    self_stride, other_stride);
+}
+
+int crdt_lub_many_multi(crdt_ctx *ctx, const crdt_lub_segment *segs, size_t nseg) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
+  CRDT_CHECK_CTX(ctx);
+  std::vector<crdt::LubReq> reqs;
+  if (int rc = crdt::lub_reqs_from_segments(ctx, segs, nseg, reqs)) return rc;
+  return crdt::lattice_lub_many_multi(ctx, reqs.data(), reqs.size());
 }
 
 }  // extern "C"

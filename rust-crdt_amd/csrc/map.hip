@@ -51,6 +51,7 @@ struct MapPlan {
   unsigned *o_nval;
   unsigned *o_flags;  // per group: bit0 > Vout values, bit1 bad def_row, bit2 state capacity
   int spec;           // speculative no-op scan on (tuning / diagnosis knob; results are identical)
+  int nt;             // LDS-DMA step images with the non-temporal policy (tuning knob)
   // LDS-DMA path: per (group, chunk of C replicas) the max of the chunk's replica clocks,
   // [G][nch][A] (map_chunk_max_kernel), staged with each chunk so a wholly skipped chunk merges
   // its clocks with one compare (the acc clock only ever takes maxima of replica clocks, map.rs:217)
@@ -251,11 +252,14 @@ __host__ __device__ __forceinline__ unsigned long long map_ws(unsigned long long
   return W + (36 - W % 32) % 32;
 }
 
+// AUX = the cache-policy bits of the load (0: default; 2: non-temporal, the streamed step images)
+template <int AUX = 0>
 __device__ __forceinline__ void glds16(const void *g, u64 *lds) {
-  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void *)lds, 16, 0, 0);
+  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void *)lds, 16, 0, AUX);
 }
+template <int AUX = 0>
 __device__ __forceinline__ void glds4(const void *g, u64 *lds) {
-  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void *)lds, 4, 0, 0);
+  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void *)lds, 4, 0, AUX);
 }
 
 // Per-lane source of the LDS-DMA pieces: piece j of a step image covers image words
@@ -298,7 +302,7 @@ __device__ __forceinline__ GldsLanes<NI> glds_lanes(const MapPlan &p, unsigned l
 // least one active lane (NI = ceil(W / 128) 1-KiB pieces per step image; the values of all C
 // steps in one 4-byte-per-lane piece; the chunk's clock max in one), so a fixed vmcnt count
 // retires a chunk.  Sources advance by their row stride (no per-step 64-bit multiply).
-template <int VI, int C, int NI>
+template <int VI, int C, int NI, int AUX = 0>
 __device__ __forceinline__ void map_chunk_glds(const MapPlan &p, const GldsLanes<NI> &L, unsigned long long g,
                                                unsigned long long k, unsigned long long i0, unsigned long long iend,
                                                u64 *img, unsigned long long WS, u64 *vals, u64 *cm, int lane) {
@@ -311,7 +315,7 @@ __device__ __forceinline__ void map_chunk_glds(const MapPlan &p, const GldsLanes
       for (int s = 0; s < C; ++s)
 #pragma unroll
         for (int j = 0; j < NI; ++j) {
-          glds16(src[j], img + s * WS + j * 128);
+          glds16<AUX>(src[j], img + s * WS + j * 128);
           src[j] += L.stride[j];
         }
     } else {
@@ -319,7 +323,7 @@ __device__ __forceinline__ void map_chunk_glds(const MapPlan &p, const GldsLanes
       for (int s = 0; s < C; ++s)
 #pragma unroll
         for (int j = 0; j < NI; ++j) {
-          if (L.on[j]) glds16(src[j], img + s * WS + j * 128);
+          if (L.on[j]) glds16<AUX>(src[j], img + s * WS + j * 128);
           src[j] += L.stride[j];
         }
     }
@@ -329,14 +333,14 @@ __device__ __forceinline__ void map_chunk_glds(const MapPlan &p, const GldsLanes
       const unsigned long long i = i0 + s < iend ? i0 + s : iend - 1;
 #pragma unroll
       for (int j = 0; j < NI; ++j)
-        if (L.on[j]) glds16(L.src0[j] + i * L.stride[j], img + s * WS + j * 128);
+        if (L.on[j]) glds16<AUX>(L.src0[j] + i * L.stride[j], img + s * WS + j * 128);
     }
   }
   const int sv = lane / (2 * VI), dw = lane % (2 * VI);
   if (sv < C) {
     const unsigned long long i = i0 + sv < iend ? i0 + sv : iend - 1;
     const unsigned *src = reinterpret_cast<const unsigned *>(p.vval + g * p.vv_gs + i * p.vv_rs + k * VI) + dw;
-    glds4(src, vals);
+    glds4<AUX>(src, vals);
   }
   // the chunk's clock max: one more piece (lanes 0 .. A/2-1, A even)
   if ((unsigned long long)(2 * lane) < p.A)
@@ -640,8 +644,12 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
     if (ni == 1) gl1 = glds_lanes<VI, 1>(p, g, k, lane);
     else gl2 = glds_lanes<VI, 2>(p, g, k, lane);
     for (unsigned long long c = 0; c + 1 < NB && c < nch; ++c) {
-      if (ni == 1) map_chunk_glds<VI, C, 1>(p, gl1, g, k, c * C, R, map_lds + c * C * WS, WS, vbase + c * C * VI, cml + c * A, lane);
-      else map_chunk_glds<VI, C, 2>(p, gl2, g, k, c * C, R, map_lds + c * C * WS, WS, vbase + c * C * VI, cml + c * A, lane);
+      if (ni == 1) {
+        if (p.nt) map_chunk_glds<VI, C, 1, 2>(p, gl1, g, k, c * C, R, map_lds + c * C * WS, WS, vbase + c * C * VI, cml + c * A, lane);
+        else map_chunk_glds<VI, C, 1>(p, gl1, g, k, c * C, R, map_lds + c * C * WS, WS, vbase + c * C * VI, cml + c * A, lane);
+      } else {
+        map_chunk_glds<VI, C, 2>(p, gl2, g, k, c * C, R, map_lds + c * C * WS, WS, vbase + c * C * VI, cml + c * A, lane);
+      }
     }
   } else {
     if (nch > 0) {
@@ -662,8 +670,12 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
       if (nx < nch) {
         const unsigned ns = (unsigned)(nx % NB);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot's last LDS reads are done
-        if (ni == 1) map_chunk_glds<VI, C, 1>(p, gl1, g, k, nx * C, R, map_lds + ns * C * WS, WS, vbase + ns * C * VI, cml + ns * A, lane);
-        else map_chunk_glds<VI, C, 2>(p, gl2, g, k, nx * C, R, map_lds + ns * C * WS, WS, vbase + ns * C * VI, cml + ns * A, lane);
+        if (ni == 1) {
+          if (p.nt) map_chunk_glds<VI, C, 1, 2>(p, gl1, g, k, nx * C, R, map_lds + ns * C * WS, WS, vbase + ns * C * VI, cml + ns * A, lane);
+          else map_chunk_glds<VI, C, 1>(p, gl1, g, k, nx * C, R, map_lds + ns * C * WS, WS, vbase + ns * C * VI, cml + ns * A, lane);
+        } else {
+          map_chunk_glds<VI, C, 2>(p, gl2, g, k, nx * C, R, map_lds + ns * C * WS, WS, vbase + ns * C * VI, cml + ns * A, lane);
+        }
       }
       MAP_TOCK(cy_issue);
       MAP_TICK();
@@ -1152,6 +1164,7 @@ extern "C" int crdt_map_lub_many(crdt_ctx *ctx, const crdt_map_batch *in, crdt_m
   p.o_nval = out->nval;
   p.o_flags = out->flags;
   p.spec = ctx->tune.map_spec;
+  p.nt = ctx->tune.map_nt;
   if (int rc = device_fill(ctx, out->flags, G * sizeof(unsigned), 0)) return rc;
   // LDS-DMA staging when every step image is whole 16-byte pieces (A even, 16-byte aligned
   // rows and strides) and the state fits 4 values; register staging otherwise

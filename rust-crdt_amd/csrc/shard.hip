@@ -383,6 +383,33 @@ int crdt_orswot_lub_many_sharded(crdt_ctx *ctx, const crdt_orswot_batch *in, crd
   return CRDT_OK;
 }
 
+int crdt_lub_many_multi_sharded(crdt_ctx *ctx, const crdt_lub_segment *segs, size_t nseg) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
+  CRDT_CHECK_CTX(ctx);
+  CRDT_TRY(need_comm(ctx));
+  std::vector<LubReq> reqs;
+  CRDT_TRY(lub_reqs_from_segments(ctx, segs, nseg, reqs));
+  std::vector<LubReq> maxr;
+  for (auto &q : reqs) {
+    if (q.G > 1 && q.out_stride != q.W)
+      return fail(ctx, CRDT_EINVAL, "lub_many_multi_sharded: out_stride must equal the row width");
+    if (q.flags) return fail(ctx, CRDT_EINVAL, "lub_many_multi_sharded: flags must be 0");
+    if (q.op == Op::Max) maxr.push_back(q);
+  }
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  CRDT_TRY(lattice_lub_many_multi(ctx, maxr.data(), maxr.size()));
+  auto comm = (ncclComm_t)ctx->comm;
+  timing_begin(ctx, "shard_exchange");
+  CRDT_NCCL(ctx, ncclGroupStart());
+  for (auto &q : maxr)
+    if (q.G && q.W) CRDT_NCCL(ctx, ncclAllReduce(q.out, q.out, q.G * q.W, ncclUint64, ncclMax, comm, ctx->stream));
+  CRDT_NCCL(ctx, ncclGroupEnd());
+  timing_end(ctx);
+  for (auto &q : reqs)
+    if (q.op == Op::Or) CRDT_TRY(lattice_sharded(ctx, q.op, q.in, q.G, q.R, q.W, q.row_stride, q.group_stride, q.out));
+  return CRDT_OK;
+}
+
 int crdt_lwwreg_lub_many_sharded(crdt_ctx *ctx, const uint64_t *marker, const uint64_t *val, size_t G, size_t R,
                                  size_t group_stride, uint64_t base, uint64_t *out_marker, uint64_t *out_val,
                                  uint64_t *first_conflict) {

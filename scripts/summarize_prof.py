@@ -10,7 +10,7 @@ tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 G = os.path.join(ROOT, "gpurun_out")
 P = os.path.join(ROOT, "profiles")
-KERNEL = "lub_stream_kernel"
+KERNELS = ("lub_stream_kernel", "lub_multi_kernel")  # per-lub launches / the fused step launch
 
 
 def find(pattern):
@@ -25,7 +25,7 @@ trace = find(f"prof_{tag}/**/*kernel_trace.csv")
 durs = []
 if trace:
     for r in csv.DictReader(open(trace)):
-        if KERNEL in r["Kernel_Name"]:
+        if any(k in r["Kernel_Name"] for k in KERNELS):
             durs.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
 
 
@@ -36,14 +36,14 @@ def pmc(pattern, counter):
         return vals
     for r in csv.DictReader(open(f)):
         name = r.get("Kernel_Name", "")
-        if KERNEL in name and r.get("Counter_Name") == counter:
+        if any(k in name for k in KERNELS) and r.get("Counter_Name") == counter:
             vals.append(float(r["Counter_Value"]))
     return vals
 
 
 fetch = pmc(f"pmc_fetch_{tag}/**/*counter_collection.csv", "FETCH_SIZE")
 write = pmc(f"pmc_write_{tag}/**/*counter_collection.csv", "WRITE_SIZE")
-summary = {"kernel": KERNEL, "launches_traced": len(durs)}
+summary = {"kernel": "/".join(KERNELS), "launches_traced": len(durs)}
 if durs:
     summary["avg_launch_us_rocprof"] = sum(durs) / len(durs)
 if fetch and write:
@@ -60,10 +60,12 @@ for line in open(os.path.join(G, f"prof_{tag}.log")) if os.path.exists(os.path.j
         bench = json.loads(line)
 if bench:
     summary["workload"] = bench["config"]["workload"]
+    summary["fused"] = bench["config"].get("launches_per_step", 2) == 1
     summary["algorithmic_bytes_per_launch"] = bench["roofline"]["algorithmic_bytes_per_launch"]
     summary["avg_launch_us_hip_events"] = bench["roofline"]["avg_launch_us"]
 json.dump(summary, open(os.path.join(P, f"{tag}_pmc_summary.json"), "w"), indent=1)
 if "hbm_bytes_per_launch" in summary and bench:
-    json.dump({"workload": summary["workload"], "hbm_bytes_per_launch": summary["hbm_bytes_per_launch"],
+    json.dump({"workload": summary["workload"], "fused": summary["fused"],
+               "hbm_bytes_per_launch": summary["hbm_bytes_per_launch"],
                "source": f"profiles/{tag}_pmc_summary.json"}, open(os.path.join(P, "pmc_traffic.json"), "w"), indent=1)
 print(json.dumps(summary, indent=1))
