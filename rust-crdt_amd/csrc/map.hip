@@ -52,6 +52,7 @@ struct MapPlan {
   unsigned *o_flags;  // per group: bit0 > Vout values, bit1 bad def_row, bit2 state capacity
   int spec;           // speculative no-op scan on (tuning / diagnosis knob; results are identical)
   int nt;             // LDS-DMA step images with the non-temporal policy (tuning knob)
+  int scan2;          // speculative scan with two actors per 16-byte LDS read (A even)
   // LDS-DMA path: per (group, chunk of C replicas) the max of the chunk's replica clocks,
   // [G][nch][A] (map_chunk_max_kernel), staged with each chunk so a wholly skipped chunk merges
   // its clocks with one compare (the acc clock only ever takes maxima of replica clocks, map.rs:217)
@@ -496,12 +497,96 @@ __device__ __forceinline__ u64 map_noop_steps(const u64 *buf, unsigned W, unsign
   return (both | only) & G1;
 }
 
+// The same scan with two adjacent actors per lane and read (A even): every operand is one 16-byte
+// LDS read (ds_read_b128) covering actors a, a+1, and the two actors' tests are combined per lane
+// before the ballot (AND for the all-actor tests, OR for "replica has the key"), so the scan
+// issues half the LDS reads and half the ballots of map_noop_steps for the same verdict.
+__device__ __forceinline__ u64x2 lds2(const u64 *p) { return *reinterpret_cast<const u64x2 *>(p); }
+
+template <int VI, int NQ, int LPS, int IT, bool PRESENT>
+__device__ __forceinline__ u64 map_noop_steps2(const u64 *buf, unsigned W, unsigned A, const u64 *me,
+                                               const u64 *mc, const u64 *mmx, unsigned n, int lane) {
+  const unsigned st = (unsigned)lane / LPS;
+  const unsigned gq = (unsigned)lane % LPS;
+  const u64 *stp = buf + (st < n ? st : n - 1) * W;
+  u64 mP2 = 0, mB = ~0ull, mO = ~0ull;
+  u64 mLe2[VI][NQ > 0 ? NQ : 1], mVan[VI];
+#pragma unroll
+  for (int t = 0; t < VI; ++t) {
+    mVan[t] = ~0ull;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) mLe2[t][q] = ~0ull;
+  }
+  constexpr int IT2 = (IT + 1) / 2;
+#pragma unroll
+  for (unsigned m = 0; m < IT2; ++m) {
+    const unsigned a0 = 2 * (gq + LPS * m);
+    const unsigned a = a0 < A ? a0 : A - 2;  // a duplicate pair is neutral (masks only AND / OR)
+    const u64x2 e2 = lds2(stp + a);
+    const u64x2 mx = lds2(mmx + a);
+    if constexpr (!PRESENT) {
+      mP2 |= __ballot((e2.x != 0) | (e2.y != 0));
+      mB &= __ballot((e2.x <= mx.x) & (e2.y <= mx.y));
+    } else {
+      const u64x2 co = lds2(stp + (1 + VI) * A + a);
+      const u64x2 ea = lds2(me + a);
+      u64x2 c2[VI], sq[NQ > 0 ? NQ : 1];
+#pragma unroll
+      for (int t = 0; t < VI; ++t) c2[t] = lds2(stp + (1 + t) * A + a);
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) sq[q] = lds2(mc + q * A + a);
+      const bool gx = ea.x - 1 >= co.x, gy = ea.y - 1 >= co.y;  // e == 0 | e > Co
+      const u64 eGtCo = __ballot(gx & gy);
+      const u64 dx = e2.x > ea.x ? e2.x : 0, dy = e2.y > ea.y ? e2.y : 0;  // deleted
+      mP2 |= __ballot((e2.x != 0) | (e2.y != 0));
+      mB &= __ballot((e2.x <= mx.x) & (e2.y <= mx.y) & (gx | (ea.x == e2.x)) & (gy | (ea.y == e2.y)));
+      mO &= eGtCo;
+#pragma unroll
+      for (int t = 0; t < VI; ++t) mVan[t] &= __ballot((c2[t].x <= dx) & (c2[t].y <= dy));
+      if constexpr (NQ > 0) {
+        const u64 rx = co.x > ea.x ? co.x : 0, ry = co.y > ea.y ? co.y : 0;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          const u64 sx = sq[q].x - 1, sy = sq[q].y - 1;  // x - 1 >= y <=> x == 0 | x > y
+          mO &= __ballot((sx >= rx) & (sy >= ry));
+          mB &= __ballot((sx >= dx) & (sy >= dy));
+#pragma unroll
+          for (int t = 0; t < VI; ++t) mLe2[t][q] &= __ballot((c2[t].x <= sq[q].x) & (c2[t].y <= sq[q].y));
+        }
+      }
+    }
+  }
+  const u64 G1 = grp_mask<LPS>();
+  const u64 P2 = orN<LPS>(mP2);
+  if constexpr (!PRESENT) return (~P2 | andN<LPS>(mB)) & G1;
+  u64 both = P2 & andN<LPS>(mB);
+  const u64 only = ~P2 & andN<LPS>(mO);
+#pragma unroll
+  for (int t = 0; t < VI; ++t) {
+    u64 cov = andN<LPS>(mVan[t]);
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) cov |= andN<LPS>(mLe2[t][q]);
+    both &= cov;
+  }
+  return (both | only) & G1;
+}
+
 // Dispatch on (present, number of own values); more than 3 own values: no scan (returns 0 = no
 // step provably a no-op).
-template <int VI, int LPS, int IT>
+template <int VI, int LPS, int IT, bool PAIR = false>
 __device__ __forceinline__ u64 map_noop_nv(const u64 *buf, unsigned W, unsigned A, const u64 *mirror,
                                            unsigned VO, bool present, int nv, unsigned n, int lane) {
   const u64 *me = mirror, *mc = mirror + A, *mmx = mirror + (1 + VO) * A;
+  if constexpr (PAIR) {
+    if (!present) return map_noop_steps2<VI, 0, LPS, IT, false>(buf, W, A, me, mc, mmx, n, lane);
+    switch (nv) {
+      case 0: return map_noop_steps2<VI, 0, LPS, IT, true>(buf, W, A, me, mc, mmx, n, lane);
+      case 1: return map_noop_steps2<VI, 1, LPS, IT, true>(buf, W, A, me, mc, mmx, n, lane);
+      case 2: return map_noop_steps2<VI, 2, LPS, IT, true>(buf, W, A, me, mc, mmx, n, lane);
+      case 3: return map_noop_steps2<VI, 3, LPS, IT, true>(buf, W, A, me, mc, mmx, n, lane);
+      default: return 0;
+    }
+  }
   if (!present) return map_noop_steps<VI, 0, LPS, IT, false>(buf, W, A, me, mc, mmx, n, lane);
   switch (nv) {
     case 0: return map_noop_steps<VI, 0, LPS, IT, true>(buf, W, A, me, mc, mmx, n, lane);
@@ -708,8 +793,10 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
         if (uni(lim > s)) {
           MAP_TICK();
           const int nv = __builtin_popcount(__builtin_amdgcn_readfirstlane(mv.vm));
-          const u64 noop = map_noop_nv<VI, LPS, ITM>(buf, (unsigned)WS, (unsigned)A, mirror, VO, present, nv,
-                                                      (unsigned)n, lane);
+          const u64 noop = p.scan2 ? map_noop_nv<VI, LPS, ITM, true>(buf, (unsigned)WS, (unsigned)A, mirror, VO,
+                                                                      present, nv, (unsigned)n, lane)
+                                   : map_noop_nv<VI, LPS, ITM>(buf, (unsigned)WS, (unsigned)A, mirror, VO, present, nv,
+                                                               (unsigned)n, lane);
           const u64 from = (s >= NS) ? 0 : (~0ull << (LPS * s));
           const u64 upto = (lim >= NS) ? ~0ull : ((1ull << (LPS * lim)) - 1);
           const u64 stop = ~noop & grp_mask<LPS>() & from & upto;
@@ -1165,6 +1252,7 @@ extern "C" int crdt_map_lub_many(crdt_ctx *ctx, const crdt_map_batch *in, crdt_m
   p.o_flags = out->flags;
   p.spec = ctx->tune.map_spec;
   p.nt = ctx->tune.map_nt;
+  p.scan2 = ctx->tune.map_scan2 && A % 2 == 0;
   if (int rc = device_fill(ctx, out->flags, G * sizeof(unsigned), 0)) return rc;
   // LDS-DMA staging when every step image is whole 16-byte pieces (A even, 16-byte aligned
   // rows and strides) and the state fits 4 values; register staging otherwise
