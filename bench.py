@@ -178,7 +178,20 @@ def main():
     if cabi:  # the C ABI's own communicator; torch.distributed only ships the 128-byte id
         uid = [cg.shard.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
-        cg.shard.comm_init(ctx, uid[0], world, rank)
+        up = 1
+        try:
+            cg.shard.comm_init(ctx, uid[0], world, rank)
+        except Exception as e:  # every rank learns it below and all take the torch exchange together
+            print(f"rank {rank}: crdt_ctx_comm_init failed ({e}); using the torch.distributed exchange",
+                  file=sys.stderr)
+            up = 0
+        flag = torch.tensor([up], dtype=torch.int64, device="cuda")
+        cdist.all_reduce_(flag, dist.ReduceOp.MIN)
+        if not int(flag.item()):
+            if up:
+                cg.shard.comm_destroy(ctx)
+            cabi = False
+            args.exchange = "torch (C-ABI communicator setup failed)"
     # Synthetic replicas, generated in HBM; rank k owns rows [k*R, (k+1)*R) of the global input.
     if args.workload == "c5":
         lubs = [("vclock", torch.empty((R, A), dtype=torch.int64, device="cuda"), SEED_V)]
@@ -284,9 +297,11 @@ def main():
                 "actors": A,
                 "types": (["VClock (A u64)"] if args.workload == "c5" else ["GCounter (A u64)", "PNCounter (2A u64)"]),
                 "replica_merges_per_step": merges_per_step,
-                "exchange": ((f"C-ABI crdt_*_lub_many_sharded: ncclAllReduce(ncclUint64, ncclMax) of each partial "
-                              f"lub ({sum(x.shape[1] for _, x, _ in lubs)} words per step)") if cabi else
-                             "torch.distributed all-reduce MAX (sign-biased u64)") if world > 1 else "none",
+                "exchange": (((f"C-ABI crdt_lub_many_multi_sharded: one grouped ncclAllReduce(ncclUint64, ncclMax) "
+                               if args.fused else "C-ABI crdt_*_lub_many_sharded: ncclAllReduce(ncclUint64, ncclMax) ")
+                              + f"of the partial lubs ({sum(x.shape[1] for _, x, _ in lubs)} words per step)") if cabi
+                             else f"torch.distributed all-reduce MAX (sign-biased u64); --exchange {args.exchange}")
+                if world > 1 else "none",
                 "parallelism": f"replica-shard x{world}",
                 "launches_per_step": launches_per_step,
             },
