@@ -584,6 +584,17 @@ int crdt_orswot_egress(crdt_ctx *ctx, const uint64_t *clock, const uint64_t *ent
                        const uint32_t *actors, const uint64_t *members, const uint64_t *def_off,
                        const uint64_t *def_clock, const uint64_t *def_members, const uint8_t *def_keep,
                        uint64_t *frame_off, uint8_t *bytes, size_t cap, size_t *total);
+/* Map<u32, MVReg<u64, u32>, u32> (BASELINE config 4's type; map.rs:31-47, mvreg.rs:32-35) frames
+ * <-> packed crdt_map_states: clock_stride A, ec_stride K*A, vclk_stride K*V*A, vval_stride K*V;
+ * key k = position of its u32 id in the sorted `keys` dictionary, MVReg values in Vec order in
+ * slots 0.., and per-state deferred slots of a crdt_map_deferred.  Ingest status bits as above
+ * (4 = a key had more than V values or a state more than Dcap removes: the excess was dropped).
+ * Egress writes present keys ascending, occupied value slots in slot order, count[s] removes. */
+int crdt_map_ingest(crdt_ctx *ctx, const uint8_t *bytes, const uint64_t *frame_off, const uint32_t *actors,
+                    const uint32_t *keys, const crdt_map_states *out, const crdt_map_deferred *out_def,
+                    uint32_t *status);
+int crdt_map_egress(crdt_ctx *ctx, const crdt_map_states *states, const crdt_map_deferred *def, const uint32_t *actors,
+                    const uint32_t *keys, uint64_t *frame_off, uint8_t *bytes, size_t cap, size_t *total);
 
 /* ---- synthetic inputs (bench / test data, generated in HBM) --------------------------------
  * Counter-based and reproducible on the CPU (oracle/oracle.py synth_* restates them; small

@@ -1459,7 +1459,10 @@ def restrict_deferred_keys(def_keys: np.ndarray, keys) -> np.ndarray:
 # derives: VClock { dots: BTreeMap<A, u64> } (vclock.rs:56-60), GCounter { inner } (gcounter.rs:25-28),
 # PNCounter { p, n } (pncounter.rs:28-32), GSet { value: BTreeSet } (gset.rs:7-10),
 # LWWReg { val, marker } (lwwreg.rs:13-19), Orswot { clock, entries: HashMap<M, VClock>,
-# deferred: HashMap<VClock, HashSet<M>> } (orswot.rs:20-25).  Actors u32, members / elements u64.
+# deferred: HashMap<VClock, HashSet<M>> } (orswot.rs:20-25), Map { clock, entries: BTreeMap<K,
+# Entry { clock, val }>, deferred: HashMap<VClock, BTreeSet<K>> } (map.rs:31-47) with
+# MVReg { vals: Vec<(VClock, V)> } (mvreg.rs:32-35).  Actors u32, members / elements u64, Map keys
+# u32, MVReg values u64 (BASELINE config 4's Map<u32, MVReg<u64>>).
 # Parity of the byte format itself is unpinned (the reference ships no serialized fixtures and
 # bincode is not among its dependencies); the semantic round trips are pinned by the KATs.
 # ---------------------------------------------------------------------------------------
@@ -1496,6 +1499,54 @@ def bc_orswot(clock, entries, deferred, order=None) -> bytes:
         mem = list(members)
         out += bc_vclock(rm) + _st.pack("<Q", len(mem)) + b"".join(_st.pack("<Q", int(x)) for x in mem)
     return out
+
+
+def bc_map(clock, entries, deferred, key_order=None) -> bytes:
+    """Map<u32, MVReg<u64, u32>, u32> (map.rs:31-47, mvreg.rs:32-35): clock {a: c}; entries
+    {k: (entry clock {a: c}, [(value clock {a: c}, val), ...] in Vec order)}, serialized in key
+    order (BTreeMap); deferred [(rm {a: c}, keys)] (HashMap<VClock, BTreeSet<K>>: keys ascending)."""
+    ks = sorted(entries) if key_order is None else key_order
+    out = bc_vclock(clock) + _st.pack("<Q", len(ks))
+    for k in ks:
+        ec, vals = entries[k]
+        out += _st.pack("<I", int(k)) + bc_vclock(ec) + _st.pack("<Q", len(vals))
+        for vc, v in vals:
+            out += bc_vclock(vc) + _st.pack("<Q", int(v))
+    out += _st.pack("<Q", len(deferred))
+    for rm, keys in deferred:
+        kk = sorted(int(x) for x in keys)
+        out += bc_vclock(rm) + _st.pack("<Q", len(kk)) + b"".join(_st.pack("<I", x) for x in kk)
+    return out
+
+
+def unbc_map(b: bytes, pos: int = 0):
+    """-> (clock, entries {k: (dots, [(dots, val)])}, deferred {tuple(sorted rm items): set(keys)}, pos)."""
+    clock, pos = unbc_vclock(b, pos)
+    (n,) = _st.unpack_from("<Q", b, pos)
+    pos += 8
+    entries = {}
+    for _ in range(n):
+        (k,) = _st.unpack_from("<I", b, pos)
+        ec, pos = unbc_vclock(b, pos + 4)
+        (m,) = _st.unpack_from("<Q", b, pos)
+        pos += 8
+        vals = []
+        for _ in range(m):
+            vc, pos = unbc_vclock(b, pos)
+            (v,) = _st.unpack_from("<Q", b, pos)
+            pos += 8
+            vals.append((vc, v))
+        entries[k] = (ec, vals)
+    (d,) = _st.unpack_from("<Q", b, pos)
+    pos += 8
+    deferred = {}
+    for _ in range(d):
+        rm, pos = unbc_vclock(b, pos)
+        (k,) = _st.unpack_from("<Q", b, pos)
+        keys = {_st.unpack_from("<I", b, pos + 8 + 4 * i)[0] for i in range(k)}
+        pos += 8 + 4 * k
+        deferred.setdefault(tuple(sorted(rm.items())), set()).update(keys)
+    return clock, entries, deferred, pos
 
 
 def unbc_vclock(b: bytes, pos: int = 0):

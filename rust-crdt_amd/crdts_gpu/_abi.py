@@ -47,7 +47,7 @@ EXPORTS = (
     "crdt_orswot_forget_batch", "crdt_map_forget_batch", "crdt_map_apply_batch",
     "crdt_orswot_merge_batch", "crdt_map_merge_batch",
     "crdt_ctx_set_mem_kind", "crdt_ctx_mem_kind", "crdt_host_alloc", "crdt_host_free",
-    "crdt_lub_many_multi", "crdt_lub_many_multi_sharded",
+    "crdt_lub_many_multi", "crdt_lub_many_multi_sharded", "crdt_map_ingest", "crdt_map_egress",
 )
 
 
@@ -155,6 +155,9 @@ _SIGS = {
     "crdt_host_free": ([P], ctypes.c_int),
     "crdt_lub_many_multi": ([P, ctypes.POINTER(LubSegment), S], ctypes.c_int),
     "crdt_lub_many_multi_sharded": ([P, ctypes.POINTER(LubSegment), S], ctypes.c_int),
+    "crdt_map_ingest": ([P, P, P, P, P, ctypes.POINTER(MapStates), ctypes.POINTER(MapDeferred), P], ctypes.c_int),
+    "crdt_map_egress": ([P, ctypes.POINTER(MapStates), ctypes.POINTER(MapDeferred), P, P, P, P, S,
+                         ctypes.POINTER(S)], ctypes.c_int),
     "crdt_synth_fill": ([P, P, S, S, S, S, U64, ctypes.c_int], ctypes.c_int),
     "crdt_synth_orswot": ([P, P, P, S, S, S, S, U64, U64], ctypes.c_int),
     "crdt_synth_orswot_rm": ([P, P, S, S, S, P, P, P], ctypes.c_int),

@@ -193,3 +193,34 @@ def orswot_egress(clock: torch.Tensor, entries: torch.Tensor, actors: torch.Tens
         dp = [dptr(def_off), dptr(def_clock), dptr(def_members), dptr(def_keep) if def_keep is not None else None]
     return _egress(ctx, "crdt_orswot_egress", N, clock.device, dptr(clock), dptr(entries), N, M, A, dptr(actors),
                    dptr(members), *dp)
+
+
+def map_ingest(data: torch.Tensor, frame_off: torch.Tensor, actors: torch.Tensor, keys: torch.Tensor, V: int,
+               Dcap: int, ctx: Optional[Context] = None):
+    """Map<u32, MVReg<u64>> frames -> (map.MapStates with V value slots per key and Dcap deferred
+    slots per state, status (N,) int32).  keys: sorted u32 key dictionary (int32 tensor)."""
+    from .map import MapStates, _map_states_structs
+    ctx = _ctx(data, ctx)
+    N = _frames(ctx, data, frame_off, "wire.map_ingest")
+    A = _dict(ctx, actors, torch.int32, "wire.map_ingest(actors)")
+    K = _dict(ctx, keys, torch.int32, "wire.map_ingest(keys)")
+    dev = data.device
+    z = lambda *shape: torch.zeros(shape, dtype=torch.int64, device=dev)  # noqa: E731
+    st = MapStates(z(N, A), z(N, K, A), z(N, K, V, A), z(N, K, V), z(N, max(Dcap, 0), A), z(N, max(Dcap, 0), (K + 63) // 64),
+                   torch.zeros(N, dtype=torch.int32, device=dev))
+    s, d = _map_states_structs(ctx, st, "wire.map_ingest")
+    status = _status(N, dev)
+    ctx.call("crdt_map_ingest", _ptr_or_dummy(data), dptr(frame_off), dptr(actors), dptr(keys), ctypes.byref(s),
+             ctypes.byref(d), dptr(status))
+    return st, status
+
+
+def map_egress(states, actors: torch.Tensor, keys: torch.Tensor, ctx: Optional[Context] = None):
+    """map.MapStates (packed per-state blocks, deferred slots) -> (frame_off (N+1,), bytes)."""
+    from .map import _map_states_structs
+    ctx = _ctx(states.clock, ctx)
+    _dict(ctx, actors, torch.int32, "wire.map_egress(actors)")
+    _dict(ctx, keys, torch.int32, "wire.map_egress(keys)")
+    s, d = _map_states_structs(ctx, states, "wire.map_egress")
+    return _egress(ctx, "crdt_map_egress", states.clock.shape[0], states.clock.device, ctypes.byref(s), ctypes.byref(d),
+                   dptr(actors), dptr(keys))

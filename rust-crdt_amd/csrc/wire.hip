@@ -15,6 +15,10 @@
 //   LWWReg<u64, u64> = u64 val, u64 marker                  (struct { val, marker })
 //   Orswot<u64, u32> = VClock clock; u64 n, n x (u64 member, VClock) (HashMap: any order);
 //                      u64 d, d x (VClock rm, u64 k, k x u64 member) (HashMap<VClock, HashSet>)
+//   Map<u32, MVReg<u64, u32>, u32> (map.rs:31-47, mvreg.rs:32-35)
+//                    = VClock clock; u64 n, n x (u32 key, VClock entry clock, u64 m,
+//                      m x (VClock value clock, u64 value)) (BTreeMap: keys ascending; MVReg vals in
+//                      Vec order); u64 d, d x (VClock rm, u64 k, k x u32 key) (BTreeSet: ascending)
 // Every field is 4 or 8 bytes, so with 4-byte-aligned frame offsets every field is 4-aligned and
 // is read / written as 32-bit words (a u64 as two).
 //
@@ -592,6 +596,239 @@ __global__ __launch_bounds__(kBlock) void orswot_egress_kernel(EgressPlan p, int
   }
 }
 
+// ---- Map<u32, MVReg<u64>> ------------------------------------------------------------------------
+struct MapWirePlan {
+  const uint8_t *bytes;
+  const u64 *frame_off;
+  unsigned long long N, A, K, Kw, V, Dcap;
+  const uint32_t *actors, *keys;  // sorted dictionaries
+  u64 *clock, *ec, *vclk, *vval;  // [N][A], [N][K][A], [N][K][V][A], [N][K][V] (zero-filled before ingest)
+  u64 *def_clock, *def_keys;      // [N][Dcap][A], [N][Dcap][Kw]
+  uint32_t *def_count;            // [N]
+  uint32_t *status;
+  int stage;                      // dictionaries staged in LDS
+  // egress
+  u64 *sizes;
+  const u64 *frame_out;
+  uint8_t *out;
+};
+
+// One wave per state: the entries in frame order (the record loop of each VClock across lanes),
+// value clocks into the key's slots in Vec order, the deferred removes into the state's slots.
+// status: kWireBad (malformed / trailing bytes), kWireMissing (an actor or key not in the
+// dictionaries: skipped), kWireCap (more values than V for a key, or removes than Dcap: dropped).
+__global__ __launch_bounds__(kBlock) void map_ingest_kernel(MapWirePlan p) {
+  extern __shared__ u64 lds[];
+  const int lane = threadIdx.x % kWave, wib = threadIdx.x / kWave;
+  const int wpb = blockDim.x / kWave;
+  const uint32_t *actors = p.actors, *keys = p.keys;
+  u64 *base = lds;
+  if (p.stage) {  // [actors u32 | keys u32], each padded to 8 bytes
+    uint32_t *la = reinterpret_cast<uint32_t *>(lds);
+    const unsigned long long aw = (p.A + 1) / 2, kw = (p.K + 1) / 2;
+    for (unsigned long long i = threadIdx.x; i < p.A; i += blockDim.x) la[i] = p.actors[i];
+    uint32_t *lk = reinterpret_cast<uint32_t *>(lds + aw);
+    for (unsigned long long i = threadIdx.x; i < p.K; i += blockDim.x) lk[i] = p.keys[i];
+    __syncthreads();
+    actors = la;
+    keys = lk;
+    base = lds + aw + kw;
+  }
+  u64 *row = base + (unsigned long long)wib * (p.A + p.Kw);
+  u64 *bits = row + p.A;
+  for (unsigned long long s = (unsigned long long)blockIdx.x * wpb + wib; s < p.N;
+       s += (unsigned long long)gridDim.x * wpb) {
+    unsigned st = 0;
+    unsigned long long nd = 0;
+    Frame f;
+    const u64 b = p.frame_off[s], e = p.frame_off[s + 1];
+    if ((b & 3) || (e & 3) || e < b) {
+      st = kWireBad;
+    } else {
+      f.w = reinterpret_cast<const uint32_t *>(p.bytes + b);
+      f.nw = (e - b) / 4;
+      unsigned long long k = parse_vclock(f, 0, actors, p.A, row, lane, st);
+      store_row<u64>(p.clock + s * p.A, row, p.A, lane);
+      wfence();
+      if (k == ~0ull || k + 2 > f.nw) {
+        st |= kWireBad;
+        k = ~0ull;
+      }
+      const u64 n = k == ~0ull ? 0 : rd64(f.w, k);
+      if (k != ~0ull) k += 2;
+      for (u64 en = 0; en < n && k != ~0ull; ++en) {
+        if (k + 1 > f.nw) {
+          st |= kWireBad;
+          k = ~0ull;
+          break;
+        }
+        const long long ki = find_u32(keys, p.K, f.w[k], en);
+        if (ki < 0) st |= kWireMissing;
+        k = parse_vclock(f, k + 1, actors, p.A, row, lane, st);
+        if (k == ~0ull || k + 2 > f.nw) {
+          st |= kWireBad;
+          k = ~0ull;
+          break;
+        }
+        if (ki >= 0) store_row<u64>(p.ec + (s * p.K + (unsigned long long)ki) * p.A, row, p.A, lane);
+        wfence();
+        const u64 m = rd64(f.w, k);
+        k += 2;
+        for (u64 v = 0; v < m && k != ~0ull; ++v) {
+          k = parse_vclock(f, k, actors, p.A, row, lane, st);
+          if (k == ~0ull || k + 2 > f.nw) {
+            st |= kWireBad;
+            k = ~0ull;
+            break;
+          }
+          const u64 val = rd64(f.w, k);
+          k += 2;
+          if (ki >= 0) {
+            if (v < p.V) {
+              const unsigned long long slot = (s * p.K + (unsigned long long)ki) * p.V + v;
+              store_row<u64>(p.vclk + slot * p.A, row, p.A, lane);
+              if (lane == 0) p.vval[slot] = val;
+            } else {
+              st |= kWireCap;
+            }
+          }
+          wfence();
+        }
+      }
+      if (k != ~0ull && k + 2 <= f.nw) {
+        const u64 d = rd64(f.w, k);
+        k += 2;
+        for (u64 j = 0; j < d && k != ~0ull; ++j) {
+          k = parse_vclock(f, k, actors, p.A, row, lane, st);
+          for (unsigned long long w = lane; w < p.Kw; w += kWave) bits[w] = 0;
+          wfence();
+          if (k == ~0ull || k + 2 > f.nw) {
+            st |= kWireBad;
+            k = ~0ull;
+            break;
+          }
+          const u64 nk = rd64(f.w, k);
+          k += 2;
+          if (nk > f.nw - k) {
+            st |= kWireBad;
+            k = ~0ull;
+            break;
+          }
+          bool miss = false;
+          for (unsigned long long i = lane; i < nk; i += kWave) {
+            const long long kb = find_u32(keys, p.K, f.w[k + i], i);
+            if (kb < 0) miss = true;
+            else atomicOr(bits + kb / 64, 1ull << (kb % 64));
+          }
+          if (__ballot(miss)) st |= kWireMissing;
+          k += nk;
+          wfence();
+          if (nd < p.Dcap) {
+            store_row<u64>(p.def_clock + (s * p.Dcap + nd) * p.A, row, p.A, lane);
+            store_row<u64>(p.def_keys + (s * p.Dcap + nd) * p.Kw, bits, p.Kw, lane);
+            ++nd;
+          } else {
+            st |= kWireCap;
+          }
+          wfence();
+        }
+      } else {
+        st |= kWireBad;
+        k = ~0ull;
+      }
+      if (k != f.nw) st |= kWireBad;
+    }
+    if (lane == 0) {
+      p.status[s] = st;
+      p.def_count[s] = (uint32_t)nd;
+    }
+  }
+}
+
+// Egress, count (write = 0: frame sizes) or write pass: clock; present keys ascending with their
+// occupied value slots in slot (Vec) order; the state's deferred slots.
+__global__ __launch_bounds__(kBlock) void map_egress_kernel(MapWirePlan p, int write) {
+  const int lane = threadIdx.x % kWave;
+  const unsigned long long w0 = (blockIdx.x * (unsigned long long)kBlock + threadIdx.x) / kWave;
+  const unsigned long long nw = (unsigned long long)gridDim.x * (kBlock / kWave);
+  for (unsigned long long s = w0; s < p.N; s += nw) {
+    const u64 *c = p.clock + s * p.A;
+    uint32_t *w = write ? reinterpret_cast<uint32_t *>(p.out + p.frame_out[s]) : nullptr;
+    u64 sz = 8 + 12 * nnz_row(c, p.A, lane);
+    unsigned long long k = write ? write_vclock(w, 0, c, p.A, p.actors, lane) : 0;
+    u64 ne = 0;
+    for (unsigned long long key = 0; key < p.K; ++key) ne += nnz_row(p.ec + (s * p.K + key) * p.A, p.A, lane) != 0;
+    sz += 8;
+    if (write) {
+      if (lane == 0) wr64(w, k, ne);
+      k += 2;
+    }
+    for (unsigned long long key = 0; key < p.K; ++key) {
+      const u64 *er = p.ec + (s * p.K + key) * p.A;
+      const u64 n = nnz_row(er, p.A, lane);
+      if (n == 0) continue;
+      const unsigned long long slot0 = (s * p.K + key) * p.V;
+      u64 m = 0, vsz = 0;
+      for (unsigned long long v = 0; v < p.V; ++v) {
+        const u64 nv = nnz_row(p.vclk + (slot0 + v) * p.A, p.A, lane);
+        if (nv) {
+          ++m;
+          vsz += 8 + 12 * nv + 8;
+        }
+      }
+      sz += 4 + 8 + 12 * n + 8 + vsz;
+      if (!write) continue;
+      if (lane == 0) w[k] = p.keys[key];
+      k = write_vclock(w, k + 1, er, p.A, p.actors, lane);
+      if (lane == 0) wr64(w, k, m);
+      k += 2;
+      for (unsigned long long v = 0; v < p.V; ++v) {
+        const u64 *vr = p.vclk + (slot0 + v) * p.A;
+        if (nnz_row(vr, p.A, lane) == 0) continue;
+        k = write_vclock(w, k, vr, p.A, p.actors, lane);
+        if (lane == 0) wr64(w, k, p.vval[slot0 + v]);
+        k += 2;
+      }
+    }
+    const unsigned long long nd = p.def_count ? p.def_count[s] : 0;
+    sz += 8;
+    if (write) {
+      if (lane == 0) wr64(w, k, nd);
+      k += 2;
+    }
+    for (unsigned long long d = 0; d < nd && d < p.Dcap; ++d) {
+      const u64 *rm = p.def_clock + (s * p.Dcap + d) * p.A, *kb = p.def_keys + (s * p.Dcap + d) * p.Kw;
+      const u64 nk = popc_row(kb, p.Kw, lane);
+      sz += 8 + 12 * nnz_row(rm, p.A, lane) + 8 + 4 * nk;
+      if (!write) continue;
+      k = write_vclock(w, k, rm, p.A, p.actors, lane);
+      if (lane == 0) wr64(w, k, nk);
+      // keys ascending = bit order: lanes take bitmap words, a wave prefix sum places them
+      unsigned long long basei = 0;
+      for (unsigned long long x0 = 0; x0 < p.Kw; x0 += kWave) {
+        const unsigned long long x = x0 + lane;
+        u64 word = x < p.Kw ? kb[x] : 0;
+        const unsigned cnt = __popcll(word);
+        unsigned long long pre = cnt;
+        for (int off = 1; off < kWave; off <<= 1) {
+          const unsigned long long t = __shfl_up(pre, off, kWave);
+          if (lane >= off) pre += t;
+        }
+        unsigned long long i = basei + pre - cnt;
+        while (word) {
+          const int b = __builtin_ctzll(word);
+          word &= word - 1;
+          w[k + 2 + i] = p.keys[x * 64 + b];
+          ++i;
+        }
+        basei += __shfl(pre, kWave - 1, kWave);
+      }
+      k += 2 + nk;
+    }
+    if (!write && lane == 0) p.sizes[s] = sz;
+  }
+}
+
 static unsigned wave_grid(crdt_ctx *ctx, unsigned long long waves, int wpb, int per_cu) {
   const unsigned long long want = (waves + wpb - 1) / wpb;
   const unsigned long long cap = (unsigned long long)ctx->cu_count * per_cu;
@@ -777,6 +1014,99 @@ int crdt_orswot_ingest(crdt_ctx *ctx, const uint8_t *bytes, const uint64_t *fram
   timing_end(ctx);
   CRDT_HIP(ctx, hipGetLastError());
   if (n_def) *n_def = D;
+  return CRDT_OK;
+}
+
+// Map<u32, MVReg<u64>>: states packed (clock_stride A, ec_stride K*A, vclk_stride K*V*A,
+// vval_stride K*V), deferred as per-state slots (crdt_map_deferred).
+static int map_wire_plan(crdt_ctx *ctx, const crdt_map_states *st, const crdt_map_deferred *df, const uint32_t *actors,
+                         const uint32_t *keys, MapWirePlan &p, const char *what) {
+  if (!st || !df || !actors || !keys) return fail(ctx, CRDT_EINVAL, "%s: NULL states / deferred / dictionaries", what);
+  const size_t N = st->N, K = st->K, A = st->A, V = st->V;
+  if (A == 0 || K == 0 || V == 0) return fail(ctx, CRDT_EINVAL, "%s: need A, K, V >= 1", what);
+  if (N && (!st->clock || !st->ec || !st->vclk || !st->vval || !df->count || (df->Dcap && (!df->clock || !df->keys))))
+    return fail(ctx, CRDT_EINVAL, "%s: NULL state buffer", what);
+  if ((N > 1 && st->clock_stride != A) || (N > 1 && st->ec_stride != K * A) || (N > 1 && st->vclk_stride != K * V * A) ||
+      (N > 1 && st->vval_stride != K * V))
+    return fail(ctx, CRDT_EUNSUPPORTED, "%s: states must be packed (strides A, K*A, K*V*A, K*V)", what);
+  const size_t Kw = (K + 63) / 64;
+  if (A + Kw > (size_t)kWireRowLds) return fail(ctx, CRDT_EUNSUPPORTED, "%s: A + K/64 too large", what);
+  p = MapWirePlan{};
+  p.N = N;
+  p.A = A;
+  p.K = K;
+  p.Kw = Kw;
+  p.V = V;
+  p.Dcap = df->Dcap;
+  p.actors = actors;
+  p.keys = keys;
+  p.clock = (u64 *)st->clock;
+  p.ec = (u64 *)st->ec;
+  p.vclk = (u64 *)st->vclk;
+  p.vval = (u64 *)st->vval;
+  p.def_clock = (u64 *)df->clock;
+  p.def_keys = (u64 *)df->keys;
+  p.def_count = df->count;
+  return CRDT_OK;
+}
+
+int crdt_map_ingest(crdt_ctx *ctx, const uint8_t *bytes, const uint64_t *frame_off, const uint32_t *actors,
+                    const uint32_t *keys, const crdt_map_states *out, const crdt_map_deferred *out_def,
+                    uint32_t *status) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
+  CRDT_CHECK_CTX(ctx);
+  MapWirePlan p;
+  if (int rc = map_wire_plan(ctx, out, out_def, actors, keys, p, "map_ingest")) return rc;
+  const size_t N = p.N;
+  if (N == 0) return CRDT_OK;
+  if (int rc = check_frames(ctx, bytes, frame_off, N, status)) return rc;
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  // absent keys / values are zero rows
+  if (int rc = device_fill(ctx, p.ec, N * p.K * p.A * 8, 0)) return rc;
+  if (int rc = device_fill(ctx, p.vclk, N * p.K * p.V * p.A * 8, 0)) return rc;
+  if (int rc = device_fill(ctx, p.vval, N * p.K * p.V * 8, 0)) return rc;
+  p.bytes = bytes;
+  p.frame_off = (const u64 *)frame_off;
+  p.status = status;
+  int wpb = 4;
+  while (wpb > 1 && (size_t)wpb * (p.A + p.Kw) * 8 > 64 * 1024) --wpb;
+  const size_t dw = (p.A + 1) / 2 + (p.K + 1) / 2;
+  p.stage = (dw + wpb * (p.A + p.Kw)) * 8 <= 64 * 1024;
+  const size_t lds = ((p.stage ? dw : 0) + wpb * (p.A + p.Kw)) * 8;
+  const unsigned grid = wave_grid(ctx, N, wpb, 32);
+  timing_begin(ctx, "wire_ingest");
+  hipLaunchKernelGGL(map_ingest_kernel, dim3(grid), dim3(wpb * kWave), lds, ctx->stream, p);
+  timing_end(ctx);
+  CRDT_HIP(ctx, hipGetLastError());
+  return CRDT_OK;
+}
+
+int crdt_map_egress(crdt_ctx *ctx, const crdt_map_states *states, const crdt_map_deferred *def, const uint32_t *actors,
+                    const uint32_t *keys, uint64_t *frame_off, uint8_t *bytes, size_t cap, size_t *total) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
+  CRDT_CHECK_CTX(ctx);
+  if (total) *total = 0;
+  MapWirePlan p;
+  if (int rc = map_wire_plan(ctx, states, def, actors, keys, p, "map_egress")) return rc;
+  const size_t N = p.N;
+  if (N == 0) return CRDT_OK;
+  if (!frame_off || !total) return fail(ctx, CRDT_EINVAL, "map_egress: need frame_off and total");
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  u64 *sizes = nullptr;
+  if (int rc = wire_scratch(ctx, N, &sizes)) return rc;
+  p.sizes = sizes;
+  const unsigned grid = wave_grid(ctx, N, 4, 32);
+  timing_begin(ctx, "wire_egress");
+  hipLaunchKernelGGL(map_egress_kernel, dim3(grid), dim3(kBlock), 0, ctx->stream, p, 0);
+  CRDT_HIP(ctx, hipGetLastError());
+  if (int rc = egress_layout(ctx, sizes, (u64 *)frame_off, N, total)) return rc;
+  if (bytes && cap >= *total) {
+    p.frame_out = (const u64 *)frame_off;
+    p.out = bytes;
+    hipLaunchKernelGGL(map_egress_kernel, dim3(grid), dim3(kBlock), 0, ctx->stream, p, 1);
+    CRDT_HIP(ctx, hipGetLastError());
+  }
+  timing_end(ctx);
   return CRDT_OK;
 }
 

@@ -28,7 +28,8 @@ ap.add_argument("--replicas", type=int, default=1 << 20)
 ap.add_argument("--actors", type=int, default=256)
 ap.add_argument("--orswot-replicas", type=int, default=4096)
 ap.add_argument("--steps", type=int, default=5)
-ap.add_argument("--skip", default="", help="comma list of workloads to skip: gcounter,pncounter,orswot")
+ap.add_argument("--map-replicas", type=int, default=4096)
+ap.add_argument("--skip", default="", help="comma list of workloads to skip: gcounter,pncounter,orswot,map")
 args = ap.parse_args()
 skip = set(args.skip.split(",")) if args.skip else set()
 
@@ -140,10 +141,47 @@ def orswot():
     return ok
 
 
+def mapw():
+    """Config-4-shaped Map<u32, MVReg<u64>> states (R x 1,024 keys x 32 actors, V = 2, deferred
+    slots) -> egress -> frames -> ingest; ingest / egress GB/s of frames."""
+    R, K, A, V = args.map_replicas, 1024, 32, 2
+    inp = synth.map_replicas(ctx, R, K, A, V, 0x5EED0004, kmax=256, p_def=0.2)
+    rows = inp.def_row.cpu().numpy().astype(np.int64)
+    cnt = np.bincount(rows, minlength=R).astype(np.int32)
+    Dcap = max(1, int(cnt.max()))
+    Kw = (K + 63) // 64
+    dcl = torch.zeros((R, Dcap, A), dtype=torch.int64, device=dev)
+    dks = torch.zeros((R, Dcap, Kw), dtype=torch.int64, device=dev)
+    slot = np.arange(rows.shape[0]) - np.searchsorted(rows, rows)
+    rt, st_ = torch.from_numpy(rows).to(dev), torch.from_numpy(slot).to(dev)
+    dcl[rt, st_] = inp.def_clock
+    dks[rt, st_] = inp.def_keys
+    states = cg.map.MapStates(inp.clock, inp.ec, inp.vclk, inp.vval, dcl, dks, torch.from_numpy(cnt).to(dev))
+    actors = torch.arange(1, A + 1, dtype=torch.int32, device=dev) * 5
+    keys = torch.arange(1, K + 1, dtype=torch.int32, device=dev) * 11
+    off, frames = wire.map_egress(states, actors, keys, ctx=ctx)
+    nbytes = frames.numel()
+    back, status = wire.map_ingest(frames, off, actors, keys, V, Dcap, ctx=ctx)
+    ok = int(status.abs().sum()) == 0 and all(bool(torch.equal(getattr(back, f), getattr(states, f)))
+                                               for f in states._fields)
+    ms_ing = ev_time(lambda: wire.map_ingest(frames, off, actors, keys, V, Dcap, ctx=ctx), args.steps)
+    ms_egr = ev_time(lambda: wire.map_egress(states, actors, keys, ctx=ctx), max(1, args.steps // 2))
+    dense = sum(t.numel() * 8 for t in (inp.clock, inp.ec, inp.vclk, inp.vval))
+    print(json.dumps({
+        "workload": f"map<u32,mvreg<u64>> {R}x{K}x{A} V={V} (+{int(cnt.sum())} deferred) from bincode frames",
+        "frames_bytes": nbytes, "dense_bytes": dense, "ingest_ms": ms_ing, "ingest_GBs_frames": nbytes / ms_ing / 1e6,
+        "ingest_GBs_frames_plus_dense": (nbytes + dense) / ms_ing / 1e6, "egress_ms": ms_egr,
+        "egress_GBs_frames": nbytes / ms_egr / 1e6, "parity": "ok" if ok else "MISMATCH"}), flush=True)
+    return ok
+
+
 good = True
 for k in ("gcounter", "pncounter"):
     if k not in skip:
         good = counters(k) and good
 if "orswot" not in skip:
     good = orswot() and good
+if "map" not in skip:
+    torch.cuda.empty_cache()
+    good = mapw() and good
 sys.exit(0 if good else 3)

@@ -306,3 +306,94 @@ CASES = [c for f in ("kat_vclock.json", "kat_counters.json", "kat_orswot.json")
 @pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
 def test_kat_merges_through_the_wire(gpu_ctx, case):
     K.run_case(case, merge_hook=wire_merge)
+
+
+# ---- Map<u32, MVReg<u64>> (BASELINE config 4's type) ---------------------------------------------
+def map_wire_form(m, aids, kids):
+    """oracle Map over dense actor / key indices -> bc_map arguments over the u32 ids."""
+    tr = lambda vc: {int(aids[a]): int(v) for a, v in vc.dots.items() if v}  # noqa: E731
+    entries = {int(kids[k]): (tr(e.clock), [(tr(c), int(v)) for c, v in e.val.vals]) for k, e in m.entries.items()}
+    deferred = [(tr(rm), [int(kids[k]) for k in keys]) for rm, keys in m.deferred.items()]
+    return tr(m.clock), entries, deferred
+
+
+def map_decoded(m, aids, kids):
+    c, e, d = map_wire_form(m, aids, kids)
+    return c, e, {tuple(sorted(rm.items())): set(ks) for rm, ks in d}
+
+
+def map_blob(maps, aids, kids):
+    return O.frames([O.bc_map(*map_wire_form(m, aids, kids)) for m in maps])
+
+
+def test_map_ingest_egress(gpu_ctx):
+    from test_gpu_merge_batch import arbitrary_maps, map_side
+    rng = np.random.default_rng(41)
+    N, K, A, V = 40, 9, 5, 3
+    maps = arbitrary_maps(rng, N, K, A, V, 4)
+    aids, ad = actor_dict(rng, A)
+    kids, kd = actor_dict(rng, K)  # u32 keys
+    blob, off = map_blob(maps, aids, kids)
+    Dcap = max(1, max(len(m.deferred) for m in maps))
+    st, status = wire.map_ingest(dev_bytes(blob), dev_off(off), ad, kd, V, Dcap, ctx=gpu_ctx)
+    assert (status.cpu().numpy() == 0).all()
+    exp = map_side(maps, K, A, V, Dcap)
+    for nm in exp._fields:
+        np.testing.assert_array_equal(getattr(st, nm).cpu().numpy(), getattr(exp, nm).cpu().numpy(), err_msg=nm)
+    assert int(st.def_count.sum()) > 0 and int((st.vclk != 0).any(dim=3).sum()) > 0
+    eoff, edata = wire.map_egress(st, ad, kd, ctx=gpu_ctx)
+    assert eoff.cpu().tolist() == off
+    assert bytes(edata.cpu().numpy().tobytes()) == blob  # canonical frames round-trip byte for byte
+
+
+def test_map_merge_batch_through_bytes(gpu_ctx):
+    """Serialized pairs -> ingest -> merge_batch -> egress -> decode == the oracle's Map::merge."""
+    from test_gpu_merge_batch import replay_maps
+    rng = np.random.default_rng(42)
+    N, K, n_origins = 24, 12, 5
+    maps = replay_maps(7, 2 * N, n_origins, K, 200)
+    lhs, rhs = maps[:N], maps[N:]
+    exp = []
+    for a, b in zip(lhs, rhs):
+        x = a.copy()
+        x.merge(b.copy())
+        exp.append(x)
+    aids, ad = actor_dict(rng, n_origins)
+    kids, kd = actor_dict(rng, K)
+    V = max(1, O.max_vals(exp), O.max_vals(lhs), O.max_vals(rhs))
+    Dcap = max(1, max(len(m.deferred) for m in list(lhs) + list(rhs) + exp))
+    b1, o1 = map_blob(lhs, aids, kids)
+    b2, o2 = map_blob(rhs, aids, kids)
+    s1, st1 = wire.map_ingest(dev_bytes(b1), dev_off(o1), ad, kd, V, Dcap, ctx=gpu_ctx)
+    s2, st2 = wire.map_ingest(dev_bytes(b2), dev_off(o2), ad, kd, V, Dcap, ctx=gpu_ctx)
+    assert (st1.cpu().numpy() == 0).all() and (st2.cpu().numpy() == 0).all()
+    status = cg.map.merge_batch(s1, s2, ctx=gpu_ctx).cpu().numpy()
+    assert (status == 0).all(), status
+    eoff, edata = wire.map_egress(s1, ad, kd, ctx=gpu_ctx)
+    for i, fr in enumerate(host_frames(edata, eoff)):
+        c, e, d, pos = O.unbc_map(fr)
+        assert pos == len(fr)
+        assert (c, e, d) == map_decoded(exp[i], aids, kids), i
+    assert sum(len(x.entries) for x in exp) > 0 and sum(len(x.deferred) for x in exp) > 0
+
+
+def test_map_malformed_missing_and_capacity(gpu_ctx):
+    rng = np.random.default_rng(43)
+    K, A = 4, 3
+    aids, ad = actor_dict(rng, A)
+    kids, kd = actor_dict(rng, K)
+    a = lambda i: int(aids[i])  # noqa: E731
+    good = O.bc_map({a(0): 3}, {int(kids[1]): ({a(0): 3}, [({a(0): 3}, 7)])}, [({a(1): 5}, [int(kids[2])])])
+    missing_key = O.bc_map({a(0): 1}, {int(kids[-1]) + 1 if int(kids[-1]) < 2**32 - 1 else 0: ({a(0): 1}, [])}, [])
+    three_vals = O.bc_map({a(0): 2, a(1): 2, a(2): 2},
+                          {int(kids[0]): ({a(0): 2, a(1): 2, a(2): 2}, [({a(0): 2}, 1), ({a(1): 2}, 2), ({a(2): 2}, 3)])},
+                          [])
+    blobs = [good, good[:-4], good + b"\0\0\0\0", missing_key, three_vals]
+    blob, off = O.frames(blobs)
+    st, status = wire.map_ingest(dev_bytes(blob), dev_off(off), ad, kd, 2, 1, ctx=gpu_ctx)
+    s = status.cpu().numpy().tolist()
+    assert s[0] == 0
+    assert s[1] & wire.BAD and s[2] & wire.BAD
+    assert s[3] == wire.MISSING
+    assert s[4] == wire.CAP  # a third value with V = 2 slots: dropped and reported
+    assert to_host(st.vval)[4, 0].tolist() == [1, 2]

@@ -36,3 +36,21 @@ def test_round_trips():
         de = [({9: 3}, [1, 2]), ({9: 3}, [4]), ({8: 1}, [])]
         c, e, d, pos = O.unbc_orswot(O.bc_orswot({1: 1}, ent, de, order=list(ent)[::-1]))
         assert c == {1: 1} and e == ent and d == {((9, 3),): {1, 2, 4}, ((8, 1),): set()}
+
+
+def test_map_bincode_round_trip_and_layout():
+    """Map<u32, MVReg<u64>> (map.rs:31-47, mvreg.rs:32-35): the restated bincode form decodes to
+    what was encoded, keys ascending (BTreeMap), values in Vec order, and its byte layout is the
+    derive's field order (clock, entries, deferred)."""
+    clock = {7: 3, 2: 9}
+    entries = {40: ({2: 9}, [({2: 9}, 11), ({7: 3}, 12)]), 5: ({7: 1}, [])}
+    deferred = [({2: 10}, [40, 5])]
+    b = O.bc_map(clock, entries, deferred)
+    c, e, d, pos = O.unbc_map(b)
+    assert pos == len(b) and len(b) % 4 == 0
+    assert c == clock and e == entries and d == {((2, 10),): {5, 40}}
+    import struct
+    # clock: 2 dots ascending by actor
+    assert struct.unpack_from("<QIQIQ", b, 0) == (2, 2, 9, 7, 3)
+    # entries: count, then key 5 first
+    assert struct.unpack_from("<QI", b, 32) == (2, 5)
