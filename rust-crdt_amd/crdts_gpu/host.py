@@ -158,3 +158,74 @@ def lwwreg_merge_batch(self_marker: np.ndarray, self_val: np.ndarray, other_mark
     conflict = np.zeros(N, np.uint8)
     ctx.call("crdt_lwwreg_merge_batch", *[_ptr(a) for a in arrs], N, _ptr(conflict))
     return conflict
+
+
+class OrswotHostLub(NamedTuple):
+    clock: np.ndarray        # (G, A)
+    entries: np.ndarray      # (G, M, A)
+    def_keep: np.ndarray     # (D,) uint8
+    def_members: np.ndarray  # (D, Mw)
+
+
+def orswot_lub_many(clock: np.ndarray, entries: np.ndarray, def_off=None, def_clock: Optional[np.ndarray] = None,
+                    def_members: Optional[np.ndarray] = None, ctx: Optional[HostContext] = None) -> OrswotHostLub:
+    """crdt_orswot_lub_many on host arrays: clock (G, R, A), entries (G, R, M, A) (or without G),
+    deferred removes pooled per group (def_off G+1, def_clock (D, A), def_members (D, Mw)).  The
+    library stages the whole batch (the deferred survival test needs every replica's clock)."""
+    ctx = ctx or HostContext()
+    c = clock[None] if clock.ndim == 2 else clock
+    e = entries[None] if entries.ndim == 3 else entries
+    c = np.ascontiguousarray(_u64(c, "clock"))
+    e = np.ascontiguousarray(_u64(e, "entries"))
+    G, R, A = c.shape
+    M = e.shape[2]
+    Mw = (M + 63) // 64
+    b = _abi.OrswotBatch()
+    b.G, b.R, b.M, b.A = G, R, M, A
+    b.clock, b.clock_rstride, b.clock_gstride = c.ctypes.data, A, R * A
+    b.entries, b.entry_mstride, b.entry_rstride, b.entry_gstride = e.ctypes.data, A, M * A, R * M * A
+    D = 0
+    keep_alive = []
+    if def_off is not None:
+        off = (ctypes.c_size_t * (G + 1))(*[int(x) for x in def_off])
+        keep_alive.append(off)
+        b.def_off = off
+        D = int(def_off[-1])
+        dcl = np.ascontiguousarray(_u64(def_clock, "def_clock"))
+        dmb = np.ascontiguousarray(_u64(def_members, "def_members"))
+        keep_alive += [dcl, dmb]
+        b.def_clock, b.def_members = dcl.ctypes.data, dmb.ctypes.data
+    out = OrswotHostLub(np.zeros((G, A), np.uint64), np.zeros((G, M, A), np.uint64), np.zeros(D, np.uint8),
+                        np.zeros((D, Mw), np.uint64))
+    o = _abi.OrswotOut()
+    o.clock, o.entries = out.clock.ctypes.data, out.entries.ctypes.data
+    o.def_keep = out.def_keep.ctypes.data if D else None
+    o.def_members = out.def_members.ctypes.data if D else None
+    ctx.call("crdt_orswot_lub_many", ctypes.byref(b), ctypes.byref(o))
+    if clock.ndim == 2:
+        return OrswotHostLub(out.clock[0], out.entries[0], out.def_keep, out.def_members)
+    return out
+
+
+def orswot_merge_batch(self_states, other_states, ctx: Optional[HostContext] = None) -> np.ndarray:
+    """crdt_orswot_merge_batch on host arrays, in place on self: each side a tuple (clock (N, A),
+    entries (N, M, A), def_clock (N, Dcap, A), def_members (N, Dcap, Mw), def_count (N,) uint32)
+    of C-contiguous arrays.  Returns status (N,) uint32."""
+    ctx = ctx or HostContext()
+    structs = []
+    for side in (self_states, other_states):
+        clock, entries, dcl, dmb, cnt = side
+        for a in (clock, entries, dcl, dmb, cnt):
+            if not a.flags.c_contiguous:
+                raise ValueError("orswot_merge_batch: C-contiguous arrays required")
+        N, A = clock.shape
+        M = entries.shape[1]
+        st = _abi.OrswotStates()
+        st.N, st.M, st.A, st.Dcap = N, M, A, dcl.shape[1]
+        st.clock, st.clock_stride = clock.ctypes.data, A
+        st.entries, st.entry_mstride, st.entry_sstride = entries.ctypes.data, A, M * A
+        st.def_clock, st.def_members, st.def_count = dcl.ctypes.data, dmb.ctypes.data, cnt.ctypes.data
+        structs.append(st)
+    status = np.zeros(self_states[0].shape[0], np.uint32)
+    ctx.call("crdt_orswot_merge_batch", ctypes.byref(structs[0]), ctypes.byref(structs[1]), _ptr(status))
+    return status

@@ -204,6 +204,9 @@ int lww_merge_batch_dev(crdt_ctx *ctx, u64 *sm, u64 *sv, const u64 *om, const u6
 int lww_lub_many_host(crdt_ctx *ctx, const u64 *marker, const u64 *val, size_t G, size_t R, size_t group_stride,
                       u64 *out_marker, u64 *out_val, u64 *first_conflict, unsigned flags);
 int lww_merge_batch_host(crdt_ctx *ctx, u64 *sm, u64 *sv, const u64 *om, const u64 *ov, size_t N, uint8_t *conflict);
+int orswot_lub_many_host(crdt_ctx *ctx, const crdt_orswot_batch *in, crdt_orswot_out *out);
+int orswot_merge_batch_host(crdt_ctx *ctx, const crdt_orswot_states *self, const crdt_orswot_states *other,
+                            uint32_t *status);
 void free_stage(crdt_ctx *ctx);
 
 // Wave-uniform row-group loop: every lane runs the same iterations (rows past N are masked),

@@ -318,6 +318,187 @@ int lww_merge_batch_host(crdt_ctx *ctx, u64 *sm, u64 *sv, const u64 *om, const u
   return finish(ctx, lww_merge_host_body(ctx, sm, sv, om, ov, N, conflict));
 }
 
+// ---- Orswot: whole-batch staging -----------------------------------------------------------------
+// The Orswot join needs every replica of a group before the deferred removes are settled (the
+// survival test and the forget ceiling read the final clock), so its host form stages the whole
+// batch into device buffers (packed), runs the device entry point, and copies the outputs back.
+struct DevScratch {  // device allocations of one host-mode call, freed on every return path
+  std::vector<void *> p;
+  ~DevScratch() {
+    for (void *x : p) (void)hipFree(x);
+  }
+  template <typename T>
+  int get(crdt_ctx *ctx, size_t n, T **out) {
+    *out = nullptr;
+    if (n == 0) return CRDT_OK;
+    void *x = nullptr;
+    if (hipMalloc(&x, n * sizeof(T)) != hipSuccess) return fail(ctx, CRDT_ENOMEM, "host staging: hipMalloc(%zu)", n * sizeof(T));
+    p.push_back(x);
+    *out = static_cast<T *>(x);
+    return CRDT_OK;
+  }
+};
+
+// Run the device-pointer form of an entry point on this ctx (host mode switched off for the call).
+struct DeviceModeScope {
+  crdt_ctx *c;
+  int saved;
+  explicit DeviceModeScope(crdt_ctx *x) : c(x), saved(x->mem_kind) { c->mem_kind = CRDT_MEM_DEVICE; }
+  ~DeviceModeScope() { c->mem_kind = saved; }
+};
+
+static int h2d_async(crdt_ctx *ctx, void *dst, const void *src, size_t bytes) {
+  if (!bytes) return CRDT_OK;
+  STAGE_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+  return CRDT_OK;
+}
+static int d2h_async(crdt_ctx *ctx, void *dst, const void *src, size_t bytes) {
+  if (!bytes || !dst) return CRDT_OK;
+  STAGE_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  return CRDT_OK;
+}
+
+static int orswot_lub_host_body(crdt_ctx *ctx, const crdt_orswot_batch *in, crdt_orswot_out *out, DevScratch &ds) {
+  const size_t G = in->G, R = in->R, M = in->M, A = in->A, Mw = (M + 63) / 64;
+  const size_t D = in->def_off ? in->def_off[G] : 0;
+  uint64_t *c = nullptr, *e = nullptr, *dc = nullptr, *dm = nullptr, *oc = nullptr, *oe = nullptr, *om = nullptr;
+  uint8_t *ok = nullptr;
+  if (int rc = ds.get(ctx, G * R * A, &c)) return rc;
+  if (int rc = ds.get(ctx, G * R * M * A, &e)) return rc;
+  if (int rc = ds.get(ctx, D * A, &dc)) return rc;
+  if (int rc = ds.get(ctx, D * Mw, &dm)) return rc;
+  if (int rc = ds.get(ctx, G * A, &oc)) return rc;
+  if (int rc = ds.get(ctx, G * M * A, &oe)) return rc;
+  if (out->def_keep && (int)ds.get(ctx, D, &ok)) return CRDT_ENOMEM;
+  if (out->def_members && (int)ds.get(ctx, D * Mw, &om)) return CRDT_ENOMEM;
+  const uint64_t *hc = in->clock, *he = in->entries;
+  for (size_t g = 0; g < G && R; ++g) {
+    STAGE_HIP(copy_rows(c + g * R * A, A * 8, hc + g * in->clock_gstride, in->clock_rstride * 8, A * 8, R,
+                        hipMemcpyHostToDevice, ctx->stream));
+    if (in->entry_mstride == A || M == 1) {
+      STAGE_HIP(copy_rows(e + g * R * M * A, M * A * 8, he + g * in->entry_gstride, in->entry_rstride * 8, M * A * 8, R,
+                          hipMemcpyHostToDevice, ctx->stream));
+    } else {
+      for (size_t r = 0; r < R; ++r)
+        STAGE_HIP(copy_rows(e + (g * R + r) * M * A, A * 8, he + g * in->entry_gstride + r * in->entry_rstride,
+                            in->entry_mstride * 8, A * 8, M, hipMemcpyHostToDevice, ctx->stream));
+    }
+  }
+  if (int rc = h2d_async(ctx, dc, in->def_clock, D * A * 8)) return rc;
+  if (int rc = h2d_async(ctx, dm, in->def_members, D * Mw * 8)) return rc;
+  crdt_orswot_batch b = *in;
+  b.clock = c;
+  b.clock_rstride = A;
+  b.clock_gstride = R * A;
+  b.entries = e;
+  b.entry_mstride = A;
+  b.entry_rstride = M * A;
+  b.entry_gstride = R * M * A;
+  b.def_clock = dc;
+  b.def_members = dm;
+  crdt_orswot_out o{oc, oe, ok, om};
+  {
+    DeviceModeScope dev(ctx);
+    if (int rc = crdt_orswot_lub_many(ctx, &b, &o)) return rc;
+  }
+  if (int rc = d2h_async(ctx, out->clock, oc, G * A * 8)) return rc;
+  if (int rc = d2h_async(ctx, out->entries, oe, G * M * A * 8)) return rc;
+  if (int rc = d2h_async(ctx, out->def_keep, ok, D)) return rc;
+  if (int rc = d2h_async(ctx, out->def_members, om, D * Mw * 8)) return rc;
+  return CRDT_OK;
+}
+
+int orswot_lub_many_host(crdt_ctx *ctx, const crdt_orswot_batch *in, crdt_orswot_out *out) {
+  if (!in || !out) return fail(ctx, CRDT_EINVAL, "orswot_lub_many: NULL batch/out");
+  if (in->G == 0 || in->M == 0 || in->A == 0) return CRDT_OK;
+  if (!out->clock || !out->entries) return fail(ctx, CRDT_EINVAL, "orswot_lub_many: NULL output");
+  if (in->R && (!in->clock || !in->entries)) return fail(ctx, CRDT_EINVAL, "orswot_lub_many: NULL input");
+  if (in->R > 1 && (in->clock_rstride < in->A || in->entry_rstride < in->M * in->entry_mstride))
+    return fail(ctx, CRDT_EINVAL, "orswot_lub_many: replica strides smaller than a replica");
+  if (in->M > 1 && in->entry_mstride < in->A) return fail(ctx, CRDT_EINVAL, "orswot_lub_many: entry_mstride < A");
+  for (auto [p, w] : {std::pair<const void *, const char *>{in->clock, "clock"}, {in->entries, "entries"},
+                      {in->def_clock, "def_clock"}, {in->def_members, "def_members"}, {out->clock, "out.clock"},
+                      {out->entries, "out.entries"}, {out->def_keep, "out.def_keep"}, {out->def_members, "out.def_members"}})
+    if (int rc = check_host(ctx, p, w)) return rc;
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  DevScratch ds;
+  return finish(ctx, orswot_lub_host_body(ctx, in, out, ds));
+}
+
+static int orswot_merge_host_body(crdt_ctx *ctx, const crdt_orswot_states *a, const crdt_orswot_states *b,
+                                  uint32_t *status, DevScratch &ds) {
+  const size_t N = a->N, M = a->M, A = a->A, Mw = (M + 63) / 64;
+  crdt_orswot_states d[2] = {*a, *b};
+  const crdt_orswot_states *h[2] = {a, b};
+  for (int i = 0; i < 2; ++i) {
+    const crdt_orswot_states &x = *h[i];
+    crdt_orswot_states &y = d[i];
+    if (int rc = ds.get(ctx, N * A, &y.clock)) return rc;
+    if (int rc = ds.get(ctx, N * M * A, &y.entries)) return rc;
+    if (int rc = ds.get(ctx, N * x.Dcap * A, &y.def_clock)) return rc;
+    if (int rc = ds.get(ctx, N * x.Dcap * Mw, &y.def_members)) return rc;
+    if (int rc = ds.get(ctx, N, &y.def_count)) return rc;
+    y.clock_stride = A;
+    y.entry_mstride = A;
+    y.entry_sstride = M * A;
+    STAGE_HIP(copy_rows(y.clock, A * 8, x.clock, x.clock_stride * 8, A * 8, N, hipMemcpyHostToDevice, ctx->stream));
+    if (x.entry_mstride == A || M == 1) {
+      STAGE_HIP(copy_rows(y.entries, M * A * 8, x.entries, x.entry_sstride * 8, M * A * 8, N, hipMemcpyHostToDevice,
+                          ctx->stream));
+    } else {
+      for (size_t s = 0; s < N; ++s)
+        STAGE_HIP(copy_rows(y.entries + s * M * A, A * 8, x.entries + s * x.entry_sstride, x.entry_mstride * 8, A * 8, M,
+                            hipMemcpyHostToDevice, ctx->stream));
+    }
+    if (int rc = h2d_async(ctx, y.def_clock, x.def_clock, N * x.Dcap * A * 8)) return rc;
+    if (int rc = h2d_async(ctx, y.def_members, x.def_members, N * x.Dcap * Mw * 8)) return rc;
+    if (x.def_count && (int)h2d_async(ctx, y.def_count, x.def_count, N * 4)) return CRDT_EHIP;
+    if (!x.def_count) y.def_count = nullptr;
+  }
+  uint32_t *dst = nullptr;
+  if (int rc = ds.get(ctx, N, &dst)) return rc;
+  {
+    DeviceModeScope dev(ctx);
+    if (int rc = crdt_orswot_merge_batch(ctx, &d[0], &d[1], dst)) return rc;
+  }
+  STAGE_HIP(copy_rows(a->clock, a->clock_stride * 8, d[0].clock, A * 8, A * 8, N, hipMemcpyDeviceToHost, ctx->stream));
+  if (a->entry_mstride == A || M == 1) {
+    STAGE_HIP(copy_rows(a->entries, a->entry_sstride * 8, d[0].entries, M * A * 8, M * A * 8, N, hipMemcpyDeviceToHost,
+                        ctx->stream));
+  } else {
+    for (size_t s = 0; s < N; ++s)
+      STAGE_HIP(copy_rows(a->entries + s * a->entry_sstride, a->entry_mstride * 8, d[0].entries + s * M * A, A * 8, A * 8,
+                          M, hipMemcpyDeviceToHost, ctx->stream));
+  }
+  if (int rc = d2h_async(ctx, a->def_clock, d[0].def_clock, N * a->Dcap * A * 8)) return rc;
+  if (int rc = d2h_async(ctx, a->def_members, d[0].def_members, N * a->Dcap * Mw * 8)) return rc;
+  if (int rc = d2h_async(ctx, a->def_count, d[0].def_count, N * 4)) return rc;
+  return d2h_async(ctx, status, dst, N * 4);
+}
+
+int orswot_merge_batch_host(crdt_ctx *ctx, const crdt_orswot_states *self, const crdt_orswot_states *other,
+                            uint32_t *status) {
+  if (!self || !other || !status) return fail(ctx, CRDT_EINVAL, "orswot_merge_batch: NULL argument");
+  const crdt_orswot_states &a = *self, &b = *other;
+  if (a.N != b.N || a.M != b.M || a.A != b.A)
+    return fail(ctx, CRDT_EINVAL, "orswot_merge_batch: self and other differ in N, M or A");
+  if (a.N == 0) return CRDT_OK;
+  if (!a.clock || !b.clock || !a.def_count || (a.M && (!a.entries || !b.entries)))
+    return fail(ctx, CRDT_EINVAL, "orswot_merge_batch: NULL buffer");
+  if (a.clock_stride < a.A || b.clock_stride < b.A || (a.M && (a.entry_mstride < a.A || b.entry_mstride < b.A ||
+                                                             a.entry_sstride < a.M * a.entry_mstride ||
+                                                             b.entry_sstride < b.M * b.entry_mstride)))
+    return fail(ctx, CRDT_EINVAL, "orswot_merge_batch: strides smaller than the rows they hold");
+  for (const crdt_orswot_states *x : {self, other})
+    for (auto [p, w] : {std::pair<const void *, const char *>{x->clock, "clock"}, {x->entries, "entries"},
+                        {x->def_clock, "def_clock"}, {x->def_members, "def_members"}, {x->def_count, "def_count"}})
+      if (int rc = check_host(ctx, p, w)) return rc;
+  if (int rc = check_host(ctx, status, "status")) return rc;
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  DevScratch ds;
+  return finish(ctx, orswot_merge_host_body(ctx, self, other, status, ds));
+}
+
 void free_stage(crdt_ctx *ctx) {
   if (ctx->hstream) (void)hipStreamSynchronize(ctx->hstream);
   for (auto &b : ctx->hbuf)

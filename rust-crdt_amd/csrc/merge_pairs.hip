@@ -874,7 +874,7 @@ using namespace crdt;
 
 extern "C" int crdt_orswot_merge_batch(crdt_ctx *ctx, const crdt_orswot_states *self, const crdt_orswot_states *other,
                                        uint32_t *status) {
-  CRDT_DEVICE_MEM_ONLY(ctx);
+  if (ctx && ctx->mem_kind == CRDT_MEM_HOST) return crdt::orswot_merge_batch_host(ctx, self, other, status);
   CRDT_CHECK_CTX(ctx);
   if (!self || !other || !status) return fail(ctx, CRDT_EINVAL, "orswot_merge_batch: NULL argument");
   const crdt_orswot_states &a = *self, &b = *other;

@@ -357,7 +357,7 @@ using namespace crdt;
 
 extern "C" int crdt_orswot_lub_many(crdt_ctx *ctx, const crdt_orswot_batch *in,
                                     crdt_orswot_out *out) {
-  CRDT_DEVICE_MEM_ONLY(ctx);
+  if (ctx && ctx->mem_kind == CRDT_MEM_HOST) return crdt::orswot_lub_many_host(ctx, in, out);
   CRDT_CHECK_CTX(ctx);
   if (!in || !out) return fail(ctx, CRDT_EINVAL, "orswot_lub_many: NULL batch/out");
   const size_t G = in->G, R = in->R, M = in->M, A = in->A;

@@ -15,7 +15,8 @@
 //! `VClock::apply_dot` never stores 0, `vclock.rs:155-159`), merged on the GPU, and rebuilt.
 //! The lattice types and `LWWReg` hand their host rows straight to the library through a second
 //! ctx in `CRDT_MEM_HOST` mode (it streams them through HBM in chunks, overlapping PCIe with the
-//! fold); `Orswot` stages its buffers with [`DeviceBuf`].  Callers that keep replica states
+//! fold; `Orswot` batches are staged whole).  [`DeviceBuf`] stays for callers that manage device
+//! memory themselves.  Callers that keep replica states
 //! resident in HBM use [`ffi`] directly on device buffers with [`GpuCtx::as_ptr`].
 //!
 //! Field access: `VClock::dots`, the `Orswot` fields and the `LWWReg` fields are already visible
@@ -609,21 +610,20 @@ impl<M: Member, A: Actor> BatchCvRDT for Orswot<M, A> {
         }
         let nd = dcl.len() / a;
         let def_off: [usize; 2] = [0, nd];
-        let (dc, de) = (DeviceBuf::from_host(&clock)?, DeviceBuf::from_host(&entries)?);
-        let (ddc, ddm) = (DeviceBuf::from_host(&dcl)?, DeviceBuf::from_host(&dmb)?);
-        let (oc, oe) = (DeviceBuf::<u64>::zeroed(a)?, DeviceBuf::<u64>::zeroed(m * a)?);
-        let (ok, om) = (DeviceBuf::<u8>::zeroed(nd)?, DeviceBuf::<u64>::zeroed(nd * mw)?);
+        // host rows straight to the CRDT_MEM_HOST ctx: the library stages the whole batch
+        let (mut c, mut e, mut keep, mut mem) = (vec![0u64; a], vec![0u64; m * a], vec![0u8; nd], vec![0u64; nd * mw]);
         let batch = ffi::crdt_orswot_batch {
             G: 1, R: r, M: m, A: a,
-            clock: dc.as_ptr(), clock_rstride: a, clock_gstride: r * a,
-            entries: de.as_ptr(), entry_mstride: a, entry_rstride: m * a, entry_gstride: r * m * a,
-            def_off: def_off.as_ptr(), def_clock: ddc.as_ptr(), def_members: ddm.as_ptr(),
+            clock: clock.as_ptr(), clock_rstride: a, clock_gstride: r * a,
+            entries: entries.as_ptr(), entry_mstride: a, entry_rstride: m * a, entry_gstride: r * m * a,
+            def_off: def_off.as_ptr(), def_clock: dcl.as_ptr(), def_members: dmb.as_ptr(),
         };
         let mut out = ffi::crdt_orswot_out {
-            clock: oc.as_mut_ptr(), entries: oe.as_mut_ptr(), def_keep: ok.as_mut_ptr(), def_members: om.as_mut_ptr(),
+            clock: c.as_mut_ptr(), entries: e.as_mut_ptr(),
+            def_keep: if nd > 0 { keep.as_mut_ptr() } else { ptr::null_mut() },
+            def_members: if nd > 0 { mem.as_mut_ptr() } else { ptr::null_mut() },
         };
-        ctx.check(unsafe { ffi::crdt_orswot_lub_many(ctx.raw, &batch, &mut out) })?;
-        let (c, e, keep, mem) = (oc.to_host()?, oe.to_host()?, ok.to_host()?, om.to_host()?);
+        ctx.check_host(unsafe { ffi::crdt_orswot_lub_many(ctx.host, &batch, &mut out) })?;
         let mut surv = Vec::new();
         for i in 0..nd {
             if keep[i] != 0 {
@@ -658,25 +658,22 @@ impl<M: Member, A: Actor> BatchCvRDT for Orswot<M, A> {
             }
             (c, e, dc, dm, cnt)
         };
-        let (sc, se, sdc, sdm, scnt) = side(&selves[..n], dcap_s);
-        let (oc, oe, odc, odm, ocnt) = side(&others[..n], dcap_o);
-        let bufs_s = (DeviceBuf::from_host(&sc)?, DeviceBuf::from_host(&se)?, DeviceBuf::from_host(&sdc)?,
-                      DeviceBuf::from_host(&sdm)?, DeviceBuf::from_host(&scnt)?);
-        let bufs_o = (DeviceBuf::from_host(&oc)?, DeviceBuf::from_host(&oe)?, DeviceBuf::from_host(&odc)?,
-                      DeviceBuf::from_host(&odm)?, DeviceBuf::from_host(&ocnt)?);
-        let st = |b: &(DeviceBuf<u64>, DeviceBuf<u64>, DeviceBuf<u64>, DeviceBuf<u64>, DeviceBuf<u32>), dcap: usize| {
-            ffi::crdt_orswot_states {
-                N: n, M: m, A: a, Dcap: dcap,
-                clock: b.0.as_mut_ptr(), clock_stride: a,
-                entries: b.1.as_mut_ptr(), entry_mstride: a, entry_sstride: m * a,
-                def_clock: b.2.as_mut_ptr(), def_members: b.3.as_mut_ptr(), def_count: b.4.as_mut_ptr(),
-            }
+        let (mut sc, mut se, mut sdc, mut sdm, mut scnt) = side(&selves[..n], dcap_s);
+        let (mut oc, mut oe, mut odc, mut odm, mut ocnt) = side(&others[..n], dcap_o);
+        let ss = ffi::crdt_orswot_states {
+            N: n, M: m, A: a, Dcap: dcap_s,
+            clock: sc.as_mut_ptr(), clock_stride: a, entries: se.as_mut_ptr(), entry_mstride: a, entry_sstride: m * a,
+            def_clock: sdc.as_mut_ptr(), def_members: sdm.as_mut_ptr(), def_count: scnt.as_mut_ptr(),
         };
-        let (ss, os) = (st(&bufs_s, dcap_s), st(&bufs_o, dcap_o));
-        let status = DeviceBuf::<u32>::zeroed(n)?;
-        ctx.check(unsafe { ffi::crdt_orswot_merge_batch(ctx.raw, &ss, &os, status.as_mut_ptr()) })?;
-        let (c, e, dc, dm, cnt, stv) = (bufs_s.0.to_host()?, bufs_s.1.to_host()?, bufs_s.2.to_host()?,
-                                         bufs_s.3.to_host()?, bufs_s.4.to_host()?, status.to_host()?);
+        let os = ffi::crdt_orswot_states {
+            N: n, M: m, A: a, Dcap: dcap_o,
+            clock: oc.as_mut_ptr(), clock_stride: a, entries: oe.as_mut_ptr(), entry_mstride: a, entry_sstride: m * a,
+            def_clock: odc.as_mut_ptr(), def_members: odm.as_mut_ptr(), def_count: ocnt.as_mut_ptr(),
+        };
+        let mut stv = vec![0u32; n];
+        // host arrays straight to the CRDT_MEM_HOST ctx: staged, merged in HBM, copied back into them
+        ctx.check_host(unsafe { ffi::crdt_orswot_merge_batch(ctx.host, &ss, &os, stv.as_mut_ptr()) })?;
+        let (c, e, dc, dm, cnt) = (&sc, &se, &sdc, &sdm, &scnt);
         for i in 0..n {
             if stv[i] != 0 {
                 return Err(GpuError { code: ffi::CRDT_EUNSUPPORTED, msg: format!("orswot merge_batch status {}", stv[i]) });

@@ -61,7 +61,7 @@ def test_ctypes_struct_layout_matches_header():
     assert ctypes.sizeof(abi.MapOut) == 10 * 8
 
 
-HOST_CAPABLE = {f"crdt_{t}_{op}" for t in ("vclock", "gcounter", "pncounter", "gset", "lwwreg")
+HOST_CAPABLE = {f"crdt_{t}_{op}" for t in ("vclock", "gcounter", "pncounter", "gset", "lwwreg", "orswot")
                 for op in ("lub_many", "merge_batch")}
 CTX_ONLY = {"crdt_ctx_destroy", "crdt_ctx_set_stream", "crdt_ctx_synchronize", "crdt_ctx_set_timing",
             "crdt_ctx_timing", "crdt_ctx_timing_reset", "crdt_ctx_tune", "crdt_ctx_set_mem_kind",
@@ -82,7 +82,8 @@ def test_every_compute_entry_point_guards_host_mode():
                 continue
             seen.add(name)
             if name in HOST_CAPABLE:
-                assert "CRDT_CHECK_CTX" in first or "_dispatch(ctx" in first or first.startswith("return crdt_"), name
+                assert ("CRDT_CHECK_CTX" in first or "_dispatch(ctx" in first or first.startswith("return crdt_")
+                        or "_host(ctx" in first), name
             elif name not in CTX_ONLY:
                 assert first.startswith("CRDT_DEVICE_MEM_ONLY(ctx);"), (f, name)
     assert HOST_CAPABLE <= seen and len(seen) > 50

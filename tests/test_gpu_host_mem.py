@@ -141,7 +141,7 @@ def test_host_mode_refusals(hctx):
     assert rc == cg._abi.CRDT_EINVAL
     # entry points without a host path refuse the mode
     assert hctx.raw("crdt_vclock_apply_batch", None, 0, 0, 0, None, None, None, 0, None) == -4
-    assert hctx.raw("crdt_orswot_lub_many", None, None) == -4
+    assert hctx.raw("crdt_orswot_lub_many", None, None) == cg._abi.CRDT_EINVAL  # host-capable: NULL batch
     assert hctx.raw("crdt_map_lub_many", None, None) == -4
     assert hctx.raw("crdt_vclock_ingest", None, None, 0, None, 0, None, 0, None) == -4
     assert hctx.raw("crdt_vclock_lub_many_sharded", None, 0, 0, 0, 0, 0, None) == -4
@@ -149,3 +149,39 @@ def test_host_mode_refusals(hctx):
     # device mode is unaffected on another ctx
     ctx = cg.Context(0)
     assert ctx.lib.crdt_ctx_mem_kind(ctx.ptr) == cg._abi.CRDT_MEM_DEVICE
+
+
+def test_orswot_host_lub_many(hctx):
+    """crdt_orswot_lub_many on host arrays == the device-pointer call == the oracle fold."""
+    c, e, off, dcl, dmem = O.gen_orswot(7, 50, 70, 9, kmax=12, p_def=0.4)
+    D = int(off[-1])
+    got = host.orswot_lub_many(c, e, def_off=[0, D], def_clock=dcl, def_members=dmem, ctx=hctx)
+    dev = cg.orswot.lub_many(torch.from_numpy(c.view(np.int64)).cuda(), torch.from_numpy(e.view(np.int64)).cuda(),
+                             def_off=[0, D], def_clock=torch.from_numpy(dcl.view(np.int64)).cuda(),
+                             def_members=torch.from_numpy(dmem.view(np.int64)).cuda())
+    np.testing.assert_array_equal(got.clock, dev.clock.cpu().numpy().view(np.uint64))
+    np.testing.assert_array_equal(got.entries, dev.entries.cpu().numpy().view(np.uint64))
+    oc, oe, odef, _ = O.orswot_fold(c, e, off, dcl, dmem)
+    np.testing.assert_array_equal(got.clock, oc)
+    np.testing.assert_array_equal(got.entries, oe)
+    surv = {(tuple(int(x) for x in dcl[d]), O.bitmap_members(got.def_members[d])) for d in range(D) if got.def_keep[d]}
+    assert D > 0 and surv == odef
+
+
+def test_orswot_host_merge_batch(hctx):
+    from orswot_apply_util import dense_states, oracle_streams, replay_streams, to_object
+    N, M, n_origins = 30, 40, 4
+    streams = replay_streams(5, 2 * N, n_origins, M, 200)
+    states = oracle_streams([O.Orswot() for _ in streams], streams)
+    lhs, rhs = states[:N], states[N:]
+    Dcap = max(1, max(len(a.deferred) + len(b.deferred) for a, b in zip(lhs, rhs)))
+    me = [np.ascontiguousarray(x) for x in dense_states(lhs, M, n_origins, Dcap)]
+    other = [np.ascontiguousarray(x) for x in dense_states(rhs, M, n_origins, Dcap)]
+    me[4], other[4] = me[4].astype(np.uint32), other[4].astype(np.uint32)
+    status = host.orswot_merge_batch(tuple(me), tuple(other), ctx=hctx)
+    assert (status == 0).all(), status
+    for i, (a, b) in enumerate(zip(lhs, rhs)):
+        exp = a.copy()
+        exp.merge(b.copy())
+        assert to_object(me[0], me[1], me[2], me[3], me[4], i) == exp, i
+    assert sum(len(s.deferred) for s in lhs) > 0
