@@ -82,11 +82,12 @@ int crdt_ctx_tune(crdt_ctx *ctx, const char *spec);
  * asynchronous on the ctx stream.  CRDT_MEM_HOST: the buffers of
  *     crdt_{vclock,gcounter,pncounter,gset}_lub_many / _merge_batch,
  *     crdt_lwwreg_lub_many / _merge_batch,
- *     crdt_orswot_lub_many / _merge_batch (every pointer in the structs; def_off stays host)
+ *     crdt_orswot_lub_many / _merge_batch, crdt_map_lub_many / _merge_batch (every pointer in
+ *     the structs; def_off stays host)
  * are HOST pointers (pageable, or pinned by crdt_host_alloc for direct DMA).  The lattice and LWW
  * forms stream them through two ctx-owned device chunk buffers (tune key stage_kb, default
- * 256 MiB each), overlapping the H2D copy of chunk k+1 with the fold of chunk k; the Orswot forms
- * stage the whole batch (the deferred removes need every replica's clock).  The call returns when
+ * 256 MiB each), overlapping the H2D copy of chunk k+1 with the fold of chunk k; the Orswot and
+ * Map forms stage the whole batch (the deferred removes need every replica's clock).  The call returns when
  * the results are in host memory.  Results are identical to the device-pointer call.  In host mode
  * crdt_lwwreg_lub_many needs out_marker and out_val; a device pointer is rejected (CRDT_EINVAL);
  * every other entry point returns CRDT_EUNSUPPORTED. */

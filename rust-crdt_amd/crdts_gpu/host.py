@@ -229,3 +229,81 @@ def orswot_merge_batch(self_states, other_states, ctx: Optional[HostContext] = N
     status = np.zeros(self_states[0].shape[0], np.uint32)
     ctx.call("crdt_orswot_merge_batch", ctypes.byref(structs[0]), ctypes.byref(structs[1]), _ptr(status))
     return status
+
+
+class MapHostLub(NamedTuple):
+    clock: np.ndarray     # (G, A)
+    ec: np.ndarray        # (G, K, A)
+    vclk: np.ndarray      # (G, K, Vout, A)
+    vval: np.ndarray      # (G, K, Vout)
+    nval: np.ndarray      # (G, K) uint32
+    flags: np.ndarray     # (G,) uint32
+    def_keep: np.ndarray  # (D,) uint8
+    def_keys: np.ndarray  # (D, Kw)
+
+
+def map_lub_many(clock, ec, vclk, vval, def_off=None, def_row=None, def_clock=None, def_keys=None, vout: int = 4,
+                 ctx: Optional[HostContext] = None) -> MapHostLub:
+    """crdt_map_lub_many on host arrays (one group): clock (R, A), ec (R, K, A), vclk (R, K, V, A),
+    vval (R, K, V); removes pooled (def_off [0, D], def_row (D,) uint32, def_clock (D, A),
+    def_keys (D, Kw)).  Whole-batch staging by the library."""
+    ctx = ctx or HostContext()
+    arrs = [np.ascontiguousarray(_u64(x, n)) for x, n in ((clock, "clock"), (ec, "ec"), (vclk, "vclk"), (vval, "vval"))]
+    c, e, vc, vv = arrs
+    R, A = c.shape
+    K, V = e.shape[1], vc.shape[2]
+    Kw = (K + 63) // 64
+    b = _abi.MapBatch()
+    b.G, b.R, b.K, b.A, b.V = 1, R, K, A, V
+    b.clock, b.clock_rstride, b.clock_gstride = c.ctypes.data, A, R * A
+    b.ec, b.ec_rstride, b.ec_gstride = e.ctypes.data, K * A, R * K * A
+    b.vclk, b.vclk_rstride, b.vclk_gstride = vc.ctypes.data, K * V * A, R * K * V * A
+    b.vval, b.vval_rstride, b.vval_gstride = vv.ctypes.data, K * V, R * K * V
+    D = 0
+    keep = [arrs]
+    if def_off is not None and int(def_off[-1]):
+        D = int(def_off[-1])
+        off = (ctypes.c_size_t * 2)(0, D)
+        dr = np.ascontiguousarray(def_row, dtype=np.uint32)
+        dcl = np.ascontiguousarray(_u64(def_clock, "def_clock"))
+        dks = np.ascontiguousarray(_u64(def_keys, "def_keys"))
+        keep += [off, dr, dcl, dks]
+        b.def_off, b.def_row, b.def_clock, b.def_keys = off, dr.ctypes.data, dcl.ctypes.data, dks.ctypes.data
+    out = MapHostLub(np.zeros((1, A), np.uint64), np.zeros((1, K, A), np.uint64), np.zeros((1, K, vout, A), np.uint64),
+                     np.zeros((1, K, vout), np.uint64), np.zeros((1, K), np.uint32), np.zeros(1, np.uint32),
+                     np.zeros(D, np.uint8), np.zeros((D, Kw), np.uint64))
+    o = _abi.MapOut()
+    o.Vout, o.Vstate = vout, 0
+    o.clock, o.ec, o.vclk, o.vval = (x.ctypes.data for x in (out.clock, out.ec, out.vclk, out.vval))
+    o.nval, o.flags = out.nval.ctypes.data, out.flags.ctypes.data
+    o.def_keep = out.def_keep.ctypes.data if D else None
+    o.def_keys = out.def_keys.ctypes.data if D else None
+    ctx.call("crdt_map_lub_many", ctypes.byref(b), ctypes.byref(o))
+    return out
+
+
+def map_merge_batch(self_states, other_states, ctx: Optional[HostContext] = None) -> np.ndarray:
+    """crdt_map_merge_batch on host arrays, in place on self: each side a tuple (clock (N, A),
+    ec (N, K, A), vclk (N, K, V, A), vval (N, K, V), def_clock (N, Dcap, A), def_keys (N, Dcap, Kw),
+    def_count (N,) uint32) of C-contiguous arrays.  Returns status (N,) uint32."""
+    ctx = ctx or HostContext()
+    ss, dd = [], []
+    for side in (self_states, other_states):
+        clock, ec, vclk, vval, dcl, dks, cnt = side
+        for a in side:
+            if not a.flags.c_contiguous:
+                raise ValueError("map_merge_batch: C-contiguous arrays required")
+        N, A = clock.shape
+        K, V = ec.shape[1], vclk.shape[2]
+        s = _abi.MapStates()
+        s.N, s.K, s.A, s.V = N, K, A, V
+        s.clock, s.clock_stride, s.ec, s.ec_stride = clock.ctypes.data, A, ec.ctypes.data, K * A
+        s.vclk, s.vclk_stride, s.vval, s.vval_stride = vclk.ctypes.data, K * V * A, vval.ctypes.data, K * V
+        d = _abi.MapDeferred()
+        d.clock, d.keys, d.count, d.Dcap = dcl.ctypes.data, dks.ctypes.data, cnt.ctypes.data, dcl.shape[1]
+        ss.append(s)
+        dd.append(d)
+    status = np.zeros(self_states[0].shape[0], np.uint32)
+    ctx.call("crdt_map_merge_batch", ctypes.byref(ss[0]), ctypes.byref(dd[0]), ctypes.byref(ss[1]),
+             ctypes.byref(dd[1]), _ptr(status))
+    return status

@@ -207,6 +207,9 @@ int lww_merge_batch_host(crdt_ctx *ctx, u64 *sm, u64 *sv, const u64 *om, const u
 int orswot_lub_many_host(crdt_ctx *ctx, const crdt_orswot_batch *in, crdt_orswot_out *out);
 int orswot_merge_batch_host(crdt_ctx *ctx, const crdt_orswot_states *self, const crdt_orswot_states *other,
                             uint32_t *status);
+int map_lub_many_host(crdt_ctx *ctx, const crdt_map_batch *in, crdt_map_out *out);
+int map_merge_batch_host(crdt_ctx *ctx, const crdt_map_states *self, const crdt_map_deferred *self_def,
+                         const crdt_map_states *other, const crdt_map_deferred *other_def, uint32_t *status);
 void free_stage(crdt_ctx *ctx);
 
 // Wave-uniform row-group loop: every lane runs the same iterations (rows past N are masked),

@@ -499,6 +499,178 @@ int orswot_merge_batch_host(crdt_ctx *ctx, const crdt_orswot_states *self, const
   return finish(ctx, orswot_merge_host_body(ctx, self, other, status, ds));
 }
 
+// ---- Map<K, MVReg<u64>>: whole-batch staging (the fold reads every replica of a key in order) ------
+// rows x width words of a (possibly strided) host block into a packed device block
+static int h2d_rows(crdt_ctx *ctx, uint64_t *dst, const uint64_t *src, size_t pitch, size_t width, size_t rows) {
+  STAGE_HIP(copy_rows(dst, width * 8, src, pitch * 8, width * 8, rows, hipMemcpyHostToDevice, ctx->stream));
+  return CRDT_OK;
+}
+static int d2h_rows(crdt_ctx *ctx, uint64_t *dst, const uint64_t *src, size_t pitch, size_t width, size_t rows) {
+  STAGE_HIP(copy_rows(dst, pitch * 8, src, width * 8, width * 8, rows, hipMemcpyDeviceToHost, ctx->stream));
+  return CRDT_OK;
+}
+
+static int map_lub_host_body(crdt_ctx *ctx, const crdt_map_batch *in, crdt_map_out *out, DevScratch &ds) {
+  const size_t G = in->G, R = in->R, K = in->K, A = in->A, V = in->V, Kw = (K + 63) / 64, Vo = out->Vout;
+  const size_t D = in->def_off ? in->def_off[G] : 0;
+  uint64_t *c, *ec, *vc, *vv, *dc, *dk, *oc, *oec, *ovc, *ovv, *odk = nullptr;
+  uint32_t *drow, *onv = nullptr, *ofl;
+  uint8_t *okp = nullptr;
+  if (int rc = ds.get(ctx, G * R * A, &c)) return rc;
+  if (int rc = ds.get(ctx, G * R * K * A, &ec)) return rc;
+  if (int rc = ds.get(ctx, G * R * K * V * A, &vc)) return rc;
+  if (int rc = ds.get(ctx, G * R * K * V, &vv)) return rc;
+  if (int rc = ds.get(ctx, D, &drow)) return rc;
+  if (int rc = ds.get(ctx, D * A, &dc)) return rc;
+  if (int rc = ds.get(ctx, D * Kw, &dk)) return rc;
+  if (int rc = ds.get(ctx, G * A, &oc)) return rc;
+  if (int rc = ds.get(ctx, G * K * A, &oec)) return rc;
+  if (int rc = ds.get(ctx, G * K * Vo * A, &ovc)) return rc;
+  if (int rc = ds.get(ctx, G * K * Vo, &ovv)) return rc;
+  if (out->nval)
+    if (int rc = ds.get(ctx, G * K, &onv)) return rc;
+  if (int rc = ds.get(ctx, G, &ofl)) return rc;
+  if (out->def_keep)
+    if (int rc = ds.get(ctx, D, &okp)) return rc;
+  if (out->def_keys)
+    if (int rc = ds.get(ctx, D * Kw, &odk)) return rc;
+  for (size_t g = 0; g < G && R; ++g) {  // per replica: one contiguous block of each plane (packed rows)
+    if (int rc = h2d_rows(ctx, c + g * R * A, in->clock + g * in->clock_gstride, in->clock_rstride, A, R)) return rc;
+    if (int rc = h2d_rows(ctx, ec + g * R * K * A, in->ec + g * in->ec_gstride, in->ec_rstride, K * A, R)) return rc;
+    if (int rc = h2d_rows(ctx, vc + g * R * K * V * A, in->vclk + g * in->vclk_gstride, in->vclk_rstride, K * V * A, R))
+      return rc;
+    if (int rc = h2d_rows(ctx, vv + g * R * K * V, in->vval + g * in->vval_gstride, in->vval_rstride, K * V, R)) return rc;
+  }
+  if (D) {
+    STAGE_HIP(hipMemcpyAsync(drow, in->def_row, D * 4, hipMemcpyHostToDevice, ctx->stream));
+    if (int rc = h2d_async(ctx, dc, in->def_clock, D * A * 8)) return rc;
+    if (int rc = h2d_async(ctx, dk, in->def_keys, D * Kw * 8)) return rc;
+  }
+  crdt_map_batch b = *in;
+  b.clock = c, b.clock_rstride = A, b.clock_gstride = R * A;
+  b.ec = ec, b.ec_rstride = K * A, b.ec_gstride = R * K * A;
+  b.vclk = vc, b.vclk_rstride = K * V * A, b.vclk_gstride = R * K * V * A;
+  b.vval = vv, b.vval_rstride = K * V, b.vval_gstride = R * K * V;
+  b.def_row = D ? drow : nullptr, b.def_clock = D ? dc : nullptr, b.def_keys = D ? dk : nullptr;
+  crdt_map_out o{Vo, out->Vstate, oc, oec, ovc, ovv, onv, ofl, okp, odk};
+  {
+    DeviceModeScope dev(ctx);
+    if (int rc = crdt_map_lub_many(ctx, &b, &o)) return rc;
+  }
+  if (int rc = d2h_async(ctx, out->clock, oc, G * A * 8)) return rc;
+  if (int rc = d2h_async(ctx, out->ec, oec, G * K * A * 8)) return rc;
+  if (int rc = d2h_async(ctx, out->vclk, ovc, G * K * Vo * A * 8)) return rc;
+  if (int rc = d2h_async(ctx, out->vval, ovv, G * K * Vo * 8)) return rc;
+  if (int rc = d2h_async(ctx, out->nval, onv, G * K * 4)) return rc;
+  if (int rc = d2h_async(ctx, out->flags, ofl, G * 4)) return rc;
+  if (int rc = d2h_async(ctx, out->def_keep, okp, D)) return rc;
+  return d2h_async(ctx, out->def_keys, odk, D * Kw * 8);
+}
+
+int map_lub_many_host(crdt_ctx *ctx, const crdt_map_batch *in, crdt_map_out *out) {
+  if (!in || !out) return fail(ctx, CRDT_EINVAL, "map_lub_many: NULL batch/out");
+  if (in->G == 0) return CRDT_OK;
+  if (!out->clock || !out->ec || !out->vclk || !out->vval || !out->flags)
+    return fail(ctx, CRDT_EINVAL, "map_lub_many: NULL output");
+  if (in->R && (!in->clock || !in->ec || !in->vclk || !in->vval))
+    return fail(ctx, CRDT_EINVAL, "map_lub_many: NULL input");
+  const size_t K = in->K, A = in->A, V = in->V;
+  if (in->R > 1 && (in->clock_rstride < A || in->ec_rstride < K * A || in->vclk_rstride < K * V * A ||
+                    in->vval_rstride < K * V))
+    return fail(ctx, CRDT_EINVAL, "map_lub_many: replica strides smaller than a replica");
+  if (in->def_off && in->def_off[in->G] && (!in->def_row || !in->def_clock || !in->def_keys))
+    return fail(ctx, CRDT_EINVAL, "map_lub_many: NULL deferred input");
+  for (auto [p, w] : {std::pair<const void *, const char *>{in->clock, "clock"}, {in->ec, "ec"}, {in->vclk, "vclk"},
+                      {in->vval, "vval"}, {in->def_row, "def_row"}, {in->def_clock, "def_clock"},
+                      {in->def_keys, "def_keys"}, {out->clock, "out.clock"}, {out->ec, "out.ec"},
+                      {out->vclk, "out.vclk"}, {out->vval, "out.vval"}, {out->nval, "out.nval"},
+                      {out->flags, "out.flags"}, {out->def_keep, "out.def_keep"}, {out->def_keys, "out.def_keys"}})
+    if (int rc = check_host(ctx, p, w)) return rc;
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  DevScratch ds;
+  return finish(ctx, map_lub_host_body(ctx, in, out, ds));
+}
+
+static int map_merge_host_body(crdt_ctx *ctx, const crdt_map_states *a, const crdt_map_deferred *ad,
+                               const crdt_map_states *b, const crdt_map_deferred *bd, uint32_t *status,
+                               DevScratch &ds) {
+  const size_t N = a->N, K = a->K, A = a->A, Kw = (K + 63) / 64;
+  crdt_map_states d[2] = {*a, *b};
+  crdt_map_deferred dd[2] = {*ad, *bd};
+  const crdt_map_states *h[2] = {a, b};
+  const crdt_map_deferred *hd[2] = {ad, bd};
+  for (int i = 0; i < 2; ++i) {
+    const crdt_map_states &x = *h[i];
+    crdt_map_states &y = d[i];
+    const size_t V = x.V, Dc = hd[i]->Dcap;
+    if (int rc = ds.get(ctx, N * A, &y.clock)) return rc;
+    if (int rc = ds.get(ctx, N * K * A, &y.ec)) return rc;
+    if (int rc = ds.get(ctx, N * K * V * A, &y.vclk)) return rc;
+    if (int rc = ds.get(ctx, N * K * V, &y.vval)) return rc;
+    y.clock_stride = A, y.ec_stride = K * A, y.vclk_stride = K * V * A, y.vval_stride = K * V;
+    if (int rc = h2d_rows(ctx, y.clock, x.clock, x.clock_stride, A, N)) return rc;
+    if (K) {
+      if (int rc = h2d_rows(ctx, y.ec, x.ec, x.ec_stride, K * A, N)) return rc;
+      if (int rc = h2d_rows(ctx, y.vclk, x.vclk, x.vclk_stride, K * V * A, N)) return rc;
+      if (int rc = h2d_rows(ctx, y.vval, x.vval, x.vval_stride, K * V, N)) return rc;
+    }
+    crdt_map_deferred &z = dd[i];
+    if (int rc = ds.get(ctx, N * Dc * A, &z.clock)) return rc;
+    if (int rc = ds.get(ctx, N * Dc * Kw, &z.keys)) return rc;
+    if (hd[i]->count) {
+      if (int rc = ds.get(ctx, N, &z.count)) return rc;
+      STAGE_HIP(hipMemcpyAsync(z.count, hd[i]->count, N * 4, hipMemcpyHostToDevice, ctx->stream));
+    }
+    if (int rc = h2d_async(ctx, z.clock, hd[i]->clock, N * Dc * A * 8)) return rc;
+    if (int rc = h2d_async(ctx, z.keys, hd[i]->keys, N * Dc * Kw * 8)) return rc;
+  }
+  uint32_t *dst = nullptr;
+  if (int rc = ds.get(ctx, N, &dst)) return rc;
+  {
+    DeviceModeScope dev(ctx);
+    if (int rc = crdt_map_merge_batch(ctx, &d[0], &dd[0], &d[1], &dd[1], dst)) return rc;
+  }
+  const size_t V = a->V, Dc = ad->Dcap;
+  if (int rc = d2h_rows(ctx, a->clock, d[0].clock, a->clock_stride, A, N)) return rc;
+  if (K) {
+    if (int rc = d2h_rows(ctx, a->ec, d[0].ec, a->ec_stride, K * A, N)) return rc;
+    if (int rc = d2h_rows(ctx, a->vclk, d[0].vclk, a->vclk_stride, K * V * A, N)) return rc;
+    if (int rc = d2h_rows(ctx, a->vval, d[0].vval, a->vval_stride, K * V, N)) return rc;
+  }
+  if (int rc = d2h_async(ctx, ad->clock, dd[0].clock, N * Dc * A * 8)) return rc;
+  if (int rc = d2h_async(ctx, ad->keys, dd[0].keys, N * Dc * Kw * 8)) return rc;
+  if (int rc = d2h_async(ctx, ad->count, dd[0].count, N * 4)) return rc;
+  return d2h_async(ctx, status, dst, N * 4);
+}
+
+int map_merge_batch_host(crdt_ctx *ctx, const crdt_map_states *self, const crdt_map_deferred *self_def,
+                         const crdt_map_states *other, const crdt_map_deferred *other_def, uint32_t *status) {
+  if (!self || !other || !self_def || !other_def || !status)
+    return fail(ctx, CRDT_EINVAL, "map_merge_batch: NULL argument");
+  const crdt_map_states &a = *self, &b = *other;
+  if (a.N != b.N || a.K != b.K || a.A != b.A)
+    return fail(ctx, CRDT_EINVAL, "map_merge_batch: self and other differ in N, K or A");
+  if (a.N == 0) return CRDT_OK;
+  if (!a.clock || !b.clock || !self_def->count || (a.K && (!a.ec || !a.vclk || !a.vval || !b.ec || !b.vclk || !b.vval)))
+    return fail(ctx, CRDT_EINVAL, "map_merge_batch: NULL buffer");
+  const size_t K = a.K, A = a.A;
+  if (a.clock_stride < A || b.clock_stride < A || a.ec_stride < K * A || b.ec_stride < K * A ||
+      a.vclk_stride < K * a.V * A || b.vclk_stride < K * b.V * A || a.vval_stride < K * a.V || b.vval_stride < K * b.V)
+    return fail(ctx, CRDT_EINVAL, "map_merge_batch: strides smaller than the rows they hold");
+  for (const crdt_map_states *x : {self, other})
+    for (auto [p, w] : {std::pair<const void *, const char *>{x->clock, "clock"}, {x->ec, "ec"}, {x->vclk, "vclk"},
+                        {x->vval, "vval"}})
+      if (int rc = check_host(ctx, p, w)) return rc;
+  for (const crdt_map_deferred *x : {self_def, other_def})
+    for (auto [p, w] : {std::pair<const void *, const char *>{x->clock, "def.clock"}, {x->keys, "def.keys"},
+                        {x->count, "def.count"}})
+      if (int rc = check_host(ctx, p, w)) return rc;
+  if (int rc = check_host(ctx, status, "status")) return rc;
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  DevScratch ds;
+  return finish(ctx, map_merge_host_body(ctx, self, self_def, other, other_def, status, ds));
+}
+
 void free_stage(crdt_ctx *ctx) {
   if (ctx->hstream) (void)hipStreamSynchronize(ctx->hstream);
   for (auto &b : ctx->hbuf)

@@ -1200,7 +1200,7 @@ static int map_vi(size_t V, size_t want) {
 static bool aligned16(const void *x) { return (reinterpret_cast<uintptr_t>(x) & 15) == 0; }
 
 extern "C" int crdt_map_lub_many(crdt_ctx *ctx, const crdt_map_batch *in, crdt_map_out *out) {
-  CRDT_DEVICE_MEM_ONLY(ctx);
+  if (ctx && ctx->mem_kind == CRDT_MEM_HOST) return crdt::map_lub_many_host(ctx, in, out);
   CRDT_CHECK_CTX(ctx);
   if (!in || !out) return fail(ctx, CRDT_EINVAL, "map_lub_many: NULL batch/out");
   const size_t G = in->G, R = in->R, K = in->K, A = in->A, V = in->V, Vout = out->Vout;

@@ -935,7 +935,8 @@ extern "C" int crdt_orswot_merge_batch(crdt_ctx *ctx, const crdt_orswot_states *
 extern "C" int crdt_map_merge_batch(crdt_ctx *ctx, const crdt_map_states *self, const crdt_map_deferred *self_def,
                                     const crdt_map_states *other, const crdt_map_deferred *other_def,
                                     uint32_t *status) {
-  CRDT_DEVICE_MEM_ONLY(ctx);
+  if (ctx && ctx->mem_kind == CRDT_MEM_HOST)
+    return crdt::map_merge_batch_host(ctx, self, self_def, other, other_def, status);
   CRDT_CHECK_CTX(ctx);
   if (!self || !other || !self_def || !other_def || !status)
     return fail(ctx, CRDT_EINVAL, "map_merge_batch: NULL argument");

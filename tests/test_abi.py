@@ -61,7 +61,7 @@ def test_ctypes_struct_layout_matches_header():
     assert ctypes.sizeof(abi.MapOut) == 10 * 8
 
 
-HOST_CAPABLE = {f"crdt_{t}_{op}" for t in ("vclock", "gcounter", "pncounter", "gset", "lwwreg", "orswot")
+HOST_CAPABLE = {f"crdt_{t}_{op}" for t in ("vclock", "gcounter", "pncounter", "gset", "lwwreg", "orswot", "map")
                 for op in ("lub_many", "merge_batch")}
 CTX_ONLY = {"crdt_ctx_destroy", "crdt_ctx_set_stream", "crdt_ctx_synchronize", "crdt_ctx_set_timing",
             "crdt_ctx_timing", "crdt_ctx_timing_reset", "crdt_ctx_tune", "crdt_ctx_set_mem_kind",
@@ -83,7 +83,7 @@ def test_every_compute_entry_point_guards_host_mode():
             seen.add(name)
             if name in HOST_CAPABLE:
                 assert ("CRDT_CHECK_CTX" in first or "_dispatch(ctx" in first or first.startswith("return crdt_")
-                        or "_host(ctx" in first), name
+                        or "_host(ctx" in first or "mem_kind == CRDT_MEM_HOST" in first), name
             elif name not in CTX_ONLY:
                 assert first.startswith("CRDT_DEVICE_MEM_ONLY(ctx);"), (f, name)
     assert HOST_CAPABLE <= seen and len(seen) > 50

@@ -142,7 +142,8 @@ def test_host_mode_refusals(hctx):
     # entry points without a host path refuse the mode
     assert hctx.raw("crdt_vclock_apply_batch", None, 0, 0, 0, None, None, None, 0, None) == -4
     assert hctx.raw("crdt_orswot_lub_many", None, None) == cg._abi.CRDT_EINVAL  # host-capable: NULL batch
-    assert hctx.raw("crdt_map_lub_many", None, None) == -4
+    assert hctx.raw("crdt_map_lub_many", None, None) == cg._abi.CRDT_EINVAL  # host-capable too
+    assert hctx.raw("crdt_map_apply_batch", None, None, None, None, 0, None, None) == -4
     assert hctx.raw("crdt_vclock_ingest", None, None, 0, None, 0, None, 0, None) == -4
     assert hctx.raw("crdt_vclock_lub_many_sharded", None, 0, 0, 0, 0, 0, None) == -4
     assert hctx.lib.crdt_ctx_mem_kind(hctx.ptr) == cg._abi.CRDT_MEM_HOST
@@ -185,3 +186,58 @@ def test_orswot_host_merge_batch(hctx):
         exp.merge(b.copy())
         assert to_object(me[0], me[1], me[2], me[3], me[4], i) == exp, i
     assert sum(len(s.deferred) for s in lhs) > 0
+
+
+def test_map_host_lub_many(hctx):
+    """crdt_map_lub_many on host arrays == the device-pointer call (bit for bit, every output)."""
+    dfr = O.synth_map_deferred(0x5EED0044, 300, 40, 8, 30, p_def=0.3)
+    rows, dcl, dks = dfr
+    d = O.synth_map(0x5EED0044, 300, 40, 8, 2, 30, keys=np.arange(40), deferred=dfr)
+    D = rows.shape[0]
+    got = host.map_lub_many(d["clock"], d["ec"], d["vclk"], d["vval"], def_off=[0, D], def_row=rows, def_clock=dcl,
+                            def_keys=dks, ctx=hctx)
+    t = lambda x: torch.from_numpy(np.ascontiguousarray(x).view(np.int64)).cuda()  # noqa: E731
+    dev = cg.map.lub_many(t(d["clock"]), t(d["ec"]), t(d["vclk"]), t(d["vval"]), def_off=[0, D],
+                          def_row=torch.from_numpy(rows.astype(np.int32)).cuda(), def_clock=t(dcl), def_keys=t(dks),
+                          vout=4, check=False)
+    h = lambda x: x.cpu().numpy().view(np.uint64) if x.dtype == torch.int64 else x.cpu().numpy()  # noqa: E731
+    np.testing.assert_array_equal(got.clock[0], h(dev.clock))
+    np.testing.assert_array_equal(got.ec[0], h(dev.ec))
+    np.testing.assert_array_equal(got.vclk[0], h(dev.vclk))
+    np.testing.assert_array_equal(got.vval[0], h(dev.vval))
+    np.testing.assert_array_equal(got.def_keep, h(dev.def_keep).astype(np.uint8))
+    assert D > 0 and got.ec.any()
+
+
+def test_map_host_merge_batch(hctx):
+    from test_gpu_merge_batch import replay_maps
+    N, K, n_origins = 20, 10, 4
+    maps = replay_maps(9, 2 * N, n_origins, K, 150)
+    lhs, rhs = maps[:N], maps[N:]
+    exp = []
+    for a, b in zip(lhs, rhs):
+        x = a.copy()
+        x.merge(b.copy())
+        exp.append(x)
+    V = max(1, O.max_vals(exp), O.max_vals(lhs), O.max_vals(rhs))
+    Dcap = max(1, max(len(m.deferred) for m in list(lhs) + list(rhs) + exp))
+
+    def side(ms):
+        dd = O.map_to_dense(ms, K, n_origins, V)
+        Kw = (K + 63) // 64
+        dcl = np.zeros((N, Dcap, n_origins), np.uint64)
+        dks = np.zeros((N, Dcap, Kw), np.uint64)
+        cnt = np.zeros(N, np.uint32)
+        for j, r in enumerate(dd["def_row"].astype(np.int64)):
+            dcl[r, cnt[r]] = dd["def_clock"][j]
+            dks[r, cnt[r]] = dd["def_keys"][j]
+            cnt[r] += 1
+        return tuple(np.ascontiguousarray(x) for x in (dd["clock"], dd["ec"], dd["vclk"], dd["vval"], dcl, dks, cnt))
+
+    me, other = side(lhs), side(rhs)
+    status = host.map_merge_batch(me, other, ctx=hctx)
+    assert (status == 0).all(), status
+    for i, e in enumerate(exp):
+        deferred = [(me[4][i, j], O.bitmap_members(me[5][i, j])) for j in range(int(me[6][i]))]
+        got = O.dense_to_map(me[0][i], me[1][i], me[2][i], me[3][i], deferred)
+        assert got == e, i
