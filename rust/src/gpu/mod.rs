@@ -20,8 +20,9 @@
 //! resident in HBM use [`ffi`] directly on device buffers with [`GpuCtx::as_ptr`].
 //!
 //! Field access: `VClock::dots`, the `Orswot` fields and the `LWWReg` fields are already visible
-//! to an in-crate module; the maintainer changes `GCounter::inner`, `PNCounter::{p, n}` and
-//! `GSet::value` from private to `pub(crate)` (visibility only, no behaviour change).
+//! to an in-crate module; the maintainer changes `GCounter::inner`, `PNCounter::{p, n}`,
+//! `GSet::value`, the `Map` fields, `map::Entry` and `MVReg::vals` from private to `pub(crate)`
+//! (visibility only, no behaviour change; `rust/lib.rs.patch`).
 //!
 //! Not built in the repository that ships it (its image has no Rust toolchain); the extern block
 //! in [`ffi`] is generated from the header and checked against it by `tests/test_rust_shim.py`.
@@ -40,7 +41,8 @@ use crate::error::Error as CrdtError;
 use crate::orswot::Member;
 use crate::traits::CvRDT;
 use crate::vclock::{Actor, VClock};
-use crate::{GCounter, GSet, LWWReg, Orswot, PNCounter};
+use crate::map::Entry;
+use crate::{GCounter, GSet, LWWReg, MVReg, Map, Orswot, PNCounter};
 
 pub use hip::DeviceBuf;
 
@@ -684,6 +686,267 @@ impl<M: Member, A: Actor> BatchCvRDT for Orswot<M, A> {
                 defs.push((dc[base * a..(base + 1) * a].to_vec(), dm[base * mw..(base + 1) * mw].to_vec()));
             }
             selves[i] = d.egress(&c[i * a..(i + 1) * a], &e[i * m * a..(i + 1) * m * a], &defs);
+        }
+        Ok(())
+    }
+}
+
+// ---- Map<K, MVReg<V, A>, A>: exact per-key left fold (map.rs:140-220, mvreg.rs:112-128) ------------
+// MVReg::merge compares value CLOCKS only (never the values), so every value instance gets a
+// fresh u64 id into a per-call arena and comes back by clone; keys and actors are interned.
+struct MapDense<K: Ord + Clone, A: Actor> {
+    actors: Index<A>,
+    keys: Index<K>,
+    vmax: usize,
+}
+
+/// One state's dense rows (the crdt_map_states / crdt_map_deferred per-state layout).
+struct MapRows {
+    clock: Vec<u64>,    // [A]
+    ec: Vec<u64>,       // [K][A]
+    vclk: Vec<u64>,     // [K][V][A]
+    vval: Vec<u64>,     // [K][V] arena ids
+    def_clock: Vec<u64>, // [D][A]
+    def_keys: Vec<u64>,  // [D][Kw]
+}
+
+impl<K: Ord + Clone, A: Actor> MapDense<K, A> {
+    fn of<'a, V: Clone + 'a, I: Iterator<Item = &'a Map<K, MVReg<V, A>, A>>>(states: I) -> Self
+    where
+        K: 'a,
+        A: 'a,
+    {
+        let mut d = MapDense { actors: Index::new(), keys: Index::new(), vmax: 1 };
+        for s in states {
+            for a in s.clock.dots.keys() {
+                d.actors.intern(a);
+            }
+            for (k, e) in s.entries.iter() {
+                d.keys.intern(k);
+                for a in e.clock.dots.keys() {
+                    d.actors.intern(a);
+                }
+                d.vmax = d.vmax.max(e.val.vals.len());
+                for (c, _) in e.val.vals.iter() {
+                    for a in c.dots.keys() {
+                        d.actors.intern(a);
+                    }
+                }
+            }
+            for (rm, ks) in s.deferred.iter() {
+                for a in rm.dots.keys() {
+                    d.actors.intern(a);
+                }
+                for k in ks {
+                    d.keys.intern(k);
+                }
+            }
+        }
+        d
+    }
+
+    fn ingest<V: Clone>(&self, s: &Map<K, MVReg<V, A>, A>, v: usize, arena: &mut Vec<V>) -> MapRows {
+        let (a, k) = (self.actors.width(), self.keys.width());
+        let kw = (k + 63) / 64;
+        let mut r = MapRows {
+            clock: vec![0u64; a],
+            ec: vec![0u64; k * a],
+            vclk: vec![0u64; k * v * a],
+            vval: vec![0u64; k * v],
+            def_clock: Vec::new(),
+            def_keys: Vec::new(),
+        };
+        clock_row(&s.clock, &self.actors, &mut r.clock);
+        for (key, e) in s.entries.iter() {
+            let i = self.keys.pos[key];
+            clock_row(&e.clock, &self.actors, &mut r.ec[i * a..(i + 1) * a]);
+            for (slot, (c, val)) in e.val.vals.iter().enumerate().take(v) {
+                let base = (i * v + slot) * a;
+                clock_row(c, &self.actors, &mut r.vclk[base..base + a]);
+                r.vval[i * v + slot] = arena.len() as u64;
+                arena.push(val.clone());
+            }
+        }
+        for (rm, ks) in s.deferred.iter() {
+            let mut row = vec![0u64; a];
+            clock_row(rm, &self.actors, &mut row);
+            let mut bits = vec![0u64; kw];
+            for key in ks {
+                let b = self.keys.pos[key];
+                bits[b / 64] |= 1u64 << (b % 64);
+            }
+            r.def_clock.extend(row);
+            r.def_keys.extend(bits);
+        }
+        r
+    }
+
+    /// Rebuild a Map from one state's rows (value slot s of key k: vclk[(k*v + s)*a ..]).
+    fn egress<V: Clone>(&self, clock: &[u64], ec: &[u64], vclk: &[u64], vval: &[u64], v: usize,
+                        deferred: &[(Vec<u64>, Vec<u64>)], arena: &[V]) -> Map<K, MVReg<V, A>, A> {
+        let a = self.actors.width();
+        let mut m = Map::new();
+        m.clock = row_clock(clock, &self.actors);
+        for (i, key) in self.keys.ids.iter().enumerate() {
+            let row = &ec[i * a..(i + 1) * a];
+            if row.iter().all(|&x| x == 0) {
+                continue;
+            }
+            let mut vals = Vec::new();
+            for slot in 0..v {
+                let base = (i * v + slot) * a;
+                let vr = &vclk[base..base + a];
+                if vr.iter().any(|&x| x != 0) {
+                    vals.push((row_clock(vr, &self.actors), arena[vval[i * v + slot] as usize].clone()));
+                }
+            }
+            m.entries.insert(key.clone(), Entry { clock: row_clock(row, &self.actors), val: MVReg { vals } });
+        }
+        for (rm, bits) in deferred {
+            let mut ks = BTreeSet::new();
+            for (w, &word) in bits.iter().enumerate() {
+                let mut x = word;
+                while x != 0 {
+                    let b = w * 64 + x.trailing_zeros() as usize;
+                    x &= x - 1;
+                    if b < self.keys.ids.len() {
+                        ks.insert(self.keys.ids[b].clone());
+                    }
+                }
+            }
+            m.deferred.entry(row_clock(rm, &self.actors)).or_insert_with(BTreeSet::new).extend(ks);
+        }
+        m
+    }
+}
+
+impl<K: Ord + Clone, V: Clone, A: Actor> BatchCvRDT for Map<K, MVReg<V, A>, A> {
+    fn lub_many(ctx: &GpuCtx, replicas: Vec<Self>) -> Result<Self, GpuError> {
+        if replicas.is_empty() {
+            return Ok(Map::new());
+        }
+        let d = MapDense::of(replicas.iter());
+        let (r, a, k, v) = (replicas.len(), d.actors.width(), d.keys.width(), d.vmax.min(4));
+        let kw = (k + 63) / 64;
+        if d.vmax > 4 {
+            return Err(GpuError { code: ffi::CRDT_EUNSUPPORTED, msg: "Map lub_many: a replica register holds more than 4 values".into() });
+        }
+        let mut arena = Vec::new();
+        let (mut clock, mut ec, mut vclk, mut vval) = (Vec::new(), Vec::new(), Vec::new(), Vec::new());
+        let (mut def_row, mut dcl, mut dks) = (Vec::new(), Vec::new(), Vec::new());
+        for (i, s) in replicas.iter().enumerate() {
+            let rows = d.ingest(s, v, &mut arena);
+            clock.extend(rows.clock);
+            ec.extend(rows.ec);
+            vclk.extend(rows.vclk);
+            vval.extend(rows.vval);
+            for _ in 0..rows.def_clock.len() / a {
+                def_row.push(i as u32);
+            }
+            dcl.extend(rows.def_clock);
+            dks.extend(rows.def_keys);
+        }
+        let nd = def_row.len();
+        let def_off: [usize; 2] = [0, nd];
+        let batch = ffi::crdt_map_batch {
+            G: 1, R: r, K: k, A: a, V: v,
+            clock: clock.as_ptr(), clock_rstride: a, clock_gstride: r * a,
+            ec: ec.as_ptr(), ec_rstride: k * a, ec_gstride: r * k * a,
+            vclk: vclk.as_ptr(), vclk_rstride: k * v * a, vclk_gstride: r * k * v * a,
+            vval: vval.as_ptr(), vval_rstride: k * v, vval_gstride: r * k * v,
+            def_off: def_off.as_ptr(), def_row: def_row.as_ptr(), def_clock: dcl.as_ptr(), def_keys: dks.as_ptr(),
+        };
+        // Vout grows until the fold fits (flags bit 0 = some key folded to more values)
+        let mut vout = 4usize;
+        loop {
+            let (mut oc, mut oec) = (vec![0u64; a], vec![0u64; k * a]);
+            let (mut ovc, mut ovv) = (vec![0u64; k * vout * a], vec![0u64; k * vout]);
+            let (mut flags, mut keep, mut okeys) = (vec![0u32; 1], vec![0u8; nd], vec![0u64; nd * kw]);
+            let mut out = ffi::crdt_map_out {
+                Vout: vout, Vstate: 8,
+                clock: oc.as_mut_ptr(), ec: oec.as_mut_ptr(), vclk: ovc.as_mut_ptr(), vval: ovv.as_mut_ptr(),
+                nval: ptr::null_mut(), flags: flags.as_mut_ptr(),
+                def_keep: if nd > 0 { keep.as_mut_ptr() } else { ptr::null_mut() },
+                def_keys: if nd > 0 { okeys.as_mut_ptr() } else { ptr::null_mut() },
+            };
+            ctx.check_host(unsafe { ffi::crdt_map_lub_many(ctx.host, &batch, &mut out) })?;
+            if flags[0] & 1 != 0 && vout < 64 {
+                vout = (vout * 2).min(64);
+                continue;
+            }
+            if flags[0] != 0 {
+                return Err(GpuError { code: ffi::CRDT_EUNSUPPORTED, msg: format!("Map lub_many flags {}", flags[0]) });
+            }
+            let mut surv = Vec::new();
+            for i in 0..nd {
+                if keep[i] != 0 {
+                    surv.push((dcl[i * a..(i + 1) * a].to_vec(), okeys[i * kw..(i + 1) * kw].to_vec()));
+                }
+            }
+            return Ok(d.egress(&oc, &oec, &ovc, &ovv, vout, &surv, &arena));
+        }
+    }
+
+    fn merge_batch(ctx: &GpuCtx, selves: &mut [Self], others: Vec<Self>) -> Result<(), GpuError> {
+        let n = selves.len().min(others.len());
+        if n == 0 {
+            return Ok(());
+        }
+        let d = MapDense::of(selves[..n].iter().chain(others[..n].iter()));
+        let (a, k) = (d.actors.width(), d.keys.width());
+        let kw = (k + 63) / 64;
+        let vo = others[..n].iter().flat_map(|s| s.entries.values().map(|e| e.val.vals.len())).max().unwrap_or(0).max(1);
+        let vs = selves[..n].iter().flat_map(|s| s.entries.values().map(|e| e.val.vals.len())).max().unwrap_or(0).max(1) + vo;
+        let dcap_o = others[..n].iter().map(|s| s.deferred.len()).max().unwrap_or(0).max(1);
+        let dcap_s = selves[..n].iter().map(|s| s.deferred.len()).max().unwrap_or(0).max(1) + dcap_o;
+        if vs > 8 {
+            return Err(GpuError { code: ffi::CRDT_EUNSUPPORTED, msg: "Map merge_batch: more than 8 values per register".into() });
+        }
+        let mut arena = Vec::new();
+        let mut side = |states: &[Self], v: usize, dcap: usize| {
+            let (mut c, mut ec, mut vc, mut vv) = (Vec::new(), Vec::new(), Vec::new(), Vec::new());
+            let (mut dc, mut dk, mut cnt) = (vec![0u64; n * dcap * a], vec![0u64; n * dcap * kw], vec![0u32; n]);
+            for (i, s) in states.iter().enumerate() {
+                let rows = d.ingest(s, v, &mut arena);
+                c.extend(rows.clock);
+                ec.extend(rows.ec);
+                vc.extend(rows.vclk);
+                vv.extend(rows.vval);
+                let nd = rows.def_clock.len() / a;
+                dc[i * dcap * a..i * dcap * a + nd * a].copy_from_slice(&rows.def_clock);
+                dk[i * dcap * kw..i * dcap * kw + nd * kw].copy_from_slice(&rows.def_keys);
+                cnt[i] = nd as u32;
+            }
+            (c, ec, vc, vv, dc, dk, cnt)
+        };
+        let (mut sc, mut sec, mut svc, mut svv, mut sdc, mut sdk, mut scnt) = side(&selves[..n], vs, dcap_s);
+        let (mut oc, mut oec, mut ovc, mut ovv, mut odc, mut odk, mut ocnt) = side(&others[..n], vo, dcap_o);
+        let ss = ffi::crdt_map_states {
+            N: n, K: k, A: a, V: vs,
+            clock: sc.as_mut_ptr(), clock_stride: a, ec: sec.as_mut_ptr(), ec_stride: k * a,
+            vclk: svc.as_mut_ptr(), vclk_stride: k * vs * a, vval: svv.as_mut_ptr(), vval_stride: k * vs,
+        };
+        let sd = ffi::crdt_map_deferred { clock: sdc.as_mut_ptr(), keys: sdk.as_mut_ptr(), count: scnt.as_mut_ptr(), Dcap: dcap_s };
+        let os = ffi::crdt_map_states {
+            N: n, K: k, A: a, V: vo,
+            clock: oc.as_mut_ptr(), clock_stride: a, ec: oec.as_mut_ptr(), ec_stride: k * a,
+            vclk: ovc.as_mut_ptr(), vclk_stride: k * vo * a, vval: ovv.as_mut_ptr(), vval_stride: k * vo,
+        };
+        let od = ffi::crdt_map_deferred { clock: odc.as_mut_ptr(), keys: odk.as_mut_ptr(), count: ocnt.as_mut_ptr(), Dcap: dcap_o };
+        let mut stv = vec![0u32; n];
+        ctx.check_host(unsafe { ffi::crdt_map_merge_batch(ctx.host, &ss, &sd, &os, &od, stv.as_mut_ptr()) })?;
+        for i in 0..n {
+            if stv[i] != 0 {
+                return Err(GpuError { code: ffi::CRDT_EUNSUPPORTED, msg: format!("Map merge_batch status {}", stv[i]) });
+            }
+            let mut defs = Vec::new();
+            for j in 0..scnt[i] as usize {
+                let base = i * dcap_s + j;
+                defs.push((sdc[base * a..(base + 1) * a].to_vec(), sdk[base * kw..(base + 1) * kw].to_vec()));
+            }
+            selves[i] = d.egress(&sc[i * a..(i + 1) * a], &sec[i * k * a..(i + 1) * k * a],
+                                 &svc[i * k * vs * a..(i + 1) * k * vs * a], &svv[i * k * vs..(i + 1) * k * vs], vs,
+                                 &defs, &arena);
         }
         Ok(())
     }
