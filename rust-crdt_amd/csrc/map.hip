@@ -53,6 +53,7 @@ struct MapPlan {
   int spec;           // speculative no-op scan on (tuning / diagnosis knob; results are identical)
   int nt;             // LDS-DMA step images with the non-temporal policy (tuning knob)
   int scan2;          // speculative scan with two actors per 16-byte LDS read (A even)
+  int scan3;          // speculative scan from per-actor thresholds, every LDS read issued first
   // LDS-DMA path: per (group, chunk of C replicas) the max of the chunk's replica clocks,
   // [G][nch][A] (map_chunk_max_kernel), staged with each chunk so a wholly skipped chunk merges
   // its clocks with one compare (the acc clock only ever takes maxima of replica clocks, map.rs:217)
@@ -571,8 +572,99 @@ __device__ __forceinline__ u64 map_noop_steps2(const u64 *buf, unsigned W, unsig
   return (both | only) & G1;
 }
 
+// The same verdict from per-actor thresholds the fold keeps beside the mirror (thr = [TB | TO],
+// A words each, rewritten after every exact step and every skip), with every LDS read of the scan
+// issued before the first compare.  With m1 = (min of the nonzero own value clocks) - 1, or
+// UINT64_MAX when none is nonzero, "sq == 0 | sq > x for every own value" is x <= m1, so
+//   both:  e2 <= max(e, Cs) and (every sq == 0 | sq > deleted)  <=>  e2 <= TB = max(e, min(Cs, m1))
+//          (deleted = e2 > e ? e2 : 0 is <= m1 iff e2 <= e or e2 <= m1)
+//   only:  (e == 0 | e > Co) and (every sq == 0 | sq > ri)       <=>  Co <= TO = e > 0 ? e - 1 : m1
+//          (e > 0: Co < e, then ri = 0; e == 0: ri = Co)
+// (tests/test_map_scan_model.py checks both forms give the same verdict.)  The compares per
+// (step, actor) drop from 5 + 2 NQ + VI NQ + VI to 5 + VI NQ + VI, and none of them waits on an LDS
+// read issued in the same iteration: one wave per SIMD has no other wave to hide that latency.
+template <int VI, int NQ, int LPS, int IT, bool PRESENT>
+__device__ __forceinline__ u64 map_noop_steps3(const u64 *buf, unsigned W, unsigned A, const u64 *me,
+                                               const u64 *mc, const u64 *thr, unsigned n, int lane) {
+  const unsigned st = (unsigned)lane / LPS;
+  const unsigned gq = (unsigned)lane % LPS;
+  const u64 *stp = buf + (st < n ? st : n - 1) * W;
+  constexpr int NQ1 = NQ > 0 ? NQ : 1;
+  u64 e2[IT], tb[IT], co[IT], to[IT], ea[IT], c2[VI][IT], sq[NQ1][IT];
+#pragma unroll
+  for (int m = 0; m < IT; ++m) {
+    const unsigned a0 = gq + LPS * m;
+    const unsigned a = a0 < A ? a0 : A - 1;  // a duplicate actor is neutral (masks only AND / OR)
+    e2[m] = stp[a];
+    tb[m] = thr[a];
+    if constexpr (PRESENT) {
+      co[m] = stp[(1 + VI) * A + a];
+      to[m] = thr[A + a];
+      ea[m] = me[a];
+#pragma unroll
+      for (int t = 0; t < VI; ++t) c2[t][m] = stp[(1 + t) * A + a];
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) sq[q][m] = mc[q * A + a];
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);  // every read above is in flight before the first compare
+  u64 mP2 = 0, mB = ~0ull, mO = ~0ull;
+  u64 mLe2[VI][NQ1], mVan[VI];
+#pragma unroll
+  for (int t = 0; t < VI; ++t) {
+    mVan[t] = ~0ull;
+#pragma unroll
+    for (int q = 0; q < NQ1; ++q) mLe2[t][q] = ~0ull;
+  }
+#pragma unroll
+  for (int m = 0; m < IT; ++m) {
+    mP2 |= __ballot(e2[m] != 0);
+    if constexpr (!PRESENT) {
+      mB &= __ballot(e2[m] <= tb[m]);
+    } else {
+      // e == 0 | e > Co | e == e2  (e - 1 wraps to UINT64_MAX at e == 0)
+      mB &= __ballot((e2[m] <= tb[m]) & ((ea[m] - 1 >= co[m]) | (ea[m] == e2[m])));
+      mO &= __ballot(co[m] <= to[m]);
+      const u64 del = e2[m] > ea[m] ? e2[m] : 0;
+#pragma unroll
+      for (int t = 0; t < VI; ++t) {
+        mVan[t] &= __ballot(c2[t][m] <= del);  // appended, then forgotten to empty
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) mLe2[t][q] &= __ballot(c2[t][m] <= sq[q][m]);
+      }
+    }
+  }
+  const u64 G1 = grp_mask<LPS>();
+  const u64 P2 = orN<LPS>(mP2);
+  if constexpr (!PRESENT) return (~P2 | andN<LPS>(mB)) & G1;
+  u64 both = P2 & andN<LPS>(mB);
+  const u64 only = ~P2 & andN<LPS>(mO);
+#pragma unroll
+  for (int t = 0; t < VI; ++t) {
+    u64 cov = andN<LPS>(mVan[t]);
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) cov |= andN<LPS>(mLe2[t][q]);
+    both &= cov;
+  }
+  return (both | only) & G1;
+}
+
 // Dispatch on (present, number of own values); more than 3 own values: no scan (returns 0 = no
 // step provably a no-op).
+template <int VI, int LPS, int IT, bool PAIR = false>
+__device__ __forceinline__ u64 map_noop_nv3(const u64 *buf, unsigned W, unsigned A, const u64 *mirror,
+                                            const u64 *thr, bool present, int nv, unsigned n, int lane) {
+  const u64 *me = mirror, *mc = mirror + A;
+  if (!present) return map_noop_steps3<VI, 0, LPS, IT, false>(buf, W, A, me, mc, thr, n, lane);
+  switch (nv) {
+    case 0: return map_noop_steps3<VI, 0, LPS, IT, true>(buf, W, A, me, mc, thr, n, lane);
+    case 1: return map_noop_steps3<VI, 1, LPS, IT, true>(buf, W, A, me, mc, thr, n, lane);
+    case 2: return map_noop_steps3<VI, 2, LPS, IT, true>(buf, W, A, me, mc, thr, n, lane);
+    case 3: return map_noop_steps3<VI, 3, LPS, IT, true>(buf, W, A, me, mc, thr, n, lane);
+    default: return 0;
+  }
+}
+
 template <int VI, int LPS, int IT, bool PAIR = false>
 __device__ __forceinline__ u64 map_noop_nv(const u64 *buf, unsigned W, unsigned A, const u64 *mirror,
                                            unsigned VO, bool present, int nv, unsigned n, int lane) {
@@ -673,8 +765,16 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
   u64 *mirror = vbase + NB * C * VI + kMapL;  // (kMapL u64 = the two u32 lists)
   constexpr bool kSpec = APL == 1 && VO <= 4;
   u64 *const cml = mirror + (2 + VO) * A;  // GL: NB staged chunk clock maxima (A words each)
-  if (kSpec)
+  // scan thresholds (map_noop_steps3): TB [A] | TO [A]; m1 = (min nonzero own value clock) - 1
+  u64 *const thr = cml + (GL ? NB * A : 0);
+  u64 m1 = ~0ull;
+  if (kSpec) {
     for (unsigned long long x = lane; x < (2 + VO) * A; x += 64) mirror[x] = 0;
+    for (unsigned long long x = lane; x < A; x += 64) {
+      thr[x] = 0;         // max(e, min(Cs, m1)) with e = Cs = 0
+      thr[A + x] = ~0ull;  // e == 0: m1, no own values
+    }
+  }
 
   // The removes naming this key, in replica order, gathered once into LDS (row, index), so the
   // fold loop never waits on a global load for them (a vector load would drain the prefetched
@@ -793,10 +893,12 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
         if (uni(lim > s)) {
           MAP_TICK();
           const int nv = __builtin_popcount(__builtin_amdgcn_readfirstlane(mv.vm));
-          const u64 noop = p.scan2 ? map_noop_nv<VI, LPS, ITM, true>(buf, (unsigned)WS, (unsigned)A, mirror, VO,
-                                                                      present, nv, (unsigned)n, lane)
-                                   : map_noop_nv<VI, LPS, ITM>(buf, (unsigned)WS, (unsigned)A, mirror, VO, present, nv,
-                                                               (unsigned)n, lane);
+          const u64 noop = p.scan3   ? map_noop_nv3<VI, LPS, ITM>(buf, (unsigned)WS, (unsigned)A, mirror, thr,
+                                                                  present, nv, (unsigned)n, lane)
+                           : p.scan2 ? map_noop_nv<VI, LPS, ITM, true>(buf, (unsigned)WS, (unsigned)A, mirror, VO,
+                                                                        present, nv, (unsigned)n, lane)
+                                     : map_noop_nv<VI, LPS, ITM>(buf, (unsigned)WS, (unsigned)A, mirror, VO, present,
+                                                                 nv, (unsigned)n, lane);
           const u64 from = (s >= NS) ? 0 : (~0ull << (LPS * s));
           const u64 upto = (lim >= NS) ? ~0ull : ((1ull << (LPS * lim)) - 1);
           const u64 stop = ~noop & grp_mask<LPS>() & from & upto;
@@ -819,7 +921,11 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
             }
             if ((unsigned long long)lane < A) cs[0] = mx;
           }
-          if (j > s && (unsigned long long)lane < A) mirror[(1 + VO) * A + lane] = e[0] > cs[0] ? e[0] : cs[0];
+          if (j > s && (unsigned long long)lane < A) {
+            mirror[(1 + VO) * A + lane] = e[0] > cs[0] ? e[0] : cs[0];
+            const u64 lo = cs[0] < m1 ? cs[0] : m1;
+            thr[lane] = e[0] > lo ? e[0] : lo;
+          }
           MAP_TOCK(cy_skip);
           if (j == s) cool = 4;  // the scan found nothing to skip: run a few exact steps first
 #ifdef MAP_STATS
@@ -1044,9 +1150,18 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
           mirror[lane] = e[0];
           mirror[(1 + VO) * A + lane] = e[0] > cs[0] ? e[0] : cs[0];
           int r = 0;  // own value clocks compacted into slots 0..nv-1 (any order)
+          m1 = ~0ull;
 #pragma unroll
           for (int q = 0; q < VO; ++q)
-            if (mv.vm & (1u << q)) mirror[(1 + r++) * A + lane] = mv.c[q][0];
+            if (mv.vm & (1u << q)) {
+              const u64 x = mv.c[q][0];
+              mirror[(1 + r++) * A + lane] = x;
+              const u64 x1 = x != 0 ? x - 1 : ~0ull;
+              m1 = x1 < m1 ? x1 : m1;
+            }
+          const u64 lo = cs[0] < m1 ? cs[0] : m1;
+          thr[lane] = e[0] > lo ? e[0] : lo;
+          thr[A + lane] = e[0] > 0 ? e[0] - 1 : m1;
         }
       }
       MAP_TOCK(cy_exact);
@@ -1139,7 +1254,7 @@ static hipError_t launch_map_it(const MapPlan &p, unsigned long long blocks, hip
   constexpr int C = GL ? CM : MapChunk<APL, VI, CM>::C;
   const size_t W = (2 + VI) * p.A;
   const size_t lds = (size_t)NB * C * (map_ws(W) + VI) * sizeof(u64) + kMapL * 2 * sizeof(unsigned) +
-                     (2 + VO) * p.A * sizeof(u64) + (GL ? NB * p.A * sizeof(u64) : 0);
+                     (2 + VO) * p.A * sizeof(u64) + (GL ? NB * p.A * sizeof(u64) : 0) + 2 * p.A * sizeof(u64);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   if (lds > 64 * 1024) {  // beyond the default dynamic-LDS limit (gfx950 has 160 KB per CU)
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&map_fold_kernel<APL, VI, VO, CM, NB, GL, ITM>),
@@ -1253,6 +1368,7 @@ extern "C" int crdt_map_lub_many(crdt_ctx *ctx, const crdt_map_batch *in, crdt_m
   p.spec = ctx->tune.map_spec;
   p.nt = ctx->tune.map_nt;
   p.scan2 = ctx->tune.map_scan2 && A % 2 == 0;
+  p.scan3 = ctx->tune.map_scan3;
   if (int rc = device_fill(ctx, out->flags, G * sizeof(unsigned), 0)) return rc;
   // LDS-DMA staging when every step image is whole 16-byte pieces (A even, 16-byte aligned
   // rows and strides) and the state fits 4 values; register staging otherwise

@@ -38,6 +38,35 @@ def _noop_test(present, e, vals, e2, v2, Cs, Co):
     return True
 
 
+U64MAX = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+def _noop_test_thr(present, e, vals, e2, v2, Cs, Co):
+    """map_noop_steps3's form of the same test: per-actor thresholds TB = max(e, min(Cs, m1)) and
+    TO = e > 0 ? e - 1 : m1, m1 = (min of the nonzero own value clocks) - 1 or UINT64_MAX."""
+    p2 = bool(e2.any())
+    m1 = np.full(e.shape, U64MAX)
+    for c, _ in vals:
+        m1 = np.minimum(m1, np.where(c != 0, c - np.uint64(1), U64MAX))
+    TB = np.maximum(e, np.minimum(Cs, m1))
+    if not present:
+        return (not p2) or bool(np.all(e2 <= TB))
+    if any(O._lt(c, c2) for c, _ in vals for c2, _ in vals):
+        return None
+    with np.errstate(over="ignore"):
+        TO = np.where(e > 0, e - np.uint64(1), m1)
+        em1 = e - np.uint64(1)  # wraps to UINT64_MAX at e == 0
+    if not p2:
+        return bool(np.all(Co <= TO))
+    if not np.all((e2 <= TB) & ((em1 >= Co) | (e == e2))):
+        return False
+    dl = np.where(e2 > e, e2, z)
+    for t, _ in v2:
+        if not (any(np.all(t <= c) for c, _ in vals) or np.all(t <= dl)):
+            return False
+    return True
+
+
 def _join(present, e, vals, e2, v2, Cs, Co, A):
     """The entry join of one step (oracle.dense_map_fold steps 1, map.rs:142-210)."""
     p2 = bool(e2.any())
@@ -76,6 +105,7 @@ def _check_fold(d):
             e2 = ec[i, k]
             v2 = [(vclk[i, k, s].copy(), int(vval[i, k, s])) for s in range(V) if vclk[i, k, s].any()]
             verdict = _noop_test(present, e, vals, e2, v2, Cs, Co)
+            assert _noop_test_thr(present, e, vals, e2, v2, Cs, Co) == verdict, f"key {k} step {i}: threshold form differs"
             np_, ne, nv = _join(present, e, vals, e2, v2, Cs, Co, A)
             if verdict:
                 n_noop += 1
@@ -130,3 +160,21 @@ def test_scan_sound_synthetic():
     d.update(def_row=dfr[0], def_clock=dfr[1], def_keys=dfr[2])
     n = _check_fold(d)
     assert n > R * K // 2
+
+
+@pytest.mark.parametrize("seed", range(20))
+def test_threshold_form_edges(seed):
+    """The threshold form on counters at 0, 1 and UINT64_MAX (the wrap cases of e - 1 and m1)."""
+    rng = np.random.default_rng(7000 + seed)
+    pool = np.array([0, 1, 2, 3, 0xFFFFFFFFFFFFFFFE, 0xFFFFFFFFFFFFFFFF], np.uint64)
+    for _ in range(300):
+        A = int(rng.integers(1, 5))
+        pick = lambda: pool[rng.integers(0, len(pool), size=A)]  # noqa: E731
+        e, e2, Cs, Co = pick(), pick(), pick(), pick()
+        if rng.random() < 0.3:
+            e2[:] = 0
+        present = bool(e.any())
+        nv = int(rng.integers(0, 3)) if present else 0
+        vals = [(pick(), 0) for _ in range(nv)]
+        v2 = [(pick(), 0) for _ in range(int(rng.integers(0, 3)))] if e2.any() else []
+        assert _noop_test_thr(present, e, vals, e2, v2, Cs, Co) == _noop_test(present, e, vals, e2, v2, Cs, Co)
