@@ -62,6 +62,7 @@ struct Tune {
   int map_nt = 0;      // ... non-temporal policy on the LDS-DMA step images
   int map_scan2 = 0;   // ... scan two actors per 16-byte LDS read (even A; measured no faster)
   int map_scan3 = 1;   // ... scan from per-actor thresholds with every LDS read issued first
+  int map_rs = 1;      // ... register-staged whole-chunk skip (A <= 32 on the LDS-DMA shapes)
   int rows_blocks_per_cu = 0;  // row-pair / row-reduction kernels (causal.hip); 0 = per-kernel default
   int apply_hot_slots = 8;     // Orswot apply: deferred slots kept in LDS per state (the rest in HBM)
   int map_forget_vec2 = 1;     // Map forget: 16-byte pieces per lane where the shape allows it

@@ -210,6 +210,7 @@ static void apply_tune(crdt_ctx *ctx, const char *t) {
       else if (k == "mnt") ctx->tune.map_nt = v != 0;
       else if (k == "mscan2") ctx->tune.map_scan2 = v != 0;
       else if (k == "mscan3") ctx->tune.map_scan3 = v != 0;
+      else if (k == "mrs") ctx->tune.map_rs = v != 0;
       else if (k == "rbpc" && v > 0) ctx->tune.rows_blocks_per_cu = v;
       else if (k == "hot" && v >= 0 && v <= 64) ctx->tune.apply_hot_slots = v;
       else if (k == "mfv2") ctx->tune.map_forget_vec2 = v != 0;

@@ -590,10 +590,22 @@ __device__ __forceinline__ u64 map_noop_steps3(const u64 *buf, unsigned W, unsig
   const unsigned gq = (unsigned)lane % LPS;
   const u64 *stp = buf + (st < n ? st : n - 1) * W;
   constexpr int NQ1 = NQ > 0 ? NQ : 1;
-  u64 e2[IT], tb[IT], co[IT], to[IT], ea[IT], c2[VI][IT], sq[NQ1][IT];
+  // batches of IB iterations (all of them up to 8; 4 at a time beyond, so the loads in flight fit)
+  constexpr int IB = IT <= 8 ? IT : 4;
+  u64 mP2 = 0, mB = ~0ull, mO = ~0ull;
+  u64 mLe2[VI][NQ1], mVan[VI];
 #pragma unroll
-  for (int m = 0; m < IT; ++m) {
-    const unsigned a0 = gq + LPS * m;
+  for (int t = 0; t < VI; ++t) {
+    mVan[t] = ~0ull;
+#pragma unroll
+    for (int q = 0; q < NQ1; ++q) mLe2[t][q] = ~0ull;
+  }
+#pragma unroll
+  for (int b = 0; b < IT; b += IB) {
+  u64 e2[IB], tb[IB], co[IB], to[IB], ea[IB], c2[VI][IB], sq[NQ1][IB];
+#pragma unroll
+  for (int m = 0; m < IB; ++m) {
+    const unsigned a0 = gq + LPS * (b + m);
     const unsigned a = a0 < A ? a0 : A - 1;  // a duplicate actor is neutral (masks only AND / OR)
     e2[m] = stp[a];
     tb[m] = thr[a];
@@ -608,16 +620,8 @@ __device__ __forceinline__ u64 map_noop_steps3(const u64 *buf, unsigned W, unsig
     }
   }
   __builtin_amdgcn_sched_barrier(0);  // every read above is in flight before the first compare
-  u64 mP2 = 0, mB = ~0ull, mO = ~0ull;
-  u64 mLe2[VI][NQ1], mVan[VI];
 #pragma unroll
-  for (int t = 0; t < VI; ++t) {
-    mVan[t] = ~0ull;
-#pragma unroll
-    for (int q = 0; q < NQ1; ++q) mLe2[t][q] = ~0ull;
-  }
-#pragma unroll
-  for (int m = 0; m < IT; ++m) {
+  for (int m = 0; m < IB; ++m) {
     mP2 |= __ballot(e2[m] != 0);
     if constexpr (!PRESENT) {
       mB &= __ballot(e2[m] <= tb[m]);
@@ -633,6 +637,7 @@ __device__ __forceinline__ u64 map_noop_steps3(const u64 *buf, unsigned W, unsig
         for (int q = 0; q < NQ; ++q) mLe2[t][q] &= __ballot(c2[t][m] <= sq[q][m]);
       }
     }
+  }
   }
   const u64 G1 = grp_mask<LPS>();
   const u64 P2 = orN<LPS>(mP2);
@@ -701,10 +706,237 @@ __device__ __forceinline__ bool mv_antichain(const MVState<APL, VO> &s) {
   return ok;
 }
 
+// ---- Register-staged whole-chunk skip (RS path, A <= 32 even, 16-replica chunks) --------------
+// Almost every 16-replica chunk of a long fold changes nothing for a key.  The RS path loads each
+// chunk straight into registers in the scan's own layout — lane (s, gq) = (lane / 4, lane % 4)
+// holds step s, actor pairs (2gq + 8m, 2gq + 8m + 1), m < NP — one chunk ahead of the one it
+// tests; the fold state's scan operands (entry clock, TB, TO, own value clocks) are read from the
+// LDS mirror in the same layout while the chunk is in flight.  A chunk whose 16 steps the test
+// proves no-ops costs one register scan and a clock max (lane = actor, from the chunk's clock max),
+// with no LDS-DMA issue and no step image in LDS; any other chunk (a failed test, a remove naming
+// the key, the scan's preconditions off) is written to LDS slot 0 and runs through the exact
+// per-step loop; the ring is drained first and restarted after it, so no chunk register is live
+// across the exact loop.
+template <int VI, int NP>
+struct RsChunk {
+  u64x2 e[NP];
+  u64x2 c[VI][NP];
+  u64x2 co[NP];
+  u64 cm;     // the chunk's clock max of actor `lane` (map_chunk_max_kernel)
+  u64 v[VI];  // the VI values of step s
+};
+
+template <int NQ, int NP>
+struct RsOwn {
+  u64x2 ea[NP], tb[NP], to[NP];
+  u64x2 sq[NQ > 0 ? NQ : 1][NP];
+};
+
+// The scan operands of the fold state from the LDS mirror (me / mc) and thresholds (TB / TO).
+template <int NQ, bool PRESENT, int NP>
+__device__ __forceinline__ RsOwn<NQ, NP> rs_own(const u64 *mirror, const u64 *thr, unsigned long long A, int lane) {
+  RsOwn<NQ, NP> o;
+  const unsigned gq = (unsigned)lane & 3;
+#pragma unroll
+  for (int m = 0; m < NP; ++m) {
+    const unsigned a0 = 2 * gq + 8 * m;
+    const unsigned long long a = a0 < A ? a0 : A - 2;
+    o.tb[m] = lds2(thr + a);
+    if constexpr (PRESENT) {
+      o.ea[m] = lds2(mirror + a);
+      o.to[m] = lds2(thr + A + a);
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) o.sq[q][m] = lds2(mirror + (1 + q) * A + a);
+    }
+  }
+  return o;
+}
+
+// Per-lane element pointers of step s of chunk 0 and the per-chunk byte advances.
+struct RsLanes {
+  const char *e0, *c0, *o0, *v0;
+  unsigned long long se, sc, so, sv;  // row strides in bytes
+};
+
+__device__ __forceinline__ u64x2 ld16nt(const char *p) {
+  return __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(p));
+}
+__device__ __forceinline__ u64x2 ld16(const char *p) { return *reinterpret_cast<const u64x2 *>(p); }
+
+// Exactly NP*(2+VI) + 1 + VI loads per lane, unpredicated, so a fixed vmcnt count retires a chunk.
+// Steps past iend re-load step iend-1 (never tested: the verdict is masked to the chunk's steps);
+// a chunk past the last one re-loads the last (the ring issues a fixed number of chunks, so every
+// ring register is written on every path and none is live across the exact loop).
+template <int VI, int NP>
+__device__ __forceinline__ void rs_load(RsChunk<VI, NP> &r, const MapPlan &p, const RsLanes &L,
+                                        unsigned long long g, unsigned long long ch, unsigned long long iend,
+                                        int lane) {
+  constexpr unsigned long long C = 16;
+  ch = ch < p.nch ? ch : p.nch - 1;
+  const unsigned long long s = (unsigned)lane >> 2;
+  const unsigned long long i = ch * C + s < iend ? ch * C + s : iend - 1;
+  const unsigned gq = (unsigned)lane & 3;
+  const unsigned long long A = p.A;
+#pragma unroll
+  for (int m = 0; m < NP; ++m) {
+    const unsigned a0 = 2 * gq + 8 * m;
+    const unsigned long long a = a0 < A ? a0 : A - 2;  // a duplicate pair is neutral
+    r.e[m] = ld16nt(L.e0 + i * L.se + a * 8);
+#pragma unroll
+    for (int t = 0; t < VI; ++t) r.c[t][m] = ld16nt(L.c0 + i * L.sc + (t * A + a) * 8);
+    r.co[m] = ld16(L.o0 + i * L.so + a * 8);
+  }
+  r.cm = p.cmax[(g * p.nch + ch) * A + ((unsigned long long)lane < A ? lane : A - 1)];
+#pragma unroll
+  for (int t = 0; t < VI; ++t)
+    r.v[t] = __builtin_nontemporal_load(reinterpret_cast<const u64 *>(L.v0 + i * L.sv) + t);
+}
+
+// The no-op verdict of map_noop_steps3 on the register chunk (bit 4s: step s provably a no-op).
+template <int VI, int NP, int NQ, bool PRESENT>
+__device__ __forceinline__ u64 rs_noop(const RsChunk<VI, NP> &r, const RsOwn<NQ, NP> &o) {
+  constexpr int LPS = 4;
+  constexpr int NQ1 = NQ > 0 ? NQ : 1;
+  bool p2 = false, bB = true, bO = true, van[VI], le[VI][NQ1];
+#pragma unroll
+  for (int t = 0; t < VI; ++t) {
+    van[t] = true;
+#pragma unroll
+    for (int q = 0; q < NQ1; ++q) le[t][q] = true;
+  }
+#pragma unroll
+  for (int m = 0; m < NP; ++m) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const u64 e2 = r.e[m][h], tb = o.tb[m][h];
+      p2 |= e2 != 0;
+      if constexpr (!PRESENT) {
+        bB &= e2 <= tb;
+      } else {
+        const u64 co = r.co[m][h], ea = o.ea[m][h];
+        bB &= (e2 <= tb) & ((ea - 1 >= co) | (ea == e2));
+        bO &= co <= o.to[m][h];
+        const u64 del = e2 > ea ? e2 : 0;
+#pragma unroll
+        for (int t = 0; t < VI; ++t) {
+          const u64 c2 = r.c[t][m][h];
+          van[t] &= c2 <= del;
+#pragma unroll
+          for (int q = 0; q < NQ; ++q) le[t][q] &= c2 <= o.sq[q][m][h];
+        }
+      }
+    }
+  }
+  const u64 G1 = grp_mask<LPS>();
+  const u64 P2 = orN<LPS>(__ballot(p2));
+  if constexpr (!PRESENT) return (~P2 | andN<LPS>(__ballot(bB))) & G1;
+  u64 both = P2 & andN<LPS>(__ballot(bB));
+  const u64 only = ~P2 & andN<LPS>(__ballot(bO));
+#pragma unroll
+  for (int t = 0; t < VI; ++t) {
+    u64 cov = andN<LPS>(__ballot(van[t]));
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) cov |= andN<LPS>(__ballot(le[t][q]));
+    both &= cov;
+  }
+  return (both | only) & G1;
+}
+
+// Own operands read (LDS) before the chunk's global loads are waited for, then the verdict.
+// (the wait keeps the LD most recent loads — the chunks behind this one — in flight)
+template <int VI, int NP, int NQ, bool PRESENT, int LD>
+__device__ __forceinline__ u64 rs_wait_noop(const RsChunk<VI, NP> &r, const u64 *mirror, const u64 *thr,
+                                            unsigned long long A, int lane) {
+  const RsOwn<NQ, NP> o = rs_own<NQ, PRESENT, NP>(mirror, thr, A, lane);
+  wait_vmcnt<LD>();
+  return rs_noop<VI, NP, NQ, PRESENT>(r, o);
+}
+template <int VI, int NP, int LD>
+__device__ __forceinline__ u64 rs_wait_noop_nv(const RsChunk<VI, NP> &r, const u64 *mirror, const u64 *thr,
+                                               unsigned long long A, bool present, int nv, int lane) {
+  if (!present) return rs_wait_noop<VI, NP, 0, false, LD>(r, mirror, thr, A, lane);
+  switch (nv) {
+    case 0: return rs_wait_noop<VI, NP, 0, true, LD>(r, mirror, thr, A, lane);
+    case 1: return rs_wait_noop<VI, NP, 1, true, LD>(r, mirror, thr, A, lane);
+    case 2: return rs_wait_noop<VI, NP, 2, true, LD>(r, mirror, thr, A, lane);
+    case 3: return rs_wait_noop<VI, NP, 3, true, LD>(r, mirror, thr, A, lane);
+    default:
+      wait_vmcnt<LD>();
+      return 0;
+  }
+}
+
+template <int VI, int NP>
+__device__ __forceinline__ void rs_reload(RsChunk<VI, NP> &r, const u64 *img, unsigned long long WS, const u64 *vals,
+                                          const u64 *cm, unsigned long long A, int lane) {
+  const unsigned s = (unsigned)lane >> 2, gq = (unsigned)lane & 3;
+  const u64 *st = img + s * WS;
+#pragma unroll
+  for (int m = 0; m < NP; ++m) {
+    const unsigned a0 = 2 * gq + 8 * m;
+    const unsigned long long a = a0 < A ? a0 : A - 2;
+    r.e[m] = lds2(st + a);
+#pragma unroll
+    for (int t = 0; t < VI; ++t) r.c[t][m] = lds2(st + (1 + t) * A + a);
+    r.co[m] = lds2(st + (1 + VI) * A + a);
+  }
+  r.cm = cm[(unsigned long long)lane < A ? lane : A - 1];
+#pragma unroll
+  for (int t = 0; t < VI; ++t) r.v[t] = vals[s * VI + t];
+}
+
+// The same test on a chunk handed to the exact loop (LDS slot 0, the step images rs_store wrote),
+// against the fold state after its exact steps: the RS kernel's only scan, so the exact loop holds
+// no scan of its own.
+template <int VI, int NP>
+__device__ __forceinline__ u64 rs_lds_noop_nv(const u64 *img, unsigned long long WS, const u64 *mirror,
+                                              const u64 *thr, unsigned long long A, bool present, int nv,
+                                              int lane) {
+  RsChunk<VI, NP> r;
+  const unsigned s = (unsigned)lane >> 2, gq = (unsigned)lane & 3;
+  const u64 *st = img + s * WS;
+#pragma unroll
+  for (int m = 0; m < NP; ++m) {
+    const unsigned a0 = 2 * gq + 8 * m;
+    const unsigned long long a = a0 < A ? a0 : A - 2;
+    r.e[m] = lds2(st + a);
+#pragma unroll
+    for (int t = 0; t < VI; ++t) r.c[t][m] = lds2(st + (1 + t) * A + a);
+    r.co[m] = lds2(st + (1 + VI) * A + a);
+  }
+  r.cm = 0;
+#pragma unroll
+  for (int t = 0; t < VI; ++t) r.v[t] = 0;
+  return rs_wait_noop_nv<VI, NP, 63>(r, mirror, thr, A, present, nv, lane);  // (no global load to wait for)
+}
+
+// A chunk the register test could not skip: its step images, values and clock max into LDS slot 0
+// in the layout the exact loop reads (map_step_read, the LDS scans, cml).
+template <int VI, int NP>
+__device__ __forceinline__ void rs_store(const RsChunk<VI, NP> &r, u64 *img, unsigned long long WS, u64 *vals,
+                                         u64 *cm, unsigned long long A, int lane) {
+  const unsigned s = (unsigned)lane >> 2, gq = (unsigned)lane & 3;
+  u64 *st = img + s * WS;
+#pragma unroll
+  for (int m = 0; m < NP; ++m) {
+    const unsigned a0 = 2 * gq + 8 * m;
+    const unsigned long long a = a0 < A ? a0 : A - 2;
+    *reinterpret_cast<u64x2 *>(st + a) = r.e[m];
+#pragma unroll
+    for (int t = 0; t < VI; ++t) *reinterpret_cast<u64x2 *>(st + (1 + t) * A + a) = r.c[t][m];
+    *reinterpret_cast<u64x2 *>(st + (1 + VI) * A + a) = r.co[m];
+  }
+  if ((unsigned long long)lane < A) cm[lane] = r.cm;
+  if (gq == 0)
+#pragma unroll
+    for (int t = 0; t < VI; ++t) vals[s * VI + t] = r.v[t];
+}
+
 // ITM: unrolled scan iterations ceil(A / LPS) rounded up to a power of two, fixed per launch so
-// each kernel's register allocation only covers its own scan shape.
-template <int APL, int VI, int VO, int CM, int NB, bool GL, int ITM>
+// each kernel's register allocation only covers its own scan shape.  NP > 0: the RS path (above).
+template <int APL, int VI, int VO, int CM, int NB, bool GL, int ITM, int NP = 0>
 __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
+  constexpr bool RS = NP > 0;
   const MapPlan p = pk;  // a local copy the optimizer can split into registers (the by-value
                          // kernel argument itself would be materialized in scratch memory)
   const unsigned long long g = blockIdx.x / p.K;
@@ -746,9 +978,10 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
   const u64 kbit = 1ull << (k % 64);
 
   extern __shared__ u64 map_lds[];
-  constexpr int C = GL ? CM : MapChunk<APL, VI, CM>::C;
+  constexpr int C = (GL || RS) ? CM : MapChunk<APL, VI, CM>::C;
   static_assert(!GL || (APL == 1 && NB >= 2), "LDS-DMA staging: one actor per lane");
-  static_assert(GL || NB == 2, "register staging double-buffers");
+  static_assert(GL || RS || NB == 2, "register staging double-buffers");
+  static_assert(!RS || (APL == 1 && !GL && NB == 2 && CM == 16 && VO <= 4 && VI <= 2), "RS path shape");
   // speculative scan geometry: NS >= C steps per scan, LPS lanes per step
   constexpr int NS = C > 8 ? 16 : (C > 4 ? 8 : (C > 2 ? 4 : 2));
   constexpr int LPS = 64 / NS;
@@ -765,8 +998,8 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
   u64 *mirror = vbase + NB * C * VI + kMapL;  // (kMapL u64 = the two u32 lists)
   constexpr bool kSpec = APL == 1 && VO <= 4;
   u64 *const cml = mirror + (2 + VO) * A;  // GL: NB staged chunk clock maxima (A words each)
-  // scan thresholds (map_noop_steps3): TB [A] | TO [A]; m1 = (min nonzero own value clock) - 1
-  u64 *const thr = cml + (GL ? NB * A : 0);
+  // scan thresholds (map_noop_steps3, RS): TB [A] | TO [A]; m1 = (min nonzero own value clock) - 1
+  u64 *const thr = cml + ((GL || RS) ? NB * A : 0);
   u64 m1 = ~0ull;
   if (kSpec) {
     for (unsigned long long x = lane; x < (2 + VO) * A; x += 64) mirror[x] = 0;
@@ -821,7 +1054,20 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
 #define MAP_TOCK(acc) ((void)0)
 #endif
   // chunk staging
-  MapChunk<APL, VI, (GL ? 2 : CM)> regs;
+  MapChunk<APL, VI, ((GL || RS) ? 2 : CM)> regs;
+  RsChunk<VI, (RS ? NP : 1)> rA, rB;
+  RsLanes rl;
+  if constexpr (RS) {
+    rl.e0 = reinterpret_cast<const char *>(p.ec + g * p.e_gs + k * A);
+    rl.c0 = reinterpret_cast<const char *>(p.vclk + g * p.vc_gs + k * VI * A);
+    rl.o0 = reinterpret_cast<const char *>(p.clock + g * p.c_gs);
+    rl.v0 = reinterpret_cast<const char *>(p.vval + g * p.vv_gs + k * VI);
+    rl.se = (unsigned long long)p.e_rs * 8;
+    rl.sc = (unsigned long long)p.vc_rs * 8;
+    rl.so = (unsigned long long)p.c_rs * 8;
+    rl.sv = (unsigned long long)p.vv_rs * 8;
+    rs_load(rA, p, rl, g, 0, R, lane);  // (R > 0 here)
+  }
   const int ni = GL ? (int)((W + 127) / 128) : 0;  // 1-KiB pieces per step image (GL: 1 or 2)
   GldsLanes<1> gl1;
   GldsLanes<2> gl2;
@@ -836,7 +1082,7 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
         map_chunk_glds<VI, C, 2>(p, gl2, g, k, c * C, R, map_lds + c * C * WS, WS, vbase + c * C * VI, cml + c * A, lane);
       }
     }
-  } else {
+  } else if constexpr (!RS) {
     if (nch > 0) {
       map_chunk_load(regs, p, g, k, 0, R, lane);
       map_chunk_store(regs, map_lds, vbase, A, WS, R < (unsigned long long)C ? R : C, lane);
@@ -845,9 +1091,66 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
   }
 
   for (unsigned long long ch = 0; ch < nch; ++ch) {
-    const unsigned slot = (unsigned)(ch % NB);
+    // (RS: slot 0 holds the chunk handed to the exact loop)
+    const unsigned slot = RS ? 0u : (unsigned)(ch % NB);
     const u64 *buf = map_lds + slot * C * WS;
     const u64 *vb = vbase + slot * C * VI;
+    if constexpr (RS) {
+      // Whole-chunk skip in registers: chunk ch is in rA (ch even) or rB (ch odd), landed or in
+      // flight; chunk ch+1 is issued into the other set before chunk ch is waited for.  A chunk
+      // that is not skipped goes to LDS slot 0 and the one behind it to slot 1, so neither register
+      // set is live across the exact loop (both are re-read from slot 1 after it).
+      constexpr int LD = NP * (2 + VI) + 1 + VI;  // loads per rs_load
+      const bool elig0 = uni(p.spec && cool == 0 && anti && !slow && !direct);
+      const int nv = __builtin_popcount(__builtin_amdgcn_readfirstlane(mv.vm));
+      const unsigned long long n0 = R - ch * C < (unsigned long long)C ? R - ch * C : C;
+      const u64 want = n0 >= 16 ? grp_mask<4>() : (grp_mask<4>() & ((1ull << (4 * n0)) - 1));
+      const bool el = elig0 && (unsigned long long)next_row >= ch * C + n0;
+      bool skip;
+      MAP_TICK();
+      if (ch & 1) {
+        rs_load(rA, p, rl, g, ch + 1, R, lane);
+        u64 noop = 0;
+        if (el) noop = rs_wait_noop_nv<VI, NP, LD>(rB, mirror, thr, A, present, nv, lane);
+        else wait_vmcnt<LD>();
+        skip = el && (noop & want) == want;
+        if (skip) {
+          if ((unsigned long long)lane < A) cs[0] = cs[0] > rB.cm ? cs[0] : rB.cm;
+        } else {
+          wait_vmcnt<0>();
+          rs_store(rB, map_lds, WS, vbase, cml, A, lane);
+          rs_store(rA, map_lds + C * WS, WS, vbase + C * VI, cml + A, A, lane);
+        }
+      } else {
+        rs_load(rB, p, rl, g, ch + 1, R, lane);
+        u64 noop = 0;
+        if (el) noop = rs_wait_noop_nv<VI, NP, LD>(rA, mirror, thr, A, present, nv, lane);
+        else wait_vmcnt<LD>();
+        skip = el && (noop & want) == want;
+        if (skip) {
+          if ((unsigned long long)lane < A) cs[0] = cs[0] > rA.cm ? cs[0] : rA.cm;
+        } else {
+          wait_vmcnt<0>();
+          rs_store(rA, map_lds, WS, vbase, cml, A, lane);
+          rs_store(rB, map_lds + C * WS, WS, vbase + C * VI, cml + A, A, lane);
+        }
+      }
+      MAP_TOCK(cy_scan);
+#ifdef MAP_STATS
+      ++st_scan;
+      if (!skip) ++st_fail;
+#endif
+      if (skip) {
+        // TB for the next chunk's test
+        if ((unsigned long long)lane < A) {
+          const u64 lo = cs[0] < m1 ? cs[0] : m1;
+          thr[lane] = e[0] > lo ? e[0] : lo;
+        }
+        continue;
+      }
+      // the round-1 scan of the exact loop reads max(e, Cs) from the mirror
+      if ((unsigned long long)lane < A) mirror[(1 + VO) * A + lane] = e[0] > cs[0] ? e[0] : cs[0];
+    }
     if constexpr (GL) {
       // issue chunk ch+NB-1 into the slot chunk ch-1 used, then wait for chunk ch
       const unsigned long long nx = ch + NB - 1;
@@ -893,7 +1196,13 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
         if (uni(lim > s)) {
           MAP_TICK();
           const int nv = __builtin_popcount(__builtin_amdgcn_readfirstlane(mv.vm));
-          const u64 noop = p.scan3   ? map_noop_nv3<VI, LPS, ITM>(buf, (unsigned)WS, (unsigned)A, mirror, thr,
+          // (the RS path and register staging keep the round-1 scan: the threshold scan's loads in
+          // flight would not fit beside their chunk registers)
+          u64 noop;
+          if constexpr (RS)
+            noop = rs_lds_noop_nv<VI, (RS ? NP : 1)>(buf, WS, mirror, thr, A, present, nv, lane);
+          else
+            noop = (p.scan3 && GL) ? map_noop_nv3<VI, LPS, ITM>(buf, (unsigned)WS, (unsigned)A, mirror, thr,
                                                                   present, nv, (unsigned)n, lane)
                            : p.scan2 ? map_noop_nv<VI, LPS, ITM, true>(buf, (unsigned)WS, (unsigned)A, mirror, VO,
                                                                         present, nv, (unsigned)n, lane)
@@ -905,7 +1214,7 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
           j = stop ? (unsigned long long)(__builtin_ctzll(stop) / LPS) : lim;
           MAP_TOCK(cy_scan);
           MAP_TICK();
-          if (GL && s == 0 && j == n) {  // the whole chunk: its staged clock max
+          if ((GL || RS) && s == 0 && j == n) {  // the whole chunk: its staged clock max
             const unsigned long long a = (unsigned long long)lane < A ? lane : A - 1;
             const u64 x = cml[slot * A + a];
             if ((unsigned long long)lane < A) cs[0] = cs[0] > x ? cs[0] : x;
@@ -1166,7 +1475,12 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
       }
       MAP_TOCK(cy_exact);
     }
-    if constexpr (!GL) {
+    if constexpr (RS) {
+      // chunk ch+1 back from slot 1 into both sets (whichever parity comes next)
+      rs_reload(rA, map_lds + C * WS, WS, vbase + C * VI, cml + A, A, lane);
+      rs_reload(rB, map_lds + C * WS, WS, vbase + C * VI, cml + A, A, lane);
+    }
+    if constexpr (!GL && !RS) {
       if (ch + 1 < nch) {  // stage the next chunk (its loads were issued a whole chunk ago)
         const unsigned long long nn = R - (ch + 1) * C < (unsigned long long)C ? R - (ch + 1) * C : C;
         const unsigned ns = (unsigned)((ch + 1) % NB);
@@ -1249,20 +1563,31 @@ __global__ __launch_bounds__(64) void map_chunk_max_kernel(const u64 *clock, lon
   }
 }
 
-template <int APL, int VI, int VO, int CM, int NB, bool GL, int ITM>
+template <int APL, int VI, int VO, int CM, int NB, bool GL, int ITM, int NP = 0>
 static hipError_t launch_map_it(const MapPlan &p, unsigned long long blocks, hipStream_t s) {
-  constexpr int C = GL ? CM : MapChunk<APL, VI, CM>::C;
+  constexpr bool RS = NP > 0;
+  constexpr int C = (GL || RS) ? CM : MapChunk<APL, VI, CM>::C;
   const size_t W = (2 + VI) * p.A;
   const size_t lds = (size_t)NB * C * (map_ws(W) + VI) * sizeof(u64) + kMapL * 2 * sizeof(unsigned) +
-                     (2 + VO) * p.A * sizeof(u64) + (GL ? NB * p.A * sizeof(u64) : 0) + 2 * p.A * sizeof(u64);
+                     (2 + VO) * p.A * sizeof(u64) + ((GL || RS) ? NB * p.A * sizeof(u64) : 0) +
+                     2 * p.A * sizeof(u64);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   if (lds > 64 * 1024) {  // beyond the default dynamic-LDS limit (gfx950 has 160 KB per CU)
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&map_fold_kernel<APL, VI, VO, CM, NB, GL, ITM>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&map_fold_kernel<APL, VI, VO, CM, NB, GL, ITM, NP>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL((map_fold_kernel<APL, VI, VO, CM, NB, GL, ITM>), dim3((unsigned)blocks), dim3(64), lds, s, p);
+  hipLaunchKernelGGL((map_fold_kernel<APL, VI, VO, CM, NB, GL, ITM, NP>), dim3((unsigned)blocks), dim3(64), lds, s, p);
   return hipGetLastError();
+}
+
+// RS path (A <= 32 even, V <= 2, 16-replica chunks): NP actor pairs per lane, LPS = 4 scan lanes per
+// step so the LDS scans of the exact loop unroll ceil(A / 4) iterations.
+template <int VI>
+static hipError_t launch_map_rs(const MapPlan &p, unsigned long long blocks, hipStream_t s) {
+  if (p.A <= 8) return launch_map_it<1, VI, 4, 16, 2, false, 2, 1>(p, blocks, s);
+  if (p.A <= 16) return launch_map_it<1, VI, 4, 16, 2, false, 4, 2>(p, blocks, s);
+  return launch_map_it<1, VI, 4, 16, 2, false, 8, 4>(p, blocks, s);
 }
 
 // Scan shape: NS steps per scan (C rounded up to a power of two, <= 16), LPS = 64 / NS lanes per
@@ -1376,7 +1701,9 @@ extern "C" int crdt_map_lub_many(crdt_ctx *ctx, const crdt_map_batch *in, crdt_m
   const bool glds = ctx->tune.map_glds && R > 0 && A <= 64 && (A & 1) == 0 && (V == 1 || V == 2) &&
                     want <= 4 && even && aligned16(p.clock) && aligned16(p.ec) && aligned16(p.vclk) &&
                     G * ((R + 7) / 8) < 0x7fffffffULL;
-  const unsigned gC = (ctx->tune.map_chunk == 8 && ctx->tune.map_ring == 4) ? 8 : 16;  // launch_map_glds
+  // the RS path: register-staged whole-chunk skip, LDS only for chunks it cannot skip
+  const bool rs = glds && ctx->tune.map_rs && A <= 32;
+  const unsigned gC = (!rs && ctx->tune.map_chunk == 8 && ctx->tune.map_ring == 4) ? 8 : 16;  // launch_map_glds
   // scratch: [def_off copy | chunk clock maxima]
   const size_t off_b = D > 0 ? ((G + 1) * sizeof(size_t) + 255) / 256 * 256 : 0;
   if (glds) p.nch = (R + gC - 1) / gC;
@@ -1399,8 +1726,11 @@ extern "C" int crdt_map_lub_many(crdt_ctx *ctx, const crdt_map_batch *in, crdt_m
     p.cmax = cm;
     hipLaunchKernelGGL(map_chunk_max_kernel, dim3((unsigned)(G * p.nch)), dim3(64), 0, ctx->stream, p.clock,
                        p.c_rs, p.c_gs, (unsigned long long)R, (unsigned long long)A, p.nch, gC, cm);
-    he = V == 1 ? launch_map_glds<1>(p, ctx->tune.map_chunk, ctx->tune.map_ring, blocks, ctx->stream)
-                : launch_map_glds<2>(p, ctx->tune.map_chunk, ctx->tune.map_ring, blocks, ctx->stream);
+    if (rs)
+      he = V == 1 ? launch_map_rs<1>(p, blocks, ctx->stream) : launch_map_rs<2>(p, blocks, ctx->stream);
+    else
+      he = V == 1 ? launch_map_glds<1>(p, ctx->tune.map_chunk, ctx->tune.map_ring, blocks, ctx->stream)
+                  : launch_map_glds<2>(p, ctx->tune.map_chunk, ctx->tune.map_ring, blocks, ctx->stream);
   } else {
     const int VI = map_vi(V, want);
     if (A <= 64) he = launch_map_vi<1>(p, VI, blocks, ctx->stream);

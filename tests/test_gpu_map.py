@@ -17,11 +17,13 @@ import crdts_gpu as cg  # noqa: E402
 # 16-replica chunks in 2 slots or 8-replica chunks in 4 slots (taken where A is even, V <= 2 and
 # the state fits 4 values), and register staging (every shape); the speculative scan with two
 # actors per 16-byte LDS read (mscan2=1, even A; off by default: no faster), the threshold scan
-# (mscan3=1, the default; mscan3=0 selects the two older scans) and the non-temporal step-image
-# loads (mnt=1, off by default).
-MODES = ["mglds=1,mchunk=16,mring=2,mscan3=1,mnt=0", "mglds=1,mchunk=8,mring=4,mscan3=1,mnt=0",
-         "mglds=0,mscan3=1,mnt=0", "mglds=1,mchunk=16,mring=2,mscan3=0,mscan2=0,mnt=0",
-         "mglds=1,mchunk=16,mring=2,mscan3=0,mscan2=1,mnt=1", "mglds=0,mscan3=0,mscan2=1,mnt=0"]
+# (mscan3=1, the default of the LDS-DMA ring) and the non-temporal step-image loads (mnt=1, off by
+# default); and the register-staged whole-chunk skip (mrs=1, the default where A <= 32 on the
+# LDS-DMA shapes), also with the scan off (mspec=0: every chunk handed to the exact loop).
+MODES = ["mglds=1,mrs=1", "mglds=1,mrs=1,mspec=0",
+         "mglds=1,mrs=0,mchunk=16,mring=2,mscan3=1,mnt=0", "mglds=1,mrs=0,mchunk=8,mring=4,mscan3=1,mnt=0",
+         "mglds=0,mscan2=0,mnt=0", "mglds=1,mrs=0,mchunk=16,mring=2,mscan3=0,mscan2=0,mnt=0",
+         "mglds=1,mrs=0,mchunk=16,mring=2,mscan3=0,mscan2=1,mnt=1", "mglds=0,mscan2=1,mnt=0"]
 
 
 @pytest.fixture(scope="module", params=MODES)
