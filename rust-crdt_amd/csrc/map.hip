@@ -706,17 +706,16 @@ __device__ __forceinline__ bool mv_antichain(const MVState<APL, VO> &s) {
   return ok;
 }
 
-// ---- Register-staged whole-chunk skip (RS path, A <= 32 even, 16-replica chunks) --------------
-// Almost every 16-replica chunk of a long fold changes nothing for a key.  The RS path loads each
-// chunk straight into registers in the scan's own layout — lane (s, gq) = (lane / 4, lane % 4)
-// holds step s, actor pairs (2gq + 8m, 2gq + 8m + 1), m < NP — one chunk ahead of the one it
-// tests; the fold state's scan operands (entry clock, TB, TO, own value clocks) are read from the
-// LDS mirror in the same layout while the chunk is in flight.  A chunk whose 16 steps the test
-// proves no-ops costs one register scan and a clock max (lane = actor, from the chunk's clock max),
-// with no LDS-DMA issue and no step image in LDS; any other chunk (a failed test, a remove naming
-// the key, the scan's preconditions off) is written to LDS slot 0 and runs through the exact
-// per-step loop; the ring is drained first and restarted after it, so no chunk register is live
-// across the exact loop.
+// ---- Register-tested whole-chunk skip (RS path, A <= 32 even, 16-replica chunks) -------------
+// Almost every 16-replica chunk of a long fold changes nothing for a key.  The RS path keeps two
+// chunks in flight (LDS-DMA into two slots) while it tests a third: chunk ch is copied from its slot
+// into registers in the scan's own layout — lane (s, gq) = (lane / 4, lane % 4) holds step s, actor
+// pairs (2gq + 8m, 2gq + 8m + 1), m < NP — the slot is refilled with chunk ch+2 at once, and the
+// whole chunk is tested in registers against the fold state's scan operands (entry clock, TB, TO,
+// own value clocks) read from the LDS mirror.  A skipped chunk costs the copy, one register scan
+// and a clock max (lane = actor, from the chunk's clock max); any other chunk (a failed test, a
+// remove naming the key, the scan's preconditions off) is written back over its slot and runs
+// through the exact per-step loop, after which chunk ch+2 is issued again.
 template <int VI, int NP>
 struct RsChunk {
   u64x2 e[NP];
@@ -750,46 +749,6 @@ __device__ __forceinline__ RsOwn<NQ, NP> rs_own(const u64 *mirror, const u64 *th
     }
   }
   return o;
-}
-
-// Per-lane element pointers of step s of chunk 0 and the per-chunk byte advances.
-struct RsLanes {
-  const char *e0, *c0, *o0, *v0;
-  unsigned long long se, sc, so, sv;  // row strides in bytes
-};
-
-__device__ __forceinline__ u64x2 ld16nt(const char *p) {
-  return __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(p));
-}
-__device__ __forceinline__ u64x2 ld16(const char *p) { return *reinterpret_cast<const u64x2 *>(p); }
-
-// Exactly NP*(2+VI) + 1 + VI loads per lane, unpredicated, so a fixed vmcnt count retires a chunk.
-// Steps past iend re-load step iend-1 (never tested: the verdict is masked to the chunk's steps);
-// a chunk past the last one re-loads the last (the ring issues a fixed number of chunks, so every
-// ring register is written on every path and none is live across the exact loop).
-template <int VI, int NP>
-__device__ __forceinline__ void rs_load(RsChunk<VI, NP> &r, const MapPlan &p, const RsLanes &L,
-                                        unsigned long long g, unsigned long long ch, unsigned long long iend,
-                                        int lane) {
-  constexpr unsigned long long C = 16;
-  ch = ch < p.nch ? ch : p.nch - 1;
-  const unsigned long long s = (unsigned)lane >> 2;
-  const unsigned long long i = ch * C + s < iend ? ch * C + s : iend - 1;
-  const unsigned gq = (unsigned)lane & 3;
-  const unsigned long long A = p.A;
-#pragma unroll
-  for (int m = 0; m < NP; ++m) {
-    const unsigned a0 = 2 * gq + 8 * m;
-    const unsigned long long a = a0 < A ? a0 : A - 2;  // a duplicate pair is neutral
-    r.e[m] = ld16nt(L.e0 + i * L.se + a * 8);
-#pragma unroll
-    for (int t = 0; t < VI; ++t) r.c[t][m] = ld16nt(L.c0 + i * L.sc + (t * A + a) * 8);
-    r.co[m] = ld16(L.o0 + i * L.so + a * 8);
-  }
-  r.cm = p.cmax[(g * p.nch + ch) * A + ((unsigned long long)lane < A ? lane : A - 1)];
-#pragma unroll
-  for (int t = 0; t < VI; ++t)
-    r.v[t] = __builtin_nontemporal_load(reinterpret_cast<const u64 *>(L.v0 + i * L.sv) + t);
 }
 
 // The no-op verdict of map_noop_steps3 on the register chunk (bit 4s: step s provably a no-op).
@@ -1055,22 +1014,15 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
 #endif
   // chunk staging
   MapChunk<APL, VI, ((GL || RS) ? 2 : CM)> regs;
-  RsChunk<VI, (RS ? NP : 1)> rA, rB;
-  RsLanes rl;
-  if constexpr (RS) {
-    rl.e0 = reinterpret_cast<const char *>(p.ec + g * p.e_gs + k * A);
-    rl.c0 = reinterpret_cast<const char *>(p.vclk + g * p.vc_gs + k * VI * A);
-    rl.o0 = reinterpret_cast<const char *>(p.clock + g * p.c_gs);
-    rl.v0 = reinterpret_cast<const char *>(p.vval + g * p.vv_gs + k * VI);
-    rl.se = (unsigned long long)p.e_rs * 8;
-    rl.sc = (unsigned long long)p.vc_rs * 8;
-    rl.so = (unsigned long long)p.c_rs * 8;
-    rl.sv = (unsigned long long)p.vv_rs * 8;
-    rs_load(rA, p, rl, g, 0, R, lane);  // (R > 0 here)
-  }
+  RsChunk<VI, (RS ? NP : 1)> rA;
   const int ni = GL ? (int)((W + 127) / 128) : 0;  // 1-KiB pieces per step image (GL: 1 or 2)
   GldsLanes<1> gl1;
   GldsLanes<2> gl2;
+  if constexpr (RS) {  // chunks 0 and 1 into the two slots (W <= 128: one piece per step)
+    gl1 = glds_lanes<VI, 1>(p, g, k, lane);
+    for (unsigned long long c = 0; c < 2 && c < nch; ++c)
+      map_chunk_glds<VI, C, 1>(p, gl1, g, k, c * C, R, map_lds + c * C * WS, WS, vbase + c * C * VI, cml + c * A, lane);
+  }
   if constexpr (GL) {
     if (ni == 1) gl1 = glds_lanes<VI, 1>(p, g, k, lane);
     else gl2 = glds_lanes<VI, 2>(p, g, k, lane);
@@ -1091,63 +1043,52 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
   }
 
   for (unsigned long long ch = 0; ch < nch; ++ch) {
-    // (RS: slot 0 holds the chunk handed to the exact loop)
-    const unsigned slot = RS ? 0u : (unsigned)(ch % NB);
+    const unsigned slot = (unsigned)(ch % NB);
     const u64 *buf = map_lds + slot * C * WS;
     const u64 *vb = vbase + slot * C * VI;
     if constexpr (RS) {
-      // Whole-chunk skip in registers: chunk ch is in rA (ch even) or rB (ch odd), landed or in
-      // flight; chunk ch+1 is issued into the other set before chunk ch is waited for.  A chunk
-      // that is not skipped goes to LDS slot 0 and the one behind it to slot 1, so neither register
-      // set is live across the exact loop (both are re-read from slot 1 after it).
-      constexpr int LD = NP * (2 + VI) + 1 + VI;  // loads per rs_load
+      // Chunk ch sits in slot ch&1 (LDS-DMA, issued two chunks ago), chunk ch+1 in the other slot.
+      // Copy chunk ch into registers, refill its slot with chunk ch+2 at once — two chunks stay in
+      // flight while this one is tested — and test it whole in registers.  A chunk that is not
+      // skipped is written back over its slot (chunk ch+2's copy is dropped and re-issued after the
+      // exact loop).
+      constexpr int P1 = C + 2;  // LDS-DMA instructions per chunk (map_chunk_glds, one piece per step)
       const bool elig0 = uni(p.spec && cool == 0 && anti && !slow && !direct);
       const int nv = __builtin_popcount(__builtin_amdgcn_readfirstlane(mv.vm));
       const unsigned long long n0 = R - ch * C < (unsigned long long)C ? R - ch * C : C;
       const u64 want = n0 >= 16 ? grp_mask<4>() : (grp_mask<4>() & ((1ull << (4 * n0)) - 1));
       const bool el = elig0 && (unsigned long long)next_row >= ch * C + n0;
-      bool skip;
+      u64 *const img = map_lds + slot * C * WS;
+      u64 *const vsl = vbase + slot * C * VI;
+      u64 *const cms = cml + slot * A;
       MAP_TICK();
-      if (ch & 1) {
-        rs_load(rA, p, rl, g, ch + 1, R, lane);
-        u64 noop = 0;
-        if (el) noop = rs_wait_noop_nv<VI, NP, LD>(rB, mirror, thr, A, present, nv, lane);
-        else wait_vmcnt<LD>();
-        skip = el && (noop & want) == want;
-        if (skip) {
-          if ((unsigned long long)lane < A) cs[0] = cs[0] > rB.cm ? cs[0] : rB.cm;
-        } else {
-          wait_vmcnt<0>();
-          rs_store(rB, map_lds, WS, vbase, cml, A, lane);
-          rs_store(rA, map_lds + C * WS, WS, vbase + C * VI, cml + A, A, lane);
-        }
-      } else {
-        rs_load(rB, p, rl, g, ch + 1, R, lane);
-        u64 noop = 0;
-        if (el) noop = rs_wait_noop_nv<VI, NP, LD>(rA, mirror, thr, A, present, nv, lane);
-        else wait_vmcnt<LD>();
-        skip = el && (noop & want) == want;
-        if (skip) {
-          if ((unsigned long long)lane < A) cs[0] = cs[0] > rA.cm ? cs[0] : rA.cm;
-        } else {
-          wait_vmcnt<0>();
-          rs_store(rA, map_lds, WS, vbase, cml, A, lane);
-          rs_store(rB, map_lds + C * WS, WS, vbase + C * VI, cml + A, A, lane);
-        }
-      }
+      if (ch + 1 < nch) wait_vmcnt<P1>();
+      else wait_vmcnt<0>();
+      MAP_TOCK(cy_wait);
+      MAP_TICK();
+      rs_reload(rA, img, WS, vsl, cms, A, lane);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot is read: refill it
+      if (ch + 2 < nch) map_chunk_glds<VI, C, 1>(p, gl1, g, k, (ch + 2) * C, R, img, WS, vsl, cms, lane);
+      MAP_TOCK(cy_issue);
+      MAP_TICK();
+      u64 noop = 0;
+      if (el) noop = rs_wait_noop_nv<VI, NP, 63>(rA, mirror, thr, A, present, nv, lane);
+      const bool skip = el && (noop & want) == want;
       MAP_TOCK(cy_scan);
 #ifdef MAP_STATS
       ++st_scan;
       if (!skip) ++st_fail;
 #endif
-      if (skip) {
-        // TB for the next chunk's test
+      if (skip) {  // acc.clock.merge of the chunk's replicas, and TB for the next chunk's test
         if ((unsigned long long)lane < A) {
+          cs[0] = cs[0] > rA.cm ? cs[0] : rA.cm;
           const u64 lo = cs[0] < m1 ? cs[0] : m1;
           thr[lane] = e[0] > lo ? e[0] : lo;
         }
         continue;
       }
+      wait_vmcnt<0>();
+      rs_store(rA, img, WS, vsl, cms, A, lane);
       // the round-1 scan of the exact loop reads max(e, Cs) from the mirror
       if ((unsigned long long)lane < A) mirror[(1 + VO) * A + lane] = e[0] > cs[0] ? e[0] : cs[0];
     }
@@ -1476,9 +1417,12 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
       MAP_TOCK(cy_exact);
     }
     if constexpr (RS) {
-      // chunk ch+1 back from slot 1 into both sets (whichever parity comes next)
-      rs_reload(rA, map_lds + C * WS, WS, vbase + C * VI, cml + A, A, lane);
-      rs_reload(rB, map_lds + C * WS, WS, vbase + C * VI, cml + A, A, lane);
+      // re-issue chunk ch+2 into the slot the exact loop used
+      if (ch + 2 < nch) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        map_chunk_glds<VI, C, 1>(p, gl1, g, k, (ch + 2) * C, R, map_lds + slot * C * WS, WS, vbase + slot * C * VI,
+                                 cml + slot * A, lane);
+      }
     }
     if constexpr (!GL && !RS) {
       if (ch + 1 < nch) {  // stage the next chunk (its loads were issued a whole chunk ago)
