@@ -723,6 +723,16 @@ struct RsChunk {
   u64x2 co[NP];
   u64 cm;     // the chunk's clock max of actor `lane` (map_chunk_max_kernel)
   u64 v[VI];  // the VI values of step s
+  u64x2 cmp[NP];  // the same clock max at the lane's actor pairs (scan layout)
+};
+
+// The fold state's scan operands kept in registers in the scan layout between exact steps
+// (reloaded from the LDS mirror after each chunk handed to the exact loop; the acc clock also
+// advances by each skipped chunk's clock max).
+template <int NP>
+struct RsReg {
+  u64x2 ea[NP], to[NP], m1[NP], cs[NP];
+  u64x2 sq[3][NP];
 };
 
 template <int NQ, int NP>
@@ -733,7 +743,8 @@ struct RsOwn {
 
 // The scan operands of the fold state from the LDS mirror (me / mc) and thresholds (TB / TO).
 template <int NQ, bool PRESENT, int NP>
-__device__ __forceinline__ RsOwn<NQ, NP> rs_own(const u64 *mirror, const u64 *thr, unsigned long long A, int lane) {
+__device__ __forceinline__ RsOwn<NQ, NP> rs_own(const u64 *mirror, const u64 *thr, unsigned long long A, int lane,
+                                                int nv = NQ) {
   RsOwn<NQ, NP> o;
   const unsigned gq = (unsigned)lane & 3;
 #pragma unroll
@@ -745,7 +756,7 @@ __device__ __forceinline__ RsOwn<NQ, NP> rs_own(const u64 *mirror, const u64 *th
       o.ea[m] = lds2(mirror + a);
       o.to[m] = lds2(thr + A + a);
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) o.sq[q][m] = lds2(mirror + (1 + q) * A + a);
+      for (int q = 0; q < NQ; ++q) o.sq[q][m] = q < nv ? lds2(mirror + (1 + q) * A + a) : u64x2{0, 0};
     }
   }
   return o;
@@ -801,28 +812,14 @@ __device__ __forceinline__ u64 rs_noop(const RsChunk<VI, NP> &r, const RsOwn<NQ,
   return (both | only) & G1;
 }
 
-// Own operands read (LDS) before the chunk's global loads are waited for, then the verdict.
-// (the wait keeps the LD most recent loads — the chunks behind this one — in flight)
-template <int VI, int NP, int NQ, bool PRESENT, int LD>
-__device__ __forceinline__ u64 rs_wait_noop(const RsChunk<VI, NP> &r, const u64 *mirror, const u64 *thr,
-                                            unsigned long long A, int lane) {
-  const RsOwn<NQ, NP> o = rs_own<NQ, PRESENT, NP>(mirror, thr, A, lane);
-  wait_vmcnt<LD>();
-  return rs_noop<VI, NP, NQ, PRESENT>(r, o);
-}
-template <int VI, int NP, int LD>
-__device__ __forceinline__ u64 rs_wait_noop_nv(const RsChunk<VI, NP> &r, const u64 *mirror, const u64 *thr,
+// The verdict from the LDS mirror (the exact loop's scan): one instantiation per presence, own
+// values as 3 zero-padded slots (see rs_reg_noop_nv).
+template <int VI, int NP>
+__device__ __forceinline__ u64 rs_lds_own_noop(const RsChunk<VI, NP> &r, const u64 *mirror, const u64 *thr,
                                                unsigned long long A, bool present, int nv, int lane) {
-  if (!present) return rs_wait_noop<VI, NP, 0, false, LD>(r, mirror, thr, A, lane);
-  switch (nv) {
-    case 0: return rs_wait_noop<VI, NP, 0, true, LD>(r, mirror, thr, A, lane);
-    case 1: return rs_wait_noop<VI, NP, 1, true, LD>(r, mirror, thr, A, lane);
-    case 2: return rs_wait_noop<VI, NP, 2, true, LD>(r, mirror, thr, A, lane);
-    case 3: return rs_wait_noop<VI, NP, 3, true, LD>(r, mirror, thr, A, lane);
-    default:
-      wait_vmcnt<LD>();
-      return 0;
-  }
+  if (!present) return rs_noop<VI, NP, 0, false>(r, rs_own<0, false, NP>(mirror, thr, A, lane));
+  if (nv > 3) return 0;
+  return rs_noop<VI, NP, 3, true>(r, rs_own<3, true, NP>(mirror, thr, A, lane, nv));
 }
 
 template <int VI, int NP>
@@ -841,7 +838,41 @@ __device__ __forceinline__ void rs_reload(RsChunk<VI, NP> &r, const u64 *img, un
   }
   r.cm = cm[(unsigned long long)lane < A ? lane : A - 1];
 #pragma unroll
+  for (int m = 0; m < NP; ++m) {
+    const unsigned a0 = 2 * gq + 8 * m;
+    r.cmp[m] = lds2(cm + (a0 < A ? a0 : A - 2));
+  }
+#pragma unroll
   for (int t = 0; t < VI; ++t) r.v[t] = vals[s * VI + t];
+}
+
+// The verdict from the register-held operands: TB = max(e, min(Cs, m1)) computed here.
+template <int VI, int NP, int NQ, bool PRESENT>
+__device__ __forceinline__ u64 rs_reg_noop(const RsChunk<VI, NP> &r, const RsReg<NP> &g) {
+  RsOwn<NQ, NP> o;
+#pragma unroll
+  for (int m = 0; m < NP; ++m) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const u64 lo = g.cs[m][h] < g.m1[m][h] ? g.cs[m][h] : g.m1[m][h];
+      o.tb[m][h] = g.ea[m][h] > lo ? g.ea[m][h] : lo;
+    }
+    o.ea[m] = g.ea[m];
+    o.to[m] = g.to[m];
+#pragma unroll
+    for (int q = 0; q < (NQ > 0 ? NQ : 1); ++q) o.sq[q][m] = g.sq[q < 3 ? q : 0][m];
+  }
+  return rs_noop<VI, NP, NQ, PRESENT>(r, o);
+}
+// One instantiation per presence: own values are compared as 3 slots, the unused ones zero —
+// neutral, since "c2 <= 0 everywhere" only covers an empty incoming slot, which the "appended, then
+// forgotten" test covers anyway — so the kernel carries two copies of the test, not five (the
+// fast path's code footprint is what sets its speed: the instruction cache is shared by two CUs).
+template <int VI, int NP>
+__device__ __forceinline__ u64 rs_reg_noop_nv(const RsChunk<VI, NP> &r, const RsReg<NP> &g, bool present, int nv) {
+  if (!present) return rs_reg_noop<VI, NP, 0, false>(r, g);
+  if (nv > 3) return 0;
+  return rs_reg_noop<VI, NP, 3, true>(r, g);
 }
 
 // The same test on a chunk handed to the exact loop (LDS slot 0, the step images rs_store wrote),
@@ -866,7 +897,7 @@ __device__ __forceinline__ u64 rs_lds_noop_nv(const u64 *img, unsigned long long
   r.cm = 0;
 #pragma unroll
   for (int t = 0; t < VI; ++t) r.v[t] = 0;
-  return rs_wait_noop_nv<VI, NP, 63>(r, mirror, thr, A, present, nv, lane);  // (no global load to wait for)
+  return rs_lds_own_noop<VI, NP>(r, mirror, thr, A, present, nv, lane);
 }
 
 // A chunk the register test could not skip: its step images, values and clock max into LDS slot 0
@@ -959,6 +990,8 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
   u64 *const cml = mirror + (2 + VO) * A;  // GL: NB staged chunk clock maxima (A words each)
   // scan thresholds (map_noop_steps3, RS): TB [A] | TO [A]; m1 = (min nonzero own value clock) - 1
   u64 *const thr = cml + ((GL || RS) ? NB * A : 0);
+  u64 *const csm = thr + 2 * A;  // RS: the acc clock and m1 handed back to the register operands
+  u64 *const m1m = thr + 3 * A;
   u64 m1 = ~0ull;
   if (kSpec) {
     for (unsigned long long x = lane; x < (2 + VO) * A; x += 64) mirror[x] = 0;
@@ -1015,6 +1048,18 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
   // chunk staging
   MapChunk<APL, VI, ((GL || RS) ? 2 : CM)> regs;
   RsChunk<VI, (RS ? NP : 1)> rA;
+  RsReg<(RS ? NP : 1)> rg;
+  if constexpr (RS) {
+#pragma unroll
+    for (int m = 0; m < NP; ++m) {
+      rg.ea[m] = 0;
+      rg.cs[m] = 0;
+      rg.to[m] = ~0ull;
+      rg.m1[m] = ~0ull;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) rg.sq[q][m] = 0;
+    }
+  }
   const int ni = GL ? (int)((W + 127) / 128) : 0;  // 1-KiB pieces per step image (GL: 1 or 2)
   GldsLanes<1> gl1;
   GldsLanes<2> gl2;
@@ -1071,26 +1116,28 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
       if (ch + 2 < nch) map_chunk_glds<VI, C, 1>(p, gl1, g, k, (ch + 2) * C, R, img, WS, vsl, cms, lane);
       MAP_TOCK(cy_issue);
       MAP_TICK();
-      u64 noop = 0;
-      if (el) noop = rs_wait_noop_nv<VI, NP, 63>(rA, mirror, thr, A, present, nv, lane);
-      const bool skip = el && (noop & want) == want;
+      const bool skip = el && (rs_reg_noop_nv<VI, NP>(rA, rg, present, nv) & want) == want;
       MAP_TOCK(cy_scan);
 #ifdef MAP_STATS
       ++st_scan;
       if (!skip) ++st_fail;
 #endif
-      if (skip) {  // acc.clock.merge of the chunk's replicas, and TB for the next chunk's test
-        if ((unsigned long long)lane < A) {
-          cs[0] = cs[0] > rA.cm ? cs[0] : rA.cm;
-          const u64 lo = cs[0] < m1 ? cs[0] : m1;
-          thr[lane] = e[0] > lo ? e[0] : lo;
-        }
+      if (skip) {  // acc.clock.merge of the chunk's replicas (both layouts)
+        if ((unsigned long long)lane < A) cs[0] = cs[0] > rA.cm ? cs[0] : rA.cm;
+#pragma unroll
+        for (int m = 0; m < NP; ++m)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) rg.cs[m][h] = rg.cs[m][h] > rA.cmp[m][h] ? rg.cs[m][h] : rA.cmp[m][h];
         continue;
       }
       wait_vmcnt<0>();
       rs_store(rA, img, WS, vsl, cms, A, lane);
-      // the round-1 scan of the exact loop reads max(e, Cs) from the mirror
-      if ((unsigned long long)lane < A) mirror[(1 + VO) * A + lane] = e[0] > cs[0] ? e[0] : cs[0];
+      // the exact loop's scans read max(e, Cs) and TB from LDS
+      if ((unsigned long long)lane < A) {
+        mirror[(1 + VO) * A + lane] = e[0] > cs[0] ? e[0] : cs[0];
+        const u64 lo = cs[0] < m1 ? cs[0] : m1;
+        thr[lane] = e[0] > lo ? e[0] : lo;
+      }
     }
     if constexpr (GL) {
       // issue chunk ch+NB-1 into the slot chunk ch-1 used, then wait for chunk ch
@@ -1417,6 +1464,26 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
       MAP_TOCK(cy_exact);
     }
     if constexpr (RS) {
+      // the register operands from the fold state after the exact loop
+      if ((unsigned long long)lane < A) {
+        csm[lane] = cs[0];
+        m1m[lane] = m1;
+      }
+      {
+        const unsigned gq = (unsigned)lane & 3;
+        const int nvx = __builtin_popcount(__builtin_amdgcn_readfirstlane(mv.vm));  // own values, compacted
+#pragma unroll
+        for (int m = 0; m < NP; ++m) {
+          const unsigned a0 = 2 * gq + 8 * m;
+          const unsigned long long a = a0 < A ? a0 : A - 2;
+          rg.ea[m] = lds2(mirror + a);
+          rg.to[m] = lds2(thr + A + a);
+          rg.m1[m] = lds2(m1m + a);
+          rg.cs[m] = lds2(csm + a);
+#pragma unroll
+          for (int q = 0; q < 3; ++q) rg.sq[q][m] = q < nvx ? lds2(mirror + (1 + q) * A + a) : u64x2{0, 0};
+        }
+      }
       // re-issue chunk ch+2 into the slot the exact loop used
       if (ch + 2 < nch) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1514,7 +1581,7 @@ static hipError_t launch_map_it(const MapPlan &p, unsigned long long blocks, hip
   const size_t W = (2 + VI) * p.A;
   const size_t lds = (size_t)NB * C * (map_ws(W) + VI) * sizeof(u64) + kMapL * 2 * sizeof(unsigned) +
                      (2 + VO) * p.A * sizeof(u64) + ((GL || RS) ? NB * p.A * sizeof(u64) : 0) +
-                     2 * p.A * sizeof(u64);
+                     4 * p.A * sizeof(u64);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   if (lds > 64 * 1024) {  // beyond the default dynamic-LDS limit (gfx950 has 160 KB per CU)
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&map_fold_kernel<APL, VI, VO, CM, NB, GL, ITM, NP>),
