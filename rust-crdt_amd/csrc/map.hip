@@ -29,6 +29,8 @@
 //                             vals = mvreg_merge(vals, vals2).forget(max(e,e2) > common ? max : 0),
 //                             e = common
 //   then the deferred ceiling forgets the entry (and drops it when its clock empties).
+#include <type_traits>
+
 #include "common.hpp"
 
 namespace crdt {
@@ -763,50 +765,76 @@ __device__ __forceinline__ RsOwn<NQ, NP> rs_own(const u64 *mirror, const u64 *th
 }
 
 // The no-op verdict of map_noop_steps3 on the register chunk (bit 4s: step s provably a no-op).
-template <int VI, int NP, int NQ, bool PRESENT>
-__device__ __forceinline__ u64 rs_noop(const RsChunk<VI, NP> &r, const RsOwn<NQ, NP> &o) {
+// An optional hook issuing the next chunk's LDS-DMA pieces between the test's compares: 18
+// back-to-back pieces stall the wave on the address unit (~65 cycles each with four waves per CU
+// issuing), while spread over the test they issue under its VALU work.
+struct RsNoDma {
+  static constexpr int count = 0;
+  __device__ __forceinline__ void operator()(int) {}
+};
+
+template <int VI, int NP, int NQ, bool PRESENT, class F = RsNoDma>
+__device__ __forceinline__ u64 rs_noop(const RsChunk<VI, NP> &r, const RsOwn<NQ, NP> &o, F &&dma = F{}) {
   constexpr int LPS = 4;
+  constexpr int ND = std::remove_reference_t<F>::count;  // pieces to issue: two per element, the rest after
   constexpr int NQ1 = NQ > 0 ? NQ : 1;
-  bool p2 = false, bB = true, bO = true, van[VI], le[VI][NQ1];
+  // per-test ballot masks (bit = lane), combined per step at the end
+  u64 mP2 = 0, mB = ~0ull, mO = ~0ull, mVan[VI], mLe[VI][NQ1];
 #pragma unroll
   for (int t = 0; t < VI; ++t) {
-    van[t] = true;
+    mVan[t] = ~0ull;
 #pragma unroll
-    for (int q = 0; q < NQ1; ++q) le[t][q] = true;
+    for (int q = 0; q < NQ1; ++q) mLe[t][q] = ~0ull;
   }
 #pragma unroll
   for (int m = 0; m < NP; ++m) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
+      if constexpr (ND > 0) {  // the masks so far are computed before these pieces issue
+        const int j = 2 * (2 * m + h);
+        asm volatile("" : "+s"(mP2), "+s"(mB), "+s"(mO));
+#pragma unroll
+        for (int t = 0; t < VI; ++t) {
+          asm volatile("" : "+s"(mVan[t]));
+#pragma unroll
+          for (int q = 0; q < NQ1; ++q) asm volatile("" : "+s"(mLe[t][q]));
+        }
+        if (j < ND) dma(j);
+        if (j + 1 < ND) dma(j + 1);
+      }
       const u64 e2 = r.e[m][h], tb = o.tb[m][h];
-      p2 |= e2 != 0;
+      mP2 |= __ballot(e2 != 0);
       if constexpr (!PRESENT) {
-        bB &= e2 <= tb;
+        mB &= __ballot(e2 <= tb);
       } else {
         const u64 co = r.co[m][h], ea = o.ea[m][h];
-        bB &= (e2 <= tb) & ((ea - 1 >= co) | (ea == e2));
-        bO &= co <= o.to[m][h];
+        mB &= __ballot((e2 <= tb) & ((ea - 1 >= co) | (ea == e2)));
+        mO &= __ballot(co <= o.to[m][h]);
         const u64 del = e2 > ea ? e2 : 0;
 #pragma unroll
         for (int t = 0; t < VI; ++t) {
           const u64 c2 = r.c[t][m][h];
-          van[t] &= c2 <= del;
+          mVan[t] &= __ballot(c2 <= del);
 #pragma unroll
-          for (int q = 0; q < NQ; ++q) le[t][q] &= c2 <= o.sq[q][m][h];
+          for (int q = 0; q < NQ; ++q) mLe[t][q] &= __ballot(c2 <= o.sq[q][m][h]);
         }
       }
     }
   }
+  if constexpr (ND > 0) {
+#pragma unroll
+    for (int j = 4 * NP; j < ND; ++j) dma(j);
+  }
   const u64 G1 = grp_mask<LPS>();
-  const u64 P2 = orN<LPS>(__ballot(p2));
-  if constexpr (!PRESENT) return (~P2 | andN<LPS>(__ballot(bB))) & G1;
-  u64 both = P2 & andN<LPS>(__ballot(bB));
-  const u64 only = ~P2 & andN<LPS>(__ballot(bO));
+  const u64 P2 = orN<LPS>(mP2);
+  if constexpr (!PRESENT) return (~P2 | andN<LPS>(mB)) & G1;
+  u64 both = P2 & andN<LPS>(mB);
+  const u64 only = ~P2 & andN<LPS>(mO);
 #pragma unroll
   for (int t = 0; t < VI; ++t) {
-    u64 cov = andN<LPS>(__ballot(van[t]));
+    u64 cov = andN<LPS>(mVan[t]);
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) cov |= andN<LPS>(__ballot(le[t][q]));
+    for (int q = 0; q < NQ; ++q) cov |= andN<LPS>(mLe[t][q]);
     both &= cov;
   }
   return (both | only) & G1;
@@ -847,8 +875,8 @@ __device__ __forceinline__ void rs_reload(RsChunk<VI, NP> &r, const u64 *img, un
 }
 
 // The verdict from the register-held operands: TB = max(e, min(Cs, m1)) computed here.
-template <int VI, int NP, int NQ, bool PRESENT>
-__device__ __forceinline__ u64 rs_reg_noop(const RsChunk<VI, NP> &r, const RsReg<NP> &g) {
+template <int VI, int NP, int NQ, bool PRESENT, class F = RsNoDma>
+__device__ __forceinline__ u64 rs_reg_noop(const RsChunk<VI, NP> &r, const RsReg<NP> &g, F &&dma = F{}) {
   RsOwn<NQ, NP> o;
 #pragma unroll
   for (int m = 0; m < NP; ++m) {
@@ -862,18 +890,50 @@ __device__ __forceinline__ u64 rs_reg_noop(const RsChunk<VI, NP> &r, const RsReg
 #pragma unroll
     for (int q = 0; q < (NQ > 0 ? NQ : 1); ++q) o.sq[q][m] = g.sq[q < 3 ? q : 0][m];
   }
-  return rs_noop<VI, NP, NQ, PRESENT>(r, o);
+  return rs_noop<VI, NP, NQ, PRESENT>(r, o, dma);
 }
 // One instantiation per presence: own values are compared as 3 slots, the unused ones zero —
 // neutral, since "c2 <= 0 everywhere" only covers an empty incoming slot, which the "appended, then
 // forgotten" test covers anyway — so the kernel carries two copies of the test, not five (the
 // fast path's code footprint is what sets its speed: the instruction cache is shared by two CUs).
-template <int VI, int NP>
-__device__ __forceinline__ u64 rs_reg_noop_nv(const RsChunk<VI, NP> &r, const RsReg<NP> &g, bool present, int nv) {
-  if (!present) return rs_reg_noop<VI, NP, 0, false>(r, g);
-  if (nv > 3) return 0;
-  return rs_reg_noop<VI, NP, 3, true>(r, g);
+template <int VI, int NP, class F = RsNoDma>
+__device__ __forceinline__ u64 rs_reg_noop_nv(const RsChunk<VI, NP> &r, const RsReg<NP> &g, bool present, int nv,
+                                              F &&dma = F{}) {
+  if (!present) return rs_reg_noop<VI, NP, 0, false>(r, g, dma);
+  if (nv > 3) {
+#pragma unroll
+    for (int j = 0; j < std::remove_reference_t<F>::count; ++j) dma(j);
+    return 0;
+  }
+  return rs_reg_noop<VI, NP, 3, true>(r, g, dma);
 }
+
+// The next chunk's LDS-DMA pieces as that hook (a whole chunk, every lane moving a piece of every
+// step image: (2+VI)*A == 128): pieces 0..15 the step images, 16 the values, 17 the clock max —
+// the same instructions, in the same order, as map_chunk_glds.
+struct RsDma {
+  static constexpr int count = 18;
+  const char *src;
+  unsigned long long stride;
+  u64 *img;
+  unsigned long long WS;
+  const unsigned *vsrc;
+  u64 *vals;
+  bool von;
+  const u64 *csrc;
+  u64 *cm;
+  bool con;
+  __device__ __forceinline__ void operator()(int j) {
+    if (j < 16) {
+      glds16(src, img + j * WS);
+      src += stride;
+    } else if (j == 16) {
+      if (von) glds4(vsrc, vals);
+    } else {
+      if (con) glds16(csrc, cm);
+    }
+  }
+};
 
 // The same test on a chunk handed to the exact loop (LDS slot 0, the step images rs_store wrote),
 // against the fold state after its exact steps: the RS kernel's only scan, so the exact loop holds
@@ -1113,10 +1173,22 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
       MAP_TICK();
       rs_reload(rA, img, WS, vsl, cms, A, lane);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot is read: refill it
-      if (ch + 2 < nch) map_chunk_glds<VI, C, 1>(p, gl1, g, k, (ch + 2) * C, R, img, WS, vsl, cms, lane);
+      // a whole next chunk with every lane moving a piece: its pieces go out during the test
+      const unsigned long long i2 = (ch + 2) * C;
+      const bool spread = el && ch + 2 < nch && i2 + C <= R && (2 + VI) * A == 128;
+      if (ch + 2 < nch && !spread) map_chunk_glds<VI, C, 1>(p, gl1, g, k, i2, R, img, WS, vsl, cms, lane);
       MAP_TOCK(cy_issue);
       MAP_TICK();
-      const bool skip = el && (rs_reg_noop_nv<VI, NP>(rA, rg, present, nv) & want) == want;
+      bool skip = false;
+      if (spread) {
+        const int sv = lane / (2 * VI), dw = lane % (2 * VI);
+        RsDma d{gl1.src0[0] + i2 * gl1.stride[0], gl1.stride[0], img, WS,
+                reinterpret_cast<const unsigned *>(p.vval + g * p.vv_gs + (i2 + (sv < C ? sv : 0)) * p.vv_rs + k * VI) + dw,
+                vsl, sv < C, p.cmax + (g * p.nch + i2 / C) * A + 2 * lane, cms, (unsigned long long)(2 * lane) < A};
+        skip = (rs_reg_noop_nv<VI, NP>(rA, rg, present, nv, d) & want) == want;
+      } else if (el) {
+        skip = (rs_reg_noop_nv<VI, NP>(rA, rg, present, nv) & want) == want;
+      }
       MAP_TOCK(cy_scan);
 #ifdef MAP_STATS
       ++st_scan;
