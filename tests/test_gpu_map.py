@@ -262,3 +262,36 @@ def test_map_even_actor_shapes(mctx, seed, R, K, A, V):
     assert d["def_row"].shape[0] > 0 or R == 1
     assert exp[4].any()  # some register survives the fold
     _check(mctx, d, 4)
+
+
+def test_map_direct_remove_walk(mctx):
+    """More removes naming one key than the per-key LDS list holds (kMapL = 256): the fold walks
+    the group's remove list directly, with even A and V <= 2, so the RS and LDS-DMA paths take it."""
+    rng = np.random.default_rng(91)
+    R, K, A = 700, 2, 4
+    d = _chain_dense(rng, R, K, A, 2, cmax=8)
+    D = 300
+    d["def_row"] = np.sort(rng.integers(0, R, size=D)).astype(np.uint64)
+    d["def_clock"] = np.where(rng.random((D, A)) < 0.5, rng.integers(1, 9, size=(D, A)), 0).astype(np.uint64)
+    d["def_keys"] = np.full((D, 1), 3, np.uint64)  # both keys
+    exp = O.map_fold(d["clock"], d["ec"], d["vclk"], d["vval"], d["def_row"], d["def_clock"],
+                     d["def_keys"], 64)
+    assert int(exp[4].max() if exp[4].size else 0) <= 4
+    _check(mctx, d, 4)
+
+
+@pytest.mark.parametrize("seed,R,A", [(31, 1000, 32), (32, 517, 16), (33, 263, 8)])
+def test_map_long_folds_mixed_chunks(mctx, seed, R, A):
+    """Long folds (many 16-replica chunks, a partial last one) where most chunks are skipped whole
+    and a few carry removes or changes: the RS path's hand-over to the exact loop and back."""
+    rng = np.random.default_rng(seed)
+    d = _chain_dense(rng, R, 6, A, 2, cmax=40)
+    # mostly old replicas: clocks and entries well below the running max, so most steps are no-ops
+    old = rng.random(R) < 0.9
+    d["ec"][old] = np.minimum(d["ec"][old], 2).astype(np.uint64)
+    d["vclk"][old] = np.minimum(d["vclk"][old], 2).astype(np.uint64)
+    exp = O.map_fold(d["clock"], d["ec"], d["vclk"], d["vval"], d["def_row"], d["def_clock"],
+                     d["def_keys"], 64)
+    if int(exp[4].max() if exp[4].size else 0) > 4:
+        pytest.skip("fold needs more than 4 values")
+    _check(mctx, d, 4)

@@ -397,3 +397,44 @@ def test_map_malformed_missing_and_capacity(gpu_ctx):
     assert s[3] == wire.MISSING
     assert s[4] == wire.CAP  # a third value with V = 2 slots: dropped and reported
     assert to_host(st.vval)[4, 0].tolist() == [1, 2]
+
+
+def test_map_ingest_large_frames():
+    """Config-4-shaped frames (1,024 keys x 32 actors, ~80 KiB each): synthetic states -> egress ->
+    ingest is the identity; truncated / extended copies of large frames are reported as malformed
+    and leave the other states' rows exact."""
+    from crdts_gpu import synth
+    torch.cuda.set_device(0)
+    ctx = cg.Context(0)
+    dev = "cuda"
+    R, K, A, V = 24, 1024, 32, 2
+    inp = synth.map_replicas(ctx, R, K, A, V, 0x5EED0004, kmax=256, p_def=0.3)
+    rows = inp.def_row.cpu().numpy().astype(np.int64)
+    cnt = np.bincount(rows, minlength=R).astype(np.int32)
+    Dcap = max(1, int(cnt.max()))
+    Kw = (K + 63) // 64
+    dcl = torch.zeros((R, Dcap, A), dtype=torch.int64, device=dev)
+    dks = torch.zeros((R, Dcap, Kw), dtype=torch.int64, device=dev)
+    slot = np.arange(rows.shape[0]) - np.searchsorted(rows, rows)
+    rt, st_ = torch.from_numpy(rows).to(dev), torch.from_numpy(slot).to(dev)
+    dcl[rt, st_] = inp.def_clock
+    dks[rt, st_] = inp.def_keys
+    states = cg.map.MapStates(inp.clock, inp.ec, inp.vclk, inp.vval, dcl, dks, torch.from_numpy(cnt).to(dev))
+    actors = torch.arange(1, A + 1, dtype=torch.int32, device=dev) * 5
+    keys = torch.arange(1, K + 1, dtype=torch.int32, device=dev) * 11
+    off, frames = wire.map_egress(states, actors, keys, ctx=ctx)
+    o = off.cpu().numpy()
+    assert int(np.diff(o).min()) > 16 * 1024  # every frame spans several 8-KiB windows
+    back, status = wire.map_ingest(frames, off, actors, keys, V, Dcap, ctx=ctx)
+    assert (status.cpu().numpy() == 0).all()
+    for f in states._fields:
+        assert torch.equal(getattr(back, f), getattr(states, f)), f
+    # malformed copies: frame 0 truncated in its last window, frame 1 with 8 trailing bytes
+    fr = host_frames(frames, off)
+    cut = fr[0][:len(fr[0]) - 12]
+    blob, noff = O.frames([cut, fr[1] + b"\0" * 8, fr[2]])
+    st2, s2 = wire.map_ingest(dev_bytes(blob), dev_off(noff), actors, keys, V, Dcap, ctx=ctx)
+    s = s2.cpu().numpy().tolist()
+    assert s[0] & wire.BAD and s[1] & wire.BAD and s[2] == 0
+    for f in states._fields:
+        assert torch.equal(getattr(st2, f)[2], getattr(states, f)[2]), f
