@@ -535,6 +535,10 @@ __global__ __launch_bounds__(kBlock) void lwwreg_egress_kernel(const u64 *marker
   }
 }
 
+constexpr int kEgRows = 16;  // entry rows in flight per wave (egress, A <= 64)
+constexpr int kEgKeys = 8;   // Map egress: keys in flight per wave (A <= 64, V <= kEgMaxV)
+constexpr int kEgMaxV = 4;
+
 // Orswot: clock; entries of every present member (index order); surviving removes.
 __global__ __launch_bounds__(kBlock) void orswot_egress_kernel(EgressPlan p, int write) {
   const int lane = threadIdx.x % kWave;
@@ -548,19 +552,70 @@ __global__ __launch_bounds__(kBlock) void orswot_egress_kernel(EgressPlan p, int
     u64 sz = 8 + 12 * nnz_row(c, p.A, lane);
     unsigned long long k = write ? write_vclock(w, 0, c, p.A, p.actors, lane) : 0;
     u64 ne = 0;
-    for (unsigned long long m = 0; m < p.M; ++m) ne += nnz_row(E + m * p.A, p.A, lane) != 0;
-    sz += 8;
-    if (write) {
-      if (lane == 0) wr64(w, k, ne);
-      k += 2;
-    }
-    for (unsigned long long m = 0; m < p.M; ++m) {
-      const u64 n = nnz_row(E + m * p.A, p.A, lane);
-      if (n == 0) continue;
-      sz += 8 + 8 + 12 * n;
+    if (p.A <= kWave) {
+      // lane = actor: a row is one coalesced load, its nonzeros one ballot; kEgRows rows are
+      // loaded before the first is examined (the rows are independent: a chain of one dependent
+      // load per row was what bound this pass)
+      const bool on = (unsigned long long)lane < p.A;
+      const uint32_t act = on ? p.actors[lane] : 0u;
+      u64 esz = 0;
+      for (unsigned long long m0 = 0; m0 < (write ? 0 : p.M); m0 += kEgRows) {
+        u64 v[kEgRows];
+#pragma unroll
+        for (int j = 0; j < kEgRows; ++j) v[j] = (on && m0 + j < p.M) ? E[(m0 + j) * p.A + lane] : 0;
+#pragma unroll
+        for (int j = 0; j < kEgRows; ++j) {
+          const u64 bm = __ballot(v[j] != 0);
+          if (bm) {
+            ++ne;
+            esz += 16 + 12 * (u64)__popcll(bm);
+          }
+        }
+      }
+      sz += 8 + esz;
+      if (write) {  // (the count sweep above is skipped when writing: ne goes to its slot at the end)
+        const unsigned long long kne = k;
+        ne = 0;
+        k += 2;
+        for (unsigned long long m0 = 0; m0 < p.M; m0 += kEgRows) {
+          u64 v[kEgRows];
+#pragma unroll
+          for (int j = 0; j < kEgRows; ++j) v[j] = (on && m0 + j < p.M) ? E[(m0 + j) * p.A + lane] : 0;
+#pragma unroll
+          for (int j = 0; j < kEgRows; ++j) {
+            const u64 bm = __ballot(v[j] != 0);
+            if (!bm) continue;
+            const u64 n = __popcll(bm);
+            if (lane == 0) {  // member, then the VClock: len, (actor, counter) ascending
+              wr64(w, k, p.members[m0 + j]);
+              wr64(w, k + 2, n);
+            }
+            if (v[j] != 0) {
+              const unsigned long long i = __popcll(bm & ((1ull << lane) - 1));
+              w[k + 4 + 3 * i] = act;
+              wr64(w, k + 5 + 3 * i, v[j]);
+            }
+            k += 4 + 3 * n;
+            ++ne;
+          }
+        }
+        if (lane == 0) wr64(w, kne, ne);
+      }
+    } else {
+      for (unsigned long long m = 0; m < p.M; ++m) ne += nnz_row(E + m * p.A, p.A, lane) != 0;
+      sz += 8;
       if (write) {
-        if (lane == 0) wr64(w, k, p.members[m]);
-        k = write_vclock(w, k + 2, E + m * p.A, p.A, p.actors, lane);
+        if (lane == 0) wr64(w, k, ne);
+        k += 2;
+      }
+      for (unsigned long long m = 0; m < p.M; ++m) {
+        const u64 n = nnz_row(E + m * p.A, p.A, lane);
+        if (n == 0) continue;
+        sz += 8 + 8 + 12 * n;
+        if (write) {
+          if (lane == 0) wr64(w, k, p.members[m]);
+          k = write_vclock(w, k + 2, E + m * p.A, p.A, p.actors, lane);
+        }
       }
     }
     u64 nd = 0;
@@ -757,6 +812,87 @@ __global__ __launch_bounds__(kBlock) void map_egress_kernel(MapWirePlan p, int w
     u64 sz = 8 + 12 * nnz_row(c, p.A, lane);
     unsigned long long k = write ? write_vclock(w, 0, c, p.A, p.actors, lane) : 0;
     u64 ne = 0;
+    if (p.A <= kWave && p.V <= kEgMaxV) {
+      // lane = actor: every row of kEgKeys keys (entry clock + V value clocks) is loaded before the
+      // first is examined, nonzeros are ballots (the plain loop below was a chain of one dependent
+      // load and a shuffle reduction per row)
+      const bool on = (unsigned long long)lane < p.A;
+      const uint32_t act = on ? p.actors[lane] : 0u;
+      {
+        const int pass = write ? 1 : 0;  // count sweep, or write sweep (ne to its slot at the end)
+        u64 esz = 0;
+        const unsigned long long kne = k;
+        if (pass == 1) k += 2;
+        ne = 0;
+        for (unsigned long long k0 = 0; k0 < p.K; k0 += kEgKeys) {
+          u64 e[kEgKeys], vc[kEgKeys][kEgMaxV];
+#pragma unroll
+          for (int j = 0; j < kEgKeys; ++j) {
+            const bool kon = on && k0 + j < p.K;
+            const unsigned long long sk = s * p.K + k0 + j;
+            e[j] = kon ? p.ec[sk * p.A + lane] : 0;
+#pragma unroll
+            for (int t = 0; t < kEgMaxV; ++t)
+              vc[j][t] = (kon && (unsigned long long)t < p.V) ? p.vclk[(sk * p.V + t) * p.A + lane] : 0;
+          }
+          // the batch's values: lane j * V + t holds key k0 + j's slot t
+          u64 vv = 0;
+          if (pass == 1 && (unsigned long long)lane < kEgKeys * p.V) {
+            const unsigned long long j = lane / p.V, t = lane % p.V;
+            if (k0 + j < p.K) vv = p.vval[(s * p.K + k0 + j) * p.V + t];
+          }
+#pragma unroll
+          for (int j = 0; j < kEgKeys; ++j) {
+            const u64 be = __ballot(e[j] != 0);
+            if (!be) continue;
+            ++ne;
+            const u64 n = __popcll(be);
+            u64 bv[kEgMaxV], m = 0, vsz = 0;
+#pragma unroll
+            for (int t = 0; t < kEgMaxV; ++t) {
+              bv[t] = __ballot(vc[j][t] != 0);
+              if (bv[t]) {
+                ++m;
+                vsz += 8 + 12 * (u64)__popcll(bv[t]) + 8;
+              }
+            }
+            esz += 4 + 8 + 12 * n + 8 + vsz;
+            if (pass == 0) continue;
+            const unsigned long long below = (1ull << lane) - 1;
+            if (lane == 0) {  // key, entry clock length
+              w[k] = p.keys[k0 + j];
+              wr64(w, k + 1, n);
+            }
+            if (e[j] != 0) {
+              const unsigned long long i = __popcll(be & below);
+              w[k + 3 + 3 * i] = act;
+              wr64(w, k + 4 + 3 * i, e[j]);
+            }
+            k += 3 + 3 * n;
+            if (lane == 0) wr64(w, k, m);
+            k += 2;
+#pragma unroll
+            for (int t = 0; t < kEgMaxV; ++t) {
+              if (!bv[t]) continue;
+              const u64 nv = __popcll(bv[t]);
+              const u64 val = __shfl(vv, j * (int)p.V + t, kWave);
+              if (lane == 0) {
+                wr64(w, k, nv);
+                wr64(w, k + 2 + 3 * nv, val);
+              }
+              if (vc[j][t] != 0) {
+                const unsigned long long i = __popcll(bv[t] & below);
+                w[k + 2 + 3 * i] = act;
+                wr64(w, k + 3 + 3 * i, vc[j][t]);
+              }
+              k += 2 + 3 * nv + 2;
+            }
+          }
+        }
+        if (pass == 0) sz += 8 + esz;
+        else if (lane == 0) wr64(w, kne, ne);
+      }
+    } else {
     for (unsigned long long key = 0; key < p.K; ++key) ne += nnz_row(p.ec + (s * p.K + key) * p.A, p.A, lane) != 0;
     sz += 8;
     if (write) {
@@ -789,6 +925,7 @@ __global__ __launch_bounds__(kBlock) void map_egress_kernel(MapWirePlan p, int w
         if (lane == 0) wr64(w, k, p.vval[slot0 + v]);
         k += 2;
       }
+    }
     }
     const unsigned long long nd = p.def_count ? p.def_count[s] : 0;
     sz += 8;
