@@ -133,9 +133,10 @@ def orswot_blob(states, aids, mids, rng):
     return O.frames(blobs)
 
 
-def test_orswot_ingest_egress(gpu_ctx):
-    rng = np.random.default_rng(11)
-    R, M, A = 40, 90, 9
+@pytest.mark.parametrize("R,M,A", [(40, 90, 9), (12, 70, 64), (10, 40, 65), (8, 30, 1)])
+def test_orswot_ingest_egress(gpu_ctx, R, M, A):
+    """A <= 64 takes the batched lane-per-actor egress, A > 64 the generic row loop."""
+    rng = np.random.default_rng(11 + A)
     states, (clock, entries, off, dcl, dmem) = orswot_objects(3, R, M, A)
     aids, ad = actor_dict(rng, A)
     mids, md = u64_dict(rng, M)
@@ -326,10 +327,12 @@ def map_blob(maps, aids, kids):
     return O.frames([O.bc_map(*map_wire_form(m, aids, kids)) for m in maps])
 
 
-def test_map_ingest_egress(gpu_ctx):
+@pytest.mark.parametrize("A,V", [(5, 3), (64, 2), (70, 2), (5, 5)])
+def test_map_ingest_egress(gpu_ctx, A, V):
+    """A <= 64 with V <= 4 takes the batched egress, the others the generic loop."""
     from test_gpu_merge_batch import arbitrary_maps, map_side
-    rng = np.random.default_rng(41)
-    N, K, A, V = 40, 9, 5, 3
+    rng = np.random.default_rng(41 + A + V)
+    N, K = 40, 9
     maps = arbitrary_maps(rng, N, K, A, V, 4)
     aids, ad = actor_dict(rng, A)
     kids, kd = actor_dict(rng, K)  # u32 keys
