@@ -224,7 +224,8 @@ int crdt_orswot_lub_many(crdt_ctx *ctx, const crdt_orswot_batch *in, crdt_orswot
  * slots (the state is incomplete: retry with a larger Dcap), bit 1 = an op named an actor,
  * member or rm row out of range or a bad kind / member range (reversed, or ending past n_mem)
  * (that op, or its bad members, were skipped), bit 2 = def_count[s] > Dcap on input, bit 3 = op_off[s..s+1] invalid (bits 2 and 3:
- * state left untouched).  Limits: A <= 256, Dcap*(A + Mw)*8 <= 65536. */
+ * state left untouched).  Limits: A <= 256 (the first slots of the deferred list are kept in LDS,
+ * as many as 64 KiB holds; the rest stay in the state's own slots). */
 typedef struct crdt_orswot_states {
   size_t N, M, A, Dcap;
   uint64_t *clock;

@@ -342,12 +342,13 @@ extern "C" int crdt_orswot_apply_batch(crdt_ctx *ctx, const crdt_orswot_states *
   if (s.clock_stride < s.A || s.entry_mstride < s.A || s.entry_sstride < s.M * s.entry_mstride)
     return fail(ctx, CRDT_EINVAL, "orswot_apply_batch: strides smaller than the rows they hold");
   const size_t Mw = (s.M + 63) / 64;
-  const size_t Dh = s.Dcap < (size_t)ctx->tune.apply_hot_slots ? s.Dcap : (size_t)ctx->tune.apply_hot_slots;
-  const size_t per_wave = Dh * (s.A + Mw) * 8;
+  // hot deferred slots in LDS: as many as fit (wide member bitmaps leave fewer, down to none: every
+  // slot then lives in the state's HBM slots, the same code path), so Dcap itself is not bounded
   const size_t lds_cap = 64 * 1024;
-  if (per_wave > lds_cap)
-    return fail(ctx, CRDT_EINVAL, "orswot_apply_batch: hot slots * (A + ceil(M/64)) * 8 = %zu B exceeds %zu B of LDS",
-                per_wave, lds_cap);
+  size_t Dh = s.Dcap < (size_t)ctx->tune.apply_hot_slots ? s.Dcap : (size_t)ctx->tune.apply_hot_slots;
+  const size_t slot_b = (s.A + Mw) * 8;
+  if (Dh * slot_b > lds_cap) Dh = lds_cap / slot_b;
+  const size_t per_wave = Dh * slot_b;
   int wpb = kBlock / kWave;
   while (wpb > 1 && per_wave * wpb > lds_cap) --wpb;
   CRDT_HIP(ctx, hipSetDevice(ctx->device));

@@ -159,9 +159,12 @@ def test_orswot_apply_empty(gpu_ctx):
     assert (status == 0).all() and all(g == O.Orswot() for g in got)
 
 
-@pytest.mark.parametrize("N,T,M,A", [(512, 64, 300, 64), (64, 200, 40, 256), (300, 32, 1000, 17)])
+@pytest.mark.parametrize("N,T,M,A", [(512, 64, 300, 64), (64, 200, 40, 256), (300, 32, 1000, 17),
+                                     (8, 64, 300000, 4), (6, 64, 600000, 4)])
 def test_orswot_apply_synth_streams(gpu_ctx, N, T, M, A):
-    """The bench's device-generated streams vs the C++ twin (std containers), every state."""
+    """The bench's device-generated streams vs the C++ twin (std containers), every state.  The
+    last two shapes have member bitmaps so wide that one / no deferred slot fits the 64 KiB of LDS:
+    the rest live in the states' HBM slots (no capacity error)."""
     ops = cg.synth.orswot_op_streams(N, T, M, A, seed=N + T, device="cuda:0")
     Dcap = 16
     clock = torch.zeros((N, A), dtype=torch.int64, device="cuda:0")
