@@ -159,7 +159,7 @@ __device__ __forceinline__ void orswot_apply_body(const OrswotApplyPlan &p) {
       // rm row of a Rm; member offsets as 32 bits (an op whose member range ends at or beyond
       // 2^32 is reported malformed, status bit 1, never silently truncated; so is a range that
       // runs past the n_mem entries of mem)
-      unsigned h_ka = kBadOp, h_mb = 0, h_me = 0;
+      unsigned h_ka = kBadOp, h_mb = 0, h_me = 0, h_m0 = 0;  // h_m0: an Add's first member
       u64 h_cr = 0;
       if (ov) {
         const unsigned kind = p.kind[o];
@@ -171,6 +171,7 @@ __device__ __forceinline__ void orswot_apply_body(const OrswotApplyPlan &p) {
           const unsigned a = p.actor ? p.actor[o] : 0u;
           h_ka = a < A ? a : kBadOp;
           h_cr = p.counter ? p.counter[o] : 0ull;
+          if (me > mb) h_m0 = p.mem[mb];  // loaded with the headers: a one-member Add skips that round trip
         } else if (range_ok && kind == 1) {
           h_ka = kRmOp;
           h_cr = p.rm_row ? p.rm_row[o] : 0u;
@@ -194,14 +195,24 @@ __device__ __forceinline__ void orswot_apply_body(const OrswotApplyPlan &p) {
             if (j == ja) cj = c[j];
           if (rl64(cj, la) >= k) continue;  // already seen (:60-63)
           bool bad = false;
-          for (u64 jm = mb + lane; jm < me; jm += kWave) {
-            const unsigned long long m = p.mem[jm];
+          if (me - mb == 1) {
+            const unsigned long long m = rl32(h_m0, i);
             if (m >= p.M) {
               bad = true;
-              continue;
+            } else if (lane == 0) {
+              u64 *cell = E + m * p.entry_mstride + a;
+              if (*cell < k) *cell = k;
             }
-            u64 *cell = E + m * p.entry_mstride + a;
-            if (*cell < k) *cell = k;
+          } else {
+            for (u64 jm = mb + lane; jm < me; jm += kWave) {
+              const unsigned long long m = p.mem[jm];
+              if (m >= p.M) {
+                bad = true;
+                continue;
+              }
+              u64 *cell = E + m * p.entry_mstride + a;
+              if (*cell < k) *cell = k;
+            }
           }
           if (__ballot(bad)) st |= 2u;
 #pragma unroll
