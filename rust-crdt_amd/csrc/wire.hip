@@ -539,6 +539,21 @@ constexpr int kEgRows = 16;  // entry rows in flight per wave (egress, A <= 64)
 constexpr int kEgKeys = 8;   // Map egress: keys in flight per wave (A <= 64, V <= kEgMaxV)
 constexpr int kEgMaxV = 4;
 
+// kEgRows rows m0.. of a [M][A] block, lane = actor: every load unconditional (rows past M and
+// lanes past A re-read valid cells, then masked to 0), so all of them issue before the first wait.
+__device__ __forceinline__ void eg_rows(u64 (&v)[kEgRows], const u64 *E, unsigned long long m0, unsigned long long M,
+                                        unsigned long long A, bool on, int lane) {
+  const unsigned long long a = on ? (unsigned long long)lane : 0;
+#pragma unroll
+  for (int j = 0; j < kEgRows; ++j) {
+    const unsigned long long m = m0 + j < M ? m0 + j : M - 1;
+    v[j] = E[m * A + a];
+  }
+#pragma unroll
+  for (int j = 0; j < kEgRows; ++j)
+    if (!on || m0 + j >= M) v[j] = 0;
+}
+
 // Orswot: clock; entries of every present member (index order); surviving removes.
 __global__ __launch_bounds__(kBlock) void orswot_egress_kernel(EgressPlan p, int write) {
   const int lane = threadIdx.x % kWave;
@@ -561,8 +576,7 @@ __global__ __launch_bounds__(kBlock) void orswot_egress_kernel(EgressPlan p, int
       u64 esz = 0;
       for (unsigned long long m0 = 0; m0 < (write ? 0 : p.M); m0 += kEgRows) {
         u64 v[kEgRows];
-#pragma unroll
-        for (int j = 0; j < kEgRows; ++j) v[j] = (on && m0 + j < p.M) ? E[(m0 + j) * p.A + lane] : 0;
+        eg_rows(v, E, m0, p.M, p.A, on, lane);
 #pragma unroll
         for (int j = 0; j < kEgRows; ++j) {
           const u64 bm = __ballot(v[j] != 0);
@@ -579,8 +593,7 @@ __global__ __launch_bounds__(kBlock) void orswot_egress_kernel(EgressPlan p, int
         k += 2;
         for (unsigned long long m0 = 0; m0 < p.M; m0 += kEgRows) {
           u64 v[kEgRows];
-#pragma unroll
-          for (int j = 0; j < kEgRows; ++j) v[j] = (on && m0 + j < p.M) ? E[(m0 + j) * p.A + lane] : 0;
+          eg_rows(v, E, m0, p.M, p.A, on, lane);
 #pragma unroll
           for (int j = 0; j < kEgRows; ++j) {
             const u64 bm = __ballot(v[j] != 0);
@@ -826,14 +839,24 @@ __global__ __launch_bounds__(kBlock) void map_egress_kernel(MapWirePlan p, int w
         ne = 0;
         for (unsigned long long k0 = 0; k0 < p.K; k0 += kEgKeys) {
           u64 e[kEgKeys], vc[kEgKeys][kEgMaxV];
+          {  // every load unconditional (clamped to valid cells), then masked: all issue before a wait
+            const unsigned long long al = on ? (unsigned long long)lane : 0;
 #pragma unroll
-          for (int j = 0; j < kEgKeys; ++j) {
-            const bool kon = on && k0 + j < p.K;
-            const unsigned long long sk = s * p.K + k0 + j;
-            e[j] = kon ? p.ec[sk * p.A + lane] : 0;
+            for (int j = 0; j < kEgKeys; ++j) {
+              const unsigned long long sk = s * p.K + (k0 + j < p.K ? k0 + j : p.K - 1);
+              e[j] = p.ec[sk * p.A + al];
 #pragma unroll
-            for (int t = 0; t < kEgMaxV; ++t)
-              vc[j][t] = (kon && (unsigned long long)t < p.V) ? p.vclk[(sk * p.V + t) * p.A + lane] : 0;
+              for (int t = 0; t < kEgMaxV; ++t)
+                vc[j][t] = p.vclk[(sk * p.V + ((unsigned long long)t < p.V ? t : p.V - 1)) * p.A + al];
+            }
+#pragma unroll
+            for (int j = 0; j < kEgKeys; ++j) {
+              const bool kon = on && k0 + j < p.K;
+              if (!kon) e[j] = 0;
+#pragma unroll
+              for (int t = 0; t < kEgMaxV; ++t)
+                if (!kon || (unsigned long long)t >= p.V) vc[j][t] = 0;
+            }
           }
           // the batch's values: lane j * V + t holds key k0 + j's slot t
           u64 vv = 0;
