@@ -440,7 +440,8 @@ int crdt_lwwreg_lub_many_sharded(crdt_ctx *ctx, const uint64_t *marker, const ui
  * group incomplete: retry with Vstate = 8).  The state holds VO = 2*pow2(V') values, V' the
  * smallest power of two with V' >= V and 2V' >= min(8, max(Vout, Vstate)); VO <= 8.
  * Deferred output as for Orswot (def_keep / def_keys over keys).
- * Limits: A <= 256, V <= 4, Vout <= 64. */
+ * Limits: A <= 256, V <= 8, Vout <= 64; the fold state holds up to 16 values per key (bit 2 of
+ * flags when a key needs more). */
 typedef struct crdt_map_batch {
   size_t G, R, K, A, V;
   const uint64_t *clock;

@@ -1677,8 +1677,8 @@ static hipError_t launch_map_rs(const MapPlan &p, unsigned long long blocks, hip
 // step, ceil(A / LPS) iterations rounded up to a power of two (A <= 64 when the scan runs).
 template <int APL, int VI, int VO, int CM, int NB, bool GL>
 static hipError_t launch_map(const MapPlan &p, unsigned long long blocks, hipStream_t s) {
-  if constexpr (APL != 1) {
-    return launch_map_it<APL, VI, VO, CM, NB, GL, 2>(p, blocks, s);  // no scan: A > 64
+  if constexpr (APL != 1 || VO > 4) {
+    return launch_map_it<APL, VI, VO, CM, NB, GL, 2>(p, blocks, s);  // no scan: A > 64 or a wide state
   } else {
     constexpr int C = GL ? CM : MapChunk<APL, VI, CM>::C;
     constexpr int NS = C > 8 ? 16 : (C > 4 ? 8 : (C > 2 ? 4 : 2));
@@ -1701,7 +1701,8 @@ static hipError_t launch_map_vi(const MapPlan &p, int VI, unsigned long long blo
   switch (VI) {
     case 1: return launch_map<APL, 1, 2, 16, 2, false>(p, blocks, s);
     case 2: return launch_map<APL, 2, 4, 16, 2, false>(p, blocks, s);
-    default: return launch_map<APL, 4, 8, 16, 2, false>(p, blocks, s);
+    case 4: return launch_map<APL, 4, 8, 16, 2, false>(p, blocks, s);
+    default: return launch_map<APL, 8, 16, 16, 2, false>(p, blocks, s);  // no scan: exact steps only
   }
 }
 
@@ -1713,11 +1714,11 @@ static hipError_t launch_map_glds(const MapPlan &p, int cm, int nb, unsigned lon
   return launch_map<1, VI, 4, 16, 2, true>(p, blocks, s);
 }
 
-// Smallest VI (1, 2, 4) with VI >= V and 2*VI >= min(8, want): the fold state holds 2*VI values.
+// Smallest VI (1, 2, 4, 8) with VI >= V and 2*VI >= min(16, want): the fold state holds 2*VI values.
 static int map_vi(size_t V, size_t want) {
   int VI = 1;
-  while ((size_t)VI < V || (size_t)(2 * VI) < (want < 8 ? want : 8)) VI *= 2;
-  return VI > 4 ? 4 : VI;
+  while ((size_t)VI < V || (size_t)(2 * VI) < (want < 16 ? want : 16)) VI *= 2;
+  return VI > 8 ? 8 : VI;
 }
 
 static bool aligned16(const void *x) { return (reinterpret_cast<uintptr_t>(x) & 15) == 0; }
@@ -1734,7 +1735,7 @@ extern "C" int crdt_map_lub_many(crdt_ctx *ctx, const crdt_map_batch *in, crdt_m
   if (R > 0 && (!in->clock || !in->ec || (V > 0 && (!in->vclk || !in->vval))))
     return fail(ctx, CRDT_EINVAL, "map_lub_many: NULL input");
   if (A > 256) return fail(ctx, CRDT_EUNSUPPORTED, "map_lub_many: A = %zu > 256 actors", A);
-  if (V > 4) return fail(ctx, CRDT_EUNSUPPORTED, "map_lub_many: V = %zu > 4 value slots per key", V);
+  if (V > 8) return fail(ctx, CRDT_EUNSUPPORTED, "map_lub_many: V = %zu > 8 value slots per key", V);
   if (Vout > 64) return fail(ctx, CRDT_EUNSUPPORTED, "map_lub_many: Vout = %zu > 64", Vout);
   if (G * K > 0x7fffffffULL) return fail(ctx, CRDT_EUNSUPPORTED, "map_lub_many: G*K too large");
   if (R > 0xfffffffeULL) return fail(ctx, CRDT_EUNSUPPORTED, "map_lub_many: R too large");

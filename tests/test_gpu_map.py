@@ -115,7 +115,7 @@ def test_map_lub_many_arbitrary(mctx, seed, R, K, A, V, cmax):
     exp = O.map_fold(d["clock"], d["ec"], d["vclk"], d["vval"], d["def_row"], d["def_clock"],
                      d["def_keys"], 64, peak=peak)
     vout = max(1, int(exp[4].max()) if exp[4].size else 1)
-    if int(peak.max()) > 8:  # beyond the kernel's state capacity: must be reported, not wrong
+    if int(peak.max()) > 16:  # beyond the kernel's state capacity: must be reported, not wrong
         with pytest.raises(cg.map.MapCapacityError):
             _gpu(mctx, d, vout)
         return
@@ -295,3 +295,32 @@ def test_map_long_folds_mixed_chunks(mctx, seed, R, A):
     if int(exp[4].max() if exp[4].size else 0) > 4:
         pytest.skip("fold needs more than 4 values")
     _check(mctx, d, 4)
+
+
+@pytest.mark.parametrize("R,V", [(12, 1), (2, 6), (2, 8), (3, 6), (1, 7)])
+def test_map_many_concurrent_values(mctx, R, V):
+    """Registers with many concurrent values: inputs with up to 8 values per key (V > 4) and folds
+    whose state needs 9-16 values (the 16-value state, exact steps only); 18 concurrent values
+    exceed the state and are reported."""
+    K, A = 3, 24
+    clock = np.zeros((R, A), np.uint64)
+    ec = np.zeros((R, K, A), np.uint64)
+    vclk = np.zeros((R, K, V, A), np.uint64)
+    vval = np.zeros((R, K, V), np.uint64)
+    for r in range(R):
+        for t in range(V):  # replica r holds V concurrent writes, every write by its own actor
+            a = r * V + t
+            clock[r, a] = 1
+            ec[r, :, a] = 1
+            vclk[r, :, t, a] = 1
+            vval[r, :, t] = 100 * r + t
+    d = dict(clock=clock, ec=ec, vclk=vclk, vval=vval, def_row=np.zeros(0, np.uint64),
+             def_clock=np.zeros((0, A), np.uint64), def_keys=np.zeros((0, 1), np.uint64))
+    peak = np.zeros(K, np.uint64)
+    exp = O.map_fold(clock, ec, vclk, vval, d["def_row"], d["def_clock"], d["def_keys"], 64, peak=peak)
+    assert int(exp[4].max()) == R * V
+    if R * V > 16:
+        with pytest.raises(cg.map.MapCapacityError):
+            _gpu(mctx, d, R * V)
+        return
+    _check(mctx, d, R * V)
