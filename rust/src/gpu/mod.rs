@@ -856,20 +856,27 @@ impl<K: Ord + Clone, V: Clone, A: Actor> BatchCvRDT for Map<K, MVReg<V, A>, A> {
             vval: vval.as_ptr(), vval_rstride: k * v, vval_gstride: r * k * v,
             def_off: def_off.as_ptr(), def_row: def_row.as_ptr(), def_clock: dcl.as_ptr(), def_keys: dks.as_ptr(),
         };
-        // Vout grows until the fold fits (flags bit 0 = some key folded to more values)
+        // Vout grows until the fold fits (flags bit 0 = some key folded to more values); the fold
+        // state starts at the library's choice (4 values: the scanned fast path) and widens to 8,
+        // then 16 values when a key overflows it (flags bit 2)
         let mut vout = 4usize;
+        let mut vstate = 0usize;
         loop {
             let (mut oc, mut oec) = (vec![0u64; a], vec![0u64; k * a]);
             let (mut ovc, mut ovv) = (vec![0u64; k * vout * a], vec![0u64; k * vout]);
             let (mut flags, mut keep, mut okeys) = (vec![0u32; 1], vec![0u8; nd], vec![0u64; nd * kw]);
             let mut out = ffi::crdt_map_out {
-                Vout: vout, Vstate: 8,
+                Vout: vout, Vstate: vstate,
                 clock: oc.as_mut_ptr(), ec: oec.as_mut_ptr(), vclk: ovc.as_mut_ptr(), vval: ovv.as_mut_ptr(),
                 nval: ptr::null_mut(), flags: flags.as_mut_ptr(),
                 def_keep: if nd > 0 { keep.as_mut_ptr() } else { ptr::null_mut() },
                 def_keys: if nd > 0 { okeys.as_mut_ptr() } else { ptr::null_mut() },
             };
             ctx.check_host(unsafe { ffi::crdt_map_lub_many(ctx.host, &batch, &mut out) })?;
+            if flags[0] & 4 != 0 && vstate < 16 {
+                vstate = if vstate < 8 { 8 } else { 16 };
+                continue;
+            }
             if flags[0] & 1 != 0 && vout < 64 {
                 vout = (vout * 2).min(64);
                 continue;
