@@ -316,8 +316,8 @@ int crdt_map_forget_batch(crdt_ctx *ctx, const crdt_map_states *states, const ui
  * key range reversed or ending past n_keys),
  * bits 2-3 = invalid input (state untouched), bit 4 = a register needed more than V values (the
  * state is incomplete: retry with more slots), bit 5 = internal slot invariant violated (never
- * expected; the value was not written).  Limits: A <= 256, 1 <= V <= 8,
- * Dcap*(A + Kw)*8 <= 65536. */
+ * expected; the value was not written).  Limits: A <= 256, 1 <= V <= 8 (the first deferred slots
+ * are kept in LDS, as many as 64 KiB holds; the rest stay in the state's own slots). */
 typedef struct crdt_map_ops {
   size_t n_ops;
   const uint64_t *op_off;   /* [N+1]       */

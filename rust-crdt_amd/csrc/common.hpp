@@ -65,6 +65,7 @@ struct Tune {
   int map_rs = 1;      // ... register-staged whole-chunk skip (A <= 32 on the LDS-DMA shapes)
   int rows_blocks_per_cu = 0;  // row-pair / row-reduction kernels (causal.hip); 0 = per-kernel default
   int apply_hot_slots = 8;     // Orswot apply: deferred slots kept in LDS per state (the rest in HBM)
+  int map_apply_hot = 1 << 20;  // Map apply: cap on the deferred slots kept in LDS (default: all that fit)
   int map_forget_vec2 = 1;     // Map forget: 16-byte pieces per lane where the shape allows it
   int map_pair_reg = 1;        // Map merge_batch, V <= 4: 1 sub-wave register kernel, 2 whole-wave one, 0 generic
   int pair_rows = 128;         // Orswot merge_batch: member rows per workgroup (64, 128, 256)

@@ -213,6 +213,7 @@ static void apply_tune(crdt_ctx *ctx, const char *t) {
       else if (k == "mrs") ctx->tune.map_rs = v != 0;
       else if (k == "rbpc" && v > 0) ctx->tune.rows_blocks_per_cu = v;
       else if (k == "hot" && v >= 0 && v <= 64) ctx->tune.apply_hot_slots = v;
+      else if (k == "mhot" && v >= 0) ctx->tune.map_apply_hot = v;
       else if (k == "mfv2") ctx->tune.map_forget_vec2 = v != 0;
       else if (k == "stage_kb" && v >= 4) ctx->tune.stage_kb = v;
       else if (k == "mpreg" && v >= 0 && v <= 2) ctx->tune.map_pair_reg = v;

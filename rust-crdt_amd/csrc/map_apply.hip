@@ -51,6 +51,7 @@ struct MapApplyPlan {
   unsigned long long n_ops;
   uint32_t *status;
   int wpb;
+  unsigned long long Dh;  // deferred slots kept in LDS (the rest in the state's own HBM slots)
 };
 
 // W clock words per lane: 1 for A <= 64 (fewer VGPRs, more waves per SIMD), 2 to A = 128, 4 to 256
@@ -169,15 +170,17 @@ __device__ __forceinline__ bool any_gt(const RowT<W> &r, const RowT<W> &c) {  //
   return !all_le(r, c);
 }
 
-template <int W>
+// SP: some deferred slots live in HBM (Dh < Dcap); without it every slot pointer is a known LDS
+// address (ds_read/ds_write, not flat accesses)
+template <int W, bool SP>
 __device__ __forceinline__ void map_apply_body(const MapApplyPlan &p) {
   extern __shared__ u64 lds[];
   const int lane = threadIdx.x % kWave;
   const int wib = threadIdx.x / kWave;
   const unsigned long long A = p.A;
-  const unsigned long long per_wave = p.Dcap * (A + p.Kw);
-  u64 *dcl = lds + wib * per_wave;  // [Dcap][A]
-  u64 *dkb = dcl + p.Dcap * A;      // [Dcap][Kw]
+  const unsigned long long per_wave = p.Dh * (A + p.Kw);
+  u64 *dcl = lds + wib * per_wave;  // [Dh][A]
+  u64 *dkb = dcl + p.Dh * A;        // [Dh][Kw]
 
   for (unsigned long long s = (unsigned long long)blockIdx.x * p.wpb + wib; s < p.N;
        s += (unsigned long long)gridDim.x * p.wpb) {
@@ -192,8 +195,16 @@ __device__ __forceinline__ void map_apply_body(const MapApplyPlan &p) {
     RowT<W> C = load_row<W>(Cg, lane, A);
     const u64 *gdc = p.def_clock + s * p.Dcap * A;
     const u64 *gdk = p.def_keys + s * p.Dcap * p.Kw;
-    for (unsigned long long i = lane; i < dcnt * A; i += kWave) dcl[i] = gdc[i];
-    for (unsigned long long i = lane; i < dcnt * p.Kw; i += kWave) dkb[i] = gdk[i];
+    const unsigned long long dhot = SP && dcnt > p.Dh ? p.Dh : dcnt;
+    for (unsigned long long i = lane; i < dhot * A; i += kWave) dcl[i] = gdc[i];
+    for (unsigned long long i = lane; i < dhot * p.Kw; i += kWave) dkb[i] = gdk[i];
+    // slot d: LDS for d < Dh, else the state's own HBM slot (SP only; generic pointers)
+    auto SC = [&](unsigned long long d) -> u64 * {
+      return !SP || d < p.Dh ? dcl + d * A : p.def_clock + (s * p.Dcap + d) * A;
+    };
+    auto SK = [&](unsigned long long d) -> u64 * {
+      return !SP || d < p.Dh ? dkb + d * p.Kw : p.def_keys + (s * p.Dcap + d) * p.Kw;
+    };
     wave_fence_m();
 
     for (unsigned long long base = ob; base < oe; base += kWave) {
@@ -297,13 +308,15 @@ __device__ __forceinline__ void map_apply_body(const MapApplyPlan &p) {
           wave_fence_m();
           unsigned nk = 0;  // apply_deferred (:134, :311-316)
           for (unsigned d = 0; d < dcnt; ++d) {
-            const RowT<W> rm = load_row<W>(dcl + d * A, lane, A);
-            keyset_rm(p, s, dkb + d * p.Kw, rm, lane);
+            const RowT<W> rm = load_row<W>(SC(d), lane, A);
+            keyset_rm(p, s, SK(d), rm, lane);
             wave_fence_m();
             if (any_gt(rm, C)) {
               if (nk != d) {
-                for (unsigned long long t = lane; t < A; t += kWave) dcl[nk * A + t] = dcl[d * A + t];
-                for (unsigned long long t = lane; t < p.Kw; t += kWave) dkb[nk * p.Kw + t] = dkb[d * p.Kw + t];
+                u64 *dc = SC(nk), *dk = SK(nk);
+                const u64 *sc = SC(d), *sk = SK(d);
+                for (unsigned long long t = lane; t < A; t += kWave) dc[t] = sc[t];
+                for (unsigned long long t = lane; t < p.Kw; t += kWave) dk[t] = sk[t];
               }
               ++nk;
             }
@@ -332,7 +345,7 @@ __device__ __forceinline__ void map_apply_body(const MapApplyPlan &p) {
           if (!any_gt(oc, C)) continue;  // rm <= clock: not deferred (:336-345)
           int slot = -1;
           for (unsigned d = 0; d < dcnt; ++d)
-            if (rows_eq(load_row<W>(dcl + d * A, lane, A), oc)) {
+            if (rows_eq(load_row<W>(SC(d), lane, A), oc)) {
               slot = (int)d;
               break;
             }
@@ -342,24 +355,39 @@ __device__ __forceinline__ void map_apply_body(const MapApplyPlan &p) {
               continue;
             }
             slot = (int)dcnt++;
-            store_row(dcl + (unsigned long long)slot * A, oc, lane, A);
-            for (unsigned long long t = lane; t < p.Kw; t += kWave) dkb[slot * p.Kw + t] = 0;
+            store_row(SC((unsigned long long)slot), oc, lane, A);
+            u64 *nb = SK((unsigned long long)slot);
+            for (unsigned long long t = lane; t < p.Kw; t += kWave) nb[t] = 0;
             wave_fence_m();
           }
-          u64 *bits = dkb + (unsigned long long)slot * p.Kw;
-          for (u64 jk = kb + lane; jk < ke; jk += kWave) {
-            const unsigned long long k = p.keys[jk];
-            if (k < p.K) atomicOr(bits + k / 64, 1ull << (k % 64));
+          u64 *bits = SK((unsigned long long)slot);
+          if (!SP || (unsigned long long)slot < p.Dh) {  // LDS: lanes OR their keys in at once
+            for (u64 jk = kb + lane; jk < ke; jk += kWave) {
+              const unsigned long long k = p.keys[jk];
+              if (k < p.K) atomicOr(bits + k / 64, 1ull << (k % 64));
+            }
+          } else {  // an HBM slot: plain read-modify-writes, one key at a time (no L2 atomics that
+                    // this wave's later plain loads could miss through its L1)
+            for (u64 jb = kb; jb < ke; jb += kWave) {
+              const unsigned kk = jb + lane < ke ? p.keys[jb + lane] : 0u;
+              const int n = (int)((ke - jb) < (u64)kWave ? (ke - jb) : kWave);
+              for (int t = 0; t < n; ++t) {
+                const unsigned long long k = (unsigned)__builtin_amdgcn_readlane((int)kk, t);
+                if (k < p.K && lane == 0) bits[k / 64] |= 1ull << (k % 64);
+                wave_fence_m();
+              }
+            }
           }
           wave_fence_m();
         }
       }
     }
     store_row(Cg, C, lane, A);
+    const unsigned long long dout = SP && dcnt > p.Dh ? p.Dh : dcnt;  // slots >= Dh are already in HBM
     u64 *wdc = p.def_clock + s * p.Dcap * A;
     u64 *wdk = p.def_keys + s * p.Dcap * p.Kw;
-    for (unsigned long long i = lane; i < dcnt * A; i += kWave) wdc[i] = dcl[i];
-    for (unsigned long long i = lane; i < dcnt * p.Kw; i += kWave) wdk[i] = dkb[i];
+    for (unsigned long long i = lane; i < dout * A; i += kWave) wdc[i] = dcl[i];
+    for (unsigned long long i = lane; i < dout * p.Kw; i += kWave) wdk[i] = dkb[i];
     if (lane == 0) {
       p.def_count[s] = dcnt;
       p.status[s] = st;
@@ -372,12 +400,13 @@ __device__ __forceinline__ void map_apply_body(const MapApplyPlan &p) {
 // compiler's 6 (3.29 vs 3.53 ms, profiles/r02_map_apply_wpe7_ab.log).  Round 1's miscompute at
 // that occupancy was a readlane of a spilled VGPR inside `if (lane == 0)` (fixed above), not the
 // spilling itself; the wider instances keep the compiler's choice (they would spill 44-116 B/lane).
+template <bool SP>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7))) void map_apply_kernel_w1(MapApplyPlan p) {
-  map_apply_body<1>(p);
+  map_apply_body<1, SP>(p);
 }
-template <int W>
+template <int W, bool SP>
 __global__ __launch_bounds__(kBlock) CRDT_APPLY_ATTR void map_apply_kernel(MapApplyPlan p) {
-  map_apply_body<W>(p);
+  map_apply_body<W, SP>(p);
 }
 
 }  // namespace crdt
@@ -401,11 +430,13 @@ extern "C" int crdt_map_apply_batch(crdt_ctx *ctx, const crdt_map_states *m, uin
   if (m->clock_stride < A || m->ec_stride < K * A || m->vclk_stride < K * V * A || m->vval_stride < K * V)
     return fail(ctx, CRDT_EINVAL, "map_apply_batch: stride smaller than the rows it holds");
   const size_t Kw = (K + 63) / 64;
-  const size_t per_wave = Dcap * (A + Kw) * 8;
+  // deferred slots in LDS: all of them when they fit (tune mhot caps them), else as many as 64 KiB
+  // holds, down to none; the rest stay in the state's own HBM slots
   const size_t lds_cap = 64 * 1024;
-  if (per_wave > lds_cap)
-    return fail(ctx, CRDT_EINVAL, "map_apply_batch: Dcap * (A + ceil(K/64)) * 8 = %zu B exceeds %zu B of LDS",
-                per_wave, lds_cap);
+  const size_t slot_b = (A + Kw) * 8;
+  size_t Dh = Dcap < (size_t)ctx->tune.map_apply_hot ? Dcap : (size_t)ctx->tune.map_apply_hot;
+  if (Dh * slot_b > lds_cap) Dh = lds_cap / slot_b;
+  const size_t per_wave = Dh * slot_b;
   int wpb = kBlock / kWave;
   while (wpb > 1 && per_wave * wpb > lds_cap) --wpb;
   CRDT_HIP(ctx, hipSetDevice(ctx->device));
@@ -413,17 +444,21 @@ extern "C" int crdt_map_apply_batch(crdt_ctx *ctx, const crdt_map_states *m, uin
                  (u64 *)m->vval, m->vval_stride, (u64 *)def_clock, (u64 *)def_keys, def_count, N, K, A, V, Kw, Dcap,
                  (const u64 *)ops->op_off, ops->kind, ops->actor, (const u64 *)ops->counter, ops->key,
                  (const u64 *)ops->val, ops->clk_row, (const u64 *)ops->clk_pool, ops->n_clk_rows,
-                 (const u64 *)ops->key_off, ops->keys, ops->keys ? ops->n_keys : 0, ops->n_ops, status, wpb};
+                 (const u64 *)ops->key_off, ops->keys, ops->keys ? ops->n_keys : 0, ops->n_ops, status, wpb, Dh};
   const unsigned long long want = (N + wpb - 1) / wpb;
   const unsigned long long cap = (unsigned long long)ctx->cu_count * 64;
   timing_begin(ctx, "map_apply");
   const dim3 grid((unsigned)(want < cap ? want : cap)), block(wpb * kWave);
+  const bool sp = Dh < Dcap;
   if (A <= (size_t)kWave)
-    hipLaunchKernelGGL(map_apply_kernel_w1, grid, block, per_wave * wpb, ctx->stream, p);
+    hipLaunchKernelGGL((sp ? map_apply_kernel_w1<true> : map_apply_kernel_w1<false>), grid, block, per_wave * wpb,
+                       ctx->stream, p);
   else if (A <= (size_t)(2 * kWave))
-    hipLaunchKernelGGL(map_apply_kernel<2>, grid, block, per_wave * wpb, ctx->stream, p);
+    hipLaunchKernelGGL((sp ? map_apply_kernel<2, true> : map_apply_kernel<2, false>), grid, block, per_wave * wpb,
+                       ctx->stream, p);
   else
-    hipLaunchKernelGGL(map_apply_kernel<kMA>, grid, block, per_wave * wpb, ctx->stream, p);
+    hipLaunchKernelGGL((sp ? map_apply_kernel<kMA, true> : map_apply_kernel<kMA, false>), grid, block,
+                       per_wave * wpb, ctx->stream, p);
   timing_end(ctx);
   CRDT_HIP(ctx, hipGetLastError());
   return CRDT_OK;

@@ -295,9 +295,22 @@ __device__ __forceinline__ void orswot_apply_body(const OrswotApplyPlan &p) {
             wave_fence();
           }
           u64 *bits = SM(slot);
-          for (u64 jm = mb + lane; jm < me; jm += kWave) {
-            const unsigned long long m = p.mem[jm];
-            if (m < p.M) atomicOr(bits + m / 64, 1ull << (m % 64));
+          if ((unsigned long long)slot < p.Dh) {  // LDS: lanes OR their members in at once
+            for (u64 jm = mb + lane; jm < me; jm += kWave) {
+              const unsigned long long m = p.mem[jm];
+              if (m < p.M) atomicOr(bits + m / 64, 1ull << (m % 64));
+            }
+          } else {  // an HBM slot: plain read-modify-writes one member at a time (L2 atomics would
+                    // leave this wave's L1 free to serve a stale line to its later plain loads)
+            for (u64 jb = mb; jb < me; jb += kWave) {
+              const unsigned mm = jb + lane < me ? (unsigned)p.mem[jb + lane] : 0u;
+              const int n = (int)((me - jb) < (u64)kWave ? (me - jb) : kWave);
+              for (int t = 0; t < n; ++t) {
+                const unsigned long long m = (unsigned)__builtin_amdgcn_readlane((int)mm, t);
+                if (m < p.M && lane == 0) bits[m / 64] |= 1ull << (m % 64);
+                wave_fence();
+              }
+            }
           }
           wave_fence();
         }

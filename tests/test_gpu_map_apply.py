@@ -17,7 +17,9 @@ pytestmark = pytest.mark.gpu
 import crdts_gpu as cg  # noqa: E402
 
 
-def replay_streams(seed, n_states, n_origins, K, n_ops):
+def replay_streams(seed, n_states, n_origins, K, n_ops, rm_heavy=False, key_stride=1):
+    """rm_heavy: keep most removes and few writes, in causal order, so removes whose context saw
+    dropped writes pile up in the deferred list."""
     rng = np.random.default_rng(seed)
     origins = [O.Map(O.MVReg) for _ in range(n_origins)]
     ops, val = [], 1
@@ -28,7 +30,7 @@ def replay_streams(seed, n_states, n_origins, K, n_ops):
         if x < 0.1:
             m.merge(origins[int(rng.integers(n_origins))])
             continue
-        k = int(rng.integers(K))
+        k = int(rng.integers(K // key_stride)) * key_stride
         if x < 0.75:
             op = m.update(k, m.get(k).derive_add_ctx(a), lambda r, c, v=val: r.write(v, c))
             val += 1
@@ -38,6 +40,11 @@ def replay_streams(seed, n_states, n_origins, K, n_ops):
         m.apply(op)
         ops.append(op)
     streams = []
+    if rm_heavy:
+        for _ in range(n_states):
+            p_up = rng.uniform(0.1, 0.4)
+            streams.append([op for op in ops if rng.random() < (p_up if isinstance(op, O.MapUp) else 0.95)])
+        return streams
     for _ in range(n_states):
         keep = np.flatnonzero(rng.random(len(ops)) < rng.uniform(0.4, 1.0))
         idx = keep[np.argsort(keep + rng.normal(0, rng.uniform(0, 10), size=keep.shape[0]))]
@@ -166,3 +173,43 @@ def test_map_apply_synth_streams(gpu_ctx, N, T, K, A, V):
     assert sum(len(m.deferred) for m in exp) > 0
     for s, ((g, _, _, _), e) in enumerate(zip(got, exp)):
         assert g == e, s
+
+
+@pytest.mark.parametrize("hot", [0, 1, 3])
+def test_map_apply_deferred_spill(hot):
+    """Deferred slots beyond the LDS-resident ones live in the state's own HBM slots (CRDT_TUNE
+    mhot=N): the same results with none, one or three slots in LDS."""
+    ctx = cg.Context(0)
+    ctx.tune(f"mhot={hot}")
+    try:
+        streams = replay_streams(20 + hot, 40, 5, 20, 200, rm_heavy=True)
+        exp, peak = oracle_apply(streams)
+        Dcap = max(1, max(sum(1 for o in s if isinstance(o, O.MapRm)) for s in streams))
+        assert max(len(m.deferred) for m in exp) > max(hot, 1)
+        got, status = gpu_apply(ctx, streams, 20, 5, min(peak, 8), min(Dcap, 24))
+        assert (status == 0).all(), status
+        for s, ((g, _, _, _), e) in enumerate(zip(got, exp)):
+            assert g.clock == e.clock and g.entries == e.entries, s
+            assert g.deferred == e.deferred, s
+    finally:
+        ctx.close()
+
+
+def test_map_apply_wide_deferred_list():
+    """A deferred list far wider than LDS (A = 70, K = 4,000: 133 words a slot; Dcap = 183 slots is
+    190 KiB per state): the launch keeps the 61 slots that fit in 64 KiB in LDS and the rest in HBM
+    instead of refusing (with mhot=0 nothing is in LDS: test_map_apply_deferred_spill)."""
+    ctx = cg.Context(0)
+    try:
+        streams = replay_streams(35, 12, 70, 4000, 700, rm_heavy=True, key_stride=100)
+        exp, peak = oracle_apply(streams)
+        assert peak <= 8
+        Dcap = max(sum(1 for o in s if isinstance(o, O.MapRm)) for s in streams)
+        assert Dcap * (70 + 63) * 8 > 64 * 1024
+        got, status = gpu_apply(ctx, streams, 4000, 70, 8, Dcap)
+        assert (status == 0).all(), status
+        for s, ((g, _, _, _), e) in enumerate(zip(got, exp)):
+            assert g.clock == e.clock and g.entries == e.entries, s
+            assert g.deferred == e.deferred, s
+    finally:
+        ctx.close()
