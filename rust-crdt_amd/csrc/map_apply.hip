@@ -206,6 +206,13 @@ __device__ __forceinline__ void map_apply_body(const MapApplyPlan &p) {
       return !SP || d < p.Dh ? dkb + d * p.Kw : p.def_keys + (s * p.Dcap + d) * p.Kw;
     };
     wave_fence_m();
+    // apply_deferred re-forgets every key of every deferred slot (map.rs:311-316).  After one full
+    // pass each slot's keys are forgotten by its clock; later ops keep that (an Rm only forgets more,
+    // and forgets commute; a new slot's keys were just forgotten by it), and an Up changes only its
+    // own key's rows, so every later pass re-forgets key k alone — the same rows as the full pass,
+    // since forgetting is idempotent.  The first pass stays full: the input state need not hold
+    // the invariant.
+    bool full = true;
 
     for (unsigned long long base = ob; base < oe; base += kWave) {
       const unsigned long long o = base + lane;
@@ -309,7 +316,11 @@ __device__ __forceinline__ void map_apply_body(const MapApplyPlan &p) {
           unsigned nk = 0;  // apply_deferred (:134, :311-316)
           for (unsigned d = 0; d < dcnt; ++d) {
             const RowT<W> rm = load_row<W>(SC(d), lane, A);
-            keyset_rm(p, s, SK(d), rm, lane);
+            if (full) {
+              keyset_rm(p, s, SK(d), rm, lane);
+            } else if ((rl64m(SK(d)[k / 64], 0) >> (k % 64)) & 1ull) {
+              key_rm(p, s, k, rm, lane);  // only key k changed since the last full pass
+            }
             wave_fence_m();
             if (any_gt(rm, C)) {
               if (nk != d) {
@@ -322,6 +333,7 @@ __device__ __forceinline__ void map_apply_body(const MapApplyPlan &p) {
             }
           }
           dcnt = nk;
+          full = false;
           wave_fence_m();
         } else {  // ---- Op::Rm -> apply_keyset_rm (:318-348)
           const u64 kb = rl64m(h_kb, i), ke = rl64m(h_ke, i);

@@ -149,6 +149,12 @@ __device__ __forceinline__ void orswot_apply_body(const OrswotApplyPlan &p) {
     for (unsigned long long i = lane; i < dhot * A; i += kWave) lcl[i] = gdc[i];
     for (unsigned long long i = lane; i < dhot * p.Mw; i += kWave) lmb[i] = gdm[i];
     wave_fence();
+    // apply_deferred re-forgets every member of every deferred slot (orswot.rs:281-286).  After
+    // one full pass each slot's members are forgotten by its clock; a Rm only forgets more (forgets
+    // commute) and a new slot's members were just forgotten by it, so a later one-member Add only
+    // needs its own member's row re-forgotten (idempotent elsewhere).  The first pass stays full:
+    // the input state need not hold the invariant.
+    bool full = true;
 
     for (unsigned long long base = ob; base < oe; base += kWave) {
       // op headers, lane = op
@@ -228,7 +234,13 @@ __device__ __forceinline__ void orswot_apply_body(const OrswotApplyPlan &p) {
               const unsigned long long aa = lane + j * kWave;
               r[j] = aa < A ? SC(d)[aa] : 0;
             }
-            forget_members(p, E, SM(d), r, lane);
+            if (full || me - mb != 1) {
+              forget_members(p, E, SM(d), r, lane);
+            } else {  // a one-member Add after a full pass: only member m0's row can need it
+              const unsigned long long m0 = rl32(h_m0, i);
+              if (m0 < p.M && ((rl64(SM(d)[m0 / 64], 0) >> (m0 % 64)) & 1ull))
+                forget_row(E + m0 * p.entry_mstride, r, lane, A);
+            }
             if (any_greater(r, c, lane, A)) {
               if (nk != d) {
                 u64 *dc = SC(nk), *sc = SC(d), *dm = SM(nk), *sm = SM(d);
@@ -239,6 +251,7 @@ __device__ __forceinline__ void orswot_apply_body(const OrswotApplyPlan &p) {
             }
           }
           dcnt = nk;
+          full = false;
           wave_fence();
         } else {  // ---- Op::Rm -> apply_rm (:230-250)
           const unsigned rr = (unsigned)rl64(h_cr, i);

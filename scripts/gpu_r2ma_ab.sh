@@ -1,5 +1,6 @@
 #!/bin/bash
-# Map apply deferred spill: parity, then A/B of the apply bench, HEAD library (ab/) vs the working tree's
+# Apply kernels: parity, then A/B of the Map and Orswot apply benches, a previous library (ab/)
+# vs the working tree's, alternating
 set -o pipefail
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
@@ -8,9 +9,11 @@ timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method threa
 tail -2 gpurun_out/r2ma_tests.log
 out=gpurun_out/r2ma_ab.log; : > $out
 for i in 1 2; do
-  echo "== prev" >> $out
-  CRDT_GPU_LIB=$PWD/ab/libcrdt_gpu_prev.so timeout -k 10 200 python -u scripts/bench_map_apply.py >> $out 2>&1 || exit 1
-  echo "== new" >> $out
-  timeout -k 10 200 python -u scripts/bench_map_apply.py >> $out 2>&1 || exit 1
+  for b in bench_map_apply bench_orswot_apply; do
+    echo "== prev $b" >> $out
+    CRDT_GPU_LIB=$PWD/ab/libcrdt_gpu_prev.so timeout -k 10 200 python -u scripts/$b.py >> $out 2>&1 || exit 1
+    echo "== new $b" >> $out
+    timeout -k 10 200 python -u scripts/$b.py >> $out 2>&1 || exit 1
+  done
 done
-grep -o '== .*\|kernel_us": [0-9.]*' $out
+grep -o '== .*\|kernel_us": [0-9.]*\|"parity": "[a-z]*"' $out

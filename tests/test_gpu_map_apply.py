@@ -213,3 +213,78 @@ def test_map_apply_wide_deferred_list():
             assert g.deferred == e.deferred, s
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_map_apply_unapplied_input_deferred(gpu_ctx, seed):
+    """Input states whose deferred removes were never applied to their rows (the reference's own
+    states always hold them applied): the first apply_deferred must re-forget every key of every
+    slot, later ones only the updated key (map_apply.hip's restricted pass).  Long Up streams on
+    random keys, some seen, some Rm ops in between."""
+    rng = np.random.default_rng(seed)
+    N, K, A, V, Dcap = 64, 8, 4, 4, 48
+    Kw = 1
+    clock = rng.integers(0, 6, size=(N, A)).astype(np.uint64)
+    ec = np.zeros((N, K, A), np.uint64)
+    vclk = np.zeros((N, K, V, A), np.uint64)
+    vval = np.zeros((N, K, V), np.uint64)
+    dcl = np.zeros((N, Dcap, A), np.uint64)
+    dks = np.zeros((N, Dcap, Kw), np.uint64)
+    cnt = np.zeros(N, np.int32)
+    states, streams = [], []
+    for s in range(N):
+        for k in range(K):
+            if rng.random() < 0.6:
+                row = np.minimum(rng.integers(0, 6, size=A).astype(np.uint64), clock[s])
+                if row.any():
+                    ec[s, k] = row
+                    vclk[s, k, 0] = row
+                    vval[s, k, 0] = rng.integers(1, 100)
+        nd, seen = int(rng.integers(1, 4)), set()
+        for _ in range(nd):
+            rm = rng.integers(0, 9, size=A).astype(np.uint64)
+            if not rm.any() or rm.tobytes() in seen:
+                continue
+            seen.add(rm.tobytes())
+            keys = [k for k in range(K) if rng.random() < 0.5] or [0]
+            dcl[s, cnt[s]] = rm
+            dks[s, cnt[s], 0] = sum(1 << k for k in keys)
+            cnt[s] += 1
+        deferred = [(dcl[s, d], O.bitmap_members(dks[s, d])) for d in range(int(cnt[s]))]
+        states.append(O.dense_to_map(clock[s], ec[s], vclk[s], vval[s], deferred))
+        ops, cur = [], clock[s].copy()
+        for _ in range(int(rng.integers(5, 40))):
+            a, k = int(rng.integers(A)), int(rng.integers(K))
+            if rng.random() < 0.15:
+                rmc = rng.integers(0, 9, size=A).astype(np.uint64)
+                rmc[int(rng.integers(A))] += 1  # a non-empty rm clock
+                ops.append(O.MapRm(O.VClock({x: int(v) for x, v in enumerate(rmc) if v}), {k}))
+                continue
+            c = int(cur[a]) + 1 if rng.random() < 0.85 else max(1, int(cur[a]))
+            cur[a] = max(cur[a], c)
+            put = {x: int(v) for x, v in enumerate(np.minimum(cur, rng.integers(0, 9, size=A))) if v}
+            put[a] = c
+            ops.append(O.MapUp(O.Dot(a, c), k, O.MVRegPut(O.VClock(put), int(rng.integers(1, 1000)))))
+        streams.append(ops)
+    exp = []
+    for m, ops in zip(states, streams):
+        m = m.copy()
+        for op in ops:
+            m.apply(op)
+        exp.append(m)
+    dev = lambda x: torch.from_numpy(x.view(np.int64).copy()).to("cuda:0")  # noqa: E731
+    t = [dev(x) for x in (clock, ec, vclk, vval, dcl, dks)]
+    tc = torch.from_numpy(cnt).to("cuda:0")
+    ops = cg.map.encode_ops([[op_tuple(o) for o in s] for s in streams], A, "cuda:0")
+    status = cg.map.apply_batch(*t, tc, ops, ctx=gpu_ctx).cpu().numpy()
+    torch.cuda.synchronize()
+    assert not (status & ~16).any(), sorted(set(status.tolist()))
+    c, e, vc, vv = (to_host(x) for x in t[:4])
+    dc, dk, n = to_host(t[4]), to_host(t[5]), tc.cpu().numpy()
+    for s in range(N):
+        if status[s] & 16:
+            continue  # more concurrent values than V slots: reported, not compared
+        deferred = [(dc[s, d], O.bitmap_members(dk[s, d])) for d in range(int(n[s]))]
+        got = O.dense_to_map(c[s], e[s], vc[s], vv[s], deferred)
+        assert got == exp[s], s
+    assert (status == 0).sum() > N // 2
