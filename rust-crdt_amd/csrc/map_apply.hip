@@ -226,14 +226,22 @@ __device__ __forceinline__ void map_apply_body(const MapApplyPlan &p) {
       const u64 h_kb = ov && p.key_off ? p.key_off[o] : 0ull;
       const u64 h_ke = ov && p.key_off ? p.key_off[o + 1] : 0ull;
       const int nb = (int)((oe - base) < (unsigned long long)kWave ? (oe - base) : kWave);
+      // op i's clock row is loaded while op i-1 runs (the pool is read-only): one dependent
+      // round trip less per op
+      auto pool_row = [&](int j) -> RowT<W> {
+        const unsigned r = rl32m(h_row, j);
+        return load_row<W>(p.clk_pool + (unsigned long long)(r < p.n_clk_rows ? r : 0u) * A, lane, A);
+      };
+      RowT<W> ocn = p.n_clk_rows ? pool_row(0) : zero_row<W>();
       for (int i = 0; i < nb; ++i) {
+        const RowT<W> oc = ocn;
+        if (i + 1 < nb && p.n_clk_rows) ocn = pool_row(i + 1);
         const unsigned kind = rl32m(h_kind, i);
         const unsigned rr = rl32m(h_row, i);
         if (kind > 1 || rr >= p.n_clk_rows) {
           st |= 2u;
           continue;
         }
-        const RowT<W> oc = load_row<W>(p.clk_pool + (unsigned long long)rr * A, lane, A);
         if (kind == 0) {  // ---- Op::Up
           const unsigned long long a = rl32m(h_actor, i), k = rl32m(h_key, i);
           const u64 kc = rl64m(h_counter, i);
