@@ -263,9 +263,24 @@ __device__ __forceinline__ void map_apply_body(const MapApplyPlan &p) {
           if (any_nz(oc)) {  // MVReg::apply (mvreg.rs:130-166)
             bool should_add = true;
             int last = -1, used = 0;
+            // the first kVB value rows in one batch of loads (clamped, unconditional, so they issue
+            // together), the rest one at a time
+            constexpr int kVB = 4;
+            RowT<W> vb[kVB];
+#pragma unroll
+            for (int j = 0; j < kVB; ++j)
+              vb[j] = load_row<W>(q.vc + ((unsigned long long)j < p.V ? j : 0) * A, lane, A);
             for (unsigned long long j = 0; j < p.V; ++j) {
               u64 *vr = q.vc + j * A;
-              const RowT<W> v = load_row<W>(vr, lane, A);
+              RowT<W> v;
+              if (j < (unsigned long long)kVB) {
+                v = vb[0];
+#pragma unroll
+                for (int t = 1; t < kVB; ++t)
+                  if ((unsigned long long)t == j) v = vb[t];
+              } else {
+                v = load_row<W>(vr, lane, A);
+              }
               if (!any_nz(v)) continue;
               if (all_le(v, oc)) {  // partial_cmp in {Less, Equal}: dropped
                 store_row(vr, zero_row<W>(), lane, A);
