@@ -181,6 +181,7 @@ __device__ __forceinline__ void orswot_apply_body(const OrswotApplyPlan &p) {
         } else if (range_ok && kind == 1) {
           h_ka = kRmOp;
           h_cr = p.rm_row ? p.rm_row[o] : 0u;
+          if (me > mb) h_m0 = p.mem[mb];  // a one-member Rm skips that round trip too
         }
       }
       const int nb = (int)((oe - base) < (unsigned long long)kWave ? (oe - base) : kWave);
@@ -266,16 +267,22 @@ __device__ __forceinline__ void orswot_apply_body(const OrswotApplyPlan &p) {
             const unsigned long long aa = lane + j * kWave;
             r[j] = aa < A ? R[aa] : 0;
           }
-          for (u64 jb = mb; jb < me; jb += kWave) {
-            const unsigned mm = jb + lane < me ? p.mem[jb + lane] : 0u;
-            const int n = (int)((me - jb) < (u64)kWave ? (me - jb) : kWave);
-            for (int t = 0; t < n; ++t) {
-              const unsigned long long m = rl32(mm, t);
-              if (m >= p.M) {
-                st |= 2u;
-                continue;
+          if (me - mb == 1) {
+            const unsigned long long m = rl32(h_m0, i);
+            if (m >= p.M) st |= 2u;
+            else forget_row(E + m * p.entry_mstride, r, lane, A);
+          } else {
+            for (u64 jb = mb; jb < me; jb += kWave) {
+              const unsigned mm = jb + lane < me ? p.mem[jb + lane] : 0u;
+              const int n = (int)((me - jb) < (u64)kWave ? (me - jb) : kWave);
+              for (int t = 0; t < n; ++t) {
+                const unsigned long long m = rl32(mm, t);
+                if (m >= p.M) {
+                  st |= 2u;
+                  continue;
+                }
+                forget_row(E + m * p.entry_mstride, r, lane, A);
               }
-              forget_row(E + m * p.entry_mstride, r, lane, A);
             }
           }
           wave_fence();
