@@ -256,6 +256,13 @@ __device__ __forceinline__ void map_apply_body(const MapApplyPlan &p) {
             if (j == ja) cj = C.w[j];
           if (rl64m(cj, la) >= kc) continue;  // seen (:123-126)
           const KeyRefs q = key_refs(p, s, k);
+          // the register's first kVB value rows in one batch of loads (clamped, unconditional, so
+          // they issue together and under the entry cell's round trip), the rest one at a time
+          constexpr int kVB = 4;
+          RowT<W> vb[kVB];
+#pragma unroll
+          for (int j = 0; j < kVB; ++j)
+            vb[j] = load_row<W>(q.vc + ((unsigned long long)j < p.V ? j : 0) * A, lane, A);
           if (lane == la) {  // entry clock apply(dot) (:130)
             u64 *cell = q.ec + a;
             if (*cell < kc) *cell = kc;
@@ -263,13 +270,6 @@ __device__ __forceinline__ void map_apply_body(const MapApplyPlan &p) {
           if (any_nz(oc)) {  // MVReg::apply (mvreg.rs:130-166)
             bool should_add = true;
             int last = -1, used = 0;
-            // the first kVB value rows in one batch of loads (clamped, unconditional, so they issue
-            // together), the rest one at a time
-            constexpr int kVB = 4;
-            RowT<W> vb[kVB];
-#pragma unroll
-            for (int j = 0; j < kVB; ++j)
-              vb[j] = load_row<W>(q.vc + ((unsigned long long)j < p.V ? j : 0) * A, lane, A);
             for (unsigned long long j = 0; j < p.V; ++j) {
               u64 *vr = q.vc + j * A;
               RowT<W> v;
