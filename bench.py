@@ -1,23 +1,31 @@
 #!/usr/bin/env python3
-"""Benchmark: batched CvRDT lub (replica-merges/s) on MI355X — BASELINE.json config 2 (default).
+"""Benchmark: batched CvRDT lub (replica-merges/s) on MI355X — BASELINE.json config 2 (`value`) and
+config 5 (the `c5` block of the same line).
 
 --workload c2 (default): one step = the two lubs of config 2 over HBM-resident synthetic replicas:
     GCounter  lub_many of 1,048,576 replicas x 256 actors (u64)       2 GiB read
     PNCounter lub_many of 1,048,576 replicas x (2 x 256) actors (u64)  4 GiB read
-= 2,097,152 replica-merges per rank per step.
---workload c5: one step = one GPU's shard of config 5, VClock lub_many of 1,048,576 replicas x
-1,024 actors (8 GiB read; 8 ranks = the 8M-replica config-5 input).
-With --gpus N (torchrun, one process per GPU) every rank holds its own 1M-replica shard of one
-global input (weak scaling) and each lub of the step is the C ABI's own sharded entry point
-(crdt_{gcounter,pncounter,vclock}_lub_many_sharded: local lub + ONE ncclAllReduce(ncclUint64,
-ncclMax) over the ctx's RCCL communicator, the path a Rust caller without torch.distributed
-takes; torch.distributed only ships the 128-byte unique id and runs the barriers).
-value = replica-merges of all ranks / max-over-ranks wall time.
+= 2,097,152 replica-merges per rank per step.  The same line then carries a `c5` block: one step =
+one GPU's shard of config 5, VClock lub_many of 1,048,576 replicas x 1,024 actors (8 GiB read; at
+--gpus 8 the global input is config 5's 8M replicas and the exchange its RCCL max all-reduce).
+--workload c5: config 5 as the headline instead (no second block).
+
+--gpus N > 1: one process per GPU.  Started without WORLD_SIZE, the script starts its own
+`python -m torch.distributed.run --nproc-per-node N` child BEFORE touching the GPU, relays rank 0's
+JSON line and exits with the child's status; under torchrun, WORLD_SIZE must equal --gpus.  Every
+rank holds its own 1M-replica shard of one global input (weak scaling) and each lub of the step is
+the C ABI's own sharded entry point (crdt_lub_many_multi_sharded / crdt_vclock_lub_many_sharded:
+local lub + ONE ncclAllReduce(ncclUint64, ncclMax) over the ctx's RCCL communicator, the path a Rust
+caller without torch.distributed takes; torch.distributed only ships the 128-byte unique id and
+runs the barriers).  --exchange cabi-ops runs the same C code over crdt_ctx_comm_init_ops with
+torch.distributed host callbacks (gloo: several ranks on one GPU); --exchange torch the
+torch.distributed twin.  value = replica-merges of all ranks / max-over-ranks wall time.
 
 The JSON line also carries
-  roofline      the dominant kernel (lub_stream_kernel, both launches of the step), its
-                average launch duration from HIP events on the launch stream vs the algorithmic
-                bytes per launch, against 8 TB/s;
+  step_ms       median / min / max of the per-step durations (HIP events around every step on the
+                launch stream, max over ranks per step); ms_per_step is the wall-clock mean
+  roofline      the dominant kernel, its average launch duration from HIP events on the launch
+                stream vs the algorithmic bytes per launch, against 8 TB/s
   cpu_baseline  the oracle's restated reference fold (VClock::merge over ordered maps) on a
                 bounded sample of the same workload, split over the host's threads (up to 16),
                 plus the one-thread figure (rank 0 at N=1 only).
@@ -25,6 +33,8 @@ The JSON line also carries
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -33,8 +43,10 @@ sys.path.insert(0, os.path.join(ROOT, "rust-crdt_amd"))
 
 R_REPLICAS = 1 << 20
 A_ACTORS = 256
+A_C5 = 1024
 SEED_G, SEED_P, SEED_V = 0x5EED0002, 0x5EED0003, 0x5EED0005
 HBM_PEAK_GBS = 8000.0
+METRIC = "replica-merges/sec (whole node) + achieved HBM GB/s as % of MI355X peak"
 
 
 def parse():
@@ -43,21 +55,43 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", choices=("c2", "c5"), default=os.environ.get("CRDT_BENCH_WORKLOAD", "c2"),
-                    help="c2: GCounter+PNCounter 1M x 256 (BASELINE config 2); c5: VClock 1M x 1024 per GPU "
-                         "(one shard of config 5)")
+                    help="c2: GCounter+PNCounter 1M x 256 (BASELINE config 2) + a config-5 block; c5: VClock "
+                         "1M x 1024 per GPU (one shard of config 5) only")
+    ap.add_argument("--c5", action=argparse.BooleanOptionalAction, default=True,
+                    help="with --workload c2: also time config 5's step and report it in the `c5` block")
     ap.add_argument("--replicas", type=int, default=R_REPLICAS, help="replicas per rank (configs 2 and 5: 1M)")
     ap.add_argument("--actors", type=int, default=None, help="default 256 (c2) / 1024 (c5)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="target fold seconds of the CPU baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--fused", action=argparse.BooleanOptionalAction, default=True,
                     help="all lubs of a step in one launch (crdt_lub_many_multi); --no-fused: one launch per lub")
-    ap.add_argument("--exchange", choices=("cabi", "torch"), default="cabi",
-                    help="N > 1: the C ABI's own RCCL communicator (crdt_*_lub_many_sharded) or torch.distributed")
+    ap.add_argument("--exchange", choices=("cabi", "cabi-ops", "torch"), default="cabi",
+                    help="N > 1: the C ABI over its own RCCL communicator, the C ABI over torch.distributed "
+                         "host callbacks (crdt_ctx_comm_init_ops), or the torch.distributed twin")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL on ROCm) for real runs; gloo lets several ranks share one GPU in tests")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="PMC-derived HBM bytes per launch (written by profiles/collect.sh)")
     return ap.parse_args()
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def self_launch(args):
+    """--gpus N > 1 without a torchrun environment: start N ranks in a fresh child (this process has
+    not touched the GPU) and relay its output and exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "4")
+    return subprocess.run(cmd, env=env).returncode
 
 
 def cpu_threads():
@@ -70,7 +104,7 @@ def cpu_threads():
     return max(1, min(16, n))
 
 
-def cpu_baseline(args):
+def cpu_baseline(args, workload, actors):
     """Restated reference fold (oracle, 'port'): VClock::merge (vclock.rs:130-136) over ordered
     maps for GCounter rows and P/N pairs for PNCounter rows, on a bounded sample of the same
     synthetic input — split over the host's threads (partials merged at the end, SURVEY §8d
@@ -86,24 +120,18 @@ def cpu_baseline(args):
         while fold_s < seconds and time.time() - t_start < 4 * seconds:
             n = per_thread * threads
             row0 = reps * n
-            g = O.synth_matrix(SEED_G, n, args.actors, 0, row0=row0)
-            _, tg = O.counter_fold_mt(g, False, threads)
-            p = O.synth_matrix(SEED_P, n, 2 * args.actors, 0, row0=row0)
-            _, tp = O.counter_fold_mt(p, True, threads)
-            fold_s += tg + tp
-            done_rows += 2 * n
-            reps += 1
-        return done_rows / fold_s, reps, fold_s
-
-    def run_c5(threads, per_thread, seconds):
-        done_rows, fold_s, reps = 0, 0.0, 0
-        t_start = time.time()
-        while fold_s < seconds and time.time() - t_start < 4 * seconds:
-            n = per_thread * threads
-            v = O.synth_matrix(SEED_V, n, args.actors, 0, row0=reps * n)
-            _, tv = O.counter_fold_mt(v, False, threads)
-            fold_s += tv
-            done_rows += n
+            if workload == "c5":
+                v = O.synth_matrix(SEED_V, n, actors, 0, row0=row0)
+                _, tv = O.counter_fold_mt(v, False, threads)
+                fold_s += tv
+                done_rows += n
+            else:
+                g = O.synth_matrix(SEED_G, n, actors, 0, row0=row0)
+                _, tg = O.counter_fold_mt(g, False, threads)
+                p = O.synth_matrix(SEED_P, n, 2 * actors, 0, row0=row0)
+                _, tp = O.counter_fold_mt(p, True, threads)
+                fold_s += tg + tp
+                done_rows += 2 * n
             reps += 1
         return done_rows / fold_s, reps, fold_s
 
@@ -111,8 +139,7 @@ def cpu_baseline(args):
         """SURVEY §8d CPU timing (3): the same fold on the dense SoA rows (elementwise u64 max over
         row ranges per thread, oracle_dense_max_mt) — the CPU's own bandwidth roofline."""
         done_rows, fold_s, reps = 0, 0.0, 0
-        width = args.actors
-        m = O.synth_matrix(SEED_V if args.workload == "c5" else SEED_G, rows_per_rep, width, 0)
+        m = O.synth_matrix(SEED_V if workload == "c5" else SEED_G, rows_per_rep, actors, 0)
         t_start = time.time()
         while fold_s < seconds and time.time() - t_start < 4 * seconds:
             _, t = O.dense_max_mt(m, threads)
@@ -121,15 +148,15 @@ def cpu_baseline(args):
             reps += 1
         return done_rows / fold_s, reps, fold_s, m.nbytes
 
-    if args.workload == "c5":
-        v1, reps1, s1 = run_c5(1, 4096, args.cpu_seconds / 2)
-        vT, repsT, sT = run_c5(T, 2048, args.cpu_seconds)
-        what = f"{repsT} x {T}x2048 VClock x {args.actors} replicas"
+    if workload == "c5":
+        v1, reps1, s1 = run(1, 4096, args.cpu_seconds / 2)
+        vT, repsT, sT = run(T, 2048, args.cpu_seconds)
+        what = f"{repsT} x {T}x2048 VClock x {actors} replicas"
         one = f"{reps1} x 4096 replicas, {s1:.2f} s of fold"
     else:
         v1, reps1, s1 = run(1, 16384, args.cpu_seconds / 2)
         vT, repsT, sT = run(T, 4096, args.cpu_seconds)
-        what = f"{repsT} x ({T}x4096 GCounter x {args.actors} + {T}x4096 PNCounter x 2x{args.actors}) replicas"
+        what = f"{repsT} x ({T}x4096 GCounter x {actors} + {T}x4096 PNCounter x 2x{actors}) replicas"
         one = f"{reps1} x (16384 + 16384) replicas, {s1:.2f} s of fold"
     vd, repsd, sd, nb = run_dense(T, 1 << 18, max(1.0, args.cpu_seconds / 4))
     return {
@@ -142,58 +169,77 @@ def cpu_baseline(args):
                    f"merge of the partials, map ingest excluded; {sT:.2f} s of fold"),
         "single_core": {"value": v1, "cores": 1, "sample": one},
         "dense_soa": {"value": vd, "cores": T, "GBs": vd * nb / (1 << 18) / 1e9,
-                      "sample": (f"{repsd} x elementwise max over {1 << 18} dense rows x {args.actors} u64 "
+                      "sample": (f"{repsd} x elementwise max over {1 << 18} dense rows x {actors} u64 "
                                  f"({nb / 2**20:.0f} MiB, {sd:.2f} s) split over {T} threads (oracle_dense_max_mt): "
                                  "the CPU fold without the reference's map containers")},
     }
 
 
-def main():
-    args = parse()
-    import numpy as np
-    import torch
-    import torch.distributed as dist
+class Env:
+    """The ranks, the ctx and the chosen exchange."""
 
-    import crdts_gpu as cg
-    from crdts_gpu import dist as cdist
+    def __init__(self, args):
+        import torch
+        import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    dev = local % torch.cuda.device_count()
-    torch.cuda.set_device(dev)
-    if world > 1:
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
-        else:
-            dist.init_process_group(args.dist_backend)
-    ctx = cg.Context.default(dev)
+        import crdts_gpu as cg
+        from crdts_gpu import dist as cdist
 
-    if args.actors is None:
-        args.actors = 1024 if args.workload == "c5" else A_ACTORS
-    R, A = args.replicas, args.actors
-    cabi = world > 1 and args.exchange == "cabi"
-    if cabi:  # the C ABI's own communicator; torch.distributed only ships the 128-byte id
-        uid = [cg.shard.unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        up = 1
-        try:
-            cg.shard.comm_init(ctx, uid[0], world, rank)
-        except Exception as e:  # every rank learns it below and all take the torch exchange together
-            print(f"rank {rank}: crdt_ctx_comm_init failed ({e}); using the torch.distributed exchange",
-                  file=sys.stderr)
-            up = 0
-        flag = torch.tensor([up], dtype=torch.int64, device="cuda")
-        cdist.all_reduce_(flag, dist.ReduceOp.MIN)
-        if not int(flag.item()):
-            if up:
-                cg.shard.comm_destroy(ctx)
-            cabi = False
-            args.exchange = "torch (C-ABI communicator setup failed)"
+        self.torch, self.dist, self.cg, self.cdist = torch, dist, cg, cdist
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.dev = local % torch.cuda.device_count()
+        torch.cuda.set_device(self.dev)
+        if self.world > 1:
+            if args.dist_backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", self.dev))
+            else:
+                dist.init_process_group(args.dist_backend)
+        self.ctx = cg.Context.default(self.dev)
+        self.exchange = args.exchange if self.world > 1 else "none"
+        self.cabi = self.world > 1 and args.exchange in ("cabi", "cabi-ops")
+        self.note = ""
+        if self.world > 1 and args.exchange == "cabi":
+            uid = [cg.shard.unique_id() if self.rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            up = 1
+            try:
+                cg.shard.comm_init(self.ctx, uid[0], self.world, self.rank)
+                self.note = cg.shard.comm_note(self.ctx)[0]
+            except Exception as e:  # every rank learns it below and all take the torch exchange together
+                print(f"rank {self.rank}: crdt_ctx_comm_init failed ({e}); using the torch.distributed exchange",
+                      file=sys.stderr)
+                up = 0
+            flag = torch.tensor([up], dtype=torch.int64, device="cuda")
+            cdist.all_reduce_(flag, dist.ReduceOp.MIN)
+            if not int(flag.item()):
+                if up:
+                    cg.shard.comm_destroy(self.ctx)
+                self.cabi = False
+                self.exchange = "torch (C-ABI communicator setup failed)"
+        elif self.world > 1 and args.exchange == "cabi-ops":
+            cg.shard.comm_init_ops(self.ctx, cg.shard.TorchCommOps(), self.world, self.rank)
+
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
+
+    def max_over_ranks(self, vals):
+        t = self.torch.tensor(vals, dtype=self.torch.float64, device="cuda")
+        if self.world > 1:
+            self.cdist.all_reduce_(t, self.dist.ReduceOp.MAX)
+        return t.tolist()
+
+
+def run_workload(args, env, workload):
+    """Generate the rank's shard in HBM, warm up, time args.steps steps; return the measured block."""
+    torch, cg, cdist = env.torch, env.cg, env.cdist
+    ctx, world, rank = env.ctx, env.world, env.rank
+    R = args.replicas
+    A = args.actors if (args.actors is not None and workload == args.workload) else (A_C5 if workload == "c5" else A_ACTORS)
     # Synthetic replicas, generated in HBM; rank k owns rows [k*R, (k+1)*R) of the global input.
-    if args.workload == "c5":
+    if workload == "c5":
         lubs = [("vclock", torch.empty((R, A), dtype=torch.int64, device="cuda"), SEED_V)]
     else:
         lubs = [("gcounter", torch.empty((R, A), dtype=torch.int64, device="cuda"), SEED_G),
@@ -202,13 +248,13 @@ def main():
         cg.synth_fill(ctx, x, seed, 0, first_row=rank * R)
     outs = [torch.empty((x.shape[1],), dtype=torch.int64, device="cuda") for _, x, _ in lubs]
     mods = {"vclock": cg.vclock, "gcounter": cg.gcounter, "pncounter": cg.pncounter}
+    items = [(kind, x, o) for (kind, x, _), o in zip(lubs, outs)]
+    fused = args.fused and len(lubs) > 1
     torch.cuda.synchronize()
 
-    items = [(kind, x, o) for (kind, x, _), o in zip(lubs, outs)]
-
     def step():
-        if args.fused:  # every lub of the step in ONE launch (crdt_lub_many_multi)
-            if cabi:  # + one grouped ncclAllReduce(ncclUint64, ncclMax) per step
+        if fused:  # every lub of the step in ONE launch (crdt_lub_many_multi)
+            if env.cabi:  # + one grouped all-reduce MAX per step
                 cg.shard.lub_many_multi_sharded(items, ctx=ctx)
             else:
                 cg.lub_many_multi(items, ctx=ctx)
@@ -217,7 +263,7 @@ def main():
                         cdist.allreduce_umax_(o)
             return
         for (kind, x, _), o in zip(lubs, outs):
-            if cabi:  # local lub + one ncclAllReduce(ncclUint64, ncclMax), one C call
+            if env.cabi:  # local lub + one all-reduce MAX, one C call
                 o.copy_(cg.shard.lub_many_sharded(kind, x, ctx=ctx))
             else:
                 mods[kind].lub_many(x, out=o, ctx=ctx)
@@ -227,107 +273,145 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    env.barrier()
     ctx.timing_reset()
     ctx.set_timing(True)
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    evs[0].record()
+    for i in range(args.steps):
         step()
+        evs[i + 1].record()
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    env.barrier()
     elapsed = time.perf_counter() - t0
     ctx.set_timing(False)
     kern_ms, launches = ctx.timing("lub_stream")
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        cdist.all_reduce_(t, dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    step_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
+    step_ms = env.max_over_ranks(step_ms)
+    elapsed = env.max_over_ranks([elapsed])[0]
 
     # Parity (outside the timed region): unsigned max with torch ops; for N > 1 the exchanged
-    # result must equal the max over every rank's torch reference (torch.distributed's own RCCL)
+    # result must equal the max over every rank's torch reference (torch.distributed's own exchange)
     sign = torch.tensor(-(2**63), dtype=torch.int64, device="cuda")
     refs = [(x ^ sign).amax(0) ^ sign for _, x, _ in lubs]
     got, ref = torch.cat(outs), torch.cat(refs)
     if world > 1:
         cdist.allreduce_umax_(ref)
-        t_ok = torch.tensor([1 if bool(torch.equal(got, ref)) else 0], dtype=torch.int64, device="cuda")
-        cdist.all_reduce_(t_ok, dist.ReduceOp.MIN)
-        ok = bool(t_ok.item())
-    else:
-        ok = bool(torch.equal(got, ref))
+    ok = env.max_over_ranks([0.0 if bool(torch.equal(got, ref)) else 1.0])[0] == 0.0
 
     merges_per_step = len(lubs) * R * world
-    value = merges_per_step * args.steps / elapsed
     bytes_per_step = sum(R * x.shape[1] * 8 + x.shape[1] * 8 for _, x, _ in lubs)
     launches_per_step = launches / args.steps if launches else float(len(lubs))
     avg_launch_bytes = bytes_per_step / launches_per_step
     avg_launch_s = (kern_ms / 1e3) / launches if launches else float("nan")
     achieved = avg_launch_bytes / avg_launch_s / 1e9
-    workload = (f"vclock lub {R}x{A} (config 5 shard)" if args.workload == "c5"
-                else f"gcounter+pncounter lub {R}x{A}")
+    srt = sorted(step_ms)
+    med = srt[len(srt) // 2] if len(srt) % 2 else 0.5 * (srt[len(srt) // 2 - 1] + srt[len(srt) // 2])
+    name = (f"vclock lub {R}x{A} (config 5 shard)" if workload == "c5" else f"gcounter+pncounter lub {R}x{A}")
     traffic = None
     try:
         with open(args.traffic_json) as f:
             tj = json.load(f)
-        if tj.get("workload") == workload and tj.get("fused", False) == bool(args.fused):
+        if tj.get("workload") == name and tj.get("fused", False) == bool(fused):
             traffic = tj.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
+    if env.cabi:
+        exch = ((f"C-ABI crdt_lub_many_multi_sharded: one grouped all-reduce MAX " if fused
+                 else "C-ABI crdt_*_lub_many_sharded: all-reduce MAX ")
+                + f"of the partial lubs ({sum(x.shape[1] for _, x, _ in lubs)} u64 words per step) over "
+                + ("the ctx's RCCL communicator (ncclUint64, ncclMax)" if args.exchange == "cabi"
+                   else "crdt_ctx_comm_init_ops host callbacks (torch.distributed " + args.dist_backend + ")"))
+    elif world > 1:
+        exch = f"torch.distributed all-reduce MAX (sign-biased u64); --exchange {env.exchange}"
+    else:
+        exch = "none"
+    block = {
+        "value": merges_per_step * args.steps / elapsed,
+        "unit": "replica-merges/s",
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "step_ms": {"median": med, "min": srt[0], "max": srt[-1], "source": "HIP events around each step, "
+                    "max over ranks"},
+        "config": {
+            "workload": name,
+            "replicas_per_gpu": R,
+            "actors": A,
+            "types": (["VClock (A u64)"] if workload == "c5" else ["GCounter (A u64)", "PNCounter (2A u64)"]),
+            "replica_merges_per_step": merges_per_step,
+            "exchange": exch,
+            "parallelism": f"replica-shard x{world}",
+            "launches_per_step": launches_per_step,
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": (("lub_multi_kernel<Max,2,8>" if fused else "lub_stream_kernel<Max,2,8>")
+                       + (" (VClock launch)" if workload == "c5" else
+                          (" (GCounter + PNCounter in one launch)" if fused else " (GCounter + PNCounter launches)"))),
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": traffic,
+            "avg_launch_us": avg_launch_s * 1e6,
+            "launches": launches,
+            "algorithmic_bytes_per_launch": avg_launch_bytes,
+        },
+        "parity": "ok" if ok else "MISMATCH",
+    }
+    del lubs, outs, items
+    torch.cuda.empty_cache()
+    return block, A
 
-    if rank == 0:
+
+def main():
+    args = parse()
+    world_env = os.environ.get("WORLD_SIZE")
+    if args.gpus > 1 and world_env is None:
+        sys.exit(self_launch(args))
+    world = int(world_env or "1")
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to time a different world "
+              "size than requested", file=sys.stderr)
+        sys.exit(2)
+    env = Env(args)
+    head, A = run_workload(args, env, args.workload)
+    c5 = None
+    if args.workload == "c2" and args.c5:
+        c5, _ = run_workload(args, env, "c5")
+    ok = head["parity"] == "ok" and (c5 is None or c5["parity"] == "ok")
+    if env.rank == 0:
         out = {
-            "metric": "replica-merges/sec (whole node) + achieved HBM GB/s as % of MI355X peak",
-            "value": value,
+            "metric": METRIC,
+            "value": head["value"],
             "unit": "replica-merges/s",
-            "n_gpus": world,
+            "n_gpus": env.world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3,
+            "ms_per_step": head["ms_per_step"],
+            "step_ms": head["step_ms"],
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u64",
             "data": "synthetic (counter-based splitmix64 replicas generated in HBM, seeds 0x5EED0002/3/5)",
-            "config": {
-                "workload": workload,
-                "replicas_per_gpu": R,
-                "actors": A,
-                "types": (["VClock (A u64)"] if args.workload == "c5" else ["GCounter (A u64)", "PNCounter (2A u64)"]),
-                "replica_merges_per_step": merges_per_step,
-                "exchange": (((f"C-ABI crdt_lub_many_multi_sharded: one grouped ncclAllReduce(ncclUint64, ncclMax) "
-                               if args.fused else "C-ABI crdt_*_lub_many_sharded: ncclAllReduce(ncclUint64, ncclMax) ")
-                              + f"of the partial lubs ({sum(x.shape[1] for _, x, _ in lubs)} words per step)") if cabi
-                             else f"torch.distributed all-reduce MAX (sign-biased u64); --exchange {args.exchange}")
-                if world > 1 else "none",
-                "parallelism": f"replica-shard x{world}",
-                "launches_per_step": launches_per_step,
-            },
-            "roofline": {
-                "bound": "hbm",
-                "kernel": (("lub_multi_kernel<Max,2,8>" if args.fused else "lub_stream_kernel<Max,2,8>")
-                           + (" (VClock launch)" if args.workload == "c5" else
-                              (" (GCounter + PNCounter in one launch)" if args.fused
-                               else " (GCounter + PNCounter launches)"))),
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS,
-                "traffic": traffic,
-                "avg_launch_us": avg_launch_s * 1e6,
-                "launches": launches,
-                "algorithmic_bytes_per_launch": avg_launch_bytes,
-            },
+            "config": head["config"],
+            "roofline": head["roofline"],
             "cpu_baseline": None,
-            "parity": "ok" if ok else "MISMATCH",
+            "parity": head["parity"],
         }
-        if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args)
+        if env.note:
+            out["config"]["rccl_note"] = env.note
+        if c5 is not None:
+            out["c5"] = dict(c5, metric=METRIC + " — BASELINE config 5 (VClock 1,024 actors; 8M replicas at 8 GPUs)")
+        if env.world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args, args.workload, A)
         print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    if env.world > 1:
+        if env.cabi:
+            env.cg.shard.comm_destroy(env.ctx)
+        env.dist.destroy_process_group()
     if not ok:
         sys.exit(3)
 

@@ -374,12 +374,44 @@ int crdt_map_merge_batch(crdt_ctx *ctx, const crdt_map_states *self, const crdt_
  *       def_members[d*Mw + w] (union over the survivors with that exact clock in the group) and
  *       def_group[d] (device u32), in group order.
  * The replaced reference operation is the same CvRDT::merge fold (traits.rs:4-7), split over
- * processes: a Rust caller would distribute the id over its own transport. */
+ * processes: a Rust caller would distribute the id over its own transport.
+ *
+ * Agreement: every *_sharded call first exchanges a small header (this rank's validation status
+ * and the call's rank-uniform dims: G, row width, M / K, A, D ...) and only runs its data
+ * collectives when every rank validated and the dims agree; otherwise EVERY rank returns an error
+ * (CRDT_EINVAL: its own validation failed, or the ranks disagree; CRDT_ECOMM with "another rank"
+ * in crdt_last_error: a peer's failed), so a bad argument on one rank never leaves the others
+ * blocked in a collective.  The header exchange runs on a side stream while the local fold runs.
+ *
+ * The caller's own collectives instead of RCCL (crdt_ctx_comm_init_ops): every *_sharded call then
+ * runs its exchange through these HOST callbacks on host buffers (the library copies device data
+ * to host memory and back around each call, after draining its stream).  A transport seam for
+ * callers with their own channel (MPI, TCP, a test harness) and for running the multi-rank code of
+ * this file with several ranks on one GPU.  Callbacks return 0 on success; any other value makes
+ * the sharded call return CRDT_ECOMM.
+ *   allgather:     recv[r*bytes .. (r+1)*bytes) = rank r's `send` bytes, for every rank r
+ *   allreduce_u64: buf[i] = op over the ranks of buf[i] (unsigned 64-bit; CRDT_RED_*) */
 #define CRDT_UNIQUE_ID_BYTES 128
+#define CRDT_RED_MAX 0
+#define CRDT_RED_MIN 1
+#define CRDT_RED_SUM 2
+typedef struct crdt_comm_ops {
+  void *user;
+  int (*allgather)(void *user, const void *send, void *recv, size_t bytes);
+  int (*allreduce_u64)(void *user, uint64_t *buf, size_t n, int op);
+} crdt_comm_ops;
 int crdt_comm_unique_id(uint8_t *id /* [CRDT_UNIQUE_ID_BYTES] */);
+/* Collective.  Also compares the RCCL runtime's version (ncclGetVersion) with the rccl.h this
+ * library was compiled against; a mismatch is not an error but is reported by crdt_ctx_comm_note. */
 int crdt_ctx_comm_init(crdt_ctx *ctx, const uint8_t *id, int nranks, int rank);
+/* Not collective (the callbacks are the caller's); ops is copied, its user pointer must stay
+ * valid until crdt_ctx_comm_destroy. */
+int crdt_ctx_comm_init_ops(crdt_ctx *ctx, const crdt_comm_ops *ops, int nranks, int rank);
 int crdt_ctx_comm_destroy(crdt_ctx *ctx);
 int crdt_ctx_comm_info(const crdt_ctx *ctx, int *nranks, int *rank);
+/* Text noted at comm init ("" if none), e.g. "RCCL runtime 2.22.3 != rccl.h 2.26.6"; storage
+ * owned by ctx.  *runtime / *header (may be NULL) = the RCCL version codes (0 without RCCL). */
+const char *crdt_ctx_comm_note(const crdt_ctx *ctx, int *runtime, int *header);
 int crdt_vclock_lub_many_sharded(crdt_ctx *ctx, const uint64_t *in, size_t G, size_t R, size_t A,
                                  size_t row_stride, size_t group_stride, uint64_t *out);
 int crdt_gcounter_lub_many_sharded(crdt_ctx *ctx, const uint64_t *in, size_t G, size_t R, size_t A,
@@ -481,6 +513,65 @@ int crdt_map_lub_many(crdt_ctx *ctx, const crdt_map_batch *in, crdt_map_out *out
  * [D][ceil(K/64)]: the surviving removes' key sets over ALL keys, assembled by one
  * ncclAllReduce(ncclSum) (disjoint ranges: sum = union).  def_keep is the same on every rank. */
 int crdt_map_lub_many_sharded(crdt_ctx *ctx, const crdt_map_batch *in, size_t k0, size_t K, crdt_map_out *out);
+
+/* ---- MVReg<u64, A> on its own (outside a Map) ------------------------------------------------
+ * Replaces MVReg::merge (mvreg.rs:112-128) and MVReg::apply (mvreg.rs:130-166) for registers in the
+ * dense layout the Map entry points use for their values: slots in Vec order, slot s of register i
+ * = (clock vclk[i*vclk_stride + s*A + a], value vval[i*vval_stride + s]); an empty slot is an
+ * all-zero clock row (skipped; results are written from slot 0, empty slots zeroed).  Values are
+ * u64 ids interned by the caller (merge and apply compare clocks only, never values).  Exact for
+ * any input: each register is folded / applied in order.
+ *   lub_many:    acc = MVReg::new(); for r in 0..R: acc.merge(replica[g][r]) per group g; replica
+ *                (g, r) at vclk + g*vclk_gstride + r*vclk_rstride (vval likewise).  out: Vout slots
+ *                per group (packed [G][Vout][A] / [G][Vout]), nval[g] (may be NULL), flags[g]: bit 0
+ *                = more than Vout values (slots incomplete: retry with a larger Vout), bit 2 = the
+ *                fold state overflowed (retry with Vstate = 16; past 16 values it is reported).
+ *   merge_batch: self[i].merge(other[i]), in place in self's V slots (own kept values, then other's
+ *                added ones); status[i] bit 4 = more than self's V values (register incomplete).
+ *   apply_batch: register i applies ops [op_off[i], op_off[i+1]) in order, Op::Put { clock:
+ *                clk_pool[clk_row[o]*A ..], val: val[o] }; status[i] bit 1 = an op's clk_row out
+ *                of range (skipped), bit 3 = op_off invalid (register untouched), bit 4 = more than
+ *                V values.
+ * Limits: A <= 256, 1 <= V <= 8 (lub_many: V <= 8, Vout <= 16). */
+typedef struct crdt_mvreg_states {
+  size_t N, A, V;
+  uint64_t *vclk;
+  size_t vclk_stride;
+  uint64_t *vval;
+  size_t vval_stride;
+} crdt_mvreg_states;
+
+typedef struct crdt_mvreg_batch {
+  size_t G, R, A, V;
+  const uint64_t *vclk;
+  size_t vclk_rstride, vclk_gstride;
+  const uint64_t *vval;
+  size_t vval_rstride, vval_gstride;
+} crdt_mvreg_batch;
+
+typedef struct crdt_mvreg_out {
+  size_t Vout;
+  size_t Vstate;   /* value capacity hint for the fold state (0 = from Vout and V) */
+  uint64_t *vclk;  /* [G][Vout][A] */
+  uint64_t *vval;  /* [G][Vout]    */
+  uint32_t *nval;  /* [G] or NULL  */
+  uint32_t *flags; /* [G]          */
+} crdt_mvreg_out;
+
+typedef struct crdt_mvreg_ops {
+  size_t n_ops;
+  const uint64_t *op_off;   /* [N+1]           */
+  const uint32_t *clk_row;  /* [n_ops]         */
+  const uint64_t *clk_pool; /* [n_clk_rows][A] */
+  size_t n_clk_rows;
+  const uint64_t *val;      /* [n_ops]         */
+} crdt_mvreg_ops;
+
+int crdt_mvreg_lub_many(crdt_ctx *ctx, const crdt_mvreg_batch *in, crdt_mvreg_out *out);
+int crdt_mvreg_merge_batch(crdt_ctx *ctx, const crdt_mvreg_states *self, const crdt_mvreg_states *other,
+                           uint32_t *status);
+int crdt_mvreg_apply_batch(crdt_ctx *ctx, const crdt_mvreg_states *states, const crdt_mvreg_ops *ops,
+                           uint32_t *status);
 
 /* ---- causal helpers on dense clock rows -----------------------------------
  * Row-pair ops over N pairs (x_i, y_i) of A-word rows (VClock, GCounter inner, or a PNCounter

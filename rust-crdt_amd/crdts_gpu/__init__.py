@@ -9,6 +9,6 @@ There is no CPU fallback: without the HIP library every call raises CrdtGpuUnava
 from ._abi import CrdtGpuError, CrdtGpuUnavailable, load as load_library  # noqa: F401
 from .context import Context, synth_fill  # noqa: F401
 from ._lattice import lub_many_multi  # noqa: F401
-from . import apply, causal, gcounter, gset, host, intern, lwwreg, map, orswot, pncounter, shard, synth, vclock, wire  # noqa: F401
+from . import apply, causal, gcounter, gset, host, intern, lwwreg, map, mvreg, orswot, pncounter, shard, synth, vclock, wire  # noqa: F401
 
 __version__ = "0.1.0"

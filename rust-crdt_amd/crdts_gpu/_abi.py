@@ -22,6 +22,7 @@ CRDT_ACCUMULATE = 0x1
 CRDT_MEM_DEVICE = 0
 CRDT_MEM_HOST = 1
 CRDT_KIND = {"vclock": 1, "gcounter": 2, "pncounter": 3, "gset": 4}
+CRDT_RED_MAX, CRDT_RED_MIN, CRDT_RED_SUM = 0, 1, 2
 
 # Every symbol declared in include/crdt_gpu.h (checked by tests/test_abi.py).
 EXPORTS = (
@@ -48,6 +49,8 @@ EXPORTS = (
     "crdt_orswot_merge_batch", "crdt_map_merge_batch",
     "crdt_ctx_set_mem_kind", "crdt_ctx_mem_kind", "crdt_host_alloc", "crdt_host_free",
     "crdt_lub_many_multi", "crdt_lub_many_multi_sharded", "crdt_map_ingest", "crdt_map_egress",
+    "crdt_ctx_comm_init_ops", "crdt_ctx_comm_note",
+    "crdt_mvreg_lub_many", "crdt_mvreg_merge_batch", "crdt_mvreg_apply_batch",
 )
 
 
@@ -119,6 +122,33 @@ class MapDeferred(ctypes.Structure):  # crdt_map_deferred
 class LubSegment(ctypes.Structure):  # crdt_lub_segment
     _fields_ = [("kind", ctypes.c_int), ("in_", P), ("G", S), ("R", S), ("A", S), ("row_stride", S),
                 ("group_stride", S), ("out", P), ("out_stride", S), ("flags", ctypes.c_uint)]
+
+
+class MVRegStates(ctypes.Structure):  # crdt_mvreg_states
+    _fields_ = [("N", S), ("A", S), ("V", S), ("vclk", P), ("vclk_stride", S), ("vval", P), ("vval_stride", S)]
+
+
+class MVRegBatch(ctypes.Structure):  # crdt_mvreg_batch
+    _fields_ = [("G", S), ("R", S), ("A", S), ("V", S), ("vclk", P), ("vclk_rstride", S), ("vclk_gstride", S),
+                ("vval", P), ("vval_rstride", S), ("vval_gstride", S)]
+
+
+class MVRegOut(ctypes.Structure):  # crdt_mvreg_out
+    _fields_ = [("Vout", S), ("Vstate", S), ("vclk", P), ("vval", P), ("nval", P), ("flags", P)]
+
+
+class MVRegOps(ctypes.Structure):  # crdt_mvreg_ops
+    _fields_ = [("n_ops", S), ("op_off", P), ("clk_row", P), ("clk_pool", P), ("n_clk_rows", S), ("val", P)]
+
+
+# crdt_comm_ops: the caller's own collectives (host buffers)
+ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
+ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_size_t,
+                                ctypes.c_int)
+
+
+class CommOps(ctypes.Structure):  # crdt_comm_ops
+    _fields_ = [("user", P), ("allgather", ALLGATHER_FN), ("allreduce_u64", ALLREDUCE_FN)]
 
 
 class MapBatch(ctypes.Structure):  # crdt_map_batch
@@ -200,6 +230,11 @@ _SIGS.update({
     "crdt_ctx_comm_init": ([P, P, ctypes.c_int, ctypes.c_int], ctypes.c_int),
     "crdt_ctx_comm_destroy": ([P], ctypes.c_int),
     "crdt_ctx_comm_info": ([P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
+    "crdt_mvreg_lub_many": ([P, ctypes.POINTER(MVRegBatch), ctypes.POINTER(MVRegOut)], ctypes.c_int),
+    "crdt_mvreg_merge_batch": ([P, ctypes.POINTER(MVRegStates), ctypes.POINTER(MVRegStates), P], ctypes.c_int),
+    "crdt_mvreg_apply_batch": ([P, ctypes.POINTER(MVRegStates), ctypes.POINTER(MVRegOps), P], ctypes.c_int),
+    "crdt_ctx_comm_init_ops": ([P, ctypes.POINTER(CommOps), ctypes.c_int, ctypes.c_int], ctypes.c_int),
+    "crdt_ctx_comm_note": ([P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)], ctypes.c_char_p),
     "crdt_orswot_lub_many_sharded": ([P, ctypes.POINTER(OrswotBatch), ctypes.POINTER(OrswotShardedOut)],
                                      ctypes.c_int),
 })

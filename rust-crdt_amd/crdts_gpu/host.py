@@ -36,6 +36,19 @@ class HostContext:
         if tune:
             self.call("crdt_ctx_tune", tune.encode())
 
+    _by_device: dict = {}
+
+    @classmethod
+    def default(cls, device: int = 0) -> "HostContext":
+        """One cached host-mode ctx per device for calls made without an explicit ctx (each ctx owns
+        two stage_kb device chunk buffers and an accumulator: a fresh one per call would churn
+        device memory until its finalizer ran)."""
+        ctx = cls._by_device.get(int(device))
+        if ctx is None or not getattr(ctx, "ptr", None):
+            ctx = cls(device)
+            cls._by_device[int(device)] = ctx
+        return ctx
+
     def call(self, name: str, *args) -> None:
         _abi.check(self.ptr, name, getattr(self.lib, name)(self.ptr, *args))
 
@@ -90,7 +103,7 @@ def lub_many(kind: str, replicas: np.ndarray, out: Optional[np.ndarray] = None, 
     """G folds over R host replicas: replicas (R, W) or (G, R, W) (W = A, 2A for pncounter,
     words for gset); rows may be strided views.  Returns (W,) or (G, W) in host memory."""
     prefix, wdiv = _KINDS[kind]
-    ctx = ctx or HostContext()
+    ctx = ctx or HostContext.default()
     _u64(replicas, "replicas")
     squeeze = replicas.ndim == 2
     r3 = replicas[None] if squeeze else replicas
@@ -118,7 +131,7 @@ def lub_many(kind: str, replicas: np.ndarray, out: Optional[np.ndarray] = None, 
 def merge_batch(kind: str, self_rows: np.ndarray, other_rows: np.ndarray, ctx: Optional[HostContext] = None) -> np.ndarray:
     """self[i] := self[i] ⊔ other[i] over host rows (N, W), in place; returns self_rows."""
     prefix, wdiv = _KINDS[kind]
-    ctx = ctx or HostContext()
+    ctx = ctx or HostContext.default()
     N, W, ss = _rows(_u64(self_rows, "self"), "self")
     N2, W2, os_ = _rows(_u64(other_rows, "other"), "other")
     if (N, W) != (N2, W2):
@@ -135,7 +148,7 @@ class LwwResult(NamedTuple):
 
 def lwwreg_lub_many(marker: np.ndarray, val: np.ndarray, ctx: Optional[HostContext] = None) -> LwwResult:
     """Folds of LWWReg::merge over host replicas: marker/val (R,) or (G, R) (crdt_lwwreg_lub_many)."""
-    ctx = ctx or HostContext()
+    ctx = ctx or HostContext.default()
     m2 = _u64(marker, "marker")[None] if marker.ndim == 1 else marker
     v2 = _u64(val, "val")[None] if val.ndim == 1 else val
     if m2.shape != v2.shape or m2.strides != v2.strides or m2.strides[1] != 8:
@@ -149,7 +162,7 @@ def lwwreg_lub_many(marker: np.ndarray, val: np.ndarray, ctx: Optional[HostConte
 def lwwreg_merge_batch(self_marker: np.ndarray, self_val: np.ndarray, other_marker: np.ndarray, other_val: np.ndarray,
                        ctx: Optional[HostContext] = None) -> np.ndarray:
     """self[i].merge(other[i]) in place over host arrays; returns the (N,) uint8 conflict flags."""
-    ctx = ctx or HostContext()
+    ctx = ctx or HostContext.default()
     arrs = [_u64(a, n) for a, n in ((self_marker, "self_marker"), (self_val, "self_val"),
                                      (other_marker, "other_marker"), (other_val, "other_val"))]
     N = arrs[0].shape[0]
@@ -172,7 +185,7 @@ def orswot_lub_many(clock: np.ndarray, entries: np.ndarray, def_off=None, def_cl
     """crdt_orswot_lub_many on host arrays: clock (G, R, A), entries (G, R, M, A) (or without G),
     deferred removes pooled per group (def_off G+1, def_clock (D, A), def_members (D, Mw)).  The
     library stages the whole batch (the deferred survival test needs every replica's clock)."""
-    ctx = ctx or HostContext()
+    ctx = ctx or HostContext.default()
     c = clock[None] if clock.ndim == 2 else clock
     e = entries[None] if entries.ndim == 3 else entries
     c = np.ascontiguousarray(_u64(c, "clock"))
@@ -211,7 +224,7 @@ def orswot_merge_batch(self_states, other_states, ctx: Optional[HostContext] = N
     """crdt_orswot_merge_batch on host arrays, in place on self: each side a tuple (clock (N, A),
     entries (N, M, A), def_clock (N, Dcap, A), def_members (N, Dcap, Mw), def_count (N,) uint32)
     of C-contiguous arrays.  Returns status (N,) uint32."""
-    ctx = ctx or HostContext()
+    ctx = ctx or HostContext.default()
     structs = []
     for side in (self_states, other_states):
         clock, entries, dcl, dmb, cnt = side
@@ -247,7 +260,7 @@ def map_lub_many(clock, ec, vclk, vval, def_off=None, def_row=None, def_clock=No
     """crdt_map_lub_many on host arrays (one group): clock (R, A), ec (R, K, A), vclk (R, K, V, A),
     vval (R, K, V); removes pooled (def_off [0, D], def_row (D,) uint32, def_clock (D, A),
     def_keys (D, Kw)).  Whole-batch staging by the library."""
-    ctx = ctx or HostContext()
+    ctx = ctx or HostContext.default()
     arrs = [np.ascontiguousarray(_u64(x, n)) for x, n in ((clock, "clock"), (ec, "ec"), (vclk, "vclk"), (vval, "vval"))]
     c, e, vc, vv = arrs
     R, A = c.shape
@@ -286,7 +299,7 @@ def map_merge_batch(self_states, other_states, ctx: Optional[HostContext] = None
     """crdt_map_merge_batch on host arrays, in place on self: each side a tuple (clock (N, A),
     ec (N, K, A), vclk (N, K, V, A), vval (N, K, V), def_clock (N, Dcap, A), def_keys (N, Dcap, Kw),
     def_count (N,) uint32) of C-contiguous arrays.  Returns status (N,) uint32."""
-    ctx = ctx or HostContext()
+    ctx = ctx or HostContext.default()
     ss, dd = [], []
     for side in (self_states, other_states):
         clock, ec, vclk, vval, dcl, dks, cnt = side

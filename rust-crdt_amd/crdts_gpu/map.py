@@ -129,10 +129,12 @@ def lub_many(clock: torch.Tensor, ec: torch.Tensor, vclk: torch.Tensor, vval: to
             f |= int(x)
         if f & 2:
             raise ValueError("map.lub_many: def_row must be non-decreasing within each group and < R")
-        if f & 4 and vstate < 16:  # the fold state overflowed: rerun with the next larger state
+        # the fold state overflowed: rerun with the next larger state (a key-sharded call already
+        # did that inside the C entry point, on every rank together)
+        if f & 4 and vstate < 16 and _key_shard is None:
             return lub_many(clock, ec, vclk, vval, def_off, def_row, def_clock, def_keys, vout, ctx,
                             check, vstate=8 if vstate < 8 else 16, _key_shard=_key_shard)
-        if f & 4:
+        if f & 4 and (vstate >= 16 or _key_shard is not None):
             raise MapCapacityError("map.lub_many: a key held more than 16 MVReg values during the "
                                    "fold (the kernel's state capacity); results incomplete")
         if f & 1:

@@ -3,15 +3,20 @@
 
     uid = unique_id()                       # rank 0; distribute the 128 bytes to every rank
     comm_init(ctx, uid, nranks, rank)       # collective
+    # or the caller's own collectives instead of RCCL (crdt_ctx_comm_init_ops), e.g. gloo:
+    comm_init_ops(ctx, TorchCommOps(), nranks, rank)
     lub_many_sharded("gcounter", shard)     # collective: every rank gets the global lub
     orswot_lub_many_sharded(clock, entries, def_off, def_clock, def_members)
     lwwreg_lub_many_sharded(marker, val, base)       # replicas [base, base + R_k) of the global order
     map_lub_many_sharded(clock, ec, vclk, vval, k0, K, ...)   # KEY shards [k0, k0 + K_k)
 
-`crdts_gpu.dist` is the torch.distributed twin of the same exchange (gloo-testable on CPU)."""
+Every *_sharded call is collective and agrees on its validation status first: a bad argument on one
+rank makes EVERY rank raise (CrdtGpuError), none blocks.  `crdts_gpu.dist` is the torch.distributed
+twin of the same exchange (gloo-testable on CPU)."""
 from __future__ import annotations
 
 import ctypes
+import warnings
 from typing import NamedTuple, Optional, Sequence
 
 import numpy as np
@@ -34,10 +39,78 @@ def comm_init(ctx: Context, uid: bytes, nranks: int, rank: int) -> None:
         raise ValueError(f"comm_init: unique id must be {_abi.CRDT_UNIQUE_ID_BYTES} bytes")
     buf = (ctypes.c_uint8 * _abi.CRDT_UNIQUE_ID_BYTES).from_buffer_copy(uid)
     ctx.call("crdt_ctx_comm_init", buf, int(nranks), int(rank))
+    note = comm_note(ctx)[0]
+    if note:
+        warnings.warn(f"crdt_ctx_comm_init: {note}", RuntimeWarning, stacklevel=2)
+
+
+def comm_note(ctx: Context):
+    """(note text, RCCL runtime version, rccl.h version) — crdt_ctx_comm_note."""
+    rt, hd = ctypes.c_int(), ctypes.c_int()
+    txt = _abi.load().crdt_ctx_comm_note(ctx.ptr, ctypes.byref(rt), ctypes.byref(hd))
+    return (txt or b"").decode(), rt.value, hd.value
+
+
+class TorchCommOps:
+    """crdt_comm_ops backed by torch.distributed on host tensors (gloo, or any backend with CPU
+    collectives): the caller's-own-transport seam of the C ABI.  The unsigned reductions are done
+    exactly on uint64 after an all-gather (gloo's int64 MAX / MIN are signed)."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+        self.dist = dist
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.errors = []
+
+        def allgather(user, send, recv, nbytes):
+            try:
+                src = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(send))
+                t = torch.from_numpy(src.copy())
+                parts = [torch.empty_like(t) for _ in range(self.world)]
+                self.dist.all_gather(parts, t, group=self.group)
+                dst = np.ctypeslib.as_array((ctypes.c_uint8 * (nbytes * self.world)).from_address(recv))
+                dst[:] = torch.cat(parts).numpy()
+                return 0
+            except Exception as e:  # noqa: BLE001 - reported to the C side as a failed collective
+                self.errors.append(repr(e))
+                return 1
+
+        def allreduce(user, buf, n, op):
+            try:
+                arr = np.ctypeslib.as_array(buf, shape=(n,))
+                t = torch.from_numpy(arr.view(np.int64).copy())
+                parts = [torch.empty_like(t) for _ in range(self.world)]
+                self.dist.all_gather(parts, t, group=self.group)
+                st = np.stack([p.numpy().view(np.uint64) for p in parts])
+                if op == _abi.CRDT_RED_MAX:
+                    arr[:] = st.max(0)
+                elif op == _abi.CRDT_RED_MIN:
+                    arr[:] = st.min(0)
+                elif op == _abi.CRDT_RED_SUM:
+                    arr[:] = st.sum(0, dtype=np.uint64)
+                else:
+                    return 2
+                return 0
+            except Exception as e:  # noqa: BLE001
+                self.errors.append(repr(e))
+                return 1
+
+        self._ag = _abi.ALLGATHER_FN(allgather)
+        self._ar = _abi.ALLREDUCE_FN(allreduce)
+        self.ops = _abi.CommOps(None, self._ag, self._ar)
+
+
+def comm_init_ops(ctx: Context, ops, nranks: int, rank: int) -> None:
+    """crdt_ctx_comm_init_ops: the sharded entry points exchange through `ops` (an object with a
+    `.ops` crdt_comm_ops struct, e.g. TorchCommOps) instead of RCCL.  The ctx keeps a reference."""
+    ctx.call("crdt_ctx_comm_init_ops", ctypes.byref(ops.ops), int(nranks), int(rank))
+    ctx._comm_ops = ops  # the callbacks must outlive the communicator
 
 
 def comm_destroy(ctx: Context) -> None:
     ctx.call("crdt_ctx_comm_destroy")
+    ctx._comm_ops = None
 
 
 def comm_info(ctx: Context):

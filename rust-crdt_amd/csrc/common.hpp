@@ -111,6 +111,18 @@ struct crdt_ctx {
   void (*comm_destroy)(void *) = nullptr;
   void *sbuf[8] = {};
   size_t sbuf_bytes[8] = {};
+  // ... or the caller's own collectives (crdt_ctx_comm_init_ops) instead of RCCL
+  bool has_ops = false;
+  crdt_comm_ops ops{};
+  // validation agreement before the first data collective of every sharded call: a side stream
+  // (so the agreement overlaps the local fold), its events, a device and a pinned host header
+  // buffer of nranks rows; released by comm_release (shard.hip)
+  hipStream_t astream = nullptr;
+  hipEvent_t a_main = nullptr, a_done = nullptr;
+  void *a_dev = nullptr, *a_host = nullptr;
+  size_t a_rows = 0;
+  std::string comm_note;  // e.g. an RCCL runtime / header version mismatch found at init
+  void (*comm_release)(crdt_ctx *) = nullptr;
   // Host-memory mode (csrc/host_stage.hip): CRDT_MEM_DEVICE / CRDT_MEM_HOST, the copy stream, two
   // device chunk buffers with their copied / free events, and the device accumulator.
   int mem_kind = CRDT_MEM_DEVICE;

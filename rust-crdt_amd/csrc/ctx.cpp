@@ -260,6 +260,7 @@ int crdt_ctx_destroy(crdt_ctx *ctx) {
   if (ctx->pinned_done) (void)hipEventDestroy(ctx->pinned_done);
   free_stage(ctx);
   if (ctx->comm && ctx->comm_destroy) ctx->comm_destroy(ctx->comm);
+  if (ctx->comm_release) ctx->comm_release(ctx);
   for (void *b : ctx->sbuf)
     if (b) (void)hipFree(b);
   delete ctx;

@@ -1,23 +1,36 @@
 // Replica-sharded lub across the GPUs of a node through the C ABI: one process
 // (one crdt_ctx) per GPU, joined into an RCCL communicator by a unique id the caller distributes
-// (a Rust caller over its own transport; the Python host over torch.distributed).
+// (a Rust caller over its own transport; the Python host over torch.distributed), or into the
+// caller's own collectives (crdt_ctx_comm_init_ops: host callbacks, e.g. MPI, TCP or gloo).
 //
 //   VClock / GCounter / PNCounter: local lub of the rank's replica shard, then ONE in-place
-//       ncclAllReduce(ncclUint64, ncclMax) of the G x W partials over xGMI: max is the join.
-//   GSet: local lub, ncclAllGather of the partial bitmaps, OR-fold of the world partials by the
+//       all-reduce MAX of the G x W partials over xGMI: max is the join.
+//   GSet: local lub, all-gather of the partial bitmaps, OR-fold of the world partials by the
 //       same lattice kernel (RCCL has no bitwise-OR reduction).
 //   Orswot: each rank joins its shard WITHOUT deferred removes (the dot-store join is associative
 //       under the reference invariants), the partial (clock, entries) are all-gathered and every
 //       rank re-merges the world partials together with ALL ranks' deferred removes (the forget
 //       ceiling and the survival test need the global clock: orswot.rs:141-147, :240-249).
-// Every rank ends with the same global result.  Multi-GPU tests without several GPUs: the
-// Python host path (crdts_gpu/dist.py) runs the same exchange under gloo on CPU; this file is
-// exercised at world size 1 on one MI355X (tests/test_gpu_shard_abi.py).
+//   LWWReg: the rank states are all-gathered, every rank continues its shard from the fold of the
+//       lower ranks' states (the error of lwwreg.rs:84-98 is order-dependent), MIN all-reduce.
+//   Map<K, MVReg>: key shards (each rank's keys are an exact left fold), SUM all-reduce of the
+//       surviving removes' key bitmaps.
+// Every rank ends with the same global result.
+//
+// Collective discipline (VERDICT r2 / ADVICE r2): every call validates locally and runs its local
+// fold, then ONE header all-gather (status + the call's rank-uniform dims) decides for all ranks at
+// once whether the data collectives run; every branch around a collective depends on rank-uniform
+// values only, so a bad argument or an empty shard on one rank never leaves the others blocked.
+// The header exchange runs on a side stream that waits only for the work issued BEFORE the call,
+// so it overlaps the local fold instead of adding a host round trip after it.
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cstring>
+#include <initializer_list>
 
 #include "common.hpp"
+#include "shard_host.hpp"
 
 namespace crdt {
 
@@ -31,6 +44,12 @@ static int nccl_fail(crdt_ctx *ctx, ncclResult_t r, const char *what) {
   do {                                                         \
     ncclResult_t _r = (expr);                                  \
     if (_r != ncclSuccess) return crdt::nccl_fail((ctx), _r, #expr); \
+  } while (0)
+
+#define CRDT_TRY(expr)             \
+  do {                             \
+    int _s = (expr);               \
+    if (_s != CRDT_OK) return _s;  \
   } while (0)
 
 static void destroy_comm(void *c) { (void)ncclCommDestroy((ncclComm_t)c); }
@@ -56,11 +75,151 @@ static int sbuf(crdt_ctx *ctx, int i, size_t bytes, void **out) {
   return CRDT_OK;
 }
 
-#define CRDT_TRY(expr)             \
-  do {                             \
-    int _s = (expr);               \
-    if (_s != CRDT_OK) return _s;  \
-  } while (0)
+static int need_comm(crdt_ctx *ctx) {
+  if (!ctx->comm && !ctx->has_ops)
+    return fail(ctx, CRDT_EINVAL, "sharded call without crdt_ctx_comm_init / crdt_ctx_comm_init_ops");
+  return CRDT_OK;
+}
+
+// ---- collectives over the ctx's backend: device buffers, ordered on the ctx stream --------------
+enum class Red : int { Max = CRDT_RED_MAX, Min = CRDT_RED_MIN, Sum = CRDT_RED_SUM };
+
+static int coll_group_begin(crdt_ctx *ctx) {
+  if (ctx->comm) CRDT_NCCL(ctx, ncclGroupStart());
+  return CRDT_OK;
+}
+static int coll_group_end(crdt_ctx *ctx) {
+  if (ctx->comm) CRDT_NCCL(ctx, ncclGroupEnd());
+  return CRDT_OK;
+}
+
+static int ops_fail(crdt_ctx *ctx, int rc, const char *what) {
+  return fail(ctx, CRDT_ECOMM, "%s: the caller's collective callback returned %d", what, rc);
+}
+
+// dst[i] = op over the ranks of src[i] (u64; dst may equal src)
+static int coll_allreduce(crdt_ctx *ctx, const u64 *src, u64 *dst, size_t n, Red op) {
+  if (n == 0) return CRDT_OK;
+  if (ctx->comm) {
+    const ncclRedOp_t r = op == Red::Max ? ncclMax : (op == Red::Min ? ncclMin : ncclSum);
+    CRDT_NCCL(ctx, ncclAllReduce(src, dst, n, ncclUint64, r, (ncclComm_t)ctx->comm, ctx->stream));
+    return CRDT_OK;
+  }
+  std::vector<uint64_t> h(n);
+  CRDT_HIP(ctx, hipMemcpyAsync(h.data(), src, n * 8, hipMemcpyDeviceToHost, ctx->stream));
+  CRDT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (int rc = ctx->ops.allreduce_u64(ctx->ops.user, h.data(), n, (int)op)) return ops_fail(ctx, rc, "allreduce_u64");
+  CRDT_HIP(ctx, hipMemcpyAsync(dst, h.data(), n * 8, hipMemcpyHostToDevice, ctx->stream));
+  CRDT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return CRDT_OK;
+}
+
+// recv[r*bytes ..] = rank r's send bytes
+static int coll_allgather(crdt_ctx *ctx, const void *send, void *recv, size_t bytes) {
+  if (bytes == 0) return CRDT_OK;
+  if (ctx->comm) {
+    if (bytes % 8 == 0)
+      CRDT_NCCL(ctx, ncclAllGather(send, recv, bytes / 8, ncclUint64, (ncclComm_t)ctx->comm, ctx->stream));
+    else
+      CRDT_NCCL(ctx, ncclAllGather(send, recv, bytes, ncclUint8, (ncclComm_t)ctx->comm, ctx->stream));
+    return CRDT_OK;
+  }
+  std::vector<uint8_t> hs(bytes), hr(bytes * (size_t)ctx->nranks);
+  CRDT_HIP(ctx, hipMemcpyAsync(hs.data(), send, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  CRDT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (int rc = ctx->ops.allgather(ctx->ops.user, hs.data(), hr.data(), bytes)) return ops_fail(ctx, rc, "allgather");
+  CRDT_HIP(ctx, hipMemcpyAsync(recv, hr.data(), hr.size(), hipMemcpyHostToDevice, ctx->stream));
+  CRDT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return CRDT_OK;
+}
+
+// ---- validation agreement ------------------------------------------------------------------
+// Header row of every rank: [failed, tag, d0..d4, hash(all dims)] (shard_host.hpp); tag names the
+// entry point.
+using shard_host::Hdr;
+using shard_host::kHdr;
+enum : uint64_t { kTagMax = 1, kTagOr, kTagOrswot, kTagMulti, kTagLww, kTagMap };
+
+static Hdr make_hdr(int st, uint64_t tag, std::initializer_list<uint64_t> dims) {
+  return shard_host::make_hdr(st != CRDT_OK, tag, dims);
+}
+
+static void comm_release(crdt_ctx *ctx) {
+  if (ctx->astream) (void)hipStreamSynchronize(ctx->astream);
+  if (ctx->a_dev) (void)hipFree(ctx->a_dev);
+  if (ctx->a_host) (void)hipHostFree(ctx->a_host);
+  if (ctx->a_main) (void)hipEventDestroy(ctx->a_main);
+  if (ctx->a_done) (void)hipEventDestroy(ctx->a_done);
+  if (ctx->astream) (void)hipStreamDestroy(ctx->astream);
+  ctx->a_dev = ctx->a_host = nullptr;
+  ctx->a_main = ctx->a_done = nullptr;
+  ctx->astream = nullptr;
+  ctx->a_rows = 0;
+}
+
+static int agree_setup(crdt_ctx *ctx) {
+  const size_t rows = (size_t)ctx->nranks + 1;  // nranks gathered rows + this rank's send row
+  if (ctx->a_rows >= rows) return CRDT_OK;
+  comm_release(ctx);
+  ctx->comm_release = comm_release;
+  CRDT_HIP(ctx, hipHostMalloc(&ctx->a_host, rows * kHdr * 8, hipHostMallocDefault));
+  if (ctx->comm) {
+    CRDT_HIP(ctx, hipMalloc(&ctx->a_dev, rows * kHdr * 8));
+    CRDT_HIP(ctx, hipStreamCreateWithFlags(&ctx->astream, hipStreamNonBlocking));
+    CRDT_HIP(ctx, hipEventCreateWithFlags(&ctx->a_main, hipEventDisableTiming));
+    CRDT_HIP(ctx, hipEventCreateWithFlags(&ctx->a_done, hipEventDisableTiming));
+  }
+  ctx->a_rows = rows;
+  return CRDT_OK;
+}
+
+// Call first: marks the work issued before the call (the header exchange waits for it, not for
+// the local fold the call issues next).
+static int agree_mark(crdt_ctx *ctx) {
+  CRDT_TRY(agree_setup(ctx));
+  if (ctx->comm) CRDT_HIP(ctx, hipEventRecord(ctx->a_main, ctx->stream));
+  return CRDT_OK;
+}
+
+// Exchange the headers; CRDT_OK on every rank iff every rank validated and the dims agree.
+static int agree(crdt_ctx *ctx, int st, const Hdr &mine, const char *what) {
+  const size_t W = (size_t)ctx->nranks;
+  uint64_t *h = static_cast<uint64_t *>(ctx->a_host);
+  uint64_t *send_h = h + W * kHdr;
+  std::memcpy(send_h, mine.w, sizeof mine.w);
+  if (ctx->comm) {
+    uint64_t *d = static_cast<uint64_t *>(ctx->a_dev);
+    CRDT_HIP(ctx, hipStreamWaitEvent(ctx->astream, ctx->a_main, 0));
+    CRDT_HIP(ctx, hipMemcpyAsync(d + W * kHdr, send_h, kHdr * 8, hipMemcpyHostToDevice, ctx->astream));
+    CRDT_NCCL(ctx, ncclAllGather(d + W * kHdr, d, kHdr, ncclUint64, (ncclComm_t)ctx->comm, ctx->astream));
+    CRDT_HIP(ctx, hipMemcpyAsync(h, d, W * kHdr * 8, hipMemcpyDeviceToHost, ctx->astream));
+    CRDT_HIP(ctx, hipEventRecord(ctx->a_done, ctx->astream));
+    CRDT_HIP(ctx, hipEventSynchronize(ctx->a_done));
+  } else {
+    if (int rc = ctx->ops.allgather(ctx->ops.user, send_h, h, kHdr * 8)) return ops_fail(ctx, rc, "allgather");
+  }
+  long bad_rank, odd_rank;
+  if (shard_host::check_headers(h, W, mine, &bad_rank, &odd_rank)) return CRDT_OK;
+  if (bad_rank >= 0) {
+    if (st != CRDT_OK) return st;  // this rank's own error text is in last_error
+    return fail(ctx, CRDT_ECOMM, "%s: another rank (%ld) failed its validation (see that rank's "
+                "crdt_last_error); no data was exchanged", what, bad_rank);
+  }
+  const uint64_t *o = h + (size_t)odd_rank * kHdr;
+  return fail(ctx, CRDT_EINVAL, "%s: the ranks disagree on the call (rank %ld: tag %llu dims %llu %llu %llu %llu "
+              "%llu; rank %d: tag %llu dims %llu %llu %llu %llu %llu); no data was exchanged", what, odd_rank,
+              (unsigned long long)o[1], (unsigned long long)o[2], (unsigned long long)o[3], (unsigned long long)o[4],
+              (unsigned long long)o[5], (unsigned long long)o[6], ctx->rank, (unsigned long long)mine.w[1],
+              (unsigned long long)mine.w[2], (unsigned long long)mine.w[3], (unsigned long long)mine.w[4],
+              (unsigned long long)mine.w[5], (unsigned long long)mine.w[6]);
+}
+
+static int device_mem_only(crdt_ctx *ctx, const char *what) {
+  if (ctx->mem_kind != CRDT_MEM_DEVICE)
+    return fail(ctx, CRDT_EUNSUPPORTED, "%s: device pointers only (CRDT_MEM_HOST is supported by the lattice "
+                "and lwwreg lub_many / merge_batch)", what);
+  return CRDT_OK;
+}
 
 // dst row i <- src row idx[i] (rows of W u64 words)
 __global__ __launch_bounds__(kBlock) void gather_rows_kernel(u64 *dst, const u64 *src, const uint32_t *idx,
@@ -83,38 +242,39 @@ static int gather_rows(crdt_ctx *ctx, u64 *dst, const u64 *src, const uint32_t *
   return CRDT_OK;
 }
 
-static int need_comm(crdt_ctx *ctx) {
-  if (!ctx->comm) return fail(ctx, CRDT_EINVAL, "sharded call without crdt_ctx_comm_init");
-  return CRDT_OK;
-}
-
 static int lattice_sharded(crdt_ctx *ctx, Op op, const u64 *in, size_t G, size_t R, size_t W, size_t row_stride,
-                           size_t group_stride, u64 *out) {
+                           size_t group_stride, u64 *out, const char *what) {
   CRDT_CHECK_CTX(ctx);
   CRDT_TRY(need_comm(ctx));
-  if (G == 0 || W == 0) return CRDT_OK;
-  if (!out) return fail(ctx, CRDT_EINVAL, "lub_many_sharded: out is NULL");
   CRDT_HIP(ctx, hipSetDevice(ctx->device));
-  auto comm = (ncclComm_t)ctx->comm;
+  CRDT_TRY(agree_mark(ctx));
   const size_t n = G * W;
+  int st = device_mem_only(ctx, what);
+  void *part = nullptr, *all = nullptr;
+  if (!st && n && !out) st = fail(ctx, CRDT_EINVAL, "%s: out is NULL", what);
+  if (!st && n) {
+    if (op == Op::Max) {
+      st = lattice_lub_many(ctx, op, in, G, R, W, row_stride, group_stride, out, W, 0);
+    } else {
+      st = sbuf(ctx, 0, n * 8, &part);
+      if (!st) st = sbuf(ctx, 1, n * 8 * ctx->nranks, &all);
+      if (!st) st = lattice_lub_many(ctx, op, in, G, R, W, row_stride, group_stride, (u64 *)part, W, 0);
+    }
+  }
+  CRDT_TRY(agree(ctx, st, make_hdr(st, op == Op::Max ? kTagMax : kTagOr, {G, W}), what));
+  if (n == 0) return CRDT_OK;
   if (op == Op::Max) {
-    CRDT_TRY(lattice_lub_many(ctx, op, in, G, R, W, row_stride, group_stride, out, W, 0));
     timing_begin(ctx, "shard_exchange");
-    CRDT_NCCL(ctx, ncclAllReduce(out, out, n, ncclUint64, ncclMax, comm, ctx->stream));
+    CRDT_TRY(coll_allreduce(ctx, out, out, n, Red::Max));
     timing_end(ctx);
     return CRDT_OK;
   }
   // GSet: partial -> all-gather [nranks][G][W] -> OR over the nranks "replicas" of each group
-  void *part = nullptr, *all = nullptr;
-  CRDT_TRY(sbuf(ctx, 0, n * 8, &part));
-  CRDT_TRY(sbuf(ctx, 1, n * 8 * ctx->nranks, &all));
-  CRDT_TRY(lattice_lub_many(ctx, op, in, G, R, W, row_stride, group_stride, (u64 *)part, W, 0));
   timing_begin(ctx, "shard_exchange");
-  CRDT_NCCL(ctx, ncclAllGather(part, all, n, ncclUint64, comm, ctx->stream));
+  CRDT_TRY(coll_allgather(ctx, part, all, n * 8));
   timing_end(ctx);
   return lattice_lub_many(ctx, op, (const u64 *)all, G, ctx->nranks, W, n, W, out, W, 0);
 }
-
 
 // LWWReg exchange: tm[g*n + j] / tv[g*n + j] <- marker / val of group g of rank ranks[j] in the
 // gathered [nranks][2G+1] buffer (so the world states of a group are one contiguous "replica" row)
@@ -165,6 +325,12 @@ static unsigned small_grid(crdt_ctx *ctx, unsigned long long n) {
   return (unsigned)(want == 0 ? 1 : (want < cap ? want : cap));
 }
 
+__global__ void widen_u32_kernel(u64 *dst, const uint32_t *src, unsigned long long n, u64 extra) {
+  for (unsigned long long i = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x; i <= n;
+       i += (unsigned long long)gridDim.x * blockDim.x)
+    dst[i] = i < n ? (u64)src[i] : extra;
+}
+
 }  // namespace crdt
 
 using namespace crdt;
@@ -183,8 +349,17 @@ int crdt_ctx_comm_init(crdt_ctx *ctx, const uint8_t *id, int nranks, int rank) {
   CRDT_CHECK_CTX(ctx);
   if (!id || nranks < 1 || rank < 0 || rank >= nranks)
     return fail(ctx, CRDT_EINVAL, "crdt_ctx_comm_init: bad id / nranks %d / rank %d", nranks, rank);
-  if (ctx->comm) return fail(ctx, CRDT_EINVAL, "crdt_ctx_comm_init: ctx already has a communicator");
+  if (ctx->comm || ctx->has_ops) return fail(ctx, CRDT_EINVAL, "crdt_ctx_comm_init: ctx already has a communicator");
   CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  // the process may have loaded another librccl.so.1 first (torch ships its own): note a mismatch
+  int v = 0;
+  ctx->comm_note.clear();
+  if (ncclGetVersion(&v) == ncclSuccess && v != NCCL_VERSION_CODE) {
+    char buf[160];
+    std::snprintf(buf, sizeof buf, "RCCL runtime version %d != rccl.h version %d this library was compiled against",
+                  v, NCCL_VERSION_CODE);
+    ctx->comm_note = buf;
+  }
   ncclUniqueId u;
   std::memcpy(u.internal, id, NCCL_UNIQUE_ID_BYTES);
   ncclComm_t c = nullptr;
@@ -196,13 +371,28 @@ int crdt_ctx_comm_init(crdt_ctx *ctx, const uint8_t *id, int nranks, int rank) {
   return CRDT_OK;
 }
 
+int crdt_ctx_comm_init_ops(crdt_ctx *ctx, const crdt_comm_ops *ops, int nranks, int rank) {
+  CRDT_CHECK_CTX(ctx);
+  if (!ops || !ops->allgather || !ops->allreduce_u64 || nranks < 1 || rank < 0 || rank >= nranks)
+    return fail(ctx, CRDT_EINVAL, "crdt_ctx_comm_init_ops: NULL callbacks / nranks %d / rank %d", nranks, rank);
+  if (ctx->comm || ctx->has_ops)
+    return fail(ctx, CRDT_EINVAL, "crdt_ctx_comm_init_ops: ctx already has a communicator");
+  ctx->ops = *ops;
+  ctx->has_ops = true;
+  ctx->nranks = nranks;
+  ctx->rank = rank;
+  ctx->comm_note.clear();
+  return CRDT_OK;
+}
+
 int crdt_ctx_comm_destroy(crdt_ctx *ctx) {
   CRDT_CHECK_CTX(ctx);
-  if (ctx->comm) {
-    (void)hipStreamSynchronize(ctx->stream);
-    CRDT_NCCL(ctx, ncclCommDestroy((ncclComm_t)ctx->comm));
-  }
+  (void)hipStreamSynchronize(ctx->stream);
+  comm_release(ctx);
+  if (ctx->comm) CRDT_NCCL(ctx, ncclCommDestroy((ncclComm_t)ctx->comm));
   ctx->comm = nullptr;
+  ctx->has_ops = false;
+  ctx->ops = crdt_comm_ops{};
   ctx->nranks = 1;
   ctx->rank = 0;
   return CRDT_OK;
@@ -210,83 +400,99 @@ int crdt_ctx_comm_destroy(crdt_ctx *ctx) {
 
 int crdt_ctx_comm_info(const crdt_ctx *ctx, int *nranks, int *rank) {
   if (!ctx) return CRDT_EINVAL;
-  if (nranks) *nranks = ctx->comm ? ctx->nranks : 0;
-  if (rank) *rank = ctx->comm ? ctx->rank : -1;
+  const bool up = ctx->comm || ctx->has_ops;
+  if (nranks) *nranks = up ? ctx->nranks : 0;
+  if (rank) *rank = up ? ctx->rank : -1;
   return CRDT_OK;
+}
+
+const char *crdt_ctx_comm_note(const crdt_ctx *ctx, int *runtime, int *header) {
+  int v = 0;
+  if (ncclGetVersion(&v) != ncclSuccess) v = 0;
+  if (runtime) *runtime = v;
+  if (header) *header = NCCL_VERSION_CODE;
+  return ctx ? ctx->comm_note.c_str() : "";
 }
 
 int crdt_vclock_lub_many_sharded(crdt_ctx *ctx, const uint64_t *in, size_t G, size_t R, size_t A, size_t row_stride,
                                  size_t group_stride, uint64_t *out) {
-  CRDT_DEVICE_MEM_ONLY(ctx);
-  return lattice_sharded(ctx, Op::Max, (const u64 *)in, G, R, A, row_stride, group_stride, (u64 *)out);
+  return lattice_sharded(ctx, Op::Max, (const u64 *)in, G, R, A, row_stride, group_stride, (u64 *)out,
+                         "vclock_lub_many_sharded");
 }
 int crdt_gcounter_lub_many_sharded(crdt_ctx *ctx, const uint64_t *in, size_t G, size_t R, size_t A,
                                    size_t row_stride, size_t group_stride, uint64_t *out) {
-  CRDT_DEVICE_MEM_ONLY(ctx);
-  return lattice_sharded(ctx, Op::Max, (const u64 *)in, G, R, A, row_stride, group_stride, (u64 *)out);
+  return lattice_sharded(ctx, Op::Max, (const u64 *)in, G, R, A, row_stride, group_stride, (u64 *)out,
+                         "gcounter_lub_many_sharded");
 }
 int crdt_pncounter_lub_many_sharded(crdt_ctx *ctx, const uint64_t *in, size_t G, size_t R, size_t A,
                                     size_t row_stride, size_t group_stride, uint64_t *out) {
-  CRDT_DEVICE_MEM_ONLY(ctx);
-  return lattice_sharded(ctx, Op::Max, (const u64 *)in, G, R, 2 * A, row_stride, group_stride, (u64 *)out);
+  return lattice_sharded(ctx, Op::Max, (const u64 *)in, G, R, 2 * A, row_stride, group_stride, (u64 *)out,
+                         "pncounter_lub_many_sharded");
 }
 int crdt_gset_lub_many_sharded(crdt_ctx *ctx, const uint64_t *in, size_t G, size_t R, size_t words,
                                size_t row_stride, size_t group_stride, uint64_t *out) {
-  CRDT_DEVICE_MEM_ONLY(ctx);
-  return lattice_sharded(ctx, Op::Or, (const u64 *)in, G, R, words, row_stride, group_stride, (u64 *)out);
+  return lattice_sharded(ctx, Op::Or, (const u64 *)in, G, R, words, row_stride, group_stride, (u64 *)out,
+                         "gset_lub_many_sharded");
 }
 
 int crdt_orswot_lub_many_sharded(crdt_ctx *ctx, const crdt_orswot_batch *in, crdt_orswot_sharded_out *out) {
-  CRDT_DEVICE_MEM_ONLY(ctx);
+  static const char *what = "orswot_lub_many_sharded";
   CRDT_CHECK_CTX(ctx);
   CRDT_TRY(need_comm(ctx));
-  if (!in || !out || !out->clock || !out->entries || !out->ndef)
-    return fail(ctx, CRDT_EINVAL, "orswot_lub_many_sharded: NULL argument");
-  const size_t G = in->G, M = in->M, A = in->A, Mw = (M + 63) / 64;
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  CRDT_TRY(agree_mark(ctx));
   const size_t W = (size_t)ctx->nranks;
-  if (G == 0 || A == 0) {
+  int st = device_mem_only(ctx, what);
+  if (!st && (!in || !out || !out->clock || !out->entries || !out->ndef))
+    st = fail(ctx, CRDT_EINVAL, "%s: NULL argument", what);
+  const size_t G = st ? 0 : in->G, M = st ? 0 : in->M, A = st ? 0 : in->A, Mw = (M + 63) / 64;
+  const bool work = G > 0 && A > 0 && M > 0;
+  // deferred removes of this rank: per-group counts
+  std::vector<uint64_t> head(G + 1, 0);
+  size_t Dk = 0;
+  if (!st && work && in->def_off) {
+    if (in->def_off[0] != 0) st = fail(ctx, CRDT_EINVAL, "%s: def_off[0] must be 0", what);
+    for (size_t g = 0; !st && g < G; ++g) {
+      if (in->def_off[g + 1] < in->def_off[g]) st = fail(ctx, CRDT_EINVAL, "%s: def_off not non-decreasing", what);
+      else head[g] = in->def_off[g + 1] - in->def_off[g];
+    }
+    if (!st) Dk = in->def_off[G];
+    if (!st && Dk && (!in->def_clock || !in->def_members))
+      st = fail(ctx, CRDT_EINVAL, "%s: deferred removes without their buffers", what);
+    if (!st && Dk > 0xffffffffULL) st = fail(ctx, CRDT_EUNSUPPORTED, "%s: too many deferred removes", what);
+  }
+  head[G] = Dk;
+  // 1. local join of the shard without deferred removes -> partial (clock, entries); every
+  //    buffer of the exchange whose size is known here is allocated before the agreement
+  void *pc = nullptr, *pe = nullptr, *gc = nullptr, *ge = nullptr, *lcnt = nullptr, *acnt = nullptr;
+  if (!st && work) {
+    st = sbuf(ctx, 0, G * A * 8, &pc);
+    if (!st) st = sbuf(ctx, 1, G * M * A * 8, &pe);
+    if (!st) st = sbuf(ctx, 2, W * G * A * 8, &gc);
+    if (!st) st = sbuf(ctx, 3, W * G * M * A * 8, &ge);
+    if (!st) st = sbuf(ctx, 4, (G + 1) * 8, &lcnt);
+    if (!st) st = sbuf(ctx, 5, W * (G + 1) * 8, &acnt);
+    if (!st) {
+      crdt_orswot_batch loc = *in;
+      loc.def_off = nullptr;
+      crdt_orswot_out po{(uint64_t *)pc, (uint64_t *)pe, nullptr, nullptr};
+      st = crdt_orswot_lub_many(ctx, &loc, &po);
+    }
+    if (!st) st = stage_h2d(ctx, lcnt, head.data(), (G + 1) * 8);
+  }
+  CRDT_TRY(agree(ctx, st, make_hdr(st, kTagOrswot, {G, M, A}), what));
+  if (!work) {
     *out->ndef = 0;
     return CRDT_OK;
   }
-  CRDT_HIP(ctx, hipSetDevice(ctx->device));
-  auto comm = (ncclComm_t)ctx->comm;
-  // 1. local join of the shard without deferred removes -> partial (clock, entries)
-  void *pc, *pe, *gc, *ge;
-  CRDT_TRY(sbuf(ctx, 0, G * A * 8, &pc));
-  CRDT_TRY(sbuf(ctx, 1, G * M * A * 8, &pe));
-  CRDT_TRY(sbuf(ctx, 2, W * G * A * 8, &gc));
-  CRDT_TRY(sbuf(ctx, 3, W * G * M * A * 8, &ge));
-  crdt_orswot_batch loc = *in;
-  loc.def_off = nullptr;
-  crdt_orswot_out po{(uint64_t *)pc, (uint64_t *)pe, nullptr, nullptr};
-  CRDT_TRY(crdt_orswot_lub_many(ctx, &loc, &po));
-  // 2. all-gather the partials: replica (g, r) of the re-merge at r*G*A + g*A (+ m*A)
+  // 2. all-gather the partials: replica (g, r) of the re-merge at r*G*A + g*A (+ m*A), and the
+  //    per-group deferred counts of every rank
   timing_begin(ctx, "shard_exchange");
-  CRDT_NCCL(ctx, ncclGroupStart());
-  CRDT_NCCL(ctx, ncclAllGather(pc, gc, G * A, ncclUint64, comm, ctx->stream));
-  CRDT_NCCL(ctx, ncclAllGather(pe, ge, G * M * A, ncclUint64, comm, ctx->stream));
-  CRDT_NCCL(ctx, ncclGroupEnd());
-  // 3. deferred removes: per-group counts of every rank, then the padded rows
-  std::vector<uint64_t> cnt(G, 0);
-  size_t Dk = 0;
-  if (in->def_off) {
-    for (size_t g = 0; g < G; ++g) {
-      if (in->def_off[g + 1] < in->def_off[g])
-        return fail(ctx, CRDT_EINVAL, "orswot_lub_many_sharded: def_off not non-decreasing");
-      cnt[g] = in->def_off[g + 1] - in->def_off[g];
-    }
-    Dk = in->def_off[G] - in->def_off[0];
-    if (Dk && (!in->def_clock || !in->def_members))
-      return fail(ctx, CRDT_EINVAL, "orswot_lub_many_sharded: deferred removes without their buffers");
-  }
-  void *lcnt, *acnt;
-  CRDT_TRY(sbuf(ctx, 4, (G + 1) * 8, &lcnt));
-  CRDT_TRY(sbuf(ctx, 5, W * (G + 1) * 8, &acnt));
-  std::vector<uint64_t> head(G + 1);
-  for (size_t g = 0; g < G; ++g) head[g] = cnt[g];
-  head[G] = Dk;
-  CRDT_TRY(stage_h2d(ctx, lcnt, head.data(), (G + 1) * 8));
-  CRDT_NCCL(ctx, ncclAllGather(lcnt, acnt, G + 1, ncclUint64, comm, ctx->stream));
+  CRDT_TRY(coll_group_begin(ctx));
+  CRDT_TRY(coll_allgather(ctx, pc, gc, G * A * 8));
+  CRDT_TRY(coll_allgather(ctx, pe, ge, G * M * A * 8));
+  CRDT_TRY(coll_allgather(ctx, lcnt, acnt, (G + 1) * 8));
+  CRDT_TRY(coll_group_end(ctx));
   std::vector<uint64_t> all((G + 1) * W);
   CRDT_HIP(ctx, hipMemcpyAsync(all.data(), acnt, all.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
   CRDT_HIP(ctx, hipStreamSynchronize(ctx->stream));
@@ -309,7 +515,7 @@ int crdt_orswot_lub_many_sharded(crdt_ctx *ctx, const crdt_orswot_batch *in, crd
   fin.entry_gstride = M * A;
   std::vector<size_t> goff(G + 1, 0);
   void *dcl = nullptr, *dmb = nullptr, *keep = nullptr, *kmb = nullptr, *idx = nullptr;
-  if (Dtot) {
+  if (Dtot) {  // rank-uniform: every rank saw the same gathered counts
     // padded send rows: [Dmax][A | Mw]
     void *sendc, *sendm, *allc, *allm;
     CRDT_TRY(sbuf(ctx, 6, Dmax * (A + Mw) * 8, &sendc));
@@ -322,27 +528,15 @@ int crdt_orswot_lub_many_sharded(crdt_ctx *ctx, const crdt_orswot_batch *in, crd
     idx = (u64 *)kmb + Dtot * Mw;       // gather index [Dtot] u32
     keep = (uint32_t *)idx + Dtot;      // [Dtot] u8
     if (Dk) {
-      const size_t d0 = in->def_off[0];
-      CRDT_HIP(ctx, hipMemcpyAsync(sendc, in->def_clock + d0 * A, Dk * A * 8, hipMemcpyDeviceToDevice, ctx->stream));
-      CRDT_HIP(ctx, hipMemcpyAsync(sendm, in->def_members + d0 * Mw, Dk * Mw * 8, hipMemcpyDeviceToDevice,
-                                   ctx->stream));
+      CRDT_HIP(ctx, hipMemcpyAsync(sendc, in->def_clock, Dk * A * 8, hipMemcpyDeviceToDevice, ctx->stream));
+      CRDT_HIP(ctx, hipMemcpyAsync(sendm, in->def_members, Dk * Mw * 8, hipMemcpyDeviceToDevice, ctx->stream));
     }
-    CRDT_NCCL(ctx, ncclGroupStart());
-    CRDT_NCCL(ctx, ncclAllGather(sendc, allc, Dmax * A, ncclUint64, comm, ctx->stream));
-    CRDT_NCCL(ctx, ncclAllGather(sendm, allm, Dmax * Mw, ncclUint64, comm, ctx->stream));
-    CRDT_NCCL(ctx, ncclGroupEnd());
-    // regroup: group g gathers rank 0's rows of g, then rank 1's, ... (rank order, local order)
+    CRDT_TRY(coll_group_begin(ctx));
+    CRDT_TRY(coll_allgather(ctx, sendc, allc, Dmax * A * 8));
+    CRDT_TRY(coll_allgather(ctx, sendm, allm, Dmax * Mw * 8));
+    CRDT_TRY(coll_group_end(ctx));
     std::vector<uint32_t> gi;
-    gi.reserve(Dtot);
-    std::vector<uint64_t> base(W, 0);
-    for (size_t g = 0; g < G; ++g) {
-      for (size_t r = 0; r < W; ++r) {
-        const uint64_t c = all[r * (G + 1) + g];
-        for (uint64_t j = 0; j < c; ++j) gi.push_back((uint32_t)(r * Dmax + base[r] + j));
-        base[r] += c;
-      }
-      goff[g + 1] = gi.size();
-    }
+    shard_host::orswot_regroup(all.data(), W, G, Dmax, gi, goff);
     CRDT_TRY(stage_h2d(ctx, idx, gi.data(), Dtot * 4));
     CRDT_TRY(gather_rows(ctx, (u64 *)dcl, (const u64 *)allc, (const uint32_t *)idx, Dtot, A));
     CRDT_TRY(gather_rows(ctx, (u64 *)dmb, (const u64 *)allm, (const uint32_t *)idx, Dtot, Mw));
@@ -351,10 +545,10 @@ int crdt_orswot_lub_many_sharded(crdt_ctx *ctx, const crdt_orswot_batch *in, crd
     fin.def_members = (const uint64_t *)dmb;
   }
   timing_end(ctx);
-  // 4. re-merge of the world partials with every deferred remove
+  // 3. re-merge of the world partials with every deferred remove (no collective from here on)
   crdt_orswot_out fo{out->clock, out->entries, (uint8_t *)keep, (uint64_t *)kmb};
   CRDT_TRY(crdt_orswot_lub_many(ctx, &fin, &fo));
-  // 5. surviving deferred removes, compacted: (rm clock, member union, group)
+  // 4. surviving deferred removes, compacted: (rm clock, member union, group)
   size_t nkeep = 0;
   if (Dtot) {
     std::vector<uint8_t> hk(Dtot);
@@ -372,7 +566,7 @@ int crdt_orswot_lub_many_sharded(crdt_ctx *ctx, const crdt_orswot_batch *in, crd
     const size_t nw = std::min(nkeep, out->def_cap);
     if (nw) {
       if (!out->def_clock || !out->def_members || !out->def_group)
-        return fail(ctx, CRDT_EINVAL, "orswot_lub_many_sharded: def_cap > 0 without output buffers");
+        return fail(ctx, CRDT_EINVAL, "%s: def_cap > 0 without output buffers", what);
       CRDT_TRY(stage_h2d(ctx, idx, ki.data(), nw * 4));
       CRDT_TRY(gather_rows(ctx, (u64 *)out->def_clock, (const u64 *)dcl, (const uint32_t *)idx, nw, A));
       CRDT_TRY(gather_rows(ctx, (u64 *)out->def_members, (const u64 *)kmb, (const uint32_t *)idx, nw, Mw));
@@ -384,129 +578,201 @@ int crdt_orswot_lub_many_sharded(crdt_ctx *ctx, const crdt_orswot_batch *in, crd
 }
 
 int crdt_lub_many_multi_sharded(crdt_ctx *ctx, const crdt_lub_segment *segs, size_t nseg) {
-  CRDT_DEVICE_MEM_ONLY(ctx);
+  static const char *what = "lub_many_multi_sharded";
   CRDT_CHECK_CTX(ctx);
   CRDT_TRY(need_comm(ctx));
-  std::vector<LubReq> reqs;
-  CRDT_TRY(lub_reqs_from_segments(ctx, segs, nseg, reqs));
-  std::vector<LubReq> maxr;
-  for (auto &q : reqs) {
-    if (q.G > 1 && q.out_stride != q.W)
-      return fail(ctx, CRDT_EINVAL, "lub_many_multi_sharded: out_stride must equal the row width");
-    if (q.flags) return fail(ctx, CRDT_EINVAL, "lub_many_multi_sharded: flags must be 0");
-    if (q.op == Op::Max) maxr.push_back(q);
-  }
   CRDT_HIP(ctx, hipSetDevice(ctx->device));
-  CRDT_TRY(lattice_lub_many_multi(ctx, maxr.data(), maxr.size()));
-  auto comm = (ncclComm_t)ctx->comm;
+  CRDT_TRY(agree_mark(ctx));
+  int st = device_mem_only(ctx, what);
+  std::vector<LubReq> reqs;
+  if (!st) st = lub_reqs_from_segments(ctx, segs, nseg, reqs);
+  std::vector<LubReq> maxr;
+  uint64_t dh = 0x9e3779b97f4a7c15ull;  // hash of every segment's (op, G, W)
+  for (auto &q : reqs) {
+    if (!st && q.G > 1 && q.out_stride != q.W) st = fail(ctx, CRDT_EINVAL, "%s: out_stride must equal the row width", what);
+    if (!st && q.flags) st = fail(ctx, CRDT_EINVAL, "%s: flags must be 0", what);
+    if (!st && q.G && q.W && !q.out) st = fail(ctx, CRDT_EINVAL, "%s: a segment's out is NULL", what);
+    if (q.op == Op::Max) maxr.push_back(q);
+    for (uint64_t d : {(uint64_t)q.op, (uint64_t)q.G, (uint64_t)q.W}) dh = (dh ^ d) * 0x100000001b3ull;
+  }
+  if (!st) st = lattice_lub_many_multi(ctx, maxr.data(), maxr.size());
+  CRDT_TRY(agree(ctx, st, make_hdr(st, kTagMulti, {(uint64_t)reqs.size(), dh}), what));
   timing_begin(ctx, "shard_exchange");
-  CRDT_NCCL(ctx, ncclGroupStart());
-  for (auto &q : maxr)
-    if (q.G && q.W) CRDT_NCCL(ctx, ncclAllReduce(q.out, q.out, q.G * q.W, ncclUint64, ncclMax, comm, ctx->stream));
-  CRDT_NCCL(ctx, ncclGroupEnd());
+  CRDT_TRY(coll_group_begin(ctx));
+  for (auto &q : maxr) CRDT_TRY(coll_allreduce(ctx, q.out, q.out, q.G * q.W, Red::Max));
+  CRDT_TRY(coll_group_end(ctx));
   timing_end(ctx);
-  for (auto &q : reqs)
-    if (q.op == Op::Or) CRDT_TRY(lattice_sharded(ctx, q.op, q.in, q.G, q.R, q.W, q.row_stride, q.group_stride, q.out));
+  for (auto &q : reqs)  // GSet segments: every rank reaches each of them (same segment list)
+    if (q.op == Op::Or) CRDT_TRY(lattice_sharded(ctx, q.op, q.in, q.G, q.R, q.W, q.row_stride, q.group_stride, q.out, what));
   return CRDT_OK;
 }
 
 int crdt_lwwreg_lub_many_sharded(crdt_ctx *ctx, const uint64_t *marker, const uint64_t *val, size_t G, size_t R,
                                  size_t group_stride, uint64_t base, uint64_t *out_marker, uint64_t *out_val,
                                  uint64_t *first_conflict) {
-  CRDT_DEVICE_MEM_ONLY(ctx);
+  static const char *what = "lwwreg_lub_many_sharded";
   CRDT_CHECK_CTX(ctx);
   CRDT_TRY(need_comm(ctx));
-  if (G == 0) return CRDT_OK;
-  if (!out_marker || !out_val) return fail(ctx, CRDT_EINVAL, "lwwreg_lub_many_sharded: NULL output");
-  if (R && (!marker || !val)) return fail(ctx, CRDT_EINVAL, "lwwreg_lub_many_sharded: NULL input");
   CRDT_HIP(ctx, hipSetDevice(ctx->device));
-  auto comm = (ncclComm_t)ctx->comm;
+  CRDT_TRY(agree_mark(ctx));
   const size_t W = (size_t)ctx->nranks, row = 2 * G + 1;
-  void *send, *all, *tmv, *pst;
-  CRDT_TRY(sbuf(ctx, 0, row * 8, &send));
-  CRDT_TRY(sbuf(ctx, 1, W * row * 8, &all));
-  CRDT_TRY(sbuf(ctx, 2, 2 * G * W * 8, &tmv));
-  CRDT_TRY(sbuf(ctx, 3, 3 * G * 8 + W * 4 + 64, &pst));
+  int st = device_mem_only(ctx, what);
+  if (!st && G && (!out_marker || !out_val)) st = fail(ctx, CRDT_EINVAL, "%s: NULL output", what);
+  if (!st && G && R && (!marker || !val)) st = fail(ctx, CRDT_EINVAL, "%s: NULL input", what);
+  void *send = nullptr, *all = nullptr, *tmv = nullptr, *pst = nullptr;
+  if (!st && G) {
+    st = sbuf(ctx, 0, row * 8, &send);
+    if (!st) st = sbuf(ctx, 1, W * row * 8, &all);
+    if (!st) st = sbuf(ctx, 2, 2 * G * W * 8, &tmv);
+    if (!st) st = sbuf(ctx, 3, 3 * G * 8 + W * 4 + 64, &pst);
+  }
   uint64_t *lm = (uint64_t *)send, *lv = lm + G;
   uint64_t *tm = (uint64_t *)tmv, *tv = tm + G * W;
   uint64_t *pm = (uint64_t *)pst, *pv = pm + G, *fc = pv + G;
   uint32_t *ranks = (uint32_t *)(fc + G);
   // 1. local fold of the shard (acc = shard[0]; conflicts indexed locally); R_k travels along
-  if (R) CRDT_TRY(crdt_lwwreg_lub_many(ctx, marker, val, G, R, group_stride, lm, lv, fc, 0));
+  if (!st && G && R) st = crdt_lwwreg_lub_many(ctx, marker, val, G, R, group_stride, lm, lv, fc, 0);
   const uint64_t rk = R;
-  CRDT_TRY(stage_h2d(ctx, lm + 2 * G, &rk, 8));
+  if (!st && G) st = stage_h2d(ctx, lm + 2 * G, &rk, 8);
+  CRDT_TRY(agree(ctx, st, make_hdr(st, kTagLww, {G}), what));
+  if (G == 0) return CRDT_OK;
   // 2. all-gather the rank states
   timing_begin(ctx, "shard_exchange");
-  CRDT_NCCL(ctx, ncclAllGather(send, all, row, ncclUint64, comm, ctx->stream));
+  CRDT_TRY(coll_allgather(ctx, send, all, row * 8));
   timing_end(ctx);
-  std::vector<uint64_t> counts(W);
-  for (size_t r = 0; r < W; ++r)
-    CRDT_HIP(ctx, hipMemcpyAsync(&counts[r], (u64 *)all + r * row + 2 * G, 8, hipMemcpyDeviceToHost, ctx->stream));
+  std::vector<uint64_t> hall(W * row);
+  CRDT_HIP(ctx, hipMemcpyAsync(hall.data(), all, hall.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
   CRDT_HIP(ctx, hipStreamSynchronize(ctx->stream));
   std::vector<uint32_t> nz;
-  size_t before = 0;  // non-empty ranks before this one
-  for (size_t r = 0; r < W; ++r)
-    if (counts[r]) {
-      if ((int)r < ctx->rank) ++before;
-      nz.push_back((uint32_t)r);
-    }
+  const size_t before = shard_host::lww_nonempty(hall.data(), W, row, G, ctx->rank, nz);
   const size_t n = nz.size();
-  if (n == 0) {  // no replica anywhere: the zero register, no conflict
+  if (n == 0) {  // no replica anywhere (rank-uniform): the zero register, no conflict
     CRDT_TRY(device_fill(ctx, out_marker, G * 8, 0));
     CRDT_TRY(device_fill(ctx, out_val, G * 8, 0));
     if (first_conflict) CRDT_TRY(device_fill(ctx, first_conflict, G * 8, 0xFF));
     return CRDT_OK;
   }
   CRDT_TRY(stage_h2d(ctx, ranks, nz.data(), n * 4));
-  hipLaunchKernelGGL(lww_world_rows_kernel, dim3(small_grid(ctx, G * n)), dim3(kBlock), 0, ctx->stream, (u64 *)tm, (u64 *)tv,
-                     (const u64 *)all, (const uint32_t *)ranks, (unsigned long long)n, (unsigned long long)G);
+  hipLaunchKernelGGL(lww_world_rows_kernel, dim3(small_grid(ctx, G * n)), dim3(kBlock), 0, ctx->stream, (u64 *)tm,
+                     (u64 *)tv, (const u64 *)all, (const uint32_t *)ranks, (unsigned long long)n, (unsigned long long)G);
   CRDT_HIP(ctx, hipGetLastError());
   // 3. the shard continues the GLOBAL fold from the fold of the lower ranks' states, so its
-  //    conflicts are those of the global left fold (lwwreg.rs:84-98 is order-dependent)
+  //    conflicts are those of the global left fold (lwwreg.rs:84-98 is order-dependent).  A local
+  //    failure here still joins the MIN all-reduce below (with "no conflict") so no rank blocks.
+  int st2 = CRDT_OK;
   if (!R) {
-    CRDT_TRY(device_fill(ctx, fc, G * 8, 0xFF));
+    st2 = device_fill(ctx, fc, G * 8, 0xFF);
   } else if (before > 0) {
-    CRDT_TRY(crdt_lwwreg_lub_many(ctx, tm, tv, G, before, n, pm, pv, nullptr, 0));
-    CRDT_TRY(crdt_lwwreg_lub_many(ctx, marker, val, G, R, group_stride, pm, pv, fc, CRDT_ACCUMULATE));
+    st2 = crdt_lwwreg_lub_many(ctx, tm, tv, G, before, n, pm, pv, nullptr, 0);
+    if (!st2) st2 = crdt_lwwreg_lub_many(ctx, marker, val, G, R, group_stride, pm, pv, fc, CRDT_ACCUMULATE);
   }
+  if (st2) (void)device_fill(ctx, fc, G * 8, 0xFF);
   hipLaunchKernelGGL(lww_rebase_kernel, dim3(small_grid(ctx, G)), dim3(kBlock), 0, ctx->stream, (u64 *)fc,
                      (unsigned long long)G, (u64)base);
   CRDT_HIP(ctx, hipGetLastError());
-  CRDT_NCCL(ctx, ncclAllReduce(fc, first_conflict ? (void *)first_conflict : (void *)fc, G, ncclUint64, ncclMin, comm,
-                               ctx->stream));
+  CRDT_TRY(coll_allreduce(ctx, (const u64 *)fc, first_conflict ? (u64 *)first_conflict : (u64 *)fc, G, Red::Min));
+  if (st2) return st2;
   // 4. the global state: the fold of the world's rank states
   return crdt_lwwreg_lub_many(ctx, tm, tv, G, n, n, out_marker, out_val, nullptr, 0);
 }
 
 int crdt_map_lub_many_sharded(crdt_ctx *ctx, const crdt_map_batch *in, size_t k0, size_t K, crdt_map_out *out) {
-  CRDT_DEVICE_MEM_ONLY(ctx);
+  static const char *what = "map_lub_many_sharded";
   CRDT_CHECK_CTX(ctx);
   CRDT_TRY(need_comm(ctx));
-  if (!in || !out) return fail(ctx, CRDT_EINVAL, "map_lub_many_sharded: NULL argument");
-  const size_t G = in->G, Kk = in->K, A = in->A;
-  if (k0 + Kk > K) return fail(ctx, CRDT_EINVAL, "map_lub_many_sharded: key range [%zu, %zu) past K = %zu", k0, k0 + Kk, K);
-  const size_t D = (in->def_off && G > 0) ? in->def_off[G] - in->def_off[0] : 0;
-  const size_t Kw = (K + 63) / 64, Kwl = (Kk + 63) / 64;
-  if (D == 0 || Kk == 0 || A == 0) return crdt_map_lub_many(ctx, in, out);
-  if (!in->def_keys || !out->def_keys || !out->def_keep)
-    return fail(ctx, CRDT_EINVAL, "map_lub_many_sharded: deferred buffers missing");
   CRDT_HIP(ctx, hipSetDevice(ctx->device));
-  auto comm = (ncclComm_t)ctx->comm;
-  // the key bitmaps restricted to this rank's keys [k0, k0 + Kk), re-indexed from 0
-  void *lk, *ok;
-  CRDT_TRY(sbuf(ctx, 0, D * Kwl * 8, &lk));
-  CRDT_TRY(sbuf(ctx, 1, D * Kwl * 8, &ok));
-  hipLaunchKernelGGL(bitmap_shift_kernel, dim3(small_grid(ctx, D * Kwl)), dim3(kBlock), 0, ctx->stream, (u64 *)lk,
-                     (const u64 *)in->def_keys, (unsigned long long)D, (unsigned long long)Kwl,
-                     (unsigned long long)Kw, (long long)k0, (long long)(k0 + Kk));
-  CRDT_HIP(ctx, hipGetLastError());
-  crdt_map_batch loc = *in;
-  loc.def_keys = (const uint64_t *)lk;
-  crdt_map_out lo = *out;
-  lo.def_keys = (uint64_t *)ok;
-  // keys are independent given the clocks and the deferred list: the exact left fold of the
-  // rank's keys, with no data-path collective
-  CRDT_TRY(crdt_map_lub_many(ctx, &loc, &lo));
+  CRDT_TRY(agree_mark(ctx));
+  const size_t W = (size_t)ctx->nranks;
+  int st = device_mem_only(ctx, what);
+  if (!st && (!in || !out)) st = fail(ctx, CRDT_EINVAL, "%s: NULL argument", what);
+  const size_t G = st ? 0 : in->G, Kk = st ? 0 : in->K, A = st ? 0 : in->A, R = st ? 0 : in->R;
+  if (!st && k0 + Kk > K) st = fail(ctx, CRDT_EINVAL, "%s: key range [%zu, %zu) past K = %zu", what, k0, k0 + Kk, K);
+  if (!st && G && A && (!out->clock || !out->flags)) st = fail(ctx, CRDT_EINVAL, "%s: NULL output", what);
+  if (!st && in->def_off && G && in->def_off[0] != 0) st = fail(ctx, CRDT_EINVAL, "%s: def_off[0] must be 0", what);
+  const size_t D = (!st && in->def_off && G > 0) ? in->def_off[G] : 0;
+  const size_t Kw = (K + 63) / 64, Kwl = Kk ? (Kk + 63) / 64 : 1;
+  if (!st && D && (!in->def_keys || !in->def_clock || !in->def_row || !out->def_keys || !out->def_keep))
+    st = fail(ctx, CRDT_EINVAL, "%s: deferred buffers missing", what);
+  if (!st && D > 0xffffffffULL) st = fail(ctx, CRDT_EUNSUPPORTED, "%s: too many deferred removes", what);
+  const bool work = G > 0 && A > 0;
+  void *lk = nullptr, *ok = nullptr, *fl = nullptr, *fall = nullptr;
+  if (!st && work) {
+    st = sbuf(ctx, 2, (G + 1) * 8, &fl);
+    if (!st) st = sbuf(ctx, 3, W * (G + 1) * 8, &fall);
+    if (!st && D) st = sbuf(ctx, 0, D * Kwl * 8, &lk);
+    if (!st && D) st = sbuf(ctx, 1, D * Kwl * 8, &ok);
+  }
+  crdt_map_batch loc{};
+  crdt_map_out lo{};
+  // the rank's part: its keys' exact left fold (keys are independent given the clocks and the
+  // deferred list: no data-path collective), or with no keys the clock lub and the
+  // removes' survival alone (def_keep is a function of the clocks and the deferred list)
+  auto local = [&](size_t vstate) -> int {
+    if (Kk > 0) {
+      lo.Vstate = vstate;
+      return crdt_map_lub_many(ctx, &loc, &lo);
+    }
+    if (int rc = device_fill(ctx, out->flags, G * 4, 0)) return rc;
+    if (int rc = lattice_lub_many(ctx, Op::Max, (const u64 *)in->clock, G, R, A, in->clock_rstride,
+                                  in->clock_gstride, (u64 *)out->clock, A, 0))
+      return rc;
+    if (!D) return CRDT_OK;
+    DefPlan q{};
+    q.G = G;
+    q.D = D;
+    q.M = 64;
+    q.A = A;
+    q.Mw = 1;
+    q.def_clock = (const u64 *)in->def_clock;
+    q.def_members = (const u64 *)lk;  // all-zero: no key of this rank
+    q.out_clock = (const u64 *)out->clock;
+    q.apply_ceiling = 0;
+    q.out_keep = out->def_keep;
+    q.out_members = (u64 *)ok;
+    return launch_deferred(ctx, in->def_off, q);
+  };
+  if (!st && work) {
+    loc = *in;
+    lo = *out;
+    if (D) {  // the key bitmaps restricted to this rank's keys [k0, k0 + Kk), re-indexed from 0
+      hipLaunchKernelGGL(bitmap_shift_kernel, dim3(small_grid(ctx, D * Kwl)), dim3(kBlock), 0, ctx->stream, (u64 *)lk,
+                         (const u64 *)in->def_keys, (unsigned long long)D, (unsigned long long)Kwl,
+                         (unsigned long long)Kw, (long long)k0, (long long)(k0 + Kk));
+      if (hipGetLastError() != hipSuccess) st = fail(ctx, CRDT_EHIP, "%s: bitmap_shift_kernel launch", what);
+      loc.def_keys = (const uint64_t *)lk;
+      lo.def_keys = (uint64_t *)ok;
+    }
+    if (!st) st = local(out->Vstate);
+  }
+  const uint64_t offh = (!st && in->def_off && G) ? shard_host::hash_offsets(in->def_off, G + 1) : 0;
+  CRDT_TRY(agree(ctx, st, make_hdr(st, kTagMap, {G, K, A, D, st ? 0 : (uint64_t)out->Vout, offh}), what));
+  if (!work) return CRDT_OK;
+  // flags of every rank (+ its status) -> the OR over the ranks, written back on every rank; a
+  // fold state that ran out of value slots (bit 2) on ANY rank reruns the fold with a larger state
+  // on EVERY rank (each key's result is independent of the state size), so the ranks take the same
+  // branches and meet in the same collectives
+  size_t vstate = out->Vstate;
+  std::vector<uint64_t> hf(W * (G + 1));
+  std::vector<uint32_t> gflags(G);
+  for (;;) {
+    hipLaunchKernelGGL(widen_u32_kernel, dim3(small_grid(ctx, G + 1)), dim3(kBlock), 0, ctx->stream, (u64 *)fl,
+                       (const uint32_t *)out->flags, (unsigned long long)G, (u64)(st ? 1 : 0));
+    CRDT_HIP(ctx, hipGetLastError());
+    CRDT_TRY(coll_allgather(ctx, fl, fall, (G + 1) * 8));
+    CRDT_HIP(ctx, hipMemcpyAsync(hf.data(), fall, hf.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
+    CRDT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    bool bad, grow;
+    shard_host::map_flags_or(hf.data(), W, G, gflags.data(), &bad, &grow);
+    if (bad) {
+      if (st) return st;
+      return fail(ctx, CRDT_ECOMM, "%s: another rank failed its local fold; no key sets were exchanged", what);
+    }
+    if (!grow || vstate >= 16) break;
+    vstate = vstate < 8 ? 8 : 16;
+    st = Kk > 0 ? local(vstate) : CRDT_OK;
+  }
+  CRDT_TRY(stage_h2d(ctx, out->flags, gflags.data(), G * 4));
+  if (!D) return CRDT_OK;
   // surviving removes' key sets over all K keys: this rank's bits placed at k0, then a SUM
   // all-reduce (disjoint key ranges: the sum is the union)
   hipLaunchKernelGGL(bitmap_shift_kernel, dim3(small_grid(ctx, D * Kw)), dim3(kBlock), 0, ctx->stream,
@@ -514,7 +780,7 @@ int crdt_map_lub_many_sharded(crdt_ctx *ctx, const crdt_map_batch *in, size_t k0
                      (unsigned long long)Kwl, -(long long)k0, (long long)Kk);
   CRDT_HIP(ctx, hipGetLastError());
   timing_begin(ctx, "shard_exchange");
-  CRDT_NCCL(ctx, ncclAllReduce(out->def_keys, out->def_keys, D * Kw, ncclUint64, ncclSum, comm, ctx->stream));
+  CRDT_TRY(coll_allreduce(ctx, (const u64 *)out->def_keys, (u64 *)out->def_keys, D * Kw, Red::Sum));
   timing_end(ctx);
   return CRDT_OK;
 }

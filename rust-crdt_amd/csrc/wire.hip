@@ -282,6 +282,13 @@ __global__ __launch_bounds__(kBlock) void orswot_ingest_kernel(IngestPlan p) {
         if (k != ~0ull && k + 2 <= f.nw) {
           dcnt = rd64(f.w, k);
           dpos = k + 2;
+          // every remove record takes at least 4 words (its clock's length and its member
+          // count): a larger count is a lying frame, and it must not reach the exclusive scan of
+          // def_off (it would shift or wrap every later state's pooled rows) -> this frame only
+          if (dcnt > (f.nw - dpos) / 4) {
+            st |= kWireBad;
+            dcnt = 0;
+          }
         } else {
           st |= kWireBad;
         }

@@ -146,6 +146,28 @@ pub trait BatchCvRDT: CvRDT + Sized {
     fn merge_batch(ctx: &GpuCtx, selves: &mut [Self], others: Vec<Self>) -> Result<(), GpuError>;
 }
 
+/// Capacity limits of the library this module binds (include/crdt_gpu.h; checked against the
+/// header's stated limits by tests/test_rust_shim.py).  Past them a call returns `GpuError` with
+/// `CRDT_EUNSUPPORTED` and leaves its inputs untouched.
+/// Values per MVReg register in a Map input (`crdt_map_lub_many`, `crdt_map_merge_batch`: V <= 8).
+pub const MAP_MAX_VALUES: usize = 8;
+/// Actors of the Map and Orswot-apply kernels (A <= 256).
+pub const MAP_MAX_ACTORS: usize = 256;
+/// Deferred-remove slots of a pairwise merge, self + other (`Dcap(self) + Dcap(other) <= 512`).
+pub const MERGE_MAX_DEFERRED: usize = 512;
+
+fn unsupported(msg: String) -> GpuError {
+    GpuError { code: ffi::CRDT_EUNSUPPORTED, msg }
+}
+
+fn check_pairs(n_self: usize, n_other: usize) -> Result<(), GpuError> {
+    if n_self != n_other {
+        return Err(GpuError { code: ffi::CRDT_EINVAL,
+                              msg: format!("merge_batch: {} selves but {} others", n_self, n_other) });
+    }
+    Ok(())
+}
+
 /// Dense indices for ids (actors, members, set elements): first-seen order.
 struct Index<T: Ord + Clone> {
     pos: BTreeMap<T, usize>,
@@ -274,7 +296,8 @@ impl<A: Actor> BatchCvRDT for VClock<A> {
     }
 
     fn merge_batch(ctx: &GpuCtx, selves: &mut [Self], others: Vec<Self>) -> Result<(), GpuError> {
-        let n = selves.len().min(others.len());
+        check_pairs(selves.len(), others.len())?;
+        let n = selves.len();
         if n == 0 {
             return Ok(());
         }
@@ -354,7 +377,8 @@ impl<A: Actor> BatchCvRDT for PNCounter<A> {
     }
 
     fn merge_batch(ctx: &GpuCtx, selves: &mut [Self], others: Vec<Self>) -> Result<(), GpuError> {
-        let n = selves.len().min(others.len());
+        check_pairs(selves.len(), others.len())?;
+        let n = selves.len();
         if n == 0 {
             return Ok(());
         }
@@ -421,7 +445,8 @@ impl<T: Ord + Clone> BatchCvRDT for GSet<T> {
     }
 
     fn merge_batch(ctx: &GpuCtx, selves: &mut [Self], others: Vec<Self>) -> Result<(), GpuError> {
-        let n = selves.len().min(others.len());
+        check_pairs(selves.len(), others.len())?;
+        let n = selves.len();
         if n == 0 {
             return Ok(());
         }
@@ -458,46 +483,75 @@ pub trait BatchFunkyLww: Sized {
                    -> Result<Vec<Result<(), CrdtError>>, GpuError>;
 }
 
-impl<V: Ord + Clone + PartialEq> BatchFunkyLww for LWWReg<V, u64> {
+/// Order-preserving interning of markers: rank among the distinct markers, + 1 (`M: Ord` is all
+/// `FunkyCvRDT for LWWReg<V, M>` asks, lwwreg.rs:30-46; equal markers <=> equal ids, and the
+/// kernel's u64 compare orders ids exactly as `M::cmp` orders the markers).
+fn marker_ids<'a, M: Ord + Clone + 'a, I: Iterator<Item = &'a M>>(markers: I) -> (Vec<u64>, BTreeMap<M, u64>) {
+    let all: Vec<&M> = markers.collect();
+    let set: BTreeSet<&M> = all.iter().cloned().collect();
+    let rank: BTreeMap<M, u64> = set.into_iter().enumerate().map(|(i, m)| (m.clone(), i as u64 + 1)).collect();
+    (all.iter().map(|m| rank[*m]).collect(), rank)
+}
+
+// ---- LWWReg<V, M>: FunkyCvRDT (lwwreg.rs:43-45 -> update :84-98) --------------------------------
+impl<V: PartialEq + Clone, M: Ord + Clone> BatchFunkyLww for LWWReg<V, M> {
     fn lub_many(ctx: &GpuCtx, replicas: Vec<Self>) -> Result<(Self, Option<usize>), GpuError> {
         let r = replicas.len();
         if r == 0 {
             return Err(GpuError { code: ffi::CRDT_EINVAL, msg: "LWWReg lub_many of no replica".into() });
         }
-        let mut vals = Index::new();
-        let markers: Vec<u64> = replicas.iter().map(|x| x.marker).collect();
-        let ids: Vec<u64> = replicas.iter().map(|x| vals.intern(&x.val) as u64).collect();
+        let (markers, _) = marker_ids(replicas.iter().map(|x| &x.marker));
+        // value ids only meet values under an EQUAL marker (the conflict test, lwwreg.rs:89-90), and
+        // `V: PartialEq` is all there is: id = the first replica of the same marker class holding an
+        // equal value (a linear scan within the class)
+        let mut classes: HashMap<u64, Vec<usize>> = HashMap::new();
+        let mut ids = Vec::with_capacity(r);
+        for (i, x) in replicas.iter().enumerate() {
+            let class = classes.entry(markers[i]).or_insert_with(Vec::new);
+            let id = match class.iter().find(|&&j| replicas[j].val == x.val) {
+                Some(&j) => j,
+                None => {
+                    class.push(i);
+                    i
+                }
+            };
+            ids.push(id as u64);
+        }
         let (mut mk, mut vi, mut fc) = (0u64, 0u64, 0u64);
         ctx.check_host(unsafe {
             ffi::crdt_lwwreg_lub_many(ctx.host, markers.as_ptr(), ids.as_ptr(), 1, r, r, &mut mk, &mut vi, &mut fc, 0)
         })?;
-        let state = LWWReg { val: vals.ids[vi as usize].clone(), marker: mk };
+        let win = &replicas[vi as usize];
+        debug_assert_eq!(markers[vi as usize], mk);
+        let state = LWWReg { val: win.val.clone(), marker: win.marker.clone() };
         Ok((state, if fc == u64::MAX { None } else { Some(fc as usize) }))
     }
 
     fn merge_batch(ctx: &GpuCtx, selves: &mut [Self], others: Vec<Self>)
                    -> Result<Vec<Result<(), CrdtError>>, GpuError> {
-        let n = selves.len().min(others.len());
-        let mut vals = Index::new();
-        let sm: Vec<u64> = selves[..n].iter().map(|x| x.marker).collect();
-        let sv: Vec<u64> = selves[..n].iter().map(|x| vals.intern(&x.val) as u64).collect();
-        let om: Vec<u64> = others[..n].iter().map(|x| x.marker).collect();
-        let ov: Vec<u64> = others[..n].iter().map(|x| vals.intern(&x.val) as u64).collect();
+        check_pairs(selves.len(), others.len())?;
+        let n = selves.len();
         if n == 0 {
             return Ok(Vec::new());
         }
+        let (ids, _) = marker_ids(selves.iter().map(|x| &x.marker).chain(others.iter().map(|x| &x.marker)));
+        let (sm, om) = (ids[..n].to_vec(), ids[n..].to_vec());
+        // per pair: self's value is id 0, other's is 0 when equal, else 1
+        let sv = vec![0u64; n];
+        let ov: Vec<u64> = (0..n).map(|i| if selves[i].val == others[i].val { 0 } else { 1 }).collect();
         let (mut m2, mut v2, mut c) = (sm, sv, vec![0u8; n]);
         ctx.check_host(unsafe {
             ffi::crdt_lwwreg_merge_batch(ctx.host, m2.as_mut_ptr(), v2.as_mut_ptr(), om.as_ptr(), ov.as_ptr(), n,
                                          c.as_mut_ptr())
         })?;
         let mut res = Vec::with_capacity(n);
-        for i in 0..n {
+        for (i, o) in others.into_iter().enumerate() {
             if c[i] != 0 {
                 res.push(Err(CrdtError::ConflictingMarker));
             } else {
-                selves[i].marker = m2[i];
-                selves[i].val = vals.ids[v2[i] as usize].clone();
+                if m2[i] != ids[i] || v2[i] != 0 {  // other won (a strictly larger marker)
+                    selves[i] = o;
+                }
                 res.push(Ok(()));
             }
         }
@@ -636,15 +690,21 @@ impl<M: Member, A: Actor> BatchCvRDT for Orswot<M, A> {
     }
 
     fn merge_batch(ctx: &GpuCtx, selves: &mut [Self], others: Vec<Self>) -> Result<(), GpuError> {
-        let n = selves.len().min(others.len());
+        check_pairs(selves.len(), others.len())?;
+        let n = selves.len();
         if n == 0 {
             return Ok(());
         }
         let d = OrswotDense::of(selves[..n].iter().chain(others[..n].iter()));
         let (a, m) = (d.actors.width(), d.members.width());
         let mw = (m + 63) / 64;
+        // self's slots hold the survivors of BOTH sides of its own pair: size them per pair
         let dcap_o = others[..n].iter().map(|s| s.deferred.len()).max().unwrap_or(0).max(1);
-        let dcap_s = selves[..n].iter().map(|s| s.deferred.len()).max().unwrap_or(0).max(1) + dcap_o;
+        let dcap_s = (0..n).map(|i| selves[i].deferred.len() + others[i].deferred.len()).max().unwrap_or(0).max(1);
+        if dcap_s + dcap_o > MERGE_MAX_DEFERRED {
+            return Err(unsupported(format!("Orswot merge_batch: {} + {} deferred slots > {}", dcap_s, dcap_o,
+                                           MERGE_MAX_DEFERRED)));
+        }
         // per-state deferred slots (the crdt_orswot_states layout)
         let side = |states: &[Self], dcap: usize| {
             let (mut c, mut e) = (Vec::with_capacity(n * a), Vec::with_capacity(n * m * a));
@@ -676,10 +736,11 @@ impl<M: Member, A: Actor> BatchCvRDT for Orswot<M, A> {
         // host arrays straight to the CRDT_MEM_HOST ctx: staged, merged in HBM, copied back into them
         ctx.check_host(unsafe { ffi::crdt_orswot_merge_batch(ctx.host, &ss, &os, stv.as_mut_ptr()) })?;
         let (c, e, dc, dm, cnt) = (&sc, &se, &sdc, &sdm, &scnt);
+        // every status first: on an error no state of `selves` has been replaced
+        if let Some(i) = (0..n).find(|&i| stv[i] != 0) {
+            return Err(unsupported(format!("Orswot merge_batch: pair {} status {}", i, stv[i])));
+        }
         for i in 0..n {
-            if stv[i] != 0 {
-                return Err(GpuError { code: ffi::CRDT_EUNSUPPORTED, msg: format!("orswot merge_batch status {}", stv[i]) });
-            }
             let mut defs = Vec::new();
             for k in 0..cnt[i] as usize {
                 let base = i * dcap_s + k;
@@ -826,10 +887,11 @@ impl<K: Ord + Clone, V: Clone, A: Actor> BatchCvRDT for Map<K, MVReg<V, A>, A> {
             return Ok(Map::new());
         }
         let d = MapDense::of(replicas.iter());
-        let (r, a, k, v) = (replicas.len(), d.actors.width(), d.keys.width(), d.vmax.min(4));
+        let (r, a, k, v) = (replicas.len(), d.actors.width(), d.keys.width(), d.vmax);
         let kw = (k + 63) / 64;
-        if d.vmax > 4 {
-            return Err(GpuError { code: ffi::CRDT_EUNSUPPORTED, msg: "Map lub_many: a replica register holds more than 4 values".into() });
+        if v > MAP_MAX_VALUES || a > MAP_MAX_ACTORS {
+            return Err(unsupported(format!("Map lub_many: {} values per register / {} actors (limits {} / {})", v, a,
+                                           MAP_MAX_VALUES, MAP_MAX_ACTORS)));
         }
         let mut arena = Vec::new();
         let (mut clock, mut ec, mut vclk, mut vval) = (Vec::new(), Vec::new(), Vec::new(), Vec::new());
@@ -895,19 +957,24 @@ impl<K: Ord + Clone, V: Clone, A: Actor> BatchCvRDT for Map<K, MVReg<V, A>, A> {
     }
 
     fn merge_batch(ctx: &GpuCtx, selves: &mut [Self], others: Vec<Self>) -> Result<(), GpuError> {
-        let n = selves.len().min(others.len());
+        check_pairs(selves.len(), others.len())?;
+        let n = selves.len();
         if n == 0 {
             return Ok(());
         }
         let d = MapDense::of(selves[..n].iter().chain(others[..n].iter()));
         let (a, k) = (d.actors.width(), d.keys.width());
         let kw = (k + 63) / 64;
-        let vo = others[..n].iter().flat_map(|s| s.entries.values().map(|e| e.val.vals.len())).max().unwrap_or(0).max(1);
-        let vs = selves[..n].iter().flat_map(|s| s.entries.values().map(|e| e.val.vals.len())).max().unwrap_or(0).max(1) + vo;
+        let nv = |s: &Self| s.entries.values().map(|e| e.val.vals.len()).max().unwrap_or(0);
+        let vo = others[..n].iter().map(|s| nv(s)).max().unwrap_or(0).max(1);
+        // a merged register holds at most its own values plus the other side's: per pair
+        let vs = (0..n).map(|i| nv(&selves[i]) + nv(&others[i])).max().unwrap_or(0).max(1);
         let dcap_o = others[..n].iter().map(|s| s.deferred.len()).max().unwrap_or(0).max(1);
-        let dcap_s = selves[..n].iter().map(|s| s.deferred.len()).max().unwrap_or(0).max(1) + dcap_o;
-        if vs > 8 {
-            return Err(GpuError { code: ffi::CRDT_EUNSUPPORTED, msg: "Map merge_batch: more than 8 values per register".into() });
+        let dcap_s = (0..n).map(|i| selves[i].deferred.len() + others[i].deferred.len()).max().unwrap_or(0).max(1);
+        if vs > MAP_MAX_VALUES || a > MAP_MAX_ACTORS || dcap_s + dcap_o > MERGE_MAX_DEFERRED {
+            return Err(unsupported(format!("Map merge_batch: {} values per register / {} actors / {} + {} deferred \
+                                            slots (limits {} / {} / {})", vs, a, dcap_s, dcap_o, MAP_MAX_VALUES,
+                                           MAP_MAX_ACTORS, MERGE_MAX_DEFERRED)));
         }
         let mut arena = Vec::new();
         let mut side = |states: &[Self], v: usize, dcap: usize| {
@@ -942,10 +1009,11 @@ impl<K: Ord + Clone, V: Clone, A: Actor> BatchCvRDT for Map<K, MVReg<V, A>, A> {
         let od = ffi::crdt_map_deferred { clock: odc.as_mut_ptr(), keys: odk.as_mut_ptr(), count: ocnt.as_mut_ptr(), Dcap: dcap_o };
         let mut stv = vec![0u32; n];
         ctx.check_host(unsafe { ffi::crdt_map_merge_batch(ctx.host, &ss, &sd, &os, &od, stv.as_mut_ptr()) })?;
+        // every status first: on an error no state of `selves` has been replaced
+        if let Some(i) = (0..n).find(|&i| stv[i] != 0) {
+            return Err(unsupported(format!("Map merge_batch: pair {} status {}", i, stv[i])));
+        }
         for i in 0..n {
-            if stv[i] != 0 {
-                return Err(GpuError { code: ffi::CRDT_EUNSUPPORTED, msg: format!("Map merge_batch status {}", stv[i]) });
-            }
             let mut defs = Vec::new();
             for j in 0..scnt[i] as usize {
                 let base = i * dcap_s + j;
@@ -954,6 +1022,135 @@ impl<K: Ord + Clone, V: Clone, A: Actor> BatchCvRDT for Map<K, MVReg<V, A>, A> {
             selves[i] = d.egress(&sc[i * a..(i + 1) * a], &sec[i * k * a..(i + 1) * k * a],
                                  &svc[i * k * vs * a..(i + 1) * k * vs * a], &svv[i * k * vs..(i + 1) * k * vs], vs,
                                  &defs, &arena);
+        }
+        Ok(())
+    }
+}
+
+// ---- MVReg<V, A>: CvRDT::merge (mvreg.rs:112-128) on device buffers ------------------------------
+// MVReg::merge compares value clocks only, so values travel as ids into a per-call arena (as for
+// Map); the register's Vec order is kept slot for slot.
+fn mvreg_rows<V: Clone, A: Actor>(r: &MVReg<V, A>, idx: &Index<A>, v: usize, arena: &mut Vec<V>, vclk: &mut [u64],
+                                  vval: &mut [u64]) {
+    let a = idx.width().max(1);
+    for (slot, (c, val)) in r.vals.iter().enumerate().take(v) {
+        clock_row(c, idx, &mut vclk[slot * a..(slot + 1) * a]);
+        vval[slot] = arena.len() as u64;
+        arena.push(val.clone());
+    }
+}
+
+fn mvreg_of<V: Clone, A: Actor>(vclk: &[u64], vval: &[u64], slots: usize, idx: &Index<A>, arena: &[V]) -> MVReg<V, A> {
+    let a = idx.width().max(1);
+    let mut vals = Vec::new();
+    for s in 0..slots {
+        let row = &vclk[s * a..(s + 1) * a];
+        if row.iter().any(|&x| x != 0) {
+            vals.push((row_clock(row, idx), arena[vval[s] as usize].clone()));
+        }
+    }
+    MVReg { vals }
+}
+
+impl<V: Clone, A: Actor> BatchCvRDT for MVReg<V, A> {
+    fn lub_many(ctx: &GpuCtx, replicas: Vec<Self>) -> Result<Self, GpuError> {
+        if replicas.is_empty() {
+            return Ok(MVReg::new());
+        }
+        let mut idx = Index::new();
+        for r in &replicas {
+            for (c, _) in r.vals.iter() {
+                for a in c.dots.keys() {
+                    idx.intern(a);
+                }
+            }
+        }
+        let (n, a) = (replicas.len(), idx.width().max(1));
+        let v = replicas.iter().map(|r| r.vals.len()).max().unwrap_or(0).max(1);
+        if v > MAP_MAX_VALUES || a > MAP_MAX_ACTORS {
+            return Err(unsupported(format!("MVReg lub_many: {} values per register / {} actors (limits {} / {})", v,
+                                           a, MAP_MAX_VALUES, MAP_MAX_ACTORS)));
+        }
+        let mut arena = Vec::new();
+        let (mut vclk, mut vval) = (vec![0u64; n * v * a], vec![0u64; n * v]);
+        for (i, r) in replicas.iter().enumerate() {
+            mvreg_rows(r, &idx, v, &mut arena, &mut vclk[i * v * a..(i + 1) * v * a], &mut vval[i * v..(i + 1) * v]);
+        }
+        let (dc, dv) = (DeviceBuf::from_host(&vclk)?, DeviceBuf::from_host(&vval)?);
+        // the fold state holds 16 values; the output grows from 4 to 16 slots when it must
+        let mut vout = 4usize;
+        loop {
+            let (oc, ov) = (DeviceBuf::<u64>::zeroed(vout * a)?, DeviceBuf::<u64>::zeroed(vout)?);
+            let (nv, fl) = (DeviceBuf::<u32>::zeroed(1)?, DeviceBuf::<u32>::zeroed(1)?);
+            let batch = ffi::crdt_mvreg_batch {
+                G: 1, R: n, A: a, V: v,
+                vclk: dc.as_ptr(), vclk_rstride: v * a, vclk_gstride: n * v * a,
+                vval: dv.as_ptr(), vval_rstride: v, vval_gstride: n * v,
+            };
+            let mut out = ffi::crdt_mvreg_out {
+                Vout: vout, Vstate: 16, vclk: oc.as_mut_ptr(), vval: ov.as_mut_ptr(), nval: nv.as_mut_ptr(),
+                flags: fl.as_mut_ptr(),
+            };
+            ctx.check(unsafe { ffi::crdt_mvreg_lub_many(ctx.raw, &batch, &mut out) })?;
+            let flags = fl.to_host()?[0];
+            if flags & 1 != 0 && vout < 16 {
+                vout = 16;
+                continue;
+            }
+            if flags != 0 {
+                return Err(unsupported(format!("MVReg lub_many: flags {} (more than 16 concurrent values)", flags)));
+            }
+            return Ok(mvreg_of(&oc.to_host()?, &ov.to_host()?, vout, &idx, &arena));
+        }
+    }
+
+    fn merge_batch(ctx: &GpuCtx, selves: &mut [Self], others: Vec<Self>) -> Result<(), GpuError> {
+        check_pairs(selves.len(), others.len())?;
+        let n = selves.len();
+        if n == 0 {
+            return Ok(());
+        }
+        let mut idx = Index::new();
+        for r in selves.iter().chain(others.iter()) {
+            for (c, _) in r.vals.iter() {
+                for a in c.dots.keys() {
+                    idx.intern(a);
+                }
+            }
+        }
+        let a = idx.width().max(1);
+        let vo = others.iter().map(|r| r.vals.len()).max().unwrap_or(0).max(1);
+        // self's slots hold its kept values plus the other side's added ones: per pair
+        let vs = (0..n).map(|i| selves[i].vals.len() + others[i].vals.len()).max().unwrap_or(0).max(1);
+        if vs > MAP_MAX_VALUES || vo > MAP_MAX_VALUES || a > MAP_MAX_ACTORS {
+            return Err(unsupported(format!("MVReg merge_batch: {} / {} values per register / {} actors (limits {} / {})",
+                                           vs, vo, a, MAP_MAX_VALUES, MAP_MAX_ACTORS)));
+        }
+        let mut arena = Vec::new();
+        let (mut sc, mut sv) = (vec![0u64; n * vs * a], vec![0u64; n * vs]);
+        let (mut oc, mut ov) = (vec![0u64; n * vo * a], vec![0u64; n * vo]);
+        for i in 0..n {
+            mvreg_rows(&selves[i], &idx, vs, &mut arena, &mut sc[i * vs * a..(i + 1) * vs * a], &mut sv[i * vs..(i + 1) * vs]);
+            mvreg_rows(&others[i], &idx, vo, &mut arena, &mut oc[i * vo * a..(i + 1) * vo * a], &mut ov[i * vo..(i + 1) * vo]);
+        }
+        let (dsc, dsv) = (DeviceBuf::from_host(&sc)?, DeviceBuf::from_host(&sv)?);
+        let (doc, dov) = (DeviceBuf::from_host(&oc)?, DeviceBuf::from_host(&ov)?);
+        let st = DeviceBuf::<u32>::zeroed(n)?;
+        let ss = ffi::crdt_mvreg_states {
+            N: n, A: a, V: vs, vclk: dsc.as_mut_ptr(), vclk_stride: vs * a, vval: dsv.as_mut_ptr(), vval_stride: vs,
+        };
+        let os = ffi::crdt_mvreg_states {
+            N: n, A: a, V: vo, vclk: doc.as_mut_ptr(), vclk_stride: vo * a, vval: dov.as_mut_ptr(), vval_stride: vo,
+        };
+        ctx.check(unsafe { ffi::crdt_mvreg_merge_batch(ctx.raw, &ss, &os, st.as_mut_ptr()) })?;
+        let stv = st.to_host()?;
+        // every status first: on an error no register of `selves` has been replaced
+        if let Some(i) = (0..n).find(|&i| stv[i] != 0) {
+            return Err(unsupported(format!("MVReg merge_batch: pair {} status {}", i, stv[i])));
+        }
+        let (rc, rv) = (dsc.to_host()?, dsv.to_host()?);
+        for i in 0..n {
+            selves[i] = mvreg_of(&rc[i * vs * a..(i + 1) * vs * a], &rv[i * vs..(i + 1) * vs], vs, &idx, &arena);
         }
         Ok(())
     }

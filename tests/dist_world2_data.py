@@ -51,3 +51,30 @@ def map_input():
     d["def_clock"] = np.concatenate([d["def_clock"], clk])[order]
     d["def_keys"] = np.concatenate([d["def_keys"], keys])[order]
     return d
+
+
+def map_overflow_input():
+    """Map input whose LAST key folds through 12 concurrent values (6 replicas x 2 concurrent
+    writes by distinct actors) while every other key holds one: in a key-sharded fold with vout=8
+    only the rank owning the last key sees its fold state overflow (flags bit 2), and every rank
+    must rerun with the larger state together (the retry used to be rank-local)."""
+    R, K, V, A = 6, 5, 2, 12
+    clock = np.zeros((R, A), np.uint64)
+    ec = np.zeros((R, K, A), np.uint64)
+    vclk = np.zeros((R, K, V, A), np.uint64)
+    vval = np.zeros((R, K, V), np.uint64)
+    for r in range(R):
+        for t in range(V):
+            a = r * V + t
+            clock[r, a] = 1
+            ec[r, K - 1, a] = 1
+            vclk[r, K - 1, t, a] = 1
+            vval[r, K - 1, t] = 100 * r + t
+        ec[r, : K - 1, 0] = clock[r, 0]  # the other keys: one write by actor 0 (replica 0 only)
+        vclk[r, : K - 1, 0, 0] = clock[r, 0]
+        vval[r, : K - 1, 0] = 7 * (r + 1) * (clock[r, 0] > 0)
+    return dict(clock=clock, ec=ec, vclk=vclk, vval=vval, def_row=np.zeros(0, np.uint64),
+                def_clock=np.zeros((0, A), np.uint64), def_keys=np.zeros((0, 1), np.uint64))
+
+
+MAP_OVF_VOUT = 16

@@ -25,6 +25,16 @@ import dist_world2_data as D  # noqa: E402
 
 
 def main():
+    try:
+        _main()
+    except BaseException:
+        import traceback
+        traceback.print_exc()
+        sys.stderr.flush()
+        raise
+
+
+def _main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", required=True)
     args = ap.parse_args()
@@ -78,11 +88,116 @@ def main():
     out["map_nval"] = mres.nval.cpu().numpy().copy()
     out["map_keep"] = mres.def_keep.cpu().numpy().copy()
     out["map_def_keys"] = h(mres.def_keys)
+    out.update(cabi_seam(rank, world, t, h))
     out["lib"] = np.frombuffer(cg._abi.LIB_PATH.encode(), np.uint8)
     torch.cuda.synchronize()
     np.savez(os.path.join(args.out, f"rank{rank}.npz"), **out)
     dist.barrier()
     dist.destroy_process_group()
+
+
+def cabi_seam(rank, world, t, h):
+    """The C ABI's own multi-rank code (csrc/shard.hip: agreement, regrouping, LWW prefix, Map key
+    placement and overflow retry) at world 2 through crdt_ctx_comm_init_ops: the exchange runs over
+    gloo host callbacks instead of RCCL (RCCL refuses two ranks on one GPU)."""
+    import crdts_gpu as cg
+    from crdts_gpu import dist as cdist
+    from crdts_gpu import shard as cs
+    from crdts_gpu._abi import CrdtGpuError
+
+    dev = "cuda:0"
+    ctx = cg.Context(0)
+    cs.comm_init_ops(ctx, cs.TorchCommOps(), world, rank)
+    o = {"cabi_comm": np.array(cs.comm_info(ctx), np.int64)}
+    for name, (kind, G, R, W) in D.LATTICES.items():
+        full = D.lattice_input(name)
+        lo, hi = cdist.shard_range(R, rank, world)
+        shard = t(full[:, lo:hi])
+        if G == 1:
+            shard = shard[0]
+        o["cabi_" + name] = h(cs.lub_many_sharded(kind, shard, ctx=ctx))
+    # fused: every lattice of the step in one local launch + one grouped exchange
+    items = []
+    for name, (kind, G, R, W) in D.LATTICES.items():
+        full = D.lattice_input(name)
+        lo, hi = cdist.shard_range(R, rank, world)
+        sh = t(full[:, lo:hi])
+        items.append((kind, sh, torch.empty((G, W), dtype=torch.int64, device=dev)))
+    cs.lub_many_multi_sharded(items, ctx=ctx)
+    for (_, _, ob), name in zip(items, D.LATTICES):
+        o["cabi_multi_" + name] = h(ob)
+    # LWWReg: even split, and rank 0 holding NO replica (the lower-non-empty-ranks prefix)
+    m, v = D.lww_input()
+    Rl = m.shape[1]
+    for tag, (lo, hi) in (("even", cdist.shard_range(Rl, rank, world)),
+                          ("r0empty", (0, 0) if rank == 0 else (0, Rl)),
+                          ("uneven", (0, 13) if rank == 0 else (13, Rl))):
+        fm, fv, fc = cs.lwwreg_lub_many_sharded(t(m[:, lo:hi]), t(v[:, lo:hi]), lo, ctx=ctx)
+        o[f"cabi_lww_{tag}_marker"], o[f"cabi_lww_{tag}_val"] = h(fm), h(fv)
+        o[f"cabi_lww_{tag}_conflict"] = fc.cpu().numpy().copy()
+    # Orswot: each rank's removes pooled per group; the regroup is rank order, then local order
+    clock, entries, off, dcl, dmem = D.orswot_input()
+    R = clock.shape[0]
+    lo, hi = cdist.shard_range(R, rank, world)
+    d0, d1 = int(off[lo]), int(off[hi])
+    kw = dict(def_off=[0, d1 - d0], def_clock=t(dcl[d0:d1]), def_members=t(dmem[d0:d1])) if d1 > d0 else {}
+    res = cs.orswot_lub_many_sharded(t(clock[lo:hi][None]), t(entries[lo:hi][None]), ctx=ctx, **kw)
+    o["cabi_orswot_clock"], o["cabi_orswot_entries"] = h(res.clock), h(res.entries)
+    o["cabi_orswot_def_clock"], o["cabi_orswot_def_members"] = h(res.def_clock), h(res.def_members)
+    o["cabi_orswot_ndef_local"] = np.array([d1 - d0], np.int64)
+    # Map<K, MVReg>: key shards (k0 != 0 on rank 1), then an EMPTY key shard on rank 1
+    d = D.map_input()
+    K = d["ec"].shape[1]
+    Dn = d["def_row"].shape[0]
+    kw = dict(def_off=[0, Dn], def_row=torch.from_numpy(d["def_row"].astype(np.int32)).to(dev),
+              def_clock=t(d["def_clock"]), def_keys=t(d["def_keys"])) if Dn else {}
+    for tag, (k0, k1) in (("even", cdist.shard_range(K, rank, world)), ("empty", (0, K) if rank == 0 else (K, K))):
+        mres = cs.map_lub_many_sharded(t(d["clock"][None]), t(d["ec"][None, :, k0:k1]), t(d["vclk"][None, :, k0:k1]),
+                                       t(d["vval"][None, :, k0:k1]), k0, K, vout=D.MAP_VOUT, ctx=ctx, **kw)
+        o[f"cabi_map_{tag}_k0"] = np.array([k0, k1], np.int64)
+        o[f"cabi_map_{tag}_clock"], o[f"cabi_map_{tag}_ec"] = h(mres.clock), h(mres.ec)
+        o[f"cabi_map_{tag}_vclk"], o[f"cabi_map_{tag}_vval"] = h(mres.vclk), h(mres.vval)
+        o[f"cabi_map_{tag}_nval"] = mres.nval.cpu().numpy().copy()
+        o[f"cabi_map_{tag}_keep"] = mres.def_keep.cpu().numpy().copy()
+        o[f"cabi_map_{tag}_def_keys"] = h(mres.def_keys)
+    # Map: only rank 1's key folds to more values than vout=8 (its fold state overflows first, so the
+    # C call reruns every rank with the larger state); the flags are global, so BOTH ranks raise the
+    # capacity error, then both succeed with vout=16
+    d = D.map_overflow_input()
+    K = d["ec"].shape[1]
+    k0, k1 = (0, K - 1) if rank == 0 else (K - 1, K)
+    args = (t(d["clock"][None]), t(d["ec"][None, :, k0:k1]), t(d["vclk"][None, :, k0:k1]),
+            t(d["vval"][None, :, k0:k1]), k0, K)
+    try:
+        cs.map_lub_many_sharded(*args, vout=8, ctx=ctx)
+        o["cabi_mapovf_raised"] = np.array([0], np.int64)
+    except cg.map.MapCapacityError:
+        o["cabi_mapovf_raised"] = np.array([1], np.int64)
+    mres = cs.map_lub_many_sharded(*args, vout=D.MAP_OVF_VOUT, ctx=ctx)
+    o["cabi_mapovf_k0"] = np.array([k0, k1], np.int64)
+    o["cabi_mapovf_ec"], o["cabi_mapovf_vclk"], o["cabi_mapovf_vval"] = h(mres.ec), h(mres.vclk), h(mres.vval)
+    o["cabi_mapovf_nval"] = mres.nval.cpu().numpy().copy()
+    o["cabi_mapovf_flags"] = mres.flags.cpu().numpy().copy()
+    # a bad argument on ONE rank: every rank raises, none blocks; then a good call still works
+    codes = []
+    x = t(D.lattice_input("vclock")[0])
+    outb = torch.empty(x.shape[1], dtype=torch.int64, device=dev)
+    for bad in ("null_out", "dims"):
+        try:
+            if bad == "null_out":
+                ctx.call("crdt_vclock_lub_many_sharded", x.data_ptr(), 1, x.shape[0], x.shape[1], x.shape[1],
+                         0, None if rank == 1 else outb.data_ptr())
+            else:
+                W = x.shape[1] if rank == 0 else x.shape[1] - 2
+                ctx.call("crdt_vclock_lub_many_sharded", x.data_ptr(), 1, x.shape[0], W, x.shape[1], 0, outb.data_ptr())
+            codes.append(0)
+        except CrdtGpuError as e:
+            codes.append(e.code)
+    o["cabi_error_codes"] = np.array(codes, np.int64)
+    o["cabi_after_errors"] = h(cs.lub_many_sharded("vclock", x, ctx=ctx))
+    torch.cuda.synchronize()
+    cs.comm_destroy(ctx)
+    return o
 
 
 if __name__ == "__main__":

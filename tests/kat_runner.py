@@ -26,7 +26,7 @@ def _vc(pairs):
 
 def _new(kind):
     return {"vclock": O.VClock, "gcounter": O.GCounter, "pncounter": O.PNCounter,
-            "gset": O.GSet, "orswot": O.Orswot}[kind]()
+            "gset": O.GSet, "orswot": O.Orswot, "mvreg": O.MVReg}[kind]()
 
 
 def _clone(x):
@@ -42,14 +42,16 @@ def _clone(x):
         return O.GSet(x.value)
     if isinstance(x, O.LWWReg):
         return O.LWWReg(x.val, x.marker)
-    if isinstance(x, O.ReadCtx):
+    if isinstance(x, O.MVReg):
+        return x.copy()
+    if isinstance(x, (O.ReadCtx, O.MVRegPut)):
         return x
     raise TypeError(type(x))
 
 
 def kind_of(x):
     for k, t in (("vclock", O.VClock), ("gcounter", O.GCounter), ("pncounter", O.PNCounter),
-                 ("gset", O.GSet), ("orswot", O.Orswot), ("lwwreg", O.LWWReg)):
+                 ("gset", O.GSet), ("orswot", O.Orswot), ("lwwreg", O.LWWReg), ("mvreg", O.MVReg)):
         if isinstance(x, t):
             return k
     raise TypeError(type(x))
@@ -197,6 +199,26 @@ def run_case(case, merge_hook=default_merge, causal_hook=None, apply_hook=defaul
             assert env[args[0]].read().add_clock == _vc(args[1])
         elif op == "assert_deferred_len":
             assert len(env[args[0]].deferred) == args[1], env[args[0]].deferred
+        elif op == "mv_write":  # reg.apply(reg.write(val, reg.read().derive_add_ctx(actor)))
+            v = env[args[0]]
+            apply_hook(v, v.write(args[1], v.read().derive_add_ctx(args[2])))
+        elif op == "mv_write_from":  # dst.apply(src.write(val, src.read().derive_add_ctx(actor)))
+            dst, src = env[args[0]], env[args[1]]
+            apply_hook(dst, src.write(args[2], src.read().derive_add_ctx(args[3])))
+        elif op == "mv_put":  # reg.apply(Op::Put { clock, val })
+            apply_hook(env[args[0]], O.MVRegPut(_vc(args[1]), args[2]))
+        elif op == "save_mv_write_ctx":  # op = reg.write(val, ctx.derive_add_ctx(actor))
+            env[args[0]] = env[args[1]].write(args[2], env[args[3]].derive_add_ctx(args[4]))
+        elif op == "apply_op":
+            apply_hook(env[args[0]], env[args[1]])
+        elif op == "assert_mv_vals":
+            assert env[args[0]].read().val == args[1], (env[args[0]].read().val, args[1])
+        elif op == "assert_mv_vals_any":
+            assert env[args[0]].read().val in args[1], (env[args[0]].read().val, args[1])
+        elif op == "assert_eq":
+            assert env[args[0]] == env[args[1]], (env[args[0]], env[args[1]])
+        elif op == "assert_eq_new":
+            assert env[args[0]] == _new(args[1]), env[args[0]]
         elif op == "assert_lww":
             assert env[args[0]] == O.LWWReg(args[1], args[2]), env[args[0]]
         else:

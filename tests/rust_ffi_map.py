@@ -15,7 +15,15 @@ def _strip_comments(text: str) -> str:
 
 
 def rust_type(ctype: str) -> str:
-    """`const uint64_t *` -> `*const u64`, `crdt_ctx **` -> `*mut *mut crdt_ctx`, `int` -> `c_int`."""
+    """`const uint64_t *` -> `*const u64`, `crdt_ctx **` -> `*mut *mut crdt_ctx`, `int` -> `c_int`;
+    a function pointer `int (*)(void *user, size_t n)` -> `Option<unsafe extern "C" fn(*mut c_void,
+    usize) -> c_int>` (NULL-able, as the header allows)."""
+    fm = re.match(r"^(.*?)\(\s*\*\s*\)\s*\((.*)\)$", " ".join(ctype.split()))
+    if fm:
+        ret, params = fm.group(1).strip(), fm.group(2).strip()
+        args = [] if params in ("", "void") else [rust_type(_split_decl(p.strip())[0]) for p in params.split(",")]
+        r = rust_type(ret)
+        return 'Option<unsafe extern "C" fn(' + ", ".join(args) + ")" + ("" if r == "()" else " -> " + r) + ">"
     t = " ".join(ctype.replace("*", " * ").split())
     if t == "void":
         return "()"
@@ -72,6 +80,10 @@ def parse_header(text: str):
         for stmt in body.split(";"):
             stmt = " ".join(stmt.split())
             if not stmt:
+                continue
+            fp = re.match(r"^(.*?)\(\s*\*\s*(\w+)\s*\)\s*\((.*)\)$", stmt)
+            if fp:  # function pointer field: 'int (*allgather)(void *user, ...)'
+                fields.append((f"{fp.group(1).strip()} (*)({fp.group(3).strip()})", fp.group(2)))
                 continue
             # 'size_t G, R, M, A' and 'const uint64_t *def_clock'
             first, *rest = [x.strip() for x in stmt.split(",")]

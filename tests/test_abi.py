@@ -65,7 +65,8 @@ HOST_CAPABLE = {f"crdt_{t}_{op}" for t in ("vclock", "gcounter", "pncounter", "g
                 for op in ("lub_many", "merge_batch")}
 CTX_ONLY = {"crdt_ctx_destroy", "crdt_ctx_set_stream", "crdt_ctx_synchronize", "crdt_ctx_set_timing",
             "crdt_ctx_timing", "crdt_ctx_timing_reset", "crdt_ctx_tune", "crdt_ctx_set_mem_kind",
-            "crdt_ctx_comm_init", "crdt_ctx_comm_destroy", "crdt_ctx_comm_info", "crdt_ctx_mem_kind"}
+            "crdt_ctx_comm_init", "crdt_ctx_comm_destroy", "crdt_ctx_comm_info", "crdt_ctx_mem_kind",
+            "crdt_ctx_comm_init_ops"}
 
 
 def test_every_compute_entry_point_guards_host_mode():
@@ -84,6 +85,12 @@ def test_every_compute_entry_point_guards_host_mode():
             if name in HOST_CAPABLE:
                 assert ("CRDT_CHECK_CTX" in first or "_dispatch(ctx" in first or first.startswith("return crdt_")
                         or "_host(ctx" in first or "mem_kind == CRDT_MEM_HOST" in first), name
+            elif name.endswith("_sharded"):
+                # collective: the host-mode refusal is part of the agreed validation status (every
+                # rank must learn it), so it is not the first statement (csrc/shard.hip)
+                body = open(f).read()[m.end(2):]
+                body = body[:body.index("\n}\n")]
+                assert first.startswith("return lattice_sharded(") or "device_mem_only(ctx, what)" in body, name
             elif name not in CTX_ONLY:
                 assert first.startswith("CRDT_DEVICE_MEM_ONLY(ctx);"), (f, name)
     assert HOST_CAPABLE <= seen and len(seen) > 50

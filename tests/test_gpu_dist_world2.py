@@ -40,7 +40,8 @@ def outs(tmp_path_factory):
            os.path.join(HERE, "dist_world2_worker.py"), "--out", str(out)]
     env = dict(os.environ, OMP_NUM_THREADS="4")
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    ranks = "\n".join(x for x in r.stderr.splitlines() if x.startswith("[rank") or "Error" in x or "File " in x)
+    assert r.returncode == 0, ranks[-6000:] + "\n" + r.stdout[-2000:] + r.stderr[-2000:]
     return [dict(np.load(out / f"rank{k}.npz")) for k in range(2)]
 
 
@@ -101,3 +102,103 @@ def test_world2_map(outs):
                for j in np.flatnonzero(o["map_keep"])}
         assert got == exp[5]
     assert sorted(ks)[0][0] == 0 and sum(n for _, n in ks) == K
+
+
+# ---- the C ABI's own multi-rank code (csrc/shard.hip) through crdt_ctx_comm_init_ops -------------
+def test_world2_cabi_comm(outs):
+    for k, o in enumerate(outs):
+        assert tuple(o["cabi_comm"]) == (2, k)
+
+
+@pytest.mark.parametrize("name", sorted(D.LATTICES))
+def test_world2_cabi_lattices(outs, name):
+    kind, G, R, W = D.LATTICES[name]
+    full = D.lattice_input(name)
+    fold = O.gset_fold if kind == "gset" else O.vclock_fold
+    exp = np.stack([fold(full[g])[0] for g in range(G)])
+    for o in outs:
+        np.testing.assert_array_equal(o["cabi_" + name].reshape(G, W), exp)
+        np.testing.assert_array_equal(o["cabi_multi_" + name].reshape(G, W), exp)
+
+
+@pytest.mark.parametrize("tag", ["even", "r0empty", "uneven"])
+def test_world2_cabi_lwwreg(outs, tag):
+    """crdt_lwwreg_lub_many_sharded at world 2: the state and the GLOBAL first conflicting merge,
+    incl. a rank holding no replica (the "lower non-empty ranks" prefix, shard.hip)."""
+    m, v = D.lww_input()
+    for o in outs:
+        for g in range(m.shape[0]):
+            om, ov, of, _ = O.lwwreg_fold(m[g], v[g])
+            fc = int(o[f"cabi_lww_{tag}_conflict"][g])
+            got = (int(o[f"cabi_lww_{tag}_marker"][g]), int(o[f"cabi_lww_{tag}_val"][g]), 2**64 - 1 if fc == -1 else fc)
+            assert got == (om, ov, of)
+    assert any(int(x) != -1 for x in outs[0][f"cabi_lww_{tag}_conflict"])
+
+
+def test_world2_cabi_orswot(outs):
+    """crdt_orswot_lub_many_sharded at world 2: both ranks hold deferred removes, so the regroup
+    (rank order, then local order: r*Dmax + base[r]) and the compaction are exercised."""
+    clock, entries, off, dcl, dmem = D.orswot_input()
+    oc, oe, odef, _ = O.orswot_fold(clock, entries, off, dcl, dmem)
+    assert odef and all(int(o["cabi_orswot_ndef_local"][0]) > 0 for o in outs)
+    for o in outs:
+        np.testing.assert_array_equal(o["cabi_orswot_clock"][0], oc)
+        np.testing.assert_array_equal(o["cabi_orswot_entries"][0], oe)
+        got = {(tuple(int(x) for x in o["cabi_orswot_def_clock"][d]), O.bitmap_members(o["cabi_orswot_def_members"][d]))
+               for d in range(o["cabi_orswot_def_clock"].shape[0])}
+        assert got == odef
+
+
+@pytest.mark.parametrize("tag", ["even", "empty"])
+def test_world2_cabi_map(outs, tag):
+    """crdt_map_lub_many_sharded at world 2: key placement at k0 != 0 with the SUM all-reduce, and
+    a rank whose key shard is EMPTY (it must still join every collective: ADVICE r2)."""
+    d = D.map_input()
+    exp = O.map_fold(d["clock"], d["ec"], d["vclk"], d["vval"], d["def_row"], d["def_clock"], d["def_keys"],
+                     D.MAP_VOUT)
+    assert exp[5]
+    covered = []
+    for o in outs:
+        k0, k1 = (int(x) for x in o[f"cabi_map_{tag}_k0"])
+        covered.append((k0, k1))
+        np.testing.assert_array_equal(o[f"cabi_map_{tag}_clock"][0], exp[0])
+        np.testing.assert_array_equal(o[f"cabi_map_{tag}_ec"][0], exp[1][k0:k1])
+        np.testing.assert_array_equal(o[f"cabi_map_{tag}_vclk"][0], exp[2][k0:k1])
+        np.testing.assert_array_equal(o[f"cabi_map_{tag}_vval"][0], exp[3][k0:k1])
+        np.testing.assert_array_equal(o[f"cabi_map_{tag}_nval"][0], exp[4][k0:k1])
+        got = {(tuple(int(x) for x in d["def_clock"][j]), O.bitmap_members(o[f"cabi_map_{tag}_def_keys"][j]))
+               for j in np.flatnonzero(o[f"cabi_map_{tag}_keep"])}
+        assert got == exp[5]
+    if tag == "empty":
+        assert (d["ec"].shape[1], d["ec"].shape[1]) in covered
+
+
+def test_world2_cabi_map_overflow_on_one_rank(outs):
+    """Only rank 1's key folds to 12 values: with vout=8 its fold state (8 values) overflows, the C
+    call reruns EVERY rank with the 16-value state (the retry used to be rank-local, so
+    one rank entered the collective twice), and the global flags make BOTH ranks raise the capacity
+    error; with vout=16 both return the exact fold."""
+    assert all(int(o["cabi_mapovf_raised"][0]) == 1 for o in outs)
+    d = D.map_overflow_input()
+    exp = O.map_fold(d["clock"], d["ec"], d["vclk"], d["vval"], d["def_row"], d["def_clock"], d["def_keys"],
+                     D.MAP_OVF_VOUT)
+    assert int(exp[4][-1]) == 12
+    for o in outs:
+        k0, k1 = (int(x) for x in o["cabi_mapovf_k0"])
+        np.testing.assert_array_equal(o["cabi_mapovf_ec"][0], exp[1][k0:k1])
+        np.testing.assert_array_equal(o["cabi_mapovf_vclk"][0], exp[2][k0:k1])
+        np.testing.assert_array_equal(o["cabi_mapovf_vval"][0], exp[3][k0:k1])
+        np.testing.assert_array_equal(o["cabi_mapovf_nval"][0], exp[4][k0:k1])
+    assert int(outs[0]["cabi_mapovf_flags"][0]) == int(outs[1]["cabi_mapovf_flags"][0])
+
+
+def test_world2_cabi_errors_agree(outs):
+    """A NULL output on rank 1 (its own validation fails) and a row width that differs between the
+    ranks: EVERY rank returns an error instead of blocking in the all-reduce, and the communicator
+    still works afterwards."""
+    EINVAL, ECOMM = -1, -5
+    assert tuple(outs[0]["cabi_error_codes"]) == (ECOMM, EINVAL)
+    assert tuple(outs[1]["cabi_error_codes"]) == (EINVAL, EINVAL)
+    exp = O.vclock_fold(D.lattice_input("vclock")[0])[0]
+    for o in outs:
+        np.testing.assert_array_equal(o["cabi_after_errors"], exp)

@@ -227,6 +227,39 @@ def test_malformed_frames_and_missing_ids(gpu_ctx):
     assert st.cpu().tolist() == [1, 1]
 
 
+def test_orswot_lying_deferred_count_only_breaks_its_frame(gpu_ctx):
+    """a frame whose deferred-remove count is far larger than its bytes could hold must be
+    malformed on its own (status bit 0, no removes), not shift / wrap the pooled def_off of every
+    later state or make the wrapper allocate a (count, A) buffer."""
+    rng = np.random.default_rng(15)
+    R, M, A = 6, 50, 8
+    states, _ = orswot_objects(5, R, M, A)
+    assert all(de for _, _, de in states[:2])
+    aids, ad = actor_dict(rng, A)
+    mids, md = u64_dict(rng, M)
+    blob, foff = orswot_blob(states, aids, mids, rng)
+    fo = [int(x) for x in foff]
+    frames = [blob[fo[i]:fo[i + 1]] for i in range(len(fo) - 1)]
+    c0, e0, _ = states[2]
+    empty_def = O.bc_orswot({int(aids[a]): v for a, v in c0.items()},
+                            {int(mids[m]): {int(aids[a]): v for a, v in e.items()} for m, e in e0.items()}, [])
+    assert empty_def[-8:] == bytes(8)  # the trailing u64 is the deferred count (0)
+    lying = empty_def[:-8] + (1 << 40).to_bytes(8, "little")
+    parts = [bytes(frames[0]), lying, bytes(frames[1])]
+    blob2 = b"".join(parts)
+    off = np.cumsum([0] + [len(x) for x in parts]).tolist()
+    res = wire.orswot_ingest(dev_bytes(blob2), dev_off(off), ad, md, ctx=gpu_ctx)
+    assert res.status.cpu().tolist()[1] & 1 and res.status.cpu().tolist()[0] == 0 and res.status.cpu().tolist()[2] == 0
+    doff = res.def_off.cpu().numpy()
+    n0, n1 = len(states[0][2]), len(states[1][2])
+    assert doff.tolist() == [0, n0, n0, n0 + n1]
+    gd, gm = to_host(res.def_clock), to_host(res.def_members)
+    for r, st_ in ((0, 0), (2, 1)):
+        got = {(tuple((a, int(v)) for a, v in enumerate(gd[d]) if v), O.bitmap_members(gm[d]))
+               for d in range(int(doff[r]), int(doff[r + 1]))}
+        assert got == {(k, frozenset(ms)) for k, ms in states[st_][2].items()}
+
+
 # ---- the reference's KATs with every merge through bytes -------------------------------------
 def _ids(values):
     """Deterministic u32 / u64 ids for the KATs' actors and members (strings or ints)."""

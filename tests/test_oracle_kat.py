@@ -3,7 +3,7 @@ import pytest
 
 import kat_runner as K
 
-CASES = [(f, c) for f in ("kat_vclock.json", "kat_counters.json", "kat_orswot.json")
+CASES = [(f, c) for f in ("kat_vclock.json", "kat_counters.json", "kat_orswot.json", "kat_mvreg.json")
          for c in K.load_cases(f)]
 
 

@@ -125,3 +125,34 @@ def test_rust_sources_balanced(path):
             assert stack and stack[-1] == pairs[ch], path
             stack.pop()
     assert not stack, path
+
+
+def test_capacity_constants_match_the_header():
+    """The shim's capacity constants are the limits the header states (VERDICT r2: Map::lub_many
+    refused V > 4 while the library takes V <= 8)."""
+    consts = dict(re.findall(r"pub const (\w+): usize = (\d+);", MOD))
+    hdr = " ".join(HEADER.split())
+    assert "V <= 8" in hdr and int(consts["MAP_MAX_VALUES"]) == 8
+    assert "Limits: A <= 256" in hdr and int(consts["MAP_MAX_ACTORS"]) == 256
+    assert "Dcap(self) + Dcap(other) <= 512" in hdr and int(consts["MERGE_MAX_DEFERRED"]) == 512
+    # the Map paths check their inputs against these constants, not literals
+    assert "vmax.min(4)" not in MOD and "d.vmax > 4" not in MOD
+    assert MOD.count("MAP_MAX_VALUES") >= 3 and MOD.count("MERGE_MAX_DEFERRED") >= 3
+
+
+def test_merge_batch_checks_statuses_before_writing_back():
+    """a merge_batch that fails on pair i must not have replaced selves[0..i], and
+    mismatched lengths are an error, not a silent truncation."""
+    assert "selves.len().min(others.len())" not in MOD
+    for m in re.finditer(r"let mut stv = vec!\[0u32; n\];", MOD):
+        tail = MOD[m.end():m.end() + 1200]
+        first_find = tail.find(".find(|&i| stv[i] != 0)")
+        first_write = tail.find("selves[i] =")
+        assert 0 <= first_find < first_write
+
+
+def test_lwwreg_binds_the_generic_marker():
+    """FunkyCvRDT for LWWReg<V: PartialEq, M: Ord> (lwwreg.rs:30-46): markers interned order-
+    preservingly, values compared with PartialEq only."""
+    assert "impl<V: PartialEq + Clone, M: Ord + Clone> BatchFunkyLww for LWWReg<V, M>" in MOD
+    assert "LWWReg<V, u64>" not in MOD.split("fn marker_ids")[1]
