@@ -711,7 +711,9 @@ _LIB = None
 def lib():
     global _LIB
     if _LIB is None:
-        path = os.path.join(HERE, "build", "liboracle.so")
+        # ORACLE_LIB: another build of the same source (tests/test_sanitizers.py loads the
+        # -fsanitize=address,undefined one)
+        path = os.environ.get("ORACLE_LIB") or os.path.join(HERE, "build", "liboracle.so")
         if not os.path.exists(path):
             raise FileNotFoundError(f"{path} missing: run `make -C oracle`")
         L = ctypes.CDLL(path)
