@@ -7,7 +7,7 @@ tag=${1:-r02}
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-B="bench.py --steps 10 --warmup 2 --no-cpu-baseline"
+B="bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-c5"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$tag -o run -- python3 $B > gpurun_out/prof_$tag.log 2>&1 || exit $?
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch_$tag -o run -- python3 $B > gpurun_out/pmc_fetch_$tag.log 2>&1 || exit $?
 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write_$tag -o run -- python3 $B > gpurun_out/pmc_write_$tag.log 2>&1 || exit $?
