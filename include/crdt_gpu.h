@@ -84,10 +84,13 @@ int crdt_ctx_tune(crdt_ctx *ctx, const char *spec);
  *     crdt_lwwreg_lub_many / _merge_batch,
  *     crdt_orswot_lub_many / _merge_batch, crdt_map_lub_many / _merge_batch (every pointer in
  *     the structs; def_off stays host)
- * are HOST pointers (pageable, or pinned by crdt_host_alloc for direct DMA).  The lattice and LWW
- * forms stream them through two ctx-owned device chunk buffers (tune key stage_kb, default
- * 256 MiB each), overlapping the H2D copy of chunk k+1 with the fold of chunk k; the Orswot and
- * Map forms stage the whole batch (the deferred removes need every replica's clock).  The call returns when
+ * are HOST pointers (pageable, or pinned by crdt_host_alloc for direct DMA).  The lub_many forms
+ * stream them through two ctx-owned device chunk buffers (tune key stage_kb, default 256 MiB
+ * each), overlapping the H2D copy of chunk k+1 with the fold of chunk k: lattice / LWW folds
+ * accumulate; Orswot joins each chunk into a running join kept in HBM and settles the deferred
+ * removes once at the end; Map folds each chunk behind the running fold as its replica 0 (its
+ * surviving removes carried along), falling back to whole-batch staging when a key needs more than
+ * 8 value slots mid-fold.  merge_batch of Orswot / Map stages the whole batch.  The call returns when
  * the results are in host memory.  Results are identical to the device-pointer call.  In host mode
  * crdt_lwwreg_lub_many needs out_marker and out_val; a device pointer is rejected (CRDT_EINVAL);
  * every other entry point returns CRDT_EUNSUPPORTED. */
@@ -176,7 +179,13 @@ int crdt_lwwreg_merge_batch(crdt_ctx *ctx, uint64_t *self_marker, uint64_t *self
 
 /* ---- Orswot<member, actor> ---------------------------------------------------------------
  * Replaces Orswot::merge (orswot.rs:81-149) incl. apply_rm (:230-250) and apply_deferred
- * (:281-286).  Dense layout per replica (g, r):
+ * (:281-286).
+ * Precondition (the reference's own invariants, kept by every state its API builds): each dot is
+ * unique to one replica and entry dots are covered by their replica's clock (E <= C).  Under them
+ * the per-cell join is associative, and the kernels fold replica slices (and host-mode chunks) in
+ * any grouping, exactly; states outside them (an arbitrary E > C) are not left-fold exact here
+ * (crdt_orswot_merge_batch below is exact for ANY pair of states).
+ * Dense layout per replica (g, r):
  *   clock   C[g][r][a]      at clock   + g*clock_gstride + r*clock_rstride + a
  *   entries E[g][r][m][a]   at entries + g*entry_gstride + r*entry_rstride + m*entry_mstride + a
  *                            (E = the member's dot clock; member absent <=> row all 0)

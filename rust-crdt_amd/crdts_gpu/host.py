@@ -184,7 +184,9 @@ def orswot_lub_many(clock: np.ndarray, entries: np.ndarray, def_off=None, def_cl
                     def_members: Optional[np.ndarray] = None, ctx: Optional[HostContext] = None) -> OrswotHostLub:
     """crdt_orswot_lub_many on host arrays: clock (G, R, A), entries (G, R, M, A) (or without G),
     deferred removes pooled per group (def_off G+1, def_clock (D, A), def_members (D, Mw)).  The
-    library stages the whole batch (the deferred survival test needs every replica's clock)."""
+    library streams replica chunks through its stage buffers (the running join kept in HBM, the
+    deferred removes settled once against the final clock); exact for states with e <= c, the
+    precondition of every Orswot lub_many (include/crdt_gpu.h)."""
     ctx = ctx or HostContext.default()
     c = clock[None] if clock.ndim == 2 else clock
     e = entries[None] if entries.ndim == 3 else entries
@@ -259,7 +261,9 @@ def map_lub_many(clock, ec, vclk, vval, def_off=None, def_row=None, def_clock=No
                  ctx: Optional[HostContext] = None) -> MapHostLub:
     """crdt_map_lub_many on host arrays (one group): clock (R, A), ec (R, K, A), vclk (R, K, V, A),
     vval (R, K, V); removes pooled (def_off [0, D], def_row (D,) uint32, def_clock (D, A),
-    def_keys (D, Kw)).  Whole-batch staging by the library."""
+    def_keys (D, Kw)).  The library streams replica chunks through its stage buffers, the running
+    fold carried as replica 0 of the next chunk (exact for any input: the fold is the exact left
+    fold); a key needing more than 8 value slots mid-fold falls back to whole-batch staging."""
     ctx = ctx or HostContext.default()
     arrs = [np.ascontiguousarray(_u64(x, n)) for x, n in ((clock, "clock"), (ec, "ec"), (vclk, "vclk"), (vval, "vval"))]
     c, e, vc, vv = arrs

@@ -70,6 +70,8 @@ struct Tune {
   int map_pair_reg = 1;        // Map merge_batch, V <= 4: 1 sub-wave register kernel, 2 whole-wave one, 0 generic
   int pair_rows = 128;         // Orswot merge_batch: member rows per workgroup (64, 128, 256)
   int stage_kb = 262144;       // CRDT_MEM_HOST: bytes per device chunk buffer (KiB; two buffers)
+  int wire_walk = 1;           // Map ingest: walk + batched parse (0: one dependent chain per state)
+  int host_stream = 1;         // CRDT_MEM_HOST Orswot / Map lub_many: stream replica chunks (0: stage whole)
 };
 
 struct PendingTiming {

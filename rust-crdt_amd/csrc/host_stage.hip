@@ -29,6 +29,27 @@ __global__ void lww_fc_combine_kernel(u64 *glob, const u64 *chunk, u64 r0, unsig
 
 static size_t stage_budget(crdt_ctx *ctx) { return (size_t)ctx->tune.stage_kb << 10; }
 
+// dst row i <- src row i (rows of `width` u64 words at pitches dpitch / spitch; src may be NULL: zeros),
+// as a kernel on the ctx stream so it is ordered with the kernels around it
+__global__ void copy_rows_kernel(u64 *dst, size_t dpitch, const u64 *src, size_t spitch, size_t width, size_t rows) {
+  const size_t n = width * rows;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const size_t r = i / width, c = i % width;
+    dst[r * dpitch + c] = src ? src[r * spitch + c] : 0;
+  }
+}
+static int dev_rows(crdt_ctx *ctx, u64 *dst, size_t dpitch, const u64 *src, size_t spitch, size_t width, size_t rows) {
+  const size_t n = width * rows;
+  if (n == 0) return CRDT_OK;
+  size_t blocks = (n + kBlock - 1) / kBlock;
+  const size_t cap = (size_t)ctx->cu_count * 8;
+  if (blocks > cap) blocks = cap;
+  hipLaunchKernelGGL(copy_rows_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, ctx->stream, dst, dpitch, src, spitch,
+                     width, rows);
+  CRDT_HIP(ctx, hipGetLastError());
+  return CRDT_OK;
+}
+
 // Two chunk buffers of >= bytes each, the copy stream and its events; plus `acc` bytes of
 // accumulator (ctx->hacc).
 static int ensure_stage(crdt_ctx *ctx, size_t bytes, size_t acc) {
@@ -408,6 +429,97 @@ static int orswot_lub_host_body(crdt_ctx *ctx, const crdt_orswot_batch *in, crdt
   return CRDT_OK;
 }
 
+// ---- Orswot: replica chunks streamed through the two device chunk buffers ---------------------------
+// The join without deferred removes is associative under the reference invariants (each dot unique,
+// e <= c: the precondition every lub_many of this library states), so the batch streams: chunk k's
+// replicas are copied (copy stream) into buffer k&1 behind slot 0 of every group, slot 0 holds the
+// running join of the chunks before (device-to-device from the accumulator, or zeros: the join's
+// identity), and the chunk is joined into the accumulator on the ctx stream while chunk k+1 copies.
+// The deferred removes (few: rm clock + member bitmap each) are staged whole and settled once, by
+// a last lub_many over the accumulator alone (R = 1: the join of one replica is itself), whose
+// survival test and forget ceiling then read the final clock (orswot.rs:141-147, :240-249).
+// Device memory: two chunk buffers (tune key stage_kb) + the accumulator + the outputs.
+static int orswot_lub_host_stream(crdt_ctx *ctx, const crdt_orswot_batch *in, crdt_orswot_out *out, DevScratch &ds,
+                                  size_t Rc) {
+  const size_t G = in->G, R = in->R, M = in->M, A = in->A, Mw = (M + 63) / 64;
+  const size_t D = in->def_off ? in->def_off[G] : 0;
+  const size_t S = Rc + 1;  // replica slots per group in a chunk buffer (slot 0 = the running join)
+  const size_t cwords = G * S * A, ewords = G * S * M * A;
+  if (int rc = ensure_stage(ctx, (cwords + ewords) * 8, G * (A + M * A) * 8)) return rc;
+  uint64_t *acc_c = static_cast<uint64_t *>(ctx->hacc), *acc_e = acc_c + G * A;
+  uint64_t *dc = nullptr, *dm = nullptr, *oc = nullptr, *oe = nullptr, *om = nullptr;
+  uint8_t *ok = nullptr;
+  if (int rc = ds.get(ctx, D * A, &dc)) return rc;
+  if (int rc = ds.get(ctx, D * Mw, &dm)) return rc;
+  if (int rc = ds.get(ctx, G * A, &oc)) return rc;
+  if (int rc = ds.get(ctx, G * M * A, &oe)) return rc;
+  if (out->def_keep && (int)ds.get(ctx, D, &ok)) return CRDT_ENOMEM;
+  if (out->def_members && (int)ds.get(ctx, D * Mw, &om)) return CRDT_ENOMEM;
+  const size_t nch = (R + Rc - 1) / Rc;
+  for (size_t k = 0; k < nch; ++k) {
+    const int b = (int)(k & 1);
+    uint64_t *bc = static_cast<uint64_t *>(ctx->hbuf[b]), *be = bc + cwords;
+    const size_t r0 = k * Rc, n = std::min(Rc, R - r0);
+    if (int rc = begin_chunk(ctx, b)) return rc;
+    for (size_t g = 0; g < G; ++g) {  // replicas r0 .. r0+n of group g behind its slot 0
+      STAGE_HIP(copy_rows(bc + (g * S + 1) * A, A * 8, in->clock + g * in->clock_gstride + r0 * in->clock_rstride,
+                          in->clock_rstride * 8, A * 8, n, hipMemcpyHostToDevice, ctx->hstream));
+      STAGE_HIP(copy_rows(be + (g * S + 1) * M * A, M * A * 8,
+                          in->entries + g * in->entry_gstride + r0 * in->entry_rstride, in->entry_rstride * 8,
+                          M * A * 8, n, hipMemcpyHostToDevice, ctx->hstream));
+    }
+    if (int rc = copied_chunk(ctx, b)) return rc;
+    // slot 0: the join so far, or for the first chunk the join's identity (no dot, zero clock)
+    if (int rc = dev_rows(ctx, (u64 *)bc, S * A, k ? (const u64 *)acc_c : nullptr, A, A, G)) return rc;
+    if (int rc = dev_rows(ctx, (u64 *)be, S * M * A, k ? (const u64 *)acc_e : nullptr, M * A, M * A, G)) return rc;
+    crdt_orswot_batch cb{};
+    cb.G = G;
+    cb.R = n + 1;
+    cb.M = M;
+    cb.A = A;
+    cb.clock = bc;
+    cb.clock_rstride = A;
+    cb.clock_gstride = S * A;
+    cb.entries = be;
+    cb.entry_mstride = A;
+    cb.entry_rstride = M * A;
+    cb.entry_gstride = S * M * A;
+    crdt_orswot_out co{acc_c, acc_e, nullptr, nullptr};
+    {
+      DeviceModeScope dev(ctx);
+      if (int rc = crdt_orswot_lub_many(ctx, &cb, &co)) return rc;
+    }
+    if (int rc = end_chunk(ctx, b)) return rc;
+  }
+  // the deferred removes, settled once against the final join
+  if (int rc = h2d_async(ctx, dc, in->def_clock, D * A * 8)) return rc;
+  if (int rc = h2d_async(ctx, dm, in->def_members, D * Mw * 8)) return rc;
+  crdt_orswot_batch fb{};
+  fb.G = G;
+  fb.R = 1;
+  fb.M = M;
+  fb.A = A;
+  fb.clock = acc_c;
+  fb.clock_rstride = A;
+  fb.clock_gstride = A;
+  fb.entries = acc_e;
+  fb.entry_mstride = A;
+  fb.entry_rstride = M * A;
+  fb.entry_gstride = M * A;
+  fb.def_off = in->def_off;
+  fb.def_clock = dc;
+  fb.def_members = dm;
+  crdt_orswot_out o{oc, oe, ok, om};
+  {
+    DeviceModeScope dev(ctx);
+    if (int rc = crdt_orswot_lub_many(ctx, &fb, &o)) return rc;
+  }
+  if (int rc = d2h_async(ctx, out->clock, oc, G * A * 8)) return rc;
+  if (int rc = d2h_async(ctx, out->entries, oe, G * M * A * 8)) return rc;
+  if (int rc = d2h_async(ctx, out->def_keep, ok, D)) return rc;
+  return d2h_async(ctx, out->def_members, om, D * Mw * 8);
+}
+
 int orswot_lub_many_host(crdt_ctx *ctx, const crdt_orswot_batch *in, crdt_orswot_out *out) {
   if (!in || !out) return fail(ctx, CRDT_EINVAL, "orswot_lub_many: NULL batch/out");
   if (in->G == 0 || in->M == 0 || in->A == 0) return CRDT_OK;
@@ -422,6 +534,12 @@ int orswot_lub_many_host(crdt_ctx *ctx, const crdt_orswot_batch *in, crdt_orswot
     if (int rc = check_host(ctx, p, w)) return rc;
   CRDT_HIP(ctx, hipSetDevice(ctx->device));
   DevScratch ds;
+  // streamed in replica chunks when a chunk of >= 2 replicas per group fits a stage buffer and the
+  // member rows are packed; the whole batch staged otherwise
+  const size_t rb = (in->A + in->M * in->A) * 8, per = in->G * rb;
+  const size_t slots = per ? stage_budget(ctx) / per : 0;
+  if (ctx->tune.host_stream && in->R > 1 && slots >= 3 && (in->entry_mstride == in->A || in->M == 1))
+    return finish(ctx, orswot_lub_host_stream(ctx, in, out, ds, std::min(slots - 1, in->R)));
   return finish(ctx, orswot_lub_host_body(ctx, in, out, ds));
 }
 
@@ -567,6 +685,249 @@ static int map_lub_host_body(crdt_ctx *ctx, const crdt_map_batch *in, crdt_map_o
   return d2h_async(ctx, out->def_keys, odk, D * Kw * 8);
 }
 
+// Value planes of n replicas widened from V to Vi slots: key row (r, key) of dw words at
+// dst + r*dslot + key*dw = the packed source row (sw words, at src + (r*K + key)*sw), then zeros.
+__global__ void widen_planes_kernel(u64 *dst, size_t dslot, const u64 *src, size_t K, size_t n, size_t dw, size_t sw) {
+  const size_t total = n * K * dw;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const size_t r = i / (K * dw), rem = i % (K * dw), key = rem / dw, c = rem % dw;
+    dst[r * dslot + key * dw + c] = c < sw ? src[(r * K + key) * sw + c] : 0;
+  }
+}
+
+// ---- Map<K, MVReg>: replica chunks, the running fold as replica 0 --------------------------------
+// The fold is an exact left fold for any input, and Map::new().merge(acc) == acc for a fold result
+// acc (its deferred removes are already applied to it and stay undominated), so
+//   fold(r_0 .. r_{n-1}) == fold(acc_k, r_k .. r_{n-1}),  acc_k = fold(r_0 .. r_{k-1})
+// (checked on the oracle's Map over op-replay histories: tests/test_oracle_map_assoc.py).  Chunk k is
+// copied (copy stream) behind slot 0 of every group, slot 0 holds acc_k (its value slots widened to
+// Vi), the chunk's deferred pool = acc_k's surviving removes (held by replica 0) + the removes the
+// chunk's replicas hold, and the fold writes acc_{k+1}.  The host reads each chunk's surviving
+// removes (a few rows) while the next chunk copies.  A key needing more than Vi value slots sets
+// *retry (the caller widens Vi or stages the whole batch).
+static int map_lub_host_stream(crdt_ctx *ctx, const crdt_map_batch *in, crdt_map_out *out, DevScratch &ds, size_t Rc,
+                               size_t Vi, bool *retry) {
+  const size_t G = in->G, R = in->R, K = in->K, A = in->A, V = in->V, Kw = (K + 63) / 64, Vo = out->Vout;
+  const size_t D = in->def_off ? in->def_off[G] : 0;
+  const size_t S = Rc + 1;
+  *retry = false;
+  // chunk buffer per group: S slots of [clock A | ec K*A | vclk K*Vi*A | vval K*Vi], then (Vi > V)
+  // the chunk's raw value planes [Rc][K*V*A | K*V] widened by a kernel
+  const size_t wc = A, we = K * A, wv = K * Vi * A, wvv = K * Vi, slot = wc + we + wv + wvv;
+  const bool widen = Vi > V;
+  const size_t raw = widen ? Rc * K * V * (A + 1) : 0;
+  if (int rc = ensure_stage(ctx, (G * (S * slot + raw)) * 8, (G * slot) * 8)) return rc;
+  uint64_t *acc = static_cast<uint64_t *>(ctx->hacc);
+  uint64_t *a_c = acc, *a_ec = a_c + G * wc, *a_vc = a_ec + G * we, *a_vv = a_vc + G * wv;
+  // the chunk pools: at most the carried survivors (<= D) + the chunk's own removes (<= D)
+  const size_t P = 2 * D + 1;
+  uint64_t *p_pack = nullptr;  // [P u32 rows, padded | P*A clocks | P*Kw keys]
+  uint64_t *p_keys_out = nullptr, *fl_nv = nullptr;
+  uint8_t *p_keep = nullptr;
+  const size_t rw = (P + 1) / 2;
+  if (int rc = ds.get(ctx, rw + P * (A + Kw), &p_pack)) return rc;
+  if (int rc = ds.get(ctx, P * Kw, &p_keys_out)) return rc;
+  if (int rc = ds.get(ctx, P, &p_keep)) return rc;
+  if (int rc = ds.get(ctx, (G + G * K + 1) / 2 + 1, &fl_nv)) return rc;  // flags [G] | nval [G*K] (u32)
+  uint32_t *d_flags = reinterpret_cast<uint32_t *>(fl_nv), *d_nval = d_flags + G;
+  // carried survivors per group: (original pool index, rm clock, key union)
+  struct Carry {
+    size_t orig;
+    std::vector<uint64_t> clock, keys;
+  };
+  std::vector<std::vector<Carry>> carry(G);
+  std::vector<size_t> dpos(G, 0);  // next of each group's removes (in replica order) not yet pooled
+  for (size_t g = 0; g < G; ++g) dpos[g] = in->def_off ? in->def_off[g] : 0;
+  const size_t nch = (R + Rc - 1) / Rc;
+  auto copy_chunk = [&](size_t k) -> int {
+    const int b = (int)(k & 1);
+    uint64_t *buf = static_cast<uint64_t *>(ctx->hbuf[b]);
+    const size_t r0 = k * Rc, n = std::min(Rc, R - r0);
+    if (int rc = begin_chunk(ctx, b)) return rc;
+    for (size_t g = 0; g < G; ++g) {
+      uint64_t *gb = buf + g * S * slot;  // slot s of group g at gb + s*slot
+      STAGE_HIP(copy_rows(gb + slot, slot * 8, in->clock + g * in->clock_gstride + r0 * in->clock_rstride,
+                          in->clock_rstride * 8, wc * 8, n, hipMemcpyHostToDevice, ctx->hstream));
+      STAGE_HIP(copy_rows(gb + slot + wc, slot * 8, in->ec + g * in->ec_gstride + r0 * in->ec_rstride,
+                          in->ec_rstride * 8, we * 8, n, hipMemcpyHostToDevice, ctx->hstream));
+      const uint64_t *hv = in->vclk + g * in->vclk_gstride + r0 * in->vclk_rstride;
+      const uint64_t *hvv = in->vval + g * in->vval_gstride + r0 * in->vval_rstride;
+      if (!widen) {
+        STAGE_HIP(copy_rows(gb + slot + wc + we, slot * 8, hv, in->vclk_rstride * 8, wv * 8, n, hipMemcpyHostToDevice,
+                            ctx->hstream));
+        STAGE_HIP(copy_rows(gb + slot + wc + we + wv, slot * 8, hvv, in->vval_rstride * 8, wvv * 8, n,
+                            hipMemcpyHostToDevice, ctx->hstream));
+      } else {
+        uint64_t *rg = buf + G * S * slot + g * Rc * K * V * (A + 1);
+        STAGE_HIP(copy_rows(rg, K * V * A * 8, hv, in->vclk_rstride * 8, K * V * A * 8, n, hipMemcpyHostToDevice,
+                            ctx->hstream));
+        STAGE_HIP(copy_rows(rg + n * K * V * A, K * V * 8, hvv, in->vval_rstride * 8, K * V * 8, n,
+                            hipMemcpyHostToDevice, ctx->hstream));
+      }
+    }
+    STAGE_HIP(hipEventRecord(ctx->hcopied[b], ctx->hstream));
+    return CRDT_OK;
+  };
+  if (nch > 0)
+    if (int rc = copy_chunk(0)) return rc;
+  std::vector<uint8_t> hkeep;
+  std::vector<uint64_t> hkeys;
+  std::vector<uint64_t> pack;
+  for (size_t k = 0; k < nch; ++k) {
+    const int b = (int)(k & 1);
+    uint64_t *buf = static_cast<uint64_t *>(ctx->hbuf[b]);
+    const size_t r0 = k * Rc, n = std::min(Rc, R - r0);
+    if (k + 1 < nch)  // the next chunk copies while this one folds (its buffer: freed by fold k-1)
+      if (int rc = copy_chunk(k + 1)) return rc;
+    STAGE_HIP(hipStreamWaitEvent(ctx->stream, ctx->hcopied[b], 0));
+    for (size_t g = 0; g < G; ++g) {
+      uint64_t *gb = buf + g * S * slot;
+      if (widen) {  // the raw V-slot planes into the chunk's Vi-slot rows (replicas 1..n)
+        const uint64_t *rg = buf + G * S * slot + g * Rc * K * V * (A + 1);
+        const size_t blocks = std::min<size_t>((n * K * Vi * A + kBlock - 1) / kBlock, (size_t)ctx->cu_count * 8);
+        hipLaunchKernelGGL(widen_planes_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, ctx->stream,
+                           (u64 *)(gb + slot + wc + we), slot, (const u64 *)rg, K, n, (size_t)(Vi * A), (size_t)(V * A));
+        hipLaunchKernelGGL(widen_planes_kernel, dim3((unsigned)std::max<size_t>(1, blocks / A)), dim3(kBlock), 0,
+                           ctx->stream, (u64 *)(gb + slot + wc + we + wv), slot, (const u64 *)(rg + n * K * V * A), K,
+                           n, (size_t)Vi, (size_t)V);
+        CRDT_HIP(ctx, hipGetLastError());
+      }
+      // slot 0: acc_k, or the empty Map for the first chunk
+      if (int rc = dev_rows(ctx, (u64 *)gb, slot, k ? (const u64 *)(a_c + g * wc) : nullptr, wc, wc, 1)) return rc;
+      if (int rc = dev_rows(ctx, (u64 *)(gb + wc), slot, k ? (const u64 *)(a_ec + g * we) : nullptr, we, we, 1)) return rc;
+      if (int rc = dev_rows(ctx, (u64 *)(gb + wc + we), slot, k ? (const u64 *)(a_vc + g * wv) : nullptr, wv, wv, 1))
+        return rc;
+      if (int rc = dev_rows(ctx, (u64 *)(gb + wc + we + wv), slot, k ? (const u64 *)(a_vv + g * wvv) : nullptr, wvv, wvv,
+                            1))
+        return rc;
+    }
+    // the chunk's deferred pool, group by group: carried survivors (replica 0), then the removes
+    // held by replicas r0 .. r0+n-1 (at rows 1..n)
+    std::vector<size_t> poff(G + 1, 0);
+    std::vector<size_t> porig;
+    std::vector<uint32_t> prow;
+    std::vector<uint64_t> pclk, pkeys;
+    for (size_t g = 0; g < G; ++g) {
+      for (auto &c : carry[g]) {
+        porig.push_back(c.orig);
+        prow.push_back(0);
+        pclk.insert(pclk.end(), c.clock.begin(), c.clock.end());
+        pkeys.insert(pkeys.end(), c.keys.begin(), c.keys.end());
+      }
+      const size_t dend = in->def_off ? in->def_off[g + 1] : 0;
+      while (dpos[g] < dend && in->def_row[dpos[g]] < r0 + n) {
+        const size_t d = dpos[g]++;
+        if (in->def_row[d] < r0) return fail(ctx, CRDT_EINVAL, "map_lub_many: def_row not non-decreasing");
+        porig.push_back(d);
+        prow.push_back((uint32_t)(in->def_row[d] - r0 + 1));
+        pclk.insert(pclk.end(), in->def_clock + d * A, in->def_clock + (d + 1) * A);
+        pkeys.insert(pkeys.end(), in->def_keys + d * Kw, in->def_keys + (d + 1) * Kw);
+      }
+      poff[g + 1] = porig.size();
+    }
+    const size_t np = porig.size();
+    if (np > P) return fail(ctx, CRDT_EINVAL, "map_lub_many: deferred pool past its bound");
+    if (np) {
+      pack.assign(rw + np * (A + Kw), 0);
+      std::memcpy(pack.data(), prow.data(), np * 4);
+      std::memcpy(pack.data() + rw, pclk.data(), np * A * 8);
+      std::memcpy(pack.data() + rw + np * A, pkeys.data(), np * Kw * 8);
+      if (int rc = stage_h2d(ctx, p_pack, pack.data(), pack.size() * 8)) return rc;
+    }
+    crdt_map_batch cb{};
+    cb.G = G;
+    cb.R = n + 1;
+    cb.K = K;
+    cb.A = A;
+    cb.V = Vi;
+    cb.clock = buf, cb.clock_rstride = slot, cb.clock_gstride = S * slot;
+    cb.ec = buf + wc, cb.ec_rstride = slot, cb.ec_gstride = S * slot;
+    cb.vclk = buf + wc + we, cb.vclk_rstride = slot, cb.vclk_gstride = S * slot;
+    cb.vval = buf + wc + we + wv, cb.vval_rstride = slot, cb.vval_gstride = S * slot;
+    if (np) {
+      cb.def_off = poff.data();
+      cb.def_row = reinterpret_cast<const uint32_t *>(p_pack);
+      cb.def_clock = p_pack + rw;
+      cb.def_keys = p_pack + rw + np * A;
+    }
+    size_t vstate = out->Vstate;
+    for (;;) {  // a fold state that ran out of value slots reruns this chunk (slot 0 still holds acc_k)
+      crdt_map_out co{Vi, vstate, a_c, a_ec, a_vc, a_vv, d_nval, d_flags, np ? p_keep : nullptr,
+                      np ? p_keys_out : nullptr};
+      {
+        DeviceModeScope dev(ctx);
+        if (int rc = crdt_map_lub_many(ctx, &cb, &co)) return rc;
+      }
+      std::vector<uint32_t> hf(G);
+      STAGE_HIP(hipMemcpyAsync(hf.data(), d_flags, G * 4, hipMemcpyDeviceToHost, ctx->stream));
+      STAGE_HIP(hipStreamSynchronize(ctx->stream));
+      uint32_t f = 0;
+      for (uint32_t x : hf) f |= x;
+      if (f & 2u) return fail(ctx, CRDT_EINVAL, "map_lub_many: def_row not non-decreasing or >= R");
+      if ((f & 4u) && vstate < 16) {
+        vstate = vstate < 8 ? 8 : 16;
+        continue;
+      }
+      if (f & 5u) {  // a key needs more than Vi slots (or than the state holds): widen / stage whole
+        *retry = true;
+        return CRDT_OK;
+      }
+      break;
+    }
+    STAGE_HIP(hipEventRecord(ctx->hfree[b], ctx->stream));
+    // the surviving removes of this chunk's pool are carried into the next (representatives with
+    // the union of their clock's key sets)
+    if (np) {
+      hkeep.resize(np);
+      hkeys.resize(np * Kw);
+      STAGE_HIP(hipMemcpyAsync(hkeep.data(), p_keep, np, hipMemcpyDeviceToHost, ctx->stream));
+      STAGE_HIP(hipMemcpyAsync(hkeys.data(), p_keys_out, np * Kw * 8, hipMemcpyDeviceToHost, ctx->stream));
+      STAGE_HIP(hipStreamSynchronize(ctx->stream));
+    }
+    for (size_t g = 0; g < G; ++g) {
+      std::vector<Carry> next;
+      for (size_t j = poff[g]; j < poff[g + 1]; ++j)
+        if (hkeep[j])
+          next.push_back(Carry{porig[j], std::vector<uint64_t>(pclk.begin() + j * A, pclk.begin() + (j + 1) * A),
+                               std::vector<uint64_t>(hkeys.begin() + j * Kw, hkeys.begin() + (j + 1) * Kw)});
+      carry[g] = std::move(next);
+    }
+  }
+  // outputs: acc (Vi slots) -> the caller's Vout slots; the survivors at their original indices
+  std::vector<uint32_t> nv(G * K, 0), hf(G, 0);
+  if (nch) {
+    STAGE_HIP(hipMemcpyAsync(nv.data(), d_nval, G * K * 4, hipMemcpyDeviceToHost, ctx->stream));
+    STAGE_HIP(hipMemcpyAsync(hf.data(), d_flags, G * 4, hipMemcpyDeviceToHost, ctx->stream));
+  } else {
+    if (int rc = device_fill(ctx, acc, G * slot * 8, 0)) return rc;
+  }
+  STAGE_HIP(copy_rows(out->clock, A * 8, a_c, A * 8, A * 8, G, hipMemcpyDeviceToHost, ctx->stream));
+  STAGE_HIP(copy_rows(out->ec, K * A * 8, a_ec, K * A * 8, K * A * 8, G, hipMemcpyDeviceToHost, ctx->stream));
+  const size_t vc = std::min(Vi, Vo);  // value slots per key that reach the caller
+  STAGE_HIP(copy_rows(out->vclk, Vo * A * 8, a_vc, Vi * A * 8, vc * A * 8, G * K, hipMemcpyDeviceToHost, ctx->stream));
+  STAGE_HIP(copy_rows(out->vval, Vo * 8, a_vv, Vi * 8, vc * 8, G * K, hipMemcpyDeviceToHost, ctx->stream));
+  STAGE_HIP(hipStreamSynchronize(ctx->stream));
+  for (size_t i = 0; i < G * K; ++i)
+    for (size_t s = vc; s < Vo; ++s) {  // slots past the acc's are empty
+      std::memset(out->vclk + (i * Vo + s) * A, 0, A * 8);
+      out->vval[i * Vo + s] = 0;
+    }
+  for (size_t g = 0; g < G; ++g) {
+    uint32_t f = hf[g] & ~1u;
+    for (size_t kk = 0; kk < K; ++kk) f |= nv[g * K + kk] > Vo ? 1u : 0u;
+    out->flags[g] = f;
+  }
+  if (out->nval) std::memcpy(out->nval, nv.data(), G * K * 4);
+  if (out->def_keep) std::memset(out->def_keep, 0, D);
+  if (out->def_keys) std::memset(out->def_keys, 0, D * Kw * 8);
+  for (size_t g = 0; g < G; ++g)
+    for (auto &c : carry[g]) {
+      if (out->def_keep) out->def_keep[c.orig] = 1;
+      if (out->def_keys) std::memcpy(out->def_keys + c.orig * Kw, c.keys.data(), Kw * 8);
+    }
+  return CRDT_OK;
+}
+
 int map_lub_many_host(crdt_ctx *ctx, const crdt_map_batch *in, crdt_map_out *out) {
   if (!in || !out) return fail(ctx, CRDT_EINVAL, "map_lub_many: NULL batch/out");
   if (in->G == 0) return CRDT_OK;
@@ -587,6 +948,23 @@ int map_lub_many_host(crdt_ctx *ctx, const crdt_map_batch *in, crdt_map_out *out
                       {out->flags, "out.flags"}, {out->def_keep, "out.def_keep"}, {out->def_keys, "out.def_keys"}})
     if (int rc = check_host(ctx, p, w)) return rc;
   CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  if (ctx->tune.host_stream && in->R > 1 && V <= 8 && out->Vout > 0) {
+    // streamed replica chunks: the running fold's value slots Vi hold the caller's Vout (at most
+    // 8, the fold's input limit); a key needing more widens Vi to 8, then stages the whole batch
+    size_t Vi = std::max(V, std::min<size_t>(out->Vout, 8));
+    for (;;) {
+      const size_t slot = A + K * A + K * Vi * A + K * Vi;
+      const size_t per = in->G * (slot + (Vi > V ? K * V * (A + 1) : 0)) * 8;
+      const size_t slots = per ? stage_budget(ctx) / per : 0;
+      if (slots < 3) break;
+      DevScratch ds;
+      bool retry = false;
+      const int rc = finish(ctx, map_lub_host_stream(ctx, in, out, ds, std::min(slots - 1, in->R), Vi, &retry));
+      if (rc || !retry) return rc;
+      if (Vi >= 8) break;
+      Vi = 8;
+    }
+  }
   DevScratch ds;
   return finish(ctx, map_lub_host_body(ctx, in, out, ds));
 }

@@ -820,6 +820,285 @@ __global__ __launch_bounds__(kBlock) void map_ingest_kernel(MapWirePlan p) {
   }
 }
 
+// ---- Map ingest, round 3: walk + batched parse ---------------------------------------------------
+// map_ingest_kernel above is one dependent chain per state: every VClock waits for its length, then
+// for its records, then fences its LDS row out (3 x 1,024 VClocks per config-4 state).  Here a state
+// is parsed in two roles by the same wave:
+//   the walk (scalar): only the lengths, keys, value counts and values — the positions of the
+//     VClocks and where each one goes — read from a 256-word register window of the frame; the
+//     frame streams through a per-wave LDS ring of kWalkRing windows by LDS-DMA, issued
+//     kWalkRing windows ahead of the walk, so a length costs a readlane, not a memory round trip;
+//   the parse (lane = VClock): every 64 VClocks found, lane i parses VClock i's records (loads in
+//     flight together, L2 hits behind the DMA) and stores each counter straight into its
+//     zero-filled destination row (no LDS row, no fence).
+// Deferred removes (a few per state, at the end of the frame) keep the row-staged parse.
+constexpr int kWalkWin = 256;  // words per window (one per lane per register, 4 registers)
+constexpr int kWalkRing = 8;   // LDS ring windows per wave
+
+template <int N>
+__device__ __forceinline__ void wire_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+struct MapWalk {
+  const uint32_t *fw;
+  unsigned long long nw, nwin, issued, cur;
+  uint32_t *ring;
+  uint32_t r0, r1, r2, r3;
+
+  __device__ void dma(unsigned long long wi, int lane) {
+    uint32_t *dst = ring + (wi % kWalkRing) * kWalkWin;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const unsigned long long w = wi * kWalkWin + 64 * j + lane;
+      __builtin_amdgcn_global_load_lds(fw + (w < nw ? w : nw - 1),
+                                       (__attribute__((address_space(3))) void *)(dst + 64 * j), 4, 0, 0);
+    }
+  }
+  __device__ void start(int lane) {
+    issued = 0;
+    cur = ~0ull;
+    while (issued < nwin && issued < (unsigned long long)kWalkRing) dma(issued++, lane);
+  }
+  // window wi into registers (wi > cur); then keep the ring full
+  __device__ void load(unsigned long long wi, int lane) {
+    // windows issued after wi: every vector-memory op issued since wi's DMA counts too, so this
+    // waits at least for wi (in-order counter)
+    switch ((int)(issued - 1 - wi)) {
+      case 0: wire_vmcnt<0>(); break;
+      case 1: wire_vmcnt<4>(); break;
+      case 2: wire_vmcnt<8>(); break;
+      case 3: wire_vmcnt<12>(); break;
+      case 4: wire_vmcnt<16>(); break;
+      case 5: wire_vmcnt<20>(); break;
+      case 6: wire_vmcnt<24>(); break;
+      default: wire_vmcnt<28>(); break;
+    }
+    const uint32_t *src = ring + (wi % kWalkRing) * kWalkWin + lane;
+    r0 = src[0];
+    r1 = src[64];
+    r2 = src[128];
+    r3 = src[192];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot is read: it may be refilled
+    cur = wi;
+    while (issued < nwin && issued <= wi + kWalkRing) dma(issued++, lane);
+  }
+  __device__ uint32_t get(unsigned long long k, int lane) {
+    const unsigned long long wi = k / kWalkWin;
+    if (wi != cur) load(wi, lane);
+    const int off = (int)(k % kWalkWin), l = off & 63;
+    switch (off >> 6) {
+      case 0: return __builtin_amdgcn_readlane(r0, l);
+      case 1: return __builtin_amdgcn_readlane(r1, l);
+      case 2: return __builtin_amdgcn_readlane(r2, l);
+      default: return __builtin_amdgcn_readlane(r3, l);
+    }
+  }
+  __device__ u64 get64(unsigned long long k, int lane) { return (u64)get(k, lane) | ((u64)get(k + 1, lane) << 32); }
+};
+
+// The batched parse: lane i < cnt parses the VClock at word pos of n records into row dst.
+__device__ __forceinline__ bool walk_parse(const uint32_t *fw, const uint32_t *actors, unsigned long long A,
+                                           int lane, int cnt, unsigned long long pos, unsigned long long n, u64 *dst) {
+  bool miss = false;
+  if (lane < cnt) {
+    const uint32_t *rec = fw + pos + 2;
+    for (unsigned long long r = 0; r < n; r += 4) {
+      uint32_t id[4];
+      u64 c[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {  // all loads of the group in flight before the first lookup
+        const unsigned long long i = r + u < n ? r + u : n - 1;
+        id[u] = rec[3 * i];
+        c[u] = (u64)rec[3 * i + 1] | ((u64)rec[3 * i + 2] << 32);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (r + u < n) {
+          const long long col = find_u32(actors, A, id[u], r + u);
+          if (col < 0) miss = true;
+          else dst[col] = c[u];
+        }
+    }
+  }
+  return miss;
+}
+
+__global__ __launch_bounds__(kBlock) void map_ingest_walk_kernel(MapWirePlan p) {
+  extern __shared__ u64 lds[];
+  const int lane = threadIdx.x % kWave, wib = threadIdx.x / kWave;
+  const int wpb = blockDim.x / kWave;
+  const uint32_t *actors = p.actors, *keys = p.keys;
+  u64 *base = lds;
+  if (p.stage) {  // [actors u32 | keys u32], each padded to 8 bytes
+    uint32_t *la = reinterpret_cast<uint32_t *>(lds);
+    const unsigned long long aw = (p.A + 1) / 2, kw = (p.K + 1) / 2;
+    for (unsigned long long i = threadIdx.x; i < p.A; i += blockDim.x) la[i] = p.actors[i];
+    uint32_t *lk = reinterpret_cast<uint32_t *>(lds + aw);
+    for (unsigned long long i = threadIdx.x; i < p.K; i += blockDim.x) lk[i] = p.keys[i];
+    __syncthreads();
+    actors = la;
+    keys = lk;
+    base = lds + aw + kw;
+  }
+  const unsigned long long per_wave = kWalkRing * kWalkWin / 2 + p.A + p.Kw;  // u64 words
+  u64 *mine = base + (unsigned long long)wib * per_wave;
+  uint32_t *ring = reinterpret_cast<uint32_t *>(mine);
+  u64 *row = mine + kWalkRing * kWalkWin / 2;
+  u64 *bits = row + p.A;
+  for (unsigned long long s = (unsigned long long)blockIdx.x * wpb + wib; s < p.N;
+       s += (unsigned long long)gridDim.x * wpb) {
+    unsigned st = 0;
+    unsigned long long nd = 0;
+    const u64 b = p.frame_off[s], e = p.frame_off[s + 1];
+    if ((b & 3) || (e & 3) || e < b || e - b < 16) {
+      st = kWireBad;  // (a valid frame holds at least the clock and entry counts)
+    } else {
+      MapWalk w;
+      w.fw = reinterpret_cast<const uint32_t *>(p.bytes + b);
+      w.nw = (e - b) / 4;
+      w.nwin = (w.nw + kWalkWin - 1) / kWalkWin;
+      w.ring = ring;
+      w.start(lane);
+      // the batch of VClocks the lanes parse next: lane i holds entry i
+      int cnt = 0;
+      unsigned long long dpos = 0, dn = 0;
+      u64 *ddst = nullptr;
+      bool miss = false;
+      auto push = [&](unsigned long long pos, unsigned long long n, u64 *dst) {
+        if (lane == cnt) {
+          dpos = pos;
+          dn = n;
+          ddst = dst;
+        }
+        if (++cnt == kWave) {
+          miss |= walk_parse(w.fw, actors, p.A, lane, cnt, dpos, dn, ddst);
+          cnt = 0;
+        }
+      };
+      // a VClock's record count at k, checked against the frame (~0: malformed)
+      auto clock_len = [&](unsigned long long k) -> unsigned long long {
+        if (k + 2 > w.nw) return ~0ull;
+        const u64 n = w.get64(k, lane);
+        return n > (w.nw - k - 2) / 3 ? ~0ull : n;
+      };
+      unsigned long long k = 0;
+      unsigned long long n = clock_len(0);
+      if (n == ~0ull) {
+        st |= kWireBad;
+        k = ~0ull;
+      } else {
+        push(0, n, p.clock + s * p.A);
+        k = 2 + 3 * n;
+      }
+      if (k != ~0ull && k + 2 > w.nw) {
+        st |= kWireBad;
+        k = ~0ull;
+      }
+      const u64 ne = k == ~0ull ? 0 : w.get64(k, lane);
+      if (k != ~0ull) k += 2;
+      long long hint = 0;
+      for (u64 en = 0; en < ne && k != ~0ull; ++en) {
+        if (k + 1 > w.nw) {
+          st |= kWireBad;
+          k = ~0ull;
+          break;
+        }
+        const long long ki = find_u32(keys, p.K, w.get(k, lane), (unsigned long long)hint);
+        if (ki < 0) st |= kWireMissing;
+        else hint = ki + 1;
+        n = clock_len(k + 1);
+        if (n == ~0ull) {
+          st |= kWireBad;
+          k = ~0ull;
+          break;
+        }
+        if (ki >= 0) push(k + 1, n, p.ec + (s * p.K + (unsigned long long)ki) * p.A);
+        k += 3 + 3 * n;
+        if (k + 2 > w.nw) {
+          st |= kWireBad;
+          k = ~0ull;
+          break;
+        }
+        const u64 m = w.get64(k, lane);
+        k += 2;
+        for (u64 v = 0; v < m && k != ~0ull; ++v) {
+          n = clock_len(k);
+          if (n == ~0ull || k + 2 + 3 * n + 2 > w.nw) {
+            st |= kWireBad;
+            k = ~0ull;
+            break;
+          }
+          const unsigned long long pos = k;
+          k += 2 + 3 * n;
+          const u64 val = w.get64(k, lane);
+          k += 2;
+          if (ki >= 0) {
+            if (v < p.V) {
+              const unsigned long long slot = (s * p.K + (unsigned long long)ki) * p.V + v;
+              push(pos, n, p.vclk + slot * p.A);
+              if (lane == 0) p.vval[slot] = val;
+            } else {
+              st |= kWireCap;
+            }
+          }
+        }
+      }
+      if (cnt) miss |= walk_parse(w.fw, actors, p.A, lane, cnt, dpos, dn, ddst);
+      if (__ballot(miss)) st |= kWireMissing;
+      // deferred removes: the row-staged parse (rare; global reads)
+      Frame f{w.fw, w.nw};
+      if (k != ~0ull && k + 2 <= f.nw) {
+        const u64 d = w.get64(k, lane);
+        k += 2;
+        for (u64 j = 0; j < d && k != ~0ull; ++j) {
+          k = parse_vclock(f, k, actors, p.A, row, lane, st);
+          for (unsigned long long x = lane; x < p.Kw; x += kWave) bits[x] = 0;
+          wfence();
+          if (k == ~0ull || k + 2 > f.nw) {
+            st |= kWireBad;
+            k = ~0ull;
+            break;
+          }
+          const u64 nk = rd64(f.w, k);
+          k += 2;
+          if (nk > f.nw - k) {
+            st |= kWireBad;
+            k = ~0ull;
+            break;
+          }
+          bool dmiss = false;
+          for (unsigned long long i = lane; i < nk; i += kWave) {
+            const long long kb = find_u32(keys, p.K, f.w[k + i], i);
+            if (kb < 0) dmiss = true;
+            else atomicOr(bits + kb / 64, 1ull << (kb % 64));
+          }
+          if (__ballot(dmiss)) st |= kWireMissing;
+          k += nk;
+          wfence();
+          if (nd < p.Dcap) {
+            store_row<u64>(p.def_clock + (s * p.Dcap + nd) * p.A, row, p.A, lane);
+            store_row<u64>(p.def_keys + (s * p.Dcap + nd) * p.Kw, bits, p.Kw, lane);
+            ++nd;
+          } else {
+            st |= kWireCap;
+          }
+          wfence();
+        }
+      } else {
+        st |= kWireBad;
+        k = ~0ull;
+      }
+      if (k != f.nw) st |= kWireBad;
+      wire_vmcnt<0>();  // no DMA of this frame may land in the ring after the next state starts
+    }
+    if (lane == 0) {
+      p.status[s] = st;
+      p.def_count[s] = (uint32_t)nd;
+    }
+  }
+}
+
 // Egress, count (write = 0: frame sizes) or write pass: clock; present keys ascending with their
 // occupied value slots in slot (Vec) order; the state's deferred slots.
 __global__ __launch_bounds__(kBlock) void map_egress_kernel(MapWirePlan p, int write) {
@@ -1235,6 +1514,23 @@ int crdt_map_ingest(crdt_ctx *ctx, const uint8_t *bytes, const uint64_t *frame_o
   p.bytes = bytes;
   p.frame_off = (const u64 *)frame_off;
   p.status = status;
+  {  // walk + batched parse when a wave's frame ring and rows fit beside the dictionaries
+    const size_t per_wave = kWalkRing * kWalkWin / 2 + p.A + p.Kw;
+    const size_t dw = (p.A + 1) / 2 + (p.K + 1) / 2;
+    int wpb = 4;
+    while (wpb > 1 && (dw + wpb * per_wave) * 8 > 64 * 1024) --wpb;
+    p.stage = (dw + wpb * per_wave) * 8 <= 64 * 1024;
+    if (ctx->tune.wire_walk && ((p.stage ? dw : 0) + wpb * per_wave) * 8 <= 64 * 1024) {
+      if (int rc = device_fill(ctx, p.clock, N * p.A * 8, 0)) return rc;  // the parse writes nonzeros only
+      const size_t lds = ((p.stage ? dw : 0) + wpb * per_wave) * 8;
+      timing_begin(ctx, "wire_ingest");
+      hipLaunchKernelGGL(map_ingest_walk_kernel, dim3(wave_grid(ctx, N, wpb, 32)), dim3(wpb * kWave), lds,
+                         ctx->stream, p);
+      timing_end(ctx);
+      CRDT_HIP(ctx, hipGetLastError());
+      return CRDT_OK;
+    }
+  }
   int wpb = 4;
   while (wpb > 1 && (size_t)wpb * (p.A + p.Kw) * 8 > 64 * 1024) --wpb;
   const size_t dw = (p.A + 1) / 2 + (p.K + 1) / 2;

@@ -648,6 +648,9 @@ impl<M: Member, A: Actor> OrswotDense<M, A> {
     }
 }
 
+/// `lub_many` is the exact left fold for replicas built through the crate's own API (each dot
+/// unique to one replica, entry dots covered by their replica's clock: the invariants under which
+/// the dot-store join is associative, `include/crdt_gpu.h`); `merge_batch` is exact for any pair.
 impl<M: Member, A: Actor> BatchCvRDT for Orswot<M, A> {
     fn lub_many(ctx: &GpuCtx, replicas: Vec<Self>) -> Result<Self, GpuError> {
         if replicas.is_empty() {

@@ -169,6 +169,40 @@ def test_orswot_host_lub_many(hctx):
     assert D > 0 and surv == odef
 
 
+@pytest.mark.parametrize("stage_kb,G,R", [(24, 1, 50), (40, 3, 37), (12, 2, 5), (1 << 18, 1, 50)])
+def test_orswot_host_lub_many_streamed(stage_kb, G, R):
+    """Replica chunks streamed through the stage buffers (running join in slot 0, deferred removes
+    settled once at the end) == the whole-batch staging == the oracle fold, per group; chunk sizes
+    from 1 to all replicas of a group."""
+    M, A = 70, 9
+    rng = np.random.default_rng(stage_kb + G)
+    cs, es, offs, dcls, dmems = [], [], [0], [], []
+    for g in range(G):
+        c, e, off, dcl, dmem = O.gen_orswot(int(rng.integers(1 << 30)), R, M, A, kmax=12, p_def=0.4)
+        cs.append(c)
+        es.append(e)
+        offs.append(offs[-1] + int(off[-1]))
+        dcls.append(dcl)
+        dmems.append(dmem)
+    c, e = np.stack(cs), np.stack(es)
+    dcl, dmem = np.concatenate(dcls), np.concatenate(dmems)
+    res = []
+    for hs in (1, 0):
+        ctx = host.HostContext(0, tune=f"stage_kb={stage_kb},hstream={hs}")
+        res.append(host.orswot_lub_many(c, e, def_off=offs, def_clock=dcl, def_members=dmem, ctx=ctx))
+        ctx.close()
+    for x in ("clock", "entries", "def_keep", "def_members"):
+        np.testing.assert_array_equal(getattr(res[0], x), getattr(res[1], x), err_msg=x)
+    for g in range(G):
+        goff = np.array([0, offs[g + 1] - offs[g]])
+        oc, oe, odef, _ = O.orswot_fold(cs[g], es[g], goff, dcls[g], dmems[g])
+        np.testing.assert_array_equal(res[0].clock[g], oc)
+        np.testing.assert_array_equal(res[0].entries[g], oe)
+        surv = {(tuple(int(x) for x in dcl[d]), O.bitmap_members(res[0].def_members[d]))
+                for d in range(offs[g], offs[g + 1]) if res[0].def_keep[d]}
+        assert surv == odef
+
+
 def test_orswot_host_merge_batch(hctx):
     from orswot_apply_util import dense_states, oracle_streams, replay_streams, to_object
     N, M, n_origins = 30, 40, 4
@@ -207,6 +241,42 @@ def test_map_host_lub_many(hctx):
     np.testing.assert_array_equal(got.vval[0], h(dev.vval))
     np.testing.assert_array_equal(got.def_keep, h(dev.def_keep).astype(np.uint8))
     assert D > 0 and got.ec.any()
+
+
+@pytest.mark.parametrize("stage_kb,vout,src", [(64, 4, "synth"), (24, 2, "replay"), (40, 4, "replay"),
+                                               (1 << 18, 4, "synth"), (16, 8, "synth")])
+def test_map_host_lub_many_streamed(stage_kb, vout, src):
+    """Replica chunks streamed with the running fold as replica 0 (its surviving removes carried)
+    == whole-batch staging, every output word, == the oracle fold; vout 2 (no widening; keys
+    needing more slots restart with 8), 4 (V = 2 inputs widened to 4 slots) and 8."""
+    if src == "synth":
+        dfr = O.synth_map_deferred(0x5EED0045, 200, 40, 8, 30, p_def=0.3)
+        rows, dcl, dks = dfr
+        d = O.synth_map(0x5EED0045, 200, 40, 8, 2, 30, keys=np.arange(40), deferred=dfr)
+    else:
+        maps = O.gen_map_replicas(11 + stage_kb, 60, 12, 5, steps=400, p_rm=0.3, p_up=0.4)
+        d = O.map_to_dense(maps, 12, 5, max(1, O.max_vals(maps)))
+        rows, dcl, dks = d["def_row"], d["def_clock"], d["def_keys"]
+    D = rows.shape[0]
+    res = []
+    for hs in (1, 0):
+        ctx = host.HostContext(0, tune=f"stage_kb={stage_kb},hstream={hs}")
+        res.append(host.map_lub_many(d["clock"], d["ec"], d["vclk"], d["vval"], def_off=[0, D], def_row=rows,
+                                     def_clock=dcl, def_keys=dks, vout=vout, ctx=ctx))
+        ctx.close()
+    for f in res[0]._fields:
+        np.testing.assert_array_equal(getattr(res[0], f), getattr(res[1], f), err_msg=f)
+    exp = O.map_fold(d["clock"], d["ec"], d["vclk"], d["vval"], rows, dcl, dks, vout)
+    if int(res[0].flags[0]) & 1:  # more values than vout on some key: reported alike by both forms
+        assert int(exp[4].max()) > vout
+        return
+    np.testing.assert_array_equal(res[0].clock[0], exp[0])
+    np.testing.assert_array_equal(res[0].ec[0], exp[1])
+    np.testing.assert_array_equal(res[0].vclk[0], exp[2])
+    np.testing.assert_array_equal(res[0].vval[0], exp[3])
+    np.testing.assert_array_equal(res[0].nval[0], exp[4])
+    got = {(tuple(int(x) for x in dcl[j]), O.bitmap_members(res[0].def_keys[j])) for j in np.flatnonzero(res[0].def_keep)}
+    assert got == exp[5]
 
 
 def test_map_host_merge_batch(hctx):

@@ -343,6 +343,14 @@ def test_kat_merges_through_the_wire(gpu_ctx, case):
 
 
 # ---- Map<u32, MVReg<u64>> (BASELINE config 4's type) ---------------------------------------------
+@pytest.fixture(params=[1, 0], ids=["walk", "chain"])
+def mctx(request, gpu_ctx):
+    """Both Map ingest kernels: the walk + batched parse (default) and the per-state dependent chain."""
+    gpu_ctx.tune(f"wwalk={request.param}")
+    yield gpu_ctx
+    gpu_ctx.tune("wwalk=1")
+
+
 def map_wire_form(m, aids, kids):
     """oracle Map over dense actor / key indices -> bc_map arguments over the u32 ids."""
     tr = lambda vc: {int(aids[a]): int(v) for a, v in vc.dots.items() if v}  # noqa: E731
@@ -361,7 +369,7 @@ def map_blob(maps, aids, kids):
 
 
 @pytest.mark.parametrize("A,V", [(5, 3), (64, 2), (70, 2), (5, 5)])
-def test_map_ingest_egress(gpu_ctx, A, V):
+def test_map_ingest_egress(mctx, A, V):
     """A <= 64 with V <= 4 takes the batched egress, the others the generic loop."""
     from test_gpu_merge_batch import arbitrary_maps, map_side
     rng = np.random.default_rng(41 + A + V)
@@ -371,18 +379,18 @@ def test_map_ingest_egress(gpu_ctx, A, V):
     kids, kd = actor_dict(rng, K)  # u32 keys
     blob, off = map_blob(maps, aids, kids)
     Dcap = max(1, max(len(m.deferred) for m in maps))
-    st, status = wire.map_ingest(dev_bytes(blob), dev_off(off), ad, kd, V, Dcap, ctx=gpu_ctx)
+    st, status = wire.map_ingest(dev_bytes(blob), dev_off(off), ad, kd, V, Dcap, ctx=mctx)
     assert (status.cpu().numpy() == 0).all()
     exp = map_side(maps, K, A, V, Dcap)
     for nm in exp._fields:
         np.testing.assert_array_equal(getattr(st, nm).cpu().numpy(), getattr(exp, nm).cpu().numpy(), err_msg=nm)
     assert int(st.def_count.sum()) > 0 and int((st.vclk != 0).any(dim=3).sum()) > 0
-    eoff, edata = wire.map_egress(st, ad, kd, ctx=gpu_ctx)
+    eoff, edata = wire.map_egress(st, ad, kd, ctx=mctx)
     assert eoff.cpu().tolist() == off
     assert bytes(edata.cpu().numpy().tobytes()) == blob  # canonical frames round-trip byte for byte
 
 
-def test_map_merge_batch_through_bytes(gpu_ctx):
+def test_map_merge_batch_through_bytes(mctx):
     """Serialized pairs -> ingest -> merge_batch -> egress -> decode == the oracle's Map::merge."""
     from test_gpu_merge_batch import replay_maps
     rng = np.random.default_rng(42)
@@ -400,12 +408,12 @@ def test_map_merge_batch_through_bytes(gpu_ctx):
     Dcap = max(1, max(len(m.deferred) for m in list(lhs) + list(rhs) + exp))
     b1, o1 = map_blob(lhs, aids, kids)
     b2, o2 = map_blob(rhs, aids, kids)
-    s1, st1 = wire.map_ingest(dev_bytes(b1), dev_off(o1), ad, kd, V, Dcap, ctx=gpu_ctx)
-    s2, st2 = wire.map_ingest(dev_bytes(b2), dev_off(o2), ad, kd, V, Dcap, ctx=gpu_ctx)
+    s1, st1 = wire.map_ingest(dev_bytes(b1), dev_off(o1), ad, kd, V, Dcap, ctx=mctx)
+    s2, st2 = wire.map_ingest(dev_bytes(b2), dev_off(o2), ad, kd, V, Dcap, ctx=mctx)
     assert (st1.cpu().numpy() == 0).all() and (st2.cpu().numpy() == 0).all()
-    status = cg.map.merge_batch(s1, s2, ctx=gpu_ctx).cpu().numpy()
+    status = cg.map.merge_batch(s1, s2, ctx=mctx).cpu().numpy()
     assert (status == 0).all(), status
-    eoff, edata = wire.map_egress(s1, ad, kd, ctx=gpu_ctx)
+    eoff, edata = wire.map_egress(s1, ad, kd, ctx=mctx)
     for i, fr in enumerate(host_frames(edata, eoff)):
         c, e, d, pos = O.unbc_map(fr)
         assert pos == len(fr)
@@ -413,7 +421,7 @@ def test_map_merge_batch_through_bytes(gpu_ctx):
     assert sum(len(x.entries) for x in exp) > 0 and sum(len(x.deferred) for x in exp) > 0
 
 
-def test_map_malformed_missing_and_capacity(gpu_ctx):
+def test_map_malformed_missing_and_capacity(mctx):
     rng = np.random.default_rng(43)
     K, A = 4, 3
     aids, ad = actor_dict(rng, A)
@@ -426,7 +434,7 @@ def test_map_malformed_missing_and_capacity(gpu_ctx):
                           [])
     blobs = [good, good[:-4], good + b"\0\0\0\0", missing_key, three_vals]
     blob, off = O.frames(blobs)
-    st, status = wire.map_ingest(dev_bytes(blob), dev_off(off), ad, kd, 2, 1, ctx=gpu_ctx)
+    st, status = wire.map_ingest(dev_bytes(blob), dev_off(off), ad, kd, 2, 1, ctx=mctx)
     s = status.cpu().numpy().tolist()
     assert s[0] == 0
     assert s[1] & wire.BAD and s[2] & wire.BAD
@@ -435,13 +443,16 @@ def test_map_malformed_missing_and_capacity(gpu_ctx):
     assert to_host(st.vval)[4, 0].tolist() == [1, 2]
 
 
-def test_map_ingest_large_frames():
+@pytest.mark.parametrize("walk", [1, 0])
+def test_map_ingest_large_frames(walk):
     """Config-4-shaped frames (1,024 keys x 32 actors, ~80 KiB each): synthetic states -> egress ->
     ingest is the identity; truncated / extended copies of large frames are reported as malformed
-    and leave the other states' rows exact."""
+    and leave the other states' rows exact.  Both ingest kernels (walk: the frame streams through
+    the LDS ring in 1-KiB windows; chain)."""
     from crdts_gpu import synth
     torch.cuda.set_device(0)
     ctx = cg.Context(0)
+    ctx.tune(f"wwalk={walk}")
     dev = "cuda"
     R, K, A, V = 24, 1024, 32, 2
     inp = synth.map_replicas(ctx, R, K, A, V, 0x5EED0004, kmax=256, p_def=0.3)
