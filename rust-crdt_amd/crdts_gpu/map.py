@@ -72,7 +72,7 @@ def lub_many(clock: torch.Tensor, ec: torch.Tensor, vclk: torch.Tensor, vval: to
     # per-replica blocks must be packed (strides only on the replica and group axes)
     for t, nm, inner in ((c, "clock", (1,)), (e, "ec", (A, 1)), (vc, "vclk", (V * A, A, 1)),
                          (vv, "vval", (V, 1))):
-        if tuple(t.stride()[2:]) != inner:
+        if t.numel() and tuple(t.stride()[2:]) != inner:  # (an empty key shard: nothing is read)
             raise ValueError(f"map.lub_many: {nm} must be packed within a replica")
     Kw = (K + 63) // 64 if _key_shard is None else (int(_key_shard[1]) + 63) // 64
     dev = clock.device

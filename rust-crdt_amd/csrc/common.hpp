@@ -63,6 +63,8 @@ struct Tune {
   int map_scan2 = 0;   // ... scan two actors per 16-byte LDS read (even A; measured no faster)
   int map_scan3 = 1;   // ... scan from per-actor thresholds with every LDS read issued first
   int map_rs = 1;      // ... register-staged whole-chunk skip (A <= 32 on the LDS-DMA shapes)
+  int map_lazyv = 1;   // ... RS path: values fetched only for chunks the exact loop runs (not streamed)
+  int map_diag = 0;    // ... timing probes only, results WRONG (bit0: no clock-max piece, bit1: 3 fewer step pieces)
   int rows_blocks_per_cu = 0;  // row-pair / row-reduction kernels (causal.hip); 0 = per-kernel default
   int apply_hot_slots = 8;     // Orswot apply: deferred slots kept in LDS per state (the rest in HBM)
   int map_apply_hot = 1 << 20;  // Map apply: cap on the deferred slots kept in LDS (default: all that fit)
@@ -72,6 +74,7 @@ struct Tune {
   int stage_kb = 262144;       // CRDT_MEM_HOST: bytes per device chunk buffer (KiB; two buffers)
   int wire_walk = 1;           // Map ingest: walk + batched parse (0: one dependent chain per state)
   int host_stream = 1;         // CRDT_MEM_HOST Orswot / Map lub_many: stream replica chunks (0: stage whole)
+  int apply_fence = 0;         // Orswot / Map apply: a workgroup fence after every op's stores (round-2 form)
 };
 
 struct PendingTiming {

@@ -211,8 +211,11 @@ static void apply_tune(crdt_ctx *ctx, const char *t) {
       else if (k == "mscan2") ctx->tune.map_scan2 = v != 0;
       else if (k == "mscan3") ctx->tune.map_scan3 = v != 0;
       else if (k == "mrs") ctx->tune.map_rs = v != 0;
+      else if (k == "mlazyv") ctx->tune.map_lazyv = v != 0;
+      else if (k == "mdiag" && v >= 0) ctx->tune.map_diag = v;
       else if (k == "wwalk") ctx->tune.wire_walk = v != 0;
       else if (k == "hstream") ctx->tune.host_stream = v != 0;
+      else if (k == "afence") ctx->tune.apply_fence = v != 0;
       else if (k == "rbpc" && v > 0) ctx->tune.rows_blocks_per_cu = v;
       else if (k == "hot" && v >= 0 && v <= 64) ctx->tune.apply_hot_slots = v;
       else if (k == "mhot" && v >= 0) ctx->tune.map_apply_hot = v;

@@ -456,9 +456,11 @@ static int orswot_lub_host_stream(crdt_ctx *ctx, const crdt_orswot_batch *in, cr
   if (out->def_keep && (int)ds.get(ctx, D, &ok)) return CRDT_ENOMEM;
   if (out->def_members && (int)ds.get(ctx, D * Mw, &om)) return CRDT_ENOMEM;
   const size_t nch = (R + Rc - 1) / Rc;
+  const bool trace = getenv("CRDT_STAGE_TRACE") != nullptr;  // (diagnosis: one stderr line per step)
   for (size_t k = 0; k < nch; ++k) {
     const int b = (int)(k & 1);
     uint64_t *bc = static_cast<uint64_t *>(ctx->hbuf[b]), *be = bc + cwords;
+    if (trace) fprintf(stderr, "orswot stream: chunk %zu/%zu Rc %zu S %zu\n", k, nch, Rc, S);
     const size_t r0 = k * Rc, n = std::min(Rc, R - r0);
     if (int rc = begin_chunk(ctx, b)) return rc;
     for (size_t g = 0; g < G; ++g) {  // replicas r0 .. r0+n of group g behind its slot 0
@@ -490,7 +492,13 @@ static int orswot_lub_host_stream(crdt_ctx *ctx, const crdt_orswot_batch *in, cr
       if (int rc = crdt_orswot_lub_many(ctx, &cb, &co)) return rc;
     }
     if (int rc = end_chunk(ctx, b)) return rc;
+    if (trace) {
+      fprintf(stderr, "orswot stream: chunk %zu queued, syncing\n", k);
+      if (int rc = finish(ctx, CRDT_OK)) return rc;
+      fprintf(stderr, "orswot stream: chunk %zu done\n", k);
+    }
   }
+  if (trace) fprintf(stderr, "orswot stream: settling %zu deferred\n", D);
   // the deferred removes, settled once against the final join
   if (int rc = h2d_async(ctx, dc, in->def_clock, D * A * 8)) return rc;
   if (int rc = h2d_async(ctx, dm, in->def_members, D * Mw * 8)) return rc;

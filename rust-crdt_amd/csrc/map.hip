@@ -61,6 +61,8 @@ struct MapPlan {
   // its clocks with one compare (the acc clock only ever takes maxima of replica clocks, map.rs:217)
   const u64 *cmax;
   unsigned long long nch;
+  int lazyv;  // RS path: the values of a chunk fetched only when the exact loop runs it
+  int diag;   // timing probes (results wrong): bit0 no clock-max piece, bit1 3 fewer step pieces
 };
 
 constexpr int kMapQ = 4;    // deferred removes tracked per key in registers before the slow path
@@ -309,7 +311,8 @@ __device__ __forceinline__ GldsLanes<NI> glds_lanes(const MapPlan &p, unsigned l
 template <int VI, int C, int NI, int AUX = 0>
 __device__ __forceinline__ void map_chunk_glds(const MapPlan &p, const GldsLanes<NI> &L, unsigned long long g,
                                                unsigned long long k, unsigned long long i0, unsigned long long iend,
-                                               u64 *img, unsigned long long WS, u64 *vals, u64 *cm, int lane) {
+                                               u64 *img, unsigned long long WS, u64 *vals, u64 *cm, int lane,
+                                               bool vpiece = true, int diag = 0) {
   if (i0 + C <= iend) {  // a whole chunk (uniform)
     const char *src[NI];
 #pragma unroll
@@ -319,7 +322,7 @@ __device__ __forceinline__ void map_chunk_glds(const MapPlan &p, const GldsLanes
       for (int s = 0; s < C; ++s)
 #pragma unroll
         for (int j = 0; j < NI; ++j) {
-          glds16<AUX>(src[j], img + s * WS + j * 128);
+          if (!(diag & 2) || s < C - 3) glds16<AUX>(src[j], img + s * WS + j * 128);
           src[j] += L.stride[j];
         }
     } else {
@@ -341,14 +344,17 @@ __device__ __forceinline__ void map_chunk_glds(const MapPlan &p, const GldsLanes
     }
   }
   const int sv = lane / (2 * VI), dw = lane % (2 * VI);
-  if (sv < C) {
-    const unsigned long long i = i0 + sv < iend ? i0 + sv : iend - 1;
-    const unsigned *src = reinterpret_cast<const unsigned *>(p.vval + g * p.vv_gs + i * p.vv_rs + k * VI) + dw;
-    glds4<AUX>(src, vals);
+  if (vpiece) {  // (uniform)
+    if (sv < C) {
+      const unsigned long long i = i0 + sv < iend ? i0 + sv : iend - 1;
+      const unsigned *src = reinterpret_cast<const unsigned *>(p.vval + g * p.vv_gs + i * p.vv_rs + k * VI) + dw;
+      glds4<AUX>(src, vals);
+    }
   }
   // the chunk's clock max: one more piece (lanes 0 .. A/2-1, A even)
-  if ((unsigned long long)(2 * lane) < p.A)
-    glds16(p.cmax + (g * p.nch + i0 / C) * p.A + 2 * lane, cm);
+  if (!(diag & 1))
+    if ((unsigned long long)(2 * lane) < p.A)
+      glds16(p.cmax + (g * p.nch + i0 / C) * p.A + 2 * lane, cm);
 }
 
 // Wait until at most N vector-memory ops are outstanding (counts above the 6-bit field clamp
@@ -852,7 +858,7 @@ __device__ __forceinline__ u64 rs_lds_own_noop(const RsChunk<VI, NP> &r, const u
 
 template <int VI, int NP>
 __device__ __forceinline__ void rs_reload(RsChunk<VI, NP> &r, const u64 *img, unsigned long long WS, const u64 *vals,
-                                          const u64 *cm, unsigned long long A, int lane) {
+                                          const u64 *cm, unsigned long long A, int lane, bool vload = true) {
   const unsigned s = (unsigned)lane >> 2, gq = (unsigned)lane & 3;
   const u64 *st = img + s * WS;
 #pragma unroll
@@ -870,8 +876,10 @@ __device__ __forceinline__ void rs_reload(RsChunk<VI, NP> &r, const u64 *img, un
     const unsigned a0 = 2 * gq + 8 * m;
     r.cmp[m] = lds2(cm + (a0 < A ? a0 : A - 2));
   }
+  if (vload) {
 #pragma unroll
-  for (int t = 0; t < VI; ++t) r.v[t] = vals[s * VI + t];
+    for (int t = 0; t < VI; ++t) r.v[t] = vals[s * VI + t];
+  }
 }
 
 // The verdict from the register-held operands: TB = max(e, min(Cs, m1)) computed here.
@@ -923,14 +931,18 @@ struct RsDma {
   const u64 *csrc;
   u64 *cm;
   bool con;
+  bool vp;   // the values piece streamed (uniform; off: fetched for exact chunks only)
+  int diag;  // MapPlan::diag timing probes
   __device__ __forceinline__ void operator()(int j) {
     if (j < 16) {
-      glds16(src, img + j * WS);
+      if (!(diag & 2) || j < 13) glds16(src, img + j * WS);
       src += stride;
     } else if (j == 16) {
-      if (von) glds4(vsrc, vals);
+      if (vp)
+        if (von) glds4(vsrc, vals);
     } else {
-      if (con) glds16(csrc, cm);
+      if (!(diag & 1))
+        if (con) glds16(csrc, cm);
     }
   }
 };
@@ -964,7 +976,7 @@ __device__ __forceinline__ u64 rs_lds_noop_nv(const u64 *img, unsigned long long
 // in the layout the exact loop reads (map_step_read, the LDS scans, cml).
 template <int VI, int NP>
 __device__ __forceinline__ void rs_store(const RsChunk<VI, NP> &r, u64 *img, unsigned long long WS, u64 *vals,
-                                         u64 *cm, unsigned long long A, int lane) {
+                                         u64 *cm, unsigned long long A, int lane, bool vstore = true) {
   const unsigned s = (unsigned)lane >> 2, gq = (unsigned)lane & 3;
   u64 *st = img + s * WS;
 #pragma unroll
@@ -977,7 +989,7 @@ __device__ __forceinline__ void rs_store(const RsChunk<VI, NP> &r, u64 *img, uns
     *reinterpret_cast<u64x2 *>(st + (1 + VI) * A + a) = r.co[m];
   }
   if ((unsigned long long)lane < A) cm[lane] = r.cm;
-  if (gq == 0)
+  if (vstore && gq == 0)
 #pragma unroll
     for (int t = 0; t < VI; ++t) vals[s * VI + t] = r.v[t];
 }
@@ -1123,10 +1135,12 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
   const int ni = GL ? (int)((W + 127) / 128) : 0;  // 1-KiB pieces per step image (GL: 1 or 2)
   GldsLanes<1> gl1;
   GldsLanes<2> gl2;
+  const bool vpiece = !(RS && p.lazyv);
   if constexpr (RS) {  // chunks 0 and 1 into the two slots (W <= 128: one piece per step)
     gl1 = glds_lanes<VI, 1>(p, g, k, lane);
     for (unsigned long long c = 0; c < 2 && c < nch; ++c)
-      map_chunk_glds<VI, C, 1>(p, gl1, g, k, c * C, R, map_lds + c * C * WS, WS, vbase + c * C * VI, cml + c * A, lane);
+      map_chunk_glds<VI, C, 1>(p, gl1, g, k, c * C, R, map_lds + c * C * WS, WS, vbase + c * C * VI, cml + c * A, lane,
+                               vpiece, p.diag);
   }
   if constexpr (GL) {
     if (ni == 1) gl1 = glds_lanes<VI, 1>(p, g, k, lane);
@@ -1167,16 +1181,21 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
       u64 *const vsl = vbase + slot * C * VI;
       u64 *const cms = cml + slot * A;
       MAP_TICK();
-      if (ch + 1 < nch) wait_vmcnt<P1>();
-      else wait_vmcnt<0>();
+      if (ch + 1 < nch) {
+        if (vpiece) wait_vmcnt<P1>();
+        else wait_vmcnt<P1 - 1>();  // (no values piece)
+      } else {
+        wait_vmcnt<0>();
+      }
       MAP_TOCK(cy_wait);
       MAP_TICK();
-      rs_reload(rA, img, WS, vsl, cms, A, lane);
+      rs_reload(rA, img, WS, vsl, cms, A, lane, vpiece);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot is read: refill it
       // a whole next chunk with every lane moving a piece: its pieces go out during the test
       const unsigned long long i2 = (ch + 2) * C;
       const bool spread = el && ch + 2 < nch && i2 + C <= R && (2 + VI) * A == 128;
-      if (ch + 2 < nch && !spread) map_chunk_glds<VI, C, 1>(p, gl1, g, k, i2, R, img, WS, vsl, cms, lane);
+      if (ch + 2 < nch && !spread)
+        map_chunk_glds<VI, C, 1>(p, gl1, g, k, i2, R, img, WS, vsl, cms, lane, vpiece, p.diag);
       MAP_TOCK(cy_issue);
       MAP_TICK();
       bool skip = false;
@@ -1184,7 +1203,8 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
         const int sv = lane / (2 * VI), dw = lane % (2 * VI);
         RsDma d{gl1.src0[0] + i2 * gl1.stride[0], gl1.stride[0], img, WS,
                 reinterpret_cast<const unsigned *>(p.vval + g * p.vv_gs + (i2 + (sv < C ? sv : 0)) * p.vv_rs + k * VI) + dw,
-                vsl, sv < C, p.cmax + (g * p.nch + i2 / C) * A + 2 * lane, cms, (unsigned long long)(2 * lane) < A};
+                vsl, sv < C, p.cmax + (g * p.nch + i2 / C) * A + 2 * lane, cms, (unsigned long long)(2 * lane) < A,
+                vpiece, p.diag};
         skip = (rs_reg_noop_nv<VI, NP>(rA, rg, present, nv, d) & want) == want;
       } else if (el) {
         skip = (rs_reg_noop_nv<VI, NP>(rA, rg, present, nv) & want) == want;
@@ -1203,7 +1223,11 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
         continue;
       }
       wait_vmcnt<0>();
-      rs_store(rA, img, WS, vsl, cms, A, lane);
+      rs_store(rA, img, WS, vsl, cms, A, lane, vpiece);
+      if (!vpiece && lane < C * VI) {  // the chunk's values, fetched now (a chunk the exact loop runs)
+        const unsigned long long iv = ch * C + lane / VI;
+        vsl[lane] = p.vval[g * p.vv_gs + (iv < R ? iv : R - 1) * p.vv_rs + k * VI + lane % VI];
+      }
       // the exact loop's scans read max(e, Cs) and TB from LDS
       if ((unsigned long long)lane < A) {
         mirror[(1 + VO) * A + lane] = e[0] > cs[0] ? e[0] : cs[0];
@@ -1560,7 +1584,7 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
       if (ch + 2 < nch) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         map_chunk_glds<VI, C, 1>(p, gl1, g, k, (ch + 2) * C, R, map_lds + slot * C * WS, WS, vbase + slot * C * VI,
-                                 cml + slot * A, lane);
+                                 cml + slot * A, lane, vpiece, p.diag);
       }
     }
     if constexpr (!GL && !RS) {
@@ -1778,6 +1802,8 @@ extern "C" int crdt_map_lub_many(crdt_ctx *ctx, const crdt_map_batch *in, crdt_m
   p.nt = ctx->tune.map_nt;
   p.scan2 = ctx->tune.map_scan2 && A % 2 == 0;
   p.scan3 = ctx->tune.map_scan3;
+  p.lazyv = ctx->tune.map_lazyv;
+  p.diag = ctx->tune.map_diag;
   if (int rc = device_fill(ctx, out->flags, G * sizeof(unsigned), 0)) return rc;
   // LDS-DMA staging when every step image is whole 16-byte pieces (A even, 16-byte aligned
   // rows and strides) and the state fits 4 values; register staging otherwise

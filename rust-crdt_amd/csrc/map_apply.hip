@@ -52,6 +52,7 @@ struct MapApplyPlan {
   uint32_t *status;
   int wpb;
   unsigned long long Dh;  // deferred slots kept in LDS (the rest in the state's own HBM slots)
+  int fence;              // 1: a workgroup fence after each op's stores (CRDT_TUNE afence=1, the round-2 form)
 };
 
 // W clock words per lane: 1 for A <= 64 (fewer VGPRs, more waves per SIMD), 2 to A = 128, 4 to 256
@@ -298,21 +299,21 @@ __device__ __forceinline__ void map_apply_body(const MapApplyPlan &p) {
                   st |= 16u;  // more values than slots: the state is incomplete
                   slot = -1;
                 } else {  // compact the used slots in order, then append
-                  wave_fence_m();
+                  if (p.fence) wave_fence_m();
                   int w = 0;
                   for (unsigned long long j = 0; j < p.V; ++j) {
                     const RowT<W> v = load_row<W>(q.vc + j * A, lane, A);
                     if (!any_nz(v)) continue;
                     if ((unsigned long long)w != j) {
                       const u64 x = q.vv[j];
-                      wave_fence_m();
+                      if (p.fence) wave_fence_m();
                       store_row(q.vc + (unsigned long long)w * A, v, lane, A);
                       store_row(q.vc + j * A, zero_row<W>(), lane, A);
                       if (lane == 0) {
                         q.vv[w] = x;
                         q.vv[j] = 0;
                       }
-                      wave_fence_m();
+                      if (p.fence) wave_fence_m();
                     }
                     ++w;
                   }
@@ -335,7 +336,7 @@ __device__ __forceinline__ void map_apply_body(const MapApplyPlan &p) {
 #pragma unroll
           for (int j = 0; j < W; ++j)
             if (j == ja && lane == la) C.w[j] = kc;  // self.clock.apply(dot) (:133)
-          wave_fence_m();
+          if (p.fence) wave_fence_m();
           unsigned nk = 0;  // apply_deferred (:134, :311-316)
           for (unsigned d = 0; d < dcnt; ++d) {
             const RowT<W> rm = load_row<W>(SC(d), lane, A);
@@ -344,7 +345,7 @@ __device__ __forceinline__ void map_apply_body(const MapApplyPlan &p) {
             } else if ((rl64m(SK(d)[k / 64], 0) >> (k % 64)) & 1ull) {
               key_rm(p, s, k, rm, lane);  // only key k changed since the last full pass
             }
-            wave_fence_m();
+            if (p.fence) wave_fence_m();
             if (any_gt(rm, C)) {
               if (nk != d) {
                 u64 *dc = SC(nk), *dk = SK(nk);
@@ -357,7 +358,7 @@ __device__ __forceinline__ void map_apply_body(const MapApplyPlan &p) {
           }
           dcnt = nk;
           full = false;
-          wave_fence_m();
+          if (p.fence) wave_fence_m();
         } else {  // ---- Op::Rm -> apply_keyset_rm (:318-348)
           const u64 kb = rl64m(h_kb, i), ke = rl64m(h_ke, i);
           if (ke < kb || ke > p.n_keys) {  // reversed, or runs past the keys buffer
@@ -374,7 +375,7 @@ __device__ __forceinline__ void map_apply_body(const MapApplyPlan &p) {
                 continue;
               }
               key_rm(p, s, k, oc, lane);
-              wave_fence_m();
+              if (p.fence) wave_fence_m();
             }
           }
           if (!any_gt(oc, C)) continue;  // rm <= clock: not deferred (:336-345)
@@ -393,7 +394,7 @@ __device__ __forceinline__ void map_apply_body(const MapApplyPlan &p) {
             store_row(SC((unsigned long long)slot), oc, lane, A);
             u64 *nb = SK((unsigned long long)slot);
             for (unsigned long long t = lane; t < p.Kw; t += kWave) nb[t] = 0;
-            wave_fence_m();
+            if (p.fence) wave_fence_m();
           }
           u64 *bits = SK((unsigned long long)slot);
           if (!SP || (unsigned long long)slot < p.Dh) {  // LDS: lanes OR their keys in at once
@@ -409,11 +410,11 @@ __device__ __forceinline__ void map_apply_body(const MapApplyPlan &p) {
               for (int t = 0; t < n; ++t) {
                 const unsigned long long k = (unsigned)__builtin_amdgcn_readlane((int)kk, t);
                 if (k < p.K && lane == 0) bits[k / 64] |= 1ull << (k % 64);
-                wave_fence_m();
+                if (p.fence) wave_fence_m();
               }
             }
           }
-          wave_fence_m();
+          if (p.fence) wave_fence_m();
         }
       }
     }
@@ -479,7 +480,8 @@ extern "C" int crdt_map_apply_batch(crdt_ctx *ctx, const crdt_map_states *m, uin
                  (u64 *)m->vval, m->vval_stride, (u64 *)def_clock, (u64 *)def_keys, def_count, N, K, A, V, Kw, Dcap,
                  (const u64 *)ops->op_off, ops->kind, ops->actor, (const u64 *)ops->counter, ops->key,
                  (const u64 *)ops->val, ops->clk_row, (const u64 *)ops->clk_pool, ops->n_clk_rows,
-                 (const u64 *)ops->key_off, ops->keys, ops->keys ? ops->n_keys : 0, ops->n_ops, status, wpb, Dh};
+                 (const u64 *)ops->key_off, ops->keys, ops->keys ? ops->n_keys : 0, ops->n_ops, status, wpb, Dh,
+                 ctx->tune.apply_fence};
   const unsigned long long want = (N + wpb - 1) / wpb;
   const unsigned long long cap = (unsigned long long)ctx->cu_count * 64;
   timing_begin(ctx, "map_apply");

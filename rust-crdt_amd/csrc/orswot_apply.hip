@@ -51,6 +51,7 @@ struct OrswotApplyPlan {
   unsigned long long n_ops;
   uint32_t *status;
   int wpb;
+  int fence;  // 1: a workgroup fence after every op's stores (CRDT_TUNE afence=1, the round-2 form)
 };
 
 __device__ __forceinline__ u64 rl64(u64 x, int l) {
@@ -185,9 +186,32 @@ __device__ __forceinline__ void orswot_apply_body(const OrswotApplyPlan &p) {
         }
       }
       const int nb = (int)((oe - base) < (unsigned long long)kWave ? (oe - base) : kWave);
+      // The cell of the NEXT op when it is a one-member Add is loaded (lane 0) while this op runs,
+      // so its read is not one more dependent round trip.  It is dropped (the op then loads its
+      // cell itself) when this op may write that member's row: a write to the same member (an Add's
+      // cell or its restricted re-forget, a one-member Rm), or to rows not tracked here (several
+      // members, a full apply_deferred pass).  A wave's later loads see its earlier stores (all
+      // lanes of a wave go through one L1 in program order), so the prefetch after them is exact.
+      bool pf_have = false;
+      unsigned long long pf_m = 0;
+      u64 pf_val = 0;
       for (int i = 0; i < nb; ++i) {
         const unsigned ka = rl32(h_ka, i);
         const u64 mb = rl32(h_mb, i), me = rl32(h_me, i);
+        const bool pf_use = pf_have;  // the prefetch made for this op is still valid
+        const u64 pf_cur = pf_val;
+        pf_have = false;
+        if (i + 1 < nb) {
+          const unsigned ka1 = rl32(h_ka, i + 1);
+          if (ka1 != kBadOp && ka1 != kRmOp && rl32(h_me, i + 1) - rl32(h_mb, i + 1) == 1) {
+            const unsigned long long m1 = rl32(h_m0, i + 1);
+            if (m1 < p.M) {
+              if (lane == 0) pf_val = E[m1 * p.entry_mstride + ka1];
+              pf_have = true;
+              pf_m = m1;
+            }
+          }
+        }
         if (ka == kBadOp) {
           st |= 2u;
           continue;
@@ -206,11 +230,16 @@ __device__ __forceinline__ void orswot_apply_body(const OrswotApplyPlan &p) {
             const unsigned long long m = rl32(h_m0, i);
             if (m >= p.M) {
               bad = true;
-            } else if (lane == 0) {
-              u64 *cell = E + m * p.entry_mstride + a;
-              if (*cell < k) *cell = k;
+            } else {
+              if (m == pf_m) pf_have = false;  // this op writes the next op's row
+              if (lane == 0) {
+                u64 *cell = E + m * p.entry_mstride + a;
+                const u64 old = pf_use ? pf_cur : *cell;
+                if (old < k) *cell = k;
+              }
             }
           } else {
+            pf_have = false;
             for (u64 jm = mb + lane; jm < me; jm += kWave) {
               const unsigned long long m = p.mem[jm];
               if (m >= p.M) {
@@ -225,8 +254,9 @@ __device__ __forceinline__ void orswot_apply_body(const OrswotApplyPlan &p) {
 #pragma unroll
           for (int j = 0; j < kCA; ++j)
             if (j == ja && lane == la) c[j] = k;
-          wave_fence();
+          if (p.fence) wave_fence();
           // apply_deferred (:281-286)
+          if (full || me - mb != 1) pf_have = false;  // rows of every slot's members may change
           unsigned nk = 0;
           for (unsigned d = 0; d < dcnt; ++d) {
             u64 r[kCA];
@@ -253,7 +283,7 @@ __device__ __forceinline__ void orswot_apply_body(const OrswotApplyPlan &p) {
           }
           dcnt = nk;
           full = false;
-          wave_fence();
+          if (p.fence) wave_fence();
         } else {  // ---- Op::Rm -> apply_rm (:230-250)
           const unsigned rr = (unsigned)rl64(h_cr, i);
           if (rr >= p.n_rm_rows) {
@@ -271,7 +301,9 @@ __device__ __forceinline__ void orswot_apply_body(const OrswotApplyPlan &p) {
             const unsigned long long m = rl32(h_m0, i);
             if (m >= p.M) st |= 2u;
             else forget_row(E + m * p.entry_mstride, r, lane, A);
+            if (m == pf_m) pf_have = false;
           } else {
+            pf_have = false;
             for (u64 jb = mb; jb < me; jb += kWave) {
               const unsigned mm = jb + lane < me ? p.mem[jb + lane] : 0u;
               const int n = (int)((me - jb) < (u64)kWave ? (me - jb) : kWave);
@@ -285,7 +317,7 @@ __device__ __forceinline__ void orswot_apply_body(const OrswotApplyPlan &p) {
               }
             }
           }
-          wave_fence();
+          if (p.fence) wave_fence();
           if (!any_greater(r, c, lane, A)) continue;  // rm <= C: already seen (:239-249)
           int slot = -1;
           for (unsigned d = 0; d < dcnt; ++d) {
@@ -400,7 +432,7 @@ extern "C" int crdt_orswot_apply_batch(crdt_ctx *ctx, const crdt_orswot_states *
                     (u64 *)s.def_clock, (u64 *)s.def_members, s.def_count, s.N, s.M, s.A, Mw, s.Dcap, Dh,
                     (const u64 *)ops->op_off, ops->kind, ops->actor, (const u64 *)ops->counter, ops->rm_row,
                     (const u64 *)ops->rm_clock, ops->rm_clock ? ops->n_rm_rows : 0, (const u64 *)ops->mem_off,
-                    ops->mem, ops->mem ? ops->n_mem : 0, ops->n_ops, status, wpb};
+                    ops->mem, ops->mem ? ops->n_mem : 0, ops->n_ops, status, wpb, ctx->tune.apply_fence};
   const unsigned long long want = (s.N + wpb - 1) / wpb;
   const unsigned long long cap = (unsigned long long)ctx->cu_count * 64;
   timing_begin(ctx, "orswot_apply");

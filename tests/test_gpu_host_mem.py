@@ -145,7 +145,8 @@ def test_host_mode_refusals(hctx):
     assert hctx.raw("crdt_map_lub_many", None, None) == cg._abi.CRDT_EINVAL  # host-capable too
     assert hctx.raw("crdt_map_apply_batch", None, None, None, None, 0, None, None) == -4
     assert hctx.raw("crdt_vclock_ingest", None, None, 0, None, 0, None, 0, None) == -4
-    assert hctx.raw("crdt_vclock_lub_many_sharded", None, 0, 0, 0, 0, 0, None) == -4
+    # (sharded entry points check for a communicator first: none on this ctx)
+    assert hctx.raw("crdt_vclock_lub_many_sharded", None, 0, 0, 0, 0, 0, None) == cg._abi.CRDT_EINVAL
     assert hctx.lib.crdt_ctx_mem_kind(hctx.ptr) == cg._abi.CRDT_MEM_HOST
     # device mode is unaffected on another ctx
     ctx = cg.Context(0)

@@ -103,13 +103,15 @@ def test_kat_mvreg_on_gpu(gpu_ctx, case, mode):
 
 
 # ---- random registers vs the oracle ---------------------------------------------------------------
-def rand_regs(rng, n, A, nact, vmax, steps=6):
+def rand_regs(rng, n, A, nact, vmax, steps=6, group=None):
     """Registers built by random Puts whose clocks advance random actors (so values are concurrent,
-    dominated or equal as the history goes)."""
+    dominated or equal as the history goes). With `group`, every run of `group` registers shares one
+    advancing causal history, so a group's fold keeps a bounded number of concurrent values."""
     regs = []
-    for _ in range(n):
+    for i in range(n):
         r = O.MVReg()
-        base = O.VClock()
+        if group is None or i % group == 0:
+            base = O.VClock()
         for _ in range(rng.integers(0, steps + 1)):
             c = base.copy()
             for a in rng.choice(nact, size=rng.integers(1, 3), replace=False):
@@ -127,17 +129,21 @@ def rand_regs(rng, n, A, nact, vmax, steps=6):
 def test_mvreg_lub_many_vs_oracle(gpu_ctx, A):
     rng = np.random.default_rng(A)
     G, R, V = 7, 40, 4
-    regs = rand_regs(rng, G * R, A, min(A, 8), V)
+    regs = rand_regs(rng, G * R, A, min(A, 8), V, group=13)
     actors = intern.Index(list(range(A)))
     vals = intern.Index()
     vc, vv = dense_regs(regs, actors, V, vals)
-    res = cg.mvreg.lub_many(to_dev(vc.reshape(G, R, V, A)), to_dev(vv.reshape(G, R, V)), vout=16)
-    got = obj_regs(to_host(res.vclk), to_host(res.vval), actors, vals, res.nval.cpu().numpy())
+    folds = []
     for g in range(G):
         acc = O.MVReg()
         for r in regs[g * R:(g + 1) * R]:
             acc.merge(r)
-        assert got[g].vals == acc.vals  # same values in the same Vec order
+        folds.append(acc)
+    assert max(len(f.vals) for f in folds) <= 16  # the generator keeps every fold within vout
+    res = cg.mvreg.lub_many(to_dev(vc.reshape(G, R, V, A)), to_dev(vv.reshape(G, R, V)), vout=16)
+    got = obj_regs(to_host(res.vclk), to_host(res.vval), actors, vals, res.nval.cpu().numpy())
+    for g in range(G):
+        assert got[g].vals == folds[g].vals  # same values in the same Vec order
 
 
 def test_mvreg_lub_many_capacity_and_empty(gpu_ctx):
