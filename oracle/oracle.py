@@ -828,6 +828,8 @@ def orswot_fold(clock: np.ndarray, entries: np.ndarray, def_off=None, def_clock=
         def_clock = np.zeros((1, A), dtype=np.uint64)
         def_members = np.zeros((1, Mw), dtype=np.uint64)
     def_off, def_clock, def_members = _c64(def_off), _c64(def_clock), _c64(def_members)
+    if def_off.shape != (R + 1,):  # per-replica offsets; anything else would be read out of bounds
+        raise ValueError(f"orswot_fold: def_off must hold R + 1 = {R + 1} per-replica offsets, got {def_off.shape}")
     D = int(def_off[-1])
     maxd = max(D, 1)
     oc = np.zeros(A, dtype=np.uint64)

@@ -63,6 +63,7 @@ struct Tune {
   int map_scan2 = 0;   // ... scan two actors per 16-byte LDS read (even A; measured no faster)
   int map_scan3 = 1;   // ... scan from per-actor thresholds with every LDS read issued first
   int map_rs = 1;      // ... register-staged whole-chunk skip (A <= 32 on the LDS-DMA shapes)
+  int map_batch = 1;   // ... RS path: chunk-test compares batched ahead of their scalar ANDs
   int map_lazyv = 1;   // ... RS path: values fetched only for chunks the exact loop runs (not streamed)
   int map_diag = 0;    // ... timing probes only, results WRONG (bit0: no clock-max piece, bit1: 3 fewer step pieces)
   int rows_blocks_per_cu = 0;  // row-pair / row-reduction kernels (causal.hip); 0 = per-kernel default

@@ -61,6 +61,7 @@ struct MapPlan {
   // its clocks with one compare (the acc clock only ever takes maxima of replica clocks, map.rs:217)
   const u64 *cmax;
   unsigned long long nch;
+  int batch;  // RS chunk test: compares batched ahead of their scalar ANDs (1) or interleaved (0)
   int lazyv;  // RS path: the values of a chunk fetched only when the exact loop runs it
   int diag;   // timing probes (results wrong): bit0 no clock-max piece, bit1 3 fewer step pieces
 };
@@ -779,7 +780,7 @@ struct RsNoDma {
   __device__ __forceinline__ void operator()(int) {}
 };
 
-template <int VI, int NP, int NQ, bool PRESENT, class F = RsNoDma>
+template <int VI, int NP, int NQ, bool PRESENT, bool BATCH = false, class F = RsNoDma>
 __device__ __forceinline__ u64 rs_noop(const RsChunk<VI, NP> &r, const RsOwn<NQ, NP> &o, F &&dma = F{}) {
   constexpr int LPS = 4;
   constexpr int ND = std::remove_reference_t<F>::count;  // pieces to issue: two per element, the rest after
@@ -809,6 +810,41 @@ __device__ __forceinline__ u64 rs_noop(const RsChunk<VI, NP> &r, const RsOwn<NQ,
         if (j + 1 < ND) dma(j + 1);
       }
       const u64 e2 = r.e[m][h], tb = o.tb[m][h];
+      if constexpr (BATCH) {
+        // Every compare of the element first, then the scalar ANDs: a compare's lane mask reaches the
+        // scalar unit ~25 cycles after issue, so an AND right behind its compare stalls the wave for
+        // that long, while a batch of compares overlaps those latencies (scripts/probe_cmp.hip:
+        // 25 -> 11.5 cycles per compare + AND on gfx950).
+        const u64 bP2 = __ballot(e2 != 0), bB0 = __ballot(e2 <= tb);
+        if constexpr (!PRESENT) {
+          __builtin_amdgcn_sched_barrier(0);
+          mP2 |= bP2;
+          mB &= bB0;
+        } else {
+          const u64 co = r.co[m][h], ea = o.ea[m][h];
+          const u64 bB1 = __ballot(ea - 1 >= co), bB2 = __ballot(ea == e2), bO = __ballot(co <= o.to[m][h]);
+          const u64 del = e2 > ea ? e2 : 0;
+          u64 bV[VI], bL[VI][NQ1];
+#pragma unroll
+          for (int t = 0; t < VI; ++t) {
+            const u64 c2 = r.c[t][m][h];
+            bV[t] = __ballot(c2 <= del);
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) bL[t][q] = __ballot(c2 <= o.sq[q][m][h]);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          mP2 |= bP2;
+          mB &= bB0 & (bB1 | bB2);
+          mO &= bO;
+#pragma unroll
+          for (int t = 0; t < VI; ++t) {
+            mVan[t] &= bV[t];
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) mLe[t][q] &= bL[t][q];
+          }
+        }
+        continue;
+      }
       mP2 |= __ballot(e2 != 0);
       if constexpr (!PRESENT) {
         mB &= __ballot(e2 <= tb);
@@ -883,7 +919,7 @@ __device__ __forceinline__ void rs_reload(RsChunk<VI, NP> &r, const u64 *img, un
 }
 
 // The verdict from the register-held operands: TB = max(e, min(Cs, m1)) computed here.
-template <int VI, int NP, int NQ, bool PRESENT, class F = RsNoDma>
+template <int VI, int NP, int NQ, bool PRESENT, bool BATCH = false, class F = RsNoDma>
 __device__ __forceinline__ u64 rs_reg_noop(const RsChunk<VI, NP> &r, const RsReg<NP> &g, F &&dma = F{}) {
   RsOwn<NQ, NP> o;
 #pragma unroll
@@ -898,22 +934,22 @@ __device__ __forceinline__ u64 rs_reg_noop(const RsChunk<VI, NP> &r, const RsReg
 #pragma unroll
     for (int q = 0; q < (NQ > 0 ? NQ : 1); ++q) o.sq[q][m] = g.sq[q < 3 ? q : 0][m];
   }
-  return rs_noop<VI, NP, NQ, PRESENT>(r, o, dma);
+  return rs_noop<VI, NP, NQ, PRESENT, BATCH>(r, o, dma);
 }
 // One instantiation per presence: own values are compared as 3 slots, the unused ones zero —
 // neutral, since "c2 <= 0 everywhere" only covers an empty incoming slot, which the "appended, then
 // forgotten" test covers anyway — so the kernel carries two copies of the test, not five (the
 // fast path's code footprint is what sets its speed: the instruction cache is shared by two CUs).
-template <int VI, int NP, class F = RsNoDma>
+template <int VI, int NP, bool BATCH = false, class F = RsNoDma>
 __device__ __forceinline__ u64 rs_reg_noop_nv(const RsChunk<VI, NP> &r, const RsReg<NP> &g, bool present, int nv,
                                               F &&dma = F{}) {
-  if (!present) return rs_reg_noop<VI, NP, 0, false>(r, g, dma);
+  if (!present) return rs_reg_noop<VI, NP, 0, false, BATCH>(r, g, dma);
   if (nv > 3) {
 #pragma unroll
     for (int j = 0; j < std::remove_reference_t<F>::count; ++j) dma(j);
     return 0;
   }
-  return rs_reg_noop<VI, NP, 3, true>(r, g, dma);
+  return rs_reg_noop<VI, NP, 3, true, BATCH>(r, g, dma);
 }
 
 // The next chunk's LDS-DMA pieces as that hook (a whole chunk, every lane moving a piece of every
@@ -1205,9 +1241,13 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
                 reinterpret_cast<const unsigned *>(p.vval + g * p.vv_gs + (i2 + (sv < C ? sv : 0)) * p.vv_rs + k * VI) + dw,
                 vsl, sv < C, p.cmax + (g * p.nch + i2 / C) * A + 2 * lane, cms, (unsigned long long)(2 * lane) < A,
                 vpiece, p.diag};
-        skip = (rs_reg_noop_nv<VI, NP>(rA, rg, present, nv, d) & want) == want;
+        skip = ((p.batch ? rs_reg_noop_nv<VI, NP, true>(rA, rg, present, nv, d)
+                         : rs_reg_noop_nv<VI, NP, false>(rA, rg, present, nv, d)) &
+                want) == want;
       } else if (el) {
-        skip = (rs_reg_noop_nv<VI, NP>(rA, rg, present, nv) & want) == want;
+        skip = ((p.batch ? rs_reg_noop_nv<VI, NP, true>(rA, rg, present, nv)
+                         : rs_reg_noop_nv<VI, NP, false>(rA, rg, present, nv)) &
+                want) == want;
       }
       MAP_TOCK(cy_scan);
 #ifdef MAP_STATS
@@ -1803,6 +1843,7 @@ extern "C" int crdt_map_lub_many(crdt_ctx *ctx, const crdt_map_batch *in, crdt_m
   p.scan2 = ctx->tune.map_scan2 && A % 2 == 0;
   p.scan3 = ctx->tune.map_scan3;
   p.lazyv = ctx->tune.map_lazyv;
+  p.batch = ctx->tune.map_batch;
   p.diag = ctx->tune.map_diag;
   if (int rc = device_fill(ctx, out->flags, G * sizeof(unsigned), 0)) return rc;
   // LDS-DMA staging when every step image is whole 16-byte pieces (A even, 16-byte aligned

@@ -177,9 +177,10 @@ def test_orswot_host_lub_many_streamed(stage_kb, G, R):
     from 1 to all replicas of a group."""
     M, A = 70, 9
     rng = np.random.default_rng(stage_kb + G)
-    cs, es, offs, dcls, dmems = [], [], [0], [], []
+    cs, es, offs, roffs, dcls, dmems = [], [], [0], [], [], []
     for g in range(G):
         c, e, off, dcl, dmem = O.gen_orswot(int(rng.integers(1 << 30)), R, M, A, kmax=12, p_def=0.4)
+        roffs.append(off)  # per-replica offsets (the oracle's form); the library takes per-group ones
         cs.append(c)
         es.append(e)
         offs.append(offs[-1] + int(off[-1]))
@@ -195,8 +196,7 @@ def test_orswot_host_lub_many_streamed(stage_kb, G, R):
     for x in ("clock", "entries", "def_keep", "def_members"):
         np.testing.assert_array_equal(getattr(res[0], x), getattr(res[1], x), err_msg=x)
     for g in range(G):
-        goff = np.array([0, offs[g + 1] - offs[g]])
-        oc, oe, odef, _ = O.orswot_fold(cs[g], es[g], goff, dcls[g], dmems[g])
+        oc, oe, odef, _ = O.orswot_fold(cs[g], es[g], roffs[g], dcls[g], dmems[g])
         np.testing.assert_array_equal(res[0].clock[g], oc)
         np.testing.assert_array_equal(res[0].entries[g], oe)
         surv = {(tuple(int(x) for x in dcl[d]), O.bitmap_members(res[0].def_members[d]))
