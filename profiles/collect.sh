@@ -11,4 +11,4 @@ B="bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-c5"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$tag -o run -- python3 $B > gpurun_out/prof_$tag.log 2>&1 || exit $?
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch_$tag -o run -- python3 $B > gpurun_out/pmc_fetch_$tag.log 2>&1 || exit $?
 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write_$tag -o run -- python3 $B > gpurun_out/pmc_write_$tag.log 2>&1 || exit $?
-python3 scripts/summarize_prof.py "$tag"  # (re-run locally after gpurun merges gpurun_out/)
+python3 scripts/prof_summary.py "$tag" lub_multi_kernel 6442457088  # (re-run locally after gpurun merges gpurun_out/)
