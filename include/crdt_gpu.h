@@ -478,7 +478,9 @@ int crdt_lwwreg_lub_many_sharded(crdt_ctx *ctx, const uint64_t *marker, const ui
  * (may be NULL); flags[g] (required): bit 0 = some key folded to more than Vout values (its
  * slots are then incomplete: retry with a larger Vout), bit 1 = def_row not non-decreasing or
  * >= R, bit 2 = the fold state of some key needed more values than it holds (results of the
- * group incomplete: retry with Vstate = 8).  The state holds VO = 2*pow2(V') values, V' the
+ * group incomplete: retry with Vstate = 8), bit 3 = internal: a key wave waited past its bound
+ * for the workgroup's shared clock-row ring (results of the group unreliable; never expected —
+ * report it).  The state holds VO = 2*pow2(V') values, V' the
  * smallest power of two with V' >= V and 2V' >= min(8, max(Vout, Vstate)); VO <= 8.
  * Deferred output as for Orswot (def_keep / def_keys over keys).
  * Limits: A <= 256, V <= 8, Vout <= 64; the fold state holds up to 16 values per key (bit 2 of

@@ -129,6 +129,8 @@ def lub_many(clock: torch.Tensor, ec: torch.Tensor, vclk: torch.Tensor, vval: to
             f |= int(x)
         if f & 2:
             raise ValueError("map.lub_many: def_row must be non-decreasing within each group and < R")
+        if f & 8:
+            raise RuntimeError("map.lub_many: internal fault (shared clock-row ring wait timed out)")
         # the fold state overflowed: rerun with the next larger state (a key-sharded call already
         # did that inside the C entry point, on every rank together)
         if f & 4 and vstate < 16 and _key_shard is None:

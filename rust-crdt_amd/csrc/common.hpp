@@ -64,6 +64,8 @@ struct Tune {
   int map_scan3 = 1;   // ... scan from per-actor thresholds with every LDS read issued first
   int map_rs = 1;      // ... register-staged whole-chunk skip (A <= 32 on the LDS-DMA shapes)
   int map_batch = 1;   // ... RS path: chunk-test compares batched ahead of their scalar ANDs
+  int map_sh = 0;      // ... RS path at A = 32, V = 2, K % 4 == 0: four key waves share each chunk's clock
+                       //     rows (less traffic, but slower: the coupled waves; opt-in)
   int map_lazyv = 1;   // ... RS path: values fetched only for chunks the exact loop runs (not streamed)
   int map_diag = 0;    // ... timing probes only, results WRONG (bit0: no clock-max piece, bit1: 3 fewer step pieces)
   int rows_blocks_per_cu = 0;  // row-pair / row-reduction kernels (causal.hip); 0 = per-kernel default

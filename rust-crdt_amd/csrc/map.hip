@@ -51,7 +51,8 @@ struct MapPlan {
   unsigned long long G, R, K, A, V, Kw, Vout;
   u64 *o_clock, *o_ec, *o_vclk, *o_vval;
   unsigned *o_nval;
-  unsigned *o_flags;  // per group: bit0 > Vout values, bit1 bad def_row, bit2 state capacity
+  unsigned *o_flags;  // per group: bit0 > Vout values, bit1 bad def_row, bit2 state capacity,
+                      // bit3 SH ring arrival wait past its bound (internal fault)
   int spec;           // speculative no-op scan on (tuning / diagnosis knob; results are identical)
   int nt;             // LDS-DMA step images with the non-temporal policy (tuning knob)
   int scan2;          // speculative scan with two actors per 16-byte LDS read (A even)
@@ -63,7 +64,8 @@ struct MapPlan {
   unsigned long long nch;
   int batch;  // RS chunk test: compares batched ahead of their scalar ANDs (1) or interleaved (0)
   int lazyv;  // RS path: the values of a chunk fetched only when the exact loop runs it
-  int diag;   // timing probes (results wrong): bit0 no clock-max piece, bit1 3 fewer step pieces
+  int diag;   // timing probes (results wrong): bit0 no clock-max piece, bit1 3 fewer step pieces,
+              // bit2 SH path without arrival waits
 };
 
 constexpr int kMapQ = 4;    // deferred removes tracked per key in registers before the slow path
@@ -751,14 +753,23 @@ struct RsOwn {
 };
 
 // The scan operands of the fold state from the LDS mirror (me / mc) and thresholds (TB / TO).
-template <int NQ, bool PRESENT, int NP>
+// The actor pair element m of lane (s, gq) holds in the scan layout: 2gq + 8m, or with PERM (the
+// SH path, whose reads are bank-conflict free only when each lane walks its pairs rotated by its
+// step) 2gq + 8((m + s) % 4) (NP == 4).
+template <bool PERM>
+__device__ __forceinline__ unsigned rs_a0(int lane, int m) {
+  const unsigned gq = (unsigned)lane & 3;
+  if constexpr (PERM) return 2 * gq + 8 * ((m + ((unsigned)lane >> 2)) & 3);
+  return 2 * gq + 8 * m;
+}
+
+template <int NQ, bool PRESENT, int NP, bool PERM = false>
 __device__ __forceinline__ RsOwn<NQ, NP> rs_own(const u64 *mirror, const u64 *thr, unsigned long long A, int lane,
                                                 int nv = NQ) {
   RsOwn<NQ, NP> o;
-  const unsigned gq = (unsigned)lane & 3;
 #pragma unroll
   for (int m = 0; m < NP; ++m) {
-    const unsigned a0 = 2 * gq + 8 * m;
+    const unsigned a0 = rs_a0<PERM>(lane, m);
     const unsigned long long a = a0 < A ? a0 : A - 2;
     o.tb[m] = lds2(thr + a);
     if constexpr (PRESENT) {
@@ -884,12 +895,12 @@ __device__ __forceinline__ u64 rs_noop(const RsChunk<VI, NP> &r, const RsOwn<NQ,
 
 // The verdict from the LDS mirror (the exact loop's scan): one instantiation per presence, own
 // values as 3 zero-padded slots (see rs_reg_noop_nv).
-template <int VI, int NP>
+template <int VI, int NP, bool PERM = false>
 __device__ __forceinline__ u64 rs_lds_own_noop(const RsChunk<VI, NP> &r, const u64 *mirror, const u64 *thr,
                                                unsigned long long A, bool present, int nv, int lane) {
-  if (!present) return rs_noop<VI, NP, 0, false>(r, rs_own<0, false, NP>(mirror, thr, A, lane));
+  if (!present) return rs_noop<VI, NP, 0, false>(r, rs_own<0, false, NP, PERM>(mirror, thr, A, lane));
   if (nv > 3) return 0;
-  return rs_noop<VI, NP, 3, true>(r, rs_own<3, true, NP>(mirror, thr, A, lane, nv));
+  return rs_noop<VI, NP, 3, true>(r, rs_own<3, true, NP, PERM>(mirror, thr, A, lane, nv));
 }
 
 template <int VI, int NP>
@@ -1030,16 +1041,192 @@ __device__ __forceinline__ void rs_store(const RsChunk<VI, NP> &r, u64 *img, uns
     for (int t = 0; t < VI; ++t) vals[s * VI + t] = r.v[t];
 }
 
+// ---- Shared replica-clock ring (SH path: the RS path at A = 32, V = 2, four key waves per CU) ------
+// A chunk's replica-clock rows are the same for every key of a group and a quarter of each step
+// image, and a CU's LDS-DMA engine takes one instruction per ~17 cycles whatever its lane count
+// (scripts/micro/glds_rate.hip: 68 cycles per piece per wave at four waves per CU, 1 KiB or 256 B
+// alike).  In the SH path the four waves of a workgroup fold four keys of one group: each wave
+// streams its key's entry / value clocks into two private slots, packed 4 steps to 3 pieces (12
+// per chunk instead of 16), and the clock rows and clock max of a chunk are staged ONCE per
+// workgroup into a ring of kShS shared slots — wave w moves steps 4w..4w+3 and a quarter of the
+// clock max.  14 instructions per chunk and wave instead of 17, and the clock rows leave L2 once
+// per workgroup instead of once per key (the excess PMC traffic of the RS path).
+// Layouts, in 16-byte units (a pair of u64 words): every 16 consecutive DMA lanes move one 256-byte
+// row (a DMA instruction whose lane quads span rows costs its CU 1.3-4x, scripts/micro/glds_rate.hip)
+//   private slot  192*(s/4) + 64*part + 16*(s%4) + pair   (part 0 entry clock, 1.. value clocks;
+//                 pair = actor / 2; 1,536 words)
+//   shared slot   64*(s/4) + 16*(s%4) + pair  (the clock rows, 512 words), then the chunk clock max [A]
+// and lane (s, gq) of the chunk test reads its pairs gq + 4m rotated by its step (rs_a0<true>), so
+// that the 16 lanes of one LDS read cycle hit 16 different banks.
+// Hand-over: a wave's pieces are in LDS once its own vmcnt retires them; it then adds 1 to the
+// slot's arrival counter, and a wave reads chunk c's shared slot only once the counter reached
+// 4 * (c / kShS + 1).  Shared pieces go out kShD chunks ahead of their use and are signalled two
+// chunks after issue (the private ring's depth), so a wave waits on another only when that one
+// runs more than kShD - 2 chunks behind (an exact loop).  A slot is refilled (chunk c + kShD, at
+// iteration c, after chunk c arrived: every wave has then signalled chunk c, i.e. finished
+// iteration c - 3) only once chunk c + kShD - kShS <= c - 3 is done everywhere: kShS = 2*kShD - 1.
+constexpr int kShD = 5;
+constexpr int kShS = 2 * kShD - 1;
+constexpr unsigned kShSlot = 1536;            // private slot, u64 words (16 steps x 3 rows x 32)
+constexpr unsigned kShShared = 512 + 32;      // shared slot: clock rows + clock max
+constexpr unsigned kShSpin = 1u << 22;        // arrival-wait bound (a protocol fault is reported, never hangs)
+
+// Per-lane LDS-DMA sources of the SH path: piece v (part v) of a 4-step group moves pair lane%16 of
+// part v of step lane/16; the shared piece of wave w the same pair of the clock row of step
+// 4w + lane/16.
+struct ShLanes {
+  const char *b[3];            // part v's row of replica 0 at the lane's pair (bytes)
+  unsigned long long st[3];    // part v's replica stride (bytes)
+  const char *cb;              // clock row of replica 0 at the lane's pair
+  unsigned long long cst;      // clock replica stride (bytes)
+  unsigned sub;                // lane / 16: the step of a 4-step group this lane moves
+};
+
+__device__ __forceinline__ ShLanes sh_lanes(const MapPlan &p, unsigned long long g, unsigned long long k, int lane) {
+  ShLanes L;
+  const unsigned long long A = p.A, pr = (unsigned)lane & 15;
+  const unsigned long long be = (unsigned long long)(p.ec + g * p.e_gs + k * A);
+  const unsigned long long bv = (unsigned long long)(p.vclk + g * p.vc_gs + k * 2 * A);
+  L.b[0] = reinterpret_cast<const char *>(be + pr * 16);
+  L.b[1] = reinterpret_cast<const char *>(bv + pr * 16);
+  L.b[2] = reinterpret_cast<const char *>(bv + A * 8 + pr * 16);
+  L.st[0] = (unsigned long long)p.e_rs * 8;
+  L.st[1] = L.st[2] = (unsigned long long)p.vc_rs * 8;
+  L.cb = reinterpret_cast<const char *>((unsigned long long)(p.clock + g * p.c_gs) + pr * 16);
+  L.cst = (unsigned long long)p.c_rs * 8;
+  L.sub = (unsigned)lane >> 4;
+  return L;
+}
+
+// The 12 private pieces of chunk [i0, i0 + 16) (steps past iend - 1 clamped: copies never read).
+__device__ __forceinline__ void sh_chunk_images(const ShLanes &L, unsigned long long i0, unsigned long long iend,
+                                                u64 *img) {
+  if (i0 + 16 <= iend) {
+    const char *src[3];
+#pragma unroll
+    for (int v = 0; v < 3; ++v) src[v] = L.b[v] + (i0 + L.sub) * L.st[v];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int v = 0; v < 3; ++v) {
+        glds16(src[v], img + (3 * q + v) * 128);
+        src[v] += 4 * L.st[v];
+      }
+  } else {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const unsigned long long i = i0 + 4 * q + L.sub < iend ? i0 + 4 * q + L.sub : iend - 1;
+#pragma unroll
+      for (int v = 0; v < 3; ++v) glds16(L.b[v] + i * L.st[v], img + (3 * q + v) * 128);
+    }
+  }
+}
+
+// Wave w's 2 shared pieces of chunk c: clock rows of steps 4w..4w+3, clock max words 8w..8w+7.
+__device__ __forceinline__ void sh_chunk_shared(const MapPlan &p, const ShLanes &L, unsigned long long g,
+                                                unsigned long long c, unsigned long long iend, unsigned w, u64 *shs,
+                                                int lane) {
+  const unsigned long long i0 = c * 16 + 4 * w + L.sub;
+  glds16(L.cb + (i0 < iend ? i0 : iend - 1) * L.cst, shs + 128 * w);
+  if (lane < 4) glds16(p.cmax + (g * p.nch + c) * p.A + 8 * w + 2 * lane, shs + 512 + 8 * w);
+}
+
+// The same 14 pieces as the chunk test's DMA hook (RsNoDma's interface).
+struct ShDma {
+  static constexpr int count = 14;
+  const char *src[3];
+  unsigned long long st4[3];
+  u64 *img;
+  const char *csrc;
+  u64 *cdst;
+  const u64 *msrc;
+  u64 *mdst;
+  bool mon;
+  __device__ __forceinline__ void operator()(int j) {
+    if (j < 12) {
+      const int v = j % 3;
+      glds16(src[v], img + j * 128);
+      src[v] += st4[v];
+    } else if (j == 12) {
+      glds16(csrc, cdst);
+    } else {
+      if (mon) glds16(msrc, mdst);
+    }
+  }
+};
+
+// u64 offsets of element m (actor pair rs_a0<true>) of lane (s, gq) = (lane / 4, lane % 4) of the
+// chunk test in the SH layouts (part t of the private slot at +128t words).
+__device__ __forceinline__ unsigned sh_poff(int lane, int m) {
+  const unsigned s = (unsigned)lane >> 2;
+  return 2 * (192 * (s >> 2) + 16 * (s & 3)) + rs_a0<true>(lane, m);
+}
+__device__ __forceinline__ unsigned sh_coff(int lane, int m) {
+  const unsigned s = (unsigned)lane >> 2;
+  return 2 * (64 * (s >> 2) + 16 * (s & 3)) + rs_a0<true>(lane, m);
+}
+// ... and of actor a at step s (lane = actor: the exact loop's reads)
+__device__ __forceinline__ unsigned sh_pword(unsigned s, unsigned a) {
+  return 2 * (192 * (s >> 2) + 16 * (s & 3)) + a;
+}
+__device__ __forceinline__ unsigned sh_cword(unsigned s, unsigned a) {
+  return 2 * (64 * (s >> 2) + 16 * (s & 3)) + a;
+}
+
+template <int VI, int NP>
+__device__ __forceinline__ void sh_reload(RsChunk<VI, NP> &r, const u64 *img, const u64 *shs, unsigned long long A,
+                                          int lane, bool cmload = true) {
+#pragma unroll
+  for (int m = 0; m < NP; ++m) {
+    const unsigned po = sh_poff(lane, m);
+    r.e[m] = lds2(img + po);
+#pragma unroll
+    for (int t = 0; t < VI; ++t) r.c[t][m] = lds2(img + po + 128 * (1 + t));
+    r.co[m] = lds2(shs + sh_coff(lane, m));
+  }
+  if (cmload) {
+    r.cm = shs[512 + ((unsigned long long)lane < A ? lane : A - 1)];
+#pragma unroll
+    for (int m = 0; m < NP; ++m) r.cmp[m] = lds2(shs + 512 + rs_a0<true>(lane, m));
+  } else {
+    r.cm = 0;
+#pragma unroll
+    for (int m = 0; m < NP; ++m) r.cmp[m] = u64x2{0, 0};
+  }
+}
+
+// A chunk the test could not skip: its entry / value clocks back into the private slot (the slot
+// was being refilled); the clock rows and clock max stay in the shared slot.
+template <int VI, int NP>
+__device__ __forceinline__ void sh_store(const RsChunk<VI, NP> &r, u64 *img, int lane) {
+#pragma unroll
+  for (int m = 0; m < NP; ++m) {
+    const unsigned po = sh_poff(lane, m);
+    *reinterpret_cast<u64x2 *>(img + po) = r.e[m];
+#pragma unroll
+    for (int t = 0; t < VI; ++t) *reinterpret_cast<u64x2 *>(img + po + 128 * (1 + t)) = r.c[t][m];
+  }
+}
+
+// The SH arrival counter of a shared slot, read through LDS each time (other waves add to it).
+__device__ __forceinline__ unsigned sh_arrived(const unsigned *cnt) {
+  return __builtin_amdgcn_readfirstlane(*reinterpret_cast<const volatile unsigned *>(cnt));
+}
+
 // ITM: unrolled scan iterations ceil(A / LPS) rounded up to a power of two, fixed per launch so
 // each kernel's register allocation only covers its own scan shape.  NP > 0: the RS path (above).
-template <int APL, int VI, int VO, int CM, int NB, bool GL, int ITM, int NP = 0>
-__global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
+template <int APL, int VI, int VO, int CM, int NB, bool GL, int ITM, int NP = 0, bool SH = false>
+__global__ __launch_bounds__(SH ? 256 : 64) void map_fold_kernel(MapPlan pk) {
   constexpr bool RS = NP > 0;
+  static_assert(!SH || (RS && VI == 2 && NP == 4), "SH path: the RS path at A = 32, V = 2");
   const MapPlan p = pk;  // a local copy the optimizer can split into registers (the by-value
                          // kernel argument itself would be materialized in scratch memory)
-  const unsigned long long g = blockIdx.x / p.K;
-  const unsigned long long k = blockIdx.x % p.K;
-  const int lane = threadIdx.x;
+  // SH: a workgroup of four waves, wave w folding key 4*blockIdx + w (K % 4 == 0: one group)
+  const unsigned wv = SH ? (unsigned)threadIdx.x >> 6 : 0u;
+  const unsigned long long gk0 = SH ? 4ull * blockIdx.x + wv : (unsigned long long)blockIdx.x;
+  const unsigned long long g = gk0 / p.K;
+  const unsigned long long k = gk0 % p.K;
+  const int lane = SH ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
   const unsigned long long R = p.R;
 
   bool present = false;
@@ -1077,6 +1264,7 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
 
   extern __shared__ u64 map_lds[];
   constexpr int C = (GL || RS) ? CM : MapChunk<APL, VI, CM>::C;
+  static_assert(!SH || C == 16, "SH path: 16-replica chunks");
   static_assert(!GL || (APL == 1 && NB >= 2), "LDS-DMA staging: one actor per lane");
   static_assert(GL || RS || NB == 2, "register staging double-buffers");
   static_assert(!RS || (APL == 1 && !GL && NB == 2 && CM == 16 && VO <= 4 && VI <= 2), "RS path shape");
@@ -1086,10 +1274,16 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
   const unsigned long long A = p.A;
   const unsigned long long W = (2 + VI) * A;
   const unsigned long long WS = map_ws(W);  // padded step stride in the ring
-  // LDS: NB image slots (C*WS words each), NB value slots (C*VI), the per-key remove list, the
-  // fold-state mirror.  (Addresses are always computed from map_lds: a pointer table would hide
-  // the LDS address space and turn every access into a flat op.)
-  u64 *const vbase = map_lds + NB * C * WS;
+  // LDS: NB image slots (C*WS words each; SH: kShSlot), NB value slots (C*VI), the per-key remove
+  // list, the fold-state mirror.  (Addresses are always computed from map_lds: a pointer table
+  // would hide the LDS address space and turn every access into a flat op.)  SH: four such wave
+  // regions (no clock-max slots), then the shared ring and its arrival counters.
+  const unsigned long long SLOT = SH ? kShSlot : C * WS;
+  const unsigned long long PW = NB * SLOT + NB * C * VI + kMapL + (2 + VO) * A + ((GL || RS) && !SH ? NB * A : 0) + 4 * A;
+  u64 *const wl = map_lds + (SH ? wv * PW : 0);
+  u64 *const shr = map_lds + 4 * PW;  // SH: kShS shared slots
+  unsigned *const arr = reinterpret_cast<unsigned *>(shr + kShS * kShShared);
+  u64 *const vbase = wl + NB * SLOT;
   unsigned *lrow = reinterpret_cast<unsigned *>(vbase + NB * C * VI);
   unsigned *lidx = lrow + kMapL;
   // fold-state mirror read by the speculative scan: entry clock, VO value clocks, acc clock
@@ -1097,7 +1291,7 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
   constexpr bool kSpec = APL == 1 && VO <= 4;
   u64 *const cml = mirror + (2 + VO) * A;  // GL: NB staged chunk clock maxima (A words each)
   // scan thresholds (map_noop_steps3, RS): TB [A] | TO [A]; m1 = (min nonzero own value clock) - 1
-  u64 *const thr = cml + ((GL || RS) ? NB * A : 0);
+  u64 *const thr = cml + ((GL || RS) && !SH ? NB * A : 0);
   u64 *const csm = thr + 2 * A;  // RS: the acc clock and m1 handed back to the register operands
   u64 *const m1m = thr + 3 * A;
   u64 m1 = ~0ull;
@@ -1145,8 +1339,8 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
   int cool = 0;
   bool anti = true;  // own values an antichain (scan precondition), refreshed after exact steps
 #ifdef MAP_STATS
-  unsigned st_exact = 0, st_scan = 0, st_fail = 0, st_nq = 0, st_pres = 0;
-  u64 cy_issue = 0, cy_wait = 0, cy_scan = 0, cy_skip = 0, cy_exact = 0, cy_t0 = 0, cy_all = __builtin_amdgcn_s_memtime();
+  unsigned st_exact = 0, st_scan = 0, st_fail = 0, st_nq = 0, st_pres = 0, st_spin = 0;
+  u64 cy_arr = 0, cy_issue = 0, cy_wait = 0, cy_scan = 0, cy_skip = 0, cy_exact = 0, cy_t0 = 0, cy_all = __builtin_amdgcn_s_memtime();
 #define MAP_TICK() (cy_t0 = __builtin_amdgcn_s_memtime())
 #define MAP_TOCK(acc) (acc += __builtin_amdgcn_s_memtime() - cy_t0)
 #else
@@ -1171,11 +1365,33 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
   const int ni = GL ? (int)((W + 127) / 128) : 0;  // 1-KiB pieces per step image (GL: 1 or 2)
   GldsLanes<1> gl1;
   GldsLanes<2> gl2;
-  const bool vpiece = !(RS && p.lazyv);
-  if constexpr (RS) {  // chunks 0 and 1 into the two slots (W <= 128: one piece per step)
+  const bool vpiece = !(RS && (SH || p.lazyv));
+  ShLanes shl;
+  // SH ring bookkeeping (uniform): the shared slot of chunk ch and the arrival count it needs, the
+  // slot of chunk ch + kShD - 2 (signalled at iteration ch) and of chunk ch + kShD (issued)
+  unsigned sh_use = 0, sh_need = 4, sh_sig = kShD - 2, sh_iss = kShD;
+  bool sh_late = false;  // an arrival wait ran past kShSpin (reported as flag bit 3)
+  unsigned sh_pre = 0;    // chunk ch's arrival count as read during iteration ch-1 (0: not read)
+  if constexpr (SH) {
+    shl = sh_lanes(p, g, k, lane);
+    if (threadIdx.x < kShS) arr[threadIdx.x] = 0;
+    __syncthreads();
+    // chunks 0 .. kShD-3: shared pieces issued, retired and signalled at once; then, in the order
+    // every iteration issues them, chunk 0's images + chunk kShD-2's shared pieces, chunk 1's
+    // images + chunk kShD-1's shared pieces
+    for (unsigned long long c = 0; c + 2 < (unsigned long long)kShD && c < nch; ++c)
+      sh_chunk_shared(p, shl, g, c, R, wv, shr + c * kShShared, lane);
+    wait_vmcnt<0>();
+    for (unsigned long long c = 0; c + 2 < (unsigned long long)kShD && c < nch; ++c)
+      if (lane == 0) atomicAdd(arr + c, 1u);
+    for (unsigned long long c = 0; c < 2 && c < nch; ++c) {
+      sh_chunk_images(shl, c * C, R, wl + c * SLOT);
+      if (c + kShD - 2 < nch) sh_chunk_shared(p, shl, g, c + kShD - 2, R, wv, shr + (c + kShD - 2) * kShShared, lane);
+    }
+  } else if constexpr (RS) {  // chunks 0 and 1 into the two slots (W <= 128: one piece per step)
     gl1 = glds_lanes<VI, 1>(p, g, k, lane);
     for (unsigned long long c = 0; c < 2 && c < nch; ++c)
-      map_chunk_glds<VI, C, 1>(p, gl1, g, k, c * C, R, map_lds + c * C * WS, WS, vbase + c * C * VI, cml + c * A, lane,
+      map_chunk_glds<VI, C, 1>(p, gl1, g, k, c * C, R, wl + c * SLOT, WS, vbase + c * C * VI, cml + c * A, lane,
                                vpiece, p.diag);
   }
   if constexpr (GL) {
@@ -1183,24 +1399,25 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
     else gl2 = glds_lanes<VI, 2>(p, g, k, lane);
     for (unsigned long long c = 0; c + 1 < NB && c < nch; ++c) {
       if (ni == 1) {
-        if (p.nt) map_chunk_glds<VI, C, 1, 2>(p, gl1, g, k, c * C, R, map_lds + c * C * WS, WS, vbase + c * C * VI, cml + c * A, lane);
-        else map_chunk_glds<VI, C, 1>(p, gl1, g, k, c * C, R, map_lds + c * C * WS, WS, vbase + c * C * VI, cml + c * A, lane);
+        if (p.nt) map_chunk_glds<VI, C, 1, 2>(p, gl1, g, k, c * C, R, wl + c * SLOT, WS, vbase + c * C * VI, cml + c * A, lane);
+        else map_chunk_glds<VI, C, 1>(p, gl1, g, k, c * C, R, wl + c * SLOT, WS, vbase + c * C * VI, cml + c * A, lane);
       } else {
-        map_chunk_glds<VI, C, 2>(p, gl2, g, k, c * C, R, map_lds + c * C * WS, WS, vbase + c * C * VI, cml + c * A, lane);
+        map_chunk_glds<VI, C, 2>(p, gl2, g, k, c * C, R, wl + c * SLOT, WS, vbase + c * C * VI, cml + c * A, lane);
       }
     }
   } else if constexpr (!RS) {
     if (nch > 0) {
       map_chunk_load(regs, p, g, k, 0, R, lane);
-      map_chunk_store(regs, map_lds, vbase, A, WS, R < (unsigned long long)C ? R : C, lane);
+      map_chunk_store(regs, wl, vbase, A, WS, R < (unsigned long long)C ? R : C, lane);
       if (nch > 1) map_chunk_load(regs, p, g, k, C, R, lane);
     }
   }
 
   for (unsigned long long ch = 0; ch < nch; ++ch) {
     const unsigned slot = (unsigned)(ch % NB);
-    const u64 *buf = map_lds + slot * C * WS;
+    const u64 *buf = wl + slot * SLOT;
     const u64 *vb = vbase + slot * C * VI;
+    const u64 *shx = shr;  // SH: chunk ch's shared slot (clock rows, clock max)
     if constexpr (RS) {
       // Chunk ch sits in slot ch&1 (LDS-DMA, issued two chunks ago), chunk ch+1 in the other slot.
       // Copy chunk ch into registers, refill its slot with chunk ch+2 at once — two chunks stay in
@@ -1213,29 +1430,98 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
       const unsigned long long n0 = R - ch * C < (unsigned long long)C ? R - ch * C : C;
       const u64 want = n0 >= 16 ? grp_mask<4>() : (grp_mask<4>() & ((1ull << (4 * n0)) - 1));
       const bool el = elig0 && (unsigned long long)next_row >= ch * C + n0;
-      u64 *const img = map_lds + slot * C * WS;
+      u64 *const img = wl + slot * SLOT;
       u64 *const vsl = vbase + slot * C * VI;
-      u64 *const cms = cml + slot * A;
+      u64 *const cms = SH ? shr + sh_use * kShShared + 512 : cml + slot * A;
+      u64 *const shs = shr + sh_use * kShShared;  // SH: chunk ch's shared slot
+      shx = shs;
       MAP_TICK();
-      if (ch + 1 < nch) {
-        if (vpiece) wait_vmcnt<P1>();
-        else wait_vmcnt<P1 - 1>();  // (no values piece)
+      if constexpr (SH) {
+        // the pieces iteration ch-1 issued may still be in flight: 12 images (chunk ch+1) and,
+        // while chunk ch+kShD-1 exists, 2 shared pieces
+        if (ch + kShD - 1 < nch) wait_vmcnt<14>();
+        else if (ch + 1 < nch) wait_vmcnt<12>();
+        else wait_vmcnt<0>();
+        // this wave's shared pieces of chunk ch+kShD-2 (issued at iteration ch-2) have landed
+        if (ch + kShD - 2 < nch && lane == 0) atomicAdd(arr + sh_sig, 1u);
+        // chunk ch's shared slot: every wave's pieces landed
+        unsigned spins = 0;
+        MAP_TOCK(cy_wait);
+        MAP_TICK();
+        // (read one iteration ahead, so normally known; after one timeout: no more waits)
+        while (!(p.diag & 4) && !sh_late && sh_pre < sh_need && (sh_pre = sh_arrived(arr + sh_use)) < sh_need) {
+#ifdef MAP_STATS
+          ++st_spin;
+#endif
+          if (++spins > kShSpin) {
+            sh_late = true;
+            break;
+          }
+        }
+        MAP_TOCK(cy_arr);
+        MAP_TICK();
       } else {
-        wait_vmcnt<0>();
+        if (ch + 1 < nch) {
+          if (vpiece) wait_vmcnt<P1>();
+          else wait_vmcnt<P1 - 1>();  // (no values piece)
+        } else {
+          wait_vmcnt<0>();
+        }
       }
       MAP_TOCK(cy_wait);
       MAP_TICK();
-      rs_reload(rA, img, WS, vsl, cms, A, lane, vpiece);
+      unsigned pre_raw = 0;
+      if constexpr (SH) {
+        sh_reload(rA, img, shs, A, lane);
+        // next chunk's arrival count, read with this chunk's slots
+        pre_raw = *reinterpret_cast<const volatile unsigned *>(arr + (sh_use + 1 == kShS ? 0 : sh_use + 1));
+      } else {
+        rs_reload(rA, img, WS, vsl, cms, A, lane, vpiece);
+      }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot is read: refill it
+      if constexpr (SH) sh_pre = __builtin_amdgcn_readfirstlane(pre_raw);
       // a whole next chunk with every lane moving a piece: its pieces go out during the test
       const unsigned long long i2 = (ch + 2) * C;
-      const bool spread = el && ch + 2 < nch && i2 + C <= R && (2 + VI) * A == 128;
-      if (ch + 2 < nch && !spread)
-        map_chunk_glds<VI, C, 1>(p, gl1, g, k, i2, R, img, WS, vsl, cms, lane, vpiece, p.diag);
+      const bool spread = el && ch + 2 < nch && i2 + C <= R && (2 + VI) * A == 128 && (!SH || ch + kShD < nch);
+      if constexpr (SH) {
+        if (!spread) {
+          if (ch + 2 < nch) sh_chunk_images(shl, i2, R, img);
+          if (ch + kShD < nch) sh_chunk_shared(p, shl, g, ch + kShD, R, wv, shr + sh_iss * kShShared, lane);
+        }
+      } else {
+        if (ch + 2 < nch && !spread)
+          map_chunk_glds<VI, C, 1>(p, gl1, g, k, i2, R, img, WS, vsl, cms, lane, vpiece, p.diag);
+      }
       MAP_TOCK(cy_issue);
+      // advance the ring bookkeeping (the rest of the iteration uses sh_use only through shs / cms)
+      if constexpr (SH) {
+        if (++sh_use == kShS) {
+          sh_use = 0;
+          sh_need += 4;
+        }
+        if (++sh_sig == kShS) sh_sig = 0;
+      }
+      const unsigned sh_iss_now = sh_iss;
+      if constexpr (SH) {
+        if (++sh_iss == kShS) sh_iss = 0;
+      }
       MAP_TICK();
       bool skip = false;
-      if (spread) {
+      if (SH && spread) {
+        const unsigned long long ic = (ch + kShD) * C + 4 * wv + shl.sub;
+        ShDma d{{shl.b[0] + (i2 + shl.sub) * shl.st[0], shl.b[1] + (i2 + shl.sub) * shl.st[1],
+                 shl.b[2] + (i2 + shl.sub) * shl.st[2]},
+                {4 * shl.st[0], 4 * shl.st[1], 4 * shl.st[2]},
+                img,
+                shl.cb + (ic < R ? ic : R - 1) * shl.cst,
+                shr + sh_iss_now * kShShared + 128 * wv,
+                p.cmax + (g * p.nch + ch + kShD) * A + 8 * wv + 2 * lane,
+                shr + sh_iss_now * kShShared + 512 + 8 * wv,
+                lane < 4};
+        skip = ((p.batch ? rs_reg_noop_nv<VI, NP, true>(rA, rg, present, nv, d)
+                         : rs_reg_noop_nv<VI, NP, false>(rA, rg, present, nv, d)) &
+                want) == want;
+      } else if (spread) {
         const int sv = lane / (2 * VI), dw = lane % (2 * VI);
         RsDma d{gl1.src0[0] + i2 * gl1.stride[0], gl1.stride[0], img, WS,
                 reinterpret_cast<const unsigned *>(p.vval + g * p.vv_gs + (i2 + (sv < C ? sv : 0)) * p.vv_rs + k * VI) + dw,
@@ -1263,7 +1549,8 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
         continue;
       }
       wait_vmcnt<0>();
-      rs_store(rA, img, WS, vsl, cms, A, lane, vpiece);
+      if constexpr (SH) sh_store(rA, img, lane);
+      else rs_store(rA, img, WS, vsl, cms, A, lane, vpiece);
       if (!vpiece && lane < C * VI) {  // the chunk's values, fetched now (a chunk the exact loop runs)
         const unsigned long long iv = ch * C + lane / VI;
         vsl[lane] = p.vval[g * p.vv_gs + (iv < R ? iv : R - 1) * p.vv_rs + k * VI + lane % VI];
@@ -1283,10 +1570,10 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
         const unsigned ns = (unsigned)(nx % NB);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot's last LDS reads are done
         if (ni == 1) {
-          if (p.nt) map_chunk_glds<VI, C, 1, 2>(p, gl1, g, k, nx * C, R, map_lds + ns * C * WS, WS, vbase + ns * C * VI, cml + ns * A, lane);
-          else map_chunk_glds<VI, C, 1>(p, gl1, g, k, nx * C, R, map_lds + ns * C * WS, WS, vbase + ns * C * VI, cml + ns * A, lane);
+          if (p.nt) map_chunk_glds<VI, C, 1, 2>(p, gl1, g, k, nx * C, R, wl + ns * SLOT, WS, vbase + ns * C * VI, cml + ns * A, lane);
+          else map_chunk_glds<VI, C, 1>(p, gl1, g, k, nx * C, R, wl + ns * SLOT, WS, vbase + ns * C * VI, cml + ns * A, lane);
         } else {
-          map_chunk_glds<VI, C, 2>(p, gl2, g, k, nx * C, R, map_lds + ns * C * WS, WS, vbase + ns * C * VI, cml + ns * A, lane);
+          map_chunk_glds<VI, C, 2>(p, gl2, g, k, nx * C, R, wl + ns * SLOT, WS, vbase + ns * C * VI, cml + ns * A, lane);
         }
       }
       MAP_TOCK(cy_issue);
@@ -1323,7 +1610,13 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
           // (the RS path and register staging keep the round-1 scan: the threshold scan's loads in
           // flight would not fit beside their chunk registers)
           u64 noop;
-          if constexpr (RS)
+          if constexpr (SH) {
+            RsChunk<VI, NP> r;
+            sh_reload(r, buf, shx, A, lane, false);
+#pragma unroll
+            for (int t = 0; t < VI; ++t) r.v[t] = 0;
+            noop = rs_lds_own_noop<VI, NP, true>(r, mirror, thr, A, present, nv, lane);
+          } else if constexpr (RS)
             noop = rs_lds_noop_nv<VI, (RS ? NP : 1)>(buf, WS, mirror, thr, A, present, nv, lane);
           else
             noop = (p.scan3 && GL) ? map_noop_nv3<VI, LPS, ITM>(buf, (unsigned)WS, (unsigned)A, mirror, thr,
@@ -1340,14 +1633,14 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
           MAP_TICK();
           if ((GL || RS) && s == 0 && j == n) {  // the whole chunk: its staged clock max
             const unsigned long long a = (unsigned long long)lane < A ? lane : A - 1;
-            const u64 x = cml[slot * A + a];
+            const u64 x = SH ? shx[512 + a] : cml[slot * A + a];
             if ((unsigned long long)lane < A) cs[0] = cs[0] > x ? cs[0] : x;
           } else {  // acc.clock.merge of the skipped replicas: every read issued at once, range masked
             const unsigned long long a = (unsigned long long)lane < A ? lane : A - 1;
             u64 mx = cs[0];
 #pragma unroll
             for (int u = 0; u < C; ++u) {
-              const u64 co = buf[u * WS + (1 + VI) * A + a];
+              const u64 co = SH ? shx[sh_cword(u, (unsigned)a)] : buf[u * WS + (1 + VI) * A + a];
               const u64 take = ((unsigned long long)u >= s && (unsigned long long)u < j) ? ~0ull : 0ull;
               const u64 x = co & take;
               mx = mx > x ? mx : x;
@@ -1374,7 +1667,19 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
 #endif
       MAP_TICK();
       const unsigned long long i = i0 + s;
-      const MapStep<APL, VI> in = map_step_read<APL, VI>(buf + s * WS, vb + s * VI, A, lane);
+      MapStep<APL, VI> in;
+      if constexpr (SH) {  // lane = actor: entry / value clocks from the private slot, clock row shared
+        const bool on = (unsigned long long)lane < A;
+        const unsigned pw = sh_pword((unsigned)s, on ? (unsigned)lane : 0u);
+        in.e[0] = on ? buf[pw] : 0;
+#pragma unroll
+        for (int t = 0; t < VI; ++t) in.c[t][0] = on ? buf[pw + 128 * (1 + t)] : 0;
+        in.co[0] = on ? shx[sh_cword((unsigned)s, (unsigned)lane)] : 0;
+#pragma unroll
+        for (int t = 0; t < VI; ++t) in.v[t] = vb[s * VI + t];
+      } else {
+        in = map_step_read<APL, VI>(buf + s * WS, vb + s * VI, A, lane);
+      }
       ++s;
       // ---- 1. entry join (map.rs:142-210) ----
       const bool p2 = any_nz(in.e);
@@ -1610,7 +1915,7 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
         const int nvx = __builtin_popcount(__builtin_amdgcn_readfirstlane(mv.vm));  // own values, compacted
 #pragma unroll
         for (int m = 0; m < NP; ++m) {
-          const unsigned a0 = 2 * gq + 8 * m;
+          const unsigned a0 = rs_a0<SH>(lane, m);
           const unsigned long long a = a0 < A ? a0 : A - 2;
           rg.ea[m] = lds2(mirror + a);
           rg.to[m] = lds2(thr + A + a);
@@ -1621,9 +1926,12 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
         }
       }
       // re-issue chunk ch+2 into the slot the exact loop used
-      if (ch + 2 < nch) {
+      if (SH && ch + 2 < nch) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        map_chunk_glds<VI, C, 1>(p, gl1, g, k, (ch + 2) * C, R, map_lds + slot * C * WS, WS, vbase + slot * C * VI,
+        sh_chunk_images(shl, (ch + 2) * C, R, wl + slot * SLOT);
+      } else if (ch + 2 < nch) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        map_chunk_glds<VI, C, 1>(p, gl1, g, k, (ch + 2) * C, R, wl + slot * SLOT, WS, vbase + slot * C * VI,
                                  cml + slot * A, lane, vpiece, p.diag);
       }
     }
@@ -1631,7 +1939,7 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
       if (ch + 1 < nch) {  // stage the next chunk (its loads were issued a whole chunk ago)
         const unsigned long long nn = R - (ch + 1) * C < (unsigned long long)C ? R - (ch + 1) * C : C;
         const unsigned ns = (unsigned)((ch + 1) % NB);
-        map_chunk_store(regs, map_lds + ns * C * WS, vbase + ns * C * VI, A, WS, nn, lane);
+        map_chunk_store(regs, wl + ns * SLOT, vbase + ns * C * VI, A, WS, nn, lane);
         if (ch + 2 < nch) map_chunk_load(regs, p, g, k, (ch + 2) * C, R, lane);
       }
     }
@@ -1641,8 +1949,8 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
 #ifdef MAP_STATS
   cy_all = __builtin_amdgcn_s_memtime() - cy_all;
   if (lane == 0 && (k % 97) == 0)
-    printf("k=%llu exact=%u scan=%u fail=%u nq=%u pres=%u nl=%llu | cyc all=%llu issue=%llu wait=%llu scan=%llu skip=%llu exact=%llu\n",
-           k, st_exact, st_scan, st_fail, st_nq, st_pres, nl, cy_all, cy_issue, cy_wait, cy_scan, cy_skip, cy_exact);
+    printf("k=%llu exact=%u scan=%u fail=%u nq=%u pres=%u nl=%llu spin=%u | cyc all=%llu issue=%llu wait=%llu arr=%llu scan=%llu skip=%llu exact=%llu\n",
+           k, st_exact, st_scan, st_fail, st_nq, st_pres, nl, st_spin, cy_all, cy_issue, cy_wait, cy_arr, cy_scan, cy_skip, cy_exact);
 #endif
   // ---- egress: slots in Vec order (ascending order key) ----
   const int nv = __builtin_popcount(mv.vm);
@@ -1684,7 +1992,7 @@ __global__ __launch_bounds__(64) void map_fold_kernel(MapPlan pk) {
       p.o_vval[gk * p.Vout + o] = v;
     }
     if (p.o_nval) p.o_nval[gk] = present ? (unsigned)nv : 0u;
-    const unsigned f = (unsigned)ovf | (bad ? 2u : 0u);
+    const unsigned f = (unsigned)ovf | (bad ? 2u : 0u) | (sh_late ? 8u : 0u);
     if (f) atomicOr(p.o_flags + g, f);
   }
 }
@@ -1735,6 +2043,20 @@ static hipError_t launch_map_rs(const MapPlan &p, unsigned long long blocks, hip
   if (p.A <= 8) return launch_map_it<1, VI, 4, 16, 2, false, 2, 1>(p, blocks, s);
   if (p.A <= 16) return launch_map_it<1, VI, 4, 16, 2, false, 4, 2>(p, blocks, s);
   return launch_map_it<1, VI, 4, 16, 2, false, 8, 4>(p, blocks, s);
+}
+
+// SH path (A = 32, V = 2, K % 4 == 0): blocks of four key waves, the shared clock-row ring after
+// the four wave regions.
+static hipError_t launch_map_sh(const MapPlan &p, unsigned long long blocks, hipStream_t s) {
+  constexpr int VI = 2, VO = 4, C = 16, NB = 2;
+  const size_t PW = NB * kShSlot + NB * C * VI + kMapL + (2 + VO) * p.A + 4 * p.A;
+  const size_t lds = (4 * PW + kShS * kShShared) * sizeof(u64) + kShS * sizeof(unsigned);
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  auto *fn = &map_fold_kernel<1, VI, VO, C, NB, false, 8, 4, true>;
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(fn), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(fn, dim3((unsigned)(blocks / 4)), dim3(256), lds, s, p);
+  return hipGetLastError();
 }
 
 // Scan shape: NS steps per scan (C rounded up to a power of two, <= 16), LPS = 64 / NS lanes per
@@ -1877,7 +2199,9 @@ extern "C" int crdt_map_lub_many(crdt_ctx *ctx, const crdt_map_batch *in, crdt_m
     p.cmax = cm;
     hipLaunchKernelGGL(map_chunk_max_kernel, dim3((unsigned)(G * p.nch)), dim3(64), 0, ctx->stream, p.clock,
                        p.c_rs, p.c_gs, (unsigned long long)R, (unsigned long long)A, p.nch, gC, cm);
-    if (rs)
+    if (rs && ctx->tune.map_sh && A == 32 && V == 2 && K % 4 == 0)
+      he = launch_map_sh(p, blocks, ctx->stream);
+    else if (rs)
       he = V == 1 ? launch_map_rs<1>(p, blocks, ctx->stream) : launch_map_rs<2>(p, blocks, ctx->stream);
     else
       he = V == 1 ? launch_map_glds<1>(p, ctx->tune.map_chunk, ctx->tune.map_ring, blocks, ctx->stream)

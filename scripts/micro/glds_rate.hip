@@ -22,8 +22,18 @@ __global__ __launch_bounds__(64) void glds_kernel(const char *src, u64 mask, int
     u64 *slot = lds + (i & 1) * 16 * 128;
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
-      if (lane < active)
-        __builtin_amdgcn_global_load_lds(src + ((off + s * 1024 + lane * 16) & mask),
+      // active < 0: the SH path's first packing, lane l moving 16 bytes of row (l % 4), the rows
+      // 4 KiB apart (every quad of lanes touches 4 lines); active == 65: rows of 256 B, lanes
+      // 16 j .. 16 j + 15 contiguous in row j (every quad one 64-byte run)
+      // active == 66: quad-interleaved (quad t = step t % 4, pairs 4 (t / 4) ..), active == 67: 16 lanes
+      // per row, the row's pairs rotated by 4 * row
+      const u64 lo = active < 0    ? (u64)(lane & 3) * 4096 + (u64)(lane >> 2) * 16
+                     : active == 65 ? (u64)(lane >> 4) * 4096 + (u64)(lane & 15) * 16
+                     : active == 66 ? (u64)((lane >> 2) & 3) * 4096 + (u64)(4 * (lane >> 4) + (lane & 3)) * 16
+                     : active == 67 ? (u64)(lane >> 4) * 4096 + (u64)(((lane & 15) + 4 * (lane >> 4)) & 15) * 16
+                                    : (u64)lane * 16;
+      if (active < 0 || active >= 65 || lane < active)
+        __builtin_amdgcn_global_load_lds(src + ((off + s * 1024 + lo) & mask),
                                          (__attribute__((address_space(3))) void *)(slot + s * 128), 16, 0, 0);
     }
     off += (u64)gridDim.x * 16 * 1024;
@@ -56,14 +66,14 @@ int main() {
   hipMemset(src, 1, big);
   hipMalloc(&out, 8192 * 8);
   const int iters = 2000;
-  for (int blocks : {256, 1024, 2048}) {
-    for (int act : {64, 48, 32, 16}) {
+  for (int blocks : {1024}) {
+    for (int act : {64, -1, 65, 66, 67}) {
       for (int which = 0; which < 2; ++which) {
         const u64 mask = which ? big - 1 : (64 << 10) - 1;
         const float ms = run(src, mask, blocks, iters, act, out);
         const double pieces = (double)iters * 16;
         const double ns = ms * 1e6 / pieces;
-        const double bytes = (double)blocks * pieces * act * 16;
+        const double bytes = (double)blocks * pieces * (act < 0 || act >= 65 ? 64 : act) * 16;
         printf("waves %5d lanes %2d src %-6s: %.2f ns (%.0f cycles @2.4GHz) per piece per wave, %.2f TB/s\n", blocks,
                act, which ? "stream" : "L2", ns, ns * 2.4, bytes / (ms * 1e-3) / 1e12);
       }

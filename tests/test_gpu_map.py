@@ -19,8 +19,10 @@ import crdts_gpu as cg  # noqa: E402
 # actors per 16-byte LDS read (mscan2=1, even A; off by default: no faster), the threshold scan
 # (mscan3=1, the default of the LDS-DMA ring) and the non-temporal step-image loads (mnt=1, off by
 # default); and the register-staged whole-chunk skip (mrs=1, the default where A <= 32 on the
-# LDS-DMA shapes), also with the scan off (mspec=0: every chunk handed to the exact loop).
-MODES = ["mglds=1,mrs=1", "mglds=1,mrs=1,mspec=0",
+# LDS-DMA shapes), also with the scan off (mspec=0: every chunk handed to the exact loop); and at
+# A = 32, V = 2, K % 4 == 0 the RS path with four key waves sharing each chunk's clock rows (msh=1,
+# opt-in: less traffic, slower).
+MODES = ["mglds=1,mrs=1", "mglds=1,mrs=1,mspec=0", "mglds=1,mrs=1,msh=1",
          "mglds=1,mrs=0,mchunk=16,mring=2,mscan3=1,mnt=0", "mglds=1,mrs=0,mchunk=8,mring=4,mscan3=1,mnt=0",
          "mglds=0,mscan2=0,mnt=0", "mglds=1,mrs=0,mchunk=16,mring=2,mscan3=0,mscan2=0,mnt=0",
          "mglds=1,mrs=0,mchunk=16,mring=2,mscan3=0,mscan2=1,mnt=1", "mglds=0,mscan2=1,mnt=0"]
@@ -324,3 +326,61 @@ def test_map_many_concurrent_values(mctx, R, V):
             _gpu(mctx, d, R * V)
         return
     _check(mctx, d, R * V)
+
+
+def _old_heavy(rng, R, K, A, G=1, D=None):
+    """_chain_dense at A = 32, V = 2 with mostly old replicas (most chunks skipped whole, a few
+    handed to the exact loop), stacked over G groups."""
+    parts = []
+    for _ in range(G):
+        d = _chain_dense(rng, R, K, A, 2, cmax=40)
+        old = rng.random(R) < 0.9
+        d["ec"][old] = np.minimum(d["ec"][old], 2).astype(np.uint64)
+        d["vclk"][old] = np.minimum(d["vclk"][old], 2).astype(np.uint64)
+        parts.append(d)
+    return parts
+
+
+@pytest.mark.parametrize("R", [1, 3, 15, 16, 17, 31, 32, 33, 48, 63, 64, 65, 80, 81, 97, 113, 150, 1000])
+def test_map_shared_ring_chunk_counts(mctx, R):
+    """The SH path (msh=1: four key waves per workgroup sharing each chunk's clock rows through a ring of
+    shared LDS slots) at every chunk count around its prologue / ring depth (1..9 chunks and past
+    it), partial last chunks, K = 8 keys (two workgroups); results must equal the oracle fold in
+    every staging mode."""
+    rng = np.random.default_rng(4000 + R)
+    d = _old_heavy(rng, R, 8, 32)[0]
+    exp = O.map_fold(d["clock"], d["ec"], d["vclk"], d["vval"], d["def_row"], d["def_clock"],
+                     d["def_keys"], 64)
+    if int(exp[4].max() if exp[4].size else 0) > 4:
+        pytest.skip("fold needs more than 4 values")
+    _check(mctx, d, 4)
+
+
+@pytest.mark.parametrize("seed,R,K", [(41, 300, 4), (42, 777, 12), (43, 64, 16)])
+def test_map_shared_ring_groups(mctx, seed, R, K):
+    """SH path over several groups (each workgroup's four keys inside one group, groups with their
+    own clock rows and deferred lists)."""
+    rng = np.random.default_rng(seed)
+    G = 3
+    parts = _old_heavy(rng, R, K, 32, G=G)
+    st = {k: np.stack([p[k] for p in parts]) for k in ("clock", "ec", "vclk", "vval")}
+    st["def_row"] = np.concatenate([p["def_row"] for p in parts])
+    st["def_clock"] = np.concatenate([p["def_clock"] for p in parts])
+    st["def_keys"] = np.concatenate([p["def_keys"] for p in parts])
+    counts = [p["def_row"].shape[0] for p in parts]
+    exps = [O.map_fold(p["clock"], p["ec"], p["vclk"], p["vval"], p["def_row"], p["def_clock"], p["def_keys"], 64)
+            for p in parts]
+    if max(int(e[4].max() if e[4].size else 0) for e in exps) > 4:
+        pytest.skip("fold needs more than 4 values")
+    exps = [O.map_fold(p["clock"], p["ec"], p["vclk"], p["vval"], p["def_row"], p["def_clock"], p["def_keys"], 4)
+            for p in parts]
+    res, kw = _gpu(mctx, st, 4, groups=counts)
+    off = np.cumsum([0] + counts)
+    for g, exp in enumerate(exps):
+        np.testing.assert_array_equal(to_host(res.clock[g]), exp[0])
+        np.testing.assert_array_equal(to_host(res.ec[g]), exp[1])
+        np.testing.assert_array_equal(to_host(res.vclk[g]), exp[2])
+        np.testing.assert_array_equal(to_host(res.vval[g]), exp[3])
+        np.testing.assert_array_equal(res.nval[g].cpu().numpy(), exp[4])
+        got = cg.map.deferred_set(kw["def_clock"], res.def_keep, res.def_keys, int(off[g]), int(off[g + 1])) if kw else set()
+        assert got == exp[5]
