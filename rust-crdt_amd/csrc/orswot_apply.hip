@@ -396,6 +396,380 @@ __global__ __launch_bounds__(kBlock) void orswot_apply_kernel_a256(OrswotApplyPl
   orswot_apply_body<kCAMax>(p);
 }
 
+// ---- Sixteen lanes per state (A <= 64) --------------------------------------------------------
+// The wave-per-state kernel above spends a whole wave on ops that touch one cell: a one-member Add
+// is a seen test, one cell read-modify-write and a clock word, so its wave issues ~70 instructions
+// for one state's op (VALU ~20% busy, profiles/r02k_apply_sq_counters.json) and the kernel is
+// bound by instruction issue.  Here a GROUP of 16 lanes runs one state's op stream (4 states per
+// wave): lane g holds actors a = g + 16j (the clock in registers, rows read 128 contiguous bytes
+// per group), a row operation costs each lane 4 words, a cell operation one lane.  (One lane per
+// state was tried first: a Rm's row work then costs every lane 64 scattered words, 3.5x slower;
+// 8 lanes per state held 157 VGPRs, 3 waves per SIMD.)
+// apply_deferred without rescanning every slot on every Add (orswot.rs:281-286):
+//  * keep test !(rm <= C): each slot keeps a WITNESS, the first actor with rm[a] > C[a] (an LDS
+//    byte).  C only grows, so actors before the witness stay dominated and the witness only moves
+//    forward: an Add to actor a re-examines only slots whose witness is a (W: bit a set iff some
+//    slot's witness is a; exact for A <= 64), from a + 1 on; a slot left without one is dropped.
+//  * re-forget: a slot's members were forgotten by its clock when it was created (apply_rm,
+//    :230-250) or, for the input's slots, by the full pass at the first Add; forgets commute and
+//    are idempotent, so an Add re-forgets only the cells it wrote, and only when one of its members
+//    may be in a slot (bloom: bit m % 64 of the OR of every slot's member-bitmap words).
+//  * identical clocks (HashMap keyed by VClock): the witness is a function of the clock (at the
+//    current C), so a Rm's clock is compared in full only with slots of the same witness.
+// Exact for ANY input state (the first Add re-forgets every input slot's members in full).
+constexpr int kG = 16;                // lanes per state
+constexpr unsigned kGMask = kG == 32 ? 0xFFFFFFFFu : (1u << kG) - 1;
+constexpr int kJ = kWave / kG;        // actors per lane (A <= 64)
+constexpr unsigned kNoWitness = 0xFFu;
+
+__device__ __forceinline__ unsigned grp_bits(u64 ballot, int lane) { return (unsigned)(ballot >> (lane & ~(kG - 1))) & kGMask; }
+__device__ __forceinline__ bool grp_any(bool x, int lane) { return grp_bits(__ballot(x), lane) != 0; }
+__device__ __forceinline__ bool grp_all(bool x, int lane) { return grp_bits(__ballot(x), lane) == kGMask; }
+// min over the 16 lanes of a DPP row: xor 1, xor 2 (quad_perm), then the mirrors within 8 and 16
+// lanes pair every lane with one of the other half — VALU moves, no LDS round trip
+__device__ __forceinline__ unsigned grp_min(unsigned x) {
+  static_assert(kG == 16, "DPP row reduction");
+  unsigned y = (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+  x = y < x ? y : x;
+  y = (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+  x = y < x ? y : x;
+  y = (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  x = y < x ? y : x;
+  y = (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0x140, 0xF, 0xF, false);  // row_mirror
+  return y < x ? y : x;
+}
+__device__ __forceinline__ u64 grp_or(u64 x) {
+#pragma unroll
+  for (int o = 1; o < kG; o <<= 1) x |= __shfl_xor(x, o);
+  return x;
+}
+
+// The group's first actor a >= from with x[a] > c[a] (kNoWitness if none); lane g holds a = g + kG*j.
+__device__ __forceinline__ unsigned grp_witness(const u64 (&x)[kJ], const u64 (&c)[kJ], int g, unsigned from,
+                                                unsigned long long A) {
+  unsigned f = kNoWitness;
+#pragma unroll
+  for (int j = kJ - 1; j >= 0; --j) {
+    const unsigned a = g + kG * j;
+    if (a < A && a >= from && x[j] > c[j]) f = a;
+  }
+  return grp_min(f);
+}
+
+__device__ __forceinline__ void grp_load_row(u64 (&x)[kJ], const u64 *row, int g, unsigned long long A) {
+#pragma unroll
+  for (int j = 0; j < kJ; ++j) {
+    const unsigned a = g + kG * j;
+    x[j] = a < A ? row[a] : 0;
+  }
+}
+
+// forget a member row by the rm clock in registers: keep e[a] iff e[a] > rm[a]
+__device__ __forceinline__ void grp_forget_row(u64 *row, const u64 (&r)[kJ], int g, unsigned long long A) {
+  u64 e[kJ];
+  grp_load_row(e, row, g, A);
+#pragma unroll
+  for (int j = 0; j < kJ; ++j) {
+    const unsigned a = g + kG * j;
+    if (a < A && e[j] != 0 && e[j] <= r[j]) row[a] = 0;
+  }
+}
+
+#ifndef CRDT_GRP_WPE
+#define CRDT_GRP_WPE 4
+#endif
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRDT_GRP_WPE))) void orswot_apply_grp_kernel(
+    OrswotApplyPlan p) {
+  extern __shared__ u64 lds[];
+  const int lane = (int)(threadIdx.x % kWave), g = lane & (kG - 1);
+  const unsigned long long s = ((unsigned long long)blockIdx.x * kBlock + threadIdx.x) / kG;
+  if (s >= p.N) return;  // (whole groups)
+  const unsigned long long A = p.A, M = p.M, Mw = p.Mw, Dcap = p.Dcap;
+  // LDS: per group the kG op headers of the current batch (32 bytes each), then the slot witnesses
+  u64 *hdr = lds + (threadIdx.x / kG) * (4 * kG);
+  uint8_t *wit = reinterpret_cast<uint8_t *>(lds + (kBlock / kG) * 4 * kG) + (threadIdx.x / kG) * Dcap;
+  const bool lead = g == 0;
+
+  const unsigned long long ob = p.op_off[s], oe = p.op_off[s + 1];
+  unsigned dcnt = p.def_count[s];
+  if (dcnt > Dcap || oe < ob || oe > p.n_ops) {
+    if (lead) p.status[s] = (dcnt > Dcap ? 4u : 0u) | (oe < ob || oe > p.n_ops ? 8u : 0u);
+    return;  // state left untouched
+  }
+  unsigned st = 0;
+  u64 *C = p.clock + s * p.clock_stride;
+  u64 *E = p.entries + s * p.entry_sstride;
+  u64 *DC = p.def_clock + s * Dcap * A;
+  u64 *DM = p.def_members + s * Dcap * Mw;
+  u64 c[kJ];
+  grp_load_row(c, C, g, A);
+
+  // W (witness actors) and bloom (member bits mod 64) of the slots, identical in the group's lanes
+  u64 W = 0, bloom = 0;
+  auto rebuild = [&]() {
+    W = 0;
+    u64 b = 0;
+    for (unsigned d = 0; d < dcnt; ++d) {
+      const unsigned w = wit[d];
+      if (w != kNoWitness) W |= 1ull << w;
+      for (unsigned long long x = g; x < Mw; x += kG) b |= DM[d * Mw + x];
+    }
+    bloom = grp_or(b);
+  };
+  for (unsigned d = 0; d < dcnt; ++d) {  // the input slots' witnesses at the input clock
+    u64 x[kJ];
+    grp_load_row(x, DC + d * A, g, A);
+    const unsigned w = grp_witness(x, c, g, 0, A);
+    if (lead) wit[d] = (uint8_t)w;
+  }
+  rebuild();
+  bool full = true;  // no Add yet: the input slots' members are re-forgotten in full at the first
+
+  // drop slot d: the last slot moves over it
+  auto drop = [&](unsigned d) {
+    const unsigned last = dcnt - 1;
+    if (d != last) {
+#pragma unroll
+      for (int j = 0; j < kJ; ++j) {
+        const unsigned a = g + kG * j;
+        if (a < A) DC[d * A + a] = DC[last * A + a];
+      }
+      for (unsigned long long x = g; x < Mw; x += kG) DM[d * Mw + x] = DM[last * Mw + x];
+      if (lead) wit[d] = wit[last];
+    }
+    dcnt = last;
+    if (p.fence) wave_fence();  // (a wave's later loads see its earlier stores; afence=1 adds fences)
+  };
+
+  // Ops go in batches of kG: lane g loads op (base + g)'s header, first member and — for a
+  // one-member Add — its cell, all at once; op i then reads them from lane i of the group.  A
+  // prefetched cell is stale once an earlier op of the batch wrote that member's row (same first
+  // member, any multi-member op, the full pass): `stale` marks those ops, which load it again.
+  const int gb = lane & ~(kG - 1);
+  for (unsigned long long base = ob; base < oe; base += kG) {
+    const unsigned long long oo = base + g;
+    unsigned h_ka = kBadOp, h_mb = 0, h_me = 0, h_m0 = 0xFFFFFFFFu;
+    u64 h_cr = 0, h_cell = 0;
+    if (oo < oe) {
+      const unsigned kind = p.kind[oo];
+      const u64 mb = p.mem_off[oo], me = p.mem_off[oo + 1];
+      h_mb = (unsigned)mb;
+      h_me = (unsigned)me;
+      const bool range_ok = me >= mb && me <= 0xFFFFFFFFull && me <= p.n_mem;
+      if (range_ok && kind == 0) {
+        const unsigned a = p.actor ? p.actor[oo] : 0u;
+        h_ka = a < A ? a : kBadOp;
+        h_cr = p.counter ? p.counter[oo] : 0ull;
+        if (me > mb) h_m0 = p.mem[mb];
+        if (h_ka != kBadOp && me - mb == 1 && h_m0 < M) h_cell = E[(unsigned long long)h_m0 * p.entry_mstride + a];
+      } else if (range_ok && kind == 1) {
+        h_ka = kRmOp;
+        h_cr = p.rm_row ? p.rm_row[oo] : 0u;
+        if (me > mb) h_m0 = p.mem[mb];
+      }
+    }
+    const int nb = (int)((oe - base) < (unsigned long long)kG ? (oe - base) : kG);
+    *reinterpret_cast<u64x2 *>(hdr + 4 * g) = u64x2{((u64)h_m0 << 32) | h_ka, ((u64)h_me << 32) | h_mb};
+    *reinterpret_cast<u64x2 *>(hdr + 4 * g + 2) = u64x2{h_cr, h_cell};
+    unsigned stale = 0;
+    for (int i = 0; i < nb; ++i) {
+      // op i's header: two 16-byte LDS reads, the same address for the group's lanes
+      const u64x2 h0 = *reinterpret_cast<const u64x2 *>(hdr + 4 * i);
+      const u64x2 h1 = *reinterpret_cast<const u64x2 *>(hdr + 4 * i + 2);
+      const unsigned ka = (unsigned)h0[0], m0 = (unsigned)(h0[0] >> 32);
+      const u64 mb = (unsigned)h0[1], me = (unsigned)(h0[1] >> 32);
+      const u64 cr = h1[0], cellv = h1[1];
+      const bool one = me - mb == 1;
+      // later ops of the batch whose first member this op may write
+      const unsigned same = grp_bits(__ballot(h_m0 == m0), lane) & ~((2u << i) - 1);
+      if (ka == kBadOp) {
+        st |= 2u;
+        continue;
+      }
+      if (ka != kRmOp) {  // ---- Op::Add (:57-72)
+        const unsigned a = ka;
+        const u64 k = cr;
+        const unsigned ja = a / kG, ga = a % kG;
+        u64 mine = c[0];
+#pragma unroll
+        for (int j = 1; j < kJ; ++j)
+          if ((unsigned)j == ja) mine = c[j];
+        const u64 ca = __shfl(mine, gb | (int)ga);
+        if (ca >= k) continue;  // already seen (:60-63)
+        if (one) {
+          if (m0 >= M) {
+            st |= 2u;
+          } else if (lead) {
+            u64 *cell = E + (unsigned long long)m0 * p.entry_mstride + a;
+            const u64 old = ((stale >> i) & 1u) ? *cell : cellv;
+            if (old < k) *cell = k;
+          }
+          stale |= same;
+        } else {
+          bool bad = false;
+          for (u64 j = mb + g; j < me; j += kG) {
+            const unsigned long long m = p.mem[j];
+            if (m >= M) {
+              bad = true;
+              continue;
+            }
+            u64 *cell = E + m * p.entry_mstride + a;
+            if (*cell < k) *cell = k;
+          }
+          if (grp_any(bad, lane)) st |= 2u;
+          stale = kGMask;
+          if (p.fence) wave_fence();  // cells written by other lanes of the group, read below
+        }
+        if ((unsigned)g == ga) {
+#pragma unroll
+          for (int j = 0; j < kJ; ++j)
+            if ((unsigned)j == ja) c[j] = k;
+        }
+        // apply_deferred (:281-286)
+        if (full) {  // every slot's members forgotten in full, every witness recomputed
+          full = false;
+          if (dcnt > 0) stale = kGMask;
+          for (unsigned d = 0; d < dcnt;) {
+            u64 rm[kJ];
+            grp_load_row(rm, DC + d * A, g, A);
+            for (unsigned long long x = 0; x < Mw; ++x) {
+              u64 bits = DM[d * Mw + x];
+              while (bits) {
+                const unsigned long long m = x * 64 + __builtin_ctzll(bits);
+                bits &= bits - 1;
+                if (m < M) grp_forget_row(E + m * p.entry_mstride, rm, g, A);
+              }
+            }
+            const unsigned w = grp_witness(rm, c, g, 0, A);
+            if (w == kNoWitness) {
+              drop(d);
+            } else {
+              if (lead) wit[d] = (uint8_t)w;
+              ++d;
+            }
+          }
+          if (p.fence) wave_fence();
+          rebuild();
+          continue;
+        }
+        // the cells this Add wrote, re-forgotten by every slot naming their member
+        if (dcnt > 0) {
+          for (u64 j = mb; j < me; ++j) {
+            const unsigned long long m = one ? m0 : p.mem[j];
+            if (m >= M || !((bloom >> (m % 64)) & 1ull)) continue;
+            for (unsigned d = 0; d < dcnt; ++d)
+              if ((DM[d * Mw + m / 64] >> (m % 64)) & 1ull) {
+                const u64 rv = DC[d * A + a];
+                if (lead) {
+                  u64 *cell = E + m * p.entry_mstride + a;
+                  const u64 v = *cell;
+                  if (v != 0 && v <= rv) *cell = 0;
+                }
+              }
+          }
+        }
+        // the slots whose witness was actor a: move the witness on, drop a slot left without one
+        if ((W >> a) & 1ull) {
+          bool dropped = false;
+          for (unsigned d = 0; d < dcnt;) {
+            if (wit[d] == a && DC[d * A + a] <= k) {
+              u64 x[kJ];
+              grp_load_row(x, DC + d * A, g, A);
+              const unsigned w = grp_witness(x, c, g, a + 1, A);
+              if (w == kNoWitness) {
+                drop(d);
+                dropped = true;
+                continue;
+              }
+              if (lead) wit[d] = (uint8_t)w;
+            }
+            ++d;
+          }
+          if (dropped) {
+            rebuild();
+          } else {
+            W = 0;
+            for (unsigned d = 0; d < dcnt; ++d) {
+              const unsigned w = wit[d];
+              if (w != kNoWitness) W |= 1ull << w;
+            }
+          }
+        }
+      } else {  // ---- Op::Rm -> apply_rm (:230-250)
+        const unsigned rr = (unsigned)cr;
+        if (rr >= p.n_rm_rows) {
+          st |= 2u;
+          continue;
+        }
+        u64 r[kJ];
+        grp_load_row(r, p.rm_clock + (unsigned long long)rr * A, g, A);
+        if (one) {
+          if (m0 >= M) st |= 2u;
+          else grp_forget_row(E + (unsigned long long)m0 * p.entry_mstride, r, g, A);
+          stale |= same;
+        } else {
+          for (u64 j = mb; j < me; ++j) {
+            const unsigned long long m = p.mem[j];
+            if (m >= M) {
+              st |= 2u;
+              continue;
+            }
+            grp_forget_row(E + m * p.entry_mstride, r, g, A);
+          }
+          stale = kGMask;
+        }
+        const unsigned wr = grp_witness(r, c, g, 0, A);
+        if (wr == kNoWitness) continue;  // rm <= C: already seen (:239-249)
+        int slot = -1;
+        for (unsigned d = 0; d < dcnt; ++d) {
+          if (wit[d] != wr) continue;
+          u64 x[kJ];
+          grp_load_row(x, DC + d * A, g, A);
+          bool eq = true;
+#pragma unroll
+          for (int j = 0; j < kJ; ++j) eq &= x[j] == r[j];
+          if (grp_all(eq, lane)) {
+            slot = (int)d;
+            break;
+          }
+        }
+        if (slot < 0) {
+          if (dcnt >= Dcap) {
+            st |= 1u;  // deferred capacity exceeded: this state's result is incomplete
+            continue;
+          }
+          slot = (int)dcnt++;
+#pragma unroll
+          for (int j = 0; j < kJ; ++j) {
+            const unsigned a = g + kG * j;
+            if (a < A) DC[slot * A + a] = r[j];
+          }
+          for (unsigned long long x = g; x < Mw; x += kG) DM[slot * Mw + x] = 0;
+          if (lead) wit[slot] = (uint8_t)wr;
+          W |= 1ull << wr;
+          if (p.fence) wave_fence();  // the zeroed words are or-ed by the group's first lane below
+        }
+        for (u64 j = mb; j < me; ++j) {
+          const unsigned long long m = one ? m0 : p.mem[j];
+          if (m >= M) continue;
+          if (lead) DM[slot * Mw + m / 64] |= 1ull << (m % 64);
+          bloom |= 1ull << (m % 64);
+        }
+        if (p.fence) wave_fence();
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < kJ; ++j) {
+    const unsigned a = g + kG * j;
+    if (a < A) C[a] = c[j];
+  }
+  if (lead) {
+    p.def_count[s] = dcnt;
+    p.status[s] = st;
+  }
+}
+
 }  // namespace crdt
 
 using namespace crdt;
@@ -433,6 +807,16 @@ extern "C" int crdt_orswot_apply_batch(crdt_ctx *ctx, const crdt_orswot_states *
                     (const u64 *)ops->op_off, ops->kind, ops->actor, (const u64 *)ops->counter, ops->rm_row,
                     (const u64 *)ops->rm_clock, ops->rm_clock ? ops->n_rm_rows : 0, (const u64 *)ops->mem_off,
                     ops->mem, ops->mem ? ops->n_mem : 0, ops->n_ops, status, wpb, ctx->tune.apply_fence};
+  if (ctx->tune.apply_lane && s.A <= (size_t)kWave && s.Dcap <= 2048) {
+    // kG lanes per state: kBlock / kG states per block, the slots' witness bytes in LDS
+    timing_begin(ctx, "orswot_apply");
+    const unsigned long long per_block = kBlock / kG;
+    hipLaunchKernelGGL(orswot_apply_grp_kernel, dim3((unsigned)((s.N + per_block - 1) / per_block)), dim3(kBlock),
+                       per_block * (4 * kG * 8 + s.Dcap), ctx->stream, p);
+    timing_end(ctx);
+    CRDT_HIP(ctx, hipGetLastError());
+    return CRDT_OK;
+  }
   const unsigned long long want = (s.N + wpb - 1) / wpb;
   const unsigned long long cap = (unsigned long long)ctx->cu_count * 64;
   timing_begin(ctx, "orswot_apply");
