@@ -17,6 +17,10 @@ pytestmark = pytest.mark.gpu
 import crdts_gpu as cg  # noqa: E402
 
 
+
+
+
+
 def replay_streams(seed, n_states, n_origins, K, n_ops, rm_heavy=False, key_stride=1):
     """rm_heavy: keep most removes and few writes, in causal order, so removes whose context saw
     dropped writes pile up in the deferred list."""
@@ -149,9 +153,10 @@ def test_map_apply_key_range_past_buffer(gpu_ctx):
         assert O.dense_to_map(c[s], e[s], vc[s], vv[s], []) == exp[s], s
 
 
-# A = 8 / 33 run the one-word-per-lane kernel, 100 the two-word one, 200 the four-word one
+# A = 8 / 16 / 17 / 32 / 33 run the one-word-per-lane kernel, 100 the two-word one, 200 the four-word one
 @pytest.mark.parametrize("N,T,K,A,V", [(256, 64, 16, 8, 4), (64, 100, 70, 33, 6), (48, 80, 24, 100, 8),
-                                       (32, 80, 20, 200, 8)])
+                                       (32, 80, 20, 200, 8), (257, 64, 16, 32, 4), (130, 70, 30, 16, 4),
+                                       (99, 64, 20, 17, 4)])
 def test_map_apply_synth_streams(gpu_ctx, N, T, K, A, V):
     """The bench's device-generated streams (crdts_gpu.synth.map_op_streams) vs the oracle."""
     b = cg.synth.map_op_streams(N, T, K, A, seed=N + K, device="cuda:0")
