@@ -18,6 +18,7 @@
 // One wave per state (lanes = actors, A <= 256; the state's clock in registers, its deferred list
 // in LDS for the whole stream, entries and values in HBM), as orswot_apply.hip.
 #include "common.hpp"
+#include "group.hpp"
 
 namespace crdt {
 
@@ -445,6 +446,339 @@ __global__ __launch_bounds__(kBlock) CRDT_APPLY_ATTR void map_apply_kernel(MapAp
   map_apply_body<W, SP>(p);
 }
 
+// ---- 16 lanes per state (A <= 64) ----------------------------------------------------------------
+// The structure of the Orswot group kernel (orswot_apply.hip, group.hpp) for Map<K, MVReg>: a group
+// of 16 lanes runs one state (4 states per wave; lane g holds actors g + 16j, the clock in
+// registers), op headers come 16 at a time through LDS, a row operation (entry clock, value clock,
+// Put / rm clock) costs each lane KJ words read 128 contiguous bytes per group.  apply_deferred
+// (map.rs:311-316) without rescanning every slot on every Up: each slot keeps a WITNESS, the first
+// actor with rm[a] > C[a] (C only grows: the witness only moves forward; an Up to actor a re-examines
+// the slots whose witness is a, W a 64-bit mask of witness actors), the re-forget after the first
+// full pass touches the Up's own key only (its rows are all the Up changed) and only when its key may
+// be in a slot (bloom of the slots' key-bitmap words), and a Rm compares its clock in full only
+// with slots of the same witness.  Exact for any input state.
+template <int KJ>
+__device__ void gkey_rm(const MapApplyPlan &p, unsigned long long s, unsigned long long k, const u64 (&rm)[KJ],
+                        int g, int lane) {
+  const KeyRefs q = key_refs(p, s, k);
+  u64 e[KJ];
+  grp::load_row<KJ>(e, q.ec, g, p.A);
+  if (!grp::any_nz<KJ>(e, lane)) return;  // no entry for this key
+#pragma unroll
+  for (int j = 0; j < KJ; ++j) e[j] = e[j] > rm[j] ? e[j] : 0ull;
+  const bool alive = grp::any_nz<KJ>(e, lane);
+  grp::store_row<KJ>(q.ec, e, g, p.A);
+  for (unsigned long long jv = 0; jv < p.V; ++jv) {
+    u64 v[KJ];
+    grp::load_row<KJ>(v, q.vc + jv * p.A, g, p.A);
+    if (!grp::any_nz<KJ>(v, lane)) continue;
+#pragma unroll
+    for (int j = 0; j < KJ; ++j) v[j] = alive && v[j] > rm[j] ? v[j] : 0ull;  // MVReg::forget mvreg.rs:88-104
+    grp::store_row<KJ>(q.vc + jv * p.A, v, g, p.A);
+    if (!grp::any_nz<KJ>(v, lane) && g == 0) q.vv[jv] = 0;
+  }
+}
+
+template <int KJ>
+__global__ __launch_bounds__(kBlock) void map_apply_grp_kernel(MapApplyPlan p) {
+  extern __shared__ u64 lds[];
+  constexpr int kG = grp::kG;
+  constexpr int kVB = 4;  // value rows of an Up loaded in one batch
+  const int lane = (int)(threadIdx.x % kWave), g = lane & (kG - 1);
+  const bool lead = g == 0;
+  const unsigned long long s = ((unsigned long long)blockIdx.x * kBlock + threadIdx.x) / kG;
+  if (s >= p.N) return;  // (whole groups)
+  const unsigned long long A = p.A, K = p.K, V = p.V, Kw = p.Kw, Dcap = p.Dcap;
+  // LDS: per group the op headers of the current batch (48 bytes each), then the slot witnesses
+  u64 *hdr = lds + (threadIdx.x / kG) * (6 * kG);
+  uint8_t *wit = reinterpret_cast<uint8_t *>(lds + (kBlock / kG) * 6 * kG) + (threadIdx.x / kG) * Dcap;
+
+  const unsigned long long ob = p.op_off[s], oe = p.op_off[s + 1];
+  unsigned dcnt = p.def_count[s];
+  if (dcnt > Dcap || oe < ob || oe > p.n_ops) {
+    if (lead) p.status[s] = (dcnt > Dcap ? 4u : 0u) | (oe < ob || oe > p.n_ops ? 8u : 0u);
+    return;  // state left untouched
+  }
+  unsigned st = 0;
+  u64 *Cg = p.clock + s * p.clock_s;
+  u64 *DC = p.def_clock + s * Dcap * A;
+  u64 *DK = p.def_keys + s * Dcap * Kw;
+  u64 c[KJ];
+  grp::load_row<KJ>(c, Cg, g, A);
+
+  u64 W = 0, bloom = 0;
+  auto rebuild = [&]() {  // witness mask and key bloom from the slots (the same in the group's lanes)
+    W = 0;
+    u64 b = 0;
+    for (unsigned d = 0; d < dcnt; ++d) {
+      const unsigned w = wit[d];
+      if (w != grp::kNone) W |= 1ull << w;
+      for (unsigned long long x = g; x < Kw; x += kG) b |= DK[d * Kw + x];
+    }
+    bloom = grp::orx(b);
+  };
+  for (unsigned d = 0; d < dcnt; ++d) {  // the input slots' witnesses at the input clock
+    u64 x[KJ];
+    grp::load_row<KJ>(x, DC + d * A, g, A);
+    const unsigned w = grp::witness<KJ>(x, c, g, 0, A);
+    if (lead) wit[d] = (uint8_t)w;
+  }
+  rebuild();
+  bool full = true;  // no Up yet: the input slots' keys are re-forgotten in full at the first
+  auto drop = [&](unsigned d) {  // the last slot moves over slot d
+    const unsigned last = dcnt - 1;
+    if (d != last) {
+#pragma unroll
+      for (int j = 0; j < KJ; ++j) {
+        const unsigned a = g + kG * j;
+        if (a < A) DC[d * A + a] = DC[last * A + a];
+      }
+      for (unsigned long long x = g; x < Kw; x += kG) DK[d * Kw + x] = DK[last * Kw + x];
+      if (lead) wit[d] = wit[last];
+    }
+    dcnt = last;
+  };
+
+  for (unsigned long long base = ob; base < oe; base += kG) {
+    // op headers, lane g = op base + g: kind (0 Up, 1 Rm, 2 malformed) | actor, key | pool row,
+    // counter, value, key range
+    {
+      const unsigned long long o = base + g;
+      u64 w0 = 2, w1 = 0, w2 = 0, w3 = 0, w4 = 0, w5 = 0;
+      if (o < oe) {
+        const unsigned kind = p.kind[o];
+        const unsigned rr = p.clk_row ? p.clk_row[o] : 0u;
+        if (kind == 0 && rr < p.n_clk_rows) {
+          const unsigned a = p.actor ? p.actor[o] : 0u, k = p.key ? p.key[o] : 0u;
+          if (a < A && k < K) {
+            w0 = (u64)a << 32;
+            w1 = ((u64)rr << 32) | k;
+            w2 = p.counter ? p.counter[o] : 0ull;
+            w3 = p.val ? p.val[o] : 0ull;
+          }
+        } else if (kind == 1 && rr < p.n_clk_rows) {
+          const u64 kb = p.key_off ? p.key_off[o] : 0ull, ke = p.key_off ? p.key_off[o + 1] : 0ull;
+          if (ke >= kb && ke <= p.n_keys) {  // (reversed, or past the keys buffer: malformed)
+            w0 = 1;
+            w1 = (u64)rr << 32;
+            w4 = kb;
+            w5 = ke;
+          }
+        }
+      }
+      *reinterpret_cast<u64x2 *>(hdr + 6 * g) = u64x2{w0, w1};
+      *reinterpret_cast<u64x2 *>(hdr + 6 * g + 2) = u64x2{w2, w3};
+      *reinterpret_cast<u64x2 *>(hdr + 6 * g + 4) = u64x2{w4, w5};
+    }
+    const int nb = (int)((oe - base) < (unsigned long long)kG ? (oe - base) : kG);
+    // the Put / rm clock of op i+1 is loaded while op i runs (the pool is read-only)
+    auto pool_row = [&](int i, u64 (&x)[KJ]) {
+      const u64 h1 = hdr[6 * i + 1];
+      grp::load_row<KJ>(x, p.clk_pool + (h1 >> 32) * A, g, A);
+    };
+    u64 ocn[KJ];
+    pool_row(0, ocn);
+    for (int i = 0; i < nb; ++i) {
+      u64 oc[KJ];
+#pragma unroll
+      for (int j = 0; j < KJ; ++j) oc[j] = ocn[j];
+      if (i + 1 < nb) pool_row(i + 1, ocn);
+      const u64x2 h0 = *reinterpret_cast<const u64x2 *>(hdr + 6 * i);
+      const unsigned kind = (unsigned)h0[0];
+      if (kind > 1) {
+        st |= 2u;
+        continue;
+      }
+      if (kind == 0) {  // ---- Op::Up (map.rs:119-137)
+        const unsigned a = (unsigned)(h0[0] >> 32);
+        const unsigned long long k = (unsigned)h0[1];
+        const u64x2 h1 = *reinterpret_cast<const u64x2 *>(hdr + 6 * i + 2);
+        const u64 kc = h1[0];
+        if (grp::clock_at<KJ>(c, a, lane) >= kc) continue;  // seen (:123-126)
+        const KeyRefs q = key_refs(p, s, k);
+        u64 vb[kVB][KJ];
+#pragma unroll
+        for (int t = 0; t < kVB; ++t) grp::load_row<KJ>(vb[t], q.vc + ((unsigned long long)t < V ? t : 0) * A, g, A);
+        if ((unsigned)g == a % kG) {  // entry clock apply(dot) (:130)
+          u64 *cell = q.ec + a;
+          if (*cell < kc) *cell = kc;
+        }
+        if (grp::any_nz<KJ>(oc, lane)) {  // MVReg::apply (mvreg.rs:130-166)
+          bool should_add = true;
+          int last = -1, used = 0;
+          for (unsigned long long j = 0; j < V; ++j) {
+            u64 v[KJ];
+            if (j < (unsigned long long)kVB) {
+#pragma unroll
+              for (int t = 0; t < KJ; ++t) v[t] = vb[0][t];
+#pragma unroll
+              for (int u = 1; u < kVB; ++u)
+                if ((unsigned long long)u == j)
+#pragma unroll
+                  for (int t = 0; t < KJ; ++t) v[t] = vb[u][t];
+            } else {
+              grp::load_row<KJ>(v, q.vc + j * A, g, A);
+            }
+            if (!grp::any_nz<KJ>(v, lane)) continue;
+            if (grp::all_le<KJ>(v, oc, lane)) {  // partial_cmp in {Less, Equal}: dropped
+              u64 z[KJ] = {};
+              grp::store_row<KJ>(q.vc + j * A, z, g, A);
+              if (lead) q.vv[j] = 0;
+              continue;
+            }
+            if (grp::all_le<KJ>(oc, v, lane)) should_add = false;  // v > pc (Greater)
+            last = (int)j;
+            ++used;
+          }
+          if (should_add) {
+            int slot = last + 1;
+            if (slot >= (int)V) {
+              if (used >= (int)V) {
+                st |= 16u;  // more values than slots: the state is incomplete
+                slot = -1;
+              } else {  // compact the used slots in order, then append
+                int w = 0;
+                for (unsigned long long j = 0; j < V; ++j) {
+                  u64 v[KJ];
+                  grp::load_row<KJ>(v, q.vc + j * A, g, A);
+                  if (!grp::any_nz<KJ>(v, lane)) continue;
+                  if ((unsigned long long)w != j) {
+                    const u64 x = q.vv[j];
+                    u64 z[KJ] = {};
+                    grp::store_row<KJ>(q.vc + (unsigned long long)w * A, v, g, A);
+                    grp::store_row<KJ>(q.vc + j * A, z, g, A);
+                    if (lead) {
+                      q.vv[w] = x;
+                      q.vv[j] = 0;
+                    }
+                  }
+                  ++w;
+                }
+                slot = w;
+              }
+            }
+            if (slot >= (int)V) {  // unreachable by construction; reported, never written
+              st |= 32u;
+              slot = -1;
+            }
+            if (slot >= 0) {
+              grp::store_row<KJ>(q.vc + (unsigned long long)slot * A, oc, g, A);
+              if (lead) q.vv[slot] = h1[1];
+            }
+          }
+        }
+        grp::clock_set<KJ>(c, a, kc, g);  // self.clock.apply(dot) (:133)
+        // apply_deferred (:134, :311-316)
+        if (full) {  // every slot's keys forgotten in full, every witness recomputed
+          full = false;
+          for (unsigned d = 0; d < dcnt;) {
+            u64 rm[KJ];
+            grp::load_row<KJ>(rm, DC + d * A, g, A);
+            for (unsigned long long x = 0; x < Kw; ++x) {
+              u64 kbits = DK[d * Kw + x];
+              while (kbits) {
+                const unsigned long long kk = x * 64 + __builtin_ctzll(kbits);
+                kbits &= kbits - 1;
+                if (kk < K) gkey_rm<KJ>(p, s, kk, rm, g, lane);
+              }
+            }
+            const unsigned w = grp::witness<KJ>(rm, c, g, 0, A);
+            if (w == grp::kNone) {
+              drop(d);
+            } else {
+              if (lead) wit[d] = (uint8_t)w;
+              ++d;
+            }
+          }
+          rebuild();
+          continue;
+        }
+        // key k re-forgotten by every slot naming it (only its rows changed)
+        if (dcnt > 0 && ((bloom >> (k % 64)) & 1ull)) {
+          for (unsigned d = 0; d < dcnt; ++d)
+            if ((DK[d * Kw + k / 64] >> (k % 64)) & 1ull) {
+              u64 rm[KJ];
+              grp::load_row<KJ>(rm, DC + d * A, g, A);
+              gkey_rm<KJ>(p, s, k, rm, g, lane);
+            }
+        }
+        // the slots whose witness was actor a: move the witness on, drop a slot left without one
+        if ((W >> a) & 1ull) {
+          bool dropped = false;
+          for (unsigned d = 0; d < dcnt;) {
+            if (wit[d] == a && DC[d * A + a] <= kc) {
+              u64 x[KJ];
+              grp::load_row<KJ>(x, DC + d * A, g, A);
+              const unsigned w = grp::witness<KJ>(x, c, g, a + 1, A);
+              if (w == grp::kNone) {
+                drop(d);
+                dropped = true;
+                continue;
+              }
+              if (lead) wit[d] = (uint8_t)w;
+            }
+            ++d;
+          }
+          if (dropped) {
+            rebuild();
+          } else {
+            W = 0;
+            for (unsigned d = 0; d < dcnt; ++d) {
+              const unsigned w = wit[d];
+              if (w != grp::kNone) W |= 1ull << w;
+            }
+          }
+        }
+      } else {  // ---- Op::Rm -> apply_keyset_rm (:318-348)
+        const u64x2 h2 = *reinterpret_cast<const u64x2 *>(hdr + 6 * i + 4);
+        const u64 kb = h2[0], ke = h2[1];
+        for (u64 jk = kb; jk < ke; ++jk) {
+          const unsigned long long kk = p.keys[jk];
+          if (kk >= K) {
+            st |= 2u;
+            continue;
+          }
+          gkey_rm<KJ>(p, s, kk, oc, g, lane);
+        }
+        const unsigned wr = grp::witness<KJ>(oc, c, g, 0, A);
+        if (wr == grp::kNone) continue;  // rm <= clock: not deferred (:336-345)
+        int slot = -1;
+        for (unsigned d = 0; d < dcnt; ++d) {
+          if (wit[d] != wr) continue;
+          u64 x[KJ];
+          grp::load_row<KJ>(x, DC + d * A, g, A);
+          if (grp::rows_eq<KJ>(x, oc, lane)) {
+            slot = (int)d;
+            break;
+          }
+        }
+        if (slot < 0) {
+          if (dcnt >= Dcap) {
+            st |= 1u;
+            continue;
+          }
+          slot = (int)dcnt++;
+          grp::store_row<KJ>(DC + (unsigned long long)slot * A, oc, g, A);
+          for (unsigned long long x = g; x < Kw; x += kG) DK[slot * Kw + x] = 0;
+          if (lead) wit[slot] = (uint8_t)wr;
+          W |= 1ull << wr;
+        }
+        for (u64 jk = kb; jk < ke; ++jk) {
+          const unsigned long long kk = p.keys[jk];
+          if (kk >= K) continue;
+          if (lead) DK[slot * Kw + kk / 64] |= 1ull << (kk % 64);
+          bloom |= 1ull << (kk % 64);
+        }
+      }
+    }
+  }
+  grp::store_row<KJ>(Cg, c, g, A);
+  if (lead) {
+    p.def_count[s] = dcnt;
+    p.status[s] = st;
+  }
+}
+
 }  // namespace crdt
 
 using namespace crdt;
@@ -482,6 +816,19 @@ extern "C" int crdt_map_apply_batch(crdt_ctx *ctx, const crdt_map_states *m, uin
                  (const u64 *)ops->val, ops->clk_row, (const u64 *)ops->clk_pool, ops->n_clk_rows,
                  (const u64 *)ops->key_off, ops->keys, ops->keys ? ops->n_keys : 0, ops->n_ops, status, wpb, Dh,
                  ctx->tune.apply_fence};
+  if (ctx->tune.apply_lane && A <= (size_t)kWave && Dcap <= 2048) {
+    // 16 lanes per state: kBlock / 16 states per block (KJ = ceil(A / 16) clock words per lane)
+    const size_t per_block = kBlock / grp::kG;
+    const dim3 g2((unsigned)((N + per_block - 1) / per_block)), b2(kBlock);
+    const size_t lds2 = per_block * (6 * grp::kG * 8 + Dcap);
+    timing_begin(ctx, "map_apply");
+    if (A <= 16) hipLaunchKernelGGL(map_apply_grp_kernel<1>, g2, b2, lds2, ctx->stream, p);
+    else if (A <= 32) hipLaunchKernelGGL(map_apply_grp_kernel<2>, g2, b2, lds2, ctx->stream, p);
+    else hipLaunchKernelGGL(map_apply_grp_kernel<4>, g2, b2, lds2, ctx->stream, p);
+    timing_end(ctx);
+    CRDT_HIP(ctx, hipGetLastError());
+    return CRDT_OK;
+  }
   const unsigned long long want = (N + wpb - 1) / wpb;
   const unsigned long long cap = (unsigned long long)ctx->cu_count * 64;
   timing_begin(ctx, "map_apply");

@@ -23,6 +23,7 @@
 // member row, as the reference does, instead of assuming the invariant the reference's own
 // states keep).
 #include "common.hpp"
+#include "group.hpp"
 
 namespace crdt {
 
@@ -417,51 +418,21 @@ __global__ __launch_bounds__(kBlock) void orswot_apply_kernel_a256(OrswotApplyPl
 //  * identical clocks (HashMap keyed by VClock): the witness is a function of the clock (at the
 //    current C), so a Rm's clock is compared in full only with slots of the same witness.
 // Exact for ANY input state (the first Add re-forgets every input slot's members in full).
-constexpr int kG = 16;                // lanes per state
-constexpr unsigned kGMask = kG == 32 ? 0xFFFFFFFFu : (1u << kG) - 1;
-constexpr int kJ = kWave / kG;        // actors per lane (A <= 64)
-constexpr unsigned kNoWitness = 0xFFu;
+constexpr int kG = grp::kG;            // lanes per state (group.hpp)
+constexpr unsigned kGMask = grp::kMask;
+constexpr int kJ = kWave / kG;         // actors per lane (A <= 64)
+constexpr unsigned kNoWitness = grp::kNone;
 
-__device__ __forceinline__ unsigned grp_bits(u64 ballot, int lane) { return (unsigned)(ballot >> (lane & ~(kG - 1))) & kGMask; }
-__device__ __forceinline__ bool grp_any(bool x, int lane) { return grp_bits(__ballot(x), lane) != 0; }
-__device__ __forceinline__ bool grp_all(bool x, int lane) { return grp_bits(__ballot(x), lane) == kGMask; }
-// min over the 16 lanes of a DPP row: xor 1, xor 2 (quad_perm), then the mirrors within 8 and 16
-// lanes pair every lane with one of the other half — VALU moves, no LDS round trip
-__device__ __forceinline__ unsigned grp_min(unsigned x) {
-  static_assert(kG == 16, "DPP row reduction");
-  unsigned y = (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
-  x = y < x ? y : x;
-  y = (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
-  x = y < x ? y : x;
-  y = (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0x141, 0xF, 0xF, false);  // row_half_mirror
-  x = y < x ? y : x;
-  y = (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0x140, 0xF, 0xF, false);  // row_mirror
-  return y < x ? y : x;
-}
-__device__ __forceinline__ u64 grp_or(u64 x) {
-#pragma unroll
-  for (int o = 1; o < kG; o <<= 1) x |= __shfl_xor(x, o);
-  return x;
-}
-
-// The group's first actor a >= from with x[a] > c[a] (kNoWitness if none); lane g holds a = g + kG*j.
+__device__ __forceinline__ unsigned grp_bits(u64 ballot, int lane) { return grp::bits(ballot, lane); }
+__device__ __forceinline__ bool grp_any(bool x, int lane) { return grp::any(x, lane); }
+__device__ __forceinline__ bool grp_all(bool x, int lane) { return grp::all(x, lane); }
+__device__ __forceinline__ u64 grp_or(u64 x) { return grp::orx(x); }
 __device__ __forceinline__ unsigned grp_witness(const u64 (&x)[kJ], const u64 (&c)[kJ], int g, unsigned from,
                                                 unsigned long long A) {
-  unsigned f = kNoWitness;
-#pragma unroll
-  for (int j = kJ - 1; j >= 0; --j) {
-    const unsigned a = g + kG * j;
-    if (a < A && a >= from && x[j] > c[j]) f = a;
-  }
-  return grp_min(f);
+  return grp::witness<kJ>(x, c, g, from, A);
 }
-
 __device__ __forceinline__ void grp_load_row(u64 (&x)[kJ], const u64 *row, int g, unsigned long long A) {
-#pragma unroll
-  for (int j = 0; j < kJ; ++j) {
-    const unsigned a = g + kG * j;
-    x[j] = a < A ? row[a] : 0;
-  }
+  grp::load_row<kJ>(x, row, g, A);
 }
 
 // forget a member row by the rm clock in registers: keep e[a] iff e[a] > rm[a]

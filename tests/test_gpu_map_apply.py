@@ -17,6 +17,18 @@ pytestmark = pytest.mark.gpu
 import crdts_gpu as cg  # noqa: E402
 
 
+@pytest.fixture(scope="module", params=["alane=1", "alane=0"])
+def mactx(request):
+    """Both kernels: 16 lanes per state (alane=1, the default for A <= 64) and one wave per state
+    (alane=0, every A); shapes with A > 64 take the wave kernel in both modes."""
+    assert torch.cuda.is_available()
+    torch.cuda.set_device(0)
+    ctx = cg.Context(0)
+    ctx.tune(request.param)
+    yield ctx
+    ctx.close()
+
+
 
 
 
@@ -95,11 +107,11 @@ def gpu_apply(ctx, streams, K, A, V, Dcap):
 
 @pytest.mark.parametrize("seed,n_states,n_origins,K,n_ops", [
     (1, 48, 3, 6, 80), (2, 100, 5, 20, 150), (3, 16, 70, 40, 300), (4, 64, 2, 2, 120)])
-def test_map_apply_replay(gpu_ctx, seed, n_states, n_origins, K, n_ops):
+def test_map_apply_replay(mactx, seed, n_states, n_origins, K, n_ops):
     streams = replay_streams(seed, n_states, n_origins, K, n_ops)
     exp, peak = oracle_apply(streams)
     Dcap = max(1, max(sum(1 for o in s if isinstance(o, O.MapRm)) for s in streams))
-    got, status = gpu_apply(gpu_ctx, streams, K, n_origins, min(peak, 8), min(Dcap, 24))
+    got, status = gpu_apply(mactx, streams, K, n_origins, min(peak, 8), min(Dcap, 24))
     assert (status == 0).all(), status
     assert sum(len(m.deferred) for m in exp) > 0 or seed in (1, 4)
     for s, ((g, vc, vv, ec), e) in enumerate(zip(got, exp)):
@@ -112,20 +124,20 @@ def test_map_apply_replay(gpu_ctx, seed, n_states, n_origins, K, n_ops):
         assert not vc[~ec.any(axis=1)].any()
 
 
-def test_map_apply_value_overflow(gpu_ctx):
+def test_map_apply_value_overflow(mactx):
     # two concurrent writes to one key need 2 value slots
     a, b = O.Map(O.MVReg), O.Map(O.MVReg)
     op1 = a.update(0, a.get(0).derive_add_ctx(0), lambda r, c: r.write(11, c))
     op2 = b.update(0, b.get(0).derive_add_ctx(1), lambda r, c: r.write(22, c))
-    got, status = gpu_apply(gpu_ctx, [[op1, op2], [op1]], 1, 2, 1, 1)
+    got, status = gpu_apply(mactx, [[op1, op2], [op1]], 1, 2, 1, 1)
     assert status[0] & 16 and status[1] == 0
     exp, _ = oracle_apply([[op1, op2], [op1]])
     assert got[1][0].entries == exp[1].entries
-    got, status = gpu_apply(gpu_ctx, [[op1, op2]], 1, 2, 2, 1)
+    got, status = gpu_apply(mactx, [[op1, op2]], 1, 2, 2, 1)
     assert status[0] == 0 and got[0][0].entries == oracle_apply([[op1, op2]])[0][0].entries
 
 
-def test_map_apply_key_range_past_buffer(gpu_ctx):
+def test_map_apply_key_range_past_buffer(mactx):
     """An Rm whose key range runs past the n_keys entries of `keys` (or is reversed) is malformed
     (status bit 1) and skipped without reading past the buffer; the rest of the stream applies."""
     a = O.Map(O.MVReg)
@@ -143,7 +155,7 @@ def test_map_apply_key_range_past_buffer(gpu_ctx):
     n_keys = ops.keys.shape[0]
     ops.key_off[2] = n_keys + 4096     # state 0's Rm (op 1): range far past keys
     ops.key_off[5] = n_keys + 1        # state 1's Rm (op 4, the last op): one past the end
-    status = cg.map.apply_batch(clock, ec, vclk, vval, dcl, dks, cnt, ops, ctx=gpu_ctx).cpu().numpy()
+    status = cg.map.apply_batch(clock, ec, vclk, vval, dcl, dks, cnt, ops, ctx=mactx).cpu().numpy()
     torch.cuda.synchronize()
     assert status.tolist() == [2, 2]
     exp, _ = oracle_apply([[up, up2], [up]])
@@ -157,7 +169,7 @@ def test_map_apply_key_range_past_buffer(gpu_ctx):
 @pytest.mark.parametrize("N,T,K,A,V", [(256, 64, 16, 8, 4), (64, 100, 70, 33, 6), (48, 80, 24, 100, 8),
                                        (32, 80, 20, 200, 8), (257, 64, 16, 32, 4), (130, 70, 30, 16, 4),
                                        (99, 64, 20, 17, 4)])
-def test_map_apply_synth_streams(gpu_ctx, N, T, K, A, V):
+def test_map_apply_synth_streams(mactx, N, T, K, A, V):
     """The bench's device-generated streams (crdts_gpu.synth.map_op_streams) vs the oracle."""
     b = cg.synth.map_op_streams(N, T, K, A, seed=N + K, device="cuda:0")
     h = {f: getattr(b, f).cpu().numpy() for f in b._fields}
@@ -173,7 +185,7 @@ def test_map_apply_synth_streams(gpu_ctx, N, T, K, A, V):
         streams.append(ops)
     exp, peak = oracle_apply(streams)
     assert peak <= V
-    got, status = gpu_apply(gpu_ctx, streams, K, A, V, 16)
+    got, status = gpu_apply(mactx, streams, K, A, V, 16)
     assert (status == 0).all()
     assert sum(len(m.deferred) for m in exp) > 0
     for s, ((g, _, _, _), e) in enumerate(zip(got, exp)):
@@ -185,7 +197,7 @@ def test_map_apply_deferred_spill(hot):
     """Deferred slots beyond the LDS-resident ones live in the state's own HBM slots (CRDT_TUNE
     mhot=N): the same results with none, one or three slots in LDS."""
     ctx = cg.Context(0)
-    ctx.tune(f"mhot={hot}")
+    ctx.tune(f"mhot={hot},alane=0")  # (LDS-resident slots: the wave-per-state kernel)
     try:
         streams = replay_streams(20 + hot, 40, 5, 20, 200, rm_heavy=True)
         exp, peak = oracle_apply(streams)
@@ -221,7 +233,7 @@ def test_map_apply_wide_deferred_list():
 
 
 @pytest.mark.parametrize("seed", [0, 1, 2])
-def test_map_apply_unapplied_input_deferred(gpu_ctx, seed):
+def test_map_apply_unapplied_input_deferred(mactx, seed):
     """Input states whose deferred removes were never applied to their rows (the reference's own
     states always hold them applied): the first apply_deferred must re-forget every key of every
     slot, later ones only the updated key (map_apply.hip's restricted pass).  Long Up streams on
@@ -281,7 +293,7 @@ def test_map_apply_unapplied_input_deferred(gpu_ctx, seed):
     t = [dev(x) for x in (clock, ec, vclk, vval, dcl, dks)]
     tc = torch.from_numpy(cnt).to("cuda:0")
     ops = cg.map.encode_ops([[op_tuple(o) for o in s] for s in streams], A, "cuda:0")
-    status = cg.map.apply_batch(*t, tc, ops, ctx=gpu_ctx).cpu().numpy()
+    status = cg.map.apply_batch(*t, tc, ops, ctx=mactx).cpu().numpy()
     torch.cuda.synchronize()
     assert not (status & ~16).any(), sorted(set(status.tolist()))
     c, e, vc, vv = (to_host(x) for x in t[:4])
