@@ -1099,6 +1099,115 @@ __global__ __launch_bounds__(kBlock) void map_ingest_walk_kernel(MapWirePlan p) 
   }
 }
 
+// ---- Orswot ingest, round 3: walk + batched parse (pass 1) ----------------------------------------
+// The same two roles as map_ingest_walk_kernel: the walk reads only the member ids and record counts
+// (a readlane from the frame window the LDS ring holds), every 64 entries found the lanes parse one
+// entry each — member lookup (binary search in the LDS dictionary), then its records straight into
+// the zero-filled entry row.  Pass 3 (the deferred removes) is unchanged.
+__device__ __forceinline__ bool walk_parse_members(const uint32_t *fw, const uint32_t *actors, unsigned long long A,
+                                                   const u64 *members, unsigned long long M, int lane, int cnt,
+                                                   unsigned long long pos, unsigned long long n, u64 id, u64 *ent) {
+  if (lane >= cnt) return false;
+  const long long mi = find_u64(members, M, id, M);
+  if (mi < 0) return true;
+  return walk_parse(fw, actors, A, lane, cnt, pos, n, ent + (unsigned long long)mi * A);
+}
+
+__global__ __launch_bounds__(kBlock) void orswot_ingest_walk_kernel(IngestPlan p) {
+  extern __shared__ u64 lds[];
+  const int lane = threadIdx.x % kWave, wib = threadIdx.x / kWave;
+  const int wpb = blockDim.x / kWave;
+  const uint32_t *actors = p.actors;
+  const u64 *elems = p.elems, *members = p.members;
+  u64 *mine = stage_dicts(p, lds, actors, elems, members) + (unsigned long long)wib * (kWalkRing * kWalkWin / 2);
+  uint32_t *ring = reinterpret_cast<uint32_t *>(mine);
+  for (unsigned long long s = (unsigned long long)blockIdx.x * wpb + wib; s < p.N;
+       s += (unsigned long long)gridDim.x * wpb) {
+    unsigned st = 0;
+    u64 dpos = 0, dcnt = 0;
+    u64 *crow = p.out + s * p.row_stride;
+    for (unsigned long long a = lane; a < p.A; a += kWave) crow[a] = 0;
+    const u64 b = p.frame_off[s], e = p.frame_off[s + 1];
+    if ((b & 3) || (e & 3) || e < b || e - b < 16) {
+      st = kWireBad;  // (a valid frame holds at least the clock and entry counts)
+    } else {
+      MapWalk w;
+      w.fw = reinterpret_cast<const uint32_t *>(p.bytes + b);
+      w.nw = (e - b) / 4;
+      w.nwin = (w.nw + kWalkWin - 1) / kWalkWin;
+      w.ring = ring;
+      w.start(lane);
+      u64 *ent = p.entries + s * p.M * p.A;
+      int cnt = 0;  // the batch the lanes parse next: lane i holds entry i
+      unsigned long long bpos = 0, bn = 0;
+      u64 bid = 0;
+      bool miss = false;
+      auto clock_len = [&](unsigned long long k) -> unsigned long long {
+        if (k + 2 > w.nw) return ~0ull;
+        const u64 n = w.get64(k, lane);
+        return n > (w.nw - k - 2) / 3 ? ~0ull : n;
+      };
+      unsigned long long k = 0;
+      unsigned long long n = clock_len(0);
+      if (n == ~0ull) {
+        st |= kWireBad;
+        k = ~0ull;
+      } else {
+        miss |= walk_parse(w.fw, actors, p.A, lane, 1, 0, n, crow);
+        k = 2 + 3 * n;
+      }
+      if (k != ~0ull && k + 2 > w.nw) {
+        st |= kWireBad;
+        k = ~0ull;
+      }
+      const u64 ne = k == ~0ull ? 0 : w.get64(k, lane);
+      if (k != ~0ull) k += 2;
+      for (u64 en = 0; en < ne && k != ~0ull; ++en) {
+        if (k + 2 > w.nw) {
+          st |= kWireBad;
+          k = ~0ull;
+          break;
+        }
+        const u64 id = w.get64(k, lane);
+        n = clock_len(k + 2);
+        if (n == ~0ull) {
+          st |= kWireBad;
+          k = ~0ull;
+          break;
+        }
+        if (lane == cnt) {
+          bpos = k + 2;
+          bn = n;
+          bid = id;
+        }
+        if (++cnt == kWave) {
+          miss |= walk_parse_members(w.fw, actors, p.A, members, p.M, lane, cnt, bpos, bn, bid, ent);
+          cnt = 0;
+        }
+        k += 4 + 3 * n;
+      }
+      if (cnt) miss |= walk_parse_members(w.fw, actors, p.A, members, p.M, lane, cnt, bpos, bn, bid, ent);
+      if (__ballot(miss)) st |= kWireMissing;
+      if (k != ~0ull && k + 2 <= w.nw) {
+        dcnt = w.get64(k, lane);
+        dpos = k + 2;
+        if (dcnt > (w.nw - dpos) / 4) {  // a lying count (see orswot_ingest_kernel)
+          st |= kWireBad;
+          dcnt = 0;
+        }
+      } else {
+        st |= kWireBad;
+      }
+      wire_vmcnt<0>();  // no DMA of this frame may land in the ring after the next state starts
+    }
+    if (lane == 0) {
+      p.status[s] = st;
+      p.dpos[s] = dpos;
+      p.dcount[s] = (st & kWireBad) ? 0 : dcnt;
+    }
+  }
+}
+
 // Egress, count (write = 0: frame sizes) or write pass: clock; present keys ascending with their
 // occupied value slots in slot (Vec) order; the state's deferred slots.
 __global__ __launch_bounds__(kBlock) void map_egress_kernel(MapWirePlan p, int write) {
@@ -1450,7 +1559,20 @@ int crdt_orswot_ingest(crdt_ctx *ctx, const uint8_t *bytes, const uint64_t *fram
   if ((dw + wpb * (A + Mw)) * 8 <= 64 * 1024) p.dict_words = dw;
   const unsigned grid = wave_grid(ctx, N, wpb, 32);
   timing_begin(ctx, "wire_ingest");
-  hipLaunchKernelGGL(orswot_ingest_kernel, dim3(grid), dim3(wpb * kWave), (p.dict_words + wpb * A) * 8, ctx->stream, p);
+  // pass 1: walk + batched parse (wwalk=1, default), the dictionaries in LDS when they fit 128 KiB
+  // beside four 8-KiB frame rings; else the one-chain kernel
+  const size_t ring_w = (size_t)kWalkRing * kWalkWin / 2;
+  const size_t walk_lds = (dw + 4 * ring_w) * 8;
+  if (ctx->tune.wire_walk && walk_lds <= 128 * 1024) {
+    IngestPlan q = p;
+    q.dict_words = dw;
+    CRDT_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void *>(&orswot_ingest_walk_kernel),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)walk_lds));
+    hipLaunchKernelGGL(orswot_ingest_walk_kernel, dim3(wave_grid(ctx, N, 4, 32)), dim3(4 * kWave), walk_lds,
+                       ctx->stream, q);
+  } else {
+    hipLaunchKernelGGL(orswot_ingest_kernel, dim3(grid), dim3(wpb * kWave), (p.dict_words + wpb * A) * 8, ctx->stream, p);
+  }
   CRDT_HIP(ctx, hipGetLastError());
   unsigned long long D = 0;
   if (int rc = exclusive_scan(ctx, dcount, (u64 *)def_off, N, sc, &D)) return rc;
