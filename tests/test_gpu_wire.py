@@ -108,6 +108,14 @@ def test_pncounter_gset_lwwreg_round_trip(gpu_ctx):
     assert bytes(edata.cpu().numpy().tobytes()) == blob
 
 
+@pytest.fixture(params=[1, 0], ids=["walk", "chain"])
+def octx(request, gpu_ctx):
+    """Both Orswot ingest pass-1 kernels: the walk + batched parse (default) and the per-state chain."""
+    gpu_ctx.tune(f"wwalk={request.param}")
+    yield gpu_ctx
+    gpu_ctx.tune("wwalk=1")
+
+
 def orswot_objects(seed, R, M, A):
     """gen_orswot replicas as (clock, entries, deferred) dicts over dense indices."""
     clock, entries, off, dcl, dmem = O.gen_orswot(seed, R, M, A, kmax=12, p_def=0.5)
@@ -134,14 +142,14 @@ def orswot_blob(states, aids, mids, rng):
 
 
 @pytest.mark.parametrize("R,M,A", [(40, 90, 9), (12, 70, 64), (10, 40, 65), (8, 30, 1)])
-def test_orswot_ingest_egress(gpu_ctx, R, M, A):
+def test_orswot_ingest_egress(octx, R, M, A):
     """A <= 64 takes the batched lane-per-actor egress, A > 64 the generic row loop."""
     rng = np.random.default_rng(11 + A)
     states, (clock, entries, off, dcl, dmem) = orswot_objects(3, R, M, A)
     aids, ad = actor_dict(rng, A)
     mids, md = u64_dict(rng, M)
     blob, foff = orswot_blob(states, aids, mids, rng)
-    res = wire.orswot_ingest(dev_bytes(blob), dev_off(foff), ad, md, ctx=gpu_ctx)
+    res = wire.orswot_ingest(dev_bytes(blob), dev_off(foff), ad, md, ctx=octx)
     assert (res.status.cpu().numpy() == 0).all()
     np.testing.assert_array_equal(to_host(res.clock), clock)
     np.testing.assert_array_equal(to_host(res.entries), entries)
@@ -156,7 +164,7 @@ def test_orswot_ingest_egress(gpu_ctx, R, M, A):
     assert int(doff[-1]) > 0
     # egress of the ingested states decodes to the same objects
     eoff, edata = wire.orswot_egress(res.clock, res.entries, ad, md, res.def_off, res.def_clock, res.def_members,
-                                     ctx=gpu_ctx)
+                                     ctx=octx)
     for r, fr in enumerate(host_frames(edata, eoff)):
         c, e, d, pos = O.unbc_orswot(fr)
         assert pos == len(fr)
@@ -166,7 +174,7 @@ def test_orswot_ingest_egress(gpu_ctx, R, M, A):
         assert d == {tuple(sorted((int(aids[a]), v) for a, v in k)): {int(mids[m]) for m in ms} for k, ms in d0.items()}
 
 
-def test_end_to_end_orswot_fold_through_bytes(gpu_ctx):
+def test_end_to_end_orswot_fold_through_bytes(octx):
     """R serialized replicas -> ingest -> lub_many -> egress -> decode == the oracle fold."""
     rng = np.random.default_rng(12)
     R, M, A = 64, 120, 16
@@ -174,13 +182,13 @@ def test_end_to_end_orswot_fold_through_bytes(gpu_ctx):
     aids, ad = actor_dict(rng, A)
     mids, md = u64_dict(rng, M)
     blob, foff = orswot_blob(states, aids, mids, rng)
-    res = wire.orswot_ingest(dev_bytes(blob), dev_off(foff), ad, md, ctx=gpu_ctx)
+    res = wire.orswot_ingest(dev_bytes(blob), dev_off(foff), ad, md, ctx=octx)
     D = res.def_clock.shape[0]
     lub = cg.orswot.lub_many(res.clock, res.entries, def_off=[0, D], def_clock=res.def_clock,
-                             def_members=res.def_members, ctx=gpu_ctx)
+                             def_members=res.def_members, ctx=octx)
     one = torch.tensor([0, D], dtype=torch.int64, device="cuda")
     eoff, edata = wire.orswot_egress(lub.clock[None].contiguous(), lub.entries[None].contiguous(), ad, md, one,
-                                     res.def_clock, lub.def_members, lub.def_keep, ctx=gpu_ctx)
+                                     res.def_clock, lub.def_members, lub.def_keep, ctx=octx)
     c, e, d, pos = O.unbc_orswot(host_frames(edata, eoff)[0])
     oc, oe, odef, _ = O.orswot_fold(*raw)
     assert c == {int(aids[a]): int(v) for a, v in enumerate(oc) if v}
@@ -227,7 +235,7 @@ def test_malformed_frames_and_missing_ids(gpu_ctx):
     assert st.cpu().tolist() == [1, 1]
 
 
-def test_orswot_lying_deferred_count_only_breaks_its_frame(gpu_ctx):
+def test_orswot_lying_deferred_count_only_breaks_its_frame(octx):
     """a frame whose deferred-remove count is far larger than its bytes could hold must be
     malformed on its own (status bit 0, no removes), not shift / wrap the pooled def_off of every
     later state or make the wrapper allocate a (count, A) buffer."""
@@ -250,7 +258,7 @@ def test_orswot_lying_deferred_count_only_breaks_its_frame(gpu_ctx):
     parts = [bytes(frames[0]), lying, bytes(frames[1])]
     blob2 = b"".join(parts)
     off = np.cumsum([0] + [len(x) for x in parts]).tolist()
-    res = wire.orswot_ingest(dev_bytes(blob2), dev_off(off), ad, md, ctx=gpu_ctx)
+    res = wire.orswot_ingest(dev_bytes(blob2), dev_off(off), ad, md, ctx=octx)
     assert res.status.cpu().tolist()[1] & 1 and res.status.cpu().tolist()[0] == 0 and res.status.cpu().tolist()[2] == 0
     doff = res.def_off.cpu().numpy()
     n0, n1 = len(states[0][2]), len(states[1][2])
@@ -487,3 +495,52 @@ def test_map_ingest_large_frames(walk):
     assert s[0] & wire.BAD and s[1] & wire.BAD and s[2] == 0
     for f in states._fields:
         assert torch.equal(getattr(st2, f)[2], getattr(states, f)[2]), f
+
+
+def test_orswot_malformed_frames(octx):
+    """Malformed Orswot frames set their own status bits and leave every other frame's rows exact:
+    a member or an actor missing from its dictionary (bit 1, the rest parsed), a truncated frame,
+    an entry count and a record count far past the frame (bit 0)."""
+    rng = np.random.default_rng(22)
+    R, M, A = 4, 40, 8
+    states, (clock, entries, off, dcl, dmem) = orswot_objects(7, R, M, A)
+    aids, ad = actor_dict(rng, A)
+    mids, md = u64_dict(rng, M)
+    blob, foff = orswot_blob(states, aids, mids, rng)
+    fo = [int(x) for x in foff]
+    good = [bytes(blob[fo[i]:fo[i + 1]]) for i in range(R)]
+    c0, e0, _ = states[0]
+    cl = {int(aids[a]): v for a, v in c0.items()}
+    ent = {int(mids[m]): {int(aids[a]): v for a, v in e.items()} for m, e in e0.items()}
+    m_any = next(iter(ent))
+    bad_member = dict(ent)
+    bad_member[int(mids.max()) + 1] = {int(aids[0]): 1}            # not in the member dictionary
+    bad_actor = dict(ent)
+    bad_actor[m_any] = {**ent[m_any], int(aids.max()) + 1: 3}      # an actor outside the dictionary
+    fr_member = O.bc_orswot(cl, bad_member, [])
+    fr_actor = O.bc_orswot(cl, bad_actor, [])
+    truncated = good[1][:-4]
+    # the entry count sits right after the clock: u64 n + n x (u32, u64)
+    ck = 8 + 12 * len(states[2][0])
+    lying_ne = good[2][:ck] + (1 << 40).to_bytes(8, "little") + good[2][ck + 8:]
+    # the first entry's record count (after its u64 member id) far past the frame
+    ck3 = 8 + 12 * len(states[3][0])
+    lying_n = good[3][:ck3 + 16] + (1 << 40).to_bytes(8, "little") + good[3][ck3 + 24:] if states[3][1] else None
+    parts = [good[0], fr_member, fr_actor, truncated, lying_ne] + ([lying_n] if lying_n else []) + [good[3]]
+    blob2 = b"".join(parts)
+    off2 = np.cumsum([0] + [len(x) for x in parts]).tolist()
+    res = wire.orswot_ingest(dev_bytes(blob2), dev_off(off2), ad, md, ctx=octx)
+    st = res.status.cpu().tolist()
+    assert st[0] == 0 and st[-1] == 0
+    assert st[1] == 2 and st[2] == 2               # missing ids: reported, the rest parsed
+    assert st[3] & 1 and st[4] & 1                  # truncated, lying entry count
+    if lying_n:
+        assert st[5] & 1
+    ce, ee = to_host(res.clock), to_host(res.entries)
+    np.testing.assert_array_equal(ce[0], clock[0])
+    np.testing.assert_array_equal(ee[0], entries[0])
+    np.testing.assert_array_equal(ce[-1], clock[3])
+    np.testing.assert_array_equal(ee[-1], entries[3])
+    for i in (1, 2):  # the parsed part of the frames with a missing id
+        np.testing.assert_array_equal(ce[i], clock[0])
+        np.testing.assert_array_equal(ee[i], entries[0])
