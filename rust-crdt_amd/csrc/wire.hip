@@ -840,6 +840,14 @@ __device__ __forceinline__ void wire_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// A wave-uniform 64-bit value the compiler cannot prove uniform (the walk's positions): made so, so
+// that the walk's arithmetic and branches stay scalar instead of EXEC-masked vector code.
+__device__ __forceinline__ unsigned long long uni64(unsigned long long x) {
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)x), hi = __builtin_amdgcn_readfirstlane((unsigned)(x >> 32));
+  return ((unsigned long long)hi << 32) | lo;
+}
+
+template <int RING = kWalkRing>
 struct MapWalk {
   const uint32_t *fw;
   unsigned long long nw, nwin, issued, cur;
@@ -847,7 +855,7 @@ struct MapWalk {
   uint32_t r0, r1, r2, r3;
 
   __device__ void dma(unsigned long long wi, int lane) {
-    uint32_t *dst = ring + (wi % kWalkRing) * kWalkWin;
+    uint32_t *dst = ring + (wi % RING) * kWalkWin;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const unsigned long long w = wi * kWalkWin + 64 * j + lane;
@@ -856,9 +864,14 @@ struct MapWalk {
     }
   }
   __device__ void start(int lane) {
+    nw = uni64(nw);
+    nwin = uni64(nwin);
     issued = 0;
     cur = ~0ull;
-    while (issued < nwin && issued < (unsigned long long)kWalkRing) dma(issued++, lane);
+    while (issued < nwin && issued < (unsigned long long)RING) {
+      dma(issued, lane);
+      issued = uni64(issued + 1);
+    }
   }
   // window wi into registers (wi > cur); then keep the ring full
   __device__ void load(unsigned long long wi, int lane) {
@@ -874,25 +887,28 @@ struct MapWalk {
       case 6: wire_vmcnt<24>(); break;
       default: wire_vmcnt<28>(); break;
     }
-    const uint32_t *src = ring + (wi % kWalkRing) * kWalkWin + lane;
+    const uint32_t *src = ring + (wi % RING) * kWalkWin + lane;
     r0 = src[0];
     r1 = src[64];
     r2 = src[128];
     r3 = src[192];
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot is read: it may be refilled
-    cur = wi;
-    while (issued < nwin && issued <= wi + kWalkRing) dma(issued++, lane);
+    cur = uni64(wi);
+    while (issued < nwin && issued <= wi + RING) {
+      dma(issued, lane);
+      issued = uni64(issued + 1);
+    }
   }
   __device__ uint32_t get(unsigned long long k, int lane) {
+    k = uni64(k);
     const unsigned long long wi = k / kWalkWin;
-    if (wi != cur) load(wi, lane);
-    const int off = (int)(k % kWalkWin), l = off & 63;
-    switch (off >> 6) {
-      case 0: return __builtin_amdgcn_readlane(r0, l);
-      case 1: return __builtin_amdgcn_readlane(r1, l);
-      case 2: return __builtin_amdgcn_readlane(r2, l);
-      default: return __builtin_amdgcn_readlane(r3, l);
-    }
+    if (wi != uni64(cur)) load(wi, lane);
+    const int off = (int)(k % kWalkWin), l = off & 63, q = off >> 6;
+    // four readlanes and scalar selects: a switch over r0..r3 may be lowered as an indexed access
+    // to a stack copy of them (scratch: a memory round trip per word read)
+    const uint32_t a = __builtin_amdgcn_readlane(r0, l), b = __builtin_amdgcn_readlane(r1, l);
+    const uint32_t c = __builtin_amdgcn_readlane(r2, l), d = __builtin_amdgcn_readlane(r3, l);
+    return q == 0 ? a : (q == 1 ? b : (q == 2 ? c : d));
   }
   __device__ u64 get64(unsigned long long k, int lane) { return (u64)get(k, lane) | ((u64)get(k + 1, lane) << 32); }
 };
@@ -954,7 +970,7 @@ __global__ __launch_bounds__(kBlock) void map_ingest_walk_kernel(MapWirePlan p) 
     if ((b & 3) || (e & 3) || e < b || e - b < 16) {
       st = kWireBad;  // (a valid frame holds at least the clock and entry counts)
     } else {
-      MapWalk w;
+      MapWalk<> w;
       w.fw = reinterpret_cast<const uint32_t *>(p.bytes + b);
       w.nw = (e - b) / 4;
       w.nwin = (w.nw + kWalkWin - 1) / kWalkWin;
@@ -988,8 +1004,9 @@ __global__ __launch_bounds__(kBlock) void map_ingest_walk_kernel(MapWirePlan p) 
         st |= kWireBad;
         k = ~0ull;
       } else {
+        n = uni64(n);
         push(0, n, p.clock + s * p.A);
-        k = 2 + 3 * n;
+        k = uni64(2 + 3 * n);
       }
       if (k != ~0ull && k + 2 > w.nw) {
         st |= kWireBad;
@@ -1007,32 +1024,32 @@ __global__ __launch_bounds__(kBlock) void map_ingest_walk_kernel(MapWirePlan p) 
         const long long ki = find_u32(keys, p.K, w.get(k, lane), (unsigned long long)hint);
         if (ki < 0) st |= kWireMissing;
         else hint = ki + 1;
-        n = clock_len(k + 1);
+        n = uni64(clock_len(k + 1));
         if (n == ~0ull) {
           st |= kWireBad;
           k = ~0ull;
           break;
         }
         if (ki >= 0) push(k + 1, n, p.ec + (s * p.K + (unsigned long long)ki) * p.A);
-        k += 3 + 3 * n;
+        k = uni64(k + 3 + 3 * n);
         if (k + 2 > w.nw) {
           st |= kWireBad;
           k = ~0ull;
           break;
         }
         const u64 m = w.get64(k, lane);
-        k += 2;
+        k = uni64(k + 2);
         for (u64 v = 0; v < m && k != ~0ull; ++v) {
-          n = clock_len(k);
+          n = uni64(clock_len(k));
           if (n == ~0ull || k + 2 + 3 * n + 2 > w.nw) {
             st |= kWireBad;
             k = ~0ull;
             break;
           }
           const unsigned long long pos = k;
-          k += 2 + 3 * n;
+          k = uni64(k + 2 + 3 * n);
           const u64 val = w.get64(k, lane);
-          k += 2;
+          k = uni64(k + 2);
           if (ki >= 0) {
             if (v < p.V) {
               const unsigned long long slot = (s * p.K + (unsigned long long)ki) * p.V + v;
@@ -1113,13 +1130,17 @@ __device__ __forceinline__ bool walk_parse_members(const uint32_t *fw, const uin
   return walk_parse(fw, actors, A, lane, cnt, pos, n, ent + (unsigned long long)mi * A);
 }
 
-__global__ __launch_bounds__(kBlock) void orswot_ingest_walk_kernel(IngestPlan p) {
+// 16 waves per block share one copy of the dictionaries, each with a 4-window frame ring: the walk is
+// a dependent scalar chain per state, so its speed is the states in flight per SIMD (4 here; 2 with
+// 4 waves per block and 8-window rings, which the 33-KiB member dictionary capped at 2 blocks/CU).
+constexpr int kOrWalkRing = 4, kOrWalkWaves = 16;
+__global__ __launch_bounds__(kOrWalkWaves * kWave) void orswot_ingest_walk_kernel(IngestPlan p) {
   extern __shared__ u64 lds[];
   const int lane = threadIdx.x % kWave, wib = threadIdx.x / kWave;
   const int wpb = blockDim.x / kWave;
   const uint32_t *actors = p.actors;
   const u64 *elems = p.elems, *members = p.members;
-  u64 *mine = stage_dicts(p, lds, actors, elems, members) + (unsigned long long)wib * (kWalkRing * kWalkWin / 2);
+  u64 *mine = stage_dicts(p, lds, actors, elems, members) + (unsigned long long)wib * (kOrWalkRing * kWalkWin / 2);
   uint32_t *ring = reinterpret_cast<uint32_t *>(mine);
   for (unsigned long long s = (unsigned long long)blockIdx.x * wpb + wib; s < p.N;
        s += (unsigned long long)gridDim.x * wpb) {
@@ -1131,13 +1152,21 @@ __global__ __launch_bounds__(kBlock) void orswot_ingest_walk_kernel(IngestPlan p
     if ((b & 3) || (e & 3) || e < b || e - b < 16) {
       st = kWireBad;  // (a valid frame holds at least the clock and entry counts)
     } else {
-      MapWalk w;
+      MapWalk<kOrWalkRing> w;
       w.fw = reinterpret_cast<const uint32_t *>(p.bytes + b);
       w.nw = (e - b) / 4;
       w.nwin = (w.nw + kWalkWin - 1) / kWalkWin;
       w.ring = ring;
       w.start(lane);
       u64 *ent = p.entries + s * p.M * p.A;
+#ifdef WIRE_STATS
+      u64 t_all = __builtin_amdgcn_s_memtime(), t_parse = 0, t0 = 0, n_ent = 0, n_win = 0;
+#define WS_T0() (t0 = __builtin_amdgcn_s_memtime())
+#define WS_T1() (t_parse += __builtin_amdgcn_s_memtime() - t0)
+#else
+#define WS_T0() ((void)0)
+#define WS_T1() ((void)0)
+#endif
       int cnt = 0;  // the batch the lanes parse next: lane i holds entry i
       unsigned long long bpos = 0, bn = 0;
       u64 bid = 0;
@@ -1175,18 +1204,29 @@ __global__ __launch_bounds__(kBlock) void orswot_ingest_walk_kernel(IngestPlan p
           k = ~0ull;
           break;
         }
+        n = uni64(n);
         if (lane == cnt) {
           bpos = k + 2;
           bn = n;
           bid = id;
         }
         if (++cnt == kWave) {
+          WS_T0();
           miss |= walk_parse_members(w.fw, actors, p.A, members, p.M, lane, cnt, bpos, bn, bid, ent);
+          WS_T1();
           cnt = 0;
         }
-        k += 4 + 3 * n;
+        k = uni64(k + 4 + 3 * n);
+#ifdef WIRE_STATS
+        ++n_ent;
+#endif
       }
       if (cnt) miss |= walk_parse_members(w.fw, actors, p.A, members, p.M, lane, cnt, bpos, bn, bid, ent);
+#ifdef WIRE_STATS
+      if (lane == 0 && s % 509 == 0)
+        printf("s=%llu entries=%llu windows=%llu cyc all=%llu parse=%llu\n", s, n_ent, w.nwin,
+               __builtin_amdgcn_s_memtime() - t_all, t_parse);
+#endif
       if (__ballot(miss)) st |= kWireMissing;
       if (k != ~0ull && k + 2 <= w.nw) {
         dcnt = w.get64(k, lane);
@@ -1559,17 +1599,17 @@ int crdt_orswot_ingest(crdt_ctx *ctx, const uint8_t *bytes, const uint64_t *fram
   if ((dw + wpb * (A + Mw)) * 8 <= 64 * 1024) p.dict_words = dw;
   const unsigned grid = wave_grid(ctx, N, wpb, 32);
   timing_begin(ctx, "wire_ingest");
-  // pass 1: walk + batched parse (wwalk=1, default), the dictionaries in LDS when they fit 128 KiB
-  // beside four 8-KiB frame rings; else the one-chain kernel
-  const size_t ring_w = (size_t)kWalkRing * kWalkWin / 2;
-  const size_t walk_lds = (dw + 4 * ring_w) * 8;
-  if (ctx->tune.wire_walk && walk_lds <= 128 * 1024) {
+  // pass 1: walk + batched parse (wwalk=1, default), the dictionaries in LDS when they fit beside
+  // sixteen 4-KiB frame rings; else the one-chain kernel
+  const size_t ring_w = (size_t)kOrWalkRing * kWalkWin / 2;
+  const size_t walk_lds = (dw + kOrWalkWaves * ring_w) * 8;
+  if (ctx->tune.wire_walk && walk_lds <= 160 * 1024) {
     IngestPlan q = p;
     q.dict_words = dw;
     CRDT_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void *>(&orswot_ingest_walk_kernel),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)walk_lds));
-    hipLaunchKernelGGL(orswot_ingest_walk_kernel, dim3(wave_grid(ctx, N, 4, 32)), dim3(4 * kWave), walk_lds,
-                       ctx->stream, q);
+    hipLaunchKernelGGL(orswot_ingest_walk_kernel, dim3(wave_grid(ctx, N, kOrWalkWaves, 8)),
+                       dim3(kOrWalkWaves * kWave), walk_lds, ctx->stream, q);
   } else {
     hipLaunchKernelGGL(orswot_ingest_kernel, dim3(grid), dim3(wpb * kWave), (p.dict_words + wpb * A) * 8, ctx->stream, p);
   }
