@@ -211,13 +211,26 @@ class Env:
                 print(f"rank {self.rank}: crdt_ctx_comm_init failed ({e}); using the torch.distributed exchange",
                       file=sys.stderr)
                 up = 0
+            if up:  # one small C-ABI exchange before the real ones: the result must be the global max
+                try:
+                    probe = torch.full((4, 8), self.rank + 1, dtype=torch.int64, device="cuda")
+                    got = cg.shard.lub_many_sharded("vclock", probe, ctx=self.ctx)
+                    torch.cuda.synchronize()
+                    if not bool((got == self.world).all()):
+                        raise RuntimeError(f"probe exchange returned {got.tolist()}, expected {self.world}")
+                except Exception as e:
+                    print(f"rank {self.rank}: C-ABI probe exchange failed ({e}); using the torch.distributed "
+                          "exchange", file=sys.stderr)
+                    up = 0
             flag = torch.tensor([up], dtype=torch.int64, device="cuda")
             cdist.all_reduce_(flag, dist.ReduceOp.MIN)
             if not int(flag.item()):
-                if up:
+                try:
                     cg.shard.comm_destroy(self.ctx)
+                except Exception:
+                    pass
                 self.cabi = False
-                self.exchange = "torch (C-ABI communicator setup failed)"
+                self.exchange = "torch (C-ABI communicator setup or probe exchange failed)"
         elif self.world > 1 and args.exchange == "cabi-ops":
             cg.shard.comm_init_ops(self.ctx, cg.shard.TorchCommOps(), self.world, self.rank)
 

@@ -2,7 +2,8 @@
 environment, the script launches its own 2-rank torch.distributed.run child (gloo: both ranks on
 GPU 0), and rank 0 prints one JSON line with n_gpus 2 and a config-5 block.  With --exchange
 cabi-ops the step's exchange is the C ABI's own sharded code (crdt_lub_many_multi_sharded,
-crdt_vclock_lub_many_sharded) over crdt_ctx_comm_init_ops host callbacks."""
+crdt_vclock_lub_many_sharded) over crdt_ctx_comm_init_ops host callbacks; with --exchange cabi the
+RCCL communicator cannot form on one GPU, and every rank falls back to the torch exchange together."""
 import json
 import os
 import subprocess
@@ -14,7 +15,7 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.mark.parametrize("exchange", ["torch", "cabi-ops"])
+@pytest.mark.parametrize("exchange", ["torch", "cabi-ops", "cabi"])
 def test_bench_self_launches_two_ranks(exchange):
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo", "--exchange",
@@ -30,3 +31,5 @@ def test_bench_self_launches_two_ranks(exchange):
     assert out["step_ms"]["min"] <= out["step_ms"]["median"] <= out["step_ms"]["max"]
     if exchange == "cabi-ops":
         assert "crdt_ctx_comm_init_ops" in out["config"]["exchange"]
+    if exchange == "cabi":  # RCCL refuses two ranks on one GPU: every rank takes the torch exchange together
+        assert "torch" in out["config"]["exchange"]
