@@ -191,7 +191,7 @@ int crdt_lwwreg_merge_batch(crdt_ctx *ctx, uint64_t *self_marker, uint64_t *self
  *                            (E = the member's dot clock; member absent <=> row all 0)
  *   deferred removes, pooled per group (CSR): group g owns d in [def_off[g], def_off[g+1]);
  *     rm clock  def_clock[d*A + a], member set bitmap def_members[d*Mw + w], Mw = ceil(M/64).
- *     def_off is a HOST array of G+1 entries.
+ *     def_off is a HOST array of G+1 entries (crdt_orswot_lub_many_doff below: a device one).
  * Output per group g: out_clock[g*A + a], out_entries[g*M*A + m*A + a] (packed), and for the
  * deferred pool: out_def_keep[d] = 1 iff d is the representative of a surviving deferred
  * remove (¬(rm ≤ final clock), first of its group with that exact clock), and
@@ -216,6 +216,16 @@ typedef struct crdt_orswot_out {
 } crdt_orswot_out;
 
 int crdt_orswot_lub_many(crdt_ctx *ctx, const crdt_orswot_batch *in, crdt_orswot_out *out);
+/* crdt_orswot_lub_many with the deferred pool's CSR offsets in DEVICE memory (a pool built on the
+ * GPU, e.g. by crdt_orswot_ingest, needs no host round trip): in->def_off must be NULL; def_off
+ * (device u64 [G+1], or NULL = no deferred removes) with def_off[G] == D, the pool length (the rows
+ * of def_clock / def_members, known to the caller from its own allocation).  The offsets are checked
+ * on the device: def_off[0] != 0, def_off[G] != D, an entry > D or a decreasing step set bit 0 of
+ * *status (device u32, written for every call; may be NULL) and the kernels then read the offsets
+ * clamped to [0, D] (in bounds; the results are unreliable).  Device-memory contexts only
+ * (CRDT_EUNSUPPORTED otherwise). */
+int crdt_orswot_lub_many_doff(crdt_ctx *ctx, const crdt_orswot_batch *in, const uint64_t *def_off, size_t D,
+                              crdt_orswot_out *out, uint32_t *status);
 
 /* Batched Orswot CmRDT::apply (orswot.rs:55-79 with apply_rm :230-250 and apply_deferred
  * :281-286): state s < N applies its ops [op_off[s], op_off[s+1]) in order, in place.
@@ -470,8 +480,9 @@ int crdt_lwwreg_lub_many_sharded(crdt_ctx *ctx, const uint64_t *marker, const ui
  *                          s < V value slots of the key's MVReg in Vec order (slot empty <=>
  *                          clock row all 0; empty slots are skipped)
  *   deferred removes pooled per group (CSR): group g owns d in [def_off[g], def_off[g+1])
- *     (def_off a HOST array of G+1 entries), held by replica def_row[d] of the group (device
- *     u32, non-decreasing within the group, < R), rm clock def_clock[d*A + a], key bitmap
+ *     (def_off a HOST array of G+1 entries; crdt_map_lub_many_doff: device), held by replica
+ *     def_row[d] of the group (device u32, non-decreasing within the group, < R), rm clock
+ *     def_clock[d*A + a], key bitmap
  *     def_keys[d*Kw + w], Kw = ceil(K/64).
  * Output per group g (packed): clock[g*A + a], ec[(g*K + k)*A + a], value slots s < Vout:
  * vclk[((g*K + k)*Vout + s)*A + a], vval[(g*K + k)*Vout + s]; nval[g*K + k] = number of values
@@ -515,6 +526,13 @@ typedef struct crdt_map_out {
 } crdt_map_out;
 
 int crdt_map_lub_many(crdt_ctx *ctx, const crdt_map_batch *in, crdt_map_out *out);
+/* crdt_map_lub_many with the deferred pool's CSR offsets in DEVICE memory, as for
+ * crdt_orswot_lub_many_doff: in->def_off NULL, def_off device u64 [G+1] (or NULL) with
+ * def_off[G] == D.  An invalid entry i (checked on the device, as there) sets bit 1 of flags[i-1]
+ * and flags[i] (the groups whose range it bounds); the fold then reads the offsets clamped to
+ * [0, D].  Device-memory contexts only. */
+int crdt_map_lub_many_doff(crdt_ctx *ctx, const crdt_map_batch *in, const uint64_t *def_off, size_t D,
+                           crdt_map_out *out);
 
 /* Map<K, MVReg> sharded by KEYS: rank k holds keys [k0, k0 + in->K) of every
  * replica (the crdt_map_batch layout with K = its key count), every replica's clock and the group's

@@ -51,6 +51,7 @@ EXPORTS = (
     "crdt_lub_many_multi", "crdt_lub_many_multi_sharded", "crdt_map_ingest", "crdt_map_egress",
     "crdt_ctx_comm_init_ops", "crdt_ctx_comm_note",
     "crdt_mvreg_lub_many", "crdt_mvreg_merge_batch", "crdt_mvreg_apply_batch",
+    "crdt_orswot_lub_many_doff", "crdt_map_lub_many_doff",
 )
 
 
@@ -197,6 +198,8 @@ _SIGS = {
     "crdt_orswot_lub_many": ([P, ctypes.POINTER(OrswotBatch), ctypes.POINTER(OrswotOut)], ctypes.c_int),
     "crdt_orswot_apply_batch": ([P, ctypes.POINTER(OrswotStates), ctypes.POINTER(OrswotOps), P], ctypes.c_int),
     "crdt_map_lub_many": ([P, ctypes.POINTER(MapBatch), ctypes.POINTER(MapOut)], ctypes.c_int),
+    "crdt_orswot_lub_many_doff": ([P, ctypes.POINTER(OrswotBatch), P, S, ctypes.POINTER(OrswotOut), P], ctypes.c_int),
+    "crdt_map_lub_many_doff": ([P, ctypes.POINTER(MapBatch), P, S, ctypes.POINTER(MapOut)], ctypes.c_int),
     "crdt_vclock_pair_op": ([P, ctypes.c_int, P, P, P, S, S, S, S, S], ctypes.c_int),
     "crdt_vclock_partial_cmp": ([P, P, P, S, S, S, S, P], ctypes.c_int),
     "crdt_vclock_cmp_matrix": ([P, P, S, S, S, P], ctypes.c_int),

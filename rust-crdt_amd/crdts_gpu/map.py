@@ -7,7 +7,8 @@ Dense layout (keys, actors and MVReg values interned to indices / u64 by the cal
     vclk  (R, K, V, A)  or (G, R, K, V, A)   MVReg value clocks, slots in Vec order (empty <=> 0)
     vval  (R, K, V)     or (G, R, K, V)      MVReg values
     deferred removes pooled per group:
-        def_off   host sequence of G+1 offsets (group g owns [def_off[g], def_off[g+1]))
+        def_off   host sequence of G+1 offsets (group g owns [def_off[g], def_off[g+1])), or a
+                  (G+1,) int64 device tensor (crdt_map_lub_many_doff: D = def_clock.shape[0], no host sync)
         def_row   (D,) device int32: replica index within the group (non-decreasing per group)
         def_clock (D, A) rm clocks; def_keys (D, ceil(K/64)) key bitmaps
 
@@ -15,13 +16,14 @@ lub_many computes, per group, the exact left fold `acc = Map::new(); for r: acc.
 (test/map.rs:660-692 merges this way) and returns MapLub(clock (G,A), ec (G,K,A),
 vclk (G,K,Vout,A), vval (G,K,Vout), nval (G,K) int32, flags (G,) int32, def_keep, def_keys).
 With check=True (default) a flagged group raises: bit 0 = more than `vout` values on a key
-(retry with a larger vout), bit 1 = def_row not sorted / out of range; bit 2 (the fold state
+(retry with a larger vout), bit 1 = def_row not sorted / out of range (or, for device def_off, the
+offsets bounding the group invalid); bit 2 (the fold state
 ran out of value slots mid-fold) first reruns the fold with the largest state (8 values).
 """
 from __future__ import annotations
 
 import ctypes
-from typing import NamedTuple, Optional, Sequence
+from typing import NamedTuple, Optional
 
 import numpy as np
 import torch
@@ -46,7 +48,7 @@ class MapCapacityError(RuntimeError):
 
 
 def lub_many(clock: torch.Tensor, ec: torch.Tensor, vclk: torch.Tensor, vval: torch.Tensor,
-             def_off: Optional[Sequence[int]] = None, def_row: Optional[torch.Tensor] = None,
+             def_off=None, def_row: Optional[torch.Tensor] = None,
              def_clock: Optional[torch.Tensor] = None, def_keys: Optional[torch.Tensor] = None,
              vout: int = 4, ctx: Optional[Context] = None, check: bool = True,
              vstate: int = 0, _key_shard: Optional[tuple] = None) -> MapLub:
@@ -94,11 +96,22 @@ def lub_many(clock: torch.Tensor, ec: torch.Tensor, vclk: torch.Tensor, vval: to
     o.nval, o.flags = nval.data_ptr(), flags.data_ptr()
     keep = keys_out = None
     off_arr = None
+    dev_off = isinstance(def_off, torch.Tensor) and def_off.device.type == "cuda"
+    if dev_off:
+        if _key_shard is not None:
+            raise ValueError("map.lub_many: a device def_off is not supported for a key-sharded fold")
+        if (def_off.dtype not in (torch.int64, torch.uint64) or tuple(def_off.shape) != (G + 1,)
+                or not def_off.is_contiguous() or def_off.device.index != ctx.device):
+            raise ValueError(f"map.lub_many: a device def_off must be a contiguous ({G + 1},) int64 "
+                             f"cuda:{ctx.device} tensor")
     if def_off is not None:
-        off = np.asarray(def_off, dtype=np.uint64)
-        if off.shape != (G + 1,):
-            raise ValueError(f"map.lub_many: def_off must have G+1 = {G + 1} entries")
-        D = int(off[-1])
+        if dev_off:
+            D = 0 if def_clock is None else int(def_clock.shape[0])
+        else:
+            off = np.asarray(def_off, dtype=np.uint64)
+            if off.shape != (G + 1,):
+                raise ValueError(f"map.lub_many: def_off must have G+1 = {G + 1} entries")
+            D = int(off[-1])
         if D > 0:
             for t, nm in ((def_clock, "def_clock"), (def_keys, "def_keys")):
                 if t is None:
@@ -112,13 +125,16 @@ def lub_many(clock: torch.Tensor, ec: torch.Tensor, vclk: torch.Tensor, vval: to
                 raise ValueError(f"map.lub_many: def_row {tuple(def_row.shape)} / def_clock "
                                  f"{tuple(def_clock.shape)} / def_keys {tuple(def_keys.shape)}; expected "
                                  f"({D},) / ({D},{A}) / ({D},{Kw})")
-            off_arr = (ctypes.c_size_t * (G + 1))(*[int(x) for x in off])
-            b.def_off = ctypes.cast(off_arr, ctypes.POINTER(ctypes.c_size_t))
+            if not dev_off:
+                off_arr = (ctypes.c_size_t * (G + 1))(*[int(x) for x in off])
+                b.def_off = ctypes.cast(off_arr, ctypes.POINTER(ctypes.c_size_t))
             b.def_row, b.def_clock, b.def_keys = def_row.data_ptr(), def_clock.data_ptr(), def_keys.data_ptr()
             keep = torch.empty(D, dtype=torch.uint8, device=dev)
             keys_out = torch.empty((D, Kw), dtype=torch.int64, device=dev)
             o.def_keep, o.def_keys = keep.data_ptr(), keys_out.data_ptr()
-    if _key_shard is None:
+    if dev_off:
+        ctx.call("crdt_map_lub_many_doff", ctypes.byref(b), def_off.data_ptr(), D, ctypes.byref(o))
+    elif _key_shard is None:
         ctx.call("crdt_map_lub_many", ctypes.byref(b), ctypes.byref(o))
     else:
         ctx.call("crdt_map_lub_many_sharded", ctypes.byref(b), int(_key_shard[0]), int(_key_shard[1]),
@@ -128,7 +144,8 @@ def lub_many(clock: torch.Tensor, ec: torch.Tensor, vclk: torch.Tensor, vval: to
         for x in flags.cpu().numpy().tolist():
             f |= int(x)
         if f & 2:
-            raise ValueError("map.lub_many: def_row must be non-decreasing within each group and < R")
+            raise ValueError("map.lub_many: def_row must be non-decreasing within each group and < R"
+                             + (" (or the device def_off is invalid)" if dev_off else ""))
         if f & 8:
             raise RuntimeError("map.lub_many: internal fault (shared clock-row ring wait timed out)")
         # the fold state overflowed: rerun with the next larger state (a key-sharded call already

@@ -4,7 +4,8 @@ Dense layout (members and actors interned to indices):
     clock   (R, A)    or (G, R, A)      replica clocks
     entries (R, M, A) or (G, R, M, A)   per-member dot clocks; member absent <=> row all 0
     deferred removes pooled per group as CSR:
-        def_off     host sequence of G+1 offsets (group g owns [def_off[g], def_off[g+1]))
+        def_off     host sequence of G+1 offsets (group g owns [def_off[g], def_off[g+1])), or a
+                    (G+1,) int64 device tensor (crdt_orswot_lub_many_doff: no host sync)
         def_clock   (D, A)   rm clocks
         def_members (D, ceil(M/64)) member bitmaps
 
@@ -16,7 +17,7 @@ survivors sharing that clock (orswot.rs:240-249).
 """
 from __future__ import annotations
 
-from typing import NamedTuple, Optional, Sequence
+from typing import NamedTuple, Optional
 
 import ctypes
 
@@ -34,10 +35,15 @@ class OrswotLub(NamedTuple):
     def_members: Optional[torch.Tensor]
 
 
-def lub_many(clock: torch.Tensor, entries: torch.Tensor, def_off: Optional[Sequence[int]] = None,
+def lub_many(clock: torch.Tensor, entries: torch.Tensor, def_off=None,
              def_clock: Optional[torch.Tensor] = None, def_members: Optional[torch.Tensor] = None,
-             ctx: Optional[Context] = None) -> OrswotLub:
+             ctx: Optional[Context] = None, def_status: Optional[torch.Tensor] = None) -> OrswotLub:
+    """def_off a device tensor: D = def_clock.shape[0] (no host read of the offsets); the offsets are
+    checked on the device into `def_status` ((1,) int32 device tensor, bit 0 = invalid offsets) when
+    one is given, else checked here (one sync) and a ValueError raised."""
     ctx = ctx or Context.default(clock.device.index)
+    if isinstance(def_off, torch.Tensor) and def_off.device.type == "cuda":
+        return _lub_many_doff(ctx, clock, entries, def_off, def_clock, def_members, def_status)
     ctx.check_tensor(clock, "orswot.lub_many(clock)")
     ctx.check_tensor(entries, "orswot.lub_many(entries)")
     squeeze = clock.dim() == 2
@@ -85,6 +91,61 @@ def lub_many(clock: torch.Tensor, entries: torch.Tensor, def_off: Optional[Seque
             members_out = torch.empty((D, Mw), dtype=clock.dtype, device=clock.device)
             o.def_keep, o.def_members = keep.data_ptr(), members_out.data_ptr()
     ctx.call("crdt_orswot_lub_many", ctypes.byref(b), ctypes.byref(o))
+    if squeeze:
+        return OrswotLub(out_clock[0], out_entries[0], keep, members_out)
+    return OrswotLub(out_clock, out_entries, keep, members_out)
+
+
+def _lub_many_doff(ctx, clock, entries, def_off, def_clock, def_members, def_status) -> OrswotLub:
+    squeeze = clock.dim() == 2
+    c = clock.unsqueeze(0) if squeeze else clock
+    e = entries.unsqueeze(0) if squeeze else entries
+    ctx.check_tensor(c, "orswot.lub_many(clock)")
+    ctx.check_tensor(e, "orswot.lub_many(entries)")
+    if c.dim() != 3 or e.dim() != 4 or c.stride(2) != 1 or e.stride(3) != 1:
+        raise ValueError("orswot.lub_many: clock (G,R,A) / entries (G,R,M,A) with the actor axis contiguous")
+    G, R, A = c.shape
+    M = e.shape[2]
+    if e.shape[0] != G or e.shape[1] != R or e.shape[3] != A:
+        raise ValueError(f"orswot.lub_many: entries {tuple(e.shape)} do not match clock {tuple(c.shape)}")
+    Mw = (M + 63) // 64
+    if (def_off.dtype not in (torch.int64, torch.uint64) or tuple(def_off.shape) != (G + 1,)
+            or not def_off.is_contiguous() or def_off.device.index != ctx.device):
+        raise ValueError(f"orswot.lub_many: a device def_off must be a contiguous ({G + 1},) int64 cuda:{ctx.device} tensor")
+    D = 0 if def_clock is None else int(def_clock.shape[0])
+    b = _abi.OrswotBatch()
+    b.G, b.R, b.M, b.A = G, R, M, A
+    b.clock, b.clock_rstride, b.clock_gstride = c.data_ptr(), c.stride(1), c.stride(0)
+    b.entries = e.data_ptr()
+    b.entry_mstride, b.entry_rstride, b.entry_gstride = e.stride(2), e.stride(1), e.stride(0)
+    out_clock = torch.empty((G, A), dtype=clock.dtype, device=clock.device)
+    out_entries = torch.empty((G, M, A), dtype=clock.dtype, device=clock.device)
+    o = _abi.OrswotOut()
+    o.clock, o.entries = out_clock.data_ptr(), out_entries.data_ptr()
+    keep = members_out = None
+    if D > 0:
+        for t, nm in ((def_clock, "def_clock"), (def_members, "def_members")):
+            if t is None:
+                raise ValueError(f"orswot.lub_many: {nm} required with deferred removes")
+            ctx.check_tensor(t, f"orswot.lub_many({nm})")
+            if not t.is_contiguous():
+                raise ValueError(f"orswot.lub_many: {nm} must be contiguous")
+        if tuple(def_clock.shape) != (D, A) or tuple(def_members.shape) != (D, Mw):
+            raise ValueError(f"orswot.lub_many: def_clock {tuple(def_clock.shape)} / def_members "
+                             f"{tuple(def_members.shape)}; expected ({D},{A}) / ({D},{Mw})")
+        b.def_clock, b.def_members = def_clock.data_ptr(), def_members.data_ptr()
+        keep = torch.empty(D, dtype=torch.uint8, device=clock.device)
+        members_out = torch.empty((D, Mw), dtype=clock.dtype, device=clock.device)
+        o.def_keep, o.def_members = keep.data_ptr(), members_out.data_ptr()
+    st = def_status
+    if st is None:
+        st = torch.empty(1, dtype=torch.int32, device=clock.device)
+    elif st.dtype not in (torch.int32, torch.uint32) or st.numel() < 1 or st.device != clock.device:
+        raise ValueError("orswot.lub_many: def_status must be an int32 device tensor of >= 1 element")
+    ctx.call("crdt_orswot_lub_many_doff", ctypes.byref(b), def_off.data_ptr(), D, ctypes.byref(o), st.data_ptr())
+    if def_status is None and int(st.item()) & 1:
+        raise ValueError("orswot.lub_many: def_off invalid (def_off[0] != 0, decreasing, or def_off[G] != "
+                         "def_clock.shape[0])")
     if squeeze:
         return OrswotLub(out_clock[0], out_entries[0], keep, members_out)
     return OrswotLub(out_clock, out_entries, keep, members_out)

@@ -180,7 +180,15 @@ struct DefPlan {
   unsigned *trep;     // ... min survivor index per key
   unsigned long long tmask;
 };
-int launch_deferred(crdt_ctx *ctx, const size_t *host_def_off, DefPlan q);
+// The pool's CSR offsets come from the host (staged) or, with dev_def_off, from device memory
+// (checked and clamped on the device by stage_def_off_dev below; no host sync).
+int launch_deferred(crdt_ctx *ctx, const size_t *host_def_off, DefPlan q, const u64 *dev_def_off = nullptr,
+                    unsigned *status = nullptr);
+// dst[i] = src[i] clamped to [0, D] (dst[0] = 0, dst[G] = D), so every kernel that walks the
+// offsets stays inside the pool; an invalid entry i (i = 0: != 0, i = G: != D, else > D or below
+// entry i-1) ORs bit 0 into *status and bit 1 into flags[i-1] / flags[i] (each may be NULL).
+int stage_def_off_dev(crdt_ctx *ctx, const u64 *src, size_t *dst, size_t G, size_t D, unsigned *status,
+                      unsigned *flags);
 
 // Max / OR join on u64 lanes.
 enum class Op : int { Max = 0, Or = 1 };

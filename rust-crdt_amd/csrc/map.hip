@@ -2109,10 +2109,8 @@ static int map_vi(size_t V, size_t want) {
 
 static bool aligned16(const void *x) { return (reinterpret_cast<uintptr_t>(x) & 15) == 0; }
 
-extern "C" int crdt_map_lub_many(crdt_ctx *ctx, const crdt_map_batch *in, crdt_map_out *out) {
-  if (ctx && ctx->mem_kind == CRDT_MEM_HOST) return crdt::map_lub_many_host(ctx, in, out);
-  CRDT_CHECK_CTX(ctx);
-  if (!in || !out) return fail(ctx, CRDT_EINVAL, "map_lub_many: NULL batch/out");
+// doff: the device-offset variant's def_off (in->def_off is then NULL and Ddev the pool length)
+static int map_lub_impl(crdt_ctx *ctx, const crdt_map_batch *in, const u64 *doff, size_t Ddev, crdt_map_out *out) {
   const size_t G = in->G, R = in->R, K = in->K, A = in->A, V = in->V, Vout = out->Vout;
   if (G == 0 || K == 0 || A == 0) return CRDT_OK;
   if (!out->clock || !out->ec || !out->vclk || !out->vval || !out->flags)
@@ -2125,7 +2123,7 @@ extern "C" int crdt_map_lub_many(crdt_ctx *ctx, const crdt_map_batch *in, crdt_m
   if (Vout > 64) return fail(ctx, CRDT_EUNSUPPORTED, "map_lub_many: Vout = %zu > 64", Vout);
   if (G * K > 0x7fffffffULL) return fail(ctx, CRDT_EUNSUPPORTED, "map_lub_many: G*K too large");
   if (R > 0xfffffffeULL) return fail(ctx, CRDT_EUNSUPPORTED, "map_lub_many: R too large");
-  const size_t D = (in->def_off && G > 0) ? in->def_off[G] - in->def_off[0] : 0;
+  const size_t D = doff ? Ddev : (in->def_off && G > 0) ? in->def_off[G] - in->def_off[0] : 0;
   if (in->def_off && in->def_off[0] != 0) return fail(ctx, CRDT_EINVAL, "map_lub_many: def_off[0] must be 0");
   if (D > 0 && (!in->def_row || !in->def_clock || !in->def_keys || !out->def_keep || !out->def_keys))
     return fail(ctx, CRDT_EINVAL, "map_lub_many: deferred buffers missing");
@@ -2178,14 +2176,21 @@ extern "C" int crdt_map_lub_many(crdt_ctx *ctx, const crdt_map_batch *in, crdt_m
   const bool rs = glds && ctx->tune.map_rs && A <= 32;
   const unsigned gC = (!rs && ctx->tune.map_chunk == 8 && ctx->tune.map_ring == 4) ? 8 : 16;  // launch_map_glds
   // scratch: [def_off copy | chunk clock maxima]
-  const size_t off_b = D > 0 ? ((G + 1) * sizeof(size_t) + 255) / 256 * 256 : 0;
+  const size_t off_b = D > 0 || doff ? ((G + 1) * sizeof(size_t) + 255) / 256 * 256 : 0;
   if (glds) p.nch = (R + gC - 1) / gC;
   const size_t cm_b = glds ? G * p.nch * A * sizeof(u64) : 0;
   if (off_b + cm_b > 0)
     if (int rc = ensure_scratch(ctx, off_b + cm_b)) return rc;
+  if (doff && D == 0)  // no pool: only the offsets' check (every entry must be 0)
+    if (int rc = stage_def_off_dev(ctx, doff, (size_t *)ctx->scratch, G, 0, nullptr, out->flags)) return rc;
   if (D > 0) {
-    // the kernel walks def_off on the device: stage it (the caller's array may be freed)
-    if (int rc = stage_h2d(ctx, ctx->scratch, in->def_off, (G + 1) * sizeof(size_t))) return rc;
+    // the kernel walks def_off on the device: stage it (the caller's array may be freed), or check
+    // and clamp the caller's device offsets into the same place (flags bit 1 of a bad group)
+    if (doff) {
+      if (int rc = stage_def_off_dev(ctx, doff, (size_t *)ctx->scratch, G, D, nullptr, out->flags)) return rc;
+    } else if (int rc = stage_h2d(ctx, ctx->scratch, in->def_off, (G + 1) * sizeof(size_t))) {
+      return rc;
+    }
     p.def_off = reinterpret_cast<const size_t *>(ctx->scratch);
     p.def_row = in->def_row;
     p.def_clock = (const u64 *)in->def_clock;
@@ -2229,5 +2234,22 @@ extern "C" int crdt_map_lub_many(crdt_ctx *ctx, const crdt_map_batch *in, crdt_m
   q.apply_ceiling = 0;  // the fold kernel applied every remove at the right step
   q.out_keep = out->def_keep;
   q.out_members = (u64 *)out->def_keys;
-  return launch_deferred(ctx, in->def_off, q);
+  return launch_deferred(ctx, in->def_off, q, doff);
+}
+
+extern "C" int crdt_map_lub_many(crdt_ctx *ctx, const crdt_map_batch *in, crdt_map_out *out) {
+  if (ctx && ctx->mem_kind == CRDT_MEM_HOST) return crdt::map_lub_many_host(ctx, in, out);
+  CRDT_CHECK_CTX(ctx);
+  if (!in || !out) return fail(ctx, CRDT_EINVAL, "map_lub_many: NULL batch/out");
+  return map_lub_impl(ctx, in, nullptr, 0, out);
+}
+
+extern "C" int crdt_map_lub_many_doff(crdt_ctx *ctx, const crdt_map_batch *in, const uint64_t *def_off, size_t D,
+                                      crdt_map_out *out) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
+  CRDT_CHECK_CTX(ctx);
+  if (!in || !out) return fail(ctx, CRDT_EINVAL, "map_lub_many_doff: NULL batch/out");
+  if (in->def_off) return fail(ctx, CRDT_EINVAL, "map_lub_many_doff: in->def_off must be NULL");
+  if (!def_off && D) return fail(ctx, CRDT_EINVAL, "map_lub_many_doff: D > 0 without def_off");
+  return map_lub_impl(ctx, in, (const u64 *)def_off, D, out);
 }

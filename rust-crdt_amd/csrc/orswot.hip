@@ -313,9 +313,37 @@ __global__ __launch_bounds__(kBlock) void orswot_dedup_kernel(DefPlan p) {
 
 static bool al16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
+__global__ __launch_bounds__(kBlock) void def_off_check_kernel(const u64 *src, size_t *dst, unsigned long long G,
+                                                               unsigned long long D, unsigned *status,
+                                                               unsigned *flags) {
+  const unsigned long long i = (unsigned long long)blockIdx.x * kBlock + threadIdx.x;
+  if (i > G) return;
+  const u64 v = src[i];
+  bool bad = i == 0 ? v != 0 : (i == G ? v != D : v > D);
+  if (i > 0 && src[i - 1] > v) bad = true;
+  dst[i] = i == 0 ? 0 : (i == G ? D : (v > D ? D : v));
+  if (bad) {
+    if (status) atomicOr(status, 1u);
+    if (flags) {
+      if (i > 0) atomicOr(flags + i - 1, 2u);
+      if (i < G) atomicOr(flags + i, 2u);
+    }
+  }
+}
+
+int stage_def_off_dev(crdt_ctx *ctx, const u64 *src, size_t *dst, size_t G, size_t D, unsigned *status,
+                      unsigned *flags) {
+  const size_t n = G + 1;
+  hipLaunchKernelGGL(def_off_check_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                     ctx->stream, src, dst, (unsigned long long)G, (unsigned long long)D, status, flags);
+  CRDT_HIP(ctx, hipGetLastError());
+  return CRDT_OK;
+}
+
 // Survival, ceiling (optional) and dedup of a pooled deferred-remove list (shared by Orswot and
-// Map): stages the host def_off, fills the outputs, launches the two kernels.
-int launch_deferred(crdt_ctx *ctx, const size_t *host_def_off, DefPlan q) {
+// Map): stages def_off (from the host, or checked from device memory), fills the outputs,
+// launches the two kernels.
+int launch_deferred(crdt_ctx *ctx, const size_t *host_def_off, DefPlan q, const u64 *dev_def_off, unsigned *status) {
   const size_t G = q.G, D = q.D;
   // Deferred bookkeeping lives in its own ctx-owned region (plain hipMalloc, like scratch), so
   // the join's scratch, possibly still in flight, is untouched.
@@ -336,7 +364,9 @@ int launch_deferred(crdt_ctx *ctx, const size_t *host_def_off, DefPlan q) {
   if (int rc = device_fill(ctx, q.tkey, T * 8, 0)) return rc;
   if (int rc = device_fill(ctx, q.trep, T * 4, 0xFF)) return rc;
   if (int rc = device_fill(ctx, q.nsurv, 4, 0)) return rc;
-  {  // the caller's def_off may be freed on return: stage it through pinned ctx memory
+  if (dev_def_off) {  // device offsets: checked (status) and clamped on the device
+    if (int rc = stage_def_off_dev(ctx, dev_def_off, (size_t *)q.def_off, G, D, status, nullptr)) return rc;
+  } else {  // the caller's def_off may be freed on return: stage it through pinned ctx memory
     int rc = stage_h2d(ctx, (void *)q.def_off, host_def_off, off_b);
     if (rc) return rc;
   }
@@ -355,11 +385,9 @@ int launch_deferred(crdt_ctx *ctx, const size_t *host_def_off, DefPlan q) {
 
 using namespace crdt;
 
-extern "C" int crdt_orswot_lub_many(crdt_ctx *ctx, const crdt_orswot_batch *in,
-                                    crdt_orswot_out *out) {
-  if (ctx && ctx->mem_kind == CRDT_MEM_HOST) return crdt::orswot_lub_many_host(ctx, in, out);
-  CRDT_CHECK_CTX(ctx);
-  if (!in || !out) return fail(ctx, CRDT_EINVAL, "orswot_lub_many: NULL batch/out");
+// doff: the device-offset variant's def_off (in->def_off is then NULL and D the pool length)
+static int orswot_lub_impl(crdt_ctx *ctx, const crdt_orswot_batch *in, const u64 *doff, size_t Ddev,
+                           crdt_orswot_out *out, unsigned *status) {
   const size_t G = in->G, R = in->R, M = in->M, A = in->A;
   if (G == 0 || M == 0 || A == 0) return CRDT_OK;
   if (!out->clock || !out->entries) return fail(ctx, CRDT_EINVAL, "orswot_lub_many: NULL output");
@@ -370,7 +398,7 @@ extern "C" int crdt_orswot_lub_many(crdt_ctx *ctx, const crdt_orswot_batch *in,
   if (A > (1u << 20) || M > (1ull << 32))
     return fail(ctx, CRDT_EUNSUPPORTED, "orswot_lub_many: A or M too large");
   CRDT_HIP(ctx, hipSetDevice(ctx->device));
-  const size_t D = (in->def_off && G > 0) ? in->def_off[G] - in->def_off[0] : 0;
+  const size_t D = doff ? Ddev : (in->def_off && G > 0) ? in->def_off[G] - in->def_off[0] : 0;
   if (in->def_off && in->def_off[0] != 0)
     return fail(ctx, CRDT_EINVAL, "orswot_lub_many: def_off[0] must be 0");
   if (D > 0 && (!in->def_clock || !in->def_members || !out->def_keep || !out->def_members))
@@ -470,5 +498,33 @@ extern "C" int crdt_orswot_lub_many(crdt_ctx *ctx, const crdt_orswot_batch *in,
   q.apply_ceiling = 1;
   q.out_keep = out->def_keep;
   q.out_members = (u64 *)out->def_members;
-  return launch_deferred(ctx, in->def_off, q);
+  return launch_deferred(ctx, in->def_off, q, doff, status);
+}
+
+extern "C" int crdt_orswot_lub_many(crdt_ctx *ctx, const crdt_orswot_batch *in,
+                                    crdt_orswot_out *out) {
+  if (ctx && ctx->mem_kind == CRDT_MEM_HOST) return crdt::orswot_lub_many_host(ctx, in, out);
+  CRDT_CHECK_CTX(ctx);
+  if (!in || !out) return fail(ctx, CRDT_EINVAL, "orswot_lub_many: NULL batch/out");
+  return orswot_lub_impl(ctx, in, nullptr, 0, out, nullptr);
+}
+
+extern "C" int crdt_orswot_lub_many_doff(crdt_ctx *ctx, const crdt_orswot_batch *in, const uint64_t *def_off,
+                                         size_t D, crdt_orswot_out *out, uint32_t *status) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
+  CRDT_CHECK_CTX(ctx);
+  if (!in || !out) return fail(ctx, CRDT_EINVAL, "orswot_lub_many_doff: NULL batch/out");
+  if (in->def_off) return fail(ctx, CRDT_EINVAL, "orswot_lub_many_doff: in->def_off must be NULL");
+  if (!def_off && D) return fail(ctx, CRDT_EINVAL, "orswot_lub_many_doff: D > 0 without def_off");
+  if (in->G == 0 || in->M == 0 || in->A == 0) return CRDT_OK;
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  if (status)
+    if (int rc = device_fill(ctx, status, sizeof(uint32_t), 0)) return rc;
+  if (def_off && D == 0) {  // no pool: only the offsets' check (every entry must be 0)
+    if (int rc = ensure_dscratch(ctx, (in->G + 1) * sizeof(size_t))) return rc;
+    if (int rc = stage_def_off_dev(ctx, (const u64 *)def_off, (size_t *)ctx->dscratch, in->G, 0, status, nullptr))
+      return rc;
+    def_off = nullptr;
+  }
+  return orswot_lub_impl(ctx, in, (const u64 *)def_off, def_off ? D : 0, out, status);
 }
