@@ -226,6 +226,11 @@ static void apply_tune(crdt_ctx *ctx, const char *t) {
       else if (k == "stage_kb" && v >= 4) ctx->tune.stage_kb = v;
       else if (k == "mpreg" && v >= 0 && v <= 2) ctx->tune.map_pair_reg = v;
       else if (k == "prows" && (v == 64 || v == 128 || v == 256)) ctx->tune.pair_rows = v;
+      else if (k == "pur" && (v == 2 || v == 4 || v == 8)) ctx->tune.pair_ur = v;
+      else if (k == "pocc" && v >= 0 && v <= 8) ctx->tune.pair_occ = v;
+      else if (k == "mppl" && v >= 1 && v <= 64) ctx->tune.merge_ppl = v;
+      else if (k == "mpbpc" && v >= 1 && v <= 64) ctx->tune.map_pair_bpc = v;
+      else if (k == "mfbpc" && v >= 1 && v <= 64) ctx->tune.map_forget_bpc = v;
     }
     pos = end + 1;
   }

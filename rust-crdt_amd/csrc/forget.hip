@@ -180,10 +180,10 @@ __global__ __launch_bounds__(kBlock) void map_forget_kernel(MapForgetPlan p) {
 }
 
 // grid: workgroups per CU (CRDT_TUNE rows_blocks_per_cu, else 4), never more than the rows need
-static unsigned forget_grid(crdt_ctx *ctx, unsigned long long rows, int lr_log) {
+static unsigned forget_grid(crdt_ctx *ctx, unsigned long long rows, int lr_log, int dflt = 4) {
   const unsigned long long per_block = kBlock >> lr_log;
   const unsigned long long want = (rows + per_block - 1) / per_block;
-  const int bpc = ctx->tune.rows_blocks_per_cu > 0 ? ctx->tune.rows_blocks_per_cu : 4;
+  const int bpc = ctx->tune.rows_blocks_per_cu > 0 ? ctx->tune.rows_blocks_per_cu : dflt;
   const unsigned long long cap = (unsigned long long)ctx->cu_count * bpc;
   return (unsigned)(want < cap ? want : cap);
 }
@@ -367,7 +367,7 @@ extern "C" int crdt_map_forget_batch(crdt_ctx *ctx, const crdt_map_states *m, co
     // stay below 2^32 so `rb += step` can never wrap (a wrapped walk would never exit)
     int lr2 = 0;
     while (lr2 < 6 && (1ull << lr2) < A / 2) ++lr2;
-    const unsigned long long grid2 = forget_grid(ctx, (N * K + kU - 1) / kU, lr2);
+    const unsigned long long grid2 = forget_grid(ctx, (N * K + kU - 1) / kU, lr2, ctx->tune.map_forget_bpc);
     const unsigned long long step2 = grid2 * (kBlock / kWave) * (kWave >> lr2) * kU;
     const bool vec2 = A % 2 == 0 && A <= 2 * (size_t)kWave && V <= 4 && N * K + step2 <= (1ull << 32) &&
                       m->ec_stride % 2 == 0 && m->vclk_stride % 2 == 0 && y_stride % 2 == 0 && al16(m->ec) &&

@@ -499,7 +499,7 @@ int lattice_merge_batch(crdt_ctx *ctx, Op op, u64 *self, const u64 *other, size_
   const bool vec2 = W % 2 == 0 && (N == 1 || (self_stride % 2 == 0 && other_stride % 2 == 0)) &&
                     aligned16(self) && aligned16(other);
   if (vec2 && ctx->tune.merge_rows) {
-    const int lr_log = row_lr_log(W / 2);
+    const int lr_log = row_lr_log(W / 2, ctx->tune.merge_ppl);
     const unsigned long long rpb = 4ull * (kWave >> lr_log);
     const unsigned long long want = (N + rpb - 1) / rpb;
     const unsigned long long cap = (unsigned long long)ctx->cu_count * ctx->tune.merge_blocks_per_cu;

@@ -150,7 +150,7 @@ __device__ __forceinline__ u64 cell_join(u64 e1, u64 e2, u64 c1, u64 c2) {  // o
 // pieces (V = 2: 16-byte non-temporal accesses), 256 >> lp_log rows per pass.  Per block the
 // deferred removes of both sides are turned into hit masks in LDS (bit d of hit[g][row] = remove
 // 32g + d names that member); a cell with hits forgets by each hit remove's rm (global, L2).
-template <int V, int kPairRows>
+template <int V, int kPairRows, int kPairUR = kPairUR>
 __global__ __launch_bounds__(kBlock) void orswot_pair_join_kernel(OrswotPairPlan p) {
   __shared__ unsigned hit[kPairGroups][kPairRows];
   const unsigned long long s = blockIdx.x / p.mblocks;
@@ -912,8 +912,14 @@ extern "C" int crdt_orswot_merge_batch(crdt_ctx *ctx, const crdt_orswot_states *
                      N, M, A, Mw, mblocks, lp};
     timing_begin(ctx, "orswot_pair_join");
     const dim3 grid((unsigned)(N * mblocks));
-#define CRDT_PAIR_JOIN(VV, RR) hipLaunchKernelGGL((orswot_pair_join_kernel<VV, RR>), grid, dim3(kBlock), 0, ctx->stream, p)
-    if (v2) {
+    // pocc > 0: at most pocc workgroups per CU (dynamic LDS padding), fewer HBM requests in flight
+    const size_t pad = ctx->tune.pair_occ > 0 ? (size_t)(160 * 1024 / ctx->tune.pair_occ) - kPairGroups * rows * 4 - 256 : 0;
+#define CRDT_PAIR_JOIN(VV, RR) hipLaunchKernelGGL((orswot_pair_join_kernel<VV, RR>), grid, dim3(kBlock), pad, ctx->stream, p)
+    if (v2 && rows == 128 && ctx->tune.pair_ur == 2)
+      hipLaunchKernelGGL((orswot_pair_join_kernel<2, 128, 2>), grid, dim3(kBlock), pad, ctx->stream, p);
+    else if (v2 && rows == 128 && ctx->tune.pair_ur == 4)
+      hipLaunchKernelGGL((orswot_pair_join_kernel<2, 128, 4>), grid, dim3(kBlock), pad, ctx->stream, p);
+    else if (v2) {
       if (rows == 64) CRDT_PAIR_JOIN(2, 64);
       else if (rows == 256) CRDT_PAIR_JOIN(2, 256);
       else CRDT_PAIR_JOIN(2, 128);
@@ -967,7 +973,7 @@ extern "C" int crdt_map_merge_batch(crdt_ctx *ctx, const crdt_map_states *self, 
                   b.vval_stride, (const u64 *)self_def->clock, (const u64 *)self_def->keys, self_def->count,
                   self_def->Dcap, (const u64 *)other_def->clock, (const u64 *)other_def->keys,
                   other_def->Dcap ? other_def->count : nullptr, other_def->Dcap, status};
-    const unsigned grid = pair_grid(ctx, (unsigned long long)N * K, 16);
+    const unsigned grid = pair_grid(ctx, (unsigned long long)N * K, ctx->tune.map_pair_bpc);
     timing_begin(ctx, "map_pair_join");
     if (ctx->tune.map_pair_reg && a.V <= 4 && b.V <= 4) {  // register-resident rows (one load batch per key)
       if (A <= 16 && ctx->tune.map_pair_reg == 1)

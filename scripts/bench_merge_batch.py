@@ -24,6 +24,7 @@ ap.add_argument("--orswot-pairs", type=int, default=8192)
 ap.add_argument("--map-pairs", type=int, default=8192)
 ap.add_argument("--steps", type=int, default=5)
 ap.add_argument("--sample", type=int, default=4)
+ap.add_argument("--only", default="calib,orswot,map", help="comma list of: calib, orswot, map")
 args = ap.parse_args()
 torch.cuda.set_device(0)
 ctx = cg.Context(0)
@@ -170,8 +171,13 @@ def calib():
     torch.cuda.empty_cache()
 
 
-calib()
-good = orswot()
-torch.cuda.empty_cache()
-good = mapb() and good
+only = set(args.only.split(","))
+good = True
+if "calib" in only:
+    calib()
+if "orswot" in only:
+    good = orswot() and good
+    torch.cuda.empty_cache()
+if "map" in only:
+    good = mapb() and good
 sys.exit(0 if good else 3)
