@@ -78,7 +78,8 @@ struct Tune {
   int pair_occ = 1;            // ... cap on workgroups per CU (LDS padding; 0 = none): one workgroup
                                //     per CU keeps fewer HBM requests in flight, 69% -> 74-75% of 8 TB/s
   int map_forget_bpc = 1;      // Map forget, 16-byte kernel: workgroups per CU (1: 67% of 8 TB/s vs 64% at 4)
-  int map_pair_bpc = 16;       // Map merge_batch key pass: workgroups per CU (grid-stride over keys)
+  int map_pair_bpc = 64;       // Map merge_batch key pass: workgroups per CU (grid-stride over keys;
+                               //     latency-bound: 16 -> 64 is 64% -> 67-69% of 8 TB/s)
   int merge_ppl = 8;           // lattice merge_batch rows: 16-byte pieces per lane per row
   int stage_kb = 262144;       // CRDT_MEM_HOST: bytes per device chunk buffer (KiB; two buffers)
   int wire_walk = 1;           // Map ingest: walk + batched parse (0: one dependent chain per state)

@@ -229,7 +229,7 @@ static void apply_tune(crdt_ctx *ctx, const char *t) {
       else if (k == "pur" && (v == 2 || v == 4 || v == 8)) ctx->tune.pair_ur = v;
       else if (k == "pocc" && v >= 0 && v <= 8) ctx->tune.pair_occ = v;
       else if (k == "mppl" && v >= 1 && v <= 64) ctx->tune.merge_ppl = v;
-      else if (k == "mpbpc" && v >= 1 && v <= 64) ctx->tune.map_pair_bpc = v;
+      else if (k == "mpbpc" && v >= 1 && v <= 4096) ctx->tune.map_pair_bpc = v;
       else if (k == "mfbpc" && v >= 1 && v <= 64) ctx->tune.map_forget_bpc = v;
     }
     pos = end + 1;

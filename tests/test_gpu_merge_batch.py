@@ -51,13 +51,18 @@ def test_orswot_merge_batch_replay(gpu_ctx, seed, N, M, n_origins, n_ops):
     assert sum(len(g.deferred) for g in got) > 0 and sum(len(g.entries) for g in got) > 0
 
 
-@pytest.mark.parametrize("seed,N,M,A", [(11, 50, 40, 16), (12, 33, 9, 3), (13, 20, 200, 65)])
-def test_orswot_merge_batch_arbitrary(gpu_ctx, seed, N, M, A):
+@pytest.mark.parametrize("mode", ["", "pocc=0,prows=128"])
+@pytest.mark.parametrize("seed,N,M,A", [(11, 50, 40, 16), (12, 33, 9, 3), (13, 20, 200, 65), (14, 30, 300, 64)])
+def test_orswot_merge_batch_arbitrary(gpu_ctx, mode, seed, N, M, A):
     """Arbitrary states (deferred removes not dominated, entries beyond the clock after random
     ops): the pairwise kernel is exact without any invariant."""
+    ctx = gpu_ctx
+    if mode:
+        ctx = cg.Context(0)
+        ctx.tune(mode)
     states, streams = arbitrary_case(seed, 2 * N, M, A, max_ops=30)
     states = oracle_streams(states, streams)
-    orswot_check(gpu_ctx, states[:N], states[N:], M, A)
+    orswot_check(ctx, states[:N], states[N:], M, A)
 
 
 def test_orswot_merge_batch_capacity_and_invalid(gpu_ctx):
@@ -74,8 +79,18 @@ def test_orswot_merge_batch_capacity_and_invalid(gpu_ctx):
     assert got[0].clock == a.clock and len(got[0].deferred) == 1
 
 
-def test_orswot_merge_batch_wide(gpu_ctx):
+# pair-join launch forms: the default (one workgroup per CU, 256 member rows), round 2's (no cap,
+# 128 rows) and the other row counts / rows-in-flight variants (CRDT_TUNE pocc / prows / pur)
+PAIR_MODES = ["", "pocc=0,prows=128", "pocc=2,prows=64", "pocc=2,prows=128,pur=2", "pocc=1,prows=128,pur=4"]
+
+
+@pytest.mark.parametrize("mode", PAIR_MODES)
+def test_orswot_merge_batch_wide(gpu_ctx, mode):
     """A bandwidth-shaped batch (odd A: the 8-byte path; even A: 16-byte path) vs the oracle."""
+    ctx = gpu_ctx
+    if mode:
+        ctx = cg.Context(0)
+        ctx.tune(mode)
     for A in (63, 64):
         c, e, off, dcl, dmem = O.gen_orswot(A, 256, 300, A, kmax=20, p_def=0.4)
         states = []
@@ -89,7 +104,7 @@ def test_orswot_merge_batch_wide(gpu_ctx):
                 k = O.VClock({a: int(v) for a, v in enumerate(dcl[d]) if v})
                 o.deferred.setdefault(k, set()).update(O.bitmap_members(dmem[d]))
             states.append(o)
-        orswot_check(gpu_ctx, states[:128], states[128:], 300, A)
+        orswot_check(ctx, states[:128], states[128:], 300, A)
 
 
 # ---- Map<K, MVReg> ------------------------------------------------------------------------------
