@@ -75,6 +75,14 @@ def parse():
     return ap.parse_args()
 
 
+def kernel_source_sha():
+    """sha256 of the source of the bench's dominant kernel (lub_multi_kernel, csrc/lattice.hip): a
+    PMC traffic figure is reported only for the kernel source it was measured on."""
+    import hashlib
+    with open(os.path.join(ROOT, "rust-crdt_amd", "csrc", "lattice.hip"), "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
 def free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -211,6 +219,11 @@ class Env:
                 print(f"rank {self.rank}: crdt_ctx_comm_init failed ({e}); using the torch.distributed exchange",
                       file=sys.stderr)
                 up = 0
+            # every rank must be up before any rank enters the probe (a collective): a rank whose init
+            # failed would otherwise leave the others blocked in the probe's header all-gather
+            flag = torch.tensor([up], dtype=torch.int64, device="cuda")
+            cdist.all_reduce_(flag, dist.ReduceOp.MIN)
+            up = int(flag.item())
             if up:  # one small C-ABI exchange before the real ones: the result must be the global max
                 try:
                     probe = torch.full((4, 8), self.rank + 1, dtype=torch.int64, device="cuda")
@@ -301,9 +314,12 @@ def run_workload(args, env, workload):
     elapsed = time.perf_counter() - t0
     ctx.set_timing(False)
     kern_ms, launches = ctx.timing("lub_stream")
+    xch_ms, xch_n = ctx.timing("shard_exchange")  # C-ABI exchange collectives (HIP events, ctx stream)
+    agr_ms, agr_n = ctx.timing("shard_agree")     # C-ABI header agreement (host wall time per call)
     step_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
     step_ms = env.max_over_ranks(step_ms)
     elapsed = env.max_over_ranks([elapsed])[0]
+    xch_ms, agr_ms = env.max_over_ranks([xch_ms, agr_ms])
 
     # Parity (outside the timed region): unsigned max with torch ops; for N > 1 the exchanged
     # result must equal the max over every rank's torch reference (torch.distributed's own exchange)
@@ -323,12 +339,15 @@ def run_workload(args, env, workload):
     srt = sorted(step_ms)
     med = srt[len(srt) // 2] if len(srt) % 2 else 0.5 * (srt[len(srt) // 2 - 1] + srt[len(srt) // 2])
     name = (f"vclock lub {R}x{A} (config 5 shard)" if workload == "c5" else f"gcounter+pncounter lub {R}x{A}")
-    traffic = None
+    traffic, traffic_src = None, "not collected for this kernel source (profiles/collect.sh writes it)"
     try:
         with open(args.traffic_json) as f:
             tj = json.load(f)
-        if tj.get("workload") == name and tj.get("fused", False) == bool(fused):
+        if (tj.get("workload") == name and tj.get("fused", False) == bool(fused)
+                and tj.get("kernel_source_sha256") == kernel_source_sha()):
             traffic = tj.get("hbm_bytes_per_launch")
+            traffic_src = (f"{tj.get('source')}: rocprofv3 FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE per "
+                           "launch, separate --pmc passes, same kernel source (sha256 of csrc/lattice.hip)")
     except (OSError, ValueError):
         pass
     if env.cabi:
@@ -367,12 +386,20 @@ def run_workload(args, env, workload):
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
+            "traffic_source": traffic_src,
             "avg_launch_us": avg_launch_s * 1e6,
             "launches": launches,
             "algorithmic_bytes_per_launch": avg_launch_bytes,
         },
         "parity": "ok" if ok else "MISMATCH",
     }
+    if env.cabi:  # where a scaling loss goes: the exchange collectives and the per-call agreement
+        block["exchange"] = {
+            "exchange_ms_per_step": xch_ms / args.steps, "exchange_calls": xch_n,
+            "agree_ms_per_step": agr_ms / args.steps, "agree_calls": agr_n,
+            "source": "libcrdt_gpu timers, max over ranks: shard_exchange = HIP events around the exchange "
+                      "collectives on the ctx stream; shard_agree = host wall time of the validation-header "
+                      "all-gather of each sharded call (csrc/shard.hip)"}
     del lubs, outs, items
     torch.cuda.empty_cache()
     return block, A

@@ -180,11 +180,14 @@ int crdt_lwwreg_merge_batch(crdt_ctx *ctx, uint64_t *self_marker, uint64_t *self
 /* ---- Orswot<member, actor> ---------------------------------------------------------------
  * Replaces Orswot::merge (orswot.rs:81-149) incl. apply_rm (:230-250) and apply_deferred
  * (:281-286).
- * Precondition (the reference's own invariants, kept by every state its API builds): each dot is
- * unique to one replica and entry dots are covered by their replica's clock (E <= C).  Under them
- * the per-cell join is associative, and the kernels fold replica slices (and host-mode chunks) in
- * any grouping, exactly; states outside them (an arbitrary E > C) are not left-fold exact here
- * (crdt_orswot_merge_batch below is exact for ANY pair of states).
+ * Exact for ANY input states: the result is the left fold acc = Orswot::new(); for r in replicas
+ * { acc.merge(r) }, removes included.  On the reference's own invariants (entry dots covered by
+ * their replica's clock, E <= C, as every state its API builds) the per-cell join is associative
+ * and the kernels fold replica slices in any grouping; where an input cell has E > C (e.g. a
+ * deserialized state) the unit holding it is re-folded in replica order inside the same launch,
+ * and applying the deferred removes after the in-order join equals applying them at their own
+ * step.  The host-memory mode continues the fold chunk by chunk, the sharded form
+ * folds the ranks in rank order when any shard holds such a cell (below).
  * Dense layout per replica (g, r):
  *   clock   C[g][r][a]      at clock   + g*clock_gstride + r*clock_rstride + a
  *   entries E[g][r][m][a]   at entries + g*entry_gstride + r*entry_rstride + m*entry_mstride + a
@@ -387,7 +390,11 @@ int crdt_map_merge_batch(crdt_ctx *ctx, const crdt_map_states *self, const crdt_
  *   gset: local lub_many + ncclAllGather of the partial bitmaps + OR-fold of the world partials
  *   orswot: local join without deferred removes, ncclAllGather of the partial (clock, entries),
  *       all ranks' deferred removes gathered and pooled per group (rank order, then local order),
- *       re-merge of the world partials with every deferred remove (orswot.rs:141-147).  Output:
+ *       re-merge of the world partials with every deferred remove (orswot.rs:141-147).  If any
+ *       rank's shard holds an entry cell with E > C (flags gathered with the deferred counts), the
+ *       partials are not joined as a tree: rank k re-folds its shard starting from rank k-1's state,
+ *       one all-gather per step (W-1 extra exchanges), and the re-merge reads the last rank's state —
+ *       the left fold over the concatenated shards for any input.  Output:
  *       clock [G][A], entries [G][M][A], and the surviving deferred removes compacted: *ndef (host)
  *       = their number; the first min(*ndef, def_cap) are written as def_clock[d*A + a],
  *       def_members[d*Mw + w] (union over the survivors with that exact clock in the group) and

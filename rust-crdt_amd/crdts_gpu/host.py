@@ -185,8 +185,8 @@ def orswot_lub_many(clock: np.ndarray, entries: np.ndarray, def_off=None, def_cl
     """crdt_orswot_lub_many on host arrays: clock (G, R, A), entries (G, R, M, A) (or without G),
     deferred removes pooled per group (def_off G+1, def_clock (D, A), def_members (D, Mw)).  The
     library streams replica chunks through its stage buffers (the running join kept in HBM, the
-    deferred removes settled once against the final clock); exact for states with e <= c, the
-    precondition of every Orswot lub_many (include/crdt_gpu.h)."""
+    deferred removes settled once against the final clock); the reference's left fold for any
+    input states (include/crdt_gpu.h)."""
     ctx = ctx or HostContext.default()
     c = clock[None] if clock.ndim == 2 else clock
     e = entries[None] if entries.ndim == 3 else entries

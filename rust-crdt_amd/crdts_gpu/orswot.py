@@ -139,7 +139,7 @@ def _lub_many_doff(ctx, clock, entries, def_off, def_clock, def_members, def_sta
         o.def_keep, o.def_members = keep.data_ptr(), members_out.data_ptr()
     st = def_status
     if st is None:
-        st = torch.empty(1, dtype=torch.int32, device=clock.device)
+        st = torch.zeros(1, dtype=torch.int32, device=clock.device)
     elif st.dtype not in (torch.int32, torch.uint32) or st.numel() < 1 or st.device != clock.device:
         raise ValueError("orswot.lub_many: def_status must be an int32 device tensor of >= 1 element")
     ctx.call("crdt_orswot_lub_many_doff", ctypes.byref(b), def_off.data_ptr(), D, ctypes.byref(o), st.data_ptr())

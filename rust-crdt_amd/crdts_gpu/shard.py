@@ -247,10 +247,12 @@ def lwwreg_lub_many_sharded(marker: torch.Tensor, val: torch.Tensor, base: int, 
 
 def map_lub_many_sharded(clock: torch.Tensor, ec: torch.Tensor, vclk: torch.Tensor, vval: torch.Tensor, k0: int,
                          K: int, def_off=None, def_row=None, def_clock=None, def_keys=None, vout: int = 4,
-                         ctx: Optional[Context] = None):
+                         ctx: Optional[Context] = None, vstate: int = 0):
     """Key-sharded Map<K, MVReg> fold (crdt_map_lub_many_sharded): this rank's keys [k0, k0 + K_k) of
     every replica (ec (G, R, K_k, A), ...), every replica clock, the whole deferred list with key
-    bitmaps over all K keys.  Returns a map.MapLub of the rank's keys whose def_keys span all K."""
+    bitmaps over all K keys.  Returns a map.MapLub of the rank's keys whose def_keys span all K.
+    `vstate` (the starting fold-state size) is part of the agreed call: it must match on every rank."""
     from . import map as cmap
     return cmap.lub_many(clock, ec, vclk, vval, def_off=def_off, def_row=def_row, def_clock=def_clock,
-                         def_keys=def_keys, vout=vout, ctx=ctx, _key_shard=(int(k0), int(K)))
+                         def_keys=def_keys, vout=vout, ctx=ctx, vstate=vstate,
+                         _key_shard=(int(k0), int(K)))

@@ -80,6 +80,8 @@ struct Tune {
   int map_forget_bpc = 1;      // Map forget, 16-byte kernel: workgroups per CU (1: 67% of 8 TB/s vs 64% at 4)
   int map_pair_bpc = 64;       // Map merge_batch key pass: workgroups per CU (grid-stride over keys;
                                //     latency-bound: 16 -> 64 is 64% -> 67-69% of 8 TB/s)
+  int merge_flat = 1;          // lattice merge_batch of packed rows: workgroups per CU of the flat
+                               //     stream (0: the row-group kernels)
   int merge_ppl = 8;           // lattice merge_batch rows: 16-byte pieces per lane per row
   int stage_kb = 262144;       // CRDT_MEM_HOST: bytes per device chunk buffer (KiB; two buffers)
   int wire_walk = 1;           // Map ingest: walk + batched parse (0: one dependent chain per state)
@@ -167,6 +169,9 @@ int device_fill(crdt_ctx *ctx, void *dst, size_t bytes, unsigned char byte);
 // Bracket the dominant kernel of a call with events when timing is on.
 void timing_begin(crdt_ctx *ctx, const char *name);
 void timing_end(crdt_ctx *ctx);
+// Host wall time of a host-synchronous step (e.g. the sharded calls' header agreement), recorded
+// under `name` like a kernel timing when timing is on.
+void timing_add_host(crdt_ctx *ctx, const char *name, double ms);
 
 // Pooled deferred-remove list of a batch (Orswot members / Map keys): survival !(rm <= final
 // clock), optional ceiling forget on the joined entries, representative + set union of
@@ -244,6 +249,14 @@ int lww_lub_many_host(crdt_ctx *ctx, const u64 *marker, const u64 *val, size_t G
                       u64 *out_marker, u64 *out_val, u64 *first_conflict, unsigned flags);
 int lww_merge_batch_host(crdt_ctx *ctx, u64 *sm, u64 *sv, const u64 *om, const u64 *ov, size_t N, uint8_t *conflict);
 int orswot_lub_many_host(crdt_ctx *ctx, const crdt_orswot_batch *in, crdt_orswot_out *out);
+// Device-mode Orswot lub_many with a fold start (the left fold continues from init instead of the
+// empty Orswot; device [G][A] / [G][M][A] packed, or NULL) and per-group flags (device u32 [G],
+// zeroed by the call, bit 0 = some input cell had E > C; or NULL).  Used by the sharded fold.
+struct OrswotJoinExtra {
+  const u64 *init_clock = nullptr, *init_entries = nullptr;
+  unsigned *viol = nullptr;
+};
+int orswot_lub_many_ex(crdt_ctx *ctx, const crdt_orswot_batch *in, crdt_orswot_out *out, const OrswotJoinExtra &ex);
 int orswot_merge_batch_host(crdt_ctx *ctx, const crdt_orswot_states *self, const crdt_orswot_states *other,
                             uint32_t *status);
 int map_lub_many_host(crdt_ctx *ctx, const crdt_map_batch *in, crdt_map_out *out);

@@ -159,6 +159,13 @@ void timing_end(crdt_ctx *ctx) {
   (void)hipEventRecord(ctx->pending.back().stop, ctx->stream);
 }
 
+void timing_add_host(crdt_ctx *ctx, const char *name, double ms) {
+  if (!ctx->timing) return;
+  auto &t = ctx->timers[name];
+  t.total_ms += ms;
+  t.launches += 1;
+}
+
 static void drain_timings(crdt_ctx *ctx) {
   for (auto &p : ctx->pending) {
     (void)hipEventSynchronize(p.stop);
@@ -229,6 +236,7 @@ static void apply_tune(crdt_ctx *ctx, const char *t) {
       else if (k == "pur" && (v == 2 || v == 4 || v == 8)) ctx->tune.pair_ur = v;
       else if (k == "pocc" && v >= 0 && v <= 8) ctx->tune.pair_occ = v;
       else if (k == "mppl" && v >= 1 && v <= 64) ctx->tune.merge_ppl = v;
+      else if (k == "mflat" && v >= 0 && v <= 16) ctx->tune.merge_flat = v;
       else if (k == "mpbpc" && v >= 1 && v <= 4096) ctx->tune.map_pair_bpc = v;
       else if (k == "mfbpc" && v >= 1 && v <= 64) ctx->tune.map_forget_bpc = v;
     }

@@ -430,8 +430,9 @@ static int orswot_lub_host_body(crdt_ctx *ctx, const crdt_orswot_batch *in, crdt
 }
 
 // ---- Orswot: replica chunks streamed through the two device chunk buffers ---------------------------
-// The join without deferred removes is associative under the reference invariants (each dot unique,
-// e <= c: the precondition every lub_many of this library states), so the batch streams: chunk k's
+// The join without deferred removes is a left fold (exact for any input: a chunk holding a cell with
+// e > c is re-folded in replica order by the join kernel, behind the running join), so the batch
+// streams: chunk k's
 // replicas are copied (copy stream) into buffer k&1 behind slot 0 of every group, slot 0 holds the
 // running join of the chunks before (device-to-device from the accumulator, or zeros: the join's
 // identity), and the chunk is joined into the accumulator on the ctx stream while chunk k+1 copies.
@@ -923,6 +924,9 @@ static int map_lub_host_stream(crdt_ctx *ctx, const crdt_map_batch *in, crdt_map
   for (size_t g = 0; g < G; ++g) {
     uint32_t f = hf[g] & ~1u;
     for (size_t kk = 0; kk < K; ++kk) f |= nv[g * K + kk] > Vo ? 1u : 0u;
+    // a remove held by no replica (def_row >= R) was never pooled: flags bit 1, as the device fold
+    // reports it, never a silently dropped remove
+    if (in->def_off && dpos[g] != in->def_off[g + 1]) f |= 2u;
     out->flags[g] = f;
   }
   if (out->nval) std::memcpy(out->nval, nv.data(), G * K * 4);

@@ -293,6 +293,23 @@ __global__ __launch_bounds__(kBlock) void merge_rows_kernel(u64 *self, const u64
   }
 }
 
+// merge_batch of packed rows (both strides == W): one flat stream of 16-byte pieces, grid-stride,
+// 2 pieces per lane in flight at one workgroup per CU — the shape at which an in-place
+// read-self / read-other / write-self stream peaks on this part (scripts/micro/stream_rate.hip,
+// 75% vs 65-69% with more requests in flight).
+template <Op OP>
+__global__ __launch_bounds__(kBlock) void merge_flat_kernel(u64x2 *self, const u64x2 *other, unsigned long long n) {
+  const unsigned long long stride = (unsigned long long)gridDim.x * kBlock;
+  unsigned long long i = (unsigned long long)blockIdx.x * kBlock + threadIdx.x;
+  for (; i + stride < n; i += 2 * stride) {
+    const u64x2 a0 = __builtin_nontemporal_load(self + i), b0 = __builtin_nontemporal_load(other + i);
+    const u64x2 a1 = __builtin_nontemporal_load(self + i + stride), b1 = __builtin_nontemporal_load(other + i + stride);
+    __builtin_nontemporal_store(join2<OP>(a0, b0), self + i);
+    __builtin_nontemporal_store(join2<OP>(a1, b1), self + i + stride);
+  }
+  if (i < n) __builtin_nontemporal_store(join2<OP>(self[i], other[i]), self + i);
+}
+
 static bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 // Validation and launch geometry of one lub (no scratch yet).  launch = false: nothing to run
@@ -498,6 +515,23 @@ int lattice_merge_batch(crdt_ctx *ctx, Op op, u64 *self, const u64 *other, size_
   CRDT_HIP(ctx, hipSetDevice(ctx->device));
   const bool vec2 = W % 2 == 0 && (N == 1 || (self_stride % 2 == 0 && other_stride % 2 == 0)) &&
                     aligned16(self) && aligned16(other);
+  const bool packed = N == 1 || (self_stride == W && other_stride == W);
+  if (vec2 && packed && ctx->tune.merge_flat) {
+    const unsigned long long n = (unsigned long long)N * W / 2;  // 16-byte pieces
+    const unsigned long long want = (n + kBlock - 1) / kBlock;
+    const unsigned long long cap = (unsigned long long)ctx->cu_count * ctx->tune.merge_flat;
+    const unsigned grid = (unsigned)(want < cap ? want : cap);
+    timing_begin(ctx, "merge_pairs");
+    if (op == Op::Max)
+      hipLaunchKernelGGL(merge_flat_kernel<Op::Max>, dim3(grid), dim3(kBlock), 0, ctx->stream,
+                         reinterpret_cast<u64x2 *>(self), reinterpret_cast<const u64x2 *>(other), n);
+    else
+      hipLaunchKernelGGL(merge_flat_kernel<Op::Or>, dim3(grid), dim3(kBlock), 0, ctx->stream,
+                         reinterpret_cast<u64x2 *>(self), reinterpret_cast<const u64x2 *>(other), n);
+    timing_end(ctx);
+    CRDT_HIP(ctx, hipGetLastError());
+    return CRDT_OK;
+  }
   if (vec2 && ctx->tune.merge_rows) {
     const int lr_log = row_lr_log(W / 2, ctx->tune.merge_ppl);
     const unsigned long long rpb = 4ull * (kWave >> lr_log);

@@ -11,11 +11,19 @@
 //                             max(c1, c2) )               // self.clock.merge (:145)
 // One-sided members reduce to the same formula (:86-101 drop-if-dominated + forget, :124-136),
 // and a member is present iff some e != 0 (empty common clock => removed, :116-118).
-// Under the reference's invariants (each dot unique, e <= c) the join is associative, so
-// replicas are folded per thread, then slice partials are joined by the last-arriving block.
+// On cells with e <= c (the reference's invariant: entry dots covered by their replica's clock)
+// the join is associative (exhaustively checked on small counters), so replicas are folded per
+// thread, then slice partials are joined by the last-arriving block.  A cell with e > c (a
+// deserialized or hand-built state) breaks associativity: every block ORs "some input cell had
+// e > c" into its arrival counter and, if any slice of the unit saw one, the last arriver re-folds
+// the unit's cells over ALL replicas in replica order — the exact left fold for any input.
 // Deferred removes (rm, S) of every replica are then applied after the join: for m in S,
 // e = e > rm[a] ? e : 0 (forget); a deferred survives iff !(rm <= final clock) (:240-249);
-// survivors with identical rm clocks merge their member sets (:242-246).
+// survivors with identical rm clocks merge their member sets (:242-246).  Applying them after the
+// in-order join instead of at their own step is exact for any input: a forget commutes with every
+// later join (forget(join(forget(x), y)) == forget(join(x, y)) per cell), a remove once dominated by
+// the clock stays dominated, and a dominated remove's dots (<= rm <= c) never re-enter by the join
+// (tests/test_oracle_twins.py checks this against the reference fold on arbitrary states).
 #include "common.hpp"
 
 namespace crdt {
@@ -63,6 +71,9 @@ struct OrPlan {
   unsigned *cnt;   // [units]
   u64 *out_clock;  // [G][A]
   u64 *out_entries;  // [G][M][A]
+  const u64 *init_clock;    // optional fold start [G][A] (NULL: the empty Orswot)
+  const u64 *init_entries;  // ... [G][M][A] packed
+  unsigned *viol;           // optional [G]: bit 0 set where an input cell had e > c
 };
 
 // MPT member rows per thread (CRDT_TUNE ompt=4/8/16): a workgroup covers MB*MPT member rows of
@@ -88,16 +99,32 @@ __global__ __launch_bounds__(kBlock) void orswot_join_kernel(OrPlan p) {
   const size_t mbase = (size_t)mb * p.MB * kOrMPT + ml;
 
   VT e[kOrMPT], c;
-  c = VT(0);
-#pragma unroll
-  for (int j = 0; j < kOrMPT; ++j) e[j] = VT(0);
   bool mok[kOrMPT];
 #pragma unroll
   for (int j = 0; j < kOrMPT; ++j) mok[j] = active && (mbase + (size_t)j * p.MB) < p.M;
-
-  if (active) {
-    const unsigned long long rbeg = (unsigned long long)s * p.Rs;
-    const unsigned long long rend = min(p.R, rbeg + p.Rs);
+  bool viol = false;
+  auto gt = [](VT x, VT y) -> bool {
+    if constexpr (V == 2) return (x.x > y.x) | (x.y > y.y);
+    else return x > y;
+  };
+  // the fold start: the caller's state (slice 0 / the exact re-fold) or the empty Orswot; a start
+  // state with e > c is itself a reason to re-fold in order
+  auto start = [&](bool from_init) {
+    c = VT(0);
+#pragma unroll
+    for (int j = 0; j < kOrMPT; ++j) e[j] = VT(0);
+    if (!from_init || !p.init_clock || !active) return;
+    c = reinterpret_cast<const VT *>(p.init_clock + g * p.A)[col];
+    const VT *ie = reinterpret_cast<const VT *>(p.init_entries + g * p.M * p.A);
+#pragma unroll
+    for (int j = 0; j < kOrMPT; ++j)
+      if (mok[j]) {
+        e[j] = ie[(mbase + (size_t)j * p.MB) * (p.A / V) + col];
+        viol |= gt(e[j], c);
+      }
+  };
+  // in-order fold of replicas [rbeg, rend) into (e, c); viol |= some loaded cell had e > c
+  auto fold = [&](unsigned long long rbeg, unsigned long long rend) {
     const VT *cp = reinterpret_cast<const VT *>(p.clock + g * p.c_gstride + rbeg * p.c_rstride) + col;
     const VT *ep = reinterpret_cast<const VT *>(p.entries + g * p.e_gstride + rbeg * p.e_rstride +
                                                 mbase * p.e_mstride) + col;
@@ -118,7 +145,10 @@ __global__ __launch_bounds__(kBlock) void orswot_join_kernel(OrPlan p) {
 #pragma unroll
       for (int q = 0; q < UR; ++q) {
 #pragma unroll
-        for (int j = 0; j < kOrMPT; ++j) e[j] = dot_join(e[j], c, e2[q][j], c2[q]);
+        for (int j = 0; j < kOrMPT; ++j) {
+          viol |= gt(e2[q][j], c2[q]);
+          e[j] = dot_join(e[j], c, e2[q][j], c2[q]);
+        }
         c = umax(c, c2[q]);
       }
       cp += UR * cstep;
@@ -131,11 +161,20 @@ __global__ __launch_bounds__(kBlock) void orswot_join_kernel(OrPlan p) {
       for (int j = 0; j < kOrMPT; ++j)
         e2[j] = mok[j] ? __builtin_nontemporal_load(ep + j * mstep) : VT(0);
 #pragma unroll
-      for (int j = 0; j < kOrMPT; ++j) e[j] = dot_join(e[j], c, e2[j], c2);
+      for (int j = 0; j < kOrMPT; ++j) {
+        viol |= gt(e2[j], c2);
+        e[j] = dot_join(e[j], c, e2[j], c2);
+      }
       c = umax(c, c2);
       cp += cstep;
       ep += estep;
     }
+  };
+
+  start(s == 0);
+  if (active) {
+    const unsigned long long rbeg = (unsigned long long)s * p.Rs;
+    fold(rbeg, min(p.R, rbeg + p.Rs));
   }
 
   const size_t slab = (size_t)p.MB * kOrMPT * p.PW + p.PW;  // vectors
@@ -147,7 +186,8 @@ __global__ __launch_bounds__(kBlock) void orswot_join_kernel(OrPlan p) {
       if (mok[j]) oe[(mbase + (size_t)j * p.MB) * (p.A / V) + col] = e[j];
     if (mb == 0 && ml == 0) reinterpret_cast<VT *>(p.out_clock + g * p.A)[col] = c;
   };
-  if (p.S == 1) {
+  if (p.S == 1) {  // one slice: the in-order fold of every replica, exact for any input
+    if (p.viol && __syncthreads_or(viol) && l == 0) atomicOr(p.viol + g, 1u);
     store_final();
     return;
   }
@@ -157,24 +197,30 @@ __global__ __launch_bounds__(kBlock) void orswot_join_kernel(OrPlan p) {
     for (int j = 0; j < kOrMPT; ++j) part[(ml + j * p.MB) * p.PW + cl] = e[j];
     if (ml == 0) part[(size_t)p.MB * kOrMPT * p.PW + cl] = c;
   }
-  // Release this slab; the last slice of the unit joins all slabs (in slice order).
+  // Release this slab; the last slice of the unit joins all slabs (in slice order).  Bit 16 of the
+  // unit's arrival counter collects "a slice saw a cell with e > c" (S <= 64 fits below it).
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  const int bviol = __syncthreads_or(viol);
   if (l == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    unsigned t = __hip_atomic_fetch_add(p.cnt + u, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    int last = t == (unsigned)p.S - 1;
+    const unsigned t = __hip_atomic_fetch_add(p.cnt + u, bviol ? 0x10001u : 1u, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+    const int last = (t & 0xffffu) == (unsigned)p.S - 1;
     if (last) {
       __hip_atomic_store(p.cnt + u, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if ((bviol || (t >> 16)) && p.viol) atomicOr(p.viol + g, 1u);
     }
-    s_flag = last;
+    s_flag = last | ((bviol || (t >> 16)) ? 2 : 0);
   }
   __syncthreads();
-  if (!s_flag) return;
-  if (active) {
+  if (!(s_flag & 1)) return;
+  if (s_flag & 2) {  // some input cell of the unit had e > c: the exact in-order re-fold
+    start(true);
+    if (active) fold(0, p.R);
+  } else if (active) {
     c = VT(0);
 #pragma unroll
     for (int j = 0; j < kOrMPT; ++j) e[j] = VT(0);
@@ -387,11 +433,11 @@ using namespace crdt;
 
 // doff: the device-offset variant's def_off (in->def_off is then NULL and D the pool length)
 static int orswot_lub_impl(crdt_ctx *ctx, const crdt_orswot_batch *in, const u64 *doff, size_t Ddev,
-                           crdt_orswot_out *out, unsigned *status) {
+                           crdt_orswot_out *out, unsigned *status, const OrswotJoinExtra *ex = nullptr) {
   const size_t G = in->G, R = in->R, M = in->M, A = in->A;
-  if (G == 0 || M == 0 || A == 0) return CRDT_OK;
-  if (!out->clock || !out->entries) return fail(ctx, CRDT_EINVAL, "orswot_lub_many: NULL output");
-  if (R > 0 && (!in->clock || !in->entries))
+  if (G == 0 || A == 0) return CRDT_OK;
+  if (!out->clock || (M && !out->entries)) return fail(ctx, CRDT_EINVAL, "orswot_lub_many: NULL output");
+  if (R > 0 && (!in->clock || (M && !in->entries)))
     return fail(ctx, CRDT_EINVAL, "orswot_lub_many: NULL input");
   if (in->entry_mstride < A && M > 1)
     return fail(ctx, CRDT_EINVAL, "orswot_lub_many: entry_mstride < A");
@@ -401,20 +447,32 @@ static int orswot_lub_impl(crdt_ctx *ctx, const crdt_orswot_batch *in, const u64
   const size_t D = doff ? Ddev : (in->def_off && G > 0) ? in->def_off[G] - in->def_off[0] : 0;
   if (in->def_off && in->def_off[0] != 0)
     return fail(ctx, CRDT_EINVAL, "orswot_lub_many: def_off[0] must be 0");
-  if (D > 0 && (!in->def_clock || !in->def_members || !out->def_keep || !out->def_members))
+  const size_t Mw = (M + 63) / 64;
+  if (D > 0 && (!in->def_clock || !out->def_keep || (Mw && (!in->def_members || !out->def_members))))
     return fail(ctx, CRDT_EINVAL, "orswot_lub_many: deferred buffers missing");
   if (D > 0xffffffffULL) return fail(ctx, CRDT_EUNSUPPORTED, "orswot_lub_many: too many deferred");
-  const size_t Mw = (M + 63) / 64;
 
-  if (R == 0) {
+  if (ex && ex->viol)
+    if (int rc = device_fill(ctx, ex->viol, G * 4, 0)) return rc;
+  if (R == 0 && ex && ex->init_clock) {  // nothing to fold: the start state
+    CRDT_HIP(ctx, hipMemcpyAsync(out->clock, ex->init_clock, G * A * 8, hipMemcpyDeviceToDevice, ctx->stream));
+    if (M)
+      CRDT_HIP(ctx, hipMemcpyAsync(out->entries, ex->init_entries, G * M * A * 8, hipMemcpyDeviceToDevice,
+                                   ctx->stream));
+  } else if (R == 0) {
     int rc = device_fill(ctx, out->clock, G * A * 8, 0);
-    if (!rc) rc = device_fill(ctx, out->entries, G * M * A * 8, 0);
+    if (!rc && M) rc = device_fill(ctx, out->entries, G * M * A * 8, 0);
     if (rc) return rc;
+  } else if (M == 0) {  // no members: the state is its clock (plus the removes' survival below)
+    if (int rc = lattice_lub_many(ctx, Op::Max, (const u64 *)in->clock, G, R, A, in->clock_rstride,
+                                  in->clock_gstride, (u64 *)out->clock, A, 0))
+      return rc;
   } else {
     const bool vec2 = A % 2 == 0 && in->clock_rstride % 2 == 0 && in->clock_gstride % 2 == 0 &&
                       in->entry_mstride % 2 == 0 && in->entry_rstride % 2 == 0 &&
                       in->entry_gstride % 2 == 0 && al16(in->clock) && al16(in->entries) &&
-                      al16(out->clock) && al16(out->entries);
+                      al16(out->clock) && al16(out->entries) &&
+                      (!ex || !ex->init_clock || (al16(ex->init_clock) && al16(ex->init_entries)));
     const int V = vec2 ? 2 : 1;
     OrPlan p{};
     p.clock = (const u64 *)in->clock;
@@ -437,6 +495,11 @@ static int orswot_lub_impl(crdt_ctx *ctx, const crdt_orswot_batch *in, const u64
     p.nmblk = (int)((M + mpb - 1) / mpb);
     p.out_clock = (u64 *)out->clock;
     p.out_entries = (u64 *)out->entries;
+    if (ex) {
+      p.init_clock = ex->init_clock;
+      p.init_entries = ex->init_entries;
+      p.viol = ex->viol;
+    }
     const size_t units = G * (size_t)p.nmblk * p.ncolblk;
     const size_t target = (size_t)ctx->cu_count * ctx->tune.orswot_blocks_per_cu;
     size_t S = 1;
@@ -501,6 +564,12 @@ static int orswot_lub_impl(crdt_ctx *ctx, const crdt_orswot_batch *in, const u64
   return launch_deferred(ctx, in->def_off, q, doff, status);
 }
 
+namespace crdt {
+int orswot_lub_many_ex(crdt_ctx *ctx, const crdt_orswot_batch *in, crdt_orswot_out *out, const OrswotJoinExtra &ex) {
+  return orswot_lub_impl(ctx, in, nullptr, 0, out, nullptr, &ex);
+}
+}  // namespace crdt
+
 extern "C" int crdt_orswot_lub_many(crdt_ctx *ctx, const crdt_orswot_batch *in,
                                     crdt_orswot_out *out) {
   if (ctx && ctx->mem_kind == CRDT_MEM_HOST) return crdt::orswot_lub_many_host(ctx, in, out);
@@ -516,10 +585,10 @@ extern "C" int crdt_orswot_lub_many_doff(crdt_ctx *ctx, const crdt_orswot_batch 
   if (!in || !out) return fail(ctx, CRDT_EINVAL, "orswot_lub_many_doff: NULL batch/out");
   if (in->def_off) return fail(ctx, CRDT_EINVAL, "orswot_lub_many_doff: in->def_off must be NULL");
   if (!def_off && D) return fail(ctx, CRDT_EINVAL, "orswot_lub_many_doff: D > 0 without def_off");
-  if (in->G == 0 || in->M == 0 || in->A == 0) return CRDT_OK;
   CRDT_HIP(ctx, hipSetDevice(ctx->device));
-  if (status)
+  if (status)  // written for every call, an empty batch included
     if (int rc = device_fill(ctx, status, sizeof(uint32_t), 0)) return rc;
+  if (in->G == 0 || in->A == 0) return CRDT_OK;
   if (def_off && D == 0) {  // no pool: only the offsets' check (every entry must be 0)
     if (int rc = ensure_dscratch(ctx, (in->G + 1) * sizeof(size_t))) return rc;
     if (int rc = stage_def_off_dev(ctx, (const u64 *)def_off, (size_t *)ctx->dscratch, in->G, 0, status, nullptr))

@@ -26,6 +26,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <initializer_list>
 
@@ -182,22 +183,16 @@ static int agree_mark(crdt_ctx *ctx) {
 }
 
 // Exchange the headers; CRDT_OK on every rank iff every rank validated and the dims agree.
+static int agree_exchange(crdt_ctx *ctx, const Hdr &mine);
+// Host wall time of the header round trip is recorded as "shard_agree" (bench.py reports it).
 static int agree(crdt_ctx *ctx, int st, const Hdr &mine, const char *what) {
+  const auto t0 = std::chrono::steady_clock::now();
+  const int xr = agree_exchange(ctx, mine);
+  timing_add_host(ctx, "shard_agree",
+                  std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+  if (xr != CRDT_OK) return xr;
   const size_t W = (size_t)ctx->nranks;
-  uint64_t *h = static_cast<uint64_t *>(ctx->a_host);
-  uint64_t *send_h = h + W * kHdr;
-  std::memcpy(send_h, mine.w, sizeof mine.w);
-  if (ctx->comm) {
-    uint64_t *d = static_cast<uint64_t *>(ctx->a_dev);
-    CRDT_HIP(ctx, hipStreamWaitEvent(ctx->astream, ctx->a_main, 0));
-    CRDT_HIP(ctx, hipMemcpyAsync(d + W * kHdr, send_h, kHdr * 8, hipMemcpyHostToDevice, ctx->astream));
-    CRDT_NCCL(ctx, ncclAllGather(d + W * kHdr, d, kHdr, ncclUint64, (ncclComm_t)ctx->comm, ctx->astream));
-    CRDT_HIP(ctx, hipMemcpyAsync(h, d, W * kHdr * 8, hipMemcpyDeviceToHost, ctx->astream));
-    CRDT_HIP(ctx, hipEventRecord(ctx->a_done, ctx->astream));
-    CRDT_HIP(ctx, hipEventSynchronize(ctx->a_done));
-  } else {
-    if (int rc = ctx->ops.allgather(ctx->ops.user, send_h, h, kHdr * 8)) return ops_fail(ctx, rc, "allgather");
-  }
+  const uint64_t *h = static_cast<const uint64_t *>(ctx->a_host);
   long bad_rank, odd_rank;
   if (shard_host::check_headers(h, W, mine, &bad_rank, &odd_rank)) return CRDT_OK;
   if (bad_rank >= 0) {
@@ -212,6 +207,26 @@ static int agree(crdt_ctx *ctx, int st, const Hdr &mine, const char *what) {
               (unsigned long long)o[5], (unsigned long long)o[6], ctx->rank, (unsigned long long)mine.w[1],
               (unsigned long long)mine.w[2], (unsigned long long)mine.w[3], (unsigned long long)mine.w[4],
               (unsigned long long)mine.w[5], (unsigned long long)mine.w[6]);
+}
+
+// The header all-gather itself: rows [0, W) of ctx->a_host <- every rank's header.
+static int agree_exchange(crdt_ctx *ctx, const Hdr &mine) {
+  const size_t W = (size_t)ctx->nranks;
+  uint64_t *h = static_cast<uint64_t *>(ctx->a_host);
+  uint64_t *send_h = h + W * kHdr;
+  std::memcpy(send_h, mine.w, sizeof mine.w);
+  if (ctx->comm) {
+    uint64_t *d = static_cast<uint64_t *>(ctx->a_dev);
+    CRDT_HIP(ctx, hipStreamWaitEvent(ctx->astream, ctx->a_main, 0));
+    CRDT_HIP(ctx, hipMemcpyAsync(d + W * kHdr, send_h, kHdr * 8, hipMemcpyHostToDevice, ctx->astream));
+    CRDT_NCCL(ctx, ncclAllGather(d + W * kHdr, d, kHdr, ncclUint64, (ncclComm_t)ctx->comm, ctx->astream));
+    CRDT_HIP(ctx, hipMemcpyAsync(h, d, W * kHdr * 8, hipMemcpyDeviceToHost, ctx->astream));
+    CRDT_HIP(ctx, hipEventRecord(ctx->a_done, ctx->astream));
+    CRDT_HIP(ctx, hipEventSynchronize(ctx->a_done));
+    return CRDT_OK;
+  }
+  if (int rc = ctx->ops.allgather(ctx->ops.user, send_h, h, kHdr * 8)) return ops_fail(ctx, rc, "allgather");
+  return CRDT_OK;
 }
 
 static int device_mem_only(crdt_ctx *ctx, const char *what) {
@@ -463,22 +478,33 @@ int crdt_orswot_lub_many_sharded(crdt_ctx *ctx, const crdt_orswot_batch *in, crd
   }
   head[G] = Dk;
   // 1. local join of the shard without deferred removes -> partial (clock, entries); every
-  //    buffer of the exchange whose size is known here is allocated before the agreement
+  //    buffer of the exchange whose size is known here is allocated before the agreement.  The
+  //    exchanged row per rank: [G+1 deferred counts | G "an input cell had E > C" flags | pad].
+  const size_t crow = 2 * G + 2;
   void *pc = nullptr, *pe = nullptr, *gc = nullptr, *ge = nullptr, *lcnt = nullptr, *acnt = nullptr;
+  crdt_orswot_batch loc{};
+  crdt_orswot_out po{};
+  OrswotJoinExtra ex{};
   if (!st && work) {
-    st = sbuf(ctx, 0, G * A * 8, &pc);
+    st = sbuf(ctx, 0, G * A * 8 + G * 4 + 64, &pc);
     if (!st) st = sbuf(ctx, 1, G * M * A * 8, &pe);
     if (!st) st = sbuf(ctx, 2, W * G * A * 8, &gc);
     if (!st) st = sbuf(ctx, 3, W * G * M * A * 8, &ge);
-    if (!st) st = sbuf(ctx, 4, (G + 1) * 8, &lcnt);
-    if (!st) st = sbuf(ctx, 5, W * (G + 1) * 8, &acnt);
+    if (!st) st = sbuf(ctx, 4, crow * 8, &lcnt);
+    if (!st) st = sbuf(ctx, 5, W * crow * 8, &acnt);
     if (!st) {
-      crdt_orswot_batch loc = *in;
+      loc = *in;
       loc.def_off = nullptr;
-      crdt_orswot_out po{(uint64_t *)pc, (uint64_t *)pe, nullptr, nullptr};
-      st = crdt_orswot_lub_many(ctx, &loc, &po);
+      po = crdt_orswot_out{(uint64_t *)pc, (uint64_t *)pe, nullptr, nullptr};
+      ex.viol = reinterpret_cast<unsigned *>((u64 *)pc + G * A);
+      st = orswot_lub_many_ex(ctx, &loc, &po, ex);
     }
     if (!st) st = stage_h2d(ctx, lcnt, head.data(), (G + 1) * 8);
+    if (!st) {
+      hipLaunchKernelGGL(widen_u32_kernel, dim3(small_grid(ctx, G + 1)), dim3(kBlock), 0, ctx->stream,
+                         (u64 *)lcnt + G + 1, (const unsigned *)ex.viol, (unsigned long long)G, (u64)0);
+      if (hipGetLastError() != hipSuccess) st = fail(ctx, CRDT_EHIP, "%s: widen_u32_kernel launch", what);
+    }
   }
   CRDT_TRY(agree(ctx, st, make_hdr(st, kTagOrswot, {G, M, A}), what));
   if (!work) {
@@ -491,25 +517,46 @@ int crdt_orswot_lub_many_sharded(crdt_ctx *ctx, const crdt_orswot_batch *in, crd
   CRDT_TRY(coll_group_begin(ctx));
   CRDT_TRY(coll_allgather(ctx, pc, gc, G * A * 8));
   CRDT_TRY(coll_allgather(ctx, pe, ge, G * M * A * 8));
-  CRDT_TRY(coll_allgather(ctx, lcnt, acnt, (G + 1) * 8));
+  CRDT_TRY(coll_allgather(ctx, lcnt, acnt, crow * 8));
   CRDT_TRY(coll_group_end(ctx));
-  std::vector<uint64_t> all((G + 1) * W);
-  CRDT_HIP(ctx, hipMemcpyAsync(all.data(), acnt, all.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
+  std::vector<uint64_t> rows(crow * W), all((G + 1) * W);
+  CRDT_HIP(ctx, hipMemcpyAsync(rows.data(), acnt, rows.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
   CRDT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  bool chain = false;  // some rank's shard holds a cell with E > C (rank-uniform: gathered flags)
+  for (size_t r = 0; r < W; ++r) {
+    std::copy(rows.begin() + r * crow, rows.begin() + r * crow + G + 1, all.begin() + r * (G + 1));
+    for (size_t g = 0; g < G; ++g) chain = chain || (rows[r * crow + G + 1 + g] & 1);
+  }
+  chain = chain && W > 1;
   size_t Dmax = 0, Dtot = 0;
   for (size_t r = 0; r < W; ++r) {
     Dmax = std::max<size_t>(Dmax, all[r * (G + 1) + G]);
     Dtot += all[r * (G + 1) + G];
   }
+  // Such a cell makes the join non-associative, so the partials may not be joined as a tree: the
+  // ranks fold in rank order instead — rank k continues from rank k-1's state (its shard re-folded
+  // with that state as the start), each step published by one more all-gather — and the re-merge
+  // below then reads the last rank's state alone (W-1 extra exchanges; exact for any input).
+  for (size_t k = 1; chain && k < W; ++k) {
+    if ((size_t)ctx->rank == k) {
+      ex.init_clock = (const u64 *)gc + (k - 1) * G * A;
+      ex.init_entries = (const u64 *)ge + (k - 1) * G * M * A;
+      CRDT_TRY(orswot_lub_many_ex(ctx, &loc, &po, ex));
+    }
+    CRDT_TRY(coll_group_begin(ctx));
+    CRDT_TRY(coll_allgather(ctx, pc, gc, G * A * 8));
+    CRDT_TRY(coll_allgather(ctx, pe, ge, G * M * A * 8));
+    CRDT_TRY(coll_group_end(ctx));
+  }
   crdt_orswot_batch fin{};
   fin.G = G;
-  fin.R = W;
+  fin.R = chain ? 1 : W;
   fin.M = M;
   fin.A = A;
-  fin.clock = (const uint64_t *)gc;
+  fin.clock = (const uint64_t *)gc + (chain ? (W - 1) * G * A : 0);
   fin.clock_rstride = G * A;
   fin.clock_gstride = A;
-  fin.entries = (const uint64_t *)ge;
+  fin.entries = (const uint64_t *)ge + (chain ? (W - 1) * G * M * A : 0);
   fin.entry_mstride = A;
   fin.entry_rstride = G * M * A;
   fin.entry_gstride = M * A;
@@ -742,16 +789,19 @@ int crdt_map_lub_many_sharded(crdt_ctx *ctx, const crdt_map_batch *in, size_t k0
       loc.def_keys = (const uint64_t *)lk;
       lo.def_keys = (uint64_t *)ok;
     }
-    if (!st) st = local(out->Vstate);
+    if (!st) st = local(std::min<size_t>(out->Vstate, 16));
   }
   const uint64_t offh = (!st && in->def_off && G) ? shard_host::hash_offsets(in->def_off, G + 1) : 0;
-  CRDT_TRY(agree(ctx, st, make_hdr(st, kTagMap, {G, K, A, D, st ? 0 : (uint64_t)out->Vout, offh}), what));
+  // the retry below branches on vstate: its start is part of the agreed call, so ranks
+  // passing different Vstate values all return EINVAL instead of meeting in different collectives
+  const size_t vst0 = st ? 0 : std::min<size_t>(out->Vstate, 16);
+  CRDT_TRY(agree(ctx, st, make_hdr(st, kTagMap, {G, K, A, D, st ? 0 : (uint64_t)out->Vout, offh, vst0}), what));
   if (!work) return CRDT_OK;
   // flags of every rank (+ its status) -> the OR over the ranks, written back on every rank; a
   // fold state that ran out of value slots (bit 2) on ANY rank reruns the fold with a larger state
   // on EVERY rank (each key's result is independent of the state size), so the ranks take the same
   // branches and meet in the same collectives
-  size_t vstate = out->Vstate;
+  size_t vstate = vst0;
   std::vector<uint64_t> hf(W * (G + 1));
   std::vector<uint32_t> gflags(G);
   for (;;) {

@@ -648,9 +648,9 @@ impl<M: Member, A: Actor> OrswotDense<M, A> {
     }
 }
 
-/// `lub_many` is the exact left fold for replicas built through the crate's own API (each dot
-/// unique to one replica, entry dots covered by their replica's clock: the invariants under which
-/// the dot-store join is associative, `include/crdt_gpu.h`); `merge_batch` is exact for any pair.
+/// `lub_many` is the exact left fold `Orswot::new()` + `merge` of every replica for ANY states (a
+/// replica with entry dots above its clock, e.g. deserialized, is folded in replica order by the
+/// library, `include/crdt_gpu.h`); `merge_batch` is exact for any pair.
 impl<M: Member, A: Actor> BatchCvRDT for Orswot<M, A> {
     fn lub_many(ctx: &GpuCtx, replicas: Vec<Self>) -> Result<Self, GpuError> {
         if replicas.is_empty() {
@@ -669,7 +669,8 @@ impl<M: Member, A: Actor> BatchCvRDT for Orswot<M, A> {
         }
         let nd = dcl.len() / a;
         let def_off: [usize; 2] = [0, nd];
-        // host rows straight to the CRDT_MEM_HOST ctx: the library stages the whole batch
+        // host rows straight to the CRDT_MEM_HOST ctx: the library streams replica chunks through its
+        // two device buffers (the join of chunk k overlaps the copy of chunk k+1)
         let (mut c, mut e, mut keep, mut mem) = (vec![0u64; a], vec![0u64; m * a], vec![0u8; nd], vec![0u64; nd * mw]);
         let batch = ffi::crdt_orswot_batch {
             G: 1, R: r, M: m, A: a,

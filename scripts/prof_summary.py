@@ -60,4 +60,13 @@ if alg and "avg_launch_us_rocprof" in out:
     out["achieved_GBs_rocprof"] = alg / out["avg_launch_us_rocprof"] / 1e3
     out["frac_of_8TBs"] = out["achieved_GBs_rocprof"] / 8000.0
 json.dump(out, open(os.path.join(P, f"{tag}_pmc_summary.json"), "w"), indent=1)
+# the bench line's roofline.traffic: this checkpoint's measurement, tied to the kernel source it was
+# measured on (bench.py reports null when csrc/lattice.hip no longer matches)
+if kernel == "lub_multi_kernel" and "hbm_bytes_per_launch" in out:
+    sys.path.insert(0, ROOT)
+    import bench
+    json.dump({"workload": "gcounter+pncounter lub 1048576x256", "fused": True,
+               "hbm_bytes_per_launch": out["hbm_bytes_per_launch"], "source": f"profiles/{tag}_pmc_summary.json",
+               "kernel_source_sha256": bench.kernel_source_sha()},
+              open(os.path.join(P, "pmc_traffic.json"), "w"), indent=1)
 print(json.dumps(out, indent=1))

@@ -78,3 +78,54 @@ def map_overflow_input():
 
 
 MAP_OVF_VOUT = 16
+
+
+# BASELINE config 5, one GPU's shard per rank (bench.py --workload c5): VClock 1,048,576 x 1,024
+C5_R, C5_A, C5_SEED = 1 << 20, 1024, 0x5EED0005
+C5_COLS = np.array([0, 1, 2, 63, 64, 127, 255, 256, 511, 512, 700, 777, 1000, 1021, 1022, 1023])
+
+
+def c5_expected_columns(R, row0=0):
+    """The oracle's left fold of VClock::merge (oracle_vclock_fold) over rows [row0, row0 + R) of the
+    config-5 synthetic input, restricted to the sampled actor columns C5_COLS (the generator is
+    closed-form per (row, actor), so a column is generated without the other 1,008)."""
+    r = np.arange(row0, row0 + R, dtype=np.uint64)
+    idx = r[:, None] * np.uint64(C5_A) + C5_COLS.astype(np.uint64)[None, :]
+    return O.vclock_fold(O.synth_values(C5_SEED, idx, 0))[0]
+
+
+def adversarial_orswot(seed, R, M, A, V=6, p_def=0.3, plant=True):
+    """Arbitrary states (E > C cells, repeated dots) plus deferred removes per replica; with `plant`,
+    the smallest non-associative cell sequence (e, c) = (1, 1), (2, 0), (1, 2) is planted on member 0,
+    actor 0 at replicas 0, R-2, R-1 (all other replicas zero there), so a fold that joins slice
+    partials as a tree keeps a dot the left fold drops."""
+    rng = np.random.default_rng(seed)
+    clock = rng.integers(0, V, size=(R, A)).astype(np.uint64)
+    entries = rng.integers(0, V, size=(R, M, A)).astype(np.uint64)
+    entries[rng.random((R, M, A)) < 0.6] = 0
+    if plant and R >= 3:
+        clock[:, 0] = 0
+        entries[:, 0, 0] = 0
+        for r, (e, c) in zip((0, R - 2, R - 1), ((1, 1), (2, 0), (1, 2))):
+            entries[r, 0, 0], clock[r, 0] = e, c
+    Mw = (M + 63) // 64
+    off, dcl, dmem = [0], [], []
+    for _ in range(R):
+        if rng.random() < p_def:
+            rm = rng.integers(0, V + 1, size=A).astype(np.uint64)
+            if plant:
+                rm[0] = 0  # removes never touch the planted cell
+            dcl.append(rm)
+            bits = np.zeros(Mw, np.uint64)
+            for m in rng.choice(M, size=min(M, 3), replace=False):
+                if not plant or m != 0:
+                    bits[m // 64] |= np.uint64(1) << np.uint64(m % 64)
+            dmem.append(bits)
+        off.append(len(dcl))
+    return (clock, entries, np.array(off, np.uint64), np.array(dcl, np.uint64).reshape(-1, A),
+            np.array(dmem, np.uint64).reshape(-1, Mw))
+
+
+def orswot_any_input():
+    """World-2 Orswot input outside the reference invariants (see adversarial_orswot)."""
+    return adversarial_orswot(0x5EED00A1, 600, 11, 8)

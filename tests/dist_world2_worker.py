@@ -145,6 +145,17 @@ def cabi_seam(rank, world, t, h):
     o["cabi_orswot_clock"], o["cabi_orswot_entries"] = h(res.clock), h(res.entries)
     o["cabi_orswot_def_clock"], o["cabi_orswot_def_members"] = h(res.def_clock), h(res.def_members)
     o["cabi_orswot_ndef_local"] = np.array([d1 - d0], np.int64)
+    # Orswot on ARBITRARY states (E > C cells): the planted non-associative cells sit
+    # at replica 0 (rank 0) and R-2, R-1 (rank 1), so joining the rank partials as a tree is wrong; the
+    # flags gathered with the deferred counts switch the ranks to the rank-order chain
+    clock, entries, off, dcl, dmem = D.orswot_any_input()
+    R = clock.shape[0]
+    lo, hi = cdist.shard_range(R, rank, world)
+    d0, d1 = int(off[lo]), int(off[hi])
+    kw = dict(def_off=[0, d1 - d0], def_clock=t(dcl[d0:d1]), def_members=t(dmem[d0:d1])) if d1 > d0 else {}
+    res = cs.orswot_lub_many_sharded(t(clock[lo:hi][None]), t(entries[lo:hi][None]), ctx=ctx, **kw)
+    o["cabi_orswot_any_clock"], o["cabi_orswot_any_entries"] = h(res.clock), h(res.entries)
+    o["cabi_orswot_any_def_clock"], o["cabi_orswot_any_def_members"] = h(res.def_clock), h(res.def_members)
     # Map<K, MVReg>: key shards (k0 != 0 on rank 1), then an EMPTY key shard on rank 1
     d = D.map_input()
     K = d["ec"].shape[1]
@@ -178,6 +189,13 @@ def cabi_seam(rank, world, t, h):
     o["cabi_mapovf_ec"], o["cabi_mapovf_vclk"], o["cabi_mapovf_vval"] = h(mres.ec), h(mres.vclk), h(mres.vval)
     o["cabi_mapovf_nval"] = mres.nval.cpu().numpy().copy()
     o["cabi_mapovf_flags"] = mres.flags.cpu().numpy().copy()
+    # ranks passing different starting fold states (Vstate 16 vs 0) with an overflowing key: the
+    # retry branches on it, so it is part of the agreed call and BOTH ranks get EINVAL
+    try:
+        cs.map_lub_many_sharded(*args, vout=D.MAP_OVF_VOUT, ctx=ctx, vstate=16 if rank == 0 else 0)
+        o["cabi_mapvstate_code"] = np.array([0], np.int64)
+    except CrdtGpuError as e:
+        o["cabi_mapvstate_code"] = np.array([e.code], np.int64)
     # a bad argument on ONE rank: every rank raises, none blocks; then a good call still works
     codes = []
     x = t(D.lattice_input("vclock")[0])
@@ -195,6 +213,23 @@ def cabi_seam(rank, world, t, h):
             codes.append(e.code)
     o["cabi_error_codes"] = np.array(codes, np.int64)
     o["cabi_after_errors"] = h(cs.lub_many_sharded("vclock", x, ctx=ctx))
+    # config 5 at full per-GPU size: rank k holds replicas [k*R, (k+1)*R) of the
+    # 1,048,576-per-rank x 1,024-actor VClock input (bench.py --workload c5's shard), lub through
+    # crdt_vclock_lub_many_sharded; the parent checks sampled actor columns against the oracle's fold
+    # of all 2M replicas and every column against the max of the ranks' local torch maxima
+    R5, A5 = D.C5_R, D.C5_A
+    x5 = torch.empty((R5, A5), dtype=torch.int64, device=dev)
+    cg.synth_fill(ctx, x5, D.C5_SEED, 0, first_row=rank * R5)
+    ctx.timing_reset()
+    ctx.set_timing(True)
+    o["cabi_c5"] = h(cs.lub_many_sharded("vclock", x5, ctx=ctx))
+    ctx.set_timing(False)
+    o["cabi_c5_timing_ms"] = np.array([ctx.timing("lub_stream")[0], ctx.timing("shard_exchange")[0],
+                                       ctx.timing("shard_agree")[0]], np.float64)
+    sign = torch.tensor(-(2**63), dtype=torch.int64, device=dev)
+    o["cabi_c5_local_max"] = h((x5 ^ sign).amax(0) ^ sign)
+    del x5
+    torch.cuda.empty_cache()
     torch.cuda.synchronize()
     cs.comm_destroy(ctx)
     return o

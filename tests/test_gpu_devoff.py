@@ -74,6 +74,33 @@ def test_orswot_devoff_no_pool(gpu_ctx):
     assert torch.equal(ref.clock, got.clock) and torch.equal(ref.entries, got.entries)
 
 
+def test_orswot_devoff_empty_members(gpu_ctx):
+    """M == 0: the state is its clock — the fold is the clock lub and a deferred remove (with an
+    empty member set, orswot.rs:230-250 keeps it) survives iff not dominated by the final clock.
+    The status is written for every call (it was left uninitialised on this path)."""
+    rng = np.random.default_rng(5)
+    clock = rng.integers(0, 9, size=(3, 5, 4), dtype=np.uint64)
+    dcl = rng.integers(0, 12, size=(6, 4), dtype=np.uint64)
+    off = np.array([0, 2, 2, 6])
+    entries = torch.empty((3, 5, 0, 4), dtype=torch.int64, device="cuda:0")
+    dmem = torch.empty((6, 0), dtype=torch.int64, device="cuda:0")
+    exp = clock.max(axis=1)
+    keep_exp = np.array([(dcl[d] > exp[g]).any() for g in range(3) for d in range(off[g], off[g + 1])])
+    for form in ("host", "device"):
+        st = torch.full((1,), -1, dtype=torch.int32, device="cuda:0")
+        kw = dict(def_off=_doff(off), def_status=st) if form == "device" else dict(def_off=off)
+        got = cg.orswot.lub_many(to_dev(clock), entries, def_clock=to_dev(dcl), def_members=dmem, ctx=gpu_ctx, **kw)
+        np.testing.assert_array_equal(to_host(got.clock), exp)
+        np.testing.assert_array_equal(got.def_keep.cpu().numpy().astype(bool), keep_exp)
+        if form == "device":
+            assert int(st.item()) == 0
+    assert keep_exp.any() and not keep_exp.all()
+    st = torch.full((1,), -1, dtype=torch.int32, device="cuda:0")
+    got = cg.orswot.lub_many(to_dev(clock), entries, def_off=_doff(np.zeros(4)), def_status=st, ctx=gpu_ctx)
+    assert int(st.item()) == 0
+    np.testing.assert_array_equal(to_host(got.clock), exp)
+
+
 @pytest.mark.parametrize("bad", ["first", "last_short", "last_long", "decreasing", "past_pool"])
 def test_orswot_devoff_invalid(gpu_ctx, bad):
     """Each kind of malformed offset array is reported (status bit 0 / ValueError without a status

@@ -149,6 +149,23 @@ def test_world2_cabi_orswot(outs):
         assert got == odef
 
 
+def test_world2_cabi_orswot_any_state(outs):
+    """crdt_orswot_lub_many_sharded at world 2 on states with E > C cells whose non-associative
+    sequence spans the rank boundary: the ranks fold in rank order (csrc/shard.hip), so both hold
+    the reference's left fold, not the tree join of the rank partials."""
+    clock, entries, off, dcl, dmem = D.orswot_any_input()
+    kw = (off, dcl, dmem) if int(off[-1]) else ()
+    oc, oe, odef, _ = O.orswot_fold(clock, entries, *kw)
+    assert int(oe[0, 0]) == 0  # the planted dot: dropped by the left fold, kept by a tree
+    for o in outs:
+        np.testing.assert_array_equal(o["cabi_orswot_any_clock"][0], oc)
+        np.testing.assert_array_equal(o["cabi_orswot_any_entries"][0], oe)
+        got = {(tuple(int(x) for x in o["cabi_orswot_any_def_clock"][d]),
+                O.bitmap_members(o["cabi_orswot_any_def_members"][d]))
+               for d in range(o["cabi_orswot_any_def_clock"].shape[0])}
+        assert got == odef
+
+
 @pytest.mark.parametrize("tag", ["even", "empty"])
 def test_world2_cabi_map(outs, tag):
     """crdt_map_lub_many_sharded at world 2: key placement at k0 != 0 with the SUM all-reduce, and
@@ -192,6 +209,15 @@ def test_world2_cabi_map_overflow_on_one_rank(outs):
     assert int(outs[0]["cabi_mapovf_flags"][0]) == int(outs[1]["cabi_mapovf_flags"][0])
 
 
+def test_world2_cabi_map_vstate_mismatch(outs):
+    """Rank 0 starts the fold with a 16-value state, rank 1 with none, and a key overflows the
+    smaller one: the overflow retry branches on the state size, so a mismatch must be refused on
+    EVERY rank (EINVAL) before the collectives instead of leaving the ranks in different ones."""
+    EINVAL = -1
+    for o in outs:
+        assert int(o["cabi_mapvstate_code"][0]) == EINVAL
+
+
 def test_world2_cabi_errors_agree(outs):
     """A NULL output on rank 1 (its own validation fails) and a row width that differs between the
     ranks: EVERY rank returns an error instead of blocking in the all-reduce, and the communicator
@@ -202,3 +228,19 @@ def test_world2_cabi_errors_agree(outs):
     exp = O.vclock_fold(D.lattice_input("vclock")[0])[0]
     for o in outs:
         np.testing.assert_array_equal(o["cabi_after_errors"], exp)
+
+
+def test_world2_cabi_config5(outs):
+    """Config 5 at world 2 through the C ABI's own sharded entry point (the callback seam: RCCL
+    refuses two ranks on one GPU): 2 x 1,048,576 VClock replicas x 1,024 actors.  Sampled actor
+    columns equal the oracle's left fold of VClock::merge over ALL 2M replicas; every column equals
+    the max of the two ranks' local maxima; both ranks hold the same result."""
+    assert (D.C5_R, D.C5_A, D.C5_SEED) == (1 << 20, 1024, 0x5EED0005)
+    exp_cols = D.c5_expected_columns(2 * D.C5_R)
+    full = np.maximum(outs[0]["cabi_c5_local_max"], outs[1]["cabi_c5_local_max"])
+    for o in outs:
+        np.testing.assert_array_equal(o["cabi_c5"][D.C5_COLS], exp_cols)
+        np.testing.assert_array_equal(o["cabi_c5"], full)
+        lub_ms, xch_ms, agr_ms = (float(v) for v in o["cabi_c5_timing_ms"])
+        assert lub_ms > 0 and xch_ms > 0 and agr_ms > 0  # the library timed every phase
+    assert not np.array_equal(outs[0]["cabi_c5_local_max"], outs[1]["cabi_c5_local_max"])

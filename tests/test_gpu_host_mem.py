@@ -280,6 +280,23 @@ def test_map_host_lub_many_streamed(stage_kb, vout, src):
     assert got == exp[5]
 
 
+@pytest.mark.parametrize("hs", [1, 0])
+def test_map_host_def_row_past_r(hs):
+    """A remove whose def_row == R (held by no replica): the streamed and the whole-batch host forms
+    both report flags bit 1, as the device fold does (the streamed form used to drop it)."""
+    dfr = O.synth_map_deferred(0x5EED0046, 100, 20, 8, 6, p_def=0.3)
+    rows, dcl, dks = dfr
+    d = O.synth_map(0x5EED0046, 100, 20, 8, 2, 6, keys=np.arange(20), deferred=dfr)
+    rows = rows.copy()
+    rows[-1] = 100
+    D = rows.shape[0]
+    ctx = host.HostContext(0, tune=f"stage_kb=64,hstream={hs}")
+    res = host.map_lub_many(d["clock"], d["ec"], d["vclk"], d["vval"], def_off=[0, D], def_row=rows,
+                            def_clock=dcl, def_keys=dks, vout=4, ctx=ctx)
+    ctx.close()
+    assert D > 1 and int(res.flags[0]) & 2
+
+
 def test_map_host_merge_batch(hctx):
     from test_gpu_merge_batch import replay_maps
     N, K, n_origins = 20, 10, 4

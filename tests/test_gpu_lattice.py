@@ -74,8 +74,14 @@ def test_gset_lub_many(gpu_ctx, R, W):
     np.testing.assert_array_equal(got, exp)
 
 
-@pytest.mark.parametrize("N,A", [(1, 1), (10, 7), (1000, 64), (3000, 256), (64, 1030)])
-def test_merge_batch(gpu_ctx, N, A):
+# merge_batch launch forms: the flat 16-byte stream of packed rows (default, one workgroup per CU;
+# mflat=4: four), and the row-group kernels (mflat=0, also the path of strided rows)
+@pytest.mark.parametrize("mode", ["", "mflat=0", "mflat=4"])
+@pytest.mark.parametrize("N,A", [(1, 1), (10, 7), (7, 2), (33, 6), (1000, 64), (3000, 256), (64, 1030)])
+def test_merge_batch(gpu_ctx, mode, N, A):
+    if mode:
+        gpu_ctx = cg.Context(0)
+        gpu_ctx.tune(mode)
     s = O.synth_matrix(11, N, A, 0)
     o = O.synth_matrix(12, N, A, 0)
     exp = O.vclock_merge_pairs(s, o)
@@ -93,6 +99,12 @@ def test_merge_batch(gpu_ctx, N, A):
     dps = to_dev(ps)
     cg.pncounter.merge_batch(dps, to_dev(po), ctx=gpu_ctx)
     np.testing.assert_array_equal(to_host(dps), exp_p)
+    # strided rows (views into wider buffers): never the flat stream
+    wide = to_dev(np.concatenate([s, np.zeros((N, 2), np.uint64)], axis=1))
+    owide = to_dev(np.concatenate([o, np.zeros((N, 2), np.uint64)], axis=1))
+    cg.vclock.merge_batch(wide[:, :A], owide[:, :A], ctx=gpu_ctx)
+    np.testing.assert_array_equal(to_host(wide[:, :A]), exp)
+    assert not to_host(wide[:, A:]).any()
 
 
 @pytest.mark.parametrize("rows,width,kind", [(3, 5, 0), (100, 256, 0), (7, 9, 1), (1, 1000, 2), (1, 1000, 3)])

@@ -112,3 +112,20 @@ def test_map_sharded_world1(comm_ctx, k0, Kk):
     got = cg.map.deferred_set(t(d["def_clock"]), res.def_keep, res.def_keys)
     want = {(c, frozenset(k for k in ks if k0 <= k < k0 + Kk)) for c, ks in exp[5]}
     assert got == want and len(want) > 0
+
+
+def test_config5_shard_world1(comm_ctx):
+    """Config 5 at full per-GPU size through crdt_vclock_lub_many_sharded over the ctx's RCCL
+    communicator: 1,048,576 VClock replicas x 1,024 actors (8 GiB) — sampled
+    actor columns against the oracle's fold, every column against a torch unsigned max of the same
+    HBM rows, and against the unsharded lub_many."""
+    from dist_world2_data import C5_A, C5_COLS, C5_R, C5_SEED, c5_expected_columns
+    x = torch.empty((C5_R, C5_A), dtype=torch.int64, device="cuda:0")
+    cg.synth_fill(comm_ctx, x, C5_SEED, 0, first_row=0)
+    got = to_host(cg.shard.lub_many_sharded("vclock", x, ctx=comm_ctx))
+    np.testing.assert_array_equal(got[C5_COLS], c5_expected_columns(C5_R))
+    np.testing.assert_array_equal(got, to_host(umax_torch(x, 0)))
+    np.testing.assert_array_equal(got, to_host(cg.vclock.lub_many(x, ctx=comm_ctx)))
+    assert (got != 0).all()
+    del x
+    torch.cuda.empty_cache()
