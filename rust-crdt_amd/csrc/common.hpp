@@ -67,6 +67,7 @@ struct Tune {
   int map_sh = 0;      // ... RS path at A = 32, V = 2, K % 4 == 0: four key waves share each chunk's clock
                        //     rows (less traffic, but slower: the coupled waves; opt-in)
   int map_lazyv = 1;   // ... RS path: values fetched only for chunks the exact loop runs (not streamed)
+  int map_ld = 0;      // ... RS path at (2+V)*A == 128: a loader wave per key issues the chunks' LDS-DMA (opt-in)
   int map_diag = 0;    // ... timing probes only, results WRONG (bit0: no clock-max piece, bit1: 3 fewer step pieces)
   int rows_blocks_per_cu = 0;  // row-pair / row-reduction kernels (causal.hip); 0 = per-kernel default
   int apply_hot_slots = 8;     // Orswot apply: deferred slots kept in LDS per state (the rest in HBM)
@@ -260,6 +261,9 @@ int orswot_lub_many_ex(crdt_ctx *ctx, const crdt_orswot_batch *in, crdt_orswot_o
 int orswot_merge_batch_host(crdt_ctx *ctx, const crdt_orswot_states *self, const crdt_orswot_states *other,
                             uint32_t *status);
 int map_lub_many_host(crdt_ctx *ctx, const crdt_map_batch *in, crdt_map_out *out);
+// The workgroup-per-key Map fold for A > 256 or V > 8 (map_wide.hip): def_off_dev = the device copy
+// of the deferred offsets (or NULL); outputs and flags as crdt_map_lub_many (flags zeroed by the caller).
+int map_lub_wide(crdt_ctx *ctx, const crdt_map_batch *in, const size_t *def_off_dev, crdt_map_out *out);
 int map_merge_batch_host(crdt_ctx *ctx, const crdt_map_states *self, const crdt_map_deferred *self_def,
                          const crdt_map_states *other, const crdt_map_deferred *other_def, uint32_t *status);
 void free_stage(crdt_ctx *ctx);

@@ -66,6 +66,7 @@ struct MapPlan {
   int lazyv;  // RS path: the values of a chunk fetched only when the exact loop runs it
   int diag;   // timing probes (results wrong): bit0 no clock-max piece, bit1 3 fewer step pieces,
               // bit2 SH path without arrival waits
+  const u64 *seq;  // LD path: [nch][2] = chunk index + 1, the arrival flag each chunk's last piece carries
 };
 
 constexpr int kMapQ = 4;    // deferred removes tracked per key in registers before the slow path
@@ -315,7 +316,7 @@ template <int VI, int C, int NI, int AUX = 0>
 __device__ __forceinline__ void map_chunk_glds(const MapPlan &p, const GldsLanes<NI> &L, unsigned long long g,
                                                unsigned long long k, unsigned long long i0, unsigned long long iend,
                                                u64 *img, unsigned long long WS, u64 *vals, u64 *cm, int lane,
-                                               bool vpiece = true, int diag = 0) {
+                                               bool vpiece = true, int diag = 0, const u64 *flag = nullptr) {
   if (i0 + C <= iend) {  // a whole chunk (uniform)
     const char *src[NI];
 #pragma unroll
@@ -354,10 +355,13 @@ __device__ __forceinline__ void map_chunk_glds(const MapPlan &p, const GldsLanes
       glds4<AUX>(src, vals);
     }
   }
-  // the chunk's clock max: one more piece (lanes 0 .. A/2-1, A even)
-  if (!(diag & 1))
-    if ((unsigned long long)(2 * lane) < p.A)
-      glds16(p.cmax + (g * p.nch + i0 / C) * p.A + 2 * lane, cm);
+  // the chunk's clock max: one more piece (lanes 0 .. A/2-1, A even); with `flag` (the LD path) lane
+  // A/2 of the same, last, piece moves the chunk's arrival flag seq[chunk] to cm[A]: the pieces of
+  // a wave retire in order, so a reader that sees the flag sees the whole chunk
+  if (!(diag & 1)) {
+    const bool con = (unsigned long long)(2 * lane) < p.A, fon = flag && (unsigned long long)(2 * lane) == p.A;
+    if (con || fon) glds16(con ? p.cmax + (g * p.nch + i0 / C) * p.A + 2 * lane : flag + 2 * (i0 / C), cm);
+  }
 }
 
 // Wait until at most N vector-memory ops are outstanding (counts above the 6-bit field clamp
@@ -1071,6 +1075,20 @@ constexpr unsigned kShSlot = 1536;            // private slot, u64 words (16 ste
 constexpr unsigned kShShared = 512 + 32;      // shared slot: clock rows + clock max
 constexpr unsigned kShSpin = 1u << 22;        // arrival-wait bound (a protocol fault is reported, never hangs)
 
+// ---- Loader wave (LD path: the RS path at (2+V)*A == 128, config 4) --------------------------------
+// The chunk's 17 LDS-DMA instructions cost the wave that issues them ~34-68 cycles each (a wave
+// issues one per ~34 cycles alone and the CU's engine one per ~17, scripts/micro/glds_rate.hip), and
+// in the RS path that wave is the key's fold wave: about a quarter of its chunk test.  In the LD path
+// a workgroup is two waves: wave 0 folds the key, wave 1 only streams its chunks into the two ring
+// slots.  Hand-over through LDS, no barriers: the last piece of a chunk carries its arrival flag
+// (lane A/2 of the clock-max piece writes seq[c] = c + 1 after the clock max), and the fold wave,
+// once its copy of chunk c out of slot c&1 is read, publishes rel[c&1] = c + 1; the loader issues
+// chunk c + 2 into that slot when it sees it.  A chunk the register test cannot skip takes its slot
+// back: the fold wave waits for chunk c + 2's flag (that copy has landed), writes chunk c over the
+// slot, runs the exact loop, clears the flag and re-issues chunk c + 2 itself.  Every wait is
+// bounded (flag bit 3 on a timeout, after which nothing waits), so the grid always drains.
+constexpr unsigned kLdSpin = 1u << 21;
+
 // Per-lane LDS-DMA sources of the SH path: piece v (part v) of a 4-step group moves pair lane%16 of
 // part v of step lane/16; the shared piece of wave w the same pair of the clock row of step
 // 4w + lane/16.
@@ -1215,10 +1233,11 @@ __device__ __forceinline__ unsigned sh_arrived(const unsigned *cnt) {
 
 // ITM: unrolled scan iterations ceil(A / LPS) rounded up to a power of two, fixed per launch so
 // each kernel's register allocation only covers its own scan shape.  NP > 0: the RS path (above).
-template <int APL, int VI, int VO, int CM, int NB, bool GL, int ITM, int NP = 0, bool SH = false>
-__global__ __launch_bounds__(SH ? 256 : 64) void map_fold_kernel(MapPlan pk) {
+template <int APL, int VI, int VO, int CM, int NB, bool GL, int ITM, int NP = 0, bool SH = false, bool LD = false>
+__global__ __launch_bounds__(SH ? 256 : (LD ? 128 : 64), LD ? 2 : 1) void map_fold_kernel(MapPlan pk) {
   constexpr bool RS = NP > 0;
   static_assert(!SH || (RS && VI == 2 && NP == 4), "SH path: the RS path at A = 32, V = 2");
+  static_assert(!LD || (RS && !SH && NB == 2), "LD path: the RS path with a loader wave");
   const MapPlan p = pk;  // a local copy the optimizer can split into registers (the by-value
                          // kernel argument itself would be materialized in scratch memory)
   // SH: a workgroup of four waves, wave w folding key 4*blockIdx + w (K % 4 == 0: one group)
@@ -1226,7 +1245,7 @@ __global__ __launch_bounds__(SH ? 256 : 64) void map_fold_kernel(MapPlan pk) {
   const unsigned long long gk0 = SH ? 4ull * blockIdx.x + wv : (unsigned long long)blockIdx.x;
   const unsigned long long g = gk0 / p.K;
   const unsigned long long k = gk0 % p.K;
-  const int lane = SH ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
+  const int lane = (SH || LD) ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
   const unsigned long long R = p.R;
 
   bool present = false;
@@ -1279,7 +1298,9 @@ __global__ __launch_bounds__(SH ? 256 : 64) void map_fold_kernel(MapPlan pk) {
   // would hide the LDS address space and turn every access into a flat op.)  SH: four such wave
   // regions (no clock-max slots), then the shared ring and its arrival counters.
   const unsigned long long SLOT = SH ? kShSlot : C * WS;
-  const unsigned long long PW = NB * SLOT + NB * C * VI + kMapL + (2 + VO) * A + ((GL || RS) && !SH ? NB * A : 0) + 4 * A;
+  const unsigned long long CMS = LD ? A + 2 : A;  // staged clock-max stride (LD: + the arrival flag)
+  const unsigned long long PW =
+      NB * SLOT + NB * C * VI + kMapL + (2 + VO) * A + ((GL || RS) && !SH ? NB * CMS : 0) + 4 * A + (LD ? 1 : 0);
   u64 *const wl = map_lds + (SH ? wv * PW : 0);
   u64 *const shr = map_lds + 4 * PW;  // SH: kShS shared slots
   unsigned *const arr = reinterpret_cast<unsigned *>(shr + kShS * kShShared);
@@ -1291,10 +1312,39 @@ __global__ __launch_bounds__(SH ? 256 : 64) void map_fold_kernel(MapPlan pk) {
   constexpr bool kSpec = APL == 1 && VO <= 4;
   u64 *const cml = mirror + (2 + VO) * A;  // GL: NB staged chunk clock maxima (A words each)
   // scan thresholds (map_noop_steps3, RS): TB [A] | TO [A]; m1 = (min nonzero own value clock) - 1
-  u64 *const thr = cml + ((GL || RS) && !SH ? NB * A : 0);
+  u64 *const thr = cml + ((GL || RS) && !SH ? NB * CMS : 0);
   u64 *const csm = thr + 2 * A;  // RS: the acc clock and m1 handed back to the register operands
   u64 *const m1m = thr + 3 * A;
+  unsigned *const rel = reinterpret_cast<unsigned *>(m1m + A);  // LD: last chunk released per slot, + 1
   u64 m1 = ~0ull;
+  const unsigned long long nch = (R + C - 1) / C;
+  bool ld_late = false;  // LD: a hand-over wait ran past kLdSpin (flag bit 3; nothing waits after it)
+  if constexpr (LD) {
+    if (threadIdx.x < NB) {
+      rel[threadIdx.x] = 0;
+      cml[threadIdx.x * CMS + A] = 0;
+    }
+    __syncthreads();  // (the only barrier: the two waves part here)
+    if (threadIdx.x >= 64) {  // the loader wave: chunks 0 and 1, then chunk c as soon as c - 2 is released
+      const GldsLanes<1> gl = glds_lanes<VI, 1>(p, g, k, lane);
+      for (unsigned long long c = 0; c < nch; ++c) {
+        const unsigned sl = (unsigned)(c & 1);
+        if (c >= 2) {
+          unsigned spins = 0;
+          while (__builtin_amdgcn_readfirstlane(*reinterpret_cast<const volatile unsigned *>(rel + sl)) <
+                 (unsigned)(c - 1)) {
+            if (++spins > kLdSpin) break;
+            __builtin_amdgcn_s_sleep(1);
+          }
+          if (spins > kLdSpin) break;  // the fold wave reports its own timeout
+        }
+        map_chunk_glds<VI, C, 1>(p, gl, g, k, c * C, R, wl + sl * SLOT, WS, vbase + sl * C * VI, cml + sl * CMS,
+                                 lane, false, p.diag, p.seq);
+      }
+      wait_vmcnt<0>();
+      return;
+    }
+  }
   if (kSpec) {
     for (unsigned long long x = lane; x < (2 + VO) * A; x += 64) mirror[x] = 0;
     for (unsigned long long x = lane; x < A; x += 64) {
@@ -1335,7 +1385,6 @@ __global__ __launch_bounds__(SH ? 256 : 64) void map_fold_kernel(MapPlan pk) {
   // (uniform values read through LDS / global memory go through readfirstlane, so that the fold's
   // control flow stays scalar)
   unsigned next_row = (!direct && nl > 0) ? __builtin_amdgcn_readfirstlane(lrow[0]) : 0xffffffffu;
-  const unsigned long long nch = (R + C - 1) / C;
   int cool = 0;
   bool anti = true;  // own values an antichain (scan precondition), refreshed after exact steps
 #ifdef MAP_STATS
@@ -1390,7 +1439,7 @@ __global__ __launch_bounds__(SH ? 256 : 64) void map_fold_kernel(MapPlan pk) {
     }
   } else if constexpr (RS) {  // chunks 0 and 1 into the two slots (W <= 128: one piece per step)
     gl1 = glds_lanes<VI, 1>(p, g, k, lane);
-    for (unsigned long long c = 0; c < 2 && c < nch; ++c)
+    for (unsigned long long c = 0; c < 2 && c < nch && !LD; ++c)
       map_chunk_glds<VI, C, 1>(p, gl1, g, k, c * C, R, wl + c * SLOT, WS, vbase + c * C * VI, cml + c * A, lane,
                                vpiece, p.diag);
   }
@@ -1432,7 +1481,7 @@ __global__ __launch_bounds__(SH ? 256 : 64) void map_fold_kernel(MapPlan pk) {
       const bool el = elig0 && (unsigned long long)next_row >= ch * C + n0;
       u64 *const img = wl + slot * SLOT;
       u64 *const vsl = vbase + slot * C * VI;
-      u64 *const cms = SH ? shr + sh_use * kShShared + 512 : cml + slot * A;
+      u64 *const cms = SH ? shr + sh_use * kShShared + 512 : cml + slot * CMS;
       u64 *const shs = shr + sh_use * kShShared;  // SH: chunk ch's shared slot
       shx = shs;
       MAP_TICK();
@@ -1460,6 +1509,12 @@ __global__ __launch_bounds__(SH ? 256 : 64) void map_fold_kernel(MapPlan pk) {
         }
         MAP_TOCK(cy_arr);
         MAP_TICK();
+      } else if constexpr (LD) {  // chunk ch's arrival flag (its last piece)
+        unsigned spins = 0;
+        while (!ld_late && __builtin_amdgcn_readfirstlane(*reinterpret_cast<const volatile unsigned *>(cms + A)) !=
+                               (unsigned)(ch + 1)) {
+          if (++spins > kLdSpin) ld_late = true;
+        }
       } else {
         if (ch + 1 < nch) {
           if (vpiece) wait_vmcnt<P1>();
@@ -1480,15 +1535,18 @@ __global__ __launch_bounds__(SH ? 256 : 64) void map_fold_kernel(MapPlan pk) {
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot is read: refill it
       if constexpr (SH) sh_pre = __builtin_amdgcn_readfirstlane(pre_raw);
+      if constexpr (LD) {
+        if (lane == 0) *reinterpret_cast<volatile unsigned *>(rel + slot) = (unsigned)(ch + 1);
+      }
       // a whole next chunk with every lane moving a piece: its pieces go out during the test
       const unsigned long long i2 = (ch + 2) * C;
-      const bool spread = el && ch + 2 < nch && i2 + C <= R && (2 + VI) * A == 128 && (!SH || ch + kShD < nch);
+      const bool spread = !LD && el && ch + 2 < nch && i2 + C <= R && (2 + VI) * A == 128 && (!SH || ch + kShD < nch);
       if constexpr (SH) {
         if (!spread) {
           if (ch + 2 < nch) sh_chunk_images(shl, i2, R, img);
           if (ch + kShD < nch) sh_chunk_shared(p, shl, g, ch + kShD, R, wv, shr + sh_iss * kShShared, lane);
         }
-      } else {
+      } else if constexpr (!LD) {
         if (ch + 2 < nch && !spread)
           map_chunk_glds<VI, C, 1>(p, gl1, g, k, i2, R, img, WS, vsl, cms, lane, vpiece, p.diag);
       }
@@ -1547,6 +1605,14 @@ __global__ __launch_bounds__(SH ? 256 : 64) void map_fold_kernel(MapPlan pk) {
 #pragma unroll
           for (int h = 0; h < 2; ++h) rg.cs[m][h] = rg.cs[m][h] > rA.cmp[m][h] ? rg.cs[m][h] : rA.cmp[m][h];
         continue;
+      }
+      if constexpr (LD) {  // the loader's copy of chunk ch+2 into this slot must land before it is overwritten
+        unsigned spins = 0;
+        while (!ld_late && ch + 2 < nch &&
+               __builtin_amdgcn_readfirstlane(*reinterpret_cast<const volatile unsigned *>(cms + A)) !=
+                   (unsigned)(ch + 3)) {
+          if (++spins > kLdSpin) ld_late = true;
+        }
       }
       wait_vmcnt<0>();
       if constexpr (SH) sh_store(rA, img, lane);
@@ -1633,7 +1699,7 @@ __global__ __launch_bounds__(SH ? 256 : 64) void map_fold_kernel(MapPlan pk) {
           MAP_TICK();
           if ((GL || RS) && s == 0 && j == n) {  // the whole chunk: its staged clock max
             const unsigned long long a = (unsigned long long)lane < A ? lane : A - 1;
-            const u64 x = SH ? shx[512 + a] : cml[slot * A + a];
+            const u64 x = SH ? shx[512 + a] : cml[slot * CMS + a];
             if ((unsigned long long)lane < A) cs[0] = cs[0] > x ? cs[0] : x;
           } else {  // acc.clock.merge of the skipped replicas: every read issued at once, range masked
             const unsigned long long a = (unsigned long long)lane < A ? lane : A - 1;
@@ -1930,9 +1996,12 @@ __global__ __launch_bounds__(SH ? 256 : 64) void map_fold_kernel(MapPlan pk) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         sh_chunk_images(shl, (ch + 2) * C, R, wl + slot * SLOT);
       } else if (ch + 2 < nch) {
+        if constexpr (LD) {  // the flag reads "not landed" until this re-issued copy lands
+          if (lane == 0) cml[slot * CMS + A] = 0;
+        }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         map_chunk_glds<VI, C, 1>(p, gl1, g, k, (ch + 2) * C, R, wl + slot * SLOT, WS, vbase + slot * C * VI,
-                                 cml + slot * A, lane, vpiece, p.diag);
+                                 cml + slot * CMS, lane, vpiece, p.diag, LD ? p.seq : nullptr);
       }
     }
     if constexpr (!GL && !RS) {
@@ -1992,7 +2061,7 @@ __global__ __launch_bounds__(SH ? 256 : 64) void map_fold_kernel(MapPlan pk) {
       p.o_vval[gk * p.Vout + o] = v;
     }
     if (p.o_nval) p.o_nval[gk] = present ? (unsigned)nv : 0u;
-    const unsigned f = (unsigned)ovf | (bad ? 2u : 0u) | (sh_late ? 8u : 0u);
+    const unsigned f = (unsigned)ovf | (bad ? 2u : 0u) | ((sh_late || ld_late) ? 8u : 0u);
     if (f) atomicOr(p.o_flags + g, f);
   }
 }
@@ -2005,8 +2074,9 @@ using namespace crdt;
 // chunk the fold skips entirely (one block per (group, chunk), lane = actor).
 __global__ __launch_bounds__(64) void map_chunk_max_kernel(const u64 *clock, long long c_rs, long long c_gs,
                                                            unsigned long long R, unsigned long long A,
-                                                           unsigned long long nch, unsigned C, u64 *out) {
+                                                           unsigned long long nch, unsigned C, u64 *out, u64 *seq) {
   const unsigned long long g = blockIdx.x / nch, ch = blockIdx.x % nch;
+  if (seq && g == 0 && threadIdx.x < 2) seq[2 * ch + threadIdx.x] = ch + 1;  // the LD path's arrival flags
   const unsigned long long i0 = ch * C, i1 = R < i0 + C ? R : i0 + C;
   for (unsigned long long a = threadIdx.x; a < A; a += 64) {
     u64 m = 0;
@@ -2018,21 +2088,22 @@ __global__ __launch_bounds__(64) void map_chunk_max_kernel(const u64 *clock, lon
   }
 }
 
-template <int APL, int VI, int VO, int CM, int NB, bool GL, int ITM, int NP = 0>
+template <int APL, int VI, int VO, int CM, int NB, bool GL, int ITM, int NP = 0, bool LD = false>
 static hipError_t launch_map_it(const MapPlan &p, unsigned long long blocks, hipStream_t s) {
   constexpr bool RS = NP > 0;
   constexpr int C = (GL || RS) ? CM : MapChunk<APL, VI, CM>::C;
   const size_t W = (2 + VI) * p.A;
   const size_t lds = (size_t)NB * C * (map_ws(W) + VI) * sizeof(u64) + kMapL * 2 * sizeof(unsigned) +
-                     (2 + VO) * p.A * sizeof(u64) + ((GL || RS) ? NB * p.A * sizeof(u64) : 0) +
-                     4 * p.A * sizeof(u64);
+                     (2 + VO) * p.A * sizeof(u64) + ((GL || RS) ? NB * (p.A + (LD ? 2 : 0)) * sizeof(u64) : 0) +
+                     4 * p.A * sizeof(u64) + (LD ? sizeof(u64) : 0);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
+  auto *fn = &map_fold_kernel<APL, VI, VO, CM, NB, GL, ITM, NP, false, LD>;
   if (lds > 64 * 1024) {  // beyond the default dynamic-LDS limit (gfx950 has 160 KB per CU)
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&map_fold_kernel<APL, VI, VO, CM, NB, GL, ITM, NP>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL((map_fold_kernel<APL, VI, VO, CM, NB, GL, ITM, NP>), dim3((unsigned)blocks), dim3(64), lds, s, p);
+  hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(LD ? 128 : 64), lds, s, p);
   return hipGetLastError();
 }
 
@@ -2040,6 +2111,8 @@ static hipError_t launch_map_it(const MapPlan &p, unsigned long long blocks, hip
 // step so the LDS scans of the exact loop unroll ceil(A / 4) iterations.
 template <int VI>
 static hipError_t launch_map_rs(const MapPlan &p, unsigned long long blocks, hipStream_t s) {
+  // the loader-wave form where every lane moves a piece of every step image (config 4's shape)
+  if (p.seq && (2 + VI) * p.A == 128 && p.lazyv) return launch_map_it<1, VI, 4, 16, 2, false, 8, 4, true>(p, blocks, s);
   if (p.A <= 8) return launch_map_it<1, VI, 4, 16, 2, false, 2, 1>(p, blocks, s);
   if (p.A <= 16) return launch_map_it<1, VI, 4, 16, 2, false, 4, 2>(p, blocks, s);
   return launch_map_it<1, VI, 4, 16, 2, false, 8, 4>(p, blocks, s);
@@ -2118,8 +2191,8 @@ static int map_lub_impl(crdt_ctx *ctx, const crdt_map_batch *in, const u64 *doff
   if (Vout == 0) return fail(ctx, CRDT_EINVAL, "map_lub_many: Vout must be >= 1");
   if (R > 0 && (!in->clock || !in->ec || (V > 0 && (!in->vclk || !in->vval))))
     return fail(ctx, CRDT_EINVAL, "map_lub_many: NULL input");
-  if (A > 256) return fail(ctx, CRDT_EUNSUPPORTED, "map_lub_many: A = %zu > 256 actors", A);
-  if (V > 8) return fail(ctx, CRDT_EUNSUPPORTED, "map_lub_many: V = %zu > 8 value slots per key", V);
+  // past the fast kernels' register shapes: the workgroup-per-key fold (map_wide.hip)
+  const bool wide = A > 256 || V > 8;
   if (Vout > 64) return fail(ctx, CRDT_EUNSUPPORTED, "map_lub_many: Vout = %zu > 64", Vout);
   if (G * K > 0x7fffffffULL) return fail(ctx, CRDT_EUNSUPPORTED, "map_lub_many: G*K too large");
   if (R > 0xfffffffeULL) return fail(ctx, CRDT_EUNSUPPORTED, "map_lub_many: R too large");
@@ -2169,7 +2242,7 @@ static int map_lub_impl(crdt_ctx *ctx, const crdt_map_batch *in, const u64 *doff
   // LDS-DMA staging when every step image is whole 16-byte pieces (A even, 16-byte aligned
   // rows and strides) and the state fits 4 values; register staging otherwise
   const bool even = ((p.c_rs | p.c_gs | p.e_rs | p.e_gs | p.vc_rs | p.vc_gs) & 1) == 0;
-  const bool glds = ctx->tune.map_glds && R > 0 && A <= 64 && (A & 1) == 0 && (V == 1 || V == 2) &&
+  const bool glds = !wide && ctx->tune.map_glds && R > 0 && A <= 64 && (A & 1) == 0 && (V == 1 || V == 2) &&
                     want <= 4 && even && aligned16(p.clock) && aligned16(p.ec) && aligned16(p.vclk) &&
                     G * ((R + 7) / 8) < 0x7fffffffULL;
   // the RS path: register-staged whole-chunk skip, LDS only for chunks it cannot skip
@@ -2178,7 +2251,8 @@ static int map_lub_impl(crdt_ctx *ctx, const crdt_map_batch *in, const u64 *doff
   // scratch: [def_off copy | chunk clock maxima]
   const size_t off_b = D > 0 || doff ? ((G + 1) * sizeof(size_t) + 255) / 256 * 256 : 0;
   if (glds) p.nch = (R + gC - 1) / gC;
-  const size_t cm_b = glds ? G * p.nch * A * sizeof(u64) : 0;
+  const bool ld = rs && ctx->tune.map_ld && !(ctx->tune.map_sh && A == 32 && V == 2 && K % 4 == 0);
+  const size_t cm_b = glds ? G * p.nch * A * sizeof(u64) + (ld ? p.nch * 2 * sizeof(u64) : 0) : 0;
   if (off_b + cm_b > 0)
     if (int rc = ensure_scratch(ctx, off_b + cm_b)) return rc;
   if (doff && D == 0)  // no pool: only the offsets' check (every entry must be 0)
@@ -2197,13 +2271,19 @@ static int map_lub_impl(crdt_ctx *ctx, const crdt_map_batch *in, const u64 *doff
     p.def_keys = (const u64 *)in->def_keys;
   }
   const unsigned long long blocks = G * K;
-  timing_begin(ctx, "map_fold");
   hipError_t he;
+  if (wide) {
+    if (int rc = map_lub_wide(ctx, in, p.def_off, out)) return rc;
+    he = hipSuccess;
+  } else {
+  timing_begin(ctx, "map_fold");
   if (glds) {
     u64 *cm = reinterpret_cast<u64 *>(static_cast<char *>(ctx->scratch) + off_b);
     p.cmax = cm;
+    p.seq = ld ? cm + G * p.nch * A : nullptr;
     hipLaunchKernelGGL(map_chunk_max_kernel, dim3((unsigned)(G * p.nch)), dim3(64), 0, ctx->stream, p.clock,
-                       p.c_rs, p.c_gs, (unsigned long long)R, (unsigned long long)A, p.nch, gC, cm);
+                       p.c_rs, p.c_gs, (unsigned long long)R, (unsigned long long)A, p.nch, gC, cm,
+                       const_cast<u64 *>(p.seq));
     if (rs && ctx->tune.map_sh && A == 32 && V == 2 && K % 4 == 0)
       he = launch_map_sh(p, blocks, ctx->stream);
     else if (rs)
@@ -2218,6 +2298,7 @@ static int map_lub_impl(crdt_ctx *ctx, const crdt_map_batch *in, const u64 *doff
     else he = launch_map_vi<4>(p, VI, blocks, ctx->stream);
   }
   timing_end(ctx);
+  }
   if (he != hipSuccess) return hip_fail(ctx, he, "map_fold_kernel launch");
 
   if (D == 0) return CRDT_OK;
