@@ -246,8 +246,9 @@ int crdt_orswot_lub_many_doff(crdt_ctx *ctx, const crdt_orswot_batch *in, const 
  * slots (the state is incomplete: retry with a larger Dcap), bit 1 = an op named an actor,
  * member or rm row out of range or a bad kind / member range (reversed, or ending past n_mem)
  * (that op, or its bad members, were skipped), bit 2 = def_count[s] > Dcap on input, bit 3 = op_off[s..s+1] invalid (bits 2 and 3:
- * state left untouched).  Limits: A <= 256 (the first slots of the deferred list are kept in LDS,
- * as many as 64 KiB holds; the rest stay in the state's own slots). */
+ * state left untouched).  Limits: A <= 1024 (1, 4 or 16 clock words per lane; the first slots of
+ * the deferred list are kept in LDS, as many as 64 KiB holds; the rest stay in the state's own
+ * slots, so Dcap is not bounded). */
 typedef struct crdt_orswot_states {
   size_t N, M, A, Dcap;
   uint64_t *clock;
@@ -286,7 +287,8 @@ int crdt_orswot_apply_batch(crdt_ctx *ctx, const crdt_orswot_states *states, con
  * slots (self's survivors first, in slot order, then other's; identical clocks merge their member
  * sets, as the reference's HashMap<VClock, HashSet<M>> does).
  * status[s] (device u32): bit 0 = more survivors than self's Dcap (state incomplete), bit 2 =
- * def_count above Dcap on input (state untouched).  Limit: Dcap(self) + Dcap(other) <= 512. */
+ * def_count above Dcap on input (state untouched).  Dcap is not bounded: a pair with more than
+ * 512 removes is forgotten in further passes of 512 (forgets compose and commute). */
 int crdt_orswot_merge_batch(crdt_ctx *ctx, const crdt_orswot_states *self, const crdt_orswot_states *other,
                             uint32_t *status);
 
@@ -338,8 +340,9 @@ int crdt_map_forget_batch(crdt_ctx *ctx, const crdt_map_states *states, const ui
  * key range reversed or ending past n_keys),
  * bits 2-3 = invalid input (state untouched), bit 4 = a register needed more than V values (the
  * state is incomplete: retry with more slots), bit 5 = internal slot invariant violated (never
- * expected; the value was not written).  Limits: A <= 256, 1 <= V <= 8 (the first deferred slots
- * are kept in LDS, as many as 64 KiB holds; the rest stay in the state's own slots). */
+ * expected; the value was not written).  Limits: A <= 1024, V >= 1 (the value slots are walked in
+ * HBM, so V is not bounded; the first deferred slots are kept in LDS, as many as 64 KiB holds; the
+ * rest stay in the state's own slots). */
 typedef struct crdt_map_ops {
   size_t n_ops;
   const uint64_t *op_off;   /* [N+1]       */
@@ -375,7 +378,7 @@ typedef struct crdt_map_deferred {
  * written from slot 0, empty slots zeroed).  Deferred removes as crdt_orswot_merge_batch over key
  * bitmaps.  status[s]: bit 0 = deferred slots exhausted, bit 2 = invalid def_count (untouched),
  * bit 4 = some register needed more than self's V slots (that key is incomplete).
- * Limits: A <= 256, 1 <= V <= 8 on each side, Dcap(self) + Dcap(other) <= 512. */
+ * Limits: A <= 1024, 1 <= V <= 32 on each side (Dcap is not bounded). */
 int crdt_map_merge_batch(crdt_ctx *ctx, const crdt_map_states *self, const crdt_map_deferred *self_def,
                          const crdt_map_states *other, const crdt_map_deferred *other_def, uint32_t *status);
 
@@ -501,8 +504,9 @@ int crdt_lwwreg_lub_many_sharded(crdt_ctx *ctx, const uint64_t *marker, const ui
  * report it).  The state holds VO = 2*pow2(V') values, V' the
  * smallest power of two with V' >= V and 2V' >= min(8, max(Vout, Vstate)); VO <= 8.
  * Deferred output as for Orswot (def_keep / def_keys over keys).
- * Limits: A <= 256, V <= 8, Vout <= 64; the fold state holds up to 16 values per key (bit 2 of
- * flags when a key needs more). */
+ * Limits: A <= 1024, V <= 16, Vout <= 64; the fold state holds up to 16 values per key (bit 2 of
+ * flags when a key needs more).  A > 256 or V > 8 runs the workgroup-per-key fold (csrc/map_wide.hip:
+ * the same exact left fold, no speculative scan — a correctness path, not a tuned one). */
 typedef struct crdt_map_batch {
   size_t G, R, K, A, V;
   const uint64_t *clock;
@@ -568,7 +572,8 @@ int crdt_map_lub_many_sharded(crdt_ctx *ctx, const crdt_map_batch *in, size_t k0
  *                clk_pool[clk_row[o]*A ..], val: val[o] }; status[i] bit 1 = an op's clk_row out
  *                of range (skipped), bit 3 = op_off invalid (register untouched), bit 4 = more than
  *                V values.
- * Limits: A <= 256, 1 <= V <= 8 (lub_many: V <= 8, Vout <= 16). */
+ * Limits: A <= 1024, 1 <= V <= 16 (lub_many: Vout <= 16); A > 256 or V > 8 run one workgroup of
+ * ceil(A / 64) waves per register. */
 typedef struct crdt_mvreg_states {
   size_t N, A, V;
   uint64_t *vclk;

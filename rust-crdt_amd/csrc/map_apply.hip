@@ -15,15 +15,16 @@
 //           (values too), else every value clock forgets rm and an emptied value is dropped
 //       if !(rm <= C) (C.partial_cmp(rm) in {None, Less}): defer (rm, keyset), OR-ing the keys
 //           into an existing deferred with the identical clock
-// One wave per state (lanes = actors, A <= 256; the state's clock in registers, its deferred list
+// One wave per state (lanes = actors, A <= 1,024 with 1-16 clock words per lane; V unbounded: the
+// value slots are walked in HBM; the state's clock in registers, its deferred list
 // in LDS for the whole stream, entries and values in HBM), as orswot_apply.hip.
 #include "common.hpp"
 #include "group.hpp"
 
 namespace crdt {
 
-constexpr int kMA = 4;  // clock words per lane (A <= 256)
-constexpr int kMaxV = 8;
+constexpr int kMA = 4;      // clock words per lane of the fast instances (A <= 256)
+constexpr int kMAWide = 16;  // ... of the widest instance (A <= 1,024; round 4: the reference is unbounded)
 
 struct MapApplyPlan {
   u64 *clock;
@@ -790,8 +791,9 @@ extern "C" int crdt_map_apply_batch(crdt_ctx *ctx, const crdt_map_states *m, uin
   if (!m || !ops || !status) return fail(ctx, CRDT_EINVAL, "map_apply_batch: NULL argument");
   const size_t N = m->N, K = m->K, A = m->A, V = m->V;
   if (N == 0) return CRDT_OK;
-  if (A == 0 || A > (size_t)(kMA * kWave) || V == 0 || V > (size_t)kMaxV || K == 0)
-    return fail(ctx, CRDT_EINVAL, "map_apply_batch: need 1 <= A <= %d, 1 <= V <= %d, K >= 1", kMA * kWave, kMaxV);
+  if (A == 0 || V == 0 || K == 0) return fail(ctx, CRDT_EINVAL, "map_apply_batch: need A, V, K >= 1");
+  if (A > (size_t)(kMAWide * kWave))
+    return fail(ctx, CRDT_EUNSUPPORTED, "map_apply_batch: A = %zu > %d actors", A, kMAWide * kWave);
   if (!m->clock || !m->ec || !m->vclk || !m->vval || !def_count || !ops->op_off)
     return fail(ctx, CRDT_EINVAL, "map_apply_batch: NULL buffer");
   if (Dcap && (!def_clock || !def_keys)) return fail(ctx, CRDT_EINVAL, "map_apply_batch: NULL deferred buffers");
@@ -840,8 +842,14 @@ extern "C" int crdt_map_apply_batch(crdt_ctx *ctx, const crdt_map_states *m, uin
   else if (A <= (size_t)(2 * kWave))
     hipLaunchKernelGGL((sp ? map_apply_kernel<2, true> : map_apply_kernel<2, false>), grid, block, per_wave * wpb,
                        ctx->stream, p);
-  else
+  else if (A <= (size_t)(kMA * kWave))
     hipLaunchKernelGGL((sp ? map_apply_kernel<kMA, true> : map_apply_kernel<kMA, false>), grid, block,
+                       per_wave * wpb, ctx->stream, p);
+  else if (A <= (size_t)(8 * kWave))  // wide states: more clock words per lane (a correctness path)
+    hipLaunchKernelGGL((sp ? map_apply_kernel<8, true> : map_apply_kernel<8, false>), grid, block, per_wave * wpb,
+                       ctx->stream, p);
+  else
+    hipLaunchKernelGGL((sp ? map_apply_kernel<kMAWide, true> : map_apply_kernel<kMAWide, false>), grid, block,
                        per_wave * wpb, ctx->stream, p);
   timing_end(ctx);
   CRDT_HIP(ctx, hipGetLastError());

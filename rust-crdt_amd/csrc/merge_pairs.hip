@@ -135,7 +135,9 @@ struct OrswotPairPlan {
   const uint32_t *d2n;
   unsigned long long D2;
   unsigned long long N, M, A, Mw, mblocks;
-  int lp_log;  // log2 lanes per member row (pieces of V words)
+  int lp_log;     // log2 lanes per member row (pieces of V words)
+  unsigned dbase;  // the removes this launch applies: [dbase, dbase + 32 * kPairGroups) of the pair's
+  int join;        // 1: join then forget; 0: forget only (a later pass of a pair with more removes)
 };
 
 __device__ __forceinline__ u64 cell_join(u64 e1, u64 e2, u64 c1, u64 c2) {  // orswot.rs:84-138
@@ -149,7 +151,9 @@ __device__ __forceinline__ u64 cell_join(u64 e1, u64 e2, u64 c1, u64 c2) {  // o
 // Workgroup = (pair s, block of kPairRows member rows); 2^lp_log lanes cover a row in V-word
 // pieces (V = 2: 16-byte non-temporal accesses), 256 >> lp_log rows per pass.  Per block the
 // deferred removes of both sides are turned into hit masks in LDS (bit d of hit[g][row] = remove
-// 32g + d names that member); a cell with hits forgets by each hit remove's rm (global, L2).
+// dbase + 32g + d names that member); a cell with hits forgets by each hit remove's rm (global, L2).
+// A pair with more than 32 * kPairGroups removes gets further forget-only launches (join = 0) for
+// the rest: forgets of the joined entries compose and commute, so the passes give the same result.
 template <int V, int kPairRows, int kPairUR = kPairUR>
 __global__ __launch_bounds__(kBlock) void orswot_pair_join_kernel(OrswotPairPlan p) {
   __shared__ unsigned hit[kPairGroups][kPairRows];
@@ -158,16 +162,18 @@ __global__ __launch_bounds__(kBlock) void orswot_pair_join_kernel(OrswotPairPlan
   const unsigned n1 = p.d1n[s], n2 = p.d2n ? p.d2n[s] : 0u;
   if (n1 > p.D1 || n2 > p.D2) return;  // reported by pair_deferred_kernel, state untouched
   const unsigned nd = n1 + n2;
-  const unsigned ng = (nd + 31) / 32;
+  if (!p.join && nd <= p.dbase) return;  // a forget-only pass with none of this pair's removes
+  const unsigned ndp = nd > p.dbase ? (nd - p.dbase < 32u * kPairGroups ? nd - p.dbase : 32u * kPairGroups) : 0u;
+  const unsigned ng = (ndp + 31) / 32;
   if (ng) {  // workgroup-uniform: most pairs carry no removes and skip the masks and the barrier
     for (unsigned i = threadIdx.x; i < ng * kPairRows; i += kBlock) {
       const unsigned g = i / kPairRows, r = i % kPairRows;
       const unsigned long long m = m0 + r;
       unsigned mask = 0;
       if (m < p.M) {
-        for (unsigned d = g * 32; d < nd && d < g * 32 + 32; ++d) {
+        for (unsigned d = p.dbase + g * 32; d < nd && d < p.dbase + g * 32 + 32; ++d) {
           const u64 *b = d < n1 ? p.d1b + (s * p.D1 + d) * p.Mw : p.d2b + (s * p.D2 + (d - n1)) * p.Mw;
-          if ((b[m / 64] >> (m % 64)) & 1ull) mask |= 1u << (d - g * 32);
+          if ((b[m / 64] >> (m % 64)) & 1ull) mask |= 1u << (d - p.dbase - g * 32);
         }
       }
       hit[g][r] = mask;
@@ -197,7 +203,7 @@ __global__ __launch_bounds__(kBlock) void orswot_pair_join_kernel(OrswotPairPlan
         const unsigned long long m = m0 + r;
         if (r >= kPairRows || m >= p.M) break;
         const u64 *pe1 = p.e1 + s * p.e1_s + m * p.e1_m + a0;
-        const u64 *pe2 = p.e2 + s * p.e2_s + m * p.e2_m + a0;
+        const u64 *pe2 = p.join ? p.e2 + s * p.e2_s + m * p.e2_m + a0 : pe1;
         if constexpr (V == 2) {
           const u64x2 a = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(pe1));
           const u64x2 b = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(pe2));
@@ -212,12 +218,14 @@ __global__ __launch_bounds__(kBlock) void orswot_pair_join_kernel(OrswotPairPlan
         const int r = rb + u * rows_per_pass;
         const unsigned long long m = m0 + r;
         if (r >= kPairRows || m >= p.M) break;
+        if (p.join) {
 #pragma unroll
-        for (int v = 0; v < V; ++v) x[u][v] = cell_join(x[u][v], y[u][v], k1[v], k2[v]);
+          for (int v = 0; v < V; ++v) x[u][v] = cell_join(x[u][v], y[u][v], k1[v], k2[v]);
+        }
         for (unsigned g = 0; g < ng; ++g) {
           unsigned mask = hit[g][r];
           while (mask) {
-            const unsigned d = g * 32 + __builtin_ctz(mask);
+            const unsigned d = p.dbase + g * 32 + __builtin_ctz(mask);
             mask &= mask - 1;
             const u64 *rm = d < n1 ? p.d1c + (s * p.D1 + d) * p.A : p.d2c + (s * p.D2 + (d - n1)) * p.A;
 #pragma unroll
@@ -240,7 +248,7 @@ __global__ __launch_bounds__(kBlock) void orswot_pair_join_kernel(OrswotPairPlan
 }
 
 // ---- Map<K, MVReg> key merge --------------------------------------------------------------------
-constexpr int kMapPairMaxV = 8;
+constexpr int kMapPairMaxV = 32;  // value slots per side (u32 slot masks of the generic kernel)
 
 struct MapPairPlan {
   unsigned long long N, K, A, V1, V2, Kw;
@@ -891,9 +899,7 @@ extern "C" int crdt_orswot_merge_batch(crdt_ctx *ctx, const crdt_orswot_states *
       (M && (a.entry_mstride < A || b.entry_mstride < A || a.entry_sstride < M * a.entry_mstride ||
              b.entry_sstride < M * b.entry_mstride)))
     return fail(ctx, CRDT_EINVAL, "orswot_merge_batch: strides smaller than the rows they hold");
-  if (a.Dcap + b.Dcap > (size_t)(32 * kPairGroups))
-    return fail(ctx, CRDT_EUNSUPPORTED, "orswot_merge_batch: Dcap(self) + Dcap(other) = %zu > %d", a.Dcap + b.Dcap,
-                32 * kPairGroups);
+  if (a.Dcap + b.Dcap > 0xffffffffull) return fail(ctx, CRDT_EUNSUPPORTED, "orswot_merge_batch: Dcap too large");
   const size_t Mw = (M + 63) / 64;
   CRDT_HIP(ctx, hipSetDevice(ctx->device));
   if (M) {
@@ -909,9 +915,13 @@ extern "C" int crdt_orswot_merge_batch(crdt_ctx *ctx, const crdt_orswot_states *
                      b.entry_sstride, (const u64 *)a.clock, a.clock_stride, (const u64 *)b.clock, b.clock_stride,
                      (const u64 *)a.def_clock, (const u64 *)a.def_members, a.def_count, a.Dcap,
                      (const u64 *)b.def_clock, (const u64 *)b.def_members, b.Dcap ? b.def_count : nullptr, b.Dcap,
-                     N, M, A, Mw, mblocks, lp};
+                     N, M, A, Mw, mblocks, lp, 0u, 1};
     timing_begin(ctx, "orswot_pair_join");
     const dim3 grid((unsigned)(N * mblocks));
+    // pass 0 joins and applies removes [0, 512); pass k > 0 only forgets by removes [512 k, 512 k + 512)
+    for (size_t db = 0; db == 0 || db < a.Dcap + b.Dcap; db += 32 * kPairGroups) {
+    p.dbase = (unsigned)db;
+    p.join = db == 0 ? 1 : 0;
     // pocc > 0: at most pocc workgroups per CU (dynamic LDS padding), fewer HBM requests in flight
     const size_t pad = ctx->tune.pair_occ > 0 ? (size_t)(160 * 1024 / ctx->tune.pair_occ) - kPairGroups * rows * 4 - 256 : 0;
 #define CRDT_PAIR_JOIN(VV, RR) hipLaunchKernelGGL((orswot_pair_join_kernel<VV, RR>), grid, dim3(kBlock), pad, ctx->stream, p)
@@ -927,6 +937,7 @@ extern "C" int crdt_orswot_merge_batch(crdt_ctx *ctx, const crdt_orswot_states *
       if (rows == 64) CRDT_PAIR_JOIN(1, 64);
       else if (rows == 256) CRDT_PAIR_JOIN(1, 256);
       else CRDT_PAIR_JOIN(1, 128);
+    }
     }
 #undef CRDT_PAIR_JOIN
     timing_end(ctx);
@@ -951,9 +962,10 @@ extern "C" int crdt_map_merge_batch(crdt_ctx *ctx, const crdt_map_states *self, 
     return fail(ctx, CRDT_EINVAL, "map_merge_batch: self and other differ in N, K or A");
   const size_t N = a.N, K = a.K, A = a.A;
   if (N == 0) return CRDT_OK;
-  if (A == 0 || A > 4 * (size_t)kWave || a.V == 0 || a.V > (size_t)kMapPairMaxV || b.V == 0 ||
-      b.V > (size_t)kMapPairMaxV)
-    return fail(ctx, CRDT_EINVAL, "map_merge_batch: need 1 <= A <= 256 and 1 <= V <= %d on both sides", kMapPairMaxV);
+  if (A == 0 || a.V == 0 || b.V == 0) return fail(ctx, CRDT_EINVAL, "map_merge_batch: need A, V >= 1 on both sides");
+  if (A > 16 * (size_t)kWave || a.V > (size_t)kMapPairMaxV || b.V > (size_t)kMapPairMaxV)
+    return fail(ctx, CRDT_EUNSUPPORTED, "map_merge_batch: need A <= %d and V <= %d on both sides", 16 * kWave,
+                kMapPairMaxV);
   if (!a.clock || !b.clock || !self_def->count || (K && (!a.ec || !a.vclk || !a.vval || !b.ec || !b.vclk || !b.vval)))
     return fail(ctx, CRDT_EINVAL, "map_merge_batch: NULL buffer");
   if ((self_def->Dcap && (!self_def->clock || !self_def->keys)) ||
@@ -975,7 +987,7 @@ extern "C" int crdt_map_merge_batch(crdt_ctx *ctx, const crdt_map_states *self, 
                   other_def->Dcap ? other_def->count : nullptr, other_def->Dcap, status};
     const unsigned grid = pair_grid(ctx, (unsigned long long)N * K, ctx->tune.map_pair_bpc);
     timing_begin(ctx, "map_pair_join");
-    if (ctx->tune.map_pair_reg && a.V <= 4 && b.V <= 4) {  // register-resident rows (one load batch per key)
+    if (ctx->tune.map_pair_reg && a.V <= 4 && b.V <= 4 && A <= 4 * (size_t)kWave) {  // register-resident rows
       if (A <= 16 && ctx->tune.map_pair_reg == 1)
         hipLaunchKernelGGL((map_pair_join_seg_kernel<16, 4>), dim3(grid), dim3(kBlock), 0, ctx->stream, p);
       else if (A <= 32 && ctx->tune.map_pair_reg == 1)
@@ -992,8 +1004,12 @@ extern "C" int crdt_map_merge_batch(crdt_ctx *ctx, const crdt_map_states *self, 
       hipLaunchKernelGGL(map_pair_join_kernel<1>, dim3(grid), dim3(kBlock), 0, ctx->stream, p);
     else if (A <= 2 * (size_t)kWave)
       hipLaunchKernelGGL(map_pair_join_kernel<2>, dim3(grid), dim3(kBlock), 0, ctx->stream, p);
-    else
+    else if (A <= 4 * (size_t)kWave)
       hipLaunchKernelGGL(map_pair_join_kernel<4>, dim3(grid), dim3(kBlock), 0, ctx->stream, p);
+    else if (A <= 8 * (size_t)kWave)  // wide states (round 4): more clock words per lane
+      hipLaunchKernelGGL(map_pair_join_kernel<8>, dim3(grid), dim3(kBlock), 0, ctx->stream, p);
+    else
+      hipLaunchKernelGGL(map_pair_join_kernel<16>, dim3(grid), dim3(kBlock), 0, ctx->stream, p);
     timing_end(ctx);
     CRDT_HIP(ctx, hipGetLastError());
   }

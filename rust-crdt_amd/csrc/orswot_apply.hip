@@ -17,7 +17,7 @@
 //       an existing deferred with the identical clock (HashMap keyed by the whole VClock)
 // Ops of one state are sequential (apply is not commutative: the seen test and the deferred
 // removes depend on order), so the unit of parallelism is the state: one wave per state, lanes
-// over actors (clock rows in registers, A <= 256) or over the op's member list.  The op headers
+// over actors (clock rows in registers, A <= 1,024) or over the op's member list.  The op headers
 // of 64 ops are loaded at once (lane = op) and read out with readlane; the deferred list lives in
 // LDS for the whole stream.  Exact for ANY input state (apply_deferred re-forgets every deferred
 // member row, as the reference does, instead of assuming the invariant the reference's own
@@ -27,8 +27,8 @@
 
 namespace crdt {
 
-constexpr int kApplyMaxA = 256;
-constexpr int kCAMax = kApplyMaxA / kWave;  // clock words per lane at the widest A
+constexpr int kApplyMaxA = 1024;  // the A <= 1,024 instance: 16 clock words per lane
+constexpr int kCAMax = 4;         // clock words per lane of the A <= 256 instance
 constexpr unsigned kBadOp = 0xFFFFFFFFu, kRmOp = 0xFFFFFFFEu;  // packed op header tags
 
 struct OrswotApplyPlan {
@@ -395,6 +395,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7))) voi
 }
 __global__ __launch_bounds__(kBlock) void orswot_apply_kernel_a256(OrswotApplyPlan p) {
   orswot_apply_body<kCAMax>(p);
+}
+// Wide states (A <= 1,024, round 4: the reference's VClock is unbounded): 16 clock words per lane,
+// the same body — a correctness path, not a tuned one.
+__global__ __launch_bounds__(kBlock) void orswot_apply_kernel_a1024(OrswotApplyPlan p) {
+  orswot_apply_body<16>(p);
 }
 
 // ---- Sixteen lanes per state (A <= 64) --------------------------------------------------------
@@ -794,8 +799,10 @@ extern "C" int crdt_orswot_apply_batch(crdt_ctx *ctx, const crdt_orswot_states *
   const dim3 grid((unsigned)(want < cap ? want : cap)), block(wpb * kWave);
   if (s.A <= (size_t)kWave)
     hipLaunchKernelGGL(orswot_apply_kernel_a64, grid, block, per_wave * wpb, ctx->stream, p);
-  else
+  else if (s.A <= (size_t)(kCAMax * kWave))
     hipLaunchKernelGGL(orswot_apply_kernel_a256, grid, block, per_wave * wpb, ctx->stream, p);
+  else
+    hipLaunchKernelGGL(orswot_apply_kernel_a1024, grid, block, per_wave * wpb, ctx->stream, p);
   timing_end(ctx);
   CRDT_HIP(ctx, hipGetLastError());
   return CRDT_OK;

@@ -149,12 +149,14 @@ pub trait BatchCvRDT: CvRDT + Sized {
 /// Capacity limits of the library this module binds (include/crdt_gpu.h; checked against the
 /// header's stated limits by tests/test_rust_shim.py).  Past them a call returns `GpuError` with
 /// `CRDT_EUNSUPPORTED` and leaves its inputs untouched.
-/// Values per MVReg register in a Map input (`crdt_map_lub_many`, `crdt_map_merge_batch`: V <= 8).
-pub const MAP_MAX_VALUES: usize = 8;
-/// Actors of the Map and Orswot-apply kernels (A <= 256).
-pub const MAP_MAX_ACTORS: usize = 256;
-/// Deferred-remove slots of a pairwise merge, self + other (`Dcap(self) + Dcap(other) <= 512`).
-pub const MERGE_MAX_DEFERRED: usize = 512;
+/// Values per MVReg register (`crdt_map_lub_many`: V <= 16; `crdt_mvreg_*`: V <= 16;
+/// `crdt_map_merge_batch` takes up to 32 per side, the smallest limit is the one checked here).
+pub const MAP_MAX_VALUES: usize = 16;
+/// Actors of the Map, MVReg and Orswot-apply kernels (A <= 1024).
+pub const MAP_MAX_ACTORS: usize = 1024;
+/// Deferred-remove slots of a pairwise merge, self + other: not bounded by the library (a pair
+/// with more than 512 removes is forgotten in further passes), so only the address space limits it.
+pub const MERGE_MAX_DEFERRED: usize = usize::MAX;
 
 fn unsupported(msg: String) -> GpuError {
     GpuError { code: ffi::CRDT_EUNSUPPORTED, msg }

@@ -108,3 +108,164 @@ def test_map_wide_op_replay(gpu_ctx):
               def_clock=widen(d["def_clock"]), def_keys=d["def_keys"])
     exp = _map_check(gpu_ctx, wd)
     assert exp is not None and exp[5]  # surviving deferred removes exercised
+
+
+# ---- standalone MVReg (csrc/mvreg.hip, BLK = true: a workgroup per register) --------------------------
+from crdts_gpu import intern  # noqa: E402
+from test_gpu_mvreg import dense_regs, obj_regs, rand_regs  # noqa: E402
+
+
+def spread(regs, A):
+    """Actor a of a register -> column (37 a) mod A: a few live actors spread over all A columns."""
+    out = []
+    for r in regs:
+        out.append(O.MVReg([(O.VClock({(37 * a) % A: k for a, k in c.dots.items()}), v) for c, v in r.vals]))
+    return out
+
+
+@pytest.mark.parametrize("A,V,nact", [(300, 4, 8), (1024, 4, 8), (64, 12, 12), (300, 12, 12)])
+def test_mvreg_lub_many_wide(gpu_ctx, A, V, nact):
+    """Left folds of registers at A = 300 / 1,024 actors and V = 12 value slots equal the oracle's
+    MVReg::merge fold (mvreg.rs:112-128), values in the reference's Vec order."""
+    rng = np.random.default_rng(A + V)
+    G, R = 5, 30
+    regs = spread(rand_regs(rng, G * R, A, nact, V, steps=14 if V > 8 else 6, group=R), A)
+    actors, vals = intern.Index(list(range(A))), intern.Index()
+    vc, vv = dense_regs(regs, actors, V, vals)
+    folds = []
+    for g in range(G):
+        acc = O.MVReg()
+        for r in regs[g * R:(g + 1) * R]:
+            acc.merge(r)
+        folds.append(acc)
+    assert max(len(f.vals) for f in folds) <= 16
+    res = cg.mvreg.lub_many(to_dev(vc.reshape(G, R, V, A)), to_dev(vv.reshape(G, R, V)), vout=16)
+    got = obj_regs(to_host(res.vclk), to_host(res.vval), actors, vals, res.nval.cpu().numpy())
+    for g in range(G):
+        assert got[g].vals == folds[g].vals
+
+
+@pytest.mark.parametrize("A,V", [(300, 3), (1024, 2), (40, 12)])
+def test_mvreg_merge_batch_wide(gpu_ctx, A, V):
+    rng = np.random.default_rng(300 + A + V)
+    N = 120
+    a_regs = rand_regs(rng, N, A, min(A, 300), V)
+    b_regs = rand_regs(rng, N, A, min(A, 300), V)
+    actors, vals = intern.Index(list(range(A))), intern.Index()
+    svc, svv = dense_regs(a_regs, actors, min(16, 2 * V), vals)
+    ovc, ovv = dense_regs(b_regs, actors, V, vals)
+    s_c, s_v = to_dev(svc), to_dev(svv)
+    st = cg.mvreg.merge_batch(s_c, s_v, to_dev(ovc), to_dev(ovv)).cpu().numpy()
+    got = obj_regs(to_host(s_c), to_host(s_v), actors, vals)
+    for i in range(N):
+        exp = a_regs[i].copy()
+        exp.merge(b_regs[i])
+        if len(exp.vals) <= svc.shape[1]:
+            assert st[i] == 0 and got[i].vals == exp.vals, i
+        else:
+            assert st[i] & 16, i
+
+
+@pytest.mark.parametrize("A,V", [(300, 6), (1024, 6), (50, 12)])
+def test_mvreg_apply_batch_wide(gpu_ctx, A, V):
+    rng = np.random.default_rng(400 + A + V)
+    N = 100
+    regs = rand_regs(rng, N, A, min(A, 200), 2)
+    streams, exp = [], []
+    for r in regs:
+        e = r.copy()
+        ops = []
+        for _ in range(rng.integers(0, 9)):
+            c = e.clock() if rng.random() < 0.6 else O.VClock()
+            c = c.copy()
+            if rng.random() < 0.85:
+                for a in rng.choice(min(A, 200), size=rng.integers(1, 3), replace=False):
+                    c.apply(O.Dot(int(a), c.get(int(a)) + int(rng.integers(0, 3))))
+            v = int(rng.integers(0, 1000))
+            ops.append((c, v))
+            e.apply(O.MVRegPut(c, v))
+        streams.append(ops)
+        exp.append(e)
+    actors, vals = intern.Index(list(range(A))), intern.Index()
+    vc, vv = dense_regs(regs, actors, V, vals)
+    enc = [[({a: k for a, k in c.dots.items()}, vals.intern(v)) for c, v in ops] for ops in streams]
+    d_c, d_v = to_dev(vc), to_dev(vv)
+    st = cg.mvreg.apply_batch(d_c, d_v, cg.mvreg.encode_ops(enc, A, "cuda")).cpu().numpy()
+    got = obj_regs(to_host(d_c), to_host(d_v), actors, vals)
+    for i in range(N):
+        if len(exp[i].vals) <= V:
+            assert st[i] == 0 and got[i].vals == exp[i].vals, i
+        else:
+            assert st[i] & 16, i
+
+
+# ---- batched apply at A > 256 (csrc/orswot_apply.hip a1024 instance, csrc/map_apply.hip W = 8 / 16) ----
+@pytest.mark.parametrize("N,T,M,A", [(32, 64, 100, 300), (12, 48, 64, 1024)])
+def test_orswot_apply_wide(gpu_ctx, N, T, M, A):
+    """Device-generated Orswot op streams at 300 / 1,024 actors vs the C++ twin, every state."""
+    ops = cg.synth.orswot_op_streams(N, T, M, A, seed=N + T, device="cuda:0")
+    Dcap = 16
+    clock = torch.zeros((N, A), dtype=torch.int64, device="cuda:0")
+    entries = torch.zeros((N, M, A), dtype=torch.int64, device="cuda:0")
+    dcl = torch.zeros((N, Dcap, A), dtype=torch.int64, device="cuda:0")
+    dmb = torch.zeros((N, Dcap, (M + 63) // 64), dtype=torch.int64, device="cuda:0")
+    cnt = torch.zeros(N, dtype=torch.int32, device="cuda:0")
+    status = cg.orswot.apply_batch(clock, entries, dcl, dmb, cnt, ops, ctx=gpu_ctx)
+    torch.cuda.synchronize()
+    arr = [t.cpu().numpy() for t in ops]
+    oc, oe, ond, _ = O.orswot_apply_streams(N, M, A, *arr)
+    assert (status.cpu().numpy() == 0).all()
+    np.testing.assert_array_equal(to_host(clock), oc)
+    np.testing.assert_array_equal(to_host(entries), oe)
+    np.testing.assert_array_equal(cnt.cpu().numpy(), ond.astype(np.int32))
+
+
+@pytest.mark.parametrize("N,T,K,A,V", [(24, 64, 12, 300, 12), (8, 48, 8, 1024, 16), (40, 64, 16, 64, 12)])
+def test_map_apply_wide(gpu_ctx, N, T, K, A, V):
+    """Device-generated Map op streams at 300 / 1,024 actors and 12 / 16 value slots vs the
+    oracle's Map.apply (map.rs:119-137 with MVReg::apply mvreg.rs:130-166), every state."""
+    from test_gpu_map_apply import gpu_apply, oracle_apply
+    b = cg.synth.map_op_streams(N, T, K, A, seed=N + K, device="cuda:0")
+    h = {f: getattr(b, f).cpu().numpy() for f in b._fields}
+    streams = []
+    for s in range(N):
+        ops = []
+        for o in range(int(h["op_off"][s]), int(h["op_off"][s + 1])):
+            row = h["clk_pool"][h["clk_row"][o]].view(np.uint64)
+            clk = O.VClock({a: int(v) for a, v in enumerate(row) if v})
+            k = int(h["keys"][h["key_off"][o]])
+            ops.append(O.MapUp(O.Dot(int(h["actor"][o]), int(h["counter"][o])), k, O.MVRegPut(clk, int(h["val"][o])))
+                       if h["kind"][o] == 0 else O.MapRm(clk, {k}))
+        streams.append(ops)
+    exp, peak = oracle_apply(streams)
+    got, status = gpu_apply(gpu_ctx, streams, K, A, V, 16)
+    for s, ((g, _, _, _), e) in enumerate(zip(got, exp)):
+        if peak <= V:
+            assert status[s] == 0 and g == e, s
+
+
+# ---- pairwise merges: more than 512 deferred removes per pair, Map at A > 256 / V > 8 -------------
+def test_orswot_merge_batch_more_than_512_removes(gpu_ctx):
+    """Dcap(self) + Dcap(other) = 1,100 (self's own 400 removes + other's 350): the join kernel
+    forgets by removes 0..511, a second forget-only pass by the rest; equal to Orswot::merge."""
+    from test_gpu_merge_batch import orswot_check
+    M, A = 700, 3
+    a, b = O.Orswot(), O.Orswot()
+    for m in range(M):
+        a.apply(O.OrswotAdd(O.Dot(0, m + 1), [m]))
+    for i in range(400):  # future on actor 2: deferred; forget nothing yet (rm[0] = 0)
+        a.apply(O.OrswotRm(O.VClock({2: i + 1}), [(7 * i) % M]))
+    for i in range(350):  # future on actor 1: deferred; forgets a's dots (0, k) <= rm[0] on merge
+        b.apply(O.OrswotRm(O.VClock({0: (3 * i) % M + 1, 1: i + 1}), [(3 * i) % M, (5 * i) % M]))
+    assert len(a.deferred) + len(b.deferred) > 512
+    got = orswot_check(gpu_ctx, [a, a.copy()], [b, b.copy()], M, A)
+    assert len(got[0].deferred) > 512 and len(got[0].entries) < M
+
+
+@pytest.mark.parametrize("seed,N,K,A,V,cmax", [(41, 20, 5, 300, 12, 3), (42, 10, 4, 1024, 3, 3), (43, 30, 6, 40, 12, 4)])
+def test_map_merge_batch_wide(gpu_ctx, seed, N, K, A, V, cmax):
+    """Arbitrary Map states at 300 / 1,024 actors and 12 value slots: Map::merge per pair."""
+    from test_gpu_merge_batch import arbitrary_maps, map_check
+    rng = np.random.default_rng(seed)
+    maps = arbitrary_maps(rng, 2 * N, K, A, V, cmax)
+    map_check(gpu_ctx, maps[:N], maps[N:], K, A)
