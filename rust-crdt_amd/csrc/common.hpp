@@ -86,6 +86,7 @@ struct Tune {
   int merge_ppl = 8;           // lattice merge_batch rows: 16-byte pieces per lane per row
   int stage_kb = 262144;       // CRDT_MEM_HOST: bytes per device chunk buffer (KiB; two buffers)
   int wire_walk = 1;           // Map ingest: walk + batched parse (0: one dependent chain per state)
+  int wire_fill = 1;           // Orswot ingest: rows zeroed by filler waves beside the walk (0: a fill pass first)
   int host_stream = 1;         // CRDT_MEM_HOST Orswot / Map lub_many: stream replica chunks (0: stage whole)
   int apply_lane = 1;          // Orswot apply at A <= 64: 16 lanes per state (0: one wave per state)
   int apply_fence = 0;         // Orswot / Map apply: a workgroup fence after every op's stores (round-2 form)

@@ -225,6 +225,7 @@ static void apply_tune(crdt_ctx *ctx, const char *t) {
       else if (k == "mdiag" && v >= 0) ctx->tune.map_diag = v;
       else if (k == "wwalk") ctx->tune.wire_walk = v != 0;
       else if (k == "hstream") ctx->tune.host_stream = v != 0;
+      else if (k == "wfill") ctx->tune.wire_fill = v != 0;
       else if (k == "afence") ctx->tune.apply_fence = v != 0;
       else if (k == "alane") ctx->tune.apply_lane = v != 0;
       else if (k == "rbpc" && v > 0) ctx->tune.rows_blocks_per_cu = v;

@@ -1248,6 +1248,188 @@ __global__ __launch_bounds__(kOrWalkWaves * kWave) void orswot_ingest_walk_kerne
   }
 }
 
+// ---- Orswot ingest, round 4: rows zeroed by filler waves while the walk runs ----------------------
+// The dense entries of a state are ~60x its frame (config 3: 2 MiB of rows per 35 KiB frame), and a
+// separate zero-fill pass before the walk costs as much HBM time as the walk itself.  Here the block
+// holds kOfWalk walker waves and kOfFill filler waves: a filler zeroes its walkers' entry blocks with
+// 16-byte non-temporal stores while the walkers walk (the walk is a scalar chain, latency-bound; the
+// zeroing is write-bandwidth-bound, so the two overlap), then publishes "state zeroed" in LDS after
+// its stores completed (vmcnt(0) + release).  A walker only records the entries it finds — the word
+// position of each, in a per-state scratch list of up to M — and parses them once its state is
+// zeroed (acquire), in batches of 64 as before: every present member's counters land in a zeroed
+// row, no row is written before it is zero.  (Separate waves: a walker's own stores would enter the
+// in-order vmcnt its window DMA waits on.)  A frame with more than M entries parses the overflow at
+// once, after the wait: the same order of row writes as the one-pass kernel.
+constexpr int kOfWalk = 8, kOfFill = 2;
+__global__ __launch_bounds__((kOfWalk + kOfFill) * kWave) void orswot_ingest_walk_fill_kernel(IngestPlan p,
+                                                                                             uint32_t *epos) {
+  extern __shared__ u64 lds[];
+  const int lane = threadIdx.x % kWave, wib = threadIdx.x / kWave;
+  const uint32_t *actors = p.actors;
+  const u64 *elems = p.elems, *members = p.members;
+  u64 *base = stage_dicts(p, lds, actors, elems, members);
+  unsigned *zeroed = reinterpret_cast<unsigned *>(base);  // [kOfWalk]: iterations zeroed, per walker
+  u64 *rings = base + (kOfWalk + 1) / 2;
+  if (threadIdx.x < kOfWalk) zeroed[threadIdx.x] = 0;
+  __syncthreads();  // (the last barrier: walkers and fillers part here)
+  const unsigned long long MA = p.M * p.A;
+  if (wib >= kOfWalk) {  // ---- filler: walkers f, f + kOfFill, ... of every iteration
+    const int f = wib - kOfWalk;
+    unsigned it = 0;
+    for (unsigned long long s0 = (unsigned long long)blockIdx.x * kOfWalk; s0 < p.N;
+         s0 += (unsigned long long)gridDim.x * kOfWalk, ++it) {
+      for (int w = f; w < kOfWalk; w += kOfFill) {
+        const unsigned long long s = s0 + w;
+        if (s >= p.N) break;
+        u64 *ent = p.entries + s * MA;
+        if ((reinterpret_cast<uintptr_t>(ent) & 15) == 0 && MA % 2 == 0) {
+          u64x2 *e2 = reinterpret_cast<u64x2 *>(ent);
+          u64x2 z;
+          z.x = 0;
+          z.y = 0;
+          for (unsigned long long i = lane; i < MA / 2; i += kWave) __builtin_nontemporal_store(z, e2 + i);
+        } else {
+          for (unsigned long long i = lane; i < MA; i += kWave) __builtin_nontemporal_store(0ull, ent + i);
+        }
+        wire_vmcnt<0>();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        if (lane == 0) __hip_atomic_store(zeroed + w, it + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
+    return;
+  }
+  // ---- walker
+  u64 *mine = rings + (unsigned long long)wib * (kOrWalkRing * kWalkWin / 2);
+  uint32_t *ring = reinterpret_cast<uint32_t *>(mine);
+  unsigned it = 0;
+  for (unsigned long long s = (unsigned long long)blockIdx.x * kOfWalk + wib; s < p.N;
+       s += (unsigned long long)gridDim.x * kOfWalk, ++it) {
+    unsigned st = 0;
+    u64 dpos = 0, dcnt = 0;
+    u64 *crow = p.out + s * p.row_stride;
+    for (unsigned long long a = lane; a < p.A; a += kWave) crow[a] = 0;
+    uint32_t *ep = epos + s * p.M;  // this state's entry positions (up to M)
+    bool ready = false;             // this state's rows are zeroed (waited for)
+    auto wait_zeroed = [&]() {
+      if (ready) return;
+      while (__builtin_amdgcn_readfirstlane(
+                 __hip_atomic_load(zeroed + wib, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < it + 1)
+        __builtin_amdgcn_s_sleep(2);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      ready = true;
+    };
+    const u64 b = p.frame_off[s], e = p.frame_off[s + 1];
+    if ((b & 3) || (e & 3) || e < b || e - b < 16) {
+      st = kWireBad;
+    } else {
+      MapWalk<kOrWalkRing> w;
+      w.fw = reinterpret_cast<const uint32_t *>(p.bytes + b);
+      w.nw = (e - b) / 4;
+      w.nwin = (w.nw + kWalkWin - 1) / kWalkWin;
+      w.ring = ring;
+      w.start(lane);
+      u64 *ent = p.entries + s * MA;
+      bool miss = false;
+      // parse the entries recorded at ep[e0 .. e1) (lane = entry)
+      auto parse_stash = [&](unsigned long long e0, unsigned long long e1) {
+        for (unsigned long long x = e0; x < e1; x += kWave) {
+          const int cnt = (int)(e1 - x < (unsigned long long)kWave ? e1 - x : kWave);
+          unsigned long long k = 0, n = 0;
+          u64 id = 0;
+          if (lane < cnt) {
+            k = ep[x + lane];
+            id = (u64)w.fw[k] | ((u64)w.fw[k + 1] << 32);
+            n = (u64)w.fw[k + 2] | ((u64)w.fw[k + 3] << 32);
+          }
+          miss |= walk_parse_members(w.fw, actors, p.A, members, p.M, lane, cnt, k + 2, n, id, ent);
+        }
+      };
+      auto clock_len = [&](unsigned long long k) -> unsigned long long {
+        if (k + 2 > w.nw) return ~0ull;
+        const u64 n = w.get64(k, lane);
+        return n > (w.nw - k - 2) / 3 ? ~0ull : n;
+      };
+      unsigned long long k = 0;
+      unsigned long long n = clock_len(0);
+      if (n == ~0ull) {
+        st |= kWireBad;
+        k = ~0ull;
+      } else {
+        miss |= walk_parse(w.fw, actors, p.A, lane, 1, 0, n, crow);
+        k = 2 + 3 * n;
+      }
+      if (k != ~0ull && k + 2 > w.nw) {
+        st |= kWireBad;
+        k = ~0ull;
+      }
+      const u64 ne = k == ~0ull ? 0 : w.get64(k, lane);
+      if (k != ~0ull) k += 2;
+      unsigned long long stashed = 0;  // entries recorded in ep[], not parsed yet
+      int cnt = 0;                     // entries of the current 64-batch; lane i holds entry i's start
+      uint32_t bk = 0;
+      for (u64 en = 0; en < ne && k != ~0ull; ++en) {
+        if (k + 2 > w.nw) {
+          st |= kWireBad;
+          k = ~0ull;
+          break;
+        }
+        n = clock_len(k + 2);
+        if (n == ~0ull) {
+          st |= kWireBad;
+          k = ~0ull;
+          break;
+        }
+        n = uni64(n);
+        if (lane == cnt) bk = (uint32_t)k;
+        if (++cnt == kWave) {
+          if (stashed + kWave <= p.M) {  // record the batch's positions (one 256-byte store)
+            ep[stashed + lane] = bk;
+            stashed += kWave;
+          } else {  // more entries than M: the stash first, then this batch, at once
+            wait_zeroed();
+            parse_stash(0, stashed);
+            stashed = 0;
+            ep[lane] = bk;
+            parse_stash(0, kWave);
+          }
+          cnt = 0;
+        }
+        k = uni64(k + 4 + 3 * n);
+      }
+      if (k != ~0ull && k + 2 <= w.nw) {
+        dcnt = w.get64(k, lane);
+        dpos = k + 2;
+        if (dcnt > (w.nw - dpos) / 4) {  // a lying count (see orswot_ingest_kernel)
+          st |= kWireBad;
+          dcnt = 0;
+        }
+      } else {
+        st |= kWireBad;
+      }
+      wire_vmcnt<0>();  // no DMA of this frame may land in the ring after the next state starts
+      // the rows: zeroed by the filler by now (the walk outlasts the zeroing), then parsed in order
+      if (cnt && stashed + (unsigned long long)cnt <= p.M) {
+        if (lane < cnt) ep[stashed + lane] = bk;
+        stashed += cnt;
+        cnt = 0;
+      }
+      wait_zeroed();
+      parse_stash(0, stashed);
+      if (cnt) {  // (the M-overflow case: the last partial batch)
+        if (lane < cnt) ep[lane] = bk;
+        parse_stash(0, cnt);
+      }
+      if (__ballot(miss)) st |= kWireMissing;
+    }
+    wait_zeroed();  // (a bad frame too: the filler zeroed its rows, the output of a bad frame is zero)
+    if (lane == 0) {
+      p.status[s] = st;
+      p.dpos[s] = dpos;
+      p.dcount[s] = (st & kWireBad) ? 0 : dcnt;
+    }
+  }
+}
+
 // Egress, count (write = 0: frame sizes) or write pass: clock; present keys ascending with their
 // occupied value slots in slot (Vec) order; the state's deferred slots.
 __global__ __launch_bounds__(kBlock) void map_egress_kernel(MapWirePlan p, int write) {
@@ -1573,7 +1755,6 @@ int crdt_orswot_ingest(crdt_ctx *ctx, const uint8_t *bytes, const uint64_t *fram
   const unsigned long long nb = (N + kScanItems - 1) / kScanItems + 2;
   if (int rc = ensure_scratch(ctx, (2 * N + nb + 8) * 8)) return rc;
   u64 *dpos = reinterpret_cast<u64 *>(ctx->scratch), *dcount = dpos + N, *sc = dcount + N;
-  if (int rc = device_fill(ctx, entries, N * M * A * 8, 0)) return rc;
   int wpb = 4;
   while (wpb > 1 && (size_t)wpb * (A + Mw) * 8 > 64 * 1024) --wpb;
   IngestPlan p{};
@@ -1603,7 +1784,23 @@ int crdt_orswot_ingest(crdt_ctx *ctx, const uint8_t *bytes, const uint64_t *fram
   // sixteen 4-KiB frame rings; else the one-chain kernel
   const size_t ring_w = (size_t)kOrWalkRing * kWalkWin / 2;
   const size_t walk_lds = (dw + kOrWalkWaves * ring_w) * 8;
-  if (ctx->tune.wire_walk && walk_lds <= 160 * 1024) {
+  const size_t fill_lds = (dw + (kOfWalk + 1) / 2 + kOfWalk * ring_w) * 8;
+  if (ctx->tune.wire_walk && ctx->tune.wire_fill && fill_lds <= 80 * 1024 && N * M <= 0xffffffffffull &&
+      N * M * A * 8 > 0) {
+    // zero rows by filler waves beside the walk (no separate fill pass); two blocks per CU
+    if (int rc = ensure_scratch(ctx, (2 * N + nb + 8) * 8 + N * M * 4)) return rc;
+    dpos = reinterpret_cast<u64 *>(ctx->scratch), dcount = dpos + N, sc = dcount + N;
+    p.dpos = dpos;
+    p.dcount = dcount;
+    IngestPlan q = p;
+    q.dict_words = dw;
+    uint32_t *epos = reinterpret_cast<uint32_t *>(sc + nb + 8);
+    CRDT_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void *>(&orswot_ingest_walk_fill_kernel),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)fill_lds));
+    hipLaunchKernelGGL(orswot_ingest_walk_fill_kernel, dim3((unsigned)((N + kOfWalk - 1) / kOfWalk)),
+                       dim3((kOfWalk + kOfFill) * kWave), fill_lds, ctx->stream, q, epos);
+  } else if (ctx->tune.wire_walk && walk_lds <= 160 * 1024) {
+    if (int rc = device_fill(ctx, entries, N * M * A * 8, 0)) return rc;
     IngestPlan q = p;
     q.dict_words = dw;
     CRDT_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void *>(&orswot_ingest_walk_kernel),
@@ -1611,6 +1808,7 @@ int crdt_orswot_ingest(crdt_ctx *ctx, const uint8_t *bytes, const uint64_t *fram
     hipLaunchKernelGGL(orswot_ingest_walk_kernel, dim3(wave_grid(ctx, N, kOrWalkWaves, 8)),
                        dim3(kOrWalkWaves * kWave), walk_lds, ctx->stream, q);
   } else {
+    if (int rc = device_fill(ctx, entries, N * M * A * 8, 0)) return rc;
     hipLaunchKernelGGL(orswot_ingest_kernel, dim3(grid), dim3(wpb * kWave), (p.dict_words + wpb * A) * 8, ctx->stream, p);
   }
   CRDT_HIP(ctx, hipGetLastError());

@@ -108,12 +108,13 @@ def test_pncounter_gset_lwwreg_round_trip(gpu_ctx):
     assert bytes(edata.cpu().numpy().tobytes()) == blob
 
 
-@pytest.fixture(params=[1, 0], ids=["walk", "chain"])
+@pytest.fixture(params=["wwalk=1,wfill=1", "wwalk=1,wfill=0", "wwalk=0"], ids=["walk_fill", "walk", "chain"])
 def octx(request, gpu_ctx):
-    """Both Orswot ingest pass-1 kernels: the walk + batched parse (default) and the per-state chain."""
-    gpu_ctx.tune(f"wwalk={request.param}")
+    """Every Orswot ingest pass-1 kernel: the walk with filler waves zeroing the rows beside it (round 4
+    default), the walk after a separate zero-fill pass, and the per-state chain."""
+    gpu_ctx.tune(request.param)
     yield gpu_ctx
-    gpu_ctx.tune("wwalk=1")
+    gpu_ctx.tune("wwalk=1,wfill=1")
 
 
 def orswot_objects(seed, R, M, A):
