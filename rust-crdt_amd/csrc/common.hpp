@@ -90,6 +90,9 @@ struct Tune {
   int host_stream = 1;         // CRDT_MEM_HOST Orswot / Map lub_many: stream replica chunks (0: stage whole)
   int apply_lane = 1;          // Orswot apply at A <= 64: 16 lanes per state (0: one wave per state)
   int apply_fence = 0;         // Orswot / Map apply: a workgroup fence after every op's stores (round-2 form)
+  int orswot_apply_pf = 1;     // Orswot apply (16-lane groups): an Rm's clock row loaded during the op before
+  int map_apply_pf = 1;        // Map apply (16-lane groups): the next op's entry-clock row prefetched with its
+                               //     Put / rm clock; absent keys skip their value rows (0: round-3 form)
 };
 
 struct PendingTiming {

@@ -228,6 +228,8 @@ static void apply_tune(crdt_ctx *ctx, const char *t) {
       else if (k == "wfill") ctx->tune.wire_fill = v != 0;
       else if (k == "afence") ctx->tune.apply_fence = v != 0;
       else if (k == "alane") ctx->tune.apply_lane = v != 0;
+      else if (k == "oapf") ctx->tune.orswot_apply_pf = v != 0;
+      else if (k == "mapf") ctx->tune.map_apply_pf = v != 0;
       else if (k == "rbpc" && v > 0) ctx->tune.rows_blocks_per_cu = v;
       else if (k == "hot" && v >= 0 && v <= 64) ctx->tune.apply_hot_slots = v;
       else if (k == "mhot" && v >= 0) ctx->tune.map_apply_hot = v;

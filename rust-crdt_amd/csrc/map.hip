@@ -1977,7 +1977,6 @@ __global__ __launch_bounds__(SH ? 256 : (LD ? 128 : 64), LD ? 2 : 1) void map_fo
         m1m[lane] = m1;
       }
       {
-        const unsigned gq = (unsigned)lane & 3;
         const int nvx = __builtin_popcount(__builtin_amdgcn_readfirstlane(mv.vm));  // own values, compacted
 #pragma unroll
         for (int m = 0; m < NP; ++m) {

@@ -458,12 +458,10 @@ __global__ __launch_bounds__(kBlock) CRDT_APPLY_ATTR void map_apply_kernel(MapAp
 // full pass touches the Up's own key only (its rows are all the Up changed) and only when its key may
 // be in a slot (bloom of the slots' key-bitmap words), and a Rm compares its clock in full only
 // with slots of the same witness.  Exact for any input state.
+// Forget rm on key k whose entry-clock row is already in e (filtered in place).
 template <int KJ>
-__device__ void gkey_rm(const MapApplyPlan &p, unsigned long long s, unsigned long long k, const u64 (&rm)[KJ],
-                        int g, int lane) {
-  const KeyRefs q = key_refs(p, s, k);
-  u64 e[KJ];
-  grp::load_row<KJ>(e, q.ec, g, p.A);
+__device__ void gkey_rm_row(const MapApplyPlan &p, const KeyRefs &q, u64 (&e)[KJ], const u64 (&rm)[KJ], int g,
+                            int lane) {
   if (!grp::any_nz<KJ>(e, lane)) return;  // no entry for this key
 #pragma unroll
   for (int j = 0; j < KJ; ++j) e[j] = e[j] > rm[j] ? e[j] : 0ull;
@@ -479,9 +477,23 @@ __device__ void gkey_rm(const MapApplyPlan &p, unsigned long long s, unsigned lo
     if (!grp::any_nz<KJ>(v, lane) && g == 0) q.vv[jv] = 0;
   }
 }
-
 template <int KJ>
-__global__ __launch_bounds__(kBlock) void map_apply_grp_kernel(MapApplyPlan p) {
+__device__ void gkey_rm(const MapApplyPlan &p, unsigned long long s, unsigned long long k, const u64 (&rm)[KJ],
+                        int g, int lane) {
+  const KeyRefs q = key_refs(p, s, k);
+  u64 e[KJ];
+  grp::load_row<KJ>(e, q.ec, g, p.A);
+  gkey_rm_row<KJ>(p, q, e, rm, g, lane);
+}
+
+// PF (round 4): the entry-clock row of op i+1's key (an Up's key, an Rm's first key — carried in the
+// header) is loaded with its Put / rm clock while op i runs; op i marks it stale when it writes that
+// key's rows (same key, or a full apply_deferred pass) and op i+1 then reloads it.  The entry cell
+// of an Up is updated from that row (no dependent read), and an Up of an absent key (entry clock
+// all 0 <=> key absent, whose value rows are all 0 by the layout) writes its value to slot 0
+// without reading the value rows: ~90% of the Ups at the apply benchmark's shape.
+template <int KJ, bool PF>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KJ <= 2 ? 4 : 1))) void map_apply_grp_kernel(MapApplyPlan p) {
   extern __shared__ u64 lds[];
   constexpr int kG = grp::kG;
   constexpr int kVB = 4;  // value rows of an Up loaded in one batch
@@ -545,7 +557,7 @@ __global__ __launch_bounds__(kBlock) void map_apply_grp_kernel(MapApplyPlan p) {
     // counter, value, key range
     {
       const unsigned long long o = base + g;
-      u64 w0 = 2, w1 = 0, w2 = 0, w3 = 0, w4 = 0, w5 = 0;
+      u64 w0 = 2, w1 = 0xFFFFFFFFull, w2 = 0, w3 = 0, w4 = 0, w5 = 0;
       if (o < oe) {
         const unsigned kind = p.kind[o];
         const unsigned rr = p.clk_row ? p.clk_row[o] : 0u;
@@ -561,7 +573,7 @@ __global__ __launch_bounds__(kBlock) void map_apply_grp_kernel(MapApplyPlan p) {
           const u64 kb = p.key_off ? p.key_off[o] : 0ull, ke = p.key_off ? p.key_off[o + 1] : 0ull;
           if (ke >= kb && ke <= p.n_keys) {  // (reversed, or past the keys buffer: malformed)
             w0 = 1;
-            w1 = (u64)rr << 32;
+            w1 = ((u64)rr << 32) | (PF && kb < ke ? (u64)p.keys[kb] : 0xFFFFFFFFull);
             w4 = kb;
             w5 = ke;
           }
@@ -577,13 +589,46 @@ __global__ __launch_bounds__(kBlock) void map_apply_grp_kernel(MapApplyPlan p) {
       const u64 h1 = hdr[6 * i + 1];
       grp::load_row<KJ>(x, p.clk_pool + (h1 >> 32) * A, g, A);
     };
-    u64 ocn[KJ];
-    pool_row(0, ocn);
-    for (int i = 0; i < nb; ++i) {
-      u64 oc[KJ];
+    // PF: the entry-clock row of op i's key (the low word of header word 1; >= K: none)
+    auto hkey = [&](int i) -> unsigned { return (unsigned)hdr[6 * i + 1]; };
+    auto ec_row = [&](unsigned k, u64 (&x)[KJ]) {
+      if (k < K) {
+        grp::load_row<KJ>(x, p.ec + s * p.ec_s + (unsigned long long)k * A, g, A);
+      } else {
 #pragma unroll
-      for (int j = 0; j < KJ; ++j) oc[j] = ocn[j];
-      if (i + 1 < nb) pool_row(i + 1, ocn);
+        for (int j = 0; j < KJ; ++j) x[j] = 0;
+      }
+    };
+    u64 ocn[KJ], ecn[KJ];
+    unsigned kn = 0xFFFFFFFFu;  // key of the row in ecn
+    bool ndirty = false;        // ecn stale: the op in flight wrote key kn's rows
+    auto touch = [&](unsigned long long k) {
+      if (PF && k == kn) ndirty = true;
+    };
+    pool_row(0, ocn);
+    if (PF) {
+      kn = hkey(0);
+      ec_row(kn, ecn);
+    }
+    for (int i = 0; i < nb; ++i) {
+      u64 oc[KJ], e[KJ];
+#pragma unroll
+      for (int j = 0; j < KJ; ++j) {
+        oc[j] = ocn[j];
+        e[j] = PF ? ecn[j] : 0ull;
+      }
+      const unsigned kcur = kn;
+      const bool stale = ndirty;
+      ndirty = false;
+      if (i + 1 < nb) {
+        pool_row(i + 1, ocn);
+        if (PF) {
+          kn = hkey(i + 1);
+          ec_row(kn, ecn);
+        }
+      } else {
+        kn = 0xFFFFFFFFu;
+      }
       const u64x2 h0 = *reinterpret_cast<const u64x2 *>(hdr + 6 * i);
       const unsigned kind = (unsigned)h0[0];
       if (kind > 1) {
@@ -598,13 +643,35 @@ __global__ __launch_bounds__(kBlock) void map_apply_grp_kernel(MapApplyPlan p) {
         if (grp::clock_at<KJ>(c, a, lane) >= kc) continue;  // seen (:123-126)
         const KeyRefs q = key_refs(p, s, k);
         u64 vb[kVB][KJ];
+        bool vals = true;  // the key's value rows are read
+        if (PF) {
+          if (stale) grp::load_row<KJ>(e, q.ec, g, A);
+          vals = grp::any_nz<KJ>(e, lane);  // an absent key holds no values
+          if ((unsigned)g == a % kG) {      // entry clock apply(dot) (:130), from the row in registers
+            u64 ea = e[0];
 #pragma unroll
-        for (int t = 0; t < kVB; ++t) grp::load_row<KJ>(vb[t], q.vc + ((unsigned long long)t < V ? t : 0) * A, g, A);
-        if ((unsigned)g == a % kG) {  // entry clock apply(dot) (:130)
-          u64 *cell = q.ec + a;
-          if (*cell < kc) *cell = kc;
+            for (int j = 1; j < KJ; ++j)
+              if ((unsigned)j == a / kG) ea = e[j];
+            if (ea < kc) q.ec[a] = kc;
+          }
+          touch(k);
+          if (vals)
+#pragma unroll
+            for (int t = 0; t < kVB; ++t)
+              grp::load_row<KJ>(vb[t], q.vc + ((unsigned long long)t < V ? t : 0) * A, g, A);
+        } else {
+#pragma unroll
+          for (int t = 0; t < kVB; ++t)
+            grp::load_row<KJ>(vb[t], q.vc + ((unsigned long long)t < V ? t : 0) * A, g, A);
+          if ((unsigned)g == a % kG) {  // entry clock apply(dot) (:130)
+            u64 *cell = q.ec + a;
+            if (*cell < kc) *cell = kc;
+          }
         }
-        if (grp::any_nz<KJ>(oc, lane)) {  // MVReg::apply (mvreg.rs:130-166)
+        if (!vals && grp::any_nz<KJ>(oc, lane)) {  // MVReg::apply on no values: slot 0
+          grp::store_row<KJ>(q.vc, oc, g, A);
+          if (lead) q.vv[0] = h1[1];
+        } else if (grp::any_nz<KJ>(oc, lane)) {  // MVReg::apply (mvreg.rs:130-166)
           bool should_add = true;
           int last = -1, used = 0;
           for (unsigned long long j = 0; j < V; ++j) {
@@ -672,6 +739,7 @@ __global__ __launch_bounds__(kBlock) void map_apply_grp_kernel(MapApplyPlan p) {
         // apply_deferred (:134, :311-316)
         if (full) {  // every slot's keys forgotten in full, every witness recomputed
           full = false;
+          if (PF) ndirty = true;
           for (unsigned d = 0; d < dcnt;) {
             u64 rm[KJ];
             grp::load_row<KJ>(rm, DC + d * A, g, A);
@@ -734,12 +802,19 @@ __global__ __launch_bounds__(kBlock) void map_apply_grp_kernel(MapApplyPlan p) {
         const u64x2 h2 = *reinterpret_cast<const u64x2 *>(hdr + 6 * i + 4);
         const u64 kb = h2[0], ke = h2[1];
         for (u64 jk = kb; jk < ke; ++jk) {
-          const unsigned long long kk = p.keys[jk];
+          const unsigned long long kk = PF && jk == kb ? kcur : p.keys[jk];
           if (kk >= K) {
             st |= 2u;
             continue;
           }
-          gkey_rm<KJ>(p, s, kk, oc, g, lane);
+          if (PF && jk == kb) {  // the first key's entry row came with the header
+            const KeyRefs q = key_refs(p, s, kk);
+            if (stale) grp::load_row<KJ>(e, q.ec, g, A);
+            gkey_rm_row<KJ>(p, q, e, oc, g, lane);
+          } else {
+            gkey_rm<KJ>(p, s, kk, oc, g, lane);
+          }
+          touch(kk);
         }
         const unsigned wr = grp::witness<KJ>(oc, c, g, 0, A);
         if (wr == grp::kNone) continue;  // rm <= clock: not deferred (:336-345)
@@ -765,7 +840,7 @@ __global__ __launch_bounds__(kBlock) void map_apply_grp_kernel(MapApplyPlan p) {
           W |= 1ull << wr;
         }
         for (u64 jk = kb; jk < ke; ++jk) {
-          const unsigned long long kk = p.keys[jk];
+          const unsigned long long kk = PF && jk == kb ? kcur : p.keys[jk];
           if (kk >= K) continue;
           if (lead) DK[slot * Kw + kk / 64] |= 1ull << (kk % 64);
           bloom |= 1ull << (kk % 64);
@@ -824,9 +899,16 @@ extern "C" int crdt_map_apply_batch(crdt_ctx *ctx, const crdt_map_states *m, uin
     const dim3 g2((unsigned)((N + per_block - 1) / per_block)), b2(kBlock);
     const size_t lds2 = per_block * (6 * grp::kG * 8 + Dcap);
     timing_begin(ctx, "map_apply");
-    if (A <= 16) hipLaunchKernelGGL(map_apply_grp_kernel<1>, g2, b2, lds2, ctx->stream, p);
-    else if (A <= 32) hipLaunchKernelGGL(map_apply_grp_kernel<2>, g2, b2, lds2, ctx->stream, p);
-    else hipLaunchKernelGGL(map_apply_grp_kernel<4>, g2, b2, lds2, ctx->stream, p);
+    const bool pf = ctx->tune.map_apply_pf;
+    if (A <= 16)
+      hipLaunchKernelGGL((pf ? map_apply_grp_kernel<1, true> : map_apply_grp_kernel<1, false>), g2, b2, lds2,
+                         ctx->stream, p);
+    else if (A <= 32)
+      hipLaunchKernelGGL((pf ? map_apply_grp_kernel<2, true> : map_apply_grp_kernel<2, false>), g2, b2, lds2,
+                         ctx->stream, p);
+    else
+      hipLaunchKernelGGL((pf ? map_apply_grp_kernel<4, true> : map_apply_grp_kernel<4, false>), g2, b2, lds2,
+                         ctx->stream, p);
     timing_end(ctx);
     CRDT_HIP(ctx, hipGetLastError());
     return CRDT_OK;

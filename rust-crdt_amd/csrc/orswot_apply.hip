@@ -454,6 +454,9 @@ __device__ __forceinline__ void grp_forget_row(u64 *row, const u64 (&r)[kJ], int
 #ifndef CRDT_GRP_WPE
 #define CRDT_GRP_WPE 4
 #endif
+// RPF (round 4): an Rm's clock row (the read-only rm pool) is loaded while the op before it runs,
+// as the Map kernel does for its Put / rm clocks, so an Rm starts with its clock in registers.
+template <bool RPF>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRDT_GRP_WPE))) void orswot_apply_grp_kernel(
     OrswotApplyPlan p) {
   extern __shared__ u64 lds[];
@@ -548,7 +551,23 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRDT_GRP
     *reinterpret_cast<u64x2 *>(hdr + 4 * g) = u64x2{((u64)h_m0 << 32) | h_ka, ((u64)h_me << 32) | h_mb};
     *reinterpret_cast<u64x2 *>(hdr + 4 * g + 2) = u64x2{h_cr, h_cell};
     unsigned stale = 0;
+    auto rm_row = [&](int i, u64 (&x)[kJ]) {  // op i's rm clock (0 unless a valid Rm)
+      const unsigned ka = (unsigned)hdr[4 * i];
+      const u64 rr = hdr[4 * i + 2];
+      if (ka == kRmOp && rr < p.n_rm_rows) {
+        grp_load_row(x, p.rm_clock + rr * A, g, A);
+      } else {
+#pragma unroll
+        for (int j = 0; j < kJ; ++j) x[j] = 0;
+      }
+    };
+    u64 rn[kJ];
+    if (RPF) rm_row(0, rn);
     for (int i = 0; i < nb; ++i) {
+      u64 rcur[kJ];
+#pragma unroll
+      for (int j = 0; j < kJ; ++j) rcur[j] = RPF ? rn[j] : 0ull;
+      if (RPF && i + 1 < nb) rm_row(i + 1, rn);
       // op i's header: two 16-byte LDS reads, the same address for the group's lanes
       const u64x2 h0 = *reinterpret_cast<const u64x2 *>(hdr + 4 * i);
       const u64x2 h1 = *reinterpret_cast<const u64x2 *>(hdr + 4 * i + 2);
@@ -678,7 +697,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRDT_GRP
           continue;
         }
         u64 r[kJ];
-        grp_load_row(r, p.rm_clock + (unsigned long long)rr * A, g, A);
+        if (RPF) {
+#pragma unroll
+          for (int j = 0; j < kJ; ++j) r[j] = rcur[j];
+        } else {
+          grp_load_row(r, p.rm_clock + (unsigned long long)rr * A, g, A);
+        }
         if (one) {
           if (m0 >= M) st |= 2u;
           else grp_forget_row(E + (unsigned long long)m0 * p.entry_mstride, r, g, A);
@@ -787,7 +811,8 @@ extern "C" int crdt_orswot_apply_batch(crdt_ctx *ctx, const crdt_orswot_states *
     // kG lanes per state: kBlock / kG states per block, the slots' witness bytes in LDS
     timing_begin(ctx, "orswot_apply");
     const unsigned long long per_block = kBlock / kG;
-    hipLaunchKernelGGL(orswot_apply_grp_kernel, dim3((unsigned)((s.N + per_block - 1) / per_block)), dim3(kBlock),
+    hipLaunchKernelGGL((ctx->tune.orswot_apply_pf ? orswot_apply_grp_kernel<true> : orswot_apply_grp_kernel<false>),
+                       dim3((unsigned)((s.N + per_block - 1) / per_block)), dim3(kBlock),
                        per_block * (4 * kG * 8 + s.Dcap), ctx->stream, p);
     timing_end(ctx);
     CRDT_HIP(ctx, hipGetLastError());

@@ -17,6 +17,10 @@ case "$mode" in
     n=$(date +%s)
     timeout -k 10 900 python -u -m pytest -m gpu -x -q --timeout 300 --timeout-method thread "$@" > gpurun_out/pytest_$n.log 2>&1
     rc=$?; echo "pytest rc=$rc"; tail -n 30 gpurun_out/pytest_$n.log; exit $rc ;;
+  testsall)  # every test runs (no -x); rc 1 = some failed, any other nonzero rc = stop
+    n=$(date +%s)
+    timeout -k 10 1000 python -u -m pytest -m gpu -q --timeout 300 --timeout-method thread "$@" > gpurun_out/pytest_$n.log 2>&1
+    rc=$?; echo "pytest rc=$rc"; grep -E "^(FAILED|ERROR)" gpurun_out/pytest_$n.log | head -40; tail -n 3 gpurun_out/pytest_$n.log; exit $rc ;;
   round)
     tag=${1:-r03}
     timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu_$tag.log 2>&1

@@ -17,10 +17,11 @@ pytestmark = pytest.mark.gpu
 import crdts_gpu as cg  # noqa: E402
 
 
-@pytest.fixture(scope="module", params=["alane=1", "alane=0"])
+@pytest.fixture(scope="module", params=["alane=1", "alane=1,mapf=0", "alane=0"])
 def mactx(request):
-    """Both kernels: 16 lanes per state (alane=1, the default for A <= 64) and one wave per state
-    (alane=0, every A); shapes with A > 64 take the wave kernel in both modes."""
+    """Both kernels: 16 lanes per state (alane=1, the default for A <= 64; mapf=0 without the
+    next op's entry-row prefetch) and one wave per state (alane=0, every A); shapes with A > 64
+    take the wave kernel in every mode."""
     assert torch.cuda.is_available()
     torch.cuda.set_device(0)
     ctx = cg.Context(0)
@@ -121,6 +122,36 @@ def test_map_apply_replay(mactx, seed, n_states, n_origins, K, n_ops):
         for k, ent in e.entries.items():
             used = [j for j in range(vc.shape[1]) if vc[k, j].any()]
             assert [int(vv[k, j]) for j in used] == [v for _, v in ent.val.vals], (s, k)
+        assert not vc[~ec.any(axis=1)].any()
+
+
+@pytest.mark.parametrize("seed", [5, 6])
+def test_map_apply_same_key_runs(mactx, seed):
+    """Arbitrary ops (not ctx-derived) on 3 keys: runs of Ups and multi-key Rms on the same key
+    back to back, so the prefetched entry row of the next op is often stale (written by the op
+    before it) and must be reloaded; Rm keysets of 1-3 keys with the first key prefetched."""
+    rng = np.random.default_rng(seed)
+    A, K, N, T = 20, 3, 64, 48
+    streams = []
+    for _ in range(N):
+        ops, ctr = [], {}
+        for _ in range(T):
+            clk = O.VClock({int(a): int(rng.integers(1, 6)) for a in rng.choice(A, size=int(rng.integers(0, 4)),
+                                                                                   replace=False)})
+            if rng.random() < 0.6:
+                a = int(rng.integers(A))
+                ctr[a] = ctr.get(a, 0) + int(rng.integers(1, 3))
+                ops.append(O.MapUp(O.Dot(a, ctr[a]), int(rng.integers(K)), O.MVRegPut(clk, int(rng.integers(1, 1 << 40)))))
+            else:
+                ks = set(int(k) for k in rng.choice(K, size=int(rng.integers(1, 4)), replace=False))
+                ops.append(O.MapRm(clk, ks))
+        streams.append(ops)
+    exp, peak = oracle_apply(streams)
+    got, status = gpu_apply(mactx, streams, K, A, min(peak, 16), 48)
+    assert (status == 0).all(), status
+    for s, ((g, vc, vv, ec), e) in enumerate(zip(got, exp)):
+        assert g.clock == e.clock and g.entries == e.entries, s
+        assert g.deferred == e.deferred, s
         assert not vc[~ec.any(axis=1)].any()
 
 
