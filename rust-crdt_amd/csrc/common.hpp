@@ -79,6 +79,7 @@ struct Tune {
   int pair_occ = 1;            // ... cap on workgroups per CU (LDS padding; 0 = none): one workgroup
                                //     per CU keeps fewer HBM requests in flight, 69% -> 74-75% of 8 TB/s
   int map_forget_bpc = 1;      // Map forget, 16-byte kernel: workgroups per CU (1: 67% of 8 TB/s vs 64% at 4)
+  int map_pair_pf = 1;         // Map merge_batch sub-wave key pass: the next keys' rows loaded before the merge
   int map_pair_bpc = 64;       // Map merge_batch key pass: workgroups per CU (grid-stride over keys;
                                //     latency-bound: 16 -> 64 is 64% -> 67-69% of 8 TB/s)
   int merge_flat = 1;          // lattice merge_batch of packed rows: workgroups per CU of the flat

@@ -684,7 +684,19 @@ struct Seg {
   __device__ u64 bits(bool x) const { return (__ballot(x) & mask) >> base; }
 };
 
+// PF (round 4): the loads of the wave's NEXT keys (grid-stride successor) are issued before the
+// current keys are merged, so each wave keeps two keys' rows in flight instead of one (a wave's
+// iteration is one load round trip, then compute and stores: latency-bound at one batch).
 template <int SEG, int VM>
+struct SegRows {
+  unsigned long long s, k;
+  bool ok;  // a key of this segment, with valid deferred counts
+  unsigned n1, n2;
+  u64 e1, e2, c1, c2, x[VM], y[VM], v1l, v2l;
+  bool hitl;  // segment lane d: remove d (self's, then other's) names k
+};
+
+template <int SEG, int VM, bool PF>
 __global__ __launch_bounds__(kBlock) void map_pair_join_seg_kernel(MapPairPlan p) {
   constexpr int KPW = kWave / SEG;  // keys per wave
   const Seg<SEG> sg(threadIdx.x % kWave);
@@ -694,56 +706,71 @@ __global__ __launch_bounds__(kBlock) void map_pair_join_seg_kernel(MapPairPlan p
   const unsigned long long A = p.A, NK = p.N * p.K;
   const unsigned V1 = (unsigned)p.V1, V2 = (unsigned)p.V2;
   const bool act = (unsigned long long)sl < A;
-  for (unsigned long long it0 = w0 * KPW; it0 < NK; it0 += nw * KPW) {
+  // ---- one batch of loads for the keys at it0 (this segment's: it0 + segment index)
+  auto load = [&](unsigned long long it0, SegRows<SEG, VM> &L) {
     const unsigned long long it = it0 + (unsigned long long)(sg.base / SEG);
-    if (it >= NK) continue;  // a segment past the end (last wave only)
+    L.ok = false;
+    L.hitl = false;
+    L.e1 = L.e2 = L.c1 = L.c2 = L.v1l = L.v2l = 0;
+#pragma unroll
+    for (int q = 0; q < VM; ++q) L.x[q] = L.y[q] = 0;
+    if (it >= NK) return;  // a segment past the end (last wave only)
     const unsigned long long s = it / p.K, k = it % p.K;
-    const unsigned n1 = p.d1n[s], n2 = p.d2n ? p.d2n[s] : 0u;
-    if (n1 > p.D1 || n2 > p.D2) continue;  // reported by pair_deferred_kernel
-    u64 *ec1 = p.ec1 + s * p.ec1_s + k * A;
-    u64 *vc1 = p.vc1 + s * p.vc1_s + k * p.V1 * A;
-    u64 *vv1 = p.vv1 + s * p.vv1_s + k * p.V1;
+    L.s = s;
+    L.k = k;
+    L.n1 = p.d1n[s];
+    L.n2 = p.d2n ? p.d2n[s] : 0u;
     const u64 *ec2 = p.ec2 + s * p.ec2_s + k * A;
     const u64 *vc2 = p.vc2 + s * p.vc2_s + k * p.V2 * A;
     const u64 *vv2 = p.vv2 + s * p.vv2_s + k * p.V2;
-    // ---- one batch of loads
-    u64 e1 = 0, e2 = 0, c1 = 0, c2 = 0, x[VM], y[VM];
-#pragma unroll
-    for (int q = 0; q < VM; ++q) x[q] = y[q] = 0;
+    const u64 *ec1 = p.ec1 + s * p.ec1_s + k * A;
+    const u64 *vc1 = p.vc1 + s * p.vc1_s + k * p.V1 * A;
+    const u64 *vv1 = p.vv1 + s * p.vv1_s + k * p.V1;
     if (act) {
-      e1 = ec1[sl];
-      e2 = ec2[sl];
-      c1 = p.c1[s * p.c1_s + sl];
-      c2 = p.c2[s * p.c2_s + sl];
+      L.e1 = ec1[sl];
+      L.e2 = ec2[sl];
+      L.c1 = p.c1[s * p.c1_s + sl];
+      L.c2 = p.c2[s * p.c2_s + sl];
 #pragma unroll
       for (int q = 0; q < VM; ++q) {
-        if ((unsigned)q < V1) x[q] = vc1[(unsigned long long)q * A + sl];
-        if ((unsigned)q < V2) y[q] = vc2[(unsigned long long)q * A + sl];
+        if ((unsigned)q < V1) L.x[q] = vc1[(unsigned long long)q * A + sl];
+        if ((unsigned)q < V2) L.y[q] = vc2[(unsigned long long)q * A + sl];
       }
     }
-    const u64 v1l = (unsigned)sl < V1 ? vv1[sl] : 0ull;
-    const u64 v2l = (unsigned)sl < V2 ? vv2[sl] : 0ull;
-    // each segment's value payloads to all its lanes while the whole wave is still converged
+    L.v1l = (unsigned)sl < V1 ? vv1[sl] : 0ull;
+    L.v2l = (unsigned)sl < V2 ? vv2[sl] : 0ull;
+    L.ok = !(L.n1 > p.D1 || L.n2 > p.D2);  // (else reported by pair_deferred_kernel)
+    const unsigned nd = L.ok ? L.n1 + L.n2 : 0u;
+    if ((unsigned)sl < nd) {
+      const u64 *kb =
+          (unsigned)sl < L.n1 ? p.d1k + (s * p.D1 + sl) * p.Kw : p.d2k + (s * p.D2 + (sl - L.n1)) * p.Kw;
+      L.hitl = (kb[k / 64] >> (k % 64)) & 1ull;
+    }
+  };
+  // ---- merge the keys whose rows are in L
+  auto merge = [&](const SegRows<SEG, VM> &L) {
+    // each segment's value payloads to all its lanes (a segment's lanes are all here or all not)
     u64 val1[VM], val2[VM];
 #pragma unroll
     for (int q = 0; q < VM; ++q) {
-      val1[q] = __shfl(v1l, sg.base + q);
-      val2[q] = __shfl(v2l, sg.base + q);
+      val1[q] = __shfl(L.v1l, sg.base + q);
+      val2[q] = __shfl(L.v2l, sg.base + q);
     }
+    if (!L.ok) return;
+    const unsigned long long s = L.s, k = L.k;
+    const unsigned n1 = L.n1, n2 = L.n2;
+    const u64 e1 = L.e1, e2 = L.e2, c1 = L.c1, c2 = L.c2;
+    u64 *ec1 = p.ec1 + s * p.ec1_s + k * A;
+    u64 *vc1 = p.vc1 + s * p.vc1_s + k * p.V1 * A;
+    u64 *vv1 = p.vv1 + s * p.vv1_s + k * p.V1;
     const unsigned nd = n1 + n2;
-    bool hitl = false;  // segment lane d: remove d (self's, then other's) names k
-    if ((unsigned)sl < nd) {
-      const u64 *kb = (unsigned)sl < n1 ? p.d1k + (s * p.D1 + sl) * p.Kw : p.d2k + (s * p.D2 + (sl - n1)) * p.Kw;
-      hitl = (kb[k / 64] >> (k % 64)) & 1ull;
-    }
-    // ---- compute
     const bool p1 = sg.any(e1 != 0), p2 = sg.any(e2 != 0);
-    if (!p1 && !p2) continue;
+    if (!p1 && !p2) return;
     unsigned m1 = 0, m2 = 0;
 #pragma unroll
     for (int q = 0; q < VM; ++q) {
-      if (sg.any(x[q] != 0)) m1 |= 1u << q;
-      if (sg.any(y[q] != 0)) m2 |= 1u << q;
+      if (sg.any(L.x[q] != 0)) m1 |= 1u << q;
+      if (sg.any(L.y[q] != 0)) m2 |= 1u << q;
     }
     auto le = [&](u64 a, u64 b) { return !sg.any(a > b); };           // a <= b everywhere
     auto lt = [&](u64 a, u64 b) { return le(a, b) && sg.any(a != b); };  // partial_cmp == Less
@@ -779,7 +806,7 @@ __global__ __launch_bounds__(kBlock) void map_pair_join_seg_kernel(MapPairPlan p
           bool dom = false;
 #pragma unroll
           for (int r = 0; r < VM; ++r)
-            if (((m2 >> r) & 1u) && !dom) dom = lt(x[q], y[r]);
+            if (((m2 >> r) & 1u) && !dom) dom = lt(L.x[q], L.y[r]);
           if (!dom) keep1 |= 1u << q;
         }
 #pragma unroll
@@ -788,7 +815,7 @@ __global__ __launch_bounds__(kBlock) void map_pair_join_seg_kernel(MapPairPlan p
           bool drop = false;
 #pragma unroll
           for (int q = 0; q < VM; ++q)
-            if (((keep1 >> q) & 1u) && !drop) drop = le(y[r], x[q]);  // y < x or y == x
+            if (((keep1 >> q) & 1u) && !drop) drop = le(L.y[r], L.x[q]);  // y < x or y == x
           if (!drop) add2 |= 1u << r;
         }
         const u64 mx = e1 > e2 ? e1 : e2;
@@ -800,7 +827,7 @@ __global__ __launch_bounds__(kBlock) void map_pair_join_seg_kernel(MapPairPlan p
     bool hasR = false;
     if (present) {
       for (unsigned b0 = 0; b0 < nd; b0 += SEG) {
-        bool h = hitl;
+        bool h = L.hitl;
         if (b0) {  // more than SEG removes on the pair
           h = false;
           const unsigned d = b0 + sl;
@@ -828,7 +855,7 @@ __global__ __launch_bounds__(kBlock) void map_pair_join_seg_kernel(MapPairPlan p
 #pragma unroll
       for (int q = 0; q < VM; ++q) {
         if (!((keep1 >> q) & 1u)) continue;
-        u64 z = x[q] > X ? x[q] : 0;  // MVReg::forget mvreg.rs:88-104
+        u64 z = L.x[q] > X ? L.x[q] : 0;  // MVReg::forget mvreg.rs:88-104
         if (hasR) z = z > Rk ? z : 0;
         const u64 val = val1[q];
         if (!sg.any(z != 0)) continue;
@@ -841,7 +868,7 @@ __global__ __launch_bounds__(kBlock) void map_pair_join_seg_kernel(MapPairPlan p
 #pragma unroll
       for (int r = 0; r < VM; ++r) {
         if (!((add2 >> r) & 1u)) continue;
-        u64 z = y[r] > X ? y[r] : 0;
+        u64 z = L.y[r] > X ? L.y[r] : 0;
         if (hasR) z = z > Rk ? z : 0;
         const u64 val = val2[r];
         if (!sg.any(z != 0)) continue;
@@ -858,6 +885,22 @@ __global__ __launch_bounds__(kBlock) void map_pair_join_seg_kernel(MapPairPlan p
     for (unsigned q = w; q < V1; ++q) {
       if (act) vc1[(unsigned long long)q * A + sl] = 0;
       if (sl == 0) vv1[q] = 0;
+    }
+  };
+  const unsigned long long step = nw * KPW;
+  unsigned long long it0 = w0 * KPW;
+  if (it0 >= NK) return;
+  SegRows<SEG, VM> cur;
+  load(it0, cur);
+  for (; it0 < NK; it0 += step) {
+    if constexpr (PF) {
+      SegRows<SEG, VM> nxt;
+      load(it0 + step, nxt);  // (nothing when past the end)
+      merge(cur);
+      cur = nxt;
+    } else {
+      merge(cur);
+      load(it0 + step, cur);
     }
   }
 }
@@ -987,13 +1030,17 @@ extern "C" int crdt_map_merge_batch(crdt_ctx *ctx, const crdt_map_states *self, 
                   other_def->Dcap ? other_def->count : nullptr, other_def->Dcap, status};
     const unsigned grid = pair_grid(ctx, (unsigned long long)N * K, ctx->tune.map_pair_bpc);
     timing_begin(ctx, "map_pair_join");
+    const bool pf = ctx->tune.map_pair_pf;
     if (ctx->tune.map_pair_reg && a.V <= 4 && b.V <= 4 && A <= 4 * (size_t)kWave) {  // register-resident rows
       if (A <= 16 && ctx->tune.map_pair_reg == 1)
-        hipLaunchKernelGGL((map_pair_join_seg_kernel<16, 4>), dim3(grid), dim3(kBlock), 0, ctx->stream, p);
+        hipLaunchKernelGGL((pf ? map_pair_join_seg_kernel<16, 4, true> : map_pair_join_seg_kernel<16, 4, false>),
+                           dim3(grid), dim3(kBlock), 0, ctx->stream, p);
       else if (A <= 32 && ctx->tune.map_pair_reg == 1)
-        hipLaunchKernelGGL((map_pair_join_seg_kernel<32, 4>), dim3(grid), dim3(kBlock), 0, ctx->stream, p);
+        hipLaunchKernelGGL((pf ? map_pair_join_seg_kernel<32, 4, true> : map_pair_join_seg_kernel<32, 4, false>),
+                           dim3(grid), dim3(kBlock), 0, ctx->stream, p);
       else if (A <= (size_t)kWave && ctx->tune.map_pair_reg == 1)
-        hipLaunchKernelGGL((map_pair_join_seg_kernel<64, 4>), dim3(grid), dim3(kBlock), 0, ctx->stream, p);
+        hipLaunchKernelGGL((pf ? map_pair_join_seg_kernel<64, 4, true> : map_pair_join_seg_kernel<64, 4, false>),
+                           dim3(grid), dim3(kBlock), 0, ctx->stream, p);
       else if (A <= (size_t)kWave)
         hipLaunchKernelGGL((map_pair_join_reg_kernel<1, 4>), dim3(grid), dim3(kBlock), 0, ctx->stream, p);
       else if (A <= 2 * (size_t)kWave)

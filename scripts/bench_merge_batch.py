@@ -49,20 +49,32 @@ def slots(def_off, def_clock, def_bits, N, Dcap):
     return dc, db, torch.from_numpy(cnt).to(dev)
 
 
-def timed(fn, reset):
+SPREAD = {}  # min / max of the last timed() call's steps (placement spread), library kernel times
+
+
+def timed(fn, reset, kernel=None):
     reset()
     fn()
     torch.cuda.synchronize()
     ms = []
+    ctx.timing_reset()
     for _ in range(args.steps):
         reset()
         torch.cuda.synchronize()
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ctx.set_timing(kernel is not None)
         s.record()
         fn()
         e.record()
         torch.cuda.synchronize()
+        ctx.set_timing(False)
         ms.append(s.elapsed_time(e))
+    SPREAD.clear()
+    SPREAD.update(ms_min=float(np.min(ms)), ms_max=float(np.max(ms)))
+    if kernel:
+        kms, n = ctx.timing(kernel)
+        if n:
+            SPREAD[kernel + "_ms"] = kms / n
     return float(np.median(ms))
 
 
@@ -127,7 +139,8 @@ def mapb():
         for d, s in zip(work, keep):
             d.copy_(s)
 
-    ms = timed(lambda: cg.map.merge_batch(work, sb, ctx=ctx), reset)
+    ms = timed(lambda: cg.map.merge_batch(work, sb, ctx=ctx), reset, kernel="map_pair_join")
+    spread = dict(SPREAD)
     reset()
     status = cg.map.merge_batch(work, sb, ctx=ctx).cpu().numpy()
     ok = bool((status == 0).all())
@@ -149,6 +162,8 @@ def mapb():
     alg = N * (per + K * (A + Vs * A + Vs) * 8 * 2)  # read other, read + write self (Vs slots)
     print(json.dumps({"op": "map_merge_batch", "pairs": N, "keys": K, "actors": A, "kernel_ms_incl_deferred": ms,
                       "algorithmic_bytes": alg, "GBs": alg / ms / 1e6, "frac_of_8TBs": alg / ms / 8e9,
+                      "frac_min_max": [alg / spread["ms_max"] / 8e9, alg / spread["ms_min"] / 8e9],
+                      "key_pass_ms": spread.get("map_pair_join_ms"), "steps": args.steps,
                       "pair_merges_per_s": N / ms * 1e3, "parity": "ok" if ok else "MISMATCH",
                       "parity_pairs": args.sample}), flush=True)
     return ok

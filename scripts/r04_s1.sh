@@ -8,6 +8,7 @@ bash scripts/gpu.sh testsall tests/test_gpu_orswot_any_state.py tests/test_gpu_w
 rc=$?; [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
 bash scripts/gpu.sh run r04_map_apply_pf_ab bash scripts/ab_tune.sh scripts/bench_map_apply.py "" mapf=0 mapf=1 || exit $?
 bash scripts/gpu.sh run r04_orswot_apply_pf_ab bash scripts/ab_tune.sh scripts/bench_orswot_apply.py "" oapf=0 oapf=1 || exit $?
+bash scripts/gpu.sh run r04_map_pair_pf_ab bash scripts/ab_tune.sh scripts/bench_merge_batch.py "--only map --steps 10" mppf=0 mppf=1 || exit $?
 bash scripts/gpu.sh tests tests/test_gpu_map.py -k "mld or fullsize" || exit $?
 bash scripts/gpu.sh run r04_wire_fill_ab bash scripts/ab_tune.sh scripts/bench_wire.py "--skip gcounter,pncounter,map" wfill=0 wfill=1 || exit $?
 bash scripts/gpu.sh run r04_map_ld_ab bash scripts/ab_tune.sh scripts/bench_map.py "--steps 5" mld=0 mld=1 || exit $?
