@@ -79,7 +79,8 @@ struct Tune {
   int pair_occ = 1;            // ... cap on workgroups per CU (LDS padding; 0 = none): one workgroup
                                //     per CU keeps fewer HBM requests in flight, 69% -> 74-75% of 8 TB/s
   int map_forget_bpc = 1;      // Map forget, 16-byte kernel: workgroups per CU (1: 67% of 8 TB/s vs 64% at 4)
-  int map_pair_pf = 1;         // Map merge_batch sub-wave key pass: the next keys' rows loaded before the merge
+  int map_pair_pf = 0;         // Map merge_batch sub-wave key pass: the next keys' rows loaded before the merge
+                               //     (opt-in: 5.86 vs 5.81 ms at 4 waves/SIMD, profiles/r04_map_pair_pf_ab.log)
   int map_pair_bpc = 64;       // Map merge_batch key pass: workgroups per CU (grid-stride over keys;
                                //     latency-bound: 16 -> 64 is 64% -> 67-69% of 8 TB/s)
   int merge_flat = 1;          // lattice merge_batch of packed rows: workgroups per CU of the flat
@@ -91,9 +92,11 @@ struct Tune {
   int host_stream = 1;         // CRDT_MEM_HOST Orswot / Map lub_many: stream replica chunks (0: stage whole)
   int apply_lane = 1;          // Orswot apply at A <= 64: 16 lanes per state (0: one wave per state)
   int apply_fence = 0;         // Orswot / Map apply: a workgroup fence after every op's stores (round-2 form)
-  int orswot_apply_pf = 1;     // Orswot apply (16-lane groups): an Rm's clock row loaded during the op before
+  int orswot_apply_pf = 0;     // Orswot apply (16-lane groups): an Rm's clock row loaded during the op before
+                               //     (opt-in: 4 VGPRs spill, 990 vs 918 us, profiles/r04_orswot_apply_pf_ab.log)
   int map_apply_pf = 1;        // Map apply (16-lane groups): the next op's entry-clock row prefetched with its
-                               //     Put / rm clock; absent keys skip their value rows (0: round-3 form)
+                               //     Put / rm clock; absent keys skip their value rows (0: round-3 form;
+                               //     1.28 vs 1.81 ms, profiles/r04_map_apply_pf_ab.log)
 };
 
 struct PendingTiming {

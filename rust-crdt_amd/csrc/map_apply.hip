@@ -835,9 +835,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KJ <= 2 
           }
           slot = (int)dcnt++;
           grp::store_row<KJ>(DC + (unsigned long long)slot * A, oc, g, A);
-          for (unsigned long long x = g; x < Kw; x += kG) DK[slot * Kw + x] = 0;
+          // a one-key Rm's bit goes in with the zeros (no read-modify-write behind the stores)
+          const unsigned long long k1 = ke == kb + 1 ? (PF ? (unsigned long long)kcur : p.keys[kb]) : ~0ull;
+          const unsigned long long wk = k1 < K ? k1 / 64 : ~0ull;
+          for (unsigned long long x = g; x < Kw; x += kG) DK[slot * Kw + x] = x == wk ? 1ull << (k1 % 64) : 0ull;
           if (lead) wit[slot] = (uint8_t)wr;
           W |= 1ull << wr;
+          if (ke == kb + 1) {
+            if (k1 < K) bloom |= 1ull << (k1 % 64);
+            continue;
+          }
         }
         for (u64 jk = kb; jk < ke; ++jk) {
           const unsigned long long kk = PF && jk == kb ? kcur : p.keys[jk];

@@ -744,10 +744,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRDT_GRP
             const unsigned a = g + kG * j;
             if (a < A) DC[slot * A + a] = r[j];
           }
-          for (unsigned long long x = g; x < Mw; x += kG) DM[slot * Mw + x] = 0;
+          // a new slot's member words are written whole: a one-member Rm's bit goes in with the
+          // zeros (no read-modify-write round trip behind the stores)
+          const unsigned long long wm = one && m0 < M ? (unsigned long long)m0 / 64 : ~0ull;
+          for (unsigned long long x = g; x < Mw; x += kG) DM[slot * Mw + x] = x == wm ? 1ull << (m0 % 64) : 0ull;
           if (lead) wit[slot] = (uint8_t)wr;
           W |= 1ull << wr;
           if (p.fence) wave_fence();  // the zeroed words are or-ed by the group's first lane below
+          if (one) {
+            if (m0 < M) bloom |= 1ull << (m0 % 64);
+            if (p.fence) wave_fence();
+            continue;
+          }
         }
         for (u64 j = mb; j < me; ++j) {
           const unsigned long long m = one ? m0 : p.mem[j];

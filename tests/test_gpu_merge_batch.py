@@ -200,13 +200,13 @@ def arbitrary_maps(rng, n, K, A, V, cmax, max_def=3):
     return maps
 
 
-@pytest.mark.parametrize("reg", ["mpreg=1", "mpreg=1,mppf=0", "mpreg=1,mpbpc=1", "mpreg=2", "mpreg=0"])
+@pytest.mark.parametrize("reg", ["mpreg=1", "mpreg=1,mppf=1", "mpreg=1,mppf=1,mpbpc=1", "mpreg=2", "mpreg=0"])
 @pytest.mark.parametrize("seed,N,K,A,V,cmax", [(21, 40, 5, 3, 2, 4), (22, 25, 9, 33, 2, 3), (23, 16, 4, 70, 1, 3),
                                                (24, 30, 70, 8, 3, 6), (25, 12, 3, 200, 2, 2), (26, 20, 6, 5, 5, 3),
                                                (27, 24, 7, 32, 2, 4), (28, 9, 5, 17, 4, 3), (29, 40, 150, 30, 2, 3)])
 def test_map_merge_batch_arbitrary_kernels(gpu_ctx, reg, seed, N, K, A, V, cmax):
     """Arbitrary dense states through each Map key kernel: the sub-wave register kernel (mpreg=1:
-    16 / 32 / 64 lanes per key by A; mppf=0 without the next keys' loads in flight; mpbpc=1 one
+    16 / 32 / 64 lanes per key by A; mppf=1 with the next keys' loads in flight; mpbpc=1 one
     workgroup per CU, so a wave walks several keys and the prefetched rows are the ones merged),
     the whole-wave register kernel (mpreg=2, and A > 64 under 1) and the generic one (mpreg=0, and
     self V = 5 under every setting): identical to the oracle."""
@@ -216,7 +216,7 @@ def test_map_merge_batch_arbitrary_kernels(gpu_ctx, reg, seed, N, K, A, V, cmax)
     try:
         map_check(gpu_ctx, maps[:N], maps[N:], K, A)
     finally:
-        gpu_ctx.tune("mpreg=1,mppf=1,mpbpc=64")
+        gpu_ctx.tune("mpreg=1,mppf=0,mpbpc=64")
 
 
 def test_map_merge_batch_many_removes(gpu_ctx):
