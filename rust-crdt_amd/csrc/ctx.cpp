@@ -229,6 +229,7 @@ static void apply_tune(crdt_ctx *ctx, const char *t) {
       else if (k == "afence") ctx->tune.apply_fence = v != 0;
       else if (k == "alane") ctx->tune.apply_lane = v != 0;
       else if (k == "mppf") ctx->tune.map_pair_pf = v != 0;
+      else if (k == "ohpf") ctx->tune.orswot_apply_hpf = v != 0;
       else if (k == "oapf") ctx->tune.orswot_apply_pf = v != 0;
       else if (k == "mapf") ctx->tune.map_apply_pf = v != 0;
       else if (k == "rbpc" && v > 0) ctx->tune.rows_blocks_per_cu = v;

@@ -456,7 +456,11 @@ __device__ __forceinline__ void grp_forget_row(u64 *row, const u64 (&r)[kJ], int
 #endif
 // RPF (round 4): an Rm's clock row (the read-only rm pool) is loaded while the op before it runs,
 // as the Map kernel does for its Put / rm clocks, so an Rm starts with its clock in registers.
-template <bool RPF>
+// HPF (round 4): a batch header is three dependent round trips (kind / member range, then the
+// first member / actor / counter, then a one-member Add's cell).  With HPF the next batch's kinds
+// and member ranges are loaded at this batch's start and its first members at the middle op, so a
+// batch boundary costs two round trips (actor / counter, then the cell).
+template <bool RPF, bool HPF>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRDT_GRP_WPE))) void orswot_apply_grp_kernel(
     OrswotApplyPlan p) {
   extern __shared__ u64 lds[];
@@ -525,11 +529,49 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRDT_GRP
   // prefetched cell is stale once an earlier op of the batch wrote that member's row (same first
   // member, any multi-member op, the full pass): `stale` marks those ops, which load it again.
   const int gb = lane & ~(kG - 1);
+  // HPF: op (base + g)'s kind, member range and first member, loaded a batch ahead
+  unsigned nx_kind = 0xFFu, nx_m0 = 0xFFFFFFFFu;
+  u64 nx_mb = 0, nx_me = 0;
+  auto pre_fields = [&](unsigned long long oo) {
+    nx_kind = 0xFFu;
+    if (oo < oe) {
+      nx_kind = p.kind[oo];
+      nx_mb = p.mem_off[oo];
+      nx_me = p.mem_off[oo + 1];
+    }
+  };
+  auto pre_member = [&]() {  // the first member of the op whose range is in nx_*
+    nx_m0 = 0xFFFFFFFFu;
+    if (nx_kind <= 1 && nx_me > nx_mb && nx_me <= p.n_mem) nx_m0 = p.mem[nx_mb];
+  };
+  if (HPF) {
+    pre_fields(ob + g);
+    pre_member();
+  }
   for (unsigned long long base = ob; base < oe; base += kG) {
     const unsigned long long oo = base + g;
     unsigned h_ka = kBadOp, h_mb = 0, h_me = 0, h_m0 = 0xFFFFFFFFu;
     u64 h_cr = 0, h_cell = 0;
-    if (oo < oe) {
+    if (HPF) {
+      if (oo < oe) {  // the actor / counter / rm row now, with the range and member already here
+        const u64 mb = nx_mb, me = nx_me;
+        h_mb = (unsigned)mb;
+        h_me = (unsigned)me;
+        const bool range_ok = me >= mb && me <= 0xFFFFFFFFull && me <= p.n_mem;
+        if (range_ok && nx_kind == 0) {
+          const unsigned a = p.actor ? p.actor[oo] : 0u;
+          h_ka = a < A ? a : kBadOp;
+          h_cr = p.counter ? p.counter[oo] : 0ull;
+          if (me > mb) h_m0 = nx_m0;
+          if (h_ka != kBadOp && me - mb == 1 && h_m0 < M) h_cell = E[(unsigned long long)h_m0 * p.entry_mstride + a];
+        } else if (range_ok && nx_kind == 1) {
+          h_ka = kRmOp;
+          h_cr = p.rm_row ? p.rm_row[oo] : 0u;
+          if (me > mb) h_m0 = nx_m0;
+        }
+      }
+      pre_fields(oo + kG);  // the next batch's kind and range while this one runs
+    } else if (oo < oe) {
       const unsigned kind = p.kind[oo];
       const u64 mb = p.mem_off[oo], me = p.mem_off[oo + 1];
       h_mb = (unsigned)mb;
@@ -568,6 +610,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRDT_GRP
 #pragma unroll
       for (int j = 0; j < kJ; ++j) rcur[j] = RPF ? rn[j] : 0ull;
       if (RPF && i + 1 < nb) rm_row(i + 1, rn);
+      if (HPF && i == kG / 2) pre_member();
       // op i's header: two 16-byte LDS reads, the same address for the group's lanes
       const u64x2 h0 = *reinterpret_cast<const u64x2 *>(hdr + 4 * i);
       const u64x2 h1 = *reinterpret_cast<const u64x2 *>(hdr + 4 * i + 2);
@@ -819,9 +862,13 @@ extern "C" int crdt_orswot_apply_batch(crdt_ctx *ctx, const crdt_orswot_states *
     // kG lanes per state: kBlock / kG states per block, the slots' witness bytes in LDS
     timing_begin(ctx, "orswot_apply");
     const unsigned long long per_block = kBlock / kG;
-    hipLaunchKernelGGL((ctx->tune.orswot_apply_pf ? orswot_apply_grp_kernel<true> : orswot_apply_grp_kernel<false>),
-                       dim3((unsigned)((s.N + per_block - 1) / per_block)), dim3(kBlock),
-                       per_block * (4 * kG * 8 + s.Dcap), ctx->stream, p);
+    const dim3 grid((unsigned)((s.N + per_block - 1) / per_block));
+    const size_t lds = per_block * (4 * kG * 8 + s.Dcap);
+    const bool rpf = ctx->tune.orswot_apply_pf, hpf = ctx->tune.orswot_apply_hpf;
+    if (rpf && hpf) hipLaunchKernelGGL((orswot_apply_grp_kernel<true, true>), grid, dim3(kBlock), lds, ctx->stream, p);
+    else if (rpf) hipLaunchKernelGGL((orswot_apply_grp_kernel<true, false>), grid, dim3(kBlock), lds, ctx->stream, p);
+    else if (hpf) hipLaunchKernelGGL((orswot_apply_grp_kernel<false, true>), grid, dim3(kBlock), lds, ctx->stream, p);
+    else hipLaunchKernelGGL((orswot_apply_grp_kernel<false, false>), grid, dim3(kBlock), lds, ctx->stream, p);
     timing_end(ctx);
     CRDT_HIP(ctx, hipGetLastError());
     return CRDT_OK;

@@ -15,7 +15,8 @@ ab() {  # ab <tag> <script>: previous vs current library, interleaved twice
 }
 ab oapply scripts/bench_orswot_apply.py > gpurun_out/r04_oapply_ab.log 2>&1 || exit $?
 ab mapply scripts/bench_map_apply.py > gpurun_out/r04_mapply_ab.log 2>&1 || exit $?
-grep -h -o '^== .*\|"kernel_us": [0-9.]*' gpurun_out/r04_oapply_ab.log gpurun_out/r04_mapply_ab.log
+bash scripts/ab_tune.sh scripts/bench_orswot_apply.py "" ohpf=0 ohpf=1 > gpurun_out/r04_oapply_hpf_ab.log 2>&1 || exit $?
+grep -h -o '^== .*\|"kernel_us": [0-9.]*' gpurun_out/r04_oapply_ab.log gpurun_out/r04_mapply_ab.log gpurun_out/r04_oapply_hpf_ab.log
 bash scripts/gpu.sh trace r04_oapply python3 scripts/bench_orswot_apply.py || exit $?
 bash scripts/gpu.sh trace r04_mapply python3 scripts/bench_map_apply.py || exit $?
 SQ=SQ_WAVE_CYCLES,SQ_WAIT_ANY,SQ_ACTIVE_INST_ANY,SQ_INSTS_VALU,SQ_INSTS_SALU,SQ_INSTS_VMEM,SQ_INSTS_LDS,SQ_WAIT_INST_ANY
