@@ -94,8 +94,8 @@ struct Tune {
   int apply_fence = 0;         // Orswot / Map apply: a workgroup fence after every op's stores (round-2 form)
   int orswot_apply_pf = 0;     // Orswot apply (16-lane groups): an Rm's clock row loaded during the op before
                                //     (opt-in: 4 VGPRs spill, 990 vs 918 us, profiles/r04_orswot_apply_pf_ab.log)
-  int orswot_apply_hpf = 1;    // Orswot apply (16-lane groups): the next op batch's fields / first members loaded
-                               //     while the current batch runs (0: three round trips per batch header)
+  int orswot_apply_hpf = 0;    // Orswot apply (16-lane groups): the next op batch's fields / first members loaded
+                               //     while the current batch runs (opt-in: 2 VGPRs spill, 878 vs 856 us, profiles/r04_oapply_hpf_ab.log)
   int map_apply_pf = 1;        // Map apply (16-lane groups): the next op's entry-clock row prefetched with its
                                //     Put / rm clock; absent keys skip their value rows (0: round-3 form;
                                //     1.28 vs 1.81 ms, profiles/r04_map_apply_pf_ab.log)

@@ -20,7 +20,7 @@ pytestmark = pytest.mark.gpu
 import crdts_gpu as cg  # noqa: E402
 
 
-@pytest.fixture(scope="module", params=["alane=1", "alane=1,oapf=1", "alane=1,ohpf=0", "alane=0"])
+@pytest.fixture(scope="module", params=["alane=1", "alane=1,oapf=1", "alane=1,ohpf=1", "alane=0"])
 def actx(request):
     """Both kernels: 16 lanes per state (alane=1, the default for A <= 64) and one wave per state
     (alane=0, every A); shapes with A > 64 take the wave kernel in both modes."""
