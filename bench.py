@@ -441,6 +441,8 @@ def main():
             "cpu_baseline": None,
             "parity": head["parity"],
         }
+        if "exchange" in head:
+            out["exchange"] = head["exchange"]
         if env.note:
             out["config"]["rccl_note"] = env.note
         if c5 is not None:

@@ -13,3 +13,4 @@ bash profiles/collect.sh "$tag" || exit $?
 timeout -k 10 400 python -u bench.py --gpus 2 --dist-backend gloo --exchange cabi-ops --steps 5 --warmup 1 \
   --no-cpu-baseline > gpurun_out/bench_world2_$tag.log 2>&1 || exit $?
 grep '^{' gpurun_out/bench_world2_$tag.log | cut -c1-1500
+bash scripts/gpu.sh trace r04_oapply_def python3 scripts/bench_orswot_apply.py
