@@ -85,6 +85,7 @@ struct Tune {
                                //     latency-bound: 16 -> 64 is 64% -> 67-69% of 8 TB/s)
   int merge_flat = 1;          // lattice merge_batch of packed rows: workgroups per CU of the flat
                                //     stream (0: the row-group kernels)
+  int merge_flat_u = 2;        // ... 16-byte pieces per lane in flight before the first store (1, 2, 4)
   int merge_ppl = 8;           // lattice merge_batch rows: 16-byte pieces per lane per row
   int stage_kb = 262144;       // CRDT_MEM_HOST: bytes per device chunk buffer (KiB; two buffers)
   int wire_walk = 1;           // Map ingest: walk + batched parse (0: one dependent chain per state)

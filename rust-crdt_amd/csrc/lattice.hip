@@ -297,17 +297,21 @@ __global__ __launch_bounds__(kBlock) void merge_rows_kernel(u64 *self, const u64
 // 2 pieces per lane in flight at one workgroup per CU — the shape at which an in-place
 // read-self / read-other / write-self stream peaks on this part (scripts/micro/stream_rate.hip,
 // 75% vs 65-69% with more requests in flight).
-template <Op OP>
+template <Op OP, int U>
 __global__ __launch_bounds__(kBlock) void merge_flat_kernel(u64x2 *self, const u64x2 *other, unsigned long long n) {
   const unsigned long long stride = (unsigned long long)gridDim.x * kBlock;
   unsigned long long i = (unsigned long long)blockIdx.x * kBlock + threadIdx.x;
-  for (; i + stride < n; i += 2 * stride) {
-    const u64x2 a0 = __builtin_nontemporal_load(self + i), b0 = __builtin_nontemporal_load(other + i);
-    const u64x2 a1 = __builtin_nontemporal_load(self + i + stride), b1 = __builtin_nontemporal_load(other + i + stride);
-    __builtin_nontemporal_store(join2<OP>(a0, b0), self + i);
-    __builtin_nontemporal_store(join2<OP>(a1, b1), self + i + stride);
+  for (; i + (U - 1) * stride < n; i += U * stride) {
+    u64x2 a[U], b[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      a[u] = __builtin_nontemporal_load(self + i + u * stride);
+      b[u] = __builtin_nontemporal_load(other + i + u * stride);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) __builtin_nontemporal_store(join2<OP>(a[u], b[u]), self + i + u * stride);
   }
-  if (i < n) __builtin_nontemporal_store(join2<OP>(self[i], other[i]), self + i);
+  for (; i < n; i += stride) __builtin_nontemporal_store(join2<OP>(self[i], other[i]), self + i);
 }
 
 static bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
@@ -522,12 +526,20 @@ int lattice_merge_batch(crdt_ctx *ctx, Op op, u64 *self, const u64 *other, size_
     const unsigned long long cap = (unsigned long long)ctx->cu_count * ctx->tune.merge_flat;
     const unsigned grid = (unsigned)(want < cap ? want : cap);
     timing_begin(ctx, "merge_pairs");
-    if (op == Op::Max)
-      hipLaunchKernelGGL(merge_flat_kernel<Op::Max>, dim3(grid), dim3(kBlock), 0, ctx->stream,
-                         reinterpret_cast<u64x2 *>(self), reinterpret_cast<const u64x2 *>(other), n);
-    else
-      hipLaunchKernelGGL(merge_flat_kernel<Op::Or>, dim3(grid), dim3(kBlock), 0, ctx->stream,
-                         reinterpret_cast<u64x2 *>(self), reinterpret_cast<const u64x2 *>(other), n);
+    u64x2 *sp = reinterpret_cast<u64x2 *>(self);
+    const u64x2 *op2 = reinterpret_cast<const u64x2 *>(other);
+    const int fu = ctx->tune.merge_flat_u;
+#define CRDT_FLAT(OPV, UU) hipLaunchKernelGGL((merge_flat_kernel<OPV, UU>), dim3(grid), dim3(kBlock), 0, ctx->stream, sp, op2, n)
+    if (op == Op::Max) {
+      if (fu == 1) CRDT_FLAT(Op::Max, 1);
+      else if (fu == 4) CRDT_FLAT(Op::Max, 4);
+      else CRDT_FLAT(Op::Max, 2);
+    } else {
+      if (fu == 1) CRDT_FLAT(Op::Or, 1);
+      else if (fu == 4) CRDT_FLAT(Op::Or, 4);
+      else CRDT_FLAT(Op::Or, 2);
+    }
+#undef CRDT_FLAT
     timing_end(ctx);
     CRDT_HIP(ctx, hipGetLastError());
     return CRDT_OK;

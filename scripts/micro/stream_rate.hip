@@ -92,7 +92,8 @@ void sweep(u64x2 *a, u64x2 *b, u64x2 *o, size_t n, int cus, u64 *sink) {
 int main(int argc, char **argv) {
   int cus = 0;
   hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
-  const size_t bytes = 4ull << 30;  // per array: far past the 256 MB of last-level cache
+  // per array: far past the 256 MB of last-level cache (argv[2]: GiB per array, default 4)
+  const size_t bytes = (argc > 2 ? (size_t)atoi(argv[2]) : 4ull) << 30;
   const size_t n = bytes / 16;
   u64x2 *a, *b, *o;
   u64 *sink;
@@ -115,6 +116,12 @@ int main(int argc, char **argv) {
     sweep<2, 4, false>(a, b, o, n, cus, sink);
     sweep<2, 8, true>(a, b, o, n, cus, sink);
     sweep<2, 1, true>(a, b, o, n, cus, sink);
+  } else if (which == 2) {  // the in-place merge at 1-4 pieces per lane, few workgroups (array size sweep)
+    for (int pass = 0; pass < 2; ++pass) {
+      sweep<2, 1, true>(a, b, o, n, cus, sink);
+      sweep<2, 2, true>(a, b, o, n, cus, sink);
+      sweep<2, 4, true>(a, b, o, n, cus, sink);
+    }
   } else {  // the in-place merge and the copy at few pieces in flight, three passes (run-to-run spread)
     for (int pass = 0; pass < 3; ++pass) {
       sweep<2, 1, true>(a, b, o, n, cus, sink);

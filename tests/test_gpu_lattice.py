@@ -75,8 +75,9 @@ def test_gset_lub_many(gpu_ctx, R, W):
 
 
 # merge_batch launch forms: the flat 16-byte stream of packed rows (default, one workgroup per CU;
-# mflat=4: four), and the row-group kernels (mflat=0, also the path of strided rows)
-@pytest.mark.parametrize("mode", ["", "mflat=0", "mflat=4"])
+# mflat=4: four; mfu = 16-byte pieces per lane in flight: 2 by default, 1 or 4), and the row-group
+# kernels (mflat=0, also the path of strided rows)
+@pytest.mark.parametrize("mode", ["", "mflat=0", "mflat=4", "mfu=1", "mfu=4", "mflat=2,mfu=4"])
 @pytest.mark.parametrize("N,A", [(1, 1), (10, 7), (7, 2), (33, 6), (1000, 64), (3000, 256), (64, 1030)])
 def test_merge_batch(gpu_ctx, mode, N, A):
     if mode:
