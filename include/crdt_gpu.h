@@ -461,6 +461,14 @@ typedef struct crdt_orswot_sharded_out {
 } crdt_orswot_sharded_out;
 
 int crdt_orswot_lub_many_sharded(crdt_ctx *ctx, const crdt_orswot_batch *in, crdt_orswot_sharded_out *out);
+/* crdt_orswot_lub_many_sharded with this rank's deferred-pool offsets in DEVICE memory (round 4):
+ * in->def_off NULL, def_off device u64 [G+1] (or NULL when D == 0) with def_off[G] == D, D the
+ * rank's pool length.  The per-group counts are taken on the device and travel in the exchange's
+ * count row, so no host sync is added: the offsets are checked there too (def_off[0] == 0,
+ * def_off[G] == D, non-decreasing), and an invalid entry on ANY rank makes every rank return
+ * before a deferred row moves (CRDT_EINVAL on that rank, CRDT_ECOMM on the others). */
+int crdt_orswot_lub_many_sharded_doff(crdt_ctx *ctx, const crdt_orswot_batch *in, const uint64_t *def_off, size_t D,
+                                      crdt_orswot_sharded_out *out);
 /* crdt_lub_many_multi over replica shards: one fused local launch, then ONE grouped RCCL call
  * (an in-place ncclMax all-reduce per max segment; GSet segments as crdt_gset_lub_many_sharded).
  * Outputs must be contiguous (out_stride == row words, or G == 1). */
@@ -553,6 +561,14 @@ int crdt_map_lub_many_doff(crdt_ctx *ctx, const crdt_map_batch *in, const uint64
  * [D][ceil(K/64)]: the surviving removes' key sets over ALL keys, assembled by one
  * ncclAllReduce(ncclSum) (disjoint ranges: sum = union).  def_keep is the same on every rank. */
 int crdt_map_lub_many_sharded(crdt_ctx *ctx, const crdt_map_batch *in, size_t k0, size_t K, crdt_map_out *out);
+/* crdt_map_lub_many_sharded with the deferred pool's offsets in DEVICE memory (round 4), as for
+ * crdt_map_lub_many_doff: in->def_off NULL, def_off device u64 [G+1] (or NULL when D == 0),
+ * def_off[G] == D.  Checked on the device (an invalid entry sets bit 1 of the flags of the groups
+ * it bounds, ORed over the ranks); instead of the host offsets' hash in the agreed header, a
+ * device hash of the offsets travels in the flags exchange and ranks holding different offsets
+ * all return CRDT_EINVAL before the key sets are exchanged. */
+int crdt_map_lub_many_sharded_doff(crdt_ctx *ctx, const crdt_map_batch *in, const uint64_t *def_off, size_t D,
+                                   size_t k0, size_t K, crdt_map_out *out);
 
 /* ---- MVReg<u64, A> on its own (outside a Map) ------------------------------------------------
  * Replaces MVReg::merge (mvreg.rs:112-128) and MVReg::apply (mvreg.rs:130-166) for registers in the

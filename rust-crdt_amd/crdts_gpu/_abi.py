@@ -52,6 +52,7 @@ EXPORTS = (
     "crdt_ctx_comm_init_ops", "crdt_ctx_comm_note",
     "crdt_mvreg_lub_many", "crdt_mvreg_merge_batch", "crdt_mvreg_apply_batch",
     "crdt_orswot_lub_many_doff", "crdt_map_lub_many_doff",
+    "crdt_orswot_lub_many_sharded_doff", "crdt_map_lub_many_sharded_doff",
 )
 
 
@@ -219,6 +220,8 @@ _SIGS.update({
                               ctypes.POINTER(MapDeferred), P], ctypes.c_int),
     "crdt_lwwreg_lub_many_sharded": ([P, P, P, S, S, S, U64, P, P, P], ctypes.c_int),
     "crdt_map_lub_many_sharded": ([P, ctypes.POINTER(MapBatch), S, S, ctypes.POINTER(MapOut)], ctypes.c_int),
+    "crdt_map_lub_many_sharded_doff": ([P, ctypes.POINTER(MapBatch), P, S, S, S, ctypes.POINTER(MapOut)],
+                                       ctypes.c_int),
     "crdt_vclock_ingest": ([P, P, P, S, P, S, P, S, P], ctypes.c_int),
     "crdt_pncounter_ingest": ([P, P, P, S, P, S, P, S, P], ctypes.c_int),
     "crdt_gset_ingest": ([P, P, P, S, P, S, P, S, P], ctypes.c_int),
@@ -240,6 +243,8 @@ _SIGS.update({
     "crdt_ctx_comm_note": ([P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)], ctypes.c_char_p),
     "crdt_orswot_lub_many_sharded": ([P, ctypes.POINTER(OrswotBatch), ctypes.POINTER(OrswotShardedOut)],
                                      ctypes.c_int),
+    "crdt_orswot_lub_many_sharded_doff": ([P, ctypes.POINTER(OrswotBatch), P, S, ctypes.POINTER(OrswotShardedOut)],
+                                          ctypes.c_int),
 })
 for _t in ("vclock", "gcounter", "pncounter", "gset"):
     _SIGS[f"crdt_{_t}_lub_many_sharded"] = ([P, P, S, S, S, S, S, P], ctypes.c_int)

@@ -98,8 +98,6 @@ def lub_many(clock: torch.Tensor, ec: torch.Tensor, vclk: torch.Tensor, vval: to
     off_arr = None
     dev_off = isinstance(def_off, torch.Tensor) and def_off.device.type == "cuda"
     if dev_off:
-        if _key_shard is not None:
-            raise ValueError("map.lub_many: a device def_off is not supported for a key-sharded fold")
         if (def_off.dtype not in (torch.int64, torch.uint64) or tuple(def_off.shape) != (G + 1,)
                 or not def_off.is_contiguous() or def_off.device.index != ctx.device):
             raise ValueError(f"map.lub_many: a device def_off must be a contiguous ({G + 1},) int64 "
@@ -132,8 +130,11 @@ def lub_many(clock: torch.Tensor, ec: torch.Tensor, vclk: torch.Tensor, vval: to
             keep = torch.empty(D, dtype=torch.uint8, device=dev)
             keys_out = torch.empty((D, Kw), dtype=torch.int64, device=dev)
             o.def_keep, o.def_keys = keep.data_ptr(), keys_out.data_ptr()
-    if dev_off:
+    if dev_off and _key_shard is None:
         ctx.call("crdt_map_lub_many_doff", ctypes.byref(b), def_off.data_ptr(), D, ctypes.byref(o))
+    elif dev_off:  # key shard with device offsets (crdt_map_lub_many_sharded_doff)
+        ctx.call("crdt_map_lub_many_sharded_doff", ctypes.byref(b), def_off.data_ptr(), D, int(_key_shard[0]),
+                 int(_key_shard[1]), ctypes.byref(o))
     elif _key_shard is None:
         ctx.call("crdt_map_lub_many", ctypes.byref(b), ctypes.byref(o))
     else:

@@ -161,7 +161,9 @@ def orswot_lub_many_sharded(clock: torch.Tensor, entries: torch.Tensor, def_off:
                             def_clock: Optional[torch.Tensor] = None, def_members: Optional[torch.Tensor] = None,
                             ctx: Optional[Context] = None, def_cap: Optional[int] = None) -> OrswotSharded:
     """Rank k's shard: clock (G, R_k, A), entries (G, R_k, M, A) and its deferred removes pooled
-    per group (host def_off of G+1 entries, def_clock (D_k, A), def_members (D_k, Mw))."""
+    per group (def_off of G+1 entries: a host sequence, or a contiguous int64 cuda tensor —
+    crdt_orswot_lub_many_sharded_doff, D_k = def_clock.shape[0] —, def_clock (D_k, A),
+    def_members (D_k, Mw))."""
     ctx = ctx or Context.default(clock.device.index)
     ctx.check_tensor(clock, "orswot.lub_many_sharded(clock)")
     ctx.check_tensor(entries, "orswot.lub_many_sharded(entries)")
@@ -177,7 +179,20 @@ def orswot_lub_many_sharded(clock: torch.Tensor, entries: torch.Tensor, def_off:
     b.entry_mstride, b.entry_rstride, b.entry_gstride = entries.stride(2), entries.stride(1), entries.stride(0)
     off_arr = None
     D = 0
-    if def_off is not None:
+    dev_off = isinstance(def_off, torch.Tensor) and def_off.device.type == "cuda"
+    if dev_off:
+        if (def_off.dtype not in (torch.int64, torch.uint64) or tuple(def_off.shape) != (G + 1,)
+                or not def_off.is_contiguous() or def_off.device.index != ctx.device):
+            raise ValueError(f"orswot.lub_many_sharded: a device def_off must be a contiguous ({G + 1},) int64 "
+                             f"cuda:{ctx.device} tensor")
+        D = 0 if def_clock is None else int(def_clock.shape[0])
+        if D:
+            for t, nm, w in ((def_clock, "def_clock", A), (def_members, "def_members", Mw)):
+                if t is None or not t.is_contiguous() or tuple(t.shape) != (D, w):
+                    raise ValueError(f"orswot.lub_many_sharded: {nm} must be a contiguous ({D}, {w}) tensor")
+                ctx.check_tensor(t, f"orswot.lub_many_sharded({nm})")
+            b.def_clock, b.def_members = def_clock.data_ptr(), def_members.data_ptr()
+    elif def_off is not None:
         off = [int(x) for x in def_off]
         if len(off) != G + 1:
             raise ValueError(f"orswot.lub_many_sharded: def_off must have G+1 = {G + 1} entries")
@@ -201,7 +216,10 @@ def orswot_lub_many_sharded(clock: torch.Tensor, entries: torch.Tensor, def_off:
     o.clock, o.entries, o.def_cap = oc.data_ptr(), oe.data_ptr(), cap
     o.def_clock, o.def_members, o.def_group = odc.data_ptr(), odm.data_ptr(), odg.data_ptr()
     o.ndef = ctypes.pointer(nd)
-    ctx.call("crdt_orswot_lub_many_sharded", ctypes.byref(b), ctypes.byref(o))
+    if dev_off:
+        ctx.call("crdt_orswot_lub_many_sharded_doff", ctypes.byref(b), def_off.data_ptr(), D, ctypes.byref(o))
+    else:
+        ctx.call("crdt_orswot_lub_many_sharded", ctypes.byref(b), ctypes.byref(o))
     n = nd.value
     if n > cap:  # more survivors than room: run again with exactly enough
         return orswot_lub_many_sharded(clock, entries, def_off, def_clock, def_members, ctx, def_cap=n)

@@ -450,8 +450,47 @@ int crdt_gset_lub_many_sharded(crdt_ctx *ctx, const uint64_t *in, size_t G, size
                          "gset_lub_many_sharded");
 }
 
-int crdt_orswot_lub_many_sharded(crdt_ctx *ctx, const crdt_orswot_batch *in, crdt_orswot_sharded_out *out) {
-  static const char *what = "orswot_lub_many_sharded";
+}  // extern "C"
+
+// The per-group deferred counts of device offsets, checked as def_off_check_kernel does: row[g] =
+// clamp(off[g+1]) - clamp(off[g]) (g < G), row[G] = D, and *bad |= 1 for an invalid entry
+// (off[0] != 0, off[G] != D, an entry past D or below its predecessor).
+__global__ __launch_bounds__(kBlock) void def_counts_kernel(const u64 *off, u64 *row, unsigned long long G,
+                                                            unsigned long long D, u64 *bad) {
+  bool b = false;
+  for (unsigned long long i = blockIdx.x * (unsigned long long)kBlock + threadIdx.x; i <= G;
+       i += (unsigned long long)gridDim.x * kBlock) {
+    const u64 v = off[i];
+    b |= i == 0 ? v != 0 : (i == G ? v != D : v > D);
+    if (i > 0 && off[i - 1] > v) b = true;
+    if (i < G) {
+      const u64 lo = v > D ? D : v, hi0 = off[i + 1], hi = hi0 > D ? D : hi0;
+      row[i] = hi > lo ? hi - lo : 0;
+    } else {
+      row[G] = D;
+    }
+  }
+  if (b) atomicOr(bad, 1ull);
+}
+
+// Position-aware, order-free hash of device offsets (the sum of a mix of (i, off[i]); u64 wrap):
+// the ranks of a key-sharded Map call compare it after their flags exchange.
+__global__ __launch_bounds__(kBlock) void def_hash_kernel(const u64 *off, unsigned long long n, u64 *out) {
+  u64 h = 0;
+  for (unsigned long long i = blockIdx.x * (unsigned long long)kBlock + threadIdx.x; i < n;
+       i += (unsigned long long)gridDim.x * kBlock) {
+    u64 z = off[i] ^ (0x9e3779b97f4a7c15ull * (i + 1));
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    h += z ^ (z >> 31);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) h += __shfl_xor(h, o);
+  if (threadIdx.x % kWave == 0 && h) atomicAdd(out, h);
+}
+
+static int orswot_sharded_impl(crdt_ctx *ctx, const crdt_orswot_batch *in, const u64 *doff, size_t Ddev,
+                               crdt_orswot_sharded_out *out, const char *what) {
   CRDT_CHECK_CTX(ctx);
   CRDT_TRY(need_comm(ctx));
   CRDT_HIP(ctx, hipSetDevice(ctx->device));
@@ -460,11 +499,20 @@ int crdt_orswot_lub_many_sharded(crdt_ctx *ctx, const crdt_orswot_batch *in, crd
   int st = device_mem_only(ctx, what);
   if (!st && (!in || !out || !out->clock || !out->entries || !out->ndef))
     st = fail(ctx, CRDT_EINVAL, "%s: NULL argument", what);
+  if (!st && doff && in->def_off) st = fail(ctx, CRDT_EINVAL, "%s: in->def_off must be NULL", what);
+  if (!st && !doff && Ddev) st = fail(ctx, CRDT_EINVAL, "%s: D > 0 without def_off", what);
   const size_t G = st ? 0 : in->G, M = st ? 0 : in->M, A = st ? 0 : in->A, Mw = (M + 63) / 64;
   const bool work = G > 0 && A > 0 && M > 0;
-  // deferred removes of this rank: per-group counts
+  // deferred removes of this rank: per-group counts (device offsets: counted on the device into
+  // the exchanged row below, their check travels in that row)
   std::vector<uint64_t> head(G + 1, 0);
   size_t Dk = 0;
+  if (!st && work && doff) {
+    Dk = Ddev;
+    if (Dk && (!in->def_clock || !in->def_members))
+      st = fail(ctx, CRDT_EINVAL, "%s: deferred removes without their buffers", what);
+    if (!st && Dk > 0xffffffffULL) st = fail(ctx, CRDT_EUNSUPPORTED, "%s: too many deferred removes", what);
+  }
   if (!st && work && in->def_off) {
     if (in->def_off[0] != 0) st = fail(ctx, CRDT_EINVAL, "%s: def_off[0] must be 0", what);
     for (size_t g = 0; !st && g < G; ++g) {
@@ -479,7 +527,8 @@ int crdt_orswot_lub_many_sharded(crdt_ctx *ctx, const crdt_orswot_batch *in, crd
   head[G] = Dk;
   // 1. local join of the shard without deferred removes -> partial (clock, entries); every
   //    buffer of the exchange whose size is known here is allocated before the agreement.  The
-  //    exchanged row per rank: [G+1 deferred counts | G "an input cell had E > C" flags | pad].
+  //    exchanged row per rank: [G+1 deferred counts | G "an input cell had E > C" flags | device
+  //    offsets invalid].
   const size_t crow = 2 * G + 2;
   void *pc = nullptr, *pe = nullptr, *gc = nullptr, *ge = nullptr, *lcnt = nullptr, *acnt = nullptr;
   crdt_orswot_batch loc{};
@@ -499,7 +548,17 @@ int crdt_orswot_lub_many_sharded(crdt_ctx *ctx, const crdt_orswot_batch *in, crd
       ex.viol = reinterpret_cast<unsigned *>((u64 *)pc + G * A);
       st = orswot_lub_many_ex(ctx, &loc, &po, ex);
     }
-    if (!st) st = stage_h2d(ctx, lcnt, head.data(), (G + 1) * 8);
+    if (!st && doff) {
+      st = device_fill(ctx, (u64 *)lcnt + 2 * G + 1, 8, 0);
+      if (!st) {
+        hipLaunchKernelGGL(def_counts_kernel, dim3(small_grid(ctx, G + 1)), dim3(kBlock), 0, ctx->stream, doff,
+                           (u64 *)lcnt, (unsigned long long)G, (unsigned long long)Dk, (u64 *)lcnt + 2 * G + 1);
+        if (hipGetLastError() != hipSuccess) st = fail(ctx, CRDT_EHIP, "%s: def_counts_kernel launch", what);
+      }
+    } else if (!st) {
+      st = stage_h2d(ctx, lcnt, head.data(), (G + 1) * 8);  // (host offsets were checked above)
+      if (!st) st = device_fill(ctx, (u64 *)lcnt + 2 * G + 1, 8, 0);
+    }
     if (!st) {
       hipLaunchKernelGGL(widen_u32_kernel, dim3(small_grid(ctx, G + 1)), dim3(kBlock), 0, ctx->stream,
                          (u64 *)lcnt + G + 1, (const unsigned *)ex.viol, (unsigned long long)G, (u64)0);
@@ -523,10 +582,21 @@ int crdt_orswot_lub_many_sharded(crdt_ctx *ctx, const crdt_orswot_batch *in, crd
   CRDT_HIP(ctx, hipMemcpyAsync(rows.data(), acnt, rows.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
   CRDT_HIP(ctx, hipStreamSynchronize(ctx->stream));
   bool chain = false;  // some rank's shard holds a cell with E > C (rank-uniform: gathered flags)
+  long bad_off = -1;   // the first rank whose device offsets failed their check
   for (size_t r = 0; r < W; ++r) {
     std::copy(rows.begin() + r * crow, rows.begin() + r * crow + G + 1, all.begin() + r * (G + 1));
     for (size_t g = 0; g < G; ++g) chain = chain || (rows[r * crow + G + 1 + g] & 1);
+    if (bad_off < 0 && rows[r * crow + 2 * G + 1]) bad_off = (long)r;
   }
+  timing_end(ctx);
+  if (bad_off >= 0) {  // every rank saw the same rows: all return here, before any deferred row moves
+    if (bad_off == (long)ctx->rank)
+      return fail(ctx, CRDT_EINVAL, "%s: invalid def_off (entry 0 must be 0, entry G must be D, "
+                  "non-decreasing)", what);
+    return fail(ctx, CRDT_ECOMM, "%s: rank %ld passed invalid def_off; no deferred removes were exchanged", what,
+                bad_off);
+  }
+  timing_begin(ctx, "shard_exchange");
   chain = chain && W > 1;
   size_t Dmax = 0, Dtot = 0;
   for (size_t r = 0; r < W; ++r) {
@@ -622,6 +692,17 @@ int crdt_orswot_lub_many_sharded(crdt_ctx *ctx, const crdt_orswot_batch *in, crd
   }
   *out->ndef = nkeep;
   return CRDT_OK;
+}
+
+extern "C" {
+
+int crdt_orswot_lub_many_sharded(crdt_ctx *ctx, const crdt_orswot_batch *in, crdt_orswot_sharded_out *out) {
+  return orswot_sharded_impl(ctx, in, nullptr, 0, out, "orswot_lub_many_sharded");
+}
+
+int crdt_orswot_lub_many_sharded_doff(crdt_ctx *ctx, const crdt_orswot_batch *in, const uint64_t *def_off, size_t D,
+                                      crdt_orswot_sharded_out *out) {
+  return orswot_sharded_impl(ctx, in, (const u64 *)def_off, D, out, "orswot_lub_many_sharded_doff");
 }
 
 int crdt_lub_many_multi_sharded(crdt_ctx *ctx, const crdt_lub_segment *segs, size_t nseg) {
@@ -723,8 +804,12 @@ int crdt_lwwreg_lub_many_sharded(crdt_ctx *ctx, const uint64_t *marker, const ui
   return crdt_lwwreg_lub_many(ctx, tm, tv, G, n, n, out_marker, out_val, nullptr, 0);
 }
 
-int crdt_map_lub_many_sharded(crdt_ctx *ctx, const crdt_map_batch *in, size_t k0, size_t K, crdt_map_out *out) {
-  static const char *what = "map_lub_many_sharded";
+}  // extern "C"
+
+// doff: device offsets (in->def_off NULL, Ddev the pool length): checked on the device (flags bit
+// 1), and their hash travels in the flags row, compared on every rank after that exchange.
+static int map_sharded_impl(crdt_ctx *ctx, const crdt_map_batch *in, const u64 *doff, size_t Ddev, size_t k0,
+                            size_t K, crdt_map_out *out, const char *what) {
   CRDT_CHECK_CTX(ctx);
   CRDT_TRY(need_comm(ctx));
   CRDT_HIP(ctx, hipSetDevice(ctx->device));
@@ -732,34 +817,43 @@ int crdt_map_lub_many_sharded(crdt_ctx *ctx, const crdt_map_batch *in, size_t k0
   const size_t W = (size_t)ctx->nranks;
   int st = device_mem_only(ctx, what);
   if (!st && (!in || !out)) st = fail(ctx, CRDT_EINVAL, "%s: NULL argument", what);
+  if (!st && doff && in->def_off) st = fail(ctx, CRDT_EINVAL, "%s: in->def_off must be NULL", what);
+  if (!st && !doff && Ddev) st = fail(ctx, CRDT_EINVAL, "%s: D > 0 without def_off", what);
   const size_t G = st ? 0 : in->G, Kk = st ? 0 : in->K, A = st ? 0 : in->A, R = st ? 0 : in->R;
   if (!st && k0 + Kk > K) st = fail(ctx, CRDT_EINVAL, "%s: key range [%zu, %zu) past K = %zu", what, k0, k0 + Kk, K);
   if (!st && G && A && (!out->clock || !out->flags)) st = fail(ctx, CRDT_EINVAL, "%s: NULL output", what);
   if (!st && in->def_off && G && in->def_off[0] != 0) st = fail(ctx, CRDT_EINVAL, "%s: def_off[0] must be 0", what);
-  const size_t D = (!st && in->def_off && G > 0) ? in->def_off[G] : 0;
+  const size_t D = st ? 0 : doff ? Ddev : (in->def_off && G > 0) ? in->def_off[G] : 0;
   const size_t Kw = (K + 63) / 64, Kwl = Kk ? (Kk + 63) / 64 : 1;
   if (!st && D && (!in->def_keys || !in->def_clock || !in->def_row || !out->def_keys || !out->def_keep))
     st = fail(ctx, CRDT_EINVAL, "%s: deferred buffers missing", what);
   if (!st && D > 0xffffffffULL) st = fail(ctx, CRDT_EUNSUPPORTED, "%s: too many deferred removes", what);
   const bool work = G > 0 && A > 0;
+  // the flags row per rank: [G flags | status | offsets hash (device offsets; 0 otherwise)]
+  const size_t frow = G + 2;
   void *lk = nullptr, *ok = nullptr, *fl = nullptr, *fall = nullptr;
   if (!st && work) {
-    st = sbuf(ctx, 2, (G + 1) * 8, &fl);
-    if (!st) st = sbuf(ctx, 3, W * (G + 1) * 8, &fall);
+    st = sbuf(ctx, 2, frow * 8, &fl);
+    if (!st) st = sbuf(ctx, 3, W * frow * 8, &fall);
     if (!st && D) st = sbuf(ctx, 0, D * Kwl * 8, &lk);
     if (!st && D) st = sbuf(ctx, 1, D * Kwl * 8, &ok);
   }
   crdt_map_batch loc{};
   crdt_map_out lo{};
+  void *dchk = nullptr;
   // the rank's part: its keys' exact left fold (keys are independent given the clocks and the
   // deferred list: no data-path collective), or with no keys the clock lub and the
   // removes' survival alone (def_keep is a function of the clocks and the deferred list)
   auto local = [&](size_t vstate) -> int {
     if (Kk > 0) {
       lo.Vstate = vstate;
-      return crdt_map_lub_many(ctx, &loc, &lo);
+      return doff ? crdt_map_lub_many_doff(ctx, &loc, (const uint64_t *)doff, D, &lo) : crdt_map_lub_many(ctx, &loc, &lo);
     }
     if (int rc = device_fill(ctx, out->flags, G * 4, 0)) return rc;
+    if (doff) {  // the offsets' check alone (flags bit 1), as the fold would make it
+      if (int rc = sbuf(ctx, 4, (G + 1) * 8, &dchk)) return rc;
+      if (int rc = stage_def_off_dev(ctx, doff, (size_t *)dchk, G, D, nullptr, out->flags)) return rc;
+    }
     if (int rc = lattice_lub_many(ctx, Op::Max, (const u64 *)in->clock, G, R, A, in->clock_rstride,
                                   in->clock_gstride, (u64 *)out->clock, A, 0))
       return rc;
@@ -776,7 +870,7 @@ int crdt_map_lub_many_sharded(crdt_ctx *ctx, const crdt_map_batch *in, size_t k0
     q.apply_ceiling = 0;
     q.out_keep = out->def_keep;
     q.out_members = (u64 *)ok;
-    return launch_deferred(ctx, in->def_off, q);
+    return launch_deferred(ctx, in->def_off, q, doff);
   };
   if (!st && work) {
     loc = *in;
@@ -802,21 +896,32 @@ int crdt_map_lub_many_sharded(crdt_ctx *ctx, const crdt_map_batch *in, size_t k0
   // on EVERY rank (each key's result is independent of the state size), so the ranks take the same
   // branches and meet in the same collectives
   size_t vstate = vst0;
-  std::vector<uint64_t> hf(W * (G + 1));
+  std::vector<uint64_t> hf(W * frow);
   std::vector<uint32_t> gflags(G);
   for (;;) {
     hipLaunchKernelGGL(widen_u32_kernel, dim3(small_grid(ctx, G + 1)), dim3(kBlock), 0, ctx->stream, (u64 *)fl,
                        (const uint32_t *)out->flags, (unsigned long long)G, (u64)(st ? 1 : 0));
     CRDT_HIP(ctx, hipGetLastError());
-    CRDT_TRY(coll_allgather(ctx, fl, fall, (G + 1) * 8));
+    CRDT_TRY(device_fill(ctx, (u64 *)fl + G + 1, 8, 0));
+    if (doff) {
+      hipLaunchKernelGGL(def_hash_kernel, dim3(small_grid(ctx, G + 1)), dim3(kBlock), 0, ctx->stream, doff,
+                         (unsigned long long)(G + 1), (u64 *)fl + G + 1);
+      CRDT_HIP(ctx, hipGetLastError());
+    }
+    CRDT_TRY(coll_allgather(ctx, fl, fall, frow * 8));
     CRDT_HIP(ctx, hipMemcpyAsync(hf.data(), fall, hf.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
     CRDT_HIP(ctx, hipStreamSynchronize(ctx->stream));
     bool bad, grow;
-    shard_host::map_flags_or(hf.data(), W, G, gflags.data(), &bad, &grow);
+    shard_host::map_flags_or(hf.data(), W, G, gflags.data(), &bad, &grow, frow);
     if (bad) {
       if (st) return st;
       return fail(ctx, CRDT_ECOMM, "%s: another rank failed its local fold; no key sets were exchanged", what);
     }
+    for (size_t r = 1; r < W; ++r)
+      if (hf[r * frow + G + 1] != hf[G + 1])
+        return fail(ctx, CRDT_EINVAL, "%s: the ranks hold different deferred offsets (device offsets' hash "
+                    "differs between rank 0 and rank %zu); no key sets were exchanged", what, r);
+
     if (!grow || vstate >= 16) break;
     vstate = vstate < 8 ? 8 : 16;
     st = Kk > 0 ? local(vstate) : CRDT_OK;
@@ -833,6 +938,17 @@ int crdt_map_lub_many_sharded(crdt_ctx *ctx, const crdt_map_batch *in, size_t k0
   CRDT_TRY(coll_allreduce(ctx, (const u64 *)out->def_keys, (u64 *)out->def_keys, D * Kw, Red::Sum));
   timing_end(ctx);
   return CRDT_OK;
+}
+
+extern "C" {
+
+int crdt_map_lub_many_sharded(crdt_ctx *ctx, const crdt_map_batch *in, size_t k0, size_t K, crdt_map_out *out) {
+  return map_sharded_impl(ctx, in, nullptr, 0, k0, K, out, "map_lub_many_sharded");
+}
+
+int crdt_map_lub_many_sharded_doff(crdt_ctx *ctx, const crdt_map_batch *in, const uint64_t *def_off, size_t D,
+                                   size_t k0, size_t K, crdt_map_out *out) {
+  return map_sharded_impl(ctx, in, (const u64 *)def_off, D, k0, K, out, "map_lub_many_sharded_doff");
 }
 
 }  // extern "C"

@@ -87,16 +87,18 @@ inline size_t lww_nonempty(const uint64_t *rows, size_t W, size_t row, size_t G,
 // Map key shards: rows[W][G+1] = every rank's per-group flags and (word G) its local status.
 // gflags[g] = OR of the ranks' flags; *bad = some rank failed; *grow = some key's fold state ran
 // out of value slots (flags bit 2) on some rank.
-inline void map_flags_or(const uint64_t *rows, size_t W, size_t G, uint32_t *gflags, bool *bad, bool *grow) {
+inline void map_flags_or(const uint64_t *rows, size_t W, size_t G, uint32_t *gflags, bool *bad, bool *grow,
+                         size_t stride = 0) {
+  if (stride == 0) stride = G + 1;  // row r: [G flags | status | ...] at rows + r * stride
   *bad = false;
   *grow = false;
   for (size_t g = 0; g < G; ++g) {
     uint32_t f = 0;
-    for (size_t r = 0; r < W; ++r) f |= (uint32_t)rows[r * (G + 1) + g];
+    for (size_t r = 0; r < W; ++r) f |= (uint32_t)rows[r * stride + g];
     gflags[g] = f;
     *grow = *grow || (f & 4u) != 0;
   }
-  for (size_t r = 0; r < W; ++r) *bad = *bad || rows[r * (G + 1) + G] != 0;
+  for (size_t r = 0; r < W; ++r) *bad = *bad || rows[r * stride + G] != 0;
 }
 
 // Order-sensitive hash of a host offset array (def_off must be identical on every rank of a

@@ -145,6 +145,23 @@ def cabi_seam(rank, world, t, h):
     o["cabi_orswot_clock"], o["cabi_orswot_entries"] = h(res.clock), h(res.entries)
     o["cabi_orswot_def_clock"], o["cabi_orswot_def_members"] = h(res.def_clock), h(res.def_members)
     o["cabi_orswot_ndef_local"] = np.array([d1 - d0], np.int64)
+    # the same with the offsets in device memory (crdt_orswot_lub_many_sharded_doff: counts taken on
+    # the device, no host copy of the offsets)
+    if d1 > d0:
+        kw["def_off"] = torch.tensor([0, d1 - d0], dtype=torch.int64, device=dev)
+    res = cs.orswot_lub_many_sharded(t(clock[lo:hi][None]), t(entries[lo:hi][None]), ctx=ctx, **kw)
+    o["cabi_orswot_doff_clock"], o["cabi_orswot_doff_entries"] = h(res.clock), h(res.entries)
+    o["cabi_orswot_doff_def_clock"], o["cabi_orswot_doff_def_members"] = h(res.def_clock), h(res.def_members)
+    # invalid device offsets on rank 1 only: rank 1 gets EINVAL, rank 0 ECOMM, nobody blocks
+    Dl = max(d1 - d0, 1)
+    bad_off = torch.tensor([0, Dl] if rank == 0 else [1, Dl], dtype=torch.int64, device=dev)
+    zc = torch.zeros((Dl, clock.shape[1]), dtype=torch.int64, device=dev)
+    zm = torch.zeros((Dl, dmem.shape[1]), dtype=torch.int64, device=dev)
+    try:
+        cs.orswot_lub_many_sharded(t(clock[lo:hi][None]), t(entries[lo:hi][None]), bad_off, zc, zm, ctx=ctx)
+        o["cabi_orswot_badoff_code"] = np.array([0], np.int64)
+    except CrdtGpuError as e:
+        o["cabi_orswot_badoff_code"] = np.array([e.code], np.int64)
     # Orswot on ARBITRARY states (E > C cells): the planted non-associative cells sit
     # at replica 0 (rank 0) and R-2, R-1 (rank 1), so joining the rank partials as a tree is wrong; the
     # flags gathered with the deferred counts switch the ranks to the rank-order chain
@@ -162,15 +179,37 @@ def cabi_seam(rank, world, t, h):
     Dn = d["def_row"].shape[0]
     kw = dict(def_off=[0, Dn], def_row=torch.from_numpy(d["def_row"].astype(np.int32)).to(dev),
               def_clock=t(d["def_clock"]), def_keys=t(d["def_keys"])) if Dn else {}
-    for tag, (k0, k1) in (("even", cdist.shard_range(K, rank, world)), ("empty", (0, K) if rank == 0 else (K, K))):
+    for tag, (k0, k1) in (("even", cdist.shard_range(K, rank, world)), ("empty", (0, K) if rank == 0 else (K, K)),
+                          ("even_doff", cdist.shard_range(K, rank, world)),
+                          ("empty_doff", (0, K) if rank == 0 else (K, K))):
+        kwt = dict(kw)
+        if tag.endswith("_doff") and Dn:  # offsets in device memory (crdt_map_lub_many_sharded_doff)
+            kwt["def_off"] = torch.tensor([0, Dn], dtype=torch.int64, device=dev)
         mres = cs.map_lub_many_sharded(t(d["clock"][None]), t(d["ec"][None, :, k0:k1]), t(d["vclk"][None, :, k0:k1]),
-                                       t(d["vval"][None, :, k0:k1]), k0, K, vout=D.MAP_VOUT, ctx=ctx, **kw)
+                                       t(d["vval"][None, :, k0:k1]), k0, K, vout=D.MAP_VOUT, ctx=ctx, **kwt)
         o[f"cabi_map_{tag}_k0"] = np.array([k0, k1], np.int64)
         o[f"cabi_map_{tag}_clock"], o[f"cabi_map_{tag}_ec"] = h(mres.clock), h(mres.ec)
         o[f"cabi_map_{tag}_vclk"], o[f"cabi_map_{tag}_vval"] = h(mres.vclk), h(mres.vval)
         o[f"cabi_map_{tag}_nval"] = mres.nval.cpu().numpy().copy()
         o[f"cabi_map_{tag}_keep"] = mres.def_keep.cpu().numpy().copy()
         o[f"cabi_map_{tag}_def_keys"] = h(mres.def_keys)
+    # Map with device offsets that differ between the ranks (same G and D, so the agreed header
+    # matches): the offsets' hash in the flags exchange differs, so BOTH ranks raise EINVAL
+    if Dn >= 2:
+        c2 = np.stack([d["clock"], d["clock"]])
+        e2 = np.stack([d["ec"], d["ec"]])
+        v2 = np.stack([d["vclk"], d["vclk"]])
+        w2 = np.stack([d["vval"], d["vval"]])
+        k0, k1 = cdist.shard_range(K, rank, world)
+        split = 1 if rank == 0 else 2
+        offd = torch.tensor([0, split, Dn], dtype=torch.int64, device=dev)
+        try:
+            cs.map_lub_many_sharded(t(c2), t(e2[:, :, k0:k1]), t(v2[:, :, k0:k1]), t(w2[:, :, k0:k1]), k0, K,
+                                    def_off=offd, def_row=kw["def_row"], def_clock=kw["def_clock"],
+                                    def_keys=kw["def_keys"], vout=D.MAP_VOUT, ctx=ctx)
+            o["cabi_mapoff_code"] = np.array([0], np.int64)
+        except CrdtGpuError as e:
+            o["cabi_mapoff_code"] = np.array([e.code], np.int64)
     # Map: only rank 1's key folds to more values than vout=8 (its fold state overflows first, so the
     # C call reruns every rank with the larger state); the flags are global, so BOTH ranks raise the
     # capacity error, then both succeed with vout=16

@@ -85,12 +85,18 @@ def test_every_compute_entry_point_guards_host_mode():
             if name in HOST_CAPABLE:
                 assert ("CRDT_CHECK_CTX" in first or "_dispatch(ctx" in first or first.startswith("return crdt_")
                         or "_host(ctx" in first or "mem_kind == CRDT_MEM_HOST" in first), name
-            elif name.endswith("_sharded"):
+            elif name.endswith("_sharded") or name.endswith("_sharded_doff"):
                 # collective: the host-mode refusal is part of the agreed validation status (every
-                # rank must learn it), so it is not the first statement (csrc/shard.hip)
+                # rank must learn it), so it is not the first statement (csrc/shard.hip); the Orswot
+                # and Map pairs share an impl that makes that check
                 body = open(f).read()[m.end(2):]
                 body = body[:body.index("\n}\n")]
-                assert first.startswith("return lattice_sharded(") or "device_mem_only(ctx, what)" in body, name
+                impl = re.match(r"return (lattice_sharded|orswot_sharded_impl|map_sharded_impl)\(", first)
+                assert impl or "device_mem_only(ctx, what)" in body, name
+                if impl:
+                    src = open(f).read()
+                    i = src.index(f"static int {impl.group(1)}(")
+                    assert "device_mem_only(ctx, what)" in src[i:src.index("\n}\n", i)], impl.group(1)
             elif name not in CTX_ONLY:
                 assert first.startswith("CRDT_DEVICE_MEM_ONLY(ctx);"), (f, name)
     assert HOST_CAPABLE <= seen and len(seen) > 50

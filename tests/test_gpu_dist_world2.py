@@ -149,6 +149,21 @@ def test_world2_cabi_orswot(outs):
         assert got == odef
 
 
+def test_world2_cabi_orswot_doff(outs):
+    """crdt_orswot_lub_many_sharded_doff at world 2: the same result as the host-offset call (device
+    counts in the exchanged row); invalid offsets on rank 1 only -> EINVAL there, ECOMM on rank 0."""
+    for o in outs:
+        for k in ("clock", "entries", "def_clock", "def_members"):
+            np.testing.assert_array_equal(o[f"cabi_orswot_doff_{k}"], o[f"cabi_orswot_{k}"])
+    codes = sorted(int(o["cabi_orswot_badoff_code"][0]) for o in outs)
+    assert codes == sorted([-1, -5]), codes  # CRDT_EINVAL, CRDT_ECOMM
+
+
+def test_world2_cabi_map_offsets_differ(outs):
+    """Device offsets that differ between the ranks (same G and D): both ranks return EINVAL."""
+    assert all(int(o["cabi_mapoff_code"][0]) == -1 for o in outs)  # CRDT_EINVAL
+
+
 def test_world2_cabi_orswot_any_state(outs):
     """crdt_orswot_lub_many_sharded at world 2 on states with E > C cells whose non-associative
     sequence spans the rank boundary: the ranks fold in rank order (csrc/shard.hip), so both hold
@@ -166,7 +181,7 @@ def test_world2_cabi_orswot_any_state(outs):
         assert got == odef
 
 
-@pytest.mark.parametrize("tag", ["even", "empty"])
+@pytest.mark.parametrize("tag", ["even", "empty", "even_doff", "empty_doff"])
 def test_world2_cabi_map(outs, tag):
     """crdt_map_lub_many_sharded at world 2: key placement at k0 != 0 with the SUM all-reduce, and
     a rank whose key shard is EMPTY (it must still join every collective: ADVICE r2)."""
@@ -186,7 +201,7 @@ def test_world2_cabi_map(outs, tag):
         got = {(tuple(int(x) for x in d["def_clock"][j]), O.bitmap_members(o[f"cabi_map_{tag}_def_keys"][j]))
                for j in np.flatnonzero(o[f"cabi_map_{tag}_keep"])}
         assert got == exp[5]
-    if tag == "empty":
+    if tag.startswith("empty"):
         assert (d["ec"].shape[1], d["ec"].shape[1]) in covered
 
 

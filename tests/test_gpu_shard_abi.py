@@ -47,8 +47,10 @@ def test_lattice_sharded_world1(comm_ctx, kind, W, G, R):
     np.testing.assert_array_equal(got, exp)
 
 
+@pytest.mark.parametrize("devoff", [False, True])
 @pytest.mark.parametrize("seed,G,R,M,A", [(1, 1, 40, 64, 8), (2, 3, 12, 50, 8), (3, 2, 1, 130, 65)])
-def test_orswot_sharded_world1(comm_ctx, seed, G, R, M, A):
+def test_orswot_sharded_world1(comm_ctx, seed, G, R, M, A, devoff):
+    """devoff: the deferred offsets as a device tensor (crdt_orswot_lub_many_sharded_doff)."""
     parts = [O.gen_orswot(seed * 10 + g, R, M, A, kmax=10, p_def=0.4) for g in range(G)]
     clock = np.stack([p[0] for p in parts])
     entries = np.stack([p[1] for p in parts])
@@ -59,6 +61,8 @@ def test_orswot_sharded_world1(comm_ctx, seed, G, R, M, A):
     dcl = np.concatenate([p[3] for p in parts]).reshape(-1, A)
     dmem = np.concatenate([p[4] for p in parts]).reshape(-1, Mw)
     kw = dict(def_off=off, def_clock=to_dev(dcl), def_members=to_dev(dmem)) if off[-1] else {}
+    if devoff:
+        kw["def_off"] = torch.tensor(off, dtype=torch.int64, device="cuda:0")
     res = cg.shard.orswot_lub_many_sharded(to_dev(clock), to_dev(entries), ctx=comm_ctx, **kw)
     got_c, got_e = to_host(res.clock), to_host(res.entries)
     got_d = cg.shard.deferred_groups(res, G)
@@ -70,6 +74,25 @@ def test_orswot_sharded_world1(comm_ctx, seed, G, R, M, A):
     # a too-small def_cap is retried with exactly enough room
     small = cg.shard.orswot_lub_many_sharded(to_dev(clock), to_dev(entries), ctx=comm_ctx, def_cap=1, **kw)
     assert cg.shard.deferred_groups(small, G) == got_d
+
+
+@pytest.mark.parametrize("bad", [[1, 3, 5], [0, 4, 3], [0, 2, 4]])
+def test_orswot_sharded_doff_invalid(comm_ctx, bad):
+    """Invalid device offsets (entry 0 != 0, decreasing, entry G != D) are refused after the count
+    exchange (EINVAL on the rank that passed them), not read out of range; the ctx stays usable."""
+    G, R, M, A = 2, 6, 40, 5
+    parts = [O.gen_orswot(70 + g, R, M, A, kmax=6, p_def=0.5) for g in range(G)]
+    clock = to_dev(np.stack([p[0] for p in parts]))
+    entries = to_dev(np.stack([p[1] for p in parts]))
+    D = 5
+    dcl = torch.zeros((D, A), dtype=torch.int64, device="cuda:0")
+    dmb = torch.zeros((D, 1), dtype=torch.int64, device="cuda:0")
+    with pytest.raises(cg.CrdtGpuError, match="def_off"):
+        cg.shard.orswot_lub_many_sharded(clock, entries, torch.tensor(bad, dtype=torch.int64, device="cuda:0"),
+                                         dcl, dmb, ctx=comm_ctx)
+    ok = cg.shard.orswot_lub_many_sharded(clock, entries, ctx=comm_ctx)
+    for g, (c, e, _, _, _) in enumerate(parts):
+        np.testing.assert_array_equal(to_host(ok.clock[g]), O.orswot_fold(c, e)[0])
 
 
 @pytest.mark.parametrize("G,R,base", [(3, 201, 0), (2, 57, 1000), (1, 0, 7)])
@@ -90,8 +113,9 @@ def test_lwwreg_sharded_world1(comm_ctx, G, R, base):
     assert R == 0 or any(int(x) != 2**64 - 1 for x in fc)
 
 
-@pytest.mark.parametrize("k0,Kk", [(0, 29), (5, 15), (20, 9)])
-def test_map_sharded_world1(comm_ctx, k0, Kk):
+@pytest.mark.parametrize("devoff", [False, True])
+@pytest.mark.parametrize("k0,Kk", [(0, 29), (5, 15), (20, 9), (3, 0)])
+def test_map_sharded_world1(comm_ctx, k0, Kk, devoff):
     """crdt_map_lub_many_sharded at world 1 over a key range: the rank's keys equal the oracle's
     whole-map fold restricted to them, and the surviving removes' key sets (over ALL keys) hold
     exactly this rank's keys of them (the bitmap restriction / placement around the exchange)."""
@@ -101,8 +125,9 @@ def test_map_sharded_world1(comm_ctx, k0, Kk):
     exp = O.map_fold(d["clock"], d["ec"], d["vclk"], d["vval"], d["def_row"], d["def_clock"], d["def_keys"], 8)
     Dn = d["def_row"].shape[0]
     t = lambda a: to_dev(np.ascontiguousarray(a))  # noqa: E731
+    off = torch.tensor([0, Dn], dtype=torch.int64, device="cuda:0") if devoff else [0, Dn]
     res = cg.shard.map_lub_many_sharded(t(d["clock"]), t(d["ec"][:, k0:k0 + Kk]), t(d["vclk"][:, k0:k0 + Kk]),
-                                        t(d["vval"][:, k0:k0 + Kk]), k0, K, def_off=[0, Dn],
+                                        t(d["vval"][:, k0:k0 + Kk]), k0, K, def_off=off,
                                         def_row=torch.from_numpy(d["def_row"].astype(np.int32)).cuda(),
                                         def_clock=t(d["def_clock"]), def_keys=t(d["def_keys"]), vout=8, ctx=comm_ctx)
     np.testing.assert_array_equal(to_host(res.clock), exp[0])
@@ -111,7 +136,10 @@ def test_map_sharded_world1(comm_ctx, k0, Kk):
     np.testing.assert_array_equal(to_host(res.vval), exp[3][k0:k0 + Kk])
     got = cg.map.deferred_set(t(d["def_clock"]), res.def_keep, res.def_keys)
     want = {(c, frozenset(k for k in ks if k0 <= k < k0 + Kk)) for c, ks in exp[5]}
-    assert got == want and len(want) > 0
+    if Kk:
+        assert got == want and len(want) > 0
+    else:  # an empty key shard: the clock lub and the removes' survival alone
+        assert {c for c, _ in got} == {c for c, _ in want} and len(want) > 0
 
 
 def test_config5_shard_world1(comm_ctx):
