@@ -548,21 +548,17 @@ static int orswot_sharded_impl(crdt_ctx *ctx, const crdt_orswot_batch *in, const
       ex.viol = reinterpret_cast<unsigned *>((u64 *)pc + G * A);
       st = orswot_lub_many_ex(ctx, &loc, &po, ex);
     }
-    if (!st && doff) {
-      st = device_fill(ctx, (u64 *)lcnt + 2 * G + 1, 8, 0);
-      if (!st) {
-        hipLaunchKernelGGL(def_counts_kernel, dim3(small_grid(ctx, G + 1)), dim3(kBlock), 0, ctx->stream, doff,
-                           (u64 *)lcnt, (unsigned long long)G, (unsigned long long)Dk, (u64 *)lcnt + 2 * G + 1);
-        if (hipGetLastError() != hipSuccess) st = fail(ctx, CRDT_EHIP, "%s: def_counts_kernel launch", what);
-      }
-    } else if (!st) {
-      st = stage_h2d(ctx, lcnt, head.data(), (G + 1) * 8);  // (host offsets were checked above)
-      if (!st) st = device_fill(ctx, (u64 *)lcnt + 2 * G + 1, 8, 0);
-    }
-    if (!st) {
+    if (!st) {  // the G flags, then word 2G+1 = 0 (widen writes G+1 words: the last is `extra`)
       hipLaunchKernelGGL(widen_u32_kernel, dim3(small_grid(ctx, G + 1)), dim3(kBlock), 0, ctx->stream,
                          (u64 *)lcnt + G + 1, (const unsigned *)ex.viol, (unsigned long long)G, (u64)0);
       if (hipGetLastError() != hipSuccess) st = fail(ctx, CRDT_EHIP, "%s: widen_u32_kernel launch", what);
+    }
+    if (!st && doff) {  // counts and the offsets' check (into word 2G+1) on the device, after widen
+      hipLaunchKernelGGL(def_counts_kernel, dim3(small_grid(ctx, G + 1)), dim3(kBlock), 0, ctx->stream, doff,
+                         (u64 *)lcnt, (unsigned long long)G, (unsigned long long)Dk, (u64 *)lcnt + 2 * G + 1);
+      if (hipGetLastError() != hipSuccess) st = fail(ctx, CRDT_EHIP, "%s: def_counts_kernel launch", what);
+    } else if (!st) {
+      st = stage_h2d(ctx, lcnt, head.data(), (G + 1) * 8);  // (host offsets were checked above)
     }
   }
   CRDT_TRY(agree(ctx, st, make_hdr(st, kTagOrswot, {G, M, A}), what));
