@@ -81,6 +81,8 @@ struct Tune {
   int map_forget_bpc = 1;      // Map forget, 16-byte kernel: workgroups per CU (1: 67% of 8 TB/s vs 64% at 4)
   int map_pair_pf = 0;         // Map merge_batch sub-wave key pass: the next keys' rows loaded before the merge
                                //     (opt-in: 5.86 vs 5.81 ms at 4 waves/SIMD, profiles/r04_map_pair_pf_ab.log)
+  int map_pair_nt = 1;         // ... sub-wave key pass: key rows loaded / stored non-temporal (5.14 -> 5.00 ms,
+                               //     profiles/r04_map_pair_nt_ab.log)
   int map_pair_bpc = 64;       // Map merge_batch key pass: workgroups per CU (grid-stride over keys;
                                //     latency-bound: 16 -> 64 is 64% -> 67-69% of 8 TB/s)
   int merge_flat = 1;          // lattice merge_batch of packed rows: workgroups per CU of the flat

@@ -229,6 +229,7 @@ static void apply_tune(crdt_ctx *ctx, const char *t) {
       else if (k == "afence") ctx->tune.apply_fence = v != 0;
       else if (k == "alane") ctx->tune.apply_lane = v != 0;
       else if (k == "mfu" && (v == 1 || v == 2 || v == 4)) ctx->tune.merge_flat_u = v;
+      else if (k == "mpnt") ctx->tune.map_pair_nt = v != 0;
       else if (k == "mppf") ctx->tune.map_pair_pf = v != 0;
       else if (k == "ohpf") ctx->tune.orswot_apply_hpf = v != 0;
       else if (k == "oapf") ctx->tune.orswot_apply_pf = v != 0;

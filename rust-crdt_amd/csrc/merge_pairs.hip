@@ -696,7 +696,7 @@ struct SegRows {
   bool hitl;  // segment lane d: remove d (self's, then other's) names k
 };
 
-template <int SEG, int VM, bool PF>
+template <int SEG, int VM, bool PF, bool NT>
 __global__ __launch_bounds__(kBlock) void map_pair_join_seg_kernel(MapPairPlan p) {
   constexpr int KPW = kWave / SEG;  // keys per wave
   const Seg<SEG> sg(threadIdx.x % kWave);
@@ -726,15 +726,18 @@ __global__ __launch_bounds__(kBlock) void map_pair_join_seg_kernel(MapPairPlan p
     const u64 *ec1 = p.ec1 + s * p.ec1_s + k * A;
     const u64 *vc1 = p.vc1 + s * p.vc1_s + k * p.V1 * A;
     const u64 *vv1 = p.vv1 + s * p.vv1_s + k * p.V1;
+    // NT: the key rows are streamed once (non-temporal); the map clocks stay cached (every key of
+    // the pair reads them)
+    auto ld = [](const u64 *x) -> u64 { return NT ? __builtin_nontemporal_load(x) : *x; };
     if (act) {
-      L.e1 = ec1[sl];
-      L.e2 = ec2[sl];
+      L.e1 = ld(ec1 + sl);
+      L.e2 = ld(ec2 + sl);
       L.c1 = p.c1[s * p.c1_s + sl];
       L.c2 = p.c2[s * p.c2_s + sl];
 #pragma unroll
       for (int q = 0; q < VM; ++q) {
-        if ((unsigned)q < V1) L.x[q] = vc1[(unsigned long long)q * A + sl];
-        if ((unsigned)q < V2) L.y[q] = vc2[(unsigned long long)q * A + sl];
+        if ((unsigned)q < V1) L.x[q] = ld(vc1 + (unsigned long long)q * A + sl);
+        if ((unsigned)q < V2) L.y[q] = ld(vc2 + (unsigned long long)q * A + sl);
       }
     }
     L.v1l = (unsigned)sl < V1 ? vv1[sl] : 0ull;
@@ -764,6 +767,10 @@ __global__ __launch_bounds__(kBlock) void map_pair_join_seg_kernel(MapPairPlan p
     u64 *vc1 = p.vc1 + s * p.vc1_s + k * p.V1 * A;
     u64 *vv1 = p.vv1 + s * p.vv1_s + k * p.V1;
     const unsigned nd = n1 + n2;
+    auto st = [](u64 *x, u64 v) {
+      if (NT) __builtin_nontemporal_store(v, x);
+      else *x = v;
+    };
     const bool p1 = sg.any(e1 != 0), p2 = sg.any(e2 != 0);
     if (!p1 && !p2) return;
     unsigned m1 = 0, m2 = 0;
@@ -851,7 +858,7 @@ __global__ __launch_bounds__(kBlock) void map_pair_join_seg_kernel(MapPairPlan p
     }
     unsigned w = 0;
     if (present) {
-      if (act) ec1[sl] = e;
+      if (act) st(ec1 + sl, e);
 #pragma unroll
       for (int q = 0; q < VM; ++q) {
         if (!((keep1 >> q) & 1u)) continue;
@@ -860,7 +867,7 @@ __global__ __launch_bounds__(kBlock) void map_pair_join_seg_kernel(MapPairPlan p
         const u64 val = val1[q];
         if (!sg.any(z != 0)) continue;
         if (w < V1) {
-          if (act) vc1[(unsigned long long)w * A + sl] = z;
+          if (act) st(vc1 + (unsigned long long)w * A + sl, z);
           if (sl == 0) vv1[w] = val;
         }
         ++w;
@@ -873,17 +880,17 @@ __global__ __launch_bounds__(kBlock) void map_pair_join_seg_kernel(MapPairPlan p
         const u64 val = val2[r];
         if (!sg.any(z != 0)) continue;
         if (w < V1) {
-          if (act) vc1[(unsigned long long)w * A + sl] = z;
+          if (act) st(vc1 + (unsigned long long)w * A + sl, z);
           if (sl == 0) vv1[w] = val;
         }
         ++w;
       }
       if (w > V1 && sl == 0) atomicOr(p.status + s, 16u);
     } else if (act) {
-      ec1[sl] = 0;
+      st(ec1 + sl, 0);
     }
     for (unsigned q = w; q < V1; ++q) {
-      if (act) vc1[(unsigned long long)q * A + sl] = 0;
+      if (act) st(vc1 + (unsigned long long)q * A + sl, 0);
       if (sl == 0) vv1[q] = 0;
     }
   };
@@ -1030,16 +1037,19 @@ extern "C" int crdt_map_merge_batch(crdt_ctx *ctx, const crdt_map_states *self, 
                   other_def->Dcap ? other_def->count : nullptr, other_def->Dcap, status};
     const unsigned grid = pair_grid(ctx, (unsigned long long)N * K, ctx->tune.map_pair_bpc);
     timing_begin(ctx, "map_pair_join");
-    const bool pf = ctx->tune.map_pair_pf;
+    const bool pf = ctx->tune.map_pair_pf, nt = ctx->tune.map_pair_nt;
     if (ctx->tune.map_pair_reg && a.V <= 4 && b.V <= 4 && A <= 4 * (size_t)kWave) {  // register-resident rows
       if (A <= 16 && ctx->tune.map_pair_reg == 1)
-        hipLaunchKernelGGL((pf ? map_pair_join_seg_kernel<16, 4, true> : map_pair_join_seg_kernel<16, 4, false>),
+        hipLaunchKernelGGL((pf ? (nt ? map_pair_join_seg_kernel<16, 4, true, true> : map_pair_join_seg_kernel<16, 4, true, false>)
+                              : (nt ? map_pair_join_seg_kernel<16, 4, false, true> : map_pair_join_seg_kernel<16, 4, false, false>)),
                            dim3(grid), dim3(kBlock), 0, ctx->stream, p);
       else if (A <= 32 && ctx->tune.map_pair_reg == 1)
-        hipLaunchKernelGGL((pf ? map_pair_join_seg_kernel<32, 4, true> : map_pair_join_seg_kernel<32, 4, false>),
+        hipLaunchKernelGGL((pf ? (nt ? map_pair_join_seg_kernel<32, 4, true, true> : map_pair_join_seg_kernel<32, 4, true, false>)
+                              : (nt ? map_pair_join_seg_kernel<32, 4, false, true> : map_pair_join_seg_kernel<32, 4, false, false>)),
                            dim3(grid), dim3(kBlock), 0, ctx->stream, p);
       else if (A <= (size_t)kWave && ctx->tune.map_pair_reg == 1)
-        hipLaunchKernelGGL((pf ? map_pair_join_seg_kernel<64, 4, true> : map_pair_join_seg_kernel<64, 4, false>),
+        hipLaunchKernelGGL((pf ? (nt ? map_pair_join_seg_kernel<64, 4, true, true> : map_pair_join_seg_kernel<64, 4, true, false>)
+                              : (nt ? map_pair_join_seg_kernel<64, 4, false, true> : map_pair_join_seg_kernel<64, 4, false, false>)),
                            dim3(grid), dim3(kBlock), 0, ctx->stream, p);
       else if (A <= (size_t)kWave)
         hipLaunchKernelGGL((map_pair_join_reg_kernel<1, 4>), dim3(grid), dim3(kBlock), 0, ctx->stream, p);

@@ -200,7 +200,7 @@ def arbitrary_maps(rng, n, K, A, V, cmax, max_def=3):
     return maps
 
 
-@pytest.mark.parametrize("reg", ["mpreg=1", "mpreg=1,mppf=1", "mpreg=1,mppf=1,mpbpc=1", "mpreg=2", "mpreg=0"])
+@pytest.mark.parametrize("reg", ["mpreg=1", "mpreg=1,mpnt=0", "mpreg=1,mppf=1", "mpreg=1,mppf=1,mpbpc=1", "mpreg=2", "mpreg=0"])
 @pytest.mark.parametrize("seed,N,K,A,V,cmax", [(21, 40, 5, 3, 2, 4), (22, 25, 9, 33, 2, 3), (23, 16, 4, 70, 1, 3),
                                                (24, 30, 70, 8, 3, 6), (25, 12, 3, 200, 2, 2), (26, 20, 6, 5, 5, 3),
                                                (27, 24, 7, 32, 2, 4), (28, 9, 5, 17, 4, 3), (29, 40, 150, 30, 2, 3)])
