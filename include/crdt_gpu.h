@@ -570,6 +570,44 @@ int crdt_map_lub_many_sharded(crdt_ctx *ctx, const crdt_map_batch *in, size_t k0
 int crdt_map_lub_many_sharded_doff(crdt_ctx *ctx, const crdt_map_batch *in, const uint64_t *def_off, size_t D,
                                    size_t k0, size_t K, crdt_map_out *out);
 
+/* ---- Map<K, GCounter<A>, A> and Map<K, PNCounter<A>, A> (round 4) ----------------------------
+ * Map::merge (map.rs:140-220) with a counter value: GCounter (gcounter.rs:44-54: merge = the VClock
+ * max, Causal::forget = VClock::forget) or PNCounter (pncounter.rs:70-82: P and N each), folded as
+ * acc = Map::new(); for r: acc.merge(replica[g][r]) — exact for any input (each key folded in
+ * replica order: the fold is not associative for these values either).  Layout as crdt_map_batch,
+ * with the value of key k a block of W counter rows (W = 1 GCounter, W = 2 PNCounter: P then N):
+ *   val + g*val_gstride + r*val_rstride + (k*W + w)*A + a   (an absent key: its rows all 0)
+ * deferred removes pooled per group as for Map<K, MVReg>: def_off a HOST array of G+1 entries,
+ * def_row device u32 non-decreasing within the group and < R, def_clock [D][A], def_keys [D][Kw].
+ * Output per group g (packed): clock[g*A + a], ec[(g*K + k)*A + a], val[((g*K + k)*W + w)*A + a],
+ * flags[g] (required): bit 1 = def_row not non-decreasing or >= R, bit 3 = more than 512 live
+ * removes named one key (results of the group unreliable); def_keep / def_keys as crdt_map_out.
+ * Limits: A <= 256.  Device-memory contexts only. */
+typedef struct crdt_map_counter_batch {
+  size_t G, R, K, A, W;
+  const uint64_t *clock;
+  size_t clock_rstride, clock_gstride;
+  const uint64_t *ec;
+  size_t ec_rstride, ec_gstride;
+  const uint64_t *val;
+  size_t val_rstride, val_gstride;
+  const size_t *def_off; /* host, G+1 entries; NULL = no deferred removes */
+  const uint32_t *def_row;
+  const uint64_t *def_clock;
+  const uint64_t *def_keys;
+} crdt_map_counter_batch;
+
+typedef struct crdt_map_counter_out {
+  uint64_t *clock;    /* [G][A]       */
+  uint64_t *ec;       /* [G][K][A]    */
+  uint64_t *val;      /* [G][K][W][A] */
+  uint32_t *flags;    /* [G]          */
+  uint8_t *def_keep;  /* [D]          */
+  uint64_t *def_keys; /* [D][Kw]      */
+} crdt_map_counter_out;
+
+int crdt_map_counter_lub_many(crdt_ctx *ctx, const crdt_map_counter_batch *in, crdt_map_counter_out *out);
+
 /* ---- MVReg<u64, A> on its own (outside a Map) ------------------------------------------------
  * Replaces MVReg::merge (mvreg.rs:112-128) and MVReg::apply (mvreg.rs:130-166) for registers in the
  * dense layout the Map entry points use for their values: slots in Vec order, slot s of register i

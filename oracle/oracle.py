@@ -154,8 +154,19 @@ class GCounter:  # gcounter.rs:25-73
     def read(self) -> int:  # gcounter.rs:70-72 (BigUint sum)
         return sum(self.inner.dots.values())
 
+    def forget(self, clock: "VClock") -> None:  # Causal::forget gcounter.rs:50-54
+        self.inner.forget(clock)
+
+    def copy(self) -> "GCounter":
+        g = GCounter()
+        g.inner = self.inner.copy()
+        return g
+
     def __eq__(self, o):
         return isinstance(o, GCounter) and self.inner == o.inner
+
+    def __repr__(self):
+        return f"GCounter({self.inner})"
 
 
 class PNCounter:  # pncounter.rs:28-115
@@ -181,6 +192,21 @@ class PNCounter:  # pncounter.rs:28-115
 
     def read(self) -> int:  # pncounter.rs:110-115
         return self.p.read() - self.n.read()
+
+    def forget(self, clock: "VClock") -> None:  # Causal::forget pncounter.rs:77-82
+        self.p.forget(clock)
+        self.n.forget(clock)
+
+    def copy(self) -> "PNCounter":
+        c = PNCounter()
+        c.p, c.n = self.p.copy(), self.n.copy()
+        return c
+
+    def __eq__(self, o):
+        return isinstance(o, PNCounter) and self.p == o.p and self.n == o.n
+
+    def __repr__(self):
+        return f"PNCounter(p={self.p.inner}, n={self.n.inner})"
 
 
 class GSet:  # gset.rs
@@ -1105,7 +1131,7 @@ def dense_to_map(clock, ec, vclk, vval, deferred=()) -> Map:
 
 def map_fold_objects(maps) -> Map:
     """The reference left fold: acc = Map::new(); for r: acc.merge(r)."""
-    acc = Map(MVReg)
+    acc = Map(maps[0].vnew if maps else MVReg)
     for m in maps:
         acc.merge(m)
     return acc
@@ -1257,16 +1283,19 @@ def map_fold(clock, ec, vclk, vval, def_row=None, def_clock=None, def_keys=None,
 
 
 def gen_map_replicas(seed: int, R: int, K: int, A: int, steps: int = 200, p_ooo: float = 0.4,
-                     p_up: float = 0.4, p_rm: float = 0.15):
+                     p_up: float = 0.4, p_rm: float = 0.15, vnew=None, write=None):
     """Realistic Map<int, MVReg<int>> replica states by op replay (reference semantics).
 
     A actors each own a replica and, at random: write a key (ctx from get(key), map.rs:272,
     test/map.rs:71-125), remove a key (rm ctx from get(key), test/map.rs:127-146), deliver
     logged ops of other actors (out of causal order with prob p_ooo — which is what leaves
     deferred removes, test/map.rs:265-300), or merge another actor's state (gossip).  R
-    snapshots of actor states at random times are returned (the fold's replicas)."""
+    snapshots of actor states at random times are returned (the fold's replicas).  `vnew` /
+    `write(value, ctx, val, actor) -> value op` select another value type (default MVReg::write)."""
     rng = np.random.default_rng(seed)
-    reps = [Map(MVReg) for _ in range(A)]
+    vnew = vnew or MVReg
+    write = write or (lambda r, c, v, a: r.write(v, c))
+    reps = [Map(vnew) for _ in range(A)]
     seen = [set() for _ in range(A)]
     log = []
     snaps = []
@@ -1277,7 +1306,7 @@ def gen_map_replicas(seed: int, R: int, K: int, A: int, steps: int = 200, p_ooo:
         x = rng.random()
         if x < p_up:
             k = int(rng.integers(K))
-            op = m.update(k, m.get(k).derive_add_ctx(a), lambda r, c, v=val: r.write(v, c))
+            op = m.update(k, m.get(k).derive_add_ctx(a), lambda r, c, v=val, a=a: write(r, c, v, a))
             val += 1
             m.apply(op)
             seen[a].add(len(log))
@@ -1310,6 +1339,78 @@ def gen_map_replicas(seed: int, R: int, K: int, A: int, steps: int = 200, p_ooo:
         snaps.append(reps[int(rng.integers(A))].copy())
     order = rng.permutation(R)
     return [snaps[int(i)] for i in order]
+
+
+# ---- Map<K, GCounter> / Map<K, PNCounter> (counter values, round 4) ------------------------------
+def counter_rows(val, A: int) -> np.ndarray:
+    """The dense value rows of a counter: GCounter -> (1, A), PNCounter -> (2, A) [P, N]."""
+    parts = [val.inner] if isinstance(val, GCounter) else [val.p.inner, val.n.inner]
+    out = np.zeros((len(parts), A), np.uint64)
+    for w, vc in enumerate(parts):
+        for a, c in vc.dots.items():
+            out[w, a] = c
+    return out
+
+
+def counter_from_rows(rows, W: int):
+    if W == 1:
+        g = GCounter()
+        g.inner = _vc_row(rows[0])
+        return g
+    c = PNCounter()
+    c.p.inner, c.n.inner = _vc_row(rows[0]), _vc_row(rows[1])
+    return c
+
+
+def map_counter_to_dense(maps, K: int, A: int, W: int):
+    """Ingest Map<int, GCounter> (W = 1) or Map<int, PNCounter> (W = 2) objects: clock (R, A),
+    ec (R, K, A), val (R, K, W, A) and the deferred pool (def_row, def_clock, def_keys)."""
+    R = len(maps)
+    clock = np.zeros((R, A), np.uint64)
+    ec = np.zeros((R, K, A), np.uint64)
+    val = np.zeros((R, K, W, A), np.uint64)
+    def_row, dcl, dk = [], [], []
+    for r, m in enumerate(maps):
+        for a, c in m.clock.dots.items():
+            clock[r, a] = c
+        for k, e in m.entries.items():
+            for a, c in e.clock.dots.items():
+                ec[r, k, a] = c
+            val[r, k] = counter_rows(e.val, A)
+        for rm, keys in m.deferred.items():
+            row = np.zeros(A, np.uint64)
+            for a, c in rm.dots.items():
+                row[a] = c
+            def_row.append(r)
+            dcl.append(row)
+            dk.append(_bits(keys, K))
+    D = len(def_row)
+    Kw = (K + 63) // 64
+    return dict(clock=clock, ec=ec, val=val, def_row=np.array(def_row, np.uint64),
+                def_clock=np.array(dcl, np.uint64).reshape(D, A), def_keys=np.array(dk, np.uint64).reshape(D, Kw))
+
+
+def dense_to_map_counter(clock, ec, val, deferred=()) -> Map:
+    """Egress of one folded dense Map<K, counter> state (clock (A,), ec (K, A), val (K, W, A))."""
+    W = val.shape[1]
+    m = Map(GCounter if W == 1 else PNCounter)
+    m.clock = _vc_row(clock)
+    for k in range(ec.shape[0]):
+        if ec[k].any():
+            m.entries[k] = MapEntry(_vc_row(ec[k]), counter_from_rows(val[k], W))
+    for rm, keys in deferred:
+        m.deferred[_vc_row(rm)] = set(keys)
+    return m
+
+
+def map_counter_objects(R: int, K: int, A: int, W: int, seed: int, steps: int = 300, **kw):
+    """Op-replay replicas of Map<int, GCounter> (W = 1: every write an inc of the writer's dot)
+    or Map<int, PNCounter> (W = 2: inc or dec at random)."""
+    rng = np.random.default_rng(seed ^ 0x6C0)
+    if W == 1:
+        return gen_map_replicas(seed, R, K, A, steps=steps, vnew=GCounter, write=lambda v, c, x, a: v.inc(a), **kw)
+    return gen_map_replicas(seed, R, K, A, steps=steps, vnew=PNCounter,
+                            write=lambda v, c, x, a: v.inc(a) if rng.random() < 0.6 else v.dec(a), **kw)
 
 
 def max_vals(maps) -> int:

@@ -52,7 +52,7 @@ EXPORTS = (
     "crdt_ctx_comm_init_ops", "crdt_ctx_comm_note",
     "crdt_mvreg_lub_many", "crdt_mvreg_merge_batch", "crdt_mvreg_apply_batch",
     "crdt_orswot_lub_many_doff", "crdt_map_lub_many_doff",
-    "crdt_orswot_lub_many_sharded_doff", "crdt_map_lub_many_sharded_doff",
+    "crdt_orswot_lub_many_sharded_doff", "crdt_map_lub_many_sharded_doff", "crdt_map_counter_lub_many",
 )
 
 
@@ -164,6 +164,20 @@ class MapBatch(ctypes.Structure):  # crdt_map_batch
     ]
 
 
+class MapCounterBatch(ctypes.Structure):  # crdt_map_counter_batch
+    _fields_ = [
+        ("G", S), ("R", S), ("K", S), ("A", S), ("W", S),
+        ("clock", P), ("clock_rstride", S), ("clock_gstride", S),
+        ("ec", P), ("ec_rstride", S), ("ec_gstride", S),
+        ("val", P), ("val_rstride", S), ("val_gstride", S),
+        ("def_off", ctypes.POINTER(S)), ("def_row", P), ("def_clock", P), ("def_keys", P),
+    ]
+
+
+class MapCounterOut(ctypes.Structure):  # crdt_map_counter_out
+    _fields_ = [("clock", P), ("ec", P), ("val", P), ("flags", P), ("def_keep", P), ("def_keys", P)]
+
+
 class MapOut(ctypes.Structure):  # crdt_map_out
     _fields_ = [("Vout", S), ("Vstate", S), ("clock", P), ("ec", P), ("vclk", P), ("vval", P), ("nval", P),
                 ("flags", P), ("def_keep", P), ("def_keys", P)]
@@ -222,6 +236,7 @@ _SIGS.update({
     "crdt_map_lub_many_sharded": ([P, ctypes.POINTER(MapBatch), S, S, ctypes.POINTER(MapOut)], ctypes.c_int),
     "crdt_map_lub_many_sharded_doff": ([P, ctypes.POINTER(MapBatch), P, S, S, S, ctypes.POINTER(MapOut)],
                                        ctypes.c_int),
+    "crdt_map_counter_lub_many": ([P, ctypes.POINTER(MapCounterBatch), ctypes.POINTER(MapCounterOut)], ctypes.c_int),
     "crdt_vclock_ingest": ([P, P, P, S, P, S, P, S, P], ctypes.c_int),
     "crdt_pncounter_ingest": ([P, P, P, S, P, S, P, S, P], ctypes.c_int),
     "crdt_gset_ingest": ([P, P, P, S, P, S, P, S, P], ctypes.c_int),

@@ -411,3 +411,87 @@ def merge_batch(self_states: MapStates, other: MapStates, ctx: Optional[Context]
     ctx.call("crdt_map_merge_batch", ctypes.byref(a), ctypes.byref(ad), ctypes.byref(b), ctypes.byref(bd),
              status.data_ptr())
     return status
+
+
+# ---- Map<K, GCounter> / Map<K, PNCounter> (crdt_map_counter_lub_many, round 4) ----------------------
+class MapCounterLub(NamedTuple):
+    clock: torch.Tensor               # (G, A)
+    ec: torch.Tensor                  # (G, K, A)
+    val: torch.Tensor                 # (G, K, W, A): GCounter row (W = 1) or P, N rows (W = 2)
+    flags: torch.Tensor               # (G,) int32
+    def_keep: Optional[torch.Tensor]  # (D,) uint8
+    def_keys: Optional[torch.Tensor]  # (D, Kw)
+
+
+def counter_lub_many(clock: torch.Tensor, ec: torch.Tensor, val: torch.Tensor, def_off=None,
+                     def_row: Optional[torch.Tensor] = None, def_clock: Optional[torch.Tensor] = None,
+                     def_keys: Optional[torch.Tensor] = None, ctx: Optional[Context] = None,
+                     check: bool = True) -> MapCounterLub:
+    """The exact left fold of Map::merge (map.rs:140-220) for Map<K, GCounter> (val (G,R,K,1,A)) or
+    Map<K, PNCounter> (val (G,R,K,2,A): P then N) — gcounter.rs:44-54 / pncounter.rs:70-82 as the
+    value's merge and forget.  clock (G,R,A) / (R,A), ec (G,R,K,A) / (R,K,A), val likewise; the
+    deferred pool as for lub_many (host def_off).  check=True raises on flags (bit 1: def_row not
+    sorted / out of range, bit 3: more than 512 live removes named one key)."""
+    ctx = ctx or Context.default(clock.device.index)
+    for t, nm in ((clock, "clock"), (ec, "ec"), (val, "val")):
+        ctx.check_tensor(t, f"map.counter_lub_many({nm})")
+    squeeze = clock.dim() == 2
+    c = clock.unsqueeze(0) if squeeze else clock
+    e = ec.unsqueeze(0) if squeeze else ec
+    v = val.unsqueeze(0) if squeeze else val
+    if c.dim() != 3 or e.dim() != 4 or v.dim() != 5:
+        raise ValueError("map.counter_lub_many: clock (G,R,A), ec (G,R,K,A), val (G,R,K,W,A) expected")
+    G, R, A = c.shape
+    K, W = e.shape[2], v.shape[3]
+    if tuple(e.shape) != (G, R, K, A) or tuple(v.shape) != (G, R, K, W, A) or W not in (1, 2):
+        raise ValueError(f"map.counter_lub_many: shapes clock {tuple(c.shape)} ec {tuple(e.shape)} "
+                         f"val {tuple(v.shape)} do not agree (W = 1 GCounter, 2 PNCounter)")
+    for t, nm, inner in ((c, "clock", (1,)), (e, "ec", (A, 1)), (v, "val", (W * A, A, 1))):
+        if t.numel() and tuple(t.stride()[2:]) != inner:
+            raise ValueError(f"map.counter_lub_many: {nm} must be packed within a replica")
+    Kw = (K + 63) // 64
+    dev = clock.device
+    out_clock = torch.empty((G, A), dtype=torch.int64, device=dev)
+    out_ec = torch.empty((G, K, A), dtype=torch.int64, device=dev)
+    out_val = torch.empty((G, K, W, A), dtype=torch.int64, device=dev)
+    flags = torch.empty(G, dtype=torch.int32, device=dev)
+    b = _abi.MapCounterBatch()
+    b.G, b.R, b.K, b.A, b.W = G, R, K, A, W
+    b.clock, b.clock_rstride, b.clock_gstride = c.data_ptr(), c.stride(1), c.stride(0)
+    b.ec, b.ec_rstride, b.ec_gstride = e.data_ptr(), e.stride(1), e.stride(0)
+    b.val, b.val_rstride, b.val_gstride = v.data_ptr(), v.stride(1), v.stride(0)
+    o = _abi.MapCounterOut()
+    o.clock, o.ec, o.val, o.flags = out_clock.data_ptr(), out_ec.data_ptr(), out_val.data_ptr(), flags.data_ptr()
+    keep = keys_out = None
+    off_arr = None
+    if def_off is not None:
+        off = np.asarray(def_off, dtype=np.uint64)
+        if off.shape != (G + 1,):
+            raise ValueError(f"map.counter_lub_many: def_off must have G+1 = {G + 1} entries")
+        D = int(off[-1])
+        if D > 0:
+            for t, nm, shape in ((def_clock, "def_clock", (D, A)), (def_keys, "def_keys", (D, Kw)),
+                                 (def_row, "def_row", (D,))):
+                if t is None or not t.is_contiguous() or tuple(t.shape) != shape:
+                    raise ValueError(f"map.counter_lub_many: {nm} must be a contiguous {shape} tensor")
+                ctx.check_tensor(t, f"map.counter_lub_many({nm})")
+            if def_row.dtype not in (torch.int32, torch.uint32):
+                raise ValueError("map.counter_lub_many: def_row must be int32")
+            off_arr = (ctypes.c_size_t * (G + 1))(*[int(x) for x in off])
+            b.def_off = ctypes.cast(off_arr, ctypes.POINTER(ctypes.c_size_t))
+            b.def_row, b.def_clock, b.def_keys = def_row.data_ptr(), def_clock.data_ptr(), def_keys.data_ptr()
+            keep = torch.empty(D, dtype=torch.uint8, device=dev)
+            keys_out = torch.empty((D, Kw), dtype=torch.int64, device=dev)
+            o.def_keep, o.def_keys = keep.data_ptr(), keys_out.data_ptr()
+    ctx.call("crdt_map_counter_lub_many", ctypes.byref(b), ctypes.byref(o))
+    if check:
+        f = 0
+        for x in flags.cpu().numpy().tolist():
+            f |= int(x)
+        if f & 2:
+            raise ValueError("map.counter_lub_many: def_row not non-decreasing per group or >= R")
+        if f & 8:
+            raise RuntimeError("map.counter_lub_many: more than 512 live removes named one key")
+    if squeeze:
+        out_clock, out_ec, out_val, flags = out_clock[0], out_ec[0], out_val[0], flags
+    return MapCounterLub(out_clock, out_ec, out_val, flags, keep, keys_out)

@@ -59,6 +59,8 @@ def test_ctypes_struct_layout_matches_header():
     # 5 dims + 4 x (ptr + 2 strides) + def_off + 3 ptrs = 21; out: Vout, Vstate + 8 ptrs = 10
     assert ctypes.sizeof(abi.MapBatch) == 21 * 8
     assert ctypes.sizeof(abi.MapOut) == 10 * 8
+    assert ctypes.sizeof(abi.MapCounterBatch) == 18 * 8
+    assert ctypes.sizeof(abi.MapCounterOut) == 6 * 8
 
 
 HOST_CAPABLE = {f"crdt_{t}_{op}" for t in ("vclock", "gcounter", "pncounter", "gset", "lwwreg", "orswot", "map")
