@@ -582,7 +582,7 @@ int crdt_map_lub_many_sharded_doff(crdt_ctx *ctx, const crdt_map_batch *in, cons
  * Output per group g (packed): clock[g*A + a], ec[(g*K + k)*A + a], val[((g*K + k)*W + w)*A + a],
  * flags[g] (required): bit 1 = def_row not non-decreasing or >= R, bit 3 = more than 512 live
  * removes named one key (results of the group unreliable); def_keep / def_keys as crdt_map_out.
- * Limits: A <= 256.  Device-memory contexts only. */
+ * Limits: A <= 512.  Device-memory contexts only. */
 typedef struct crdt_map_counter_batch {
   size_t G, R, K, A, W;
   const uint64_t *clock;

@@ -474,9 +474,10 @@ def counter_lub_many(clock: torch.Tensor, ec: torch.Tensor, val: torch.Tensor, d
                                  (def_row, "def_row", (D,))):
                 if t is None or not t.is_contiguous() or tuple(t.shape) != shape:
                     raise ValueError(f"map.counter_lub_many: {nm} must be a contiguous {shape} tensor")
-                ctx.check_tensor(t, f"map.counter_lub_many({nm})")
-            if def_row.dtype not in (torch.int32, torch.uint32):
-                raise ValueError("map.counter_lub_many: def_row must be int32")
+                if nm != "def_row":
+                    ctx.check_tensor(t, f"map.counter_lub_many({nm})")
+            if def_row.dtype not in (torch.int32, torch.uint32) or def_row.device != dev:
+                raise ValueError(f"map.counter_lub_many: def_row must be an int32 tensor on {dev}")
             off_arr = (ctypes.c_size_t * (G + 1))(*[int(x) for x in off])
             b.def_off = ctypes.cast(off_arr, ctypes.POINTER(ctypes.c_size_t))
             b.def_row, b.def_clock, b.def_keys = def_row.data_ptr(), def_clock.data_ptr(), def_keys.data_ptr()
