@@ -65,11 +65,15 @@ __global__ __launch_bounds__(kMcWaves * kWave) void map_counter_fold_kernel(MapC
   uint32_t *live = reinterpret_cast<uint32_t *>(lst + kMcList);
   u64 *rows = lst + kMcList + kMcLive / 2;  // [NROW][APL][64]
 
+  // Loads are never EXEC-masked: lanes past A read the row's last word and zero it after (a masked
+  // load puts the wait counter's bookkeeping on branches, and the compiler then drains every
+  // outstanding load — the replica ring's prefetch included — at the join).
   auto ld_row = [&](u64 (&x)[APL], const u64 *src) {
 #pragma unroll
     for (int j = 0; j < APL; ++j) {
       const unsigned long long a = (unsigned long long)lane + (unsigned long long)kWave * j;
-      x[j] = a < A ? src[a] : 0ull;
+      const u64 t = src[a < A ? a : A - 1];
+      x[j] = a < A ? t : 0ull;
     }
   };
 
@@ -150,16 +154,38 @@ __global__ __launch_bounds__(kMcWaves * kWave) void map_counter_fold_kernel(MapC
 
   // ---- replica rows, DEPTH steps ahead
   u64 c2r[DEPTH][APL], e2r[DEPTH][APL], v2r[DEPTH][W][APL];
-  auto load_step = [&](unsigned long long r, int s) {
-    if (r < R) {
-      ld_row(c2r[s], p.clock + g * p.c_gs + r * p.c_rs);
-      ld_row(e2r[s], p.ec + g * p.e_gs + r * p.e_rs + k * A);
+  // the lane's word of each row, advanced by one replica stride per step (no per-step multiplies);
+  // past the last replica the pointers stay on it (loaded, never used)
+  const u64 *pc = p.clock + g * p.c_gs, *pe = p.ec + g * p.e_gs + k * A, *pv = p.val + g * p.v_gs + k * W * A;
+  unsigned long long nload = 0;  // replica of the next load_step
+  unsigned aj[APL];              // the lane's actor per word, clamped to the row (see ld_row)
+  bool inj[APL];
 #pragma unroll
-      for (int w = 0; w < W; ++w) ld_row(v2r[s][w], p.val + g * p.v_gs + r * p.v_rs + (k * W + w) * A);
+  for (int j = 0; j < APL; ++j) {
+    const unsigned long long a = (unsigned long long)lane + (unsigned long long)kWave * j;
+    inj[j] = a < A;
+    aj[j] = (unsigned)(a < A ? a : A - 1);
+  }
+  auto load_step = [&](int s) {
+#pragma unroll
+    for (int j = 0; j < APL; ++j) {
+      const u64 tc = pc[aj[j]], te = pe[aj[j]];
+      c2r[s][j] = inj[j] ? tc : 0ull;
+      e2r[s][j] = inj[j] ? te : 0ull;
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        const u64 tv = pv[w * A + aj[j]];
+        v2r[s][w][j] = inj[j] ? tv : 0ull;
+      }
+    }
+    if (++nload < R) {
+      pc += p.c_rs;
+      pe += p.e_rs;
+      pv += p.v_rs;
     }
   };
 #pragma unroll
-  for (int s = 0; s < DEPTH; ++s) load_step((unsigned long long)s, s);
+  for (int s = 0; s < DEPTH; ++s) load_step(s);
 
   for (unsigned long long r0 = 0; r0 < R; r0 += DEPTH) {
 #pragma unroll
@@ -297,7 +323,7 @@ __global__ __launch_bounds__(kMcWaves * kWave) void map_counter_fold_kernel(MapC
           }
         }
       }
-      load_step(r + DEPTH, s);
+      load_step(s);
     }
   }
   // ---- the key's folded entry, the group's clock (key 0's wave)
