@@ -36,34 +36,66 @@ struct MapCounterPlan {
   unsigned *o_flags;
 };
 
+__device__ __forceinline__ void glds16_mc(const void *g, u64 *lds) {
+  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void *)lds, 16, 0, 0);
+}
+
+// votes over the lanes of the caller's key (hm: its lanes' bits; ~0 with one key per wave)
 template <int APL>
-__device__ __forceinline__ bool mc_any(const u64 (&x)[APL], const u64 (&y)[APL]) {  // some x[a] > y[a]
+__device__ __forceinline__ bool mc_any(const u64 (&x)[APL], const u64 (&y)[APL], u64 hm) {  // some x[a] > y[a]
   bool b = false;
 #pragma unroll
   for (int j = 0; j < APL; ++j) b |= x[j] > y[j];
-  return __ballot(b) != 0;
+  return (__ballot(b) & hm) != 0;
 }
 template <int APL>
-__device__ __forceinline__ bool mc_nz(const u64 (&x)[APL]) {
+__device__ __forceinline__ bool mc_nz(const u64 (&x)[APL], u64 hm) {
   bool b = false;
 #pragma unroll
   for (int j = 0; j < APL; ++j) b |= x[j] != 0;
-  return __ballot(b) != 0;
+  return (__ballot(b) & hm) != 0;
 }
 
-template <int APL, int W>
+// DMA (APL = 1, (2+W)*A <= 128 words, A even, 16-byte aligned rows): the replica rows of a step
+// arrive as ONE 1-KiB LDS-DMA piece (lane l moves words 2l, 2l+1 of the step image [ec | val rows |
+// clock]) into a ring of RING slots (8 or 16), waited on with an explicit vmcnt; otherwise
+// (RING = 0) a register ring.  (The register ring's loads are register values, and the compiler
+// drains them all at the loop's back edge — one memory latency every DEPTH steps; LDS-DMA loads
+// it leaves to us.)
+// KPW keys per wave (APL = 1, register ring, A <= 64 / KPW): lanes [h*64/KPW, (h+1)*64/KPW) fold
+// key kb + h of the group, so a 32-actor key no longer leaves half the wave idle.  The group's
+// clock C and a remove's liveness (!(rm <= C)) are the same for every key of the group, so the
+// keys share one walk of the remove pool; each entry carries which of the wave's keys it names.
+template <int APL, int W, int RING, int KPW, int DEP = 8>
 __global__ __launch_bounds__(kMcWaves * kWave) void map_counter_fold_kernel(MapCounterPlan p) {
-  constexpr int DEPTH = APL >= 8 ? 1 : 8 / APL;    // replica steps in flight (16 at APL 1 ran slower:
-                                                   // 20.0 vs 12.9 ms, probably the unrolled body's size)
+  constexpr bool DMA = RING > 0;
+  constexpr int kMcRing = DMA ? RING : 1;
+  constexpr int DEPTH = DMA ? 1 : (APL >= 8 ? 1 : DEP / APL);  // register ring: steps in flight (16 at
+                                                   // APL 1 ran slower: 20.0 vs 12.9 ms, probably the
+                                                   // unrolled body's size)
+  static_assert(KPW == 1 || (APL == 1 && !DMA), "several keys per wave: APL 1, register ring");
   constexpr int NROW = kMcRowsB / (8 * kWave * APL);  // live rm rows cached in LDS
+  constexpr int HL = kWave / KPW;                     // lanes per key
   extern __shared__ u64 lds[];
   const int lane = (int)(threadIdx.x % kWave), wv = (int)(threadIdx.x / kWave);
-  const unsigned long long gk = (unsigned long long)blockIdx.x * kMcWaves + wv;
-  if (gk >= p.G * p.K) return;  // (whole waves; nothing below synchronises the workgroup)
-  const unsigned long long g = gk / p.K, k = gk % p.K, A = p.A, R = p.R;
-  u64 *lst = lds + (unsigned long long)wv * (kMcList + kMcLive / 2 + NROW * kWave * APL);
+  const int h = lane / HL, al = lane % HL;  // the lane's key of the wave / actor lane
+  const u64 hm = KPW == 1 ? ~0ull : (((1ull << HL) - 1) << (h * HL));
+  const unsigned long long KW = (p.K + KPW - 1) / KPW;  // waves per group
+  const unsigned long long wk = (unsigned long long)blockIdx.x * kMcWaves + wv;
+  if (wk >= p.G * KW) return;  // (whole waves; nothing below synchronises the workgroup)
+  const unsigned long long g = wk / KW, kb = (wk % KW) * KPW, A = p.A, R = p.R;
+  const unsigned long long k = kb + h;  // the lane's key (past K: a copy of key K-1, not written)
+  const bool kval = k < p.K;
+  const unsigned long long kc = kval ? k : p.K - 1;
+  const unsigned kbits = (unsigned)(p.K - kb < (unsigned long long)KPW ? (1u << (p.K - kb)) - 1 : (1u << KPW) - 1);
+  constexpr unsigned long long WQ = kMcList + kMcLive / 2 + NROW * kWave * APL + (DMA ? kMcRing * 128 : 0);
+  u64 *lst = lds + (unsigned long long)wv * WQ;
   uint32_t *live = reinterpret_cast<uint32_t *>(lst + kMcList);
   u64 *rows = lst + kMcList + kMcLive / 2;  // [NROW][APL][64]
+  u64 *ring = rows + NROW * kWave * APL;    // DMA: [kMcRing][128] step images
+  // which of the wave's keys each gathered / live remove names (bit h)
+  uint8_t *lmask = reinterpret_cast<uint8_t *>(lds + kMcWaves * WQ) + wv * (kMcList + kMcLive);
+  uint8_t *lvm = lmask + kMcList;
 
   // Loads are never EXEC-masked: lanes past A read the row's last word and zero it after (a masked
   // load puts the wait counter's bookkeeping on branches, and the compiler then drains every
@@ -71,13 +103,13 @@ __global__ __launch_bounds__(kMcWaves * kWave) void map_counter_fold_kernel(MapC
   auto ld_row = [&](u64 (&x)[APL], const u64 *src) {
 #pragma unroll
     for (int j = 0; j < APL; ++j) {
-      const unsigned long long a = (unsigned long long)lane + (unsigned long long)kWave * j;
+      const unsigned long long a = (unsigned long long)al + (unsigned long long)HL * j;
       const u64 t = src[a < A ? a : A - 1];
       x[j] = a < A ? t : 0ull;
     }
   };
 
-  // ---- the removes naming key k, in replica order (windows of kMcList)
+  // ---- the removes naming the wave's keys, in replica order (windows of kMcList)
   const unsigned long long d0 = p.def_off ? p.def_off[g] : 0, d1 = p.def_off ? p.def_off[g + 1] : 0;
   unsigned long long dc = d0;  // next pool entry to scan
   int nl = 0, li = 0;          // window length / next entry
@@ -88,32 +120,39 @@ __global__ __launch_bounds__(kMcWaves * kWave) void map_counter_fold_kernel(MapC
     li = 0;
     while (dc < d1 && nl + kWave <= kMcList) {
       const unsigned long long d = dc + lane;
-      bool hit = false;
+      unsigned bits = 0;  // (the wave's keys share one def_keys word: KPW divides 64)
       u64 row = 0;
       if (d < d1) {
         row = p.def_row[d];
-        hit = (p.def_keys[d * p.Kw + k / 64] >> (k % 64)) & 1ull;
+        bits = (unsigned)(p.def_keys[d * p.Kw + kb / 64] >> (kb % 64)) & kbits;
       }
+      const bool hit = bits != 0;
       const u64 prev = __shfl_up(row, 1);
       bool b = d < d1 && (row >= R || (lane == 0 ? row < last_row : row < prev));
       if (__ballot(b)) bad = true;
       const unsigned long long n = d1 - dc < (unsigned long long)kWave ? d1 - dc : kWave;
       last_row = __shfl(row, (int)n - 1);
       const u64 m = __ballot(hit);
-      if (hit) lst[nl + __popcll(m & ((1ull << lane) - 1))] = (row << 32) | (u64)(d - d0);
+      if (hit) {
+        const int at = nl + __popcll(m & ((1ull << lane) - 1));
+        lst[at] = (row << 32) | (u64)(d - d0);
+        lmask[at] = (uint8_t)bits;
+      }
       nl += __popcll(m);
       dc += n;
     }
   };
-  u64 nxt = ~0ull;  // replica row of lst[li], the next remove naming k (~0: none left)
+  unsigned nxt = ~0u;  // replica row of lst[li], the next remove naming one of the keys (~0: none
+                       // left; rows < R <= 0xfffffffe)
   auto advance = [&]() {
     for (;;) {
-      if (li < nl) {
-        nxt = lst[li] >> 32;
+      if (li < nl) {  // (uniform: a scalar, so the per-step test is a scalar compare)
+        const u64 x = lst[li] >> 32;
+        nxt = (unsigned)__builtin_amdgcn_readfirstlane((unsigned)x);
         return;
       }
       if (dc >= d1) {
-        nxt = ~0ull;
+        nxt = ~0u;
         return;
       }
       refill();
@@ -128,7 +167,7 @@ __global__ __launch_bounds__(kMcWaves * kWave) void map_counter_fold_kernel(MapC
   auto live_row = [&](int i, u64 (&x)[APL]) {
     if (i < NROW) {
 #pragma unroll
-      for (int j = 0; j < APL; ++j) x[j] = rows[((unsigned long long)i * APL + j) * kWave + lane];
+      for (int j = 0; j < APL; ++j) x[j] = rows[((unsigned long long)i * APL + j) * kWave + lane];  // (KPW > 1: each key's lanes hold a copy)
     } else {
       ld_row(x, p.def_clock + (d0 + live[i]) * A);
     }
@@ -140,8 +179,12 @@ __global__ __launch_bounds__(kMcWaves * kWave) void map_counter_fold_kernel(MapC
     }
   };
   u64 rk[APL];  // max of the live removes' clocks (the forget every later step applies)
+  u64 T[APL];   // witness thresholds (see step 3)
 #pragma unroll
-  for (int j = 0; j < APL; ++j) rk[j] = 0;
+  for (int j = 0; j < APL; ++j) {
+    rk[j] = 0;
+    T[j] = ~0ull;
+  }
 
   u64 C[APL], e[APL], v[W][APL];
 #pragma unroll
@@ -152,152 +195,111 @@ __global__ __launch_bounds__(kMcWaves * kWave) void map_counter_fold_kernel(MapC
     for (int w = 0; w < W; ++w) v[w][j] = 0;
   }
 
-  // ---- replica rows, DEPTH steps ahead
-  u64 c2r[DEPTH][APL], e2r[DEPTH][APL], v2r[DEPTH][W][APL];
-  // the lane's word of each row, advanced by one replica stride per step (no per-step multiplies);
-  // past the last replica the pointers stay on it (loaded, never used)
-  const u64 *pc = p.clock + g * p.c_gs, *pe = p.ec + g * p.e_gs + k * A, *pv = p.val + g * p.v_gs + k * W * A;
-  unsigned long long nload = 0;  // replica of the next load_step
-  unsigned aj[APL];              // the lane's actor per word, clamped to the row (see ld_row)
-  bool inj[APL];
+  // ---- replica rows
+  unsigned aj[APL];  // the lane's actor per word, clamped to the row (see ld_row)
 #pragma unroll
   for (int j = 0; j < APL; ++j) {
-    const unsigned long long a = (unsigned long long)lane + (unsigned long long)kWave * j;
-    inj[j] = a < A;
+    const unsigned long long a = (unsigned long long)al + (unsigned long long)HL * j;
     aj[j] = (unsigned)(a < A ? a : A - 1);
   }
-  auto load_step = [&](int s) {
+  // one replica step on the key's state.  Lanes past A hold copies of actor A-1 (clamped loads;
+  // every operation is lane-local), so they never change a vote and need no masking.
+  //
+  // The entry join is branch-free.  With forget(x, c)[a] = x[a] > c[a] ? x[a] : 0, the joined
+  // entry clock is, in all four presence cases (map.rs:146-161, :170-192, :193-208, absent both),
+  //     e' = max(e == e2 ? e : 0, forget(e2, C), forget(e, c2))
+  // (the "common" clock of :174-178 — it reduces to forget(e, c2) when the replica has no entry,
+  // to forget(e2, C) when we have none, and is empty exactly when the reference drops the key),
+  // and the value is forget(max(v, v2), forget(Y, e')) with Y = c2 (removed_information, :151),
+  // C (we_deleted, :200) or max(e, e2) (deleted, :185) by case.  An entry whose clock is empty
+  // keeps a stale value row, ignored (read as 0) from then on: the next step masks v by the same
+  // presence vote it needs anyway, and the final rows are masked once.  Two votes per step, both
+  // on the step's inputs.
+  auto step = [&](unsigned long long r, const u64 (&c2)[APL], const u64 (&e2)[APL], const u64 (&v2)[W][APL]) {
+    // 1. entry join (map.rs:142-210) against the state before this step (clock C)
+    const bool p1 = mc_nz<APL>(e, hm), p2 = mc_nz<APL>(e2, hm);
 #pragma unroll
     for (int j = 0; j < APL; ++j) {
-      const u64 tc = pc[aj[j]], te = pe[aj[j]];
-      c2r[s][j] = inj[j] ? tc : 0ull;
-      e2r[s][j] = inj[j] ? te : 0ull;
+      const u64 t0 = e[j] == e2[j] ? e[j] : 0, t1 = e2[j] > C[j] ? e2[j] : 0, t2 = e[j] > c2[j] ? e[j] : 0;
+      const u64 t = t0 > t1 ? t0 : t1;
+      const u64 en = t > t2 ? t : t2;
+      const u64 mx = e[j] > e2[j] ? e[j] : e2[j];
+      const u64 y = p1 ? (p2 ? mx : c2[j]) : C[j];
+      const u64 x = y > en ? y : 0;
 #pragma unroll
       for (int w = 0; w < W; ++w) {
-        const u64 tv = pv[w * A + aj[j]];
-        v2r[s][w][j] = inj[j] ? tv : 0ull;
+        const u64 a1 = p1 ? v[w][j] : 0, a2 = p2 ? v2[w][j] : 0;
+        const u64 m = a1 > a2 ? a1 : a2;  // val.merge
+        v[w][j] = m > x ? m : 0;          // val.forget
       }
+      e[j] = en;
     }
-    if (++nload < R) {
-      pc += p.c_rs;
-      pe += p.e_rs;
-      pv += p.v_rs;
-    }
-  };
+    // 2. this step's forget: replica r's removes naming k (apply_keyset_rm, unconditional) and the
+    //    removes still deferred after step r-1 (apply_deferred, rk: 0 when there are none, so the
+    //    common step applies it without a branch)
+    bool chg = false;  // removes joined the live set this step
+    u64 f[APL];
 #pragma unroll
-  for (int s = 0; s < DEPTH; ++s) load_step(s);
-
-  for (unsigned long long r0 = 0; r0 < R; r0 += DEPTH) {
-#pragma unroll
-    for (int s = 0; s < DEPTH; ++s) {
-      const unsigned long long r = r0 + s;
-      if (r >= R) break;
-      const u64(&c2)[APL] = c2r[s];
-      const u64(&e2)[APL] = e2r[s];
-      // 1. entry join (map.rs:142-210) against the state before this step (clock C)
-      const bool p1 = mc_nz<APL>(e), p2 = mc_nz<APL>(e2);
-      if (p1 && !p2) {  // :146-161
-        if (!mc_any<APL>(e, c2)) {  // other.clock >= entry.clock: dropped
-#pragma unroll
-          for (int j = 0; j < APL; ++j) {
-            e[j] = 0;
-#pragma unroll
-            for (int w = 0; w < W; ++w) v[w][j] = 0;
-          }
-        } else {
-#pragma unroll
-          for (int j = 0; j < APL; ++j) {
-            e[j] = e[j] > c2[j] ? e[j] : 0;                 // entry.clock.forget(other.clock)
-            const u64 ri = c2[j] > e[j] ? c2[j] : 0;        // removed_information
-#pragma unroll
-            for (int w = 0; w < W; ++w) v[w][j] = v[w][j] > ri ? v[w][j] : 0;
-          }
-        }
-      } else if (!p1 && p2) {  // :193-208
-        if (mc_any<APL>(e2, C)) {  // else self.clock >= entry.clock: not added
-#pragma unroll
-          for (int j = 0; j < APL; ++j) {
-            e[j] = e2[j] > C[j] ? e2[j] : 0;                // entry.clock.forget(self.clock)
-            const u64 wd = C[j] > e[j] ? C[j] : 0;          // we_deleted
-#pragma unroll
-            for (int w = 0; w < W; ++w) v[w][j] = v2r[s][w][j] > wd ? v2r[s][w][j] : 0;
-          }
-        }
-      } else if (p1 && p2) {  // :170-192
-        u64 cm[APL];
-        bool nz = false;
-#pragma unroll
-        for (int j = 0; j < APL; ++j) {
-          const u64 t0 = e[j] == e2[j] ? e[j] : 0, t1 = e2[j] > C[j] ? e2[j] : 0, t2 = e[j] > c2[j] ? e[j] : 0;
-          const u64 t = t0 > t1 ? t0 : t1;
-          cm[j] = t > t2 ? t : t2;
-          nz |= cm[j] != 0;
-        }
-        if (!__ballot(nz)) {  // common empty: the key is dropped
-#pragma unroll
-          for (int j = 0; j < APL; ++j) {
-            e[j] = 0;
-#pragma unroll
-            for (int w = 0; w < W; ++w) v[w][j] = 0;
-          }
-        } else {
-#pragma unroll
-          for (int j = 0; j < APL; ++j) {
-            const u64 mx = e[j] > e2[j] ? e[j] : e2[j];
-            const u64 del = mx > cm[j] ? mx : 0;            // (e1 + e2).forget(common)
-#pragma unroll
-            for (int w = 0; w < W; ++w) {
-              const u64 m = v[w][j] > v2r[s][w][j] ? v[w][j] : v2r[s][w][j];  // val.merge
-              v[w][j] = m > del ? m : 0;                                      // val.forget(deleted)
-            }
-            e[j] = cm[j];
-          }
-        }
-      }
-      // 2. this step's forget: replica r's removes naming k (apply_keyset_rm, unconditional) and the
-      //    removes still deferred after step r-1 (apply_deferred)
-      u64 f[APL];
-#pragma unroll
-      for (int j = 0; j < APL; ++j) f[j] = rk[j];
-      int nnew = 0;
-      while (nxt <= r) {  // (a row below r only when def_row is unsorted: flagged)
+    for (int j = 0; j < APL; ++j) f[j] = rk[j];
+    const unsigned r32 = (unsigned)r;
+    if (nxt <= r32) {  // (a row below r only when def_row is unsorted: flagged)
+      do {
         const unsigned idx = (unsigned)lst[li];
+        const unsigned bits = lmask[li];
+        const bool named = (bits >> h) & 1u;
         u64 rm[APL];
         ld_row(rm, p.def_clock + (d0 + idx) * A);
 #pragma unroll
-        for (int j = 0; j < APL; ++j) f[j] = f[j] > rm[j] ? f[j] : rm[j];
+        for (int j = 0; j < APL; ++j) f[j] = named && rm[j] > f[j] ? rm[j] : f[j];
         if (na < kMcLive) {  // a candidate for the live set (checked against C below)
-          if (lane == 0) live[na] = idx;
+          if (lane == 0) {
+            live[na] = idx;
+            lvm[na] = (uint8_t)bits;
+          }
           put_row(na, rm);
           ++na;
-          ++nnew;
+          chg = true;
         } else {
           full = true;  // (more than kMcLive live removes on one key: reported, never silent)
         }
         ++li;
         advance();
-      }
+      } while (nxt <= r32);
+    }
 #pragma unroll
-      for (int j = 0; j < APL; ++j) {
-        e[j] = e[j] > f[j] ? e[j] : 0;
+    for (int j = 0; j < APL; ++j) {
+      e[j] = e[j] > f[j] ? e[j] : 0;
 #pragma unroll
-        for (int w = 0; w < W; ++w) v[w][j] = v[w][j] > f[j] ? v[w][j] : 0;
-      }
-      if (!mc_nz<APL>(e)) {  // an entry whose clock emptied is dropped with its value
+      for (int w = 0; w < W; ++w) v[w][j] = v[w][j] > f[j] ? v[w][j] : 0;
+    }
+    // 3. self.clock.merge(other.clock) (:217), then a remove stays deferred while !(rm <= C)
 #pragma unroll
-        for (int j = 0; j < APL; ++j)
+    for (int j = 0; j < APL; ++j) C[j] = C[j] > c2[j] ? C[j] : c2[j];
+    //    Each live remove keeps a witness: an actor whose rm word is still above C.  T holds, per
+    //    lane word, the least rm word among the removes witnessed there; while no C word reached its
+    //    T, no live remove can have become dominated (C only grows), and the scan is skipped.
+    {
+      bool b = false;  // (no live removes: every T word is ~0, no vote)
 #pragma unroll
-          for (int w = 0; w < W; ++w) v[w][j] = 0;
-      }
-      // 3. self.clock.merge(other.clock) (:217), then a remove stays deferred while !(rm <= C)
+      for (int j = 0; j < APL; ++j) b |= C[j] >= T[j];
+      if (chg || __ballot(b) != 0) {
+        bool changed = chg;
 #pragma unroll
-      for (int j = 0; j < APL; ++j) C[j] = C[j] > c2[j] ? C[j] : c2[j];
-      if (na > 0) {
-        bool changed = nnew > 0;
+        for (int j = 0; j < APL; ++j) T[j] = ~0ull;
         for (int i = 0; i < na;) {
           u64 rm[APL];
           live_row(i, rm);
-          if (mc_any<APL>(rm, C)) {
+          bool wit = false;  // (every key's lanes hold rm and C: one vote)
+#pragma unroll
+          for (int j = 0; j < APL; ++j) {
+            const u64 m = __ballot(rm[j] > C[j]);
+            if (m && !wit) {
+              wit = true;
+              const int wl = __builtin_ctzll(m);
+              T[j] = lane == wl && rm[j] < T[j] ? rm[j] : T[j];
+            }
+          }
+          if (wit) {
             ++i;
             continue;
           }
@@ -308,7 +310,11 @@ __global__ __launch_bounds__(kMcWaves * kWave) void map_counter_fold_kernel(MapC
             live_row(lastp, x);
             put_row(i, x);
             const unsigned li_last = live[lastp];
-            if (lane == 0) live[i] = li_last;
+            const uint8_t lm_last = lvm[lastp];
+            if (lane == 0) {
+              live[i] = li_last;
+              lvm[i] = lm_last;
+            }
           }
           --na;
         }
@@ -318,40 +324,120 @@ __global__ __launch_bounds__(kMcWaves * kWave) void map_counter_fold_kernel(MapC
           for (int i = 0; i < na; ++i) {
             u64 rm[APL];
             live_row(i, rm);
+            const bool named = (lvm[i] >> h) & 1u;
 #pragma unroll
-            for (int j = 0; j < APL; ++j) rk[j] = rk[j] > rm[j] ? rk[j] : rm[j];
+            for (int j = 0; j < APL; ++j) rk[j] = named && rm[j] > rk[j] ? rm[j] : rk[j];
           }
         }
       }
-      load_step(s);
+    }
+  };
+  if constexpr (DMA) {
+    // lane l's 16-byte piece of the step image and its source row (advanced by the row stride)
+    const unsigned long long o = 2ull * lane, I = (2 + W) * A;
+    const bool on = o < I;
+    const u64 *src0 = o < A ? p.ec + g * p.e_gs + k * A + o
+                            : (o < (1 + W) * A ? p.val + g * p.v_gs + k * W * A + (o - A)
+                                               : p.clock + g * p.c_gs + (o < I ? o - (1 + W) * A : 0));
+    const unsigned long long st = o < A ? p.e_rs : (o < (1 + W) * A ? p.v_rs : p.c_rs);
+    auto issue = [&](unsigned long long r) {  // step r's image into its slot (past R: row R-1 again)
+      const unsigned long long rr = r < R ? r : R - 1;
+      if (on) glds16_mc(src0 + rr * st, ring + (r % kMcRing) * 128);
+    };
+    for (int s = 0; s < kMcRing; ++s) issue((unsigned long long)s);
+    for (unsigned long long r = 0; r < R; ++r) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kMcRing - 1) : "memory");  // step r's piece has landed
+      const u64 *img = ring + (r % kMcRing) * 128;
+      u64 c2[APL], e2[APL], v2[W][APL];
+      const unsigned a0 = aj[0];
+      e2[0] = img[a0];
+      c2[0] = img[(1 + W) * A + a0];
+#pragma unroll
+      for (int w = 0; w < W; ++w) v2[w][0] = img[(1 + w) * A + a0];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot is read: refill it
+      issue(r + kMcRing);
+      step(r, c2, e2, v2);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (no piece lands after the wave ends)
+  } else {
+    u64 c2r[DEPTH][APL], e2r[DEPTH][APL], v2r[DEPTH][W][APL];
+    // the lane's word of each row, advanced by one replica stride per step (no per-step
+    // multiplies); past the last replica the pointers stay on it (loaded, never used)
+    const u64 *pc = p.clock + g * p.c_gs, *pe = p.ec + g * p.e_gs + kc * A, *pv = p.val + g * p.v_gs + kc * W * A;
+    unsigned long long nload = 0;  // replica of the next load_step
+    // (the ring holds the raw words; lanes past A are zeroed when the step uses them, DEPTH steps
+    // later — a select right behind the load would make the wave wait for it at once)
+    auto load_step = [&](int s, bool last_check) {
+#pragma unroll
+      for (int j = 0; j < APL; ++j) {
+        c2r[s][j] = pc[aj[j]];
+        e2r[s][j] = pe[aj[j]];
+#pragma unroll
+        for (int w = 0; w < W; ++w) v2r[s][w][j] = pv[w * A + aj[j]];
+      }
+      if (!last_check || nload + 1 < R) {
+        pc += p.c_rs;
+        pe += p.e_rs;
+        pv += p.v_rs;
+      }
+      ++nload;
+    };
+#pragma unroll
+    for (int s = 0; s < DEPTH; ++s) load_step(s, true);
+    unsigned long long r0 = 0;
+    // blocks whose loads (rows r0 + DEPTH .. r0 + 2 DEPTH - 1) all have a next row: no clamp
+    for (; r0 + 2 * DEPTH < R; r0 += DEPTH) {
+#pragma unroll
+      for (int s = 0; s < DEPTH; ++s) {
+        step(r0 + s, c2r[s], e2r[s], v2r[s]);
+        load_step(s, false);
+      }
+    }
+    for (; r0 < R; r0 += DEPTH) {
+#pragma unroll
+      for (int s = 0; s < DEPTH; ++s) {
+        const unsigned long long r = r0 + s;
+        if (r >= R) break;
+        step(r, c2r[s], e2r[s], v2r[s]);
+        load_step(s, true);
+      }
     }
   }
-  // ---- the key's folded entry, the group's clock (key 0's wave)
-  u64 *oe = p.o_ec + gk * A;
-  u64 *ov = p.o_val + gk * W * A;
+  // ---- the key's folded entry (a stale value behind an empty clock reads 0), the group's clock
+  //      (key 0's lanes)
+  const bool pf = mc_nz<APL>(e, hm);
+  u64 *oe = p.o_ec + (g * p.K + kc) * A;
+  u64 *ov = p.o_val + (g * p.K + kc) * W * A;
 #pragma unroll
   for (int j = 0; j < APL; ++j) {
-    const unsigned long long a = (unsigned long long)lane + (unsigned long long)kWave * j;
-    if (a < A) {
+    const unsigned long long a = (unsigned long long)al + (unsigned long long)HL * j;
+    if (kval && a < A) {
       oe[a] = e[j];
 #pragma unroll
-      for (int w = 0; w < W; ++w) ov[w * A + a] = v[w][j];
+      for (int w = 0; w < W; ++w) ov[w * A + a] = pf ? v[w][j] : 0ull;
       if (k == 0) p.o_clock[g * A + a] = C[j];
     }
   }
   if ((bad || full) && lane == 0) atomicOr(p.o_flags + g, (bad ? 2u : 0u) | (full ? 8u : 0u));
 }
 
-template <int APL, int W>
+template <int APL, int RING>
 static size_t mc_lds() {
-  return (size_t)kMcWaves * (kMcList * 8 + kMcLive * 4 + (kMcRowsB / (8 * kWave * APL)) * kWave * APL * 8);
+  return (size_t)kMcWaves * (kMcList * 8 + kMcLive * 4 + (kMcRowsB / (8 * kWave * APL)) * kWave * APL * 8 +
+                             RING * 128 * 8 + kMcList + kMcLive);
 }
 
-template <int APL, int W>
+template <int APL, int W, int RING = 0, int KPW = 1, int DEP = 8>
 static hipError_t launch_mc(const MapCounterPlan &p, hipStream_t s) {
-  const unsigned long long blocks = (p.G * p.K + kMcWaves - 1) / kMcWaves;
-  const size_t lds = mc_lds<APL, W>();
-  hipLaunchKernelGGL((map_counter_fold_kernel<APL, W>), dim3((unsigned)blocks), dim3(kMcWaves * kWave), lds, s, p);
+  const unsigned long long blocks = (p.G * ((p.K + KPW - 1) / KPW) + kMcWaves - 1) / kMcWaves;
+  const size_t lds = mc_lds<APL, RING>();
+  auto *fn = &map_counter_fold_kernel<APL, W, RING, KPW, DEP>;
+  if (lds > 64 * 1024) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(fn),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(kMcWaves * kWave), lds, s, p);
   return hipGetLastError();
 }
 
@@ -400,7 +486,21 @@ extern "C" int crdt_map_counter_lub_many(crdt_ctx *ctx, const crdt_map_counter_b
     }
     timing_begin(ctx, "map_counter_fold");
     hipError_t he;
-    if (A <= (size_t)kWave) he = W == 1 ? launch_mc<1, 1>(p, ctx->stream) : launch_mc<1, 2>(p, ctx->stream);
+    const bool al = ((p.c_rs | p.c_gs | p.e_rs | p.e_gs | p.v_rs | p.v_gs) & 1) == 0 &&
+                    ((uintptr_t)in->clock & 15) == 0 && ((uintptr_t)in->ec & 15) == 0 && ((uintptr_t)in->val & 15) == 0;
+    const int ring = A % 2 == 0 && (2 + W) * A <= 128 && al ? ctx->tune.map_counter_dma : 0;
+    const int kpw = ctx->tune.map_counter_kpw;
+    if (!ring && kpw >= 4 && A <= (size_t)kWave / 4)
+      he = W == 1 ? launch_mc<1, 1, 0, 4>(p, ctx->stream) : launch_mc<1, 2, 0, 4>(p, ctx->stream);
+    else if (!ring && kpw >= 2 && A <= (size_t)kWave / 2)
+      he = W == 1 ? launch_mc<1, 1, 0, 2>(p, ctx->stream) : launch_mc<1, 2, 0, 2>(p, ctx->stream);
+    else if (ring == 16) he = W == 1 ? launch_mc<1, 1, 16>(p, ctx->stream) : launch_mc<1, 2, 16>(p, ctx->stream);
+    else if (ring) he = W == 1 ? launch_mc<1, 1, 8>(p, ctx->stream) : launch_mc<1, 2, 8>(p, ctx->stream);
+    else if (A <= (size_t)kWave && ctx->tune.map_counter_depth == 16)
+      he = W == 1 ? launch_mc<1, 1, 0, 1, 16>(p, ctx->stream) : launch_mc<1, 2, 0, 1, 16>(p, ctx->stream);
+    else if (A <= (size_t)kWave && ctx->tune.map_counter_depth == 4)
+      he = W == 1 ? launch_mc<1, 1, 0, 1, 4>(p, ctx->stream) : launch_mc<1, 2, 0, 1, 4>(p, ctx->stream);
+    else if (A <= (size_t)kWave) he = W == 1 ? launch_mc<1, 1>(p, ctx->stream) : launch_mc<1, 2>(p, ctx->stream);
     else if (A <= 2 * (size_t)kWave) he = W == 1 ? launch_mc<2, 1>(p, ctx->stream) : launch_mc<2, 2>(p, ctx->stream);
     else if (A <= 4 * (size_t)kWave) he = W == 1 ? launch_mc<4, 1>(p, ctx->stream) : launch_mc<4, 2>(p, ctx->stream);
     else he = W == 1 ? launch_mc<8, 1>(p, ctx->stream) : launch_mc<8, 2>(p, ctx->stream);

@@ -27,11 +27,12 @@ ap.add_argument("--actors", type=int, default=32)
 ap.add_argument("--steps", type=int, default=5)
 ap.add_argument("--sample-keys", type=int, default=6)
 ap.add_argument("--parity-replicas", type=int, default=512)
+ap.add_argument("--p-def", type=float, default=0.1)  # share of replicas holding deferred removes
 args = ap.parse_args()
 R, K, A = args.replicas, args.keys, args.actors
 torch.cuda.set_device(0)
 ctx = cg.Context(0)
-inp = synth.map_replicas(ctx, R, K, A, 2, 0x5EED0004, kmax=256, p_def=0.1)
+inp = synth.map_replicas(ctx, R, K, A, 2, 0x5EED0004, kmax=256, p_def=args.p_def)
 D = inp.def_clock.shape[0]
 Kw = (K + 63) // 64
 u64 = lambda t: t.cpu().numpy().view(np.uint64)  # noqa: E731

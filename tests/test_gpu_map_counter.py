@@ -17,6 +17,19 @@ pytestmark = pytest.mark.gpu
 import crdts_gpu as cg  # noqa: E402
 
 
+@pytest.fixture(params=["mckpw=1", "mckpw=2", "mckpw=4", "mcdma=8", "mcdma=16"])
+def mcctx(request):
+    """The register ring with 1 (the default), up to 2 or up to 4 keys per wave (A <= 64 / keys), or
+    the replica rows by LDS-DMA into an 8- or 16-slot LDS ring (A even, (2+W)*A <= 128; one key
+    per wave).  Shapes outside a mode's bound take the one-key register ring."""
+    assert torch.cuda.is_available()
+    torch.cuda.set_device(0)
+    ctx = cg.Context(0)
+    ctx.tune(request.param)
+    yield ctx
+    ctx.close()
+
+
 def _run(ctx, d, G=1, off=None, check=True):
     """d: dense replicas (clock (R,A), ec (R,K,A), val (R,K,W,A), def_row/def_clock/def_keys) of one
     group, or G groups stacked when off (per-group CSR offsets of the pool) is given."""
@@ -52,11 +65,11 @@ def _same(got, exp):
 
 @pytest.mark.parametrize("W", [1, 2])
 @pytest.mark.parametrize("seed,R,K,A", [(1, 40, 6, 5), (2, 60, 12, 8), (3, 25, 3, 4), (4, 90, 20, 12)])
-def test_map_counter_op_replay(gpu_ctx, W, seed, R, K, A):
+def test_map_counter_op_replay(mcctx, W, seed, R, K, A):
     maps = O.map_counter_objects(R, K, A, W, seed=seed, steps=6 * R, p_rm=0.3)
     exp = O.map_fold_objects(maps)
     d = O.map_counter_to_dense(maps, K, A, W)
-    res, kw = _run(gpu_ctx, d)
+    res, kw = _run(mcctx, d)
     assert int(res.flags.cpu()[0]) == 0
     _same(_got_maps(res, kw, 1)[0], exp)
 
@@ -81,17 +94,17 @@ def _arbitrary(rng, R, K, A, W, cmax, ndef):
 @pytest.mark.parametrize("W", [1, 2])
 @pytest.mark.parametrize("seed,R,K,A,cmax", [(11, 30, 5, 6, 4), (12, 50, 3, 3, 3), (13, 20, 9, 64, 5),
                                              (14, 16, 4, 100, 3), (15, 12, 3, 300, 4)])
-def test_map_counter_arbitrary(gpu_ctx, W, seed, R, K, A, cmax):
+def test_map_counter_arbitrary(mcctx, W, seed, R, K, A, cmax):
     rng = np.random.default_rng(seed)
     maps = _arbitrary(rng, R, K, A, W, cmax, 2)
     exp = O.map_fold_objects(maps)
     d = O.map_counter_to_dense(maps, K, A, W)
-    res, kw = _run(gpu_ctx, d)
+    res, kw = _run(mcctx, d)
     _same(_got_maps(res, kw, 1)[0], exp)
 
 
 @pytest.mark.parametrize("W", [1, 2])
-def test_map_counter_groups(gpu_ctx, W):
+def test_map_counter_groups(mcctx, W):
     """G = 4 groups of one launch, each with its own slice of the pooled removes (CSR offsets)."""
     G, R, K, A = 4, 30, 7, 6
     parts = [O.map_counter_objects(R, K, A, W, seed=40 + g, steps=200, p_rm=0.35) for g in range(G)]
@@ -100,13 +113,13 @@ def test_map_counter_groups(gpu_ctx, W):
     cat["def_row"] = np.concatenate([x["def_row"] for x in ds])
     off = np.cumsum([0] + [x["def_row"].shape[0] for x in ds]).tolist()
     assert off[-1] > 0
-    res, kw = _run(gpu_ctx, cat, G=G, off=off)
+    res, kw = _run(mcctx, cat, G=G, off=off)
     got = _got_maps(res, kw, G)
     for g in range(G):
         _same(got[g], O.map_fold_objects(parts[g]))
 
 
-def test_map_counter_many_live_removes(gpu_ctx):
+def test_map_counter_many_live_removes(mcctx):
     """40 removes naming key 0 stay deferred (future clocks on an actor no replica reaches): more
     than the LDS row cache holds, so the rest are re-read from HBM every step; all survive."""
     R, K, A, W = 24, 2, 4, 1
@@ -125,7 +138,7 @@ def test_map_counter_many_live_removes(gpu_ctx):
     exp = O.map_fold_objects(maps)
     assert len(exp.deferred) == 40
     d = O.map_counter_to_dense(maps, K, A, W)
-    res, kw = _run(gpu_ctx, d)
+    res, kw = _run(mcctx, d)
     _same(_got_maps(res, kw, 1)[0], exp)
 
 
