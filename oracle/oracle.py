@@ -1413,6 +1413,93 @@ def map_counter_objects(R: int, K: int, A: int, W: int, seed: int, steps: int = 
                             write=lambda v, c, x, a: v.inc(a) if rng.random() < 0.6 else v.dec(a), **kw)
 
 
+# ---- Map<K, Orswot<M>> (nested Orswot values, round 4; the reference's merge_error KAT type) -------
+def map_orswot_to_dense(maps, K: int, M: int, A: int):
+    """Ingest Map<int, Orswot<int>> objects (keys < K, members < M <= 64, actors < A): clock (R, A),
+    ec (R, K, A), oc (R, K, A) the nested Orswot clocks, ent (R, K, M, A) its member dots, the
+    nested deferred removes as a CSR over (replica, key) — vd_off (R*K + 1), vd_clock (Dv, A),
+    vd_members (Dv,) member bitmasks — and the Map's own deferred pool (def_row, def_clock,
+    def_keys)."""
+    R = len(maps)
+    clock = np.zeros((R, A), np.uint64)
+    ec = np.zeros((R, K, A), np.uint64)
+    oc = np.zeros((R, K, A), np.uint64)
+    ent = np.zeros((R, K, M, A), np.uint64)
+    vd_off, vdc, vdm = [0], [], []
+    def_row, dcl, dk = [], [], []
+    for r, m in enumerate(maps):
+        for a, c in m.clock.dots.items():
+            clock[r, a] = c
+        for k in range(K):
+            e = m.entries.get(k)
+            if e is not None:
+                for a, c in e.clock.dots.items():
+                    ec[r, k, a] = c
+                for a, c in e.val.clock.dots.items():
+                    oc[r, k, a] = c
+                for mem, mc in e.val.entries.items():
+                    for a, c in mc.dots.items():
+                        ent[r, k, mem, a] = c
+                for rm, mems in e.val.deferred.items():
+                    row = np.zeros(A, np.uint64)
+                    for a, c in rm.dots.items():
+                        row[a] = c
+                    vdc.append(row)
+                    vdm.append(int(_bits(mems, 64)[0]))
+            vd_off.append(len(vdc))
+        for rm, keys in m.deferred.items():
+            row = np.zeros(A, np.uint64)
+            for a, c in rm.dots.items():
+                row[a] = c
+            def_row.append(r)
+            dcl.append(row)
+            dk.append(_bits(keys, K))
+    D, Dv = len(def_row), len(vdc)
+    Kw = (K + 63) // 64
+    return dict(clock=clock, ec=ec, oc=oc, ent=ent, vd_off=np.array(vd_off, np.uint64),
+                vd_clock=np.array(vdc, np.uint64).reshape(Dv, A), vd_members=np.array(vdm, np.uint64),
+                def_row=np.array(def_row, np.uint64), def_clock=np.array(dcl, np.uint64).reshape(D, A),
+                def_keys=np.array(dk, np.uint64).reshape(D, Kw))
+
+
+def dense_to_map_orswot(clock, ec, oc, ent, vdeferred=None, deferred=()) -> Map:
+    """Egress of one folded dense Map<K, Orswot> state: clock (A,), ec / oc (K, A), ent (K, M, A),
+    vdeferred {key: [(rm row, member set)]}, deferred [(rm row, key set)]."""
+    m = Map(Orswot)
+    m.clock = _vc_row(clock)
+    for k in range(ec.shape[0]):
+        if ec[k].any():
+            o = Orswot()
+            o.clock = _vc_row(oc[k])
+            for mem in range(ent.shape[1]):
+                if ent[k, mem].any():
+                    o.entries[mem] = _vc_row(ent[k, mem])
+            for rm, mems in (vdeferred or {}).get(k, []):
+                o.deferred[_vc_row(rm)] = set(mems)
+            m.entries[k] = MapEntry(_vc_row(ec[k]), o)
+    for rm, keys in deferred:
+        m.deferred[_vc_row(rm)] = set(keys)
+    return m
+
+
+def map_orswot_objects(R: int, K: int, M: int, A: int, seed: int, steps: int = 300, p_vrm: float = 0.35, **kw):
+    """Op-replay replicas of Map<int, Orswot<int>>: a write adds a member under the Map's dot, or
+    (p_vrm) removes one with the nested Orswot's contains() context (test/map.rs's nested-set
+    pattern), so out-of-order delivery leaves deferred removes at both levels."""
+    rng = np.random.default_rng(seed ^ 0x0E5)
+
+    def write(v, c, x, a):
+        mem = int(rng.integers(M))
+        if rng.random() < p_vrm:
+            ctx = v.contains(mem).derive_rm_ctx()
+            if rng.random() < 0.5:  # a context read at a replica that has seen more adds: deferred
+                b = int(rng.integers(A))
+                ctx.clock.apply(Dot(b, ctx.clock.get(b) + int(rng.integers(1, 3))))
+            return v.rm(mem, ctx)
+        return v.add(mem, c)
+    return gen_map_replicas(seed, R, K, A, steps=steps, vnew=Orswot, write=write, **kw)
+
+
 def max_vals(maps) -> int:
     return max([len(e.val.vals) for m in maps for e in m.entries.values()] + [1])
 

@@ -52,7 +52,7 @@ EXPORTS = (
     "crdt_ctx_comm_init_ops", "crdt_ctx_comm_note",
     "crdt_mvreg_lub_many", "crdt_mvreg_merge_batch", "crdt_mvreg_apply_batch",
     "crdt_orswot_lub_many_doff", "crdt_map_lub_many_doff",
-    "crdt_orswot_lub_many_sharded_doff", "crdt_map_lub_many_sharded_doff", "crdt_map_counter_lub_many",
+    "crdt_orswot_lub_many_sharded_doff", "crdt_map_lub_many_sharded_doff", "crdt_map_counter_lub_many", "crdt_map_orswot_lub_many",
 )
 
 
@@ -178,6 +178,20 @@ class MapCounterOut(ctypes.Structure):  # crdt_map_counter_out
     _fields_ = [("clock", P), ("ec", P), ("val", P), ("flags", P), ("def_keep", P), ("def_keys", P)]
 
 
+class MapOrswotBatch(ctypes.Structure):  # crdt_map_orswot_batch
+    _fields_ = [
+        ("G", S), ("R", S), ("K", S), ("M", S), ("A", S),
+        ("clock", P), ("ec", P), ("oc", P), ("ent", P),
+        ("vd_off", P), ("vd_clock", P), ("vd_mem", P),
+        ("def_off", ctypes.POINTER(S)), ("def_row", P), ("def_clock", P), ("def_keys", P),
+    ]
+
+
+class MapOrswotOut(ctypes.Structure):  # crdt_map_orswot_out
+    _fields_ = [("clock", P), ("ec", P), ("oc", P), ("ent", P), ("vd_n", P), ("vd_clock", P), ("vd_mem", P),
+                ("flags", P), ("def_keep", P), ("def_keys", P)]
+
+
 class MapOut(ctypes.Structure):  # crdt_map_out
     _fields_ = [("Vout", S), ("Vstate", S), ("clock", P), ("ec", P), ("vclk", P), ("vval", P), ("nval", P),
                 ("flags", P), ("def_keep", P), ("def_keys", P)]
@@ -237,6 +251,7 @@ _SIGS.update({
     "crdt_map_lub_many_sharded_doff": ([P, ctypes.POINTER(MapBatch), P, S, S, S, ctypes.POINTER(MapOut)],
                                        ctypes.c_int),
     "crdt_map_counter_lub_many": ([P, ctypes.POINTER(MapCounterBatch), ctypes.POINTER(MapCounterOut)], ctypes.c_int),
+    "crdt_map_orswot_lub_many": ([P, ctypes.POINTER(MapOrswotBatch), ctypes.POINTER(MapOrswotOut)], ctypes.c_int),
     "crdt_vclock_ingest": ([P, P, P, S, P, S, P, S, P], ctypes.c_int),
     "crdt_pncounter_ingest": ([P, P, P, S, P, S, P, S, P], ctypes.c_int),
     "crdt_gset_ingest": ([P, P, P, S, P, S, P, S, P], ctypes.c_int),

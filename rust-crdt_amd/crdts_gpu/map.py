@@ -496,3 +496,108 @@ def counter_lub_many(clock: torch.Tensor, ec: torch.Tensor, val: torch.Tensor, d
     if squeeze:
         out_clock, out_ec, out_val, flags = out_clock[0], out_ec[0], out_val[0], flags
     return MapCounterLub(out_clock, out_ec, out_val, flags, keep, keys_out)
+
+
+# ---- Map<K, Orswot<M>> (crdt_map_orswot_lub_many, round 4) ------------------------------------------
+VD_CAP = 16  # nested deferred removes per key state (crdt_gpu.h)
+
+
+class MapOrswotLub(NamedTuple):
+    clock: torch.Tensor               # (G, A)
+    ec: torch.Tensor                  # (G, K, A)
+    oc: torch.Tensor                  # (G, K, A) the nested Orswot clocks
+    ent: torch.Tensor                 # (G, K, M, A) its member dots
+    vd_n: torch.Tensor                # (G, K) int32: nested deferred removes per key
+    vd_clock: torch.Tensor            # (G, K, 16, A)
+    vd_mem: torch.Tensor              # (G, K, 16) member bitmasks
+    flags: torch.Tensor               # (G,) int32
+    def_keep: Optional[torch.Tensor]  # (D,) uint8
+    def_keys: Optional[torch.Tensor]  # (D, Kw)
+
+
+def orswot_lub_many(clock: torch.Tensor, ec: torch.Tensor, oc: torch.Tensor, ent: torch.Tensor,
+                    vd_off: torch.Tensor, vd_clock: Optional[torch.Tensor] = None,
+                    vd_mem: Optional[torch.Tensor] = None, def_off=None, def_row: Optional[torch.Tensor] = None,
+                    def_clock: Optional[torch.Tensor] = None, def_keys: Optional[torch.Tensor] = None,
+                    ctx: Optional[Context] = None, check: bool = True) -> MapOrswotLub:
+    """The exact left fold of Map::merge (map.rs:140-220) for Map<K, Orswot<M>> — orswot.rs:81-149 as
+    the value's merge, :150-183 as its forget.  clock (G,R,A) / (R,A), ec and oc (G,R,K,A), ent
+    (G,R,K,M,A), all contiguous; the nested deferred removes as a device CSR over (g, r, k): vd_off
+    (G*R*K + 1,) int64, vd_clock (Dv, A), vd_mem (Dv,) member bitmasks; the Map's own deferred pool as
+    for lub_many (host def_off).  check=True raises on flags (bit 1: def_row not sorted / out of
+    range, bit 3: more than 256 live Map removes named one key, bit 4: more than 16 nested deferred
+    removes on one key)."""
+    ctx = ctx or Context.default(clock.device.index)
+    squeeze = clock.dim() == 2
+    c, e, o, m = ((t.unsqueeze(0) if squeeze else t) for t in (clock, ec, oc, ent))
+    if c.dim() != 3 or e.dim() != 4 or o.dim() != 4 or m.dim() != 5:
+        raise ValueError("map.orswot_lub_many: clock (G,R,A), ec / oc (G,R,K,A), ent (G,R,K,M,A) expected")
+    G, R, A = c.shape
+    K, M = e.shape[2], m.shape[3]
+    if tuple(e.shape) != (G, R, K, A) or tuple(o.shape) != (G, R, K, A) or tuple(m.shape) != (G, R, K, M, A):
+        raise ValueError(f"map.orswot_lub_many: shapes clock {tuple(c.shape)} ec {tuple(e.shape)} oc "
+                         f"{tuple(o.shape)} ent {tuple(m.shape)} do not agree")
+    for t, nm in ((c, "clock"), (e, "ec"), (o, "oc"), (m, "ent")):
+        ctx.check_tensor(t, f"map.orswot_lub_many({nm})")
+        if not t.is_contiguous():
+            raise ValueError(f"map.orswot_lub_many: {nm} must be contiguous")
+    dev = clock.device
+    if vd_off.device != dev or not vd_off.is_contiguous() or tuple(vd_off.shape) != (G * R * K + 1,):
+        raise ValueError(f"map.orswot_lub_many: vd_off must be a contiguous ({G * R * K + 1},) tensor on {dev}")
+    Dv = int(vd_off[-1].item()) if vd_off.numel() else 0
+    if Dv > 0:
+        for t, nm, shape in ((vd_clock, "vd_clock", (Dv, A)), (vd_mem, "vd_mem", (Dv,))):
+            if t is None or not t.is_contiguous() or tuple(t.shape) != shape:
+                raise ValueError(f"map.orswot_lub_many: {nm} must be a contiguous {shape} tensor")
+            ctx.check_tensor(t, f"map.orswot_lub_many({nm})")
+    Kw = (K + 63) // 64
+    out = [torch.empty(sh, dtype=torch.int64, device=dev)
+           for sh in ((G, A), (G, K, A), (G, K, A), (G, K, M, A), (G, K, VD_CAP, A), (G, K, VD_CAP))]
+    vd_n = torch.empty((G, K), dtype=torch.int32, device=dev)
+    flags = torch.empty(G, dtype=torch.int32, device=dev)
+    b = _abi.MapOrswotBatch()
+    b.G, b.R, b.K, b.M, b.A = G, R, K, M, A
+    b.clock, b.ec, b.oc, b.ent = c.data_ptr(), e.data_ptr(), o.data_ptr(), m.data_ptr()
+    b.vd_off = vd_off.data_ptr()
+    if Dv > 0:
+        b.vd_clock, b.vd_mem = vd_clock.data_ptr(), vd_mem.data_ptr()
+    ob = _abi.MapOrswotOut()
+    ob.clock, ob.ec, ob.oc, ob.ent, ob.vd_clock, ob.vd_mem = (t.data_ptr() for t in out)
+    ob.vd_n, ob.flags = vd_n.data_ptr(), flags.data_ptr()
+    keep = keys_out = None
+    off_arr = None
+    if def_off is not None:
+        off = np.asarray(def_off, dtype=np.uint64)
+        if off.shape != (G + 1,):
+            raise ValueError(f"map.orswot_lub_many: def_off must have G+1 = {G + 1} entries")
+        D = int(off[-1])
+        if D > 0:
+            for t, nm, shape in ((def_clock, "def_clock", (D, A)), (def_keys, "def_keys", (D, Kw)),
+                                 (def_row, "def_row", (D,))):
+                if t is None or not t.is_contiguous() or tuple(t.shape) != shape:
+                    raise ValueError(f"map.orswot_lub_many: {nm} must be a contiguous {shape} tensor")
+                if nm != "def_row":
+                    ctx.check_tensor(t, f"map.orswot_lub_many({nm})")
+            if def_row.dtype not in (torch.int32, torch.uint32) or def_row.device != dev:
+                raise ValueError(f"map.orswot_lub_many: def_row must be an int32 tensor on {dev}")
+            off_arr = (ctypes.c_size_t * (G + 1))(*[int(x) for x in off])
+            b.def_off = ctypes.cast(off_arr, ctypes.POINTER(ctypes.c_size_t))
+            b.def_row, b.def_clock, b.def_keys = def_row.data_ptr(), def_clock.data_ptr(), def_keys.data_ptr()
+            keep = torch.empty(D, dtype=torch.uint8, device=dev)
+            keys_out = torch.empty((D, Kw), dtype=torch.int64, device=dev)
+            ob.def_keep, ob.def_keys = keep.data_ptr(), keys_out.data_ptr()
+    ctx.call("crdt_map_orswot_lub_many", ctypes.byref(b), ctypes.byref(ob))
+    if check:
+        f = 0
+        for x in flags.cpu().numpy().tolist():
+            f |= int(x)
+        if f & 2:
+            raise ValueError("map.orswot_lub_many: def_row not non-decreasing per group or >= R")
+        if f & 8:
+            raise RuntimeError("map.orswot_lub_many: more than 256 live removes named one key")
+        if f & 16:
+            raise RuntimeError("map.orswot_lub_many: more than 16 deferred removes in one key's Orswot")
+    oclk, oec, ooc, oent, ovdc, ovdm = out
+    if squeeze:
+        oclk, oec, ooc, oent, vd_n, ovdc, ovdm = oclk[0], oec[0], ooc[0], oent[0], vd_n[0], ovdc[0], ovdm[0]
+    return MapOrswotLub(oclk, oec, ooc, oent, vd_n, ovdc, ovdm, flags, keep, keys_out)

@@ -97,15 +97,15 @@ __global__ __launch_bounds__(kMcWaves * kWave) void map_counter_fold_kernel(MapC
   uint8_t *lmask = reinterpret_cast<uint8_t *>(lds + kMcWaves * WQ) + wv * (kMcList + kMcLive);
   uint8_t *lvm = lmask + kMcList;
 
-  // Loads are never EXEC-masked: lanes past A read the row's last word and zero it after (a masked
-  // load puts the wait counter's bookkeeping on branches, and the compiler then drains every
-  // outstanding load — the replica ring's prefetch included — at the join).
+  // Loads are never EXEC-masked: lanes past A read the row's last word (a masked load puts the wait
+  // counter's bookkeeping on branches, and the compiler then drains every outstanding load — the
+  // replica ring's prefetch included — at the join).  Every row a lane holds, remove rows included,
+  // is a copy of actor A-1 past A, so those lanes evolve exactly as actor A-1 and never change a vote.
   auto ld_row = [&](u64 (&x)[APL], const u64 *src) {
 #pragma unroll
     for (int j = 0; j < APL; ++j) {
       const unsigned long long a = (unsigned long long)al + (unsigned long long)HL * j;
-      const u64 t = src[a < A ? a : A - 1];
-      x[j] = a < A ? t : 0ull;
+      x[j] = src[a < A ? a : A - 1];
     }
   };
 
@@ -365,8 +365,8 @@ __global__ __launch_bounds__(kMcWaves * kWave) void map_counter_fold_kernel(MapC
     // multiplies); past the last replica the pointers stay on it (loaded, never used)
     const u64 *pc = p.clock + g * p.c_gs, *pe = p.ec + g * p.e_gs + kc * A, *pv = p.val + g * p.v_gs + kc * W * A;
     unsigned long long nload = 0;  // replica of the next load_step
-    // (the ring holds the raw words; lanes past A are zeroed when the step uses them, DEPTH steps
-    // later — a select right behind the load would make the wave wait for it at once)
+    // (the ring holds the raw words, lanes past A copies of actor A-1, used as they are: a select
+    // right behind a load would make the wave wait for it at once)
     auto load_step = [&](int s, bool last_check) {
 #pragma unroll
       for (int j = 0; j < APL; ++j) {

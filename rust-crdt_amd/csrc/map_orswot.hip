@@ -1,0 +1,417 @@
+// Map<K, Orswot<M>> lub_many (round 4): Map::merge (map.rs:140-220) with a nested Orswot value —
+// the value type of the reference's own full Map KAT (map.rs:435-494, merge_error).  The value's
+// merge is Orswot::merge (orswot.rs:81-149) and its forget Orswot's Causal::forget
+// (orswot.rs:150-183).  As for every Map value type the fold acc = Map::new(); for r: acc.merge(r)
+// is not associative, so each key is folded in replica order (exact for any input), one wave per
+// (group, key), lane = actor (A <= 64), the member rows of the key's Orswot in registers (M <= 32).
+//
+// Step r on the key's state (map clock C, entry clock e, Orswot clock oc, member rows E[m], nested
+// deferred removes D in LDS) with replica r's (c2, e2, oc2, E2[m], D2):
+//  - entry clock: the branch-free join of map_counter.hip (the "common" clock covers all four
+//    presence cases) and the case's forget clock X (removed_information / we_deleted / deleted);
+//  - value, both present (:183): Orswot::merge — per member the dot-survival join
+//    max(E == E2 ? E : 0, forget(E2, oc), forget(E, oc2)) (:84-138: elementwise, and empty exactly
+//    when the reference drops the member), then every remove of D and D2 forgets its members
+//    (apply_rm of other.deferred :141-143 and apply_deferred :147; forgets commute), D2 joins D
+//    (an equal clock unions its members, apply_rm :242-246), oc |= oc2, and D keeps the removes
+//    with !(rm <= oc) (the re-test of apply_deferred);  only the replica's entry (:193-208): the
+//    value is the replica's;  then the value forgets X (:160, :188, :205);
+//  - the Map's own removes naming the key (apply_keyset_rm / apply_deferred, :213-219, :318-348),
+//    one forget by their max: the entry clock, and the value while the entry stays;
+//  - C |= c2 and the Map-level deferral test (witness thresholds, as in map_counter.hip).
+// Orswot::forget rebuilds its deferred map with collect(): two removes whose clocks become equal
+// keep one entry, the later one's members (HashMap insert order; the reference's own iteration
+// order is unspecified, this is the oracle's dict order) at the earlier one's place.
+// Lanes past A hold copies of actor A-1 (clamped loads), so they never change a vote.
+#include "common.hpp"
+
+namespace crdt {
+
+constexpr int kMoWaves = 4;   // key waves per workgroup
+constexpr int kMoList = 256;  // Map removes naming the key, gathered per window (row << 32 | index)
+constexpr int kMoLive = 256;  // live Map removes per key
+constexpr int kMoRows = 8;    // live Map-remove rows cached in LDS
+constexpr int kMoVd = 16;     // nested deferred removes per key state (flags bit 4 past it)
+
+struct MapOrswotPlan {
+  const u64 *clock, *ec, *oc, *ent;   // (G,R,A), (G,R,K,A), (G,R,K,A), (G,R,K,M,A)
+  const u64 *vd_off;                  // nested deferred CSR over (g, r, k): G*R*K + 1 (device)
+  const u64 *vd_clock, *vd_mem;       // (Dv, A), (Dv) member bitmasks
+  unsigned long long G, R, K, M, A, Kw;
+  const size_t *def_off;  // device copy (G+1), or null: no Map-level removes
+  const uint32_t *def_row;
+  const u64 *def_clock, *def_keys;
+  u64 *o_clock, *o_ec, *o_oc, *o_ent, *o_vd_clock, *o_vd_mem;
+  unsigned *o_vd_n, *o_flags;
+};
+
+__device__ __forceinline__ bool mo_nz(u64 x) { return __ballot(x != 0) != 0; }
+__device__ __forceinline__ u64 mo_fg(u64 x, u64 c) { return x > c ? x : 0; }  // VClock::forget, per actor
+__device__ __forceinline__ u64 mo_max(u64 x, u64 y) { return x > y ? x : y; }
+
+template <int MT>
+__global__ __launch_bounds__(kMoWaves * kWave) void map_orswot_fold_kernel(MapOrswotPlan p) {
+  constexpr int DEPTH = MT <= 8 ? 4 : 2;  // replica steps in flight (register ring)
+  extern __shared__ u64 lds[];
+  const int lane = (int)(threadIdx.x % kWave), wv = (int)(threadIdx.x / kWave);
+  const unsigned long long gk = (unsigned long long)blockIdx.x * kMoWaves + wv;
+  if (gk >= p.G * p.K) return;  // (whole waves; nothing below synchronises the workgroup)
+  const unsigned long long g = gk / p.K, k = gk % p.K, A = p.A, R = p.R, K = p.K, M = p.M;
+  constexpr unsigned long long WQ = kMoList + kMoLive / 2 + kMoRows * kWave + kMoVd * kWave + kMoVd;
+  u64 *lst = lds + (unsigned long long)wv * WQ;
+  uint32_t *live = reinterpret_cast<uint32_t *>(lst + kMoList);
+  u64 *rows = lst + kMoList + kMoLive / 2;  // [kMoRows][64] live Map-remove rows
+  u64 *vrow = rows + kMoRows * kWave;       // [kMoVd][64] nested deferred rm rows
+  u64 *vmsk = vrow + kMoVd * kWave;         // [kMoVd] their member masks
+  const unsigned la = (unsigned)((unsigned long long)lane < A ? lane : A - 1);  // the lane's actor
+  auto ld = [&](const u64 *row) { return row[la]; };
+
+  // ---- the Map's removes naming key k, in replica order (map_counter.hip's walk, one key)
+  const unsigned long long d0 = p.def_off ? p.def_off[g] : 0, d1 = p.def_off ? p.def_off[g + 1] : 0;
+  unsigned long long dc = d0;
+  int nl = 0, li = 0;
+  bool bad = false;  // def_row not non-decreasing or >= R (flags bit 1)
+  u64 last_row = 0;
+  auto refill = [&]() {
+    nl = 0;
+    li = 0;
+    while (dc < d1 && nl + kWave <= kMoList) {
+      const unsigned long long d = dc + lane;
+      bool hit = false;
+      u64 row = 0;
+      if (d < d1) {
+        row = p.def_row[d];
+        hit = (p.def_keys[d * p.Kw + k / 64] >> (k % 64)) & 1ull;
+      }
+      const u64 prev = __shfl_up(row, 1);
+      bool b = d < d1 && (row >= R || (lane == 0 ? row < last_row : row < prev));
+      if (__ballot(b)) bad = true;
+      const unsigned long long n = d1 - dc < (unsigned long long)kWave ? d1 - dc : kWave;
+      last_row = __shfl(row, (int)n - 1);
+      const u64 m = __ballot(hit);
+      if (hit) lst[nl + __popcll(m & ((1ull << lane) - 1))] = (row << 32) | (u64)(d - d0);
+      nl += __popcll(m);
+      dc += n;
+    }
+  };
+  unsigned nxt = ~0u;  // replica row of the next remove naming k (~0: none left)
+  auto advance = [&]() {
+    for (;;) {
+      if (li < nl) {
+        nxt = (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(lst[li] >> 32));
+        return;
+      }
+      if (dc >= d1) {
+        nxt = ~0u;
+        return;
+      }
+      refill();
+    }
+  };
+  refill();
+  advance();
+  bool full = false;   // more than kMoLive live Map removes on the key (flags bit 3)
+  bool vfull = false;  // more than kMoVd nested deferred removes (flags bit 4)
+  int na = 0;
+  auto live_row = [&](int i) -> u64 {
+    return i < kMoRows ? rows[(unsigned long long)i * kWave + lane] : ld(p.def_clock + (d0 + live[i]) * A);
+  };
+  auto put_row = [&](int i, u64 x) {
+    if (i < kMoRows) rows[(unsigned long long)i * kWave + lane] = x;
+  };
+  u64 rk = 0, T = ~0ull;  // max of the live Map removes / witness thresholds
+
+  // ---- the key's state
+  u64 C = 0, e = 0, oc = 0, E[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) E[m] = 0;
+  int nd = 0;  // nested deferred removes in vrow / vmsk (uniform)
+
+  // nested deferred helpers (LDS rows, uniform control flow)
+  auto forget_members = [&](u64 rm, u64 msk) {  // Orswot::apply_rm's member forget (orswot.rs:231-238)
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+      if ((msk >> m) & 1ull) E[m] = mo_fg(E[m], rm);
+  };
+  auto vd_add = [&](u64 rm, u64 msk) {  // deferred.entry(clock) extend / insert (orswot.rs:242-246)
+    for (int i = 0; i < nd; ++i) {
+      if (!__ballot(vrow[(unsigned long long)i * kWave + lane] != rm)) {
+        const u64 mm = vmsk[i] | msk;
+        if (lane == 0) vmsk[i] = mm;
+        return;
+      }
+    }
+    if (nd < kMoVd) {
+      vrow[(unsigned long long)nd * kWave + lane] = rm;
+      if (lane == 0) vmsk[nd] = msk;
+      ++nd;
+    } else {
+      vfull = true;
+    }
+  };
+  auto vd_keep_live = [&]() {  // apply_deferred's re-test: keep !(rm <= oc), in order
+    int o = 0;
+    for (int i = 0; i < nd; ++i) {
+      const u64 x = vrow[(unsigned long long)i * kWave + lane];
+      const u64 mi = vmsk[i];
+      if (__ballot(x > oc)) {
+        if (o != i) {
+          vrow[(unsigned long long)o * kWave + lane] = x;
+          if (lane == 0) vmsk[o] = mi;
+        }
+        ++o;
+      }
+    }
+    nd = o;
+  };
+  auto value_forget = [&](u64 X) {  // Orswot's Causal::forget (orswot.rs:150-183)
+    oc = mo_fg(oc, X);
+#pragma unroll
+    for (int m = 0; m < MT; ++m) E[m] = mo_fg(E[m], X);
+    int o = 0;
+    for (int i = 0; i < nd; ++i) {
+      const u64 x = mo_fg(vrow[(unsigned long long)i * kWave + lane], X);
+      const u64 mi = vmsk[i];
+      if (!__ballot(x != 0)) continue;  // forgotten
+      int j = 0;
+      for (; j < o; ++j)  // equal to a kept one: the later members at the earlier place (collect())
+        if (!__ballot(vrow[(unsigned long long)j * kWave + lane] != x)) break;
+      if (j < o) {
+        if (lane == 0) vmsk[j] = mi;
+        continue;
+      }
+      vrow[(unsigned long long)o * kWave + lane] = x;
+      if (lane == 0) vmsk[o] = mi;
+      ++o;
+    }
+    nd = o;
+  };
+
+  // one replica step
+  auto step = [&](unsigned long long r, u64 c2, u64 e2, u64 o2, const u64 (&E2)[MT], u64 vlo, u64 vhi) {
+    const bool p1 = mo_nz(e), p2 = mo_nz(e2);
+    const u64 t0 = e == e2 ? e : 0, t1 = mo_fg(e2, C), t2 = mo_fg(e, c2);
+    const u64 en = mo_max(mo_max(t0, t1), t2);
+    const u64 y = p1 ? (p2 ? mo_max(e, e2) : c2) : C;
+    const u64 X = mo_fg(y, en);
+    if (p1 && p2) {  // our_entry.val.merge(entry.val) (map.rs:183) = Orswot::merge
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+        E[m] = mo_max(mo_max(E[m] == E2[m] ? E[m] : 0, mo_fg(E2[m], oc)), mo_fg(E[m], o2));
+      for (u64 d = vlo; d < vhi; ++d) {
+        const u64 rm = ld(p.vd_clock + d * A), msk = p.vd_mem[d];
+        vd_add(rm, msk);
+      }
+      for (int i = 0; i < nd; ++i) forget_members(vrow[(unsigned long long)i * kWave + lane], vmsk[i]);
+      oc = mo_max(oc, o2);
+      vd_keep_live();
+    } else if (p2) {  // the replica's entry (map.rs:193-208)
+#pragma unroll
+      for (int m = 0; m < MT; ++m) E[m] = E2[m];
+      oc = o2;
+      nd = 0;
+      for (u64 d = vlo; d < vhi; ++d) {
+        const u64 rm = ld(p.vd_clock + d * A), msk = p.vd_mem[d];
+        vd_add(rm, msk);
+      }
+    }
+    if (p1 || p2) value_forget(X);
+    e = en;
+    // the Map's removes: replica r's own (apply_keyset_rm) and the live ones (apply_deferred)
+    bool chg = false;
+    u64 f = rk;
+    const unsigned r32 = (unsigned)r;
+    if (nxt <= r32) {
+      do {
+        const unsigned idx = (unsigned)lst[li];
+        const u64 rm = ld(p.def_clock + (d0 + idx) * A);
+        f = mo_max(f, rm);
+        if (na < kMoLive) {
+          if (lane == 0) live[na] = idx;
+          put_row(na, rm);
+          ++na;
+          chg = true;
+        } else {
+          full = true;
+        }
+        ++li;
+        advance();
+      } while (nxt <= r32);
+    }
+    if (na > 0) {  // (f = 0 otherwise: nothing to forget)
+      e = mo_fg(e, f);
+      if (mo_nz(e)) value_forget(f);  // entry.val.forget only while the entry stays (map.rs:321-330)
+    }
+    C = mo_max(C, c2);
+    if (na > 0 && (chg || __ballot(C >= T))) {  // live set re-test (witness thresholds)
+      bool changed = chg;
+      T = ~0ull;
+      for (int i = 0; i < na;) {
+        const u64 rm = live_row(i);
+        const u64 m = __ballot(rm > C);
+        if (m) {
+          const int wl = __builtin_ctzll(m);
+          T = lane == wl && rm < T ? rm : T;
+          ++i;
+          continue;
+        }
+        changed = true;
+        const int lastp = na - 1;
+        if (i != lastp) {
+          put_row(i, live_row(lastp));
+          const unsigned li_last = live[lastp];
+          if (lane == 0) live[i] = li_last;
+        }
+        --na;
+      }
+      if (changed) {
+        rk = 0;
+        for (int i = 0; i < na; ++i) rk = mo_max(rk, live_row(i));
+      }
+    }
+  };
+
+  // ---- replica rows through a register ring (DEPTH steps ahead; clamped past the last replica)
+  const u64 *pc = p.clock + g * R * A, *pe = p.ec + (g * R * K + k) * A, *po = p.oc + (g * R * K + k) * A;
+  const u64 *pm = p.ent + (g * R * K + k) * M * A;
+  const u64 *pvo = p.vd_off + g * R * K + k;
+  const unsigned long long rsK = K * A, rsM = K * M * A;
+  u64 c2r[DEPTH], e2r[DEPTH], o2r[DEPTH], E2r[DEPTH][MT], vlr[DEPTH], vhr[DEPTH];
+  unsigned long long nload = 0;
+  auto load_step = [&](int s) {
+    c2r[s] = ld(pc);
+    e2r[s] = ld(pe);
+    o2r[s] = ld(po);
+#pragma unroll
+    for (int m = 0; m < MT; ++m) E2r[s][m] = (unsigned long long)m < M ? ld(pm + m * A) : 0ull;
+    vlr[s] = pvo[0];
+    vhr[s] = pvo[1];
+    if (++nload < R) {
+      pc += A;
+      pe += rsK;
+      po += rsK;
+      pm += rsM;
+      pvo += K;
+    }
+  };
+#pragma unroll
+  for (int s = 0; s < DEPTH; ++s) load_step(s);
+  for (unsigned long long r0 = 0; r0 < R; r0 += DEPTH) {
+#pragma unroll
+    for (int s = 0; s < DEPTH; ++s) {
+      const unsigned long long r = r0 + s;
+      if (r >= R) break;
+      const u64 vlo = __builtin_amdgcn_readfirstlane((unsigned)vlr[s]) |
+                      ((u64)__builtin_amdgcn_readfirstlane((unsigned)(vlr[s] >> 32)) << 32);
+      const u64 vhi = __builtin_amdgcn_readfirstlane((unsigned)vhr[s]) |
+                      ((u64)__builtin_amdgcn_readfirstlane((unsigned)(vhr[s] >> 32)) << 32);
+      step(r, c2r[s], e2r[s], o2r[s], E2r[s], vlo, vhi);
+      load_step(s);
+    }
+  }
+
+  // ---- the key's folded entry (an empty entry clock: absent, value rows 0), the group's clock
+  const bool pf = mo_nz(e);
+  if ((unsigned long long)lane < A) {
+    p.o_ec[gk * A + lane] = e;
+    p.o_oc[gk * A + lane] = pf ? oc : 0ull;
+    for (unsigned long long m = 0; m < M; ++m) {
+      u64 x = 0;
+#pragma unroll
+      for (int q = 0; q < MT; ++q)
+        if ((unsigned long long)q == m) x = E[q];
+      p.o_ent[(gk * M + m) * A + lane] = pf ? x : 0ull;
+    }
+    if (k == 0) p.o_clock[g * A + lane] = C;
+  }
+  const int no = pf ? nd : 0;
+  for (int i = 0; i < no; ++i) {
+    const u64 x = vrow[(unsigned long long)i * kWave + lane];
+    if ((unsigned long long)lane < A) p.o_vd_clock[(gk * kMoVd + i) * A + lane] = x;
+    if (lane == 0) p.o_vd_mem[gk * kMoVd + i] = vmsk[i];
+  }
+  if (lane == 0) p.o_vd_n[gk] = (unsigned)no;
+  if ((bad || full || vfull) && lane == 0)
+    atomicOr(p.o_flags + g, (bad ? 2u : 0u) | (full ? 8u : 0u) | (vfull ? 16u : 0u));
+}
+
+static size_t mo_lds() {
+  return (size_t)kMoWaves * (kMoList * 8 + kMoLive * 4 + kMoRows * kWave * 8 + kMoVd * kWave * 8 + kMoVd * 8);
+}
+
+template <int MT>
+static hipError_t launch_mo(const MapOrswotPlan &p, hipStream_t s) {
+  const unsigned long long blocks = (p.G * p.K + kMoWaves - 1) / kMoWaves;
+  hipLaunchKernelGGL(map_orswot_fold_kernel<MT>, dim3((unsigned)blocks), dim3(kMoWaves * kWave), mo_lds(), s, p);
+  return hipGetLastError();
+}
+
+}  // namespace crdt
+
+using namespace crdt;
+
+extern "C" int crdt_map_orswot_lub_many(crdt_ctx *ctx, const crdt_map_orswot_batch *in, crdt_map_orswot_out *out) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
+  CRDT_CHECK_CTX(ctx);
+  if (!in || !out) return fail(ctx, CRDT_EINVAL, "map_orswot_lub_many: NULL batch/out");
+  const size_t G = in->G, R = in->R, K = in->K, M = in->M, A = in->A;
+  if (G == 0 || K == 0 || A == 0) return CRDT_OK;
+  if (A > (size_t)kWave) return fail(ctx, CRDT_EUNSUPPORTED, "map_orswot_lub_many: A = %zu > %d", A, kWave);
+  if (M > 32) return fail(ctx, CRDT_EUNSUPPORTED, "map_orswot_lub_many: M = %zu > 32", M);
+  if (!out->clock || !out->ec || !out->oc || (M && !out->ent) || !out->vd_n || !out->vd_clock || !out->vd_mem ||
+      !out->flags)
+    return fail(ctx, CRDT_EINVAL, "map_orswot_lub_many: NULL output");
+  if (R > 0 && (!in->clock || !in->ec || !in->oc || (M && !in->ent) || !in->vd_off))
+    return fail(ctx, CRDT_EINVAL, "map_orswot_lub_many: NULL input");
+  if (G * K > 0x7fffffffULL * (size_t)kMoWaves || R > 0xfffffffeULL)
+    return fail(ctx, CRDT_EUNSUPPORTED, "map_orswot_lub_many: G*K or R too large");
+  if (in->def_off && in->def_off[0] != 0) return fail(ctx, CRDT_EINVAL, "map_orswot_lub_many: def_off[0] must be 0");
+  const size_t D = (in->def_off && G > 0) ? in->def_off[G] : 0;
+  for (size_t i = 0; in->def_off && i < G; ++i)
+    if (in->def_off[i + 1] < in->def_off[i])
+      return fail(ctx, CRDT_EINVAL, "map_orswot_lub_many: def_off not non-decreasing");
+  if (D > 0 && (!in->def_row || !in->def_clock || !in->def_keys || !out->def_keep || !out->def_keys))
+    return fail(ctx, CRDT_EINVAL, "map_orswot_lub_many: deferred buffers missing");
+  if (D > 0xffffffffULL) return fail(ctx, CRDT_EUNSUPPORTED, "map_orswot_lub_many: too many deferred");
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  const size_t Kw = (K + 63) / 64;
+  MapOrswotPlan p{(const u64 *)in->clock, (const u64 *)in->ec, (const u64 *)in->oc, (const u64 *)in->ent,
+                  (const u64 *)in->vd_off, (const u64 *)in->vd_clock, (const u64 *)in->vd_mem, G, R, K, M, A, Kw,
+                  nullptr, in->def_row, (const u64 *)in->def_clock, (const u64 *)in->def_keys,
+                  (u64 *)out->clock, (u64 *)out->ec, (u64 *)out->oc, (u64 *)out->ent, (u64 *)out->vd_clock,
+                  (u64 *)out->vd_mem, out->vd_n, out->flags};
+  if (int rc = device_fill(ctx, out->flags, G * sizeof(unsigned), 0)) return rc;
+  if (R == 0) {  // fold of nothing: Map::new()
+    if (int rc = device_fill(ctx, out->clock, G * A * 8, 0)) return rc;
+    if (int rc = device_fill(ctx, out->ec, G * K * A * 8, 0)) return rc;
+    if (int rc = device_fill(ctx, out->oc, G * K * A * 8, 0)) return rc;
+    if (M)
+      if (int rc = device_fill(ctx, out->ent, G * K * M * A * 8, 0)) return rc;
+    if (int rc = device_fill(ctx, out->vd_n, G * K * sizeof(unsigned), 0)) return rc;
+  } else {
+    if (D > 0) {
+      if (int rc = ensure_scratch(ctx, (G + 1) * sizeof(size_t))) return rc;
+      if (int rc = stage_h2d(ctx, ctx->scratch, in->def_off, (G + 1) * sizeof(size_t))) return rc;
+      p.def_off = reinterpret_cast<const size_t *>(ctx->scratch);
+    }
+    timing_begin(ctx, "map_orswot_fold");
+    const hipError_t he = M <= 8 ? launch_mo<8>(p, ctx->stream) : launch_mo<32>(p, ctx->stream);
+    timing_end(ctx);
+    if (he != hipSuccess) return hip_fail(ctx, he, "map_orswot_fold_kernel launch");
+  }
+  if (D == 0) return CRDT_OK;
+  DefPlan q{};  // the Map's surviving removes (!(rm <= C_final)), identical clocks merged
+  q.G = G;
+  q.D = D;
+  q.M = K;
+  q.A = A;
+  q.Mw = Kw;
+  q.def_clock = (const u64 *)in->def_clock;
+  q.def_members = (const u64 *)in->def_keys;
+  q.out_clock = (const u64 *)out->clock;
+  q.out_entries = nullptr;
+  q.apply_ceiling = 0;
+  q.out_keep = out->def_keep;
+  q.out_members = (u64 *)out->def_keys;
+  return launch_deferred(ctx, in->def_off, q);
+}

@@ -157,3 +157,37 @@ def test_map_counter_empty_and_unsorted(gpu_ctx):
         pytest.skip("reversal did not unsort")
     with pytest.raises(ValueError, match="def_row"):
         _run(gpu_ctx, d)
+
+
+@pytest.mark.parametrize("W", [1, 2])
+def test_map_counter_remove_empties_last_actor(mcctx, W):
+    """A deferred remove empties an entry whose only dot is on the last actor (A = 5: lanes past A
+    hold copies of actor A-1, remove rows included), leaving a stale value behind; the next
+    replica re-adds the key, which must read as absent-then-added (value v2 forgotten by
+    we_deleted), not as a join with the stale value."""
+    A = 5
+
+    def cnt(dots):
+        g = O.GCounter()
+        g.inner = O.VClock(dots)
+        if W == 1:
+            return g
+        c = O.PNCounter()
+        c.p.inner = g.inner
+        c.n.inner = O.VClock({a: x + 1 for a, x in dots.items()})
+        return c
+
+    r0 = O.Map(O.GCounter if W == 1 else O.PNCounter)
+    r0.clock = O.VClock({4: 1})
+    r0.entries[0] = O.MapEntry(O.VClock({4: 1}), cnt({3: 7}))
+    r1 = O.Map(r0.vnew)
+    r1.deferred[O.VClock({4: 1, 0: 5})] = {0}
+    r2 = O.Map(r0.vnew)
+    r2.clock = O.VClock({0: 1, 1: 1})
+    r2.entries[0] = O.MapEntry(O.VClock({1: 1}), cnt({1: 3}))
+    maps = [r0, r1, r2]
+    exp = O.map_fold_objects(maps)
+    assert exp.entries[0].val == cnt({1: 3})
+    d = O.map_counter_to_dense(maps, 2, A, W)
+    res, kw = _run(mcctx, d)
+    _same(_got_maps(res, kw, 1)[0], exp)

@@ -1,0 +1,206 @@
+"""GPU parity: Map<K, Orswot<M>> lub_many (crdt_map_orswot_lub_many, round 4) against the oracle's
+left fold of Map::merge (map.rs:140-220) with Orswot::merge / forget (orswot.rs:81-183) as the
+value's: the reference's merge_error KAT (map.rs:435-494) folded both ways, op-replay replicas
+whose nested sets add and remove members with contexts that leave deferred removes at both
+levels, arbitrary dense states, several groups with a CSR pool, and an empty fold."""
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+from gpu_util import to_dev, to_host
+
+pytestmark = pytest.mark.gpu
+
+import crdts_gpu as cg  # noqa: E402
+
+
+def _run(ctx, d, G=1, off=None):
+    R = d["clock"].shape[0] // G
+    shp = lambda x: x.reshape((G, R) + x.shape[1:])  # noqa: E731
+    D = d["def_row"].shape[0]
+    kw = {}
+    if D:
+        kw = dict(def_off=off if off is not None else [0, D],
+                  def_row=torch.from_numpy(np.asarray(d["def_row"], np.int64).astype(np.int32)).cuda(),
+                  def_clock=to_dev(d["def_clock"]), def_keys=to_dev(d["def_keys"]))
+    Dv = int(d["vd_off"][-1])
+    vkw = dict(vd_clock=to_dev(d["vd_clock"]), vd_mem=to_dev(d["vd_members"])) if Dv else {}
+    res = cg.map.orswot_lub_many(to_dev(shp(d["clock"])), to_dev(shp(d["ec"])), to_dev(shp(d["oc"])),
+                                 to_dev(shp(d["ent"])), to_dev(d["vd_off"]), ctx=ctx, **vkw, **kw)
+    return res, kw
+
+
+def _got_maps(res, kw, G):
+    out = []
+    c, e, o, m = to_host(res.clock), to_host(res.ec), to_host(res.oc), to_host(res.ent)
+    vn = res.vd_n.cpu().numpy().reshape(G, -1)
+    vc, vm = to_host(res.vd_clock), to_host(res.vd_mem)
+    if c.ndim == 1:
+        c, e, o, m, vc, vm = c[None], e[None], o[None], m[None], vc[None], vm[None]
+    for g in range(G):
+        dset = set()
+        if kw:
+            off = kw["def_off"]
+            dset = cg.map.deferred_set(kw["def_clock"], res.def_keep, res.def_keys, int(off[g]), int(off[g + 1]))
+        vd = {k: [(vc[g, k, i], O.bitmap_members(vm[g, k, i:i + 1])) for i in range(int(vn[g, k]))]
+              for k in range(e.shape[1])}
+        out.append(O.dense_to_map_orswot(c[g], e[g], o[g], m[g], vd,
+                                         [(np.array(rm, np.uint64), ks) for rm, ks in dset]))
+    return out
+
+
+def _same(got, exp):
+    assert got.clock == exp.clock
+    assert got.entries == exp.entries
+    assert got.deferred == exp.deferred
+
+
+def _intern(maps):
+    """Dense indices for the KAT's u8 actors / keys / members."""
+    acts, keys, mems = set(), set(), set()
+    for m in maps:
+        acts |= set(m.clock.dots)
+        for k, e in m.entries.items():
+            keys.add(k)
+            acts |= set(e.clock.dots) | set(e.val.clock.dots)
+            for mem, mc in e.val.entries.items():
+                mems.add(mem)
+                acts |= set(mc.dots)
+    ai = {a: i for i, a in enumerate(sorted(acts))}
+    ki = {k: i for i, k in enumerate(sorted(keys))}
+    mi = {x: i for i, x in enumerate(sorted(mems))}
+
+    def vc(c):
+        return O.VClock({ai[a]: n for a, n in c.dots.items()})
+
+    out = []
+    for m in maps:
+        n = O.Map(O.Orswot)
+        n.clock = vc(m.clock)
+        for k, e in m.entries.items():
+            o = O.Orswot()
+            o.clock = vc(e.val.clock)
+            o.entries = {mi[x]: vc(c) for x, c in e.val.entries.items()}
+            n.entries[ki[k]] = O.MapEntry(vc(e.clock), o)
+        out.append(n)
+    return out, len(ai), len(ki), len(mi)
+
+
+def test_map_orswot_merge_error_kat(gpu_ctx):
+    """map.rs:435-494: m1 (clock {75: 1}) merged with m2 (key 101 -> Orswot {1: {75: 1}, 2: {93: 1}})
+    keeps only member 2 under entry clock {93: 1}; folded as [m1, m2] and as [m2, m1]."""
+    def vc(*ds):
+        return O.VClock({a: c for a, c in ds})
+
+    m1 = O.Map(O.Orswot)
+    m1.clock = vc((75, 1))
+    m2 = O.Map(O.Orswot)
+    m2.clock = vc((75, 1), (93, 1))
+    o = O.Orswot()
+    o.clock = vc((75, 1), (93, 1))
+    o.entries = {1: vc((75, 1)), 2: vc((93, 1))}
+    m2.entries = {101: O.MapEntry(vc((75, 1), (93, 1)), o)}
+    (d1, d2), A, K, M = _intern([m1, m2])
+    for maps in ([d1, d2], [d2, d1]):
+        exp = O.map_fold_objects(maps)
+        d = O.map_orswot_to_dense(maps, K, M, A)
+        res, kw = _run(gpu_ctx, d)
+        got = _got_maps(res, kw, 1)[0]
+        _same(got, exp)
+    # the KAT's expected state, in interned form: actor 93 -> 1, member 2 -> 1
+    assert got.entries[0].clock == O.VClock({1: 1})
+    assert got.entries[0].val.entries == {1: O.VClock({1: 1})}
+
+
+@pytest.mark.parametrize("seed,R,K,M,A", [(1, 40, 4, 5, 4), (2, 60, 6, 8, 5), (3, 30, 3, 12, 6),
+                                           (4, 80, 8, 3, 8), (5, 50, 5, 32, 3)])
+def test_map_orswot_op_replay(gpu_ctx, seed, R, K, M, A):
+    maps = O.map_orswot_objects(R, K, M, A, seed=seed, steps=7 * R)
+    exp = O.map_fold_objects(maps)
+    d = O.map_orswot_to_dense(maps, K, M, A)
+    res, kw = _run(gpu_ctx, d)
+    assert int(res.flags.cpu()[0]) == 0
+    _same(_got_maps(res, kw, 1)[0], exp)
+
+
+def test_map_orswot_nested_deferred_survive(gpu_ctx):
+    """Enough op-replay histories that some folds end with nested deferred removes."""
+    n = 0
+    for seed in range(10, 22):
+        maps = O.map_orswot_objects(30, 3, 6, 4, seed=seed, steps=220, p_vrm=0.5)
+        exp = O.map_fold_objects(maps)
+        n += sum(len(e.val.deferred) for e in exp.entries.values())
+        d = O.map_orswot_to_dense(maps, 3, 6, 4)
+        res, kw = _run(gpu_ctx, d)
+        _same(_got_maps(res, kw, 1)[0], exp)
+    assert n > 0
+
+
+def _arbitrary(rng, R, K, M, A, cmax):
+    maps = []
+    for _ in range(R):
+        m = O.Map(O.Orswot)
+        m.clock = O.VClock({a: int(x) for a, x in enumerate(rng.integers(0, cmax + 1, A)) if x})
+        for k in range(K):
+            if rng.random() < 0.6:
+                ec = {a: int(x) for a, x in enumerate(rng.integers(0, cmax + 2, A)) if x and rng.random() < 0.5}
+                if not ec:
+                    continue
+                o = O.Orswot()
+                o.clock = O.VClock({a: int(x) for a, x in enumerate(rng.integers(0, cmax + 2, A)) if x})
+                for mem in range(M):
+                    if rng.random() < 0.5:
+                        dots = {a: int(x) for a, x in enumerate(rng.integers(0, cmax + 2, A)) if x and rng.random() < 0.5}
+                        if dots:
+                            o.entries[mem] = O.VClock(dots)
+                for _ in range(int(rng.integers(0, 3))):
+                    rm = {a: int(x) for a, x in enumerate(rng.integers(0, cmax + 3, A)) if x and rng.random() < 0.4}
+                    if rm:
+                        o.deferred[O.VClock(rm)] = set(int(x) for x in rng.choice(M, size=int(rng.integers(1, M + 1)),
+                                                                                    replace=False))
+                m.entries[k] = O.MapEntry(O.VClock(ec), o)
+        for _ in range(int(rng.integers(0, 2))):
+            rm = {a: int(x) for a, x in enumerate(rng.integers(0, cmax + 3, A)) if x and rng.random() < 0.4}
+            if rm:
+                m.deferred[O.VClock(rm)] = set(int(x) for x in rng.choice(K, size=int(rng.integers(1, K + 1)),
+                                                                            replace=False))
+        maps.append(m)
+    return maps
+
+
+@pytest.mark.parametrize("seed,R,K,M,A,cmax", [(21, 20, 3, 4, 5, 3), (22, 30, 4, 6, 3, 4), (23, 12, 2, 9, 64, 3),
+                                                (24, 25, 5, 2, 7, 2)])
+def test_map_orswot_arbitrary(gpu_ctx, seed, R, K, M, A, cmax):
+    rng = np.random.default_rng(seed)
+    maps = _arbitrary(rng, R, K, M, A, cmax)
+    exp = O.map_fold_objects(maps)
+    if any(len(e.val.deferred) > cg.map.VD_CAP for e in exp.entries.values()):
+        pytest.skip("nested deferred past the kernel's capacity")
+    d = O.map_orswot_to_dense(maps, K, M, A)
+    res, kw = _run(gpu_ctx, d)
+    _same(_got_maps(res, kw, 1)[0], exp)
+
+
+def test_map_orswot_groups(gpu_ctx):
+    """G = 3 groups of one launch: the value CSR spans the groups, the Map pool has CSR offsets."""
+    G, R, K, M, A = 3, 25, 4, 5, 4
+    parts = [O.map_orswot_objects(R, K, M, A, seed=60 + g, steps=180) for g in range(G)]
+    allm = [m for p in parts for m in p]
+    d = O.map_orswot_to_dense(allm, K, M, A)
+    d["def_row"] = d["def_row"] % R  # (rows within the group)
+    off = [0]
+    for p in parts:
+        off.append(off[-1] + sum(len(m.deferred) for m in p))
+    res, kw = _run(gpu_ctx, d, G=G, off=off)
+    got = _got_maps(res, kw, G)
+    for g in range(G):
+        _same(got[g], O.map_fold_objects(parts[g]))
+
+
+def test_map_orswot_empty(gpu_ctx):
+    """R = 0 folds to Map::new()."""
+    z = lambda *s: torch.zeros(s, dtype=torch.int64, device="cuda:0")  # noqa: E731
+    res = cg.map.orswot_lub_many(z(2, 0, 4), z(2, 0, 3, 4), z(2, 0, 3, 4), z(2, 0, 3, 5, 4), z(1), ctx=gpu_ctx)
+    assert not to_host(res.clock).any() and not to_host(res.ec).any() and not to_host(res.ent).any()
+    assert not res.vd_n.cpu().numpy().any()
