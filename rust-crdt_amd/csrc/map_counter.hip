@@ -220,9 +220,9 @@ __global__ __launch_bounds__(kMcWaves * kWave) void map_counter_fold_kernel(MapC
     const bool p1 = mc_nz<APL>(e, hm), p2 = mc_nz<APL>(e2, hm);
 #pragma unroll
     for (int j = 0; j < APL; ++j) {
-      const u64 t0 = e[j] == e2[j] ? e[j] : 0, t1 = e2[j] > C[j] ? e2[j] : 0, t2 = e[j] > c2[j] ? e[j] : 0;
-      const u64 t = t0 > t1 ? t0 : t1;
-      const u64 en = t > t2 ? t : t2;
+      // (where e == e2 the common clock is e itself: the two forgets are at most e there)
+      const u64 t1 = e2[j] > C[j] ? e2[j] : 0, t2 = e[j] > c2[j] ? e[j] : 0;
+      const u64 en = e[j] == e2[j] ? e[j] : (t1 > t2 ? t1 : t2);
       const u64 mx = e[j] > e2[j] ? e[j] : e2[j];
       const u64 y = p1 ? (p2 ? mx : c2[j]) : C[j];
       const u64 x = y > en ? y : 0;

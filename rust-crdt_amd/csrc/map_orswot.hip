@@ -190,14 +190,13 @@ __global__ __launch_bounds__(kMoWaves * kWave) void map_orswot_fold_kernel(MapOr
   // one replica step
   auto step = [&](unsigned long long r, u64 c2, u64 e2, u64 o2, const u64 (&E2)[MT], u64 vlo, u64 vhi) {
     const bool p1 = mo_nz(e), p2 = mo_nz(e2);
-    const u64 t0 = e == e2 ? e : 0, t1 = mo_fg(e2, C), t2 = mo_fg(e, c2);
-    const u64 en = mo_max(mo_max(t0, t1), t2);
+    const u64 en = e == e2 ? e : mo_max(mo_fg(e2, C), mo_fg(e, c2));  // (the forgets are <= e where e == e2)
     const u64 y = p1 ? (p2 ? mo_max(e, e2) : c2) : C;
     const u64 X = mo_fg(y, en);
     if (p1 && p2) {  // our_entry.val.merge(entry.val) (map.rs:183) = Orswot::merge
 #pragma unroll
       for (int m = 0; m < MT; ++m)
-        E[m] = mo_max(mo_max(E[m] == E2[m] ? E[m] : 0, mo_fg(E2[m], oc)), mo_fg(E[m], o2));
+        E[m] = E[m] == E2[m] ? E[m] : mo_max(mo_fg(E2[m], oc), mo_fg(E[m], o2));
       for (u64 d = vlo; d < vhi; ++d) {
         const u64 rm = ld(p.vd_clock + d * A), msk = p.vd_mem[d];
         vd_add(rm, msk);
