@@ -100,8 +100,8 @@ struct Tune {
   int orswot_apply_hpf = 0;    // Orswot apply (16-lane groups): the next op batch's fields / first members loaded
                                //     while the current batch runs (opt-in: 2 VGPRs spill, 878 vs 856 us, profiles/r04_oapply_hpf_ab.log)
   int map_counter_dma = 0;     // Map<K, counter> fold: LDS-DMA ring slots (8 or 16; 0: register ring, 8.7 vs 9.1 ms)
-  int map_counter_depth = 8;   // Map<K, counter> fold: register-ring depth at A <= 64 (4, 8, 16)
-  int map_counter_kpw = 1;     // Map<K, counter> fold: at most this many keys per wave (1, 2, 4; A <= 64 / KPW)
+  int map_counter_depth = 8;   // Map<K, counter> fold: register-ring depth at A <= 64 (4, 8, 16; 16: 4.86 vs 4.33 ms)
+  int map_counter_kpw = 0;     // Map<K, counter> fold: keys per wave (1, 2, 4; A <= 64 / KPW; 0: automatic)
   int map_apply_pf = 1;        // Map apply (16-lane groups): the next op's entry-clock row prefetched with its
                                //     Put / rm clock; absent keys skip their value rows (0: round-3 form;
                                //     1.28 vs 1.81 ms, profiles/r04_map_apply_pf_ab.log)

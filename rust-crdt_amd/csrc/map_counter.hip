@@ -489,7 +489,16 @@ extern "C" int crdt_map_counter_lub_many(crdt_ctx *ctx, const crdt_map_counter_b
     const bool al = ((p.c_rs | p.c_gs | p.e_rs | p.e_gs | p.v_rs | p.v_gs) & 1) == 0 &&
                     ((uintptr_t)in->clock & 15) == 0 && ((uintptr_t)in->ec & 15) == 0 && ((uintptr_t)in->val & 15) == 0;
     const int ring = A % 2 == 0 && (2 + W) * A <= 128 && al ? ctx->tune.map_counter_dma : 0;
-    const int kpw = ctx->tune.map_counter_kpw;
+    // keys per wave: explicit (mckpw=1/2/4), or automatic (0): pair keys in a wave only while the
+    // paired grid still has 2,048+ waves (2 per SIMD) — at 4,096 keys x 4,096 replicas two keys per
+    // wave ran 1.60 vs 2.52 ms, at 1,024 keys (one wave per SIMD) 5.33 vs 5.03 ms
+    int kpw = ctx->tune.map_counter_kpw;
+    if (kpw == 0) {
+      const size_t waves_per_simd2 = 2048;
+      kpw = A <= (size_t)kWave / 4 && G * ((K + 3) / 4) >= waves_per_simd2   ? 4
+            : A <= (size_t)kWave / 2 && G * ((K + 1) / 2) >= waves_per_simd2 ? 2
+                                                                                : 1;
+    }
     if (!ring && kpw >= 4 && A <= (size_t)kWave / 4)
       he = W == 1 ? launch_mc<1, 1, 0, 4>(p, ctx->stream) : launch_mc<1, 2, 0, 4>(p, ctx->stream);
     else if (!ring && kpw >= 2 && A <= (size_t)kWave / 2)

@@ -17,9 +17,10 @@ pytestmark = pytest.mark.gpu
 import crdts_gpu as cg  # noqa: E402
 
 
-@pytest.fixture(params=["mckpw=1", "mckpw=2", "mckpw=4", "mcdma=8", "mcdma=16"])
+@pytest.fixture(params=["mckpw=0", "mckpw=1", "mckpw=2", "mckpw=4", "mcdma=8", "mcdma=16"])
 def mcctx(request):
-    """The register ring with 1 (the default), up to 2 or up to 4 keys per wave (A <= 64 / keys), or
+    """The register ring with keys per wave chosen by the grid size (mckpw=0, the default), 1, up to 2
+    or up to 4 keys per wave (A <= 64 / keys), or
     the replica rows by LDS-DMA into an 8- or 16-slot LDS ring (A even, (2+W)*A <= 128; one key
     per wave).  Shapes outside a mode's bound take the one-key register ring."""
     assert torch.cuda.is_available()
