@@ -51,7 +51,7 @@ __device__ __forceinline__ u64 mo_max(u64 x, u64 y) { return x > y ? x : y; }
 
 template <int MT>
 __global__ __launch_bounds__(kMoWaves * kWave) void map_orswot_fold_kernel(MapOrswotPlan p) {
-  constexpr int DEPTH = MT <= 8 ? 4 : 2;  // replica steps in flight (register ring)
+  constexpr int DEPTH = MT <= 4 ? 8 : (MT <= 8 ? 4 : 2);  // replica steps in flight (register ring)
   extern __shared__ u64 lds[];
   const int lane = (int)(threadIdx.x % kWave), wv = (int)(threadIdx.x / kWave);
   const unsigned long long gk = (unsigned long long)blockIdx.x * kMoWaves + wv;
@@ -394,7 +394,10 @@ extern "C" int crdt_map_orswot_lub_many(crdt_ctx *ctx, const crdt_map_orswot_bat
       p.def_off = reinterpret_cast<const size_t *>(ctx->scratch);
     }
     timing_begin(ctx, "map_orswot_fold");
-    const hipError_t he = M <= 8 ? launch_mo<8>(p, ctx->stream) : launch_mo<32>(p, ctx->stream);
+    // (member rows past M are zero and still joined: the register capacity follows M)
+    const hipError_t he = M <= 4   ? launch_mo<4>(p, ctx->stream)
+                          : M <= 8 ? launch_mo<8>(p, ctx->stream)
+                                   : launch_mo<32>(p, ctx->stream);
     timing_end(ctx);
     if (he != hipSuccess) return hip_fail(ctx, he, "map_orswot_fold_kernel launch");
   }
