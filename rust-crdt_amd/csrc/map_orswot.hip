@@ -277,7 +277,7 @@ __global__ __launch_bounds__(kMoWaves * kWave) void map_orswot_fold_kernel(MapOr
   const unsigned long long rsK = K * A, rsM = K * M * A;
   u64 c2r[DEPTH], e2r[DEPTH], o2r[DEPTH], E2r[DEPTH][MT], vlr[DEPTH], vhr[DEPTH];
   unsigned long long nload = 0;
-  auto load_step = [&](int s) {
+  auto load_step = [&](int s, bool last_check) {
     c2r[s] = ld(pc);
     e2r[s] = ld(pe);
     o2r[s] = ld(po);
@@ -285,27 +285,36 @@ __global__ __launch_bounds__(kMoWaves * kWave) void map_orswot_fold_kernel(MapOr
     for (int m = 0; m < MT; ++m) E2r[s][m] = (unsigned long long)m < M ? ld(pm + m * A) : 0ull;
     vlr[s] = pvo[0];
     vhr[s] = pvo[1];
-    if (++nload < R) {
+    if (!last_check || nload + 1 < R) {
       pc += A;
       pe += rsK;
       po += rsK;
       pm += rsM;
       pvo += K;
     }
+    ++nload;
+  };
+  auto run = [&](unsigned long long r, int s, bool last_check) {
+    const u64 vlo = __builtin_amdgcn_readfirstlane((unsigned)vlr[s]) |
+                    ((u64)__builtin_amdgcn_readfirstlane((unsigned)(vlr[s] >> 32)) << 32);
+    const u64 vhi = __builtin_amdgcn_readfirstlane((unsigned)vhr[s]) |
+                    ((u64)__builtin_amdgcn_readfirstlane((unsigned)(vhr[s] >> 32)) << 32);
+    step(r, c2r[s], e2r[s], o2r[s], E2r[s], vlo, vhi);
+    load_step(s, last_check);
   };
 #pragma unroll
-  for (int s = 0; s < DEPTH; ++s) load_step(s);
-  for (unsigned long long r0 = 0; r0 < R; r0 += DEPTH) {
+  for (int s = 0; s < DEPTH; ++s) load_step(s, true);
+  unsigned long long r0 = 0;
+  // blocks whose loads (rows r0 + DEPTH .. r0 + 2 DEPTH - 1) all have a next row: no clamp
+  for (; r0 + 2 * DEPTH < R; r0 += DEPTH) {
+#pragma unroll
+    for (int s = 0; s < DEPTH; ++s) run(r0 + s, s, false);
+  }
+  for (; r0 < R; r0 += DEPTH) {
 #pragma unroll
     for (int s = 0; s < DEPTH; ++s) {
-      const unsigned long long r = r0 + s;
-      if (r >= R) break;
-      const u64 vlo = __builtin_amdgcn_readfirstlane((unsigned)vlr[s]) |
-                      ((u64)__builtin_amdgcn_readfirstlane((unsigned)(vlr[s] >> 32)) << 32);
-      const u64 vhi = __builtin_amdgcn_readfirstlane((unsigned)vhr[s]) |
-                      ((u64)__builtin_amdgcn_readfirstlane((unsigned)(vhr[s] >> 32)) << 32);
-      step(r, c2r[s], e2r[s], o2r[s], E2r[s], vlo, vhi);
-      load_step(s);
+      if (r0 + s >= R) break;
+      run(r0 + s, s, true);
     }
   }
 
