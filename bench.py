@@ -9,6 +9,13 @@ config 5 (the `c5` block of the same line).
 one GPU's shard of config 5, VClock lub_many of 1,048,576 replicas x 1,024 actors (8 GiB read; at
 --gpus 8 the global input is config 5's 8M replicas and the exchange its RCCL max all-reduce).
 --workload c5: config 5 as the headline instead (no second block).
+At N = 1 the line also carries `c3` and `c4` blocks (--no-c3 / --no-c4 drop them): BASELINE config 3,
+Orswot<u64, u32> lub_many of 65,536 replicas x 4,096 members x 64 actors with deferred removes (128 GiB
+of entries), and config 4, Map<u32, MVReg<u64>> lub_many of 16,384 replicas x 1,024 keys x 32 actors,
+V = 2 (12.25 GiB), both generated in HBM; one step = one whole lub_many (every kernel of it), the
+roofline is its dominant kernel (orswot_join_kernel / map_fold_kernel), and the oracle leg (rank 0,
+N = 1) checks the result on a member / key sample and times the restated reference fold on a replica
+subsample.
 
 --gpus N > 1: one process per GPU.  Started without WORLD_SIZE, the script starts its own
 `python -m torch.distributed.run --nproc-per-node N` child BEFORE touching the GPU, relays rank 0's
@@ -70,17 +77,50 @@ def parse():
                          "host callbacks (crdt_ctx_comm_init_ops), or the torch.distributed twin")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL on ROCm) for real runs; gloo lets several ranks share one GPU in tests")
+    ap.add_argument("--c3", action=argparse.BooleanOptionalAction, default=None,
+                    help="also time BASELINE config 3 (Orswot 65,536 x 4,096 x 64 with deferred removes) in a "
+                         "`c3` block; default on at N = 1")
+    ap.add_argument("--c4", action=argparse.BooleanOptionalAction, default=None,
+                    help="also time BASELINE config 4 (Map<u32, MVReg<u64>> 16,384 x 1,024 x 32, V = 2) in a "
+                         "`c4` block; default on at N = 1")
+    ap.add_argument("--causal-steps", type=int, default=5, help="timed lub_many calls of the c3 / c4 blocks")
+    ap.add_argument("--parity-seed", type=int, default=1, help="member / key sample of the c3 / c4 parity checks")
+    ap.add_argument("--parity-members", type=int, default=16)
+    ap.add_argument("--parity-keys", type=int, default=16)
+    ap.add_argument("--c3-cpu-replicas", type=int, default=1024, help="replicas of the c3 CPU baseline sample")
+    ap.add_argument("--c4-cpu-replicas", type=int, default=4096, help="replicas of the c4 CPU baseline sample")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="PMC-derived HBM bytes per launch (written by profiles/collect.sh)")
     return ap.parse_args()
 
 
-def kernel_source_sha():
-    """sha256 of the source of the bench's dominant kernel (lub_multi_kernel, csrc/lattice.hip): a
-    PMC traffic figure is reported only for the kernel source it was measured on."""
+KERNEL_SOURCES = {"c2": "lattice.hip", "c5": "lattice.hip", "c3": "orswot.hip", "c4": "map.hip"}
+
+
+def kernel_source_sha(block="c2"):
+    """sha256 of the source of a block's dominant kernel (c2 / c5: lub_multi_kernel /
+    lub_stream_kernel, csrc/lattice.hip; c3: orswot_join_kernel, csrc/orswot.hip; c4:
+    map_fold_kernel, csrc/map.hip): a PMC traffic figure is reported only for the kernel source it
+    was measured on."""
     import hashlib
-    with open(os.path.join(ROOT, "rust-crdt_amd", "csrc", "lattice.hip"), "rb") as f:
+    with open(os.path.join(ROOT, "rust-crdt_amd", "csrc", KERNEL_SOURCES[block]), "rb") as f:
         return hashlib.sha256(f.read()).hexdigest()
+
+
+def pmc_traffic(args, block, workload):
+    """(hbm bytes per launch, source note) from profiles/pmc_traffic.json — one entry per block,
+    used only when the entry's workload and kernel source sha256 match this run."""
+    try:
+        with open(args.traffic_json) as f:
+            tj = json.load(f)
+    except (OSError, ValueError):
+        return None, "not collected for this kernel source (profiles/collect.sh writes it)"
+    e = tj.get(block) if isinstance(tj.get(block), dict) else None
+    if e and e.get("workload") == workload and e.get("kernel_source_sha256") == kernel_source_sha(block):
+        return e.get("hbm_bytes_per_launch"), (
+            f"{e.get('source')}: rocprofv3 FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE per launch of "
+            f"{e.get('kernel')}, separate --pmc passes, same kernel source (sha256 of csrc/{KERNEL_SOURCES[block]})")
+    return None, "not collected for this kernel source (profiles/collect.sh writes it)"
 
 
 def free_port():
@@ -339,17 +379,9 @@ def run_workload(args, env, workload):
     srt = sorted(step_ms)
     med = srt[len(srt) // 2] if len(srt) % 2 else 0.5 * (srt[len(srt) // 2 - 1] + srt[len(srt) // 2])
     name = (f"vclock lub {R}x{A} (config 5 shard)" if workload == "c5" else f"gcounter+pncounter lub {R}x{A}")
-    traffic, traffic_src = None, "not collected for this kernel source (profiles/collect.sh writes it)"
-    try:
-        with open(args.traffic_json) as f:
-            tj = json.load(f)
-        if (tj.get("workload") == name and tj.get("fused", False) == bool(fused)
-                and tj.get("kernel_source_sha256") == kernel_source_sha()):
-            traffic = tj.get("hbm_bytes_per_launch")
-            traffic_src = (f"{tj.get('source')}: rocprofv3 FETCH_SIZE x 2 (gfx950 correction) + WRITE_SIZE per "
-                           "launch, separate --pmc passes, same kernel source (sha256 of csrc/lattice.hip)")
-    except (OSError, ValueError):
-        pass
+    traffic, traffic_src = pmc_traffic(args, workload, name)
+    if workload == "c2" and not fused:
+        traffic, traffic_src = None, "collected for the fused launch only"
     if env.cabi:
         exch = ((f"C-ABI crdt_lub_many_multi_sharded: one grouped all-reduce MAX " if fused
                  else "C-ABI crdt_*_lub_many_sharded: all-reduce MAX ")
@@ -405,6 +437,203 @@ def run_workload(args, env, workload):
     return block, A
 
 
+C3 = dict(R=65536, M=4096, A=64, kmax=48, p_def=0.1, seed=0x5EED0003)
+C4 = dict(R=16384, K=1024, A=32, V=2, kmax=256, p_def=0.1, seed=0x5EED0004, vout=4)
+
+
+def c3_oracle_leg(args, inp, res, ctx):
+    """BASELINE config 3 through the oracle (the checker; rank 0, N = 1 only).
+
+    parity   the oracle's dense Orswot fold (join fold, then every deferred remove; cross-checked
+             against the map-based restatement in tests/test_oracle_twins.py) over EVERY replica
+             restricted to a member sample — the merge is independent per member given the clocks
+             (orswot.rs:81-149) — plus every surviving deferred remove with its whole member set.
+    baseline the map-based restatement of Orswot::merge (oracle/ref_fold.cpp, orswot.rs:81-149)
+             folding the first replicas of the same HBM input with all members, one thread."""
+    import numpy as np
+    import torch
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    u64 = lambda t: t.cpu().numpy().view(np.uint64)  # noqa: E731
+    R, M, A = C3["R"], C3["M"], C3["A"]
+    msub = np.sort(np.random.default_rng(args.parity_seed).choice(M, size=args.parity_members, replace=False))
+    tsub = torch.from_numpy(msub).cuda()
+    clock_h, ent_h = u64(inp.clock), u64(inp.entries[:, tsub, :].contiguous())
+    dcl_h, dmem_h = u64(inp.def_clock), u64(inp.def_members)
+    got_c, got_e = u64(res.clock), u64(res.entries[tsub])
+    keep, gmem = res.def_keep.cpu().numpy(), u64(res.def_members)
+    D = dcl_h.shape[0]
+    sub_mem = np.zeros((D, (len(msub) + 63) // 64), np.uint64)
+    for j, m in enumerate(msub):
+        sub_mem[:, j // 64] |= ((dmem_h[:, m // 64] >> np.uint64(m % 64)) & np.uint64(1)) << np.uint64(j % 64)
+    t0 = time.time()
+    oc, oe, _ = O.dense_orswot_lub(clock_h, ent_h, dcl_h, sub_mem)
+    exp_def = O.dense_orswot_survivors(oc, dcl_h, dmem_h)
+    got_def = {(tuple(int(x) for x in dcl_h[d]), O.bitmap_members(gmem[d])) for d in np.flatnonzero(keep)}
+    ok = bool(np.array_equal(got_c, oc) and np.array_equal(got_e, oe) and got_def == exp_def)
+    check_s = time.time() - t0
+    parity = {"result": "ok" if ok else "MISMATCH",
+              "method": (f"oracle dense Orswot fold over all {R} replicas on {len(msub)} sampled members (seed "
+                         f"{args.parity_seed}) + all {len(exp_def)} surviving deferred removes with whole member "
+                         f"sets ({D} removes in the input)"), "check_s": check_s}
+    # CPU baseline: the map-based fold of the first Rc replicas (all members), their own removes
+    Rc = min(R, args.c3_cpu_replicas)
+    off = np.asarray(inp.def_off, np.int64)  # per-replica CSR offsets (R + 1) of the generator
+    dend = int(off[Rc])
+    c_h = u64(inp.clock[:Rc])
+    e_h = u64(inp.entries[:Rc])
+    d_off = off[:Rc + 1].astype(np.uint64)
+    _, _, _, fold_s = O.orswot_fold(c_h, e_h, d_off, dcl_h[:dend], dmem_h[:dend])
+    del e_h
+    base = {"value": Rc / fold_s, "unit": "replica-merges/s", "cores": 1, "kind": "port",
+            "sample": (f"first {Rc} of the {R} replicas (all {M} members x {A} actors, their {dend} deferred "
+                       f"removes), left fold of the restated Orswot::merge over std::unordered_map / std::map "
+                       f"states (oracle/ref_fold.cpp), 1 thread, ingest excluded; {fold_s:.2f} s of fold")}
+    return parity, base
+
+
+def c4_oracle_leg(args, inp, res, ctx):
+    """BASELINE config 4 through the oracle (the checker; rank 0, N = 1 only).
+
+    parity   the restated Map::merge fold over map-based states (oracle/ref_fold.cpp,
+             map.rs:140-220) over EVERY replica restricted to a key sample (keys are independent
+             given the replica clocks and the deferred list), plus the surviving removes restricted
+             to the sample.
+    baseline the same restated fold over the first replicas with all keys, one thread."""
+    import numpy as np
+    import torch
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    u64 = lambda t: t.cpu().numpy().view(np.uint64)  # noqa: E731
+    R, K, A, V, vout = C4["R"], C4["K"], C4["A"], C4["V"], C4["vout"]
+    keys = np.sort(np.random.default_rng(args.parity_seed).choice(K, size=args.parity_keys, replace=False))
+    tk = torch.from_numpy(keys).cuda()
+    clock_h = u64(inp.clock)
+    ec_h, vc_h, vv_h = (u64(t[:, tk].contiguous()) for t in (inp.ec, inp.vclk, inp.vval))
+    rows = inp.def_row.cpu().numpy().astype(np.int64)
+    dcl_h, dks_h = u64(inp.def_clock), u64(inp.def_keys)
+    t0 = time.time()
+    exp = O.map_fold(clock_h, ec_h, vc_h, vv_h, rows, dcl_h, O.restrict_deferred_keys(dks_h, keys), vout)
+    ok = (np.array_equal(u64(res.clock), exp[0]) and np.array_equal(u64(res.ec)[keys], exp[1])
+          and np.array_equal(u64(res.vclk)[keys], exp[2]) and np.array_equal(u64(res.vval)[keys], exp[3])
+          and np.array_equal(res.nval.cpu().numpy()[keys], exp[4]) and int(res.flags.max()) == 0)
+    pos = {int(k): i for i, k in enumerate(keys)}
+    gk = u64(res.def_keys)
+    got_sub = set()
+    for j in np.flatnonzero(res.def_keep.cpu().numpy()):
+        s = frozenset(pos[k] for k in O.bitmap_members(gk[j]) if k in pos)
+        if s:
+            got_sub.add((tuple(int(x) for x in dcl_h[j]), s))
+    ok = bool(ok and got_sub == {x for x in exp[5] if x[1]})
+    parity = {"result": "ok" if ok else "MISMATCH",
+              "method": (f"restated Map::merge fold (oracle/ref_fold.cpp) over all {R} replicas on {len(keys)} "
+                         f"sampled keys (seed {args.parity_seed}), incl. the surviving removes restricted to them"),
+              "check_s": time.time() - t0}
+    Rc = min(R, args.c4_cpu_replicas)
+    sel = rows < Rc
+    e_h = [u64(t[:Rc]) for t in (inp.clock, inp.ec, inp.vclk, inp.vval)]
+    fold_s = O.map_fold(*e_h, rows[sel], dcl_h[sel], dks_h[sel], vout)[6]
+    base = {"value": Rc / fold_s, "unit": "replica-merges/s", "cores": 1, "kind": "port",
+            "sample": (f"first {Rc} of the {R} replicas (all {K} keys, {int(sel.sum())} deferred removes), left "
+                       f"fold of the restated Map::merge over std::map states (oracle/ref_fold.cpp), 1 thread, "
+                       f"ingest excluded; {fold_s:.2f} s of fold")}
+    return parity, base
+
+
+def run_causal(args, env, block):
+    """BASELINE config 3 (Orswot) or 4 (Map<u32, MVReg<u64>>) at full size on this GPU: generate the
+    replicas in HBM, time args.steps lub_many calls (one step = one fold of every replica), report
+    the dominant kernel's roofline, and (rank 0, N = 1) the oracle's parity check and CPU baseline."""
+    torch, cg = env.torch, env.cg
+    from crdts_gpu import synth
+    ctx = env.ctx
+    if block == "c3":
+        p = C3
+        inp = synth.orswot_replicas(ctx, p["R"], p["M"], p["A"], seed=p["seed"], kmax=p["kmax"], p_def=p["p_def"])
+        D = inp.def_clock.shape[0]
+        goff = [0, D]
+
+        def step():
+            return cg.orswot.lub_many(inp.clock, inp.entries, def_off=goff, def_clock=inp.def_clock,
+                                      def_members=inp.def_members, ctx=ctx)
+        R = p["R"]
+        name = f"orswot<u64,u32> lub {R}x{p['M']}x{p['A']} (config 3)"
+        timer, kernel = "orswot_join", "orswot_join_kernel"
+        alg = (R + 1) * (p["M"] * p["A"] + p["A"]) * 8
+        alg_note = "8·(M·A + A) per replica read + the (M·A + A) u64 output"
+        cfg = {"replicas": R, "members": p["M"], "actors": p["A"], "deferred_removes": D,
+               "types": ["Orswot<u64 member, u32 actor>"]}
+    else:
+        p = C4
+        inp = synth.map_replicas(ctx, p["R"], p["K"], p["A"], p["V"], p["seed"], kmax=p["kmax"], p_def=p["p_def"])
+        D = inp.def_clock.shape[0]
+
+        def step():
+            return cg.map.lub_many(inp.clock, inp.ec, inp.vclk, inp.vval, def_off=inp.def_off,
+                                   def_row=inp.def_row, def_clock=inp.def_clock, def_keys=inp.def_keys,
+                                   vout=p["vout"], ctx=ctx, check=False)
+        R, K, A, V, vout = p["R"], p["K"], p["A"], p["V"], p["vout"]
+        Kw = (K + 63) // 64
+        name = f"map<u32,mvreg<u64>> lub {R}x{K}x{A} V={V} (config 4)"
+        timer, kernel = "map_fold", "map_fold_kernel"
+        alg = (R * (K * (A * 8 + V * A * 8 + V * 8) + A * 8) + D * (A + Kw + 1) * 8
+               + K * (A + vout * A + vout) * 8 + A * 8)
+        alg_note = ("8·(K·(A + V·A + V) + A) per replica read + 8·(A + Kw + 1) per deferred remove + the "
+                    "K·(A + Vout·A + Vout) + A u64 output")
+        cfg = {"replicas": R, "keys": K, "actors": A, "value_slots": V, "deferred_removes": D,
+               "types": ["Map<u32, MVReg<u64>>"]}
+    torch.cuda.synchronize()
+    res = None
+    for _ in range(args.warmup):
+        res = step()
+    torch.cuda.synchronize()
+    env.barrier()
+    ctx.timing_reset()
+    ctx.set_timing(True)
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.causal_steps + 1)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    evs[0].record()
+    for i in range(args.causal_steps):
+        res = step()
+        evs[i + 1].record()
+    torch.cuda.synchronize()
+    env.barrier()
+    elapsed = time.perf_counter() - t0
+    ctx.set_timing(False)
+    kern_ms, launches = ctx.timing(timer)
+    step_ms = env.max_over_ranks([evs[i].elapsed_time(evs[i + 1]) for i in range(args.causal_steps)])
+    elapsed = env.max_over_ranks([elapsed])[0]
+    srt = sorted(step_ms)
+    avg_launch_s = (kern_ms / 1e3) / launches if launches else float("nan")
+    achieved = alg / avg_launch_s / 1e9
+    traffic, traffic_src = pmc_traffic(args, block, name)
+    block_out = {
+        "metric": METRIC + (" — BASELINE config 3 (Orswot)" if block == "c3" else " — BASELINE config 4 (Map)"),
+        "value": R * env.world * args.causal_steps / elapsed,
+        "unit": "replica-merges/s",
+        "steps": args.causal_steps,
+        "ms_per_step": elapsed / args.causal_steps * 1e3,
+        "step_ms": {"median": srt[len(srt) // 2], "min": srt[0], "max": srt[-1],
+                    "source": "HIP events around each lub_many (all of its kernels), max over ranks"},
+        "config": dict(cfg, workload=name, parallelism="one GPU (replicas in HBM)"),
+        "roofline": {"bound": "hbm", "kernel": kernel, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                     "avg_launch_us": avg_launch_s * 1e6, "launches": launches,
+                     "algorithmic_bytes_per_launch": alg, "algorithmic_bytes_rule": alg_note},
+        "parity": {"result": "unchecked (the oracle leg runs at N = 1 without --no-cpu-baseline)"},
+        "cpu_baseline": None,
+    }
+    if env.world == 1 and env.rank == 0 and not args.no_cpu_baseline:
+        leg = c3_oracle_leg if block == "c3" else c4_oracle_leg
+        block_out["parity"], block_out["cpu_baseline"] = leg(args, inp, res, ctx)
+    del inp, res
+    torch.cuda.empty_cache()
+    return block_out
+
+
 def main():
     args = parse()
     world_env = os.environ.get("WORLD_SIZE")
@@ -420,7 +649,15 @@ def main():
     c5 = None
     if args.workload == "c2" and args.c5:
         c5, _ = run_workload(args, env, "c5")
-    ok = head["parity"] == "ok" and (c5 is None or c5["parity"] == "ok")
+    causal = {}
+    for blk in ("c3", "c4"):
+        on = getattr(args, blk)
+        if on is None:
+            on = env.world == 1
+        if on:
+            causal[blk] = run_causal(args, env, blk)
+    ok = (head["parity"] == "ok" and (c5 is None or c5["parity"] == "ok")
+          and all(b["parity"]["result"] != "MISMATCH" for b in causal.values()))
     if env.rank == 0:
         out = {
             "metric": METRIC,
@@ -447,6 +684,7 @@ def main():
             out["config"]["rccl_note"] = env.note
         if c5 is not None:
             out["c5"] = dict(c5, metric=METRIC + " — BASELINE config 5 (VClock 1,024 actors; 8M replicas at 8 GPUs)")
+        out.update(causal)
         if env.world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args, args.workload, A)
         print(json.dumps(out), flush=True)

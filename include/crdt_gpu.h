@@ -430,16 +430,20 @@ typedef struct crdt_comm_ops {
   int (*allreduce_u64)(void *user, uint64_t *buf, size_t n, int op);
 } crdt_comm_ops;
 int crdt_comm_unique_id(uint8_t *id /* [CRDT_UNIQUE_ID_BYTES] */);
-/* Collective.  Also compares the RCCL runtime's version (ncclGetVersion) with the rccl.h this
- * library was compiled against; a mismatch is not an error but is reported by crdt_ctx_comm_note. */
+/* Collective.  RCCL is bound at run time (dlopen + dlsym, csrc/shard.hip), from ONE librccl.so.1:
+ * $CRDT_RCCL_LIB when set, else the copy the process already has loaded (torch's own RCCL inside
+ * a torch process, so the library and torch.distributed share one RCCL), else librccl.so.1 through
+ * the library's RUNPATH (/opt/rocm/lib).  CRDT_ECOMM if none loads or it is older than 2.18. */
 int crdt_ctx_comm_init(crdt_ctx *ctx, const uint8_t *id, int nranks, int rank);
 /* Not collective (the callbacks are the caller's); ops is copied, its user pointer must stay
  * valid until crdt_ctx_comm_destroy. */
 int crdt_ctx_comm_init_ops(crdt_ctx *ctx, const crdt_comm_ops *ops, int nranks, int rank);
 int crdt_ctx_comm_destroy(crdt_ctx *ctx);
 int crdt_ctx_comm_info(const crdt_ctx *ctx, int *nranks, int *rank);
-/* Text noted at comm init ("" if none), e.g. "RCCL runtime 2.22.3 != rccl.h 2.26.6"; storage
- * owned by ctx.  *runtime / *header (may be NULL) = the RCCL version codes (0 without RCCL). */
+/* The RCCL the ctx's communicator runs on, noted at comm init ("" before it / for caller ops), e.g.
+ * "RCCL 2.26.6 (22606) at /.../librccl.so.1, already loaded by the process ..."; storage owned by
+ * ctx.  *runtime = the bound RCCL's version code (0 if none binds), *header = the rccl.h version
+ * the types were taken from (may be NULL). */
 const char *crdt_ctx_comm_note(const crdt_ctx *ctx, int *runtime, int *header);
 int crdt_vclock_lub_many_sharded(crdt_ctx *ctx, const uint64_t *in, size_t G, size_t R, size_t A,
                                  size_t row_stride, size_t group_stride, uint64_t *out);
@@ -622,7 +626,9 @@ int crdt_map_counter_lub_many(crdt_ctx *ctx, const crdt_map_counter_batch *in, c
  * + a], nested deferred vd_n[g*K + k] (<= 16) with vd_clock [((g*K + k)*16 + i)*A + a] and
  * vd_mem [(g*K + k)*16 + i]; flags[g]: bit 1 = def_row not non-decreasing or >= R, bit 3 = more
  * than 256 live Map removes named one key, bit 4 = a key's Orswot held more than 16 deferred
- * removes (results of the group unreliable); def_keep / def_keys as crdt_map_out.
+ * removes, bit 5 = vd_off invalid (checked on the device: vd_off[0] == 0, non-decreasing,
+ * vd_off[G*R*K] == Dv; the fold reads only rows [0, Dv) whatever it holds) — results of the
+ * group unreliable; def_keep / def_keys as crdt_map_out.
  * Orswot::forget collects its deferred removes into a new map: two whose clocks become equal keep
  * one entry with the later one's members (the oracle's dict order).
  * Limits: A <= 64, M <= 32.  Device-memory contexts only. */
@@ -636,6 +642,7 @@ typedef struct crdt_map_orswot_batch {
   const uint32_t *def_row;
   const uint64_t *def_clock;
   const uint64_t *def_keys;
+  size_t Dv;                /* rows of vd_clock / vd_mem (= vd_off[G*R*K]) */
 } crdt_map_orswot_batch;
 
 typedef struct crdt_map_orswot_out {
@@ -652,6 +659,60 @@ typedef struct crdt_map_orswot_out {
 } crdt_map_orswot_out;
 
 int crdt_map_orswot_lub_many(crdt_ctx *ctx, const crdt_map_orswot_batch *in, crdt_map_orswot_out *out);
+
+/* ---- Map<K, Map<K2, MVReg<u64, A>, A>, A> (round 5) -----------------------------------------------
+ * The nested type of the reference's own Map tests (TMap, test/map.rs:10; TestMap, map.rs:359):
+ * Map::merge (map.rs:140-220) whose value is a Map<K2, MVReg> — merged by Map::merge again with
+ * MVReg::merge (mvreg.rs:112-128) innermost, and forgotten by Map's Causal::forget (map.rs:85-114) —
+ * folded as acc = Map::new(); for r: acc.merge(replica[g][r]), exact for any input (each outer key in
+ * replica order).  Contiguous layouts (no strides), per replica r of group g:
+ *   clock [G][R][A]; ec [G][R][K][A] outer entry clocks (key absent: row 0); ic [G][R][K][A] the
+ *   inner Map clocks; iec [G][R][K][K2][A] inner entry clocks; ivc [G][R][K][K2][V][A] / ivv
+ *   [G][R][K][K2][V] the inner MVReg slots in Vec order (an empty slot: clock row 0); the inner
+ *   deferred removes as a device CSR over (g, r, k): id_off u64 [G*R*K + 1], id_clock [Di][A],
+ *   id_keys [Di] inner-key bitmasks; the outer deferred removes as for the MVReg Map: def_off HOST
+ *   (G+1), def_row, def_clock [D][A], def_keys [D][Kw].
+ * Output per (g, k) (packed): clock [g*A + a], ec / ic [(g*K + k)*A + a], iec [((g*K + k)*K2 + j)*A +
+ *   a], 8 slots per inner key ivc [(((g*K + k)*K2 + j)*8 + s)*A + a], ivv [((g*K + k)*K2 + j)*8 + s]
+ *   with nval [(g*K + k)*K2 + j] used (unused slots 0), inner deferred id_n [g*K + k] (<= 16),
+ *   id_clock [((g*K + k)*16 + i)*A + a], id_keys [(g*K + k)*16 + i]; flags[g]: bit 1 = def_row not
+ *   non-decreasing or >= R, bit 3 = more than 256 live outer removes named one key, bit 4 = an inner
+ *   Map held more than 16 deferred removes, bit 5 = id_off invalid (checked on the device: starts at
+ *   0, non-decreasing, ends at Di; the fold never reads past Di), bit 6 = an inner key held more than
+ *   8 values — results of the group unreliable; def_keep / def_keys as crdt_map_out.
+ * Map::forget collects the inner deferred removes into a new map: two whose clocks become equal keep
+ * one entry with the later one's keys (the oracle's dict order; the reference's is unspecified).
+ * Limits: A <= 64, K2 <= 64, V <= 8.  Device-memory contexts only. */
+typedef struct crdt_map_nested_batch {
+  size_t G, R, K, K2, V, A;
+  const uint64_t *clock, *ec, *ic, *iec, *ivc, *ivv;
+  const uint64_t *id_off;   /* device, G*R*K + 1 */
+  const uint64_t *id_clock; /* [Di][A] */
+  const uint64_t *id_keys;  /* [Di]    */
+  size_t Di;
+  const size_t *def_off;    /* host, G+1 entries; NULL = no outer deferred removes */
+  const uint32_t *def_row;
+  const uint64_t *def_clock;
+  const uint64_t *def_keys;
+} crdt_map_nested_batch;
+
+typedef struct crdt_map_nested_out {
+  uint64_t *clock;    /* [G][A]            */
+  uint64_t *ec;       /* [G][K][A]         */
+  uint64_t *ic;       /* [G][K][A]         */
+  uint64_t *iec;      /* [G][K][K2][A]     */
+  uint64_t *ivc;      /* [G][K][K2][8][A]  */
+  uint64_t *ivv;      /* [G][K][K2][8]     */
+  uint32_t *nval;     /* [G][K][K2]        */
+  uint32_t *id_n;     /* [G][K]            */
+  uint64_t *id_clock; /* [G][K][16][A]     */
+  uint64_t *id_keys;  /* [G][K][16]        */
+  uint32_t *flags;    /* [G]               */
+  uint8_t *def_keep;  /* [D]               */
+  uint64_t *def_keys; /* [D][Kw]           */
+} crdt_map_nested_out;
+
+int crdt_map_nested_lub_many(crdt_ctx *ctx, const crdt_map_nested_batch *in, crdt_map_nested_out *out);
 
 /* ---- MVReg<u64, A> on its own (outside a Map) ------------------------------------------------
  * Replaces MVReg::merge (mvreg.rs:112-128) and MVReg::apply (mvreg.rs:130-166) for registers in the

@@ -1500,6 +1500,100 @@ def map_orswot_objects(R: int, K: int, M: int, A: int, seed: int, steps: int = 3
     return gen_map_replicas(seed, R, K, A, steps=steps, vnew=Orswot, write=write, **kw)
 
 
+# ---- Map<K, Map<K2, MVReg<int>>> (the reference's own Map test type TMap, test/map.rs:10; round 5) ----
+def nested_map_to_dense(maps, K: int, K2: int, A: int, V: int):
+    """Ingest Map<int, Map<int, MVReg<int>>> objects (outer keys < K, inner keys < K2 <= 64, actors < A,
+    at most V values per register): clock (R, A), ec / ic (R, K, A) the outer entry / inner Map clocks,
+    iec (R, K, K2, A), ivc (R, K, K2, V, A) / ivv (R, K, K2, V) the MVReg slots in Vec order, the inner
+    deferred removes as a CSR over (replica, key) — id_off (R*K + 1), id_clock (Di, A), id_keys (Di,)
+    inner-key bitmasks — and the outer deferred pool (def_row, def_clock, def_keys)."""
+    R = len(maps)
+    clock = np.zeros((R, A), np.uint64)
+    ec = np.zeros((R, K, A), np.uint64)
+    ic = np.zeros((R, K, A), np.uint64)
+    iec = np.zeros((R, K, K2, A), np.uint64)
+    ivc = np.zeros((R, K, K2, V, A), np.uint64)
+    ivv = np.zeros((R, K, K2, V), np.uint64)
+    id_off, idc, idk = [0], [], []
+    def_row, dcl, dk = [], [], []
+
+    def row(vc):
+        out = np.zeros(A, np.uint64)
+        for a, c in vc.dots.items():
+            out[a] = c
+        return out
+
+    for r, m in enumerate(maps):
+        clock[r] = row(m.clock)
+        for k in range(K):
+            e = m.entries.get(k)
+            if e is not None:
+                ec[r, k] = row(e.clock)
+                ic[r, k] = row(e.val.clock)
+                for j, ie in e.val.entries.items():
+                    iec[r, k, j] = row(ie.clock)
+                    assert len(ie.val.vals) <= V, "more values than V slots"
+                    for s, (vcl, x) in enumerate(ie.val.vals):
+                        ivc[r, k, j, s] = row(vcl)
+                        ivv[r, k, j, s] = x
+                for rm, keys in e.val.deferred.items():
+                    idc.append(row(rm))
+                    idk.append(int(_bits(keys, 64)[0]))
+            id_off.append(len(idc))
+        for rm, keys in m.deferred.items():
+            def_row.append(r)
+            dcl.append(row(rm))
+            dk.append(_bits(keys, K))
+    D, Di = len(def_row), len(idc)
+    Kw = (K + 63) // 64
+    return dict(clock=clock, ec=ec, ic=ic, iec=iec, ivc=ivc, ivv=ivv, id_off=np.array(id_off, np.uint64),
+                id_clock=np.array(idc, np.uint64).reshape(Di, A), id_keys=np.array(idk, np.uint64),
+                def_row=np.array(def_row, np.uint64), def_clock=np.array(dcl, np.uint64).reshape(D, A),
+                def_keys=np.array(dk, np.uint64).reshape(D, Kw))
+
+
+def dense_to_nested_map(clock, ec, ic, iec, ivc, ivv, nval, ideferred=None, deferred=()) -> Map:
+    """Egress of one folded dense nested Map state: clock (A,), ec / ic (K, A), iec (K, K2, A), ivc (K,
+    K2, S, A) / ivv (K, K2, S) with nval (K, K2) slots used, ideferred {key: [(rm row, key set)]},
+    deferred [(rm row, key set)]."""
+    m = Map(lambda: Map(MVReg))
+    m.clock = _vc_row(clock)
+    for k in range(ec.shape[0]):
+        if ec[k].any():
+            inner = Map(MVReg)
+            inner.clock = _vc_row(ic[k])
+            for j in range(iec.shape[1]):
+                if iec[k, j].any():
+                    reg = MVReg()
+                    reg.vals = [(_vc_row(ivc[k, j, s]), int(ivv[k, j, s])) for s in range(int(nval[k, j]))]
+                    inner.entries[j] = MapEntry(_vc_row(iec[k, j]), reg)
+            for rm, keys in (ideferred or {}).get(k, []):
+                inner.deferred[_vc_row(rm)] = set(keys)
+            m.entries[k] = MapEntry(_vc_row(ec[k]), inner)
+    for rm, keys in deferred:
+        m.deferred[_vc_row(rm)] = set(keys)
+    return m
+
+
+def nested_map_objects(R: int, K: int, K2: int, A: int, seed: int, steps: int = 300, p_irm: float = 0.3, **kw):
+    """Op-replay replicas of Map<int, Map<int, MVReg<int>>>: a write updates the outer key with an inner
+    write (inner.update(k2, ctx, reg.write)) or (p_irm) an inner remove whose context is read at the
+    inner Map — sometimes at a replica that has seen more (a deferred inner remove), as test/map.rs's
+    build_ops mixes inner Up / Rm under one outer dot."""
+    rng = np.random.default_rng(seed ^ 0x4E5)
+
+    def write(v, c, x, a):
+        j = int(rng.integers(K2))
+        if rng.random() < p_irm:
+            ctx = v.get(j).derive_rm_ctx()
+            if rng.random() < 0.5:
+                b = int(rng.integers(A))
+                ctx.clock.apply(Dot(b, ctx.clock.get(b) + int(rng.integers(1, 3))))
+            return v.rm(j, ctx)
+        return v.update(j, c, lambda reg, cx, x=x: reg.write(x, cx))
+    return gen_map_replicas(seed, R, K, A, steps=steps, vnew=lambda: Map(MVReg), write=write, **kw)
+
+
 def max_vals(maps) -> int:
     return max([len(e.val.vals) for m in maps for e in m.entries.values()] + [1])
 

@@ -53,6 +53,7 @@ EXPORTS = (
     "crdt_mvreg_lub_many", "crdt_mvreg_merge_batch", "crdt_mvreg_apply_batch",
     "crdt_orswot_lub_many_doff", "crdt_map_lub_many_doff",
     "crdt_orswot_lub_many_sharded_doff", "crdt_map_lub_many_sharded_doff", "crdt_map_counter_lub_many", "crdt_map_orswot_lub_many",
+    "crdt_map_nested_lub_many",
 )
 
 
@@ -183,13 +184,27 @@ class MapOrswotBatch(ctypes.Structure):  # crdt_map_orswot_batch
         ("G", S), ("R", S), ("K", S), ("M", S), ("A", S),
         ("clock", P), ("ec", P), ("oc", P), ("ent", P),
         ("vd_off", P), ("vd_clock", P), ("vd_mem", P),
-        ("def_off", ctypes.POINTER(S)), ("def_row", P), ("def_clock", P), ("def_keys", P),
+        ("def_off", ctypes.POINTER(S)), ("def_row", P), ("def_clock", P), ("def_keys", P), ("Dv", S),
     ]
 
 
 class MapOrswotOut(ctypes.Structure):  # crdt_map_orswot_out
     _fields_ = [("clock", P), ("ec", P), ("oc", P), ("ent", P), ("vd_n", P), ("vd_clock", P), ("vd_mem", P),
                 ("flags", P), ("def_keep", P), ("def_keys", P)]
+
+
+class MapNestedBatch(ctypes.Structure):  # crdt_map_nested_batch
+    _fields_ = [
+        ("G", S), ("R", S), ("K", S), ("K2", S), ("V", S), ("A", S),
+        ("clock", P), ("ec", P), ("ic", P), ("iec", P), ("ivc", P), ("ivv", P),
+        ("id_off", P), ("id_clock", P), ("id_keys", P), ("Di", S),
+        ("def_off", ctypes.POINTER(S)), ("def_row", P), ("def_clock", P), ("def_keys", P),
+    ]
+
+
+class MapNestedOut(ctypes.Structure):  # crdt_map_nested_out
+    _fields_ = [("clock", P), ("ec", P), ("ic", P), ("iec", P), ("ivc", P), ("ivv", P), ("nval", P), ("id_n", P),
+                ("id_clock", P), ("id_keys", P), ("flags", P), ("def_keep", P), ("def_keys", P)]
 
 
 class MapOut(ctypes.Structure):  # crdt_map_out
@@ -252,6 +267,7 @@ _SIGS.update({
                                        ctypes.c_int),
     "crdt_map_counter_lub_many": ([P, ctypes.POINTER(MapCounterBatch), ctypes.POINTER(MapCounterOut)], ctypes.c_int),
     "crdt_map_orswot_lub_many": ([P, ctypes.POINTER(MapOrswotBatch), ctypes.POINTER(MapOrswotOut)], ctypes.c_int),
+    "crdt_map_nested_lub_many": ([P, ctypes.POINTER(MapNestedBatch), ctypes.POINTER(MapNestedOut)], ctypes.c_int),
     "crdt_vclock_ingest": ([P, P, P, S, P, S, P, S, P], ctypes.c_int),
     "crdt_pncounter_ingest": ([P, P, P, S, P, S, P, S, P], ctypes.c_int),
     "crdt_gset_ingest": ([P, P, P, S, P, S, P, S, P], ctypes.c_int),

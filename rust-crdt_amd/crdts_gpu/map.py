@@ -544,7 +544,10 @@ def orswot_lub_many(clock: torch.Tensor, ec: torch.Tensor, oc: torch.Tensor, ent
     dev = clock.device
     if vd_off.device != dev or not vd_off.is_contiguous() or tuple(vd_off.shape) != (G * R * K + 1,):
         raise ValueError(f"map.orswot_lub_many: vd_off must be a contiguous ({G * R * K + 1},) tensor on {dev}")
-    Dv = int(vd_off[-1].item()) if vd_off.numel() else 0
+    if vd_off.dtype not in (torch.int64, torch.uint64):
+        raise ValueError(f"map.orswot_lub_many: vd_off must be int64 / uint64 (got {vd_off.dtype})")
+    # Dv = rows of vd_clock / vd_mem; the library checks vd_off against it on the device (flags bit 5)
+    Dv = int(vd_clock.shape[0]) if vd_clock is not None else 0
     if Dv > 0:
         for t, nm, shape in ((vd_clock, "vd_clock", (Dv, A)), (vd_mem, "vd_mem", (Dv,))):
             if t is None or not t.is_contiguous() or tuple(t.shape) != shape:
@@ -558,7 +561,7 @@ def orswot_lub_many(clock: torch.Tensor, ec: torch.Tensor, oc: torch.Tensor, ent
     b = _abi.MapOrswotBatch()
     b.G, b.R, b.K, b.M, b.A = G, R, K, M, A
     b.clock, b.ec, b.oc, b.ent = c.data_ptr(), e.data_ptr(), o.data_ptr(), m.data_ptr()
-    b.vd_off = vd_off.data_ptr()
+    b.vd_off, b.Dv = vd_off.data_ptr(), Dv
     if Dv > 0:
         b.vd_clock, b.vd_mem = vd_clock.data_ptr(), vd_mem.data_ptr()
     ob = _abi.MapOrswotOut()
@@ -595,9 +598,134 @@ def orswot_lub_many(clock: torch.Tensor, ec: torch.Tensor, oc: torch.Tensor, ent
             raise ValueError("map.orswot_lub_many: def_row not non-decreasing per group or >= R")
         if f & 8:
             raise RuntimeError("map.orswot_lub_many: more than 256 live removes named one key")
+        if f & 32:
+            raise ValueError("map.orswot_lub_many: vd_off invalid (must start at 0, be non-decreasing and end at "
+                             "vd_clock.shape[0])")
         if f & 16:
             raise RuntimeError("map.orswot_lub_many: more than 16 deferred removes in one key's Orswot")
     oclk, oec, ooc, oent, ovdc, ovdm = out
     if squeeze:
         oclk, oec, ooc, oent, vd_n, ovdc, ovdm = oclk[0], oec[0], ooc[0], oent[0], vd_n[0], ovdc[0], ovdm[0]
     return MapOrswotLub(oclk, oec, ooc, oent, vd_n, ovdc, ovdm, flags, keep, keys_out)
+
+
+# ---- Map<K, Map<K2, MVReg<u64>>> (crdt_map_nested_lub_many, round 5) -------------------------------
+NM_VS = 8   # MVReg slots per inner key in the fold state (crdt_gpu.h)
+NM_ID = 16  # inner deferred removes per key state
+
+
+class MapNestedLub(NamedTuple):
+    clock: torch.Tensor               # (G, A)
+    ec: torch.Tensor                  # (G, K, A) outer entry clocks
+    ic: torch.Tensor                  # (G, K, A) inner Map clocks
+    iec: torch.Tensor                 # (G, K, K2, A) inner entry clocks
+    ivc: torch.Tensor                 # (G, K, K2, 8, A) inner MVReg slot clocks
+    ivv: torch.Tensor                 # (G, K, K2, 8) values
+    nval: torch.Tensor                # (G, K, K2) int32 slots used
+    id_n: torch.Tensor                # (G, K) int32 inner deferred removes
+    id_clock: torch.Tensor            # (G, K, 16, A)
+    id_keys: torch.Tensor             # (G, K, 16) inner key bitmasks
+    flags: torch.Tensor               # (G,) int32
+    def_keep: Optional[torch.Tensor]  # (D,) uint8
+    def_keys: Optional[torch.Tensor]  # (D, Kw)
+
+
+def nested_lub_many(clock: torch.Tensor, ec: torch.Tensor, ic: torch.Tensor, iec: torch.Tensor, ivc: torch.Tensor,
+                    ivv: torch.Tensor, id_off: torch.Tensor, id_clock: Optional[torch.Tensor] = None,
+                    id_keys: Optional[torch.Tensor] = None, def_off=None, def_row: Optional[torch.Tensor] = None,
+                    def_clock: Optional[torch.Tensor] = None, def_keys: Optional[torch.Tensor] = None,
+                    ctx: Optional[Context] = None, check: bool = True) -> MapNestedLub:
+    """The exact left fold of Map::merge (map.rs:140-220) for Map<K, Map<K2, MVReg<u64>>> — the type of
+    the reference's own Map tests (test/map.rs:10) — with the inner Map's merge (map.rs:140-220,
+    mvreg.rs:112-128) and forget (map.rs:85-114) as the value's.  clock (G,R,A) / (R,A); ec, ic
+    (G,R,K,A); iec (G,R,K,K2,A); ivc (G,R,K,K2,V,A); ivv (G,R,K,K2,V), all contiguous; the inner
+    deferred removes as a device CSR over (g, r, k): id_off (G*R*K + 1,) int64, id_clock (Di, A),
+    id_keys (Di,) inner-key bitmasks; the outer deferred pool as for lub_many (host def_off).
+    check=True raises on flags (bit 1: def_row unsorted / out of range, bit 3: more than 256 live outer
+    removes named one key, bit 4: more than 16 inner deferred removes, bit 5: id_off invalid, bit 6:
+    more than 8 values on one inner key)."""
+    ctx = ctx or Context.default(clock.device.index)
+    squeeze = clock.dim() == 2
+    c, e, i, ie, vc, vv = ((t.unsqueeze(0) if squeeze else t) for t in (clock, ec, ic, iec, ivc, ivv))
+    if c.dim() != 3 or e.dim() != 4 or i.dim() != 4 or ie.dim() != 5 or vc.dim() != 6 or vv.dim() != 5:
+        raise ValueError("map.nested_lub_many: clock (G,R,A), ec / ic (G,R,K,A), iec (G,R,K,K2,A), "
+                         "ivc (G,R,K,K2,V,A), ivv (G,R,K,K2,V) expected")
+    G, R, A = c.shape
+    K, K2, V = e.shape[2], ie.shape[3], vc.shape[4]
+    if (tuple(e.shape) != (G, R, K, A) or tuple(i.shape) != (G, R, K, A) or tuple(ie.shape) != (G, R, K, K2, A)
+            or tuple(vc.shape) != (G, R, K, K2, V, A) or tuple(vv.shape) != (G, R, K, K2, V)):
+        raise ValueError("map.nested_lub_many: shapes do not agree")
+    for t, nm in ((c, "clock"), (e, "ec"), (i, "ic"), (ie, "iec"), (vc, "ivc"), (vv, "ivv")):
+        ctx.check_tensor(t, f"map.nested_lub_many({nm})")
+        if not t.is_contiguous():
+            raise ValueError(f"map.nested_lub_many: {nm} must be contiguous")
+    dev = clock.device
+    if id_off.device != dev or not id_off.is_contiguous() or tuple(id_off.shape) != (G * R * K + 1,):
+        raise ValueError(f"map.nested_lub_many: id_off must be a contiguous ({G * R * K + 1},) tensor on {dev}")
+    if id_off.dtype not in (torch.int64, torch.uint64):
+        raise ValueError(f"map.nested_lub_many: id_off must be int64 / uint64 (got {id_off.dtype})")
+    Di = int(id_clock.shape[0]) if id_clock is not None else 0
+    if Di > 0:
+        for t, nm, shape in ((id_clock, "id_clock", (Di, A)), (id_keys, "id_keys", (Di,))):
+            if t is None or not t.is_contiguous() or tuple(t.shape) != shape:
+                raise ValueError(f"map.nested_lub_many: {nm} must be a contiguous {shape} tensor")
+            ctx.check_tensor(t, f"map.nested_lub_many({nm})")
+    Kw = (K + 63) // 64
+    out = [torch.empty(sh, dtype=torch.int64, device=dev)
+           for sh in ((G, A), (G, K, A), (G, K, A), (G, K, K2, A), (G, K, K2, NM_VS, A), (G, K, K2, NM_VS),
+                      (G, K, NM_ID, A), (G, K, NM_ID))]
+    nval = torch.empty((G, K, K2), dtype=torch.int32, device=dev)
+    id_n = torch.empty((G, K), dtype=torch.int32, device=dev)
+    flags = torch.empty(G, dtype=torch.int32, device=dev)
+    b = _abi.MapNestedBatch()
+    b.G, b.R, b.K, b.K2, b.V, b.A = G, R, K, K2, V, A
+    b.clock, b.ec, b.ic, b.iec, b.ivc, b.ivv = (t.data_ptr() for t in (c, e, i, ie, vc, vv))
+    b.id_off, b.Di = id_off.data_ptr(), Di
+    if Di > 0:
+        b.id_clock, b.id_keys = id_clock.data_ptr(), id_keys.data_ptr()
+    ob = _abi.MapNestedOut()
+    ob.clock, ob.ec, ob.ic, ob.iec, ob.ivc, ob.ivv, ob.id_clock, ob.id_keys = (t.data_ptr() for t in out)
+    ob.nval, ob.id_n, ob.flags = nval.data_ptr(), id_n.data_ptr(), flags.data_ptr()
+    keep = keys_out = None
+    off_arr = None
+    if def_off is not None:
+        off = np.asarray(def_off, dtype=np.uint64)
+        if off.shape != (G + 1,):
+            raise ValueError(f"map.nested_lub_many: def_off must have G+1 = {G + 1} entries")
+        D = int(off[-1])
+        if D > 0:
+            for t, nm, shape in ((def_clock, "def_clock", (D, A)), (def_keys, "def_keys", (D, Kw)),
+                                 (def_row, "def_row", (D,))):
+                if t is None or not t.is_contiguous() or tuple(t.shape) != shape:
+                    raise ValueError(f"map.nested_lub_many: {nm} must be a contiguous {shape} tensor")
+                if nm != "def_row":
+                    ctx.check_tensor(t, f"map.nested_lub_many({nm})")
+            if def_row.dtype not in (torch.int32, torch.uint32) or def_row.device != dev:
+                raise ValueError(f"map.nested_lub_many: def_row must be an int32 tensor on {dev}")
+            off_arr = (ctypes.c_size_t * (G + 1))(*[int(x) for x in off])
+            b.def_off = ctypes.cast(off_arr, ctypes.POINTER(ctypes.c_size_t))
+            b.def_row, b.def_clock, b.def_keys = def_row.data_ptr(), def_clock.data_ptr(), def_keys.data_ptr()
+            keep = torch.empty(D, dtype=torch.uint8, device=dev)
+            keys_out = torch.empty((D, Kw), dtype=torch.int64, device=dev)
+            ob.def_keep, ob.def_keys = keep.data_ptr(), keys_out.data_ptr()
+    ctx.call("crdt_map_nested_lub_many", ctypes.byref(b), ctypes.byref(ob))
+    if check:
+        f = 0
+        for x in flags.cpu().numpy().tolist():
+            f |= int(x)
+        if f & 2:
+            raise ValueError("map.nested_lub_many: def_row not non-decreasing per group or >= R")
+        if f & 32:
+            raise ValueError("map.nested_lub_many: id_off invalid (must start at 0, be non-decreasing and end at "
+                             "id_clock.shape[0])")
+        if f & 8:
+            raise RuntimeError("map.nested_lub_many: more than 256 live removes named one key")
+        if f & 16:
+            raise RuntimeError("map.nested_lub_many: more than 16 deferred removes in one key's inner Map")
+        if f & 64:
+            raise RuntimeError("map.nested_lub_many: more than 8 values on one inner key")
+    oclk, oec, oic, oiec, oivc, oivv, oidc, oidk = out
+    if squeeze:
+        oclk, oec, oic, oiec, oivc, oivv, nval, id_n, oidc, oidk = (
+            oclk[0], oec[0], oic[0], oiec[0], oivc[0], oivv[0], nval[0], id_n[0], oidc[0], oidk[0])
+    return MapNestedLub(oclk, oec, oic, oiec, oivc, oivv, nval, id_n, oidc, oidk, flags, keep, keys_out)

@@ -16,7 +16,6 @@ twin of the same exchange (gloo-testable on CPU)."""
 from __future__ import annotations
 
 import ctypes
-import warnings
 from typing import NamedTuple, Optional, Sequence
 
 import numpy as np
@@ -39,13 +38,11 @@ def comm_init(ctx: Context, uid: bytes, nranks: int, rank: int) -> None:
         raise ValueError(f"comm_init: unique id must be {_abi.CRDT_UNIQUE_ID_BYTES} bytes")
     buf = (ctypes.c_uint8 * _abi.CRDT_UNIQUE_ID_BYTES).from_buffer_copy(uid)
     ctx.call("crdt_ctx_comm_init", buf, int(nranks), int(rank))
-    note = comm_note(ctx)[0]
-    if note:
-        warnings.warn(f"crdt_ctx_comm_init: {note}", RuntimeWarning, stacklevel=2)
 
 
 def comm_note(ctx: Context):
-    """(note text, RCCL runtime version, rccl.h version) — crdt_ctx_comm_note."""
+    """(which RCCL the communicator runs on, its version code, the rccl.h version of the types) —
+    crdt_ctx_comm_note.  One RCCL per process: inside a torch process the library binds torch's."""
     rt, hd = ctypes.c_int(), ctypes.c_int()
     txt = _abi.load().crdt_ctx_comm_note(ctx.ptr, ctypes.byref(rt), ctypes.byref(hd))
     return (txt or b"").decode(), rt.value, hd.value

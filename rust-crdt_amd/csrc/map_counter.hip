@@ -34,6 +34,13 @@ struct MapCounterPlan {
   const u64 *def_clock, *def_keys;
   u64 *o_clock, *o_ec, *o_val;
   unsigned *o_flags;
+  // Keys per wave > 1 share one live-remove list of kMcLive entries, so a wave can run out of room
+  // while each of its keys holds <= kMcLive live removes.  With rerun_out set, such a
+  // wave marks its group in rerun_out instead of flags bit 3; a second launch with one key per wave
+  // and rerun_in = that array re-folds exactly the marked groups (every other wave returns at once),
+  // so the documented per-key capacity holds whatever the automatic keys-per-wave choice.
+  const unsigned *rerun_in;
+  unsigned *rerun_out;
 };
 
 __device__ __forceinline__ void glds16_mc(const void *g, u64 *lds) {
@@ -84,6 +91,7 @@ __global__ __launch_bounds__(kMcWaves * kWave) void map_counter_fold_kernel(MapC
   const unsigned long long wk = (unsigned long long)blockIdx.x * kMcWaves + wv;
   if (wk >= p.G * KW) return;  // (whole waves; nothing below synchronises the workgroup)
   const unsigned long long g = wk / KW, kb = (wk % KW) * KPW, A = p.A, R = p.R;
+  if (p.rerun_in && p.rerun_in[g] == 0) return;  // (the re-fold launch: only the marked groups)
   const unsigned long long k = kb + h;  // the lane's key (past K: a copy of key K-1, not written)
   const bool kval = k < p.K;
   const unsigned long long kc = kval ? k : p.K - 1;
@@ -418,6 +426,10 @@ __global__ __launch_bounds__(kMcWaves * kWave) void map_counter_fold_kernel(MapC
       if (k == 0) p.o_clock[g * A + a] = C[j];
     }
   }
+  if (full && p.rerun_out) {  // the shared list overflowed: the group is re-folded one key per wave
+    if (lane == 0) atomicOr(p.rerun_out + g, 1u);
+    full = false;
+  }
   if ((bad || full) && lane == 0) atomicOr(p.o_flags + g, (bad ? 2u : 0u) | (full ? 8u : 0u));
 }
 
@@ -472,33 +484,41 @@ extern "C" int crdt_map_counter_lub_many(crdt_ctx *ctx, const crdt_map_counter_b
   MapCounterPlan p{(const u64 *)in->clock, (const u64 *)in->ec, (const u64 *)in->val, in->clock_rstride,
                    in->clock_gstride, in->ec_rstride, in->ec_gstride, in->val_rstride, in->val_gstride, G, R, K, A,
                    Kw, nullptr, in->def_row, (const u64 *)in->def_clock, (const u64 *)in->def_keys,
-                   (u64 *)out->clock, (u64 *)out->ec, (u64 *)out->val, out->flags};
+                   (u64 *)out->clock, (u64 *)out->ec, (u64 *)out->val, out->flags, nullptr, nullptr};
   if (int rc = device_fill(ctx, out->flags, G * sizeof(unsigned), 0)) return rc;
   if (R == 0) {  // fold of nothing: Map::new()
     if (int rc = device_fill(ctx, out->clock, G * A * 8, 0)) return rc;
     if (int rc = device_fill(ctx, out->ec, G * K * A * 8, 0)) return rc;
     if (int rc = device_fill(ctx, out->val, G * K * W * A * 8, 0)) return rc;
   } else {
+    // keys per wave: explicit (mckpw=1/2/4), or automatic (0): pair keys in a wave only while the
+    // paired grid still has 2,048+ waves (2 per SIMD) — at 4,096 keys x 4,096 replicas two keys per
+    // wave ran 1.60 vs 2.52 ms, at 1,024 keys (one wave per SIMD) 5.33 vs 5.03 ms
+    int kpw = ctx->tune.map_counter_kpw;
+    const bool auto_kpw = kpw == 0;
+    if (auto_kpw) {
+      const size_t waves_per_simd2 = 2048;
+      kpw = A <= (size_t)kWave / 4 && G * ((K + 3) / 4) >= waves_per_simd2   ? 4
+            : A <= (size_t)kWave / 2 && G * ((K + 1) / 2) >= waves_per_simd2 ? 2
+                                                                                : 1;
+    }
+    // scratch: [def_off (G+1) size_t | rerun marks (G) unsigned, automatic keys per wave > 1 only]
+    const size_t off_bytes = (G + 1) * sizeof(size_t);
+    const bool rerun = D > 0 && auto_kpw && kpw > 1;
     if (D > 0) {
-      if (int rc = ensure_scratch(ctx, (G + 1) * sizeof(size_t))) return rc;
-      if (int rc = stage_h2d(ctx, ctx->scratch, in->def_off, (G + 1) * sizeof(size_t))) return rc;
+      if (int rc = ensure_scratch(ctx, off_bytes + (rerun ? G * sizeof(unsigned) : 0))) return rc;
+      if (int rc = stage_h2d(ctx, ctx->scratch, in->def_off, off_bytes)) return rc;
       p.def_off = reinterpret_cast<const size_t *>(ctx->scratch);
+      if (rerun) {
+        p.rerun_out = reinterpret_cast<unsigned *>(static_cast<char *>(ctx->scratch) + off_bytes);
+        if (int rc = device_fill(ctx, p.rerun_out, G * sizeof(unsigned), 0)) return rc;
+      }
     }
     timing_begin(ctx, "map_counter_fold");
     hipError_t he;
     const bool al = ((p.c_rs | p.c_gs | p.e_rs | p.e_gs | p.v_rs | p.v_gs) & 1) == 0 &&
                     ((uintptr_t)in->clock & 15) == 0 && ((uintptr_t)in->ec & 15) == 0 && ((uintptr_t)in->val & 15) == 0;
     const int ring = A % 2 == 0 && (2 + W) * A <= 128 && al ? ctx->tune.map_counter_dma : 0;
-    // keys per wave: explicit (mckpw=1/2/4), or automatic (0): pair keys in a wave only while the
-    // paired grid still has 2,048+ waves (2 per SIMD) — at 4,096 keys x 4,096 replicas two keys per
-    // wave ran 1.60 vs 2.52 ms, at 1,024 keys (one wave per SIMD) 5.33 vs 5.03 ms
-    int kpw = ctx->tune.map_counter_kpw;
-    if (kpw == 0) {
-      const size_t waves_per_simd2 = 2048;
-      kpw = A <= (size_t)kWave / 4 && G * ((K + 3) / 4) >= waves_per_simd2   ? 4
-            : A <= (size_t)kWave / 2 && G * ((K + 1) / 2) >= waves_per_simd2 ? 2
-                                                                                : 1;
-    }
     if (!ring && kpw >= 4 && A <= (size_t)kWave / 4)
       he = W == 1 ? launch_mc<1, 1, 0, 4>(p, ctx->stream) : launch_mc<1, 2, 0, 4>(p, ctx->stream);
     else if (!ring && kpw >= 2 && A <= (size_t)kWave / 2)
@@ -513,6 +533,12 @@ extern "C" int crdt_map_counter_lub_many(crdt_ctx *ctx, const crdt_map_counter_b
     else if (A <= 2 * (size_t)kWave) he = W == 1 ? launch_mc<2, 1>(p, ctx->stream) : launch_mc<2, 2>(p, ctx->stream);
     else if (A <= 4 * (size_t)kWave) he = W == 1 ? launch_mc<4, 1>(p, ctx->stream) : launch_mc<4, 2>(p, ctx->stream);
     else he = W == 1 ? launch_mc<8, 1>(p, ctx->stream) : launch_mc<8, 2>(p, ctx->stream);
+    if (he == hipSuccess && rerun && p.rerun_out) {  // re-fold the groups whose shared list overflowed
+      MapCounterPlan q = p;
+      q.rerun_in = p.rerun_out;
+      q.rerun_out = nullptr;
+      he = W == 1 ? launch_mc<1, 1>(q, ctx->stream) : launch_mc<1, 2>(q, ctx->stream);
+    }
     timing_end(ctx);
     if (he != hipSuccess) return hip_fail(ctx, he, "map_counter_fold_kernel launch");
   }

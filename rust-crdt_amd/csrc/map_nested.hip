@@ -1,0 +1,600 @@
+// Map<K, Map<K2, MVReg<u64>>> lub_many (round 5): the nested type of the reference's own Map tests
+// (TMap, test/map.rs:10; TestMap, src/map.rs:359).  The outer Map::merge (map.rs:140-220) carries an
+// inner Map as its value, whose merge is Map::merge again (with MVReg::merge, mvreg.rs:112-128, as the
+// innermost value merge) and whose forget is Map's Causal::forget (map.rs:85-114: entry clocks,
+// values, deferred clocks and the inner Map's own clock).  As for every Map value type the fold
+// acc = Map::new(); for r: acc.merge(r) is not associative, so each outer key is folded in replica
+// order (exact for any input): one wave per (group, outer key), lane = actor (A <= 64).
+//
+// Step r on the key's state (outer clock C, entry clock e, inner Map: clock ic, entry clocks iec[j],
+// MVReg slots in Vec order, inner deferred removes) with replica r's (c2, e2, ic2, iec2, values, D2):
+//  - outer entry clock: the branch-free join of map_counter.hip, e' = max(e == e2 ? e : 0,
+//    forget(e2, C), forget(e, c2)), and the case's forget clock X (removed_information :151 /
+//    we_deleted :200 / deleted :185); an empty e' drops the entry without touching its value;
+//  - both present: the inner Map::merge — per inner key the same join over the inner clocks (ic, ic2),
+//    MVReg::merge of the slots then their forget by the inner case's clock; then apply_keyset_rm of
+//    each of the replica's inner removes against ic (forget, defer iff !(rm <= ic)), ic |= ic2, and
+//    apply_deferred (every held remove forgets its keys again, stays iff !(rm <= ic));  only the
+//    replica holds the key: its inner Map;  then the inner Map forgets X (Causal::forget);
+//  - the outer removes naming the key (apply_keyset_rm / apply_deferred, :213-219, :318-348): one
+//    forget by their max — the entry clock, and the inner Map while the entry stays;
+//  - C |= c2 and the outer deferral test (witness thresholds, as map_counter.hip / map_orswot.hip).
+// The inner Map's rows live in the key's own output rows (global memory, touched by this wave only);
+// its deferred removes (<= 16) and slot counts in LDS.  Map::forget collects the deferred removes into
+// a new HashMap: two whose clocks become equal keep one entry with the later one's keys at the earlier
+// one's place (the reference's HashMap order is unspecified; this is the oracle's dict order —
+// parity unpinned for that collision).  Lanes past A hold 0 in every row, so they never change a vote.
+#include "common.hpp"
+
+namespace crdt {
+
+constexpr int kNmWaves = 4;   // key waves per workgroup
+constexpr int kNmList = 256;  // outer removes naming the key, gathered per window (row << 32 | index)
+constexpr int kNmLive = 256;  // live outer removes per key (flags bit 3 past it)
+constexpr int kNmRows = 8;    // live outer-remove rows cached in LDS
+constexpr int kNmId = 16;     // inner deferred removes per key state (flags bit 4 past it)
+constexpr int kNmVs = 8;      // MVReg slots per inner key in the fold state (flags bit 6 past it)
+constexpr int kNmVin = 8;     // MVReg slots per inner key in the input
+constexpr int kNmK2 = 64;     // inner keys (key sets of inner removes: one u64 mask)
+
+struct NestedMapPlan {
+  const u64 *clock, *ec, *ic, *iec, *ivc, *ivv;  // (G,R,A) (G,R,K,A) (G,R,K,A) (G,R,K,K2,A) (G,R,K,K2,V,A) (G,R,K,K2,V)
+  const u64 *id_off, *id_clock, *id_keys;        // inner deferred CSR over (g, r, k)
+  unsigned long long Di;
+  unsigned long long G, R, K, K2, V, A, Kw;
+  const size_t *def_off;  // device copy (G+1), or null
+  const uint32_t *def_row;
+  const u64 *def_clock, *def_keys;
+  u64 *o_clock, *o_ec, *o_ic, *o_iec, *o_ivc, *o_ivv;
+  unsigned *o_nval, *o_id_n;
+  u64 *o_id_clock, *o_id_keys;
+  unsigned *o_flags;
+};
+
+__device__ __forceinline__ bool nm_nz(u64 x) { return __ballot(x != 0) != 0; }
+__device__ __forceinline__ u64 nm_fg(u64 x, u64 c) { return x > c ? x : 0; }  // VClock::forget, per actor
+__device__ __forceinline__ u64 nm_max(u64 x, u64 y) { return x > y ? x : y; }
+// VClock partial order, whole clock: x < y (x <= y everywhere and x != y somewhere)
+__device__ __forceinline__ bool nm_lt(u64 x, u64 y) { return !__ballot(x > y) && __ballot(x != y); }
+__device__ __forceinline__ bool nm_eq(u64 x, u64 y) { return !__ballot(x != y); }
+
+__global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(NestedMapPlan p) {
+  extern __shared__ u64 lds[];
+  const int lane = (int)(threadIdx.x % kWave), wv = (int)(threadIdx.x / kWave);
+  const unsigned long long gk = (unsigned long long)blockIdx.x * kNmWaves + wv;
+  if (gk >= p.G * p.K) return;  // (whole waves; nothing below synchronises the workgroup)
+  const unsigned long long g = gk / p.K, k = gk % p.K, A = p.A, R = p.R, K = p.K, K2 = p.K2, V = p.V;
+  constexpr unsigned long long WQ = kNmList + kNmLive / 2 + kNmRows * kWave + kNmId * kWave + kNmId + kNmK2 / 8;
+  u64 *lst = lds + (unsigned long long)wv * WQ;
+  uint32_t *live = reinterpret_cast<uint32_t *>(lst + kNmList);
+  u64 *rows = lst + kNmList + kNmLive / 2;  // [kNmRows][64] live outer-remove rows
+  u64 *drow = rows + kNmRows * kWave;       // [kNmId][64] inner deferred rm rows
+  u64 *dkey = drow + kNmId * kWave;         // [kNmId] their inner key masks
+  uint8_t *nv = reinterpret_cast<uint8_t *>(dkey + kNmId);  // [K2] MVReg slots held per inner key
+  const bool al = (unsigned long long)lane < A;
+  auto ld = [&](const u64 *row) -> u64 { return al ? row[lane] : 0ull; };
+  auto st = [&](u64 *row, u64 x) {
+    if (al) row[lane] = x;
+  };
+
+  // ---- the outer removes naming key k, in replica order (map_orswot.hip's walk)
+  const unsigned long long d0 = p.def_off ? p.def_off[g] : 0, d1 = p.def_off ? p.def_off[g + 1] : 0;
+  unsigned long long dc = d0;
+  int nl = 0, li = 0;
+  bool bad = false;  // def_row not non-decreasing or >= R (flags bit 1)
+  u64 last_row = 0;
+  auto refill = [&]() {
+    nl = 0;
+    li = 0;
+    while (dc < d1 && nl + kWave <= kNmList) {
+      const unsigned long long d = dc + lane;
+      bool hit = false;
+      u64 row = 0;
+      if (d < d1) {
+        row = p.def_row[d];
+        hit = (p.def_keys[d * p.Kw + k / 64] >> (k % 64)) & 1ull;
+      }
+      const u64 prev = __shfl_up(row, 1);
+      bool b = d < d1 && (row >= R || (lane == 0 ? row < last_row : row < prev));
+      if (__ballot(b)) bad = true;
+      const unsigned long long n = d1 - dc < (unsigned long long)kWave ? d1 - dc : kWave;
+      last_row = __shfl(row, (int)n - 1);
+      const u64 m = __ballot(hit);
+      if (hit) lst[nl + __popcll(m & ((1ull << lane) - 1))] = (row << 32) | (u64)(d - d0);
+      nl += __popcll(m);
+      dc += n;
+    }
+  };
+  unsigned nxt = ~0u;
+  auto advance = [&]() {
+    for (;;) {
+      if (li < nl) {
+        nxt = (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(lst[li] >> 32));
+        return;
+      }
+      if (dc >= d1) {
+        nxt = ~0u;
+        return;
+      }
+      refill();
+    }
+  };
+  refill();
+  advance();
+  bool full = false, dfull = false, vfull = false;
+  int na = 0;
+  auto live_row = [&](int i) -> u64 {
+    return i < kNmRows ? rows[(unsigned long long)i * kWave + lane] : ld(p.def_clock + (d0 + live[i]) * A);
+  };
+  auto put_row = [&](int i, u64 x) {
+    if (i < kNmRows) rows[(unsigned long long)i * kWave + lane] = x;
+  };
+  u64 rk = 0, T = ~0ull;
+
+  // ---- the key's state: outer C, e; the inner Map's clock ic (registers), rows in the output
+  u64 C = 0, e = 0, ic = 0;
+  int nd = 0;  // inner deferred removes held (uniform)
+  u64 *const iec_o = p.o_iec + gk * K2 * A;
+  u64 *const ivc_o = p.o_ivc + gk * K2 * kNmVs * A;
+  u64 *const ivv_o = p.o_ivv + gk * K2 * kNmVs;
+  for (unsigned long long j = 0; j < K2; ++j) {
+    st(iec_o + j * A, 0);
+    if (lane == 0) nv[j] = 0;
+  }
+
+  // MVReg::forget (mvreg.rs:88-104) of inner key j's slots by x, compacted in order
+  auto vals_forget = [&](unsigned long long j, u64 x) {
+    const int n = __builtin_amdgcn_readfirstlane((int)nv[j]);
+    int o = 0;
+    for (int s = 0; s < n; ++s) {
+      const u64 c = nm_fg(ld(ivc_o + (j * kNmVs + s) * A), x);
+      if (!nm_nz(c)) continue;
+      const u64 v = ivv_o[j * kNmVs + s];
+      st(ivc_o + (j * kNmVs + o) * A, c);
+      ivv_o[j * kNmVs + o] = v;  // (every lane stores the value: each later reads back its own store)
+      ++o;
+    }
+    if (lane == 0) nv[j] = (uint8_t)o;
+  };
+  // inner apply_keyset_rm's forget (map.rs:320-333): the keys' entry clocks, their values while they stay
+  auto forget_keys = [&](u64 rm, u64 km) {
+    while (km) {
+      const unsigned long long j = (unsigned long long)__builtin_ctzll(km);
+      km &= km - 1;
+      if (j >= K2) break;
+      const u64 ej = ld(iec_o + j * A);
+      if (!nm_nz(ej)) continue;
+      const u64 ej2 = nm_fg(ej, rm);
+      st(iec_o + j * A, ej2);
+      if (!nm_nz(ej2)) {
+        if (lane == 0) nv[j] = 0;
+      } else {
+        vals_forget(j, rm);
+      }
+    }
+  };
+  auto id_add = [&](u64 rm, u64 km) {  // deferred.entry(clock).or_default().append(keys) (map.rs:341-342)
+    for (int i = 0; i < nd; ++i) {
+      if (nm_eq(drow[(unsigned long long)i * kWave + lane], rm)) {
+        const u64 mm = dkey[i] | km;
+        if (lane == 0) dkey[i] = mm;
+        return;
+      }
+    }
+    if (nd < kNmId) {
+      drow[(unsigned long long)nd * kWave + lane] = rm;
+      if (lane == 0) dkey[nd] = km;
+      ++nd;
+    } else {
+      dfull = true;
+    }
+  };
+  // the inner Map's Causal::forget (map.rs:85-114)
+  auto inner_forget = [&](u64 x) {
+    if (!nm_nz(x)) return;  // (forget by the empty clock is the identity)
+    for (unsigned long long j = 0; j < K2; ++j) {
+      const u64 ej = ld(iec_o + j * A);
+      if (!nm_nz(ej)) continue;
+      const u64 ej2 = nm_fg(ej, x);
+      st(iec_o + j * A, ej2);
+      if (!nm_nz(ej2)) {
+        if (lane == 0) nv[j] = 0;
+      } else {
+        vals_forget(j, x);
+      }
+    }
+    int o = 0;
+    for (int i = 0; i < nd; ++i) {
+      const u64 r2 = nm_fg(drow[(unsigned long long)i * kWave + lane], x);
+      const u64 ki = dkey[i];
+      if (!nm_nz(r2)) continue;
+      int jj = 0;
+      for (; jj < o; ++jj)  // equal to a kept one: the later keys at the earlier place (collect())
+        if (nm_eq(drow[(unsigned long long)jj * kWave + lane], r2)) break;
+      if (jj < o) {
+        if (lane == 0) dkey[jj] = ki;
+        continue;
+      }
+      drow[(unsigned long long)o * kWave + lane] = r2;
+      if (lane == 0) dkey[o] = ki;
+      ++o;
+    }
+    nd = o;
+    ic = nm_fg(ic, x);
+  };
+
+  // replica r's inner Map at key k
+  auto rin_iec = [&](unsigned long long r) { return p.iec + ((g * R + r) * K + k) * K2 * A; };
+  auto rin_ivc = [&](unsigned long long r) { return p.ivc + ((g * R + r) * K + k) * K2 * V * A; };
+  auto rin_ivv = [&](unsigned long long r) { return p.ivv + ((g * R + r) * K + k) * K2 * V; };
+  auto rin_id = [&](unsigned long long r, u64 &lo, u64 &hi) {
+    const u64 *po = p.id_off + (g * R + r) * K + k;
+    u64 a = __builtin_amdgcn_readfirstlane((unsigned)po[0]) | ((u64)__builtin_amdgcn_readfirstlane((unsigned)(po[0] >> 32)) << 32);
+    u64 b = __builtin_amdgcn_readfirstlane((unsigned)po[1]) | ((u64)__builtin_amdgcn_readfirstlane((unsigned)(po[1] >> 32)) << 32);
+    b = b < p.Di ? b : p.Di;  // (a malformed id_off never reads past the rows: flags bit 5)
+    lo = a < b ? a : b;
+    hi = b;
+  };
+
+  // the replica's inner Map as the key's value (map.rs:193-208): clock, entries, slots, deferred
+  auto inner_load = [&](unsigned long long r, u64 ic2) {
+    ic = ic2;
+    const u64 *ri = rin_iec(r), *rc = rin_ivc(r), *rv = rin_ivv(r);
+    for (unsigned long long j = 0; j < K2; ++j) {
+      const u64 ej = ld(ri + j * A);
+      st(iec_o + j * A, ej);
+      int o = 0;
+      if (nm_nz(ej)) {
+        for (unsigned long long s = 0; s < V; ++s) {
+          const u64 c = ld(rc + (j * V + s) * A);
+          if (!nm_nz(c)) continue;
+          if (o < kNmVs) {
+            st(ivc_o + (j * kNmVs + o) * A, c);
+            ivv_o[j * kNmVs + o] = rv[j * V + s];
+            ++o;
+          } else {
+            vfull = true;
+          }
+        }
+      }
+      if (lane == 0) nv[j] = (uint8_t)o;
+    }
+    nd = 0;
+    u64 lo, hi;
+    rin_id(r, lo, hi);
+    for (u64 d = lo; d < hi; ++d) id_add(ld(p.id_clock + d * A), p.id_keys[d]);
+  };
+
+  // the inner Map::merge (map.rs:140-220) of replica r's inner Map (clock ic2) into the state
+  auto inner_merge = [&](unsigned long long r, u64 ic2) {
+    const u64 *ri = rin_iec(r), *rc = rin_ivc(r), *rv = rin_ivv(r);
+    for (unsigned long long j = 0; j < K2; ++j) {
+      const u64 ej = ld(iec_o + j * A), e2j = ld(ri + j * A);
+      const bool q1 = nm_nz(ej), q2 = nm_nz(e2j);
+      if (!q1 && !q2) continue;
+      const u64 enj = ej == e2j ? ej : nm_max(nm_fg(e2j, ic), nm_fg(ej, ic2));
+      if (!nm_nz(enj)) {  // dropped (or not added): no value merge
+        if (q1) {
+          st(iec_o + j * A, 0);
+          if (lane == 0) nv[j] = 0;
+        }
+        continue;
+      }
+      const u64 xj = nm_fg(q1 ? (q2 ? nm_max(ej, e2j) : ic2) : ic, enj);
+      // the slots: ours (Vec order), then the replica's (MVReg::merge, mvreg.rs:112-128), forgotten by xj
+      u64 cs[kNmVs], co[kNmVin], vs[kNmVs], vo[kNmVin];
+      const int n1 = q1 ? __builtin_amdgcn_readfirstlane((int)nv[j]) : 0;
+      int n2 = 0;
+#pragma unroll
+      for (int s = 0; s < kNmVs; ++s) {
+        cs[s] = s < n1 ? ld(ivc_o + (j * kNmVs + s) * A) : 0;
+        vs[s] = s < n1 ? ivv_o[j * kNmVs + s] : 0;
+      }
+#pragma unroll
+      for (int s = 0; s < kNmVin; ++s) {
+        co[s] = 0;
+        vo[s] = 0;
+      }
+      if (q2) {
+#pragma unroll
+        for (int s = 0; s < kNmVin; ++s) {
+          if ((unsigned long long)s < V) {
+            const u64 c = ld(rc + (j * V + s) * A);
+            if (nm_nz(c)) {  // (an empty slot is no value)
+              co[n2 < kNmVin ? n2 : kNmVin - 1] = c;
+              vo[n2 < kNmVin ? n2 : kNmVin - 1] = rv[j * V + s];
+              ++n2;
+            }
+          }
+        }
+      }
+      // self's values not strictly below one of other's; then other's not strictly below or equal
+      // to a kept one of ours
+      unsigned keep1 = 0, keep2 = 0;
+#pragma unroll
+      for (int s = 0; s < kNmVs; ++s) {
+        if (s >= n1) break;
+        bool dominated = false;
+#pragma unroll
+        for (int t = 0; t < kNmVin; ++t)
+          if (t < n2 && nm_lt(cs[s], co[t])) dominated = true;
+        if (!dominated) keep1 |= 1u << s;
+      }
+#pragma unroll
+      for (int t = 0; t < kNmVin; ++t) {
+        if (t >= n2) break;
+        bool drop = false;
+#pragma unroll
+        for (int s = 0; s < kNmVs; ++s)
+          if (((keep1 >> s) & 1u) && (nm_lt(co[t], cs[s]) || nm_eq(co[t], cs[s]))) drop = true;
+        if (!drop) keep2 |= 1u << t;
+      }
+      // write the merged slots forgotten by xj, in order
+      int o = 0;
+#pragma unroll
+      for (int s = 0; s < kNmVs; ++s) {
+        if (!((keep1 >> s) & 1u)) continue;
+        const u64 c = nm_fg(cs[s], xj);
+        if (!nm_nz(c)) continue;
+        st(ivc_o + (j * kNmVs + o) * A, c);  // (the slots were read into registers above)
+        ivv_o[j * kNmVs + o] = vs[s];
+        ++o;
+      }
+#pragma unroll
+      for (int t = 0; t < kNmVin; ++t) {
+        if (!((keep2 >> t) & 1u)) continue;
+        const u64 c = nm_fg(co[t], xj);
+        if (!nm_nz(c)) continue;
+        if (o < kNmVs) {
+          st(ivc_o + (j * kNmVs + o) * A, c);
+          ivv_o[j * kNmVs + o] = vo[t];
+          ++o;
+        } else {
+          vfull = true;
+        }
+      }
+      if (lane == 0) nv[j] = (uint8_t)o;
+      st(iec_o + j * A, enj);
+    }
+    // apply_keyset_rm of the replica's inner removes, against the pre-merge inner clock (:213-215)
+    u64 lo, hi;
+    rin_id(r, lo, hi);
+    for (u64 d = lo; d < hi; ++d) {
+      const u64 rm = ld(p.id_clock + d * A), km = p.id_keys[d];
+      forget_keys(rm, km);
+      if (__ballot(rm > ic)) id_add(rm, km);
+    }
+    ic = nm_max(ic, ic2);  // (:217)
+    // apply_deferred (:219, :311-316): every held remove forgets its keys again, stays iff !(rm <= ic)
+    int o = 0;
+    for (int i = 0; i < nd; ++i) {
+      const u64 rm = drow[(unsigned long long)i * kWave + lane], km = dkey[i];
+      forget_keys(rm, km);
+      if (__ballot(rm > ic)) {
+        if (o != i) {
+          drow[(unsigned long long)o * kWave + lane] = rm;
+          if (lane == 0) dkey[o] = km;
+        }
+        ++o;
+      }
+    }
+    nd = o;
+  };
+
+  // ---- one outer replica step
+  auto step = [&](unsigned long long r, u64 c2, u64 e2, u64 ic2) {
+    const bool p1 = nm_nz(e), p2 = nm_nz(e2);
+    const u64 en = e == e2 ? e : nm_max(nm_fg(e2, C), nm_fg(e, c2));
+    const bool stays = nm_nz(en);
+    if (stays && (p1 || p2)) {
+      const u64 X = nm_fg(p1 ? (p2 ? nm_max(e, e2) : c2) : C, en);
+      if (p1 && p2) inner_merge(r, ic2);  // our_entry.val.merge(entry.val) (map.rs:183)
+      else if (p2) inner_load(r, ic2);    // the replica's entry (:193-208)
+      inner_forget(X);
+    }
+    e = en;
+    // the outer removes: replica r's own naming k (apply_keyset_rm) and the live ones (apply_deferred)
+    bool chg = false;
+    u64 f = rk;
+    const unsigned r32 = (unsigned)r;
+    if (nxt <= r32) {
+      do {
+        const unsigned idx = (unsigned)lst[li];
+        const u64 rm = ld(p.def_clock + (d0 + idx) * A);
+        f = nm_max(f, rm);
+        if (na < kNmLive) {
+          if (lane == 0) live[na] = idx;
+          put_row(na, rm);
+          ++na;
+          chg = true;
+        } else {
+          full = true;
+        }
+        ++li;
+        advance();
+      } while (nxt <= r32);
+    }
+    if (na > 0 && nm_nz(e)) {
+      e = nm_fg(e, f);
+      if (nm_nz(e)) inner_forget(f);  // entry.val.forget only while the entry stays (map.rs:321-330)
+    }
+    C = nm_max(C, c2);
+    if (na > 0 && (chg || __ballot(C >= T))) {  // outer live set re-test (witness thresholds)
+      bool changed = chg;
+      T = ~0ull;
+      for (int i = 0; i < na;) {
+        const u64 rm = live_row(i);
+        const u64 m = __ballot(rm > C);
+        if (m) {
+          const int wl = __builtin_ctzll(m);
+          T = lane == wl && rm < T ? rm : T;
+          ++i;
+          continue;
+        }
+        changed = true;
+        const int lastp = na - 1;
+        if (i != lastp) {
+          put_row(i, live_row(lastp));
+          const unsigned li_last = live[lastp];
+          if (lane == 0) live[i] = li_last;
+        }
+        --na;
+      }
+      if (changed) {
+        rk = 0;
+        for (int i = 0; i < na; ++i) rk = nm_max(rk, live_row(i));
+      }
+    }
+  };
+
+  // ---- replica rows (c2, e2, ic2) through a register ring, DEPTH steps ahead
+  constexpr int DEPTH = 4;
+  const u64 *pc = p.clock + g * R * A, *pe = p.ec + (g * R * K + k) * A, *pi = p.ic + (g * R * K + k) * A;
+  u64 c2r[DEPTH], e2r[DEPTH], i2r[DEPTH];
+  auto load_step = [&](int s, unsigned long long r) {
+    const unsigned long long rr = r < R ? r : R - 1;
+    c2r[s] = ld(pc + rr * A);
+    e2r[s] = ld(pe + rr * K * A);
+    i2r[s] = ld(pi + rr * K * A);
+  };
+#pragma unroll
+  for (int s = 0; s < DEPTH; ++s) load_step(s, (unsigned long long)s);
+  for (unsigned long long r0 = 0; r0 < R; r0 += DEPTH) {
+#pragma unroll
+    for (int s = 0; s < DEPTH; ++s) {
+      const unsigned long long r = r0 + s;
+      if (r >= R) break;
+      const u64 c2 = c2r[s], e2 = e2r[s], i2 = i2r[s];
+      load_step(s, r + DEPTH);
+      step(r, c2, e2, i2);
+    }
+  }
+
+  // ---- egress: the key's entry (an empty entry clock: absent, inner rows 0), the group's clock
+  const bool pf = nm_nz(e);
+  st(p.o_ec + gk * A, e);
+  st(p.o_ic + gk * A, pf ? ic : 0ull);
+  for (unsigned long long j = 0; j < K2; ++j) {
+    const int n = pf ? __builtin_amdgcn_readfirstlane((int)nv[j]) : 0;
+    if (!pf) st(iec_o + j * A, 0);
+    for (int s = n; s < kNmVs; ++s) {  // (unused slots zero)
+      st(ivc_o + (j * kNmVs + s) * A, 0);
+      ivv_o[j * kNmVs + s] = 0;
+    }
+    if (lane == 0) p.o_nval[gk * K2 + j] = (unsigned)n;
+  }
+  if (k == 0) st(p.o_clock + g * A, C);
+  const int no = pf ? nd : 0;
+  for (int i = 0; i < no; ++i) {
+    st(p.o_id_clock + (gk * kNmId + i) * A, drow[(unsigned long long)i * kWave + lane]);
+    if (lane == 0) p.o_id_keys[gk * kNmId + i] = dkey[i];
+  }
+  if (lane == 0) p.o_id_n[gk] = (unsigned)no;
+  if ((bad || full || dfull || vfull) && lane == 0)
+    atomicOr(p.o_flags + g, (bad ? 2u : 0u) | (full ? 8u : 0u) | (dfull ? 16u : 0u) | (vfull ? 64u : 0u));
+}
+
+// id_off's CSR invariants: entry 0 is 0, entries never decrease, the last is Di (flags bit 5)
+__global__ void map_nested_id_check_kernel(const u64 *off, unsigned long long n, unsigned long long per_group,
+                                           unsigned long long G, unsigned long long Di, unsigned *flags) {
+  for (unsigned long long i = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x; i <= n;
+       i += (unsigned long long)gridDim.x * blockDim.x) {
+    const u64 x = off[i];
+    const bool bad = (i == 0 && x != 0) || (i == n && x != Di) || (i < n && off[i + 1] < x);
+    if (bad) {
+      const unsigned long long g = i / per_group;
+      atomicOr(flags + (g < G ? g : G - 1), 32u);
+    }
+  }
+}
+
+static size_t nm_lds() {
+  return (size_t)kNmWaves * (kNmList * 8 + kNmLive * 4 + kNmRows * kWave * 8 + kNmId * kWave * 8 + kNmId * 8 + kNmK2);
+}
+
+}  // namespace crdt
+
+using namespace crdt;
+
+extern "C" int crdt_map_nested_lub_many(crdt_ctx *ctx, const crdt_map_nested_batch *in, crdt_map_nested_out *out) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
+  CRDT_CHECK_CTX(ctx);
+  if (!in || !out) return fail(ctx, CRDT_EINVAL, "map_nested_lub_many: NULL batch/out");
+  const size_t G = in->G, R = in->R, K = in->K, K2 = in->K2, V = in->V, A = in->A;
+  if (G == 0 || K == 0 || A == 0) return CRDT_OK;
+  if (A > (size_t)kWave) return fail(ctx, CRDT_EUNSUPPORTED, "map_nested_lub_many: A = %zu > %d", A, kWave);
+  if (K2 > (size_t)kNmK2) return fail(ctx, CRDT_EUNSUPPORTED, "map_nested_lub_many: K2 = %zu > %d", K2, kNmK2);
+  if (V > (size_t)kNmVin) return fail(ctx, CRDT_EUNSUPPORTED, "map_nested_lub_many: V = %zu > %d", V, kNmVin);
+  if (!out->clock || !out->ec || !out->ic || (K2 && (!out->iec || !out->ivc || !out->ivv || !out->nval)) ||
+      !out->id_n || !out->id_clock || !out->id_keys || !out->flags)
+    return fail(ctx, CRDT_EINVAL, "map_nested_lub_many: NULL output");
+  if (R > 0 && (!in->clock || !in->ec || !in->ic || !in->id_off || (K2 && !in->iec) || (K2 && V && (!in->ivc || !in->ivv))))
+    return fail(ctx, CRDT_EINVAL, "map_nested_lub_many: NULL input");
+  if (R > 0 && in->Di > 0 && (!in->id_clock || !in->id_keys))
+    return fail(ctx, CRDT_EINVAL, "map_nested_lub_many: Di = %zu inner removes but NULL id_clock / id_keys", in->Di);
+  if (G * K > 0x7fffffffULL * (size_t)kNmWaves || R > 0xfffffffeULL)
+    return fail(ctx, CRDT_EUNSUPPORTED, "map_nested_lub_many: G*K or R too large");
+  if (in->def_off && in->def_off[0] != 0) return fail(ctx, CRDT_EINVAL, "map_nested_lub_many: def_off[0] must be 0");
+  const size_t D = (in->def_off && G > 0) ? in->def_off[G] : 0;
+  for (size_t i = 0; in->def_off && i < G; ++i)
+    if (in->def_off[i + 1] < in->def_off[i])
+      return fail(ctx, CRDT_EINVAL, "map_nested_lub_many: def_off not non-decreasing");
+  if (D > 0 && (!in->def_row || !in->def_clock || !in->def_keys || !out->def_keep || !out->def_keys))
+    return fail(ctx, CRDT_EINVAL, "map_nested_lub_many: deferred buffers missing");
+  if (D > 0xffffffffULL) return fail(ctx, CRDT_EUNSUPPORTED, "map_nested_lub_many: too many deferred");
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  const size_t Kw = (K + 63) / 64;
+  NestedMapPlan p{(const u64 *)in->clock, (const u64 *)in->ec, (const u64 *)in->ic, (const u64 *)in->iec,
+                  (const u64 *)in->ivc, (const u64 *)in->ivv, (const u64 *)in->id_off, (const u64 *)in->id_clock,
+                  (const u64 *)in->id_keys, in->Di, G, R, K, K2, V, A, Kw, nullptr, in->def_row,
+                  (const u64 *)in->def_clock, (const u64 *)in->def_keys, (u64 *)out->clock, (u64 *)out->ec,
+                  (u64 *)out->ic, (u64 *)out->iec, (u64 *)out->ivc, (u64 *)out->ivv, out->nval, out->id_n,
+                  (u64 *)out->id_clock, (u64 *)out->id_keys, out->flags};
+  if (int rc = device_fill(ctx, out->flags, G * sizeof(unsigned), 0)) return rc;
+  if (R == 0) {  // fold of nothing: Map::new()
+    if (int rc = device_fill(ctx, out->clock, G * A * 8, 0)) return rc;
+    if (int rc = device_fill(ctx, out->ec, G * K * A * 8, 0)) return rc;
+    if (int rc = device_fill(ctx, out->ic, G * K * A * 8, 0)) return rc;
+    if (K2) {
+      if (int rc = device_fill(ctx, out->iec, G * K * K2 * A * 8, 0)) return rc;
+      if (int rc = device_fill(ctx, out->ivc, G * K * K2 * kNmVs * A * 8, 0)) return rc;
+      if (int rc = device_fill(ctx, out->ivv, G * K * K2 * kNmVs * 8, 0)) return rc;
+      if (int rc = device_fill(ctx, out->nval, G * K * K2 * sizeof(unsigned), 0)) return rc;
+    }
+    if (int rc = device_fill(ctx, out->id_n, G * K * sizeof(unsigned), 0)) return rc;
+  } else {
+    if (D > 0) {
+      if (int rc = ensure_scratch(ctx, (G + 1) * sizeof(size_t))) return rc;
+      if (int rc = stage_h2d(ctx, ctx->scratch, in->def_off, (G + 1) * sizeof(size_t))) return rc;
+      p.def_off = reinterpret_cast<const size_t *>(ctx->scratch);
+    }
+    {
+      const unsigned long long n = (unsigned long long)G * R * K;
+      const unsigned blocks = (unsigned)std::min<unsigned long long>((n + 256) / 256, 4096);
+      hipLaunchKernelGGL(map_nested_id_check_kernel, dim3(blocks), dim3(256), 0, ctx->stream, p.id_off, n,
+                         (unsigned long long)R * K, (unsigned long long)G, (unsigned long long)in->Di, out->flags);
+      CRDT_HIP(ctx, hipGetLastError());
+    }
+    timing_begin(ctx, "map_nested_fold");
+    const unsigned long long blocks = (G * K + kNmWaves - 1) / kNmWaves;
+    hipLaunchKernelGGL(map_nested_fold_kernel, dim3((unsigned)blocks), dim3(kNmWaves * kWave), nm_lds(), ctx->stream, p);
+    const hipError_t he = hipGetLastError();
+    timing_end(ctx);
+    if (he != hipSuccess) return hip_fail(ctx, he, "map_nested_fold_kernel launch");
+  }
+  if (D == 0) return CRDT_OK;
+  DefPlan q{};  // the outer Map's surviving removes (!(rm <= C_final)), identical clocks merged
+  q.G = G;
+  q.D = D;
+  q.M = K;
+  q.A = A;
+  q.Mw = Kw;
+  q.def_clock = (const u64 *)in->def_clock;
+  q.def_members = (const u64 *)in->def_keys;
+  q.out_clock = (const u64 *)out->clock;
+  q.out_entries = nullptr;
+  q.apply_ceiling = 0;
+  q.out_keep = out->def_keep;
+  q.out_members = (u64 *)out->def_keys;
+  return launch_deferred(ctx, in->def_off, q);
+}

@@ -37,6 +37,7 @@ struct MapOrswotPlan {
   const u64 *clock, *ec, *oc, *ent;   // (G,R,A), (G,R,K,A), (G,R,K,A), (G,R,K,M,A)
   const u64 *vd_off;                  // nested deferred CSR over (g, r, k): G*R*K + 1 (device)
   const u64 *vd_clock, *vd_mem;       // (Dv, A), (Dv) member bitmasks
+  unsigned long long Dv;              // (a step reads rows [min(lo, hi'), hi') with hi' = min(hi, Dv))
   unsigned long long G, R, K, M, A, Kw;
   const size_t *def_off;  // device copy (G+1), or null: no Map-level removes
   const uint32_t *def_row;
@@ -193,18 +194,27 @@ __global__ __launch_bounds__(kMoWaves * kWave) void map_orswot_fold_kernel(MapOr
     const u64 en = e == e2 ? e : mo_max(mo_fg(e2, C), mo_fg(e, c2));  // (the forgets are <= e where e == e2)
     const u64 y = p1 ? (p2 ? mo_max(e, e2) : c2) : C;
     const u64 X = mo_fg(y, en);
-    if (p1 && p2) {  // our_entry.val.merge(entry.val) (map.rs:183) = Orswot::merge
+    // An empty joined clock drops the entry without touching its value (map.rs:178-180, :191-192:
+    // no val.merge), so the value work runs only while the entry stays; a dropped entry's stale rows
+    // are never read again (p1 is false until the key is re-added, which overwrites them).
+    const bool stays = mo_nz(en);
+    if (p1 && p2 && stays) {  // our_entry.val.merge(entry.val) (map.rs:183) = Orswot::merge
 #pragma unroll
       for (int m = 0; m < MT; ++m)
         E[m] = E[m] == E2[m] ? E[m] : mo_max(mo_fg(E2[m], oc), mo_fg(E[m], o2));
+      // apply_rm of each of the replica's removes against the clock BEFORE oc |= oc2 (orswot.rs:
+      // 141-143, :230-238): its members are forgotten, and it is deferred only if !(rm <= oc)
       for (u64 d = vlo; d < vhi; ++d) {
         const u64 rm = ld(p.vd_clock + d * A), msk = p.vd_mem[d];
-        vd_add(rm, msk);
+        forget_members(rm, msk);
+        if (__ballot(rm > oc)) vd_add(rm, msk);
       }
-      for (int i = 0; i < nd; ++i) forget_members(vrow[(unsigned long long)i * kWave + lane], vmsk[i]);
+      // apply_deferred (:147, :281-286): every remove still held forgets its members again with
+      // the merged clock, and stays while !(rm <= oc)
       oc = mo_max(oc, o2);
+      for (int i = 0; i < nd; ++i) forget_members(vrow[(unsigned long long)i * kWave + lane], vmsk[i]);
       vd_keep_live();
-    } else if (p2) {  // the replica's entry (map.rs:193-208)
+    } else if (p2 && !p1 && stays) {  // the replica's entry (map.rs:193-208)
 #pragma unroll
       for (int m = 0; m < MT; ++m) E[m] = E2[m];
       oc = o2;
@@ -214,7 +224,7 @@ __global__ __launch_bounds__(kMoWaves * kWave) void map_orswot_fold_kernel(MapOr
         vd_add(rm, msk);
       }
     }
-    if (p1 || p2) value_forget(X);
+    if (stays && (p1 || p2)) value_forget(X);
     e = en;
     // the Map's removes: replica r's own (apply_keyset_rm) and the live ones (apply_deferred)
     bool chg = false;
@@ -297,9 +307,10 @@ __global__ __launch_bounds__(kMoWaves * kWave) void map_orswot_fold_kernel(MapOr
   auto run = [&](unsigned long long r, int s, bool last_check) {
     const u64 vlo = __builtin_amdgcn_readfirstlane((unsigned)vlr[s]) |
                     ((u64)__builtin_amdgcn_readfirstlane((unsigned)(vlr[s] >> 32)) << 32);
-    const u64 vhi = __builtin_amdgcn_readfirstlane((unsigned)vhr[s]) |
-                    ((u64)__builtin_amdgcn_readfirstlane((unsigned)(vhr[s] >> 32)) << 32);
-    step(r, c2r[s], e2r[s], o2r[s], E2r[s], vlo, vhi);
+    u64 vhi = __builtin_amdgcn_readfirstlane((unsigned)vhr[s]) |
+              ((u64)__builtin_amdgcn_readfirstlane((unsigned)(vhr[s] >> 32)) << 32);
+    vhi = vhi < p.Dv ? vhi : p.Dv;  // (a malformed vd_off never reads past the rows: flags bit 5)
+    step(r, c2r[s], e2r[s], o2r[s], E2r[s], vlo < vhi ? vlo : vhi, vhi);
     load_step(s, last_check);
   };
 #pragma unroll
@@ -343,6 +354,21 @@ __global__ __launch_bounds__(kMoWaves * kWave) void map_orswot_fold_kernel(MapOr
     atomicOr(p.o_flags + g, (bad ? 2u : 0u) | (full ? 8u : 0u) | (vfull ? 16u : 0u));
 }
 
+// vd_off's CSR invariants: entry 0 is 0, entries never decrease, the last is Dv.  A
+// violation marks the group of the offending entry (flags bit 5); the fold clamps its reads anyway.
+__global__ void map_orswot_vd_check_kernel(const u64 *vd_off, unsigned long long n, unsigned long long per_group,
+                                           unsigned long long G, unsigned long long Dv, unsigned *flags) {
+  for (unsigned long long i = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x; i <= n;
+       i += (unsigned long long)gridDim.x * blockDim.x) {
+    const u64 x = vd_off[i];
+    const bool bad = (i == 0 && x != 0) || (i == n && x != Dv) || (i < n && vd_off[i + 1] < x);
+    if (bad) {
+      const unsigned long long g = i / per_group;
+      atomicOr(flags + (g < G ? g : G - 1), 32u);
+    }
+  }
+}
+
 static size_t mo_lds() {
   return (size_t)kMoWaves * (kMoList * 8 + kMoLive * 4 + kMoRows * kWave * 8 + kMoVd * kWave * 8 + kMoVd * 8);
 }
@@ -371,6 +397,8 @@ extern "C" int crdt_map_orswot_lub_many(crdt_ctx *ctx, const crdt_map_orswot_bat
     return fail(ctx, CRDT_EINVAL, "map_orswot_lub_many: NULL output");
   if (R > 0 && (!in->clock || !in->ec || !in->oc || (M && !in->ent) || !in->vd_off))
     return fail(ctx, CRDT_EINVAL, "map_orswot_lub_many: NULL input");
+  if (R > 0 && in->Dv > 0 && (!in->vd_clock || !in->vd_mem))
+    return fail(ctx, CRDT_EINVAL, "map_orswot_lub_many: Dv = %zu nested removes but NULL vd_clock / vd_mem", in->Dv);
   if (G * K > 0x7fffffffULL * (size_t)kMoWaves || R > 0xfffffffeULL)
     return fail(ctx, CRDT_EUNSUPPORTED, "map_orswot_lub_many: G*K or R too large");
   if (in->def_off && in->def_off[0] != 0) return fail(ctx, CRDT_EINVAL, "map_orswot_lub_many: def_off[0] must be 0");
@@ -384,7 +412,7 @@ extern "C" int crdt_map_orswot_lub_many(crdt_ctx *ctx, const crdt_map_orswot_bat
   CRDT_HIP(ctx, hipSetDevice(ctx->device));
   const size_t Kw = (K + 63) / 64;
   MapOrswotPlan p{(const u64 *)in->clock, (const u64 *)in->ec, (const u64 *)in->oc, (const u64 *)in->ent,
-                  (const u64 *)in->vd_off, (const u64 *)in->vd_clock, (const u64 *)in->vd_mem, G, R, K, M, A, Kw,
+                  (const u64 *)in->vd_off, (const u64 *)in->vd_clock, (const u64 *)in->vd_mem, in->Dv, G, R, K, M, A, Kw,
                   nullptr, in->def_row, (const u64 *)in->def_clock, (const u64 *)in->def_keys,
                   (u64 *)out->clock, (u64 *)out->ec, (u64 *)out->oc, (u64 *)out->ent, (u64 *)out->vd_clock,
                   (u64 *)out->vd_mem, out->vd_n, out->flags};
@@ -401,6 +429,13 @@ extern "C" int crdt_map_orswot_lub_many(crdt_ctx *ctx, const crdt_map_orswot_bat
       if (int rc = ensure_scratch(ctx, (G + 1) * sizeof(size_t))) return rc;
       if (int rc = stage_h2d(ctx, ctx->scratch, in->def_off, (G + 1) * sizeof(size_t))) return rc;
       p.def_off = reinterpret_cast<const size_t *>(ctx->scratch);
+    }
+    {
+      const unsigned long long n = (unsigned long long)G * R * K;
+      const unsigned blocks = (unsigned)std::min<unsigned long long>((n + 256) / 256, 4096);
+      hipLaunchKernelGGL(map_orswot_vd_check_kernel, dim3(blocks), dim3(256), 0, ctx->stream, p.vd_off, n,
+                         (unsigned long long)R * K, (unsigned long long)G, (unsigned long long)in->Dv, out->flags);
+      CRDT_HIP(ctx, hipGetLastError());
     }
     timing_begin(ctx, "map_orswot_fold");
     // (member rows past M are zero and still joined: the register capacity follows M)

@@ -23,12 +23,24 @@
 // values only, so a bad argument or an empty shard on one rank never leaves the others blocked.
 // The header exchange runs on a side stream that waits only for the work issued BEFORE the call,
 // so it overlaps the local fold instead of adding a host round trip after it.
+// RCCL is bound at run time, not at link time: rccl.h supplies only the types and
+// enum values (stable across RCCL 2.x), and the nine entry points used here are resolved by dlsym
+// from ONE librccl.so.1 chosen in this order:
+//   1. $CRDT_RCCL_LIB, when set (an explicit path: the caller names the RCCL it wants);
+//   2. the librccl.so.1 the process has already loaded (RTLD_NOLOAD) — inside a torch process that is
+//      torch's own RCCL, so the library and torch.distributed share one RCCL;
+//   3. librccl.so.1 through the library's RUNPATH (/opt/rocm/lib), for a caller without torch.
+// A library loaded by step 3 owns the soname, so a torch imported later binds the same copy.
+#include <dlfcn.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <initializer_list>
+#include <mutex>
+#include <string>
 
 #include "common.hpp"
 #include "shard_host.hpp"
@@ -37,8 +49,91 @@ namespace crdt {
 
 static_assert(CRDT_UNIQUE_ID_BYTES == NCCL_UNIQUE_ID_BYTES, "unique id size");
 
+// The oldest RCCL whose ABI for these calls this file was checked against (ncclUint64 / ncclMax
+// exist since 2.x; the version code is major*10000 + minor*100 + patch since 2.9).
+constexpr int kRcclMinVersion = 21800;
+
+struct RcclApi {
+  bool ok = false;
+  int version = 0;
+  std::string path, origin, err;
+  ncclResult_t (*GetVersion)(int *) = nullptr;
+  ncclResult_t (*GetUniqueId)(ncclUniqueId *) = nullptr;
+  ncclResult_t (*CommInitRank)(ncclComm_t *, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*AllReduce)(const void *, void *, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
+                            hipStream_t) = nullptr;
+  ncclResult_t (*AllGather)(const void *, void *, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*GroupStart)() = nullptr;
+  ncclResult_t (*GroupEnd)() = nullptr;
+  const char *(*GetErrorString)(ncclResult_t) = nullptr;
+};
+
+static bool rccl_bind(RcclApi &a, void *h) {
+  auto sym = [&](const char *n) { return dlsym(h, n); };
+#define CRDT_RCCL_SYM(field, name) a.field = reinterpret_cast<decltype(a.field)>(sym(name))
+  CRDT_RCCL_SYM(GetVersion, "ncclGetVersion");
+  CRDT_RCCL_SYM(GetUniqueId, "ncclGetUniqueId");
+  CRDT_RCCL_SYM(CommInitRank, "ncclCommInitRank");
+  CRDT_RCCL_SYM(CommDestroy, "ncclCommDestroy");
+  CRDT_RCCL_SYM(AllReduce, "ncclAllReduce");
+  CRDT_RCCL_SYM(AllGather, "ncclAllGather");
+  CRDT_RCCL_SYM(GroupStart, "ncclGroupStart");
+  CRDT_RCCL_SYM(GroupEnd, "ncclGroupEnd");
+  CRDT_RCCL_SYM(GetErrorString, "ncclGetErrorString");
+#undef CRDT_RCCL_SYM
+  if (!a.GetVersion || !a.GetUniqueId || !a.CommInitRank || !a.CommDestroy || !a.AllReduce || !a.AllGather ||
+      !a.GroupStart || !a.GroupEnd || !a.GetErrorString) {
+    a.err = "an RCCL entry point is missing from the loaded library";
+    return false;
+  }
+  return true;
+}
+
+// Loaded once per process; never unloaded (communicators may outlive any one ctx).
+static const RcclApi &rccl() {
+  static RcclApi a;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    void *h = nullptr;
+    const char *env = std::getenv("CRDT_RCCL_LIB");
+    if (env && *env) {
+      h = dlopen(env, RTLD_NOW | RTLD_LOCAL);
+      a.origin = "CRDT_RCCL_LIB";
+      if (!h) {
+        a.err = std::string("dlopen($CRDT_RCCL_LIB=") + env + "): " + dlerror();
+        return;
+      }
+    } else if ((h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD))) {
+      a.origin = "already loaded by the process (shared with torch.distributed when torch is imported)";
+    } else if ((h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL))) {
+      a.origin = "loaded by libcrdt_gpu (RUNPATH)";
+    } else {
+      a.err = std::string("dlopen(librccl.so.1): ") + dlerror();
+      return;
+    }
+    if (!rccl_bind(a, h)) return;
+    Dl_info info{};
+    if (dladdr(reinterpret_cast<void *>(a.GetVersion), &info) && info.dli_fname) a.path = info.dli_fname;
+    if (a.GetVersion(&a.version) != ncclSuccess) a.version = 0;
+    if (a.version < kRcclMinVersion) {
+      a.err = "RCCL version " + std::to_string(a.version) + " at " + a.path + " is older than " +
+              std::to_string(kRcclMinVersion);
+      return;
+    }
+    a.ok = true;
+  });
+  return a;
+}
+
+static int need_rccl(crdt_ctx *ctx) {
+  const RcclApi &a = rccl();
+  if (!a.ok) return fail(ctx, CRDT_ECOMM, "RCCL unavailable: %s", a.err.c_str());
+  return CRDT_OK;
+}
+
 static int nccl_fail(crdt_ctx *ctx, ncclResult_t r, const char *what) {
-  return fail(ctx, CRDT_ECOMM, "%s: %s", what, ncclGetErrorString(r));
+  return fail(ctx, CRDT_ECOMM, "%s: %s", what, rccl().GetErrorString(r));
 }
 
 #define CRDT_NCCL(ctx, expr)                                   \
@@ -53,7 +148,7 @@ static int nccl_fail(crdt_ctx *ctx, ncclResult_t r, const char *what) {
     if (_s != CRDT_OK) return _s;  \
   } while (0)
 
-static void destroy_comm(void *c) { (void)ncclCommDestroy((ncclComm_t)c); }
+static void destroy_comm(void *c) { (void)rccl().CommDestroy((ncclComm_t)c); }
 
 // ctx-owned exchange buffer slot i (grown on demand, stream drained before a re-allocation)
 static int sbuf(crdt_ctx *ctx, int i, size_t bytes, void **out) {
@@ -86,11 +181,11 @@ static int need_comm(crdt_ctx *ctx) {
 enum class Red : int { Max = CRDT_RED_MAX, Min = CRDT_RED_MIN, Sum = CRDT_RED_SUM };
 
 static int coll_group_begin(crdt_ctx *ctx) {
-  if (ctx->comm) CRDT_NCCL(ctx, ncclGroupStart());
+  if (ctx->comm) CRDT_NCCL(ctx, rccl().GroupStart());
   return CRDT_OK;
 }
 static int coll_group_end(crdt_ctx *ctx) {
-  if (ctx->comm) CRDT_NCCL(ctx, ncclGroupEnd());
+  if (ctx->comm) CRDT_NCCL(ctx, rccl().GroupEnd());
   return CRDT_OK;
 }
 
@@ -103,7 +198,7 @@ static int coll_allreduce(crdt_ctx *ctx, const u64 *src, u64 *dst, size_t n, Red
   if (n == 0) return CRDT_OK;
   if (ctx->comm) {
     const ncclRedOp_t r = op == Red::Max ? ncclMax : (op == Red::Min ? ncclMin : ncclSum);
-    CRDT_NCCL(ctx, ncclAllReduce(src, dst, n, ncclUint64, r, (ncclComm_t)ctx->comm, ctx->stream));
+    CRDT_NCCL(ctx, rccl().AllReduce(src, dst, n, ncclUint64, r, (ncclComm_t)ctx->comm, ctx->stream));
     return CRDT_OK;
   }
   std::vector<uint64_t> h(n);
@@ -120,9 +215,9 @@ static int coll_allgather(crdt_ctx *ctx, const void *send, void *recv, size_t by
   if (bytes == 0) return CRDT_OK;
   if (ctx->comm) {
     if (bytes % 8 == 0)
-      CRDT_NCCL(ctx, ncclAllGather(send, recv, bytes / 8, ncclUint64, (ncclComm_t)ctx->comm, ctx->stream));
+      CRDT_NCCL(ctx, rccl().AllGather(send, recv, bytes / 8, ncclUint64, (ncclComm_t)ctx->comm, ctx->stream));
     else
-      CRDT_NCCL(ctx, ncclAllGather(send, recv, bytes, ncclUint8, (ncclComm_t)ctx->comm, ctx->stream));
+      CRDT_NCCL(ctx, rccl().AllGather(send, recv, bytes, ncclUint8, (ncclComm_t)ctx->comm, ctx->stream));
     return CRDT_OK;
   }
   std::vector<uint8_t> hs(bytes), hr(bytes * (size_t)ctx->nranks);
@@ -219,7 +314,7 @@ static int agree_exchange(crdt_ctx *ctx, const Hdr &mine) {
     uint64_t *d = static_cast<uint64_t *>(ctx->a_dev);
     CRDT_HIP(ctx, hipStreamWaitEvent(ctx->astream, ctx->a_main, 0));
     CRDT_HIP(ctx, hipMemcpyAsync(d + W * kHdr, send_h, kHdr * 8, hipMemcpyHostToDevice, ctx->astream));
-    CRDT_NCCL(ctx, ncclAllGather(d + W * kHdr, d, kHdr, ncclUint64, (ncclComm_t)ctx->comm, ctx->astream));
+    CRDT_NCCL(ctx, rccl().AllGather(d + W * kHdr, d, kHdr, ncclUint64, (ncclComm_t)ctx->comm, ctx->astream));
     CRDT_HIP(ctx, hipMemcpyAsync(h, d, W * kHdr * 8, hipMemcpyDeviceToHost, ctx->astream));
     CRDT_HIP(ctx, hipEventRecord(ctx->a_done, ctx->astream));
     CRDT_HIP(ctx, hipEventSynchronize(ctx->a_done));
@@ -354,8 +449,9 @@ extern "C" {
 
 int crdt_comm_unique_id(uint8_t *id) {
   if (!id) return CRDT_EINVAL;
+  if (!rccl().ok) return CRDT_ECOMM;
   ncclUniqueId u;
-  if (ncclGetUniqueId(&u) != ncclSuccess) return CRDT_ECOMM;
+  if (rccl().GetUniqueId(&u) != ncclSuccess) return CRDT_ECOMM;
   std::memcpy(id, u.internal, NCCL_UNIQUE_ID_BYTES);
   return CRDT_OK;
 }
@@ -366,19 +462,16 @@ int crdt_ctx_comm_init(crdt_ctx *ctx, const uint8_t *id, int nranks, int rank) {
     return fail(ctx, CRDT_EINVAL, "crdt_ctx_comm_init: bad id / nranks %d / rank %d", nranks, rank);
   if (ctx->comm || ctx->has_ops) return fail(ctx, CRDT_EINVAL, "crdt_ctx_comm_init: ctx already has a communicator");
   CRDT_HIP(ctx, hipSetDevice(ctx->device));
-  // the process may have loaded another librccl.so.1 first (torch ships its own): note a mismatch
-  int v = 0;
-  ctx->comm_note.clear();
-  if (ncclGetVersion(&v) == ncclSuccess && v != NCCL_VERSION_CODE) {
-    char buf[160];
-    std::snprintf(buf, sizeof buf, "RCCL runtime version %d != rccl.h version %d this library was compiled against",
-                  v, NCCL_VERSION_CODE);
-    ctx->comm_note = buf;
-  }
+  CRDT_TRY(need_rccl(ctx));
+  // which RCCL this communicator runs on (one copy per process: see the binding order above)
+  const RcclApi &api = rccl();
+  ctx->comm_note = "RCCL " + std::to_string(api.version / 10000) + "." + std::to_string(api.version / 100 % 100) +
+                   "." + std::to_string(api.version % 100) + " (" + std::to_string(api.version) + ") at " + api.path +
+                   ", " + api.origin;
   ncclUniqueId u;
   std::memcpy(u.internal, id, NCCL_UNIQUE_ID_BYTES);
   ncclComm_t c = nullptr;
-  CRDT_NCCL(ctx, ncclCommInitRank(&c, nranks, u, rank));
+  CRDT_NCCL(ctx, api.CommInitRank(&c, nranks, u, rank));
   ctx->comm = c;
   ctx->nranks = nranks;
   ctx->rank = rank;
@@ -404,7 +497,7 @@ int crdt_ctx_comm_destroy(crdt_ctx *ctx) {
   CRDT_CHECK_CTX(ctx);
   (void)hipStreamSynchronize(ctx->stream);
   comm_release(ctx);
-  if (ctx->comm) CRDT_NCCL(ctx, ncclCommDestroy((ncclComm_t)ctx->comm));
+  if (ctx->comm) CRDT_NCCL(ctx, rccl().CommDestroy((ncclComm_t)ctx->comm));
   ctx->comm = nullptr;
   ctx->has_ops = false;
   ctx->ops = crdt_comm_ops{};
@@ -422,9 +515,8 @@ int crdt_ctx_comm_info(const crdt_ctx *ctx, int *nranks, int *rank) {
 }
 
 const char *crdt_ctx_comm_note(const crdt_ctx *ctx, int *runtime, int *header) {
-  int v = 0;
-  if (ncclGetVersion(&v) != ncclSuccess) v = 0;
-  if (runtime) *runtime = v;
+  const RcclApi &api = rccl();
+  if (runtime) *runtime = api.ok ? api.version : 0;
   if (header) *header = NCCL_VERSION_CODE;
   return ctx ? ctx->comm_note.c_str() : "";
 }

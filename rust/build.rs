@@ -1,6 +1,7 @@
 // build.rs of the `crdts` crate's `gpu` feature: the hipcc step.  Builds libcrdt_gpu.so for gfx950
 // (`make -C <CRDT_GPU_DIR>`: hipcc --offload-arch=gfx950 of the HIP kernels and the C ABI, see
-// rust-crdt_amd/Makefile) and links it, with the ROCm runtime and RCCL, into the crate.
+// rust-crdt_amd/Makefile) and links it, with the ROCm runtime, into the crate.  RCCL is bound by
+// the library at run time (CRDT_RCCL_LIB, else the process's librccl.so.1, else /opt/rocm/lib).
 //
 //   CRDT_GPU_DIR   directory holding the Makefile and csrc/ (default: ../rust-crdt_amd)
 //   ROCM_PATH      ROCm install (default: /opt/rocm)
@@ -35,7 +36,6 @@ fn main() {
     println!("cargo:rustc-link-arg=-Wl,-rpath,{}", dir.display());
     println!("cargo:rustc-link-search=native={}/lib", rocm);
     println!("cargo:rustc-link-lib=dylib=amdhip64");
-    println!("cargo:rustc-link-lib=dylib=rccl");
     println!("cargo:rustc-link-arg=-Wl,-rpath,{}/lib", rocm);
     for f in ["csrc", "Makefile"] {
         println!("cargo:rerun-if-changed={}", dir.join(f).display());

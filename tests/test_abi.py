@@ -61,7 +61,7 @@ def test_ctypes_struct_layout_matches_header():
     assert ctypes.sizeof(abi.MapOut) == 10 * 8
     assert ctypes.sizeof(abi.MapCounterBatch) == 18 * 8
     assert ctypes.sizeof(abi.MapCounterOut) == 6 * 8
-    assert ctypes.sizeof(abi.MapOrswotBatch) == 16 * 8
+    assert ctypes.sizeof(abi.MapOrswotBatch) == 17 * 8
     assert ctypes.sizeof(abi.MapOrswotOut) == 10 * 8
 
 

@@ -192,3 +192,31 @@ def test_map_counter_remove_empties_last_actor(mcctx, W):
     d = O.map_counter_to_dense(maps, 2, A, W)
     res, kw = _run(mcctx, d)
     _same(_got_maps(res, kw, 1)[0], exp)
+
+
+@pytest.mark.parametrize("W", [1, 2])
+def test_map_counter_auto_keys_per_wave_keeps_per_key_capacity(gpu_ctx, W):
+    """with keys per wave chosen automatically (K = 4,096, A = 16: two keys per wave), keys 0
+    and 1 share a wave and hold 300 live removes each (600 together, past the shared 512-entry list);
+    the per-key limit of the header still holds — the group is re-folded one key per wave."""
+    R, K, A = 4, 4096, 16
+    vnew = O.GCounter if W == 1 else O.PNCounter
+    maps = []
+    for r in range(R):
+        m = O.Map(vnew)
+        m.clock = O.VClock({0: r + 1, 1: r + 1})
+        for k in (0, 1, 2):
+            v = vnew()
+            (v.inner if W == 1 else v.p.inner).dots[k % A] = r + 2
+            m.entries[k] = O.MapEntry(O.VClock({0: r + 1}), v)
+        if r == 1:
+            for i in range(300):
+                m.deferred[O.VClock({3: 1000 + i})] = {0}
+                m.deferred[O.VClock({5: 1000 + i})] = {1}
+        maps.append(m)
+    exp = O.map_fold_objects(maps)
+    assert len(exp.deferred) == 600
+    d = O.map_counter_to_dense(maps, K, A, W)
+    res, kw = _run(gpu_ctx, d)  # the default ctx: mckpw=0 (automatic)
+    assert int(res.flags.cpu()[0]) == 0
+    _same(_got_maps(res, kw, 1)[0], exp)

@@ -1,0 +1,359 @@
+"""GPU parity: Map<K, Map<K2, MVReg<u64>>> lub_many (crdt_map_nested_lub_many, round 5) — the nested
+type of the reference's own Map tests (TMap, /root/reference/test/map.rs:10; TestMap, src/map.rs:359).
+
+Every merge of the reference's TMap tests runs on the GPU here: `gpu_merge(a, b)` interns the two
+states' actors / keys to dense indices, folds [a, b] with the kernel (Map::new().merge(a).merge(b) ==
+a.merge(b) for the reference's states) and turns the result back into oracle objects, so the
+reference's own assertions check the kernel:
+  test/map.rs:148-174 (reset-remove), :197-235 (add bias), :331-362, :364-404, :406-430, :432-478,
+  :480-516 (the quickcheck regressions) and the merge laws of :524-827 (commutative, associative,
+  idempotent, merge-followed-by-merge, op exchange == merge) over seeded quickcheck-style ops.
+Plus op-replay histories (inner writes and inner removes read at replicas that have seen more, so
+removes defer at both levels) folded over many replicas against the oracle's left fold."""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+from gpu_util import to_dev, to_host
+from oracle import Dot, Map, MapRm, MapUp, MVReg, MVRegPut, VClock
+
+pytestmark = pytest.mark.gpu
+
+import crdts_gpu as cg  # noqa: E402
+
+
+def TMap():  # test/map.rs:9
+    return Map(lambda: Map(MVReg))
+
+
+def vc(*dots):
+    return VClock.from_dots(Dot(a, c) for a, c in dots)
+
+
+def apply_ops(m, ops):  # test/map.rs:473-477
+    for op in ops:
+        m.apply(op)
+
+
+def build_ops(actor, ops_data):  # test/map.rs:11-46
+    ops = []
+    for i, (choice, inner_choice, key, inner_key, val) in enumerate(ops_data):
+        clock = vc((actor, i))
+        if choice % 2 == 0:
+            if inner_choice % 2 == 0:
+                inner = MapUp(clock.inc(actor), inner_key, MVRegPut(clock.copy(), val))
+            else:
+                inner = MapRm(clock.copy(), {inner_key})
+            ops.append(MapUp(clock.inc(actor), key, inner))
+        else:
+            ops.append(MapRm(clock.copy(), {key}))
+    return actor, ops
+
+
+# ---- dense interning of reference-shaped states ----------------------------------------------------
+class _Dict:
+    def __init__(self, items):
+        self.fwd = {x: i for i, x in enumerate(sorted(items))}
+        self.inv = {i: x for x, i in self.fwd.items()}
+
+
+def _clocks(m):
+    yield m.clock
+    for rm in m.deferred:
+        yield rm
+    for e in m.entries.values():
+        yield e.clock
+        yield e.val.clock
+        for rm in e.val.deferred:
+            yield rm
+        for ie in e.val.entries.values():
+            yield ie.clock
+            for c, _ in ie.val.vals:
+                yield c
+
+
+def _map_clock(c, d):
+    return VClock({d[a]: n for a, n in c.dots.items()})
+
+
+def _intern(maps):
+    acts, keys, ikeys = set(), set(), set()
+    for m in maps:
+        for c in _clocks(m):
+            acts |= set(c.dots)
+        keys |= set(m.entries)
+        for ks in m.deferred.values():
+            keys |= set(ks)
+        for e in m.entries.values():
+            ikeys |= set(e.val.entries)
+            for ks in e.val.deferred.values():
+                ikeys |= set(ks)
+    A, K, J = _Dict(acts or {0}), _Dict(keys or {0}), _Dict(ikeys or {0})
+
+    def conv(m, a, k, j):
+        n = TMap()
+        n.clock = _map_clock(m.clock, a)
+        for rm, ks in m.deferred.items():
+            n.deferred[_map_clock(rm, a)] = {k[x] for x in ks}
+        for key, e in m.entries.items():
+            inner = Map(MVReg)
+            inner.clock = _map_clock(e.val.clock, a)
+            for rm, ks in e.val.deferred.items():
+                inner.deferred[_map_clock(rm, a)] = {j[x] for x in ks}
+            for ik, ie in e.val.entries.items():
+                inner.entries[j[ik]] = O.MapEntry(_map_clock(ie.clock, a),
+                                                  MVReg([(_map_clock(c, a), v) for c, v in ie.val.vals]))
+            n.entries[k[key]] = O.MapEntry(_map_clock(e.clock, a), inner)
+        return n
+
+    dense = [conv(m, A.fwd, K.fwd, J.fwd) for m in maps]
+    back = lambda m: conv(m, A.inv, K.inv, J.inv)  # noqa: E731
+    return dense, back, len(A.fwd), len(K.fwd), len(J.fwd)
+
+
+def gpu_fold(ctx, maps):
+    """acc = Map::new(); for m in maps: acc.merge(m), every merge on the GPU (one nested_lub_many)."""
+    dense, back, A, K, K2 = _intern(maps)
+    if A > 64 or K2 > 64:
+        pytest.skip("more than 64 actors / inner keys in one case")
+    V = max([len(ie.val.vals) for m in dense for e in m.entries.values() for ie in e.val.entries.values()] + [1])
+    d = O.nested_map_to_dense(dense, K, K2, A, V)
+    D = d["def_row"].shape[0]
+    kw = {}
+    if D:
+        kw = dict(def_off=[0, D], def_row=torch.from_numpy(d["def_row"].astype(np.int32)).cuda(),
+                  def_clock=to_dev(d["def_clock"]), def_keys=to_dev(d["def_keys"]))
+    Di = d["id_clock"].shape[0]
+    ikw = dict(id_clock=to_dev(d["id_clock"]), id_keys=to_dev(d["id_keys"])) if Di else {}
+    res = cg.map.nested_lub_many(to_dev(d["clock"]), to_dev(d["ec"]), to_dev(d["ic"]), to_dev(d["iec"]),
+                                 to_dev(d["ivc"]), to_dev(d["ivv"]), to_dev(d["id_off"]), ctx=ctx, **ikw, **kw)
+    dset = []
+    if D:
+        dset = [(np.array(rm, np.uint64), ks)
+                for rm, ks in cg.map.deferred_set(kw["def_clock"], res.def_keep, res.def_keys)]
+    idn = res.id_n.cpu().numpy()
+    idc, idk = to_host(res.id_clock), to_host(res.id_keys)
+    ideferred = {k: [(idc[k, i], O.bitmap_members(idk[k, i:i + 1])) for i in range(int(idn[k]))]
+                 for k in range(K)}
+    got = O.dense_to_nested_map(to_host(res.clock), to_host(res.ec), to_host(res.ic), to_host(res.iec),
+                                to_host(res.ivc), to_host(res.ivv), res.nval.cpu().numpy(), ideferred, dset)
+    return back(got)
+
+
+@pytest.fixture
+def gm(gpu_ctx):
+    def merge(a, b):  # a.merge(b) on the GPU; returns the merged state
+        return gpu_fold(gpu_ctx, [a, b])
+    return merge
+
+
+def read_nested(m, k1, k2):
+    v = m.get(k1).val
+    if v is None:
+        return None
+    r = v.get(k2).val
+    return None if r is None else r.read().val
+
+
+# ---- the reference's TMap tests, every merge on the GPU --------------------------------------------
+def test_reset_remove_semantics(gm):  # test/map.rs:148-174
+    m1 = TMap()
+    m1.apply(m1.update(101, m1.get(101).derive_add_ctx(74),
+                       lambda mp, c: mp.update(110, c, lambda r, c2: r.write(32, c2))))
+    m2 = m1.copy()
+    m1.apply(m1.rm(101, m1.get(101).derive_rm_ctx()))
+    m2.apply(m2.update(101, m2.get(101).derive_add_ctx(37),
+                       lambda mp, c: mp.update(220, c, lambda r, c2: r.write(5, c2))))
+    snap = m1.copy()
+    m1 = gm(m1, m2)
+    m2 = gm(m2, snap)
+    assert m1 == m2
+    inner = m1.get(101).val
+    assert inner.get(220).val.read().val == [5]
+    assert inner.get(110).val is None
+    assert inner.len().val == 1
+
+
+def test_concurrent_update_and_remove_add_bias(gm):  # test/map.rs:197-235
+    m1, m2 = TMap(), TMap()
+    op1 = MapRm(vc((1, 1)), {102})
+    op2 = m2.update(102, m2.get(102).derive_add_ctx(2),
+                    lambda mp, c: mp.update(42, c, lambda r, c2: r.write(7, c2)))
+    m1.apply(op1)
+    m2.apply(op2)
+    m1c = gm(m1, m2)
+    m2c = gm(m2, m1)
+    m1.apply(op2)
+    m2.apply(op1)
+    assert m1c == m2c
+    assert m1 == m2
+    assert m1 == m1c
+    assert read_nested(m1c, 102, 42) == [7]
+
+
+def test_commute_quickcheck_bug(gm):  # test/map.rs:331-362
+    ops = [MapRm(vc((45, 1)), {0}),
+           MapUp(Dot(45, 2), 0, MapUp(Dot(45, 1), 0, MVRegPut(VClock(), 0)))]
+    m = TMap()
+    apply_ops(m, ops)
+    empty = TMap()
+    assert gm(m, empty) == gm(empty, m)
+
+
+def test_idempotent_quickcheck_bug1(gm):  # test/map.rs:364-404
+    ops = [MapUp(Dot(21, 5), 0, MapUp(Dot(21, 1), 32, MVRegPut(VClock(), 42))),
+           MapRm(vc((21, 5)), {0}),
+           MapUp(Dot(21, 6), 1, MapUp(Dot(21, 1), 0, MVRegPut(VClock(), 0)))]
+    m = TMap()
+    apply_ops(m, ops)
+    assert gm(m, m.copy()) == m
+
+
+def test_idempotent_quickcheck_bug2(gm):  # test/map.rs:406-430
+    m = TMap()
+    m.apply(MapUp(Dot(32, 5), 0, MapUp(Dot(32, 5), 0, MVRegPut(VClock(), 0))))
+    assert gm(m, m.copy()) == m
+
+
+def test_op_exchange_same_as_merge_quickcheck1(gm):  # test/map.rs:432-478
+    op1 = MapUp(Dot(38, 4), 216, MapUp(Dot(38, 1), 37, MVRegPut(vc((38, 1)), 94)))
+    op2 = MapUp(Dot(91, 9), 216, MapUp(Dot(91, 1), 37, MVRegPut(vc((91, 1)), 94)))
+    m1, m2 = TMap(), TMap()
+    m1.apply(op1)
+    m2.apply(op2)
+    m1m = gm(m1, m2)
+    m2m = gm(m2, m1)
+    m1.apply(op2)
+    m2.apply(op1)
+    assert m1 == m2
+    assert m1m == m2m
+    assert m1 == m1m and m2 == m2m and m1 == m2m and m2 == m1m
+    assert sorted(read_nested(m1m, 216, 37)) == [94, 94]
+
+
+def test_idempotent_quickcheck1(gm):  # test/map.rs:480-516
+    ops = [MapUp(Dot(62, 9), 47, MapUp(Dot(62, 1), 65, MVRegPut(vc((62, 1)), 240))),
+           MapUp(Dot(62, 11), 60, MapUp(Dot(62, 1), 193, MVRegPut(vc((62, 1)), 28)))]
+    m = TMap()
+    apply_ops(m, ops)
+    assert gm(m, m.copy()) == m
+
+
+# ---- quickcheck properties of test/map.rs (seeded), every merge on the GPU --------------------------
+def _prim(rng, n_max=40):
+    actor = rng.randrange(256)
+    ops = [tuple(rng.randrange(256) for _ in range(5)) for _ in range(rng.randrange(n_max))]
+    if rng.random() < 0.5:  # quickcheck's u8 generator favours small values: mix both regimes for keys
+        ops = [(c, ic, k % 4, ik % 4, v) for c, ic, k, ik, v in ops]
+    return actor, ops
+
+
+def _maps(rng, n):
+    while True:
+        prims = [_prim(rng) for _ in range(n)]
+        if len(set(p[0] for p in prims)) == n:  # the props discard equal actors
+            return [build_ops(*p)[1] for p in prims]
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_prop_map_merge_laws_on_gpu(gm, seed):
+    """prop_op_exchange_same_as_merge, prop_merge_commutative, prop_merge_associative,
+    prop_merge_followed_by_merge, prop_merge_idempotent (test/map.rs:526-550, :694-721, :660-692,
+    :723-748, :750-764), and each GPU merge equal to the oracle's."""
+    rng = random.Random(seed)
+    ops1, ops2, ops3 = _maps(rng, 3)
+    m1, m2, m3 = TMap(), TMap(), TMap()
+    apply_ops(m1, ops1)
+    apply_ops(m2, ops2)
+    apply_ops(m3, ops3)
+    for m in (m1, m2):
+        assert gm(m, m.copy()) == m  # idempotent
+    mm = gm(m1, m2)
+    exp = m1.copy()
+    exp.merge(m2.copy())
+    assert mm == exp  # the oracle's merge
+    a, b = m1.copy(), m2.copy()
+    apply_ops(a, ops2)
+    apply_ops(b, ops1)
+    assert a == mm and b == mm  # op exchange == merge
+    assert gm(m2, m1) == mm  # commutative
+    x = gm(m1, m2)
+    y = gm(m2, x)
+    assert x == y  # merge followed by merge
+    left = gm(gm(m1, m2), m3)
+    right = gm(m1, gm(m2, m3))
+    assert left == right  # associative
+
+
+# ---- op-replay folds over many replicas against the oracle's left fold -------------------------------
+@pytest.mark.parametrize("seed,R,K,K2,A", [(1, 30, 3, 4, 4), (2, 50, 5, 6, 5), (3, 40, 2, 3, 3),
+                                            (4, 70, 6, 8, 6), (5, 25, 4, 20, 8)])
+def test_map_nested_op_replay_fold(gpu_ctx, seed, R, K, K2, A):
+    maps = O.nested_map_objects(R, K, K2, A, seed=seed, steps=8 * R)
+    exp = O.map_fold_objects(maps)
+    got = gpu_fold(gpu_ctx, maps)
+    assert got == exp
+
+
+def test_map_nested_deferred_at_both_levels(gpu_ctx):
+    """Enough histories that some folds end with inner and outer deferred removes."""
+    n_in = n_out = 0
+    for seed in range(30, 40):
+        maps = O.nested_map_objects(24, 3, 5, 4, seed=seed, steps=220, p_irm=0.5, p_ooo=0.8, p_rm=0.3)
+        exp = O.map_fold_objects(maps)
+        n_in += sum(len(e.val.deferred) for e in exp.entries.values())
+        n_out += len(exp.deferred)
+        assert gpu_fold(gpu_ctx, maps) == exp
+    assert n_in > 0 and n_out > 0
+
+
+def test_map_nested_groups_and_validation(gpu_ctx):
+    """G = 2 groups in one launch (CSR over (g, r, k) spanning them, the outer pool with offsets);
+    a malformed id_off is reported (flags bit 5), an int32 one refused."""
+    R, K, K2, A = 12, 3, 4, 4
+    parts = [O.nested_map_objects(R, K, K2, A, seed=70 + g, steps=160) for g in range(2)]
+    allm = parts[0] + parts[1]
+    V = max([len(ie.val.vals) for m in allm for e in m.entries.values() for ie in e.val.entries.values()] + [1])
+    d = O.nested_map_to_dense(allm, K, K2, A, V)
+    off = [0, sum(len(m.deferred) for m in parts[0]), sum(len(m.deferred) for m in allm)]
+    d["def_row"] = d["def_row"] % R
+    shp = lambda x: to_dev(x.reshape((2, R) + x.shape[1:]))  # noqa: E731
+    Dn = off[-1]
+    kw = dict(def_off=off, def_row=torch.from_numpy(d["def_row"].astype(np.int32)).cuda(),
+              def_clock=to_dev(d["def_clock"]), def_keys=to_dev(d["def_keys"])) if Dn else {}
+    Di = d["id_clock"].shape[0]
+    ikw = dict(id_clock=to_dev(d["id_clock"]), id_keys=to_dev(d["id_keys"])) if Di else {}
+    args = [shp(d[x]) for x in ("clock", "ec", "ic", "iec", "ivc", "ivv")]
+    res = cg.map.nested_lub_many(*args, to_dev(d["id_off"]), ctx=gpu_ctx, **ikw, **kw)
+    for g in range(2):
+        dset = []
+        if Dn:
+            dset = [(np.array(rm, np.uint64), ks) for rm, ks in
+                    cg.map.deferred_set(kw["def_clock"], res.def_keep, res.def_keys, off[g], off[g + 1])]
+        idn = res.id_n.cpu().numpy()[g]
+        idc, idk = to_host(res.id_clock)[g], to_host(res.id_keys)[g]
+        idef = {k: [(idc[k, i], O.bitmap_members(idk[k, i:i + 1])) for i in range(int(idn[k]))] for k in range(K)}
+        got = O.dense_to_nested_map(to_host(res.clock)[g], to_host(res.ec)[g], to_host(res.ic)[g],
+                                    to_host(res.iec)[g], to_host(res.ivc)[g], to_host(res.ivv)[g],
+                                    res.nval.cpu().numpy()[g], idef, dset)
+        assert got == O.map_fold_objects(parts[g])
+    off32 = torch.from_numpy(d["id_off"].astype(np.int32)).cuda()
+    with pytest.raises(ValueError, match="int64"):
+        cg.map.nested_lub_many(*args, off32, ctx=gpu_ctx, **ikw, **kw)
+    if Di >= 1:
+        bad = d["id_off"].copy()
+        bad[-1] += np.uint64(1)  # last entry past the rows
+        with pytest.raises(ValueError, match="id_off invalid"):
+            cg.map.nested_lub_many(*args, to_dev(bad), ctx=gpu_ctx, **ikw, **kw)
+
+
+def test_map_nested_empty(gpu_ctx):
+    """R = 0 folds to Map::new()."""
+    z = lambda *s: torch.zeros(s, dtype=torch.int64, device="cuda:0")  # noqa: E731
+    res = cg.map.nested_lub_many(z(2, 0, 4), z(2, 0, 3, 4), z(2, 0, 3, 4), z(2, 0, 3, 2, 4), z(2, 0, 3, 2, 1, 4),
+                                 z(2, 0, 3, 2, 1), z(1), ctx=gpu_ctx)
+    assert not to_host(res.clock).any() and not to_host(res.ec).any() and not to_host(res.iec).any()
+    assert not res.nval.cpu().numpy().any() and not res.id_n.cpu().numpy().any()

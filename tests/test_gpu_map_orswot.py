@@ -204,3 +204,69 @@ def test_map_orswot_empty(gpu_ctx):
     res = cg.map.orswot_lub_many(z(2, 0, 4), z(2, 0, 3, 4), z(2, 0, 3, 4), z(2, 0, 3, 5, 4), z(1), ctx=gpu_ctx)
     assert not to_host(res.clock).any() and not to_host(res.ec).any() and not to_host(res.ent).any()
     assert not res.vd_n.cpu().numpy().any()
+
+
+def test_map_orswot_vd_off_validation(gpu_ctx):
+    """vd_off must be int64 / uint64, start at 0, never decrease and end at the rows of
+    vd_clock; a malformed CSR is reported (flags bit 5 -> ValueError), never read past its rows."""
+    maps = O.map_orswot_objects(20, 3, 5, 4, seed=3, steps=160, p_vrm=0.5)
+    d = O.map_orswot_to_dense(maps, 3, 5, 4)
+    Dv = int(d["vd_off"][-1])
+    assert Dv >= 2
+    args = lambda: (to_dev(d["clock"]), to_dev(d["ec"]), to_dev(d["oc"]), to_dev(d["ent"]))  # noqa: E731
+    vkw = dict(vd_clock=to_dev(d["vd_clock"]), vd_mem=to_dev(d["vd_members"]))
+    off32 = torch.from_numpy(np.asarray(d["vd_off"], np.int64).astype(np.int32)).cuda()
+    with pytest.raises(ValueError, match="int64"):
+        cg.map.orswot_lub_many(*args(), off32, ctx=gpu_ctx, **vkw)
+    bad = np.asarray(d["vd_off"], np.uint64).copy()
+    i = int(np.flatnonzero(np.diff(bad.astype(np.int64)) > 0)[0]) + 1  # an entry that can be lowered
+    bad[i] = bad[i - 1] + np.uint64(Dv + 5)  # then the next entry decreases
+    with pytest.raises(ValueError, match="vd_off invalid"):
+        cg.map.orswot_lub_many(*args(), to_dev(bad), ctx=gpu_ctx, **vkw)
+    extra = dict(vd_clock=to_dev(np.concatenate([d["vd_clock"], d["vd_clock"][:1]])),
+                 vd_mem=to_dev(np.concatenate([d["vd_members"], d["vd_members"][:1]])))
+    with pytest.raises(ValueError, match="vd_off invalid"):  # last entry != rows of vd_clock
+        cg.map.orswot_lub_many(*args(), to_dev(d["vd_off"]), ctx=gpu_ctx, **extra)
+    res = cg.map.orswot_lub_many(*args(), to_dev(d["vd_off"]), ctx=gpu_ctx, **vkw)  # the valid CSR still folds
+    assert int(res.flags.cpu()[0]) == 0
+
+
+@pytest.mark.parametrize("M,R", [(4, 16), (4, 17), (4, 24), (8, 8), (8, 9), (8, 12), (32, 4), (32, 5), (32, 6)])
+def test_map_orswot_ring_block_boundaries(gpu_ctx, M, R):
+    """ADVICE r4: the register ring runs unclamped blocks while r0 + 2*DEPTH < R and clamped ones after;
+    R = 2*DEPTH, 2*DEPTH + 1 and 3*DEPTH for DEPTH = 8 / 4 / 2 (M <= 4 / <= 8 / <= 32)."""
+    maps = O.map_orswot_objects(R, 3, M, 4, seed=100 + R + M, steps=12 * R, p_vrm=0.4)
+    exp = O.map_fold_objects(maps)
+    d = O.map_orswot_to_dense(maps, 3, M, 4)
+    res, kw = _run(gpu_ctx, d)
+    assert int(res.flags.cpu()[0]) == 0
+    _same(_got_maps(res, kw, 1)[0], exp)
+
+
+def test_map_orswot_dominated_nested_removes_not_held(gpu_ctx):
+    """a replica's nested removes already covered by our Orswot clock (rm <= oc) are applied
+    and never deferred (orswot.rs:230-238), so 20 of them do not count toward the 16-remove capacity."""
+    m0 = O.Map(O.Orswot)
+    m0.clock = O.VClock({0: 5, 1: 5})
+    o0 = O.Orswot()
+    o0.clock = O.VClock({0: 5, 1: 5})
+    o0.entries = {0: O.VClock({0: 5}), 1: O.VClock({1: 3})}
+    m0.entries[0] = O.MapEntry(O.VClock({0: 5}), o0)
+    m1 = O.Map(O.Orswot)
+    m1.clock = O.VClock({0: 5, 2: 1})
+    o1 = O.Orswot()
+    o1.clock = O.VClock({0: 5, 2: 1})
+    o1.entries = {0: O.VClock({0: 5}), 2: O.VClock({2: 1})}
+    n = 0
+    for a in range(1, 6):
+        for b in range(1, 5):
+            if n < 20:
+                o1.deferred[O.VClock({0: a, 1: b})] = {1 + (n % 2)}
+                n += 1
+    m1.entries[0] = O.MapEntry(O.VClock({0: 5, 2: 1}), o1)
+    maps = [m0, m1]
+    exp = O.map_fold_objects(maps)
+    d = O.map_orswot_to_dense(maps, 1, 3, 3)
+    res, kw = _run(gpu_ctx, d)
+    assert int(res.flags.cpu()[0]) == 0
+    _same(_got_maps(res, kw, 1)[0], exp)
