@@ -150,6 +150,23 @@ def gm(gpu_ctx):
     return merge
 
 
+def canon(m):
+    """A comparable form of a nested Map state with each MVReg's values as a sorted multiset: op-replay
+    histories can leave one (clock, value) twice in a register (the oracle's fold — a restatement of
+    mvreg.rs:112-128 — does so too), where MVReg's own PartialEq (mvreg.rs:62-86) would assert."""
+    def c(vc):
+        return tuple(sorted(vc.dots.items()))
+
+    def reg(r):
+        return tuple(sorted((c(x), v) for x, v in r.vals))
+
+    def inner(n):
+        return (c(n.clock), tuple(sorted((j, c(e.clock), reg(e.val)) for j, e in n.entries.items())),
+                tuple(sorted((c(rm), tuple(sorted(ks))) for rm, ks in n.deferred.items())))
+    return (c(m.clock), tuple(sorted((k, c(e.clock), inner(e.val)) for k, e in m.entries.items())),
+            tuple(sorted((c(rm), tuple(sorted(ks))) for rm, ks in m.deferred.items())))
+
+
 def read_nested(m, k1, k2):
     v = m.get(k1).val
     if v is None:
@@ -295,7 +312,7 @@ def test_map_nested_op_replay_fold(gpu_ctx, seed, R, K, K2, A):
     maps = O.nested_map_objects(R, K, K2, A, seed=seed, steps=8 * R)
     exp = O.map_fold_objects(maps)
     got = gpu_fold(gpu_ctx, maps)
-    assert got == exp
+    assert canon(got) == canon(exp)
 
 
 def test_map_nested_deferred_at_both_levels(gpu_ctx):
@@ -306,7 +323,7 @@ def test_map_nested_deferred_at_both_levels(gpu_ctx):
         exp = O.map_fold_objects(maps)
         n_in += sum(len(e.val.deferred) for e in exp.entries.values())
         n_out += len(exp.deferred)
-        assert gpu_fold(gpu_ctx, maps) == exp
+        assert canon(gpu_fold(gpu_ctx, maps)) == canon(exp)
     assert n_in > 0 and n_out > 0
 
 
@@ -339,7 +356,7 @@ def test_map_nested_groups_and_validation(gpu_ctx):
         got = O.dense_to_nested_map(to_host(res.clock)[g], to_host(res.ec)[g], to_host(res.ic)[g],
                                     to_host(res.iec)[g], to_host(res.ivc)[g], to_host(res.ivv)[g],
                                     res.nval.cpu().numpy()[g], idef, dset)
-        assert got == O.map_fold_objects(parts[g])
+        assert canon(got) == canon(O.map_fold_objects(parts[g]))
     off32 = torch.from_numpy(d["id_off"].astype(np.int32)).cuda()
     with pytest.raises(ValueError, match="int64"):
         cg.map.nested_lub_many(*args, off32, ctx=gpu_ctx, **ikw, **kw)
