@@ -324,3 +324,115 @@ def map_merge_batch(self_states, other_states, ctx: Optional[HostContext] = None
     ctx.call("crdt_map_merge_batch", ctypes.byref(ss[0]), ctypes.byref(dd[0]), ctypes.byref(ss[1]),
              ctypes.byref(dd[1]), _ptr(status))
     return status
+
+
+# ---- the value-typed Maps (round 5): whole-batch staging in the library ----------------------------
+def _def_pool(b, def_off, def_row, def_clock, def_keys, keep):
+    D = 0
+    if def_off is not None and int(def_off[-1]):
+        D = int(def_off[-1])
+        off = (ctypes.c_size_t * 2)(0, D)
+        dr = np.ascontiguousarray(def_row, dtype=np.uint32)
+        dcl = np.ascontiguousarray(_u64(def_clock, "def_clock"))
+        dks = np.ascontiguousarray(_u64(def_keys, "def_keys"))
+        keep += [off, dr, dcl, dks]
+        b.def_off, b.def_row, b.def_clock, b.def_keys = off, dr.ctypes.data, dcl.ctypes.data, dks.ctypes.data
+    return D
+
+
+def map_counter_lub_many(clock, ec, val, def_off=None, def_row=None, def_clock=None, def_keys=None,
+                         ctx: Optional[HostContext] = None) -> dict:
+    """crdt_map_counter_lub_many on host arrays (one group): clock (R, A), ec (R, K, A), val (R, K, W, A)
+    (W = 1 GCounter, 2 PNCounter P | N); the Map's removes pooled as for map_lub_many."""
+    ctx = ctx or HostContext.default()
+    c, e, v = (np.ascontiguousarray(_u64(x, n)) for x, n in ((clock, "clock"), (ec, "ec"), (val, "val")))
+    R, A = c.shape
+    K, W = e.shape[1], v.shape[2]
+    b = _abi.MapCounterBatch()
+    b.G, b.R, b.K, b.A, b.W = 1, R, K, A, W
+    b.clock, b.clock_rstride, b.clock_gstride = c.ctypes.data, A, R * A
+    b.ec, b.ec_rstride, b.ec_gstride = e.ctypes.data, K * A, R * K * A
+    b.val, b.val_rstride, b.val_gstride = v.ctypes.data, K * W * A, R * K * W * A
+    keep = [c, e, v]
+    D = _def_pool(b, def_off, def_row, def_clock, def_keys, keep)
+    Kw = (K + 63) // 64
+    out = dict(clock=np.zeros((1, A), np.uint64), ec=np.zeros((1, K, A), np.uint64),
+               val=np.zeros((1, K, W, A), np.uint64), flags=np.zeros(1, np.uint32), def_keep=np.zeros(D, np.uint8),
+               def_keys=np.zeros((D, Kw), np.uint64))
+    o = _abi.MapCounterOut()
+    o.clock, o.ec, o.val, o.flags = (out[n].ctypes.data for n in ("clock", "ec", "val", "flags"))
+    o.def_keep = out["def_keep"].ctypes.data if D else None
+    o.def_keys = out["def_keys"].ctypes.data if D else None
+    ctx.call("crdt_map_counter_lub_many", ctypes.byref(b), ctypes.byref(o))
+    return out
+
+
+def map_orswot_lub_many(clock, ec, oc, ent, vd_off, vd_clock=None, vd_mem=None, def_off=None, def_row=None,
+                        def_clock=None, def_keys=None, ctx: Optional[HostContext] = None) -> dict:
+    """crdt_map_orswot_lub_many on host arrays (one group): clock (R, A), ec / oc (R, K, A), ent (R, K, M, A),
+    the nested removes as a CSR over (r, k): vd_off (R*K + 1,), vd_clock (Dv, A), vd_mem (Dv,)."""
+    ctx = ctx or HostContext.default()
+    c, e, o_, m = (np.ascontiguousarray(_u64(x, n)) for x, n in ((clock, "clock"), (ec, "ec"), (oc, "oc"), (ent, "ent")))
+    R, A = c.shape
+    K, M = e.shape[1], m.shape[2]
+    vo = np.ascontiguousarray(_u64(vd_off, "vd_off"))
+    Dv = int(vd_clock.shape[0]) if vd_clock is not None else 0
+    vc = np.ascontiguousarray(_u64(vd_clock, "vd_clock")) if Dv else None
+    vm = np.ascontiguousarray(_u64(vd_mem, "vd_mem")) if Dv else None
+    b = _abi.MapOrswotBatch()
+    b.G, b.R, b.K, b.M, b.A = 1, R, K, M, A
+    b.clock, b.ec, b.oc, b.ent = (x.ctypes.data for x in (c, e, o_, m))
+    b.vd_off, b.Dv = vo.ctypes.data, Dv
+    if Dv:
+        b.vd_clock, b.vd_mem = vc.ctypes.data, vm.ctypes.data
+    keep = [c, e, o_, m, vo, vc, vm]
+    D = _def_pool(b, def_off, def_row, def_clock, def_keys, keep)
+    Kw = (K + 63) // 64
+    out = dict(clock=np.zeros((1, A), np.uint64), ec=np.zeros((1, K, A), np.uint64), oc=np.zeros((1, K, A), np.uint64),
+               ent=np.zeros((1, K, M, A), np.uint64), vd_n=np.zeros((1, K), np.uint32),
+               vd_clock=np.zeros((1, K, 16, A), np.uint64), vd_mem=np.zeros((1, K, 16), np.uint64),
+               flags=np.zeros(1, np.uint32), def_keep=np.zeros(D, np.uint8), def_keys=np.zeros((D, Kw), np.uint64))
+    ob = _abi.MapOrswotOut()
+    for n in ("clock", "ec", "oc", "ent", "vd_n", "vd_clock", "vd_mem", "flags"):
+        setattr(ob, n, out[n].ctypes.data)
+    ob.def_keep = out["def_keep"].ctypes.data if D else None
+    ob.def_keys = out["def_keys"].ctypes.data if D else None
+    ctx.call("crdt_map_orswot_lub_many", ctypes.byref(b), ctypes.byref(ob))
+    return out
+
+
+def map_nested_lub_many(clock, ec, ic, iec, ivc, ivv, id_off, id_clock=None, id_keys=None, def_off=None, def_row=None,
+                        def_clock=None, def_keys=None, ctx: Optional[HostContext] = None) -> dict:
+    """crdt_map_nested_lub_many on host arrays (one group): clock (R, A), ec / ic (R, K, A), iec (R, K, K2, A),
+    ivc (R, K, K2, V, A), ivv (R, K, K2, V), the inner removes as a CSR over (r, k)."""
+    ctx = ctx or HostContext.default()
+    arrs = [np.ascontiguousarray(_u64(x, n)) for x, n in ((clock, "clock"), (ec, "ec"), (ic, "ic"), (iec, "iec"),
+                                                          (ivc, "ivc"), (ivv, "ivv"), (id_off, "id_off"))]
+    c, e, i_, ie, vc, vv, io = arrs
+    R, A = c.shape
+    K, K2, V = e.shape[1], ie.shape[2], vc.shape[3]
+    Di = int(id_clock.shape[0]) if id_clock is not None else 0
+    idc = np.ascontiguousarray(_u64(id_clock, "id_clock")) if Di else None
+    idk = np.ascontiguousarray(_u64(id_keys, "id_keys")) if Di else None
+    b = _abi.MapNestedBatch()
+    b.G, b.R, b.K, b.K2, b.V, b.A = 1, R, K, K2, V, A
+    b.clock, b.ec, b.ic, b.iec, b.ivc, b.ivv = (x.ctypes.data for x in (c, e, i_, ie, vc, vv))
+    b.id_off, b.Di = io.ctypes.data, Di
+    if Di:
+        b.id_clock, b.id_keys = idc.ctypes.data, idk.ctypes.data
+    keep = arrs + [idc, idk]
+    D = _def_pool(b, def_off, def_row, def_clock, def_keys, keep)
+    Kw = (K + 63) // 64
+    out = dict(clock=np.zeros((1, A), np.uint64), ec=np.zeros((1, K, A), np.uint64), ic=np.zeros((1, K, A), np.uint64),
+               iec=np.zeros((1, K, K2, A), np.uint64), ivc=np.zeros((1, K, K2, 8, A), np.uint64),
+               ivv=np.zeros((1, K, K2, 8), np.uint64), nval=np.zeros((1, K, K2), np.uint32),
+               id_n=np.zeros((1, K), np.uint32), id_clock=np.zeros((1, K, 16, A), np.uint64),
+               id_keys=np.zeros((1, K, 16), np.uint64), flags=np.zeros(1, np.uint32), def_keep=np.zeros(D, np.uint8),
+               def_keys=np.zeros((D, Kw), np.uint64))
+    ob = _abi.MapNestedOut()
+    for n in ("clock", "ec", "ic", "iec", "ivc", "ivv", "nval", "id_n", "id_clock", "id_keys", "flags"):
+        setattr(ob, n, out[n].ctypes.data)
+    ob.def_keep = out["def_keep"].ctypes.data if D else None
+    ob.def_keys = out["def_keys"].ctypes.data if D else None
+    ctx.call("crdt_map_nested_lub_many", ctypes.byref(b), ctypes.byref(ob))
+    return out

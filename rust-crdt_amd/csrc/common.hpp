@@ -102,6 +102,7 @@ struct Tune {
   int map_counter_dma = 0;     // Map<K, counter> fold: LDS-DMA ring slots (8 or 16; 0: register ring, 8.7 vs 9.1 ms)
   int map_counter_depth = 8;   // Map<K, counter> fold: register-ring depth at A <= 64 (4, 8, 16; 16: 4.86 vs 4.33 ms)
   int map_counter_kpw = 0;     // Map<K, counter> fold: keys per wave (1, 2, 4; A <= 64 / KPW; 0: automatic)
+  int map_counter_cs = 1;      // Map<K, counter> fold: whole-chunk skip (A = 8, 16, 32; one key per wave)
   int map_apply_pf = 1;        // Map apply (16-lane groups): the next op's entry-clock row prefetched with its
                                //     Put / rm clock; absent keys skip their value rows (0: round-3 form;
                                //     1.28 vs 1.81 ms, profiles/r04_map_apply_pf_ab.log)
@@ -277,6 +278,9 @@ int orswot_lub_many_ex(crdt_ctx *ctx, const crdt_orswot_batch *in, crdt_orswot_o
 int orswot_merge_batch_host(crdt_ctx *ctx, const crdt_orswot_states *self, const crdt_orswot_states *other,
                             uint32_t *status);
 int map_lub_many_host(crdt_ctx *ctx, const crdt_map_batch *in, crdt_map_out *out);
+int map_counter_lub_many_host(crdt_ctx *ctx, const crdt_map_counter_batch *in, crdt_map_counter_out *out);
+int map_orswot_lub_many_host(crdt_ctx *ctx, const crdt_map_orswot_batch *in, crdt_map_orswot_out *out);
+int map_nested_lub_many_host(crdt_ctx *ctx, const crdt_map_nested_batch *in, crdt_map_nested_out *out);
 // The workgroup-per-key Map fold for A > 256 or V > 8 (map_wide.hip): def_off_dev = the device copy
 // of the deferred offsets (or NULL); outputs and flags as crdt_map_lub_many (flags zeroed by the caller).
 int map_lub_wide(crdt_ctx *ctx, const crdt_map_batch *in, const size_t *def_off_dev, crdt_map_out *out);

@@ -940,6 +940,300 @@ static int map_lub_host_stream(crdt_ctx *ctx, const crdt_map_batch *in, crdt_map
   return CRDT_OK;
 }
 
+// ---- the value-typed Maps (round 5): whole-batch staging ------------------------------------------
+// Map<K, GCounter / PNCounter>, Map<K, Orswot> and Map<K, Map<K2, MVReg>> fold every key in replica
+// order, so their host form stages the whole batch (packed) into device buffers, runs the device
+// entry point and copies the outputs back (synchronous on return, as every host-mode call).
+static int map_counter_lub_host_body(crdt_ctx *ctx, const crdt_map_counter_batch *in, crdt_map_counter_out *out,
+                                     DevScratch &ds) {
+  const size_t G = in->G, R = in->R, K = in->K, A = in->A, W = in->W, Kw = (K + 63) / 64;
+  const size_t D = in->def_off ? in->def_off[G] : 0;
+  uint64_t *c = nullptr, *e = nullptr, *v = nullptr, *dc = nullptr, *dk = nullptr, *oc = nullptr, *oe = nullptr,
+           *ov = nullptr, *ok2 = nullptr;
+  uint32_t *dr = nullptr, *of = nullptr;
+  uint8_t *okp = nullptr;
+  if (int rc = ds.get(ctx, G * R * A, &c)) return rc;
+  if (int rc = ds.get(ctx, G * R * K * A, &e)) return rc;
+  if (int rc = ds.get(ctx, G * R * K * W * A, &v)) return rc;
+  if (int rc = ds.get(ctx, D, &dr)) return rc;
+  if (int rc = ds.get(ctx, D * A, &dc)) return rc;
+  if (int rc = ds.get(ctx, D * Kw, &dk)) return rc;
+  if (int rc = ds.get(ctx, G * A, &oc)) return rc;
+  if (int rc = ds.get(ctx, G * K * A, &oe)) return rc;
+  if (int rc = ds.get(ctx, G * K * W * A, &ov)) return rc;
+  if (int rc = ds.get(ctx, G, &of)) return rc;
+  if (out->def_keep)
+    if (int rc = ds.get(ctx, D, &okp)) return rc;
+  if (out->def_keys)
+    if (int rc = ds.get(ctx, D * Kw, &ok2)) return rc;
+  for (size_t g = 0; g < G && R; ++g) {
+    STAGE_HIP(copy_rows(c + g * R * A, A * 8, in->clock + g * in->clock_gstride, in->clock_rstride * 8, A * 8, R,
+                        hipMemcpyHostToDevice, ctx->stream));
+    STAGE_HIP(copy_rows(e + g * R * K * A, K * A * 8, in->ec + g * in->ec_gstride, in->ec_rstride * 8, K * A * 8, R,
+                        hipMemcpyHostToDevice, ctx->stream));
+    STAGE_HIP(copy_rows(v + g * R * K * W * A, K * W * A * 8, in->val + g * in->val_gstride, in->val_rstride * 8,
+                        K * W * A * 8, R, hipMemcpyHostToDevice, ctx->stream));
+  }
+  if (int rc = h2d_async(ctx, dr, in->def_row, D * 4)) return rc;
+  if (int rc = h2d_async(ctx, dc, in->def_clock, D * A * 8)) return rc;
+  if (int rc = h2d_async(ctx, dk, in->def_keys, D * Kw * 8)) return rc;
+  crdt_map_counter_batch b = *in;
+  b.clock = c;
+  b.clock_rstride = A;
+  b.clock_gstride = R * A;
+  b.ec = e;
+  b.ec_rstride = K * A;
+  b.ec_gstride = R * K * A;
+  b.val = v;
+  b.val_rstride = K * W * A;
+  b.val_gstride = R * K * W * A;
+  b.def_row = dr;
+  b.def_clock = dc;
+  b.def_keys = dk;
+  crdt_map_counter_out o{oc, oe, ov, of, okp, ok2};
+  {
+    DeviceModeScope dev(ctx);
+    if (int rc = crdt_map_counter_lub_many(ctx, &b, &o)) return rc;
+  }
+  if (int rc = d2h_async(ctx, out->clock, oc, G * A * 8)) return rc;
+  if (int rc = d2h_async(ctx, out->ec, oe, G * K * A * 8)) return rc;
+  if (int rc = d2h_async(ctx, out->val, ov, G * K * W * A * 8)) return rc;
+  if (int rc = d2h_async(ctx, out->flags, of, G * 4)) return rc;
+  if (int rc = d2h_async(ctx, out->def_keep, okp, D)) return rc;
+  if (int rc = d2h_async(ctx, out->def_keys, ok2, D * Kw * 8)) return rc;
+  return CRDT_OK;
+}
+
+int map_counter_lub_many_host(crdt_ctx *ctx, const crdt_map_counter_batch *in, crdt_map_counter_out *out) {
+  if (!in || !out) return fail(ctx, CRDT_EINVAL, "map_counter_lub_many: NULL batch/out");
+  if (in->G == 0 || in->K == 0 || in->A == 0) return CRDT_OK;
+  if (in->W != 1 && in->W != 2) return fail(ctx, CRDT_EINVAL, "map_counter_lub_many: W = %zu (1 GCounter, 2 PNCounter)", in->W);
+  if (!out->clock || !out->ec || !out->val || !out->flags) return fail(ctx, CRDT_EINVAL, "map_counter_lub_many: NULL output");
+  if (in->R && (!in->clock || !in->ec || !in->val)) return fail(ctx, CRDT_EINVAL, "map_counter_lub_many: NULL input");
+  const size_t K = in->K, A = in->A, W = in->W;
+  if (in->R > 1 && (in->clock_rstride < A || in->ec_rstride < K * A || in->val_rstride < K * W * A))
+    return fail(ctx, CRDT_EINVAL, "map_counter_lub_many: replica strides smaller than a replica");
+  if (in->def_off && in->def_off[0] != 0) return fail(ctx, CRDT_EINVAL, "map_counter_lub_many: def_off[0] must be 0");
+  for (size_t i = 0; in->def_off && i < in->G; ++i)
+    if (in->def_off[i + 1] < in->def_off[i]) return fail(ctx, CRDT_EINVAL, "map_counter_lub_many: def_off not non-decreasing");
+  if (in->def_off && in->def_off[in->G] && (!in->def_row || !in->def_clock || !in->def_keys))
+    return fail(ctx, CRDT_EINVAL, "map_counter_lub_many: NULL deferred input");
+  for (auto [p, w] : {std::pair<const void *, const char *>{in->clock, "clock"}, {in->ec, "ec"}, {in->val, "val"},
+                      {in->def_row, "def_row"}, {in->def_clock, "def_clock"}, {in->def_keys, "def_keys"},
+                      {out->clock, "out.clock"}, {out->ec, "out.ec"}, {out->val, "out.val"}, {out->flags, "out.flags"},
+                      {out->def_keep, "out.def_keep"}, {out->def_keys, "out.def_keys"}})
+    if (int rc = check_host(ctx, p, w)) return rc;
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  DevScratch ds;
+  return finish(ctx, map_counter_lub_host_body(ctx, in, out, ds));
+}
+
+static int map_orswot_lub_host_body(crdt_ctx *ctx, const crdt_map_orswot_batch *in, crdt_map_orswot_out *out,
+                                    DevScratch &ds) {
+  const size_t G = in->G, R = in->R, K = in->K, M = in->M, A = in->A, Kw = (K + 63) / 64, Dv = in->Dv;
+  const size_t D = in->def_off ? in->def_off[G] : 0, N = G * R * K;
+  constexpr size_t VD = 16;  // nested deferred slots per key in the output (crdt_gpu.h)
+  uint64_t *c, *e, *o, *m, *vo, *vc, *vm, *dc, *dk, *oc, *oe, *oo, *om, *ovc, *ovm, *ok2 = nullptr;
+  uint32_t *dr, *ovn, *of;
+  uint8_t *okp = nullptr;
+  if (int rc = ds.get(ctx, G * R * A, &c)) return rc;
+  if (int rc = ds.get(ctx, N * A, &e)) return rc;
+  if (int rc = ds.get(ctx, N * A, &o)) return rc;
+  if (int rc = ds.get(ctx, N * M * A, &m)) return rc;
+  if (int rc = ds.get(ctx, N + 1, &vo)) return rc;
+  if (int rc = ds.get(ctx, Dv * A, &vc)) return rc;
+  if (int rc = ds.get(ctx, Dv, &vm)) return rc;
+  if (int rc = ds.get(ctx, D, &dr)) return rc;
+  if (int rc = ds.get(ctx, D * A, &dc)) return rc;
+  if (int rc = ds.get(ctx, D * Kw, &dk)) return rc;
+  if (int rc = ds.get(ctx, G * A, &oc)) return rc;
+  if (int rc = ds.get(ctx, G * K * A, &oe)) return rc;
+  if (int rc = ds.get(ctx, G * K * A, &oo)) return rc;
+  if (int rc = ds.get(ctx, G * K * M * A, &om)) return rc;
+  if (int rc = ds.get(ctx, G * K * VD * A, &ovc)) return rc;
+  if (int rc = ds.get(ctx, G * K * VD, &ovm)) return rc;
+  if (int rc = ds.get(ctx, G * K, &ovn)) return rc;
+  if (int rc = ds.get(ctx, G, &of)) return rc;
+  if (out->def_keep)
+    if (int rc = ds.get(ctx, D, &okp)) return rc;
+  if (out->def_keys)
+    if (int rc = ds.get(ctx, D * Kw, &ok2)) return rc;
+  if (int rc = h2d_async(ctx, c, in->clock, G * R * A * 8)) return rc;
+  if (int rc = h2d_async(ctx, e, in->ec, N * A * 8)) return rc;
+  if (int rc = h2d_async(ctx, o, in->oc, N * A * 8)) return rc;
+  if (int rc = h2d_async(ctx, m, in->ent, N * M * A * 8)) return rc;
+  if (int rc = h2d_async(ctx, vo, in->vd_off, (N + 1) * 8)) return rc;
+  if (int rc = h2d_async(ctx, vc, in->vd_clock, Dv * A * 8)) return rc;
+  if (int rc = h2d_async(ctx, vm, in->vd_mem, Dv * 8)) return rc;
+  if (int rc = h2d_async(ctx, dr, in->def_row, D * 4)) return rc;
+  if (int rc = h2d_async(ctx, dc, in->def_clock, D * A * 8)) return rc;
+  if (int rc = h2d_async(ctx, dk, in->def_keys, D * Kw * 8)) return rc;
+  crdt_map_orswot_batch b = *in;
+  b.clock = c;
+  b.ec = e;
+  b.oc = o;
+  b.ent = m;
+  b.vd_off = vo;
+  b.vd_clock = vc;
+  b.vd_mem = vm;
+  b.def_row = dr;
+  b.def_clock = dc;
+  b.def_keys = dk;
+  crdt_map_orswot_out ob{oc, oe, oo, om, ovn, ovc, ovm, of, okp, ok2};
+  {
+    DeviceModeScope dev(ctx);
+    if (int rc = crdt_map_orswot_lub_many(ctx, &b, &ob)) return rc;
+  }
+  if (int rc = d2h_async(ctx, out->clock, oc, G * A * 8)) return rc;
+  if (int rc = d2h_async(ctx, out->ec, oe, G * K * A * 8)) return rc;
+  if (int rc = d2h_async(ctx, out->oc, oo, G * K * A * 8)) return rc;
+  if (int rc = d2h_async(ctx, out->ent, om, G * K * M * A * 8)) return rc;
+  if (int rc = d2h_async(ctx, out->vd_n, ovn, G * K * 4)) return rc;
+  if (int rc = d2h_async(ctx, out->vd_clock, ovc, G * K * VD * A * 8)) return rc;
+  if (int rc = d2h_async(ctx, out->vd_mem, ovm, G * K * VD * 8)) return rc;
+  if (int rc = d2h_async(ctx, out->flags, of, G * 4)) return rc;
+  if (int rc = d2h_async(ctx, out->def_keep, okp, D)) return rc;
+  if (int rc = d2h_async(ctx, out->def_keys, ok2, D * Kw * 8)) return rc;
+  return CRDT_OK;
+}
+
+int map_orswot_lub_many_host(crdt_ctx *ctx, const crdt_map_orswot_batch *in, crdt_map_orswot_out *out) {
+  if (!in || !out) return fail(ctx, CRDT_EINVAL, "map_orswot_lub_many: NULL batch/out");
+  if (in->G == 0 || in->K == 0 || in->A == 0) return CRDT_OK;
+  if (!out->clock || !out->ec || !out->oc || (in->M && !out->ent) || !out->vd_n || !out->vd_clock || !out->vd_mem ||
+      !out->flags)
+    return fail(ctx, CRDT_EINVAL, "map_orswot_lub_many: NULL output");
+  if (in->R && (!in->clock || !in->ec || !in->oc || (in->M && !in->ent) || !in->vd_off))
+    return fail(ctx, CRDT_EINVAL, "map_orswot_lub_many: NULL input");
+  if (in->R && in->Dv && (!in->vd_clock || !in->vd_mem)) return fail(ctx, CRDT_EINVAL, "map_orswot_lub_many: NULL vd rows");
+  if (in->def_off && in->def_off[0] != 0) return fail(ctx, CRDT_EINVAL, "map_orswot_lub_many: def_off[0] must be 0");
+  for (size_t i = 0; in->def_off && i < in->G; ++i)
+    if (in->def_off[i + 1] < in->def_off[i]) return fail(ctx, CRDT_EINVAL, "map_orswot_lub_many: def_off not non-decreasing");
+  if (in->def_off && in->def_off[in->G] && (!in->def_row || !in->def_clock || !in->def_keys))
+    return fail(ctx, CRDT_EINVAL, "map_orswot_lub_many: NULL deferred input");
+  for (auto [p, w] : {std::pair<const void *, const char *>{in->clock, "clock"}, {in->ec, "ec"}, {in->oc, "oc"},
+                      {in->ent, "ent"}, {in->vd_off, "vd_off"}, {in->vd_clock, "vd_clock"}, {in->vd_mem, "vd_mem"},
+                      {in->def_row, "def_row"}, {in->def_clock, "def_clock"}, {in->def_keys, "def_keys"},
+                      {out->clock, "out.clock"}, {out->ec, "out.ec"}, {out->oc, "out.oc"}, {out->ent, "out.ent"},
+                      {out->vd_n, "out.vd_n"}, {out->vd_clock, "out.vd_clock"}, {out->vd_mem, "out.vd_mem"},
+                      {out->flags, "out.flags"}, {out->def_keep, "out.def_keep"}, {out->def_keys, "out.def_keys"}})
+    if (int rc = check_host(ctx, p, w)) return rc;
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  DevScratch ds;
+  return finish(ctx, map_orswot_lub_host_body(ctx, in, out, ds));
+}
+
+static int map_nested_lub_host_body(crdt_ctx *ctx, const crdt_map_nested_batch *in, crdt_map_nested_out *out,
+                                    DevScratch &ds) {
+  const size_t G = in->G, R = in->R, K = in->K, K2 = in->K2, V = in->V, A = in->A, Kw = (K + 63) / 64, Di = in->Di;
+  const size_t D = in->def_off ? in->def_off[G] : 0, N = G * R * K;
+  constexpr size_t VS = 8, ID = 16;  // output slots per inner key / inner deferred per key (crdt_gpu.h)
+  uint64_t *c, *e, *ic, *iec, *ivc, *ivv, *io, *idc, *idk, *dc, *dk, *oc, *oe, *oic, *oiec, *oivc, *oivv, *oidc, *oidk,
+      *ok2 = nullptr;
+  uint32_t *dr, *onv, *oidn, *of;
+  uint8_t *okp = nullptr;
+  if (int rc = ds.get(ctx, G * R * A, &c)) return rc;
+  if (int rc = ds.get(ctx, N * A, &e)) return rc;
+  if (int rc = ds.get(ctx, N * A, &ic)) return rc;
+  if (int rc = ds.get(ctx, N * K2 * A, &iec)) return rc;
+  if (int rc = ds.get(ctx, N * K2 * V * A, &ivc)) return rc;
+  if (int rc = ds.get(ctx, N * K2 * V, &ivv)) return rc;
+  if (int rc = ds.get(ctx, N + 1, &io)) return rc;
+  if (int rc = ds.get(ctx, Di * A, &idc)) return rc;
+  if (int rc = ds.get(ctx, Di, &idk)) return rc;
+  if (int rc = ds.get(ctx, D, &dr)) return rc;
+  if (int rc = ds.get(ctx, D * A, &dc)) return rc;
+  if (int rc = ds.get(ctx, D * Kw, &dk)) return rc;
+  if (int rc = ds.get(ctx, G * A, &oc)) return rc;
+  if (int rc = ds.get(ctx, G * K * A, &oe)) return rc;
+  if (int rc = ds.get(ctx, G * K * A, &oic)) return rc;
+  if (int rc = ds.get(ctx, G * K * K2 * A, &oiec)) return rc;
+  if (int rc = ds.get(ctx, G * K * K2 * VS * A, &oivc)) return rc;
+  if (int rc = ds.get(ctx, G * K * K2 * VS, &oivv)) return rc;
+  if (int rc = ds.get(ctx, G * K * K2, &onv)) return rc;
+  if (int rc = ds.get(ctx, G * K, &oidn)) return rc;
+  if (int rc = ds.get(ctx, G * K * ID * A, &oidc)) return rc;
+  if (int rc = ds.get(ctx, G * K * ID, &oidk)) return rc;
+  if (int rc = ds.get(ctx, G, &of)) return rc;
+  if (out->def_keep)
+    if (int rc = ds.get(ctx, D, &okp)) return rc;
+  if (out->def_keys)
+    if (int rc = ds.get(ctx, D * Kw, &ok2)) return rc;
+  if (int rc = h2d_async(ctx, c, in->clock, G * R * A * 8)) return rc;
+  if (int rc = h2d_async(ctx, e, in->ec, N * A * 8)) return rc;
+  if (int rc = h2d_async(ctx, ic, in->ic, N * A * 8)) return rc;
+  if (int rc = h2d_async(ctx, iec, in->iec, N * K2 * A * 8)) return rc;
+  if (int rc = h2d_async(ctx, ivc, in->ivc, N * K2 * V * A * 8)) return rc;
+  if (int rc = h2d_async(ctx, ivv, in->ivv, N * K2 * V * 8)) return rc;
+  if (int rc = h2d_async(ctx, io, in->id_off, (N + 1) * 8)) return rc;
+  if (int rc = h2d_async(ctx, idc, in->id_clock, Di * A * 8)) return rc;
+  if (int rc = h2d_async(ctx, idk, in->id_keys, Di * 8)) return rc;
+  if (int rc = h2d_async(ctx, dr, in->def_row, D * 4)) return rc;
+  if (int rc = h2d_async(ctx, dc, in->def_clock, D * A * 8)) return rc;
+  if (int rc = h2d_async(ctx, dk, in->def_keys, D * Kw * 8)) return rc;
+  crdt_map_nested_batch b = *in;
+  b.clock = c;
+  b.ec = e;
+  b.ic = ic;
+  b.iec = iec;
+  b.ivc = ivc;
+  b.ivv = ivv;
+  b.id_off = io;
+  b.id_clock = idc;
+  b.id_keys = idk;
+  b.def_row = dr;
+  b.def_clock = dc;
+  b.def_keys = dk;
+  crdt_map_nested_out ob{oc, oe, oic, oiec, oivc, oivv, onv, oidn, oidc, oidk, of, okp, ok2};
+  {
+    DeviceModeScope dev(ctx);
+    if (int rc = crdt_map_nested_lub_many(ctx, &b, &ob)) return rc;
+  }
+  if (int rc = d2h_async(ctx, out->clock, oc, G * A * 8)) return rc;
+  if (int rc = d2h_async(ctx, out->ec, oe, G * K * A * 8)) return rc;
+  if (int rc = d2h_async(ctx, out->ic, oic, G * K * A * 8)) return rc;
+  if (int rc = d2h_async(ctx, out->iec, oiec, G * K * K2 * A * 8)) return rc;
+  if (int rc = d2h_async(ctx, out->ivc, oivc, G * K * K2 * VS * A * 8)) return rc;
+  if (int rc = d2h_async(ctx, out->ivv, oivv, G * K * K2 * VS * 8)) return rc;
+  if (int rc = d2h_async(ctx, out->nval, onv, G * K * K2 * 4)) return rc;
+  if (int rc = d2h_async(ctx, out->id_n, oidn, G * K * 4)) return rc;
+  if (int rc = d2h_async(ctx, out->id_clock, oidc, G * K * ID * A * 8)) return rc;
+  if (int rc = d2h_async(ctx, out->id_keys, oidk, G * K * ID * 8)) return rc;
+  if (int rc = d2h_async(ctx, out->flags, of, G * 4)) return rc;
+  if (int rc = d2h_async(ctx, out->def_keep, okp, D)) return rc;
+  if (int rc = d2h_async(ctx, out->def_keys, ok2, D * Kw * 8)) return rc;
+  return CRDT_OK;
+}
+
+int map_nested_lub_many_host(crdt_ctx *ctx, const crdt_map_nested_batch *in, crdt_map_nested_out *out) {
+  if (!in || !out) return fail(ctx, CRDT_EINVAL, "map_nested_lub_many: NULL batch/out");
+  if (in->G == 0 || in->K == 0 || in->A == 0) return CRDT_OK;
+  const size_t K2 = in->K2;
+  if (!out->clock || !out->ec || !out->ic || (K2 && (!out->iec || !out->ivc || !out->ivv || !out->nval)) || !out->id_n ||
+      !out->id_clock || !out->id_keys || !out->flags)
+    return fail(ctx, CRDT_EINVAL, "map_nested_lub_many: NULL output");
+  if (in->R && (!in->clock || !in->ec || !in->ic || !in->id_off || (K2 && !in->iec) || (K2 && in->V && (!in->ivc || !in->ivv))))
+    return fail(ctx, CRDT_EINVAL, "map_nested_lub_many: NULL input");
+  if (in->R && in->Di && (!in->id_clock || !in->id_keys)) return fail(ctx, CRDT_EINVAL, "map_nested_lub_many: NULL id rows");
+  if (in->def_off && in->def_off[0] != 0) return fail(ctx, CRDT_EINVAL, "map_nested_lub_many: def_off[0] must be 0");
+  for (size_t i = 0; in->def_off && i < in->G; ++i)
+    if (in->def_off[i + 1] < in->def_off[i]) return fail(ctx, CRDT_EINVAL, "map_nested_lub_many: def_off not non-decreasing");
+  if (in->def_off && in->def_off[in->G] && (!in->def_row || !in->def_clock || !in->def_keys))
+    return fail(ctx, CRDT_EINVAL, "map_nested_lub_many: NULL deferred input");
+  for (auto [p, w] : {std::pair<const void *, const char *>{in->clock, "clock"}, {in->ec, "ec"}, {in->ic, "ic"},
+                      {in->iec, "iec"}, {in->ivc, "ivc"}, {in->ivv, "ivv"}, {in->id_off, "id_off"},
+                      {in->id_clock, "id_clock"}, {in->id_keys, "id_keys"}, {in->def_row, "def_row"},
+                      {in->def_clock, "def_clock"}, {in->def_keys, "def_keys"}, {out->clock, "out.clock"},
+                      {out->ec, "out.ec"}, {out->ic, "out.ic"}, {out->iec, "out.iec"}, {out->ivc, "out.ivc"},
+                      {out->ivv, "out.ivv"}, {out->nval, "out.nval"}, {out->id_n, "out.id_n"},
+                      {out->id_clock, "out.id_clock"}, {out->id_keys, "out.id_keys"}, {out->flags, "out.flags"},
+                      {out->def_keep, "out.def_keep"}, {out->def_keys, "out.def_keys"}})
+    if (int rc = check_host(ctx, p, w)) return rc;
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  DevScratch ds;
+  return finish(ctx, map_nested_lub_host_body(ctx, in, out, ds));
+}
+
 int map_lub_many_host(crdt_ctx *ctx, const crdt_map_batch *in, crdt_map_out *out) {
   if (!in || !out) return fail(ctx, CRDT_EINVAL, "map_lub_many: NULL batch/out");
   if (in->G == 0) return CRDT_OK;

@@ -73,7 +73,9 @@ __device__ __forceinline__ bool mc_nz(const u64 (&x)[APL], u64 hm) {
 // key kb + h of the group, so a 32-actor key no longer leaves half the wave idle.  The group's
 // clock C and a remove's liveness (!(rm <= C)) are the same for every key of the group, so the
 // keys share one walk of the remove pool; each entry carries which of the wave's keys it names.
-template <int APL, int W, int RING, int KPW, int DEP = 8>
+// SPL > 0 (A == 64 / SPL: 32, 16 or 8 actors; one key per wave, register rows): the whole-chunk
+// skip below, with lane l holding actor l % A in every register of the key's state.
+template <int APL, int W, int RING, int KPW, int DEP = 8, int SPL = 0>
 __global__ __launch_bounds__(kMcWaves * kWave) void map_counter_fold_kernel(MapCounterPlan p) {
   constexpr bool DMA = RING > 0;
   constexpr int kMcRing = DMA ? RING : 1;
@@ -81,6 +83,7 @@ __global__ __launch_bounds__(kMcWaves * kWave) void map_counter_fold_kernel(MapC
                                                    // APL 1 ran slower: 20.0 vs 12.9 ms, probably the
                                                    // unrolled body's size)
   static_assert(KPW == 1 || (APL == 1 && !DMA), "several keys per wave: APL 1, register ring");
+  static_assert(SPL == 0 || (APL == 1 && KPW == 1 && !DMA), "chunk skip: one key per wave, APL 1, register rows");
   constexpr int NROW = kMcRowsB / (8 * kWave * APL);  // live rm rows cached in LDS
   constexpr int HL = kWave / KPW;                     // lanes per key
   extern __shared__ u64 lds[];
@@ -109,10 +112,12 @@ __global__ __launch_bounds__(kMcWaves * kWave) void map_counter_fold_kernel(MapC
   // counter's bookkeeping on branches, and the compiler then drains every outstanding load — the
   // replica ring's prefetch included — at the join).  Every row a lane holds, remove rows included,
   // is a copy of actor A-1 past A, so those lanes evolve exactly as actor A-1 and never change a vote.
+  // (SPL > 0: lane l reads actor l % A, A == 64 / SPL, so every lane holds a real actor)
   auto ld_row = [&](u64 (&x)[APL], const u64 *src) {
 #pragma unroll
     for (int j = 0; j < APL; ++j) {
-      const unsigned long long a = (unsigned long long)al + (unsigned long long)HL * j;
+      const unsigned long long a = SPL > 0 ? (unsigned long long)(lane & (kWave / (SPL > 0 ? SPL : 1) - 1))
+                                           : (unsigned long long)al + (unsigned long long)HL * j;
       x[j] = src[a < A ? a : A - 1];
     }
   };
@@ -207,9 +212,69 @@ __global__ __launch_bounds__(kMcWaves * kWave) void map_counter_fold_kernel(MapC
   unsigned aj[APL];  // the lane's actor per word, clamped to the row (see ld_row)
 #pragma unroll
   for (int j = 0; j < APL; ++j) {
-    const unsigned long long a = (unsigned long long)al + (unsigned long long)HL * j;
+    const unsigned long long a = SPL > 0 ? (unsigned long long)(lane & (kWave / (SPL > 0 ? SPL : 1) - 1))
+                                         : (unsigned long long)al + (unsigned long long)HL * j;
     aj[j] = (unsigned)(a < A ? a : A - 1);
   }
+  // Each live remove keeps a witness: an actor whose rm word is still above C.  T holds, per lane
+  // word, the least rm word among the removes witnessed there; while no C word reached its T, no
+  // live remove can have become dominated (C only grows), and the scan is skipped.  (chg: removes
+  // joined the live set this step.)
+  auto liveness = [&](bool chg) {
+    {
+      bool b = false;  // (no live removes: every T word is ~0, no vote)
+#pragma unroll
+      for (int j = 0; j < APL; ++j) b |= C[j] >= T[j];
+      if (chg || __ballot(b) != 0) {
+        bool changed = chg;
+#pragma unroll
+        for (int j = 0; j < APL; ++j) T[j] = ~0ull;
+        for (int i = 0; i < na;) {
+          u64 rm[APL];
+          live_row(i, rm);
+          bool wit = false;  // (every key's lanes hold rm and C: one vote)
+#pragma unroll
+          for (int j = 0; j < APL; ++j) {
+            const u64 m = __ballot(rm[j] > C[j]);
+            if (m && !wit) {
+              wit = true;
+              const int wl = __builtin_ctzll(m);
+              T[j] = lane == wl && rm[j] < T[j] ? rm[j] : T[j];
+            }
+          }
+          if (wit) {
+            ++i;
+            continue;
+          }
+          changed = true;  // dominated: no longer deferred; the last entry moves over it
+          const int lastp = na - 1;
+          if (i != lastp) {
+            u64 x[APL];
+            live_row(lastp, x);
+            put_row(i, x);
+            const unsigned li_last = live[lastp];
+            const uint8_t lm_last = lvm[lastp];
+            if (lane == 0) {
+              live[i] = li_last;
+              lvm[i] = lm_last;
+            }
+          }
+          --na;
+        }
+        if (changed) {
+#pragma unroll
+          for (int j = 0; j < APL; ++j) rk[j] = 0;
+          for (int i = 0; i < na; ++i) {
+            u64 rm[APL];
+            live_row(i, rm);
+            const bool named = (lvm[i] >> h) & 1u;
+#pragma unroll
+            for (int j = 0; j < APL; ++j) rk[j] = named && rm[j] > rk[j] ? rm[j] : rk[j];
+          }
+        }
+      }
+    }
+  };
   // one replica step on the key's state.  Lanes past A hold copies of actor A-1 (clamped loads;
   // every operation is lane-local), so they never change a vote and need no masking.
   //
@@ -283,64 +348,147 @@ __global__ __launch_bounds__(kMcWaves * kWave) void map_counter_fold_kernel(MapC
     // 3. self.clock.merge(other.clock) (:217), then a remove stays deferred while !(rm <= C)
 #pragma unroll
     for (int j = 0; j < APL; ++j) C[j] = C[j] > c2[j] ? C[j] : c2[j];
-    //    Each live remove keeps a witness: an actor whose rm word is still above C.  T holds, per
-    //    lane word, the least rm word among the removes witnessed there; while no C word reached its
-    //    T, no live remove can have become dominated (C only grows), and the scan is skipped.
-    {
-      bool b = false;  // (no live removes: every T word is ~0, no vote)
+    liveness(chg);
+  };
+  if constexpr (SPL > 0) {
+    // ---- whole-chunk skip (round 5).  Almost every replica step of a long fold leaves the key's
+    // (entry clock, value) unchanged (config-4 shape: ~7 of 16,384 steps change it), and a step's
+    // no-change test needs only the state, not the steps before it, once the state is assumed
+    // unchanged.  Chunks of S = 16 steps come into registers in a transposed layout — lane
+    // (hh, a) = (lane / A, lane % A) holds, in element i, actor a of step i*SPL + hh, so a 32-actor
+    // key uses all 64 lanes (two steps per instruction) — and are tested against the state at the
+    // chunk's start.  By induction every step of a chunk that passes leaves the state unchanged, so
+    // the chunk only merges its clocks (C |= its clock max) and re-tests the live removes once at
+    // its end (liveness only shrinks the forget rk, whose re-application is the identity on a state
+    // already forgotten by it).  A chunk holding a remove that names the key, a partial last chunk
+    // or a failed test runs its steps exactly.
+    //
+    // The per-element test, with the state (e, v_w, C0 = C at the chunk's start) and the step's
+    // (c2, e2, v2_w), derived from the exact join above (en == e and the value unchanged):
+    //   the acc holds the key (p1) and the step's replica too (p2):
+    //     (e2 == e || (c2 <= TE && e2 <= TB)) && e2 <= TV && v2_w <= (v_w ? v_w : x)   for every w
+    //     with TE = e ? e-1 : MAX (e == 0 or c2 < e), TB = max(C0, e ? e-1 : 0) (e2 < e or e2 <= C),
+    //     x = e2 > e ? e2 : 0 (the case's forget word) and TV = min_w (v_w ? max(e, v_w - 1) : MAX)
+    //     (the kept value survives x);
+    //   p1 without p2:  c2 <= min(TE, TV)  (the entry survives forget(e, c2); the value forget(.., x = c2 > e ? c2 : 0));
+    //   no p1:          e2 <= C0 (the replica's entry is not added: forget(e2, C) is empty).
+    // C only grows, so testing against C0 is sound; tests/test_map_counter_chunk_model.py checks the
+    // test against the exact join on op-replay, arbitrary and synthetic states.
+    constexpr int S = 16, NE = S / SPL, NB = W == 1 ? 4 : 3;
+    constexpr unsigned long long AA = kWave / SPL;  // == A
+    const int hh = lane / (int)AA;
+    const unsigned a = (unsigned)lane & (unsigned)(AA - 1);
+    const u64 *bc = p.clock + g * p.c_gs + a, *be = p.ec + g * p.e_gs + k * AA + a,
+              *bv = p.val + g * p.v_gs + k * W * AA + a;
+    const unsigned long long nch = (R + S - 1) / S;
+    u64 qc[NB][NE], qe[NB][NE], qv[NB][W][NE];
+    auto load_chunk = [&](auto B, unsigned long long c) {
+      constexpr int b = decltype(B)::value;
+      const unsigned long long r0 = c * S;
 #pragma unroll
-      for (int j = 0; j < APL; ++j) b |= C[j] >= T[j];
-      if (chg || __ballot(b) != 0) {
-        bool changed = chg;
+      for (int i = 0; i < NE; ++i) {
+        unsigned long long rr = r0 + (unsigned long long)(i * SPL + hh);
+        rr = rr < R ? rr : R - 1;  // (past the last replica: its row again, never used)
+        qc[b][i] = bc[rr * p.c_rs];
+        qe[b][i] = be[rr * p.e_rs];
 #pragma unroll
-        for (int j = 0; j < APL; ++j) T[j] = ~0ull;
-        for (int i = 0; i < na;) {
-          u64 rm[APL];
-          live_row(i, rm);
-          bool wit = false;  // (every key's lanes hold rm and C: one vote)
+        for (int w = 0; w < W; ++w) qv[b][w][i] = bv[rr * p.v_rs + w * AA];
+      }
+    };
+    auto test_chunk = [&](auto B) -> bool {
+      constexpr int b = decltype(B)::value;
+      const u64 e0 = e[0], C0 = C[0];
+      if (!mc_nz<1>(e, ~0ull)) {  // the acc lacks the key: no replica of the chunk may add it
+        u64 okm = ~0ull;
 #pragma unroll
-          for (int j = 0; j < APL; ++j) {
-            const u64 m = __ballot(rm[j] > C[j]);
-            if (m && !wit) {
-              wit = true;
-              const int wl = __builtin_ctzll(m);
-              T[j] = lane == wl && rm[j] < T[j] ? rm[j] : T[j];
-            }
-          }
-          if (wit) {
-            ++i;
-            continue;
-          }
-          changed = true;  // dominated: no longer deferred; the last entry moves over it
-          const int lastp = na - 1;
-          if (i != lastp) {
-            u64 x[APL];
-            live_row(lastp, x);
-            put_row(i, x);
-            const unsigned li_last = live[lastp];
-            const uint8_t lm_last = lvm[lastp];
-            if (lane == 0) {
-              live[i] = li_last;
-              lvm[i] = lm_last;
-            }
-          }
-          --na;
-        }
-        if (changed) {
+        for (int i = 0; i < NE; ++i) okm &= __ballot(qe[b][i] <= C0);
+        return okm == ~0ull;
+      }
+      const u64 em1 = e0 ? e0 - 1 : 0;
+      const u64 TE = e0 ? em1 : ~0ull, TB = C0 > em1 ? C0 : em1;
+      u64 TV = ~0ull;
+      bool vz[W];
 #pragma unroll
-          for (int j = 0; j < APL; ++j) rk[j] = 0;
-          for (int i = 0; i < na; ++i) {
-            u64 rm[APL];
-            live_row(i, rm);
-            const bool named = (lvm[i] >> h) & 1u;
+      for (int w = 0; w < W; ++w) {
+        const u64 vw = v[w][0];
+        vz[w] = vw == 0;
+        const u64 t = vz[w] ? ~0ull : (e0 > vw - 1 ? e0 : vw - 1);
+        TV = t < TV ? t : TV;
+      }
+      const u64 TN = TE < TV ? TE : TV;
+      u64 fail = 0;
 #pragma unroll
-            for (int j = 0; j < APL; ++j) rk[j] = named && rm[j] > rk[j] ? rm[j] : rk[j];
-          }
+      for (int i = 0; i < NE; ++i) {
+        const u64 e2 = qe[b][i], c2 = qc[b][i];
+        const u64 x = e2 > e0 ? e2 : 0;
+        bool cb = (e2 == e0 || (c2 <= TE && e2 <= TB)) && e2 <= TV;
+#pragma unroll
+        for (int w = 0; w < W; ++w) cb = cb && qv[b][w][i] <= (vz[w] ? x : v[w][0]);
+        const u64 mN = __ballot(e2 != 0), mB = __ballot(cb), mO = __ballot(c2 <= TN);
+#pragma unroll
+        for (int s2 = 0; s2 < SPL; ++s2) {
+          const u64 M = (AA == 64 ? ~0ull : ((1ull << AA) - 1)) << (s2 * AA);
+          const u64 sel = (mN & M) ? mB : mO;
+          fail |= ~sel & M;
         }
       }
+      return fail == 0;
+    };
+    auto body = [&](auto B, unsigned long long c) {
+      constexpr int b = decltype(B)::value;
+      if (c >= nch) return;
+      if (c + NB - 1 < nch) load_chunk(std::integral_constant<int, (b + NB - 1) % NB>{}, c + NB - 1);
+      const unsigned long long r0 = c * S;
+      const unsigned long long n = R - r0 < (unsigned long long)S ? R - r0 : S;
+      const bool skip = n == S && (unsigned long long)nxt >= r0 + S && test_chunk(B);
+      if (skip) {
+        u64 cm = 0;
+#pragma unroll
+        for (int i = 0; i < NE; ++i) cm = qc[b][i] > cm ? qc[b][i] : cm;
+#pragma unroll
+        for (int off = (int)AA; off < kWave; off <<= 1) {
+          const u64 o = __shfl_xor(cm, off);
+          cm = o > cm ? o : cm;
+        }
+        C[0] = C[0] > cm ? C[0] : cm;
+        liveness(false);
+        return;
+      }
+      for (int s2 = 0; s2 < (int)n; ++s2) {  // the chunk's steps, exactly (a step's rows moved into
+        const int i = s2 / SPL, src = (s2 % SPL) * (int)AA + (int)a;  // the lane = actor layout)
+        u64 c2[1] = {0}, e2[1] = {0}, v2[W][1];
+#pragma unroll
+        for (int w = 0; w < W; ++w) v2[w][0] = 0;
+#pragma unroll
+        for (int ii = 0; ii < NE; ++ii) {
+          if (ii == i) {
+            c2[0] = qc[b][ii];
+            e2[0] = qe[b][ii];
+#pragma unroll
+            for (int w = 0; w < W; ++w) v2[w][0] = qv[b][w][ii];
+          }
+        }
+        c2[0] = __shfl(c2[0], src);
+        e2[0] = __shfl(e2[0], src);
+#pragma unroll
+        for (int w = 0; w < W; ++w) v2[w][0] = __shfl(v2[w][0], src);
+        step(r0 + s2, c2, e2, v2);
+      }
+    };
+#pragma unroll
+    for (int b = 0; b + 1 < NB; ++b)
+      if ((unsigned long long)b < nch) {
+        if (b == 0) load_chunk(std::integral_constant<int, 0>{}, 0);
+        if (b == 1) load_chunk(std::integral_constant<int, 1>{}, 1);
+        if (b == 2) load_chunk(std::integral_constant<int, 2>{}, 2);
+      }
+    for (unsigned long long c = 0; c < nch; c += NB) {
+      body(std::integral_constant<int, 0>{}, c);
+      body(std::integral_constant<int, 1>{}, c + 1);
+      body(std::integral_constant<int, 2>{}, c + 2);
+      if constexpr (NB > 3) body(std::integral_constant<int, (NB > 3 ? 3 : 0)>{}, c + 3);
     }
-  };
-  if constexpr (DMA) {
+  } else if constexpr (DMA) {
     // lane l's 16-byte piece of the step image and its source row (advanced by the row stride)
     const unsigned long long o = 2ull * lane, I = (2 + W) * A;
     const bool on = o < I;
@@ -439,11 +587,11 @@ static size_t mc_lds() {
                              RING * 128 * 8 + kMcList + kMcLive);
 }
 
-template <int APL, int W, int RING = 0, int KPW = 1, int DEP = 8>
+template <int APL, int W, int RING = 0, int KPW = 1, int DEP = 8, int SPL = 0>
 static hipError_t launch_mc(const MapCounterPlan &p, hipStream_t s) {
   const unsigned long long blocks = (p.G * ((p.K + KPW - 1) / KPW) + kMcWaves - 1) / kMcWaves;
   const size_t lds = mc_lds<APL, RING>();
-  auto *fn = &map_counter_fold_kernel<APL, W, RING, KPW, DEP>;
+  auto *fn = &map_counter_fold_kernel<APL, W, RING, KPW, DEP, SPL>;
   if (lds > 64 * 1024) {
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(fn),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -459,7 +607,7 @@ using namespace crdt;
 
 extern "C" int crdt_map_counter_lub_many(crdt_ctx *ctx, const crdt_map_counter_batch *in,
                                          crdt_map_counter_out *out) {
-  CRDT_DEVICE_MEM_ONLY(ctx);
+  if (ctx && ctx->mem_kind == CRDT_MEM_HOST) return crdt::map_counter_lub_many_host(ctx, in, out);
   CRDT_CHECK_CTX(ctx);
   if (!in || !out) return fail(ctx, CRDT_EINVAL, "map_counter_lub_many: NULL batch/out");
   const size_t G = in->G, R = in->R, K = in->K, A = in->A, W = in->W;
@@ -496,7 +644,16 @@ extern "C" int crdt_map_counter_lub_many(crdt_ctx *ctx, const crdt_map_counter_b
     // wave ran 1.60 vs 2.52 ms, at 1,024 keys (one wave per SIMD) 5.33 vs 5.03 ms
     int kpw = ctx->tune.map_counter_kpw;
     const bool auto_kpw = kpw == 0;
-    if (auto_kpw) {
+    // the whole-chunk skip (one key per wave, A = 32 / 16 / 8, register rows) wins over pairing keys
+    const bool al16 = ((p.c_rs | p.c_gs | p.e_rs | p.e_gs | p.v_rs | p.v_gs) & 1) == 0 &&
+                      ((uintptr_t)in->clock & 15) == 0 && ((uintptr_t)in->ec & 15) == 0 &&
+                      ((uintptr_t)in->val & 15) == 0;
+    const int ring0 = A % 2 == 0 && (2 + W) * A <= 128 && al16 ? ctx->tune.map_counter_dma : 0;
+    const int spl = ctx->tune.map_counter_cs && !ring0 && ctx->tune.map_counter_depth == 8 && (auto_kpw || kpw == 1)
+                        ? (A == 32 ? 2 : (A == 16 ? 4 : (A == 8 ? 8 : 0)))
+                        : 0;
+    if (spl) kpw = 1;
+    if (auto_kpw && !spl) {
       const size_t waves_per_simd2 = 2048;
       kpw = A <= (size_t)kWave / 4 && G * ((K + 3) / 4) >= waves_per_simd2   ? 4
             : A <= (size_t)kWave / 2 && G * ((K + 1) / 2) >= waves_per_simd2 ? 2
@@ -519,7 +676,10 @@ extern "C" int crdt_map_counter_lub_many(crdt_ctx *ctx, const crdt_map_counter_b
     const bool al = ((p.c_rs | p.c_gs | p.e_rs | p.e_gs | p.v_rs | p.v_gs) & 1) == 0 &&
                     ((uintptr_t)in->clock & 15) == 0 && ((uintptr_t)in->ec & 15) == 0 && ((uintptr_t)in->val & 15) == 0;
     const int ring = A % 2 == 0 && (2 + W) * A <= 128 && al ? ctx->tune.map_counter_dma : 0;
-    if (!ring && kpw >= 4 && A <= (size_t)kWave / 4)
+    if (spl == 2) he = W == 1 ? launch_mc<1, 1, 0, 1, 8, 2>(p, ctx->stream) : launch_mc<1, 2, 0, 1, 8, 2>(p, ctx->stream);
+    else if (spl == 4) he = W == 1 ? launch_mc<1, 1, 0, 1, 8, 4>(p, ctx->stream) : launch_mc<1, 2, 0, 1, 8, 4>(p, ctx->stream);
+    else if (spl == 8) he = W == 1 ? launch_mc<1, 1, 0, 1, 8, 8>(p, ctx->stream) : launch_mc<1, 2, 0, 1, 8, 8>(p, ctx->stream);
+    else if (!ring && kpw >= 4 && A <= (size_t)kWave / 4)
       he = W == 1 ? launch_mc<1, 1, 0, 4>(p, ctx->stream) : launch_mc<1, 2, 0, 4>(p, ctx->stream);
     else if (!ring && kpw >= 2 && A <= (size_t)kWave / 2)
       he = W == 1 ? launch_mc<1, 1, 0, 2>(p, ctx->stream) : launch_mc<1, 2, 0, 2>(p, ctx->stream);

@@ -517,7 +517,7 @@ static size_t nm_lds() {
 using namespace crdt;
 
 extern "C" int crdt_map_nested_lub_many(crdt_ctx *ctx, const crdt_map_nested_batch *in, crdt_map_nested_out *out) {
-  CRDT_DEVICE_MEM_ONLY(ctx);
+  if (ctx && ctx->mem_kind == CRDT_MEM_HOST) return crdt::map_nested_lub_many_host(ctx, in, out);
   CRDT_CHECK_CTX(ctx);
   if (!in || !out) return fail(ctx, CRDT_EINVAL, "map_nested_lub_many: NULL batch/out");
   const size_t G = in->G, R = in->R, K = in->K, K2 = in->K2, V = in->V, A = in->A;

@@ -385,7 +385,7 @@ static hipError_t launch_mo(const MapOrswotPlan &p, hipStream_t s) {
 using namespace crdt;
 
 extern "C" int crdt_map_orswot_lub_many(crdt_ctx *ctx, const crdt_map_orswot_batch *in, crdt_map_orswot_out *out) {
-  CRDT_DEVICE_MEM_ONLY(ctx);
+  if (ctx && ctx->mem_kind == CRDT_MEM_HOST) return crdt::map_orswot_lub_many_host(ctx, in, out);
   CRDT_CHECK_CTX(ctx);
   if (!in || !out) return fail(ctx, CRDT_EINVAL, "map_orswot_lub_many: NULL batch/out");
   const size_t G = in->G, R = in->R, K = in->K, M = in->M, A = in->A;

@@ -15,7 +15,8 @@
 //! `VClock::apply_dot` never stores 0, `vclock.rs:155-159`), merged on the GPU, and rebuilt.
 //! The lattice types and `LWWReg` hand their host rows straight to the library through a second
 //! ctx in `CRDT_MEM_HOST` mode (it streams them through HBM in chunks, overlapping PCIe with the
-//! fold; `Orswot` batches are staged whole).  [`DeviceBuf`] stays for callers that manage device
+//! fold; `Orswot` and `Map` batches stream the same way, the value-typed Maps are staged whole).
+//! [`DeviceBuf`] stays for callers that manage device
 //! memory themselves.  Callers that keep replica states
 //! resident in HBM use [`ffi`] directly on device buffers with [`GpuCtx::as_ptr`].
 //!
@@ -1028,6 +1029,538 @@ impl<K: Ord + Clone, V: Clone, A: Actor> BatchCvRDT for Map<K, MVReg<V, A>, A> {
             selves[i] = d.egress(&sc[i * a..(i + 1) * a], &sec[i * k * a..(i + 1) * k * a],
                                  &svc[i * k * vs * a..(i + 1) * k * vs * a], &svv[i * k * vs..(i + 1) * k * vs], vs,
                                  &defs, &arena);
+        }
+        Ok(())
+    }
+}
+
+// ---- Map<K, V, A> with counter, Orswot and nested-Map values (round 5) ----------------------------
+// The library folds each key of these Maps in replica order (crdt_map_counter_lub_many,
+// crdt_map_orswot_lub_many, crdt_map_nested_lub_many; host arrays through the CRDT_MEM_HOST ctx, staged
+// whole).  `lub_many` is one group of R replicas; `merge_batch` is N groups of the two replicas
+// [self_i, other_i]: Map::new().merge(s).merge(o) == s.merge(o) for every state a replica can hold (its
+// deferred removes already applied to its entries and not covered by its own clock, map.rs:318-348).
+
+/// A batch of groups, each a fold of its replicas: (clock, ec [K][A], the Map's deferred pool).
+struct GroupPool {
+    def_off: Vec<usize>,
+    def_row: Vec<u32>,
+    def_clock: Vec<u64>,
+    def_keys: Vec<u64>,
+}
+
+fn key_bits<K: Ord + Clone>(ks: &BTreeSet<K>, idx: &Index<K>, kw: usize) -> Vec<u64> {
+    let mut bits = vec![0u64; kw];
+    for key in ks {
+        let b = idx.pos[key];
+        bits[b / 64] |= 1u64 << (b % 64);
+    }
+    bits
+}
+
+fn bit_keys<K: Ord + Clone>(bits: &[u64], idx: &Index<K>) -> BTreeSet<K> {
+    let mut ks = BTreeSet::new();
+    for (w, &word) in bits.iter().enumerate() {
+        let mut x = word;
+        while x != 0 {
+            let b = w * 64 + x.trailing_zeros() as usize;
+            x &= x - 1;
+            if b < idx.ids.len() {
+                ks.insert(idx.ids[b].clone());
+            }
+        }
+    }
+    ks
+}
+
+/// The Map-level interning shared by the value-typed Maps: actors and keys of the Map itself.
+fn map_level_index<'a, K: Ord + Clone + 'a, V: crate::map::Val<A> + 'a, A: Actor + 'a>(
+    states: &[&'a Map<K, V, A>], actors: &mut Index<A>, keys: &mut Index<K>) {
+    for s in states {
+        for a in s.clock.dots.keys() {
+            actors.intern(a);
+        }
+        for (k, e) in s.entries.iter() {
+            keys.intern(k);
+            for a in e.clock.dots.keys() {
+                actors.intern(a);
+            }
+        }
+        for (rm, ks) in s.deferred.iter() {
+            for a in rm.dots.keys() {
+                actors.intern(a);
+            }
+            for k in ks {
+                keys.intern(k);
+            }
+        }
+    }
+}
+
+/// The Map's own deferred removes of every group, pooled in replica order (def_row local to its group).
+fn group_pool<K: Ord + Clone, V: crate::map::Val<A>, A: Actor>(groups: &[Vec<&Map<K, V, A>>], actors: &Index<A>,
+                                                               keys: &Index<K>) -> GroupPool {
+    let (a, kw) = (actors.width(), (keys.width() + 63) / 64);
+    let mut p = GroupPool { def_off: vec![0], def_row: Vec::new(), def_clock: Vec::new(), def_keys: Vec::new() };
+    for g in groups {
+        for (r, s) in g.iter().enumerate() {
+            for (rm, ks) in s.deferred.iter() {
+                let mut row = vec![0u64; a];
+                clock_row(rm, actors, &mut row);
+                p.def_row.push(r as u32);
+                p.def_clock.extend(row);
+                p.def_keys.extend(key_bits(ks, keys, kw));
+            }
+        }
+        p.def_off.push(p.def_row.len());
+    }
+    p
+}
+
+/// The surviving removes of group g (def_keep / def_keys of the call) as the Map's deferred map.
+fn group_survivors<K: Ord + Clone, A: Actor>(p: &GroupPool, g: usize, keep: &[u8], okeys: &[u64], actors: &Index<A>,
+                                             keys: &Index<K>) -> HashMap<VClock<A>, BTreeSet<K>> {
+    let (a, kw) = (actors.width(), (keys.width() + 63) / 64);
+    let mut out: HashMap<VClock<A>, BTreeSet<K>> = HashMap::new();
+    for d in p.def_off[g]..p.def_off[g + 1] {
+        if keep[d] != 0 {
+            let ks = bit_keys(&okeys[d * kw..(d + 1) * kw], keys);
+            out.entry(row_clock(&p.def_clock[d * a..(d + 1) * a], actors)).or_insert_with(BTreeSet::new).extend(ks);
+        }
+    }
+    out
+}
+
+fn pairs_as_groups<'a, T>(selves: &'a [T], others: &'a [T]) -> Vec<Vec<&'a T>> {
+    selves.iter().zip(others.iter()).map(|(s, o)| vec![s, o]).collect()
+}
+
+/// GCounter (one row) / PNCounter (P | N rows) as the value rows of the counter Map fold.
+trait CounterVal<A: Actor>: crate::map::Val<A> + Default + Sized {
+    const W: usize;
+    fn intern_actors(&self, idx: &mut Index<A>);
+    fn rows(&self, idx: &Index<A>, out: &mut [u64]);
+    fn from_rows(rows: &[u64], idx: &Index<A>) -> Self;
+}
+
+impl<A: Actor> CounterVal<A> for GCounter<A> {
+    const W: usize = 1;
+    fn intern_actors(&self, idx: &mut Index<A>) {
+        for a in self.inner.dots.keys() {
+            idx.intern(a);
+        }
+    }
+    fn rows(&self, idx: &Index<A>, out: &mut [u64]) {
+        clock_row(&self.inner, idx, out);
+    }
+    fn from_rows(rows: &[u64], idx: &Index<A>) -> Self {
+        let mut g = GCounter::new();
+        g.inner = row_clock(rows, idx);
+        g
+    }
+}
+
+impl<A: Actor> CounterVal<A> for PNCounter<A> {
+    const W: usize = 2;
+    fn intern_actors(&self, idx: &mut Index<A>) {
+        for a in self.p.inner.dots.keys().chain(self.n.inner.dots.keys()) {
+            idx.intern(a);
+        }
+    }
+    fn rows(&self, idx: &Index<A>, out: &mut [u64]) {
+        let a = idx.width();
+        clock_row(&self.p.inner, idx, &mut out[..a]);
+        clock_row(&self.n.inner, idx, &mut out[a..2 * a]);
+    }
+    fn from_rows(rows: &[u64], idx: &Index<A>) -> Self {
+        let a = idx.width();
+        let mut c = PNCounter::new();
+        c.p.inner = row_clock(&rows[..a], idx);
+        c.n.inner = row_clock(&rows[a..2 * a], idx);
+        c
+    }
+}
+
+/// Every group's fold of Map<K, counter> (crdt_map_counter_lub_many, G groups of equal R).
+fn counter_map_folds<K: Ord + Clone, V: CounterVal<A>, A: Actor>(ctx: &GpuCtx, groups: &[Vec<&Map<K, V, A>>])
+                                                                 -> Result<Vec<Map<K, V, A>>, GpuError> {
+    let (g, r) = (groups.len(), groups[0].len());
+    let (mut actors, mut keys) = (Index::new(), Index::new());
+    let all: Vec<&Map<K, V, A>> = groups.iter().flat_map(|x| x.iter().copied()).collect();
+    map_level_index(&all, &mut actors, &mut keys);
+    for s in &all {
+        for e in s.entries.values() {
+            e.val.intern_actors(&mut actors);
+        }
+    }
+    let (a, k, w) = (actors.width(), keys.width(), V::W);
+    let kw = (k + 63) / 64;
+    let (mut clock, mut ec, mut val) = (vec![0u64; g * r * a], vec![0u64; g * r * k * a], vec![0u64; g * r * k * w * a]);
+    for (i, s) in all.iter().enumerate() {
+        clock_row(&s.clock, &actors, &mut clock[i * a..(i + 1) * a]);
+        for (key, e) in s.entries.iter() {
+            let j = keys.pos[key];
+            clock_row(&e.clock, &actors, &mut ec[(i * k + j) * a..(i * k + j + 1) * a]);
+            e.val.rows(&actors, &mut val[(i * k + j) * w * a..(i * k + j + 1) * w * a]);
+        }
+    }
+    let pool = group_pool(groups, &actors, &keys);
+    let nd = pool.def_row.len();
+    let batch = ffi::crdt_map_counter_batch {
+        G: g, R: r, K: k, A: a, W: w,
+        clock: clock.as_ptr(), clock_rstride: a, clock_gstride: r * a,
+        ec: ec.as_ptr(), ec_rstride: k * a, ec_gstride: r * k * a,
+        val: val.as_ptr(), val_rstride: k * w * a, val_gstride: r * k * w * a,
+        def_off: if nd > 0 { pool.def_off.as_ptr() } else { ptr::null() },
+        def_row: pool.def_row.as_ptr(), def_clock: pool.def_clock.as_ptr(), def_keys: pool.def_keys.as_ptr(),
+    };
+    let (mut oc, mut oec, mut ov) = (vec![0u64; g * a], vec![0u64; g * k * a], vec![0u64; g * k * w * a]);
+    let (mut flags, mut keep, mut okeys) = (vec![0u32; g], vec![0u8; nd], vec![0u64; nd * kw]);
+    let mut out = ffi::crdt_map_counter_out {
+        clock: oc.as_mut_ptr(), ec: oec.as_mut_ptr(), val: ov.as_mut_ptr(), flags: flags.as_mut_ptr(),
+        def_keep: if nd > 0 { keep.as_mut_ptr() } else { ptr::null_mut() },
+        def_keys: if nd > 0 { okeys.as_mut_ptr() } else { ptr::null_mut() },
+    };
+    ctx.check_host(unsafe { ffi::crdt_map_counter_lub_many(ctx.host, &batch, &mut out) })?;
+    if let Some(f) = flags.iter().find(|&&f| f != 0) {
+        return Err(unsupported(format!("Map<K, counter> lub_many flags {}", f)));
+    }
+    let mut res = Vec::with_capacity(g);
+    for gi in 0..g {
+        let mut m: Map<K, V, A> = Map::new();
+        m.clock = row_clock(&oc[gi * a..(gi + 1) * a], &actors);
+        for (j, key) in keys.ids.iter().enumerate() {
+            let row = &oec[(gi * k + j) * a..(gi * k + j + 1) * a];
+            if row.iter().any(|&x| x != 0) {
+                let v = V::from_rows(&ov[(gi * k + j) * w * a..(gi * k + j + 1) * w * a], &actors);
+                m.entries.insert(key.clone(), Entry { clock: row_clock(row, &actors), val: v });
+            }
+        }
+        m.deferred = group_survivors(&pool, gi, &keep, &okeys, &actors, &keys);
+        res.push(m);
+    }
+    Ok(res)
+}
+
+impl<K: Ord + Clone, A: Actor> BatchCvRDT for Map<K, GCounter<A>, A> {
+    fn lub_many(ctx: &GpuCtx, replicas: Vec<Self>) -> Result<Self, GpuError> {
+        if replicas.is_empty() {
+            return Ok(Map::new());
+        }
+        Ok(counter_map_folds(ctx, &[replicas.iter().collect()])?.remove(0))
+    }
+    fn merge_batch(ctx: &GpuCtx, selves: &mut [Self], others: Vec<Self>) -> Result<(), GpuError> {
+        check_pairs(selves.len(), others.len())?;
+        if selves.is_empty() {
+            return Ok(());
+        }
+        let merged = counter_map_folds(ctx, &pairs_as_groups(selves, &others))?;
+        for (s, m) in selves.iter_mut().zip(merged) {
+            *s = m;
+        }
+        Ok(())
+    }
+}
+
+impl<K: Ord + Clone, A: Actor> BatchCvRDT for Map<K, PNCounter<A>, A> {
+    fn lub_many(ctx: &GpuCtx, replicas: Vec<Self>) -> Result<Self, GpuError> {
+        if replicas.is_empty() {
+            return Ok(Map::new());
+        }
+        Ok(counter_map_folds(ctx, &[replicas.iter().collect()])?.remove(0))
+    }
+    fn merge_batch(ctx: &GpuCtx, selves: &mut [Self], others: Vec<Self>) -> Result<(), GpuError> {
+        check_pairs(selves.len(), others.len())?;
+        if selves.is_empty() {
+            return Ok(());
+        }
+        let merged = counter_map_folds(ctx, &pairs_as_groups(selves, &others))?;
+        for (s, m) in selves.iter_mut().zip(merged) {
+            *s = m;
+        }
+        Ok(())
+    }
+}
+
+/// Limits of the Map<K, Orswot> fold (include/crdt_gpu.h: A <= 64, M <= 32, 16 nested removes).
+pub const MAP_ORSWOT_MAX_ACTORS: usize = 64;
+pub const MAP_ORSWOT_MAX_MEMBERS: usize = 32;
+
+/// Every group's fold of Map<K, Orswot<M>> (crdt_map_orswot_lub_many, G groups of equal R).
+fn orswot_map_folds<K: Ord + Clone, M: Member, A: Actor>(ctx: &GpuCtx, groups: &[Vec<&Map<K, Orswot<M, A>, A>>])
+                                                         -> Result<Vec<Map<K, Orswot<M, A>, A>>, GpuError> {
+    let (g, r) = (groups.len(), groups[0].len());
+    let (mut actors, mut keys, mut mems) = (Index::new(), Index::new(), HIndex::new());
+    let all: Vec<&Map<K, Orswot<M, A>, A>> = groups.iter().flat_map(|x| x.iter().copied()).collect();
+    map_level_index(&all, &mut actors, &mut keys);
+    for s in &all {
+        for e in s.entries.values() {
+            for x in e.val.clock.dots.keys() {
+                actors.intern(x);
+            }
+            for (mem, c) in e.val.entries.iter() {
+                mems.intern(mem);
+                for x in c.dots.keys() {
+                    actors.intern(x);
+                }
+            }
+            for (rm, ms) in e.val.deferred.iter() {
+                for x in rm.dots.keys() {
+                    actors.intern(x);
+                }
+                for mem in ms {
+                    mems.intern(mem);
+                }
+            }
+        }
+    }
+    let (a, k, m) = (actors.width(), keys.width(), mems.width());
+    if a > MAP_ORSWOT_MAX_ACTORS || m > MAP_ORSWOT_MAX_MEMBERS {
+        return Err(unsupported(format!("Map<K, Orswot> lub_many: {} actors / {} members (limits {} / {})", a, m,
+                                       MAP_ORSWOT_MAX_ACTORS, MAP_ORSWOT_MAX_MEMBERS)));
+    }
+    let kw = (k + 63) / 64;
+    let n = g * r * k;
+    let (mut clock, mut ec, mut oc) = (vec![0u64; g * r * a], vec![0u64; n * a], vec![0u64; n * a]);
+    let mut ent = vec![0u64; n * m * a];
+    let (mut vd_off, mut vd_clock, mut vd_mem) = (vec![0u64], Vec::new(), Vec::new());
+    for (i, s) in all.iter().enumerate() {
+        clock_row(&s.clock, &actors, &mut clock[i * a..(i + 1) * a]);
+        for j in 0..k {
+            if let Some(e) = s.entries.get(&keys.ids[j]) {
+                let b = i * k + j;
+                clock_row(&e.clock, &actors, &mut ec[b * a..(b + 1) * a]);
+                clock_row(&e.val.clock, &actors, &mut oc[b * a..(b + 1) * a]);
+                for (mem, c) in e.val.entries.iter() {
+                    let mi = mems.pos[mem];
+                    clock_row(c, &actors, &mut ent[(b * m + mi) * a..(b * m + mi + 1) * a]);
+                }
+                for (rm, ms) in e.val.deferred.iter() {
+                    let mut row = vec![0u64; a];
+                    clock_row(rm, &actors, &mut row);
+                    vd_clock.extend(row);
+                    vd_mem.push(ms.iter().fold(0u64, |acc, x| acc | (1u64 << mems.pos[x])));
+                }
+            }
+            vd_off.push(vd_mem.len() as u64);
+        }
+    }
+    let pool = group_pool(groups, &actors, &keys);
+    let (nd, dv) = (pool.def_row.len(), vd_mem.len());
+    let batch = ffi::crdt_map_orswot_batch {
+        G: g, R: r, K: k, M: m, A: a,
+        clock: clock.as_ptr(), ec: ec.as_ptr(), oc: oc.as_ptr(), ent: ent.as_ptr(),
+        vd_off: vd_off.as_ptr(), vd_clock: vd_clock.as_ptr(), vd_mem: vd_mem.as_ptr(),
+        def_off: if nd > 0 { pool.def_off.as_ptr() } else { ptr::null() },
+        def_row: pool.def_row.as_ptr(), def_clock: pool.def_clock.as_ptr(), def_keys: pool.def_keys.as_ptr(),
+        Dv: dv,
+    };
+    let (mut o_clock, mut o_ec, mut o_oc) = (vec![0u64; g * a], vec![0u64; g * k * a], vec![0u64; g * k * a]);
+    let (mut o_ent, mut o_vdn) = (vec![0u64; g * k * m * a], vec![0u32; g * k]);
+    let (mut o_vdc, mut o_vdm) = (vec![0u64; g * k * 16 * a], vec![0u64; g * k * 16]);
+    let (mut flags, mut keep, mut okeys) = (vec![0u32; g], vec![0u8; nd], vec![0u64; nd * kw]);
+    let mut out = ffi::crdt_map_orswot_out {
+        clock: o_clock.as_mut_ptr(), ec: o_ec.as_mut_ptr(), oc: o_oc.as_mut_ptr(), ent: o_ent.as_mut_ptr(),
+        vd_n: o_vdn.as_mut_ptr(), vd_clock: o_vdc.as_mut_ptr(), vd_mem: o_vdm.as_mut_ptr(), flags: flags.as_mut_ptr(),
+        def_keep: if nd > 0 { keep.as_mut_ptr() } else { ptr::null_mut() },
+        def_keys: if nd > 0 { okeys.as_mut_ptr() } else { ptr::null_mut() },
+    };
+    ctx.check_host(unsafe { ffi::crdt_map_orswot_lub_many(ctx.host, &batch, &mut out) })?;
+    if let Some(f) = flags.iter().find(|&&f| f != 0) {
+        return Err(unsupported(format!("Map<K, Orswot> lub_many flags {}", f)));
+    }
+    let mut res = Vec::with_capacity(g);
+    for gi in 0..g {
+        let mut mp: Map<K, Orswot<M, A>, A> = Map::new();
+        mp.clock = row_clock(&o_clock[gi * a..(gi + 1) * a], &actors);
+        for (j, key) in keys.ids.iter().enumerate() {
+            let b = gi * k + j;
+            let row = &o_ec[b * a..(b + 1) * a];
+            if row.iter().all(|&x| x == 0) {
+                continue;
+            }
+            let mut o = Orswot::new();
+            o.clock = row_clock(&o_oc[b * a..(b + 1) * a], &actors);
+            for (mi, mem) in mems.ids.iter().enumerate() {
+                let er = &o_ent[(b * m + mi) * a..(b * m + mi + 1) * a];
+                if er.iter().any(|&x| x != 0) {
+                    o.entries.insert(mem.clone(), row_clock(er, &actors));
+                }
+            }
+            for i in 0..o_vdn[b] as usize {
+                let bits = o_vdm[b * 16 + i];
+                let ms: HashSet<M> = (0..m).filter(|&x| (bits >> x) & 1 != 0).map(|x| mems.ids[x].clone()).collect();
+                o.deferred.entry(row_clock(&o_vdc[(b * 16 + i) * a..(b * 16 + i + 1) * a], &actors))
+                    .or_insert_with(HashSet::new).extend(ms);
+            }
+            mp.entries.insert(key.clone(), Entry { clock: row_clock(row, &actors), val: o });
+        }
+        mp.deferred = group_survivors(&pool, gi, &keep, &okeys, &actors, &keys);
+        res.push(mp);
+    }
+    Ok(res)
+}
+
+impl<K: Ord + Clone, M: Member, A: Actor> BatchCvRDT for Map<K, Orswot<M, A>, A> {
+    fn lub_many(ctx: &GpuCtx, replicas: Vec<Self>) -> Result<Self, GpuError> {
+        if replicas.is_empty() {
+            return Ok(Map::new());
+        }
+        Ok(orswot_map_folds(ctx, &[replicas.iter().collect()])?.remove(0))
+    }
+    fn merge_batch(ctx: &GpuCtx, selves: &mut [Self], others: Vec<Self>) -> Result<(), GpuError> {
+        check_pairs(selves.len(), others.len())?;
+        if selves.is_empty() {
+            return Ok(());
+        }
+        let merged = orswot_map_folds(ctx, &pairs_as_groups(selves, &others))?;
+        for (s, m) in selves.iter_mut().zip(merged) {
+            *s = m;
+        }
+        Ok(())
+    }
+}
+
+/// Limits of the nested Map fold (include/crdt_gpu.h: A <= 64, K2 <= 64, V <= 8 values per register).
+pub const MAP_NESTED_MAX_ACTORS: usize = 64;
+pub const MAP_NESTED_MAX_INNER_KEYS: usize = 64;
+pub const MAP_NESTED_MAX_VALUES: usize = 8;
+
+/// Every group's fold of Map<K, Map<K2, MVReg<V>>> (crdt_map_nested_lub_many, G groups of equal R) —
+/// the type of the reference's own Map tests (test/map.rs:10).  Values travel as arena ids, as for
+/// Map<K, MVReg> (MVReg::merge compares value clocks only).
+fn nested_map_folds<K: Ord + Clone, K2: Ord + Clone, V: Clone, A: Actor>(
+    ctx: &GpuCtx, groups: &[Vec<&Map<K, Map<K2, MVReg<V, A>, A>, A>>])
+    -> Result<Vec<Map<K, Map<K2, MVReg<V, A>, A>, A>>, GpuError> {
+    let (g, r) = (groups.len(), groups[0].len());
+    let (mut actors, mut keys, mut ikeys) = (Index::new(), Index::new(), Index::new());
+    let all: Vec<&Map<K, Map<K2, MVReg<V, A>, A>, A>> = groups.iter().flat_map(|x| x.iter().copied()).collect();
+    map_level_index(&all, &mut actors, &mut keys);
+    let mut vmax = 1usize;
+    for s in &all {
+        for e in s.entries.values() {
+            let inner = [&e.val];
+            map_level_index(&inner, &mut actors, &mut ikeys);
+            for ie in e.val.entries.values() {
+                vmax = vmax.max(ie.val.vals.len());
+                for (c, _) in ie.val.vals.iter() {
+                    for x in c.dots.keys() {
+                        actors.intern(x);
+                    }
+                }
+            }
+        }
+    }
+    let (a, k, k2, v) = (actors.width(), keys.width(), ikeys.width(), vmax);
+    if a > MAP_NESTED_MAX_ACTORS || k2 > MAP_NESTED_MAX_INNER_KEYS || v > MAP_NESTED_MAX_VALUES {
+        return Err(unsupported(format!("nested Map lub_many: {} actors / {} inner keys / {} values (limits {} / {} / {})",
+                                       a, k2, v, MAP_NESTED_MAX_ACTORS, MAP_NESTED_MAX_INNER_KEYS,
+                                       MAP_NESTED_MAX_VALUES)));
+    }
+    let kw = (k + 63) / 64;
+    let n = g * r * k;
+    let (mut clock, mut ec, mut ic) = (vec![0u64; g * r * a], vec![0u64; n * a], vec![0u64; n * a]);
+    let (mut iec, mut ivc, mut ivv) = (vec![0u64; n * k2 * a], vec![0u64; n * k2 * v * a], vec![0u64; n * k2 * v]);
+    let (mut id_off, mut id_clock, mut id_keys) = (vec![0u64], Vec::new(), Vec::new());
+    let mut arena: Vec<V> = Vec::new();
+    for (i, s) in all.iter().enumerate() {
+        clock_row(&s.clock, &actors, &mut clock[i * a..(i + 1) * a]);
+        for j in 0..k {
+            if let Some(e) = s.entries.get(&keys.ids[j]) {
+                let b = i * k + j;
+                clock_row(&e.clock, &actors, &mut ec[b * a..(b + 1) * a]);
+                clock_row(&e.val.clock, &actors, &mut ic[b * a..(b + 1) * a]);
+                for (ik, ie) in e.val.entries.iter() {
+                    let q = b * k2 + ikeys.pos[ik];
+                    clock_row(&ie.clock, &actors, &mut iec[q * a..(q + 1) * a]);
+                    mvreg_rows(&ie.val, &actors, v, &mut arena, &mut ivc[q * v * a..(q + 1) * v * a],
+                               &mut ivv[q * v..(q + 1) * v]);
+                }
+                for (rm, ks) in e.val.deferred.iter() {
+                    let mut row = vec![0u64; a];
+                    clock_row(rm, &actors, &mut row);
+                    id_clock.extend(row);
+                    id_keys.push(key_bits(ks, &ikeys, 1)[0]);
+                }
+            }
+            id_off.push(id_keys.len() as u64);
+        }
+    }
+    let pool = group_pool(groups, &actors, &keys);
+    let (nd, di) = (pool.def_row.len(), id_keys.len());
+    let batch = ffi::crdt_map_nested_batch {
+        G: g, R: r, K: k, K2: k2, V: v, A: a,
+        clock: clock.as_ptr(), ec: ec.as_ptr(), ic: ic.as_ptr(), iec: iec.as_ptr(), ivc: ivc.as_ptr(), ivv: ivv.as_ptr(),
+        id_off: id_off.as_ptr(), id_clock: id_clock.as_ptr(), id_keys: id_keys.as_ptr(), Di: di,
+        def_off: if nd > 0 { pool.def_off.as_ptr() } else { ptr::null() },
+        def_row: pool.def_row.as_ptr(), def_clock: pool.def_clock.as_ptr(), def_keys: pool.def_keys.as_ptr(),
+    };
+    let (mut o_clock, mut o_ec, mut o_ic) = (vec![0u64; g * a], vec![0u64; g * k * a], vec![0u64; g * k * a]);
+    let (mut o_iec, mut o_ivc, mut o_ivv) = (vec![0u64; g * k * k2 * a], vec![0u64; g * k * k2 * 8 * a],
+                                             vec![0u64; g * k * k2 * 8]);
+    let (mut o_nval, mut o_idn) = (vec![0u32; g * k * k2], vec![0u32; g * k]);
+    let (mut o_idc, mut o_idk) = (vec![0u64; g * k * 16 * a], vec![0u64; g * k * 16]);
+    let (mut flags, mut keep, mut okeys) = (vec![0u32; g], vec![0u8; nd], vec![0u64; nd * kw]);
+    let mut out = ffi::crdt_map_nested_out {
+        clock: o_clock.as_mut_ptr(), ec: o_ec.as_mut_ptr(), ic: o_ic.as_mut_ptr(), iec: o_iec.as_mut_ptr(),
+        ivc: o_ivc.as_mut_ptr(), ivv: o_ivv.as_mut_ptr(), nval: o_nval.as_mut_ptr(), id_n: o_idn.as_mut_ptr(),
+        id_clock: o_idc.as_mut_ptr(), id_keys: o_idk.as_mut_ptr(), flags: flags.as_mut_ptr(),
+        def_keep: if nd > 0 { keep.as_mut_ptr() } else { ptr::null_mut() },
+        def_keys: if nd > 0 { okeys.as_mut_ptr() } else { ptr::null_mut() },
+    };
+    ctx.check_host(unsafe { ffi::crdt_map_nested_lub_many(ctx.host, &batch, &mut out) })?;
+    if let Some(f) = flags.iter().find(|&&f| f != 0) {
+        return Err(unsupported(format!("nested Map lub_many flags {}", f)));
+    }
+    let mut res = Vec::with_capacity(g);
+    for gi in 0..g {
+        let mut mp: Map<K, Map<K2, MVReg<V, A>, A>, A> = Map::new();
+        mp.clock = row_clock(&o_clock[gi * a..(gi + 1) * a], &actors);
+        for (j, key) in keys.ids.iter().enumerate() {
+            let b = gi * k + j;
+            let row = &o_ec[b * a..(b + 1) * a];
+            if row.iter().all(|&x| x == 0) {
+                continue;
+            }
+            let mut inner: Map<K2, MVReg<V, A>, A> = Map::new();
+            inner.clock = row_clock(&o_ic[b * a..(b + 1) * a], &actors);
+            for (jj, ik) in ikeys.ids.iter().enumerate() {
+                let q = b * k2 + jj;
+                let ir = &o_iec[q * a..(q + 1) * a];
+                if ir.iter().any(|&x| x != 0) {
+                    let reg = mvreg_of(&o_ivc[q * 8 * a..(q + 1) * 8 * a], &o_ivv[q * 8..(q + 1) * 8],
+                                       o_nval[q] as usize, &actors, &arena);
+                    inner.entries.insert(ik.clone(), Entry { clock: row_clock(ir, &actors), val: reg });
+                }
+            }
+            for i in 0..o_idn[b] as usize {
+                let ks = bit_keys(&o_idk[b * 16 + i..b * 16 + i + 1], &ikeys);
+                inner.deferred.entry(row_clock(&o_idc[(b * 16 + i) * a..(b * 16 + i + 1) * a], &actors))
+                    .or_insert_with(BTreeSet::new).extend(ks);
+            }
+            mp.entries.insert(key.clone(), Entry { clock: row_clock(row, &actors), val: inner });
+        }
+        mp.deferred = group_survivors(&pool, gi, &keep, &okeys, &actors, &keys);
+        res.push(mp);
+    }
+    Ok(res)
+}
+
+impl<K: Ord + Clone, K2: Ord + Clone, V: Clone, A: Actor> BatchCvRDT for Map<K, Map<K2, MVReg<V, A>, A>, A> {
+    fn lub_many(ctx: &GpuCtx, replicas: Vec<Self>) -> Result<Self, GpuError> {
+        if replicas.is_empty() {
+            return Ok(Map::new());
+        }
+        Ok(nested_map_folds(ctx, &[replicas.iter().collect()])?.remove(0))
+    }
+    fn merge_batch(ctx: &GpuCtx, selves: &mut [Self], others: Vec<Self>) -> Result<(), GpuError> {
+        check_pairs(selves.len(), others.len())?;
+        if selves.is_empty() {
+            return Ok(());
+        }
+        let merged = nested_map_folds(ctx, &pairs_as_groups(selves, &others))?;
+        for (s, m) in selves.iter_mut().zip(merged) {
+            *s = m;
         }
         Ok(())
     }

@@ -65,8 +65,9 @@ def test_ctypes_struct_layout_matches_header():
     assert ctypes.sizeof(abi.MapOrswotOut) == 10 * 8
 
 
-HOST_CAPABLE = {f"crdt_{t}_{op}" for t in ("vclock", "gcounter", "pncounter", "gset", "lwwreg", "orswot", "map")
-                for op in ("lub_many", "merge_batch")}
+HOST_CAPABLE = ({f"crdt_{t}_{op}" for t in ("vclock", "gcounter", "pncounter", "gset", "lwwreg", "orswot", "map")
+                 for op in ("lub_many", "merge_batch")}
+                | {"crdt_map_counter_lub_many", "crdt_map_orswot_lub_many", "crdt_map_nested_lub_many"})
 CTX_ONLY = {"crdt_ctx_destroy", "crdt_ctx_set_stream", "crdt_ctx_synchronize", "crdt_ctx_set_timing",
             "crdt_ctx_timing", "crdt_ctx_timing_reset", "crdt_ctx_tune", "crdt_ctx_set_mem_kind",
             "crdt_ctx_comm_init", "crdt_ctx_comm_destroy", "crdt_ctx_comm_info", "crdt_ctx_mem_kind",

@@ -329,3 +329,65 @@ def test_map_host_merge_batch(hctx):
         deferred = [(me[4][i, j], O.bitmap_members(me[5][i, j])) for j in range(int(me[6][i]))]
         got = O.dense_to_map(me[0][i], me[1][i], me[2][i], me[3][i], deferred)
         assert got == e, i
+
+
+# ---- the value-typed Maps in host mode (round 5: whole-batch staging) -----------------------------
+def _host_deferred(out, dcl):
+    return {(tuple(int(x) for x in dcl[d]), O.bitmap_members(out["def_keys"][d]))
+            for d in np.flatnonzero(out["def_keep"])}
+
+
+@pytest.mark.parametrize("W", [1, 2])
+def test_map_counter_host_lub_many(hctx, W):
+    """crdt_map_counter_lub_many from host arrays equals the oracle's left fold (map.rs:140-220 with
+    the counters' merge / forget); the chunk-skip path (A = 32) and the generic one (A = 5)."""
+    for A, seed in ((32, 3), (5, 4)):
+        maps = O.map_counter_objects(40, 6, A, W, seed=seed, steps=240, p_rm=0.3)
+        exp = O.map_fold_objects(maps)
+        d = O.map_counter_to_dense(maps, 6, A, W)
+        D = d["def_row"].shape[0]
+        out = host.map_counter_lub_many(d["clock"], d["ec"], d["val"], def_off=[0, D] if D else None,
+                                        def_row=d["def_row"], def_clock=d["def_clock"], def_keys=d["def_keys"], ctx=hctx)
+        assert int(out["flags"][0]) == 0
+        dset = _host_deferred(out, d["def_clock"]) if D else set()
+        got = O.dense_to_map_counter(out["clock"][0], out["ec"][0], out["val"][0],
+                                     [(np.array(rm, np.uint64), ks) for rm, ks in dset])
+        assert got == exp
+
+
+def test_map_orswot_host_lub_many(hctx):
+    maps = O.map_orswot_objects(30, 4, 6, 4, seed=5, steps=200, p_vrm=0.5)
+    exp = O.map_fold_objects(maps)
+    d = O.map_orswot_to_dense(maps, 4, 6, 4)
+    D, Dv = d["def_row"].shape[0], d["vd_clock"].shape[0]
+    out = host.map_orswot_lub_many(d["clock"], d["ec"], d["oc"], d["ent"], d["vd_off"],
+                                   d["vd_clock"] if Dv else None, d["vd_members"] if Dv else None,
+                                   def_off=[0, D] if D else None, def_row=d["def_row"], def_clock=d["def_clock"],
+                                   def_keys=d["def_keys"], ctx=hctx)
+    assert int(out["flags"][0]) == 0
+    dset = _host_deferred(out, d["def_clock"]) if D else set()
+    vd = {k: [(out["vd_clock"][0, k, i], O.bitmap_members(out["vd_mem"][0, k, i:i + 1]))
+              for i in range(int(out["vd_n"][0, k]))] for k in range(4)}
+    got = O.dense_to_map_orswot(out["clock"][0], out["ec"][0], out["oc"][0], out["ent"][0], vd,
+                                [(np.array(rm, np.uint64), ks) for rm, ks in dset])
+    assert got == exp
+
+
+def test_map_nested_host_lub_many(hctx):
+    maps = O.nested_map_objects(30, 3, 5, 4, seed=6, steps=240, p_irm=0.5, p_ooo=0.8, p_rm=0.3)
+    exp = O.map_fold_objects(maps)
+    V = max([len(ie.val.vals) for m in maps for e in m.entries.values() for ie in e.val.entries.values()] + [1])
+    d = O.nested_map_to_dense(maps, 3, 5, 4, V)
+    D, Di = d["def_row"].shape[0], d["id_clock"].shape[0]
+    out = host.map_nested_lub_many(d["clock"], d["ec"], d["ic"], d["iec"], d["ivc"], d["ivv"], d["id_off"],
+                                   d["id_clock"] if Di else None, d["id_keys"] if Di else None,
+                                   def_off=[0, D] if D else None, def_row=d["def_row"], def_clock=d["def_clock"],
+                                   def_keys=d["def_keys"], ctx=hctx)
+    assert int(out["flags"][0]) == 0
+    dset = _host_deferred(out, d["def_clock"]) if D else set()
+    idef = {k: [(out["id_clock"][0, k, i], O.bitmap_members(out["id_keys"][0, k, i:i + 1]))
+                for i in range(int(out["id_n"][0, k]))] for k in range(3)}
+    got = O.dense_to_nested_map(out["clock"][0], out["ec"][0], out["ic"][0], out["iec"][0], out["ivc"][0],
+                                out["ivv"][0], out["nval"][0], idef, [(np.array(rm, np.uint64), ks) for rm, ks in dset])
+    from test_gpu_map_nested import canon
+    assert canon(got) == canon(exp)
