@@ -955,16 +955,27 @@ __device__ __forceinline__ u64 rs_reg_noop(const RsChunk<VI, NP> &r, const RsReg
 // neutral, since "c2 <= 0 everywhere" only covers an empty incoming slot, which the "appended, then
 // forgotten" test covers anyway — so the kernel carries two copies of the test, not five (the
 // fast path's code footprint is what sets its speed: the instruction cache is shared by two CUs).
+// MAP_REG_NQ (build option, 2 by default; 3 before round 5): own-value slots the register test compares;
+// 2 drops two compares per element and sends a 3-value state's chunks to the exact loop (config 4:
+// 2.29 -> 2.155 ms by HIP events, profiles/r05_map_nq2_ab.log).
+#ifndef MAP_REG_NQ
+#define MAP_REG_NQ 2
+#endif
+// MAP_BATCH_ONLY (build option, 0 by default): compile only the batched-compare form of the register
+// test (CRDT_TUNE mbatch=0 then has no effect), halving the test's code in the kernel.
+#ifndef MAP_BATCH_ONLY
+#define MAP_BATCH_ONLY 0
+#endif
 template <int VI, int NP, bool BATCH = false, class F = RsNoDma>
 __device__ __forceinline__ u64 rs_reg_noop_nv(const RsChunk<VI, NP> &r, const RsReg<NP> &g, bool present, int nv,
                                               F &&dma = F{}) {
   if (!present) return rs_reg_noop<VI, NP, 0, false, BATCH>(r, g, dma);
-  if (nv > 3) {
+  if (nv > MAP_REG_NQ) {  // (a state holding more values: the exact loop's own test settles the chunk)
 #pragma unroll
     for (int j = 0; j < std::remove_reference_t<F>::count; ++j) dma(j);
     return 0;
   }
-  return rs_reg_noop<VI, NP, 3, true, BATCH>(r, g, dma);
+  return rs_reg_noop<VI, NP, MAP_REG_NQ, true, BATCH>(r, g, dma);
 }
 
 // The next chunk's LDS-DMA pieces as that hook (a whole chunk, every lane moving a piece of every
@@ -1576,7 +1587,7 @@ __global__ __launch_bounds__(SH ? 256 : (LD ? 128 : 64), LD ? 2 : 1) void map_fo
                 p.cmax + (g * p.nch + ch + kShD) * A + 8 * wv + 2 * lane,
                 shr + sh_iss_now * kShShared + 512 + 8 * wv,
                 lane < 4};
-        skip = ((p.batch ? rs_reg_noop_nv<VI, NP, true>(rA, rg, present, nv, d)
+        skip = (((MAP_BATCH_ONLY || p.batch) ? rs_reg_noop_nv<VI, NP, true>(rA, rg, present, nv, d)
                          : rs_reg_noop_nv<VI, NP, false>(rA, rg, present, nv, d)) &
                 want) == want;
       } else if (spread) {
@@ -1585,11 +1596,11 @@ __global__ __launch_bounds__(SH ? 256 : (LD ? 128 : 64), LD ? 2 : 1) void map_fo
                 reinterpret_cast<const unsigned *>(p.vval + g * p.vv_gs + (i2 + (sv < C ? sv : 0)) * p.vv_rs + k * VI) + dw,
                 vsl, sv < C, p.cmax + (g * p.nch + i2 / C) * A + 2 * lane, cms, (unsigned long long)(2 * lane) < A,
                 vpiece, p.diag};
-        skip = ((p.batch ? rs_reg_noop_nv<VI, NP, true>(rA, rg, present, nv, d)
+        skip = (((MAP_BATCH_ONLY || p.batch) ? rs_reg_noop_nv<VI, NP, true>(rA, rg, present, nv, d)
                          : rs_reg_noop_nv<VI, NP, false>(rA, rg, present, nv, d)) &
                 want) == want;
       } else if (el) {
-        skip = ((p.batch ? rs_reg_noop_nv<VI, NP, true>(rA, rg, present, nv)
+        skip = (((MAP_BATCH_ONLY || p.batch) ? rs_reg_noop_nv<VI, NP, true>(rA, rg, present, nv)
                          : rs_reg_noop_nv<VI, NP, false>(rA, rg, present, nv)) &
                 want) == want;
       }

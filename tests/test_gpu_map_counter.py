@@ -17,12 +17,13 @@ pytestmark = pytest.mark.gpu
 import crdts_gpu as cg  # noqa: E402
 
 
-@pytest.fixture(params=["mckpw=0", "mckpw=1", "mckpw=2", "mckpw=4", "mcdma=8", "mcdma=16"])
+@pytest.fixture(params=["mckpw=0", "mckpw=1", "mckpw=2", "mckpw=4", "mcdma=8", "mcdma=16", "mccs=0"])
 def mcctx(request):
-    """The register ring with keys per wave chosen by the grid size (mckpw=0, the default), 1, up to 2
-    or up to 4 keys per wave (A <= 64 / keys), or
-    the replica rows by LDS-DMA into an 8- or 16-slot LDS ring (A even, (2+W)*A <= 128; one key
-    per wave).  Shapes outside a mode's bound take the one-key register ring."""
+    """The default (A = 32 / 16 / 8: the whole-chunk skip, round 5; otherwise the register ring with
+    keys per wave chosen by the grid size), 1, up to 2 or up to 4 keys per wave (A <= 64 / keys), the
+    replica rows by LDS-DMA into an 8- or 16-slot LDS ring (A even, (2+W)*A <= 128; one key per
+    wave), or the register ring without the chunk skip (mccs=0).  Shapes outside a mode's bound take
+    the one-key register ring."""
     assert torch.cuda.is_available()
     torch.cuda.set_device(0)
     ctx = cg.Context(0)
@@ -219,4 +220,52 @@ def test_map_counter_auto_keys_per_wave_keeps_per_key_capacity(gpu_ctx, W):
     d = O.map_counter_to_dense(maps, K, A, W)
     res, kw = _run(gpu_ctx, d)  # the default ctx: mckpw=0 (automatic)
     assert int(res.flags.cpu()[0]) == 0
+    _same(_got_maps(res, kw, 1)[0], exp)
+
+
+@pytest.mark.parametrize("W", [1, 2])
+@pytest.mark.parametrize("A,seed", [(32, 21), (16, 22), (8, 23)])
+def test_map_counter_chunk_skip_op_replay(mcctx, W, A, seed):
+    """The whole-chunk skip's shapes (A = 32 / 16 / 8) over long op-replay folds: 16-replica chunks
+    with and without removes naming the key, skipped and exact chunks, a partial last chunk."""
+    R, K = 150, 6
+    maps = O.map_counter_objects(R, K, A, W, seed=seed, steps=5 * R, p_rm=0.25)
+    exp = O.map_fold_objects(maps)
+    d = O.map_counter_to_dense(maps, K, A, W)
+    res, kw = _run(mcctx, d)
+    assert int(res.flags.cpu()[0]) == 0
+    _same(_got_maps(res, kw, 1)[0], exp)
+
+
+@pytest.mark.parametrize("W", [1, 2])
+@pytest.mark.parametrize("A,R,cmax,seed", [(32, 64, 3, 31), (16, 80, 2, 32), (8, 96, 4, 33), (32, 48, 1, 34)])
+def test_map_counter_chunk_skip_arbitrary(mcctx, W, A, R, cmax, seed):
+    """Arbitrary dense states with small counters (equal words, zeros, stale values behind empty
+    clocks) at the chunk-skip shapes: whatever the test decides, the result is the exact left fold."""
+    rng = np.random.default_rng(seed)
+    maps = _arbitrary(rng, R, 3, A, W, cmax, 1)
+    exp = O.map_fold_objects(maps)
+    d = O.map_counter_to_dense(maps, 3, A, W)
+    res, kw = _run(mcctx, d)
+    _same(_got_maps(res, kw, 1)[0], exp)
+
+
+@pytest.mark.parametrize("W", [1, 2])
+def test_map_counter_chunk_skip_steady_state(mcctx, W):
+    """Replicas that repeat one key's state (every chunk after the first skippable), then a late
+    change and a late remove: the skipped chunks only merge their clocks."""
+    A, K, R = 32, 2, 200
+    base = O.map_counter_objects(12, K, A, W, seed=41, steps=120, p_rm=0.0)
+    fold = O.map_fold_objects(base)
+    maps = [fold.copy() for _ in range(R)]
+    for r in range(R):
+        maps[r].clock = fold.clock.copy()
+        maps[r].clock.apply(O.Dot(r % A, fold.clock.get(r % A) + 1 + r // A))  # clocks keep growing
+    late = O.map_counter_objects(4, K, A, W, seed=42, steps=80, p_rm=0.4)
+    maps[150] = late[-1]
+    if late[-2].deferred:
+        maps[170] = late[-2]
+    exp = O.map_fold_objects(maps)
+    d = O.map_counter_to_dense(maps, K, A, W)
+    res, kw = _run(mcctx, d)
     _same(_got_maps(res, kw, 1)[0], exp)
