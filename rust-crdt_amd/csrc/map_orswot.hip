@@ -50,7 +50,9 @@ __device__ __forceinline__ bool mo_nz(u64 x) { return __ballot(x != 0) != 0; }
 __device__ __forceinline__ u64 mo_fg(u64 x, u64 c) { return x > c ? x : 0; }  // VClock::forget, per actor
 __device__ __forceinline__ u64 mo_max(u64 x, u64 y) { return x > y ? x : y; }
 
-template <int MT>
+// SPL > 0 (A == 64 / SPL: 32, 16 or 8 actors): the whole-chunk skip below, lane l holding actor
+// l % A in every register of the key's state.
+template <int MT, int SPL = 0>
 __global__ __launch_bounds__(kMoWaves * kWave) void map_orswot_fold_kernel(MapOrswotPlan p) {
   constexpr int DEPTH = MT <= 4 ? 8 : (MT <= 8 ? 4 : 2);  // replica steps in flight (register ring)
   extern __shared__ u64 lds[];
@@ -64,7 +66,8 @@ __global__ __launch_bounds__(kMoWaves * kWave) void map_orswot_fold_kernel(MapOr
   u64 *rows = lst + kMoList + kMoLive / 2;  // [kMoRows][64] live Map-remove rows
   u64 *vrow = rows + kMoRows * kWave;       // [kMoVd][64] nested deferred rm rows
   u64 *vmsk = vrow + kMoVd * kWave;         // [kMoVd] their member masks
-  const unsigned la = (unsigned)((unsigned long long)lane < A ? lane : A - 1);  // the lane's actor
+  const unsigned la = SPL > 0 ? (unsigned)lane & (unsigned)(kWave / (SPL > 0 ? SPL : 1) - 1)  // the lane's actor
+                              : (unsigned)((unsigned long long)lane < A ? lane : A - 1);
   auto ld = [&](const u64 *row) { return row[la]; };
 
   // ---- the Map's removes naming key k, in replica order (map_counter.hip's walk, one key)
@@ -127,6 +130,10 @@ __global__ __launch_bounds__(kMoWaves * kWave) void map_orswot_fold_kernel(MapOr
 #pragma unroll
   for (int m = 0; m < MT; ++m) E[m] = 0;
   int nd = 0;  // nested deferred removes in vrow / vmsk (uniform)
+  // the member rows are forgotten by every held nested remove (true after a both-present merge, which
+  // re-applies them all, and kept by forgets; false after the replica's Orswot was taken as it came,
+  // whose own removes need not have been applied to its rows): a precondition of the chunk skip
+  bool vnorm = true;
 
   // nested deferred helpers (LDS rows, uniform control flow)
   auto forget_members = [&](u64 rm, u64 msk) {  // Orswot::apply_rm's member forget (orswot.rs:231-238)
@@ -188,6 +195,36 @@ __global__ __launch_bounds__(kMoWaves * kWave) void map_orswot_fold_kernel(MapOr
     nd = o;
   };
 
+  // the Map-level live set re-test (witness thresholds; chg: removes joined the live set)
+  auto liveness = [&](bool chg) {
+    if (na > 0 && (chg || __ballot(C >= T))) {
+      bool changed = chg;
+      T = ~0ull;
+      for (int i = 0; i < na;) {
+        const u64 rm = live_row(i);
+        const u64 m = __ballot(rm > C);
+        if (m) {
+          const int wl = __builtin_ctzll(m);
+          T = lane == wl && rm < T ? rm : T;
+          ++i;
+          continue;
+        }
+        changed = true;
+        const int lastp = na - 1;
+        if (i != lastp) {
+          put_row(i, live_row(lastp));
+          const unsigned li_last = live[lastp];
+          if (lane == 0) live[i] = li_last;
+        }
+        --na;
+      }
+      if (changed) {
+        rk = 0;
+        for (int i = 0; i < na; ++i) rk = mo_max(rk, live_row(i));
+      }
+    }
+  };
+
   // one replica step
   auto step = [&](unsigned long long r, u64 c2, u64 e2, u64 o2, const u64 (&E2)[MT], u64 vlo, u64 vhi) {
     const bool p1 = mo_nz(e), p2 = mo_nz(e2);
@@ -214,6 +251,7 @@ __global__ __launch_bounds__(kMoWaves * kWave) void map_orswot_fold_kernel(MapOr
       oc = mo_max(oc, o2);
       for (int i = 0; i < nd; ++i) forget_members(vrow[(unsigned long long)i * kWave + lane], vmsk[i]);
       vd_keep_live();
+      vnorm = true;
     } else if (p2 && !p1 && stays) {  // the replica's entry (map.rs:193-208)
 #pragma unroll
       for (int m = 0; m < MT; ++m) E[m] = E2[m];
@@ -223,6 +261,7 @@ __global__ __launch_bounds__(kMoWaves * kWave) void map_orswot_fold_kernel(MapOr
         const u64 rm = ld(p.vd_clock + d * A), msk = p.vd_mem[d];
         vd_add(rm, msk);
       }
+      vnorm = nd == 0;
     }
     if (stays && (p1 || p2)) value_forget(X);
     e = en;
@@ -252,34 +291,159 @@ __global__ __launch_bounds__(kMoWaves * kWave) void map_orswot_fold_kernel(MapOr
       if (mo_nz(e)) value_forget(f);  // entry.val.forget only while the entry stays (map.rs:321-330)
     }
     C = mo_max(C, c2);
-    if (na > 0 && (chg || __ballot(C >= T))) {  // live set re-test (witness thresholds)
-      bool changed = chg;
-      T = ~0ull;
-      for (int i = 0; i < na;) {
-        const u64 rm = live_row(i);
-        const u64 m = __ballot(rm > C);
-        if (m) {
-          const int wl = __builtin_ctzll(m);
-          T = lane == wl && rm < T ? rm : T;
-          ++i;
-          continue;
-        }
-        changed = true;
-        const int lastp = na - 1;
-        if (i != lastp) {
-          put_row(i, live_row(lastp));
-          const unsigned li_last = live[lastp];
-          if (lane == 0) live[i] = li_last;
-        }
-        --na;
-      }
-      if (changed) {
-        rk = 0;
-        for (int i = 0; i < na; ++i) rk = mo_max(rk, live_row(i));
-      }
-    }
+    liveness(chg);
   };
 
+  if constexpr (SPL > 0) {
+    // ---- whole-chunk skip (round 5), the counter Map's (map_counter.hip) with the nested Orswot:
+    // chunks of S = 8 steps in the transposed layout (lane (hh, a): actor a of step i*SPL + hh),
+    // tested against the state at the chunk's start; a chunk all of whose steps leave (entry clock,
+    // Orswot clock, member dots, nested deferred removes) unchanged only merges its clocks.  With
+    // the acc holding the key (p1), per word, besides the entry tests of map_counter.hip:
+    //   the replica holds it too (p2):  o2 <= oc (the Orswot clock does not grow), and for every
+    //     member E2 == E || (E2 <= oc && o2 <= TE_m), TE_m = E ? E-1 : MAX (the dot-survival join
+    //     keeps E: forget(E2, oc) is empty and forget(E, o2) is E), no nested removes in the step,
+    //     and e2 <= TX, TX = min over oc, every E and every held nested rm word v of
+    //     (v ? max(e, v-1) : MAX) (the value forget by x = e2 > e ? e2 : 0 keeps every word);
+    //   only the acc holds it:  c2 <= min(TE, TX) (entry and value survive forget by c2);
+    //   no p1:  e2 <= C0.
+    // The held nested removes and the Map's live removes were applied when they joined (forgets
+    // are idempotent), so an unchanged state stays unchanged under their re-application.
+    constexpr int S = 8, NE = S / SPL, NB = 3;
+    constexpr unsigned long long AA = kWave / SPL;  // == A
+    const int hh = lane / (int)AA;
+    const unsigned a = (unsigned)lane & (unsigned)(AA - 1);
+    const unsigned long long rsK = K * AA, rsM = K * M * AA;
+    const u64 *bc = p.clock + g * R * AA + a, *be = p.ec + (g * R * K + k) * AA + a,
+              *bo = p.oc + (g * R * K + k) * AA + a, *bm = p.ent + (g * R * K + k) * M * AA + a;
+    const u64 *pvo0 = p.vd_off + g * R * K + k;
+    const unsigned long long nch = (R + S - 1) / S;
+    u64 qc[NB][NE], qe[NB][NE], qo[NB][NE], qm[NB][MT][NE], qlo[NB], qhi[NB];
+    auto load_chunk = [&](auto B, unsigned long long c) {
+      constexpr int b = decltype(B)::value;
+      const unsigned long long r0 = c * S;
+#pragma unroll
+      for (int i = 0; i < NE; ++i) {
+        unsigned long long rr = r0 + (unsigned long long)(i * SPL + hh);
+        rr = rr < R ? rr : R - 1;  // (past the last replica: its row again, never used)
+        qc[b][i] = bc[rr * AA];
+        qe[b][i] = be[rr * rsK];
+        qo[b][i] = bo[rr * rsK];
+#pragma unroll
+        for (int m = 0; m < MT; ++m) qm[b][m][i] = (unsigned long long)m < M ? bm[rr * rsM + m * AA] : 0ull;
+      }
+      unsigned long long rs = r0 + (unsigned long long)(lane < S ? lane : 0);
+      rs = rs < R ? rs : R - 1;
+      qlo[b] = lane < S ? pvo0[rs * K] : 0ull;  // lane s < S: step r0 + s's nested remove range
+      qhi[b] = lane < S ? pvo0[rs * K + 1] : 0ull;
+    };
+    auto test_chunk = [&](auto B) -> bool {
+      constexpr int b = decltype(B)::value;
+      if (__ballot(qhi[b] != qlo[b])) return false;  // a step carries nested removes: exact
+      // the held nested removes must already be applied to the rows and live (!(rm <= oc)): a
+      // both-present step re-applies them and re-tests their liveness
+      if (!vnorm) return false;
+      for (int i = 0; i < nd; ++i)
+        if (!__ballot(vrow[(unsigned long long)i * kWave + lane] > oc)) return false;
+      const u64 e0 = e, C0 = C;
+      if (!mo_nz(e0)) {  // the acc lacks the key: no replica of the chunk may add it
+        u64 okm = ~0ull;
+#pragma unroll
+        for (int i = 0; i < NE; ++i) okm &= __ballot(qe[b][i] <= C0);
+        return okm == ~0ull;
+      }
+      const u64 em1 = e0 ? e0 - 1 : 0;
+      const u64 TE = e0 ? em1 : ~0ull, TB = C0 > em1 ? C0 : em1;
+      auto tv = [&](u64 v) -> u64 { return v == 0 ? ~0ull : (e0 > v - 1 ? e0 : v - 1); };
+      u64 TX = tv(oc), TEm[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        const u64 t = tv(E[m]);
+        TX = t < TX ? t : TX;
+        TEm[m] = E[m] ? E[m] - 1 : ~0ull;
+      }
+      for (int i = 0; i < nd; ++i) {
+        const u64 t = tv(vrow[(unsigned long long)i * kWave + lane]);
+        TX = t < TX ? t : TX;
+      }
+      const u64 TN = TE < TX ? TE : TX;
+      u64 fail = 0;
+#pragma unroll
+      for (int i = 0; i < NE; ++i) {
+        const u64 e2 = qe[b][i], c2 = qc[b][i], o2 = qo[b][i];
+        bool cb = (e2 == e0 || (c2 <= TE && e2 <= TB)) && e2 <= TX && o2 <= oc;
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+          const u64 E2 = qm[b][m][i];
+          cb = cb && (E2 == E[m] || (E2 <= oc && o2 <= TEm[m]));
+        }
+        const u64 mN = __ballot(e2 != 0), mB = __ballot(cb), mO = __ballot(c2 <= TN);
+#pragma unroll
+        for (int s2 = 0; s2 < SPL; ++s2) {
+          const u64 Mk = (AA == 64 ? ~0ull : ((1ull << AA) - 1)) << (s2 * AA);
+          const u64 sel = (mN & Mk) ? mB : mO;
+          fail |= ~sel & Mk;
+        }
+      }
+      return fail == 0;
+    };
+    auto body = [&](auto B, unsigned long long c) {
+      constexpr int b = decltype(B)::value;
+      if (c >= nch) return;
+      if (c + NB - 1 < nch) load_chunk(std::integral_constant<int, (b + NB - 1) % NB>{}, c + NB - 1);
+      const unsigned long long r0 = c * S;
+      const unsigned long long n = R - r0 < (unsigned long long)S ? R - r0 : S;
+      const bool skip = n == S && (unsigned long long)nxt >= r0 + S && test_chunk(B);
+      if (skip) {
+        u64 cm = 0;
+#pragma unroll
+        for (int i = 0; i < NE; ++i) cm = qc[b][i] > cm ? qc[b][i] : cm;
+#pragma unroll
+        for (int off = (int)AA; off < kWave; off <<= 1) {
+          const u64 o = __shfl_xor(cm, off);
+          cm = o > cm ? o : cm;
+        }
+        C = C > cm ? C : cm;
+        liveness(false);
+        return;
+      }
+      for (int s2 = 0; s2 < (int)n; ++s2) {  // the chunk's steps, exactly (rows moved into lane = actor)
+        const int i = s2 / SPL, src = (s2 % SPL) * (int)AA + (int)a;
+        u64 c2 = 0, e2 = 0, o2 = 0, E2[MT];
+#pragma unroll
+        for (int m = 0; m < MT; ++m) E2[m] = 0;
+#pragma unroll
+        for (int ii = 0; ii < NE; ++ii) {
+          if (ii == i) {
+            c2 = qc[b][ii];
+            e2 = qe[b][ii];
+            o2 = qo[b][ii];
+#pragma unroll
+            for (int m = 0; m < MT; ++m) E2[m] = qm[b][m][ii];
+          }
+        }
+        c2 = __shfl(c2, src);
+        e2 = __shfl(e2, src);
+        o2 = __shfl(o2, src);
+#pragma unroll
+        for (int m = 0; m < MT; ++m) E2[m] = __shfl(E2[m], src);
+        const u64 lo = __shfl(qlo[b], s2), hi0 = __shfl(qhi[b], s2);
+        const u64 vlo = __builtin_amdgcn_readfirstlane((unsigned)lo) |
+                        ((u64)__builtin_amdgcn_readfirstlane((unsigned)(lo >> 32)) << 32);
+        u64 vhi = __builtin_amdgcn_readfirstlane((unsigned)hi0) |
+                  ((u64)__builtin_amdgcn_readfirstlane((unsigned)(hi0 >> 32)) << 32);
+        vhi = vhi < p.Dv ? vhi : p.Dv;  // (a malformed vd_off never reads past the rows: flags bit 5)
+        step(r0 + s2, c2, e2, o2, E2, vlo < vhi ? vlo : vhi, vhi);
+      }
+    };
+    load_chunk(std::integral_constant<int, 0>{}, 0);
+    if (nch > 1) load_chunk(std::integral_constant<int, 1>{}, 1);
+    for (unsigned long long c = 0; c < nch; c += NB) {
+      body(std::integral_constant<int, 0>{}, c);
+      body(std::integral_constant<int, 1>{}, c + 1);
+      body(std::integral_constant<int, 2>{}, c + 2);
+    }
+  } else {
   // ---- replica rows through a register ring (DEPTH steps ahead; clamped past the last replica)
   const u64 *pc = p.clock + g * R * A, *pe = p.ec + (g * R * K + k) * A, *po = p.oc + (g * R * K + k) * A;
   const u64 *pm = p.ent + (g * R * K + k) * M * A;
@@ -328,6 +492,7 @@ __global__ __launch_bounds__(kMoWaves * kWave) void map_orswot_fold_kernel(MapOr
       run(r0 + s, s, true);
     }
   }
+  }  // (register ring)
 
   // ---- the key's folded entry (an empty entry clock: absent, value rows 0), the group's clock
   const bool pf = mo_nz(e);
@@ -373,10 +538,10 @@ static size_t mo_lds() {
   return (size_t)kMoWaves * (kMoList * 8 + kMoLive * 4 + kMoRows * kWave * 8 + kMoVd * kWave * 8 + kMoVd * 8);
 }
 
-template <int MT>
+template <int MT, int SPL = 0>
 static hipError_t launch_mo(const MapOrswotPlan &p, hipStream_t s) {
   const unsigned long long blocks = (p.G * p.K + kMoWaves - 1) / kMoWaves;
-  hipLaunchKernelGGL(map_orswot_fold_kernel<MT>, dim3((unsigned)blocks), dim3(kMoWaves * kWave), mo_lds(), s, p);
+  hipLaunchKernelGGL((map_orswot_fold_kernel<MT, SPL>), dim3((unsigned)blocks), dim3(kMoWaves * kWave), mo_lds(), s, p);
   return hipGetLastError();
 }
 
@@ -439,9 +604,14 @@ extern "C" int crdt_map_orswot_lub_many(crdt_ctx *ctx, const crdt_map_orswot_bat
     }
     timing_begin(ctx, "map_orswot_fold");
     // (member rows past M are zero and still joined: the register capacity follows M)
-    const hipError_t he = M <= 4   ? launch_mo<4>(p, ctx->stream)
-                          : M <= 8 ? launch_mo<8>(p, ctx->stream)
-                                   : launch_mo<32>(p, ctx->stream);
+    // the whole-chunk skip (round 5) for A = 32 / 16 / 8 and up to 4 members (CRDT_TUNE mocs=0: off)
+    const int spl = ctx->tune.map_orswot_cs && M <= 4 ? (A == 32 ? 2 : (A == 16 ? 4 : (A == 8 ? 8 : 0))) : 0;
+    const hipError_t he = spl == 2   ? launch_mo<4, 2>(p, ctx->stream)
+                          : spl == 4 ? launch_mo<4, 4>(p, ctx->stream)
+                          : spl == 8 ? launch_mo<4, 8>(p, ctx->stream)
+                          : M <= 4   ? launch_mo<4>(p, ctx->stream)
+                          : M <= 8   ? launch_mo<8>(p, ctx->stream)
+                                     : launch_mo<32>(p, ctx->stream);
     timing_end(ctx);
     if (he != hipSuccess) return hip_fail(ctx, he, "map_orswot_fold_kernel launch");
   }

@@ -270,3 +270,62 @@ def test_map_orswot_dominated_nested_removes_not_held(gpu_ctx):
     res, kw = _run(gpu_ctx, d)
     assert int(res.flags.cpu()[0]) == 0
     _same(_got_maps(res, kw, 1)[0], exp)
+
+
+@pytest.fixture(params=["", "mocs=0"])
+def moctx(request):
+    """The default (A = 32 / 16 / 8 with up to 4 members: the whole-chunk skip, round 5) and the
+    register ring alone (mocs=0)."""
+    torch.cuda.set_device(0)
+    ctx = cg.Context(0)
+    if request.param:
+        ctx.tune(request.param)
+    yield ctx
+    ctx.close()
+
+
+@pytest.mark.parametrize("seed,R,K,M,A", [(41, 120, 3, 4, 32), (42, 150, 4, 3, 16), (43, 100, 3, 4, 8),
+                                           (44, 90, 2, 2, 32)])
+def test_map_orswot_chunk_skip_op_replay(moctx, seed, R, K, M, A):
+    """The chunk-skip shapes over long op-replay folds: nested removes inside chunks (exact), chunks
+    skipped in between, a partial last chunk."""
+    maps = O.map_orswot_objects(R, K, M, A, seed=seed, steps=6 * R, p_vrm=0.4)
+    exp = O.map_fold_objects(maps)
+    d = O.map_orswot_to_dense(maps, K, M, A)
+    res, kw = _run(moctx, d)
+    assert int(res.flags.cpu()[0]) == 0
+    _same(_got_maps(res, kw, 1)[0], exp)
+
+
+@pytest.mark.parametrize("seed,R,A,cmax", [(51, 64, 16, 3), (52, 48, 32, 2), (53, 80, 8, 4)])
+def test_map_orswot_chunk_skip_arbitrary(moctx, seed, R, A, cmax):
+    """Arbitrary states (nested removes never applied to their rows, entry dots above clocks) at the
+    chunk-skip shapes: a replica's Orswot taken as it comes leaves the state un-normalized, which the
+    skip must not assume."""
+    rng = np.random.default_rng(seed)
+    maps = _arbitrary(rng, R, 3, 4, A, cmax)
+    exp = O.map_fold_objects(maps)
+    if any(len(e.val.deferred) > cg.map.VD_CAP for e in exp.entries.values()):
+        pytest.skip("nested deferred past the kernel's capacity")
+    d = O.map_orswot_to_dense(maps, 3, 4, A)
+    res, kw = _run(moctx, d)
+    _same(_got_maps(res, kw, 1)[0], exp)
+
+
+def test_map_orswot_chunk_skip_steady_state(moctx):
+    """Replicas repeating one folded state with growing clocks (every chunk skippable), then a late
+    replica with new dots: the skipped chunks merge only their clocks."""
+    A, K, M, R = 32, 2, 4, 160
+    base = O.map_orswot_objects(10, K, M, A, seed=61, steps=100, p_vrm=0.3)
+    fold = O.map_fold_objects(base)
+    maps = []
+    for r in range(R):
+        m = fold.copy()
+        m.clock.apply(O.Dot(r % A, fold.clock.get(r % A) + 1 + r // A))
+        maps.append(m)
+    late = O.map_orswot_objects(4, K, M, A, seed=62, steps=60, p_vrm=0.5)
+    maps[130] = late[-1]
+    exp = O.map_fold_objects(maps)
+    d = O.map_orswot_to_dense(maps, K, M, A)
+    res, kw = _run(moctx, d)
+    _same(_got_maps(res, kw, 1)[0], exp)

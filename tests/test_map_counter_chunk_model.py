@@ -103,3 +103,98 @@ def test_chunk_test_skips_the_config4_generator(W):
         ch_changed = changed.reshape(-1, 16).any(1)
         assert not (ch_pass & ch_changed).any()
         assert (~ch_pass).sum() <= ch_changed.sum() + 2, ((~ch_pass).sum(), ch_changed.sum())
+
+
+# ---- Map<K, Orswot<M>> (csrc/map_orswot.hip, SPL > 0) ------------------------------------------------
+def orswot_exact_step(C, e, oc, E, D, c2, e2, o2, E2):
+    """One step of the Map<K, Orswot> fold without removes in the step (the chunk test's scope): the
+    entry join, Orswot::merge (dot-survival join, held removes re-applied, oc |= o2, live re-test;
+    orswot.rs:81-149) when both hold the key, the replica's Orswot when only it does, then the value
+    forget by the case's clock (Causal::forget, orswot.rs:150-183).  Single state; D: list of
+    (rm row, member mask).  Returns (e', oc', E', D')."""
+    p1, p2 = e.any(), e2.any()
+    en = np.where(e == e2, e, np.maximum(fg(e2, C), fg(e, c2)))
+    if not en.any():
+        return en, oc, E, D
+    y = (np.maximum(e, e2) if p2 else c2) if p1 else C
+    X = fg(y, en)
+    if p1 and p2:
+        E = np.where(E == E2, E, np.maximum(fg(E2, oc[None]), fg(E, o2[None])))
+        for rm, msk in D:
+            for m in range(E.shape[0]):
+                if (msk >> m) & 1:
+                    E[m] = fg(E[m], rm)
+        oc = np.maximum(oc, o2)
+        D = [(rm, msk) for rm, msk in D if (rm > oc).any()]
+    elif p2:
+        E, oc, D = E2.copy(), o2.copy(), []
+    if X.any():  # Orswot::forget
+        oc = fg(oc, X)
+        E = fg(E, X[None])
+        out = []
+        for rm, msk in D:
+            r2 = fg(rm, X)
+            if not r2.any():
+                continue
+            hit = [i for i, (x, _) in enumerate(out) if np.array_equal(x, r2)]
+            if hit:
+                out[hit[0]] = (r2, msk)
+            else:
+                out.append((r2, msk))
+        D = out
+    return en, oc, E, D
+
+
+def orswot_chunk_test(C0, e, oc, E, D, c2, e2, o2, E2):
+    """map_orswot.hip test_chunk's per-step verdict (the state normalized: held removes applied)."""
+    if any(not (rm > oc).any() for rm, _ in D):
+        return False
+    if not e.any():
+        return bool((e2 <= C0).all())
+    em1 = np.where(e > 0, e - ONE, Z)
+    TE = np.where(e > 0, em1, MAXU)
+    TB = np.maximum(C0, em1)
+    tv = lambda v: np.where(v == 0, MAXU, np.maximum(e, np.where(v > 0, v - ONE, Z)))  # noqa: E731
+    TX = tv(oc)
+    for m in range(E.shape[0]):
+        TX = np.minimum(TX, tv(E[m]))
+    for rm, _ in D:
+        TX = np.minimum(TX, tv(rm))
+    if e2.any():
+        TEm = np.where(E > 0, E - ONE, MAXU)
+        cb = ((e2 == e) | ((c2 <= TE) & (e2 <= TB))) & (e2 <= TX) & (o2 <= oc)
+        cb &= ((E2 == E) | ((E2 <= oc[None]) & (o2[None] <= TEm))).all(0)
+        return bool(cb.all())
+    return bool((c2 <= np.minimum(TE, TX)).all())
+
+
+@pytest.mark.parametrize("cmax,seed", [(2, 5), (3, 6), (5, 7)])
+def test_orswot_chunk_test_is_sound_on_random_states(cmax, seed):
+    rng = np.random.default_rng(seed)
+    A, MT = 3, 3
+    n_pass = 0
+    for _ in range(30000):
+        r = lambda p=0.6, shape=(A,): (rng.integers(0, cmax + 1, size=shape) * (rng.random(shape) < p)).astype(np.uint64)  # noqa: E731
+        C0, e, oc, c2, e2, o2 = r(0.9), r(), r(0.8), r(0.9), r(), r(0.8)
+        E, E2 = r(0.5, (MT, A)), r(0.5, (MT, A))
+        D = []
+        for _ in range(int(rng.integers(0, 3))):
+            rm = r(0.5)
+            if rm.any() and not any(np.array_equal(rm, x) for x, _ in D):  # (held clocks are distinct)
+                D.append((rm, int(rng.integers(1, 1 << MT))))
+        # the kernel's precondition: the held removes are applied to the rows
+        for rm, msk in D:
+            for m in range(MT):
+                if (msk >> m) & 1:
+                    E[m] = fg(E[m], rm)
+        C = np.maximum(C0, r(0.3))
+        ok = orswot_chunk_test(C0, e, oc, E, D, c2, e2, o2, E2)
+        if not ok:
+            continue
+        n_pass += 1
+        en, oc2, En, Dn = orswot_exact_step(C, e, oc.copy(), E.copy(), list(D), c2, e2, o2, E2)
+        assert np.array_equal(en, e)
+        if e.any():
+            assert np.array_equal(oc2, oc) and np.array_equal(En, E)
+            assert len(Dn) == len(D) and all(np.array_equal(a[0], b[0]) and a[1] == b[1] for a, b in zip(Dn, D))
+    assert n_pass > 1000
