@@ -79,6 +79,10 @@ struct OrPlan {
 // MPT member rows per thread (CRDT_TUNE ompt=4/8/16): a workgroup covers MB*MPT member rows of
 // PW actor vectors, so MPT sets the bytes in flight per thread and how many workgroups re-read
 // each replica clock row.
+// OR_VIOL_BALLOT (build option): the main loop's e > c votes as ballots or-ed on the scalar unit
+#ifndef OR_VIOL_BALLOT
+#define OR_VIOL_BALLOT 0
+#endif
 template <int V, int UR, int MPT>
 __global__ __launch_bounds__(kBlock) void orswot_join_kernel(OrPlan p) {
   constexpr int kOrMPT = MPT;
@@ -103,6 +107,9 @@ __global__ __launch_bounds__(kBlock) void orswot_join_kernel(OrPlan p) {
 #pragma unroll
   for (int j = 0; j < kOrMPT; ++j) mok[j] = active && (mbase + (size_t)j * p.MB) < p.M;
   bool viol = false;
+#if OR_VIOL_BALLOT
+  u64 vmask = 0;  // (the violation votes collected on the scalar unit: one compare + one SALU or)
+#endif
   auto gt = [](VT x, VT y) -> bool {
     if constexpr (V == 2) return (x.x > y.x) | (x.y > y.y);
     else return x > y;
@@ -146,7 +153,12 @@ __global__ __launch_bounds__(kBlock) void orswot_join_kernel(OrPlan p) {
       for (int q = 0; q < UR; ++q) {
 #pragma unroll
         for (int j = 0; j < kOrMPT; ++j) {
+#if OR_VIOL_BALLOT
+          if constexpr (V == 2) vmask |= __ballot(e2[q][j].x > c2[q].x) | __ballot(e2[q][j].y > c2[q].y);
+          else vmask |= __ballot(e2[q][j] > c2[q]);
+#else
           viol |= gt(e2[q][j], c2[q]);
+#endif
           e[j] = dot_join(e[j], c, e2[q][j], c2[q]);
         }
         c = umax(c, c2[q]);
@@ -176,6 +188,9 @@ __global__ __launch_bounds__(kBlock) void orswot_join_kernel(OrPlan p) {
     const unsigned long long rbeg = (unsigned long long)s * p.Rs;
     fold(rbeg, min(p.R, rbeg + p.Rs));
   }
+#if OR_VIOL_BALLOT
+  viol |= vmask != 0;
+#endif
 
   const size_t slab = (size_t)p.MB * kOrMPT * p.PW + p.PW;  // vectors
   auto store_final = [&](void) {
@@ -220,6 +235,9 @@ __global__ __launch_bounds__(kBlock) void orswot_join_kernel(OrPlan p) {
   if (s_flag & 2) {  // some input cell of the unit had e > c: the exact in-order re-fold
     start(true);
     if (active) fold(0, p.R);
+#if OR_VIOL_BALLOT
+    viol |= vmask != 0;
+#endif
   } else if (active) {
     c = VT(0);
 #pragma unroll
