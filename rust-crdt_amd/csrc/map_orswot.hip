@@ -32,6 +32,8 @@ constexpr int kMoList = 256;  // Map removes naming the key, gathered per window
 constexpr int kMoLive = 256;  // live Map removes per key
 constexpr int kMoRows = 8;    // live Map-remove rows cached in LDS
 constexpr int kMoVd = 16;     // nested deferred removes per key state (flags bit 4 past it)
+constexpr unsigned long long kMoRingSpan = 2048;  // chunk-skip mode: register-ring steps run after a
+                                                  // window of chunks that rarely skipped (multiple of 8)
 
 struct MapOrswotPlan {
   const u64 *clock, *ec, *oc, *ent;   // (G,R,A), (G,R,K,A), (G,R,K,A), (G,R,K,M,A)
@@ -54,7 +56,11 @@ __device__ __forceinline__ u64 mo_max(u64 x, u64 y) { return x > y ? x : y; }
 // l % A in every register of the key's state.
 template <int MT, int SPL = 0>
 __global__ __launch_bounds__(kMoWaves * kWave) void map_orswot_fold_kernel(MapOrswotPlan p) {
-  constexpr int DEPTH = MT <= 4 ? 8 : (MT <= 8 ? 4 : 2);  // replica steps in flight (register ring)
+#ifndef MO_RING_DEPTH4
+#define MO_RING_DEPTH4 8
+#endif
+  // replica steps in flight (register ring); the chunk-skip mode's ring phase runs half as deep
+  constexpr int DEPTH = SPL > 0 ? (MT <= 4 ? 4 : 2) : (MT <= 4 ? MO_RING_DEPTH4 : (MT <= 8 ? 4 : 2));
   extern __shared__ u64 lds[];
   const int lane = (int)(threadIdx.x % kWave), wv = (int)(threadIdx.x / kWave);
   const unsigned long long gk = (unsigned long long)blockIdx.x * kMoWaves + wv;
@@ -294,6 +300,58 @@ __global__ __launch_bounds__(kMoWaves * kWave) void map_orswot_fold_kernel(MapOr
     liveness(chg);
   };
 
+  // ---- replica rows [rs, re) through a register ring (DEPTH steps ahead; clamped at row re - 1)
+  auto ring_phase = [&](unsigned long long rs, unsigned long long re) {
+    const u64 *pc = p.clock + (g * R + rs) * A, *pe = p.ec + ((g * R + rs) * K + k) * A,
+              *po = p.oc + ((g * R + rs) * K + k) * A;
+    const u64 *pm = p.ent + ((g * R + rs) * K + k) * M * A;
+    const u64 *pvo = p.vd_off + (g * R + rs) * K + k;
+    const unsigned long long rsK = K * A, rsM = K * M * A;
+    u64 c2r[DEPTH], e2r[DEPTH], o2r[DEPTH], E2r[DEPTH][MT], vlr[DEPTH], vhr[DEPTH];
+    unsigned long long nload = rs;
+    auto load_step = [&](int s, bool last_check) {
+      c2r[s] = ld(pc);
+      e2r[s] = ld(pe);
+      o2r[s] = ld(po);
+#pragma unroll
+      for (int m = 0; m < MT; ++m) E2r[s][m] = (unsigned long long)m < M ? ld(pm + m * A) : 0ull;
+      vlr[s] = pvo[0];
+      vhr[s] = pvo[1];
+      if (!last_check || nload + 1 < re) {
+        pc += A;
+        pe += rsK;
+        po += rsK;
+        pm += rsM;
+        pvo += K;
+      }
+      ++nload;
+    };
+    auto run = [&](unsigned long long r, int s, bool last_check) {
+      const u64 vlo = __builtin_amdgcn_readfirstlane((unsigned)vlr[s]) |
+                      ((u64)__builtin_amdgcn_readfirstlane((unsigned)(vlr[s] >> 32)) << 32);
+      u64 vhi = __builtin_amdgcn_readfirstlane((unsigned)vhr[s]) |
+                ((u64)__builtin_amdgcn_readfirstlane((unsigned)(vhr[s] >> 32)) << 32);
+      vhi = vhi < p.Dv ? vhi : p.Dv;  // (a malformed vd_off never reads past the rows: flags bit 5)
+      step(r, c2r[s], e2r[s], o2r[s], E2r[s], vlo < vhi ? vlo : vhi, vhi);
+      load_step(s, last_check);
+    };
+#pragma unroll
+    for (int s = 0; s < DEPTH; ++s) load_step(s, true);
+    unsigned long long r0 = rs;
+    // blocks whose loads (rows r0 + DEPTH .. r0 + 2 DEPTH - 1) all have a next row: no clamp
+    for (; r0 + 2 * DEPTH < re; r0 += DEPTH) {
+#pragma unroll
+      for (int s = 0; s < DEPTH; ++s) run(r0 + s, s, false);
+    }
+    for (; r0 < re; r0 += DEPTH) {
+#pragma unroll
+      for (int s = 0; s < DEPTH; ++s) {
+        if (r0 + s >= re) break;
+        run(r0 + s, s, true);
+      }
+    }
+  };
+
   if constexpr (SPL > 0) {
     // ---- whole-chunk skip (round 5), the counter Map's (map_counter.hip) with the nested Orswot:
     // chunks of S = 8 steps in the transposed layout (lane (hh, a): actor a of step i*SPL + hh),
@@ -387,9 +445,13 @@ __global__ __launch_bounds__(kMoWaves * kWave) void map_orswot_fold_kernel(MapOr
       }
       return fail == 0;
     };
-    auto body = [&](auto B, unsigned long long c) {
+    // The skip only pays where most chunks pass (a failed chunk's exact steps move their rows from
+    // the transposed layout, ~1.6x the ring's step): after a window of 8 chunks with fewer than 3
+    // skipped the wave runs kMoRingSpan steps through the register ring, then tests chunks again.
+    unsigned hist = ~0u;  // skip bits of the latest chunks (uniform)
+    auto body = [&](auto B, unsigned long long c) -> bool {  // true: leave the chunk mode after c
       constexpr int b = decltype(B)::value;
-      if (c >= nch) return;
+      if (c >= nch) return false;
       if (c + NB - 1 < nch) load_chunk(std::integral_constant<int, (b + NB - 1) % NB>{}, c + NB - 1);
       const unsigned long long r0 = c * S;
       const unsigned long long n = R - r0 < (unsigned long long)S ? R - r0 : S;
@@ -405,7 +467,8 @@ __global__ __launch_bounds__(kMoWaves * kWave) void map_orswot_fold_kernel(MapOr
         }
         C = C > cm ? C : cm;
         liveness(false);
-        return;
+        hist = hist << 1 | 1u;
+        return false;
       }
       for (int s2 = 0; s2 < (int)n; ++s2) {  // the chunk's steps, exactly (rows moved into lane = actor)
         const int i = s2 / SPL, src = (s2 % SPL) * (int)AA + (int)a;
@@ -435,64 +498,31 @@ __global__ __launch_bounds__(kMoWaves * kWave) void map_orswot_fold_kernel(MapOr
         vhi = vhi < p.Dv ? vhi : p.Dv;  // (a malformed vd_off never reads past the rows: flags bit 5)
         step(r0 + s2, c2, e2, o2, E2, vlo < vhi ? vlo : vhi, vhi);
       }
+      hist <<= 1;
+      return __builtin_popcount(hist & 0xFFu) < 3;
     };
-    load_chunk(std::integral_constant<int, 0>{}, 0);
-    if (nch > 1) load_chunk(std::integral_constant<int, 1>{}, 1);
-    for (unsigned long long c = 0; c < nch; c += NB) {
-      body(std::integral_constant<int, 0>{}, c);
-      body(std::integral_constant<int, 1>{}, c + 1);
-      body(std::integral_constant<int, 2>{}, c + 2);
+    // chunks c0.. (chunk c0 + j in buffer j % NB) until the last or a poor window; the next chunk
+    auto chunk_phase = [&](unsigned long long c0) -> unsigned long long {
+      load_chunk(std::integral_constant<int, 0>{}, c0);
+      if (c0 + 1 < nch) load_chunk(std::integral_constant<int, 1>{}, c0 + 1);
+      hist = ~0u;
+      for (unsigned long long c = c0; c < nch; c += NB) {
+        if (body(std::integral_constant<int, 0>{}, c)) return c + 1;
+        if (body(std::integral_constant<int, 1>{}, c + 1)) return c + 2;
+        if (body(std::integral_constant<int, 2>{}, c + 2)) return c + 3;
+      }
+      return nch;
+    };
+    for (unsigned long long c = 0; c < nch;) {
+      c = chunk_phase(c);
+      if (c >= nch) break;
+      const unsigned long long rs = c * S, re = R - rs < kMoRingSpan ? R : rs + kMoRingSpan;
+      ring_phase(rs, re);
+      c = re == R ? nch : re / S;
     }
   } else {
-  // ---- replica rows through a register ring (DEPTH steps ahead; clamped past the last replica)
-  const u64 *pc = p.clock + g * R * A, *pe = p.ec + (g * R * K + k) * A, *po = p.oc + (g * R * K + k) * A;
-  const u64 *pm = p.ent + (g * R * K + k) * M * A;
-  const u64 *pvo = p.vd_off + g * R * K + k;
-  const unsigned long long rsK = K * A, rsM = K * M * A;
-  u64 c2r[DEPTH], e2r[DEPTH], o2r[DEPTH], E2r[DEPTH][MT], vlr[DEPTH], vhr[DEPTH];
-  unsigned long long nload = 0;
-  auto load_step = [&](int s, bool last_check) {
-    c2r[s] = ld(pc);
-    e2r[s] = ld(pe);
-    o2r[s] = ld(po);
-#pragma unroll
-    for (int m = 0; m < MT; ++m) E2r[s][m] = (unsigned long long)m < M ? ld(pm + m * A) : 0ull;
-    vlr[s] = pvo[0];
-    vhr[s] = pvo[1];
-    if (!last_check || nload + 1 < R) {
-      pc += A;
-      pe += rsK;
-      po += rsK;
-      pm += rsM;
-      pvo += K;
-    }
-    ++nload;
-  };
-  auto run = [&](unsigned long long r, int s, bool last_check) {
-    const u64 vlo = __builtin_amdgcn_readfirstlane((unsigned)vlr[s]) |
-                    ((u64)__builtin_amdgcn_readfirstlane((unsigned)(vlr[s] >> 32)) << 32);
-    u64 vhi = __builtin_amdgcn_readfirstlane((unsigned)vhr[s]) |
-              ((u64)__builtin_amdgcn_readfirstlane((unsigned)(vhr[s] >> 32)) << 32);
-    vhi = vhi < p.Dv ? vhi : p.Dv;  // (a malformed vd_off never reads past the rows: flags bit 5)
-    step(r, c2r[s], e2r[s], o2r[s], E2r[s], vlo < vhi ? vlo : vhi, vhi);
-    load_step(s, last_check);
-  };
-#pragma unroll
-  for (int s = 0; s < DEPTH; ++s) load_step(s, true);
-  unsigned long long r0 = 0;
-  // blocks whose loads (rows r0 + DEPTH .. r0 + 2 DEPTH - 1) all have a next row: no clamp
-  for (; r0 + 2 * DEPTH < R; r0 += DEPTH) {
-#pragma unroll
-    for (int s = 0; s < DEPTH; ++s) run(r0 + s, s, false);
+    ring_phase(0, R);
   }
-  for (; r0 < R; r0 += DEPTH) {
-#pragma unroll
-    for (int s = 0; s < DEPTH; ++s) {
-      if (r0 + s >= R) break;
-      run(r0 + s, s, true);
-    }
-  }
-  }  // (register ring)
 
   // ---- the key's folded entry (an empty entry clock: absent, value rows 0), the group's clock
   const bool pf = mo_nz(e);

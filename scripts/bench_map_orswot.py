@@ -3,7 +3,11 @@
 in HBM by torch): replica clocks, for each key present with probability 1/2 an entry clock and a
 nested Orswot clock drawn under the replica clock, member dots under the nested clock (a member
 present with probability 1/2); no deferred removes at either level (the fold is exact for any input;
-the removes' own paths are covered by tests/test_gpu_map_orswot.py).  HIP-event kernel time,
+the removes' own paths are covered by tests/test_gpu_map_orswot.py).  --input causal instead takes
+the config-4 generator's replicas (causally closed states of one op history, crdts_gpu.synth
+.map_replicas, no Map-level removes; key k written by actors k % A and (k+1) % A): the entry clock as
+the nested Orswot clock, writer i's live dot on k as the dot of member i (i = 0, 1: a member keeps
+its writer across replicas), members 2.. absent.  HIP-event kernel time,
 algorithmic bytes (every input row read once), parity of the GPU fold of the first
 --parity-replicas replicas against the oracle's left fold restricted to a key sample."""
 import argparse
@@ -27,6 +31,7 @@ ap.add_argument("--members", type=int, default=4)
 ap.add_argument("--steps", type=int, default=5)
 ap.add_argument("--sample-keys", type=int, default=4)
 ap.add_argument("--parity-replicas", type=int, default=256)
+ap.add_argument("--input", choices=("random", "causal"), default="random")
 args = ap.parse_args()
 R, K, A, M = args.replicas, args.keys, args.actors, args.members
 torch.cuda.set_device(0)
@@ -40,14 +45,25 @@ def below(hi):  # a random row under hi (per element in [0, hi]), 0 with probabi
     return x * (torch.rand(hi.shape, generator=gen, device=dev) < 0.5)
 
 
-clock = torch.randint(1, 1 << 20, (R, A), generator=gen, device=dev)
-pres = (torch.rand((R, K, 1), generator=gen, device=dev) < 0.5)
-ec = below(clock[:, None, :].expand(R, K, A)) * pres
-ec[..., 0] += pres[..., 0].long() * (ec.sum(-1) == 0)  # a present key has a non-empty entry clock
-oc = below(clock[:, None, :].expand(R, K, A)) * pres
-ent = torch.empty((R, K, M, A), dtype=torch.int64, device=dev)
-for m in range(M):
-    ent[:, :, m] = below(oc) * (torch.rand((R, K, 1), generator=gen, device=dev) < 0.5)
+if args.input == "random":
+    clock = torch.randint(1, 1 << 20, (R, A), generator=gen, device=dev)
+    pres = (torch.rand((R, K, 1), generator=gen, device=dev) < 0.5)
+    ec = below(clock[:, None, :].expand(R, K, A)) * pres
+    ec[..., 0] += pres[..., 0].long() * (ec.sum(-1) == 0)  # a present key has a non-empty entry clock
+    oc = below(clock[:, None, :].expand(R, K, A)) * pres
+    ent = torch.empty((R, K, M, A), dtype=torch.int64, device=dev)
+    for m in range(M):
+        ent[:, :, m] = below(oc) * (torch.rand((R, K, 1), generator=gen, device=dev) < 0.5)
+else:
+    from crdts_gpu import synth  # noqa: E402
+    inp = synth.map_replicas(ctx, R, K, A, 2, 0x5EED0004, kmax=256, p_def=0.0)
+    clock, ec = inp.clock, inp.ec
+    oc = ec.clone()
+    ent = torch.zeros((R, K, M, A), dtype=torch.int64, device=dev)
+    act = torch.arange(A, device=dev)
+    for i in range(min(M, 2)):  # member i: writer (k + i) % A's dot
+        ent[:, :, i] = ec * (act[None, :] == (torch.arange(K, device=dev)[:, None] + i) % A)[None]
+    del inp
 vd_off = torch.zeros(R * K + 1, dtype=torch.int64, device=dev)
 torch.cuda.synchronize()
 
@@ -85,7 +101,7 @@ full_sub = cg.map.orswot_lub_many(clock[:P].contiguous(), ec[:P].contiguous(), o
 ok = (got.clock == exp.clock and got.entries == exp.entries
       and np.array_equal(u64(full_sub.ec)[keys], u64(sub.ec)) and np.array_equal(u64(full_sub.ent)[keys], u64(sub.ent)))
 print(json.dumps({
-    "op": "map_orswot_lub_many", "replicas": R, "keys": K, "actors": A, "members": M, "kernel_ms": kern,
+    "op": "map_orswot_lub_many", "input": args.input, "replicas": R, "keys": K, "actors": A, "members": M, "kernel_ms": kern,
     "algorithmic_bytes": alg, "kernel_GBs": alg / kern / 1e6, "frac_of_8TBs": alg / kern / 8e9,
     "replica_merges_per_s": R / kern * 1e3, "parity": "ok" if ok else "MISMATCH",
     "parity_sample": f"first {P} replicas, keys {keys}",

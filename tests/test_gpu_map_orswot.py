@@ -331,3 +331,28 @@ def test_map_orswot_chunk_skip_steady_state(moctx):
     d = O.map_orswot_to_dense(maps, K, M, A)
     res, kw = _run(moctx, d)
     _same(_got_maps(res, kw, 1)[0], exp)
+
+
+@pytest.mark.parametrize("R1,R2,late", [(200, 2400, 2300), (120, 500, 400), (64, 2060, 2100)])
+def test_map_orswot_chunk_mode_switch(moctx, R1, R2, late):
+    """The chunk-skip mode's exits: R1 op-replay replicas (each a different view of the history: chunks
+    fail, and the wave leaves for kMoRingSpan = 2048 register-ring steps, which end inside the fold
+    or at its last replica), then R2 replicas repeating the fold so far (nested removes held) with
+    growing clocks (chunks pass again once the ring span is over), one late replica with new dots,
+    and a partial last chunk."""
+    A, K, M = 32, 2, 4
+    first = O.map_orswot_objects(R1, K, M, A, seed=R1, steps=6 * R1, p_vrm=0.4)
+    fold = O.map_fold_objects(first)
+    maps = list(first)
+    for r in range(R2):
+        m = fold.copy()
+        m.clock.apply(O.Dot(r % A, fold.clock.get(r % A) + 1 + r // A))
+        maps.append(m)
+    if late < len(maps):
+        maps[late] = O.map_orswot_objects(4, K, M, A, seed=63, steps=60, p_vrm=0.5)[-1]
+    maps.append(fold.copy())
+    exp = O.map_fold_objects(maps)
+    d = O.map_orswot_to_dense(maps, K, M, A)
+    res, kw = _run(moctx, d)
+    assert int(res.flags.cpu()[0]) == 0
+    _same(_got_maps(res, kw, 1)[0], exp)
