@@ -620,24 +620,27 @@ int crdt_map_counter_lub_many(crdt_ctx *ctx, const crdt_map_counter_batch *in, c
  *   clock [G][R][A], ec [G][R][K][A] the entry clocks, oc [G][R][K][A] the nested Orswot clocks,
  *   ent [G][R][K][M][A] its member dots (a member absent: its row 0; a key absent: ec row 0),
  *   the nested deferred removes as a device CSR over (g, r, k): vd_off u64 [G*R*K + 1],
- *   vd_clock [Dv][A], vd_mem [Dv] member bitmasks (an equal clock twice in one list: unioned);
+ *   vd_clock [Dv][A], vd_mem [Dv][Mw] member bitmasks, Mw = ceil(M / 64) words (1 for M <= 64: [Dv])
+ *   (an equal clock twice in one list: unioned);
  *   the Map's own deferred removes as for the counter Map: def_off HOST, G+1 entries.
  * Output per group g (packed): clock[g*A + a], ec / oc [(g*K + k)*A + a], ent [((g*K + k)*M + m)*A
  * + a], nested deferred vd_n[g*K + k] (<= 16) with vd_clock [((g*K + k)*16 + i)*A + a] and
- * vd_mem [(g*K + k)*16 + i]; flags[g]: bit 1 = def_row not non-decreasing or >= R, bit 3 = more
+ * vd_mem [((g*K + k)*16 + i)*Mw + w]; flags[g]: bit 1 = def_row not non-decreasing or >= R, bit 3 = more
  * than 256 live Map removes named one key, bit 4 = a key's Orswot held more than 16 deferred
  * removes, bit 5 = vd_off invalid (checked on the device: vd_off[0] == 0, non-decreasing,
  * vd_off[G*R*K] == Dv; the fold reads only rows [0, Dv) whatever it holds) — results of the
  * group unreliable; def_keep / def_keys as crdt_map_out.
  * Orswot::forget collects its deferred removes into a new map: two whose clocks become equal keep
  * one entry with the later one's members (the oracle's dict order).
- * Limits: A <= 64, M <= 32.  Device-memory contexts only. */
+ * Limits: A <= 1,024, M <= 1,024 (round 5: past A = 64 or M = 32 a wide kernel, lane = 64 actors
+ * apart, the key's member rows in its own output rows; CRDT_TUNE mowide=1 runs it at every shape).
+ * Device and host memory (crdt_mem_kind). */
 typedef struct crdt_map_orswot_batch {
   size_t G, R, K, M, A;
   const uint64_t *clock, *ec, *oc, *ent;
   const uint64_t *vd_off;   /* device, G*R*K + 1 */
   const uint64_t *vd_clock; /* [Dv][A] */
-  const uint64_t *vd_mem;   /* [Dv]    */
+  const uint64_t *vd_mem;   /* [Dv][Mw] */
   const size_t *def_off;    /* host, G+1 entries; NULL = no Map-level deferred removes */
   const uint32_t *def_row;
   const uint64_t *def_clock;
@@ -652,7 +655,7 @@ typedef struct crdt_map_orswot_out {
   uint64_t *ent;      /* [G][K][M][A]    */
   uint32_t *vd_n;     /* [G][K]          */
   uint64_t *vd_clock; /* [G][K][16][A]   */
-  uint64_t *vd_mem;   /* [G][K][16]      */
+  uint64_t *vd_mem;   /* [G][K][16][Mw]  */
   uint32_t *flags;    /* [G]             */
   uint8_t *def_keep;  /* [D]             */
   uint64_t *def_keys; /* [D][Kw]         */

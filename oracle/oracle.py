@@ -1415,11 +1415,12 @@ def map_counter_objects(R: int, K: int, A: int, W: int, seed: int, steps: int = 
 
 # ---- Map<K, Orswot<M>> (nested Orswot values, round 4; the reference's merge_error KAT type) -------
 def map_orswot_to_dense(maps, K: int, M: int, A: int):
-    """Ingest Map<int, Orswot<int>> objects (keys < K, members < M <= 64, actors < A): clock (R, A),
+    """Ingest Map<int, Orswot<int>> objects (keys < K, members < M, actors < A): clock (R, A),
     ec (R, K, A), oc (R, K, A) the nested Orswot clocks, ent (R, K, M, A) its member dots, the
     nested deferred removes as a CSR over (replica, key) — vd_off (R*K + 1), vd_clock (Dv, A),
-    vd_members (Dv,) member bitmasks — and the Map's own deferred pool (def_row, def_clock,
-    def_keys)."""
+    vd_members (Dv,) member bitmasks ((Dv, Mw) words past M = 64) — and the Map's own deferred pool
+    (def_row, def_clock, def_keys)."""
+    Mw = max(1, (M + 63) // 64)
     R = len(maps)
     clock = np.zeros((R, A), np.uint64)
     ec = np.zeros((R, K, A), np.uint64)
@@ -1445,7 +1446,7 @@ def map_orswot_to_dense(maps, K: int, M: int, A: int):
                     for a, c in rm.dots.items():
                         row[a] = c
                     vdc.append(row)
-                    vdm.append(int(_bits(mems, 64)[0]))
+                    vdm.append(int(_bits(mems, 64)[0]) if Mw == 1 else _bits(mems, 64 * Mw))
             vd_off.append(len(vdc))
         for rm, keys in m.deferred.items():
             row = np.zeros(A, np.uint64)
@@ -1457,7 +1458,7 @@ def map_orswot_to_dense(maps, K: int, M: int, A: int):
     D, Dv = len(def_row), len(vdc)
     Kw = (K + 63) // 64
     return dict(clock=clock, ec=ec, oc=oc, ent=ent, vd_off=np.array(vd_off, np.uint64),
-                vd_clock=np.array(vdc, np.uint64).reshape(Dv, A), vd_members=np.array(vdm, np.uint64),
+                vd_clock=np.array(vdc, np.uint64).reshape(Dv, A), vd_members=np.array(vdm, np.uint64).reshape((Dv,) if Mw == 1 else (Dv, Mw)),
                 def_row=np.array(def_row, np.uint64), def_clock=np.array(dcl, np.uint64).reshape(D, A),
                 def_keys=np.array(dk, np.uint64).reshape(D, Kw))
 

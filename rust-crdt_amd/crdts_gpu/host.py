@@ -370,7 +370,8 @@ def map_counter_lub_many(clock, ec, val, def_off=None, def_row=None, def_clock=N
 def map_orswot_lub_many(clock, ec, oc, ent, vd_off, vd_clock=None, vd_mem=None, def_off=None, def_row=None,
                         def_clock=None, def_keys=None, ctx: Optional[HostContext] = None) -> dict:
     """crdt_map_orswot_lub_many on host arrays (one group): clock (R, A), ec / oc (R, K, A), ent (R, K, M, A),
-    the nested removes as a CSR over (r, k): vd_off (R*K + 1,), vd_clock (Dv, A), vd_mem (Dv,)."""
+    the nested removes as a CSR over (r, k): vd_off (R*K + 1,), vd_clock (Dv, A), vd_mem (Dv,) ((Dv, Mw)
+    member-mask words past M = 64; the results' vd_mem then (1, K, 16, Mw))."""
     ctx = ctx or HostContext.default()
     c, e, o_, m = (np.ascontiguousarray(_u64(x, n)) for x, n in ((clock, "clock"), (ec, "ec"), (oc, "oc"), (ent, "ent")))
     R, A = c.shape
@@ -390,7 +391,8 @@ def map_orswot_lub_many(clock, ec, oc, ent, vd_off, vd_clock=None, vd_mem=None, 
     Kw = (K + 63) // 64
     out = dict(clock=np.zeros((1, A), np.uint64), ec=np.zeros((1, K, A), np.uint64), oc=np.zeros((1, K, A), np.uint64),
                ent=np.zeros((1, K, M, A), np.uint64), vd_n=np.zeros((1, K), np.uint32),
-               vd_clock=np.zeros((1, K, 16, A), np.uint64), vd_mem=np.zeros((1, K, 16), np.uint64),
+               vd_clock=np.zeros((1, K, 16, A), np.uint64),
+               vd_mem=np.zeros((1, K, 16) if M <= 64 else (1, K, 16, (M + 63) // 64), np.uint64),
                flags=np.zeros(1, np.uint32), def_keep=np.zeros(D, np.uint8), def_keys=np.zeros((D, Kw), np.uint64))
     ob = _abi.MapOrswotOut()
     for n in ("clock", "ec", "oc", "ent", "vd_n", "vd_clock", "vd_mem", "flags"):

@@ -509,7 +509,7 @@ class MapOrswotLub(NamedTuple):
     ent: torch.Tensor                 # (G, K, M, A) its member dots
     vd_n: torch.Tensor                # (G, K) int32: nested deferred removes per key
     vd_clock: torch.Tensor            # (G, K, 16, A)
-    vd_mem: torch.Tensor              # (G, K, 16) member bitmasks
+    vd_mem: torch.Tensor              # (G, K, 16) member bitmasks ((G, K, 16, Mw) past M = 64)
     flags: torch.Tensor               # (G,) int32
     def_keep: Optional[torch.Tensor]  # (D,) uint8
     def_keys: Optional[torch.Tensor]  # (D, Kw)
@@ -523,8 +523,9 @@ def orswot_lub_many(clock: torch.Tensor, ec: torch.Tensor, oc: torch.Tensor, ent
     """The exact left fold of Map::merge (map.rs:140-220) for Map<K, Orswot<M>> — orswot.rs:81-149 as
     the value's merge, :150-183 as its forget.  clock (G,R,A) / (R,A), ec and oc (G,R,K,A), ent
     (G,R,K,M,A), all contiguous; the nested deferred removes as a device CSR over (g, r, k): vd_off
-    (G*R*K + 1,) int64, vd_clock (Dv, A), vd_mem (Dv,) member bitmasks; the Map's own deferred pool as
-    for lub_many (host def_off).  check=True raises on flags (bit 1: def_row not sorted / out of
+    (G*R*K + 1,) int64, vd_clock (Dv, A), vd_mem (Dv,) member bitmasks ((Dv, Mw) words, Mw = ceil(M/64),
+    past M = 64); the Map's own deferred pool as for lub_many (host def_off).  A <= 1,024, M <= 1,024
+    (past A = 64 or M = 32 the library runs its wide kernel).  check=True raises on flags (bit 1: def_row not sorted / out of
     range, bit 3: more than 256 live Map removes named one key, bit 4: more than 16 nested deferred
     removes on one key)."""
     ctx = ctx or Context.default(clock.device.index)
@@ -548,14 +549,16 @@ def orswot_lub_many(clock: torch.Tensor, ec: torch.Tensor, oc: torch.Tensor, ent
         raise ValueError(f"map.orswot_lub_many: vd_off must be int64 / uint64 (got {vd_off.dtype})")
     # Dv = rows of vd_clock / vd_mem; the library checks vd_off against it on the device (flags bit 5)
     Dv = int(vd_clock.shape[0]) if vd_clock is not None else 0
+    Mw = max(1, (M + 63) // 64)
     if Dv > 0:
-        for t, nm, shape in ((vd_clock, "vd_clock", (Dv, A)), (vd_mem, "vd_mem", (Dv,))):
-            if t is None or not t.is_contiguous() or tuple(t.shape) != shape:
+        for t, nm, shape in ((vd_clock, "vd_clock", (Dv, A)), (vd_mem, "vd_mem", (Dv,) if Mw == 1 else (Dv, Mw))):
+            if t is None or not t.is_contiguous() or tuple(t.shape) not in (shape, (Dv, 1) if Mw == 1 else shape):
                 raise ValueError(f"map.orswot_lub_many: {nm} must be a contiguous {shape} tensor")
             ctx.check_tensor(t, f"map.orswot_lub_many({nm})")
     Kw = (K + 63) // 64
     out = [torch.empty(sh, dtype=torch.int64, device=dev)
-           for sh in ((G, A), (G, K, A), (G, K, A), (G, K, M, A), (G, K, VD_CAP, A), (G, K, VD_CAP))]
+           for sh in ((G, A), (G, K, A), (G, K, A), (G, K, M, A), (G, K, VD_CAP, A),
+                      (G, K, VD_CAP) if Mw == 1 else (G, K, VD_CAP, Mw))]
     vd_n = torch.empty((G, K), dtype=torch.int32, device=dev)
     flags = torch.empty(G, dtype=torch.int32, device=dev)
     b = _abi.MapOrswotBatch()

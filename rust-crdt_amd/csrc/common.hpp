@@ -103,7 +103,10 @@ struct Tune {
   int map_counter_depth = 8;   // Map<K, counter> fold: register-ring depth at A <= 64 (4, 8, 16; 16: 4.86 vs 4.33 ms)
   int map_counter_kpw = 0;     // Map<K, counter> fold: keys per wave (1, 2, 4; A <= 64 / KPW; 0: automatic)
   int map_counter_cs = 1;      // Map<K, counter> fold: whole-chunk skip (A = 8, 16, 32; one key per wave)
-  int map_orswot_cs = 1;       // Map<K, Orswot> fold: whole-chunk skip (A = 8, 16, 32; M <= 4)
+  int map_orswot_cs = 0;       // Map<K, Orswot> fold: whole-chunk skip (A = 8, 16, 32; M <= 4; opt-in: the kernel
+                               //     takes as long as its slowest key, and on the config-4 generator's replicas
+                               //     some keys change in most chunks, profiles/r05_map_orswot_chunk_ab.log)
+  int map_orswot_wide = 0;     // Map<K, Orswot> fold: the wide kernel at every shape (it is used past A = 64 / M = 32)
   int map_apply_pf = 1;        // Map apply (16-lane groups): the next op's entry-clock row prefetched with its
                                //     Put / rm clock; absent keys skip their value rows (0: round-3 form;
                                //     1.28 vs 1.81 ms, profiles/r04_map_apply_pf_ab.log)

@@ -237,6 +237,7 @@ static void apply_tune(crdt_ctx *ctx, const char *t) {
       else if (k == "mckpw") ctx->tune.map_counter_kpw = v >= 4 ? 4 : (v >= 2 ? 2 : (v == 1 ? 1 : 0));
       else if (k == "mccs") ctx->tune.map_counter_cs = v ? 1 : 0;
       else if (k == "mocs") ctx->tune.map_orswot_cs = v ? 1 : 0;
+      else if (k == "mowide") ctx->tune.map_orswot_wide = v ? 1 : 0;
       else if (k == "mcdma") ctx->tune.map_counter_dma = v >= 16 ? 16 : (v > 0 ? 8 : 0);
       else if (k == "mapf") ctx->tune.map_apply_pf = v != 0;
       else if (k == "rbpc" && v > 0) ctx->tune.rows_blocks_per_cu = v;

@@ -1033,6 +1033,7 @@ static int map_orswot_lub_host_body(crdt_ctx *ctx, const crdt_map_orswot_batch *
   const size_t G = in->G, R = in->R, K = in->K, M = in->M, A = in->A, Kw = (K + 63) / 64, Dv = in->Dv;
   const size_t D = in->def_off ? in->def_off[G] : 0, N = G * R * K;
   constexpr size_t VD = 16;  // nested deferred slots per key in the output (crdt_gpu.h)
+  const size_t Mw = M > 64 ? (M + 63) / 64 : 1;  // member-mask words
   uint64_t *c, *e, *o, *m, *vo, *vc, *vm, *dc, *dk, *oc, *oe, *oo, *om, *ovc, *ovm, *ok2 = nullptr;
   uint32_t *dr, *ovn, *of;
   uint8_t *okp = nullptr;
@@ -1042,7 +1043,7 @@ static int map_orswot_lub_host_body(crdt_ctx *ctx, const crdt_map_orswot_batch *
   if (int rc = ds.get(ctx, N * M * A, &m)) return rc;
   if (int rc = ds.get(ctx, N + 1, &vo)) return rc;
   if (int rc = ds.get(ctx, Dv * A, &vc)) return rc;
-  if (int rc = ds.get(ctx, Dv, &vm)) return rc;
+  if (int rc = ds.get(ctx, Dv * Mw, &vm)) return rc;
   if (int rc = ds.get(ctx, D, &dr)) return rc;
   if (int rc = ds.get(ctx, D * A, &dc)) return rc;
   if (int rc = ds.get(ctx, D * Kw, &dk)) return rc;
@@ -1051,7 +1052,7 @@ static int map_orswot_lub_host_body(crdt_ctx *ctx, const crdt_map_orswot_batch *
   if (int rc = ds.get(ctx, G * K * A, &oo)) return rc;
   if (int rc = ds.get(ctx, G * K * M * A, &om)) return rc;
   if (int rc = ds.get(ctx, G * K * VD * A, &ovc)) return rc;
-  if (int rc = ds.get(ctx, G * K * VD, &ovm)) return rc;
+  if (int rc = ds.get(ctx, G * K * VD * Mw, &ovm)) return rc;
   if (int rc = ds.get(ctx, G * K, &ovn)) return rc;
   if (int rc = ds.get(ctx, G, &of)) return rc;
   if (out->def_keep)
@@ -1064,7 +1065,7 @@ static int map_orswot_lub_host_body(crdt_ctx *ctx, const crdt_map_orswot_batch *
   if (int rc = h2d_async(ctx, m, in->ent, N * M * A * 8)) return rc;
   if (int rc = h2d_async(ctx, vo, in->vd_off, (N + 1) * 8)) return rc;
   if (int rc = h2d_async(ctx, vc, in->vd_clock, Dv * A * 8)) return rc;
-  if (int rc = h2d_async(ctx, vm, in->vd_mem, Dv * 8)) return rc;
+  if (int rc = h2d_async(ctx, vm, in->vd_mem, Dv * Mw * 8)) return rc;
   if (int rc = h2d_async(ctx, dr, in->def_row, D * 4)) return rc;
   if (int rc = h2d_async(ctx, dc, in->def_clock, D * A * 8)) return rc;
   if (int rc = h2d_async(ctx, dk, in->def_keys, D * Kw * 8)) return rc;
@@ -1090,7 +1091,7 @@ static int map_orswot_lub_host_body(crdt_ctx *ctx, const crdt_map_orswot_batch *
   if (int rc = d2h_async(ctx, out->ent, om, G * K * M * A * 8)) return rc;
   if (int rc = d2h_async(ctx, out->vd_n, ovn, G * K * 4)) return rc;
   if (int rc = d2h_async(ctx, out->vd_clock, ovc, G * K * VD * A * 8)) return rc;
-  if (int rc = d2h_async(ctx, out->vd_mem, ovm, G * K * VD * 8)) return rc;
+  if (int rc = d2h_async(ctx, out->vd_mem, ovm, G * K * VD * Mw * 8)) return rc;
   if (int rc = d2h_async(ctx, out->flags, of, G * 4)) return rc;
   if (int rc = d2h_async(ctx, out->def_keep, okp, D)) return rc;
   if (int rc = d2h_async(ctx, out->def_keys, ok2, D * Kw * 8)) return rc;

@@ -41,6 +41,7 @@ struct MapOrswotPlan {
   const u64 *vd_clock, *vd_mem;       // (Dv, A), (Dv) member bitmasks
   unsigned long long Dv;              // (a step reads rows [min(lo, hi'), hi') with hi' = min(hi, Dv))
   unsigned long long G, R, K, M, A, Kw;
+  unsigned long long Mw;  // u64 words per member bitmask: (M + 63) / 64 (1 for M <= 64)
   const size_t *def_off;  // device copy (G+1), or null: no Map-level removes
   const uint32_t *def_row;
   const u64 *def_clock, *def_keys;
@@ -387,27 +388,36 @@ __global__ __launch_bounds__(kMoWaves * kWave) void map_orswot_fold_kernel(MapOr
         qc[b][i] = bc[rr * AA];
         qe[b][i] = be[rr * rsK];
         qo[b][i] = bo[rr * rsK];
+        // (every load unconditional, so that no load sits in a branch and none is waited for at
+        // once: a member past M reads member 0's row, which the test ignores)
 #pragma unroll
-        for (int m = 0; m < MT; ++m) qm[b][m][i] = (unsigned long long)m < M ? bm[rr * rsM + m * AA] : 0ull;
+        for (int m = 0; m < MT; ++m) qm[b][m][i] = bm[rr * rsM + ((unsigned long long)m < M ? m : 0) * AA];
       }
-      unsigned long long rs = r0 + (unsigned long long)(lane < S ? lane : 0);
+      unsigned long long rs = r0 + (unsigned long long)(lane & (S - 1));
       rs = rs < R ? rs : R - 1;
-      qlo[b] = lane < S ? pvo0[rs * K] : 0ull;  // lane s < S: step r0 + s's nested remove range
-      qhi[b] = lane < S ? pvo0[rs * K + 1] : 0ull;
+      qlo[b] = pvo0[rs * K];  // lane s (mod S): step r0 + s's nested remove range
+      qhi[b] = pvo0[rs * K + 1];
     };
+#ifdef MO_STATS
+    unsigned st[7] = {0, 0, 0, 0, 0, 0, 0};  // skipped, nested rm, !vnorm, held dead, no p1, test, other
+#define MO_ST(i) (++st[i])
+#else
+#define MO_ST(i) ((void)0)
+#endif
     auto test_chunk = [&](auto B) -> bool {
       constexpr int b = decltype(B)::value;
-      if (__ballot(qhi[b] != qlo[b])) return false;  // a step carries nested removes: exact
+      if (__ballot(qhi[b] != qlo[b])) return MO_ST(1), false;  // a step carries nested removes: exact
       // the held nested removes must already be applied to the rows and live (!(rm <= oc)): a
       // both-present step re-applies them and re-tests their liveness
-      if (!vnorm) return false;
+      if (!vnorm) return MO_ST(2), false;
       for (int i = 0; i < nd; ++i)
-        if (!__ballot(vrow[(unsigned long long)i * kWave + lane] > oc)) return false;
+        if (!__ballot(vrow[(unsigned long long)i * kWave + lane] > oc)) return MO_ST(3), false;
       const u64 e0 = e, C0 = C;
       if (!mo_nz(e0)) {  // the acc lacks the key: no replica of the chunk may add it
         u64 okm = ~0ull;
 #pragma unroll
         for (int i = 0; i < NE; ++i) okm &= __ballot(qe[b][i] <= C0);
+        if (okm != ~0ull) MO_ST(4);
         return okm == ~0ull;
       }
       const u64 em1 = e0 ? e0 - 1 : 0;
@@ -432,7 +442,7 @@ __global__ __launch_bounds__(kMoWaves * kWave) void map_orswot_fold_kernel(MapOr
         bool cb = (e2 == e0 || (c2 <= TE && e2 <= TB)) && e2 <= TX && o2 <= oc;
 #pragma unroll
         for (int m = 0; m < MT; ++m) {
-          const u64 E2 = qm[b][m][i];
+          const u64 E2 = (unsigned long long)m < M ? qm[b][m][i] : E[m];  // (E[m] = 0 past M)
           cb = cb && (E2 == E[m] || (E2 <= oc && o2 <= TEm[m]));
         }
         const u64 mN = __ballot(e2 != 0), mB = __ballot(cb), mO = __ballot(c2 <= TN);
@@ -443,83 +453,65 @@ __global__ __launch_bounds__(kMoWaves * kWave) void map_orswot_fold_kernel(MapOr
           fail |= ~sel & Mk;
         }
       }
+      if (fail) MO_ST(5);
       return fail == 0;
     };
-    // The skip only pays where most chunks pass (a failed chunk's exact steps move their rows from
-    // the transposed layout, ~1.6x the ring's step): after a window of 8 chunks with fewer than 3
-    // skipped the wave runs kMoRingSpan steps through the register ring, then tests chunks again.
-    unsigned hist = ~0u;  // skip bits of the latest chunks (uniform)
-    auto body = [&](auto B, unsigned long long c) -> bool {  // true: leave the chunk mode after c
+    // The chunk loop only tests and skips: a chunk that fails the test ends it, and its steps run
+    // through the register ring (one copy of the exact step in the kernel, rows in lane = actor
+    // layout), then chunks are tested again.  The skip only pays where most chunks pass: after a
+    // window of 8 tested chunks with fewer than 3 skipped the ring runs kMoRingSpan steps.
+    unsigned hist = ~0u;  // skip bits of the latest tested chunks (uniform)
+    auto body = [&](auto B, unsigned long long c) -> bool {  // false: chunk c must run exactly
       constexpr int b = decltype(B)::value;
-      if (c >= nch) return false;
+      if (c >= nch) return true;
       if (c + NB - 1 < nch) load_chunk(std::integral_constant<int, (b + NB - 1) % NB>{}, c + NB - 1);
       const unsigned long long r0 = c * S;
       const unsigned long long n = R - r0 < (unsigned long long)S ? R - r0 : S;
-      const bool skip = n == S && (unsigned long long)nxt >= r0 + S && test_chunk(B);
-      if (skip) {
-        u64 cm = 0;
+      if (!(n == S && (unsigned long long)nxt >= r0 + S && test_chunk(B))) return false;
+      MO_ST(0);
+      u64 cm = 0;
 #pragma unroll
-        for (int i = 0; i < NE; ++i) cm = qc[b][i] > cm ? qc[b][i] : cm;
+      for (int i = 0; i < NE; ++i) cm = qc[b][i] > cm ? qc[b][i] : cm;
 #pragma unroll
-        for (int off = (int)AA; off < kWave; off <<= 1) {
-          const u64 o = __shfl_xor(cm, off);
-          cm = o > cm ? o : cm;
-        }
-        C = C > cm ? C : cm;
-        liveness(false);
-        hist = hist << 1 | 1u;
-        return false;
+      for (int off = (int)AA; off < kWave; off <<= 1) {
+        const u64 o = __shfl_xor(cm, off);
+        cm = o > cm ? o : cm;
       }
-      for (int s2 = 0; s2 < (int)n; ++s2) {  // the chunk's steps, exactly (rows moved into lane = actor)
-        const int i = s2 / SPL, src = (s2 % SPL) * (int)AA + (int)a;
-        u64 c2 = 0, e2 = 0, o2 = 0, E2[MT];
-#pragma unroll
-        for (int m = 0; m < MT; ++m) E2[m] = 0;
-#pragma unroll
-        for (int ii = 0; ii < NE; ++ii) {
-          if (ii == i) {
-            c2 = qc[b][ii];
-            e2 = qe[b][ii];
-            o2 = qo[b][ii];
-#pragma unroll
-            for (int m = 0; m < MT; ++m) E2[m] = qm[b][m][ii];
-          }
-        }
-        c2 = __shfl(c2, src);
-        e2 = __shfl(e2, src);
-        o2 = __shfl(o2, src);
-#pragma unroll
-        for (int m = 0; m < MT; ++m) E2[m] = __shfl(E2[m], src);
-        const u64 lo = __shfl(qlo[b], s2), hi0 = __shfl(qhi[b], s2);
-        const u64 vlo = __builtin_amdgcn_readfirstlane((unsigned)lo) |
-                        ((u64)__builtin_amdgcn_readfirstlane((unsigned)(lo >> 32)) << 32);
-        u64 vhi = __builtin_amdgcn_readfirstlane((unsigned)hi0) |
-                  ((u64)__builtin_amdgcn_readfirstlane((unsigned)(hi0 >> 32)) << 32);
-        vhi = vhi < p.Dv ? vhi : p.Dv;  // (a malformed vd_off never reads past the rows: flags bit 5)
-        step(r0 + s2, c2, e2, o2, E2, vlo < vhi ? vlo : vhi, vhi);
-      }
-      hist <<= 1;
-      return __builtin_popcount(hist & 0xFFu) < 3;
+      C = C > cm ? C : cm;
+      liveness(false);
+      hist = hist << 1 | 1u;
+      return true;
     };
-    // chunks c0.. (chunk c0 + j in buffer j % NB) until the last or a poor window; the next chunk
+    // chunks c0.. (chunk c0 + j in buffer j % NB) while they skip; the first one that does not (nch: none)
     auto chunk_phase = [&](unsigned long long c0) -> unsigned long long {
       load_chunk(std::integral_constant<int, 0>{}, c0);
       if (c0 + 1 < nch) load_chunk(std::integral_constant<int, 1>{}, c0 + 1);
-      hist = ~0u;
       for (unsigned long long c = c0; c < nch; c += NB) {
-        if (body(std::integral_constant<int, 0>{}, c)) return c + 1;
-        if (body(std::integral_constant<int, 1>{}, c + 1)) return c + 2;
-        if (body(std::integral_constant<int, 2>{}, c + 2)) return c + 3;
+        if (!body(std::integral_constant<int, 0>{}, c)) return c;
+        if (!body(std::integral_constant<int, 1>{}, c + 1)) return c + 1;
+        if (!body(std::integral_constant<int, 2>{}, c + 2)) return c + 2;
       }
       return nch;
     };
+    unsigned long long nring = 0;
     for (unsigned long long c = 0; c < nch;) {
       c = chunk_phase(c);
       if (c >= nch) break;
-      const unsigned long long rs = c * S, re = R - rs < kMoRingSpan ? R : rs + kMoRingSpan;
+      hist <<= 1;
+      const bool poor = __builtin_popcount(hist & 0xFFu) < 3;
+      const unsigned long long span = poor ? kMoRingSpan : (unsigned long long)S;
+      const unsigned long long rs = c * S, re = R - rs < span ? R : rs + span;
       ring_phase(rs, re);
+      if (poor) hist = ~0u;
+      nring += re - rs;
       c = re == R ? nch : re / S;
     }
+#ifdef MO_STATS
+    if (lane == 0 && gk < 6)
+      printf("mo key %llu: chunks %llu skipped %u | nested-rm %u !vnorm %u held-dead %u no-p1 %u test %u | ring steps %llu nd %d\n",
+             gk, nch, st[0], st[1], st[2], st[3], st[4], st[5], nring, nd);
+#endif
+    (void)nring;
   } else {
     ring_phase(0, R);
   }
@@ -549,6 +541,364 @@ __global__ __launch_bounds__(kMoWaves * kWave) void map_orswot_fold_kernel(MapOr
     atomicOr(p.o_flags + g, (bad ? 2u : 0u) | (full ? 8u : 0u) | (vfull ? 16u : 0u));
 }
 
+// ---- wide shapes (round 5): A <= 1,024 actors, M <= 1,024 members ---------------------------------
+// The same fold, step for step (the comments of map_orswot_fold_kernel's step() apply line by line),
+// one wave per (group, key) with lane l holding actors l + 64 j (j < APL).  The key's member rows and
+// its nested deferred rm rows live in the key's own output rows (o_ent, o_vd_clock: each lane reads
+// back only the words it wrote), the nested removes' member masks (Mw words each) and the Map's
+// removes naming the key in LDS.  Every replica row is read straight from global memory: a
+// correctness path for shapes past the register kernel's, not a fast one.
+constexpr int kMoWideMw = 16;  // member-mask words (M <= 1,024)
+template <int APL>
+__global__ __launch_bounds__(kMoWaves * kWave) void map_orswot_wide_kernel(MapOrswotPlan p) {
+  extern __shared__ u64 lds[];
+  const int lane = (int)(threadIdx.x % kWave), wv = (int)(threadIdx.x / kWave);
+  const unsigned long long gk = (unsigned long long)blockIdx.x * kMoWaves + wv;
+  if (gk >= p.G * p.K) return;  // (whole waves; nothing below synchronises the workgroup)
+  const unsigned long long g = gk / p.K, k = gk % p.K, A = p.A, R = p.R, K = p.K, M = p.M, Mw = p.Mw;
+  constexpr unsigned long long WQ = kMoList + kMoLive / 2 + kMoVd * kMoWideMw;
+  u64 *lst = lds + (unsigned long long)wv * WQ;
+  uint32_t *live = reinterpret_cast<uint32_t *>(lst + kMoList);
+  u64 *vmsk = lst + kMoList + kMoLive / 2;  // [kMoVd][Mw] nested removes' member masks
+  u64 *wE = p.o_ent + gk * M * A;           // [M][A] the key's member rows (working state)
+  u64 *wV = p.o_vd_clock + gk * kMoVd * A;  // [kMoVd][A] its nested deferred rm rows
+  // row I/O: word j of the lane is actor lane + 64 j; words past A read 0 and are never written
+  auto ldr = [&](const u64 *row, u64 (&x)[APL]) {
+#pragma unroll
+    for (int j = 0; j < APL; ++j) {
+      const unsigned long long a = (unsigned long long)lane + 64ull * j;
+      x[j] = a < A ? row[a] : 0ull;
+    }
+  };
+  auto str = [&](u64 *row, const u64 (&x)[APL]) {
+#pragma unroll
+    for (int j = 0; j < APL; ++j) {
+      const unsigned long long a = (unsigned long long)lane + 64ull * j;
+      if (a < A) row[a] = x[j];
+    }
+  };
+  auto any_nz = [&](const u64 (&x)[APL]) {
+    u64 o = 0;
+#pragma unroll
+    for (int j = 0; j < APL; ++j) o |= x[j];
+    return __ballot(o != 0) != 0;
+  };
+  auto any_gt = [&](const u64 (&x)[APL], const u64 (&c)[APL]) {
+    bool b = false;
+#pragma unroll
+    for (int j = 0; j < APL; ++j) b = b || x[j] > c[j];
+    return __ballot(b) != 0;
+  };
+  auto any_ne = [&](const u64 (&x)[APL], const u64 (&c)[APL]) {
+    bool b = false;
+#pragma unroll
+    for (int j = 0; j < APL; ++j) b = b || x[j] != c[j];
+    return __ballot(b) != 0;
+  };
+  auto fg_row = [&](u64 (&x)[APL], const u64 (&c)[APL]) {
+#pragma unroll
+    for (int j = 0; j < APL; ++j) x[j] = mo_fg(x[j], c[j]);
+  };
+
+  // ---- the Map's removes naming key k, in replica order (map_orswot_fold_kernel's walk)
+  const unsigned long long d0 = p.def_off ? p.def_off[g] : 0, d1 = p.def_off ? p.def_off[g + 1] : 0;
+  unsigned long long dc = d0;
+  int nl = 0, li = 0;
+  bool bad = false;
+  u64 last_row = 0;
+  auto refill = [&]() {
+    nl = 0;
+    li = 0;
+    while (dc < d1 && nl + kWave <= kMoList) {
+      const unsigned long long d = dc + lane;
+      bool hit = false;
+      u64 row = 0;
+      if (d < d1) {
+        row = p.def_row[d];
+        hit = (p.def_keys[d * p.Kw + k / 64] >> (k % 64)) & 1ull;
+      }
+      const u64 prev = __shfl_up(row, 1);
+      bool b = d < d1 && (row >= R || (lane == 0 ? row < last_row : row < prev));
+      if (__ballot(b)) bad = true;
+      const unsigned long long n = d1 - dc < (unsigned long long)kWave ? d1 - dc : kWave;
+      last_row = __shfl(row, (int)n - 1);
+      const u64 m = __ballot(hit);
+      if (hit) lst[nl + __popcll(m & ((1ull << lane) - 1))] = (row << 32) | (u64)(d - d0);
+      nl += __popcll(m);
+      dc += n;
+    }
+  };
+  unsigned nxt = ~0u;
+  auto advance = [&]() {
+    for (;;) {
+      if (li < nl) {
+        nxt = (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(lst[li] >> 32));
+        return;
+      }
+      if (dc >= d1) {
+        nxt = ~0u;
+        return;
+      }
+      refill();
+    }
+  };
+  refill();
+  advance();
+  bool full = false, vfull = false;
+  int na = 0;
+  auto live_row = [&](int i, u64 (&x)[APL]) { ldr(p.def_clock + (d0 + live[i]) * A, x); };
+  u64 rk[APL], T[APL];
+
+  // ---- the key's state (members and nested removes in wE / wV / vmsk)
+  u64 C[APL], e[APL], oc[APL];
+#pragma unroll
+  for (int j = 0; j < APL; ++j) C[j] = e[j] = oc[j] = rk[j] = 0, T[j] = ~0ull;
+  int nd = 0;
+
+  auto forget_members = [&](const u64 (&rm)[APL], const u64 *msk) {  // apply_rm's member forget
+    for (unsigned long long w = 0; w < Mw; ++w) {
+      u64 bits = msk[w];
+      while (bits) {
+        const unsigned long long m = w * 64 + (unsigned long long)__builtin_ctzll(bits);
+        bits &= bits - 1;
+        if (m >= M) break;
+        u64 x[APL];
+        ldr(wE + m * A, x);
+        fg_row(x, rm);
+        str(wE + m * A, x);
+      }
+    }
+  };
+  auto vd_add = [&](const u64 (&rm)[APL], const u64 *msk) {  // deferred.entry(clock) extend / insert
+    for (int i = 0; i < nd; ++i) {
+      u64 x[APL];
+      ldr(wV + (unsigned long long)i * A, x);
+      if (!any_ne(x, rm)) {
+        for (unsigned long long w = (unsigned long long)lane; w < Mw; w += kWave) vmsk[i * Mw + w] |= msk[w];
+        return;
+      }
+    }
+    if (nd < kMoVd) {
+      str(wV + (unsigned long long)nd * A, rm);
+      for (unsigned long long w = (unsigned long long)lane; w < Mw; w += kWave) vmsk[nd * Mw + w] = msk[w];
+      ++nd;
+    } else {
+      vfull = true;
+    }
+  };
+  auto vd_keep_live = [&]() {  // apply_deferred's re-test: keep !(rm <= oc), in order
+    int o = 0;
+    for (int i = 0; i < nd; ++i) {
+      u64 x[APL];
+      ldr(wV + (unsigned long long)i * A, x);
+      if (any_gt(x, oc)) {
+        if (o != i) {
+          str(wV + (unsigned long long)o * A, x);
+          for (unsigned long long w = (unsigned long long)lane; w < Mw; w += kWave) vmsk[o * Mw + w] = vmsk[i * Mw + w];
+        }
+        ++o;
+      }
+    }
+    nd = o;
+  };
+  auto value_forget = [&](const u64 (&X)[APL]) {  // Orswot's Causal::forget
+    fg_row(oc, X);
+    for (unsigned long long m = 0; m < M; ++m) {
+      u64 x[APL];
+      ldr(wE + m * A, x);
+      fg_row(x, X);
+      str(wE + m * A, x);
+    }
+    int o = 0;
+    for (int i = 0; i < nd; ++i) {
+      u64 x[APL];
+      ldr(wV + (unsigned long long)i * A, x);
+      fg_row(x, X);
+      if (!any_nz(x)) continue;  // forgotten
+      int jj = 0;
+      for (; jj < o; ++jj) {  // equal to a kept one: the later members at the earlier place
+        u64 y[APL];
+        ldr(wV + (unsigned long long)jj * A, y);
+        if (!any_ne(y, x)) break;
+      }
+      if (jj < o) {
+        for (unsigned long long w = (unsigned long long)lane; w < Mw; w += kWave) vmsk[jj * Mw + w] = vmsk[i * Mw + w];
+        continue;
+      }
+      str(wV + (unsigned long long)o * A, x);
+      if (o != i)
+        for (unsigned long long w = (unsigned long long)lane; w < Mw; w += kWave) vmsk[o * Mw + w] = vmsk[i * Mw + w];
+      ++o;
+    }
+    nd = o;
+  };
+  auto liveness = [&](bool chg) {
+    bool hitT = false;
+#pragma unroll
+    for (int j = 0; j < APL; ++j) hitT = hitT || C[j] >= T[j];
+    if (na > 0 && (chg || __ballot(hitT))) {
+      bool changed = chg;
+#pragma unroll
+      for (int j = 0; j < APL; ++j) T[j] = ~0ull;
+      for (int i = 0; i < na;) {
+        u64 rm[APL];
+        live_row(i, rm);
+        bool w = false;
+#pragma unroll
+        for (int j = 0; j < APL; ++j) w = w || rm[j] > C[j];
+        const u64 mb = __ballot(w);
+        if (mb) {
+          if (lane == __builtin_ctzll(mb)) {
+            bool done = false;
+#pragma unroll
+            for (int j = 0; j < APL; ++j) {
+              if (!done && rm[j] > C[j]) {
+                T[j] = rm[j] < T[j] ? rm[j] : T[j];
+                done = true;
+              }
+            }
+          }
+          ++i;
+          continue;
+        }
+        changed = true;
+        const int lastp = na - 1;
+        if (i != lastp) {
+          const unsigned li_last = live[lastp];
+          if (lane == 0) live[i] = li_last;
+        }
+        --na;
+      }
+      if (changed) {
+#pragma unroll
+        for (int j = 0; j < APL; ++j) rk[j] = 0;
+        for (int i = 0; i < na; ++i) {
+          u64 rm[APL];
+          live_row(i, rm);
+#pragma unroll
+          for (int j = 0; j < APL; ++j) rk[j] = mo_max(rk[j], rm[j]);
+        }
+      }
+    }
+  };
+
+  for (unsigned long long r = 0; r < R; ++r) {
+    const unsigned long long rk_ = (g * R + r) * K + k;
+    u64 c2[APL], e2[APL], o2[APL];
+    ldr(p.clock + (g * R + r) * A, c2);
+    ldr(p.ec + rk_ * A, e2);
+    ldr(p.oc + rk_ * A, o2);
+    u64 vlo = p.vd_off[rk_], vhi = p.vd_off[rk_ + 1];
+    vhi = vhi < p.Dv ? vhi : p.Dv;  // (a malformed vd_off never reads past the rows: flags bit 5)
+    vlo = vlo < vhi ? vlo : vhi;
+    const bool p1 = any_nz(e), p2 = any_nz(e2);
+    u64 en[APL], X[APL];
+#pragma unroll
+    for (int j = 0; j < APL; ++j) {
+      en[j] = e[j] == e2[j] ? e[j] : mo_max(mo_fg(e2[j], C[j]), mo_fg(e[j], c2[j]));
+      const u64 y = p1 ? (p2 ? mo_max(e[j], e2[j]) : c2[j]) : C[j];
+      X[j] = mo_fg(y, en[j]);
+    }
+    const bool stays = any_nz(en);
+    if (p1 && p2 && stays) {  // Orswot::merge
+      const u64 *E2 = p.ent + rk_ * M * A;
+      for (unsigned long long m = 0; m < M; ++m) {
+        u64 x[APL], x2[APL];
+        ldr(wE + m * A, x);
+        ldr(E2 + m * A, x2);
+#pragma unroll
+        for (int j = 0; j < APL; ++j) x[j] = x[j] == x2[j] ? x[j] : mo_max(mo_fg(x2[j], oc[j]), mo_fg(x[j], o2[j]));
+        str(wE + m * A, x);
+      }
+      for (u64 d = vlo; d < vhi; ++d) {
+        u64 rm[APL];
+        ldr(p.vd_clock + d * A, rm);
+        const u64 *msk = p.vd_mem + d * Mw;
+        forget_members(rm, msk);
+        if (any_gt(rm, oc)) vd_add(rm, msk);
+      }
+#pragma unroll
+      for (int j = 0; j < APL; ++j) oc[j] = mo_max(oc[j], o2[j]);
+      for (int i = 0; i < nd; ++i) {
+        u64 rm[APL];
+        ldr(wV + (unsigned long long)i * A, rm);
+        forget_members(rm, vmsk + i * Mw);
+      }
+      vd_keep_live();
+    } else if (p2 && !p1 && stays) {  // the replica's entry
+      const u64 *E2 = p.ent + rk_ * M * A;
+      for (unsigned long long m = 0; m < M; ++m) {
+        u64 x[APL];
+        ldr(E2 + m * A, x);
+        str(wE + m * A, x);
+      }
+#pragma unroll
+      for (int j = 0; j < APL; ++j) oc[j] = o2[j];
+      nd = 0;
+      for (u64 d = vlo; d < vhi; ++d) {
+        u64 rm[APL];
+        ldr(p.vd_clock + d * A, rm);
+        vd_add(rm, p.vd_mem + d * Mw);
+      }
+    }
+    if (stays && (p1 || p2)) value_forget(X);
+#pragma unroll
+    for (int j = 0; j < APL; ++j) e[j] = en[j];
+    // the Map's removes: replica r's own and the live ones
+    bool chg = false;
+    u64 f[APL];
+#pragma unroll
+    for (int j = 0; j < APL; ++j) f[j] = rk[j];
+    const unsigned r32 = (unsigned)r;
+    while (nxt <= r32) {
+      const unsigned idx = (unsigned)lst[li];
+      u64 rm[APL];
+      ldr(p.def_clock + (d0 + idx) * A, rm);
+#pragma unroll
+      for (int j = 0; j < APL; ++j) f[j] = mo_max(f[j], rm[j]);
+      if (na < kMoLive) {
+        if (lane == 0) live[na] = idx;
+        ++na;
+        chg = true;
+      } else {
+        full = true;
+      }
+      ++li;
+      advance();
+    }
+    if (na > 0) {
+      fg_row(e, f);
+      if (any_nz(e)) value_forget(f);
+    }
+#pragma unroll
+    for (int j = 0; j < APL; ++j) C[j] = mo_max(C[j], c2[j]);
+    liveness(chg);
+  }
+
+  // ---- the key's folded entry (absent: every row 0), the group's clock
+  const bool pf = any_nz(e);
+  if (!pf) {
+    u64 z[APL];
+#pragma unroll
+    for (int j = 0; j < APL; ++j) z[j] = 0;
+    for (unsigned long long m = 0; m < M; ++m) str(wE + m * A, z);
+  }
+  str(p.o_ec + gk * A, e);
+  if (!pf) {
+#pragma unroll
+    for (int j = 0; j < APL; ++j) oc[j] = 0;
+  }
+  str(p.o_oc + gk * A, oc);
+  if (k == 0) str(p.o_clock + g * A, C);
+  const int no = pf ? nd : 0;
+  for (int i = 0; i < no; ++i)
+    for (unsigned long long w = (unsigned long long)lane; w < Mw; w += kWave)
+      p.o_vd_mem[(gk * kMoVd + i) * Mw + w] = vmsk[i * Mw + w];
+  if (lane == 0) p.o_vd_n[gk] = (unsigned)no;
+  if ((bad || full || vfull) && lane == 0)
+    atomicOr(p.o_flags + g, (bad ? 2u : 0u) | (full ? 8u : 0u) | (vfull ? 16u : 0u));
+}
+
 // vd_off's CSR invariants: entry 0 is 0, entries never decrease, the last is Dv.  A
 // violation marks the group of the offending entry (flags bit 5); the fold clamps its reads anyway.
 __global__ void map_orswot_vd_check_kernel(const u64 *vd_off, unsigned long long n, unsigned long long per_group,
@@ -568,6 +918,15 @@ static size_t mo_lds() {
   return (size_t)kMoWaves * (kMoList * 8 + kMoLive * 4 + kMoRows * kWave * 8 + kMoVd * kWave * 8 + kMoVd * 8);
 }
 
+static size_t mo_wide_lds() { return (size_t)kMoWaves * (kMoList * 8 + kMoLive * 4 + kMoVd * kMoWideMw * 8); }
+
+template <int APL>
+static hipError_t launch_mo_wide(const MapOrswotPlan &p, hipStream_t s) {
+  const unsigned long long blocks = (p.G * p.K + kMoWaves - 1) / kMoWaves;
+  hipLaunchKernelGGL((map_orswot_wide_kernel<APL>), dim3((unsigned)blocks), dim3(kMoWaves * kWave), mo_wide_lds(), s, p);
+  return hipGetLastError();
+}
+
 template <int MT, int SPL = 0>
 static hipError_t launch_mo(const MapOrswotPlan &p, hipStream_t s) {
   const unsigned long long blocks = (p.G * p.K + kMoWaves - 1) / kMoWaves;
@@ -585,8 +944,9 @@ extern "C" int crdt_map_orswot_lub_many(crdt_ctx *ctx, const crdt_map_orswot_bat
   if (!in || !out) return fail(ctx, CRDT_EINVAL, "map_orswot_lub_many: NULL batch/out");
   const size_t G = in->G, R = in->R, K = in->K, M = in->M, A = in->A;
   if (G == 0 || K == 0 || A == 0) return CRDT_OK;
-  if (A > (size_t)kWave) return fail(ctx, CRDT_EUNSUPPORTED, "map_orswot_lub_many: A = %zu > %d", A, kWave);
-  if (M > 32) return fail(ctx, CRDT_EUNSUPPORTED, "map_orswot_lub_many: M = %zu > 32", M);
+  if (A > 16 * (size_t)kWave) return fail(ctx, CRDT_EUNSUPPORTED, "map_orswot_lub_many: A = %zu > %d", A, 16 * kWave);
+  if (M > 64 * (size_t)kMoWideMw)
+    return fail(ctx, CRDT_EUNSUPPORTED, "map_orswot_lub_many: M = %zu > %d", M, 64 * kMoWideMw);
   if (!out->clock || !out->ec || !out->oc || (M && !out->ent) || !out->vd_n || !out->vd_clock || !out->vd_mem ||
       !out->flags)
     return fail(ctx, CRDT_EINVAL, "map_orswot_lub_many: NULL output");
@@ -608,7 +968,7 @@ extern "C" int crdt_map_orswot_lub_many(crdt_ctx *ctx, const crdt_map_orswot_bat
   const size_t Kw = (K + 63) / 64;
   MapOrswotPlan p{(const u64 *)in->clock, (const u64 *)in->ec, (const u64 *)in->oc, (const u64 *)in->ent,
                   (const u64 *)in->vd_off, (const u64 *)in->vd_clock, (const u64 *)in->vd_mem, in->Dv, G, R, K, M, A, Kw,
-                  nullptr, in->def_row, (const u64 *)in->def_clock, (const u64 *)in->def_keys,
+                  (M + 63) / 64 > 0 ? (M + 63) / 64 : 1, nullptr, in->def_row, (const u64 *)in->def_clock, (const u64 *)in->def_keys,
                   (u64 *)out->clock, (u64 *)out->ec, (u64 *)out->oc, (u64 *)out->ent, (u64 *)out->vd_clock,
                   (u64 *)out->vd_mem, out->vd_n, out->flags};
   if (int rc = device_fill(ctx, out->flags, G * sizeof(unsigned), 0)) return rc;
@@ -634,9 +994,16 @@ extern "C" int crdt_map_orswot_lub_many(crdt_ctx *ctx, const crdt_map_orswot_bat
     }
     timing_begin(ctx, "map_orswot_fold");
     // (member rows past M are zero and still joined: the register capacity follows M)
-    // the whole-chunk skip (round 5) for A = 32 / 16 / 8 and up to 4 members (CRDT_TUNE mocs=0: off)
+    // the whole-chunk skip (round 5, opt-in: CRDT_TUNE mocs=1) for A = 32 / 16 / 8 and up to 4 members
+    // past A = 64 or M = 32 (or with CRDT_TUNE mowide=1): the wide kernel, APL actors per lane
+    const bool wide = ctx->tune.map_orswot_wide || A > (size_t)kWave || M > 32;
     const int spl = ctx->tune.map_orswot_cs && M <= 4 ? (A == 32 ? 2 : (A == 16 ? 4 : (A == 8 ? 8 : 0))) : 0;
-    const hipError_t he = spl == 2   ? launch_mo<4, 2>(p, ctx->stream)
+    const hipError_t he = wide ? (A <= 64    ? launch_mo_wide<1>(p, ctx->stream)
+                                  : A <= 128 ? launch_mo_wide<2>(p, ctx->stream)
+                                  : A <= 256 ? launch_mo_wide<4>(p, ctx->stream)
+                                  : A <= 512 ? launch_mo_wide<8>(p, ctx->stream)
+                                             : launch_mo_wide<16>(p, ctx->stream))
+                          : spl == 2 ? launch_mo<4, 2>(p, ctx->stream)
                           : spl == 4 ? launch_mo<4, 4>(p, ctx->stream)
                           : spl == 8 ? launch_mo<4, 8>(p, ctx->stream)
                           : M <= 4   ? launch_mo<4>(p, ctx->stream)

@@ -1282,9 +1282,10 @@ impl<K: Ord + Clone, A: Actor> BatchCvRDT for Map<K, PNCounter<A>, A> {
     }
 }
 
-/// Limits of the Map<K, Orswot> fold (include/crdt_gpu.h: A <= 64, M <= 32, 16 nested removes).
-pub const MAP_ORSWOT_MAX_ACTORS: usize = 64;
-pub const MAP_ORSWOT_MAX_MEMBERS: usize = 32;
+/// Limits of the Map<K, Orswot> fold (include/crdt_gpu.h: A <= 1,024, M <= 1,024, 16 nested removes;
+/// past A = 64 or M = 32 the library runs its wide kernel).
+pub const MAP_ORSWOT_MAX_ACTORS: usize = 1024;
+pub const MAP_ORSWOT_MAX_MEMBERS: usize = 1024;
 
 /// Every group's fold of Map<K, Orswot<M>> (crdt_map_orswot_lub_many, G groups of equal R).
 fn orswot_map_folds<K: Ord + Clone, M: Member, A: Actor>(ctx: &GpuCtx, groups: &[Vec<&Map<K, Orswot<M, A>, A>>])
@@ -1320,6 +1321,7 @@ fn orswot_map_folds<K: Ord + Clone, M: Member, A: Actor>(ctx: &GpuCtx, groups: &
                                        MAP_ORSWOT_MAX_ACTORS, MAP_ORSWOT_MAX_MEMBERS)));
     }
     let kw = (k + 63) / 64;
+    let mw = if m > 64 { (m + 63) / 64 } else { 1 }; // member-mask words
     let n = g * r * k;
     let (mut clock, mut ec, mut oc) = (vec![0u64; g * r * a], vec![0u64; n * a], vec![0u64; n * a]);
     let mut ent = vec![0u64; n * m * a];
@@ -1339,14 +1341,19 @@ fn orswot_map_folds<K: Ord + Clone, M: Member, A: Actor>(ctx: &GpuCtx, groups: &
                     let mut row = vec![0u64; a];
                     clock_row(rm, &actors, &mut row);
                     vd_clock.extend(row);
-                    vd_mem.push(ms.iter().fold(0u64, |acc, x| acc | (1u64 << mems.pos[x])));
+                    let mut words = vec![0u64; mw];
+                    for x in ms {
+                        let p = mems.pos[x];
+                        words[p / 64] |= 1u64 << (p % 64);
+                    }
+                    vd_mem.extend(words);
                 }
             }
-            vd_off.push(vd_mem.len() as u64);
+            vd_off.push((vd_mem.len() / mw) as u64);
         }
     }
     let pool = group_pool(groups, &actors, &keys);
-    let (nd, dv) = (pool.def_row.len(), vd_mem.len());
+    let (nd, dv) = (pool.def_row.len(), vd_mem.len() / mw);
     let batch = ffi::crdt_map_orswot_batch {
         G: g, R: r, K: k, M: m, A: a,
         clock: clock.as_ptr(), ec: ec.as_ptr(), oc: oc.as_ptr(), ent: ent.as_ptr(),
@@ -1357,7 +1364,7 @@ fn orswot_map_folds<K: Ord + Clone, M: Member, A: Actor>(ctx: &GpuCtx, groups: &
     };
     let (mut o_clock, mut o_ec, mut o_oc) = (vec![0u64; g * a], vec![0u64; g * k * a], vec![0u64; g * k * a]);
     let (mut o_ent, mut o_vdn) = (vec![0u64; g * k * m * a], vec![0u32; g * k]);
-    let (mut o_vdc, mut o_vdm) = (vec![0u64; g * k * 16 * a], vec![0u64; g * k * 16]);
+    let (mut o_vdc, mut o_vdm) = (vec![0u64; g * k * 16 * a], vec![0u64; g * k * 16 * mw]);
     let (mut flags, mut keep, mut okeys) = (vec![0u32; g], vec![0u8; nd], vec![0u64; nd * kw]);
     let mut out = ffi::crdt_map_orswot_out {
         clock: o_clock.as_mut_ptr(), ec: o_ec.as_mut_ptr(), oc: o_oc.as_mut_ptr(), ent: o_ent.as_mut_ptr(),
@@ -1388,8 +1395,9 @@ fn orswot_map_folds<K: Ord + Clone, M: Member, A: Actor>(ctx: &GpuCtx, groups: &
                 }
             }
             for i in 0..o_vdn[b] as usize {
-                let bits = o_vdm[b * 16 + i];
-                let ms: HashSet<M> = (0..m).filter(|&x| (bits >> x) & 1 != 0).map(|x| mems.ids[x].clone()).collect();
+                let bits = &o_vdm[(b * 16 + i) * mw..(b * 16 + i + 1) * mw];
+                let ms: HashSet<M> =
+                    (0..m).filter(|&x| (bits[x / 64] >> (x % 64)) & 1 != 0).map(|x| mems.ids[x].clone()).collect();
                 o.deferred.entry(row_clock(&o_vdc[(b * 16 + i) * a..(b * 16 + i + 1) * a], &actors))
                     .or_insert_with(HashSet::new).extend(ms);
             }

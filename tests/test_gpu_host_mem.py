@@ -355,10 +355,12 @@ def test_map_counter_host_lub_many(hctx, W):
         assert got == exp
 
 
-def test_map_orswot_host_lub_many(hctx):
-    maps = O.map_orswot_objects(30, 4, 6, 4, seed=5, steps=200, p_vrm=0.5)
+@pytest.mark.parametrize("M,A", [(6, 4), (70, 80)])
+def test_map_orswot_host_lub_many(hctx, M, A):
+    """(M = 70, A = 80: the wide kernel with two-word member masks, from host memory.)"""
+    maps = O.map_orswot_objects(30, 4, M, A, seed=5, steps=200, p_vrm=0.5)
     exp = O.map_fold_objects(maps)
-    d = O.map_orswot_to_dense(maps, 4, 6, 4)
+    d = O.map_orswot_to_dense(maps, 4, M, A)
     D, Dv = d["def_row"].shape[0], d["vd_clock"].shape[0]
     out = host.map_orswot_lub_many(d["clock"], d["ec"], d["oc"], d["ent"], d["vd_off"],
                                    d["vd_clock"] if Dv else None, d["vd_members"] if Dv else None,
@@ -366,7 +368,9 @@ def test_map_orswot_host_lub_many(hctx):
                                    def_keys=d["def_keys"], ctx=hctx)
     assert int(out["flags"][0]) == 0
     dset = _host_deferred(out, d["def_clock"]) if D else set()
-    vd = {k: [(out["vd_clock"][0, k, i], O.bitmap_members(out["vd_mem"][0, k, i:i + 1]))
+    vm = out["vd_mem"]
+    mw = (lambda k, i: vm[0, k, i]) if vm.ndim == 4 else (lambda k, i: vm[0, k, i:i + 1])  # noqa: E731
+    vd = {k: [(out["vd_clock"][0, k, i], O.bitmap_members(mw(k, i)))
               for i in range(int(out["vd_n"][0, k]))] for k in range(4)}
     got = O.dense_to_map_orswot(out["clock"][0], out["ec"][0], out["oc"][0], out["ent"][0], vd,
                                 [(np.array(rm, np.uint64), ks) for rm, ks in dset])

@@ -43,7 +43,8 @@ def _got_maps(res, kw, G):
         if kw:
             off = kw["def_off"]
             dset = cg.map.deferred_set(kw["def_clock"], res.def_keep, res.def_keys, int(off[g]), int(off[g + 1]))
-        vd = {k: [(vc[g, k, i], O.bitmap_members(vm[g, k, i:i + 1])) for i in range(int(vn[g, k]))]
+        mw = (lambda k, i: vm[g, k, i]) if vm.ndim == 4 else (lambda k, i: vm[g, k, i:i + 1])  # noqa: E731
+        vd = {k: [(vc[g, k, i], O.bitmap_members(mw(k, i))) for i in range(int(vn[g, k]))]
               for k in range(e.shape[1])}
         out.append(O.dense_to_map_orswot(c[g], e[g], o[g], m[g], vd,
                                          [(np.array(rm, np.uint64), ks) for rm, ks in dset]))
@@ -272,10 +273,10 @@ def test_map_orswot_dominated_nested_removes_not_held(gpu_ctx):
     _same(_got_maps(res, kw, 1)[0], exp)
 
 
-@pytest.fixture(params=["", "mocs=0"])
+@pytest.fixture(params=["mocs=1", "", "mowide=1"])
 def moctx(request):
-    """The default (A = 32 / 16 / 8 with up to 4 members: the whole-chunk skip, round 5) and the
-    register ring alone (mocs=0)."""
+    """The whole-chunk skip (mocs=1, opt-in; A = 32 / 16 / 8 with up to 4 members, round 5), the
+    default register ring and the wide kernel (mowide=1; the one past A = 64 / M = 32)."""
     torch.cuda.set_device(0)
     ctx = cg.Context(0)
     if request.param:
@@ -356,3 +357,35 @@ def test_map_orswot_chunk_mode_switch(moctx, R1, R2, late):
     res, kw = _run(moctx, d)
     assert int(res.flags.cpu()[0]) == 0
     _same(_got_maps(res, kw, 1)[0], exp)
+
+
+@pytest.mark.parametrize("seed,R,K,M,A", [(71, 40, 3, 40, 100), (72, 30, 2, 70, 64), (73, 24, 2, 6, 300),
+                                           (74, 20, 2, 130, 70), (75, 12, 2, 3, 1024)])
+def test_map_orswot_wide_shapes(gpu_ctx, seed, R, K, M, A):
+    """Past the register kernel's limits (A > 64 actors: 2 / 8 / 16 words per lane; M > 32 members,
+    past 64: multi-word nested member masks), op-replay folds with deferred removes at both levels."""
+    maps = O.map_orswot_objects(R, K, M, A, seed=seed, steps=8 * R, p_vrm=0.4)
+    exp = O.map_fold_objects(maps)
+    d = O.map_orswot_to_dense(maps, K, M, A)
+    res, kw = _run(gpu_ctx, d)
+    assert int(res.flags.cpu()[0]) == 0
+    _same(_got_maps(res, kw, 1)[0], exp)
+
+
+def test_map_orswot_wide_grouped_arbitrary(gpu_ctx):
+    """Arbitrary states at A = 96 in 3 groups of one launch (the group offsets of every row, the value
+    CSR spanning the groups, the Map pool's CSR offsets) through the wide kernel."""
+    rng = np.random.default_rng(77)
+    G, R, K, M, A = 3, 16, 3, 4, 96
+    parts = [_arbitrary(rng, R, K, M, A, 3) for _ in range(G)]
+    exps = [O.map_fold_objects(p) for p in parts]
+    if any(len(e.val.deferred) > cg.map.VD_CAP for x in exps for e in x.entries.values()):
+        pytest.skip("nested deferred past the kernel's capacity")
+    d = O.map_orswot_to_dense([m for p in parts for m in p], K, M, A)
+    d["def_row"] = d["def_row"] % R  # (rows within the group)
+    off = [0]
+    for p in parts:
+        off.append(off[-1] + sum(len(m.deferred) for m in p))
+    res, kw = _run(gpu_ctx, d, G=G, off=off)
+    for g, got in enumerate(_got_maps(res, kw, G)):
+        _same(got, exps[g])
