@@ -103,6 +103,8 @@ struct Tune {
   int map_counter_depth = 8;   // Map<K, counter> fold: register-ring depth at A <= 64 (4, 8, 16; 16: 4.86 vs 4.33 ms)
   int map_counter_kpw = 0;     // Map<K, counter> fold: keys per wave (1, 2, 4; A <= 64 / KPW; 0: automatic)
   int map_counter_cs = 1;      // Map<K, counter> fold: whole-chunk skip (A = 8, 16, 32; one key per wave)
+  int map_counter_cl = 0;      // ... its chunks staged in LDS by LDS-DMA (opt-in: 2.24 vs 2.07 ms in registers,
+                               //     profiles/r05_map_counter_cl_ab.log; the fold is issue-bound per wave)
   int map_orswot_cs = 0;       // Map<K, Orswot> fold: whole-chunk skip (A = 8, 16, 32; M <= 4; opt-in: the kernel
                                //     takes as long as its slowest key, and on the config-4 generator's replicas
                                //     some keys change in most chunks, profiles/r05_map_orswot_chunk_ab.log)

@@ -236,6 +236,7 @@ static void apply_tune(crdt_ctx *ctx, const char *t) {
       else if (k == "mcdep") ctx->tune.map_counter_depth = v >= 16 ? 16 : (v <= 4 ? 4 : 8);
       else if (k == "mckpw") ctx->tune.map_counter_kpw = v >= 4 ? 4 : (v >= 2 ? 2 : (v == 1 ? 1 : 0));
       else if (k == "mccs") ctx->tune.map_counter_cs = v ? 1 : 0;
+      else if (k == "mccl") ctx->tune.map_counter_cl = v ? 1 : 0;
       else if (k == "mocs") ctx->tune.map_orswot_cs = v ? 1 : 0;
       else if (k == "mowide") ctx->tune.map_orswot_wide = v ? 1 : 0;
       else if (k == "mcdma") ctx->tune.map_counter_dma = v >= 16 ? 16 : (v > 0 ? 8 : 0);

@@ -73,9 +73,21 @@ __device__ __forceinline__ bool mc_nz(const u64 (&x)[APL], u64 hm) {
 // key kb + h of the group, so a 32-actor key no longer leaves half the wave idle.  The group's
 // clock C and a remove's liveness (!(rm <= C)) are the same for every key of the group, so the
 // keys share one walk of the remove pool; each entry carries which of the wave's keys it names.
+// LDS-staged chunk skip (SPL > 0, CL): chunks of kMcClS steps, each step an image [ec | val_0..W-1 |
+// clock] of (2 + W) * A words, moved by 1-KiB global_load_lds pieces into kMcClNB slots per wave.
+constexpr int kMcClS = 8, kMcClNB = 4;
+template <int W, int SPL>
+__host__ __device__ constexpr int mc_cl_pieces() {
+  return SPL > 0 ? (kMcClS * (2 + W) * (kWave / (SPL > 0 ? SPL : 1)) + 127) / 128 : 0;
+}
+template <int W, int SPL>
+__host__ __device__ constexpr unsigned long long mc_cl_words() {
+  return (unsigned long long)kMcClNB * mc_cl_pieces<W, SPL>() * 128;
+}
+
 // SPL > 0 (A == 64 / SPL: 32, 16 or 8 actors; one key per wave, register rows): the whole-chunk
 // skip below, with lane l holding actor l % A in every register of the key's state.
-template <int APL, int W, int RING, int KPW, int DEP = 8, int SPL = 0>
+template <int APL, int W, int RING, int KPW, int DEP = 8, int SPL = 0, int CL = 0>
 __global__ __launch_bounds__(kMcWaves * kWave) void map_counter_fold_kernel(MapCounterPlan p) {
   constexpr bool DMA = RING > 0;
   constexpr int kMcRing = DMA ? RING : 1;
@@ -84,7 +96,8 @@ __global__ __launch_bounds__(kMcWaves * kWave) void map_counter_fold_kernel(MapC
                                                    // unrolled body's size)
   static_assert(KPW == 1 || (APL == 1 && !DMA), "several keys per wave: APL 1, register ring");
   static_assert(SPL == 0 || (APL == 1 && KPW == 1 && !DMA), "chunk skip: one key per wave, APL 1, register rows");
-  constexpr int NROW = kMcRowsB / (8 * kWave * APL);  // live rm rows cached in LDS
+  // live rm rows cached in LDS (the LDS-staged chunk skip keeps 4: its chunk slots take the room)
+  constexpr int NROW = (SPL > 0 && CL) ? 4 : kMcRowsB / (8 * kWave * APL);
   constexpr int HL = kWave / KPW;                     // lanes per key
   extern __shared__ u64 lds[];
   const int lane = (int)(threadIdx.x % kWave), wv = (int)(threadIdx.x / kWave);
@@ -107,6 +120,8 @@ __global__ __launch_bounds__(kMcWaves * kWave) void map_counter_fold_kernel(MapC
   // which of the wave's keys each gathered / live remove names (bit h)
   uint8_t *lmask = reinterpret_cast<uint8_t *>(lds + kMcWaves * WQ) + wv * (kMcList + kMcLive);
   uint8_t *lvm = lmask + kMcList;
+  // (SPL > 0, CL: the wave's LDS chunk slots, after every wave's lists; 16-byte aligned)
+  u64 *cslots = lds + kMcWaves * WQ + (kMcWaves * (kMcList + kMcLive)) / 8 + (unsigned long long)wv * mc_cl_words<W, SPL>();
 
   // Loads are never EXEC-masked: lanes past A read the row's last word (a masked load puts the wait
   // counter's bookkeeping on branches, and the compiler then drains every outstanding load — the
@@ -350,7 +365,157 @@ __global__ __launch_bounds__(kMcWaves * kWave) void map_counter_fold_kernel(MapC
     for (int j = 0; j < APL; ++j) C[j] = C[j] > c2[j] ? C[j] : c2[j];
     liveness(chg);
   };
-  if constexpr (SPL > 0) {
+  if constexpr (SPL > 0 && CL) {
+    // ---- whole-chunk skip, LDS-staged (round 5, opt-in: CRDT_TUNE mccl=1).  The test and the
+    // per-step verdicts are the register path's below; the chunks come by LDS-DMA instead of into
+    // registers.  A register still pending at the chunk loop's back-edge makes the compiler drain
+    // every load there (vmcnt(0)), so the register path keeps about one chunk in flight; LDS-DMA
+    // writes no register, and the fold waits for a chunk with a counted vmcnt, keeping
+    // kMcClNB - 1 chunks in flight.  Measured slower all the same (profiles/r05_map_counter_cl_ab.log).
+    constexpr int S = kMcClS, NE = S / SPL, NB = kMcClNB, P = mc_cl_pieces<W, SPL>();
+    constexpr unsigned long long AA = kWave / SPL;      // == A
+    constexpr unsigned long long IMG = (2 + W) * AA;    // words per step image
+    const int hh = lane / (int)AA;
+    const unsigned a = (unsigned)lane & (unsigned)(AA - 1);
+    const unsigned long long nch = (R + S - 1) / S;
+    // lane l's 16-byte piece j: image word o = j*128 + 2l of the chunk, i.e. step o / IMG, row
+    // (o % IMG) / A (0: ec, 1..W: val, 1+W: clock), actors (o % A, +1); source row bases as values
+    // (a per-lane choice between struct fields would be lowered as a dynamic-offset load)
+    const unsigned long long be = (unsigned long long)(p.ec + g * p.e_gs + k * AA),
+                             bv = (unsigned long long)(p.val + g * p.v_gs + k * W * AA),
+                             bcl = (unsigned long long)(p.clock + g * p.c_gs);
+    const unsigned long long se = (unsigned long long)p.e_rs * 8, sv = (unsigned long long)p.v_rs * 8,
+                             sc = (unsigned long long)p.c_rs * 8;
+    unsigned long long pb[P], ps[P];
+    unsigned pst[P];
+    bool pon[P];
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+      const unsigned long long o = (unsigned long long)j * 128 + 2ull * lane;
+      const unsigned long long st = o / IMG, q = o % IMG, row = q / AA, col = q % AA;
+      pon[j] = o < (unsigned long long)S * IMG;
+      pst[j] = (unsigned)st;
+      pb[j] = row == 0 ? be + col * 8 : (row <= W ? bv + ((row - 1) * AA + col) * 8 : bcl + col * 8);
+      ps[j] = row == 0 ? se : (row <= W ? sv : sc);
+    }
+    auto issue = [&](auto B, unsigned long long c) {  // chunk c into slot B (past R: row R-1 again)
+      constexpr int b = decltype(B)::value;
+      u64 *slot = cslots + (unsigned long long)b * P * 128;
+#pragma unroll
+      for (int j = 0; j < P; ++j) {
+        unsigned long long rr = c * S + pst[j];
+        rr = rr < R ? rr : R - 1;
+        if (pon[j]) glds16_mc(reinterpret_cast<const void *>(pb[j] + rr * ps[j]), slot + j * 128);
+      }
+    };
+    auto wait_chunk = [&](unsigned long long c) {  // chunk c has landed: later chunks may be in flight
+      const unsigned long long later = nch - 1 - c < (unsigned long long)(NB - 1) ? nch - 1 - c : NB - 1;
+      if (later >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * P > 63 ? 63 : 3 * P) : "memory");
+      else if (later == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * P) : "memory");
+      else if (later == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    };
+    auto test_chunk = [&](const u64 *slot) -> bool {
+      // (every element read first, then one branch-free test: a read inside a short-circuit would
+      // put each on its own EXEC-masked branch with its own wait)
+      u64 qe[NE], qc[NE], qv[W][NE];
+#pragma unroll
+      for (int i = 0; i < NE; ++i) {
+        const u64 *img = slot + (i * SPL + hh) * IMG;
+        qe[i] = img[a];
+        qc[i] = img[(1 + W) * AA + a];
+#pragma unroll
+        for (int w = 0; w < W; ++w) qv[w][i] = img[(1 + w) * AA + a];
+      }
+      const u64 e0 = e[0], C0 = C[0];
+      if (!mc_nz<1>(e, ~0ull)) {
+        u64 okm = ~0ull;
+#pragma unroll
+        for (int i = 0; i < NE; ++i) okm &= __ballot(qe[i] <= C0);
+        return okm == ~0ull;
+      }
+      const u64 em1 = e0 ? e0 - 1 : 0;
+      const u64 TE = e0 ? em1 : ~0ull, TB = C0 > em1 ? C0 : em1;
+      u64 TV = ~0ull;
+      bool vz[W];
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        const u64 vw = v[w][0];
+        vz[w] = vw == 0;
+        const u64 t = vz[w] ? ~0ull : (e0 > vw - 1 ? e0 : vw - 1);
+        TV = t < TV ? t : TV;
+      }
+      const u64 TN = TE < TV ? TE : TV;
+      u64 fail = 0;
+#pragma unroll
+      for (int i = 0; i < NE; ++i) {
+        const u64 e2 = qe[i], c2 = qc[i];
+        const u64 x = e2 > e0 ? e2 : 0;
+        bool cb = ((e2 == e0) | ((c2 <= TE) & (e2 <= TB))) & (e2 <= TV);
+#pragma unroll
+        for (int w = 0; w < W; ++w) cb = cb & (qv[w][i] <= (vz[w] ? x : v[w][0]));
+        const u64 mN = __ballot(e2 != 0), mB = __ballot(cb), mO = __ballot(c2 <= TN);
+#pragma unroll
+        for (int s2 = 0; s2 < SPL; ++s2) {
+          const u64 M = (AA == 64 ? ~0ull : ((1ull << AA) - 1)) << (s2 * AA);
+          const u64 sel = (mN & M) ? mB : mO;
+          fail |= ~sel & M;
+        }
+      }
+      return fail == 0;
+    };
+    auto body = [&](auto B, unsigned long long c) {
+      constexpr int b = decltype(B)::value;
+      if (c >= nch) return;
+      if (c + NB - 1 < nch) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // chunk c-1's slot is read: refill it
+        issue(std::integral_constant<int, (b + NB - 1) % NB>{}, c + NB - 1);
+      }
+      wait_chunk(c);
+      const u64 *slot = cslots + (unsigned long long)b * P * 128;
+      const unsigned long long r0 = c * S;
+      const unsigned long long n = R - r0 < (unsigned long long)S ? R - r0 : S;
+      if (n == S && (unsigned long long)nxt >= r0 + S && test_chunk(slot)) {
+        u64 cm = 0;
+#pragma unroll
+        for (int i = 0; i < NE; ++i) {
+          const u64 c2 = slot[(i * SPL + hh) * IMG + (1 + W) * AA + a];
+          cm = c2 > cm ? c2 : cm;
+        }
+#pragma unroll
+        for (int off = (int)AA; off < kWave; off <<= 1) {
+          const u64 o = __shfl_xor(cm, off);
+          cm = o > cm ? o : cm;
+        }
+        C[0] = C[0] > cm ? C[0] : cm;
+        liveness(false);
+        return;
+      }
+      for (int s2 = 0; s2 < (int)n; ++s2) {  // the chunk's steps, exactly (lane = actor a: its words)
+        const u64 *img = slot + (unsigned long long)s2 * IMG;
+        u64 c2[1], e2[1], v2[W][1];
+        e2[0] = img[a];
+        c2[0] = img[(1 + W) * AA + a];
+#pragma unroll
+        for (int w = 0; w < W; ++w) v2[w][0] = img[(1 + w) * AA + a];
+        step(r0 + s2, c2, e2, v2);
+      }
+    };
+#pragma unroll
+    for (int b = 0; b + 1 < NB; ++b)
+      if ((unsigned long long)b < nch) {
+        if (b == 0) issue(std::integral_constant<int, 0>{}, 0);
+        if (b == 1) issue(std::integral_constant<int, 1>{}, 1);
+        if (b == 2) issue(std::integral_constant<int, 2>{}, 2);
+      }
+    for (unsigned long long c = 0; c < nch; c += NB) {
+      body(std::integral_constant<int, 0>{}, c);
+      body(std::integral_constant<int, 1>{}, c + 1);
+      body(std::integral_constant<int, 2>{}, c + 2);
+      body(std::integral_constant<int, 3>{}, c + 3);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (no piece lands after the wave ends)
+  } else if constexpr (SPL > 0) {
     // ---- whole-chunk skip (round 5).  Almost every replica step of a long fold leaves the key's
     // (entry clock, value) unchanged (config-4 shape: ~7 of 16,384 steps change it), and a step's
     // no-change test needs only the state, not the steps before it, once the state is assumed
@@ -581,17 +746,18 @@ __global__ __launch_bounds__(kMcWaves * kWave) void map_counter_fold_kernel(MapC
   if ((bad || full) && lane == 0) atomicOr(p.o_flags + g, (bad ? 2u : 0u) | (full ? 8u : 0u));
 }
 
-template <int APL, int RING>
+template <int APL, int RING, int W = 1, int SPL = 0, int CL = 0>
 static size_t mc_lds() {
-  return (size_t)kMcWaves * (kMcList * 8 + kMcLive * 4 + (kMcRowsB / (8 * kWave * APL)) * kWave * APL * 8 +
-                             RING * 128 * 8 + kMcList + kMcLive);
+  const size_t nrow = (SPL > 0 && CL) ? 4 : kMcRowsB / (8 * kWave * APL);
+  return (size_t)kMcWaves * (kMcList * 8 + kMcLive * 4 + nrow * kWave * APL * 8 + RING * 128 * 8 + kMcList + kMcLive +
+                             ((SPL > 0 && CL) ? mc_cl_words<W, SPL>() * 8 : 0));
 }
 
-template <int APL, int W, int RING = 0, int KPW = 1, int DEP = 8, int SPL = 0>
+template <int APL, int W, int RING = 0, int KPW = 1, int DEP = 8, int SPL = 0, int CL = 0>
 static hipError_t launch_mc(const MapCounterPlan &p, hipStream_t s) {
   const unsigned long long blocks = (p.G * ((p.K + KPW - 1) / KPW) + kMcWaves - 1) / kMcWaves;
-  const size_t lds = mc_lds<APL, RING>();
-  auto *fn = &map_counter_fold_kernel<APL, W, RING, KPW, DEP, SPL>;
+  const size_t lds = mc_lds<APL, RING, W, SPL, CL>();
+  auto *fn = &map_counter_fold_kernel<APL, W, RING, KPW, DEP, SPL, CL>;
   if (lds > 64 * 1024) {
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(fn),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -676,7 +842,12 @@ extern "C" int crdt_map_counter_lub_many(crdt_ctx *ctx, const crdt_map_counter_b
     const bool al = ((p.c_rs | p.c_gs | p.e_rs | p.e_gs | p.v_rs | p.v_gs) & 1) == 0 &&
                     ((uintptr_t)in->clock & 15) == 0 && ((uintptr_t)in->ec & 15) == 0 && ((uintptr_t)in->val & 15) == 0;
     const int ring = A % 2 == 0 && (2 + W) * A <= 128 && al ? ctx->tune.map_counter_dma : 0;
-    if (spl == 2) he = W == 1 ? launch_mc<1, 1, 0, 1, 8, 2>(p, ctx->stream) : launch_mc<1, 2, 0, 1, 8, 2>(p, ctx->stream);
+    // the LDS-staged chunk skip (opt-in, CRDT_TUNE mccl=1) needs 16-byte aligned rows
+    const bool cl = spl && al && ctx->tune.map_counter_cl;
+    if (cl && spl == 2) he = W == 1 ? launch_mc<1, 1, 0, 1, 8, 2, 1>(p, ctx->stream) : launch_mc<1, 2, 0, 1, 8, 2, 1>(p, ctx->stream);
+    else if (cl && spl == 4) he = W == 1 ? launch_mc<1, 1, 0, 1, 8, 4, 1>(p, ctx->stream) : launch_mc<1, 2, 0, 1, 8, 4, 1>(p, ctx->stream);
+    else if (cl && spl == 8) he = W == 1 ? launch_mc<1, 1, 0, 1, 8, 8, 1>(p, ctx->stream) : launch_mc<1, 2, 0, 1, 8, 8, 1>(p, ctx->stream);
+    else if (spl == 2) he = W == 1 ? launch_mc<1, 1, 0, 1, 8, 2>(p, ctx->stream) : launch_mc<1, 2, 0, 1, 8, 2>(p, ctx->stream);
     else if (spl == 4) he = W == 1 ? launch_mc<1, 1, 0, 1, 8, 4>(p, ctx->stream) : launch_mc<1, 2, 0, 1, 8, 4>(p, ctx->stream);
     else if (spl == 8) he = W == 1 ? launch_mc<1, 1, 0, 1, 8, 8>(p, ctx->stream) : launch_mc<1, 2, 0, 1, 8, 8>(p, ctx->stream);
     else if (!ring && kpw >= 4 && A <= (size_t)kWave / 4)

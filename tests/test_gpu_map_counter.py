@@ -17,13 +17,14 @@ pytestmark = pytest.mark.gpu
 import crdts_gpu as cg  # noqa: E402
 
 
-@pytest.fixture(params=["mckpw=0", "mckpw=1", "mckpw=2", "mckpw=4", "mcdma=8", "mcdma=16", "mccs=0"])
+@pytest.fixture(params=["mckpw=0", "mckpw=1", "mckpw=2", "mckpw=4", "mcdma=8", "mcdma=16", "mccs=0", "mccl=1"])
 def mcctx(request):
-    """The default (A = 32 / 16 / 8: the whole-chunk skip, round 5; otherwise the register ring with
-    keys per wave chosen by the grid size), 1, up to 2 or up to 4 keys per wave (A <= 64 / keys), the
-    replica rows by LDS-DMA into an 8- or 16-slot LDS ring (A even, (2+W)*A <= 128; one key per
-    wave), or the register ring without the chunk skip (mccs=0).  Shapes outside a mode's bound take
-    the one-key register ring."""
+    """The default (A = 32 / 16 / 8: the whole-chunk skip with register-staged chunks, round 5; otherwise
+    the register ring with keys per wave chosen by the grid size), 1, up to 2 or up to 4 keys per
+    wave (A <= 64 / keys), the replica rows by LDS-DMA into an 8- or 16-slot LDS ring (A even,
+    (2+W)*A <= 128; one key per wave), the register ring without the chunk skip (mccs=0), or the
+    chunk skip with LDS-staged chunks (mccl=1, opt-in).  Shapes outside a mode's bound take the one-key
+    register ring."""
     assert torch.cuda.is_available()
     torch.cuda.set_device(0)
     ctx = cg.Context(0)
