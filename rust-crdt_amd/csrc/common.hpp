@@ -97,6 +97,8 @@ struct Tune {
   int apply_fence = 0;         // Orswot / Map apply: a workgroup fence after every op's stores (round-2 form)
   int orswot_apply_pf = 0;     // Orswot apply (16-lane groups): an Rm's clock row loaded during the op before
                                //     (opt-in: 4 VGPRs spill, 990 vs 918 us, profiles/r04_orswot_apply_pf_ab.log)
+  int orswot_apply_stg = 0;    // Orswot apply (16-lane groups): a batch's first 2 Rm clock rows staged in LDS by LDS-DMA
+                               //     (opt-in: 872 vs 854 us, profiles/r05_oapply_stg_ab.log)
   int orswot_apply_hpf = 0;    // Orswot apply (16-lane groups): the next op batch's fields / first members loaded
                                //     while the current batch runs (opt-in: 2 VGPRs spill, 878 vs 856 us, profiles/r04_oapply_hpf_ab.log)
   int map_counter_dma = 0;     // Map<K, counter> fold: LDS-DMA ring slots (8 or 16; 0: register ring, 8.7 vs 9.1 ms)

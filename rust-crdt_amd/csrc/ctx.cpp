@@ -232,6 +232,7 @@ static void apply_tune(crdt_ctx *ctx, const char *t) {
       else if (k == "mpnt") ctx->tune.map_pair_nt = v != 0;
       else if (k == "mppf") ctx->tune.map_pair_pf = v != 0;
       else if (k == "ohpf") ctx->tune.orswot_apply_hpf = v != 0;
+      else if (k == "oastg") ctx->tune.orswot_apply_stg = v != 0;
       else if (k == "oapf") ctx->tune.orswot_apply_pf = v != 0;
       else if (k == "mcdep") ctx->tune.map_counter_depth = v >= 16 ? 16 : (v <= 4 ? 4 : 8);
       else if (k == "mckpw") ctx->tune.map_counter_kpw = v >= 4 ? 4 : (v >= 2 ? 2 : (v == 1 ? 1 : 0));

@@ -423,6 +423,9 @@ __global__ __launch_bounds__(kBlock) void orswot_apply_kernel_a1024(OrswotApplyP
 //  * identical clocks (HashMap keyed by VClock): the witness is a function of the clock (at the
 //    current C), so a Rm's clock is compared in full only with slots of the same witness.
 // Exact for ANY input state (the first Add re-forgets every input slot's members in full).
+__device__ __forceinline__ void glds16_oa(const void *g, u64 *lds) {
+  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void *)lds, 16, 0, 0);
+}
 constexpr int kG = grp::kG;            // lanes per state (group.hpp)
 constexpr unsigned kGMask = grp::kMask;
 constexpr int kJ = kWave / kG;         // actors per lane (A <= 64)
@@ -460,7 +463,15 @@ __device__ __forceinline__ void grp_forget_row(u64 *row, const u64 (&r)[kJ], int
 // first member / actor / counter, then a one-member Add's cell).  With HPF the next batch's kinds
 // and member ranges are loaded at this batch's start and its first members at the middle op, so a
 // batch boundary costs two round trips (actor / counter, then the cell).
-template <bool RPF, bool HPF>
+// STG (round 5, opt-in: measured 2% slower, profiles/r05_oapply_stg_ab.log — the batch start's added
+// wait costs more than the Rm round trips it removes): the clock rows of a batch's first STG Rm ops
+// are moved into LDS by LDS-DMA with the
+// batch's headers (issued before the one-member Adds' cell loads, whose wait then covers them), and
+// an Rm reads its clock there: no dependent HBM round trip, no registers held across ops.  A DMA
+// piece puts lane l's 16 bytes at byte 16 l of a 1-KiB block, so a group's 16 lanes fill its own
+// quarter of each block: half a row (32 words) per block, 2 STG blocks per batch (A even, rm_clock
+// 16-byte aligned; otherwise STG = 0).
+template <bool RPF, bool HPF, int STG = 0>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRDT_GRP_WPE))) void orswot_apply_grp_kernel(
     OrswotApplyPlan p) {
   extern __shared__ u64 lds[];
@@ -468,9 +479,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRDT_GRP
   const unsigned long long s = ((unsigned long long)blockIdx.x * kBlock + threadIdx.x) / kG;
   if (s >= p.N) return;  // (whole groups)
   const unsigned long long A = p.A, M = p.M, Mw = p.Mw, Dcap = p.Dcap;
-  // LDS: per group the kG op headers of the current batch (32 bytes each), then the slot witnesses
+  // LDS: per group the kG op headers of the current batch (32 bytes each), then the slot witnesses,
+  // then (STG) per wave 2 STG blocks of 128 words, group q's words at 32 q .. 32 q + 31 of each
   u64 *hdr = lds + (threadIdx.x / kG) * (4 * kG);
   uint8_t *wit = reinterpret_cast<uint8_t *>(lds + (kBlock / kG) * 4 * kG) + (threadIdx.x / kG) * Dcap;
+  u64 *stg = lds + (kBlock / kG) * 4 * kG + ((kBlock / kG) * Dcap + 15) / 16 * 2 + (threadIdx.x / kWave) * (2 * STG * 128);
+  const unsigned gw32 = (unsigned)(lane / kG) * 32;  // the group's quarter of a block
   const bool lead = g == 0;
 
   const unsigned long long ob = p.op_off[s], oe = p.op_off[s + 1];
@@ -590,6 +604,24 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRDT_GRP
       }
     }
     const int nb = (int)((oe - base) < (unsigned long long)kG ? (oe - base) : kG);
+    unsigned rmask = 0;  // (STG) the batch's valid Rm ops, bit i = op base + i (group-uniform)
+    if constexpr (STG > 0) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the last batch's staged rows are read
+      rmask = grp_bits(__ballot(h_ka == kRmOp && h_cr < p.n_rm_rows), lane);
+      unsigned m = rmask;
+#pragma unroll
+      for (int t = 0; t < STG; ++t) {
+        const int pos = m ? __builtin_ctz(m) : 0;
+        const u64 rr = __shfl(h_cr, gb | pos);  // the t-th Rm's rm row
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const unsigned long long w = 32ull * h + 2ull * g;
+          if (m && w < A) glds16_oa(p.rm_clock + rr * A + w, stg + (2 * t + h) * 128);
+        }
+        m &= m ? m - 1 : 0u;
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the rows (and the cells before them) landed
+    }
     *reinterpret_cast<u64x2 *>(hdr + 4 * g) = u64x2{((u64)h_m0 << 32) | h_ka, ((u64)h_me << 32) | h_mb};
     *reinterpret_cast<u64x2 *>(hdr + 4 * g + 2) = u64x2{h_cr, h_cell};
     unsigned stale = 0;
@@ -740,7 +772,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRDT_GRP
           continue;
         }
         u64 r[kJ];
-        if (RPF) {
+        const unsigned rank = STG > 0 ? (unsigned)__builtin_popcount(rmask & ((1u << i) - 1)) : 0u;
+        if (STG > 0 && rank < (unsigned)STG) {  // staged with the batch (rmask bit i is set: a valid Rm)
+#pragma unroll
+          for (int j = 0; j < kJ; ++j) {
+            const unsigned a = g + kG * j;
+            r[j] = a < A ? stg[(2 * rank + (a >> 5)) * 128 + gw32 + (a & 31)] : 0ull;
+          }
+        } else if (RPF) {
 #pragma unroll
           for (int j = 0; j < kJ; ++j) r[j] = rcur[j];
         } else {
@@ -863,9 +902,14 @@ extern "C" int crdt_orswot_apply_batch(crdt_ctx *ctx, const crdt_orswot_states *
     timing_begin(ctx, "orswot_apply");
     const unsigned long long per_block = kBlock / kG;
     const dim3 grid((unsigned)((s.N + per_block - 1) / per_block));
-    const size_t lds = per_block * (4 * kG * 8 + s.Dcap);
     const bool rpf = ctx->tune.orswot_apply_pf, hpf = ctx->tune.orswot_apply_hpf;
-    if (rpf && hpf) hipLaunchKernelGGL((orswot_apply_grp_kernel<true, true>), grid, dim3(kBlock), lds, ctx->stream, p);
+    // STG: the batch's first 2 Rm clock rows by LDS-DMA (opt-in, CRDT_TUNE oastg=1)
+    const bool stg = ctx->tune.orswot_apply_stg && !rpf && !hpf && s.A % 2 == 0 && ops->rm_clock &&
+                     ((uintptr_t)ops->rm_clock & 15) == 0;
+    const size_t lds = per_block * 4 * kG * 8 + (per_block * s.Dcap + 15) / 16 * 16 +
+                       (stg ? (kBlock / kWave) * 2 * 2 * 128 * 8 : 0);
+    if (stg) hipLaunchKernelGGL((orswot_apply_grp_kernel<false, false, 2>), grid, dim3(kBlock), lds, ctx->stream, p);
+    else if (rpf && hpf) hipLaunchKernelGGL((orswot_apply_grp_kernel<true, true>), grid, dim3(kBlock), lds, ctx->stream, p);
     else if (rpf) hipLaunchKernelGGL((orswot_apply_grp_kernel<true, false>), grid, dim3(kBlock), lds, ctx->stream, p);
     else if (hpf) hipLaunchKernelGGL((orswot_apply_grp_kernel<false, true>), grid, dim3(kBlock), lds, ctx->stream, p);
     else hipLaunchKernelGGL((orswot_apply_grp_kernel<false, false>), grid, dim3(kBlock), lds, ctx->stream, p);
