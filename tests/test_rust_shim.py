@@ -137,6 +137,9 @@ def test_capacity_constants_match_the_header():
     assert "Limits: A <= 1024, 1 <= V <= 16" in hdr and int(consts["MAP_MAX_ACTORS"]) == 1024
     assert "Dcap is not bounded" in hdr and consts["MERGE_MAX_DEFERRED"] == "usize::MAX"
     assert "Dcap(self) + Dcap(other) <= 512" not in hdr
+    # round 5: Map<K, Orswot> past A = 64 / M = 32 by the wide kernel
+    assert "Limits: A <= 1,024, M <= 1,024" in hdr
+    assert int(consts["MAP_ORSWOT_MAX_ACTORS"]) == 1024 and int(consts["MAP_ORSWOT_MAX_MEMBERS"]) == 1024
     # the Map paths check their inputs against these constants, not literals
     assert "vmax.min(4)" not in MOD and "d.vmax > 4" not in MOD
     assert MOD.count("MAP_MAX_VALUES") >= 3 and MOD.count("MERGE_MAX_DEFERRED") >= 3
