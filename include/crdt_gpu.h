@@ -586,7 +586,7 @@ int crdt_map_lub_many_sharded_doff(crdt_ctx *ctx, const crdt_map_batch *in, cons
  * Output per group g (packed): clock[g*A + a], ec[(g*K + k)*A + a], val[((g*K + k)*W + w)*A + a],
  * flags[g] (required): bit 1 = def_row not non-decreasing or >= R, bit 3 = more than 512 live
  * removes named one key (results of the group unreliable); def_keep / def_keys as crdt_map_out.
- * Limits: A <= 512.  Device-memory contexts only. */
+ * Limits: A <= 512.  Device and host memory (crdt_mem_kind; round 5). */
 typedef struct crdt_map_counter_batch {
   size_t G, R, K, A, W;
   const uint64_t *clock;
@@ -611,6 +611,14 @@ typedef struct crdt_map_counter_out {
 } crdt_map_counter_out;
 
 int crdt_map_counter_lub_many(crdt_ctx *ctx, const crdt_map_counter_batch *in, crdt_map_counter_out *out);
+/* Map<K, GCounter / PNCounter> sharded by KEYS (round 5), as crdt_map_lub_many_sharded: rank k holds keys
+ * [k0, k0 + in->K) of every replica (the layout above with K = its key count), every replica's
+ * clock and the group's whole deferred list with key bitmaps over all K keys (def_keys
+ * [D][ceil(K/64)]); its fold of its keys is the exact left fold (no data-path collective).  out holds
+ * the rank's keys, flags ORed over the ranks, and out->def_keys [D][ceil(K/64)] the surviving removes'
+ * key sets over ALL keys (one ncclAllReduce(ncclSum): disjoint ranges).  Device memory only. */
+int crdt_map_counter_lub_many_sharded(crdt_ctx *ctx, const crdt_map_counter_batch *in, size_t k0, size_t K,
+                                      crdt_map_counter_out *out);
 
 /* ---- Map<K, Orswot<M, A>, A> (round 4) ----------------------------------------------------------
  * Map::merge (map.rs:140-220) with a nested Orswot value (orswot.rs:81-149 merge, :150-183 forget)
@@ -662,6 +670,14 @@ typedef struct crdt_map_orswot_out {
 } crdt_map_orswot_out;
 
 int crdt_map_orswot_lub_many(crdt_ctx *ctx, const crdt_map_orswot_batch *in, crdt_map_orswot_out *out);
+/* Map<K, Orswot> sharded by KEYS (round 5), as crdt_map_lub_many_sharded: rank k holds keys
+ * [k0, k0 + in->K) of every replica (the layout above with K = its key count; the nested removes' CSR over the rank's (g, r, k)), every replica's
+ * clock and the group's whole deferred list with key bitmaps over all K keys (def_keys
+ * [D][ceil(K/64)]); its fold of its keys is the exact left fold (no data-path collective).  out holds
+ * the rank's keys, flags ORed over the ranks, and out->def_keys [D][ceil(K/64)] the surviving removes'
+ * key sets over ALL keys (one ncclAllReduce(ncclSum): disjoint ranges).  Device memory only. */
+int crdt_map_orswot_lub_many_sharded(crdt_ctx *ctx, const crdt_map_orswot_batch *in, size_t k0, size_t K,
+                                     crdt_map_orswot_out *out);
 
 /* ---- Map<K, Map<K2, MVReg<u64, A>, A>, A> (round 5) -----------------------------------------------
  * The nested type of the reference's own Map tests (TMap, test/map.rs:10; TestMap, map.rs:359):
@@ -685,7 +701,7 @@ int crdt_map_orswot_lub_many(crdt_ctx *ctx, const crdt_map_orswot_batch *in, crd
  *   8 values — results of the group unreliable; def_keep / def_keys as crdt_map_out.
  * Map::forget collects the inner deferred removes into a new map: two whose clocks become equal keep
  * one entry with the later one's keys (the oracle's dict order; the reference's is unspecified).
- * Limits: A <= 64, K2 <= 64, V <= 8.  Device-memory contexts only. */
+ * Limits: A <= 64, K2 <= 64, V <= 8.  Device and host memory (crdt_mem_kind). */
 typedef struct crdt_map_nested_batch {
   size_t G, R, K, K2, V, A;
   const uint64_t *clock, *ec, *ic, *iec, *ivc, *ivv;
@@ -716,6 +732,14 @@ typedef struct crdt_map_nested_out {
 } crdt_map_nested_out;
 
 int crdt_map_nested_lub_many(crdt_ctx *ctx, const crdt_map_nested_batch *in, crdt_map_nested_out *out);
+/* Map<K, Map<K2, MVReg>> sharded by KEYS (round 5), as crdt_map_lub_many_sharded: rank k holds keys
+ * [k0, k0 + in->K) of every replica (the layout above with K = its key count; the inner removes' CSR over the rank's (g, r, k)), every replica's
+ * clock and the group's whole deferred list with key bitmaps over all K keys (def_keys
+ * [D][ceil(K/64)]); its fold of its keys is the exact left fold (no data-path collective).  out holds
+ * the rank's keys, flags ORed over the ranks, and out->def_keys [D][ceil(K/64)] the surviving removes'
+ * key sets over ALL keys (one ncclAllReduce(ncclSum): disjoint ranges).  Device memory only. */
+int crdt_map_nested_lub_many_sharded(crdt_ctx *ctx, const crdt_map_nested_batch *in, size_t k0, size_t K,
+                                     crdt_map_nested_out *out);
 
 /* ---- MVReg<u64, A> on its own (outside a Map) ------------------------------------------------
  * Replaces MVReg::merge (mvreg.rs:112-128) and MVReg::apply (mvreg.rs:130-166) for registers in the

@@ -53,7 +53,8 @@ EXPORTS = (
     "crdt_mvreg_lub_many", "crdt_mvreg_merge_batch", "crdt_mvreg_apply_batch",
     "crdt_orswot_lub_many_doff", "crdt_map_lub_many_doff",
     "crdt_orswot_lub_many_sharded_doff", "crdt_map_lub_many_sharded_doff", "crdt_map_counter_lub_many", "crdt_map_orswot_lub_many",
-    "crdt_map_nested_lub_many",
+    "crdt_map_nested_lub_many", "crdt_map_counter_lub_many_sharded", "crdt_map_orswot_lub_many_sharded",
+    "crdt_map_nested_lub_many_sharded",
 )
 
 
@@ -268,6 +269,12 @@ _SIGS.update({
     "crdt_map_counter_lub_many": ([P, ctypes.POINTER(MapCounterBatch), ctypes.POINTER(MapCounterOut)], ctypes.c_int),
     "crdt_map_orswot_lub_many": ([P, ctypes.POINTER(MapOrswotBatch), ctypes.POINTER(MapOrswotOut)], ctypes.c_int),
     "crdt_map_nested_lub_many": ([P, ctypes.POINTER(MapNestedBatch), ctypes.POINTER(MapNestedOut)], ctypes.c_int),
+    "crdt_map_counter_lub_many_sharded": ([P, ctypes.POINTER(MapCounterBatch), S, S, ctypes.POINTER(MapCounterOut)],
+                                          ctypes.c_int),
+    "crdt_map_orswot_lub_many_sharded": ([P, ctypes.POINTER(MapOrswotBatch), S, S, ctypes.POINTER(MapOrswotOut)],
+                                         ctypes.c_int),
+    "crdt_map_nested_lub_many_sharded": ([P, ctypes.POINTER(MapNestedBatch), S, S, ctypes.POINTER(MapNestedOut)],
+                                         ctypes.c_int),
     "crdt_vclock_ingest": ([P, P, P, S, P, S, P, S, P], ctypes.c_int),
     "crdt_pncounter_ingest": ([P, P, P, S, P, S, P, S, P], ctypes.c_int),
     "crdt_gset_ingest": ([P, P, P, S, P, S, P, S, P], ctypes.c_int),

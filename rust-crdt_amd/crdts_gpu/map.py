@@ -426,7 +426,7 @@ class MapCounterLub(NamedTuple):
 def counter_lub_many(clock: torch.Tensor, ec: torch.Tensor, val: torch.Tensor, def_off=None,
                      def_row: Optional[torch.Tensor] = None, def_clock: Optional[torch.Tensor] = None,
                      def_keys: Optional[torch.Tensor] = None, ctx: Optional[Context] = None,
-                     check: bool = True) -> MapCounterLub:
+                     check: bool = True, _key_shard: Optional[tuple] = None) -> MapCounterLub:
     """The exact left fold of Map::merge (map.rs:140-220) for Map<K, GCounter> (val (G,R,K,1,A)) or
     Map<K, PNCounter> (val (G,R,K,2,A): P then N) — gcounter.rs:44-54 / pncounter.rs:70-82 as the
     value's merge and forget.  clock (G,R,A) / (R,A), ec (G,R,K,A) / (R,K,A), val likewise; the
@@ -449,7 +449,7 @@ def counter_lub_many(clock: torch.Tensor, ec: torch.Tensor, val: torch.Tensor, d
     for t, nm, inner in ((c, "clock", (1,)), (e, "ec", (A, 1)), (v, "val", (W * A, A, 1))):
         if t.numel() and tuple(t.stride()[2:]) != inner:
             raise ValueError(f"map.counter_lub_many: {nm} must be packed within a replica")
-    Kw = (K + 63) // 64
+    Kw = (K + 63) // 64 if _key_shard is None else (int(_key_shard[1]) + 63) // 64
     dev = clock.device
     out_clock = torch.empty((G, A), dtype=torch.int64, device=dev)
     out_ec = torch.empty((G, K, A), dtype=torch.int64, device=dev)
@@ -484,7 +484,11 @@ def counter_lub_many(clock: torch.Tensor, ec: torch.Tensor, val: torch.Tensor, d
             keep = torch.empty(D, dtype=torch.uint8, device=dev)
             keys_out = torch.empty((D, Kw), dtype=torch.int64, device=dev)
             o.def_keep, o.def_keys = keep.data_ptr(), keys_out.data_ptr()
-    ctx.call("crdt_map_counter_lub_many", ctypes.byref(b), ctypes.byref(o))
+    if _key_shard is None:
+        ctx.call("crdt_map_counter_lub_many", ctypes.byref(b), ctypes.byref(o))
+    else:  # (shard.map_counter_lub_many_sharded: this rank's keys of a key-sharded fold)
+        ctx.call("crdt_map_counter_lub_many_sharded", ctypes.byref(b), int(_key_shard[0]), int(_key_shard[1]),
+                 ctypes.byref(o))
     if check:
         f = 0
         for x in flags.cpu().numpy().tolist():
@@ -519,7 +523,8 @@ def orswot_lub_many(clock: torch.Tensor, ec: torch.Tensor, oc: torch.Tensor, ent
                     vd_off: torch.Tensor, vd_clock: Optional[torch.Tensor] = None,
                     vd_mem: Optional[torch.Tensor] = None, def_off=None, def_row: Optional[torch.Tensor] = None,
                     def_clock: Optional[torch.Tensor] = None, def_keys: Optional[torch.Tensor] = None,
-                    ctx: Optional[Context] = None, check: bool = True) -> MapOrswotLub:
+                    ctx: Optional[Context] = None, check: bool = True,
+                    _key_shard: Optional[tuple] = None) -> MapOrswotLub:
     """The exact left fold of Map::merge (map.rs:140-220) for Map<K, Orswot<M>> — orswot.rs:81-149 as
     the value's merge, :150-183 as its forget.  clock (G,R,A) / (R,A), ec and oc (G,R,K,A), ent
     (G,R,K,M,A), all contiguous; the nested deferred removes as a device CSR over (g, r, k): vd_off
@@ -555,7 +560,7 @@ def orswot_lub_many(clock: torch.Tensor, ec: torch.Tensor, oc: torch.Tensor, ent
             if t is None or not t.is_contiguous() or tuple(t.shape) not in (shape, (Dv, 1) if Mw == 1 else shape):
                 raise ValueError(f"map.orswot_lub_many: {nm} must be a contiguous {shape} tensor")
             ctx.check_tensor(t, f"map.orswot_lub_many({nm})")
-    Kw = (K + 63) // 64
+    Kw = (K + 63) // 64 if _key_shard is None else (int(_key_shard[1]) + 63) // 64
     out = [torch.empty(sh, dtype=torch.int64, device=dev)
            for sh in ((G, A), (G, K, A), (G, K, A), (G, K, M, A), (G, K, VD_CAP, A),
                       (G, K, VD_CAP) if Mw == 1 else (G, K, VD_CAP, Mw))]
@@ -592,7 +597,11 @@ def orswot_lub_many(clock: torch.Tensor, ec: torch.Tensor, oc: torch.Tensor, ent
             keep = torch.empty(D, dtype=torch.uint8, device=dev)
             keys_out = torch.empty((D, Kw), dtype=torch.int64, device=dev)
             ob.def_keep, ob.def_keys = keep.data_ptr(), keys_out.data_ptr()
-    ctx.call("crdt_map_orswot_lub_many", ctypes.byref(b), ctypes.byref(ob))
+    if _key_shard is None:
+        ctx.call("crdt_map_orswot_lub_many", ctypes.byref(b), ctypes.byref(ob))
+    else:  # (shard.map_orswot_lub_many_sharded)
+        ctx.call("crdt_map_orswot_lub_many_sharded", ctypes.byref(b), int(_key_shard[0]), int(_key_shard[1]),
+                 ctypes.byref(ob))
     if check:
         f = 0
         for x in flags.cpu().numpy().tolist():
@@ -637,7 +646,8 @@ def nested_lub_many(clock: torch.Tensor, ec: torch.Tensor, ic: torch.Tensor, iec
                     ivv: torch.Tensor, id_off: torch.Tensor, id_clock: Optional[torch.Tensor] = None,
                     id_keys: Optional[torch.Tensor] = None, def_off=None, def_row: Optional[torch.Tensor] = None,
                     def_clock: Optional[torch.Tensor] = None, def_keys: Optional[torch.Tensor] = None,
-                    ctx: Optional[Context] = None, check: bool = True) -> MapNestedLub:
+                    ctx: Optional[Context] = None, check: bool = True,
+                    _key_shard: Optional[tuple] = None) -> MapNestedLub:
     """The exact left fold of Map::merge (map.rs:140-220) for Map<K, Map<K2, MVReg<u64>>> — the type of
     the reference's own Map tests (test/map.rs:10) — with the inner Map's merge (map.rs:140-220,
     mvreg.rs:112-128) and forget (map.rs:85-114) as the value's.  clock (G,R,A) / (R,A); ec, ic
@@ -673,7 +683,7 @@ def nested_lub_many(clock: torch.Tensor, ec: torch.Tensor, ic: torch.Tensor, iec
             if t is None or not t.is_contiguous() or tuple(t.shape) != shape:
                 raise ValueError(f"map.nested_lub_many: {nm} must be a contiguous {shape} tensor")
             ctx.check_tensor(t, f"map.nested_lub_many({nm})")
-    Kw = (K + 63) // 64
+    Kw = (K + 63) // 64 if _key_shard is None else (int(_key_shard[1]) + 63) // 64
     out = [torch.empty(sh, dtype=torch.int64, device=dev)
            for sh in ((G, A), (G, K, A), (G, K, A), (G, K, K2, A), (G, K, K2, NM_VS, A), (G, K, K2, NM_VS),
                       (G, K, NM_ID, A), (G, K, NM_ID))]
@@ -711,7 +721,11 @@ def nested_lub_many(clock: torch.Tensor, ec: torch.Tensor, ic: torch.Tensor, iec
             keep = torch.empty(D, dtype=torch.uint8, device=dev)
             keys_out = torch.empty((D, Kw), dtype=torch.int64, device=dev)
             ob.def_keep, ob.def_keys = keep.data_ptr(), keys_out.data_ptr()
-    ctx.call("crdt_map_nested_lub_many", ctypes.byref(b), ctypes.byref(ob))
+    if _key_shard is None:
+        ctx.call("crdt_map_nested_lub_many", ctypes.byref(b), ctypes.byref(ob))
+    else:  # (shard.map_nested_lub_many_sharded)
+        ctx.call("crdt_map_nested_lub_many_sharded", ctypes.byref(b), int(_key_shard[0]), int(_key_shard[1]),
+                 ctypes.byref(ob))
     if check:
         f = 0
         for x in flags.cpu().numpy().tolist():

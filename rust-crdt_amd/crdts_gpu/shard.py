@@ -271,3 +271,41 @@ def map_lub_many_sharded(clock: torch.Tensor, ec: torch.Tensor, vclk: torch.Tens
     return cmap.lub_many(clock, ec, vclk, vval, def_off=def_off, def_row=def_row, def_clock=def_clock,
                          def_keys=def_keys, vout=vout, ctx=ctx, vstate=vstate,
                          _key_shard=(int(k0), int(K)))
+
+
+def map_counter_lub_many_sharded(clock: torch.Tensor, ec: torch.Tensor, val: torch.Tensor, k0: int, K: int,
+                                 def_off=None, def_row=None, def_clock=None, def_keys=None,
+                                 ctx: Optional[Context] = None, check: bool = True):
+    """Key-sharded Map<K, GCounter / PNCounter> fold (crdt_map_counter_lub_many_sharded, round 5):
+    this rank's keys [k0, k0 + K_k) of every replica (ec (G, R, K_k, A), val (G, R, K_k, W, A)), every
+    replica clock, the whole deferred list with key bitmaps over all K keys.  Returns a
+    map.MapCounterLub of the rank's keys whose def_keys span all K."""
+    from . import map as cmap
+    return cmap.counter_lub_many(clock, ec, val, def_off=def_off, def_row=def_row, def_clock=def_clock,
+                                 def_keys=def_keys, ctx=ctx, check=check, _key_shard=(int(k0), int(K)))
+
+
+def map_orswot_lub_many_sharded(clock: torch.Tensor, ec: torch.Tensor, oc: torch.Tensor, ent: torch.Tensor,
+                                vd_off: torch.Tensor, k0: int, K: int, vd_clock=None, vd_mem=None, def_off=None,
+                                def_row=None, def_clock=None, def_keys=None, ctx: Optional[Context] = None,
+                                check: bool = True):
+    """Key-sharded Map<K, Orswot> fold (crdt_map_orswot_lub_many_sharded, round 5): this rank's keys
+    (ec / oc (G, R, K_k, A), ent (G, R, K_k, M, A), the nested removes' CSR over (g, r, its keys)),
+    every replica clock, the whole deferred list with key bitmaps over all K keys."""
+    from . import map as cmap
+    return cmap.orswot_lub_many(clock, ec, oc, ent, vd_off, vd_clock=vd_clock, vd_mem=vd_mem, def_off=def_off,
+                                def_row=def_row, def_clock=def_clock, def_keys=def_keys, ctx=ctx, check=check,
+                                _key_shard=(int(k0), int(K)))
+
+
+def map_nested_lub_many_sharded(clock: torch.Tensor, ec: torch.Tensor, ic: torch.Tensor, iec: torch.Tensor,
+                                ivc: torch.Tensor, ivv: torch.Tensor, id_off: torch.Tensor, k0: int, K: int,
+                                id_clock=None, id_keys=None, def_off=None, def_row=None, def_clock=None,
+                                def_keys=None, ctx: Optional[Context] = None, check: bool = True):
+    """Key-sharded Map<K, Map<K2, MVReg>> fold (crdt_map_nested_lub_many_sharded, round 5): this rank's
+    outer keys of every replica, every replica clock, the whole outer deferred list with key bitmaps
+    over all K keys."""
+    from . import map as cmap
+    return cmap.nested_lub_many(clock, ec, ic, iec, ivc, ivv, id_off, id_clock=id_clock, id_keys=id_keys,
+                                def_off=def_off, def_row=def_row, def_clock=def_clock, def_keys=def_keys, ctx=ctx,
+                                check=check, _key_shard=(int(k0), int(K)))

@@ -234,7 +234,8 @@ static int coll_allgather(crdt_ctx *ctx, const void *send, void *recv, size_t by
 // entry point.
 using shard_host::Hdr;
 using shard_host::kHdr;
-enum : uint64_t { kTagMax = 1, kTagOr, kTagOrswot, kTagMulti, kTagLww, kTagMap };
+enum : uint64_t { kTagMax = 1, kTagOr, kTagOrswot, kTagMulti, kTagLww, kTagMap, kTagMapCounter, kTagMapOrswot,
+                  kTagMapNested };
 
 static Hdr make_hdr(int st, uint64_t tag, std::initializer_list<uint64_t> dims) {
   return shard_host::make_hdr(st != CRDT_OK, tag, dims);
@@ -1028,7 +1029,159 @@ static int map_sharded_impl(crdt_ctx *ctx, const crdt_map_batch *in, const u64 *
   return CRDT_OK;
 }
 
+// ---- the value-typed Maps sharded by KEYS (round 5): Map<K, GCounter / PNCounter>, Map<K, Orswot>,
+// Map<K, Map<K2, MVReg>>.  As map_sharded_impl: rank k holds keys [k0, k0 + Kk) of every replica,
+// every replica's clock and the group's whole deferred list with key bitmaps over all K keys; its
+// fold of its keys is the exact left fold (keys are independent given the clocks and the deferred
+// list), the flags are ORed over the ranks and the surviving removes' key sets assembled by one
+// SUM all-reduce (disjoint key ranges).  `fold(loc_def_keys, loc_out_def_keys)` runs the local
+// fold of the rank's keys with the key bitmaps restricted to them (Kw of Kk words).
+struct VMapShard {
+  size_t G, R, A, Kk, k0, K;
+  const size_t *def_off;  // host, G+1 (NULL: no deferred removes)
+  const uint32_t *def_row;
+  const uint64_t *def_clock, *def_keys;  // def_keys [D][ceil(K/64)]
+  const uint64_t *clock;
+  size_t c_rs, c_gs;
+  uint64_t *out_clock;
+  uint32_t *out_flags;
+  uint8_t *out_def_keep;
+  uint64_t *out_def_keys;  // [D][ceil(K/64)]
+};
+
+template <class Fold>
+static int vmap_sharded_impl(crdt_ctx *ctx, int st0, const VMapShard &v, uint64_t tag, uint64_t dimx, Fold &&fold,
+                             const char *what) {
+  CRDT_CHECK_CTX(ctx);
+  CRDT_TRY(need_comm(ctx));
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  CRDT_TRY(agree_mark(ctx));
+  const size_t W = (size_t)ctx->nranks;
+  int st = device_mem_only(ctx, what);
+  if (!st) st = st0;
+  const size_t G = st ? 0 : v.G, Kk = st ? 0 : v.Kk, A = st ? 0 : v.A, R = st ? 0 : v.R, K = st ? 0 : v.K;
+  const size_t k0 = st ? 0 : v.k0;
+  if (!st && k0 + Kk > K) st = fail(ctx, CRDT_EINVAL, "%s: key range [%zu, %zu) past K = %zu", what, k0, k0 + Kk, K);
+  if (!st && G && A && (!v.out_clock || !v.out_flags)) st = fail(ctx, CRDT_EINVAL, "%s: NULL output", what);
+  if (!st && v.def_off && G && v.def_off[0] != 0) st = fail(ctx, CRDT_EINVAL, "%s: def_off[0] must be 0", what);
+  const size_t D = (st || !v.def_off || G == 0) ? 0 : v.def_off[G];
+  const size_t Kw = (K + 63) / 64, Kwl = Kk ? (Kk + 63) / 64 : 1;
+  if (!st && D && (!v.def_keys || !v.def_clock || !v.def_row || !v.out_def_keys || !v.out_def_keep))
+    st = fail(ctx, CRDT_EINVAL, "%s: deferred buffers missing", what);
+  if (!st && D > 0xffffffffULL) st = fail(ctx, CRDT_EUNSUPPORTED, "%s: too many deferred removes", what);
+  const bool work = !st && G > 0 && A > 0;
+  const size_t frow = G + 2;  // [G flags | status | 0]
+  void *lk = nullptr, *ok = nullptr, *fl = nullptr, *fall = nullptr;
+  if (work) {
+    st = sbuf(ctx, 2, frow * 8, &fl);
+    if (!st) st = sbuf(ctx, 3, W * frow * 8, &fall);
+    if (!st && D) st = sbuf(ctx, 0, D * Kwl * 8, &lk);
+    if (!st && D) st = sbuf(ctx, 1, D * Kwl * 8, &ok);
+  }
+  if (!st && work) {
+    if (D) {  // the key bitmaps restricted to this rank's keys [k0, k0 + Kk), re-indexed from 0
+      hipLaunchKernelGGL(bitmap_shift_kernel, dim3(small_grid(ctx, D * Kwl)), dim3(kBlock), 0, ctx->stream, (u64 *)lk,
+                         (const u64 *)v.def_keys, (unsigned long long)D, (unsigned long long)Kwl,
+                         (unsigned long long)Kw, (long long)k0, (long long)(k0 + Kk));
+      if (hipGetLastError() != hipSuccess) st = fail(ctx, CRDT_EHIP, "%s: bitmap_shift_kernel launch", what);
+    }
+    if (!st && Kk > 0) {
+      st = fold((const uint64_t *)lk, (uint64_t *)ok);
+    } else if (!st) {  // no keys here: the clock lub and the removes' survival alone
+      st = device_fill(ctx, v.out_flags, G * 4, 0);
+      if (!st) st = lattice_lub_many(ctx, Op::Max, (const u64 *)v.clock, G, R, A, v.c_rs, v.c_gs, (u64 *)v.out_clock, A, 0);
+      if (!st && D) {
+        DefPlan q{};
+        q.G = G;
+        q.D = D;
+        q.M = 64;
+        q.A = A;
+        q.Mw = 1;
+        q.def_clock = (const u64 *)v.def_clock;
+        q.def_members = (const u64 *)lk;  // all-zero: no key of this rank
+        q.out_clock = (const u64 *)v.out_clock;
+        q.apply_ceiling = 0;
+        q.out_keep = v.out_def_keep;
+        q.out_members = (u64 *)ok;
+        st = launch_deferred(ctx, v.def_off, q, nullptr);
+      }
+    }
+  }
+  const uint64_t offh = (!st && v.def_off && G) ? shard_host::hash_offsets(v.def_off, G + 1) : 0;
+  CRDT_TRY(agree(ctx, st, make_hdr(st, tag, {G, K, A, D, dimx, offh}), what));
+  if (!work) return st;
+  hipLaunchKernelGGL(widen_u32_kernel, dim3(small_grid(ctx, G + 1)), dim3(kBlock), 0, ctx->stream, (u64 *)fl,
+                     (const uint32_t *)v.out_flags, (unsigned long long)G, (u64)(st ? 1 : 0));
+  CRDT_HIP(ctx, hipGetLastError());
+  CRDT_TRY(device_fill(ctx, (u64 *)fl + G + 1, 8, 0));
+  CRDT_TRY(coll_allgather(ctx, fl, fall, frow * 8));
+  std::vector<uint64_t> hf(W * frow);
+  std::vector<uint32_t> gflags(G);
+  CRDT_HIP(ctx, hipMemcpyAsync(hf.data(), fall, hf.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
+  CRDT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  bool bad, grow;
+  shard_host::map_flags_or(hf.data(), W, G, gflags.data(), &bad, &grow, frow);
+  if (bad) {
+    if (st) return st;
+    return fail(ctx, CRDT_ECOMM, "%s: another rank failed its local fold; no key sets were exchanged", what);
+  }
+  CRDT_TRY(stage_h2d(ctx, v.out_flags, gflags.data(), G * 4));
+  if (!D) return CRDT_OK;
+  hipLaunchKernelGGL(bitmap_shift_kernel, dim3(small_grid(ctx, D * Kw)), dim3(kBlock), 0, ctx->stream,
+                     (u64 *)v.out_def_keys, (const u64 *)ok, (unsigned long long)D, (unsigned long long)Kw,
+                     (unsigned long long)Kwl, -(long long)k0, (long long)Kk);
+  CRDT_HIP(ctx, hipGetLastError());
+  timing_begin(ctx, "shard_exchange");
+  CRDT_TRY(coll_allreduce(ctx, (const u64 *)v.out_def_keys, (u64 *)v.out_def_keys, D * Kw, Red::Sum));
+  timing_end(ctx);
+  return CRDT_OK;
+}
+
 extern "C" {
+
+int crdt_map_counter_lub_many_sharded(crdt_ctx *ctx, const crdt_map_counter_batch *in, size_t k0, size_t K,
+                                      crdt_map_counter_out *out) {
+  const int st0 = (!in || !out) ? fail(ctx, CRDT_EINVAL, "map_counter_lub_many_sharded: NULL argument") : CRDT_OK;
+  VMapShard v{};
+  if (!st0) v = VMapShard{in->G, in->R, in->A, in->K, k0, K, in->def_off, in->def_row, in->def_clock, in->def_keys,
+                          in->clock, in->clock_rstride, in->clock_gstride, out->clock, out->flags, out->def_keep,
+                          out->def_keys};
+  return vmap_sharded_impl(ctx, st0, v, kTagMapCounter, st0 ? 0 : in->W, [&](const uint64_t *lk, uint64_t *ok) {
+    crdt_map_counter_batch loc = *in;
+    crdt_map_counter_out lo = *out;
+    if (lk) loc.def_keys = lk, lo.def_keys = ok;
+    return crdt_map_counter_lub_many(ctx, &loc, &lo);
+  }, "map_counter_lub_many_sharded");
+}
+
+int crdt_map_orswot_lub_many_sharded(crdt_ctx *ctx, const crdt_map_orswot_batch *in, size_t k0, size_t K,
+                                     crdt_map_orswot_out *out) {
+  const int st0 = (!in || !out) ? fail(ctx, CRDT_EINVAL, "map_orswot_lub_many_sharded: NULL argument") : CRDT_OK;
+  VMapShard v{};
+  if (!st0) v = VMapShard{in->G, in->R, in->A, in->K, k0, K, in->def_off, in->def_row, in->def_clock, in->def_keys,
+                          in->clock, in->A, in->R * in->A, out->clock, out->flags, out->def_keep, out->def_keys};
+  return vmap_sharded_impl(ctx, st0, v, kTagMapOrswot, st0 ? 0 : in->M, [&](const uint64_t *lk, uint64_t *ok) {
+    crdt_map_orswot_batch loc = *in;
+    crdt_map_orswot_out lo = *out;
+    if (lk) loc.def_keys = lk, lo.def_keys = ok;
+    return crdt_map_orswot_lub_many(ctx, &loc, &lo);
+  }, "map_orswot_lub_many_sharded");
+}
+
+int crdt_map_nested_lub_many_sharded(crdt_ctx *ctx, const crdt_map_nested_batch *in, size_t k0, size_t K,
+                                     crdt_map_nested_out *out) {
+  const int st0 = (!in || !out) ? fail(ctx, CRDT_EINVAL, "map_nested_lub_many_sharded: NULL argument") : CRDT_OK;
+  VMapShard v{};
+  if (!st0) v = VMapShard{in->G, in->R, in->A, in->K, k0, K, in->def_off, in->def_row, in->def_clock, in->def_keys,
+                          in->clock, in->A, in->R * in->A, out->clock, out->flags, out->def_keep, out->def_keys};
+  return vmap_sharded_impl(ctx, st0, v, kTagMapNested, st0 ? 0 : (in->K2 << 8 | in->V),
+                           [&](const uint64_t *lk, uint64_t *ok) {
+    crdt_map_nested_batch loc = *in;
+    crdt_map_nested_out lo = *out;
+    if (lk) loc.def_keys = lk, lo.def_keys = ok;
+    return crdt_map_nested_lub_many(ctx, &loc, &lo);
+  }, "map_nested_lub_many_sharded");
+}
 
 int crdt_map_lub_many_sharded(crdt_ctx *ctx, const crdt_map_batch *in, size_t k0, size_t K, crdt_map_out *out) {
   return map_sharded_impl(ctx, in, nullptr, 0, k0, K, out, "map_lub_many_sharded");

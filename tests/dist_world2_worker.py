@@ -193,6 +193,38 @@ def cabi_seam(rank, world, t, h):
         o[f"cabi_map_{tag}_nval"] = mres.nval.cpu().numpy().copy()
         o[f"cabi_map_{tag}_keep"] = mres.def_keep.cpu().numpy().copy()
         o[f"cabi_map_{tag}_def_keys"] = h(mres.def_keys)
+    # value-typed Maps (round 5): key shards of Map<K, GCounter / PNCounter> (the MVReg input's value
+    # clocks as counter rows) and Map<K, Orswot> (entry clock as the nested clock, value clocks as
+    # member dots); each rank also folds every key unsharded (no collective) for the check
+    k0, k1 = cdist.shard_range(K, rank, world)
+    vc = d["vclk"]
+    if vc.shape[2] < 2:
+        vc = np.concatenate([vc, np.zeros(vc.shape[:2] + (2 - vc.shape[2],) + vc.shape[3:], np.uint64)], axis=2)
+    for W in (1, 2):
+        val = np.ascontiguousarray(vc[:, :, :W])
+        full = cg.map.counter_lub_many(t(d["clock"]), t(d["ec"]), t(val), ctx=ctx, **kw)
+        sh = cs.map_counter_lub_many_sharded(t(d["clock"]), t(d["ec"][:, k0:k1]), t(val[:, k0:k1]), k0, K,
+                                             ctx=ctx, **kw)
+        o[f"vmap_c{W}_k0"] = np.array([k0, k1], np.int64)
+        for nm, a, b in (("clock", full.clock, sh.clock), ("ec", full.ec[k0:k1], sh.ec),
+                         ("val", full.val[k0:k1], sh.val), ("keep", full.def_keep, sh.def_keep),
+                         ("keys", full.def_keys, sh.def_keys), ("flags", full.flags, sh.flags)):
+            if a is not None:
+                o[f"vmap_c{W}_full_{nm}"], o[f"vmap_c{W}_sh_{nm}"] = a.cpu().numpy().copy(), b.cpu().numpy().copy()
+    oc = np.ascontiguousarray(d["ec"])
+    ent = np.ascontiguousarray(vc[:, :, :2])
+    R = d["clock"].shape[0]
+    full = cg.map.orswot_lub_many(t(d["clock"]), t(d["ec"]), t(oc), t(ent),
+                                  torch.zeros(R * K + 1, dtype=torch.int64, device=dev), ctx=ctx, **kw)
+    sh = cs.map_orswot_lub_many_sharded(t(d["clock"]), t(d["ec"][:, k0:k1]), t(oc[:, k0:k1]), t(ent[:, k0:k1]),
+                                        torch.zeros(R * (k1 - k0) + 1, dtype=torch.int64, device=dev), k0, K,
+                                        ctx=ctx, **kw)
+    o["vmap_o_k0"] = np.array([k0, k1], np.int64)
+    for nm, a, b in (("clock", full.clock, sh.clock), ("ec", full.ec[k0:k1], sh.ec), ("oc", full.oc[k0:k1], sh.oc),
+                     ("ent", full.ent[k0:k1], sh.ent), ("keep", full.def_keep, sh.def_keep),
+                     ("keys", full.def_keys, sh.def_keys), ("flags", full.flags, sh.flags)):
+        if a is not None:
+            o[f"vmap_o_full_{nm}"], o[f"vmap_o_sh_{nm}"] = a.cpu().numpy().copy(), b.cpu().numpy().copy()
     # Map with device offsets that differ between the ranks (same G and D, so the agreed header
     # matches): the offsets' hash in the flags exchange differs, so BOTH ranks raise EINVAL
     if Dn >= 2:

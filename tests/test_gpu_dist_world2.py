@@ -205,6 +205,27 @@ def test_world2_cabi_map(outs, tag):
         assert (d["ec"].shape[1], d["ec"].shape[1]) in covered
 
 
+@pytest.mark.parametrize("tag,names", [("c1", ("clock", "ec", "val", "keep", "keys", "flags")),
+                                       ("c2", ("clock", "ec", "val", "keep", "keys", "flags")),
+                                       ("o", ("clock", "ec", "oc", "ent", "keep", "keys", "flags"))])
+def test_world2_cabi_value_maps(outs, tag, names):
+    """crdt_map_counter_lub_many_sharded (W = 1, 2) and crdt_map_orswot_lub_many_sharded at world 2
+    (round 5): each rank's keys equal the same rank's unsharded fold of every key restricted to them,
+    and the surviving removes' key sets after the SUM all-reduce equal the unsharded fold's over ALL
+    keys (the two key ranges cover K).  The unsharded folds are parity-tested against the oracle in
+    tests/test_gpu_map_counter.py / test_gpu_map_orswot.py."""
+    K = D.map_input()["ec"].shape[1]
+    covered = set()
+    for o in outs:
+        k0, k1 = (int(x) for x in o[f"vmap_{tag}_k0"])
+        covered |= set(range(k0, k1))
+        for nm in names:
+            if f"vmap_{tag}_full_{nm}" in o:
+                np.testing.assert_array_equal(o[f"vmap_{tag}_sh_{nm}"], o[f"vmap_{tag}_full_{nm}"], err_msg=nm)
+        assert f"vmap_{tag}_sh_keys" in o  # (the input holds surviving removes)
+    assert covered == set(range(K))
+
+
 def test_world2_cabi_map_overflow_on_one_rank(outs):
     """Only rank 1's key folds to 12 values: with vout=8 its fold state (8 values) overflows, the C
     call reruns EVERY rank with the 16-value state (the retry used to be rank-local, so

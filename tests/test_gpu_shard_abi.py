@@ -157,3 +157,82 @@ def test_config5_shard_world1(comm_ctx):
     assert (got != 0).all()
     del x
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("k0,Kk", [(0, 29), (5, 15), (20, 9), (3, 0)])
+def test_value_maps_sharded_world1(comm_ctx, k0, Kk):
+    """The value-typed Maps' key-sharded folds (round 5) at world 1 over a key range: the rank's keys
+    equal the unsharded fold of every key restricted to them (itself parity-tested against the
+    oracle), and the surviving removes' key sets hold exactly this rank's keys of the unsharded ones."""
+    import dist_world2_data as D
+    d = D.map_input()
+    K = d["ec"].shape[1]
+    R = d["clock"].shape[0]
+    Dn = d["def_row"].shape[0]
+    t = lambda a: to_dev(np.ascontiguousarray(a))  # noqa: E731
+    kw = dict(def_off=[0, Dn], def_row=torch.from_numpy(d["def_row"].astype(np.int32)).cuda(),
+              def_clock=t(d["def_clock"]), def_keys=t(d["def_keys"]))
+    mask = np.zeros(((K + 63) // 64,), np.uint64)
+    for k in range(k0, k0 + Kk):
+        mask[k // 64] |= np.uint64(1) << np.uint64(k % 64)
+    vc = d["vclk"]
+    if vc.shape[2] < 2:
+        vc = np.concatenate([vc, np.zeros(vc.shape[:2] + (2 - vc.shape[2],) + vc.shape[3:], np.uint64)], axis=2)
+
+    def same(full, sh, rows):
+        np.testing.assert_array_equal(to_host(sh.clock), to_host(full.clock))
+        for nm in rows:
+            np.testing.assert_array_equal(to_host(getattr(sh, nm)), to_host(getattr(full, nm))[k0:k0 + Kk], err_msg=nm)
+        np.testing.assert_array_equal(sh.def_keep.cpu().numpy(), full.def_keep.cpu().numpy())
+        np.testing.assert_array_equal(to_host(sh.def_keys), to_host(full.def_keys) & mask[None])
+        assert full.def_keep.cpu().numpy().any()
+
+    for W in (1, 2):
+        val = np.ascontiguousarray(vc[:, :, :W])
+        full = cg.map.counter_lub_many(t(d["clock"]), t(d["ec"]), t(val), ctx=comm_ctx, **kw)
+        sh = cg.shard.map_counter_lub_many_sharded(t(d["clock"]), t(d["ec"][:, k0:k0 + Kk]), t(val[:, k0:k0 + Kk]),
+                                                   k0, K, ctx=comm_ctx, **kw)
+        same(full, sh, ("ec", "val"))
+    oc, ent = np.ascontiguousarray(d["ec"]), np.ascontiguousarray(vc[:, :, :2])
+    full = cg.map.orswot_lub_many(t(d["clock"]), t(d["ec"]), t(oc), t(ent),
+                                  torch.zeros(R * K + 1, dtype=torch.int64, device="cuda:0"), ctx=comm_ctx, **kw)
+    sh = cg.shard.map_orswot_lub_many_sharded(t(d["clock"]), t(d["ec"][:, k0:k0 + Kk]), t(oc[:, k0:k0 + Kk]),
+                                              t(ent[:, k0:k0 + Kk]),
+                                              torch.zeros(R * Kk + 1, dtype=torch.int64, device="cuda:0"), k0, K,
+                                              ctx=comm_ctx, **kw)
+    same(full, sh, ("ec", "oc", "ent"))
+    # Map<K, Map<K2, MVReg>>: the nested generator's replicas with the far-future outer removes
+    maps = O.nested_map_objects(30, K, 5, 6, seed=91, steps=400)
+    V = max([len(ie.val.vals) for m in maps for e in m.entries.values() for ie in e.val.entries.values()] + [1])
+    nd = O.nested_map_to_dense(maps, K, 5, 6, V)
+    args = [t(nd[x]) for x in ("clock", "ec", "ic", "iec", "ivc", "ivv")]
+    Dn2 = nd["def_row"].shape[0]
+    kw2 = dict(def_off=[0, Dn2], def_row=torch.from_numpy(nd["def_row"].astype(np.int32)).cuda(),
+               def_clock=t(nd["def_clock"]), def_keys=t(nd["def_keys"])) if Dn2 else {}
+    ikw = dict(id_clock=t(nd["id_clock"]), id_keys=t(nd["id_keys"])) if nd["id_off"][-1] else {}
+    full = cg.map.nested_lub_many(*args, t(nd["id_off"]), ctx=comm_ctx, **ikw, **kw2)
+    R2 = nd["clock"].shape[0]
+    # the inner removes' CSR restricted to this rank's keys: rows of (r, k) for k in the range
+    off = nd["id_off"].astype(np.int64)
+    rows, soff = [], [0]
+    for r in range(R2):
+        for k in range(k0, k0 + Kk):
+            a, b = int(off[r * K + k]), int(off[r * K + k + 1])
+            rows.extend(range(a, b))
+            soff.append(len(rows))
+    ikw2 = dict(id_clock=t(nd["id_clock"][rows]), id_keys=t(nd["id_keys"][rows])) if rows else {}
+    sl = lambda x: t(nd[x][:, k0:k0 + Kk])  # noqa: E731
+    sh = cg.shard.map_nested_lub_many_sharded(args[0], sl("ec"), sl("ic"), sl("iec"), sl("ivc"), sl("ivv"),
+                                              t(np.array(soff, np.int64)), k0, K, ctx=comm_ctx, **ikw2, **kw2)
+    np.testing.assert_array_equal(to_host(sh.clock), to_host(full.clock))
+    hv = lambda x: x.cpu().numpy() if x.dtype == torch.int32 else to_host(x)  # noqa: E731
+    for nm in ("ec", "ic", "iec", "ivc", "ivv", "nval", "id_n"):
+        np.testing.assert_array_equal(hv(getattr(sh, nm)), hv(getattr(full, nm))[k0:k0 + Kk], err_msg=nm)
+    idn = hv(full.id_n)[k0:k0 + Kk]  # (rows past a key's id_n are not written)
+    for nm in ("id_clock", "id_keys"):
+        a, b = hv(getattr(sh, nm)), hv(getattr(full, nm))[k0:k0 + Kk]
+        for k in range(Kk):
+            np.testing.assert_array_equal(a[k, :idn[k]], b[k, :idn[k]], err_msg=nm)
+    assert idn.sum() > 0 or Kk == 0
+    if Dn2:
+        np.testing.assert_array_equal(sh.def_keep.cpu().numpy(), full.def_keep.cpu().numpy())
