@@ -327,6 +327,47 @@ typedef struct crdt_map_states {
 int crdt_map_forget_batch(crdt_ctx *ctx, const crdt_map_states *states, const uint64_t *y, size_t y_stride,
                           uint64_t *def_clock, const uint32_t *def_state, size_t D, uint8_t *def_keep);
 
+/* Map::forget (map.rs:85-114) of whole value-typed Map states (round 5), in place, arguments as
+ * crdt_map_forget_batch (one forget clock per state, the Map-level deferred rm clocks as a pool of
+ * D rows with their states, def_keep[d] = 0 where one emptied):
+ *  - Map<K, GCounter / PNCounter>: the crdt_map_counter_lub_many output layout per state s:
+ *    clock + s*clock_stride, ec + s*ec_stride + k*A, val + s*val_stride + (k*W + w)*A; a dropped
+ *    entry has all-zero rows; the counter rows forget word by word (gcounter.rs:51-53,
+ *    pncounter.rs:78-81).
+ *  - Map<K, Orswot<M>>: the crdt_map_orswot_lub_many output layout (packed; N states), the Orswot
+ *    clock, member rows and nested deferred removes forgotten (orswot.rs:150-183): an emptied member
+ *    row is absent, an emptied nested rm clock dropped, two that become equal keep one entry with the
+ *    later one's members at the earlier one's place (the fold's rule; the reference's HashMap order is
+ *    unspecified), and a dropped entry drops its nested removes (vd_n = 0).  A <= 1,024. */
+typedef struct crdt_map_counter_states {
+  size_t N, K, A, W;
+  uint64_t *clock;
+  size_t clock_stride;
+  uint64_t *ec;
+  size_t ec_stride;
+  uint64_t *val;
+  size_t val_stride;
+} crdt_map_counter_states;
+
+int crdt_map_counter_forget_batch(crdt_ctx *ctx, const crdt_map_counter_states *states, const uint64_t *y,
+                                  size_t y_stride, uint64_t *def_clock, const uint32_t *def_state, size_t D,
+                                  uint8_t *def_keep);
+
+typedef struct crdt_map_orswot_states {
+  size_t N, K, M, A;
+  uint64_t *clock;    /* [N][A]            */
+  uint64_t *ec;       /* [N][K][A]         */
+  uint64_t *oc;       /* [N][K][A]         */
+  uint64_t *ent;      /* [N][K][M][A]      */
+  uint32_t *vd_n;     /* [N][K]            */
+  uint64_t *vd_clock; /* [N][K][16][A]     */
+  uint64_t *vd_mem;   /* [N][K][16][Mw]    */
+} crdt_map_orswot_states;
+
+int crdt_map_orswot_forget_batch(crdt_ctx *ctx, const crdt_map_orswot_states *states, const uint64_t *y,
+                                 size_t y_stride, uint64_t *def_clock, const uint32_t *def_state, size_t D,
+                                 uint8_t *def_keep);
+
 /* Batched Map<K, MVReg<u64>> CmRDT::apply (map.rs:119-137, apply_keyset_rm :318-348,
  * apply_deferred :311-316, MVReg::apply mvreg.rs:130-166): state s applies its ops
  * [op_off[s], op_off[s+1]) in order, in place, on the crdt_map_states layout (value slots in Vec

@@ -54,7 +54,7 @@ EXPORTS = (
     "crdt_orswot_lub_many_doff", "crdt_map_lub_many_doff",
     "crdt_orswot_lub_many_sharded_doff", "crdt_map_lub_many_sharded_doff", "crdt_map_counter_lub_many", "crdt_map_orswot_lub_many",
     "crdt_map_nested_lub_many", "crdt_map_counter_lub_many_sharded", "crdt_map_orswot_lub_many_sharded",
-    "crdt_map_nested_lub_many_sharded",
+    "crdt_map_nested_lub_many_sharded", "crdt_map_counter_forget_batch", "crdt_map_orswot_forget_batch",
 )
 
 
@@ -111,6 +111,16 @@ class OrswotShardedOut(ctypes.Structure):  # crdt_orswot_sharded_out
 class MapStates(ctypes.Structure):  # crdt_map_states
     _fields_ = [("N", S), ("K", S), ("A", S), ("V", S), ("clock", P), ("clock_stride", S), ("ec", P),
                 ("ec_stride", S), ("vclk", P), ("vclk_stride", S), ("vval", P), ("vval_stride", S)]
+
+
+class MapCounterStates(ctypes.Structure):  # crdt_map_counter_states
+    _fields_ = [("N", S), ("K", S), ("A", S), ("W", S), ("clock", P), ("clock_stride", S), ("ec", P),
+                ("ec_stride", S), ("val", P), ("val_stride", S)]
+
+
+class MapOrswotStates(ctypes.Structure):  # crdt_map_orswot_states
+    _fields_ = [("N", S), ("K", S), ("M", S), ("A", S), ("clock", P), ("ec", P), ("oc", P), ("ent", P),
+                ("vd_n", P), ("vd_clock", P), ("vd_mem", P)]
 
 
 class MapOps(ctypes.Structure):  # crdt_map_ops
@@ -258,6 +268,8 @@ _SIGS = {
 _SIGS.update({
     "crdt_orswot_forget_batch": ([P, P, S, P, S, S, S, S, S, P, S, P, P, S, P], ctypes.c_int),
     "crdt_map_forget_batch": ([P, ctypes.POINTER(MapStates), P, S, P, P, S, P], ctypes.c_int),
+    "crdt_map_counter_forget_batch": ([P, ctypes.POINTER(MapCounterStates), P, S, P, P, S, P], ctypes.c_int),
+    "crdt_map_orswot_forget_batch": ([P, ctypes.POINTER(MapOrswotStates), P, S, P, P, S, P], ctypes.c_int),
     "crdt_map_apply_batch": ([P, ctypes.POINTER(MapStates), P, P, P, S, ctypes.POINTER(MapOps), P], ctypes.c_int),
     "crdt_orswot_merge_batch": ([P, ctypes.POINTER(OrswotStates), ctypes.POINTER(OrswotStates), P], ctypes.c_int),
     "crdt_map_merge_batch": ([P, ctypes.POINTER(MapStates), ctypes.POINTER(MapDeferred), ctypes.POINTER(MapStates),

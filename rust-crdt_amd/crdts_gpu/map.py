@@ -746,3 +746,61 @@ def nested_lub_many(clock: torch.Tensor, ec: torch.Tensor, ic: torch.Tensor, iec
         oclk, oec, oic, oiec, oivc, oivv, nval, id_n, oidc, oidk = (
             oclk[0], oec[0], oic[0], oiec[0], oivc[0], oivv[0], nval[0], id_n[0], oidc[0], oidk[0])
     return MapNestedLub(oclk, oec, oic, oiec, oivc, oivv, nval, id_n, oidc, oidk, flags, keep, keys_out)
+
+
+# ---- Causal::forget of value-typed Map states (round 5) --------------------------------------------
+def counter_forget_batch(clock: torch.Tensor, ec: torch.Tensor, val: torch.Tensor, y: torch.Tensor,
+                         def_clock: Optional[torch.Tensor] = None, def_state: Optional[torch.Tensor] = None,
+                         ctx: Optional[Context] = None) -> Optional[torch.Tensor]:
+    """Causal::forget of N Map<K, GCounter / PNCounter> states in place (map.rs:85-114 with
+    gcounter.rs:51-53 / pncounter.rs:78-81; crdt_map_counter_forget_batch): clock (N, A), ec (N, K, A),
+    val (N, K, W, A) — the counter_lub_many output layout —, y (A,) or (N, A); deferred as for
+    forget_batch.  Returns def_keep or None."""
+    ctx = ctx or Context.default(clock.device.index)
+    for t, nm in ((clock, "clock"), (ec, "ec"), (val, "val")):
+        ctx.check_tensor(t, f"map.counter_forget_batch({nm})")
+    if clock.dim() != 2 or ec.dim() != 3 or val.dim() != 4:
+        raise ValueError("map.counter_forget_batch: clock (N,A), ec (N,K,A), val (N,K,W,A) expected")
+    N, A = clock.shape
+    K, W = val.shape[1], val.shape[2]
+    if (tuple(ec.shape) != (N, K, A) or tuple(val.shape) != (N, K, W, A) or W not in (1, 2)
+            or clock.stride(1) != 1 or ec.stride(2) != 1 or ec.stride(1) != A or val.stride(3) != 1
+            or val.stride(2) != A or val.stride(1) != W * A):
+        raise ValueError("map.counter_forget_batch: per-state blocks must be packed (K, A) / (K, W, A), W = 1 or 2")
+    y, ys = _forget_clock(ctx, y, N, A, "map.counter_forget_batch(y)")
+    dp, sp, D, keep = _forget_deferred(ctx, def_clock, def_state, N, A, "map.counter_forget_batch(def_clock)")
+    st = _abi.MapCounterStates()
+    st.N, st.K, st.A, st.W = N, K, A, W
+    st.clock, st.clock_stride = clock.data_ptr(), clock.stride(0)
+    st.ec, st.ec_stride = ec.data_ptr(), ec.stride(0)
+    st.val, st.val_stride = val.data_ptr(), val.stride(0)
+    ctx.call("crdt_map_counter_forget_batch", ctypes.byref(st), y.data_ptr(), ys, dp, sp, D,
+             keep.data_ptr() if keep is not None else None)
+    return keep
+
+
+def orswot_forget_batch(res: "MapOrswotLub", y: torch.Tensor, def_clock: Optional[torch.Tensor] = None,
+                        def_state: Optional[torch.Tensor] = None,
+                        ctx: Optional[Context] = None) -> Optional[torch.Tensor]:
+    """Causal::forget of N Map<K, Orswot> states in place (map.rs:85-114 with orswot.rs:150-183;
+    crdt_map_orswot_forget_batch): `res` an orswot_lub_many result with G = N states (its tensors are
+    updated: clock, ec, oc, ent, vd_n, vd_clock, vd_mem), y (A,) or (N, A); the Map-level deferred rm
+    clocks as for forget_batch.  Returns def_keep or None."""
+    clock, ec, oc, ent = res.clock, res.ec, res.oc, res.ent
+    if clock.dim() != 2:
+        raise ValueError("map.orswot_forget_batch: a grouped result (clock (N, A)) expected")
+    ctx = ctx or Context.default(clock.device.index)
+    N, A = clock.shape
+    K, M = ent.shape[1], ent.shape[2]
+    for t in (clock, ec, oc, ent, res.vd_n, res.vd_clock, res.vd_mem):
+        if not t.is_contiguous():
+            raise ValueError("map.orswot_forget_batch: the result's tensors must be contiguous")
+    y, ys = _forget_clock(ctx, y, N, A, "map.orswot_forget_batch(y)")
+    dp, sp, D, keep = _forget_deferred(ctx, def_clock, def_state, N, A, "map.orswot_forget_batch(def_clock)")
+    st = _abi.MapOrswotStates()
+    st.N, st.K, st.M, st.A = N, K, M, A
+    st.clock, st.ec, st.oc, st.ent = clock.data_ptr(), ec.data_ptr(), oc.data_ptr(), ent.data_ptr()
+    st.vd_n, st.vd_clock, st.vd_mem = res.vd_n.data_ptr(), res.vd_clock.data_ptr(), res.vd_mem.data_ptr()
+    ctx.call("crdt_map_orswot_forget_batch", ctypes.byref(st), y.data_ptr(), ys, dp, sp, D,
+             keep.data_ptr() if keep is not None else None)
+    return keep
