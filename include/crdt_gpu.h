@@ -353,6 +353,38 @@ int crdt_map_counter_forget_batch(crdt_ctx *ctx, const crdt_map_counter_states *
                                   size_t y_stride, uint64_t *def_clock, const uint32_t *def_state, size_t D,
                                   uint8_t *def_keep);
 
+/* Batched Map<K, GCounter / PNCounter> CmRDT::apply (round 5; map.rs:119-137 with gcounter.rs:36-42 /
+ * pncounter.rs:59-68, apply_keyset_rm :318-348, apply_deferred :311-316): state s applies its ops
+ * [op_off[s], op_off[s+1]) in order, in place, on the crdt_map_counter_states layout; deferred
+ * removes as crdt_map_apply_batch (def_count[s] <= Dcap slots, rm clock def_clock[(s*Dcap + d)*A + a],
+ * key bitmap def_keys[(s*Dcap + d)*Kw + w]).  Ops: kind 0 = Op::Up { dot: (actor, counter), key,
+ * op: the counter's op (vactor, vcounter) — a Dot — with vdir 0 = P (GCounter: always 0), 1 = N
+ * (vdir may be NULL: all P) }, kind 1 = Op::Rm { clock: clk_pool[clk_row*A ..], keyset: keys[key_off[o]
+ * .. key_off[o+1]) }.  status[s]: bit 0 = deferred slots exhausted, bit 1 = a malformed op / key
+ * skipped, bits 2-3 = invalid input (state untouched).  Limits: A <= 512, Dcap * (A + Kw) <= 8192
+ * words (the deferred slots live in LDS during the stream). */
+typedef struct crdt_map_counter_ops {
+  size_t n_ops;
+  const uint64_t *op_off;    /* [N+1]       */
+  const uint8_t *kind;       /* [n_ops]     */
+  const uint32_t *actor;     /* [n_ops] Up: the Map's dot */
+  const uint64_t *counter;   /* [n_ops] Up  */
+  const uint32_t *key;       /* [n_ops] Up  */
+  const uint32_t *vactor;    /* [n_ops] Up: the counter's dot */
+  const uint64_t *vcounter;  /* [n_ops] Up  */
+  const uint8_t *vdir;       /* [n_ops] Up: 0 P, 1 N (or NULL) */
+  const uint32_t *clk_row;   /* [n_ops] Rm  */
+  const uint64_t *clk_pool;  /* [n_clk_rows][A] */
+  size_t n_clk_rows;
+  const uint64_t *key_off;   /* [n_ops+1] Rm */
+  const uint32_t *keys;      /* [n_keys]    */
+  size_t n_keys;
+} crdt_map_counter_ops;
+
+int crdt_map_counter_apply_batch(crdt_ctx *ctx, const crdt_map_counter_states *states, uint64_t *def_clock,
+                                 uint64_t *def_keys, uint32_t *def_count, size_t Dcap,
+                                 const crdt_map_counter_ops *ops, uint32_t *status);
+
 typedef struct crdt_map_orswot_states {
   size_t N, K, M, A;
   uint64_t *clock;    /* [N][A]            */

@@ -55,6 +55,7 @@ EXPORTS = (
     "crdt_orswot_lub_many_sharded_doff", "crdt_map_lub_many_sharded_doff", "crdt_map_counter_lub_many", "crdt_map_orswot_lub_many",
     "crdt_map_nested_lub_many", "crdt_map_counter_lub_many_sharded", "crdt_map_orswot_lub_many_sharded",
     "crdt_map_nested_lub_many_sharded", "crdt_map_counter_forget_batch", "crdt_map_orswot_forget_batch",
+    "crdt_map_counter_apply_batch",
 )
 
 
@@ -121,6 +122,12 @@ class MapCounterStates(ctypes.Structure):  # crdt_map_counter_states
 class MapOrswotStates(ctypes.Structure):  # crdt_map_orswot_states
     _fields_ = [("N", S), ("K", S), ("M", S), ("A", S), ("clock", P), ("ec", P), ("oc", P), ("ent", P),
                 ("vd_n", P), ("vd_clock", P), ("vd_mem", P)]
+
+
+class MapCounterOps(ctypes.Structure):  # crdt_map_counter_ops
+    _fields_ = [("n_ops", S), ("op_off", P), ("kind", P), ("actor", P), ("counter", P), ("key", P), ("vactor", P),
+                ("vcounter", P), ("vdir", P), ("clk_row", P), ("clk_pool", P), ("n_clk_rows", S), ("key_off", P),
+                ("keys", P), ("n_keys", S)]
 
 
 class MapOps(ctypes.Structure):  # crdt_map_ops
@@ -270,6 +277,8 @@ _SIGS.update({
     "crdt_map_forget_batch": ([P, ctypes.POINTER(MapStates), P, S, P, P, S, P], ctypes.c_int),
     "crdt_map_counter_forget_batch": ([P, ctypes.POINTER(MapCounterStates), P, S, P, P, S, P], ctypes.c_int),
     "crdt_map_orswot_forget_batch": ([P, ctypes.POINTER(MapOrswotStates), P, S, P, P, S, P], ctypes.c_int),
+    "crdt_map_counter_apply_batch": ([P, ctypes.POINTER(MapCounterStates), P, P, P, S, ctypes.POINTER(MapCounterOps),
+                                      P], ctypes.c_int),
     "crdt_map_apply_batch": ([P, ctypes.POINTER(MapStates), P, P, P, S, ctypes.POINTER(MapOps), P], ctypes.c_int),
     "crdt_orswot_merge_batch": ([P, ctypes.POINTER(OrswotStates), ctypes.POINTER(OrswotStates), P], ctypes.c_int),
     "crdt_map_merge_batch": ([P, ctypes.POINTER(MapStates), ctypes.POINTER(MapDeferred), ctypes.POINTER(MapStates),

@@ -804,3 +804,104 @@ def orswot_forget_batch(res: "MapOrswotLub", y: torch.Tensor, def_clock: Optiona
     ctx.call("crdt_map_orswot_forget_batch", ctypes.byref(st), y.data_ptr(), ys, dp, sp, D,
              keep.data_ptr() if keep is not None else None)
     return keep
+
+
+# ---- CmRDT::apply of Map<K, GCounter / PNCounter> (round 5) ---------------------------------------
+class MapCounterOpBatch(NamedTuple):
+    """Device op streams (crdt_map_counter_ops): state s applies ops [op_off[s], op_off[s+1]) in order."""
+    op_off: torch.Tensor    # (N+1,) int64
+    kind: torch.Tensor      # (n_ops,) uint8: 0 = Op::Up, 1 = Op::Rm
+    actor: torch.Tensor     # (n_ops,) int32   Up: the Map's dot
+    counter: torch.Tensor   # (n_ops,) int64
+    key: torch.Tensor       # (n_ops,) int32
+    vactor: torch.Tensor    # (n_ops,) int32   Up: the counter's dot
+    vcounter: torch.Tensor  # (n_ops,) int64
+    vdir: torch.Tensor      # (n_ops,) uint8   0 = P, 1 = N
+    clk_row: torch.Tensor   # (n_ops,) int32   Rm: row of clk_pool
+    clk_pool: torch.Tensor  # (n_clk, A) int64
+    key_off: torch.Tensor   # (n_ops+1,) int64 Rm keysets
+    keys: torch.Tensor      # (n_keys,) int32
+
+
+def encode_counter_ops(streams, A: int, device) -> MapCounterOpBatch:
+    """Host ingest of per-state op streams: ("up", actor, counter, key, vactor, vcounter, dir) for
+    Op::Up { dot, key, op } with the counter's op a Dot (dir 0; PNCounter: dir 1 = Neg), or
+    ("rm", clock, keys) for Op::Rm { clock, keyset } (clock: mapping actor -> counter or a row)."""
+    def row(clk):
+        r = np.zeros(A, dtype=np.uint64)
+        if hasattr(clk, "items"):
+            for a, c in clk.items():
+                r[int(a)] = np.uint64(c)
+        else:
+            r[:] = np.asarray(clk, dtype=np.uint64)
+        return r
+
+    op_off, kind, actor, counter, key, vactor, vcounter, vdir = [0], [], [], [], [], [], [], []
+    clk_row, key_off, keys, pool = [], [0], [], []
+    for ops in streams:
+        for op in ops:
+            if op[0] == "up":
+                _, a, c, k, va, vc, d = op
+                kind.append(0)
+                actor.append(int(a)); counter.append(int(c)); key.append(int(k))  # noqa: E702
+                vactor.append(int(va)); vcounter.append(int(vc)); vdir.append(int(d))  # noqa: E702
+                clk_row.append(0)
+            else:
+                _, rc, ks = op
+                kind.append(1)
+                actor.append(0); counter.append(0); key.append(0)  # noqa: E702
+                vactor.append(0); vcounter.append(0); vdir.append(0)  # noqa: E702
+                clk_row.append(len(pool))
+                pool.append(row(rc))
+                keys.extend(int(x) for x in ks)
+            key_off.append(len(keys))
+        op_off.append(len(kind))
+    i64 = lambda x: torch.tensor(np.asarray(x, dtype=np.uint64).view(np.int64), device=device)  # noqa: E731
+    pool_t = (torch.from_numpy(np.stack(pool).view(np.int64)).to(device) if pool
+              else torch.zeros((1, A), dtype=torch.int64, device=device))
+    return MapCounterOpBatch(
+        i64(op_off), torch.tensor(kind, dtype=torch.uint8, device=device),
+        torch.tensor(actor, dtype=torch.int32, device=device), i64(counter),
+        torch.tensor(key, dtype=torch.int32, device=device), torch.tensor(vactor, dtype=torch.int32, device=device),
+        i64(vcounter), torch.tensor(vdir, dtype=torch.uint8, device=device),
+        torch.tensor(clk_row, dtype=torch.int32, device=device), pool_t, i64(key_off),
+        torch.tensor(keys if keys else [0], dtype=torch.int32, device=device))
+
+
+def counter_apply_batch(clock: torch.Tensor, ec: torch.Tensor, val: torch.Tensor, def_clock: torch.Tensor,
+                        def_keys: torch.Tensor, def_count: torch.Tensor, ops: MapCounterOpBatch,
+                        ctx: Optional[Context] = None) -> torch.Tensor:
+    """Apply every state's op stream in place (crdt_map_counter_apply_batch): clock (N, A), ec (N, K, A),
+    val (N, K, W, A), deferred slots def_clock (N, Dcap, A) / def_keys (N, Dcap, ceil(K/64)) / def_count
+    (N,) int32.  Returns the per-state status (N,) int32 (include/crdt_gpu.h)."""
+    ctx = ctx or Context.default(clock.device.index)
+    for t_, nm in ((clock, "clock"), (ec, "ec"), (val, "val"), (def_clock, "def_clock"), (def_keys, "def_keys")):
+        ctx.check_tensor(t_, f"map.counter_apply_batch({nm})")
+    N, A = clock.shape
+    K, W = val.shape[1], val.shape[2]
+    Kw = (K + 63) // 64
+    Dcap = def_clock.shape[1]
+    if (tuple(ec.shape) != (N, K, A) or tuple(val.shape) != (N, K, W, A) or not clock.is_contiguous()
+            or not ec.is_contiguous() or not val.is_contiguous()):
+        raise ValueError("map.counter_apply_batch: contiguous clock (N,A), ec (N,K,A), val (N,K,W,A) expected")
+    if (tuple(def_clock.shape) != (N, Dcap, A) or tuple(def_keys.shape) != (N, Dcap, Kw)
+            or not def_clock.is_contiguous() or not def_keys.is_contiguous() or tuple(def_count.shape) != (N,)
+            or def_count.dtype != torch.int32):
+        raise ValueError("map.counter_apply_batch: deferred slots (N, Dcap, A) / (N, Dcap, Kw) / (N,) int32 expected")
+    n = ops.kind.shape[0]
+    if ops.op_off.shape[0] != N + 1 or ops.key_off.shape[0] != n + 1 or ops.clk_pool.shape[1] != A:
+        raise ValueError("map.counter_apply_batch: op_off (N+1), key_off (n_ops+1), clk_pool (n, A) expected")
+    st = _abi.MapCounterStates()
+    st.N, st.K, st.A, st.W = N, K, A, W
+    st.clock, st.clock_stride, st.ec, st.ec_stride = clock.data_ptr(), A, ec.data_ptr(), K * A
+    st.val, st.val_stride = val.data_ptr(), K * W * A
+    o = _abi.MapCounterOps()
+    o.n_ops, o.op_off, o.kind = n, ops.op_off.data_ptr(), ops.kind.data_ptr()
+    o.actor, o.counter, o.key = ops.actor.data_ptr(), ops.counter.data_ptr(), ops.key.data_ptr()
+    o.vactor, o.vcounter, o.vdir = ops.vactor.data_ptr(), ops.vcounter.data_ptr(), ops.vdir.data_ptr()
+    o.clk_row, o.clk_pool, o.n_clk_rows = ops.clk_row.data_ptr(), ops.clk_pool.data_ptr(), ops.clk_pool.shape[0]
+    o.key_off, o.keys, o.n_keys = ops.key_off.data_ptr(), ops.keys.data_ptr(), int(ops.key_off[-1].item())
+    status = torch.empty(N, dtype=torch.int32, device=clock.device)
+    ctx.call("crdt_map_counter_apply_batch", ctypes.byref(st), def_clock.data_ptr(), def_keys.data_ptr(),
+             def_count.data_ptr(), Dcap, ctypes.byref(o), status.data_ptr())
+    return status

@@ -1,0 +1,271 @@
+// Batched CmRDT::apply of Map<K, GCounter> / Map<K, PNCounter> (round 5): Map::apply (map.rs:119-137)
+// with the counter's apply inside (gcounter.rs:36-42: the value op is a Dot, VClock::apply;
+// pncounter.rs:59-68: a Dot and a direction, applied to P or N), apply_keyset_rm (:318-348) and
+// apply_deferred (:311-316).  State s applies its ops [op_off[s], op_off[s+1]) in order, in place.
+//
+// One wave per state (ops are ordered: the "seen" test and the deferred removes depend on what came
+// before), lane l holding actors l + 64 j of every row (j < APL), the map clock in registers, the
+// state's deferred removes (rm clock + key bitmap) staged in LDS for the whole stream and written
+// back at the end.  Per op:
+//  * Up { dot (a, c), key k, op (va, vc, dir) }: skipped when clock[a] >= c (seen); else the entry
+//    clock's word a and the value row dir's word va take the max with c / vc (VClock::apply), the map
+//    clock's word a too, then every deferred remove is re-applied (apply_deferred): its keys' entries
+//    forget its clock (an emptied entry is dropped: all-zero rows; a surviving one's value rows
+//    forget it too) and it stays deferred while !(clock >= rm);
+//  * Rm { clock rm, keyset }: the keys' entries forget rm as above, then rm is deferred unless
+//    clock >= rm (an equal clock already deferred unions its key set).
+// The forgets of apply_deferred commute (each forget is idempotent; an entry emptied by one stays
+// empty), so the HashMap's iteration order does not matter.  Each row word is read and written by
+// the lane owning its actor (lane-local), the deferred slots live in LDS.
+#include "common.hpp"
+
+namespace crdt {
+
+struct MapCounterApplyPlan {
+  u64 *clock, *ec, *val;
+  unsigned long long c_s, e_s, v_s;  // state strides (words)
+  unsigned long long N, K, A, W, Kw, Dcap;
+  u64 *def_clock, *def_keys;
+  unsigned *def_count;
+  const u64 *op_off;
+  const uint8_t *kind;
+  const uint32_t *actor, *key, *vactor;
+  const u64 *counter, *vcounter;
+  const uint8_t *vdir;
+  const uint32_t *clk_row;
+  const u64 *clk_pool;
+  unsigned long long n_clk_rows;
+  const u64 *key_off;
+  const uint32_t *keys;
+  unsigned long long n_keys, n_ops;
+  unsigned *status;
+  unsigned wpb;  // waves per block
+};
+
+template <int APL>
+__global__ __launch_bounds__(256) void map_counter_apply_kernel(MapCounterApplyPlan p) {
+  extern __shared__ u64 lds[];
+  const int lane = (int)(threadIdx.x % kWave), wv = (int)(threadIdx.x / kWave);
+  const unsigned long long s = (unsigned long long)blockIdx.x * p.wpb + wv;
+  if (wv >= (int)p.wpb || s >= p.N) return;  // (whole waves)
+  const unsigned long long A = p.A, K = p.K, W = p.W, Kw = p.Kw, Dcap = p.Dcap;
+  u64 *sclk = lds + (unsigned long long)wv * Dcap * (A + Kw);  // [Dcap][A] rm clocks
+  u64 *skey = sclk + Dcap * A;                                 // [Dcap][Kw] key bitmaps
+  const unsigned long long ob = p.op_off[s], oe = p.op_off[s + 1];
+  unsigned dcnt = p.def_count[s];
+  if (dcnt > Dcap || oe < ob || oe > p.n_ops) {
+    if (lane == 0) p.status[s] = (dcnt > Dcap ? 4u : 0u) | (oe < ob || oe > p.n_ops ? 8u : 0u);
+    return;  // state left untouched
+  }
+  unsigned st = 0;
+  u64 *C = p.clock + s * p.c_s, *E = p.ec + s * p.e_s, *V = p.val + s * p.v_s;
+  auto word = [&](int j) { return (unsigned long long)lane + 64ull * j; };
+  u64 c[APL];
+#pragma unroll
+  for (int j = 0; j < APL; ++j) c[j] = word(j) < A ? C[word(j)] : 0ull;
+  for (unsigned d = 0; d < dcnt; ++d) {
+    for (unsigned long long a = (unsigned long long)lane; a < A; a += kWave)
+      sclk[d * A + a] = p.def_clock[(s * Dcap + d) * A + a];
+    for (unsigned long long w = (unsigned long long)lane; w < Kw; w += kWave)
+      skey[d * Kw + w] = p.def_keys[(s * Dcap + d) * Kw + w];
+  }
+
+  // the clock's word of actor a (uniform)
+  auto clock_of = [&](unsigned a) -> u64 {
+    u64 x = 0;
+#pragma unroll
+    for (int j = 0; j < APL; ++j)
+      if ((unsigned)j == a / 64) x = c[j];
+    return __shfl(x, (int)(a % 64));
+  };
+  // clock >= r (every word): r is dominated
+  auto dominated = [&](const u64 (&r)[APL]) {
+    bool b = false;
+#pragma unroll
+    for (int j = 0; j < APL; ++j) b = b || r[j] > c[j];
+    return __ballot(b) == 0;
+  };
+  // key k's entry forgets r: dropped (all-zero rows) when its clock empties, else its value too
+  auto key_rm = [&](unsigned long long k, const u64 (&r)[APL]) {
+    u64 e[APL];
+    bool live = false, left = false;
+#pragma unroll
+    for (int j = 0; j < APL; ++j) {
+      e[j] = word(j) < A ? E[k * A + word(j)] : 0ull;
+      live = live || e[j] != 0;
+      e[j] = e[j] > r[j] ? e[j] : 0ull;
+      left = left || e[j] != 0;
+    }
+    if (!__ballot(live)) return;  // no entry
+    const bool keep = __ballot(left) != 0;
+#pragma unroll
+    for (int j = 0; j < APL; ++j)
+      if (word(j) < A) E[k * A + word(j)] = e[j];
+    for (unsigned long long w = 0; w < W; ++w) {
+#pragma unroll
+      for (int j = 0; j < APL; ++j) {
+        if (word(j) >= A) continue;
+        u64 *vp = V + (k * W + w) * A + word(j);
+        const u64 v = *vp;
+        const u64 nv = keep && v > r[j] ? v : 0ull;
+        if (nv != v) *vp = nv;
+      }
+    }
+  };
+  auto apply_deferred = [&]() {
+    unsigned o = 0;
+    for (unsigned d = 0; d < dcnt; ++d) {
+      u64 r[APL];
+#pragma unroll
+      for (int j = 0; j < APL; ++j) r[j] = word(j) < A ? sclk[d * A + word(j)] : 0ull;
+      for (unsigned long long w = 0; w < Kw; ++w) {
+        u64 bits = skey[d * Kw + w];
+        while (bits) {
+          const unsigned long long k = w * 64 + (unsigned long long)__builtin_ctzll(bits);
+          bits &= bits - 1;
+          if (k < K) key_rm(k, r);
+        }
+      }
+      if (dominated(r)) continue;  // no longer deferred
+      if (o != d) {
+        for (unsigned long long a = (unsigned long long)lane; a < A; a += kWave) sclk[o * A + a] = sclk[d * A + a];
+        for (unsigned long long w = (unsigned long long)lane; w < Kw; w += kWave) skey[o * Kw + w] = skey[d * Kw + w];
+      }
+      ++o;
+    }
+    dcnt = o;
+  };
+
+  for (unsigned long long o = ob; o < oe; ++o) {
+    const unsigned kind = p.kind[o];
+    if (kind == 0) {  // ---- Op::Up
+      const unsigned a = p.actor[o], va = p.vactor[o];
+      const unsigned long long k = p.key[o];
+      const u64 cnt = p.counter[o], vc = p.vcounter[o];
+      const unsigned dir = p.vdir ? p.vdir[o] : 0u;
+      if (a >= A || va >= A || k >= K || dir >= W) {
+        st |= 2u;
+        continue;
+      }
+      if (clock_of(a) >= cnt) continue;  // seen (map.rs:123-126)
+      if ((unsigned long long)lane == a % 64) {
+        u64 *ep = E + k * A + a;
+        if (*ep < cnt) *ep = cnt;  // entry.clock.apply(dot)
+#pragma unroll
+        for (int j = 0; j < APL; ++j)
+          if ((unsigned)j == a / 64 && c[j] < cnt) c[j] = cnt;  // self.clock.apply(dot)
+      }
+      if ((unsigned long long)lane == va % 64) {
+        u64 *vp = V + (k * W + dir) * A + va;
+        if (*vp < vc) *vp = vc;  // entry.val.apply(op)
+      }
+      apply_deferred();
+    } else if (kind == 1) {  // ---- Op::Rm -> apply_keyset_rm
+      const unsigned rr = p.clk_row ? p.clk_row[o] : 0xffffffffu;
+      const u64 kb = p.key_off[o], ke = p.key_off[o + 1];
+      if (rr >= p.n_clk_rows || ke < kb || ke > p.n_keys) {
+        st |= 2u;
+        continue;
+      }
+      u64 r[APL];
+#pragma unroll
+      for (int j = 0; j < APL; ++j) r[j] = word(j) < A ? p.clk_pool[(unsigned long long)rr * A + word(j)] : 0ull;
+      for (u64 i = kb; i < ke; ++i) {
+        const unsigned long long k = p.keys[i];
+        if (k < K) key_rm(k, r);
+        else st |= 2u;
+      }
+      if (dominated(r)) continue;  // every key this clock has seen, we have seen
+      int slot = -1;
+      for (unsigned d = 0; d < dcnt && slot < 0; ++d) {
+        bool ne = false;
+#pragma unroll
+        for (int j = 0; j < APL; ++j) ne = ne || (word(j) < A && sclk[d * A + word(j)] != r[j]);
+        if (!__ballot(ne)) slot = (int)d;
+      }
+      if (slot < 0) {
+        if (dcnt >= Dcap) {
+          st |= 1u;  // deferred capacity exceeded: the state is incomplete
+          continue;
+        }
+        slot = (int)dcnt++;
+#pragma unroll
+        for (int j = 0; j < APL; ++j)
+          if (word(j) < A) sclk[slot * A + word(j)] = r[j];
+        for (unsigned long long w = (unsigned long long)lane; w < Kw; w += kWave) skey[slot * Kw + w] = 0;
+      }
+      // deferred_set.append(keyset): one lane per key word
+      for (u64 i = kb; i < ke; ++i) {
+        const unsigned long long k = p.keys[i];
+        if (k < K && (unsigned long long)lane == (k / 64) % kWave) skey[slot * Kw + k / 64] |= 1ull << (k % 64);
+      }
+    } else {
+      st |= 2u;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < APL; ++j)
+    if (word(j) < A) C[word(j)] = c[j];
+  for (unsigned d = 0; d < dcnt; ++d) {
+    for (unsigned long long a = (unsigned long long)lane; a < A; a += kWave)
+      p.def_clock[(s * Dcap + d) * A + a] = sclk[d * A + a];
+    for (unsigned long long w = (unsigned long long)lane; w < Kw; w += kWave)
+      p.def_keys[(s * Dcap + d) * Kw + w] = skey[d * Kw + w];
+  }
+  if (lane == 0) {
+    p.def_count[s] = dcnt;
+    p.status[s] = st;
+  }
+}
+
+}  // namespace crdt
+
+using namespace crdt;
+
+extern "C" int crdt_map_counter_apply_batch(crdt_ctx *ctx, const crdt_map_counter_states *m, uint64_t *def_clock,
+                                            uint64_t *def_keys, uint32_t *def_count, size_t Dcap,
+                                            const crdt_map_counter_ops *ops, uint32_t *status) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
+  CRDT_CHECK_CTX(ctx);
+  if (!m || !ops || !status) return fail(ctx, CRDT_EINVAL, "map_counter_apply_batch: NULL argument");
+  const size_t N = m->N, K = m->K, A = m->A, W = m->W;
+  if (W != 1 && W != 2) return fail(ctx, CRDT_EINVAL, "map_counter_apply_batch: W = %zu (1 GCounter, 2 PNCounter)", W);
+  if (N == 0) return CRDT_OK;
+  if (A == 0 || A > 512) return fail(ctx, CRDT_EUNSUPPORTED, "map_counter_apply_batch: A = %zu outside 1..512", A);
+  if (!m->clock || !m->ec || (K && !m->val) || !def_count || (Dcap && (!def_clock || !def_keys)) || !ops->op_off)
+    return fail(ctx, CRDT_EINVAL, "map_counter_apply_batch: NULL buffer");
+  if (ops->n_ops && (!ops->kind || !ops->actor || !ops->counter || !ops->key || !ops->vactor || !ops->vcounter))
+    return fail(ctx, CRDT_EINVAL, "map_counter_apply_batch: NULL op buffer");
+  if (m->clock_stride < A || m->ec_stride < K * A || m->val_stride < K * W * A)
+    return fail(ctx, CRDT_EINVAL, "map_counter_apply_batch: strides smaller than the rows they hold");
+  const size_t Kw = K ? (K + 63) / 64 : 1;
+  const size_t per_wave = Dcap * (A + Kw) * 8;
+  if (per_wave > 64 * 1024)
+    return fail(ctx, CRDT_EUNSUPPORTED, "map_counter_apply_batch: Dcap * (A + ceil(K/64)) = %zu words > 8192",
+                per_wave / 8);
+  unsigned wpb = 4;
+  while (wpb > 1 && per_wave * wpb > 64 * 1024) --wpb;
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  MapCounterApplyPlan p{(u64 *)m->clock, (u64 *)m->ec, (u64 *)m->val, m->clock_stride, m->ec_stride, m->val_stride,
+                        N, K, A, W, Kw, Dcap, (u64 *)def_clock, (u64 *)def_keys, def_count,
+                        (const u64 *)ops->op_off, ops->kind, ops->actor, ops->key, ops->vactor,
+                        (const u64 *)ops->counter, (const u64 *)ops->vcounter, ops->vdir, ops->clk_row,
+                        (const u64 *)ops->clk_pool, ops->clk_pool ? ops->n_clk_rows : 0,
+                        (const u64 *)ops->key_off, ops->keys, ops->keys ? ops->n_keys : 0, ops->n_ops, status, wpb};
+  // an Rm op needs key_off (n_ops + 1 entries); without it every Rm reads an empty key range
+  if (!ops->key_off) {
+    if (int rc = ensure_scratch(ctx, (ops->n_ops + 1) * 8)) return rc;
+    if (int rc = device_fill(ctx, ctx->scratch, (ops->n_ops + 1) * 8, 0)) return rc;
+    p.key_off = static_cast<const u64 *>(ctx->scratch);
+  }
+  const dim3 grid((unsigned)((N + wpb - 1) / wpb)), block(wpb * kWave);
+  const size_t lds = per_wave * wpb;
+  timing_begin(ctx, "map_counter_apply");
+  if (A <= 64) hipLaunchKernelGGL(map_counter_apply_kernel<1>, grid, block, lds, ctx->stream, p);
+  else if (A <= 128) hipLaunchKernelGGL(map_counter_apply_kernel<2>, grid, block, lds, ctx->stream, p);
+  else if (A <= 256) hipLaunchKernelGGL(map_counter_apply_kernel<4>, grid, block, lds, ctx->stream, p);
+  else hipLaunchKernelGGL(map_counter_apply_kernel<8>, grid, block, lds, ctx->stream, p);
+  timing_end(ctx);
+  CRDT_HIP(ctx, hipGetLastError());
+  return CRDT_OK;
+}

@@ -1,0 +1,109 @@
+"""GPU: CmRDT::apply of Map<K, GCounter> / Map<K, PNCounter> (round 5; crdt_map_counter_apply_batch)
+against the oracle's Map.apply (map.rs:119-137, apply_keyset_rm :318-348, apply_deferred :311-316,
+gcounter.rs:36-42, pncounter.rs:59-68) on op-replay states with deferred removes: fresh, stale (seen)
+and gapped dots, removes from the future (deferred, then re-applied by later Ups), equal rm clocks
+(key sets unioned), malformed ops, and A past one lane word."""
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+from gpu_util import to_dev, to_host
+
+pytestmark = pytest.mark.gpu
+
+import crdts_gpu as cg  # noqa: E402
+
+
+def _streams(rng, maps, K, A, W, T):
+    """Per-state op streams (the kernel's tuple form and the oracle's op objects)."""
+    streams, oracle_ops = [], []
+    for m in maps:
+        clk = {a: m.clock.get(a) for a in range(A)}
+        ops, oops, last_rm = [], [], None
+        for _ in range(T):
+            x = rng.random()
+            if x < 0.7:  # Op::Up
+                a = int(rng.integers(A))
+                c = clk[a] + int(rng.integers(1, 3)) if rng.random() < 0.85 else max(clk[a] - int(rng.integers(0, 2)), 1)
+                clk[a] = max(clk[a], c)
+                k, va = int(rng.integers(K)), int(rng.integers(A))
+                vc = int(rng.integers(1, 60))
+                d = int(rng.integers(W))
+                ops.append(("up", a, c, k, va, vc, d))
+                vop = O.Dot(va, vc) if W == 1 else (O.Dot(va, vc), O.PNCounter.POS if d == 0 else O.PNCounter.NEG)
+                oops.append(O.MapUp(O.Dot(a, c), k, vop))
+            else:  # Op::Rm: a clock up to 2 ahead of ours on a few actors (deferred) or behind
+                if last_rm is not None and rng.random() < 0.25:
+                    row = last_rm  # an equal clock again: its key set is unioned
+                else:
+                    row = {a: max(0, clk[a] + int(rng.integers(-3, 3))) for a in range(A) if rng.random() < 0.5}
+                    row = {a: c for a, c in row.items() if c}
+                last_rm = row
+                ks = sorted(set(int(z) for z in rng.choice(K, size=int(rng.integers(1, 4)), replace=False)))
+                ops.append(("rm", row, ks))
+                oops.append(O.MapRm(O.VClock(dict(row)), ks))
+        streams.append(ops)
+        oracle_ops.append(oops)
+    return streams, oracle_ops
+
+
+@pytest.mark.parametrize("W,A,seed", [(1, 6, 1), (2, 6, 2), (1, 70, 3), (2, 130, 4)])
+def test_map_counter_apply(gpu_ctx, W, A, seed):
+    N, K, T, Dcap = 24, 6, 40, 16
+    maps = O.map_counter_objects(N, K, A, W, seed=40, steps=220) if A <= 6 else \
+        O.map_counter_objects(N, K, A, W, seed=40 + seed, steps=260)
+    d = O.map_counter_to_dense(maps, K, A, W)
+    rng = np.random.default_rng(seed)
+    streams, oracle_ops = _streams(rng, maps, K, A, W, T)
+    Kw = (K + 63) // 64
+    dcl = np.zeros((N, Dcap, A), np.uint64)
+    dks = np.zeros((N, Dcap, Kw), np.uint64)
+    cnt = np.zeros(N, np.int32)
+    for j in range(d["def_row"].shape[0]):  # the replicas' own deferred removes, as slots
+        n = int(d["def_row"][j])
+        dcl[n, cnt[n]] = d["def_clock"][j]
+        dks[n, cnt[n]] = d["def_keys"][j]
+        cnt[n] += 1
+    clock, ec, val = to_dev(d["clock"]), to_dev(d["ec"]), to_dev(d["val"])
+    tdc, tdk, tcnt = to_dev(dcl), to_dev(dks), torch.from_numpy(cnt).cuda()
+    ops = cg.map.encode_counter_ops(streams, A, "cuda:0")
+    status = cg.map.counter_apply_batch(clock, ec, val, tdc, tdk, tcnt, ops, ctx=gpu_ctx).cpu().numpy()
+    c, e, v = to_host(clock), to_host(ec), to_host(val)
+    hdc, hdk, hcnt = to_host(tdc), to_host(tdk), tcnt.cpu().numpy()
+    deferred_seen = 0
+    for n in range(N):
+        exp = maps[n].copy()
+        for op in oracle_ops[n]:
+            exp.apply(op)
+        assert status[n] == 0, (n, status[n])
+        dfr = [(hdc[n, i], O.bitmap_members(hdk[n, i])) for i in range(int(hcnt[n]))]
+        got = O.dense_to_map_counter(c[n], e[n], v[n], dfr)
+        assert got == exp, n
+        deferred_seen += len(exp.deferred)
+    assert deferred_seen > 0
+
+
+def test_map_counter_apply_malformed_and_capacity(gpu_ctx):
+    """Malformed ops (actor / key / dir out of range, an rm row past the pool) are skipped and flagged
+    (bit 1); a deferred list past Dcap is flagged (bit 0); a def_count past Dcap leaves the state
+    untouched (bit 2)."""
+    K, A, W = 4, 4, 2
+    streams = [
+        [("up", 9, 1, 0, 0, 1, 0), ("up", 0, 1, 9, 0, 1, 0), ("up", 0, 1, 0, 0, 1, 5), ("up", 1, 1, 2, 3, 7, 1)],
+        [("rm", {0: 5 + i}, [i % K]) for i in range(3)],
+        [("up", 0, 1, 0, 0, 1, 0)],
+    ]
+    ops = cg.map.encode_counter_ops(streams, A, "cuda:0")
+    N, Dcap = 3, 2
+    clock = torch.zeros((N, A), dtype=torch.int64, device="cuda:0")
+    ec = torch.zeros((N, K, A), dtype=torch.int64, device="cuda:0")
+    val = torch.zeros((N, K, W, A), dtype=torch.int64, device="cuda:0")
+    dc = torch.zeros((N, Dcap, A), dtype=torch.int64, device="cuda:0")
+    dk = torch.zeros((N, Dcap, 1), dtype=torch.int64, device="cuda:0")
+    cnt = torch.tensor([0, 0, 3], dtype=torch.int32, device="cuda:0")
+    st = cg.map.counter_apply_batch(clock, ec, val, dc, dk, cnt, ops, ctx=gpu_ctx).cpu().numpy()
+    assert st[0] == 2 and st[1] == 1 and st[2] == 4
+    v = to_host(val)
+    assert v[0, 2, 1, 3] == 7 and to_host(ec)[0, 2, 1] == 1  # the one good op of state 0 applied
+    assert int(cnt[1]) == 2 and to_host(clock)[2].sum() == 0
