@@ -400,6 +400,44 @@ int crdt_map_orswot_forget_batch(crdt_ctx *ctx, const crdt_map_orswot_states *st
                                  size_t y_stride, uint64_t *def_clock, const uint32_t *def_state, size_t D,
                                  uint8_t *def_keep);
 
+/* Batched Map<K, Orswot<M>> CmRDT::apply (round 5; map.rs:119-137 with Orswot::apply orswot.rs:55-79,
+ * apply_rm :230-250 and apply_deferred :281-286 inside, the Map's apply_keyset_rm :318-348 with
+ * Orswot::forget :150-183 and apply_deferred :311-316): state s applies its ops [op_off[s],
+ * op_off[s+1]) in order, in place, on the crdt_map_orswot_states layout (nested deferred lists of
+ * <= 16 per key); the Map's deferred removes as crdt_map_counter_apply_batch.  Ops: kind 0 = Op::Up
+ * { dot: (actor, counter), key, op } with vkind 0 = Orswot Add { dot: (vactor, vcounter), members }
+ * or 1 = Orswot Rm { clock: clk_pool[clk_row*A ..], members }, the members mems[mem_off[o] ..
+ * mem_off[o+1]); kind 1 = Op::Rm { clock: clk_pool[clk_row*A ..], keyset: keys[key_off[o] ..
+ * key_off[o+1]) } (key_off may be NULL when no op is a Map Rm).  status[s]: bit 0 = a deferred list
+ * (the Map's or a nested one) exhausted, bit 1 = a malformed op / key / member skipped, bits 2-3 =
+ * invalid input (state untouched).  Nested removes whose clocks become equal under a Map-level
+ * forget keep one entry, the later one's members (the fold's rule).  Limits: A <= 512, M <= 1,024,
+ * Dcap * (A + Kw) + 256 <= 8192 words. */
+typedef struct crdt_map_orswot_ops {
+  size_t n_ops;
+  const uint64_t *op_off;    /* [N+1]       */
+  const uint8_t *kind;       /* [n_ops]     */
+  const uint32_t *actor;     /* [n_ops] Up: the Map's dot */
+  const uint64_t *counter;   /* [n_ops] Up  */
+  const uint32_t *key;       /* [n_ops] Up  */
+  const uint8_t *vkind;      /* [n_ops] Up: 0 Orswot Add, 1 Orswot Rm */
+  const uint32_t *vactor;    /* [n_ops] Up / Add: the Orswot's dot */
+  const uint64_t *vcounter;  /* [n_ops] Up / Add */
+  const uint32_t *clk_row;   /* [n_ops] Up / Rm and Map Rm: row of clk_pool */
+  const uint64_t *clk_pool;  /* [n_clk_rows][A] */
+  size_t n_clk_rows;
+  const uint64_t *key_off;   /* [n_ops+1] Map Rm keysets */
+  const uint32_t *keys;      /* [n_keys]    */
+  size_t n_keys;
+  const uint64_t *mem_off;   /* [n_ops+1] Up: the Orswot op's members */
+  const uint32_t *mems;      /* [n_mems]    */
+  size_t n_mems;
+} crdt_map_orswot_ops;
+
+int crdt_map_orswot_apply_batch(crdt_ctx *ctx, const crdt_map_orswot_states *states, uint64_t *def_clock,
+                                uint64_t *def_keys, uint32_t *def_count, size_t Dcap,
+                                const crdt_map_orswot_ops *ops, uint32_t *status);
+
 /* Batched Map<K, MVReg<u64>> CmRDT::apply (map.rs:119-137, apply_keyset_rm :318-348,
  * apply_deferred :311-316, MVReg::apply mvreg.rs:130-166): state s applies its ops
  * [op_off[s], op_off[s+1]) in order, in place, on the crdt_map_states layout (value slots in Vec

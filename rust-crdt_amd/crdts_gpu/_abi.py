@@ -55,7 +55,7 @@ EXPORTS = (
     "crdt_orswot_lub_many_sharded_doff", "crdt_map_lub_many_sharded_doff", "crdt_map_counter_lub_many", "crdt_map_orswot_lub_many",
     "crdt_map_nested_lub_many", "crdt_map_counter_lub_many_sharded", "crdt_map_orswot_lub_many_sharded",
     "crdt_map_nested_lub_many_sharded", "crdt_map_counter_forget_batch", "crdt_map_orswot_forget_batch",
-    "crdt_map_counter_apply_batch",
+    "crdt_map_counter_apply_batch", "crdt_map_orswot_apply_batch",
 )
 
 
@@ -128,6 +128,12 @@ class MapCounterOps(ctypes.Structure):  # crdt_map_counter_ops
     _fields_ = [("n_ops", S), ("op_off", P), ("kind", P), ("actor", P), ("counter", P), ("key", P), ("vactor", P),
                 ("vcounter", P), ("vdir", P), ("clk_row", P), ("clk_pool", P), ("n_clk_rows", S), ("key_off", P),
                 ("keys", P), ("n_keys", S)]
+
+
+class MapOrswotOps(ctypes.Structure):  # crdt_map_orswot_ops
+    _fields_ = [("n_ops", S), ("op_off", P), ("kind", P), ("actor", P), ("counter", P), ("key", P), ("vkind", P),
+                ("vactor", P), ("vcounter", P), ("clk_row", P), ("clk_pool", P), ("n_clk_rows", S), ("key_off", P),
+                ("keys", P), ("n_keys", S), ("mem_off", P), ("mems", P), ("n_mems", S)]
 
 
 class MapOps(ctypes.Structure):  # crdt_map_ops
@@ -279,6 +285,8 @@ _SIGS.update({
     "crdt_map_orswot_forget_batch": ([P, ctypes.POINTER(MapOrswotStates), P, S, P, P, S, P], ctypes.c_int),
     "crdt_map_counter_apply_batch": ([P, ctypes.POINTER(MapCounterStates), P, P, P, S, ctypes.POINTER(MapCounterOps),
                                       P], ctypes.c_int),
+    "crdt_map_orswot_apply_batch": ([P, ctypes.POINTER(MapOrswotStates), P, P, P, S, ctypes.POINTER(MapOrswotOps),
+                                     P], ctypes.c_int),
     "crdt_map_apply_batch": ([P, ctypes.POINTER(MapStates), P, P, P, S, ctypes.POINTER(MapOps), P], ctypes.c_int),
     "crdt_orswot_merge_batch": ([P, ctypes.POINTER(OrswotStates), ctypes.POINTER(OrswotStates), P], ctypes.c_int),
     "crdt_map_merge_batch": ([P, ctypes.POINTER(MapStates), ctypes.POINTER(MapDeferred), ctypes.POINTER(MapStates),

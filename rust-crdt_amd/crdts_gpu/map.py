@@ -905,3 +905,109 @@ def counter_apply_batch(clock: torch.Tensor, ec: torch.Tensor, val: torch.Tensor
     ctx.call("crdt_map_counter_apply_batch", ctypes.byref(st), def_clock.data_ptr(), def_keys.data_ptr(),
              def_count.data_ptr(), Dcap, ctypes.byref(o), status.data_ptr())
     return status
+
+
+# ---- CmRDT::apply of Map<K, Orswot> (round 5) -------------------------------------------------------
+class MapOrswotOpBatch(NamedTuple):
+    """Device op streams (crdt_map_orswot_ops)."""
+    op_off: torch.Tensor    # (N+1,) int64
+    kind: torch.Tensor      # (n_ops,) uint8: 0 = Map Op::Up, 1 = Map Op::Rm
+    actor: torch.Tensor     # (n_ops,) int32   Up: the Map's dot
+    counter: torch.Tensor   # (n_ops,) int64
+    key: torch.Tensor       # (n_ops,) int32
+    vkind: torch.Tensor     # (n_ops,) uint8   Up: 0 = Orswot Add, 1 = Orswot Rm
+    vactor: torch.Tensor    # (n_ops,) int32   Add: the Orswot's dot
+    vcounter: torch.Tensor  # (n_ops,) int64
+    clk_row: torch.Tensor   # (n_ops,) int32   Orswot Rm / Map Rm clock row
+    clk_pool: torch.Tensor  # (n_clk, A) int64
+    key_off: torch.Tensor   # (n_ops+1,) int64 Map Rm keysets
+    keys: torch.Tensor      # (n_keys,) int32
+    mem_off: torch.Tensor   # (n_ops+1,) int64 the Orswot op's members
+    mems: torch.Tensor      # (n_mems,) int32
+
+
+def encode_orswot_map_ops(streams, A: int, device) -> MapOrswotOpBatch:
+    """Host ingest of per-state op streams: ("add", actor, counter, key, vactor, vcounter, members),
+    ("orm", actor, counter, key, clock, members) for Map Op::Up with an Orswot Add / Rm, or ("rm",
+    clock, keys) for Map Op::Rm (clocks: mapping actor -> counter or a row)."""
+    def row(clk):
+        r = np.zeros(A, dtype=np.uint64)
+        if hasattr(clk, "items"):
+            for a, c in clk.items():
+                r[int(a)] = np.uint64(c)
+        else:
+            r[:] = np.asarray(clk, dtype=np.uint64)
+        return r
+
+    f = {n: [] for n in ("kind", "actor", "counter", "key", "vkind", "vactor", "vcounter", "clk_row")}
+    op_off, key_off, keys, mem_off, mems, pool = [0], [0], [], [0], [], []
+    for ops in streams:
+        for op in ops:
+            vals = dict(kind=0, actor=0, counter=0, key=0, vkind=0, vactor=0, vcounter=0, clk_row=0)
+            if op[0] == "add":
+                _, a, c, k, va, vc, ms = op
+                vals.update(actor=a, counter=c, key=k, vactor=va, vcounter=vc)
+                mems.extend(int(x) for x in ms)
+            elif op[0] == "orm":
+                _, a, c, k, rc, ms = op
+                vals.update(actor=a, counter=c, key=k, vkind=1, clk_row=len(pool))
+                pool.append(row(rc))
+                mems.extend(int(x) for x in ms)
+            else:
+                _, rc, ks = op
+                vals.update(kind=1, clk_row=len(pool))
+                pool.append(row(rc))
+                keys.extend(int(x) for x in ks)
+            for n, v in vals.items():
+                f[n].append(int(v))
+            key_off.append(len(keys))
+            mem_off.append(len(mems))
+        op_off.append(len(f["kind"]))
+    i64 = lambda x: torch.tensor(np.asarray(x, dtype=np.uint64).view(np.int64), device=device)  # noqa: E731
+    i32 = lambda x: torch.tensor(x if x else [0], dtype=torch.int32, device=device)  # noqa: E731
+    u8 = lambda x: torch.tensor(x, dtype=torch.uint8, device=device)  # noqa: E731
+    pool_t = (torch.from_numpy(np.stack(pool).view(np.int64)).to(device) if pool
+              else torch.zeros((1, A), dtype=torch.int64, device=device))
+    return MapOrswotOpBatch(i64(op_off), u8(f["kind"]), i32(f["actor"]), i64(f["counter"]), i32(f["key"]),
+                            u8(f["vkind"]), i32(f["vactor"]), i64(f["vcounter"]), i32(f["clk_row"]), pool_t,
+                            i64(key_off), i32(keys), i64(mem_off), i32(mems))
+
+
+def orswot_apply_batch(res: "MapOrswotLub", def_clock: torch.Tensor, def_keys: torch.Tensor,
+                       def_count: torch.Tensor, ops: MapOrswotOpBatch, ctx: Optional[Context] = None) -> torch.Tensor:
+    """Apply every state's op stream in place (crdt_map_orswot_apply_batch): `res` an orswot_lub_many
+    result with G = N states (its tensors are updated), the Map's deferred slots def_clock (N, Dcap, A)
+    / def_keys (N, Dcap, ceil(K/64)) / def_count (N,) int32.  Returns the per-state status (N,) int32."""
+    clock, ec, oc, ent = res.clock, res.ec, res.oc, res.ent
+    if clock.dim() != 2:
+        raise ValueError("map.orswot_apply_batch: a grouped result (clock (N, A)) expected")
+    ctx = ctx or Context.default(clock.device.index)
+    N, A = clock.shape
+    K, M = ent.shape[1], ent.shape[2]
+    Kw = (K + 63) // 64
+    Dcap = def_clock.shape[1]
+    for t_ in (clock, ec, oc, ent, res.vd_n, res.vd_clock, res.vd_mem, def_clock, def_keys):
+        if not t_.is_contiguous():
+            raise ValueError("map.orswot_apply_batch: contiguous tensors expected")
+    if (tuple(def_clock.shape) != (N, Dcap, A) or tuple(def_keys.shape) != (N, Dcap, Kw)
+            or tuple(def_count.shape) != (N,) or def_count.dtype != torch.int32):
+        raise ValueError("map.orswot_apply_batch: deferred slots (N, Dcap, A) / (N, Dcap, Kw) / (N,) int32 expected")
+    n = ops.kind.shape[0]
+    if (ops.op_off.shape[0] != N + 1 or ops.key_off.shape[0] != n + 1 or ops.mem_off.shape[0] != n + 1
+            or ops.clk_pool.shape[1] != A):
+        raise ValueError("map.orswot_apply_batch: op_off (N+1), key_off / mem_off (n_ops+1), clk_pool (n, A) expected")
+    st = _abi.MapOrswotStates()
+    st.N, st.K, st.M, st.A = N, K, M, A
+    st.clock, st.ec, st.oc, st.ent = clock.data_ptr(), ec.data_ptr(), oc.data_ptr(), ent.data_ptr()
+    st.vd_n, st.vd_clock, st.vd_mem = res.vd_n.data_ptr(), res.vd_clock.data_ptr(), res.vd_mem.data_ptr()
+    o = _abi.MapOrswotOps()
+    o.n_ops, o.op_off, o.kind = n, ops.op_off.data_ptr(), ops.kind.data_ptr()
+    o.actor, o.counter, o.key = ops.actor.data_ptr(), ops.counter.data_ptr(), ops.key.data_ptr()
+    o.vkind, o.vactor, o.vcounter = ops.vkind.data_ptr(), ops.vactor.data_ptr(), ops.vcounter.data_ptr()
+    o.clk_row, o.clk_pool, o.n_clk_rows = ops.clk_row.data_ptr(), ops.clk_pool.data_ptr(), ops.clk_pool.shape[0]
+    o.key_off, o.keys, o.n_keys = ops.key_off.data_ptr(), ops.keys.data_ptr(), int(ops.key_off[-1].item())
+    o.mem_off, o.mems, o.n_mems = ops.mem_off.data_ptr(), ops.mems.data_ptr(), int(ops.mem_off[-1].item())
+    status = torch.empty(N, dtype=torch.int32, device=clock.device)
+    ctx.call("crdt_map_orswot_apply_batch", ctypes.byref(st), def_clock.data_ptr(), def_keys.data_ptr(),
+             def_count.data_ptr(), Dcap, ctypes.byref(o), status.data_ptr())
+    return status

@@ -1,0 +1,444 @@
+// Batched CmRDT::apply of Map<K, Orswot<M>> (round 5): Map::apply (map.rs:119-137) with the nested
+// Orswot's apply inside (orswot.rs:55-79: Add { dot, members } skipped when the Orswot's clock has
+// seen the dot, else every member's clock and the Orswot clock apply it, then apply_deferred
+// :281-286; Rm { clock, members } -> apply_rm :230-250), the Map's apply_keyset_rm (:318-348, the
+// value forgotten by Orswot::forget :150-183) and apply_deferred (:311-316).  State s applies its
+// ops [op_off[s], op_off[s+1]) in order, in place, on the crdt_map_orswot_lub_many output layout.
+//
+// One wave per state, lane l holding actors l + 64 j (j < APL) of every row: the Map clock in
+// registers, the Map's deferred removes (rm clock + key bitmap) in LDS for the whole stream.  The
+// nested Orswot of a key lives in its rows (oc, ent, vd_clock, vd_mem, vd_n); an op that touches
+// its nested deferred list stages the list's member masks in LDS (the words read by every lane),
+// and every global word is read back only by the lane that wrote it (row words by the lane of
+// their actor, mask word w by lane w % 64, vd_n by every lane).
+#include "common.hpp"
+
+namespace crdt {
+
+constexpr int kMoaVd = 16;    // nested deferred slots per key (crdt_map_orswot_out)
+constexpr int kMoaMw = 16;    // member-mask words (M <= 1,024)
+
+struct MapOrswotApplyPlan {
+  u64 *clock, *ec, *oc, *ent, *vd_clock, *vd_mem;
+  unsigned *vd_n;
+  unsigned long long N, K, M, A, Mw, Kw, Dcap;
+  u64 *def_clock, *def_keys;
+  unsigned *def_count;
+  const u64 *op_off;
+  const uint8_t *kind, *vkind;
+  const uint32_t *actor, *key, *vactor;
+  const u64 *counter, *vcounter;
+  const uint32_t *clk_row;
+  const u64 *clk_pool;
+  unsigned long long n_clk_rows;
+  const u64 *key_off;
+  const uint32_t *keys;
+  unsigned long long n_keys;
+  const u64 *mem_off;
+  const uint32_t *mems;
+  unsigned long long n_mems, n_ops;
+  unsigned *status;
+  unsigned wpb;
+};
+
+template <int APL>
+__global__ __launch_bounds__(256) void map_orswot_apply_kernel(MapOrswotApplyPlan p) {
+  extern __shared__ u64 lds[];
+  const int lane = (int)(threadIdx.x % kWave), wv = (int)(threadIdx.x / kWave);
+  const unsigned long long s = (unsigned long long)blockIdx.x * p.wpb + wv;
+  if (wv >= (int)p.wpb || s >= p.N) return;  // (whole waves)
+  const unsigned long long A = p.A, K = p.K, M = p.M, Mw = p.Mw, Kw = p.Kw, Dcap = p.Dcap;
+  const unsigned long long WQ = Dcap * (A + Kw) + kMoaVd * kMoaMw;
+  u64 *sclk = lds + (unsigned long long)wv * WQ;  // [Dcap][A] the Map's rm clocks
+  u64 *skey = sclk + Dcap * A;                     // [Dcap][Kw] their key bitmaps
+  u64 *smsk = skey + Dcap * Kw;                    // [16][Mw] the current key's nested member masks
+  const unsigned long long ob = p.op_off[s], oe = p.op_off[s + 1];
+  unsigned dcnt = p.def_count[s];
+  if (dcnt > Dcap || oe < ob || oe > p.n_ops) {
+    if (lane == 0) p.status[s] = (dcnt > Dcap ? 4u : 0u) | (oe < ob || oe > p.n_ops ? 8u : 0u);
+    return;  // state left untouched
+  }
+  unsigned st = 0;
+  auto word = [&](int j) { return (unsigned long long)lane + 64ull * j; };
+  u64 *C = p.clock + s * A;
+  u64 c[APL];
+#pragma unroll
+  for (int j = 0; j < APL; ++j) c[j] = word(j) < A ? C[word(j)] : 0ull;
+  for (unsigned d = 0; d < dcnt; ++d) {
+    for (unsigned long long a = (unsigned long long)lane; a < A; a += kWave)
+      sclk[d * A + a] = p.def_clock[(s * Dcap + d) * A + a];
+    for (unsigned long long w = (unsigned long long)lane; w < Kw; w += kWave)
+      skey[d * Kw + w] = p.def_keys[(s * Dcap + d) * Kw + w];
+  }
+  auto ldrow = [&](const u64 *row, u64 (&x)[APL]) {
+#pragma unroll
+    for (int j = 0; j < APL; ++j) x[j] = word(j) < A ? row[word(j)] : 0ull;
+  };
+  auto strow = [&](u64 *row, const u64 (&x)[APL]) {
+#pragma unroll
+    for (int j = 0; j < APL; ++j)
+      if (word(j) < A) row[word(j)] = x[j];
+  };
+  auto any_nz = [&](const u64 (&x)[APL]) {
+    bool b = false;
+#pragma unroll
+    for (int j = 0; j < APL; ++j) b = b || x[j] != 0;
+    return __ballot(b) != 0;
+  };
+  auto leq = [&](const u64 (&x)[APL], const u64 (&y)[APL]) {  // x <= y (every word)
+    bool b = false;
+#pragma unroll
+    for (int j = 0; j < APL; ++j) b = b || x[j] > y[j];
+    return __ballot(b) == 0;
+  };
+  auto word_of = [&](const u64 (&x)[APL], unsigned a) -> u64 {  // x[a] (uniform)
+    u64 v = 0;
+#pragma unroll
+    for (int j = 0; j < APL; ++j)
+      if ((unsigned)j == a / 64) v = x[j];
+    return __shfl(v, (int)(a % 64));
+  };
+  auto bump = [&](u64 *row, unsigned a, u64 cnt) {  // VClock::apply(dot) on a global row
+    if ((unsigned long long)lane == a % 64) {
+      u64 *q = row + a;
+      if (*q < cnt) *q = cnt;
+    }
+  };
+
+  // ---- the nested Orswot of key k (its rows) ----------------------------------------------------
+  struct Keyp {
+    u64 *ec, *oc, *ent, *vc, *vm;
+    unsigned *vn;
+  };
+  auto keyp = [&](unsigned long long k) {
+    const unsigned long long sk = s * K + k;
+    return Keyp{p.ec + sk * A, p.oc + sk * A, p.ent + sk * M * A, p.vd_clock + sk * kMoaVd * A,
+                p.vd_mem + sk * kMoaVd * Mw, p.vd_n + sk};
+  };
+  auto stage_masks = [&](const Keyp &q, unsigned n) {  // global -> LDS (lane w % 64 moves word w)
+    for (unsigned i = 0; i < n; ++i)
+      for (unsigned long long w = (unsigned long long)lane; w < Mw; w += kWave) smsk[i * Mw + w] = q.vm[i * Mw + w];
+  };
+  auto unstage_masks = [&](const Keyp &q, unsigned n) {  // LDS -> global, and the count (every lane)
+    for (unsigned i = 0; i < n; ++i)
+      for (unsigned long long w = (unsigned long long)lane; w < Mw; w += kWave) q.vm[i * Mw + w] = smsk[i * Mw + w];
+    *q.vn = n;
+  };
+  // Orswot::apply_rm's member forget (orswot.rs:231-238): the members of mask row `mrow` (LDS or
+  // a member list) forget r; an emptied member row is absent (all zero)
+  auto forget_members_mask = [&](const Keyp &q, const u64 *mrow, const u64 (&r)[APL]) {
+    for (unsigned long long w = 0; w < Mw; ++w) {
+      u64 bits = mrow[w];
+      while (bits) {
+        const unsigned long long m = w * 64 + (unsigned long long)__builtin_ctzll(bits);
+        bits &= bits - 1;
+        if (m >= M) break;
+        u64 x[APL];
+        ldrow(q.ent + m * A, x);
+#pragma unroll
+        for (int j = 0; j < APL; ++j) x[j] = x[j] > r[j] ? x[j] : 0ull;
+        strow(q.ent + m * A, x);
+      }
+    }
+  };
+  // the nested apply_deferred (orswot.rs:281-286) over the staged list: every remove forgets its
+  // members again and stays while !(rm <= oc); returns the new count
+  auto nested_apply_deferred = [&](const Keyp &q, unsigned n, const u64 (&oc)[APL]) -> unsigned {
+    unsigned o = 0;
+    for (unsigned i = 0; i < n; ++i) {
+      u64 r[APL];
+      ldrow(q.vc + (unsigned long long)i * A, r);
+      forget_members_mask(q, smsk + i * Mw, r);
+      if (leq(r, oc)) continue;
+      if (o != i) {
+        strow(q.vc + (unsigned long long)o * A, r);
+        for (unsigned long long w = (unsigned long long)lane; w < Mw; w += kWave) smsk[o * Mw + w] = smsk[i * Mw + w];
+      }
+      ++o;
+    }
+    return o;
+  };
+  // Orswot::forget (orswot.rs:150-183) of key k's value by r (the entry stays)
+  auto value_forget = [&](const Keyp &q, const u64 (&r)[APL]) {
+    u64 x[APL];
+    ldrow(q.oc, x);
+#pragma unroll
+    for (int j = 0; j < APL; ++j) x[j] = x[j] > r[j] ? x[j] : 0ull;
+    strow(q.oc, x);
+    for (unsigned long long m = 0; m < M; ++m) {
+      ldrow(q.ent + m * A, x);
+#pragma unroll
+      for (int j = 0; j < APL; ++j) x[j] = x[j] > r[j] ? x[j] : 0ull;
+      strow(q.ent + m * A, x);
+    }
+    const unsigned n = *q.vn;
+    if (n == 0) return;
+    stage_masks(q, n);
+    unsigned o = 0;
+    for (unsigned i = 0; i < n; ++i) {
+      ldrow(q.vc + (unsigned long long)i * A, x);
+#pragma unroll
+      for (int j = 0; j < APL; ++j) x[j] = x[j] > r[j] ? x[j] : 0ull;
+      if (!any_nz(x)) continue;  // forgotten
+      unsigned jj = 0;
+      for (; jj < o; ++jj) {  // equal to a kept one: the later members at the earlier place
+        u64 y[APL];
+        ldrow(q.vc + (unsigned long long)jj * A, y);
+        bool ne = false;
+#pragma unroll
+        for (int j = 0; j < APL; ++j) ne = ne || y[j] != x[j];
+        if (!__ballot(ne)) break;
+      }
+      if (jj < o) {
+        for (unsigned long long w = (unsigned long long)lane; w < Mw; w += kWave) smsk[jj * Mw + w] = smsk[i * Mw + w];
+        continue;
+      }
+      strow(q.vc + (unsigned long long)o * A, x);
+      if (o != i)
+        for (unsigned long long w = (unsigned long long)lane; w < Mw; w += kWave) smsk[o * Mw + w] = smsk[i * Mw + w];
+      ++o;
+    }
+    unstage_masks(q, o);
+  };
+  // the Map's apply_keyset_rm on key k (map.rs:319-333): forget its entry by r, drop an emptied one
+  // (all rows zero, no nested removes), else forget its value
+  auto key_rm = [&](unsigned long long k, const u64 (&r)[APL]) {
+    const Keyp q = keyp(k);
+    u64 e[APL];
+    ldrow(q.ec, e);
+    if (!any_nz(e)) return;  // no entry
+#pragma unroll
+    for (int j = 0; j < APL; ++j) e[j] = e[j] > r[j] ? e[j] : 0ull;
+    strow(q.ec, e);
+    if (any_nz(e)) {
+      value_forget(q, r);
+      return;
+    }
+    u64 z[APL];
+#pragma unroll
+    for (int j = 0; j < APL; ++j) z[j] = 0;
+    strow(q.oc, z);
+    for (unsigned long long m = 0; m < M; ++m) strow(q.ent + m * A, z);
+    *q.vn = 0u;
+  };
+  auto map_apply_deferred = [&]() {
+    unsigned o = 0;
+    for (unsigned d = 0; d < dcnt; ++d) {
+      u64 r[APL];
+#pragma unroll
+      for (int j = 0; j < APL; ++j) r[j] = word(j) < A ? sclk[d * A + word(j)] : 0ull;
+      for (unsigned long long w = 0; w < Kw; ++w) {
+        u64 bits = skey[d * Kw + w];
+        while (bits) {
+          const unsigned long long k = w * 64 + (unsigned long long)__builtin_ctzll(bits);
+          bits &= bits - 1;
+          if (k < K) key_rm(k, r);
+        }
+      }
+      if (leq(r, c)) continue;  // no longer deferred
+      if (o != d) {
+        for (unsigned long long a = (unsigned long long)lane; a < A; a += kWave) sclk[o * A + a] = sclk[d * A + a];
+        for (unsigned long long w = (unsigned long long)lane; w < Kw; w += kWave) skey[o * Kw + w] = skey[d * Kw + w];
+      }
+      ++o;
+    }
+    dcnt = o;
+  };
+
+  for (unsigned long long o = ob; o < oe; ++o) {
+    const unsigned kind = p.kind[o];
+    if (kind == 0) {  // ---- Map Op::Up { dot, key, op: an Orswot op }
+      const unsigned a = p.actor[o];
+      const unsigned long long k = p.key[o];
+      const u64 cnt = p.counter[o];
+      const unsigned vk = p.vkind[o];
+      const u64 mb = p.mem_off[o], me = p.mem_off[o + 1];
+      if (a >= A || k >= K || vk > 1 || me < mb || me > p.n_mems) {
+        st |= 2u;
+        continue;
+      }
+      if (word_of(c, a) >= cnt) continue;  // seen (map.rs:123-126)
+      const Keyp q = keyp(k);
+      bump(q.ec, a, cnt);  // entry.clock.apply(dot) (an absent entry: its rows are the default Orswot)
+      u64 oc[APL];
+      ldrow(q.oc, oc);
+      if (vk == 0) {  // Orswot Op::Add { dot, members }
+        const unsigned va = p.vactor[o];
+        const u64 vc = p.vcounter[o];
+        if (va >= A) {
+          st |= 2u;
+        } else if (word_of(oc, va) < vc) {  // (seen by the Orswot's clock: nothing)
+          for (u64 i = mb; i < me; ++i) {
+            const unsigned long long m = p.mems[i];
+            if (m < M) bump(q.ent + m * A, va, vc);
+            else st |= 2u;
+          }
+          bump(q.oc, va, vc);
+#pragma unroll
+          for (int j = 0; j < APL; ++j)
+            if ((unsigned)j == va / 64 && (unsigned long long)lane == va % 64 && oc[j] < vc) oc[j] = vc;
+          const unsigned n = *q.vn;
+          if (n > 0) {
+            stage_masks(q, n);
+            unstage_masks(q, nested_apply_deferred(q, n, oc));
+          }
+        }
+      } else {  // Orswot Op::Rm { clock, members } -> apply_rm
+        const unsigned rr = p.clk_row[o];
+        if (rr >= p.n_clk_rows) {
+          st |= 2u;
+        } else {
+          u64 r[APL];
+          ldrow(p.clk_pool + (unsigned long long)rr * A, r);
+          for (u64 i = mb; i < me; ++i) {
+            const unsigned long long m = p.mems[i];
+            if (m >= M) {
+              st |= 2u;
+              continue;
+            }
+            u64 x[APL];
+            ldrow(q.ent + m * A, x);
+#pragma unroll
+            for (int j = 0; j < APL; ++j) x[j] = x[j] > r[j] ? x[j] : 0ull;
+            strow(q.ent + m * A, x);
+          }
+          if (!leq(r, oc)) {  // !(clock <= self.clock): deferred, an equal clock's members unioned
+            unsigned n = *q.vn;
+            stage_masks(q, n);
+            int slot = -1;
+            for (unsigned i = 0; i < n && slot < 0; ++i) {
+              u64 y[APL];
+              ldrow(q.vc + (unsigned long long)i * A, y);
+              bool ne = false;
+#pragma unroll
+              for (int j = 0; j < APL; ++j) ne = ne || y[j] != r[j];
+              if (!__ballot(ne)) slot = (int)i;
+            }
+            if (slot < 0 && n >= (unsigned)kMoaVd) {
+              st |= 1u;  // nested deferred capacity exceeded
+            } else {
+              if (slot < 0) {
+                slot = (int)n++;
+                strow(q.vc + (unsigned long long)slot * A, r);
+                for (unsigned long long w = (unsigned long long)lane; w < Mw; w += kWave) smsk[slot * Mw + w] = 0;
+              }
+              for (u64 i = mb; i < me; ++i) {
+                const unsigned long long m = p.mems[i];
+                if (m < M && (unsigned long long)lane == (m / 64) % kWave) smsk[slot * Mw + m / 64] |= 1ull << (m % 64);
+              }
+            }
+            unstage_masks(q, n);
+          }
+        }
+      }
+      // self.clock.apply(dot), then the Map's apply_deferred
+#pragma unroll
+      for (int j = 0; j < APL; ++j)
+        if ((unsigned)j == a / 64 && (unsigned long long)lane == a % 64 && c[j] < cnt) c[j] = cnt;
+      map_apply_deferred();
+    } else if (kind == 1) {  // ---- Map Op::Rm -> apply_keyset_rm
+      const unsigned rr = p.clk_row[o];
+      const u64 kb = p.key_off[o], ke = p.key_off[o + 1];
+      if (rr >= p.n_clk_rows || ke < kb || ke > p.n_keys) {
+        st |= 2u;
+        continue;
+      }
+      u64 r[APL];
+      ldrow(p.clk_pool + (unsigned long long)rr * A, r);
+      for (u64 i = kb; i < ke; ++i) {
+        const unsigned long long k = p.keys[i];
+        if (k < K) key_rm(k, r);
+        else st |= 2u;
+      }
+      if (leq(r, c)) continue;
+      int slot = -1;
+      for (unsigned d = 0; d < dcnt && slot < 0; ++d) {
+        bool ne = false;
+#pragma unroll
+        for (int j = 0; j < APL; ++j) ne = ne || (word(j) < A && sclk[d * A + word(j)] != r[j]);
+        if (!__ballot(ne)) slot = (int)d;
+      }
+      if (slot < 0) {
+        if (dcnt >= Dcap) {
+          st |= 1u;
+          continue;
+        }
+        slot = (int)dcnt++;
+#pragma unroll
+        for (int j = 0; j < APL; ++j)
+          if (word(j) < A) sclk[slot * A + word(j)] = r[j];
+        for (unsigned long long w = (unsigned long long)lane; w < Kw; w += kWave) skey[slot * Kw + w] = 0;
+      }
+      for (u64 i = kb; i < ke; ++i) {
+        const unsigned long long k = p.keys[i];
+        if (k < K && (unsigned long long)lane == (k / 64) % kWave) skey[slot * Kw + k / 64] |= 1ull << (k % 64);
+      }
+    } else {
+      st |= 2u;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < APL; ++j)
+    if (word(j) < A) C[word(j)] = c[j];
+  for (unsigned d = 0; d < dcnt; ++d) {
+    for (unsigned long long a = (unsigned long long)lane; a < A; a += kWave)
+      p.def_clock[(s * Dcap + d) * A + a] = sclk[d * A + a];
+    for (unsigned long long w = (unsigned long long)lane; w < Kw; w += kWave)
+      p.def_keys[(s * Dcap + d) * Kw + w] = skey[d * Kw + w];
+  }
+  if (lane == 0) {
+    p.def_count[s] = dcnt;
+    p.status[s] = st;
+  }
+}
+
+}  // namespace crdt
+
+using namespace crdt;
+
+extern "C" int crdt_map_orswot_apply_batch(crdt_ctx *ctx, const crdt_map_orswot_states *m, uint64_t *def_clock,
+                                           uint64_t *def_keys, uint32_t *def_count, size_t Dcap,
+                                           const crdt_map_orswot_ops *ops, uint32_t *status) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
+  CRDT_CHECK_CTX(ctx);
+  if (!m || !ops || !status) return fail(ctx, CRDT_EINVAL, "map_orswot_apply_batch: NULL argument");
+  const size_t N = m->N, K = m->K, M = m->M, A = m->A;
+  if (N == 0) return CRDT_OK;
+  if (A == 0 || A > 512) return fail(ctx, CRDT_EUNSUPPORTED, "map_orswot_apply_batch: A = %zu outside 1..512", A);
+  if (M > 64 * (size_t)kMoaMw) return fail(ctx, CRDT_EUNSUPPORTED, "map_orswot_apply_batch: M = %zu > %d", M, 64 * kMoaMw);
+  if (!m->clock || (K && (!m->ec || !m->oc || (M && !m->ent) || !m->vd_n || !m->vd_clock || !m->vd_mem)) ||
+      !def_count || (Dcap && (!def_clock || !def_keys)) || !ops->op_off || !ops->mem_off)
+    return fail(ctx, CRDT_EINVAL, "map_orswot_apply_batch: NULL buffer");
+  if (ops->n_ops && (!ops->kind || !ops->vkind || !ops->actor || !ops->counter || !ops->key || !ops->vactor ||
+                     !ops->vcounter || !ops->clk_row))
+    return fail(ctx, CRDT_EINVAL, "map_orswot_apply_batch: NULL op buffer");
+  const size_t Kw = K ? (K + 63) / 64 : 1, Mw = M > 64 ? (M + 63) / 64 : 1;
+  const size_t per_wave = (Dcap * (A + Kw) + kMoaVd * kMoaMw) * 8;
+  if (per_wave > 64 * 1024)
+    return fail(ctx, CRDT_EUNSUPPORTED, "map_orswot_apply_batch: Dcap * (A + ceil(K/64)) too large for LDS");
+  unsigned wpb = 4;
+  while (wpb > 1 && per_wave * wpb > 64 * 1024) --wpb;
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  MapOrswotApplyPlan p{(u64 *)m->clock, (u64 *)m->ec, (u64 *)m->oc, (u64 *)m->ent, (u64 *)m->vd_clock,
+                       (u64 *)m->vd_mem, m->vd_n, N, K, M, A, Mw, Kw, Dcap, (u64 *)def_clock, (u64 *)def_keys,
+                       def_count, (const u64 *)ops->op_off, ops->kind, ops->vkind, ops->actor, ops->key, ops->vactor,
+                       (const u64 *)ops->counter, (const u64 *)ops->vcounter, ops->clk_row,
+                       (const u64 *)ops->clk_pool, ops->clk_pool ? ops->n_clk_rows : 0, (const u64 *)ops->key_off,
+                       ops->keys, ops->keys ? ops->n_keys : 0, (const u64 *)ops->mem_off, ops->mems,
+                       ops->mems ? ops->n_mems : 0, ops->n_ops, status, wpb};
+  if (!ops->key_off) {  // (no Map-level Rm: every key range empty)
+    if (int rc = ensure_scratch(ctx, (ops->n_ops + 1) * 8)) return rc;
+    if (int rc = device_fill(ctx, ctx->scratch, (ops->n_ops + 1) * 8, 0)) return rc;
+    p.key_off = static_cast<const u64 *>(ctx->scratch);
+  }
+  const dim3 grid((unsigned)((N + wpb - 1) / wpb)), block(wpb * kWave);
+  const size_t lds = per_wave * wpb;
+  timing_begin(ctx, "map_orswot_apply");
+  if (A <= 64) hipLaunchKernelGGL(map_orswot_apply_kernel<1>, grid, block, lds, ctx->stream, p);
+  else if (A <= 128) hipLaunchKernelGGL(map_orswot_apply_kernel<2>, grid, block, lds, ctx->stream, p);
+  else if (A <= 256) hipLaunchKernelGGL(map_orswot_apply_kernel<4>, grid, block, lds, ctx->stream, p);
+  else hipLaunchKernelGGL(map_orswot_apply_kernel<8>, grid, block, lds, ctx->stream, p);
+  timing_end(ctx);
+  CRDT_HIP(ctx, hipGetLastError());
+  return CRDT_OK;
+}

@@ -1,0 +1,119 @@
+"""GPU: CmRDT::apply of Map<K, Orswot<M>> (round 5; crdt_map_orswot_apply_batch) against the oracle's
+Map.apply (map.rs:119-137) with Orswot::apply (orswot.rs:55-79, apply_rm :230-250, apply_deferred
+:281-286) inside and the Map's apply_keyset_rm / apply_deferred (:311-348, Orswot::forget :150-183):
+op-replay states folded alone, then streams of Orswot Adds (fresh / seen dots), Orswot Rms (clocks
+from the future: nested deferred removes, re-applied by later Adds), Map Rms (deferred at the Map
+level, re-applied by later Ups), at A within and past one lane word and M past 64."""
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+from gpu_util import to_dev, to_host
+
+pytestmark = pytest.mark.gpu
+
+import crdts_gpu as cg  # noqa: E402
+
+
+def _states(ctx, maps, K, M, A):
+    N = len(maps)
+    d = O.map_orswot_to_dense(maps, K, M, A)
+    D = d["def_row"].shape[0]
+    off = [0]
+    for m in maps:
+        off.append(off[-1] + len(m.deferred))
+    kw = dict(def_off=off, def_row=torch.zeros(D, dtype=torch.int32, device="cuda:0"),
+              def_clock=to_dev(d["def_clock"]), def_keys=to_dev(d["def_keys"])) if D else {}
+    Dv = int(d["vd_off"][-1])
+    vkw = dict(vd_clock=to_dev(d["vd_clock"]), vd_mem=to_dev(d["vd_members"])) if Dv else {}
+    shp = lambda x: to_dev(x.reshape((N, 1) + x.shape[1:]))  # noqa: E731
+    res = cg.map.orswot_lub_many(shp(d["clock"]), shp(d["ec"]), shp(d["oc"]), shp(d["ent"]), to_dev(d["vd_off"]),
+                                 ctx=ctx, **vkw, **kw)
+    return res, kw, off
+
+
+def _streams(rng, exps, K, M, A, T):
+    streams, oops = [], []
+    for m in exps:
+        clk = {a: m.clock.get(a) for a in range(A)}
+        occ = {}  # the Orswot clocks the stream has seen (per key), for fresh / seen nested dots
+        for k, e in m.entries.items():
+            occ[k] = {a: e.val.clock.get(a) for a in range(A)}
+        ops, oo = [], []
+        for _ in range(T):
+            x = rng.random()
+            if x < 0.8:
+                a = int(rng.integers(A))
+                c = clk[a] + int(rng.integers(1, 3)) if rng.random() < 0.85 else max(clk[a] - int(rng.integers(0, 2)), 1)
+                clk[a] = max(clk[a], c)
+                k = int(rng.integers(K))
+                oc = occ.setdefault(k, {a2: 0 for a2 in range(A)})
+                ms = sorted(set(int(z) for z in rng.choice(M, size=int(rng.integers(1, 3)), replace=False)))
+                if rng.random() < 0.65:  # Orswot Add
+                    va = int(rng.integers(A))
+                    vc = oc[va] + int(rng.integers(1, 3)) if rng.random() < 0.85 else max(oc[va], 1)
+                    oc[va] = max(oc[va], vc)
+                    ops.append(("add", a, c, k, va, vc, ms))
+                    oo.append(O.MapUp(O.Dot(a, c), k, O.OrswotAdd(O.Dot(va, vc), ms)))
+                else:  # Orswot Rm, its clock up to 2 ahead of the seen Orswot clock on some actors
+                    row = {a2: max(0, oc[a2] + int(rng.integers(-2, 3))) for a2 in range(A) if rng.random() < 0.6}
+                    row = {a2: v for a2, v in row.items() if v}
+                    ops.append(("orm", a, c, k, row, ms))
+                    oo.append(O.MapUp(O.Dot(a, c), k, O.OrswotRm(O.VClock(dict(row)), ms)))
+            else:  # Map Rm
+                row = {a2: max(0, clk[a2] + int(rng.integers(-3, 3))) for a2 in range(A) if rng.random() < 0.5}
+                row = {a2: v for a2, v in row.items() if v}
+                ks = sorted(set(int(z) for z in rng.choice(K, size=int(rng.integers(1, 3)), replace=False)))
+                ops.append(("rm", row, ks))
+                oo.append(O.MapRm(O.VClock(dict(row)), ks))
+        streams.append(ops)
+        oops.append(oo)
+    return streams, oops
+
+
+@pytest.mark.parametrize("M,A,seed", [(4, 5, 1), (3, 6, 2), (70, 6, 3), (4, 80, 4)])
+def test_map_orswot_apply(gpu_ctx, M, A, seed):
+    N, K, T, Dcap = 16, 4, 30, 16
+    maps = O.map_orswot_objects(N, K, M, A, seed=60 + seed, steps=160, p_vrm=0.4)
+    res, kw, off = _states(gpu_ctx, maps, K, M, A)
+    exps = [O.map_fold_objects([m]) for m in maps]
+    rng = np.random.default_rng(seed)
+    streams, oops = _streams(rng, exps, K, M, A, T)
+    for n in range(N):
+        for op in oops[n]:
+            exps[n].apply(op)
+    if any(len(e.val.deferred) > cg.map.VD_CAP for x in exps for e in x.entries.values()) or \
+            any(len(x.deferred) > Dcap for x in exps):
+        pytest.skip("past the kernel's deferred capacity")
+    Kw = (K + 63) // 64
+    dcl = np.zeros((N, Dcap, A), np.uint64)
+    dks = np.zeros((N, Dcap, Kw), np.uint64)
+    cnt = np.zeros(N, np.int32)
+    if kw:
+        keep, hk, hc = res.def_keep.cpu().numpy(), to_host(res.def_keys), to_host(kw["def_clock"])
+        for n in range(N):
+            for j in range(off[n], off[n + 1]):
+                if keep[j]:
+                    dcl[n, cnt[n]], dks[n, cnt[n]] = hc[j], hk[j]
+                    cnt[n] += 1
+    tdc, tdk, tcnt = to_dev(dcl), to_dev(dks), torch.from_numpy(cnt).cuda()
+    ops = cg.map.encode_orswot_map_ops(streams, A, "cuda:0")
+    status = cg.map.orswot_apply_batch(res, tdc, tdk, tcnt, ops, ctx=gpu_ctx).cpu().numpy()
+    c, e, o, m = to_host(res.clock), to_host(res.ec), to_host(res.oc), to_host(res.ent)
+    vn, vc, vm = res.vd_n.cpu().numpy(), to_host(res.vd_clock), to_host(res.vd_mem)
+    hdc, hdk, hcnt = to_host(tdc), to_host(tdk), tcnt.cpu().numpy()
+    nested = mapdef = 0
+    for n in range(N):
+        assert status[n] == 0, (n, status[n])
+        mw = (lambda k, i: vm[n, k, i]) if vm.ndim == 4 else (lambda k, i: vm[n, k, i:i + 1])  # noqa: E731
+        vd = {k: [(vc[n, k, i], O.bitmap_members(mw(k, i))) for i in range(int(vn[n, k]))] for k in range(K)}
+        dfr = [(hdc[n, i], O.bitmap_members(hdk[n, i])) for i in range(int(hcnt[n]))]
+        got = O.dense_to_map_orswot(c[n], e[n], o[n], m[n], vd, dfr)
+        exp = exps[n]
+        assert got.clock == exp.clock, n
+        assert got.entries == exp.entries, n
+        assert got.deferred == exp.deferred, n
+        nested += sum(len(x.val.deferred) for x in exp.entries.values())
+        mapdef += len(exp.deferred)
+    assert nested > 0 and mapdef > 0
