@@ -1030,6 +1030,28 @@ int crdt_map_ingest(crdt_ctx *ctx, const uint8_t *bytes, const uint64_t *frame_o
                     uint32_t *status);
 int crdt_map_egress(crdt_ctx *ctx, const crdt_map_states *states, const crdt_map_deferred *def, const uint32_t *actors,
                     const uint32_t *keys, uint64_t *frame_off, uint8_t *bytes, size_t cap, size_t *total);
+/* The value-typed Maps (round 5): Map<u32, GCounter<u32>, u32> / Map<u32, PNCounter<u32>, u32>
+ * (W = 1 / 2) frames <-> packed crdt_map_counter_states: clock_stride A, ec_stride K*A, val_stride
+ * K*W*A; and Map<u32, Orswot<u64, u32>, u32> frames <-> crdt_map_orswot_states: the nested Orswot's
+ * clock oc, member dots ent by the sorted u64 `members` dictionary, its deferred removes in slots
+ * 0 .. vd_n[s][k] < 16 with member bitmaps vd_mem [N][K][16][ceil(M/64)]; the Map's deferred removes
+ * in per-state slots, a crdt_map_deferred.  Value encodings: GCounter = VClock, PNCounter = VClock p,
+ * VClock n, Orswot as crdt_orswot_ingest.  Ingest status bits as above (4 = a state held more than
+ * Dcap Map removes or a key's Orswot more than 16: the excess was dropped).  Egress writes present
+ * keys ascending (entry clock nonzero), present members ascending (dot row nonzero), vd_n nested
+ * removes and count[s] Map removes with their ids ascending. */
+int crdt_map_counter_ingest(crdt_ctx *ctx, const uint8_t *bytes, const uint64_t *frame_off, const uint32_t *actors,
+                            const uint32_t *keys, const crdt_map_counter_states *out, const crdt_map_deferred *out_def,
+                            uint32_t *status);
+int crdt_map_counter_egress(crdt_ctx *ctx, const crdt_map_counter_states *states, const crdt_map_deferred *def,
+                            const uint32_t *actors, const uint32_t *keys, uint64_t *frame_off, uint8_t *bytes,
+                            size_t cap, size_t *total);
+int crdt_map_orswot_ingest(crdt_ctx *ctx, const uint8_t *bytes, const uint64_t *frame_off, const uint32_t *actors,
+                           const uint32_t *keys, const uint64_t *members, const crdt_map_orswot_states *out,
+                           const crdt_map_deferred *out_def, uint32_t *status);
+int crdt_map_orswot_egress(crdt_ctx *ctx, const crdt_map_orswot_states *states, const crdt_map_deferred *def,
+                           const uint32_t *actors, const uint32_t *keys, const uint64_t *members, uint64_t *frame_off,
+                           uint8_t *bytes, size_t cap, size_t *total);
 
 /* ---- synthetic inputs (bench / test data, generated in HBM) --------------------------------
  * Counter-based and reproducible on the CPU (oracle/oracle.py synth_* restates them; small

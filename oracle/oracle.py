@@ -1875,6 +1875,89 @@ def unbc_orswot(b: bytes, pos: int = 0):
     return clock, entries, deferred, pos
 
 
+def bc_map_obj(m, aid, kid, mid=None) -> bytes:
+    """A value-typed Map object (Map<u32, GCounter / PNCounter / Orswot<u64>, u32>, map.rs:31-47 with
+    gcounter.rs:25-28, pncounter.rs:28-32, orswot.rs:20-25 inside) -> bincode, its dense actor / key /
+    member indices mapped to ids through aid / kid / mid (ascending sequences, so index order is id
+    order).  Entries by key (BTreeMap), Orswot members ascending (a HashMap: any order decodes the
+    same; ascending is what crdt_map_*_egress writes), removes in the dict's order."""
+    vc = lambda v: bc_vclock({int(aid[a]): c for a, c in v.dots.items()})  # noqa: E731
+
+    def val(v):
+        if isinstance(v, GCounter):
+            return vc(v.inner)
+        if isinstance(v, PNCounter):
+            return vc(v.p.inner) + vc(v.n.inner)
+        out = vc(v.clock) + _st.pack("<Q", len(v.entries))
+        for x in sorted(v.entries):
+            out += _st.pack("<Q", int(mid[x])) + vc(v.entries[x])
+        out += _st.pack("<Q", len(v.deferred))
+        for rm, mems in v.deferred.items():
+            ms = sorted(int(mid[x]) for x in mems)
+            out += vc(rm) + _st.pack("<Q", len(ms)) + b"".join(_st.pack("<Q", x) for x in ms)
+        return out
+
+    out = vc(m.clock) + _st.pack("<Q", len(m.entries))
+    for k in sorted(m.entries):
+        e = m.entries[k]
+        out += _st.pack("<I", int(kid[k])) + vc(e.clock) + val(e.val)
+    out += _st.pack("<Q", len(m.deferred))
+    for rm, keys in m.deferred.items():
+        kk = sorted(int(kid[x]) for x in keys)
+        out += vc(rm) + _st.pack("<Q", len(kk)) + b"".join(_st.pack("<I", x) for x in kk)
+    return out
+
+
+def unbc_map_obj(b: bytes, vnew, aid, kid, mid=None, pos: int = 0):
+    """Inverse of bc_map_obj -> (Map object over dense indices, pos); vnew = GCounter, PNCounter or
+    Orswot.  Removes with equal clocks union their sets (the HashMap keyed by the clock)."""
+    ai = {int(x): i for i, x in enumerate(aid)}
+    ki = {int(x): i for i, x in enumerate(kid)}
+    mi = {int(x): i for i, x in enumerate(mid)} if mid is not None else {}
+
+    def vc(pos):
+        d, pos = unbc_vclock(b, pos)
+        return VClock({ai[a]: c for a, c in d.items()}), pos
+
+    m = Map(vnew)
+    m.clock, pos = vc(pos)
+    (n,) = _st.unpack_from("<Q", b, pos)
+    pos += 8
+    for _ in range(n):
+        (k,) = _st.unpack_from("<I", b, pos)
+        ec, pos = vc(pos + 4)
+        v = vnew()
+        if vnew is GCounter:
+            v.inner, pos = vc(pos)
+        elif vnew is PNCounter:
+            v.p.inner, pos = vc(pos)
+            v.n.inner, pos = vc(pos)
+        else:
+            v.clock, pos = vc(pos)
+            (ne,) = _st.unpack_from("<Q", b, pos)
+            pos += 8
+            for _ in range(ne):
+                (x,) = _st.unpack_from("<Q", b, pos)
+                v.entries[mi[x]], pos = vc(pos + 8)
+            (nd,) = _st.unpack_from("<Q", b, pos)
+            pos += 8
+            for _ in range(nd):
+                rm, pos = vc(pos)
+                (j,) = _st.unpack_from("<Q", b, pos)
+                v.deferred.setdefault(rm, set()).update(mi[_st.unpack_from("<Q", b, pos + 8 + 8 * i)[0]]
+                                                        for i in range(j))
+                pos += 8 + 8 * j
+        m.entries[ki[k]] = MapEntry(ec, v)
+    (d,) = _st.unpack_from("<Q", b, pos)
+    pos += 8
+    for _ in range(d):
+        rm, pos = vc(pos)
+        (j,) = _st.unpack_from("<Q", b, pos)
+        m.deferred.setdefault(rm, set()).update(ki[_st.unpack_from("<I", b, pos + 8 + 4 * i)[0]] for i in range(j))
+        pos += 8 + 4 * j
+    return m, pos
+
+
 def frames(blobs, align: int = 4):
     """Concatenate frames (each padded to `align` bytes by construction) -> (bytes, offsets)."""
     off = [0]

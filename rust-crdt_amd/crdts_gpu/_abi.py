@@ -56,6 +56,7 @@ EXPORTS = (
     "crdt_map_nested_lub_many", "crdt_map_counter_lub_many_sharded", "crdt_map_orswot_lub_many_sharded",
     "crdt_map_nested_lub_many_sharded", "crdt_map_counter_forget_batch", "crdt_map_orswot_forget_batch",
     "crdt_map_counter_apply_batch", "crdt_map_orswot_apply_batch",
+    "crdt_map_counter_ingest", "crdt_map_counter_egress", "crdt_map_orswot_ingest", "crdt_map_orswot_egress",
 )
 
 
@@ -279,6 +280,14 @@ _SIGS = {
     "crdt_gset_apply_batch": ([P, P, S, S, S, P, P, S, P], ctypes.c_int),
 }
 _SIGS.update({
+    "crdt_map_counter_ingest": ([P, P, P, P, P, ctypes.POINTER(MapCounterStates), ctypes.POINTER(MapDeferred), P],
+                                ctypes.c_int),
+    "crdt_map_counter_egress": ([P, ctypes.POINTER(MapCounterStates), ctypes.POINTER(MapDeferred), P, P, P, P, S,
+                                 ctypes.POINTER(S)], ctypes.c_int),
+    "crdt_map_orswot_ingest": ([P, P, P, P, P, P, ctypes.POINTER(MapOrswotStates), ctypes.POINTER(MapDeferred), P],
+                               ctypes.c_int),
+    "crdt_map_orswot_egress": ([P, ctypes.POINTER(MapOrswotStates), ctypes.POINTER(MapDeferred), P, P, P, P, P, S,
+                                ctypes.POINTER(S)], ctypes.c_int),
     "crdt_orswot_forget_batch": ([P, P, S, P, S, S, S, S, S, P, S, P, P, S, P], ctypes.c_int),
     "crdt_map_forget_batch": ([P, ctypes.POINTER(MapStates), P, S, P, P, S, P], ctypes.c_int),
     "crdt_map_counter_forget_batch": ([P, ctypes.POINTER(MapCounterStates), P, S, P, P, S, P], ctypes.c_int),

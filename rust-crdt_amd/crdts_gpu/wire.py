@@ -224,3 +224,149 @@ def map_egress(states, actors: torch.Tensor, keys: torch.Tensor, ctx: Optional[C
     s, d = _map_states_structs(ctx, states, "wire.map_egress")
     return _egress(ctx, "crdt_map_egress", states.clock.shape[0], states.clock.device, ctypes.byref(s), ctypes.byref(d),
                    dptr(actors), dptr(keys))
+
+
+# ---- the value-typed Maps (round 5) ---------------------------------------------------------------
+class MapCounterFrames(NamedTuple):
+    """Map<u32, GCounter / PNCounter> states in the crdt_map_counter_states layout + deferred slots."""
+    clock: torch.Tensor      # (N, A)
+    ec: torch.Tensor         # (N, K, A)
+    val: torch.Tensor        # (N, K, W, A)
+    def_clock: torch.Tensor  # (N, Dcap, A)
+    def_keys: torch.Tensor   # (N, Dcap, Kw)
+    def_count: torch.Tensor  # (N,) int32
+
+
+class MapOrswotFrames(NamedTuple):
+    """Map<u32, Orswot<u64>> states in the crdt_map_orswot_states layout (the field names of
+    map.MapOrswotLub, so map.orswot_apply_batch / orswot_forget_batch take it) + deferred slots."""
+    clock: torch.Tensor      # (N, A)
+    ec: torch.Tensor         # (N, K, A)
+    oc: torch.Tensor         # (N, K, A)
+    ent: torch.Tensor        # (N, K, M, A)
+    vd_n: torch.Tensor       # (N, K) int32
+    vd_clock: torch.Tensor   # (N, K, 16, A)
+    vd_mem: torch.Tensor     # (N, K, 16) member bitmasks ((N, K, 16, Mw) past M = 64)
+    def_clock: torch.Tensor  # (N, Dcap, A)
+    def_keys: torch.Tensor   # (N, Dcap, Kw)
+    def_count: torch.Tensor  # (N,) int32
+
+
+def _vmap_deferred(st):
+    from . import _abi
+    d = _abi.MapDeferred()
+    Dcap = st.def_clock.shape[1]
+    d.clock = dptr(st.def_clock) if Dcap else None
+    d.keys = dptr(st.def_keys) if Dcap else None
+    d.count = dptr(st.def_count)
+    d.Dcap = Dcap
+    return d
+
+
+def _vmap_check(ctx, st, what):
+    for nm, t in st._asdict().items():
+        ctx.check_tensor(t, f"{what}({nm})", (torch.int32,) if nm in ("vd_n", "def_count") else None)
+        if not t.is_contiguous():
+            raise ValueError(f"{what}: {nm} must be contiguous")
+    N, A = st.clock.shape
+    Dcap = st.def_clock.shape[1]
+    K = st.ec.shape[1]
+    if tuple(st.def_clock.shape) != (N, Dcap, A) or tuple(st.def_keys.shape) != (N, Dcap, (K + 63) // 64) \
+            or tuple(st.def_count.shape) != (N,) or st.def_count.dtype != torch.int32:
+        raise ValueError(f"{what}: deferred slots must be (N, Dcap, A), (N, Dcap, ceil(K/64)), (N,) int32")
+    return N, K, A
+
+
+def _counter_struct(ctx, st, what):
+    from . import _abi
+    N, K, A = _vmap_check(ctx, st, what)
+    W = st.val.shape[2]
+    if tuple(st.ec.shape) != (N, K, A) or tuple(st.val.shape) != (N, K, W, A) or W not in (1, 2):
+        raise ValueError(f"{what}: clock (N, A), ec (N, K, A), val (N, K, W, A) with W = 1 or 2 expected")
+    s = _abi.MapCounterStates()
+    s.N, s.K, s.A, s.W = N, K, A, W
+    s.clock, s.clock_stride = dptr(st.clock), A
+    s.ec, s.ec_stride = dptr(st.ec), K * A
+    s.val, s.val_stride = dptr(st.val), K * W * A
+    return s, _vmap_deferred(st)
+
+
+def _orswot_struct(ctx, st, what):
+    from . import _abi
+    N, K, A = _vmap_check(ctx, st, what)
+    M = st.ent.shape[2]
+    Mw = (M + 63) // 64
+    vm = (N, K, 16) if Mw == 1 else (N, K, 16, Mw)
+    if (tuple(st.oc.shape) != (N, K, A) or tuple(st.ent.shape) != (N, K, M, A) or tuple(st.vd_n.shape) != (N, K)
+            or tuple(st.vd_clock.shape) != (N, K, 16, A) or tuple(st.vd_mem.shape) != vm):
+        raise ValueError(f"{what}: the crdt_map_orswot_states shapes expected")
+    s = _abi.MapOrswotStates()
+    s.N, s.K, s.M, s.A = N, K, M, A
+    s.clock, s.ec, s.oc, s.ent = dptr(st.clock), dptr(st.ec), dptr(st.oc), dptr(st.ent)
+    s.vd_n, s.vd_clock, s.vd_mem = dptr(st.vd_n), dptr(st.vd_clock), dptr(st.vd_mem)
+    return s, _vmap_deferred(st)
+
+
+def map_counter_ingest(data: torch.Tensor, frame_off: torch.Tensor, actors: torch.Tensor, keys: torch.Tensor,
+                       W: int, Dcap: int, ctx: Optional[Context] = None):
+    """Map<u32, GCounter<u32>> (W = 1) / Map<u32, PNCounter<u32>> (W = 2) frames ->
+    (MapCounterFrames, status (N,) int32); keys: sorted u32 key dictionary (int32 tensor)."""
+    ctx = _ctx(data, ctx)
+    N = _frames(ctx, data, frame_off, "wire.map_counter_ingest")
+    A = _dict(ctx, actors, torch.int32, "wire.map_counter_ingest(actors)")
+    K = _dict(ctx, keys, torch.int32, "wire.map_counter_ingest(keys)")
+    dev = data.device
+    z = lambda *shape: torch.zeros(shape, dtype=torch.int64, device=dev)  # noqa: E731
+    st = MapCounterFrames(z(N, A), z(N, K, A), z(N, K, W, A), z(N, Dcap, A), z(N, Dcap, (K + 63) // 64),
+                          torch.zeros(N, dtype=torch.int32, device=dev))
+    s, d = _counter_struct(ctx, st, "wire.map_counter_ingest")
+    status = _status(N, dev)
+    ctx.call("crdt_map_counter_ingest", _ptr_or_dummy(data), dptr(frame_off), dptr(actors), dptr(keys),
+             ctypes.byref(s), ctypes.byref(d), dptr(status))
+    return st, status
+
+
+def map_counter_egress(states: MapCounterFrames, actors: torch.Tensor, keys: torch.Tensor,
+                       ctx: Optional[Context] = None):
+    """MapCounterFrames -> (frame_off (N+1,), bytes)."""
+    ctx = _ctx(states.clock, ctx)
+    _dict(ctx, actors, torch.int32, "wire.map_counter_egress(actors)")
+    _dict(ctx, keys, torch.int32, "wire.map_counter_egress(keys)")
+    s, d = _counter_struct(ctx, states, "wire.map_counter_egress")
+    return _egress(ctx, "crdt_map_counter_egress", states.clock.shape[0], states.clock.device, ctypes.byref(s),
+                   ctypes.byref(d), dptr(actors), dptr(keys))
+
+
+def map_orswot_ingest(data: torch.Tensor, frame_off: torch.Tensor, actors: torch.Tensor, keys: torch.Tensor,
+                      members: torch.Tensor, Dcap: int, ctx: Optional[Context] = None):
+    """Map<u32, Orswot<u64, u32>> frames -> (MapOrswotFrames, status (N,) int32); members: sorted
+    u64 member dictionary (int64 tensor)."""
+    ctx = _ctx(data, ctx)
+    N = _frames(ctx, data, frame_off, "wire.map_orswot_ingest")
+    A = _dict(ctx, actors, torch.int32, "wire.map_orswot_ingest(actors)")
+    K = _dict(ctx, keys, torch.int32, "wire.map_orswot_ingest(keys)")
+    M = _dict(ctx, members, torch.int64, "wire.map_orswot_ingest(members)")
+    dev = data.device
+    Mw = (M + 63) // 64
+    z = lambda *shape: torch.zeros(shape, dtype=torch.int64, device=dev)  # noqa: E731
+    st = MapOrswotFrames(z(N, A), z(N, K, A), z(N, K, A), z(N, K, M, A),
+                         torch.zeros((N, K), dtype=torch.int32, device=dev), z(N, K, 16, A),
+                         z(N, K, 16) if Mw == 1 else z(N, K, 16, Mw), z(N, Dcap, A), z(N, Dcap, (K + 63) // 64),
+                         torch.zeros(N, dtype=torch.int32, device=dev))
+    s, d = _orswot_struct(ctx, st, "wire.map_orswot_ingest")
+    status = _status(N, dev)
+    ctx.call("crdt_map_orswot_ingest", _ptr_or_dummy(data), dptr(frame_off), dptr(actors), dptr(keys),
+             dptr(members), ctypes.byref(s), ctypes.byref(d), dptr(status))
+    return st, status
+
+
+def map_orswot_egress(states: MapOrswotFrames, actors: torch.Tensor, keys: torch.Tensor, members: torch.Tensor,
+                      ctx: Optional[Context] = None):
+    """MapOrswotFrames -> (frame_off (N+1,), bytes)."""
+    ctx = _ctx(states.clock, ctx)
+    _dict(ctx, actors, torch.int32, "wire.map_orswot_egress(actors)")
+    _dict(ctx, keys, torch.int32, "wire.map_orswot_egress(keys)")
+    _dict(ctx, members, torch.int64, "wire.map_orswot_egress(members)")
+    s, d = _orswot_struct(ctx, states, "wire.map_orswot_egress")
+    return _egress(ctx, "crdt_map_orswot_egress", states.clock.shape[0], states.clock.device, ctypes.byref(s),
+                   ctypes.byref(d), dptr(actors), dptr(keys), dptr(members))

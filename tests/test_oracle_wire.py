@@ -54,3 +54,35 @@ def test_map_bincode_round_trip_and_layout():
     assert struct.unpack_from("<QIQIQ", b, 0) == (2, 2, 9, 7, 3)
     # entries: count, then key 5 first
     assert struct.unpack_from("<QI", b, 32) == (2, 5)
+
+
+def test_value_map_bincode_round_trips_and_layout():
+    """Map<u32, GCounter / PNCounter / Orswot<u64>> (map.rs:31-47 with gcounter.rs:25-28,
+    pncounter.rs:28-32, orswot.rs:20-25 as the value): decode(encode(m)) == m over op-replay states
+    with deferred removes at both levels, and the byte layout of a small one by hand."""
+    aid = [3, 10, 11, 40, 41, 90]
+    kid = [2, 7, 8, 100, 101]
+    mid = [5, 6, 2**40, 2**40 + 1, 2**62]
+    for W, vnew in ((1, O.GCounter), (2, O.PNCounter)):
+        maps = O.map_counter_objects(12, 5, 6, W, seed=40, steps=200)
+        assert sum(len(m.deferred) for m in maps) > 0
+        for m in maps:
+            b = O.bc_map_obj(m, aid, kid)
+            got, pos = O.unbc_map_obj(b, vnew, aid, kid)
+            assert pos == len(b) and got == m
+    maps = O.map_orswot_objects(12, 5, 5, 6, seed=55, steps=200, p_vrm=0.45)
+    assert sum(len(e.val.deferred) for m in maps for e in m.entries.values()) > 0
+    for m in maps:
+        b = O.bc_map_obj(m, aid, kid, mid)
+        got, pos = O.unbc_map_obj(b, O.Orswot, aid, kid, mid)
+        assert pos == len(b) and got == m
+    # by hand: Map<u32, PNCounter>: clock {a0: 2}, key 1 -> (entry clock {a0: 2}, p {a0: 1}, n {a0: 1})
+    m = O.Map(O.PNCounter)
+    m.clock = O.VClock({0: 2})
+    v = O.PNCounter()
+    v.p.inner, v.n.inner = O.VClock({0: 1}), O.VClock({0: 1})
+    m.entries[1] = O.MapEntry(O.VClock({0: 2}), v)
+    m.deferred[O.VClock({1: 4})] = {0, 2}
+    b = O.bc_map_obj(m, aid, kid)
+    assert b == (O.bc_vclock({3: 2}) + struct.pack("<QI", 1, 7) + O.bc_vclock({3: 2}) + O.bc_vclock({3: 1})
+                 + O.bc_vclock({3: 1}) + struct.pack("<Q", 1) + O.bc_vclock({10: 4}) + struct.pack("<QII", 2, 2, 8))
