@@ -852,6 +852,68 @@ int crdt_map_nested_lub_many(crdt_ctx *ctx, const crdt_map_nested_batch *in, crd
 int crdt_map_nested_lub_many_sharded(crdt_ctx *ctx, const crdt_map_nested_batch *in, size_t k0, size_t K,
                                      crdt_map_nested_out *out);
 
+/* Map<K, Map<K2, MVReg<u64>>> states in place (round 5), on the crdt_map_nested_lub_many output layout
+ * with N states (packed; 8 MVReg slots per inner key in Vec order, nval used, the rest zero; 16 inner
+ * deferred removes per key with one inner-key mask each):
+ *   crdt_map_nested_apply_batch — CmRDT::apply (map.rs:119-137, apply_keyset_rm :318-348,
+ *     apply_deferred :311-316) with the inner Map's apply one level down and MVReg::apply
+ *     (mvreg.rs:130-166) innermost: state s applies ops [op_off[s], op_off[s+1]) in order; the outer
+ *     deferred removes as crdt_map_counter_apply_batch (def_count[s] <= Dcap slots).  Ops: kind 0 =
+ *     Op::Up { dot: (actor, counter), key, op } with ikind 0 = inner Op::Up { dot: (iactor, icounter),
+ *     key: ikey, op: Put { clock: clk_pool[clk_row*A ..], val } } or 1 = inner Op::Rm { clock:
+ *     clk_pool[clk_row*A ..], keyset: the inner-key mask ikeys }; kind 1 = Op::Rm { clock:
+ *     clk_pool[clk_row*A ..], keyset: keys[key_off[o] .. key_off[o+1]) } (key_off may be NULL when no
+ *     op is an outer Rm).  status[s]: bit 0 = a deferred list (outer Dcap or an inner one's 16)
+ *     exhausted, bit 1 = a malformed op skipped whole, bits 2-3 = invalid input (state untouched),
+ *     bit 4 = a register needed more than 8 values (that value was not added).
+ *   crdt_map_nested_forget_batch — Causal::forget (map.rs:85-114) of the whole state by y[s] (y_stride
+ *     0: one row for all): entry clocks, the inner Maps (their entries, registers — MVReg::forget
+ *     mvreg.rs:88-104, emptied values dropped, order kept —, deferred removes, clocks), an emptied
+ *     entry dropped; the outer deferred pool and the map clock as crdt_map_forget_batch.  Inner removes
+ *     whose clocks become equal keep one entry with the later one's keys (the fold's rule).
+ * Limits: A <= 512, K2 <= 64.  Device memory only. */
+typedef struct crdt_map_nested_states {
+  size_t N, K, K2, A;
+  uint64_t *clock;    /* [N][A]           */
+  uint64_t *ec;       /* [N][K][A]        */
+  uint64_t *ic;       /* [N][K][A]        */
+  uint64_t *iec;      /* [N][K][K2][A]    */
+  uint64_t *ivc;      /* [N][K][K2][8][A] */
+  uint64_t *ivv;      /* [N][K][K2][8]    */
+  uint32_t *nval;     /* [N][K][K2]       */
+  uint32_t *id_n;     /* [N][K]           */
+  uint64_t *id_clock; /* [N][K][16][A]    */
+  uint64_t *id_keys;  /* [N][K][16]       */
+} crdt_map_nested_states;
+
+typedef struct crdt_map_nested_ops {
+  size_t n_ops;
+  const uint64_t *op_off;    /* [N+1]       */
+  const uint8_t *kind;       /* [n_ops] 0 = Op::Up, 1 = Op::Rm */
+  const uint32_t *actor;     /* [n_ops] Up: the outer dot */
+  const uint64_t *counter;   /* [n_ops] Up  */
+  const uint32_t *key;       /* [n_ops] Up  */
+  const uint8_t *ikind;      /* [n_ops] Up: 0 inner Up (Put), 1 inner Rm */
+  const uint32_t *iactor;    /* [n_ops] inner Up: its dot */
+  const uint64_t *icounter;  /* [n_ops] inner Up */
+  const uint32_t *ikey;      /* [n_ops] inner Up: the inner key */
+  const uint64_t *val;       /* [n_ops] inner Up: the Put's value */
+  const uint64_t *ikeys;     /* [n_ops] inner Rm: inner-key mask */
+  const uint32_t *clk_row;   /* [n_ops] the Put clock / an rm clock: row of clk_pool */
+  const uint64_t *clk_pool;  /* [n_clk_rows][A] */
+  size_t n_clk_rows;
+  const uint64_t *key_off;   /* [n_ops+1] outer Rm keysets */
+  const uint32_t *keys;      /* [n_keys]    */
+  size_t n_keys;
+} crdt_map_nested_ops;
+
+int crdt_map_nested_apply_batch(crdt_ctx *ctx, const crdt_map_nested_states *states, uint64_t *def_clock,
+                                uint64_t *def_keys, uint32_t *def_count, size_t Dcap,
+                                const crdt_map_nested_ops *ops, uint32_t *status);
+int crdt_map_nested_forget_batch(crdt_ctx *ctx, const crdt_map_nested_states *states, const uint64_t *y,
+                                 size_t y_stride, uint64_t *def_clock, const uint32_t *def_state, size_t D,
+                                 uint8_t *def_keep);
+
 /* ---- MVReg<u64, A> on its own (outside a Map) ------------------------------------------------
  * Replaces MVReg::merge (mvreg.rs:112-128) and MVReg::apply (mvreg.rs:130-166) for registers in the
  * dense layout the Map entry points use for their values: slots in Vec order, slot s of register i

@@ -56,6 +56,7 @@ EXPORTS = (
     "crdt_map_nested_lub_many", "crdt_map_counter_lub_many_sharded", "crdt_map_orswot_lub_many_sharded",
     "crdt_map_nested_lub_many_sharded", "crdt_map_counter_forget_batch", "crdt_map_orswot_forget_batch",
     "crdt_map_counter_apply_batch", "crdt_map_orswot_apply_batch",
+    "crdt_map_nested_apply_batch", "crdt_map_nested_forget_batch",
     "crdt_map_counter_ingest", "crdt_map_counter_egress", "crdt_map_orswot_ingest", "crdt_map_orswot_egress",
 )
 
@@ -123,6 +124,17 @@ class MapCounterStates(ctypes.Structure):  # crdt_map_counter_states
 class MapOrswotStates(ctypes.Structure):  # crdt_map_orswot_states
     _fields_ = [("N", S), ("K", S), ("M", S), ("A", S), ("clock", P), ("ec", P), ("oc", P), ("ent", P),
                 ("vd_n", P), ("vd_clock", P), ("vd_mem", P)]
+
+
+class MapNestedStates(ctypes.Structure):  # crdt_map_nested_states
+    _fields_ = [("N", S), ("K", S), ("K2", S), ("A", S), ("clock", P), ("ec", P), ("ic", P), ("iec", P), ("ivc", P),
+                ("ivv", P), ("nval", P), ("id_n", P), ("id_clock", P), ("id_keys", P)]
+
+
+class MapNestedOps(ctypes.Structure):  # crdt_map_nested_ops
+    _fields_ = [("n_ops", S), ("op_off", P), ("kind", P), ("actor", P), ("counter", P), ("key", P), ("ikind", P),
+                ("iactor", P), ("icounter", P), ("ikey", P), ("val", P), ("ikeys", P), ("clk_row", P),
+                ("clk_pool", P), ("n_clk_rows", S), ("key_off", P), ("keys", P), ("n_keys", S)]
 
 
 class MapCounterOps(ctypes.Structure):  # crdt_map_counter_ops
@@ -280,6 +292,9 @@ _SIGS = {
     "crdt_gset_apply_batch": ([P, P, S, S, S, P, P, S, P], ctypes.c_int),
 }
 _SIGS.update({
+    "crdt_map_nested_apply_batch": ([P, ctypes.POINTER(MapNestedStates), P, P, P, S, ctypes.POINTER(MapNestedOps), P],
+                                    ctypes.c_int),
+    "crdt_map_nested_forget_batch": ([P, ctypes.POINTER(MapNestedStates), P, S, P, P, S, P], ctypes.c_int),
     "crdt_map_counter_ingest": ([P, P, P, P, P, ctypes.POINTER(MapCounterStates), ctypes.POINTER(MapDeferred), P],
                                 ctypes.c_int),
     "crdt_map_counter_egress": ([P, ctypes.POINTER(MapCounterStates), ctypes.POINTER(MapDeferred), P, P, P, P, S,

@@ -1011,3 +1011,133 @@ def orswot_apply_batch(res: "MapOrswotLub", def_clock: torch.Tensor, def_keys: t
     ctx.call("crdt_map_orswot_apply_batch", ctypes.byref(st), def_clock.data_ptr(), def_keys.data_ptr(),
              def_count.data_ptr(), Dcap, ctypes.byref(o), status.data_ptr())
     return status
+
+
+# ---- CmRDT::apply and Causal::forget of Map<K, Map<K2, MVReg>> (round 5) ----------------------------
+class MapNestedOpBatch(NamedTuple):
+    """Device op streams (crdt_map_nested_ops): state s applies ops [op_off[s], op_off[s+1]) in order."""
+    op_off: torch.Tensor    # (N+1,) int64
+    kind: torch.Tensor      # (n_ops,) uint8: 0 = Op::Up, 1 = Op::Rm
+    actor: torch.Tensor     # (n_ops,) int32   Up: the outer dot
+    counter: torch.Tensor   # (n_ops,) int64
+    key: torch.Tensor       # (n_ops,) int32
+    ikind: torch.Tensor     # (n_ops,) uint8   Up: 0 inner Up (MVReg Put), 1 inner Rm
+    iactor: torch.Tensor    # (n_ops,) int32   inner Up: its dot
+    icounter: torch.Tensor  # (n_ops,) int64
+    ikey: torch.Tensor      # (n_ops,) int32
+    val: torch.Tensor       # (n_ops,) int64   inner Up: the Put's value
+    ikeys: torch.Tensor     # (n_ops,) int64   inner Rm: inner-key mask
+    clk_row: torch.Tensor   # (n_ops,) int32   the Put clock / an rm clock
+    clk_pool: torch.Tensor  # (n_clk, A) int64
+    key_off: torch.Tensor   # (n_ops+1,) int64 outer Rm keysets
+    keys: torch.Tensor      # (n_keys,) int32
+
+
+def encode_nested_ops(streams, A: int, device) -> MapNestedOpBatch:
+    """Host ingest of per-state op streams: ("put", actor, counter, key, iactor, icounter, ikey, clock, val)
+    for Op::Up { dot, key, op: inner Op::Up { dot, key, op: Put { clock, val } } }, ("irm", actor,
+    counter, key, clock, ikeys) for Op::Up with an inner Op::Rm { clock, keyset }, ("rm", clock, keys)
+    for Op::Rm (clocks: mapping actor -> counter or a row)."""
+    def row(clk):
+        r = np.zeros(A, dtype=np.uint64)
+        if hasattr(clk, "items"):
+            for a, c in clk.items():
+                r[int(a)] = np.uint64(c)
+        else:
+            r[:] = np.asarray(clk, dtype=np.uint64)
+        return r
+
+    names = ("kind", "actor", "counter", "key", "ikind", "iactor", "icounter", "ikey", "val", "ikeys", "clk_row")
+    f = {n: [] for n in names}
+    op_off, key_off, keys, pool = [0], [0], [], []
+    for ops in streams:
+        for op in ops:
+            v = dict.fromkeys(names, 0)
+            if op[0] == "put":
+                _, a, c, k, ia, ic, j, rc, x = op
+                v.update(actor=a, counter=c, key=k, iactor=ia, icounter=ic, ikey=j, val=x, clk_row=len(pool))
+            elif op[0] == "irm":
+                _, a, c, k, rc, js = op
+                v.update(actor=a, counter=c, key=k, ikind=1, ikeys=sum(1 << int(j) for j in set(js)), clk_row=len(pool))
+            else:
+                _, rc, ks = op
+                v.update(kind=1, clk_row=len(pool))
+                keys.extend(int(x) for x in ks)
+            pool.append(row(rc))
+            for n, x in v.items():
+                f[n].append(int(x))
+            key_off.append(len(keys))
+        op_off.append(len(f["kind"]))
+    i64 = lambda x: torch.tensor(np.asarray(x, dtype=np.uint64).view(np.int64), device=device)  # noqa: E731
+    i32 = lambda x: torch.tensor(x if x else [0], dtype=torch.int32, device=device)  # noqa: E731
+    u8 = lambda x: torch.tensor(x, dtype=torch.uint8, device=device)  # noqa: E731
+    pool_t = (torch.from_numpy(np.stack(pool).view(np.int64)).to(device) if pool
+              else torch.zeros((1, A), dtype=torch.int64, device=device))
+    return MapNestedOpBatch(i64(op_off), u8(f["kind"]), i32(f["actor"]), i64(f["counter"]), i32(f["key"]),
+                            u8(f["ikind"]), i32(f["iactor"]), i64(f["icounter"]), i32(f["ikey"]), i64(f["val"]),
+                            i64(f["ikeys"]), i32(f["clk_row"]), pool_t, i64(key_off), i32(keys))
+
+
+def _nested_states(res, what):
+    clock = res.clock
+    if clock.dim() != 2:
+        raise ValueError(f"{what}: a grouped result (clock (N, A)) expected")
+    N, A = clock.shape
+    K, K2 = res.iec.shape[1], res.iec.shape[2]
+    shapes = dict(ec=(N, K, A), ic=(N, K, A), iec=(N, K, K2, A), ivc=(N, K, K2, 8, A), ivv=(N, K, K2, 8),
+                  nval=(N, K, K2), id_n=(N, K), id_clock=(N, K, 16, A), id_keys=(N, K, 16))
+    for nm, shp in shapes.items():
+        t = getattr(res, nm)
+        if tuple(t.shape) != shp or not t.is_contiguous():
+            raise ValueError(f"{what}: {nm} must be a contiguous {shp} tensor")
+    if not clock.is_contiguous():
+        raise ValueError(f"{what}: clock must be contiguous")
+    st = _abi.MapNestedStates()
+    st.N, st.K, st.K2, st.A = N, K, K2, A
+    for nm in ("clock", "ec", "ic", "iec", "ivc", "ivv", "nval", "id_n", "id_clock", "id_keys"):
+        setattr(st, nm, getattr(res, nm).data_ptr())
+    return st, N, K, A
+
+
+def nested_apply_batch(res: "MapNestedLub", def_clock: torch.Tensor, def_keys: torch.Tensor,
+                       def_count: torch.Tensor, ops: MapNestedOpBatch, ctx: Optional[Context] = None) -> torch.Tensor:
+    """Apply every state's op stream in place (crdt_map_nested_apply_batch): `res` a nested_lub_many
+    result with G = N states (its tensors are updated), the outer deferred slots def_clock (N, Dcap, A)
+    / def_keys (N, Dcap, ceil(K/64)) / def_count (N,) int32.  Returns the per-state status (N,) int32."""
+    st, N, K, A = _nested_states(res, "map.nested_apply_batch")
+    ctx = ctx or Context.default(res.clock.device.index)
+    Kw = (K + 63) // 64
+    Dcap = def_clock.shape[1]
+    if (tuple(def_clock.shape) != (N, Dcap, A) or tuple(def_keys.shape) != (N, Dcap, Kw)
+            or tuple(def_count.shape) != (N,) or def_count.dtype != torch.int32
+            or not def_clock.is_contiguous() or not def_keys.is_contiguous()):
+        raise ValueError("map.nested_apply_batch: deferred slots (N, Dcap, A) / (N, Dcap, Kw) / (N,) int32 expected")
+    n = ops.kind.shape[0]
+    if ops.op_off.shape[0] != N + 1 or ops.key_off.shape[0] != n + 1 or ops.clk_pool.shape[1] != A:
+        raise ValueError("map.nested_apply_batch: op_off (N+1), key_off (n_ops+1), clk_pool (n, A) expected")
+    o = _abi.MapNestedOps()
+    o.n_ops, o.op_off = n, ops.op_off.data_ptr()
+    for nm in ("kind", "actor", "counter", "key", "ikind", "iactor", "icounter", "ikey", "val", "ikeys", "clk_row",
+               "key_off", "keys"):
+        setattr(o, nm, getattr(ops, nm).data_ptr())
+    o.clk_pool, o.n_clk_rows = ops.clk_pool.data_ptr(), ops.clk_pool.shape[0]
+    o.n_keys = ops.keys.shape[0]
+    status = torch.zeros(N, dtype=torch.int32, device=res.clock.device)
+    ctx.call("crdt_map_nested_apply_batch", ctypes.byref(st), def_clock.data_ptr(), def_keys.data_ptr(),
+             def_count.data_ptr(), Dcap, ctypes.byref(o), status.data_ptr())
+    return status
+
+
+def nested_forget_batch(res: "MapNestedLub", y: torch.Tensor, def_clock: Optional[torch.Tensor] = None,
+                        def_state: Optional[torch.Tensor] = None,
+                        ctx: Optional[Context] = None) -> Optional[torch.Tensor]:
+    """Causal::forget of N Map<K, Map<K2, MVReg>> states in place (map.rs:85-114 at both levels,
+    mvreg.rs:88-104; crdt_map_nested_forget_batch): `res` a nested_lub_many result with G = N states,
+    y (A,) or (N, A); the outer deferred rm clocks as for forget_batch.  Returns def_keep or None."""
+    st, N, K, A = _nested_states(res, "map.nested_forget_batch")
+    ctx = ctx or Context.default(res.clock.device.index)
+    y, ys = _forget_clock(ctx, y, N, A, "map.nested_forget_batch(y)")
+    dp, sp, D, keep = _forget_deferred(ctx, def_clock, def_state, N, A, "map.nested_forget_batch(def_clock)")
+    ctx.call("crdt_map_nested_forget_batch", ctypes.byref(st), y.data_ptr(), ys, dp, sp, D,
+             keep.data_ptr() if keep is not None else None)
+    return keep

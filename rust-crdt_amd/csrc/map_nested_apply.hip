@@ -1,0 +1,618 @@
+// CmRDT::apply and Causal::forget of whole Map<K, Map<K2, MVReg<u64>>> states (round 5) — the nested
+// type of the reference's own Map tests (TMap, test/map.rs:10; TestMap, src/map.rs:359), on the
+// crdt_map_nested_lub_many output layout (8 MVReg slots per inner key in Vec order with nval used,
+// 16 inner deferred removes per key).
+//
+// apply (map.rs:119-137), per state its ops in order:
+//   Op::Up { dot, key, op }: skipped when clock[dot.actor] >= dot.counter; else the entry (an absent
+//     one: all-zero rows = Map::default()) applies the dot to its clock, its inner Map applies `op`,
+//     the clock applies the dot, and apply_deferred (:311-316) re-runs every deferred remove;
+//   Op::Rm { clock, keyset }: apply_keyset_rm (:318-348): each named key's entry clock forgets the
+//     rm clock — an emptied entry is dropped, a kept one's inner Map forgets it (Causal::forget,
+//     :85-114) — and the remove is deferred unless clock >= rm (an equal rm clock unions its keys).
+// The inner Map's op is the same pair one level down, with MVReg::apply (mvreg.rs:130-166) for
+// Op::Up's op Put { clock, val }: an empty clock is a no-op; values whose clock is <= the Put clock are
+// dropped (order kept), and the value is appended unless a remaining one strictly dominates it.
+// MVReg::forget (mvreg.rs:88-104) forgets every value clock and drops the emptied ones, order kept.
+// Map::forget collects the deferred removes into a new map: two whose clocks become equal keep one
+// entry with the later one's keys (the fold's rule, csrc/map_nested.hip; the reference's HashMap
+// order is unspecified).
+//
+// One wave per state (apply) or per (state, key) (forget), lane l holding actors l + 64 j (j < APL)
+// of every row; the outer deferred removes in LDS for the whole stream.  Every global word is read
+// back only by the lane that wrote it (row words by the lane of their actor), or is a scalar every
+// lane writes with the same value (nval, ivv, id_n, id_keys).
+#include "common.hpp"
+
+namespace crdt {
+
+constexpr int kNaVs = 8;   // MVReg slots per inner key (crdt_map_nested_out)
+constexpr int kNaId = 16;  // inner deferred removes per key
+
+struct NestedApplyPlan {
+  u64 *clock, *ec, *ic, *iec, *ivc, *ivv, *id_clock, *id_keys;
+  unsigned *nval, *id_n;
+  unsigned long long N, K, K2, A, Kw, Dcap;
+  u64 *def_clock, *def_keys;
+  unsigned *def_count;
+  const u64 *op_off;
+  const uint8_t *kind, *ikind;
+  const uint32_t *actor, *key, *iactor, *ikey;
+  const u64 *counter, *icounter, *val, *ikeys;
+  const uint32_t *clk_row;
+  const u64 *clk_pool;
+  unsigned long long n_clk_rows;
+  const u64 *key_off;
+  const uint32_t *keys;
+  unsigned long long n_keys, n_ops;
+  unsigned *status;
+  unsigned wpb;
+  const u64 *y;  // forget
+  unsigned long long y_stride;
+};
+
+// The rows of outer key k of state s, and the inner-Map operations on them.
+template <int APL>
+struct NaKey {
+  u64 *ec, *ic, *iec, *ivc, *ivv, *idc, *idk;
+  unsigned *nval, *idn;
+  unsigned long long A, K2;
+  int lane;
+  mutable unsigned stb;  // status bits raised by these operations (the caller ORs them in)
+
+  __device__ __forceinline__ unsigned long long word(int j) const { return (unsigned long long)lane + 64ull * j; }
+  __device__ __forceinline__ void ld(const u64 *row, u64 (&x)[APL]) const {
+#pragma unroll
+    for (int j = 0; j < APL; ++j) x[j] = word(j) < A ? row[word(j)] : 0ull;
+  }
+  __device__ __forceinline__ void st_(u64 *row, const u64 (&x)[APL]) const {
+#pragma unroll
+    for (int j = 0; j < APL; ++j)
+      if (word(j) < A) row[word(j)] = x[j];
+  }
+  __device__ __forceinline__ void zero(u64 *row) const {
+#pragma unroll
+    for (int j = 0; j < APL; ++j)
+      if (word(j) < A) row[word(j)] = 0ull;
+  }
+  static __device__ __forceinline__ bool nz(const u64 (&x)[APL]) {
+    bool b = false;
+#pragma unroll
+    for (int j = 0; j < APL; ++j) b = b || x[j] != 0;
+    return __ballot(b) != 0;
+  }
+  static __device__ __forceinline__ bool leq(const u64 (&x)[APL], const u64 (&y)[APL]) {  // x <= y
+    bool b = false;
+#pragma unroll
+    for (int j = 0; j < APL; ++j) b = b || x[j] > y[j];
+    return __ballot(b) == 0;
+  }
+  static __device__ __forceinline__ bool eq(const u64 (&x)[APL], const u64 (&y)[APL]) {
+    bool b = false;
+#pragma unroll
+    for (int j = 0; j < APL; ++j) b = b || x[j] != y[j];
+    return __ballot(b) == 0;
+  }
+  static __device__ __forceinline__ void fg(u64 (&x)[APL], const u64 (&r)[APL]) {  // VClock::forget
+#pragma unroll
+    for (int j = 0; j < APL; ++j) x[j] = x[j] > r[j] ? x[j] : 0ull;
+  }
+  __device__ __forceinline__ u64 *slot(unsigned long long jk, unsigned i) const {
+    return ivc + (jk * kNaVs + i) * A;
+  }
+
+  // MVReg::forget of inner key jk's register (order kept, emptied values dropped)
+  __device__ void reg_forget(unsigned long long jk, const u64 (&r)[APL]) const {
+    const unsigned n = nval[jk];
+    unsigned o = 0;
+    for (unsigned i = 0; i < n; ++i) {
+      u64 x[APL];
+      ld(slot(jk, i), x);
+      fg(x, r);
+      if (!nz(x)) continue;
+      const u64 v = ivv[jk * kNaVs + i];
+      st_(slot(jk, o), x);
+      ivv[jk * kNaVs + o] = v;
+      ++o;
+    }
+    for (unsigned i = o; i < n; ++i) {
+      zero(slot(jk, i));
+      ivv[jk * kNaVs + i] = 0;
+    }
+    nval[jk] = o;
+  }
+  // drop inner entry jk (its rows all zero)
+  __device__ void inner_drop(unsigned long long jk) const {
+    zero(iec + jk * A);
+    const unsigned n = nval[jk];
+    for (unsigned i = 0; i < n; ++i) {
+      zero(slot(jk, i));
+      ivv[jk * kNaVs + i] = 0;
+    }
+    nval[jk] = 0;
+  }
+  // the inner Map's apply_keyset_rm on inner key jk = its entry's forget (map.rs:319-333)
+  __device__ void inner_key_rm(unsigned long long jk, const u64 (&r)[APL]) const {
+    u64 e[APL];
+    ld(iec + jk * A, e);
+    if (!nz(e)) return;
+    fg(e, r);
+    if (!nz(e)) {
+      inner_drop(jk);
+      return;
+    }
+    st_(iec + jk * A, e);
+    reg_forget(jk, r);
+  }
+  // Causal::forget of the inner Map (map.rs:85-114)
+  __device__ void inner_forget(const u64 (&r)[APL]) const {
+    for (unsigned long long jk = 0; jk < K2; ++jk) inner_key_rm(jk, r);
+    const unsigned n = *idn;
+    unsigned o = 0;
+    for (unsigned i = 0; i < n; ++i) {
+      u64 x[APL];
+      ld(idc + (unsigned long long)i * A, x);
+      fg(x, r);
+      if (!nz(x)) continue;
+      const u64 ks = idk[i];
+      unsigned jj = 0;
+      for (; jj < o; ++jj) {  // equal to a kept one: the later keys at the earlier place
+        u64 y[APL];
+        ld(idc + (unsigned long long)jj * A, y);
+        if (eq(x, y)) break;
+      }
+      if (jj < o) {
+        idk[jj] = ks;
+        continue;
+      }
+      st_(idc + (unsigned long long)o * A, x);
+      idk[o] = ks;
+      ++o;
+    }
+    for (unsigned i = o; i < n; ++i) {
+      zero(idc + (unsigned long long)i * A);
+      idk[i] = 0;
+    }
+    *idn = o;
+    u64 c[APL];
+    ld(ic, c);
+    fg(c, r);
+    st_(ic, c);
+  }
+  // the inner Map's apply_deferred (map.rs:311-316) against its clock c
+  __device__ void inner_apply_deferred(const u64 (&c)[APL]) const {
+    const unsigned n = *idn;
+    unsigned o = 0;
+    for (unsigned i = 0; i < n; ++i) {
+      u64 r[APL];
+      ld(idc + (unsigned long long)i * A, r);
+      const u64 ks = idk[i];
+      for (u64 b = ks; b;) {
+        const unsigned long long jk = (unsigned long long)__builtin_ctzll(b);
+        b &= b - 1;
+        if (jk < K2) inner_key_rm(jk, r);
+      }
+      if (leq(r, c)) continue;  // seen: no longer deferred
+      if (o != i) {
+        st_(idc + (unsigned long long)o * A, r);
+        idk[o] = ks;
+      }
+      ++o;
+    }
+    for (unsigned i = o; i < n; ++i) {
+      zero(idc + (unsigned long long)i * A);
+      idk[i] = 0;
+    }
+    *idn = o;
+  }
+  // MVReg::apply(Put { clock: r, val }) on inner key jk (mvreg.rs:130-166)
+  __device__ void reg_put(unsigned long long jk, const u64 (&r)[APL], u64 v) const {
+    if (!nz(r)) return;
+    const unsigned n = nval[jk];
+    unsigned o = 0;
+    bool dominated = false;
+    for (unsigned i = 0; i < n; ++i) {
+      u64 x[APL];
+      ld(slot(jk, i), x);
+      if (leq(x, r)) continue;             // Less or Equal: dropped
+      if (leq(r, x)) dominated = true;     // (x != r here) strictly greater: the Put is not added
+      const u64 xv = ivv[jk * kNaVs + i];
+      if (o != i) {
+        st_(slot(jk, o), x);
+        ivv[jk * kNaVs + o] = xv;
+      }
+      ++o;
+    }
+    for (unsigned i = o; i < n; ++i) {
+      zero(slot(jk, i));
+      ivv[jk * kNaVs + i] = 0;
+    }
+    if (!dominated) {
+      if (o < (unsigned)kNaVs) {
+        st_(slot(jk, o), r);
+        ivv[jk * kNaVs + o] = v;
+        ++o;
+      } else {
+        stb |= 16u;  // the register needed more than 8 values
+      }
+    }
+    nval[jk] = o;
+  }
+  __device__ __forceinline__ u64 word_of(const u64 (&x)[APL], unsigned a) const {
+    u64 v = 0;
+#pragma unroll
+    for (int j = 0; j < APL; ++j)
+      if ((unsigned)j == a / 64) v = x[j];
+    return __shfl(v, (int)(a % 64));
+  }
+  __device__ __forceinline__ void bump(u64 *row, unsigned a, u64 cnt) const {  // VClock::apply(dot)
+    if ((unsigned long long)lane == a % 64) {
+      u64 *q = row + a;
+      if (*q < cnt) *q = cnt;
+    }
+  }
+  // the inner Map's Op::Up { dot: (ia, icnt), key: jk, op: Put { clock: r, val: v } }
+  __device__ void inner_up(unsigned ia, u64 icnt, unsigned long long jk, const u64 (&r)[APL], u64 v) const {
+    u64 c[APL];
+    ld(ic, c);
+    if (word_of(c, ia) >= icnt) return;  // seen
+    bump(iec + jk * A, ia, icnt);
+    reg_put(jk, r, v);
+    bump(ic, ia, icnt);
+#pragma unroll
+    for (int j = 0; j < APL; ++j)
+      if ((unsigned)j == ia / 64 && (unsigned long long)lane == ia % 64 && c[j] < icnt) c[j] = icnt;
+    inner_apply_deferred(c);
+  }
+  // the inner Map's Op::Rm { clock: r, keyset: bits }
+  __device__ void inner_rm(const u64 (&r)[APL], u64 bits) const {
+    for (u64 b = bits; b;) {
+      const unsigned long long jk = (unsigned long long)__builtin_ctzll(b);
+      b &= b - 1;
+      if (jk < K2) inner_key_rm(jk, r);
+    }
+    u64 c[APL];
+    ld(ic, c);
+    if (leq(r, c)) return;
+    const unsigned n = *idn;
+    for (unsigned i = 0; i < n; ++i) {
+      u64 y[APL];
+      ld(idc + (unsigned long long)i * A, y);
+      if (eq(y, r)) {
+        idk[i] = idk[i] | bits;
+        return;
+      }
+    }
+    if (n >= (unsigned)kNaId) {
+      stb |= 1u;
+      return;
+    }
+    st_(idc + (unsigned long long)n * A, r);
+    idk[n] = bits;
+    *idn = n + 1;
+  }
+  // drop the outer entry: every row of the key zero
+  __device__ void drop_all() const {
+    zero(ec);
+    zero(ic);
+    for (unsigned long long jk = 0; jk < K2; ++jk)
+      if (nz_row(iec + jk * A) || nval[jk]) inner_drop(jk);
+    const unsigned n = *idn;
+    for (unsigned i = 0; i < n; ++i) {
+      zero(idc + (unsigned long long)i * A);
+      idk[i] = 0;
+    }
+    *idn = 0;
+  }
+  __device__ __forceinline__ bool nz_row(const u64 *row) const {
+    u64 x[APL];
+    ld(row, x);
+    return nz(x);
+  }
+  // the outer apply_keyset_rm / forget on this key (map.rs:319-333, :85-98)
+  __device__ void key_rm(const u64 (&r)[APL]) const {
+    u64 e[APL];
+    ld(ec, e);
+    if (!nz(e)) return;
+    fg(e, r);
+    if (!nz(e)) {
+      drop_all();
+      return;
+    }
+    st_(ec, e);
+    inner_forget(r);
+  }
+};
+
+template <int APL>
+__device__ __forceinline__ NaKey<APL> na_key(const NestedApplyPlan &p, unsigned long long s, unsigned long long k,
+                                             int lane) {
+  const unsigned long long sk = s * p.K + k, A = p.A, K2 = p.K2;
+  return NaKey<APL>{p.ec + sk * A, p.ic + sk * A, p.iec + sk * K2 * A, p.ivc + sk * K2 * kNaVs * A,
+                    p.ivv + sk * K2 * kNaVs, p.id_clock + sk * kNaId * A, p.id_keys + sk * kNaId,
+                    p.nval + sk * K2, p.id_n + sk, A, K2, lane, 0u};
+}
+
+template <int APL>
+__global__ __launch_bounds__(256) void map_nested_apply_kernel(NestedApplyPlan p) {
+  extern __shared__ u64 lds[];
+  const int lane = (int)(threadIdx.x % kWave), wv = (int)(threadIdx.x / kWave);
+  const unsigned long long s = (unsigned long long)blockIdx.x * p.wpb + wv;
+  if (wv >= (int)p.wpb || s >= p.N) return;  // (whole waves)
+  const unsigned long long A = p.A, K = p.K, K2 = p.K2, Kw = p.Kw, Dcap = p.Dcap;
+  u64 *sclk = lds + (unsigned long long)wv * Dcap * (A + Kw);  // [Dcap][A] the outer rm clocks
+  u64 *skey = sclk + Dcap * A;                                 // [Dcap][Kw] their key bitmaps
+  const unsigned long long ob = p.op_off[s], oe = p.op_off[s + 1];
+  unsigned dcnt = p.def_count[s];
+  if (dcnt > Dcap || oe < ob || oe > p.n_ops) {
+    if (lane == 0) p.status[s] = (dcnt > Dcap ? 4u : 0u) | (oe < ob || oe > p.n_ops ? 8u : 0u);
+    return;  // state left untouched
+  }
+  unsigned st = 0;
+  auto word = [&](int j) { return (unsigned long long)lane + 64ull * j; };
+  u64 *C = p.clock + s * A;
+  u64 c[APL];
+#pragma unroll
+  for (int j = 0; j < APL; ++j) c[j] = word(j) < A ? C[word(j)] : 0ull;
+  for (unsigned d = 0; d < dcnt; ++d) {
+    for (unsigned long long a = (unsigned long long)lane; a < A; a += kWave)
+      sclk[d * A + a] = p.def_clock[(s * Dcap + d) * A + a];
+    for (unsigned long long w = (unsigned long long)lane; w < Kw; w += kWave)
+      skey[d * Kw + w] = p.def_keys[(s * Dcap + d) * Kw + w];
+  }
+  auto map_apply_deferred = [&]() {
+    unsigned o = 0;
+    for (unsigned d = 0; d < dcnt; ++d) {
+      u64 r[APL];
+#pragma unroll
+      for (int j = 0; j < APL; ++j) r[j] = word(j) < A ? sclk[d * A + word(j)] : 0ull;
+      for (unsigned long long w = 0; w < Kw; ++w) {
+        u64 bits = skey[d * Kw + w];
+        while (bits) {
+          const unsigned long long k = w * 64 + (unsigned long long)__builtin_ctzll(bits);
+          bits &= bits - 1;
+          if (k < K) {
+            const NaKey<APL> q = na_key<APL>(p, s, k, lane);
+            q.key_rm(r);
+            st |= q.stb;
+          }
+        }
+      }
+      if (NaKey<APL>::leq(r, c)) continue;  // no longer deferred
+      if (o != d) {
+        for (unsigned long long a = (unsigned long long)lane; a < A; a += kWave) sclk[o * A + a] = sclk[d * A + a];
+        for (unsigned long long w = (unsigned long long)lane; w < Kw; w += kWave) skey[o * Kw + w] = skey[d * Kw + w];
+      }
+      ++o;
+    }
+    dcnt = o;
+  };
+
+  for (unsigned long long o = ob; o < oe; ++o) {
+    const unsigned kind = p.kind[o];
+    if (kind == 0) {  // ---- Op::Up { dot, key, op: an inner Map op }
+      const unsigned a = p.actor[o], ik = p.ikind[o];
+      const unsigned long long k = p.key[o];
+      const u64 cnt = p.counter[o];
+      const unsigned rr = p.clk_row[o];
+      const unsigned ia = ik == 0 ? p.iactor[o] : 0u;
+      const unsigned long long jk = ik == 0 ? p.ikey[o] : 0ull;
+      const u64 ib = ik == 1 ? p.ikeys[o] : 0ull;
+      if (a >= A || k >= K || ik > 1 || rr >= p.n_clk_rows || ia >= A || jk >= K2 || (K2 < 64 && (ib >> K2))) {
+        st |= 2u;  // malformed: skipped whole
+        continue;
+      }
+      const NaKey<APL> q = na_key<APL>(p, s, k, lane);
+      if (q.word_of(c, a) >= cnt) continue;  // seen (map.rs:123-126)
+      q.bump(q.ec, a, cnt);  // entry.clock.apply(dot) (an absent entry: its rows are Map::default())
+      u64 r[APL];
+      q.ld(p.clk_pool + (unsigned long long)rr * A, r);
+      if (ik == 0) q.inner_up(ia, p.icounter[o], jk, r, p.val[o]);
+      else q.inner_rm(r, ib);
+      st |= q.stb;
+#pragma unroll
+      for (int j = 0; j < APL; ++j)
+        if ((unsigned)j == a / 64 && (unsigned long long)lane == a % 64 && c[j] < cnt) c[j] = cnt;
+      map_apply_deferred();
+    } else if (kind == 1) {  // ---- Op::Rm -> apply_keyset_rm
+      const unsigned rr = p.clk_row[o];
+      const u64 kb = p.key_off[o], ke = p.key_off[o + 1];
+      if (rr >= p.n_clk_rows || ke < kb || ke > p.n_keys) {
+        st |= 2u;
+        continue;
+      }
+      u64 r[APL];
+#pragma unroll
+      for (int j = 0; j < APL; ++j) r[j] = word(j) < A ? p.clk_pool[(unsigned long long)rr * A + word(j)] : 0ull;
+      for (u64 i = kb; i < ke; ++i) {
+        const unsigned long long k = p.keys[i];
+        if (k < K) {
+          const NaKey<APL> q = na_key<APL>(p, s, k, lane);
+          q.key_rm(r);
+          st |= q.stb;
+        } else {
+          st |= 2u;
+        }
+      }
+      if (NaKey<APL>::leq(r, c)) continue;
+      int slot = -1;
+      for (unsigned d = 0; d < dcnt && slot < 0; ++d) {
+        bool ne = false;
+#pragma unroll
+        for (int j = 0; j < APL; ++j) ne = ne || (word(j) < A && sclk[d * A + word(j)] != r[j]);
+        if (!__ballot(ne)) slot = (int)d;
+      }
+      if (slot < 0) {
+        if (dcnt >= Dcap) {
+          st |= 1u;
+          continue;
+        }
+        slot = (int)dcnt++;
+#pragma unroll
+        for (int j = 0; j < APL; ++j)
+          if (word(j) < A) sclk[slot * A + word(j)] = r[j];
+        for (unsigned long long w = (unsigned long long)lane; w < Kw; w += kWave) skey[slot * Kw + w] = 0;
+      }
+      for (u64 i = kb; i < ke; ++i) {
+        const unsigned long long k = p.keys[i];
+        if (k < K && (unsigned long long)lane == (k / 64) % kWave) skey[slot * Kw + k / 64] |= 1ull << (k % 64);
+      }
+    } else {
+      st |= 2u;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < APL; ++j)
+    if (word(j) < A) C[word(j)] = c[j];
+  for (unsigned d = 0; d < dcnt; ++d) {
+    for (unsigned long long a = (unsigned long long)lane; a < A; a += kWave)
+      p.def_clock[(s * Dcap + d) * A + a] = sclk[d * A + a];
+    for (unsigned long long w = (unsigned long long)lane; w < Kw; w += kWave)
+      p.def_keys[(s * Dcap + d) * Kw + w] = skey[d * Kw + w];
+  }
+  if (lane == 0) {
+    p.def_count[s] = dcnt;
+    p.status[s] = st;
+  }
+}
+
+// Causal::forget of the entries: one wave per (state, key), y row y[s] (the map clock and the outer
+// deferred pool go through crdt_map_forget_batch afterwards)
+template <int APL>
+__global__ __launch_bounds__(256) void map_nested_forget_kernel(NestedApplyPlan p) {
+  const int lane = (int)(threadIdx.x % kWave);
+  const unsigned long long sk = (unsigned long long)blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
+  if (sk >= p.N * p.K) return;  // (whole waves)
+  const unsigned long long s = sk / p.K, k = sk % p.K;
+  const NaKey<APL> q = na_key<APL>(p, s, k, lane);
+  u64 r[APL];
+  q.ld(p.y + s * p.y_stride, r);
+  q.key_rm(r);  // (Map::forget on an entry = apply_keyset_rm's per-key step)
+}
+
+}  // namespace crdt
+
+using namespace crdt;
+
+static int nested_states_check(crdt_ctx *ctx, const crdt_map_nested_states *m, const char *what) {
+  if (!m) return fail(ctx, CRDT_EINVAL, "%s: NULL states", what);
+  if (m->A > 512) return fail(ctx, CRDT_EUNSUPPORTED, "%s: A = %zu > 512", what, m->A);
+  if (m->K2 > 64) return fail(ctx, CRDT_EUNSUPPORTED, "%s: K2 = %zu > 64 (inner key sets are one u64 mask)", what, m->K2);
+  if (m->N && (!m->clock || (m->K && (!m->ec || !m->ic || !m->id_n || !m->id_clock || !m->id_keys ||
+                                      (m->K2 && (!m->iec || !m->ivc || !m->ivv || !m->nval))))))
+    return fail(ctx, CRDT_EINVAL, "%s: NULL state buffer", what);
+  return CRDT_OK;
+}
+
+static NestedApplyPlan nested_plan(const crdt_map_nested_states *m) {
+  NestedApplyPlan p{};
+  p.clock = (u64 *)m->clock;
+  p.ec = (u64 *)m->ec;
+  p.ic = (u64 *)m->ic;
+  p.iec = (u64 *)m->iec;
+  p.ivc = (u64 *)m->ivc;
+  p.ivv = (u64 *)m->ivv;
+  p.id_clock = (u64 *)m->id_clock;
+  p.id_keys = (u64 *)m->id_keys;
+  p.nval = m->nval;
+  p.id_n = m->id_n;
+  p.N = m->N;
+  p.K = m->K;
+  p.K2 = m->K2;
+  p.A = m->A;
+  p.Kw = m->K ? (m->K + 63) / 64 : 1;
+  return p;
+}
+
+extern "C" int crdt_map_nested_apply_batch(crdt_ctx *ctx, const crdt_map_nested_states *m, uint64_t *def_clock,
+                                           uint64_t *def_keys, uint32_t *def_count, size_t Dcap,
+                                           const crdt_map_nested_ops *ops, uint32_t *status) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
+  CRDT_CHECK_CTX(ctx);
+  if (int rc = nested_states_check(ctx, m, "map_nested_apply_batch")) return rc;
+  if (!ops || !status) return fail(ctx, CRDT_EINVAL, "map_nested_apply_batch: NULL argument");
+  const size_t N = m->N, A = m->A;
+  if (N == 0) return CRDT_OK;
+  if (A == 0) return fail(ctx, CRDT_EINVAL, "map_nested_apply_batch: A = 0");
+  if (!def_count || (Dcap && (!def_clock || !def_keys)) || !ops->op_off)
+    return fail(ctx, CRDT_EINVAL, "map_nested_apply_batch: NULL buffer");
+  if (ops->n_ops && (!ops->kind || !ops->actor || !ops->counter || !ops->key || !ops->ikind || !ops->iactor ||
+                     !ops->icounter || !ops->ikey || !ops->val || !ops->ikeys || !ops->clk_row))
+    return fail(ctx, CRDT_EINVAL, "map_nested_apply_batch: NULL op buffer");
+  NestedApplyPlan p = nested_plan(m);
+  const size_t per_wave = Dcap * (A + p.Kw) * 8;
+  if (per_wave > 64 * 1024)
+    return fail(ctx, CRDT_EUNSUPPORTED, "map_nested_apply_batch: Dcap * (A + ceil(K/64)) too large for LDS");
+  unsigned wpb = 4;
+  while (wpb > 1 && per_wave * wpb > 64 * 1024) --wpb;
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  p.Dcap = Dcap;
+  p.def_clock = (u64 *)def_clock;
+  p.def_keys = (u64 *)def_keys;
+  p.def_count = def_count;
+  p.op_off = (const u64 *)ops->op_off;
+  p.kind = ops->kind;
+  p.ikind = ops->ikind;
+  p.actor = ops->actor;
+  p.key = ops->key;
+  p.iactor = ops->iactor;
+  p.ikey = ops->ikey;
+  p.counter = (const u64 *)ops->counter;
+  p.icounter = (const u64 *)ops->icounter;
+  p.val = (const u64 *)ops->val;
+  p.ikeys = (const u64 *)ops->ikeys;
+  p.clk_row = ops->clk_row;
+  p.clk_pool = (const u64 *)ops->clk_pool;
+  p.n_clk_rows = ops->clk_pool ? ops->n_clk_rows : 0;
+  p.key_off = (const u64 *)ops->key_off;
+  p.keys = ops->keys;
+  p.n_keys = ops->keys ? ops->n_keys : 0;
+  p.n_ops = ops->n_ops;
+  p.status = status;
+  p.wpb = wpb;
+  if (!ops->key_off) {  // (no outer Rm: every key range empty)
+    if (int rc = ensure_scratch(ctx, (ops->n_ops + 1) * 8)) return rc;
+    if (int rc = device_fill(ctx, ctx->scratch, (ops->n_ops + 1) * 8, 0)) return rc;
+    p.key_off = static_cast<const u64 *>(ctx->scratch);
+  }
+  const dim3 grid((unsigned)((N + wpb - 1) / wpb)), block(wpb * kWave);
+  const size_t lds = per_wave * wpb;
+  timing_begin(ctx, "map_nested_apply");
+  if (A <= 64) hipLaunchKernelGGL(map_nested_apply_kernel<1>, grid, block, lds, ctx->stream, p);
+  else if (A <= 128) hipLaunchKernelGGL(map_nested_apply_kernel<2>, grid, block, lds, ctx->stream, p);
+  else if (A <= 256) hipLaunchKernelGGL(map_nested_apply_kernel<4>, grid, block, lds, ctx->stream, p);
+  else hipLaunchKernelGGL(map_nested_apply_kernel<8>, grid, block, lds, ctx->stream, p);
+  timing_end(ctx);
+  CRDT_HIP(ctx, hipGetLastError());
+  return CRDT_OK;
+}
+
+extern "C" int crdt_map_nested_forget_batch(crdt_ctx *ctx, const crdt_map_nested_states *m, const uint64_t *y,
+                                            size_t y_stride, uint64_t *def_clock, const uint32_t *def_state,
+                                            size_t D, uint8_t *def_keep) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
+  CRDT_CHECK_CTX(ctx);
+  if (int rc = nested_states_check(ctx, m, "map_nested_forget_batch")) return rc;
+  const size_t N = m->N, K = m->K, A = m->A;
+  if (N == 0 || A == 0) return CRDT_OK;
+  if (!y) return fail(ctx, CRDT_EINVAL, "map_nested_forget_batch: NULL y");
+  if (y_stride && y_stride < A) return fail(ctx, CRDT_EINVAL, "map_nested_forget_batch: y_stride < A");
+  if (K) {
+    NestedApplyPlan p = nested_plan(m);
+    p.y = (const u64 *)y;
+    p.y_stride = y_stride;
+    const unsigned long long waves = (unsigned long long)N * K, blocks = (waves + 3) / 4;
+    if (blocks > 0x7fffffffULL) return fail(ctx, CRDT_EUNSUPPORTED, "map_nested_forget_batch: N*K too large");
+    CRDT_HIP(ctx, hipSetDevice(ctx->device));
+    timing_begin(ctx, "map_nested_forget");
+    if (A <= 64) hipLaunchKernelGGL(map_nested_forget_kernel<1>, dim3((unsigned)blocks), dim3(256), 0, ctx->stream, p);
+    else if (A <= 128) hipLaunchKernelGGL(map_nested_forget_kernel<2>, dim3((unsigned)blocks), dim3(256), 0, ctx->stream, p);
+    else if (A <= 256) hipLaunchKernelGGL(map_nested_forget_kernel<4>, dim3((unsigned)blocks), dim3(256), 0, ctx->stream, p);
+    else hipLaunchKernelGGL(map_nested_forget_kernel<8>, dim3((unsigned)blocks), dim3(256), 0, ctx->stream, p);
+    timing_end(ctx);
+    CRDT_HIP(ctx, hipGetLastError());
+  }
+  // the map clock and the outer deferred pool (no entries: K = 0)
+  crdt_map_states s{N, 0, A, 1, m->clock, A, nullptr, 0, nullptr, 0, nullptr, 0};
+  return crdt_map_forget_batch(ctx, &s, y, y_stride, def_clock, def_state, D, def_keep);
+}

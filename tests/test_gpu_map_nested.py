@@ -11,6 +11,7 @@ reference's own assertions check the kernel:
 Plus op-replay histories (inner writes and inner removes read at replicas that have seen more, so
 removes defer at both levels) folded over many replicas against the oracle's left fold."""
 import random
+from typing import NamedTuple
 
 import numpy as np
 import pytest
@@ -79,8 +80,8 @@ def _map_clock(c, d):
     return VClock({d[a]: n for a, n in c.dots.items()})
 
 
-def _intern(maps):
-    acts, keys, ikeys = set(), set(), set()
+def _intern(maps, extra=None, with_dicts=False):
+    acts, keys, ikeys = (set(x) for x in extra) if extra else (set(), set(), set())
     for m in maps:
         for c in _clocks(m):
             acts |= set(c.dots)
@@ -111,6 +112,8 @@ def _intern(maps):
 
     dense = [conv(m, A.fwd, K.fwd, J.fwd) for m in maps]
     back = lambda m: conv(m, A.inv, K.inv, J.inv)  # noqa: E731
+    if with_dicts:
+        return dense, back, A, K, J
     return dense, back, len(A.fwd), len(K.fwd), len(J.fwd)
 
 
@@ -141,6 +144,153 @@ def gpu_fold(ctx, maps):
     got = O.dense_to_nested_map(to_host(res.clock), to_host(res.ec), to_host(res.ic), to_host(res.iec),
                                 to_host(res.ivc), to_host(res.ivv), res.nval.cpu().numpy(), ideferred, dset)
     return back(got)
+
+
+class _States(NamedTuple):
+    """The crdt_map_nested_states layout of N states (nested_lub_many's output shapes, G = N)."""
+    clock: torch.Tensor
+    ec: torch.Tensor
+    ic: torch.Tensor
+    iec: torch.Tensor
+    ivc: torch.Tensor
+    ivv: torch.Tensor
+    nval: torch.Tensor
+    id_n: torch.Tensor
+    id_clock: torch.Tensor
+    id_keys: torch.Tensor
+
+
+def nested_states(maps, K, K2, A):
+    """Dense objects -> (_States on the device, outer deferred as slots (N, Dcap, A) / (N, Dcap, Kw) /
+    (N,) int32 with Dcap = 16, and as a pool (def_clock (D, A), def_state (D,)))."""
+    N = len(maps)
+    d = O.nested_map_to_dense(maps, K, K2, A, 8)
+    nval = np.zeros((N, K, K2), np.int32)
+    for n, m in enumerate(maps):
+        for k, e in m.entries.items():
+            for j, ie in e.val.entries.items():
+                nval[n, k, j] = len(ie.val.vals)
+    idn = np.zeros((N, K), np.int32)
+    idc = np.zeros((N, K, 16, A), np.uint64)
+    idk = np.zeros((N, K, 16), np.uint64)
+    off = d["id_off"].astype(np.int64)
+    for i in range(N * K):
+        a, b = off[i], off[i + 1]
+        assert b - a <= 16
+        idn[i // K, i % K] = b - a
+        idc[i // K, i % K, :b - a] = d["id_clock"][a:b]
+        idk[i // K, i % K, :b - a] = d["id_keys"][a:b]
+    st = _States(to_dev(d["clock"]), to_dev(d["ec"]), to_dev(d["ic"]), to_dev(d["iec"]), to_dev(d["ivc"]),
+                 to_dev(d["ivv"]), torch.from_numpy(nval).cuda(), torch.from_numpy(idn).cuda(), to_dev(idc),
+                 to_dev(idk))
+    Dcap, Kw = 16, (K + 63) // 64
+    dcl = np.zeros((N, Dcap, A), np.uint64)
+    dks = np.zeros((N, Dcap, Kw), np.uint64)
+    cnt = np.zeros(N, np.int32)
+    for j in range(d["def_row"].shape[0]):
+        n = int(d["def_row"][j])
+        assert cnt[n] < Dcap
+        dcl[n, cnt[n]], dks[n, cnt[n]] = d["def_clock"][j], d["def_keys"][j]
+        cnt[n] += 1
+    return st, (to_dev(dcl), to_dev(dks), torch.from_numpy(cnt).cuda()), d
+
+
+def decode_states(st, n, dfr):
+    idn = st.id_n.cpu().numpy()[n]
+    idc, idk = to_host(st.id_clock)[n], to_host(st.id_keys)[n]
+    K = idn.shape[0]
+    idef = {k: [(idc[k, i], O.bitmap_members(idk[k, i:i + 1])) for i in range(int(idn[k]))] for k in range(K)}
+    return O.dense_to_nested_map(to_host(st.clock)[n], to_host(st.ec)[n], to_host(st.ic)[n], to_host(st.iec)[n],
+                                 to_host(st.ivc)[n], to_host(st.ivv)[n], st.nval.cpu().numpy()[n], idef, dfr)
+
+
+def _slot_deferred(slots, n):
+    dcl, dks, cnt = to_host(slots[0]), to_host(slots[1]), slots[2].cpu().numpy()
+    return [(dcl[n, i], O.bitmap_members(dks[n, i])) for i in range(int(cnt[n]))]
+
+
+def _op_ids(ops):
+    acts, keys, ikeys, clocks = set(), set(), set(), []
+    for op in ops:
+        if isinstance(op, MapRm):
+            clocks.append(op.clock)
+            keys |= set(op.keyset)
+            continue
+        acts.add(op.dot.actor)
+        keys.add(op.key)
+        if isinstance(op.op, MapRm):
+            clocks.append(op.op.clock)
+            ikeys |= set(op.op.keyset)
+        else:
+            acts.add(op.op.dot.actor)
+            ikeys.add(op.op.key)
+            clocks.append(op.op.op.clock)
+    for c in clocks:
+        acts |= set(c.dots)
+    return acts, keys, ikeys
+
+
+def _map_vals(m, f):
+    n = m.copy()
+    for e in n.entries.values():
+        for ie in e.val.entries.values():
+            ie.val.vals = [(c, f[v]) for c, v in ie.val.vals]
+    return n
+
+
+def gpu_apply(ctx, m, ops):
+    """for op in ops: m.apply(op), every apply on the GPU (one crdt_map_nested_apply_batch stream);
+    returns the new state.  Register values that are not u64 travel as ids (MVReg compares clocks only)."""
+    vals = {v for e in m.entries.values() for ie in e.val.entries.values() for _, v in ie.val.vals}
+    vals |= {op.op.op.val for op in ops if isinstance(op, MapUp) and isinstance(op.op, MapUp)}
+    if not all(isinstance(v, int) and 0 <= v < 2**64 for v in vals):
+        fv = {v: i for i, v in enumerate(sorted(vals, key=repr))}
+        inv = {i: v for v, i in fv.items()}
+        ops = [MapUp(op.dot, op.key, MapUp(op.op.dot, op.op.key, MVRegPut(op.op.op.clock, fv[op.op.op.val])))
+               if isinstance(op, MapUp) and isinstance(op.op, MapUp) else op for op in ops]
+        return _map_vals(gpu_apply(ctx, _map_vals(m, fv), ops), inv)
+    dense, back, Ad, Kd, Jd = _intern([m], extra=_op_ids(ops), with_dicts=True)
+    A, K, K2 = len(Ad.fwd), len(Kd.fwd), len(Jd.fwd)
+    if A > 512 or K2 > 64:
+        pytest.skip("more than 512 actors / 64 inner keys in one case")
+    st, slots, _ = nested_states(dense, K, K2, A)
+    row = lambda c: {Ad.fwd[a]: n for a, n in c.dots.items()}  # noqa: E731
+    stream = []
+    for op in ops:
+        if isinstance(op, MapRm):
+            stream.append(("rm", row(op.clock), [Kd.fwd[k] for k in op.keyset]))
+        elif isinstance(op.op, MapRm):
+            stream.append(("irm", Ad.fwd[op.dot.actor], op.dot.counter, Kd.fwd[op.key], row(op.op.clock),
+                           [Jd.fwd[j] for j in op.op.keyset]))
+        else:
+            put = op.op.op
+            stream.append(("put", Ad.fwd[op.dot.actor], op.dot.counter, Kd.fwd[op.key], Ad.fwd[op.op.dot.actor],
+                           op.op.dot.counter, Jd.fwd[op.op.key], row(put.clock), int(put.val)))
+    enc = cg.map.encode_nested_ops([stream], A, "cuda:0")
+    status = cg.map.nested_apply_batch(st, *slots, enc, ctx=ctx).cpu().numpy()
+    assert status[0] == 0, status
+    return back(decode_states(st, 0, _slot_deferred(slots, 0)))
+
+
+def gpu_forget(ctx, m, clock):
+    """m.forget(clock) on the GPU (crdt_map_nested_forget_batch); returns the new state."""
+    dense, back, Ad, Kd, Jd = _intern([m], extra=(set(clock.dots), set(), set()), with_dicts=True)
+    A, K, K2 = len(Ad.fwd), len(Kd.fwd), len(Jd.fwd)
+    if A > 512 or K2 > 64:
+        pytest.skip("more than 512 actors / 64 inner keys in one case")
+    st, _, d = nested_states(dense, K, K2, A)
+    y = np.zeros(A, np.uint64)
+    for a, c in clock.dots.items():
+        y[Ad.fwd[a]] = c
+    D = d["def_row"].shape[0]
+    dcl = to_dev(d["def_clock"]) if D else None
+    dst = torch.from_numpy(d["def_row"].astype(np.int32)).cuda() if D else None
+    keep = cg.map.nested_forget_batch(st, to_dev(y), def_clock=dcl, def_state=dst, ctx=ctx)
+    dfr = []
+    if D:
+        kp, hc = keep.cpu().numpy(), to_host(dcl)
+        dfr = [(hc[j], O.bitmap_members(d["def_keys"][j])) for j in range(D) if kp[j]]
+    return back(decode_states(st, 0, dfr))
 
 
 @pytest.fixture
