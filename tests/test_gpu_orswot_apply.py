@@ -212,3 +212,13 @@ def test_orswot_apply_deferred_spill(hot):
             assert g == e, s
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("mode", ["lub2", "merge_batch"])
+@pytest.mark.parametrize("case", APPLY_CASES, ids=[c["name"] for c in APPLY_CASES])
+def test_kat_orswot_apply_and_merge_gpu(actx, case, mode):
+    """The reference's Orswot KATs (test/orswot.rs, orswot.rs:294-394) with EVERY apply and EVERY
+    merge on the GPU (crdt_orswot_apply_batch; crdt_orswot_lub_many of the pair or the in-place
+    crdt_orswot_merge_batch)."""
+    from test_gpu_kat import gpu_merge
+    K.run_case(case, merge_hook=lambda d, s, k: gpu_merge(d, s, k, mode), apply_hook=gpu_apply_hook(actx))
