@@ -1114,6 +1114,18 @@ int crdt_map_orswot_ingest(crdt_ctx *ctx, const uint8_t *bytes, const uint64_t *
 int crdt_map_orswot_egress(crdt_ctx *ctx, const crdt_map_orswot_states *states, const crdt_map_deferred *def,
                            const uint32_t *actors, const uint32_t *keys, const uint64_t *members, uint64_t *frame_off,
                            uint8_t *bytes, size_t cap, size_t *total);
+/* Map<u32, Map<u32, MVReg<u64, u32>, u32>, u32> (the reference's own Map test type, test/map.rs:10)
+ * frames <-> crdt_map_nested_states: the inner Map's clock ic, its entries by the sorted u32 inner-key
+ * dictionary `ikeys` (K2 <= 64) with their MVReg values in slots 0 .. nval < 8 (Vec order), its
+ * deferred removes in slots 0 .. id_n < 16 with one inner-key mask each; the outer Map's removes in
+ * per-state slots.  Status bit 4: a register past 8 values, an inner list past 16 or an outer one
+ * past Dcap (the excess dropped). */
+int crdt_map_nested_ingest(crdt_ctx *ctx, const uint8_t *bytes, const uint64_t *frame_off, const uint32_t *actors,
+                           const uint32_t *keys, const uint32_t *ikeys, const crdt_map_nested_states *out,
+                           const crdt_map_deferred *out_def, uint32_t *status);
+int crdt_map_nested_egress(crdt_ctx *ctx, const crdt_map_nested_states *states, const crdt_map_deferred *def,
+                           const uint32_t *actors, const uint32_t *keys, const uint32_t *ikeys, uint64_t *frame_off,
+                           uint8_t *bytes, size_t cap, size_t *total);
 
 /* ---- synthetic inputs (bench / test data, generated in HBM) --------------------------------
  * Counter-based and reproducible on the CPU (oracle/oracle.py synth_* restates them; small

@@ -1875,7 +1875,7 @@ def unbc_orswot(b: bytes, pos: int = 0):
     return clock, entries, deferred, pos
 
 
-def bc_map_obj(m, aid, kid, mid=None) -> bytes:
+def bc_map_obj(m, aid, kid, mid=None, iid=None) -> bytes:
     """A value-typed Map object (Map<u32, GCounter / PNCounter / Orswot<u64>, u32>, map.rs:31-47 with
     gcounter.rs:25-28, pncounter.rs:28-32, orswot.rs:20-25 inside) -> bincode, its dense actor / key /
     member indices mapped to ids through aid / kid / mid (ascending sequences, so index order is id
@@ -1884,6 +1884,18 @@ def bc_map_obj(m, aid, kid, mid=None) -> bytes:
     vc = lambda v: bc_vclock({int(aid[a]): c for a, c in v.dots.items()})  # noqa: E731
 
     def val(v):
+        if isinstance(v, Map):  # the nested Map<u32, MVReg<u64>> (iid maps its keys)
+            out = vc(v.clock) + _st.pack("<Q", len(v.entries))
+            for j in sorted(v.entries):
+                ie = v.entries[j]
+                out += _st.pack("<I", int(iid[j])) + vc(ie.clock) + _st.pack("<Q", len(ie.val.vals))
+                for c, x in ie.val.vals:
+                    out += vc(c) + _st.pack("<Q", int(x))
+            out += _st.pack("<Q", len(v.deferred))
+            for rm, ks in v.deferred.items():
+                kk = sorted(int(iid[x]) for x in ks)
+                out += vc(rm) + _st.pack("<Q", len(kk)) + b"".join(_st.pack("<I", x) for x in kk)
+            return out
         if isinstance(v, GCounter):
             return vc(v.inner)
         if isinstance(v, PNCounter):
@@ -1908,12 +1920,17 @@ def bc_map_obj(m, aid, kid, mid=None) -> bytes:
     return out
 
 
-def unbc_map_obj(b: bytes, vnew, aid, kid, mid=None, pos: int = 0):
-    """Inverse of bc_map_obj -> (Map object over dense indices, pos); vnew = GCounter, PNCounter or
-    Orswot.  Removes with equal clocks union their sets (the HashMap keyed by the clock)."""
+def unbc_map_obj(b: bytes, vnew, aid, kid, mid=None, pos: int = 0, iid=None):
+    """Inverse of bc_map_obj -> (Map object over dense indices, pos); vnew = GCounter, PNCounter,
+    Orswot or "nested" (Map<K2, MVReg<u64>> values, inner keys through iid).  Removes with equal clocks
+    union their sets (the HashMap keyed by the clock)."""
     ai = {int(x): i for i, x in enumerate(aid)}
     ki = {int(x): i for i, x in enumerate(kid)}
     mi = {int(x): i for i, x in enumerate(mid)} if mid is not None else {}
+    ii = {int(x): i for i, x in enumerate(iid)} if iid is not None else {}
+    nested = vnew == "nested"
+    if nested:
+        vnew = lambda: Map(MVReg)  # noqa: E731
 
     def vc(pos):
         d, pos = unbc_vclock(b, pos)
@@ -1927,7 +1944,30 @@ def unbc_map_obj(b: bytes, vnew, aid, kid, mid=None, pos: int = 0):
         (k,) = _st.unpack_from("<I", b, pos)
         ec, pos = vc(pos + 4)
         v = vnew()
-        if vnew is GCounter:
+        if nested:
+            v.clock, pos = vc(pos)
+            (n2,) = _st.unpack_from("<Q", b, pos)
+            pos += 8
+            for _ in range(n2):
+                (j,) = _st.unpack_from("<I", b, pos)
+                iec, pos = vc(pos + 4)
+                (nv,) = _st.unpack_from("<Q", b, pos)
+                pos += 8
+                vals = []
+                for _ in range(nv):
+                    c, pos = vc(pos)
+                    (x,) = _st.unpack_from("<Q", b, pos)
+                    pos += 8
+                    vals.append((c, x))
+                v.entries[ii[j]] = MapEntry(iec, MVReg(vals))
+            (nd,) = _st.unpack_from("<Q", b, pos)
+            pos += 8
+            for _ in range(nd):
+                rm, pos = vc(pos)
+                (j,) = _st.unpack_from("<Q", b, pos)
+                v.deferred.setdefault(rm, set()).update(ii[_st.unpack_from("<I", b, pos + 8 + 4 * i)[0]] for i in range(j))
+                pos += 8 + 4 * j
+        elif vnew is GCounter:
             v.inner, pos = vc(pos)
         elif vnew is PNCounter:
             v.p.inner, pos = vc(pos)

@@ -56,7 +56,7 @@ EXPORTS = (
     "crdt_map_nested_lub_many", "crdt_map_counter_lub_many_sharded", "crdt_map_orswot_lub_many_sharded",
     "crdt_map_nested_lub_many_sharded", "crdt_map_counter_forget_batch", "crdt_map_orswot_forget_batch",
     "crdt_map_counter_apply_batch", "crdt_map_orswot_apply_batch",
-    "crdt_map_nested_apply_batch", "crdt_map_nested_forget_batch",
+    "crdt_map_nested_apply_batch", "crdt_map_nested_forget_batch", "crdt_map_nested_ingest", "crdt_map_nested_egress",
     "crdt_map_counter_ingest", "crdt_map_counter_egress", "crdt_map_orswot_ingest", "crdt_map_orswot_egress",
 )
 
@@ -295,6 +295,10 @@ _SIGS.update({
     "crdt_map_nested_apply_batch": ([P, ctypes.POINTER(MapNestedStates), P, P, P, S, ctypes.POINTER(MapNestedOps), P],
                                     ctypes.c_int),
     "crdt_map_nested_forget_batch": ([P, ctypes.POINTER(MapNestedStates), P, S, P, P, S, P], ctypes.c_int),
+    "crdt_map_nested_ingest": ([P, P, P, P, P, P, ctypes.POINTER(MapNestedStates), ctypes.POINTER(MapDeferred), P],
+                               ctypes.c_int),
+    "crdt_map_nested_egress": ([P, ctypes.POINTER(MapNestedStates), ctypes.POINTER(MapDeferred), P, P, P, P, P, S,
+                                ctypes.POINTER(S)], ctypes.c_int),
     "crdt_map_counter_ingest": ([P, P, P, P, P, ctypes.POINTER(MapCounterStates), ctypes.POINTER(MapDeferred), P],
                                 ctypes.c_int),
     "crdt_map_counter_egress": ([P, ctypes.POINTER(MapCounterStates), ctypes.POINTER(MapDeferred), P, P, P, P, S,

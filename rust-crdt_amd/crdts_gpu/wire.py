@@ -252,6 +252,24 @@ class MapOrswotFrames(NamedTuple):
     def_count: torch.Tensor  # (N,) int32
 
 
+class MapNestedFrames(NamedTuple):
+    """Map<u32, Map<u32, MVReg<u64>>> states in the crdt_map_nested_states layout (the field names of
+    map.MapNestedLub, so map.nested_apply_batch / nested_forget_batch take it) + deferred slots."""
+    clock: torch.Tensor      # (N, A)
+    ec: torch.Tensor         # (N, K, A)
+    ic: torch.Tensor         # (N, K, A)
+    iec: torch.Tensor        # (N, K, K2, A)
+    ivc: torch.Tensor        # (N, K, K2, 8, A)
+    ivv: torch.Tensor        # (N, K, K2, 8)
+    nval: torch.Tensor       # (N, K, K2) int32
+    id_n: torch.Tensor       # (N, K) int32
+    id_clock: torch.Tensor   # (N, K, 16, A)
+    id_keys: torch.Tensor    # (N, K, 16)
+    def_clock: torch.Tensor  # (N, Dcap, A)
+    def_keys: torch.Tensor   # (N, Dcap, Kw)
+    def_count: torch.Tensor  # (N,) int32
+
+
 def _vmap_deferred(st):
     from . import _abi
     d = _abi.MapDeferred()
@@ -265,7 +283,7 @@ def _vmap_deferred(st):
 
 def _vmap_check(ctx, st, what):
     for nm, t in st._asdict().items():
-        ctx.check_tensor(t, f"{what}({nm})", (torch.int32,) if nm in ("vd_n", "def_count") else None)
+        ctx.check_tensor(t, f"{what}({nm})", (torch.int32,) if nm in ("vd_n", "def_count", "nval", "id_n") else None)
         if not t.is_contiguous():
             raise ValueError(f"{what}: {nm} must be contiguous")
     N, A = st.clock.shape
@@ -370,3 +388,53 @@ def map_orswot_egress(states: MapOrswotFrames, actors: torch.Tensor, keys: torch
     s, d = _orswot_struct(ctx, states, "wire.map_orswot_egress")
     return _egress(ctx, "crdt_map_orswot_egress", states.clock.shape[0], states.clock.device, ctypes.byref(s),
                    ctypes.byref(d), dptr(actors), dptr(keys), dptr(members))
+
+
+def _nested_struct(ctx, st, what):
+    from . import _abi
+    N, K, A = _vmap_check(ctx, st, what)
+    K2 = st.iec.shape[2]
+    shapes = dict(ic=(N, K, A), iec=(N, K, K2, A), ivc=(N, K, K2, 8, A), ivv=(N, K, K2, 8), nval=(N, K, K2),
+                  id_n=(N, K), id_clock=(N, K, 16, A), id_keys=(N, K, 16))
+    for nm, shp in shapes.items():
+        if tuple(getattr(st, nm).shape) != shp:
+            raise ValueError(f"{what}: {nm} must be {shp}")
+    s = _abi.MapNestedStates()
+    s.N, s.K, s.K2, s.A = N, K, K2, A
+    for nm in ("clock", "ec", "ic", "iec", "ivc", "ivv", "nval", "id_n", "id_clock", "id_keys"):
+        setattr(s, nm, dptr(getattr(st, nm)))
+    return s, _vmap_deferred(st)
+
+
+def map_nested_ingest(data: torch.Tensor, frame_off: torch.Tensor, actors: torch.Tensor, keys: torch.Tensor,
+                      ikeys: torch.Tensor, Dcap: int, ctx: Optional[Context] = None):
+    """Map<u32, Map<u32, MVReg<u64>>> frames -> (MapNestedFrames, status (N,) int32); ikeys: sorted
+    u32 inner-key dictionary (int32 tensor, at most 64)."""
+    ctx = _ctx(data, ctx)
+    N = _frames(ctx, data, frame_off, "wire.map_nested_ingest")
+    A = _dict(ctx, actors, torch.int32, "wire.map_nested_ingest(actors)")
+    K = _dict(ctx, keys, torch.int32, "wire.map_nested_ingest(keys)")
+    K2 = _dict(ctx, ikeys, torch.int32, "wire.map_nested_ingest(ikeys)")
+    dev = data.device
+    z = lambda *shape: torch.zeros(shape, dtype=torch.int64, device=dev)  # noqa: E731
+    z32 = lambda *shape: torch.zeros(shape, dtype=torch.int32, device=dev)  # noqa: E731
+    st = MapNestedFrames(z(N, A), z(N, K, A), z(N, K, A), z(N, K, K2, A), z(N, K, K2, 8, A), z(N, K, K2, 8),
+                         z32(N, K, K2), z32(N, K), z(N, K, 16, A), z(N, K, 16), z(N, Dcap, A),
+                         z(N, Dcap, (K + 63) // 64), z32(N))
+    s, d = _nested_struct(ctx, st, "wire.map_nested_ingest")
+    status = _status(N, dev)
+    ctx.call("crdt_map_nested_ingest", _ptr_or_dummy(data), dptr(frame_off), dptr(actors), dptr(keys), dptr(ikeys),
+             ctypes.byref(s), ctypes.byref(d), dptr(status))
+    return st, status
+
+
+def map_nested_egress(states: MapNestedFrames, actors: torch.Tensor, keys: torch.Tensor, ikeys: torch.Tensor,
+                      ctx: Optional[Context] = None):
+    """MapNestedFrames -> (frame_off (N+1,), bytes)."""
+    ctx = _ctx(states.clock, ctx)
+    _dict(ctx, actors, torch.int32, "wire.map_nested_egress(actors)")
+    _dict(ctx, keys, torch.int32, "wire.map_nested_egress(keys)")
+    _dict(ctx, ikeys, torch.int32, "wire.map_nested_egress(ikeys)")
+    s, d = _nested_struct(ctx, states, "wire.map_nested_egress")
+    return _egress(ctx, "crdt_map_nested_egress", states.clock.shape[0], states.clock.device, ctypes.byref(s),
+                   ctypes.byref(d), dptr(actors), dptr(keys), dptr(ikeys))

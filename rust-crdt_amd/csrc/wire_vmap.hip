@@ -2,7 +2,9 @@
 // the Map value types the library folds, applies and forgets): Map<u32, GCounter<u32>, u32>,
 // Map<u32, PNCounter<u32>, u32> (the crdt_map_counter_states layout) and Map<u32, Orswot<u64, u32>,
 // u32> (the crdt_map_orswot_states layout — the value type of the reference's merge_error KAT,
-// map.rs:435-494), with the Map's deferred removes as per-state slots (crdt_map_deferred).
+// map.rs:435-494) and Map<u32, Map<u32, MVReg<u64, u32>, u32>, u32> (the crdt_map_nested_states
+// layout — the reference's own Map test type, test/map.rs:10), with the Map's deferred removes as
+// per-state slots (crdt_map_deferred).
 //
 // bincode 1.x of the derives (map.rs:31-47 Map { clock, entries: BTreeMap<K, Entry { clock, val }>,
 // deferred: HashMap<VClock, BTreeSet<K>> }; gcounter.rs:25-28, pncounter.rs:28-32, orswot.rs:20-25):
@@ -10,7 +12,9 @@
 //   u64 d, d x (VClock rm, u64 k, k x u32 key)                       keys ascending (BTreeSet)
 // with value = GCounter: VClock | PNCounter: VClock p, VClock n |
 //   Orswot: VClock clock; u64 m, m x (u64 member, VClock) (HashMap: any order);
-//           u64 e, e x (VClock rm, u64 j, j x u64 member)   (HashMap<VClock, HashSet<M>>: any order)
+//           u64 e, e x (VClock rm, u64 j, j x u64 member)   (HashMap<VClock, HashSet<M>>: any order) |
+//   Map<K2, MVReg>: the same Map layout one level down, its value u64 m, m x (VClock, u64 val)
+//           (mvreg.rs:32-35, Vec order), inner key sets u32 ascending
 // Ingest is one wave per state (the record loop of every VClock across lanes, rows assembled in LDS,
 // written with coalesced stores), as map_ingest_kernel (wire.hip); egress is count -> exclusive scan
 // -> write, present keys / members / key sets in ascending dictionary order (the HashMaps' order is
@@ -21,15 +25,19 @@
 
 namespace crdt {
 
-constexpr int kVwVd = 16;  // nested Orswot deferred removes per key (crdt_map_orswot_states)
+constexpr int kVwVd = 16;  // nested deferred removes per key (crdt_map_orswot_states / crdt_map_nested_states)
+constexpr int kVwVs = 8;   // MVReg slots per inner key (crdt_map_nested_states)
 
 struct VMapWirePlan {
   const uint8_t *bytes;
   const u64 *frame_off;
   unsigned long long N, A, K, Kw, W, M, Mw, Dcap;
-  int orswot;  // value type: 0 = W counter VClocks (GCounter W = 1, PNCounter W = 2), 1 = Orswot
-  const uint32_t *actors, *keys;
+  int vt;  // value type: 0 = W counter VClocks (GCounter W = 1, PNCounter W = 2), 1 = Orswot, 2 = Map<K2, MVReg>
+  const uint32_t *actors, *keys, *ikeys;
   const u64 *members;
+  unsigned long long K2;
+  u64 *ic, *iec, *ivc, *ivv, *id_clock, *id_keys;  // nested Map [N][K][A], [N][K][K2][A], [N][K][K2][8][A],
+  uint32_t *nval, *id_n;                           // [N][K][K2][8], [N][K][16][A], [N][K][16]; [N][K][K2], [N][K]
   u64 *clock, *ec, *val;           // [N][A], [N][K][A], counter [N][K][W][A]
   u64 *oc, *ent;                   // Orswot [N][K][A], [N][K][M][A]
   uint32_t *vd_n;                  // [N][K]
@@ -71,22 +79,26 @@ __global__ __launch_bounds__(kBlock) void vmap_ingest_kernel(VMapWirePlan p) {
   extern __shared__ u64 lds[];
   const int lane = threadIdx.x % kWave, wib = threadIdx.x / kWave;
   const int wpb = blockDim.x / kWave;
-  const uint32_t *actors = p.actors, *keys = p.keys;
+  const uint32_t *actors = p.actors, *keys = p.keys, *ikeys = p.ikeys;
   const u64 *members = p.members;
   u64 *base = lds;
-  if (p.stage) {  // [actors u32 | keys u32 | members u64], the u32 arrays padded to 8 bytes
+  if (p.stage) {  // [actors u32 | keys u32 | members u64 or inner keys u32], the u32 arrays padded to 8 bytes
     uint32_t *la = reinterpret_cast<uint32_t *>(lds);
     const unsigned long long aw = (p.A + 1) / 2, kw = (p.K + 1) / 2;
     for (unsigned long long i = threadIdx.x; i < p.A; i += blockDim.x) la[i] = p.actors[i];
     uint32_t *lk = reinterpret_cast<uint32_t *>(lds + aw);
     for (unsigned long long i = threadIdx.x; i < p.K; i += blockDim.x) lk[i] = p.keys[i];
     u64 *lm = lds + aw + kw;
-    const unsigned long long nm = p.orswot ? p.M : 0;
-    for (unsigned long long i = threadIdx.x; i < nm; i += blockDim.x) lm[i] = p.members[i];
+    const unsigned long long nm = p.vt == 1 ? p.M : (p.vt == 2 ? (p.K2 + 1) / 2 : 0);
+    if (p.vt == 1)
+      for (unsigned long long i = threadIdx.x; i < p.M; i += blockDim.x) lm[i] = p.members[i];
+    if (p.vt == 2)
+      for (unsigned long long i = threadIdx.x; i < p.K2; i += blockDim.x) reinterpret_cast<uint32_t *>(lm)[i] = p.ikeys[i];
     __syncthreads();
     actors = la;
     keys = lk;
-    if (p.orswot) members = lm;
+    if (p.vt == 1) members = lm;
+    if (p.vt == 2) ikeys = reinterpret_cast<const uint32_t *>(lm);
     base = lds + aw + kw + nm;
   }
   const unsigned long long bw = p.Kw > p.Mw ? p.Kw : p.Mw;
@@ -122,7 +134,82 @@ __global__ __launch_bounds__(kBlock) void vmap_ingest_kernel(VMapWirePlan p) {
         if (k == ~0ull) break;
         if (ki >= 0) store_row<u64>(p.ec + sk * p.A, row, p.A, lane);
         wfence();
-        if (!p.orswot) {
+        if (p.vt == 2) {  // the inner Map<K2, MVReg>: clock, entries, deferred removes
+          k = parse_vclock(f, k, actors, p.A, row, lane, st);
+          if (k == ~0ull || k + 2 > f.nw) {
+            k = ~0ull;
+            break;
+          }
+          if (ki >= 0) store_row<u64>(p.ic + sk * p.A, row, p.A, lane);
+          wfence();
+          const u64 n2 = rd64(f.w, k);
+          k += 2;
+          for (u64 j = 0; j < n2 && k != ~0ull; ++j) {
+            if (k + 1 > f.nw) {
+              k = ~0ull;
+              break;
+            }
+            const long long ji = find_u32(ikeys, p.K2, f.w[k], j);
+            if (ji < 0) st |= kWireMissing;
+            const bool on = ki >= 0 && ji >= 0;
+            const unsigned long long skj = sk * p.K2 + (unsigned long long)(ji < 0 ? 0 : ji);
+            k = parse_vclock(f, k + 1, actors, p.A, row, lane, st);
+            if (k == ~0ull || k + 2 > f.nw) {
+              k = ~0ull;
+              break;
+            }
+            if (on) store_row<u64>(p.iec + skj * p.A, row, p.A, lane);
+            wfence();
+            const u64 m = rd64(f.w, k);
+            k += 2;
+            unsigned long long nv = 0;
+            for (u64 v = 0; v < m && k != ~0ull; ++v) {
+              k = parse_vclock(f, k, actors, p.A, row, lane, st);
+              if (k == ~0ull || k + 2 > f.nw) {
+                k = ~0ull;
+                break;
+              }
+              const u64 val = rd64(f.w, k);
+              k += 2;
+              if (on) {
+                if (nv < (unsigned long long)kVwVs) {
+                  store_row<u64>(p.ivc + (skj * kVwVs + nv) * p.A, row, p.A, lane);
+                  if (lane == 0) p.ivv[skj * kVwVs + nv] = val;
+                  ++nv;
+                } else {
+                  st |= kWireCap;
+                }
+              }
+              wfence();
+            }
+            if (on && lane == 0) p.nval[skj] = (uint32_t)nv;
+          }
+          if (k == ~0ull || k + 2 > f.nw) {
+            k = ~0ull;
+            break;
+          }
+          const u64 d2 = rd64(f.w, k);
+          k += 2;
+          unsigned long long dn = 0;
+          for (u64 j = 0; j < d2 && k != ~0ull; ++j) {
+            k = parse_vclock(f, k, actors, p.A, row, lane, st);
+            k = parse_idset(f, k, false, ikeys, nullptr, p.K2, bits, 1, lane, st);
+            if (k == ~0ull) break;
+            if (ki >= 0) {
+              if (dn < (unsigned long long)kVwVd) {
+                store_row<u64>(p.id_clock + (sk * kVwVd + dn) * p.A, row, p.A, lane);
+                if (lane == 0) p.id_keys[sk * kVwVd + dn] = bits[0];
+                ++dn;
+              } else {
+                st |= kWireCap;
+              }
+            }
+            wfence();
+          }
+          if (ki >= 0 && lane == 0) p.id_n[sk] = (uint32_t)dn;
+          continue;
+        }
+        if (p.vt == 0) {
           for (unsigned long long w = 0; w < p.W && k != ~0ull; ++w) {
             k = parse_vclock(f, k, actors, p.A, row, lane, st);
             if (k != ~0ull && ki >= 0) store_row<u64>(p.val + (sk * p.W + w) * p.A, row, p.A, lane);
@@ -264,7 +351,55 @@ __global__ __launch_bounds__(kBlock) void vmap_egress_kernel(VMapWirePlan p, int
         if (lane == 0) w[k] = p.keys[key];
         k = write_vclock(w, k + 1, er, p.A, p.actors, lane);
       }
-      if (!p.orswot) {
+      if (p.vt == 2) {
+        const u64 *ic = p.ic + sk * p.A;
+        sz += vclock_bytes(ic, p.A, lane) + 8;
+        if (write) k = write_vclock(w, k, ic, p.A, p.actors, lane);
+        u64 n2 = 0;
+        for (unsigned long long j = 0; j < p.K2; ++j) n2 += nnz_row(p.iec + (sk * p.K2 + j) * p.A, p.A, lane) != 0;
+        if (write) {
+          if (lane == 0) wr64(w, k, n2);
+          k += 2;
+        }
+        for (unsigned long long j = 0; j < p.K2; ++j) {
+          const unsigned long long skj = sk * p.K2 + j;
+          const u64 *er2 = p.iec + skj * p.A;
+          if (nnz_row(er2, p.A, lane) == 0) continue;
+          const unsigned long long m = p.nval[skj] < (uint32_t)kVwVs ? p.nval[skj] : kVwVs;
+          sz += 4 + vclock_bytes(er2, p.A, lane) + 8;
+          if (write) {
+            if (lane == 0) w[k] = p.ikeys[j];
+            k = write_vclock(w, k + 1, er2, p.A, p.actors, lane);
+            if (lane == 0) wr64(w, k, m);
+            k += 2;
+          }
+          for (unsigned long long v = 0; v < m; ++v) {
+            const u64 *vr = p.ivc + (skj * kVwVs + v) * p.A;
+            sz += vclock_bytes(vr, p.A, lane) + 8;
+            if (write) {
+              k = write_vclock(w, k, vr, p.A, p.actors, lane);
+              if (lane == 0) wr64(w, k, p.ivv[skj * kVwVs + v]);
+              k += 2;
+            }
+          }
+        }
+        const unsigned long long dn = p.id_n[sk] < (uint32_t)kVwVd ? p.id_n[sk] : kVwVd;
+        sz += 8;
+        if (write) {
+          if (lane == 0) wr64(w, k, dn);
+          k += 2;
+        }
+        for (unsigned long long i = 0; i < dn; ++i) {
+          const u64 *rm = p.id_clock + (sk * kVwVd + i) * p.A, *kb = p.id_keys + sk * kVwVd + i;
+          sz += vclock_bytes(rm, p.A, lane) + 8 + 4 * popc_row(kb, 1, lane);
+          if (write) {
+            k = write_vclock(w, k, rm, p.A, p.actors, lane);
+            k = write_idset(w, k, kb, 1, false, p.ikeys, nullptr, lane);
+          }
+        }
+        continue;
+      }
+      if (p.vt == 0) {
         for (unsigned long long x = 0; x < p.W; ++x) {
           const u64 *vr = p.val + (sk * p.W + x) * p.A;
           sz += vclock_bytes(vr, p.A, lane);
@@ -378,7 +513,7 @@ static int vmap_orswot_plan(crdt_ctx *ctx, const crdt_map_orswot_states *st, con
   p.Kw = Kw;
   p.M = M;
   p.Mw = Mw;
-  p.orswot = 1;
+  p.vt = 1;
   p.actors = actors;
   p.keys = keys;
   p.members = (const u64 *)members;
@@ -392,6 +527,42 @@ static int vmap_orswot_plan(crdt_ctx *ctx, const crdt_map_orswot_states *st, con
   return CRDT_OK;
 }
 
+static int vmap_nested_plan(crdt_ctx *ctx, const crdt_map_nested_states *st, const crdt_map_deferred *df,
+                            const uint32_t *actors, const uint32_t *keys, const uint32_t *ikeys, VMapWirePlan &p,
+                            const char *what) {
+  if (!st || !actors || !keys || !ikeys) return fail(ctx, CRDT_EINVAL, "%s: NULL states / dictionaries", what);
+  const size_t N = st->N, K = st->K, K2 = st->K2, A = st->A;
+  if (A == 0 || K == 0 || K2 == 0) return fail(ctx, CRDT_EINVAL, "%s: need A, K, K2 >= 1", what);
+  if (K2 > 64) return fail(ctx, CRDT_EUNSUPPORTED, "%s: K2 = %zu > 64 (inner key sets are one u64 mask)", what, K2);
+  if (N && (!st->clock || !st->ec || !st->ic || !st->iec || !st->ivc || !st->ivv || !st->nval || !st->id_n ||
+            !st->id_clock || !st->id_keys))
+    return fail(ctx, CRDT_EINVAL, "%s: NULL state buffer", what);
+  const size_t Kw = (K + 63) / 64;
+  if (A + Kw > (size_t)kWireRowLds) return fail(ctx, CRDT_EUNSUPPORTED, "%s: A + K/64 too large", what);
+  p = VMapWirePlan{};
+  if (int rc = vmap_deferred_plan(ctx, df, N, p, what)) return rc;
+  p.N = N;
+  p.A = A;
+  p.K = K;
+  p.Kw = Kw;
+  p.K2 = K2;
+  p.vt = 2;
+  p.actors = actors;
+  p.keys = keys;
+  p.ikeys = ikeys;
+  p.clock = (u64 *)st->clock;
+  p.ec = (u64 *)st->ec;
+  p.ic = (u64 *)st->ic;
+  p.iec = (u64 *)st->iec;
+  p.ivc = (u64 *)st->ivc;
+  p.ivv = (u64 *)st->ivv;
+  p.nval = st->nval;
+  p.id_n = st->id_n;
+  p.id_clock = (u64 *)st->id_clock;
+  p.id_keys = (u64 *)st->id_keys;
+  return CRDT_OK;
+}
+
 static int vmap_ingest(crdt_ctx *ctx, VMapWirePlan &p, const uint8_t *bytes, const uint64_t *frame_off,
                        uint32_t *status) {
   const size_t N = p.N;
@@ -400,8 +571,17 @@ static int vmap_ingest(crdt_ctx *ctx, VMapWirePlan &p, const uint8_t *bytes, con
   CRDT_HIP(ctx, hipSetDevice(ctx->device));
   // absent keys / members / nested removes are zero rows
   if (int rc = device_fill(ctx, p.ec, N * p.K * p.A * 8, 0)) return rc;
-  if (!p.orswot) {
+  if (p.vt == 0) {
     if (int rc = device_fill(ctx, p.val, N * p.K * p.W * p.A * 8, 0)) return rc;
+  } else if (p.vt == 2) {
+    if (int rc = device_fill(ctx, p.ic, N * p.K * p.A * 8, 0)) return rc;
+    if (int rc = device_fill(ctx, p.iec, N * p.K * p.K2 * p.A * 8, 0)) return rc;
+    if (int rc = device_fill(ctx, p.ivc, N * p.K * p.K2 * kVwVs * p.A * 8, 0)) return rc;
+    if (int rc = device_fill(ctx, p.ivv, N * p.K * p.K2 * kVwVs * 8, 0)) return rc;
+    if (int rc = device_fill(ctx, p.nval, N * p.K * p.K2 * 4, 0)) return rc;
+    if (int rc = device_fill(ctx, p.id_n, N * p.K * 4, 0)) return rc;
+    if (int rc = device_fill(ctx, p.id_clock, N * p.K * kVwVd * p.A * 8, 0)) return rc;
+    if (int rc = device_fill(ctx, p.id_keys, N * p.K * kVwVd * 8, 0)) return rc;
   } else {
     if (int rc = device_fill(ctx, p.oc, N * p.K * p.A * 8, 0)) return rc;
     if (int rc = device_fill(ctx, p.ent, N * p.K * p.M * p.A * 8, 0)) return rc;
@@ -416,7 +596,7 @@ static int vmap_ingest(crdt_ctx *ctx, VMapWirePlan &p, const uint8_t *bytes, con
   const size_t per_wave = p.A + bw;
   int wpb = 4;
   while (wpb > 1 && (size_t)wpb * per_wave * 8 > 64 * 1024) --wpb;
-  const size_t dw = (p.A + 1) / 2 + (p.K + 1) / 2 + (p.orswot ? p.M : 0);
+  const size_t dw = (p.A + 1) / 2 + (p.K + 1) / 2 + (p.vt == 1 ? p.M : (p.vt == 2 ? (p.K2 + 1) / 2 : 0));
   p.stage = (dw + wpb * per_wave) * 8 <= 64 * 1024;
   const size_t lds = ((p.stage ? dw : 0) + wpb * per_wave) * 8;
   timing_begin(ctx, "wire_ingest");
@@ -496,6 +676,27 @@ int crdt_map_orswot_egress(crdt_ctx *ctx, const crdt_map_orswot_states *states, 
   VMapWirePlan p;
   if (int rc = vmap_orswot_plan(ctx, states, def, actors, keys, members, p, "map_orswot_egress")) return rc;
   return vmap_egress(ctx, p, frame_off, bytes, cap, total, "map_orswot_egress");
+}
+
+int crdt_map_nested_ingest(crdt_ctx *ctx, const uint8_t *bytes, const uint64_t *frame_off, const uint32_t *actors,
+                           const uint32_t *keys, const uint32_t *ikeys, const crdt_map_nested_states *out,
+                           const crdt_map_deferred *out_def, uint32_t *status) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
+  CRDT_CHECK_CTX(ctx);
+  VMapWirePlan p;
+  if (int rc = vmap_nested_plan(ctx, out, out_def, actors, keys, ikeys, p, "map_nested_ingest")) return rc;
+  return vmap_ingest(ctx, p, bytes, frame_off, status);
+}
+
+int crdt_map_nested_egress(crdt_ctx *ctx, const crdt_map_nested_states *states, const crdt_map_deferred *def,
+                           const uint32_t *actors, const uint32_t *keys, const uint32_t *ikeys, uint64_t *frame_off,
+                           uint8_t *bytes, size_t cap, size_t *total) {
+  CRDT_DEVICE_MEM_ONLY(ctx);
+  CRDT_CHECK_CTX(ctx);
+  if (total) *total = 0;
+  VMapWirePlan p;
+  if (int rc = vmap_nested_plan(ctx, states, def, actors, keys, ikeys, p, "map_nested_egress")) return rc;
+  return vmap_egress(ctx, p, frame_off, bytes, cap, total, "map_nested_egress");
 }
 
 }  // extern "C"

@@ -1,7 +1,7 @@
-"""GPU: serde wire ingest / egress of the value-typed Maps (round 5; crdt_map_counter_ingest /
-_egress, crdt_map_orswot_ingest / _egress) against the oracle's bincode
-restatement of the derives (oracle.bc_map_obj / unbc_map_obj; map.rs:31-47 with gcounter.rs:25-28,
-pncounter.rs:28-32, orswot.rs:20-25 as the value):
+"""GPU: serde wire ingest / egress of the value-typed Maps (round 5; crdt_map_{counter,orswot,nested}_
+ingest / _egress) against the oracle's bincode restatement of the derives
+(oracle.bc_map_obj / unbc_map_obj; map.rs:31-47 with gcounter.rs:25-28, pncounter.rs:28-32,
+orswot.rs:20-25 or Map<K2, MVReg> (mvreg.rs:32-35, the reference's TMap) as the value):
   * ingest of op-replay states (deferred removes at both levels) equals the oracle's dense layouts
     (map_counter_to_dense / map_orswot_to_dense), and egress writes the same frames byte for byte;
   * serialized replicas -> ingest -> CmRDT::apply op streams -> egress -> decode == the oracle's
@@ -200,3 +200,68 @@ def test_value_map_malformed_missing_and_capacity(gpu_ctx):
     assert s[0] == wire.CAP and s[1] == wire.MISSING and s[2] & wire.BAD, s
     assert int(ost.vd_n[0, 0]) == 16
     assert to_host(ost.ec)[1, 2].any() and not to_host(ost.ent)[1, 2].any()  # the unknown member skipped
+
+
+def _nested_fits(m):
+    return (len(m.deferred) <= 16 and all(len(e.val.deferred) <= 16 for e in m.entries.values())
+            and all(len(ie.val.vals) <= 8 for e in m.entries.values() for ie in e.val.entries.values()))
+
+
+@pytest.mark.parametrize("K2,A", [(6, 5), (64, 4), (5, 70)])
+def test_map_nested_ingest_egress(gpu_ctx, K2, A):
+    """Map<u32, Map<u32, MVReg<u64>>> (test/map.rs:10): ingest equals the state layout built from the
+    oracle objects, egress reproduces the frames byte for byte."""
+    from test_gpu_map_nested import nested_states
+    K = 4
+    maps = [m for m in O.nested_map_objects(28, K, K2, A, seed=50 + K2 + A, steps=200, p_irm=0.5, p_ooo=0.8,
+                                            p_rm=0.3) if _nested_fits(m)]
+    N = len(maps)
+    rng = np.random.default_rng(K2 + A)
+    aids, ad = actor_dict(rng, A)
+    kids, kd = actor_dict(rng, K)
+    iids, idd = actor_dict(rng, K2)
+    blob, off = O.frames([O.bc_map_obj(m, aids, kids, iid=iids) for m in maps])
+    Dcap = 16
+    st, status = wire.map_nested_ingest(dev_bytes(blob), dev_off(off), ad, kd, idd, Dcap, ctx=gpu_ctx)
+    assert (status.cpu().numpy() == 0).all()
+    exp, slots, _ = nested_states(maps, K, K2, A)
+    for nm in exp._fields:
+        np.testing.assert_array_equal(getattr(st, nm).cpu().numpy(), getattr(exp, nm).cpu().numpy(), err_msg=nm)
+    for got, e in zip((st.def_clock, st.def_keys, st.def_count), slots):
+        np.testing.assert_array_equal(got.cpu().numpy(), e.cpu().numpy())
+    assert int(st.id_n.sum()) > 0 and int(st.def_count.sum()) > 0
+    eoff, edata = wire.map_nested_egress(st, ad, kd, idd, ctx=gpu_ctx)
+    assert eoff.cpu().tolist() == off
+    assert bytes(edata.cpu().numpy().tobytes()) == blob
+
+
+def test_map_nested_apply_through_bytes(gpu_ctx):
+    """Serialized TMap replicas -> ingest -> nested_apply_batch -> egress -> decode == Map.apply."""
+    from test_gpu_map_nested import canon
+    from test_gpu_map_nested_apply import _regs_in_order, _streams
+    K, K2, A, T = 4, 6, 5, 30
+    maps = [m for m in O.nested_map_objects(32, K, K2, A, seed=81, steps=200, p_irm=0.5, p_ooo=0.8, p_rm=0.3)
+            if _nested_fits(m)][:24]
+    rng = np.random.default_rng(73)
+    streams, oops = _streams(rng, maps, K, K2, A, T)
+    exps = [m.copy() for m in maps]
+    for n, e in enumerate(exps):
+        for op in oops[n]:
+            e.apply(op)
+    keep = [n for n, e in enumerate(exps) if _nested_fits(e)]
+    maps, exps, streams = [maps[n] for n in keep], [exps[n] for n in keep], [streams[n] for n in keep]
+    aids, ad = actor_dict(rng, A)
+    kids, kd = actor_dict(rng, K)
+    iids, idd = actor_dict(rng, K2)
+    blob, off = O.frames([O.bc_map_obj(m, aids, kids, iid=iids) for m in maps])
+    st, status = wire.map_nested_ingest(dev_bytes(blob), dev_off(off), ad, kd, idd, 16, ctx=gpu_ctx)
+    assert (status.cpu().numpy() == 0).all()
+    ops = cg.map.encode_nested_ops(streams, A, "cuda:0")
+    ast = cg.map.nested_apply_batch(st, st.def_clock, st.def_keys, st.def_count, ops, ctx=gpu_ctx).cpu().numpy()
+    assert (ast == 0).all(), ast
+    eoff, edata = wire.map_nested_egress(st, ad, kd, idd, ctx=gpu_ctx)
+    for n, fr in enumerate(host_frames(edata, eoff)):
+        got, pos = O.unbc_map_obj(fr, "nested", aids, kids, iid=iids)
+        assert pos == len(fr)
+        assert canon(got) == canon(exps[n]) and _regs_in_order(got) == _regs_in_order(exps[n]), n
+    assert len(exps) >= 12

@@ -86,3 +86,20 @@ def test_value_map_bincode_round_trips_and_layout():
     b = O.bc_map_obj(m, aid, kid)
     assert b == (O.bc_vclock({3: 2}) + struct.pack("<QI", 1, 7) + O.bc_vclock({3: 2}) + O.bc_vclock({3: 1})
                  + O.bc_vclock({3: 1}) + struct.pack("<Q", 1) + O.bc_vclock({10: 4}) + struct.pack("<QII", 2, 2, 8))
+
+
+def test_nested_map_bincode_round_trip():
+    """Map<u32, Map<u32, MVReg<u64>>> (the reference's TMap, test/map.rs:10): decode(encode(m)) == m
+    over op-replay states with inner and outer deferred removes, registers in Vec order."""
+    aid = [3, 10, 11, 40, 41, 90]
+    kid = [2, 7, 8, 100, 101]
+    iid = [1, 4, 9, 16, 25, 36, 49]
+    maps = O.nested_map_objects(16, 5, 7, 6, seed=33, steps=220, p_irm=0.5, p_ooo=0.8, p_rm=0.3)
+    assert sum(len(e.val.deferred) for m in maps for e in m.entries.values()) > 0
+    for m in maps:
+        b = O.bc_map_obj(m, aid, kid, iid=iid)
+        got, pos = O.unbc_map_obj(b, "nested", aid, kid, iid=iid)
+        assert pos == len(b) and got == m
+        for k, e in m.entries.items():
+            for j, ie in e.val.entries.items():
+                assert [x for _, x in got.entries[k].val.entries[j].val.vals] == [x for _, x in ie.val.vals]
