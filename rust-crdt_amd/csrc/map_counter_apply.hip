@@ -112,19 +112,29 @@ __global__ __launch_bounds__(256) void map_counter_apply_kernel(MapCounterApplyP
       }
     }
   };
-  auto apply_deferred = [&]() {
+  // apply_deferred re-forgets every key of every deferred remove (map.rs:311-316).  After one full
+  // pass each remove's keys are forgotten by its clock, and later ops keep that (an Rm forgets its own
+  // keys by its clock; forgets are idempotent and commute) except an Up, which changes only its own
+  // key's rows: every later pass re-forgets that key alone — the same rows the full pass would
+  // change.  The first pass stays full (the input state need not hold the invariant).
+  bool full = true;
+  auto apply_deferred = [&](unsigned long long kk) {
     unsigned o = 0;
     for (unsigned d = 0; d < dcnt; ++d) {
       u64 r[APL];
 #pragma unroll
       for (int j = 0; j < APL; ++j) r[j] = word(j) < A ? sclk[d * A + word(j)] : 0ull;
-      for (unsigned long long w = 0; w < Kw; ++w) {
-        u64 bits = skey[d * Kw + w];
-        while (bits) {
-          const unsigned long long k = w * 64 + (unsigned long long)__builtin_ctzll(bits);
-          bits &= bits - 1;
-          if (k < K) key_rm(k, r);
+      if (full) {
+        for (unsigned long long w = 0; w < Kw; ++w) {
+          u64 bits = skey[d * Kw + w];
+          while (bits) {
+            const unsigned long long k = w * 64 + (unsigned long long)__builtin_ctzll(bits);
+            bits &= bits - 1;
+            if (k < K) key_rm(k, r);
+          }
         }
+      } else if ((skey[d * Kw + kk / 64] >> (kk % 64)) & 1ull) {
+        key_rm(kk, r);
       }
       if (dominated(r)) continue;  // no longer deferred
       if (o != d) {
@@ -134,6 +144,7 @@ __global__ __launch_bounds__(256) void map_counter_apply_kernel(MapCounterApplyP
       ++o;
     }
     dcnt = o;
+    full = false;
   };
 
   for (unsigned long long o = ob; o < oe; ++o) {
@@ -159,7 +170,7 @@ __global__ __launch_bounds__(256) void map_counter_apply_kernel(MapCounterApplyP
         u64 *vp = V + (k * W + dir) * A + va;
         if (*vp < vc) *vp = vc;  // entry.val.apply(op)
       }
-      apply_deferred();
+      apply_deferred(k);
     } else if (kind == 1) {  // ---- Op::Rm -> apply_keyset_rm
       const unsigned rr = p.clk_row ? p.clk_row[o] : 0xffffffffu;
       const u64 kb = p.key_off[o], ke = p.key_off[o + 1];

@@ -360,14 +360,17 @@ __global__ __launch_bounds__(256) void map_nested_apply_kernel(NestedApplyPlan p
     for (unsigned long long w = (unsigned long long)lane; w < Kw; w += kWave)
       skey[d * Kw + w] = p.def_keys[(s * Dcap + d) * Kw + w];
   }
-  auto map_apply_deferred = [&]() {
+  // apply_deferred (map.rs:311-316): full on its first run, then restricted to the Up's own key (the
+  // only rows an Up changes; forgets are idempotent and commute — see csrc/map_counter_apply.hip)
+  bool full = true;
+  auto map_apply_deferred = [&](unsigned long long kk) {
     unsigned o = 0;
     for (unsigned d = 0; d < dcnt; ++d) {
       u64 r[APL];
 #pragma unroll
       for (int j = 0; j < APL; ++j) r[j] = word(j) < A ? sclk[d * A + word(j)] : 0ull;
-      for (unsigned long long w = 0; w < Kw; ++w) {
-        u64 bits = skey[d * Kw + w];
+      for (unsigned long long w = full ? 0 : kk / 64; w < (full ? Kw : kk / 64 + 1); ++w) {
+        u64 bits = skey[d * Kw + w] & (full ? ~0ull : 1ull << (kk % 64));
         while (bits) {
           const unsigned long long k = w * 64 + (unsigned long long)__builtin_ctzll(bits);
           bits &= bits - 1;
@@ -386,6 +389,7 @@ __global__ __launch_bounds__(256) void map_nested_apply_kernel(NestedApplyPlan p
       ++o;
     }
     dcnt = o;
+    full = false;
   };
 
   for (unsigned long long o = ob; o < oe; ++o) {
@@ -413,7 +417,7 @@ __global__ __launch_bounds__(256) void map_nested_apply_kernel(NestedApplyPlan p
 #pragma unroll
       for (int j = 0; j < APL; ++j)
         if ((unsigned)j == a / 64 && (unsigned long long)lane == a % 64 && c[j] < cnt) c[j] = cnt;
-      map_apply_deferred();
+      map_apply_deferred(k);
     } else if (kind == 1) {  // ---- Op::Rm -> apply_keyset_rm
       const unsigned rr = p.clk_row[o];
       const u64 kb = p.key_off[o], ke = p.key_off[o + 1];
