@@ -107,3 +107,42 @@ def test_map_counter_apply_malformed_and_capacity(gpu_ctx):
     v = to_host(val)
     assert v[0, 2, 1, 3] == 7 and to_host(ec)[0, 2, 1] == 1  # the one good op of state 0 applied
     assert int(cnt[1]) == 2 and to_host(clock)[2].sum() == 0
+
+
+@pytest.mark.parametrize("W", [1, 2])
+def test_map_counter_apply_unapplied_input_deferred(gpu_ctx, W):
+    """Input states holding deferred removes never applied to their keys (the reference's apply_deferred
+    still forgets those keys on the next Up): the kernel's first apply_deferred pass is a full one, the
+    later ones re-forget the Up's own key only."""
+    N, K, A, T, Dcap = 16, 5, 6, 12, 16
+    maps = O.map_counter_objects(N, K, A, W, seed=40, steps=220)
+    rng = np.random.default_rng(90 + W)
+    for m in maps:  # a remove from the future naming present keys, not applied to them
+        row = {a: m.clock.get(a) + 1 for a in range(2)}
+        m.deferred[O.VClock(dict(row))] = set(int(k) for k in rng.choice(K, size=2, replace=False))
+    d = O.map_counter_to_dense(maps, K, A, W)
+    streams, oracle_ops = _streams(rng, maps, K, A, W, T)
+    Kw = (K + 63) // 64
+    dcl = np.zeros((N, Dcap, A), np.uint64)
+    dks = np.zeros((N, Dcap, Kw), np.uint64)
+    cnt = np.zeros(N, np.int32)
+    for j in range(d["def_row"].shape[0]):
+        n = int(d["def_row"][j])
+        dcl[n, cnt[n]], dks[n, cnt[n]] = d["def_clock"][j], d["def_keys"][j]
+        cnt[n] += 1
+    clock, ec, val = to_dev(d["clock"]), to_dev(d["ec"]), to_dev(d["val"])
+    tdc, tdk, tcnt = to_dev(dcl), to_dev(dks), torch.from_numpy(cnt).cuda()
+    ops = cg.map.encode_counter_ops(streams, A, "cuda:0")
+    status = cg.map.counter_apply_batch(clock, ec, val, tdc, tdk, tcnt, ops, ctx=gpu_ctx).cpu().numpy()
+    c, e, v = to_host(clock), to_host(ec), to_host(val)
+    hdc, hdk, hcnt = to_host(tdc), to_host(tdk), tcnt.cpu().numpy()
+    ups = 0
+    for n in range(N):
+        exp = maps[n].copy()
+        for op in oracle_ops[n]:
+            exp.apply(op)
+        ups += sum(isinstance(op, O.MapUp) for op in oracle_ops[n])
+        assert status[n] == 0, (n, status[n])
+        dfr = [(hdc[n, i], O.bitmap_members(hdk[n, i])) for i in range(int(hcnt[n]))]
+        assert O.dense_to_map_counter(c[n], e[n], v[n], dfr) == exp, n
+    assert ups > 0

@@ -298,3 +298,29 @@ def test_map_nested_apply_malformed_and_capacity(gpu_ctx):
     assert status[2] == 16, status
     got = decode_states(st, 2, _slot_deferred(slots, 2))
     assert [v for _, v in got.entries[0].val.entries[0].val.vals] == list(range(8))
+
+
+def test_map_nested_apply_unapplied_input_deferred(gpu_ctx):
+    """Outer removes in the input never applied to their keys: the first Up's full apply_deferred pass
+    applies them (the later passes re-forget the Up's key only)."""
+    K, K2, A, T = 4, 6, 5, 20
+    maps = [m for m in O.nested_map_objects(24, K, K2, A, seed=84, steps=200, p_irm=0.5, p_ooo=0.8, p_rm=0.3)
+            if _fits(m) and len(m.deferred) < 16][:16]
+    rng = np.random.default_rng(85)
+    for m in maps:
+        row = {0: m.clock.get(0) + 1, 1: m.clock.get(1) + 1}
+        m.deferred[VClock(row)] = set(int(k) for k in rng.choice(K, size=2, replace=False))
+    streams, oops = _streams(rng, maps, K, K2, A, T)
+    exps = [m.copy() for m in maps]
+    for n, e in enumerate(exps):
+        for op in oops[n]:
+            e.apply(op)
+    keep = [n for n, e in enumerate(exps) if _fits(e)]
+    st, slots, _ = nested_states([maps[n] for n in keep], K, K2, A)
+    ops = cg.map.encode_nested_ops([streams[n] for n in keep], A, "cuda:0")
+    status = cg.map.nested_apply_batch(st, *slots, ops, ctx=gpu_ctx).cpu().numpy()
+    for i, n in enumerate(keep):
+        assert status[i] == 0, (i, status[i])
+        got = decode_states(st, i, _slot_deferred(slots, i))
+        assert canon(got) == canon(exps[n]) and _regs_in_order(got) == _regs_in_order(exps[n]), n
+    assert len(keep) >= 8

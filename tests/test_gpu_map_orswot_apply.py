@@ -117,3 +117,53 @@ def test_map_orswot_apply(gpu_ctx, M, A, seed):
         nested += sum(len(x.val.deferred) for x in exp.entries.values())
         mapdef += len(exp.deferred)
     assert nested > 0 and mapdef > 0
+
+
+def test_map_orswot_apply_unapplied_input_deferred(gpu_ctx):
+    """As the counter Map's test: Map-level removes in the input never applied to their keys are
+    applied by the first Up's full apply_deferred pass, later passes re-forget the Up's key only."""
+    N, K, M, A, T, Dcap = 12, 4, 5, 5, 16, 16
+    maps = O.map_orswot_objects(N, K, M, A, seed=61, steps=160, p_vrm=0.3)
+    exps = [O.map_fold_objects([m]) for m in maps]
+    if any(len(e.val.deferred) > cg.map.VD_CAP for x in exps for e in x.entries.values()):
+        pytest.skip("nested deferred past the kernel's capacity")
+    res, kw, off = _states(gpu_ctx, maps, K, M, A)
+    rng = np.random.default_rng(91)
+    Kw = (K + 63) // 64
+    dcl = np.zeros((N, Dcap, A), np.uint64)
+    dks = np.zeros((N, Dcap, Kw), np.uint64)
+    cnt = np.zeros(N, np.int32)
+    if kw:
+        keep, hk, hc = res.def_keep.cpu().numpy(), to_host(res.def_keys), to_host(kw["def_clock"])
+        for n in range(N):
+            for j in range(off[n], off[n + 1]):
+                if keep[j]:
+                    dcl[n, cnt[n]], dks[n, cnt[n]] = hc[j], hk[j]
+                    cnt[n] += 1
+    for n, x in enumerate(exps):  # one more remove from the future, not applied to its keys
+        row = np.zeros(A, np.uint64)
+        row[0], row[1] = x.clock.get(0) + 1, x.clock.get(1) + 1
+        ks = set(int(k) for k in rng.choice(K, size=2, replace=False))
+        x.deferred[O.VClock({0: int(row[0]), 1: int(row[1])})] = set(ks)
+        dcl[n, cnt[n]] = row
+        dks[n, cnt[n], 0] = sum(1 << k for k in ks)
+        cnt[n] += 1
+    streams, oops = _streams(rng, exps, K, M, A, T)
+    for n in range(N):
+        for op in oops[n]:
+            exps[n].apply(op)
+    if any(len(e.val.deferred) > cg.map.VD_CAP for x in exps for e in x.entries.values()) or \
+            any(len(x.deferred) > Dcap for x in exps):
+        pytest.skip("past the kernel's deferred capacity")
+    tdc, tdk, tcnt = to_dev(dcl), to_dev(dks), torch.from_numpy(cnt).cuda()
+    ops = cg.map.encode_orswot_map_ops(streams, A, "cuda:0")
+    status = cg.map.orswot_apply_batch(res, tdc, tdk, tcnt, ops, ctx=gpu_ctx).cpu().numpy()
+    c, e, o, m = to_host(res.clock), to_host(res.ec), to_host(res.oc), to_host(res.ent)
+    vn, vc, vm = res.vd_n.cpu().numpy(), to_host(res.vd_clock), to_host(res.vd_mem)
+    hdc, hdk, hcnt = to_host(tdc), to_host(tdk), tcnt.cpu().numpy()
+    for n in range(N):
+        assert status[n] == 0, (n, status[n])
+        vd = {k: [(vc[n, k, i], O.bitmap_members(vm[n, k, i:i + 1])) for i in range(int(vn[n, k]))] for k in range(K)}
+        dfr = [(hdc[n, i], O.bitmap_members(hdk[n, i])) for i in range(int(hcnt[n]))]
+        got = O.dense_to_map_orswot(c[n], e[n], o[n], m[n], vd, dfr)
+        assert got.clock == exps[n].clock and got.entries == exps[n].entries and got.deferred == exps[n].deferred, n
