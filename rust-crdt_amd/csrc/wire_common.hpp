@@ -78,10 +78,13 @@ __device__ __forceinline__ void store_row(u64 *dst, const u64 *row, unsigned lon
   for (unsigned long long a = lane; a < W; a += kWave) dst[a] = row[a];
 }
 
+// nonzero words of a row: one ballot per 64 words (no shuffle-reduction chain; the count is uniform)
 __device__ __forceinline__ u64 nnz_row(const u64 *r, unsigned long long A, int lane) {
   unsigned long long c = 0;
-  for (unsigned long long a = lane; a < A; a += kWave) c += r[a] != 0;
-  for (int off = kWave / 2; off > 0; off >>= 1) c += __shfl_xor(c, off, kWave);
+  for (unsigned long long a0 = 0; a0 < A; a0 += kWave) {
+    const unsigned long long a = a0 + lane;
+    c += __popcll(__ballot(a < A && r[a] != 0));
+  }
   return c;
 }
 __device__ __forceinline__ u64 popc_row(const u64 *r, unsigned long long W, int lane) {
