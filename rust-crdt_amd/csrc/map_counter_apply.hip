@@ -43,7 +43,7 @@ struct MapCounterApplyPlan {
 };
 
 template <int APL>
-__global__ __launch_bounds__(256) void map_counter_apply_kernel(MapCounterApplyPlan p) {
+__global__ __launch_bounds__(256) CRDT_VAPPLY_ATTR void map_counter_apply_kernel(MapCounterApplyPlan p) {
   extern __shared__ u64 lds[];
   const int lane = (int)(threadIdx.x % kWave), wv = (int)(threadIdx.x / kWave);
   const unsigned long long s = (unsigned long long)blockIdx.x * p.wpb + wv;

@@ -42,7 +42,7 @@ struct MapOrswotApplyPlan {
 };
 
 template <int APL>
-__global__ __launch_bounds__(256) void map_orswot_apply_kernel(MapOrswotApplyPlan p) {
+__global__ __launch_bounds__(256) CRDT_VAPPLY_ATTR void map_orswot_apply_kernel(MapOrswotApplyPlan p) {
   extern __shared__ u64 lds[];
   const int lane = (int)(threadIdx.x % kWave), wv = (int)(threadIdx.x / kWave);
   const unsigned long long s = (unsigned long long)blockIdx.x * p.wpb + wv;
