@@ -20,16 +20,6 @@ using u64x2 = unsigned long long __attribute__((ext_vector_type(2)));
 
 // One wave is 64 lanes on gfx950; every block size below is a multiple of it.
 constexpr int kWave = 64;
-// value-Map apply kernels: waves per SIMD requested from the register allocator (build option; 0 =
-// the compiler's choice)
-#ifndef CRDT_VAPPLY_WPE
-#define CRDT_VAPPLY_WPE 0
-#endif
-#if CRDT_VAPPLY_WPE
-#define CRDT_VAPPLY_ATTR __attribute__((amdgpu_waves_per_eu(CRDT_VAPPLY_WPE)))
-#else
-#define CRDT_VAPPLY_ATTR
-#endif
 
 // Waves per SIMD asked of the A > 64 map_apply_kernel instances (0: the compiler's choice).  The
 // A <= 64 instance asks for 7 (map_apply.hip).  Round 1 blamed a miscompute of a forced-7 build

@@ -21,6 +21,11 @@
 
 namespace crdt {
 
+// waves per SIMD asked of the register allocator (build option; A/B in profiles/r05_vapply_wpe_ab.log)
+#ifndef CRDT_MCA_WPE
+#define CRDT_MCA_WPE 8
+#endif
+
 struct MapCounterApplyPlan {
   u64 *clock, *ec, *val;
   unsigned long long c_s, e_s, v_s;  // state strides (words)
@@ -43,7 +48,7 @@ struct MapCounterApplyPlan {
 };
 
 template <int APL>
-__global__ __launch_bounds__(256) CRDT_VAPPLY_ATTR void map_counter_apply_kernel(MapCounterApplyPlan p) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CRDT_MCA_WPE))) void map_counter_apply_kernel(MapCounterApplyPlan p) {
   extern __shared__ u64 lds[];
   const int lane = (int)(threadIdx.x % kWave), wv = (int)(threadIdx.x / kWave);
   const unsigned long long s = (unsigned long long)blockIdx.x * p.wpb + wv;

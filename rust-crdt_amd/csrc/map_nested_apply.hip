@@ -334,7 +334,7 @@ __device__ __forceinline__ NaKey<APL> na_key(const NestedApplyPlan &p, unsigned 
 }
 
 template <int APL>
-__global__ __launch_bounds__(256) CRDT_VAPPLY_ATTR void map_nested_apply_kernel(NestedApplyPlan p) {
+__global__ __launch_bounds__(256) void map_nested_apply_kernel(NestedApplyPlan p) {
   extern __shared__ u64 lds[];
   const int lane = (int)(threadIdx.x % kWave), wv = (int)(threadIdx.x / kWave);
   const unsigned long long s = (unsigned long long)blockIdx.x * p.wpb + wv;

@@ -15,6 +15,11 @@
 
 namespace crdt {
 
+// waves per SIMD asked of the register allocator (build option; A/B in profiles/r05_vapply_wpe_ab.log)
+#ifndef CRDT_MOA_WPE
+#define CRDT_MOA_WPE 6
+#endif
+
 constexpr int kMoaVd = 16;    // nested deferred slots per key (crdt_map_orswot_out)
 constexpr int kMoaMw = 16;    // member-mask words (M <= 1,024)
 
@@ -42,7 +47,7 @@ struct MapOrswotApplyPlan {
 };
 
 template <int APL>
-__global__ __launch_bounds__(256) CRDT_VAPPLY_ATTR void map_orswot_apply_kernel(MapOrswotApplyPlan p) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CRDT_MOA_WPE))) void map_orswot_apply_kernel(MapOrswotApplyPlan p) {
   extern __shared__ u64 lds[];
   const int lane = (int)(threadIdx.x % kWave), wv = (int)(threadIdx.x / kWave);
   const unsigned long long s = (unsigned long long)blockIdx.x * p.wpb + wv;
