@@ -493,7 +493,10 @@ __device__ void gkey_rm(const MapApplyPlan &p, unsigned long long s, unsigned lo
 // all 0 <=> key absent, whose value rows are all 0 by the layout) writes its value to slot 0
 // without reading the value rows: ~90% of the Ups at the apply benchmark's shape.
 template <int KJ, bool PF>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KJ <= 2 ? 4 : 1))) void map_apply_grp_kernel(MapApplyPlan p) {
+#ifndef CRDT_MAPGRP_WPE
+#define CRDT_MAPGRP_WPE 4  // waves per SIMD of the KJ <= 2 instances (build option)
+#endif
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KJ <= 2 ? CRDT_MAPGRP_WPE : 1))) void map_apply_grp_kernel(MapApplyPlan p) {
   extern __shared__ u64 lds[];
   constexpr int kG = grp::kG;
   constexpr int kVB = 4;  // value rows of an Up loaded in one batch
