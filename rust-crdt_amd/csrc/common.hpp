@@ -111,6 +111,7 @@ struct Tune {
                                //     takes as long as its slowest key, and on the config-4 generator's replicas
                                //     some keys change in most chunks, profiles/r05_map_orswot_chunk_ab.log)
   int map_orswot_wide = 0;     // Map<K, Orswot> fold: the wide kernel at every shape (it is used past A = 64 / M = 32)
+  int map_nested_lds = 1;      // Map<K, Map<K2, MVReg>> fold: inner state in LDS + staged replica rows, where they fit
   int map_apply_pf = 1;        // Map apply (16-lane groups): the next op's entry-clock row prefetched with its
                                //     Put / rm clock; absent keys skip their value rows (0: round-3 form;
                                //     1.28 vs 1.81 ms, profiles/r04_map_apply_pf_ab.log)

@@ -240,6 +240,7 @@ static void apply_tune(crdt_ctx *ctx, const char *t) {
       else if (k == "mccl") ctx->tune.map_counter_cl = v ? 1 : 0;
       else if (k == "mocs") ctx->tune.map_orswot_cs = v ? 1 : 0;
       else if (k == "mowide") ctx->tune.map_orswot_wide = v ? 1 : 0;
+      else if (k == "nmlds") ctx->tune.map_nested_lds = v ? 1 : 0;
       else if (k == "mcdma") ctx->tune.map_counter_dma = v >= 16 ? 16 : (v > 0 ? 8 : 0);
       else if (k == "mapf") ctx->tune.map_apply_pf = v != 0;
       else if (k == "rbpc" && v > 0) ctx->tune.rows_blocks_per_cu = v;

@@ -49,6 +49,10 @@ struct NestedMapPlan {
   unsigned *o_nval, *o_id_n;
   u64 *o_id_clock, *o_id_keys;
   unsigned *o_flags;
+  // u64 words of LDS per wave for the key's inner Map state (iec [K2][A], slots [K2][8][A], values
+  // [K2][8]) and for a staged copy of the replica's inner Map (iec, slots, values); 0 = off (the state
+  // then lives in the key's output rows, the replica is read from HBM where it is used)
+  unsigned long long xs_state, xs_stage;
 };
 
 __device__ __forceinline__ bool nm_nz(u64 x) { return __ballot(x != 0) != 0; }
@@ -65,7 +69,8 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
   if (gk >= p.G * p.K) return;  // (whole waves; nothing below synchronises the workgroup)
   const unsigned long long g = gk / p.K, k = gk % p.K, A = p.A, R = p.R, K = p.K, K2 = p.K2, V = p.V;
   constexpr unsigned long long WQ = kNmList + kNmLive / 2 + kNmRows * kWave + kNmId * kWave + kNmId + kNmK2 / 8;
-  u64 *lst = lds + (unsigned long long)wv * WQ;
+  u64 *lst = lds + (unsigned long long)wv * (WQ + p.xs_state + p.xs_stage);
+  u64 *const xst = lst + WQ, *const xsg = xst + p.xs_state;  // (LDS state, staged replica)
   uint32_t *live = reinterpret_cast<uint32_t *>(lst + kNmList);
   u64 *rows = lst + kNmList + kNmLive / 2;  // [kNmRows][64] live outer-remove rows
   u64 *drow = rows + kNmRows * kWave;       // [kNmId][64] inner deferred rm rows
@@ -134,9 +139,10 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
   // ---- the key's state: outer C, e; the inner Map's clock ic (registers), rows in the output
   u64 C = 0, e = 0, ic = 0;
   int nd = 0;  // inner deferred removes held (uniform)
-  u64 *const iec_o = p.o_iec + gk * K2 * A;
-  u64 *const ivc_o = p.o_ivc + gk * K2 * kNmVs * A;
-  u64 *const ivv_o = p.o_ivv + gk * K2 * kNmVs;
+  // (generic pointers: the LDS copy when it fits, else the key's own output rows)
+  u64 *const iec_o = p.xs_state ? xst : p.o_iec + gk * K2 * A;
+  u64 *const ivc_o = p.xs_state ? xst + K2 * A : p.o_ivc + gk * K2 * kNmVs * A;
+  u64 *const ivv_o = p.xs_state ? xst + K2 * A + K2 * kNmVs * A : p.o_ivv + gk * K2 * kNmVs;
   for (unsigned long long j = 0; j < K2; ++j) {
     st(iec_o + j * A, 0);
     if (lane == 0) nv[j] = 0;
@@ -227,6 +233,21 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
   auto rin_iec = [&](unsigned long long r) { return p.iec + ((g * R + r) * K + k) * K2 * A; };
   auto rin_ivc = [&](unsigned long long r) { return p.ivc + ((g * R + r) * K + k) * K2 * V * A; };
   auto rin_ivv = [&](unsigned long long r) { return p.ivv + ((g * R + r) * K + k) * K2 * V; };
+  // replica r's inner rows (iec, slots, values: three contiguous blocks) copied to LDS with every
+  // load in flight at once; returns the three (generic) base pointers
+  struct Rin {
+    const u64 *iec, *ivc, *ivv;
+  };
+  auto rin = [&](unsigned long long r) -> Rin {
+    if (!p.xs_stage) return Rin{rin_iec(r), rin_ivc(r), rin_ivv(r)};
+    const unsigned long long n1 = K2 * A, n2 = K2 * V * A, n3 = K2 * V;
+    const u64 *s1 = rin_iec(r), *s2 = rin_ivc(r), *s3 = rin_ivv(r);
+#pragma unroll 4
+    for (unsigned long long i = (unsigned long long)lane; i < n1 + n2 + n3; i += kWave)
+      xsg[i] = i < n1 ? s1[i] : (i < n1 + n2 ? s2[i - n1] : s3[i - n1 - n2]);
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");  // (other lanes read these words)
+    return Rin{xsg, xsg + n1, xsg + n1 + n2};
+  };
   auto rin_id = [&](unsigned long long r, u64 &lo, u64 &hi) {
     const u64 *po = p.id_off + (g * R + r) * K + k;
     u64 a = __builtin_amdgcn_readfirstlane((unsigned)po[0]) | ((u64)__builtin_amdgcn_readfirstlane((unsigned)(po[0] >> 32)) << 32);
@@ -239,7 +260,8 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
   // the replica's inner Map as the key's value (map.rs:193-208): clock, entries, slots, deferred
   auto inner_load = [&](unsigned long long r, u64 ic2) {
     ic = ic2;
-    const u64 *ri = rin_iec(r), *rc = rin_ivc(r), *rv = rin_ivv(r);
+    const Rin rn = rin(r);
+    const u64 *ri = rn.iec, *rc = rn.ivc, *rv = rn.ivv;
     for (unsigned long long j = 0; j < K2; ++j) {
       const u64 ej = ld(ri + j * A);
       st(iec_o + j * A, ej);
@@ -267,7 +289,8 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
 
   // the inner Map::merge (map.rs:140-220) of replica r's inner Map (clock ic2) into the state
   auto inner_merge = [&](unsigned long long r, u64 ic2) {
-    const u64 *ri = rin_iec(r), *rc = rin_ivc(r), *rv = rin_ivv(r);
+    const Rin rn = rin(r);
+    const u64 *ri = rn.iec, *rc = rn.ivc, *rv = rn.ivv;
     for (unsigned long long j = 0; j < K2; ++j) {
       const u64 ej = ld(iec_o + j * A), e2j = ld(ri + j * A);
       const bool q1 = nm_nz(ej), q2 = nm_nz(e2j);
@@ -282,9 +305,12 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
       }
       const u64 xj = nm_fg(q1 ? (q2 ? nm_max(ej, e2j) : ic2) : ic, enj);
       // the slots: ours (Vec order), then the replica's (MVReg::merge, mvreg.rs:112-128), forgotten by xj
+      // (every register array is indexed by unrolled constants only: the replica's slots keep their
+      // own positions with a validity mask m2 instead of being compacted by a running count, which
+      // made the compiler spill the arrays to scratch)
       u64 cs[kNmVs], co[kNmVin], vs[kNmVs], vo[kNmVin];
       const int n1 = q1 ? __builtin_amdgcn_readfirstlane((int)nv[j]) : 0;
-      int n2 = 0;
+      unsigned m2 = 0;
 #pragma unroll
       for (int s = 0; s < kNmVs; ++s) {
         cs[s] = s < n1 ? ld(ivc_o + (j * kNmVs + s) * A) : 0;
@@ -301,9 +327,9 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
           if ((unsigned long long)s < V) {
             const u64 c = ld(rc + (j * V + s) * A);
             if (nm_nz(c)) {  // (an empty slot is no value)
-              co[n2 < kNmVin ? n2 : kNmVin - 1] = c;
-              vo[n2 < kNmVin ? n2 : kNmVin - 1] = rv[j * V + s];
-              ++n2;
+              co[s] = c;
+              vo[s] = rv[j * V + s];
+              m2 |= 1u << s;
             }
           }
         }
@@ -316,17 +342,22 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
         if (s >= n1) break;
         bool dominated = false;
 #pragma unroll
-        for (int t = 0; t < kNmVin; ++t)
-          if (t < n2 && nm_lt(cs[s], co[t])) dominated = true;
+        for (int t = 0; t < kNmVin; ++t) {
+          if (!(m2 >> t) || dominated) break;  // (uniform exits: the unrolled pairs past the values cost nothing)
+          if (((m2 >> t) & 1u) && nm_lt(cs[s], co[t])) dominated = true;
+        }
         if (!dominated) keep1 |= 1u << s;
       }
 #pragma unroll
       for (int t = 0; t < kNmVin; ++t) {
-        if (t >= n2) break;
+        if (!(m2 >> t)) break;
+        if (!((m2 >> t) & 1u)) continue;
         bool drop = false;
 #pragma unroll
-        for (int s = 0; s < kNmVs; ++s)
+        for (int s = 0; s < kNmVs; ++s) {
+          if (s >= n1 || drop) break;
           if (((keep1 >> s) & 1u) && (nm_lt(co[t], cs[s]) || nm_eq(co[t], cs[s]))) drop = true;
+        }
         if (!drop) keep2 |= 1u << t;
       }
       // write the merged slots forgotten by xj, in order
@@ -474,12 +505,16 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
   const bool pf = nm_nz(e);
   st(p.o_ec + gk * A, e);
   st(p.o_ic + gk * A, pf ? ic : 0ull);
+  u64 *const oiec = p.o_iec + gk * K2 * A, *const oivc = p.o_ivc + gk * K2 * kNmVs * A;
+  u64 *const oivv = p.o_ivv + gk * K2 * kNmVs;
   for (unsigned long long j = 0; j < K2; ++j) {
     const int n = pf ? __builtin_amdgcn_readfirstlane((int)nv[j]) : 0;
-    if (!pf) st(iec_o + j * A, 0);
-    for (int s = n; s < kNmVs; ++s) {  // (unused slots zero)
-      st(ivc_o + (j * kNmVs + s) * A, 0);
-      ivv_o[j * kNmVs + s] = 0;
+    st(oiec + j * A, pf ? ld(iec_o + j * A) : 0ull);  // (the same word when the state is the output)
+    for (int s = 0; s < kNmVs; ++s) {  // the held slots, then zeros
+      const u64 c = s < n ? ld(ivc_o + (j * kNmVs + s) * A) : 0ull;
+      const u64 v = s < n ? ivv_o[j * kNmVs + s] : 0ull;
+      st(oivc + (j * kNmVs + s) * A, c);
+      oivv[j * kNmVs + s] = v;
     }
     if (lane == 0) p.o_nval[gk * K2 + j] = (unsigned)n;
   }
@@ -575,9 +610,30 @@ extern "C" int crdt_map_nested_lub_many(crdt_ctx *ctx, const crdt_map_nested_bat
                          (unsigned long long)R * K, (unsigned long long)G, (unsigned long long)in->Di, out->flags);
       CRDT_HIP(ctx, hipGetLastError());
     }
+    // LDS per wave beyond the fixed lists: the inner state, then the staged replica rows, while the
+    // block fits (up to 160 KiB when one block per CU already gives every key a SIMD of its own,
+    // else 80 KiB so that two blocks share a CU as without them)
+    p.xs_state = p.xs_stage = 0;
+    size_t lds = nm_lds();
+    if (ctx->tune.map_nested_lds && K2 > 0) {
+      const size_t base = nm_lds() / kNmWaves, cap = G * K <= 4 * (size_t)ctx->cu_count ? 160 * 1024 : 80 * 1024;
+      const size_t st_w = K2 * (1 + kNmVs) * A + K2 * kNmVs, sg_w = K2 * (1 + V) * A + K2 * V;
+      if ((base + st_w * 8) * kNmWaves <= cap) p.xs_state = st_w;
+      if ((base + (p.xs_state + sg_w) * 8) * kNmWaves <= cap) p.xs_stage = sg_w;
+      lds = (base + (p.xs_state + p.xs_stage) * 8) * kNmWaves;
+      if (lds > 64 * 1024) {
+        const hipError_t ae = hipFuncSetAttribute(reinterpret_cast<const void *>(&map_nested_fold_kernel),
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (ae != hipSuccess) {
+          (void)hipGetLastError();
+          p.xs_state = p.xs_stage = 0;
+          lds = nm_lds();
+        }
+      }
+    }
     timing_begin(ctx, "map_nested_fold");
     const unsigned long long blocks = (G * K + kNmWaves - 1) / kNmWaves;
-    hipLaunchKernelGGL(map_nested_fold_kernel, dim3((unsigned)blocks), dim3(kNmWaves * kWave), nm_lds(), ctx->stream, p);
+    hipLaunchKernelGGL(map_nested_fold_kernel, dim3((unsigned)blocks), dim3(kNmWaves * kWave), lds, ctx->stream, p);
     const hipError_t he = hipGetLastError();
     timing_end(ctx);
     if (he != hipSuccess) return hip_fail(ctx, he, "map_nested_fold_kernel launch");

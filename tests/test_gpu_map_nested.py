@@ -456,12 +456,19 @@ def test_prop_map_merge_laws_on_gpu(gm, seed):
 
 
 # ---- op-replay folds over many replicas against the oracle's left fold -------------------------------
+@pytest.mark.parametrize("mode", ["", "nmlds=0"])
 @pytest.mark.parametrize("seed,R,K,K2,A", [(1, 30, 3, 4, 4), (2, 50, 5, 6, 5), (3, 40, 2, 3, 3),
                                             (4, 70, 6, 8, 6), (5, 25, 4, 20, 8), (6, 40, 3, 64, 64)])
-def test_map_nested_op_replay_fold(gpu_ctx, seed, R, K, K2, A):
-    maps = O.nested_map_objects(R, K, K2, A, seed=seed, steps=8 * R)
-    exp = O.map_fold_objects(maps)
-    got = gpu_fold(gpu_ctx, maps)
+def test_map_nested_op_replay_fold(gpu_ctx, seed, R, K, K2, A, mode):
+    """Both state placements: the key's inner Map and the staged replica rows in LDS (default, where
+    they fit; at K2 = 64, A = 64 they do not) and the inner Map in the key's output rows."""
+    gpu_ctx.tune(mode)
+    try:
+        maps = O.nested_map_objects(R, K, K2, A, seed=seed, steps=8 * R)
+        exp = O.map_fold_objects(maps)
+        got = gpu_fold(gpu_ctx, maps)
+    finally:
+        gpu_ctx.tune("nmlds=1")  # (tune specs are additive: restore the default)
     assert canon(got) == canon(exp)
 
 
