@@ -21,7 +21,8 @@
 
 namespace crdt {
 
-// waves per SIMD asked of the register allocator (build option; A/B in profiles/r05_vapply_wpe_ab.log)
+// waves per SIMD asked of the register allocator for A <= 128 (build option; A/B in
+// profiles/r05_vapply_wpe_ab.log); the wider instances keep the compiler's choice (they would spill)
 #ifndef CRDT_MCA_WPE
 #define CRDT_MCA_WPE 8
 #endif
@@ -48,7 +49,7 @@ struct MapCounterApplyPlan {
 };
 
 template <int APL>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CRDT_MCA_WPE))) void map_counter_apply_kernel(MapCounterApplyPlan p) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APL <= 2 ? CRDT_MCA_WPE : 1))) void map_counter_apply_kernel(MapCounterApplyPlan p) {
   extern __shared__ u64 lds[];
   const int lane = (int)(threadIdx.x % kWave), wv = (int)(threadIdx.x / kWave);
   const unsigned long long s = (unsigned long long)blockIdx.x * p.wpb + wv;

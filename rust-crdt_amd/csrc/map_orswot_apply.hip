@@ -15,7 +15,8 @@
 
 namespace crdt {
 
-// waves per SIMD asked of the register allocator (build option; A/B in profiles/r05_vapply_wpe_ab.log)
+// waves per SIMD asked of the register allocator for A <= 128 (build option; A/B in
+// profiles/r05_vapply_wpe_ab.log); the wider instances keep the compiler's choice (they would spill)
 #ifndef CRDT_MOA_WPE
 #define CRDT_MOA_WPE 6
 #endif
@@ -47,7 +48,7 @@ struct MapOrswotApplyPlan {
 };
 
 template <int APL>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CRDT_MOA_WPE))) void map_orswot_apply_kernel(MapOrswotApplyPlan p) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APL <= 2 ? CRDT_MOA_WPE : 1))) void map_orswot_apply_kernel(MapOrswotApplyPlan p) {
   extern __shared__ u64 lds[];
   const int lane = (int)(threadIdx.x % kWave), wv = (int)(threadIdx.x / kWave);
   const unsigned long long s = (unsigned long long)blockIdx.x * p.wpb + wv;
