@@ -981,9 +981,12 @@ int crdt_mvreg_apply_batch(crdt_ctx *ctx, const crdt_mvreg_states *states, const
  *   CRDT_PAIR_FORGET  out_i = x_i.forget(y_i): keep x[a] iff x[a] > y[a]         vclock.rs:95-105
  *                     (GCounter::forget gcounter.rs:51-53, PNCounter::forget pncounter.rs:78-81
  *                     are the same op on their rows)
+ *   CRDT_PAIR_INTERSECTION  out_i = VClock::intersection(x_i, y_i): keep x[a] iff
+ *                     y[a] == x[a] (the common dots)                            vclock.rs:218-227
  * `out` may alias `x` (in place, like the reference's &mut self). */
 #define CRDT_PAIR_GLB 1
 #define CRDT_PAIR_FORGET 2
+#define CRDT_PAIR_INTERSECTION 3
 int crdt_vclock_pair_op(crdt_ctx *ctx, int op, uint64_t *out, const uint64_t *x, const uint64_t *y,
                         size_t N, size_t A, size_t out_stride, size_t x_stride, size_t y_stride);
 

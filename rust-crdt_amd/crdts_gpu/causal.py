@@ -3,8 +3,11 @@
     glb(x, y)            VClock::glb           (vclock.rs:246-259) per row pair: pointwise min
     forget(x, y)         Causal::forget        (vclock.rs:95-105; GCounter gcounter.rs:51-53,
                                                 PNCounter pncounter.rs:78-81): keep x iff x > y
+    intersection(x, y)   VClock::intersection  (vclock.rs:218-227) per row pair: keep x[a] iff
+                                                y[a] == x[a]
     partial_cmp(x, y)    VClock::partial_cmp   (vclock.rs:68-80) per row pair, coded
                          EQUAL 0 / GREATER 1 / LESS -1 / CONCURRENT 2 (None)
+    concurrent(x, y)     VClock::concurrent    (vclock.rs:201-203): partial_cmp is None
     cmp_matrix(x)        partial_cmp of every pair of N clocks: (N, N) codes
 
 Rows are (N, A) int64/uint64 device tensors (actor interned to a column, absent = 0) or a single
@@ -19,7 +22,7 @@ import torch
 from .context import Context, dptr
 
 EQUAL, GREATER, LESS, CONCURRENT = 0, 1, -1, 2
-_GLB, _FORGET = 1, 2
+_GLB, _FORGET, _INTERSECTION = 1, 2, 3
 
 
 def _rows(t: torch.Tensor, what: str) -> torch.Tensor:
@@ -61,6 +64,11 @@ def forget(x: torch.Tensor, y: torch.Tensor, out: Optional[torch.Tensor] = None,
     return _pair_op(_FORGET, "causal.forget", x, y, out, ctx)
 
 
+def intersection(x: torch.Tensor, y: torch.Tensor, out: Optional[torch.Tensor] = None,
+                 ctx: Optional[Context] = None) -> torch.Tensor:
+    return _pair_op(_INTERSECTION, "causal.intersection", x, y, out, ctx)
+
+
 def partial_cmp(x: torch.Tensor, y: torch.Tensor, ctx: Optional[Context] = None) -> torch.Tensor:
     ctx = ctx or Context.default(x.device.index)
     ctx.check_tensor(x, "causal.partial_cmp(x)")
@@ -72,6 +80,10 @@ def partial_cmp(x: torch.Tensor, y: torch.Tensor, ctx: Optional[Context] = None)
     out = torch.empty(N, dtype=torch.int8, device=x.device)
     ctx.call("crdt_vclock_partial_cmp", dptr(x2), dptr(y2), N, A, x2.stride(0), y2.stride(0), dptr(out))
     return out[0] if x.dim() == 1 else out
+
+
+def concurrent(x: torch.Tensor, y: torch.Tensor, ctx: Optional[Context] = None) -> torch.Tensor:
+    return partial_cmp(x, y, ctx) == CONCURRENT
 
 
 def cmp_matrix(x: torch.Tensor, ctx: Optional[Context] = None) -> torch.Tensor:

@@ -19,15 +19,18 @@ struct PairPlan {
   u64 *out;
   const u64 *x, *y;
   unsigned long long N, A, os, xs, ys;
-  int op;  // CRDT_PAIR_GLB / CRDT_PAIR_FORGET
+  int op;  // CRDT_PAIR_GLB / CRDT_PAIR_FORGET / CRDT_PAIR_INTERSECTION
   int vec2;
   int lr_log;  // log2(LR)
 };
 
 __device__ __forceinline__ u64 pair_apply(int op, u64 a, u64 b) {
   // glb: min (vclock.rs:246-259); forget: keep a iff a > b (vclock.rs:98-104: counter >= own
-  // removes the actor)
-  return op == CRDT_PAIR_GLB ? (a < b ? a : b) : (a > b ? a : 0);
+  // removes the actor); intersection: keep a iff b holds the same counter (vclock.rs:218-227; an
+  // absent actor is 0 on both sides, so it stays absent)
+  if (op == CRDT_PAIR_GLB) return a < b ? a : b;
+  if (op == CRDT_PAIR_FORGET) return a > b ? a : 0;
+  return a == b ? a : 0;
 }
 
 __global__ __launch_bounds__(kBlock) void pair_op_kernel(PairPlan p) {
@@ -236,7 +239,7 @@ extern "C" int crdt_vclock_pair_op(crdt_ctx *ctx, int op, uint64_t *out, const u
                                    size_t N, size_t A, size_t out_stride, size_t x_stride, size_t y_stride) {
   CRDT_DEVICE_MEM_ONLY(ctx);
   CRDT_CHECK_CTX(ctx);
-  if (op != CRDT_PAIR_GLB && op != CRDT_PAIR_FORGET) return fail(ctx, CRDT_EINVAL, "vclock_pair_op: op %d", op);
+  if (op != CRDT_PAIR_GLB && op != CRDT_PAIR_FORGET && op != CRDT_PAIR_INTERSECTION) return fail(ctx, CRDT_EINVAL, "vclock_pair_op: op %d", op);
   if (N == 0 || A == 0) return CRDT_OK;
   if (!out || !x || !y) return fail(ctx, CRDT_EINVAL, "vclock_pair_op: NULL buffer");
   if (N > 1 && (out_stride < A || x_stride < A || y_stride < A)) return fail(ctx, CRDT_EINVAL, "vclock_pair_op: stride < A");

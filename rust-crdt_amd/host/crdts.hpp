@@ -286,6 +286,14 @@ template <class A>
 void forget_batch(Gpu &gpu, std::vector<VClock<A>> &selves, const std::vector<VClock<A>> &others) {
   detail::pair_op(gpu, CRDT_PAIR_FORGET, selves, others);
 }
+// VClock::intersection(&lefts[i], &rights[i]): the common dots   (vclock.rs:218-227)
+template <class A>
+std::vector<VClock<A>> intersection_batch(Gpu &gpu, const std::vector<VClock<A>> &lefts,
+                                          const std::vector<VClock<A>> &rights) {
+  std::vector<VClock<A>> out(lefts);
+  detail::pair_op(gpu, CRDT_PAIR_INTERSECTION, out, rights);
+  return out;
+}
 // xs[i].partial_cmp(&ys[i])               (vclock.rs:68-80; nullopt = concurrent)
 template <class A>
 std::vector<std::optional<Ordering>> partial_cmp_batch(Gpu &gpu, const std::vector<VClock<A>> &xs,

@@ -141,6 +141,15 @@ static void test_causal_batches_gpu(Gpu &g) {  // GPU vs host on random clocks
   bool ok = cmp.size() == xs.size();
   for (size_t i = 0; ok && i < xs.size(); ++i) ok = cmp[i] == xs[i].partial_cmp(ys[i]);
   CHECK(ok);
+  auto in = intersection_batch(g, xs, ys);  // vclock.rs:218-227, restated on the host
+  ok = in.size() == xs.size();
+  for (size_t i = 0; ok && i < xs.size(); ++i) {
+    VClock<uint32_t> e;
+    for (auto &kv : xs[i].dots)
+      if (ys[i].get(kv.first) == kv.second) e.dots[kv.first] = kv.second;
+    ok = in[i] == e;
+  }
+  CHECK(ok);
   auto m = cmp_matrix(g, xs);
   ok = m.size() == xs.size() * xs.size();
   for (size_t i = 0; ok && i < xs.size(); i += 7)

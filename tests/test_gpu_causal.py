@@ -49,7 +49,9 @@ def test_glb_forget_cmp(gpu_ctx, N, A, cmax):
     x, y = _pairs(rng, N, A, cmax)
     dx, dy = to_dev(x), to_dev(y)
     glb, fgt = to_host(cg.causal.glb(dx, dy)), to_host(cg.causal.forget(dx, dy))
+    inter = to_host(cg.causal.intersection(dx, dy))
     cmpv = cg.causal.partial_cmp(dx, dy).cpu().numpy()
+    conc = cg.causal.concurrent(dx, dy).cpu().numpy()
     for i in range(N):
         a, b = _vc(x[i]), _vc(y[i])
         g = a.copy()
@@ -58,7 +60,9 @@ def test_glb_forget_cmp(gpu_ctx, N, A, cmax):
         f.forget(b)
         assert np.array_equal(glb[i], _dense(g, A)), i
         assert np.array_equal(fgt[i], _dense(f, A)), i
+        assert np.array_equal(inter[i], _dense(O.VClock.intersection(a, b), A)), i
         assert cmpv[i] == CODE[a.partial_cmp(b)], i
+        assert bool(conc[i]) == (a.partial_cmp(b) is O.NONE), i
     assert set(cmpv.tolist()) >= ({0, 1, -1, 2} if N > 100 else set())
 
 
@@ -113,3 +117,71 @@ def test_counter_read(gpu_ctx, N, A, full):
 
 def got_single(row):
     return sum(int(x) for x in row)
+
+
+def test_vclock_module_api(gpu_ctx):
+    """crdts_gpu.vclock mirrors src/vclock.rs's batch-able surface: each call against the oracle's
+    VClock methods on the same rows (vclock.rs:68-80, :95-105, :125-159, :148-152, :201-259)."""
+    rng = np.random.default_rng(21)
+    x, y = _pairs(rng, 300, 24, 6)
+    dx, dy = to_dev(x), to_dev(y)
+    vc = cg.vclock
+    out = {"glb": to_host(vc.glb(dx, dy)), "forget": to_host(vc.forget(dx, dy)),
+           "clone_without": to_host(vc.clone_without(dx, dy)), "intersection": to_host(vc.intersection(dx, dy)),
+           "merge": to_host(vc.merge_batch(dx.clone(), dy))}
+    cmpv, conc = vc.partial_cmp(dx, dy).cpu().numpy(), vc.concurrent(dx, dy).cpu().numpy()
+    for i in range(300):
+        a, b = _vc(x[i]), _vc(y[i])
+        g = a.copy()
+        g.glb(b)
+        m = a.copy()
+        m.merge(b)
+        assert np.array_equal(out["glb"][i], _dense(g, 24))
+        assert np.array_equal(out["forget"][i], _dense(a.clone_without(b), 24))
+        assert np.array_equal(out["clone_without"][i], _dense(a.clone_without(b), 24))
+        assert np.array_equal(out["intersection"][i], _dense(O.VClock.intersection(a, b), 24))
+        assert np.array_equal(out["merge"][i], _dense(m, 24))
+        assert cmpv[i] == CODE[a.partial_cmp(b)] and bool(conc[i]) == a.concurrent(b)
+    assert np.array_equal(to_host(dx), x)  # forget / glb / intersection without out= leave x alone
+    # CmRDT::apply of Dot ops in stream order, and the fold
+    st = to_dev(x[:50].copy())
+    n = 2000
+    idx, act = rng.integers(0, 50, n), rng.integers(0, 24, n)
+    ctr = rng.integers(0, 9, n).astype(np.uint64)
+    assert vc.apply(st, torch.from_numpy(idx.astype(np.int32)).cuda(), torch.from_numpy(act.astype(np.int32)).cuda(),
+                    to_dev(ctr)) == 0
+    exp = [_vc(x[i]) for i in range(50)]
+    for i, a, c in zip(idx, act, ctr):
+        exp[i].apply(O.Dot(int(a), int(c)))
+    assert all(np.array_equal(to_host(st)[i], _dense(exp[i], 24)) for i in range(50))
+    acc = O.VClock()
+    for i in range(300):
+        acc.merge(_vc(x[i]))
+    assert np.array_equal(to_host(vc.lub_many(dx)), _dense(acc, 24))
+    assert np.array_equal(vc.cmp_matrix(dx[:40]).cpu().numpy(), cg.causal.cmp_matrix(dx[:40]).cpu().numpy())
+
+
+def test_gset_module_api(gpu_ctx):
+    """crdts_gpu.gset: insert ops (gset.rs:46-48, :69-71), contains (:83-85), read (:103-105) and
+    the fold (:38-40) against the oracle's GSet on the same interned elements."""
+    rng = np.random.default_rng(22)
+    N, U = 40, 200
+    W = (U + 63) // 64
+    st = torch.zeros((N, W), dtype=torch.int64, device="cuda")
+    n = 3000
+    idx, el = rng.integers(0, N, n), rng.integers(0, U, n)
+    assert cg.gset.apply(st, torch.from_numpy(idx.astype(np.int32)).cuda(),
+                         torch.from_numpy(el.astype(np.int32)).cuda(), U) == 0
+    exp = [O.GSet() for _ in range(N)]
+    for i, e in zip(idx, el):
+        exp[i].insert(int(e))
+    vals = torch.arange(U, dtype=torch.int64) * 7 + 3  # interning dictionary: position -> value
+    assert cg.gset.read(st) == [sorted(e.value) for e in exp]
+    assert cg.gset.read(st, vals) == [[7 * p + 3 for p in sorted(e.value)] for e in exp]
+    probe = torch.from_numpy(rng.integers(-5, U + 70, N)).cuda()
+    got = cg.gset.contains(st, probe).cpu().numpy()
+    assert [bool(g) for g in got] == [exp[i].contains(int(p)) for i, p in enumerate(probe.tolist())]
+    acc = O.GSet()
+    for e in exp:
+        acc.merge(e)
+    assert cg.gset.read(cg.gset.lub_many(st).unsqueeze(0)) == [sorted(acc.value)]
