@@ -99,6 +99,9 @@ struct Tune {
                                //     (opt-in: 4 VGPRs spill, 990 vs 918 us, profiles/r04_orswot_apply_pf_ab.log)
   int orswot_apply_stg = 0;    // Orswot apply (16-lane groups): a batch's first 2 Rm clock rows staged in LDS by LDS-DMA
                                //     (opt-in: 872 vs 854 us, profiles/r05_oapply_stg_ab.log)
+  int orswot_apply_l2pf = 0;   // Orswot apply (16-lane groups): a one-member Rm's entry row touched with the batch header
+                               // (lines pulled toward L2 while the header's other loads are in flight; CRDT_TUNE oal2=1)
+  int orswot_apply_meta = 1;   // Orswot apply (16-lane groups): per-slot member blooms in LDS (oameta)
   int orswot_apply_hpf = 0;    // Orswot apply (16-lane groups): the next op batch's fields / first members loaded
                                //     while the current batch runs (opt-in: 2 VGPRs spill, 878 vs 856 us, profiles/r04_oapply_hpf_ab.log)
   int map_counter_dma = 0;     // Map<K, counter> fold: LDS-DMA ring slots (8 or 16; 0: register ring, 8.7 vs 9.1 ms)
@@ -112,6 +115,7 @@ struct Tune {
                                //     some keys change in most chunks, profiles/r05_map_orswot_chunk_ab.log)
   int map_orswot_wide = 0;     // Map<K, Orswot> fold: the wide kernel at every shape (it is used past A = 64 / M = 32)
   int map_nested_lds = 1;      // Map<K, Map<K2, MVReg>> fold: inner state in LDS + staged replica rows, where they fit
+  int map_apply_meta = 1;      // Map apply (16-lane groups, with mapf): per-slot key blooms in LDS (mameta)
   int map_apply_pf = 1;        // Map apply (16-lane groups): the next op's entry-clock row prefetched with its
                                //     Put / rm clock; absent keys skip their value rows (0: round-3 form;
                                //     1.28 vs 1.81 ms, profiles/r04_map_apply_pf_ab.log)

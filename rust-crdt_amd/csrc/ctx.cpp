@@ -232,6 +232,8 @@ static void apply_tune(crdt_ctx *ctx, const char *t) {
       else if (k == "mpnt") ctx->tune.map_pair_nt = v != 0;
       else if (k == "mppf") ctx->tune.map_pair_pf = v != 0;
       else if (k == "ohpf") ctx->tune.orswot_apply_hpf = v != 0;
+      else if (k == "oal2") ctx->tune.orswot_apply_l2pf = v != 0;
+      else if (k == "oameta") ctx->tune.orswot_apply_meta = v != 0;
       else if (k == "oastg") ctx->tune.orswot_apply_stg = v != 0;
       else if (k == "oapf") ctx->tune.orswot_apply_pf = v != 0;
       else if (k == "mcdep") ctx->tune.map_counter_depth = v >= 16 ? 16 : (v <= 4 ? 4 : 8);
@@ -243,6 +245,7 @@ static void apply_tune(crdt_ctx *ctx, const char *t) {
       else if (k == "nmlds") ctx->tune.map_nested_lds = v ? 1 : 0;
       else if (k == "mcdma") ctx->tune.map_counter_dma = v >= 16 ? 16 : (v > 0 ? 8 : 0);
       else if (k == "mapf") ctx->tune.map_apply_pf = v != 0;
+      else if (k == "mameta") ctx->tune.map_apply_meta = v != 0;
       else if (k == "rbpc" && v > 0) ctx->tune.rows_blocks_per_cu = v;
       else if (k == "hot" && v >= 0 && v <= 64) ctx->tune.apply_hot_slots = v;
       else if (k == "mhot" && v >= 0) ctx->tune.map_apply_hot = v;

@@ -492,7 +492,12 @@ __device__ void gkey_rm(const MapApplyPlan &p, unsigned long long s, unsigned lo
 // of an Up is updated from that row (no dependent read), and an Up of an absent key (entry clock
 // all 0 <=> key absent, whose value rows are all 0 by the layout) writes its value to slot 0
 // without reading the value rows: ~90% of the Ups at the apply benchmark's shape.
-template <int KJ, bool PF>
+// MT (round 5, default with PF while Dcap <= kMapMetaSlots): per slot, next to its witness byte, the
+// OR of the slot's key-bitmap words in LDS — the bloom is rebuilt from LDS alone after a slot is
+// dropped, and an Up's re-forget tests a slot's LDS word before reading its key word (as the Orswot
+// kernel's MT, orswot_apply.hip).
+constexpr unsigned long long kMapMetaSlots = 64;
+template <int KJ, bool PF, bool MT = false>
 #ifndef CRDT_MAPGRP_WPE
 #define CRDT_MAPGRP_WPE 4  // waves per SIMD of the KJ <= 2 instances (build option)
 #endif
@@ -508,6 +513,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KJ <= 2 
   // LDS: per group the op headers of the current batch (48 bytes each), then the slot witnesses
   u64 *hdr = lds + (threadIdx.x / kG) * (6 * kG);
   uint8_t *wit = reinterpret_cast<uint8_t *>(lds + (kBlock / kG) * 6 * kG) + (threadIdx.x / kG) * Dcap;
+  u64 *sbl = lds + (kBlock / kG) * 6 * kG + ((kBlock / kG) * Dcap + 7) / 8 + (threadIdx.x / kG) * Dcap;  // (MT)
 
   const unsigned long long ob = p.op_off[s], oe = p.op_off[s + 1];
   unsigned dcnt = p.def_count[s];
@@ -529,15 +535,23 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KJ <= 2 
     for (unsigned d = 0; d < dcnt; ++d) {
       const unsigned w = wit[d];
       if (w != grp::kNone) W |= 1ull << w;
-      for (unsigned long long x = g; x < Kw; x += kG) b |= DK[d * Kw + x];
+      if (MT) b |= sbl[d];
+      else
+        for (unsigned long long x = g; x < Kw; x += kG) b |= DK[d * Kw + x];
     }
-    bloom = grp::orx(b);
+    bloom = MT ? b : grp::orx(b);
   };
   for (unsigned d = 0; d < dcnt; ++d) {  // the input slots' witnesses at the input clock
     u64 x[KJ];
     grp::load_row<KJ>(x, DC + d * A, g, A);
     const unsigned w = grp::witness<KJ>(x, c, g, 0, A);
     if (lead) wit[d] = (uint8_t)w;
+    if (MT) {
+      u64 b = 0;
+      for (unsigned long long y = g; y < Kw; y += kG) b |= DK[d * Kw + y];
+      b = grp::orx(b);
+      if (lead) sbl[d] = b;
+    }
   }
   rebuild();
   bool full = true;  // no Up yet: the input slots' keys are re-forgotten in full at the first
@@ -551,6 +565,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KJ <= 2 
       }
       for (unsigned long long x = g; x < Kw; x += kG) DK[d * Kw + x] = DK[last * Kw + x];
       if (lead) wit[d] = wit[last];
+      if (MT && lead) sbl[d] = sbl[last];
     }
     dcnt = last;
   };
@@ -768,7 +783,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KJ <= 2 
         // key k re-forgotten by every slot naming it (only its rows changed)
         if (dcnt > 0 && ((bloom >> (k % 64)) & 1ull)) {
           for (unsigned d = 0; d < dcnt; ++d)
-            if ((DK[d * Kw + k / 64] >> (k % 64)) & 1ull) {
+            if ((!MT || ((sbl[d] >> (k % 64)) & 1ull)) && ((DK[d * Kw + k / 64] >> (k % 64)) & 1ull)) {
               u64 rm[KJ];
               grp::load_row<KJ>(rm, DC + d * A, g, A);
               gkey_rm<KJ>(p, s, k, rm, g, lane);
@@ -843,6 +858,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KJ <= 2 
           const unsigned long long wk = k1 < K ? k1 / 64 : ~0ull;
           for (unsigned long long x = g; x < Kw; x += kG) DK[slot * Kw + x] = x == wk ? 1ull << (k1 % 64) : 0ull;
           if (lead) wit[slot] = (uint8_t)wr;
+          if (MT && lead) sbl[slot] = k1 < K ? 1ull << (k1 % 64) : 0ull;
           W |= 1ull << wr;
           if (ke == kb + 1) {
             if (k1 < K) bloom |= 1ull << (k1 % 64);
@@ -853,6 +869,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KJ <= 2 
           const unsigned long long kk = PF && jk == kb ? kcur : p.keys[jk];
           if (kk >= K) continue;
           if (lead) DK[slot * Kw + kk / 64] |= 1ull << (kk % 64);
+          if (MT && lead) sbl[slot] |= 1ull << (kk % 64);
           bloom |= 1ull << (kk % 64);
         }
       }
@@ -907,18 +924,21 @@ extern "C" int crdt_map_apply_batch(crdt_ctx *ctx, const crdt_map_states *m, uin
     // 16 lanes per state: kBlock / 16 states per block (KJ = ceil(A / 16) clock words per lane)
     const size_t per_block = kBlock / grp::kG;
     const dim3 g2((unsigned)((N + per_block - 1) / per_block)), b2(kBlock);
-    const size_t lds2 = per_block * (6 * grp::kG * 8 + Dcap);
-    timing_begin(ctx, "map_apply");
     const bool pf = ctx->tune.map_apply_pf;
+    // MT: the slots' key blooms in LDS (with PF; CRDT_TUNE mameta=0: the round-4 form, HBM only)
+    const bool mt = pf && ctx->tune.map_apply_meta && Dcap <= kMapMetaSlots;
+    const size_t lds2 = per_block * 6 * grp::kG * 8 + (per_block * Dcap + 7) / 8 * 8 + (mt ? per_block * Dcap * 8 : 0);
+    timing_begin(ctx, "map_apply");
+    auto pick = [&](auto m, auto mf, auto nf) { return mt ? m : pf ? mf : nf; };
     if (A <= 16)
-      hipLaunchKernelGGL((pf ? map_apply_grp_kernel<1, true> : map_apply_grp_kernel<1, false>), g2, b2, lds2,
-                         ctx->stream, p);
+      hipLaunchKernelGGL(pick(map_apply_grp_kernel<1, true, true>, map_apply_grp_kernel<1, true, false>,
+                              map_apply_grp_kernel<1, false, false>), g2, b2, lds2, ctx->stream, p);
     else if (A <= 32)
-      hipLaunchKernelGGL((pf ? map_apply_grp_kernel<2, true> : map_apply_grp_kernel<2, false>), g2, b2, lds2,
-                         ctx->stream, p);
+      hipLaunchKernelGGL(pick(map_apply_grp_kernel<2, true, true>, map_apply_grp_kernel<2, true, false>,
+                              map_apply_grp_kernel<2, false, false>), g2, b2, lds2, ctx->stream, p);
     else
-      hipLaunchKernelGGL((pf ? map_apply_grp_kernel<4, true> : map_apply_grp_kernel<4, false>), g2, b2, lds2,
-                         ctx->stream, p);
+      hipLaunchKernelGGL(pick(map_apply_grp_kernel<4, true, true>, map_apply_grp_kernel<4, true, false>,
+                              map_apply_grp_kernel<4, false, false>), g2, b2, lds2, ctx->stream, p);
     timing_end(ctx);
     CRDT_HIP(ctx, hipGetLastError());
     return CRDT_OK;

@@ -53,6 +53,7 @@ struct OrswotApplyPlan {
   uint32_t *status;
   int wpb;
   int fence;  // 1: a workgroup fence after every op's stores (CRDT_TUNE afence=1, the round-2 form)
+  int l2pf;   // 1: touch a one-member Rm's entry row with the batch header (CRDT_TUNE oal2=1)
 };
 
 __device__ __forceinline__ u64 rl64(u64 x, int l) {
@@ -454,6 +455,20 @@ __device__ __forceinline__ void grp_forget_row(u64 *row, const u64 (&r)[kJ], int
   }
 }
 
+// L2PF (round 5): a one-member Rm forgets its member's whole entry row, a dependent HBM round trip
+// in the op loop (the Add's cell comes with the header; the Rm's 64-word row cannot be held per
+// lane).  With p.l2pf the header lane of such an Rm loads one word of each 128-byte line of the row
+// alongside the batch's other header loads; the XOR of those words goes into the Rm's unused cell
+// field of the header (so the loads are kept, and waited for where the header is written), and the
+// op's own row load later finds its lines in the cache.  Nothing reads the value.
+__device__ __forceinline__ u64 touch_row(const u64 *row, unsigned long long A) {
+  u64 x = 0;
+#pragma unroll
+  for (int j = 0; j < kWave / 16; ++j)
+    if (16ull * j < A) x ^= row[16 * j];
+  return x;
+}
+
 #ifndef CRDT_GRP_WPE
 #define CRDT_GRP_WPE 4
 #endif
@@ -471,7 +486,18 @@ __device__ __forceinline__ void grp_forget_row(u64 *row, const u64 (&r)[kJ], int
 // piece puts lane l's 16 bytes at byte 16 l of a 1-KiB block, so a group's 16 lanes fill its own
 // quarter of each block: half a row (32 words) per block, 2 STG blocks per batch (A even, rm_clock
 // 16-byte aligned; otherwise STG = 0).
-template <bool RPF, bool HPF, int STG = 0>
+// MT (round 5, default while Dcap <= kMetaSlots): per slot, next to its witness byte, the OR of the
+// slot's member words in LDS — the bloom is rebuilt from LDS alone after a slot is dropped (no HBM
+// read of every slot's member words) and an Add's re-forget tests a slot's LDS word before reading
+// its member word.  At the apply bench's default mix, where the deferred slots cost ~40% of the
+// kernel (profiles/r05_oapply_mix.log): 855 -> 808 us, no change without deferred removes.  Two more
+// LDS words per slot were measured and not kept (profiles/r05_oapply_meta_ab.log): the rm counter at
+// the witness plus a candidate-actor mask (an Add dropping a dominated slot without loading its row)
+// and an Rm's same-clock filter on that counter both made the kernel slower, 969-1,055 us, and 705
+// vs 522 us without deferred removes at all — the shuffles and ballots that keep them cost more in
+// every op step than the HBM reads they remove.
+constexpr unsigned long long kMetaSlots = 64;
+template <bool RPF, bool HPF, int STG = 0, bool MT = true>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRDT_GRP_WPE))) void orswot_apply_grp_kernel(
     OrswotApplyPlan p) {
   extern __shared__ u64 lds[];
@@ -483,7 +509,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRDT_GRP
   // then (STG) per wave 2 STG blocks of 128 words, group q's words at 32 q .. 32 q + 31 of each
   u64 *hdr = lds + (threadIdx.x / kG) * (4 * kG);
   uint8_t *wit = reinterpret_cast<uint8_t *>(lds + (kBlock / kG) * 4 * kG) + (threadIdx.x / kG) * Dcap;
-  u64 *stg = lds + (kBlock / kG) * 4 * kG + ((kBlock / kG) * Dcap + 15) / 16 * 2 + (threadIdx.x / kWave) * (2 * STG * 128);
+  const unsigned long long witw = ((kBlock / kG) * Dcap + 15) / 16 * 2;  // the witness bytes, in words
+  u64 *sbl = lds + (kBlock / kG) * 4 * kG + witw + (threadIdx.x / kG) * Dcap;  // (MT) slot member blooms
+  constexpr bool MB = MT;
+  u64 *stg = lds + (kBlock / kG) * 4 * kG + witw + (MT ? (kBlock / kG) * Dcap : 0) + (threadIdx.x / kWave) * (2 * STG * 128);
   const unsigned gw32 = (unsigned)(lane / kG) * 32;  // the group's quarter of a block
   const bool lead = g == 0;
 
@@ -509,15 +538,23 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRDT_GRP
     for (unsigned d = 0; d < dcnt; ++d) {
       const unsigned w = wit[d];
       if (w != kNoWitness) W |= 1ull << w;
-      for (unsigned long long x = g; x < Mw; x += kG) b |= DM[d * Mw + x];
+      if (MB) b |= sbl[d];
+      else
+        for (unsigned long long x = g; x < Mw; x += kG) b |= DM[d * Mw + x];
     }
-    bloom = grp_or(b);
+    bloom = MB ? b : grp_or(b);
   };
   for (unsigned d = 0; d < dcnt; ++d) {  // the input slots' witnesses at the input clock
     u64 x[kJ];
     grp_load_row(x, DC + d * A, g, A);
     const unsigned w = grp_witness(x, c, g, 0, A);
     if (lead) wit[d] = (uint8_t)w;
+    if (MB) {
+      u64 b = 0;
+      for (unsigned long long y = g; y < Mw; y += kG) b |= DM[d * Mw + y];
+      b = grp_or(b);
+      if (lead) sbl[d] = b;
+    }
   }
   rebuild();
   bool full = true;  // no Add yet: the input slots' members are re-forgotten in full at the first
@@ -533,6 +570,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRDT_GRP
       }
       for (unsigned long long x = g; x < Mw; x += kG) DM[d * Mw + x] = DM[last * Mw + x];
       if (lead) wit[d] = wit[last];
+      if (MB && lead) sbl[d] = sbl[last];
     }
     dcnt = last;
     if (p.fence) wave_fence();  // (a wave's later loads see its earlier stores; afence=1 adds fences)
@@ -582,6 +620,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRDT_GRP
           h_ka = kRmOp;
           h_cr = p.rm_row ? p.rm_row[oo] : 0u;
           if (me > mb) h_m0 = nx_m0;
+          if (p.l2pf && me - mb == 1 && h_m0 < M) h_cell = touch_row(E + (unsigned long long)h_m0 * p.entry_mstride, A);
         }
       }
       pre_fields(oo + kG);  // the next batch's kind and range while this one runs
@@ -601,6 +640,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRDT_GRP
         h_ka = kRmOp;
         h_cr = p.rm_row ? p.rm_row[oo] : 0u;
         if (me > mb) h_m0 = p.mem[mb];
+        if (p.l2pf && me - mb == 1 && h_m0 < M) h_cell = touch_row(E + (unsigned long long)h_m0 * p.entry_mstride, A);
       }
     }
     const int nb = (int)((oe - base) < (unsigned long long)kG ? (oe - base) : kG);
@@ -728,7 +768,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRDT_GRP
             const unsigned long long m = one ? m0 : p.mem[j];
             if (m >= M || !((bloom >> (m % 64)) & 1ull)) continue;
             for (unsigned d = 0; d < dcnt; ++d)
-              if ((DM[d * Mw + m / 64] >> (m % 64)) & 1ull) {
+              if ((!MB || ((sbl[d] >> (m % 64)) & 1ull)) && ((DM[d * Mw + m / 64] >> (m % 64)) & 1ull)) {
                 const u64 rv = DC[d * A + a];
                 if (lead) {
                   u64 *cell = E + m * p.entry_mstride + a;
@@ -831,6 +871,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRDT_GRP
           const unsigned long long wm = one && m0 < M ? (unsigned long long)m0 / 64 : ~0ull;
           for (unsigned long long x = g; x < Mw; x += kG) DM[slot * Mw + x] = x == wm ? 1ull << (m0 % 64) : 0ull;
           if (lead) wit[slot] = (uint8_t)wr;
+          if (MB && lead) sbl[slot] = one && m0 < M ? 1ull << (m0 % 64) : 0ull;
           W |= 1ull << wr;
           if (p.fence) wave_fence();  // the zeroed words are or-ed by the group's first lane below
           if (one) {
@@ -843,6 +884,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRDT_GRP
           const unsigned long long m = one ? m0 : p.mem[j];
           if (m >= M) continue;
           if (lead) DM[slot * Mw + m / 64] |= 1ull << (m % 64);
+          if (MB && lead) sbl[slot] |= 1ull << (m % 64);
           bloom |= 1ull << (m % 64);
         }
         if (p.fence) wave_fence();
@@ -896,7 +938,8 @@ extern "C" int crdt_orswot_apply_batch(crdt_ctx *ctx, const crdt_orswot_states *
                     (u64 *)s.def_clock, (u64 *)s.def_members, s.def_count, s.N, s.M, s.A, Mw, s.Dcap, Dh,
                     (const u64 *)ops->op_off, ops->kind, ops->actor, (const u64 *)ops->counter, ops->rm_row,
                     (const u64 *)ops->rm_clock, ops->rm_clock ? ops->n_rm_rows : 0, (const u64 *)ops->mem_off,
-                    ops->mem, ops->mem ? ops->n_mem : 0, ops->n_ops, status, wpb, ctx->tune.apply_fence};
+                    ops->mem, ops->mem ? ops->n_mem : 0, ops->n_ops, status, wpb, ctx->tune.apply_fence,
+                    ctx->tune.orswot_apply_l2pf};
   if (ctx->tune.apply_lane && s.A <= (size_t)kWave && s.Dcap <= 2048) {
     // kG lanes per state: kBlock / kG states per block, the slots' witness bytes in LDS
     timing_begin(ctx, "orswot_apply");
@@ -906,13 +949,18 @@ extern "C" int crdt_orswot_apply_batch(crdt_ctx *ctx, const crdt_orswot_states *
     // STG: the batch's first 2 Rm clock rows by LDS-DMA (opt-in, CRDT_TUNE oastg=1)
     const bool stg = ctx->tune.orswot_apply_stg && !rpf && !hpf && s.A % 2 == 0 && ops->rm_clock &&
                      ((uintptr_t)ops->rm_clock & 15) == 0;
+    // MT: the slots' member blooms in LDS (CRDT_TUNE oameta=0: the round-4 form, HBM only)
+    // (the opt-in prefetch forms rpf / hpf keep the round-4 form)
+    const bool mt = ctx->tune.orswot_apply_meta && s.Dcap <= kMetaSlots && !rpf && !hpf;
     const size_t lds = per_block * 4 * kG * 8 + (per_block * s.Dcap + 15) / 16 * 16 +
-                       (stg ? (kBlock / kWave) * 2 * 2 * 128 * 8 : 0);
-    if (stg) hipLaunchKernelGGL((orswot_apply_grp_kernel<false, false, 2>), grid, dim3(kBlock), lds, ctx->stream, p);
-    else if (rpf && hpf) hipLaunchKernelGGL((orswot_apply_grp_kernel<true, true>), grid, dim3(kBlock), lds, ctx->stream, p);
-    else if (rpf) hipLaunchKernelGGL((orswot_apply_grp_kernel<true, false>), grid, dim3(kBlock), lds, ctx->stream, p);
-    else if (hpf) hipLaunchKernelGGL((orswot_apply_grp_kernel<false, true>), grid, dim3(kBlock), lds, ctx->stream, p);
-    else hipLaunchKernelGGL((orswot_apply_grp_kernel<false, false>), grid, dim3(kBlock), lds, ctx->stream, p);
+                       (mt ? per_block * s.Dcap * 8 : 0) + (stg ? (kBlock / kWave) * 2 * 2 * 128 * 8 : 0);
+    if (stg && mt) hipLaunchKernelGGL((orswot_apply_grp_kernel<false, false, 2, true>), grid, dim3(kBlock), lds, ctx->stream, p);
+    else if (stg) hipLaunchKernelGGL((orswot_apply_grp_kernel<false, false, 2, false>), grid, dim3(kBlock), lds, ctx->stream, p);
+    else if (rpf && hpf) hipLaunchKernelGGL((orswot_apply_grp_kernel<true, true, 0, false>), grid, dim3(kBlock), lds, ctx->stream, p);
+    else if (rpf) hipLaunchKernelGGL((orswot_apply_grp_kernel<true, false, 0, false>), grid, dim3(kBlock), lds, ctx->stream, p);
+    else if (hpf) hipLaunchKernelGGL((orswot_apply_grp_kernel<false, true, 0, false>), grid, dim3(kBlock), lds, ctx->stream, p);
+    else if (mt) hipLaunchKernelGGL((orswot_apply_grp_kernel<false, false, 0, true>), grid, dim3(kBlock), lds, ctx->stream, p);
+    else hipLaunchKernelGGL((orswot_apply_grp_kernel<false, false, 0, false>), grid, dim3(kBlock), lds, ctx->stream, p);
     timing_end(ctx);
     CRDT_HIP(ctx, hipGetLastError());
     return CRDT_OK;

@@ -25,12 +25,15 @@ ap.add_argument("--actors", type=int, default=32)
 ap.add_argument("--vals", type=int, default=4)
 ap.add_argument("--dcap", type=int, default=16)
 ap.add_argument("--reps", type=int, default=5)
+ap.add_argument("--tune", default="")
 args = ap.parse_args()
 N, T, K, A, V, Dcap = args.states, args.ops, args.keys, args.actors, args.vals, args.dcap
 Kw = (K + 63) // 64
 
 torch.cuda.set_device(0)
 ctx = cg.Context(0)
+if args.tune:
+    ctx.tune(args.tune)
 ops = cg.synth.map_op_streams(N, T, K, A, seed=0x5EED000A, device="cuda")
 z = lambda *s: torch.zeros(s, dtype=torch.int64, device="cuda")  # noqa: E731
 clock, ec, vclk, vval = z(N, A), z(N, K, A), z(N, K, V, A), z(N, K, V)

@@ -25,6 +25,9 @@ ap.add_argument("--actors", type=int, default=64)
 ap.add_argument("--dcap", type=int, default=16)
 ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--tune", default="")
+ap.add_argument("--p-rm", type=float, default=0.2)
+ap.add_argument("--p-future", type=float, default=0.3)
+ap.add_argument("--cpu-s", type=float, default=10.0, help="CPU-baseline budget (0: none)")
 args = ap.parse_args()
 N, T, M, A, Dcap = args.states, args.ops, args.members, args.actors, args.dcap
 Mw = (M + 63) // 64
@@ -34,7 +37,7 @@ ctx = cg.Context(0)
 if args.tune:
     ctx.tune(args.tune)
 t0 = time.time()
-ops = cg.synth.orswot_op_streams(N, T, M, A, seed=0x5EED0009, device="cuda")
+ops = cg.synth.orswot_op_streams(N, T, M, A, seed=0x5EED0009, p_rm=args.p_rm, p_future=args.p_future, device="cuda")
 clock = torch.zeros((N, A), dtype=torch.int64, device="cuda")
 entries = torch.zeros((N, M, A), dtype=torch.int64, device="cuda")
 dcl = torch.zeros((N, Dcap, A), dtype=torch.int64, device="cuda")
@@ -101,7 +104,7 @@ ok = (np.array_equal(gc, oc) and np.array_equal(ge, oe) and np.array_equal(gn, o
 
 # CPU baseline: the twin on a bounded sample of states (~10 s), one thread
 cpu_states, cpu_s, k = 0, 0.0, 0
-while cpu_s < 10.0 and k * 4096 < N:
+while cpu_s < args.cpu_s and k * 4096 < N:
     blk = np.arange(k * 4096, min(N, (k + 1) * 4096))
     _, _, _, secs = O.orswot_apply_streams(len(blk), M, A, *sub(blk))
     cpu_states += len(blk)
@@ -113,6 +116,7 @@ print(json.dumps({
     "adds": n_add, "removes": n_rm, "deferred_left": int(cnt.sum().item()), "overflow_states": int((st & 1).astype(bool).sum()),
     "kernel_us": t * 1e6, "ops_per_s": N * T / t, "min_traffic_GBs": traffic / t / 1e9,
     "parity": "ok" if ok else "MISMATCH", "parity_states": int(len(sample)),
-    "cpu_baseline": {"ops_per_s": cpu_states * T / cpu_s, "cores": 1, "kind": "port",
+    "p_rm": args.p_rm, "p_future": args.p_future,
+    "cpu_baseline": None if not cpu_states else {"ops_per_s": cpu_states * T / cpu_s, "cores": 1, "kind": "port",
                      "sample": f"{cpu_states} states x {T} ops, C++ twin over std containers, {cpu_s:.2f} s"},
 }), flush=True)

@@ -17,7 +17,7 @@ pytestmark = pytest.mark.gpu
 import crdts_gpu as cg  # noqa: E402
 
 
-@pytest.fixture(scope="module", params=["alane=1", "alane=1,mapf=0", "alane=0"])
+@pytest.fixture(scope="module", params=["alane=1", "alane=1,mameta=0", "alane=1,mapf=0", "alane=0"])
 def mactx(request):
     """Both kernels: 16 lanes per state (alane=1, the default for A <= 64; mapf=0 without the
     next op's entry-row prefetch) and one wave per state (alane=0, every A); shapes with A > 64

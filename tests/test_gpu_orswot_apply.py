@@ -20,7 +20,7 @@ pytestmark = pytest.mark.gpu
 import crdts_gpu as cg  # noqa: E402
 
 
-@pytest.fixture(scope="module", params=["alane=1", "alane=1,oastg=1", "alane=1,oapf=1", "alane=1,ohpf=1", "alane=0"])
+@pytest.fixture(scope="module", params=["alane=1", "alane=1,oameta=0", "alane=1,oastg=1", "alane=1,oastg=1,oameta=0", "alane=1,oapf=1", "alane=1,ohpf=1", "alane=0"])
 def actx(request):
     """Both kernels: 16 lanes per state (alane=1, the default for A <= 64; its batch's first two Rm
     clock rows staged in LDS by LDS-DMA for even A with oastg=1, opt-in) and one wave per state (alane=0,
