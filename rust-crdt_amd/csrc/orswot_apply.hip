@@ -497,6 +497,9 @@ __device__ __forceinline__ u64 touch_row(const u64 *row, unsigned long long A) {
 // vs 522 us without deferred removes at all — the shuffles and ballots that keep them cost more in
 // every op step than the HBM reads they remove.
 constexpr unsigned long long kMetaSlots = 64;
+#ifndef CRDT_OA_WITV
+#define CRDT_OA_WITV 1  // (MT) the witness counter in LDS too (build option, for the A/B)
+#endif
 template <bool RPF, bool HPF, int STG = 0, bool MT = true>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRDT_GRP_WPE))) void orswot_apply_grp_kernel(
     OrswotApplyPlan p) {
@@ -510,9 +513,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRDT_GRP
   u64 *hdr = lds + (threadIdx.x / kG) * (4 * kG);
   uint8_t *wit = reinterpret_cast<uint8_t *>(lds + (kBlock / kG) * 4 * kG) + (threadIdx.x / kG) * Dcap;
   const unsigned long long witw = ((kBlock / kG) * Dcap + 15) / 16 * 2;  // the witness bytes, in words
-  u64 *sbl = lds + (kBlock / kG) * 4 * kG + witw + (threadIdx.x / kG) * Dcap;  // (MT) slot member blooms
-  constexpr bool MB = MT;
-  u64 *stg = lds + (kBlock / kG) * 4 * kG + witw + (MT ? (kBlock / kG) * Dcap : 0) + (threadIdx.x / kWave) * (2 * STG * 128);
+  u64 *sbl = lds + (kBlock / kG) * 4 * kG + witw + (threadIdx.x / kG) * 2 * Dcap;  // (MT) slot member blooms
+  u64 *witv = sbl + Dcap;  // (MT) each slot's rm counter at its witness
+  constexpr bool MB = MT, MW = MT && CRDT_OA_WITV;
+  u64 *stg = lds + (kBlock / kG) * 4 * kG + witw + (MT ? (kBlock / kG) * 2 * Dcap : 0) + (threadIdx.x / kWave) * (2 * STG * 128);
   const unsigned gw32 = (unsigned)(lane / kG) * 32;  // the group's quarter of a block
   const bool lead = g == 0;
 
@@ -549,6 +553,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRDT_GRP
     grp_load_row(x, DC + d * A, g, A);
     const unsigned w = grp_witness(x, c, g, 0, A);
     if (lead) wit[d] = (uint8_t)w;
+    if (MW && lead && w != kNoWitness) witv[d] = DC[d * A + w];
     if (MB) {
       u64 b = 0;
       for (unsigned long long y = g; y < Mw; y += kG) b |= DM[d * Mw + y];
@@ -570,7 +575,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRDT_GRP
       }
       for (unsigned long long x = g; x < Mw; x += kG) DM[d * Mw + x] = DM[last * Mw + x];
       if (lead) wit[d] = wit[last];
-      if (MB && lead) sbl[d] = sbl[last];
+      if (MB && lead) {
+        sbl[d] = sbl[last];
+        if (MW) witv[d] = witv[last];
+      }
     }
     dcnt = last;
     if (p.fence) wave_fence();  // (a wave's later loads see its earlier stores; afence=1 adds fences)
@@ -755,6 +763,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRDT_GRP
               drop(d);
             } else {
               if (lead) wit[d] = (uint8_t)w;
+              if (MW && lead) witv[d] = DC[d * A + w];
               ++d;
             }
           }
@@ -782,7 +791,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRDT_GRP
         if ((W >> a) & 1ull) {
           bool dropped = false;
           for (unsigned d = 0; d < dcnt;) {
-            if (wit[d] == a && DC[d * A + a] <= k) {
+            if (wit[d] == a && (MW ? witv[d] : DC[d * A + a]) <= k) {
               u64 x[kJ];
               grp_load_row(x, DC + d * A, g, A);
               const unsigned w = grp_witness(x, c, g, a + 1, A);
@@ -792,6 +801,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRDT_GRP
                 continue;
               }
               if (lead) wit[d] = (uint8_t)w;
+              if (MW && lead) witv[d] = DC[d * A + w];  // (the row just loaded: a cache hit)
             }
             ++d;
           }
@@ -872,6 +882,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(CRDT_GRP
           for (unsigned long long x = g; x < Mw; x += kG) DM[slot * Mw + x] = x == wm ? 1ull << (m0 % 64) : 0ull;
           if (lead) wit[slot] = (uint8_t)wr;
           if (MB && lead) sbl[slot] = one && m0 < M ? 1ull << (m0 % 64) : 0ull;
+          if (MW && (unsigned)g == wr % kG) {  // the lane holding actor wr: no cross-lane move
+            u64 v = r[0];
+#pragma unroll
+            for (int j = 1; j < kJ; ++j)
+              if ((unsigned)j == wr / kG) v = r[j];
+            witv[slot] = v;
+          }
           W |= 1ull << wr;
           if (p.fence) wave_fence();  // the zeroed words are or-ed by the group's first lane below
           if (one) {
@@ -953,7 +970,7 @@ extern "C" int crdt_orswot_apply_batch(crdt_ctx *ctx, const crdt_orswot_states *
     // (the opt-in prefetch forms rpf / hpf keep the round-4 form)
     const bool mt = ctx->tune.orswot_apply_meta && s.Dcap <= kMetaSlots && !rpf && !hpf;
     const size_t lds = per_block * 4 * kG * 8 + (per_block * s.Dcap + 15) / 16 * 16 +
-                       (mt ? per_block * s.Dcap * 8 : 0) + (stg ? (kBlock / kWave) * 2 * 2 * 128 * 8 : 0);
+                       (mt ? per_block * 2 * s.Dcap * 8 : 0) + (stg ? (kBlock / kWave) * 2 * 2 * 128 * 8 : 0);
     if (stg && mt) hipLaunchKernelGGL((orswot_apply_grp_kernel<false, false, 2, true>), grid, dim3(kBlock), lds, ctx->stream, p);
     else if (stg) hipLaunchKernelGGL((orswot_apply_grp_kernel<false, false, 2, false>), grid, dim3(kBlock), lds, ctx->stream, p);
     else if (rpf && hpf) hipLaunchKernelGGL((orswot_apply_grp_kernel<true, true, 0, false>), grid, dim3(kBlock), lds, ctx->stream, p);
