@@ -490,11 +490,13 @@ __device__ __forceinline__ u64 touch_row(const u64 *row, unsigned long long A) {
 // slot's member words in LDS — the bloom is rebuilt from LDS alone after a slot is dropped (no HBM
 // read of every slot's member words) and an Add's re-forget tests a slot's LDS word before reading
 // its member word.  At the apply bench's default mix, where the deferred slots cost ~40% of the
-// kernel (profiles/r05_oapply_mix.log): 855 -> 808 us, no change without deferred removes.  Two more
-// LDS words per slot were measured and not kept (profiles/r05_oapply_meta_ab.log): the rm counter at
-// the witness plus a candidate-actor mask (an Add dropping a dominated slot without loading its row)
-// and an Rm's same-clock filter on that counter both made the kernel slower, 969-1,055 us, and 705
-// vs 522 us without deferred removes at all — the shuffles and ballots that keep them cost more in
+// kernel (profiles/r05_oapply_mix.log): 855 -> 808 us, no change without deferred removes.  Also the
+// slot's rm counter at its witness (an Add to the witness actor tests it in LDS, not HBM; written by
+// the lane that holds that actor, or read back by the group's first lane on the rare paths): 817 ->
+// 813 us (profiles/r05_apply_witv_ab.log).  Measured and not kept (profiles/r05_oapply_meta_ab.log):
+// that counter moved between lanes by shuffles plus a candidate-actor mask by ballots (an Add
+// dropping a dominated slot without loading its row), and an Rm's same-clock filter on the counter:
+// 969-1,055 us, and 705 vs 522 us without deferred removes at all — the cross-lane moves cost more in
 // every op step than the HBM reads they remove.
 constexpr unsigned long long kMetaSlots = 64;
 #ifndef CRDT_OA_WITV
