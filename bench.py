@@ -83,6 +83,9 @@ def parse():
     ap.add_argument("--c4", action=argparse.BooleanOptionalAction, default=None,
                     help="also time BASELINE config 4 (Map<u32, MVReg<u64>> 16,384 x 1,024 x 32, V = 2) in a "
                          "`c4` block; default on at N = 1")
+    ap.add_argument("--contig-input", action=argparse.BooleanOptionalAction, default=True,
+                    help="c3: generate the replicas in one physically contiguous device block (crdt_device_alloc) "
+                         "when one is free")
     ap.add_argument("--causal-steps", type=int, default=5, help="timed lub_many calls of the c3 / c4 blocks")
     ap.add_argument("--parity-seed", type=int, default=1, help="member / key sample of the c3 / c4 parity checks")
     ap.add_argument("--parity-members", type=int, default=16)
@@ -551,7 +554,12 @@ def run_causal(args, env, block):
     ctx = env.ctx
     if block == "c3":
         p = C3
-        inp = synth.orswot_replicas(ctx, p["R"], p["M"], p["A"], seed=p["seed"], kmax=p["kmax"], p_def=p["p_def"])
+        # the 128 GiB of replicas in one physically contiguous block where one is free (fewer
+        # translation misses for the one streaming pass), else the torch allocator
+        ent = ctx.device_empty((p["R"], p["M"], p["A"])) if args.contig_input else None
+        alloc = "contiguous block (crdt_device_alloc)" if ent is not None else "torch caching allocator"
+        inp = synth.orswot_replicas(ctx, p["R"], p["M"], p["A"], seed=p["seed"], kmax=p["kmax"], p_def=p["p_def"],
+                                    entries=ent)
         D = inp.def_clock.shape[0]
         goff = [0, D]
 
@@ -564,7 +572,7 @@ def run_causal(args, env, block):
         alg = (R + 1) * (p["M"] * p["A"] + p["A"]) * 8
         alg_note = "8·(M·A + A) per replica read + the (M·A + A) u64 output"
         cfg = {"replicas": R, "members": p["M"], "actors": p["A"], "deferred_removes": D,
-               "types": ["Orswot<u64 member, u32 actor>"]}
+               "types": ["Orswot<u64 member, u32 actor>"], "input_alloc": alloc}
     else:
         p = C4
         inp = synth.map_replicas(ctx, p["R"], p["K"], p["A"], p["V"], p["seed"], kmax=p["kmax"], p_def=p["p_def"])

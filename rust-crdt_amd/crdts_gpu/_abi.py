@@ -48,6 +48,7 @@ EXPORTS = (
     "crdt_orswot_forget_batch", "crdt_map_forget_batch", "crdt_map_apply_batch",
     "crdt_orswot_merge_batch", "crdt_map_merge_batch",
     "crdt_ctx_set_mem_kind", "crdt_ctx_mem_kind", "crdt_host_alloc", "crdt_host_free",
+    "crdt_device_alloc", "crdt_device_free",
     "crdt_lub_many_multi", "crdt_lub_many_multi_sharded", "crdt_map_ingest", "crdt_map_egress",
     "crdt_ctx_comm_init_ops", "crdt_ctx_comm_note",
     "crdt_mvreg_lub_many", "crdt_mvreg_merge_batch", "crdt_mvreg_apply_batch",
@@ -265,6 +266,8 @@ _SIGS = {
     "crdt_ctx_mem_kind": ([P], ctypes.c_int),
     "crdt_host_alloc": ([S, ctypes.POINTER(P)], ctypes.c_int),
     "crdt_host_free": ([P], ctypes.c_int),
+    "crdt_device_alloc": ([P, S, ctypes.POINTER(P)], ctypes.c_int),
+    "crdt_device_free": ([P, P], ctypes.c_int),
     "crdt_lub_many_multi": ([P, ctypes.POINTER(LubSegment), S], ctypes.c_int),
     "crdt_lub_many_multi_sharded": ([P, ctypes.POINTER(LubSegment), S], ctypes.c_int),
     "crdt_map_ingest": ([P, P, P, P, P, ctypes.POINTER(MapStates), ctypes.POINTER(MapDeferred), P], ctypes.c_int),

@@ -81,6 +81,22 @@ class Context:
         """Override launch-geometry knobs ("key=value,...", CRDT_TUNE syntax); never changes results."""
         self.call("crdt_ctx_tune", spec.encode())
 
+    def device_empty(self, shape, dtype: torch.dtype = torch.int64) -> Optional[torch.Tensor]:
+        """An uninitialised tensor on this ctx's GPU in one physically contiguous block
+        (crdt_device_alloc), freed when the last view of it dies; None when no such block is free
+        (the caller then takes any device memory, e.g. torch.empty)."""
+        n = 1
+        for x in shape:
+            n *= int(x)
+        nbytes = n * torch.empty((), dtype=dtype).element_size()
+        p = ctypes.c_void_p()
+        rc = self.lib.crdt_device_alloc(self.ptr, max(nbytes, 1), ctypes.byref(p))
+        if rc != 0 or not p.value:
+            return None
+        typestr = {torch.int64: "<i8", torch.int32: "<i4", torch.uint8: "|u1", torch.int8: "|i1"}[dtype]
+        blk = _DeviceBlock(self.lib, p.value, tuple(int(x) for x in shape), typestr)
+        return torch.as_tensor(blk, device=torch.device("cuda", self.device))
+
     # -- tensor checks ----------------------------------------------------------------------
     def check_tensor(self, t: torch.Tensor, what: str, dtypes=None) -> None:
         if not isinstance(t, torch.Tensor):
@@ -92,6 +108,21 @@ class Context:
             raise TypeError(f"{what}: dtype {t.dtype}; expected int64/uint64 holding u64 bits")
         if t.device.type != "cuda" or t.device.index != self.device:
             raise ValueError(f"{what}: tensor on {t.device}; expected cuda:{self.device}")
+
+
+class _DeviceBlock:
+    """A crdt_device_alloc block seen by torch through __cuda_array_interface__; torch holds a
+    reference for as long as a tensor views it, and the block is freed after the last one."""
+
+    def __init__(self, lib, ptr: int, shape, typestr: str):
+        self._lib, self._ptr = lib, ptr
+        self.__cuda_array_interface__ = {"shape": shape, "typestr": typestr, "data": (ptr, False),
+                                         "version": 2, "strides": None}
+
+    def __del__(self):
+        if self._ptr:
+            self._lib.crdt_device_free(None, ctypes.c_void_p(self._ptr))
+            self._ptr = 0
 
 
 def dptr(t: torch.Tensor) -> ctypes.c_void_p:

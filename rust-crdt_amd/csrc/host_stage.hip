@@ -1400,4 +1400,26 @@ int crdt_host_free(void *p) {
   return e == hipSuccess ? CRDT_OK : crdt::hip_fail(nullptr, e, "hipHostFree");
 }
 
+int crdt_device_alloc(crdt_ctx *ctx, size_t bytes, void **out) {
+  CRDT_CHECK_CTX(ctx);
+  if (!out) return crdt::fail(ctx, CRDT_EINVAL, "crdt_device_alloc: out is NULL");
+  *out = nullptr;
+  if (bytes == 0) return CRDT_OK;
+  CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  hipError_t e = hipExtMallocWithFlags(out, bytes, hipDeviceMallocContiguous);
+  if (e != hipSuccess) {
+    *out = nullptr;
+    (void)hipGetLastError();  // (not sticky: the caller may fall back)
+    return crdt::fail(ctx, CRDT_ENOMEM, "crdt_device_alloc(%zu): %s", bytes, hipGetErrorString(e));
+  }
+  return CRDT_OK;
+}
+
+int crdt_device_free(crdt_ctx *ctx, void *p) {  // (ctx may be NULL: the block knows its device)
+  if (!p) return CRDT_OK;
+  if (ctx) CRDT_HIP(ctx, hipSetDevice(ctx->device));
+  hipError_t e = hipFree(p);
+  return e == hipSuccess ? CRDT_OK : crdt::hip_fail(ctx, e, "hipFree");
+}
+
 }  // extern "C"

@@ -71,7 +71,7 @@ HOST_CAPABLE = ({f"crdt_{t}_{op}" for t in ("vclock", "gcounter", "pncounter", "
 CTX_ONLY = {"crdt_ctx_destroy", "crdt_ctx_set_stream", "crdt_ctx_synchronize", "crdt_ctx_set_timing",
             "crdt_ctx_timing", "crdt_ctx_timing_reset", "crdt_ctx_tune", "crdt_ctx_set_mem_kind",
             "crdt_ctx_comm_init", "crdt_ctx_comm_destroy", "crdt_ctx_comm_info", "crdt_ctx_mem_kind",
-            "crdt_ctx_comm_init_ops"}
+            "crdt_ctx_comm_init_ops", "crdt_device_alloc", "crdt_device_free"}  # (allocation, no compute)
 
 
 def test_every_compute_entry_point_guards_host_mode():

@@ -185,3 +185,19 @@ def test_gset_module_api(gpu_ctx):
     for e in exp:
         acc.merge(e)
     assert cg.gset.read(cg.gset.lub_many(st).unsqueeze(0)) == [sorted(acc.value)]
+
+
+def test_device_empty_block(gpu_ctx):
+    """crdt_device_alloc (one physically contiguous block) seen as a torch tensor: the fold reads it
+    like any other replica batch, and the block is freed with its last view."""
+    t = gpu_ctx.device_empty((1000, 64))
+    assert t is not None and t.shape == (1000, 64) and t.dtype == torch.int64 and t.device.index == gpu_ctx.device
+    rng = np.random.default_rng(9)
+    x = rng.integers(0, 1 << 40, size=(1000, 64)).astype(np.uint64)
+    t.copy_(to_dev(x))
+    assert np.array_equal(to_host(cg.vclock.lub_many(t, ctx=gpu_ctx)), x.max(axis=0))
+    v = t[10:20]
+    del t
+    assert np.array_equal(to_host(v), x[10:20])  # the view keeps the block alive
+    del v
+    assert gpu_ctx.device_empty((0,)) is not None
