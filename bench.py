@@ -84,7 +84,7 @@ def parse():
                     help="also time BASELINE config 4 (Map<u32, MVReg<u64>> 16,384 x 1,024 x 32, V = 2) in a "
                          "`c4` block; default on at N = 1")
     ap.add_argument("--contig-input", action=argparse.BooleanOptionalAction, default=True,
-                    help="c3: generate the replicas in one physically contiguous device block (crdt_device_alloc) "
+                    help="generate each input batch in one physically contiguous device block (crdt_device_alloc) "
                          "when one is free")
     ap.add_argument("--causal-steps", type=int, default=5, help="timed lub_many calls of the c3 / c4 blocks")
     ap.add_argument("--parity-seed", type=int, default=1, help="member / key sample of the c3 / c4 parity checks")
@@ -308,11 +308,14 @@ def run_workload(args, env, workload):
     R = args.replicas
     A = args.actors if (args.actors is not None and workload == args.workload) else (A_C5 if workload == "c5" else A_ACTORS)
     # Synthetic replicas, generated in HBM; rank k owns rows [k*R, (k+1)*R) of the global input.
+    def alloc(shape):  # one contiguous device block where one is free (--contig-input), else torch's
+        t = ctx.device_empty(shape) if args.contig_input else None
+        return t if t is not None else torch.empty(shape, dtype=torch.int64, device="cuda")
+
     if workload == "c5":
-        lubs = [("vclock", torch.empty((R, A), dtype=torch.int64, device="cuda"), SEED_V)]
+        lubs = [("vclock", alloc((R, A)), SEED_V)]
     else:
-        lubs = [("gcounter", torch.empty((R, A), dtype=torch.int64, device="cuda"), SEED_G),
-                ("pncounter", torch.empty((R, 2 * A), dtype=torch.int64, device="cuda"), SEED_P)]
+        lubs = [("gcounter", alloc((R, A)), SEED_G), ("pncounter", alloc((R, 2 * A)), SEED_P)]
     for _, x, seed in lubs:
         cg.synth_fill(ctx, x, seed, 0, first_row=rank * R)
     outs = [torch.empty((x.shape[1],), dtype=torch.int64, device="cuda") for _, x, _ in lubs]
