@@ -23,6 +23,12 @@ namespace crdt {
 
 // waves per SIMD asked of the register allocator for A <= 128 (build option; A/B in
 // profiles/r05_vapply_wpe_ab.log); the wider instances keep the compiler's choice (they would spill)
+// op headers batched 64 at a time into lanes and read by v_readlane (build option, off: at the
+// kernel's 8 waves per SIMD it measured 2.30 vs 2.18 ms, profiles/r05_vapply_hdr_ab.log; the
+// Orswot-valued kernel, at 5 waves, gains from it and has it on)
+#ifndef CRDT_MCA_HDR
+#define CRDT_MCA_HDR 0
+#endif
 #ifndef CRDT_MCA_WPE
 #define CRDT_MCA_WPE 8
 #endif
@@ -47,6 +53,11 @@ struct MapCounterApplyPlan {
   unsigned *status;
   unsigned wpb;  // waves per block
 };
+
+__device__ __forceinline__ unsigned rl32(unsigned x, int i) { return (unsigned)__builtin_amdgcn_readlane((int)x, i); }
+__device__ __forceinline__ u64 rl64(u64 x, int i) {
+  return ((u64)rl32((unsigned)(x >> 32), i) << 32) | rl32((unsigned)x, i);
+}
 
 template <int APL>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APL <= 2 ? CRDT_MCA_WPE : 1))) void map_counter_apply_kernel(MapCounterApplyPlan p) {
@@ -153,13 +164,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APL <= 2 ? 
     full = false;
   };
 
-  for (unsigned long long o = ob; o < oe; ++o) {
-    const unsigned kind = p.kind[o];
+  // Op headers in batches of 64: lane i loads op o0 + i's fields (coalesced, all in flight
+  // together) and op o's fields reach the wave by v_readlane, not by a global round trip per op.
+  for (unsigned long long o0 = ob; o0 < oe; o0 += kWave) {
+    const unsigned long long mo = o0 + (unsigned long long)lane;
+    const bool hin = CRDT_MCA_HDR && mo < oe;
+    const unsigned h_kind = hin ? p.kind[mo] : 0u;
+    const unsigned h_a = hin ? p.actor[mo] : 0u, h_va = hin ? p.vactor[mo] : 0u, h_k = hin ? p.key[mo] : 0u;
+    const u64 h_c = hin ? p.counter[mo] : 0ull, h_vc = hin ? p.vcounter[mo] : 0ull;
+    const unsigned h_dir = hin && p.vdir ? p.vdir[mo] : 0u;
+    const unsigned h_rr = hin && p.clk_row ? p.clk_row[mo] : 0xffffffffu;
+    const u64 h_kb = hin ? p.key_off[mo] : 0ull, h_ke = hin ? p.key_off[mo + 1] : 0ull;
+    const int nb = (int)(oe - o0 < (unsigned long long)kWave ? oe - o0 : (unsigned long long)kWave);
+  for (int i = 0; i < nb; ++i) {
+    const unsigned long long o = o0 + (unsigned long long)i;
+    const unsigned kind = CRDT_MCA_HDR ? rl32(h_kind, i) : p.kind[o];
     if (kind == 0) {  // ---- Op::Up
-      const unsigned a = p.actor[o], va = p.vactor[o];
-      const unsigned long long k = p.key[o];
-      const u64 cnt = p.counter[o], vc = p.vcounter[o];
-      const unsigned dir = p.vdir ? p.vdir[o] : 0u;
+      const unsigned a = CRDT_MCA_HDR ? rl32(h_a, i) : p.actor[o], va = CRDT_MCA_HDR ? rl32(h_va, i) : p.vactor[o];
+      const unsigned long long k = CRDT_MCA_HDR ? rl32(h_k, i) : p.key[o];
+      const u64 cnt = CRDT_MCA_HDR ? rl64(h_c, i) : p.counter[o], vc = CRDT_MCA_HDR ? rl64(h_vc, i) : p.vcounter[o];
+      const unsigned dir = CRDT_MCA_HDR ? rl32(h_dir, i) : (p.vdir ? p.vdir[o] : 0u);
       if (a >= A || va >= A || k >= K || dir >= W) {
         st |= 2u;
         continue;
@@ -178,8 +202,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APL <= 2 ? 
       }
       apply_deferred(k);
     } else if (kind == 1) {  // ---- Op::Rm -> apply_keyset_rm
-      const unsigned rr = p.clk_row ? p.clk_row[o] : 0xffffffffu;
-      const u64 kb = p.key_off[o], ke = p.key_off[o + 1];
+      const unsigned rr = CRDT_MCA_HDR ? rl32(h_rr, i) : (p.clk_row ? p.clk_row[o] : 0xffffffffu);
+      const u64 kb = CRDT_MCA_HDR ? rl64(h_kb, i) : p.key_off[o], ke = CRDT_MCA_HDR ? rl64(h_ke, i) : p.key_off[o + 1];
       if (rr >= p.n_clk_rows || ke < kb || ke > p.n_keys) {
         st |= 2u;
         continue;
@@ -219,6 +243,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APL <= 2 ? 
     } else {
       st |= 2u;
     }
+  }
   }
 #pragma unroll
   for (int j = 0; j < APL; ++j)

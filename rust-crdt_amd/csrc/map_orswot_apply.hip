@@ -17,6 +17,11 @@ namespace crdt {
 
 // waves per SIMD asked of the register allocator for A <= 128 (build option; A/B in
 // profiles/r05_vapply_wpe_ab.log); the wider instances keep the compiler's choice (they would spill)
+// op headers batched 64 at a time into lanes and read by v_readlane (build option; 0 = one global
+// read of each field per op)
+#ifndef CRDT_MOA_HDR
+#define CRDT_MOA_HDR 1
+#endif
 #ifndef CRDT_MOA_WPE
 #define CRDT_MOA_WPE 6
 #endif
@@ -46,6 +51,11 @@ struct MapOrswotApplyPlan {
   unsigned *status;
   unsigned wpb;
 };
+
+__device__ __forceinline__ unsigned rl32(unsigned x, int i) { return (unsigned)__builtin_amdgcn_readlane((int)x, i); }
+__device__ __forceinline__ u64 rl64(u64 x, int i) {
+  return ((u64)rl32((unsigned)(x >> 32), i) << 32) | rl32((unsigned)x, i);
+}
 
 template <int APL>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APL <= 2 ? CRDT_MOA_WPE : 1))) void map_orswot_apply_kernel(MapOrswotApplyPlan p) {
@@ -255,14 +265,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APL <= 2 ? 
     full = false;
   };
 
-  for (unsigned long long o = ob; o < oe; ++o) {
-    const unsigned kind = p.kind[o];
+  // Op headers in batches of 64: lane i loads op o0 + i's fields (coalesced, all in flight
+  // together) and op o's fields reach the wave by v_readlane, not by a global round trip per op.
+  for (unsigned long long o0 = ob; o0 < oe; o0 += kWave) {
+    const unsigned long long mo = o0 + (unsigned long long)lane;
+    const bool hin = CRDT_MOA_HDR && mo < oe;
+    const unsigned h_kind = hin ? p.kind[mo] : 0u, h_a = hin ? p.actor[mo] : 0u, h_k = hin ? p.key[mo] : 0u;
+    const unsigned h_vk = hin ? p.vkind[mo] : 0u, h_va = hin ? p.vactor[mo] : 0u;
+    const u64 h_c = hin ? p.counter[mo] : 0ull, h_vc = hin ? p.vcounter[mo] : 0ull;
+    const u64 h_mb = hin ? p.mem_off[mo] : 0ull, h_me = hin ? p.mem_off[mo + 1] : 0ull;
+    const unsigned h_rr = hin ? p.clk_row[mo] : 0u;
+    const u64 h_kb = hin ? p.key_off[mo] : 0ull, h_ke = hin ? p.key_off[mo + 1] : 0ull;
+    const int nb = (int)(oe - o0 < (unsigned long long)kWave ? oe - o0 : (unsigned long long)kWave);
+  for (int hi = 0; hi < nb; ++hi) {
+    const unsigned long long o = o0 + (unsigned long long)hi;
+    const unsigned kind = CRDT_MOA_HDR ? rl32(h_kind, hi) : p.kind[o];
     if (kind == 0) {  // ---- Map Op::Up { dot, key, op: an Orswot op }
-      const unsigned a = p.actor[o];
-      const unsigned long long k = p.key[o];
-      const u64 cnt = p.counter[o];
-      const unsigned vk = p.vkind[o];
-      const u64 mb = p.mem_off[o], me = p.mem_off[o + 1];
+      const unsigned a = CRDT_MOA_HDR ? rl32(h_a, hi) : p.actor[o];
+      const unsigned long long k = CRDT_MOA_HDR ? rl32(h_k, hi) : p.key[o];
+      const u64 cnt = CRDT_MOA_HDR ? rl64(h_c, hi) : p.counter[o];
+      const unsigned vk = CRDT_MOA_HDR ? rl32(h_vk, hi) : p.vkind[o];
+      const u64 mb = CRDT_MOA_HDR ? rl64(h_mb, hi) : p.mem_off[o], me = CRDT_MOA_HDR ? rl64(h_me, hi) : p.mem_off[o + 1];
       if (a >= A || k >= K || vk > 1 || me < mb || me > p.n_mems) {
         st |= 2u;
         continue;
@@ -273,8 +296,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APL <= 2 ? 
       u64 oc[APL];
       ldrow(q.oc, oc);
       if (vk == 0) {  // Orswot Op::Add { dot, members }
-        const unsigned va = p.vactor[o];
-        const u64 vc = p.vcounter[o];
+        const unsigned va = CRDT_MOA_HDR ? rl32(h_va, hi) : p.vactor[o];
+        const u64 vc = CRDT_MOA_HDR ? rl64(h_vc, hi) : p.vcounter[o];
         if (va >= A) {
           st |= 2u;
         } else if (word_of(oc, va) < vc) {  // (seen by the Orswot's clock: nothing)
@@ -294,7 +317,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APL <= 2 ? 
           }
         }
       } else {  // Orswot Op::Rm { clock, members } -> apply_rm
-        const unsigned rr = p.clk_row[o];
+        const unsigned rr = CRDT_MOA_HDR ? rl32(h_rr, hi) : p.clk_row[o];
         if (rr >= p.n_clk_rows) {
           st |= 2u;
         } else {
@@ -347,8 +370,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APL <= 2 ? 
         if ((unsigned)j == a / 64 && (unsigned long long)lane == a % 64 && c[j] < cnt) c[j] = cnt;
       map_apply_deferred(k);
     } else if (kind == 1) {  // ---- Map Op::Rm -> apply_keyset_rm
-      const unsigned rr = p.clk_row[o];
-      const u64 kb = p.key_off[o], ke = p.key_off[o + 1];
+      const unsigned rr = CRDT_MOA_HDR ? rl32(h_rr, hi) : p.clk_row[o];
+      const u64 kb = CRDT_MOA_HDR ? rl64(h_kb, hi) : p.key_off[o], ke = CRDT_MOA_HDR ? rl64(h_ke, hi) : p.key_off[o + 1];
       if (rr >= p.n_clk_rows || ke < kb || ke > p.n_keys) {
         st |= 2u;
         continue;
@@ -386,6 +409,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APL <= 2 ? 
     } else {
       st |= 2u;
     }
+  }
   }
 #pragma unroll
   for (int j = 0; j < APL; ++j)
