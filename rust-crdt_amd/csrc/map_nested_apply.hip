@@ -52,6 +52,16 @@ struct NestedApplyPlan {
 };
 
 // The rows of outer key k of state s, and the inner-Map operations on them.
+// op headers batched 64 at a time into lanes and read by v_readlane (build option; 0 = one global
+// read of each field per op)
+#ifndef CRDT_MNA_HDR
+#define CRDT_MNA_HDR 1
+#endif
+__device__ __forceinline__ unsigned rl32(unsigned x, int i) { return (unsigned)__builtin_amdgcn_readlane((int)x, i); }
+__device__ __forceinline__ u64 rl64(u64 x, int i) {
+  return ((u64)rl32((unsigned)(x >> 32), i) << 32) | rl32((unsigned)x, i);
+}
+
 template <int APL>
 struct NaKey {
   u64 *ec, *ic, *iec, *ivc, *ivv, *idc, *idk;
@@ -392,16 +402,28 @@ __global__ __launch_bounds__(256) void map_nested_apply_kernel(NestedApplyPlan p
     full = false;
   };
 
-  for (unsigned long long o = ob; o < oe; ++o) {
-    const unsigned kind = p.kind[o];
+  // Op headers in batches of 64 (CRDT_MNA_HDR): lane i loads op o0 + i's fields (coalesced, all in
+  // flight together) and op o's fields reach the wave by v_readlane, not by a global round trip per op.
+  for (unsigned long long o0 = ob; o0 < oe; o0 += kWave) {
+    const unsigned long long mo = o0 + (unsigned long long)lane;
+    const bool hin = CRDT_MNA_HDR && mo < oe;
+    const unsigned h_kind = hin ? p.kind[mo] : 0u, h_ik = hin ? p.ikind[mo] : 0u, h_a = hin ? p.actor[mo] : 0u;
+    const unsigned h_k = hin ? p.key[mo] : 0u, h_ia = hin ? p.iactor[mo] : 0u, h_jk = hin ? p.ikey[mo] : 0u;
+    const unsigned h_rr = hin ? p.clk_row[mo] : 0u;
+    const u64 h_c = hin ? p.counter[mo] : 0ull, h_ic = hin ? p.icounter[mo] : 0ull, h_v = hin ? p.val[mo] : 0ull;
+    const u64 h_ib = hin ? p.ikeys[mo] : 0ull, h_kb = hin ? p.key_off[mo] : 0ull, h_ke = hin ? p.key_off[mo + 1] : 0ull;
+    const int nb = (int)(oe - o0 < (unsigned long long)kWave ? oe - o0 : (unsigned long long)kWave);
+  for (int hi = 0; hi < nb; ++hi) {
+    const unsigned long long o = o0 + (unsigned long long)hi;
+    const unsigned kind = CRDT_MNA_HDR ? rl32(h_kind, hi) : p.kind[o];
     if (kind == 0) {  // ---- Op::Up { dot, key, op: an inner Map op }
-      const unsigned a = p.actor[o], ik = p.ikind[o];
-      const unsigned long long k = p.key[o];
-      const u64 cnt = p.counter[o];
-      const unsigned rr = p.clk_row[o];
-      const unsigned ia = ik == 0 ? p.iactor[o] : 0u;
-      const unsigned long long jk = ik == 0 ? p.ikey[o] : 0ull;
-      const u64 ib = ik == 1 ? p.ikeys[o] : 0ull;
+      const unsigned a = CRDT_MNA_HDR ? rl32(h_a, hi) : p.actor[o], ik = CRDT_MNA_HDR ? rl32(h_ik, hi) : p.ikind[o];
+      const unsigned long long k = CRDT_MNA_HDR ? rl32(h_k, hi) : p.key[o];
+      const u64 cnt = CRDT_MNA_HDR ? rl64(h_c, hi) : p.counter[o];
+      const unsigned rr = CRDT_MNA_HDR ? rl32(h_rr, hi) : p.clk_row[o];
+      const unsigned ia = ik == 0 ? (CRDT_MNA_HDR ? rl32(h_ia, hi) : p.iactor[o]) : 0u;
+      const unsigned long long jk = ik == 0 ? (CRDT_MNA_HDR ? rl32(h_jk, hi) : p.ikey[o]) : 0ull;
+      const u64 ib = ik == 1 ? (CRDT_MNA_HDR ? rl64(h_ib, hi) : p.ikeys[o]) : 0ull;
       if (a >= A || k >= K || ik > 1 || rr >= p.n_clk_rows || ia >= A || jk >= K2 || (K2 < 64 && (ib >> K2))) {
         st |= 2u;  // malformed: skipped whole
         continue;
@@ -411,7 +433,7 @@ __global__ __launch_bounds__(256) void map_nested_apply_kernel(NestedApplyPlan p
       q.bump(q.ec, a, cnt);  // entry.clock.apply(dot) (an absent entry: its rows are Map::default())
       u64 r[APL];
       q.ld(p.clk_pool + (unsigned long long)rr * A, r);
-      if (ik == 0) q.inner_up(ia, p.icounter[o], jk, r, p.val[o]);
+      if (ik == 0) q.inner_up(ia, CRDT_MNA_HDR ? rl64(h_ic, hi) : p.icounter[o], jk, r, CRDT_MNA_HDR ? rl64(h_v, hi) : p.val[o]);
       else q.inner_rm(r, ib);
       st |= q.stb;
 #pragma unroll
@@ -419,8 +441,8 @@ __global__ __launch_bounds__(256) void map_nested_apply_kernel(NestedApplyPlan p
         if ((unsigned)j == a / 64 && (unsigned long long)lane == a % 64 && c[j] < cnt) c[j] = cnt;
       map_apply_deferred(k);
     } else if (kind == 1) {  // ---- Op::Rm -> apply_keyset_rm
-      const unsigned rr = p.clk_row[o];
-      const u64 kb = p.key_off[o], ke = p.key_off[o + 1];
+      const unsigned rr = CRDT_MNA_HDR ? rl32(h_rr, hi) : p.clk_row[o];
+      const u64 kb = CRDT_MNA_HDR ? rl64(h_kb, hi) : p.key_off[o], ke = CRDT_MNA_HDR ? rl64(h_ke, hi) : p.key_off[o + 1];
       if (rr >= p.n_clk_rows || ke < kb || ke > p.n_keys) {
         st |= 2u;
         continue;
@@ -464,6 +486,7 @@ __global__ __launch_bounds__(256) void map_nested_apply_kernel(NestedApplyPlan p
     } else {
       st |= 2u;
     }
+  }
   }
 #pragma unroll
   for (int j = 0; j < APL; ++j)
