@@ -23,14 +23,15 @@ namespace crdt {
 
 // waves per SIMD asked of the register allocator for A <= 128 (build option; A/B in
 // profiles/r05_vapply_wpe_ab.log); the wider instances keep the compiler's choice (they would spill)
-// op headers batched 64 at a time into lanes and read by v_readlane (build option, off: at the
-// kernel's 8 waves per SIMD it measured 2.30 vs 2.18 ms, profiles/r05_vapply_hdr_ab.log; the
-// Orswot-valued kernel, at 5 waves, gains from it and has it on)
+// op headers batched 64 at a time into lanes and read by v_readlane (build option; 0 = one global
+// read of each field per op).  With it the kernel runs at 7 waves per SIMD (room for the batch's
+// registers): 1.89 ms against 2.17 ms for per-op reads at 8 and 2.30 ms for the batch at 8
+// (profiles/r05_vapply_hdr_ab.log, r05_mca_h1w_ab.log)
 #ifndef CRDT_MCA_HDR
-#define CRDT_MCA_HDR 0
+#define CRDT_MCA_HDR 1
 #endif
 #ifndef CRDT_MCA_WPE
-#define CRDT_MCA_WPE 8
+#define CRDT_MCA_WPE 7
 #endif
 
 struct MapCounterApplyPlan {
