@@ -22,8 +22,10 @@ namespace crdt {
 #ifndef CRDT_MOA_HDR
 #define CRDT_MOA_HDR 1
 #endif
+// waves per SIMD asked of the register allocator (build option): 5 with the header batch (6.10 vs
+// 6.31 ms at 6, profiles/r05_moa_w5_ab.log; 6 was the best before it, r05_vapply_wpe_ab.log)
 #ifndef CRDT_MOA_WPE
-#define CRDT_MOA_WPE 6
+#define CRDT_MOA_WPE 5
 #endif
 
 constexpr int kMoaVd = 16;    // nested deferred slots per key (crdt_map_orswot_out)
