@@ -54,6 +54,15 @@ struct NestedApplyPlan {
 // The rows of outer key k of state s, and the inner-Map operations on them.
 // op headers batched 64 at a time into lanes and read by v_readlane (build option; 0 = one global
 // read of each field per op)
+// waves per SIMD asked of the register allocator (build option; 0 = the compiler's choice, 4)
+#ifndef CRDT_MNA_WPE
+#define CRDT_MNA_WPE 0
+#endif
+#if CRDT_MNA_WPE > 0
+#define MNA_WPE_ATTR __attribute__((amdgpu_waves_per_eu(CRDT_MNA_WPE)))
+#else
+#define MNA_WPE_ATTR
+#endif
 #ifndef CRDT_MNA_HDR
 #define CRDT_MNA_HDR 1
 #endif
@@ -344,7 +353,7 @@ __device__ __forceinline__ NaKey<APL> na_key(const NestedApplyPlan &p, unsigned 
 }
 
 template <int APL>
-__global__ __launch_bounds__(256) void map_nested_apply_kernel(NestedApplyPlan p) {
+__global__ __launch_bounds__(256) MNA_WPE_ATTR void map_nested_apply_kernel(NestedApplyPlan p) {
   extern __shared__ u64 lds[];
   const int lane = (int)(threadIdx.x % kWave), wv = (int)(threadIdx.x / kWave);
   const unsigned long long s = (unsigned long long)blockIdx.x * p.wpb + wv;
