@@ -62,8 +62,14 @@ int crdt_ctx_set_stream(crdt_ctx *ctx, void *hip_stream);
 int crdt_ctx_synchronize(crdt_ctx *ctx);
 /* Text of the last failure on this ctx (static storage owned by ctx). ctx may be NULL. */
 const char *crdt_last_error(const crdt_ctx *ctx);
-/* Library version, e.g. "0.1.0"; and the gfx target the code objects were built for. */
+/* Library version, e.g. "0.6.0"; and the gfx target the code objects were built for. */
 const char *crdt_version(void);
+/* ABI revision of this header: bumped whenever a struct or signature changes incompatibly (round 5
+ * appended `size_t Dv` to crdt_map_orswot_batch: revision 5 -> 6).  A caller checks
+ * crdt_abi_version() == CRDT_ABI_VERSION of the header it was built against before any other call,
+ * so a mismatched library fails clearly instead of reading a shorter struct. */
+#define CRDT_ABI_VERSION 6
+int crdt_abi_version(void);
 const char *crdt_build_target(void);
 
 /* Per-kernel timing with HIP events recorded on the ctx stream around the DOMINANT kernel of

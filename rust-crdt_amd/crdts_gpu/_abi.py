@@ -20,6 +20,7 @@ CRDT_ECOMM = -5
 CRDT_UNIQUE_ID_BYTES = 128
 CRDT_ACCUMULATE = 0x1
 CRDT_MEM_DEVICE = 0
+CRDT_ABI_VERSION = 6  # include/crdt_gpu.h
 CRDT_MEM_HOST = 1
 CRDT_KIND = {"vclock": 1, "gcounter": 2, "pncounter": 3, "gset": 4}
 CRDT_RED_MAX, CRDT_RED_MIN, CRDT_RED_SUM = 0, 1, 2
@@ -27,7 +28,7 @@ CRDT_RED_MAX, CRDT_RED_MIN, CRDT_RED_SUM = 0, 1, 2
 # Every symbol declared in include/crdt_gpu.h (checked by tests/test_abi.py).
 EXPORTS = (
     "crdt_ctx_create", "crdt_ctx_destroy", "crdt_ctx_set_stream", "crdt_ctx_synchronize",
-    "crdt_last_error", "crdt_version", "crdt_build_target", "crdt_ctx_set_timing",
+    "crdt_last_error", "crdt_version", "crdt_abi_version", "crdt_build_target", "crdt_ctx_set_timing",
     "crdt_ctx_timing", "crdt_ctx_timing_reset", "crdt_ctx_tune",
     "crdt_vclock_lub_many", "crdt_vclock_merge_batch",
     "crdt_gcounter_lub_many", "crdt_gcounter_merge_batch",
@@ -257,6 +258,7 @@ _SIGS = {
     "crdt_ctx_synchronize": ([P], ctypes.c_int),
     "crdt_last_error": ([P], ctypes.c_char_p),
     "crdt_version": ([], ctypes.c_char_p),
+    "crdt_abi_version": ([], ctypes.c_int),
     "crdt_build_target": ([], ctypes.c_char_p),
     "crdt_ctx_set_timing": ([P, ctypes.c_int], ctypes.c_int),
     "crdt_ctx_timing": ([P, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(U64)], ctypes.c_int),
@@ -385,6 +387,9 @@ def load():
         fn = getattr(lib, name)
         fn.argtypes = argtypes
         fn.restype = restype
+    if lib.crdt_abi_version() != CRDT_ABI_VERSION:  # a library built from another header revision
+        raise CrdtGpuUnavailable(f"{LIB_PATH}: ABI revision {lib.crdt_abi_version()}, these bindings expect "
+                                 f"{CRDT_ABI_VERSION} (include/crdt_gpu.h CRDT_ABI_VERSION)")
     _lib = lib
     return lib
 

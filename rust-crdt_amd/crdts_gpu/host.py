@@ -376,14 +376,14 @@ def map_orswot_lub_many(clock, ec, oc, ent, vd_off, vd_clock=None, vd_mem=None, 
     c, e, o_, m = (np.ascontiguousarray(_u64(x, n)) for x, n in ((clock, "clock"), (ec, "ec"), (oc, "oc"), (ent, "ent")))
     R, A = c.shape
     K, M = e.shape[1], m.shape[2]
-    vo = np.ascontiguousarray(_u64(vd_off, "vd_off"))
+    vo = np.ascontiguousarray(_u64(vd_off, "vd_off")) if vd_off is not None else None  # (None: R == 0 only)
     Dv = int(vd_clock.shape[0]) if vd_clock is not None else 0
     vc = np.ascontiguousarray(_u64(vd_clock, "vd_clock")) if Dv else None
     vm = np.ascontiguousarray(_u64(vd_mem, "vd_mem")) if Dv else None
     b = _abi.MapOrswotBatch()
     b.G, b.R, b.K, b.M, b.A = 1, R, K, M, A
     b.clock, b.ec, b.oc, b.ent = (x.ctypes.data for x in (c, e, o_, m))
-    b.vd_off, b.Dv = vo.ctypes.data, Dv
+    b.vd_off, b.Dv = (vo.ctypes.data if vo is not None else None), Dv
     if Dv:
         b.vd_clock, b.vd_mem = vc.ctypes.data, vm.ctypes.data
     keep = [c, e, o_, m, vo, vc, vm]
@@ -409,8 +409,9 @@ def map_nested_lub_many(clock, ec, ic, iec, ivc, ivv, id_off, id_clock=None, id_
     ivc (R, K, K2, V, A), ivv (R, K, K2, V), the inner removes as a CSR over (r, k)."""
     ctx = ctx or HostContext.default()
     arrs = [np.ascontiguousarray(_u64(x, n)) for x, n in ((clock, "clock"), (ec, "ec"), (ic, "ic"), (iec, "iec"),
-                                                          (ivc, "ivc"), (ivv, "ivv"), (id_off, "id_off"))]
-    c, e, i_, ie, vc, vv, io = arrs
+                                                          (ivc, "ivc"), (ivv, "ivv"))]
+    c, e, i_, ie, vc, vv = arrs
+    io = np.ascontiguousarray(_u64(id_off, "id_off")) if id_off is not None else None  # (None: R == 0 only)
     R, A = c.shape
     K, K2, V = e.shape[1], ie.shape[2], vc.shape[3]
     Di = int(id_clock.shape[0]) if id_clock is not None else 0
@@ -419,10 +420,10 @@ def map_nested_lub_many(clock, ec, ic, iec, ivc, ivv, id_off, id_clock=None, id_
     b = _abi.MapNestedBatch()
     b.G, b.R, b.K, b.K2, b.V, b.A = 1, R, K, K2, V, A
     b.clock, b.ec, b.ic, b.iec, b.ivc, b.ivv = (x.ctypes.data for x in (c, e, i_, ie, vc, vv))
-    b.id_off, b.Di = io.ctypes.data, Di
+    b.id_off, b.Di = (io.ctypes.data if io is not None else None), Di
     if Di:
         b.id_clock, b.id_keys = idc.ctypes.data, idk.ctypes.data
-    keep = arrs + [idc, idk]
+    keep = arrs + [io, idc, idk]
     D = _def_pool(b, def_off, def_row, def_clock, def_keys, keep)
     Kw = (K + 63) // 64
     out = dict(clock=np.zeros((1, A), np.uint64), ec=np.zeros((1, K, A), np.uint64), ic=np.zeros((1, K, A), np.uint64),

@@ -868,6 +868,32 @@ def encode_counter_ops(streams, A: int, device) -> MapCounterOpBatch:
         torch.tensor(keys if keys else [0], dtype=torch.int32, device=device))
 
 
+_I64 = (torch.int64,)
+_I32 = (torch.int32,)
+_U8 = (torch.uint8,)
+
+
+def _check_op_fields(ctx: Context, ops, n: int, fields, what: str) -> None:
+    """Every per-op field of an op batch: shape (n,), the dtype the header states, on the ctx's device,
+    contiguous.  The header-batched apply kernels load each field for every op index below n_ops, so a
+    shorter, wrongly typed or host-resident field would be read out of bounds on the device."""
+    for nm, dts in fields:
+        t = getattr(ops, nm)
+        ctx.check_tensor(t, f"{what}({nm})", dts)
+        if tuple(t.shape) != (n,) or not t.is_contiguous():
+            raise ValueError(f"{what}: {nm} must be a contiguous ({n},) tensor, got {tuple(t.shape)}")
+
+
+def _check_op_pools(ctx: Context, ops, pools, what: str) -> None:
+    """The pooled arrays (offsets, key / member lists, clock rows): dtype, device, contiguity; their
+    lengths are what the kernels bound every offset by."""
+    for nm, dts in pools:
+        t = getattr(ops, nm)
+        ctx.check_tensor(t, f"{what}({nm})", dts)
+        if not t.is_contiguous():
+            raise ValueError(f"{what}: {nm} must be contiguous")
+
+
 def counter_apply_batch(clock: torch.Tensor, ec: torch.Tensor, val: torch.Tensor, def_clock: torch.Tensor,
                         def_keys: torch.Tensor, def_count: torch.Tensor, ops: MapCounterOpBatch,
                         ctx: Optional[Context] = None) -> torch.Tensor:
@@ -891,6 +917,10 @@ def counter_apply_batch(clock: torch.Tensor, ec: torch.Tensor, val: torch.Tensor
     n = ops.kind.shape[0]
     if ops.op_off.shape[0] != N + 1 or ops.key_off.shape[0] != n + 1 or ops.clk_pool.shape[1] != A:
         raise ValueError("map.counter_apply_batch: op_off (N+1), key_off (n_ops+1), clk_pool (n, A) expected")
+    what = "map.counter_apply_batch"
+    _check_op_fields(ctx, ops, n, (("kind", _U8), ("actor", _I32), ("counter", _I64), ("key", _I32),
+                                   ("vactor", _I32), ("vcounter", _I64), ("vdir", _U8), ("clk_row", _I32)), what)
+    _check_op_pools(ctx, ops, (("op_off", _I64), ("key_off", _I64), ("keys", _I32), ("clk_pool", _I64)), what)
     st = _abi.MapCounterStates()
     st.N, st.K, st.A, st.W = N, K, A, W
     st.clock, st.clock_stride, st.ec, st.ec_stride = clock.data_ptr(), A, ec.data_ptr(), K * A
@@ -900,7 +930,8 @@ def counter_apply_batch(clock: torch.Tensor, ec: torch.Tensor, val: torch.Tensor
     o.actor, o.counter, o.key = ops.actor.data_ptr(), ops.counter.data_ptr(), ops.key.data_ptr()
     o.vactor, o.vcounter, o.vdir = ops.vactor.data_ptr(), ops.vcounter.data_ptr(), ops.vdir.data_ptr()
     o.clk_row, o.clk_pool, o.n_clk_rows = ops.clk_row.data_ptr(), ops.clk_pool.data_ptr(), ops.clk_pool.shape[0]
-    o.key_off, o.keys, o.n_keys = ops.key_off.data_ptr(), ops.keys.data_ptr(), int(ops.key_off[-1].item())
+    # the pool lengths, not the (untrusted) last offsets: the kernel flags an offset past them (status bit 1)
+    o.key_off, o.keys, o.n_keys = ops.key_off.data_ptr(), ops.keys.data_ptr(), ops.keys.shape[0]
     status = torch.empty(N, dtype=torch.int32, device=clock.device)
     ctx.call("crdt_map_counter_apply_batch", ctypes.byref(st), def_clock.data_ptr(), def_keys.data_ptr(),
              def_count.data_ptr(), Dcap, ctypes.byref(o), status.data_ptr())
@@ -996,6 +1027,11 @@ def orswot_apply_batch(res: "MapOrswotLub", def_clock: torch.Tensor, def_keys: t
     if (ops.op_off.shape[0] != N + 1 or ops.key_off.shape[0] != n + 1 or ops.mem_off.shape[0] != n + 1
             or ops.clk_pool.shape[1] != A):
         raise ValueError("map.orswot_apply_batch: op_off (N+1), key_off / mem_off (n_ops+1), clk_pool (n, A) expected")
+    what = "map.orswot_apply_batch"
+    _check_op_fields(ctx, ops, n, (("kind", _U8), ("actor", _I32), ("counter", _I64), ("key", _I32),
+                                   ("vkind", _U8), ("vactor", _I32), ("vcounter", _I64), ("clk_row", _I32)), what)
+    _check_op_pools(ctx, ops, (("op_off", _I64), ("key_off", _I64), ("keys", _I32), ("mem_off", _I64),
+                               ("mems", _I32), ("clk_pool", _I64)), what)
     st = _abi.MapOrswotStates()
     st.N, st.K, st.M, st.A = N, K, M, A
     st.clock, st.ec, st.oc, st.ent = clock.data_ptr(), ec.data_ptr(), oc.data_ptr(), ent.data_ptr()
@@ -1005,8 +1041,9 @@ def orswot_apply_batch(res: "MapOrswotLub", def_clock: torch.Tensor, def_keys: t
     o.actor, o.counter, o.key = ops.actor.data_ptr(), ops.counter.data_ptr(), ops.key.data_ptr()
     o.vkind, o.vactor, o.vcounter = ops.vkind.data_ptr(), ops.vactor.data_ptr(), ops.vcounter.data_ptr()
     o.clk_row, o.clk_pool, o.n_clk_rows = ops.clk_row.data_ptr(), ops.clk_pool.data_ptr(), ops.clk_pool.shape[0]
-    o.key_off, o.keys, o.n_keys = ops.key_off.data_ptr(), ops.keys.data_ptr(), int(ops.key_off[-1].item())
-    o.mem_off, o.mems, o.n_mems = ops.mem_off.data_ptr(), ops.mems.data_ptr(), int(ops.mem_off[-1].item())
+    # the pool lengths, not the (untrusted) last offsets: the kernel flags an offset past them (status bit 1)
+    o.key_off, o.keys, o.n_keys = ops.key_off.data_ptr(), ops.keys.data_ptr(), ops.keys.shape[0]
+    o.mem_off, o.mems, o.n_mems = ops.mem_off.data_ptr(), ops.mems.data_ptr(), ops.mems.shape[0]
     status = torch.empty(N, dtype=torch.int32, device=clock.device)
     ctx.call("crdt_map_orswot_apply_batch", ctypes.byref(st), def_clock.data_ptr(), def_keys.data_ptr(),
              def_count.data_ptr(), Dcap, ctypes.byref(o), status.data_ptr())
@@ -1115,6 +1152,11 @@ def nested_apply_batch(res: "MapNestedLub", def_clock: torch.Tensor, def_keys: t
     n = ops.kind.shape[0]
     if ops.op_off.shape[0] != N + 1 or ops.key_off.shape[0] != n + 1 or ops.clk_pool.shape[1] != A:
         raise ValueError("map.nested_apply_batch: op_off (N+1), key_off (n_ops+1), clk_pool (n, A) expected")
+    what = "map.nested_apply_batch"
+    _check_op_fields(ctx, ops, n, (("kind", _U8), ("actor", _I32), ("counter", _I64), ("key", _I32),
+                                   ("ikind", _U8), ("iactor", _I32), ("icounter", _I64), ("ikey", _I32),
+                                   ("val", _I64), ("ikeys", _I64), ("clk_row", _I32)), what)
+    _check_op_pools(ctx, ops, (("op_off", _I64), ("key_off", _I64), ("keys", _I32), ("clk_pool", _I64)), what)
     o = _abi.MapNestedOps()
     o.n_ops, o.op_off = n, ops.op_off.data_ptr()
     for nm in ("kind", "actor", "counter", "key", "ikind", "iactor", "icounter", "ikey", "val", "ikeys", "clk_row",

@@ -373,6 +373,11 @@ static int h2d_async(crdt_ctx *ctx, void *dst, const void *src, size_t bytes) {
   STAGE_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
   return CRDT_OK;
 }
+static int zero_async(crdt_ctx *ctx, void *dst, size_t bytes) {
+  if (!bytes) return CRDT_OK;
+  STAGE_HIP(hipMemsetAsync(dst, 0, bytes, ctx->stream));
+  return CRDT_OK;
+}
 static int d2h_async(crdt_ctx *ctx, void *dst, const void *src, size_t bytes) {
   if (!bytes || !dst) return CRDT_OK;
   STAGE_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
@@ -1063,7 +1068,8 @@ static int map_orswot_lub_host_body(crdt_ctx *ctx, const crdt_map_orswot_batch *
   if (int rc = h2d_async(ctx, e, in->ec, N * A * 8)) return rc;
   if (int rc = h2d_async(ctx, o, in->oc, N * A * 8)) return rc;
   if (int rc = h2d_async(ctx, m, in->ent, N * M * A * 8)) return rc;
-  if (int rc = h2d_async(ctx, vo, in->vd_off, (N + 1) * 8)) return rc;
+  // (vd_off may be NULL when R == 0, as on the device path: the one offset word is then 0)
+  if (int rc = in->vd_off ? h2d_async(ctx, vo, in->vd_off, (N + 1) * 8) : zero_async(ctx, vo, (N + 1) * 8)) return rc;
   if (int rc = h2d_async(ctx, vc, in->vd_clock, Dv * A * 8)) return rc;
   if (int rc = h2d_async(ctx, vm, in->vd_mem, Dv * Mw * 8)) return rc;
   if (int rc = h2d_async(ctx, dr, in->def_row, D * 4)) return rc;
@@ -1166,7 +1172,8 @@ static int map_nested_lub_host_body(crdt_ctx *ctx, const crdt_map_nested_batch *
   if (int rc = h2d_async(ctx, iec, in->iec, N * K2 * A * 8)) return rc;
   if (int rc = h2d_async(ctx, ivc, in->ivc, N * K2 * V * A * 8)) return rc;
   if (int rc = h2d_async(ctx, ivv, in->ivv, N * K2 * V * 8)) return rc;
-  if (int rc = h2d_async(ctx, io, in->id_off, (N + 1) * 8)) return rc;
+  // (id_off may be NULL when R == 0, as on the device path: the one offset word is then 0)
+  if (int rc = in->id_off ? h2d_async(ctx, io, in->id_off, (N + 1) * 8) : zero_async(ctx, io, (N + 1) * 8)) return rc;
   if (int rc = h2d_async(ctx, idc, in->id_clock, Di * A * 8)) return rc;
   if (int rc = h2d_async(ctx, idk, in->id_keys, Di * 8)) return rc;
   if (int rc = h2d_async(ctx, dr, in->def_row, D * 4)) return rc;

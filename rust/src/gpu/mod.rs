@@ -74,6 +74,14 @@ pub struct GpuCtx {
 impl GpuCtx {
     /// `crdt_ctx_create(device)`.
     pub fn new(device: i32) -> Result<Self, GpuError> {
+        // a library built from another header revision reads these structs differently
+        let abi = unsafe { ffi::crdt_abi_version() };
+        if abi != ffi::CRDT_ABI_VERSION {
+            return Err(GpuError {
+                code: ffi::CRDT_EUNSUPPORTED,
+                msg: format!("libcrdt_gpu ABI revision {}, this binding expects {}", abi, ffi::CRDT_ABI_VERSION),
+            });
+        }
         let mut raw = ptr::null_mut();
         let rc = unsafe { ffi::crdt_ctx_create(device, &mut raw) };
         if rc != ffi::CRDT_OK {

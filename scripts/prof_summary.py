@@ -89,11 +89,15 @@ for b, blk in blocks.items():
 json.dump(summary, open(os.path.join(P, f"{tag}_pmc_summary.json"), "w"), indent=1)
 # the bench line's roofline.traffic: this checkpoint's measurement per block, tied to the kernel
 # source it was measured on (bench.py reports null when the source no longer matches)
-traffic = {}
+# (merged into the existing file: a run of some blocks keeps the other blocks' entries)
+try:
+    traffic = json.load(open(os.path.join(P, "pmc_traffic.json")))
+except (OSError, ValueError):
+    traffic = {}
 for b, s in summary.items():
     if "hbm_bytes_per_launch" in s:
         traffic[b] = {"workload": s["workload"], "kernel": s["kernel"], "hbm_bytes_per_launch": s["hbm_bytes_per_launch"],
                       "source": f"profiles/{tag}_pmc_summary.json", "kernel_source_sha256": s["kernel_source_sha256"]}
-if traffic:
+if any("hbm_bytes_per_launch" in s for s in summary.values()):
     json.dump(traffic, open(os.path.join(P, "pmc_traffic.json"), "w"), indent=1)
 print(json.dumps(summary, indent=1))

@@ -395,3 +395,15 @@ def test_map_nested_host_lub_many(hctx):
                                 out["ivv"][0], out["nval"][0], idef, [(np.array(rm, np.uint64), ks) for rm, ks in dset])
     from test_gpu_map_nested import canon
     assert canon(got) == canon(exp)
+
+
+def test_map_value_host_lub_many_empty_batch(hctx):
+    """R == 0 from host memory with a NULL vd_off / id_off, as the device path accepts:
+    the empty fold Map::new(), no copy from NULL."""
+    z = lambda *s: np.zeros(s, np.uint64)  # noqa: E731
+    K, M, A, K2, V = 3, 5, 4, 2, 2
+    out = host.map_orswot_lub_many(z(0, A), z(0, K, A), z(0, K, A), z(0, K, M, A), None, ctx=hctx)
+    assert int(out["flags"][0]) == 0 and not out["clock"].any() and not out["ec"].any() and not out["vd_n"].any()
+    out = host.map_nested_lub_many(z(0, A), z(0, K, A), z(0, K, A), z(0, K, K2, A), z(0, K, K2, V, A),
+                                   z(0, K, K2, V), None, ctx=hctx)
+    assert int(out["flags"][0]) == 0 and not out["clock"].any() and not out["nval"].any()

@@ -146,3 +146,29 @@ def test_map_counter_apply_unapplied_input_deferred(gpu_ctx, W):
         dfr = [(hdc[n, i], O.bitmap_members(hdk[n, i])) for i in range(int(hcnt[n]))]
         assert O.dense_to_map_counter(c[n], e[n], v[n], dfr) == exp, n
     assert ups > 0
+
+
+def test_map_counter_apply_offsets_past_the_key_pool(gpu_ctx):
+    """A key_off whose last entry claims more keys than the pool holds: the bound is the
+    pool's length, so the op is flagged (status bit 1) and skipped instead of read past the buffer;
+    wrongly typed / short / host-resident op fields are refused on the host."""
+    K, A, W, N, Dcap = 4, 4, 1, 2, 2
+    streams = [[("rm", {0: 3}, [1])], [("up", 0, 1, 0, 0, 1, 0)]]
+    ops = cg.map.encode_counter_ops(streams, A, "cuda:0")
+    bad_off = ops.key_off.clone()
+    bad_off[1:] = 1 << 20  # op 0 claims a million keys
+    bad = ops._replace(key_off=bad_off)
+    mk = lambda *s: torch.zeros(s, dtype=torch.int64, device="cuda:0")  # noqa: E731
+    clock, ec, val, dc, dk = mk(N, A), mk(N, K, A), mk(N, K, W, A), mk(N, Dcap, A), mk(N, Dcap, 1)
+    cnt = torch.zeros(N, dtype=torch.int32, device="cuda:0")
+    st = cg.map.counter_apply_batch(clock, ec, val, dc, dk, cnt, bad, ctx=gpu_ctx).cpu().numpy()
+    torch.cuda.synchronize()
+    assert st[0] & 2 and st[1] == 0
+    assert int(cnt[0]) == 0 and to_host(ec)[1, 0, 0] == 1
+    with pytest.raises(TypeError):
+        cg.map.counter_apply_batch(clock, ec, val, dc, dk, cnt, ops._replace(counter=ops.counter.to(torch.int32)),
+                                   ctx=gpu_ctx)
+    with pytest.raises(ValueError):
+        cg.map.counter_apply_batch(clock, ec, val, dc, dk, cnt, ops._replace(key=ops.key[:0]), ctx=gpu_ctx)
+    with pytest.raises(ValueError):
+        cg.map.counter_apply_batch(clock, ec, val, dc, dk, cnt, ops._replace(vdir=ops.vdir.cpu()), ctx=gpu_ctx)

@@ -167,3 +167,26 @@ def test_map_orswot_apply_unapplied_input_deferred(gpu_ctx):
         dfr = [(hdc[n, i], O.bitmap_members(hdk[n, i])) for i in range(int(hcnt[n]))]
         got = O.dense_to_map_orswot(c[n], e[n], o[n], m[n], vd, dfr)
         assert got.clock == exps[n].clock and got.entries == exps[n].entries and got.deferred == exps[n].deferred, n
+
+
+def test_map_orswot_apply_offsets_past_the_pools(gpu_ctx):
+    """mem_off / key_off claiming more entries than the pools hold: the pools' lengths
+    bound them, so the ops are flagged (status bit 1) and skipped instead of read past the buffers."""
+    N, K, M, A, Dcap = 3, 4, 5, 5, 4
+    maps = O.map_orswot_objects(N, K, M, A, seed=62, steps=40, p_vrm=0.0)
+    res, _, _ = _states(gpu_ctx, maps, K, M, A)
+    streams = [[("add", 0, 999, 1, 0, 999, [2])], [("rm", {0: 1}, [0])], [("add", 1, 999, 2, 1, 999, [3])]]
+    ops = cg.map.encode_orswot_map_ops(streams, A, "cuda:0")
+    mo, ko = ops.mem_off.clone(), ops.key_off.clone()
+    mo[1:] = 1 << 20    # op 0 (state 0) claims a million members; op 2 starts past the pool too
+    ko[2:] = 1 << 20    # op 1 (state 1) claims a million keys
+    bad = ops._replace(mem_off=mo, key_off=ko)
+    Kw = (K + 63) // 64
+    z = lambda *s: torch.zeros(s, dtype=torch.int64, device="cuda:0")  # noqa: E731
+    st = cg.map.orswot_apply_batch(res, z(N, Dcap, A), z(N, Dcap, Kw),
+                                   torch.zeros(N, dtype=torch.int32, device="cuda:0"), bad, ctx=gpu_ctx).cpu().numpy()
+    torch.cuda.synchronize()
+    assert st[0] & 2 and st[1] & 2 and st[2] & 2, st
+    with pytest.raises(TypeError):
+        cg.map.orswot_apply_batch(res, z(N, Dcap, A), z(N, Dcap, Kw), torch.zeros(N, dtype=torch.int32, device="cuda:0"),
+                                  ops._replace(vcounter=ops.vcounter.to(torch.int32)), ctx=gpu_ctx)
