@@ -92,6 +92,10 @@ def parse():
     ap.add_argument("--parity-keys", type=int, default=16)
     ap.add_argument("--c3-cpu-replicas", type=int, default=1024, help="replicas of the c3 CPU baseline sample")
     ap.add_argument("--c4-cpu-replicas", type=int, default=4096, help="replicas of the c4 CPU baseline sample")
+    ap.add_argument("--c3-cpu-replicas-per-thread", type=int, default=256,
+                    help="replicas per host thread of the c3 multi-core CPU baseline")
+    ap.add_argument("--c4-cpu-mt-replicas", type=int, default=8192,
+                    help="replicas of the c4 multi-core CPU baseline (key ranges per thread)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="PMC-derived HBM bytes per launch (written by profiles/collect.sh)")
     return ap.parse_args()
@@ -492,10 +496,25 @@ def c3_oracle_leg(args, inp, res, ctx):
     d_off = off[:Rc + 1].astype(np.uint64)
     _, _, _, fold_s = O.orswot_fold(c_h, e_h, d_off, dcl_h[:dend], dmem_h[:dend])
     del e_h
-    base = {"value": Rc / fold_s, "unit": "replica-merges/s", "cores": 1, "kind": "port",
-            "sample": (f"first {Rc} of the {R} replicas (all {M} members x {A} actors, their {dend} deferred "
-                       f"removes), left fold of the restated Orswot::merge over std::unordered_map / std::map "
-                       f"states (oracle/ref_fold.cpp), 1 thread, ingest excluded; {fold_s:.2f} s of fold")}
+    one = {"value": Rc / fold_s, "unit": "replica-merges/s", "cores": 1, "kind": "port",
+           "sample": (f"first {Rc} of the {R} replicas (all {M} members x {A} actors, their {dend} deferred "
+                      f"removes), left fold of the restated Orswot::merge over std::unordered_map / std::map "
+                      f"states (oracle/ref_fold.cpp), 1 thread, ingest excluded; {fold_s:.2f} s of fold")}
+    # the same fold over the host's threads (SURVEY §8d CPU timing (2)): replica ranges per thread, the
+    # partial states merged in order (oracle_orswot_fold_mt; tests/test_oracle_mt.py: same result)
+    T = cpu_threads()
+    Rm = min(R, args.c3_cpu_replicas_per_thread * T)
+    dm = int(off[Rm])
+    e_h = u64(inp.entries[:Rm])
+    _, _, _, mt_s = O.orswot_fold(u64(inp.clock[:Rm]), e_h, off[:Rm + 1].astype(np.uint64), dcl_h[:dm], dmem_h[:dm],
+                                  threads=T)
+    del e_h
+    base = {"value": Rm / mt_s, "unit": "replica-merges/s", "cores": T, "kind": "port",
+            "sample": (f"subsample: first {Rm} of the {R} replicas (all {M} members x {A} actors, their {dm} deferred "
+                       f"removes), the restated Orswot::merge over std::unordered_map / std::map states "
+                       f"(oracle/ref_fold.cpp oracle_orswot_fold_mt) split over {T} threads by replica ranges + the "
+                       f"final merge of the {T} partial states, ingest excluded; {mt_s:.2f} s of fold"),
+            "single_core": one}
     return parity, base
 
 
@@ -541,10 +560,25 @@ def c4_oracle_leg(args, inp, res, ctx):
     sel = rows < Rc
     e_h = [u64(t[:Rc]) for t in (inp.clock, inp.ec, inp.vclk, inp.vval)]
     fold_s = O.map_fold(*e_h, rows[sel], dcl_h[sel], dks_h[sel], vout)[6]
-    base = {"value": Rc / fold_s, "unit": "replica-merges/s", "cores": 1, "kind": "port",
-            "sample": (f"first {Rc} of the {R} replicas (all {K} keys, {int(sel.sum())} deferred removes), left "
-                       f"fold of the restated Map::merge over std::map states (oracle/ref_fold.cpp), 1 thread, "
-                       f"ingest excluded; {fold_s:.2f} s of fold")}
+    del e_h
+    one = {"value": Rc / fold_s, "unit": "replica-merges/s", "cores": 1, "kind": "port",
+           "sample": (f"first {Rc} of the {R} replicas (all {K} keys, {int(sel.sum())} deferred removes), left "
+                      f"fold of the restated Map::merge over std::map states (oracle/ref_fold.cpp), 1 thread, "
+                      f"ingest excluded; {fold_s:.2f} s of fold")}
+    # the same fold over the host's threads: KEY ranges per thread over every replica of the sample (the
+    # Map fold is not associative, so not replica ranges; keys are independent given the clocks and the
+    # removes — oracle_map_fold_mt, tests/test_oracle_mt.py: same result)
+    T = cpu_threads()
+    Rm = min(R, args.c4_cpu_mt_replicas)
+    sel = rows < Rm
+    e_h = [u64(t[:Rm]) for t in (inp.clock, inp.ec, inp.vclk, inp.vval)]
+    mt_s = O.map_fold(*e_h, rows[sel], dcl_h[sel], dks_h[sel], vout, threads=T)[6]
+    del e_h
+    base = {"value": Rm / mt_s, "unit": "replica-merges/s", "cores": T, "kind": "port",
+            "sample": (f"subsample: first {Rm} of the {R} replicas (all {K} keys, {int(sel.sum())} deferred removes), "
+                       f"the restated Map::merge left fold over std::map states (oracle/ref_fold.cpp "
+                       f"oracle_map_fold_mt) split over {T} threads by key ranges, ingest excluded; {mt_s:.2f} s of fold"),
+            "single_core": one}
     return parity, base
 
 

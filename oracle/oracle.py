@@ -768,6 +768,12 @@ def lib():
         L.oracle_counter_fold_mt.restype = ctypes.c_double
         L.oracle_dense_max_mt.argtypes = [P, S, S, S, ctypes.c_int, P]
         L.oracle_dense_max_mt.restype = ctypes.c_double
+        I = ctypes.c_int
+        L.oracle_orswot_fold_mt.argtypes = [P, P, S, S, S, P, P, P, I, P, P, P, P, S, ctypes.POINTER(S)]
+        L.oracle_orswot_fold_mt.restype = ctypes.c_double
+        L.oracle_map_fold_mt.argtypes = [P, P, P, P, S, S, S, S, P, P, P, S, I, P, P, P, P, P, P, P, S,
+                                         ctypes.POINTER(S)]
+        L.oracle_map_fold_mt.restype = ctypes.c_double
         _LIB = L
     return _LIB
 
@@ -839,12 +845,14 @@ def vclock_merge_pairs(self_rows: np.ndarray, other_rows: np.ndarray) -> np.ndar
 
 
 def orswot_fold(clock: np.ndarray, entries: np.ndarray, def_off=None, def_clock=None,
-                def_members=None):
+                def_members=None, threads: Optional[int] = None):
     """Fold of Orswot::merge from new() over dense replicas.
 
     clock (R, A), entries (R, M, A); deferred pooled per replica as CSR def_off (R+1,),
     def_clock (D, A), def_members (D, Mw).  Returns (clock (A,), entries (M, A),
-    deferred: set of (tuple rm clock, frozenset members), seconds).
+    deferred: set of (tuple rm clock, frozenset members), seconds).  `threads`: the multi-core
+    baseline (ref_fold.cpp oracle_orswot_fold_mt: replica ranges folded per thread, the partial
+    states then merged in order; same result).
     """
     clock, entries = _c64(clock), _c64(entries)
     R, M, A = entries.shape
@@ -863,9 +871,14 @@ def orswot_fold(clock: np.ndarray, entries: np.ndarray, def_off=None, def_clock=
     odc = np.zeros((maxd, A), dtype=np.uint64)
     odm = np.zeros((maxd, Mw), dtype=np.uint64)
     nd = ctypes.c_size_t(0)
-    t = lib().oracle_orswot_fold(_p(clock), _p(entries), R, M, A, _p(def_off), _p(def_clock),
-                                 _p(def_members), _p(oc), _p(oe), _p(odc), _p(odm), maxd,
-                                 ctypes.byref(nd))
+    if threads is None:
+        t = lib().oracle_orswot_fold(_p(clock), _p(entries), R, M, A, _p(def_off), _p(def_clock),
+                                     _p(def_members), _p(oc), _p(oe), _p(odc), _p(odm), maxd,
+                                     ctypes.byref(nd))
+    else:
+        t = lib().oracle_orswot_fold_mt(_p(clock), _p(entries), R, M, A, _p(def_off), _p(def_clock),
+                                        _p(def_members), int(threads), _p(oc), _p(oe), _p(odc), _p(odm), maxd,
+                                        ctypes.byref(nd))
     n = nd.value
     assert n <= maxd
     deferred = set()
@@ -1244,10 +1257,11 @@ def dense_map_fold(clock, ec, vclk, vval, def_row, def_clock, def_keys, Vout: in
 
 
 def map_fold(clock, ec, vclk, vval, def_row=None, def_clock=None, def_keys=None, Vout: int = 4,
-             peak: Optional[np.ndarray] = None):
+             peak: Optional[np.ndarray] = None, threads: Optional[int] = None):
     """C++ twin (ref_fold.cpp oracle_map_fold): the reference fold over map-based states.
     Returns (clock, ec, vclk, vval, nval, deferred set, fold seconds); `peak` (K,) u64, if
-    given, receives the most values each key held after any step's entry join."""
+    given, receives the most values each key held after any step's entry join.  `threads`: the
+    multi-core baseline (oracle_map_fold_mt: key ranges per thread, every replica; same result)."""
     clock, ec, vclk, vval = _c64(clock), _c64(ec), _c64(vclk), _c64(vval)
     R, K, A = ec.shape
     V = vclk.shape[2]
@@ -1272,10 +1286,16 @@ def map_fold(clock, ec, vclk, vval, def_row=None, def_clock=None, def_keys=None,
     odc = np.zeros((maxd, A), np.uint64)
     odk = np.zeros((maxd, Kw), np.uint64)
     nd = ctypes.c_size_t(0)
-    t = lib().oracle_map_fold(_p(clock), _p(ec), _p(vclk), _p(vval), R, K, A, V, _p(def_off),
-                              _p(def_clock), _p(def_keys), Vout, _p(oc), _p(oe), _p(ovc), _p(ovv),
-                              _p(on), _p(odc), _p(odk), maxd, ctypes.byref(nd),
-                              _p(peak) if peak is not None else None)
+    if threads is None:
+        t = lib().oracle_map_fold(_p(clock), _p(ec), _p(vclk), _p(vval), R, K, A, V, _p(def_off),
+                                  _p(def_clock), _p(def_keys), Vout, _p(oc), _p(oe), _p(ovc), _p(ovv),
+                                  _p(on), _p(odc), _p(odk), maxd, ctypes.byref(nd),
+                                  _p(peak) if peak is not None else None)
+    else:
+        assert peak is None, "map_fold: peak is single-threaded instrumentation"
+        t = lib().oracle_map_fold_mt(_p(clock), _p(ec), _p(vclk), _p(vval), R, K, A, V, _p(def_off),
+                                     _p(def_clock), _p(def_keys), Vout, int(threads), _p(oc), _p(oe), _p(ovc),
+                                     _p(ovv), _p(on), _p(odc), _p(odk), maxd, ctypes.byref(nd))
     n = nd.value
     assert n <= maxd
     deferred = {(tuple(int(x) for x in odc[k]), bitmap_members(odk[k])) for k in range(n)}

@@ -667,4 +667,158 @@ double oracle_map_fold(const uint64_t *clock, const uint64_t *ec, const uint64_t
   return t1 - t0;
 }
 
+
+// ---- Multi-threaded CPU baselines (SURVEY §8d CPU timing (2), configs 3 and 4) ----------------
+// Orswot: thread t ingests and folds replicas [t*R/T, (t+1)*R/T) from Orswot::new(), then the T
+// partial states are merged in thread order (orswot.rs:81-149 is a join on the states a fold
+// produces: tests/test_oracle_twins.py checks tree == left fold, tests/test_oracle_mt.py this
+// split).  Timed: the parallel folds plus the final merges.  Output as oracle_orswot_fold.
+double oracle_orswot_fold_mt(const uint64_t *clock, const uint64_t *entries, size_t R, size_t M, size_t A,
+                             const uint64_t *def_off, const uint64_t *def_clock, const uint64_t *def_members,
+                             int threads, uint64_t *out_clock, uint64_t *out_entries, uint64_t *out_def_clock,
+                             uint64_t *out_def_members, size_t max_def, size_t *out_ndef) {
+  const size_t T = threads < 1 ? 1 : (size_t)threads, Mw = (M + 63) / 64;
+  std::vector<Orswot> part(T);
+  std::atomic<int> ready{0}, go{0};
+  std::vector<std::thread> pool;
+  for (size_t t = 0; t < T; ++t)
+    pool.emplace_back([&, t] {
+      const size_t lo = t * R / T, hi = (t + 1) * R / T;
+      std::vector<Orswot> reps(hi - lo);
+      for (size_t r = lo; r < hi; ++r) {  // ingest, as oracle_orswot_fold
+        Orswot &o = reps[r - lo];
+        o.clock = vclock_from_row(clock + r * A, A);
+        for (size_t m = 0; m < M; ++m) {
+          VClock e = vclock_from_row(entries + (r * M + m) * A, A);
+          if (!e.empty()) o.entries.emplace((Member)m, std::move(e));
+        }
+        if (def_off)
+          for (uint64_t d = def_off[r]; d < def_off[r + 1]; ++d) {
+            VClock rm = vclock_from_row(def_clock + d * A, A);
+            std::set<Member> mem;
+            for (size_t w = 0; w < Mw; ++w)
+              for (uint64_t x = def_members[d * Mw + w]; x; x &= x - 1) mem.insert((Member)(w * 64 + __builtin_ctzll(x)));
+            auto it = o.deferred.find(rm);
+            if (it != o.deferred.end()) it->second.insert(mem.begin(), mem.end());
+            else o.deferred.emplace(std::move(rm), std::move(mem));
+          }
+      }
+      ready.fetch_add(1);
+      while (!go.load(std::memory_order_acquire)) std::this_thread::yield();
+      for (auto &r : reps) part[t].merge(std::move(r));
+    });
+  while (ready.load() < (int)T) std::this_thread::yield();
+  const double t0 = now_s();
+  go.store(1, std::memory_order_release);
+  for (auto &th : pool) th.join();
+  Orswot acc = std::move(part[0]);
+  for (size_t t = 1; t < T; ++t) acc.merge(std::move(part[t]));
+  const double t1 = now_s();
+  vclock_to_row(acc.clock, out_clock, A);
+  std::memset(out_entries, 0, M * A * 8);
+  for (auto &kv : acc.entries) vclock_to_row(kv.second, out_entries + (size_t)kv.first * A, A);
+  size_t k = 0;
+  for (auto &kv : acc.deferred) {
+    if (k < max_def) {
+      vclock_to_row(kv.first, out_def_clock + k * A, A);
+      std::memset(out_def_members + k * Mw, 0, Mw * 8);
+      for (Member m : kv.second) out_def_members[k * Mw + m / 64] |= 1ull << (m % 64);
+    }
+    ++k;
+  }
+  *out_ndef = k;
+  return t1 - t0;
+}
+
+// Map<u32, MVReg<u64>>: the fold is not associative, so the threads split KEYS, not
+// replicas — keys are independent given the replica clocks and the deferred list (map.rs:140-220:
+// the entry loop is per key, the clock merge and the removes' survival see only clocks).  Thread t
+// folds every replica restricted to keys [t*K/T, (t+1)*K/T), with every deferred remove restricted
+// to those keys (possibly to none: its clock still joins acc.deferred as the reference's does).
+// Timed: the parallel folds.  Output as oracle_map_fold (the survivors' key sets are the union of
+// the threads' restrictions; every thread keeps the same surviving clocks).
+double oracle_map_fold_mt(const uint64_t *clock, const uint64_t *ec, const uint64_t *vclk, const uint64_t *vval,
+                          size_t R, size_t K, size_t A, size_t V, const uint64_t *def_off, const uint64_t *def_clock,
+                          const uint64_t *def_keys, size_t Vout, int threads, uint64_t *out_clock, uint64_t *out_ec,
+                          uint64_t *out_vclk, uint64_t *out_vval, uint64_t *out_nval, uint64_t *out_def_clock,
+                          uint64_t *out_def_keys, size_t max_def, size_t *out_ndef) {
+  const size_t T = threads < 1 ? 1 : (size_t)threads, Kw = (K + 63) / 64;
+  std::vector<MapMV> part(T);
+  std::atomic<int> ready{0}, go{0};
+  std::vector<std::thread> pool;
+  for (size_t t = 0; t < T; ++t)
+    pool.emplace_back([&, t] {
+      const size_t k0 = t * K / T, k1 = (t + 1) * K / T;
+      std::vector<MapMV> reps(R);
+      for (size_t r = 0; r < R; ++r) {  // ingest of the thread's keys, as oracle_map_fold
+        MapMV &m = reps[r];
+        m.clock = vclock_from_row(clock + r * A, A);
+        for (size_t k = k0; k < k1; ++k) {
+          VClock e = vclock_from_row(ec + (r * K + k) * A, A);
+          if (e.empty()) continue;
+          MapEntry ent;
+          ent.clock = std::move(e);
+          for (size_t s = 0; s < V; ++s) {
+            VClock c = vclock_from_row(vclk + ((r * K + k) * V + s) * A, A);
+            if (!c.empty()) ent.val.vals.emplace_back(std::move(c), vval[(r * K + k) * V + s]);
+          }
+          m.entries.emplace((uint32_t)k, std::move(ent));
+        }
+        if (def_off)
+          for (uint64_t d = def_off[r]; d < def_off[r + 1]; ++d) {
+            VClock rm = vclock_from_row(def_clock + d * A, A);
+            std::set<uint32_t> keys;
+            for (size_t w = 0; w < Kw; ++w)
+              for (uint64_t x = def_keys[d * Kw + w]; x; x &= x - 1) {
+                const size_t key = w * 64 + __builtin_ctzll(x);
+                if (key >= k0 && key < k1) keys.insert((uint32_t)key);
+              }
+            auto it = m.deferred.find(rm);
+            if (it != m.deferred.end()) it->second.insert(keys.begin(), keys.end());
+            else m.deferred.emplace(std::move(rm), std::move(keys));
+          }
+      }
+      ready.fetch_add(1);
+      while (!go.load(std::memory_order_acquire)) std::this_thread::yield();
+      for (auto &r : reps) part[t].merge(std::move(r));
+    });
+  while (ready.load() < (int)T) std::this_thread::yield();
+  const double t0 = now_s();
+  go.store(1, std::memory_order_release);
+  for (auto &th : pool) th.join();
+  const double t1 = now_s();
+  vclock_to_row(part[0].clock, out_clock, A);
+  std::memset(out_ec, 0, K * A * 8);
+  std::memset(out_vclk, 0, K * Vout * A * 8);
+  std::memset(out_vval, 0, K * Vout * 8);
+  std::memset(out_nval, 0, K * 8);
+  std::map<VClock, std::set<uint32_t>> dfr;
+  for (size_t t = 0; t < T; ++t) {
+    for (auto &kv : part[t].entries) {
+      const size_t k = kv.first;
+      vclock_to_row(kv.second.clock, out_ec + k * A, A);
+      out_nval[k] = kv.second.val.vals.size();
+      size_t s = 0;
+      for (auto &cv : kv.second.val.vals) {
+        if (s >= Vout) break;
+        vclock_to_row(cv.first, out_vclk + (k * Vout + s) * A, A);
+        out_vval[k * Vout + s] = cv.second;
+        ++s;
+      }
+    }
+    for (auto &kv : part[t].deferred) dfr[kv.first].insert(kv.second.begin(), kv.second.end());
+  }
+  size_t k = 0;
+  for (auto &kv : dfr) {
+    if (k < max_def) {
+      vclock_to_row(kv.first, out_def_clock + k * A, A);
+      std::memset(out_def_keys + k * Kw, 0, Kw * 8);
+      for (uint32_t key : kv.second) out_def_keys[k * Kw + key / 64] |= 1ull << (key % 64);
+    }
+    ++k;
+  }
+  *out_ndef = k;
+  return t1 - t0;
+}
+
 }  // extern "C"

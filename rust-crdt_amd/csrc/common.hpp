@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "crdt_gpu.h"
+#include "shard_host.hpp"
 
 namespace crdt {
 
@@ -67,7 +68,8 @@ struct Tune {
   int map_sh = 0;      // ... RS path at A = 32, V = 2, K % 4 == 0: four key waves share each chunk's clock
                        //     rows (less traffic, but slower: the coupled waves; opt-in)
   int map_lazyv = 1;   // ... RS path: values fetched only for chunks the exact loop runs (not streamed)
-  int map_ld = 0;      // ... RS path at (2+V)*A == 128: a loader wave per key issues the chunks' LDS-DMA (opt-in)
+  int map_sp = 0;      // ... RS path at A = 32, V = 2: two waves per key, each testing half the actors (SP)
+  int shagree = 0;     // sharded calls: 1 = the validation-header exchange on every call (no agreed-plan path)
   int map_diag = 0;    // ... timing probes only, results WRONG (bit0: no clock-max piece, bit1: 3 fewer step pieces)
   int rows_blocks_per_cu = 0;  // row-pair / row-reduction kernels (causal.hip); 0 = per-kernel default
   int apply_hot_slots = 8;     // Orswot apply: deferred slots kept in LDS per state (the rest in HBM)
@@ -172,6 +174,16 @@ struct crdt_ctx {
   size_t a_rows = 0;
   std::string comm_note;  // e.g. an RCCL runtime / header version mismatch found at init
   void (*comm_release)(crdt_ctx *) = nullptr;
+  // agreed plans (shard_host::PlanCache keys) and the pending check of the last cached-path call:
+  // 3 device words all-reduced beside the data, their pinned host copy [send 3 | reduced 3] and the
+  // event after the copy back (shard.hip)
+  crdt::shard_host::PlanCache plans;
+  bool chk_pending = false;
+  uint64_t chk_key = 0;
+  void *chk_dev = nullptr;
+  uint64_t *chk_host = nullptr;
+  hipEvent_t chk_ev = nullptr;
+  int (*comm_check)(crdt_ctx *) = nullptr;  // the pending check (crdt_ctx_synchronize runs it)
   // Host-memory mode (csrc/host_stage.hip): CRDT_MEM_DEVICE / CRDT_MEM_HOST, the copy stream, two
   // device chunk buffers with their copied / free events, and the device accumulator.
   int mem_kind = CRDT_MEM_DEVICE;

@@ -219,7 +219,8 @@ static void apply_tune(crdt_ctx *ctx, const char *t) {
       else if (k == "mscan3") ctx->tune.map_scan3 = v != 0;
       else if (k == "mrs") ctx->tune.map_rs = v != 0;
       else if (k == "msh") ctx->tune.map_sh = v != 0;
-      else if (k == "mld") ctx->tune.map_ld = v != 0;
+      else if (k == "msp") ctx->tune.map_sp = v != 0;
+      else if (k == "shagree") ctx->tune.shagree = v != 0;
       else if (k == "mbatch") ctx->tune.map_batch = v != 0;
       else if (k == "mlazyv") ctx->tune.map_lazyv = v != 0;
       else if (k == "mdiag" && v >= 0) ctx->tune.map_diag = v;
@@ -318,6 +319,8 @@ int crdt_ctx_synchronize(crdt_ctx *ctx) {
   CRDT_CHECK_CTX(ctx);
   CRDT_HIP(ctx, hipSetDevice(ctx->device));
   CRDT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  // a sharded call on an agreed plan verifies its check words here or at the next sharded call
+  if (ctx->comm_check) return ctx->comm_check(ctx);
   return CRDT_OK;
 }
 

@@ -66,7 +66,7 @@ struct MapPlan {
   int lazyv;  // RS path: the values of a chunk fetched only when the exact loop runs it
   int diag;   // timing probes (results wrong): bit0 no clock-max piece, bit1 3 fewer step pieces,
               // bit2 SH path without arrival waits
-  const u64 *seq;  // LD path: [nch][2] = chunk index + 1, the arrival flag each chunk's last piece carries
+  int sp;  // SP path (A = 32, V = 2 on the RS shapes): two waves per key, each testing half the actors
 };
 
 constexpr int kMapQ = 4;    // deferred removes tracked per key in registers before the slow path
@@ -316,7 +316,7 @@ template <int VI, int C, int NI, int AUX = 0>
 __device__ __forceinline__ void map_chunk_glds(const MapPlan &p, const GldsLanes<NI> &L, unsigned long long g,
                                                unsigned long long k, unsigned long long i0, unsigned long long iend,
                                                u64 *img, unsigned long long WS, u64 *vals, u64 *cm, int lane,
-                                               bool vpiece = true, int diag = 0, const u64 *flag = nullptr) {
+                                               bool vpiece = true, int diag = 0) {
   if (i0 + C <= iend) {  // a whole chunk (uniform)
     const char *src[NI];
 #pragma unroll
@@ -355,12 +355,9 @@ __device__ __forceinline__ void map_chunk_glds(const MapPlan &p, const GldsLanes
       glds4<AUX>(src, vals);
     }
   }
-  // the chunk's clock max: one more piece (lanes 0 .. A/2-1, A even); with `flag` (the LD path) lane
-  // A/2 of the same, last, piece moves the chunk's arrival flag seq[chunk] to cm[A]: the pieces of
-  // a wave retire in order, so a reader that sees the flag sees the whole chunk
+  // the chunk's clock max: one more piece (lanes 0 .. A/2-1, A even)
   if (!(diag & 1)) {
-    const bool con = (unsigned long long)(2 * lane) < p.A, fon = flag && (unsigned long long)(2 * lane) == p.A;
-    if (con || fon) glds16(con ? p.cmax + (g * p.nch + i0 / C) * p.A + 2 * lane : flag + 2 * (i0 / C), cm);
+    if ((unsigned long long)(2 * lane) < p.A) glds16(p.cmax + (g * p.nch + i0 / C) * p.A + 2 * lane, cm);
   }
 }
 
@@ -769,11 +766,11 @@ __device__ __forceinline__ unsigned rs_a0(int lane, int m) {
 
 template <int NQ, bool PRESENT, int NP, bool PERM = false>
 __device__ __forceinline__ RsOwn<NQ, NP> rs_own(const u64 *mirror, const u64 *thr, unsigned long long A, int lane,
-                                                int nv = NQ) {
+                                                int nv = NQ, unsigned ab = 0) {
   RsOwn<NQ, NP> o;
 #pragma unroll
   for (int m = 0; m < NP; ++m) {
-    const unsigned a0 = rs_a0<PERM>(lane, m);
+    const unsigned a0 = ab + rs_a0<PERM>(lane, m);
     const unsigned long long a = a0 < A ? a0 : A - 2;
     o.tb[m] = lds2(thr + a);
     if constexpr (PRESENT) {
@@ -795,8 +792,63 @@ struct RsNoDma {
   __device__ __forceinline__ void operator()(int) {}
 };
 
+// The test's per-step partial results over one actor range (bit 4s: step s), its LPS lanes combined:
+// p2 "the replica has the key" (an OR over actors), the rest ANDs over actors — b the both-present
+// entry test, o the acc-only test, van[t] "incoming value t forgotten to empty", le[t][q] "incoming
+// value t <= own value q".  The SP path tests two actor halves in two waves and combines their parts
+// (p2 OR-ed, the rest AND-ed) before the verdict, which ORs over q: a verdict per half would be wrong.
+template <int VI, int NQ>
+struct RsPart {
+  u64 p2, b, o, van[VI], le[VI][NQ > 0 ? NQ : 1];
+};
+
+template <int VI, int NQ>
+__device__ __forceinline__ RsPart<VI, NQ> rs_part_fail() {  // a range that settles nothing: verdict 0
+  RsPart<VI, NQ> x;
+  x.p2 = grp_mask<4>();  // (only bits 4s: the SP path packs four masks per word)
+  x.b = x.o = 0;
+#pragma unroll
+  for (int t = 0; t < VI; ++t) {
+    x.van[t] = 0;
+#pragma unroll
+    for (int q = 0; q < (NQ > 0 ? NQ : 1); ++q) x.le[t][q] = 0;
+  }
+  return x;
+}
+
+template <int VI, int NQ>
+__device__ __forceinline__ RsPart<VI, NQ> rs_part_join(const RsPart<VI, NQ> &x, const RsPart<VI, NQ> &y) {
+  RsPart<VI, NQ> z;
+  z.p2 = x.p2 | y.p2;
+  z.b = x.b & y.b;
+  z.o = x.o & y.o;
+#pragma unroll
+  for (int t = 0; t < VI; ++t) {
+    z.van[t] = x.van[t] & y.van[t];
+#pragma unroll
+    for (int q = 0; q < (NQ > 0 ? NQ : 1); ++q) z.le[t][q] = x.le[t][q] & y.le[t][q];
+  }
+  return z;
+}
+
+template <int VI, int NQ, bool PRESENT>
+__device__ __forceinline__ u64 rs_verdict(const RsPart<VI, NQ> &x) {
+  const u64 G1 = grp_mask<4>();
+  if constexpr (!PRESENT) return (~x.p2 | x.b) & G1;
+  u64 both = x.p2 & x.b;
+  const u64 only = ~x.p2 & x.o;
+#pragma unroll
+  for (int t = 0; t < VI; ++t) {
+    u64 cov = x.van[t];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) cov |= x.le[t][q];
+    both &= cov;
+  }
+  return (both | only) & G1;
+}
+
 template <int VI, int NP, int NQ, bool PRESENT, bool BATCH = false, class F = RsNoDma>
-__device__ __forceinline__ u64 rs_noop(const RsChunk<VI, NP> &r, const RsOwn<NQ, NP> &o, F &&dma = F{}) {
+__device__ __forceinline__ RsPart<VI, NQ> rs_part(const RsChunk<VI, NP> &r, const RsOwn<NQ, NP> &o, F &&dma = F{}) {
   constexpr int LPS = 4;
   constexpr int ND = std::remove_reference_t<F>::count;  // pieces to issue: two per element, the rest after
   constexpr int NQ1 = NQ > 0 ? NQ : 1;
@@ -882,19 +934,22 @@ __device__ __forceinline__ u64 rs_noop(const RsChunk<VI, NP> &r, const RsOwn<NQ,
 #pragma unroll
     for (int j = 4 * NP; j < ND; ++j) dma(j);
   }
-  const u64 G1 = grp_mask<LPS>();
-  const u64 P2 = orN<LPS>(mP2);
-  if constexpr (!PRESENT) return (~P2 | andN<LPS>(mB)) & G1;
-  u64 both = P2 & andN<LPS>(mB);
-  const u64 only = ~P2 & andN<LPS>(mO);
+  RsPart<VI, NQ> x;
+  x.p2 = orN<LPS>(mP2);
+  x.b = andN<LPS>(mB);
+  x.o = PRESENT ? andN<LPS>(mO) : 0;
 #pragma unroll
   for (int t = 0; t < VI; ++t) {
-    u64 cov = andN<LPS>(mVan[t]);
+    x.van[t] = PRESENT ? andN<LPS>(mVan[t]) : 0;
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) cov |= andN<LPS>(mLe[t][q]);
-    both &= cov;
+    for (int q = 0; q < NQ1; ++q) x.le[t][q] = (PRESENT && q < NQ) ? andN<LPS>(mLe[t][q]) : 0;
   }
-  return (both | only) & G1;
+  return x;
+}
+
+template <int VI, int NP, int NQ, bool PRESENT, bool BATCH = false, class F = RsNoDma>
+__device__ __forceinline__ u64 rs_noop(const RsChunk<VI, NP> &r, const RsOwn<NQ, NP> &o, F &&dma = F{}) {
+  return rs_verdict<VI, NQ, PRESENT>(rs_part<VI, NP, NQ, PRESENT, BATCH>(r, o, dma));
 }
 
 // The verdict from the LDS mirror (the exact loop's scan): one instantiation per presence, own
@@ -905,6 +960,20 @@ __device__ __forceinline__ u64 rs_lds_own_noop(const RsChunk<VI, NP> &r, const u
   if (!present) return rs_noop<VI, NP, 0, false>(r, rs_own<0, false, NP, PERM>(mirror, thr, A, lane));
   if (nv > 3) return 0;
   return rs_noop<VI, NP, 3, true>(r, rs_own<3, true, NP, PERM>(mirror, thr, A, lane, nv));
+}
+// The partial masks of the same test over the actor range starting at ab (the SP path's halves).
+template <int VI, int NP, bool PRESENT>
+__device__ __forceinline__ RsPart<VI, 3> rs_lds_own_part(const RsChunk<VI, NP> &r, const u64 *mirror, const u64 *thr,
+                                                         unsigned long long A, int nv, int lane, unsigned ab) {
+  if constexpr (!PRESENT) {
+    const RsPart<VI, 0> y = rs_part<VI, NP, 0, false>(r, rs_own<0, false, NP>(mirror, thr, A, lane, 0, ab));
+    RsPart<VI, 3> x = rs_part_fail<VI, 3>();
+    x.p2 = y.p2;
+    x.b = y.b;
+    return x;
+  } else {
+    return rs_part<VI, NP, 3, true>(r, rs_own<3, true, NP>(mirror, thr, A, lane, nv, ab));
+  }
 }
 
 template <int VI, int NP>
@@ -950,6 +1019,23 @@ __device__ __forceinline__ u64 rs_reg_noop(const RsChunk<VI, NP> &r, const RsReg
     for (int q = 0; q < (NQ > 0 ? NQ : 1); ++q) o.sq[q][m] = g.sq[q < 3 ? q : 0][m];
   }
   return rs_noop<VI, NP, NQ, PRESENT, BATCH>(r, o, dma);
+}
+template <int VI, int NP, int NQ, bool PRESENT, bool BATCH = false, class F = RsNoDma>
+__device__ __forceinline__ RsPart<VI, NQ> rs_reg_part(const RsChunk<VI, NP> &r, const RsReg<NP> &g, F &&dma = F{}) {
+  RsOwn<NQ, NP> o;
+#pragma unroll
+  for (int m = 0; m < NP; ++m) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const u64 lo = g.cs[m][h] < g.m1[m][h] ? g.cs[m][h] : g.m1[m][h];
+      o.tb[m][h] = g.ea[m][h] > lo ? g.ea[m][h] : lo;
+    }
+    o.ea[m] = g.ea[m];
+    o.to[m] = g.to[m];
+#pragma unroll
+    for (int q = 0; q < (NQ > 0 ? NQ : 1); ++q) o.sq[q][m] = g.sq[q < 3 ? q : 0][m];
+  }
+  return rs_part<VI, NP, NQ, PRESENT, BATCH>(r, o, dma);
 }
 // One instantiation per presence: own values are compared as 3 slots, the unused ones zero —
 // neutral, since "c2 <= 0 everywhere" only covers an empty incoming slot, which the "appended, then
@@ -1056,6 +1142,246 @@ __device__ __forceinline__ void rs_store(const RsChunk<VI, NP> &r, u64 *img, uns
     for (int t = 0; t < VI; ++t) vals[s * VI + t] = r.v[t];
 }
 
+// ---- Split-actor pair (SP path: the RS path at A = 32, V = 2 with two waves per key) ---------------
+// The RS path runs one wave per key: config 4's 1,024 keys are one wave per SIMD, so nothing hides the
+// chunk test's latencies.  In the SP path a key is a workgroup of two waves, wave h testing actors
+// 16h .. 16h+15 of every chunk: each moves half of every step image (two steps per 1-KiB LDS-DMA
+// instruction, 8 per chunk instead of 16) and runs half of the test's compares, and the 2,048 waves are
+// two per SIMD.  The test is an OR over actors for "the replica has the key" and ANDs over actors for
+// the rest, so the halves exchange their partial masks (RsPart, 3 LDS words per wave and chunk, one
+// s_barrier) and both form the same verdict.  A chunk neither skips: both waves write their halves back
+// over the slot, wave 0 runs the exact loop over the whole chunk (lane = actor, as in the RS path) while
+// wave 1 waits at a barrier, and both reload their scan operands from the fold-state mirror.
+// scripts/micro/map_stream.hip measured this access pattern's ceiling at 2.05-2.06 ms for config 4
+// (80% of 8 TB/s) at one and at two waves per key, with two waves holding it to ~2.1 ms at twice the
+// per-wave work (profiles/r06_map_stream.log).
+constexpr unsigned kSpSlot = 1024;  // u64 words of one wave's chunk slot: 8 pieces x two 512-byte step halves
+
+// Word (in a wave's slot) of step s, part t (0 entry clock, 1 + v value clock v, 3 replica clock) and
+// actor a < 16 of the wave's half: piece s / 2, lane quad 2 (2t + a / 8) + s % 2 (every quad moves
+// 64 contiguous bytes of one row), word a % 8 of the quad's 64 bytes.
+__host__ __device__ __forceinline__ unsigned sp_word(unsigned s, unsigned t, unsigned a) {
+  return (s >> 1) * 128 + (2 * (2 * t + (a >> 3)) + (s & 1)) * 8 + (a & 7);
+}
+
+// Per-lane LDS-DMA source of the SP path: lane quad q moves, for step parity q % 2, 64 bytes of row
+// part (q / 2) / 2 at actors 16h + 8 ((q / 2) % 2) + 2 (lane % 4) .. + 1.
+struct SpLanes {
+  const char *base;       // the lane's 16 bytes of replica 0's row (bytes)
+  unsigned long long rs;  // that row's replica stride (bytes)
+  unsigned b;             // the step parity the lane moves
+};
+
+__device__ __forceinline__ SpLanes sp_lanes(const MapPlan &p, unsigned long long g, unsigned long long k, int lane,
+                                            unsigned h) {
+  SpLanes L;
+  const unsigned q = (unsigned)lane >> 2, c = q >> 1, t = c >> 1;
+  L.b = q & 1;
+  const unsigned long long A = p.A, a = 16ull * h + 8 * (c & 1) + 2 * ((unsigned)lane & 3);
+  // (the row sources as values: a per-lane choice between struct fields would put the plan in scratch)
+  const unsigned long long be = (unsigned long long)(p.ec + g * p.e_gs + k * A);
+  const unsigned long long bv = (unsigned long long)(p.vclk + g * p.vc_gs + k * 2 * A);
+  const unsigned long long bc = (unsigned long long)(p.clock + g * p.c_gs);
+  const unsigned long long se = (unsigned long long)p.e_rs * 8, sv = (unsigned long long)p.vc_rs * 8,
+                           sc = (unsigned long long)p.c_rs * 8;
+  const unsigned long long base = t == 0 ? be : (t < 3 ? bv + (t - 1) * A * 8 : bc);
+  L.base = reinterpret_cast<const char *>(base + a * 8);
+  L.rs = t == 0 ? se : (t < 3 ? sv : sc);
+  return L;
+}
+
+// DMA chunk ch's half step images (steps clamped to R - 1 past the end: copies never read) into a
+// wave's slot, then the chunk's clock max over all A actors (each wave keeps its own copy).  Exactly
+// 9 global_load_lds per call, so a fixed vmcnt count retires a chunk.
+__device__ __forceinline__ void sp_chunk_glds(const MapPlan &p, const SpLanes &L, unsigned long long g,
+                                              unsigned long long ch, unsigned long long R, u64 *img, u64 *cm,
+                                              int lane) {
+  const unsigned long long i0 = ch * 16;
+  if (i0 + 16 <= R) {  // (uniform)
+    const char *src = L.base + (i0 + L.b) * L.rs;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      glds16(src, img + j * 128);
+      src += 2 * L.rs;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const unsigned long long i = i0 + 2 * j + L.b < R ? i0 + 2 * j + L.b : R - 1;
+      glds16(L.base + i * L.rs, img + j * 128);
+    }
+  }
+  if ((unsigned long long)(2 * lane) < p.A) glds16(p.cmax + (g * p.nch + ch) * p.A + 2 * lane, cm);
+}
+
+// sp_chunk_glds of a whole chunk as the chunk test's DMA hook (pieces between the test's compares).
+struct SpDma {
+  static constexpr int count = 9;
+  const char *src;
+  unsigned long long st2;  // two rows
+  u64 *img;
+  const u64 *csrc;
+  u64 *cm;
+  bool con;
+  __device__ __forceinline__ void operator()(int j) {
+    if (j < 8) {
+      glds16(src, img + j * 128);
+      src += st2;
+    } else if (con) {
+      glds16(csrc, cm);
+    }
+  }
+};
+
+// A wave's half of chunk ch from its slot into the scan layout (lane (s, gq): actor pairs 16h + 2gq + 8m),
+// and the chunk's clock max (lane = actor, and at the lane's pairs).
+template <int VI, int NP>
+__device__ __forceinline__ void sp_reload(RsChunk<VI, NP> &r, const u64 *img, const u64 *cm, unsigned long long A,
+                                          int lane, unsigned h, bool wcm = true) {
+  static_assert(VI == 2 && NP == 2, "SP path: A = 32, V = 2");
+  const unsigned s = (unsigned)lane >> 2, gq = (unsigned)lane & 3;
+#pragma unroll
+  for (int m = 0; m < NP; ++m) {
+    const unsigned a = 2 * gq + 8 * m;
+    r.e[m] = lds2(img + sp_word(s, 0, a));
+#pragma unroll
+    for (int t = 0; t < VI; ++t) r.c[t][m] = lds2(img + sp_word(s, 1 + t, a));
+    r.co[m] = lds2(img + sp_word(s, 1 + VI, a));
+  }
+  if (wcm) {
+    r.cm = cm[(unsigned long long)lane < A ? lane : A - 1];
+#pragma unroll
+    for (int m = 0; m < NP; ++m) r.cmp[m] = lds2(cm + 16 * h + 2 * gq + 8 * m);
+  }
+}
+
+// A chunk neither wave could skip: the wave's half back over its slot (the layout the DMA wrote).
+template <int VI, int NP>
+__device__ __forceinline__ void sp_store(const RsChunk<VI, NP> &r, u64 *img, u64 *cm, unsigned long long A, int lane) {
+  const unsigned s = (unsigned)lane >> 2, gq = (unsigned)lane & 3;
+#pragma unroll
+  for (int m = 0; m < NP; ++m) {
+    const unsigned a = 2 * gq + 8 * m;
+    *reinterpret_cast<u64x2 *>(img + sp_word(s, 0, a)) = r.e[m];
+#pragma unroll
+    for (int t = 0; t < VI; ++t) *reinterpret_cast<u64x2 *>(img + sp_word(s, 1 + t, a)) = r.c[t][m];
+    *reinterpret_cast<u64x2 *>(img + sp_word(s, 1 + VI, a)) = r.co[m];
+  }
+  if ((unsigned long long)lane < A) cm[lane] = r.cm;
+}
+
+// The partial masks through LDS: 4 masks per u64 word (the masks only use bits 4s), 3 words per wave.
+template <int NQ>
+__device__ __forceinline__ void sp_put(u64 *vw, const RsPart<2, NQ> &x, int lane) {
+  constexpr int NQ1 = NQ > 0 ? NQ : 1;
+  static_assert(5 + 2 * NQ1 <= 12, "three vote words");
+  u64 w[3] = {0, 0, 0};
+  const u64 G1 = grp_mask<4>();
+  int i = 0;
+  auto put = [&](u64 m) {
+    w[i >> 2] |= (m & G1) << (i & 3);
+    ++i;
+  };
+  put(x.p2);
+  put(x.b);
+  put(x.o);
+  put(x.van[0]);
+  put(x.van[1]);
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int q = 0; q < NQ1; ++q) put(x.le[t][q]);
+  if (lane < 3) vw[lane] = lane == 0 ? w[0] : (lane == 1 ? w[1] : w[2]);
+}
+
+template <int NQ>
+__device__ __forceinline__ RsPart<2, NQ> sp_get(const u64 *vw) {
+  constexpr int NQ1 = NQ > 0 ? NQ : 1;
+  u64 w[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const u64 x = *reinterpret_cast<const volatile u64 *>(vw + j);
+    w[j] = ((u64)(unsigned)__builtin_amdgcn_readfirstlane((int)(x >> 32)) << 32) |
+           (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)x);
+  }
+  const u64 G1 = grp_mask<4>();
+  int i = 0;
+  auto get = [&]() {
+    const u64 m = (w[i >> 2] >> (i & 3)) & G1;
+    ++i;
+    return m;
+  };
+  RsPart<2, NQ> x;
+  x.p2 = get();
+  x.b = get();
+  x.o = get();
+  x.van[0] = get();
+  x.van[1] = get();
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int q = 0; q < NQ1; ++q) x.le[t][q] = get();
+  return x;
+}
+
+// The pair's barrier: this wave's LDS writes done, both waves here, no LDS access moved across it.
+// (No vmcnt wait: the LDS-DMA of later chunks stays in flight.)
+__device__ __forceinline__ void sp_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// One chunk's vote: this wave's partial masks (or "settles nothing" when it did not test), exchanged
+// with the partner's through LDS around one s_barrier, then the common verdict.  vw: this chunk
+// parity's 8 words (wave h at 4h).  Both waves call it with the same present / nv.
+template <bool PRESENT>
+__device__ __forceinline__ u64 sp_vote(u64 *vw, const RsPart<2, MAP_REG_NQ> &mine, unsigned h, int lane) {
+  sp_put<MAP_REG_NQ>(vw + 4 * h, mine, lane);
+  sp_barrier();
+  const RsPart<2, MAP_REG_NQ> other = sp_get<MAP_REG_NQ>(vw + 4 * (h ^ 1));
+  return rs_verdict<2, MAP_REG_NQ, PRESENT>(rs_part_join(mine, other));
+}
+
+// This wave's partial masks of the register test (the RS dispatch on presence / own value count:
+// a state holding more than MAP_REG_NQ values settles nothing here, as rs_reg_noop_nv).
+template <bool BATCH, class F = RsNoDma>
+__device__ __forceinline__ RsPart<2, MAP_REG_NQ> sp_reg_part(const RsChunk<2, 2> &r, const RsReg<2> &g, bool present,
+                                                             int nv, bool test, F &&dma = F{}) {
+  if (!test || (present && nv > MAP_REG_NQ)) {
+#pragma unroll
+    for (int j = 0; j < std::remove_reference_t<F>::count; ++j) dma(j);
+    return rs_part_fail<2, MAP_REG_NQ>();
+  }
+  if (!present) {
+    const RsPart<2, 0> y = rs_reg_part<2, 2, 0, false, BATCH>(r, g, dma);
+    RsPart<2, MAP_REG_NQ> x = rs_part_fail<2, MAP_REG_NQ>();
+    x.p2 = y.p2;
+    x.b = y.b;
+    return x;
+  }
+  return rs_reg_part<2, 2, MAP_REG_NQ, true, BATCH>(r, g, dma);
+}
+
+// The exact loop's test of a chunk from LDS (wave 0 alone, both halves): the two halves' parts joined.
+__device__ __forceinline__ u64 sp_lds_noop(const u64 *img0, const u64 *img1, const u64 *mirror, const u64 *thr,
+                                           unsigned long long A, bool present, int nv, int lane) {
+  if (present && nv > 3) return 0;
+  RsChunk<2, 2> r;
+  r.cm = 0;
+  r.v[0] = r.v[1] = 0;
+  if (!present) {
+    sp_reload(r, img0, nullptr, A, lane, 0, false);
+    const RsPart<2, 3> x = rs_lds_own_part<2, 2, false>(r, mirror, thr, A, nv, lane, 0);
+    sp_reload(r, img1, nullptr, A, lane, 1, false);
+    return rs_verdict<2, 3, false>(rs_part_join(x, rs_lds_own_part<2, 2, false>(r, mirror, thr, A, nv, lane, 16)));
+  }
+  sp_reload(r, img0, nullptr, A, lane, 0, false);
+  const RsPart<2, 3> x = rs_lds_own_part<2, 2, true>(r, mirror, thr, A, nv, lane, 0);
+  sp_reload(r, img1, nullptr, A, lane, 1, false);
+  return rs_verdict<2, 3, true>(rs_part_join(x, rs_lds_own_part<2, 2, true>(r, mirror, thr, A, nv, lane, 16)));
+}
+
 // ---- Shared replica-clock ring (SH path: the RS path at A = 32, V = 2, four key waves per CU) ------
 // A chunk's replica-clock rows are the same for every key of a group and a quarter of each step
 // image, and a CU's LDS-DMA engine takes one instruction per ~17 cycles whatever its lane count
@@ -1085,20 +1411,6 @@ constexpr int kShS = 2 * kShD - 1;
 constexpr unsigned kShSlot = 1536;            // private slot, u64 words (16 steps x 3 rows x 32)
 constexpr unsigned kShShared = 512 + 32;      // shared slot: clock rows + clock max
 constexpr unsigned kShSpin = 1u << 22;        // arrival-wait bound (a protocol fault is reported, never hangs)
-
-// ---- Loader wave (LD path: the RS path at (2+V)*A == 128, config 4) --------------------------------
-// The chunk's 17 LDS-DMA instructions cost the wave that issues them ~34-68 cycles each (a wave
-// issues one per ~34 cycles alone and the CU's engine one per ~17, scripts/micro/glds_rate.hip), and
-// in the RS path that wave is the key's fold wave: about a quarter of its chunk test.  In the LD path
-// a workgroup is two waves: wave 0 folds the key, wave 1 only streams its chunks into the two ring
-// slots.  Hand-over through LDS, no barriers: the last piece of a chunk carries its arrival flag
-// (lane A/2 of the clock-max piece writes seq[c] = c + 1 after the clock max), and the fold wave,
-// once its copy of chunk c out of slot c&1 is read, publishes rel[c&1] = c + 1; the loader issues
-// chunk c + 2 into that slot when it sees it.  A chunk the register test cannot skip takes its slot
-// back: the fold wave waits for chunk c + 2's flag (that copy has landed), writes chunk c over the
-// slot, runs the exact loop, clears the flag and re-issues chunk c + 2 itself.  Every wait is
-// bounded (flag bit 3 on a timeout, after which nothing waits), so the grid always drains.
-constexpr unsigned kLdSpin = 1u << 21;
 
 // Per-lane LDS-DMA sources of the SH path: piece v (part v) of a 4-step group moves pair lane%16 of
 // part v of step lane/16; the shared piece of wave w the same pair of the clock row of step
@@ -1244,11 +1556,11 @@ __device__ __forceinline__ unsigned sh_arrived(const unsigned *cnt) {
 
 // ITM: unrolled scan iterations ceil(A / LPS) rounded up to a power of two, fixed per launch so
 // each kernel's register allocation only covers its own scan shape.  NP > 0: the RS path (above).
-template <int APL, int VI, int VO, int CM, int NB, bool GL, int ITM, int NP = 0, bool SH = false, bool LD = false>
-__global__ __launch_bounds__(SH ? 256 : (LD ? 128 : 64), LD ? 2 : 1) void map_fold_kernel(MapPlan pk) {
+template <int APL, int VI, int VO, int CM, int NB, bool GL, int ITM, int NP = 0, bool SH = false, bool SP = false>
+__global__ __launch_bounds__(SH ? 256 : (SP ? 128 : 64), SP ? 2 : 1) void map_fold_kernel(MapPlan pk) {
   constexpr bool RS = NP > 0;
   static_assert(!SH || (RS && VI == 2 && NP == 4), "SH path: the RS path at A = 32, V = 2");
-  static_assert(!LD || (RS && !SH && NB == 2), "LD path: the RS path with a loader wave");
+  static_assert(!SP || (RS && !SH && NB == 2 && VI == 2 && NP == 2 && CM == 16), "SP path: the RS path at A = 32, V = 2");
   const MapPlan p = pk;  // a local copy the optimizer can split into registers (the by-value
                          // kernel argument itself would be materialized in scratch memory)
   // SH: a workgroup of four waves, wave w folding key 4*blockIdx + w (K % 4 == 0: one group)
@@ -1256,7 +1568,8 @@ __global__ __launch_bounds__(SH ? 256 : (LD ? 128 : 64), LD ? 2 : 1) void map_fo
   const unsigned long long gk0 = SH ? 4ull * blockIdx.x + wv : (unsigned long long)blockIdx.x;
   const unsigned long long g = gk0 / p.K;
   const unsigned long long k = gk0 % p.K;
-  const int lane = (SH || LD) ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
+  const int lane = (SH || SP) ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
+  const unsigned hw = SP ? (unsigned)threadIdx.x >> 6 : 0u;  // SP: the wave's actor half
   const unsigned long long R = p.R;
 
   bool present = false;
@@ -1308,14 +1621,18 @@ __global__ __launch_bounds__(SH ? 256 : (LD ? 128 : 64), LD ? 2 : 1) void map_fo
   // list, the fold-state mirror.  (Addresses are always computed from map_lds: a pointer table
   // would hide the LDS address space and turn every access into a flat op.)  SH: four such wave
   // regions (no clock-max slots), then the shared ring and its arrival counters.
-  const unsigned long long SLOT = SH ? kShSlot : C * WS;
-  const unsigned long long CMS = LD ? A + 2 : A;  // staged clock-max stride (LD: + the arrival flag)
+  // SP: both waves' slots (wave h's at wl + h * NB * SLOT), both waves' clock-max copies, and after the
+  // thresholds the vote words [chunk parity][wave][4] and the fold state word for the partner (present,
+  // own value count)
+  const unsigned long long SLOT = SH ? kShSlot : (SP ? kSpSlot : C * WS);
+  constexpr unsigned long long NW = SP ? 2 : 1;
+  const unsigned long long CMS = A;  // staged clock-max stride
   const unsigned long long PW =
-      NB * SLOT + NB * C * VI + kMapL + (2 + VO) * A + ((GL || RS) && !SH ? NB * CMS : 0) + 4 * A + (LD ? 1 : 0);
+      NW * NB * SLOT + NB * C * VI + kMapL + (2 + VO) * A + ((GL || RS) && !SH ? NW * NB * CMS : 0) + 4 * A + (SP ? 18 : 0);
   u64 *const wl = map_lds + (SH ? wv * PW : 0);
   u64 *const shr = map_lds + 4 * PW;  // SH: kShS shared slots
   unsigned *const arr = reinterpret_cast<unsigned *>(shr + kShS * kShShared);
-  u64 *const vbase = wl + NB * SLOT;
+  u64 *const vbase = wl + NW * NB * SLOT;
   unsigned *lrow = reinterpret_cast<unsigned *>(vbase + NB * C * VI);
   unsigned *lidx = lrow + kMapL;
   // fold-state mirror read by the speculative scan: entry clock, VO value clocks, acc clock
@@ -1323,36 +1640,85 @@ __global__ __launch_bounds__(SH ? 256 : (LD ? 128 : 64), LD ? 2 : 1) void map_fo
   constexpr bool kSpec = APL == 1 && VO <= 4;
   u64 *const cml = mirror + (2 + VO) * A;  // GL: NB staged chunk clock maxima (A words each)
   // scan thresholds (map_noop_steps3, RS): TB [A] | TO [A]; m1 = (min nonzero own value clock) - 1
-  u64 *const thr = cml + ((GL || RS) && !SH ? NB * CMS : 0);
+  u64 *const thr = cml + ((GL || RS) && !SH ? NW * NB * CMS : 0);
   u64 *const csm = thr + 2 * A;  // RS: the acc clock and m1 handed back to the register operands
   u64 *const m1m = thr + 3 * A;
-  unsigned *const rel = reinterpret_cast<unsigned *>(m1m + A);  // LD: last chunk released per slot, + 1
+  u64 *const vw = m1m + A;                                        // SP: vote words
+  unsigned *const spst = reinterpret_cast<unsigned *>(vw + 16);   // SP: present | own values << 1
   u64 m1 = ~0ull;
   const unsigned long long nch = (R + C - 1) / C;
-  bool ld_late = false;  // LD: a hand-over wait ran past kLdSpin (flag bit 3; nothing waits after it)
-  if constexpr (LD) {
-    if (threadIdx.x < NB) {
-      rel[threadIdx.x] = 0;
-      cml[threadIdx.x * CMS + A] = 0;
-    }
-    __syncthreads();  // (the only barrier: the two waves part here)
-    if (threadIdx.x >= 64) {  // the loader wave: chunks 0 and 1, then chunk c as soon as c - 2 is released
-      const GldsLanes<1> gl = glds_lanes<VI, 1>(p, g, k, lane);
-      for (unsigned long long c = 0; c < nch; ++c) {
-        const unsigned sl = (unsigned)(c & 1);
-        if (c >= 2) {
-          unsigned spins = 0;
-          while (__builtin_amdgcn_readfirstlane(*reinterpret_cast<const volatile unsigned *>(rel + sl)) <
-                 (unsigned)(c - 1)) {
-            if (++spins > kLdSpin) break;
-            __builtin_amdgcn_s_sleep(1);
-          }
-          if (spins > kLdSpin) break;  // the fold wave reports its own timeout
-        }
-        map_chunk_glds<VI, C, 1>(p, gl, g, k, c * C, R, wl + sl * SLOT, WS, vbase + sl * C * VI, cml + sl * CMS,
-                                 lane, false, p.diag, p.seq);
+  if constexpr (SP) {
+    if (hw == 1) {  // the partner wave: actors 16 .. 31 of every chunk (wave 0 holds the fold state)
+      const SpLanes spl = sp_lanes(p, g, k, lane, 1);
+      u64 *const img1 = wl + NB * SLOT;  // this wave's slots and clock-max copies
+      u64 *const cm1 = cml + NB * CMS;
+      RsChunk<VI, NP> r;
+      RsReg<NP> q;
+#pragma unroll
+      for (int m = 0; m < NP; ++m) {
+        q.ea[m] = 0;
+        q.cs[m] = 0;
+        q.to[m] = ~0ull;
+        q.m1[m] = ~0ull;
+#pragma unroll
+        for (int x = 0; x < 3; ++x) q.sq[x][m] = 0;
       }
-      wait_vmcnt<0>();
+      bool pres = false;
+      int nvp = 0;
+      const bool batch = MAP_BATCH_ONLY || p.batch;
+      for (unsigned long long c = 0; c < 2 && c < nch; ++c)
+        sp_chunk_glds(p, spl, g, c, R, img1 + c * SLOT, cm1 + c * CMS, lane);
+      for (unsigned long long ch = 0; ch < nch; ++ch) {
+        const unsigned slot = (unsigned)(ch & 1);
+        u64 *const img = img1 + slot * SLOT;
+        u64 *const cms = cm1 + slot * CMS;
+        if (ch + 1 < nch) wait_vmcnt<9>();
+        else wait_vmcnt<0>();
+        sp_reload(r, img, cms, A, lane, 1);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot is read: refill it
+        const unsigned long long n0 = R - ch * C < (unsigned long long)C ? R - ch * C : C;
+        const u64 want = n0 >= 16 ? grp_mask<4>() : (grp_mask<4>() & ((1ull << (4 * n0)) - 1));
+        const unsigned long long i2 = (ch + 2) * C;
+        const bool spread = p.spec && ch + 2 < nch && i2 + C <= R;
+        if (!spread && ch + 2 < nch) sp_chunk_glds(p, spl, g, ch + 2, R, img, cms, lane);
+        RsPart<2, MAP_REG_NQ> part;
+        if (spread) {
+          SpDma d{spl.base + (i2 + spl.b) * spl.rs, 2 * spl.rs, img, p.cmax + (g * p.nch + ch + 2) * A + 2 * lane, cms,
+                  (unsigned long long)(2 * lane) < A};
+          part = batch ? sp_reg_part<true>(r, q, pres, nvp, true, d) : sp_reg_part<false>(r, q, pres, nvp, true, d);
+        } else {
+          part = batch ? sp_reg_part<true>(r, q, pres, nvp, p.spec != 0) : sp_reg_part<false>(r, q, pres, nvp, p.spec != 0);
+        }
+        const u64 verdict = pres ? sp_vote<true>(vw + 8 * slot, part, 1, lane) : sp_vote<false>(vw + 8 * slot, part, 1, lane);
+        if ((verdict & want) == want) {
+#pragma unroll
+          for (int m = 0; m < NP; ++m)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) q.cs[m][h] = q.cs[m][h] > r.cmp[m][h] ? q.cs[m][h] : r.cmp[m][h];
+          continue;
+        }
+        wait_vmcnt<0>();  // chunk ch+2's copy into this slot has landed: write chunk ch back over it
+        sp_store(r, img, cms, A, lane);
+        sp_barrier();  // (A) both halves in LDS: wave 0 runs the exact loop
+        sp_barrier();  // (B) the exact loop is done, the mirror and state word written
+        const unsigned st = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const volatile unsigned *>(spst));
+        pres = (st & 1) != 0;
+        nvp = (int)(st >> 1);
+#pragma unroll
+        for (int m = 0; m < NP; ++m) {
+          const unsigned a0 = 16 + rs_a0<false>(lane, m);
+          q.ea[m] = lds2(mirror + a0);
+          q.to[m] = lds2(thr + A + a0);
+          q.m1[m] = lds2(m1m + a0);
+          q.cs[m] = lds2(csm + a0);
+#pragma unroll
+          for (int x = 0; x < 3; ++x) q.sq[x][m] = x < nvp ? lds2(mirror + (1 + x) * A + a0) : u64x2{0, 0};
+        }
+        if (ch + 2 < nch) {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          sp_chunk_glds(p, spl, g, ch + 2, R, img, cms, lane);
+        }
+      }
       return;
     }
   }
@@ -1425,7 +1791,8 @@ __global__ __launch_bounds__(SH ? 256 : (LD ? 128 : 64), LD ? 2 : 1) void map_fo
   const int ni = GL ? (int)((W + 127) / 128) : 0;  // 1-KiB pieces per step image (GL: 1 or 2)
   GldsLanes<1> gl1;
   GldsLanes<2> gl2;
-  const bool vpiece = !(RS && (SH || p.lazyv));
+  const bool vpiece = !(RS && (SH || SP || p.lazyv));
+  SpLanes spl;  // SP: wave 0's LDS-DMA sources (actors 0 .. 15)
   ShLanes shl;
   // SH ring bookkeeping (uniform): the shared slot of chunk ch and the arrival count it needs, the
   // slot of chunk ch + kShD - 2 (signalled at iteration ch) and of chunk ch + kShD (issued)
@@ -1448,9 +1815,12 @@ __global__ __launch_bounds__(SH ? 256 : (LD ? 128 : 64), LD ? 2 : 1) void map_fo
       sh_chunk_images(shl, c * C, R, wl + c * SLOT);
       if (c + kShD - 2 < nch) sh_chunk_shared(p, shl, g, c + kShD - 2, R, wv, shr + (c + kShD - 2) * kShShared, lane);
     }
+  } else if constexpr (SP) {
+    spl = sp_lanes(p, g, k, lane, 0);
+    for (unsigned long long c = 0; c < 2 && c < nch; ++c) sp_chunk_glds(p, spl, g, c, R, wl + c * SLOT, cml + c * CMS, lane);
   } else if constexpr (RS) {  // chunks 0 and 1 into the two slots (W <= 128: one piece per step)
     gl1 = glds_lanes<VI, 1>(p, g, k, lane);
-    for (unsigned long long c = 0; c < 2 && c < nch && !LD; ++c)
+    for (unsigned long long c = 0; c < 2 && c < nch; ++c)
       map_chunk_glds<VI, C, 1>(p, gl1, g, k, c * C, R, wl + c * SLOT, WS, vbase + c * C * VI, cml + c * A, lane,
                                vpiece, p.diag);
   }
@@ -1476,6 +1846,7 @@ __global__ __launch_bounds__(SH ? 256 : (LD ? 128 : 64), LD ? 2 : 1) void map_fo
   for (unsigned long long ch = 0; ch < nch; ++ch) {
     const unsigned slot = (unsigned)(ch % NB);
     const u64 *buf = wl + slot * SLOT;
+    const u64 *sp1 = wl + NB * SLOT + slot * SLOT;  // SP: the partner's half of the chunk (buf: wave 0's)
     const u64 *vb = vbase + slot * C * VI;
     const u64 *shx = shr;  // SH: chunk ch's shared slot (clock rows, clock max)
     if constexpr (RS) {
@@ -1520,12 +1891,9 @@ __global__ __launch_bounds__(SH ? 256 : (LD ? 128 : 64), LD ? 2 : 1) void map_fo
         }
         MAP_TOCK(cy_arr);
         MAP_TICK();
-      } else if constexpr (LD) {  // chunk ch's arrival flag (its last piece)
-        unsigned spins = 0;
-        while (!ld_late && __builtin_amdgcn_readfirstlane(*reinterpret_cast<const volatile unsigned *>(cms + A)) !=
-                               (unsigned)(ch + 1)) {
-          if (++spins > kLdSpin) ld_late = true;
-        }
+      } else if constexpr (SP) {  // 9 pieces per chunk (sp_chunk_glds)
+        if (ch + 1 < nch) wait_vmcnt<9>();
+        else wait_vmcnt<0>();
       } else {
         if (ch + 1 < nch) {
           if (vpiece) wait_vmcnt<P1>();
@@ -1541,23 +1909,24 @@ __global__ __launch_bounds__(SH ? 256 : (LD ? 128 : 64), LD ? 2 : 1) void map_fo
         sh_reload(rA, img, shs, A, lane);
         // next chunk's arrival count, read with this chunk's slots
         pre_raw = *reinterpret_cast<const volatile unsigned *>(arr + (sh_use + 1 == kShS ? 0 : sh_use + 1));
+      } else if constexpr (SP) {
+        sp_reload(rA, img, cms, A, lane, 0);
       } else {
         rs_reload(rA, img, WS, vsl, cms, A, lane, vpiece);
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot is read: refill it
       if constexpr (SH) sh_pre = __builtin_amdgcn_readfirstlane(pre_raw);
-      if constexpr (LD) {
-        if (lane == 0) *reinterpret_cast<volatile unsigned *>(rel + slot) = (unsigned)(ch + 1);
-      }
       // a whole next chunk with every lane moving a piece: its pieces go out during the test
       const unsigned long long i2 = (ch + 2) * C;
-      const bool spread = !LD && el && ch + 2 < nch && i2 + C <= R && (2 + VI) * A == 128 && (!SH || ch + kShD < nch);
+      const bool spread = el && ch + 2 < nch && i2 + C <= R && (2 + VI) * A == 128 && (!SH || ch + kShD < nch);
       if constexpr (SH) {
         if (!spread) {
           if (ch + 2 < nch) sh_chunk_images(shl, i2, R, img);
           if (ch + kShD < nch) sh_chunk_shared(p, shl, g, ch + kShD, R, wv, shr + sh_iss * kShShared, lane);
         }
-      } else if constexpr (!LD) {
+      } else if constexpr (SP) {
+        if (ch + 2 < nch && !spread) sp_chunk_glds(p, spl, g, ch + 2, R, img, cms, lane);
+      } else {
         if (ch + 2 < nch && !spread)
           map_chunk_glds<VI, C, 1>(p, gl1, g, k, i2, R, img, WS, vsl, cms, lane, vpiece, p.diag);
       }
@@ -1576,7 +1945,19 @@ __global__ __launch_bounds__(SH ? 256 : (LD ? 128 : 64), LD ? 2 : 1) void map_fo
       }
       MAP_TICK();
       bool skip = false;
-      if (SH && spread) {
+      if constexpr (SP) {  // this half's partial masks, exchanged with the partner wave's: one verdict
+        const bool batch = MAP_BATCH_ONLY || p.batch;
+        RsPart<2, MAP_REG_NQ> part;
+        if (spread) {
+          SpDma d{spl.base + (i2 + spl.b) * spl.rs, 2 * spl.rs, img, p.cmax + (g * p.nch + ch + 2) * A + 2 * lane, cms,
+                  (unsigned long long)(2 * lane) < A};
+          part = batch ? sp_reg_part<true>(rA, rg, present, nv, true, d) : sp_reg_part<false>(rA, rg, present, nv, true, d);
+        } else {
+          part = batch ? sp_reg_part<true>(rA, rg, present, nv, el) : sp_reg_part<false>(rA, rg, present, nv, el);
+        }
+        const u64 verdict = present ? sp_vote<true>(vw + 8 * slot, part, 0, lane) : sp_vote<false>(vw + 8 * slot, part, 0, lane);
+        skip = (verdict & want) == want;
+      } else if (SH && spread) {
         const unsigned long long ic = (ch + kShD) * C + 4 * wv + shl.sub;
         ShDma d{{shl.b[0] + (i2 + shl.sub) * shl.st[0], shl.b[1] + (i2 + shl.sub) * shl.st[1],
                  shl.b[2] + (i2 + shl.sub) * shl.st[2]},
@@ -1617,16 +1998,9 @@ __global__ __launch_bounds__(SH ? 256 : (LD ? 128 : 64), LD ? 2 : 1) void map_fo
           for (int h = 0; h < 2; ++h) rg.cs[m][h] = rg.cs[m][h] > rA.cmp[m][h] ? rg.cs[m][h] : rA.cmp[m][h];
         continue;
       }
-      if constexpr (LD) {  // the loader's copy of chunk ch+2 into this slot must land before it is overwritten
-        unsigned spins = 0;
-        while (!ld_late && ch + 2 < nch &&
-               __builtin_amdgcn_readfirstlane(*reinterpret_cast<const volatile unsigned *>(cms + A)) !=
-                   (unsigned)(ch + 3)) {
-          if (++spins > kLdSpin) ld_late = true;
-        }
-      }
       wait_vmcnt<0>();
       if constexpr (SH) sh_store(rA, img, lane);
+      else if constexpr (SP) sp_store(rA, img, cms, A, lane);
       else rs_store(rA, img, WS, vsl, cms, A, lane, vpiece);
       if (!vpiece && lane < C * VI) {  // the chunk's values, fetched now (a chunk the exact loop runs)
         const unsigned long long iv = ch * C + lane / VI;
@@ -1638,6 +2012,7 @@ __global__ __launch_bounds__(SH ? 256 : (LD ? 128 : 64), LD ? 2 : 1) void map_fo
         const u64 lo = cs[0] < m1 ? cs[0] : m1;
         thr[lane] = e[0] > lo ? e[0] : lo;
       }
+      if constexpr (SP) sp_barrier();  // (A) both halves are back in LDS: the exact loop reads the whole chunk
     }
     if constexpr (GL) {
       // issue chunk ch+NB-1 into the slot chunk ch-1 used, then wait for chunk ch
@@ -1693,7 +2068,9 @@ __global__ __launch_bounds__(SH ? 256 : (LD ? 128 : 64), LD ? 2 : 1) void map_fo
 #pragma unroll
             for (int t = 0; t < VI; ++t) r.v[t] = 0;
             noop = rs_lds_own_noop<VI, NP, true>(r, mirror, thr, A, present, nv, lane);
-          } else if constexpr (RS)
+          } else if constexpr (SP)
+            noop = sp_lds_noop(buf, sp1, mirror, thr, A, present, nv, lane);
+          else if constexpr (RS)
             noop = rs_lds_noop_nv<VI, (RS ? NP : 1)>(buf, WS, mirror, thr, A, present, nv, lane);
           else
             noop = (p.scan3 && GL) ? map_noop_nv3<VI, LPS, ITM>(buf, (unsigned)WS, (unsigned)A, mirror, thr,
@@ -1717,7 +2094,9 @@ __global__ __launch_bounds__(SH ? 256 : (LD ? 128 : 64), LD ? 2 : 1) void map_fo
             u64 mx = cs[0];
 #pragma unroll
             for (int u = 0; u < C; ++u) {
-              const u64 co = SH ? shx[sh_cword(u, (unsigned)a)] : buf[u * WS + (1 + VI) * A + a];
+              const u64 co = SH   ? shx[sh_cword(u, (unsigned)a)]
+                             : SP ? (a < 16 ? buf : sp1)[sp_word(u, 3, (unsigned)a & 15)]
+                                  : buf[u * WS + (1 + VI) * A + a];
               const u64 take = ((unsigned long long)u >= s && (unsigned long long)u < j) ? ~0ull : 0ull;
               const u64 x = co & take;
               mx = mx > x ? mx : x;
@@ -1752,6 +2131,16 @@ __global__ __launch_bounds__(SH ? 256 : (LD ? 128 : 64), LD ? 2 : 1) void map_fo
 #pragma unroll
         for (int t = 0; t < VI; ++t) in.c[t][0] = on ? buf[pw + 128 * (1 + t)] : 0;
         in.co[0] = on ? shx[sh_cword((unsigned)s, (unsigned)lane)] : 0;
+#pragma unroll
+        for (int t = 0; t < VI; ++t) in.v[t] = vb[s * VI + t];
+      } else if constexpr (SP) {  // lane = actor: the word of its half (actors >= A: zero)
+        const bool on = (unsigned long long)lane < A;
+        const u64 *hb = lane < 16 ? buf : sp1;
+        const unsigned a = (unsigned)lane & 15;
+        in.e[0] = on ? hb[sp_word((unsigned)s, 0, a)] : 0;
+#pragma unroll
+        for (int t = 0; t < VI; ++t) in.c[t][0] = on ? hb[sp_word((unsigned)s, 1 + t, a)] : 0;
+        in.co[0] = on ? hb[sp_word((unsigned)s, 1 + VI, a)] : 0;
 #pragma unroll
         for (int t = 0; t < VI; ++t) in.v[t] = vb[s * VI + t];
       } else {
@@ -2000,18 +2389,22 @@ __global__ __launch_bounds__(SH ? 256 : (LD ? 128 : 64), LD ? 2 : 1) void map_fo
 #pragma unroll
           for (int q = 0; q < 3; ++q) rg.sq[q][m] = q < nvx ? lds2(mirror + (1 + q) * A + a) : u64x2{0, 0};
         }
+        if constexpr (SP) {  // (B) the partner reloads its operands from the same mirror
+          if (lane == 0) *reinterpret_cast<volatile unsigned *>(spst) = (present ? 1u : 0u) | ((unsigned)nvx << 1);
+          sp_barrier();
+        }
       }
       // re-issue chunk ch+2 into the slot the exact loop used
       if (SH && ch + 2 < nch) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         sh_chunk_images(shl, (ch + 2) * C, R, wl + slot * SLOT);
+      } else if (SP && ch + 2 < nch) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        sp_chunk_glds(p, spl, g, ch + 2, R, wl + slot * SLOT, cml + slot * CMS, lane);
       } else if (ch + 2 < nch) {
-        if constexpr (LD) {  // the flag reads "not landed" until this re-issued copy lands
-          if (lane == 0) cml[slot * CMS + A] = 0;
-        }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         map_chunk_glds<VI, C, 1>(p, gl1, g, k, (ch + 2) * C, R, wl + slot * SLOT, WS, vbase + slot * C * VI,
-                                 cml + slot * CMS, lane, vpiece, p.diag, LD ? p.seq : nullptr);
+                                 cml + slot * CMS, lane, vpiece, p.diag);
       }
     }
     if constexpr (!GL && !RS) {
@@ -2071,7 +2464,7 @@ __global__ __launch_bounds__(SH ? 256 : (LD ? 128 : 64), LD ? 2 : 1) void map_fo
       p.o_vval[gk * p.Vout + o] = v;
     }
     if (p.o_nval) p.o_nval[gk] = present ? (unsigned)nv : 0u;
-    const unsigned f = (unsigned)ovf | (bad ? 2u : 0u) | ((sh_late || ld_late) ? 8u : 0u);
+    const unsigned f = (unsigned)ovf | (bad ? 2u : 0u) | (sh_late ? 8u : 0u);
     if (f) atomicOr(p.o_flags + g, f);
   }
 }
@@ -2084,9 +2477,8 @@ using namespace crdt;
 // chunk the fold skips entirely (one block per (group, chunk), lane = actor).
 __global__ __launch_bounds__(64) void map_chunk_max_kernel(const u64 *clock, long long c_rs, long long c_gs,
                                                            unsigned long long R, unsigned long long A,
-                                                           unsigned long long nch, unsigned C, u64 *out, u64 *seq) {
+                                                           unsigned long long nch, unsigned C, u64 *out) {
   const unsigned long long g = blockIdx.x / nch, ch = blockIdx.x % nch;
-  if (seq && g == 0 && threadIdx.x < 2) seq[2 * ch + threadIdx.x] = ch + 1;  // the LD path's arrival flags
   const unsigned long long i0 = ch * C, i1 = R < i0 + C ? R : i0 + C;
   for (unsigned long long a = threadIdx.x; a < A; a += 64) {
     u64 m = 0;
@@ -2098,22 +2490,24 @@ __global__ __launch_bounds__(64) void map_chunk_max_kernel(const u64 *clock, lon
   }
 }
 
-template <int APL, int VI, int VO, int CM, int NB, bool GL, int ITM, int NP = 0, bool LD = false>
+template <int APL, int VI, int VO, int CM, int NB, bool GL, int ITM, int NP = 0, bool SP = false>
 static hipError_t launch_map_it(const MapPlan &p, unsigned long long blocks, hipStream_t s) {
   constexpr bool RS = NP > 0;
   constexpr int C = (GL || RS) ? CM : MapChunk<APL, VI, CM>::C;
   const size_t W = (2 + VI) * p.A;
-  const size_t lds = (size_t)NB * C * (map_ws(W) + VI) * sizeof(u64) + kMapL * 2 * sizeof(unsigned) +
-                     (2 + VO) * p.A * sizeof(u64) + ((GL || RS) ? NB * (p.A + (LD ? 2 : 0)) * sizeof(u64) : 0) +
-                     4 * p.A * sizeof(u64) + (LD ? sizeof(u64) : 0);
+  // (the kernel's PW: slots, values, remove lists, mirror, clock-max copies, thresholds, SP words)
+  const size_t slots = SP ? 2 * NB * (size_t)kSpSlot : (size_t)NB * C * map_ws(W);
+  const size_t lds = (slots + (size_t)NB * C * VI) * sizeof(u64) + kMapL * 2 * sizeof(unsigned) +
+                     (2 + VO) * p.A * sizeof(u64) + ((GL || RS) ? (SP ? 2 : 1) * NB * p.A * sizeof(u64) : 0) +
+                     4 * p.A * sizeof(u64) + (SP ? 18 * sizeof(u64) : 0);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
-  auto *fn = &map_fold_kernel<APL, VI, VO, CM, NB, GL, ITM, NP, false, LD>;
+  auto *fn = &map_fold_kernel<APL, VI, VO, CM, NB, GL, ITM, NP, false, SP>;
   if (lds > 64 * 1024) {  // beyond the default dynamic-LDS limit (gfx950 has 160 KB per CU)
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(LD ? 128 : 64), lds, s, p);
+  hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(SP ? 128 : 64), lds, s, p);
   return hipGetLastError();
 }
 
@@ -2121,8 +2515,10 @@ static hipError_t launch_map_it(const MapPlan &p, unsigned long long blocks, hip
 // step so the LDS scans of the exact loop unroll ceil(A / 4) iterations.
 template <int VI>
 static hipError_t launch_map_rs(const MapPlan &p, unsigned long long blocks, hipStream_t s) {
-  // the loader-wave form where every lane moves a piece of every step image (config 4's shape)
-  if (p.seq && (2 + VI) * p.A == 128 && p.lazyv) return launch_map_it<1, VI, 4, 16, 2, false, 8, 4, true>(p, blocks, s);
+  // two waves per key at config 4's shape (A = 32, V = 2)
+  if constexpr (VI == 2) {
+    if (p.sp && p.A == 32) return launch_map_it<1, 2, 4, 16, 2, false, 4, 2, true>(p, blocks, s);
+  }
   if (p.A <= 8) return launch_map_it<1, VI, 4, 16, 2, false, 2, 1>(p, blocks, s);
   if (p.A <= 16) return launch_map_it<1, VI, 4, 16, 2, false, 4, 2>(p, blocks, s);
   return launch_map_it<1, VI, 4, 16, 2, false, 8, 4>(p, blocks, s);
@@ -2261,8 +2657,8 @@ static int map_lub_impl(crdt_ctx *ctx, const crdt_map_batch *in, const u64 *doff
   // scratch: [def_off copy | chunk clock maxima]
   const size_t off_b = D > 0 || doff ? ((G + 1) * sizeof(size_t) + 255) / 256 * 256 : 0;
   if (glds) p.nch = (R + gC - 1) / gC;
-  const bool ld = rs && ctx->tune.map_ld && !(ctx->tune.map_sh && A == 32 && V == 2 && K % 4 == 0);
-  const size_t cm_b = glds ? G * p.nch * A * sizeof(u64) + (ld ? p.nch * 2 * sizeof(u64) : 0) : 0;
+  p.sp = rs && ctx->tune.map_sp && A == 32 && V == 2 && !(ctx->tune.map_sh && K % 4 == 0);
+  const size_t cm_b = glds ? G * p.nch * A * sizeof(u64) : 0;
   if (off_b + cm_b > 0)
     if (int rc = ensure_scratch(ctx, off_b + cm_b)) return rc;
   if (doff && D == 0)  // no pool: only the offsets' check (every entry must be 0)
@@ -2290,10 +2686,8 @@ static int map_lub_impl(crdt_ctx *ctx, const crdt_map_batch *in, const u64 *doff
   if (glds) {
     u64 *cm = reinterpret_cast<u64 *>(static_cast<char *>(ctx->scratch) + off_b);
     p.cmax = cm;
-    p.seq = ld ? cm + G * p.nch * A : nullptr;
     hipLaunchKernelGGL(map_chunk_max_kernel, dim3((unsigned)(G * p.nch)), dim3(64), 0, ctx->stream, p.clock,
-                       p.c_rs, p.c_gs, (unsigned long long)R, (unsigned long long)A, p.nch, gC, cm,
-                       const_cast<u64 *>(p.seq));
+                       p.c_rs, p.c_gs, (unsigned long long)R, (unsigned long long)A, p.nch, gC, cm);
     if (rs && ctx->tune.map_sh && A == 32 && V == 2 && K % 4 == 0)
       he = launch_map_sh(p, blocks, ctx->stream);
     else if (rs)

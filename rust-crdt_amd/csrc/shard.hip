@@ -171,6 +171,23 @@ static int sbuf(crdt_ctx *ctx, int i, size_t bytes, void **out) {
   return CRDT_OK;
 }
 
+// The check words of the last call on an agreed plan (shard_host.hpp PlanCache): every rank holds the
+// same reduced words, so every rank fails the same call here, before any collective of it, and forgets
+// its agreed plans (the next calls agree again).  Run after the call's local fold is issued (the
+// wait for the earlier call's exchange then overlaps this call's fold).
+static int check_pending(crdt_ctx *ctx) {
+  if (!ctx->chk_pending) return CRDT_OK;
+  ctx->chk_pending = false;
+  CRDT_HIP(ctx, hipEventSynchronize(ctx->chk_ev));
+  const uint64_t *r = ctx->chk_host + 3;
+  if (shard_host::check_ok(r, ctx->chk_key)) return CRDT_OK;
+  ctx->plans.clear();
+  return fail(ctx, CRDT_ECOMM, "an earlier sharded call on an agreed plan failed: %s; its outputs are unspecified "
+              "(every rank reports this at its next sharded call or crdt_ctx_synchronize)",
+              r[0] ? "some rank failed its validation (see that rank's crdt_last_error)"
+                   : "the ranks called different plans");
+}
+
 static int need_comm(crdt_ctx *ctx) {
   if (!ctx->comm && !ctx->has_ops)
     return fail(ctx, CRDT_EINVAL, "sharded call without crdt_ctx_comm_init / crdt_ctx_comm_init_ops");
@@ -242,6 +259,15 @@ static Hdr make_hdr(int st, uint64_t tag, std::initializer_list<uint64_t> dims) 
 }
 
 static void comm_release(crdt_ctx *ctx) {
+  if (ctx->chk_ev) (void)hipEventSynchronize(ctx->chk_ev);
+  if (ctx->chk_dev) (void)hipFree(ctx->chk_dev);
+  if (ctx->chk_host) (void)hipHostFree(ctx->chk_host);
+  if (ctx->chk_ev) (void)hipEventDestroy(ctx->chk_ev);
+  ctx->chk_dev = nullptr;
+  ctx->chk_host = nullptr;
+  ctx->chk_ev = nullptr;
+  ctx->chk_pending = false;
+  ctx->plans.clear();
   if (ctx->astream) (void)hipStreamSynchronize(ctx->astream);
   if (ctx->a_dev) (void)hipFree(ctx->a_dev);
   if (ctx->a_host) (void)hipHostFree(ctx->a_host);
@@ -260,6 +286,10 @@ static int agree_setup(crdt_ctx *ctx) {
   comm_release(ctx);
   ctx->comm_release = comm_release;
   CRDT_HIP(ctx, hipHostMalloc(&ctx->a_host, rows * kHdr * 8, hipHostMallocDefault));
+  CRDT_HIP(ctx, hipMalloc(&ctx->chk_dev, 3 * 8));
+  CRDT_HIP(ctx, hipHostMalloc(reinterpret_cast<void **>(&ctx->chk_host), 6 * 8, hipHostMallocDefault));
+  CRDT_HIP(ctx, hipEventCreateWithFlags(&ctx->chk_ev, hipEventDisableTiming));
+  ctx->comm_check = check_pending;
   if (ctx->comm) {
     CRDT_HIP(ctx, hipMalloc(&ctx->a_dev, rows * kHdr * 8));
     CRDT_HIP(ctx, hipStreamCreateWithFlags(&ctx->astream, hipStreamNonBlocking));
@@ -282,6 +312,7 @@ static int agree_mark(crdt_ctx *ctx) {
 static int agree_exchange(crdt_ctx *ctx, const Hdr &mine);
 // Host wall time of the header round trip is recorded as "shard_agree" (bench.py reports it).
 static int agree(crdt_ctx *ctx, int st, const Hdr &mine, const char *what) {
+  CRDT_TRY(check_pending(ctx));
   const auto t0 = std::chrono::steady_clock::now();
   const int xr = agree_exchange(ctx, mine);
   timing_add_host(ctx, "shard_agree",
@@ -290,7 +321,11 @@ static int agree(crdt_ctx *ctx, int st, const Hdr &mine, const char *what) {
   const size_t W = (size_t)ctx->nranks;
   const uint64_t *h = static_cast<const uint64_t *>(ctx->a_host);
   long bad_rank, odd_rank;
-  if (shard_host::check_headers(h, W, mine, &bad_rank, &odd_rank)) return CRDT_OK;
+  if (shard_host::check_headers(h, W, mine, &bad_rank, &odd_rank)) {
+    ctx->plans.add(shard_host::plan_key(mine));
+    return CRDT_OK;
+  }
+  ctx->plans.clear();
   if (bad_rank >= 0) {
     if (st != CRDT_OK) return st;  // this rank's own error text is in last_error
     return fail(ctx, CRDT_ECOMM, "%s: another rank (%ld) failed its validation (see that rank's "
@@ -322,6 +357,29 @@ static int agree_exchange(crdt_ctx *ctx, const Hdr &mine) {
     return CRDT_OK;
   }
   if (int rc = ctx->ops.allgather(ctx->ops.user, send_h, h, kHdr * 8)) return ops_fail(ctx, rc, "allgather");
+  return CRDT_OK;
+}
+
+// The agreed-plan path (shard_host.hpp PlanCache): this rank's plan was agreed by an earlier call and
+// the exchange is MAX all-reduces.  No header exchange; the data collectives run whatever this rank's
+// own status (a rank that failed its validation joins with zero partials), and the check words go in
+// the same group.  Their copy back is verified at the next sharded call (check_pending).
+static bool plan_agreed(crdt_ctx *ctx, const Hdr &mine) {
+  return !ctx->tune.shagree && ctx->chk_dev && ctx->plans.has(shard_host::plan_key(mine));
+}
+
+static int check_issue(crdt_ctx *ctx, int st, const Hdr &mine) {
+  const uint64_t key = shard_host::plan_key(mine);
+  shard_host::check_words(st != CRDT_OK, key, ctx->chk_host);
+  CRDT_HIP(ctx, hipMemcpyAsync(ctx->chk_dev, ctx->chk_host, 3 * 8, hipMemcpyHostToDevice, ctx->stream));
+  return CRDT_OK;
+}
+
+static int check_finish(crdt_ctx *ctx, const Hdr &mine) {
+  CRDT_HIP(ctx, hipMemcpyAsync(ctx->chk_host + 3, ctx->chk_dev, 3 * 8, hipMemcpyDeviceToHost, ctx->stream));
+  CRDT_HIP(ctx, hipEventRecord(ctx->chk_ev, ctx->stream));
+  ctx->chk_key = shard_host::plan_key(mine);
+  ctx->chk_pending = true;
   return CRDT_OK;
 }
 
@@ -372,7 +430,27 @@ static int lattice_sharded(crdt_ctx *ctx, Op op, const u64 *in, size_t G, size_t
       if (!st) st = lattice_lub_many(ctx, op, in, G, R, W, row_stride, group_stride, (u64 *)part, W, 0);
     }
   }
-  CRDT_TRY(agree(ctx, st, make_hdr(st, op == Op::Max ? kTagMax : kTagOr, {G, W}), what));
+  const Hdr hd = make_hdr(st, op == Op::Max ? kTagMax : kTagOr, {G, W});
+  if (op == Op::Max && n && plan_agreed(ctx, hd)) {  // an agreed plan: the data all-reduce + check words
+    CRDT_TRY(check_pending(ctx));
+    u64 *buf = out;
+    if (st != CRDT_OK || !out) {  // (this rank failed its validation: it joins with a zero partial)
+      void *z = nullptr;
+      CRDT_TRY(sbuf(ctx, 0, n * 8, &z));
+      CRDT_HIP(ctx, hipMemsetAsync(z, 0, n * 8, ctx->stream));
+      buf = (u64 *)z;
+    }
+    CRDT_TRY(check_issue(ctx, st, hd));
+    timing_begin(ctx, "shard_exchange");
+    CRDT_TRY(coll_group_begin(ctx));
+    CRDT_TRY(coll_allreduce(ctx, buf, buf, n, Red::Max));
+    CRDT_TRY(coll_allreduce(ctx, (const u64 *)ctx->chk_dev, (u64 *)ctx->chk_dev, 3, Red::Max));
+    CRDT_TRY(coll_group_end(ctx));
+    timing_end(ctx);
+    CRDT_TRY(check_finish(ctx, hd));
+    return st;
+  }
+  CRDT_TRY(agree(ctx, st, hd, what));
   if (n == 0) return CRDT_OK;
   if (op == Op::Max) {
     timing_begin(ctx, "shard_exchange");
@@ -803,6 +881,7 @@ int crdt_lub_many_multi_sharded(crdt_ctx *ctx, const crdt_lub_segment *segs, siz
   int st = device_mem_only(ctx, what);
   std::vector<LubReq> reqs;
   if (!st) st = lub_reqs_from_segments(ctx, segs, nseg, reqs);
+  const bool parsed = reqs.size() == nseg;
   std::vector<LubReq> maxr;
   uint64_t dh = 0x9e3779b97f4a7c15ull;  // hash of every segment's (op, G, W)
   for (auto &q : reqs) {
@@ -813,7 +892,36 @@ int crdt_lub_many_multi_sharded(crdt_ctx *ctx, const crdt_lub_segment *segs, siz
     for (uint64_t d : {(uint64_t)q.op, (uint64_t)q.G, (uint64_t)q.W}) dh = (dh ^ d) * 0x100000001b3ull;
   }
   if (!st) st = lattice_lub_many_multi(ctx, maxr.data(), maxr.size());
-  CRDT_TRY(agree(ctx, st, make_hdr(st, kTagMulti, {(uint64_t)reqs.size(), dh}), what));
+  const Hdr hd = make_hdr(st, kTagMulti, {(uint64_t)reqs.size(), dh});
+  if (parsed && maxr.size() == reqs.size() && plan_agreed(ctx, hd)) {  // an agreed plan (max segments only)
+    CRDT_TRY(check_pending(ctx));
+    std::vector<u64 *> bufs;
+    if (st != CRDT_OK) {  // (this rank failed its validation: it joins with zero partials of the same sizes)
+      size_t tot = 0;
+      for (auto &q : maxr) tot += q.G * q.W;
+      void *z = nullptr;
+      CRDT_TRY(sbuf(ctx, 0, (tot ? tot : 1) * 8, &z));
+      CRDT_HIP(ctx, hipMemsetAsync(z, 0, tot * 8, ctx->stream));
+      size_t o = 0;
+      for (auto &q : maxr) {
+        bufs.push_back((u64 *)z + o);
+        o += q.G * q.W;
+      }
+    } else {
+      for (auto &q : maxr) bufs.push_back(q.out);
+    }
+    CRDT_TRY(check_issue(ctx, st, hd));
+    timing_begin(ctx, "shard_exchange");
+    CRDT_TRY(coll_group_begin(ctx));
+    for (size_t i = 0; i < maxr.size(); ++i)
+      CRDT_TRY(coll_allreduce(ctx, bufs[i], bufs[i], maxr[i].G * maxr[i].W, Red::Max));
+    CRDT_TRY(coll_allreduce(ctx, (const u64 *)ctx->chk_dev, (u64 *)ctx->chk_dev, 3, Red::Max));
+    CRDT_TRY(coll_group_end(ctx));
+    timing_end(ctx);
+    CRDT_TRY(check_finish(ctx, hd));
+    return st;
+  }
+  CRDT_TRY(agree(ctx, st, hd, what));
   timing_begin(ctx, "shard_exchange");
   CRDT_TRY(coll_group_begin(ctx));
   for (auto &q : maxr) CRDT_TRY(coll_allreduce(ctx, q.out, q.out, q.G * q.W, Red::Max));

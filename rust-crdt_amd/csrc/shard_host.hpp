@@ -50,6 +50,44 @@ inline bool check_headers(const uint64_t *rows, size_t W, const Hdr &mine, long 
   return *failed_rank < 0 && *mismatch_rank < 0;
 }
 
+// Agreed plans (round 6).  A plan is an entry point with its dims: the key of a header hashes its tag
+// and dims hash.  Once the ranks agreed a plan (the header all-gather above found every rank valid
+// and equal), later calls with that plan skip the header exchange: they all-reduce (MAX) three check
+// words [failed, key, ~key] beside their data instead, and every rank verifies the reduced words at
+// its next sharded call (or crdt_ctx_synchronize).  All ranks see the same reduced words, so all reach
+// the same verdict at the same call: any rank failed, or ranks sent different keys (max(key) == key
+// and max(~key) == ~key on a rank only if every rank sent that key).
+inline uint64_t plan_key(const Hdr &h) { return (h.w[1] * 0x9E3779B97F4A7C15ull) ^ h.w[kHdr - 1]; }
+
+struct PlanCache {
+  static constexpr int kCap = 16;
+  uint64_t key[kCap] = {};
+  int n = 0;
+  bool has(uint64_t k) const {
+    for (int i = 0; i < n; ++i)
+      if (key[i] == k) return true;
+    return false;
+  }
+  void add(uint64_t k) {
+    if (has(k)) return;
+    if (n == kCap) {  // oldest out
+      for (int i = 1; i < kCap; ++i) key[i - 1] = key[i];
+      --n;
+    }
+    key[n++] = k;
+  }
+  void clear() { n = 0; }
+};
+
+inline void check_words(bool failed, uint64_t key, uint64_t *w) {
+  w[0] = failed ? 1 : 0;
+  w[1] = key;
+  w[2] = ~key;
+}
+inline bool check_ok(const uint64_t *reduced, uint64_t key) {
+  return reduced[0] == 0 && reduced[1] == key && reduced[2] == ~key;
+}
+
 // Orswot deferred regrouping: cnt[W][G+1] are the gathered per-group counts (entry G = the rank's
 // total), the all-gathered rows sit rank-major with rank r's rows of group g at
 // r*Dmax + (r's rows of the groups before g) + j.  Group g gathers rank 0's rows of g, then rank

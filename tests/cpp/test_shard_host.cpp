@@ -1,6 +1,7 @@
 // Unit tests of the host-side bookkeeping of the sharded entry points (csrc/shard_host.hpp), built
 // with g++ -fsanitize=address,undefined by tests/test_sanitizers.py.  Every function is checked
 // against a brute-force restatement on random inputs; any failed check aborts with a message.
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <random>
@@ -127,8 +128,42 @@ static void test_map_flags(std::mt19937_64 &rng) {
   CHECK(hash_offsets(off1, 3) != hash_offsets(off2, 3) && hash_offsets(off1, 3) == hash_offsets(off1, 3));
 }
 
+// Agreed-plan cache and the cached path's check words: the MAX over ranks of [failed, key, ~key] passes
+// on every rank iff every rank sent the same key and none failed.
+static void test_plan_cache(std::mt19937_64 &rng) {
+  PlanCache c;
+  for (uint64_t k = 0; k < 40; ++k) {
+    c.add(k * 7 + 1);
+    CHECK(c.has(k * 7 + 1) && c.n <= PlanCache::kCap);
+  }
+  CHECK(!c.has(1) && c.has(39 * 7 + 1));  // the oldest plans left the full cache
+  c.add(39 * 7 + 1);
+  CHECK(c.n == PlanCache::kCap);  // no duplicate
+  c.clear();
+  CHECK(c.n == 0 && !c.has(39 * 7 + 1));
+  const Hdr a = make_hdr(false, 1, {4, 256}), b = make_hdr(true, 1, {4, 256}), d = make_hdr(false, 1, {4, 254});
+  CHECK(plan_key(a) == plan_key(b) && plan_key(a) != plan_key(d));  // a rank's own status is not in the key
+  CHECK(plan_key(a) != plan_key(make_hdr(false, 2, {4, 256})));
+  for (int it = 0; it < 500; ++it) {
+    const size_t W = 1 + rng() % 8;
+    const uint64_t key = rng();
+    std::vector<uint64_t> red(3, 0), w(3);
+    bool failed = false, odd = false;
+    for (size_t r = 0; r < W; ++r) {
+      const bool f = rng() % 5 == 0;
+      const uint64_t k = rng() % 4 == 0 ? rng() : key;
+      failed = failed || f;
+      odd = odd || k != key;
+      check_words(f, k, w.data());
+      for (int j = 0; j < 3; ++j) red[j] = std::max(red[j], w[j]);
+    }
+    CHECK(check_ok(red.data(), key) == (!failed && !odd));
+  }
+}
+
 int main() {
   std::mt19937_64 rng(0x5EED);
+  test_plan_cache(rng);
   test_regroup(rng);
   test_headers(rng);
   test_lww_nonempty(rng);

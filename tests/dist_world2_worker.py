@@ -267,11 +267,17 @@ def cabi_seam(rank, world, t, h):
         o["cabi_mapvstate_code"] = np.array([0], np.int64)
     except CrdtGpuError as e:
         o["cabi_mapvstate_code"] = np.array([e.code], np.int64)
-    # a bad argument on ONE rank: every rank raises, none blocks; then a good call still works
-    codes = []
+    # a bad argument on ONE rank, none blocks:
+    #  * on a plan the ranks agreed earlier (the vclock (G, W) above; the agreed-plan path runs no header
+    #    exchange): rank 1's NULL output travels in the check words, the call returns its own error on
+    #    rank 1 only, and EVERY rank reports ECOMM at its next sharded call, which runs no collective;
+    #  * on plans forgotten after that error (the header exchange): both ranks err in the same call;
+    #  * with shagree=1 (the exchange on every call): both ranks err in the call itself.
+    # Then good calls work again: the first agrees the plan, the next two take the agreed-plan path.
     x = t(D.lattice_input("vclock")[0])
     outb = torch.empty(x.shape[1], dtype=torch.int64, device=dev)
-    for bad in ("null_out", "dims"):
+
+    def bad_call(bad):
         try:
             if bad == "null_out":
                 ctx.call("crdt_vclock_lub_many_sharded", x.data_ptr(), 1, x.shape[0], x.shape[1], x.shape[1],
@@ -279,11 +285,21 @@ def cabi_seam(rank, world, t, h):
             else:
                 W = x.shape[1] if rank == 0 else x.shape[1] - 2
                 ctx.call("crdt_vclock_lub_many_sharded", x.data_ptr(), 1, x.shape[0], W, x.shape[1], 0, outb.data_ptr())
-            codes.append(0)
+            return 0
         except CrdtGpuError as e:
-            codes.append(e.code)
-    o["cabi_error_codes"] = np.array(codes, np.int64)
+            return e.code
+
+    o["cabi_error_codes"] = np.array([bad_call("null_out"), bad_call("dims"), bad_call("dims")], np.int64)
+    ctx.tune("shagree=1")
+    o["cabi_error_codes_sync"] = np.array([bad_call("null_out"), bad_call("dims")], np.int64)
+    ctx.tune("shagree=0")
+    ctx.timing_reset()
+    ctx.set_timing(True)
     o["cabi_after_errors"] = h(cs.lub_many_sharded("vclock", x, ctx=ctx))
+    o["cabi_after_errors_cached"] = np.stack([h(cs.lub_many_sharded("vclock", x, ctx=ctx)) for _ in range(2)])
+    ctx.synchronize()  # (verifies the last agreed-plan call's check words)
+    ctx.set_timing(False)
+    o["cabi_agree_calls"] = np.array([ctx.timing("shard_agree")[1], ctx.timing("shard_exchange")[1]], np.int64)
     # config 5 at full per-GPU size: rank k holds replicas [k*R, (k+1)*R) of the
     # 1,048,576-per-rank x 1,024-actor VClock input (bench.py --workload c5's shard), lub through
     # crdt_vclock_lub_many_sharded; the parent checks sampled actor columns against the oracle's fold

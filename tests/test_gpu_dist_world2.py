@@ -256,14 +256,22 @@ def test_world2_cabi_map_vstate_mismatch(outs):
 
 def test_world2_cabi_errors_agree(outs):
     """A NULL output on rank 1 (its own validation fails) and a row width that differs between the
-    ranks: EVERY rank returns an error instead of blocking in the all-reduce, and the communicator
-    still works afterwards."""
+    ranks: no rank blocks, every rank reports an error.  On a plan the ranks agreed earlier (no header
+    exchange, csrc/shard_host.hpp PlanCache) rank 1 errs in the call and every rank reports ECOMM at its
+    next sharded call; the plans are then forgotten and the width mismatch errs on both ranks in the
+    call; with shagree=1 both errors come in the call itself.  Afterwards the communicator works: one
+    header exchange for three good calls, the last two on the agreed plan, all equal to the oracle fold."""
     EINVAL, ECOMM = -1, -5
-    assert tuple(outs[0]["cabi_error_codes"]) == (ECOMM, EINVAL)
-    assert tuple(outs[1]["cabi_error_codes"]) == (EINVAL, EINVAL)
+    assert tuple(outs[0]["cabi_error_codes"]) == (0, ECOMM, EINVAL)
+    assert tuple(outs[1]["cabi_error_codes"]) == (EINVAL, ECOMM, EINVAL)
+    assert tuple(outs[0]["cabi_error_codes_sync"]) == (ECOMM, EINVAL)
+    assert tuple(outs[1]["cabi_error_codes_sync"]) == (EINVAL, EINVAL)
     exp = O.vclock_fold(D.lattice_input("vclock")[0])[0]
     for o in outs:
         np.testing.assert_array_equal(o["cabi_after_errors"], exp)
+        for r in o["cabi_after_errors_cached"]:
+            np.testing.assert_array_equal(r, exp)
+        assert tuple(o["cabi_agree_calls"]) == (1, 3)  # one header exchange, three data exchanges
 
 
 def test_world2_cabi_config5(outs):

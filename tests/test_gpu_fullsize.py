@@ -87,7 +87,18 @@ def test_config4_map_full_size(gpu_ctx):
     res = cg.map.lub_many(inp.clock, inp.ec, inp.vclk, inp.vval, def_off=[0, Dn],
                           def_row=torch.from_numpy(rows.astype(np.int32)).cuda(), def_clock=t(dcl),
                           def_keys=t(dks), vout=vout, ctx=gpu_ctx)
-    torch.cuda.synchronize()
+    # the one- and two-wave (msp) forms of the A = 32, V = 2 fold agree on the whole result
+    for spec in ("msp=0", "msp=1"):
+        alt = cg.Context(0)
+        alt.tune(spec)
+        res2 = cg.map.lub_many(inp.clock, inp.ec, inp.vclk, inp.vval, def_off=[0, Dn],
+                               def_row=torch.from_numpy(rows.astype(np.int32)).cuda(), def_clock=t(dcl),
+                               def_keys=t(dks), vout=vout, ctx=alt)
+        torch.cuda.synchronize()
+        for nm in ("clock", "ec", "vclk", "vval", "nval", "flags", "def_keep", "def_keys"):
+            assert torch.equal(getattr(res, nm), getattr(res2, nm)), (spec, nm)
+        del res2
+        alt.close()
     keys = np.sort(np.random.default_rng(5).choice(K, size=64, replace=False))
     tk = torch.from_numpy(keys).cuda()
     dev = {nm: u64(getattr(inp, nm) if nm == "clock" else getattr(inp, nm)[:, tk]) for nm in ("clock", "ec", "vclk", "vval")}
