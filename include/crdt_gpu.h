@@ -375,8 +375,9 @@ int crdt_map_counter_forget_batch(crdt_ctx *ctx, const crdt_map_counter_states *
  * op: the counter's op (vactor, vcounter) — a Dot — with vdir 0 = P (GCounter: always 0), 1 = N
  * (vdir may be NULL: all P) }, kind 1 = Op::Rm { clock: clk_pool[clk_row*A ..], keyset: keys[key_off[o]
  * .. key_off[o+1]) }.  status[s]: bit 0 = deferred slots exhausted, bit 1 = a malformed op / key
- * skipped, bits 2-3 = invalid input (state untouched).  Limits: A <= 512, Dcap * (A + Kw) <= 8192
- * words (the deferred slots live in LDS during the stream). */
+ * skipped, bits 2-3 = invalid input (state untouched).  Limits: A <= 512.  Dcap is not bounded:
+ * during the stream the first min(Dcap, 16) slots live in LDS and the rest are used in place in
+ * def_clock / def_keys (round 6: exact up to Dcap; bit 0 only past Dcap). */
 typedef struct crdt_map_counter_ops {
   size_t n_ops;
   const uint64_t *op_off;    /* [N+1]       */
@@ -425,8 +426,8 @@ int crdt_map_orswot_forget_batch(crdt_ctx *ctx, const crdt_map_orswot_states *st
  * key_off[o+1]) } (key_off may be NULL when no op is a Map Rm).  status[s]: bit 0 = a deferred list
  * (the Map's or a nested one) exhausted, bit 1 = a malformed op / key / member skipped, bits 2-3 =
  * invalid input (state untouched).  Nested removes whose clocks become equal under a Map-level
- * forget keep one entry, the later one's members (the fold's rule).  Limits: A <= 512, M <= 1,024,
- * Dcap * (A + Kw) + 256 <= 8192 words. */
+ * forget keep one entry, the later one's members (the fold's rule).  Limits: A <= 512, M <= 1,024;
+ * Dcap is not bounded (the Map's first min(Dcap, 16) slots in LDS, the rest in place, round 6). */
 typedef struct crdt_map_orswot_ops {
   size_t n_ops;
   const uint64_t *op_off;    /* [N+1]       */
@@ -885,7 +886,8 @@ int crdt_map_nested_lub_many_sharded(crdt_ctx *ctx, const crdt_map_nested_batch 
  *     mvreg.rs:88-104, emptied values dropped, order kept —, deferred removes, clocks), an emptied
  *     entry dropped; the outer deferred pool and the map clock as crdt_map_forget_batch.  Inner removes
  *     whose clocks become equal keep one entry with the later one's keys (the fold's rule).
- * Limits: A <= 512, K2 <= 64.  Device memory only. */
+ * Limits: A <= 512, K2 <= 64; the outer Dcap is not bounded (its first min(Dcap, 16) slots in LDS during
+ * an apply stream, the rest used in place, round 6).  Device memory only. */
 typedef struct crdt_map_nested_states {
   size_t N, K, K2, A;
   uint64_t *clock;    /* [N][A]           */

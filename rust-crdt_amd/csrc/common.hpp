@@ -68,7 +68,7 @@ struct Tune {
   int map_sh = 0;      // ... RS path at A = 32, V = 2, K % 4 == 0: four key waves share each chunk's clock
                        //     rows (less traffic, but slower: the coupled waves; opt-in)
   int map_lazyv = 1;   // ... RS path: values fetched only for chunks the exact loop runs (not streamed)
-  int map_sp = 0;      // ... RS path at A = 32, V = 2: two waves per key, each testing half the actors (SP)
+  int map_st = 0;      // ... RS path at A = 32, V = 2: two waves per key, each testing 8 steps of a chunk (ST)
   int shagree = 0;     // sharded calls: 1 = the validation-header exchange on every call (no agreed-plan path)
   int map_diag = 0;    // ... timing probes only, results WRONG (bit0: no clock-max piece, bit1: 3 fewer step pieces)
   int rows_blocks_per_cu = 0;  // row-pair / row-reduction kernels (causal.hip); 0 = per-kernel default

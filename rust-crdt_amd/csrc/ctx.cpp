@@ -219,7 +219,7 @@ static void apply_tune(crdt_ctx *ctx, const char *t) {
       else if (k == "mscan3") ctx->tune.map_scan3 = v != 0;
       else if (k == "mrs") ctx->tune.map_rs = v != 0;
       else if (k == "msh") ctx->tune.map_sh = v != 0;
-      else if (k == "msp") ctx->tune.map_sp = v != 0;
+      else if (k == "mst") ctx->tune.map_st = v != 0;
       else if (k == "shagree") ctx->tune.shagree = v != 0;
       else if (k == "mbatch") ctx->tune.map_batch = v != 0;
       else if (k == "mlazyv") ctx->tune.map_lazyv = v != 0;

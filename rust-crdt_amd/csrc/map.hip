@@ -66,7 +66,7 @@ struct MapPlan {
   int lazyv;  // RS path: the values of a chunk fetched only when the exact loop runs it
   int diag;   // timing probes (results wrong): bit0 no clock-max piece, bit1 3 fewer step pieces,
               // bit2 SH path without arrival waits
-  int sp;  // SP path (A = 32, V = 2 on the RS shapes): two waves per key, each testing half the actors
+  int st;  // ST path (A = 32, V = 2 on the RS shapes): two waves per key, each testing 8 steps of a chunk
 };
 
 constexpr int kMapQ = 4;    // deferred removes tracked per key in registers before the slow path
@@ -728,6 +728,24 @@ __device__ __forceinline__ bool mv_antichain(const MVState<APL, VO> &s) {
 // and a clock max (lane = actor, from the chunk's clock max); any other chunk (a failed test, a
 // remove naming the key, the scan's preconditions off) is written back over its slot and runs
 // through the exact per-step loop, after which chunk ch+2 is issued again.
+// MAP_VAN_MASK (build option): the chunk test's "incoming value forgotten to empty" (c2 <= deleted,
+// deleted = e2 > e ? e2 : 0) as a combination of ballots instead of a select then a compare.
+#ifndef MAP_VAN_MASK
+#define MAP_VAN_MASK 0
+#endif
+// MAP_TB_INC (build option): the register operands hold TB = max(e, min(Cs, m1)) itself instead of the
+// acc clock Cs, advanced on a skipped chunk by TB' = max(TB, min(chunk clock max, m1)) (min distributes
+// over max), so the chunk test no longer recomputes it (-24 VALU per chunk); reloaded from thr after
+// the exact loop.  RsReg::cs then holds TB.
+#ifndef MAP_TB_INC
+#define MAP_TB_INC 0
+#endif
+// The register operands' clock word after a skipped chunk (Cs, or TB under MAP_TB_INC).
+__device__ __forceinline__ u64 rs_adv(u64 cur, u64 cmax, u64 m1) {
+  if (MAP_TB_INC) cmax = cmax < m1 ? cmax : m1;
+  return cur > cmax ? cur : cmax;
+}
+
 template <int VI, int NP>
 struct RsChunk {
   u64x2 e[NP];
@@ -764,13 +782,17 @@ __device__ __forceinline__ unsigned rs_a0(int lane, int m) {
   return 2 * gq + 8 * m;
 }
 
-template <int NQ, bool PRESENT, int NP, bool PERM = false>
+// The ST path's layout (two waves per key, each testing 8 steps of a chunk): lane (s, g8) = (lane / 8,
+// lane % 8) holds actor pairs (2 g8 + 16 m, 2 g8 + 16 m + 1), m < 2.
+__device__ __forceinline__ unsigned st_a0(int lane, int m) { return 2 * ((unsigned)lane & 7) + 16 * m; }
+
+template <int NQ, bool PRESENT, int NP, bool PERM = false, int LPS = 4>
 __device__ __forceinline__ RsOwn<NQ, NP> rs_own(const u64 *mirror, const u64 *thr, unsigned long long A, int lane,
-                                                int nv = NQ, unsigned ab = 0) {
+                                                int nv = NQ) {
   RsOwn<NQ, NP> o;
 #pragma unroll
   for (int m = 0; m < NP; ++m) {
-    const unsigned a0 = ab + rs_a0<PERM>(lane, m);
+    const unsigned a0 = LPS == 8 ? st_a0(lane, m) : rs_a0<PERM>(lane, m);
     const unsigned long long a = a0 < A ? a0 : A - 2;
     o.tb[m] = lds2(thr + a);
     if constexpr (PRESENT) {
@@ -792,48 +814,18 @@ struct RsNoDma {
   __device__ __forceinline__ void operator()(int) {}
 };
 
-// The test's per-step partial results over one actor range (bit 4s: step s), its LPS lanes combined:
-// p2 "the replica has the key" (an OR over actors), the rest ANDs over actors — b the both-present
-// entry test, o the acc-only test, van[t] "incoming value t forgotten to empty", le[t][q] "incoming
-// value t <= own value q".  The SP path tests two actor halves in two waves and combines their parts
-// (p2 OR-ed, the rest AND-ed) before the verdict, which ORs over q: a verdict per half would be wrong.
+// The test's per-step results (bit LPS*s: step s), its LPS lanes combined: p2 "the replica has the
+// key" (an OR over actors), the rest ANDs over actors — b the both-present entry test, o the
+// acc-only test, van[t] "incoming value t forgotten to empty", le[t][q] "incoming value t <= own value
+// q"; rs_verdict then ORs over q.
 template <int VI, int NQ>
 struct RsPart {
   u64 p2, b, o, van[VI], le[VI][NQ > 0 ? NQ : 1];
 };
 
-template <int VI, int NQ>
-__device__ __forceinline__ RsPart<VI, NQ> rs_part_fail() {  // a range that settles nothing: verdict 0
-  RsPart<VI, NQ> x;
-  x.p2 = grp_mask<4>();  // (only bits 4s: the SP path packs four masks per word)
-  x.b = x.o = 0;
-#pragma unroll
-  for (int t = 0; t < VI; ++t) {
-    x.van[t] = 0;
-#pragma unroll
-    for (int q = 0; q < (NQ > 0 ? NQ : 1); ++q) x.le[t][q] = 0;
-  }
-  return x;
-}
-
-template <int VI, int NQ>
-__device__ __forceinline__ RsPart<VI, NQ> rs_part_join(const RsPart<VI, NQ> &x, const RsPart<VI, NQ> &y) {
-  RsPart<VI, NQ> z;
-  z.p2 = x.p2 | y.p2;
-  z.b = x.b & y.b;
-  z.o = x.o & y.o;
-#pragma unroll
-  for (int t = 0; t < VI; ++t) {
-    z.van[t] = x.van[t] & y.van[t];
-#pragma unroll
-    for (int q = 0; q < (NQ > 0 ? NQ : 1); ++q) z.le[t][q] = x.le[t][q] & y.le[t][q];
-  }
-  return z;
-}
-
-template <int VI, int NQ, bool PRESENT>
+template <int VI, int NQ, bool PRESENT, int LPS = 4>
 __device__ __forceinline__ u64 rs_verdict(const RsPart<VI, NQ> &x) {
-  const u64 G1 = grp_mask<4>();
+  const u64 G1 = grp_mask<LPS>();
   if constexpr (!PRESENT) return (~x.p2 | x.b) & G1;
   u64 both = x.p2 & x.b;
   const u64 only = ~x.p2 & x.o;
@@ -847,9 +839,8 @@ __device__ __forceinline__ u64 rs_verdict(const RsPart<VI, NQ> &x) {
   return (both | only) & G1;
 }
 
-template <int VI, int NP, int NQ, bool PRESENT, bool BATCH = false, class F = RsNoDma>
+template <int VI, int NP, int NQ, bool PRESENT, bool BATCH = false, int LPS = 4, class F = RsNoDma>
 __device__ __forceinline__ RsPart<VI, NQ> rs_part(const RsChunk<VI, NP> &r, const RsOwn<NQ, NP> &o, F &&dma = F{}) {
-  constexpr int LPS = 4;
   constexpr int ND = std::remove_reference_t<F>::count;  // pieces to issue: two per element, the rest after
   constexpr int NQ1 = NQ > 0 ? NQ : 1;
   // per-test ballot masks (bit = lane), combined per step at the end
@@ -891,11 +882,13 @@ __device__ __forceinline__ RsPart<VI, NQ> rs_part(const RsChunk<VI, NP> &r, cons
           const u64 co = r.co[m][h], ea = o.ea[m][h];
           const u64 bB1 = __ballot(ea - 1 >= co), bB2 = __ballot(ea == e2), bO = __ballot(co <= o.to[m][h]);
           const u64 del = e2 > ea ? e2 : 0;
+          const u64 bGt = MAP_VAN_MASK ? __ballot(e2 > ea) : 0;
           u64 bV[VI], bL[VI][NQ1];
 #pragma unroll
           for (int t = 0; t < VI; ++t) {
             const u64 c2 = r.c[t][m][h];
-            bV[t] = __ballot(c2 <= del);
+            // c2 <= deleted: (e2 > ea && c2 <= e2) || (e2 <= ea && c2 == 0), as masks (no select chain)
+            bV[t] = MAP_VAN_MASK ? (bGt & __ballot(c2 <= e2)) | (~bGt & __ballot(c2 == 0)) : __ballot(c2 <= del);
 #pragma unroll
             for (int q = 0; q < NQ; ++q) bL[t][q] = __ballot(c2 <= o.sq[q][m][h]);
           }
@@ -920,10 +913,11 @@ __device__ __forceinline__ RsPart<VI, NQ> rs_part(const RsChunk<VI, NP> &r, cons
         mB &= __ballot((e2 <= tb) & ((ea - 1 >= co) | (ea == e2)));
         mO &= __ballot(co <= o.to[m][h]);
         const u64 del = e2 > ea ? e2 : 0;
+        const u64 bGt = MAP_VAN_MASK ? __ballot(e2 > ea) : 0;
 #pragma unroll
         for (int t = 0; t < VI; ++t) {
           const u64 c2 = r.c[t][m][h];
-          mVan[t] &= __ballot(c2 <= del);
+          mVan[t] &= MAP_VAN_MASK ? (bGt & __ballot(c2 <= e2)) | (~bGt & __ballot(c2 == 0)) : __ballot(c2 <= del);
 #pragma unroll
           for (int q = 0; q < NQ; ++q) mLe[t][q] &= __ballot(c2 <= o.sq[q][m][h]);
         }
@@ -961,21 +955,6 @@ __device__ __forceinline__ u64 rs_lds_own_noop(const RsChunk<VI, NP> &r, const u
   if (nv > 3) return 0;
   return rs_noop<VI, NP, 3, true>(r, rs_own<3, true, NP, PERM>(mirror, thr, A, lane, nv));
 }
-// The partial masks of the same test over the actor range starting at ab (the SP path's halves).
-template <int VI, int NP, bool PRESENT>
-__device__ __forceinline__ RsPart<VI, 3> rs_lds_own_part(const RsChunk<VI, NP> &r, const u64 *mirror, const u64 *thr,
-                                                         unsigned long long A, int nv, int lane, unsigned ab) {
-  if constexpr (!PRESENT) {
-    const RsPart<VI, 0> y = rs_part<VI, NP, 0, false>(r, rs_own<0, false, NP>(mirror, thr, A, lane, 0, ab));
-    RsPart<VI, 3> x = rs_part_fail<VI, 3>();
-    x.p2 = y.p2;
-    x.b = y.b;
-    return x;
-  } else {
-    return rs_part<VI, NP, 3, true>(r, rs_own<3, true, NP>(mirror, thr, A, lane, nv, ab));
-  }
-}
-
 template <int VI, int NP>
 __device__ __forceinline__ void rs_reload(RsChunk<VI, NP> &r, const u64 *img, unsigned long long WS, const u64 *vals,
                                           const u64 *cm, unsigned long long A, int lane, bool vload = true) {
@@ -1010,8 +989,12 @@ __device__ __forceinline__ u64 rs_reg_noop(const RsChunk<VI, NP> &r, const RsReg
   for (int m = 0; m < NP; ++m) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const u64 lo = g.cs[m][h] < g.m1[m][h] ? g.cs[m][h] : g.m1[m][h];
-      o.tb[m][h] = g.ea[m][h] > lo ? g.ea[m][h] : lo;
+      if (MAP_TB_INC) {
+        o.tb[m][h] = g.cs[m][h];
+      } else {
+        const u64 lo = g.cs[m][h] < g.m1[m][h] ? g.cs[m][h] : g.m1[m][h];
+        o.tb[m][h] = g.ea[m][h] > lo ? g.ea[m][h] : lo;
+      }
     }
     o.ea[m] = g.ea[m];
     o.to[m] = g.to[m];
@@ -1020,22 +1003,26 @@ __device__ __forceinline__ u64 rs_reg_noop(const RsChunk<VI, NP> &r, const RsReg
   }
   return rs_noop<VI, NP, NQ, PRESENT, BATCH>(r, o, dma);
 }
-template <int VI, int NP, int NQ, bool PRESENT, bool BATCH = false, class F = RsNoDma>
+template <int VI, int NP, int NQ, bool PRESENT, bool BATCH = false, int LPS = 4, class F = RsNoDma>
 __device__ __forceinline__ RsPart<VI, NQ> rs_reg_part(const RsChunk<VI, NP> &r, const RsReg<NP> &g, F &&dma = F{}) {
   RsOwn<NQ, NP> o;
 #pragma unroll
   for (int m = 0; m < NP; ++m) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const u64 lo = g.cs[m][h] < g.m1[m][h] ? g.cs[m][h] : g.m1[m][h];
-      o.tb[m][h] = g.ea[m][h] > lo ? g.ea[m][h] : lo;
+      if (MAP_TB_INC) {
+        o.tb[m][h] = g.cs[m][h];
+      } else {
+        const u64 lo = g.cs[m][h] < g.m1[m][h] ? g.cs[m][h] : g.m1[m][h];
+        o.tb[m][h] = g.ea[m][h] > lo ? g.ea[m][h] : lo;
+      }
     }
     o.ea[m] = g.ea[m];
     o.to[m] = g.to[m];
 #pragma unroll
     for (int q = 0; q < (NQ > 0 ? NQ : 1); ++q) o.sq[q][m] = g.sq[q < 3 ? q : 0][m];
   }
-  return rs_part<VI, NP, NQ, PRESENT, BATCH>(r, o, dma);
+  return rs_part<VI, NP, NQ, PRESENT, BATCH, LPS>(r, o, dma);
 }
 // One instantiation per presence: own values are compared as 3 slots, the unused ones zero —
 // neutral, since "c2 <= 0 everywhere" only covers an empty incoming slot, which the "appended, then
@@ -1142,244 +1129,167 @@ __device__ __forceinline__ void rs_store(const RsChunk<VI, NP> &r, u64 *img, uns
     for (int t = 0; t < VI; ++t) vals[s * VI + t] = r.v[t];
 }
 
-// ---- Split-actor pair (SP path: the RS path at A = 32, V = 2 with two waves per key) ---------------
+// ---- Step-split pair (ST path: the RS path at A = 32, V = 2 with two waves per key) ------------------
 // The RS path runs one wave per key: config 4's 1,024 keys are one wave per SIMD, so nothing hides the
-// chunk test's latencies.  In the SP path a key is a workgroup of two waves, wave h testing actors
-// 16h .. 16h+15 of every chunk: each moves half of every step image (two steps per 1-KiB LDS-DMA
-// instruction, 8 per chunk instead of 16) and runs half of the test's compares, and the 2,048 waves are
-// two per SIMD.  The test is an OR over actors for "the replica has the key" and ANDs over actors for
-// the rest, so the halves exchange their partial masks (RsPart, 3 LDS words per wave and chunk, one
-// s_barrier) and both form the same verdict.  A chunk neither skips: both waves write their halves back
-// over the slot, wave 0 runs the exact loop over the whole chunk (lane = actor, as in the RS path) while
-// wave 1 waits at a barrier, and both reload their scan operands from the fold-state mirror.
-// scripts/micro/map_stream.hip measured this access pattern's ceiling at 2.05-2.06 ms for config 4
-// (80% of 8 TB/s) at one and at two waves per key, with two waves holding it to ~2.1 ms at twice the
-// per-wave work (profiles/r06_map_stream.log).
-constexpr unsigned kSpSlot = 1024;  // u64 words of one wave's chunk slot: 8 pieces x two 512-byte step halves
+// chunk test's latencies (LDS reads, compare -> scalar mask hand-offs, LDS-DMA issue).  In the ST path
+// a key is a workgroup of two waves, wave h testing steps 8h .. 8h+7 of every 16-step chunk over all
+// 32 actors (lane (s, g8): step 8h + s, actor pairs 2 g8 + 16 m): each moves its 8 step images (8
+// LDS-DMA instructions + the chunk's clock max) into the standard slot layout and runs half the test,
+// and the 2,048 waves are two per SIMD.  A step's verdict needs only its own lanes, so the waves
+// exchange one bit per chunk (their steps all skippable) around one s_barrier.  A chunk either wave
+// cannot skip: both write their steps back over the slot, wave 0 runs the RS exact loop over the whole
+// chunk while wave 1 waits at a barrier, and both reload their scan operands from the fold-state mirror.
+// (Round 6's first two-wave form split the ACTORS and exchanged nine partial masks per chunk: parity
+// green, 2.40 vs 2.245 ms for the one-wave RS path, profiles/r06_s4_map_sp_ab.log.)
+// scripts/micro/map_stream.hip put this access pattern's ceiling at 2.05-2.06 ms for config 4 (80% of
+// 8 TB/s), with two waves per key holding it near 2.1 ms at half the per-wave work of one
+// (profiles/r06_map_stream.log).
 
-// Word (in a wave's slot) of step s, part t (0 entry clock, 1 + v value clock v, 3 replica clock) and
-// actor a < 16 of the wave's half: piece s / 2, lane quad 2 (2t + a / 8) + s % 2 (every quad moves
-// 64 contiguous bytes of one row), word a % 8 of the quad's 64 bytes.
-__host__ __device__ __forceinline__ unsigned sp_word(unsigned s, unsigned t, unsigned a) {
-  return (s >> 1) * 128 + (2 * (2 * t + (a >> 3)) + (s & 1)) * 8 + (a & 7);
-}
-
-// Per-lane LDS-DMA source of the SP path: lane quad q moves, for step parity q % 2, 64 bytes of row
-// part (q / 2) / 2 at actors 16h + 8 ((q / 2) % 2) + 2 (lane % 4) .. + 1.
-struct SpLanes {
-  const char *base;       // the lane's 16 bytes of replica 0's row (bytes)
-  unsigned long long rs;  // that row's replica stride (bytes)
-  unsigned b;             // the step parity the lane moves
-};
-
-__device__ __forceinline__ SpLanes sp_lanes(const MapPlan &p, unsigned long long g, unsigned long long k, int lane,
-                                            unsigned h) {
-  SpLanes L;
-  const unsigned q = (unsigned)lane >> 2, c = q >> 1, t = c >> 1;
-  L.b = q & 1;
-  const unsigned long long A = p.A, a = 16ull * h + 8 * (c & 1) + 2 * ((unsigned)lane & 3);
-  // (the row sources as values: a per-lane choice between struct fields would put the plan in scratch)
-  const unsigned long long be = (unsigned long long)(p.ec + g * p.e_gs + k * A);
-  const unsigned long long bv = (unsigned long long)(p.vclk + g * p.vc_gs + k * 2 * A);
-  const unsigned long long bc = (unsigned long long)(p.clock + g * p.c_gs);
-  const unsigned long long se = (unsigned long long)p.e_rs * 8, sv = (unsigned long long)p.vc_rs * 8,
-                           sc = (unsigned long long)p.c_rs * 8;
-  const unsigned long long base = t == 0 ? be : (t < 3 ? bv + (t - 1) * A * 8 : bc);
-  L.base = reinterpret_cast<const char *>(base + a * 8);
-  L.rs = t == 0 ? se : (t < 3 ? sv : sc);
-  return L;
-}
-
-// DMA chunk ch's half step images (steps clamped to R - 1 past the end: copies never read) into a
-// wave's slot, then the chunk's clock max over all A actors (each wave keeps its own copy).  Exactly
-// 9 global_load_lds per call, so a fixed vmcnt count retires a chunk.
-__device__ __forceinline__ void sp_chunk_glds(const MapPlan &p, const SpLanes &L, unsigned long long g,
-                                              unsigned long long ch, unsigned long long R, u64 *img, u64 *cm,
-                                              int lane) {
-  const unsigned long long i0 = ch * 16;
-  if (i0 + 16 <= R) {  // (uniform)
-    const char *src = L.base + (i0 + L.b) * L.rs;
+// DMA the 8 step images of wave h of chunk ch (steps clamped to R - 1 past the end: copies never read)
+// into the slot, then the chunk's clock max (each wave keeps its own copy).  Exactly 9 global_load_lds.
+// (2 + V) * A == 128: every lane moves 16 bytes of every image.
+__device__ __forceinline__ void st_chunk_glds(const MapPlan &p, const GldsLanes<1> &L, unsigned long long g,
+                                              unsigned long long ch, unsigned long long R, u64 *img,
+                                              unsigned long long WS, u64 *cm, int lane, unsigned h) {
+  const unsigned long long i0 = ch * 16 + 8 * h;
+  u64 *dst = img + 8 * h * WS;
+  if (ch * 16 + 16 <= R) {  // (uniform)
+    const char *src = L.src0[0] + i0 * L.stride[0];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      glds16(src, img + j * 128);
-      src += 2 * L.rs;
+      glds16(src, dst + j * WS);
+      src += L.stride[0];
     }
   } else {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const unsigned long long i = i0 + 2 * j + L.b < R ? i0 + 2 * j + L.b : R - 1;
-      glds16(L.base + i * L.rs, img + j * 128);
+      const unsigned long long i = i0 + j < R ? i0 + j : R - 1;
+      glds16(L.src0[0] + i * L.stride[0], dst + j * WS);
     }
   }
   if ((unsigned long long)(2 * lane) < p.A) glds16(p.cmax + (g * p.nch + ch) * p.A + 2 * lane, cm);
 }
 
-// sp_chunk_glds of a whole chunk as the chunk test's DMA hook (pieces between the test's compares).
-struct SpDma {
+// st_chunk_glds of a whole chunk as the chunk test's DMA hook.
+struct StDma {
   static constexpr int count = 9;
   const char *src;
-  unsigned long long st2;  // two rows
-  u64 *img;
+  unsigned long long stride;
+  u64 *img;  // the wave's first step image of the slot
+  unsigned long long WS;
   const u64 *csrc;
   u64 *cm;
   bool con;
   __device__ __forceinline__ void operator()(int j) {
     if (j < 8) {
-      glds16(src, img + j * 128);
-      src += st2;
+      glds16(src, img + j * WS);
+      src += stride;
     } else if (con) {
       glds16(csrc, cm);
     }
   }
 };
 
-// A wave's half of chunk ch from its slot into the scan layout (lane (s, gq): actor pairs 16h + 2gq + 8m),
-// and the chunk's clock max (lane = actor, and at the lane's pairs).
+// Wave h's 8 steps of a slot into the ST scan layout, and the chunk's clock max (lane = actor, and at
+// the lane's pairs).
 template <int VI, int NP>
-__device__ __forceinline__ void sp_reload(RsChunk<VI, NP> &r, const u64 *img, const u64 *cm, unsigned long long A,
-                                          int lane, unsigned h, bool wcm = true) {
-  static_assert(VI == 2 && NP == 2, "SP path: A = 32, V = 2");
-  const unsigned s = (unsigned)lane >> 2, gq = (unsigned)lane & 3;
+__device__ __forceinline__ void st_reload(RsChunk<VI, NP> &r, const u64 *img, unsigned long long WS, const u64 *cm,
+                                          unsigned long long A, int lane, unsigned h, bool wcm = true) {
+  const u64 *st = img + (8 * h + ((unsigned)lane >> 3)) * WS;
 #pragma unroll
   for (int m = 0; m < NP; ++m) {
-    const unsigned a = 2 * gq + 8 * m;
-    r.e[m] = lds2(img + sp_word(s, 0, a));
+    const unsigned a0 = st_a0(lane, m);
+    const unsigned long long a = a0 < A ? a0 : A - 2;
+    r.e[m] = lds2(st + a);
 #pragma unroll
-    for (int t = 0; t < VI; ++t) r.c[t][m] = lds2(img + sp_word(s, 1 + t, a));
-    r.co[m] = lds2(img + sp_word(s, 1 + VI, a));
+    for (int t = 0; t < VI; ++t) r.c[t][m] = lds2(st + (1 + t) * A + a);
+    r.co[m] = lds2(st + (1 + VI) * A + a);
   }
   if (wcm) {
     r.cm = cm[(unsigned long long)lane < A ? lane : A - 1];
 #pragma unroll
-    for (int m = 0; m < NP; ++m) r.cmp[m] = lds2(cm + 16 * h + 2 * gq + 8 * m);
+    for (int m = 0; m < NP; ++m) {
+      const unsigned a0 = st_a0(lane, m);
+      r.cmp[m] = lds2(cm + (a0 < A ? a0 : A - 2));
+    }
   }
 }
 
-// A chunk neither wave could skip: the wave's half back over its slot (the layout the DMA wrote).
+// A chunk neither wave could skip: the wave's steps back over the slot, and its clock-max copy.
 template <int VI, int NP>
-__device__ __forceinline__ void sp_store(const RsChunk<VI, NP> &r, u64 *img, u64 *cm, unsigned long long A, int lane) {
-  const unsigned s = (unsigned)lane >> 2, gq = (unsigned)lane & 3;
+__device__ __forceinline__ void st_store(const RsChunk<VI, NP> &r, u64 *img, unsigned long long WS, u64 *cm,
+                                         unsigned long long A, int lane, unsigned h) {
+  u64 *st = img + (8 * h + ((unsigned)lane >> 3)) * WS;
 #pragma unroll
   for (int m = 0; m < NP; ++m) {
-    const unsigned a = 2 * gq + 8 * m;
-    *reinterpret_cast<u64x2 *>(img + sp_word(s, 0, a)) = r.e[m];
+    const unsigned a0 = st_a0(lane, m);
+    const unsigned long long a = a0 < A ? a0 : A - 2;
+    *reinterpret_cast<u64x2 *>(st + a) = r.e[m];
 #pragma unroll
-    for (int t = 0; t < VI; ++t) *reinterpret_cast<u64x2 *>(img + sp_word(s, 1 + t, a)) = r.c[t][m];
-    *reinterpret_cast<u64x2 *>(img + sp_word(s, 1 + VI, a)) = r.co[m];
+    for (int t = 0; t < VI; ++t) *reinterpret_cast<u64x2 *>(st + (1 + t) * A + a) = r.c[t][m];
+    *reinterpret_cast<u64x2 *>(st + (1 + VI) * A + a) = r.co[m];
   }
   if ((unsigned long long)lane < A) cm[lane] = r.cm;
 }
 
-// The partial masks through LDS: 4 masks per u64 word (the masks only use bits 4s), 3 words per wave.
-template <int NQ>
-__device__ __forceinline__ void sp_put(u64 *vw, const RsPart<2, NQ> &x, int lane) {
-  constexpr int NQ1 = NQ > 0 ? NQ : 1;
-  static_assert(5 + 2 * NQ1 <= 12, "three vote words");
-  u64 w[3] = {0, 0, 0};
-  const u64 G1 = grp_mask<4>();
-  int i = 0;
-  auto put = [&](u64 m) {
-    w[i >> 2] |= (m & G1) << (i & 3);
-    ++i;
-  };
-  put(x.p2);
-  put(x.b);
-  put(x.o);
-  put(x.van[0]);
-  put(x.van[1]);
+// This wave's verdict (bit 8s: its step s skippable) from the register-held operands, with the RS
+// dispatch on presence / own value count (a state holding more than MAP_REG_NQ values settles nothing
+// here, as rs_reg_noop_nv); `test` off: the DMA hook still issues its pieces.
+template <bool BATCH, class F = RsNoDma>
+__device__ __forceinline__ u64 st_reg_verdict(const RsChunk<2, 2> &r, const RsReg<2> &g, bool present, int nv,
+                                              bool test, F &&dma = F{}) {
+  if (!test || (present && nv > MAP_REG_NQ)) {
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int q = 0; q < NQ1; ++q) put(x.le[t][q]);
-  if (lane < 3) vw[lane] = lane == 0 ? w[0] : (lane == 1 ? w[1] : w[2]);
+    for (int j = 0; j < std::remove_reference_t<F>::count; ++j) dma(j);
+    return 0;
+  }
+  if (!present) return rs_verdict<2, 0, false, 8>(rs_reg_part<2, 2, 0, false, BATCH, 8>(r, g, dma));
+  return rs_verdict<2, MAP_REG_NQ, true, 8>(rs_reg_part<2, 2, MAP_REG_NQ, true, BATCH, 8>(r, g, dma));
 }
 
-template <int NQ>
-__device__ __forceinline__ RsPart<2, NQ> sp_get(const u64 *vw) {
-  constexpr int NQ1 = NQ > 0 ? NQ : 1;
-  u64 w[3];
-#pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    const u64 x = *reinterpret_cast<const volatile u64 *>(vw + j);
-    w[j] = ((u64)(unsigned)__builtin_amdgcn_readfirstlane((int)(x >> 32)) << 32) |
-           (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)x);
-  }
-  const u64 G1 = grp_mask<4>();
-  int i = 0;
-  auto get = [&]() {
-    const u64 m = (w[i >> 2] >> (i & 3)) & G1;
-    ++i;
-    return m;
-  };
-  RsPart<2, NQ> x;
-  x.p2 = get();
-  x.b = get();
-  x.o = get();
-  x.van[0] = get();
-  x.van[1] = get();
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int q = 0; q < NQ1; ++q) x.le[t][q] = get();
-  return x;
+// The steps of wave h a chunk of n0 steps holds, as verdict bits.
+__device__ __forceinline__ u64 st_want(unsigned long long n0, unsigned h) {
+  const unsigned long long nh = n0 > 8 * h ? (n0 - 8 * h < 8 ? n0 - 8 * h : 8) : 0;
+  return nh >= 8 ? grp_mask<8>() : (grp_mask<8>() & ((1ull << (8 * nh)) - 1));
 }
 
 // The pair's barrier: this wave's LDS writes done, both waves here, no LDS access moved across it.
 // (No vmcnt wait: the LDS-DMA of later chunks stays in flight.)
-__device__ __forceinline__ void sp_barrier() {
+__device__ __forceinline__ void st_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 }
 
-// One chunk's vote: this wave's partial masks (or "settles nothing" when it did not test), exchanged
-// with the partner's through LDS around one s_barrier, then the common verdict.  vw: this chunk
-// parity's 8 words (wave h at 4h).  Both waves call it with the same present / nv.
-template <bool PRESENT>
-__device__ __forceinline__ u64 sp_vote(u64 *vw, const RsPart<2, MAP_REG_NQ> &mine, unsigned h, int lane) {
-  sp_put<MAP_REG_NQ>(vw + 4 * h, mine, lane);
-  sp_barrier();
-  const RsPart<2, MAP_REG_NQ> other = sp_get<MAP_REG_NQ>(vw + 4 * (h ^ 1));
-  return rs_verdict<2, MAP_REG_NQ, PRESENT>(rs_part_join(mine, other));
+// One chunk's vote: both waves' steps skippable.  vw: this chunk parity's two words.
+__device__ __forceinline__ bool st_vote(unsigned *vw, bool mine, unsigned h, int lane) {
+  if (lane == 0) reinterpret_cast<volatile unsigned *>(vw)[h] = mine ? 1u : 0u;
+  st_barrier();
+  const unsigned other = __builtin_amdgcn_readfirstlane(reinterpret_cast<const volatile unsigned *>(vw)[h ^ 1]);
+  return mine && other != 0;
 }
 
-// This wave's partial masks of the register test (the RS dispatch on presence / own value count:
-// a state holding more than MAP_REG_NQ values settles nothing here, as rs_reg_noop_nv).
-template <bool BATCH, class F = RsNoDma>
-__device__ __forceinline__ RsPart<2, MAP_REG_NQ> sp_reg_part(const RsChunk<2, 2> &r, const RsReg<2> &g, bool present,
-                                                             int nv, bool test, F &&dma = F{}) {
-  if (!test || (present && nv > MAP_REG_NQ)) {
-#pragma unroll
-    for (int j = 0; j < std::remove_reference_t<F>::count; ++j) dma(j);
-    return rs_part_fail<2, MAP_REG_NQ>();
-  }
-  if (!present) {
-    const RsPart<2, 0> y = rs_reg_part<2, 2, 0, false, BATCH>(r, g, dma);
-    RsPart<2, MAP_REG_NQ> x = rs_part_fail<2, MAP_REG_NQ>();
-    x.p2 = y.p2;
-    x.b = y.b;
-    return x;
-  }
-  return rs_reg_part<2, 2, MAP_REG_NQ, true, BATCH>(r, g, dma);
-}
-
-// The exact loop's test of a chunk from LDS (wave 0 alone, both halves): the two halves' parts joined.
-__device__ __forceinline__ u64 sp_lds_noop(const u64 *img0, const u64 *img1, const u64 *mirror, const u64 *thr,
+// The exact loop's test of a chunk from LDS (wave 0 alone, all 16 steps, in two 8-step passes of the
+// ST layout), as bits 4s (the exact loop's LPS = 4 convention).
+__device__ __forceinline__ u64 st_lds_noop(const u64 *img, unsigned long long WS, const u64 *mirror, const u64 *thr,
                                            unsigned long long A, bool present, int nv, int lane) {
   if (present && nv > 3) return 0;
-  RsChunk<2, 2> r;
-  r.cm = 0;
-  r.v[0] = r.v[1] = 0;
-  if (!present) {
-    sp_reload(r, img0, nullptr, A, lane, 0, false);
-    const RsPart<2, 3> x = rs_lds_own_part<2, 2, false>(r, mirror, thr, A, nv, lane, 0);
-    sp_reload(r, img1, nullptr, A, lane, 1, false);
-    return rs_verdict<2, 3, false>(rs_part_join(x, rs_lds_own_part<2, 2, false>(r, mirror, thr, A, nv, lane, 16)));
+  u64 out = 0;
+#pragma unroll
+  for (unsigned hh = 0; hh < 2; ++hh) {
+    RsChunk<2, 2> r;
+    r.cm = 0;
+    r.v[0] = r.v[1] = 0;
+    st_reload(r, img, WS, nullptr, A, lane, hh, false);
+    const u64 v8 = present ? rs_verdict<2, 3, true, 8>(rs_part<2, 2, 3, true, false, 8>(
+                                 r, rs_own<3, true, 2, false, 8>(mirror, thr, A, lane, nv)))
+                           : rs_verdict<2, 0, false, 8>(rs_part<2, 2, 0, false, false, 8>(
+                                 r, rs_own<0, false, 2, false, 8>(mirror, thr, A, lane, 0)));
+#pragma unroll
+    for (int sv = 0; sv < 8; ++sv)
+      if ((v8 >> (8 * sv)) & 1ull) out |= 1ull << (4 * (8 * hh + sv));
   }
-  sp_reload(r, img0, nullptr, A, lane, 0, false);
-  const RsPart<2, 3> x = rs_lds_own_part<2, 2, true>(r, mirror, thr, A, nv, lane, 0);
-  sp_reload(r, img1, nullptr, A, lane, 1, false);
-  return rs_verdict<2, 3, true>(rs_part_join(x, rs_lds_own_part<2, 2, true>(r, mirror, thr, A, nv, lane, 16)));
+  return out;
 }
 
 // ---- Shared replica-clock ring (SH path: the RS path at A = 32, V = 2, four key waves per CU) ------
@@ -1556,11 +1466,11 @@ __device__ __forceinline__ unsigned sh_arrived(const unsigned *cnt) {
 
 // ITM: unrolled scan iterations ceil(A / LPS) rounded up to a power of two, fixed per launch so
 // each kernel's register allocation only covers its own scan shape.  NP > 0: the RS path (above).
-template <int APL, int VI, int VO, int CM, int NB, bool GL, int ITM, int NP = 0, bool SH = false, bool SP = false>
-__global__ __launch_bounds__(SH ? 256 : (SP ? 128 : 64), SP ? 2 : 1) void map_fold_kernel(MapPlan pk) {
+template <int APL, int VI, int VO, int CM, int NB, bool GL, int ITM, int NP = 0, bool SH = false, bool ST = false>
+__global__ __launch_bounds__(SH ? 256 : (ST ? 128 : 64), ST ? 2 : 1) void map_fold_kernel(MapPlan pk) {
   constexpr bool RS = NP > 0;
   static_assert(!SH || (RS && VI == 2 && NP == 4), "SH path: the RS path at A = 32, V = 2");
-  static_assert(!SP || (RS && !SH && NB == 2 && VI == 2 && NP == 2 && CM == 16), "SP path: the RS path at A = 32, V = 2");
+  static_assert(!ST || (RS && !SH && NB == 2 && VI == 2 && NP == 2 && CM == 16), "ST path: the RS path at A = 32, V = 2");
   const MapPlan p = pk;  // a local copy the optimizer can split into registers (the by-value
                          // kernel argument itself would be materialized in scratch memory)
   // SH: a workgroup of four waves, wave w folding key 4*blockIdx + w (K % 4 == 0: one group)
@@ -1568,8 +1478,8 @@ __global__ __launch_bounds__(SH ? 256 : (SP ? 128 : 64), SP ? 2 : 1) void map_fo
   const unsigned long long gk0 = SH ? 4ull * blockIdx.x + wv : (unsigned long long)blockIdx.x;
   const unsigned long long g = gk0 / p.K;
   const unsigned long long k = gk0 % p.K;
-  const int lane = (SH || SP) ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
-  const unsigned hw = SP ? (unsigned)threadIdx.x >> 6 : 0u;  // SP: the wave's actor half
+  const int lane = (SH || ST) ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
+  const unsigned hw = ST ? (unsigned)threadIdx.x >> 6 : 0u;  // ST: the wave's 8 steps of each chunk
   const unsigned long long R = p.R;
 
   bool present = false;
@@ -1621,18 +1531,17 @@ __global__ __launch_bounds__(SH ? 256 : (SP ? 128 : 64), SP ? 2 : 1) void map_fo
   // list, the fold-state mirror.  (Addresses are always computed from map_lds: a pointer table
   // would hide the LDS address space and turn every access into a flat op.)  SH: four such wave
   // regions (no clock-max slots), then the shared ring and its arrival counters.
-  // SP: both waves' slots (wave h's at wl + h * NB * SLOT), both waves' clock-max copies, and after the
-  // thresholds the vote words [chunk parity][wave][4] and the fold state word for the partner (present,
-  // own value count)
-  const unsigned long long SLOT = SH ? kShSlot : (SP ? kSpSlot : C * WS);
-  constexpr unsigned long long NW = SP ? 2 : 1;
+  // ST: both waves' clock-max copies (wave h's at cml + h * NB * CMS), and after the thresholds the vote
+  // words [chunk parity][wave] (u32) and the fold-state word for the partner (present, own value count)
+  const unsigned long long SLOT = SH ? kShSlot : C * WS;
+  constexpr unsigned long long NW = ST ? 2 : 1;
   const unsigned long long CMS = A;  // staged clock-max stride
   const unsigned long long PW =
-      NW * NB * SLOT + NB * C * VI + kMapL + (2 + VO) * A + ((GL || RS) && !SH ? NW * NB * CMS : 0) + 4 * A + (SP ? 18 : 0);
+      NB * SLOT + NB * C * VI + kMapL + (2 + VO) * A + ((GL || RS) && !SH ? NW * NB * CMS : 0) + 4 * A + (ST ? 4 : 0);
   u64 *const wl = map_lds + (SH ? wv * PW : 0);
   u64 *const shr = map_lds + 4 * PW;  // SH: kShS shared slots
   unsigned *const arr = reinterpret_cast<unsigned *>(shr + kShS * kShShared);
-  u64 *const vbase = wl + NW * NB * SLOT;
+  u64 *const vbase = wl + NB * SLOT;
   unsigned *lrow = reinterpret_cast<unsigned *>(vbase + NB * C * VI);
   unsigned *lidx = lrow + kMapL;
   // fold-state mirror read by the speculative scan: entry clock, VO value clocks, acc clock
@@ -1643,15 +1552,14 @@ __global__ __launch_bounds__(SH ? 256 : (SP ? 128 : 64), SP ? 2 : 1) void map_fo
   u64 *const thr = cml + ((GL || RS) && !SH ? NW * NB * CMS : 0);
   u64 *const csm = thr + 2 * A;  // RS: the acc clock and m1 handed back to the register operands
   u64 *const m1m = thr + 3 * A;
-  u64 *const vw = m1m + A;                                        // SP: vote words
-  unsigned *const spst = reinterpret_cast<unsigned *>(vw + 16);   // SP: present | own values << 1
+  unsigned *const vw = reinterpret_cast<unsigned *>(m1m + A);  // ST: vote words [parity][wave]
+  unsigned *const spst = vw + 4;                                 // ST: present | own values << 1
   u64 m1 = ~0ull;
   const unsigned long long nch = (R + C - 1) / C;
-  if constexpr (SP) {
-    if (hw == 1) {  // the partner wave: actors 16 .. 31 of every chunk (wave 0 holds the fold state)
-      const SpLanes spl = sp_lanes(p, g, k, lane, 1);
-      u64 *const img1 = wl + NB * SLOT;  // this wave's slots and clock-max copies
-      u64 *const cm1 = cml + NB * CMS;
+  if constexpr (ST) {
+    if (hw == 1) {  // the partner wave: steps 8 .. 15 of every chunk (wave 0 holds the fold state)
+      const GldsLanes<1> gp = glds_lanes<VI, 1>(p, g, k, lane);
+      u64 *const cm1 = cml + NB * CMS;  // this wave's clock-max copies
       RsChunk<VI, NP> r;
       RsReg<NP> q;
 #pragma unroll
@@ -1667,56 +1575,56 @@ __global__ __launch_bounds__(SH ? 256 : (SP ? 128 : 64), SP ? 2 : 1) void map_fo
       int nvp = 0;
       const bool batch = MAP_BATCH_ONLY || p.batch;
       for (unsigned long long c = 0; c < 2 && c < nch; ++c)
-        sp_chunk_glds(p, spl, g, c, R, img1 + c * SLOT, cm1 + c * CMS, lane);
+        st_chunk_glds(p, gp, g, c, R, wl + c * SLOT, WS, cm1 + c * CMS, lane, 1);
       for (unsigned long long ch = 0; ch < nch; ++ch) {
         const unsigned slot = (unsigned)(ch & 1);
-        u64 *const img = img1 + slot * SLOT;
+        u64 *const img = wl + slot * SLOT;
         u64 *const cms = cm1 + slot * CMS;
         if (ch + 1 < nch) wait_vmcnt<9>();
         else wait_vmcnt<0>();
-        sp_reload(r, img, cms, A, lane, 1);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot is read: refill it
+        st_reload(r, img, WS, cms, A, lane, 1);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot's steps are read: refill them
         const unsigned long long n0 = R - ch * C < (unsigned long long)C ? R - ch * C : C;
-        const u64 want = n0 >= 16 ? grp_mask<4>() : (grp_mask<4>() & ((1ull << (4 * n0)) - 1));
+        const u64 want = st_want(n0, 1);
         const unsigned long long i2 = (ch + 2) * C;
         const bool spread = p.spec && ch + 2 < nch && i2 + C <= R;
-        if (!spread && ch + 2 < nch) sp_chunk_glds(p, spl, g, ch + 2, R, img, cms, lane);
-        RsPart<2, MAP_REG_NQ> part;
+        if (!spread && ch + 2 < nch) st_chunk_glds(p, gp, g, ch + 2, R, img, WS, cms, lane, 1);
+        u64 verdict;
         if (spread) {
-          SpDma d{spl.base + (i2 + spl.b) * spl.rs, 2 * spl.rs, img, p.cmax + (g * p.nch + ch + 2) * A + 2 * lane, cms,
-                  (unsigned long long)(2 * lane) < A};
-          part = batch ? sp_reg_part<true>(r, q, pres, nvp, true, d) : sp_reg_part<false>(r, q, pres, nvp, true, d);
+          StDma d{gp.src0[0] + (i2 + 8) * gp.stride[0], gp.stride[0], img + 8 * WS, WS,
+                  p.cmax + (g * p.nch + ch + 2) * A + 2 * lane, cms, (unsigned long long)(2 * lane) < A};
+          verdict = batch ? st_reg_verdict<true>(r, q, pres, nvp, true, d) : st_reg_verdict<false>(r, q, pres, nvp, true, d);
         } else {
-          part = batch ? sp_reg_part<true>(r, q, pres, nvp, p.spec != 0) : sp_reg_part<false>(r, q, pres, nvp, p.spec != 0);
+          verdict = batch ? st_reg_verdict<true>(r, q, pres, nvp, p.spec != 0)
+                          : st_reg_verdict<false>(r, q, pres, nvp, p.spec != 0);
         }
-        const u64 verdict = pres ? sp_vote<true>(vw + 8 * slot, part, 1, lane) : sp_vote<false>(vw + 8 * slot, part, 1, lane);
-        if ((verdict & want) == want) {
+        if (st_vote(vw + 2 * slot, (verdict & want) == want, 1, lane)) {
 #pragma unroll
           for (int m = 0; m < NP; ++m)
 #pragma unroll
-            for (int h = 0; h < 2; ++h) q.cs[m][h] = q.cs[m][h] > r.cmp[m][h] ? q.cs[m][h] : r.cmp[m][h];
+            for (int h = 0; h < 2; ++h) q.cs[m][h] = rs_adv(q.cs[m][h], r.cmp[m][h], q.m1[m][h]);
           continue;
         }
-        wait_vmcnt<0>();  // chunk ch+2's copy into this slot has landed: write chunk ch back over it
-        sp_store(r, img, cms, A, lane);
-        sp_barrier();  // (A) both halves in LDS: wave 0 runs the exact loop
-        sp_barrier();  // (B) the exact loop is done, the mirror and state word written
-        const unsigned st = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const volatile unsigned *>(spst));
-        pres = (st & 1) != 0;
-        nvp = (int)(st >> 1);
+        wait_vmcnt<0>();  // chunk ch+2's copy into these steps has landed: write chunk ch back over it
+        st_store(r, img, WS, cms, A, lane, 1);
+        st_barrier();  // (A) the whole chunk is in LDS: wave 0 runs the exact loop
+        st_barrier();  // (B) the exact loop is done, the mirror and the state word written
+        const unsigned sw = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const volatile unsigned *>(spst));
+        pres = (sw & 1) != 0;
+        nvp = (int)(sw >> 1);
 #pragma unroll
         for (int m = 0; m < NP; ++m) {
-          const unsigned a0 = 16 + rs_a0<false>(lane, m);
+          const unsigned a0 = st_a0(lane, m);
           q.ea[m] = lds2(mirror + a0);
           q.to[m] = lds2(thr + A + a0);
           q.m1[m] = lds2(m1m + a0);
-          q.cs[m] = lds2(csm + a0);
+          q.cs[m] = lds2((MAP_TB_INC ? thr : csm) + a0);
 #pragma unroll
           for (int x = 0; x < 3; ++x) q.sq[x][m] = x < nvp ? lds2(mirror + (1 + x) * A + a0) : u64x2{0, 0};
         }
         if (ch + 2 < nch) {
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          sp_chunk_glds(p, spl, g, ch + 2, R, img, cms, lane);
+          st_chunk_glds(p, gp, g, ch + 2, R, img, WS, cms, lane, 1);
         }
       }
       return;
@@ -1791,8 +1699,7 @@ __global__ __launch_bounds__(SH ? 256 : (SP ? 128 : 64), SP ? 2 : 1) void map_fo
   const int ni = GL ? (int)((W + 127) / 128) : 0;  // 1-KiB pieces per step image (GL: 1 or 2)
   GldsLanes<1> gl1;
   GldsLanes<2> gl2;
-  const bool vpiece = !(RS && (SH || SP || p.lazyv));
-  SpLanes spl;  // SP: wave 0's LDS-DMA sources (actors 0 .. 15)
+  const bool vpiece = !(RS && (SH || ST || p.lazyv));
   ShLanes shl;
   // SH ring bookkeeping (uniform): the shared slot of chunk ch and the arrival count it needs, the
   // slot of chunk ch + kShD - 2 (signalled at iteration ch) and of chunk ch + kShD (issued)
@@ -1815,9 +1722,10 @@ __global__ __launch_bounds__(SH ? 256 : (SP ? 128 : 64), SP ? 2 : 1) void map_fo
       sh_chunk_images(shl, c * C, R, wl + c * SLOT);
       if (c + kShD - 2 < nch) sh_chunk_shared(p, shl, g, c + kShD - 2, R, wv, shr + (c + kShD - 2) * kShShared, lane);
     }
-  } else if constexpr (SP) {
-    spl = sp_lanes(p, g, k, lane, 0);
-    for (unsigned long long c = 0; c < 2 && c < nch; ++c) sp_chunk_glds(p, spl, g, c, R, wl + c * SLOT, cml + c * CMS, lane);
+  } else if constexpr (ST) {  // steps 0 .. 7 of chunks 0 and 1
+    gl1 = glds_lanes<VI, 1>(p, g, k, lane);
+    for (unsigned long long c = 0; c < 2 && c < nch; ++c)
+      st_chunk_glds(p, gl1, g, c, R, wl + c * SLOT, WS, cml + c * CMS, lane, 0);
   } else if constexpr (RS) {  // chunks 0 and 1 into the two slots (W <= 128: one piece per step)
     gl1 = glds_lanes<VI, 1>(p, g, k, lane);
     for (unsigned long long c = 0; c < 2 && c < nch; ++c)
@@ -1846,7 +1754,6 @@ __global__ __launch_bounds__(SH ? 256 : (SP ? 128 : 64), SP ? 2 : 1) void map_fo
   for (unsigned long long ch = 0; ch < nch; ++ch) {
     const unsigned slot = (unsigned)(ch % NB);
     const u64 *buf = wl + slot * SLOT;
-    const u64 *sp1 = wl + NB * SLOT + slot * SLOT;  // SP: the partner's half of the chunk (buf: wave 0's)
     const u64 *vb = vbase + slot * C * VI;
     const u64 *shx = shr;  // SH: chunk ch's shared slot (clock rows, clock max)
     if constexpr (RS) {
@@ -1891,7 +1798,7 @@ __global__ __launch_bounds__(SH ? 256 : (SP ? 128 : 64), SP ? 2 : 1) void map_fo
         }
         MAP_TOCK(cy_arr);
         MAP_TICK();
-      } else if constexpr (SP) {  // 9 pieces per chunk (sp_chunk_glds)
+      } else if constexpr (ST) {  // 9 pieces per chunk (st_chunk_glds)
         if (ch + 1 < nch) wait_vmcnt<9>();
         else wait_vmcnt<0>();
       } else {
@@ -1909,8 +1816,8 @@ __global__ __launch_bounds__(SH ? 256 : (SP ? 128 : 64), SP ? 2 : 1) void map_fo
         sh_reload(rA, img, shs, A, lane);
         // next chunk's arrival count, read with this chunk's slots
         pre_raw = *reinterpret_cast<const volatile unsigned *>(arr + (sh_use + 1 == kShS ? 0 : sh_use + 1));
-      } else if constexpr (SP) {
-        sp_reload(rA, img, cms, A, lane, 0);
+      } else if constexpr (ST) {
+        st_reload(rA, img, WS, cms, A, lane, 0);
       } else {
         rs_reload(rA, img, WS, vsl, cms, A, lane, vpiece);
       }
@@ -1924,8 +1831,8 @@ __global__ __launch_bounds__(SH ? 256 : (SP ? 128 : 64), SP ? 2 : 1) void map_fo
           if (ch + 2 < nch) sh_chunk_images(shl, i2, R, img);
           if (ch + kShD < nch) sh_chunk_shared(p, shl, g, ch + kShD, R, wv, shr + sh_iss * kShShared, lane);
         }
-      } else if constexpr (SP) {
-        if (ch + 2 < nch && !spread) sp_chunk_glds(p, spl, g, ch + 2, R, img, cms, lane);
+      } else if constexpr (ST) {
+        if (ch + 2 < nch && !spread) st_chunk_glds(p, gl1, g, ch + 2, R, img, WS, cms, lane, 0);
       } else {
         if (ch + 2 < nch && !spread)
           map_chunk_glds<VI, C, 1>(p, gl1, g, k, i2, R, img, WS, vsl, cms, lane, vpiece, p.diag);
@@ -1945,18 +1852,18 @@ __global__ __launch_bounds__(SH ? 256 : (SP ? 128 : 64), SP ? 2 : 1) void map_fo
       }
       MAP_TICK();
       bool skip = false;
-      if constexpr (SP) {  // this half's partial masks, exchanged with the partner wave's: one verdict
+      if constexpr (ST) {  // this wave's steps, then the pair's vote
         const bool batch = MAP_BATCH_ONLY || p.batch;
-        RsPart<2, MAP_REG_NQ> part;
+        u64 verdict;
         if (spread) {
-          SpDma d{spl.base + (i2 + spl.b) * spl.rs, 2 * spl.rs, img, p.cmax + (g * p.nch + ch + 2) * A + 2 * lane, cms,
-                  (unsigned long long)(2 * lane) < A};
-          part = batch ? sp_reg_part<true>(rA, rg, present, nv, true, d) : sp_reg_part<false>(rA, rg, present, nv, true, d);
+          StDma d{gl1.src0[0] + i2 * gl1.stride[0], gl1.stride[0], img, WS, p.cmax + (g * p.nch + ch + 2) * A + 2 * lane,
+                  cms, (unsigned long long)(2 * lane) < A};
+          verdict = batch ? st_reg_verdict<true>(rA, rg, present, nv, true, d) : st_reg_verdict<false>(rA, rg, present, nv, true, d);
         } else {
-          part = batch ? sp_reg_part<true>(rA, rg, present, nv, el) : sp_reg_part<false>(rA, rg, present, nv, el);
+          verdict = batch ? st_reg_verdict<true>(rA, rg, present, nv, el) : st_reg_verdict<false>(rA, rg, present, nv, el);
         }
-        const u64 verdict = present ? sp_vote<true>(vw + 8 * slot, part, 0, lane) : sp_vote<false>(vw + 8 * slot, part, 0, lane);
-        skip = (verdict & want) == want;
+        const u64 want0 = st_want(n0, 0);
+        skip = st_vote(vw + 2 * slot, el && (verdict & want0) == want0, 0, lane);
       } else if (SH && spread) {
         const unsigned long long ic = (ch + kShD) * C + 4 * wv + shl.sub;
         ShDma d{{shl.b[0] + (i2 + shl.sub) * shl.st[0], shl.b[1] + (i2 + shl.sub) * shl.st[1],
@@ -1995,12 +1902,12 @@ __global__ __launch_bounds__(SH ? 256 : (SP ? 128 : 64), SP ? 2 : 1) void map_fo
 #pragma unroll
         for (int m = 0; m < NP; ++m)
 #pragma unroll
-          for (int h = 0; h < 2; ++h) rg.cs[m][h] = rg.cs[m][h] > rA.cmp[m][h] ? rg.cs[m][h] : rA.cmp[m][h];
+          for (int h = 0; h < 2; ++h) rg.cs[m][h] = rs_adv(rg.cs[m][h], rA.cmp[m][h], rg.m1[m][h]);
         continue;
       }
       wait_vmcnt<0>();
       if constexpr (SH) sh_store(rA, img, lane);
-      else if constexpr (SP) sp_store(rA, img, cms, A, lane);
+      else if constexpr (ST) st_store(rA, img, WS, cms, A, lane, 0);
       else rs_store(rA, img, WS, vsl, cms, A, lane, vpiece);
       if (!vpiece && lane < C * VI) {  // the chunk's values, fetched now (a chunk the exact loop runs)
         const unsigned long long iv = ch * C + lane / VI;
@@ -2012,7 +1919,7 @@ __global__ __launch_bounds__(SH ? 256 : (SP ? 128 : 64), SP ? 2 : 1) void map_fo
         const u64 lo = cs[0] < m1 ? cs[0] : m1;
         thr[lane] = e[0] > lo ? e[0] : lo;
       }
-      if constexpr (SP) sp_barrier();  // (A) both halves are back in LDS: the exact loop reads the whole chunk
+      if constexpr (ST) st_barrier();  // (A) both waves' steps are back in LDS: the exact loop reads the whole chunk
     }
     if constexpr (GL) {
       // issue chunk ch+NB-1 into the slot chunk ch-1 used, then wait for chunk ch
@@ -2068,8 +1975,8 @@ __global__ __launch_bounds__(SH ? 256 : (SP ? 128 : 64), SP ? 2 : 1) void map_fo
 #pragma unroll
             for (int t = 0; t < VI; ++t) r.v[t] = 0;
             noop = rs_lds_own_noop<VI, NP, true>(r, mirror, thr, A, present, nv, lane);
-          } else if constexpr (SP)
-            noop = sp_lds_noop(buf, sp1, mirror, thr, A, present, nv, lane);
+          } else if constexpr (ST)
+            noop = st_lds_noop(buf, WS, mirror, thr, A, present, nv, lane);
           else if constexpr (RS)
             noop = rs_lds_noop_nv<VI, (RS ? NP : 1)>(buf, WS, mirror, thr, A, present, nv, lane);
           else
@@ -2094,9 +2001,7 @@ __global__ __launch_bounds__(SH ? 256 : (SP ? 128 : 64), SP ? 2 : 1) void map_fo
             u64 mx = cs[0];
 #pragma unroll
             for (int u = 0; u < C; ++u) {
-              const u64 co = SH   ? shx[sh_cword(u, (unsigned)a)]
-                             : SP ? (a < 16 ? buf : sp1)[sp_word(u, 3, (unsigned)a & 15)]
-                                  : buf[u * WS + (1 + VI) * A + a];
+              const u64 co = SH ? shx[sh_cword(u, (unsigned)a)] : buf[u * WS + (1 + VI) * A + a];
               const u64 take = ((unsigned long long)u >= s && (unsigned long long)u < j) ? ~0ull : 0ull;
               const u64 x = co & take;
               mx = mx > x ? mx : x;
@@ -2131,16 +2036,6 @@ __global__ __launch_bounds__(SH ? 256 : (SP ? 128 : 64), SP ? 2 : 1) void map_fo
 #pragma unroll
         for (int t = 0; t < VI; ++t) in.c[t][0] = on ? buf[pw + 128 * (1 + t)] : 0;
         in.co[0] = on ? shx[sh_cword((unsigned)s, (unsigned)lane)] : 0;
-#pragma unroll
-        for (int t = 0; t < VI; ++t) in.v[t] = vb[s * VI + t];
-      } else if constexpr (SP) {  // lane = actor: the word of its half (actors >= A: zero)
-        const bool on = (unsigned long long)lane < A;
-        const u64 *hb = lane < 16 ? buf : sp1;
-        const unsigned a = (unsigned)lane & 15;
-        in.e[0] = on ? hb[sp_word((unsigned)s, 0, a)] : 0;
-#pragma unroll
-        for (int t = 0; t < VI; ++t) in.c[t][0] = on ? hb[sp_word((unsigned)s, 1 + t, a)] : 0;
-        in.co[0] = on ? hb[sp_word((unsigned)s, 1 + VI, a)] : 0;
 #pragma unroll
         for (int t = 0; t < VI; ++t) in.v[t] = vb[s * VI + t];
       } else {
@@ -2380,27 +2275,27 @@ __global__ __launch_bounds__(SH ? 256 : (SP ? 128 : 64), SP ? 2 : 1) void map_fo
         const int nvx = __builtin_popcount(__builtin_amdgcn_readfirstlane(mv.vm));  // own values, compacted
 #pragma unroll
         for (int m = 0; m < NP; ++m) {
-          const unsigned a0 = rs_a0<SH>(lane, m);
+          const unsigned a0 = ST ? st_a0(lane, m) : rs_a0<SH>(lane, m);
           const unsigned long long a = a0 < A ? a0 : A - 2;
           rg.ea[m] = lds2(mirror + a);
           rg.to[m] = lds2(thr + A + a);
           rg.m1[m] = lds2(m1m + a);
-          rg.cs[m] = lds2(csm + a);
+          rg.cs[m] = lds2((MAP_TB_INC ? thr : csm) + a);
 #pragma unroll
           for (int q = 0; q < 3; ++q) rg.sq[q][m] = q < nvx ? lds2(mirror + (1 + q) * A + a) : u64x2{0, 0};
         }
-        if constexpr (SP) {  // (B) the partner reloads its operands from the same mirror
+        if constexpr (ST) {  // (B) the partner reloads its operands from the same mirror
           if (lane == 0) *reinterpret_cast<volatile unsigned *>(spst) = (present ? 1u : 0u) | ((unsigned)nvx << 1);
-          sp_barrier();
+          st_barrier();
         }
       }
       // re-issue chunk ch+2 into the slot the exact loop used
       if (SH && ch + 2 < nch) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         sh_chunk_images(shl, (ch + 2) * C, R, wl + slot * SLOT);
-      } else if (SP && ch + 2 < nch) {
+      } else if (ST && ch + 2 < nch) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        sp_chunk_glds(p, spl, g, ch + 2, R, wl + slot * SLOT, cml + slot * CMS, lane);
+        st_chunk_glds(p, gl1, g, ch + 2, R, wl + slot * SLOT, WS, cml + slot * CMS, lane, 0);
       } else if (ch + 2 < nch) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         map_chunk_glds<VI, C, 1>(p, gl1, g, k, (ch + 2) * C, R, wl + slot * SLOT, WS, vbase + slot * C * VI,
@@ -2490,24 +2385,23 @@ __global__ __launch_bounds__(64) void map_chunk_max_kernel(const u64 *clock, lon
   }
 }
 
-template <int APL, int VI, int VO, int CM, int NB, bool GL, int ITM, int NP = 0, bool SP = false>
+template <int APL, int VI, int VO, int CM, int NB, bool GL, int ITM, int NP = 0, bool ST = false>
 static hipError_t launch_map_it(const MapPlan &p, unsigned long long blocks, hipStream_t s) {
   constexpr bool RS = NP > 0;
   constexpr int C = (GL || RS) ? CM : MapChunk<APL, VI, CM>::C;
   const size_t W = (2 + VI) * p.A;
-  // (the kernel's PW: slots, values, remove lists, mirror, clock-max copies, thresholds, SP words)
-  const size_t slots = SP ? 2 * NB * (size_t)kSpSlot : (size_t)NB * C * map_ws(W);
-  const size_t lds = (slots + (size_t)NB * C * VI) * sizeof(u64) + kMapL * 2 * sizeof(unsigned) +
-                     (2 + VO) * p.A * sizeof(u64) + ((GL || RS) ? (SP ? 2 : 1) * NB * p.A * sizeof(u64) : 0) +
-                     4 * p.A * sizeof(u64) + (SP ? 18 * sizeof(u64) : 0);
+  // (the kernel's PW: slots, values, remove lists, mirror, clock-max copies, thresholds, ST words)
+  const size_t lds = (size_t)NB * C * (map_ws(W) + VI) * sizeof(u64) + kMapL * 2 * sizeof(unsigned) +
+                     (2 + VO) * p.A * sizeof(u64) + ((GL || RS) ? (ST ? 2 : 1) * NB * p.A * sizeof(u64) : 0) +
+                     4 * p.A * sizeof(u64) + (ST ? 4 * sizeof(u64) : 0);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
-  auto *fn = &map_fold_kernel<APL, VI, VO, CM, NB, GL, ITM, NP, false, SP>;
+  auto *fn = &map_fold_kernel<APL, VI, VO, CM, NB, GL, ITM, NP, false, ST>;
   if (lds > 64 * 1024) {  // beyond the default dynamic-LDS limit (gfx950 has 160 KB per CU)
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(SP ? 128 : 64), lds, s, p);
+  hipLaunchKernelGGL(fn, dim3((unsigned)blocks), dim3(ST ? 128 : 64), lds, s, p);
   return hipGetLastError();
 }
 
@@ -2517,7 +2411,7 @@ template <int VI>
 static hipError_t launch_map_rs(const MapPlan &p, unsigned long long blocks, hipStream_t s) {
   // two waves per key at config 4's shape (A = 32, V = 2)
   if constexpr (VI == 2) {
-    if (p.sp && p.A == 32) return launch_map_it<1, 2, 4, 16, 2, false, 4, 2, true>(p, blocks, s);
+    if (p.st && p.A == 32) return launch_map_it<1, 2, 4, 16, 2, false, 4, 2, true>(p, blocks, s);
   }
   if (p.A <= 8) return launch_map_it<1, VI, 4, 16, 2, false, 2, 1>(p, blocks, s);
   if (p.A <= 16) return launch_map_it<1, VI, 4, 16, 2, false, 4, 2>(p, blocks, s);
@@ -2657,7 +2551,7 @@ static int map_lub_impl(crdt_ctx *ctx, const crdt_map_batch *in, const u64 *doff
   // scratch: [def_off copy | chunk clock maxima]
   const size_t off_b = D > 0 || doff ? ((G + 1) * sizeof(size_t) + 255) / 256 * 256 : 0;
   if (glds) p.nch = (R + gC - 1) / gC;
-  p.sp = rs && ctx->tune.map_sp && A == 32 && V == 2 && !(ctx->tune.map_sh && K % 4 == 0);
+  p.st = rs && ctx->tune.map_st && A == 32 && V == 2 && !(ctx->tune.map_sh && K % 4 == 0);
   const size_t cm_b = glds ? G * p.nch * A * sizeof(u64) : 0;
   if (off_b + cm_b > 0)
     if (int rc = ensure_scratch(ctx, off_b + cm_b)) return rc;

@@ -27,6 +27,9 @@ namespace crdt {
 // read of each field per op).  With it the kernel runs at 7 waves per SIMD (room for the batch's
 // registers): 1.89 ms against 2.17 ms for per-op reads at 8 and 2.30 ms for the batch at 8
 // (profiles/r05_vapply_hdr_ab.log, r05_mca_h1w_ab.log)
+// Deferred slots held in LDS per state (the rest of the caller's Dcap slots are used in place, in global
+// memory: exact up to Dcap, slower past kMcaDl).  16 = the round-5 LDS footprint.
+constexpr size_t kMcaDl = 16;
 #ifndef CRDT_MCA_HDR
 #define CRDT_MCA_HDR 1
 #endif
@@ -38,6 +41,7 @@ struct MapCounterApplyPlan {
   u64 *clock, *ec, *val;
   unsigned long long c_s, e_s, v_s;  // state strides (words)
   unsigned long long N, K, A, W, Kw, Dcap;
+  unsigned long long Dl;  // deferred slots held in LDS (<= Dcap); slots Dl .. Dcap-1 stay in def_clock / def_keys
   u64 *def_clock, *def_keys;
   unsigned *def_count;
   const u64 *op_off;
@@ -66,9 +70,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APL <= 2 ? 
   const int lane = (int)(threadIdx.x % kWave), wv = (int)(threadIdx.x / kWave);
   const unsigned long long s = (unsigned long long)blockIdx.x * p.wpb + wv;
   if (wv >= (int)p.wpb || s >= p.N) return;  // (whole waves)
-  const unsigned long long A = p.A, K = p.K, W = p.W, Kw = p.Kw, Dcap = p.Dcap;
-  u64 *sclk = lds + (unsigned long long)wv * Dcap * (A + Kw);  // [Dcap][A] rm clocks
-  u64 *skey = sclk + Dcap * A;                                 // [Dcap][Kw] key bitmaps
+  const unsigned long long A = p.A, K = p.K, W = p.W, Kw = p.Kw, Dcap = p.Dcap, Dl = p.Dl;
+  // The Map's deferred removes: slots d < Dl in LDS, slots Dl <= d < Dcap in the caller's own slot
+  // arrays (global memory: a long list runs slower, never incomplete below Dcap)
+  u64 *sclk = lds + (unsigned long long)wv * Dl * (A + Kw);  // [Dl][A] rm clocks
+  u64 *skey = sclk + Dl * A;                                 // [Dl][Kw] key bitmaps
+  u64 *gclk = p.def_clock + s * Dcap * A, *gkey = p.def_keys + s * Dcap * Kw;
+  // (d is wave-uniform: one branch per access, each side keeps its own address space — no flat ops)
+  auto clk = [&](unsigned d, unsigned long long a) -> u64 {
+    if (d < Dl) return sclk[d * A + a];
+    return gclk[d * A + a];
+  };
+  auto set_clk = [&](unsigned d, unsigned long long a, u64 v) {
+    if (d < Dl) sclk[d * A + a] = v;
+    else gclk[d * A + a] = v;
+  };
+  auto key = [&](unsigned d, unsigned long long w) -> u64 {
+    if (d < Dl) return skey[d * Kw + w];
+    return gkey[d * Kw + w];
+  };
+  auto set_key = [&](unsigned d, unsigned long long w, u64 v) {
+    if (d < Dl) skey[d * Kw + w] = v;
+    else gkey[d * Kw + w] = v;
+  };
   const unsigned long long ob = p.op_off[s], oe = p.op_off[s + 1];
   unsigned dcnt = p.def_count[s];
   if (dcnt > Dcap || oe < ob || oe > p.n_ops) {
@@ -81,11 +105,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APL <= 2 ? 
   u64 c[APL];
 #pragma unroll
   for (int j = 0; j < APL; ++j) c[j] = word(j) < A ? C[word(j)] : 0ull;
-  for (unsigned d = 0; d < dcnt; ++d) {
-    for (unsigned long long a = (unsigned long long)lane; a < A; a += kWave)
-      sclk[d * A + a] = p.def_clock[(s * Dcap + d) * A + a];
-    for (unsigned long long w = (unsigned long long)lane; w < Kw; w += kWave)
-      skey[d * Kw + w] = p.def_keys[(s * Dcap + d) * Kw + w];
+  for (unsigned d = 0; d < dcnt && d < Dl; ++d) {
+    for (unsigned long long a = (unsigned long long)lane; a < A; a += kWave) sclk[d * A + a] = gclk[d * A + a];
+    for (unsigned long long w = (unsigned long long)lane; w < Kw; w += kWave) skey[d * Kw + w] = gkey[d * Kw + w];
   }
 
   // the clock's word of actor a (uniform)
@@ -141,23 +163,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APL <= 2 ? 
     for (unsigned d = 0; d < dcnt; ++d) {
       u64 r[APL];
 #pragma unroll
-      for (int j = 0; j < APL; ++j) r[j] = word(j) < A ? sclk[d * A + word(j)] : 0ull;
+      for (int j = 0; j < APL; ++j) r[j] = word(j) < A ? clk(d, word(j)) : 0ull;
       if (full) {
         for (unsigned long long w = 0; w < Kw; ++w) {
-          u64 bits = skey[d * Kw + w];
+          u64 bits = key(d, w);
           while (bits) {
             const unsigned long long k = w * 64 + (unsigned long long)__builtin_ctzll(bits);
             bits &= bits - 1;
             if (k < K) key_rm(k, r);
           }
         }
-      } else if ((skey[d * Kw + kk / 64] >> (kk % 64)) & 1ull) {
+      } else if ((key(d, kk / 64) >> (kk % 64)) & 1ull) {
         key_rm(kk, r);
       }
       if (dominated(r)) continue;  // no longer deferred
       if (o != d) {
-        for (unsigned long long a = (unsigned long long)lane; a < A; a += kWave) sclk[o * A + a] = sclk[d * A + a];
-        for (unsigned long long w = (unsigned long long)lane; w < Kw; w += kWave) skey[o * Kw + w] = skey[d * Kw + w];
+        for (unsigned long long a = (unsigned long long)lane; a < A; a += kWave) set_clk(o, a, clk(d, a));
+        for (unsigned long long w = (unsigned long long)lane; w < Kw; w += kWave) set_key(o, w, key(d, w));
       }
       ++o;
     }
@@ -222,7 +244,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APL <= 2 ? 
       for (unsigned d = 0; d < dcnt && slot < 0; ++d) {
         bool ne = false;
 #pragma unroll
-        for (int j = 0; j < APL; ++j) ne = ne || (word(j) < A && sclk[d * A + word(j)] != r[j]);
+        for (int j = 0; j < APL; ++j) ne = ne || (word(j) < A && clk(d, word(j)) != r[j]);
         if (!__ballot(ne)) slot = (int)d;
       }
       if (slot < 0) {
@@ -233,13 +255,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APL <= 2 ? 
         slot = (int)dcnt++;
 #pragma unroll
         for (int j = 0; j < APL; ++j)
-          if (word(j) < A) sclk[slot * A + word(j)] = r[j];
-        for (unsigned long long w = (unsigned long long)lane; w < Kw; w += kWave) skey[slot * Kw + w] = 0;
+          if (word(j) < A) set_clk(slot, word(j), r[j]);
+        for (unsigned long long w = (unsigned long long)lane; w < Kw; w += kWave) set_key(slot, w, 0);
       }
       // deferred_set.append(keyset): one lane per key word
       for (u64 i = kb; i < ke; ++i) {
         const unsigned long long k = p.keys[i];
-        if (k < K && (unsigned long long)lane == (k / 64) % kWave) skey[slot * Kw + k / 64] |= 1ull << (k % 64);
+        if (k < K && (unsigned long long)lane == (k / 64) % kWave) set_key(slot, k / 64, key(slot, k / 64) | 1ull << (k % 64));
       }
     } else {
       st |= 2u;
@@ -249,11 +271,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APL <= 2 ? 
 #pragma unroll
   for (int j = 0; j < APL; ++j)
     if (word(j) < A) C[word(j)] = c[j];
-  for (unsigned d = 0; d < dcnt; ++d) {
-    for (unsigned long long a = (unsigned long long)lane; a < A; a += kWave)
-      p.def_clock[(s * Dcap + d) * A + a] = sclk[d * A + a];
-    for (unsigned long long w = (unsigned long long)lane; w < Kw; w += kWave)
-      p.def_keys[(s * Dcap + d) * Kw + w] = skey[d * Kw + w];
+  for (unsigned d = 0; d < dcnt && d < Dl; ++d) {  // (slots past Dl are already in place)
+    for (unsigned long long a = (unsigned long long)lane; a < A; a += kWave) gclk[d * A + a] = sclk[d * A + a];
+    for (unsigned long long w = (unsigned long long)lane; w < Kw; w += kWave) gkey[d * Kw + w] = skey[d * Kw + w];
   }
   if (lane == 0) {
     p.def_count[s] = dcnt;
@@ -282,15 +302,15 @@ extern "C" int crdt_map_counter_apply_batch(crdt_ctx *ctx, const crdt_map_counte
   if (m->clock_stride < A || m->ec_stride < K * A || m->val_stride < K * W * A)
     return fail(ctx, CRDT_EINVAL, "map_counter_apply_batch: strides smaller than the rows they hold");
   const size_t Kw = K ? (K + 63) / 64 : 1;
-  const size_t per_wave = Dcap * (A + Kw) * 8;
-  if (per_wave > 64 * 1024)
-    return fail(ctx, CRDT_EUNSUPPORTED, "map_counter_apply_batch: Dcap * (A + ceil(K/64)) = %zu words > 8192",
-                per_wave / 8);
+  // deferred slots in LDS: up to kMcaDl (the rest of Dcap in the caller's slot arrays), fewer where a
+  // slot is wide (at most 8,192 words per wave)
+  const size_t Dl = std::min<size_t>(Dcap, std::min<size_t>(kMcaDl, 8192 / (A + Kw)));
+  const size_t per_wave = Dl * (A + Kw) * 8;
   unsigned wpb = 4;
   while (wpb > 1 && per_wave * wpb > 64 * 1024) --wpb;
   CRDT_HIP(ctx, hipSetDevice(ctx->device));
   MapCounterApplyPlan p{(u64 *)m->clock, (u64 *)m->ec, (u64 *)m->val, m->clock_stride, m->ec_stride, m->val_stride,
-                        N, K, A, W, Kw, Dcap, (u64 *)def_clock, (u64 *)def_keys, def_count,
+                        N, K, A, W, Kw, Dcap, Dl, (u64 *)def_clock, (u64 *)def_keys, def_count,
                         (const u64 *)ops->op_off, ops->kind, ops->actor, ops->key, ops->vactor,
                         (const u64 *)ops->counter, (const u64 *)ops->vcounter, ops->vdir, ops->clk_row,
                         (const u64 *)ops->clk_pool, ops->clk_pool ? ops->n_clk_rows : 0,

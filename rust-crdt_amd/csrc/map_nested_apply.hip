@@ -33,6 +33,7 @@ struct NestedApplyPlan {
   u64 *clock, *ec, *ic, *iec, *ivc, *ivv, *id_clock, *id_keys;
   unsigned *nval, *id_n;
   unsigned long long N, K, K2, A, Kw, Dcap;
+  unsigned long long Dl;  // outer deferred slots held in LDS (<= Dcap); slots Dl .. Dcap-1 stay in place
   u64 *def_clock, *def_keys;
   unsigned *def_count;
   const u64 *op_off;
@@ -358,9 +359,29 @@ __global__ __launch_bounds__(256) MNA_WPE_ATTR void map_nested_apply_kernel(Nest
   const int lane = (int)(threadIdx.x % kWave), wv = (int)(threadIdx.x / kWave);
   const unsigned long long s = (unsigned long long)blockIdx.x * p.wpb + wv;
   if (wv >= (int)p.wpb || s >= p.N) return;  // (whole waves)
-  const unsigned long long A = p.A, K = p.K, K2 = p.K2, Kw = p.Kw, Dcap = p.Dcap;
-  u64 *sclk = lds + (unsigned long long)wv * Dcap * (A + Kw);  // [Dcap][A] the outer rm clocks
-  u64 *skey = sclk + Dcap * A;                                 // [Dcap][Kw] their key bitmaps
+  const unsigned long long A = p.A, K = p.K, K2 = p.K2, Kw = p.Kw, Dcap = p.Dcap, Dl = p.Dl;
+  // The outer deferred removes: slots d < Dl in LDS, slots Dl <= d < Dcap in the caller's own slot
+  // arrays (global memory: a long list runs slower, never incomplete below Dcap)
+  u64 *sclk = lds + (unsigned long long)wv * Dl * (A + Kw);  // [Dl][A] the outer rm clocks
+  u64 *skey = sclk + Dl * A;                                 // [Dl][Kw] their key bitmaps
+  u64 *gclk = p.def_clock + s * Dcap * A, *gkey = p.def_keys + s * Dcap * Kw;
+  // (d is wave-uniform: one branch per access, each side keeps its own address space — no flat ops)
+  auto clk = [&](unsigned d, unsigned long long a) -> u64 {
+    if (d < Dl) return sclk[d * A + a];
+    return gclk[d * A + a];
+  };
+  auto set_clk = [&](unsigned d, unsigned long long a, u64 v) {
+    if (d < Dl) sclk[d * A + a] = v;
+    else gclk[d * A + a] = v;
+  };
+  auto key = [&](unsigned d, unsigned long long w) -> u64 {
+    if (d < Dl) return skey[d * Kw + w];
+    return gkey[d * Kw + w];
+  };
+  auto set_key = [&](unsigned d, unsigned long long w, u64 v) {
+    if (d < Dl) skey[d * Kw + w] = v;
+    else gkey[d * Kw + w] = v;
+  };
   const unsigned long long ob = p.op_off[s], oe = p.op_off[s + 1];
   unsigned dcnt = p.def_count[s];
   if (dcnt > Dcap || oe < ob || oe > p.n_ops) {
@@ -373,11 +394,9 @@ __global__ __launch_bounds__(256) MNA_WPE_ATTR void map_nested_apply_kernel(Nest
   u64 c[APL];
 #pragma unroll
   for (int j = 0; j < APL; ++j) c[j] = word(j) < A ? C[word(j)] : 0ull;
-  for (unsigned d = 0; d < dcnt; ++d) {
-    for (unsigned long long a = (unsigned long long)lane; a < A; a += kWave)
-      sclk[d * A + a] = p.def_clock[(s * Dcap + d) * A + a];
-    for (unsigned long long w = (unsigned long long)lane; w < Kw; w += kWave)
-      skey[d * Kw + w] = p.def_keys[(s * Dcap + d) * Kw + w];
+  for (unsigned d = 0; d < dcnt && d < Dl; ++d) {
+    for (unsigned long long a = (unsigned long long)lane; a < A; a += kWave) sclk[d * A + a] = gclk[d * A + a];
+    for (unsigned long long w = (unsigned long long)lane; w < Kw; w += kWave) skey[d * Kw + w] = gkey[d * Kw + w];
   }
   // apply_deferred (map.rs:311-316): full on its first run, then restricted to the Up's own key (the
   // only rows an Up changes; forgets are idempotent and commute — see csrc/map_counter_apply.hip)
@@ -387,9 +406,9 @@ __global__ __launch_bounds__(256) MNA_WPE_ATTR void map_nested_apply_kernel(Nest
     for (unsigned d = 0; d < dcnt; ++d) {
       u64 r[APL];
 #pragma unroll
-      for (int j = 0; j < APL; ++j) r[j] = word(j) < A ? sclk[d * A + word(j)] : 0ull;
+      for (int j = 0; j < APL; ++j) r[j] = word(j) < A ? clk(d, word(j)) : 0ull;
       for (unsigned long long w = full ? 0 : kk / 64; w < (full ? Kw : kk / 64 + 1); ++w) {
-        u64 bits = skey[d * Kw + w] & (full ? ~0ull : 1ull << (kk % 64));
+        u64 bits = key(d, w) & (full ? ~0ull : 1ull << (kk % 64));
         while (bits) {
           const unsigned long long k = w * 64 + (unsigned long long)__builtin_ctzll(bits);
           bits &= bits - 1;
@@ -402,8 +421,8 @@ __global__ __launch_bounds__(256) MNA_WPE_ATTR void map_nested_apply_kernel(Nest
       }
       if (NaKey<APL>::leq(r, c)) continue;  // no longer deferred
       if (o != d) {
-        for (unsigned long long a = (unsigned long long)lane; a < A; a += kWave) sclk[o * A + a] = sclk[d * A + a];
-        for (unsigned long long w = (unsigned long long)lane; w < Kw; w += kWave) skey[o * Kw + w] = skey[d * Kw + w];
+        for (unsigned long long a = (unsigned long long)lane; a < A; a += kWave) set_clk(o, a, clk(d, a));
+        for (unsigned long long w = (unsigned long long)lane; w < Kw; w += kWave) set_key(o, w, key(d, w));
       }
       ++o;
     }
@@ -474,7 +493,7 @@ __global__ __launch_bounds__(256) MNA_WPE_ATTR void map_nested_apply_kernel(Nest
       for (unsigned d = 0; d < dcnt && slot < 0; ++d) {
         bool ne = false;
 #pragma unroll
-        for (int j = 0; j < APL; ++j) ne = ne || (word(j) < A && sclk[d * A + word(j)] != r[j]);
+        for (int j = 0; j < APL; ++j) ne = ne || (word(j) < A && clk(d, word(j)) != r[j]);
         if (!__ballot(ne)) slot = (int)d;
       }
       if (slot < 0) {
@@ -485,12 +504,12 @@ __global__ __launch_bounds__(256) MNA_WPE_ATTR void map_nested_apply_kernel(Nest
         slot = (int)dcnt++;
 #pragma unroll
         for (int j = 0; j < APL; ++j)
-          if (word(j) < A) sclk[slot * A + word(j)] = r[j];
-        for (unsigned long long w = (unsigned long long)lane; w < Kw; w += kWave) skey[slot * Kw + w] = 0;
+          if (word(j) < A) set_clk(slot, word(j), r[j]);
+        for (unsigned long long w = (unsigned long long)lane; w < Kw; w += kWave) set_key(slot, w, 0);
       }
       for (u64 i = kb; i < ke; ++i) {
         const unsigned long long k = p.keys[i];
-        if (k < K && (unsigned long long)lane == (k / 64) % kWave) skey[slot * Kw + k / 64] |= 1ull << (k % 64);
+        if (k < K && (unsigned long long)lane == (k / 64) % kWave) set_key(slot, k / 64, key(slot, k / 64) | 1ull << (k % 64));
       }
     } else {
       st |= 2u;
@@ -500,11 +519,9 @@ __global__ __launch_bounds__(256) MNA_WPE_ATTR void map_nested_apply_kernel(Nest
 #pragma unroll
   for (int j = 0; j < APL; ++j)
     if (word(j) < A) C[word(j)] = c[j];
-  for (unsigned d = 0; d < dcnt; ++d) {
-    for (unsigned long long a = (unsigned long long)lane; a < A; a += kWave)
-      p.def_clock[(s * Dcap + d) * A + a] = sclk[d * A + a];
-    for (unsigned long long w = (unsigned long long)lane; w < Kw; w += kWave)
-      p.def_keys[(s * Dcap + d) * Kw + w] = skey[d * Kw + w];
+  for (unsigned d = 0; d < dcnt && d < Dl; ++d) {  // (slots past Dl are already in place)
+    for (unsigned long long a = (unsigned long long)lane; a < A; a += kWave) gclk[d * A + a] = sclk[d * A + a];
+    for (unsigned long long w = (unsigned long long)lane; w < Kw; w += kWave) gkey[d * Kw + w] = skey[d * Kw + w];
   }
   if (lane == 0) {
     p.def_count[s] = dcnt;
@@ -576,13 +593,15 @@ extern "C" int crdt_map_nested_apply_batch(crdt_ctx *ctx, const crdt_map_nested_
                      !ops->icounter || !ops->ikey || !ops->val || !ops->ikeys || !ops->clk_row))
     return fail(ctx, CRDT_EINVAL, "map_nested_apply_batch: NULL op buffer");
   NestedApplyPlan p = nested_plan(m);
-  const size_t per_wave = Dcap * (A + p.Kw) * 8;
-  if (per_wave > 64 * 1024)
-    return fail(ctx, CRDT_EUNSUPPORTED, "map_nested_apply_batch: Dcap * (A + ceil(K/64)) too large for LDS");
+  // outer deferred slots in LDS: up to 16 (the rest of Dcap in the caller's slot arrays), fewer where a
+  // slot is wide (at most 8,192 words per wave)
+  const size_t Dl = std::min<size_t>(Dcap, std::min<size_t>(16, 8192 / (A + p.Kw)));
+  const size_t per_wave = Dl * (A + p.Kw) * 8;
   unsigned wpb = 4;
   while (wpb > 1 && per_wave * wpb > 64 * 1024) --wpb;
   CRDT_HIP(ctx, hipSetDevice(ctx->device));
   p.Dcap = Dcap;
+  p.Dl = Dl;
   p.def_clock = (u64 *)def_clock;
   p.def_keys = (u64 *)def_keys;
   p.def_count = def_count;

@@ -30,11 +30,13 @@ namespace crdt {
 
 constexpr int kMoaVd = 16;    // nested deferred slots per key (crdt_map_orswot_out)
 constexpr int kMoaMw = 16;    // member-mask words (M <= 1,024)
+constexpr size_t kMoaDl = 16;  // the Map's deferred slots held in LDS per state (the rest of Dcap in place)
 
 struct MapOrswotApplyPlan {
   u64 *clock, *ec, *oc, *ent, *vd_clock, *vd_mem;
   unsigned *vd_n;
   unsigned long long N, K, M, A, Mw, Kw, Dcap;
+  unsigned long long Dl;  // the Map's deferred slots held in LDS (<= Dcap); slots Dl .. Dcap-1 stay in place
   u64 *def_clock, *def_keys;
   unsigned *def_count;
   const u64 *op_off;
@@ -65,11 +67,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APL <= 2 ? 
   const int lane = (int)(threadIdx.x % kWave), wv = (int)(threadIdx.x / kWave);
   const unsigned long long s = (unsigned long long)blockIdx.x * p.wpb + wv;
   if (wv >= (int)p.wpb || s >= p.N) return;  // (whole waves)
-  const unsigned long long A = p.A, K = p.K, M = p.M, Mw = p.Mw, Kw = p.Kw, Dcap = p.Dcap;
-  const unsigned long long WQ = Dcap * (A + Kw) + kMoaVd * kMoaMw;
-  u64 *sclk = lds + (unsigned long long)wv * WQ;  // [Dcap][A] the Map's rm clocks
-  u64 *skey = sclk + Dcap * A;                     // [Dcap][Kw] their key bitmaps
-  u64 *smsk = skey + Dcap * Kw;                    // [16][Mw] the current key's nested member masks
+  const unsigned long long A = p.A, K = p.K, M = p.M, Mw = p.Mw, Kw = p.Kw, Dcap = p.Dcap, Dl = p.Dl;
+  const unsigned long long WQ = Dl * (A + Kw) + kMoaVd * kMoaMw;
+  // The Map's deferred removes: slots d < Dl in LDS, slots Dl <= d < Dcap in the caller's own slot
+  // arrays (global memory: a long list runs slower, never incomplete below Dcap)
+  u64 *sclk = lds + (unsigned long long)wv * WQ;  // [Dl][A] the Map's rm clocks
+  u64 *skey = sclk + Dl * A;                       // [Dl][Kw] their key bitmaps
+  u64 *smsk = skey + Dl * Kw;                      // [16][Mw] the current key's nested member masks
   const unsigned long long ob = p.op_off[s], oe = p.op_off[s + 1];
   unsigned dcnt = p.def_count[s];
   if (dcnt > Dcap || oe < ob || oe > p.n_ops) {
@@ -78,15 +82,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APL <= 2 ? 
   }
   unsigned st = 0;
   auto word = [&](int j) { return (unsigned long long)lane + 64ull * j; };
+  u64 *gclk = p.def_clock + s * Dcap * A, *gkey = p.def_keys + s * Dcap * Kw;
+  // (d is wave-uniform: one branch per access, each side keeps its own address space — no flat ops)
+  auto clk = [&](unsigned d, unsigned long long a) -> u64 {
+    if (d < Dl) return sclk[d * A + a];
+    return gclk[d * A + a];
+  };
+  auto set_clk = [&](unsigned d, unsigned long long a, u64 v) {
+    if (d < Dl) sclk[d * A + a] = v;
+    else gclk[d * A + a] = v;
+  };
+  auto key = [&](unsigned d, unsigned long long w) -> u64 {
+    if (d < Dl) return skey[d * Kw + w];
+    return gkey[d * Kw + w];
+  };
+  auto set_key = [&](unsigned d, unsigned long long w, u64 v) {
+    if (d < Dl) skey[d * Kw + w] = v;
+    else gkey[d * Kw + w] = v;
+  };
   u64 *C = p.clock + s * A;
   u64 c[APL];
 #pragma unroll
   for (int j = 0; j < APL; ++j) c[j] = word(j) < A ? C[word(j)] : 0ull;
-  for (unsigned d = 0; d < dcnt; ++d) {
-    for (unsigned long long a = (unsigned long long)lane; a < A; a += kWave)
-      sclk[d * A + a] = p.def_clock[(s * Dcap + d) * A + a];
-    for (unsigned long long w = (unsigned long long)lane; w < Kw; w += kWave)
-      skey[d * Kw + w] = p.def_keys[(s * Dcap + d) * Kw + w];
+  for (unsigned d = 0; d < dcnt && d < Dl; ++d) {
+    for (unsigned long long a = (unsigned long long)lane; a < A; a += kWave) sclk[d * A + a] = gclk[d * A + a];
+    for (unsigned long long w = (unsigned long long)lane; w < Kw; w += kWave) skey[d * Kw + w] = gkey[d * Kw + w];
   }
   auto ldrow = [&](const u64 *row, u64 (&x)[APL]) {
 #pragma unroll
@@ -247,9 +267,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APL <= 2 ? 
     for (unsigned d = 0; d < dcnt; ++d) {
       u64 r[APL];
 #pragma unroll
-      for (int j = 0; j < APL; ++j) r[j] = word(j) < A ? sclk[d * A + word(j)] : 0ull;
+      for (int j = 0; j < APL; ++j) r[j] = word(j) < A ? clk(d, word(j)) : 0ull;
       for (unsigned long long w = full ? 0 : kk / 64; w < (full ? Kw : kk / 64 + 1); ++w) {
-        u64 bits = skey[d * Kw + w] & (full ? ~0ull : 1ull << (kk % 64));
+        u64 bits = key(d, w) & (full ? ~0ull : 1ull << (kk % 64));
         while (bits) {
           const unsigned long long k = w * 64 + (unsigned long long)__builtin_ctzll(bits);
           bits &= bits - 1;
@@ -258,8 +278,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APL <= 2 ? 
       }
       if (leq(r, c)) continue;  // no longer deferred
       if (o != d) {
-        for (unsigned long long a = (unsigned long long)lane; a < A; a += kWave) sclk[o * A + a] = sclk[d * A + a];
-        for (unsigned long long w = (unsigned long long)lane; w < Kw; w += kWave) skey[o * Kw + w] = skey[d * Kw + w];
+        for (unsigned long long a = (unsigned long long)lane; a < A; a += kWave) set_clk(o, a, clk(d, a));
+        for (unsigned long long w = (unsigned long long)lane; w < Kw; w += kWave) set_key(o, w, key(d, w));
       }
       ++o;
     }
@@ -390,7 +410,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APL <= 2 ? 
       for (unsigned d = 0; d < dcnt && slot < 0; ++d) {
         bool ne = false;
 #pragma unroll
-        for (int j = 0; j < APL; ++j) ne = ne || (word(j) < A && sclk[d * A + word(j)] != r[j]);
+        for (int j = 0; j < APL; ++j) ne = ne || (word(j) < A && clk(d, word(j)) != r[j]);
         if (!__ballot(ne)) slot = (int)d;
       }
       if (slot < 0) {
@@ -401,12 +421,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APL <= 2 ? 
         slot = (int)dcnt++;
 #pragma unroll
         for (int j = 0; j < APL; ++j)
-          if (word(j) < A) sclk[slot * A + word(j)] = r[j];
-        for (unsigned long long w = (unsigned long long)lane; w < Kw; w += kWave) skey[slot * Kw + w] = 0;
+          if (word(j) < A) set_clk(slot, word(j), r[j]);
+        for (unsigned long long w = (unsigned long long)lane; w < Kw; w += kWave) set_key(slot, w, 0);
       }
       for (u64 i = kb; i < ke; ++i) {
         const unsigned long long k = p.keys[i];
-        if (k < K && (unsigned long long)lane == (k / 64) % kWave) skey[slot * Kw + k / 64] |= 1ull << (k % 64);
+        if (k < K && (unsigned long long)lane == (k / 64) % kWave) set_key(slot, k / 64, key(slot, k / 64) | 1ull << (k % 64));
       }
     } else {
       st |= 2u;
@@ -416,11 +436,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APL <= 2 ? 
 #pragma unroll
   for (int j = 0; j < APL; ++j)
     if (word(j) < A) C[word(j)] = c[j];
-  for (unsigned d = 0; d < dcnt; ++d) {
-    for (unsigned long long a = (unsigned long long)lane; a < A; a += kWave)
-      p.def_clock[(s * Dcap + d) * A + a] = sclk[d * A + a];
-    for (unsigned long long w = (unsigned long long)lane; w < Kw; w += kWave)
-      p.def_keys[(s * Dcap + d) * Kw + w] = skey[d * Kw + w];
+  for (unsigned d = 0; d < dcnt && d < Dl; ++d) {  // (slots past Dl are already in place)
+    for (unsigned long long a = (unsigned long long)lane; a < A; a += kWave) gclk[d * A + a] = sclk[d * A + a];
+    for (unsigned long long w = (unsigned long long)lane; w < Kw; w += kWave) gkey[d * Kw + w] = skey[d * Kw + w];
   }
   if (lane == 0) {
     p.def_count[s] = dcnt;
@@ -449,14 +467,15 @@ extern "C" int crdt_map_orswot_apply_batch(crdt_ctx *ctx, const crdt_map_orswot_
                      !ops->vcounter || !ops->clk_row))
     return fail(ctx, CRDT_EINVAL, "map_orswot_apply_batch: NULL op buffer");
   const size_t Kw = K ? (K + 63) / 64 : 1, Mw = M > 64 ? (M + 63) / 64 : 1;
-  const size_t per_wave = (Dcap * (A + Kw) + kMoaVd * kMoaMw) * 8;
-  if (per_wave > 64 * 1024)
-    return fail(ctx, CRDT_EUNSUPPORTED, "map_orswot_apply_batch: Dcap * (A + ceil(K/64)) too large for LDS");
+  // the Map's deferred slots in LDS: up to kMoaDl (the rest of Dcap in the caller's slot arrays), fewer
+  // where a slot is wide (the wave's LDS at most 8,192 words)
+  const size_t Dl = std::min<size_t>(Dcap, std::min<size_t>(kMoaDl, (8192 - kMoaVd * kMoaMw) / (A + Kw)));
+  const size_t per_wave = (Dl * (A + Kw) + kMoaVd * kMoaMw) * 8;
   unsigned wpb = 4;
   while (wpb > 1 && per_wave * wpb > 64 * 1024) --wpb;
   CRDT_HIP(ctx, hipSetDevice(ctx->device));
   MapOrswotApplyPlan p{(u64 *)m->clock, (u64 *)m->ec, (u64 *)m->oc, (u64 *)m->ent, (u64 *)m->vd_clock,
-                       (u64 *)m->vd_mem, m->vd_n, N, K, M, A, Mw, Kw, Dcap, (u64 *)def_clock, (u64 *)def_keys,
+                       (u64 *)m->vd_mem, m->vd_n, N, K, M, A, Mw, Kw, Dcap, Dl, (u64 *)def_clock, (u64 *)def_keys,
                        def_count, (const u64 *)ops->op_off, ops->kind, ops->vkind, ops->actor, ops->key, ops->vactor,
                        (const u64 *)ops->counter, (const u64 *)ops->vcounter, ops->clk_row,
                        (const u64 *)ops->clk_pool, ops->clk_pool ? ops->n_clk_rows : 0, (const u64 *)ops->key_off,

@@ -1,4 +1,4 @@
-"""Diagnose the SP (two waves per key) Map fold against the RS path and the oracle on the
+"""Diagnose the ST (two waves per key) Map fold against the RS path and the oracle on the
 old-heavy A = 32, V = 2 inputs of tests/test_gpu_map.py: per case, which keys differ and whether
 repeated SP runs agree with each other (determinism)."""
 import os
@@ -17,7 +17,7 @@ from gpu_util import to_host  # noqa: E402
 
 torch.cuda.set_device(0)
 ctxs = {}
-for spec in ("msp=0", "msp=1"):
+for spec in ("mst=0", "mst=1"):
     c = cg.Context(0)
     c.tune(spec)
     ctxs[spec] = c
@@ -38,8 +38,8 @@ for R, s in cases:
     if int(exp[4].max() if exp[4].size else 0) > 4:
         continue
     exp = O.map_fold(d["clock"], d["ec"], d["vclk"], d["vval"], d["def_row"], d["def_clock"], d["def_keys"], 4)
-    rs = run(ctxs["msp=0"], d)
-    sps = [run(ctxs["msp=1"], d) for _ in range(3)]
+    rs = run(ctxs["mst=0"], d)
+    sps = [run(ctxs["mst=1"], d) for _ in range(3)]
     ok_rs = np.array_equal(rs["ec"], exp[1]) and np.array_equal(rs["vclk"], exp[2])
     det = all(all(np.array_equal(sps[0][n], x[n]) for n in x) for x in sps[1:])
     diff_keys = sorted({int(k) for x in sps for k in np.flatnonzero((x["ec"] != exp[1]).any(axis=1) | (x["vclk"] != exp[2]).reshape(8, -1).any(axis=1))})

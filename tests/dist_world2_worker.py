@@ -276,6 +276,7 @@ def cabi_seam(rank, world, t, h):
     # Then good calls work again: the first agrees the plan, the next two take the agreed-plan path.
     x = t(D.lattice_input("vclock")[0])
     outb = torch.empty(x.shape[1], dtype=torch.int64, device=dev)
+    o["cabi_pre_errors"] = h(cs.lub_many_sharded("vclock", x, ctx=ctx))  # agrees the plan (G = 1, this W)
 
     def bad_call(bad):
         try:

@@ -268,6 +268,7 @@ def test_world2_cabi_errors_agree(outs):
     assert tuple(outs[1]["cabi_error_codes_sync"]) == (EINVAL, EINVAL)
     exp = O.vclock_fold(D.lattice_input("vclock")[0])[0]
     for o in outs:
+        np.testing.assert_array_equal(o["cabi_pre_errors"], exp)
         np.testing.assert_array_equal(o["cabi_after_errors"], exp)
         for r in o["cabi_after_errors_cached"]:
             np.testing.assert_array_equal(r, exp)

@@ -87,8 +87,8 @@ def test_config4_map_full_size(gpu_ctx):
     res = cg.map.lub_many(inp.clock, inp.ec, inp.vclk, inp.vval, def_off=[0, Dn],
                           def_row=torch.from_numpy(rows.astype(np.int32)).cuda(), def_clock=t(dcl),
                           def_keys=t(dks), vout=vout, ctx=gpu_ctx)
-    # the one- and two-wave (msp) forms of the A = 32, V = 2 fold agree on the whole result
-    for spec in ("msp=0", "msp=1"):
+    # the one- and two-wave (mst) forms of the A = 32, V = 2 fold agree on the whole result
+    for spec in ("mst=0", "mst=1"):
         alt = cg.Context(0)
         alt.tune(spec)
         res2 = cg.map.lub_many(inp.clock, inp.ec, inp.vclk, inp.vval, def_off=[0, Dn],

@@ -22,8 +22,8 @@ import crdts_gpu as cg  # noqa: E402
 # LDS-DMA shapes), also with the scan off (mspec=0: every chunk handed to the exact loop); and at
 # A = 32, V = 2, K % 4 == 0 the RS path with four key waves sharing each chunk's clock rows (msh=1,
 # opt-in: less traffic, slower); and at A = 32, V = 2 the RS path with two waves per key, each testing
-# half the actors (msp=1, SP) or one (msp=0).
-MODES = ["mglds=1,mrs=1", "mglds=1,mrs=1,mspec=0", "mglds=1,mrs=1,msh=1", "mglds=1,mrs=1,msp=0", "mglds=1,mrs=1,msp=1",
+# 8 steps of every chunk (mst=1, ST) or one (mst=0).
+MODES = ["mglds=1,mrs=1", "mglds=1,mrs=1,mspec=0", "mglds=1,mrs=1,msh=1", "mglds=1,mrs=1,mst=0", "mglds=1,mrs=1,mst=1",
          "mglds=1,mrs=0,mchunk=16,mring=2,mscan3=1,mnt=0", "mglds=1,mrs=0,mchunk=8,mring=4,mscan3=1,mnt=0",
          "mglds=0,mscan2=0,mnt=0", "mglds=1,mrs=0,mchunk=16,mring=2,mscan3=0,mscan2=0,mnt=0",
          "mglds=1,mrs=0,mchunk=16,mring=2,mscan3=0,mscan2=1,mnt=1", "mglds=0,mscan2=1,mnt=0"]

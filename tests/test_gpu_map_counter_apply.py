@@ -172,3 +172,72 @@ def test_map_counter_apply_offsets_past_the_key_pool(gpu_ctx):
         cg.map.counter_apply_batch(clock, ec, val, dc, dk, cnt, ops._replace(key=ops.key[:0]), ctx=gpu_ctx)
     with pytest.raises(ValueError):
         cg.map.counter_apply_batch(clock, ec, val, dc, dk, cnt, ops._replace(vdir=ops.vdir.cpu()), ctx=gpu_ctx)
+
+
+def _future_rm_streams(rng, maps, K, A, W, T, p_rm=0.55):
+    """Streams whose Rms carry clocks far ahead on actor 0 (distinct per op) while the Ups use actors
+    1.. only: no Rm is ever dominated, so every one stays deferred (a long deferred list)."""
+    streams, oracle_ops = [], []
+    for m in maps:
+        clk = {a: m.clock.get(a) for a in range(A)}
+        ops, oops = [], []
+        for i in range(T):
+            if rng.random() < p_rm:
+                row = {0: clk[0] + 1000 + i}
+                if rng.random() < 0.5:
+                    row[1] = max(1, clk[1])
+                ks = sorted(set(int(z) for z in rng.choice(K, size=int(rng.integers(1, 4)), replace=False)))
+                ops.append(("rm", row, ks))
+                oops.append(O.MapRm(O.VClock(dict(row)), ks))
+            else:
+                a = int(rng.integers(1, A))
+                c = clk[a] + int(rng.integers(1, 3))
+                clk[a] = c
+                k, va, vc, d = int(rng.integers(K)), int(rng.integers(A)), int(rng.integers(1, 60)), int(rng.integers(W))
+                ops.append(("up", a, c, k, va, vc, d))
+                vop = O.Dot(va, vc) if W == 1 else (O.Dot(va, vc), O.PNCounter.POS if d == 0 else O.PNCounter.NEG)
+                oops.append(O.MapUp(O.Dot(a, c), k, vop))
+        streams.append(ops)
+        oracle_ops.append(oops)
+    return streams, oracle_ops
+
+
+@pytest.mark.parametrize("W", [1, 2])
+def test_map_counter_apply_long_deferred_list(gpu_ctx, W):
+    """More deferred removes than the 16 slots the kernel holds in LDS (round 6: slots 16 .. Dcap-1 are
+    used in place in the caller's slot arrays): with Dcap = 48 every state ends with 20+ removes and
+    status 0, equal to the oracle's Map.apply; Dcap = 16 on the same streams flags bit 0."""
+    N, K, A, T = 10, 6, 5, 64
+    maps = O.map_counter_objects(N, K, A, W, seed=44, steps=120)
+    d = O.map_counter_to_dense(maps, K, A, W)
+    rng = np.random.default_rng(7 + W)
+    streams, oracle_ops = _future_rm_streams(rng, maps, K, A, W, T)
+    Kw = (K + 63) // 64
+    for Dcap in (48, 16):
+        dcl = np.zeros((N, Dcap, A), np.uint64)
+        dks = np.zeros((N, Dcap, Kw), np.uint64)
+        cnt = np.zeros(N, np.int32)
+        for j in range(d["def_row"].shape[0]):
+            n = int(d["def_row"][j])
+            dcl[n, cnt[n]] = d["def_clock"][j]
+            dks[n, cnt[n]] = d["def_keys"][j]
+            cnt[n] += 1
+        clock, ec, val = to_dev(d["clock"]), to_dev(d["ec"]), to_dev(d["val"])
+        tdc, tdk, tcnt = to_dev(dcl), to_dev(dks), torch.from_numpy(cnt).cuda()
+        ops = cg.map.encode_counter_ops(streams, A, "cuda:0")
+        status = cg.map.counter_apply_batch(clock, ec, val, tdc, tdk, tcnt, ops, ctx=gpu_ctx).cpu().numpy()
+        if Dcap == 16:
+            assert (status & 1).all()  # every state ran past 16 removes
+            continue
+        c, e, v = to_host(clock), to_host(ec), to_host(val)
+        hdc, hdk, hcnt = to_host(tdc), to_host(tdk), tcnt.cpu().numpy()
+        longest = 0
+        for n in range(N):
+            exp = maps[n].copy()
+            for op in oracle_ops[n]:
+                exp.apply(op)
+            assert status[n] == 0, (n, status[n])
+            dfr = [(hdc[n, i], O.bitmap_members(hdk[n, i])) for i in range(int(hcnt[n]))]
+            assert O.dense_to_map_counter(c[n], e[n], v[n], dfr) == exp, n
+            longest = max(longest, len(exp.deferred))
+        assert 20 <= longest <= 48

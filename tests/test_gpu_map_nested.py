@@ -160,9 +160,9 @@ class _States(NamedTuple):
     id_keys: torch.Tensor
 
 
-def nested_states(maps, K, K2, A):
+def nested_states(maps, K, K2, A, Dcap=16):
     """Dense objects -> (_States on the device, outer deferred as slots (N, Dcap, A) / (N, Dcap, Kw) /
-    (N,) int32 with Dcap = 16, and as a pool (def_clock (D, A), def_state (D,)))."""
+    (N,) int32, and as a pool (def_clock (D, A), def_state (D,)))."""
     N = len(maps)
     d = O.nested_map_to_dense(maps, K, K2, A, 8)
     nval = np.zeros((N, K, K2), np.int32)
@@ -183,7 +183,7 @@ def nested_states(maps, K, K2, A):
     st = _States(to_dev(d["clock"]), to_dev(d["ec"]), to_dev(d["ic"]), to_dev(d["iec"]), to_dev(d["ivc"]),
                  to_dev(d["ivv"]), torch.from_numpy(nval).cuda(), torch.from_numpy(idn).cuda(), to_dev(idc),
                  to_dev(idk))
-    Dcap, Kw = 16, (K + 63) // 64
+    Kw = (K + 63) // 64
     dcl = np.zeros((N, Dcap, A), np.uint64)
     dks = np.zeros((N, Dcap, Kw), np.uint64)
     cnt = np.zeros(N, np.int32)

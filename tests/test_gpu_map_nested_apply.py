@@ -324,3 +324,48 @@ def test_map_nested_apply_unapplied_input_deferred(gpu_ctx):
         got = decode_states(st, i, _slot_deferred(slots, i))
         assert canon(got) == canon(exps[n]) and _regs_in_order(got) == _regs_in_order(exps[n]), n
     assert len(keep) >= 8
+
+
+def test_map_nested_apply_long_outer_deferred_list(gpu_ctx):
+    """More outer deferred removes than the 16 slots the kernel holds in LDS (round 6: the rest of Dcap
+    used in place in the caller's slot arrays): outer Rms from the far future on actor 0 (Ups on actors
+    1..), 20+ removes per state at Dcap = 48, equal to the oracle's Map.apply."""
+    K, K2, A, T, Dcap = 4, 5, 4, 60, 48
+    maps = [m for m in O.nested_map_objects(14, K, K2, A, seed=85, steps=150, p_irm=0.4, p_ooo=0.5, p_rm=0.2)
+            if _fits(m)][:10]
+    N = len(maps)
+    rng = np.random.default_rng(19)
+    streams, oops = [], []
+    for m in maps:
+        clk = {a: m.clock.get(a) for a in range(A)}
+        ops, oo = [], []
+        for i in range(T):
+            if rng.random() < 0.55:
+                row = {0: clk[0] + 1000 + i}
+                ks = sorted(set(int(z) for z in rng.choice(K, size=int(rng.integers(1, 3)), replace=False)))
+                ops.append(("rm", row, ks))
+                oo.append(MapRm(VClock(dict(row)), ks))
+            else:
+                a = int(rng.integers(1, A))
+                c = clk[a] + 1
+                clk[a] = c
+                k, j, ia = int(rng.integers(K)), int(rng.integers(K2)), int(rng.integers(1, A))
+                icn, val = 500 + i, int(rng.integers(100))
+                ops.append(("put", a, c, k, ia, icn, j, {}, val))
+                oo.append(MapUp(Dot(a, c), k, MapUp(Dot(ia, icn), j, MVRegPut(VClock({}), val))))
+        streams.append(ops)
+        oops.append(oo)
+    exps = [m.copy() for m in maps]
+    for n in range(N):
+        for op in oops[n]:
+            exps[n].apply(op)
+    st, slots, _ = nested_states(maps, K, K2, A, Dcap=Dcap)
+    ops = cg.map.encode_nested_ops(streams, A, "cuda:0")
+    status = cg.map.nested_apply_batch(st, *slots, ops, ctx=gpu_ctx).cpu().numpy()
+    longest = 0
+    for n, exp in enumerate(exps):
+        assert status[n] == 0, (n, status[n])
+        got = decode_states(st, n, _slot_deferred(slots, n))
+        assert canon(got) == canon(exp), n
+        longest = max(longest, len(exp.deferred))
+    assert N >= 8 and 20 <= longest <= Dcap

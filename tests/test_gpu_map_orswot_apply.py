@@ -190,3 +190,67 @@ def test_map_orswot_apply_offsets_past_the_pools(gpu_ctx):
     with pytest.raises(TypeError):
         cg.map.orswot_apply_batch(res, z(N, Dcap, A), z(N, Dcap, Kw), torch.zeros(N, dtype=torch.int32, device="cuda:0"),
                                   ops._replace(vcounter=ops.vcounter.to(torch.int32)), ctx=gpu_ctx)
+
+
+def test_map_orswot_apply_long_deferred_list(gpu_ctx):
+    """More Map-level deferred removes than the 16 slots the kernel holds in LDS (round 6: the rest of
+    Dcap used in place in the caller's slot arrays): Map Rms from the far future on actor 0 (Ups on
+    actors 1..), 20+ removes per state at Dcap = 48, equal to the oracle's Map.apply."""
+    N, K, M, A, T, Dcap = 10, 4, 6, 5, 60, 48
+    maps = O.map_orswot_objects(N, K, M, A, seed=63, steps=120, p_vrm=0.3)
+    exps = [O.map_fold_objects([m]) for m in maps]
+    if any(len(e.val.deferred) > cg.map.VD_CAP for x in exps for e in x.entries.values()):
+        pytest.skip("nested deferred past the kernel's capacity")
+    res, kw, off = _states(gpu_ctx, maps, K, M, A)
+    rng = np.random.default_rng(17)
+    streams, oops = [], []
+    for x in exps:
+        clk = {a: x.clock.get(a) for a in range(A)}
+        ops, oo = [], []
+        for i in range(T):
+            if rng.random() < 0.55:
+                row = {0: clk[0] + 1000 + i}
+                ks = sorted(set(int(z) for z in rng.choice(K, size=int(rng.integers(1, 3)), replace=False)))
+                ops.append(("rm", row, ks))
+                oo.append(O.MapRm(O.VClock(dict(row)), ks))
+            else:
+                a = int(rng.integers(1, A))
+                c = clk[a] + 1
+                clk[a] = c
+                k = int(rng.integers(K))
+                ms = sorted(set(int(z) for z in rng.choice(M, size=int(rng.integers(1, 3)), replace=False)))
+                va, vc = int(rng.integers(1, A)), 500 + i
+                ops.append(("add", a, c, k, va, vc, ms))
+                oo.append(O.MapUp(O.Dot(a, c), k, O.OrswotAdd(O.Dot(va, vc), ms)))
+        streams.append(ops)
+        oops.append(oo)
+    for n in range(N):
+        for op in oops[n]:
+            exps[n].apply(op)
+    Kw = (K + 63) // 64
+    dcl = np.zeros((N, Dcap, A), np.uint64)
+    dks = np.zeros((N, Dcap, Kw), np.uint64)
+    cnt = np.zeros(N, np.int32)
+    if kw:
+        keep, hk, hc = res.def_keep.cpu().numpy(), to_host(res.def_keys), to_host(kw["def_clock"])
+        for n in range(N):
+            for j in range(off[n], off[n + 1]):
+                if keep[j]:
+                    dcl[n, cnt[n]], dks[n, cnt[n]] = hc[j], hk[j]
+                    cnt[n] += 1
+    tdc, tdk, tcnt = to_dev(dcl), to_dev(dks), torch.from_numpy(cnt).cuda()
+    ops = cg.map.encode_orswot_map_ops(streams, A, "cuda:0")
+    status = cg.map.orswot_apply_batch(res, tdc, tdk, tcnt, ops, ctx=gpu_ctx).cpu().numpy()
+    c, e, o, m = to_host(res.clock), to_host(res.ec), to_host(res.oc), to_host(res.ent)
+    vn, vc, vm = res.vd_n.cpu().numpy(), to_host(res.vd_clock), to_host(res.vd_mem)
+    hdc, hdk, hcnt = to_host(tdc), to_host(tdk), tcnt.cpu().numpy()
+    longest = 0
+    for n in range(N):
+        assert status[n] == 0, (n, status[n])
+        mw = (lambda k, i: vm[n, k, i]) if vm.ndim == 4 else (lambda k, i: vm[n, k, i:i + 1])  # noqa: E731
+        vd = {k: [(vc[n, k, i], O.bitmap_members(mw(k, i))) for i in range(int(vn[n, k]))] for k in range(K)}
+        dfr = [(hdc[n, i], O.bitmap_members(hdk[n, i])) for i in range(int(hcnt[n]))]
+        got = O.dense_to_map_orswot(c[n], e[n], o[n], m[n], vd, dfr)
+        assert got.clock == exps[n].clock and got.entries == exps[n].entries and got.deferred == exps[n].deferred, n
+        longest = max(longest, len(exps[n].deferred))
+    assert 20 <= longest <= Dcap
