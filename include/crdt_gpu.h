@@ -377,7 +377,10 @@ int crdt_map_counter_forget_batch(crdt_ctx *ctx, const crdt_map_counter_states *
  * .. key_off[o+1]) }.  status[s]: bit 0 = deferred slots exhausted, bit 1 = a malformed op / key
  * skipped, bits 2-3 = invalid input (state untouched).  Limits: A <= 512.  Dcap is not bounded:
  * during the stream the first min(Dcap, 16) slots live in LDS and the rest are used in place in
- * def_clock / def_keys (round 6: exact up to Dcap; bit 0 only past Dcap). */
+ * def_clock / def_keys (round 6: exact up to Dcap; bit 0 only past Dcap).  Slots the list vacates
+ * during a call (a remove that became dominated) are written zero, so a state whose slots past
+ * def_count were zero keeps them zero (the wire ingest's form); the same holds for the Orswot and
+ * nested Map apply below. */
 typedef struct crdt_map_counter_ops {
   size_t n_ops;
   const uint64_t *op_off;    /* [N+1]       */

@@ -70,7 +70,19 @@ struct MapPlan {
 };
 
 constexpr int kMapQ = 4;    // deferred removes tracked per key in registers before the slow path
-constexpr int kMapL = 256;  // removes naming one key listed in LDS (beyond: walk the group list)
+// MAP_RS_WS8 (build option): the RS / ST step images at a stride of 8 (mod 32) words instead of 4, which
+// makes the register test's 16-byte reloads (lane (s, gq), steps 0/3/5/6 and 1/2/4/7 in one LDS lane
+// group) bank-conflict free; the remove list shrinks to 128 entries to keep 4 key waves per CU.
+// MAP_RS_NT (build option, default 1 since round 6): the RS / ST LDS-DMA with the non-temporal policy
+// (aux = 2) — each step image is read once, and keeping it out of the caches' LRU measured 2.175 ms
+// against 2.24 ms at config 4 (profiles/r06_map_ab2.log); 0 restores the default policy.
+#ifndef MAP_RS_WS8
+#define MAP_RS_WS8 0
+#endif
+#ifndef MAP_RS_NT
+#define MAP_RS_NT 1
+#endif
+constexpr int kMapL = MAP_RS_WS8 ? 128 : 256;  // removes naming one key listed in LDS (beyond: walk the group list)
 
 template <int APL, int VI>
 struct MapStep {
@@ -260,6 +272,10 @@ __device__ __forceinline__ void map_chunk_store(const MapChunk<APL, VI, CM> &r, 
 // side by side start 8 banks apart instead of on the same bank.
 __host__ __device__ __forceinline__ unsigned long long map_ws(unsigned long long W) {
   return W + (36 - W % 32) % 32;
+}
+// The RS / ST step stride (MAP_RS_WS8: 8 mod 32 words).
+__host__ __device__ __forceinline__ unsigned long long map_ws_rs(unsigned long long W) {
+  return MAP_RS_WS8 ? W + (40 - W % 32) % 32 : map_ws(W);
 }
 
 // AUX = the cache-policy bits of the load (0: default; 2: non-temporal, the streamed step images)
@@ -1070,7 +1086,7 @@ struct RsDma {
   int diag;  // MapPlan::diag timing probes
   __device__ __forceinline__ void operator()(int j) {
     if (j < 16) {
-      if (!(diag & 2) || j < 13) glds16(src, img + j * WS);
+      if (!(diag & 2) || j < 13) glds16<MAP_RS_NT ? 2 : 0>(src, img + j * WS);
       src += stride;
     } else if (j == 16) {
       if (vp)
@@ -1157,14 +1173,14 @@ __device__ __forceinline__ void st_chunk_glds(const MapPlan &p, const GldsLanes<
     const char *src = L.src0[0] + i0 * L.stride[0];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      glds16(src, dst + j * WS);
+      glds16<MAP_RS_NT ? 2 : 0>(src, dst + j * WS);
       src += L.stride[0];
     }
   } else {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const unsigned long long i = i0 + j < R ? i0 + j : R - 1;
-      glds16(L.src0[0] + i * L.stride[0], dst + j * WS);
+      glds16<MAP_RS_NT ? 2 : 0>(L.src0[0] + i * L.stride[0], dst + j * WS);
     }
   }
   if ((unsigned long long)(2 * lane) < p.A) glds16(p.cmax + (g * p.nch + ch) * p.A + 2 * lane, cm);
@@ -1182,7 +1198,7 @@ struct StDma {
   bool con;
   __device__ __forceinline__ void operator()(int j) {
     if (j < 8) {
-      glds16(src, img + j * WS);
+      glds16<MAP_RS_NT ? 2 : 0>(src, img + j * WS);
       src += stride;
     } else if (con) {
       glds16(csrc, cm);
@@ -1526,7 +1542,7 @@ __global__ __launch_bounds__(SH ? 256 : (ST ? 128 : 64), ST ? 2 : 1) void map_fo
   constexpr int LPS = 64 / NS;
   const unsigned long long A = p.A;
   const unsigned long long W = (2 + VI) * A;
-  const unsigned long long WS = map_ws(W);  // padded step stride in the ring
+  const unsigned long long WS = RS ? map_ws_rs(W) : map_ws(W);  // padded step stride in the ring
   // LDS: NB image slots (C*WS words each; SH: kShSlot), NB value slots (C*VI), the per-key remove
   // list, the fold-state mirror.  (Addresses are always computed from map_lds: a pointer table
   // would hide the LDS address space and turn every access into a flat op.)  SH: four such wave
@@ -1729,7 +1745,7 @@ __global__ __launch_bounds__(SH ? 256 : (ST ? 128 : 64), ST ? 2 : 1) void map_fo
   } else if constexpr (RS) {  // chunks 0 and 1 into the two slots (W <= 128: one piece per step)
     gl1 = glds_lanes<VI, 1>(p, g, k, lane);
     for (unsigned long long c = 0; c < 2 && c < nch; ++c)
-      map_chunk_glds<VI, C, 1>(p, gl1, g, k, c * C, R, wl + c * SLOT, WS, vbase + c * C * VI, cml + c * A, lane,
+      map_chunk_glds<VI, C, 1, (MAP_RS_NT ? 2 : 0)>(p, gl1, g, k, c * C, R, wl + c * SLOT, WS, vbase + c * C * VI, cml + c * A, lane,
                                vpiece, p.diag);
   }
   if constexpr (GL) {
@@ -1835,7 +1851,7 @@ __global__ __launch_bounds__(SH ? 256 : (ST ? 128 : 64), ST ? 2 : 1) void map_fo
         if (ch + 2 < nch && !spread) st_chunk_glds(p, gl1, g, ch + 2, R, img, WS, cms, lane, 0);
       } else {
         if (ch + 2 < nch && !spread)
-          map_chunk_glds<VI, C, 1>(p, gl1, g, k, i2, R, img, WS, vsl, cms, lane, vpiece, p.diag);
+          map_chunk_glds<VI, C, 1, (MAP_RS_NT ? 2 : 0)>(p, gl1, g, k, i2, R, img, WS, vsl, cms, lane, vpiece, p.diag);
       }
       MAP_TOCK(cy_issue);
       // advance the ring bookkeeping (the rest of the iteration uses sh_use only through shs / cms)
@@ -2298,7 +2314,7 @@ __global__ __launch_bounds__(SH ? 256 : (ST ? 128 : 64), ST ? 2 : 1) void map_fo
         st_chunk_glds(p, gl1, g, ch + 2, R, wl + slot * SLOT, WS, cml + slot * CMS, lane, 0);
       } else if (ch + 2 < nch) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        map_chunk_glds<VI, C, 1>(p, gl1, g, k, (ch + 2) * C, R, wl + slot * SLOT, WS, vbase + slot * C * VI,
+        map_chunk_glds<VI, C, 1, (MAP_RS_NT ? 2 : 0)>(p, gl1, g, k, (ch + 2) * C, R, wl + slot * SLOT, WS, vbase + slot * C * VI,
                                  cml + slot * CMS, lane, vpiece, p.diag);
       }
     }
@@ -2391,7 +2407,7 @@ static hipError_t launch_map_it(const MapPlan &p, unsigned long long blocks, hip
   constexpr int C = (GL || RS) ? CM : MapChunk<APL, VI, CM>::C;
   const size_t W = (2 + VI) * p.A;
   // (the kernel's PW: slots, values, remove lists, mirror, clock-max copies, thresholds, ST words)
-  const size_t lds = (size_t)NB * C * (map_ws(W) + VI) * sizeof(u64) + kMapL * 2 * sizeof(unsigned) +
+  const size_t lds = (size_t)NB * C * ((RS ? map_ws_rs(W) : map_ws(W)) + VI) * sizeof(u64) + kMapL * 2 * sizeof(unsigned) +
                      (2 + VO) * p.A * sizeof(u64) + ((GL || RS) ? (ST ? 2 : 1) * NB * p.A * sizeof(u64) : 0) +
                      4 * p.A * sizeof(u64) + (ST ? 4 * sizeof(u64) : 0);
   if (lds > 160 * 1024) return hipErrorInvalidValue;

@@ -99,7 +99,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APL <= 2 ? 
     if (lane == 0) p.status[s] = (dcnt > Dcap ? 4u : 0u) | (oe < ob || oe > p.n_ops ? 8u : 0u);
     return;  // state left untouched
   }
-  unsigned st = 0;
+  unsigned st = 0, peak = dcnt;  // peak: the most slots this call has held (vacated ones are zeroed)
   u64 *C = p.clock + s * p.c_s, *E = p.ec + s * p.e_s, *V = p.val + s * p.v_s;
   auto word = [&](int j) { return (unsigned long long)lane + 64ull * j; };
   u64 c[APL];
@@ -253,6 +253,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APL <= 2 ? 
           continue;
         }
         slot = (int)dcnt++;
+        peak = dcnt > peak ? dcnt : peak;
 #pragma unroll
         for (int j = 0; j < APL; ++j)
           if (word(j) < A) set_clk(slot, word(j), r[j]);
@@ -274,6 +275,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APL <= 2 ? 
   for (unsigned d = 0; d < dcnt && d < Dl; ++d) {  // (slots past Dl are already in place)
     for (unsigned long long a = (unsigned long long)lane; a < A; a += kWave) gclk[d * A + a] = sclk[d * A + a];
     for (unsigned long long w = (unsigned long long)lane; w < Kw; w += kWave) gkey[d * Kw + w] = skey[d * Kw + w];
+  }
+  for (unsigned d = dcnt; d < peak; ++d) {  // slots the deferred list vacated: zero, as a fresh state's
+    for (unsigned long long a = (unsigned long long)lane; a < A; a += kWave) gclk[d * A + a] = 0ull;
+    for (unsigned long long w = (unsigned long long)lane; w < Kw; w += kWave) gkey[d * Kw + w] = 0ull;
   }
   if (lane == 0) {
     p.def_count[s] = dcnt;

@@ -80,7 +80,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APL <= 2 ? 
     if (lane == 0) p.status[s] = (dcnt > Dcap ? 4u : 0u) | (oe < ob || oe > p.n_ops ? 8u : 0u);
     return;  // state left untouched
   }
-  unsigned st = 0;
+  unsigned st = 0, peak = dcnt;  // peak: the most slots this call has held (vacated ones are zeroed)
   auto word = [&](int j) { return (unsigned long long)lane + 64ull * j; };
   u64 *gclk = p.def_clock + s * Dcap * A, *gkey = p.def_keys + s * Dcap * Kw;
   // (d is wave-uniform: one branch per access, each side keeps its own address space — no flat ops)
@@ -419,6 +419,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APL <= 2 ? 
           continue;
         }
         slot = (int)dcnt++;
+        peak = dcnt > peak ? dcnt : peak;
 #pragma unroll
         for (int j = 0; j < APL; ++j)
           if (word(j) < A) set_clk(slot, word(j), r[j]);
@@ -439,6 +440,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APL <= 2 ? 
   for (unsigned d = 0; d < dcnt && d < Dl; ++d) {  // (slots past Dl are already in place)
     for (unsigned long long a = (unsigned long long)lane; a < A; a += kWave) gclk[d * A + a] = sclk[d * A + a];
     for (unsigned long long w = (unsigned long long)lane; w < Kw; w += kWave) gkey[d * Kw + w] = skey[d * Kw + w];
+  }
+  for (unsigned d = dcnt; d < peak; ++d) {  // slots the deferred list vacated: zero, as a fresh state's
+    for (unsigned long long a = (unsigned long long)lane; a < A; a += kWave) gclk[d * A + a] = 0ull;
+    for (unsigned long long w = (unsigned long long)lane; w < Kw; w += kWave) gkey[d * Kw + w] = 0ull;
   }
   if (lane == 0) {
     p.def_count[s] = dcnt;

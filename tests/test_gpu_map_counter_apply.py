@@ -241,3 +241,34 @@ def test_map_counter_apply_long_deferred_list(gpu_ctx, W):
             assert O.dense_to_map_counter(c[n], e[n], v[n], dfr) == exp, n
             longest = max(longest, len(exp.deferred))
         assert 20 <= longest <= 48
+
+
+def test_map_counter_apply_vacated_slots_zeroed(gpu_ctx):
+    """A deferred list that grows past the 16 LDS slots and then empties (a last Up on actor 0 from
+    and actor 1 from past every remove's clock dominate them all): count 0, every slot written back zero (the form
+    the wire ingest produces), state equal to the oracle's Map.apply."""
+    N, K, A, T, W, Dcap = 6, 6, 5, 64, 2, 48
+    maps = O.map_counter_objects(N, K, A, W, seed=45, steps=0)
+    d = O.map_counter_to_dense(maps, K, A, W)
+    rng = np.random.default_rng(9)
+    streams, oracle_ops = _future_rm_streams(rng, maps, K, A, W, T)
+    for s, oo in zip(streams, oracle_ops):
+        for a in (1, 0):  # (the removes' clocks name actors 0 and 1 only)
+            s.append(("up", a, 1 << 20, 0, 1, 1, 0))
+            oo.append(O.MapUp(O.Dot(a, 1 << 20), 0, (O.Dot(1, 1), O.PNCounter.POS)))
+    Kw = (K + 63) // 64
+    clock, ec, val = to_dev(d["clock"]), to_dev(d["ec"]), to_dev(d["val"])
+    tdc, tdk = to_dev(np.zeros((N, Dcap, A), np.uint64)), to_dev(np.zeros((N, Dcap, Kw), np.uint64))
+    tcnt = torch.zeros(N, dtype=torch.int32, device="cuda:0")
+    ops = cg.map.encode_counter_ops(streams, A, "cuda:0")
+    status = cg.map.counter_apply_batch(clock, ec, val, tdc, tdk, tcnt, ops, ctx=gpu_ctx).cpu().numpy()
+    assert (status == 0).all(), status
+    assert (tcnt.cpu().numpy() == 0).all()
+    assert not to_host(tdc).any() and not to_host(tdk).any()
+    c, e, v = to_host(clock), to_host(ec), to_host(val)
+    for n in range(N):
+        exp = maps[n].copy()
+        for op in oracle_ops[n]:
+            exp.apply(op)
+        assert not exp.deferred
+        assert O.dense_to_map_counter(c[n], e[n], v[n], []) == exp, n
