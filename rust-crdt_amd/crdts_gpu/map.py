@@ -1183,3 +1183,162 @@ def nested_forget_batch(res: "MapNestedLub", y: torch.Tensor, def_clock: Optiona
     ctx.call("crdt_map_nested_forget_batch", ctypes.byref(st), y.data_ptr(), ys, dp, sp, D,
              keep.data_ptr() if keep is not None else None)
     return keep
+
+
+# ---- Pairwise merge_batch of value-typed Map states (round 6) --------------------------------------
+# self[i].merge(other[i]) for Map<K, GCounter / PNCounter>, Map<K, Orswot<M>> and Map<K, Map<K2, MVReg>>
+# states in their apply layouts (wire.MapCounterFrames / MapOrswotFrames / MapNestedFrames or any
+# object with those fields): each pair is one group of the exact left-fold kernel (Map::new() merged
+# with self, then with other — counter_lub_many / orswot_lub_many / nested_lub_many, R = 2), whose
+# result is written back into self, the surviving Map-level deferred removes compacted into self's
+# slots.  Map::merge from an empty Map reproduces a state whose deferred removes are applied and not
+# dominated by its clock — every state apply, merge, forget or ingest leaves — so the fold of
+# [self, other] is self.merge(other) (map.rs:140-220) on those states.
+def _pair(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    return torch.stack((a, b), dim=1).contiguous()
+
+
+def _pair_pool(me, other, N: int, A: int, Kw: int, what: str):
+    """The two states' Map-level deferred slots as one pool grouped by pair (self's first): host
+    def_off (N+1,), def_row (D,) int32 (0 self, 1 other), def_clock (D, A), def_keys (D, Kw), and
+    the pair index of every row."""
+    dev = me.clock.device
+    masks, rows = [], []
+    for s_, r in ((me, 0), (other, 1)):
+        Dc = s_.def_clock.shape[1]
+        if (tuple(s_.def_clock.shape) != (N, Dc, A) or tuple(s_.def_keys.shape) != (N, Dc, Kw)
+                or tuple(s_.def_count.shape) != (N,) or s_.def_count.dtype not in (torch.int32, torch.uint32)
+                or s_.def_count.device != dev):
+            raise ValueError(f"{what}: deferred slots (N, Dcap, A) / (N, Dcap, Kw) / (N,) int32 expected")
+        cnt = s_.def_count.to(torch.int64)
+        if bool(((cnt < 0) | (cnt > Dc)).any()):
+            raise ValueError(f"{what}: def_count outside [0, Dcap]")
+        masks.append(torch.arange(Dc, device=dev)[None, :] < cnt[:, None])
+        rows.append(torch.full((N, Dc), r, dtype=torch.int32, device=dev))
+    mask = torch.cat(masks, 1)
+    clk = torch.cat((me.def_clock, other.def_clock), 1)[mask].contiguous()
+    keys = torch.cat((me.def_keys, other.def_keys), 1)[mask].contiguous()
+    row = torch.cat(rows, 1)[mask].contiguous()
+    gid = torch.arange(N, device=dev)[:, None].expand_as(mask)[mask]
+    per = mask.sum(1).cpu().numpy()
+    off = np.concatenate([[0], np.cumsum(per)]).astype(np.uint64)
+    return off, row, clk, keys, gid
+
+
+def _store_survivors(me, keep, keys_out, clk, gid, N: int) -> torch.Tensor:
+    """Compact the fold's surviving deferred removes (def_keep, their merged key sets) into self's
+    slots in pool order; status bit 0 where more survive than self's Dcap (the first Dcap kept)."""
+    dev = me.clock.device
+    Dcap = me.def_clock.shape[1]
+    status = torch.zeros(N, dtype=torch.int32, device=dev)
+    me.def_clock.zero_()
+    me.def_keys.zero_()
+    if keep is None or clk.shape[0] == 0:
+        me.def_count.zero_()
+        return status
+    k = keep.bool()
+    g = gid[k]
+    counts = torch.bincount(g, minlength=N)
+    pos = torch.arange(g.numel(), device=dev) - (torch.cumsum(counts, 0) - counts)[g]
+    fit = pos < Dcap
+    me.def_clock[g[fit], pos[fit]] = clk[k][fit]
+    me.def_keys[g[fit], pos[fit]] = keys_out[k][fit]
+    me.def_count.copy_(torch.clamp(counts, max=Dcap).to(me.def_count.dtype))
+    status |= (counts > Dcap).to(torch.int32)
+    return status
+
+
+def _same_shapes(me, other, fields, what):
+    for nm in fields:
+        a, b = getattr(me, nm), getattr(other, nm)
+        if tuple(a.shape) != tuple(b.shape) or a.device != b.device:
+            raise ValueError(f"{what}: self.{nm} {tuple(a.shape)} and other.{nm} {tuple(b.shape)} differ")
+        if not a.is_contiguous():
+            raise ValueError(f"{what}: self.{nm} must be contiguous")
+
+
+def counter_merge_batch(me, other, ctx: Optional[Context] = None) -> torch.Tensor:
+    """self[i].merge(other[i]) for N Map<K, GCounter / PNCounter> states, in place on `me` (Map::merge
+    map.rs:140-220 with gcounter.rs:44-54 / pncounter.rs:70-82 as the value's merge and forget):
+    clock (N, A), ec (N, K, A), val (N, K, W, A), def_clock (N, Dcap, A), def_keys (N, Dcap, Kw),
+    def_count (N,) int32 — the crdt_map_counter_states layout.  Returns status (N,) int32: bit 0 =
+    more surviving deferred removes than self's Dcap (the first Dcap kept)."""
+    what = "map.counter_merge_batch"
+    _same_shapes(me, other, ("clock", "ec", "val"), what)
+    ctx = ctx or Context.default(me.clock.device.index)
+    N, A = me.clock.shape
+    K = me.ec.shape[1]
+    if N == 0:
+        return torch.zeros(0, dtype=torch.int32, device=me.clock.device)
+    off, row, clk, keys, gid = _pair_pool(me, other, N, A, (K + 63) // 64, what)
+    dk = dict(def_off=off, def_row=row, def_clock=clk, def_keys=keys) if clk.shape[0] else {}
+    res = counter_lub_many(_pair(me.clock, other.clock), _pair(me.ec, other.ec), _pair(me.val, other.val),
+                           ctx=ctx, **dk)
+    me.clock.copy_(res.clock)
+    me.ec.copy_(res.ec)
+    me.val.copy_(res.val)
+    return _store_survivors(me, res.def_keep, res.def_keys, clk, gid, N)
+
+
+def _pair_csr(n_a, n_b, c_a, c_b, x_a, x_b, cap: int, what: str):
+    """Two states' per-key slot lists (counts (N, K), slots (N, K, cap, ...)) as one device CSR over
+    (pair, replica, key): off (N*2*K + 1,) int64, rows of c and x."""
+    n = _pair(n_a, n_b).to(torch.int64)
+    if bool(((n < 0) | (n > cap)).any()):
+        raise ValueError(f"{what}: nested deferred counts outside [0, {cap}]")
+    mask = torch.arange(cap, device=n.device) < n[..., None]
+    off = torch.zeros(n.numel() + 1, dtype=torch.int64, device=n.device)
+    off[1:] = torch.cumsum(n.flatten(), 0)
+    return off, _pair(c_a, c_b)[mask].contiguous(), _pair(x_a, x_b)[mask].contiguous()
+
+
+def orswot_merge_batch(me, other, ctx: Optional[Context] = None) -> torch.Tensor:
+    """self[i].merge(other[i]) for N Map<K, Orswot<M>> states, in place on `me` (Map::merge
+    map.rs:140-220 with Orswot::merge orswot.rs:81-149 and forget :150-183): the crdt_map_orswot_states
+    layout (clock, ec, oc, ent, vd_n, vd_clock, vd_mem) + the Map's deferred slots def_clock /
+    def_keys / def_count.  Returns status (N,) int32 as counter_merge_batch; a fold limit (more than
+    16 nested deferred removes on a key, more than 256 live Map removes naming one key) raises."""
+    what = "map.orswot_merge_batch"
+    _same_shapes(me, other, ("clock", "ec", "oc", "ent", "vd_n", "vd_clock", "vd_mem"), what)
+    ctx = ctx or Context.default(me.clock.device.index)
+    N, A = me.clock.shape
+    K = me.ec.shape[1]
+    if N == 0:
+        return torch.zeros(0, dtype=torch.int32, device=me.clock.device)
+    off, row, clk, keys, gid = _pair_pool(me, other, N, A, (K + 63) // 64, what)
+    vd_off, vclk, vmem = _pair_csr(me.vd_n, other.vd_n, me.vd_clock, other.vd_clock, me.vd_mem, other.vd_mem,
+                                   VD_CAP, what)
+    vk = dict(vd_clock=vclk, vd_mem=vmem) if vclk.shape[0] else {}
+    dk = dict(def_off=off, def_row=row, def_clock=clk, def_keys=keys) if clk.shape[0] else {}
+    res = orswot_lub_many(_pair(me.clock, other.clock), _pair(me.ec, other.ec), _pair(me.oc, other.oc),
+                          _pair(me.ent, other.ent), vd_off, ctx=ctx, **vk, **dk)
+    for nm in ("clock", "ec", "oc", "ent", "vd_n", "vd_clock", "vd_mem"):
+        getattr(me, nm).copy_(getattr(res, nm).reshape(getattr(me, nm).shape))
+    return _store_survivors(me, res.def_keep, res.def_keys, clk, gid, N)
+
+
+def nested_merge_batch(me, other, ctx: Optional[Context] = None) -> torch.Tensor:
+    """self[i].merge(other[i]) for N Map<K, Map<K2, MVReg<u64>>> states, in place on `me` (Map::merge
+    map.rs:140-220 at both levels, MVReg::merge mvreg.rs:112-128): the crdt_map_nested_states layout
+    (clock, ec, ic, iec, ivc, ivv, nval, id_n, id_clock, id_keys) + the outer deferred slots def_clock /
+    def_keys / def_count.  Returns status (N,) int32 as counter_merge_batch; a fold limit (more than 8
+    values on an inner key, 16 inner deferred removes on a key, 256 live outer removes naming one
+    key) raises."""
+    what = "map.nested_merge_batch"
+    _same_shapes(me, other, ("clock", "ec", "ic", "iec", "ivc", "ivv", "nval", "id_n", "id_clock", "id_keys"), what)
+    ctx = ctx or Context.default(me.clock.device.index)
+    N, A = me.clock.shape
+    K = me.ec.shape[1]
+    if N == 0:
+        return torch.zeros(0, dtype=torch.int32, device=me.clock.device)
+    off, row, clk, keys, gid = _pair_pool(me, other, N, A, (K + 63) // 64, what)
+    id_off, iclk, ikeys = _pair_csr(me.id_n, other.id_n, me.id_clock, other.id_clock, me.id_keys, other.id_keys,
+                                    NM_ID, what)
+    ik = dict(id_clock=iclk, id_keys=ikeys) if iclk.shape[0] else {}
+    dk = dict(def_off=off, def_row=row, def_clock=clk, def_keys=keys) if clk.shape[0] else {}
+    res = nested_lub_many(_pair(me.clock, other.clock), _pair(me.ec, other.ec), _pair(me.ic, other.ic),
+                          _pair(me.iec, other.iec), _pair(me.ivc, other.ivc), _pair(me.ivv, other.ivv), id_off,
+                          ctx=ctx, **ik, **dk)
+    for nm in ("clock", "ec", "ic", "iec", "ivc", "ivv", "nval", "id_n", "id_clock", "id_keys"):
+        getattr(me, nm).copy_(getattr(res, nm).reshape(getattr(me, nm).shape))
+    return _store_survivors(me, res.def_keep, res.def_keys, clk, gid, N)
