@@ -57,49 +57,75 @@ struct MapCounterApplyPlan {
   unsigned long long n_keys, n_ops;
   unsigned *status;
   unsigned wpb;  // waves per block
+  u64 *resume;   // [N] (Dcap > Dl): op offset where the state's stream continues in the tier-2 pass, or kMcaDone
 };
+constexpr u64 kMcaDone = ~0ull;
 
 __device__ __forceinline__ unsigned rl32(unsigned x, int i) { return (unsigned)__builtin_amdgcn_readlane((int)x, i); }
 __device__ __forceinline__ u64 rl64(u64 x, int i) {
   return ((u64)rl32((unsigned)(x >> 32), i) << 32) | rl32((unsigned)x, i);
 }
 
-template <int APL>
+// TIER false: every state, its deferred list in the Dl LDS slots only; a state whose list needs slot
+// Dl (Dcap > Dl) stores itself and records the op to continue from (resume[s]).  TIER true: those
+// states alone, the list's slots past Dl used in place in the caller's slot arrays (one branch per
+// access).  Two passes rather than one body with the branch: that body compiles the slot accesses to
+// flat instructions and cost every state ~40% (2.73 vs 1.90 ms at the bench shape).
+template <int APL, int PASS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APL <= 2 ? CRDT_MCA_WPE : 1))) void map_counter_apply_kernel(MapCounterApplyPlan p) {
   extern __shared__ u64 lds[];
   const int lane = (int)(threadIdx.x % kWave), wv = (int)(threadIdx.x / kWave);
   const unsigned long long s = (unsigned long long)blockIdx.x * p.wpb + wv;
   if (wv >= (int)p.wpb || s >= p.N) return;  // (whole waves)
+  constexpr bool TIER = PASS == 2;
+  if constexpr (TIER) {
+    if (p.resume[s] == kMcaDone) return;
+  }
   const unsigned long long A = p.A, K = p.K, W = p.W, Kw = p.Kw, Dcap = p.Dcap, Dl = p.Dl;
   // The Map's deferred removes: slots d < Dl in LDS, slots Dl <= d < Dcap in the caller's own slot
   // arrays (global memory: a long list runs slower, never incomplete below Dcap)
   u64 *sclk = lds + (unsigned long long)wv * Dl * (A + Kw);  // [Dl][A] rm clocks
   u64 *skey = sclk + Dl * A;                                 // [Dl][Kw] key bitmaps
   u64 *gclk = p.def_clock + s * Dcap * A, *gkey = p.def_keys + s * Dcap * Kw;
-  // (d is wave-uniform: one branch per access, each side keeps its own address space — no flat ops)
+  // (d is wave-uniform; the pass-1 body never reaches d >= Dl)
   auto clk = [&](unsigned d, unsigned long long a) -> u64 {
-    if (d < Dl) return sclk[d * A + a];
-    return gclk[d * A + a];
+    if (TIER && d >= Dl) return gclk[d * A + a];
+    return sclk[d * A + a];
   };
   auto set_clk = [&](unsigned d, unsigned long long a, u64 v) {
-    if (d < Dl) sclk[d * A + a] = v;
-    else gclk[d * A + a] = v;
+    if (TIER && d >= Dl) gclk[d * A + a] = v;
+    else sclk[d * A + a] = v;
   };
   auto key = [&](unsigned d, unsigned long long w) -> u64 {
-    if (d < Dl) return skey[d * Kw + w];
-    return gkey[d * Kw + w];
+    if (TIER && d >= Dl) return gkey[d * Kw + w];
+    return skey[d * Kw + w];
   };
   auto set_key = [&](unsigned d, unsigned long long w, u64 v) {
-    if (d < Dl) skey[d * Kw + w] = v;
-    else gkey[d * Kw + w] = v;
+    if (TIER && d >= Dl) gkey[d * Kw + w] = v;
+    else skey[d * Kw + w] = v;
   };
   const unsigned long long ob = p.op_off[s], oe = p.op_off[s + 1];
   unsigned dcnt = p.def_count[s];
   if (dcnt > Dcap || oe < ob || oe > p.n_ops) {
-    if (lane == 0) p.status[s] = (dcnt > Dcap ? 4u : 0u) | (oe < ob || oe > p.n_ops ? 8u : 0u);
+    if (lane == 0) {
+      p.status[s] = (dcnt > Dcap ? 4u : 0u) | (oe < ob || oe > p.n_ops ? 8u : 0u);
+      if (PASS == 1) p.resume[s] = kMcaDone;
+    }
     return;  // state left untouched
   }
-  unsigned st = 0, peak = dcnt;  // peak: the most slots this call has held (vacated ones are zeroed)
+  if constexpr (PASS == 1) {
+    if (dcnt > Dl) {  // arrives with more removes than the LDS slots: the whole stream in pass 2
+      if (lane == 0) {
+        p.status[s] = 0;
+        p.resume[s] = 0;
+      }
+      return;
+    }
+  }
+  // pass 2 continues with pass 1's status bits and from a state whose first deferred pass is not known
+  // to have run (full = true below re-forgets every listed key: exact either way)
+  unsigned st = TIER ? p.status[s] : 0u, peak = dcnt;  // peak: the most slots held (vacated ones are zeroed)
+  const unsigned long long start = TIER ? ob + p.resume[s] : ob;
   u64 *C = p.clock + s * p.c_s, *E = p.ec + s * p.e_s, *V = p.val + s * p.v_s;
   auto word = [&](int j) { return (unsigned long long)lane + 64ull * j; };
   u64 c[APL];
@@ -187,9 +213,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APL <= 2 ? 
     full = false;
   };
 
+  // pass 1: the op where pass 2 continues (offset within the state's stream; < 2^32, checked on the host)
+  unsigned resume_at = 0xffffffffu;
   // Op headers in batches of 64: lane i loads op o0 + i's fields (coalesced, all in flight
   // together) and op o's fields reach the wave by v_readlane, not by a global round trip per op.
-  for (unsigned long long o0 = ob; o0 < oe; o0 += kWave) {
+  for (unsigned long long o0 = start; o0 < oe; o0 += kWave) {
     const unsigned long long mo = o0 + (unsigned long long)lane;
     const bool hin = CRDT_MCA_HDR && mo < oe;
     const unsigned h_kind = hin ? p.kind[mo] : 0u;
@@ -248,12 +276,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APL <= 2 ? 
         if (!__ballot(ne)) slot = (int)d;
       }
       if (slot < 0) {
+        if constexpr (PASS == 1) {
+          if (dcnt >= Dl) {  // the list outgrows the LDS slots: pass 2 from this op
+            resume_at = (unsigned)(o - ob);
+            goto done;
+          }
+        }
         if (dcnt >= Dcap) {
           st |= 1u;  // deferred capacity exceeded: the state is incomplete
           continue;
         }
         slot = (int)dcnt++;
-        peak = dcnt > peak ? dcnt : peak;
+        if (TIER) peak = dcnt > peak ? dcnt : peak;  // (pass 1: never past the input count's slots in memory)
 #pragma unroll
         for (int j = 0; j < APL; ++j)
           if (word(j) < A) set_clk(slot, word(j), r[j]);
@@ -269,6 +303,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APL <= 2 ? 
     }
   }
   }
+done:
+  // the state back to memory: clock, the LDS slots, the count and status (and, at a pass-1 exit, the
+  // op to continue from)
 #pragma unroll
   for (int j = 0; j < APL; ++j)
     if (word(j) < A) C[word(j)] = c[j];
@@ -276,13 +313,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APL <= 2 ? 
     for (unsigned long long a = (unsigned long long)lane; a < A; a += kWave) gclk[d * A + a] = sclk[d * A + a];
     for (unsigned long long w = (unsigned long long)lane; w < Kw; w += kWave) gkey[d * Kw + w] = skey[d * Kw + w];
   }
-  for (unsigned d = dcnt; d < peak; ++d) {  // slots the deferred list vacated: zero, as a fresh state's
+  // slots the deferred list vacated, zeroed as a fresh state's: pass 1 wrote none past its final count
+  // to memory, so only the input's [dcnt, def_count[s]) can be stale there; pass 2 tracks its peak
+  const unsigned hi = TIER ? peak : p.def_count[s];
+  for (unsigned d = dcnt; d < hi; ++d) {
     for (unsigned long long a = (unsigned long long)lane; a < A; a += kWave) gclk[d * A + a] = 0ull;
     for (unsigned long long w = (unsigned long long)lane; w < Kw; w += kWave) gkey[d * Kw + w] = 0ull;
   }
   if (lane == 0) {
     p.def_count[s] = dcnt;
     p.status[s] = st;
+    if (PASS == 1) p.resume[s] = resume_at == 0xffffffffu ? kMcaDone : resume_at;
   }
 }
 
@@ -319,20 +360,44 @@ extern "C" int crdt_map_counter_apply_batch(crdt_ctx *ctx, const crdt_map_counte
                         (const u64 *)ops->op_off, ops->kind, ops->actor, ops->key, ops->vactor,
                         (const u64 *)ops->counter, (const u64 *)ops->vcounter, ops->vdir, ops->clk_row,
                         (const u64 *)ops->clk_pool, ops->clk_pool ? ops->n_clk_rows : 0,
-                        (const u64 *)ops->key_off, ops->keys, ops->keys ? ops->n_keys : 0, ops->n_ops, status, wpb};
-  // an Rm op needs key_off (n_ops + 1 entries); without it every Rm reads an empty key range
-  if (!ops->key_off) {
-    if (int rc = ensure_scratch(ctx, (ops->n_ops + 1) * 8)) return rc;
-    if (int rc = device_fill(ctx, ctx->scratch, (ops->n_ops + 1) * 8, 0)) return rc;
-    p.key_off = static_cast<const u64 *>(ctx->scratch);
+                        (const u64 *)ops->key_off, ops->keys, ops->keys ? ops->n_keys : 0, ops->n_ops, status, wpb,
+                        nullptr};
+  // an Rm op needs key_off (n_ops + 1 entries); without it every Rm reads an empty key range.  Scratch:
+  // [resume: N words when Dcap > Dl][zero key_off: n_ops + 1 words when absent]
+  const bool tier = Dcap > Dl;
+  const size_t kz = ops->key_off ? 0 : (ops->n_ops + 1) * 8, rz = tier ? N * 8 : 0;
+  if (kz + rz) {
+    if (int rc = ensure_scratch(ctx, kz + rz)) return rc;
+    char *sc = static_cast<char *>(ctx->scratch);
+    if (tier) p.resume = reinterpret_cast<u64 *>(sc);
+    if (kz) {
+      if (int rc = device_fill(ctx, sc + rz, kz, 0)) return rc;
+      p.key_off = reinterpret_cast<const u64 *>(sc + rz);
+    }
   }
+  if (Dcap > Dl && ops->n_ops >= 0xffffffffull)  // (pass 2 resumes at a 32-bit op offset)
+    return fail(ctx, CRDT_EUNSUPPORTED, "map_counter_apply_batch: 2^32 or more ops with Dcap past the LDS slots");
   const dim3 grid((unsigned)((N + wpb - 1) / wpb)), block(wpb * kWave);
   const size_t lds = per_wave * wpb;
   timing_begin(ctx, "map_counter_apply");
-  if (A <= 64) hipLaunchKernelGGL(map_counter_apply_kernel<1>, grid, block, lds, ctx->stream, p);
-  else if (A <= 128) hipLaunchKernelGGL(map_counter_apply_kernel<2>, grid, block, lds, ctx->stream, p);
-  else if (A <= 256) hipLaunchKernelGGL(map_counter_apply_kernel<4>, grid, block, lds, ctx->stream, p);
-  else hipLaunchKernelGGL(map_counter_apply_kernel<8>, grid, block, lds, ctx->stream, p);
+  auto go = [&](auto t, dim3 g, dim3 b, size_t l) {
+    constexpr int T = decltype(t)::value;
+    if (A <= 64) hipLaunchKernelGGL((map_counter_apply_kernel<1, T>), g, b, l, ctx->stream, p);
+    else if (A <= 128) hipLaunchKernelGGL((map_counter_apply_kernel<2, T>), g, b, l, ctx->stream, p);
+    else if (A <= 256) hipLaunchKernelGGL((map_counter_apply_kernel<4, T>), g, b, l, ctx->stream, p);
+    else hipLaunchKernelGGL((map_counter_apply_kernel<8, T>), g, b, l, ctx->stream, p);
+  };
+  if (Dcap <= Dl) {
+    go(std::integral_constant<int, 0>{}, grid, block, lds);  // one pass: the whole list fits the LDS slots
+  } else {
+    go(std::integral_constant<int, 1>{}, grid, block, lds);
+    // pass 2: the few states pass 1 handed on (the rest exit at once), one wave per workgroup with the
+    // whole wave-LDS budget as slots (up to 64 KiB), so a long list mostly stays out of global memory
+    const size_t Dl2 = std::min<size_t>(Dcap, 8192 / (A + Kw));
+    p.Dl = Dl2;
+    p.wpb = 1;
+    go(std::integral_constant<int, 2>{}, dim3((unsigned)N), dim3(kWave), Dl2 * (A + Kw) * 8);
+  }
   timing_end(ctx);
   CRDT_HIP(ctx, hipGetLastError());
   return CRDT_OK;

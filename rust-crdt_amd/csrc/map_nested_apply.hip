@@ -48,19 +48,23 @@ struct NestedApplyPlan {
   unsigned long long n_keys, n_ops;
   unsigned *status;
   unsigned wpb;
+  u64 *resume = nullptr;  // [N] (Dcap > Dl): op offset where a state continues in pass 2, or kMnaDone
   const u64 *y;  // forget
   unsigned long long y_stride;
 };
+constexpr u64 kMnaDone = ~0ull;
 
 // The rows of outer key k of state s, and the inner-Map operations on them.
 // op headers batched 64 at a time into lanes and read by v_readlane (build option; 0 = one global
 // read of each field per op)
-// waves per SIMD asked of the register allocator (build option; 0 = the compiler's choice, 4)
+// waves per SIMD asked of the register allocator for A <= 128 (build option).  4 = the round-5 kernel's
+// natural 127 VGPRs; the round-6 pass structure needs 131 unforced, which is 3 waves per SIMD and ran
+// 25% slower (2.09 vs 1.67 ms, profiles/r06_apply_ab.log).  0 = the compiler's choice.
 #ifndef CRDT_MNA_WPE
-#define CRDT_MNA_WPE 0
+#define CRDT_MNA_WPE 4
 #endif
 #if CRDT_MNA_WPE > 0
-#define MNA_WPE_ATTR __attribute__((amdgpu_waves_per_eu(CRDT_MNA_WPE)))
+#define MNA_WPE_ATTR __attribute__((amdgpu_waves_per_eu(APL <= 2 ? CRDT_MNA_WPE : 1)))
 #else
 #define MNA_WPE_ATTR
 #endif
@@ -353,42 +357,67 @@ __device__ __forceinline__ NaKey<APL> na_key(const NestedApplyPlan &p, unsigned 
                     p.nval + sk * K2, p.id_n + sk, A, K2, lane, 0u};
 }
 
-template <int APL>
+// TIER false: every state, the Map's deferred list in the Dl LDS slots only; a state whose list
+// needs slot Dl (Dcap > Dl) stores itself and records the op to continue from (resume[s]).  TIER
+// true: those states alone, slots past Dl used in place in the caller's slot arrays.  (One body with
+// the branch compiles the slot accesses to flat instructions and slows every state; see
+// csrc/map_counter_apply.hip.)
+template <int APL, int PASS>
 __global__ __launch_bounds__(256) MNA_WPE_ATTR void map_nested_apply_kernel(NestedApplyPlan p) {
   extern __shared__ u64 lds[];
   const int lane = (int)(threadIdx.x % kWave), wv = (int)(threadIdx.x / kWave);
   const unsigned long long s = (unsigned long long)blockIdx.x * p.wpb + wv;
   if (wv >= (int)p.wpb || s >= p.N) return;  // (whole waves)
+  constexpr bool TIER = PASS == 2;
+  if constexpr (TIER) {
+    if (p.resume[s] == kMnaDone) return;
+  }
   const unsigned long long A = p.A, K = p.K, K2 = p.K2, Kw = p.Kw, Dcap = p.Dcap, Dl = p.Dl;
   // The outer deferred removes: slots d < Dl in LDS, slots Dl <= d < Dcap in the caller's own slot
   // arrays (global memory: a long list runs slower, never incomplete below Dcap)
   u64 *sclk = lds + (unsigned long long)wv * Dl * (A + Kw);  // [Dl][A] the outer rm clocks
   u64 *skey = sclk + Dl * A;                                 // [Dl][Kw] their key bitmaps
   u64 *gclk = p.def_clock + s * Dcap * A, *gkey = p.def_keys + s * Dcap * Kw;
-  // (d is wave-uniform: one branch per access, each side keeps its own address space — no flat ops)
+  // (d is wave-uniform; the pass-1 body never reaches d >= Dl)
   auto clk = [&](unsigned d, unsigned long long a) -> u64 {
-    if (d < Dl) return sclk[d * A + a];
-    return gclk[d * A + a];
+    if (TIER && d >= Dl) return gclk[d * A + a];
+    return sclk[d * A + a];
   };
   auto set_clk = [&](unsigned d, unsigned long long a, u64 v) {
-    if (d < Dl) sclk[d * A + a] = v;
-    else gclk[d * A + a] = v;
+    if (TIER && d >= Dl) gclk[d * A + a] = v;
+    else sclk[d * A + a] = v;
   };
   auto key = [&](unsigned d, unsigned long long w) -> u64 {
-    if (d < Dl) return skey[d * Kw + w];
-    return gkey[d * Kw + w];
+    if (TIER && d >= Dl) return gkey[d * Kw + w];
+    return skey[d * Kw + w];
   };
   auto set_key = [&](unsigned d, unsigned long long w, u64 v) {
-    if (d < Dl) skey[d * Kw + w] = v;
-    else gkey[d * Kw + w] = v;
+    if (TIER && d >= Dl) gkey[d * Kw + w] = v;
+    else skey[d * Kw + w] = v;
   };
   const unsigned long long ob = p.op_off[s], oe = p.op_off[s + 1];
   unsigned dcnt = p.def_count[s];
   if (dcnt > Dcap || oe < ob || oe > p.n_ops) {
-    if (lane == 0) p.status[s] = (dcnt > Dcap ? 4u : 0u) | (oe < ob || oe > p.n_ops ? 8u : 0u);
+    if (lane == 0) {
+      p.status[s] = (dcnt > Dcap ? 4u : 0u) | (oe < ob || oe > p.n_ops ? 8u : 0u);
+      if (PASS == 1) p.resume[s] = kMnaDone;
+    }
     return;  // state left untouched
   }
-  unsigned st = 0, peak = dcnt;  // peak: the most slots this call has held (vacated ones are zeroed)
+  if constexpr (PASS == 1) {
+    if (dcnt > Dl) {  // arrives with more removes than the LDS slots: the whole stream in pass 2
+      if (lane == 0) {
+        p.status[s] = 0;
+        p.resume[s] = 0;
+      }
+      return;
+    }
+  }
+  // pass 2 continues with pass 1's status bits; its first deferred pass is full (exact either way)
+  unsigned st = TIER ? p.status[s] : 0u, peak = dcnt;  // peak: the most slots held (vacated ones are zeroed)
+  const unsigned long long start = TIER ? ob + p.resume[s] : ob;
+  // pass 1: the op where pass 2 continues (offset within the state's stream; < 2^32, checked on the host)
+  unsigned resume_at = 0xffffffffu;
   auto word = [&](int j) { return (unsigned long long)lane + 64ull * j; };
   u64 *C = p.clock + s * A;
   u64 c[APL];
@@ -432,7 +461,7 @@ __global__ __launch_bounds__(256) MNA_WPE_ATTR void map_nested_apply_kernel(Nest
 
   // Op headers in batches of 64 (CRDT_MNA_HDR): lane i loads op o0 + i's fields (coalesced, all in
   // flight together) and op o's fields reach the wave by v_readlane, not by a global round trip per op.
-  for (unsigned long long o0 = ob; o0 < oe; o0 += kWave) {
+  for (unsigned long long o0 = start; o0 < oe; o0 += kWave) {
     const unsigned long long mo = o0 + (unsigned long long)lane;
     const bool hin = CRDT_MNA_HDR && mo < oe;
     const unsigned h_kind = hin ? p.kind[mo] : 0u, h_ik = hin ? p.ikind[mo] : 0u, h_a = hin ? p.actor[mo] : 0u;
@@ -497,12 +526,18 @@ __global__ __launch_bounds__(256) MNA_WPE_ATTR void map_nested_apply_kernel(Nest
         if (!__ballot(ne)) slot = (int)d;
       }
       if (slot < 0) {
+        if constexpr (PASS == 1) {
+          if (dcnt >= Dl) {  // the list outgrows the LDS slots: pass 2 from this op
+            resume_at = (unsigned)(o - ob);
+            goto done;
+          }
+        }
         if (dcnt >= Dcap) {
           st |= 1u;
           continue;
         }
         slot = (int)dcnt++;
-        peak = dcnt > peak ? dcnt : peak;
+        if (TIER) peak = dcnt > peak ? dcnt : peak;  // (pass 1: never past the input count's slots in memory)
 #pragma unroll
         for (int j = 0; j < APL; ++j)
           if (word(j) < A) set_clk(slot, word(j), r[j]);
@@ -517,6 +552,7 @@ __global__ __launch_bounds__(256) MNA_WPE_ATTR void map_nested_apply_kernel(Nest
     }
   }
   }
+done:
 #pragma unroll
   for (int j = 0; j < APL; ++j)
     if (word(j) < A) C[word(j)] = c[j];
@@ -524,13 +560,17 @@ __global__ __launch_bounds__(256) MNA_WPE_ATTR void map_nested_apply_kernel(Nest
     for (unsigned long long a = (unsigned long long)lane; a < A; a += kWave) gclk[d * A + a] = sclk[d * A + a];
     for (unsigned long long w = (unsigned long long)lane; w < Kw; w += kWave) gkey[d * Kw + w] = skey[d * Kw + w];
   }
-  for (unsigned d = dcnt; d < peak; ++d) {  // slots the deferred list vacated: zero, as a fresh state's
+  // slots the deferred list vacated, zeroed as a fresh state's: pass 1 wrote none past its final count
+  // to memory, so only the input's [dcnt, def_count[s]) can be stale there; pass 2 tracks its peak
+  const unsigned hi = TIER ? peak : p.def_count[s];
+  for (unsigned d = dcnt; d < hi; ++d) {
     for (unsigned long long a = (unsigned long long)lane; a < A; a += kWave) gclk[d * A + a] = 0ull;
     for (unsigned long long w = (unsigned long long)lane; w < Kw; w += kWave) gkey[d * Kw + w] = 0ull;
   }
   if (lane == 0) {
     p.def_count[s] = dcnt;
     p.status[s] = st;
+    if (PASS == 1) p.resume[s] = resume_at == 0xffffffffu ? kMnaDone : resume_at;
   }
 }
 
@@ -630,18 +670,40 @@ extern "C" int crdt_map_nested_apply_batch(crdt_ctx *ctx, const crdt_map_nested_
   p.n_ops = ops->n_ops;
   p.status = status;
   p.wpb = wpb;
-  if (!ops->key_off) {  // (no outer Rm: every key range empty)
-    if (int rc = ensure_scratch(ctx, (ops->n_ops + 1) * 8)) return rc;
-    if (int rc = device_fill(ctx, ctx->scratch, (ops->n_ops + 1) * 8, 0)) return rc;
-    p.key_off = static_cast<const u64 *>(ctx->scratch);
+  // scratch: [resume: N words when Dcap > Dl][zero key_off: n_ops + 1 words when there is none]
+  const size_t kz = ops->key_off ? 0 : (ops->n_ops + 1) * 8, rz = Dcap > Dl ? N * 8 : 0;
+  if (kz + rz) {
+    if (int rc = ensure_scratch(ctx, kz + rz)) return rc;
+    char *sc = static_cast<char *>(ctx->scratch);
+    if (rz) p.resume = reinterpret_cast<u64 *>(sc);
+    if (kz) {  // (no Map-level Rm: every key range empty)
+      if (int rc = device_fill(ctx, sc + rz, kz, 0)) return rc;
+      p.key_off = reinterpret_cast<const u64 *>(sc + rz);
+    }
   }
+  if (Dcap > Dl && ops->n_ops >= 0xffffffffull)  // (pass 2 resumes at a 32-bit op offset)
+    return fail(ctx, CRDT_EUNSUPPORTED, "map_nested_apply_batch: 2^32 or more ops with Dcap past the LDS slots");
   const dim3 grid((unsigned)((N + wpb - 1) / wpb)), block(wpb * kWave);
   const size_t lds = per_wave * wpb;
   timing_begin(ctx, "map_nested_apply");
-  if (A <= 64) hipLaunchKernelGGL(map_nested_apply_kernel<1>, grid, block, lds, ctx->stream, p);
-  else if (A <= 128) hipLaunchKernelGGL(map_nested_apply_kernel<2>, grid, block, lds, ctx->stream, p);
-  else if (A <= 256) hipLaunchKernelGGL(map_nested_apply_kernel<4>, grid, block, lds, ctx->stream, p);
-  else hipLaunchKernelGGL(map_nested_apply_kernel<8>, grid, block, lds, ctx->stream, p);
+  auto go = [&](auto t, dim3 g, dim3 b, size_t l) {
+    constexpr int T = decltype(t)::value;
+    if (A <= 64) hipLaunchKernelGGL((map_nested_apply_kernel<1, T>), g, b, l, ctx->stream, p);
+    else if (A <= 128) hipLaunchKernelGGL((map_nested_apply_kernel<2, T>), g, b, l, ctx->stream, p);
+    else if (A <= 256) hipLaunchKernelGGL((map_nested_apply_kernel<4, T>), g, b, l, ctx->stream, p);
+    else hipLaunchKernelGGL((map_nested_apply_kernel<8, T>), g, b, l, ctx->stream, p);
+  };
+  if (Dcap <= Dl) {
+    go(std::integral_constant<int, 0>{}, grid, block, lds);  // one pass: the whole list fits the LDS slots
+  } else {
+    go(std::integral_constant<int, 1>{}, grid, block, lds);
+    // pass 2: the few states pass 1 handed on (the rest exit at once), one wave per workgroup with the
+    // whole wave-LDS budget as slots (up to 64 KiB), so a long list mostly stays out of global memory
+    const size_t Dl2 = std::min<size_t>(Dcap, 8192 / (A + p.Kw));
+    p.Dl = Dl2;
+    p.wpb = 1;
+    go(std::integral_constant<int, 2>{}, dim3((unsigned)N), dim3(kWave), Dl2 * (A + p.Kw) * 8);
+  }
   timing_end(ctx);
   CRDT_HIP(ctx, hipGetLastError());
   return CRDT_OK;
