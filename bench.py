@@ -305,6 +305,32 @@ class Env:
         return t.tolist()
 
 
+def oracle_parity_counters(args, torch, lubs, outs, A):
+    """The oracle's restated GCounter / PNCounter / VClock fold (VClock::merge vclock.rs:130-136 over
+    ordered maps, oracle_counter_fold_mt over the host's threads) on a sample of actors over EVERY
+    replica row of the launch, against the same words of the GPU result (outside the timed region)."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    t0 = time.time()
+    acts = np.sort(np.random.default_rng(args.parity_seed).choice(A, size=min(args.parity_members, A),
+                                                                   replace=False))
+    ok, rows = True, 0
+    for (kind, x, _), o in zip(lubs, outs):
+        pn = kind == "pncounter"
+        cols = np.concatenate([acts, acts + A]) if pn else acts
+        idx = torch.from_numpy(cols.astype(np.int64)).to(x.device)
+        sub = np.ascontiguousarray(x.index_select(1, idx).cpu().numpy().view(np.uint64))
+        exp, _ = O.counter_fold_mt(sub, pn, cpu_threads())
+        got = o.index_select(0, idx).cpu().numpy().view(np.uint64)
+        ok = ok and bool(np.array_equal(exp, got))
+        rows += sub.shape[0]
+    return {"result": "ok" if ok else "MISMATCH",
+            "sample": (f"{len(acts)} actors (seed {args.parity_seed}) x every replica row "
+                       f"({rows} rows over {len(lubs)} lub(s)), oracle_counter_fold_mt on {cpu_threads()} threads"),
+            "seconds": time.time() - t0}
+
+
 def run_workload(args, env, workload):
     """Generate the rank's shard in HBM, warm up, time args.steps steps; return the measured block."""
     torch, cg, cdist = env.torch, env.cg, env.cdist
@@ -379,6 +405,11 @@ def run_workload(args, env, workload):
     if world > 1:
         cdist.allreduce_umax_(ref)
     ok = env.max_over_ranks([0.0 if bool(torch.equal(got, ref)) else 1.0])[0] == 0.0
+    # and (N = 1, rank 0, with the CPU leg) the oracle's restated fold on a sample of actors over
+    # every replica row: the CPU check the c3 / c4 blocks already carry
+    oracle_par = {"result": "unchecked (the oracle leg runs at N = 1 without --no-cpu-baseline)"}
+    if world == 1 and not args.no_cpu_baseline:
+        oracle_par = oracle_parity_counters(args, torch, lubs, outs, A)
 
     merges_per_step = len(lubs) * R * world
     bytes_per_step = sum(R * x.shape[1] * 8 + x.shape[1] * 8 for _, x, _ in lubs)
@@ -433,7 +464,8 @@ def run_workload(args, env, workload):
             "launches": launches,
             "algorithmic_bytes_per_launch": avg_launch_bytes,
         },
-        "parity": "ok" if ok else "MISMATCH",
+        "parity": "ok" if ok and oracle_par["result"] != "MISMATCH" else "MISMATCH",
+        "parity_detail": {"torch_umax": "ok" if ok else "MISMATCH", "oracle": oracle_par},
     }
     if env.cabi:  # where a scaling loss goes: the exchange collectives and the per-call agreement
         block["exchange"] = {
@@ -722,6 +754,7 @@ def main():
             "roofline": head["roofline"],
             "cpu_baseline": None,
             "parity": head["parity"],
+            "parity_detail": head["parity_detail"],
         }
         if "exchange" in head:
             out["exchange"] = head["exchange"]

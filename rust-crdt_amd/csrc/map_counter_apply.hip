@@ -36,6 +36,9 @@ constexpr size_t kMcaDl = 16;
 #ifndef CRDT_MCA_WPE
 #define CRDT_MCA_WPE 7
 #endif
+#ifndef CRDT_MCA_WPE1  // the pass-1 instance (Dcap past the LDS slots): 6, 2.185 vs 2.334 ms at 7
+#define CRDT_MCA_WPE1 6    // (profiles/r06_apply_ab.log)
+#endif
 
 struct MapCounterApplyPlan {
   u64 *clock, *ec, *val;
@@ -72,7 +75,7 @@ __device__ __forceinline__ u64 rl64(u64 x, int i) {
 // access).  Two passes rather than one body with the branch: that body compiles the slot accesses to
 // flat instructions and cost every state ~40% (2.73 vs 1.90 ms at the bench shape).
 template <int APL, int PASS>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APL <= 2 ? CRDT_MCA_WPE : 1))) void map_counter_apply_kernel(MapCounterApplyPlan p) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APL <= 2 ? (PASS == 1 ? CRDT_MCA_WPE1 : CRDT_MCA_WPE) : 1))) void map_counter_apply_kernel(MapCounterApplyPlan p) {
   extern __shared__ u64 lds[];
   const int lane = (int)(threadIdx.x % kWave), wv = (int)(threadIdx.x / kWave);
   const unsigned long long s = (unsigned long long)blockIdx.x * p.wpb + wv;

@@ -27,6 +27,9 @@ namespace crdt {
 #ifndef CRDT_MOA_WPE
 #define CRDT_MOA_WPE 5
 #endif
+#ifndef CRDT_MOA_WPE1  // (the pass-1 instance, Dcap past the LDS slots)
+#define CRDT_MOA_WPE1 CRDT_MOA_WPE
+#endif
 
 constexpr int kMoaVd = 16;    // nested deferred slots per key (crdt_map_orswot_out)
 constexpr int kMoaMw = 16;    // member-mask words (M <= 1,024)
@@ -69,7 +72,7 @@ __device__ __forceinline__ u64 rl64(u64 x, int i) {
 // the branch compiles the slot accesses to flat instructions and slows every state; see
 // csrc/map_counter_apply.hip.)
 template <int APL, int PASS>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APL <= 2 ? CRDT_MOA_WPE : 1))) void map_orswot_apply_kernel(MapOrswotApplyPlan p) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APL <= 2 ? (PASS == 1 ? CRDT_MOA_WPE1 : CRDT_MOA_WPE) : 1))) void map_orswot_apply_kernel(MapOrswotApplyPlan p) {
   extern __shared__ u64 lds[];
   const int lane = (int)(threadIdx.x % kWave), wv = (int)(threadIdx.x / kWave);
   const unsigned long long s = (unsigned long long)blockIdx.x * p.wpb + wv;

@@ -7,7 +7,7 @@ mkdir -p gpurun_out && export TMPDIR=/tmp
 for rep in 1 2; do
   for v in cur ${AB_VARIANTS:-r5ap}; do
     lib=rust-crdt_amd/libcrdt_gpu.so; [ $v != cur ] && lib=rust-crdt_amd/libcrdt_gpu_$v.so
-    CRDT_GPU_LIB=$PWD/$lib timeout -k 10 300 python -u scripts/bench_vmap_ops.py --dcap 16 > gpurun_out/r06_apply_ab_${v}_$rep.log 2>&1 || exit $?
+    CRDT_GPU_LIB=$PWD/$lib timeout -k 10 300 python -u scripts/bench_vmap_ops.py --dcap ${AB_DCAP:-16} > gpurun_out/r06_apply_ab_${v}_$rep.log 2>&1 || exit $?
     echo "$v $rep $(grep -o '"op": "map_[a-z]*_apply_batch[^"]*", "states": [0-9]*, "ops_per_state": [0-9]*, "actors": [0-9]*, "kernel_us": [0-9.]*' gpurun_out/r06_apply_ab_${v}_$rep.log | sed 's/"states.*kernel_us"//' | tr '\n' ' ')"
   done
 done

@@ -11,7 +11,7 @@ for rep in 1 2; do
   timeout -k 10 400 python -u scripts/bench_vmap_ops.py --dcap 64 > gpurun_out/r06_s11_vmap64_$rep.log 2>&1 || exit $?
   grep '^{' gpurun_out/r06_s11_vmap64_$rep.log | grep apply_batch | cut -c1-230
 done
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_r06_vmap64 -o run -- python3 -u scripts/bench_vmap_ops.py --dcap 64 > gpurun_out/prof_r06_vmap64.log 2>&1 || exit $?
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_r06_vmap64 -o run -- python3 -u scripts/bench_vmap_ops.py --dcap 64 > gpurun_out/prof_r06_vmap64.log 2>&1 || exit $?
 python3 - <<'PY'
 import csv, glob
 f = glob.glob("gpurun_out/prof_r06_vmap64/**/*kernel_stats.csv", recursive=True)
@@ -19,4 +19,6 @@ for r in csv.DictReader(open(f[0])):
     if "apply" in r["Name"]:
         print(r["Name"][:90], r["Calls"], r["AverageNs"], r["MaxNs"])
 PY
+timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 > gpurun_out/r06_s11_bench.log 2>&1 || exit $?
+grep -o "\"parity_detail\": {[^}]*}[^}]*}" gpurun_out/r06_s11_bench.log | head -3
 echo "session 11 done"
