@@ -82,6 +82,9 @@ constexpr int kMapQ = 4;    // deferred removes tracked per key in registers bef
 #ifndef MAP_RS_NT
 #define MAP_RS_NT 1
 #endif
+#ifndef MAP_RS_AUX  // the policy bits themselves (2 = nt; 16 = sc1, 18 = sc1 nt: A/B options)
+#define MAP_RS_AUX (MAP_RS_NT ? 2 : 0)
+#endif
 constexpr int kMapL = MAP_RS_WS8 ? 128 : 256;  // removes naming one key listed in LDS (beyond: walk the group list)
 
 template <int APL, int VI>
@@ -1086,7 +1089,7 @@ struct RsDma {
   int diag;  // MapPlan::diag timing probes
   __device__ __forceinline__ void operator()(int j) {
     if (j < 16) {
-      if (!(diag & 2) || j < 13) glds16<MAP_RS_NT ? 2 : 0>(src, img + j * WS);
+      if (!(diag & 2) || j < 13) glds16<MAP_RS_AUX>(src, img + j * WS);
       src += stride;
     } else if (j == 16) {
       if (vp)
@@ -1173,14 +1176,14 @@ __device__ __forceinline__ void st_chunk_glds(const MapPlan &p, const GldsLanes<
     const char *src = L.src0[0] + i0 * L.stride[0];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      glds16<MAP_RS_NT ? 2 : 0>(src, dst + j * WS);
+      glds16<MAP_RS_AUX>(src, dst + j * WS);
       src += L.stride[0];
     }
   } else {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const unsigned long long i = i0 + j < R ? i0 + j : R - 1;
-      glds16<MAP_RS_NT ? 2 : 0>(L.src0[0] + i * L.stride[0], dst + j * WS);
+      glds16<MAP_RS_AUX>(L.src0[0] + i * L.stride[0], dst + j * WS);
     }
   }
   if ((unsigned long long)(2 * lane) < p.A) glds16(p.cmax + (g * p.nch + ch) * p.A + 2 * lane, cm);
@@ -1198,7 +1201,7 @@ struct StDma {
   bool con;
   __device__ __forceinline__ void operator()(int j) {
     if (j < 8) {
-      glds16<MAP_RS_NT ? 2 : 0>(src, img + j * WS);
+      glds16<MAP_RS_AUX>(src, img + j * WS);
       src += stride;
     } else if (con) {
       glds16(csrc, cm);
@@ -1745,7 +1748,7 @@ __global__ __launch_bounds__(SH ? 256 : (ST ? 128 : 64), ST ? 2 : 1) void map_fo
   } else if constexpr (RS) {  // chunks 0 and 1 into the two slots (W <= 128: one piece per step)
     gl1 = glds_lanes<VI, 1>(p, g, k, lane);
     for (unsigned long long c = 0; c < 2 && c < nch; ++c)
-      map_chunk_glds<VI, C, 1, (MAP_RS_NT ? 2 : 0)>(p, gl1, g, k, c * C, R, wl + c * SLOT, WS, vbase + c * C * VI, cml + c * A, lane,
+      map_chunk_glds<VI, C, 1, MAP_RS_AUX>(p, gl1, g, k, c * C, R, wl + c * SLOT, WS, vbase + c * C * VI, cml + c * A, lane,
                                vpiece, p.diag);
   }
   if constexpr (GL) {
@@ -1851,7 +1854,7 @@ __global__ __launch_bounds__(SH ? 256 : (ST ? 128 : 64), ST ? 2 : 1) void map_fo
         if (ch + 2 < nch && !spread) st_chunk_glds(p, gl1, g, ch + 2, R, img, WS, cms, lane, 0);
       } else {
         if (ch + 2 < nch && !spread)
-          map_chunk_glds<VI, C, 1, (MAP_RS_NT ? 2 : 0)>(p, gl1, g, k, i2, R, img, WS, vsl, cms, lane, vpiece, p.diag);
+          map_chunk_glds<VI, C, 1, MAP_RS_AUX>(p, gl1, g, k, i2, R, img, WS, vsl, cms, lane, vpiece, p.diag);
       }
       MAP_TOCK(cy_issue);
       // advance the ring bookkeeping (the rest of the iteration uses sh_use only through shs / cms)
@@ -2314,7 +2317,7 @@ __global__ __launch_bounds__(SH ? 256 : (ST ? 128 : 64), ST ? 2 : 1) void map_fo
         st_chunk_glds(p, gl1, g, ch + 2, R, wl + slot * SLOT, WS, cml + slot * CMS, lane, 0);
       } else if (ch + 2 < nch) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        map_chunk_glds<VI, C, 1, (MAP_RS_NT ? 2 : 0)>(p, gl1, g, k, (ch + 2) * C, R, wl + slot * SLOT, WS, vbase + slot * C * VI,
+        map_chunk_glds<VI, C, 1, MAP_RS_AUX>(p, gl1, g, k, (ch + 2) * C, R, wl + slot * SLOT, WS, vbase + slot * C * VI,
                                  cml + slot * CMS, lane, vpiece, p.diag);
       }
     }

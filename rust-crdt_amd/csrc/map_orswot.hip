@@ -32,6 +32,7 @@ constexpr int kMoList = 256;  // Map removes naming the key, gathered per window
 constexpr int kMoLive = 256;  // live Map removes per key
 constexpr int kMoRows = 8;    // live Map-remove rows cached in LDS
 constexpr int kMoVd = 16;     // nested deferred removes per key state (flags bit 4 past it)
+constexpr size_t kMoShallowWaves = 2048;  // key waves from which the 4-step ring (2 waves per SIMD) runs
 constexpr unsigned long long kMoRingSpan = 2048;  // chunk-skip mode: register-ring steps run after a
                                                   // window of chunks that rarely skipped (multiple of 8)
 
@@ -54,14 +55,17 @@ __device__ __forceinline__ u64 mo_fg(u64 x, u64 c) { return x > c ? x : 0; }  //
 __device__ __forceinline__ u64 mo_max(u64 x, u64 y) { return x > y ? x : y; }
 
 // SPL > 0 (A == 64 / SPL: 32, 16 or 8 actors): the whole-chunk skip below, lane l holding actor
-// l % A in every register of the key's state.
-template <int MT, int SPL = 0>
+// l % A in every register of the key's state.  SHALLOW (M <= 4): a ring of 4 steps instead of 8, which
+// fits two waves per SIMD — chosen where the launch has at least two key waves per SIMD (G*K >= 2,048):
+// the config-4-scale causal fold cut into 2 groups of 8,192 replicas ran 6.4-6.7 ms against 11.4 ms for
+// the deep ring at 1 wave per SIMD (profiles/r06_mo_split.log).
+template <int MT, int SPL = 0, bool SHALLOW = false>
 __global__ __launch_bounds__(kMoWaves * kWave) void map_orswot_fold_kernel(MapOrswotPlan p) {
 #ifndef MO_RING_DEPTH4
 #define MO_RING_DEPTH4 8
 #endif
   // replica steps in flight (register ring); the chunk-skip mode's ring phase runs half as deep
-  constexpr int DEPTH = SPL > 0 ? (MT <= 4 ? 4 : 2) : (MT <= 4 ? MO_RING_DEPTH4 : (MT <= 8 ? 4 : 2));
+  constexpr int DEPTH = SPL > 0 ? (MT <= 4 ? 4 : 2) : (MT <= 4 ? (SHALLOW ? 4 : MO_RING_DEPTH4) : (MT <= 8 ? 4 : 2));
   extern __shared__ u64 lds[];
   const int lane = (int)(threadIdx.x % kWave), wv = (int)(threadIdx.x / kWave);
   const unsigned long long gk = (unsigned long long)blockIdx.x * kMoWaves + wv;
@@ -927,10 +931,11 @@ static hipError_t launch_mo_wide(const MapOrswotPlan &p, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <int MT, int SPL = 0>
+template <int MT, int SPL = 0, bool SHALLOW = false>
 static hipError_t launch_mo(const MapOrswotPlan &p, hipStream_t s) {
   const unsigned long long blocks = (p.G * p.K + kMoWaves - 1) / kMoWaves;
-  hipLaunchKernelGGL((map_orswot_fold_kernel<MT, SPL>), dim3((unsigned)blocks), dim3(kMoWaves * kWave), mo_lds(), s, p);
+  hipLaunchKernelGGL((map_orswot_fold_kernel<MT, SPL, SHALLOW>), dim3((unsigned)blocks), dim3(kMoWaves * kWave), mo_lds(),
+                     s, p);
   return hipGetLastError();
 }
 
@@ -1006,6 +1011,7 @@ extern "C" int crdt_map_orswot_lub_many(crdt_ctx *ctx, const crdt_map_orswot_bat
                           : spl == 2 ? launch_mo<4, 2>(p, ctx->stream)
                           : spl == 4 ? launch_mo<4, 4>(p, ctx->stream)
                           : spl == 8 ? launch_mo<4, 8>(p, ctx->stream)
+                          : M <= 4 && G * K >= kMoShallowWaves ? launch_mo<4, 0, true>(p, ctx->stream)
                           : M <= 4   ? launch_mo<4>(p, ctx->stream)
                           : M <= 8   ? launch_mo<8>(p, ctx->stream)
                                      : launch_mo<32>(p, ctx->stream);

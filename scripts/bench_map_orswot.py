@@ -32,6 +32,8 @@ ap.add_argument("--steps", type=int, default=5)
 ap.add_argument("--sample-keys", type=int, default=4)
 ap.add_argument("--parity-replicas", type=int, default=256)
 ap.add_argument("--input", choices=("random", "causal"), default="random")
+ap.add_argument("--split-probe", type=int, default=0,
+                help="also time the fold of the replicas cut into P groups (level 1 of a replica split)")
 args = ap.parse_args()
 R, K, A, M = args.replicas, args.keys, args.actors, args.members
 torch.cuda.set_device(0)
@@ -78,6 +80,20 @@ ctx.set_timing(False)
 ms, n = ctx.timing("map_orswot_fold")
 kern = ms / n
 alg = R * (A + K * A * (2 + M)) * 8 + K * A * (2 + M) * 8 + A * 8
+if args.split_probe > 1:
+    Ps = args.split_probe
+    v = lambda t: t.view((Ps, R // Ps) + tuple(t.shape[1:]))  # noqa: E731
+    for _ in range(2):
+        cg.map.orswot_lub_many(v(clock), v(ec), v(oc), v(ent), vd_off, ctx=ctx, check=False)
+    torch.cuda.synchronize()
+    ctx.timing_reset()
+    ctx.set_timing(True)
+    for _ in range(args.steps):
+        cg.map.orswot_lub_many(v(clock), v(ec), v(oc), v(ent), vd_off, ctx=ctx, check=False)
+    torch.cuda.synchronize()
+    ctx.set_timing(False)
+    ms1, n1 = ctx.timing("map_orswot_fold")
+    print(json.dumps({"split_probe": Ps, "level1_kernel_ms": ms1 / n1, "whole_kernel_ms": kern}), flush=True)
 
 import oracle as O  # noqa: E402  (checker only)
 

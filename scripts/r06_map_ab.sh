@@ -9,9 +9,9 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 mkdir -p gpurun_out && export TMPDIR=/tmp
 for rep in 1 2; do
-  for v in base ws8 nt wsnt; do
+  for v in base ${AB_VARIANTS:-ws8 nt wsnt}; do
     lib=rust-crdt_amd/libcrdt_gpu.so; [ $v != base ] && lib=rust-crdt_amd/libcrdt_gpu_$v.so
-    CRDT_GPU_LIB=$PWD/$lib timeout -k 10 200 python -u scripts/bench_map.py --steps 10 --cpu-replicas 16 > gpurun_out/r06_map_ab2_${v}_$rep.log 2>&1 || exit $?
-    echo "$v $rep $(grep -o '"kernel_ms": [0-9.]*' gpurun_out/r06_map_ab2_${v}_$rep.log) $(grep -o '"parity": "[A-Za-z]*"' gpurun_out/r06_map_ab2_${v}_$rep.log)"
+    CRDT_GPU_LIB=$PWD/$lib timeout -k 10 200 python -u scripts/bench_map.py --steps 10 --cpu-replicas 16 > gpurun_out/r06_map_${AB_TAG:-ab2}_${v}_$rep.log 2>&1 || exit $?
+    echo "$v $rep $(grep -o '"kernel_ms": [0-9.]*' gpurun_out/r06_map_${AB_TAG:-ab2}_${v}_$rep.log) $(grep -o '"parity": "[A-Za-z]*"' gpurun_out/r06_map_${AB_TAG:-ab2}_${v}_$rep.log)"
   done
 done

@@ -389,3 +389,23 @@ def test_map_orswot_wide_grouped_arbitrary(gpu_ctx):
     res, kw = _run(gpu_ctx, d, G=G, off=off)
     for g, got in enumerate(_got_maps(res, kw, G)):
         _same(got, exps[g])
+
+
+# ---- the 4-step ring at >= 2,048 key waves (round 6: two waves per SIMD) ------------------------------
+def test_map_orswot_shallow_ring_many_groups(gpu_ctx):
+    """G = 512 groups x K = 4 keys (2,048 key waves: the library's 4-step-ring instance), op-replay replicas
+    with deferred removes at both levels, 8 per group: every group equal to its own left fold."""
+    G, R, K, M, A = 512, 8, 4, 4, 6
+    maps = O.map_orswot_objects(G * R, K, M, A, seed=99, steps=3 * G * R, p_vrm=0.5)
+    d = O.map_orswot_to_dense(maps, K, M, A)
+    d["def_row"] = d["def_row"] % R
+    off = [0]
+    for g in range(G):
+        off.append(off[-1] + sum(len(m.deferred) for m in maps[g * R:(g + 1) * R]))
+    exps = [O.map_fold_objects(maps[g * R:(g + 1) * R]) for g in range(G)]
+    if any(len(e.val.deferred) > cg.map.VD_CAP for x in exps for e in x.entries.values()):
+        pytest.skip("nested deferred past the kernel's capacity")
+    res, kw = _run(gpu_ctx, d, G=G, off=off if off[-1] else None)
+    got = _got_maps(res, kw, G)
+    for g in range(G):
+        _same(got[g], exps[g])
