@@ -13,17 +13,23 @@ absent actor is 0.  Every entry point of the crate's VClock that acts on a batch
                                 causal.EQUAL / GREATER / LESS / CONCURRENT
     cmp_matrix                  partial_cmp of every pair of N clocks
     ingest / egress             the serde (bincode 1.x) wire form (vclock.rs:57-60)
+    from_clocks / to_clocks     reference-shaped clocks ({actor: counter} maps, any hashable actor)
+                                <-> dense rows, with the actor index kept across calls
+    get / inc / is_empty        VClock::get (:207-209), inc (:183-189, the next Dot, the state
+                                unchanged) and is_empty (:212-214) for a batch
 
-Each is one HIP launch through the C ABI (`crdt_vclock_*`, include/crdt_gpu.h); this module only
-shapes arguments.
+The ops above are one HIP launch each through the C ABI (`crdt_vclock_*`, include/crdt_gpu.h); the
+last two groups are the host-side helpers a caller of the crate's VClock API needs around them.
 """
 from __future__ import annotations
 
-from typing import Optional
+from typing import Dict, Hashable, List, Mapping, Optional, Sequence, Tuple
 
+import numpy as np
 import torch
 
 from . import _lattice, apply as _apply, causal as _causal, wire as _wire
+from .intern import Index, clocks_to_dense, dense_to_clocks
 from .causal import CONCURRENT, EQUAL, GREATER, LESS  # noqa: F401
 from .context import Context
 
@@ -79,3 +85,59 @@ def cmp_matrix(x: torch.Tensor, ctx: Optional[Context] = None) -> torch.Tensor:
 
 ingest = _wire.vclock_ingest
 egress = _wire.vclock_egress
+
+
+# ---- reference-shaped clocks <-> dense rows, and the per-clock accessors ----------------------------
+def from_clocks(clocks: Sequence[Mapping[Hashable, int]], actors: Optional[Index] = None, width: int = 0,
+                device=None) -> Tuple[torch.Tensor, Index]:
+    """A batch of reference clocks ({actor: counter}, u64 counters) as (N, max(width, |actors|)) int64
+    rows (u64 bits) on `device`, actors interned into `actors` (a new Index when None; pass the same
+    one to keep columns stable across batches).  Returns (rows, actors)."""
+    actors = actors if actors is not None else Index()
+    rows = clocks_to_dense(clocks, actors, width)
+    t = torch.from_numpy(rows.view(np.int64))
+    return (t.to(device) if device is not None else t), actors
+
+
+def to_clocks(rows: torch.Tensor, actors: Index) -> List[Dict[Hashable, int]]:
+    """Dense rows back to reference clocks: zero counters are dropped, as apply_dot never stores one
+    (vclock.rs:155-159), so from_clocks / to_clocks round-trip exactly."""
+    return dense_to_clocks(rows.detach().cpu().numpy().view(np.uint64), actors)
+
+
+def _cols(rows: torch.Tensor, actor) -> torch.Tensor:
+    if rows.dim() != 2:
+        raise ValueError("vclock: rows (N, A) expected")
+    a = torch.as_tensor(actor, dtype=torch.int64, device=rows.device)
+    if a.dim() == 0:
+        a = a.expand(rows.shape[0])
+    if a.shape != (rows.shape[0],):
+        raise ValueError("vclock: one actor column for all rows, or one per row")
+    if bool(((a < 0) | (a >= rows.shape[1])).any()):
+        raise ValueError("vclock: actor column out of range")
+    return a
+
+
+def get(rows: torch.Tensor, actor) -> torch.Tensor:
+    """VClock::get (vclock.rs:207-209) of every row: the counter of `actor` (a column index, or one per
+    row), 0 for an actor the clock does not hold.  (N,) int64 (u64 bits)."""
+    a = _cols(rows, actor)
+    return rows.gather(1, a[:, None])[:, 0]
+
+
+def inc(rows: torch.Tensor, actor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """VClock::inc (vclock.rs:183-189) of every row: the Dot {actor, get(actor) + 1}; the rows are not
+    changed (apply the dots with `apply`).  Returns (actor columns, counters).  A counter at u64::MAX
+    raises (the reference's `+ 1` would overflow)."""
+    a = _cols(rows, actor)
+    c = rows.gather(1, a[:, None])[:, 0]
+    if bool((c == -1).any()):
+        raise OverflowError("vclock.inc: counter at u64::MAX")
+    return a, c + 1
+
+
+def is_empty(rows: torch.Tensor) -> torch.Tensor:
+    """VClock::is_empty (vclock.rs:212-214) of every row: no actor with a nonzero counter.  (N,) bool."""
+    if rows.dim() != 2:
+        raise ValueError("vclock: rows (N, A) expected")
+    return ~(rows != 0).any(1)
