@@ -43,8 +43,13 @@ struct MapCounterPlan {
   unsigned *rerun_out;
 };
 
+// MC_AUX (build option): the cache-policy bits of the step-image LDS-DMA (0 default; 2 = nt, as the
+// MVReg Map fold's step images since round 6)
+#ifndef MC_AUX
+#define MC_AUX 0
+#endif
 __device__ __forceinline__ void glds16_mc(const void *g, u64 *lds) {
-  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void *)lds, 16, 0, 0);
+  __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void *)lds, 16, 0, MC_AUX);
 }
 
 // votes over the lanes of the caller's key (hm: its lanes' bits; ~0 with one key per wave)
