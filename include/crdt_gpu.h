@@ -68,7 +68,7 @@ const char *crdt_version(void);
  * appended `size_t Dv` to crdt_map_orswot_batch: revision 5 -> 6).  A caller checks
  * crdt_abi_version() == CRDT_ABI_VERSION of the header it was built against before any other call,
  * so a mismatched library fails clearly instead of reading a shorter struct. */
-#define CRDT_ABI_VERSION 6
+#define CRDT_ABI_VERSION 7
 int crdt_abi_version(void);
 const char *crdt_build_target(void);
 
@@ -932,6 +932,31 @@ int crdt_map_nested_apply_batch(crdt_ctx *ctx, const crdt_map_nested_states *sta
 int crdt_map_nested_forget_batch(crdt_ctx *ctx, const crdt_map_nested_states *states, const uint64_t *y,
                                  size_t y_stride, uint64_t *def_clock, const uint32_t *def_state, size_t D,
                                  uint8_t *def_keep);
+
+/* Pairwise in-place merge of value-typed Map states (round 6): self[i].merge(other[i]) for i < N
+ * (Map::merge map.rs:140-220 with the value's merge / forget: gcounter.rs:44-54 / pncounter.rs:70-82,
+ * orswot.rs:81-183, or the inner Map's map.rs:85-220 with mvreg.rs:88-128), on the apply layouts
+ * (crdt_map_counter_states / crdt_map_orswot_states / crdt_map_nested_states, N, K, A and W / M / K2
+ * equal on both sides) with each side's Map-level deferred removes as crdt_map_deferred slots (the
+ * counts may differ in Dcap).  Each pair is one group of the exact left fold above with R = 2
+ * (Map::new() merged with self, then other): self.merge(other) on every state apply, merge, forget or
+ * ingest leaves (deferred removes applied and not dominated by the clock).  self is rewritten: its
+ * rows, its nested lists, and its slots with the surviving removes (their merged key sets) in pool
+ * order, vacated slots zeroed; other is read only.  status[i]: bit 0 = more surviving removes than
+ * self's Dcap (the first Dcap kept), bit 3 = the fold reported a capacity for the pair (more than
+ * 256 / 512 live removes naming one key, more than 16 nested deferred removes on a key, more than 8
+ * values on an inner key: that pair's state is incomplete).  A def_count above its Dcap or a nested
+ * count above 16 fails the call (CRDT_EINVAL) before anything is written.  The call reads the slot
+ * counts on the host (one stream synchronisation).  Device memory only. */
+int crdt_map_counter_merge_batch(crdt_ctx *ctx, const crdt_map_counter_states *self, const crdt_map_deferred *self_def,
+                                 const crdt_map_counter_states *other, const crdt_map_deferred *other_def,
+                                 uint32_t *status);
+int crdt_map_orswot_merge_batch(crdt_ctx *ctx, const crdt_map_orswot_states *self, const crdt_map_deferred *self_def,
+                                const crdt_map_orswot_states *other, const crdt_map_deferred *other_def,
+                                uint32_t *status);
+int crdt_map_nested_merge_batch(crdt_ctx *ctx, const crdt_map_nested_states *self, const crdt_map_deferred *self_def,
+                                const crdt_map_nested_states *other, const crdt_map_deferred *other_def,
+                                uint32_t *status);
 
 /* ---- MVReg<u64, A> on its own (outside a Map) ------------------------------------------------
  * Replaces MVReg::merge (mvreg.rs:112-128) and MVReg::apply (mvreg.rs:130-166) for registers in the

@@ -20,7 +20,7 @@ CRDT_ECOMM = -5
 CRDT_UNIQUE_ID_BYTES = 128
 CRDT_ACCUMULATE = 0x1
 CRDT_MEM_DEVICE = 0
-CRDT_ABI_VERSION = 6  # include/crdt_gpu.h
+CRDT_ABI_VERSION = 7  # include/crdt_gpu.h
 CRDT_MEM_HOST = 1
 CRDT_KIND = {"vclock": 1, "gcounter": 2, "pncounter": 3, "gset": 4}
 CRDT_RED_MAX, CRDT_RED_MIN, CRDT_RED_SUM = 0, 1, 2
@@ -59,6 +59,7 @@ EXPORTS = (
     "crdt_map_nested_lub_many_sharded", "crdt_map_counter_forget_batch", "crdt_map_orswot_forget_batch",
     "crdt_map_counter_apply_batch", "crdt_map_orswot_apply_batch",
     "crdt_map_nested_apply_batch", "crdt_map_nested_forget_batch", "crdt_map_nested_ingest", "crdt_map_nested_egress",
+    "crdt_map_counter_merge_batch", "crdt_map_orswot_merge_batch", "crdt_map_nested_merge_batch",
     "crdt_map_counter_ingest", "crdt_map_counter_egress", "crdt_map_orswot_ingest", "crdt_map_orswot_egress",
 )
 
@@ -322,6 +323,12 @@ _SIGS.update({
                                      P], ctypes.c_int),
     "crdt_map_apply_batch": ([P, ctypes.POINTER(MapStates), P, P, P, S, ctypes.POINTER(MapOps), P], ctypes.c_int),
     "crdt_orswot_merge_batch": ([P, ctypes.POINTER(OrswotStates), ctypes.POINTER(OrswotStates), P], ctypes.c_int),
+    "crdt_map_counter_merge_batch": ([P, ctypes.POINTER(MapCounterStates), ctypes.POINTER(MapDeferred),
+                                      ctypes.POINTER(MapCounterStates), ctypes.POINTER(MapDeferred), P], ctypes.c_int),
+    "crdt_map_orswot_merge_batch": ([P, ctypes.POINTER(MapOrswotStates), ctypes.POINTER(MapDeferred),
+                                     ctypes.POINTER(MapOrswotStates), ctypes.POINTER(MapDeferred), P], ctypes.c_int),
+    "crdt_map_nested_merge_batch": ([P, ctypes.POINTER(MapNestedStates), ctypes.POINTER(MapDeferred),
+                                     ctypes.POINTER(MapNestedStates), ctypes.POINTER(MapDeferred), P], ctypes.c_int),
     "crdt_map_merge_batch": ([P, ctypes.POINTER(MapStates), ctypes.POINTER(MapDeferred), ctypes.POINTER(MapStates),
                               ctypes.POINTER(MapDeferred), P], ctypes.c_int),
     "crdt_lwwreg_lub_many_sharded": ([P, P, P, S, S, S, U64, P, P, P], ctypes.c_int),

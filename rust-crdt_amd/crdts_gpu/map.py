@@ -1188,64 +1188,26 @@ def nested_forget_batch(res: "MapNestedLub", y: torch.Tensor, def_clock: Optiona
 # ---- Pairwise merge_batch of value-typed Map states (round 6) --------------------------------------
 # self[i].merge(other[i]) for Map<K, GCounter / PNCounter>, Map<K, Orswot<M>> and Map<K, Map<K2, MVReg>>
 # states in their apply layouts (wire.MapCounterFrames / MapOrswotFrames / MapNestedFrames or any
-# object with those fields): each pair is one group of the exact left-fold kernel (Map::new() merged
-# with self, then with other — counter_lub_many / orswot_lub_many / nested_lub_many, R = 2), whose
-# result is written back into self, the surviving Map-level deferred removes compacted into self's
-# slots.  Map::merge from an empty Map reproduces a state whose deferred removes are applied and not
-# dominated by its clock — every state apply, merge, forget or ingest leaves — so the fold of
-# [self, other] is self.merge(other) (map.rs:140-220) on those states.
-def _pair(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
-    return torch.stack((a, b), dim=1).contiguous()
-
-
-def _pair_pool(me, other, N: int, A: int, Kw: int, what: str):
-    """The two states' Map-level deferred slots as one pool grouped by pair (self's first): host
-    def_off (N+1,), def_row (D,) int32 (0 self, 1 other), def_clock (D, A), def_keys (D, Kw), and
-    the pair index of every row."""
-    dev = me.clock.device
-    masks, rows = [], []
-    for s_, r in ((me, 0), (other, 1)):
-        Dc = s_.def_clock.shape[1]
-        if (tuple(s_.def_clock.shape) != (N, Dc, A) or tuple(s_.def_keys.shape) != (N, Dc, Kw)
-                or tuple(s_.def_count.shape) != (N,) or s_.def_count.dtype not in (torch.int32, torch.uint32)
-                or s_.def_count.device != dev):
-            raise ValueError(f"{what}: deferred slots (N, Dcap, A) / (N, Dcap, Kw) / (N,) int32 expected")
-        cnt = s_.def_count.to(torch.int64)
-        if bool(((cnt < 0) | (cnt > Dc)).any()):
-            raise ValueError(f"{what}: def_count outside [0, Dcap]")
-        masks.append(torch.arange(Dc, device=dev)[None, :] < cnt[:, None])
-        rows.append(torch.full((N, Dc), r, dtype=torch.int32, device=dev))
-    mask = torch.cat(masks, 1)
-    clk = torch.cat((me.def_clock, other.def_clock), 1)[mask].contiguous()
-    keys = torch.cat((me.def_keys, other.def_keys), 1)[mask].contiguous()
-    row = torch.cat(rows, 1)[mask].contiguous()
-    gid = torch.arange(N, device=dev)[:, None].expand_as(mask)[mask]
-    per = mask.sum(1).cpu().numpy()
-    off = np.concatenate([[0], np.cumsum(per)]).astype(np.uint64)
-    return off, row, clk, keys, gid
-
-
-def _store_survivors(me, keep, keys_out, clk, gid, N: int) -> torch.Tensor:
-    """Compact the fold's surviving deferred removes (def_keep, their merged key sets) into self's
-    slots in pool order; status bit 0 where more survive than self's Dcap (the first Dcap kept)."""
-    dev = me.clock.device
-    Dcap = me.def_clock.shape[1]
-    status = torch.zeros(N, dtype=torch.int32, device=dev)
-    me.def_clock.zero_()
-    me.def_keys.zero_()
-    if keep is None or clk.shape[0] == 0:
-        me.def_count.zero_()
-        return status
-    k = keep.bool()
-    g = gid[k]
-    counts = torch.bincount(g, minlength=N)
-    pos = torch.arange(g.numel(), device=dev) - (torch.cumsum(counts, 0) - counts)[g]
-    fit = pos < Dcap
-    me.def_clock[g[fit], pos[fit]] = clk[k][fit]
-    me.def_keys[g[fit], pos[fit]] = keys_out[k][fit]
-    me.def_count.copy_(torch.clamp(counts, max=Dcap).to(me.def_count.dtype))
-    status |= (counts > Dcap).to(torch.int32)
-    return status
+# object with those fields): crdt_map_{counter,orswot,nested}_merge_batch (csrc/vmap_merge.hip) — each
+# pair one group of the exact left-fold kernel (Map::new() merged with self, then with other, R = 2),
+# self's rows, nested lists and Map-level slots rewritten (the surviving removes in pool order).  Map::merge
+# from an empty Map reproduces a state whose deferred removes are applied and not dominated by its
+# clock — every state apply, merge, forget or ingest leaves — so this is self.merge(other) (map.rs:140-220)
+# on those states.  Status bits as the header: 0 = survivors past self's Dcap (first Dcap kept), 3 = a
+# fold capacity (the pair's state incomplete).
+def _vm_deferred(ctx, st, N: int, A: int, Kw: int, what: str):
+    Dc = st.def_clock.shape[1] if st.def_clock.dim() == 3 else 0
+    if (tuple(st.def_clock.shape) != (N, Dc, A) or tuple(st.def_keys.shape) != (N, Dc, Kw)
+            or not st.def_clock.is_contiguous() or not st.def_keys.is_contiguous()):
+        raise ValueError(f"{what}: def_clock / def_keys must be contiguous (N, Dcap, A) / (N, Dcap, Kw)")
+    if (tuple(st.def_count.shape) != (N,) or st.def_count.dtype not in (torch.int32, torch.uint32)
+            or st.def_count.device != st.clock.device):
+        raise ValueError(f"{what}: def_count must be an (N,) int32 tensor on the states' device")
+    ctx.check_tensor(st.def_clock, f"{what}(def_clock)")
+    ctx.check_tensor(st.def_keys, f"{what}(def_keys)")
+    d = _abi.MapDeferred()
+    d.clock, d.keys, d.count, d.Dcap = st.def_clock.data_ptr(), st.def_keys.data_ptr(), st.def_count.data_ptr(), Dc
+    return d
 
 
 def _same_shapes(me, other, fields, what):
@@ -1253,92 +1215,81 @@ def _same_shapes(me, other, fields, what):
         a, b = getattr(me, nm), getattr(other, nm)
         if tuple(a.shape) != tuple(b.shape) or a.device != b.device:
             raise ValueError(f"{what}: self.{nm} {tuple(a.shape)} and other.{nm} {tuple(b.shape)} differ")
-        if not a.is_contiguous():
-            raise ValueError(f"{what}: self.{nm} must be contiguous")
+        if not a.is_contiguous() or not b.is_contiguous():
+            raise ValueError(f"{what}: {nm} must be contiguous")
+
+
+def _vm_call(ctx, fn, sa, sb, me, other, N, A, K, what):
+    Kw = (K + 63) // 64
+    da, db = _vm_deferred(ctx, me, N, A, Kw, what), _vm_deferred(ctx, other, N, A, Kw, what)
+    status = torch.zeros(N, dtype=torch.int32, device=me.clock.device)
+    ctx.call(fn, ctypes.byref(sa), ctypes.byref(da), ctypes.byref(sb), ctypes.byref(db), status.data_ptr())
+    return status
 
 
 def counter_merge_batch(me, other, ctx: Optional[Context] = None) -> torch.Tensor:
-    """self[i].merge(other[i]) for N Map<K, GCounter / PNCounter> states, in place on `me` (Map::merge
-    map.rs:140-220 with gcounter.rs:44-54 / pncounter.rs:70-82 as the value's merge and forget):
+    """self[i].merge(other[i]) for N Map<K, GCounter / PNCounter> states, in place on `me`
+    (crdt_map_counter_merge_batch; Map::merge map.rs:140-220 with gcounter.rs:44-54 / pncounter.rs:70-82):
     clock (N, A), ec (N, K, A), val (N, K, W, A), def_clock (N, Dcap, A), def_keys (N, Dcap, Kw),
-    def_count (N,) int32 — the crdt_map_counter_states layout.  Returns status (N,) int32: bit 0 =
-    more surviving deferred removes than self's Dcap (the first Dcap kept)."""
+    def_count (N,) int32 — the crdt_map_counter_states layout.  Returns status (N,) int32."""
     what = "map.counter_merge_batch"
     _same_shapes(me, other, ("clock", "ec", "val"), what)
     ctx = ctx or Context.default(me.clock.device.index)
     N, A = me.clock.shape
-    K = me.ec.shape[1]
+    K, W = me.ec.shape[1], me.val.shape[2]
+    if tuple(me.ec.shape) != (N, K, A) or tuple(me.val.shape) != (N, K, W, A):
+        raise ValueError(f"{what}: clock (N, A), ec (N, K, A), val (N, K, W, A) expected")
     if N == 0:
         return torch.zeros(0, dtype=torch.int32, device=me.clock.device)
-    off, row, clk, keys, gid = _pair_pool(me, other, N, A, (K + 63) // 64, what)
-    dk = dict(def_off=off, def_row=row, def_clock=clk, def_keys=keys) if clk.shape[0] else {}
-    res = counter_lub_many(_pair(me.clock, other.clock), _pair(me.ec, other.ec), _pair(me.val, other.val),
-                           ctx=ctx, **dk)
-    me.clock.copy_(res.clock)
-    me.ec.copy_(res.ec)
-    me.val.copy_(res.val)
-    return _store_survivors(me, res.def_keep, res.def_keys, clk, gid, N)
-
-
-def _pair_csr(n_a, n_b, c_a, c_b, x_a, x_b, cap: int, what: str):
-    """Two states' per-key slot lists (counts (N, K), slots (N, K, cap, ...)) as one device CSR over
-    (pair, replica, key): off (N*2*K + 1,) int64, rows of c and x."""
-    n = _pair(n_a, n_b).to(torch.int64)
-    if bool(((n < 0) | (n > cap)).any()):
-        raise ValueError(f"{what}: nested deferred counts outside [0, {cap}]")
-    mask = torch.arange(cap, device=n.device) < n[..., None]
-    off = torch.zeros(n.numel() + 1, dtype=torch.int64, device=n.device)
-    off[1:] = torch.cumsum(n.flatten(), 0)
-    return off, _pair(c_a, c_b)[mask].contiguous(), _pair(x_a, x_b)[mask].contiguous()
+    sts = []
+    for st in (me, other):
+        for t, nm in ((st.clock, "clock"), (st.ec, "ec"), (st.val, "val")):
+            ctx.check_tensor(t, f"{what}({nm})")
+        x = _abi.MapCounterStates()
+        x.N, x.K, x.A, x.W = N, K, A, W
+        x.clock, x.clock_stride = st.clock.data_ptr(), A
+        x.ec, x.ec_stride = st.ec.data_ptr(), K * A
+        x.val, x.val_stride = st.val.data_ptr(), K * W * A
+        sts.append(x)
+    return _vm_call(ctx, "crdt_map_counter_merge_batch", sts[0], sts[1], me, other, N, A, K, what)
 
 
 def orswot_merge_batch(me, other, ctx: Optional[Context] = None) -> torch.Tensor:
-    """self[i].merge(other[i]) for N Map<K, Orswot<M>> states, in place on `me` (Map::merge
-    map.rs:140-220 with Orswot::merge orswot.rs:81-149 and forget :150-183): the crdt_map_orswot_states
-    layout (clock, ec, oc, ent, vd_n, vd_clock, vd_mem) + the Map's deferred slots def_clock /
-    def_keys / def_count.  Returns status (N,) int32 as counter_merge_batch; a fold limit (more than
-    16 nested deferred removes on a key, more than 256 live Map removes naming one key) raises."""
+    """self[i].merge(other[i]) for N Map<K, Orswot<M>> states, in place on `me`
+    (crdt_map_orswot_merge_batch; Map::merge map.rs:140-220 with Orswot::merge orswot.rs:81-149 and forget
+    :150-183): the crdt_map_orswot_states layout (clock, ec, oc, ent, vd_n, vd_clock, vd_mem) + the Map's
+    deferred slots def_clock / def_keys / def_count.  Returns status (N,) int32."""
     what = "map.orswot_merge_batch"
     _same_shapes(me, other, ("clock", "ec", "oc", "ent", "vd_n", "vd_clock", "vd_mem"), what)
     ctx = ctx or Context.default(me.clock.device.index)
     N, A = me.clock.shape
-    K = me.ec.shape[1]
+    K, M = me.ent.shape[1], me.ent.shape[2]
     if N == 0:
         return torch.zeros(0, dtype=torch.int32, device=me.clock.device)
-    off, row, clk, keys, gid = _pair_pool(me, other, N, A, (K + 63) // 64, what)
-    vd_off, vclk, vmem = _pair_csr(me.vd_n, other.vd_n, me.vd_clock, other.vd_clock, me.vd_mem, other.vd_mem,
-                                   VD_CAP, what)
-    vk = dict(vd_clock=vclk, vd_mem=vmem) if vclk.shape[0] else {}
-    dk = dict(def_off=off, def_row=row, def_clock=clk, def_keys=keys) if clk.shape[0] else {}
-    res = orswot_lub_many(_pair(me.clock, other.clock), _pair(me.ec, other.ec), _pair(me.oc, other.oc),
-                          _pair(me.ent, other.ent), vd_off, ctx=ctx, **vk, **dk)
-    for nm in ("clock", "ec", "oc", "ent", "vd_n", "vd_clock", "vd_mem"):
-        getattr(me, nm).copy_(getattr(res, nm).reshape(getattr(me, nm).shape))
-    return _store_survivors(me, res.def_keep, res.def_keys, clk, gid, N)
+    sts = []
+    for st in (me, other):
+        for nm in ("clock", "ec", "oc", "ent", "vd_clock", "vd_mem"):
+            ctx.check_tensor(getattr(st, nm), f"{what}({nm})")
+        if st.vd_n.dtype != torch.int32 or tuple(st.vd_n.shape) != (N, K):
+            raise ValueError(f"{what}: vd_n must be an (N, K) int32 tensor")
+        x = _abi.MapOrswotStates()
+        x.N, x.K, x.M, x.A = N, K, M, A
+        x.clock, x.ec, x.oc, x.ent = st.clock.data_ptr(), st.ec.data_ptr(), st.oc.data_ptr(), st.ent.data_ptr()
+        x.vd_n, x.vd_clock, x.vd_mem = st.vd_n.data_ptr(), st.vd_clock.data_ptr(), st.vd_mem.data_ptr()
+        sts.append(x)
+    return _vm_call(ctx, "crdt_map_orswot_merge_batch", sts[0], sts[1], me, other, N, A, K, what)
 
 
 def nested_merge_batch(me, other, ctx: Optional[Context] = None) -> torch.Tensor:
-    """self[i].merge(other[i]) for N Map<K, Map<K2, MVReg<u64>>> states, in place on `me` (Map::merge
-    map.rs:140-220 at both levels, MVReg::merge mvreg.rs:112-128): the crdt_map_nested_states layout
-    (clock, ec, ic, iec, ivc, ivv, nval, id_n, id_clock, id_keys) + the outer deferred slots def_clock /
-    def_keys / def_count.  Returns status (N,) int32 as counter_merge_batch; a fold limit (more than 8
-    values on an inner key, 16 inner deferred removes on a key, 256 live outer removes naming one
-    key) raises."""
+    """self[i].merge(other[i]) for N Map<K, Map<K2, MVReg<u64>>> states, in place on `me`
+    (crdt_map_nested_merge_batch; Map::merge map.rs:140-220 at both levels, MVReg::merge mvreg.rs:112-128):
+    the crdt_map_nested_states layout (clock, ec, ic, iec, ivc, ivv, nval, id_n, id_clock, id_keys) + the
+    outer deferred slots def_clock / def_keys / def_count.  Returns status (N,) int32."""
     what = "map.nested_merge_batch"
     _same_shapes(me, other, ("clock", "ec", "ic", "iec", "ivc", "ivv", "nval", "id_n", "id_clock", "id_keys"), what)
     ctx = ctx or Context.default(me.clock.device.index)
-    N, A = me.clock.shape
-    K = me.ec.shape[1]
-    if N == 0:
+    if me.clock.shape[0] == 0:
         return torch.zeros(0, dtype=torch.int32, device=me.clock.device)
-    off, row, clk, keys, gid = _pair_pool(me, other, N, A, (K + 63) // 64, what)
-    id_off, iclk, ikeys = _pair_csr(me.id_n, other.id_n, me.id_clock, other.id_clock, me.id_keys, other.id_keys,
-                                    NM_ID, what)
-    ik = dict(id_clock=iclk, id_keys=ikeys) if iclk.shape[0] else {}
-    dk = dict(def_off=off, def_row=row, def_clock=clk, def_keys=keys) if clk.shape[0] else {}
-    res = nested_lub_many(_pair(me.clock, other.clock), _pair(me.ec, other.ec), _pair(me.ic, other.ic),
-                          _pair(me.iec, other.iec), _pair(me.ivc, other.ivc), _pair(me.ivv, other.ivv), id_off,
-                          ctx=ctx, **ik, **dk)
-    for nm in ("clock", "ec", "ic", "iec", "ivc", "ivv", "nval", "id_n", "id_clock", "id_keys"):
-        getattr(me, nm).copy_(getattr(res, nm).reshape(getattr(me, nm).shape))
-    return _store_survivors(me, res.def_keep, res.def_keys, clk, gid, N)
+    sa, N, K, A = _nested_states(me, what)
+    sb, _, _, _ = _nested_states(other, what)
+    return _vm_call(ctx, "crdt_map_nested_merge_batch", sa, sb, me, other, N, A, K, what)

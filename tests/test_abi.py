@@ -32,7 +32,7 @@ def test_library_exports_every_declared_symbol():
     import crdts_gpu._abi as abi
     assert sorted(abi.EXPORTS) == declared()
     lib.crdt_version.restype = ctypes.c_char_p
-    assert lib.crdt_version() == b"0.6.0"
+    assert lib.crdt_version() == b"0.7.0"
     lib.crdt_build_target.restype = ctypes.c_char_p
     assert lib.crdt_build_target() == b"gfx950"
 

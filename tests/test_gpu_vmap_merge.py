@@ -1,5 +1,6 @@
-"""GPU: pairwise CvRDT::merge of value-typed Map states (round 6; map.counter_merge_batch /
-orswot_merge_batch / nested_merge_batch): self[i].merge(other[i]) for N pairs at once, against the
+"""GPU: pairwise CvRDT::merge of value-typed Map states (round 6; crdt_map_{counter,orswot,nested}_merge_batch
+through map.counter_merge_batch / orswot_merge_batch / nested_merge_batch): self[i].merge(other[i]) for
+N pairs at once, against the
 oracle's Map.merge (map.rs:140-220) with the value's merge inside — GCounter / PNCounter
 (gcounter.rs:44-54, pncounter.rs:70-82), Orswot (orswot.rs:81-149) and the nested Map<K2, MVReg>
 (mvreg.rs:112-128).  Pairs are op-replay replicas of one history (concurrent entries, removes seen by
@@ -93,8 +94,10 @@ def test_counter_merge_batch_validation(gpu_ctx):
         cg.map.counter_merge_batch(me, other._replace(ec=other.ec[:, :2].contiguous()), ctx=gpu_ctx)
     bad = other.def_count.clone()
     bad[0] = 5
-    with pytest.raises(ValueError):
+    before = me.clock.clone()
+    with pytest.raises(cg.CrdtGpuError) as ei:  # (the C entry point: EINVAL before anything is written)
         cg.map.counter_merge_batch(me, other._replace(def_count=bad), ctx=gpu_ctx)
+    assert ei.value.code == -1 and torch.equal(me.clock, before)
     z = _counter_frames([], 3, 3, 2, 4)
     assert cg.map.counter_merge_batch(z, z, ctx=gpu_ctx).numel() == 0
 
@@ -164,3 +167,43 @@ def test_nested_merge_batch(gpu_ctx, seed, N, K, K2, A):
     for i in range(N):
         got = back(decode_states(me, i, _slot_list(me, i)))
         assert canon(got) == canon(exps[i]), i
+
+
+def test_counter_merge_batch_different_dcaps(gpu_ctx):
+    """self and other with different slot capacities (other's Dcap 3 x self's): the pool takes both."""
+    N, K, A, W = 10, 6, 5, 2
+    maps = O.map_counter_objects(2 * N, K, A, W, seed=8, steps=20 * N)
+    Dc = max([len(m.deferred) for m in maps] + [1])
+    me, other = _counter_frames(maps[:N], K, A, W, 2 * Dc), _counter_frames(maps[N:], K, A, W, 3 * Dc)
+    status = cg.map.counter_merge_batch(me, other, ctx=gpu_ctx).cpu().numpy()
+    assert (status == 0).all(), status
+    c, e, v = to_host(me.clock), to_host(me.ec), to_host(me.val)
+    for i in range(N):
+        exp = maps[i].copy()
+        exp.merge(maps[N + i].copy())
+        assert O.dense_to_map_counter(c[i], e[i], v[i], _slot_list(me, i)) == exp, i
+
+
+def test_orswot_merge_batch_other_untouched_and_validation(gpu_ctx):
+    N, K, M, A = 6, 4, 5, 4
+    maps = O.map_orswot_objects(2 * N, K, M, A, seed=11, steps=60, p_vrm=0.5)
+    me, other = _orswot_frames(gpu_ctx, maps[:N], K, M, A, 8), _orswot_frames(gpu_ctx, maps[N:], K, M, A, 8)
+    snap = [t.clone() for t in other]
+    bad = other.vd_n.clone()
+    bad[0, 0] = 17
+    with pytest.raises(cg.CrdtGpuError):
+        cg.map.orswot_merge_batch(me, other._replace(vd_n=bad), ctx=gpu_ctx)
+    exps = []
+    for i in range(N):
+        exp = maps[i].copy()
+        exp.merge(maps[N + i].copy())
+        exps.append(exp)
+    if any(len(e.val.deferred) > cg.map.VD_CAP for x in exps for e in x.entries.values()):
+        pytest.skip("nested deferred past the kernel's capacity")
+    status = cg.map.orswot_merge_batch(me, other, ctx=gpu_ctx).cpu().numpy()
+    assert (status == 0).all(), status
+    for a_, b_ in zip(snap, other):
+        assert torch.equal(a_, b_)
+    for i in range(N):
+        got = _orswot_state(me, i, K)
+        assert got.clock == exps[i].clock and got.entries == exps[i].entries and got.deferred == exps[i].deferred, i
