@@ -830,7 +830,8 @@ int crdt_map_orswot_lub_many_sharded(crdt_ctx *ctx, const crdt_map_orswot_batch 
  *   8 values — results of the group unreliable; def_keep / def_keys as crdt_map_out.
  * Map::forget collects the inner deferred removes into a new map: two whose clocks become equal keep
  * one entry with the later one's keys (the oracle's dict order; the reference's is unspecified).
- * Limits: A <= 64, K2 <= 64, V <= 8.  Device and host memory (crdt_mem_kind). */
+ * Limits: A <= 256 (round 6: lane l holds actors l + 64 j), K2 <= 64, V <= 8.  Device and host memory
+ * (crdt_mem_kind). */
 typedef struct crdt_map_nested_batch {
   size_t G, R, K, K2, V, A;
   const uint64_t *clock, *ec, *ic, *iec, *ivc, *ivv;

@@ -4,7 +4,7 @@
 // innermost value merge) and whose forget is Map's Causal::forget (map.rs:85-114: entry clocks,
 // values, deferred clocks and the inner Map's own clock).  As for every Map value type the fold
 // acc = Map::new(); for r: acc.merge(r) is not associative, so each outer key is folded in replica
-// order (exact for any input): one wave per (group, outer key), lane = actor (A <= 64).
+// order (exact for any input): one wave per (group, outer key), lane l = actors l + 64 j (A <= 256, round 6).
 //
 // Step r on the key's state (outer clock C, entry clock e, inner Map: clock ic, entry clocks iec[j],
 // MVReg slots in Vec order, inner deferred removes) with replica r's (c2, e2, ic2, iec2, values, D2):
@@ -53,34 +53,138 @@ struct NestedMapPlan {
   // [K2][8]) and for a staged copy of the replica's inner Map (iec, slots, values); 0 = off (the state
   // then lives in the key's output rows, the replica is read from HBM where it is used)
   unsigned long long xs_state, xs_stage;
+  unsigned wpb;  // key waves per workgroup (kNmWaves; fewer for the wide instances' LDS rows)
 };
 
-__device__ __forceinline__ bool nm_nz(u64 x) { return __ballot(x != 0) != 0; }
-__device__ __forceinline__ u64 nm_fg(u64 x, u64 c) { return x > c ? x : 0; }  // VClock::forget, per actor
-__device__ __forceinline__ u64 nm_max(u64 x, u64 y) { return x > y ? x : y; }
+// A clock across the wave: lane l holds actors l + 64 j, j < APL (A <= 64 APL; round 6: APL 2 and 4 take
+// the reference's TMap domain of u8 actors).  Words past A are 0 in every row, so they never change a
+// vote.
+template <int APL>
+struct NVc {
+  u64 w[APL];
+};
+template <int APL>
+__device__ __forceinline__ NVc<APL> nv_fill(u64 v) {
+  NVc<APL> x;
+#pragma unroll
+  for (int j = 0; j < APL; ++j) x.w[j] = v;
+  return x;
+}
+template <int APL>
+__device__ __forceinline__ NVc<APL> nv_zero() { return nv_fill<APL>(0ull); }
+template <int APL>
+__device__ __forceinline__ NVc<APL> nv_ld(const u64 *row, int lane, unsigned long long A) {
+  NVc<APL> x;
+#pragma unroll
+  for (int j = 0; j < APL; ++j) {
+    const unsigned long long a = (unsigned long long)lane + 64ull * j;
+    x.w[j] = a < A ? row[a] : 0ull;
+  }
+  return x;
+}
+template <int APL>
+__device__ __forceinline__ void nv_st(u64 *row, const NVc<APL> &x, int lane, unsigned long long A) {
+#pragma unroll
+  for (int j = 0; j < APL; ++j) {
+    const unsigned long long a = (unsigned long long)lane + 64ull * j;
+    if (a < A) row[a] = x.w[j];
+  }
+}
+// an LDS row array [i][64 APL] (word j of lane l at 64 j + l)
+template <int APL>
+__device__ __forceinline__ NVc<APL> nv_lr(const u64 *base, int i, int lane) {
+  NVc<APL> x;
+#pragma unroll
+  for (int j = 0; j < APL; ++j) x.w[j] = base[(unsigned long long)i * kWave * APL + 64ull * j + lane];
+  return x;
+}
+template <int APL>
+__device__ __forceinline__ void nv_lw(u64 *base, int i, const NVc<APL> &x, int lane) {
+#pragma unroll
+  for (int j = 0; j < APL; ++j) base[(unsigned long long)i * kWave * APL + 64ull * j + lane] = x.w[j];
+}
+template <int APL>
+__device__ __forceinline__ bool nm_nz(const NVc<APL> &x) {
+  bool b = false;
+#pragma unroll
+  for (int j = 0; j < APL; ++j) b = b || x.w[j] != 0;
+  return __ballot(b) != 0;
+}
+template <int APL>  // VClock::forget, per actor
+__device__ __forceinline__ NVc<APL> nm_fg(const NVc<APL> &x, const NVc<APL> &c) {
+  NVc<APL> r;
+#pragma unroll
+  for (int j = 0; j < APL; ++j) r.w[j] = x.w[j] > c.w[j] ? x.w[j] : 0ull;
+  return r;
+}
+template <int APL>
+__device__ __forceinline__ NVc<APL> nm_max(const NVc<APL> &x, const NVc<APL> &y) {
+  NVc<APL> r;
+#pragma unroll
+  for (int j = 0; j < APL; ++j) r.w[j] = x.w[j] > y.w[j] ? x.w[j] : y.w[j];
+  return r;
+}
+// per actor: x where x == y, else z (the branch-free entry join's first case)
+template <int APL>
+__device__ __forceinline__ NVc<APL> nm_sel_eq(const NVc<APL> &x, const NVc<APL> &y, const NVc<APL> &z) {
+  NVc<APL> r;
+#pragma unroll
+  for (int j = 0; j < APL; ++j) r.w[j] = x.w[j] == y.w[j] ? x.w[j] : z.w[j];
+  return r;
+}
+template <int APL>  // some actor with x > y
+__device__ __forceinline__ bool nm_gt_any(const NVc<APL> &x, const NVc<APL> &y) {
+  bool b = false;
+#pragma unroll
+  for (int j = 0; j < APL; ++j) b = b || x.w[j] > y.w[j];
+  return __ballot(b) != 0;
+}
+template <int APL>  // some actor with x >= y
+__device__ __forceinline__ bool nm_ge_any(const NVc<APL> &x, const NVc<APL> &y) {
+  bool b = false;
+#pragma unroll
+  for (int j = 0; j < APL; ++j) b = b || x.w[j] >= y.w[j];
+  return __ballot(b) != 0;
+}
 // VClock partial order, whole clock: x < y (x <= y everywhere and x != y somewhere)
-__device__ __forceinline__ bool nm_lt(u64 x, u64 y) { return !__ballot(x > y) && __ballot(x != y); }
-__device__ __forceinline__ bool nm_eq(u64 x, u64 y) { return !__ballot(x != y); }
+template <int APL>
+__device__ __forceinline__ bool nm_lt(const NVc<APL> &x, const NVc<APL> &y) {
+  bool gt = false, ne = false;
+#pragma unroll
+  for (int j = 0; j < APL; ++j) {
+    gt = gt || x.w[j] > y.w[j];
+    ne = ne || x.w[j] != y.w[j];
+  }
+  return !__ballot(gt) && __ballot(ne);
+}
+template <int APL>
+__device__ __forceinline__ bool nm_eq(const NVc<APL> &x, const NVc<APL> &y) {
+  bool ne = false;
+#pragma unroll
+  for (int j = 0; j < APL; ++j) ne = ne || x.w[j] != y.w[j];
+  return !__ballot(ne);
+}
 
+template <int APL>
 __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(NestedMapPlan p) {
+  using Vc = NVc<APL>;
   extern __shared__ u64 lds[];
   const int lane = (int)(threadIdx.x % kWave), wv = (int)(threadIdx.x / kWave);
-  const unsigned long long gk = (unsigned long long)blockIdx.x * kNmWaves + wv;
-  if (gk >= p.G * p.K) return;  // (whole waves; nothing below synchronises the workgroup)
+  const unsigned long long gk = (unsigned long long)blockIdx.x * p.wpb + wv;
+  if (wv >= (int)p.wpb || gk >= p.G * p.K) return;  // (whole waves; nothing below synchronises the workgroup)
   const unsigned long long g = gk / p.K, k = gk % p.K, A = p.A, R = p.R, K = p.K, K2 = p.K2, V = p.V;
-  constexpr unsigned long long WQ = kNmList + kNmLive / 2 + kNmRows * kWave + kNmId * kWave + kNmId + kNmK2 / 8;
+  constexpr unsigned long long WQ =
+      kNmList + kNmLive / 2 + kNmRows * kWave * APL + kNmId * kWave * APL + kNmId + kNmK2 / 8;
   u64 *lst = lds + (unsigned long long)wv * (WQ + p.xs_state + p.xs_stage);
   u64 *const xst = lst + WQ, *const xsg = xst + p.xs_state;  // (LDS state, staged replica)
   uint32_t *live = reinterpret_cast<uint32_t *>(lst + kNmList);
-  u64 *rows = lst + kNmList + kNmLive / 2;  // [kNmRows][64] live outer-remove rows
-  u64 *drow = rows + kNmRows * kWave;       // [kNmId][64] inner deferred rm rows
-  u64 *dkey = drow + kNmId * kWave;         // [kNmId] their inner key masks
+  u64 *rows = lst + kNmList + kNmLive / 2;  // [kNmRows][64 APL] live outer-remove rows
+  u64 *drow = rows + kNmRows * kWave * APL; // [kNmId][64 APL] inner deferred rm rows
+  u64 *dkey = drow + kNmId * kWave * APL;   // [kNmId] their inner key masks
   uint8_t *nv = reinterpret_cast<uint8_t *>(dkey + kNmId);  // [K2] MVReg slots held per inner key
-  const bool al = (unsigned long long)lane < A;
-  auto ld = [&](const u64 *row) -> u64 { return al ? row[lane] : 0ull; };
-  auto st = [&](u64 *row, u64 x) {
-    if (al) row[lane] = x;
-  };
+  const Vc Z = nv_zero<APL>();
+  auto ld = [&](const u64 *row) -> Vc { return nv_ld<APL>(row, lane, A); };
+  auto st = [&](u64 *row, const Vc &x) { nv_st<APL>(row, x, lane, A); };
 
   // ---- the outer removes naming key k, in replica order (map_orswot.hip's walk)
   const unsigned long long d0 = p.def_off ? p.def_off[g] : 0, d1 = p.def_off ? p.def_off[g + 1] : 0;
@@ -128,32 +232,32 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
   advance();
   bool full = false, dfull = false, vfull = false;
   int na = 0;
-  auto live_row = [&](int i) -> u64 {
-    return i < kNmRows ? rows[(unsigned long long)i * kWave + lane] : ld(p.def_clock + (d0 + live[i]) * A);
+  auto live_row = [&](int i) -> Vc {
+    return i < kNmRows ? nv_lr<APL>(rows, i, lane) : ld(p.def_clock + (d0 + live[i]) * A);
   };
-  auto put_row = [&](int i, u64 x) {
-    if (i < kNmRows) rows[(unsigned long long)i * kWave + lane] = x;
+  auto put_row = [&](int i, const Vc &x) {
+    if (i < kNmRows) nv_lw<APL>(rows, i, x, lane);
   };
-  u64 rk = 0, T = ~0ull;
+  Vc rk = Z, T = nv_fill<APL>(~0ull);
 
   // ---- the key's state: outer C, e; the inner Map's clock ic (registers), rows in the output
-  u64 C = 0, e = 0, ic = 0;
+  Vc C = Z, e = Z, ic = Z;
   int nd = 0;  // inner deferred removes held (uniform)
   // (generic pointers: the LDS copy when it fits, else the key's own output rows)
   u64 *const iec_o = p.xs_state ? xst : p.o_iec + gk * K2 * A;
   u64 *const ivc_o = p.xs_state ? xst + K2 * A : p.o_ivc + gk * K2 * kNmVs * A;
   u64 *const ivv_o = p.xs_state ? xst + K2 * A + K2 * kNmVs * A : p.o_ivv + gk * K2 * kNmVs;
   for (unsigned long long j = 0; j < K2; ++j) {
-    st(iec_o + j * A, 0);
+    st(iec_o + j * A, Z);
     if (lane == 0) nv[j] = 0;
   }
 
   // MVReg::forget (mvreg.rs:88-104) of inner key j's slots by x, compacted in order
-  auto vals_forget = [&](unsigned long long j, u64 x) {
+  auto vals_forget = [&](unsigned long long j, const Vc &x) {
     const int n = __builtin_amdgcn_readfirstlane((int)nv[j]);
     int o = 0;
     for (int s = 0; s < n; ++s) {
-      const u64 c = nm_fg(ld(ivc_o + (j * kNmVs + s) * A), x);
+      const Vc c = nm_fg(ld(ivc_o + (j * kNmVs + s) * A), x);
       if (!nm_nz(c)) continue;
       const u64 v = ivv_o[j * kNmVs + s];
       st(ivc_o + (j * kNmVs + o) * A, c);
@@ -163,14 +267,14 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
     if (lane == 0) nv[j] = (uint8_t)o;
   };
   // inner apply_keyset_rm's forget (map.rs:320-333): the keys' entry clocks, their values while they stay
-  auto forget_keys = [&](u64 rm, u64 km) {
+  auto forget_keys = [&](const Vc &rm, u64 km) {
     while (km) {
       const unsigned long long j = (unsigned long long)__builtin_ctzll(km);
       km &= km - 1;
       if (j >= K2) break;
-      const u64 ej = ld(iec_o + j * A);
+      const Vc ej = ld(iec_o + j * A);
       if (!nm_nz(ej)) continue;
-      const u64 ej2 = nm_fg(ej, rm);
+      const Vc ej2 = nm_fg(ej, rm);
       st(iec_o + j * A, ej2);
       if (!nm_nz(ej2)) {
         if (lane == 0) nv[j] = 0;
@@ -179,16 +283,16 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
       }
     }
   };
-  auto id_add = [&](u64 rm, u64 km) {  // deferred.entry(clock).or_default().append(keys) (map.rs:341-342)
+  auto id_add = [&](const Vc &rm, u64 km) {  // deferred.entry(clock).or_default().append(keys) (map.rs:341-342)
     for (int i = 0; i < nd; ++i) {
-      if (nm_eq(drow[(unsigned long long)i * kWave + lane], rm)) {
+      if (nm_eq(nv_lr<APL>(drow, i, lane), rm)) {
         const u64 mm = dkey[i] | km;
         if (lane == 0) dkey[i] = mm;
         return;
       }
     }
     if (nd < kNmId) {
-      drow[(unsigned long long)nd * kWave + lane] = rm;
+      nv_lw<APL>(drow, nd, rm, lane);
       if (lane == 0) dkey[nd] = km;
       ++nd;
     } else {
@@ -196,12 +300,12 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
     }
   };
   // the inner Map's Causal::forget (map.rs:85-114)
-  auto inner_forget = [&](u64 x) {
+  auto inner_forget = [&](const Vc &x) {
     if (!nm_nz(x)) return;  // (forget by the empty clock is the identity)
     for (unsigned long long j = 0; j < K2; ++j) {
-      const u64 ej = ld(iec_o + j * A);
+      const Vc ej = ld(iec_o + j * A);
       if (!nm_nz(ej)) continue;
-      const u64 ej2 = nm_fg(ej, x);
+      const Vc ej2 = nm_fg(ej, x);
       st(iec_o + j * A, ej2);
       if (!nm_nz(ej2)) {
         if (lane == 0) nv[j] = 0;
@@ -211,17 +315,17 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
     }
     int o = 0;
     for (int i = 0; i < nd; ++i) {
-      const u64 r2 = nm_fg(drow[(unsigned long long)i * kWave + lane], x);
+      const Vc r2 = nm_fg(nv_lr<APL>(drow, i, lane), x);
       const u64 ki = dkey[i];
       if (!nm_nz(r2)) continue;
       int jj = 0;
       for (; jj < o; ++jj)  // equal to a kept one: the later keys at the earlier place (collect())
-        if (nm_eq(drow[(unsigned long long)jj * kWave + lane], r2)) break;
+        if (nm_eq(nv_lr<APL>(drow, jj, lane), r2)) break;
       if (jj < o) {
         if (lane == 0) dkey[jj] = ki;
         continue;
       }
-      drow[(unsigned long long)o * kWave + lane] = r2;
+      nv_lw<APL>(drow, o, r2, lane);
       if (lane == 0) dkey[o] = ki;
       ++o;
     }
@@ -258,17 +362,17 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
   };
 
   // the replica's inner Map as the key's value (map.rs:193-208): clock, entries, slots, deferred
-  auto inner_load = [&](unsigned long long r, u64 ic2) {
+  auto inner_load = [&](unsigned long long r, const Vc &ic2) {
     ic = ic2;
     const Rin rn = rin(r);
     const u64 *ri = rn.iec, *rc = rn.ivc, *rv = rn.ivv;
     for (unsigned long long j = 0; j < K2; ++j) {
-      const u64 ej = ld(ri + j * A);
+      const Vc ej = ld(ri + j * A);
       st(iec_o + j * A, ej);
       int o = 0;
       if (nm_nz(ej)) {
         for (unsigned long long s = 0; s < V; ++s) {
-          const u64 c = ld(rc + (j * V + s) * A);
+          const Vc c = ld(rc + (j * V + s) * A);
           if (!nm_nz(c)) continue;
           if (o < kNmVs) {
             st(ivc_o + (j * kNmVs + o) * A, c);
@@ -288,44 +392,45 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
   };
 
   // the inner Map::merge (map.rs:140-220) of replica r's inner Map (clock ic2) into the state
-  auto inner_merge = [&](unsigned long long r, u64 ic2) {
+  auto inner_merge = [&](unsigned long long r, const Vc &ic2) {
     const Rin rn = rin(r);
     const u64 *ri = rn.iec, *rc = rn.ivc, *rv = rn.ivv;
     for (unsigned long long j = 0; j < K2; ++j) {
-      const u64 ej = ld(iec_o + j * A), e2j = ld(ri + j * A);
+      const Vc ej = ld(iec_o + j * A), e2j = ld(ri + j * A);
       const bool q1 = nm_nz(ej), q2 = nm_nz(e2j);
       if (!q1 && !q2) continue;
-      const u64 enj = ej == e2j ? ej : nm_max(nm_fg(e2j, ic), nm_fg(ej, ic2));
+      const Vc enj = nm_sel_eq(ej, e2j, nm_max(nm_fg(e2j, ic), nm_fg(ej, ic2)));
       if (!nm_nz(enj)) {  // dropped (or not added): no value merge
         if (q1) {
-          st(iec_o + j * A, 0);
+          st(iec_o + j * A, Z);
           if (lane == 0) nv[j] = 0;
         }
         continue;
       }
-      const u64 xj = nm_fg(q1 ? (q2 ? nm_max(ej, e2j) : ic2) : ic, enj);
+      const Vc xj = nm_fg(q1 ? (q2 ? nm_max(ej, e2j) : ic2) : ic, enj);
       // the slots: ours (Vec order), then the replica's (MVReg::merge, mvreg.rs:112-128), forgotten by xj
       // (every register array is indexed by unrolled constants only: the replica's slots keep their
       // own positions with a validity mask m2 instead of being compacted by a running count, which
       // made the compiler spill the arrays to scratch)
-      u64 cs[kNmVs], co[kNmVin], vs[kNmVs], vo[kNmVin];
+      Vc cs[kNmVs], co[kNmVin];
+      u64 vs[kNmVs], vo[kNmVin];
       const int n1 = q1 ? __builtin_amdgcn_readfirstlane((int)nv[j]) : 0;
       unsigned m2 = 0;
 #pragma unroll
       for (int s = 0; s < kNmVs; ++s) {
-        cs[s] = s < n1 ? ld(ivc_o + (j * kNmVs + s) * A) : 0;
+        cs[s] = s < n1 ? ld(ivc_o + (j * kNmVs + s) * A) : Z;
         vs[s] = s < n1 ? ivv_o[j * kNmVs + s] : 0;
       }
 #pragma unroll
       for (int s = 0; s < kNmVin; ++s) {
-        co[s] = 0;
+        co[s] = Z;
         vo[s] = 0;
       }
       if (q2) {
 #pragma unroll
         for (int s = 0; s < kNmVin; ++s) {
           if ((unsigned long long)s < V) {
-            const u64 c = ld(rc + (j * V + s) * A);
+            const Vc c = ld(rc + (j * V + s) * A);
             if (nm_nz(c)) {  // (an empty slot is no value)
               co[s] = c;
               vo[s] = rv[j * V + s];
@@ -365,7 +470,7 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
 #pragma unroll
       for (int s = 0; s < kNmVs; ++s) {
         if (!((keep1 >> s) & 1u)) continue;
-        const u64 c = nm_fg(cs[s], xj);
+        const Vc c = nm_fg(cs[s], xj);
         if (!nm_nz(c)) continue;
         st(ivc_o + (j * kNmVs + o) * A, c);  // (the slots were read into registers above)
         ivv_o[j * kNmVs + o] = vs[s];
@@ -374,7 +479,7 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
 #pragma unroll
       for (int t = 0; t < kNmVin; ++t) {
         if (!((keep2 >> t) & 1u)) continue;
-        const u64 c = nm_fg(co[t], xj);
+        const Vc c = nm_fg(co[t], xj);
         if (!nm_nz(c)) continue;
         if (o < kNmVs) {
           st(ivc_o + (j * kNmVs + o) * A, c);
@@ -391,19 +496,21 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
     u64 lo, hi;
     rin_id(r, lo, hi);
     for (u64 d = lo; d < hi; ++d) {
-      const u64 rm = ld(p.id_clock + d * A), km = p.id_keys[d];
+      const Vc rm = ld(p.id_clock + d * A);
+      const u64 km = p.id_keys[d];
       forget_keys(rm, km);
-      if (__ballot(rm > ic)) id_add(rm, km);
+      if (nm_gt_any(rm, ic)) id_add(rm, km);
     }
     ic = nm_max(ic, ic2);  // (:217)
     // apply_deferred (:219, :311-316): every held remove forgets its keys again, stays iff !(rm <= ic)
     int o = 0;
     for (int i = 0; i < nd; ++i) {
-      const u64 rm = drow[(unsigned long long)i * kWave + lane], km = dkey[i];
+      const Vc rm = nv_lr<APL>(drow, i, lane);
+      const u64 km = dkey[i];
       forget_keys(rm, km);
-      if (__ballot(rm > ic)) {
+      if (nm_gt_any(rm, ic)) {
         if (o != i) {
-          drow[(unsigned long long)o * kWave + lane] = rm;
+          nv_lw<APL>(drow, o, rm, lane);
           if (lane == 0) dkey[o] = km;
         }
         ++o;
@@ -413,12 +520,12 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
   };
 
   // ---- one outer replica step
-  auto step = [&](unsigned long long r, u64 c2, u64 e2, u64 ic2) {
+  auto step = [&](unsigned long long r, const Vc &c2, const Vc &e2, const Vc &ic2) __attribute__((always_inline)) {
     const bool p1 = nm_nz(e), p2 = nm_nz(e2);
-    const u64 en = e == e2 ? e : nm_max(nm_fg(e2, C), nm_fg(e, c2));
+    const Vc en = nm_sel_eq(e, e2, nm_max(nm_fg(e2, C), nm_fg(e, c2)));
     const bool stays = nm_nz(en);
     if (stays && (p1 || p2)) {
-      const u64 X = nm_fg(p1 ? (p2 ? nm_max(e, e2) : c2) : C, en);
+      const Vc X = nm_fg(p1 ? (p2 ? nm_max(e, e2) : c2) : C, en);
       if (p1 && p2) inner_merge(r, ic2);  // our_entry.val.merge(entry.val) (map.rs:183)
       else if (p2) inner_load(r, ic2);    // the replica's entry (:193-208)
       inner_forget(X);
@@ -426,12 +533,12 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
     e = en;
     // the outer removes: replica r's own naming k (apply_keyset_rm) and the live ones (apply_deferred)
     bool chg = false;
-    u64 f = rk;
+    Vc f = rk;
     const unsigned r32 = (unsigned)r;
     if (nxt <= r32) {
       do {
         const unsigned idx = (unsigned)lst[li];
-        const u64 rm = ld(p.def_clock + (d0 + idx) * A);
+        const Vc rm = ld(p.def_clock + (d0 + idx) * A);
         f = nm_max(f, rm);
         if (na < kNmLive) {
           if (lane == 0) live[na] = idx;
@@ -450,15 +557,22 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
       if (nm_nz(e)) inner_forget(f);  // entry.val.forget only while the entry stays (map.rs:321-330)
     }
     C = nm_max(C, c2);
-    if (na > 0 && (chg || __ballot(C >= T))) {  // outer live set re-test (witness thresholds)
+    if (na > 0 && (chg || nm_ge_any(C, T))) {  // outer live set re-test (witness thresholds)
       bool changed = chg;
-      T = ~0ull;
+      T = nv_fill<APL>(~0ull);
       for (int i = 0; i < na;) {
-        const u64 rm = live_row(i);
-        const u64 m = __ballot(rm > C);
-        if (m) {
-          const int wl = __builtin_ctzll(m);
-          T = lane == wl && rm < T ? rm : T;
+        const Vc rm = live_row(i);
+        bool held = false;  // the first actor with rm > C (the witness) holds the remove's threshold
+#pragma unroll
+        for (int j = 0; j < APL; ++j) {
+          const u64 m = __ballot(rm.w[j] > C.w[j]);
+          if (!held && m) {
+            const int wl = __builtin_ctzll(m);
+            T.w[j] = lane == wl && rm.w[j] < T.w[j] ? rm.w[j] : T.w[j];
+            held = true;
+          }
+        }
+        if (held) {
           ++i;
           continue;
         }
@@ -472,7 +586,7 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
         --na;
       }
       if (changed) {
-        rk = 0;
+        rk = Z;
         for (int i = 0; i < na; ++i) rk = nm_max(rk, live_row(i));
       }
     }
@@ -481,7 +595,7 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
   // ---- replica rows (c2, e2, ic2) through a register ring, DEPTH steps ahead
   constexpr int DEPTH = 4;
   const u64 *pc = p.clock + g * R * A, *pe = p.ec + (g * R * K + k) * A, *pi = p.ic + (g * R * K + k) * A;
-  u64 c2r[DEPTH], e2r[DEPTH], i2r[DEPTH];
+  Vc c2r[DEPTH], e2r[DEPTH], i2r[DEPTH];
   auto load_step = [&](int s, unsigned long long r) {
     const unsigned long long rr = r < R ? r : R - 1;
     c2r[s] = ld(pc + rr * A);
@@ -490,28 +604,36 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
   };
 #pragma unroll
   for (int s = 0; s < DEPTH; ++s) load_step(s, (unsigned long long)s);
+  // (the DEPTH ring slots written out with constant indices: an unroll pragma over the inlined step
+  // is refused as too large at APL > 1, which left the ring in scratch)
+  auto ring = [&](auto sc, unsigned long long r0) __attribute__((always_inline)) -> bool {
+    constexpr int s = decltype(sc)::value;
+    const unsigned long long r = r0 + s;
+    if (r >= R) return false;
+    const Vc c2 = c2r[s], e2 = e2r[s], i2 = i2r[s];
+    load_step(s, r + DEPTH);
+    step(r, c2, e2, i2);
+    return true;
+  };
+  static_assert(DEPTH == 4, "the ring below is written for 4 slots");
   for (unsigned long long r0 = 0; r0 < R; r0 += DEPTH) {
-#pragma unroll
-    for (int s = 0; s < DEPTH; ++s) {
-      const unsigned long long r = r0 + s;
-      if (r >= R) break;
-      const u64 c2 = c2r[s], e2 = e2r[s], i2 = i2r[s];
-      load_step(s, r + DEPTH);
-      step(r, c2, e2, i2);
-    }
+    if (!ring(std::integral_constant<int, 0>{}, r0)) break;
+    if (!ring(std::integral_constant<int, 1>{}, r0)) break;
+    if (!ring(std::integral_constant<int, 2>{}, r0)) break;
+    if (!ring(std::integral_constant<int, 3>{}, r0)) break;
   }
 
   // ---- egress: the key's entry (an empty entry clock: absent, inner rows 0), the group's clock
   const bool pf = nm_nz(e);
   st(p.o_ec + gk * A, e);
-  st(p.o_ic + gk * A, pf ? ic : 0ull);
+  st(p.o_ic + gk * A, pf ? ic : Z);
   u64 *const oiec = p.o_iec + gk * K2 * A, *const oivc = p.o_ivc + gk * K2 * kNmVs * A;
   u64 *const oivv = p.o_ivv + gk * K2 * kNmVs;
   for (unsigned long long j = 0; j < K2; ++j) {
     const int n = pf ? __builtin_amdgcn_readfirstlane((int)nv[j]) : 0;
-    st(oiec + j * A, pf ? ld(iec_o + j * A) : 0ull);  // (the same word when the state is the output)
+    st(oiec + j * A, pf ? ld(iec_o + j * A) : Z);  // (the same word when the state is the output)
     for (int s = 0; s < kNmVs; ++s) {  // the held slots, then zeros
-      const u64 c = s < n ? ld(ivc_o + (j * kNmVs + s) * A) : 0ull;
+      const Vc c = s < n ? ld(ivc_o + (j * kNmVs + s) * A) : Z;
       const u64 v = s < n ? ivv_o[j * kNmVs + s] : 0ull;
       st(oivc + (j * kNmVs + s) * A, c);
       oivv[j * kNmVs + s] = v;
@@ -521,7 +643,7 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
   if (k == 0) st(p.o_clock + g * A, C);
   const int no = pf ? nd : 0;
   for (int i = 0; i < no; ++i) {
-    st(p.o_id_clock + (gk * kNmId + i) * A, drow[(unsigned long long)i * kWave + lane]);
+    st(p.o_id_clock + (gk * kNmId + i) * A, nv_lr<APL>(drow, i, lane));
     if (lane == 0) p.o_id_keys[gk * kNmId + i] = dkey[i];
   }
   if (lane == 0) p.o_id_n[gk] = (unsigned)no;
@@ -543,8 +665,9 @@ __global__ void map_nested_id_check_kernel(const u64 *off, unsigned long long n,
   }
 }
 
-static size_t nm_lds() {
-  return (size_t)kNmWaves * (kNmList * 8 + kNmLive * 4 + kNmRows * kWave * 8 + kNmId * kWave * 8 + kNmId * 8 + kNmK2);
+// LDS bytes per key wave beyond the optional state / staging rows
+static size_t nm_lds(int apl) {
+  return kNmList * 8 + kNmLive * 4 + kNmRows * kWave * 8 * apl + kNmId * kWave * 8 * apl + kNmId * 8 + kNmK2;
 }
 
 }  // namespace crdt
@@ -557,7 +680,7 @@ extern "C" int crdt_map_nested_lub_many(crdt_ctx *ctx, const crdt_map_nested_bat
   if (!in || !out) return fail(ctx, CRDT_EINVAL, "map_nested_lub_many: NULL batch/out");
   const size_t G = in->G, R = in->R, K = in->K, K2 = in->K2, V = in->V, A = in->A;
   if (G == 0 || K == 0 || A == 0) return CRDT_OK;
-  if (A > (size_t)kWave) return fail(ctx, CRDT_EUNSUPPORTED, "map_nested_lub_many: A = %zu > %d", A, kWave);
+  if (A > 4 * (size_t)kWave) return fail(ctx, CRDT_EUNSUPPORTED, "map_nested_lub_many: A = %zu > %d", A, 4 * kWave);
   if (K2 > (size_t)kNmK2) return fail(ctx, CRDT_EUNSUPPORTED, "map_nested_lub_many: K2 = %zu > %d", K2, kNmK2);
   if (V > (size_t)kNmVin) return fail(ctx, CRDT_EUNSUPPORTED, "map_nested_lub_many: V = %zu > %d", V, kNmVin);
   if (!out->clock || !out->ec || !out->ic || (K2 && (!out->iec || !out->ivc || !out->ivv || !out->nval)) ||
@@ -614,26 +737,37 @@ extern "C" int crdt_map_nested_lub_many(crdt_ctx *ctx, const crdt_map_nested_bat
     // block fits (up to 160 KiB when one block per CU already gives every key a SIMD of its own,
     // else 80 KiB so that two blocks share a CU as without them)
     p.xs_state = p.xs_stage = 0;
-    size_t lds = nm_lds();
+    const int apl = A <= (size_t)kWave ? 1 : (A <= 2 * (size_t)kWave ? 2 : 4);  // actor words per lane
+    const void *kfn = apl == 1 ? reinterpret_cast<const void *>(&map_nested_fold_kernel<1>)
+                      : apl == 2 ? reinterpret_cast<const void *>(&map_nested_fold_kernel<2>)
+                                 : reinterpret_cast<const void *>(&map_nested_fold_kernel<4>);
+    // waves per workgroup: 4, fewer where the wide rows would pass 64 KiB (APL 2: 2 x 27 KiB, 4: 51 KiB)
+    const unsigned wpb = apl == 1 ? kNmWaves : (apl == 2 ? 2 : 1);
+    p.wpb = wpb;
+    size_t lds = nm_lds(apl) * wpb;
     if (ctx->tune.map_nested_lds && K2 > 0) {
-      const size_t base = nm_lds() / kNmWaves, cap = G * K <= 4 * (size_t)ctx->cu_count ? 160 * 1024 : 80 * 1024;
+      const size_t base = nm_lds(apl), cap = G * K <= 4 * (size_t)ctx->cu_count ? 160 * 1024 : 80 * 1024;
       const size_t st_w = K2 * (1 + kNmVs) * A + K2 * kNmVs, sg_w = K2 * (1 + V) * A + K2 * V;
-      if ((base + st_w * 8) * kNmWaves <= cap) p.xs_state = st_w;
-      if ((base + (p.xs_state + sg_w) * 8) * kNmWaves <= cap) p.xs_stage = sg_w;
-      lds = (base + (p.xs_state + p.xs_stage) * 8) * kNmWaves;
+      if ((base + st_w * 8) * wpb <= cap) p.xs_state = st_w;
+      if ((base + (p.xs_state + sg_w) * 8) * wpb <= cap) p.xs_stage = sg_w;
+      lds = (base + (p.xs_state + p.xs_stage) * 8) * wpb;
       if (lds > 64 * 1024) {
-        const hipError_t ae = hipFuncSetAttribute(reinterpret_cast<const void *>(&map_nested_fold_kernel),
-                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        const hipError_t ae = hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (ae != hipSuccess) {
           (void)hipGetLastError();
           p.xs_state = p.xs_stage = 0;
-          lds = nm_lds();
+          lds = nm_lds(apl) * wpb;
         }
       }
     }
     timing_begin(ctx, "map_nested_fold");
-    const unsigned long long blocks = (G * K + kNmWaves - 1) / kNmWaves;
-    hipLaunchKernelGGL(map_nested_fold_kernel, dim3((unsigned)blocks), dim3(kNmWaves * kWave), lds, ctx->stream, p);
+    const unsigned long long blocks = (G * K + wpb - 1) / wpb;
+    if (apl == 1)
+      hipLaunchKernelGGL(map_nested_fold_kernel<1>, dim3((unsigned)blocks), dim3(wpb * kWave), lds, ctx->stream, p);
+    else if (apl == 2)
+      hipLaunchKernelGGL(map_nested_fold_kernel<2>, dim3((unsigned)blocks), dim3(wpb * kWave), lds, ctx->stream, p);
+    else
+      hipLaunchKernelGGL(map_nested_fold_kernel<4>, dim3((unsigned)blocks), dim3(wpb * kWave), lds, ctx->stream, p);
     const hipError_t he = hipGetLastError();
     timing_end(ctx);
     if (he != hipSuccess) return hip_fail(ctx, he, "map_nested_fold_kernel launch");

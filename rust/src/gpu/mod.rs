@@ -1437,8 +1437,9 @@ impl<K: Ord + Clone, M: Member, A: Actor> BatchCvRDT for Map<K, Orswot<M, A>, A>
     }
 }
 
-/// Limits of the nested Map fold (include/crdt_gpu.h: A <= 64, K2 <= 64, V <= 8 values per register).
-pub const MAP_NESTED_MAX_ACTORS: usize = 64;
+/// Limits of the nested Map fold (include/crdt_gpu.h: A <= 256 since round 6, K2 <= 64, V <= 8 values per
+/// register).
+pub const MAP_NESTED_MAX_ACTORS: usize = 256;
 pub const MAP_NESTED_MAX_INNER_KEYS: usize = 64;
 pub const MAP_NESTED_MAX_VALUES: usize = 8;
 

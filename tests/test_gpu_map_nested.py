@@ -120,8 +120,8 @@ def _intern(maps, extra=None, with_dicts=False):
 def gpu_fold(ctx, maps):
     """acc = Map::new(); for m in maps: acc.merge(m), every merge on the GPU (one nested_lub_many)."""
     dense, back, A, K, K2 = _intern(maps)
-    if A > 64 or K2 > 64:
-        pytest.skip("more than 64 actors / inner keys in one case")
+    if A > 256 or K2 > 64:
+        pytest.skip("more than 256 actors / 64 inner keys in one case")
     V = max([len(ie.val.vals) for m in dense for e in m.entries.values() for ie in e.val.entries.values()] + [1])
     d = O.nested_map_to_dense(dense, K, K2, A, V)
     D = d["def_row"].shape[0]
@@ -455,10 +455,55 @@ def test_prop_map_merge_laws_on_gpu(gm, seed):
     assert left == right  # associative
 
 
+def _wide_ops(rng, actors):
+    """One state's op list from many actors (each a quickcheck prim with its own u8 actor): applying the
+    concatenation is the merge of the actors' maps (op exchange, test/map.rs:526-550)."""
+    ops = []
+    for actor in actors:
+        _, o = _prim(rng, n_max=8)
+        # outer keys over the whole u8 range (few inner removes deferred per key: the fold holds 16), inner
+        # keys within the fold's 64
+        o = [(c, ic, (k * 37 + actor) % 256, ik % 32, v) for c, ic, k, ik, v in o]
+        ops.extend(build_ops(actor, o)[1])
+    return ops
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_prop_map_merge_laws_wide_actors_on_gpu(gm, seed):
+    """The merge laws of test/map.rs:524-827 on TMap states written by up to 256 distinct u8 actors (the
+    type's whole actor domain; round 6: the fold takes A <= 256, lane l holding actors l + 64 j): three
+    states from disjoint actor sets of 60-90 actors each, every merge on the GPU and equal to the
+    oracle's."""
+    rng = random.Random(1000 + seed)
+    pool = list(range(256))
+    rng.shuffle(pool)
+    n = [rng.randrange(60, 90) for _ in range(3)]
+    groups = [pool[:n[0]], pool[n[0]:n[0] + n[1]], pool[n[0] + n[1]:n[0] + n[1] + n[2]]]
+    ops1, ops2, ops3 = (_wide_ops(rng, g) for g in groups)
+    m1, m2, m3 = TMap(), TMap(), TMap()
+    apply_ops(m1, ops1)
+    apply_ops(m2, ops2)
+    apply_ops(m3, ops3)
+    mm = gm(m1, m2)
+    exp = m1.copy()
+    exp.merge(m2.copy())
+    assert canon(mm) == canon(exp)  # the oracle's merge (> 64 actors: the wide fold)
+    assert canon(gm(m1, m1.copy())) == canon(m1)  # idempotent
+    a = m1.copy()
+    apply_ops(a, ops2)
+    assert canon(a) == canon(mm)  # op exchange == merge
+    assert canon(gm(m2, m1)) == canon(mm)  # commutative
+    assert canon(gm(m2, mm)) == canon(mm)  # merge followed by merge
+    left = gm(gm(m1, m2), m3)
+    right = gm(m1, gm(m2, m3))
+    assert canon(left) == canon(right)  # associative
+
+
 # ---- op-replay folds over many replicas against the oracle's left fold -------------------------------
 @pytest.mark.parametrize("mode", ["", "nmlds=0"])
 @pytest.mark.parametrize("seed,R,K,K2,A", [(1, 30, 3, 4, 4), (2, 50, 5, 6, 5), (3, 40, 2, 3, 3),
-                                            (4, 70, 6, 8, 6), (5, 25, 4, 20, 8), (6, 40, 3, 64, 64)])
+                                            (4, 70, 6, 8, 6), (5, 25, 4, 20, 8), (6, 40, 3, 64, 64),
+                                            (7, 40, 3, 6, 100), (8, 24, 2, 5, 200), (9, 30, 2, 8, 256)])
 def test_map_nested_op_replay_fold(gpu_ctx, seed, R, K, K2, A, mode):
     """Both state placements: the key's inner Map and the staged replica rows in LDS (default, where
     they fit; at K2 = 64, A = 64 they do not) and the inner Map in the key's output rows."""
