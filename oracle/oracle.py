@@ -1523,11 +1523,12 @@ def map_orswot_objects(R: int, K: int, M: int, A: int, seed: int, steps: int = 3
 
 # ---- Map<K, Map<K2, MVReg<int>>> (the reference's own Map test type TMap, test/map.rs:10; round 5) ----
 def nested_map_to_dense(maps, K: int, K2: int, A: int, V: int):
-    """Ingest Map<int, Map<int, MVReg<int>>> objects (outer keys < K, inner keys < K2 <= 64, actors < A,
+    """Ingest Map<int, Map<int, MVReg<int>>> objects (outer keys < K, inner keys < K2 <= 256, actors < A,
     at most V values per register): clock (R, A), ec / ic (R, K, A) the outer entry / inner Map clocks,
     iec (R, K, K2, A), ivc (R, K, K2, V, A) / ivv (R, K, K2, V) the MVReg slots in Vec order, the inner
     deferred removes as a CSR over (replica, key) — id_off (R*K + 1), id_clock (Di, A), id_keys (Di,)
-    inner-key bitmasks — and the outer deferred pool (def_row, def_clock, def_keys)."""
+    inner-key bitmasks ((Di, ceil(K2/64)) words past K2 = 64) — and the outer deferred pool (def_row,
+    def_clock, def_keys)."""
     R = len(maps)
     clock = np.zeros((R, A), np.uint64)
     ec = np.zeros((R, K, A), np.uint64)
@@ -1559,7 +1560,7 @@ def nested_map_to_dense(maps, K: int, K2: int, A: int, V: int):
                         ivv[r, k, j, s] = x
                 for rm, keys in e.val.deferred.items():
                     idc.append(row(rm))
-                    idk.append(int(_bits(keys, 64)[0]))
+                    idk.append(_bits(keys, max(K2, 64)))
             id_off.append(len(idc))
         for rm, keys in m.deferred.items():
             def_row.append(r)
@@ -1568,7 +1569,9 @@ def nested_map_to_dense(maps, K: int, K2: int, A: int, V: int):
     D, Di = len(def_row), len(idc)
     Kw = (K + 63) // 64
     return dict(clock=clock, ec=ec, ic=ic, iec=iec, ivc=ivc, ivv=ivv, id_off=np.array(id_off, np.uint64),
-                id_clock=np.array(idc, np.uint64).reshape(Di, A), id_keys=np.array(idk, np.uint64),
+                id_clock=np.array(idc, np.uint64).reshape(Di, A),
+                id_keys=(np.array(idk, np.uint64).reshape(Di, max(K2, 64) // 64 if K2 <= 64 else (K2 + 63) // 64)
+                         if K2 > 64 else np.array([int(x[0]) for x in idk], np.uint64)),
                 def_row=np.array(def_row, np.uint64), def_clock=np.array(dcl, np.uint64).reshape(D, A),
                 def_keys=np.array(dk, np.uint64).reshape(D, Kw))
 

@@ -636,7 +636,7 @@ class MapNestedLub(NamedTuple):
     nval: torch.Tensor                # (G, K, K2) int32 slots used
     id_n: torch.Tensor                # (G, K) int32 inner deferred removes
     id_clock: torch.Tensor            # (G, K, 16, A)
-    id_keys: torch.Tensor             # (G, K, 16) inner key bitmasks
+    id_keys: torch.Tensor             # (G, K, 16) inner key bitmasks ((G, K, 16, K2w) past K2 = 64)
     flags: torch.Tensor               # (G,) int32
     def_keep: Optional[torch.Tensor]  # (D,) uint8
     def_keys: Optional[torch.Tensor]  # (D, Kw)
@@ -653,7 +653,8 @@ def nested_lub_many(clock: torch.Tensor, ec: torch.Tensor, ic: torch.Tensor, iec
     mvreg.rs:112-128) and forget (map.rs:85-114) as the value's.  clock (G,R,A) / (R,A); ec, ic
     (G,R,K,A); iec (G,R,K,K2,A); ivc (G,R,K,K2,V,A); ivv (G,R,K,K2,V), all contiguous; the inner
     deferred removes as a device CSR over (g, r, k): id_off (G*R*K + 1,) int64, id_clock (Di, A),
-    id_keys (Di,) inner-key bitmasks; the outer deferred pool as for lub_many (host def_off).
+    id_keys (Di,) inner-key bitmasks ((Di, K2w) words past K2 = 64; K2 <= 256, A <= 256); the outer
+    deferred pool as for lub_many (host def_off).
     check=True raises on flags (bit 1: def_row unsorted / out of range, bit 3: more than 256 live outer
     removes named one key, bit 4: more than 16 inner deferred removes, bit 5: id_off invalid, bit 6:
     more than 8 values on one inner key)."""
@@ -678,15 +679,17 @@ def nested_lub_many(clock: torch.Tensor, ec: torch.Tensor, ic: torch.Tensor, iec
     if id_off.dtype not in (torch.int64, torch.uint64):
         raise ValueError(f"map.nested_lub_many: id_off must be int64 / uint64 (got {id_off.dtype})")
     Di = int(id_clock.shape[0]) if id_clock is not None else 0
+    K2w = max(1, (K2 + 63) // 64)
     if Di > 0:
-        for t, nm, shape in ((id_clock, "id_clock", (Di, A)), (id_keys, "id_keys", (Di,))):
-            if t is None or not t.is_contiguous() or tuple(t.shape) != shape:
-                raise ValueError(f"map.nested_lub_many: {nm} must be a contiguous {shape} tensor")
+        for t, nm, shapes in ((id_clock, "id_clock", ((Di, A),)),
+                              (id_keys, "id_keys", ((Di,), (Di, 1)) if K2w == 1 else ((Di, K2w),))):
+            if t is None or not t.is_contiguous() or tuple(t.shape) not in shapes:
+                raise ValueError(f"map.nested_lub_many: {nm} must be a contiguous {shapes[0]} tensor")
             ctx.check_tensor(t, f"map.nested_lub_many({nm})")
     Kw = (K + 63) // 64 if _key_shard is None else (int(_key_shard[1]) + 63) // 64
     out = [torch.empty(sh, dtype=torch.int64, device=dev)
            for sh in ((G, A), (G, K, A), (G, K, A), (G, K, K2, A), (G, K, K2, NM_VS, A), (G, K, K2, NM_VS),
-                      (G, K, NM_ID, A), (G, K, NM_ID))]
+                      (G, K, NM_ID, A), (G, K, NM_ID) if K2w == 1 else (G, K, NM_ID, K2w))]
     nval = torch.empty((G, K, K2), dtype=torch.int32, device=dev)
     id_n = torch.empty((G, K), dtype=torch.int32, device=dev)
     flags = torch.empty(G, dtype=torch.int32, device=dev)

@@ -35,11 +35,12 @@ constexpr int kNmRows = 8;    // live outer-remove rows cached in LDS
 constexpr int kNmId = 16;     // inner deferred removes per key state (flags bit 4 past it)
 constexpr int kNmVs = 8;      // MVReg slots per inner key in the fold state (flags bit 6 past it)
 constexpr int kNmVin = 8;     // MVReg slots per inner key in the input
-constexpr int kNmK2 = 64;     // inner keys (key sets of inner removes: one u64 mask)
+constexpr int kNmK2 = 256;    // inner keys (round 6: 256 — key sets of inner removes as K2w <= 4 mask words)
+constexpr int kNmKw = kNmK2 / 64;
 
 struct NestedMapPlan {
   const u64 *clock, *ec, *ic, *iec, *ivc, *ivv;  // (G,R,A) (G,R,K,A) (G,R,K,A) (G,R,K,K2,A) (G,R,K,K2,V,A) (G,R,K,K2,V)
-  const u64 *id_off, *id_clock, *id_keys;        // inner deferred CSR over (g, r, k)
+  const u64 *id_off, *id_clock, *id_keys;        // inner deferred CSR over (g, r, k); id_keys [Di][K2w]
   unsigned long long Di;
   unsigned long long G, R, K, K2, V, A, Kw;
   const size_t *def_off;  // device copy (G+1), or null
@@ -54,6 +55,7 @@ struct NestedMapPlan {
   // then lives in the key's output rows, the replica is read from HBM where it is used)
   unsigned long long xs_state, xs_stage;
   unsigned wpb;  // key waves per workgroup (kNmWaves; fewer for the wide instances' LDS rows)
+  unsigned K2w;  // inner-key mask words, ceil(K2 / 64) (1 up to 64 inner keys: the round-5 layout)
 };
 
 // A clock across the wave: lane l holds actors l + 64 j, j < APL (A <= 64 APL; round 6: APL 2 and 4 take
@@ -165,6 +167,17 @@ __device__ __forceinline__ bool nm_eq(const NVc<APL> &x, const NVc<APL> &y) {
   return !__ballot(ne);
 }
 
+// an inner-key set (the same in every lane): words past K2w stay 0
+struct NKm {
+  u64 w[kNmKw];
+};
+__device__ __forceinline__ bool km_any(const NKm &k) {
+  u64 x = 0;
+#pragma unroll
+  for (int i = 0; i < kNmKw; ++i) x |= k.w[i];
+  return x != 0;
+}
+
 template <int APL>
 __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(NestedMapPlan p) {
   using Vc = NVc<APL>;
@@ -174,14 +187,32 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
   if (wv >= (int)p.wpb || gk >= p.G * p.K) return;  // (whole waves; nothing below synchronises the workgroup)
   const unsigned long long g = gk / p.K, k = gk % p.K, A = p.A, R = p.R, K = p.K, K2 = p.K2, V = p.V;
   constexpr unsigned long long WQ =
-      kNmList + kNmLive / 2 + kNmRows * kWave * APL + kNmId * kWave * APL + kNmId + kNmK2 / 8;
+      kNmList + kNmLive / 2 + kNmRows * kWave * APL + kNmId * kWave * APL + kNmId * kNmKw + kNmK2 / 8;
   u64 *lst = lds + (unsigned long long)wv * (WQ + p.xs_state + p.xs_stage);
   u64 *const xst = lst + WQ, *const xsg = xst + p.xs_state;  // (LDS state, staged replica)
   uint32_t *live = reinterpret_cast<uint32_t *>(lst + kNmList);
   u64 *rows = lst + kNmList + kNmLive / 2;  // [kNmRows][64 APL] live outer-remove rows
   u64 *drow = rows + kNmRows * kWave * APL; // [kNmId][64 APL] inner deferred rm rows
-  u64 *dkey = drow + kNmId * kWave * APL;   // [kNmId] their inner key masks
-  uint8_t *nv = reinterpret_cast<uint8_t *>(dkey + kNmId);  // [K2] MVReg slots held per inner key
+  u64 *dkey = drow + kNmId * kWave * APL;   // [kNmId][kNmKw] their inner key sets
+  uint8_t *nv = reinterpret_cast<uint8_t *>(dkey + kNmId * kNmKw);  // [K2] MVReg slots held per inner key
+  const unsigned K2w = p.K2w;
+  auto km_lr = [&](int i) -> NKm {  // held remove i's key set
+    NKm k;
+#pragma unroll
+    for (int x = 0; x < kNmKw; ++x) k.w[x] = dkey[i * kNmKw + x];
+    return k;
+  };
+  auto km_lw = [&](int i, const NKm &k) {
+    if (lane == 0)
+#pragma unroll
+      for (int x = 0; x < kNmKw; ++x) dkey[i * kNmKw + x] = k.w[x];
+  };
+  auto km_in = [&](unsigned long long d) -> NKm {  // input remove d's key set (id_keys [Di][K2w])
+    NKm k;
+#pragma unroll
+    for (int x = 0; x < kNmKw; ++x) k.w[x] = (unsigned)x < K2w ? p.id_keys[d * K2w + x] : 0ull;
+    return k;
+  };
   const Vc Z = nv_zero<APL>();
   auto ld = [&](const u64 *row) -> Vc { return nv_ld<APL>(row, lane, A); };
   auto st = [&](u64 *row, const Vc &x) { nv_st<APL>(row, x, lane, A); };
@@ -267,9 +298,12 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
     if (lane == 0) nv[j] = (uint8_t)o;
   };
   // inner apply_keyset_rm's forget (map.rs:320-333): the keys' entry clocks, their values while they stay
-  auto forget_keys = [&](const Vc &rm, u64 km) {
+  auto forget_keys = [&](const Vc &rm, const NKm &kset) {
+#pragma unroll
+    for (int x = 0; x < kNmKw; ++x) {
+    u64 km = kset.w[x];
     while (km) {
-      const unsigned long long j = (unsigned long long)__builtin_ctzll(km);
+      const unsigned long long j = 64ull * x + (unsigned long long)__builtin_ctzll(km);
       km &= km - 1;
       if (j >= K2) break;
       const Vc ej = ld(iec_o + j * A);
@@ -282,18 +316,21 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
         vals_forget(j, rm);
       }
     }
+    }
   };
-  auto id_add = [&](const Vc &rm, u64 km) {  // deferred.entry(clock).or_default().append(keys) (map.rs:341-342)
+  auto id_add = [&](const Vc &rm, const NKm &km) {  // deferred.entry(clock).or_default().append(keys) (map.rs:341-342)
     for (int i = 0; i < nd; ++i) {
       if (nm_eq(nv_lr<APL>(drow, i, lane), rm)) {
-        const u64 mm = dkey[i] | km;
-        if (lane == 0) dkey[i] = mm;
+        NKm mm = km_lr(i);
+#pragma unroll
+        for (int x = 0; x < kNmKw; ++x) mm.w[x] |= km.w[x];
+        km_lw(i, mm);
         return;
       }
     }
     if (nd < kNmId) {
       nv_lw<APL>(drow, nd, rm, lane);
-      if (lane == 0) dkey[nd] = km;
+      km_lw(nd, km);
       ++nd;
     } else {
       dfull = true;
@@ -316,17 +353,17 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
     int o = 0;
     for (int i = 0; i < nd; ++i) {
       const Vc r2 = nm_fg(nv_lr<APL>(drow, i, lane), x);
-      const u64 ki = dkey[i];
+      const NKm ki = km_lr(i);
       if (!nm_nz(r2)) continue;
       int jj = 0;
       for (; jj < o; ++jj)  // equal to a kept one: the later keys at the earlier place (collect())
         if (nm_eq(nv_lr<APL>(drow, jj, lane), r2)) break;
       if (jj < o) {
-        if (lane == 0) dkey[jj] = ki;
+        km_lw(jj, ki);
         continue;
       }
       nv_lw<APL>(drow, o, r2, lane);
-      if (lane == 0) dkey[o] = ki;
+      km_lw(o, ki);
       ++o;
     }
     nd = o;
@@ -388,7 +425,7 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
     nd = 0;
     u64 lo, hi;
     rin_id(r, lo, hi);
-    for (u64 d = lo; d < hi; ++d) id_add(ld(p.id_clock + d * A), p.id_keys[d]);
+    for (u64 d = lo; d < hi; ++d) id_add(ld(p.id_clock + d * A), km_in(d));
   };
 
   // the inner Map::merge (map.rs:140-220) of replica r's inner Map (clock ic2) into the state
@@ -497,7 +534,7 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
     rin_id(r, lo, hi);
     for (u64 d = lo; d < hi; ++d) {
       const Vc rm = ld(p.id_clock + d * A);
-      const u64 km = p.id_keys[d];
+      const NKm km = km_in(d);
       forget_keys(rm, km);
       if (nm_gt_any(rm, ic)) id_add(rm, km);
     }
@@ -506,12 +543,12 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
     int o = 0;
     for (int i = 0; i < nd; ++i) {
       const Vc rm = nv_lr<APL>(drow, i, lane);
-      const u64 km = dkey[i];
+      const NKm km = km_lr(i);
       forget_keys(rm, km);
       if (nm_gt_any(rm, ic)) {
         if (o != i) {
           nv_lw<APL>(drow, o, rm, lane);
-          if (lane == 0) dkey[o] = km;
+          km_lw(o, km);
         }
         ++o;
       }
@@ -644,7 +681,8 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
   const int no = pf ? nd : 0;
   for (int i = 0; i < no; ++i) {
     st(p.o_id_clock + (gk * kNmId + i) * A, nv_lr<APL>(drow, i, lane));
-    if (lane == 0) p.o_id_keys[gk * kNmId + i] = dkey[i];
+    if (lane == 0)
+      for (unsigned x = 0; x < K2w; ++x) p.o_id_keys[(gk * kNmId + i) * K2w + x] = dkey[i * kNmKw + x];
   }
   if (lane == 0) p.o_id_n[gk] = (unsigned)no;
   if ((bad || full || dfull || vfull) && lane == 0)
@@ -667,7 +705,7 @@ __global__ void map_nested_id_check_kernel(const u64 *off, unsigned long long n,
 
 // LDS bytes per key wave beyond the optional state / staging rows
 static size_t nm_lds(int apl) {
-  return kNmList * 8 + kNmLive * 4 + kNmRows * kWave * 8 * apl + kNmId * kWave * 8 * apl + kNmId * 8 + kNmK2;
+  return kNmList * 8 + kNmLive * 4 + kNmRows * kWave * 8 * apl + kNmId * kWave * 8 * apl + kNmId * kNmKw * 8 + kNmK2;
 }
 
 }  // namespace crdt
@@ -708,6 +746,7 @@ extern "C" int crdt_map_nested_lub_many(crdt_ctx *ctx, const crdt_map_nested_bat
                   (const u64 *)in->def_clock, (const u64 *)in->def_keys, (u64 *)out->clock, (u64 *)out->ec,
                   (u64 *)out->ic, (u64 *)out->iec, (u64 *)out->ivc, (u64 *)out->ivv, out->nval, out->id_n,
                   (u64 *)out->id_clock, (u64 *)out->id_keys, out->flags};
+  p.K2w = K2 > 64 ? (unsigned)((K2 + 63) / 64) : 1u;
   if (int rc = device_fill(ctx, out->flags, G * sizeof(unsigned), 0)) return rc;
   if (R == 0) {  // fold of nothing: Map::new()
     if (int rc = device_fill(ctx, out->clock, G * A * 8, 0)) return rc;

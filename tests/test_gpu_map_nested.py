@@ -120,8 +120,8 @@ def _intern(maps, extra=None, with_dicts=False):
 def gpu_fold(ctx, maps):
     """acc = Map::new(); for m in maps: acc.merge(m), every merge on the GPU (one nested_lub_many)."""
     dense, back, A, K, K2 = _intern(maps)
-    if A > 256 or K2 > 64:
-        pytest.skip("more than 256 actors / 64 inner keys in one case")
+    if A > 256 or K2 > 256:
+        pytest.skip("more than 256 actors / inner keys in one case")
     V = max([len(ie.val.vals) for m in dense for e in m.entries.values() for ie in e.val.entries.values()] + [1])
     d = O.nested_map_to_dense(dense, K, K2, A, V)
     D = d["def_row"].shape[0]
@@ -139,8 +139,7 @@ def gpu_fold(ctx, maps):
                 for rm, ks in cg.map.deferred_set(kw["def_clock"], res.def_keep, res.def_keys)]
     idn = res.id_n.cpu().numpy()
     idc, idk = to_host(res.id_clock), to_host(res.id_keys)
-    ideferred = {k: [(idc[k, i], O.bitmap_members(idk[k, i:i + 1])) for i in range(int(idn[k]))]
-                 for k in range(K)}
+    ideferred = {k: [(idc[k, i], O.bitmap_members(_kw(idk, k, i))) for i in range(int(idn[k]))] for k in range(K)}
     got = O.dense_to_nested_map(to_host(res.clock), to_host(res.ec), to_host(res.ic), to_host(res.iec),
                                 to_host(res.ivc), to_host(res.ivv), res.nval.cpu().numpy(), ideferred, dset)
     return back(got)
@@ -195,11 +194,16 @@ def nested_states(maps, K, K2, A, Dcap=16):
     return st, (to_dev(dcl), to_dev(dks), torch.from_numpy(cnt).cuda()), d
 
 
+def _kw(idk, k, i):
+    """Inner-key mask words of held remove i of key k: (K, 16) one word, (K, 16, K2w) past 64 keys."""
+    return idk[k, i:i + 1] if idk.ndim == 2 else idk[k, i]
+
+
 def decode_states(st, n, dfr):
     idn = st.id_n.cpu().numpy()[n]
     idc, idk = to_host(st.id_clock)[n], to_host(st.id_keys)[n]
     K = idn.shape[0]
-    idef = {k: [(idc[k, i], O.bitmap_members(idk[k, i:i + 1])) for i in range(int(idn[k]))] for k in range(K)}
+    idef = {k: [(idc[k, i], O.bitmap_members(_kw(idk, k, i))) for i in range(int(idn[k]))] for k in range(K)}
     return O.dense_to_nested_map(to_host(st.clock)[n], to_host(st.ec)[n], to_host(st.ic)[n], to_host(st.iec)[n],
                                  to_host(st.ivc)[n], to_host(st.ivv)[n], st.nval.cpu().numpy()[n], idef, dfr)
 
@@ -462,18 +466,18 @@ def _wide_ops(rng, actors):
     for actor in actors:
         _, o = _prim(rng, n_max=8)
         # outer keys over the whole u8 range (few inner removes deferred per key: the fold holds 16), inner
-        # keys within the fold's 64
-        o = [(c, ic, (k * 37 + actor) % 256, ik % 32, v) for c, ic, k, ik, v in o]
+        # keys too (round 6: up to 256 inner keys, their sets as 4 mask words)
+        o = [(c, ic, (k * 37 + actor) % 256, ik, v) for c, ic, k, ik, v in o]
         ops.extend(build_ops(actor, o)[1])
     return ops
 
 
 @pytest.mark.parametrize("seed", range(6))
 def test_prop_map_merge_laws_wide_actors_on_gpu(gm, seed):
-    """The merge laws of test/map.rs:524-827 on TMap states written by up to 256 distinct u8 actors (the
-    type's whole actor domain; round 6: the fold takes A <= 256, lane l holding actors l + 64 j): three
-    states from disjoint actor sets of 60-90 actors each, every merge on the GPU and equal to the
-    oracle's."""
+    """The merge laws of test/map.rs:524-827 on TMap states written by up to 256 distinct u8 actors over
+    inner keys from the whole u8 range (the type's whole domain; round 6: the fold takes A <= 256 with
+    lane l holding actors l + 64 j, and K2 <= 256 with inner key sets as 4 mask words): three states from
+    disjoint actor sets of 60-90 actors each, every merge on the GPU and equal to the oracle's."""
     rng = random.Random(1000 + seed)
     pool = list(range(256))
     rng.shuffle(pool)
@@ -503,7 +507,8 @@ def test_prop_map_merge_laws_wide_actors_on_gpu(gm, seed):
 @pytest.mark.parametrize("mode", ["", "nmlds=0"])
 @pytest.mark.parametrize("seed,R,K,K2,A", [(1, 30, 3, 4, 4), (2, 50, 5, 6, 5), (3, 40, 2, 3, 3),
                                             (4, 70, 6, 8, 6), (5, 25, 4, 20, 8), (6, 40, 3, 64, 64),
-                                            (7, 40, 3, 6, 100), (8, 24, 2, 5, 200), (9, 30, 2, 8, 256)])
+                                            (7, 40, 3, 6, 100), (8, 24, 2, 5, 200), (9, 30, 2, 8, 256),
+                                            (10, 30, 2, 100, 6), (11, 24, 2, 256, 5), (12, 20, 2, 130, 100)])
 def test_map_nested_op_replay_fold(gpu_ctx, seed, R, K, K2, A, mode):
     """Both state placements: the key's inner Map and the staged replica rows in LDS (default, where
     they fit; at K2 = 64, A = 64 they do not) and the inner Map in the key's output rows."""
