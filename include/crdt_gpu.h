@@ -818,26 +818,28 @@ int crdt_map_orswot_lub_many_sharded(crdt_ctx *ctx, const crdt_map_orswot_batch 
  *   inner Map clocks; iec [G][R][K][K2][A] inner entry clocks; ivc [G][R][K][K2][V][A] / ivv
  *   [G][R][K][K2][V] the inner MVReg slots in Vec order (an empty slot: clock row 0); the inner
  *   deferred removes as a device CSR over (g, r, k): id_off u64 [G*R*K + 1], id_clock [Di][A],
- *   id_keys [Di] inner-key bitmasks; the outer deferred removes as for the MVReg Map: def_off HOST
+ *   id_keys [Di][K2w] inner-key bitmasks (K2w = 1 up to K2 = 64, else ceil(K2/64) words, round 6);
+ *   the outer deferred removes as for the MVReg Map: def_off HOST
  *   (G+1), def_row, def_clock [D][A], def_keys [D][Kw].
  * Output per (g, k) (packed): clock [g*A + a], ec / ic [(g*K + k)*A + a], iec [((g*K + k)*K2 + j)*A +
  *   a], 8 slots per inner key ivc [(((g*K + k)*K2 + j)*8 + s)*A + a], ivv [((g*K + k)*K2 + j)*8 + s]
  *   with nval [(g*K + k)*K2 + j] used (unused slots 0), inner deferred id_n [g*K + k] (<= 16),
- *   id_clock [((g*K + k)*16 + i)*A + a], id_keys [(g*K + k)*16 + i]; flags[g]: bit 1 = def_row not
+ *   id_clock [((g*K + k)*16 + i)*A + a], id_keys [((g*K + k)*16 + i)*K2w + w]; flags[g]: bit 1 = def_row not
  *   non-decreasing or >= R, bit 3 = more than 256 live outer removes named one key, bit 4 = an inner
  *   Map held more than 16 deferred removes, bit 5 = id_off invalid (checked on the device: starts at
  *   0, non-decreasing, ends at Di; the fold never reads past Di), bit 6 = an inner key held more than
  *   8 values — results of the group unreliable; def_keep / def_keys as crdt_map_out.
  * Map::forget collects the inner deferred removes into a new map: two whose clocks become equal keep
  * one entry with the later one's keys (the oracle's dict order; the reference's is unspecified).
- * Limits: A <= 256 (round 6: lane l holds actors l + 64 j), K2 <= 64, V <= 8.  Device and host memory
+ * Limits: A <= 256 and K2 <= 256 (round 6: lane l holds actors l + 64 j; K2w key-set words), V <= 8.
+ * Device and host memory
  * (crdt_mem_kind). */
 typedef struct crdt_map_nested_batch {
   size_t G, R, K, K2, V, A;
   const uint64_t *clock, *ec, *ic, *iec, *ivc, *ivv;
   const uint64_t *id_off;   /* device, G*R*K + 1 */
   const uint64_t *id_clock; /* [Di][A] */
-  const uint64_t *id_keys;  /* [Di]    */
+  const uint64_t *id_keys;  /* [Di][K2w] */
   size_t Di;
   const size_t *def_off;    /* host, G+1 entries; NULL = no outer deferred removes */
   const uint32_t *def_row;
@@ -855,7 +857,7 @@ typedef struct crdt_map_nested_out {
   uint32_t *nval;     /* [G][K][K2]        */
   uint32_t *id_n;     /* [G][K]            */
   uint64_t *id_clock; /* [G][K][16][A]     */
-  uint64_t *id_keys;  /* [G][K][16]        */
+  uint64_t *id_keys;  /* [G][K][16][K2w]   */
   uint32_t *flags;    /* [G]               */
   uint8_t *def_keep;  /* [D]               */
   uint64_t *def_keys; /* [D][Kw]           */
@@ -873,14 +875,14 @@ int crdt_map_nested_lub_many_sharded(crdt_ctx *ctx, const crdt_map_nested_batch 
 
 /* Map<K, Map<K2, MVReg<u64>>> states in place (round 5), on the crdt_map_nested_lub_many output layout
  * with N states (packed; 8 MVReg slots per inner key in Vec order, nval used, the rest zero; 16 inner
- * deferred removes per key with one inner-key mask each):
+ * deferred removes per key with a K2w-word inner-key mask each, K2w = 1 up to K2 = 64):
  *   crdt_map_nested_apply_batch — CmRDT::apply (map.rs:119-137, apply_keyset_rm :318-348,
  *     apply_deferred :311-316) with the inner Map's apply one level down and MVReg::apply
  *     (mvreg.rs:130-166) innermost: state s applies ops [op_off[s], op_off[s+1]) in order; the outer
  *     deferred removes as crdt_map_counter_apply_batch (def_count[s] <= Dcap slots).  Ops: kind 0 =
  *     Op::Up { dot: (actor, counter), key, op } with ikind 0 = inner Op::Up { dot: (iactor, icounter),
  *     key: ikey, op: Put { clock: clk_pool[clk_row*A ..], val } } or 1 = inner Op::Rm { clock:
- *     clk_pool[clk_row*A ..], keyset: the inner-key mask ikeys }; kind 1 = Op::Rm { clock:
+ *     clk_pool[clk_row*A ..], keyset: the inner-key mask ikeys [n_ops][K2w] }; kind 1 = Op::Rm { clock:
  *     clk_pool[clk_row*A ..], keyset: keys[key_off[o] .. key_off[o+1]) } (key_off may be NULL when no
  *     op is an outer Rm).  status[s]: bit 0 = a deferred list (outer Dcap or an inner one's 16)
  *     exhausted, bit 1 = a malformed op skipped whole, bits 2-3 = invalid input (state untouched),
@@ -890,7 +892,7 @@ int crdt_map_nested_lub_many_sharded(crdt_ctx *ctx, const crdt_map_nested_batch 
  *     mvreg.rs:88-104, emptied values dropped, order kept —, deferred removes, clocks), an emptied
  *     entry dropped; the outer deferred pool and the map clock as crdt_map_forget_batch.  Inner removes
  *     whose clocks become equal keep one entry with the later one's keys (the fold's rule).
- * Limits: A <= 512, K2 <= 64; the outer Dcap is not bounded (its first min(Dcap, 16) slots in LDS during
+ * Limits: A <= 512, K2 <= 256 (round 6; a key bit past K2 makes the op malformed); the outer Dcap is not bounded (its first min(Dcap, 16) slots in LDS during
  * an apply stream, the rest used in place, round 6).  Device memory only. */
 typedef struct crdt_map_nested_states {
   size_t N, K, K2, A;
@@ -903,7 +905,7 @@ typedef struct crdt_map_nested_states {
   uint32_t *nval;     /* [N][K][K2]       */
   uint32_t *id_n;     /* [N][K]           */
   uint64_t *id_clock; /* [N][K][16][A]    */
-  uint64_t *id_keys;  /* [N][K][16]       */
+  uint64_t *id_keys;  /* [N][K][16][K2w]  */
 } crdt_map_nested_states;
 
 typedef struct crdt_map_nested_ops {
@@ -918,7 +920,7 @@ typedef struct crdt_map_nested_ops {
   const uint64_t *icounter;  /* [n_ops] inner Up */
   const uint32_t *ikey;      /* [n_ops] inner Up: the inner key */
   const uint64_t *val;       /* [n_ops] inner Up: the Put's value */
-  const uint64_t *ikeys;     /* [n_ops] inner Rm: inner-key mask */
+  const uint64_t *ikeys;     /* [n_ops][K2w] inner Rm: inner-key mask */
   const uint32_t *clk_row;   /* [n_ops] the Put clock / an rm clock: row of clk_pool */
   const uint64_t *clk_pool;  /* [n_clk_rows][A] */
   size_t n_clk_rows;
@@ -1164,8 +1166,8 @@ int crdt_map_orswot_egress(crdt_ctx *ctx, const crdt_map_orswot_states *states, 
                            uint8_t *bytes, size_t cap, size_t *total);
 /* Map<u32, Map<u32, MVReg<u64, u32>, u32>, u32> (the reference's own Map test type, test/map.rs:10)
  * frames <-> crdt_map_nested_states: the inner Map's clock ic, its entries by the sorted u32 inner-key
- * dictionary `ikeys` (K2 <= 64) with their MVReg values in slots 0 .. nval < 8 (Vec order), its
- * deferred removes in slots 0 .. id_n < 16 with one inner-key mask each; the outer Map's removes in
+ * dictionary `ikeys` (K2 <= 256, round 6) with their MVReg values in slots 0 .. nval < 8 (Vec order), its
+ * deferred removes in slots 0 .. id_n < 16 with a K2w-word inner-key mask each; the outer Map's removes in
  * per-state slots.  Status bit 4: a register past 8 values, an inner list past 16 or an outer one
  * past Dcap (the excess dropped). */
 int crdt_map_nested_ingest(crdt_ctx *ctx, const uint8_t *bytes, const uint64_t *frame_off, const uint32_t *actors,

@@ -1066,18 +1066,20 @@ class MapNestedOpBatch(NamedTuple):
     icounter: torch.Tensor  # (n_ops,) int64
     ikey: torch.Tensor      # (n_ops,) int32
     val: torch.Tensor       # (n_ops,) int64   inner Up: the Put's value
-    ikeys: torch.Tensor     # (n_ops,) int64   inner Rm: inner-key mask
+    ikeys: torch.Tensor     # (n_ops,) int64   inner Rm: inner-key mask ((n_ops, K2w) words past K2 = 64)
     clk_row: torch.Tensor   # (n_ops,) int32   the Put clock / an rm clock
     clk_pool: torch.Tensor  # (n_clk, A) int64
     key_off: torch.Tensor   # (n_ops+1,) int64 outer Rm keysets
     keys: torch.Tensor      # (n_keys,) int32
 
 
-def encode_nested_ops(streams, A: int, device) -> MapNestedOpBatch:
+def encode_nested_ops(streams, A: int, device, K2: int = 64) -> MapNestedOpBatch:
     """Host ingest of per-state op streams: ("put", actor, counter, key, iactor, icounter, ikey, clock, val)
     for Op::Up { dot, key, op: inner Op::Up { dot, key, op: Put { clock, val } } }, ("irm", actor,
     counter, key, clock, ikeys) for Op::Up with an inner Op::Rm { clock, keyset }, ("rm", clock, keys)
-    for Op::Rm (clocks: mapping actor -> counter or a row)."""
+    for Op::Rm (clocks: mapping actor -> counter or a row).  K2 > 64 (up to 256): the inner key sets
+    are (n_ops, ceil(K2/64)) mask words, the layout crdt_map_nested_apply_batch reads for such states."""
+    K2w = (K2 + 63) // 64 if K2 > 64 else 1
     def row(clk):
         r = np.zeros(A, dtype=np.uint64)
         if hasattr(clk, "items"):
@@ -1099,13 +1101,18 @@ def encode_nested_ops(streams, A: int, device) -> MapNestedOpBatch:
             elif op[0] == "irm":
                 _, a, c, k, rc, js = op
                 v.update(actor=a, counter=c, key=k, ikind=1, ikeys=sum(1 << int(j) for j in set(js)), clk_row=len(pool))
+                if v["ikeys"] >> (64 * K2w):
+                    raise ValueError(f"encode_nested_ops: an inner key past {64 * K2w} (K2 = {K2})")
             else:
                 _, rc, ks = op
                 v.update(kind=1, clk_row=len(pool))
                 keys.extend(int(x) for x in ks)
             pool.append(row(rc))
             for n, x in v.items():
-                f[n].append(int(x))
+                if n == "ikeys" and K2w > 1:
+                    f[n].extend((int(x) >> (64 * w)) & 0xFFFFFFFFFFFFFFFF for w in range(K2w))
+                else:
+                    f[n].append(int(x))
             key_off.append(len(keys))
         op_off.append(len(f["kind"]))
     i64 = lambda x: torch.tensor(np.asarray(x, dtype=np.uint64).view(np.int64), device=device)  # noqa: E731
@@ -1113,9 +1120,12 @@ def encode_nested_ops(streams, A: int, device) -> MapNestedOpBatch:
     u8 = lambda x: torch.tensor(x, dtype=torch.uint8, device=device)  # noqa: E731
     pool_t = (torch.from_numpy(np.stack(pool).view(np.int64)).to(device) if pool
               else torch.zeros((1, A), dtype=torch.int64, device=device))
+    ikeys = i64(f["ikeys"])
+    if K2w > 1:
+        ikeys = ikeys.reshape(-1, K2w)
     return MapNestedOpBatch(i64(op_off), u8(f["kind"]), i32(f["actor"]), i64(f["counter"]), i32(f["key"]),
                             u8(f["ikind"]), i32(f["iactor"]), i64(f["icounter"]), i32(f["ikey"]), i64(f["val"]),
-                            i64(f["ikeys"]), i32(f["clk_row"]), pool_t, i64(key_off), i32(keys))
+                            ikeys, i32(f["clk_row"]), pool_t, i64(key_off), i32(keys))
 
 
 def _nested_states(res, what):
@@ -1124,8 +1134,10 @@ def _nested_states(res, what):
         raise ValueError(f"{what}: a grouped result (clock (N, A)) expected")
     N, A = clock.shape
     K, K2 = res.iec.shape[1], res.iec.shape[2]
+    K2w = (K2 + 63) // 64 if K2 > 64 else 1  # inner key sets: K2w mask words past K2 = 64
     shapes = dict(ec=(N, K, A), ic=(N, K, A), iec=(N, K, K2, A), ivc=(N, K, K2, 8, A), ivv=(N, K, K2, 8),
-                  nval=(N, K, K2), id_n=(N, K), id_clock=(N, K, 16, A), id_keys=(N, K, 16))
+                  nval=(N, K, K2), id_n=(N, K), id_clock=(N, K, 16, A),
+                  id_keys=(N, K, 16) if K2w == 1 else (N, K, 16, K2w))
     for nm, shp in shapes.items():
         t = getattr(res, nm)
         if tuple(t.shape) != shp or not t.is_contiguous():
@@ -1143,7 +1155,9 @@ def nested_apply_batch(res: "MapNestedLub", def_clock: torch.Tensor, def_keys: t
                        def_count: torch.Tensor, ops: MapNestedOpBatch, ctx: Optional[Context] = None) -> torch.Tensor:
     """Apply every state's op stream in place (crdt_map_nested_apply_batch): `res` a nested_lub_many
     result with G = N states (its tensors are updated), the outer deferred slots def_clock (N, Dcap, A)
-    / def_keys (N, Dcap, ceil(K/64)) / def_count (N,) int32.  Returns the per-state status (N,) int32."""
+    / def_keys (N, Dcap, ceil(K/64)) / def_count (N,) int32.  Returns the per-state status (N,) int32.
+    K2 > 64 (up to 256): id_keys (N, K, 16, K2w) and ops.ikeys (n_ops, K2w) mask words
+    (encode_nested_ops(..., K2=K2))."""
     st, N, K, A = _nested_states(res, "map.nested_apply_batch")
     ctx = ctx or Context.default(res.clock.device.index)
     Kw = (K + 63) // 64
@@ -1158,8 +1172,15 @@ def nested_apply_batch(res: "MapNestedLub", def_clock: torch.Tensor, def_keys: t
     what = "map.nested_apply_batch"
     _check_op_fields(ctx, ops, n, (("kind", _U8), ("actor", _I32), ("counter", _I64), ("key", _I32),
                                    ("ikind", _U8), ("iactor", _I32), ("icounter", _I64), ("ikey", _I32),
-                                   ("val", _I64), ("ikeys", _I64), ("clk_row", _I32)), what)
+                                   ("val", _I64), ("clk_row", _I32)), what)
     _check_op_pools(ctx, ops, (("op_off", _I64), ("key_off", _I64), ("keys", _I32), ("clk_pool", _I64)), what)
+    K2 = res.iec.shape[2]
+    K2w = (K2 + 63) // 64 if K2 > 64 else 1
+    ctx.check_tensor(ops.ikeys, f"{what}(ikeys)", _I64)
+    ik_shape = (n,) if K2w == 1 else (n, K2w)
+    if tuple(ops.ikeys.shape) != ik_shape or not ops.ikeys.is_contiguous():
+        raise ValueError(f"{what}: ikeys must be a contiguous {ik_shape} tensor (K2 = {K2}), "
+                         f"got {tuple(ops.ikeys.shape)}")
     o = _abi.MapNestedOps()
     o.n_ops, o.op_off = n, ops.op_off.data_ptr()
     for nm in ("kind", "actor", "counter", "key", "ikind", "iactor", "icounter", "ikey", "val", "ikeys", "clk_row",

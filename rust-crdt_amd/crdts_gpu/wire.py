@@ -264,7 +264,7 @@ class MapNestedFrames(NamedTuple):
     nval: torch.Tensor       # (N, K, K2) int32
     id_n: torch.Tensor       # (N, K) int32
     id_clock: torch.Tensor   # (N, K, 16, A)
-    id_keys: torch.Tensor    # (N, K, 16)
+    id_keys: torch.Tensor    # (N, K, 16) ((N, K, 16, K2w) mask words past K2 = 64)
     def_clock: torch.Tensor  # (N, Dcap, A)
     def_keys: torch.Tensor   # (N, Dcap, Kw)
     def_count: torch.Tensor  # (N,) int32
@@ -394,8 +394,9 @@ def _nested_struct(ctx, st, what):
     from . import _abi
     N, K, A = _vmap_check(ctx, st, what)
     K2 = st.iec.shape[2]
+    K2w = (K2 + 63) // 64 if K2 > 64 else 1
     shapes = dict(ic=(N, K, A), iec=(N, K, K2, A), ivc=(N, K, K2, 8, A), ivv=(N, K, K2, 8), nval=(N, K, K2),
-                  id_n=(N, K), id_clock=(N, K, 16, A), id_keys=(N, K, 16))
+                  id_n=(N, K), id_clock=(N, K, 16, A), id_keys=(N, K, 16) if K2w == 1 else (N, K, 16, K2w))
     for nm, shp in shapes.items():
         if tuple(getattr(st, nm).shape) != shp:
             raise ValueError(f"{what}: {nm} must be {shp}")
@@ -409,7 +410,7 @@ def _nested_struct(ctx, st, what):
 def map_nested_ingest(data: torch.Tensor, frame_off: torch.Tensor, actors: torch.Tensor, keys: torch.Tensor,
                       ikeys: torch.Tensor, Dcap: int, ctx: Optional[Context] = None):
     """Map<u32, Map<u32, MVReg<u64>>> frames -> (MapNestedFrames, status (N,) int32); ikeys: sorted
-    u32 inner-key dictionary (int32 tensor, at most 64)."""
+    u32 inner-key dictionary (int32 tensor, at most 256; past 64 the inner key sets are K2w words)."""
     ctx = _ctx(data, ctx)
     N = _frames(ctx, data, frame_off, "wire.map_nested_ingest")
     A = _dict(ctx, actors, torch.int32, "wire.map_nested_ingest(actors)")
@@ -419,7 +420,8 @@ def map_nested_ingest(data: torch.Tensor, frame_off: torch.Tensor, actors: torch
     z = lambda *shape: torch.zeros(shape, dtype=torch.int64, device=dev)  # noqa: E731
     z32 = lambda *shape: torch.zeros(shape, dtype=torch.int32, device=dev)  # noqa: E731
     st = MapNestedFrames(z(N, A), z(N, K, A), z(N, K, A), z(N, K, K2, A), z(N, K, K2, 8, A), z(N, K, K2, 8),
-                         z32(N, K, K2), z32(N, K), z(N, K, 16, A), z(N, K, 16), z(N, Dcap, A),
+                         z32(N, K, K2), z32(N, K), z(N, K, 16, A),
+                         z(N, K, 16) if K2 <= 64 else z(N, K, 16, (K2 + 63) // 64), z(N, Dcap, A),
                          z(N, Dcap, (K + 63) // 64), z32(N))
     s, d = _nested_struct(ctx, st, "wire.map_nested_ingest")
     status = _status(N, dev)

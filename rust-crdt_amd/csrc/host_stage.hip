@@ -1147,7 +1147,8 @@ static int map_nested_lub_host_body(crdt_ctx *ctx, const crdt_map_nested_batch *
   if (int rc = ds.get(ctx, N * K2 * V, &ivv)) return rc;
   if (int rc = ds.get(ctx, N + 1, &io)) return rc;
   if (int rc = ds.get(ctx, Di * A, &idc)) return rc;
-  if (int rc = ds.get(ctx, Di, &idk)) return rc;
+  const size_t K2w = K2 > 64 ? (K2 + 63) / 64 : 1;  // inner key-set mask words
+  if (int rc = ds.get(ctx, Di * K2w, &idk)) return rc;
   if (int rc = ds.get(ctx, D, &dr)) return rc;
   if (int rc = ds.get(ctx, D * A, &dc)) return rc;
   if (int rc = ds.get(ctx, D * Kw, &dk)) return rc;
@@ -1160,7 +1161,7 @@ static int map_nested_lub_host_body(crdt_ctx *ctx, const crdt_map_nested_batch *
   if (int rc = ds.get(ctx, G * K * K2, &onv)) return rc;
   if (int rc = ds.get(ctx, G * K, &oidn)) return rc;
   if (int rc = ds.get(ctx, G * K * ID * A, &oidc)) return rc;
-  if (int rc = ds.get(ctx, G * K * ID, &oidk)) return rc;
+  if (int rc = ds.get(ctx, G * K * ID * K2w, &oidk)) return rc;
   if (int rc = ds.get(ctx, G, &of)) return rc;
   if (out->def_keep)
     if (int rc = ds.get(ctx, D, &okp)) return rc;
@@ -1175,7 +1176,7 @@ static int map_nested_lub_host_body(crdt_ctx *ctx, const crdt_map_nested_batch *
   // (id_off may be NULL when R == 0, as on the device path: the one offset word is then 0)
   if (int rc = in->id_off ? h2d_async(ctx, io, in->id_off, (N + 1) * 8) : zero_async(ctx, io, (N + 1) * 8)) return rc;
   if (int rc = h2d_async(ctx, idc, in->id_clock, Di * A * 8)) return rc;
-  if (int rc = h2d_async(ctx, idk, in->id_keys, Di * 8)) return rc;
+  if (int rc = h2d_async(ctx, idk, in->id_keys, Di * K2w * 8)) return rc;
   if (int rc = h2d_async(ctx, dr, in->def_row, D * 4)) return rc;
   if (int rc = h2d_async(ctx, dc, in->def_clock, D * A * 8)) return rc;
   if (int rc = h2d_async(ctx, dk, in->def_keys, D * Kw * 8)) return rc;
@@ -1206,7 +1207,7 @@ static int map_nested_lub_host_body(crdt_ctx *ctx, const crdt_map_nested_batch *
   if (int rc = d2h_async(ctx, out->nval, onv, G * K * K2 * 4)) return rc;
   if (int rc = d2h_async(ctx, out->id_n, oidn, G * K * 4)) return rc;
   if (int rc = d2h_async(ctx, out->id_clock, oidc, G * K * ID * A * 8)) return rc;
-  if (int rc = d2h_async(ctx, out->id_keys, oidk, G * K * ID * 8)) return rc;
+  if (int rc = d2h_async(ctx, out->id_keys, oidk, G * K * ID * K2w * 8)) return rc;
   if (int rc = d2h_async(ctx, out->flags, of, G * 4)) return rc;
   if (int rc = d2h_async(ctx, out->def_keep, okp, D)) return rc;
   if (int rc = d2h_async(ctx, out->def_keys, ok2, D * Kw * 8)) return rc;

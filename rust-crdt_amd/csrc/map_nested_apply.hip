@@ -33,6 +33,7 @@ struct NestedApplyPlan {
   u64 *clock, *ec, *ic, *iec, *ivc, *ivv, *id_clock, *id_keys;
   unsigned *nval, *id_n;
   unsigned long long N, K, K2, A, Kw, Dcap;
+  unsigned long long K2w;  // inner-key mask words per key set (1 up to K2 = 64: the round-5 layout)
   unsigned long long Dl;  // outer deferred slots held in LDS (<= Dcap); slots Dl .. Dcap-1 stay in place
   u64 *def_clock, *def_keys;
   unsigned *def_count;
@@ -76,13 +77,34 @@ __device__ __forceinline__ u64 rl64(u64 x, int i) {
   return ((u64)rl32((unsigned)(x >> 32), i) << 32) | rl32((unsigned)x, i);
 }
 
-template <int APL>
+constexpr int kNaKw = 4;  // inner-key mask words at most (K2 <= 256)
+
+// KW: mask words per key set at compile time, 1 (K2 <= 64: the round-5 code) or kNaKw (kw of them live)
+template <int APL, int KW = 1>
 struct NaKey {
-  u64 *ec, *ic, *iec, *ivc, *ivv, *idc, *idk;
+  u64 *ec, *ic, *iec, *ivc, *ivv, *idc, *idk;  // idk [kNaId][kwn()] inner key sets
   unsigned *nval, *idn;
   unsigned long long A, K2;
   int lane;
   mutable unsigned stb;  // status bits raised by these operations (the caller ORs them in)
+  unsigned kw_;          // mask words per key set (KW > 1)
+  __device__ __forceinline__ unsigned kwn() const { return KW == 1 ? 1u : kw_; }
+
+  // held remove i's key set in registers (words past kwn(): 0) and back
+  __device__ __forceinline__ void ks_ld(unsigned i, u64 (&k)[KW]) const {
+#pragma unroll
+    for (int x = 0; x < KW; ++x) k[x] = (unsigned)x < kwn() ? idk[(unsigned long long)i * kwn() + x] : 0ull;
+  }
+  __device__ __forceinline__ void ks_st(unsigned i, const u64 (&k)[KW]) const {
+#pragma unroll
+    for (int x = 0; x < KW; ++x)
+      if ((unsigned)x < kwn()) idk[(unsigned long long)i * kwn() + x] = k[x];
+  }
+  __device__ __forceinline__ void ks_zero(unsigned i) const {
+#pragma unroll
+    for (int x = 0; x < KW; ++x)
+      if ((unsigned)x < kwn()) idk[(unsigned long long)i * kwn() + x] = 0ull;
+  }
 
   __device__ __forceinline__ unsigned long long word(int j) const { return (unsigned long long)lane + 64ull * j; }
   __device__ __forceinline__ void ld(const u64 *row, u64 (&x)[APL]) const {
@@ -178,7 +200,8 @@ struct NaKey {
       ld(idc + (unsigned long long)i * A, x);
       fg(x, r);
       if (!nz(x)) continue;
-      const u64 ks = idk[i];
+      u64 ks[KW];
+      ks_ld(i, ks);
       unsigned jj = 0;
       for (; jj < o; ++jj) {  // equal to a kept one: the later keys at the earlier place
         u64 y[APL];
@@ -186,16 +209,16 @@ struct NaKey {
         if (eq(x, y)) break;
       }
       if (jj < o) {
-        idk[jj] = ks;
+        ks_st(jj, ks);
         continue;
       }
       st_(idc + (unsigned long long)o * A, x);
-      idk[o] = ks;
+      ks_st(o, ks);
       ++o;
     }
     for (unsigned i = o; i < n; ++i) {
       zero(idc + (unsigned long long)i * A);
-      idk[i] = 0;
+      ks_zero(i);
     }
     *idn = o;
     u64 c[APL];
@@ -210,22 +233,19 @@ struct NaKey {
     for (unsigned i = 0; i < n; ++i) {
       u64 r[APL];
       ld(idc + (unsigned long long)i * A, r);
-      const u64 ks = idk[i];
-      for (u64 b = ks; b;) {
-        const unsigned long long jk = (unsigned long long)__builtin_ctzll(b);
-        b &= b - 1;
-        if (jk < K2) inner_key_rm(jk, r);
-      }
+      u64 ks[KW];
+      ks_ld(i, ks);
+      keys_rm(ks, r);
       if (leq(r, c)) continue;  // seen: no longer deferred
       if (o != i) {
         st_(idc + (unsigned long long)o * A, r);
-        idk[o] = ks;
+        ks_st(o, ks);
       }
       ++o;
     }
     for (unsigned i = o; i < n; ++i) {
       zero(idc + (unsigned long long)i * A);
-      idk[i] = 0;
+      ks_zero(i);
     }
     *idn = o;
   }
@@ -288,13 +308,19 @@ struct NaKey {
       if ((unsigned)j == ia / 64 && (unsigned long long)lane == ia % 64 && c[j] < icnt) c[j] = icnt;
     inner_apply_deferred(c);
   }
+  // the inner keys of a key set forgotten by r (apply_keyset_rm's forget, map.rs:320-333)
+  __device__ void keys_rm(const u64 (&bits)[KW], const u64 (&r)[APL]) const {
+#pragma unroll
+    for (int x = 0; x < KW; ++x)
+      for (u64 b = bits[x]; b;) {
+        const unsigned long long jk = 64ull * x + (unsigned long long)__builtin_ctzll(b);
+        b &= b - 1;
+        if (jk < K2) inner_key_rm(jk, r);
+      }
+  }
   // the inner Map's Op::Rm { clock: r, keyset: bits }
-  __device__ void inner_rm(const u64 (&r)[APL], u64 bits) const {
-    for (u64 b = bits; b;) {
-      const unsigned long long jk = (unsigned long long)__builtin_ctzll(b);
-      b &= b - 1;
-      if (jk < K2) inner_key_rm(jk, r);
-    }
+  __device__ void inner_rm(const u64 (&r)[APL], const u64 (&bits)[KW]) const {
+    keys_rm(bits, r);
     u64 c[APL];
     ld(ic, c);
     if (leq(r, c)) return;
@@ -303,7 +329,11 @@ struct NaKey {
       u64 y[APL];
       ld(idc + (unsigned long long)i * A, y);
       if (eq(y, r)) {
-        idk[i] = idk[i] | bits;
+        u64 ks[KW];
+        ks_ld(i, ks);
+#pragma unroll
+        for (int x = 0; x < KW; ++x) ks[x] |= bits[x];
+        ks_st(i, ks);
         return;
       }
     }
@@ -312,7 +342,7 @@ struct NaKey {
       return;
     }
     st_(idc + (unsigned long long)n * A, r);
-    idk[n] = bits;
+    ks_st(n, bits);
     *idn = n + 1;
   }
   // drop the outer entry: every row of the key zero
@@ -324,7 +354,7 @@ struct NaKey {
     const unsigned n = *idn;
     for (unsigned i = 0; i < n; ++i) {
       zero(idc + (unsigned long long)i * A);
-      idk[i] = 0;
+      ks_zero(i);
     }
     *idn = 0;
   }
@@ -348,13 +378,13 @@ struct NaKey {
   }
 };
 
-template <int APL>
-__device__ __forceinline__ NaKey<APL> na_key(const NestedApplyPlan &p, unsigned long long s, unsigned long long k,
+template <int APL, int KW = 1>
+__device__ __forceinline__ NaKey<APL, KW> na_key(const NestedApplyPlan &p, unsigned long long s, unsigned long long k,
                                              int lane) {
   const unsigned long long sk = s * p.K + k, A = p.A, K2 = p.K2;
-  return NaKey<APL>{p.ec + sk * A, p.ic + sk * A, p.iec + sk * K2 * A, p.ivc + sk * K2 * kNaVs * A,
-                    p.ivv + sk * K2 * kNaVs, p.id_clock + sk * kNaId * A, p.id_keys + sk * kNaId,
-                    p.nval + sk * K2, p.id_n + sk, A, K2, lane, 0u};
+  return NaKey<APL, KW>{p.ec + sk * A, p.ic + sk * A, p.iec + sk * K2 * A, p.ivc + sk * K2 * kNaVs * A,
+                    p.ivv + sk * K2 * kNaVs, p.id_clock + sk * kNaId * A, p.id_keys + sk * kNaId * p.K2w,
+                    p.nval + sk * K2, p.id_n + sk, A, K2, lane, 0u, (unsigned)p.K2w};
 }
 
 // TIER false: every state, the Map's deferred list in the Dl LDS slots only; a state whose list
@@ -362,7 +392,7 @@ __device__ __forceinline__ NaKey<APL> na_key(const NestedApplyPlan &p, unsigned 
 // true: those states alone, slots past Dl used in place in the caller's slot arrays.  (One body with
 // the branch compiles the slot accesses to flat instructions and slows every state; see
 // csrc/map_counter_apply.hip.)
-template <int APL, int PASS>
+template <int APL, int PASS, int KW>
 __global__ __launch_bounds__(256) MNA_WPE_ATTR void map_nested_apply_kernel(NestedApplyPlan p) {
   extern __shared__ u64 lds[];
   const int lane = (int)(threadIdx.x % kWave), wv = (int)(threadIdx.x / kWave);
@@ -442,13 +472,13 @@ __global__ __launch_bounds__(256) MNA_WPE_ATTR void map_nested_apply_kernel(Nest
           const unsigned long long k = w * 64 + (unsigned long long)__builtin_ctzll(bits);
           bits &= bits - 1;
           if (k < K) {
-            const NaKey<APL> q = na_key<APL>(p, s, k, lane);
+            const NaKey<APL, KW> q = na_key<APL, KW>(p, s, k, lane);
             q.key_rm(r);
             st |= q.stb;
           }
         }
       }
-      if (NaKey<APL>::leq(r, c)) continue;  // no longer deferred
+      if (NaKey<APL, KW>::leq(r, c)) continue;  // no longer deferred
       if (o != d) {
         for (unsigned long long a = (unsigned long long)lane; a < A; a += kWave) set_clk(o, a, clk(d, a));
         for (unsigned long long w = (unsigned long long)lane; w < Kw; w += kWave) set_key(o, w, key(d, w));
@@ -468,7 +498,7 @@ __global__ __launch_bounds__(256) MNA_WPE_ATTR void map_nested_apply_kernel(Nest
     const unsigned h_k = hin ? p.key[mo] : 0u, h_ia = hin ? p.iactor[mo] : 0u, h_jk = hin ? p.ikey[mo] : 0u;
     const unsigned h_rr = hin ? p.clk_row[mo] : 0u;
     const u64 h_c = hin ? p.counter[mo] : 0ull, h_ic = hin ? p.icounter[mo] : 0ull, h_v = hin ? p.val[mo] : 0ull;
-    const u64 h_ib = hin ? p.ikeys[mo] : 0ull, h_kb = hin ? p.key_off[mo] : 0ull, h_ke = hin ? p.key_off[mo + 1] : 0ull;
+    const u64 h_ib = hin && p.K2w == 1 ? p.ikeys[mo] : 0ull, h_kb = hin ? p.key_off[mo] : 0ull, h_ke = hin ? p.key_off[mo + 1] : 0ull;
     const int nb = (int)(oe - o0 < (unsigned long long)kWave ? oe - o0 : (unsigned long long)kWave);
   for (int hi = 0; hi < nb; ++hi) {
     const unsigned long long o = o0 + (unsigned long long)hi;
@@ -480,18 +510,36 @@ __global__ __launch_bounds__(256) MNA_WPE_ATTR void map_nested_apply_kernel(Nest
       const unsigned rr = CRDT_MNA_HDR ? rl32(h_rr, hi) : p.clk_row[o];
       const unsigned ia = ik == 0 ? (CRDT_MNA_HDR ? rl32(h_ia, hi) : p.iactor[o]) : 0u;
       const unsigned long long jk = ik == 0 ? (CRDT_MNA_HDR ? rl32(h_jk, hi) : p.ikey[o]) : 0ull;
-      const u64 ib = ik == 1 ? (CRDT_MNA_HDR ? rl64(h_ib, hi) : p.ikeys[o]) : 0ull;
-      if (a >= A || k >= K || ik > 1 || rr >= p.n_clk_rows || ia >= A || jk >= K2 || (K2 < 64 && (ib >> K2))) {
+      // an inner Rm's key set: K2w words of ikeys [n_ops][K2w] (one word batched with the headers);
+      // read here for the range check and again at the Rm, so no word is held across the key's setup
+      const auto ibw = [&](int x) -> u64 {
+        return ik != 1 || (unsigned long long)x >= p.K2w ? 0ull
+               : p.K2w == 1 ? (CRDT_MNA_HDR ? rl64(h_ib, hi) : p.ikeys[o])
+                            : p.ikeys[o * p.K2w + x];
+      };
+      bool kbad = false;  // a key bit past K2
+#pragma unroll
+      for (int x = 0; x < KW; ++x) {
+        const unsigned long long lo = 64ull * x;
+        const u64 w = ibw(x);
+        kbad = kbad || (K2 < lo + 64 && (K2 <= lo ? w != 0 : (w >> (K2 - lo)) != 0));
+      }
+      if (a >= A || k >= K || ik > 1 || rr >= p.n_clk_rows || ia >= A || jk >= K2 || kbad) {
         st |= 2u;  // malformed: skipped whole
         continue;
       }
-      const NaKey<APL> q = na_key<APL>(p, s, k, lane);
+      const NaKey<APL, KW> q = na_key<APL, KW>(p, s, k, lane);
       if (q.word_of(c, a) >= cnt) continue;  // seen (map.rs:123-126)
       q.bump(q.ec, a, cnt);  // entry.clock.apply(dot) (an absent entry: its rows are Map::default())
       u64 r[APL];
       q.ld(p.clk_pool + (unsigned long long)rr * A, r);
       if (ik == 0) q.inner_up(ia, CRDT_MNA_HDR ? rl64(h_ic, hi) : p.icounter[o], jk, r, CRDT_MNA_HDR ? rl64(h_v, hi) : p.val[o]);
-      else q.inner_rm(r, ib);
+      else {
+        u64 ib[KW];
+#pragma unroll
+        for (int x = 0; x < KW; ++x) ib[x] = ibw(x);
+        q.inner_rm(r, ib);
+      }
       st |= q.stb;
 #pragma unroll
       for (int j = 0; j < APL; ++j)
@@ -510,14 +558,14 @@ __global__ __launch_bounds__(256) MNA_WPE_ATTR void map_nested_apply_kernel(Nest
       for (u64 i = kb; i < ke; ++i) {
         const unsigned long long k = p.keys[i];
         if (k < K) {
-          const NaKey<APL> q = na_key<APL>(p, s, k, lane);
+          const NaKey<APL, KW> q = na_key<APL, KW>(p, s, k, lane);
           q.key_rm(r);
           st |= q.stb;
         } else {
           st |= 2u;
         }
       }
-      if (NaKey<APL>::leq(r, c)) continue;
+      if (NaKey<APL, KW>::leq(r, c)) continue;
       int slot = -1;
       for (unsigned d = 0; d < dcnt && slot < 0; ++d) {
         bool ne = false;
@@ -576,13 +624,13 @@ done:
 
 // Causal::forget of the entries: one wave per (state, key), y row y[s] (the map clock and the outer
 // deferred pool go through crdt_map_forget_batch afterwards)
-template <int APL>
+template <int APL, int KW>
 __global__ __launch_bounds__(256) void map_nested_forget_kernel(NestedApplyPlan p) {
   const int lane = (int)(threadIdx.x % kWave);
   const unsigned long long sk = (unsigned long long)blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
   if (sk >= p.N * p.K) return;  // (whole waves)
   const unsigned long long s = sk / p.K, k = sk % p.K;
-  const NaKey<APL> q = na_key<APL>(p, s, k, lane);
+  const NaKey<APL, KW> q = na_key<APL, KW>(p, s, k, lane);
   u64 r[APL];
   q.ld(p.y + s * p.y_stride, r);
   q.key_rm(r);  // (Map::forget on an entry = apply_keyset_rm's per-key step)
@@ -595,7 +643,7 @@ using namespace crdt;
 static int nested_states_check(crdt_ctx *ctx, const crdt_map_nested_states *m, const char *what) {
   if (!m) return fail(ctx, CRDT_EINVAL, "%s: NULL states", what);
   if (m->A > 512) return fail(ctx, CRDT_EUNSUPPORTED, "%s: A = %zu > 512", what, m->A);
-  if (m->K2 > 64) return fail(ctx, CRDT_EUNSUPPORTED, "%s: K2 = %zu > 64 (inner key sets are one u64 mask)", what, m->K2);
+  if (m->K2 > 256) return fail(ctx, CRDT_EUNSUPPORTED, "%s: K2 = %zu > 256 (inner key sets of 4 mask words)", what, m->K2);
   if (m->N && (!m->clock || (m->K && (!m->ec || !m->ic || !m->id_n || !m->id_clock || !m->id_keys ||
                                       (m->K2 && (!m->iec || !m->ivc || !m->ivv || !m->nval))))))
     return fail(ctx, CRDT_EINVAL, "%s: NULL state buffer", what);
@@ -617,6 +665,7 @@ static NestedApplyPlan nested_plan(const crdt_map_nested_states *m) {
   p.N = m->N;
   p.K = m->K;
   p.K2 = m->K2;
+  p.K2w = m->K2 > 64 ? (m->K2 + 63) / 64 : 1;
   p.A = m->A;
   p.Kw = m->K ? (m->K + 63) / 64 : 1;
   return p;
@@ -686,12 +735,16 @@ extern "C" int crdt_map_nested_apply_batch(crdt_ctx *ctx, const crdt_map_nested_
   const dim3 grid((unsigned)((N + wpb - 1) / wpb)), block(wpb * kWave);
   const size_t lds = per_wave * wpb;
   timing_begin(ctx, "map_nested_apply");
-  auto go = [&](auto t, dim3 g, dim3 b, size_t l) {
-    constexpr int T = decltype(t)::value;
-    if (A <= 64) hipLaunchKernelGGL((map_nested_apply_kernel<1, T>), g, b, l, ctx->stream, p);
-    else if (A <= 128) hipLaunchKernelGGL((map_nested_apply_kernel<2, T>), g, b, l, ctx->stream, p);
-    else if (A <= 256) hipLaunchKernelGGL((map_nested_apply_kernel<4, T>), g, b, l, ctx->stream, p);
-    else hipLaunchKernelGGL((map_nested_apply_kernel<8, T>), g, b, l, ctx->stream, p);
+  auto go_kw = [&](auto t, auto w, dim3 g, dim3 b, size_t l) {
+    constexpr int T = decltype(t)::value, W = decltype(w)::value;
+    if (A <= 64) hipLaunchKernelGGL((map_nested_apply_kernel<1, T, W>), g, b, l, ctx->stream, p);
+    else if (A <= 128) hipLaunchKernelGGL((map_nested_apply_kernel<2, T, W>), g, b, l, ctx->stream, p);
+    else if (A <= 256) hipLaunchKernelGGL((map_nested_apply_kernel<4, T, W>), g, b, l, ctx->stream, p);
+    else hipLaunchKernelGGL((map_nested_apply_kernel<8, T, W>), g, b, l, ctx->stream, p);
+  };
+  auto go = [&](auto t, dim3 g, dim3 b, size_t l) {  // (one mask word per key set up to K2 = 64)
+    if (p.K2w == 1) go_kw(t, std::integral_constant<int, 1>{}, g, b, l);
+    else go_kw(t, std::integral_constant<int, kNaKw>{}, g, b, l);
   };
   if (Dcap <= Dl) {
     go(std::integral_constant<int, 0>{}, grid, block, lds);  // one pass: the whole list fits the LDS slots
@@ -727,10 +780,16 @@ extern "C" int crdt_map_nested_forget_batch(crdt_ctx *ctx, const crdt_map_nested
     if (blocks > 0x7fffffffULL) return fail(ctx, CRDT_EUNSUPPORTED, "map_nested_forget_batch: N*K too large");
     CRDT_HIP(ctx, hipSetDevice(ctx->device));
     timing_begin(ctx, "map_nested_forget");
-    if (A <= 64) hipLaunchKernelGGL(map_nested_forget_kernel<1>, dim3((unsigned)blocks), dim3(256), 0, ctx->stream, p);
-    else if (A <= 128) hipLaunchKernelGGL(map_nested_forget_kernel<2>, dim3((unsigned)blocks), dim3(256), 0, ctx->stream, p);
-    else if (A <= 256) hipLaunchKernelGGL(map_nested_forget_kernel<4>, dim3((unsigned)blocks), dim3(256), 0, ctx->stream, p);
-    else hipLaunchKernelGGL(map_nested_forget_kernel<8>, dim3((unsigned)blocks), dim3(256), 0, ctx->stream, p);
+    auto fgo = [&](auto w) {
+      constexpr int W = decltype(w)::value;
+      const dim3 g((unsigned)blocks), b(256);
+      if (A <= 64) hipLaunchKernelGGL((map_nested_forget_kernel<1, W>), g, b, 0, ctx->stream, p);
+      else if (A <= 128) hipLaunchKernelGGL((map_nested_forget_kernel<2, W>), g, b, 0, ctx->stream, p);
+      else if (A <= 256) hipLaunchKernelGGL((map_nested_forget_kernel<4, W>), g, b, 0, ctx->stream, p);
+      else hipLaunchKernelGGL((map_nested_forget_kernel<8, W>), g, b, 0, ctx->stream, p);
+    };
+    if (p.K2w == 1) fgo(std::integral_constant<int, 1>{});
+    else fgo(std::integral_constant<int, kNaKw>{});
     timing_end(ctx);
     CRDT_HIP(ctx, hipGetLastError());
   }

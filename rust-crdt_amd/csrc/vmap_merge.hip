@@ -396,6 +396,7 @@ extern "C" int crdt_map_nested_merge_batch(crdt_ctx *ctx, const crdt_map_nested_
       return fail(ctx, CRDT_EINVAL, "%s: NULL state buffer", what);
   CRDT_HIP(ctx, hipSetDevice(ctx->device));
   const size_t Kw = (K + 63) / 64, VS = 8;
+  const size_t K2w = K2 > 64 ? (K2 + 63) / 64 : 1;  // inner key-set mask words (the fold's layout)
   std::vector<size_t> off;
   if (int rc = pool_offsets(ctx, ad, bd, N, off, what)) return rc;
   std::vector<u64> ioff;
@@ -405,7 +406,7 @@ extern "C" int crdt_map_nested_merge_batch(crdt_ctx *ctx, const crdt_map_nested_
   const size_t c2 = cv.take(N * 2 * A * 8), e2 = cv.take(N * 2 * K * A * 8), i2 = cv.take(N * 2 * K * A * 8);
   const size_t ie2 = cv.take(N * 2 * K * K2 * A * 8), vc2 = cv.take(N * 2 * K * K2 * VS * A * 8);
   const size_t vv2 = cv.take(N * 2 * K * K2 * VS * 8), of = cv.take(N * 4);
-  const size_t io = cv.take((N * 2 * K + 1) * 8), ic = cv.take(Di * A * 8), ik = cv.take(Di * 8);
+  const size_t io = cv.take((N * 2 * K + 1) * 8), ic = cv.take(Di * A * 8), ik = cv.take(Di * K2w * 8);
   size_t at[6];
   pool_bytes(N, D, A, Kw, cv, at);
   if (int rc = ensure_dscratch(ctx, cv.used)) return rc;
@@ -420,7 +421,7 @@ extern "C" int crdt_map_nested_merge_batch(crdt_ctx *ctx, const crdt_map_nested_
   if (int rc = stage_h2d(ctx, base + io, ioff.data(), ioff.size() * 8)) return rc;
   if (Di) {
     hipLaunchKernelGGL(vmm_csr_kernel, dim3((unsigned)(N * 2 * K)), dim3(64), 0, ctx->stream, (unsigned long long)N,
-                       (unsigned long long)K, (unsigned long long)A, 1ull, a->id_n, (const u64 *)a->id_clock,
+                       (unsigned long long)K, (unsigned long long)A, (unsigned long long)K2w, a->id_n, (const u64 *)a->id_clock,
                        (const u64 *)a->id_keys, b->id_n, (const u64 *)b->id_clock, (const u64 *)b->id_keys,
                        reinterpret_cast<const u64 *>(base + io), reinterpret_cast<u64 *>(base + ic),
                        reinterpret_cast<u64 *>(base + ik));

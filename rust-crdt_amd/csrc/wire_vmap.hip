@@ -35,9 +35,9 @@ struct VMapWirePlan {
   int vt;  // value type: 0 = W counter VClocks (GCounter W = 1, PNCounter W = 2), 1 = Orswot, 2 = Map<K2, MVReg>
   const uint32_t *actors, *keys, *ikeys;
   const u64 *members;
-  unsigned long long K2;
+  unsigned long long K2, K2w;  // inner keys; inner key-set mask words (1 up to K2 = 64)
   u64 *ic, *iec, *ivc, *ivv, *id_clock, *id_keys;  // nested Map [N][K][A], [N][K][K2][A], [N][K][K2][8][A],
-  uint32_t *nval, *id_n;                           // [N][K][K2][8], [N][K][16][A], [N][K][16]; [N][K][K2], [N][K]
+  uint32_t *nval, *id_n;                           // [N][K][K2][8], [N][K][16][A], [N][K][16][K2w]; [N][K][K2], [N][K]
   u64 *clock, *ec, *val;           // [N][A], [N][K][A], counter [N][K][W][A]
   u64 *oc, *ent;                   // Orswot [N][K][A], [N][K][M][A]
   uint32_t *vd_n;                  // [N][K]
@@ -75,6 +75,12 @@ __device__ __forceinline__ unsigned long long parse_idset(const Frame &f, unsign
   return k + per * n;
 }
 
+__host__ __device__ __forceinline__ unsigned long long max3(unsigned long long a, unsigned long long b,
+                                                            unsigned long long c) {
+  const unsigned long long m = a > b ? a : b;
+  return m > c ? m : c;
+}
+
 __global__ __launch_bounds__(kBlock) void vmap_ingest_kernel(VMapWirePlan p) {
   extern __shared__ u64 lds[];
   const int lane = threadIdx.x % kWave, wib = threadIdx.x / kWave;
@@ -101,7 +107,7 @@ __global__ __launch_bounds__(kBlock) void vmap_ingest_kernel(VMapWirePlan p) {
     if (p.vt == 2) ikeys = reinterpret_cast<const uint32_t *>(lm);
     base = lds + aw + kw + nm;
   }
-  const unsigned long long bw = p.Kw > p.Mw ? p.Kw : p.Mw;
+  const unsigned long long bw = max3(p.Kw, p.Mw, p.K2w);
   u64 *row = base + (unsigned long long)wib * (p.A + bw);
   u64 *bits = row + p.A;
   for (unsigned long long s = (unsigned long long)blockIdx.x * wpb + wib; s < p.N;
@@ -193,12 +199,12 @@ __global__ __launch_bounds__(kBlock) void vmap_ingest_kernel(VMapWirePlan p) {
           unsigned long long dn = 0;
           for (u64 j = 0; j < d2 && k != ~0ull; ++j) {
             k = parse_vclock(f, k, actors, p.A, row, lane, st);
-            k = parse_idset(f, k, false, ikeys, nullptr, p.K2, bits, 1, lane, st);
+            k = parse_idset(f, k, false, ikeys, nullptr, p.K2, bits, p.K2w, lane, st);
             if (k == ~0ull) break;
             if (ki >= 0) {
               if (dn < (unsigned long long)kVwVd) {
                 store_row<u64>(p.id_clock + (sk * kVwVd + dn) * p.A, row, p.A, lane);
-                if (lane == 0) p.id_keys[sk * kVwVd + dn] = bits[0];
+                for (unsigned long long x = lane; x < p.K2w; x += kWave) p.id_keys[(sk * kVwVd + dn) * p.K2w + x] = bits[x];
                 ++dn;
               } else {
                 st |= kWireCap;
@@ -390,11 +396,11 @@ __global__ __launch_bounds__(kBlock) void vmap_egress_kernel(VMapWirePlan p, int
           k += 2;
         }
         for (unsigned long long i = 0; i < dn; ++i) {
-          const u64 *rm = p.id_clock + (sk * kVwVd + i) * p.A, *kb = p.id_keys + sk * kVwVd + i;
-          sz += vclock_bytes(rm, p.A, lane) + 8 + 4 * popc_row(kb, 1, lane);
+          const u64 *rm = p.id_clock + (sk * kVwVd + i) * p.A, *kb = p.id_keys + (sk * kVwVd + i) * p.K2w;
+          sz += vclock_bytes(rm, p.A, lane) + 8 + 4 * popc_row(kb, p.K2w, lane);
           if (write) {
             k = write_vclock(w, k, rm, p.A, p.actors, lane);
-            k = write_idset(w, k, kb, 1, false, p.ikeys, nullptr, lane);
+            k = write_idset(w, k, kb, p.K2w, false, p.ikeys, nullptr, lane);
           }
         }
         continue;
@@ -533,12 +539,13 @@ static int vmap_nested_plan(crdt_ctx *ctx, const crdt_map_nested_states *st, con
   if (!st || !actors || !keys || !ikeys) return fail(ctx, CRDT_EINVAL, "%s: NULL states / dictionaries", what);
   const size_t N = st->N, K = st->K, K2 = st->K2, A = st->A;
   if (A == 0 || K == 0 || K2 == 0) return fail(ctx, CRDT_EINVAL, "%s: need A, K, K2 >= 1", what);
-  if (K2 > 64) return fail(ctx, CRDT_EUNSUPPORTED, "%s: K2 = %zu > 64 (inner key sets are one u64 mask)", what, K2);
+  if (K2 > 256) return fail(ctx, CRDT_EUNSUPPORTED, "%s: K2 = %zu > 256", what, K2);
   if (N && (!st->clock || !st->ec || !st->ic || !st->iec || !st->ivc || !st->ivv || !st->nval || !st->id_n ||
             !st->id_clock || !st->id_keys))
     return fail(ctx, CRDT_EINVAL, "%s: NULL state buffer", what);
-  const size_t Kw = (K + 63) / 64;
-  if (A + Kw > (size_t)kWireRowLds) return fail(ctx, CRDT_EUNSUPPORTED, "%s: A + K/64 too large", what);
+  const size_t Kw = (K + 63) / 64, K2w = K2 > 64 ? (K2 + 63) / 64 : 1;
+  if (A + (Kw > K2w ? Kw : K2w) > (size_t)kWireRowLds)
+    return fail(ctx, CRDT_EUNSUPPORTED, "%s: A + K/64 too large", what);
   p = VMapWirePlan{};
   if (int rc = vmap_deferred_plan(ctx, df, N, p, what)) return rc;
   p.N = N;
@@ -546,6 +553,7 @@ static int vmap_nested_plan(crdt_ctx *ctx, const crdt_map_nested_states *st, con
   p.K = K;
   p.Kw = Kw;
   p.K2 = K2;
+  p.K2w = K2 > 64 ? (K2 + 63) / 64 : 1;
   p.vt = 2;
   p.actors = actors;
   p.keys = keys;
@@ -581,7 +589,7 @@ static int vmap_ingest(crdt_ctx *ctx, VMapWirePlan &p, const uint8_t *bytes, con
     if (int rc = device_fill(ctx, p.nval, N * p.K * p.K2 * 4, 0)) return rc;
     if (int rc = device_fill(ctx, p.id_n, N * p.K * 4, 0)) return rc;
     if (int rc = device_fill(ctx, p.id_clock, N * p.K * kVwVd * p.A * 8, 0)) return rc;
-    if (int rc = device_fill(ctx, p.id_keys, N * p.K * kVwVd * 8, 0)) return rc;
+    if (int rc = device_fill(ctx, p.id_keys, N * p.K * kVwVd * p.K2w * 8, 0)) return rc;
   } else {
     if (int rc = device_fill(ctx, p.oc, N * p.K * p.A * 8, 0)) return rc;
     if (int rc = device_fill(ctx, p.ent, N * p.K * p.M * p.A * 8, 0)) return rc;
@@ -592,7 +600,7 @@ static int vmap_ingest(crdt_ctx *ctx, VMapWirePlan &p, const uint8_t *bytes, con
   p.bytes = bytes;
   p.frame_off = (const u64 *)frame_off;
   p.status = status;
-  const size_t bw = p.Kw > p.Mw ? p.Kw : p.Mw;
+  const size_t bw = max3(p.Kw, p.Mw, p.K2w);
   const size_t per_wave = p.A + bw;
   int wpb = 4;
   while (wpb > 1 && (size_t)wpb * per_wave * 8 > 64 * 1024) --wpb;

@@ -1437,10 +1437,10 @@ impl<K: Ord + Clone, M: Member, A: Actor> BatchCvRDT for Map<K, Orswot<M, A>, A>
     }
 }
 
-/// Limits of the nested Map fold (include/crdt_gpu.h: A <= 256 since round 6, K2 <= 64, V <= 8 values per
-/// register).
+/// Limits of the nested Map fold (include/crdt_gpu.h: A <= 256 and K2 <= 256 since round 6, V <= 8 values
+/// per register).  Past 64 inner keys an inner key set is ceil(K2/64) mask words.
 pub const MAP_NESTED_MAX_ACTORS: usize = 256;
-pub const MAP_NESTED_MAX_INNER_KEYS: usize = 64;
+pub const MAP_NESTED_MAX_INNER_KEYS: usize = 256;
 pub const MAP_NESTED_MAX_VALUES: usize = 8;
 
 /// Every group's fold of Map<K, Map<K2, MVReg<V>>> (crdt_map_nested_lub_many, G groups of equal R) —
@@ -1475,6 +1475,7 @@ fn nested_map_folds<K: Ord + Clone, K2: Ord + Clone, V: Clone, A: Actor>(
                                        MAP_NESTED_MAX_VALUES)));
     }
     let kw = (k + 63) / 64;
+    let k2w = if k2 > 64 { (k2 + 63) / 64 } else { 1 };  // inner key-set mask words
     let n = g * r * k;
     let (mut clock, mut ec, mut ic) = (vec![0u64; g * r * a], vec![0u64; n * a], vec![0u64; n * a]);
     let (mut iec, mut ivc, mut ivv) = (vec![0u64; n * k2 * a], vec![0u64; n * k2 * v * a], vec![0u64; n * k2 * v]);
@@ -1497,14 +1498,14 @@ fn nested_map_folds<K: Ord + Clone, K2: Ord + Clone, V: Clone, A: Actor>(
                     let mut row = vec![0u64; a];
                     clock_row(rm, &actors, &mut row);
                     id_clock.extend(row);
-                    id_keys.push(key_bits(ks, &ikeys, 1)[0]);
+                    id_keys.extend(key_bits(ks, &ikeys, k2w));
                 }
             }
-            id_off.push(id_keys.len() as u64);
+            id_off.push((id_keys.len() / k2w) as u64);
         }
     }
     let pool = group_pool(groups, &actors, &keys);
-    let (nd, di) = (pool.def_row.len(), id_keys.len());
+    let (nd, di) = (pool.def_row.len(), id_keys.len() / k2w);
     let batch = ffi::crdt_map_nested_batch {
         G: g, R: r, K: k, K2: k2, V: v, A: a,
         clock: clock.as_ptr(), ec: ec.as_ptr(), ic: ic.as_ptr(), iec: iec.as_ptr(), ivc: ivc.as_ptr(), ivv: ivv.as_ptr(),
@@ -1516,7 +1517,7 @@ fn nested_map_folds<K: Ord + Clone, K2: Ord + Clone, V: Clone, A: Actor>(
     let (mut o_iec, mut o_ivc, mut o_ivv) = (vec![0u64; g * k * k2 * a], vec![0u64; g * k * k2 * 8 * a],
                                              vec![0u64; g * k * k2 * 8]);
     let (mut o_nval, mut o_idn) = (vec![0u32; g * k * k2], vec![0u32; g * k]);
-    let (mut o_idc, mut o_idk) = (vec![0u64; g * k * 16 * a], vec![0u64; g * k * 16]);
+    let (mut o_idc, mut o_idk) = (vec![0u64; g * k * 16 * a], vec![0u64; g * k * 16 * k2w]);
     let (mut flags, mut keep, mut okeys) = (vec![0u32; g], vec![0u8; nd], vec![0u64; nd * kw]);
     let mut out = ffi::crdt_map_nested_out {
         clock: o_clock.as_mut_ptr(), ec: o_ec.as_mut_ptr(), ic: o_ic.as_mut_ptr(), iec: o_iec.as_mut_ptr(),
@@ -1551,7 +1552,7 @@ fn nested_map_folds<K: Ord + Clone, K2: Ord + Clone, V: Clone, A: Actor>(
                 }
             }
             for i in 0..o_idn[b] as usize {
-                let ks = bit_keys(&o_idk[b * 16 + i..b * 16 + i + 1], &ikeys);
+                let ks = bit_keys(&o_idk[(b * 16 + i) * k2w..(b * 16 + i + 1) * k2w], &ikeys);
                 inner.deferred.entry(row_clock(&o_idc[(b * 16 + i) * a..(b * 16 + i + 1) * a], &actors))
                     .or_insert_with(BTreeSet::new).extend(ks);
             }

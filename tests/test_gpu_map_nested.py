@@ -171,7 +171,8 @@ def nested_states(maps, K, K2, A, Dcap=16):
                 nval[n, k, j] = len(ie.val.vals)
     idn = np.zeros((N, K), np.int32)
     idc = np.zeros((N, K, 16, A), np.uint64)
-    idk = np.zeros((N, K, 16), np.uint64)
+    K2w = (K2 + 63) // 64 if K2 > 64 else 1  # inner key sets: K2w mask words past 64 keys
+    idk = np.zeros((N, K, 16) if K2w == 1 else (N, K, 16, K2w), np.uint64)
     off = d["id_off"].astype(np.int64)
     for i in range(N * K):
         a, b = off[i], off[i + 1]
@@ -255,8 +256,8 @@ def gpu_apply(ctx, m, ops):
         return _map_vals(gpu_apply(ctx, _map_vals(m, fv), ops), inv)
     dense, back, Ad, Kd, Jd = _intern([m], extra=_op_ids(ops), with_dicts=True)
     A, K, K2 = len(Ad.fwd), len(Kd.fwd), len(Jd.fwd)
-    if A > 512 or K2 > 64:
-        pytest.skip("more than 512 actors / 64 inner keys in one case")
+    if A > 512 or K2 > 256:
+        pytest.skip("more than 512 actors / 256 inner keys in one case")
     st, slots, _ = nested_states(dense, K, K2, A)
     row = lambda c: {Ad.fwd[a]: n for a, n in c.dots.items()}  # noqa: E731
     stream = []
@@ -270,7 +271,7 @@ def gpu_apply(ctx, m, ops):
             put = op.op.op
             stream.append(("put", Ad.fwd[op.dot.actor], op.dot.counter, Kd.fwd[op.key], Ad.fwd[op.op.dot.actor],
                            op.op.dot.counter, Jd.fwd[op.op.key], row(put.clock), int(put.val)))
-    enc = cg.map.encode_nested_ops([stream], A, "cuda:0")
+    enc = cg.map.encode_nested_ops([stream], A, "cuda:0", K2=K2)
     status = cg.map.nested_apply_batch(st, *slots, enc, ctx=ctx).cpu().numpy()
     assert status[0] == 0, status
     return back(decode_states(st, 0, _slot_deferred(slots, 0)))
@@ -280,8 +281,8 @@ def gpu_forget(ctx, m, clock):
     """m.forget(clock) on the GPU (crdt_map_nested_forget_batch); returns the new state."""
     dense, back, Ad, Kd, Jd = _intern([m], extra=(set(clock.dots), set(), set()), with_dicts=True)
     A, K, K2 = len(Ad.fwd), len(Kd.fwd), len(Jd.fwd)
-    if A > 512 or K2 > 64:
-        pytest.skip("more than 512 actors / 64 inner keys in one case")
+    if A > 512 or K2 > 256:
+        pytest.skip("more than 512 actors / 256 inner keys in one case")
     st, _, d = nested_states(dense, K, K2, A)
     y = np.zeros(A, np.uint64)
     for a, c in clock.dots.items():

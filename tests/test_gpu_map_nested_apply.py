@@ -216,7 +216,8 @@ def _fits(m):
             and all(len(ie.val.vals) <= 8 for e in m.entries.values() for ie in e.val.entries.values()))
 
 
-@pytest.mark.parametrize("K,K2,A,seed", [(4, 6, 5, 1), (3, 64, 4, 2), (5, 5, 70, 3)])
+@pytest.mark.parametrize("K,K2,A,seed", [(4, 6, 5, 1), (3, 64, 4, 2), (5, 5, 70, 3),
+                                         (3, 200, 5, 4), (2, 256, 130, 5)])  # (K2 > 64: K2w mask words)
 def test_map_nested_apply_streams(gpu_ctx, K, K2, A, seed):
     N, T = 24, 30
     maps = [m for m in O.nested_map_objects(N + 8, K, K2, A, seed=80 + seed, steps=200, p_irm=0.5, p_ooo=0.8,
@@ -232,7 +233,7 @@ def test_map_nested_apply_streams(gpu_ctx, K, K2, A, seed):
     maps, exps = [maps[n] for n in keep], [exps[n] for n in keep]
     streams = [streams[n] for n in keep]
     st, slots, _ = nested_states(maps, K, K2, A)
-    ops = cg.map.encode_nested_ops(streams, A, "cuda:0")
+    ops = cg.map.encode_nested_ops(streams, A, "cuda:0", K2=K2)
     status = cg.map.nested_apply_batch(st, *slots, ops, ctx=gpu_ctx).cpu().numpy()
     inner_def = outer_def = 0
     for n, exp in enumerate(exps):
@@ -245,9 +246,9 @@ def test_map_nested_apply_streams(gpu_ctx, K, K2, A, seed):
     assert len(exps) >= 12 and inner_def > 0 and outer_def > 0
 
 
-@pytest.mark.parametrize("mode", ["below", "all", "zero"])
-def test_map_nested_forget_batch(gpu_ctx, mode):
-    K, K2, A = 4, 6, 5
+@pytest.mark.parametrize("mode,K2", [("below", 6), ("all", 6), ("zero", 6), ("zero", 200), ("below", 256)])
+def test_map_nested_forget_batch(gpu_ctx, mode, K2):
+    K, A = 4, 5
     maps = [m for m in O.nested_map_objects(32, K, K2, A, seed=90, steps=220, p_irm=0.5, p_ooo=0.8, p_rm=0.3)
             if _fits(m)]
     N = len(maps)
@@ -273,6 +274,28 @@ def test_map_nested_forget_batch(gpu_ctx, mode):
         inner_def += sum(len(e.val.deferred) for e in exp.entries.values())
     if mode == "zero":
         assert inner_def > 0 and D > 0
+
+
+def test_map_nested_apply_wide_keyset_malformed(gpu_ctx):
+    """K2 = 100 (two mask words per key set): an inner Rm naming key 120 (word 1, past K2) is malformed
+    and skipped whole (bit 1); one over keys 3 and 90 (both words) removes both."""
+    K, K2, A = 2, 100, 3
+    m = Map(lambda: Map(O.MVReg))
+    for a, j in ((0, 3), (1, 90), (2, 50)):
+        m.apply(MapUp(Dot(a, 1), 0, MapUp(Dot(a, 1), j, MVRegPut(VClock({}), 10 + a))))
+    st, slots, _ = nested_states([m, m.copy()], K, K2, A)
+    rm_row = {0: 1, 1: 1}
+    streams = [[("irm", 0, 2, 0, rm_row, [3, 120])], [("irm", 0, 2, 0, rm_row, [3, 90])]]
+    ops = cg.map.encode_nested_ops(streams, A, "cuda:0", K2=K2)
+    assert tuple(ops.ikeys.shape) == (2, 2)
+    status = cg.map.nested_apply_batch(st, *slots, ops, ctx=gpu_ctx).cpu().numpy()
+    assert status[0] & 2 and not status[1] & 2, status
+    assert canon(decode_states(st, 0, _slot_deferred(slots, 0))) == canon(m)
+    exp = m.copy()
+    exp.apply(MapUp(Dot(0, 2), 0, MapRm(VClock(dict(rm_row)), [3, 90])))
+    got = decode_states(st, 1, _slot_deferred(slots, 1))
+    assert canon(got) == canon(exp)
+    assert sorted(got.entries[0].val.entries) == [50]
 
 
 def test_map_nested_apply_malformed_and_capacity(gpu_ctx):

@@ -169,6 +169,29 @@ def test_nested_merge_batch(gpu_ctx, seed, N, K, K2, A):
         assert canon(got) == canon(exps[i]), i
 
 
+@pytest.mark.parametrize("K2,A,seed", [(200, 6, 5), (256, 70, 6)])
+def test_nested_merge_batch_wide_inner_keys(gpu_ctx, K2, A, seed):
+    """K2 > 64 (inner key sets of K2w mask words), states not interned so the inner keys spread over
+    the whole range."""
+    N, K = 6, 3
+    maps = O.nested_map_objects(2 * N, K, K2, A, seed=seed, steps=300)
+    exps = []
+    for i in range(N):
+        exp = maps[i].copy()
+        exp.merge(maps[N + i].copy())
+        exps.append(exp)
+    Dcap = max([len(m.deferred) for m in maps] + [1]) * 2
+    sa, slots_a, _ = nested_states(maps[:N], K, K2, A, Dcap)
+    sb, slots_b, _ = nested_states(maps[N:], K, K2, A, Dcap)
+    assert sa.id_keys.dim() == 4
+    me, other = wire.MapNestedFrames(*sa, *slots_a), wire.MapNestedFrames(*sb, *slots_b)
+    status = cg.map.nested_merge_batch(me, other, ctx=gpu_ctx).cpu().numpy()
+    assert (status == 0).all(), status
+    for i in range(N):
+        assert canon(decode_states(me, i, _slot_list(me, i))) == canon(exps[i]), i
+    assert any(j >= 64 for e in exps[0].entries.values() for j in e.val.entries) or K2 <= 64
+
+
 def test_counter_merge_batch_different_dcaps(gpu_ctx):
     """self and other with different slot capacities (other's Dcap 3 x self's): the pool takes both."""
     N, K, A, W = 10, 6, 5, 2

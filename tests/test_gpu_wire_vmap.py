@@ -207,7 +207,7 @@ def _nested_fits(m):
             and all(len(ie.val.vals) <= 8 for e in m.entries.values() for ie in e.val.entries.values()))
 
 
-@pytest.mark.parametrize("K2,A", [(6, 5), (64, 4), (5, 70)])
+@pytest.mark.parametrize("K2,A", [(6, 5), (64, 4), (5, 70), (200, 5), (256, 6)])  # (K2 > 64: K2w key-set words)
 def test_map_nested_ingest_egress(gpu_ctx, K2, A):
     """Map<u32, Map<u32, MVReg<u64>>> (test/map.rs:10): ingest equals the state layout built from the
     oracle objects, egress reproduces the frames byte for byte."""
