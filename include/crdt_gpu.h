@@ -65,10 +65,11 @@ const char *crdt_last_error(const crdt_ctx *ctx);
 /* Library version, e.g. "0.6.0"; and the gfx target the code objects were built for. */
 const char *crdt_version(void);
 /* ABI revision of this header: bumped whenever a struct or signature changes incompatibly (round 5
- * appended `size_t Dv` to crdt_map_orswot_batch: revision 5 -> 6).  A caller checks
+ * appended `size_t Dv` to crdt_map_orswot_batch: revision 5 -> 6; round 6 appended `size_t Vd` to
+ * crdt_map_orswot_states / crdt_map_orswot_out: 7 -> 8).  A caller checks
  * crdt_abi_version() == CRDT_ABI_VERSION of the header it was built against before any other call,
  * so a mismatched library fails clearly instead of reading a shorter struct. */
-#define CRDT_ABI_VERSION 7
+#define CRDT_ABI_VERSION 8
 int crdt_abi_version(void);
 const char *crdt_build_target(void);
 
@@ -410,8 +411,9 @@ typedef struct crdt_map_orswot_states {
   uint64_t *oc;       /* [N][K][A]         */
   uint64_t *ent;      /* [N][K][M][A]      */
   uint32_t *vd_n;     /* [N][K]            */
-  uint64_t *vd_clock; /* [N][K][16][A]     */
-  uint64_t *vd_mem;   /* [N][K][16][Mw]    */
+  uint64_t *vd_clock; /* [N][K][Vd][A]     */
+  uint64_t *vd_mem;   /* [N][K][Vd][Mw]    */
+  size_t Vd;          /* nested deferred slots per key (round 6, ABI 8; 0 = 16) */
 } crdt_map_orswot_states;
 
 int crdt_map_orswot_forget_batch(crdt_ctx *ctx, const crdt_map_orswot_states *states, const uint64_t *y,
@@ -761,10 +763,12 @@ int crdt_map_counter_lub_many_sharded(crdt_ctx *ctx, const crdt_map_counter_batc
  *   (an equal clock twice in one list: unioned);
  *   the Map's own deferred removes as for the counter Map: def_off HOST, G+1 entries.
  * Output per group g (packed): clock[g*A + a], ec / oc [(g*K + k)*A + a], ent [((g*K + k)*M + m)*A
- * + a], nested deferred vd_n[g*K + k] (<= 16) with vd_clock [((g*K + k)*16 + i)*A + a] and
- * vd_mem [((g*K + k)*16 + i)*Mw + w]; flags[g]: bit 1 = def_row not non-decreasing or >= R, bit 3 = more
- * than 256 live Map removes named one key, bit 4 = a key's Orswot held more than 16 deferred
- * removes, bit 5 = vd_off invalid (checked on the device: vd_off[0] == 0, non-decreasing,
+ * + a], nested deferred vd_n[g*K + k] (<= Vd) with vd_clock [((g*K + k)*Vd + i)*A + a] and
+ * vd_mem [((g*K + k)*Vd + i)*Mw + w] (Vd = out->Vd, 0 meaning 16; round 6: the fold keeps 16 slots per
+ * key in LDS and re-folds, exactly, the keys whose list passed 16 with all Vd — a second launch of one
+ * wave per marked key, its Vd member masks in LDS: Vd * Mw * 8 + 6 KiB <= 160 KiB); flags[g]: bit 1 =
+ * def_row not non-decreasing or >= R, bit 3 = more than 256 live Map removes named one key, bit 4 = a
+ * key's Orswot held more than Vd deferred removes, bit 5 = vd_off invalid (checked on the device: vd_off[0] == 0, non-decreasing,
  * vd_off[G*R*K] == Dv; the fold reads only rows [0, Dv) whatever it holds) — results of the
  * group unreliable; def_keep / def_keys as crdt_map_out.
  * Orswot::forget collects its deferred removes into a new map: two whose clocks become equal keep
@@ -791,11 +795,12 @@ typedef struct crdt_map_orswot_out {
   uint64_t *oc;       /* [G][K][A]       */
   uint64_t *ent;      /* [G][K][M][A]    */
   uint32_t *vd_n;     /* [G][K]          */
-  uint64_t *vd_clock; /* [G][K][16][A]   */
-  uint64_t *vd_mem;   /* [G][K][16][Mw]  */
+  uint64_t *vd_clock; /* [G][K][Vd][A]   */
+  uint64_t *vd_mem;   /* [G][K][Vd][Mw]  */
   uint32_t *flags;    /* [G]             */
   uint8_t *def_keep;  /* [D]             */
   uint64_t *def_keys; /* [D][Kw]         */
+  size_t Vd;          /* nested deferred slots per key (round 6, ABI 8; 0 = 16) */
 } crdt_map_orswot_out;
 
 int crdt_map_orswot_lub_many(crdt_ctx *ctx, const crdt_map_orswot_batch *in, crdt_map_orswot_out *out);

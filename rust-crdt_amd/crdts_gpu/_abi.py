@@ -20,7 +20,7 @@ CRDT_ECOMM = -5
 CRDT_UNIQUE_ID_BYTES = 128
 CRDT_ACCUMULATE = 0x1
 CRDT_MEM_DEVICE = 0
-CRDT_ABI_VERSION = 7  # include/crdt_gpu.h
+CRDT_ABI_VERSION = 8  # include/crdt_gpu.h
 CRDT_MEM_HOST = 1
 CRDT_KIND = {"vclock": 1, "gcounter": 2, "pncounter": 3, "gset": 4}
 CRDT_RED_MAX, CRDT_RED_MIN, CRDT_RED_SUM = 0, 1, 2
@@ -126,7 +126,7 @@ class MapCounterStates(ctypes.Structure):  # crdt_map_counter_states
 
 class MapOrswotStates(ctypes.Structure):  # crdt_map_orswot_states
     _fields_ = [("N", S), ("K", S), ("M", S), ("A", S), ("clock", P), ("ec", P), ("oc", P), ("ent", P),
-                ("vd_n", P), ("vd_clock", P), ("vd_mem", P)]
+                ("vd_n", P), ("vd_clock", P), ("vd_mem", P), ("Vd", S)]
 
 
 class MapNestedStates(ctypes.Structure):  # crdt_map_nested_states
@@ -230,7 +230,7 @@ class MapOrswotBatch(ctypes.Structure):  # crdt_map_orswot_batch
 
 class MapOrswotOut(ctypes.Structure):  # crdt_map_orswot_out
     _fields_ = [("clock", P), ("ec", P), ("oc", P), ("ent", P), ("vd_n", P), ("vd_clock", P), ("vd_mem", P),
-                ("flags", P), ("def_keep", P), ("def_keys", P)]
+                ("flags", P), ("def_keep", P), ("def_keys", P), ("Vd", S)]
 
 
 class MapNestedBatch(ctypes.Structure):  # crdt_map_nested_batch

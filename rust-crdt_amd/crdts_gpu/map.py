@@ -503,7 +503,7 @@ def counter_lub_many(clock: torch.Tensor, ec: torch.Tensor, val: torch.Tensor, d
 
 
 # ---- Map<K, Orswot<M>> (crdt_map_orswot_lub_many, round 4) ------------------------------------------
-VD_CAP = 16  # nested deferred removes per key state (crdt_gpu.h)
+VD_CAP = 16  # nested deferred removes per key state by default (crdt_gpu.h; round 6: any Vd >= 16)
 
 
 class MapOrswotLub(NamedTuple):
@@ -512,8 +512,8 @@ class MapOrswotLub(NamedTuple):
     oc: torch.Tensor                  # (G, K, A) the nested Orswot clocks
     ent: torch.Tensor                 # (G, K, M, A) its member dots
     vd_n: torch.Tensor                # (G, K) int32: nested deferred removes per key
-    vd_clock: torch.Tensor            # (G, K, 16, A)
-    vd_mem: torch.Tensor              # (G, K, 16) member bitmasks ((G, K, 16, Mw) past M = 64)
+    vd_clock: torch.Tensor            # (G, K, Vd, A)  (Vd = vd_cap, 16 by default)
+    vd_mem: torch.Tensor              # (G, K, Vd) member bitmasks ((G, K, Vd, Mw) past M = 64)
     flags: torch.Tensor               # (G,) int32
     def_keep: Optional[torch.Tensor]  # (D,) uint8
     def_keys: Optional[torch.Tensor]  # (D, Kw)
@@ -524,15 +524,17 @@ def orswot_lub_many(clock: torch.Tensor, ec: torch.Tensor, oc: torch.Tensor, ent
                     vd_mem: Optional[torch.Tensor] = None, def_off=None, def_row: Optional[torch.Tensor] = None,
                     def_clock: Optional[torch.Tensor] = None, def_keys: Optional[torch.Tensor] = None,
                     ctx: Optional[Context] = None, check: bool = True,
-                    _key_shard: Optional[tuple] = None) -> MapOrswotLub:
+                    _key_shard: Optional[tuple] = None, vd_cap=VD_CAP) -> MapOrswotLub:
     """The exact left fold of Map::merge (map.rs:140-220) for Map<K, Orswot<M>> — orswot.rs:81-149 as
     the value's merge, :150-183 as its forget.  clock (G,R,A) / (R,A), ec and oc (G,R,K,A), ent
     (G,R,K,M,A), all contiguous; the nested deferred removes as a device CSR over (g, r, k): vd_off
     (G*R*K + 1,) int64, vd_clock (Dv, A), vd_mem (Dv,) member bitmasks ((Dv, Mw) words, Mw = ceil(M/64),
     past M = 64); the Map's own deferred pool as for lub_many (host def_off).  A <= 1,024, M <= 1,024
     (past A = 64 or M = 32 the library runs its wide kernel).  check=True raises on flags (bit 1: def_row not sorted / out of
-    range, bit 3: more than 256 live Map removes named one key, bit 4: more than 16 nested deferred
-    removes on one key)."""
+    range, bit 3: more than 256 live Map removes named one key, bit 4: more than vd_cap nested deferred
+    removes on one key).  vd_cap: nested slots per key in the result (>= 16; round 6: the fold keeps 16
+    in LDS and re-folds exactly the keys that need more); "auto" sizes it to the largest sum of one
+    key's nested list lengths over its group's replicas, a bound no fold result can pass."""
     ctx = ctx or Context.default(clock.device.index)
     squeeze = clock.dim() == 2
     c, e, o, m = ((t.unsqueeze(0) if squeeze else t) for t in (clock, ec, oc, ent))
@@ -561,9 +563,16 @@ def orswot_lub_many(clock: torch.Tensor, ec: torch.Tensor, oc: torch.Tensor, ent
                 raise ValueError(f"map.orswot_lub_many: {nm} must be a contiguous {shape} tensor")
             ctx.check_tensor(t, f"map.orswot_lub_many({nm})")
     Kw = (K + 63) // 64 if _key_shard is None else (int(_key_shard[1]) + 63) // 64
+    if vd_cap == "auto":
+        lens = vd_off.view(torch.int64).reshape(-1)
+        lens = (lens[1:] - lens[:-1]).clamp(min=0).reshape(G, R, K).sum(dim=1)
+        vd_cap = max(VD_CAP, int(lens.max().item()) if lens.numel() else 0)
+    Vd = int(vd_cap)
+    if Vd < VD_CAP:
+        raise ValueError(f"map.orswot_lub_many: vd_cap = {Vd} < {VD_CAP}")
     out = [torch.empty(sh, dtype=torch.int64, device=dev)
-           for sh in ((G, A), (G, K, A), (G, K, A), (G, K, M, A), (G, K, VD_CAP, A),
-                      (G, K, VD_CAP) if Mw == 1 else (G, K, VD_CAP, Mw))]
+           for sh in ((G, A), (G, K, A), (G, K, A), (G, K, M, A), (G, K, Vd, A),
+                      (G, K, Vd) if Mw == 1 else (G, K, Vd, Mw))]
     vd_n = torch.empty((G, K), dtype=torch.int32, device=dev)
     flags = torch.empty(G, dtype=torch.int32, device=dev)
     b = _abi.MapOrswotBatch()
@@ -574,7 +583,7 @@ def orswot_lub_many(clock: torch.Tensor, ec: torch.Tensor, oc: torch.Tensor, ent
         b.vd_clock, b.vd_mem = vd_clock.data_ptr(), vd_mem.data_ptr()
     ob = _abi.MapOrswotOut()
     ob.clock, ob.ec, ob.oc, ob.ent, ob.vd_clock, ob.vd_mem = (t.data_ptr() for t in out)
-    ob.vd_n, ob.flags = vd_n.data_ptr(), flags.data_ptr()
+    ob.vd_n, ob.flags, ob.Vd = vd_n.data_ptr(), flags.data_ptr(), Vd
     keep = keys_out = None
     off_arr = None
     if def_off is not None:
@@ -614,7 +623,8 @@ def orswot_lub_many(clock: torch.Tensor, ec: torch.Tensor, oc: torch.Tensor, ent
             raise ValueError("map.orswot_lub_many: vd_off invalid (must start at 0, be non-decreasing and end at "
                              "vd_clock.shape[0])")
         if f & 16:
-            raise RuntimeError("map.orswot_lub_many: more than 16 deferred removes in one key's Orswot")
+            raise RuntimeError(f"map.orswot_lub_many: more than vd_cap = {Vd} deferred removes in one key's Orswot "
+                               "(vd_cap='auto' always fits)")
     oclk, oec, ooc, oent, ovdc, ovdm = out
     if squeeze:
         oclk, oec, ooc, oent, vd_n, ovdc, ovdm = oclk[0], oec[0], ooc[0], oent[0], vd_n[0], ovdc[0], ovdm[0]
@@ -782,6 +792,19 @@ def counter_forget_batch(clock: torch.Tensor, ec: torch.Tensor, val: torch.Tenso
     return keep
 
 
+def _vd_slots(st, N: int, K: int, M: int, A: int, what: str) -> int:
+    """The nested slots per key Vd of a Map<K, Orswot> state layout: vd_clock (N, K, Vd, A), vd_mem
+    (N, K, Vd) or (N, K, Vd, Mw) past M = 64, vd_n (N, K) int32 (crdt_map_orswot_states.Vd)."""
+    Vd = st.vd_clock.shape[2] if st.vd_clock.dim() == 4 else -1
+    Mw = (M + 63) // 64 if M > 64 else 1
+    vm = (N, K, Vd) if Mw == 1 else (N, K, Vd, Mw)
+    if (Vd < VD_CAP or tuple(st.vd_clock.shape) != (N, K, Vd, A) or tuple(st.vd_mem.shape) != vm
+            or tuple(st.vd_n.shape) != (N, K)):
+        raise ValueError(f"{what}: vd_clock (N, K, Vd, A), vd_mem {'(N, K, Vd)' if Mw == 1 else '(N, K, Vd, Mw)'} "
+                         f"with Vd >= {VD_CAP} and vd_n (N, K) expected")
+    return Vd
+
+
 def orswot_forget_batch(res: "MapOrswotLub", y: torch.Tensor, def_clock: Optional[torch.Tensor] = None,
                         def_state: Optional[torch.Tensor] = None,
                         ctx: Optional[Context] = None) -> Optional[torch.Tensor]:
@@ -798,10 +821,11 @@ def orswot_forget_batch(res: "MapOrswotLub", y: torch.Tensor, def_clock: Optiona
     for t in (clock, ec, oc, ent, res.vd_n, res.vd_clock, res.vd_mem):
         if not t.is_contiguous():
             raise ValueError("map.orswot_forget_batch: the result's tensors must be contiguous")
+    Vd = _vd_slots(res, N, K, M, A, "map.orswot_forget_batch")
     y, ys = _forget_clock(ctx, y, N, A, "map.orswot_forget_batch(y)")
     dp, sp, D, keep = _forget_deferred(ctx, def_clock, def_state, N, A, "map.orswot_forget_batch(def_clock)")
     st = _abi.MapOrswotStates()
-    st.N, st.K, st.M, st.A = N, K, M, A
+    st.N, st.K, st.M, st.A, st.Vd = N, K, M, A, Vd
     st.clock, st.ec, st.oc, st.ent = clock.data_ptr(), ec.data_ptr(), oc.data_ptr(), ent.data_ptr()
     st.vd_n, st.vd_clock, st.vd_mem = res.vd_n.data_ptr(), res.vd_clock.data_ptr(), res.vd_mem.data_ptr()
     ctx.call("crdt_map_orswot_forget_batch", ctypes.byref(st), y.data_ptr(), ys, dp, sp, D,
@@ -1037,6 +1061,7 @@ def orswot_apply_batch(res: "MapOrswotLub", def_clock: torch.Tensor, def_keys: t
                                ("mems", _I32), ("clk_pool", _I64)), what)
     st = _abi.MapOrswotStates()
     st.N, st.K, st.M, st.A = N, K, M, A
+    st.Vd = _vd_slots(res, N, K, M, A, what)
     st.clock, st.ec, st.oc, st.ent = clock.data_ptr(), ec.data_ptr(), oc.data_ptr(), ent.data_ptr()
     st.vd_n, st.vd_clock, st.vd_mem = res.vd_n.data_ptr(), res.vd_clock.data_ptr(), res.vd_mem.data_ptr()
     o = _abi.MapOrswotOps()
@@ -1298,6 +1323,7 @@ def orswot_merge_batch(me, other, ctx: Optional[Context] = None) -> torch.Tensor
             raise ValueError(f"{what}: vd_n must be an (N, K) int32 tensor")
         x = _abi.MapOrswotStates()
         x.N, x.K, x.M, x.A = N, K, M, A
+        x.Vd = _vd_slots(st, N, K, M, A, what)
         x.clock, x.ec, x.oc, x.ent = st.clock.data_ptr(), st.ec.data_ptr(), st.oc.data_ptr(), st.ent.data_ptr()
         x.vd_n, x.vd_clock, x.vd_mem = st.vd_n.data_ptr(), st.vd_clock.data_ptr(), st.vd_mem.data_ptr()
         sts.append(x)

@@ -245,8 +245,8 @@ class MapOrswotFrames(NamedTuple):
     oc: torch.Tensor         # (N, K, A)
     ent: torch.Tensor        # (N, K, M, A)
     vd_n: torch.Tensor       # (N, K) int32
-    vd_clock: torch.Tensor   # (N, K, 16, A)
-    vd_mem: torch.Tensor     # (N, K, 16) member bitmasks ((N, K, 16, Mw) past M = 64)
+    vd_clock: torch.Tensor   # (N, K, Vd, A)  (Vd nested slots per key, 16 by default)
+    vd_mem: torch.Tensor     # (N, K, Vd) member bitmasks ((N, K, Vd, Mw) past M = 64)
     def_clock: torch.Tensor  # (N, Dcap, A)
     def_keys: torch.Tensor   # (N, Dcap, Kw)
     def_count: torch.Tensor  # (N,) int32
@@ -314,12 +314,13 @@ def _orswot_struct(ctx, st, what):
     N, K, A = _vmap_check(ctx, st, what)
     M = st.ent.shape[2]
     Mw = (M + 63) // 64
-    vm = (N, K, 16) if Mw == 1 else (N, K, 16, Mw)
+    Vd = st.vd_clock.shape[2] if st.vd_clock.dim() == 4 else 0
+    vm = (N, K, Vd) if Mw == 1 else (N, K, Vd, Mw)
     if (tuple(st.oc.shape) != (N, K, A) or tuple(st.ent.shape) != (N, K, M, A) or tuple(st.vd_n.shape) != (N, K)
-            or tuple(st.vd_clock.shape) != (N, K, 16, A) or tuple(st.vd_mem.shape) != vm):
+            or Vd < 16 or tuple(st.vd_clock.shape) != (N, K, Vd, A) or tuple(st.vd_mem.shape) != vm):
         raise ValueError(f"{what}: the crdt_map_orswot_states shapes expected")
     s = _abi.MapOrswotStates()
-    s.N, s.K, s.M, s.A = N, K, M, A
+    s.N, s.K, s.M, s.A, s.Vd = N, K, M, A, Vd
     s.clock, s.ec, s.oc, s.ent = dptr(st.clock), dptr(st.ec), dptr(st.oc), dptr(st.ent)
     s.vd_n, s.vd_clock, s.vd_mem = dptr(st.vd_n), dptr(st.vd_clock), dptr(st.vd_mem)
     return s, _vmap_deferred(st)
@@ -356,9 +357,9 @@ def map_counter_egress(states: MapCounterFrames, actors: torch.Tensor, keys: tor
 
 
 def map_orswot_ingest(data: torch.Tensor, frame_off: torch.Tensor, actors: torch.Tensor, keys: torch.Tensor,
-                      members: torch.Tensor, Dcap: int, ctx: Optional[Context] = None):
+                      members: torch.Tensor, Dcap: int, ctx: Optional[Context] = None, vd_cap: int = 16):
     """Map<u32, Orswot<u64, u32>> frames -> (MapOrswotFrames, status (N,) int32); members: sorted
-    u64 member dictionary (int64 tensor)."""
+    u64 member dictionary (int64 tensor); vd_cap nested deferred slots per key (>= 16)."""
     ctx = _ctx(data, ctx)
     N = _frames(ctx, data, frame_off, "wire.map_orswot_ingest")
     A = _dict(ctx, actors, torch.int32, "wire.map_orswot_ingest(actors)")
@@ -368,8 +369,8 @@ def map_orswot_ingest(data: torch.Tensor, frame_off: torch.Tensor, actors: torch
     Mw = (M + 63) // 64
     z = lambda *shape: torch.zeros(shape, dtype=torch.int64, device=dev)  # noqa: E731
     st = MapOrswotFrames(z(N, A), z(N, K, A), z(N, K, A), z(N, K, M, A),
-                         torch.zeros((N, K), dtype=torch.int32, device=dev), z(N, K, 16, A),
-                         z(N, K, 16) if Mw == 1 else z(N, K, 16, Mw), z(N, Dcap, A), z(N, Dcap, (K + 63) // 64),
+                         torch.zeros((N, K), dtype=torch.int32, device=dev), z(N, K, vd_cap, A),
+                         z(N, K, vd_cap) if Mw == 1 else z(N, K, vd_cap, Mw), z(N, Dcap, A), z(N, Dcap, (K + 63) // 64),
                          torch.zeros(N, dtype=torch.int32, device=dev))
     s, d = _orswot_struct(ctx, st, "wire.map_orswot_ingest")
     status = _status(N, dev)

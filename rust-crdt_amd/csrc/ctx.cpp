@@ -328,7 +328,7 @@ const char *crdt_last_error(const crdt_ctx *ctx) {
   return ctx ? ctx->last_error.c_str() : g_orphan_error.c_str();
 }
 
-const char *crdt_version(void) { return "0.7.0"; }
+const char *crdt_version(void) { return "0.8.0"; }
 int crdt_abi_version(void) { return CRDT_ABI_VERSION; }
 const char *crdt_build_target(void) { return "gfx950"; }
 

@@ -1037,7 +1037,7 @@ static int map_orswot_lub_host_body(crdt_ctx *ctx, const crdt_map_orswot_batch *
                                     DevScratch &ds) {
   const size_t G = in->G, R = in->R, K = in->K, M = in->M, A = in->A, Kw = (K + 63) / 64, Dv = in->Dv;
   const size_t D = in->def_off ? in->def_off[G] : 0, N = G * R * K;
-  constexpr size_t VD = 16;  // nested deferred slots per key in the output (crdt_gpu.h)
+  const size_t VD = out->Vd ? out->Vd : 16;  // nested deferred slots per key in the output (crdt_gpu.h)
   const size_t Mw = M > 64 ? (M + 63) / 64 : 1;  // member-mask words
   uint64_t *c, *e, *o, *m, *vo, *vc, *vm, *dc, *dk, *oc, *oe, *oo, *om, *ovc, *ovm, *ok2 = nullptr;
   uint32_t *dr, *ovn, *of;
@@ -1086,7 +1086,7 @@ static int map_orswot_lub_host_body(crdt_ctx *ctx, const crdt_map_orswot_batch *
   b.def_row = dr;
   b.def_clock = dc;
   b.def_keys = dk;
-  crdt_map_orswot_out ob{oc, oe, oo, om, ovn, ovc, ovm, of, okp, ok2};
+  crdt_map_orswot_out ob{oc, oe, oo, om, ovn, ovc, ovm, of, okp, ok2, VD};
   {
     DeviceModeScope dev(ctx);
     if (int rc = crdt_map_orswot_lub_many(ctx, &b, &ob)) return rc;

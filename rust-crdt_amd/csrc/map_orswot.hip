@@ -48,6 +48,10 @@ struct MapOrswotPlan {
   const u64 *def_clock, *def_keys;
   u64 *o_clock, *o_ec, *o_oc, *o_ent, *o_vd_clock, *o_vd_mem;
   unsigned *o_vd_n, *o_flags;
+  // round 6: the output's nested slots per key (>= kMoVd; the first kMoVd in LDS during the fold), and
+  // when Vd > kMoVd a per-(g, k) marker: the key's list passed kMoVd, re-fold it deep (pass 2)
+  unsigned long long Vd;
+  uint8_t *ovf;
 };
 
 __device__ __forceinline__ bool mo_nz(u64 x) { return __ballot(x != 0) != 0; }
@@ -537,10 +541,14 @@ __global__ __launch_bounds__(kMoWaves * kWave) void map_orswot_fold_kernel(MapOr
   const int no = pf ? nd : 0;
   for (int i = 0; i < no; ++i) {
     const u64 x = vrow[(unsigned long long)i * kWave + lane];
-    if ((unsigned long long)lane < A) p.o_vd_clock[(gk * kMoVd + i) * A + lane] = x;
-    if (lane == 0) p.o_vd_mem[gk * kMoVd + i] = vmsk[i];
+    if ((unsigned long long)lane < A) p.o_vd_clock[(gk * p.Vd + i) * A + lane] = x;
+    if (lane == 0) p.o_vd_mem[gk * p.Vd + i] = vmsk[i];
   }
   if (lane == 0) p.o_vd_n[gk] = (unsigned)no;
+  if (vfull && p.ovf) {  // past the LDS slots with room in the output: the deep pass re-folds this key
+    if (lane == 0) p.ovf[gk] = 1;
+    vfull = false;
+  }
   if ((bad || full || vfull) && lane == 0)
     atomicOr(p.o_flags + g, (bad ? 2u : 0u) | (full ? 8u : 0u) | (vfull ? 16u : 0u));
 }
@@ -553,19 +561,25 @@ __global__ __launch_bounds__(kMoWaves * kWave) void map_orswot_fold_kernel(MapOr
 // removes naming the key in LDS.  Every replica row is read straight from global memory: a
 // correctness path for shapes past the register kernel's, not a fast one.
 constexpr int kMoWideMw = 16;  // member-mask words (M <= 1,024)
-template <int APL>
+// DEEP (round 6, the exact overflow pass): one wave per workgroup re-folds only the keys the first
+// pass marked in p.ovf, with p.Vd nested slots (their masks in LDS: Vd * Mw words)
+template <int APL, bool DEEP = false>
 __global__ __launch_bounds__(kMoWaves * kWave) void map_orswot_wide_kernel(MapOrswotPlan p) {
   extern __shared__ u64 lds[];
   const int lane = (int)(threadIdx.x % kWave), wv = (int)(threadIdx.x / kWave);
-  const unsigned long long gk = (unsigned long long)blockIdx.x * kMoWaves + wv;
+  const unsigned long long gk = DEEP ? (unsigned long long)blockIdx.x : (unsigned long long)blockIdx.x * kMoWaves + wv;
   if (gk >= p.G * p.K) return;  // (whole waves; nothing below synchronises the workgroup)
+  if constexpr (DEEP) {
+    if (!p.ovf[gk]) return;
+  }
   const unsigned long long g = gk / p.K, k = gk % p.K, A = p.A, R = p.R, K = p.K, M = p.M, Mw = p.Mw;
-  constexpr unsigned long long WQ = kMoList + kMoLive / 2 + kMoVd * kMoWideMw;
+  const unsigned long long WQ = kMoList + kMoLive / 2 + (DEEP ? p.Vd * Mw : (unsigned long long)kMoVd * kMoWideMw);
+  const int cap = DEEP ? (int)p.Vd : kMoVd;
   u64 *lst = lds + (unsigned long long)wv * WQ;
   uint32_t *live = reinterpret_cast<uint32_t *>(lst + kMoList);
-  u64 *vmsk = lst + kMoList + kMoLive / 2;  // [kMoVd][Mw] nested removes' member masks
+  u64 *vmsk = lst + kMoList + kMoLive / 2;  // [cap][Mw] nested removes' member masks
   u64 *wE = p.o_ent + gk * M * A;           // [M][A] the key's member rows (working state)
-  u64 *wV = p.o_vd_clock + gk * kMoVd * A;  // [kMoVd][A] its nested deferred rm rows
+  u64 *wV = p.o_vd_clock + gk * p.Vd * A;   // [cap][A] its nested deferred rm rows
   // row I/O: word j of the lane is actor lane + 64 j; words past A read 0 and are never written
   auto ldr = [&](const u64 *row, u64 (&x)[APL]) {
 #pragma unroll
@@ -682,7 +696,7 @@ __global__ __launch_bounds__(kMoWaves * kWave) void map_orswot_wide_kernel(MapOr
         return;
       }
     }
-    if (nd < kMoVd) {
+    if (nd < cap) {
       str(wV + (unsigned long long)nd * A, rm);
       for (unsigned long long w = (unsigned long long)lane; w < Mw; w += kWave) vmsk[nd * Mw + w] = msk[w];
       ++nd;
@@ -897,8 +911,14 @@ __global__ __launch_bounds__(kMoWaves * kWave) void map_orswot_wide_kernel(MapOr
   const int no = pf ? nd : 0;
   for (int i = 0; i < no; ++i)
     for (unsigned long long w = (unsigned long long)lane; w < Mw; w += kWave)
-      p.o_vd_mem[(gk * kMoVd + i) * Mw + w] = vmsk[i * Mw + w];
+      p.o_vd_mem[(gk * p.Vd + i) * Mw + w] = vmsk[i * Mw + w];
   if (lane == 0) p.o_vd_n[gk] = (unsigned)no;
+  if constexpr (!DEEP) {
+    if (vfull && p.ovf) {  // (as the register kernel: the deep pass re-folds this key)
+      if (lane == 0) p.ovf[gk] = 1;
+      vfull = false;
+    }
+  }
   if ((bad || full || vfull) && lane == 0)
     atomicOr(p.o_flags + g, (bad ? 2u : 0u) | (full ? 8u : 0u) | (vfull ? 16u : 0u));
 }
@@ -928,6 +948,22 @@ template <int APL>
 static hipError_t launch_mo_wide(const MapOrswotPlan &p, hipStream_t s) {
   const unsigned long long blocks = (p.G * p.K + kMoWaves - 1) / kMoWaves;
   hipLaunchKernelGGL((map_orswot_wide_kernel<APL>), dim3((unsigned)blocks), dim3(kMoWaves * kWave), mo_wide_lds(), s, p);
+  return hipGetLastError();
+}
+
+// the deep pass's LDS: one wave, its Map-remove lists and Vd nested member masks
+static size_t mo_deep_lds(size_t Vd, size_t Mw) { return kMoList * 8 + kMoLive * 4 + Vd * Mw * 8; }
+constexpr size_t kMoDeepLds = 160 * 1024;  // (one workgroup per CU at the most)
+
+template <int APL>
+static hipError_t launch_mo_deep(const MapOrswotPlan &p, hipStream_t s) {
+  const size_t lds = mo_deep_lds(p.Vd, p.Mw);
+  if (lds > 64 * 1024) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&map_orswot_wide_kernel<APL, true>),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL((map_orswot_wide_kernel<APL, true>), dim3((unsigned)(p.G * p.K)), dim3(kWave), lds, s, p);
   return hipGetLastError();
 }
 
@@ -969,13 +1005,20 @@ extern "C" int crdt_map_orswot_lub_many(crdt_ctx *ctx, const crdt_map_orswot_bat
   if (D > 0 && (!in->def_row || !in->def_clock || !in->def_keys || !out->def_keep || !out->def_keys))
     return fail(ctx, CRDT_EINVAL, "map_orswot_lub_many: deferred buffers missing");
   if (D > 0xffffffffULL) return fail(ctx, CRDT_EUNSUPPORTED, "map_orswot_lub_many: too many deferred");
+  const size_t Vd = out->Vd ? out->Vd : (size_t)kMoVd, Mw0 = (M + 63) / 64 > 0 ? (M + 63) / 64 : 1;
+  if (Vd < (size_t)kMoVd) return fail(ctx, CRDT_EINVAL, "map_orswot_lub_many: out->Vd = %zu < %d", Vd, kMoVd);
+  if (Vd > (size_t)kMoVd && mo_deep_lds(Vd, Mw0) > kMoDeepLds)
+    return fail(ctx, CRDT_EUNSUPPORTED, "map_orswot_lub_many: out->Vd = %zu nested slots of %zu mask words exceed the LDS",
+                Vd, Mw0);
+  if (Vd > (size_t)kMoVd && G * K > 0x7fffffffULL)
+    return fail(ctx, CRDT_EUNSUPPORTED, "map_orswot_lub_many: G*K too large for the deep pass");
   CRDT_HIP(ctx, hipSetDevice(ctx->device));
   const size_t Kw = (K + 63) / 64;
   MapOrswotPlan p{(const u64 *)in->clock, (const u64 *)in->ec, (const u64 *)in->oc, (const u64 *)in->ent,
                   (const u64 *)in->vd_off, (const u64 *)in->vd_clock, (const u64 *)in->vd_mem, in->Dv, G, R, K, M, A, Kw,
                   (M + 63) / 64 > 0 ? (M + 63) / 64 : 1, nullptr, in->def_row, (const u64 *)in->def_clock, (const u64 *)in->def_keys,
                   (u64 *)out->clock, (u64 *)out->ec, (u64 *)out->oc, (u64 *)out->ent, (u64 *)out->vd_clock,
-                  (u64 *)out->vd_mem, out->vd_n, out->flags};
+                  (u64 *)out->vd_mem, out->vd_n, out->flags, Vd, nullptr};
   if (int rc = device_fill(ctx, out->flags, G * sizeof(unsigned), 0)) return rc;
   if (R == 0) {  // fold of nothing: Map::new()
     if (int rc = device_fill(ctx, out->clock, G * A * 8, 0)) return rc;
@@ -985,10 +1028,18 @@ extern "C" int crdt_map_orswot_lub_many(crdt_ctx *ctx, const crdt_map_orswot_bat
       if (int rc = device_fill(ctx, out->ent, G * K * M * A * 8, 0)) return rc;
     if (int rc = device_fill(ctx, out->vd_n, G * K * sizeof(unsigned), 0)) return rc;
   } else {
+    // scratch: [def_off (G+1) when D > 0][the deep pass's per-(g, k) markers when Vd > 16]
+    const size_t so = D > 0 ? (G + 1) * sizeof(size_t) : 0, sv = Vd > (size_t)kMoVd ? G * K : 0;
+    if (so + sv) {
+      if (int rc = ensure_scratch(ctx, so + sv)) return rc;
+    }
     if (D > 0) {
-      if (int rc = ensure_scratch(ctx, (G + 1) * sizeof(size_t))) return rc;
       if (int rc = stage_h2d(ctx, ctx->scratch, in->def_off, (G + 1) * sizeof(size_t))) return rc;
       p.def_off = reinterpret_cast<const size_t *>(ctx->scratch);
+    }
+    if (sv) {
+      p.ovf = static_cast<uint8_t *>(ctx->scratch) + so;
+      if (int rc = device_fill(ctx, p.ovf, sv, 0)) return rc;
     }
     {
       const unsigned long long n = (unsigned long long)G * R * K;
@@ -1015,8 +1066,16 @@ extern "C" int crdt_map_orswot_lub_many(crdt_ctx *ctx, const crdt_map_orswot_bat
                           : M <= 4   ? launch_mo<4>(p, ctx->stream)
                           : M <= 8   ? launch_mo<8>(p, ctx->stream)
                                      : launch_mo<32>(p, ctx->stream);
-    timing_end(ctx);
     if (he != hipSuccess) return hip_fail(ctx, he, "map_orswot_fold_kernel launch");
+    if (sv) {  // the deep pass: the marked keys again, exactly, with all Vd nested slots
+      const hipError_t hd = A <= 64    ? launch_mo_deep<1>(p, ctx->stream)
+                            : A <= 128 ? launch_mo_deep<2>(p, ctx->stream)
+                            : A <= 256 ? launch_mo_deep<4>(p, ctx->stream)
+                            : A <= 512 ? launch_mo_deep<8>(p, ctx->stream)
+                                       : launch_mo_deep<16>(p, ctx->stream);
+      if (hd != hipSuccess) return hip_fail(ctx, hd, "map_orswot deep pass launch");
+    }
+    timing_end(ctx);
   }
   if (D == 0) return CRDT_OK;
   DefPlan q{};  // the Map's surviving removes (!(rm <= C_final)), identical clocks merged

@@ -31,7 +31,7 @@ namespace crdt {
 #define CRDT_MOA_WPE1 CRDT_MOA_WPE
 #endif
 
-constexpr int kMoaVd = 16;    // nested deferred slots per key (crdt_map_orswot_out)
+constexpr int kMoaVd = 16;    // nested deferred slots per key by default (crdt_map_orswot_states.Vd)
 constexpr int kMoaMw = 16;    // member-mask words (M <= 1,024)
 constexpr size_t kMoaDl = 16;  // the Map's deferred slots held in LDS per state (the rest of Dcap in place)
 
@@ -58,6 +58,8 @@ struct MapOrswotApplyPlan {
   unsigned *status;
   unsigned wpb;
   u64 *resume = nullptr;  // [N] (Dcap > Dl): op offset where a state continues in pass 2, or kMoaDone
+  unsigned long long Vd = kMoaVd;  // nested deferred slots per key (round 6: any, their masks in LDS)
+  unsigned long long VW = (unsigned long long)kMoaVd * kMoaMw;  // LDS words for them: max(256, Vd * Mw)
 };
 constexpr u64 kMoaDone = ~0ull;
 
@@ -82,12 +84,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APL <= 2 ? 
     if (p.resume[s] == kMoaDone) return;
   }
   const unsigned long long A = p.A, K = p.K, M = p.M, Mw = p.Mw, Kw = p.Kw, Dcap = p.Dcap, Dl = p.Dl;
-  const unsigned long long WQ = Dl * (A + Kw) + kMoaVd * kMoaMw;
+  const unsigned long long WQ = Dl * (A + Kw) + p.VW;
   // The Map's deferred removes: slots d < Dl in LDS, slots Dl <= d < Dcap in the caller's own slot
   // arrays (global memory: a long list runs slower, never incomplete below Dcap)
   u64 *sclk = lds + (unsigned long long)wv * WQ;  // [Dl][A] the Map's rm clocks
   u64 *skey = sclk + Dl * A;                       // [Dl][Kw] their key bitmaps
-  u64 *smsk = skey + Dl * Kw;                      // [16][Mw] the current key's nested member masks
+  u64 *smsk = skey + Dl * Kw;                      // [Vd][Mw] the current key's nested member masks
   const unsigned long long ob = p.op_off[s], oe = p.op_off[s + 1];
   unsigned dcnt = p.def_count[s];
   if (dcnt > Dcap || oe < ob || oe > p.n_ops) {
@@ -180,8 +182,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APL <= 2 ? 
   };
   auto keyp = [&](unsigned long long k) {
     const unsigned long long sk = s * K + k;
-    return Keyp{p.ec + sk * A, p.oc + sk * A, p.ent + sk * M * A, p.vd_clock + sk * kMoaVd * A,
-                p.vd_mem + sk * kMoaVd * Mw, p.vd_n + sk};
+    return Keyp{p.ec + sk * A, p.oc + sk * A, p.ent + sk * M * A, p.vd_clock + sk * p.Vd * A,
+                p.vd_mem + sk * p.Vd * Mw, p.vd_n + sk};
   };
   auto stage_masks = [&](const Keyp &q, unsigned n) {  // global -> LDS (lane w % 64 moves word w)
     for (unsigned i = 0; i < n; ++i)
@@ -239,7 +241,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APL <= 2 ? 
       for (int j = 0; j < APL; ++j) x[j] = x[j] > r[j] ? x[j] : 0ull;
       strow(q.ent + m * A, x);
     }
-    const unsigned n = *q.vn;
+    const unsigned n = min((unsigned)p.Vd, *q.vn);  // (a count past the slots: clamped)
     if (n == 0) return;
     stage_masks(q, n);
     unsigned o = 0;
@@ -362,7 +364,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APL <= 2 ? 
 #pragma unroll
           for (int j = 0; j < APL; ++j)
             if ((unsigned)j == va / 64 && (unsigned long long)lane == va % 64 && oc[j] < vc) oc[j] = vc;
-          const unsigned n = *q.vn;
+          const unsigned n = min((unsigned)p.Vd, *q.vn);  // (a count past the slots: clamped)
           if (n > 0) {
             stage_masks(q, n);
             unstage_masks(q, nested_apply_deferred(q, n, oc));
@@ -388,7 +390,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APL <= 2 ? 
             strow(q.ent + m * A, x);
           }
           if (!leq(r, oc)) {  // !(clock <= self.clock): deferred, an equal clock's members unioned
-            unsigned n = *q.vn;
+            unsigned n = min((unsigned)p.Vd, *q.vn);
             stage_masks(q, n);
             int slot = -1;
             for (unsigned i = 0; i < n && slot < 0; ++i) {
@@ -399,7 +401,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(APL <= 2 ? 
               for (int j = 0; j < APL; ++j) ne = ne || y[j] != r[j];
               if (!__ballot(ne)) slot = (int)i;
             }
-            if (slot < 0 && n >= (unsigned)kMoaVd) {
+            if (slot < 0 && n >= p.Vd) {
               st |= 1u;  // nested deferred capacity exceeded
             } else {
               if (slot < 0) {
@@ -513,10 +515,12 @@ extern "C" int crdt_map_orswot_apply_batch(crdt_ctx *ctx, const crdt_map_orswot_
                      !ops->vcounter || !ops->clk_row))
     return fail(ctx, CRDT_EINVAL, "map_orswot_apply_batch: NULL op buffer");
   const size_t Kw = K ? (K + 63) / 64 : 1, Mw = M > 64 ? (M + 63) / 64 : 1;
+  const size_t Vd = m->Vd ? m->Vd : (size_t)kMoaVd, VW = std::max<size_t>((size_t)kMoaVd * kMoaMw, Vd * Mw);
+  if (VW > 8192 - 64) return fail(ctx, CRDT_EUNSUPPORTED, "map_orswot_apply_batch: Vd * Mw = %zu words past the LDS", Vd * Mw);
   // the Map's deferred slots in LDS: up to kMoaDl (the rest of Dcap in the caller's slot arrays), fewer
-  // where a slot is wide (the wave's LDS at most 8,192 words)
-  const size_t Dl = std::min<size_t>(Dcap, std::min<size_t>(kMoaDl, (8192 - kMoaVd * kMoaMw) / (A + Kw)));
-  const size_t per_wave = (Dl * (A + Kw) + kMoaVd * kMoaMw) * 8;
+  // where a slot is wide (the wave's LDS at most 8,192 words, the nested masks' VW words included)
+  const size_t Dl = std::min<size_t>(Dcap, std::min<size_t>(kMoaDl, (8192 - VW) / (A + Kw)));
+  const size_t per_wave = (Dl * (A + Kw) + VW) * 8;
   unsigned wpb = 4;
   while (wpb > 1 && per_wave * wpb > 64 * 1024) --wpb;
   CRDT_HIP(ctx, hipSetDevice(ctx->device));
@@ -526,7 +530,7 @@ extern "C" int crdt_map_orswot_apply_batch(crdt_ctx *ctx, const crdt_map_orswot_
                        (const u64 *)ops->counter, (const u64 *)ops->vcounter, ops->clk_row,
                        (const u64 *)ops->clk_pool, ops->clk_pool ? ops->n_clk_rows : 0, (const u64 *)ops->key_off,
                        ops->keys, ops->keys ? ops->n_keys : 0, (const u64 *)ops->mem_off, ops->mems,
-                       ops->mems ? ops->n_mems : 0, ops->n_ops, status, wpb};
+                       ops->mems ? ops->n_mems : 0, ops->n_ops, status, wpb, nullptr, Vd, VW};
   // scratch: [resume: N words when Dcap > Dl][zero key_off: n_ops + 1 words when there is none]
   const size_t kz = ops->key_off ? 0 : (ops->n_ops + 1) * 8, rz = Dcap > Dl ? N * 8 : 0;
   if (kz + rz) {
@@ -556,10 +560,10 @@ extern "C" int crdt_map_orswot_apply_batch(crdt_ctx *ctx, const crdt_map_orswot_
     go(std::integral_constant<int, 1>{}, grid, block, lds);
     // pass 2: the few states pass 1 handed on (the rest exit at once), one wave per workgroup with the
     // whole wave-LDS budget as slots (up to 64 KiB), so a long list mostly stays out of global memory
-    const size_t Dl2 = std::min<size_t>(Dcap, (8192 - kMoaVd * kMoaMw) / (A + Kw));
+    const size_t Dl2 = std::min<size_t>(Dcap, (8192 - VW) / (A + Kw));
     p.Dl = Dl2;
     p.wpb = 1;
-    go(std::integral_constant<int, 2>{}, dim3((unsigned)N), dim3(kWave), (Dl2 * (A + Kw) + kMoaVd * kMoaMw) * 8);
+    go(std::integral_constant<int, 2>{}, dim3((unsigned)N), dim3(kWave), (Dl2 * (A + Kw) + VW) * 8);
   }
   timing_end(ctx);
   CRDT_HIP(ctx, hipGetLastError());

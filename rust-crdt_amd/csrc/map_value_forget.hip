@@ -17,14 +17,13 @@
 
 namespace crdt {
 
-constexpr int kMvfVd = 16;  // nested deferred slots per key (crdt_map_orswot_out)
-
 // one wave per (state, key): the key's nested deferred list after the forget by y[s]
 template <int APL>
 __global__ __launch_bounds__(256) void map_orswot_vd_forget_kernel(const u64 *ec, unsigned *vd_n, u64 *vd_clock,
                                                                    u64 *vd_mem, const u64 *y, unsigned long long y_stride,
                                                                    unsigned long long N, unsigned long long K,
-                                                                   unsigned long long A, unsigned long long Mw) {
+                                                                   unsigned long long A, unsigned long long Mw,
+                                                                   unsigned long long Vd) {
   const int lane = (int)(threadIdx.x % kWave);
   const unsigned long long sk = (unsigned long long)blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
   if (sk >= N * K) return;  // (whole waves)
@@ -43,10 +42,10 @@ __global__ __launch_bounds__(256) void map_orswot_vd_forget_kernel(const u64 *ec
     if (lane == 0) vd_n[sk] = 0;
     return;
   }
-  u64 *rows = vd_clock + sk * kMvfVd * A;
-  u64 *msk = vd_mem + sk * kMvfVd * Mw;
+  u64 *rows = vd_clock + sk * Vd * A;  // [Vd][A] the key's nested slots (Vd: crdt_map_orswot_states)
+  u64 *msk = vd_mem + sk * Vd * Mw;
   unsigned o = 0;
-  for (unsigned i = 0; i < nd && i < (unsigned)kMvfVd; ++i) {
+  for (unsigned i = 0; i < nd && i < Vd; ++i) {
     u64 x[APL];
     bool nz = false;
 #pragma unroll
@@ -140,7 +139,7 @@ extern "C" int crdt_map_orswot_forget_batch(crdt_ctx *ctx, const crdt_map_orswot
   hipLaunchKernelGGL(map_orswot_vd_forget_kernel<APL>, dim3((unsigned)blocks), dim3(256), 0, ctx->stream,       \
                      (const u64 *)m->ec, m->vd_n, (u64 *)m->vd_clock, (u64 *)m->vd_mem, (const u64 *)y,         \
                      (unsigned long long)y_stride, (unsigned long long)N, (unsigned long long)K,                \
-                     (unsigned long long)A, (unsigned long long)Mw)
+                     (unsigned long long)A, (unsigned long long)Mw, (unsigned long long)(m->Vd ? m->Vd : 16))
   if (A <= 64) MVF(1);
   else if (A <= 128) MVF(2);
   else if (A <= 256) MVF(4);

@@ -45,20 +45,22 @@ __global__ __launch_bounds__(64) void vmm_pool_kernel(unsigned long long N, unsi
   }
 }
 
-// nested slot lists (cnt [N][K], rows [N][K][16][A], words [N][K][16][W]) of both sides as a CSR over
-// (pair, side, key): voff[(i*2 + s)*K + k] = the first row
+// nested slot lists (cnt [N][K], rows [N][K][S][A], words [N][K][S][W], S = Sa / Sb slots per key) of
+// both sides as a CSR over (pair, side, key): voff[(i*2 + s)*K + k] = the first row
 __global__ __launch_bounds__(64) void vmm_csr_kernel(unsigned long long N, unsigned long long K, unsigned long long A,
                                                      unsigned long long W, const unsigned *na, const u64 *ca,
                                                      const u64 *wa, const unsigned *nb, const u64 *cb, const u64 *wb,
-                                                     const u64 *voff, u64 *oc, u64 *ow) {
+                                                     const u64 *voff, u64 *oc, u64 *ow, unsigned long long Sa,
+                                                     unsigned long long Sb) {
   const unsigned long long b = blockIdx.x;  // (i, s, k)
   if (b >= N * 2 * K) return;
   const unsigned long long i = b / (2 * K), s = (b / K) % 2, k = b % K;
   const unsigned lane = threadIdx.x;
   const unsigned long long sk = i * K + k;
   const unsigned n = s ? nb[sk] : na[sk];
-  const u64 *c = (s ? cb : ca) + sk * 16 * A;
-  const u64 *w = (s ? wb : wa) + sk * 16 * W;
+  const unsigned long long S = s ? Sb : Sa;
+  const u64 *c = (s ? cb : ca) + sk * S * A;
+  const u64 *w = (s ? wb : wa) + sk * S * W;
   const unsigned long long d0 = voff[b];
   for (unsigned j = 0; j < n; ++j) {
     for (unsigned long long a = lane; a < A; a += 64) oc[(d0 + j) * A + a] = c[j * A + a];
@@ -140,9 +142,9 @@ int pool_offsets(crdt_ctx *ctx, const crdt_map_deferred *ad, const crdt_map_defe
   return CRDT_OK;
 }
 
-// the nested lists' CSR offsets over (pair, side, key) from both sides' counts (<= 16 each)
+// the nested lists' CSR offsets over (pair, side, key) from both sides' counts (<= each side's slots)
 int nested_offsets(crdt_ctx *ctx, const uint32_t *na, const uint32_t *nb, size_t N, size_t K,
-                   std::vector<u64> &voff, const char *what) {
+                   std::vector<u64> &voff, const char *what, size_t ca = 16, size_t cb = 16) {
   std::vector<uint32_t> ha, hb;
   if (int rc = read_counts(ctx, na, N * K, ha)) return rc;
   if (int rc = read_counts(ctx, nb, N * K, hb)) return rc;
@@ -152,7 +154,7 @@ int nested_offsets(crdt_ctx *ctx, const uint32_t *na, const uint32_t *nb, size_t
     for (size_t s = 0; s < 2; ++s)
       for (size_t k = 0; k < K; ++k, ++b) {
         const uint32_t n = s ? hb[i * K + k] : ha[i * K + k];
-        if (n > 16) return fail(ctx, CRDT_EINVAL, "%s: a nested deferred count above 16", what);
+        if (n > (s ? cb : ca)) return fail(ctx, CRDT_EINVAL, "%s: a nested deferred count above its slots", what);
         voff[b + 1] = voff[b] + n;
       }
   return CRDT_OK;
@@ -318,7 +320,8 @@ extern "C" int crdt_map_orswot_merge_batch(crdt_ctx *ctx, const crdt_map_orswot_
   std::vector<size_t> off;
   if (int rc = pool_offsets(ctx, ad, bd, N, off, what)) return rc;
   std::vector<u64> voff;
-  if (int rc = nested_offsets(ctx, a->vd_n, b->vd_n, N, K, voff, what)) return rc;
+  const size_t Va = a->Vd ? a->Vd : 16, Vb = b->Vd ? b->Vd : 16;  // nested slots per key, each side
+  if (int rc = nested_offsets(ctx, a->vd_n, b->vd_n, N, K, voff, what, Va, Vb)) return rc;
   const size_t D = off[N], Dv = voff[N * 2 * K];
   Carve cv;
   const size_t c2 = cv.take(N * 2 * A * 8), e2 = cv.take(N * 2 * K * A * 8), o2 = cv.take(N * 2 * K * A * 8);
@@ -338,7 +341,8 @@ extern "C" int crdt_map_orswot_merge_batch(crdt_ctx *ctx, const crdt_map_orswot_
                        (unsigned long long)K, (unsigned long long)A, (unsigned long long)Mw, a->vd_n,
                        (const u64 *)a->vd_clock, (const u64 *)a->vd_mem, b->vd_n, (const u64 *)b->vd_clock,
                        (const u64 *)b->vd_mem, reinterpret_cast<const u64 *>(base + vo),
-                       reinterpret_cast<u64 *>(base + vc), reinterpret_cast<u64 *>(base + vm));
+                       reinterpret_cast<u64 *>(base + vc), reinterpret_cast<u64 *>(base + vm), (unsigned long long)Va,
+                       (unsigned long long)Vb);
     CRDT_HIP(ctx, hipGetLastError());
   }
   Pool pl;
@@ -369,6 +373,7 @@ extern "C" int crdt_map_orswot_merge_batch(crdt_ctx *ctx, const crdt_map_orswot_
   out.vd_n = a->vd_n;
   out.vd_clock = a->vd_clock;
   out.vd_mem = a->vd_mem;
+  out.Vd = Va;  // (self's slots: other's lists merge into them, bit 3 past Va)
   out.flags = reinterpret_cast<uint32_t *>(base + of);
   out.def_keep = pl.keep;
   out.def_keys = reinterpret_cast<uint64_t *>(pl.kout);
@@ -424,7 +429,7 @@ extern "C" int crdt_map_nested_merge_batch(crdt_ctx *ctx, const crdt_map_nested_
                        (unsigned long long)K, (unsigned long long)A, (unsigned long long)K2w, a->id_n, (const u64 *)a->id_clock,
                        (const u64 *)a->id_keys, b->id_n, (const u64 *)b->id_clock, (const u64 *)b->id_keys,
                        reinterpret_cast<const u64 *>(base + io), reinterpret_cast<u64 *>(base + ic),
-                       reinterpret_cast<u64 *>(base + ik));
+                       reinterpret_cast<u64 *>(base + ik), 16ull, 16ull);
     CRDT_HIP(ctx, hipGetLastError());
   }
   Pool pl;

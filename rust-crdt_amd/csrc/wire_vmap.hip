@@ -41,7 +41,8 @@ struct VMapWirePlan {
   u64 *clock, *ec, *val;           // [N][A], [N][K][A], counter [N][K][W][A]
   u64 *oc, *ent;                   // Orswot [N][K][A], [N][K][M][A]
   uint32_t *vd_n;                  // [N][K]
-  u64 *vd_clock, *vd_mem;          // [N][K][16][A], [N][K][16][Mw]
+  u64 *vd_clock, *vd_mem;          // [N][K][Vd][A], [N][K][Vd][Mw]
+  unsigned long long Vd;           // nested Orswot slots per key (crdt_map_orswot_states.Vd; 16 if 0)
   u64 *def_clock, *def_keys;       // [N][Dcap][A], [N][Dcap][Kw]
   uint32_t *def_count;             // [N]
   uint32_t *status;
@@ -257,9 +258,9 @@ __global__ __launch_bounds__(kBlock) void vmap_ingest_kernel(VMapWirePlan p) {
           k = parse_idset(f, k, true, nullptr, members, p.M, bits, p.Mw, lane, st);
           if (k == ~0ull) break;
           if (ki >= 0) {
-            if (vn < (unsigned long long)kVwVd) {
-              store_row<u64>(p.vd_clock + (sk * kVwVd + vn) * p.A, row, p.A, lane);
-              store_row<u64>(p.vd_mem + (sk * kVwVd + vn) * p.Mw, bits, p.Mw, lane);
+            if (vn < p.Vd) {
+              store_row<u64>(p.vd_clock + (sk * p.Vd + vn) * p.A, row, p.A, lane);
+              store_row<u64>(p.vd_mem + (sk * p.Vd + vn) * p.Mw, bits, p.Mw, lane);
               ++vn;
             } else {
               st |= kWireCap;
@@ -431,14 +432,14 @@ __global__ __launch_bounds__(kBlock) void vmap_egress_kernel(VMapWirePlan p, int
           k = write_vclock(w, k + 2, mr, p.A, p.actors, lane);
         }
       }
-      const unsigned long long vn = p.vd_n[sk] < (uint32_t)kVwVd ? p.vd_n[sk] : kVwVd;
+      const unsigned long long vn = p.vd_n[sk] < p.Vd ? p.vd_n[sk] : p.Vd;
       sz += 8;
       if (write) {
         if (lane == 0) wr64(w, k, vn);
         k += 2;
       }
       for (unsigned long long i = 0; i < vn; ++i) {
-        const u64 *rm = p.vd_clock + (sk * kVwVd + i) * p.A, *mb = p.vd_mem + (sk * kVwVd + i) * p.Mw;
+        const u64 *rm = p.vd_clock + (sk * p.Vd + i) * p.A, *mb = p.vd_mem + (sk * p.Vd + i) * p.Mw;
         sz += vclock_bytes(rm, p.A, lane) + 8 + 8 * popc_row(mb, p.Mw, lane);
         if (write) {
           k = write_vclock(w, k, rm, p.A, p.actors, lane);
@@ -530,6 +531,7 @@ static int vmap_orswot_plan(crdt_ctx *ctx, const crdt_map_orswot_states *st, con
   p.vd_n = st->vd_n;
   p.vd_clock = (u64 *)st->vd_clock;
   p.vd_mem = (u64 *)st->vd_mem;
+  p.Vd = st->Vd ? st->Vd : (size_t)kVwVd;
   return CRDT_OK;
 }
 
@@ -594,8 +596,8 @@ static int vmap_ingest(crdt_ctx *ctx, VMapWirePlan &p, const uint8_t *bytes, con
     if (int rc = device_fill(ctx, p.oc, N * p.K * p.A * 8, 0)) return rc;
     if (int rc = device_fill(ctx, p.ent, N * p.K * p.M * p.A * 8, 0)) return rc;
     if (int rc = device_fill(ctx, p.vd_n, N * p.K * 4, 0)) return rc;
-    if (int rc = device_fill(ctx, p.vd_clock, N * p.K * kVwVd * p.A * 8, 0)) return rc;
-    if (int rc = device_fill(ctx, p.vd_mem, N * p.K * kVwVd * p.Mw * 8, 0)) return rc;
+    if (int rc = device_fill(ctx, p.vd_clock, N * p.K * p.Vd * p.A * 8, 0)) return rc;
+    if (int rc = device_fill(ctx, p.vd_mem, N * p.K * p.Vd * p.Mw * 8, 0)) return rc;
   }
   p.bytes = bytes;
   p.frame_off = (const u64 *)frame_off;

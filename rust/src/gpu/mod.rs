@@ -1362,6 +1362,19 @@ fn orswot_map_folds<K: Ord + Clone, M: Member, A: Actor>(ctx: &GpuCtx, groups: &
     }
     let pool = group_pool(groups, &actors, &keys);
     let (nd, dv) = (pool.def_row.len(), vd_mem.len() / mw);
+    // nested slots per key: the largest sum of one key's list lengths over its group (no fold result
+    // holds more), at least the library's 16 (round 6: past 16 the library re-folds those keys exactly)
+    let mut vdc = 16usize;
+    for gi in 0..g {
+        for j in 0..k {
+            let mut t = 0usize;
+            for ri in 0..r {
+                let b = (gi * r + ri) * k + j;
+                t += (vd_off[b + 1] - vd_off[b]) as usize;
+            }
+            vdc = vdc.max(t);
+        }
+    }
     let batch = ffi::crdt_map_orswot_batch {
         G: g, R: r, K: k, M: m, A: a,
         clock: clock.as_ptr(), ec: ec.as_ptr(), oc: oc.as_ptr(), ent: ent.as_ptr(),
@@ -1372,13 +1385,14 @@ fn orswot_map_folds<K: Ord + Clone, M: Member, A: Actor>(ctx: &GpuCtx, groups: &
     };
     let (mut o_clock, mut o_ec, mut o_oc) = (vec![0u64; g * a], vec![0u64; g * k * a], vec![0u64; g * k * a]);
     let (mut o_ent, mut o_vdn) = (vec![0u64; g * k * m * a], vec![0u32; g * k]);
-    let (mut o_vdc, mut o_vdm) = (vec![0u64; g * k * 16 * a], vec![0u64; g * k * 16 * mw]);
+    let (mut o_vdc, mut o_vdm) = (vec![0u64; g * k * vdc * a], vec![0u64; g * k * vdc * mw]);
     let (mut flags, mut keep, mut okeys) = (vec![0u32; g], vec![0u8; nd], vec![0u64; nd * kw]);
     let mut out = ffi::crdt_map_orswot_out {
         clock: o_clock.as_mut_ptr(), ec: o_ec.as_mut_ptr(), oc: o_oc.as_mut_ptr(), ent: o_ent.as_mut_ptr(),
         vd_n: o_vdn.as_mut_ptr(), vd_clock: o_vdc.as_mut_ptr(), vd_mem: o_vdm.as_mut_ptr(), flags: flags.as_mut_ptr(),
         def_keep: if nd > 0 { keep.as_mut_ptr() } else { ptr::null_mut() },
         def_keys: if nd > 0 { okeys.as_mut_ptr() } else { ptr::null_mut() },
+        Vd: vdc,
     };
     ctx.check_host(unsafe { ffi::crdt_map_orswot_lub_many(ctx.host, &batch, &mut out) })?;
     if let Some(f) = flags.iter().find(|&&f| f != 0) {
@@ -1403,10 +1417,10 @@ fn orswot_map_folds<K: Ord + Clone, M: Member, A: Actor>(ctx: &GpuCtx, groups: &
                 }
             }
             for i in 0..o_vdn[b] as usize {
-                let bits = &o_vdm[(b * 16 + i) * mw..(b * 16 + i + 1) * mw];
+                let bits = &o_vdm[(b * vdc + i) * mw..(b * vdc + i + 1) * mw];
                 let ms: HashSet<M> =
                     (0..m).filter(|&x| (bits[x / 64] >> (x % 64)) & 1 != 0).map(|x| mems.ids[x].clone()).collect();
-                o.deferred.entry(row_clock(&o_vdc[(b * 16 + i) * a..(b * 16 + i + 1) * a], &actors))
+                o.deferred.entry(row_clock(&o_vdc[(b * vdc + i) * a..(b * vdc + i + 1) * a], &actors))
                     .or_insert_with(HashSet::new).extend(ms);
             }
             mp.entries.insert(key.clone(), Entry { clock: row_clock(row, &actors), val: o });

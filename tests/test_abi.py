@@ -32,7 +32,7 @@ def test_library_exports_every_declared_symbol():
     import crdts_gpu._abi as abi
     assert sorted(abi.EXPORTS) == declared()
     lib.crdt_version.restype = ctypes.c_char_p
-    assert lib.crdt_version() == b"0.7.0"
+    assert lib.crdt_version() == b"0.8.0"
     lib.crdt_build_target.restype = ctypes.c_char_p
     assert lib.crdt_build_target() == b"gfx950"
 
@@ -62,7 +62,8 @@ def test_ctypes_struct_layout_matches_header():
     assert ctypes.sizeof(abi.MapCounterBatch) == 18 * 8
     assert ctypes.sizeof(abi.MapCounterOut) == 6 * 8
     assert ctypes.sizeof(abi.MapOrswotBatch) == 17 * 8
-    assert ctypes.sizeof(abi.MapOrswotOut) == 10 * 8
+    assert ctypes.sizeof(abi.MapOrswotOut) == 11 * 8  # (+ Vd, ABI 8)
+    assert ctypes.sizeof(abi.MapOrswotStates) == 12 * 8
 
 
 HOST_CAPABLE = ({f"crdt_{t}_{op}" for t in ("vclock", "gcounter", "pncounter", "gset", "lwwreg", "orswot", "map")
