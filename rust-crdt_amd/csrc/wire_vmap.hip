@@ -333,7 +333,8 @@ __device__ __forceinline__ u64 vclock_bytes(const u64 *r, unsigned long long A, 
   return 8 + 12 * nnz_row(r, A, lane);
 }
 
-__global__ __launch_bounds__(kBlock) void vmap_egress_kernel(VMapWirePlan p, int write) {
+// (4 waves per SIMD: the K2w key sets of round 6 took the kernel past 128 VGPRs, 3 waves, 25% slower)
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void vmap_egress_kernel(VMapWirePlan p, int write) {
   const int lane = threadIdx.x % kWave;
   const unsigned long long w0 = (blockIdx.x * (unsigned long long)kBlock + threadIdx.x) / kWave;
   const unsigned long long nwv = (unsigned long long)gridDim.x * (kBlock / kWave);

@@ -19,26 +19,28 @@ from crdts_gpu import wire  # noqa: E402
 
 
 def _deep_maps(rng, R, K, M, A, per=8):
-    """R replicas whose keys' Orswots hold up to `per` deferred removes each, clocks from the far
-    future on actor 0 (distinct, so a fold unions them: up to R * per on one key)."""
+    """R replicas (replica r writes as actor r: A >= R, so no replica's clock dominates another's
+    entries) whose keys' Orswots hold up to `per` deferred removes each, clocks from the far future
+    on actor 0 (distinct, so a fold unions them: up to R * per on one key)."""
+    assert A >= R
     maps = []
-    for _ in range(R):
+    for r in range(R):
         m = O.Map(O.Orswot)
-        m.clock = O.VClock({a: int(x) for a, x in enumerate(rng.integers(1, 4, A))})
+        m.clock = O.VClock({r: 5})
         for k in range(K):
-            if rng.random() < 0.8:
+            if rng.random() < 0.9:
                 o = O.Orswot()
-                o.clock = O.VClock({a: int(x) for a, x in enumerate(rng.integers(0, 4, A)) if x})
+                o.clock = O.VClock({r: int(rng.integers(1, 4))})
                 for mem in range(M):
                     if rng.random() < 0.4:
-                        o.entries[mem] = O.VClock({int(rng.integers(A)): int(rng.integers(1, 4))})
+                        o.entries[mem] = O.VClock({r: int(rng.integers(1, 4))})
                 for _ in range(int(rng.integers(1, per + 1))):
                     rm = {0: int(rng.integers(100, 100000))}
                     if rng.random() < 0.5:
                         rm[int(rng.integers(1, A))] = int(rng.integers(1, 3))
                     o.deferred[O.VClock(rm)] = set(int(x) for x in rng.choice(M, size=int(rng.integers(1, min(M, 3) + 1)),
                                                                               replace=False))
-                m.entries[k] = O.MapEntry(O.VClock({int(rng.integers(A)): int(rng.integers(1, 4))}), o)
+                m.entries[k] = O.MapEntry(O.VClock({r: int(rng.integers(1, 5))}), o)
         maps.append(m)
     return maps
 
@@ -73,8 +75,8 @@ def _longest(maps):
     return max(len(e.val.deferred) for x in maps for e in x.entries.values())
 
 
-@pytest.mark.parametrize("R,K,M,A,seed,vd_cap", [(10, 3, 4, 5, 1, "auto"), (12, 2, 6, 8, 2, 96),
-                                                 (6, 3, 70, 5, 3, "auto"), (6, 2, 5, 80, 4, "auto")])
+@pytest.mark.parametrize("R,K,M,A,seed,vd_cap", [(10, 3, 4, 16, 1, "auto"), (12, 2, 6, 12, 2, 96),
+                                                 (6, 3, 70, 8, 3, "auto"), (6, 2, 5, 80, 4, "auto")])
 def test_map_orswot_fold_past_16_nested(gpu_ctx, R, K, M, A, seed, vd_cap):
     """The register kernel (M <= 32, A <= 64) and the wide kernel (M = 70, A = 80) as the first pass;
     the keys past 16 re-folded with all Vd slots: equal to the oracle's left fold."""
@@ -83,7 +85,7 @@ def test_map_orswot_fold_past_16_nested(gpu_ctx, R, K, M, A, seed, vd_cap):
     exp = O.map_fold_objects(maps)
     assert _longest([exp]) > 16
     res = _fold(gpu_ctx, maps, K, M, A, vd_cap=vd_cap)
-    assert res.vd_clock.shape[1] >= _longest([exp])
+    assert res.vd_clock.shape[-2] >= _longest([exp])
     assert int(res.flags.cpu().numpy()[0]) == 0
     _same(_decode(res, 0, K), exp)
 
@@ -91,7 +93,7 @@ def test_map_orswot_fold_past_16_nested(gpu_ctx, R, K, M, A, seed, vd_cap):
 def test_map_orswot_fold_groups_mixed_depths(gpu_ctx):
     """G = 4 groups, two with keys past 16 nested removes and two within: only the deep keys re-fold,
     every group equal to its own fold."""
-    K, M, A, R = 3, 5, 6, 8
+    K, M, A, R = 3, 5, 8, 8
     rng = np.random.default_rng(7)
     parts = [_deep_maps(rng, R, K, M, A, per=8 if g % 2 == 0 else 1) for g in range(4)]
     res = _fold(gpu_ctx, [m for p in parts for m in p], K, M, A, G=4, vd_cap=80)
@@ -105,10 +107,10 @@ def test_map_orswot_fold_vd_cap_16_flags(gpu_ctx):
     """The default 16 slots on a fold that needs more: flags bit 4, raised by check=True (never a
     silently truncated state)."""
     rng = np.random.default_rng(5)
-    maps = _deep_maps(rng, 10, 2, 4, 5)
+    maps = _deep_maps(rng, 10, 2, 4, 10)
     with pytest.raises(RuntimeError, match="vd_cap"):
-        _fold(gpu_ctx, maps, 2, 4, 5, vd_cap=16)
-    res = _fold(gpu_ctx, maps, 2, 4, 5, vd_cap=16, check=False)
+        _fold(gpu_ctx, maps, 2, 4, 10, vd_cap=16)
+    res = _fold(gpu_ctx, maps, 2, 4, 10, vd_cap=16, check=False)
     assert int(res.flags.cpu().numpy()[0]) & 16
 
 
@@ -117,7 +119,7 @@ def _slots(N, Dcap, A, K):
     return z(N, Dcap, A), z(N, Dcap, (K + 63) // 64), torch.zeros(N, dtype=torch.int32, device="cuda:0")
 
 
-@pytest.mark.parametrize("M,A", [(4, 5), (70, 6)])
+@pytest.mark.parametrize("M,A", [(4, 8), (70, 8)])
 def test_map_orswot_apply_past_16_nested(gpu_ctx, M, A):
     """Orswot Rms from the far future on one key, 40 per state, on states with Vd = 64 slots: the
     nested list grows past 16 (masks of all 64 in LDS) and later Adds re-apply every one of them."""
@@ -170,13 +172,14 @@ def test_map_orswot_apply_past_16_nested(gpu_ctx, M, A):
 
 
 def test_map_orswot_forget_merge_wire_past_16_nested(gpu_ctx):
-    """Deep states (Vd = 72) through forget, merge_batch and the wire form, each equal to the oracle."""
-    K, M, A, R, N = 3, 5, 6, 9, 4
+    """Deep states (Vd = 128: the merged lists reach ~100) through forget, merge_batch and the wire
+    form, each equal to the oracle."""
+    K, M, A, R, N = 3, 5, 9, 9, 4
     rng = np.random.default_rng(21)
     groups = [_deep_maps(rng, R, K, M, A) for _ in range(2 * N)]
     folds = [O.map_fold_objects(g) for g in groups]
     assert _longest(folds) > 16
-    res = _fold(gpu_ctx, [m for g in groups for m in g], K, M, A, G=2 * N, vd_cap=72)
+    res = _fold(gpu_ctx, [m for g in groups for m in g], K, M, A, G=2 * N, vd_cap=128)
     Dc = 2
     me = wire.MapOrswotFrames(*[t[:N].contiguous() for t in res[:7]], *_slots(N, Dc, A, K))
     other = wire.MapOrswotFrames(*[t[N:].contiguous() for t in res[:7]], *_slots(N, Dc, A, K))
@@ -189,7 +192,7 @@ def test_map_orswot_forget_merge_wire_past_16_nested(gpu_ctx):
     kd = torch.tensor(kids, dtype=torch.int32, device="cuda:0")
     md = torch.tensor(mids, dtype=torch.int64, device="cuda:0")
     off, data = wire.map_orswot_egress(me, ad, kd, md, ctx=gpu_ctx)
-    back, st = wire.map_orswot_ingest(data, off, ad, kd, md, Dc, ctx=gpu_ctx, vd_cap=72)
+    back, st = wire.map_orswot_ingest(data, off, ad, kd, md, Dc, ctx=gpu_ctx, vd_cap=128)
     assert (st.cpu().numpy() == 0).all()
     for i in range(N):
         _same(_decode(back, i, K), folds[i])
