@@ -66,7 +66,8 @@ const char *crdt_last_error(const crdt_ctx *ctx);
 const char *crdt_version(void);
 /* ABI revision of this header: bumped whenever a struct or signature changes incompatibly (round 5
  * appended `size_t Dv` to crdt_map_orswot_batch: revision 5 -> 6; round 6 appended `size_t Vd` to
- * crdt_map_orswot_states / crdt_map_orswot_out: 7 -> 8).  A caller checks
+ * crdt_map_orswot_states / crdt_map_orswot_out and `size_t Id` to crdt_map_nested_states /
+ * crdt_map_nested_out: 7 -> 8).  A caller checks
  * crdt_abi_version() == CRDT_ABI_VERSION of the header it was built against before any other call,
  * so a mismatched library fails clearly instead of reading a shorter struct. */
 #define CRDT_ABI_VERSION 8
@@ -828,10 +829,12 @@ int crdt_map_orswot_lub_many_sharded(crdt_ctx *ctx, const crdt_map_orswot_batch 
  *   (G+1), def_row, def_clock [D][A], def_keys [D][Kw].
  * Output per (g, k) (packed): clock [g*A + a], ec / ic [(g*K + k)*A + a], iec [((g*K + k)*K2 + j)*A +
  *   a], 8 slots per inner key ivc [(((g*K + k)*K2 + j)*8 + s)*A + a], ivv [((g*K + k)*K2 + j)*8 + s]
- *   with nval [(g*K + k)*K2 + j] used (unused slots 0), inner deferred id_n [g*K + k] (<= 16),
- *   id_clock [((g*K + k)*16 + i)*A + a], id_keys [((g*K + k)*16 + i)*K2w + w]; flags[g]: bit 1 = def_row not
- *   non-decreasing or >= R, bit 3 = more than 256 live outer removes named one key, bit 4 = an inner
- *   Map held more than 16 deferred removes, bit 5 = id_off invalid (checked on the device: starts at
+ *   with nval [(g*K + k)*K2 + j] used (unused slots 0), inner deferred id_n [g*K + k] (<= Id = out->Id,
+ *   0 meaning 16), id_clock [((g*K + k)*Id + i)*A + a], id_keys [((g*K + k)*Id + i)*K2w + w] (round 6:
+ *   the fold keeps 16 in LDS and re-folds, exactly, the keys whose inner list passed 16 with all Id —
+ *   a second launch of one wave per marked key); flags[g]: bit 1 = def_row not non-decreasing or >= R,
+ *   bit 3 = more than 256 live outer removes named one key, bit 4 = an inner Map held more than Id
+ *   deferred removes, bit 5 = id_off invalid (checked on the device: starts at
  *   0, non-decreasing, ends at Di; the fold never reads past Di), bit 6 = an inner key held more than
  *   8 values — results of the group unreliable; def_keep / def_keys as crdt_map_out.
  * Map::forget collects the inner deferred removes into a new map: two whose clocks become equal keep
@@ -861,11 +864,12 @@ typedef struct crdt_map_nested_out {
   uint64_t *ivv;      /* [G][K][K2][8]     */
   uint32_t *nval;     /* [G][K][K2]        */
   uint32_t *id_n;     /* [G][K]            */
-  uint64_t *id_clock; /* [G][K][16][A]     */
-  uint64_t *id_keys;  /* [G][K][16][K2w]   */
+  uint64_t *id_clock; /* [G][K][Id][A]     */
+  uint64_t *id_keys;  /* [G][K][Id][K2w]   */
   uint32_t *flags;    /* [G]               */
   uint8_t *def_keep;  /* [D]               */
   uint64_t *def_keys; /* [D][Kw]           */
+  size_t Id;          /* inner deferred slots per key (round 6, ABI 8; 0 = 16) */
 } crdt_map_nested_out;
 
 int crdt_map_nested_lub_many(crdt_ctx *ctx, const crdt_map_nested_batch *in, crdt_map_nested_out *out);
@@ -879,17 +883,18 @@ int crdt_map_nested_lub_many_sharded(crdt_ctx *ctx, const crdt_map_nested_batch 
                                      crdt_map_nested_out *out);
 
 /* Map<K, Map<K2, MVReg<u64>>> states in place (round 5), on the crdt_map_nested_lub_many output layout
- * with N states (packed; 8 MVReg slots per inner key in Vec order, nval used, the rest zero; 16 inner
- * deferred removes per key with a K2w-word inner-key mask each, K2w = 1 up to K2 = 64):
+ * with N states (packed; 8 MVReg slots per inner key in Vec order, nval used, the rest zero; Id inner
+ * deferred slots per key (states->Id, 0 = 16) with a K2w-word inner-key mask each, K2w = 1 up to K2 = 64):
  *   crdt_map_nested_apply_batch — CmRDT::apply (map.rs:119-137, apply_keyset_rm :318-348,
  *     apply_deferred :311-316) with the inner Map's apply one level down and MVReg::apply
  *     (mvreg.rs:130-166) innermost: state s applies ops [op_off[s], op_off[s+1]) in order; the outer
- *     deferred removes as crdt_map_counter_apply_batch (def_count[s] <= Dcap slots).  Ops: kind 0 =
+ *     deferred removes as crdt_map_counter_apply_batch (def_count[s] <= Dcap slots); an inner list past
+ *     Id sets bit 0.  Ops: kind 0 =
  *     Op::Up { dot: (actor, counter), key, op } with ikind 0 = inner Op::Up { dot: (iactor, icounter),
  *     key: ikey, op: Put { clock: clk_pool[clk_row*A ..], val } } or 1 = inner Op::Rm { clock:
  *     clk_pool[clk_row*A ..], keyset: the inner-key mask ikeys [n_ops][K2w] }; kind 1 = Op::Rm { clock:
  *     clk_pool[clk_row*A ..], keyset: keys[key_off[o] .. key_off[o+1]) } (key_off may be NULL when no
- *     op is an outer Rm).  status[s]: bit 0 = a deferred list (outer Dcap or an inner one's 16)
+ *     op is an outer Rm).  status[s]: bit 0 = a deferred list (outer Dcap or an inner one's Id)
  *     exhausted, bit 1 = a malformed op skipped whole, bits 2-3 = invalid input (state untouched),
  *     bit 4 = a register needed more than 8 values (that value was not added).
  *   crdt_map_nested_forget_batch — Causal::forget (map.rs:85-114) of the whole state by y[s] (y_stride
@@ -909,8 +914,9 @@ typedef struct crdt_map_nested_states {
   uint64_t *ivv;      /* [N][K][K2][8]    */
   uint32_t *nval;     /* [N][K][K2]       */
   uint32_t *id_n;     /* [N][K]           */
-  uint64_t *id_clock; /* [N][K][16][A]    */
-  uint64_t *id_keys;  /* [N][K][16][K2w]  */
+  uint64_t *id_clock; /* [N][K][Id][A]    */
+  uint64_t *id_keys;  /* [N][K][Id][K2w]  */
+  size_t Id;          /* inner deferred slots per key (round 6, ABI 8; 0 = 16) */
 } crdt_map_nested_states;
 
 typedef struct crdt_map_nested_ops {

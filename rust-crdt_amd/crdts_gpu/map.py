@@ -633,7 +633,7 @@ def orswot_lub_many(clock: torch.Tensor, ec: torch.Tensor, oc: torch.Tensor, ent
 
 # ---- Map<K, Map<K2, MVReg<u64>>> (crdt_map_nested_lub_many, round 5) -------------------------------
 NM_VS = 8   # MVReg slots per inner key in the fold state (crdt_gpu.h)
-NM_ID = 16  # inner deferred removes per key state
+NM_ID = 16  # inner deferred removes per key state by default (round 6: any Id >= 16)
 
 
 class MapNestedLub(NamedTuple):
@@ -645,8 +645,8 @@ class MapNestedLub(NamedTuple):
     ivv: torch.Tensor                 # (G, K, K2, 8) values
     nval: torch.Tensor                # (G, K, K2) int32 slots used
     id_n: torch.Tensor                # (G, K) int32 inner deferred removes
-    id_clock: torch.Tensor            # (G, K, 16, A)
-    id_keys: torch.Tensor             # (G, K, 16) inner key bitmasks ((G, K, 16, K2w) past K2 = 64)
+    id_clock: torch.Tensor            # (G, K, Id, A)  (Id = id_cap, 16 by default)
+    id_keys: torch.Tensor             # (G, K, Id) inner key bitmasks ((G, K, Id, K2w) past K2 = 64)
     flags: torch.Tensor               # (G,) int32
     def_keep: Optional[torch.Tensor]  # (D,) uint8
     def_keys: Optional[torch.Tensor]  # (D, Kw)
@@ -657,7 +657,7 @@ def nested_lub_many(clock: torch.Tensor, ec: torch.Tensor, ic: torch.Tensor, iec
                     id_keys: Optional[torch.Tensor] = None, def_off=None, def_row: Optional[torch.Tensor] = None,
                     def_clock: Optional[torch.Tensor] = None, def_keys: Optional[torch.Tensor] = None,
                     ctx: Optional[Context] = None, check: bool = True,
-                    _key_shard: Optional[tuple] = None) -> MapNestedLub:
+                    _key_shard: Optional[tuple] = None, id_cap=NM_ID) -> MapNestedLub:
     """The exact left fold of Map::merge (map.rs:140-220) for Map<K, Map<K2, MVReg<u64>>> — the type of
     the reference's own Map tests (test/map.rs:10) — with the inner Map's merge (map.rs:140-220,
     mvreg.rs:112-128) and forget (map.rs:85-114) as the value's.  clock (G,R,A) / (R,A); ec, ic
@@ -666,8 +666,10 @@ def nested_lub_many(clock: torch.Tensor, ec: torch.Tensor, ic: torch.Tensor, iec
     id_keys (Di,) inner-key bitmasks ((Di, K2w) words past K2 = 64; K2 <= 256, A <= 256); the outer
     deferred pool as for lub_many (host def_off).
     check=True raises on flags (bit 1: def_row unsorted / out of range, bit 3: more than 256 live outer
-    removes named one key, bit 4: more than 16 inner deferred removes, bit 5: id_off invalid, bit 6:
-    more than 8 values on one inner key)."""
+    removes named one key, bit 4: more than id_cap inner deferred removes, bit 5: id_off invalid, bit 6:
+    more than 8 values on one inner key).  id_cap: inner deferred slots per key in the result (>= 16;
+    round 6: the fold keeps 16 in LDS and re-folds exactly the keys that need more); "auto" sizes it to
+    the largest sum of one key's inner list lengths over its group's replicas."""
     ctx = ctx or Context.default(clock.device.index)
     squeeze = clock.dim() == 2
     c, e, i, ie, vc, vv = ((t.unsqueeze(0) if squeeze else t) for t in (clock, ec, ic, iec, ivc, ivv))
@@ -697,9 +699,16 @@ def nested_lub_many(clock: torch.Tensor, ec: torch.Tensor, ic: torch.Tensor, iec
                 raise ValueError(f"map.nested_lub_many: {nm} must be a contiguous {shapes[0]} tensor")
             ctx.check_tensor(t, f"map.nested_lub_many({nm})")
     Kw = (K + 63) // 64 if _key_shard is None else (int(_key_shard[1]) + 63) // 64
+    if id_cap == "auto":
+        lens = id_off.view(torch.int64).reshape(-1)
+        lens = (lens[1:] - lens[:-1]).clamp(min=0).reshape(G, R, K).sum(dim=1)
+        id_cap = max(NM_ID, int(lens.max().item()) if lens.numel() else 0)
+    Id = int(id_cap)
+    if Id < NM_ID:
+        raise ValueError(f"map.nested_lub_many: id_cap = {Id} < {NM_ID}")
     out = [torch.empty(sh, dtype=torch.int64, device=dev)
            for sh in ((G, A), (G, K, A), (G, K, A), (G, K, K2, A), (G, K, K2, NM_VS, A), (G, K, K2, NM_VS),
-                      (G, K, NM_ID, A), (G, K, NM_ID) if K2w == 1 else (G, K, NM_ID, K2w))]
+                      (G, K, Id, A), (G, K, Id) if K2w == 1 else (G, K, Id, K2w))]
     nval = torch.empty((G, K, K2), dtype=torch.int32, device=dev)
     id_n = torch.empty((G, K), dtype=torch.int32, device=dev)
     flags = torch.empty(G, dtype=torch.int32, device=dev)
@@ -711,7 +720,7 @@ def nested_lub_many(clock: torch.Tensor, ec: torch.Tensor, ic: torch.Tensor, iec
         b.id_clock, b.id_keys = id_clock.data_ptr(), id_keys.data_ptr()
     ob = _abi.MapNestedOut()
     ob.clock, ob.ec, ob.ic, ob.iec, ob.ivc, ob.ivv, ob.id_clock, ob.id_keys = (t.data_ptr() for t in out)
-    ob.nval, ob.id_n, ob.flags = nval.data_ptr(), id_n.data_ptr(), flags.data_ptr()
+    ob.nval, ob.id_n, ob.flags, ob.Id = nval.data_ptr(), id_n.data_ptr(), flags.data_ptr(), Id
     keep = keys_out = None
     off_arr = None
     if def_off is not None:
@@ -751,7 +760,8 @@ def nested_lub_many(clock: torch.Tensor, ec: torch.Tensor, ic: torch.Tensor, iec
         if f & 8:
             raise RuntimeError("map.nested_lub_many: more than 256 live removes named one key")
         if f & 16:
-            raise RuntimeError("map.nested_lub_many: more than 16 deferred removes in one key's inner Map")
+            raise RuntimeError(f"map.nested_lub_many: more than id_cap = {Id} deferred removes in one key's inner "
+                               "Map (id_cap='auto' always fits)")
         if f & 64:
             raise RuntimeError("map.nested_lub_many: more than 8 values on one inner key")
     oclk, oec, oic, oiec, oivc, oivv, oidc, oidk = out
@@ -1160,9 +1170,12 @@ def _nested_states(res, what):
     N, A = clock.shape
     K, K2 = res.iec.shape[1], res.iec.shape[2]
     K2w = (K2 + 63) // 64 if K2 > 64 else 1  # inner key sets: K2w mask words past K2 = 64
+    Id = res.id_clock.shape[2] if res.id_clock.dim() == 4 else -1  # inner deferred slots per key
+    if Id < NM_ID:
+        raise ValueError(f"{what}: id_clock (N, K, Id, A) with Id >= {NM_ID} expected")
     shapes = dict(ec=(N, K, A), ic=(N, K, A), iec=(N, K, K2, A), ivc=(N, K, K2, 8, A), ivv=(N, K, K2, 8),
-                  nval=(N, K, K2), id_n=(N, K), id_clock=(N, K, 16, A),
-                  id_keys=(N, K, 16) if K2w == 1 else (N, K, 16, K2w))
+                  nval=(N, K, K2), id_n=(N, K), id_clock=(N, K, Id, A),
+                  id_keys=(N, K, Id) if K2w == 1 else (N, K, Id, K2w))
     for nm, shp in shapes.items():
         t = getattr(res, nm)
         if tuple(t.shape) != shp or not t.is_contiguous():
@@ -1170,7 +1183,7 @@ def _nested_states(res, what):
     if not clock.is_contiguous():
         raise ValueError(f"{what}: clock must be contiguous")
     st = _abi.MapNestedStates()
-    st.N, st.K, st.K2, st.A = N, K, K2, A
+    st.N, st.K, st.K2, st.A, st.Id = N, K, K2, A, Id
     for nm in ("clock", "ec", "ic", "iec", "ivc", "ivv", "nval", "id_n", "id_clock", "id_keys"):
         setattr(st, nm, getattr(res, nm).data_ptr())
     return st, N, K, A

@@ -263,7 +263,7 @@ class MapNestedFrames(NamedTuple):
     ivv: torch.Tensor        # (N, K, K2, 8)
     nval: torch.Tensor       # (N, K, K2) int32
     id_n: torch.Tensor       # (N, K) int32
-    id_clock: torch.Tensor   # (N, K, 16, A)
+    id_clock: torch.Tensor   # (N, K, Id, A)  (Id inner deferred slots per key, 16 by default)
     id_keys: torch.Tensor    # (N, K, 16) ((N, K, 16, K2w) mask words past K2 = 64)
     def_clock: torch.Tensor  # (N, Dcap, A)
     def_keys: torch.Tensor   # (N, Dcap, Kw)
@@ -396,20 +396,23 @@ def _nested_struct(ctx, st, what):
     N, K, A = _vmap_check(ctx, st, what)
     K2 = st.iec.shape[2]
     K2w = (K2 + 63) // 64 if K2 > 64 else 1
+    Id = st.id_clock.shape[2] if st.id_clock.dim() == 4 else 0
+    if Id < 16:
+        raise ValueError(f"{what}: id_clock (N, K, Id, A) with Id >= 16 expected")
     shapes = dict(ic=(N, K, A), iec=(N, K, K2, A), ivc=(N, K, K2, 8, A), ivv=(N, K, K2, 8), nval=(N, K, K2),
-                  id_n=(N, K), id_clock=(N, K, 16, A), id_keys=(N, K, 16) if K2w == 1 else (N, K, 16, K2w))
+                  id_n=(N, K), id_clock=(N, K, Id, A), id_keys=(N, K, Id) if K2w == 1 else (N, K, Id, K2w))
     for nm, shp in shapes.items():
         if tuple(getattr(st, nm).shape) != shp:
             raise ValueError(f"{what}: {nm} must be {shp}")
     s = _abi.MapNestedStates()
-    s.N, s.K, s.K2, s.A = N, K, K2, A
+    s.N, s.K, s.K2, s.A, s.Id = N, K, K2, A, Id
     for nm in ("clock", "ec", "ic", "iec", "ivc", "ivv", "nval", "id_n", "id_clock", "id_keys"):
         setattr(s, nm, dptr(getattr(st, nm)))
     return s, _vmap_deferred(st)
 
 
 def map_nested_ingest(data: torch.Tensor, frame_off: torch.Tensor, actors: torch.Tensor, keys: torch.Tensor,
-                      ikeys: torch.Tensor, Dcap: int, ctx: Optional[Context] = None):
+                      ikeys: torch.Tensor, Dcap: int, ctx: Optional[Context] = None, id_cap: int = 16):
     """Map<u32, Map<u32, MVReg<u64>>> frames -> (MapNestedFrames, status (N,) int32); ikeys: sorted
     u32 inner-key dictionary (int32 tensor, at most 256; past 64 the inner key sets are K2w words)."""
     ctx = _ctx(data, ctx)
@@ -421,8 +424,8 @@ def map_nested_ingest(data: torch.Tensor, frame_off: torch.Tensor, actors: torch
     z = lambda *shape: torch.zeros(shape, dtype=torch.int64, device=dev)  # noqa: E731
     z32 = lambda *shape: torch.zeros(shape, dtype=torch.int32, device=dev)  # noqa: E731
     st = MapNestedFrames(z(N, A), z(N, K, A), z(N, K, A), z(N, K, K2, A), z(N, K, K2, 8, A), z(N, K, K2, 8),
-                         z32(N, K, K2), z32(N, K), z(N, K, 16, A),
-                         z(N, K, 16) if K2 <= 64 else z(N, K, 16, (K2 + 63) // 64), z(N, Dcap, A),
+                         z32(N, K, K2), z32(N, K), z(N, K, id_cap, A),
+                         z(N, K, id_cap) if K2 <= 64 else z(N, K, id_cap, (K2 + 63) // 64), z(N, Dcap, A),
                          z(N, Dcap, (K + 63) // 64), z32(N))
     s, d = _nested_struct(ctx, st, "wire.map_nested_ingest")
     status = _status(N, dev)

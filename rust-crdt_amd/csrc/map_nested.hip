@@ -56,6 +56,10 @@ struct NestedMapPlan {
   unsigned long long xs_state, xs_stage;
   unsigned wpb;  // key waves per workgroup (kNmWaves; fewer for the wide instances' LDS rows)
   unsigned K2w;  // inner-key mask words, ceil(K2 / 64) (1 up to 64 inner keys: the round-5 layout)
+  // round 6: the output's inner deferred slots per key (>= kNmId; the first kNmId in LDS during the
+  // fold) and when Id > kNmId a per-(g, k) marker: the key's list passed kNmId, re-fold it deep
+  unsigned long long Id;
+  uint8_t *ovf;
 };
 
 // A clock across the wave: lane l holds actors l + 64 j, j < APL (A <= 64 APL; round 6: APL 2 and 4 take
@@ -178,23 +182,40 @@ __device__ __forceinline__ bool km_any(const NKm &k) {
   return x != 0;
 }
 
-template <int APL>
+// DEEP (round 6, the exact overflow pass): one wave per workgroup re-folds only the keys the first
+// pass marked in p.ovf, with p.Id inner deferred slots — their rm rows in the key's own output rows
+// (each lane reads back only the words it wrote), their key sets in LDS (Id * kNmKw words).
+template <int APL, bool DEEP = false>
 __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(NestedMapPlan p) {
   using Vc = NVc<APL>;
   extern __shared__ u64 lds[];
   const int lane = (int)(threadIdx.x % kWave), wv = (int)(threadIdx.x / kWave);
   const unsigned long long gk = (unsigned long long)blockIdx.x * p.wpb + wv;
   if (wv >= (int)p.wpb || gk >= p.G * p.K) return;  // (whole waves; nothing below synchronises the workgroup)
+  if constexpr (DEEP) {
+    if (!p.ovf[gk]) return;
+  }
   const unsigned long long g = gk / p.K, k = gk % p.K, A = p.A, R = p.R, K = p.K, K2 = p.K2, V = p.V;
-  constexpr unsigned long long WQ =
-      kNmList + kNmLive / 2 + kNmRows * kWave * APL + kNmId * kWave * APL + kNmId * kNmKw + kNmK2 / 8;
+  const int cap = DEEP ? (int)p.Id : kNmId;  // inner deferred slots
+  const unsigned long long WQ = kNmList + kNmLive / 2 + kNmRows * kWave * APL +
+                                (DEEP ? 0ull : (unsigned long long)kNmId * kWave * APL) +
+                                (unsigned long long)cap * kNmKw + kNmK2 / 8;
   u64 *lst = lds + (unsigned long long)wv * (WQ + p.xs_state + p.xs_stage);
   u64 *const xst = lst + WQ, *const xsg = xst + p.xs_state;  // (LDS state, staged replica)
   uint32_t *live = reinterpret_cast<uint32_t *>(lst + kNmList);
   u64 *rows = lst + kNmList + kNmLive / 2;  // [kNmRows][64 APL] live outer-remove rows
-  u64 *drow = rows + kNmRows * kWave * APL; // [kNmId][64 APL] inner deferred rm rows
-  u64 *dkey = drow + kNmId * kWave * APL;   // [kNmId][kNmKw] their inner key sets
-  uint8_t *nv = reinterpret_cast<uint8_t *>(dkey + kNmId * kNmKw);  // [K2] MVReg slots held per inner key
+  u64 *drow = rows + kNmRows * kWave * APL; // [kNmId][64 APL] inner deferred rm rows (not DEEP)
+  u64 *dkey = drow + (DEEP ? 0 : kNmId * kWave * APL);  // [cap][kNmKw] their inner key sets
+  uint8_t *nv = reinterpret_cast<uint8_t *>(dkey + (unsigned long long)cap * kNmKw);  // [K2] MVReg slots held per inner key
+  u64 *const gdr = p.o_id_clock + gk * p.Id * p.A;  // (DEEP) [Id][A] the rm rows in the output
+  auto dr_ld = [&](int i) -> NVc<APL> {
+    if constexpr (DEEP) return nv_ld<APL>(gdr + (unsigned long long)i * p.A, lane, p.A);
+    else return nv_lr<APL>(drow, i, lane);
+  };
+  auto dr_st = [&](int i, const NVc<APL> &x) {
+    if constexpr (DEEP) nv_st<APL>(gdr + (unsigned long long)i * p.A, x, lane, p.A);
+    else nv_lw<APL>(drow, i, x, lane);
+  };
   const unsigned K2w = p.K2w;
   auto km_lr = [&](int i) -> NKm {  // held remove i's key set
     NKm k;
@@ -320,7 +341,7 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
   };
   auto id_add = [&](const Vc &rm, const NKm &km) {  // deferred.entry(clock).or_default().append(keys) (map.rs:341-342)
     for (int i = 0; i < nd; ++i) {
-      if (nm_eq(nv_lr<APL>(drow, i, lane), rm)) {
+      if (nm_eq(dr_ld(i), rm)) {
         NKm mm = km_lr(i);
 #pragma unroll
         for (int x = 0; x < kNmKw; ++x) mm.w[x] |= km.w[x];
@@ -328,8 +349,8 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
         return;
       }
     }
-    if (nd < kNmId) {
-      nv_lw<APL>(drow, nd, rm, lane);
+    if (nd < cap) {
+      dr_st(nd, rm);
       km_lw(nd, km);
       ++nd;
     } else {
@@ -352,17 +373,17 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
     }
     int o = 0;
     for (int i = 0; i < nd; ++i) {
-      const Vc r2 = nm_fg(nv_lr<APL>(drow, i, lane), x);
+      const Vc r2 = nm_fg(dr_ld(i), x);
       const NKm ki = km_lr(i);
       if (!nm_nz(r2)) continue;
       int jj = 0;
       for (; jj < o; ++jj)  // equal to a kept one: the later keys at the earlier place (collect())
-        if (nm_eq(nv_lr<APL>(drow, jj, lane), r2)) break;
+        if (nm_eq(dr_ld(jj), r2)) break;
       if (jj < o) {
         km_lw(jj, ki);
         continue;
       }
-      nv_lw<APL>(drow, o, r2, lane);
+      dr_st(o, r2);
       km_lw(o, ki);
       ++o;
     }
@@ -542,12 +563,12 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
     // apply_deferred (:219, :311-316): every held remove forgets its keys again, stays iff !(rm <= ic)
     int o = 0;
     for (int i = 0; i < nd; ++i) {
-      const Vc rm = nv_lr<APL>(drow, i, lane);
+      const Vc rm = dr_ld(i);
       const NKm km = km_lr(i);
       forget_keys(rm, km);
       if (nm_gt_any(rm, ic)) {
         if (o != i) {
-          nv_lw<APL>(drow, o, rm, lane);
+          dr_st(o, rm);
           km_lw(o, km);
         }
         ++o;
@@ -680,11 +701,17 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
   if (k == 0) st(p.o_clock + g * A, C);
   const int no = pf ? nd : 0;
   for (int i = 0; i < no; ++i) {
-    st(p.o_id_clock + (gk * kNmId + i) * A, nv_lr<APL>(drow, i, lane));
+    if constexpr (!DEEP) st(p.o_id_clock + (gk * p.Id + i) * A, dr_ld(i));  // (DEEP: the rows are there)
     if (lane == 0)
-      for (unsigned x = 0; x < K2w; ++x) p.o_id_keys[(gk * kNmId + i) * K2w + x] = dkey[i * kNmKw + x];
+      for (unsigned x = 0; x < K2w; ++x) p.o_id_keys[(gk * p.Id + i) * K2w + x] = dkey[i * kNmKw + x];
   }
   if (lane == 0) p.o_id_n[gk] = (unsigned)no;
+  if constexpr (!DEEP) {
+    if (dfull && p.ovf) {  // past the LDS slots with room in the output: the deep pass re-folds this key
+      if (lane == 0) p.ovf[gk] = 1;
+      dfull = false;
+    }
+  }
   if ((bad || full || dfull || vfull) && lane == 0)
     atomicOr(p.o_flags + g, (bad ? 2u : 0u) | (full ? 8u : 0u) | (dfull ? 16u : 0u) | (vfull ? 64u : 0u));
 }
@@ -707,6 +734,11 @@ __global__ void map_nested_id_check_kernel(const u64 *off, unsigned long long n,
 static size_t nm_lds(int apl) {
   return kNmList * 8 + kNmLive * 4 + kNmRows * kWave * 8 * apl + kNmId * kWave * 8 * apl + kNmId * kNmKw * 8 + kNmK2;
 }
+// the deep pass's LDS (one wave): no rm rows (they live in the output), Id key sets
+static size_t nm_deep_lds(int apl, size_t Id) {
+  return kNmList * 8 + kNmLive * 4 + kNmRows * kWave * 8 * apl + Id * kNmKw * 8 + kNmK2;
+}
+constexpr size_t kNmDeepLds = 160 * 1024;
 
 }  // namespace crdt
 
@@ -738,6 +770,11 @@ extern "C" int crdt_map_nested_lub_many(crdt_ctx *ctx, const crdt_map_nested_bat
   if (D > 0 && (!in->def_row || !in->def_clock || !in->def_keys || !out->def_keep || !out->def_keys))
     return fail(ctx, CRDT_EINVAL, "map_nested_lub_many: deferred buffers missing");
   if (D > 0xffffffffULL) return fail(ctx, CRDT_EUNSUPPORTED, "map_nested_lub_many: too many deferred");
+  const size_t Id = out->Id ? out->Id : (size_t)kNmId;  // inner deferred slots per key in the output
+  const int apl0 = A <= (size_t)kWave ? 1 : (A <= 2 * (size_t)kWave ? 2 : 4);
+  if (Id < (size_t)kNmId) return fail(ctx, CRDT_EINVAL, "map_nested_lub_many: out->Id = %zu < %d", Id, kNmId);
+  if (Id > (size_t)kNmId && (nm_deep_lds(apl0, Id) > kNmDeepLds || G * K > 0x7fffffffULL))
+    return fail(ctx, CRDT_EUNSUPPORTED, "map_nested_lub_many: out->Id = %zu inner slots past the deep pass's limits", Id);
   CRDT_HIP(ctx, hipSetDevice(ctx->device));
   const size_t Kw = (K + 63) / 64;
   NestedMapPlan p{(const u64 *)in->clock, (const u64 *)in->ec, (const u64 *)in->ic, (const u64 *)in->iec,
@@ -747,6 +784,8 @@ extern "C" int crdt_map_nested_lub_many(crdt_ctx *ctx, const crdt_map_nested_bat
                   (u64 *)out->ic, (u64 *)out->iec, (u64 *)out->ivc, (u64 *)out->ivv, out->nval, out->id_n,
                   (u64 *)out->id_clock, (u64 *)out->id_keys, out->flags};
   p.K2w = K2 > 64 ? (unsigned)((K2 + 63) / 64) : 1u;
+  p.Id = Id;
+  p.ovf = nullptr;
   if (int rc = device_fill(ctx, out->flags, G * sizeof(unsigned), 0)) return rc;
   if (R == 0) {  // fold of nothing: Map::new()
     if (int rc = device_fill(ctx, out->clock, G * A * 8, 0)) return rc;
@@ -760,10 +799,18 @@ extern "C" int crdt_map_nested_lub_many(crdt_ctx *ctx, const crdt_map_nested_bat
     }
     if (int rc = device_fill(ctx, out->id_n, G * K * sizeof(unsigned), 0)) return rc;
   } else {
+    // scratch: [def_off (G+1) when D > 0][the deep pass's per-(g, k) markers when Id > 16]
+    const size_t so = D > 0 ? (G + 1) * sizeof(size_t) : 0, sv = Id > (size_t)kNmId ? G * K : 0;
+    if (so + sv) {
+      if (int rc = ensure_scratch(ctx, so + sv)) return rc;
+    }
     if (D > 0) {
-      if (int rc = ensure_scratch(ctx, (G + 1) * sizeof(size_t))) return rc;
       if (int rc = stage_h2d(ctx, ctx->scratch, in->def_off, (G + 1) * sizeof(size_t))) return rc;
       p.def_off = reinterpret_cast<const size_t *>(ctx->scratch);
+    }
+    if (sv) {
+      p.ovf = static_cast<uint8_t *>(ctx->scratch) + so;
+      if (int rc = device_fill(ctx, p.ovf, sv, 0)) return rc;
     }
     {
       const unsigned long long n = (unsigned long long)G * R * K;
@@ -807,7 +854,24 @@ extern "C" int crdt_map_nested_lub_many(crdt_ctx *ctx, const crdt_map_nested_bat
       hipLaunchKernelGGL(map_nested_fold_kernel<2>, dim3((unsigned)blocks), dim3(wpb * kWave), lds, ctx->stream, p);
     else
       hipLaunchKernelGGL(map_nested_fold_kernel<4>, dim3((unsigned)blocks), dim3(wpb * kWave), lds, ctx->stream, p);
-    const hipError_t he = hipGetLastError();
+    hipError_t he = hipGetLastError();
+    if (he == hipSuccess && sv) {  // the deep pass: the marked keys again, exactly, with all Id slots
+      NestedMapPlan q = p;
+      q.xs_state = q.xs_stage = 0;
+      q.wpb = 1;
+      const size_t dl = nm_deep_lds(apl, Id);
+      const void *dfn = apl == 1 ? reinterpret_cast<const void *>(&map_nested_fold_kernel<1, true>)
+                        : apl == 2 ? reinterpret_cast<const void *>(&map_nested_fold_kernel<2, true>)
+                                   : reinterpret_cast<const void *>(&map_nested_fold_kernel<4, true>);
+      if (dl > 64 * 1024) he = hipFuncSetAttribute(dfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dl);
+      if (he == hipSuccess) {
+        const dim3 dg((unsigned)(G * K)), db(kWave);
+        if (apl == 1) hipLaunchKernelGGL((map_nested_fold_kernel<1, true>), dg, db, dl, ctx->stream, q);
+        else if (apl == 2) hipLaunchKernelGGL((map_nested_fold_kernel<2, true>), dg, db, dl, ctx->stream, q);
+        else hipLaunchKernelGGL((map_nested_fold_kernel<4, true>), dg, db, dl, ctx->stream, q);
+        he = hipGetLastError();
+      }
+    }
     timing_end(ctx);
     if (he != hipSuccess) return hip_fail(ctx, he, "map_nested_fold_kernel launch");
   }

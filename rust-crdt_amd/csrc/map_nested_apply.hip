@@ -34,6 +34,7 @@ struct NestedApplyPlan {
   unsigned *nval, *id_n;
   unsigned long long N, K, K2, A, Kw, Dcap;
   unsigned long long K2w;  // inner-key mask words per key set (1 up to K2 = 64: the round-5 layout)
+  unsigned long long Id;   // inner deferred slots per key (crdt_map_nested_states.Id; 16 if 0)
   unsigned long long Dl;  // outer deferred slots held in LDS (<= Dcap); slots Dl .. Dcap-1 stay in place
   u64 *def_clock, *def_keys;
   unsigned *def_count;
@@ -88,6 +89,7 @@ struct NaKey {
   int lane;
   mutable unsigned stb;  // status bits raised by these operations (the caller ORs them in)
   unsigned kw_;          // mask words per key set (KW > 1)
+  unsigned cap;          // inner deferred slots (round 6: states->Id)
   __device__ __forceinline__ unsigned kwn() const { return KW == 1 ? 1u : kw_; }
 
   // held remove i's key set in registers (words past kwn(): 0) and back
@@ -193,7 +195,7 @@ struct NaKey {
   // Causal::forget of the inner Map (map.rs:85-114)
   __device__ void inner_forget(const u64 (&r)[APL]) const {
     for (unsigned long long jk = 0; jk < K2; ++jk) inner_key_rm(jk, r);
-    const unsigned n = *idn;
+    const unsigned n = min(cap, *idn);  // (a count past the slots: clamped)
     unsigned o = 0;
     for (unsigned i = 0; i < n; ++i) {
       u64 x[APL];
@@ -228,7 +230,7 @@ struct NaKey {
   }
   // the inner Map's apply_deferred (map.rs:311-316) against its clock c
   __device__ void inner_apply_deferred(const u64 (&c)[APL]) const {
-    const unsigned n = *idn;
+    const unsigned n = min(cap, *idn);  // (a count past the slots: clamped)
     unsigned o = 0;
     for (unsigned i = 0; i < n; ++i) {
       u64 r[APL];
@@ -324,7 +326,7 @@ struct NaKey {
     u64 c[APL];
     ld(ic, c);
     if (leq(r, c)) return;
-    const unsigned n = *idn;
+    const unsigned n = min(cap, *idn);  // (a count past the slots: clamped)
     for (unsigned i = 0; i < n; ++i) {
       u64 y[APL];
       ld(idc + (unsigned long long)i * A, y);
@@ -337,7 +339,7 @@ struct NaKey {
         return;
       }
     }
-    if (n >= (unsigned)kNaId) {
+    if (n >= cap) {
       stb |= 1u;
       return;
     }
@@ -351,7 +353,7 @@ struct NaKey {
     zero(ic);
     for (unsigned long long jk = 0; jk < K2; ++jk)
       if (nz_row(iec + jk * A) || nval[jk]) inner_drop(jk);
-    const unsigned n = *idn;
+    const unsigned n = min(cap, *idn);  // (a count past the slots: clamped)
     for (unsigned i = 0; i < n; ++i) {
       zero(idc + (unsigned long long)i * A);
       ks_zero(i);
@@ -383,8 +385,9 @@ __device__ __forceinline__ NaKey<APL, KW> na_key(const NestedApplyPlan &p, unsig
                                              int lane) {
   const unsigned long long sk = s * p.K + k, A = p.A, K2 = p.K2;
   return NaKey<APL, KW>{p.ec + sk * A, p.ic + sk * A, p.iec + sk * K2 * A, p.ivc + sk * K2 * kNaVs * A,
-                    p.ivv + sk * K2 * kNaVs, p.id_clock + sk * kNaId * A, p.id_keys + sk * kNaId * p.K2w,
-                    p.nval + sk * K2, p.id_n + sk, A, K2, lane, 0u, (unsigned)p.K2w};
+                    p.ivv + sk * K2 * kNaVs, p.id_clock + sk * p.Id * A, p.id_keys + sk * p.Id * p.K2w,
+                    p.nval + sk * K2, p.id_n + sk, A, K2, lane, 0u, (unsigned)p.K2w,
+                    (unsigned)p.Id};
 }
 
 // TIER false: every state, the Map's deferred list in the Dl LDS slots only; a state whose list
@@ -666,6 +669,7 @@ static NestedApplyPlan nested_plan(const crdt_map_nested_states *m) {
   p.K = m->K;
   p.K2 = m->K2;
   p.K2w = m->K2 > 64 ? (m->K2 + 63) / 64 : 1;
+  p.Id = m->Id ? m->Id : (size_t)kNaId;
   p.A = m->A;
   p.Kw = m->K ? (m->K + 63) / 64 : 1;
   return p;

@@ -405,7 +405,8 @@ extern "C" int crdt_map_nested_merge_batch(crdt_ctx *ctx, const crdt_map_nested_
   std::vector<size_t> off;
   if (int rc = pool_offsets(ctx, ad, bd, N, off, what)) return rc;
   std::vector<u64> ioff;
-  if (int rc = nested_offsets(ctx, a->id_n, b->id_n, N, K, ioff, what)) return rc;
+  const size_t Ia = a->Id ? a->Id : 16, Ib = b->Id ? b->Id : 16;  // inner deferred slots per key, each side
+  if (int rc = nested_offsets(ctx, a->id_n, b->id_n, N, K, ioff, what, Ia, Ib)) return rc;
   const size_t D = off[N], Di = ioff[N * 2 * K];
   Carve cv;
   const size_t c2 = cv.take(N * 2 * A * 8), e2 = cv.take(N * 2 * K * A * 8), i2 = cv.take(N * 2 * K * A * 8);
@@ -429,7 +430,7 @@ extern "C" int crdt_map_nested_merge_batch(crdt_ctx *ctx, const crdt_map_nested_
                        (unsigned long long)K, (unsigned long long)A, (unsigned long long)K2w, a->id_n, (const u64 *)a->id_clock,
                        (const u64 *)a->id_keys, b->id_n, (const u64 *)b->id_clock, (const u64 *)b->id_keys,
                        reinterpret_cast<const u64 *>(base + io), reinterpret_cast<u64 *>(base + ic),
-                       reinterpret_cast<u64 *>(base + ik), 16ull, 16ull);
+                       reinterpret_cast<u64 *>(base + ik), (unsigned long long)Ia, (unsigned long long)Ib);
     CRDT_HIP(ctx, hipGetLastError());
   }
   Pool pl;
@@ -466,6 +467,7 @@ extern "C" int crdt_map_nested_merge_batch(crdt_ctx *ctx, const crdt_map_nested_
   out.id_n = a->id_n;
   out.id_clock = a->id_clock;
   out.id_keys = a->id_keys;
+  out.Id = Ia;  // (self's slots: other's lists merge into them, bit 3 past Ia)
   out.flags = reinterpret_cast<uint32_t *>(base + of);
   out.def_keep = pl.keep;
   out.def_keys = reinterpret_cast<uint64_t *>(pl.kout);

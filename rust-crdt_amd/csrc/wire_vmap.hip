@@ -42,7 +42,7 @@ struct VMapWirePlan {
   u64 *oc, *ent;                   // Orswot [N][K][A], [N][K][M][A]
   uint32_t *vd_n;                  // [N][K]
   u64 *vd_clock, *vd_mem;          // [N][K][Vd][A], [N][K][Vd][Mw]
-  unsigned long long Vd;           // nested Orswot slots per key (crdt_map_orswot_states.Vd; 16 if 0)
+  unsigned long long Vd;           // nested slots per key: the Orswot's Vd or the inner Map's Id (16 if 0)
   u64 *def_clock, *def_keys;       // [N][Dcap][A], [N][Dcap][Kw]
   uint32_t *def_count;             // [N]
   uint32_t *status;
@@ -203,9 +203,9 @@ __global__ __launch_bounds__(kBlock) void vmap_ingest_kernel(VMapWirePlan p) {
             k = parse_idset(f, k, false, ikeys, nullptr, p.K2, bits, p.K2w, lane, st);
             if (k == ~0ull) break;
             if (ki >= 0) {
-              if (dn < (unsigned long long)kVwVd) {
-                store_row<u64>(p.id_clock + (sk * kVwVd + dn) * p.A, row, p.A, lane);
-                for (unsigned long long x = lane; x < p.K2w; x += kWave) p.id_keys[(sk * kVwVd + dn) * p.K2w + x] = bits[x];
+              if (dn < p.Vd) {
+                store_row<u64>(p.id_clock + (sk * p.Vd + dn) * p.A, row, p.A, lane);
+                for (unsigned long long x = lane; x < p.K2w; x += kWave) p.id_keys[(sk * p.Vd + dn) * p.K2w + x] = bits[x];
                 ++dn;
               } else {
                 st |= kWireCap;
@@ -391,14 +391,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
             }
           }
         }
-        const unsigned long long dn = p.id_n[sk] < (uint32_t)kVwVd ? p.id_n[sk] : kVwVd;
+        const unsigned long long dn = p.id_n[sk] < p.Vd ? p.id_n[sk] : p.Vd;
         sz += 8;
         if (write) {
           if (lane == 0) wr64(w, k, dn);
           k += 2;
         }
         for (unsigned long long i = 0; i < dn; ++i) {
-          const u64 *rm = p.id_clock + (sk * kVwVd + i) * p.A, *kb = p.id_keys + (sk * kVwVd + i) * p.K2w;
+          const u64 *rm = p.id_clock + (sk * p.Vd + i) * p.A, *kb = p.id_keys + (sk * p.Vd + i) * p.K2w;
           sz += vclock_bytes(rm, p.A, lane) + 8 + 4 * popc_row(kb, p.K2w, lane);
           if (write) {
             k = write_vclock(w, k, rm, p.A, p.actors, lane);
@@ -557,6 +557,7 @@ static int vmap_nested_plan(crdt_ctx *ctx, const crdt_map_nested_states *st, con
   p.Kw = Kw;
   p.K2 = K2;
   p.K2w = K2 > 64 ? (K2 + 63) / 64 : 1;
+  p.Vd = st->Id ? st->Id : (size_t)kVwVd;
   p.vt = 2;
   p.actors = actors;
   p.keys = keys;
@@ -591,8 +592,8 @@ static int vmap_ingest(crdt_ctx *ctx, VMapWirePlan &p, const uint8_t *bytes, con
     if (int rc = device_fill(ctx, p.ivv, N * p.K * p.K2 * kVwVs * 8, 0)) return rc;
     if (int rc = device_fill(ctx, p.nval, N * p.K * p.K2 * 4, 0)) return rc;
     if (int rc = device_fill(ctx, p.id_n, N * p.K * 4, 0)) return rc;
-    if (int rc = device_fill(ctx, p.id_clock, N * p.K * kVwVd * p.A * 8, 0)) return rc;
-    if (int rc = device_fill(ctx, p.id_keys, N * p.K * kVwVd * p.K2w * 8, 0)) return rc;
+    if (int rc = device_fill(ctx, p.id_clock, N * p.K * p.Vd * p.A * 8, 0)) return rc;
+    if (int rc = device_fill(ctx, p.id_keys, N * p.K * p.Vd * p.K2w * 8, 0)) return rc;
   } else {
     if (int rc = device_fill(ctx, p.oc, N * p.K * p.A * 8, 0)) return rc;
     if (int rc = device_fill(ctx, p.ent, N * p.K * p.M * p.A * 8, 0)) return rc;

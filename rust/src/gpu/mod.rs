@@ -1520,6 +1520,19 @@ fn nested_map_folds<K: Ord + Clone, K2: Ord + Clone, V: Clone, A: Actor>(
     }
     let pool = group_pool(groups, &actors, &keys);
     let (nd, di) = (pool.def_row.len(), id_keys.len() / k2w);
+    // inner deferred slots per key: the largest sum of one key's inner list lengths over its group (no
+    // fold result holds more), at least the library's 16 (round 6: past 16 those keys re-fold exactly)
+    let mut idc = 16usize;
+    for gi in 0..g {
+        for j in 0..k {
+            let mut t = 0usize;
+            for ri in 0..r {
+                let b = (gi * r + ri) * k + j;
+                t += (id_off[b + 1] - id_off[b]) as usize;
+            }
+            idc = idc.max(t);
+        }
+    }
     let batch = ffi::crdt_map_nested_batch {
         G: g, R: r, K: k, K2: k2, V: v, A: a,
         clock: clock.as_ptr(), ec: ec.as_ptr(), ic: ic.as_ptr(), iec: iec.as_ptr(), ivc: ivc.as_ptr(), ivv: ivv.as_ptr(),
@@ -1531,7 +1544,7 @@ fn nested_map_folds<K: Ord + Clone, K2: Ord + Clone, V: Clone, A: Actor>(
     let (mut o_iec, mut o_ivc, mut o_ivv) = (vec![0u64; g * k * k2 * a], vec![0u64; g * k * k2 * 8 * a],
                                              vec![0u64; g * k * k2 * 8]);
     let (mut o_nval, mut o_idn) = (vec![0u32; g * k * k2], vec![0u32; g * k]);
-    let (mut o_idc, mut o_idk) = (vec![0u64; g * k * 16 * a], vec![0u64; g * k * 16 * k2w]);
+    let (mut o_idc, mut o_idk) = (vec![0u64; g * k * idc * a], vec![0u64; g * k * idc * k2w]);
     let (mut flags, mut keep, mut okeys) = (vec![0u32; g], vec![0u8; nd], vec![0u64; nd * kw]);
     let mut out = ffi::crdt_map_nested_out {
         clock: o_clock.as_mut_ptr(), ec: o_ec.as_mut_ptr(), ic: o_ic.as_mut_ptr(), iec: o_iec.as_mut_ptr(),
@@ -1539,6 +1552,7 @@ fn nested_map_folds<K: Ord + Clone, K2: Ord + Clone, V: Clone, A: Actor>(
         id_clock: o_idc.as_mut_ptr(), id_keys: o_idk.as_mut_ptr(), flags: flags.as_mut_ptr(),
         def_keep: if nd > 0 { keep.as_mut_ptr() } else { ptr::null_mut() },
         def_keys: if nd > 0 { okeys.as_mut_ptr() } else { ptr::null_mut() },
+        Id: idc,
     };
     ctx.check_host(unsafe { ffi::crdt_map_nested_lub_many(ctx.host, &batch, &mut out) })?;
     if let Some(f) = flags.iter().find(|&&f| f != 0) {
@@ -1566,8 +1580,8 @@ fn nested_map_folds<K: Ord + Clone, K2: Ord + Clone, V: Clone, A: Actor>(
                 }
             }
             for i in 0..o_idn[b] as usize {
-                let ks = bit_keys(&o_idk[(b * 16 + i) * k2w..(b * 16 + i + 1) * k2w], &ikeys);
-                inner.deferred.entry(row_clock(&o_idc[(b * 16 + i) * a..(b * 16 + i + 1) * a], &actors))
+                let ks = bit_keys(&o_idk[(b * idc + i) * k2w..(b * idc + i + 1) * k2w], &ikeys);
+                inner.deferred.entry(row_clock(&o_idc[(b * idc + i) * a..(b * idc + i + 1) * a], &actors))
                     .or_insert_with(BTreeSet::new).extend(ks);
             }
             mp.entries.insert(key.clone(), Entry { clock: row_clock(row, &actors), val: inner });

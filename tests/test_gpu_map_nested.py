@@ -159,9 +159,9 @@ class _States(NamedTuple):
     id_keys: torch.Tensor
 
 
-def nested_states(maps, K, K2, A, Dcap=16):
+def nested_states(maps, K, K2, A, Dcap=16, Id=16):
     """Dense objects -> (_States on the device, outer deferred as slots (N, Dcap, A) / (N, Dcap, Kw) /
-    (N,) int32, and as a pool (def_clock (D, A), def_state (D,)))."""
+    (N,) int32, and as a pool (def_clock (D, A), def_state (D,))); Id inner deferred slots per key."""
     N = len(maps)
     d = O.nested_map_to_dense(maps, K, K2, A, 8)
     nval = np.zeros((N, K, K2), np.int32)
@@ -170,13 +170,13 @@ def nested_states(maps, K, K2, A, Dcap=16):
             for j, ie in e.val.entries.items():
                 nval[n, k, j] = len(ie.val.vals)
     idn = np.zeros((N, K), np.int32)
-    idc = np.zeros((N, K, 16, A), np.uint64)
+    idc = np.zeros((N, K, Id, A), np.uint64)
     K2w = (K2 + 63) // 64 if K2 > 64 else 1  # inner key sets: K2w mask words past 64 keys
-    idk = np.zeros((N, K, 16) if K2w == 1 else (N, K, 16, K2w), np.uint64)
+    idk = np.zeros((N, K, Id) if K2w == 1 else (N, K, Id, K2w), np.uint64)
     off = d["id_off"].astype(np.int64)
     for i in range(N * K):
         a, b = off[i], off[i + 1]
-        assert b - a <= 16
+        assert b - a <= Id
         idn[i // K, i % K] = b - a
         idc[i // K, i % K, :b - a] = d["id_clock"][a:b]
         idk[i // K, i % K, :b - a] = d["id_keys"][a:b]
