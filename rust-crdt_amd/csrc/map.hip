@@ -85,6 +85,15 @@ constexpr int kMapQ = 4;    // deferred removes tracked per key in registers bef
 #ifndef MAP_RS_AUX  // the policy bits themselves (2 = nt; 16 = sc1, 18 = sc1 nt: A/B options)
 #define MAP_RS_AUX (MAP_RS_NT ? 2 : 0)
 #endif
+// MAP_RS_LATE (build option, round 6, off): with the next chunk's pieces spread through the register
+// test, the slot's reload is no longer waited for in full before the test — the wait moves into the DMA
+// hook (before piece 0, which overwrites step 0's image) and every element's two pieces issue after
+// that element's compares, so element 0's compares run while the later reads land.  Parity green, but
+// 2.188 / 2.209 ms against 2.166 / 2.171 ms for the default, interleaved on one box
+// (profiles/r06_map_late_ab.log): the later DMA issue costs more than the overlap gains.
+#ifndef MAP_RS_LATE
+#define MAP_RS_LATE 0
+#endif
 constexpr int kMapL = MAP_RS_WS8 ? 128 : 256;  // removes naming one key listed in LDS (beyond: walk the group list)
 
 template <int APL, int VI>
@@ -830,6 +839,7 @@ __device__ __forceinline__ RsOwn<NQ, NP> rs_own(const u64 *mirror, const u64 *th
 // issuing), while spread over the test they issue under its VALU work.
 struct RsNoDma {
   static constexpr int count = 0;
+  static constexpr bool late = false;
   __device__ __forceinline__ void operator()(int) {}
 };
 
@@ -870,12 +880,13 @@ __device__ __forceinline__ RsPart<VI, NQ> rs_part(const RsChunk<VI, NP> &r, cons
 #pragma unroll
     for (int q = 0; q < NQ1; ++q) mLe[t][q] = ~0ull;
   }
+  constexpr int JS = (MAP_RS_LATE && std::remove_reference_t<F>::late) ? 2 : 0;  // (pieces one element later)
 #pragma unroll
   for (int m = 0; m < NP; ++m) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       if constexpr (ND > 0) {  // the masks so far are computed before these pieces issue
-        const int j = 2 * (2 * m + h);
+        const int j = 2 * (2 * m + h) - JS;
         asm volatile("" : "+s"(mP2), "+s"(mB), "+s"(mO));
 #pragma unroll
         for (int t = 0; t < VI; ++t) {
@@ -883,8 +894,8 @@ __device__ __forceinline__ RsPart<VI, NQ> rs_part(const RsChunk<VI, NP> &r, cons
 #pragma unroll
           for (int q = 0; q < NQ1; ++q) asm volatile("" : "+s"(mLe[t][q]));
         }
-        if (j < ND) dma(j);
-        if (j + 1 < ND) dma(j + 1);
+        if (j >= 0 && j < ND) dma(j);
+        if (j + 1 >= 0 && j + 1 < ND) dma(j + 1);
       }
       const u64 e2 = r.e[m][h], tb = o.tb[m][h];
       if constexpr (BATCH) {
@@ -945,7 +956,7 @@ __device__ __forceinline__ RsPart<VI, NQ> rs_part(const RsChunk<VI, NP> &r, cons
   }
   if constexpr (ND > 0) {
 #pragma unroll
-    for (int j = 4 * NP; j < ND; ++j) dma(j);
+    for (int j = 4 * NP - JS; j < ND; ++j) dma(j);
   }
   RsPart<VI, NQ> x;
   x.p2 = orN<LPS>(mP2);
@@ -1075,6 +1086,7 @@ __device__ __forceinline__ u64 rs_reg_noop_nv(const RsChunk<VI, NP> &r, const Rs
 // the same instructions, in the same order, as map_chunk_glds.
 struct RsDma {
   static constexpr int count = 18;
+  static constexpr bool late = true;  // (its piece 0 waits for the slot's reads: MAP_RS_LATE)
   const char *src;
   unsigned long long stride;
   u64 *img;
@@ -1088,6 +1100,7 @@ struct RsDma {
   bool vp;   // the values piece streamed (uniform; off: fetched for exact chunks only)
   int diag;  // MapPlan::diag timing probes
   __device__ __forceinline__ void operator()(int j) {
+    if (MAP_RS_LATE && j == 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot is read
     if (j < 16) {
       if (!(diag & 2) || j < 13) glds16<MAP_RS_AUX>(src, img + j * WS);
       src += stride;
@@ -1192,6 +1205,7 @@ __device__ __forceinline__ void st_chunk_glds(const MapPlan &p, const GldsLanes<
 // st_chunk_glds of a whole chunk as the chunk test's DMA hook.
 struct StDma {
   static constexpr int count = 9;
+  static constexpr bool late = false;
   const char *src;
   unsigned long long stride;
   u64 *img;  // the wave's first step image of the slot
@@ -1404,6 +1418,7 @@ __device__ __forceinline__ void sh_chunk_shared(const MapPlan &p, const ShLanes 
 // The same 14 pieces as the chunk test's DMA hook (RsNoDma's interface).
 struct ShDma {
   static constexpr int count = 14;
+  static constexpr bool late = false;
   const char *src[3];
   unsigned long long st4[3];
   u64 *img;
@@ -1840,11 +1855,12 @@ __global__ __launch_bounds__(SH ? 256 : (ST ? 128 : 64), ST ? 2 : 1) void map_fo
       } else {
         rs_reload(rA, img, WS, vsl, cms, A, lane, vpiece);
       }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot is read: refill it
-      if constexpr (SH) sh_pre = __builtin_amdgcn_readfirstlane(pre_raw);
       // a whole next chunk with every lane moving a piece: its pieces go out during the test
       const unsigned long long i2 = (ch + 2) * C;
       const bool spread = el && ch + 2 < nch && i2 + C <= R && (2 + VI) * A == 128 && (!SH || ch + kShD < nch);
+      // the slot is read: refill it (MAP_RS_LATE, RS path spreading the refill: the DMA hook waits)
+      if (SH || ST || !MAP_RS_LATE || !spread) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if constexpr (SH) sh_pre = __builtin_amdgcn_readfirstlane(pre_raw);
       if constexpr (SH) {
         if (!spread) {
           if (ch + 2 < nch) sh_chunk_images(shl, i2, R, img);
