@@ -958,9 +958,9 @@ int crdt_map_nested_forget_batch(crdt_ctx *ctx, const crdt_map_nested_states *st
  * rows, its nested lists, and its slots with the surviving removes (their merged key sets) in pool
  * order, vacated slots zeroed; other is read only.  status[i]: bit 0 = more surviving removes than
  * self's Dcap (the first Dcap kept), bit 3 = the fold reported a capacity for the pair (more than
- * 256 / 512 live removes naming one key, more than 16 nested deferred removes on a key, more than 8
- * values on an inner key: that pair's state is incomplete).  A def_count above its Dcap or a nested
- * count above 16 fails the call (CRDT_EINVAL) before anything is written.  The call reads the slot
+ * 256 / 512 live removes naming one key, more than self's Vd / Id nested deferred removes on a key,
+ * more than 8 values on an inner key: that pair's state is incomplete).  A def_count above its Dcap or
+ * a nested count above its side's Vd / Id fails the call (CRDT_EINVAL) before anything is written.  The call reads the slot
  * counts on the host (one stream synchronisation).  Device memory only. */
 int crdt_map_counter_merge_batch(crdt_ctx *ctx, const crdt_map_counter_states *self, const crdt_map_deferred *self_def,
                                  const crdt_map_counter_states *other, const crdt_map_deferred *other_def,
@@ -1157,10 +1157,10 @@ int crdt_map_egress(crdt_ctx *ctx, const crdt_map_states *states, const crdt_map
  * (W = 1 / 2) frames <-> packed crdt_map_counter_states: clock_stride A, ec_stride K*A, val_stride
  * K*W*A; and Map<u32, Orswot<u64, u32>, u32> frames <-> crdt_map_orswot_states: the nested Orswot's
  * clock oc, member dots ent by the sorted u64 `members` dictionary, its deferred removes in slots
- * 0 .. vd_n[s][k] < 16 with member bitmaps vd_mem [N][K][16][ceil(M/64)]; the Map's deferred removes
+ * 0 .. vd_n[s][k] < Vd with member bitmaps vd_mem [N][K][Vd][ceil(M/64)]; the Map's deferred removes
  * in per-state slots, a crdt_map_deferred.  Value encodings: GCounter = VClock, PNCounter = VClock p,
  * VClock n, Orswot as crdt_orswot_ingest.  Ingest status bits as above (4 = a state held more than
- * Dcap Map removes or a key's Orswot more than 16: the excess was dropped).  Egress writes present
+ * Dcap Map removes or a key's Orswot more than Vd: the excess was dropped).  Egress writes present
  * keys ascending (entry clock nonzero), present members ascending (dot row nonzero), vd_n nested
  * removes and count[s] Map removes with their ids ascending. */
 int crdt_map_counter_ingest(crdt_ctx *ctx, const uint8_t *bytes, const uint64_t *frame_off, const uint32_t *actors,
