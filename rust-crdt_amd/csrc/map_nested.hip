@@ -60,6 +60,7 @@ struct NestedMapPlan {
   // fold) and when Id > kNmId a per-(g, k) marker: the key's list passed kNmId, re-fold it deep
   unsigned long long Id;
   uint8_t *ovf;
+  unsigned long long Lc;  // the deep pass's live outer-remove capacity per key (>= kNmLive)
 };
 
 // A clock across the wave: lane l holds actors l + 64 j, j < APL (A <= 64 APL; round 6: APL 2 and 4 take
@@ -197,13 +198,14 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
   }
   const unsigned long long g = gk / p.K, k = gk % p.K, A = p.A, R = p.R, K = p.K, K2 = p.K2, V = p.V;
   const int cap = DEEP ? (int)p.Id : kNmId;  // inner deferred slots
-  const unsigned long long WQ = kNmList + kNmLive / 2 + kNmRows * kWave * APL +
+  const unsigned long long LC = DEEP ? p.Lc : (unsigned long long)kNmLive;  // live outer removes held
+  const unsigned long long WQ = kNmList + (LC + 1) / 2 + kNmRows * kWave * APL +
                                 (DEEP ? 0ull : (unsigned long long)kNmId * kWave * APL) +
                                 (unsigned long long)cap * kNmKw + kNmK2 / 8;
   u64 *lst = lds + (unsigned long long)wv * (WQ + p.xs_state + p.xs_stage);
   u64 *const xst = lst + WQ, *const xsg = xst + p.xs_state;  // (LDS state, staged replica)
   uint32_t *live = reinterpret_cast<uint32_t *>(lst + kNmList);
-  u64 *rows = lst + kNmList + kNmLive / 2;  // [kNmRows][64 APL] live outer-remove rows
+  u64 *rows = lst + kNmList + (LC + 1) / 2;  // [kNmRows][64 APL] live outer-remove rows
   u64 *drow = rows + kNmRows * kWave * APL; // [kNmId][64 APL] inner deferred rm rows (not DEEP)
   u64 *dkey = drow + (DEEP ? 0 : kNmId * kWave * APL);  // [cap][kNmKw] their inner key sets
   uint8_t *nv = reinterpret_cast<uint8_t *>(dkey + (unsigned long long)cap * kNmKw);  // [K2] MVReg slots held per inner key
@@ -598,7 +600,7 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
         const unsigned idx = (unsigned)lst[li];
         const Vc rm = ld(p.def_clock + (d0 + idx) * A);
         f = nm_max(f, rm);
-        if (na < kNmLive) {
+        if ((unsigned long long)na < LC) {
           if (lane == 0) live[na] = idx;
           put_row(na, rm);
           ++na;
@@ -707,9 +709,11 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
   }
   if (lane == 0) p.o_id_n[gk] = (unsigned)no;
   if constexpr (!DEEP) {
-    if (dfull && p.ovf) {  // past the LDS slots with room in the output: the deep pass re-folds this key
+    // past the LDS slots / the live list, where the deep pass has room for both: it re-folds this key
+    if ((dfull || full) && p.ovf && (!dfull || p.Id > (unsigned long long)kNmId) &&
+        (!full || p.Lc > (unsigned long long)kNmLive)) {
       if (lane == 0) p.ovf[gk] = 1;
-      dfull = false;
+      dfull = full = false;
     }
   }
   if ((bad || full || dfull || vfull) && lane == 0)
@@ -735,8 +739,8 @@ static size_t nm_lds(int apl) {
   return kNmList * 8 + kNmLive * 4 + kNmRows * kWave * 8 * apl + kNmId * kWave * 8 * apl + kNmId * kNmKw * 8 + kNmK2;
 }
 // the deep pass's LDS (one wave): no rm rows (they live in the output), Id key sets
-static size_t nm_deep_lds(int apl, size_t Id) {
-  return kNmList * 8 + kNmLive * 4 + kNmRows * kWave * 8 * apl + Id * kNmKw * 8 + kNmK2;
+static size_t nm_deep_lds(int apl, size_t Id, size_t Lc = kNmLive) {
+  return kNmList * 8 + (Lc + 1) / 2 * 8 + kNmRows * kWave * 8 * apl + Id * kNmKw * 8 + kNmK2;
 }
 constexpr size_t kNmDeepLds = 160 * 1024;
 
@@ -775,6 +779,13 @@ extern "C" int crdt_map_nested_lub_many(crdt_ctx *ctx, const crdt_map_nested_bat
   if (Id < (size_t)kNmId) return fail(ctx, CRDT_EINVAL, "map_nested_lub_many: out->Id = %zu < %d", Id, kNmId);
   if (Id > (size_t)kNmId && (nm_deep_lds(apl0, Id) > kNmDeepLds || G * K > 0x7fffffffULL))
     return fail(ctx, CRDT_EUNSUPPORTED, "map_nested_lub_many: out->Id = %zu inner slots past the deep pass's limits", Id);
+  // the deep pass's live list: every outer remove of the largest group (beyond kNmLive only when some
+  // group has more), as far as the LDS holds it (past that, flags bit 3 as before)
+  size_t Lc = kNmLive;
+  for (size_t i = 0; in->def_off && i < G; ++i) Lc = std::max<size_t>(Lc, in->def_off[i + 1] - in->def_off[i]);
+  while (Lc > (size_t)kNmLive && nm_deep_lds(apl0, Id, Lc) > kNmDeepLds) Lc = std::max<size_t>(kNmLive, Lc / 2);
+  const bool deep = Id > (size_t)kNmId || Lc > (size_t)kNmLive;
+  if (deep && G * K > 0x7fffffffULL) return fail(ctx, CRDT_EUNSUPPORTED, "map_nested_lub_many: G*K too large");
   CRDT_HIP(ctx, hipSetDevice(ctx->device));
   const size_t Kw = (K + 63) / 64;
   NestedMapPlan p{(const u64 *)in->clock, (const u64 *)in->ec, (const u64 *)in->ic, (const u64 *)in->iec,
@@ -786,6 +797,7 @@ extern "C" int crdt_map_nested_lub_many(crdt_ctx *ctx, const crdt_map_nested_bat
   p.K2w = K2 > 64 ? (unsigned)((K2 + 63) / 64) : 1u;
   p.Id = Id;
   p.ovf = nullptr;
+  p.Lc = Lc;
   if (int rc = device_fill(ctx, out->flags, G * sizeof(unsigned), 0)) return rc;
   if (R == 0) {  // fold of nothing: Map::new()
     if (int rc = device_fill(ctx, out->clock, G * A * 8, 0)) return rc;
@@ -800,7 +812,7 @@ extern "C" int crdt_map_nested_lub_many(crdt_ctx *ctx, const crdt_map_nested_bat
     if (int rc = device_fill(ctx, out->id_n, G * K * sizeof(unsigned), 0)) return rc;
   } else {
     // scratch: [def_off (G+1) when D > 0][the deep pass's per-(g, k) markers when Id > 16]
-    const size_t so = D > 0 ? (G + 1) * sizeof(size_t) : 0, sv = Id > (size_t)kNmId ? G * K : 0;
+    const size_t so = D > 0 ? (G + 1) * sizeof(size_t) : 0, sv = deep ? G * K : 0;
     if (so + sv) {
       if (int rc = ensure_scratch(ctx, so + sv)) return rc;
     }
@@ -859,7 +871,7 @@ extern "C" int crdt_map_nested_lub_many(crdt_ctx *ctx, const crdt_map_nested_bat
       NestedMapPlan q = p;
       q.xs_state = q.xs_stage = 0;
       q.wpb = 1;
-      const size_t dl = nm_deep_lds(apl, Id);
+      const size_t dl = nm_deep_lds(apl, Id, Lc);
       const void *dfn = apl == 1 ? reinterpret_cast<const void *>(&map_nested_fold_kernel<1, true>)
                         : apl == 2 ? reinterpret_cast<const void *>(&map_nested_fold_kernel<2, true>)
                                    : reinterpret_cast<const void *>(&map_nested_fold_kernel<4, true>);

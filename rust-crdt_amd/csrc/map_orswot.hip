@@ -52,6 +52,7 @@ struct MapOrswotPlan {
   // when Vd > kMoVd a per-(g, k) marker: the key's list passed kMoVd, re-fold it deep (pass 2)
   unsigned long long Vd;
   uint8_t *ovf;
+  unsigned long long Lc;  // the deep pass's live Map-remove capacity per key (>= kMoLive)
 };
 
 __device__ __forceinline__ bool mo_nz(u64 x) { return __ballot(x != 0) != 0; }
@@ -545,9 +546,10 @@ __global__ __launch_bounds__(kMoWaves * kWave) void map_orswot_fold_kernel(MapOr
     if (lane == 0) p.o_vd_mem[gk * p.Vd + i] = vmsk[i];
   }
   if (lane == 0) p.o_vd_n[gk] = (unsigned)no;
-  if (vfull && p.ovf) {  // past the LDS slots with room in the output: the deep pass re-folds this key
+  // past the LDS slots / the live list, where the deep pass has room for both: it re-folds this key
+  if ((vfull || full) && p.ovf && (!vfull || p.Vd > (unsigned long long)kMoVd) && (!full || p.Lc > (unsigned long long)kMoLive)) {
     if (lane == 0) p.ovf[gk] = 1;
-    vfull = false;
+    vfull = full = false;
   }
   if ((bad || full || vfull) && lane == 0)
     atomicOr(p.o_flags + g, (bad ? 2u : 0u) | (full ? 8u : 0u) | (vfull ? 16u : 0u));
@@ -573,11 +575,12 @@ __global__ __launch_bounds__(kMoWaves * kWave) void map_orswot_wide_kernel(MapOr
     if (!p.ovf[gk]) return;
   }
   const unsigned long long g = gk / p.K, k = gk % p.K, A = p.A, R = p.R, K = p.K, M = p.M, Mw = p.Mw;
-  const unsigned long long WQ = kMoList + kMoLive / 2 + (DEEP ? p.Vd * Mw : (unsigned long long)kMoVd * kMoWideMw);
+  const unsigned long long LC = DEEP ? p.Lc : (unsigned long long)kMoLive;  // live Map removes held
+  const unsigned long long WQ = kMoList + (LC + 1) / 2 + (DEEP ? p.Vd * Mw : (unsigned long long)kMoVd * kMoWideMw);
   const int cap = DEEP ? (int)p.Vd : kMoVd;
   u64 *lst = lds + (unsigned long long)wv * WQ;
   uint32_t *live = reinterpret_cast<uint32_t *>(lst + kMoList);
-  u64 *vmsk = lst + kMoList + kMoLive / 2;  // [cap][Mw] nested removes' member masks
+  u64 *vmsk = lst + kMoList + (LC + 1) / 2;  // [cap][Mw] nested removes' member masks
   u64 *wE = p.o_ent + gk * M * A;           // [M][A] the key's member rows (working state)
   u64 *wV = p.o_vd_clock + gk * p.Vd * A;   // [cap][A] its nested deferred rm rows
   // row I/O: word j of the lane is actor lane + 64 j; words past A read 0 and are never written
@@ -874,7 +877,7 @@ __global__ __launch_bounds__(kMoWaves * kWave) void map_orswot_wide_kernel(MapOr
       ldr(p.def_clock + (d0 + idx) * A, rm);
 #pragma unroll
       for (int j = 0; j < APL; ++j) f[j] = mo_max(f[j], rm[j]);
-      if (na < kMoLive) {
+      if ((unsigned long long)na < LC) {
         if (lane == 0) live[na] = idx;
         ++na;
         chg = true;
@@ -913,10 +916,11 @@ __global__ __launch_bounds__(kMoWaves * kWave) void map_orswot_wide_kernel(MapOr
     for (unsigned long long w = (unsigned long long)lane; w < Mw; w += kWave)
       p.o_vd_mem[(gk * p.Vd + i) * Mw + w] = vmsk[i * Mw + w];
   if (lane == 0) p.o_vd_n[gk] = (unsigned)no;
-  if constexpr (!DEEP) {
-    if (vfull && p.ovf) {  // (as the register kernel: the deep pass re-folds this key)
+  if constexpr (!DEEP) {  // (as the register kernel: the deep pass re-folds this key)
+    if ((vfull || full) && p.ovf && (!vfull || p.Vd > (unsigned long long)kMoVd) &&
+        (!full || p.Lc > (unsigned long long)kMoLive)) {
       if (lane == 0) p.ovf[gk] = 1;
-      vfull = false;
+      vfull = full = false;
     }
   }
   if ((bad || full || vfull) && lane == 0)
@@ -952,12 +956,12 @@ static hipError_t launch_mo_wide(const MapOrswotPlan &p, hipStream_t s) {
 }
 
 // the deep pass's LDS: one wave, its Map-remove lists and Vd nested member masks
-static size_t mo_deep_lds(size_t Vd, size_t Mw) { return kMoList * 8 + kMoLive * 4 + Vd * Mw * 8; }
+static size_t mo_deep_lds(size_t Vd, size_t Mw, size_t Lc = kMoLive) { return kMoList * 8 + (Lc + 1) / 2 * 8 + Vd * Mw * 8; }
 constexpr size_t kMoDeepLds = 160 * 1024;  // (one workgroup per CU at the most)
 
 template <int APL>
 static hipError_t launch_mo_deep(const MapOrswotPlan &p, hipStream_t s) {
-  const size_t lds = mo_deep_lds(p.Vd, p.Mw);
+  const size_t lds = mo_deep_lds(p.Vd, p.Mw, p.Lc);
   if (lds > 64 * 1024) {
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&map_orswot_wide_kernel<APL, true>),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -1010,7 +1014,13 @@ extern "C" int crdt_map_orswot_lub_many(crdt_ctx *ctx, const crdt_map_orswot_bat
   if (Vd > (size_t)kMoVd && mo_deep_lds(Vd, Mw0) > kMoDeepLds)
     return fail(ctx, CRDT_EUNSUPPORTED, "map_orswot_lub_many: out->Vd = %zu nested slots of %zu mask words exceed the LDS",
                 Vd, Mw0);
-  if (Vd > (size_t)kMoVd && G * K > 0x7fffffffULL)
+  // the deep pass's live list: every Map remove of the largest group (beyond kMoLive only when some
+  // group has more), as far as the LDS holds it (past that, flags bit 3 as before)
+  size_t Lc = kMoLive;
+  for (size_t i = 0; in->def_off && i < G; ++i) Lc = std::max<size_t>(Lc, in->def_off[i + 1] - in->def_off[i]);
+  while (Lc > (size_t)kMoLive && mo_deep_lds(Vd, Mw0, Lc) > kMoDeepLds) Lc = std::max<size_t>(kMoLive, Lc / 2);
+  const bool deep = Vd > (size_t)kMoVd || Lc > (size_t)kMoLive;
+  if (deep && G * K > 0x7fffffffULL)
     return fail(ctx, CRDT_EUNSUPPORTED, "map_orswot_lub_many: G*K too large for the deep pass");
   CRDT_HIP(ctx, hipSetDevice(ctx->device));
   const size_t Kw = (K + 63) / 64;
@@ -1018,7 +1028,7 @@ extern "C" int crdt_map_orswot_lub_many(crdt_ctx *ctx, const crdt_map_orswot_bat
                   (const u64 *)in->vd_off, (const u64 *)in->vd_clock, (const u64 *)in->vd_mem, in->Dv, G, R, K, M, A, Kw,
                   (M + 63) / 64 > 0 ? (M + 63) / 64 : 1, nullptr, in->def_row, (const u64 *)in->def_clock, (const u64 *)in->def_keys,
                   (u64 *)out->clock, (u64 *)out->ec, (u64 *)out->oc, (u64 *)out->ent, (u64 *)out->vd_clock,
-                  (u64 *)out->vd_mem, out->vd_n, out->flags, Vd, nullptr};
+                  (u64 *)out->vd_mem, out->vd_n, out->flags, Vd, nullptr, Lc};
   if (int rc = device_fill(ctx, out->flags, G * sizeof(unsigned), 0)) return rc;
   if (R == 0) {  // fold of nothing: Map::new()
     if (int rc = device_fill(ctx, out->clock, G * A * 8, 0)) return rc;
@@ -1029,7 +1039,7 @@ extern "C" int crdt_map_orswot_lub_many(crdt_ctx *ctx, const crdt_map_orswot_bat
     if (int rc = device_fill(ctx, out->vd_n, G * K * sizeof(unsigned), 0)) return rc;
   } else {
     // scratch: [def_off (G+1) when D > 0][the deep pass's per-(g, k) markers when Vd > 16]
-    const size_t so = D > 0 ? (G + 1) * sizeof(size_t) : 0, sv = Vd > (size_t)kMoVd ? G * K : 0;
+    const size_t so = D > 0 ? (G + 1) * sizeof(size_t) : 0, sv = deep ? G * K : 0;
     if (so + sv) {
       if (int rc = ensure_scratch(ctx, so + sv)) return rc;
     }

@@ -174,3 +174,21 @@ def test_map_nested_forget_merge_wire_past_16_inner(gpu_ctx):
     for i in range(N):
         exps[i].forget(VClock({0: 50000}))
         assert canon(decode_states(me, i, [])) == canon(exps[i]), i
+
+
+def test_map_nested_fold_past_256_live_removes(gpu_ctx):
+    """320 live outer removes naming one key (flags bit 3 before round 6): the deep pass holds the
+    group's whole remove list; equal to the oracle's fold, outer survivors included."""
+    from test_gpu_map_orswot_deep import _many_live
+    from test_gpu_map_nested import gpu_fold
+
+    def val(r, k):
+        inner = O.Map(O.MVReg)
+        inner.clock = VClock({r: 2})
+        c = VClock({r: 1 + k % 2})
+        inner.entries[k % 3] = O.MapEntry(c.copy(), O.MVReg([(c, 7 + r)]))
+        return inner
+    maps = _many_live(40, 3, lambda *a: val(*a) if a else O.Map(O.MVReg))
+    exp = O.map_fold_objects(maps)
+    assert len(exp.deferred) > 256
+    assert canon(gpu_fold(gpu_ctx, maps)) == canon(exp)

@@ -212,3 +212,39 @@ def test_map_orswot_forget_merge_wire_past_16_nested(gpu_ctx):
         exp.merge(folds[N + i].copy())
         exp.forget(O.VClock({0: 50000}))
         _same(_decode(me, i, K), exp)
+
+
+def _many_live(R, K, mk_val, per=8):
+    """R replicas (actor r) each holding `per` Map-level removes from the far future on actor 0 that
+    name key 0 (distinct clocks: a fold keeps all R * per live on key 0, past the 256 the first pass
+    holds)."""
+    maps = []
+    for r in range(R):
+        m = O.Map(mk_val)
+        m.clock = O.VClock({r: 5})
+        for k in range(K):
+            m.entries[k] = O.MapEntry(O.VClock({r: 2 + k % 2}), mk_val(r, k))
+        for i in range(per):
+            m.deferred[O.VClock({0: 1000 + per * r + i})] = {0} if i % 3 else {0, K - 1}
+        maps.append(m)
+    return maps
+
+
+def test_map_orswot_fold_past_256_live_removes(gpu_ctx):
+    """320 live Map-level removes naming one key (flags bit 3 before round 6): the deep pass holds the
+    group's whole remove list; equal to the oracle's fold, Map-level survivors included."""
+    from test_gpu_map_orswot import _got_maps, _run
+
+    def val(r, k):
+        o = O.Orswot()
+        o.clock = O.VClock({r: 2})
+        o.entries[k % 3] = O.VClock({r: 1 + k % 2})
+        return o
+    R, K, M, A = 40, 3, 3, 40
+    maps = _many_live(R, K, lambda *a: val(*a) if a else O.Orswot())
+    exp = O.map_fold_objects(maps)
+    assert len(exp.deferred) > 256
+    d = O.map_orswot_to_dense(maps, K, M, A)
+    res, kw = _run(gpu_ctx, d)
+    assert int(res.flags.cpu().numpy()[0]) == 0
+    _same(_got_maps(res, kw, 1)[0], exp)
