@@ -186,7 +186,7 @@ def test_map_nested_fold_past_256_live_removes(gpu_ctx):
         inner = O.Map(O.MVReg)
         inner.clock = VClock({r: 2})
         c = VClock({r: 1 + k % 2})
-        inner.entries[k % 3] = O.MapEntry(c.copy(), O.MVReg([(c, 7 + r)]))
+        inner.entries[r] = O.MapEntry(c.copy(), O.MVReg([(c, 7 + r)]))  # (one writer per inner key)
         return inner
     maps = _many_live(40, 3, lambda *a: val(*a) if a else O.Map(O.MVReg))
     exp = O.map_fold_objects(maps)
