@@ -768,8 +768,9 @@ int crdt_map_counter_lub_many_sharded(crdt_ctx *ctx, const crdt_map_counter_batc
  * vd_mem [((g*K + k)*Vd + i)*Mw + w] (Vd = out->Vd, 0 meaning 16; round 6: the fold keeps 16 slots per
  * key in LDS and re-folds, exactly, the keys whose list passed 16 with all Vd — a second launch of one
  * wave per marked key, its Vd member masks in LDS: Vd * Mw * 8 + 6 KiB <= 160 KiB); flags[g]: bit 1 =
- * def_row not non-decreasing or >= R, bit 3 = more than 256 live Map removes named one key, bit 4 = a
- * key's Orswot held more than Vd deferred removes, bit 5 = vd_off invalid (checked on the device: vd_off[0] == 0, non-decreasing,
+ * def_row not non-decreasing or >= R, bit 3 = more live Map removes named one key than the deep pass
+ * holds (256 in the first pass; the deep pass takes the largest group's whole list, ~80,000 in its
+ * LDS), bit 4 = a key's Orswot held more than Vd deferred removes, bit 5 = vd_off invalid (checked on the device: vd_off[0] == 0, non-decreasing,
  * vd_off[G*R*K] == Dv; the fold reads only rows [0, Dv) whatever it holds) — results of the
  * group unreliable; def_keep / def_keys as crdt_map_out.
  * Orswot::forget collects its deferred removes into a new map: two whose clocks become equal keep
@@ -833,8 +834,9 @@ int crdt_map_orswot_lub_many_sharded(crdt_ctx *ctx, const crdt_map_orswot_batch 
  *   0 meaning 16), id_clock [((g*K + k)*Id + i)*A + a], id_keys [((g*K + k)*Id + i)*K2w + w] (round 6:
  *   the fold keeps 16 in LDS and re-folds, exactly, the keys whose inner list passed 16 with all Id —
  *   a second launch of one wave per marked key); flags[g]: bit 1 = def_row not non-decreasing or >= R,
- *   bit 3 = more than 256 live outer removes named one key, bit 4 = an inner Map held more than Id
- *   deferred removes, bit 5 = id_off invalid (checked on the device: starts at
+ *   bit 3 = more live outer removes named one key than the deep pass holds (256 in the first pass,
+ *   the largest group's whole list in the deep pass), bit 4 = an inner Map held more than Id deferred
+ *   removes, bit 5 = id_off invalid (checked on the device: starts at
  *   0, non-decreasing, ends at Di; the fold never reads past Di), bit 6 = an inner key held more than
  *   8 values — results of the group unreliable; def_keep / def_keys as crdt_map_out.
  * Map::forget collects the inner deferred removes into a new map: two whose clocks become equal keep

@@ -618,7 +618,7 @@ def orswot_lub_many(clock: torch.Tensor, ec: torch.Tensor, oc: torch.Tensor, ent
         if f & 2:
             raise ValueError("map.orswot_lub_many: def_row not non-decreasing per group or >= R")
         if f & 8:
-            raise RuntimeError("map.orswot_lub_many: more than 256 live removes named one key")
+            raise RuntimeError("map.orswot_lub_many: more live removes named one key than the deep pass holds")
         if f & 32:
             raise ValueError("map.orswot_lub_many: vd_off invalid (must start at 0, be non-decreasing and end at "
                              "vd_clock.shape[0])")
@@ -758,7 +758,7 @@ def nested_lub_many(clock: torch.Tensor, ec: torch.Tensor, ic: torch.Tensor, iec
             raise ValueError("map.nested_lub_many: id_off invalid (must start at 0, be non-decreasing and end at "
                              "id_clock.shape[0])")
         if f & 8:
-            raise RuntimeError("map.nested_lub_many: more than 256 live removes named one key")
+            raise RuntimeError("map.nested_lub_many: more live removes named one key than the deep pass holds")
         if f & 16:
             raise RuntimeError(f"map.nested_lub_many: more than id_cap = {Id} deferred removes in one key's inner "
                                "Map (id_cap='auto' always fits)")
