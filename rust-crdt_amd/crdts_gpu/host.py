@@ -368,10 +368,11 @@ def map_counter_lub_many(clock, ec, val, def_off=None, def_row=None, def_clock=N
 
 
 def map_orswot_lub_many(clock, ec, oc, ent, vd_off, vd_clock=None, vd_mem=None, def_off=None, def_row=None,
-                        def_clock=None, def_keys=None, ctx: Optional[HostContext] = None) -> dict:
+                        def_clock=None, def_keys=None, ctx: Optional[HostContext] = None, vd_cap: int = 16) -> dict:
     """crdt_map_orswot_lub_many on host arrays (one group): clock (R, A), ec / oc (R, K, A), ent (R, K, M, A),
     the nested removes as a CSR over (r, k): vd_off (R*K + 1,), vd_clock (Dv, A), vd_mem (Dv,) ((Dv, Mw)
-    member-mask words past M = 64; the results' vd_mem then (1, K, 16, Mw))."""
+    member-mask words past M = 64; the results' vd_mem then (1, K, Vd, Mw)); vd_cap = Vd nested slots
+    per key in the result (>= 16)."""
     ctx = ctx or HostContext.default()
     c, e, o_, m = (np.ascontiguousarray(_u64(x, n)) for x, n in ((clock, "clock"), (ec, "ec"), (oc, "oc"), (ent, "ent")))
     R, A = c.shape
@@ -391,22 +392,25 @@ def map_orswot_lub_many(clock, ec, oc, ent, vd_off, vd_clock=None, vd_mem=None, 
     Kw = (K + 63) // 64
     out = dict(clock=np.zeros((1, A), np.uint64), ec=np.zeros((1, K, A), np.uint64), oc=np.zeros((1, K, A), np.uint64),
                ent=np.zeros((1, K, M, A), np.uint64), vd_n=np.zeros((1, K), np.uint32),
-               vd_clock=np.zeros((1, K, 16, A), np.uint64),
-               vd_mem=np.zeros((1, K, 16) if M <= 64 else (1, K, 16, (M + 63) // 64), np.uint64),
+               vd_clock=np.zeros((1, K, vd_cap, A), np.uint64),
+               vd_mem=np.zeros((1, K, vd_cap) if M <= 64 else (1, K, vd_cap, (M + 63) // 64), np.uint64),
                flags=np.zeros(1, np.uint32), def_keep=np.zeros(D, np.uint8), def_keys=np.zeros((D, Kw), np.uint64))
     ob = _abi.MapOrswotOut()
     for n in ("clock", "ec", "oc", "ent", "vd_n", "vd_clock", "vd_mem", "flags"):
         setattr(ob, n, out[n].ctypes.data)
     ob.def_keep = out["def_keep"].ctypes.data if D else None
     ob.def_keys = out["def_keys"].ctypes.data if D else None
+    ob.Vd = vd_cap
     ctx.call("crdt_map_orswot_lub_many", ctypes.byref(b), ctypes.byref(ob))
     return out
 
 
 def map_nested_lub_many(clock, ec, ic, iec, ivc, ivv, id_off, id_clock=None, id_keys=None, def_off=None, def_row=None,
-                        def_clock=None, def_keys=None, ctx: Optional[HostContext] = None) -> dict:
+                        def_clock=None, def_keys=None, ctx: Optional[HostContext] = None, id_cap: int = 16) -> dict:
     """crdt_map_nested_lub_many on host arrays (one group): clock (R, A), ec / ic (R, K, A), iec (R, K, K2, A),
-    ivc (R, K, K2, V, A), ivv (R, K, K2, V), the inner removes as a CSR over (r, k)."""
+    ivc (R, K, K2, V, A), ivv (R, K, K2, V), the inner removes as a CSR over (r, k) (id_keys (Di,), or
+    (Di, K2w) mask words past K2 = 64, as the results' id_keys (1, K, Id[, K2w])); id_cap = Id inner
+    slots per key in the result (>= 16)."""
     ctx = ctx or HostContext.default()
     arrs = [np.ascontiguousarray(_u64(x, n)) for x, n in ((clock, "clock"), (ec, "ec"), (ic, "ic"), (iec, "iec"),
                                                           (ivc, "ivc"), (ivv, "ivv"))]
@@ -429,13 +433,15 @@ def map_nested_lub_many(clock, ec, ic, iec, ivc, ivv, id_off, id_clock=None, id_
     out = dict(clock=np.zeros((1, A), np.uint64), ec=np.zeros((1, K, A), np.uint64), ic=np.zeros((1, K, A), np.uint64),
                iec=np.zeros((1, K, K2, A), np.uint64), ivc=np.zeros((1, K, K2, 8, A), np.uint64),
                ivv=np.zeros((1, K, K2, 8), np.uint64), nval=np.zeros((1, K, K2), np.uint32),
-               id_n=np.zeros((1, K), np.uint32), id_clock=np.zeros((1, K, 16, A), np.uint64),
-               id_keys=np.zeros((1, K, 16), np.uint64), flags=np.zeros(1, np.uint32), def_keep=np.zeros(D, np.uint8),
+               id_n=np.zeros((1, K), np.uint32), id_clock=np.zeros((1, K, id_cap, A), np.uint64),
+               id_keys=np.zeros((1, K, id_cap) if K2 <= 64 else (1, K, id_cap, (K2 + 63) // 64), np.uint64),
+               flags=np.zeros(1, np.uint32), def_keep=np.zeros(D, np.uint8),
                def_keys=np.zeros((D, Kw), np.uint64))
     ob = _abi.MapNestedOut()
     for n in ("clock", "ec", "ic", "iec", "ivc", "ivv", "nval", "id_n", "id_clock", "id_keys", "flags"):
         setattr(ob, n, out[n].ctypes.data)
     ob.def_keep = out["def_keep"].ctypes.data if D else None
     ob.def_keys = out["def_keys"].ctypes.data if D else None
+    ob.Id = id_cap
     ctx.call("crdt_map_nested_lub_many", ctypes.byref(b), ctypes.byref(ob))
     return out

@@ -397,6 +397,41 @@ def test_map_nested_host_lub_many(hctx):
     assert canon(got) == canon(exp)
 
 
+def test_map_value_host_lub_many_deep(hctx):
+    """Host memory (round 6): a Map<K, Orswot> fold with keys past 16 nested removes (Vd = 64) and a
+    nested Map fold with keys past 16 inner removes and K2 = 100 inner keys (Id = 64, two mask words):
+    the staged deep passes, equal to the oracle."""
+    from test_gpu_map_nested import canon
+    from test_gpu_map_nested_deep import _deep_nested
+    from test_gpu_map_orswot_deep import _deep_maps
+    rng = np.random.default_rng(31)
+    R, K, M, A = 8, 3, 5, 8
+    maps = _deep_maps(rng, R, K, M, A)
+    exp = O.map_fold_objects(maps)
+    assert max(len(e.val.deferred) for e in exp.entries.values()) > 16
+    d = O.map_orswot_to_dense(maps, K, M, A)
+    out = host.map_orswot_lub_many(d["clock"], d["ec"], d["oc"], d["ent"], d["vd_off"], d["vd_clock"],
+                                   d["vd_members"], ctx=hctx, vd_cap=64)
+    assert int(out["flags"][0]) == 0
+    vd = {k: [(out["vd_clock"][0, k, i], O.bitmap_members(out["vd_mem"][0, k, i:i + 1]))
+              for i in range(int(out["vd_n"][0, k]))] for k in range(K)}
+    got = O.dense_to_map_orswot(out["clock"][0], out["ec"][0], out["oc"][0], out["ent"][0], vd, [])
+    assert got == exp
+    K2 = 100
+    maps = _deep_nested(rng, 6, 2, K2, 8)
+    exp = O.map_fold_objects(maps)
+    assert max(len(e.val.deferred) for e in exp.entries.values()) > 16
+    d = O.nested_map_to_dense(maps, 2, K2, 8, 8)
+    out = host.map_nested_lub_many(d["clock"], d["ec"], d["ic"], d["iec"], d["ivc"], d["ivv"], d["id_off"],
+                                   d["id_clock"], d["id_keys"], ctx=hctx, id_cap=64)
+    assert int(out["flags"][0]) == 0 and out["id_keys"].shape == (1, 2, 64, 2)
+    idef = {k: [(out["id_clock"][0, k, i], O.bitmap_members(out["id_keys"][0, k, i]))
+                for i in range(int(out["id_n"][0, k]))] for k in range(2)}
+    got = O.dense_to_nested_map(out["clock"][0], out["ec"][0], out["ic"][0], out["iec"][0], out["ivc"][0],
+                                out["ivv"][0], out["nval"][0], idef, [])
+    assert canon(got) == canon(exp)
+
+
 def test_map_value_host_lub_many_empty_batch(hctx):
     """R == 0 from host memory with a NULL vd_off / id_off, as the device path accepts:
     the empty fold Map::new(), no copy from NULL."""
