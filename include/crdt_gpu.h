@@ -829,8 +829,9 @@ int crdt_map_orswot_lub_many_sharded(crdt_ctx *ctx, const crdt_map_orswot_batch 
  *   the outer deferred removes as for the MVReg Map: def_off HOST
  *   (G+1), def_row, def_clock [D][A], def_keys [D][Kw].
  * Output per (g, k) (packed): clock [g*A + a], ec / ic [(g*K + k)*A + a], iec [((g*K + k)*K2 + j)*A +
- *   a], 8 slots per inner key ivc [(((g*K + k)*K2 + j)*8 + s)*A + a], ivv [((g*K + k)*K2 + j)*8 + s]
- *   with nval [(g*K + k)*K2 + j] used (unused slots 0), inner deferred id_n [g*K + k] (<= Id = out->Id,
+ *   a], Vs slots per inner key (out->Vs, 0 meaning 8, at most 64) ivc [(((g*K + k)*K2 + j)*Vs + s)*A +
+ *   a], ivv [((g*K + k)*K2 + j)*Vs + s] with nval [(g*K + k)*K2 + j] used (unused slots 0; round 6: a
+ *   key past 8 values re-folds in the deep pass, which also takes inputs with V up to 64), inner deferred id_n [g*K + k] (<= Id = out->Id,
  *   0 meaning 16), id_clock [((g*K + k)*Id + i)*A + a], id_keys [((g*K + k)*Id + i)*K2w + w] (round 6:
  *   the fold keeps 16 in LDS and re-folds, exactly, the keys whose inner list passed 16 with all Id —
  *   a second launch of one wave per marked key); flags[g]: bit 1 = def_row not non-decreasing or >= R,
@@ -838,7 +839,7 @@ int crdt_map_orswot_lub_many_sharded(crdt_ctx *ctx, const crdt_map_orswot_batch 
  *   the largest group's whole list in the deep pass), bit 4 = an inner Map held more than Id deferred
  *   removes, bit 5 = id_off invalid (checked on the device: starts at
  *   0, non-decreasing, ends at Di; the fold never reads past Di), bit 6 = an inner key held more than
- *   8 values — results of the group unreliable; def_keep / def_keys as crdt_map_out.
+ *   Vs values — results of the group unreliable; def_keep / def_keys as crdt_map_out.
  * Map::forget collects the inner deferred removes into a new map: two whose clocks become equal keep
  * one entry with the later one's keys (the oracle's dict order; the reference's is unspecified).
  * Limits: A <= 256 and K2 <= 256 (round 6: lane l holds actors l + 64 j; K2w key-set words), V <= 8.
@@ -862,8 +863,8 @@ typedef struct crdt_map_nested_out {
   uint64_t *ec;       /* [G][K][A]         */
   uint64_t *ic;       /* [G][K][A]         */
   uint64_t *iec;      /* [G][K][K2][A]     */
-  uint64_t *ivc;      /* [G][K][K2][8][A]  */
-  uint64_t *ivv;      /* [G][K][K2][8]     */
+  uint64_t *ivc;      /* [G][K][K2][Vs][A] */
+  uint64_t *ivv;      /* [G][K][K2][Vs]    */
   uint32_t *nval;     /* [G][K][K2]        */
   uint32_t *id_n;     /* [G][K]            */
   uint64_t *id_clock; /* [G][K][Id][A]     */
@@ -872,6 +873,7 @@ typedef struct crdt_map_nested_out {
   uint8_t *def_keep;  /* [D]               */
   uint64_t *def_keys; /* [D][Kw]           */
   size_t Id;          /* inner deferred slots per key (round 6, ABI 8; 0 = 16) */
+  size_t Vs;          /* MVReg slots per inner key (round 6, ABI 8; 0 = 8, at most 64) */
 } crdt_map_nested_out;
 
 int crdt_map_nested_lub_many(crdt_ctx *ctx, const crdt_map_nested_batch *in, crdt_map_nested_out *out);
@@ -885,7 +887,7 @@ int crdt_map_nested_lub_many_sharded(crdt_ctx *ctx, const crdt_map_nested_batch 
                                      crdt_map_nested_out *out);
 
 /* Map<K, Map<K2, MVReg<u64>>> states in place (round 5), on the crdt_map_nested_lub_many output layout
- * with N states (packed; 8 MVReg slots per inner key in Vec order, nval used, the rest zero; Id inner
+ * with N states (packed; Vs MVReg slots per inner key in Vec order (states->Vs, 0 = 8), nval used, the rest zero; Id inner
  * deferred slots per key (states->Id, 0 = 16) with a K2w-word inner-key mask each, K2w = 1 up to K2 = 64):
  *   crdt_map_nested_apply_batch — CmRDT::apply (map.rs:119-137, apply_keyset_rm :318-348,
  *     apply_deferred :311-316) with the inner Map's apply one level down and MVReg::apply
@@ -898,7 +900,7 @@ int crdt_map_nested_lub_many_sharded(crdt_ctx *ctx, const crdt_map_nested_batch 
  *     clk_pool[clk_row*A ..], keyset: keys[key_off[o] .. key_off[o+1]) } (key_off may be NULL when no
  *     op is an outer Rm).  status[s]: bit 0 = a deferred list (outer Dcap or an inner one's Id)
  *     exhausted, bit 1 = a malformed op skipped whole, bits 2-3 = invalid input (state untouched),
- *     bit 4 = a register needed more than 8 values (that value was not added).
+ *     bit 4 = a register needed more than Vs values (that value was not added).
  *   crdt_map_nested_forget_batch — Causal::forget (map.rs:85-114) of the whole state by y[s] (y_stride
  *     0: one row for all): entry clocks, the inner Maps (their entries, registers — MVReg::forget
  *     mvreg.rs:88-104, emptied values dropped, order kept —, deferred removes, clocks), an emptied
@@ -912,13 +914,14 @@ typedef struct crdt_map_nested_states {
   uint64_t *ec;       /* [N][K][A]        */
   uint64_t *ic;       /* [N][K][A]        */
   uint64_t *iec;      /* [N][K][K2][A]    */
-  uint64_t *ivc;      /* [N][K][K2][8][A] */
-  uint64_t *ivv;      /* [N][K][K2][8]    */
+  uint64_t *ivc;      /* [N][K][K2][Vs][A] */
+  uint64_t *ivv;      /* [N][K][K2][Vs]   */
   uint32_t *nval;     /* [N][K][K2]       */
   uint32_t *id_n;     /* [N][K]           */
   uint64_t *id_clock; /* [N][K][Id][A]    */
   uint64_t *id_keys;  /* [N][K][Id][K2w]  */
   size_t Id;          /* inner deferred slots per key (round 6, ABI 8; 0 = 16) */
+  size_t Vs;          /* MVReg slots per inner key (round 6, ABI 8; 0 = 8, at most 64) */
 } crdt_map_nested_states;
 
 typedef struct crdt_map_nested_ops {

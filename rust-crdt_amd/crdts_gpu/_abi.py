@@ -131,7 +131,7 @@ class MapOrswotStates(ctypes.Structure):  # crdt_map_orswot_states
 
 class MapNestedStates(ctypes.Structure):  # crdt_map_nested_states
     _fields_ = [("N", S), ("K", S), ("K2", S), ("A", S), ("clock", P), ("ec", P), ("ic", P), ("iec", P), ("ivc", P),
-                ("ivv", P), ("nval", P), ("id_n", P), ("id_clock", P), ("id_keys", P), ("Id", S)]
+                ("ivv", P), ("nval", P), ("id_n", P), ("id_clock", P), ("id_keys", P), ("Id", S), ("Vs", S)]
 
 
 class MapNestedOps(ctypes.Structure):  # crdt_map_nested_ops
@@ -244,7 +244,7 @@ class MapNestedBatch(ctypes.Structure):  # crdt_map_nested_batch
 
 class MapNestedOut(ctypes.Structure):  # crdt_map_nested_out
     _fields_ = [("clock", P), ("ec", P), ("ic", P), ("iec", P), ("ivc", P), ("ivv", P), ("nval", P), ("id_n", P),
-                ("id_clock", P), ("id_keys", P), ("flags", P), ("def_keep", P), ("def_keys", P), ("Id", S)]
+                ("id_clock", P), ("id_keys", P), ("flags", P), ("def_keep", P), ("def_keys", P), ("Id", S), ("Vs", S)]
 
 
 class MapOut(ctypes.Structure):  # crdt_map_out

@@ -406,7 +406,8 @@ def map_orswot_lub_many(clock, ec, oc, ent, vd_off, vd_clock=None, vd_mem=None, 
 
 
 def map_nested_lub_many(clock, ec, ic, iec, ivc, ivv, id_off, id_clock=None, id_keys=None, def_off=None, def_row=None,
-                        def_clock=None, def_keys=None, ctx: Optional[HostContext] = None, id_cap: int = 16) -> dict:
+                        def_clock=None, def_keys=None, ctx: Optional[HostContext] = None, id_cap: int = 16,
+                        v_cap: int = 8) -> dict:
     """crdt_map_nested_lub_many on host arrays (one group): clock (R, A), ec / ic (R, K, A), iec (R, K, K2, A),
     ivc (R, K, K2, V, A), ivv (R, K, K2, V), the inner removes as a CSR over (r, k) (id_keys (Di,), or
     (Di, K2w) mask words past K2 = 64, as the results' id_keys (1, K, Id[, K2w])); id_cap = Id inner
@@ -431,8 +432,8 @@ def map_nested_lub_many(clock, ec, ic, iec, ivc, ivv, id_off, id_clock=None, id_
     D = _def_pool(b, def_off, def_row, def_clock, def_keys, keep)
     Kw = (K + 63) // 64
     out = dict(clock=np.zeros((1, A), np.uint64), ec=np.zeros((1, K, A), np.uint64), ic=np.zeros((1, K, A), np.uint64),
-               iec=np.zeros((1, K, K2, A), np.uint64), ivc=np.zeros((1, K, K2, 8, A), np.uint64),
-               ivv=np.zeros((1, K, K2, 8), np.uint64), nval=np.zeros((1, K, K2), np.uint32),
+               iec=np.zeros((1, K, K2, A), np.uint64), ivc=np.zeros((1, K, K2, v_cap, A), np.uint64),
+               ivv=np.zeros((1, K, K2, v_cap), np.uint64), nval=np.zeros((1, K, K2), np.uint32),
                id_n=np.zeros((1, K), np.uint32), id_clock=np.zeros((1, K, id_cap, A), np.uint64),
                id_keys=np.zeros((1, K, id_cap) if K2 <= 64 else (1, K, id_cap, (K2 + 63) // 64), np.uint64),
                flags=np.zeros(1, np.uint32), def_keep=np.zeros(D, np.uint8),
@@ -442,6 +443,6 @@ def map_nested_lub_many(clock, ec, ic, iec, ivc, ivv, id_off, id_clock=None, id_
         setattr(ob, n, out[n].ctypes.data)
     ob.def_keep = out["def_keep"].ctypes.data if D else None
     ob.def_keys = out["def_keys"].ctypes.data if D else None
-    ob.Id = id_cap
+    ob.Id, ob.Vs = id_cap, v_cap
     ctx.call("crdt_map_nested_lub_many", ctypes.byref(b), ctypes.byref(ob))
     return out

@@ -632,7 +632,7 @@ def orswot_lub_many(clock: torch.Tensor, ec: torch.Tensor, oc: torch.Tensor, ent
 
 
 # ---- Map<K, Map<K2, MVReg<u64>>> (crdt_map_nested_lub_many, round 5) -------------------------------
-NM_VS = 8   # MVReg slots per inner key in the fold state (crdt_gpu.h)
+NM_VS = 8   # MVReg slots per inner key in the fold state by default (round 6: any Vs in 8..64)
 NM_ID = 16  # inner deferred removes per key state by default (round 6: any Id >= 16)
 
 
@@ -641,8 +641,8 @@ class MapNestedLub(NamedTuple):
     ec: torch.Tensor                  # (G, K, A) outer entry clocks
     ic: torch.Tensor                  # (G, K, A) inner Map clocks
     iec: torch.Tensor                 # (G, K, K2, A) inner entry clocks
-    ivc: torch.Tensor                 # (G, K, K2, 8, A) inner MVReg slot clocks
-    ivv: torch.Tensor                 # (G, K, K2, 8) values
+    ivc: torch.Tensor                 # (G, K, K2, Vs, A) inner MVReg slot clocks (Vs = v_cap, 8 by default)
+    ivv: torch.Tensor                 # (G, K, K2, Vs) values
     nval: torch.Tensor                # (G, K, K2) int32 slots used
     id_n: torch.Tensor                # (G, K) int32 inner deferred removes
     id_clock: torch.Tensor            # (G, K, Id, A)  (Id = id_cap, 16 by default)
@@ -657,7 +657,7 @@ def nested_lub_many(clock: torch.Tensor, ec: torch.Tensor, ic: torch.Tensor, iec
                     id_keys: Optional[torch.Tensor] = None, def_off=None, def_row: Optional[torch.Tensor] = None,
                     def_clock: Optional[torch.Tensor] = None, def_keys: Optional[torch.Tensor] = None,
                     ctx: Optional[Context] = None, check: bool = True,
-                    _key_shard: Optional[tuple] = None, id_cap=NM_ID) -> MapNestedLub:
+                    _key_shard: Optional[tuple] = None, id_cap=NM_ID, v_cap: int = NM_VS) -> MapNestedLub:
     """The exact left fold of Map::merge (map.rs:140-220) for Map<K, Map<K2, MVReg<u64>>> — the type of
     the reference's own Map tests (test/map.rs:10) — with the inner Map's merge (map.rs:140-220,
     mvreg.rs:112-128) and forget (map.rs:85-114) as the value's.  clock (G,R,A) / (R,A); ec, ic
@@ -669,7 +669,9 @@ def nested_lub_many(clock: torch.Tensor, ec: torch.Tensor, ic: torch.Tensor, iec
     removes named one key, bit 4: more than id_cap inner deferred removes, bit 5: id_off invalid, bit 6:
     more than 8 values on one inner key).  id_cap: inner deferred slots per key in the result (>= 16;
     round 6: the fold keeps 16 in LDS and re-folds exactly the keys that need more); "auto" sizes it to
-    the largest sum of one key's inner list lengths over its group's replicas."""
+    the largest sum of one key's inner list lengths over its group's replicas.  v_cap: MVReg slots per
+    inner key in the result (8..64; round 6: keys past 8 values re-fold in the deep pass, which also
+    takes inputs with V up to 64)."""
     ctx = ctx or Context.default(clock.device.index)
     squeeze = clock.dim() == 2
     c, e, i, ie, vc, vv = ((t.unsqueeze(0) if squeeze else t) for t in (clock, ec, ic, iec, ivc, ivv))
@@ -704,10 +706,13 @@ def nested_lub_many(clock: torch.Tensor, ec: torch.Tensor, ic: torch.Tensor, iec
         lens = (lens[1:] - lens[:-1]).clamp(min=0).reshape(G, R, K).sum(dim=1)
         id_cap = max(NM_ID, int(lens.max().item()) if lens.numel() else 0)
     Id = int(id_cap)
+    Vs = int(v_cap)
+    if not NM_VS <= Vs <= 64 or Vs < V:
+        raise ValueError(f"map.nested_lub_many: v_cap = {Vs} outside {max(NM_VS, V)}..64")
     if Id < NM_ID:
         raise ValueError(f"map.nested_lub_many: id_cap = {Id} < {NM_ID}")
     out = [torch.empty(sh, dtype=torch.int64, device=dev)
-           for sh in ((G, A), (G, K, A), (G, K, A), (G, K, K2, A), (G, K, K2, NM_VS, A), (G, K, K2, NM_VS),
+           for sh in ((G, A), (G, K, A), (G, K, A), (G, K, K2, A), (G, K, K2, Vs, A), (G, K, K2, Vs),
                       (G, K, Id, A), (G, K, Id) if K2w == 1 else (G, K, Id, K2w))]
     nval = torch.empty((G, K, K2), dtype=torch.int32, device=dev)
     id_n = torch.empty((G, K), dtype=torch.int32, device=dev)
@@ -720,7 +725,7 @@ def nested_lub_many(clock: torch.Tensor, ec: torch.Tensor, ic: torch.Tensor, iec
         b.id_clock, b.id_keys = id_clock.data_ptr(), id_keys.data_ptr()
     ob = _abi.MapNestedOut()
     ob.clock, ob.ec, ob.ic, ob.iec, ob.ivc, ob.ivv, ob.id_clock, ob.id_keys = (t.data_ptr() for t in out)
-    ob.nval, ob.id_n, ob.flags, ob.Id = nval.data_ptr(), id_n.data_ptr(), flags.data_ptr(), Id
+    ob.nval, ob.id_n, ob.flags, ob.Id, ob.Vs = nval.data_ptr(), id_n.data_ptr(), flags.data_ptr(), Id, Vs
     keep = keys_out = None
     off_arr = None
     if def_off is not None:
@@ -763,7 +768,7 @@ def nested_lub_many(clock: torch.Tensor, ec: torch.Tensor, ic: torch.Tensor, iec
             raise RuntimeError(f"map.nested_lub_many: more than id_cap = {Id} deferred removes in one key's inner "
                                "Map (id_cap='auto' always fits)")
         if f & 64:
-            raise RuntimeError("map.nested_lub_many: more than 8 values on one inner key")
+            raise RuntimeError(f"map.nested_lub_many: more than v_cap = {Vs} values on one inner key")
     oclk, oec, oic, oiec, oivc, oivv, oidc, oidk = out
     if squeeze:
         oclk, oec, oic, oiec, oivc, oivv, nval, id_n, oidc, oidk = (
@@ -1173,7 +1178,10 @@ def _nested_states(res, what):
     Id = res.id_clock.shape[2] if res.id_clock.dim() == 4 else -1  # inner deferred slots per key
     if Id < NM_ID:
         raise ValueError(f"{what}: id_clock (N, K, Id, A) with Id >= {NM_ID} expected")
-    shapes = dict(ec=(N, K, A), ic=(N, K, A), iec=(N, K, K2, A), ivc=(N, K, K2, 8, A), ivv=(N, K, K2, 8),
+    Vs = res.ivc.shape[3] if res.ivc.dim() == 5 else -1  # MVReg slots per inner key
+    if not NM_VS <= Vs <= 64:
+        raise ValueError(f"{what}: ivc (N, K, K2, Vs, A) with Vs in {NM_VS}..64 expected")
+    shapes = dict(ec=(N, K, A), ic=(N, K, A), iec=(N, K, K2, A), ivc=(N, K, K2, Vs, A), ivv=(N, K, K2, Vs),
                   nval=(N, K, K2), id_n=(N, K), id_clock=(N, K, Id, A),
                   id_keys=(N, K, Id) if K2w == 1 else (N, K, Id, K2w))
     for nm, shp in shapes.items():
@@ -1183,7 +1191,7 @@ def _nested_states(res, what):
     if not clock.is_contiguous():
         raise ValueError(f"{what}: clock must be contiguous")
     st = _abi.MapNestedStates()
-    st.N, st.K, st.K2, st.A, st.Id = N, K, K2, A, Id
+    st.N, st.K, st.K2, st.A, st.Id, st.Vs = N, K, K2, A, Id, Vs
     for nm in ("clock", "ec", "ic", "iec", "ivc", "ivv", "nval", "id_n", "id_clock", "id_keys"):
         setattr(st, nm, getattr(res, nm).data_ptr())
     return st, N, K, A

@@ -259,8 +259,8 @@ class MapNestedFrames(NamedTuple):
     ec: torch.Tensor         # (N, K, A)
     ic: torch.Tensor         # (N, K, A)
     iec: torch.Tensor        # (N, K, K2, A)
-    ivc: torch.Tensor        # (N, K, K2, 8, A)
-    ivv: torch.Tensor        # (N, K, K2, 8)
+    ivc: torch.Tensor        # (N, K, K2, Vs, A)  (Vs MVReg slots per inner key, 8 by default)
+    ivv: torch.Tensor        # (N, K, K2, Vs)
     nval: torch.Tensor       # (N, K, K2) int32
     id_n: torch.Tensor       # (N, K) int32
     id_clock: torch.Tensor   # (N, K, Id, A)  (Id inner deferred slots per key, 16 by default)
@@ -399,20 +399,24 @@ def _nested_struct(ctx, st, what):
     Id = st.id_clock.shape[2] if st.id_clock.dim() == 4 else 0
     if Id < 16:
         raise ValueError(f"{what}: id_clock (N, K, Id, A) with Id >= 16 expected")
-    shapes = dict(ic=(N, K, A), iec=(N, K, K2, A), ivc=(N, K, K2, 8, A), ivv=(N, K, K2, 8), nval=(N, K, K2),
+    Vs = st.ivc.shape[3] if st.ivc.dim() == 5 else 0
+    if not 8 <= Vs <= 64:
+        raise ValueError(f"{what}: ivc (N, K, K2, Vs, A) with Vs in 8..64 expected")
+    shapes = dict(ic=(N, K, A), iec=(N, K, K2, A), ivc=(N, K, K2, Vs, A), ivv=(N, K, K2, Vs), nval=(N, K, K2),
                   id_n=(N, K), id_clock=(N, K, Id, A), id_keys=(N, K, Id) if K2w == 1 else (N, K, Id, K2w))
     for nm, shp in shapes.items():
         if tuple(getattr(st, nm).shape) != shp:
             raise ValueError(f"{what}: {nm} must be {shp}")
     s = _abi.MapNestedStates()
-    s.N, s.K, s.K2, s.A, s.Id = N, K, K2, A, Id
+    s.N, s.K, s.K2, s.A, s.Id, s.Vs = N, K, K2, A, Id, Vs
     for nm in ("clock", "ec", "ic", "iec", "ivc", "ivv", "nval", "id_n", "id_clock", "id_keys"):
         setattr(s, nm, dptr(getattr(st, nm)))
     return s, _vmap_deferred(st)
 
 
 def map_nested_ingest(data: torch.Tensor, frame_off: torch.Tensor, actors: torch.Tensor, keys: torch.Tensor,
-                      ikeys: torch.Tensor, Dcap: int, ctx: Optional[Context] = None, id_cap: int = 16):
+                      ikeys: torch.Tensor, Dcap: int, ctx: Optional[Context] = None, id_cap: int = 16,
+                      v_cap: int = 8):
     """Map<u32, Map<u32, MVReg<u64>>> frames -> (MapNestedFrames, status (N,) int32); ikeys: sorted
     u32 inner-key dictionary (int32 tensor, at most 256; past 64 the inner key sets are K2w words)."""
     ctx = _ctx(data, ctx)
@@ -423,7 +427,7 @@ def map_nested_ingest(data: torch.Tensor, frame_off: torch.Tensor, actors: torch
     dev = data.device
     z = lambda *shape: torch.zeros(shape, dtype=torch.int64, device=dev)  # noqa: E731
     z32 = lambda *shape: torch.zeros(shape, dtype=torch.int32, device=dev)  # noqa: E731
-    st = MapNestedFrames(z(N, A), z(N, K, A), z(N, K, A), z(N, K, K2, A), z(N, K, K2, 8, A), z(N, K, K2, 8),
+    st = MapNestedFrames(z(N, A), z(N, K, A), z(N, K, A), z(N, K, K2, A), z(N, K, K2, v_cap, A), z(N, K, K2, v_cap),
                          z32(N, K, K2), z32(N, K), z(N, K, id_cap, A),
                          z(N, K, id_cap) if K2 <= 64 else z(N, K, id_cap, (K2 + 63) // 64), z(N, Dcap, A),
                          z(N, Dcap, (K + 63) // 64), z32(N))

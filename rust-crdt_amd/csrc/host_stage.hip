@@ -1134,7 +1134,7 @@ static int map_nested_lub_host_body(crdt_ctx *ctx, const crdt_map_nested_batch *
                                     DevScratch &ds) {
   const size_t G = in->G, R = in->R, K = in->K, K2 = in->K2, V = in->V, A = in->A, Kw = (K + 63) / 64, Di = in->Di;
   const size_t D = in->def_off ? in->def_off[G] : 0, N = G * R * K;
-  constexpr size_t VS = 8;  // output slots per inner key (crdt_gpu.h)
+  const size_t VS = out->Vs ? out->Vs : 8;  // output slots per inner key (crdt_gpu.h)
   const size_t ID = out->Id ? out->Id : 16;  // inner deferred slots per key in the output
   uint64_t *c, *e, *ic, *iec, *ivc, *ivv, *io, *idc, *idk, *dc, *dk, *oc, *oe, *oic, *oiec, *oivc, *oivv, *oidc, *oidk,
       *ok2 = nullptr;
@@ -1194,7 +1194,7 @@ static int map_nested_lub_host_body(crdt_ctx *ctx, const crdt_map_nested_batch *
   b.def_row = dr;
   b.def_clock = dc;
   b.def_keys = dk;
-  crdt_map_nested_out ob{oc, oe, oic, oiec, oivc, oivv, onv, oidn, oidc, oidk, of, okp, ok2, ID};
+  crdt_map_nested_out ob{oc, oe, oic, oiec, oivc, oivv, onv, oidn, oidc, oidk, of, okp, ok2, ID, VS};
   {
     DeviceModeScope dev(ctx);
     if (int rc = crdt_map_nested_lub_many(ctx, &b, &ob)) return rc;

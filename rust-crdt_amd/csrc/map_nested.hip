@@ -61,7 +61,9 @@ struct NestedMapPlan {
   unsigned long long Id;
   uint8_t *ovf;
   unsigned long long Lc;  // the deep pass's live outer-remove capacity per key (>= kNmLive)
+  unsigned long long Vs;  // the output's MVReg slots per inner key (>= kNmVs; the deep pass holds all)
 };
+constexpr int kNmVsMax = 64;  // (the deep pass's kept-slot masks are one word)
 
 // A clock across the wave: lane l holds actors l + 64 j, j < APL (A <= 64 APL; round 6: APL 2 and 4 take
 // the reference's TMap domain of u8 actors).  Words past A are 0 in every row, so they never change a
@@ -299,8 +301,11 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
   int nd = 0;  // inner deferred removes held (uniform)
   // (generic pointers: the LDS copy when it fits, else the key's own output rows)
   u64 *const iec_o = p.xs_state ? xst : p.o_iec + gk * K2 * A;
-  u64 *const ivc_o = p.xs_state ? xst + K2 * A : p.o_ivc + gk * K2 * kNmVs * A;
-  u64 *const ivv_o = p.xs_state ? xst + K2 * A + K2 * kNmVs * A : p.o_ivv + gk * K2 * kNmVs;
+  // MVReg slots: VSt the state rows' stride (the output's Vs, or kNmVs in the LDS copy), VC those held
+  const unsigned long long VSt = p.xs_state ? (unsigned long long)kNmVs : p.Vs;
+  const int VC = DEEP ? (int)p.Vs : kNmVs;
+  u64 *const ivc_o = p.xs_state ? xst + K2 * A : p.o_ivc + gk * K2 * VSt * A;
+  u64 *const ivv_o = p.xs_state ? xst + K2 * A + K2 * kNmVs * A : p.o_ivv + gk * K2 * VSt;
   for (unsigned long long j = 0; j < K2; ++j) {
     st(iec_o + j * A, Z);
     if (lane == 0) nv[j] = 0;
@@ -311,11 +316,11 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
     const int n = __builtin_amdgcn_readfirstlane((int)nv[j]);
     int o = 0;
     for (int s = 0; s < n; ++s) {
-      const Vc c = nm_fg(ld(ivc_o + (j * kNmVs + s) * A), x);
+      const Vc c = nm_fg(ld(ivc_o + (j * VSt + s) * A), x);
       if (!nm_nz(c)) continue;
-      const u64 v = ivv_o[j * kNmVs + s];
-      st(ivc_o + (j * kNmVs + o) * A, c);
-      ivv_o[j * kNmVs + o] = v;  // (every lane stores the value: each later reads back its own store)
+      const u64 v = ivv_o[j * VSt + s];
+      st(ivc_o + (j * VSt + o) * A, c);
+      ivv_o[j * VSt + o] = v;  // (every lane stores the value: each later reads back its own store)
       ++o;
     }
     if (lane == 0) nv[j] = (uint8_t)o;
@@ -434,9 +439,9 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
         for (unsigned long long s = 0; s < V; ++s) {
           const Vc c = ld(rc + (j * V + s) * A);
           if (!nm_nz(c)) continue;
-          if (o < kNmVs) {
-            st(ivc_o + (j * kNmVs + o) * A, c);
-            ivv_o[j * kNmVs + o] = rv[j * V + s];
+          if (o < VC) {
+            st(ivc_o + (j * VSt + o) * A, c);
+            ivv_o[j * VSt + o] = rv[j * V + s];
             ++o;
           } else {
             vfull = true;
@@ -468,6 +473,58 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
         continue;
       }
       const Vc xj = nm_fg(q1 ? (q2 ? nm_max(ej, e2j) : ic2) : ic, enj);
+      if constexpr (DEEP) {  // the same merge with our slots read from the rows one at a time (up to Vs)
+        // (the replica's V slots are read from its rows too: V may pass kNmVin here)
+        const int n1 = q1 ? __builtin_amdgcn_readfirstlane((int)nv[j]) : 0, n2 = q2 ? (int)V : 0;
+        u64 m2 = 0;  // the replica's non-empty slots
+        for (int t = 0; t < n2; ++t)
+          if (nm_nz(ld(rc + (j * V + t) * A))) m2 |= 1ull << t;
+        u64 keep1 = 0;  // ours not strictly below one of the replica's
+        for (int s2 = 0; s2 < n1; ++s2) {
+          const Vc c = ld(ivc_o + (j * VSt + s2) * A);
+          bool dominated = false;
+          for (int t = 0; t < n2 && !dominated; ++t)
+            if (((m2 >> t) & 1ull) && nm_lt(c, ld(rc + (j * V + t) * A))) dominated = true;
+          if (!dominated) keep1 |= 1ull << s2;
+        }
+        u64 keep2 = 0;  // the replica's not strictly below or equal to a kept one of ours
+        for (int t = 0; t < n2; ++t) {
+          if (!((m2 >> t) & 1ull)) continue;
+          const Vc ct = ld(rc + (j * V + t) * A);
+          bool drop = false;
+          for (int s2 = 0; s2 < n1 && !drop; ++s2) {
+            if (!((keep1 >> s2) & 1ull)) continue;
+            const Vc c = ld(ivc_o + (j * VSt + s2) * A);
+            if (nm_lt(ct, c) || nm_eq(ct, c)) drop = true;
+          }
+          if (!drop) keep2 |= 1ull << t;
+        }
+        int o = 0;  // kept slots forgotten by xj, in order (o <= s2: compacted in place)
+        for (int s2 = 0; s2 < n1; ++s2) {
+          if (!((keep1 >> s2) & 1ull)) continue;
+          const Vc c = nm_fg(ld(ivc_o + (j * VSt + s2) * A), xj);
+          if (!nm_nz(c)) continue;
+          const u64 v = ivv_o[j * VSt + s2];
+          st(ivc_o + (j * VSt + o) * A, c);
+          ivv_o[j * VSt + o] = v;
+          ++o;
+        }
+        for (int t = 0; t < n2; ++t) {
+          if (!((keep2 >> t) & 1ull)) continue;
+          const Vc c = nm_fg(ld(rc + (j * V + t) * A), xj);
+          if (!nm_nz(c)) continue;
+          if (o < VC) {
+            st(ivc_o + (j * VSt + o) * A, c);
+            ivv_o[j * VSt + o] = rv[j * V + t];
+            ++o;
+          } else {
+            vfull = true;
+          }
+        }
+        if (lane == 0) nv[j] = (uint8_t)o;
+        st(iec_o + j * A, enj);
+        continue;
+      }
       // the slots: ours (Vec order), then the replica's (MVReg::merge, mvreg.rs:112-128), forgotten by xj
       // (every register array is indexed by unrolled constants only: the replica's slots keep their
       // own positions with a validity mask m2 instead of being compacted by a running count, which
@@ -478,8 +535,8 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
       unsigned m2 = 0;
 #pragma unroll
       for (int s = 0; s < kNmVs; ++s) {
-        cs[s] = s < n1 ? ld(ivc_o + (j * kNmVs + s) * A) : Z;
-        vs[s] = s < n1 ? ivv_o[j * kNmVs + s] : 0;
+        cs[s] = s < n1 ? ld(ivc_o + (j * VSt + s) * A) : Z;
+        vs[s] = s < n1 ? ivv_o[j * VSt + s] : 0;
       }
 #pragma unroll
       for (int s = 0; s < kNmVin; ++s) {
@@ -532,8 +589,8 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
         if (!((keep1 >> s) & 1u)) continue;
         const Vc c = nm_fg(cs[s], xj);
         if (!nm_nz(c)) continue;
-        st(ivc_o + (j * kNmVs + o) * A, c);  // (the slots were read into registers above)
-        ivv_o[j * kNmVs + o] = vs[s];
+        st(ivc_o + (j * VSt + o) * A, c);  // (the slots were read into registers above)
+        ivv_o[j * VSt + o] = vs[s];
         ++o;
       }
 #pragma unroll
@@ -542,8 +599,8 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
         const Vc c = nm_fg(co[t], xj);
         if (!nm_nz(c)) continue;
         if (o < kNmVs) {
-          st(ivc_o + (j * kNmVs + o) * A, c);
-          ivv_o[j * kNmVs + o] = vo[t];
+          st(ivc_o + (j * VSt + o) * A, c);
+          ivv_o[j * VSt + o] = vo[t];
           ++o;
         } else {
           vfull = true;
@@ -687,16 +744,16 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
   const bool pf = nm_nz(e);
   st(p.o_ec + gk * A, e);
   st(p.o_ic + gk * A, pf ? ic : Z);
-  u64 *const oiec = p.o_iec + gk * K2 * A, *const oivc = p.o_ivc + gk * K2 * kNmVs * A;
-  u64 *const oivv = p.o_ivv + gk * K2 * kNmVs;
+  u64 *const oiec = p.o_iec + gk * K2 * A, *const oivc = p.o_ivc + gk * K2 * p.Vs * A;
+  u64 *const oivv = p.o_ivv + gk * K2 * p.Vs;
   for (unsigned long long j = 0; j < K2; ++j) {
     const int n = pf ? __builtin_amdgcn_readfirstlane((int)nv[j]) : 0;
     st(oiec + j * A, pf ? ld(iec_o + j * A) : Z);  // (the same word when the state is the output)
-    for (int s = 0; s < kNmVs; ++s) {  // the held slots, then zeros
-      const Vc c = s < n ? ld(ivc_o + (j * kNmVs + s) * A) : Z;
-      const u64 v = s < n ? ivv_o[j * kNmVs + s] : 0ull;
-      st(oivc + (j * kNmVs + s) * A, c);
-      oivv[j * kNmVs + s] = v;
+    for (int s = 0; s < (int)p.Vs; ++s) {  // the held slots, then zeros
+      const Vc c = s < n ? ld(ivc_o + (j * VSt + s) * A) : Z;
+      const u64 v = s < n ? ivv_o[j * VSt + s] : 0ull;
+      st(oivc + (j * p.Vs + s) * A, c);
+      oivv[j * p.Vs + s] = v;
     }
     if (lane == 0) p.o_nval[gk * K2 + j] = (unsigned)n;
   }
@@ -710,10 +767,10 @@ __global__ __launch_bounds__(kNmWaves * kWave) void map_nested_fold_kernel(Neste
   if (lane == 0) p.o_id_n[gk] = (unsigned)no;
   if constexpr (!DEEP) {
     // past the LDS slots / the live list, where the deep pass has room for both: it re-folds this key
-    if ((dfull || full) && p.ovf && (!dfull || p.Id > (unsigned long long)kNmId) &&
-        (!full || p.Lc > (unsigned long long)kNmLive)) {
+    if ((dfull || full || vfull) && p.ovf && (!dfull || p.Id > (unsigned long long)kNmId) &&
+        (!full || p.Lc > (unsigned long long)kNmLive) && (!vfull || p.Vs > (unsigned long long)kNmVs)) {
       if (lane == 0) p.ovf[gk] = 1;
-      dfull = full = false;
+      dfull = full = vfull = false;
     }
   }
   if ((bad || full || dfull || vfull) && lane == 0)
@@ -756,7 +813,7 @@ extern "C" int crdt_map_nested_lub_many(crdt_ctx *ctx, const crdt_map_nested_bat
   if (G == 0 || K == 0 || A == 0) return CRDT_OK;
   if (A > 4 * (size_t)kWave) return fail(ctx, CRDT_EUNSUPPORTED, "map_nested_lub_many: A = %zu > %d", A, 4 * kWave);
   if (K2 > (size_t)kNmK2) return fail(ctx, CRDT_EUNSUPPORTED, "map_nested_lub_many: K2 = %zu > %d", K2, kNmK2);
-  if (V > (size_t)kNmVin) return fail(ctx, CRDT_EUNSUPPORTED, "map_nested_lub_many: V = %zu > %d", V, kNmVin);
+  if (V > (size_t)kNmVsMax) return fail(ctx, CRDT_EUNSUPPORTED, "map_nested_lub_many: V = %zu > %d", V, kNmVsMax);
   if (!out->clock || !out->ec || !out->ic || (K2 && (!out->iec || !out->ivc || !out->ivv || !out->nval)) ||
       !out->id_n || !out->id_clock || !out->id_keys || !out->flags)
     return fail(ctx, CRDT_EINVAL, "map_nested_lub_many: NULL output");
@@ -784,7 +841,13 @@ extern "C" int crdt_map_nested_lub_many(crdt_ctx *ctx, const crdt_map_nested_bat
   size_t Lc = kNmLive;
   for (size_t i = 0; in->def_off && i < G; ++i) Lc = std::max<size_t>(Lc, in->def_off[i + 1] - in->def_off[i]);
   while (Lc > (size_t)kNmLive && nm_deep_lds(apl0, Id, Lc) > kNmDeepLds) Lc = std::max<size_t>(kNmLive, Lc / 2);
-  const bool deep = Id > (size_t)kNmId || Lc > (size_t)kNmLive;
+  const size_t Vs = out->Vs ? out->Vs : (size_t)kNmVs;  // MVReg slots per inner key in the output
+  if (Vs < (size_t)kNmVs || Vs > (size_t)kNmVsMax)
+    return fail(ctx, CRDT_EUNSUPPORTED, "map_nested_lub_many: out->Vs = %zu outside %d..%d", Vs, kNmVs, kNmVsMax);
+  // inputs with more than kNmVin slots per inner key go to the deep pass alone (every key marked)
+  const bool deep_only = V > (size_t)kNmVin;
+  if (deep_only && Vs < V) return fail(ctx, CRDT_EINVAL, "map_nested_lub_many: out->Vs = %zu < V = %zu", Vs, V);
+  const bool deep = deep_only || Id > (size_t)kNmId || Lc > (size_t)kNmLive || Vs > (size_t)kNmVs;
   if (deep && G * K > 0x7fffffffULL) return fail(ctx, CRDT_EUNSUPPORTED, "map_nested_lub_many: G*K too large");
   CRDT_HIP(ctx, hipSetDevice(ctx->device));
   const size_t Kw = (K + 63) / 64;
@@ -798,6 +861,7 @@ extern "C" int crdt_map_nested_lub_many(crdt_ctx *ctx, const crdt_map_nested_bat
   p.Id = Id;
   p.ovf = nullptr;
   p.Lc = Lc;
+  p.Vs = Vs;
   if (int rc = device_fill(ctx, out->flags, G * sizeof(unsigned), 0)) return rc;
   if (R == 0) {  // fold of nothing: Map::new()
     if (int rc = device_fill(ctx, out->clock, G * A * 8, 0)) return rc;
@@ -805,8 +869,8 @@ extern "C" int crdt_map_nested_lub_many(crdt_ctx *ctx, const crdt_map_nested_bat
     if (int rc = device_fill(ctx, out->ic, G * K * A * 8, 0)) return rc;
     if (K2) {
       if (int rc = device_fill(ctx, out->iec, G * K * K2 * A * 8, 0)) return rc;
-      if (int rc = device_fill(ctx, out->ivc, G * K * K2 * kNmVs * A * 8, 0)) return rc;
-      if (int rc = device_fill(ctx, out->ivv, G * K * K2 * kNmVs * 8, 0)) return rc;
+      if (int rc = device_fill(ctx, out->ivc, G * K * K2 * Vs * A * 8, 0)) return rc;
+      if (int rc = device_fill(ctx, out->ivv, G * K * K2 * Vs * 8, 0)) return rc;
       if (int rc = device_fill(ctx, out->nval, G * K * K2 * sizeof(unsigned), 0)) return rc;
     }
     if (int rc = device_fill(ctx, out->id_n, G * K * sizeof(unsigned), 0)) return rc;
@@ -820,9 +884,9 @@ extern "C" int crdt_map_nested_lub_many(crdt_ctx *ctx, const crdt_map_nested_bat
       if (int rc = stage_h2d(ctx, ctx->scratch, in->def_off, (G + 1) * sizeof(size_t))) return rc;
       p.def_off = reinterpret_cast<const size_t *>(ctx->scratch);
     }
-    if (sv) {
+    if (sv) {  // (deep_only: every key marked, the first pass skipped)
       p.ovf = static_cast<uint8_t *>(ctx->scratch) + so;
-      if (int rc = device_fill(ctx, p.ovf, sv, 0)) return rc;
+      if (int rc = device_fill(ctx, p.ovf, sv, deep_only ? 1 : 0)) return rc;
     }
     {
       const unsigned long long n = (unsigned long long)G * R * K;
@@ -860,7 +924,8 @@ extern "C" int crdt_map_nested_lub_many(crdt_ctx *ctx, const crdt_map_nested_bat
     }
     timing_begin(ctx, "map_nested_fold");
     const unsigned long long blocks = (G * K + wpb - 1) / wpb;
-    if (apl == 1)
+    if (deep_only) {
+    } else if (apl == 1)
       hipLaunchKernelGGL(map_nested_fold_kernel<1>, dim3((unsigned)blocks), dim3(wpb * kWave), lds, ctx->stream, p);
     else if (apl == 2)
       hipLaunchKernelGGL(map_nested_fold_kernel<2>, dim3((unsigned)blocks), dim3(wpb * kWave), lds, ctx->stream, p);

@@ -35,6 +35,7 @@ struct NestedApplyPlan {
   unsigned long long N, K, K2, A, Kw, Dcap;
   unsigned long long K2w;  // inner-key mask words per key set (1 up to K2 = 64: the round-5 layout)
   unsigned long long Id;   // inner deferred slots per key (crdt_map_nested_states.Id; 16 if 0)
+  unsigned long long Vs;   // MVReg slots per inner key (crdt_map_nested_states.Vs; 8 if 0)
   unsigned long long Dl;  // outer deferred slots held in LDS (<= Dcap); slots Dl .. Dcap-1 stay in place
   u64 *def_clock, *def_keys;
   unsigned *def_count;
@@ -90,6 +91,7 @@ struct NaKey {
   mutable unsigned stb;  // status bits raised by these operations (the caller ORs them in)
   unsigned kw_;          // mask words per key set (KW > 1)
   unsigned cap;          // inner deferred slots (round 6: states->Id)
+  unsigned vs;           // MVReg slots per inner key (round 6: states->Vs)
   __device__ __forceinline__ unsigned kwn() const { return KW == 1 ? 1u : kw_; }
 
   // held remove i's key set in registers (words past kwn(): 0) and back
@@ -146,36 +148,36 @@ struct NaKey {
     for (int j = 0; j < APL; ++j) x[j] = x[j] > r[j] ? x[j] : 0ull;
   }
   __device__ __forceinline__ u64 *slot(unsigned long long jk, unsigned i) const {
-    return ivc + (jk * kNaVs + i) * A;
+    return ivc + (jk * vs + i) * A;
   }
 
   // MVReg::forget of inner key jk's register (order kept, emptied values dropped)
   __device__ void reg_forget(unsigned long long jk, const u64 (&r)[APL]) const {
-    const unsigned n = nval[jk];
+    const unsigned n = min(vs, nval[jk]);
     unsigned o = 0;
     for (unsigned i = 0; i < n; ++i) {
       u64 x[APL];
       ld(slot(jk, i), x);
       fg(x, r);
       if (!nz(x)) continue;
-      const u64 v = ivv[jk * kNaVs + i];
+      const u64 v = ivv[jk * vs + i];
       st_(slot(jk, o), x);
-      ivv[jk * kNaVs + o] = v;
+      ivv[jk * vs + o] = v;
       ++o;
     }
     for (unsigned i = o; i < n; ++i) {
       zero(slot(jk, i));
-      ivv[jk * kNaVs + i] = 0;
+      ivv[jk * vs + i] = 0;
     }
     nval[jk] = o;
   }
   // drop inner entry jk (its rows all zero)
   __device__ void inner_drop(unsigned long long jk) const {
     zero(iec + jk * A);
-    const unsigned n = nval[jk];
+    const unsigned n = min(vs, nval[jk]);
     for (unsigned i = 0; i < n; ++i) {
       zero(slot(jk, i));
-      ivv[jk * kNaVs + i] = 0;
+      ivv[jk * vs + i] = 0;
     }
     nval[jk] = 0;
   }
@@ -254,7 +256,7 @@ struct NaKey {
   // MVReg::apply(Put { clock: r, val }) on inner key jk (mvreg.rs:130-166)
   __device__ void reg_put(unsigned long long jk, const u64 (&r)[APL], u64 v) const {
     if (!nz(r)) return;
-    const unsigned n = nval[jk];
+    const unsigned n = min(vs, nval[jk]);
     unsigned o = 0;
     bool dominated = false;
     for (unsigned i = 0; i < n; ++i) {
@@ -262,24 +264,24 @@ struct NaKey {
       ld(slot(jk, i), x);
       if (leq(x, r)) continue;             // Less or Equal: dropped
       if (leq(r, x)) dominated = true;     // (x != r here) strictly greater: the Put is not added
-      const u64 xv = ivv[jk * kNaVs + i];
+      const u64 xv = ivv[jk * vs + i];
       if (o != i) {
         st_(slot(jk, o), x);
-        ivv[jk * kNaVs + o] = xv;
+        ivv[jk * vs + o] = xv;
       }
       ++o;
     }
     for (unsigned i = o; i < n; ++i) {
       zero(slot(jk, i));
-      ivv[jk * kNaVs + i] = 0;
+      ivv[jk * vs + i] = 0;
     }
     if (!dominated) {
-      if (o < (unsigned)kNaVs) {
+      if (o < vs) {
         st_(slot(jk, o), r);
-        ivv[jk * kNaVs + o] = v;
+        ivv[jk * vs + o] = v;
         ++o;
       } else {
-        stb |= 16u;  // the register needed more than 8 values
+        stb |= 16u;  // the register needed more than vs values
       }
     }
     nval[jk] = o;
@@ -384,10 +386,10 @@ template <int APL, int KW = 1>
 __device__ __forceinline__ NaKey<APL, KW> na_key(const NestedApplyPlan &p, unsigned long long s, unsigned long long k,
                                              int lane) {
   const unsigned long long sk = s * p.K + k, A = p.A, K2 = p.K2;
-  return NaKey<APL, KW>{p.ec + sk * A, p.ic + sk * A, p.iec + sk * K2 * A, p.ivc + sk * K2 * kNaVs * A,
-                    p.ivv + sk * K2 * kNaVs, p.id_clock + sk * p.Id * A, p.id_keys + sk * p.Id * p.K2w,
+  return NaKey<APL, KW>{p.ec + sk * A, p.ic + sk * A, p.iec + sk * K2 * A, p.ivc + sk * K2 * p.Vs * A,
+                    p.ivv + sk * K2 * p.Vs, p.id_clock + sk * p.Id * A, p.id_keys + sk * p.Id * p.K2w,
                     p.nval + sk * K2, p.id_n + sk, A, K2, lane, 0u, (unsigned)p.K2w,
-                    (unsigned)p.Id};
+                    (unsigned)p.Id, (unsigned)p.Vs};
 }
 
 // TIER false: every state, the Map's deferred list in the Dl LDS slots only; a state whose list
@@ -670,6 +672,7 @@ static NestedApplyPlan nested_plan(const crdt_map_nested_states *m) {
   p.K2 = m->K2;
   p.K2w = m->K2 > 64 ? (m->K2 + 63) / 64 : 1;
   p.Id = m->Id ? m->Id : (size_t)kNaId;
+  p.Vs = m->Vs ? m->Vs : (size_t)kNaVs;
   p.A = m->A;
   p.Kw = m->K ? (m->K + 63) / 64 : 1;
   return p;

@@ -400,7 +400,8 @@ extern "C" int crdt_map_nested_merge_batch(crdt_ctx *ctx, const crdt_map_nested_
         !s->id_clock || !s->id_keys)
       return fail(ctx, CRDT_EINVAL, "%s: NULL state buffer", what);
   CRDT_HIP(ctx, hipSetDevice(ctx->device));
-  const size_t Kw = (K + 63) / 64, VS = 8;
+  const size_t Kw = (K + 63) / 64, VS = a->Vs ? a->Vs : 8;  // MVReg slots per inner key (both sides)
+  if ((b->Vs ? b->Vs : 8) != VS) return fail(ctx, CRDT_EINVAL, "%s: self and other differ in Vs", what);
   const size_t K2w = K2 > 64 ? (K2 + 63) / 64 : 1;  // inner key-set mask words (the fold's layout)
   std::vector<size_t> off;
   if (int rc = pool_offsets(ctx, ad, bd, N, off, what)) return rc;
@@ -468,6 +469,7 @@ extern "C" int crdt_map_nested_merge_batch(crdt_ctx *ctx, const crdt_map_nested_
   out.id_clock = a->id_clock;
   out.id_keys = a->id_keys;
   out.Id = Ia;  // (self's slots: other's lists merge into them, bit 3 past Ia)
+  out.Vs = VS;
   out.flags = reinterpret_cast<uint32_t *>(base + of);
   out.def_keep = pl.keep;
   out.def_keys = reinterpret_cast<uint64_t *>(pl.kout);

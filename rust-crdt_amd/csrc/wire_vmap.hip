@@ -36,6 +36,7 @@ struct VMapWirePlan {
   const uint32_t *actors, *keys, *ikeys;
   const u64 *members;
   unsigned long long K2, K2w;  // inner keys; inner key-set mask words (1 up to K2 = 64)
+  unsigned long long Vs;       // MVReg slots per inner key (crdt_map_nested_states.Vs; 8 if 0)
   u64 *ic, *iec, *ivc, *ivv, *id_clock, *id_keys;  // nested Map [N][K][A], [N][K][K2][A], [N][K][K2][8][A],
   uint32_t *nval, *id_n;                           // [N][K][K2][8], [N][K][16][A], [N][K][16][K2w]; [N][K][K2], [N][K]
   u64 *clock, *ec, *val;           // [N][A], [N][K][A], counter [N][K][W][A]
@@ -179,9 +180,9 @@ __global__ __launch_bounds__(kBlock) void vmap_ingest_kernel(VMapWirePlan p) {
               const u64 val = rd64(f.w, k);
               k += 2;
               if (on) {
-                if (nv < (unsigned long long)kVwVs) {
-                  store_row<u64>(p.ivc + (skj * kVwVs + nv) * p.A, row, p.A, lane);
-                  if (lane == 0) p.ivv[skj * kVwVs + nv] = val;
+                if (nv < p.Vs) {
+                  store_row<u64>(p.ivc + (skj * p.Vs + nv) * p.A, row, p.A, lane);
+                  if (lane == 0) p.ivv[skj * p.Vs + nv] = val;
                   ++nv;
                 } else {
                   st |= kWireCap;
@@ -373,7 +374,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
           const unsigned long long skj = sk * p.K2 + j;
           const u64 *er2 = p.iec + skj * p.A;
           if (nnz_row(er2, p.A, lane) == 0) continue;
-          const unsigned long long m = p.nval[skj] < (uint32_t)kVwVs ? p.nval[skj] : kVwVs;
+          const unsigned long long m = p.nval[skj] < p.Vs ? p.nval[skj] : p.Vs;
           sz += 4 + vclock_bytes(er2, p.A, lane) + 8;
           if (write) {
             if (lane == 0) w[k] = p.ikeys[j];
@@ -382,11 +383,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
             k += 2;
           }
           for (unsigned long long v = 0; v < m; ++v) {
-            const u64 *vr = p.ivc + (skj * kVwVs + v) * p.A;
+            const u64 *vr = p.ivc + (skj * p.Vs + v) * p.A;
             sz += vclock_bytes(vr, p.A, lane) + 8;
             if (write) {
               k = write_vclock(w, k, vr, p.A, p.actors, lane);
-              if (lane == 0) wr64(w, k, p.ivv[skj * kVwVs + v]);
+              if (lane == 0) wr64(w, k, p.ivv[skj * p.Vs + v]);
               k += 2;
             }
           }
@@ -558,6 +559,8 @@ static int vmap_nested_plan(crdt_ctx *ctx, const crdt_map_nested_states *st, con
   p.K2 = K2;
   p.K2w = K2 > 64 ? (K2 + 63) / 64 : 1;
   p.Vd = st->Id ? st->Id : (size_t)kVwVd;
+  p.Vs = st->Vs ? st->Vs : (size_t)kVwVs;
+  if (p.Vs > 64) return fail(ctx, CRDT_EUNSUPPORTED, "%s: Vs = %zu > 64", what, (size_t)p.Vs);
   p.vt = 2;
   p.actors = actors;
   p.keys = keys;
@@ -588,8 +591,8 @@ static int vmap_ingest(crdt_ctx *ctx, VMapWirePlan &p, const uint8_t *bytes, con
   } else if (p.vt == 2) {
     if (int rc = device_fill(ctx, p.ic, N * p.K * p.A * 8, 0)) return rc;
     if (int rc = device_fill(ctx, p.iec, N * p.K * p.K2 * p.A * 8, 0)) return rc;
-    if (int rc = device_fill(ctx, p.ivc, N * p.K * p.K2 * kVwVs * p.A * 8, 0)) return rc;
-    if (int rc = device_fill(ctx, p.ivv, N * p.K * p.K2 * kVwVs * 8, 0)) return rc;
+    if (int rc = device_fill(ctx, p.ivc, N * p.K * p.K2 * p.Vs * p.A * 8, 0)) return rc;
+    if (int rc = device_fill(ctx, p.ivv, N * p.K * p.K2 * p.Vs * 8, 0)) return rc;
     if (int rc = device_fill(ctx, p.nval, N * p.K * p.K2 * 4, 0)) return rc;
     if (int rc = device_fill(ctx, p.id_n, N * p.K * 4, 0)) return rc;
     if (int rc = device_fill(ctx, p.id_clock, N * p.K * p.Vd * p.A * 8, 0)) return rc;

@@ -1451,11 +1451,11 @@ impl<K: Ord + Clone, M: Member, A: Actor> BatchCvRDT for Map<K, Orswot<M, A>, A>
     }
 }
 
-/// Limits of the nested Map fold (include/crdt_gpu.h: A <= 256 and K2 <= 256 since round 6, V <= 8 values
-/// per register).  Past 64 inner keys an inner key set is ceil(K2/64) mask words.
+/// Limits of the nested Map fold (include/crdt_gpu.h: A <= 256, K2 <= 256 and V <= 64 values per register
+/// since round 6).  Past 64 inner keys an inner key set is ceil(K2/64) mask words.
 pub const MAP_NESTED_MAX_ACTORS: usize = 256;
 pub const MAP_NESTED_MAX_INNER_KEYS: usize = 256;
-pub const MAP_NESTED_MAX_VALUES: usize = 8;
+pub const MAP_NESTED_MAX_VALUES: usize = 64;  // (round 6: past 8 the library's deep pass; was 8)
 
 /// Every group's fold of Map<K, Map<K2, MVReg<V>>> (crdt_map_nested_lub_many, G groups of equal R) —
 /// the type of the reference's own Map tests (test/map.rs:10).  Values travel as arena ids, as for
@@ -1541,8 +1541,11 @@ fn nested_map_folds<K: Ord + Clone, K2: Ord + Clone, V: Clone, A: Actor>(
         def_row: pool.def_row.as_ptr(), def_clock: pool.def_clock.as_ptr(), def_keys: pool.def_keys.as_ptr(),
     };
     let (mut o_clock, mut o_ec, mut o_ic) = (vec![0u64; g * a], vec![0u64; g * k * a], vec![0u64; g * k * a]);
-    let (mut o_iec, mut o_ivc, mut o_ivv) = (vec![0u64; g * k * k2 * a], vec![0u64; g * k * k2 * 8 * a],
-                                             vec![0u64; g * k * k2 * 8]);
+    // MVReg slots per inner key in the result: every value the group's replicas hold for one register
+    // fits (r * v), at least the library's 8, at most its 64 (past that the fold reports flags bit 6)
+    let vs = (r * v).clamp(8, MAP_NESTED_MAX_VALUES);
+    let (mut o_iec, mut o_ivc, mut o_ivv) = (vec![0u64; g * k * k2 * a], vec![0u64; g * k * k2 * vs * a],
+                                             vec![0u64; g * k * k2 * vs]);
     let (mut o_nval, mut o_idn) = (vec![0u32; g * k * k2], vec![0u32; g * k]);
     let (mut o_idc, mut o_idk) = (vec![0u64; g * k * idc * a], vec![0u64; g * k * idc * k2w]);
     let (mut flags, mut keep, mut okeys) = (vec![0u32; g], vec![0u8; nd], vec![0u64; nd * kw]);
@@ -1552,7 +1555,7 @@ fn nested_map_folds<K: Ord + Clone, K2: Ord + Clone, V: Clone, A: Actor>(
         id_clock: o_idc.as_mut_ptr(), id_keys: o_idk.as_mut_ptr(), flags: flags.as_mut_ptr(),
         def_keep: if nd > 0 { keep.as_mut_ptr() } else { ptr::null_mut() },
         def_keys: if nd > 0 { okeys.as_mut_ptr() } else { ptr::null_mut() },
-        Id: idc,
+        Id: idc, Vs: vs,
     };
     ctx.check_host(unsafe { ffi::crdt_map_nested_lub_many(ctx.host, &batch, &mut out) })?;
     if let Some(f) = flags.iter().find(|&&f| f != 0) {
@@ -1574,7 +1577,7 @@ fn nested_map_folds<K: Ord + Clone, K2: Ord + Clone, V: Clone, A: Actor>(
                 let q = b * k2 + jj;
                 let ir = &o_iec[q * a..(q + 1) * a];
                 if ir.iter().any(|&x| x != 0) {
-                    let reg = mvreg_of(&o_ivc[q * 8 * a..(q + 1) * 8 * a], &o_ivv[q * 8..(q + 1) * 8],
+                    let reg = mvreg_of(&o_ivc[q * vs * a..(q + 1) * vs * a], &o_ivv[q * vs..(q + 1) * vs],
                                        o_nval[q] as usize, &actors, &arena);
                     inner.entries.insert(ik.clone(), Entry { clock: row_clock(ir, &actors), val: reg });
                 }

@@ -64,7 +64,7 @@ def test_ctypes_struct_layout_matches_header():
     assert ctypes.sizeof(abi.MapOrswotBatch) == 17 * 8
     assert ctypes.sizeof(abi.MapOrswotOut) == 11 * 8  # (+ Vd, ABI 8)
     assert ctypes.sizeof(abi.MapOrswotStates) == 12 * 8
-    assert ctypes.sizeof(abi.MapNestedStates) == 15 * 8 and ctypes.sizeof(abi.MapNestedOut) == 14 * 8
+    assert ctypes.sizeof(abi.MapNestedStates) == 16 * 8 and ctypes.sizeof(abi.MapNestedOut) == 15 * 8
 
 
 HOST_CAPABLE = ({f"crdt_{t}_{op}" for t in ("vclock", "gcounter", "pncounter", "gset", "lwwreg", "orswot", "map")

@@ -51,14 +51,15 @@ def _longest(maps):
     return max([len(e.val.deferred) for x in maps for e in x.entries.values()] + [0])
 
 
-def _fold(ctx, maps, K, K2, A, G=1, id_cap="auto", check=True):
-    d = O.nested_map_to_dense(maps, K, K2, A, 8)
+def _fold(ctx, maps, K, K2, A, G=1, id_cap="auto", check=True, v_cap=8, V=8):
+    d = O.nested_map_to_dense(maps, K, K2, A, V)
     R = len(maps) // G
     shp = lambda x: to_dev(x.reshape((G, R) + x.shape[1:]))  # noqa: E731
     Di = int(d["id_off"][-1])
     ikw = dict(id_clock=to_dev(d["id_clock"]), id_keys=to_dev(d["id_keys"])) if Di else {}
     return cg.map.nested_lub_many(shp(d["clock"]), shp(d["ec"]), shp(d["ic"]), shp(d["iec"]), shp(d["ivc"]),
-                                  shp(d["ivv"]), to_dev(d["id_off"]), ctx=ctx, check=check, id_cap=id_cap, **ikw)
+                                  shp(d["ivv"]), to_dev(d["id_off"]), ctx=ctx, check=check, id_cap=id_cap,
+                                  v_cap=v_cap, **ikw)
 
 
 def _decode_fold(res, g):
@@ -192,3 +193,105 @@ def test_map_nested_fold_past_256_live_removes(gpu_ctx):
     exp = O.map_fold_objects(maps)
     assert len(exp.deferred) > 256
     assert canon(gpu_fold(gpu_ctx, maps)) == canon(exp)
+
+
+def _many_values(R, K2, per=1):
+    """R replicas (actor r) each writing `per` concurrent values to inner key 0 of outer key 0 (clocks
+    {r: 1 + i} per writer... one writer per value: actor r * per + i), so a fold holds R * per values."""
+    maps = []
+    for r in range(R):
+        m = O.Map(lambda: O.Map(O.MVReg))
+        inner = O.Map(O.MVReg)
+        acts = [r * per + i for i in range(per)]
+        m.clock = VClock({a: 2 for a in acts})
+        inner.clock = VClock({a: 1 for a in acts})
+        reg = O.MVReg([(VClock({a: 1}), 100 + a) for a in acts])
+        inner.entries[0] = O.MapEntry(VClock({a: 1 for a in acts}), reg)
+        inner.entries[1 + r % (K2 - 1)] = O.MapEntry(VClock({acts[0]: 1}), O.MVReg([(VClock({acts[0]: 1}), 7)]))
+        m.entries[0] = O.MapEntry(VClock({a: 2 for a in acts}), inner)
+        maps.append(m)
+    return maps
+
+
+def _max_vals(m):
+    return max(len(ie.val.vals) for e in m.entries.values() for ie in e.val.entries.values())
+
+
+def test_map_nested_fold_past_8_values(gpu_ctx):
+    """20 concurrent writers of one register (flags bit 6 before round 6): v_cap = 32 slots, the keys past
+    8 values re-folded in the deep pass; inputs with 12 values per register (V = 12 > 8) fold in the deep
+    pass alone; equal to the oracle, and the default 8 slots flag the overflow."""
+    maps = _many_values(20, 4)
+    exp = O.map_fold_objects(maps)
+    assert _max_vals(exp) == 20
+    res = _fold(gpu_ctx, maps, 1, 4, 20, v_cap=32, V=1)
+    assert int(res.flags.cpu().numpy()[0]) == 0 and res.ivc.shape[-2] == 32
+    assert canon(_decode_fold(res, 0)) == canon(exp)
+    with pytest.raises(RuntimeError, match="v_cap"):
+        _fold(gpu_ctx, maps, 1, 4, 20, V=1)
+    maps = _many_values(4, 4, per=12)  # 12 values per register in every input
+    exp = O.map_fold_objects(maps)
+    assert _max_vals(exp) == 48
+    res = _fold(gpu_ctx, maps, 1, 4, 48, v_cap=64, V=12)
+    assert int(res.flags.cpu().numpy()[0]) == 0
+    assert canon(_decode_fold(res, 0)) == canon(exp)
+
+
+def test_map_nested_apply_merge_wire_past_8_values(gpu_ctx):
+    """States with Vs = 32 value slots: Puts from 20 concurrent writers on one register (16-slot... the
+    default 8-slot states flag status bit 4), then merge_batch and the wire form, equal to the oracle."""
+    N, K2, A = 4, 4, 24
+    base = [O.map_fold_objects([m]) for m in _many_values(1, K2)] * N
+    base = [m.copy() for m in base]
+    streams, oops = [], []
+    for n in range(N):
+        ops, oo = [], []
+        for i in range(20):
+            a = 1 + i  # writer i (actor 1 + i), concurrent with every other
+            c = 10 + i
+            ops.append(("put", a, c, 0, a, 5, 0, {a: 5}, 1000 * n + i))
+            oo.append(MapUp(Dot(a, c), 0, MapUp(Dot(a, 5), 0, MVRegPut(VClock({a: 5}), 1000 * n + i))))
+        streams.append(ops)
+        oops.append(oo)
+    exps = [m.copy() for m in base]
+    for n in range(N):
+        for op in oops[n]:
+            exps[n].apply(op)
+    assert _max_vals(exps[0]) > 8
+    d = O.nested_map_to_dense(base, 1, K2, A, 8)
+    z = lambda *s_: torch.zeros(s_, dtype=torch.int64, device="cuda:0")  # noqa: E731
+    ivc = z(N, 1, K2, 32, A)
+    ivv = z(N, 1, K2, 32)
+    ivc[:, :, :, :8] = to_dev(d["ivc"])
+    ivv[:, :, :, :8] = to_dev(d["ivv"])
+    st8, slots, _ = nested_states(base, 1, K2, A, Dcap=2)
+    st = st8._replace(ivc=ivc.contiguous(), ivv=ivv.contiguous())
+    enc = cg.map.encode_nested_ops(streams, A, "cuda:0", K2=K2)
+    status = cg.map.nested_apply_batch(st, *slots, enc, ctx=gpu_ctx).cpu().numpy()
+    assert (status == 0).all(), status
+    for n in range(N):
+        assert canon(decode_states(st, n, [])) == canon(exps[n]), n
+    s8 = cg.map.nested_apply_batch(st8, *nested_states(base, 1, K2, A, Dcap=2)[1], enc, ctx=gpu_ctx).cpu().numpy()
+    assert all(x & 16 for x in s8)
+    # merge_batch of state 0..1 with 2..3 (Vs = 32 both), then the wire form of the result
+    Kw = 1
+    slot = lambda: (z(2, 2, A), z(2, 2, Kw), torch.zeros(2, dtype=torch.int32, device="cuda:0"))  # noqa: E731
+    me = wire.MapNestedFrames(*[t[:2].contiguous() for t in st], *slot())
+    other = wire.MapNestedFrames(*[t[2:].contiguous() for t in st], *slot())
+    mst = cg.map.nested_merge_batch(me, other, ctx=gpu_ctx).cpu().numpy()
+    assert (mst == 0).all(), mst
+    merged = []
+    for i in range(2):
+        e = exps[i].copy()
+        e.merge(exps[2 + i].copy())
+        merged.append(e)
+        assert canon(decode_states(me, i, [])) == canon(e), i
+    r2 = np.random.default_rng(4)
+    ad = torch.tensor(np.sort(r2.choice(2**31, size=A, replace=False)), dtype=torch.int32, device="cuda:0")
+    kd = torch.tensor([5], dtype=torch.int32, device="cuda:0")
+    idd = torch.tensor(np.sort(r2.choice(2**31, size=K2, replace=False)), dtype=torch.int32, device="cuda:0")
+    off, data = wire.map_nested_egress(me, ad, kd, idd, ctx=gpu_ctx)
+    back, wst = wire.map_nested_ingest(data, off, ad, kd, idd, 2, ctx=gpu_ctx, v_cap=32)
+    assert (wst.cpu().numpy() == 0).all()
+    for i in range(2):
+        assert canon(decode_states(back, i, [])) == canon(merged[i]), i
