@@ -238,8 +238,8 @@ def test_map_nested_fold_past_8_values(gpu_ctx):
 
 
 def test_map_nested_apply_merge_wire_past_8_values(gpu_ctx):
-    """States with Vs = 32 value slots: Puts from 20 concurrent writers on one register (16-slot... the
-    default 8-slot states flag status bit 4), then merge_batch and the wire form, equal to the oracle."""
+    """States with Vs = 32 value slots: Puts from 20 concurrent writers on one register (the default
+    8-slot states flag status bit 4), then merge_batch and the wire form, equal to the oracle."""
     N, K2, A = 4, 4, 24
     base = [O.map_fold_objects([m]) for m in _many_values(1, K2)] * N
     base = [m.copy() for m in base]
@@ -271,7 +271,8 @@ def test_map_nested_apply_merge_wire_past_8_values(gpu_ctx):
     assert (status == 0).all(), status
     for n in range(N):
         assert canon(decode_states(st, n, [])) == canon(exps[n]), n
-    s8 = cg.map.nested_apply_batch(st8, *nested_states(base, 1, K2, A, Dcap=2)[1], enc, ctx=gpu_ctx).cpu().numpy()
+    st8, slots8, _ = nested_states(base, 1, K2, A, Dcap=2)  # (fresh: st shares st8's other tensors)
+    s8 = cg.map.nested_apply_batch(st8, *slots8, enc, ctx=gpu_ctx).cpu().numpy()
     assert all(x & 16 for x in s8)
     # merge_batch of state 0..1 with 2..3 (Vs = 32 both), then the wire form of the result
     Kw = 1
