@@ -644,7 +644,8 @@ def run_causal(args, env, block):
                "types": ["Orswot<u64 member, u32 actor>"], "input_alloc": alloc}
     else:
         p = C4
-        inp = synth.map_replicas(ctx, p["R"], p["K"], p["A"], p["V"], p["seed"], kmax=p["kmax"], p_def=p["p_def"])
+        inp = synth.map_replicas(ctx, p["R"], p["K"], p["A"], p["V"], p["seed"], kmax=p["kmax"], p_def=p["p_def"],
+                                 contig=args.contig_input)
         D = inp.def_clock.shape[0]
 
         def step():

@@ -150,15 +150,24 @@ def map_clock_rows(seed: int, rows: np.ndarray, A: int, kmax: int) -> np.ndarray
 
 
 def map_replicas(ctx: Optional[Context], R: int, K: int, A: int, V: int, seed: int, kmax: int = 256,
-                 first_row: int = 0, p_def: float = 0.1) -> MapInput:
+                 first_row: int = 0, p_def: float = 0.1, contig: bool = False) -> MapInput:
     """Generate R well-formed Map<K, MVReg<u64>> replicas in HBM (crdt_synth_map), with their
-    deferred removes (host-built, then uploaded) pre-applied."""
+    deferred removes (host-built, then uploaded) pre-applied.  contig: the four replica arrays as views
+    of one physically contiguous device block (Context.device_empty) where one is free."""
     ctx = ctx or Context.default()
     dev = torch.device("cuda", ctx.device)
-    clock = torch.empty((R, A), dtype=torch.int64, device=dev)
-    ec = torch.empty((R, K, A), dtype=torch.int64, device=dev)
-    vclk = torch.empty((R, K, V, A), dtype=torch.int64, device=dev)
-    vval = torch.empty((R, K, V), dtype=torch.int64, device=dev)
+    shapes = ((R, A), (R, K, A), (R, K, V, A), (R, K, V))
+    sizes = [int(np.prod(sh)) for sh in shapes]
+    pad = lambda n: (n + 511) // 512 * 512  # noqa: E731  (4-KiB aligned views)
+    block = ctx.device_empty((sum(pad(n) for n in sizes),)) if contig else None
+    if block is not None:
+        views, at = [], 0
+        for sh, n in zip(shapes, sizes):
+            views.append(block[at:at + n].view(sh))
+            at += pad(n)
+        clock, ec, vclk, vval = views
+    else:
+        clock, ec, vclk, vval = (torch.empty(sh, dtype=torch.int64, device=dev) for sh in shapes)
     rows, rm, keys = map_deferred(seed, R, K, A, kmax, p_def, first_row)
     D = rm.shape[0]
     off = np.searchsorted(rows, np.arange(R + 1), side="left").astype(np.int64)
