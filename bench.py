@@ -661,7 +661,7 @@ def run_causal(args, env, block):
         alg_note = ("8·(K·(A + V·A + V) + A) per replica read + 8·(A + Kw + 1) per deferred remove + the "
                     "K·(A + Vout·A + Vout) + A u64 output")
         cfg = {"replicas": R, "keys": K, "actors": A, "value_slots": V, "deferred_removes": D,
-               "types": ["Map<u32, MVReg<u64>>"]}
+               "types": ["Map<u32, MVReg<u64>>"], "input_alloc": inp.alloc}
     torch.cuda.synchronize()
     res = None
     for _ in range(args.warmup):

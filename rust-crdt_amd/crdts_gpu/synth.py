@@ -100,6 +100,7 @@ class MapInput(NamedTuple):
     def_row: torch.Tensor    # (D,) int32
     def_clock: torch.Tensor  # (D, A)
     def_keys: torch.Tensor   # (D, Kw)
+    alloc: str = "torch caching allocator"  # (or "contiguous block (crdt_device_alloc)")
 
 
 def map_deferred(seed: int, R: int, K: int, A: int, kmax: int, p_def: float = 0.1, first_row: int = 0):
@@ -179,7 +180,8 @@ def map_replicas(ctx: Optional[Context], R: int, K: int, A: int, V: int, seed: i
              dptr(d_off) if D else None, dptr(dcl) if D else None, dptr(dk) if D else None)
     torch.cuda.current_stream(dev).synchronize()
     drow = torch.from_numpy(rows.astype(np.int32)).to(dev)
-    return MapInput(clock, ec, vclk, vval, [0, D], drow, dcl, dk)
+    return MapInput(clock, ec, vclk, vval, [0, D], drow, dcl, dk,
+                    "contiguous block (crdt_device_alloc)" if block is not None else "torch caching allocator")
 
 
 def orswot_op_streams(N: int, T: int, M: int, A: int, seed: int, p_rm: float = 0.2, p_future: float = 0.3,
