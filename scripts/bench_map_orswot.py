@@ -32,6 +32,7 @@ ap.add_argument("--steps", type=int, default=5)
 ap.add_argument("--sample-keys", type=int, default=4)
 ap.add_argument("--parity-replicas", type=int, default=256)
 ap.add_argument("--input", choices=("random", "causal"), default="random")
+ap.add_argument("--contig", action="store_true", help="the replicas in one contiguous device block")
 ap.add_argument("--split-probe", type=int, default=0,
                 help="also time the fold of the replicas cut into P groups (level 1 of a replica split)")
 args = ap.parse_args()
@@ -66,6 +67,20 @@ else:
     for i in range(min(M, 2)):  # member i: writer (k + i) % A's dot
         ent[:, :, i] = ec * (act[None, :] == (torch.arange(K, device=dev)[:, None] + i) % A)[None]
     del inp
+if args.contig:  # the replica arrays moved into one physically contiguous device block (crdt_device_alloc)
+    arrs = [clock, ec, oc, ent]
+    pad = lambda n: (n + 511) // 512 * 512  # noqa: E731
+    block = ctx.device_empty((sum(pad(t.numel()) for t in arrs),))
+    if block is not None:
+        views, at = [], 0
+        for t in arrs:
+            v = block[at:at + t.numel()].view(t.shape)
+            v.copy_(t)
+            views.append(v)
+            at += pad(t.numel())
+        clock, ec, oc, ent = views
+        del arrs, t
+        torch.cuda.empty_cache()
 vd_off = torch.zeros(R * K + 1, dtype=torch.int64, device=dev)
 torch.cuda.synchronize()
 
