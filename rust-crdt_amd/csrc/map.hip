@@ -2611,12 +2611,17 @@ static int map_lub_impl(crdt_ctx *ctx, const crdt_map_batch *in, const u64 *doff
     if (int rc = map_lub_wide(ctx, in, p.def_off, out)) return rc;
     he = hipSuccess;
   } else {
-  timing_begin(ctx, "map_fold");
   if (glds) {
     u64 *cm = reinterpret_cast<u64 *>(static_cast<char *>(ctx->scratch) + off_b);
     p.cmax = cm;
+    // (its own timer section: "map_fold" times the fold kernel alone, as rocprofv3 does)
+    timing_begin(ctx, "map_chunk_max");
     hipLaunchKernelGGL(map_chunk_max_kernel, dim3((unsigned)(G * p.nch)), dim3(64), 0, ctx->stream, p.clock,
                        p.c_rs, p.c_gs, (unsigned long long)R, (unsigned long long)A, p.nch, gC, cm);
+    timing_end(ctx);
+  }
+  timing_begin(ctx, "map_fold");
+  if (glds) {
     if (rs && ctx->tune.map_sh && A == 32 && V == 2 && K % 4 == 0)
       he = launch_map_sh(p, blocks, ctx->stream);
     else if (rs)
