@@ -26,6 +26,7 @@ ap.add_argument("--vals", type=int, default=4)
 ap.add_argument("--dcap", type=int, default=16)
 ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--tune", default="")
+ap.add_argument("--contig", action="store_true", help="the states in one contiguous device block")
 args = ap.parse_args()
 N, T, K, A, V, Dcap = args.states, args.ops, args.keys, args.actors, args.vals, args.dcap
 Kw = (K + 63) // 64
@@ -35,9 +36,20 @@ ctx = cg.Context(0)
 if args.tune:
     ctx.tune(args.tune)
 ops = cg.synth.map_op_streams(N, T, K, A, seed=0x5EED000A, device="cuda")
-z = lambda *s: torch.zeros(s, dtype=torch.int64, device="cuda")  # noqa: E731
-clock, ec, vclk, vval = z(N, A), z(N, K, A), z(N, K, V, A), z(N, K, V)
-dcl, dks = z(N, Dcap, A), z(N, Dcap, Kw)
+shapes = ((N, A), (N, K, A), (N, K, V, A), (N, K, V), (N, Dcap, A), (N, Dcap, Kw))
+block = None
+if args.contig:  # the states in one physically contiguous device block (crdt_device_alloc)
+    block = ctx.device_empty((sum((int(np.prod(sh)) + 511) // 512 * 512 for sh in shapes),))
+if block is not None:
+    views, at = [], 0
+    for sh in shapes:
+        n = int(np.prod(sh))
+        views.append(block[at:at + n].view(sh).zero_())
+        at += (n + 511) // 512 * 512
+    clock, ec, vclk, vval, dcl, dks = views
+else:
+    clock, ec, vclk, vval, dcl, dks = (torch.zeros(sh, dtype=torch.int64, device="cuda") for sh in shapes)
+print(f"# states: {'contiguous block' if block is not None else 'torch allocator'}", file=sys.stderr, flush=True)
 cnt = torch.zeros(N, dtype=torch.int32, device="cuda")
 
 

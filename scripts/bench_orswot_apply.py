@@ -27,6 +27,7 @@ ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--tune", default="")
 ap.add_argument("--p-rm", type=float, default=0.2)
 ap.add_argument("--p-future", type=float, default=0.3)
+ap.add_argument("--contig", action="store_true", help="the states in one contiguous device block")
 ap.add_argument("--cpu-s", type=float, default=10.0, help="CPU-baseline budget (0: none)")
 args = ap.parse_args()
 N, T, M, A, Dcap = args.states, args.ops, args.members, args.actors, args.dcap
@@ -38,10 +39,21 @@ if args.tune:
     ctx.tune(args.tune)
 t0 = time.time()
 ops = cg.synth.orswot_op_streams(N, T, M, A, seed=0x5EED0009, p_rm=args.p_rm, p_future=args.p_future, device="cuda")
-clock = torch.zeros((N, A), dtype=torch.int64, device="cuda")
-entries = torch.zeros((N, M, A), dtype=torch.int64, device="cuda")
-dcl = torch.zeros((N, Dcap, A), dtype=torch.int64, device="cuda")
-dmb = torch.zeros((N, Dcap, Mw), dtype=torch.int64, device="cuda")
+shapes = ((N, A), (N, M, A), (N, Dcap, A), (N, Dcap, Mw))
+block = None
+if args.contig:  # the states in one physically contiguous device block (crdt_device_alloc)
+    pad = lambda n: (n + 511) // 512 * 512  # noqa: E731
+    block = ctx.device_empty((sum(pad(int(np.prod(sh))) for sh in shapes),))
+if block is not None:
+    views, at = [], 0
+    for sh in shapes:
+        n = int(np.prod(sh))
+        views.append(block[at:at + n].view(sh).zero_())
+        at += (n + 511) // 512 * 512
+    clock, entries, dcl, dmb = views
+else:
+    clock, entries, dcl, dmb = (torch.zeros(sh, dtype=torch.int64, device="cuda") for sh in shapes)
+print(f"# states: {'contiguous block' if block is not None else 'torch allocator'}", file=sys.stderr, flush=True)
 cnt = torch.zeros(N, dtype=torch.int32, device="cuda")
 torch.cuda.synchronize()
 print(f"# generated {N * T} ops in {time.time() - t0:.1f} s", file=sys.stderr, flush=True)
