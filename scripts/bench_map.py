@@ -32,6 +32,8 @@ ap.add_argument("--steps", type=int, default=5)
 ap.add_argument("--sample-keys", type=int, default=8)
 ap.add_argument("--cpu-replicas", type=int, default=4096, help="replica subsample for the CPU fold")
 ap.add_argument("--no-parity", action="store_true")
+ap.add_argument("--contig", action=argparse.BooleanOptionalAction, default=True,
+                help="the replicas in one contiguous device block (as bench.py's c4 block)")
 args = ap.parse_args()
 
 R, K, A, V = args.replicas, args.keys, args.actors, args.slots
@@ -48,7 +50,7 @@ ctx = cg.Context(0)
 in_bytes = R * (K * (A * 8 + V * A * 8 + V * 8) + A * 8)
 log(f"generating {R}x{K}x{A} V={V} ({in_bytes / 2**30:.2f} GiB)")
 t0 = time.time()
-inp = synth.map_replicas(ctx, R, K, A, V, SEED, kmax=args.kmax, p_def=args.p_def)
+inp = synth.map_replicas(ctx, R, K, A, V, SEED, kmax=args.kmax, p_def=args.p_def, contig=args.contig)
 torch.cuda.synchronize()
 gen_s = time.time() - t0
 D = inp.def_clock.shape[0]
@@ -82,7 +84,7 @@ out = {"workload": f"map<u32,mvreg<u64>> lub {R}x{K}x{A} V={V}", "replicas": R, 
        "actors": A, "slots": V, "deferred": D, "wall_ms": wall * 1e3, "kernel_ms": kern * 1e3, "tune": os.environ.get("CRDT_TUNE", ""),
        "algorithmic_bytes": alg_bytes, "kernel_GBs": alg_bytes / kern / 1e9,
        "frac_of_8TBs": alg_bytes / kern / 8e12, "replica_merges_per_s": R / wall,
-       "flags": int(np.bitwise_or.reduce(flags)) if flags.size else 0}
+       "flags": int(np.bitwise_or.reduce(flags)) if flags.size else 0, "input_alloc": inp.alloc}
 print(json.dumps(out), flush=True)
 if args.no_parity:
     sys.exit(0)
