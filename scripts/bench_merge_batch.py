@@ -24,6 +24,7 @@ ap.add_argument("--orswot-pairs", type=int, default=8192)
 ap.add_argument("--map-pairs", type=int, default=8192)
 ap.add_argument("--steps", type=int, default=5)
 ap.add_argument("--sample", type=int, default=4)
+ap.add_argument("--contig", action="store_true", help="map: the states in contiguous device blocks")
 ap.add_argument("--only", default="calib,orswot,map", help="comma list of: calib, orswot, map")
 args = ap.parse_args()
 torch.cuda.set_device(0)
@@ -134,6 +135,21 @@ def mapb():
     sb = cg.map.MapStates(b.clock, b.ec, b.vclk, b.vval, *slots(offs(b), b.def_clock, b.def_keys, N, Dcap))
     keep = [x.clone() for x in sa]
     work = cg.map.MapStates(*[x.clone() for x in sa])
+    if args.contig:  # self's and other's arrays each in one physically contiguous device block
+        def blockify(st):
+            pad = lambda n: (n + 511) // 512 * 512  # noqa: E731
+            blk = ctx.device_empty((sum(pad(x.numel() * x.element_size() // 8) for x in st),))
+            if blk is None:
+                return st
+            out, at = [], 0
+            for x in st:
+                n = x.numel() * x.element_size() // 8
+                v = blk[at:at + n].view(x.dtype).view(x.shape) if x.element_size() != 8 else blk[at:at + n].view(x.shape)
+                v.copy_(x)
+                out.append(v)
+                at += pad(n)
+            return cg.map.MapStates(*out)
+        work, sb = blockify(work), blockify(sb)
 
     def reset():
         for d, s in zip(work, keep):
